@@ -1,0 +1,173 @@
+/*
+ * ngsep_gpu.h -- C ABI of the MI355X-native NGSEP SNV pileup caller (libngsep_amd.so).
+ *
+ * Drop-in boundary for the reference's SingleSampleVariantsDetector path:
+ *   Java caller (JNI shim) or the bundled CLI/Python host
+ *        |  plain pointers + sizes, caller-owned buffers, int status codes
+ *        v
+ *   host admission sweep + reference projection (C++)  ->  HBM-resident read SoA
+ *        v
+ *   HIP kernels on gfx950 (K1 candidate scan, K2 SNVQ genotyping)
+ *
+ * Every entry point names the reference interface it replaces
+ * (paths relative to src/ngsep/ of acastem15/NGSEPcore 4.3.2).
+ *
+ * Conventions: 0 = success, negative = error (see NGSEP_E_*); after an error
+ * ngsep_last_error(ctx) returns a message.  One context per device per host
+ * thread; contexts are independent (re-entrant across contexts).
+ */
+#ifndef NGSEP_GPU_H
+#define NGSEP_GPU_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NGSEP_ABI_VERSION 1
+
+#define NGSEP_OK 0
+#define NGSEP_E_INVALID (-1)      /* bad argument / state */
+#define NGSEP_E_IO (-2)           /* file cannot be read or written */
+#define NGSEP_E_FORMAT (-3)       /* malformed BAM / FASTA */
+#define NGSEP_E_DEVICE (-4)       /* HIP runtime error or no device */
+#define NGSEP_E_UNSUPPORTED (-5)  /* input outside the implemented path (indels, ploidy>=3, ...) */
+#define NGSEP_E_NOMEM (-6)
+
+typedef struct ngsep_ctx ngsep_ctx;
+
+/* Options of SingleSampleVariantsDetector (main/CommandsDescriptor.xml:565-703);
+ * defaults are the DEF_* constants (SingleSampleVariantsDetector.java:65-78,
+ * CountsHelper.java:42-48, AlignmentsPileupGenerator.java:40,53-58). */
+typedef struct ngsep_params {
+    int32_t min_mq;               /* -minMQ                 20 */
+    int32_t max_alns_per_start;   /* -maxAlnsPerStartPos    5  */
+    int32_t ignore5;              /* -ignore5               0  */
+    int32_t ignore3;              /* -ignore3               0  */
+    int32_t max_base_qs;          /* -maxBaseQS             30 */
+    int32_t min_quality;          /* -minQuality            40 */
+    int32_t ploidy;               /* -ploidy                2  */
+    int32_t process_nonunique;    /* -p                     0  */
+    int32_t process_secondary;    /* -s                     0  */
+    int32_t ignore_lowercase_ref; /* -ignoreLowerCaseRef    0  */
+    int32_t call_embedded;        /* -embeddedSNVs          0  */
+    int32_t calc_strand_bias;     /* -csb                   0  */
+    int32_t print_sample_ploidy;  /* -psp                   0  */
+    int32_t het_rate_set;         /* 1 if -h was given (haploid default switch, :591-593) */
+    double  het_rate;             /* -h                     0.001 */
+    int32_t query_first;          /* -first                 0 (used only with query_seq) */
+    int32_t query_last;           /* -last                  1e9 */
+    char    query_seq[256];       /* -querySeq              "" = all */
+    char    sample_id[256];       /* -sampleId              "Sample" */
+    /* engine knobs (no reference counterpart) */
+    int32_t prune_candidates;     /* 1: exact non-candidate pruning (DESIGN.md "K1"), 0: genotype every position */
+    int32_t dump_all_positions;   /* 1: ngsep_fetch_sites returns a record for every position with DP>0 */
+    int32_t window_positions;     /* max positions per device window (0 = whole contig) */
+} ngsep_params;
+
+/* Alignments as AlignmentsPileupGenerator.processAlignment receives them
+ * (AlignmentsPileupGenerator.java:377-403): already filtered by the reader,
+ * coordinate-sorted.  Mirrors the ReadAlignment fields the JNI side copies out
+ * (alignments/ReadAlignment.java:87-122). */
+typedef struct ngsep_read_batch {
+    int64_t n_reads;
+    const int32_t* seq_id;      /* index of the reference sequence (order of ngsep_set_reference) */
+    const int32_t* first;       /* 1-based first aligned reference position (getFirst) */
+    const int32_t* flags;       /* SAM flags (0x10 strand, 0x100 secondary are used) */
+    const int32_t* read_group;  /* caller's read-group index, -1 = DEF_READ_GROUP "" */
+    const int64_t* cigar_off;   /* offset of the read's CIGAR items in cigar[] */
+    const int32_t* cigar_n;     /* number of CIGAR items */
+    const int32_t* cigar;       /* NGSEP encoding len*8+op, op: H0 D1 I2 M3 P4 N5 S6 X7 (ReadAlignment.java:60-67,1180-1198) */
+    const int64_t* seq_off;     /* offset of the read's characters in bases[] and quals[] */
+    const int32_t* seq_len;     /* read length; 0 = no read characters (getReadCharacters()==null) */
+    const char*    bases;       /* read characters, upper case */
+    const char*    quals;       /* phred+33 quality characters (NULL = no qualities for any read) */
+    const uint8_t* has_quals;   /* per read: 0 = quality string absent ('*'), may be NULL = all present */
+} ngsep_read_batch;
+
+/* One called variant = one VCF data line of SingleSampleVariantsDetector
+ * (CalledSNV / triallelic CalledGenomicVariantImpl, VariantDiscoverySNVQAlgorithm.java:100-222). */
+typedef struct ngsep_site_out {
+    int32_t seq_id;
+    int32_t pos;             /* 1-based */
+    int8_t  ref;             /* upper-case reference base 'A','C','G','T' */
+    int8_t  n_alleles;       /* 2 = biallelic CalledSNV, 3 = MULTISNV (called 1/2) */
+    int8_t  alt;             /* DNA index (0=A,1=C,2=G,3=T) of ALT (first ALT if triallelic) */
+    int8_t  third;           /* DNA index of the second ALT, or -1 */
+    int8_t  genotype;        /* 0 hom-ref (dump mode only), 1 het, 2 hom-alt, 3 het alt/third, -1 none */
+    int8_t  strand_bias;     /* FS phred score (-csb) or -1 */
+    int16_t gq;              /* genotype quality, PhredScoreHelper.calculatePhredScore(1-maxP) */
+    int16_t qual;            /* variant QS, phred(P[ref][ref]) */
+    int16_t is_call;         /* 1 = passes the listener filters (always 1 unless dump_all_positions) */
+    int32_t dp;              /* CountsHelper.getTotalCount() */
+    int32_t counts[4];       /* A,C,G,T base counts (BSDP) */
+    int32_t strand_counts[4][2]; /* [allele][0=negative,1=positive] (CountsHelper.countsStrand) */
+    double  logc[10];        /* log10 P(data|genotype) upper triangle: 00 01 02 03 11 12 13 22 23 33 */
+} ngsep_site_out;
+
+typedef struct ngsep_stats {
+    int64_t alignments_in;          /* alignments received */
+    int64_t alignments_admitted;    /* after the maxAlnsPerStartPos cap */
+    int64_t positions_genotyped;    /* positions with >=1 overlapping admitted alignment */
+    int64_t candidates;             /* positions sent to K2 */
+    int64_t sites_called;
+    int64_t read_bases;             /* projected read bytes resident in HBM */
+    int64_t slot_bytes;             /* bytes of the slot array (incl. padding) */
+    double  kernel_ms;              /* device time of the last run (all kernels) */
+    double  scan_ms;                /* device time of K1 (candidate scan) */
+    double  genotype_ms;            /* device time of K2 */
+} ngsep_stats;
+
+/* ---- context ---- */
+int  ngsep_abi_version(void);
+void ngsep_params_default(ngsep_params* p);
+/* device: HIP ordinal.  Replaces `new SingleSampleVariantsDetector()` + option setters */
+int  ngsep_open(int device, const ngsep_params* params, ngsep_ctx** out);
+int  ngsep_close(ngsep_ctx* ctx);
+const char* ngsep_last_error(ngsep_ctx* ctx);
+int  ngsep_get_stats(ngsep_ctx* ctx, ngsep_stats* out);
+int  ngsep_device_count(void);
+
+/* ---- reference: ReferenceGenome(filename, keepLowerCase=true) (genome/ReferenceGenome.java:40-62) ---- */
+int ngsep_set_reference(ngsep_ctx* ctx, const char* seq_name, const char* bases, int64_t len);
+int ngsep_load_fasta(ngsep_ctx* ctx, const char* path);
+int ngsep_n_sequences(ngsep_ctx* ctx);
+const char* ngsep_sequence_name(ngsep_ctx* ctx, int seq_id);
+
+/* ---- path A: alignments pushed by the host (AlignmentsPileupGenerator.processAlignments, :334-361) ---- */
+int ngsep_process_alignments(ngsep_ctx* ctx, const ngsep_read_batch* batch);
+/* AlignmentsPileupGenerator.notifyEndOfAlignments (:447-452): flushes the last sequence */
+int ngsep_notify_end(ngsep_ctx* ctx);
+/* Calls accumulated so far (SingleSampleVariantPileupListener.getCalledVariants, :139-141), in
+ * (sequence, position) order.  n_out receives the number available; at most cap are copied. */
+int ngsep_fetch_sites(ngsep_ctx* ctx, ngsep_site_out* out, int64_t cap, int64_t* n_out);
+int ngsep_clear_sites(ngsep_ctx* ctx);
+
+/* ---- VCF text, VCFFileWriter.printHeader / printVCFRecord (vcf/VCFFileWriter.java:44-68,309-311) ---- */
+int ngsep_write_vcf_header(ngsep_ctx* ctx, const char* path);
+int ngsep_append_vcf_records(ngsep_ctx* ctx, const char* path);   /* all fetched sites, then clears them */
+int64_t ngsep_format_site(ngsep_ctx* ctx, const ngsep_site_out* site, char* buf, int64_t cap);
+
+/* ---- path B: the whole SingleSampleVariantsDetector.findSNVS on a BAM file (:896-931) ---- */
+int ngsep_call_bam(ngsep_ctx* ctx, const char* bam_path, const char* out_vcf_path);
+
+/* ---- BAM reading (ReadAlignmentFileReader semantics, alignments/io/ReadAlignmentFileReader.java:219-354) ---- */
+typedef struct ngsep_bam ngsep_bam;
+int  ngsep_bam_open(ngsep_ctx* ctx, const char* path, ngsep_bam** out);
+/* reads up to max_reads filtered alignments; the batch arrays stay valid until the next call */
+int  ngsep_bam_next_batch(ngsep_bam* bam, int64_t max_reads, ngsep_read_batch* batch);
+int  ngsep_bam_close(ngsep_bam* bam);
+
+/* ---- measurement entry points (bench.py): split staging (pack + H2D) from the device run ---- */
+int ngsep_stage_alignments(ngsep_ctx* ctx, const ngsep_read_batch* batch);  /* pack + upload, keep resident */
+int ngsep_stage_finish(ngsep_ctx* ctx);
+/* one pass of K1+K2 (+ D2H of the calls) over every resident window; returns elapsed ms (host wall, synchronized) */
+int ngsep_run_staged(ngsep_ctx* ctx, double* elapsed_ms);
+int ngsep_release_staged(ngsep_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

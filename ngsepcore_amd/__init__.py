@@ -1,0 +1,10 @@
+"""ngsepcore_amd -- MI355X-native drop-in for NGSEP's SNV pileup-calling path.
+
+The compute path is libngsep_amd.so (HIP kernels for gfx950 behind the C ABI in
+include/ngsep_gpu.h); this package is the host-side mirror of the reference interface.
+"""
+from ._lib import LIB_PATH, NgsepError, load  # noqa: F401
+from .discovery import CalledSite, GpuPileupSession, SingleSampleVariantsDetector, default_params  # noqa: F401
+
+__all__ = ["GpuPileupSession", "SingleSampleVariantsDetector", "CalledSite", "NgsepError", "default_params",
+           "load", "LIB_PATH"]

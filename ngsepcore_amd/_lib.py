@@ -1,0 +1,160 @@
+"""ctypes binding of libngsep_amd.so (include/ngsep_gpu.h).
+
+The library is the product: HIP kernels for gfx950 behind a C ABI.  Loading fails loudly
+when the shared object is missing -- there is no CPU fallback in this package.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libngsep_amd.so")
+
+NGSEP_OK = 0
+NGSEP_E_INVALID = -1
+NGSEP_E_IO = -2
+NGSEP_E_FORMAT = -3
+NGSEP_E_DEVICE = -4
+NGSEP_E_UNSUPPORTED = -5
+
+
+class NgsepParams(ctypes.Structure):
+    _fields_ = [
+        ("min_mq", ctypes.c_int32),
+        ("max_alns_per_start", ctypes.c_int32),
+        ("ignore5", ctypes.c_int32),
+        ("ignore3", ctypes.c_int32),
+        ("max_base_qs", ctypes.c_int32),
+        ("min_quality", ctypes.c_int32),
+        ("ploidy", ctypes.c_int32),
+        ("process_nonunique", ctypes.c_int32),
+        ("process_secondary", ctypes.c_int32),
+        ("ignore_lowercase_ref", ctypes.c_int32),
+        ("call_embedded", ctypes.c_int32),
+        ("calc_strand_bias", ctypes.c_int32),
+        ("print_sample_ploidy", ctypes.c_int32),
+        ("het_rate_set", ctypes.c_int32),
+        ("het_rate", ctypes.c_double),
+        ("query_first", ctypes.c_int32),
+        ("query_last", ctypes.c_int32),
+        ("query_seq", ctypes.c_char * 256),
+        ("sample_id", ctypes.c_char * 256),
+        ("prune_candidates", ctypes.c_int32),
+        ("dump_all_positions", ctypes.c_int32),
+        ("window_positions", ctypes.c_int32),
+    ]
+
+
+P = ctypes.POINTER
+
+
+class NgsepReadBatch(ctypes.Structure):
+    _fields_ = [
+        ("n_reads", ctypes.c_int64),
+        ("seq_id", P(ctypes.c_int32)),
+        ("first", P(ctypes.c_int32)),
+        ("flags", P(ctypes.c_int32)),
+        ("read_group", P(ctypes.c_int32)),
+        ("cigar_off", P(ctypes.c_int64)),
+        ("cigar_n", P(ctypes.c_int32)),
+        ("cigar", P(ctypes.c_int32)),
+        ("seq_off", P(ctypes.c_int64)),
+        ("seq_len", P(ctypes.c_int32)),
+        ("bases", ctypes.c_char_p),
+        ("quals", ctypes.c_char_p),
+        ("has_quals", P(ctypes.c_uint8)),
+    ]
+
+
+class NgsepSiteOut(ctypes.Structure):
+    _fields_ = [
+        ("seq_id", ctypes.c_int32),
+        ("pos", ctypes.c_int32),
+        ("ref", ctypes.c_int8),
+        ("n_alleles", ctypes.c_int8),
+        ("alt", ctypes.c_int8),
+        ("third", ctypes.c_int8),
+        ("genotype", ctypes.c_int8),
+        ("strand_bias", ctypes.c_int8),
+        ("gq", ctypes.c_int16),
+        ("qual", ctypes.c_int16),
+        ("is_call", ctypes.c_int16),
+        ("dp", ctypes.c_int32),
+        ("counts", ctypes.c_int32 * 4),
+        ("strand_counts", (ctypes.c_int32 * 2) * 4),
+        ("logc", ctypes.c_double * 10),
+    ]
+
+
+class NgsepStats(ctypes.Structure):
+    _fields_ = [
+        ("alignments_in", ctypes.c_int64),
+        ("alignments_admitted", ctypes.c_int64),
+        ("positions_genotyped", ctypes.c_int64),
+        ("candidates", ctypes.c_int64),
+        ("sites_called", ctypes.c_int64),
+        ("read_bases", ctypes.c_int64),
+        ("slot_bytes", ctypes.c_int64),
+        ("kernel_ms", ctypes.c_double),
+        ("scan_ms", ctypes.c_double),
+        ("genotype_ms", ctypes.c_double),
+    ]
+
+
+# exported symbols and their signatures (kept in sync with include/ngsep_gpu.h)
+_CTX = ctypes.c_void_p
+SIGNATURES = {
+    "ngsep_abi_version": (ctypes.c_int, []),
+    "ngsep_params_default": (None, [P(NgsepParams)]),
+    "ngsep_open": (ctypes.c_int, [ctypes.c_int, P(NgsepParams), P(_CTX)]),
+    "ngsep_close": (ctypes.c_int, [_CTX]),
+    "ngsep_last_error": (ctypes.c_char_p, [_CTX]),
+    "ngsep_get_stats": (ctypes.c_int, [_CTX, P(NgsepStats)]),
+    "ngsep_device_count": (ctypes.c_int, []),
+    "ngsep_set_reference": (ctypes.c_int, [_CTX, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64]),
+    "ngsep_load_fasta": (ctypes.c_int, [_CTX, ctypes.c_char_p]),
+    "ngsep_n_sequences": (ctypes.c_int, [_CTX]),
+    "ngsep_sequence_name": (ctypes.c_char_p, [_CTX, ctypes.c_int]),
+    "ngsep_process_alignments": (ctypes.c_int, [_CTX, P(NgsepReadBatch)]),
+    "ngsep_notify_end": (ctypes.c_int, [_CTX]),
+    "ngsep_fetch_sites": (ctypes.c_int, [_CTX, P(NgsepSiteOut), ctypes.c_int64, P(ctypes.c_int64)]),
+    "ngsep_clear_sites": (ctypes.c_int, [_CTX]),
+    "ngsep_write_vcf_header": (ctypes.c_int, [_CTX, ctypes.c_char_p]),
+    "ngsep_append_vcf_records": (ctypes.c_int, [_CTX, ctypes.c_char_p]),
+    "ngsep_format_site": (ctypes.c_int64, [_CTX, P(NgsepSiteOut), ctypes.c_char_p, ctypes.c_int64]),
+    "ngsep_call_bam": (ctypes.c_int, [_CTX, ctypes.c_char_p, ctypes.c_char_p]),
+    "ngsep_bam_open": (ctypes.c_int, [_CTX, ctypes.c_char_p, P(ctypes.c_void_p)]),
+    "ngsep_bam_next_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, P(NgsepReadBatch)]),
+    "ngsep_bam_close": (ctypes.c_int, [ctypes.c_void_p]),
+    "ngsep_stage_alignments": (ctypes.c_int, [_CTX, P(NgsepReadBatch)]),
+    "ngsep_stage_finish": (ctypes.c_int, [_CTX]),
+    "ngsep_run_staged": (ctypes.c_int, [_CTX, P(ctypes.c_double)]),
+    "ngsep_release_staged": (ctypes.c_int, [_CTX]),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Loads libngsep_amd.so; raises if it was not built (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the MI355X HIP extension is required; there is no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class NgsepError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"ngsep error {code}: {msg}")
+        self.code = code

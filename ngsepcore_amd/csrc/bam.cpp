@@ -1,0 +1,329 @@
+// bam.cpp -- BGZF/BAM decoding with ReadAlignmentFileReader's record semantics
+// (alignments/io/ReadAlignmentFileReader.java:171-354).  htsjdk (lib/htsjdk-2.22.jar) plays this
+// role in the reference; this reader reproduces the fields NGSEP takes from it:
+//   getAlignmentStart/End, getFlags, getMappingQuality, CIGAR, getReadString
+//   ("=ACMGRSVTWYHKDBN" decoding), getBaseQualityString (0xFF -> "*"), RG (header lookup), NH.
+// Reader filters: consecutive duplicates (isSameAlignment :292-306), FLAG_MULTIPLE_ALN (:284-291),
+// unmapped/secondary/multiple filter flags (AlignmentsPileupGenerator.java:363-375).
+#include <zlib.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "engine.hpp"
+
+struct ngsep_bam {
+    ngsep_ctx* ctx = nullptr;
+    std::FILE* f = nullptr;
+    std::vector<uint8_t> comp;
+    std::string buf;        // inflated bytes not yet consumed
+    size_t pos = 0;
+    bool eof = false;
+    std::vector<int32_t> ref_to_seq;   // BAM refID -> ctx sequence id
+    std::vector<std::string> rg_ids;   // header read groups
+    std::unordered_map<std::string, int32_t> rg_index;
+    int filter_flags = 0;
+    int min_mq = 20;
+    // previous raw record for isSameAlignment
+    bool have_last = false;
+    int32_t last_pos = 0;
+    int last_paired = 0, last_fop = 0;
+    std::string last_name;
+    // batch storage
+    std::vector<int32_t> b_seq, b_first, b_flags, b_rg, b_cig_n, b_cigar, b_seqlen;
+    std::vector<int64_t> b_cig_off, b_seq_off;
+    std::vector<uint8_t> b_hasq;
+    std::string b_bases, b_quals;
+};
+
+namespace {
+
+// inflates the next BGZF block into bam->buf; returns false at end of file
+bool next_block(ngsep_bam* b, std::string& err) {
+    uint8_t h[18];
+    size_t n = std::fread(h, 1, 18, b->f);
+    if (n == 0) return false;
+    if (n < 18 || h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) { err = "not a BGZF file"; return false; }
+    uint16_t xlen = (uint16_t)(h[10] | (h[11] << 8));
+    // standard BGZF: XLEN=6 with the BC subfield
+    std::vector<uint8_t> extra(xlen);
+    std::memcpy(extra.data(), h + 12, std::min<size_t>(6, xlen));
+    if (xlen > 6 && std::fread(extra.data() + 6, 1, xlen - 6, b->f) != (size_t)(xlen - 6)) { err = "truncated BGZF header"; return false; }
+    int bsize = -1;
+    for (size_t i = 0; i + 4 <= extra.size();) {
+        uint16_t sl = (uint16_t)(extra[i + 2] | (extra[i + 3] << 8));
+        if (extra[i] == 'B' && extra[i + 1] == 'C' && sl == 2) bsize = extra[i + 4] | (extra[i + 5] << 8);
+        i += 4 + sl;
+    }
+    if (bsize < 0) { err = "BGZF block without BC field"; return false; }
+    size_t rest = (size_t)bsize + 1 - 12 - xlen;
+    b->comp.resize(rest);
+    if (std::fread(b->comp.data(), 1, rest, b->f) != rest) { err = "truncated BGZF block"; return false; }
+    uint32_t isize = (uint32_t)(b->comp[rest - 4] | (b->comp[rest - 3] << 8) | (b->comp[rest - 2] << 16) | ((uint32_t)b->comp[rest - 1] << 24));
+    if (isize == 0) return true;
+    size_t o = b->buf.size();
+    b->buf.resize(o + isize);
+    z_stream z{};
+    inflateInit2(&z, -15);
+    z.next_in = b->comp.data();
+    z.avail_in = (uInt)(rest - 8);
+    z.next_out = (Bytef*)&b->buf[o];
+    z.avail_out = isize;
+    int rc = inflate(&z, Z_FINISH);
+    inflateEnd(&z);
+    if (rc != Z_STREAM_END) { err = "BGZF inflate failed"; return false; }
+    return true;
+}
+
+// ensures at least n unconsumed bytes; false at EOF
+bool need(ngsep_bam* b, size_t n, std::string& err) {
+    while (b->buf.size() - b->pos < n) {
+        if (b->pos > (1u << 20)) { b->buf.erase(0, b->pos); b->pos = 0; }
+        if (!next_block(b, err)) return false;
+    }
+    return true;
+}
+
+template <class T> T rd(const char* p) { T v; std::memcpy(&v, p, sizeof(T)); return v; }
+
+}  // namespace
+
+using namespace ngsep;
+
+extern "C" int ngsep_bam_open(ngsep_ctx* c, const char* path, ngsep_bam** out) {
+    if (!c || !path || !out) return NGSEP_E_INVALID;
+    ngsep_bam* b = new ngsep_bam();
+    b->ctx = c;
+    b->f = std::fopen(path, "rb");
+    if (!b->f) { delete b; return set_error(c, NGSEP_E_IO, std::string("cannot open ") + path); }
+    std::string err;
+    if (!need(b, 8, err) || std::memcmp(&b->buf[0], "BAM\1", 4) != 0) {
+        std::fclose(b->f); delete b;
+        return set_error(c, NGSEP_E_FORMAT, err.empty() ? "not a BAM file" : err);
+    }
+    int32_t l_text = rd<int32_t>(&b->buf[4]);
+    if (!need(b, 8 + (size_t)l_text + 4, err)) { std::fclose(b->f); delete b; return set_error(c, NGSEP_E_FORMAT, "truncated BAM header"); }
+    std::string text = b->buf.substr(8, (size_t)l_text);
+    b->pos = 8 + (size_t)l_text;
+    int32_t n_ref = rd<int32_t>(&b->buf[b->pos]);
+    b->pos += 4;
+    std::unordered_map<std::string, int32_t> seq_index;
+    for (size_t i = 0; i < c->seq_names.size(); i++) seq_index[c->seq_names[i]] = (int32_t)i;
+    for (int32_t i = 0; i < n_ref; i++) {
+        if (!need(b, 4, err)) break;
+        int32_t ln = rd<int32_t>(&b->buf[b->pos]);
+        if (!need(b, 4 + (size_t)ln + 4, err)) break;
+        std::string name(&b->buf[b->pos + 4], (size_t)(ln > 0 ? ln - 1 : 0));
+        int32_t lref = rd<int32_t>(&b->buf[b->pos + 4 + ln]);
+        b->pos += 8 + (size_t)ln;
+        auto it = seq_index.find(name);
+        // ReadAlignmentFileReader.loadHeader validation (:198-214)
+        if (it == seq_index.end()) {
+            std::fclose(b->f); delete b;
+            return set_error(c, NGSEP_E_FORMAT, "Inconsistent file header. Sequence " + name + " not present in the reference sequences");
+        }
+        if ((int64_t)c->seq_bases[it->second].size() != lref) {
+            std::fclose(b->f); delete b;
+            return set_error(c, NGSEP_E_FORMAT, "Inconsistent length in file header. Sequence " + name);
+        }
+        b->ref_to_seq.push_back(it->second);
+    }
+    // @RG lines
+    size_t p = 0;
+    while (p < text.size()) {
+        size_t e = text.find('\n', p);
+        if (e == std::string::npos) e = text.size();
+        std::string line = text.substr(p, e - p);
+        if (line.compare(0, 3, "@RG") == 0) {
+            size_t id = line.find("\tID:");
+            if (id != std::string::npos) {
+                size_t ie = line.find('\t', id + 4);
+                std::string v = line.substr(id + 4, ie == std::string::npos ? std::string::npos : ie - id - 4);
+                if (!b->rg_index.count(v)) { b->rg_index[v] = (int32_t)b->rg_ids.size(); b->rg_ids.push_back(v); }
+            }
+        }
+        p = e + 1;
+    }
+    // AlignmentsPileupGenerator.createReader (:363-375)
+    b->filter_flags = 0x4;
+    if (!c->params.process_secondary) {
+        b->filter_flags |= 0x100;
+        if (!c->params.process_nonunique) b->filter_flags |= 0x1000;
+    }
+    b->min_mq = c->params.min_mq;
+    *out = b;
+    return NGSEP_OK;
+}
+
+extern "C" int ngsep_bam_next_batch(ngsep_bam* b, int64_t max_reads, ngsep_read_batch* out) {
+    if (!b || !out) return NGSEP_E_INVALID;
+    static const int kOp[9] = {3, 2, 1, 5, 6, 0, 4, 3, 7};   // BAM M I D N S H P = X -> NGSEP H0 D1 I2 M3 P4 N5 S6 X7
+    static const char kNt[] = "=ACMGRSVTWYHKDBN";
+    b->b_seq.clear(); b->b_first.clear(); b->b_flags.clear(); b->b_rg.clear(); b->b_cig_n.clear();
+    b->b_cigar.clear(); b->b_seqlen.clear(); b->b_cig_off.clear(); b->b_seq_off.clear(); b->b_hasq.clear();
+    b->b_bases.clear(); b->b_quals.clear();
+    std::string err;
+    int64_t n = 0;
+    while (n < max_reads) {
+        if (!need(b, 4, err)) break;
+        int32_t bs = rd<int32_t>(&b->buf[b->pos]);
+        if (bs < 32) return set_error(b->ctx, NGSEP_E_FORMAT, "malformed BAM record");
+        if (!need(b, 4 + (size_t)bs, err)) return set_error(b->ctx, NGSEP_E_FORMAT, "truncated BAM record");
+        const char* r = &b->buf[b->pos + 4];
+        b->pos += 4 + (size_t)bs;
+        int32_t refid = rd<int32_t>(r);
+        int32_t pos0 = rd<int32_t>(r + 4);
+        uint8_t l_name = (uint8_t)r[8];
+        uint8_t mapq = (uint8_t)r[9];
+        uint16_t n_cig = rd<uint16_t>(r + 12);
+        uint16_t flag = rd<uint16_t>(r + 14);
+        int32_t l_seq = rd<int32_t>(r + 16);
+        const char* name = r + 32;
+        const char* cig = name + l_name;
+        const char* seq = cig + 4 * n_cig;
+        const char* qual = seq + (l_seq + 1) / 2;
+        const char* aux = qual + l_seq;
+        const char* end = r + bs;
+        int32_t start = pos0 + 1;
+        // isSameAlignment (ReadAlignmentFileReader.java:292-306)
+        int paired = (flag & 1) != 0, fop = (flag & 0x40) != 0;
+        std::string nm(name, l_name ? l_name - 1 : 0);
+        if (b->have_last && b->last_pos == start && b->last_paired == paired && (!paired || b->last_fop == fop) && b->last_name == nm) continue;
+        b->have_last = true; b->last_pos = start; b->last_paired = paired; b->last_fop = fop; b->last_name = nm;
+        if (flag & 0x4) continue;               // FLAG_READ_UNMAPPED (filtered)
+        if (refid < 0 || refid >= (int32_t)b->ref_to_seq.size()) continue;
+        // tags: NH and RG
+        int nh = 0, nh_present = 0, rg = -1;
+        for (const char* t = aux; t + 3 <= end;) {
+            char t0 = t[0], t1 = t[1], ty = t[2];
+            const char* v = t + 3;
+            size_t sz = 0;
+            long long iv = 0;
+            bool isint = true;
+            switch (ty) {
+                case 'A': case 'c': case 'C': sz = 1; iv = ty == 'c' ? (int8_t)v[0] : (uint8_t)v[0]; break;
+                case 's': sz = 2; iv = rd<int16_t>(v); break;
+                case 'S': sz = 2; iv = rd<uint16_t>(v); break;
+                case 'i': sz = 4; iv = rd<int32_t>(v); break;
+                case 'I': sz = 4; iv = rd<uint32_t>(v); break;
+                case 'f': sz = 4; isint = false; break;
+                case 'Z': case 'H': { isint = false; const char* z = v; while (z < end && *z) z++; sz = (size_t)(z - v) + 1; break; }
+                case 'B': {
+                    isint = false;
+                    char sub = v[0];
+                    int32_t cnt = rd<int32_t>(v + 1);
+                    int es = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
+                    sz = 5 + (size_t)cnt * es;
+                    break;
+                }
+                default: t = end; continue;
+            }
+            if (t0 == 'N' && t1 == 'H' && isint && ty != 'A') { nh = (int)iv; nh_present = 1; }
+            if (t0 == 'R' && t1 == 'G' && ty == 'Z') {
+                auto it = b->rg_index.find(std::string(v));
+                rg = it == b->rg_index.end() ? -1 : it->second;   // getReadGroup() is null if not in header
+            }
+            t = v + sz;
+        }
+        int flags = flag;
+        // isMultiple (:284-291)
+        bool multiple;
+        if (flag & 0x100) multiple = true;
+        else if (nh_present && nh > 1) multiple = true;
+        else if (nh_present && nh == 1) multiple = false;
+        else multiple = mapq < b->min_mq;
+        if (multiple) flags += 0x1000;
+        if (n_cig == 0) continue;               // mapped read without CIGAR: setCigarString throws
+        // CIGAR -> NGSEP codes with collapseEqualEvents
+        int64_t coff = (int64_t)b->b_cigar.size();
+        int read_len = 0;
+        bool bad = false;
+        int nc = 0;
+        for (int i = 0; i < n_cig; i++) {
+            uint32_t v = rd<uint32_t>(cig + 4 * i);
+            uint32_t op = v & 15, len = v >> 4;
+            if (op > 8) { bad = true; break; }
+            int nop = kOp[op];
+            if (nc > 0 && (b->b_cigar.back() & 7) == nop) b->b_cigar.back() += (int32_t)len * 8;
+            else { b->b_cigar.push_back((int32_t)len * 8 + nop); nc++; }
+            if (nop & 2) read_len += (int)len;
+        }
+        if (bad) { b->b_cigar.resize((size_t)coff); continue; }
+        if (l_seq > 0 && l_seq != read_len) { b->b_cigar.resize((size_t)coff); continue; }   // setReadCharacters throws
+        if ((flags & b->filter_flags) != 0) { b->b_cigar.resize((size_t)coff); continue; }
+        b->b_seq.push_back(b->ref_to_seq[refid]);
+        b->b_first.push_back(start);
+        b->b_flags.push_back(flags);
+        b->b_rg.push_back(rg);
+        b->b_cig_off.push_back(coff);
+        b->b_cig_n.push_back(nc);
+        b->b_seq_off.push_back((int64_t)b->b_bases.size());
+        b->b_seqlen.push_back(l_seq);
+        size_t so = b->b_bases.size();
+        b->b_bases.resize(so + (size_t)l_seq);
+        b->b_quals.resize(so + (size_t)l_seq);
+        for (int32_t i = 0; i < l_seq; i++) {
+            uint8_t byte = (uint8_t)seq[i >> 1];
+            b->b_bases[so + i] = kNt[(i & 1) ? (byte & 15) : (byte >> 4)];
+        }
+        bool hasq = l_seq > 0 && (uint8_t)qual[0] != 0xFF;
+        for (int32_t i = 0; i < l_seq; i++) b->b_quals[so + i] = hasq ? (char)((uint8_t)qual[i] + 33) : '!';
+        b->b_hasq.push_back(hasq ? 1 : 0);
+        n++;
+    }
+    if (!err.empty()) return set_error(b->ctx, NGSEP_E_FORMAT, err);
+    out->n_reads = n;
+    out->seq_id = b->b_seq.data();
+    out->first = b->b_first.data();
+    out->flags = b->b_flags.data();
+    out->read_group = b->b_rg.data();
+    out->cigar_off = b->b_cig_off.data();
+    out->cigar_n = b->b_cig_n.data();
+    out->cigar = b->b_cigar.data();
+    out->seq_off = b->b_seq_off.data();
+    out->seq_len = b->b_seqlen.data();
+    out->bases = b->b_bases.data();
+    out->quals = b->b_quals.data();
+    out->has_quals = b->b_hasq.data();
+    return NGSEP_OK;
+}
+
+extern "C" int ngsep_bam_close(ngsep_bam* b) {
+    if (!b) return NGSEP_E_INVALID;
+    if (b->f) std::fclose(b->f);
+    delete b;
+    return NGSEP_OK;
+}
+
+namespace ngsep {
+// SingleSampleVariantsDetector.findSNVS (:896-931) + onSequenceEnd/saveSequenceVariants (:933-968, :1026-1032)
+int call_bam(ngsep_ctx* c, const char* bam_path, const char* out_vcf) {
+    ngsep_bam* b = nullptr;
+    int rc = ngsep_bam_open(c, bam_path, &b);
+    if (rc != NGSEP_OK) return rc;
+    rc = ngsep_write_vcf_header(c, out_vcf);
+    if (rc != NGSEP_OK) { ngsep_bam_close(b); return rc; }
+    ngsep_read_batch batch;
+    while (true) {
+        rc = ngsep_bam_next_batch(b, 1 << 20, &batch);
+        if (rc != NGSEP_OK) break;
+        if (batch.n_reads == 0) break;
+        rc = ngsep_process_alignments(c, &batch);
+        if (rc != NGSEP_OK) break;
+        if (!c->sites.empty()) { rc = ngsep_append_vcf_records(c, out_vcf); if (rc != NGSEP_OK) break; }
+    }
+    ngsep_bam_close(b);
+    if (rc != NGSEP_OK) return rc;
+    rc = ngsep_notify_end(c);
+    if (rc != NGSEP_OK) return rc;
+    return ngsep_append_vcf_records(c, out_vcf);
+}
+}  // namespace ngsep
+
+extern "C" int ngsep_call_bam(ngsep_ctx* c, const char* bam_path, const char* out_vcf_path) {
+    if (!c || !bam_path || !out_vcf_path) return NGSEP_E_INVALID;
+    return ngsep::call_bam(c, bam_path, out_vcf_path);
+}

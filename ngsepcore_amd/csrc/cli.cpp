@@ -1,0 +1,72 @@
+// cli.cpp -- `ngsep-amd SingleSampleVariantsDetector ...`: same option names and defaults as
+// `java -jar NGSEPcore.jar SingleSampleVariantsDetector` (main/CommandsDescriptor.xml:565-703,
+// SingleSampleVariantsDetector.main/run :583-656).  Options of the SV/CNV analyses
+// (-runRD, -runRP, -runRep, -runLongReadSVs, ...) are outside this build and rejected.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "../../include/ngsep_gpu.h"
+
+static int usage(const char* argv0) {
+    std::fprintf(stderr,
+                 "usage: %s SingleSampleVariantsDetector -i <alignments.bam> -r <reference.fa> -o <output prefix> [options]\n"
+                 "options: -sampleId S -ploidy N -psp -minMQ N -maxAlnsPerStartPos N -p -s -ignore5 N -ignore3 N\n"
+                 "         -h RATE -maxBaseQS N -minQuality N -ignoreLowerCaseRef -embeddedSNVs -csb\n"
+                 "         -querySeq SEQ -first N -last N -device N\n", argv0);
+    return 2;
+}
+
+int main(int argc, char** argv) {
+    ngsep_params p;
+    ngsep_params_default(&p);
+    const char *in = nullptr, *ref = nullptr, *outp = nullptr;
+    int device = 0;
+    int i = 1;
+    if (i < argc && std::strcmp(argv[i], "SingleSampleVariantsDetector") == 0) i++;
+    else if (i < argc && argv[i][0] != '-') { std::fprintf(stderr, "unsupported command %s\n", argv[i]); return usage(argv[0]); }
+    for (; i < argc; i++) {
+        const char* a = argv[i];
+        const char* v = i + 1 < argc ? argv[i + 1] : nullptr;
+        auto takes = [&](const char* name) { if (std::strcmp(a, name) == 0 && v) { i++; return true; } return false; };
+        if (takes("-i")) in = v;
+        else if (takes("-r")) ref = v;
+        else if (takes("-o")) outp = v;
+        else if (takes("-sampleId")) std::snprintf(p.sample_id, sizeof p.sample_id, "%s", v);
+        else if (takes("-ploidy")) p.ploidy = std::atoi(v);
+        else if (takes("-minMQ")) p.min_mq = std::atoi(v);
+        else if (takes("-maxAlnsPerStartPos")) p.max_alns_per_start = std::atoi(v);
+        else if (takes("-ignore5")) p.ignore5 = std::atoi(v);
+        else if (takes("-ignore3")) p.ignore3 = std::atoi(v);
+        else if (takes("-h")) { p.het_rate = std::atof(v); p.het_rate_set = 1; }
+        else if (takes("-maxBaseQS")) p.max_base_qs = std::atoi(v);
+        else if (takes("-minQuality")) p.min_quality = std::atoi(v);
+        else if (takes("-querySeq")) std::snprintf(p.query_seq, sizeof p.query_seq, "%s", v);
+        else if (takes("-first")) p.query_first = std::atoi(v);
+        else if (takes("-last")) p.query_last = std::atoi(v);
+        else if (takes("-device")) device = std::atoi(v);
+        else if (!std::strcmp(a, "-psp")) p.print_sample_ploidy = 1;
+        else if (!std::strcmp(a, "-p")) p.process_nonunique = 1;
+        else if (!std::strcmp(a, "-s")) p.process_secondary = 1;
+        else if (!std::strcmp(a, "-ignoreLowerCaseRef")) p.ignore_lowercase_ref = 1;
+        else if (!std::strcmp(a, "-embeddedSNVs")) p.call_embedded = 1;
+        else if (!std::strcmp(a, "-csb")) p.calc_strand_bias = 1;
+        else { std::fprintf(stderr, "unknown or unsupported option %s\n", a); return usage(argv[0]); }
+    }
+    if (!in || !ref || !outp) return usage(argv[0]);
+    ngsep_ctx* c = nullptr;
+    int rc = ngsep_open(device, &p, &c);
+    if (rc != NGSEP_OK) { std::fprintf(stderr, "error: %s\n", c ? ngsep_last_error(c) : "open failed"); return 1; }
+    rc = ngsep_load_fasta(c, ref);
+    std::string vcf = std::string(outp) + ".vcf";
+    if (rc == NGSEP_OK) rc = ngsep_call_bam(c, in, vcf.c_str());
+    if (rc != NGSEP_OK) { std::fprintf(stderr, "error %d: %s\n", rc, ngsep_last_error(c)); ngsep_close(c); return 1; }
+    ngsep_stats st;
+    ngsep_get_stats(c, &st);
+    std::fprintf(stderr, "alignments=%lld admitted=%lld positions=%lld candidates=%lld variants=%lld\n",
+                 (long long)st.alignments_in, (long long)st.alignments_admitted, (long long)st.positions_genotyped,
+                 (long long)st.candidates, (long long)st.sites_called);
+    ngsep_close(c);
+    return 0;
+}

@@ -1,0 +1,706 @@
+// engine.cpp -- host side of the MI355X NGSEP SNV caller.
+//
+//  * admission sweep: the reference's AlignmentsPileupGenerator.processAlignment /
+//    processSameStartAlns (discovery/AlignmentsPileupGenerator.java:377-433) decides which
+//    alignments enter the pending list and in which order;
+//  * projection: ReadAlignment.updateAlleleCallsInfo / getAlignedReadPosition /
+//    getAlleleCall / getBaseQualityScore (alignments/ReadAlignment.java:747-871,989-1027)
+//    are evaluated once per read and stored as one code byte per covered reference position;
+//  * staging: reads of every window are laid out as fixed-stride slots (SoA) in HBM;
+//    the per-position pileup work is done by the kernels in kernels.hip.
+#include "engine.hpp"
+
+#include <algorithm>
+#include <cctype>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+
+namespace ngsep {
+
+int set_error(ngsep_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+static inline int dna_index(char ch) {
+    switch (ch) {
+        case 'A': return 0;
+        case 'C': return 1;
+        case 'G': return 2;
+        case 'T': return 3;
+        default: return -1;
+    }
+}
+
+// Likelihood addends exactly as CountsHelper computes its caches (CountsHelper.java:147-185).
+void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g) {
+    std::memset(t, 0, sizeof(*t));
+    const int f = 250;   // round(0.5*500): SingleSampleVariantPileupListener.discoverSNV passes 0.5
+    const double af = (double)f / 500.0;
+    for (int q = 3; q <= 30; q++) {
+        double e0 = -0.1 * q;
+        t->E[q] = e0 - std::log10(3.0);                        // logProbCacheError[q][4]
+        double errorProb = std::pow(10.0, -0.1 * q);           // PhredScoreHelper.calculateProbability
+        double successProb = 1 - errorProb;
+        t->A[q] = std::log10(successProb);                     // logProbCacheGT[f][q][0]
+        double hetProb = af * successProb + (1 - af) * errorProb / 3;
+        t->H[q] = std::log10(hetProb);                         // logProbCacheGT[f][q][4]
+    }
+    double h = c->het_rate;
+    g->log_prior_hetero = std::log10(h / 12);                  // CountsHelper.java:415
+    g->log_prior_homo = std::log10((1 - h) / 4);               // CountsHelper.java:416
+    int8_t mq = (int8_t)c->params.max_base_qs;                 // byte field, CountsHelper.java:88
+    g->max_q = mq > 0 ? mq : 30;
+    g->min_quality = (int16_t)c->params.min_quality;
+    g->dump_all = c->params.dump_all_positions;
+    g->pad = 0;
+}
+
+// ReadAlignment.updateAlleleCallsInfo (ReadAlignment.java:747-834): allele-call length per read position.
+static void allele_call_lengths(const RawRead& r, int read_length, int ignore_start, int ignore_end, std::vector<int16_t>& acl) {
+    acl.assign(read_length > 0 ? read_length : 1, 0);
+    int readPos = 0;
+    bool prevIndel = false;
+    const int closeIndel = 2;   // basesToIgnoreCloseToIndel (:115)
+    const int n = (int)r.cigar.size();
+    for (int i = 0; i < n; i++) {
+        int len = r.cigar[i] / 8, op = r.cigar[i] & 7;
+        bool cRef = op & 1, cRead = (op & 2) != 0;
+        int nextOp = -1, nextLen = 0, nextReadCons = 0;
+        bool nextIsIndel = false;
+        if (i < n - 1) {
+            nextOp = r.cigar[i + 1] & 7;
+            nextLen = r.cigar[i + 1] / 8;
+            nextIsIndel = nextOp == 1 || nextOp == 2;
+            nextReadCons = (nextOp & 2) ? nextLen : 0;
+        }
+        if (cRef) {
+            if (cRead) {
+                for (int j = 0; j < len; j++) {
+                    bool skip = readPos < ignore_start;
+                    skip = skip || (read_length - readPos) <= ignore_end;
+                    skip = skip || (prevIndel && j < closeIndel);
+                    skip = skip || (nextIsIndel && j < len - 1 && j >= len - closeIndel);
+                    skip = skip || (nextIsIndel && j == len - 1 &&
+                                    (readPos < closeIndel || read_length - readPos - nextReadCons < closeIndel));
+                    int readPosAfterIndel = readPos + nextReadCons + 1;
+                    skip = skip || (nextIsIndel && j == len - 1 && (read_length - readPosAfterIndel < ignore_end));
+                    if (!skip && readPos < read_length) {
+                        if (j == len - 1 && nextIsIndel) acl[readPos] = (int16_t)(nextOp == 2 ? nextLen + 2 : 2);
+                        else acl[readPos] = 1;
+                    }
+                    readPos++;
+                }
+            }
+        } else if (cRead) {
+            readPos += len;
+        }
+        prevIndel = (op == 1 || op == 2);
+    }
+}
+
+// Projects one admitted read to one code byte per reference position in [first, last].
+// Equivalent to evaluating, for every covered position p, PileupRecord.getAlleleCalls(1)'s
+// per-read step (PileupRecord.java:132-148) and CountsHelper.calculateCountsGTSNV's
+// quality clamp (CountsHelper.java:91).
+void project_read(const ngsep_ctx* c, const RawRead& r, int32_t last, std::vector<uint8_t>& out) {
+    const int64_t span = (int64_t)last - r.first + 1;
+    out.assign(span > 0 ? span : 0, 0);
+    if (span <= 0 || r.chars.empty()) return;   // getAlleleCall returns null without characters
+    int read_length = 0;
+    for (int32_t v : r.cigar) if (v & 2) read_length += v / 8;
+    // setBasesToIgnore5P/3P (ReadAlignment.java:613-644)
+    const bool neg = (r.flags & 0x10) != 0;
+    int ignore_start = neg ? c->params.ignore3 : c->params.ignore5;
+    int ignore_end = neg ? c->params.ignore5 : c->params.ignore3;
+    std::vector<int16_t> acl;
+    allele_call_lengths(r, read_length, ignore_start, ignore_end, acl);
+    int64_t refPos = r.first, readPos = 0;
+    for (int32_t v : r.cigar) {
+        int len = v / 8, op = v & 7;
+        bool cRef = op & 1, cRead = (op & 2) != 0;
+        if (cRef && cRead) {
+            for (int j = 0; j < len; j++) {
+                int64_t rp = readPos + j;
+                int64_t o = refPos + j - r.first;
+                if (rp >= read_length || o < 0 || o >= span) continue;
+                if (acl[rp] != 1) continue;   // 0: masked (getAlleleCall null); >1: skipped for span 1
+                int qc = r.quals.empty() ? '+' : (unsigned char)r.quals[rp];   // getBaseQualityScore
+                if (qc > 127) qc = 127;                                          // setQualityScores cap
+                int q = (int8_t)std::min(30, qc - 33);
+                int a = dna_index(r.chars[rp]);
+                uint8_t code;
+                if (q <= 3) code = (uint8_t)(kCodeCounted | (q < 0 ? 0 : q));
+                else if (a < 0) code = (uint8_t)(kCodeCounted | q);
+                else code = (uint8_t)(kCodeValid | (a << 5) | q);
+                out[o] = code;
+            }
+        }
+        if (cRef) refPos += len;
+        if (cRead) readPos += len;
+    }
+}
+
+static int32_t alignment_last(const RawRead& r) {
+    int32_t e = r.first;
+    for (int32_t v : r.cigar) if (v & 1) e += v / 8;
+    return e - 1;
+}
+
+static void admit(ngsep_ctx* c, const RawRead& r) {
+    ContigReads& cr = c->contig;
+    int32_t last = alignment_last(r);
+    std::vector<uint8_t> bytes;
+    project_read(c, r, last, bytes);
+    cr.first.push_back(r.first);
+    cr.last.push_back(last);
+    cr.neg.push_back((r.flags & 0x10) ? 1 : 0);
+    cr.boff.push_back((int64_t)cr.bytes.size());
+    cr.bytes.insert(cr.bytes.end(), bytes.begin(), bytes.end());
+    int32_t span = last - r.first + 1;
+    if (span > cr.max_span) cr.max_span = span;
+    // union of covered positions inside the sequence (and the query range)
+    int64_t lo = r.first, hi = last;
+    int64_t len = (int64_t)c->seq_bases[r.seq_id].size();
+    if (hi > len) hi = len;
+    if (lo < 1) lo = 1;
+    if (c->params.query_seq[0]) {
+        lo = std::max<int64_t>(lo, c->params.query_first);
+        hi = std::min<int64_t>(hi, c->params.query_last);
+    }
+    if (hi >= lo) {
+        if (lo > cr.cov_last) cr.covered += hi - lo + 1;
+        else if (hi > cr.cov_last) cr.covered += hi - cr.cov_last;
+        if (hi > cr.cov_last) cr.cov_last = (int32_t)hi;
+    }
+    c->stats.alignments_admitted++;
+}
+
+// AlignmentsPileupGenerator.processSameStartAlns (:407-433)
+static void process_same_start(ngsep_ctx* c) {
+    if (c->ss_primary.empty() && c->ss_secondary.empty()) return;
+    std::vector<std::pair<int32_t, int32_t>> per_rg;   // (rg, count): few read groups per start
+    auto handle = [&](const RawRead& r) {
+        for (auto& pr : per_rg) {
+            if (pr.first == r.rg) {
+                if (c->params.max_alns_per_start <= 0 || pr.second < c->params.max_alns_per_start) { pr.second++; admit(c, r); }
+                return;
+            }
+        }
+        per_rg.push_back({r.rg, 1});
+        admit(c, r);
+    };
+    for (const RawRead& r : c->ss_primary) handle(r);
+    for (const RawRead& r : c->ss_secondary) handle(r);
+    c->ss_primary.clear();
+    c->ss_secondary.clear();
+}
+
+// flushes the current sequence: onSequenceEnd of the listener chain
+static int flush_sequence(ngsep_ctx* c) {
+    if (c->cur_seq < 0) return NGSEP_OK;
+    process_same_start(c);
+    int rc = stage_contig_reads(c, c->contig, !c->staging_mode);
+    c->contig.clear();
+    c->cur_seq = -1;
+    return rc;
+}
+
+int stage_contig_reads(ngsep_ctx* c, ContigReads& cr, bool run_now) {
+    if (cr.seq_id < 0) return NGSEP_OK;
+    c->stats.positions_genotyped += cr.covered;
+    if (!run_now) {
+        c->staged_contigs.emplace_back(std::move(cr));
+        cr = ContigReads();
+        return NGSEP_OK;
+    }
+    std::vector<ContigReads> one;
+    one.emplace_back(std::move(cr));
+    cr = ContigReads();
+    int rc = build_and_upload(c, one);
+    if (rc != NGSEP_OK) return rc;
+    double ms = 0;
+    rc = run_device(c, &ms);
+    device_release(c->dev);
+    return rc;
+}
+
+static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b) {
+    if (!b || b->n_reads < 0) return set_error(c, NGSEP_E_INVALID, "null batch");
+    const int nseq = (int)c->seq_names.size();
+    for (int64_t i = 0; i < b->n_reads; i++) {
+        if (c->query_done) break;
+        c->stats.alignments_in++;
+        RawRead r;
+        r.seq_id = b->seq_id[i];
+        r.first = b->first[i];
+        r.flags = b->flags[i];
+        r.rg = b->read_group ? b->read_group[i] : -1;
+        if (r.seq_id < 0 || r.seq_id >= nseq)
+            return set_error(c, NGSEP_E_INVALID, "alignment on unknown sequence id " + std::to_string(r.seq_id));
+        r.cigar.assign(b->cigar + b->cigar_off[i], b->cigar + b->cigar_off[i] + b->cigar_n[i]);
+        for (int32_t v : r.cigar) {
+            int op = v & 7;
+            if (op == 1 || op == 2)
+                return set_error(c, NGSEP_E_UNSUPPORTED,
+                                 "alignment with an indel (CIGAR I/D): the indel realigner path "
+                                 "(IndelRealignerPileupListener) is not implemented on the GPU yet");
+        }
+        int32_t sl = b->seq_len[i];
+        if (sl > 0) {
+            r.chars.assign(b->bases + b->seq_off[i], sl);
+            bool hq = b->quals && (!b->has_quals || b->has_quals[i]);
+            if (hq) r.quals.assign(b->quals + b->seq_off[i], sl);
+            int read_length = 0;
+            for (int32_t v : r.cigar) if (v & 2) read_length += v / 8;
+            if (read_length != sl) continue;   // ReadAlignment.setReadCharacters throws -> record skipped
+        }
+        int32_t last = alignment_last(r);
+        // querySeq handling (AlignmentsPileupGenerator.java:342-354)
+        if (c->params.query_seq[0]) {
+            if (c->seq_names[r.seq_id] == c->params.query_seq) {
+                c->query_found = true;
+                if (r.first > c->params.query_last) { c->query_done = true; break; }
+                if (c->params.query_first > last) continue;
+            } else if (c->query_found) {
+                c->query_done = true;
+                break;
+            } else {
+                continue;
+            }
+        }
+        // processAlignment (:377-403)
+        if (c->cur_seq >= 0) {
+            bool same = c->cur_seq == r.seq_id;
+            if (same && r.first < c->last_start)
+                return set_error(c, NGSEP_E_INVALID, "alignments are not coordinate-sorted");
+            if (!same || c->last_start != r.first) {
+                process_same_start(c);
+                if (!same) {
+                    int rc = flush_sequence(c);
+                    if (rc != NGSEP_OK) return rc;
+                }
+            }
+        }
+        if (c->cur_seq < 0) {   // startSequence (:435-444)
+            c->cur_seq = r.seq_id;
+            c->contig.clear();
+            c->contig.seq_id = r.seq_id;
+            c->cur_last = last;
+        }
+        if (last > c->cur_last) c->cur_last = last;
+        if (r.flags & 0x100) c->ss_secondary.push_back(std::move(r));
+        else c->ss_primary.push_back(std::move(r));
+        c->last_start = b->first[i];
+    }
+    return NGSEP_OK;
+}
+
+// ---- staging: fixed-stride slot layout of every window's reads ----
+static int choose_slot_size(const std::vector<ContigReads>& contigs) {
+    std::vector<int64_t> hist(4097, 0);
+    for (const ContigReads& cr : contigs)
+        for (size_t i = 0; i < cr.first.size(); i++) {
+            int64_t span = (int64_t)cr.last[i] - cr.first[i] + 1;
+            if (span < 1) span = 1;
+            hist[std::min<int64_t>(span, 4096)]++;
+        }
+    int best = 16;
+    double best_cost = -1;
+    for (int S = 16; S <= 512; S += 16) {
+        double cost = 0;
+        for (int s = 1; s <= 4096; s++)
+            if (hist[s]) cost += (double)hist[s] * ((s + S - 1) / S) * (S + 4);
+        if (best_cost < 0 || cost < best_cost) { best_cost = cost; best = S; }
+    }
+    return best;
+}
+
+static inline uint8_t ref_code(const ngsep_ctx* c, char ch) {
+    if (c->params.ignore_lowercase_ref && std::islower((unsigned char)ch)) return kRefInWindow;   // :198
+    int a = dna_index((char)std::toupper((unsigned char)ch));                                      // :199
+    if (a < 0) return kRefInWindow;    // VariantDiscoverySNVQAlgorithm.java:104-107 (N reference)
+    return (uint8_t)(kRefCallable | (a << 5));
+}
+
+int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
+    Staged& s = c->staged;
+    s = Staged();
+    int32_t max_span = 1;
+    for (const ContigReads& cr : contigs) max_span = std::max(max_span, cr.max_span);
+    const int S = choose_slot_size(contigs);
+    const int32_t pad = ((max_span + 63) / 64) * 64;
+    s.slot_size = S;
+    s.max_span = max_span;
+    // windows
+    int64_t g = 0;
+    const int64_t W = c->params.window_positions > 0 ? c->params.window_positions : (int64_t)1 << 40;
+    struct WR { size_t contig; int64_t lo, hi; };
+    std::vector<WR> wr;
+    for (size_t ci = 0; ci < contigs.size(); ci++) {
+        const ContigReads& cr = contigs[ci];
+        if (cr.first.empty()) continue;
+        int64_t len = (int64_t)c->seq_bases[cr.seq_id].size();
+        int64_t lo = 1, hi = len;
+        if (c->params.query_seq[0]) { lo = std::max<int64_t>(lo, c->params.query_first); hi = std::min<int64_t>(hi, c->params.query_last); }
+        // only the span of covered positions is needed
+        lo = std::max<int64_t>(lo, cr.first.front());
+        int64_t maxlast = 0;
+        for (int32_t l : cr.last) maxlast = std::max<int64_t>(maxlast, l);
+        hi = std::min<int64_t>(hi, maxlast);
+        for (int64_t w0 = lo; w0 <= hi; w0 += W) {
+            int64_t w1 = std::min(hi, w0 + W - 1);
+            Window w;
+            w.seq_id = cr.seq_id; w.w0 = (int32_t)w0; w.wlen = (int32_t)(w1 - w0 + 1);
+            w.gbase = g; w.pad = pad;
+            g += (int64_t)w.wlen + 2 * pad;
+            s.windows.push_back(w);
+            wr.push_back({ci, w0, w1});
+        }
+    }
+    s.g_len = g + 64;
+    if (s.g_len >= ((int64_t)1 << 31))
+        return set_error(c, NGSEP_E_UNSUPPORTED, "staged genome exceeds 2^31 positions per device run; use window batching");
+    // reads and slots
+    s.h_reads.clear();
+    s.h_slot_pos.clear();
+    s.h_slots.clear();
+    int64_t nslots = 0, nreads = 0, nbases = 0;
+    std::vector<std::pair<int64_t, int64_t>> ranges(s.windows.size());
+    for (size_t wi = 0; wi < s.windows.size(); wi++) {
+        const ContigReads& cr = contigs[wr[wi].contig];
+        int64_t w0 = wr[wi].lo, w1 = wr[wi].hi;
+        auto lo_it = std::lower_bound(cr.first.begin(), cr.first.end(), (int32_t)std::max<int64_t>(INT32_MIN, w0 - max_span + 1));
+        auto hi_it = std::upper_bound(cr.first.begin(), cr.first.end(), (int32_t)w1);
+        int64_t a = lo_it - cr.first.begin(), b = hi_it - cr.first.begin();
+        ranges[wi] = {a, b};
+        for (int64_t i = a; i < b; i++) {
+            int64_t span = (int64_t)cr.last[i] - cr.first[i] + 1;
+            if (span < 1) span = 1;
+            nslots += (span + S - 1) / S;
+        }
+        nreads += b - a;
+    }
+    s.h_slots.assign((size_t)nslots * S, 0);
+    s.h_slot_pos.resize(nslots);
+    s.h_reads.resize((size_t)nreads * 4);
+    int64_t slot = 0, ri = 0;
+    for (size_t wi = 0; wi < s.windows.size(); wi++) {
+        Window& w = s.windows[wi];
+        const ContigReads& cr = contigs[wr[wi].contig];
+        w.read_begin = ri;
+        const int64_t goff = w.gbase + w.pad - w.w0;   // G = pos + goff
+        for (int64_t i = ranges[wi].first; i < ranges[wi].second; i++) {
+            int64_t span = (int64_t)cr.last[i] - cr.first[i] + 1;
+            int64_t ns = span < 1 ? 1 : (span + S - 1) / S;
+            int64_t gfirst = cr.first[i] + goff;
+            s.h_reads[ri * 4 + 0] = (int32_t)gfirst;
+            s.h_reads[ri * 4 + 1] = (int32_t)(cr.last[i] + goff);
+            s.h_reads[ri * 4 + 2] = (int32_t)slot;
+            s.h_reads[ri * 4 + 3] = cr.neg[i];
+            if (span > 0) std::memcpy(&s.h_slots[(size_t)slot * S], &cr.bytes[cr.boff[i]], (size_t)span);
+            for (int64_t k = 0; k < ns; k++) s.h_slot_pos[slot + k] = (int32_t)(gfirst + k * S);
+            slot += ns;
+            nbases += span > 0 ? span : 0;
+            ri++;
+        }
+        w.read_end = ri;
+    }
+    s.n_reads = nreads;
+    s.n_slots = nslots;
+    s.n_read_bases = nbases;
+    for (const ContigReads& cr : contigs) s.covered += cr.covered;
+    // reference codes in global coordinates
+    s.h_ref.assign((size_t)s.g_len, 0);
+    for (const Window& w : s.windows) {
+        const std::string& ref = c->seq_bases[w.seq_id];
+        uint8_t* dst = &s.h_ref[(size_t)(w.gbase + w.pad)];
+        for (int32_t k = 0; k < w.wlen; k++) dst[k] = ref_code(c, ref[(size_t)w.w0 - 1 + k]);
+    }
+    c->stats.read_bases = nbases;
+    c->stats.slot_bytes = nslots * S;
+    if (!c->dev) {
+        std::string err;
+        c->dev = device_create(c->device, err);
+        if (!c->dev) return set_error(c, NGSEP_E_DEVICE, err);
+    }
+    std::string err;
+    if (device_upload(c->dev, s, err) != 0) return set_error(c, NGSEP_E_DEVICE, err);
+    // host mirrors are not needed any more
+    std::vector<uint8_t>().swap(s.h_slots);
+    std::vector<int32_t>().swap(s.h_slot_pos);
+    std::vector<int32_t>().swap(s.h_reads);
+    std::vector<uint8_t>().swap(s.h_ref);
+    return NGSEP_OK;
+}
+
+// java.lang.Math.round + PhredScoreHelper.calculatePhredScore (math/PhredScoreHelper.java:31-40)
+int64_t java_round(double x) {
+    if (std::isnan(x)) return 0;
+    double f = std::floor(x);
+    double r = (x - f >= 0.5) ? f + 1.0 : f;
+    if (r >= 9.2233720368547758e18) return INT64_MAX;
+    if (r <= -9.2233720368547758e18) return INT64_MIN;
+    return (int64_t)r;
+}
+int java_phred(double p) {
+    if (p == 0) return 255;
+    double score = -10 * std::log10(p);
+    if (score > 255) return 255;
+    return (int16_t)java_round(score);
+}
+
+// -csb: CountsHelper.getScoreStrandBiasFisher (CountsHelper.java:563-576), host side, emitted calls only.
+static double fisher_exact(std::vector<double>& lf, int a, int b, int c, int d) {
+    int n = a + b + c + d;
+    if ((int)lf.size() <= n) {   // FisherExactTest.initLogFactorials (math/FisherExactTest.java:103-110)
+        int m = std::max(n, 10000);
+        lf.assign(m + 1, 0);
+        for (int i = 2; i <= m; i++) lf[i] = lf[i - 1] + std::log10((double)i);
+    }
+    double ans = lf[a + b];
+    ans += lf[c + d];
+    ans += lf[a + c];
+    ans += lf[b + d];
+    ans -= lf[a];
+    ans -= lf[b];
+    ans -= lf[c];
+    ans -= lf[d];
+    ans -= lf[n];
+    return std::pow(10.0, ans);
+}
+static double fisher_pvalue(std::vector<double>& lf, int a, int b, int c, int d) {   // FisherExactTest.java:65-101
+    if (a > b) { std::swap(a, b); std::swap(c, d); }
+    if (a > c) { std::swap(a, c); std::swap(b, d); }
+    int e = std::min(a, d);
+    double answer = 0;
+    while (a >= 0 && d >= 0) {
+        double p = fisher_exact(lf, a, b, c, d);
+        if (e >= 10 && answer > (double)(100 * e) * p) break;
+        answer += p;
+        a--; b++; c++; d--; e++;
+    }
+    return answer;
+}
+static void apply_strand_bias(std::vector<ngsep_site_out>& sites, size_t from) {
+    std::vector<double> lf;
+    for (size_t i = from; i < sites.size(); i++) {
+        ngsep_site_out& s = sites[i];
+        if (s.n_alleles != 2 || s.genotype <= 0) continue;   // CalledSNV, not undecided/homRef (:218-220)
+        int r = dna_index(s.ref), a = s.alt;
+        double pv = fisher_pvalue(lf, s.strand_counts[r][0], s.strand_counts[a][0], s.strand_counts[r][1], s.strand_counts[a][1]);
+        s.strand_bias = (int8_t)std::min(100, java_phred(pv));   // MAX_STRAND_BIAS_SCORE
+    }
+}
+
+int run_device(ngsep_ctx* c, double* elapsed_ms) {
+    LikTables t;
+    GenotypeParams gp;
+    compute_tables(c, &t, &gp);
+    std::vector<ngsep_site_out> out;
+    double scan_ms = 0, geno_ms = 0, total_ms = 0;
+    int64_t ncand = 0;
+    std::string err;
+    // exact pruning is proven for h <= 0.1 ("K1: why pruning is exact")
+    int prune = c->params.prune_candidates && !c->params.dump_all_positions && c->het_rate <= 0.1;
+    if (device_run(c->dev, c->staged, t, gp, prune, out, &scan_ms, &geno_ms, &total_ms, &ncand, err) != 0)
+        return set_error(c, NGSEP_E_DEVICE, err);
+    // windows are laid out in processing order, so global order == (sequence order, position)
+    std::sort(out.begin(), out.end(), [](const ngsep_site_out& a, const ngsep_site_out& b) { return a.pos < b.pos; });
+    const std::vector<Window>& ws = c->staged.windows;
+    size_t from = c->sites.size();
+    for (ngsep_site_out& o : out) {
+        int64_t gpos = o.pos;
+        auto it = std::upper_bound(ws.begin(), ws.end(), gpos, [](int64_t v, const Window& w) { return v < w.gbase; });
+        if (it == ws.begin()) continue;
+        const Window& w = *(it - 1);
+        int64_t off = gpos - w.gbase - w.pad;
+        if (off < 0 || off >= w.wlen) continue;
+        o.seq_id = w.seq_id;
+        o.pos = (int32_t)(w.w0 + off);
+        c->sites.push_back(o);
+    }
+    if (c->params.calc_strand_bias) apply_strand_bias(c->sites, from);
+    c->stats.candidates = ncand;
+    c->stats.sites_called += (int64_t)(c->sites.size() - from);
+    c->stats.kernel_ms = total_ms;
+    c->stats.scan_ms = scan_ms;
+    c->stats.genotype_ms = geno_ms;
+    if (elapsed_ms) *elapsed_ms = total_ms;
+    return NGSEP_OK;
+}
+
+// ---- reference loading: FastaFileReader with keepLowerCase (sequences/io/FastaFileReader.java:170-205) ----
+static inline char mask_base(char ch) {
+    switch (ch) {
+        case 'A': case 'a': case 'C': case 'c': case 'N': case 'n':
+        case 'G': case 'g': case 'T': case 't': return ch;
+        default: return 'N';   // DNAMaskedSequence default index
+    }
+}
+int load_fasta(ngsep_ctx* c, const char* path) {
+    std::FILE* f = std::fopen(path, "rb");
+    if (!f) return set_error(c, NGSEP_E_IO, std::string("cannot open ") + path);
+    std::string name, seq;
+    bool have = false;
+    char* line = nullptr;
+    size_t cap = 0;
+    ssize_t l;
+    auto commit = [&]() {
+        if (!have) return;
+        c->seq_names.push_back(name);
+        c->seq_bases.push_back(std::move(seq));
+        seq.clear();
+    };
+    while ((l = getline(&line, &cap, f)) >= 0) {
+        while (l > 0 && (line[l - 1] == '\n' || line[l - 1] == '\r')) line[--l] = 0;
+        if (l > 0 && line[0] == '>') {
+            commit();
+            size_t e = 1;
+            while (line[e] && line[e] != ' ' && line[e] != '\t') e++;
+            name.assign(line + 1, e - 1);
+            have = true;
+        } else if (have) {
+            size_t o = seq.size();
+            seq.resize(o + (size_t)l);
+            for (ssize_t i = 0; i < l; i++) seq[o + i] = mask_base(line[i]);
+        }
+    }
+    commit();
+    std::free(line);
+    std::fclose(f);
+    return NGSEP_OK;
+}
+
+}  // namespace ngsep
+
+// ======================= C ABI (engine part) =======================
+using namespace ngsep;
+
+extern "C" int ngsep_abi_version(void) { return NGSEP_ABI_VERSION; }
+
+extern "C" void ngsep_params_default(ngsep_params* p) {
+    std::memset(p, 0, sizeof(*p));
+    p->min_mq = 20;
+    p->max_alns_per_start = 5;
+    p->max_base_qs = 30;
+    p->min_quality = 40;
+    p->ploidy = 2;
+    p->het_rate = 0.001;
+    p->query_first = 0;
+    p->query_last = 1000000000;
+    std::snprintf(p->sample_id, sizeof p->sample_id, "Sample");
+    p->prune_candidates = 1;
+    p->window_positions = 1 << 26;
+}
+
+extern "C" int ngsep_open(int device, const ngsep_params* params, ngsep_ctx** out) {
+    if (!out) return NGSEP_E_INVALID;
+    ngsep_ctx* c = new ngsep_ctx();
+    if (params) c->params = *params;
+    else ngsep_params_default(&c->params);
+    c->device = device;
+    if (c->params.ploidy >= 3) {
+        *out = c;
+        return set_error(c, NGSEP_E_UNSUPPORTED, "ploidy >= 3 uses the pool algorithm (SingleSampleVariantPileupListener.genotypeVariantPool), not implemented");
+    }
+    // SingleSampleVariantsDetector.run (:591-593)
+    c->het_rate = c->params.het_rate;
+    if (!c->params.het_rate_set && c->params.ploidy == 1) c->het_rate = 1e-6;
+    *out = c;
+    return NGSEP_OK;
+}
+
+extern "C" int ngsep_close(ngsep_ctx* c) {
+    if (!c) return NGSEP_E_INVALID;
+    if (c->dev) device_destroy(c->dev);
+    delete c;
+    return NGSEP_OK;
+}
+
+extern "C" const char* ngsep_last_error(ngsep_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+extern "C" int ngsep_get_stats(ngsep_ctx* c, ngsep_stats* out) {
+    if (!c || !out) return NGSEP_E_INVALID;
+    *out = c->stats;
+    return NGSEP_OK;
+}
+
+extern "C" int ngsep_device_count(void) { return device_count(); }
+
+extern "C" int ngsep_set_reference(ngsep_ctx* c, const char* name, const char* bases, int64_t len) {
+    if (!c || !name || (!bases && len > 0) || len < 0) return NGSEP_E_INVALID;
+    c->seq_names.emplace_back(name);
+    std::string s(bases, (size_t)len);
+    for (char& ch : s) ch = mask_base(ch);
+    c->seq_bases.push_back(std::move(s));
+    return NGSEP_OK;
+}
+
+extern "C" int ngsep_load_fasta(ngsep_ctx* c, const char* path) {
+    if (!c || !path) return NGSEP_E_INVALID;
+    return load_fasta(c, path);
+}
+
+extern "C" int ngsep_n_sequences(ngsep_ctx* c) { return c ? (int)c->seq_names.size() : 0; }
+extern "C" const char* ngsep_sequence_name(ngsep_ctx* c, int i) {
+    if (!c || i < 0 || i >= (int)c->seq_names.size()) return nullptr;
+    return c->seq_names[i].c_str();
+}
+
+extern "C" int ngsep_process_alignments(ngsep_ctx* c, const ngsep_read_batch* b) {
+    if (!c) return NGSEP_E_INVALID;
+    c->staging_mode = false;
+    return process_batch(c, b);
+}
+
+extern "C" int ngsep_notify_end(ngsep_ctx* c) {
+    if (!c) return NGSEP_E_INVALID;
+    return flush_sequence(c);
+}
+
+extern "C" int ngsep_fetch_sites(ngsep_ctx* c, ngsep_site_out* out, int64_t cap, int64_t* n_out) {
+    if (!c) return NGSEP_E_INVALID;
+    int64_t n = (int64_t)c->sites.size();
+    if (n_out) *n_out = n;
+    if (out && cap > 0) std::memcpy(out, c->sites.data(), sizeof(ngsep_site_out) * (size_t)std::min(n, cap));
+    return NGSEP_OK;
+}
+
+extern "C" int ngsep_clear_sites(ngsep_ctx* c) {
+    if (!c) return NGSEP_E_INVALID;
+    c->sites.clear();
+    return NGSEP_OK;
+}
+
+extern "C" int ngsep_stage_alignments(ngsep_ctx* c, const ngsep_read_batch* b) {
+    if (!c) return NGSEP_E_INVALID;
+    c->staging_mode = true;
+    return process_batch(c, b);
+}
+
+extern "C" int ngsep_stage_finish(ngsep_ctx* c) {
+    if (!c) return NGSEP_E_INVALID;
+    c->staging_mode = true;
+    int rc = flush_sequence(c);
+    if (rc != NGSEP_OK) return rc;
+    rc = build_and_upload(c, c->staged_contigs);
+    c->staged_contigs.clear();
+    return rc;
+}
+
+extern "C" int ngsep_run_staged(ngsep_ctx* c, double* elapsed_ms) {
+    if (!c || !c->dev) return set_error(c, NGSEP_E_INVALID, "nothing staged");
+    c->sites.clear();
+    c->stats.sites_called = 0;
+    return run_device(c, elapsed_ms);
+}
+
+extern "C" int ngsep_release_staged(ngsep_ctx* c) {
+    if (!c) return NGSEP_E_INVALID;
+    if (c->dev) device_release(c->dev);
+    c->staged = Staged();
+    return NGSEP_OK;
+}

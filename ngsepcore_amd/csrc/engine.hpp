@@ -1,0 +1,149 @@
+// engine.hpp -- internal types of libngsep_amd.so (not part of the C ABI).
+//
+// Host side mirrors the reference's AlignmentsPileupGenerator admission sweep
+// (discovery/AlignmentsPileupGenerator.java:377-452) and ReadAlignment's allele-call
+// projection (alignments/ReadAlignment.java:747-871); the per-position work
+// (PileupRecord -> CountsHelper -> VariantDiscoverySNVQAlgorithm) runs in kernels.hip.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+#include <mutex>
+
+#include "../../include/ngsep_gpu.h"
+
+namespace ngsep {
+
+// ---- projected read-base code (one byte per reference position a read covers) ----
+//   0x00                  : no allele call (deletion/skip, masked base, base before an indel, padding)
+//   0x20 | q              : counted call that does not update likelihoods (q<=3 or not A/C/G/T)
+//   0x80 | a<<5 | q       : valid call, allele a (0..3 = A,C,G,T), q = min(30, phred) > 3
+// q is CountsHelper.java:91's min(DEF_MAX_BASE_QS, qual-33); the -maxBaseQS cap (:217-219)
+// is applied in the kernel.
+constexpr uint8_t kCodeCounted = 0x20;
+constexpr uint8_t kCodeValid = 0x80;
+
+// ---- reference code per position (global coordinate) ----
+//   0x00 : padding between windows (outside any window)
+//   0x01 : inside a window, not callable (N, lower case with -ignoreLowerCaseRef)
+//   0x80 | a<<5 : callable reference base a
+constexpr uint8_t kRefInWindow = 0x01;
+constexpr uint8_t kRefCallable = 0x80;
+
+// K2 output record (device layout == ngsep_site_out, with gpos in .pos)
+static_assert(sizeof(ngsep_site_out) == 152, "site record layout");
+
+// Likelihood addends for the SNV model with n=4 alleles and f=g=250
+// (CountsHelper.java:147-185 with heterozygousProportion 0.5, SingleSampleVariantPileupListener.java:236)
+struct LikTables {
+    double A[32];   // log10(1-e)                     logProbCacheGT[f][q][0]
+    double H[32];   // log10(0.5(1-e)+0.5 e/3)        logProbCacheGT[250][q][4]
+    double E[32];   // -0.1 q - log10(3)              logProbCacheError[q][4]
+};
+
+struct GenotypeParams {
+    double log_prior_homo;     // log10((1-h)/4), CountsHelper.java:416
+    double log_prior_hetero;   // log10(h/12),    CountsHelper.java:415
+    int32_t max_q;             // effective -maxBaseQS cap
+    int32_t min_quality;       // -minQuality
+    int32_t dump_all;          // emit a record for every position with DP>0
+    int32_t pad;
+};
+
+struct Window {            // a contiguous range of one sequence, resident in HBM
+    int32_t seq_id;
+    int32_t w0;            // first 1-based position
+    int32_t wlen;          // number of positions
+    int64_t gbase;         // global coordinate of position w0 is gbase + pad
+    int32_t pad;           // halo positions on each side (>= max read span)
+    int64_t read_begin, read_end;    // index range in the global read table
+};
+
+// Admitted reads of one sequence in pending order (AlignmentsPileupGenerator.pendingAlignments)
+struct ContigReads {
+    int32_t seq_id = -1;
+    std::vector<int32_t> first, last;
+    std::vector<uint8_t> neg;          // 1 = negative strand
+    std::vector<int64_t> boff;         // offset of the read's projected bytes
+    std::vector<uint8_t> bytes;        // projected codes over [first, last]
+    int32_t max_span = 0;
+    int64_t covered = 0;               // union of [first,last] (positions with a pileup)
+    int32_t cov_last = 0;              // running max of last (for `covered`)
+    void clear() { first.clear(); last.clear(); neg.clear(); boff.clear(); bytes.clear(); max_span = 0; covered = 0; cov_last = 0; seq_id = -1; }
+};
+
+// One raw alignment as received (kept while its same-start group is open)
+struct RawRead {
+    int32_t seq_id, first, flags, rg;
+    std::vector<int32_t> cigar;
+    std::string chars;     // empty = no characters
+    std::string quals;     // empty = no qualities ('*')
+};
+
+struct Device;   // kernels.hip
+
+struct Staged {            // everything resident for one run
+    std::vector<Window> windows;
+    int64_t g_len = 0;                  // global coordinate length
+    int64_t n_reads = 0, n_slots = 0, n_read_bases = 0, covered = 0;
+    int32_t slot_size = 0;
+    int32_t max_span = 0;
+    // host mirrors (freed after upload)
+    std::vector<uint8_t> h_slots;
+    std::vector<int32_t> h_slot_pos;
+    std::vector<int32_t> h_reads;       // 4 ints per read: gfirst, glast, slot, flags
+    std::vector<uint8_t> h_ref;
+};
+
+}  // namespace ngsep
+
+struct ngsep_ctx {
+    ngsep_params params;
+    int device = 0;
+    std::string err;
+    double het_rate = 0.001;
+    // reference
+    std::vector<std::string> seq_names;
+    std::vector<std::string> seq_bases;      // case kept, masked to AaCcNngGtT
+    // admission sweep state
+    int32_t cur_seq = -1;
+    int32_t last_start = 0;
+    int32_t cur_last = 0;
+    std::vector<ngsep::RawRead> ss_primary, ss_secondary;
+    ngsep::ContigReads contig;
+    bool query_found = false;
+    bool query_done = false;
+    bool staging_mode = false;
+    // windows collected for a staged run
+    std::vector<ngsep::ContigReads> staged_contigs;
+    ngsep::Staged staged;
+    ngsep::Device* dev = nullptr;
+    // outputs
+    std::vector<ngsep_site_out> sites;
+    ngsep_stats stats{};
+};
+
+namespace ngsep {
+// engine.cpp
+int set_error(ngsep_ctx* c, int code, const std::string& msg);
+void project_read(const ngsep_ctx* c, const RawRead& r, int32_t last, std::vector<uint8_t>& out);
+int stage_contig_reads(ngsep_ctx* c, ContigReads& cr, bool run_now);
+int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs);
+int run_device(ngsep_ctx* c, double* elapsed_ms);
+void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g);
+// kernels.hip
+Device* device_create(int ordinal, std::string& err);
+void device_destroy(Device* d);
+int device_upload(Device* d, const Staged& s, std::string& err);
+int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypeParams& g, int prune,
+               std::vector<ngsep_site_out>& out, double* scan_ms, double* geno_ms, double* total_ms,
+               int64_t* n_candidates, std::string& err);
+void device_release(Device* d);
+int device_count();
+// vcf.cpp
+std::string format_header(const ngsep_ctx* c);
+int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& out);
+// bam.cpp
+int call_bam(ngsep_ctx* c, const char* bam_path, const char* out_vcf);
+}  // namespace ngsep

@@ -1,0 +1,189 @@
+// vcf.cpp -- VCF text exactly as SingleSampleVariantsDetector writes it:
+// VCFFileHeader.makeDefaultEmptyHeader/print (vcf/VCFFileHeader.java:46-95,219-245) and
+// VCFFileWriter.printVCFRecord/printGenotypeInfo (vcf/VCFFileWriter.java:44-308) for
+// CalledSNV (variants/CalledSNV.java) and triallelic CalledGenomicVariantImpl calls.
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "engine.hpp"
+
+namespace ngsep {
+
+int64_t java_round(double x);
+
+static const char* kHeaderLines[][5] = {
+    // type, id, description, number, data type (attribute order ID,Number,Type,Description: VCFHeaderLine.java:43-50)
+    {"INFO", "CNV", "\"Number of samples with CNVs around this variant\"", "1", "Integer"},
+    {"INFO", "TA", "\"Variant annotation based on a gene model\"", "1", "String"},
+    {"INFO", "TID", "\"Id of the transcript related to the variant annotation\"", "1", "String"},
+    {"INFO", "TGN", "\"Name of the gene related to the variant annotation\"", "1", "String"},
+    {"INFO", "TCO", "\"One based codon position of the start of the variant. The decimal is the codon position\"", "1", "Float"},
+    {"INFO", "TACH", "\"Description of the aminoacid change produced by a non-synonymous mutation. String encoded as reference aminoacid, position and mutated aminoacid\"", "1", "String"},
+    {"INFO", "NS", "\"Number of samples genotyped\"", "1", "Integer"},
+    {"INFO", "MAF", "\"Minor allele frequency\"", "1", "Float"},
+    {"INFO", "OH", "\"Observed heterozygosity\"", "1", "Float"},
+    {"INFO", "AN", "\"Number of alleles in called genotypes\"", "1", "Integer"},
+    {"INFO", "AFS", "\"Allele counts over the population for all alleles, including the reference\"", "R", "Integer"},
+    {"INFO", "TYPE", "\"Type of variant\"", "1", "String"},
+    {"INFO", "FS", "\"Phred-scaled p-value using Fisher's exact test to detect strand bias\"", "1", "Float"},
+    {"INFO", "END", "\"End position of the structural variant\"", "1", "Integer"},
+    {"INFO", "SVTYPE", "\"Type of SV:DEL=Deletion, INS=Insertion, DUP=Duplication, INV=Inversion\"", "1", "String"},
+    {"INFO", "SVLEN", "\"Difference in length between REF and ALT alleles\"", "1", "Integer"},
+    {"FORMAT", "GT", "\"Genotype\"", "1", "String"},
+    {"FORMAT", "PL", "\"Phred-scaled genotype likelihoods rounded to the closest integer\"", "G", "Integer"},
+    {"FORMAT", "GQ", "\"Genotype quality\"", "1", "Integer"},
+    {"FORMAT", "DP", "\"Read depth\"", "1", "Integer"},
+    {"FORMAT", "ADP", "\"Counts for observed alleles, including the reference allele\"", "R", "Integer"},
+    {"FORMAT", "BSDP", "\"Number of base calls (depth) for the 4 nucleotides in called SNVs sorted as A,C,G,T\"", "4", "Integer"},
+    {"FORMAT", "ACN", "\"Predicted copy number of each allele taking into account the prediction of number of copies of the region surrounding the variant\"", "R", "Integer"},
+};
+
+std::string format_header(const ngsep_ctx* c) {
+    std::string h = "##fileformat=VCFv4.2\n";
+    for (const auto& l : kHeaderLines) {
+        h += "##"; h += l[0]; h += "=<ID="; h += l[1]; h += ",Number="; h += l[3];
+        h += ",Type="; h += l[4]; h += ",Description="; h += l[2]; h += ">\n";
+    }
+    if (c->params.print_sample_ploidy)
+        h += "##SAMPLE=<ID=" + std::string(c->params.sample_id) + ",PL=" + std::to_string(c->params.ploidy) + ">\n";
+    h += "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t";
+    h += c->params.sample_id;
+    h += "\n";
+    return h;
+}
+
+static inline int tri(int i, int j) {   // index of L[i][j] in the upper-triangle layout of ngsep_site_out.logc
+    if (i > j) { int t = i; i = j; j = t; }
+    static const int base[4] = {0, 4, 7, 9};
+    return base[i] + (j - i);
+}
+
+static void app(std::string& o, long long v) { o += std::to_string(v); }
+
+int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& o) {
+    static const char kB[] = "ACGT";
+    const size_t start = o.size();
+    const int ploidy = c->params.ploidy;
+    int ri = 0;
+    while (ri < 4 && kB[ri] != s.ref) ri++;
+    if (ri == 4 || s.n_alleles < 2) return 0;
+    const std::string& name = (s.seq_id >= 0 && s.seq_id < (int)c->seq_names.size()) ? c->seq_names[s.seq_id] : std::string("?");
+    o += name; o += '\t'; app(o, s.pos); o += "\t.\t"; o += (char)s.ref; o += '\t';
+    o += kB[(int)s.alt];
+    if (s.n_alleles == 3) { o += ','; o += kB[(int)s.third]; }
+    o += '\t'; app(o, s.qual); o += "\t.\t";
+    // INFO: FS for CalledSNV (SingleSampleVariantsDetector.java:956-958), TYPE for non-SNV types (VCFFileWriter.java:47-49)
+    bool printed = false;
+    if (s.n_alleles == 2 && s.strand_bias != -1) { o += "FS="; app(o, s.strand_bias); printed = true; }
+    if (s.n_alleles == 3) { if (printed) o += ';'; o += "TYPE=MULTISNV"; printed = true; }
+    if (!printed) o += '.';
+    o += "\tGT:PL:GQ:DP:BSDP:ACN\t";
+    if (s.n_alleles == 2) {
+        const int ai = s.alt;
+        if (s.genotype == 2) { o += '1'; if (ploidy > 1) o += "/1"; }
+        else o += "0/1";
+        o += ':';
+        // CalledSNV keeps float log-conditionals (CalledSNV.java:42-45,259-265)
+        const float hr = (float)s.logc[tri(ri, ri)], ha = (float)s.logc[tri(ai, ai)];
+        const float ra = (float)s.logc[tri(ri, ai)], ar = ra;
+        const bool present = (hr + ra + ar + ha) != 0;                  // CalledSNV.java:422
+        const double lc[2][2] = {{hr, ra}, {ar, ha}};
+        for (int j = 0; j < 2; j++)
+            for (int i = 0; i <= j; i++) {
+                if (i > 0 || j > 0) o += ',';
+                app(o, present ? (int)java_round(-10 * lc[i][j]) : 0);   // VCFFileWriter.java:203-211
+            }
+        o += ':'; app(o, s.gq); o += ':'; app(o, s.dp); o += ':';
+        for (int k = 0; k < 4; k++) { if (k) o += ','; app(o, s.counts[k]); }
+        o += ':';
+        // CalledSNV.updateAllelesCopyNumberFromCounts (CalledSNV.java:134-158)
+        int total = ploidy, refcn = 0;
+        if (s.genotype == 2) refcn = 0;
+        else if (total <= 2) { total = 2; refcn = 1; }
+        else {
+            double cr = s.counts[ri], sum = cr + s.counts[ai];
+            double prop = sum > 0 ? cr / sum : 0.5;
+            if (prop > 1) prop = 1;
+            refcn = (int16_t)java_round(prop * total);
+            if (refcn == 0) refcn = 1;
+            else if (refcn >= total) refcn = total - 1;
+        }
+        if (total == 0) o += '.';
+        else { app(o, refcn); o += ','; app(o, total - refcn); }
+    } else {
+        const int idx[3] = {ri, s.alt, s.third};
+        o += "1/2:";
+        for (int j = 0; j < 3; j++)
+            for (int i = 0; i <= j; i++) {
+                if (i > 0 || j > 0) o += ',';
+                app(o, (int)java_round(-10 * s.logc[tri(idx[i], idx[j])]));
+            }
+        o += ':'; app(o, s.gq); o += ':'; app(o, s.dp); o += ':';
+        for (int k = 0; k < 4; k++) { if (k) o += ','; app(o, s.counts[k]); }
+        o += ':';
+        // CalledGenomicVariantImpl.updateAllelesCopyNumberFromCounts (:228-282), called alleles {1,2}
+        if (ploidy <= 2) o += "0,1,1";
+        else {
+            int cnt[2], tot = 0;
+            for (int i = 0; i < 2; i++) { cnt[i] = s.counts[idx[i + 1]]; if (!cnt[i]) cnt[i] = 1; tot += cnt[i]; }
+            int cn[3] = {0, 0, 0}, tc = 0;
+            for (int i = 0; i < 2; i++) {
+                long long r = java_round((double)ploidy * cnt[i] / tot);
+                cn[i + 1] = (int)(r < 1 ? 1 : r);
+                tc += cn[i + 1];
+            }
+            if (tc < ploidy) cn[1] += ploidy - tc;
+            else {
+                int ex = tc - ploidy;
+                for (int i = 2; ex > 0 && i >= 1; i--) { int rm = ex < cn[i] - 1 ? ex : cn[i] - 1; cn[i] -= rm; ex -= rm; }
+            }
+            app(o, cn[0]); o += ','; app(o, cn[1]); o += ','; app(o, cn[2]);
+        }
+    }
+    o += '\n';
+    return (int64_t)(o.size() - start);
+}
+
+}  // namespace ngsep
+
+using namespace ngsep;
+
+extern "C" int ngsep_write_vcf_header(ngsep_ctx* c, const char* path) {
+    if (!c || !path) return NGSEP_E_INVALID;
+    std::FILE* f = std::fopen(path, "w");
+    if (!f) return set_error(c, NGSEP_E_IO, std::string("cannot write ") + path);
+    std::string h = format_header(c);
+    std::fwrite(h.data(), 1, h.size(), f);
+    std::fclose(f);
+    return NGSEP_OK;
+}
+
+extern "C" int ngsep_append_vcf_records(ngsep_ctx* c, const char* path) {
+    if (!c || !path) return NGSEP_E_INVALID;
+    std::FILE* f = std::fopen(path, "a");
+    if (!f) return set_error(c, NGSEP_E_IO, std::string("cannot write ") + path);
+    std::string buf;
+    buf.reserve(1 << 20);
+    for (const ngsep_site_out& s : c->sites) {
+        if (!s.is_call) continue;
+        format_site(c, s, buf);
+        if (buf.size() > (1 << 20)) { std::fwrite(buf.data(), 1, buf.size(), f); buf.clear(); }
+    }
+    std::fwrite(buf.data(), 1, buf.size(), f);
+    std::fclose(f);
+    c->sites.clear();
+    return NGSEP_OK;
+}
+
+extern "C" int64_t ngsep_format_site(ngsep_ctx* c, const ngsep_site_out* s, char* buf, int64_t cap) {
+    if (!c || !s) return NGSEP_E_INVALID;
+    std::string o;
+    int64_t n = format_site(c, *s, o);
+    if (buf && cap > 0) {
+        int64_t k = std::min<int64_t>(n, cap - 1);
+        std::memcpy(buf, o.data(), (size_t)k);
+        buf[k] = 0;
+    }
+    return n;
+}

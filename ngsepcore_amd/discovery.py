@@ -1,0 +1,252 @@
+"""Host-side mirror of NGSEP's SNV discovery interface, backed by libngsep_amd.so.
+
+Names, option meanings and defaults follow the reference:
+  * SingleSampleVariantsDetector  (src/ngsep/discovery/SingleSampleVariantsDetector.java:62-1082,
+    options main/CommandsDescriptor.xml:565-703)
+  * AlignmentsPileupGenerator.processAlignments / notifyEndOfAlignments
+    (discovery/AlignmentsPileupGenerator.java:334-361,447-452) -> GpuPileupSession
+  * SingleSampleVariantPileupListener.getCalledVariants (:139-141) -> GpuPileupSession.getCalledVariants
+Errors surface as NgsepError (the reference throws IOException / IllegalArgumentException).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+from . import _lib
+from ._lib import NgsepError, NgsepParams, NgsepReadBatch, NgsepSiteOut, NgsepStats
+
+BASES = "ACGT"
+
+
+def default_params() -> NgsepParams:
+    p = NgsepParams()
+    _lib.load().ngsep_params_default(ctypes.byref(p))
+    return p
+
+
+@dataclass
+class CalledSite:
+    """One called variant (CalledSNV or triallelic CalledGenomicVariantImpl)."""
+    sequence: str
+    pos: int
+    ref: str
+    alleles: List[str]
+    genotype: int
+    gq: int
+    qual: int
+    dp: int
+    counts: List[int]
+    strand_counts: List[List[int]]
+    logc: List[float]
+    strand_bias: int
+    is_call: bool
+
+    def log_conditional(self, i: int, j: int) -> float:
+        if i > j:
+            i, j = j, i
+        base = (0, 4, 7, 9)[i]
+        return self.logc[base + j - i]
+
+
+class GpuPileupSession:
+    """One device context: reference + alignment stream -> called SNVs.
+
+    Mirrors the listener chain IndelRealigner -> SingleSampleVariantPileupListener ->
+    SingleSampleVariantsDetector for SNV-only alignments (SingleSampleVariantsDetector.java:919-925).
+    """
+
+    def __init__(self, params: Optional[NgsepParams] = None, device: int = 0):
+        self._lib = _lib.load()
+        self._ctx = ctypes.c_void_p()
+        p = params if params is not None else default_params()
+        rc = self._lib.ngsep_open(device, ctypes.byref(p), ctypes.byref(self._ctx))
+        self._check(rc)
+        self.params = p
+
+    # -- plumbing
+    def _check(self, rc: int):
+        if rc != _lib.NGSEP_OK:
+            msg = self._lib.ngsep_last_error(self._ctx).decode() if self._ctx else "open failed"
+            raise NgsepError(rc, msg)
+
+    def close(self):
+        if self._ctx:
+            self._lib.ngsep_close(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- reference (ReferenceGenome with lower case kept)
+    def load_fasta(self, path: str):
+        self._check(self._lib.ngsep_load_fasta(self._ctx, path.encode()))
+
+    def set_reference(self, name: str, bases: bytes):
+        self._check(self._lib.ngsep_set_reference(self._ctx, name.encode(), bases, len(bases)))
+
+    def sequence_names(self) -> List[str]:
+        n = self._lib.ngsep_n_sequences(self._ctx)
+        return [self._lib.ngsep_sequence_name(self._ctx, i).decode() for i in range(n)]
+
+    # -- alignments (AlignmentsPileupGenerator)
+    def processAlignments(self, batch: NgsepReadBatch):
+        self._check(self._lib.ngsep_process_alignments(self._ctx, ctypes.byref(batch)))
+
+    def notifyEndOfAlignments(self):
+        self._check(self._lib.ngsep_notify_end(self._ctx))
+
+    def processFile(self, bam_path: str, out_vcf: str):
+        """SingleSampleVariantsDetector.findSNVS on a BAM file, VCF written to out_vcf."""
+        self._check(self._lib.ngsep_call_bam(self._ctx, bam_path.encode(), out_vcf.encode()))
+
+    # -- staged runs (measurement)
+    def stage(self, batch: NgsepReadBatch):
+        self._check(self._lib.ngsep_stage_alignments(self._ctx, ctypes.byref(batch)))
+
+    def stage_finish(self):
+        self._check(self._lib.ngsep_stage_finish(self._ctx))
+
+    def run_staged(self) -> float:
+        ms = ctypes.c_double()
+        self._check(self._lib.ngsep_run_staged(self._ctx, ctypes.byref(ms)))
+        return ms.value
+
+    def release_staged(self):
+        self._check(self._lib.ngsep_release_staged(self._ctx))
+
+    # -- results
+    def raw_sites(self) -> Sequence[NgsepSiteOut]:
+        n = ctypes.c_int64()
+        self._check(self._lib.ngsep_fetch_sites(self._ctx, None, 0, ctypes.byref(n)))
+        arr = (NgsepSiteOut * max(n.value, 1))()
+        self._check(self._lib.ngsep_fetch_sites(self._ctx, arr, n.value, ctypes.byref(n)))
+        return arr[: n.value]
+
+    def getCalledVariants(self) -> List[CalledSite]:
+        names = self.sequence_names()
+        out = []
+        for s in self.raw_sites():
+            alleles = [chr(s.ref)]
+            if s.n_alleles >= 2:
+                alleles.append(BASES[s.alt])
+            if s.n_alleles == 3:
+                alleles.append(BASES[s.third])
+            out.append(CalledSite(
+                sequence=names[s.seq_id] if 0 <= s.seq_id < len(names) else "?", pos=s.pos, ref=chr(s.ref),
+                alleles=alleles, genotype=s.genotype, gq=s.gq, qual=s.qual, dp=s.dp, counts=list(s.counts),
+                strand_counts=[list(x) for x in s.strand_counts], logc=list(s.logc),
+                strand_bias=s.strand_bias, is_call=bool(s.is_call)))
+        return out
+
+    def clear(self):
+        self._check(self._lib.ngsep_clear_sites(self._ctx))
+
+    def format_site(self, s: NgsepSiteOut) -> str:
+        buf = ctypes.create_string_buffer(4096)
+        self._lib.ngsep_format_site(self._ctx, ctypes.byref(s), buf, 4096)
+        return buf.value.decode()
+
+    def write_vcf(self, path: str):
+        self._check(self._lib.ngsep_write_vcf_header(self._ctx, path.encode()))
+        self._check(self._lib.ngsep_append_vcf_records(self._ctx, path.encode()))
+
+    def stats(self) -> NgsepStats:
+        st = NgsepStats()
+        self._check(self._lib.ngsep_get_stats(self._ctx, ctypes.byref(st)))
+        return st
+
+
+class SingleSampleVariantsDetector:
+    """Drop-in for ngsep.discovery.SingleSampleVariantsDetector (SNV path).
+
+    Setter names follow the Java class; run() is SingleSampleVariantsDetector.run (:589-656)
+    restricted to findSNVS (the SV/CNV analyses are off by default and out of scope).
+    """
+
+    DEF_MIN_QUALITY = 40
+    DEF_MAX_BASE_QS = 30
+    DEF_MIN_MQ = 20
+    DEF_PLOIDY = 2
+    DEF_MAX_ALNS_PER_START_POS = 5
+    DEF_HETEROZYGOSITY_RATE_DIPLOID = 0.001
+
+    def __init__(self):
+        self.params = default_params()
+        self.inputFile: Optional[str] = None
+        self.genomeFile: Optional[str] = None
+        self.outputPrefix: Optional[str] = None
+        self.device = 0
+
+    # setters (CommandsDescriptor reflective setters)
+    def setInputFile(self, v: str): self.inputFile = v
+    def setGenome(self, v: str): self.genomeFile = v
+    def setOutputPrefix(self, v: str): self.outputPrefix = v
+    def setSampleId(self, v: str): self.params.sample_id = v.encode()
+    def setNormalPloidy(self, v: int): self.params.ploidy = int(v)
+    def setPrintSamplePloidy(self, v: bool): self.params.print_sample_ploidy = int(bool(v))
+    def setMinMQ(self, v: int): self.params.min_mq = int(v)
+    def setMaxAlnsPerStartPos(self, v: int): self.params.max_alns_per_start = int(v)
+    def setProcessNonUniquePrimaryAlignments(self, v: bool): self.params.process_nonunique = int(bool(v))
+    def setProcessSecondaryAlignments(self, v: bool): self.params.process_secondary = int(bool(v))
+    def setBasesToIgnore5P(self, v: int): self.params.ignore5 = int(v)
+    def setBasesToIgnore3P(self, v: int): self.params.ignore3 = int(v)
+    def setHeterozygosityRate(self, v: float):
+        self.params.het_rate = float(v)
+        self.params.het_rate_set = 1
+    def setMaxBaseQS(self, v: int): self.params.max_base_qs = int(v)
+    def setMinQuality(self, v: int): self.params.min_quality = int(v)
+    def setIgnoreLowerCaseRef(self, v: bool): self.params.ignore_lowercase_ref = int(bool(v))
+    def setCallEmbeddedSNVs(self, v: bool): self.params.call_embedded = int(bool(v))
+    def setCalcStrandBias(self, v: bool): self.params.calc_strand_bias = int(bool(v))
+    def setQuerySeq(self, v: str): self.params.query_seq = v.encode()
+    def setQueryFirst(self, v: int): self.params.query_first = int(v)
+    def setQueryLast(self, v: int): self.params.query_last = int(v)
+
+    _OPTIONS = {
+        "-i": ("setInputFile", str), "-r": ("setGenome", str), "-o": ("setOutputPrefix", str),
+        "-sampleId": ("setSampleId", str), "-ploidy": ("setNormalPloidy", int),
+        "-minMQ": ("setMinMQ", int), "-maxAlnsPerStartPos": ("setMaxAlnsPerStartPos", int),
+        "-ignore5": ("setBasesToIgnore5P", int), "-ignore3": ("setBasesToIgnore3P", int),
+        "-h": ("setHeterozygosityRate", float), "-maxBaseQS": ("setMaxBaseQS", int),
+        "-minQuality": ("setMinQuality", int), "-querySeq": ("setQuerySeq", str),
+        "-first": ("setQueryFirst", int), "-last": ("setQueryLast", int),
+    }
+    _FLAGS = {
+        "-psp": "setPrintSamplePloidy", "-p": "setProcessNonUniquePrimaryAlignments",
+        "-s": "setProcessSecondaryAlignments", "-ignoreLowerCaseRef": "setIgnoreLowerCaseRef",
+        "-embeddedSNVs": "setCallEmbeddedSNVs", "-csb": "setCalcStrandBias",
+    }
+
+    @classmethod
+    def main(cls, args: Sequence[str]) -> "SingleSampleVariantsDetector":
+        inst = cls()
+        i = 0
+        args = list(args)
+        while i < len(args):
+            a = args[i]
+            if a in cls._OPTIONS and i + 1 < len(args):
+                name, typ = cls._OPTIONS[a]
+                getattr(inst, name)(typ(args[i + 1]))
+                i += 2
+            elif a in cls._FLAGS:
+                getattr(inst, cls._FLAGS[a])(True)
+                i += 1
+            else:
+                raise ValueError(f"Unrecognized option {a}")
+        inst.run()
+        return inst
+
+    def run(self):
+        if self.inputFile is None:
+            raise NgsepError(_lib.NGSEP_E_IO, "The input file with alignments is a required parameter")
+        if self.genomeFile is None:
+            raise NgsepError(_lib.NGSEP_E_IO, "The reference genome file is a required parameter")
+        with GpuPileupSession(self.params, self.device) as s:
+            s.load_fasta(self.genomeFile)
+            s.processFile(self.inputFile, (self.outputPrefix or "variants") + ".vcf")
+            self.stats = s.stats()
