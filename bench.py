@@ -1,0 +1,213 @@
+"""bench.py -- genotyped reference positions/s of the MI355X SNV pileup path.
+
+Workload (BASELINE.json configs[1]): yeast whole genome (sacCer3 contig names/lengths,
+12,157,105 bp, synthetic bases) at 30x, 150 bp single-end synthetic reads, one sample.
+A step = one pass of the hot path over the whole genome with the read SoA already resident
+in HBM: k_tile_pileup (LDS-staged pileup tiles: candidate scan + tally) + k_posterior
+(SNVQ posterior/call of the undecided candidates) + D2H of the called sites
+(libngsep_amd.so, ngsep_run_staged).  N>1: one process per GPU, each rank owns its own
+synthetic genome (seed 2+rank) -- windows shard with no data-path collective ("weak").
+
+Prints one JSON line (rank 0).  --gpus N under torch.distributed.run for N>1.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "tools", "synth"), os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+METRIC = "genotyped ref positions/sec on 30x synthetic BAM; 1/2/4/8 GPU scaling"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(depth: float, seed: int, n_contigs: int):
+    """The oracle (single-thread C restatement of the reference) on a bounded sample of the same
+    workload: the first n_contigs yeast contigs at the same depth, SAM text -> VCF."""
+    import ngsep_oracle
+    import pysynth
+    syn = pysynth.Synth(genome=pysynth.YEAST, depth=depth, seed=seed, n_contigs=n_contigs)
+    names = [n for n, _ in syn.contigs()]
+    with tempfile.TemporaryDirectory() as d:
+        fa, sam, _ = syn.write(os.path.join(d, "cpu"))
+        st = ngsep_oracle.run_ssvd(fa, sam, os.path.join(d, "cpu.vcf"))
+    syn.close()
+    return {
+        "value": st.positions_genotyped / st.seconds,
+        "unit": "positions/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"oracle (C restatement, SAM->VCF incl. parsing) on yeast {names[0]}..{names[-1]} "
+                  f"({st.positions_genotyped} positions) at {depth:g}x, {st.seconds:.2f} s",
+    }
+
+
+def load_traffic(workload_key: str):
+    """Per-launch HBM bytes of k_tile_pileup from the committed PMC pass (profiles/), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if d.get("workload_key") != workload_key:
+        return None
+    return d.get("bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--depth", type=float, default=30.0)
+    ap.add_argument("--genome", default="yeast", choices=["yeast", "human_chr20"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-contigs", type=int, default=4)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group(backend="nccl")
+        dist = tdist
+
+    import pysynth
+    from ngsepcore_amd import GpuPileupSession, default_params
+
+    seed = 2 + rank
+    t0 = time.time()
+    if args.genome == "yeast":
+        syn = pysynth.Synth(genome=pysynth.YEAST, depth=args.depth, seed=seed)
+        workload = "yeast whole genome (sacCer3 names/lengths, 12,157,105 bp) 30x synthetic 150 bp SE"
+    else:
+        syn = pysynth.Synth(genome=pysynth.HUMAN, depth=args.depth, seed=3 + rank, contig_first=19, n_contigs=1)
+        workload = "human chr20 (64,444,167 bp) 30x synthetic 150 bp SE"
+    t_gen = time.time() - t0
+    params = default_params()
+    sess = GpuPileupSession(params, device=local_rank)
+    for name, seq in syn.contigs():
+        sess.set_reference(name, seq)
+    t1 = time.time()
+    sess.stage(syn.batch())
+    sess.stage_finish()
+    t_stage = time.time() - t1
+    n_reads_in = syn.n_reads
+    syn.close()
+    st = sess.stats()
+    positions = st.positions_genotyped
+    log(f"[rank {rank}] generated in {t_gen:.1f}s, staged {st.alignments_admitted} reads "
+        f"({st.read_bases} read bases, {st.slot_bytes} slot bytes) over {positions} positions in {t_stage:.1f}s")
+
+    def barrier():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        sess.run_staged()
+    barrier()
+    scan_ms, geno_ms, dev_ms = [], [], []
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        sess.run_staged()
+        s = sess.stats()
+        scan_ms.append(s.scan_ms)
+        geno_ms.append(s.genotype_ms)
+        dev_ms.append(s.kernel_ms)
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    st = sess.stats()
+    n_sites = st.sites_called
+    log(f"[rank {rank}] tile {st.tile_positions} positions (variant {st.tile_variant}), slot {st.slot_size} B, "
+        f"{st.candidates} candidates, {st.hard_sites} needed the posterior")
+    sess.release_staged()
+    sess.close()
+
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed, float(positions)], dtype=torch.float64, device="cuda")
+        mx = t.clone()
+        dist.all_reduce(mx[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed = float(mx[0])
+        total_positions = float(t[1])
+    else:
+        total_positions = float(positions)
+
+    if rank == 0:
+        steps = args.steps
+        value = total_positions * steps / elapsed
+        k_avg_ms = sum(scan_ms) / len(scan_ms)
+        # algorithmic bytes per k_tile_pileup launch: 1 B per projected read base,
+        # 1 B reference per genotyped position, 16 B read header per admitted read
+        alg_bytes = st.read_bases + positions + 16 * st.alignments_admitted
+        achieved = alg_bytes / (k_avg_ms * 1e-3) / 1e9
+        workload_key = f"{args.genome}:{args.depth:g}x:seed{seed}"
+        traffic = load_traffic(workload_key)
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "positions/s",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8,f64",
+            "data": "synthetic (seeded generator, SURVEY.md 8(d)); read SoA resident in HBM",
+            "config": {
+                "workload": workload,
+                "positions_per_gpu": positions,
+                "reads_per_gpu": int(st.alignments_admitted),
+                "read_bases_per_gpu": int(st.read_bases),
+                "sites_called_per_gpu": int(n_sites),
+                "candidates_per_gpu": int(st.candidates),
+                "parallelism": f"dp{world} (independent genomic windows per GPU, no collective)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_tile_pileup",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "alg_bytes_per_launch": alg_bytes,
+                "kernel_avg_ms": k_avg_ms,
+                "posterior_kernel_avg_ms": sum(geno_ms) / len(geno_ms),
+            },
+            "kernel_positions_per_s": total_positions / ((k_avg_ms + sum(geno_ms) / len(geno_ms)) * 1e-3),
+        }
+        if not args.no_cpu_baseline:
+            try:
+                line["cpu_baseline"] = cpu_baseline(args.depth, 2, args.cpu_contigs)
+            except Exception as e:  # the baseline is reported, never required
+                line["cpu_baseline"] = {"value": None, "error": str(e)}
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

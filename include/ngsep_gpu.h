@@ -115,9 +115,13 @@ typedef struct ngsep_stats {
     int64_t sites_called;
     int64_t read_bases;             /* projected read bytes resident in HBM */
     int64_t slot_bytes;             /* bytes of the slot array (incl. padding) */
-    double  kernel_ms;              /* device time of the last run (all kernels) */
-    double  scan_ms;                /* device time of K1 (candidate scan) */
-    double  genotype_ms;            /* device time of K2 */
+    double  kernel_ms;              /* host wall time of the last device run (kernels + D2H) */
+    double  scan_ms;                /* device time of k_tile_pileup (scan + tally) */
+    double  genotype_ms;            /* device time of the posterior kernel */
+    int32_t tile_positions;         /* positions per LDS pileup tile */
+    int32_t tile_variant;           /* 0 small-LDS tiles, 1 large-LDS tiles */
+    int32_t slot_size;              /* bytes per read slot in the SoA */
+    int32_t hard_sites;             /* candidates that needed the full posterior */
 } ngsep_stats;
 
 /* ---- context ---- */

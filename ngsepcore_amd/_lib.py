@@ -99,6 +99,10 @@ class NgsepStats(ctypes.Structure):
         ("kernel_ms", ctypes.c_double),
         ("scan_ms", ctypes.c_double),
         ("genotype_ms", ctypes.c_double),
+        ("tile_positions", ctypes.c_int32),
+        ("tile_variant", ctypes.c_int32),
+        ("slot_size", ctypes.c_int32),
+        ("hard_sites", ctypes.c_int32),
     ]
 
 

@@ -15,6 +15,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <chrono>
+#include <cstdlib>
 #include <fstream>
 
 namespace ngsep {
@@ -55,7 +57,8 @@ void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g) {
     g->max_q = mq > 0 ? mq : 30;
     g->min_quality = (int16_t)c->params.min_quality;
     g->dump_all = c->params.dump_all_positions;
-    g->pad = 0;
+    const char* ab = std::getenv("NGSEP_ABLATE");
+    g->ablate = ab ? std::atoi(ab) : 0;
 }
 
 // ReadAlignment.updateAlleleCallsInfo (ReadAlignment.java:747-834): allele-call length per read position.
@@ -360,7 +363,7 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
             wr.push_back({ci, w0, w1});
         }
     }
-    s.g_len = g + 64;
+    s.g_len = ((g + 64 + kTileMaxPos - 1) / kTileMaxPos) * kTileMaxPos;   // whole tiles, halo for 16-B reads
     if (s.g_len >= ((int64_t)1 << 31))
         return set_error(c, NGSEP_E_UNSUPPORTED, "staged genome exceeds 2^31 positions per device run; use window batching");
     // reads and slots
@@ -412,6 +415,29 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     s.n_slots = nslots;
     s.n_read_bases = nbases;
     for (const ContigReads& cr : contigs) s.covered += cr.covered;
+    // tile size: the largest T whose tiles (reads overlapping [t*T, (t+1)*T)) fit the LDS budget
+    // for >= 99.9% of tiles; the rest run the same kernel on global memory
+    {
+        std::vector<int32_t> gfirst(nreads);
+        for (int64_t i = 0; i < nreads; i++) gfirst[i] = s.h_reads[i * 4];
+        auto slot_of = [&](int64_t r) -> int64_t { return r < nreads ? s.h_reads[r * 4 + 2] : nslots; };
+        s.tile = 256;
+        s.tile_variant = 1;
+        bool found = false;
+        for (int v = 0; v < 2 && !found; v++) {
+            const TileBudget& tb = v == 0 ? kTileSmall : kTileLarge;
+            for (int T = tb.max_pos; T >= 256; T /= 2) {
+                int64_t ntiles = (s.g_len + T - 1) / T, over = 0;
+                for (int64_t t = 0; t < ntiles; t++) {
+                    int64_t lo = std::lower_bound(gfirst.begin(), gfirst.end(), (int32_t)(t * T - pad + 1)) - gfirst.begin();
+                    int64_t hi = std::lower_bound(gfirst.begin(), gfirst.end(), (int32_t)((t + 1) * T + 1)) - gfirst.begin();
+                    int64_t ns = slot_of(hi) - slot_of(lo);
+                    if (ns * S > tb.img_bytes || ns > tb.max_slots || hi - lo > tb.max_reads) over++;
+                }
+                if (over * 1000 <= ntiles) { s.tile = T; s.tile_variant = v; found = true; break; }
+            }
+        }
+    }
     // reference codes in global coordinates
     s.h_ref.assign((size_t)s.g_len, 0);
     for (const Window& w : s.windows) {
@@ -484,7 +510,7 @@ static double fisher_pvalue(std::vector<double>& lf, int a, int b, int c, int d)
     }
     return answer;
 }
-static void apply_strand_bias(std::vector<ngsep_site_out>& sites, size_t from) {
+static void apply_strand_bias(SiteStore& sites, size_t from) {
     std::vector<double> lf;
     for (size_t i = from; i < sites.size(); i++) {
         ngsep_site_out& s = sites[i];
@@ -499,31 +525,38 @@ int run_device(ngsep_ctx* c, double* elapsed_ms) {
     LikTables t;
     GenotypeParams gp;
     compute_tables(c, &t, &gp);
-    std::vector<ngsep_site_out> out;
+    int64_t n = 0;
     double scan_ms = 0, geno_ms = 0, total_ms = 0;
     int64_t ncand = 0;
     std::string err;
-    // exact pruning is proven for h <= 0.1 ("K1: why pruning is exact")
+    // exact pruning is proven for h <= 0.1 ("why pruning is exact")
     int prune = c->params.prune_candidates && !c->params.dump_all_positions && c->het_rate <= 0.1;
-    if (device_run(c->dev, c->staged, t, gp, prune, out, &scan_ms, &geno_ms, &total_ms, &ncand, err) != 0)
+    const size_t from = c->sites.size();
+    if (device_run(c->dev, c->staged, t, gp, prune, &c->sites, &n, &scan_ms, &geno_ms, &total_ms, &ncand, err) != 0)
         return set_error(c, NGSEP_E_DEVICE, err);
-    // windows are laid out in processing order, so global order == (sequence order, position)
-    std::sort(out.begin(), out.end(), [](const ngsep_site_out& a, const ngsep_site_out& b) { return a.pos < b.pos; });
+    // records arrive sorted by global position; windows are laid out in processing order, so this is
+    // (sequence order, position).  Map global coordinates back to (sequence, position) in place.
     const std::vector<Window>& ws = c->staged.windows;
-    size_t from = c->sites.size();
-    for (ngsep_site_out& o : out) {
-        int64_t gpos = o.pos;
-        auto it = std::upper_bound(ws.begin(), ws.end(), gpos, [](int64_t v, const Window& w) { return v < w.gbase; });
-        if (it == ws.begin()) continue;
-        const Window& w = *(it - 1);
-        int64_t off = gpos - w.gbase - w.pad;
+    size_t wi = 0, k = from;
+    for (int64_t i = 0; i < n; i++) {
+        ngsep_site_out& o = c->sites.buf[from + (size_t)i];
+        const int64_t gpos = o.pos;
+        while (wi + 1 < ws.size() && ws[wi + 1].gbase <= gpos) wi++;
+        const Window& w = ws[wi];
+        const int64_t off = gpos - w.gbase - w.pad;
         if (off < 0 || off >= w.wlen) continue;
         o.seq_id = w.seq_id;
         o.pos = (int32_t)(w.w0 + off);
-        c->sites.push_back(o);
+        if (k != from + (size_t)i) c->sites.buf[k] = o;
+        k++;
     }
+    c->sites.n = k;
     if (c->params.calc_strand_bias) apply_strand_bias(c->sites, from);
     c->stats.candidates = ncand;
+    c->stats.tile_positions = c->staged.tile;
+    c->stats.tile_variant = c->staged.tile_variant;
+    c->stats.slot_size = c->staged.slot_size;
+    c->stats.hard_sites = (int32_t)device_last_hard(c->dev);
     c->stats.sites_called += (int64_t)(c->sites.size() - from);
     c->stats.kernel_ms = total_ms;
     c->stats.scan_ms = scan_ms;

@@ -7,6 +7,7 @@
 #pragma once
 
 #include <cstdint>
+#include <cstring>
 #include <string>
 #include <vector>
 #include <mutex>
@@ -31,6 +32,14 @@ constexpr uint8_t kCodeValid = 0x80;
 constexpr uint8_t kRefInWindow = 0x01;
 constexpr uint8_t kRefCallable = 0x80;
 
+// pileup-tile kernel LDS budgets (kernels.hip k_tile_pileup).  Two variants: the small one
+// (~24 KB of LDS, 6 workgroups per CU) is used whenever the data's depth lets a tile of >= 256
+// positions fit; the large one (~48 KB, 3 per CU) otherwise.
+struct TileBudget { int img_bytes, max_reads, max_slots, max_pos; };
+constexpr TileBudget kTileSmall = {18 * 1024, 192, 192, 1024};
+constexpr TileBudget kTileLarge = {32 * 1024, 512, 1024, 2048};
+constexpr int kTileMaxPos = 2048;          // largest tile of any variant (positions)
+
 // K2 output record (device layout == ngsep_site_out, with gpos in .pos)
 static_assert(sizeof(ngsep_site_out) == 152, "site record layout");
 
@@ -48,7 +57,7 @@ struct GenotypeParams {
     int32_t max_q;             // effective -maxBaseQS cap
     int32_t min_quality;       // -minQuality
     int32_t dump_all;          // emit a record for every position with DP>0
-    int32_t pad;
+    int32_t ablate;            // diagnostics only (env NGSEP_ABLATE): 1 skip genotyping, 2 skip posterior
 };
 
 struct Window {            // a contiguous range of one sequence, resident in HBM
@@ -83,12 +92,47 @@ struct RawRead {
 
 struct Device;   // kernels.hip
 
+// pinned host memory (kernels.hip): the device copies results straight into it
+void* pinned_alloc(size_t bytes);
+void pinned_free(void* p);
+
+// Called-site list (SingleSampleVariantPileupListener.calledVariants).  Backed by pinned host
+// memory so the per-run D2H copy lands in place, without a staging copy.
+struct SiteStore {
+    ngsep_site_out* buf = nullptr;
+    size_t n = 0, cap = 0;
+    SiteStore() = default;
+    SiteStore(const SiteStore&) = delete;
+    SiteStore& operator=(const SiteStore&) = delete;
+    ~SiteStore() { if (buf) pinned_free(buf); }
+    size_t size() const { return n; }
+    bool empty() const { return n == 0; }
+    void clear() { n = 0; }
+    ngsep_site_out* data() { return buf; }
+    ngsep_site_out& operator[](size_t i) { return buf[i]; }
+    const ngsep_site_out* begin() const { return buf; }
+    const ngsep_site_out* end() const { return buf + n; }
+    void reserve(size_t want) {
+        if (want <= cap) return;
+        size_t nc = cap ? cap : 4096;
+        while (nc < want) nc *= 2;
+        auto* nb = static_cast<ngsep_site_out*>(pinned_alloc(nc * sizeof(ngsep_site_out)));
+        if (n) std::memcpy(nb, buf, n * sizeof(ngsep_site_out));
+        if (buf) pinned_free(buf);
+        buf = nb;
+        cap = nc;
+    }
+    void push_back(const ngsep_site_out& o) { reserve(n + 1); buf[n++] = o; }
+};
+
 struct Staged {            // everything resident for one run
     std::vector<Window> windows;
     int64_t g_len = 0;                  // global coordinate length
     int64_t n_reads = 0, n_slots = 0, n_read_bases = 0, covered = 0;
     int32_t slot_size = 0;
     int32_t max_span = 0;
+    int32_t tile = 1024;                // positions per pileup tile
+    int32_t tile_variant = 0;           // 0 = kTileSmall, 1 = kTileLarge
     // host mirrors (freed after upload)
     std::vector<uint8_t> h_slots;
     std::vector<int32_t> h_slot_pos;
@@ -120,7 +164,7 @@ struct ngsep_ctx {
     ngsep::Staged staged;
     ngsep::Device* dev = nullptr;
     // outputs
-    std::vector<ngsep_site_out> sites;
+    ngsep::SiteStore sites;
     ngsep_stats stats{};
 };
 
@@ -136,10 +180,12 @@ void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g);
 Device* device_create(int ordinal, std::string& err);
 void device_destroy(Device* d);
 int device_upload(Device* d, const Staged& s, std::string& err);
+// runs the tile + posterior kernels and copies the position-ordered records into out->buf[out->n ...]
 int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypeParams& g, int prune,
-               std::vector<ngsep_site_out>& out, double* scan_ms, double* geno_ms, double* total_ms,
+               SiteStore* out, int64_t* n_out, double* scan_ms, double* geno_ms, double* total_ms,
                int64_t* n_candidates, std::string& err);
 void device_release(Device* d);
+int64_t device_last_hard(const Device* d);
 int device_count();
 // vcf.cpp
 std::string format_header(const ngsep_ctx* c);

@@ -5,7 +5,9 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <cctype>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -406,6 +408,124 @@ extern "C" int ngs_synth_write_truth(const ngs_synth* s, const char* path) {
     std::fprintf(f, "##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tTRUTH\n");
     for (const Snv& v : s->truth)
         std::fprintf(f, "%s\t%d\t.\t%c\t%c\t.\t.\t.\tGT\t%s\n", s->names[v.contig].c_str(), v.pos, v.ref, v.alt, v.gt == 2 ? "1/1" : "0/1");
+    std::fclose(f);
+    return 0;
+}
+
+// ---- SAM text -> BAM (for hand-written fixtures under tests/golden) ----
+// Keeps the header text verbatim, all records in file order, and the aux tags of types
+// A/i/f/Z (integers written as 'i').  Test infrastructure only.
+extern "C" int ngs_sam_to_bam(const char* sam_path, const char* bam_path) {
+    FILE* in = std::fopen(sam_path, "r");
+    if (!in) return -1;
+    std::string header;
+    std::vector<std::string> names;
+    std::vector<int32_t> lens;
+    std::vector<std::string> lines;
+    char* line = nullptr;
+    size_t cap = 0;
+    ssize_t got;
+    while ((got = getline(&line, &cap, in)) > 0) {
+        std::string l(line, got);
+        while (!l.empty() && (l.back() == '\n' || l.back() == '\r')) l.pop_back();
+        if (l.empty()) continue;
+        if (l[0] == '@') {
+            header += l + "\n";
+            if (l.compare(0, 3, "@SQ") == 0) {
+                std::string sn;
+                int32_t ln = 0;
+                size_t p = 0;
+                while ((p = l.find('\t', p)) != std::string::npos) {
+                    ++p;
+                    if (l.compare(p, 3, "SN:") == 0) sn = l.substr(p + 3, l.find('\t', p) - p - 3);
+                    if (l.compare(p, 3, "LN:") == 0) ln = std::atoi(l.c_str() + p + 3);
+                }
+                names.push_back(sn);
+                lens.push_back(ln);
+            }
+        } else {
+            lines.push_back(l);
+        }
+    }
+    std::free(line);
+    std::fclose(in);
+    FILE* f = std::fopen(bam_path, "wb");
+    if (!f) return -1;
+    Bgzf z(f);
+    std::string b = "BAM\1";
+    put<int32_t>(b, (int32_t)header.size());
+    b += header;
+    put<int32_t>(b, (int32_t)names.size());
+    for (size_t c = 0; c < names.size(); c++) {
+        put<int32_t>(b, (int32_t)names[c].size() + 1);
+        b += names[c]; b.push_back(0);
+        put<int32_t>(b, lens[c]);
+    }
+    z.write(b.data(), b.size());
+    const char* nt16 = "=ACMGRSVTWYHKDBN";
+    const char* ops = "MIDNSHP=X";
+    for (const std::string& l : lines) {
+        std::vector<std::string> fl;
+        size_t p = 0, q;
+        while ((q = l.find('\t', p)) != std::string::npos) { fl.push_back(l.substr(p, q - p)); p = q + 1; }
+        fl.push_back(l.substr(p));
+        if (fl.size() < 11) { std::fclose(f); return -2; }
+        int32_t ref = -1;
+        for (size_t c = 0; c < names.size(); c++) if (names[c] == fl[2]) ref = (int32_t)c;
+        int32_t pos = std::atoi(fl[3].c_str()) - 1;
+        std::vector<uint32_t> cig;
+        int reflen = 0;
+        if (fl[5] != "*") {
+            int n = 0;
+            for (char ch : fl[5]) {
+                if (ch >= '0' && ch <= '9') { n = n * 10 + (ch - '0'); continue; }
+                const char* o = std::strchr(ops, ch);
+                if (!o) { std::fclose(f); return -2; }
+                int op = (int)(o - ops);
+                cig.push_back((uint32_t)n << 4 | (uint32_t)op);
+                if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) reflen += n;
+                n = 0;
+            }
+        }
+        std::string seq = fl[9] == "*" ? "" : fl[9];
+        std::string r;
+        put<int32_t>(r, ref);
+        put<int32_t>(r, pos);
+        put<uint8_t>(r, (uint8_t)(fl[0].size() + 1));
+        put<uint8_t>(r, (uint8_t)std::atoi(fl[4].c_str()));
+        put<uint16_t>(r, (uint16_t)reg2bin(pos < 0 ? 0 : pos, (pos < 0 ? 0 : pos) + (reflen ? reflen : 1)));
+        put<uint16_t>(r, (uint16_t)cig.size());
+        put<uint16_t>(r, (uint16_t)std::atoi(fl[1].c_str()));
+        put<int32_t>(r, (int32_t)seq.size());
+        put<int32_t>(r, -1);
+        put<int32_t>(r, -1);
+        put<int32_t>(r, 0);
+        r += fl[0]; r.push_back(0);
+        for (uint32_t v : cig) put<uint32_t>(r, v);
+        for (size_t i = 0; i < seq.size(); i += 2) {
+            const char* hi = std::strchr(nt16, std::toupper((unsigned char)seq[i]));
+            const char* lo = i + 1 < seq.size() ? std::strchr(nt16, std::toupper((unsigned char)seq[i + 1])) : nt16;
+            put<uint8_t>(r, (uint8_t)((hi ? hi - nt16 : 15) << 4 | (lo ? lo - nt16 : 15)));
+        }
+        for (size_t i = 0; i < seq.size(); i++)
+            put<uint8_t>(r, fl[10] == "*" ? 0xff : (uint8_t)(fl[10][i] - 33));
+        for (size_t t = 11; t < fl.size(); t++) {
+            const std::string& tg = fl[t];
+            if (tg.size() < 5) continue;
+            r += tg.substr(0, 2);
+            char ty = tg[3];
+            std::string v = tg.substr(5);
+            if (ty == 'i') { r.push_back('i'); put<int32_t>(r, std::atoi(v.c_str())); }
+            else if (ty == 'f') { r.push_back('f'); put<float>(r, std::strtof(v.c_str(), nullptr)); }
+            else if (ty == 'A') { r.push_back('A'); r.push_back(v.empty() ? ' ' : v[0]); }
+            else { r.push_back('Z'); r += v; r.push_back(0); }
+        }
+        std::string rec;
+        put<int32_t>(rec, (int32_t)r.size());
+        rec += r;
+        z.write(rec.data(), rec.size());
+    }
+    z.close();
     std::fclose(f);
     return 0;
 }

@@ -52,8 +52,16 @@ def lib():
         l.ngs_synth_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(NgsepReadBatch)]
         for f in ("ngs_synth_write_fasta", "ngs_synth_write_sam", "ngs_synth_write_bam", "ngs_synth_write_truth"):
             getattr(l, f).argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+        l.ngs_sam_to_bam.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
         _lib = l
     return _lib
+
+
+def sam_to_bam(sam: str, bam: str) -> str:
+    rc = lib().ngs_sam_to_bam(sam.encode(), bam.encode())
+    if rc != 0:
+        raise IOError(f"sam_to_bam failed ({rc}) for {sam}")
+    return bam
 
 
 class Synth:
