@@ -1,0 +1,106 @@
+"""Regenerates the committed golden fixtures (run in the build container, not on the GPU box).
+
+1. reference_demo_pl.csv.gz -- data extracted from the reference's own output file
+   training/yeastDemo_ann_q40_s_fi_I2_noREP_noCNV.vcf.gz (an NGSEP VCF, 2 samples): every
+   biallelic-SNV genotype field whose BSDP holds only REF/ALT base counts, as
+   (n_ref, n_alt, ref_idx, alt_idx, PL0, PL1, PL2, DP).  Needs /root/reference (read only).
+2. <case>.vcf / <case>.dump.gz -- outputs of the oracle (CPU restatement) on seeded synthetic
+   inputs (tools/synth), plus <case>.sam.md5 pinning the generator's output.  The GPU tests
+   compare the HIP path with these files without running the oracle.
+
+Usage: python tests/golden/make_golden.py [--no-reference]
+"""
+from __future__ import annotations
+
+import gzip
+import hashlib
+import os
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tools", "synth")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+REF_VCF = "/root/reference/training/yeastDemo_ann_q40_s_fi_I2_noREP_noCNV.vcf.gz"
+
+# name -> (synth kwargs, oracle option kwargs); kept small so the oracle runs in seconds
+CASES = {
+    "c1_chrI_10x": (dict(genome=0, n_contigs=1, depth=10, seed=1), {}),
+    "edge_2contigs_25x": (dict(genome=0, n_contigs=2, depth=25, seed=7, secondary_rate=0.01, lowmq_rate=0.01,
+                               noqual_rate=0.005, softclip_rate=0.05, dup_rate=0.02, lower_frac=0.01,
+                               quality_model=2, snv_rate=3e-3), {}),
+    "edge_2contigs_25x_csb_ploidy1": (dict(genome=0, n_contigs=2, depth=25, seed=7, secondary_rate=0.01,
+                                           lowmq_rate=0.01, noqual_rate=0.005, softclip_rate=0.05, dup_rate=0.02,
+                                           lower_frac=0.01, quality_model=2, snv_rate=3e-3),
+                                      {"calc_strand_bias": 1, "ploidy": 1, "min_quality": 20}),
+}
+DUMP_CASE = ("dump_custom8k_30x", dict(genome=2, custom_len=8000, depth=30, seed=5, noqual_rate=0.01,
+                                       softclip_rate=0.05, quality_model=2))
+
+
+def reference_fixture(out_path: str) -> int:
+    rows = []
+    with gzip.open(REF_VCF, "rt") as f:
+        for line in f:
+            if line.startswith("#"):
+                continue
+            fs = line.rstrip("\n").split("\t")
+            ref, alt = fs[3], fs[4]
+            if len(ref) != 1 or len(alt) != 1 or ref not in "ACGT" or alt not in "ACGT":
+                continue
+            fmt = fs[8].split(":")
+            ri, ai = "ACGT".index(ref), "ACGT".index(alt)
+            for s in fs[9:]:
+                d = dict(zip(fmt, s.split(":")))
+                if "BSDP" not in d or "PL" not in d or "DP" not in d:
+                    continue
+                b = [int(x) for x in d["BSDP"].split(",")]
+                if sum(b) != b[ri] + b[ai]:
+                    continue
+                pl = d["PL"].split(",")
+                rows.append(f"{b[ri]},{b[ai]},{ri},{ai},{pl[0]},{pl[1]},{pl[2]},{d['DP']}\n")
+    with gzip.GzipFile(out_path, "wb", mtime=0) as g:
+        g.write(b"n_ref,n_alt,ref_idx,alt_idx,pl_rr,pl_ra,pl_aa,dp\n")
+        g.write("".join(rows).encode())
+    return len(rows)
+
+
+def md5(path: str) -> str:
+    h = hashlib.md5()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def oracle_fixtures():
+    import ngsep_oracle
+    import pysynth
+    with tempfile.TemporaryDirectory() as d:
+        for name, (skw, opts) in CASES.items():
+            syn = pysynth.Synth(**skw)
+            fa, sam, _ = syn.write(os.path.join(d, name))
+            syn.close()
+            ngsep_oracle.run_ssvd(fa, sam, os.path.join(HERE, name + ".vcf"), **opts)
+            open(os.path.join(HERE, name + ".sam.md5"), "w").write(md5(sam) + "\n")
+            print(name, "ok")
+        name, skw = DUMP_CASE
+        syn = pysynth.Synth(**skw)
+        fa, sam, _ = syn.write(os.path.join(d, name))
+        syn.close()
+        dump = os.path.join(d, name + ".dump")
+        ngsep_oracle.run_ssvd(fa, sam, os.path.join(d, name + ".vcf"), dump)
+        with open(dump, "rb") as f, gzip.GzipFile(os.path.join(HERE, name + ".dump.gz"), "wb", mtime=0) as g:
+            g.write(f.read())
+        open(os.path.join(HERE, name + ".sam.md5"), "w").write(md5(sam) + "\n")
+        print(name, "ok")
+
+
+if __name__ == "__main__":
+    if "--no-reference" not in sys.argv:
+        n = reference_fixture(os.path.join(HERE, "reference_demo_pl.csv.gz"))
+        print("reference fixture rows:", n)
+    oracle_fixtures()

@@ -77,6 +77,51 @@ def test_every_position_tally_bitexact(tmp_path):
         assert tuple(x.logc) == logc, k   # bit-exact fp64
 
 
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _golden_cases():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+@pytest.mark.parametrize("name", ["c1_chrI_10x", "edge_2contigs_25x", "edge_2contigs_25x_csb_ploidy1"])
+def test_golden_vcf(tmp_path, name):
+    """HIP path vs the committed oracle VCFs (tests/golden), no oracle run needed."""
+    skw, opts = _golden_cases().CASES[name]
+    syn = pysynth.Synth(**skw)
+    fa, _, bam = syn.write(os.path.join(str(tmp_path), name))
+    syn.close()
+    g, _ = gpu_vcf_bam(tmp_path, fa, bam, **opts)
+    d = diff_vcf(os.path.join(GOLDEN, name + ".vcf"), g)
+    assert not d, "\n".join(d)
+
+
+def test_golden_dump_bitexact(tmp_path):
+    """DP, counts and the 10 fp64 log-conditionals at every covered position == committed dump."""
+    import gzip
+    name, skw = _golden_cases().DUMP_CASE
+    ref = {}
+    for l in gzip.open(os.path.join(GOLDEN, name + ".dump.gz"), "rt"):
+        f = l.rstrip("\n").split("\t")
+        ref[(f[0], int(f[1]))] = (int(f[3]), tuple(int(x) for x in f[4].split(",")), tuple(float(x) for x in f[5:15]))
+    syn = pysynth.Synth(**skw)
+    with GpuPileupSession(gpu_params(dump_all_positions=1)) as s:
+        for n, seq in syn.contigs():
+            s.set_reference(n, seq)
+        s.processAlignments(syn.batch())
+        s.notifyEndOfAlignments()
+        got = {(x.sequence, x.pos): x for x in s.getCalledVariants()}
+    syn.close()
+    assert len(got) == len(ref)
+    for k, (dp, counts, logc) in ref.items():
+        x = got[k]
+        assert (x.dp, tuple(x.counts), tuple(x.logc)) == (dp, counts, logc), k
+
+
 def test_pruning_is_exact(tmp_path):
     """K1's candidate pruning returns exactly the calls of genotyping every position."""
     syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=3, depth=30, seed=3, quality_model=2)
