@@ -137,8 +137,8 @@ def main():
     elapsed = time.perf_counter() - t_start
     st = sess.stats()
     n_sites = st.sites_called
-    log(f"[rank {rank}] tile {st.tile_positions} positions (variant {st.tile_variant}), slot {st.slot_size} B, "
-        f"{st.candidates} candidates, {st.hard_sites} needed the posterior")
+    log(f"[rank {rank}] tile {st.tile_positions} positions (max {st.tile_rows_max} rows), pile {st.pile_bytes} B, "
+        f"slot {st.slot_size} B, {st.candidates} candidates, {st.hard_sites} needed the exact tally + posterior")
     sess.release_staged()
     sess.close()
 
@@ -183,6 +183,9 @@ def main():
                 "read_bases_per_gpu": int(st.read_bases),
                 "sites_called_per_gpu": int(n_sites),
                 "candidates_per_gpu": int(st.candidates),
+                "exact_sites_per_gpu": int(st.hard_sites),
+                "pile_bytes_per_gpu": int(st.pile_bytes),
+                "tile_positions": int(st.tile_positions),
                 "parallelism": f"dp{world} (independent genomic windows per GPU, no collective)",
             },
             "roofline": {

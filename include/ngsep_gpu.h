@@ -118,10 +118,11 @@ typedef struct ngsep_stats {
     double  kernel_ms;              /* host wall time of the last device run (kernels + D2H) */
     double  scan_ms;                /* device time of k_tile_pileup (scan + tally) */
     double  genotype_ms;            /* device time of the posterior kernel */
-    int32_t tile_positions;         /* positions per LDS pileup tile */
-    int32_t tile_variant;           /* 0 small-LDS tiles, 1 large-LDS tiles */
-    int32_t slot_size;              /* bytes per read slot in the SoA */
-    int32_t hard_sites;             /* candidates that needed the full posterior */
+    int32_t tile_positions;         /* positions per pileup tile (T) */
+    int32_t tile_rows_max;          /* largest tile depth (rows of the tile-blocked pileup matrix) */
+    int32_t slot_size;              /* bytes per read slot of the read-major SoA */
+    int32_t hard_sites;             /* candidates that needed the exact tally + posterior */
+    int64_t pile_bytes;             /* bytes of the tile-blocked pileup matrix streamed by the scan */
 } ngsep_stats;
 
 /* ---- context ---- */

@@ -100,9 +100,10 @@ class NgsepStats(ctypes.Structure):
         ("scan_ms", ctypes.c_double),
         ("genotype_ms", ctypes.c_double),
         ("tile_positions", ctypes.c_int32),
-        ("tile_variant", ctypes.c_int32),
+        ("tile_rows_max", ctypes.c_int32),
         ("slot_size", ctypes.c_int32),
         ("hard_sites", ctypes.c_int32),
+        ("pile_bytes", ctypes.c_int64),
     ]
 
 

@@ -18,6 +18,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <fstream>
+#include <functional>
 
 namespace ngsep {
 
@@ -59,6 +60,25 @@ void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g) {
     g->dump_all = c->params.dump_all_positions;
     const char* ab = std::getenv("NGSEP_ABLATE");
     g->ablate = ab ? std::atoi(ab) : 0;
+    // Integer hom-ref bound.  Per valid call of quality q the differences
+    // L[r][r]-L[r][x] etc. take one of the four values below; floor/ceil make the integer sums
+    // lower bounds of the exact differences, so a position the bound proves hom-ref is hom-ref.
+    const double K = kBoundScale;
+    bool ok = true;
+    for (int q = 4; q <= 30; q++) {
+        const double rh = t->A[q] - t->H[q], re = t->A[q] - t->E[q], xh = t->H[q] - t->E[q];
+        if (!(rh >= 0 && re >= 0 && xh >= 0)) ok = false;
+        const unsigned long long wrh = (unsigned long long)std::floor(K * rh), wre = (unsigned long long)std::floor(K * re);
+        const unsigned long long wxh = (unsigned long long)std::ceil(K * xh), wxa = (unsigned long long)std::ceil(K * re);
+        t->wR[q] = wrh | (wre << 32);
+        t->wX[q] = wxh | (wxa << 32);
+    }
+    // 2 P(x,y) <= P(r,r) and P(x,x) <= P(r,r) for every other genotype keeps getIndexesMaxGenotype
+    // (VariantDiscoverySNVQAlgorithm.java:223-243) at ref/ref, which the listener drops (:223)
+    const double t_het = g->log_prior_hetero - g->log_prior_homo + std::log10(2.0);
+    t->t_het = (long long)std::floor(K * t_het) + kBoundMargin;
+    t->t_homo = kBoundMargin;
+    g->use_bound = ok && !g->dump_all && std::isfinite(t_het) ? 1 : 0;
 }
 
 // ReadAlignment.updateAlleleCallsInfo (ReadAlignment.java:747-834): allele-call length per read position.
@@ -328,6 +348,125 @@ static inline uint8_t ref_code(const ngsep_ctx* c, char ch) {
     return (uint8_t)(kRefCallable | (a << 5));
 }
 
+// ---- tile-blocked pileup matrix (engine.hpp TileInfo) ----
+// Tile size: every T in [kTileMinPos, kTileMaxPos] is costed as the bytes of its matrix
+// (sum over tiles of rows_t * T, rows_t = the tile's maximum depth) plus a fixed per-tile cost;
+// T must keep >= 99.9 % of tiles within the registers of one workgroup (the rest reload).
+static int choose_tile(const std::vector<int32_t>& cov_max16, int64_t g_len, std::vector<int32_t>& rows_out) {
+    std::vector<int32_t> cur = cov_max16;   // maxima over blocks of T positions, T = 16, 32, ...
+    int bestT = kTileMinPos;
+    double best_cost = -1;
+    std::vector<int32_t> best_rows;
+    const int64_t budget = (int64_t)kScanThreads * kUnitsPerThread;   // 16-byte units held in registers
+    for (int T = kTileMinPos; T <= kTileMaxPos; T *= 2) {
+        if (T > kTileMinPos) {
+            std::vector<int32_t> nxt((cur.size() + 1) / 2);
+            for (size_t i = 0; i < nxt.size(); i++)
+                nxt[i] = std::max(cur[2 * i], 2 * i + 1 < cur.size() ? cur[2 * i + 1] : 0);
+            cur.swap(nxt);
+        }
+        const int64_t ntiles = g_len / T;
+        int64_t over = 0;
+        double bytes = 0;
+        for (int64_t t = 0; t < ntiles; t++) {
+            bytes += (double)cur[t] * T;
+            if ((int64_t)cur[t] * (T / 16) > budget) over++;
+        }
+        if (over * 1000 > ntiles) continue;
+        const double cost = bytes + 2048.0 * (double)ntiles;
+        if (best_cost < 0 || cost < best_cost) { best_cost = cost; bestT = T; best_rows.assign(cur.begin(), cur.begin() + ntiles); }
+    }
+    if (best_cost < 0) {   // every T overflows the registers somewhere: smallest tiles, reload path
+        bestT = kTileMinPos;
+        best_rows.assign(cov_max16.begin(), cov_max16.begin() + g_len / kTileMinPos);
+    }
+    rows_out.swap(best_rows);
+    return bestT;
+}
+
+// Each tile's reads (clipped to the tile) are packed into rows by greedy interval colouring in
+// pending-list order: a read takes a row whose previous read ended before it starts, so rows_t
+// equals the maximum depth inside the tile.  Codes are stored allele-XOR-reference.
+static void build_pile(Staged& s) {
+    const int64_t g_len = s.g_len, nreads = s.n_reads;
+    const int32_t* R = s.h_reads.data();
+    // depth per position (difference array), then maxima over 16-position blocks
+    std::vector<int32_t> cov((size_t)g_len + 1, 0);
+    for (int64_t i = 0; i < nreads; i++) {
+        const int32_t a = R[i * 4], b = R[i * 4 + 1];
+        if (b < a) continue;
+        cov[a]++;
+        cov[(size_t)b + 1]--;
+    }
+    std::vector<int32_t> m16((size_t)(g_len / kTileMinPos), 0);
+    int32_t run = 0;
+    for (int64_t p = 0; p < g_len; p++) {
+        run += cov[p];
+        int32_t& m = m16[p / kTileMinPos];
+        if (run > m) m = run;
+    }
+    std::vector<int32_t>().swap(cov);
+    std::vector<int32_t> rows;
+    const int T = choose_tile(m16, g_len, rows);
+    const int64_t ntiles = g_len / T;
+    s.tile = T;
+    s.n_tiles = ntiles;
+    s.h_tinfo.resize((size_t)ntiles);
+    int64_t off = 0;
+    int32_t rmax = 0;
+    for (int64_t t = 0; t < ntiles; t++) {
+        s.h_tinfo[t].off = off;
+        s.h_tinfo[t].rows = rows[t];
+        s.h_tinfo[t].pad = 0;
+        off += (int64_t)rows[t] * T;
+        rmax = std::max(rmax, rows[t]);
+    }
+    s.pile_bytes = off;
+    s.tile_rows_max = rmax;
+    s.h_pile.assign((size_t)off, 0);
+    const int S = s.slot_size;
+    const uint8_t* slots = s.h_slots.data();
+    const uint8_t* ref = s.h_ref.data();
+    std::vector<std::pair<int32_t, int32_t>> heap;   // (last clipped position, row): min-heap
+    std::vector<int32_t> free_rows;
+    int64_t r_lo = 0;
+    for (int64_t t = 0; t < ntiles; t++) {
+        if (!rows[t]) continue;
+        const int32_t tstart = (int32_t)(t * T), tend = tstart + T;
+        while (r_lo < nreads && R[r_lo * 4] <= tstart - s.max_span) r_lo++;   // cannot reach this tile
+        heap.clear();
+        free_rows.clear();
+        int32_t next_row = 0;
+        uint8_t* blk = &s.h_pile[(size_t)s.h_tinfo[t].off];
+        for (int64_t r = r_lo; r < nreads && R[r * 4] < tend; r++) {
+            const int32_t gfirst = R[r * 4], glast = R[r * 4 + 1];
+            if (glast < tstart || glast < gfirst) continue;
+            const int32_t a = std::max(gfirst, tstart) - tstart, b = std::min(glast, tend - 1) - tstart;
+            while (!heap.empty() && heap.front().first < a) {
+                free_rows.push_back(heap.front().second);
+                std::pop_heap(heap.begin(), heap.end(), std::greater<>());
+                heap.pop_back();
+            }
+            int32_t row;
+            if (!free_rows.empty()) { row = free_rows.back(); free_rows.pop_back(); }
+            else row = next_row++;
+            heap.push_back({b, row});
+            std::push_heap(heap.begin(), heap.end(), std::greater<>());
+            const uint8_t* src = slots + (size_t)R[r * 4 + 2] * S + (tstart + a - gfirst);
+            uint8_t* dst = blk + (size_t)row * T;
+            for (int32_t p = a; p <= b; p++) {
+                uint8_t cd = src[p - a];
+                if (cd & kCodeValid) {
+                    const uint8_t rc = ref[tstart + p];
+                    const uint8_t ra = (rc & kRefCallable) ? (uint8_t)((rc >> 5) & 3) : 0;
+                    cd = (uint8_t)((cd & 0x9F) | ((((cd >> 5) & 3) ^ ra) << 5));
+                }
+                dst[p] = cd;
+            }
+        }
+    }
+}
+
 int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     Staged& s = c->staged;
     s = Staged();
@@ -366,9 +505,8 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     s.g_len = ((g + 64 + kTileMaxPos - 1) / kTileMaxPos) * kTileMaxPos;   // whole tiles, halo for 16-B reads
     if (s.g_len >= ((int64_t)1 << 31))
         return set_error(c, NGSEP_E_UNSUPPORTED, "staged genome exceeds 2^31 positions per device run; use window batching");
-    // reads and slots
+    // reads and slots (read-major SoA: the exact tally of queued candidates walks it in pending order)
     s.h_reads.clear();
-    s.h_slot_pos.clear();
     s.h_slots.clear();
     int64_t nslots = 0, nreads = 0, nbases = 0;
     std::vector<std::pair<int64_t, int64_t>> ranges(s.windows.size());
@@ -387,7 +525,6 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
         nreads += b - a;
     }
     s.h_slots.assign((size_t)nslots * S, 0);
-    s.h_slot_pos.resize(nslots);
     s.h_reads.resize((size_t)nreads * 4);
     int64_t slot = 0, ri = 0;
     for (size_t wi = 0; wi < s.windows.size(); wi++) {
@@ -404,7 +541,6 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
             s.h_reads[ri * 4 + 2] = (int32_t)slot;
             s.h_reads[ri * 4 + 3] = cr.neg[i];
             if (span > 0) std::memcpy(&s.h_slots[(size_t)slot * S], &cr.bytes[cr.boff[i]], (size_t)span);
-            for (int64_t k = 0; k < ns; k++) s.h_slot_pos[slot + k] = (int32_t)(gfirst + k * S);
             slot += ns;
             nbases += span > 0 ? span : 0;
             ri++;
@@ -415,29 +551,6 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     s.n_slots = nslots;
     s.n_read_bases = nbases;
     for (const ContigReads& cr : contigs) s.covered += cr.covered;
-    // tile size: the largest T whose tiles (reads overlapping [t*T, (t+1)*T)) fit the LDS budget
-    // for >= 99.9% of tiles; the rest run the same kernel on global memory
-    {
-        std::vector<int32_t> gfirst(nreads);
-        for (int64_t i = 0; i < nreads; i++) gfirst[i] = s.h_reads[i * 4];
-        auto slot_of = [&](int64_t r) -> int64_t { return r < nreads ? s.h_reads[r * 4 + 2] : nslots; };
-        s.tile = 256;
-        s.tile_variant = 1;
-        bool found = false;
-        for (int v = 0; v < 2 && !found; v++) {
-            const TileBudget& tb = v == 0 ? kTileSmall : kTileLarge;
-            for (int T = tb.max_pos; T >= 256; T /= 2) {
-                int64_t ntiles = (s.g_len + T - 1) / T, over = 0;
-                for (int64_t t = 0; t < ntiles; t++) {
-                    int64_t lo = std::lower_bound(gfirst.begin(), gfirst.end(), (int32_t)(t * T - pad + 1)) - gfirst.begin();
-                    int64_t hi = std::lower_bound(gfirst.begin(), gfirst.end(), (int32_t)((t + 1) * T + 1)) - gfirst.begin();
-                    int64_t ns = slot_of(hi) - slot_of(lo);
-                    if (ns * S > tb.img_bytes || ns > tb.max_slots || hi - lo > tb.max_reads) over++;
-                }
-                if (over * 1000 <= ntiles) { s.tile = T; s.tile_variant = v; found = true; break; }
-            }
-        }
-    }
     // reference codes in global coordinates
     s.h_ref.assign((size_t)s.g_len, 0);
     for (const Window& w : s.windows) {
@@ -445,8 +558,13 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
         uint8_t* dst = &s.h_ref[(size_t)(w.gbase + w.pad)];
         for (int32_t k = 0; k < w.wlen; k++) dst[k] = ref_code(c, ref[(size_t)w.w0 - 1 + k]);
     }
+    build_pile(s);
     c->stats.read_bases = nbases;
     c->stats.slot_bytes = nslots * S;
+    c->stats.pile_bytes = s.pile_bytes;
+    c->stats.tile_positions = s.tile;
+    c->stats.tile_rows_max = s.tile_rows_max;
+    c->stats.slot_size = S;
     if (!c->dev) {
         std::string err;
         c->dev = device_create(c->device, err);
@@ -456,9 +574,10 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     if (device_upload(c->dev, s, err) != 0) return set_error(c, NGSEP_E_DEVICE, err);
     // host mirrors are not needed any more
     std::vector<uint8_t>().swap(s.h_slots);
-    std::vector<int32_t>().swap(s.h_slot_pos);
     std::vector<int32_t>().swap(s.h_reads);
     std::vector<uint8_t>().swap(s.h_ref);
+    std::vector<uint8_t>().swap(s.h_pile);
+    std::vector<TileInfo>().swap(s.h_tinfo);
     return NGSEP_OK;
 }
 
@@ -553,9 +672,6 @@ int run_device(ngsep_ctx* c, double* elapsed_ms) {
     c->sites.n = k;
     if (c->params.calc_strand_bias) apply_strand_bias(c->sites, from);
     c->stats.candidates = ncand;
-    c->stats.tile_positions = c->staged.tile;
-    c->stats.tile_variant = c->staged.tile_variant;
-    c->stats.slot_size = c->staged.slot_size;
     c->stats.hard_sites = (int32_t)device_last_hard(c->dev);
     c->stats.sites_called += (int64_t)(c->sites.size() - from);
     c->stats.kernel_ms = total_ms;

@@ -32,13 +32,22 @@ constexpr uint8_t kCodeValid = 0x80;
 constexpr uint8_t kRefInWindow = 0x01;
 constexpr uint8_t kRefCallable = 0x80;
 
-// pileup-tile kernel LDS budgets (kernels.hip k_tile_pileup).  Two variants: the small one
-// (~24 KB of LDS, 6 workgroups per CU) is used whenever the data's depth lets a tile of >= 256
-// positions fit; the large one (~48 KB, 3 per CU) otherwise.
-struct TileBudget { int img_bytes, max_reads, max_slots, max_pos; };
-constexpr TileBudget kTileSmall = {18 * 1024, 192, 192, 1024};
-constexpr TileBudget kTileLarge = {32 * 1024, 512, 1024, 2048};
-constexpr int kTileMaxPos = 2048;          // largest tile of any variant (positions)
+// Tile-blocked pileup matrix ("pile"), the layout the scan kernel streams:
+// the positions are cut into tiles of T (power of two) positions; tile t stores rows_t x T code
+// bytes, row-major, where every row holds non-overlapping reads clipped to the tile (greedy
+// interval colouring, rows_t = the tile's maximum depth).  Codes are stored with the allele
+// XOR-ed with the reference allele, so a valid non-reference call is a valid byte with nonzero
+// allele bits and the scan needs no reference lookup.
+struct TileInfo {
+    int64_t off;     // byte offset of the tile's block in the pile (16-B aligned)
+    int32_t rows;    // rows_t (0 = no reads overlap the tile)
+    int32_t pad;
+};
+static_assert(sizeof(TileInfo) == 16, "TileInfo layout");
+constexpr int kScanThreads = 256;          // threads per tile workgroup
+constexpr int kUnitsPerThread = 8;         // 16-byte units a thread keeps in registers
+constexpr int kTileMaxPos = 2048;          // largest tile (positions)
+constexpr int kTileMinPos = 16;
 
 // K2 output record (device layout == ngsep_site_out, with gpos in .pos)
 static_assert(sizeof(ngsep_site_out) == 152, "site record layout");
@@ -49,7 +58,16 @@ struct LikTables {
     double A[32];   // log10(1-e)                     logProbCacheGT[f][q][0]
     double H[32];   // log10(0.5(1-e)+0.5 e/3)        logProbCacheGT[250][q][4]
     double E[32];   // -0.1 q - log10(3)              logProbCacheError[q][4]
+    // Integer hom-ref bound (DESIGN.md "hom-ref bound"), fixed point with kBoundScale units:
+    //   wR[q] = floor(K(A-H)) | floor(K(A-E)) << 32   added once per reference-allele call
+    //   wX[q] =  ceil(K(H-E)) |  ceil(K(A-E)) << 32   added once per call of a non-reference allele
+    unsigned long long wR[32];
+    unsigned long long wX[32];
+    long long t_het;      // floor(K (log10 h/12 - log10 (1-h)/4 + log10 2)) + margin
+    long long t_homo;     // margin
 };
+constexpr double kBoundScale = 1048576.0;   // 2^20: a tile holds <= 512 reads -> sums < 2^31
+constexpr long long kBoundMargin = 64;      // 6e-5 in log10 units, >> fp64 rounding of the sums
 
 struct GenotypeParams {
     double log_prior_homo;     // log10((1-h)/4), CountsHelper.java:416
@@ -57,7 +75,8 @@ struct GenotypeParams {
     int32_t max_q;             // effective -maxBaseQS cap
     int32_t min_quality;       // -minQuality
     int32_t dump_all;          // emit a record for every position with DP>0
-    int32_t ablate;            // diagnostics only (env NGSEP_ABLATE): 1 skip genotyping, 2 skip posterior
+    int32_t ablate;            // diagnostics only (env NGSEP_ABLATE): 1 scan only (no bound, no queue)
+    int32_t use_bound;         // 1: candidates proven hom-ref by the integer bound are dropped in the tile kernel
 };
 
 struct Window {            // a contiguous range of one sequence, resident in HBM
@@ -131,11 +150,14 @@ struct Staged {            // everything resident for one run
     int64_t n_reads = 0, n_slots = 0, n_read_bases = 0, covered = 0;
     int32_t slot_size = 0;
     int32_t max_span = 0;
-    int32_t tile = 1024;                // positions per pileup tile
-    int32_t tile_variant = 0;           // 0 = kTileSmall, 1 = kTileLarge
+    int32_t tile = 512;                 // positions per pileup tile (T)
+    int32_t tile_rows_max = 0;          // largest rows_t
+    int64_t n_tiles = 0;
+    int64_t pile_bytes = 0;
     // host mirrors (freed after upload)
     std::vector<uint8_t> h_slots;
-    std::vector<int32_t> h_slot_pos;
+    std::vector<uint8_t> h_pile;
+    std::vector<TileInfo> h_tinfo;
     std::vector<int32_t> h_reads;       // 4 ints per read: gfirst, glast, slot, flags
     std::vector<uint8_t> h_ref;
 };

@@ -1,20 +1,21 @@
 // kernels.hip -- gfx950 kernels of the NGSEP SNV pileup path.
 //
 //   KT  k_tile_pileup : one workgroup per tile of T reference positions (global coordinates).
-//        phase 1  stream the tile's read slots HBM -> VGPR -> LDS (16 B per lane, coalesced; the
-//                 slots of the reads overlapping a tile are one contiguous range) and, on the way,
-//                 compare every projected read byte with the reference code of its position:
-//                 a position whose pileup holds a valid non-reference call becomes a candidate
-//                 (LDS bitmap).  This is AlignmentsPileupGenerator.processCurrentPosition
-//                 (discovery/AlignmentsPileupGenerator.java:475-498) reduced to the fact that decides
-//                 whether SNVQ can call a variant there ("why pruning is exact").
-//        phase 2  genotype each candidate from LDS: CountsHelper.calculateCountsSNV/updateCounts
-//                 (discovery/CountsHelper.java:83-95,209-251) over the reads in pending-list order
-//                 (bit-exact fp64 sums), getPosteriorProbabilities (:410-495) and
-//                 VariantDiscoverySNVQAlgorithm.discoverSNV (:100-243) + the listener filters
-//                 (SingleSampleVariantPileupListener.java:213-232).
-//        Tiles whose reads do not fit the LDS budget run the same two phases on global memory.
+//        phase 1  stage the tile's read slots HBM -> LDS (global_load_lds, 16 B per lane; the slots
+//                 of the reads overlapping a tile are one contiguous range) and compare every
+//                 projected read byte with the reference code of its position: a position whose
+//                 pileup holds a valid non-reference call becomes a candidate (LDS bitmap).  This is
+//                 AlignmentsPileupGenerator.processCurrentPosition (discovery/AlignmentsPileupGenerator.java:475-498)
+//                 reduced to the fact that decides whether SNVQ can call a variant there
+//                 ("why pruning is exact").
+//        phase 2  integer hom-ref bound of every candidate (order-independent LDS atomics).
+//        phase 3  drop the candidates the bound proves hom-ref, queue the rest.
+//        Tiles whose reads do not fit the LDS budget scan from global memory and queue every candidate.
+//   KP  k_posterior : exact CountsHelper tally (pending-list order, bit-exact fp64), posterior and
+//                 SNVQ call of the queued candidates (discovery/CountsHelper.java:83-95,209-251,410-495,
+//                 VariantDiscoverySNVQAlgorithm.java:100-243, SingleSampleVariantPileupListener.java:213-232).
 //   KL  kl_read_index : per 64-position block, first read that can cover it (binary search).
+//   KO  ko_* : position order of the emitted records.
 //
 // HBM-bound integer/byte work: no MFMA.  Layout and roofline: DESIGN.md.
 #include <hip/hip_runtime.h>
@@ -41,32 +42,33 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         }                                                                              \
     } while (0)
 
-struct HardSite;
+struct QueueSite;
 
 struct Device {
     int ordinal = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {};
     uint8_t* d_slots = nullptr;
-    int32_t* d_slot_pos = nullptr;
+    uint8_t* d_pile = nullptr;
     int4* d_reads = nullptr;
     uint8_t* d_ref = nullptr;
     int32_t* d_lb = nullptr;
-    int4* d_tiles = nullptr;
+    TileInfo* d_tinfo = nullptr;
     LikTables* d_tables = nullptr;
     ngsep_site_out* d_sites = nullptr;
     ngsep_site_out* d_sorted = nullptr;
     int32_t* d_bucket = nullptr;     // counts, then starts (nb+1), then cursors (nb)
     int64_t nb_cap = 0;
-    HardSite* d_hard = nullptr;
+    QueueSite* d_hard = nullptr;
     int64_t cap_hard = 0;
     unsigned long long* d_counters = nullptr;
     unsigned long long* h_counters = nullptr;
     int64_t cap_sites = 0;
     int64_t n_units = 0, n_slots = 0, n_lb = 0, n_reads = 0, g_len = 0, n_tiles = 0;
-    int32_t slot_size = 0, max_span = 0, pad = 0, tile = 1024, tile_variant = 0;
+    int32_t slot_size = 0, max_span = 0, pad = 0, tile = 512, log2_tile = 9;
     int64_t last_n_sites = 1024;
     int64_t last_hard = 0;
+    int32_t n_cu = 256;
 };
 
 // ------------------------------------------------------------------------------------------
@@ -85,158 +87,105 @@ __device__ inline int16_t phred_d(double p) {
     return (int16_t)java_round_d(score);
 }
 
-// 16 bytes starting at byte offset o (o >= 0) of a dword-aligned byte array
-__device__ inline void load16(const uint8_t* base, int64_t o, uint32_t R[4]) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(base) + (o >> 2);
-    const uint32_t sh = (uint32_t)(o & 3);
-    const uint32_t r0 = w[0], r1 = w[1], r2 = w[2], r3 = w[3], r4 = w[4];
-    R[0] = __builtin_amdgcn_alignbyte(r1, r0, sh);
-    R[1] = __builtin_amdgcn_alignbyte(r2, r1, sh);
-    R[2] = __builtin_amdgcn_alignbyte(r3, r2, sh);
-    R[3] = __builtin_amdgcn_alignbyte(r4, r3, sh);
+// bit 7 of the four bytes of a dword -> 4 bits
+__device__ inline uint32_t nib4(uint32_t w) {
+    const uint32_t c = w & 0x80808080u;
+    return ((c >> 7) & 1u) | ((c >> 14) & 2u) | ((c >> 21) & 4u) | ((c >> 28) & 8u);
+}
+// bit k set <=> byte k of a 16-byte unit has bit 7 (a valid call)
+__device__ inline uint32_t unit_valid_mask(const u32x4 d) {
+    return nib4(d.x) | (nib4(d.y) << 4) | (nib4(d.z) << 8) | (nib4(d.w) << 12);
+}
+// byte k (0..15) of a 16-byte unit
+__device__ inline uint32_t unit_byte(const u32x4 d, int k) {
+    const uint32_t w = k < 8 ? (k < 4 ? d.x : d.y) : (k < 12 ? d.z : d.w);
+    return (w >> (8 * (k & 3))) & 0xFFu;
 }
 
-// candidate bits of one 16-byte unit: bit i set <=> byte i is a valid call (code bit 7) whose
-// allele differs from a callable reference base (MODE 0), or any counted call at an
-// in-window position (MODE 1: genotype every position)
-template <int MODE>
-__device__ inline uint32_t unit_candidates(const uint32_t D[4], const uint32_t R[4]) {
-    uint32_t mask = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        uint32_t c;
-        if (MODE == 0) {
-            const uint32_t diff = ((D[k] ^ R[k]) & 0x60606060u) + 0x60606060u;
-            c = D[k] & R[k] & diff & 0x80808080u;
-        } else {
-            const uint32_t nzd = (((D[k] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | D[k]) & 0x80808080u;
-            const uint32_t nzr = (((R[k] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | R[k]) & 0x80808080u;
-            c = nzd & nzr;
-        }
-        mask |= (((c >> 7) & 1u) | ((c >> 14) & 2u) | ((c >> 21) & 4u) | ((c >> 28) & 8u)) << (4 * k);
-    }
-    return mask;
-}
-
-// A candidate whose call needs the full posterior (queued by the tile kernel for k_posterior)
-struct HardSite {
-    double L[10];          // log-conditionals, upper triangle 00 01 02 03 11 12 13 22 23 33
-    int32_t gpos, total;
-    int32_t c[4];
-    int32_t r_begin;       // first read that can cover gpos (global read index)
+// A candidate the tile kernel could not prove hom-ref; k_posterior genotypes it exactly
+struct QueueSite {
+    int32_t gpos;          // global position
     int32_t rc;            // reference code
 };
-static_assert(sizeof(HardSite) == 112, "HardSite layout");
+static_assert(sizeof(QueueSite) == 8, "QueueSite layout");
 
-// Tally one candidate over the reads in pending-list order (CountsHelper.calculateCountsSNV /
-// updateCounts, discovery/CountsHelper.java:83-95,209-251: bit-exact fp64 sums), then decide
-// whether the call can be settled without the posterior: the exact hom-ref shortcut drops the
-// position (SingleSampleVariantPileupListener.java:223); anything else is queued for k_posterior.
-// STAGED: headers/image/tables in LDS (32-bit offsets); otherwise global memory.
-template <bool STAGED>
-__device__ void tally_position(int32_t gpos, uint8_t rc, int32_t r_begin, int32_t r_end,
-                               const int4* __restrict__ hdr, int32_t hdr_base,
-                               const uint8_t* __restrict__ img, int32_t img_slot0, int32_t S,
-                               const double* __restrict__ TA, const double* __restrict__ TH,
-                               const double* __restrict__ TE, const GenotypeParams& gp,
-                               HardSite* __restrict__ queue, unsigned long long* counters, int64_t qcap) {
-    int32_t total = 0;
-    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-    double L00 = 0, L01 = 0, L02 = 0, L03 = 0, L11 = 0, L12 = 0, L13 = 0, L22 = 0, L23 = 0, L33 = 0;
-    // reads [r_begin, r_end) all have gfirst <= gpos (r_end is the upper bound); batches of 4 issue
-    // every LDS load of the batch before the in-order accumulation
-    for (int32_t r0 = r_begin; r0 < r_end; r0 += 4) {
-        uint8_t code[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int32_t r = r0 + k < r_end ? r0 + k : r_end - 1;
-            const int4 h = hdr[r - hdr_base];   // gfirst, glast, slot, flags
-            const int32_t off = gpos - h.x;
-            const int32_t sidx = off >= S ? off / S : 0;
-            uint8_t cd;
-            if (STAGED) cd = img[(h.z + sidx - img_slot0) * S + (off - sidx * S)];
-            else cd = img[(int64_t)(h.z + sidx) * S + (off - sidx * S)];
-            code[k] = (r0 + k < r_end && h.y >= gpos) ? cd : 0;   // read must cover gpos
-        }
-        double tA[4], tH[4], tE[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            int q = code[k] & 31;
-            q = q > gp.max_q ? gp.max_q : q;
-            tA[k] = TA[q];
-            tH[k] = TH[q];
-            tE[k] = TE[q];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint8_t cd = code[k];
-            total += cd != 0;                       // CountsHelper.java:210 (no call -> not counted)
-            if (!(cd & 0x80)) continue;             // q<=3 or not A/C/G/T (:214-221)
-            const uint32_t a = (cd >> 5) & 3;
-            c0 += a == 0; c1 += a == 1; c2 += a == 2; c3 += a == 3;
-            const double A = tA[k], H = tH[k], E = tE[k];   // q clamped to -maxBaseQS (:217-219) above
-            // updateCounts (:231-248) with f == g: the [i][j] and [j][i] sums are identical sequences
-            L00 += a == 0 ? A : E;
-            L11 += a == 1 ? A : E;
-            L22 += a == 2 ? A : E;
-            L33 += a == 3 ? A : E;
-            L01 += a <= 1 ? H : E;
-            L02 += (a & 1) == 0 ? H : E;
-            L03 += (a == 0 || a == 3) ? H : E;
-            L12 += (a == 1 || a == 2) ? H : E;
-            L13 += (a & 1) == 1 ? H : E;
-            L23 += a >= 2 ? H : E;
-        }
-    }
-    if (total == 0) return;                     // VariantDiscoverySNVQAlgorithm.java:101-103
-    if (gp.ablate & 2) {                        // diagnostics: keep the tally live, skip the posterior
-        if (L00 + L11 + L22 + L33 + L01 + L02 + L03 + L12 + L13 + L23 == 1.0) atomicAdd(&counters[0], 1ull);
-        return;
-    }
-    if ((rc & 0x80) && !gp.dump_all) {
-        // Exact shortcut (DESIGN.md "hom-ref shortcut"): with m the largest event, every genotype
-        // other than ref/ref has posterior <= 2*10^(ev-m) (CountsHelper.java:472-495 divides by a
-        // total >= 1).  If that is < 0.01 for all of them, none can beat P(ref/ref)+0.01 in
-        // getIndexesMaxGenotype (VariantDiscoverySNVQAlgorithm.java:223-243): hom-ref, dropped.
-        const int ri = (rc >> 5) & 3;
-        const double ph = gp.log_prior_homo, px = gp.log_prior_hetero;
-        const double d00 = L00 + ph, d11 = L11 + ph, d22 = L22 + ph, d33 = L33 + ph;
-        const double h01 = L01 + px, h02 = L02 + px, h03 = L03 + px, h12 = L12 + px, h13 = L13 + px, h23 = L23 + px;
-        const double m = fmax(fmax(fmax(d00, d11), fmax(d22, d33)), fmax(fmax(fmax(h01, h02), fmax(h03, h12)), fmax(h13, h23)));
-        const double lim = m - 2.4;
-        const double others = fmax(fmax(fmax(h01, h02), fmax(h03, h12)), fmax(h13, h23));
-        const double homo_other = fmax(fmax(ri == 0 ? -INFINITY : d00, ri == 1 ? -INFINITY : d11),
-                                       fmax(ri == 2 ? -INFINITY : d22, ri == 3 ? -INFINITY : d33));
-        if (others < lim && homo_other < lim) return;
-    }
-    const unsigned long long qi = atomicAdd(&counters[2], 1ull);
-    if ((int64_t)qi >= qcap) return;            // host re-runs with a larger queue
-    HardSite hs;
-    hs.L[0] = L00; hs.L[1] = L01; hs.L[2] = L02; hs.L[3] = L03; hs.L[4] = L11;
-    hs.L[5] = L12; hs.L[6] = L13; hs.L[7] = L22; hs.L[8] = L23; hs.L[9] = L33;
-    hs.gpos = gpos;
-    hs.total = total;
-    hs.c[0] = (int32_t)c0; hs.c[1] = (int32_t)c1; hs.c[2] = (int32_t)c2; hs.c[3] = (int32_t)c3;
-    hs.r_begin = r_begin;
-    hs.rc = rc;
-    queue[qi] = hs;
-}
+constexpr int kCandCap = 256;   // candidates per tile with integer-bound accumulators in LDS
+constexpr int kTileBlocksPerCU = 4;
+constexpr int kQueueStage = 1024;    // survivors staged in LDS per tile-scan block   // persistent tile-scan blocks per CU (register-limited occupancy)
 
 // ------------------------------------------------------------------------------------------
-// KP: posterior + SNVQ call for queued candidates (thread per site)
+// KP: exact tally + posterior + SNVQ call of the queued candidates (thread per site)
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_posterior(const HardSite* __restrict__ queue, const unsigned long long* qn,
+// CountsHelper.calculateCountsSNV/updateCounts (discovery/CountsHelper.java:83-95,209-251) over the
+// reads covering gpos in pending-list order (the order of the read table), so the fp64 sums are
+// bit-identical to the reference's; then getPosteriorProbabilities (:410-495),
+// VariantDiscoverySNVQAlgorithm.discoverSNV (:100-243) and the listener filters
+// (SingleSampleVariantPileupListener.java:213-232).
+__global__ __launch_bounds__(256) void k_posterior(const QueueSite* __restrict__ queue, const unsigned long long* qn,
                                                    int64_t qcap, const int4* __restrict__ reads, int64_t n_reads,
-                                                   const uint8_t* __restrict__ slots, int32_t S, GenotypeParams gp,
+                                                   const int32_t* __restrict__ lb, const uint8_t* __restrict__ slots,
+                                                   int32_t S, const LikTables* __restrict__ tabs, GenotypeParams gp,
                                                    ngsep_site_out* __restrict__ out, unsigned long long* counters,
                                                    int64_t cap) {
+    __shared__ double s_t[3][32];
+    if (threadIdx.x < 96)
+        s_t[threadIdx.x >> 5][threadIdx.x & 31] =
+            (threadIdx.x < 32 ? tabs->A : threadIdx.x < 64 ? tabs->H : tabs->E)[threadIdx.x & 31];
+    __syncthreads();
     int64_t n = (int64_t)*qn;
     if (n > qcap) n = qcap;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const HardSite hs = queue[i];
-        const uint8_t rc = (uint8_t)hs.rc;
-        const double L00 = hs.L[0], L01 = hs.L[1], L02 = hs.L[2], L03 = hs.L[3], L11 = hs.L[4];
-        const double L12 = hs.L[5], L13 = hs.L[6], L22 = hs.L[7], L23 = hs.L[8], L33 = hs.L[9];
+    auto site = [&](int64_t i, ngsep_site_out& o) -> bool {
+        const QueueSite qs = queue[i];
+        const int32_t gpos = qs.gpos;
+        const uint8_t rc = (uint8_t)qs.rc;
+        int32_t total = 0;
+        uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+        int32_t sc[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
+        double L00 = 0, L01 = 0, L02 = 0, L03 = 0, L11 = 0, L12 = 0, L13 = 0, L22 = 0, L23 = 0, L33 = 0;
+        // reads that can cover gpos start at lb[gpos/64] (every earlier read ends before gpos)
+        bool more = true;
+        for (int64_t r0 = lb[gpos >> 6]; more && r0 < n_reads; r0 += 8) {
+            int4 h[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) h[k] = reads[r0 + k < n_reads ? r0 + k : n_reads - 1];
+            uint8_t code[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const bool in = r0 + k < n_reads && h[k].x <= gpos;
+                if (!in) more = false;
+                const int32_t off = gpos - h[k].x;
+                const bool cov = in && h[k].y >= gpos;
+                const int32_t o = cov ? off : 0;
+                const uint8_t cd = slots[(int64_t)(h[k].z + o / S) * S + (o % S)];
+                code[k] = cov ? cd : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint8_t cd = code[k];
+                total += cd != 0;                       // CountsHelper.java:210 (no call -> not counted)
+                if (!(cd & 0x80)) continue;             // q<=3 or not A/C/G/T (:214-221)
+                const uint32_t a = (cd >> 5) & 3;
+                int q = cd & 31;
+                q = q > gp.max_q ? gp.max_q : q;        // -maxBaseQS (:217-219)
+                const double A = s_t[0][q], H = s_t[1][q], E = s_t[2][q];
+                c0 += a == 0; c1 += a == 1; c2 += a == 2; c3 += a == 3;
+                const int side = (h[k].w & 1) ? 0 : 1;  // countsStrand[idx][neg?0:1] (:226-227)
+#pragma unroll
+                for (int t = 0; t < 4; t++) { sc[t][0] += (t == (int)a && side == 0); sc[t][1] += (t == (int)a && side == 1); }
+                // updateCounts (:231-248) with f == g: the [i][j] and [j][i] sums are identical sequences
+                L00 += a == 0 ? A : E;
+                L11 += a == 1 ? A : E;
+                L22 += a == 2 ? A : E;
+                L33 += a == 3 ? A : E;
+                L01 += a <= 1 ? H : E;
+                L02 += (a & 1) == 0 ? H : E;
+                L03 += (a == 0 || a == 3) ? H : E;
+                L12 += (a == 1 || a == 2) ? H : E;
+                L13 += (a & 1) == 1 ? H : E;
+                L23 += a >= 2 ? H : E;
+            }
+        }
+        if (total == 0) return false;                   // VariantDiscoverySNVQAlgorithm.java:101-103
         const bool callable = (rc & 0x80) != 0;
         int8_t genotype = -1, alt = -1, third = -1, nal = 0;
         int16_t gq = 0, qual = 0;
@@ -300,12 +249,9 @@ __global__ __launch_bounds__(256) void k_posterior(const HardSite* __restrict__ 
             }
             if (keep && gp.min_quality > gq) keep = false;
         }
-        if (!keep && !gp.dump_all) continue;
-        const unsigned long long idx = atomicAdd(&counters[0], 1ull);
-        if ((int64_t)idx >= cap) continue;
-        ngsep_site_out o;
+        if (!keep && !gp.dump_all) return false;
         o.seq_id = -1;
-        o.pos = hs.gpos;
+        o.pos = gpos;
         o.ref = callable ? "ACGT"[(rc >> 5) & 3] : 'N';
         o.n_alleles = nal;
         o.alt = alt;
@@ -315,178 +261,212 @@ __global__ __launch_bounds__(256) void k_posterior(const HardSite* __restrict__ 
         o.gq = gq;
         o.qual = qual;
         o.is_call = keep ? 1 : 0;
-        o.dp = hs.total;
-#pragma unroll
-        for (int k = 0; k < 4; k++) o.counts[k] = hs.c[k];
-        // CountsHelper.countsStrand (:226-227), recounted for emitted records only
-        int32_t sc[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
-        for (int64_t r = hs.r_begin; r < n_reads; r++) {
-            const int4 h = reads[r];
-            if (h.x > hs.gpos) break;
-            if (h.y < hs.gpos) continue;
-            const int32_t off = hs.gpos - h.x;
-            const uint8_t code = slots[(int64_t)(h.z + off / S) * S + (off % S)];
-            if (!(code & 0x80)) continue;
-            const int a = (code >> 5) & 3;
-            const int side = (h.w & 1) ? 0 : 1;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                sc[k][0] += (k == a && side == 0);
-                sc[k][1] += (k == a && side == 1);
-            }
-        }
+        o.dp = total;
+        o.counts[0] = (int32_t)c0; o.counts[1] = (int32_t)c1; o.counts[2] = (int32_t)c2; o.counts[3] = (int32_t)c3;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             o.strand_counts[k][0] = sc[k][0];
             o.strand_counts[k][1] = sc[k][1];
         }
-#pragma unroll
-        for (int k = 0; k < 10; k++) o.logc[k] = hs.L[k];
-        out[idx] = o;
+        o.logc[0] = L00; o.logc[1] = L01; o.logc[2] = L02; o.logc[3] = L03; o.logc[4] = L11;
+        o.logc[5] = L12; o.logc[6] = L13; o.logc[7] = L22; o.logc[8] = L23; o.logc[9] = L33;
+        return true;
+    };
+    // wave-uniform grid-stride loop: one output reservation per wave (ballot), not per site
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t ib = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); ib < n; ib += stride) {
+        const int64_t i = ib + lane;
+        ngsep_site_out o;
+        const bool emit = i < n && site(i, o);
+        const unsigned long long m = __ballot(emit);
+        if (!m) continue;
+        unsigned long long base = 0;
+        if (lane == __ffsll((long long)m) - 1) base = atomicAdd(&counters[0], (unsigned long long)__popcll(m));
+        base = __shfl(base, __ffsll((long long)m) - 1, 64);
+        const unsigned long long idx = base + __popcll(m & ((1ull << lane) - 1ull));
+        if (emit && (int64_t)idx < cap) out[idx] = o;
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// KT: fused pileup tile
-// ------------------------------------------------------------------------------------------
-// tile descriptor: {first read, end read, first slot, end slot} of the reads overlapping the tile
-template <int MODE, int IMG_BYTES, int MAX_READS, int MAX_SLOTS, int MAX_POS>
-__global__ __launch_bounds__(256, 2) void k_tile_pileup(
-    const u32x4* __restrict__ slots, const int32_t* __restrict__ slot_pos, const int4* __restrict__ reads,
-    const int4* __restrict__ tiles, const uint8_t* __restrict__ ref, const int32_t* __restrict__ lb,
-    int32_t T, int32_t S, int32_t max_span, int64_t n_tiles, const LikTables* __restrict__ tabs, GenotypeParams gp,
-    HardSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_img[IMG_BYTES];
-    __shared__ int4 s_hdr[MAX_READS];
-    __shared__ int32_t s_spos[MAX_SLOTS];                      // position of byte 0 of every staged slot
-    __shared__ __attribute__((aligned(16))) uint8_t s_ref[MAX_POS + 64];
-    __shared__ uint32_t s_bits[MAX_POS / 32];
-    __shared__ int32_t s_pref[MAX_POS / 32 + 1];
-    __shared__ double s_tab[3][32];                            // A, H, E likelihood addends
 
-    // XCD-aware tile order: consecutive tiles (which share boundary reads) run on one XCD
-    const int64_t b = blockIdx.x;
-    const int64_t q8 = n_tiles / 8, r8 = n_tiles % 8, xcd = b % 8, idx = b / 8;
-    const int64_t tile = xcd < r8 ? xcd * (q8 + 1) + idx : r8 * (q8 + 1) + (xcd - r8) * q8 + idx;
-    const int32_t tstart = (int32_t)(tile * T);
-    const int32_t tend = tstart + T;
+// ------------------------------------------------------------------------------------------
+// KT: pileup tile scan over the tile-blocked pileup matrix
+// ------------------------------------------------------------------------------------------
+// nonzero-allele valid bytes (MODE 0: a valid call that is not the reference allele, codes are
+// allele-XOR-reference) or any counted byte (MODE 1), one bit per byte
+template <int MODE>
+__device__ inline uint32_t unit_hits(const u32x4 d) {
+    auto f = [](uint32_t w) -> uint32_t {
+        uint32_t c;
+        if (MODE == 0) c = w & (((w & 0x60606060u) + 0x60606060u)) & 0x80808080u;
+        else c = (((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u;
+        return nib4(c);
+    };
+    return f(d.x) | (f(d.y) << 4) | (f(d.z) << 8) | (f(d.w) << 12);
+}
+
+//   phase 1  stream the tile's block of the pileup matrix (rows_t x T bytes, one coalesced
+//            16-byte load per lane and unit, kept in registers) and mark the positions whose pileup
+//            holds a valid non-reference call (MODE 0) or any counted call (MODE 1): LDS bitmap,
+//            restricted to callable / in-window positions.  Every other position is hom-ref
+//            (DESIGN.md "why pruning is exact") or has no pileup.  This is
+//            AlignmentsPileupGenerator.processCurrentPosition (discovery/AlignmentsPileupGenerator.java:475-498)
+//            reduced to the fact that decides whether SNVQ can call a variant there.
+//   phase 2  (MODE 0) integer hom-ref bound of every candidate: one LDS atomic per valid call at a
+//            candidate position adds its fixed-point contribution to the candidate's reference or
+//            allele accumulator (integer sums: order-independent, so exact).
+//   phase 3  a candidate the bound proves hom-ref is dropped; the others are queued for k_posterior.
+struct TileShared {
+    uint32_t bits[kTileMaxPos / 32];        // candidate bitmap
+    uint32_t ok[kTileMaxPos / 32];          // callable (MODE 0) / in-window (MODE 1) positions
+    int32_t pref[kTileMaxPos / 32 + 1];
+    unsigned long long w[2][32];            // bound addends: [0] reference call, [1] other allele
+    unsigned long long acc[kCandCap * 4];   // per candidate: R, X[1..3] (indexed by allele XOR reference)
+    QueueSite q[kQueueStage];               // survivors staged for one global reservation per flush
+    int32_t qn;
+    int32_t qbase;
+    unsigned long long ncand;               // candidates seen by this block (statistics)
+};
+
+// moves the block's staged survivors to the global queue with ONE atomic (same-address global
+// atomics from every tile serialise in L2 and were the scan's bottleneck)
+__device__ __forceinline__ void flush_queue(TileShared& sh, QueueSite* __restrict__ queue,
+                                            unsigned long long* __restrict__ counters, int64_t qcap) {
+    __syncthreads();
+    const int32_t n = sh.qn;
+    if (n == 0) return;
+    if (threadIdx.x == 0) sh.qbase = (int32_t)atomicAdd(&counters[2], (unsigned long long)n);
+    __syncthreads();
+    const int64_t base = sh.qbase;
+    for (int i = threadIdx.x; i < n; i += kScanThreads)
+        if (base + i < qcap) queue[base + i] = sh.q[i];
+    __syncthreads();
+    if (threadIdx.x == 0) sh.qn = 0;
+    __syncthreads();
+}
+
+template <int MODE>
+__device__ __forceinline__ void tile_body(TileShared& sh, const int64_t tile, const TileInfo ti,
+    const u32x4* __restrict__ pile, const uint8_t* __restrict__ ref,
+    int32_t log2T, const LikTables* __restrict__ tabs, const GenotypeParams& gp,
+    QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap) {
+    uint32_t* s_bits = sh.bits;
+    uint32_t* s_ok = sh.ok;
+    int32_t* s_pref = sh.pref;
+    unsigned long long (*s_w)[32] = sh.w;
+    unsigned long long* s_acc = sh.acc;
+    if (ti.rows == 0 || (gp.ablate & 4)) return;
     const int tid = threadIdx.x;
-    const int4 td = tiles[tile];
-    const int32_t rlo = td.x, rhi = td.y, s0 = td.z, s1 = td.w;
-    if (rhi <= rlo) return;
-    const int32_t nslot = s1 - s0;
-    const bool staged = (int64_t)nslot * S <= IMG_BYTES && nslot <= MAX_SLOTS && (rhi - rlo) <= MAX_READS;
-    const uint32_t ups = (uint32_t)(S / 16);
+    const int32_t T = 1 << log2T;
+    const int32_t tstart = (int32_t)(tile << log2T);
+    const int nw = T >= 32 ? T / 32 : 1;
+    const int log2U = log2T - 4;                                // units per row = T/16
+    const int32_t nunits = ti.rows << log2U;
+    const u32x4* blk = pile + (ti.off >> 4);
 
-    // reference codes of the tile, zero outside [tstart, tend): outside positions are never candidates
-    {
-        const uint32_t* refw = reinterpret_cast<const uint32_t*>(ref);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(s_ref);
-        for (int i = tid; i < (T + 64) / 4; i += 256) {
-            const int32_t g = tstart - 16 + 4 * i;
-            uint32_t v = (g >= tstart && g + 3 < tend) ? refw[g >> 2] : 0u;
-            dst[i] = v;
-        }
+    // phase 1: issue every register-resident unit load first
+    u32x4 U[kUnitsPerThread];
+#pragma unroll
+    for (int k = 0; k < kUnitsPerThread; k++) {
+        const int32_t u = tid + k * kScanThreads;
+        U[k] = u < nunits ? blk[u] : u32x4{0u, 0u, 0u, 0u};
     }
-    for (int i = tid; i < T / 32; i += 256) s_bits[i] = 0;
-    if (tid < 96) s_tab[tid >> 5][tid & 31] = (tid < 32 ? tabs->A : tid < 64 ? tabs->H : tabs->E)[tid & 31];
-    if (staged) {
-        for (int i = tid; i < rhi - rlo; i += 256) s_hdr[i] = reads[rlo + i];
-        for (int i = tid; i < nslot; i += 256) s_spos[i] = slot_pos[s0 + i];
-        __syncthreads();
-        // phase 1a: LDS-DMA of every 16-byte unit that overlaps the tile (lane-masked, all in flight)
-        const int32_t nunits = nslot * (int32_t)ups;
-        const int wave = tid >> 6, lane = tid & 63;
-        for (int32_t base = wave * 64; base < nunits; base += 256) {
-            const int32_t uu = base + lane;
-            bool need = false;
-            if (uu < nunits) {
-                const int32_t sl = uu / (int32_t)ups, jj = uu - sl * (int32_t)ups;
-                const int32_t p0 = s_spos[sl] + 16 * jj;
-                need = p0 + 15 >= tstart && p0 < tend;
+    // position masks from the reference codes: one dword (4 positions) per thread, eight
+    // neighbouring lanes OR their nibbles into one bitmap word
+    {
+        const uint32_t* refw = reinterpret_cast<const uint32_t*>(ref + tstart);
+        for (int i0 = 0; i0 < T / 4; i0 += kScanThreads) {
+            const int i = i0 + tid;
+            uint32_t bits = 0;
+            if (i < T / 4) {
+                const uint32_t v = refw[i];
+                const uint32_t m = MODE == 0 ? (v & 0x80808080u) : ((((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u);
+                bits = nib4(m) << (4 * (i & 7));
             }
-            if (need)
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(&slots[(int64_t)s0 * ups + uu]),
-                                                 (__attribute__((address_space(3))) void*)(&s_img[base * 16]),
-                                                 16, 0, 0);
-        }
-        __syncthreads();   // drains the LDS-DMA (vmcnt(0)) before anyone reads the image
-        // phase 1b: scan units from LDS, mark candidates
-        for (int32_t uu = tid; uu < nunits; uu += 256) {
-            const int32_t sl = uu / (int32_t)ups, jj = uu - sl * (int32_t)ups;
-            const int32_t p0 = s_spos[sl] + 16 * jj;
-            if (!(p0 + 15 >= tstart && p0 < tend)) continue;
-            const u32x4 d = *reinterpret_cast<const u32x4*>(&s_img[uu * 16]);
-            uint32_t any = d.x | d.y | d.z | d.w;
-            if (MODE == 0) any &= 0x80808080u;
-            if (!any) continue;
-            const uint32_t D[4] = {d.x, d.y, d.z, d.w};
-            uint32_t R[4];
-            load16(s_ref, p0 - tstart + 16, R);
-            const uint32_t m = unit_candidates<MODE>(D, R);
-            if (m) {
-                const int32_t o = p0 - tstart;
-                if (o >= 0) {
-                    const uint64_t m64 = (uint64_t)m << (o & 31);
-                    atomicOr(&s_bits[o >> 5], (uint32_t)m64);
-                    if ((m64 >> 32) && ((o >> 5) + 1) < T / 32) atomicOr(&s_bits[(o >> 5) + 1], (uint32_t)(m64 >> 32));
-                } else {
-                    atomicOr(&s_bits[0], m >> (-o));
-                }
+            bits |= __shfl_xor(bits, 1, 64);
+            bits |= __shfl_xor(bits, 2, 64);
+            bits |= __shfl_xor(bits, 4, 64);
+            if ((i & 7) == 0 && i < T / 4) {
+                s_ok[i >> 3] = bits;
+                s_bits[i >> 3] = 0;
             }
         }
-    } else {
-        // oversized tile: the same scan straight from global memory
-        __syncthreads();
-        const int64_t u0 = (int64_t)s0 * ups, u1 = (int64_t)s1 * ups;
-        for (int64_t u = u0 + tid; u < u1; u += 256) {
-            const int64_t sl = u / ups;
-            const int32_t p0 = slot_pos[sl] + 16 * (int32_t)(u - sl * ups);
-            if (!(p0 + 15 >= tstart && p0 < tend)) continue;
-            const u32x4 d = slots[u];
-            uint32_t any = d.x | d.y | d.z | d.w;
-            if (MODE == 0) any &= 0x80808080u;
-            if (!any) continue;
-            const uint32_t D[4] = {d.x, d.y, d.z, d.w};
-            uint32_t R[4];
-            load16(s_ref, p0 - tstart + 16, R);
-            const uint32_t m = unit_candidates<MODE>(D, R);
-            if (m) {
-                const int32_t o = p0 - tstart;
-                if (o >= 0) {
-                    const uint64_t m64 = (uint64_t)m << (o & 31);
-                    atomicOr(&s_bits[o >> 5], (uint32_t)m64);
-                    if ((m64 >> 32) && ((o >> 5) + 1) < T / 32) atomicOr(&s_bits[(o >> 5) + 1], (uint32_t)(m64 >> 32));
-                } else {
-                    atomicOr(&s_bits[0], m >> (-o));
-                }
-            }
-        }
+        if (T < 32 && tid == 0) s_bits[0] = 0;
+    }
+    if (MODE == 0) {
+        if (tid < 64) s_w[tid >> 5][tid & 31] = (tid < 32 ? tabs->wR : tabs->wX)[tid & 31];
+        for (int i = tid; i < kCandCap * 4; i += kScanThreads) s_acc[i] = 0;
     }
     __syncthreads();
-    // candidate prefix counts over bitmap words
-    const int nw = T / 32;
+    const uint32_t colmask = (1u << log2U) - 1u;
+    auto mark = [&](const u32x4 d, int32_t u) {
+        const uint32_t m = unit_hits<MODE>(d);
+        if (m) {
+            const int32_t p = (int32_t)(((uint32_t)u & colmask) << 4);   // tile-relative position of byte 0
+            const uint32_t sh = (uint32_t)p & 16u;
+            atomicOr(&s_bits[p >> 5], (m & (s_ok[p >> 5] >> sh)) << sh);
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < kUnitsPerThread; k++) {
+        const int32_t u = tid + k * kScanThreads;
+        if (u < nunits) mark(U[k], u);
+    }
+    for (int32_t u = tid + kUnitsPerThread * kScanThreads; u < nunits; u += kScanThreads) mark(blk[u], u);   // deep tiles
+    __syncthreads();
+    // candidate prefix counts over bitmap words (nw <= 64: one word per lane of wave 0)
     if (tid < 64) {
-        // wave-wide exclusive scan of popcounts (nw <= 128: two words per lane)
-        const int w0 = 2 * tid, w1 = 2 * tid + 1;
-        const int32_t c0 = w0 < nw ? __popc(s_bits[w0]) : 0, c1 = w1 < nw ? __popc(s_bits[w1]) : 0;
-        int32_t v = c0 + c1, incl = v;
+        const int32_t v = tid < nw ? __popc(s_bits[tid]) : 0;
+        int32_t incl = v;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const int32_t n = __shfl_up(incl, o, 64);
             if (tid >= o) incl += n;
         }
-        const int32_t excl = incl - v;
-        if (w0 < nw) s_pref[w0] = excl;
-        if (w1 < nw) s_pref[w1] = excl + c0;
+        if (tid < nw) s_pref[tid] = incl - v;
         if (tid == 63) s_pref[nw] = incl;
     }
     __syncthreads();
     const int32_t ncand = s_pref[nw];
-    if (tid == 0 && ncand) atomicAdd(&counters[1], (unsigned long long)ncand);
-    // phase 2: tally candidates.  Candidate c runs on thread (c%4)*64 + c/4 so that a tile's few
-    // candidates spread over all four waves (SIMDs) instead of queueing on one.
-    for (int32_t c = (gp.ablate & 1) ? ncand : ((tid & 63) * 4 + (tid >> 6)); c < ncand; c += 256) {
+    if (ncand == 0) return;
+    if (tid == 0) sh.ncand += (unsigned long long)ncand;
+    if (gp.ablate & 1) return;                               // diagnostics: scan only
+    const bool bound = MODE == 0 && gp.use_bound;
+    if (bound) {
+        // phase 2: one LDS atomic per valid call at a candidate position
+        auto accumulate = [&](const u32x4 d, int32_t u) {
+            const int32_t p = (int32_t)(((uint32_t)u & colmask) << 4);
+            uint32_t cm = (s_bits[p >> 5] >> ((uint32_t)p & 16u)) & 0xFFFFu;
+            if (!cm) return;
+            cm &= unit_valid_mask(d);
+            while (cm) {
+                const int k = __builtin_ctz(cm);
+                cm &= cm - 1;
+                const int32_t pos = p + k;
+                const uint32_t cd = unit_byte(d, k);
+                const uint32_t a = (cd >> 5) & 3;                   // allele XOR reference allele
+                int q = cd & 31;
+                q = q > gp.max_q ? gp.max_q : q;
+                const int w = pos >> 5;
+                const int32_t ci = s_pref[w] + __popc(s_bits[w] & ((1u << (pos & 31)) - 1u));
+                if (ci < kCandCap) atomicAdd(&s_acc[ci * 4 + (int)a], s_w[a == 0 ? 0 : 1][q]);
+            }
+        };
+#pragma unroll
+        for (int k = 0; k < kUnitsPerThread; k++) {
+            const int32_t u = tid + k * kScanThreads;
+            if (u < nunits) accumulate(U[k], u);
+        }
+        for (int32_t u = tid + kUnitsPerThread * kScanThreads; u < nunits; u += kScanThreads) accumulate(blk[u], u);
+        __syncthreads();
+    }
+    // phase 3: decide every candidate.  Candidate c runs on thread (c%4)*64 + c/4 so that a tile's
+    // few candidates spread over all four waves (SIMDs) instead of queueing on one.
+    for (int32_t c0 = 0; c0 < ncand; c0 += kScanThreads) {
+        if (c0 > 0 || sh.qn > kQueueStage - kScanThreads) flush_queue(sh, queue, counters, qcap);   // room for one chunk
+        const int32_t c = c0 + (tid & 63) * 4 + (tid >> 6);
+        if (c >= ncand) continue;
         int lo = 0, hi = nw - 1;              // last word whose prefix <= c
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
@@ -495,50 +475,52 @@ __global__ __launch_bounds__(256, 2) void k_tile_pileup(
         uint32_t w = s_bits[lo];
         for (int k = c - s_pref[lo]; k > 0; k--) w &= w - 1;
         const int32_t gpos = tstart + lo * 32 + __builtin_ctz(w);
-        const uint8_t rc = s_ref[gpos - tstart + 16];
-        if (staged) {
-            // first read that can cover gpos: gfirst >= gpos - max_span + 1 (headers sorted by gfirst)
-            int a = 0, z = rhi - rlo;
-            const int32_t key = gpos - max_span + 1;
-            while (a < z) {
-                const int m = (a + z) >> 1;
-                if (s_hdr[m].x < key) a = m + 1; else z = m;
-            }
-            int e = a;                            // first read starting after gpos
-            z = rhi - rlo;
-            while (e < z) {
-                const int m = (e + z) >> 1;
-                if (s_hdr[m].x <= gpos) e = m + 1; else z = m;
-            }
-            tally_position<true>(gpos, rc, rlo + a, rlo + e, s_hdr, rlo, s_img, s0, S, s_tab[0], s_tab[1], s_tab[2], gp,
-                                 queue, counters, qcap);
-        } else {
-            int32_t rb = lb[gpos >> 6];
-            if (rb < rlo) rb = rlo;
-            int32_t re = rb, z = rhi;             // first read starting after gpos
-            while (re < z) {
-                const int32_t m = (re + z) >> 1;
-                if (reads[m].x <= gpos) re = m + 1; else z = m;
-            }
-            tally_position<false>(gpos, rc, rb, re, reads, 0, reinterpret_cast<const uint8_t*>(slots), 0, S,
-                                  s_tab[0], s_tab[1], s_tab[2], gp, queue, counters, qcap);
+        bool drop = false;
+        if (bound && c < kCandCap) {
+            // hom-ref if, for every other genotype G, the lower bound of L[r][r]-L[G] keeps
+            // P(G) (het: P(x,y)+P(y,x)) <= P(r,r)  (DESIGN.md "hom-ref bound").  Accumulators are
+            // indexed by allele XOR reference: 0 = reference, 1..3 = the three other alleles.
+            const unsigned long long Rp = s_acc[c * 4];
+            const long long R1 = (long long)(Rp & 0xFFFFFFFFull), R2 = (long long)(Rp >> 32);
+            const unsigned long long Xa = s_acc[c * 4 + 1], Xb = s_acc[c * 4 + 2], Xc = s_acc[c * 4 + 3];
+            const long long a1 = (long long)(Xa & 0xFFFFFFFFull), b1 = (long long)(Xb & 0xFFFFFFFFull);
+            const long long c1 = (long long)(Xc & 0xFFFFFFFFull);
+            const long long a2 = (long long)(Xa >> 32), b2 = (long long)(Xb >> 32), c2 = (long long)(Xc >> 32);
+            const long long th = tabs->t_het, to = tabs->t_homo;
+            // het (r,x): R1 - X1[x];  hom (x,x): R2 - X2[x];  het (x,y), x,y != r: R2 - X1[x] - X1[y]
+            drop = (R1 - a1 > th) && (R1 - b1 > th) && (R1 - c1 > th) &&
+                   (R2 - a2 > to) && (R2 - b2 > to) && (R2 - c2 > to) &&
+                   (R2 - a1 - b1 > th) && (R2 - a1 - c1 > th) && (R2 - b1 - c1 > th);
         }
+        if (drop) continue;
+        sh.q[atomicAdd(&sh.qn, 1)] = QueueSite{gpos, (int32_t)ref[gpos]};
     }
 }
 
-// tile descriptors from the read index
-__global__ __launch_bounds__(256) void kt_tile_info(const int4* __restrict__ reads, int64_t n_reads, int64_t n_slots,
-                                                    const int32_t* __restrict__ lb, int64_t n_lb, int32_t T, int32_t pad,
-                                                    int64_t n_tiles, int4* __restrict__ tiles) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_tiles) return;
-    const int64_t tstart = t * T, tend = tstart + T;
-    const int64_t rlo = lb[tstart >> 6];
-    int64_t k = (tend + pad) >> 6;
-    if (k >= n_lb) k = n_lb - 1;
-    const int64_t rhi = lb[k];
-    tiles[t] = make_int4((int)rlo, (int)rhi, (int)(rlo < n_reads ? reads[rlo].z : n_slots),
-                         (int)(rhi < n_reads ? reads[rhi].z : n_slots));
+// Persistent grid: block b works on XCD b % 8 (round-robin placement, speed only) through that
+// XCD's contiguous share of the tiles, so neighbouring tiles stay in one L2.
+template <int MODE>
+__global__ __launch_bounds__(kScanThreads) void k_tile_pileup(
+    const u32x4* __restrict__ pile, const TileInfo* __restrict__ tinfo, const uint8_t* __restrict__ ref,
+    int32_t log2T, int64_t n_tiles, const LikTables* __restrict__ tabs, GenotypeParams gp,
+    QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap) {
+    __shared__ TileShared sh;
+    const int64_t nb = gridDim.x, b = blockIdx.x;
+    const int64_t xcd = b % 8, j = b / 8, nbx = (nb - xcd + 7) / 8;
+    const int64_t q8 = n_tiles / 8, r8 = n_tiles % 8;
+    const int64_t c0 = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+    const int64_t c1 = c0 + q8 + (xcd < r8 ? 1 : 0);
+    if (threadIdx.x == 0) { sh.qn = 0; sh.ncand = 0; }
+    __syncthreads();
+    TileInfo next = c0 + j < c1 ? tinfo[c0 + j] : TileInfo{0, 0, 0};
+    for (int64_t t = c0 + j; t < c1; t += nbx) {
+        const TileInfo ti = next;
+        if (t + nbx < c1) next = tinfo[t + nbx];   // descriptor of the next tile in flight meanwhile
+        tile_body<MODE>(sh, t, ti, pile, ref, log2T, tabs, gp, queue, counters, qcap);
+        __syncthreads();   // the shared tile state is reused by the next tile
+    }
+    flush_queue(sh, queue, counters, qcap);
+    if (threadIdx.x == 0 && sh.ncand) atomicAdd(&counters[1], sh.ncand);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -645,6 +627,11 @@ Device* device_create(int ordinal, std::string& err) {
     if (hipSetDevice(ordinal) != hipSuccess) { err = "hipSetDevice failed"; return nullptr; }
     Device* d = new Device();
     d->ordinal = ordinal;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, ordinal) == hipSuccess && prop.multiProcessorCount > 0)
+            d->n_cu = prop.multiProcessorCount;
+    }
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) { err = "stream"; delete d; return nullptr; }
     for (auto& e : d->ev) (void)hipEventCreate(&e);
     if (hipMalloc(&d->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess ||
@@ -663,11 +650,11 @@ void device_release(Device* d) {
     if (!d) return;
     (void)hipSetDevice(d->ordinal);
     (void)hipFree(d->d_slots); d->d_slots = nullptr;
-    (void)hipFree(d->d_slot_pos); d->d_slot_pos = nullptr;
+    (void)hipFree(d->d_pile); d->d_pile = nullptr;
     (void)hipFree(d->d_reads); d->d_reads = nullptr;
     (void)hipFree(d->d_ref); d->d_ref = nullptr;
     (void)hipFree(d->d_lb); d->d_lb = nullptr;
-    (void)hipFree(d->d_tiles); d->d_tiles = nullptr;
+    (void)hipFree(d->d_tinfo); d->d_tinfo = nullptr;
     d->n_units = d->n_slots = d->n_lb = d->n_reads = d->g_len = d->n_tiles = 0;
 }
 
@@ -693,13 +680,15 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
     const int64_t slot_bytes = s.n_slots * (int64_t)S;
     const int32_t pad = s.windows.empty() ? 64 : s.windows[0].pad;
     HIP_TRY(hipMalloc(&d->d_slots, (size_t)std::max<int64_t>(slot_bytes, 16)));
-    HIP_TRY(hipMalloc(&d->d_slot_pos, (size_t)std::max<int64_t>(s.n_slots, 1) * 4));
+    HIP_TRY(hipMalloc(&d->d_pile, (size_t)std::max<int64_t>(s.pile_bytes, 16)));
+    HIP_TRY(hipMalloc(&d->d_tinfo, (size_t)std::max<int64_t>(s.n_tiles, 1) * sizeof(TileInfo)));
     HIP_TRY(hipMalloc(&d->d_reads, (size_t)std::max<int64_t>(s.n_reads, 1) * sizeof(int4)));
     HIP_TRY(hipMalloc(&d->d_ref, (size_t)s.g_len + 64));
     d->n_lb = (s.g_len + pad + 63) / 64 + 2;
     HIP_TRY(hipMalloc(&d->d_lb, (size_t)d->n_lb * 4));
     if (slot_bytes) HIP_TRY(hipMemcpyAsync(d->d_slots, s.h_slots.data(), (size_t)slot_bytes, hipMemcpyHostToDevice, d->stream));
-    if (s.n_slots) HIP_TRY(hipMemcpyAsync(d->d_slot_pos, s.h_slot_pos.data(), (size_t)s.n_slots * 4, hipMemcpyHostToDevice, d->stream));
+    if (s.pile_bytes) HIP_TRY(hipMemcpyAsync(d->d_pile, s.h_pile.data(), (size_t)s.pile_bytes, hipMemcpyHostToDevice, d->stream));
+    if (s.n_tiles) HIP_TRY(hipMemcpyAsync(d->d_tinfo, s.h_tinfo.data(), (size_t)s.n_tiles * sizeof(TileInfo), hipMemcpyHostToDevice, d->stream));
     if (s.n_reads) HIP_TRY(hipMemcpyAsync(d->d_reads, s.h_reads.data(), (size_t)s.n_reads * 16, hipMemcpyHostToDevice, d->stream));
     HIP_TRY(hipMemsetAsync(d->d_ref, 0, (size_t)s.g_len + 64, d->stream));
     HIP_TRY(hipMemcpyAsync(d->d_ref, s.h_ref.data(), (size_t)s.g_len, hipMemcpyHostToDevice, d->stream));
@@ -711,16 +700,12 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
     d->max_span = s.max_span;
     d->pad = pad;
     d->tile = s.tile;
-    d->tile_variant = s.tile_variant;
-    d->n_tiles = (s.g_len + s.tile - 1) / s.tile;
+    d->log2_tile = 0;
+    while ((1 << d->log2_tile) < s.tile) d->log2_tile++;
+    d->n_tiles = s.n_tiles;
     {
         dim3 grid((unsigned)((d->n_lb + 255) / 256));
         hipLaunchKernelGGL(kl_read_index, grid, dim3(256), 0, d->stream, d->d_reads, d->n_reads, d->d_lb, d->n_lb, pad);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMalloc(&d->d_tiles, (size_t)std::max<int64_t>(d->n_tiles, 1) * sizeof(int4)));
-        dim3 gt((unsigned)((d->n_tiles + 255) / 256));
-        hipLaunchKernelGGL(kt_tile_info, gt, dim3(256), 0, d->stream, d->d_reads, d->n_reads, d->n_slots, d->d_lb, d->n_lb,
-                           d->tile, pad, d->n_tiles, d->d_tiles);
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipStreamSynchronize(d->stream));
@@ -747,36 +732,38 @@ int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypePar
         HIP_TRY(hipMalloc(&d->d_bucket, (size_t)(3 * nb + 1) * sizeof(int32_t)));
         d->nb_cap = nb;
     }
-    // queue of candidates that need the full posterior: ~2% of candidates; dump mode: every position
+    // queue of candidates the tile kernel could not prove hom-ref; dump mode: every position
     int64_t qwant = g.dump_all ? std::max<int64_t>(s.covered + 1024, 1024) : std::max<int64_t>(s.g_len / 64 + 65536, 65536);
     if (qwant < d->cap_hard) qwant = d->cap_hard;
     {
         if (qwant > d->cap_hard) {
             (void)hipFree(d->d_hard);
-            HIP_TRY(hipMalloc(&d->d_hard, (size_t)qwant * sizeof(HardSite)));
+            HIP_TRY(hipMalloc(&d->d_hard, (size_t)qwant * sizeof(QueueSite)));
             d->cap_hard = qwant;
         }
         HIP_TRY(hipMemcpyAsync(d->d_tables, &t, sizeof(LikTables), hipMemcpyHostToDevice, d->stream));
         HIP_TRY(hipMemsetAsync(d->d_counters, 0, 4 * sizeof(unsigned long long), d->stream));
         HIP_TRY(hipEventRecord(d->ev[0], d->stream));
         if (d->n_tiles > 0) {
-            dim3 grid((unsigned)d->n_tiles);
-#define NGSEP_LAUNCH_TILE(MODE, B)                                                                                     \
-    hipLaunchKernelGGL((k_tile_pileup<MODE, B.img_bytes, B.max_reads, B.max_slots, B.max_pos>), grid, dim3(256), 0,  \
-                       d->stream, (const u32x4*)d->d_slots, d->d_slot_pos, d->d_reads, d->d_tiles, d->d_ref, d->d_lb, \
-                       d->tile, d->slot_size, d->max_span, d->n_tiles, d->d_tables, g, d->d_hard, d->d_counters,       \
-                       d->cap_hard)
-            if (d->tile_variant == 0) {
-                if (prune) NGSEP_LAUNCH_TILE(0, kTileSmall); else NGSEP_LAUNCH_TILE(1, kTileSmall);
-            } else {
-                if (prune) NGSEP_LAUNCH_TILE(0, kTileLarge); else NGSEP_LAUNCH_TILE(1, kTileLarge);
-            }
-#undef NGSEP_LAUNCH_TILE
+            // persistent blocks: a few per CU, each loops over its XCD's tiles
+            int per_cu = kTileBlocksPerCU;
+            if (const char* e = std::getenv("NGSEP_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(e));   // tuning
+            const int64_t nblk = std::min<int64_t>(d->n_tiles, (int64_t)d->n_cu * per_cu);
+            dim3 grid((unsigned)nblk);
+            if (prune)
+                hipLaunchKernelGGL(k_tile_pileup<0>, grid, dim3(kScanThreads), 0, d->stream, (const u32x4*)d->d_pile,
+                                   d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, d->d_tables, g, d->d_hard,
+                                   d->d_counters, d->cap_hard);
+            else
+                hipLaunchKernelGGL(k_tile_pileup<1>, grid, dim3(kScanThreads), 0, d->stream, (const u32x4*)d->d_pile,
+                                   d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, d->d_tables, g, d->d_hard,
+                                   d->d_counters, d->cap_hard);
             HIP_TRY(hipGetLastError());
         }
         HIP_TRY(hipEventRecord(d->ev[1], d->stream));
         hipLaunchKernelGGL(k_posterior, dim3(1024), dim3(256), 0, d->stream, d->d_hard, d->d_counters + 2, d->cap_hard,
-                           d->d_reads, d->n_reads, d->d_slots, d->slot_size, g, d->d_sites, d->d_counters, d->cap_sites);
+                           d->d_reads, d->n_reads, d->d_lb, d->d_slots, d->slot_size, d->d_tables, g, d->d_sites,
+                           d->d_counters, d->cap_sites);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(d->ev[2], d->stream));   // queue overflow is checked after the copy below
         // order the records by position on the device
@@ -801,12 +788,23 @@ int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypePar
     HIP_TRY(hipStreamSynchronize(d->stream));
     auto ts = std::chrono::steady_clock::now();
     const int64_t n = (int64_t)d->h_counters[0];
-    if (n > d->cap_sites) { err = "site buffer overflow"; return -1; }
+    if (n > d->cap_sites) {
+        // more calls than the record buffer holds (e.g. -minQuality 0): grow it and run again
+        (void)hipFree(d->d_sites);
+        (void)hipFree(d->d_sorted);
+        d->d_sites = d->d_sorted = nullptr;
+        d->cap_sites = 0;
+        HIP_TRY(hipMalloc(&d->d_sites, (size_t)(n + 1024) * sizeof(ngsep_site_out)));
+        HIP_TRY(hipMalloc(&d->d_sorted, (size_t)(n + 1024) * sizeof(ngsep_site_out)));
+        d->cap_sites = n + 1024;
+        d->last_n_sites = n;
+        return device_run(d, s, t, g, prune, out, n_out, scan_ms, geno_ms, total_ms, n_candidates, err);
+    }
     if ((int64_t)d->h_counters[2] > d->cap_hard) {
         // rare: more undecided candidates than the queue holds -> grow it and run again
         (void)hipFree(d->d_hard);
         d->d_hard = nullptr;
-        HIP_TRY(hipMalloc(&d->d_hard, (size_t)(d->h_counters[2] + 1024) * sizeof(HardSite)));
+        HIP_TRY(hipMalloc(&d->d_hard, (size_t)(d->h_counters[2] + 1024) * sizeof(QueueSite)));
         d->cap_hard = (int64_t)d->h_counters[2] + 1024;
         d->last_n_sites = n;
         return device_run(d, s, t, g, prune, out, n_out, scan_ms, geno_ms, total_ms, n_candidates, err);

@@ -122,19 +122,24 @@ def test_golden_dump_bitexact(tmp_path):
         assert (x.dp, tuple(x.counts), tuple(x.logc)) == (dp, counts, logc), k
 
 
-def test_pruning_is_exact(tmp_path):
-    """K1's candidate pruning returns exactly the calls of genotyping every position."""
-    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=3, depth=30, seed=3, quality_model=2)
+@pytest.mark.parametrize("depth,snv_rate,het", [(30, 1e-3, 0.001), (6, 3e-3, 0.001), (12, 1e-2, 0.05), (40, 1e-3, 0.1)])
+def test_pruning_is_exact(tmp_path, depth, snv_rate, het):
+    """KT's candidate pruning + integer hom-ref bound return exactly the calls of genotyping every
+    position (low depth and high error/heterozygosity put many candidates near the bound)."""
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=3, depth=depth, seed=3, quality_model=2, snv_rate=snv_rate)
     res = []
     for prune in (1, 0):
-        with GpuPileupSession(gpu_params(prune_candidates=prune)) as s:
+        with GpuPileupSession(gpu_params(prune_candidates=prune, het_rate=het, min_quality=0)) as s:
             for name, seq in syn.contigs():
                 s.set_reference(name, seq)
             s.processAlignments(syn.batch())
             s.notifyEndOfAlignments()
             res.append([(x.sequence, x.pos, x.gq, x.qual, tuple(x.logc)) for x in s.getCalledVariants()])
+            if prune:
+                st = s.stats()
     assert res[0] == res[1]
     assert len(res[0]) > 100
+    assert st.hard_sites < st.candidates     # the bound dropped candidates
 
 
 def test_path_a_equals_path_b(tmp_path):
