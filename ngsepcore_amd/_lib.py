@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libngsep_amd.so")
+LIB_PATH = os.environ.get("NGSEP_LIB_PATH") or os.path.join(_HERE, "lib", "libngsep_amd.so")   # override: tuning builds only
 
 NGSEP_OK = 0
 NGSEP_E_INVALID = -1

@@ -79,6 +79,16 @@ void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g) {
     t->t_het = (long long)std::floor(K * t_het) + kBoundMargin;
     t->t_homo = kBoundMargin;
     g->use_bound = ok && !g->dump_all && std::isfinite(t_het) ? 1 : 0;
+    // count bound: a valid call carries q in [4, 30] (engine.hpp code), capped at max_q in the kernel
+    t->c_r1 = t->c_r2 = INT64_MAX;
+    t->c_x1 = t->c_x2 = 0;
+    for (int q0 = 4; q0 <= 30; q0++) {
+        const int q = q0 > g->max_q ? g->max_q : q0;
+        t->c_r1 = std::min<long long>(t->c_r1, (long long)(t->wR[q] & 0xFFFFFFFFull));
+        t->c_r2 = std::min<long long>(t->c_r2, (long long)(t->wR[q] >> 32));
+        t->c_x1 = std::max<long long>(t->c_x1, (long long)(t->wX[q] & 0xFFFFFFFFull));
+        t->c_x2 = std::max<long long>(t->c_x2, (long long)(t->wX[q] >> 32));
+    }
 }
 
 // ReadAlignment.updateAlleleCallsInfo (ReadAlignment.java:747-834): allele-call length per read position.
@@ -351,13 +361,13 @@ static inline uint8_t ref_code(const ngsep_ctx* c, char ch) {
 // ---- tile-blocked pileup matrix (engine.hpp TileInfo) ----
 // Tile size: every T in [kTileMinPos, kTileMaxPos] is costed as the bytes of its matrix
 // (sum over tiles of rows_t * T, rows_t = the tile's maximum depth) plus a fixed per-tile cost;
-// T must keep >= 99.9 % of tiles within the registers of one workgroup (the rest reload).
+// T must keep >= 99.9 % of tiles within the registers of one wavefront (the rest reload).
 static int choose_tile(const std::vector<int32_t>& cov_max16, int64_t g_len, std::vector<int32_t>& rows_out) {
     std::vector<int32_t> cur = cov_max16;   // maxima over blocks of T positions, T = 16, 32, ...
     int bestT = kTileMinPos;
     double best_cost = -1;
     std::vector<int32_t> best_rows;
-    const int64_t budget = (int64_t)kScanThreads * kUnitsPerThread;   // 16-byte units held in registers
+    const int64_t budget = kScanRegUnits;   // 16-byte units held in registers
     for (int T = kTileMinPos; T <= kTileMaxPos; T *= 2) {
         if (T > kTileMinPos) {
             std::vector<int32_t> nxt((cur.size() + 1) / 2);

@@ -44,9 +44,9 @@ struct TileInfo {
     int32_t pad;
 };
 static_assert(sizeof(TileInfo) == 16, "TileInfo layout");
-constexpr int kScanThreads = 256;          // threads per tile workgroup
-constexpr int kUnitsPerThread = 8;         // 16-byte units a thread keeps in registers
-constexpr int kTileMaxPos = 2048;          // largest tile (positions)
+constexpr int kScanThreads = 256;          // threads per tile-scan workgroup (one tile per wavefront)
+constexpr int kScanRegUnits = 64 * 24;     // tile-size budget: 16-byte units per tile (deeper tiles are rare)
+constexpr int kTileMaxPos = 1024;          // largest tile (positions): <= 64 units per row
 constexpr int kTileMinPos = 16;
 
 // K2 output record (device layout == ngsep_site_out, with gpos in .pos)
@@ -65,6 +65,9 @@ struct LikTables {
     unsigned long long wX[32];
     long long t_het;      // floor(K (log10 h/12 - log10 (1-h)/4 + log10 2)) + margin
     long long t_homo;     // margin
+    // count bound (kernels.hip phase 2): extreme addends over the qualities a valid call can carry
+    long long c_r1, c_r2; // min over q of the low / high half of wR
+    long long c_x1, c_x2; // max over q of the low / high half of wX
 };
 constexpr double kBoundScale = 1048576.0;   // 2^20: a tile holds <= 512 reads -> sums < 2^31
 constexpr long long kBoundMargin = 64;      // 6e-5 in log10 units, >> fp64 rounding of the sums
@@ -75,7 +78,8 @@ struct GenotypeParams {
     int32_t max_q;             // effective -maxBaseQS cap
     int32_t min_quality;       // -minQuality
     int32_t dump_all;          // emit a record for every position with DP>0
-    int32_t ablate;            // diagnostics only (env NGSEP_ABLATE): 1 scan only (no bound, no queue)
+    int32_t ablate;            // diagnostics only (env NGSEP_ABLATE): 1 scan only (no bound, no queue),
+                               // 4 no tiles, 8 tally without posterior, 16 posterior kernel reads the queue only
     int32_t use_bound;         // 1: candidates proven hom-ref by the integer bound are dropped in the tile kernel
 };
 

@@ -57,6 +57,7 @@ struct Device {
     LikTables* d_tables = nullptr;
     ngsep_site_out* d_sites = nullptr;
     ngsep_site_out* d_sorted = nullptr;
+    unsigned long long* d_keys = nullptr;   // ordering keys (position << 32 | record): 2 x cap_sites
     int32_t* d_bucket = nullptr;     // counts, then starts (nb+1), then cursors (nb)
     int64_t nb_cap = 0;
     QueueSite* d_hard = nullptr;
@@ -109,70 +110,105 @@ struct QueueSite {
 };
 static_assert(sizeof(QueueSite) == 8, "QueueSite layout");
 
-constexpr int kCandCap = 256;   // candidates per tile with integer-bound accumulators in LDS
-constexpr int kTileBlocksPerCU = 4;
-constexpr int kQueueStage = 1024;    // survivors staged in LDS per tile-scan block   // persistent tile-scan blocks per CU (register-limited occupancy)
 
 // ------------------------------------------------------------------------------------------
-// KP: exact tally + posterior + SNVQ call of the queued candidates (thread per site)
+// KP: exact tally + posterior + SNVQ call of the queued candidates (one wavefront per site)
 // ------------------------------------------------------------------------------------------
 // CountsHelper.calculateCountsSNV/updateCounts (discovery/CountsHelper.java:83-95,209-251) over the
 // reads covering gpos in pending-list order (the order of the read table), so the fp64 sums are
 // bit-identical to the reference's; then getPosteriorProbabilities (:410-495),
 // VariantDiscoverySNVQAlgorithm.discoverSNV (:100-243) and the listener filters
 // (SingleSampleVariantPileupListener.java:213-232).
-__global__ __launch_bounds__(256) void k_posterior(const QueueSite* __restrict__ queue, const unsigned long long* qn,
+// The 64 lanes fetch 64 consecutive reads' codes at once (the memory round trips are what a site
+// costs); integer counts come from ballots, and the fp64 sums are then added in lane (= read) order,
+// wave-uniformly.  Emitted records are staged in LDS and reserved once per workgroup.
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+constexpr int kPostWaves = 4;
+constexpr int kPostStage = 8;           // records staged per wave
+
+__device__ __forceinline__ void post_flush(ngsep_site_out* rec, int32_t n, int lane, ngsep_site_out* __restrict__ out,
+                                           unsigned long long* counters, int64_t cap) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(&counters[0], (unsigned long long)n);
+    base = __shfl(base, 0, 64);
+    constexpr int W = sizeof(ngsep_site_out) / 4;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(rec);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(out);
+    for (int k = lane; k < n * W; k += 64)
+        if ((int64_t)base + k / W < cap) dst[(base * W) + k] = src[k];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* __restrict__ queue, const unsigned long long* qn,
                                                    int64_t qcap, const int4* __restrict__ reads, int64_t n_reads,
                                                    const int32_t* __restrict__ lb, const uint8_t* __restrict__ slots,
                                                    int32_t S, const LikTables* __restrict__ tabs, GenotypeParams gp,
                                                    ngsep_site_out* __restrict__ out, unsigned long long* counters,
                                                    int64_t cap) {
     __shared__ double s_t[3][32];
+    __shared__ ngsep_site_out s_rec[kPostWaves][kPostStage];
+    __shared__ int32_t s_n[kPostWaves];
+    __shared__ unsigned long long s_base;
     if (threadIdx.x < 96)
         s_t[threadIdx.x >> 5][threadIdx.x & 31] =
             (threadIdx.x < 32 ? tabs->A : threadIdx.x < 64 ? tabs->H : tabs->E)[threadIdx.x & 31];
     __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int64_t n = (int64_t)*qn;
     if (n > qcap) n = qcap;
-    auto site = [&](int64_t i, ngsep_site_out& o) -> bool {
+    int32_t ns = 0;                                   // records staged by this wave (uniform)
+    const int64_t nwaves = (int64_t)gridDim.x * kPostWaves;
+    for (int64_t i = (int64_t)blockIdx.x * kPostWaves + wv; i < n; i += nwaves) {
         const QueueSite qs = queue[i];
-        const int32_t gpos = qs.gpos;
-        const uint8_t rc = (uint8_t)qs.rc;
+        const int32_t gpos = __builtin_amdgcn_readfirstlane(qs.gpos);
+        const uint32_t rc = (uint32_t)__builtin_amdgcn_readfirstlane(qs.rc);
+        if (gp.ablate & 16) continue;                     // diagnostics: queue read only
         int32_t total = 0;
-        uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+        int32_t cnt[4] = {0, 0, 0, 0};
         int32_t sc[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
         double L00 = 0, L01 = 0, L02 = 0, L03 = 0, L11 = 0, L12 = 0, L13 = 0, L22 = 0, L23 = 0, L33 = 0;
-        // reads that can cover gpos start at lb[gpos/64] (every earlier read ends before gpos)
-        bool more = true;
-        for (int64_t r0 = lb[gpos >> 6]; more && r0 < n_reads; r0 += 8) {
-            int4 h[8];
+        // reads that can cover gpos start at lb[gpos/64] (every earlier read ends before gpos); the
+        // table is sorted by start, so the first read starting after gpos ends the walk
+        for (int64_t r0 = lb[gpos >> 6]; r0 < n_reads; r0 += 64) {
+            const int64_t r = r0 + lane;
+            const int4 h = r < n_reads ? reads[r] : int4{INT32_MAX, 0, 0, 0};
+            const bool in = h.x <= gpos;
+            const bool cov = in && h.y >= gpos;
+            const int32_t o = cov ? gpos - h.x : 0;
+            const uint32_t code = cov ? (uint32_t)slots[(int64_t)(h.z + o / S) * S + (o % S)] : 0u;
+            total += __popcll(__ballot(code != 0));                       // CountsHelper.java:210
+            const bool valid = (code & 0x80u) != 0;                       // q<=3 or not A/C/G/T: not counted (:214-221)
+            const uint32_t al = (code >> 5) & 3u;
+            const unsigned long long negm = __ballot(h.w & 1);
 #pragma unroll
-            for (int k = 0; k < 8; k++) h[k] = reads[r0 + k < n_reads ? r0 + k : n_reads - 1];
-            uint8_t code[8];
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const bool in = r0 + k < n_reads && h[k].x <= gpos;
-                if (!in) more = false;
-                const int32_t off = gpos - h[k].x;
-                const bool cov = in && h[k].y >= gpos;
-                const int32_t o = cov ? off : 0;
-                const uint8_t cd = slots[(int64_t)(h[k].z + o / S) * S + (o % S)];
-                code[k] = cov ? cd : 0;
+            for (int t = 0; t < 4; t++) {
+                const unsigned long long m = __ballot(valid && al == (uint32_t)t);
+                cnt[t] += __popcll(m);
+                sc[t][0] += __popcll(m & negm);                           // countsStrand[idx][neg?0:1] (:226-227)
+                sc[t][1] += __popcll(m & ~negm);
             }
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const uint8_t cd = code[k];
-                total += cd != 0;                       // CountsHelper.java:210 (no call -> not counted)
-                if (!(cd & 0x80)) continue;             // q<=3 or not A/C/G/T (:214-221)
-                const uint32_t a = (cd >> 5) & 3;
-                int q = cd & 31;
-                q = q > gp.max_q ? gp.max_q : q;        // -maxBaseQS (:217-219)
+            unsigned long long mv = __ballot(valid);
+            while (mv) {                                                  // updateCounts (:231-248), read order
+                const int l = __builtin_ctzll(mv);
+                mv &= mv - 1ull;
+                const uint32_t cd = (uint32_t)__builtin_amdgcn_readlane((int)code, l);
+                const uint32_t a = (cd >> 5) & 3u;
+                int q = (int)(cd & 31u);
+                q = q > gp.max_q ? gp.max_q : q;                          // -maxBaseQS (:217-219)
                 const double A = s_t[0][q], H = s_t[1][q], E = s_t[2][q];
-                c0 += a == 0; c1 += a == 1; c2 += a == 2; c3 += a == 3;
-                const int side = (h[k].w & 1) ? 0 : 1;  // countsStrand[idx][neg?0:1] (:226-227)
-#pragma unroll
-                for (int t = 0; t < 4; t++) { sc[t][0] += (t == (int)a && side == 0); sc[t][1] += (t == (int)a && side == 1); }
-                // updateCounts (:231-248) with f == g: the [i][j] and [j][i] sums are identical sequences
+                // f == g: the [i][j] and [j][i] sums are identical sequences
                 L00 += a == 0 ? A : E;
                 L11 += a == 1 ? A : E;
                 L22 += a == 2 ? A : E;
@@ -184,14 +220,15 @@ __global__ __launch_bounds__(256) void k_posterior(const QueueSite* __restrict__
                 L13 += (a & 1) == 1 ? H : E;
                 L23 += a >= 2 ? H : E;
             }
+            if (__ballot(!in)) break;
         }
-        if (total == 0) return false;                   // VariantDiscoverySNVQAlgorithm.java:101-103
-        const bool callable = (rc & 0x80) != 0;
+        if (total == 0 || (gp.ablate & 8)) continue;                      // VariantDiscoverySNVQAlgorithm.java:101-103
+        const bool callable = (rc & 0x80u) != 0;
         int8_t genotype = -1, alt = -1, third = -1, nal = 0;
         int16_t gq = 0, qual = 0;
         bool keep = false;
         if (callable) {
-            const int refIdx = (rc >> 5) & 3;
+            const int refIdx = (int)((rc >> 5) & 3u);
             const double ph = gp.log_prior_homo, px = gp.log_prior_hetero;
             // getPosteriorProbabilities (CountsHelper.java:410-443): events in Java order;
             // row i holds post(i,i) at 4i and post(i,j) at 4i+1+j (j<i) or 4i+j (j>i)
@@ -199,16 +236,21 @@ __global__ __launch_bounds__(256) void k_posterior(const QueueSite* __restrict__
                              L11 + ph, L01 + px, L12 + px, L13 + px,
                              L22 + ph, L02 + px, L12 + px, L23 + px,
                              L33 + ph, L03 + px, L13 + px, L23 + px};
-            // calculatePosteriorProbabilities (:472-495)
+            // calculatePosteriorProbabilities (:472-495): lane k % 16 evaluates event k's power of
+            // ten, then the normaliser is summed in Java's order
             double logMax = 1;
 #pragma unroll
             for (int k = 0; k < 16; k++)
                 if (logMax > 0 || logMax < ev[k]) logMax = ev[k];
+            double mine = 0;
+#pragma unroll
+            for (int k = 0; k < 16; k++) mine = (lane & 15) == k ? ev[k] : mine;
+            const double x = mine - logMax;
+            const double pk = x < -20 ? 0.0 : pow(10.0, x);
             double totalProb = 0;
 #pragma unroll
             for (int k = 0; k < 16; k++) {
-                const double x = ev[k] - logMax;
-                ev[k] = x < -20 ? 0.0 : pow(10.0, x);
+                ev[k] = readlane_d(pk, k);
                 totalProb += ev[k];
             }
 #pragma unroll
@@ -249,50 +291,78 @@ __global__ __launch_bounds__(256) void k_posterior(const QueueSite* __restrict__
             }
             if (keep && gp.min_quality > gq) keep = false;
         }
-        if (!keep && !gp.dump_all) return false;
-        o.seq_id = -1;
-        o.pos = gpos;
-        o.ref = callable ? "ACGT"[(rc >> 5) & 3] : 'N';
-        o.n_alleles = nal;
-        o.alt = alt;
-        o.third = third;
-        o.genotype = genotype;
-        o.strand_bias = -1;
-        o.gq = gq;
-        o.qual = qual;
-        o.is_call = keep ? 1 : 0;
-        o.dp = total;
-        o.counts[0] = (int32_t)c0; o.counts[1] = (int32_t)c1; o.counts[2] = (int32_t)c2; o.counts[3] = (int32_t)c3;
+        if (!keep && !gp.dump_all) continue;
+        if (ns == kPostStage) { post_flush(s_rec[wv], ns, lane, out, counters, cap); ns = 0; }
+        if (lane == 0) {
+            ngsep_site_out& o = s_rec[wv][ns];
+            o.seq_id = -1;
+            o.pos = gpos;
+            o.ref = callable ? "ACGT"[(rc >> 5) & 3] : 'N';
+            o.n_alleles = nal;
+            o.alt = alt;
+            o.third = third;
+            o.genotype = genotype;
+            o.strand_bias = -1;
+            o.gq = gq;
+            o.qual = qual;
+            o.is_call = keep ? 1 : 0;
+            o.dp = total;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            o.strand_counts[k][0] = sc[k][0];
-            o.strand_counts[k][1] = sc[k][1];
+            for (int k = 0; k < 4; k++) {
+                o.counts[k] = cnt[k];
+                o.strand_counts[k][0] = sc[k][0];
+                o.strand_counts[k][1] = sc[k][1];
+            }
+            o.logc[0] = L00; o.logc[1] = L01; o.logc[2] = L02; o.logc[3] = L03; o.logc[4] = L11;
+            o.logc[5] = L12; o.logc[6] = L13; o.logc[7] = L22; o.logc[8] = L23; o.logc[9] = L33;
         }
-        o.logc[0] = L00; o.logc[1] = L01; o.logc[2] = L02; o.logc[3] = L03; o.logc[4] = L11;
-        o.logc[5] = L12; o.logc[6] = L13; o.logc[7] = L22; o.logc[8] = L23; o.logc[9] = L33;
-        return true;
-    };
-    // wave-uniform grid-stride loop: one output reservation per wave (ballot), not per site
-    const int lane = threadIdx.x & 63;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t ib = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); ib < n; ib += stride) {
-        const int64_t i = ib + lane;
-        ngsep_site_out o;
-        const bool emit = i < n && site(i, o);
-        const unsigned long long m = __ballot(emit);
-        if (!m) continue;
-        unsigned long long base = 0;
-        if (lane == __ffsll((long long)m) - 1) base = atomicAdd(&counters[0], (unsigned long long)__popcll(m));
-        base = __shfl(base, __ffsll((long long)m) - 1, 64);
-        const unsigned long long idx = base + __popcll(m & ((1ull << lane) - 1ull));
-        if (emit && (int64_t)idx < cap) out[idx] = o;
+        ns++;
     }
+    // one reservation per workgroup for the staged records
+    if (lane == 0) s_n[wv] = ns;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long tot = 0;
+        for (int w = 0; w < kPostWaves; w++) tot += (unsigned long long)s_n[w];
+        s_base = tot ? atomicAdd(&counters[0], tot) : 0ull;
+    }
+    __syncthreads();
+    unsigned long long base = s_base;
+    for (int w = 0; w < wv; w++) base += (unsigned long long)s_n[w];
+    constexpr int W = sizeof(ngsep_site_out) / 4;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(s_rec[wv]);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(out);
+    for (int k = lane; k < ns * W; k += 64)
+        if ((int64_t)base + k / W < cap) dst[(base * W) + k] = src[k];
 }
 
 
 // ------------------------------------------------------------------------------------------
-// KT: pileup tile scan over the tile-blocked pileup matrix
+// KT: pileup tile scan over the tile-blocked pileup matrix -- one wavefront per tile
 // ------------------------------------------------------------------------------------------
+// Tile t is rows_t x T code bytes, row-major, U = T/16 sixteen-byte units per row (T <= 1024, so
+// U <= 64).  Lane l of the wave owns column c = l % U (positions 16c .. 16c+15 of the tile) and
+// rows l/U, l/U + 64/U, ... : wave-load j fetches the contiguous kilobyte of units 64j .. 64j+63
+// (buffer loads, bounds-checked by the descriptor, so a short tile reads zeros past its end --
+// no branches around the loads), and every unit a lane holds belongs to its own column.
+//   phase 1  per-lane OR of the unit hit masks, then OR across the lanes of a column (shuffles):
+//            the positions whose pileup holds a valid non-reference call (MODE 0) or any counted
+//            call (MODE 1), restricted to callable / in-window positions.  Every other position is
+//            hom-ref (DESIGN.md "why pruning is exact") or has no pileup.  This is
+//            AlignmentsPileupGenerator.processCurrentPosition (discovery/AlignmentsPileupGenerator.java:475-498)
+//            reduced to the fact that decides whether SNVQ can call a variant there.  The same pass
+//            counts reference / other valid calls per position (byte-wise SWAR counters).
+//   phase 2  (MODE 0) count bound: a candidate whose counts already prove it hom-ref is dropped.
+//            The rest get the integer hom-ref bound: the lanes of a column re-read (L2-warm) their
+//            rows' byte at the candidate position and sum its fixed-point addends (integers:
+//            order-independent, so exact), then add up across the column's lanes.
+//   phase 3  a candidate the bounds prove hom-ref is dropped; the others are staged in LDS and
+//            queued for k_posterior (one global reservation per workgroup).
+// No LDS traffic on the streamed bytes, no workgroup barriers inside the tile loop.
+constexpr int kScanChunk = 8;           // wave-loads (16 B per lane) in flight per chunk
+constexpr int kScanWaves = kScanThreads / 64;
+constexpr int kWaveQ = 512;             // survivors staged per wave before a global reservation
+
 // nonzero-allele valid bytes (MODE 0: a valid call that is not the reference allele, codes are
 // allele-XOR-reference) or any counted byte (MODE 1), one bit per byte
 template <int MODE>
@@ -305,222 +375,214 @@ __device__ inline uint32_t unit_hits(const u32x4 d) {
     };
     return f(d.x) | (f(d.y) << 4) | (f(d.z) << 8) | (f(d.w) << 12);
 }
+// dword `sel` (0..3) of a unit without dynamic register indexing
+__device__ inline uint32_t unit_dword(const u32x4 d, int sel) {
+    const uint32_t lo = (sel & 1) ? d.y : d.x, hi = (sel & 1) ? d.w : d.z;
+    return (sel & 2) ? hi : lo;
+}
 
-//   phase 1  stream the tile's block of the pileup matrix (rows_t x T bytes, one coalesced
-//            16-byte load per lane and unit, kept in registers) and mark the positions whose pileup
-//            holds a valid non-reference call (MODE 0) or any counted call (MODE 1): LDS bitmap,
-//            restricted to callable / in-window positions.  Every other position is hom-ref
-//            (DESIGN.md "why pruning is exact") or has no pileup.  This is
-//            AlignmentsPileupGenerator.processCurrentPosition (discovery/AlignmentsPileupGenerator.java:475-498)
-//            reduced to the fact that decides whether SNVQ can call a variant there.
-//   phase 2  (MODE 0) integer hom-ref bound of every candidate: one LDS atomic per valid call at a
-//            candidate position adds its fixed-point contribution to the candidate's reference or
-//            allele accumulator (integer sums: order-independent, so exact).
-//   phase 3  a candidate the bound proves hom-ref is dropped; the others are queued for k_posterior.
-struct TileShared {
-    uint32_t bits[kTileMaxPos / 32];        // candidate bitmap
-    uint32_t ok[kTileMaxPos / 32];          // callable (MODE 0) / in-window (MODE 1) positions
-    int32_t pref[kTileMaxPos / 32 + 1];
+struct ScanShared {
     unsigned long long w[2][32];            // bound addends: [0] reference call, [1] other allele
-    unsigned long long acc[kCandCap * 4];   // per candidate: R, X[1..3] (indexed by allele XOR reference)
-    QueueSite q[kQueueStage];               // survivors staged for one global reservation per flush
-    int32_t qn;
-    int32_t qbase;
-    unsigned long long ncand;               // candidates seen by this block (statistics)
+    QueueSite q[kScanWaves][kWaveQ];        // survivors staged per wave
+    int32_t qn[kScanWaves];
+    int32_t qbase[kScanWaves];
+    unsigned long long ncand[kScanWaves];
 };
 
-// moves the block's staged survivors to the global queue with ONE atomic (same-address global
-// atomics from every tile serialise in L2 and were the scan's bottleneck)
-__device__ __forceinline__ void flush_queue(TileShared& sh, QueueSite* __restrict__ queue,
-                                            unsigned long long* __restrict__ counters, int64_t qcap) {
-    __syncthreads();
-    const int32_t n = sh.qn;
-    if (n == 0) return;
-    if (threadIdx.x == 0) sh.qbase = (int32_t)atomicAdd(&counters[2], (unsigned long long)n);
-    __syncthreads();
-    const int64_t base = sh.qbase;
-    for (int i = threadIdx.x; i < n; i += kScanThreads)
-        if (base + i < qcap) queue[base + i] = sh.q[i];
-    __syncthreads();
-    if (threadIdx.x == 0) sh.qn = 0;
-    __syncthreads();
+// wave-level reservation of the wave's staged survivors in the global queue
+__device__ __forceinline__ void wave_flush(ScanShared& sh, int wv, int lane, int32_t n, QueueSite* __restrict__ queue,
+                                           unsigned long long* __restrict__ counters, int64_t qcap) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(&counters[2], (unsigned long long)n);
+    base = __shfl(base, 0, 64);
+    for (int i = lane; i < n; i += 64)
+        if ((int64_t)base + i < qcap) queue[base + i] = sh.q[wv][i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 template <int MODE>
-__device__ __forceinline__ void tile_body(TileShared& sh, const int64_t tile, const TileInfo ti,
-    const u32x4* __restrict__ pile, const uint8_t* __restrict__ ref,
-    int32_t log2T, const LikTables* __restrict__ tabs, const GenotypeParams& gp,
-    QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap) {
-    uint32_t* s_bits = sh.bits;
-    uint32_t* s_ok = sh.ok;
-    int32_t* s_pref = sh.pref;
-    unsigned long long (*s_w)[32] = sh.w;
-    unsigned long long* s_acc = sh.acc;
-    if (ti.rows == 0 || (gp.ablate & 4)) return;
-    const int tid = threadIdx.x;
-    const int32_t T = 1 << log2T;
-    const int32_t tstart = (int32_t)(tile << log2T);
-    const int nw = T >= 32 ? T / 32 : 1;
-    const int log2U = log2T - 4;                                // units per row = T/16
-    const int32_t nunits = ti.rows << log2U;
-    const u32x4* blk = pile + (ti.off >> 4);
-
-    // phase 1: issue every register-resident unit load first
-    u32x4 U[kUnitsPerThread];
-#pragma unroll
-    for (int k = 0; k < kUnitsPerThread; k++) {
-        const int32_t u = tid + k * kScanThreads;
-        U[k] = u < nunits ? blk[u] : u32x4{0u, 0u, 0u, 0u};
-    }
-    // position masks from the reference codes: one dword (4 positions) per thread, eight
-    // neighbouring lanes OR their nibbles into one bitmap word
-    {
-        const uint32_t* refw = reinterpret_cast<const uint32_t*>(ref + tstart);
-        for (int i0 = 0; i0 < T / 4; i0 += kScanThreads) {
-            const int i = i0 + tid;
-            uint32_t bits = 0;
-            if (i < T / 4) {
-                const uint32_t v = refw[i];
-                const uint32_t m = MODE == 0 ? (v & 0x80808080u) : ((((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u);
-                bits = nib4(m) << (4 * (i & 7));
-            }
-            bits |= __shfl_xor(bits, 1, 64);
-            bits |= __shfl_xor(bits, 2, 64);
-            bits |= __shfl_xor(bits, 4, 64);
-            if ((i & 7) == 0 && i < T / 4) {
-                s_ok[i >> 3] = bits;
-                s_bits[i >> 3] = 0;
-            }
-        }
-        if (T < 32 && tid == 0) s_bits[0] = 0;
-    }
-    if (MODE == 0) {
-        if (tid < 64) s_w[tid >> 5][tid & 31] = (tid < 32 ? tabs->wR : tabs->wX)[tid & 31];
-        for (int i = tid; i < kCandCap * 4; i += kScanThreads) s_acc[i] = 0;
-    }
-    __syncthreads();
-    const uint32_t colmask = (1u << log2U) - 1u;
-    auto mark = [&](const u32x4 d, int32_t u) {
-        const uint32_t m = unit_hits<MODE>(d);
-        if (m) {
-            const int32_t p = (int32_t)(((uint32_t)u & colmask) << 4);   // tile-relative position of byte 0
-            const uint32_t sh = (uint32_t)p & 16u;
-            atomicOr(&s_bits[p >> 5], (m & (s_ok[p >> 5] >> sh)) << sh);
-        }
-    };
-#pragma unroll
-    for (int k = 0; k < kUnitsPerThread; k++) {
-        const int32_t u = tid + k * kScanThreads;
-        if (u < nunits) mark(U[k], u);
-    }
-    for (int32_t u = tid + kUnitsPerThread * kScanThreads; u < nunits; u += kScanThreads) mark(blk[u], u);   // deep tiles
-    __syncthreads();
-    // candidate prefix counts over bitmap words (nw <= 64: one word per lane of wave 0)
-    if (tid < 64) {
-        const int32_t v = tid < nw ? __popc(s_bits[tid]) : 0;
-        int32_t incl = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t n = __shfl_up(incl, o, 64);
-            if (tid >= o) incl += n;
-        }
-        if (tid < nw) s_pref[tid] = incl - v;
-        if (tid == 63) s_pref[nw] = incl;
-    }
-    __syncthreads();
-    const int32_t ncand = s_pref[nw];
-    if (ncand == 0) return;
-    if (tid == 0) sh.ncand += (unsigned long long)ncand;
-    if (gp.ablate & 1) return;                               // diagnostics: scan only
-    const bool bound = MODE == 0 && gp.use_bound;
-    if (bound) {
-        // phase 2: one LDS atomic per valid call at a candidate position
-        auto accumulate = [&](const u32x4 d, int32_t u) {
-            const int32_t p = (int32_t)(((uint32_t)u & colmask) << 4);
-            uint32_t cm = (s_bits[p >> 5] >> ((uint32_t)p & 16u)) & 0xFFFFu;
-            if (!cm) return;
-            cm &= unit_valid_mask(d);
-            while (cm) {
-                const int k = __builtin_ctz(cm);
-                cm &= cm - 1;
-                const int32_t pos = p + k;
-                const uint32_t cd = unit_byte(d, k);
-                const uint32_t a = (cd >> 5) & 3;                   // allele XOR reference allele
-                int q = cd & 31;
-                q = q > gp.max_q ? gp.max_q : q;
-                const int w = pos >> 5;
-                const int32_t ci = s_pref[w] + __popc(s_bits[w] & ((1u << (pos & 31)) - 1u));
-                if (ci < kCandCap) atomicAdd(&s_acc[ci * 4 + (int)a], s_w[a == 0 ? 0 : 1][q]);
-            }
-        };
-#pragma unroll
-        for (int k = 0; k < kUnitsPerThread; k++) {
-            const int32_t u = tid + k * kScanThreads;
-            if (u < nunits) accumulate(U[k], u);
-        }
-        for (int32_t u = tid + kUnitsPerThread * kScanThreads; u < nunits; u += kScanThreads) accumulate(blk[u], u);
-        __syncthreads();
-    }
-    // phase 3: decide every candidate.  Candidate c runs on thread (c%4)*64 + c/4 so that a tile's
-    // few candidates spread over all four waves (SIMDs) instead of queueing on one.
-    for (int32_t c0 = 0; c0 < ncand; c0 += kScanThreads) {
-        if (c0 > 0 || sh.qn > kQueueStage - kScanThreads) flush_queue(sh, queue, counters, qcap);   // room for one chunk
-        const int32_t c = c0 + (tid & 63) * 4 + (tid >> 6);
-        if (c >= ncand) continue;
-        int lo = 0, hi = nw - 1;              // last word whose prefix <= c
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (s_pref[mid] <= c) lo = mid; else hi = mid - 1;
-        }
-        uint32_t w = s_bits[lo];
-        for (int k = c - s_pref[lo]; k > 0; k--) w &= w - 1;
-        const int32_t gpos = tstart + lo * 32 + __builtin_ctz(w);
-        bool drop = false;
-        if (bound && c < kCandCap) {
-            // hom-ref if, for every other genotype G, the lower bound of L[r][r]-L[G] keeps
-            // P(G) (het: P(x,y)+P(y,x)) <= P(r,r)  (DESIGN.md "hom-ref bound").  Accumulators are
-            // indexed by allele XOR reference: 0 = reference, 1..3 = the three other alleles.
-            const unsigned long long Rp = s_acc[c * 4];
-            const long long R1 = (long long)(Rp & 0xFFFFFFFFull), R2 = (long long)(Rp >> 32);
-            const unsigned long long Xa = s_acc[c * 4 + 1], Xb = s_acc[c * 4 + 2], Xc = s_acc[c * 4 + 3];
-            const long long a1 = (long long)(Xa & 0xFFFFFFFFull), b1 = (long long)(Xb & 0xFFFFFFFFull);
-            const long long c1 = (long long)(Xc & 0xFFFFFFFFull);
-            const long long a2 = (long long)(Xa >> 32), b2 = (long long)(Xb >> 32), c2 = (long long)(Xc >> 32);
-            const long long th = tabs->t_het, to = tabs->t_homo;
-            // het (r,x): R1 - X1[x];  hom (x,x): R2 - X2[x];  het (x,y), x,y != r: R2 - X1[x] - X1[y]
-            drop = (R1 - a1 > th) && (R1 - b1 > th) && (R1 - c1 > th) &&
-                   (R2 - a2 > to) && (R2 - b2 > to) && (R2 - c2 > to) &&
-                   (R2 - a1 - b1 > th) && (R2 - a1 - c1 > th) && (R2 - b1 - c1 > th);
-        }
-        if (drop) continue;
-        sh.q[atomicAdd(&sh.qn, 1)] = QueueSite{gpos, (int32_t)ref[gpos]};
-    }
-}
-
-// Persistent grid: block b works on XCD b % 8 (round-robin placement, speed only) through that
-// XCD's contiguous share of the tiles, so neighbouring tiles stay in one L2.
-template <int MODE>
-__global__ __launch_bounds__(kScanThreads) void k_tile_pileup(
+#ifndef NGSEP_KT_WAVES_PER_EU
+#define NGSEP_KT_WAVES_PER_EU 5      // build-time tuning: resident waves per SIMD the register budget targets
+#endif
+__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(NGSEP_KT_WAVES_PER_EU)))
+void k_tile_pileup(
     const u32x4* __restrict__ pile, const TileInfo* __restrict__ tinfo, const uint8_t* __restrict__ ref,
     int32_t log2T, int64_t n_tiles, const LikTables* __restrict__ tabs, GenotypeParams gp,
     QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap) {
-    __shared__ TileShared sh;
-    const int64_t nb = gridDim.x, b = blockIdx.x;
-    const int64_t xcd = b % 8, j = b / 8, nbx = (nb - xcd + 7) / 8;
-    const int64_t q8 = n_tiles / 8, r8 = n_tiles % 8;
-    const int64_t c0 = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
-    const int64_t c1 = c0 + q8 + (xcd < r8 ? 1 : 0);
-    if (threadIdx.x == 0) { sh.qn = 0; sh.ncand = 0; }
+    __shared__ ScanShared sh;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (threadIdx.x < 64) sh.w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
     __syncthreads();
-    TileInfo next = c0 + j < c1 ? tinfo[c0 + j] : TileInfo{0, 0, 0};
-    for (int64_t t = c0 + j; t < c1; t += nbx) {
-        const TileInfo ti = next;
-        if (t + nbx < c1) next = tinfo[t + nbx];   // descriptor of the next tile in flight meanwhile
-        tile_body<MODE>(sh, t, ti, pile, ref, log2T, tabs, gp, queue, counters, qcap);
-        __syncthreads();   // the shared tile state is reused by the next tile
+    const int log2U = log2T - 4;
+    const uint32_t U = 1u << log2U;
+    const int col = lane & (int)(U - 1);
+    const bool lead = lane < (int)U;               // phase-0 lane of its column: reports the column's candidates
+    const bool bound_on = MODE == 0 && gp.use_bound;
+    const long long th = tabs->t_het, to = tabs->t_homo;
+    const int32_t maxq = gp.max_q;
+    int32_t qn = 0;                                 // wave-uniform count of staged survivors
+    unsigned long long ncand = 0;
+    const int64_t nwaves = (int64_t)gridDim.x * kScanWaves;
+    const int64_t t0 = (int64_t)blockIdx.x * kScanWaves + wv;
+    TileInfo nxt = t0 < n_tiles ? tinfo[t0] : TileInfo{0, 0, 0};
+    for (int64_t t = t0; t < n_tiles; t += nwaves) {
+        if (gp.ablate & 4) break;
+        const TileInfo ti = nxt;
+        if (t + nwaves < n_tiles) nxt = tinfo[t + nwaves];    // the next descriptor is in flight meanwhile
+        const int32_t rows = __builtin_amdgcn_readfirstlane(ti.rows);
+        if (rows == 0) continue;
+        const int32_t nunits = rows << log2U;
+        const int64_t off = ((int64_t)__builtin_amdgcn_readfirstlane((int32_t)(ti.off >> 32)) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)ti.off);
+        const u32x4* blk = pile + (off >> 4);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)blk, 0, nunits * 16, 0x00020000);
+        const int32_t tstart = (int32_t)(t << log2T);
+        const u32x4 rc = *reinterpret_cast<const u32x4*>(ref + tstart + col * 16);
+        uint32_t ok;
+        {
+            auto okf = [](uint32_t v) -> uint32_t {
+                return nib4(MODE == 0 ? (v & 0x80808080u) : ((((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u));
+            };
+            ok = okf(rc.x) | (okf(rc.y) << 4) | (okf(rc.z) << 8) | (okf(rc.w) << 12);
+        }
+        uint32_t hits = 0;
+        uint32_t nr0 = 0, nr1 = 0, nr2 = 0, nr3 = 0, na0 = 0, na1 = 0, na2 = 0, na3 = 0;   // byte-wise call counts
+        auto scan = [&](const u32x4 d) {
+            hits |= unit_hits<MODE>(d);
+            if (MODE == 0) {
+                auto cnt = [](uint32_t w, uint32_t& r, uint32_t& x) {
+                    const uint32_t v = w & 0x80808080u;                              // valid calls
+                    const uint32_t n = w & ((w & 0x60606060u) + 0x60606060u) & 0x80808080u;   // ... not the reference allele
+                    r += (v ^ n) >> 7;
+                    x += n >> 7;
+                };
+                cnt(d.x, nr0, na0); cnt(d.y, nr1, na1); cnt(d.z, nr2, na2); cnt(d.w, nr3, na3);
+            }
+        };
+        // stream the block: chunks of kScanChunk wave-loads (8 KiB per wave) issued back to back;
+        // loads past the block's end return zeros, which hold no calls
+        for (int32_t u0 = 0; u0 < nunits; u0 += kScanChunk * 64) {
+            u32x4 R[kScanChunk];
+#pragma unroll
+            for (int j = 0; j < kScanChunk; j++)
+                R[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u0 + j * 64 + lane) * 16, 0, 0));
+#pragma unroll
+            for (int j = 0; j < kScanChunk; j++) scan(R[j]);
+        }
+        for (int s = (int)U; s < 64; s <<= 1) hits |= __shfl_xor(hits, s, 64);
+        uint32_t cm = hits & ok;
+        if (lead) ncand += (unsigned long long)__popc(cm);
+        if (gp.ablate & 1) continue;                                  // diagnostics: scan only
+        const bool bound = bound_on && rows <= 255;                   // byte counters and 32-bit sums cannot overflow
+        if (bound && __ballot(cm != 0)) {
+            // count bound: with nr reference and na other valid calls at the position, the exact
+            // integer sums below satisfy R >= nr * (smallest addend) and X <= na * (largest), so a
+            // candidate that passes with those is hom-ref without walking its column.  Most candidates
+            // are one or two sequencing errors in a deep pileup and end here.
+            for (int s = (int)U; s < 64; s <<= 1) {
+                nr0 += __shfl_xor(nr0, s, 64); nr1 += __shfl_xor(nr1, s, 64);
+                nr2 += __shfl_xor(nr2, s, 64); nr3 += __shfl_xor(nr3, s, 64);
+                na0 += __shfl_xor(na0, s, 64); na1 += __shfl_xor(na1, s, 64);
+                na2 += __shfl_xor(na2, s, 64); na3 += __shfl_xor(na3, s, 64);
+            }
+            const u32x4 nref = {nr0, nr1, nr2, nr3}, nalt = {na0, na1, na2, na3};
+            uint32_t c = cm;
+            while (c) {
+                const int k = __builtin_ctz(c);
+                c &= c - 1u;
+                const long long nr = (unit_dword(nref, k >> 2) >> (8 * (k & 3))) & 0xFFu;
+                const long long na = (unit_dword(nalt, k >> 2) >> (8 * (k & 3))) & 0xFFu;
+                if (nr * tabs->c_r1 - na * tabs->c_x1 > th && nr * tabs->c_r2 - na * tabs->c_x2 > to &&
+                    nr * tabs->c_r2 - na * tabs->c_x1 > th)
+                    cm &= ~(1u << k);
+            }
+        }
+        // wave-uniform candidate loop: the lanes of one column hold the same mask, so they visit the
+        // same position in the same iteration and their partial sums meet in the shuffles below
+        while (__ballot(cm != 0)) {
+            const bool has = cm != 0;
+            const int k = has ? __builtin_ctz(cm) : 0;
+            cm &= cm - 1u;
+            const int sel = k >> 2, shb = 8 * (k & 3);
+            bool keep = has;
+            if (bound) {
+                unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;   // indexed by allele XOR reference
+                auto add = [&](const u32x4 d) {
+                    const uint32_t cd = (unit_dword(d, sel) >> shb) & 0xFFu;
+                    if (cd & 0x80u) {
+                        const uint32_t a = (cd >> 5) & 3u;
+                        int q = (int)(cd & 31u);
+                        q = q > maxq ? maxq : q;
+                        const unsigned long long w = sh.w[a == 0 ? 0 : 1][q];
+                        a0 += a == 0 ? w : 0ull;
+                        a1 += a == 1 ? w : 0ull;
+                        a2 += a == 2 ? w : 0ull;
+                        a3 += a == 3 ? w : 0ull;
+                    }
+                };
+                for (int32_t u0 = 0; u0 < nunits; u0 += 4 * 64) {   // re-read (L2-warm)
+                    u32x4 R[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        R[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u0 + j * 64 + lane) * 16, 0, 0));
+#pragma unroll
+                    for (int j = 0; j < 4; j++) add(R[j]);
+                }
+                for (int s = (int)U; s < 64; s <<= 1) {
+                    a0 += __shfl_xor(a0, s, 64);
+                    a1 += __shfl_xor(a1, s, 64);
+                    a2 += __shfl_xor(a2, s, 64);
+                    a3 += __shfl_xor(a3, s, 64);
+                }
+                // hom-ref if, for every other genotype G, the lower bound of L[r][r]-L[G] keeps
+                // P(G) (het: P(x,y)+P(y,x)) <= P(r,r)  (DESIGN.md "hom-ref bound").
+                // het (r,x): R1 - X1[x];  hom (x,x): R2 - X2[x];  het (x,y), x,y != r: R2 - X1[x] - X1[y]
+                const long long R1 = (long long)(a0 & 0xFFFFFFFFull), R2 = (long long)(a0 >> 32);
+                const long long x1 = (long long)(a1 & 0xFFFFFFFFull), y1 = (long long)(a2 & 0xFFFFFFFFull);
+                const long long z1 = (long long)(a3 & 0xFFFFFFFFull);
+                const long long x2 = (long long)(a1 >> 32), y2 = (long long)(a2 >> 32), z2 = (long long)(a3 >> 32);
+                const bool drop = (R1 - x1 > th) && (R1 - y1 > th) && (R1 - z1 > th) &&
+                                  (R2 - x2 > to) && (R2 - y2 > to) && (R2 - z2 > to) &&
+                                  (R2 - x1 - y1 > th) && (R2 - x1 - z1 > th) && (R2 - y1 - z1 > th);
+                keep = has && !drop;
+            }
+            const bool emit = keep && lead;
+            const unsigned long long m = __ballot(emit);
+            if (!m) continue;
+            const int32_t nm = __popcll(m);
+            if (qn + nm > kWaveQ) { wave_flush(sh, wv, lane, qn, queue, counters, qcap); qn = 0; }
+            if (emit) {
+                const int32_t idx = qn + __popcll(m & ((1ull << lane) - 1ull));
+                const uint32_t rcode = (unit_dword(rc, sel) >> shb) & 0xFFu;
+                sh.q[wv][idx] = QueueSite{tstart + col * 16 + k, (int32_t)rcode};
+            }
+            qn += nm;
+        }
     }
-    flush_queue(sh, queue, counters, qcap);
-    if (threadIdx.x == 0 && sh.ncand) atomicAdd(&counters[1], sh.ncand);
+    // one global reservation per workgroup for what its waves staged; one statistics atomic
+    for (int s = 1; s < 64; s <<= 1) ncand += __shfl_xor(ncand, s, 64);
+    if (lane == 0) { sh.qn[wv] = qn; sh.ncand[wv] = ncand; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t tot = 0;
+        unsigned long long nc = 0;
+        for (int w = 0; w < kScanWaves; w++) { sh.qbase[w] = tot; tot += sh.qn[w]; nc += sh.ncand[w]; }
+        const unsigned long long base = tot ? atomicAdd(&counters[2], (unsigned long long)tot) : 0ull;
+        for (int w = 0; w < kScanWaves; w++) sh.qbase[w] += (int32_t)base;   // queue indices fit 31 bits (g_len < 2^31)
+        if (nc) atomicAdd(&counters[1], nc);
+    }
+    __syncthreads();
+    {
+        const int64_t base = sh.qbase[wv];
+        for (int i = lane; i < qn; i += 64)
+            if (base + i < qcap) queue[base + i] = sh.q[wv][i];
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -541,15 +603,16 @@ __global__ __launch_bounds__(256) void kl_read_index(const int4* __restrict__ re
 }
 
 // ------------------------------------------------------------------------------------------
-// KO: order the emitted records by global position (counting sort on 4096-position buckets,
-//     insertion sort inside a bucket: a handful of records each)
+// KO: order the emitted records by global position: counting sort of (position, record) keys on
+//     2^shift-position buckets, insertion sort inside a bucket (a handful of keys each), then one
+//     coalesced gather of the records in key order
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void ko_hist(const ngsep_site_out* __restrict__ recs, const unsigned long long* n_ptr,
-                                               int64_t cap, int32_t* __restrict__ bucket) {
+                                               int64_t cap, int32_t* __restrict__ bucket, int shift) {
     int64_t n = (int64_t)*n_ptr;
     if (n > cap) n = cap;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        atomicAdd(&bucket[recs[i].pos >> 12], 1);
+        atomicAdd(&bucket[recs[i].pos >> shift], 1);
 }
 // exclusive scan of nb bucket counts into start[0..nb] (one workgroup of 1024)
 __global__ __launch_bounds__(1024) void ko_scan(const int32_t* __restrict__ bucket, int32_t* __restrict__ start,
@@ -574,24 +637,51 @@ __global__ __launch_bounds__(1024) void ko_scan(const int32_t* __restrict__ buck
 }
 __global__ __launch_bounds__(256) void ko_scatter(const ngsep_site_out* __restrict__ recs, const unsigned long long* n_ptr,
                                                   int64_t cap, int32_t* __restrict__ cursor,
-                                                  ngsep_site_out* __restrict__ sorted) {
+                                                  unsigned long long* __restrict__ keys, int shift) {
     int64_t n = (int64_t)*n_ptr;
     if (n > cap) n = cap;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t slot = atomicAdd(&cursor[recs[i].pos >> 12], 1);
-        sorted[slot] = recs[i];
+        const uint32_t pos = (uint32_t)recs[i].pos;
+        const int32_t slot = atomicAdd(&cursor[pos >> shift], 1);
+        keys[slot] = ((unsigned long long)pos << 32) | (unsigned long long)i;
     }
 }
-__global__ __launch_bounds__(256) void ko_bucket_sort(ngsep_site_out* __restrict__ sorted,
+// one wavefront per bucket: every key's rank among the bucket's keys (positions are distinct) is
+// its place; the keys are read from L2, a bucket holds a handful
+__global__ __launch_bounds__(256) void ko_bucket_sort(const unsigned long long* __restrict__ keys,
+                                                      unsigned long long* __restrict__ sorted_keys,
                                                       const int32_t* __restrict__ start, int64_t nb) {
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= nb) return;
-    const int32_t a = start[b], z = start[b + 1];
-    for (int32_t i = a + 1; i < z; i++) {
-        const ngsep_site_out v = sorted[i];
-        int32_t k = i;
-        while (k > a && sorted[k - 1].pos > v.pos) { sorted[k] = sorted[k - 1]; k--; }
-        sorted[k] = v;
+    const int32_t a = start[b], z = start[b + 1], k = z - a;
+    if (k == 0) return;
+    if (k <= 64) {
+        const unsigned long long mine = lane < k ? keys[a + lane] : ~0ull;
+        int32_t rank = 0;
+        for (int j = 0; j < k; j++) rank += __shfl(mine, j, 64) < mine;
+        if (lane < k) sorted_keys[a + rank] = mine;
+        return;
+    }
+    for (int32_t i = lane; i < k; i += 64) {
+        const unsigned long long mine = keys[a + i];
+        int32_t rank = 0;
+        for (int32_t j = 0; j < k; j++) rank += keys[a + j] < mine;
+        sorted_keys[a + rank] = mine;
+    }
+}
+__global__ __launch_bounds__(256) void ko_gather(const ngsep_site_out* __restrict__ recs,
+                                                 const unsigned long long* __restrict__ keys,
+                                                 const unsigned long long* n_ptr, int64_t cap,
+                                                 ngsep_site_out* __restrict__ sorted) {
+    constexpr int W = sizeof(ngsep_site_out) / 4;
+    int64_t n = (int64_t)*n_ptr;
+    if (n > cap) n = cap;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(recs);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(sorted);
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n * W; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = t / W, w = t - r * W;
+        dst[t] = src[(int64_t)(keys[r] & 0xFFFFFFFFull) * W + w];
     }
 }
 
@@ -663,6 +753,7 @@ void device_destroy(Device* d) {
     device_release(d);
     (void)hipFree(d->d_sites);
     (void)hipFree(d->d_sorted);
+    (void)hipFree(d->d_keys);
     (void)hipFree(d->d_bucket);
     (void)hipFree(d->d_hard);
     (void)hipFree(d->d_counters);
@@ -722,11 +813,16 @@ int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypePar
     if (want > d->cap_sites) {
         (void)hipFree(d->d_sites);
         (void)hipFree(d->d_sorted);
+        (void)hipFree(d->d_keys);
         HIP_TRY(hipMalloc(&d->d_sites, (size_t)want * sizeof(ngsep_site_out)));
         HIP_TRY(hipMalloc(&d->d_sorted, (size_t)want * sizeof(ngsep_site_out)));
+        HIP_TRY(hipMalloc(&d->d_keys, (size_t)want * 2 * sizeof(unsigned long long)));
         d->cap_sites = want;
     }
-    const int64_t nb = s.g_len / 4096 + 1;
+    // position buckets of the ordering pass: a few records each (calls are sparse; dump mode has one
+    // record per covered position)
+    const int shift = g.dump_all ? 4 : 12;
+    const int64_t nb = (s.g_len >> shift) + 1;
     if (nb > d->nb_cap) {
         (void)hipFree(d->d_bucket);
         HIP_TRY(hipMalloc(&d->d_bucket, (size_t)(3 * nb + 1) * sizeof(int32_t)));
@@ -745,10 +841,14 @@ int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypePar
         HIP_TRY(hipMemsetAsync(d->d_counters, 0, 4 * sizeof(unsigned long long), d->stream));
         HIP_TRY(hipEventRecord(d->ev[0], d->stream));
         if (d->n_tiles > 0) {
-            // persistent blocks: a few per CU, each loops over its XCD's tiles
-            int per_cu = kTileBlocksPerCU;
+            // persistent waves: as many workgroups as are co-resident (register-limited), each wave
+            // walks the tiles with a grid stride, so at any moment the waves stream one contiguous
+            // stretch of the pile
+            auto kt = prune ? (const void*)k_tile_pileup<0> : (const void*)k_tile_pileup<1>;
+            int per_cu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kt, kScanThreads, 0) != hipSuccess || per_cu < 1) per_cu = 2;
             if (const char* e = std::getenv("NGSEP_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(e));   // tuning
-            const int64_t nblk = std::min<int64_t>(d->n_tiles, (int64_t)d->n_cu * per_cu);
+            const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((d->n_tiles + kScanWaves - 1) / kScanWaves, (int64_t)d->n_cu * per_cu));
             dim3 grid((unsigned)nblk);
             if (prune)
                 hipLaunchKernelGGL(k_tile_pileup<0>, grid, dim3(kScanThreads), 0, d->stream, (const u32x4*)d->d_pile,
@@ -761,7 +861,7 @@ int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypePar
             HIP_TRY(hipGetLastError());
         }
         HIP_TRY(hipEventRecord(d->ev[1], d->stream));
-        hipLaunchKernelGGL(k_posterior, dim3(1024), dim3(256), 0, d->stream, d->d_hard, d->d_counters + 2, d->cap_hard,
+        hipLaunchKernelGGL(k_posterior, dim3(2048), dim3(kPostWaves * 64), 0, d->stream, d->d_hard, d->d_counters + 2, d->cap_hard,
                            d->d_reads, d->n_reads, d->d_lb, d->d_slots, d->slot_size, d->d_tables, g, d->d_sites,
                            d->d_counters, d->cap_sites);
         HIP_TRY(hipGetLastError());
@@ -771,11 +871,14 @@ int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypePar
         int32_t* start = d->d_bucket + nb;
         int32_t* cursor = d->d_bucket + 2 * nb + 1;
         HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)nb * sizeof(int32_t), d->stream));
-        hipLaunchKernelGGL(ko_hist, dim3(256), dim3(256), 0, d->stream, d->d_sites, d->d_counters, d->cap_sites, cnt);
+        hipLaunchKernelGGL(ko_hist, dim3(256), dim3(256), 0, d->stream, d->d_sites, d->d_counters, d->cap_sites, cnt, shift);
         hipLaunchKernelGGL(ko_scan, dim3(1), dim3(1024), 0, d->stream, cnt, start, cursor, nb);
         hipLaunchKernelGGL(ko_scatter, dim3(256), dim3(256), 0, d->stream, d->d_sites, d->d_counters, d->cap_sites, cursor,
+                           d->d_keys, shift);
+        unsigned long long* skeys = d->d_keys + d->cap_sites;    // second half: keys in position order
+        hipLaunchKernelGGL(ko_bucket_sort, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, d->stream, d->d_keys, skeys, start, nb);
+        hipLaunchKernelGGL(ko_gather, dim3(1024), dim3(256), 0, d->stream, d->d_sites, skeys, d->d_counters, d->cap_sites,
                            d->d_sorted);
-        hipLaunchKernelGGL(ko_bucket_sort, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, d->stream, d->d_sorted, start, nb);
         HIP_TRY(hipGetLastError());
     }
     // counters and a prefix of the ordered records in one round trip, straight into the result store
@@ -792,10 +895,13 @@ int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypePar
         // more calls than the record buffer holds (e.g. -minQuality 0): grow it and run again
         (void)hipFree(d->d_sites);
         (void)hipFree(d->d_sorted);
+        (void)hipFree(d->d_keys);
         d->d_sites = d->d_sorted = nullptr;
+        d->d_keys = nullptr;
         d->cap_sites = 0;
         HIP_TRY(hipMalloc(&d->d_sites, (size_t)(n + 1024) * sizeof(ngsep_site_out)));
         HIP_TRY(hipMalloc(&d->d_sorted, (size_t)(n + 1024) * sizeof(ngsep_site_out)));
+        HIP_TRY(hipMalloc(&d->d_keys, (size_t)(n + 1024) * 2 * sizeof(unsigned long long)));
         d->cap_sites = n + 1024;
         d->last_n_sites = n;
         return device_run(d, s, t, g, prune, out, n_out, scan_ms, geno_ms, total_ms, n_candidates, err);
