@@ -138,7 +138,8 @@ def main():
     st = sess.stats()
     n_sites = st.sites_called
     log(f"[rank {rank}] tile {st.tile_positions} positions (max {st.tile_rows_max} rows), pile {st.pile_bytes} B, "
-        f"slot {st.slot_size} B, {st.candidates} candidates, {st.hard_sites} needed the exact tally + posterior")
+        f"slot {st.slot_size} B, {st.candidates} candidates, {st.exact_bound_passes} exact-bound passes, "
+        f"{st.hard_sites} needed the exact tally + posterior")
     sess.release_staged()
     sess.close()
 

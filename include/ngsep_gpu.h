@@ -123,6 +123,7 @@ typedef struct ngsep_stats {
     int32_t slot_size;              /* bytes per read slot of the read-major SoA */
     int32_t hard_sites;             /* candidates that needed the exact tally + posterior */
     int64_t pile_bytes;             /* bytes of the tile-blocked pileup matrix streamed by the scan */
+    int64_t exact_bound_passes;     /* wavefront passes of the scan's exact integer hom-ref bound */
 } ngsep_stats;
 
 /* ---- context ---- */

@@ -104,6 +104,7 @@ class NgsepStats(ctypes.Structure):
         ("slot_size", ctypes.c_int32),
         ("hard_sites", ctypes.c_int32),
         ("pile_bytes", ctypes.c_int64),
+        ("exact_bound_passes", ctypes.c_int64),
     ]
 
 

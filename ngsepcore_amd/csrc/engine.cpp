@@ -683,6 +683,7 @@ int run_device(ngsep_ctx* c, double* elapsed_ms) {
     if (c->params.calc_strand_bias) apply_strand_bias(c->sites, from);
     c->stats.candidates = ncand;
     c->stats.hard_sites = (int32_t)device_last_hard(c->dev);
+    c->stats.exact_bound_passes = device_last_exact(c->dev);
     c->stats.sites_called += (int64_t)(c->sites.size() - from);
     c->stats.kernel_ms = total_ms;
     c->stats.scan_ms = scan_ms;

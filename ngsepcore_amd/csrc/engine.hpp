@@ -212,6 +212,7 @@ int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypePar
                int64_t* n_candidates, std::string& err);
 void device_release(Device* d);
 int64_t device_last_hard(const Device* d);
+int64_t device_last_exact(const Device* d);
 int device_count();
 // vcf.cpp
 std::string format_header(const ngsep_ctx* c);

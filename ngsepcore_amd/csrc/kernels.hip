@@ -69,6 +69,12 @@ struct Device {
     int32_t slot_size = 0, max_span = 0, pad = 0, tile = 512, log2_tile = 9;
     int64_t last_n_sites = 1024;
     int64_t last_hard = 0;
+    int64_t last_exact = 0;     // wave passes of KT's exact integer bound in the last run
+    int cpar = 0;               // counter set (of two) the next run uses
+    int64_t nb_clean = 0;       // bucket counts known to be zero
+    int kt_blocks_per_cu[2] = {0, 0};
+    LikTables h_tables;         // last uploaded tables (pinned copy source)
+    bool tables_valid = false;
     int32_t n_cu = 256;
 };
 
@@ -359,7 +365,10 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
 //   phase 3  a candidate the bounds prove hom-ref is dropped; the others are staged in LDS and
 //            queued for k_posterior (one global reservation per workgroup).
 // No LDS traffic on the streamed bytes, no workgroup barriers inside the tile loop.
-constexpr int kScanChunk = 8;           // wave-loads (16 B per lane) in flight per chunk
+#ifndef NGSEP_KT_CHUNK
+#define NGSEP_KT_CHUNK 16
+#endif
+constexpr int kScanChunk = NGSEP_KT_CHUNK;   // wave-loads (16 B per lane) in flight per chunk (build-time tuning)
 constexpr int kScanWaves = kScanThreads / 64;
 constexpr int kWaveQ = 512;             // survivors staged per wave before a global reservation
 
@@ -387,6 +396,7 @@ struct ScanShared {
     int32_t qn[kScanWaves];
     int32_t qbase[kScanWaves];
     unsigned long long ncand[kScanWaves];
+    uint32_t nexact[kScanWaves];
 };
 
 // wave-level reservation of the wave's staged survivors in the global queue
@@ -407,7 +417,7 @@ __device__ __forceinline__ void wave_flush(ScanShared& sh, int wv, int lane, int
 
 template <int MODE>
 #ifndef NGSEP_KT_WAVES_PER_EU
-#define NGSEP_KT_WAVES_PER_EU 5      // build-time tuning: resident waves per SIMD the register budget targets
+#define NGSEP_KT_WAVES_PER_EU 4      // build-time tuning: resident waves per SIMD the register budget targets
 #endif
 __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(NGSEP_KT_WAVES_PER_EU)))
 void k_tile_pileup(
@@ -428,6 +438,7 @@ void k_tile_pileup(
     const int32_t maxq = gp.max_q;
     int32_t qn = 0;                                 // wave-uniform count of staged survivors
     unsigned long long ncand = 0;
+    uint32_t nexact = 0;                            // wave passes of the exact integer bound (statistics)
     const int64_t nwaves = (int64_t)gridDim.x * kScanWaves;
     const int64_t t0 = (int64_t)blockIdx.x * kScanWaves + wv;
     TileInfo nxt = t0 < n_tiles ? tinfo[t0] : TileInfo{0, 0, 0};
@@ -451,47 +462,60 @@ void k_tile_pileup(
             };
             ok = okf(rc.x) | (okf(rc.y) << 4) | (okf(rc.z) << 8) | (okf(rc.w) << 12);
         }
+        // MODE 0 counts valid calls (cv) and non-reference valid calls (ca) per position, byte-wise
+        // (SWAR): a column holds <= rows_t <= 255 calls, so no byte carries into its neighbour, and
+        // the candidates are the positions with ca > 0.  Deeper tiles (and MODE 1) OR hit bits.
+        const bool counted = MODE == 0 && rows <= 255;
         uint32_t hits = 0;
-        uint32_t nr0 = 0, nr1 = 0, nr2 = 0, nr3 = 0, na0 = 0, na1 = 0, na2 = 0, na3 = 0;   // byte-wise call counts
-        auto scan = [&](const u32x4 d) {
-            hits |= unit_hits<MODE>(d);
-            if (MODE == 0) {
-                auto cnt = [](uint32_t w, uint32_t& r, uint32_t& x) {
-                    const uint32_t v = w & 0x80808080u;                              // valid calls
-                    const uint32_t n = w & ((w & 0x60606060u) + 0x60606060u) & 0x80808080u;   // ... not the reference allele
-                    r += (v ^ n) >> 7;
-                    x += n >> 7;
-                };
-                cnt(d.x, nr0, na0); cnt(d.y, nr1, na1); cnt(d.z, nr2, na2); cnt(d.w, nr3, na3);
-            }
+        uint32_t cv0 = 0, cv1 = 0, cv2 = 0, cv3 = 0, ca0 = 0, ca1 = 0, ca2 = 0, ca3 = 0;
+        auto cnt = [](uint32_t w, uint32_t& cv, uint32_t& ca) {
+            const uint32_t v = w & 0x80808080u;                             // valid calls
+            const uint32_t n = ((w & 0x60606060u) + 0x60606060u) & v;       // ... of an allele other than the reference
+            cv += v >> 7;
+            ca += n >> 7;
         };
         // stream the block: chunks of kScanChunk wave-loads (8 KiB per wave) issued back to back;
         // loads past the block's end return zeros, which hold no calls
-        for (int32_t u0 = 0; u0 < nunits; u0 += kScanChunk * 64) {
-            u32x4 R[kScanChunk];
+        if (counted) {
+            for (int32_t u0 = 0; u0 < nunits; u0 += kScanChunk * 64) {
+                u32x4 R[kScanChunk];
 #pragma unroll
-            for (int j = 0; j < kScanChunk; j++)
-                R[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u0 + j * 64 + lane) * 16, 0, 0));
+                for (int j = 0; j < kScanChunk; j++)
+                    R[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u0 + j * 64 + lane) * 16, 0, 0));
 #pragma unroll
-            for (int j = 0; j < kScanChunk; j++) scan(R[j]);
+                for (int j = 0; j < kScanChunk; j++) {
+                    cnt(R[j].x, cv0, ca0); cnt(R[j].y, cv1, ca1); cnt(R[j].z, cv2, ca2); cnt(R[j].w, cv3, ca3);
+                }
+            }
+            for (int s = (int)U; s < 64; s <<= 1) {
+                cv0 += __shfl_xor(cv0, s, 64); cv1 += __shfl_xor(cv1, s, 64);
+                cv2 += __shfl_xor(cv2, s, 64); cv3 += __shfl_xor(cv3, s, 64);
+                ca0 += __shfl_xor(ca0, s, 64); ca1 += __shfl_xor(ca1, s, 64);
+                ca2 += __shfl_xor(ca2, s, 64); ca3 += __shfl_xor(ca3, s, 64);
+            }
+            auto nz = [](uint32_t w) -> uint32_t { return nib4((((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u); };
+            hits = nz(ca0) | (nz(ca1) << 4) | (nz(ca2) << 8) | (nz(ca3) << 12);
+        } else {
+            for (int32_t u0 = 0; u0 < nunits; u0 += kScanChunk * 64) {
+                u32x4 R[kScanChunk];
+#pragma unroll
+                for (int j = 0; j < kScanChunk; j++)
+                    R[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u0 + j * 64 + lane) * 16, 0, 0));
+#pragma unroll
+                for (int j = 0; j < kScanChunk; j++) hits |= unit_hits<MODE>(R[j]);
+            }
+            for (int s = (int)U; s < 64; s <<= 1) hits |= __shfl_xor(hits, s, 64);
         }
-        for (int s = (int)U; s < 64; s <<= 1) hits |= __shfl_xor(hits, s, 64);
         uint32_t cm = hits & ok;
         if (lead) ncand += (unsigned long long)__popc(cm);
         if (gp.ablate & 1) continue;                                  // diagnostics: scan only
-        const bool bound = bound_on && rows <= 255;                   // byte counters and 32-bit sums cannot overflow
+        const bool bound = bound_on && counted;                       // 32-bit halves of the sums cannot overflow either
         if (bound && __ballot(cm != 0)) {
             // count bound: with nr reference and na other valid calls at the position, the exact
             // integer sums below satisfy R >= nr * (smallest addend) and X <= na * (largest), so a
             // candidate that passes with those is hom-ref without walking its column.  Most candidates
             // are one or two sequencing errors in a deep pileup and end here.
-            for (int s = (int)U; s < 64; s <<= 1) {
-                nr0 += __shfl_xor(nr0, s, 64); nr1 += __shfl_xor(nr1, s, 64);
-                nr2 += __shfl_xor(nr2, s, 64); nr3 += __shfl_xor(nr3, s, 64);
-                na0 += __shfl_xor(na0, s, 64); na1 += __shfl_xor(na1, s, 64);
-                na2 += __shfl_xor(na2, s, 64); na3 += __shfl_xor(na3, s, 64);
-            }
-            const u32x4 nref = {nr0, nr1, nr2, nr3}, nalt = {na0, na1, na2, na3};
+            const u32x4 nref = {cv0 - ca0, cv1 - ca1, cv2 - ca2, cv3 - ca3}, nalt = {ca0, ca1, ca2, ca3};
             uint32_t c = cm;
             while (c) {
                 const int k = __builtin_ctz(c);
@@ -526,13 +550,14 @@ void k_tile_pileup(
                         a3 += a == 3 ? w : 0ull;
                     }
                 };
-                for (int32_t u0 = 0; u0 < nunits; u0 += 4 * 64) {   // re-read (L2-warm)
-                    u32x4 R[4];
+                nexact++;
+                for (int32_t u0 = 0; u0 < nunits; u0 += kScanChunk * 64) {   // re-read (L2-warm)
+                    u32x4 R[kScanChunk];
 #pragma unroll
-                    for (int j = 0; j < 4; j++)
+                    for (int j = 0; j < kScanChunk; j++)
                         R[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u0 + j * 64 + lane) * 16, 0, 0));
 #pragma unroll
-                    for (int j = 0; j < 4; j++) add(R[j]);
+                    for (int j = 0; j < kScanChunk; j++) add(R[j]);
                 }
                 for (int s = (int)U; s < 64; s <<= 1) {
                     a0 += __shfl_xor(a0, s, 64);
@@ -567,12 +592,13 @@ void k_tile_pileup(
     }
     // one global reservation per workgroup for what its waves staged; one statistics atomic
     for (int s = 1; s < 64; s <<= 1) ncand += __shfl_xor(ncand, s, 64);
-    if (lane == 0) { sh.qn[wv] = qn; sh.ncand[wv] = ncand; }
+    if (lane == 0) { sh.qn[wv] = qn; sh.ncand[wv] = ncand; sh.nexact[wv] = nexact; }
     __syncthreads();
     if (threadIdx.x == 0) {
         int32_t tot = 0;
-        unsigned long long nc = 0;
-        for (int w = 0; w < kScanWaves; w++) { sh.qbase[w] = tot; tot += sh.qn[w]; nc += sh.ncand[w]; }
+        unsigned long long nc = 0, ne = 0;
+        for (int w = 0; w < kScanWaves; w++) { sh.qbase[w] = tot; tot += sh.qn[w]; nc += sh.ncand[w]; ne += sh.nexact[w]; }
+        if (ne) atomicAdd(&counters[3], ne);
         const unsigned long long base = tot ? atomicAdd(&counters[2], (unsigned long long)tot) : 0ull;
         for (int w = 0; w < kScanWaves; w++) sh.qbase[w] += (int32_t)base;   // queue indices fit 31 bits (g_len < 2^31)
         if (nc) atomicAdd(&counters[1], nc);
@@ -650,10 +676,12 @@ __global__ __launch_bounds__(256) void ko_scatter(const ngsep_site_out* __restri
 // its place; the keys are read from L2, a bucket holds a handful
 __global__ __launch_bounds__(256) void ko_bucket_sort(const unsigned long long* __restrict__ keys,
                                                       unsigned long long* __restrict__ sorted_keys,
-                                                      const int32_t* __restrict__ start, int64_t nb) {
+                                                      const int32_t* __restrict__ start, int32_t* __restrict__ bucket,
+                                                      int64_t nb) {
     const int lane = threadIdx.x & 63;
     const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= nb) return;
+    if (lane == 0) bucket[b] = 0;       // the counts were consumed by ko_scan: clean for the next run
     const int32_t a = start[b], z = start[b + 1], k = z - a;
     if (k == 0) return;
     if (k <= 64) {
@@ -673,8 +701,9 @@ __global__ __launch_bounds__(256) void ko_bucket_sort(const unsigned long long* 
 __global__ __launch_bounds__(256) void ko_gather(const ngsep_site_out* __restrict__ recs,
                                                  const unsigned long long* __restrict__ keys,
                                                  const unsigned long long* n_ptr, int64_t cap,
-                                                 ngsep_site_out* __restrict__ sorted) {
+                                                 ngsep_site_out* __restrict__ sorted, unsigned long long* next_counters) {
     constexpr int W = sizeof(ngsep_site_out) / 4;
+    if (blockIdx.x == 0 && threadIdx.x < 4) next_counters[threadIdx.x] = 0;   // the next run's counter set
     int64_t n = (int64_t)*n_ptr;
     if (n > cap) n = cap;
     const uint32_t* src = reinterpret_cast<const uint32_t*>(recs);
@@ -724,7 +753,8 @@ Device* device_create(int ordinal, std::string& err) {
     }
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) { err = "stream"; delete d; return nullptr; }
     for (auto& e : d->ev) (void)hipEventCreate(&e);
-    if (hipMalloc(&d->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc(&d->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(d->d_counters, 0, 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&d->h_counters, 4 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
         hipMalloc(&d->d_tables, sizeof(LikTables)) != hipSuccess) {
         err = "device allocation failed";
@@ -735,6 +765,7 @@ Device* device_create(int ordinal, std::string& err) {
 }
 
 int64_t device_last_hard(const Device* d) { return d ? d->last_hard : 0; }
+int64_t device_last_exact(const Device* d) { return d ? d->last_exact : 0; }
 
 void device_release(Device* d) {
     if (!d) return;
@@ -827,7 +858,10 @@ int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypePar
         (void)hipFree(d->d_bucket);
         HIP_TRY(hipMalloc(&d->d_bucket, (size_t)(3 * nb + 1) * sizeof(int32_t)));
         d->nb_cap = nb;
+        d->nb_clean = 0;
     }
+    unsigned long long* ctr = d->d_counters + 4 * d->cpar;
+    unsigned long long* ctr_next = d->d_counters + 4 * (1 - d->cpar);
     // queue of candidates the tile kernel could not prove hom-ref; dump mode: every position
     int64_t qwant = g.dump_all ? std::max<int64_t>(s.covered + 1024, 1024) : std::max<int64_t>(s.g_len / 64 + 65536, 65536);
     if (qwant < d->cap_hard) qwant = d->cap_hard;
@@ -837,59 +871,68 @@ int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypePar
             HIP_TRY(hipMalloc(&d->d_hard, (size_t)qwant * sizeof(QueueSite)));
             d->cap_hard = qwant;
         }
-        HIP_TRY(hipMemcpyAsync(d->d_tables, &t, sizeof(LikTables), hipMemcpyHostToDevice, d->stream));
-        HIP_TRY(hipMemsetAsync(d->d_counters, 0, 4 * sizeof(unsigned long long), d->stream));
+        // fixed per-run costs kept off the stream: the tables are uploaded only when they change, the
+        // counters alternate between two sets (the last kernel of a run zeroes the other set) and the
+        // bucket counts are zeroed by the ordering pass that consumed them
+        if (!d->tables_valid || std::memcmp(&d->h_tables, &t, sizeof(LikTables)) != 0) {
+            d->h_tables = t;
+            HIP_TRY(hipMemcpyAsync(d->d_tables, &d->h_tables, sizeof(LikTables), hipMemcpyHostToDevice, d->stream));
+            d->tables_valid = true;
+        }
         HIP_TRY(hipEventRecord(d->ev[0], d->stream));
         if (d->n_tiles > 0) {
             // persistent waves: as many workgroups as are co-resident (register-limited), each wave
             // walks the tiles with a grid stride, so at any moment the waves stream one contiguous
             // stretch of the pile
             auto kt = prune ? (const void*)k_tile_pileup<0> : (const void*)k_tile_pileup<1>;
-            int per_cu = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kt, kScanThreads, 0) != hipSuccess || per_cu < 1) per_cu = 2;
-            if (const char* e = std::getenv("NGSEP_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(e));   // tuning
-            const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((d->n_tiles + kScanWaves - 1) / kScanWaves, (int64_t)d->n_cu * per_cu));
+            int& per_cu = d->kt_blocks_per_cu[prune ? 0 : 1];
+            if (per_cu == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kt, kScanThreads, 0) != hipSuccess || per_cu < 1)) per_cu = 2;
+            int bpc = per_cu;
+            if (const char* e = std::getenv("NGSEP_BLOCKS_PER_CU")) bpc = std::max(1, std::atoi(e));   // tuning
+            const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((d->n_tiles + kScanWaves - 1) / kScanWaves, (int64_t)d->n_cu * bpc));
             dim3 grid((unsigned)nblk);
             if (prune)
                 hipLaunchKernelGGL(k_tile_pileup<0>, grid, dim3(kScanThreads), 0, d->stream, (const u32x4*)d->d_pile,
                                    d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, d->d_tables, g, d->d_hard,
-                                   d->d_counters, d->cap_hard);
+                                   ctr, d->cap_hard);
             else
                 hipLaunchKernelGGL(k_tile_pileup<1>, grid, dim3(kScanThreads), 0, d->stream, (const u32x4*)d->d_pile,
                                    d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, d->d_tables, g, d->d_hard,
-                                   d->d_counters, d->cap_hard);
+                                   ctr, d->cap_hard);
             HIP_TRY(hipGetLastError());
         }
         HIP_TRY(hipEventRecord(d->ev[1], d->stream));
-        hipLaunchKernelGGL(k_posterior, dim3(2048), dim3(kPostWaves * 64), 0, d->stream, d->d_hard, d->d_counters + 2, d->cap_hard,
+        hipLaunchKernelGGL(k_posterior, dim3(2048), dim3(kPostWaves * 64), 0, d->stream, d->d_hard, ctr + 2, d->cap_hard,
                            d->d_reads, d->n_reads, d->d_lb, d->d_slots, d->slot_size, d->d_tables, g, d->d_sites,
-                           d->d_counters, d->cap_sites);
+                           ctr, d->cap_sites);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(d->ev[2], d->stream));   // queue overflow is checked after the copy below
         // order the records by position on the device
         int32_t* cnt = d->d_bucket;
         int32_t* start = d->d_bucket + nb;
         int32_t* cursor = d->d_bucket + 2 * nb + 1;
-        HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)nb * sizeof(int32_t), d->stream));
-        hipLaunchKernelGGL(ko_hist, dim3(256), dim3(256), 0, d->stream, d->d_sites, d->d_counters, d->cap_sites, cnt, shift);
+        if (nb > d->nb_clean) HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)nb * sizeof(int32_t), d->stream));
+        hipLaunchKernelGGL(ko_hist, dim3(256), dim3(256), 0, d->stream, d->d_sites, ctr, d->cap_sites, cnt, shift);
         hipLaunchKernelGGL(ko_scan, dim3(1), dim3(1024), 0, d->stream, cnt, start, cursor, nb);
-        hipLaunchKernelGGL(ko_scatter, dim3(256), dim3(256), 0, d->stream, d->d_sites, d->d_counters, d->cap_sites, cursor,
+        hipLaunchKernelGGL(ko_scatter, dim3(256), dim3(256), 0, d->stream, d->d_sites, ctr, d->cap_sites, cursor,
                            d->d_keys, shift);
         unsigned long long* skeys = d->d_keys + d->cap_sites;    // second half: keys in position order
-        hipLaunchKernelGGL(ko_bucket_sort, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, d->stream, d->d_keys, skeys, start, nb);
-        hipLaunchKernelGGL(ko_gather, dim3(1024), dim3(256), 0, d->stream, d->d_sites, skeys, d->d_counters, d->cap_sites,
-                           d->d_sorted);
+        hipLaunchKernelGGL(ko_bucket_sort, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, d->stream, d->d_keys, skeys, start, cnt, nb);
+        d->nb_clean = std::max(d->nb_clean, nb);
+        hipLaunchKernelGGL(ko_gather, dim3(1024), dim3(256), 0, d->stream, d->d_sites, skeys, ctr, d->cap_sites,
+                           d->d_sorted, ctr_next);
         HIP_TRY(hipGetLastError());
     }
     // counters and a prefix of the ordered records in one round trip, straight into the result store
     const size_t from = out->size();
-    const int64_t guess = std::min<int64_t>(d->cap_sites, d->last_n_sites + d->last_n_sites / 4 + 256);
+    const int64_t guess = std::min<int64_t>(d->cap_sites, d->last_n_sites + d->last_n_sites / 64 + 64);
     out->reserve(from + (size_t)guess);
-    HIP_TRY(hipMemcpyAsync(d->h_counters, d->d_counters, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, d->stream));
+    HIP_TRY(hipMemcpyAsync(d->h_counters, ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, d->stream));
     HIP_TRY(hipMemcpyAsync(out->buf + from, d->d_sorted, (size_t)guess * sizeof(ngsep_site_out), hipMemcpyDeviceToHost, d->stream));
     auto tq = std::chrono::steady_clock::now();
     HIP_TRY(hipStreamSynchronize(d->stream));
     auto ts = std::chrono::steady_clock::now();
+    d->cpar = 1 - d->cpar;              // ko_gather zeroed the other counter set for the next run
     const int64_t n = (int64_t)d->h_counters[0];
     if (n > d->cap_sites) {
         // more calls than the record buffer holds (e.g. -minQuality 0): grow it and run again
@@ -939,6 +982,7 @@ int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypePar
     *total_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     *n_candidates = (int64_t)d->h_counters[1];
     d->last_hard = (int64_t)d->h_counters[2];
+    d->last_exact = (int64_t)d->h_counters[3];
     return 0;
 }
 
