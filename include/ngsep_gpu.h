@@ -65,6 +65,9 @@ typedef struct ngsep_params {
     int32_t prune_candidates;     /* 1: exact non-candidate pruning (DESIGN.md "K1"), 0: genotype every position */
     int32_t dump_all_positions;   /* 1: ngsep_fetch_sites returns a record for every position with DP>0 */
     int32_t window_positions;     /* max positions per device window (0 = whole contig) */
+    /* MultisampleVariantsDetector (discovery/MultisampleVariantsDetector.java:54-95) */
+    int32_t multisample;          /* 1: population calling over the samples of ngsep_set_samples */
+    double  min_allele_depth_freq;/* -minAlleleDepthFrequency 0 (setMinAlleleDepthFrequency, :398-403) */
 } ngsep_params;
 
 /* Alignments as AlignmentsPileupGenerator.processAlignment receives them
@@ -106,6 +109,32 @@ typedef struct ngsep_site_out {
     int32_t strand_counts[4][2]; /* [allele][0=negative,1=positive] (CountsHelper.countsStrand) */
     double  logc[10];        /* log10 P(data|genotype) upper triangle: 00 01 02 03 11 12 13 22 23 33 */
 } ngsep_site_out;
+
+/* One population VCF line of MultisampleVariantsDetector (VCFRecord.createDefaultPopulationVCFRecord,
+ * vcf/VCFRecord.java:277-301): the variant and n_samples ngsep_sample_call records. */
+typedef struct ngsep_popsite_out {
+    int32_t seq_id;
+    int32_t pos;             /* 1-based */
+    int8_t  n_alleles;       /* 2..4 */
+    int8_t  alleles[4];      /* DNA indexes (0=A..3=T): reference first, then alternatives in A,C,G,T order */
+    int8_t  multisnv_type;   /* 1: the pooled multi-allelic SNV kept all its alleles -> INFO TYPE=MULTISNV */
+    int16_t qual;            /* variant QS: max GQ over decided non-reference sample calls (:674-693) */
+    int16_t pad;
+} ngsep_popsite_out;
+
+/* One sample's genotype call at a population site: CalledSNV (biallelic) or
+ * CalledGenomicVariantImpl (multi-allelic / no data), as VCFFileWriter.printGenotypeInfo prints it. */
+typedef struct ngsep_sample_call {
+    int8_t  kind;            /* 0 CalledSNV, 1 CalledGenomicVariantImpl */
+    int8_t  n_called;        /* 0 = undecided ("./."), 1 homozygous, 2 heterozygous */
+    int8_t  called[2];       /* indexes into the site's alleles */
+    int16_t gq;
+    int16_t total_cn;        /* getCopyNumber (ACN "." when 0) */
+    int32_t dp;              /* CountsHelper.getTotalCount() of the sample */
+    int32_t counts[4];       /* BSDP A,C,G,T */
+    int16_t acn[4];          /* getAllelesCopyNumber over the site's alleles */
+    int32_t pl[10];          /* PL in VCF order (j-major, i<=j over the site's alleles) */
+} ngsep_sample_call;
 
 typedef struct ngsep_stats {
     int64_t alignments_in;          /* alignments received */
@@ -155,6 +184,20 @@ int ngsep_clear_sites(ngsep_ctx* ctx);
 int ngsep_write_vcf_header(ngsep_ctx* ctx, const char* path);
 int ngsep_append_vcf_records(ngsep_ctx* ctx, const char* path);   /* all fetched sites, then clears them */
 int64_t ngsep_format_site(ngsep_ctx* ctx, const ngsep_site_out* site, char* buf, int64_t cap);
+
+/* ---- MultisampleVariantsDetector (discovery/MultisampleVariantsDetector.java:421-693) ----
+ * Samples in VCF column order (loadSamplesFromAlignmentHeaders: TreeMap by id, :499-523).
+ * rg_sample[g] = sample of read group g (the read_group index of ngsep_read_batch; -1 = none: the
+ * read still counts in the pooled allele counts); rg_rank[g] = position of g in its sample's read
+ * group set iteration (Sample.getReadGroups, variants/Sample.java:36-67), the order in which
+ * PileupRecord.getAlleleCalls(span, readGroups) (:104-111) visits them. */
+int ngsep_set_samples(ngsep_ctx* ctx, int32_t n_samples, const char* const* sample_ids,
+                      int32_t n_read_groups, const int32_t* rg_sample, const int32_t* rg_rank);
+/* Population sites in (sequence, position) order; calls[i * n_samples + s] is sample s at site i. */
+int ngsep_fetch_population_sites(ngsep_ctx* ctx, ngsep_popsite_out* sites, ngsep_sample_call* calls,
+                                 int64_t cap, int64_t* n_out);
+/* MultisampleVariantsDetector output: VCF header with the samples, then every fetched site */
+int ngsep_write_population_vcf(ngsep_ctx* ctx, const char* path);
 
 /* ---- path B: the whole SingleSampleVariantsDetector.findSNVS on a BAM file (:896-931) ---- */
 int ngsep_call_bam(ngsep_ctx* ctx, const char* bam_path, const char* out_vcf_path);

@@ -43,6 +43,8 @@ class NgsepParams(ctypes.Structure):
         ("prune_candidates", ctypes.c_int32),
         ("dump_all_positions", ctypes.c_int32),
         ("window_positions", ctypes.c_int32),
+        ("multisample", ctypes.c_int32),
+        ("min_allele_depth_freq", ctypes.c_double),
     ]
 
 
@@ -84,6 +86,32 @@ class NgsepSiteOut(ctypes.Structure):
         ("counts", ctypes.c_int32 * 4),
         ("strand_counts", (ctypes.c_int32 * 2) * 4),
         ("logc", ctypes.c_double * 10),
+    ]
+
+
+class NgsepPopSiteOut(ctypes.Structure):
+    _fields_ = [
+        ("seq_id", ctypes.c_int32),
+        ("pos", ctypes.c_int32),
+        ("n_alleles", ctypes.c_int8),
+        ("alleles", ctypes.c_int8 * 4),
+        ("multisnv_type", ctypes.c_int8),
+        ("qual", ctypes.c_int16),
+        ("pad", ctypes.c_int16),
+    ]
+
+
+class NgsepSampleCall(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int8),
+        ("n_called", ctypes.c_int8),
+        ("called", ctypes.c_int8 * 2),
+        ("gq", ctypes.c_int16),
+        ("total_cn", ctypes.c_int16),
+        ("dp", ctypes.c_int32),
+        ("counts", ctypes.c_int32 * 4),
+        ("acn", ctypes.c_int16 * 4),
+        ("pl", ctypes.c_int32 * 10),
     ]
 
 
@@ -130,6 +158,11 @@ SIGNATURES = {
     "ngsep_append_vcf_records": (ctypes.c_int, [_CTX, ctypes.c_char_p]),
     "ngsep_format_site": (ctypes.c_int64, [_CTX, P(NgsepSiteOut), ctypes.c_char_p, ctypes.c_int64]),
     "ngsep_call_bam": (ctypes.c_int, [_CTX, ctypes.c_char_p, ctypes.c_char_p]),
+    "ngsep_set_samples": (ctypes.c_int, [_CTX, ctypes.c_int32, P(ctypes.c_char_p), ctypes.c_int32, P(ctypes.c_int32),
+                                         P(ctypes.c_int32)]),
+    "ngsep_fetch_population_sites": (ctypes.c_int, [_CTX, P(NgsepPopSiteOut), P(NgsepSampleCall), ctypes.c_int64,
+                                                    P(ctypes.c_int64)]),
+    "ngsep_write_population_vcf": (ctypes.c_int, [_CTX, ctypes.c_char_p]),
     "ngsep_bam_open": (ctypes.c_int, [_CTX, ctypes.c_char_p, P(ctypes.c_void_p)]),
     "ngsep_bam_next_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, P(NgsepReadBatch)]),
     "ngsep_bam_close": (ctypes.c_int, [ctypes.c_void_p]),

@@ -190,6 +190,11 @@ static void admit(ngsep_ctx* c, const RawRead& r) {
     cr.first.push_back(r.first);
     cr.last.push_back(last);
     cr.neg.push_back((r.flags & 0x10) ? 1 : 0);
+    if (c->params.multisample) {
+        const bool in = r.rg >= 0 && r.rg < (int32_t)c->rg_sample.size();
+        cr.sample.push_back((int16_t)(in ? c->rg_sample[r.rg] : -1));
+        cr.rank.push_back((uint8_t)(in && c->rg_sample[r.rg] >= 0 ? c->rg_rank[r.rg] : 0));
+    }
     cr.boff.push_back((int64_t)cr.bytes.size());
     cr.bytes.insert(cr.bytes.end(), bytes.begin(), bytes.end());
     int32_t span = last - r.first + 1;
@@ -477,6 +482,136 @@ static void build_pile(Staged& s) {
     }
 }
 
+// Multisample layout: the same tiles of T positions, one block per (tile, sample) holding that
+// sample's reads coloured into rows (MultisampleVariantsDetector genotypes every sample from its own
+// read groups, PileupRecord.getAlleleCalls(span, readGroups), :104-111).  Reads of no sample only
+// enter the pooled counts, which the population kernel takes from the read table.
+static void build_pile_multi(Staged& s) {
+    const int64_t g_len = s.g_len, nreads = s.n_reads;
+    const int S = s.n_samples;
+    const int32_t* R = s.h_reads.data();
+    const int64_t nb16 = g_len / kTileMinPos;
+    std::vector<std::vector<int64_t>> by_sample((size_t)S);
+    for (int64_t i = 0; i < nreads; i++) {
+        const int sm = (R[i * 4 + 3] >> 8) - 1;
+        if (sm >= 0 && sm < S) by_sample[(size_t)sm].push_back(i);
+    }
+    // per-sample maxima of the depth over 16-position blocks (saturating at 65535)
+    std::vector<uint16_t> m16((size_t)S * (size_t)nb16, 0);
+    {
+        std::vector<int32_t> cov((size_t)g_len + 1);
+        for (int sm = 0; sm < S; sm++) {
+            std::fill(cov.begin(), cov.end(), 0);
+            for (int64_t i : by_sample[(size_t)sm]) {
+                const int32_t a = R[i * 4], b = R[i * 4 + 1];
+                if (b < a) continue;
+                cov[a]++;
+                cov[(size_t)b + 1]--;
+            }
+            uint16_t* m = &m16[(size_t)sm * (size_t)nb16];
+            int32_t run = 0;
+            for (int64_t p = 0; p < nb16 * kTileMinPos; p++) {
+                run += cov[p];
+                const int32_t v = run > 65535 ? 65535 : run;
+                if (v > m[p / kTileMinPos]) m[p / kTileMinPos] = (uint16_t)v;
+            }
+        }
+    }
+    // tile size: bytes of all blocks + a fixed cost per (tile, sample) block
+    int bestT = kTileMinPos;
+    double best = -1;
+    for (int T = kTileMinPos; T <= kTileMaxPos; T *= 2) {
+        const int64_t f = T / kTileMinPos, nt = g_len / T;
+        double bytes = 0;
+        for (int sm = 0; sm < S; sm++) {
+            const uint16_t* m = &m16[(size_t)sm * (size_t)nb16];
+            for (int64_t t = 0; t < nt; t++) {
+                uint16_t mx = 0;
+                for (int64_t k = 0; k < f; k++) mx = std::max(mx, m[t * f + k]);
+                bytes += (double)mx * T;
+            }
+        }
+        const double cost = bytes + 256.0 * (double)nt * S;
+        if (best < 0 || cost < best) { best = cost; bestT = T; }
+    }
+    const int T = bestT;
+    const int64_t nt = g_len / T, f = T / kTileMinPos;
+    s.tile = T;
+    s.n_tiles = nt;
+    s.h_rows.assign((size_t)nt * S, 0);
+    s.h_toff.assign((size_t)nt + 1, 0);
+    int64_t off = 0;
+    int32_t rmax = 0;
+    for (int64_t t = 0; t < nt; t++) {
+        s.h_toff[(size_t)t] = off;
+        for (int sm = 0; sm < S; sm++) {
+            const uint16_t* m = &m16[(size_t)sm * (size_t)nb16];
+            uint16_t mx = 0;
+            for (int64_t k = 0; k < f; k++) mx = std::max(mx, m[t * f + k]);
+            s.h_rows[(size_t)t * S + sm] = mx;
+            off += (int64_t)mx * T;
+            rmax = std::max<int32_t>(rmax, mx);
+        }
+    }
+    s.h_toff[(size_t)nt] = off;
+    std::vector<uint16_t>().swap(m16);
+    s.pile_bytes = off;
+    s.tile_rows_max = rmax;
+    s.h_pile.assign((size_t)off, 0);
+    const int SL = s.slot_size;
+    const uint8_t* slots = s.h_slots.data();
+    const uint8_t* ref = s.h_ref.data();
+    std::vector<std::vector<int64_t>> tile_reads((size_t)S);
+    std::vector<std::pair<int32_t, int32_t>> heap;
+    std::vector<int32_t> free_rows;
+    int64_t r_lo = 0;
+    for (int64_t t = 0; t < nt; t++) {
+        const int32_t tstart = (int32_t)(t * T), tend = tstart + T;
+        while (r_lo < nreads && R[r_lo * 4] <= tstart - s.max_span) r_lo++;
+        for (auto& v : tile_reads) v.clear();
+        for (int64_t r = r_lo; r < nreads && R[r * 4] < tend; r++) {
+            const int32_t gfirst = R[r * 4], glast = R[r * 4 + 1];
+            if (glast < tstart || glast < gfirst) continue;
+            const int sm = (R[r * 4 + 3] >> 8) - 1;
+            if (sm >= 0 && sm < S) tile_reads[(size_t)sm].push_back(r);
+        }
+        int64_t boff = s.h_toff[(size_t)t];
+        for (int sm = 0; sm < S; sm++) {
+            const int32_t rows = s.h_rows[(size_t)t * S + sm];
+            uint8_t* blk = &s.h_pile[(size_t)boff];
+            boff += (int64_t)rows * T;
+            heap.clear();
+            free_rows.clear();
+            int32_t next_row = 0;
+            for (int64_t r : tile_reads[(size_t)sm]) {
+                const int32_t gfirst = R[r * 4], glast = R[r * 4 + 1];
+                const int32_t a = std::max(gfirst, tstart) - tstart, b = std::min(glast, tend - 1) - tstart;
+                while (!heap.empty() && heap.front().first < a) {
+                    free_rows.push_back(heap.front().second);
+                    std::pop_heap(heap.begin(), heap.end(), std::greater<>());
+                    heap.pop_back();
+                }
+                int32_t row;
+                if (!free_rows.empty()) { row = free_rows.back(); free_rows.pop_back(); }
+                else row = next_row++;
+                heap.push_back({b, row});
+                std::push_heap(heap.begin(), heap.end(), std::greater<>());
+                const uint8_t* src = slots + (size_t)R[r * 4 + 2] * SL + (tstart + a - gfirst);
+                uint8_t* dst = blk + (size_t)row * T;
+                for (int32_t p = a; p <= b; p++) {
+                    uint8_t cd = src[p - a];
+                    if (cd & kCodeValid) {
+                        const uint8_t rc = ref[tstart + p];
+                        const uint8_t ra = (rc & kRefCallable) ? (uint8_t)((rc >> 5) & 3) : 0;
+                        cd = (uint8_t)((cd & 0x9F) | ((((cd >> 5) & 3) ^ ra) << 5));
+                    }
+                    dst[p] = cd;
+                }
+            }
+        }
+    }
+}
+
 int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     Staged& s = c->staged;
     s = Staged();
@@ -549,7 +684,9 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
             s.h_reads[ri * 4 + 0] = (int32_t)gfirst;
             s.h_reads[ri * 4 + 1] = (int32_t)(cr.last[i] + goff);
             s.h_reads[ri * 4 + 2] = (int32_t)slot;
-            s.h_reads[ri * 4 + 3] = cr.neg[i];
+            int32_t fl = cr.neg[i];
+            if (!cr.sample.empty()) fl |= ((int32_t)cr.rank[i] << 1) | (((int32_t)cr.sample[i] + 1) << 8);
+            s.h_reads[ri * 4 + 3] = fl;
             if (span > 0) std::memcpy(&s.h_slots[(size_t)slot * S], &cr.bytes[cr.boff[i]], (size_t)span);
             slot += ns;
             nbases += span > 0 ? span : 0;
@@ -568,7 +705,12 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
         uint8_t* dst = &s.h_ref[(size_t)(w.gbase + w.pad)];
         for (int32_t k = 0; k < w.wlen; k++) dst[k] = ref_code(c, ref[(size_t)w.w0 - 1 + k]);
     }
-    build_pile(s);
+    if (c->params.multisample) {
+        s.n_samples = (int32_t)c->sample_ids.size();
+        build_pile_multi(s);
+    } else {
+        build_pile(s);
+    }
     c->stats.read_bases = nbases;
     c->stats.slot_bytes = nslots * S;
     c->stats.pile_bytes = s.pile_bytes;
@@ -588,6 +730,8 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     std::vector<uint8_t>().swap(s.h_ref);
     std::vector<uint8_t>().swap(s.h_pile);
     std::vector<TileInfo>().swap(s.h_tinfo);
+    std::vector<uint16_t>().swap(s.h_rows);
+    std::vector<int64_t>().swap(s.h_toff);
     return NGSEP_OK;
 }
 
@@ -650,10 +794,52 @@ static void apply_strand_bias(SiteStore& sites, size_t from) {
     }
 }
 
+// MultisampleVariantsDetector run: sites come back unordered with global positions; order them by
+// position and map them to (sequence, position) (the listener writes in pileup order, :534-535)
+static int run_device_multi(ngsep_ctx* c, const LikTables& t, const GenotypeParams& gp, double* elapsed_ms) {
+    std::vector<ngsep_popsite_out> sites;
+    std::vector<ngsep_sample_call> calls;
+    double scan_ms = 0, geno_ms = 0, total_ms = 0;
+    int64_t ncand = 0;
+    std::string err;
+    if (device_run_multi(c->dev, c->staged, t, gp, c->sample_nrank, c->params.min_allele_depth_freq, c->params.ploidy,
+                         &sites, &calls, &scan_ms, &geno_ms, &total_ms, &ncand, err) != 0)
+        return set_error(c, NGSEP_E_DEVICE, err);
+    const size_t S = c->sample_ids.size();
+    std::vector<int64_t> order(sites.size());
+    for (size_t i = 0; i < order.size(); i++) order[i] = (int64_t)i;
+    std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return sites[a].pos < sites[b].pos; });
+    const std::vector<Window>& ws = c->staged.windows;
+    size_t wi = 0;
+    const size_t from = c->pop_sites.size();
+    for (int64_t i : order) {
+        ngsep_popsite_out o = sites[(size_t)i];
+        const int64_t gpos = o.pos;
+        while (wi + 1 < ws.size() && ws[wi + 1].gbase <= gpos) wi++;
+        const Window& w = ws[wi];
+        const int64_t off = gpos - w.gbase - w.pad;
+        if (off < 0 || off >= w.wlen) continue;
+        o.seq_id = w.seq_id;
+        o.pos = (int32_t)(w.w0 + off);
+        c->pop_sites.push_back(o);
+        c->pop_calls.insert(c->pop_calls.end(), calls.begin() + (ptrdiff_t)((size_t)i * S), calls.begin() + (ptrdiff_t)((size_t)(i + 1) * S));
+    }
+    c->stats.candidates = ncand;
+    c->stats.hard_sites = (int32_t)device_last_hard(c->dev);
+    c->stats.exact_bound_passes = device_last_exact(c->dev);
+    c->stats.sites_called += (int64_t)(c->pop_sites.size() - from);
+    c->stats.kernel_ms = total_ms;
+    c->stats.scan_ms = scan_ms;
+    c->stats.genotype_ms = geno_ms;
+    if (elapsed_ms) *elapsed_ms = total_ms;
+    return NGSEP_OK;
+}
+
 int run_device(ngsep_ctx* c, double* elapsed_ms) {
     LikTables t;
     GenotypeParams gp;
     compute_tables(c, &t, &gp);
+    if (c->params.multisample) return run_device_multi(c, t, gp, elapsed_ms);
     int64_t n = 0;
     double scan_ms = 0, geno_ms = 0, total_ms = 0;
     int64_t ncand = 0;
@@ -766,9 +952,9 @@ extern "C" int ngsep_open(int device, const ngsep_params* params, ngsep_ctx** ou
         *out = c;
         return set_error(c, NGSEP_E_UNSUPPORTED, "ploidy >= 3 uses the pool algorithm (SingleSampleVariantPileupListener.genotypeVariantPool), not implemented");
     }
-    // SingleSampleVariantsDetector.run (:591-593)
+    // SingleSampleVariantsDetector.run (:591-593); MultisampleVariantsDetector keeps -h as given
     c->het_rate = c->params.het_rate;
-    if (!c->params.het_rate_set && c->params.ploidy == 1) c->het_rate = 1e-6;
+    if (!c->params.multisample && !c->params.het_rate_set && c->params.ploidy == 1) c->het_rate = 1e-6;
     *out = c;
     return NGSEP_OK;
 }
@@ -854,6 +1040,8 @@ extern "C" int ngsep_stage_finish(ngsep_ctx* c) {
 extern "C" int ngsep_run_staged(ngsep_ctx* c, double* elapsed_ms) {
     if (!c || !c->dev) return set_error(c, NGSEP_E_INVALID, "nothing staged");
     c->sites.clear();
+    c->pop_sites.clear();
+    c->pop_calls.clear();
     c->stats.sites_called = 0;
     return run_device(c, elapsed_ms);
 }
@@ -862,5 +1050,40 @@ extern "C" int ngsep_release_staged(ngsep_ctx* c) {
     if (!c) return NGSEP_E_INVALID;
     if (c->dev) device_release(c->dev);
     c->staged = Staged();
+    return NGSEP_OK;
+}
+
+// ---- MultisampleVariantsDetector entry points ----
+extern "C" int ngsep_set_samples(ngsep_ctx* c, int32_t n_samples, const char* const* sample_ids,
+                                 int32_t n_read_groups, const int32_t* rg_sample, const int32_t* rg_rank) {
+    if (!c || n_samples < 0 || n_read_groups < 0 || (n_samples && !sample_ids) || (n_read_groups && (!rg_sample || !rg_rank)))
+        return set_error(c, NGSEP_E_INVALID, "bad sample description");
+    if (n_samples > kMaxSamplesDevice)
+        return set_error(c, NGSEP_E_UNSUPPORTED, "more than " + std::to_string(kMaxSamplesDevice) + " samples per device run");
+    c->sample_ids.clear();
+    for (int32_t i = 0; i < n_samples; i++) c->sample_ids.emplace_back(sample_ids[i] ? sample_ids[i] : "");
+    c->rg_sample.assign(rg_sample, rg_sample + n_read_groups);
+    c->rg_rank.assign(rg_rank, rg_rank + n_read_groups);
+    c->sample_nrank.assign((size_t)n_samples, 0);
+    for (int32_t g = 0; g < n_read_groups; g++) {
+        const int32_t sm = rg_sample[g];
+        if (sm < -1 || sm >= n_samples) return set_error(c, NGSEP_E_INVALID, "read group mapped to an unknown sample");
+        if (sm >= 0) {
+            if (rg_rank[g] < 0 || rg_rank[g] > 126) return set_error(c, NGSEP_E_INVALID, "read group rank out of range");
+            c->sample_nrank[(size_t)sm] = (int8_t)std::max<int>(c->sample_nrank[(size_t)sm], rg_rank[g] + 1);
+        }
+    }
+    return NGSEP_OK;
+}
+
+extern "C" int ngsep_fetch_population_sites(ngsep_ctx* c, ngsep_popsite_out* sites, ngsep_sample_call* calls,
+                                            int64_t cap, int64_t* n_out) {
+    if (!c || !n_out) return NGSEP_E_INVALID;
+    const int64_t n = (int64_t)c->pop_sites.size();
+    *n_out = n;
+    const size_t S = c->sample_ids.size();
+    const int64_t k = std::min<int64_t>(n, std::max<int64_t>(cap, 0));
+    if (sites && k) std::memcpy(sites, c->pop_sites.data(), (size_t)k * sizeof(ngsep_popsite_out));
+    if (calls && k && S) std::memcpy(calls, c->pop_calls.data(), (size_t)k * S * sizeof(ngsep_sample_call));
     return NGSEP_OK;
 }

@@ -51,6 +51,10 @@ constexpr int kTileMinPos = 16;
 
 // K2 output record (device layout == ngsep_site_out, with gpos in .pos)
 static_assert(sizeof(ngsep_site_out) == 152, "site record layout");
+static_assert(sizeof(ngsep_sample_call) == 76, "sample call layout");
+static_assert(sizeof(ngsep_popsite_out) == 20, "population site layout");
+constexpr int kMaxSamplesDevice = 256;     // samples genotyped by one workgroup (one thread each)
+constexpr int kPopListCap = 12288;         // reads covering one position in the population kernel (LDS)
 
 // Likelihood addends for the SNV model with n=4 alleles and f=g=250
 // (CountsHelper.java:147-185 with heterozygousProportion 0.5, SingleSampleVariantPileupListener.java:236)
@@ -97,12 +101,17 @@ struct ContigReads {
     int32_t seq_id = -1;
     std::vector<int32_t> first, last;
     std::vector<uint8_t> neg;          // 1 = negative strand
+    std::vector<int16_t> sample;       // multisample: sample of the read's group (-1 none)
+    std::vector<uint8_t> rank;         // multisample: rank of the read group in its sample's set
     std::vector<int64_t> boff;         // offset of the read's projected bytes
     std::vector<uint8_t> bytes;        // projected codes over [first, last]
     int32_t max_span = 0;
     int64_t covered = 0;               // union of [first,last] (positions with a pileup)
     int32_t cov_last = 0;              // running max of last (for `covered`)
-    void clear() { first.clear(); last.clear(); neg.clear(); boff.clear(); bytes.clear(); max_span = 0; covered = 0; cov_last = 0; seq_id = -1; }
+    void clear() {
+        first.clear(); last.clear(); neg.clear(); sample.clear(); rank.clear(); boff.clear(); bytes.clear();
+        max_span = 0; covered = 0; cov_last = 0; seq_id = -1;
+    }
 };
 
 // One raw alignment as received (kept while its same-start group is open)
@@ -163,6 +172,12 @@ struct Staged {            // everything resident for one run
     std::vector<uint8_t> h_pile;
     std::vector<TileInfo> h_tinfo;
     std::vector<int32_t> h_reads;       // 4 ints per read: gfirst, glast, slot, flags
+                                        //   flags: bit0 negative strand, bits 1-7 read-group rank,
+                                        //   bits 8-23 sample + 1 (0: no sample) -- multisample only
+    // multisample: per-sample tile blocks (tile t, sample s: rows[t*S+s] x T bytes at toff[t] + ...)
+    int32_t n_samples = 0;
+    std::vector<uint16_t> h_rows;
+    std::vector<int64_t> h_toff;
     std::vector<uint8_t> h_ref;
 };
 
@@ -189,8 +204,14 @@ struct ngsep_ctx {
     std::vector<ngsep::ContigReads> staged_contigs;
     ngsep::Staged staged;
     ngsep::Device* dev = nullptr;
+    // multisample (ngsep_set_samples)
+    std::vector<std::string> sample_ids;
+    std::vector<int32_t> rg_sample, rg_rank;
+    std::vector<int8_t> sample_nrank;        // read groups per sample
     // outputs
     ngsep::SiteStore sites;
+    std::vector<ngsep_popsite_out> pop_sites;     // (sequence, position) order
+    std::vector<ngsep_sample_call> pop_calls;     // pop_sites.size() x n_samples
     ngsep_stats stats{};
 };
 
@@ -211,12 +232,20 @@ int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypePar
                SiteStore* out, int64_t* n_out, double* scan_ms, double* geno_ms, double* total_ms,
                int64_t* n_candidates, std::string& err);
 void device_release(Device* d);
+// multisample: tile scan over the per-sample blocks + population genotyping of the queued
+// positions; appends the sites (global positions, unordered) and their calls
+int device_run_multi(Device* d, const Staged& s, const LikTables& t, const GenotypeParams& g,
+                     const std::vector<int8_t>& sample_nrank, double min_adf, int ploidy,
+                     std::vector<ngsep_popsite_out>* sites, std::vector<ngsep_sample_call>* calls,
+                     double* scan_ms, double* geno_ms, double* total_ms, int64_t* n_candidates, std::string& err);
 int64_t device_last_hard(const Device* d);
 int64_t device_last_exact(const Device* d);
 int device_count();
 // vcf.cpp
 std::string format_header(const ngsep_ctx* c);
 int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& out);
+std::string format_population_header(const ngsep_ctx* c);
+void format_population_site(const ngsep_ctx* c, const ngsep_popsite_out& s, const ngsep_sample_call* calls, std::string& out);
 // bam.cpp
 int call_bam(ngsep_ctx* c, const char* bam_path, const char* out_vcf);
 }  // namespace ngsep

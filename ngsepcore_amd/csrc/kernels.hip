@@ -54,6 +54,13 @@ struct Device {
     uint8_t* d_ref = nullptr;
     int32_t* d_lb = nullptr;
     TileInfo* d_tinfo = nullptr;
+    uint16_t* d_rows = nullptr;      // multisample: rows per (tile, sample)
+    int64_t* d_toff = nullptr;       // multisample: block offset per tile
+    int8_t* d_nrank = nullptr;       // multisample: read groups per sample
+    int32_t n_samples = 0;
+    ngsep_popsite_out* d_psites = nullptr;
+    ngsep_sample_call* d_pcalls = nullptr;
+    int64_t cap_psites = 0;
     LikTables* d_tables = nullptr;
     ngsep_site_out* d_sites = nullptr;
     ngsep_site_out* d_sorted = nullptr;
@@ -611,6 +618,541 @@ void k_tile_pileup(
     }
 }
 
+
+// ------------------------------------------------------------------------------------------
+// KTM: multisample tile scan -- one wavefront per tile, the samples in turn
+// ------------------------------------------------------------------------------------------
+// Tile t holds one block per sample (rows[t*S+s] x T code bytes, consecutive from toff[t]).  The wave
+// streams each sample's block as KT streams a tile and bounds every candidate with that SAMPLE's
+// calls: a sample the bounds prove hom-ref cannot make a decided non-reference call
+// (SingleSampleVariantPileupListener.genotypeVariantSample, :361-391, evaluates the same posterior),
+// and a position where every sample is proven hom-ref gets variant QS 0, which
+// MultisampleVariantsDetector.onPileup never writes (:534).  The other positions are queued for KPM.
+__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(NGSEP_KT_WAVES_PER_EU)))
+void k_tile_pileup_multi(const u32x4* __restrict__ pile, const int64_t* __restrict__ toff,
+                         const uint16_t* __restrict__ rows_ts, int32_t n_samples, const uint8_t* __restrict__ ref,
+                         int32_t log2T, int64_t n_tiles, const LikTables* __restrict__ tabs, GenotypeParams gp,
+                         QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap) {
+    __shared__ ScanShared sh;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (threadIdx.x < 64) sh.w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
+    __syncthreads();
+    const int log2U = log2T - 4;
+    const uint32_t U = 1u << log2U;
+    const int col = lane & (int)(U - 1);
+    const bool lead = lane < (int)U;
+    const bool bound_on = gp.use_bound != 0;
+    const long long th = tabs->t_het, to = tabs->t_homo;
+    const int32_t maxq = gp.max_q;
+    int32_t qn = 0;
+    unsigned long long ncand = 0;
+    uint32_t nexact = 0;
+    const int64_t nwaves = (int64_t)gridDim.x * kScanWaves;
+    for (int64_t t = (int64_t)blockIdx.x * kScanWaves + wv; t < n_tiles; t += nwaves) {
+        int64_t off = toff[t];
+        off = ((int64_t)__builtin_amdgcn_readfirstlane((int32_t)(off >> 32)) << 32) |
+              (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)off);
+        const int32_t tstart = (int32_t)(t << log2T);
+        const u32x4 rc = *reinterpret_cast<const u32x4*>(ref + tstart + col * 16);
+        const uint32_t ok = nib4(rc.x & 0x80808080u) | (nib4(rc.y & 0x80808080u) << 4) |
+                            (nib4(rc.z & 0x80808080u) << 8) | (nib4(rc.w & 0x80808080u) << 12);
+        uint32_t need = 0;      // positions with a sample the bounds leave open (same in every lane of a column)
+        for (int32_t s0 = 0; s0 < n_samples; s0 += 64) {
+            const int32_t myrows = s0 + lane < n_samples ? (int32_t)rows_ts[t * n_samples + s0 + lane] : 0;
+            const int32_t nsb = n_samples - s0 < 64 ? n_samples - s0 : 64;
+            for (int j = 0; j < nsb; j++) {
+                const int32_t rows = __builtin_amdgcn_readlane(myrows, j);
+                if (rows == 0) continue;
+                const int32_t nunits = rows << log2U;
+                const u32x4* blk = pile + (off >> 4);
+                off += (int64_t)rows << log2T;
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)blk, 0, nunits * 16, 0x00020000);
+                const bool counted = rows <= 255;
+                uint32_t hits = 0;
+                uint32_t cv0 = 0, cv1 = 0, cv2 = 0, cv3 = 0, ca0 = 0, ca1 = 0, ca2 = 0, ca3 = 0;
+                auto cnt = [](uint32_t w, uint32_t& cv, uint32_t& ca) {
+                    const uint32_t v = w & 0x80808080u;
+                    const uint32_t n = ((w & 0x60606060u) + 0x60606060u) & v;
+                    cv += v >> 7;
+                    ca += n >> 7;
+                };
+                for (int32_t u0 = 0; u0 < nunits; u0 += kScanChunk * 64) {
+                    u32x4 R[kScanChunk];
+#pragma unroll
+                    for (int k = 0; k < kScanChunk; k++)
+                        R[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u0 + k * 64 + lane) * 16, 0, 0));
+                    if (counted) {
+#pragma unroll
+                        for (int k = 0; k < kScanChunk; k++) {
+                            cnt(R[k].x, cv0, ca0); cnt(R[k].y, cv1, ca1); cnt(R[k].z, cv2, ca2); cnt(R[k].w, cv3, ca3);
+                        }
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < kScanChunk; k++) hits |= unit_hits<0>(R[k]);
+                    }
+                }
+                if (counted) {
+                    for (int sft = (int)U; sft < 64; sft <<= 1) {
+                        cv0 += __shfl_xor(cv0, sft, 64); cv1 += __shfl_xor(cv1, sft, 64);
+                        cv2 += __shfl_xor(cv2, sft, 64); cv3 += __shfl_xor(cv3, sft, 64);
+                        ca0 += __shfl_xor(ca0, sft, 64); ca1 += __shfl_xor(ca1, sft, 64);
+                        ca2 += __shfl_xor(ca2, sft, 64); ca3 += __shfl_xor(ca3, sft, 64);
+                    }
+                    auto nz = [](uint32_t w) -> uint32_t { return nib4((((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u); };
+                    hits = nz(ca0) | (nz(ca1) << 4) | (nz(ca2) << 8) | (nz(ca3) << 12);
+                } else {
+                    for (int sft = (int)U; sft < 64; sft <<= 1) hits |= __shfl_xor(hits, sft, 64);
+                }
+                uint32_t cm = hits & ok & ~need;
+                if (lead) ncand += (unsigned long long)__popc(cm);
+                if (gp.ablate & 1) continue;
+                const bool bound = bound_on && counted;
+                if (bound && __ballot(cm != 0)) {
+                    const u32x4 nref = {cv0 - ca0, cv1 - ca1, cv2 - ca2, cv3 - ca3}, nalt = {ca0, ca1, ca2, ca3};
+                    uint32_t c = cm;
+                    while (c) {
+                        const int k = __builtin_ctz(c);
+                        c &= c - 1u;
+                        const long long nr = (unit_dword(nref, k >> 2) >> (8 * (k & 3))) & 0xFFu;
+                        const long long na = (unit_dword(nalt, k >> 2) >> (8 * (k & 3))) & 0xFFu;
+                        if (nr * tabs->c_r1 - na * tabs->c_x1 > th && nr * tabs->c_r2 - na * tabs->c_x2 > to &&
+                            nr * tabs->c_r2 - na * tabs->c_x1 > th)
+                            cm &= ~(1u << k);
+                    }
+                }
+                while (__ballot(cm != 0)) {
+                    const bool has = cm != 0;
+                    const int k = has ? __builtin_ctz(cm) : 0;
+                    cm &= cm - 1u;
+                    const int sel = k >> 2, shb = 8 * (k & 3);
+                    bool keep = has;
+                    if (bound) {
+                        unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+                        auto add = [&](const u32x4 d) {
+                            const uint32_t cd = (unit_dword(d, sel) >> shb) & 0xFFu;
+                            if (cd & 0x80u) {
+                                const uint32_t a = (cd >> 5) & 3u;
+                                int q = (int)(cd & 31u);
+                                q = q > maxq ? maxq : q;
+                                const unsigned long long w = sh.w[a == 0 ? 0 : 1][q];
+                                a0 += a == 0 ? w : 0ull;
+                                a1 += a == 1 ? w : 0ull;
+                                a2 += a == 2 ? w : 0ull;
+                                a3 += a == 3 ? w : 0ull;
+                            }
+                        };
+                        nexact++;
+                        for (int32_t u0 = 0; u0 < nunits; u0 += kScanChunk * 64) {
+                            u32x4 R[kScanChunk];
+#pragma unroll
+                            for (int kk = 0; kk < kScanChunk; kk++)
+                                R[kk] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u0 + kk * 64 + lane) * 16, 0, 0));
+#pragma unroll
+                            for (int kk = 0; kk < kScanChunk; kk++) add(R[kk]);
+                        }
+                        for (int sft = (int)U; sft < 64; sft <<= 1) {
+                            a0 += __shfl_xor(a0, sft, 64);
+                            a1 += __shfl_xor(a1, sft, 64);
+                            a2 += __shfl_xor(a2, sft, 64);
+                            a3 += __shfl_xor(a3, sft, 64);
+                        }
+                        const long long R1 = (long long)(a0 & 0xFFFFFFFFull), R2 = (long long)(a0 >> 32);
+                        const long long x1 = (long long)(a1 & 0xFFFFFFFFull), y1 = (long long)(a2 & 0xFFFFFFFFull);
+                        const long long z1 = (long long)(a3 & 0xFFFFFFFFull);
+                        const long long x2 = (long long)(a1 >> 32), y2 = (long long)(a2 >> 32), z2 = (long long)(a3 >> 32);
+                        const bool drop = (R1 - x1 > th) && (R1 - y1 > th) && (R1 - z1 > th) &&
+                                          (R2 - x2 > to) && (R2 - y2 > to) && (R2 - z2 > to) &&
+                                          (R2 - x1 - y1 > th) && (R2 - x1 - z1 > th) && (R2 - y1 - z1 > th);
+                        keep = has && !drop;
+                    }
+                    if (keep) need |= 1u << k;
+                }
+            }
+        }
+        // queue the open positions (the lead lane of each column)
+        while (__ballot(need != 0)) {
+            const bool has = need != 0;
+            const int k = has ? __builtin_ctz(need) : 0;
+            need &= need - 1u;
+            const bool emit = has && lead;
+            const unsigned long long m = __ballot(emit);
+            if (!m) continue;
+            const int32_t nm = __popcll(m);
+            if (qn + nm > kWaveQ) { wave_flush(sh, wv, lane, qn, queue, counters, qcap); qn = 0; }
+            if (emit) {
+                const int32_t idx = qn + __popcll(m & ((1ull << lane) - 1ull));
+                const uint32_t rcode = (unit_dword(rc, k >> 2) >> (8 * (k & 3))) & 0xFFu;
+                sh.q[wv][idx] = QueueSite{tstart + col * 16 + k, (int32_t)rcode};
+            }
+            qn += nm;
+        }
+    }
+    for (int sft = 1; sft < 64; sft <<= 1) ncand += __shfl_xor(ncand, sft, 64);
+    if (lane == 0) { sh.qn[wv] = qn; sh.ncand[wv] = ncand; sh.nexact[wv] = nexact; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t tot = 0;
+        unsigned long long nc = 0, ne = 0;
+        for (int w = 0; w < kScanWaves; w++) { sh.qbase[w] = tot; tot += sh.qn[w]; nc += sh.ncand[w]; ne += sh.nexact[w]; }
+        if (ne) atomicAdd(&counters[3], ne);
+        const unsigned long long base = tot ? atomicAdd(&counters[2], (unsigned long long)tot) : 0ull;
+        for (int w = 0; w < kScanWaves; w++) sh.qbase[w] += (int32_t)base;
+        if (nc) atomicAdd(&counters[1], nc);
+    }
+    __syncthreads();
+    {
+        const int64_t base = sh.qbase[wv];
+        for (int i = lane; i < qn; i += 64)
+            if (base + i < qcap) queue[base + i] = sh.q[wv][i];
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// KPM: population genotyping of the queued positions -- one workgroup per position
+// ------------------------------------------------------------------------------------------
+// MultisampleVariantsDetector.onPileup (discovery/MultisampleVariantsDetector.java:522-558) for an
+// SNV pileup: the reads covering the position are gathered in pending order into LDS; the pooled
+// counts give the candidate alleles (SingleSampleVariantPileupListener.createSNVVariantPool, :297-332);
+// thread s tallies sample s in its read-group order (PileupRecord.getAlleleCalls, :104-111; the fp64
+// sums in the reference's order) and genotypes it (genotypeVariantSample, :361-391, with
+// VariantDiscoverySNVQAlgorithm.genotypeSNV, :21-97); the multi-allelic loop (discoverPopulationSNV,
+// :585-597, makeNewVariant :642-656) and the variant QS (genotypeVariant, :674-693) are block reductions.
+constexpr int kPopThreads = 256;
+static_assert(kPopThreads >= kMaxSamplesDevice, "one thread per sample");
+
+struct PopCall {
+    int kind, n_called, c0, c1, gq, total_cn;
+    int acn[4];
+};
+
+__device__ inline int tri_d(int i, int j) {      // upper-triangle index of L[i][j] (symmetric, f == g)
+    const int a = i < j ? i : j, b = i < j ? j : i;
+    return (a == 0 ? 0 : a == 1 ? 4 : a == 2 ? 7 : 9) + (b - a);
+}
+__device__ inline double sel10(const double* L, int k) {
+    double v = 0;
+#pragma unroll
+    for (int e = 0; e < 10; e++) v = e == k ? L[e] : v;
+    return v;
+}
+__device__ inline int sel4i(const int* a, int k) {
+    int v = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) v = e == k ? a[e] : v;
+    return v;
+}
+
+// CalledSNV.updateAllelesCopyNumberFromCounts (variants/CalledSNV.java:134-158)
+__device__ inline void csnv_cn(int genotype, int cref, int calt, int total, int* tot_out, int* ref_out) {
+    int ref = 0;
+    if (genotype == -1) { *tot_out = total; *ref_out = 0; return; }
+    if (genotype == 0) ref = total;
+    else if (genotype == 2) ref = 0;
+    else if (total <= 2) { total = 2; ref = 1; }
+    else {
+        const double sum = (double)cref + (double)calt;
+        double prop = sum > 0 ? (double)cref / sum : 0.5;
+        if (prop > 1) prop = 1;
+        ref = (int16_t)java_round_d(prop * total);
+        if (ref == 0) ref = 1;
+        else if (ref >= total) ref = total - 1;
+    }
+    *tot_out = total;
+    *ref_out = ref;
+}
+// CalledGenomicVariantImpl.updateAllelesCopyNumberFromCounts (variants/CalledGenomicVariantImpl.java:228-282)
+__device__ inline void cgv_cn(PopCall& c, int total, const int* rcounts, bool report) {
+    c.total_cn = total;
+    c.acn[0] = c.acn[1] = c.acn[2] = c.acn[3] = 0;
+    if (c.n_called == 0) return;
+    const int called[2] = {c.c0, c.c1};
+    if (c.n_called == 1 && c.c0 == 0) { c.acn[0] = total; return; }
+    const int nc = c.n_called;
+    auto addcn = [&](int j, int v) {
+#pragma unroll
+        for (int e = 0; e < 4; e++) if (e == j) c.acn[e] += v;
+    };
+    auto getcn = [&](int j) -> int { return sel4i(c.acn, j); };
+    if (total <= nc) { for (int i = 0; i < nc; i++) addcn(called[i], 1); return; }
+    if (!report) {
+        const int def = total / nc;
+        for (int i = 0; i < nc; i++) addcn(called[i], def);
+        addcn(called[0], total - def * nc);
+        return;
+    }
+    int rc[2] = {0, 0}, tr = 0;
+    for (int i = 0; i < nc; i++) { rc[i] = sel4i(rcounts, called[i]); if (rc[i] == 0) rc[i] = 1; tr += rc[i]; }
+    int tc = 0;
+    for (int i = 0; i < nc; i++) {
+        const long long r = java_round_d((double)total * rc[i] / tr);
+        const int v = (int)(r > 1 ? r : 1);
+        addcn(called[i], v - getcn(called[i]));
+        tc += v;
+    }
+    if (tc < total) addcn(called[0], total - tc);
+    else {
+        int ex = tc - total;
+        for (int i = nc - 1; ex > 0 && i >= 0; i--) {
+            const int cur = getcn(called[i]);
+            const int rm = ex < cur - 1 ? ex : cur - 1;
+            addcn(called[i], -rm);
+            ex -= rm;
+        }
+    }
+}
+
+// genotypeVariantSample with a fresh listener (minQuality = DEF_MIN_QUALITY 40) + genotypeSNV
+__device__ PopCall genotype_sample_d(const double* L, const int* cnt, int total, int nal, const int* idx,
+                                     const GenotypeParams& gp, int ploidy) {
+    PopCall c;
+    c.kind = 1; c.n_called = 0; c.c0 = 0; c.c1 = 0; c.gq = 0; c.total_cn = ploidy;
+    c.acn[0] = c.acn[1] = c.acn[2] = c.acn[3] = 0;
+    if (total == 0) return c;                   // undecided CalledGenomicVariantImpl(variant, new byte[0])
+    const double ph = gp.log_prior_homo, px = gp.log_prior_hetero;
+    double ev[16] = {L[0] + ph, L[1] + px, L[2] + px, L[3] + px,
+                     L[4] + ph, L[1] + px, L[5] + px, L[6] + px,
+                     L[7] + ph, L[2] + px, L[5] + px, L[8] + px,
+                     L[9] + ph, L[3] + px, L[6] + px, L[8] + px};
+    double logMax = 1;
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+        if (logMax > 0 || logMax < ev[k]) logMax = ev[k];
+    double totalProb = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const double x = ev[k] - logMax;
+        ev[k] = x < -20 ? 0.0 : pow(10.0, x);
+        totalProb += ev[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) ev[k] = ev[k] / totalProb;
+    auto post = [&](int a, int b) -> double {
+        const int k = a == b ? 4 * a : (b < a ? 4 * a + 1 + b : 4 * a + b);
+        double v = 0;
+#pragma unroll
+        for (int e = 0; e < 16; e++) v = (e == k) ? ev[e] : v;
+        return v;
+    };
+    if (nal == 2) {
+        const int r = idx[0], a = idx[1];
+        double pMax = post(r, r);
+        int genotype = 0;
+        const double pHomoAlt = post(a, a);
+        if (pHomoAlt > pMax + 0.01) { pMax = pHomoAlt; genotype = 2; }
+        const double pHetero = post(r, a) + post(a, r);
+        if (pHetero > pMax + 0.01) { pMax = pHetero; genotype = 1; }
+        int gq = phred_d(1 - pMax);
+        if (gq == 0) genotype = -1;
+        c.kind = 0;
+        int tot = 0, ref = 0;
+        csnv_cn(genotype, sel4i(cnt, r), sel4i(cnt, a), ploidy, &tot, &ref);
+        if (40 > gq) { genotype = -1; gq = 0; ref = 0; }      // makeUndecided (CalledSNV.java:279-285)
+        c.gq = gq;
+        c.total_cn = tot;
+        if (genotype == -1) c.n_called = 0;
+        else if (genotype == 0) { c.n_called = 1; c.c0 = 0; }
+        else if (genotype == 2) { c.n_called = 1; c.c0 = 1; }
+        else { c.n_called = 2; c.c0 = 0; c.c1 = 1; }
+        c.acn[0] = genotype == -1 ? 0 : ref;
+        c.acn[1] = genotype == -1 ? 0 : tot - ref;
+        return c;
+    }
+    int rcounts[4] = {0, 0, 0, 0};
+    for (int i = 0; i < nal; i++) rcounts[i] = sel4i(cnt, idx[i]);
+    int bi = 0, bj = 0;                                       // getIndexesMaxGenotype(report, 0)
+    double probMax = post(idx[0], idx[0]);
+    for (int i = 0; i < nal; i++)
+        for (int j = i; j < nal; j++) {
+            double g = post(idx[i], idx[j]);
+            if (i != j) g += post(idx[j], idx[i]);
+            if (g > probMax + 0.01) { probMax = g; bi = i; bj = j; }
+        }
+    double maxP = post(idx[bi], idx[bj]);
+    if (bi != bj) { maxP += post(idx[bj], idx[bi]); c.n_called = 2; c.c0 = bi; c.c1 = bj; }
+    else { c.n_called = 1; c.c0 = bi; }
+    c.gq = phred_d(1 - maxP);
+    c.kind = 1;
+    cgv_cn(c, ploidy, rcounts, true);
+    if (40 > c.gq) { c.n_called = 0; c.gq = 0; cgv_cn(c, c.total_cn, rcounts, true); }   // makeUndecided
+    return c;
+}
+
+__global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
+    const QueueSite* __restrict__ queue, const unsigned long long* qn, int64_t qcap,
+    const int4* __restrict__ reads, int64_t n_reads, const int32_t* __restrict__ lb,
+    const uint8_t* __restrict__ slots, int32_t S, const LikTables* __restrict__ tabs, GenotypeParams gp,
+    const int8_t* __restrict__ sample_nrank, int32_t n_samples, double min_adf, int32_t ploidy,
+    ngsep_popsite_out* __restrict__ sites, ngsep_sample_call* __restrict__ calls,
+    unsigned long long* counters, int64_t cap) {
+    __shared__ uint32_t s_list[kPopListCap];     // code | flags << 8 (strand bit 8, rank 9-15, sample+1 16-31)
+    __shared__ double s_t[3][32];
+    __shared__ int32_t s_wn[kPopThreads / 64];
+    __shared__ int32_t s_pc[4];
+    __shared__ int32_t s_n, s_called, s_qs;
+    __shared__ unsigned long long s_base;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid < 96) s_t[tid >> 5][tid & 31] = (tid < 32 ? tabs->A : tid < 64 ? tabs->H : tabs->E)[tid & 31];
+    int64_t n = (int64_t)*qn;
+    if (n > qcap) n = qcap;
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        __syncthreads();
+        const QueueSite qs = queue[i];
+        const int32_t gpos = qs.gpos;
+        const uint32_t rc = (uint32_t)qs.rc;
+        if (tid == 0) { s_n = 0; s_pc[0] = s_pc[1] = s_pc[2] = s_pc[3] = 0; s_called = 0; s_qs = 0; }
+        // 1. the reads covering gpos, in pending order (the table is sorted by start)
+        for (int64_t r0 = lb[gpos >> 6];; r0 += kPopThreads) {
+            const int64_t r = r0 + tid;
+            const int4 h = r < n_reads ? reads[r] : int4{INT32_MAX, 0, 0, 0};
+            const bool in = h.x <= gpos;
+            const bool cov = in && h.y >= gpos;
+            const int32_t o = cov ? gpos - h.x : 0;
+            const uint32_t code = cov ? (uint32_t)slots[(int64_t)(h.z + o / S) * S + (o % S)] : 0u;
+            const bool keep = code != 0;                          // CountsHelper.java:210: a call is counted
+            const unsigned long long m = __ballot(keep);
+            if (lane == 0) s_wn[wv] = __popcll(m);
+            __syncthreads();
+            int32_t woff = 0, tot = 0;
+            for (int w = 0; w < kPopThreads / 64; w++) { if (w < wv) woff += s_wn[w]; tot += s_wn[w]; }
+            const int32_t pos_l = s_n + woff + __popcll(m & ((1ull << lane) - 1ull));
+            if (keep && pos_l < kPopListCap) s_list[pos_l] = code | ((uint32_t)h.w << 8);
+            const int stop = __syncthreads_or(!in);
+            if (tid == 0) s_n += tot;
+            if (stop) break;
+        }
+        __syncthreads();
+        const int32_t nl = s_n;
+        if (nl > kPopListCap) {                                   // deeper than the LDS list: reported, not called
+            if (tid == 0) atomicOr(&counters[3], 1ull << 63);
+            continue;
+        }
+        if (nl == 0) continue;                                    // createSNVVariantPool: totalCount 0
+        // 2. pooled counts over every alignment (getAlleleCalls(1, null))
+        for (int e = tid; e < nl; e += kPopThreads) {
+            const uint32_t cd = s_list[e] & 0xFFu;
+            if (cd & 0x80u) atomicAdd(&s_pc[(cd >> 5) & 3], 1);
+        }
+        // 3. per-sample tallies, thread = sample, in the sample's read-group order
+        int total = 0;
+        int cnt[4] = {0, 0, 0, 0};
+        double L[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        if (tid < n_samples) {
+            const int nr = sample_nrank[tid];
+            const uint32_t me = (uint32_t)(tid + 1);
+            for (int rk = 0; rk < nr; rk++) {
+                for (int e = 0; e < nl; e++) {
+                    const uint32_t ent = s_list[e];
+                    if ((ent >> 16) != me || ((ent >> 9) & 127u) != (uint32_t)rk) continue;
+                    total++;
+                    const uint32_t cd = ent & 0xFFu;
+                    if (!(cd & 0x80u)) continue;
+                    const uint32_t a = (cd >> 5) & 3u;
+                    int q = (int)(cd & 31u);
+                    q = q > gp.max_q ? gp.max_q : q;
+                    const double A = s_t[0][q], H = s_t[1][q], E = s_t[2][q];
+                    cnt[0] += a == 0; cnt[1] += a == 1; cnt[2] += a == 2; cnt[3] += a == 3;
+                    L[0] += a == 0 ? A : E;
+                    L[4] += a == 1 ? A : E;
+                    L[7] += a == 2 ? A : E;
+                    L[9] += a == 3 ? A : E;
+                    L[1] += a <= 1 ? H : E;
+                    L[2] += (a & 1) == 0 ? H : E;
+                    L[3] += (a == 0 || a == 3) ? H : E;
+                    L[5] += (a == 1 || a == 2) ? H : E;
+                    L[6] += (a & 1) == 1 ? H : E;
+                    L[8] += a >= 2 ? H : E;
+                }
+            }
+        }
+        __syncthreads();
+        // 4. candidate alleles from the pooled counts (createSNVVariantPool)
+        if (!(rc & 0x80u)) continue;                               // N (or masked) reference: no variant
+        const int refIdx = (int)((rc >> 5) & 3u);
+        const int pc[4] = {s_pc[0], s_pc[1], s_pc[2], s_pc[3]};
+        const int sum = pc[0] + pc[1] + pc[2] + pc[3];
+        double minCount = min_adf * sum;
+        if (minCount < 1) minCount = 1;
+        int idx[4] = {refIdx, 0, 0, 0};
+        int nal = 1;
+        for (int a = 0; a < 4; a++)
+            if (a != refIdx && pc[a] >= minCount) { idx[nal < 4 ? nal : 3] = a; nal++; }
+        if (nal < 2) continue;
+        int multisnv = nal > 2;
+        // 5. genotype every sample; shrink a multi-allelic variant to the called alleles
+        PopCall call;
+        int qsv = 0;
+        for (;;) {
+            if (tid == 0) { s_called = 0; s_qs = 0; }
+            __syncthreads();
+            if (tid < n_samples) {
+                call = genotype_sample_d(L, cnt, total, nal, idx, gp, ploidy);
+                const bool homref = call.n_called == 1 && call.c0 == 0;
+                if (call.n_called > 0 && !homref) atomicMax(&s_qs, call.gq);
+                int bits = 0;
+                if (call.n_called >= 1) bits |= 1 << idx[call.c0 & 3];
+                if (call.n_called == 2) bits |= 1 << idx[call.c1 & 3];
+                if (bits) atomicOr(&s_called, bits);
+            }
+            __syncthreads();
+            qsv = s_qs;
+            const int set = s_called | (1 << refIdx);
+            __syncthreads();                                       // everyone has read before the next reset
+            if (nal <= 2) break;
+            if (__popc(set) == nal) break;
+            nal = 1;
+            for (int a = 0; a < 4; a++) if (a != refIdx && (set >> a & 1)) idx[nal++] = a;
+            multisnv = 0;                                          // makeNewVariant: SNV or GenomicVariantImpl (no TYPE)
+            if (nal < 2) break;
+        }
+        if (nal < 2) continue;                                     // only the reference allele is left
+        if (qsv == 0 || qsv < gp.min_quality) continue;            // MultisampleVariantsDetector.java:534
+        // 6. emit the site and its calls
+        __syncthreads();
+        if (tid == 0) s_base = atomicAdd(&counters[0], 1ull);
+        __syncthreads();
+        const unsigned long long at = s_base;
+        if ((int64_t)at >= cap) continue;
+        if (tid == 0) {
+            ngsep_popsite_out o;
+            o.seq_id = -1; o.pos = gpos; o.n_alleles = (int8_t)nal;
+            for (int k = 0; k < 4; k++) o.alleles[k] = (int8_t)(k < nal ? idx[k] : -1);
+            o.multisnv_type = (int8_t)multisnv; o.qual = (int16_t)qsv; o.pad = 0;
+            sites[at] = o;
+        }
+        if (tid < n_samples) {
+            ngsep_sample_call o;
+            o.kind = (int8_t)call.kind; o.n_called = (int8_t)call.n_called;
+            o.called[0] = (int8_t)call.c0; o.called[1] = (int8_t)call.c1;
+            o.gq = (int16_t)call.gq; o.total_cn = (int16_t)call.total_cn;
+            o.dp = total;
+            for (int k = 0; k < 4; k++) { o.counts[k] = cnt[k]; o.acn[k] = (int16_t)call.acn[k]; o.pl[k] = 0; }
+            for (int k = 4; k < 10; k++) o.pl[k] = 0;
+            // PL (VCFFileWriter.java:200-212) from the call report
+            if (call.kind == 0) {
+                const float hr = (float)sel10(L, tri_d(idx[0], idx[0])), ha = (float)sel10(L, tri_d(idx[1], idx[1]));
+                const float ra = (float)sel10(L, tri_d(idx[0], idx[1])), ar = ra;
+                const bool present = (hr + ra + ar + ha) != 0;     // CalledSNV.java:422 (float sum)
+                if (present) {
+                    o.pl[0] = (int32_t)java_round_d(-10 * (double)hr);
+                    o.pl[1] = (int32_t)java_round_d(-10 * (double)ra);
+                    o.pl[2] = (int32_t)java_round_d(-10 * (double)ha);
+                }
+            } else if (total > 0) {
+                int k = 0;
+                for (int j = 0; j < nal; j++)
+                    for (int ii = 0; ii <= j; ii++) {
+                        const int32_t v = (int32_t)java_round_d(-10 * sel10(L, tri_d(idx[ii], idx[j])));
+#pragma unroll
+                        for (int e = 0; e < 10; e++) if (e == k) o.pl[e] = v;
+                        k++;
+                    }
+            }
+            calls[(int64_t)at * n_samples + tid] = o;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // KL: lb[k] = first read index whose gfirst >= 64k - pad + 1
 // ------------------------------------------------------------------------------------------
@@ -776,6 +1318,10 @@ void device_release(Device* d) {
     (void)hipFree(d->d_ref); d->d_ref = nullptr;
     (void)hipFree(d->d_lb); d->d_lb = nullptr;
     (void)hipFree(d->d_tinfo); d->d_tinfo = nullptr;
+    (void)hipFree(d->d_rows); d->d_rows = nullptr;
+    (void)hipFree(d->d_toff); d->d_toff = nullptr;
+    (void)hipFree(d->d_nrank); d->d_nrank = nullptr;
+    d->n_samples = 0;
     d->n_units = d->n_slots = d->n_lb = d->n_reads = d->g_len = d->n_tiles = 0;
 }
 
@@ -785,6 +1331,8 @@ void device_destroy(Device* d) {
     (void)hipFree(d->d_sites);
     (void)hipFree(d->d_sorted);
     (void)hipFree(d->d_keys);
+    (void)hipFree(d->d_psites);
+    (void)hipFree(d->d_pcalls);
     (void)hipFree(d->d_bucket);
     (void)hipFree(d->d_hard);
     (void)hipFree(d->d_counters);
@@ -810,7 +1358,15 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
     HIP_TRY(hipMalloc(&d->d_lb, (size_t)d->n_lb * 4));
     if (slot_bytes) HIP_TRY(hipMemcpyAsync(d->d_slots, s.h_slots.data(), (size_t)slot_bytes, hipMemcpyHostToDevice, d->stream));
     if (s.pile_bytes) HIP_TRY(hipMemcpyAsync(d->d_pile, s.h_pile.data(), (size_t)s.pile_bytes, hipMemcpyHostToDevice, d->stream));
-    if (s.n_tiles) HIP_TRY(hipMemcpyAsync(d->d_tinfo, s.h_tinfo.data(), (size_t)s.n_tiles * sizeof(TileInfo), hipMemcpyHostToDevice, d->stream));
+    if (s.n_tiles && !s.h_tinfo.empty()) HIP_TRY(hipMemcpyAsync(d->d_tinfo, s.h_tinfo.data(), (size_t)s.n_tiles * sizeof(TileInfo), hipMemcpyHostToDevice, d->stream));
+    if (s.n_samples > 0) {
+        HIP_TRY(hipMalloc(&d->d_rows, std::max<size_t>(s.h_rows.size(), 1) * sizeof(uint16_t)));
+        HIP_TRY(hipMalloc(&d->d_toff, std::max<size_t>(s.h_toff.size(), 1) * sizeof(int64_t)));
+        HIP_TRY(hipMalloc(&d->d_nrank, (size_t)s.n_samples));
+        if (!s.h_rows.empty()) HIP_TRY(hipMemcpyAsync(d->d_rows, s.h_rows.data(), s.h_rows.size() * sizeof(uint16_t), hipMemcpyHostToDevice, d->stream));
+        if (!s.h_toff.empty()) HIP_TRY(hipMemcpyAsync(d->d_toff, s.h_toff.data(), s.h_toff.size() * sizeof(int64_t), hipMemcpyHostToDevice, d->stream));
+        d->n_samples = s.n_samples;
+    }
     if (s.n_reads) HIP_TRY(hipMemcpyAsync(d->d_reads, s.h_reads.data(), (size_t)s.n_reads * 16, hipMemcpyHostToDevice, d->stream));
     HIP_TRY(hipMemsetAsync(d->d_ref, 0, (size_t)s.g_len + 64, d->stream));
     HIP_TRY(hipMemcpyAsync(d->d_ref, s.h_ref.data(), (size_t)s.g_len, hipMemcpyHostToDevice, d->stream));
@@ -983,6 +1539,94 @@ int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypePar
     *n_candidates = (int64_t)d->h_counters[1];
     d->last_hard = (int64_t)d->h_counters[2];
     d->last_exact = (int64_t)d->h_counters[3];
+    return 0;
+}
+
+// MultisampleVariantsDetector run: KTM over every resident tile, KPM over the queued positions,
+// D2H of the emitted sites and their per-sample calls (unordered; the host orders them)
+int device_run_multi(Device* d, const Staged& s, const LikTables& t, const GenotypeParams& g,
+                     const std::vector<int8_t>& sample_nrank, double min_adf, int ploidy,
+                     std::vector<ngsep_popsite_out>* sites, std::vector<ngsep_sample_call>* calls,
+                     double* scan_ms, double* geno_ms, double* total_ms, int64_t* n_candidates, std::string& err) {
+    HIP_TRY(hipSetDevice(d->ordinal));
+    auto t0 = std::chrono::steady_clock::now();
+    const int32_t S = d->n_samples;
+    if (S <= 0 || (int32_t)sample_nrank.size() != S) { err = "multisample run without samples (ngsep_set_samples)"; return -1; }
+    if (S > kMaxSamplesDevice) { err = "too many samples for one device run"; return -1; }
+    HIP_TRY(hipMemcpyAsync(d->d_nrank, sample_nrank.data(), (size_t)S, hipMemcpyHostToDevice, d->stream));
+    int64_t want = std::max<int64_t>(d->last_n_sites + d->last_n_sites / 4 + 1024, 4096);
+    if (want > d->cap_psites) {
+        (void)hipFree(d->d_psites);
+        (void)hipFree(d->d_pcalls);
+        d->d_psites = nullptr;
+        d->d_pcalls = nullptr;
+        HIP_TRY(hipMalloc(&d->d_psites, (size_t)want * sizeof(ngsep_popsite_out)));
+        HIP_TRY(hipMalloc(&d->d_pcalls, (size_t)want * S * sizeof(ngsep_sample_call)));
+        d->cap_psites = want;
+    }
+    int64_t qwant = std::max<int64_t>(s.g_len / 64 + 65536, 65536);
+    if (qwant > d->cap_hard) {
+        (void)hipFree(d->d_hard);
+        HIP_TRY(hipMalloc(&d->d_hard, (size_t)qwant * sizeof(QueueSite)));
+        d->cap_hard = qwant;
+    }
+    if (!d->tables_valid || std::memcmp(&d->h_tables, &t, sizeof(LikTables)) != 0) {
+        d->h_tables = t;
+        HIP_TRY(hipMemcpyAsync(d->d_tables, &d->h_tables, sizeof(LikTables), hipMemcpyHostToDevice, d->stream));
+        d->tables_valid = true;
+    }
+    unsigned long long* ctr = d->d_counters + 4 * d->cpar;
+    HIP_TRY(hipMemsetAsync(ctr, 0, 4 * sizeof(unsigned long long), d->stream));
+    HIP_TRY(hipEventRecord(d->ev[0], d->stream));
+    if (d->n_tiles > 0) {
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_tile_pileup_multi, kScanThreads, 0) != hipSuccess || per_cu < 1) per_cu = 2;
+        const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((d->n_tiles + kScanWaves - 1) / kScanWaves, (int64_t)d->n_cu * per_cu));
+        hipLaunchKernelGGL(k_tile_pileup_multi, dim3((unsigned)nblk), dim3(kScanThreads), 0, d->stream, (const u32x4*)d->d_pile,
+                           d->d_toff, d->d_rows, S, d->d_ref, d->log2_tile, d->n_tiles, d->d_tables, g, d->d_hard, ctr,
+                           d->cap_hard);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipEventRecord(d->ev[1], d->stream));
+    hipLaunchKernelGGL(k_posterior_multi, dim3(2048), dim3(kPopThreads), 0, d->stream, d->d_hard, ctr + 2, d->cap_hard,
+                       d->d_reads, d->n_reads, d->d_lb, d->d_slots, d->slot_size, d->d_tables, g, d->d_nrank, S, min_adf,
+                       ploidy, d->d_psites, d->d_pcalls, ctr, d->cap_psites);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(d->ev[2], d->stream));
+    HIP_TRY(hipMemcpyAsync(d->h_counters, ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, d->stream));
+    HIP_TRY(hipStreamSynchronize(d->stream));
+    const unsigned long long c3 = d->h_counters[3];
+    if (c3 >> 63) { err = "a position is covered by more reads than the population kernel holds (" + std::to_string(kPopListCap) + ")"; return -1; }
+    const int64_t n = (int64_t)d->h_counters[0];
+    if ((int64_t)d->h_counters[2] > d->cap_hard) {
+        (void)hipFree(d->d_hard);
+        d->d_hard = nullptr;
+        HIP_TRY(hipMalloc(&d->d_hard, (size_t)(d->h_counters[2] + 1024) * sizeof(QueueSite)));
+        d->cap_hard = (int64_t)d->h_counters[2] + 1024;
+        return device_run_multi(d, s, t, g, sample_nrank, min_adf, ploidy, sites, calls, scan_ms, geno_ms, total_ms, n_candidates, err);
+    }
+    if (n > d->cap_psites) {
+        d->last_n_sites = n;
+        d->cap_psites = 0;
+        return device_run_multi(d, s, t, g, sample_nrank, min_adf, ploidy, sites, calls, scan_ms, geno_ms, total_ms, n_candidates, err);
+    }
+    sites->resize((size_t)n);
+    calls->resize((size_t)n * S);
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(sites->data(), d->d_psites, (size_t)n * sizeof(ngsep_popsite_out), hipMemcpyDeviceToHost, d->stream));
+        HIP_TRY(hipMemcpyAsync(calls->data(), d->d_pcalls, (size_t)n * S * sizeof(ngsep_sample_call), hipMemcpyDeviceToHost, d->stream));
+        HIP_TRY(hipStreamSynchronize(d->stream));
+    }
+    d->last_n_sites = n;
+    d->last_hard = (int64_t)d->h_counters[2];
+    d->last_exact = (int64_t)(c3 & 0x7FFFFFFFFFFFFFFFull);
+    float a = 0, a2 = 0;
+    (void)hipEventElapsedTime(&a, d->ev[0], d->ev[1]);
+    (void)hipEventElapsedTime(&a2, d->ev[1], d->ev[2]);
+    *scan_ms = a;
+    *geno_ms = a2;
+    *total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    *n_candidates = (int64_t)d->h_counters[1];
     return 0;
 }
 

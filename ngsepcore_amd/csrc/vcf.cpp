@@ -2,6 +2,7 @@
 // VCFFileHeader.makeDefaultEmptyHeader/print (vcf/VCFFileHeader.java:46-95,219-245) and
 // VCFFileWriter.printVCFRecord/printGenotypeInfo (vcf/VCFFileWriter.java:44-308) for
 // CalledSNV (variants/CalledSNV.java) and triallelic CalledGenomicVariantImpl calls.
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -145,9 +146,105 @@ int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& o)
     return (int64_t)(o.size() - start);
 }
 
+// ---- MultisampleVariantsDetector output ----
+// VCFFileHeader.print with the detector's samples (vcf/VCFFileHeader.java:219-245)
+std::string format_population_header(const ngsep_ctx* c) {
+    std::string h = "##fileformat=VCFv4.2\n";
+    for (const auto& l : kHeaderLines) {
+        h += "##"; h += l[0]; h += "=<ID="; h += l[1]; h += ",Number="; h += l[3];
+        h += ",Type="; h += l[4]; h += ",Description="; h += l[2]; h += ">\n";
+    }
+    if (c->params.print_sample_ploidy)
+        for (const std::string& id : c->sample_ids) h += "##SAMPLE=<ID=" + id + ",PL=" + std::to_string(c->params.ploidy) + ">\n";
+    h += "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT";
+    for (const std::string& id : c->sample_ids) { h += '\t'; h += id; }
+    h += '\n';
+    return h;
+}
+
+// DecimalFormat("##0.0#") (main/io/ParseUtils.java:29): HALF_EVEN rounding of the exact binary value
+static void app_fmt2(std::string& o, double x) {
+    const double p = x * 100.0, err = std::fma(x, 100.0, -p);
+    const double k = std::floor(p), fr = p - k;
+    long long n = (long long)k;
+    if (fr > 0.5 || (fr == 0.5 && (err > 0 || (err == 0 && (n & 1))))) n++;
+    char b[48];
+    if (n % 10 == 0) std::snprintf(b, sizeof b, "%lld.%lld", n / 100, (n % 100) / 10);
+    else std::snprintf(b, sizeof b, "%lld.%02lld", n / 100, n % 100);
+    o += b;
+}
+
+// VCFFileWriter.printVCFRecord (:44-68) of VCFRecord.createDefaultPopulationVCFRecord: INFO from
+// DiversityStatistics.calculateDiversityStatistics(calls, false) (variants/DiversityStatistics.java:123-218)
+// in VCFRecord.updateDiversityStatistics order (NS, AN, AFS, OH, MAF; vcf/VCFRecord.java:288-301),
+// then TYPE; FORMAT GT:PL:GQ:DP:BSDP:ACN per sample (printGenotypeInfo, :159-308)
+void format_population_site(const ngsep_ctx* c, const ngsep_popsite_out& s, const ngsep_sample_call* calls, std::string& o) {
+    static const char kB[] = "ACGT";
+    const int S = (int)c->sample_ids.size();
+    const int ploidy = c->params.ploidy;
+    const std::string& name = (s.seq_id >= 0 && s.seq_id < (int)c->seq_names.size()) ? c->seq_names[s.seq_id] : std::string("?");
+    o += name; o += '\t'; app(o, s.pos); o += "\t.\t"; o += kB[(int)s.alleles[0]]; o += '\t';
+    for (int i = 1; i < s.n_alleles; i++) { if (i > 1) o += ','; o += kB[(int)s.alleles[i]]; }
+    o += '\t'; app(o, s.qual); o += "\t.\t";
+    int counts[4] = {0, 0, 0, 0}, sum = 0, ng = 0, nhet = 0;
+    for (int k = 0; k < S; k++) {
+        const ngsep_sample_call& cl = calls[k];
+        if (cl.n_called == 0) continue;
+        ng++;
+        if (cl.n_called > 1) nhet++;
+        for (int i = 0; i < cl.n_called; i++) { const int j = cl.called[i]; counts[j] += cl.acn[j]; sum += cl.acn[j]; }
+    }
+    int ncalled = 0, minAC = 0;
+    for (int i = 0; i < s.n_alleles; i++)
+        if (counts[i] > 0) { ncalled++; if (minAC == 0 || minAC > counts[i]) minAC = counts[i]; }
+    o += "NS="; app(o, ng); o += ";AN="; app(o, ncalled); o += ";AFS=";
+    for (int i = 0; i < s.n_alleles; i++) { if (i) o += ','; app(o, counts[i]); }
+    o += ";OH="; app_fmt2(o, ng > 0 ? (double)nhet / ng : 0.0);
+    if (s.n_alleles == 2) { o += ";MAF="; app_fmt2(o, ncalled < 2 ? 0.0 : (double)minAC / sum); }
+    if (s.multisnv_type) o += ";TYPE=MULTISNV";
+    o += "\tGT:PL:GQ:DP:BSDP:ACN";
+    for (int k = 0; k < S; k++) {
+        const ngsep_sample_call& cl = calls[k];
+        o += '\t';
+        if (cl.n_called == 0) o += ploidy > 1 ? "./." : ".";
+        else if (cl.n_called == 1) { app(o, cl.called[0]); if (ploidy > 1) { o += '/'; app(o, cl.called[0]); } }
+        else { app(o, cl.called[0]); o += '/'; app(o, cl.called[1]); }
+        o += ':';
+        const int npl = s.n_alleles * (s.n_alleles + 1) / 2;
+        for (int i = 0; i < npl; i++) { if (i) o += ','; app(o, cl.pl[i]); }
+        o += ':'; app(o, cl.gq); o += ':'; app(o, cl.dp); o += ':';
+        for (int i = 0; i < 4; i++) { if (i) o += ','; app(o, cl.counts[i]); }
+        o += ':';
+        if (cl.total_cn == 0) o += '.';
+        else {
+            const int nal = cl.kind == 0 ? 2 : s.n_alleles;
+            for (int j = 0; j < nal; j++) {
+                if (j) o += ',';
+                app(o, (cl.n_called == 0 && j == 0) ? cl.total_cn : cl.acn[j]);
+            }
+        }
+    }
+    o += '\n';
+}
+
 }  // namespace ngsep
 
 using namespace ngsep;
+
+extern "C" int ngsep_write_population_vcf(ngsep_ctx* c, const char* path) {
+    if (!c || !path) return NGSEP_E_INVALID;
+    std::FILE* f = std::fopen(path, "w");
+    if (!f) return set_error(c, NGSEP_E_IO, std::string("cannot write ") + path);
+    std::string buf = format_population_header(c);
+    const size_t S = c->sample_ids.size();
+    for (size_t i = 0; i < c->pop_sites.size(); i++) {
+        format_population_site(c, c->pop_sites[i], c->pop_calls.data() + i * S, buf);
+        if (buf.size() > (1 << 20)) { std::fwrite(buf.data(), 1, buf.size(), f); buf.clear(); }
+    }
+    std::fwrite(buf.data(), 1, buf.size(), f);
+    std::fclose(f);
+    return NGSEP_OK;
+}
 
 extern "C" int ngsep_write_vcf_header(ngsep_ctx* c, const char* path) {
     if (!c || !path) return NGSEP_E_INVALID;

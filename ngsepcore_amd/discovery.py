@@ -15,7 +15,8 @@ from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
 from . import _lib
-from ._lib import NgsepError, NgsepParams, NgsepReadBatch, NgsepSiteOut, NgsepStats
+from ._lib import (NgsepError, NgsepParams, NgsepPopSiteOut, NgsepReadBatch, NgsepSampleCall, NgsepSiteOut,
+                   NgsepStats)
 
 BASES = "ACGT"
 
@@ -48,6 +49,37 @@ class CalledSite:
             i, j = j, i
         base = (0, 4, 7, 9)[i]
         return self.logc[base + j - i]
+
+
+def java_string_hash(s: str) -> int:
+    h = 0
+    for ch in s.encode("utf-16-be").decode("utf-16-be"):
+        h = (31 * h + ord(ch)) & 0xFFFFFFFF
+    return h
+
+
+def java_hashset_order(ids: Sequence[str]) -> List[int]:
+    """Iteration order of a java.util.HashSet<String> filled with ids in order (Sample.readGroups,
+    variants/Sample.java:36): buckets of the final table (16, doubled past 0.75 load), insertion order
+    inside a bucket.  Returns indexes into ids."""
+    cap = 16
+    while len(ids) > cap * 3 // 4:
+        cap *= 2
+    def bucket(i):
+        h = java_string_hash(ids[i])
+        return (h ^ (h >> 16)) & (cap - 1)
+    return sorted(range(len(ids)), key=lambda i: (bucket(i), i))
+
+
+@dataclass
+class PopulationSite:
+    """One MultisampleVariantsDetector VCF line: the variant and one call per sample."""
+    sequence: str
+    pos: int
+    alleles: List[str]
+    qual: int
+    multisnv_type: bool
+    calls: List[NgsepSampleCall]
 
 
 class GpuPileupSession:
@@ -155,6 +187,50 @@ class GpuPileupSession:
         self._check(self._lib.ngsep_write_vcf_header(self._ctx, path.encode()))
         self._check(self._lib.ngsep_append_vcf_records(self._ctx, path.encode()))
 
+    # -- multisample (MultisampleVariantsDetector)
+    def set_samples(self, read_groups: Sequence[tuple]):
+        """read_groups: (read group id, sample id) per read-group index of the batches, as the BAM
+        headers list them (MultisampleVariantsDetector.loadSamplesFromAlignmentHeaders, :499-523):
+        samples are sorted by id, each sample's groups are visited in Java HashSet order."""
+        samples = sorted({sm for _, sm in read_groups if sm is not None})
+        sidx = {sm: i for i, sm in enumerate(samples)}
+        rg_sample = [sidx[sm] if sm is not None else -1 for _, sm in read_groups]
+        rg_rank = [0] * len(read_groups)
+        for sm in samples:
+            members = [g for g, (_, s2) in enumerate(read_groups) if s2 == sm]
+            order = java_hashset_order([read_groups[g][0] for g in members])
+            for rank, k in enumerate(order):
+                rg_rank[members[k]] = rank
+        self.samples = samples
+        ids = (ctypes.c_char_p * max(len(samples), 1))(*[x.encode() for x in samples])
+        gs = (ctypes.c_int32 * max(len(read_groups), 1))(*rg_sample)
+        gr = (ctypes.c_int32 * max(len(read_groups), 1))(*rg_rank)
+        self._check(self._lib.ngsep_set_samples(self._ctx, len(samples), ids, len(read_groups), gs, gr))
+
+    def raw_population_sites(self):
+        n = ctypes.c_int64()
+        self._check(self._lib.ngsep_fetch_population_sites(self._ctx, None, None, 0, ctypes.byref(n)))
+        S = len(self.samples)
+        sites = (NgsepPopSiteOut * max(n.value, 1))()
+        calls = (NgsepSampleCall * max(n.value * S, 1))()
+        self._check(self._lib.ngsep_fetch_population_sites(self._ctx, sites, calls, n.value, ctypes.byref(n)))
+        return sites[: n.value], calls[: n.value * S]
+
+    def getPopulationVariants(self) -> List[PopulationSite]:
+        names = self.sequence_names()
+        sites, calls = self.raw_population_sites()
+        S = len(self.samples)
+        out = []
+        for i, s in enumerate(sites):
+            out.append(PopulationSite(
+                sequence=names[s.seq_id] if 0 <= s.seq_id < len(names) else "?", pos=s.pos,
+                alleles=[BASES[s.alleles[k]] for k in range(s.n_alleles)], qual=s.qual,
+                multisnv_type=bool(s.multisnv_type), calls=list(calls[i * S:(i + 1) * S])))
+        return out
+
+    def write_population_vcf(self, path: str):
+        self._check(self._lib.ngsep_write_population_vcf(self._ctx, path.encode()))
+
     def stats(self) -> NgsepStats:
         st = NgsepStats()
         self._check(self._lib.ngsep_get_stats(self._ctx, ctypes.byref(st)))
@@ -250,3 +326,64 @@ class SingleSampleVariantsDetector:
             s.load_fasta(self.genomeFile)
             s.processFile(self.inputFile, (self.outputPrefix or "variants") + ".vcf")
             self.stats = s.stats()
+
+
+class MultisampleVariantsDetector:
+    """Drop-in for ngsep.discovery.MultisampleVariantsDetector (SNV path,
+    discovery/MultisampleVariantsDetector.java:54-693; options main/CommandsDescriptor.xml).
+
+    Alignments arrive through a GpuPileupSession in multisample mode; run() processes one batch
+    stream whose read-group indexes refer to read_groups (e.g. a merged BAM of all samples)."""
+
+    DEF_MIN_QUALITY = 40
+    DEF_MIN_ALLELE_DEPTH_FREQUENCY = 0.0
+    DEF_OUTPUT_FILE = "variants.vcf"
+
+    def __init__(self):
+        self.params = default_params()
+        self.params.multisample = 1
+        self.genomeFile: Optional[str] = None
+        self.outFilename = self.DEF_OUTPUT_FILE
+        self.device = 0
+
+    def setGenome(self, v: str): self.genomeFile = v
+    def setOutFilename(self, v: str): self.outFilename = v
+    def setMinAlleleDepthFrequency(self, v: float): self.params.min_allele_depth_freq = float(v)
+    def setHeterozygosityRate(self, v: float):
+        self.params.het_rate = float(v)
+        self.params.het_rate_set = 1
+    def setMinQuality(self, v: int): self.params.min_quality = int(v)
+    def setMaxBaseQS(self, v: int): self.params.max_base_qs = int(v)
+    def setNormalPloidy(self, v: int): self.params.ploidy = int(v)
+    def setPrintSamplePloidy(self, v: bool): self.params.print_sample_ploidy = int(bool(v))
+    def setMinMQ(self, v: int): self.params.min_mq = int(v)
+    def setMaxAlnsPerStartPos(self, v: int): self.params.max_alns_per_start = int(v)
+    def setProcessNonUniquePrimaryAlignments(self, v: bool): self.params.process_nonunique = int(bool(v))
+    def setProcessSecondaryAlignments(self, v: bool): self.params.process_secondary = int(bool(v))
+    def setBasesToIgnore5P(self, v: int): self.params.ignore5 = int(v)
+    def setBasesToIgnore3P(self, v: int): self.params.ignore3 = int(v)
+    def setIgnoreLowerCaseRef(self, v: bool): self.params.ignore_lowercase_ref = int(bool(v))
+    def setQuerySeq(self, v: str): self.params.query_seq = v.encode()
+    def setQueryFirst(self, v: int): self.params.query_first = int(v)
+    def setQueryLast(self, v: int): self.params.query_last = int(v)
+
+    def session(self, read_groups: Sequence[tuple]) -> GpuPileupSession:
+        s = GpuPileupSession(self.params, self.device)
+        s.set_samples(read_groups)
+        return s
+
+    def run_batches(self, read_groups: Sequence[tuple], batches, contigs=None) -> GpuPileupSession:
+        """AlignmentsPileupGenerator.processFiles over already merged batches, then the VCF."""
+        s = self.session(read_groups)
+        if contigs is not None:
+            for name, seq in contigs:
+                s.set_reference(name, seq)
+        elif self.genomeFile is not None:
+            s.load_fasta(self.genomeFile)
+        else:
+            raise NgsepError(_lib.NGSEP_E_IO, "The reference genome file is a required parameter")
+        for b in batches:
+            s.processAlignments(b)
+        s.notifyEndOfAlignments()
+        s.write_population_vcf(self.outFilename)
+        return s

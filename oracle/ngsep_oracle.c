@@ -452,6 +452,29 @@ static void print_header(FILE* out, const ngo_params* p) {
     fprintf(out, "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t%s\n", p->sample_id);
 }
 
+/* VCFFileHeader.print with the samples of MultisampleVariantsDetector (vcf/VCFFileHeader.java:219-245) */
+static void print_header_samples(FILE* out, const ngo_params* p, const char* const* ids, int n) {
+    ngo_params q = *p;
+    q.print_sample_ploidy = 0;
+    q.sample_id = "";
+    /* reuse the fixed lines; the sample part differs */
+    FILE* tmp = out;
+    static const char* tail = "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT";
+    char* buf = NULL; size_t len = 0;
+    FILE* mem = open_memstream(&buf, &len);
+    print_header(mem, &q);
+    fclose(mem);
+    char* cut = strstr(buf, "#CHROM");
+    if (cut) *cut = 0;
+    fputs(buf, tmp);
+    free(buf);
+    if (p->print_sample_ploidy)
+        for (int i = 0; i < n; i++) fprintf(tmp, "##SAMPLE=<ID=%s,PL=%d>\n", ids[i], p->ploidy);
+    fputs(tail, tmp);
+    for (int i = 0; i < n; i++) fprintf(tmp, "\t%s", ids[i]);
+    fputs("\n", tmp);
+}
+
 /* one VCF line per call: VCFFileWriter.printVCFRecord + printGenotypeInfo */
 static void print_call(FILE* out, const char* seqName, const ngo_call* c) {
     fprintf(out, "%s\t%d\t.\t%c\t", seqName, c->pos, c->ref);
@@ -592,8 +615,10 @@ static void alist_push(ngo_alist* l, ngo_aln* a) {
     l->a[l->n++] = a;
 }
 
+struct ngo_mvd;
 typedef struct {
     const ngo_params* p;
+    struct ngo_mvd* mvd;       /* MultisampleVariantsDetector listener instead of the single-sample one */
     double het_rate;
     ngo_genome* g;
     FILE* out;
@@ -613,12 +638,341 @@ static void on_sequence_end(ngo_gen* G) {
     G->calls.n = 0;
 }
 
+/* ------------------------------------------------------------------ */
+/* MultisampleVariantsDetector, SNV-only (discovery/MultisampleVariantsDetector.java:522-693) */
+/* ------------------------------------------------------------------ */
+/* Java String.hashCode */
+static int32_t java_string_hash(const char* s) {
+    uint32_t h = 0;
+    for (; *s; s++) h = 31u * h + (uint8_t)*s;
+    return (int32_t)h;
+}
+/* Iteration order of a java.util.HashSet<String> filled in the given order (Sample.readGroups,
+ * variants/Sample.java:36): buckets of the final table (16, doubled past 0.75 load), insertion
+ * order inside a bucket.  Used for PileupRecord.getAlleleCalls(span, readGroups) (:104-111). */
+static void java_hashset_order(char** ids, int* idx, int n) {
+    int cap = 16;
+    while (n > cap * 3 / 4) cap *= 2;
+    int* bucket = malloc(sizeof(int) * (n > 0 ? n : 1));
+    for (int i = 0; i < n; i++) {
+        uint32_t h = (uint32_t)java_string_hash(ids[idx[i]]);
+        bucket[i] = (int)((h ^ (h >> 16)) & (uint32_t)(cap - 1));
+    }
+    for (int i = 1; i < n; i++) {          /* stable insertion sort by bucket */
+        int b = bucket[i], v = idx[i], j = i - 1;
+        while (j >= 0 && bucket[j] > b) { bucket[j + 1] = bucket[j]; idx[j + 1] = idx[j]; j--; }
+        bucket[j + 1] = b; idx[j + 1] = v;
+    }
+    free(bucket);
+}
+
+/* One sample's call: CalledSNV (biallelic SNV) or CalledGenomicVariantImpl (multi-allelic SNV or
+ * the no-data undecided call), as far as the VCF line and DiversityStatistics read them. */
+typedef struct {
+    int kind;                 /* 0 CalledSNV, 1 CalledGenomicVariantImpl */
+    int n_called, called[2];  /* indexes into the variant alleles (CalledSNV: 0 ref, 1 alt) */
+    int gq, dp;
+    int counts[4];            /* getAllCounts: A,C,G,T */
+    int has_logs;             /* report log-conditionals present */
+    double logs[4][4];        /* over the variant alleles (CalledSNV: float values) */
+    int total_cn;             /* getCopyNumber */
+    int acn[4];               /* getAllelesCopyNumber over the variant alleles */
+} ngo_scall;
+
+/* GenomicVariant as the MVD path builds it: reference first, then alternatives in A,C,G,T order */
+typedef struct { int n; int idx[4]; int multisnv_type; } ngo_pvar;
+
+/* CalledSNV.updateAllelesCopyNumberFromCounts (variants/CalledSNV.java:134-158); genotype -1..2 */
+static void csnv_update_cn(int genotype, const int* counts, const ngo_pvar* v, int total, int* tot_out, int* ref_out) {
+    int ref = 0;
+    if (genotype == -1) { *tot_out = total; *ref_out = 0; return; }
+    if (genotype == 0) ref = total;
+    else if (genotype == 2) ref = 0;
+    else if (total <= 2) { total = 2; ref = 1; }
+    else {
+        double cr = counts[v->idx[0]], sum = cr + counts[v->idx[1]];
+        double prop = sum > 0 ? cr / sum : 0.5;
+        if (prop > 1) prop = 1;
+        ref = (int16_t)ngo_java_round(prop * total);
+        if (ref == 0) ref = 1;
+        else if (ref >= total) ref = total - 1;
+    }
+    *tot_out = total; *ref_out = ref;
+}
+
+/* CalledGenomicVariantImpl.updateAllelesCopyNumberFromCounts (variants/CalledGenomicVariantImpl.java:228-282) */
+static void cgv_update_cn(ngo_scall* c, int n_alleles, int total, const int* report_counts /* NULL: absent */) {
+    c->total_cn = total;
+    for (int i = 0; i < 4; i++) c->acn[i] = 0;
+    if (c->n_called == 0) return;
+    if (c->n_called == 1 && c->called[0] == 0) { c->acn[0] = total; return; }
+    int nc = c->n_called;
+    if (total <= nc) { for (int i = 0; i < nc; i++) c->acn[c->called[i]] = 1; return; }
+    if (!report_counts) {
+        int def = total / nc;
+        for (int i = 0; i < nc; i++) c->acn[c->called[i]] = def;
+        c->acn[c->called[0]] += total - def * nc;
+        return;
+    }
+    int rc[2], tr = 0;
+    for (int i = 0; i < nc; i++) { rc[i] = report_counts[c->called[i]]; if (rc[i] == 0) rc[i] = 1; tr += rc[i]; }
+    int tc = 0;
+    for (int i = 0; i < nc; i++) {
+        int64_t r = ngo_java_round((double)total * rc[i] / tr);
+        c->acn[c->called[i]] = (int)(r > 1 ? r : 1);
+        tc += c->acn[c->called[i]];
+    }
+    if (tc < total) c->acn[c->called[0]] += total - tc;
+    else {
+        int ex = tc - total;
+        for (int i = nc - 1; ex > 0 && i >= 0; i--) {
+            int j = c->called[i];
+            int rm = ex < c->acn[j] - 1 ? ex : c->acn[j] - 1;
+            c->acn[j] -= rm; ex -= rm;
+        }
+    }
+    (void)n_alleles;
+}
+
+/* SingleSampleVariantPileupListener.genotypeVariantSample (:361-391) with a fresh listener
+ * (minQuality = DEF_MIN_QUALITY 40) and VariantDiscoverySNVQAlgorithm.genotypeSNV (:21-97) */
+static void genotype_sample(const ngo_counts* h, const ngo_pvar* v, double het, int ploidy, ngo_scall* c) {
+    memset(c, 0, sizeof(*c));
+    memcpy(c->counts, h->counts, sizeof(c->counts));
+    if (h->total_count == 0) {
+        /* undecided CalledGenomicVariantImpl(variant, new byte[0]) with the counts, no report */
+        c->kind = 1;
+        cgv_update_cn(c, v->n, ploidy, NULL);
+        return;
+    }
+    double post[16];
+    ngo_counts_posteriors(h, het, post);
+    c->dp = h->total_count;
+    if (v->n == 2) {
+        int r = v->idx[0], a = v->idx[1];
+        double pHomoRef = post[r * 4 + r], pMax = pHomoRef;
+        int genotype = 0;
+        double pHomoAlt = post[a * 4 + a];
+        if (pHomoAlt > pMax + 0.01) { pMax = pHomoAlt; genotype = 2; }
+        double pHetero = post[r * 4 + a] + post[a * 4 + r];
+        if (pHetero > pMax + 0.01) { pMax = pHetero; genotype = 1; }
+        int gq = ngo_phred(1 - pMax);
+        if (gq == 0) genotype = -1;
+        c->kind = 0;
+        c->gq = gq;
+        float hr = (float)h->logc[r][r], ha = (float)h->logc[a][a], ra = (float)h->logc[r][a], ar = (float)h->logc[a][r];
+        c->has_logs = (hr + ra + ar + ha) != 0;      /* float sum, CalledSNV.java:422 */
+        c->logs[0][0] = hr; c->logs[0][1] = ra; c->logs[1][0] = ar; c->logs[1][1] = ha;
+        /* constructor: setGenotype with copy number 0, then updateAllelesCopyNumberFromCounts(ploidy) */
+        int tot = 0, ref = 0;
+        if (genotype != -1) csnv_update_cn(genotype, h->counts, v, 0, &tot, &ref);
+        csnv_update_cn(genotype, h->counts, v, ploidy, &tot, &ref);
+        if (40 > gq) { genotype = -1; c->gq = 0; ref = 0; }          /* makeUndecided, CalledSNV.java:279-285 */
+        c->total_cn = tot;
+        if (genotype == -1) c->n_called = 0;
+        else if (genotype == 0) { c->n_called = 1; c->called[0] = 0; }
+        else if (genotype == 2) { c->n_called = 1; c->called[0] = 1; }
+        else { c->n_called = 2; c->called[0] = 0; c->called[1] = 1; }
+        c->acn[0] = genotype == -1 ? 0 : ref;
+        c->acn[1] = genotype == -1 ? 0 : tot - ref;
+        return;
+    }
+    /* multi-allelic: report submatrices over the variant alleles (:59-96) */
+    int n = v->n;
+    int rcounts[4] = {0, 0, 0, 0};
+    double rpost[4][4] = {{0}};
+    for (int i = 0; i < n; i++) {
+        rcounts[i] = h->counts[v->idx[i]];
+        for (int j = 0; j < n; j++) { c->logs[i][j] = h->logc[v->idx[i]][v->idx[j]]; rpost[i][j] = post[v->idx[i] * 4 + v->idx[j]]; }
+    }
+    c->has_logs = 1;
+    int bi = 0, bj = 0;                                   /* getIndexesMaxGenotype(report, 0), :223-243 */
+    double probMax = rpost[0][0];
+    for (int i = 0; i < n; i++)
+        for (int j = i; j < n; j++) {
+            double gp = rpost[i][j];
+            if (i != j) gp += rpost[j][i];
+            if (gp > probMax + 0.01) { probMax = gp; bi = i; bj = j; }
+        }
+    double maxP = rpost[bi][bj];
+    if (bi != bj) { maxP += rpost[bj][bi]; c->n_called = 2; c->called[0] = bi; c->called[1] = bj; }
+    else { c->n_called = 1; c->called[0] = bi; }
+    c->gq = ngo_phred(1 - maxP);
+    c->kind = 1;
+    cgv_update_cn(c, n, ploidy, rcounts);                 /* genotypeVariantSample: updateAllelesCopyNumberFromCounts(ploidy) */
+    if (40 > c->gq) { c->n_called = 0; c->gq = 0; cgv_update_cn(c, n, c->total_cn, rcounts); }   /* makeUndecided, :320-325 */
+}
+
+typedef struct ngo_mvd {
+    int n_samples;
+    char** ids;                   /* sorted sample ids (TreeMap order, MultisampleVariantsDetector.java:499-523) */
+    int* rg_sample;               /* read group -> sample (-1: none) */
+    int* rg_rank;                 /* rank of the read group in its sample's HashSet order */
+    int* n_rank;                  /* read groups per sample */
+    double min_adf;
+    int ploidy;
+    ngo_counts* h;                /* per-sample helpers */
+    ngo_scall* calls;
+} ngo_mvd;
+
+/* DecimalFormat("##0.0#") (main/io/ParseUtils.java:29), HALF_EVEN on the exact binary value */
+static void java_fmt2(FILE* out, double x) {
+    double p = x * 100.0, err = fma(x, 100.0, -p);
+    double k = floor(p), fr = p - k;
+    long long n = (long long)k;
+    if (fr > 0.5 || (fr == 0.5 && (err > 0 || (err == 0 && (n & 1))))) n++;
+    if (n % 10 == 0) fprintf(out, "%lld.%lld", n / 100, (n % 100) / 10);
+    else fprintf(out, "%lld.%02lld", n / 100, n % 100);
+}
+
+static void mvd_genotype_all(ngo_mvd* M, const ngo_pvar* v, double het, int* qs) {
+    int q = 0;
+    for (int s = 0; s < M->n_samples; s++) {
+        genotype_sample(&M->h[s], v, het, M->ploidy, &M->calls[s]);
+        const ngo_scall* c = &M->calls[s];
+        int homref = c->n_called == 1 && c->called[0] == 0;
+        if (c->n_called > 0 && !homref && c->gq > q) q = c->gq;   /* MultisampleVariantsDetector.java:683-685 */
+    }
+    *qs = q;
+}
+
+static void mvd_print(FILE* out, const char* seqName, int pos, const ngo_pvar* v, int qs, const ngo_mvd* M) {
+    fprintf(out, "%s\t%d\t.\t%c\t", seqName, pos, BASES[v->idx[0]]);
+    for (int i = 1; i < v->n; i++) fprintf(out, "%s%c", i > 1 ? "," : "", BASES[v->idx[i]]);
+    fprintf(out, "\t%d\t.\t", qs);
+    /* VCFRecord.updateDiversityStatistics (vcf/VCFRecord.java:288-301) with
+     * DiversityStatistics.calculateDiversityStatistics(calls, false) (variants/DiversityStatistics.java:123-218) */
+    int counts[4] = {0, 0, 0, 0}, sum = 0, ng = 0, nhet = 0;
+    for (int s = 0; s < M->n_samples; s++) {
+        const ngo_scall* c = &M->calls[s];
+        if (c->n_called == 0) continue;
+        ng++;
+        if (c->n_called > 1) nhet++;
+        for (int i = 0; i < c->n_called; i++) { int j = c->called[i]; counts[j] += c->acn[j]; sum += c->acn[j]; }
+    }
+    int ncalled = 0, minAC = 0;
+    for (int i = 0; i < v->n; i++)
+        if (counts[i] > 0) { ncalled++; if (minAC == 0 || minAC > counts[i]) minAC = counts[i]; }
+    fprintf(out, "NS=%d;AN=%d;AFS=", ng, ncalled);
+    for (int i = 0; i < v->n; i++) fprintf(out, "%s%d", i ? "," : "", counts[i]);
+    fprintf(out, ";OH=");
+    java_fmt2(out, ng > 0 ? (double)nhet / ng : 0.0);
+    if (v->n == 2) { fprintf(out, ";MAF="); java_fmt2(out, ncalled < 2 ? 0.0 : (double)minAC / sum); }
+    if (v->multisnv_type) fprintf(out, ";TYPE=MULTISNV");   /* VCFFileWriter.java:47-49 */
+    fprintf(out, "\tGT:PL:GQ:DP:BSDP:ACN");
+    for (int s = 0; s < M->n_samples; s++) {
+        const ngo_scall* c = &M->calls[s];
+        fprintf(out, "\t");
+        /* VCFFileWriter.printGenotypeInfo (:159-308) */
+        if (c->n_called == 0) fprintf(out, M->ploidy > 1 ? "./." : ".");
+        else if (c->n_called == 1) { fprintf(out, "%d", c->called[0]); if (M->ploidy > 1) fprintf(out, "/%d", c->called[0]); }
+        else fprintf(out, "%d/%d", c->called[0], c->called[1]);
+        fprintf(out, ":");
+        for (int j = 0; j < v->n; j++)
+            for (int i = 0; i <= j; i++) {
+                if (i > 0 || j > 0) fprintf(out, ",");
+                fprintf(out, "%d", c->has_logs ? (int)ngo_java_round(-10 * c->logs[i][j]) : 0);
+            }
+        fprintf(out, ":%d:%d:%d,%d,%d,%d:", c->gq, c->dp, c->counts[0], c->counts[1], c->counts[2], c->counts[3]);
+        if (c->total_cn == 0) fprintf(out, ".");
+        else {
+            int nal = c->kind == 0 ? 2 : v->n;
+            for (int j = 0; j < nal; j++) {
+                int val = c->acn[j];
+                if (c->n_called == 0 && j == 0) val = c->total_cn;
+                fprintf(out, "%s%d", j ? "," : "", val);
+            }
+        }
+    }
+    fprintf(out, "\n");
+}
+
+/* MultisampleVariantsDetector.onPileup (:522-558) for a pileup without STRs / known variants */
+static void mvd_on_pileup(ngo_gen* G, int pos) {
+    ngo_mvd* M = G->mvd;
+    const ngo_params* p = G->p;
+    const ngo_seq* sq = &G->g->s[G->cur_seq];
+    if (pos < 1 || pos > sq->len) return;
+    char r = sq->seq[pos - 1];
+    /* calculateReferenceAlleleDiscovery (SingleSampleVariantPileupListener.java:191-206) */
+    if (p->ignore_lowercase_ref && islower((unsigned char)r)) return;
+    char R = (char)toupper((unsigned char)r);
+    /* discoverPopulationSNV (:585-597): pooled calls of every alignment, then per sample in the
+     * order of its read groups (PileupRecord.getAlleleCalls, :104-152) */
+    ngo_counts pooled;
+    ngo_counts_init(&pooled, 4, 0.5, p->max_base_qs);
+    for (int s = 0; s < M->n_samples; s++) ngo_counts_init(&M->h[s], 4, 0.5, p->max_base_qs);
+    int maxrank = 0;
+    for (int s = 0; s < M->n_samples; s++) if (M->n_rank[s] > maxrank) maxrank = M->n_rank[s];
+    for (int rank = -1; rank < maxrank; rank++) {
+        for (int k = 0; k < G->pending.n; k++) {
+            ngo_aln* a = G->pending.a[k];
+            if (a->first > pos || a->last < pos) continue;
+            int sm = a->rg >= 0 ? M->rg_sample[a->rg] : -1;
+            if (rank >= 0 && (sm < 0 || M->rg_rank[a->rg] != rank)) continue;
+            if (!a->chars) continue;
+            int rp = aligned_read_pos(a, pos);
+            if (rp < 0) continue;
+            int len = a->acl[rp];
+            if (len != 1) continue;
+            int qc = a->quals ? a->quals[rp] : '+';
+            int q = qc - 33; if (q > 30) q = 30;
+            ngo_counts* h = rank < 0 ? &pooled : &M->h[sm];
+            ngo_counts_update(h, base_idx(a->chars[rp]), (int8_t)q, (a->flags & FLAG_REVERSE) != 0);
+        }
+    }
+    /* SingleSampleVariantPileupListener.createSNVVariantPool (:297-332) */
+    if (pooled.total_count == 0) return;
+    int refIdx = base_idx(R);
+    if (refIdx < 0) return;
+    int sum = pooled.counts[0] + pooled.counts[1] + pooled.counts[2] + pooled.counts[3];
+    double minCount = M->min_adf * sum;
+    if (minCount < 1) minCount = 1;
+    ngo_pvar v = {0, {0}, 0};
+    v.idx[v.n++] = refIdx;
+    for (int i = 0; i < 4; i++)
+        if (pooled.counts[i] >= minCount && i != refIdx) v.idx[v.n++] = i;
+    if (v.n < 2) return;
+    v.multisnv_type = v.n > 2;
+    int qs = 0;
+    while (v.n > 2) {
+        mvd_genotype_all(M, &v, G->het_rate, &qs);
+        /* makeNewVariant (MultisampleVariantsDetector.java:642-656, SingleSampleVariantPileupListener.java:346-359) */
+        int called[4] = {0, 0, 0, 0};
+        called[v.idx[0]] = 1;
+        for (int s = 0; s < M->n_samples; s++)
+            for (int i = 0; i < M->calls[s].n_called; i++) called[v.idx[M->calls[s].called[i]]] = 1;
+        int nset = called[0] + called[1] + called[2] + called[3];
+        if (nset == v.n) break;
+        ngo_pvar nv = {0, {0}, 0};
+        nv.idx[nv.n++] = v.idx[0];
+        for (int i = 0; i < 4; i++) if (called[i] && i != v.idx[0]) nv.idx[nv.n++] = i;
+        v = nv;   /* SNV (BIALLELIC type) or GenomicVariantImpl (UNDETERMINED type): no TYPE annotation */
+    }
+    if (v.n < 2) return;   /* only the reference allele is left: not an SNV, no decided non-reference call */
+    mvd_genotype_all(M, &v, G->het_rate, &qs);
+    if (qs == 0 || qs < p->min_quality) return;           /* MultisampleVariantsDetector.java:534 */
+    mvd_print(G->out, sq->name, pos, &v, qs, M);
+    G->st->variants_called++;
+}
+
 /* processCurrentPosition + listeners for one position, AlignmentsPileupGenerator.java:475-498 */
 static int process_current_position(ngo_gen* G) {
     if (G->pending.n == 0) { G->cur_pos++; return 0; }
     const ngo_params* p = G->p;
     if (p->query_seq && (G->cur_pos < p->query_first || G->cur_pos > p->query_last)) { G->cur_pos++; return 0; }
     int pos = G->cur_pos;
+    if (G->mvd) {
+        int numAlignments = 0;
+        for (int k = 0; k < G->pending.n; k++)
+            if (G->pending.a[k]->first <= pos && G->pending.a[k]->last >= pos) numAlignments++;
+        if (numAlignments > 0) {
+            G->st->positions_genotyped++;
+            mvd_on_pileup(G, pos);
+        }
+        G->cur_pos++;
+        return numAlignments > 0;
+    }
     int numAlignments = 0;
     ngo_counts h;
     ngo_counts_init(&h, 4, 0.5, p->max_base_qs);     /* CountsHelper.calculateCountsSNV(calls, maxBaseQS, 0.5) */
@@ -753,8 +1107,8 @@ static char* split_tab(char** s) {
     return b;
 }
 
-int ngo_run_ssvd(const char* fasta, const char* sam, const char* out_vcf,
-                 const char* dump_path, const ngo_params* p, ngo_stats* stats) {
+static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
+                        const char* dump_path, const ngo_params* p, ngo_stats* stats, double min_adf, int multisample) {
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     ngo_stats st_local; ngo_stats* st = stats ? stats : &st_local;
@@ -770,10 +1124,13 @@ int ngo_run_ssvd(const char* fasta, const char* sam, const char* out_vcf,
 
     ngo_gen G; memset(&G, 0, sizeof(G));
     G.p = p; G.g = &g; G.out = out; G.dump = dump; G.cur_seq = -1; G.st = st;
-    /* SingleSampleVariantsDetector.run, :591-593 */
+    /* SingleSampleVariantsDetector.run, :591-593 (MultisampleVariantsDetector keeps -h as given) */
     G.het_rate = p->het_rate;
-    if (!p->het_rate_set && p->ploidy == 1) G.het_rate = 1e-6;
-    print_header(out, p);
+    if (!multisample && !p->het_rate_set && p->ploidy == 1) G.het_rate = 1e-6;
+    if (!multisample) print_header(out, p);
+    ngo_mvd M; memset(&M, 0, sizeof(M));
+    ngo_strlist rg_sm = {0};       /* SM of each @RG (parallel to rgs) */
+    int header_done = !multisample;
 
     int filterFlags = FLAG_UNMAPPED;          /* AlignmentsPileupGenerator.createReader, :367-372 */
     if (!p->process_secondary) {
@@ -791,9 +1148,57 @@ int ngo_run_ssvd(const char* fasta, const char* sam, const char* out_vcf,
         if (line[0] == '@') {
             if (strncmp(line, "@RG", 3) == 0) {
                 char* id = strstr(line, "\tID:");
-                if (id) { id += 4; char* e = strchr(id, '\t'); char save = 0; if (e) { save = *e; *e = 0; } strlist_get(&rgs, id, 1); if (e) *e = save; }
+                char* sm = strstr(line, "\tSM:");
+                char smv[256] = "";
+                if (sm) { sm += 4; size_t k = 0; while (sm[k] && sm[k] != '\t' && k < sizeof(smv) - 1) { smv[k] = sm[k]; k++; } smv[k] = 0; }
+                if (id) {
+                    id += 4; char* e = strchr(id, '\t'); char save = 0; if (e) { save = *e; *e = 0; }
+                    int before = rgs.n;
+                    int ri = strlist_get(&rgs, id, 1);
+                    if (rgs.n > before) {
+                        if (rg_sm.n == rg_sm.cap) { rg_sm.cap = rg_sm.cap ? 2 * rg_sm.cap : 8; rg_sm.ids = realloc(rg_sm.ids, sizeof(char*) * rg_sm.cap); }
+                        rg_sm.ids[rg_sm.n++] = strdup(sm ? smv : "");
+                    }
+                    (void)ri;
+                    if (e) *e = save;
+                }
             }
             continue;
+        }
+        if (!header_done) {
+            /* MultisampleVariantsDetector.loadSamplesFromAlignmentHeaders (:499-523): samples by id
+             * (TreeMap), each with its read groups (HashSet, Sample.java:36) */
+            header_done = 1;
+            ngo_strlist smids = {0};
+            for (int i = 0; i < rg_sm.n; i++) if (rg_sm.ids[i][0]) strlist_get(&smids, rg_sm.ids[i], 1);
+            M.n_samples = smids.n;
+            M.ids = malloc(sizeof(char*) * (smids.n ? smids.n : 1));
+            for (int i = 0; i < smids.n; i++) M.ids[i] = smids.ids[i];
+            for (int i = 1; i < M.n_samples; i++) {
+                char* v = M.ids[i]; int j = i - 1;
+                while (j >= 0 && strcmp(M.ids[j], v) > 0) { M.ids[j + 1] = M.ids[j]; j--; }
+                M.ids[j + 1] = v;
+            }
+            free(smids.ids);
+            M.rg_sample = malloc(sizeof(int) * (rgs.n ? rgs.n : 1));
+            M.rg_rank = malloc(sizeof(int) * (rgs.n ? rgs.n : 1));
+            M.n_rank = calloc(M.n_samples ? M.n_samples : 1, sizeof(int));
+            int* tmp = malloc(sizeof(int) * (rgs.n ? rgs.n : 1));
+            for (int i = 0; i < rgs.n; i++) { M.rg_sample[i] = -1; M.rg_rank[i] = 0; }
+            for (int s2 = 0; s2 < M.n_samples; s2++) {
+                int n = 0;
+                for (int i = 0; i < rgs.n; i++) if (rg_sm.ids[i][0] && strcmp(rg_sm.ids[i], M.ids[s2]) == 0) tmp[n++] = i;
+                java_hashset_order(rgs.ids, tmp, n);
+                for (int k = 0; k < n; k++) { M.rg_sample[tmp[k]] = s2; M.rg_rank[tmp[k]] = k; }
+                M.n_rank[s2] = n;
+            }
+            free(tmp);
+            M.min_adf = min_adf;
+            M.ploidy = p->ploidy;
+            M.h = calloc(M.n_samples ? M.n_samples : 1, sizeof(ngo_counts));
+            M.calls = calloc(M.n_samples ? M.n_samples : 1, sizeof(ngo_scall));
+            G.mvd = &M;
+            print_header_samples(out, p, (const char* const*)M.ids, M.n_samples);
         }
         char* cur = line;
         char* f[11];
@@ -868,6 +1273,7 @@ int ngo_run_ssvd(const char* fasta, const char* sam, const char* out_vcf,
         if (a->has_indel) { G.unsupported = 1; aln_free(a); rc = NGO_UNSUPPORTED; break; }
         process_alignment(&G, a);
     }
+    if (multisample && !header_done) { header_done = 1; print_header_samples(out, p, NULL, 0); }
     if (rc == NGO_OK) notify_end(&G);
     free(line); free(last_qname); fclose(in);
     if (out != stdout) fclose(out); else fflush(out);
@@ -880,7 +1286,26 @@ int ngo_run_ssvd(const char* fasta, const char* sam, const char* out_vcf,
     free(g.s);
     for (int i = 0; i < rgs.n; i++) free(rgs.ids[i]);
     free(rgs.ids);
+    for (int i = 0; i < rg_sm.n; i++) free(rg_sm.ids[i]);
+    free(rg_sm.ids);
+    if (multisample) {
+        for (int i = 0; i < M.n_samples; i++) free(M.ids[i]);
+        free(M.ids); free(M.rg_sample); free(M.rg_rank); free(M.n_rank); free(M.h); free(M.calls);
+    }
     clock_gettime(CLOCK_MONOTONIC, &t1);
     st->seconds = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
     return rc;
+}
+
+int ngo_run_ssvd(const char* fasta, const char* sam, const char* out_vcf,
+                 const char* dump_path, const ngo_params* p, ngo_stats* stats) {
+    return run_detector(fasta, sam, out_vcf, dump_path, p, stats, 0.0, 0);
+}
+
+/* MultisampleVariantsDetector.run (discovery/MultisampleVariantsDetector.java:421-459) on one SAM
+ * holding every sample's read groups (the generator's merge of per-sample files). */
+int ngo_run_mvd(const char* fasta, const char* sam, const char* out_vcf, const ngo_params* p,
+                double min_allele_depth_freq, ngo_stats* stats) {
+    if (p->ploidy >= 3) return NGO_UNSUPPORTED;
+    return run_detector(fasta, sam, out_vcf, NULL, p, stats, min_allele_depth_freq, 1);
 }

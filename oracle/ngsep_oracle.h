@@ -94,6 +94,12 @@ typedef struct ngo_stats {
 int ngo_run_ssvd(const char* fasta, const char* sam, const char* out_vcf,
                  const char* dump_path, const ngo_params* p, ngo_stats* stats);
 
+/* MultisampleVariantsDetector (discovery/MultisampleVariantsDetector.java:421-693), SNV-only inputs,
+ * samples from the @RG SM tags of one SAM file (the generator's merge of per-sample files).
+ * p->min_quality is -minQuality; per-sample calls use the fresh listener's DEF_MIN_QUALITY 40. */
+int ngo_run_mvd(const char* fasta, const char* sam, const char* out_vcf, const ngo_params* p,
+                double min_allele_depth_freq, ngo_stats* stats);
+
 #ifdef __cplusplus
 }
 #endif

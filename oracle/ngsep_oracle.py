@@ -63,6 +63,8 @@ def lib():
         l.ngo_table_gt.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         l.ngo_run_ssvd.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                    ctypes.POINTER(OracleParams), ctypes.POINTER(OracleStats)]
+        l.ngo_run_mvd.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(OracleParams),
+                                  ctypes.c_double, ctypes.POINTER(OracleStats)]
         _lib = l
     return _lib
 
@@ -84,6 +86,16 @@ def run_ssvd(fasta: str, sam: str, out_vcf: str, dump: str | None = None, **kw) 
     st = OracleStats()
     rc = lib().ngo_run_ssvd(fasta.encode(), sam.encode(), out_vcf.encode(), dump.encode() if dump else None,
                             ctypes.byref(p), ctypes.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"oracle failed rc={rc}")
+    return st
+
+
+def run_mvd(fasta: str, sam: str, out_vcf: str, min_adf: float = 0.0, **kw) -> OracleStats:
+    """MultisampleVariantsDetector restatement (discovery/MultisampleVariantsDetector.java:421-693)."""
+    p = params(**kw)
+    st = OracleStats()
+    rc = lib().ngo_run_mvd(fasta.encode(), sam.encode(), out_vcf.encode(), ctypes.byref(p), min_adf, ctypes.byref(st))
     if rc != 0:
         raise RuntimeError(f"oracle failed rc={rc}")
     return st

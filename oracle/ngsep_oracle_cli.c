@@ -12,8 +12,10 @@
 int main(int argc, char** argv) {
     ngo_params p; ngo_params_default(&p);
     const char *ref = NULL, *in = NULL, *outp = NULL, *dump = NULL;
-    int i = 1;
+    int i = 1, mvd = 0;
+    double min_adf = 0;
     if (i < argc && strcmp(argv[i], "SingleSampleVariantsDetector") == 0) i++;
+    else if (i < argc && strcmp(argv[i], "MultisampleVariantsDetector") == 0) { i++; mvd = 1; }
     for (; i < argc; i++) {
         const char* a = argv[i];
         const char* v = (i + 1 < argc) ? argv[i + 1] : NULL;
@@ -22,6 +24,8 @@ int main(int argc, char** argv) {
         else if (OPT("-i")) in = v;
         else if (OPT("-o")) outp = v;
         else if (OPT("-dump")) dump = v;
+        else if (OPT("-minAlleleDepthFrequency")) min_adf = atof(v);
+        else if (mvd && a[0] != '-' && !in) in = a;    /* MultisampleVariantsDetector: positional alignments file */
         else if (OPT("-sampleId")) p.sample_id = v;
         else if (OPT("-ploidy")) p.ploidy = atoi(v);
         else if (OPT("-minMQ")) p.min_mq = atoi(v);
@@ -47,7 +51,8 @@ int main(int argc, char** argv) {
     char* vcf = malloc(strlen(outp) + 8);
     sprintf(vcf, "%s.vcf", outp);
     ngo_stats st;
-    int rc = ngo_run_ssvd(ref, in, strcmp(outp, "-") == 0 ? "-" : vcf, dump, &p, &st);
+    int rc = mvd ? ngo_run_mvd(ref, in, outp, &p, min_adf, &st)     /* MVD: -o is the VCF path (MultisampleVariantsDetector.java:64) */
+                 : ngo_run_ssvd(ref, in, strcmp(outp, "-") == 0 ? "-" : vcf, dump, &p, &st);
     fprintf(stderr, "oracle rc=%d alignments=%lld admitted=%lld positions=%lld variants=%lld seconds=%.3f\n", rc,
             (long long)st.alignments_read, (long long)st.alignments_admitted, (long long)st.positions_genotyped,
             (long long)st.variants_called, st.seconds);

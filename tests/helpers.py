@@ -81,3 +81,8 @@ def read_dump(path):
         f = l.rstrip("\n").split("\t")
         rows[(f[0], int(f[1]))] = (int(f[3]), tuple(int(x) for x in f[4].split(",")), tuple(float(x) for x in f[5:15]))
     return rows
+
+
+def oracle_params_from(opts):
+    """GPU option names -> oracle parameter names (same meaning)."""
+    return {OPTION_MAP[k]: v for k, v in opts.items()}

@@ -53,6 +53,7 @@ const char kBases[] = "ACGT";
 
 struct Read {
     int32_t contig, pos, flags, mapq;
+    int32_t sample = 0;             // index into the sample list (RG/SM S%03d of sample_idx + sample)
     std::string name, cigar_s;      // SAM CIGAR text
     std::vector<int32_t> cigar;     // NGSEP codes
     std::string seq, qual;          // qual empty -> '*'
@@ -98,10 +99,18 @@ static int sample_quality(Rng& r, int model) {
     return 37;
 }
 
+static void make_population(ngs_synth* s);
+static void make_batch(ngs_synth* s);
+
 extern "C" ngs_synth* ngs_synth_create(const ngs_synth_params* pp) {
     ngs_synth* s = new ngs_synth();
     s->p = *pp;
     const ngs_synth_params& p = s->p;
+    if (p.n_samples > 1) {
+        make_population(s);
+        make_batch(s);
+        return s;
+    }
     std::vector<ContigDef> defs;
     double pa = 0.31;  // P(A)=P(T)
     if (p.genome == NGS_GENOME_YEAST) defs.assign(std::begin(kYeast), std::end(kYeast));
@@ -217,6 +226,122 @@ extern "C" ngs_synth* ngs_synth_create(const ngs_synth_params* pp) {
         std::stable_sort(s->reads.begin() + (ptrdiff_t)cstart, s->reads.end(),
                          [](const Read& a, const Read& b) { return a.pos < b.pos; });
     }
+    make_batch(s);
+    return s;
+}
+
+// Population of n_samples diploid individuals (the multisample configuration):
+// population SNVs at snv_rate with allele frequency U(0.02, 0.98), genotypes in Hardy-Weinberg
+// proportions, depth/read model per sample as for one individual.  Records of all samples are
+// merged in (position, sample) order -- AlignmentsPileupGenerator's multi-file merge
+// (discovery/AlignmentsPileupGenerator.java:268-289: ties go to the lowest file index) of one
+// BAM per sample with equal read lengths.
+static void make_population(ngs_synth* s) {
+    const ngs_synth_params& p = s->p;
+    std::vector<ContigDef> defs;
+    double pa = 0.31;
+    if (p.genome == NGS_GENOME_YEAST) defs.assign(std::begin(kYeast), std::end(kYeast));
+    else if (p.genome == NGS_GENOME_HUMAN) { defs.assign(std::begin(kHuman), std::end(kHuman)); pa = 0.295; }
+    else defs.push_back({"chrS", p.custom_len});
+    int first = std::max(0, p.contig_first);
+    int n = p.n_contigs > 0 ? std::min<int>(p.n_contigs, (int)defs.size() - first) : (int)defs.size() - first;
+    const int ns = p.n_samples;
+    for (int c = 0; c < n; c++) {
+        const ContigDef& d = defs[first + c];
+        Rng r(0x4E475345ull + (uint64_t)(first + c) + (p.seed << 32));
+        std::string seq(d.len, 'A');
+        for (int64_t i = 0; i < d.len; i++) {
+            double u = r.uniform();
+            char b = u < pa ? 'A' : u < 0.5 ? 'C' : u < 1.0 - pa ? 'G' : 'T';
+            if (p.lower_frac > 0 && r.uniform() < p.lower_frac) b = (char)(b - 'A' + 'a');
+            seq[i] = b;
+        }
+        s->names.push_back(d.name);
+        s->seqs.push_back(std::move(seq));
+    }
+    Rng r(p.seed * 0x9E3779B97F4A7C15ull + 31);
+    int64_t readno = 0;
+    for (size_t c = 0; c < s->seqs.size(); c++) {
+        const std::string& ref = s->seqs[c];
+        const int64_t L = (int64_t)ref.size();
+        // population variants: position, alt base, per-sample allele bits (bit0 hap0, bit1 hap1)
+        std::vector<int32_t> vpos;
+        std::vector<char> valt;
+        std::vector<uint8_t> vgt;    // vpos.size() x ns
+        for (int64_t i = 0; i < L; i++) {
+            if (r.uniform() >= p.snv_rate) continue;
+            char rb = (char)std::toupper(ref[i]);
+            const char* pr = std::strchr(kBases, rb);
+            if (!pr) continue;
+            int ai = ((int)(pr - kBases) + 1 + (int)r.below(3)) % 4;
+            double af = 0.02 + 0.96 * r.uniform();
+            vpos.push_back((int32_t)(i + 1));
+            valt.push_back(kBases[ai]);
+            int carriers = 0;
+            for (int k = 0; k < ns; k++) {
+                uint8_t g = (uint8_t)((r.uniform() < af ? 1 : 0) | (r.uniform() < af ? 2 : 0));
+                vgt.push_back(g);
+                carriers += g != 0;
+            }
+            if (carriers) s->truth.push_back({(int32_t)c, (int32_t)(i + 1), rb, kBases[ai], 1});
+        }
+        const int rl = p.read_len;
+        if (L < rl) continue;
+        const int64_t nper = (int64_t)std::llround(p.depth * (double)L / rl);
+        struct Gen { int32_t pos; int32_t sample; int64_t order; };
+        std::vector<Gen> starts;
+        starts.reserve((size_t)(nper * ns));
+        for (int k = 0; k < ns; k++)
+            for (int64_t j = 0; j < nper; j++) starts.push_back({(int32_t)(1 + r.below((uint64_t)(L - rl + 1))), k, j});
+        std::sort(starts.begin(), starts.end(), [](const Gen& a, const Gen& b) {
+            if (a.pos != b.pos) return a.pos < b.pos;
+            if (a.sample != b.sample) return a.sample < b.sample;
+            return a.order < b.order;
+        });
+        for (const Gen& g : starts) {
+            Read rd;
+            rd.contig = (int32_t)c;
+            rd.pos = g.pos;
+            rd.sample = g.sample;
+            const int hap = (int)r.below(2);
+            rd.flags = r.below(2) ? 16 : 0;
+            rd.mapq = 60;
+            char nm[32];
+            std::snprintf(nm, sizeof nm, "r%09lld", (long long)readno++);
+            rd.name = nm;
+            rd.seq.resize(rl);
+            rd.qual.resize(rl);
+            size_t vi = (size_t)(std::lower_bound(vpos.begin(), vpos.end(), g.pos) - vpos.begin());
+            for (int i = 0; i < rl; i++) {
+                const int32_t pos = g.pos + i;
+                char b = (char)std::toupper(ref[pos - 1]);
+                while (vi < vpos.size() && vpos[vi] < pos) vi++;
+                if (vi < vpos.size() && vpos[vi] == pos && ((vgt[vi * ns + g.sample] >> hap) & 1)) b = valt[vi];
+                int q = sample_quality(r, p.quality_model);
+                double e = std::pow(10.0, -q / 10.0);
+                if (r.uniform() < e) {
+                    const char* pb = std::strchr(kBases, b);
+                    int bi = pb ? (int)(pb - kBases) : 0;
+                    b = kBases[(bi + 1 + (int)r.below(3)) % 4];
+                }
+                if (p.n_frac > 0 && r.uniform() < p.n_frac) { b = 'N'; q = 2; }
+                rd.seq[i] = b;
+                rd.qual[i] = (char)(33 + q);
+            }
+            rd.cigar_s = std::to_string(rl) + "M";
+            rd.cigar = {rl * 8 + 3};
+            const bool dup = p.dup_rate > 0 && r.uniform() < p.dup_rate;
+            s->reads.push_back(rd);
+            if (dup) {
+                Read d = rd;
+                d.name += "d";
+                s->reads.push_back(d);
+            }
+        }
+    }
+}
+
+static void make_batch(ngs_synth* s) {
     // batch view: reader filters with default options (drop secondary and MAPQ<20 without NH)
     for (const Read& rd : s->reads) {
         if (rd.flags & 0x100) continue;
@@ -224,7 +349,7 @@ extern "C" ngs_synth* ngs_synth_create(const ngs_synth_params* pp) {
         s->b_seq.push_back(rd.contig);
         s->b_first.push_back(rd.pos);
         s->b_flags.push_back(rd.flags);
-        s->b_rg.push_back(0);
+        s->b_rg.push_back(rd.sample);
         s->b_cig_off.push_back((int64_t)s->b_cigar.size());
         s->b_cig_n.push_back((int32_t)rd.cigar.size());
         for (int32_t v : rd.cigar) s->b_cigar.push_back(v);
@@ -234,7 +359,6 @@ extern "C" ngs_synth* ngs_synth_create(const ngs_synth_params* pp) {
         if (rd.qual.empty()) { s->b_quals += std::string(rd.seq.size(), '!'); s->b_hasq.push_back(0); }
         else { s->b_quals += rd.qual; s->b_hasq.push_back(1); }
     }
-    return s;
 }
 
 extern "C" void ngs_synth_free(ngs_synth* s) { delete s; }
@@ -280,9 +404,12 @@ extern "C" int ngs_synth_write_fasta(const ngs_synth* s, const char* path) {
 static std::string header_text(const ngs_synth* s) {
     std::string h = "@HD\tVN:1.6\tSO:coordinate\n";
     for (size_t c = 0; c < s->seqs.size(); c++) h += "@SQ\tSN:" + s->names[c] + "\tLN:" + std::to_string(s->seqs[c].size()) + "\n";
-    char rg[64];
-    std::snprintf(rg, sizeof rg, "@RG\tID:S%03d\tSM:S%03d\n", s->p.sample_idx, s->p.sample_idx);
-    h += rg;
+    const int ns = s->p.n_samples > 1 ? s->p.n_samples : 1;
+    for (int k = 0; k < ns; k++) {
+        char rg[64];
+        std::snprintf(rg, sizeof rg, "@RG\tID:S%03d\tSM:S%03d\n", s->p.sample_idx + k, s->p.sample_idx + k);
+        h += rg;
+    }
     return h;
 }
 
@@ -294,7 +421,7 @@ extern "C" int ngs_synth_write_sam(const ngs_synth* s, const char* path) {
     for (const Read& rd : s->reads) {
         std::fprintf(f, "%s\t%d\t%s\t%d\t%d\t%s\t*\t0\t0\t%s\t%s\tRG:Z:S%03d\n", rd.name.c_str(), rd.flags,
                      s->names[rd.contig].c_str(), rd.pos, rd.mapq, rd.cigar_s.c_str(), rd.seq.c_str(),
-                     rd.qual.empty() ? "*" : rd.qual.c_str(), s->p.sample_idx);
+                     rd.qual.empty() ? "*" : rd.qual.c_str(), s->p.sample_idx + rd.sample);
     }
     std::fclose(f);
     return 0;
@@ -365,9 +492,9 @@ extern "C" int ngs_synth_write_bam(const ngs_synth* s, const char* path) {
     z.write(b.data(), b.size());
     static const int bam_op[8] = {5, 2, 1, 0, 6, 3, 4, 8};  // NGSEP op -> BAM op (H D I M P N S X)
     const char* nt16 = "=ACMGRSVTWYHKDBN";
-    char rg[16];
-    std::snprintf(rg, sizeof rg, "S%03d", s->p.sample_idx);
     for (const Read& rd : s->reads) {
+        char rg[16];
+        std::snprintf(rg, sizeof rg, "S%03d", s->p.sample_idx + rd.sample);
         std::string r;
         int l_seq = (int)rd.seq.size();
         int reflen = 0;

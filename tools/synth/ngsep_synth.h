@@ -34,6 +34,8 @@ typedef struct ngs_synth_params {
     double  lowmq_rate;      /* fraction of reads with MAPQ 5 */
     double  noqual_rate;     /* fraction of reads whose QUAL is '*' */
     double  softclip_rate;   /* fraction of reads with a 5-20 bp soft clip at one end */
+    int32_t n_samples;       /* >1: a population of diploid samples S%03d (sample_idx..), depth per sample,
+                                population SNVs at snv_rate with AF U(0.02,0.98) in HWE (multisample config C5) */
 } ngs_synth_params;
 
 typedef struct ngs_synth ngs_synth;
