@@ -816,13 +816,39 @@ typedef struct ngo_mvd {
 } ngo_mvd;
 
 /* DecimalFormat("##0.0#") (main/io/ParseUtils.java:29), HALF_EVEN on the exact binary value */
-static void java_fmt2(FILE* out, double x) {
+int ngo_java_fmt2(double x, char* buf, int cap) {
     double p = x * 100.0, err = fma(x, 100.0, -p);
     double k = floor(p), fr = p - k;
     long long n = (long long)k;
     if (fr > 0.5 || (fr == 0.5 && (err > 0 || (err == 0 && (n & 1))))) n++;
-    if (n % 10 == 0) fprintf(out, "%lld.%lld", n / 100, (n % 100) / 10);
-    else fprintf(out, "%lld.%02lld", n / 100, n % 100);
+    if (n % 10 == 0) return snprintf(buf, cap, "%lld.%lld", n / 100, (n % 100) / 10);
+    return snprintf(buf, cap, "%lld.%02lld", n / 100, n % 100);
+}
+
+/* VCFRecord.updateDiversityStatistics (vcf/VCFRecord.java:288-301) with
+ * DiversityStatistics.calculateDiversityStatistics(calls, false) (variants/DiversityStatistics.java:123-218):
+ * "NS=..;AN=..;AFS=..;OH=..[;MAF=..]" for calls given as (n_called, called[2], acn[4]) */
+int ngo_population_info(int n_calls, const int* n_called, const int* called, const int* acn, int n_alleles,
+                        char* buf, int cap) {
+    int counts[4] = {0, 0, 0, 0}, sum = 0, ng = 0, nhet = 0;
+    for (int s = 0; s < n_calls; s++) {
+        if (n_called[s] == 0) continue;
+        ng++;
+        if (n_called[s] > 1) nhet++;
+        for (int i = 0; i < n_called[s]; i++) { int j = called[2 * s + i]; counts[j] += acn[4 * s + j]; sum += acn[4 * s + j]; }
+    }
+    int ncalled = 0, minAC = 0;
+    for (int i = 0; i < n_alleles; i++)
+        if (counts[i] > 0) { ncalled++; if (minAC == 0 || minAC > counts[i]) minAC = counts[i]; }
+    int k = snprintf(buf, cap, "NS=%d;AN=%d;AFS=", ng, ncalled);
+    for (int i = 0; i < n_alleles; i++) k += snprintf(buf + k, cap - k, "%s%d", i ? "," : "", counts[i]);
+    k += snprintf(buf + k, cap - k, ";OH=");
+    k += ngo_java_fmt2(ng > 0 ? (double)nhet / ng : 0.0, buf + k, cap - k);
+    if (n_alleles == 2) {
+        k += snprintf(buf + k, cap - k, ";MAF=");
+        k += ngo_java_fmt2(ncalled < 2 ? 0.0 : (double)minAC / sum, buf + k, cap - k);
+    }
+    return k;
 }
 
 static void mvd_genotype_all(ngo_mvd* M, const ngo_pvar* v, double het, int* qs) {
@@ -840,24 +866,21 @@ static void mvd_print(FILE* out, const char* seqName, int pos, const ngo_pvar* v
     fprintf(out, "%s\t%d\t.\t%c\t", seqName, pos, BASES[v->idx[0]]);
     for (int i = 1; i < v->n; i++) fprintf(out, "%s%c", i > 1 ? "," : "", BASES[v->idx[i]]);
     fprintf(out, "\t%d\t.\t", qs);
-    /* VCFRecord.updateDiversityStatistics (vcf/VCFRecord.java:288-301) with
-     * DiversityStatistics.calculateDiversityStatistics(calls, false) (variants/DiversityStatistics.java:123-218) */
-    int counts[4] = {0, 0, 0, 0}, sum = 0, ng = 0, nhet = 0;
-    for (int s = 0; s < M->n_samples; s++) {
-        const ngo_scall* c = &M->calls[s];
-        if (c->n_called == 0) continue;
-        ng++;
-        if (c->n_called > 1) nhet++;
-        for (int i = 0; i < c->n_called; i++) { int j = c->called[i]; counts[j] += c->acn[j]; sum += c->acn[j]; }
+    {
+        int S = M->n_samples;
+        int* nc = malloc(sizeof(int) * (S ? S : 1));
+        int* cl = malloc(sizeof(int) * 2 * (S ? S : 1));
+        int* acn = malloc(sizeof(int) * 4 * (S ? S : 1));
+        for (int s = 0; s < S; s++) {
+            nc[s] = M->calls[s].n_called;
+            cl[2 * s] = M->calls[s].called[0]; cl[2 * s + 1] = M->calls[s].called[1];
+            for (int j = 0; j < 4; j++) acn[4 * s + j] = M->calls[s].acn[j];
+        }
+        char info[256];
+        ngo_population_info(S, nc, cl, acn, v->n, info, sizeof info);
+        fputs(info, out);
+        free(nc); free(cl); free(acn);
     }
-    int ncalled = 0, minAC = 0;
-    for (int i = 0; i < v->n; i++)
-        if (counts[i] > 0) { ncalled++; if (minAC == 0 || minAC > counts[i]) minAC = counts[i]; }
-    fprintf(out, "NS=%d;AN=%d;AFS=", ng, ncalled);
-    for (int i = 0; i < v->n; i++) fprintf(out, "%s%d", i ? "," : "", counts[i]);
-    fprintf(out, ";OH=");
-    java_fmt2(out, ng > 0 ? (double)nhet / ng : 0.0);
-    if (v->n == 2) { fprintf(out, ";MAF="); java_fmt2(out, ncalled < 2 ? 0.0 : (double)minAC / sum); }
     if (v->multisnv_type) fprintf(out, ";TYPE=MULTISNV");   /* VCFFileWriter.java:47-49 */
     fprintf(out, "\tGT:PL:GQ:DP:BSDP:ACN");
     for (int s = 0; s < M->n_samples; s++) {

@@ -100,6 +100,12 @@ int ngo_run_ssvd(const char* fasta, const char* sam, const char* out_vcf,
 int ngo_run_mvd(const char* fasta, const char* sam, const char* out_vcf, const ngo_params* p,
                 double min_allele_depth_freq, ngo_stats* stats);
 
+/* DecimalFormat("##0.0#") with HALF_EVEN (main/io/ParseUtils.java:29) */
+int ngo_java_fmt2(double x, char* buf, int cap);
+/* INFO of a population record: NS, AN, AFS, OH, MAF (biallelic) from the calls' (n_called, called[2], acn[4]) */
+int ngo_population_info(int n_calls, const int* n_called, const int* called, const int* acn, int n_alleles,
+                        char* buf, int cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -63,6 +63,9 @@ def lib():
         l.ngo_table_gt.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         l.ngo_run_ssvd.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                    ctypes.POINTER(OracleParams), ctypes.POINTER(OracleStats)]
+        l.ngo_java_fmt2.argtypes = [ctypes.c_double, ctypes.c_char_p, ctypes.c_int]
+        l.ngo_population_info.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                          ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         l.ngo_run_mvd.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(OracleParams),
                                   ctypes.c_double, ctypes.POINTER(OracleStats)]
         _lib = l
@@ -99,6 +102,23 @@ def run_mvd(fasta: str, sam: str, out_vcf: str, min_adf: float = 0.0, **kw) -> O
     if rc != 0:
         raise RuntimeError(f"oracle failed rc={rc}")
     return st
+
+
+def java_fmt2(x: float) -> str:
+    buf = ctypes.create_string_buffer(64)
+    lib().ngo_java_fmt2(x, buf, 64)
+    return buf.value.decode()
+
+
+def population_info(calls, n_alleles: int) -> str:
+    """calls: list of (n_called, [called0, called1], [acn0..acn3])."""
+    n = len(calls)
+    nc = (ctypes.c_int * max(n, 1))(*[c[0] for c in calls])
+    cl = (ctypes.c_int * max(2 * n, 1))(*[x for c in calls for x in (list(c[1]) + [0, 0])[:2]])
+    acn = (ctypes.c_int * max(4 * n, 1))(*[x for c in calls for x in (list(c[2]) + [0, 0, 0, 0])[:4]])
+    buf = ctypes.create_string_buffer(256)
+    lib().ngo_population_info(n, nc, cl, acn, n_alleles, buf, 256)
+    return buf.value.decode()
 
 
 class Counts:

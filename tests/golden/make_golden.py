@@ -68,6 +68,33 @@ def reference_fixture(out_path: str) -> int:
     return len(rows)
 
 
+def reference_population_fixture(out_path: str) -> int:
+    """Biallelic SNV lines of the reference's population VCF: both samples' GT/ACN and the INFO
+    fields DiversityStatistics produces (NS, AN, AFS, MAF; this older NGSEP does not print OH)."""
+    rows = []
+    with gzip.open(REF_VCF, "rt") as f:
+        for line in f:
+            if line.startswith("#"):
+                continue
+            fs = line.rstrip("\n").split("\t")
+            ref, alt = fs[3], fs[4]
+            if len(ref) != 1 or len(alt) != 1 or ref not in "ACGT" or alt not in "ACGT":
+                continue
+            info = dict(kv.split("=", 1) for kv in fs[7].split(";") if "=" in kv)
+            if not all(k in info for k in ("NS", "AN", "AFS", "MAF")):
+                continue
+            fmt = fs[8].split(":")
+            cols = []
+            for smp in fs[9:]:
+                d = dict(zip(fmt, smp.split(":")))
+                cols += [d.get("GT", "."), d.get("ACN", ".").replace(",", "|")]
+            rows.append(",".join(cols + [info["NS"], info["AN"], info["AFS"].replace(",", "|"), info["MAF"]]) + "\n")
+    with gzip.GzipFile(out_path, "wb", mtime=0) as g:
+        g.write(b"gt0,acn0,gt1,acn1,ns,an,afs,maf\n")
+        g.write("".join(rows).encode())
+    return len(rows)
+
+
 def md5(path: str) -> str:
     h = hashlib.md5()
     with open(path, "rb") as f:
@@ -103,4 +130,6 @@ if __name__ == "__main__":
     if "--no-reference" not in sys.argv:
         n = reference_fixture(os.path.join(HERE, "reference_demo_pl.csv.gz"))
         print("reference fixture rows:", n)
+        n = reference_population_fixture(os.path.join(HERE, "reference_demo_population.csv.gz"))
+        print("reference population rows:", n)
     oracle_fixtures()
