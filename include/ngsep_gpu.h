@@ -198,6 +198,10 @@ int ngsep_fetch_population_sites(ngsep_ctx* ctx, ngsep_popsite_out* sites, ngsep
                                  int64_t cap, int64_t* n_out);
 /* MultisampleVariantsDetector output: VCF header with the samples, then every fetched site */
 int ngsep_write_population_vcf(ngsep_ctx* ctx, const char* path);
+/* path B of the multisample detector: `MultisampleVariantsDetector -r REF -o OUT.vcf BAM...`
+ * (MultisampleVariantsDetector.main/run, :412-459): samples from the BAM headers' @RG SM tags,
+ * files merged as AlignmentsPileupGenerator.processFiles does (:201-266, chooseNextAln :268-289) */
+int ngsep_call_population_bams(ngsep_ctx* ctx, const char* const* bam_paths, int32_t n_files, const char* out_vcf_path);
 
 /* ---- path B: the whole SingleSampleVariantsDetector.findSNVS on a BAM file (:896-931) ---- */
 int ngsep_call_bam(ngsep_ctx* ctx, const char* bam_path, const char* out_vcf_path);

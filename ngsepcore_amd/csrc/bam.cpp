@@ -7,6 +7,7 @@
 // unmapped/secondary/multiple filter flags (AlignmentsPileupGenerator.java:363-375).
 #include <zlib.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -24,6 +25,7 @@ struct ngsep_bam {
     bool eof = false;
     std::vector<int32_t> ref_to_seq;   // BAM refID -> ctx sequence id
     std::vector<std::string> rg_ids;   // header read groups
+    std::vector<std::string> rg_sm;    // their SM tags (the read group id when absent, ReadAlignmentFileReader.java:186-188)
     std::unordered_map<std::string, int32_t> rg_index;
     int filter_flags = 0;
     int min_mq = 20;
@@ -142,7 +144,13 @@ extern "C" int ngsep_bam_open(ngsep_ctx* c, const char* path, ngsep_bam** out) {
             if (id != std::string::npos) {
                 size_t ie = line.find('\t', id + 4);
                 std::string v = line.substr(id + 4, ie == std::string::npos ? std::string::npos : ie - id - 4);
-                if (!b->rg_index.count(v)) { b->rg_index[v] = (int32_t)b->rg_ids.size(); b->rg_ids.push_back(v); }
+                std::string sm = v;
+                size_t sp = line.find("\tSM:");
+                if (sp != std::string::npos) {
+                    size_t se = line.find('\t', sp + 4);
+                    sm = line.substr(sp + 4, se == std::string::npos ? std::string::npos : se - sp - 4);
+                }
+                if (!b->rg_index.count(v)) { b->rg_index[v] = (int32_t)b->rg_ids.size(); b->rg_ids.push_back(v); b->rg_sm.push_back(sm); }
             }
         }
         p = e + 1;
@@ -326,4 +334,152 @@ int call_bam(ngsep_ctx* c, const char* bam_path, const char* out_vcf) {
 extern "C" int ngsep_call_bam(ngsep_ctx* c, const char* bam_path, const char* out_vcf_path) {
     if (!c || !bam_path || !out_vcf_path) return NGSEP_E_INVALID;
     return ngsep::call_bam(c, bam_path, out_vcf_path);
+}
+
+// ---- MultisampleVariantsDetector.run on BAM files (discovery/MultisampleVariantsDetector.java:421-459) ----
+namespace {
+int32_t java_hash(const std::string& s) {
+    uint32_t h = 0;
+    for (unsigned char ch : s) h = 31u * h + ch;
+    return (int32_t)h;
+}
+// iteration order of a java.util.HashSet<String> filled in the given order (variants/Sample.java:36)
+std::vector<int> hashset_order(const std::vector<std::string>& ids) {
+    size_t cap = 16;
+    while (ids.size() > cap * 3 / 4) cap *= 2;
+    std::vector<int> idx(ids.size());
+    std::vector<uint32_t> bucket(ids.size());
+    for (size_t i = 0; i < ids.size(); i++) {
+        idx[i] = (int)i;
+        const uint32_t h = (uint32_t)java_hash(ids[i]);
+        bucket[i] = (h ^ (h >> 16)) & (uint32_t)(cap - 1);
+    }
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return bucket[a] < bucket[b]; });
+    return idx;
+}
+struct Cursor {
+    ngsep_bam* bam = nullptr;
+    ngsep_read_batch batch{};
+    int64_t i = 0;
+    bool done = false;
+    std::vector<int32_t> rg_global;    // file read group -> global read group
+    int32_t last(int64_t k) const {
+        int32_t e = batch.first[k];
+        for (int32_t j = 0; j < batch.cigar_n[k]; j++) { const int32_t v = batch.cigar[batch.cigar_off[k] + j]; if (v & 1) e += v / 8; }
+        return e - 1;
+    }
+};
+}  // namespace
+
+extern "C" int ngsep_call_population_bams(ngsep_ctx* c, const char* const* bam_paths, int32_t n_files, const char* out_vcf_path) {
+    if (!c || !bam_paths || n_files <= 0 || !out_vcf_path) return NGSEP_E_INVALID;
+    if (!c->params.multisample) return set_error(c, NGSEP_E_INVALID, "ngsep_call_population_bams needs params.multisample = 1");
+    std::vector<Cursor> cur((size_t)n_files);
+    auto close_all = [&]() { for (auto& k : cur) if (k.bam) ngsep_bam_close(k.bam); };
+    // loadSamplesFromAlignmentHeaders (:499-523): read group -> sample over all files, samples by id
+    std::vector<std::string> rg_ids, rg_sm;
+    std::unordered_map<std::string, int32_t> rg_global;
+    for (int f = 0; f < n_files; f++) {
+        int rc = ngsep_bam_open(c, bam_paths[f], &cur[(size_t)f].bam);
+        if (rc != NGSEP_OK) { close_all(); return rc; }
+        ngsep_bam* b = cur[(size_t)f].bam;
+        for (size_t g = 0; g < b->rg_ids.size(); g++) {
+            auto it = rg_global.find(b->rg_ids[g]);
+            if (it == rg_global.end()) {
+                it = rg_global.emplace(b->rg_ids[g], (int32_t)rg_ids.size()).first;
+                rg_ids.push_back(b->rg_ids[g]);
+                rg_sm.push_back(b->rg_sm[g]);
+            } else if (rg_sm[(size_t)it->second] != b->rg_sm[g]) {
+                close_all();
+                return set_error(c, NGSEP_E_FORMAT, "The read group ID: " + b->rg_ids[g] + " is associated to two different samples");
+            }
+            cur[(size_t)f].rg_global.push_back(it->second);
+        }
+    }
+    std::vector<std::string> samples(rg_sm);
+    std::sort(samples.begin(), samples.end());
+    samples.erase(std::unique(samples.begin(), samples.end()), samples.end());
+    std::vector<int32_t> rg_sample(rg_ids.size(), -1), rg_rank(rg_ids.size(), 0);
+    for (size_t sm = 0; sm < samples.size(); sm++) {
+        std::vector<int32_t> members;
+        std::vector<std::string> mids;
+        for (size_t g = 0; g < rg_ids.size(); g++)
+            if (rg_sm[g] == samples[sm]) { members.push_back((int32_t)g); mids.push_back(rg_ids[g]); }
+        std::vector<int> ord = hashset_order(mids);
+        for (size_t r = 0; r < ord.size(); r++) { rg_sample[(size_t)members[(size_t)ord[r]]] = (int32_t)sm; rg_rank[(size_t)members[(size_t)ord[r]]] = (int32_t)r; }
+    }
+    std::vector<const char*> sid;
+    for (const auto& x : samples) sid.push_back(x.c_str());
+    int rc = ngsep_set_samples(c, (int32_t)samples.size(), sid.data(), (int32_t)rg_ids.size(), rg_sample.data(), rg_rank.data());
+    if (rc != NGSEP_OK) { close_all(); return rc; }
+    // AlignmentsPileupGenerator.processFiles: k-way merge by GenomicRegionComparator (sequence order,
+    // first, last), ties to the lowest file index (chooseNextAln, :268-289)
+    auto refill = [&](Cursor& k) -> int {
+        while (!k.done && k.i >= k.batch.n_reads) {
+            int r = ngsep_bam_next_batch(k.bam, 1 << 18, &k.batch);
+            if (r != NGSEP_OK) return r;
+            k.i = 0;
+            if (k.batch.n_reads == 0) k.done = true;
+        }
+        return NGSEP_OK;
+    };
+    for (auto& k : cur) { rc = refill(k); if (rc != NGSEP_OK) { close_all(); return rc; } }
+    // merged batch storage
+    std::vector<int32_t> m_seq, m_first, m_flags, m_rg, m_cig_n, m_cigar, m_seqlen;
+    std::vector<int64_t> m_cig_off, m_seq_off;
+    std::vector<uint8_t> m_hasq;
+    std::string m_bases, m_quals;
+    auto flush = [&]() -> int {
+        if (m_first.empty()) return NGSEP_OK;
+        ngsep_read_batch mb{};
+        mb.n_reads = (int64_t)m_first.size();
+        mb.seq_id = m_seq.data(); mb.first = m_first.data(); mb.flags = m_flags.data(); mb.read_group = m_rg.data();
+        mb.cigar_off = m_cig_off.data(); mb.cigar_n = m_cig_n.data(); mb.cigar = m_cigar.data();
+        mb.seq_off = m_seq_off.data(); mb.seq_len = m_seqlen.data(); mb.bases = m_bases.data(); mb.quals = m_quals.data();
+        mb.has_quals = m_hasq.data();
+        int r = ngsep_process_alignments(c, &mb);
+        m_seq.clear(); m_first.clear(); m_flags.clear(); m_rg.clear(); m_cig_n.clear(); m_cigar.clear(); m_seqlen.clear();
+        m_cig_off.clear(); m_seq_off.clear(); m_hasq.clear(); m_bases.clear(); m_quals.clear();
+        return r;
+    };
+    while (true) {
+        int best = -1;
+        int32_t bs = 0, bf = 0, bl = 0;
+        for (int f = 0; f < n_files; f++) {
+            Cursor& k = cur[(size_t)f];
+            if (k.done) continue;
+            const int32_t s2 = k.batch.seq_id[k.i], f2 = k.batch.first[k.i];
+            if (best >= 0 && (s2 > bs || (s2 == bs && (f2 > bf || (f2 == bf && k.last(k.i) >= bl))))) continue;
+            best = f; bs = s2; bf = f2; bl = k.last(k.i);
+        }
+        if (best < 0) break;
+        Cursor& k = cur[(size_t)best];
+        const int64_t i = k.i;
+        m_seq.push_back(k.batch.seq_id[i]);
+        m_first.push_back(k.batch.first[i]);
+        m_flags.push_back(k.batch.flags[i]);
+        const int32_t lrg = k.batch.read_group ? k.batch.read_group[i] : -1;
+        m_rg.push_back(lrg >= 0 && lrg < (int32_t)k.rg_global.size() ? k.rg_global[(size_t)lrg] : -1);
+        m_cig_off.push_back((int64_t)m_cigar.size());
+        m_cig_n.push_back(k.batch.cigar_n[i]);
+        m_cigar.insert(m_cigar.end(), k.batch.cigar + k.batch.cigar_off[i], k.batch.cigar + k.batch.cigar_off[i] + k.batch.cigar_n[i]);
+        m_seq_off.push_back((int64_t)m_bases.size());
+        m_seqlen.push_back(k.batch.seq_len[i]);
+        m_bases.append(k.batch.bases + k.batch.seq_off[i], (size_t)k.batch.seq_len[i]);
+        m_quals.append(k.batch.quals + k.batch.seq_off[i], (size_t)k.batch.seq_len[i]);
+        m_hasq.push_back(k.batch.has_quals ? k.batch.has_quals[i] : 1);
+        k.i++;
+        if (k.i >= k.batch.n_reads) {
+            // the merged batch references nothing of this reader's arrays any more (copied above)
+            rc = refill(k);
+            if (rc != NGSEP_OK) { close_all(); return rc; }
+        }
+        if (m_first.size() >= (1u << 18)) { rc = flush(); if (rc != NGSEP_OK) { close_all(); return rc; } }
+    }
+    rc = flush();
+    close_all();
+    if (rc != NGSEP_OK) return rc;
+    rc = ngsep_notify_end(c);
+    if (rc != NGSEP_OK) return rc;
+    return ngsep_write_population_vcf(c, out_vcf_path);
 }

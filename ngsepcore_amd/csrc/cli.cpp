@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/ngsep_gpu.h"
 
@@ -18,12 +19,66 @@ static int usage(const char* argv0) {
     return 2;
 }
 
+// `ngsep-amd MultisampleVariantsDetector -r REF -o OUT.vcf [options] BAM...`
+// (MultisampleVariantsDetector.main/run, discovery/MultisampleVariantsDetector.java:412-459)
+static int main_mvd(int argc, char** argv, int i) {
+    ngsep_params p;
+    ngsep_params_default(&p);
+    p.multisample = 1;
+    const char *ref = nullptr, *outp = "variants.vcf";
+    int device = 0;
+    std::vector<const char*> bams;
+    for (; i < argc; i++) {
+        const char* a = argv[i];
+        const char* v = i + 1 < argc ? argv[i + 1] : nullptr;
+        auto takes = [&](const char* name) { if (std::strcmp(a, name) == 0 && v) { i++; return true; } return false; };
+        if (takes("-r")) ref = v;
+        else if (takes("-o")) outp = v;
+        else if (takes("-ploidy")) p.ploidy = std::atoi(v);
+        else if (takes("-minMQ")) p.min_mq = std::atoi(v);
+        else if (takes("-maxAlnsPerStartPos")) p.max_alns_per_start = std::atoi(v);
+        else if (takes("-ignore5")) p.ignore5 = std::atoi(v);
+        else if (takes("-ignore3")) p.ignore3 = std::atoi(v);
+        else if (takes("-h")) { p.het_rate = std::atof(v); p.het_rate_set = 1; }
+        else if (takes("-maxBaseQS")) p.max_base_qs = std::atoi(v);
+        else if (takes("-minQuality")) p.min_quality = std::atoi(v);
+        else if (takes("-minAlleleDepthFrequency")) p.min_allele_depth_freq = std::atof(v);
+        else if (takes("-querySeq")) std::snprintf(p.query_seq, sizeof p.query_seq, "%s", v);
+        else if (takes("-first")) p.query_first = std::atoi(v);
+        else if (takes("-last")) p.query_last = std::atoi(v);
+        else if (takes("-device")) device = std::atoi(v);
+        else if (!std::strcmp(a, "-psp")) p.print_sample_ploidy = 1;
+        else if (!std::strcmp(a, "-p")) p.process_nonunique = 1;
+        else if (!std::strcmp(a, "-s")) p.process_secondary = 1;
+        else if (!std::strcmp(a, "-ignoreLowerCaseRef")) p.ignore_lowercase_ref = 1;
+        else if (a[0] == '-') { std::fprintf(stderr, "unknown or unsupported option %s\n", a); return 2; }
+        else bams.push_back(a);
+    }
+    if (!ref || bams.empty()) {
+        std::fprintf(stderr, "usage: ngsep-amd MultisampleVariantsDetector -r <reference.fa> -o <out.vcf> [options] <BAM>...\n");
+        return 2;
+    }
+    ngsep_ctx* c = nullptr;
+    int rc = ngsep_open(device, &p, &c);
+    if (rc == NGSEP_OK) rc = ngsep_load_fasta(c, ref);
+    if (rc == NGSEP_OK) rc = ngsep_call_population_bams(c, bams.data(), (int32_t)bams.size(), outp);
+    if (rc != NGSEP_OK) { std::fprintf(stderr, "error %d: %s\n", rc, c ? ngsep_last_error(c) : "open failed"); if (c) ngsep_close(c); return 1; }
+    ngsep_stats st;
+    ngsep_get_stats(c, &st);
+    std::fprintf(stderr, "alignments=%lld admitted=%lld positions=%lld candidates=%lld variants=%lld\n",
+                 (long long)st.alignments_in, (long long)st.alignments_admitted, (long long)st.positions_genotyped,
+                 (long long)st.candidates, (long long)st.sites_called);
+    ngsep_close(c);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     ngsep_params p;
     ngsep_params_default(&p);
     const char *in = nullptr, *ref = nullptr, *outp = nullptr;
     int device = 0;
     int i = 1;
+    if (i < argc && std::strcmp(argv[i], "MultisampleVariantsDetector") == 0) return main_mvd(argc, argv, i + 1);
     if (i < argc && std::strcmp(argv[i], "SingleSampleVariantsDetector") == 0) i++;
     else if (i < argc && argv[i][0] != '-') { std::fprintf(stderr, "unsupported command %s\n", argv[i]); return usage(argv[0]); }
     for (; i < argc; i++) {

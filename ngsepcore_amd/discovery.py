@@ -367,6 +367,17 @@ class MultisampleVariantsDetector:
     def setQueryFirst(self, v: int): self.params.query_first = int(v)
     def setQueryLast(self, v: int): self.params.query_last = int(v)
 
+    def run(self, input_files: Sequence[str]) -> GpuPileupSession:
+        """MultisampleVariantsDetector.run (:421-459) on BAM files: samples from the headers,
+        files merged in the generator's order, VCF written to outFilename."""
+        if self.genomeFile is None:
+            raise NgsepError(_lib.NGSEP_E_IO, "The reference genome file is a required parameter")
+        s = GpuPileupSession(self.params, self.device)
+        s.load_fasta(self.genomeFile)
+        arr = (ctypes.c_char_p * len(input_files))(*[f.encode() for f in input_files])
+        s._check(s._lib.ngsep_call_population_bams(s._ctx, arr, len(input_files), self.outFilename.encode()))
+        return s
+
     def session(self, read_groups: Sequence[tuple]) -> GpuPileupSession:
         s = GpuPileupSession(self.params, self.device)
         s.set_samples(read_groups)

@@ -81,3 +81,25 @@ def test_population_200_samples_staged(tmp_path):
     assert not d, "\n".join(d[:20])
     assert n_records(o) > 10
     assert st.hard_sites < st.positions_genotyped      # the per-sample bounds dropped positions
+
+
+def test_population_bams_path_b(tmp_path):
+    """`MultisampleVariantsDetector -r REF -o OUT.vcf S000.bam ... S011.bam`: samples from the BAM
+    headers, files merged in AlignmentsPileupGenerator's order (C++ path, ngsep_call_population_bams)."""
+    import subprocess
+    from ngsepcore_amd import MultisampleVariantsDetector
+    syn, fa, sam, rgs = population(tmp_path, genome=pysynth.CUSTOM, custom_len=30000, seed=8, n_samples=12,
+                                   depth=10, snv_rate=3e-3)
+    bams = syn.write_sample_bams(os.path.join(str(tmp_path), "pop"))
+    o = oracle_mvd(tmp_path, fa, sam)
+    d = MultisampleVariantsDetector()
+    d.setGenome(fa)
+    d.setOutFilename(os.path.join(str(tmp_path), "gpu_b.vcf"))
+    d.run(bams[::-1])                       # file order does not change the merge (ties: equal spans)
+    diff = diff_vcf(o, d.outFilename)
+    assert not diff, "\n".join(diff[:20])
+    cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ngsepcore_amd", "lib", "ngsep-amd")
+    out_cli = os.path.join(str(tmp_path), "cli.vcf")
+    subprocess.run([cli, "MultisampleVariantsDetector", "-r", fa, "-o", out_cli] + bams, check=True)
+    diff = diff_vcf(o, out_cli)
+    assert not diff, "\n".join(diff[:20])

@@ -475,11 +475,29 @@ int reg2bin(int beg, int end) {
 template <class T> void put(std::string& b, T v) { b.append((const char*)&v, sizeof(T)); }
 }  // namespace
 
-extern "C" int ngs_synth_write_bam(const ngs_synth* s, const char* path) {
+static int write_bam_impl(const ngs_synth* s, const char* path, int only_sample);
+extern "C" int ngs_synth_write_bam(const ngs_synth* s, const char* path) { return write_bam_impl(s, path, -1); }
+// one sample's records (and only its @RG line): the per-sample BAM files a multisample run reads
+extern "C" int ngs_synth_write_bam_sample(const ngs_synth* s, const char* path, int sample) { return write_bam_impl(s, path, sample); }
+
+static int write_bam_impl(const ngs_synth* s, const char* path, int only_sample) {
     FILE* f = std::fopen(path, "wb");
     if (!f) return -1;
     Bgzf z(f);
     std::string h = header_text(s);
+    if (only_sample >= 0) {
+        std::string keep;
+        char want[32];
+        std::snprintf(want, sizeof want, "@RG\tID:S%03d\t", s->p.sample_idx + only_sample);
+        size_t p0 = 0;
+        while (p0 < h.size()) {
+            size_t e = h.find('\n', p0);
+            std::string line = h.substr(p0, e - p0 + 1);
+            if (line.compare(0, 3, "@RG") != 0 || line.compare(0, std::strlen(want), want) == 0) keep += line;
+            p0 = e + 1;
+        }
+        h = keep;
+    }
     std::string b = "BAM\1";
     put<int32_t>(b, (int32_t)h.size());
     b += h;
@@ -493,6 +511,7 @@ extern "C" int ngs_synth_write_bam(const ngs_synth* s, const char* path) {
     static const int bam_op[8] = {5, 2, 1, 0, 6, 3, 4, 8};  // NGSEP op -> BAM op (H D I M P N S X)
     const char* nt16 = "=ACMGRSVTWYHKDBN";
     for (const Read& rd : s->reads) {
+        if (only_sample >= 0 && rd.sample != only_sample) continue;
         char rg[16];
         std::snprintf(rg, sizeof rg, "S%03d", s->p.sample_idx + rd.sample);
         std::string r;

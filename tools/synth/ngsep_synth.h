@@ -55,6 +55,7 @@ int ngs_synth_batch(ngs_synth* s, ngsep_read_batch* out);
 int ngs_synth_write_fasta(const ngs_synth* s, const char* path);
 int ngs_synth_write_sam(const ngs_synth* s, const char* path);
 int ngs_synth_write_bam(const ngs_synth* s, const char* path);
+int ngs_synth_write_bam_sample(const ngs_synth* s, const char* path, int sample);
 int ngs_synth_write_truth(const ngs_synth* s, const char* path);
 /* SAM text -> BAM (header verbatim, records in file order, aux tags A/i/f/Z) */
 int ngs_sam_to_bam(const char* sam_path, const char* bam_path);

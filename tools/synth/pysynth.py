@@ -53,6 +53,7 @@ def lib():
         for f in ("ngs_synth_write_fasta", "ngs_synth_write_sam", "ngs_synth_write_bam", "ngs_synth_write_truth"):
             getattr(l, f).argtypes = [ctypes.c_void_p, ctypes.c_char_p]
         l.ngs_sam_to_bam.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        l.ngs_synth_write_bam_sample.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
         _lib = l
     return _lib
 
@@ -112,3 +113,13 @@ class Synth:
             if rc != 0:
                 raise IOError(f"{f} failed for {prefix}{suf}")
         return prefix + ".fa", prefix + ".sam", prefix + ".bam"
+
+    def write_sample_bams(self, prefix: str):
+        """one BAM per sample of a population (n_samples > 1)"""
+        out = []
+        for k in range(max(1, self.params.n_samples)):
+            path = f"{prefix}_S{self.params.sample_idx + k:03d}.bam"
+            if lib().ngs_synth_write_bam_sample(self.h, path.encode(), k) != 0:
+                raise IOError(f"write failed for {path}")
+            out.append(path)
+        return out
