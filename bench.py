@@ -8,6 +8,11 @@ in HBM: k_tile_pileup (LDS-staged pileup tiles: candidate scan + tally) + k_post
 (libngsep_amd.so, ngsep_run_staged).  N>1: one process per GPU, each rank owns its own
 synthetic genome (seed 2+rank) -- windows shard with no data-path collective ("weak").
 
+--config multisample (BASELINE.json configs[4], MultisampleVariantsDetector): 200 samples at 10x
+(population SNVs in HWE), one rank = one contig shard of the 8-GPU split (default chrIV, the largest
+yeast contig, ~1/8 of the genome); a step = KTM (per-sample tile scan) + KPM (population
+genotyping) + D2H of the sites and every sample's call.
+
 Prints one JSON line (rank 0).  --gpus N under torch.distributed.run for N>1.
 """
 from __future__ import annotations
@@ -54,6 +59,26 @@ def cpu_baseline(depth: float, seed: int, n_contigs: int):
     }
 
 
+def cpu_baseline_mvd(samples: int, depth: float, length: int = 20000):
+    """The oracle's MultisampleVariantsDetector (single thread) on a bounded sample: the same
+    population model on a 20 kb contig."""
+    import ngsep_oracle
+    import pysynth
+    syn = pysynth.Synth(genome=pysynth.CUSTOM, custom_len=length, depth=depth, seed=5, n_samples=samples)
+    with tempfile.TemporaryDirectory() as d:
+        fa, sam, _ = syn.write(os.path.join(d, "cpu"))
+        st = ngsep_oracle.run_mvd(fa, sam, os.path.join(d, "cpu.vcf"))
+    syn.close()
+    return {
+        "value": st.positions_genotyped / st.seconds,
+        "unit": "positions/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"oracle MultisampleVariantsDetector (C restatement, SAM->VCF) on {samples} samples x "
+                  f"{length} bp at {depth:g}x ({st.positions_genotyped} positions), {st.seconds:.2f} s",
+    }
+
+
 def load_traffic(workload_key: str):
     """Per-launch HBM bytes of k_tile_pileup from the committed PMC pass (profiles/), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -75,7 +100,13 @@ def main():
     ap.add_argument("--genome", default="yeast", choices=["yeast", "human_chr20"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-contigs", type=int, default=4)
+    ap.add_argument("--config", default="single", choices=["single", "multisample"])
+    ap.add_argument("--samples", type=int, default=200)
+    ap.add_argument("--contig-first", type=int, default=3, help="multisample: first yeast contig of the shard")
+    ap.add_argument("--n-contigs", type=int, default=1, help="multisample: contigs in the shard")
     args = ap.parse_args()
+    if args.config == "multisample" and args.depth == 30.0:
+        args.depth = 10.0
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -93,7 +124,15 @@ def main():
 
     seed = 2 + rank
     t0 = time.time()
-    if args.genome == "yeast":
+    multi = args.config == "multisample"
+    if multi:
+        seed = 5
+        syn = pysynth.Synth(genome=pysynth.YEAST, depth=args.depth, seed=seed, n_samples=args.samples,
+                            contig_first=args.contig_first + rank, n_contigs=args.n_contigs)
+        names = [n for n, _ in syn.contigs()]
+        workload = (f"MultisampleVariantsDetector: {args.samples} synthetic yeast samples at {args.depth:g}x, "
+                    f"shard {'+'.join(names)} (one GPU's contig shard of the 8-GPU split)")
+    elif args.genome == "yeast":
         syn = pysynth.Synth(genome=pysynth.YEAST, depth=args.depth, seed=seed)
         workload = "yeast whole genome (sacCer3 names/lengths, 12,157,105 bp) 30x synthetic 150 bp SE"
     else:
@@ -101,7 +140,12 @@ def main():
         workload = "human chr20 (64,444,167 bp) 30x synthetic 150 bp SE"
     t_gen = time.time() - t0
     params = default_params()
+    if multi:
+        params.multisample = 1
     sess = GpuPileupSession(params, device=local_rank)
+    if multi:
+        n = max(1, syn.params.n_samples)
+        sess.set_samples([(f"S{k:03d}", f"S{k:03d}") for k in range(n)])
     for name, seq in syn.contigs():
         sess.set_reference(name, seq)
     t1 = time.time()
@@ -162,7 +206,8 @@ def main():
         # 1 B reference per genotyped position, 16 B read header per admitted read
         alg_bytes = st.read_bases + positions + 16 * st.alignments_admitted
         achieved = alg_bytes / (k_avg_ms * 1e-3) / 1e9
-        workload_key = f"{args.genome}:{args.depth:g}x:seed{seed}"
+        workload_key = (f"multisample{args.samples}:{args.depth:g}x:contig{args.contig_first}" if multi
+                        else f"{args.genome}:{args.depth:g}x:seed{seed}")
         traffic = load_traffic(workload_key)
         line = {
             "metric": METRIC,
@@ -191,7 +236,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_tile_pileup",
+                "kernel": "k_tile_pileup_multi" if multi else "k_tile_pileup",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -203,9 +248,13 @@ def main():
             },
             "kernel_positions_per_s": total_positions / ((k_avg_ms + sum(geno_ms) / len(geno_ms)) * 1e-3),
         }
+        if multi:
+            line["config"]["samples"] = args.samples
+            line["config"]["sample_calls_per_step"] = int(n_sites) * args.samples
         if not args.no_cpu_baseline:
             try:
-                line["cpu_baseline"] = cpu_baseline(args.depth, 2, args.cpu_contigs)
+                line["cpu_baseline"] = (cpu_baseline_mvd(args.samples, args.depth) if multi
+                                        else cpu_baseline(args.depth, 2, args.cpu_contigs))
             except Exception as e:  # the baseline is reported, never required
                 line["cpu_baseline"] = {"value": None, "error": str(e)}
         print(json.dumps(line), flush=True)

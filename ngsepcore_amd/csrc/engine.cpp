@@ -612,6 +612,44 @@ static void build_pile_multi(Staged& s) {
     }
 }
 
+// Population kernel read index: bucket b = (sample, read-group rank) in sample order, then the reads
+// of no sample; a stable counting sort of the read table by bucket keeps the pending order inside a
+// bucket, so walking a sample's buckets in rank order visits its calls exactly as
+// PileupRecord.getAlleleCalls(span, readGroups) does (:104-111).
+static void build_buckets(const ngsep_ctx* c, Staged& s) {
+    const int S = s.n_samples;
+    const int32_t* R = s.h_reads.data();
+    s.h_bbase.assign((size_t)S + 2, 0);
+    for (int sm = 0; sm < S; sm++) s.h_bbase[(size_t)sm + 1] = s.h_bbase[(size_t)sm] + std::max<int>(1, c->sample_nrank[(size_t)sm]);
+    s.h_bbase[(size_t)S + 1] = s.h_bbase[(size_t)S] + 1;
+    const int nb = s.h_bbase[(size_t)S + 1];
+    auto bucket = [&](int64_t r) -> int {
+        const int32_t fl = R[r * 4 + 3];
+        const int sm = (fl >> 8) - 1, rk = (fl >> 1) & 127;
+        return sm >= 0 && sm < S ? s.h_bbase[(size_t)sm] + rk : nb - 1;
+    };
+    s.h_bseg.assign((size_t)nb + 1, 0);
+    for (int64_t r = 0; r < s.n_reads; r++) s.h_bseg[(size_t)bucket(r) + 1]++;
+    for (int b = 0; b < nb; b++) s.h_bseg[(size_t)b + 1] += s.h_bseg[(size_t)b];
+    s.h_perm.assign((size_t)s.n_reads, 0);
+    std::vector<int32_t> fill(s.h_bseg.begin(), s.h_bseg.end() - 1);
+    for (int64_t r = 0; r < s.n_reads; r++) s.h_perm[(size_t)fill[(size_t)bucket(r)]++] = (int32_t)r;
+    // per bucket and 64-position block k: first index whose read starts at >= 64k - pad + 1
+    const int32_t pad = s.windows.empty() ? 64 : s.windows[0].pad;
+    s.nblk_b = (s.g_len + pad + 63) / 64 + 2;
+    s.h_blb.assign((size_t)nb * (size_t)s.nblk_b, 0);
+    for (int b = 0; b < nb; b++) {
+        int32_t j = s.h_bseg[(size_t)b];
+        const int32_t end = s.h_bseg[(size_t)b + 1];
+        int32_t* out = &s.h_blb[(size_t)b * (size_t)s.nblk_b];
+        for (int64_t k = 0; k < s.nblk_b; k++) {
+            const int64_t key = k * 64 - pad + 1;
+            while (j < end && (int64_t)R[(int64_t)s.h_perm[(size_t)j] * 4] < key) j++;
+            out[k] = j;
+        }
+    }
+}
+
 int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     Staged& s = c->staged;
     s = Staged();
@@ -708,6 +746,7 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     if (c->params.multisample) {
         s.n_samples = (int32_t)c->sample_ids.size();
         build_pile_multi(s);
+        build_buckets(c, s);
     } else {
         build_pile(s);
     }
@@ -732,6 +771,10 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     std::vector<TileInfo>().swap(s.h_tinfo);
     std::vector<uint16_t>().swap(s.h_rows);
     std::vector<int64_t>().swap(s.h_toff);
+    std::vector<int32_t>().swap(s.h_perm);
+    std::vector<int32_t>().swap(s.h_bseg);
+    std::vector<int32_t>().swap(s.h_blb);
+    std::vector<int32_t>().swap(s.h_bbase);
     return NGSEP_OK;
 }
 

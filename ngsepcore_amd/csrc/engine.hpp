@@ -53,8 +53,8 @@ constexpr int kTileMinPos = 16;
 static_assert(sizeof(ngsep_site_out) == 152, "site record layout");
 static_assert(sizeof(ngsep_sample_call) == 76, "sample call layout");
 static_assert(sizeof(ngsep_popsite_out) == 20, "population site layout");
-constexpr int kMaxSamplesDevice = 256;     // samples genotyped by one workgroup (one thread each)
-constexpr int kPopListCap = 12288;         // reads covering one position in the population kernel (LDS)
+constexpr int kMaxSamplesDevice = 255;     // samples genotyped by one workgroup (one thread each, one for reads of no sample)
+constexpr int kPopListCap = 8192;          // reads covering one position in the population kernel (LDS, twice)
 
 // Likelihood addends for the SNV model with n=4 alleles and f=g=250
 // (CountsHelper.java:147-185 with heterozygousProportion 0.5, SingleSampleVariantPileupListener.java:236)
@@ -83,7 +83,8 @@ struct GenotypeParams {
     int32_t min_quality;       // -minQuality
     int32_t dump_all;          // emit a record for every position with DP>0
     int32_t ablate;            // diagnostics only (env NGSEP_ABLATE): 1 scan only (no bound, no queue),
-                               // 4 no tiles, 8 tally without posterior, 16 posterior kernel reads the queue only
+                               // 4 no tiles, 8 tally without posterior, 16 posterior kernel reads the queue only,
+                               // 32 population kernel gathers only, 64 population kernel stops after the tallies
     int32_t use_bound;         // 1: candidates proven hom-ref by the integer bound are dropped in the tile kernel
 };
 
@@ -178,6 +179,9 @@ struct Staged {            // everything resident for one run
     int32_t n_samples = 0;
     std::vector<uint16_t> h_rows;
     std::vector<int64_t> h_toff;
+    // multisample: reads grouped by (sample, read-group rank) bucket for the population kernel
+    std::vector<int32_t> h_perm, h_bseg, h_blb, h_bbase;
+    int64_t nblk_b = 0;
     std::vector<uint8_t> h_ref;
 };
 

@@ -57,10 +57,16 @@ struct Device {
     uint16_t* d_rows = nullptr;      // multisample: rows per (tile, sample)
     int64_t* d_toff = nullptr;       // multisample: block offset per tile
     int8_t* d_nrank = nullptr;       // multisample: read groups per sample
+    int32_t* d_perm = nullptr;       // multisample: read indexes grouped by (sample, read-group rank) bucket
+    int32_t* d_bseg = nullptr;       // bucket b = perm[bseg[b] .. bseg[b+1])
+    int32_t* d_blb = nullptr;        // per bucket and 64-position block: first perm index that can cover it
+    int32_t* d_bbase = nullptr;      // sample s = buckets bbase[s] .. bbase[s+1]; sample n_samples = reads of no sample
+    int64_t nblk_b = 0;
     int32_t n_samples = 0;
     ngsep_popsite_out* d_psites = nullptr;
     ngsep_sample_call* d_pcalls = nullptr;
     int64_t cap_psites = 0;
+    unsigned long long* d_stamps = nullptr;   // diagnostics (NGSEP_TIMING)
     LikTables* d_tables = nullptr;
     ngsep_site_out* d_sites = nullptr;
     ngsep_site_out* d_sorted = nullptr;
@@ -628,7 +634,8 @@ void k_tile_pileup(
 // (SingleSampleVariantPileupListener.genotypeVariantSample, :361-391, evaluates the same posterior),
 // and a position where every sample is proven hom-ref gets variant QS 0, which
 // MultisampleVariantsDetector.onPileup never writes (:534).  The other positions are queued for KPM.
-__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(NGSEP_KT_WAVES_PER_EU)))
+constexpr int kScanChunkMulti = 8;      // a sample's block at 10x is a few wave-loads: one chunk
+__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(3)))
 void k_tile_pileup_multi(const u32x4* __restrict__ pile, const int64_t* __restrict__ toff,
                          const uint16_t* __restrict__ rows_ts, int32_t n_samples, const uint8_t* __restrict__ ref,
                          int32_t log2T, int64_t n_tiles, const LikTables* __restrict__ tabs, GenotypeParams gp,
@@ -648,11 +655,14 @@ void k_tile_pileup_multi(const u32x4* __restrict__ pile, const int64_t* __restri
     int32_t qn = 0;
     unsigned long long ncand = 0;
     uint32_t nexact = 0;
-    const int64_t nwaves = (int64_t)gridDim.x * kScanWaves;
-    for (int64_t t = (int64_t)blockIdx.x * kScanWaves + wv; t < n_tiles; t += nwaves) {
-        int64_t off = toff[t];
-        off = ((int64_t)__builtin_amdgcn_readfirstlane((int32_t)(off >> 32)) << 32) |
-              (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)off);
+    // one workgroup per tile: its waves take the samples in turn (s % 4 == wave) and OR their open
+    // positions in LDS, so a tile's samples are scanned in parallel
+    static_assert(kScanWaves == 4, "the open-position OR below combines four waves");
+    __shared__ uint32_t s_need[kScanWaves][64];
+    for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        int64_t base = toff[t];
+        base = ((int64_t)__builtin_amdgcn_readfirstlane((int32_t)(base >> 32)) << 32) |
+               (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)base);
         const int32_t tstart = (int32_t)(t << log2T);
         const u32x4 rc = *reinterpret_cast<const u32x4*>(ref + tstart + col * 16);
         const uint32_t ok = nib4(rc.x & 0x80808080u) | (nib4(rc.y & 0x80808080u) << 4) |
@@ -661,12 +671,19 @@ void k_tile_pileup_multi(const u32x4* __restrict__ pile, const int64_t* __restri
         for (int32_t s0 = 0; s0 < n_samples; s0 += 64) {
             const int32_t myrows = s0 + lane < n_samples ? (int32_t)rows_ts[t * n_samples + s0 + lane] : 0;
             const int32_t nsb = n_samples - s0 < 64 ? n_samples - s0 : 64;
-            for (int j = 0; j < nsb; j++) {
+            int32_t incl = myrows;                       // block offsets: prefix of rows over the samples
+            for (int o = 1; o < 64; o <<= 1) {
+                const int32_t v = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += v;
+            }
+            const int32_t excl = incl - myrows;
+            const int32_t btot = __shfl(incl, 63, 64);
+            for (int j = wv; j < nsb; j += kScanWaves) {
                 const int32_t rows = __builtin_amdgcn_readlane(myrows, j);
                 if (rows == 0) continue;
                 const int32_t nunits = rows << log2U;
+                const int64_t off = base + ((int64_t)__builtin_amdgcn_readlane(excl, j) << log2T);
                 const u32x4* blk = pile + (off >> 4);
-                off += (int64_t)rows << log2T;
                 const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)blk, 0, nunits * 16, 0x00020000);
                 const bool counted = rows <= 255;
                 uint32_t hits = 0;
@@ -677,19 +694,19 @@ void k_tile_pileup_multi(const u32x4* __restrict__ pile, const int64_t* __restri
                     cv += v >> 7;
                     ca += n >> 7;
                 };
-                for (int32_t u0 = 0; u0 < nunits; u0 += kScanChunk * 64) {
-                    u32x4 R[kScanChunk];
+                for (int32_t u0 = 0; u0 < nunits; u0 += kScanChunkMulti * 64) {
+                    u32x4 R[kScanChunkMulti];
 #pragma unroll
-                    for (int k = 0; k < kScanChunk; k++)
+                    for (int k = 0; k < kScanChunkMulti; k++)
                         R[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u0 + k * 64 + lane) * 16, 0, 0));
                     if (counted) {
 #pragma unroll
-                        for (int k = 0; k < kScanChunk; k++) {
+                        for (int k = 0; k < kScanChunkMulti; k++) {
                             cnt(R[k].x, cv0, ca0); cnt(R[k].y, cv1, ca1); cnt(R[k].z, cv2, ca2); cnt(R[k].w, cv3, ca3);
                         }
                     } else {
 #pragma unroll
-                        for (int k = 0; k < kScanChunk; k++) hits |= unit_hits<0>(R[k]);
+                        for (int k = 0; k < kScanChunkMulti; k++) hits |= unit_hits<0>(R[k]);
                     }
                 }
                 if (counted) {
@@ -743,13 +760,13 @@ void k_tile_pileup_multi(const u32x4* __restrict__ pile, const int64_t* __restri
                             }
                         };
                         nexact++;
-                        for (int32_t u0 = 0; u0 < nunits; u0 += kScanChunk * 64) {
-                            u32x4 R[kScanChunk];
+                        for (int32_t u0 = 0; u0 < nunits; u0 += kScanChunkMulti * 64) {
+                            u32x4 R[kScanChunkMulti];
 #pragma unroll
-                            for (int kk = 0; kk < kScanChunk; kk++)
+                            for (int kk = 0; kk < kScanChunkMulti; kk++)
                                 R[kk] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u0 + kk * 64 + lane) * 16, 0, 0));
 #pragma unroll
-                            for (int kk = 0; kk < kScanChunk; kk++) add(R[kk]);
+                            for (int kk = 0; kk < kScanChunkMulti; kk++) add(R[kk]);
                         }
                         for (int sft = (int)U; sft < 64; sft <<= 1) {
                             a0 += __shfl_xor(a0, sft, 64);
@@ -769,7 +786,13 @@ void k_tile_pileup_multi(const u32x4* __restrict__ pile, const int64_t* __restri
                     if (keep) need |= 1u << k;
                 }
             }
+            base += (int64_t)btot << log2T;
         }
+        s_need[wv][lane] = need;
+        __syncthreads();
+        need = s_need[0][lane] | s_need[1][lane] | s_need[2][lane] | s_need[3][lane];
+        if (wv != 0) need = 0;                           // wave 0 queues the tile's open positions
+        __syncthreads();
         // queue the open positions (the lead lane of each column)
         while (__ballot(need != 0)) {
             const bool has = need != 0;
@@ -980,18 +1003,22 @@ __device__ PopCall genotype_sample_d(const double* L, const int* cnt, int total,
 
 __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
     const QueueSite* __restrict__ queue, const unsigned long long* qn, int64_t qcap,
-    const int4* __restrict__ reads, int64_t n_reads, const int32_t* __restrict__ lb,
+    const int4* __restrict__ reads, const int32_t* __restrict__ perm, const int32_t* __restrict__ bseg,
+    const int32_t* __restrict__ blb, int64_t nblk, const int32_t* __restrict__ bbase,
     const uint8_t* __restrict__ slots, int32_t S, const LikTables* __restrict__ tabs, GenotypeParams gp,
-    const int8_t* __restrict__ sample_nrank, int32_t n_samples, double min_adf, int32_t ploidy,
+    int32_t n_samples, double min_adf, int32_t ploidy,
     ngsep_popsite_out* __restrict__ sites, ngsep_sample_call* __restrict__ calls,
-    unsigned long long* counters, int64_t cap) {
-    __shared__ uint32_t s_list[kPopListCap];     // code | flags << 8 (strand bit 8, rank 9-15, sample+1 16-31)
+    unsigned long long* counters, int64_t cap, unsigned long long* __restrict__ stamps) {
+    // stamps (diagnostics, NGSEP_TIMING): s_memtime at the phase ends of block 0's first site
+    auto stamp = [&](int k) {
+        if (stamps && blockIdx.x == 0 && threadIdx.x == 0) stamps[k] = __builtin_amdgcn_s_memtime();
+    };
+    stamp(0);
     __shared__ double s_t[3][32];
-    __shared__ int32_t s_wn[kPopThreads / 64];
-    __shared__ int32_t s_pc[4];
-    __shared__ int32_t s_n, s_called, s_qs;
+    __shared__ int32_t s_pc[4], s_tot;
+    __shared__ int32_t s_called, s_qs;
     __shared__ unsigned long long s_base;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
     if (tid < 96) s_t[tid >> 5][tid & 31] = (tid < 32 ? tabs->A : tid < 64 ? tabs->H : tabs->E)[tid & 31];
     int64_t n = (int64_t)*qn;
     if (n > qcap) n = qcap;
@@ -1000,72 +1027,79 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
         const QueueSite qs = queue[i];
         const int32_t gpos = qs.gpos;
         const uint32_t rc = (uint32_t)qs.rc;
-        if (tid == 0) { s_n = 0; s_pc[0] = s_pc[1] = s_pc[2] = s_pc[3] = 0; s_called = 0; s_qs = 0; }
-        // 1. the reads covering gpos, in pending order (the table is sorted by start)
-        for (int64_t r0 = lb[gpos >> 6];; r0 += kPopThreads) {
-            const int64_t r = r0 + tid;
-            const int4 h = r < n_reads ? reads[r] : int4{INT32_MAX, 0, 0, 0};
-            const bool in = h.x <= gpos;
-            const bool cov = in && h.y >= gpos;
-            const int32_t o = cov ? gpos - h.x : 0;
-            const uint32_t code = cov ? (uint32_t)slots[(int64_t)(h.z + o / S) * S + (o % S)] : 0u;
-            const bool keep = code != 0;                          // CountsHelper.java:210: a call is counted
-            const unsigned long long m = __ballot(keep);
-            if (lane == 0) s_wn[wv] = __popcll(m);
-            __syncthreads();
-            int32_t woff = 0, tot = 0;
-            for (int w = 0; w < kPopThreads / 64; w++) { if (w < wv) woff += s_wn[w]; tot += s_wn[w]; }
-            const int32_t pos_l = s_n + woff + __popcll(m & ((1ull << lane) - 1ull));
-            if (keep && pos_l < kPopListCap) s_list[pos_l] = code | ((uint32_t)h.w << 8);
-            const int stop = __syncthreads_or(!in);
-            if (tid == 0) s_n += tot;
-            if (stop) break;
-        }
+        if (tid == 0) { s_pc[0] = s_pc[1] = s_pc[2] = s_pc[3] = 0; s_tot = 0; s_called = 0; s_qs = 0; }
         __syncthreads();
-        const int32_t nl = s_n;
-        if (nl > kPopListCap) {                                   // deeper than the LDS list: reported, not called
-            if (tid == 0) atomicOr(&counters[3], 1ull << 63);
-            continue;
-        }
-        if (nl == 0) continue;                                    // createSNVVariantPool: totalCount 0
-        // 2. pooled counts over every alignment (getAlleleCalls(1, null))
-        for (int e = tid; e < nl; e += kPopThreads) {
-            const uint32_t cd = s_list[e] & 0xFFu;
-            if (cd & 0x80u) atomicAdd(&s_pc[(cd >> 5) & 3], 1);
-        }
-        // 3. per-sample tallies, thread = sample, in the sample's read-group order
+        // 1-3. thread s walks sample s's reads (bucket = sample, read-group rank: the order of
+        //      PileupRecord.getAlleleCalls(span, readGroups), :104-111, pending order inside a group)
+        //      that can cover gpos, 8 in flight; thread n_samples walks the reads of no sample, which
+        //      only enter the pooled counts (getAlleleCalls(1, null))
         int total = 0;
         int cnt[4] = {0, 0, 0, 0};
         double L[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        if (tid < n_samples) {
-            const int nr = sample_nrank[tid];
-            const uint32_t me = (uint32_t)(tid + 1);
-            for (int rk = 0; rk < nr; rk++) {
-                for (int e = 0; e < nl; e++) {
-                    const uint32_t ent = s_list[e];
-                    if ((ent >> 16) != me || ((ent >> 9) & 127u) != (uint32_t)rk) continue;
-                    total++;
-                    const uint32_t cd = ent & 0xFFu;
-                    if (!(cd & 0x80u)) continue;
-                    const uint32_t a = (cd >> 5) & 3u;
-                    int q = (int)(cd & 31u);
-                    q = q > gp.max_q ? gp.max_q : q;
-                    const double A = s_t[0][q], H = s_t[1][q], E = s_t[2][q];
-                    cnt[0] += a == 0; cnt[1] += a == 1; cnt[2] += a == 2; cnt[3] += a == 3;
-                    L[0] += a == 0 ? A : E;
-                    L[4] += a == 1 ? A : E;
-                    L[7] += a == 2 ? A : E;
-                    L[9] += a == 3 ? A : E;
-                    L[1] += a <= 1 ? H : E;
-                    L[2] += (a & 1) == 0 ? H : E;
-                    L[3] += (a == 0 || a == 3) ? H : E;
-                    L[5] += (a == 1 || a == 2) ? H : E;
-                    L[6] += (a & 1) == 1 ? H : E;
-                    L[8] += a >= 2 ? H : E;
+        if (tid <= n_samples) {
+            const int b0 = bbase[tid], b1 = bbase[tid + 1];
+            const bool tally = tid < n_samples;
+            for (int b = b0; b < b1; b++) {
+                const int32_t kend = bseg[b + 1];
+                bool more = true;
+                for (int32_t k0 = blb[(int64_t)b * nblk + (gpos >> 6)]; more && k0 < kend; k0 += 8) {
+                    int4 h[8];
+#pragma unroll
+                    for (int k = 0; k < 8; k++) h[k] = reads[perm[k0 + k < kend ? k0 + k : kend - 1]];
+                    uint32_t code[8];
+#pragma unroll
+                    for (int k = 0; k < 8; k++) {
+                        const bool in = k0 + k < kend && h[k].x <= gpos;
+                        if (!in) more = false;
+                        const bool cov = in && h[k].y >= gpos;
+                        const int32_t o = cov ? gpos - h[k].x : 0;
+                        const uint32_t cd = slots[(int64_t)(h[k].z + o / S) * S + (o % S)];
+                        code[k] = cov ? cd : 0u;
+                    }
+#pragma unroll
+                    for (int k = 0; k < 8; k++) {
+                        const uint32_t cd = code[k];
+                        total += cd != 0;                                  // CountsHelper.java:210
+                        if (!(cd & 0x80u)) continue;                       // q<=3 or not A/C/G/T (:214-221)
+                        const uint32_t a = (cd >> 5) & 3u;
+                        cnt[0] += a == 0; cnt[1] += a == 1; cnt[2] += a == 2; cnt[3] += a == 3;
+                        if (!tally) continue;
+                        int q = (int)(cd & 31u);
+                        q = q > gp.max_q ? gp.max_q : q;                   // -maxBaseQS (:217-219)
+                        const double A = s_t[0][q], H = s_t[1][q], E = s_t[2][q];
+                        L[0] += a == 0 ? A : E;
+                        L[4] += a == 1 ? A : E;
+                        L[7] += a == 2 ? A : E;
+                        L[9] += a == 3 ? A : E;
+                        L[1] += a <= 1 ? H : E;
+                        L[2] += (a & 1) == 0 ? H : E;
+                        L[3] += (a == 0 || a == 3) ? H : E;
+                        L[5] += (a == 1 || a == 2) ? H : E;
+                        L[6] += (a & 1) == 1 ? H : E;
+                        L[8] += a >= 2 ? H : E;
+                    }
                 }
             }
         }
+        if (i == blockIdx.x) stamp(1);
+        // pooled counts: the sum over every sample and the reads of no sample
+        {
+            int c0 = cnt[0], c1 = cnt[1], c2 = cnt[2], c3 = cnt[3], tt = total;
+            for (int o = 32; o > 0; o >>= 1) {
+                c0 += __shfl_xor(c0, o, 64); c1 += __shfl_xor(c1, o, 64);
+                c2 += __shfl_xor(c2, o, 64); c3 += __shfl_xor(c3, o, 64);
+                tt += __shfl_xor(tt, o, 64);
+            }
+            if (lane == 0) {
+                atomicAdd(&s_pc[0], c0); atomicAdd(&s_pc[1], c1); atomicAdd(&s_pc[2], c2); atomicAdd(&s_pc[3], c3);
+                atomicAdd(&s_tot, tt);
+            }
+        }
+        if (tid == n_samples) { total = 0; cnt[0] = cnt[1] = cnt[2] = cnt[3] = 0; }
         __syncthreads();
+        if (i == blockIdx.x) stamp(2);
+        if (s_tot == 0) continue;                                 // createSNVVariantPool: totalCount 0
+        if (gp.ablate & 64) continue;                             // diagnostics: tallies only
         // 4. candidate alleles from the pooled counts (createSNVVariantPool)
         if (!(rc & 0x80u)) continue;                               // N (or masked) reference: no variant
         const int refIdx = (int)((rc >> 5) & 3u);
@@ -1105,6 +1139,7 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
             multisnv = 0;                                          // makeNewVariant: SNV or GenomicVariantImpl (no TYPE)
             if (nal < 2) break;
         }
+        if (i == blockIdx.x) stamp(5);
         if (nal < 2) continue;                                     // only the reference allele is left
         if (qsv == 0 || qsv < gp.min_quality) continue;            // MultisampleVariantsDetector.java:534
         // 6. emit the site and its calls
@@ -1321,6 +1356,10 @@ void device_release(Device* d) {
     (void)hipFree(d->d_rows); d->d_rows = nullptr;
     (void)hipFree(d->d_toff); d->d_toff = nullptr;
     (void)hipFree(d->d_nrank); d->d_nrank = nullptr;
+    (void)hipFree(d->d_perm); d->d_perm = nullptr;
+    (void)hipFree(d->d_bseg); d->d_bseg = nullptr;
+    (void)hipFree(d->d_blb); d->d_blb = nullptr;
+    (void)hipFree(d->d_bbase); d->d_bbase = nullptr;
     d->n_samples = 0;
     d->n_units = d->n_slots = d->n_lb = d->n_reads = d->g_len = d->n_tiles = 0;
 }
@@ -1365,6 +1404,13 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
         HIP_TRY(hipMalloc(&d->d_nrank, (size_t)s.n_samples));
         if (!s.h_rows.empty()) HIP_TRY(hipMemcpyAsync(d->d_rows, s.h_rows.data(), s.h_rows.size() * sizeof(uint16_t), hipMemcpyHostToDevice, d->stream));
         if (!s.h_toff.empty()) HIP_TRY(hipMemcpyAsync(d->d_toff, s.h_toff.data(), s.h_toff.size() * sizeof(int64_t), hipMemcpyHostToDevice, d->stream));
+        auto up32 = [&](int32_t** dst, const std::vector<int32_t>& v) -> int {
+            HIP_TRY(hipMalloc(dst, std::max<size_t>(v.size(), 1) * sizeof(int32_t)));
+            if (!v.empty()) HIP_TRY(hipMemcpyAsync(*dst, v.data(), v.size() * sizeof(int32_t), hipMemcpyHostToDevice, d->stream));
+            return 0;
+        };
+        if (up32(&d->d_perm, s.h_perm) || up32(&d->d_bseg, s.h_bseg) || up32(&d->d_blb, s.h_blb) || up32(&d->d_bbase, s.h_bbase)) return -1;
+        d->nblk_b = s.nblk_b;
         d->n_samples = s.n_samples;
     }
     if (s.n_reads) HIP_TRY(hipMemcpyAsync(d->d_reads, s.h_reads.data(), (size_t)s.n_reads * 16, hipMemcpyHostToDevice, d->stream));
@@ -1554,6 +1600,9 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     if (S <= 0 || (int32_t)sample_nrank.size() != S) { err = "multisample run without samples (ngsep_set_samples)"; return -1; }
     if (S > kMaxSamplesDevice) { err = "too many samples for one device run"; return -1; }
     HIP_TRY(hipMemcpyAsync(d->d_nrank, sample_nrank.data(), (size_t)S, hipMemcpyHostToDevice, d->stream));
+    const bool timing = std::getenv("NGSEP_TIMING") != nullptr;
+    if (timing && !d->d_stamps) HIP_TRY(hipMalloc(&d->d_stamps, 16 * sizeof(unsigned long long)));
+    if (timing) HIP_TRY(hipMemsetAsync(d->d_stamps, 0, 16 * sizeof(unsigned long long), d->stream));
     int64_t want = std::max<int64_t>(d->last_n_sites + d->last_n_sites / 4 + 1024, 4096);
     if (want > d->cap_psites) {
         (void)hipFree(d->d_psites);
@@ -1581,7 +1630,7 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     if (d->n_tiles > 0) {
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_tile_pileup_multi, kScanThreads, 0) != hipSuccess || per_cu < 1) per_cu = 2;
-        const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((d->n_tiles + kScanWaves - 1) / kScanWaves, (int64_t)d->n_cu * per_cu));
+        const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>(d->n_tiles, (int64_t)d->n_cu * per_cu));
         hipLaunchKernelGGL(k_tile_pileup_multi, dim3((unsigned)nblk), dim3(kScanThreads), 0, d->stream, (const u32x4*)d->d_pile,
                            d->d_toff, d->d_rows, S, d->d_ref, d->log2_tile, d->n_tiles, d->d_tables, g, d->d_hard, ctr,
                            d->cap_hard);
@@ -1589,8 +1638,8 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     }
     HIP_TRY(hipEventRecord(d->ev[1], d->stream));
     hipLaunchKernelGGL(k_posterior_multi, dim3(2048), dim3(kPopThreads), 0, d->stream, d->d_hard, ctr + 2, d->cap_hard,
-                       d->d_reads, d->n_reads, d->d_lb, d->d_slots, d->slot_size, d->d_tables, g, d->d_nrank, S, min_adf,
-                       ploidy, d->d_psites, d->d_pcalls, ctr, d->cap_psites);
+                       d->d_reads, d->d_perm, d->d_bseg, d->d_blb, d->nblk_b, d->d_bbase, d->d_slots, d->slot_size,
+                       d->d_tables, g, S, min_adf, ploidy, d->d_psites, d->d_pcalls, ctr, d->cap_psites, d->d_stamps);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(d->ev[2], d->stream));
     HIP_TRY(hipMemcpyAsync(d->h_counters, ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, d->stream));
@@ -1620,6 +1669,12 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     d->last_n_sites = n;
     d->last_hard = (int64_t)d->h_counters[2];
     d->last_exact = (int64_t)(c3 & 0x7FFFFFFFFFFFFFFFull);
+    if (timing) {
+        unsigned long long st[16];
+        HIP_TRY(hipMemcpy(st, d->d_stamps, sizeof st, hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[ngsep timing] KPM block 0 phases (cycles): tally %lld, pooled %lld, genotype %lld\n",
+                     (long long)(st[1] - st[0]), (long long)(st[2] - st[1]), (long long)(st[5] - st[2]));
+    }
     float a = 0, a2 = 0;
     (void)hipEventElapsedTime(&a, d->ev[0], d->ev[1]);
     (void)hipEventElapsedTime(&a2, d->ev[1], d->ev[2]);
