@@ -517,7 +517,10 @@ static void build_pile_multi(Staged& s) {
             }
         }
     }
-    // tile size: bytes of all blocks + a fixed cost per (tile, sample) block
+    // tile size: bytes of all blocks + a fixed cost per (tile, sample) block (the scan's per-block
+    // reduction and bound work, in byte equivalents; NGSEP_MS_BLOCK_COST overrides it for tuning)
+    double block_cost = 1024.0;
+    if (const char* e = std::getenv("NGSEP_MS_BLOCK_COST")) block_cost = std::atof(e);
     int bestT = kTileMinPos;
     double best = -1;
     for (int T = kTileMinPos; T <= kTileMaxPos; T *= 2) {
@@ -531,7 +534,7 @@ static void build_pile_multi(Staged& s) {
                 bytes += (double)mx * T;
             }
         }
-        const double cost = bytes + 256.0 * (double)nt * S;
+        const double cost = bytes + block_cost * (double)nt * S;
         if (best < 0 || cost < best) { best = cost; bestT = T; }
     }
     const int T = bestT;
