@@ -2,10 +2,11 @@
 
 Workload (BASELINE.json configs[1]): yeast whole genome (sacCer3 contig names/lengths,
 12,157,105 bp, synthetic bases) at 30x, 150 bp single-end synthetic reads, one sample.
-A step = one pass of the hot path over the whole genome with the read SoA already resident
-in HBM: k_tile_pileup (LDS-staged pileup tiles: candidate scan + tally) + k_posterior
-(SNVQ posterior/call of the undecided candidates) + D2H of the called sites
-(libngsep_amd.so, ngsep_run_staged).  N>1: one process per GPU, each rank owns its own
+A step = one pass of the hot path over the whole genome with the pileup resident in HBM:
+k_tile_pileup (tile scan + hom-ref bounds) + k_posterior (exact tally, posterior and call of the
+undecided candidates) + ko_* (position order) + D2H of the called sites + host mapping to
+(sequence, position) (libngsep_amd.so, ngsep_submit_staged / ngsep_collect_staged, two passes in
+flight so one pass's copies overlap the next pass's kernels).  N>1: one process per GPU, each rank owns its own
 synthetic genome (seed 2+rank) -- windows shard with no data-path collective ("weak").
 
 --config multisample (BASELINE.json configs[4], MultisampleVariantsDetector): 200 samples at 10x
@@ -171,8 +172,13 @@ def main():
     barrier()
     scan_ms, geno_ms, dev_ms = [], [], []
     t_start = time.perf_counter()
-    for _ in range(args.steps):
-        sess.run_staged()
+    # a stream of passes, two in flight: pass k+1's kernels run while pass k's records are copied
+    # back and mapped (ngsep_submit_staged / ngsep_collect_staged); every pass is collected
+    sess.submit_staged()
+    for k in range(args.steps):
+        if k + 1 < args.steps:
+            sess.submit_staged()
+        sess.collect_staged()
         s = sess.stats()
         scan_ms.append(s.scan_ms)
         geno_ms.append(s.genotype_ms)

@@ -219,6 +219,12 @@ int ngsep_stage_finish(ngsep_ctx* ctx);
 /* one pass of K1+K2 (+ D2H of the calls) over every resident window; returns elapsed ms (host wall, synchronized) */
 int ngsep_run_staged(ngsep_ctx* ctx, double* elapsed_ms);
 int ngsep_release_staged(ngsep_ctx* ctx);
+/* the same pass split in two: submit enqueues the kernels and the result copies and returns at once;
+ * collect waits for the oldest submitted pass and makes its calls the context's result
+ * (ngsep_fetch_sites).  At most two passes in flight: the copies and host work of one overlap the
+ * kernels of the next (a streaming caller's pipeline over windows). */
+int ngsep_submit_staged(ngsep_ctx* ctx);
+int ngsep_collect_staged(ngsep_ctx* ctx, double* elapsed_ms);
 
 #ifdef __cplusplus
 }

@@ -163,6 +163,8 @@ SIGNATURES = {
     "ngsep_fetch_population_sites": (ctypes.c_int, [_CTX, P(NgsepPopSiteOut), P(NgsepSampleCall), ctypes.c_int64,
                                                     P(ctypes.c_int64)]),
     "ngsep_write_population_vcf": (ctypes.c_int, [_CTX, ctypes.c_char_p]),
+    "ngsep_submit_staged": (ctypes.c_int, [_CTX]),
+    "ngsep_collect_staged": (ctypes.c_int, [_CTX, P(ctypes.c_double)]),
     "ngsep_call_population_bams": (ctypes.c_int, [_CTX, P(ctypes.c_char_p), ctypes.c_int32, ctypes.c_char_p]),
     "ngsep_bam_open": (ctypes.c_int, [_CTX, ctypes.c_char_p, P(ctypes.c_void_p)]),
     "ngsep_bam_next_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, P(NgsepReadBatch)]),

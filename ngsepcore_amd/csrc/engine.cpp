@@ -881,6 +881,9 @@ static int run_device_multi(ngsep_ctx* c, const LikTables& t, const GenotypePara
     return NGSEP_OK;
 }
 
+static int finish_run(ngsep_ctx* c, size_t from, int64_t n, double scan_ms, double geno_ms, double total_ms,
+                      int64_t ncand, double* elapsed_ms);
+
 int run_device(ngsep_ctx* c, double* elapsed_ms) {
     LikTables t;
     GenotypeParams gp;
@@ -895,8 +898,13 @@ int run_device(ngsep_ctx* c, double* elapsed_ms) {
     const size_t from = c->sites.size();
     if (device_run(c->dev, c->staged, t, gp, prune, &c->sites, &n, &scan_ms, &geno_ms, &total_ms, &ncand, err) != 0)
         return set_error(c, NGSEP_E_DEVICE, err);
-    // records arrive sorted by global position; windows are laid out in processing order, so this is
-    // (sequence order, position).  Map global coordinates back to (sequence, position) in place.
+    return finish_run(c, from, n, scan_ms, geno_ms, total_ms, ncand, elapsed_ms);
+}
+
+// records arrive sorted by global position; windows are laid out in processing order, so this is
+// (sequence order, position).  Map global coordinates back to (sequence, position) in place.
+static int finish_run(ngsep_ctx* c, size_t from, int64_t n, double scan_ms, double geno_ms, double total_ms,
+                      int64_t ncand, double* elapsed_ms) {
     const std::vector<Window>& ws = c->staged.windows;
     size_t wi = 0, k = from;
     for (int64_t i = 0; i < n; i++) {
@@ -1090,6 +1098,47 @@ extern "C" int ngsep_run_staged(ngsep_ctx* c, double* elapsed_ms) {
     c->pop_calls.clear();
     c->stats.sites_called = 0;
     return run_device(c, elapsed_ms);
+}
+
+// asynchronous staged runs: submit enqueues one pass (kernels + copies) and returns; collect waits for
+// the oldest submitted pass and makes its calls the context's result.  At most two passes in flight,
+// so the D2H and host work of one pass overlap the next pass's kernels.
+extern "C" int ngsep_submit_staged(ngsep_ctx* c) {
+    if (!c || !c->dev) return set_error(c, NGSEP_E_INVALID, "nothing staged");
+    if (c->params.multisample) {            // population runs are synchronous: the result waits for collect
+        c->pop_sites.clear();
+        c->pop_calls.clear();
+        c->stats.sites_called = 0;
+        const int rc = run_device(c, nullptr);
+        if (rc == NGSEP_OK) c->pending_sync++;
+        return rc;
+    }
+    if (device_inflight(c->dev) >= 2) return set_error(c, NGSEP_E_INVALID, "two staged runs already in flight: collect first");
+    LikTables t;
+    GenotypeParams gp;
+    compute_tables(c, &t, &gp);
+    const int prune = c->params.prune_candidates && !c->params.dump_all_positions && c->het_rate <= 0.1;
+    std::string err;
+    if (device_submit(c->dev, c->staged, t, gp, prune, err) != 0) return set_error(c, NGSEP_E_DEVICE, err);
+    return NGSEP_OK;
+}
+
+extern "C" int ngsep_collect_staged(ngsep_ctx* c, double* elapsed_ms) {
+    if (!c || !c->dev) return set_error(c, NGSEP_E_INVALID, "nothing staged");
+    if (c->params.multisample) {
+        if (c->pending_sync <= 0) return set_error(c, NGSEP_E_INVALID, "no run to collect");
+        c->pending_sync--;
+        if (elapsed_ms) *elapsed_ms = c->stats.kernel_ms;
+        return NGSEP_OK;
+    }
+    c->sites.clear();
+    c->stats.sites_called = 0;
+    int64_t n = 0, ncand = 0;
+    double scan_ms = 0, geno_ms = 0, total_ms = 0;
+    std::string err;
+    if (device_collect(c->dev, &c->sites, &n, &scan_ms, &geno_ms, &total_ms, &ncand, err) != 0)
+        return set_error(c, NGSEP_E_DEVICE, err);
+    return finish_run(c, 0, n, scan_ms, geno_ms, total_ms, ncand, elapsed_ms);
 }
 
 extern "C" int ngsep_release_staged(ngsep_ctx* c) {

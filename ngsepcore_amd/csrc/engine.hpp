@@ -11,6 +11,7 @@
 #include <string>
 #include <vector>
 #include <mutex>
+#include <utility>
 
 #include "../../include/ngsep_gpu.h"
 
@@ -156,6 +157,7 @@ struct SiteStore {
         cap = nc;
     }
     void push_back(const ngsep_site_out& o) { reserve(n + 1); buf[n++] = o; }
+    void swap(SiteStore& o) { std::swap(buf, o.buf); std::swap(n, o.n); std::swap(cap, o.cap); }
 };
 
 struct Staged {            // everything resident for one run
@@ -214,6 +216,7 @@ struct ngsep_ctx {
     std::vector<int8_t> sample_nrank;        // read groups per sample
     // outputs
     ngsep::SiteStore sites;
+    int pending_sync = 0;                         // multisample runs submitted, not yet collected
     std::vector<ngsep_popsite_out> pop_sites;     // (sequence, position) order
     std::vector<ngsep_sample_call> pop_calls;     // pop_sites.size() x n_samples
     ngsep_stats stats{};
@@ -236,6 +239,12 @@ int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypePar
                SiteStore* out, int64_t* n_out, double* scan_ms, double* geno_ms, double* total_ms,
                int64_t* n_candidates, std::string& err);
 void device_release(Device* d);
+// asynchronous single-sample runs (two result slots): submit enqueues kernels and copies; collect
+// waits for the oldest run (an overflowed run is grown and re-run in place)
+int device_submit(Device* d, const Staged& s, const LikTables& t, const GenotypeParams& g, int prune, std::string& err);
+int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, double* geno_ms, double* total_ms,
+                   int64_t* n_candidates, std::string& err);
+int64_t device_inflight(const Device* d);
 // multisample: tile scan over the per-sample blocks + population genotyping of the queued
 // positions; appends the sites (global positions, unordered) and their calls
 int device_run_multi(Device* d, const Staged& s, const LikTables& t, const GenotypeParams& g,

@@ -44,9 +44,28 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 struct QueueSite;
 
+struct RunSlot {                     // one in-flight single-sample run's results (see device_submit)
+    ngsep_site_out* d_sorted = nullptr;
+    int64_t cap = 0;
+    unsigned long long* d_ctr = nullptr;     // its counter set (4)
+    unsigned long long* h_ctr = nullptr;     // pinned copy
+    SiteStore host;                          // pinned D2H destination of the ordered records
+    hipEvent_t ev[5] = {};                   // before KT, after KT, after KP, after KO, copies done
+    int64_t guess = 0;
+    bool busy = false;
+    int prune = 0;
+    GenotypeParams g{};
+    LikTables tabs{};
+    const Staged* staged = nullptr;
+    std::chrono::steady_clock::time_point t0;
+};
+
 struct Device {
     int ordinal = 0;
     hipStream_t stream = nullptr;
+    hipStream_t copy_stream = nullptr;
+    RunSlot slot[2];
+    int64_t n_submitted = 0, n_collected = 0;
     hipEvent_t ev[4] = {};
     uint8_t* d_slots = nullptr;
     uint8_t* d_pile = nullptr;
@@ -1278,9 +1297,8 @@ __global__ __launch_bounds__(256) void ko_bucket_sort(const unsigned long long* 
 __global__ __launch_bounds__(256) void ko_gather(const ngsep_site_out* __restrict__ recs,
                                                  const unsigned long long* __restrict__ keys,
                                                  const unsigned long long* n_ptr, int64_t cap,
-                                                 ngsep_site_out* __restrict__ sorted, unsigned long long* next_counters) {
+                                                 ngsep_site_out* __restrict__ sorted) {
     constexpr int W = sizeof(ngsep_site_out) / 4;
-    if (blockIdx.x == 0 && threadIdx.x < 4) next_counters[threadIdx.x] = 0;   // the next run's counter set
     int64_t n = (int64_t)*n_ptr;
     if (n > cap) n = cap;
     const uint32_t* src = reinterpret_cast<const uint32_t*>(recs);
@@ -1328,15 +1346,26 @@ Device* device_create(int ordinal, std::string& err) {
         if (hipGetDeviceProperties(&prop, ordinal) == hipSuccess && prop.multiProcessorCount > 0)
             d->n_cu = prop.multiProcessorCount;
     }
-    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) { err = "stream"; delete d; return nullptr; }
+    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&d->copy_stream, hipStreamNonBlocking) != hipSuccess) { err = "stream"; delete d; return nullptr; }
     for (auto& e : d->ev) (void)hipEventCreate(&e);
-    if (hipMalloc(&d->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(d->d_counters, 0, 8 * sizeof(unsigned long long)) != hipSuccess ||
+    for (auto& sl : d->slot)
+        for (auto& e : sl.ev) (void)hipEventCreateWithFlags(&e, hipEventDefault);
+    if (hipMalloc(&d->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(d->d_counters, 0, 16 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&d->h_counters, 4 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
         hipMalloc(&d->d_tables, sizeof(LikTables)) != hipSuccess) {
         err = "device allocation failed";
         delete d;
         return nullptr;
+    }
+    for (int k = 0; k < 2; k++) {
+        d->slot[k].d_ctr = d->d_counters + 8 + 4 * k;          // sets 2 and 3 (0-1: the multisample run)
+        if (hipHostMalloc(&d->slot[k].h_ctr, 4 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
+            err = "pinned allocation failed";
+            return nullptr;
+        }
+        (void)hipEventRecord(d->slot[k].ev[4], d->copy_stream);  // a fresh slot is free
     }
     return d;
 }
@@ -1347,6 +1376,9 @@ int64_t device_last_exact(const Device* d) { return d ? d->last_exact : 0; }
 void device_release(Device* d) {
     if (!d) return;
     (void)hipSetDevice(d->ordinal);
+    (void)hipDeviceSynchronize();                    // uncollected runs are dropped
+    for (auto& sl : d->slot) sl.busy = false;
+    d->n_collected = d->n_submitted;
     (void)hipFree(d->d_slots); d->d_slots = nullptr;
     (void)hipFree(d->d_pile); d->d_pile = nullptr;
     (void)hipFree(d->d_reads); d->d_reads = nullptr;
@@ -1367,8 +1399,14 @@ void device_release(Device* d) {
 void device_destroy(Device* d) {
     if (!d) return;
     device_release(d);
+    (void)hipDeviceSynchronize();
     (void)hipFree(d->d_sites);
     (void)hipFree(d->d_sorted);
+    for (auto& sl : d->slot) {
+        (void)hipFree(sl.d_sorted);
+        (void)hipHostFree(sl.h_ctr);
+        for (auto& e : sl.ev) (void)hipEventDestroy(e);
+    }
     (void)hipFree(d->d_keys);
     (void)hipFree(d->d_psites);
     (void)hipFree(d->d_pcalls);
@@ -1379,6 +1417,7 @@ void device_destroy(Device* d) {
     (void)hipHostFree(d->h_counters);
     for (auto& e : d->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(d->stream);
+    (void)hipStreamDestroy(d->copy_stream);
     delete d;
 }
 
@@ -1436,156 +1475,201 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
     return 0;
 }
 
-int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypeParams& g, int prune,
-               SiteStore* out, int64_t* n_out, double* scan_ms, double* geno_ms, double* total_ms,
-               int64_t* n_candidates, std::string& err) {
-    HIP_TRY(hipSetDevice(d->ordinal));
-    auto t0 = std::chrono::steady_clock::now();
-    // output capacity: calls are rare; dump mode needs one record per covered position
-    int64_t want = g.dump_all ? std::max<int64_t>(s.covered + 1024, 1024) : std::max<int64_t>(s.g_len / 256 + 4096, 4096);
-    if (want > d->cap_sites) {
+// ------------------------------------------------------------------------------------------
+// single-sample runs: submit (kernels + D2H enqueued) and collect (wait, finish) so that a run's
+// copies and host post-processing overlap the next run's kernels.  Two result slots; slot s owns
+// its ordered-record buffer, its counter set and a pinned host store.  Compute stream: [wait slot
+// free] KT KP KO; copy stream: [wait KO] D2H counters + records, clear the counter set.
+// ------------------------------------------------------------------------------------------
+static int grow_shared(Device* d, int64_t sites, int64_t queue, std::string& err) {
+    if (sites > d->cap_sites) {
         (void)hipFree(d->d_sites);
-        (void)hipFree(d->d_sorted);
         (void)hipFree(d->d_keys);
-        HIP_TRY(hipMalloc(&d->d_sites, (size_t)want * sizeof(ngsep_site_out)));
-        HIP_TRY(hipMalloc(&d->d_sorted, (size_t)want * sizeof(ngsep_site_out)));
-        HIP_TRY(hipMalloc(&d->d_keys, (size_t)want * 2 * sizeof(unsigned long long)));
-        d->cap_sites = want;
+        d->d_sites = nullptr;
+        d->d_keys = nullptr;
+        HIP_TRY(hipMalloc(&d->d_sites, (size_t)sites * sizeof(ngsep_site_out)));
+        HIP_TRY(hipMalloc(&d->d_keys, (size_t)sites * 2 * sizeof(unsigned long long)));
+        d->cap_sites = sites;
     }
-    // position buckets of the ordering pass: a few records each (calls are sparse; dump mode has one
-    // record per covered position)
+    if (queue > d->cap_hard) {
+        (void)hipFree(d->d_hard);
+        d->d_hard = nullptr;
+        HIP_TRY(hipMalloc(&d->d_hard, (size_t)queue * sizeof(QueueSite)));
+        d->cap_hard = queue;
+    }
+    return 0;
+}
+
+// enqueues one run into slot sl (kernels on the compute stream, copies on the copy stream)
+static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables& t, const GenotypeParams& g, int prune,
+                       bool idle, std::string& err) {
+    // capacities (shared buffers only change while nothing runs): calls are rare; dump mode needs one
+    // record per covered position
+    const int64_t want = g.dump_all ? std::max<int64_t>(s.covered + 1024, 1024) : std::max<int64_t>(s.g_len / 256 + 4096, 4096);
+    const int64_t qwant = g.dump_all ? std::max<int64_t>(s.covered + 1024, 1024) : std::max<int64_t>(s.g_len / 64 + 65536, 65536);
+    if (want > d->cap_sites || qwant > d->cap_hard) {
+        if (!idle) HIP_TRY(hipDeviceSynchronize());
+        if (grow_shared(d, want, qwant, err) != 0) return -1;
+    }
+    if (sl.cap < d->cap_sites) {
+        HIP_TRY(hipEventSynchronize(sl.ev[4]));
+        (void)hipFree(sl.d_sorted);
+        sl.d_sorted = nullptr;
+        HIP_TRY(hipMalloc(&sl.d_sorted, (size_t)d->cap_sites * sizeof(ngsep_site_out)));
+        sl.cap = d->cap_sites;
+    }
+    // position buckets of the ordering pass: a few records each
     const int shift = g.dump_all ? 4 : 12;
     const int64_t nb = (s.g_len >> shift) + 1;
     if (nb > d->nb_cap) {
+        if (!idle) HIP_TRY(hipDeviceSynchronize());
         (void)hipFree(d->d_bucket);
         HIP_TRY(hipMalloc(&d->d_bucket, (size_t)(3 * nb + 1) * sizeof(int32_t)));
         d->nb_cap = nb;
         d->nb_clean = 0;
     }
-    unsigned long long* ctr = d->d_counters + 4 * d->cpar;
-    unsigned long long* ctr_next = d->d_counters + 4 * (1 - d->cpar);
-    // queue of candidates the tile kernel could not prove hom-ref; dump mode: every position
-    int64_t qwant = g.dump_all ? std::max<int64_t>(s.covered + 1024, 1024) : std::max<int64_t>(s.g_len / 64 + 65536, 65536);
-    if (qwant < d->cap_hard) qwant = d->cap_hard;
-    {
-        if (qwant > d->cap_hard) {
-            (void)hipFree(d->d_hard);
-            HIP_TRY(hipMalloc(&d->d_hard, (size_t)qwant * sizeof(QueueSite)));
-            d->cap_hard = qwant;
-        }
-        // fixed per-run costs kept off the stream: the tables are uploaded only when they change, the
-        // counters alternate between two sets (the last kernel of a run zeroes the other set) and the
-        // bucket counts are zeroed by the ordering pass that consumed them
-        if (!d->tables_valid || std::memcmp(&d->h_tables, &t, sizeof(LikTables)) != 0) {
-            d->h_tables = t;
-            HIP_TRY(hipMemcpyAsync(d->d_tables, &d->h_tables, sizeof(LikTables), hipMemcpyHostToDevice, d->stream));
-            d->tables_valid = true;
-        }
-        HIP_TRY(hipEventRecord(d->ev[0], d->stream));
-        if (d->n_tiles > 0) {
-            // persistent waves: as many workgroups as are co-resident (register-limited), each wave
-            // walks the tiles with a grid stride, so at any moment the waves stream one contiguous
-            // stretch of the pile
-            auto kt = prune ? (const void*)k_tile_pileup<0> : (const void*)k_tile_pileup<1>;
-            int& per_cu = d->kt_blocks_per_cu[prune ? 0 : 1];
-            if (per_cu == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kt, kScanThreads, 0) != hipSuccess || per_cu < 1)) per_cu = 2;
-            int bpc = per_cu;
-            if (const char* e = std::getenv("NGSEP_BLOCKS_PER_CU")) bpc = std::max(1, std::atoi(e));   // tuning
-            const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((d->n_tiles + kScanWaves - 1) / kScanWaves, (int64_t)d->n_cu * bpc));
-            dim3 grid((unsigned)nblk);
-            if (prune)
-                hipLaunchKernelGGL(k_tile_pileup<0>, grid, dim3(kScanThreads), 0, d->stream, (const u32x4*)d->d_pile,
-                                   d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, d->d_tables, g, d->d_hard,
-                                   ctr, d->cap_hard);
-            else
-                hipLaunchKernelGGL(k_tile_pileup<1>, grid, dim3(kScanThreads), 0, d->stream, (const u32x4*)d->d_pile,
-                                   d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, d->d_tables, g, d->d_hard,
-                                   ctr, d->cap_hard);
-            HIP_TRY(hipGetLastError());
-        }
-        HIP_TRY(hipEventRecord(d->ev[1], d->stream));
-        hipLaunchKernelGGL(k_posterior, dim3(2048), dim3(kPostWaves * 64), 0, d->stream, d->d_hard, ctr + 2, d->cap_hard,
-                           d->d_reads, d->n_reads, d->d_lb, d->d_slots, d->slot_size, d->d_tables, g, d->d_sites,
-                           ctr, d->cap_sites);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(d->ev[2], d->stream));   // queue overflow is checked after the copy below
-        // order the records by position on the device
-        int32_t* cnt = d->d_bucket;
-        int32_t* start = d->d_bucket + nb;
-        int32_t* cursor = d->d_bucket + 2 * nb + 1;
-        if (nb > d->nb_clean) HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)nb * sizeof(int32_t), d->stream));
-        hipLaunchKernelGGL(ko_hist, dim3(256), dim3(256), 0, d->stream, d->d_sites, ctr, d->cap_sites, cnt, shift);
-        hipLaunchKernelGGL(ko_scan, dim3(1), dim3(1024), 0, d->stream, cnt, start, cursor, nb);
-        hipLaunchKernelGGL(ko_scatter, dim3(256), dim3(256), 0, d->stream, d->d_sites, ctr, d->cap_sites, cursor,
-                           d->d_keys, shift);
-        unsigned long long* skeys = d->d_keys + d->cap_sites;    // second half: keys in position order
-        hipLaunchKernelGGL(ko_bucket_sort, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, d->stream, d->d_keys, skeys, start, cnt, nb);
-        d->nb_clean = std::max(d->nb_clean, nb);
-        hipLaunchKernelGGL(ko_gather, dim3(1024), dim3(256), 0, d->stream, d->d_sites, skeys, ctr, d->cap_sites,
-                           d->d_sorted, ctr_next);
+    unsigned long long* ctr = sl.d_ctr;
+    sl.t0 = std::chrono::steady_clock::now();
+    // the slot's previous copies (and the reset of its counter set) are done before it is reused
+    HIP_TRY(hipStreamWaitEvent(d->stream, sl.ev[4], 0));
+    if (!d->tables_valid || std::memcmp(&d->h_tables, &t, sizeof(LikTables)) != 0) {
+        HIP_TRY(hipStreamSynchronize(d->stream));     // the previous upload may still read h_tables
+        d->h_tables = t;
+        HIP_TRY(hipMemcpyAsync(d->d_tables, &d->h_tables, sizeof(LikTables), hipMemcpyHostToDevice, d->stream));
+        d->tables_valid = true;
+    }
+    HIP_TRY(hipEventRecord(sl.ev[0], d->stream));
+    if (d->n_tiles > 0) {
+        // persistent waves: as many workgroups as are co-resident (register-limited), each wave
+        // walks the tiles with a grid stride, so at any moment the waves stream one contiguous
+        // stretch of the pile
+        auto kt = prune ? (const void*)k_tile_pileup<0> : (const void*)k_tile_pileup<1>;
+        int& per_cu = d->kt_blocks_per_cu[prune ? 0 : 1];
+        if (per_cu == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kt, kScanThreads, 0) != hipSuccess || per_cu < 1)) per_cu = 2;
+        int bpc = per_cu;
+        if (const char* e = std::getenv("NGSEP_BLOCKS_PER_CU")) bpc = std::max(1, std::atoi(e));   // tuning
+        const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((d->n_tiles + kScanWaves - 1) / kScanWaves, (int64_t)d->n_cu * bpc));
+        dim3 grid((unsigned)nblk);
+        if (prune)
+            hipLaunchKernelGGL(k_tile_pileup<0>, grid, dim3(kScanThreads), 0, d->stream, (const u32x4*)d->d_pile,
+                               d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, d->d_tables, g, d->d_hard, ctr, d->cap_hard);
+        else
+            hipLaunchKernelGGL(k_tile_pileup<1>, grid, dim3(kScanThreads), 0, d->stream, (const u32x4*)d->d_pile,
+                               d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, d->d_tables, g, d->d_hard, ctr, d->cap_hard);
         HIP_TRY(hipGetLastError());
     }
-    // counters and a prefix of the ordered records in one round trip, straight into the result store
-    const size_t from = out->size();
-    const int64_t guess = std::min<int64_t>(d->cap_sites, d->last_n_sites + d->last_n_sites / 64 + 64);
-    out->reserve(from + (size_t)guess);
-    HIP_TRY(hipMemcpyAsync(d->h_counters, ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, d->stream));
-    HIP_TRY(hipMemcpyAsync(out->buf + from, d->d_sorted, (size_t)guess * sizeof(ngsep_site_out), hipMemcpyDeviceToHost, d->stream));
-    auto tq = std::chrono::steady_clock::now();
-    HIP_TRY(hipStreamSynchronize(d->stream));
-    auto ts = std::chrono::steady_clock::now();
-    d->cpar = 1 - d->cpar;              // ko_gather zeroed the other counter set for the next run
-    const int64_t n = (int64_t)d->h_counters[0];
-    if (n > d->cap_sites) {
-        // more calls than the record buffer holds (e.g. -minQuality 0): grow it and run again
-        (void)hipFree(d->d_sites);
-        (void)hipFree(d->d_sorted);
-        (void)hipFree(d->d_keys);
-        d->d_sites = d->d_sorted = nullptr;
-        d->d_keys = nullptr;
-        d->cap_sites = 0;
-        HIP_TRY(hipMalloc(&d->d_sites, (size_t)(n + 1024) * sizeof(ngsep_site_out)));
-        HIP_TRY(hipMalloc(&d->d_sorted, (size_t)(n + 1024) * sizeof(ngsep_site_out)));
-        HIP_TRY(hipMalloc(&d->d_keys, (size_t)(n + 1024) * 2 * sizeof(unsigned long long)));
-        d->cap_sites = n + 1024;
+    HIP_TRY(hipEventRecord(sl.ev[1], d->stream));
+    hipLaunchKernelGGL(k_posterior, dim3(2048), dim3(kPostWaves * 64), 0, d->stream, d->d_hard, ctr + 2, d->cap_hard,
+                       d->d_reads, d->n_reads, d->d_lb, d->d_slots, d->slot_size, d->d_tables, g, d->d_sites, ctr,
+                       d->cap_sites);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(sl.ev[2], d->stream));
+    // order the records by position on the device
+    int32_t* cnt = d->d_bucket;
+    int32_t* start = d->d_bucket + nb;
+    int32_t* cursor = d->d_bucket + 2 * nb + 1;
+    if (nb > d->nb_clean) HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)nb * sizeof(int32_t), d->stream));
+    hipLaunchKernelGGL(ko_hist, dim3(256), dim3(256), 0, d->stream, d->d_sites, ctr, d->cap_sites, cnt, shift);
+    hipLaunchKernelGGL(ko_scan, dim3(1), dim3(1024), 0, d->stream, cnt, start, cursor, nb);
+    hipLaunchKernelGGL(ko_scatter, dim3(256), dim3(256), 0, d->stream, d->d_sites, ctr, d->cap_sites, cursor, d->d_keys, shift);
+    unsigned long long* skeys = d->d_keys + d->cap_sites;    // second half: keys in position order
+    hipLaunchKernelGGL(ko_bucket_sort, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, d->stream, d->d_keys, skeys, start, cnt, nb);
+    d->nb_clean = std::max(d->nb_clean, nb);
+    hipLaunchKernelGGL(ko_gather, dim3(1024), dim3(256), 0, d->stream, d->d_sites, skeys, ctr, d->cap_sites, sl.d_sorted);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(sl.ev[3], d->stream));
+    // copies: counters and a prefix of the ordered records (sized from the previous run) straight into
+    // the slot's pinned store, then the counter set is cleared for the slot's next run
+    sl.guess = std::min<int64_t>(d->cap_sites, d->last_n_sites + d->last_n_sites / 64 + 64);
+    sl.host.reserve((size_t)sl.guess);
+    HIP_TRY(hipStreamWaitEvent(d->copy_stream, sl.ev[3], 0));
+    HIP_TRY(hipMemcpyAsync(sl.h_ctr, ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, d->copy_stream));
+    HIP_TRY(hipMemcpyAsync(sl.host.buf, sl.d_sorted, (size_t)sl.guess * sizeof(ngsep_site_out), hipMemcpyDeviceToHost, d->copy_stream));
+    HIP_TRY(hipMemsetAsync(ctr, 0, 4 * sizeof(unsigned long long), d->copy_stream));
+    HIP_TRY(hipEventRecord(sl.ev[4], d->copy_stream));
+    sl.g = g;
+    sl.prune = prune;
+    sl.tabs = t;
+    sl.staged = &s;
+    return 0;
+}
+
+int device_submit(Device* d, const Staged& s, const LikTables& t, const GenotypeParams& g, int prune, std::string& err) {
+    HIP_TRY(hipSetDevice(d->ordinal));
+    RunSlot& sl = d->slot[d->n_submitted % 2];
+    if (sl.busy) { err = "both result slots hold uncollected runs"; return -1; }
+    if (enqueue_run(d, sl, s, t, g, prune, d->n_submitted == d->n_collected, err) != 0) return -1;
+    sl.busy = true;
+    d->n_submitted++;
+    return 0;
+}
+
+// waits for the oldest submitted run and moves its position-ordered records into out (appended at
+// out->size(); swapped in when out is empty).  Returns 1 when the run overflowed a buffer: the
+// buffers have been grown and the caller runs it again.
+int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, double* geno_ms, double* total_ms,
+                   int64_t* n_candidates, std::string& err) {
+    HIP_TRY(hipSetDevice(d->ordinal));
+    if (d->n_collected == d->n_submitted) { err = "no run to collect"; return -1; }
+    RunSlot& sl = d->slot[d->n_collected % 2];
+    HIP_TRY(hipEventSynchronize(sl.ev[4]));
+    int64_t n = (int64_t)sl.h_ctr[0];
+    int64_t q = (int64_t)sl.h_ctr[2];
+    for (int attempt = 0; n > d->cap_sites || q > d->cap_hard; attempt++) {
+        // more calls or undecided candidates than the buffers hold (e.g. -minQuality 0): drain, grow
+        // and run this slot again in place (a later run in the other slot keeps its own results)
+        if (attempt == 3) { err = "result buffers kept overflowing"; return -1; }
+        HIP_TRY(hipDeviceSynchronize());
+        if (grow_shared(d, std::max(d->cap_sites, n + 1024), std::max(d->cap_hard, q + 1024), err) != 0) return -1;
         d->last_n_sites = n;
-        return device_run(d, s, t, g, prune, out, n_out, scan_ms, geno_ms, total_ms, n_candidates, err);
+        if (enqueue_run(d, sl, *sl.staged, sl.tabs, sl.g, sl.prune, true, err) != 0) return -1;
+        HIP_TRY(hipEventSynchronize(sl.ev[4]));
+        n = (int64_t)sl.h_ctr[0];
+        q = (int64_t)sl.h_ctr[2];
     }
-    if ((int64_t)d->h_counters[2] > d->cap_hard) {
-        // rare: more undecided candidates than the queue holds -> grow it and run again
-        (void)hipFree(d->d_hard);
-        d->d_hard = nullptr;
-        HIP_TRY(hipMalloc(&d->d_hard, (size_t)(d->h_counters[2] + 1024) * sizeof(QueueSite)));
-        d->cap_hard = (int64_t)d->h_counters[2] + 1024;
-        d->last_n_sites = n;
-        return device_run(d, s, t, g, prune, out, n_out, scan_ms, geno_ms, total_ms, n_candidates, err);
+    sl.busy = false;
+    d->n_collected++;
+    if (n > sl.guess) {
+        sl.host.n = (size_t)sl.guess;                 // keep the records already copied when the store grows
+        sl.host.reserve((size_t)n);
+        HIP_TRY(hipMemcpy(sl.host.buf + sl.guess, sl.d_sorted + sl.guess, (size_t)(n - sl.guess) * sizeof(ngsep_site_out),
+                          hipMemcpyDeviceToHost));
     }
-    if (n > guess) {
-        out->n = from + (size_t)guess;      // keep the records already copied when the store grows
-        out->reserve(from + (size_t)n);
-        HIP_TRY(hipMemcpyAsync(out->buf + from + guess, d->d_sorted + guess, (size_t)(n - guess) * sizeof(ngsep_site_out),
-                               hipMemcpyDeviceToHost, d->stream));
-        HIP_TRY(hipStreamSynchronize(d->stream));
-    }
+    sl.host.n = (size_t)n;
     d->last_n_sites = n;
-    out->n = from + (size_t)n;
-    *n_out = n;
-    auto t1 = std::chrono::steady_clock::now();
-    float a = 0, a2 = 0;
-    (void)hipEventElapsedTime(&a, d->ev[0], d->ev[1]);
-    (void)hipEventElapsedTime(&a2, d->ev[1], d->ev[2]);
-    if (std::getenv("NGSEP_TIMING")) {
-        auto us = [](auto x, auto y) { return std::chrono::duration<double, std::micro>(y - x).count(); };
-        std::fprintf(stderr, "[ngsep timing] enqueue %.1f us, sync %.1f us, rest %.1f us, tile %.1f us, posterior %.1f us, n=%lld guess=%lld\n",
-                     us(t0, tq), us(tq, ts), us(ts, t1), a * 1000.0, a2 * 1000.0, (long long)n, (long long)guess);
+    if (out->size() == 0) out->swap(sl.host);
+    else {
+        const size_t from = out->size();
+        out->reserve(from + (size_t)n);
+        std::memcpy(out->buf + from, sl.host.buf, (size_t)n * sizeof(ngsep_site_out));
+        out->n = from + (size_t)n;
     }
+    sl.host.n = 0;
+    *n_out = n;
+    float a = 0, a2 = 0;
+    (void)hipEventElapsedTime(&a, sl.ev[0], sl.ev[1]);
+    (void)hipEventElapsedTime(&a2, sl.ev[1], sl.ev[2]);
     *scan_ms = a;
     *geno_ms = a2;
-    *total_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-    *n_candidates = (int64_t)d->h_counters[1];
-    d->last_hard = (int64_t)d->h_counters[2];
-    d->last_exact = (int64_t)d->h_counters[3];
+    *total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - sl.t0).count();
+    *n_candidates = (int64_t)sl.h_ctr[1];
+    d->last_hard = q;
+    d->last_exact = (int64_t)sl.h_ctr[3];
     return 0;
+}
+
+int64_t device_inflight(const Device* d) { return d ? d->n_submitted - d->n_collected : 0; }
+
+int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypeParams& g, int prune,
+               SiteStore* out, int64_t* n_out, double* scan_ms, double* geno_ms, double* total_ms,
+               int64_t* n_candidates, std::string& err) {
+    while (d->n_collected < d->n_submitted) {        // finish anything asynchronous first (results dropped)
+        SiteStore drop;
+        int64_t nn = 0; double a = 0, b = 0, c2 = 0; int64_t nc = 0;
+        if (device_collect(d, &drop, &nn, &a, &b, &c2, &nc, err) != 0) return -1;
+    }
+    if (device_submit(d, s, t, g, prune, err) != 0) return -1;
+    return device_collect(d, out, n_out, scan_ms, geno_ms, total_ms, n_candidates, err);
 }
 
 // MultisampleVariantsDetector run: KTM over every resident tile, KPM over the queued positions,
@@ -1624,7 +1708,7 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
         HIP_TRY(hipMemcpyAsync(d->d_tables, &d->h_tables, sizeof(LikTables), hipMemcpyHostToDevice, d->stream));
         d->tables_valid = true;
     }
-    unsigned long long* ctr = d->d_counters + 4 * d->cpar;
+    unsigned long long* ctr = d->d_counters;
     HIP_TRY(hipMemsetAsync(ctr, 0, 4 * sizeof(unsigned long long), d->stream));
     HIP_TRY(hipEventRecord(d->ev[0], d->stream));
     if (d->n_tiles > 0) {

@@ -148,6 +148,14 @@ class GpuPileupSession:
         self._check(self._lib.ngsep_run_staged(self._ctx, ctypes.byref(ms)))
         return ms.value
 
+    def submit_staged(self):
+        self._check(self._lib.ngsep_submit_staged(self._ctx))
+
+    def collect_staged(self) -> float:
+        ms = ctypes.c_double()
+        self._check(self._lib.ngsep_collect_staged(self._ctx, ctypes.byref(ms)))
+        return ms.value
+
     def release_staged(self):
         self._check(self._lib.ngsep_release_staged(self._ctx))
 

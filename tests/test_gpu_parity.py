@@ -170,3 +170,26 @@ def test_staged_run_repeatable(tmp_path):
             runs.append([(x.sequence, x.pos, x.gq) for x in s.getCalledVariants()])
         s.release_staged()
     assert runs[0] == runs[1] == runs[2] and len(runs[0]) > 100
+
+
+def test_async_passes_identical(tmp_path):
+    """ngsep_submit_staged / ngsep_collect_staged (two passes in flight) give every pass the same
+    calls as a synchronous run, including when the first pass's record estimate is too small."""
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=2, depth=20, seed=4, quality_model=2, snv_rate=3e-3)
+    with GpuPileupSession(gpu_params(min_quality=0)) as s:
+        for name, seq in syn.contigs():
+            s.set_reference(name, seq)
+        s.stage(syn.batch())
+        s.stage_finish()
+        s.run_staged()
+        ref = [(x.sequence, x.pos, x.gq, x.qual, tuple(x.logc)) for x in s.getCalledVariants()]
+        got = []
+        s.submit_staged()
+        for k in range(5):
+            if k + 1 < 5:
+                s.submit_staged()
+            s.collect_staged()
+            got.append([(x.sequence, x.pos, x.gq, x.qual, tuple(x.logc)) for x in s.getCalledVariants()])
+    assert len(ref) > 1000
+    for g in got:
+        assert g == ref
