@@ -208,6 +208,7 @@ def main():
         steps = args.steps
         value = total_positions * steps / elapsed
         k_avg_ms = sum(scan_ms) / len(scan_ms)
+        post_avg_ms = (sum(geno_ms) / len(geno_ms)) if max(geno_ms, default=0) > 0 else None
         # algorithmic bytes per k_tile_pileup launch: 1 B per projected read base,
         # 1 B reference per genotyped position, 16 B read header per admitted read
         alg_bytes = st.read_bases + positions + 16 * st.alignments_admitted
@@ -250,9 +251,10 @@ def main():
                 "traffic": traffic,
                 "alg_bytes_per_launch": alg_bytes,
                 "kernel_avg_ms": k_avg_ms,
-                "posterior_kernel_avg_ms": sum(geno_ms) / len(geno_ms),
+                # KP is timed only with NGSEP_TIME_POSTERIOR=1 (its event costs ~7 us of pipeline gap)
+                "posterior_kernel_avg_ms": post_avg_ms,
             },
-            "kernel_positions_per_s": total_positions / ((k_avg_ms + sum(geno_ms) / len(geno_ms)) * 1e-3),
+            "kernel_positions_per_s": (total_positions / ((k_avg_ms + post_avg_ms) * 1e-3)) if post_avg_ms else None,
         }
         if multi:
             line["config"]["samples"] = args.samples

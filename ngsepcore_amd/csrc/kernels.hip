@@ -66,6 +66,9 @@ struct Device {
     hipStream_t copy_stream = nullptr;
     RunSlot slot[2];
     int64_t n_submitted = 0, n_collected = 0;
+    // an event between KP and KO costs a few microseconds of idle GPU per pass: recorded only when
+    // the posterior kernel's duration is asked for (NGSEP_TIME_POSTERIOR, diagnostics)
+    bool time_posterior = std::getenv("NGSEP_TIME_POSTERIOR") != nullptr;
     hipEvent_t ev[4] = {};
     uint8_t* d_slots = nullptr;
     uint8_t* d_pile = nullptr;
@@ -87,11 +90,10 @@ struct Device {
     int64_t cap_psites = 0;
     unsigned long long* d_stamps = nullptr;   // diagnostics (NGSEP_TIMING)
     LikTables* d_tables = nullptr;
-    ngsep_site_out* d_sites = nullptr;
-    ngsep_site_out* d_sorted = nullptr;
-    unsigned long long* d_keys = nullptr;   // ordering keys (position << 32 | record): 2 x cap_sites
-    int32_t* d_bucket = nullptr;     // counts, then starts (nb+1), then cursors (nb)
-    int64_t nb_cap = 0;
+    ngsep_site_out* d_brec = nullptr;  // KP's records by position bucket: bucket b = d_brec[b * bcap ..]
+    int32_t* d_bcount = nullptr;       // records per bucket (zeroed by KT)
+    int64_t nb_cap = 0, brec_cap = 0;
+    int32_t ko_shift = 12, ko_bcap = 64;   // 2^ko_shift positions per bucket (grown on overflow)
     QueueSite* d_hard = nullptr;
     int64_t cap_hard = 0;
     unsigned long long* d_counters = nullptr;
@@ -102,8 +104,6 @@ struct Device {
     int64_t last_n_sites = 1024;
     int64_t last_hard = 0;
     int64_t last_exact = 0;     // wave passes of KT's exact integer bound in the last run
-    int cpar = 0;               // counter set (of two) the next run uses
-    int64_t nb_clean = 0;       // bucket counts known to be zero
     int kt_blocks_per_cu[2] = {0, 0};
     LikTables h_tables;         // last uploaded tables (pinned copy source)
     bool tables_valid = false;
@@ -159,7 +159,7 @@ static_assert(sizeof(QueueSite) == 8, "QueueSite layout");
 // (SingleSampleVariantPileupListener.java:213-232).
 // The 64 lanes fetch 64 consecutive reads' codes at once (the memory round trips are what a site
 // costs); integer counts come from ballots, and the fp64 sums are then added in lane (= read) order,
-// wave-uniformly.  Emitted records are staged in LDS and reserved once per workgroup.
+// wave-uniformly.  Lane 0 appends each emitted record to the bucket of its position (KO orders them).
 __device__ __forceinline__ double readlane_d(double v, int l) {
     const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
@@ -168,36 +168,13 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 }
 
 constexpr int kPostWaves = 4;
-constexpr int kPostStage = 8;           // records staged per wave
-
-__device__ __forceinline__ void post_flush(ngsep_site_out* rec, int32_t n, int lane, ngsep_site_out* __restrict__ out,
-                                           unsigned long long* counters, int64_t cap) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    unsigned long long base = 0;
-    if (lane == 0) base = atomicAdd(&counters[0], (unsigned long long)n);
-    base = __shfl(base, 0, 64);
-    constexpr int W = sizeof(ngsep_site_out) / 4;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(rec);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(out);
-    for (int k = lane; k < n * W; k += 64)
-        if ((int64_t)base + k / W < cap) dst[(base * W) + k] = src[k];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* __restrict__ queue, const unsigned long long* qn,
                                                    int64_t qcap, const int4* __restrict__ reads, int64_t n_reads,
                                                    const int32_t* __restrict__ lb, const uint8_t* __restrict__ slots,
                                                    int32_t S, const LikTables* __restrict__ tabs, GenotypeParams gp,
-                                                   ngsep_site_out* __restrict__ out, unsigned long long* counters,
-                                                   int64_t cap) {
+                                                   ngsep_site_out* __restrict__ brec, int32_t* __restrict__ bcount,
+                                                   int shift, int32_t bcap) {
     __shared__ double s_t[3][32];
-    __shared__ ngsep_site_out s_rec[kPostWaves][kPostStage];
-    __shared__ int32_t s_n[kPostWaves];
-    __shared__ unsigned long long s_base;
     if (threadIdx.x < 96)
         s_t[threadIdx.x >> 5][threadIdx.x & 31] =
             (threadIdx.x < 32 ? tabs->A : threadIdx.x < 64 ? tabs->H : tabs->E)[threadIdx.x & 31];
@@ -206,7 +183,6 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int64_t n = (int64_t)*qn;
     if (n > qcap) n = qcap;
-    int32_t ns = 0;                                   // records staged by this wave (uniform)
     const int64_t nwaves = (int64_t)gridDim.x * kPostWaves;
     for (int64_t i = (int64_t)blockIdx.x * kPostWaves + wv; i < n; i += nwaves) {
         const QueueSite qs = queue[i];
@@ -330,9 +306,9 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
             if (keep && gp.min_quality > gq) keep = false;
         }
         if (!keep && !gp.dump_all) continue;
-        if (ns == kPostStage) { post_flush(s_rec[wv], ns, lane, out, counters, cap); ns = 0; }
+        // the record goes to its position bucket (KO orders each bucket; no global reservation)
         if (lane == 0) {
-            ngsep_site_out& o = s_rec[wv][ns];
+            ngsep_site_out o;
             o.seq_id = -1;
             o.pos = gpos;
             o.ref = callable ? "ACGT"[(rc >> 5) & 3] : 'N';
@@ -353,25 +329,11 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
             }
             o.logc[0] = L00; o.logc[1] = L01; o.logc[2] = L02; o.logc[3] = L03; o.logc[4] = L11;
             o.logc[5] = L12; o.logc[6] = L13; o.logc[7] = L22; o.logc[8] = L23; o.logc[9] = L33;
+            const int32_t b = gpos >> shift;
+            const int32_t k = atomicAdd(&bcount[b], 1);
+            if (k < bcap) brec[(int64_t)b * bcap + k] = o;
         }
-        ns++;
     }
-    // one reservation per workgroup for the staged records
-    if (lane == 0) s_n[wv] = ns;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long tot = 0;
-        for (int w = 0; w < kPostWaves; w++) tot += (unsigned long long)s_n[w];
-        s_base = tot ? atomicAdd(&counters[0], tot) : 0ull;
-    }
-    __syncthreads();
-    unsigned long long base = s_base;
-    for (int w = 0; w < wv; w++) base += (unsigned long long)s_n[w];
-    constexpr int W = sizeof(ngsep_site_out) / 4;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(s_rec[wv]);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(out);
-    for (int k = lane; k < ns * W; k += 64)
-        if ((int64_t)base + k / W < cap) dst[(base * W) + k] = src[k];
 }
 
 
@@ -455,10 +417,13 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(NG
 void k_tile_pileup(
     const u32x4* __restrict__ pile, const TileInfo* __restrict__ tinfo, const uint8_t* __restrict__ ref,
     int32_t log2T, int64_t n_tiles, const LikTables* __restrict__ tabs, GenotypeParams gp,
-    QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap) {
+    QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap,
+    int32_t* __restrict__ bcount, int64_t nb) {
     __shared__ ScanShared sh;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // KP's position buckets start empty (KT precedes KP on the stream)
+    for (int64_t i = (int64_t)blockIdx.x * kScanThreads + threadIdx.x; i < nb; i += (int64_t)gridDim.x * kScanThreads) bcount[i] = 0;
     if (threadIdx.x < 64) sh.w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
     __syncthreads();
     const int log2U = log2T - 4;
@@ -1225,87 +1190,80 @@ __global__ __launch_bounds__(256) void kl_read_index(const int4* __restrict__ re
 }
 
 // ------------------------------------------------------------------------------------------
-// KO: order the emitted records by global position: counting sort of (position, record) keys on
-//     2^shift-position buckets, insertion sort inside a bucket (a handful of keys each), then one
-//     coalesced gather of the records in key order
+// KO: order the emitted records by global position.  KP appended every record to the bucket of its
+//     position (2^shift positions per bucket, bcap records each); one workgroup per kKofBuckets
+//     buckets sums the counts of the earlier buckets (its output offset), each wave ranks a
+//     bucket's keys and copies the records in order.  One kernel, no atomics, no global scan.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void ko_hist(const ngsep_site_out* __restrict__ recs, const unsigned long long* n_ptr,
-                                               int64_t cap, int32_t* __restrict__ bucket, int shift) {
-    int64_t n = (int64_t)*n_ptr;
-    if (n > cap) n = cap;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        atomicAdd(&bucket[recs[i].pos >> shift], 1);
-}
-// exclusive scan of nb bucket counts into start[0..nb] (one workgroup of 1024)
-__global__ __launch_bounds__(1024) void ko_scan(const int32_t* __restrict__ bucket, int32_t* __restrict__ start,
-                                                int32_t* __restrict__ cursor, int64_t nb) {
-    __shared__ int32_t s_part[1024];
-    const int tid = threadIdx.x;
-    const int64_t per = (nb + 1023) / 1024;
-    const int64_t b0 = tid * per, b1 = b0 + per < nb ? b0 + per : nb;
-    int32_t sum = 0;
-    for (int64_t b = b0; b < b1; b++) sum += bucket[b];
-    s_part[tid] = sum;
+constexpr int kKofBuckets = 16;
+__global__ __launch_bounds__(256) void ko_fused(const ngsep_site_out* __restrict__ brec, const int32_t* __restrict__ bcount,
+                                                int64_t nb, int32_t bcap, ngsep_site_out* __restrict__ sorted, int64_t cap,
+                                                unsigned long long* counters) {
+    __shared__ int32_t s_red[4], s_mx[4];
+    __shared__ int32_t s_cnt[kKofBuckets], s_off[kKofBuckets];
+    __shared__ unsigned long long s_keys[4][1024];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t b0 = (int64_t)blockIdx.x * kKofBuckets;
+    // offset of this block's records: the records of every earlier bucket (block 0: all, for the total)
+    const bool all = blockIdx.x == 0;
+    const int64_t lim = all ? nb : b0;
+    int32_t part = 0, mx = 0;
+    for (int64_t b = tid; b < lim; b += 256) {
+        const int32_t c = bcount[b];
+        part += all || c < bcap ? c : bcap;
+        mx = c > mx ? c : mx;
+    }
+    for (int o = 32; o > 0; o >>= 1) { part += __shfl_xor(part, o, 64); const int32_t m2 = __shfl_xor(mx, o, 64); mx = m2 > mx ? m2 : mx; }
+    if (lane == 0) { s_red[wv] = part; s_mx[wv] = mx; }
+    if (tid < kKofBuckets) s_cnt[tid] = b0 + tid < nb ? (bcount[b0 + tid] < bcap ? bcount[b0 + tid] : bcap) : 0;
     __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        const int32_t v = tid >= o ? s_part[tid - o] : 0;
-        __syncthreads();
-        s_part[tid] += v;
-        __syncthreads();
+    const int64_t total_before = (int64_t)s_red[0] + s_red[1] + s_red[2] + s_red[3];
+    if (tid == 0) {
+        int32_t acc = 0;
+        for (int j = 0; j < kKofBuckets; j++) { s_off[j] = acc; acc += s_cnt[j]; }
+        if (all) {
+            // every record KP emitted (block 0 summed all buckets) and the fullest bucket: above bcap the
+            // host grows the buckets and runs again
+            const int32_t m = max(max(s_mx[0], s_mx[1]), max(s_mx[2], s_mx[3]));
+            counters[0] = (unsigned long long)total_before | ((unsigned long long)m << 40);
+        }
     }
-    int32_t acc = s_part[tid] - sum;
-    for (int64_t b = b0; b < b1; b++) { start[b] = acc; cursor[b] = acc; acc += bucket[b]; }
-    if (tid == 1023) start[nb] = s_part[1023];
-}
-__global__ __launch_bounds__(256) void ko_scatter(const ngsep_site_out* __restrict__ recs, const unsigned long long* n_ptr,
-                                                  int64_t cap, int32_t* __restrict__ cursor,
-                                                  unsigned long long* __restrict__ keys, int shift) {
-    int64_t n = (int64_t)*n_ptr;
-    if (n > cap) n = cap;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t pos = (uint32_t)recs[i].pos;
-        const int32_t slot = atomicAdd(&cursor[pos >> shift], 1);
-        keys[slot] = ((unsigned long long)pos << 32) | (unsigned long long)i;
-    }
-}
-// one wavefront per bucket: every key's rank among the bucket's keys (positions are distinct) is
-// its place; the keys are read from L2, a bucket holds a handful
-__global__ __launch_bounds__(256) void ko_bucket_sort(const unsigned long long* __restrict__ keys,
-                                                      unsigned long long* __restrict__ sorted_keys,
-                                                      const int32_t* __restrict__ start, int32_t* __restrict__ bucket,
-                                                      int64_t nb) {
-    const int lane = threadIdx.x & 63;
-    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (b >= nb) return;
-    if (lane == 0) bucket[b] = 0;       // the counts were consumed by ko_scan: clean for the next run
-    const int32_t a = start[b], z = start[b + 1], k = z - a;
-    if (k == 0) return;
-    if (k <= 64) {
-        const unsigned long long mine = lane < k ? keys[a + lane] : ~0ull;
-        int32_t rank = 0;
-        for (int j = 0; j < k; j++) rank += __shfl(mine, j, 64) < mine;
-        if (lane < k) sorted_keys[a + rank] = mine;
-        return;
-    }
-    for (int32_t i = lane; i < k; i += 64) {
-        const unsigned long long mine = keys[a + i];
-        int32_t rank = 0;
-        for (int32_t j = 0; j < k; j++) rank += keys[a + j] < mine;
-        sorted_keys[a + rank] = mine;
-    }
-}
-__global__ __launch_bounds__(256) void ko_gather(const ngsep_site_out* __restrict__ recs,
-                                                 const unsigned long long* __restrict__ keys,
-                                                 const unsigned long long* n_ptr, int64_t cap,
-                                                 ngsep_site_out* __restrict__ sorted) {
+    __syncthreads();
+    const int64_t base = all ? 0 : total_before;
     constexpr int W = sizeof(ngsep_site_out) / 4;
-    int64_t n = (int64_t)*n_ptr;
-    if (n > cap) n = cap;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(recs);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(sorted);
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n * W; t += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = t / W, w = t - r * W;
-        dst[t] = src[(int64_t)(keys[r] & 0xFFFFFFFFull) * W + w];
+    for (int j = wv; j < kKofBuckets; j += 4) {
+        const int64_t b = b0 + j;
+        if (b >= nb) break;
+        const int32_t c = s_cnt[j];
+        if (c == 0) continue;
+        const ngsep_site_out* src = brec + b * bcap;
+        const int64_t off = base + s_off[j];
+        auto copy = [&](int32_t from, int64_t to) {
+            if (to >= cap) return;
+            const uint32_t* sw = reinterpret_cast<const uint32_t*>(src + from);
+            uint32_t* dw = reinterpret_cast<uint32_t*>(sorted + to);
+            for (int w = 0; w < W; w++) dw[w] = sw[w];
+        };
+        if (c <= 64) {
+            const unsigned long long mine = lane < c ? ((unsigned long long)(uint32_t)src[lane].pos << 32) | (uint32_t)lane : ~0ull;
+            int32_t rank = 0;
+            for (int k = 0; k < c; k++) rank += __shfl(mine, k, 64) < mine;
+            if (lane < c) copy(lane, off + rank);
+        } else {                                      // a crowded bucket (dump mode, -minQuality 0): keys via LDS
+            for (int k = lane; k < c; k += 64) s_keys[wv][k] = ((unsigned long long)(uint32_t)src[k].pos << 32) | (uint32_t)k;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int k = lane; k < c; k += 64) {
+                const unsigned long long mine = s_keys[wv][k];
+                int32_t rank = 0;
+                for (int m = 0; m < c; m++) rank += s_keys[wv][m] < mine;
+                copy(k, off + rank);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
     }
 }
 
@@ -1350,7 +1308,8 @@ Device* device_create(int ordinal, std::string& err) {
         hipStreamCreateWithFlags(&d->copy_stream, hipStreamNonBlocking) != hipSuccess) { err = "stream"; delete d; return nullptr; }
     for (auto& e : d->ev) (void)hipEventCreate(&e);
     for (auto& sl : d->slot)
-        for (auto& e : sl.ev) (void)hipEventCreateWithFlags(&e, hipEventDefault);
+        for (int k = 0; k < 5; k++)     // 0-2 time the kernels; 3-4 only order the two streams
+            (void)hipEventCreateWithFlags(&sl.ev[k], k < 3 ? hipEventDefault : hipEventDisableTiming);
     if (hipMalloc(&d->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(d->d_counters, 0, 16 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&d->h_counters, 4 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
@@ -1400,17 +1359,15 @@ void device_destroy(Device* d) {
     if (!d) return;
     device_release(d);
     (void)hipDeviceSynchronize();
-    (void)hipFree(d->d_sites);
-    (void)hipFree(d->d_sorted);
+    (void)hipFree(d->d_brec);
+    (void)hipFree(d->d_bcount);
     for (auto& sl : d->slot) {
         (void)hipFree(sl.d_sorted);
         (void)hipHostFree(sl.h_ctr);
         for (auto& e : sl.ev) (void)hipEventDestroy(e);
     }
-    (void)hipFree(d->d_keys);
     (void)hipFree(d->d_psites);
     (void)hipFree(d->d_pcalls);
-    (void)hipFree(d->d_bucket);
     (void)hipFree(d->d_hard);
     (void)hipFree(d->d_counters);
     (void)hipFree(d->d_tables);
@@ -1482,15 +1439,7 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
 // free] KT KP KO; copy stream: [wait KO] D2H counters + records, clear the counter set.
 // ------------------------------------------------------------------------------------------
 static int grow_shared(Device* d, int64_t sites, int64_t queue, std::string& err) {
-    if (sites > d->cap_sites) {
-        (void)hipFree(d->d_sites);
-        (void)hipFree(d->d_keys);
-        d->d_sites = nullptr;
-        d->d_keys = nullptr;
-        HIP_TRY(hipMalloc(&d->d_sites, (size_t)sites * sizeof(ngsep_site_out)));
-        HIP_TRY(hipMalloc(&d->d_keys, (size_t)sites * 2 * sizeof(unsigned long long)));
-        d->cap_sites = sites;
-    }
+    if (sites > d->cap_sites) d->cap_sites = sites;     // the slots' ordered-record buffers follow
     if (queue > d->cap_hard) {
         (void)hipFree(d->d_hard);
         d->d_hard = nullptr;
@@ -1518,20 +1467,30 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         HIP_TRY(hipMalloc(&sl.d_sorted, (size_t)d->cap_sites * sizeof(ngsep_site_out)));
         sl.cap = d->cap_sites;
     }
-    // position buckets of the ordering pass: a few records each
-    const int shift = g.dump_all ? 4 : 12;
+    // position buckets of the ordering pass: a few records each (dump mode: 16 positions, so 16
+    // records at most; calls: 4096 positions and room for 64, grown when a run overflows)
+    const int shift = g.dump_all ? 4 : d->ko_shift;
+    const int32_t bcap = g.dump_all ? 16 : d->ko_bcap;
     const int64_t nb = (s.g_len >> shift) + 1;
-    if (nb > d->nb_cap) {
+    if (nb > d->nb_cap || nb * bcap > d->brec_cap) {
         if (!idle) HIP_TRY(hipDeviceSynchronize());
-        (void)hipFree(d->d_bucket);
-        HIP_TRY(hipMalloc(&d->d_bucket, (size_t)(3 * nb + 1) * sizeof(int32_t)));
-        d->nb_cap = nb;
-        d->nb_clean = 0;
+        if (nb > d->nb_cap) {
+            (void)hipFree(d->d_bcount);
+            d->d_bcount = nullptr;
+            HIP_TRY(hipMalloc(&d->d_bcount, (size_t)nb * sizeof(int32_t)));
+            d->nb_cap = nb;
+        }
+        if (nb * bcap > d->brec_cap) {
+            (void)hipFree(d->d_brec);
+            d->d_brec = nullptr;
+            HIP_TRY(hipMalloc(&d->d_brec, (size_t)(nb * bcap) * sizeof(ngsep_site_out)));
+            d->brec_cap = nb * bcap;
+        }
     }
     unsigned long long* ctr = sl.d_ctr;
     sl.t0 = std::chrono::steady_clock::now();
     // the slot's previous copies (and the reset of its counter set) are done before it is reused
-    HIP_TRY(hipStreamWaitEvent(d->stream, sl.ev[4], 0));
+    if (hipEventQuery(sl.ev[4]) != hipSuccess) HIP_TRY(hipStreamWaitEvent(d->stream, sl.ev[4], 0));
     if (!d->tables_valid || std::memcmp(&d->h_tables, &t, sizeof(LikTables)) != 0) {
         HIP_TRY(hipStreamSynchronize(d->stream));     // the previous upload may still read h_tables
         d->h_tables = t;
@@ -1552,30 +1511,25 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         dim3 grid((unsigned)nblk);
         if (prune)
             hipLaunchKernelGGL(k_tile_pileup<0>, grid, dim3(kScanThreads), 0, d->stream, (const u32x4*)d->d_pile,
-                               d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, d->d_tables, g, d->d_hard, ctr, d->cap_hard);
+                               d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, d->d_tables, g, d->d_hard, ctr, d->cap_hard,
+                               d->d_bcount, nb);
         else
             hipLaunchKernelGGL(k_tile_pileup<1>, grid, dim3(kScanThreads), 0, d->stream, (const u32x4*)d->d_pile,
-                               d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, d->d_tables, g, d->d_hard, ctr, d->cap_hard);
+                               d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, d->d_tables, g, d->d_hard, ctr, d->cap_hard,
+                               d->d_bcount, nb);
         HIP_TRY(hipGetLastError());
+    } else {
+        HIP_TRY(hipMemsetAsync(d->d_bcount, 0, (size_t)nb * sizeof(int32_t), d->stream));
     }
     HIP_TRY(hipEventRecord(sl.ev[1], d->stream));
     hipLaunchKernelGGL(k_posterior, dim3(2048), dim3(kPostWaves * 64), 0, d->stream, d->d_hard, ctr + 2, d->cap_hard,
-                       d->d_reads, d->n_reads, d->d_lb, d->d_slots, d->slot_size, d->d_tables, g, d->d_sites, ctr,
-                       d->cap_sites);
+                       d->d_reads, d->n_reads, d->d_lb, d->d_slots, d->slot_size, d->d_tables, g, d->d_brec,
+                       d->d_bcount, shift, bcap);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(sl.ev[2], d->stream));
-    // order the records by position on the device
-    int32_t* cnt = d->d_bucket;
-    int32_t* start = d->d_bucket + nb;
-    int32_t* cursor = d->d_bucket + 2 * nb + 1;
-    if (nb > d->nb_clean) HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)nb * sizeof(int32_t), d->stream));
-    hipLaunchKernelGGL(ko_hist, dim3(256), dim3(256), 0, d->stream, d->d_sites, ctr, d->cap_sites, cnt, shift);
-    hipLaunchKernelGGL(ko_scan, dim3(1), dim3(1024), 0, d->stream, cnt, start, cursor, nb);
-    hipLaunchKernelGGL(ko_scatter, dim3(256), dim3(256), 0, d->stream, d->d_sites, ctr, d->cap_sites, cursor, d->d_keys, shift);
-    unsigned long long* skeys = d->d_keys + d->cap_sites;    // second half: keys in position order
-    hipLaunchKernelGGL(ko_bucket_sort, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, d->stream, d->d_keys, skeys, start, cnt, nb);
-    d->nb_clean = std::max(d->nb_clean, nb);
-    hipLaunchKernelGGL(ko_gather, dim3(1024), dim3(256), 0, d->stream, d->d_sites, skeys, ctr, d->cap_sites, sl.d_sorted);
+    if (d->time_posterior) HIP_TRY(hipEventRecord(sl.ev[2], d->stream));
+    // order the records by position on the device (one kernel; counters[0] = records | max bucket << 40)
+    hipLaunchKernelGGL(ko_fused, dim3((unsigned)((nb + kKofBuckets - 1) / kKofBuckets)), dim3(256), 0, d->stream, d->d_brec,
+                       d->d_bcount, nb, bcap, sl.d_sorted, sl.cap, ctr);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(sl.ev[3], d->stream));
     // copies: counters and a prefix of the ordered records (sized from the previous run) straight into
@@ -1613,18 +1567,27 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
     if (d->n_collected == d->n_submitted) { err = "no run to collect"; return -1; }
     RunSlot& sl = d->slot[d->n_collected % 2];
     HIP_TRY(hipEventSynchronize(sl.ev[4]));
-    int64_t n = (int64_t)sl.h_ctr[0];
+    constexpr unsigned long long kNMask = (1ull << 40) - 1;
+    int64_t n = (int64_t)(sl.h_ctr[0] & kNMask);
+    int64_t mx = (int64_t)(sl.h_ctr[0] >> 40);          // fullest position bucket
     int64_t q = (int64_t)sl.h_ctr[2];
-    for (int attempt = 0; n > d->cap_sites || q > d->cap_hard; attempt++) {
+    for (int attempt = 0; n > d->cap_sites || q > d->cap_hard || (!sl.g.dump_all && mx > d->ko_bcap); attempt++) {
         // more calls or undecided candidates than the buffers hold (e.g. -minQuality 0): drain, grow
         // and run this slot again in place (a later run in the other slot keeps its own results)
         if (attempt == 3) { err = "result buffers kept overflowing"; return -1; }
         HIP_TRY(hipDeviceSynchronize());
         if (grow_shared(d, std::max(d->cap_sites, n + 1024), std::max(d->cap_hard, q + 1024), err) != 0) return -1;
+        if (!sl.g.dump_all && mx > d->ko_bcap) {
+            // crowded buckets (e.g. -minQuality 0 calls most positions): room for the fullest one, up to
+            // the 1024 keys a KO wave ranks; past that, 16-position buckets that cannot overflow
+            if (mx <= 1024) while (d->ko_bcap < mx) d->ko_bcap *= 2;
+            else { d->ko_shift = 4; d->ko_bcap = 16; }
+        }
         d->last_n_sites = n;
         if (enqueue_run(d, sl, *sl.staged, sl.tabs, sl.g, sl.prune, true, err) != 0) return -1;
         HIP_TRY(hipEventSynchronize(sl.ev[4]));
-        n = (int64_t)sl.h_ctr[0];
+        n = (int64_t)(sl.h_ctr[0] & kNMask);
+        mx = (int64_t)(sl.h_ctr[0] >> 40);
         q = (int64_t)sl.h_ctr[2];
     }
     sl.busy = false;
@@ -1648,7 +1611,7 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
     *n_out = n;
     float a = 0, a2 = 0;
     (void)hipEventElapsedTime(&a, sl.ev[0], sl.ev[1]);
-    (void)hipEventElapsedTime(&a2, sl.ev[1], sl.ev[2]);
+    if (d->time_posterior) (void)hipEventElapsedTime(&a2, sl.ev[1], sl.ev[2]);
     *scan_ms = a;
     *geno_ms = a2;
     *total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - sl.t0).count();
