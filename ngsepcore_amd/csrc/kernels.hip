@@ -173,8 +173,17 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
                                                    const int32_t* __restrict__ lb, const uint8_t* __restrict__ slots,
                                                    int32_t S, const LikTables* __restrict__ tabs, GenotypeParams gp,
                                                    ngsep_site_out* __restrict__ brec, int32_t* __restrict__ bcount,
-                                                   int shift, int32_t bcap) {
+                                                   int shift, int32_t bcap, unsigned long long* __restrict__ stamps) {
+#ifdef NGSEP_KP_STAMPS
+    // diagnostics build: cycles per phase summed over sites, walk iterations, valid reads, wave spans
+    unsigned long long st_w0 = __builtin_amdgcn_s_memtime(), st_a = 0, st_b = 0, st_c = 0;
+    int32_t st_it = 0, st_nv = 0, st_sites = 0;
+#define KP_STAMP(v) v = __builtin_amdgcn_s_memtime()
+#else
+#define KP_STAMP(v)
+#endif
     __shared__ double s_t[3][32];
+    __shared__ uint8_t s_code[kPostWaves][64];      // a chunk's valid codes in read order
     if (threadIdx.x < 96)
         s_t[threadIdx.x >> 5][threadIdx.x & 31] =
             (threadIdx.x < 32 ? tabs->A : threadIdx.x < 64 ? tabs->H : tabs->E)[threadIdx.x & 31];
@@ -184,20 +193,38 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
     int64_t n = (int64_t)*qn;
     if (n > qcap) n = qcap;
     const int64_t nwaves = (int64_t)gridDim.x * kPostWaves;
-    for (int64_t i = (int64_t)blockIdx.x * kPostWaves + wv; i < n; i += nwaves) {
-        const QueueSite qs = queue[i];
+    // lane k < 10 owns one of the ten log-likelihood sums (k: L00 L11 L22 L33 L01 L02 L03 L12 L13 L23):
+    // a read of allele a adds table tm[q] when bit a of am is set, else E[q] (CountsHelper.java:231-248)
+    const uint32_t am = lane < 4 ? 1u << lane : lane < 10 ? (0xCA6953u >> (4 * (lane - 4))) & 15u : 0u;
+    const int tm = lane < 4 ? 0 : 1;
+    int64_t i = (int64_t)blockIdx.x * kPostWaves + wv;
+    // the next site's queue entry and read-index entry are loaded while the current site is processed
+    QueueSite qs = i < n ? queue[i] : QueueSite{0, 0};
+    int32_t lb_cur = i < n ? lb[qs.gpos >> 6] : 0;
+    for (; i < n; i += nwaves) {
+#ifdef NGSEP_KP_STAMPS
+        unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+        KP_STAMP(t0);
+        st_sites++;
+#endif
         const int32_t gpos = __builtin_amdgcn_readfirstlane(qs.gpos);
         const uint32_t rc = (uint32_t)__builtin_amdgcn_readfirstlane(qs.rc);
-        if (gp.ablate & 16) continue;                     // diagnostics: queue read only
+        const int64_t r_first = __builtin_amdgcn_readfirstlane(lb_cur);
+        const bool more = i + nwaves < n;
+        qs = more ? queue[i + nwaves] : QueueSite{0, 0};
+        if (gp.ablate & 16) { lb_cur = more ? lb[qs.gpos >> 6] : 0; continue; }   // diagnostics: queue read only
         int32_t total = 0;
         int32_t cnt[4] = {0, 0, 0, 0};
         int32_t sc[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
-        double L00 = 0, L01 = 0, L02 = 0, L03 = 0, L11 = 0, L12 = 0, L13 = 0, L22 = 0, L23 = 0, L33 = 0;
+        double acc = 0;                                   // this lane's log-likelihood sum
         // reads that can cover gpos start at lb[gpos/64] (every earlier read ends before gpos); the
         // table is sorted by start, so the first read starting after gpos ends the walk
-        for (int64_t r0 = lb[gpos >> 6]; r0 < n_reads; r0 += 64) {
+        for (int64_t r0 = r_first; r0 < n_reads; r0 += 64) {
             const int64_t r = r0 + lane;
             const int4 h = r < n_reads ? reads[r] : int4{INT32_MAX, 0, 0, 0};
+#ifdef NGSEP_KP_STAMPS
+            st_it++;
+#endif
             const bool in = h.x <= gpos;
             const bool cov = in && h.y >= gpos;
             const int32_t o = cov ? gpos - h.x : 0;
@@ -213,30 +240,42 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
                 sc[t][0] += __popcll(m & negm);                           // countsStrand[idx][neg?0:1] (:226-227)
                 sc[t][1] += __popcll(m & ~negm);
             }
-            unsigned long long mv = __ballot(valid);
-            while (mv) {                                                  // updateCounts (:231-248), read order
-                const int l = __builtin_ctzll(mv);
-                mv &= mv - 1ull;
-                const uint32_t cd = (uint32_t)__builtin_amdgcn_readlane((int)code, l);
-                const uint32_t a = (cd >> 5) & 3u;
-                int q = (int)(cd & 31u);
-                q = q > gp.max_q ? gp.max_q : q;                          // -maxBaseQS (:217-219)
-                const double A = s_t[0][q], H = s_t[1][q], E = s_t[2][q];
-                // f == g: the [i][j] and [j][i] sums are identical sequences
-                L00 += a == 0 ? A : E;
-                L11 += a == 1 ? A : E;
-                L22 += a == 2 ? A : E;
-                L33 += a == 3 ? A : E;
-                L01 += a <= 1 ? H : E;
-                L02 += (a & 1) == 0 ? H : E;
-                L03 += (a == 0 || a == 3) ? H : E;
-                L12 += (a == 1 || a == 2) ? H : E;
-                L13 += (a & 1) == 1 ? H : E;
-                L23 += a >= 2 ? H : E;
+            const unsigned long long mv = __ballot(valid);
+#ifdef NGSEP_KP_STAMPS
+            st_nv += __popcll(mv);
+#endif
+            // updateCounts (:231-248) in read order: the valid codes are compacted in LDS, then each
+            // of the ten sum lanes adds its term of every read in turn (the loads do not depend on the
+            // sums, so they pipeline; each sum's order of additions is the reference's)
+            const int32_t nv = __popcll(mv);
+            const int32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mv >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mv, 0u));
+            if (valid) s_code[wv][rank] = (uint8_t)code;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < 10) {
+#pragma unroll 4
+                for (int32_t j = 0; j < nv; j++) {
+                    const uint32_t cd = s_code[wv][j];
+                    int q = (int)(cd & 31u);
+                    q = q > gp.max_q ? gp.max_q : q;                      // -maxBaseQS (:217-219)
+                    acc += s_t[((am >> ((cd >> 5) & 3u)) & 1u) ? tm : 2][q];
+                }
             }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             if (__ballot(!in)) break;
         }
+#ifdef NGSEP_KP_STAMPS
+        KP_STAMP(t1);
+        st_a += t1 - t0;
+#endif
+        lb_cur = more ? lb[qs.gpos >> 6] : 0;
         if (total == 0 || (gp.ablate & 8)) continue;                      // VariantDiscoverySNVQAlgorithm.java:101-103
+        const double L00 = readlane_d(acc, 0), L11 = readlane_d(acc, 1), L22 = readlane_d(acc, 2), L33 = readlane_d(acc, 3);
+        const double L01 = readlane_d(acc, 4), L02 = readlane_d(acc, 5), L03 = readlane_d(acc, 6);
+        const double L12 = readlane_d(acc, 7), L13 = readlane_d(acc, 8), L23 = readlane_d(acc, 9);
         const bool callable = (rc & 0x80u) != 0;
         int8_t genotype = -1, alt = -1, third = -1, nal = 0;
         int16_t gq = 0, qual = 0;
@@ -305,6 +344,10 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
             }
             if (keep && gp.min_quality > gq) keep = false;
         }
+#ifdef NGSEP_KP_STAMPS
+        KP_STAMP(t2);
+        st_b += t2 - t1;
+#endif
         if (!keep && !gp.dump_all) continue;
         // the record goes to its position bucket (KO orders each bucket; no global reservation)
         if (lane == 0) {
@@ -333,7 +376,26 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
             const int32_t k = atomicAdd(&bcount[b], 1);
             if (k < bcap) brec[(int64_t)b * bcap + k] = o;
         }
+#ifdef NGSEP_KP_STAMPS
+        KP_STAMP(t3);
+        st_c += t3 - t2;
+#endif
     }
+#ifdef NGSEP_KP_STAMPS
+    if (lane == 0 && stamps) {
+        const unsigned long long w1 = __builtin_amdgcn_s_memtime();
+        atomicAdd(&stamps[0], st_a);
+        atomicAdd(&stamps[1], st_b);
+        atomicAdd(&stamps[2], st_c);
+        atomicAdd(&stamps[3], (unsigned long long)st_it);
+        atomicAdd(&stamps[4], (unsigned long long)st_nv);
+        atomicAdd(&stamps[5], (unsigned long long)st_sites);
+        atomicAdd(&stamps[6], w1 - st_w0);
+        atomicMin(&stamps[7], st_w0);
+        atomicMax(&stamps[8], w1);
+        atomicAdd(&stamps[9], 1ull);
+    }
+#endif
 }
 
 
@@ -1522,9 +1584,17 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         HIP_TRY(hipMemsetAsync(d->d_bcount, 0, (size_t)nb * sizeof(int32_t), d->stream));
     }
     HIP_TRY(hipEventRecord(sl.ev[1], d->stream));
+#ifdef NGSEP_KP_STAMPS
+    if (!d->d_stamps) HIP_TRY(hipMalloc(&d->d_stamps, 16 * sizeof(unsigned long long)));
+    {
+        unsigned long long init[16] = {0, 0, 0, 0, 0, 0, 0, ~0ull, 0, 0, 0, 0, 0, 0, 0, 0};
+        HIP_TRY(hipMemcpyAsync(d->d_stamps, init, sizeof init, hipMemcpyHostToDevice, d->stream));
+        HIP_TRY(hipStreamSynchronize(d->stream));
+    }
+#endif
     hipLaunchKernelGGL(k_posterior, dim3(2048), dim3(kPostWaves * 64), 0, d->stream, d->d_hard, ctr + 2, d->cap_hard,
                        d->d_reads, d->n_reads, d->d_lb, d->d_slots, d->slot_size, d->d_tables, g, d->d_brec,
-                       d->d_bcount, shift, bcap);
+                       d->d_bcount, shift, bcap, d->d_stamps);
     HIP_TRY(hipGetLastError());
     if (d->time_posterior) HIP_TRY(hipEventRecord(sl.ev[2], d->stream));
     // order the records by position on the device (one kernel; counters[0] = records | max bucket << 40)
@@ -1592,6 +1662,17 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
     }
     sl.busy = false;
     d->n_collected++;
+#ifdef NGSEP_KP_STAMPS
+    {
+        unsigned long long st[16];
+        HIP_TRY(hipMemcpy(st, d->d_stamps, sizeof st, hipMemcpyDeviceToHost));
+        const double ns = st[5] ? (double)st[5] : 1.0;
+        std::fprintf(stderr, "[kp stamps] sites %llu waves %llu | per site cycles: tally %.0f posterior %.0f emit %.0f | "
+                     "walk iters %.2f valid reads %.1f | wave busy avg %.0f, span %llu\n",
+                     st[5], st[9], st[0] / ns, st[1] / ns, st[2] / ns, st[3] / ns, st[4] / ns,
+                     st[9] ? (double)st[6] / st[9] : 0.0, st[8] - st[7]);
+    }
+#endif
     if (n > sl.guess) {
         sl.host.n = (size_t)sl.guess;                 // keep the records already copied when the store grows
         sl.host.reserve((size_t)n);
