@@ -197,11 +197,24 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
     // a read of allele a adds table tm[q] when bit a of am is set, else E[q] (CountsHelper.java:231-248)
     const uint32_t am = lane < 4 ? 1u << lane : lane < 10 ? (0xCA6953u >> (4 * (lane - 4))) & 15u : 0u;
     const int tm = lane < 4 ? 0 : 1;
+    auto load_h = [&](int64_t r0) -> int4 {
+        const int64_t r = r0 + lane;
+        return r < n_reads ? reads[r] : int4{INT32_MAX, 0, 0, 0};
+    };
+    auto load_code = [&](const int4& h, int32_t g) -> uint32_t {
+        const bool cov = h.x <= g && h.y >= g;
+        const int32_t o = cov ? g - h.x : 0;
+        return cov ? (uint32_t)slots[(int64_t)(h.z + o / S) * S + (o % S)] : 0u;
+    };
+    // software pipeline over this wave's sites: the next site's queue entry and read-index entry are
+    // loaded during the current site's walk, its first 64 reads during the current posterior, the
+    // entry after next meanwhile, so a site waits on one dependent load (its read bytes)
     int64_t i = (int64_t)blockIdx.x * kPostWaves + wv;
-    // the next site's queue entry and read-index entry are loaded while the current site is processed
     QueueSite qs = i < n ? queue[i] : QueueSite{0, 0};
-    int32_t lb_cur = i < n ? lb[qs.gpos >> 6] : 0;
-    for (; i < n; i += nwaves) {
+    int32_t lb_c = i < n ? lb[qs.gpos >> 6] : 0, lb_n = 0;
+    int4 h_c = i < n ? load_h(lb_c) : int4{INT32_MAX, 0, 0, 0};
+    QueueSite qs_n = i + nwaves < n ? queue[i + nwaves] : QueueSite{0, 0}, qs_nn{0, 0};
+    for (; i < n; i += nwaves, qs = qs_n, qs_n = qs_nn, lb_c = lb_n) {
 #ifdef NGSEP_KP_STAMPS
         unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
         KP_STAMP(t0);
@@ -209,26 +222,24 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
 #endif
         const int32_t gpos = __builtin_amdgcn_readfirstlane(qs.gpos);
         const uint32_t rc = (uint32_t)__builtin_amdgcn_readfirstlane(qs.rc);
-        const int64_t r_first = __builtin_amdgcn_readfirstlane(lb_cur);
+        const int64_t r_first = __builtin_amdgcn_readfirstlane(lb_c);
         const bool more = i + nwaves < n;
-        qs = more ? queue[i + nwaves] : QueueSite{0, 0};
-        if (gp.ablate & 16) { lb_cur = more ? lb[qs.gpos >> 6] : 0; continue; }   // diagnostics: queue read only
+        lb_n = more ? lb[qs_n.gpos >> 6] : 0;
+        qs_nn = i + 2 * nwaves < n ? queue[i + 2 * nwaves] : QueueSite{0, 0};
+        int4 h = h_c;
+        uint32_t code = load_code(h, gpos);
+        if (gp.ablate & 16) { h_c = more ? load_h(lb_n) : int4{INT32_MAX, 0, 0, 0}; continue; }   // diagnostics
         int32_t total = 0;
         int32_t cnt[4] = {0, 0, 0, 0};
         int32_t sc[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
         double acc = 0;                                   // this lane's log-likelihood sum
         // reads that can cover gpos start at lb[gpos/64] (every earlier read ends before gpos); the
         // table is sorted by start, so the first read starting after gpos ends the walk
-        for (int64_t r0 = r_first; r0 < n_reads; r0 += 64) {
-            const int64_t r = r0 + lane;
-            const int4 h = r < n_reads ? reads[r] : int4{INT32_MAX, 0, 0, 0};
+        for (int64_t r0 = r_first;;) {
 #ifdef NGSEP_KP_STAMPS
             st_it++;
 #endif
             const bool in = h.x <= gpos;
-            const bool cov = in && h.y >= gpos;
-            const int32_t o = cov ? gpos - h.x : 0;
-            const uint32_t code = cov ? (uint32_t)slots[(int64_t)(h.z + o / S) * S + (o % S)] : 0u;
             total += __popcll(__ballot(code != 0));                       // CountsHelper.java:210
             const bool valid = (code & 0x80u) != 0;                       // q<=3 or not A/C/G/T: not counted (:214-221)
             const uint32_t al = (code >> 5) & 3u;
@@ -266,73 +277,68 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             if (__ballot(!in)) break;
+            r0 += 64;
+            if (r0 >= n_reads) break;
+            h = load_h(r0);
+            code = load_code(h, gpos);
         }
+        h_c = more ? load_h(lb_n) : int4{INT32_MAX, 0, 0, 0};
 #ifdef NGSEP_KP_STAMPS
         KP_STAMP(t1);
         st_a += t1 - t0;
 #endif
-        lb_cur = more ? lb[qs.gpos >> 6] : 0;
         if (total == 0 || (gp.ablate & 8)) continue;                      // VariantDiscoverySNVQAlgorithm.java:101-103
-        const double L00 = readlane_d(acc, 0), L11 = readlane_d(acc, 1), L22 = readlane_d(acc, 2), L33 = readlane_d(acc, 3);
-        const double L01 = readlane_d(acc, 4), L02 = readlane_d(acc, 5), L03 = readlane_d(acc, 6);
-        const double L12 = readlane_d(acc, 7), L13 = readlane_d(acc, 8), L23 = readlane_d(acc, 9);
         const bool callable = (rc & 0x80u) != 0;
         int8_t genotype = -1, alt = -1, third = -1, nal = 0;
         int16_t gq = 0, qual = 0;
         bool keep = false;
         if (callable) {
             const int refIdx = (int)((rc >> 5) & 3u);
-            const double ph = gp.log_prior_homo, px = gp.log_prior_hetero;
-            // getPosteriorProbabilities (CountsHelper.java:410-443): events in Java order;
-            // row i holds post(i,i) at 4i and post(i,j) at 4i+1+j (j<i) or 4i+j (j>i)
-            double ev[16] = {L00 + ph, L01 + px, L02 + px, L03 + px,
-                             L11 + ph, L01 + px, L12 + px, L13 + px,
-                             L22 + ph, L02 + px, L12 + px, L23 + px,
-                             L33 + ph, L03 + px, L13 + px, L23 + px};
-            // calculatePosteriorProbabilities (:472-495): lane k % 16 evaluates event k's power of
-            // ten, then the normaliser is summed in Java's order
-            double logMax = 1;
+            // getPosteriorProbabilities (CountsHelper.java:410-443), one event per lane k < 16 in Java's
+            // order: row i holds post(i,i) at 4i and post(i,j) at 4i+1+j (j<i) or 4i+j (j>i); event
+            // k's log-likelihood is the sum on lane kEvSum[k] (nibble k of 0x9863975287416540)
+            const int k16 = lane & 15;
+            const int src = (int)((0x9863975287416540ull >> (4 * k16)) & 15u);
+            const double ev = __shfl(acc, src, 64) + ((k16 & 3) == 0 ? gp.log_prior_homo : gp.log_prior_hetero);
+            // calculatePosteriorProbabilities (:472-495): the maximum (no NaN: order-free), each
+            // lane's power of ten, the normaliser summed in Java's order, one division per lane
+            double logMax = ev;
 #pragma unroll
-            for (int k = 0; k < 16; k++)
-                if (logMax > 0 || logMax < ev[k]) logMax = ev[k];
-            double mine = 0;
-#pragma unroll
-            for (int k = 0; k < 16; k++) mine = (lane & 15) == k ? ev[k] : mine;
-            const double x = mine - logMax;
+            for (int o = 1; o < 16; o <<= 1) {
+                const double w = __shfl_xor(logMax, o, 64);
+                logMax = w > logMax ? w : logMax;
+            }
+            const double x = ev - logMax;
             const double pk = x < -20 ? 0.0 : pow(10.0, x);
             double totalProb = 0;
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                ev[k] = readlane_d(pk, k);
-                totalProb += ev[k];
-            }
-#pragma unroll
-            for (int k = 0; k < 16; k++) ev[k] = ev[k] / totalProb;
-            auto post = [&](int a, int b) -> double {    // register-resident select, no dynamic indexing
-                const int k = a == b ? 4 * a : (b < a ? 4 * a + 1 + b : 4 * a + b);
-                double v = 0;
-#pragma unroll
-                for (int e = 0; e < 16; e++) v = (e == k) ? ev[e] : v;
-                return v;
-            };
-            // getIndexesMaxGenotype (VariantDiscoverySNVQAlgorithm.java:223-243)
+            for (int k = 0; k < 16; k++) totalProb += readlane_d(pk, k);
+            const double post = pk / totalProb;            // lane k: posterior of event k
+            // getIndexesMaxGenotype (VariantDiscoverySNVQAlgorithm.java:223-243): lane p < 10 sums pair
+            // p = (a,b), a <= b, as post(a,b) + post(b,a); the scan keeps the reference's order and margin
+            const int pa = (int)((0x3221110000ull >> (4 * (lane % 10))) & 15u);
+            const int pb = (int)((0x3323213210ull >> (4 * (lane % 10))) & 15u);
+            const double p_ab = __shfl(post, pa == pb ? 4 * pa : 4 * pa + pb, 64);
+            const double p_ba = __shfl(post, 4 * pb + 1 + pa, 64);
+            const double gsum = pa == pb ? p_ab : p_ab + p_ba;
             int I = refIdx, J = refIdx;
-            double probMax = post(refIdx, refIdx);
+            double probMax = readlane_d(post, 4 * refIdx);
+            const double refProb = probMax;
 #pragma unroll
-            for (int a = 0; a < 4; a++)
-#pragma unroll
-                for (int b = a; b < 4; b++) {
-                    double g = ev[a == b ? 4 * a : 4 * a + b];   // post(a,b), b >= a
-                    if (a != b) g += ev[4 * b + 1 + a];           // post(b,a)
-                    if (g > probMax + 0.01) { probMax = g; I = a; J = b; }
+            for (int p = 0; p < 10; p++) {
+                const double g = readlane_d(gsum, p);
+                if (g > probMax + 0.01) {
+                    probMax = g;
+                    I = (int)((0x3221110000ull >> (4 * p)) & 15u);
+                    J = (int)((0x3323213210ull >> (4 * p)) & 15u);
                 }
-            const double refProb = post(refIdx, refIdx);
-            double maxP = post(I, J);
-            if (I != J) maxP += post(J, I);
-            gq = phred_d(1 - maxP);
-            qual = phred_d(refProb);
+            }
+            // maxP = post(I,J) [+ post(J,I)] is the pair sum the scan kept (the initial one: post(ref,ref))
+            const int16_t ph2 = phred_d(lane == 0 ? 1 - probMax : refProb);    // lanes 0, 1 in parallel
+            gq = (int16_t)__builtin_amdgcn_readlane((int)ph2, 0);
+            qual = (int16_t)__builtin_amdgcn_readlane((int)ph2, 1);
             if (I != J && I != refIdx && J != refIdx) {           // triallelic (:128-177)
-                if (post(I, I) > post(J, J) + 0.01) { alt = (int8_t)I; third = (int8_t)J; }
+                if (readlane_d(post, 4 * I) > readlane_d(post, 4 * J) + 0.01) { alt = (int8_t)I; third = (int8_t)J; }
                 else { alt = (int8_t)J; third = (int8_t)I; }
                 nal = 3; genotype = 3; keep = true;
             } else if (I != J) {
@@ -349,32 +355,29 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
         st_b += t2 - t1;
 #endif
         if (!keep && !gp.dump_all) continue;
-        // the record goes to its position bucket (KO orders each bucket; no global reservation)
-        if (lane == 0) {
-            ngsep_site_out o;
-            o.seq_id = -1;
-            o.pos = gpos;
-            o.ref = callable ? "ACGT"[(rc >> 5) & 3] : 'N';
-            o.n_alleles = nal;
-            o.alt = alt;
-            o.third = third;
-            o.genotype = genotype;
-            o.strand_bias = -1;
-            o.gq = gq;
-            o.qual = qual;
-            o.is_call = keep ? 1 : 0;
-            o.dp = total;
+        // the record goes to its position bucket (KO orders each bucket; no global reservation): lane 0
+        // writes the header, sum lane m its log-likelihood (logc order 00 01 02 03 11 12 13 22 23 33)
+        {
+            const int32_t bk = gpos >> shift;
+            int32_t k = 0;
+            if (lane == 0) k = atomicAdd(&bcount[bk], 1);
+            k = __builtin_amdgcn_readfirstlane(k);
+            if (k < bcap) {
+                ngsep_site_out* dst = brec + (int64_t)bk * bcap + k;
+                if (lane == 0) {
+                    const uint32_t ref = callable ? (uint32_t)(uint8_t)"ACGT"[(rc >> 5) & 3] : (uint32_t)'N';
+                    uint2* h8 = reinterpret_cast<uint2*>(dst);
+                    h8[0] = uint2{0xFFFFFFFFu, (uint32_t)gpos};
+                    h8[1] = uint2{ref | (uint32_t)(uint8_t)nal << 8 | (uint32_t)(uint8_t)alt << 16 | (uint32_t)(uint8_t)third << 24,
+                                  (uint32_t)(uint8_t)genotype | 0xFF00u | (uint32_t)(uint16_t)gq << 16};
+                    h8[2] = uint2{(uint32_t)(uint16_t)qual | (uint32_t)(keep ? 1 : 0) << 16, (uint32_t)total};
+                    h8[3] = uint2{(uint32_t)cnt[0], (uint32_t)cnt[1]};
+                    h8[4] = uint2{(uint32_t)cnt[2], (uint32_t)cnt[3]};
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                o.counts[k] = cnt[k];
-                o.strand_counts[k][0] = sc[k][0];
-                o.strand_counts[k][1] = sc[k][1];
+                    for (int t = 0; t < 4; t++) h8[5 + t] = uint2{(uint32_t)sc[t][0], (uint32_t)sc[t][1]};
+                }
+                if (lane < 10) dst->logc[(0x8653219740ull >> (4 * lane)) & 15u] = acc;
             }
-            o.logc[0] = L00; o.logc[1] = L01; o.logc[2] = L02; o.logc[3] = L03; o.logc[4] = L11;
-            o.logc[5] = L12; o.logc[6] = L13; o.logc[7] = L22; o.logc[8] = L23; o.logc[9] = L33;
-            const int32_t b = gpos >> shift;
-            const int32_t k = atomicAdd(&bcount[b], 1);
-            if (k < bcap) brec[(int64_t)b * bcap + k] = o;
         }
 #ifdef NGSEP_KP_STAMPS
         KP_STAMP(t3);
@@ -1592,7 +1595,8 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         HIP_TRY(hipStreamSynchronize(d->stream));
     }
 #endif
-    hipLaunchKernelGGL(k_posterior, dim3(2048), dim3(kPostWaves * 64), 0, d->stream, d->d_hard, ctr + 2, d->cap_hard,
+    static const int kp_grid = std::getenv("NGSEP_KP_GRID") ? std::max(1, std::atoi(std::getenv("NGSEP_KP_GRID"))) : 2048;   // tuning
+    hipLaunchKernelGGL(k_posterior, dim3(kp_grid), dim3(kPostWaves * 64), 0, d->stream, d->d_hard, ctr + 2, d->cap_hard,
                        d->d_reads, d->n_reads, d->d_lb, d->d_slots, d->slot_size, d->d_tables, g, d->d_brec,
                        d->d_bcount, shift, bcap, d->d_stamps);
     HIP_TRY(hipGetLastError());
