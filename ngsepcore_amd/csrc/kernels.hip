@@ -44,7 +44,16 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 struct QueueSite;
 
-struct RunSlot {                     // one in-flight single-sample run's results (see device_submit)
+struct RunSlot {                     // one in-flight single-sample run (see device_submit)
+    hipStream_t stream = nullptr;            // its compute stream (runs of the two slots overlap)
+    QueueSite* d_hard = nullptr;             // KT -> KP queue
+    int64_t cap_hard = 0;
+    ngsep_site_out* d_brec = nullptr;        // KP's records by position bucket: bucket b = d_brec[b * bcap ..]
+    int32_t* d_bcount = nullptr;             // records per bucket (zeroed by KT)
+    int64_t nb_cap = 0, brec_cap = 0;
+    LikTables* d_tables = nullptr;
+    LikTables h_tables{};                    // last uploaded tables
+    bool tables_valid = false;
     ngsep_site_out* d_sorted = nullptr;
     int64_t cap = 0;
     unsigned long long* d_ctr = nullptr;     // its counter set (4)
@@ -90,9 +99,6 @@ struct Device {
     int64_t cap_psites = 0;
     unsigned long long* d_stamps = nullptr;   // diagnostics (NGSEP_TIMING)
     LikTables* d_tables = nullptr;
-    ngsep_site_out* d_brec = nullptr;  // KP's records by position bucket: bucket b = d_brec[b * bcap ..]
-    int32_t* d_bcount = nullptr;       // records per bucket (zeroed by KT)
-    int64_t nb_cap = 0, brec_cap = 0;
     int32_t ko_shift = 12, ko_bcap = 64;   // 2^ko_shift positions per bucket (grown on overflow)
     QueueSite* d_hard = nullptr;
     int64_t cap_hard = 0;
@@ -1372,9 +1378,16 @@ Device* device_create(int ordinal, std::string& err) {
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&d->copy_stream, hipStreamNonBlocking) != hipSuccess) { err = "stream"; delete d; return nullptr; }
     for (auto& e : d->ev) (void)hipEventCreate(&e);
-    for (auto& sl : d->slot)
-        for (int k = 0; k < 5; k++)     // 0-2 time the kernels; 3-4 only order the two streams
+    // both slots' runs go to the device stream: with a stream per slot (NGSEP_SLOT_STREAMS=1) the next
+    // run's KT overlaps this run's KP/KO, measured slower (KT shares the CUs: 70 -> 60 G positions/s)
+    const bool one_stream = std::getenv("NGSEP_SLOT_STREAMS") == nullptr;
+    for (auto& sl : d->slot) {
+        if (one_stream) sl.stream = d->stream;
+        else if (hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess) { err = "stream"; return nullptr; }
+        if (hipMalloc(&sl.d_tables, sizeof(LikTables)) != hipSuccess) { err = "device allocation failed"; return nullptr; }
+        for (int k = 0; k < 5; k++)     // 0-2 time the kernels; 3-4 only order the streams
             (void)hipEventCreateWithFlags(&sl.ev[k], k < 3 ? hipEventDefault : hipEventDisableTiming);
+    }
     if (hipMalloc(&d->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(d->d_counters, 0, 16 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&d->h_counters, 4 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
@@ -1424,9 +1437,12 @@ void device_destroy(Device* d) {
     if (!d) return;
     device_release(d);
     (void)hipDeviceSynchronize();
-    (void)hipFree(d->d_brec);
-    (void)hipFree(d->d_bcount);
     for (auto& sl : d->slot) {
+        (void)hipFree(sl.d_brec);
+        (void)hipFree(sl.d_bcount);
+        (void)hipFree(sl.d_hard);
+        (void)hipFree(sl.d_tables);
+        if (sl.stream && sl.stream != d->stream) (void)hipStreamDestroy(sl.stream);
         (void)hipFree(sl.d_sorted);
         (void)hipHostFree(sl.h_ctr);
         for (auto& e : sl.ev) (void)hipEventDestroy(e);
@@ -1503,13 +1519,13 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
 // its ordered-record buffer, its counter set and a pinned host store.  Compute stream: [wait slot
 // free] KT KP KO; copy stream: [wait KO] D2H counters + records, clear the counter set.
 // ------------------------------------------------------------------------------------------
-static int grow_shared(Device* d, int64_t sites, int64_t queue, std::string& err) {
+static int grow_slot(Device* d, RunSlot& sl, int64_t sites, int64_t queue, std::string& err) {
     if (sites > d->cap_sites) d->cap_sites = sites;     // the slots' ordered-record buffers follow
-    if (queue > d->cap_hard) {
-        (void)hipFree(d->d_hard);
-        d->d_hard = nullptr;
-        HIP_TRY(hipMalloc(&d->d_hard, (size_t)queue * sizeof(QueueSite)));
-        d->cap_hard = queue;
+    if (queue > sl.cap_hard) {
+        (void)hipFree(sl.d_hard);
+        sl.d_hard = nullptr;
+        HIP_TRY(hipMalloc(&sl.d_hard, (size_t)queue * sizeof(QueueSite)));
+        sl.cap_hard = queue;
     }
     return 0;
 }
@@ -1521,9 +1537,9 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     // record per covered position
     const int64_t want = g.dump_all ? std::max<int64_t>(s.covered + 1024, 1024) : std::max<int64_t>(s.g_len / 256 + 4096, 4096);
     const int64_t qwant = g.dump_all ? std::max<int64_t>(s.covered + 1024, 1024) : std::max<int64_t>(s.g_len / 64 + 65536, 65536);
-    if (want > d->cap_sites || qwant > d->cap_hard) {
-        if (!idle) HIP_TRY(hipDeviceSynchronize());
-        if (grow_shared(d, want, qwant, err) != 0) return -1;
+    if (want > d->cap_sites || qwant > sl.cap_hard) {
+        if (!idle) HIP_TRY(hipStreamSynchronize(sl.stream));
+        if (grow_slot(d, sl, want, qwant, err) != 0) return -1;
     }
     if (sl.cap < d->cap_sites) {
         HIP_TRY(hipEventSynchronize(sl.ev[4]));
@@ -1537,32 +1553,32 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     const int shift = g.dump_all ? 4 : d->ko_shift;
     const int32_t bcap = g.dump_all ? 16 : d->ko_bcap;
     const int64_t nb = (s.g_len >> shift) + 1;
-    if (nb > d->nb_cap || nb * bcap > d->brec_cap) {
-        if (!idle) HIP_TRY(hipDeviceSynchronize());
-        if (nb > d->nb_cap) {
-            (void)hipFree(d->d_bcount);
-            d->d_bcount = nullptr;
-            HIP_TRY(hipMalloc(&d->d_bcount, (size_t)nb * sizeof(int32_t)));
-            d->nb_cap = nb;
+    if (nb > sl.nb_cap || nb * bcap > sl.brec_cap) {
+        if (!idle) HIP_TRY(hipStreamSynchronize(sl.stream));
+        if (nb > sl.nb_cap) {
+            (void)hipFree(sl.d_bcount);
+            sl.d_bcount = nullptr;
+            HIP_TRY(hipMalloc(&sl.d_bcount, (size_t)nb * sizeof(int32_t)));
+            sl.nb_cap = nb;
         }
-        if (nb * bcap > d->brec_cap) {
-            (void)hipFree(d->d_brec);
-            d->d_brec = nullptr;
-            HIP_TRY(hipMalloc(&d->d_brec, (size_t)(nb * bcap) * sizeof(ngsep_site_out)));
-            d->brec_cap = nb * bcap;
+        if (nb * bcap > sl.brec_cap) {
+            (void)hipFree(sl.d_brec);
+            sl.d_brec = nullptr;
+            HIP_TRY(hipMalloc(&sl.d_brec, (size_t)(nb * bcap) * sizeof(ngsep_site_out)));
+            sl.brec_cap = nb * bcap;
         }
     }
     unsigned long long* ctr = sl.d_ctr;
     sl.t0 = std::chrono::steady_clock::now();
     // the slot's previous copies (and the reset of its counter set) are done before it is reused
-    if (hipEventQuery(sl.ev[4]) != hipSuccess) HIP_TRY(hipStreamWaitEvent(d->stream, sl.ev[4], 0));
-    if (!d->tables_valid || std::memcmp(&d->h_tables, &t, sizeof(LikTables)) != 0) {
-        HIP_TRY(hipStreamSynchronize(d->stream));     // the previous upload may still read h_tables
-        d->h_tables = t;
-        HIP_TRY(hipMemcpyAsync(d->d_tables, &d->h_tables, sizeof(LikTables), hipMemcpyHostToDevice, d->stream));
-        d->tables_valid = true;
+    if (hipEventQuery(sl.ev[4]) != hipSuccess) HIP_TRY(hipStreamWaitEvent(sl.stream, sl.ev[4], 0));
+    if (!sl.tables_valid || std::memcmp(&sl.h_tables, &t, sizeof(LikTables)) != 0) {
+        HIP_TRY(hipStreamSynchronize(sl.stream));     // the previous upload may still read h_tables
+        sl.h_tables = t;
+        HIP_TRY(hipMemcpyAsync(sl.d_tables, &sl.h_tables, sizeof(LikTables), hipMemcpyHostToDevice, sl.stream));
+        sl.tables_valid = true;
     }
-    HIP_TRY(hipEventRecord(sl.ev[0], d->stream));
+    HIP_TRY(hipEventRecord(sl.ev[0], sl.stream));
     if (d->n_tiles > 0) {
         // persistent waves: as many workgroups as are co-resident (register-limited), each wave
         // walks the tiles with a grid stride, so at any moment the waves stream one contiguous
@@ -1575,37 +1591,37 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((d->n_tiles + kScanWaves - 1) / kScanWaves, (int64_t)d->n_cu * bpc));
         dim3 grid((unsigned)nblk);
         if (prune)
-            hipLaunchKernelGGL(k_tile_pileup<0>, grid, dim3(kScanThreads), 0, d->stream, (const u32x4*)d->d_pile,
-                               d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, d->d_tables, g, d->d_hard, ctr, d->cap_hard,
-                               d->d_bcount, nb);
+            hipLaunchKernelGGL(k_tile_pileup<0>, grid, dim3(kScanThreads), 0, sl.stream, (const u32x4*)d->d_pile,
+                               d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, sl.d_tables, g, sl.d_hard, ctr, sl.cap_hard,
+                               sl.d_bcount, nb);
         else
-            hipLaunchKernelGGL(k_tile_pileup<1>, grid, dim3(kScanThreads), 0, d->stream, (const u32x4*)d->d_pile,
-                               d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, d->d_tables, g, d->d_hard, ctr, d->cap_hard,
-                               d->d_bcount, nb);
+            hipLaunchKernelGGL(k_tile_pileup<1>, grid, dim3(kScanThreads), 0, sl.stream, (const u32x4*)d->d_pile,
+                               d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, sl.d_tables, g, sl.d_hard, ctr, sl.cap_hard,
+                               sl.d_bcount, nb);
         HIP_TRY(hipGetLastError());
     } else {
-        HIP_TRY(hipMemsetAsync(d->d_bcount, 0, (size_t)nb * sizeof(int32_t), d->stream));
+        HIP_TRY(hipMemsetAsync(sl.d_bcount, 0, (size_t)nb * sizeof(int32_t), sl.stream));
     }
-    HIP_TRY(hipEventRecord(sl.ev[1], d->stream));
+    HIP_TRY(hipEventRecord(sl.ev[1], sl.stream));
 #ifdef NGSEP_KP_STAMPS
     if (!d->d_stamps) HIP_TRY(hipMalloc(&d->d_stamps, 16 * sizeof(unsigned long long)));
     {
         unsigned long long init[16] = {0, 0, 0, 0, 0, 0, 0, ~0ull, 0, 0, 0, 0, 0, 0, 0, 0};
-        HIP_TRY(hipMemcpyAsync(d->d_stamps, init, sizeof init, hipMemcpyHostToDevice, d->stream));
-        HIP_TRY(hipStreamSynchronize(d->stream));
+        HIP_TRY(hipMemcpyAsync(d->d_stamps, init, sizeof init, hipMemcpyHostToDevice, sl.stream));
+        HIP_TRY(hipStreamSynchronize(sl.stream));
     }
 #endif
     static const int kp_grid = std::getenv("NGSEP_KP_GRID") ? std::max(1, std::atoi(std::getenv("NGSEP_KP_GRID"))) : 2048;   // tuning
-    hipLaunchKernelGGL(k_posterior, dim3(kp_grid), dim3(kPostWaves * 64), 0, d->stream, d->d_hard, ctr + 2, d->cap_hard,
-                       d->d_reads, d->n_reads, d->d_lb, d->d_slots, d->slot_size, d->d_tables, g, d->d_brec,
-                       d->d_bcount, shift, bcap, d->d_stamps);
+    hipLaunchKernelGGL(k_posterior, dim3(kp_grid), dim3(kPostWaves * 64), 0, sl.stream, sl.d_hard, ctr + 2, sl.cap_hard,
+                       d->d_reads, d->n_reads, d->d_lb, d->d_slots, d->slot_size, sl.d_tables, g, sl.d_brec,
+                       sl.d_bcount, shift, bcap, d->d_stamps);
     HIP_TRY(hipGetLastError());
-    if (d->time_posterior) HIP_TRY(hipEventRecord(sl.ev[2], d->stream));
+    if (d->time_posterior) HIP_TRY(hipEventRecord(sl.ev[2], sl.stream));
     // order the records by position on the device (one kernel; counters[0] = records | max bucket << 40)
-    hipLaunchKernelGGL(ko_fused, dim3((unsigned)((nb + kKofBuckets - 1) / kKofBuckets)), dim3(256), 0, d->stream, d->d_brec,
-                       d->d_bcount, nb, bcap, sl.d_sorted, sl.cap, ctr);
+    hipLaunchKernelGGL(ko_fused, dim3((unsigned)((nb + kKofBuckets - 1) / kKofBuckets)), dim3(256), 0, sl.stream, sl.d_brec,
+                       sl.d_bcount, nb, bcap, sl.d_sorted, sl.cap, ctr);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(sl.ev[3], d->stream));
+    HIP_TRY(hipEventRecord(sl.ev[3], sl.stream));
     // copies: counters and a prefix of the ordered records (sized from the previous run) straight into
     // the slot's pinned store, then the counter set is cleared for the slot's next run
     sl.guess = std::min<int64_t>(d->cap_sites, d->last_n_sites + d->last_n_sites / 64 + 64);
@@ -1645,12 +1661,12 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
     int64_t n = (int64_t)(sl.h_ctr[0] & kNMask);
     int64_t mx = (int64_t)(sl.h_ctr[0] >> 40);          // fullest position bucket
     int64_t q = (int64_t)sl.h_ctr[2];
-    for (int attempt = 0; n > d->cap_sites || q > d->cap_hard || (!sl.g.dump_all && mx > d->ko_bcap); attempt++) {
+    for (int attempt = 0; n > d->cap_sites || q > sl.cap_hard || (!sl.g.dump_all && mx > d->ko_bcap); attempt++) {
         // more calls or undecided candidates than the buffers hold (e.g. -minQuality 0): drain, grow
         // and run this slot again in place (a later run in the other slot keeps its own results)
         if (attempt == 3) { err = "result buffers kept overflowing"; return -1; }
         HIP_TRY(hipDeviceSynchronize());
-        if (grow_shared(d, std::max(d->cap_sites, n + 1024), std::max(d->cap_hard, q + 1024), err) != 0) return -1;
+        if (grow_slot(d, sl, std::max(d->cap_sites, n + 1024), std::max(sl.cap_hard, q + 1024), err) != 0) return -1;
         if (!sl.g.dump_all && mx > d->ko_bcap) {
             // crowded buckets (e.g. -minQuality 0 calls most positions): room for the fullest one, up to
             // the 1024 keys a KO wave ranks; past that, 16-position buckets that cannot overflow
