@@ -391,6 +391,19 @@ static int choose_tile(const std::vector<int32_t>& cov_max16, int64_t g_len, std
         const double cost = bytes + 2048.0 * (double)ntiles;
         if (best_cost < 0 || cost < best_cost) { best_cost = cost; bestT = T; best_rows.assign(cur.begin(), cur.begin() + ntiles); }
     }
+    if (const char* e = std::getenv("NGSEP_TILE_T")) {   // tests and tuning: a fixed tile width
+        const int T = std::atoi(e);
+        if (T >= kTileMinPos && T <= kTileMaxPos && (T & (T - 1)) == 0) {
+            std::vector<int32_t> c = cov_max16;
+            for (int t = kTileMinPos; t < T; t *= 2) {
+                std::vector<int32_t> nxt((c.size() + 1) / 2);
+                for (size_t i = 0; i < nxt.size(); i++) nxt[i] = std::max(c[2 * i], 2 * i + 1 < c.size() ? c[2 * i + 1] : 0);
+                c.swap(nxt);
+            }
+            rows_out.assign(c.begin(), c.begin() + g_len / T);
+            return T;
+        }
+    }
     if (best_cost < 0) {   // every T overflows the registers somewhere: smallest tiles, reload path
         bestT = kTileMinPos;
         best_rows.assign(cov_max16.begin(), cov_max16.begin() + g_len / kTileMinPos);

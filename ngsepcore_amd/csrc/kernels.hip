@@ -81,6 +81,8 @@ struct Device {
     hipEvent_t ev[4] = {};
     uint8_t* d_slots = nullptr;
     uint8_t* d_pile = nullptr;
+    uint32_t* d_planes = nullptr;    // bit planes of the pile (KB), 0 when the tile width has none
+    int32_t planes_W = 0;            // words per plane row (T / 32)
     int4* d_reads = nullptr;
     uint8_t* d_ref = nullptr;
     int32_t* d_lb = nullptr;
@@ -111,6 +113,7 @@ struct Device {
     int64_t last_hard = 0;
     int64_t last_exact = 0;     // wave passes of KT's exact integer bound in the last run
     int kt_blocks_per_cu[2] = {0, 0};
+    int kt_planes_per_cu[3] = {0, 0, 0};
     LikTables h_tables;         // last uploaded tables (pinned copy source)
     bool tables_valid = false;
     int32_t n_cu = 256;
@@ -679,6 +682,224 @@ void k_tile_pileup(
     }
 }
 
+
+// ------------------------------------------------------------------------------------------
+// KB: bit planes of the pile (once per staged batch, for KT's scan).  Row r of a tile holds W = T/32
+//     words of "valid call" bits, then W words of "valid call of another allele" bits; bit j of word
+//     w is position 32w + j of the tile.  The planes of a tile start at word (pile offset / 16).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void kb_planes(const uint8_t* __restrict__ pile, const TileInfo* __restrict__ tinfo,
+                                                 int64_t n_tiles, int32_t T, uint32_t* __restrict__ planes) {
+    const int lane = threadIdx.x & 63;
+    const int W = T >> 5;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t t = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6; t < n_tiles; t += nw) {
+        const TileInfo ti = tinfo[t];
+        uint32_t* dst = planes + (ti.off >> 4);
+        for (int64_t idx = lane; idx < (int64_t)ti.rows * W; idx += 64) {
+            const int64_t r = idx / W;
+            const int w = (int)(idx % W);
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(pile + ti.off + r * T + 32 * w);
+            uint32_t v = 0, x = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t d = src[k];
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const uint32_t c = (d >> (8 * b)) & 0xFFu;
+                    v |= ((c >> 7) & 1u) << (4 * k + b);
+                    x |= (((c & 0x80u) && (c & 0x60u)) ? 1u : 0u) << (4 * k + b);
+                }
+            }
+            dst[r * 2 * W + w] = v;
+            dst[r * 2 * W + W + w] = x;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// KT (bit planes): the single-sample scan over the planes instead of the byte pile -- a quarter of
+// the bytes.  Wave per tile, lane = row (groups of 64 rows); the candidates (a valid call of another
+// allele at a callable position) are the OR of the rows' second plane; a candidate's counts are
+// two ballots; the count bound and the exact integer bound are those of k_tile_pileup<0>, the exact
+// sums read the candidate's column from the byte pile.  The next tile's planes are in flight while
+// the current tile's candidates are examined.
+// ------------------------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(W >= 16 ? 2 : NGSEP_KT_WAVES_PER_EU)))
+void k_tile_planes(const uint32_t* __restrict__ planes, const uint8_t* __restrict__ pile, const TileInfo* __restrict__ tinfo,
+                   const uint8_t* __restrict__ ref, int64_t n_tiles, const LikTables* __restrict__ tabs, GenotypeParams gp,
+                   QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap,
+                   int32_t* __restrict__ bcount, int64_t nb) {
+    constexpr int T = W * 32;
+    constexpr int RB = W * 8;                       // plane bytes per row
+    __shared__ ScanShared sh;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (int64_t i = (int64_t)blockIdx.x * kScanThreads + threadIdx.x; i < nb; i += (int64_t)gridDim.x * kScanThreads) bcount[i] = 0;
+    if (threadIdx.x < 64) sh.w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
+    __syncthreads();
+    const long long th = tabs->t_het, to = tabs->t_homo;
+    const long long cr1 = tabs->c_r1, cr2 = tabs->c_r2, cx1 = tabs->c_x1, cx2 = tabs->c_x2;
+    const int32_t maxq = gp.max_q;
+    int32_t qn = 0;
+    unsigned long long ncand = 0;
+    uint32_t nexact = 0;
+    const int64_t nwaves = (int64_t)gridDim.x * kScanWaves;
+    const int64_t t0 = (int64_t)blockIdx.x * kScanWaves + wv;
+    auto load_rows = [&](int64_t off, int32_t rows, int g, uint32_t (&V)[W], uint32_t (&N)[W]) {
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(planes + (off >> 4)), 0, rows * RB, 0x00020000);
+        const int r = g * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < W / 4; k++) {
+            const u32x4 a = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, r * RB + 16 * k, 0, 0));
+            const u32x4 b = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, r * RB + 4 * W + 16 * k, 0, 0));
+            V[4 * k] = a.x; V[4 * k + 1] = a.y; V[4 * k + 2] = a.z; V[4 * k + 3] = a.w;
+            N[4 * k] = b.x; N[4 * k + 1] = b.y; N[4 * k + 2] = b.z; N[4 * k + 3] = b.w;
+        }
+    };
+    auto uni64 = [](int64_t v) -> int64_t {
+        return ((int64_t)__builtin_amdgcn_readfirstlane((int32_t)(v >> 32)) << 32) |
+               (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)v);
+    };
+    TileInfo cur = t0 < n_tiles ? tinfo[t0] : TileInfo{0, 0, 0};
+    TileInfo nxt = t0 + nwaves < n_tiles ? tinfo[t0 + nwaves] : TileInfo{0, 0, 0};
+    uint32_t Vn[W], Nn[W];
+#pragma unroll
+    for (int w = 0; w < W; w++) { Vn[w] = 0; Nn[w] = 0; }
+    if (t0 < n_tiles && !(gp.ablate & 4)) load_rows(uni64(cur.off), __builtin_amdgcn_readfirstlane(cur.rows), 0, Vn, Nn);
+    for (int64_t t = t0; t < n_tiles; t += nwaves) {
+        if (gp.ablate & 4) break;
+        const int32_t rows = __builtin_amdgcn_readfirstlane(cur.rows);
+        const int64_t off = uni64(cur.off);
+        uint32_t V[W], N[W];
+#pragma unroll
+        for (int w = 0; w < W; w++) { V[w] = Vn[w]; N[w] = Nn[w]; }
+        const int32_t tstart = (int32_t)(t * T);
+        uint32_t refb[T / 64];
+#pragma unroll
+        for (int k = 0; k < T / 64; k++) refb[k] = ref[tstart + 64 * k + lane];
+        // the next tile's descriptor is here: its planes are loaded while this tile is examined
+        const TileInfo nt = nxt;
+        if (t + 2 * nwaves < n_tiles) nxt = tinfo[t + 2 * nwaves];
+        if (t + nwaves < n_tiles) load_rows(uni64(nt.off), __builtin_amdgcn_readfirstlane(nt.rows), 0, Vn, Nn);
+        cur = nt;
+        if (rows == 0) continue;
+        const int ng = (rows + 63) >> 6;
+        uint32_t hv[W];
+#pragma unroll
+        for (int w = 0; w < W; w++) hv[w] = N[w];
+        for (int g = 1; g < ng; g++) {                 // deep tiles: further row groups
+            uint32_t V2[W], N2[W];
+            load_rows(off, rows, g, V2, N2);
+#pragma unroll
+            for (int w = 0; w < W; w++) hv[w] |= N2[w];
+        }
+#pragma unroll
+        for (int w = 0; w < W; w++)
+            for (int sft = 1; sft < 64; sft <<= 1) hv[w] |= __shfl_xor(hv[w], sft, 64);
+        uint32_t cm[W];
+#pragma unroll
+        for (int k = 0; k < T / 64; k++) {
+            const unsigned long long okm = __ballot((refb[k] & 0x80u) != 0);    // callable reference
+            cm[2 * k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(hv[2 * k] & (uint32_t)okm));
+            cm[2 * k + 1] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(hv[2 * k + 1] & (uint32_t)(okm >> 32)));
+        }
+#pragma unroll
+        for (int w = 0; w < W; w++) ncand += (unsigned long long)__popc(cm[w]);
+        if (gp.ablate & 1) continue;                   // diagnostics: scan only
+        const bool bound = gp.use_bound && rows <= 255;   // 32-bit halves of the exact sums cannot overflow
+        const bool multi = ng > 1;
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+            uint32_t c = cm[w];
+            while (c) {
+                const int j = __builtin_ctz(c);
+                c &= c - 1u;
+                const int p = 32 * w + j;
+                bool keep = true;
+                if (bound) {
+                    // count bound (as k_tile_pileup<0>): nr reference and na other valid calls
+                    long long cv = 0, ca = 0;
+                    if (!multi) {
+                        cv = __popcll(__ballot((V[w] >> j) & 1u));
+                        ca = __popcll(__ballot((N[w] >> j) & 1u));
+                    } else {
+                        const uint32_t* pl = planes + (off >> 4);
+                        for (int g = 0; g < ng; g++) {
+                            const int r = g * 64 + lane;
+                            const uint32_t v = r < rows ? pl[(int64_t)r * 2 * W + w] : 0u;
+                            const uint32_t x = r < rows ? pl[(int64_t)r * 2 * W + W + w] : 0u;
+                            cv += __popcll(__ballot((v >> j) & 1u));
+                            ca += __popcll(__ballot((x >> j) & 1u));
+                        }
+                    }
+                    const long long nr = cv - ca, na = ca;
+                    if (nr * cr1 - na * cx1 > th && nr * cr2 - na * cx2 > to && nr * cr2 - na * cx1 > th) {
+                        keep = false;
+                    } else {
+                        // exact integer bound over the candidate's column of the byte pile
+                        nexact++;
+                        unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+                        for (int g = 0; g < ng; g++) {
+                            const int r = g * 64 + lane;
+                            const uint32_t cd = r < rows ? (uint32_t)pile[off + (int64_t)r * T + p] : 0u;
+                            if (cd & 0x80u) {
+                                const uint32_t a = (cd >> 5) & 3u;
+                                int q = (int)(cd & 31u);
+                                q = q > maxq ? maxq : q;
+                                const unsigned long long wt = sh.w[a == 0 ? 0 : 1][q];
+                                a0 += a == 0 ? wt : 0ull;
+                                a1 += a == 1 ? wt : 0ull;
+                                a2 += a == 2 ? wt : 0ull;
+                                a3 += a == 3 ? wt : 0ull;
+                            }
+                        }
+                        for (int sft = 1; sft < 64; sft <<= 1) {
+                            a0 += __shfl_xor(a0, sft, 64);
+                            a1 += __shfl_xor(a1, sft, 64);
+                            a2 += __shfl_xor(a2, sft, 64);
+                            a3 += __shfl_xor(a3, sft, 64);
+                        }
+                        const long long R1 = (long long)(a0 & 0xFFFFFFFFull), R2 = (long long)(a0 >> 32);
+                        const long long x1 = (long long)(a1 & 0xFFFFFFFFull), y1 = (long long)(a2 & 0xFFFFFFFFull);
+                        const long long z1 = (long long)(a3 & 0xFFFFFFFFull);
+                        const long long x2 = (long long)(a1 >> 32), y2 = (long long)(a2 >> 32), z2 = (long long)(a3 >> 32);
+                        const bool drop = (R1 - x1 > th) && (R1 - y1 > th) && (R1 - z1 > th) &&
+                                          (R2 - x2 > to) && (R2 - y2 > to) && (R2 - z2 > to) &&
+                                          (R2 - x1 - y1 > th) && (R2 - x1 - z1 > th) && (R2 - y1 - z1 > th);
+                        keep = !drop;
+                    }
+                }
+                if (keep) {
+                    if (qn + 1 > kWaveQ) { wave_flush(sh, wv, lane, qn, queue, counters, qcap); qn = 0; }
+                    const uint32_t rcode = (uint32_t)__builtin_amdgcn_readlane((int)refb[w >> 1], p & 63);
+                    if (lane == 0) sh.q[wv][qn] = QueueSite{tstart + p, (int32_t)rcode};
+                    qn++;
+                }
+            }
+        }
+    }
+    // one global reservation per workgroup for what its waves staged; one statistics atomic
+    if (lane == 0) { sh.qn[wv] = qn; sh.ncand[wv] = ncand; sh.nexact[wv] = nexact; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t tot = 0;
+        unsigned long long nc = 0, ne = 0;
+        for (int w = 0; w < kScanWaves; w++) { sh.qbase[w] = tot; tot += sh.qn[w]; nc += sh.ncand[w]; ne += sh.nexact[w]; }
+        if (ne) atomicAdd(&counters[3], ne);
+        const unsigned long long base = tot ? atomicAdd(&counters[2], (unsigned long long)tot) : 0ull;
+        for (int w = 0; w < kScanWaves; w++) sh.qbase[w] += (int32_t)base;
+        if (nc) atomicAdd(&counters[1], nc);
+    }
+    __syncthreads();
+    {
+        const int64_t base = sh.qbase[wv];
+        for (int i = lane; i < qn; i += 64)
+            if (base + i < qcap) queue[base + i] = sh.q[wv][i];
+    }
+}
 
 // ------------------------------------------------------------------------------------------
 // KTM: multisample tile scan -- one wavefront per tile, the samples in turn
@@ -1418,6 +1639,8 @@ void device_release(Device* d) {
     d->n_collected = d->n_submitted;
     (void)hipFree(d->d_slots); d->d_slots = nullptr;
     (void)hipFree(d->d_pile); d->d_pile = nullptr;
+    (void)hipFree(d->d_planes); d->d_planes = nullptr;
+    d->planes_W = 0;
     (void)hipFree(d->d_reads); d->d_reads = nullptr;
     (void)hipFree(d->d_ref); d->d_ref = nullptr;
     (void)hipFree(d->d_lb); d->d_lb = nullptr;
@@ -1509,6 +1732,14 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
         hipLaunchKernelGGL(kl_read_index, grid, dim3(256), 0, d->stream, d->d_reads, d->n_reads, d->d_lb, d->n_lb, pad);
         HIP_TRY(hipGetLastError());
     }
+    // single-sample tiles of 128..512 positions: KT scans bit planes (NGSEP_NO_PLANES=1: the byte pile)
+    if (s.h_rows.empty() && s.n_tiles > 0 && (s.tile == 128 || s.tile == 256 || s.tile == 512) &&
+        std::getenv("NGSEP_NO_PLANES") == nullptr) {
+        HIP_TRY(hipMalloc(&d->d_planes, (size_t)std::max<int64_t>(s.pile_bytes / 4, 16)));
+        hipLaunchKernelGGL(kb_planes, dim3(1024), dim3(256), 0, d->stream, d->d_pile, d->d_tinfo, d->n_tiles, s.tile, d->d_planes);
+        HIP_TRY(hipGetLastError());
+        d->planes_W = s.tile / 32;
+    }
     HIP_TRY(hipStreamSynchronize(d->stream));
     return 0;
 }
@@ -1579,7 +1810,23 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         sl.tables_valid = true;
     }
     HIP_TRY(hipEventRecord(sl.ev[0], sl.stream));
-    if (d->n_tiles > 0) {
+    if (d->n_tiles > 0 && prune && d->planes_W) {
+        // bit-plane scan, persistent waves as below
+        const int wi = d->planes_W == 4 ? 0 : d->planes_W == 8 ? 1 : 2;
+        auto kt = wi == 0 ? (const void*)k_tile_planes<4> : wi == 1 ? (const void*)k_tile_planes<8> : (const void*)k_tile_planes<16>;
+        int& per_cu = d->kt_planes_per_cu[wi];
+        if (per_cu == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kt, kScanThreads, 0) != hipSuccess || per_cu < 1)) per_cu = 2;
+        int bpc = per_cu;
+        if (const char* e = std::getenv("NGSEP_BLOCKS_PER_CU")) bpc = std::max(1, std::atoi(e));   // tuning
+        const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((d->n_tiles + kScanWaves - 1) / kScanWaves, (int64_t)d->n_cu * bpc));
+        dim3 grid((unsigned)nblk);
+#define NGSEP_KTP_ARGS d->d_planes, d->d_pile, d->d_tinfo, d->d_ref, d->n_tiles, sl.d_tables, g, sl.d_hard, ctr, sl.cap_hard, sl.d_bcount, nb
+        if (wi == 0) hipLaunchKernelGGL(k_tile_planes<4>, grid, dim3(kScanThreads), 0, sl.stream, NGSEP_KTP_ARGS);
+        else if (wi == 1) hipLaunchKernelGGL(k_tile_planes<8>, grid, dim3(kScanThreads), 0, sl.stream, NGSEP_KTP_ARGS);
+        else hipLaunchKernelGGL(k_tile_planes<16>, grid, dim3(kScanThreads), 0, sl.stream, NGSEP_KTP_ARGS);
+#undef NGSEP_KTP_ARGS
+        HIP_TRY(hipGetLastError());
+    } else if (d->n_tiles > 0) {
         // persistent waves: as many workgroups as are co-resident (register-limited), each wave
         // walks the tiles with a grid stride, so at any moment the waves stream one contiguous
         // stretch of the pile

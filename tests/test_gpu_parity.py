@@ -193,3 +193,37 @@ def test_async_passes_identical(tmp_path):
     assert len(ref) > 1000
     for g in got:
         assert g == ref
+
+
+@pytest.mark.parametrize("tile", [64, 128, 256, 512])
+@pytest.mark.parametrize("depth,het", [(12, 0.05), (40, 0.1), (90, 0.001)])
+def test_tile_width_scan_paths(tmp_path, monkeypatch, tile, depth, het):
+    """Fixed tile widths: 128..512 take the bit-plane scan (one or several 64-row groups; above 255
+    rows no bound), 64 the byte-pile scan.  Pruned calls == genotyping every position."""
+    monkeypatch.setenv("NGSEP_TILE_T", str(tile))
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=1, depth=depth, seed=11, quality_model=2, snv_rate=3e-3)
+    res = []
+    for prune in (1, 0):
+        with GpuPileupSession(gpu_params(prune_candidates=prune, het_rate=het, min_quality=0)) as s:
+            for name, seq in syn.contigs():
+                s.set_reference(name, seq)
+            s.processAlignments(syn.batch())
+            s.notifyEndOfAlignments()
+            res.append([(x.sequence, x.pos, x.gq, x.qual, tuple(x.counts), tuple(x.logc)) for x in s.getCalledVariants()])
+            if prune:
+                st = s.stats()
+    assert st.tile_positions == tile
+    assert res[0] == res[1]
+    assert len(res[0]) > 100
+
+
+@pytest.mark.parametrize("tile", [128, 256, 512])
+def test_tile_width_vcf_identical(tmp_path, monkeypatch, tile):
+    """configs[0] data through each bit-plane tile width: VCF identical to the oracle's."""
+    monkeypatch.setenv("NGSEP_TILE_T", str(tile))
+    _, fa, sam, bam = make_data(tmp_path, genome=pysynth.YEAST, n_contigs=1, depth=10, seed=1)
+    o, _, _ = oracle_vcf(tmp_path, fa, sam)
+    g, gst = gpu_vcf_bam(tmp_path, fa, bam)
+    d = diff_vcf(o, g)
+    assert not d, "\n".join(d)
+    assert gst.tile_positions == tile
