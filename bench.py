@@ -175,10 +175,16 @@ def main():
     # a stream of passes, two in flight: pass k+1's kernels run while pass k's records are copied
     # back and mapped (ngsep_submit_staged / ngsep_collect_staged); every pass is collected
     sess.submit_staged()
+    t_sub = t_col = 0.0
     for k in range(args.steps):
+        t1 = time.perf_counter()
         if k + 1 < args.steps:
             sess.submit_staged()
+        t2 = time.perf_counter()
         sess.collect_staged()
+        t3 = time.perf_counter()
+        t_sub += t2 - t1
+        t_col += t3 - t2
         s = sess.stats()
         scan_ms.append(s.scan_ms)
         geno_ms.append(s.genotype_ms)
@@ -186,7 +192,24 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t_start
     st = sess.stats()
+    if os.environ.get("NGSEP_PROBE_HOST"):     # diagnostics: host cost of a collect whose pass is done
+        tc = ts = tt = 0.0
+        for _ in range(20):
+            t1 = time.perf_counter()
+            sess.submit_staged()
+            t2 = time.perf_counter()
+            time.sleep(0.003)
+            t3 = time.perf_counter()
+            sess.collect_staged()
+            t4 = time.perf_counter()
+            sess.stats()
+            t5 = time.perf_counter()
+            ts += t2 - t1
+            tc += t4 - t3
+            tt += t5 - t4
+        log(f"[rank {rank}] idle-GPU host cost: submit {ts / 20 * 1e3:.4f} ms, collect {tc / 20 * 1e3:.4f} ms, stats {tt / 20 * 1e3:.4f} ms")
     n_sites = st.sites_called
+    log(f"[rank {rank}] host per pass: submit {1e3 * t_sub / args.steps:.4f} ms, collect (incl. wait) {1e3 * t_col / args.steps:.4f} ms")
     log(f"[rank {rank}] tile {st.tile_positions} positions (max {st.tile_rows_max} rows), pile {st.pile_bytes} B, "
         f"slot {st.slot_size} B, {st.candidates} candidates, {st.exact_bound_passes} exact-bound passes, "
         f"{st.hard_sites} needed the exact tally + posterior")

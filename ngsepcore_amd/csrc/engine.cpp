@@ -89,6 +89,20 @@ void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g) {
         t->c_x1 = std::max<long long>(t->c_x1, (long long)(t->wX[q] & 0xFFFFFFFFull));
         t->c_x2 = std::max<long long>(t->c_x2, (long long)(t->wX[q] >> 32));
     }
+    // (the test is non-decreasing in nr: c_r1, c_r2 >= 0, so the first dropping nr is found by bisection)
+    auto drops = [t](long long nr, long long na) {
+        return nr * t->c_r1 - na * t->c_x1 > t->t_het && nr * t->c_r2 - na * t->c_x2 > t->t_homo &&
+               nr * t->c_r2 - na * t->c_x1 > t->t_het;
+    };
+    for (long long na = 0; na < 256; na++) {
+        long long lo = 0, hi = 256;          // first nr in [lo, hi] that drops; 256: none
+        while (lo < hi) {
+            const long long mid = (lo + hi) / 2;
+            if (drops(mid, na)) hi = mid;
+            else lo = mid + 1;
+        }
+        t->cb_nr[na] = (int16_t)lo;
+    }
 }
 
 // ReadAlignment.updateAlleleCallsInfo (ReadAlignment.java:747-834): allele-call length per read position.
@@ -914,25 +928,11 @@ int run_device(ngsep_ctx* c, double* elapsed_ms) {
     return finish_run(c, from, n, scan_ms, geno_ms, total_ms, ncand, elapsed_ms);
 }
 
-// records arrive sorted by global position; windows are laid out in processing order, so this is
-// (sequence order, position).  Map global coordinates back to (sequence, position) in place.
+// records arrive sorted by global position with their (sequence, position) set by KO; windows are
+// laid out in processing order, so this is (sequence order, position).
 static int finish_run(ngsep_ctx* c, size_t from, int64_t n, double scan_ms, double geno_ms, double total_ms,
                       int64_t ncand, double* elapsed_ms) {
-    const std::vector<Window>& ws = c->staged.windows;
-    size_t wi = 0, k = from;
-    for (int64_t i = 0; i < n; i++) {
-        ngsep_site_out& o = c->sites.buf[from + (size_t)i];
-        const int64_t gpos = o.pos;
-        while (wi + 1 < ws.size() && ws[wi + 1].gbase <= gpos) wi++;
-        const Window& w = ws[wi];
-        const int64_t off = gpos - w.gbase - w.pad;
-        if (off < 0 || off >= w.wlen) continue;
-        o.seq_id = w.seq_id;
-        o.pos = (int32_t)(w.w0 + off);
-        if (k != from + (size_t)i) c->sites.buf[k] = o;
-        k++;
-    }
-    c->sites.n = k;
+    c->sites.n = from + (size_t)n;
     if (c->params.calc_strand_bias) apply_strand_bias(c->sites, from);
     c->stats.candidates = ncand;
     c->stats.hard_sites = (int32_t)device_last_hard(c->dev);
@@ -1127,9 +1127,16 @@ extern "C" int ngsep_submit_staged(ngsep_ctx* c) {
         return rc;
     }
     if (device_inflight(c->dev) >= 2) return set_error(c, NGSEP_E_INVALID, "two staged runs already in flight: collect first");
-    LikTables t;
-    GenotypeParams gp;
-    compute_tables(c, &t, &gp);
+    // the tables depend only on the options: computed once per option set
+    if (!c->tables_cached || std::memcmp(&c->tables_params, &c->params, sizeof(ngsep_params)) != 0 ||
+        c->tables_het != c->het_rate) {
+        compute_tables(c, &c->tables_t, &c->tables_gp);
+        c->tables_params = c->params;
+        c->tables_het = c->het_rate;
+        c->tables_cached = true;
+    }
+    const LikTables& t = c->tables_t;
+    const GenotypeParams& gp = c->tables_gp;
     const int prune = c->params.prune_candidates && !c->params.dump_all_positions && c->het_rate <= 0.1;
     std::string err;
     if (device_submit(c->dev, c->staged, t, gp, prune, err) != 0) return set_error(c, NGSEP_E_DEVICE, err);
@@ -1149,9 +1156,24 @@ extern "C" int ngsep_collect_staged(ngsep_ctx* c, double* elapsed_ms) {
     int64_t n = 0, ncand = 0;
     double scan_ms = 0, geno_ms = 0, total_ms = 0;
     std::string err;
+    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    const auto h0 = std::chrono::steady_clock::now();
     if (device_collect(c->dev, &c->sites, &n, &scan_ms, &geno_ms, &total_ms, &ncand, err) != 0)
         return set_error(c, NGSEP_E_DEVICE, err);
-    return finish_run(c, 0, n, scan_ms, geno_ms, total_ms, ncand, elapsed_ms);
+    const auto h1 = std::chrono::steady_clock::now();
+    const int rc = finish_run(c, 0, n, scan_ms, geno_ms, total_ms, ncand, elapsed_ms);
+    if (host_timing) {
+        static double acc_c = 0, acc_f = 0;
+        static int cnt = 0;
+        acc_c += std::chrono::duration<double, std::micro>(h1 - h0).count();
+        acc_f += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h1).count();
+        if (++cnt == 20) {
+            std::fprintf(stderr, "[ngsep host] collect: device_collect %.1f us, finish_run %.1f us (avg of 20)\n", acc_c / 20, acc_f / 20);
+            acc_c = acc_f = 0;
+            cnt = 0;
+        }
+    }
+    return rc;
 }
 
 extern "C" int ngsep_release_staged(ngsep_ctx* c) {

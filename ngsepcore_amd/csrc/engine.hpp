@@ -73,6 +73,9 @@ struct LikTables {
     // count bound (kernels.hip phase 2): extreme addends over the qualities a valid call can carry
     long long c_r1, c_r2; // min over q of the low / high half of wR
     long long c_x1, c_x2; // max over q of the low / high half of wX
+    // the count bound as a table: with na other-allele calls, nr >= cb_nr[na] reference calls drop
+    // the candidate (the three inequalities are non-decreasing in nr); 256: never (nr, na <= 255)
+    int16_t cb_nr[256];
 };
 constexpr double kBoundScale = 1048576.0;   // 2^20: a tile holds <= 512 reads -> sums < 2^31
 constexpr long long kBoundMargin = 64;      // 6e-5 in log10 units, >> fp64 rounding of the sums
@@ -194,6 +197,12 @@ struct ngsep_ctx {
     int device = 0;
     std::string err;
     double het_rate = 0.001;
+    // compute_tables cache of the staged-run entry points (keyed by the options)
+    bool tables_cached = false;
+    ngsep_params tables_params{};
+    double tables_het = 0;
+    ngsep::LikTables tables_t{};
+    ngsep::GenotypeParams tables_gp{};
     // reference
     std::vector<std::string> seq_names;
     std::vector<std::string> seq_bases;      // case kept, masked to AaCcNngGtT

@@ -78,10 +78,13 @@ struct Device {
     // an event between KP and KO costs a few microseconds of idle GPU per pass: recorded only when
     // the posterior kernel's duration is asked for (NGSEP_TIME_POSTERIOR, diagnostics)
     bool time_posterior = std::getenv("NGSEP_TIME_POSTERIOR") != nullptr;
+    bool time_scan = std::getenv("NGSEP_NO_SCAN_TIMING") == nullptr;   // diagnostics: without KT's events
     hipEvent_t ev[4] = {};
     uint8_t* d_slots = nullptr;
     uint8_t* d_pile = nullptr;
     uint32_t* d_planes = nullptr;    // bit planes of the pile (KB), 0 when the tile width has none
+    int4* d_wins = nullptr;          // windows {global start of w0, w0, seq_id, wlen}, ascending (KO maps records)
+    int32_t n_wins = 0;
     int32_t planes_W = 0;            // words per plane row (T / 32)
     int4* d_reads = nullptr;
     uint8_t* d_ref = nullptr;
@@ -460,6 +463,7 @@ __device__ inline uint32_t unit_dword(const u32x4 d, int sel) {
 
 struct ScanShared {
     unsigned long long w[2][32];            // bound addends: [0] reference call, [1] other allele
+    int16_t cb[256];                        // count bound table (LikTables::cb_nr)
     QueueSite q[kScanWaves][kWaveQ];        // survivors staged per wave
     int32_t qn[kScanWaves];
     int32_t qbase[kScanWaves];
@@ -719,169 +723,262 @@ __global__ __launch_bounds__(256) void kb_planes(const uint8_t* __restrict__ pil
 
 // ------------------------------------------------------------------------------------------
 // KT (bit planes): the single-sample scan over the planes instead of the byte pile -- a quarter of
-// the bytes.  Wave per tile, lane = row (groups of 64 rows); the candidates (a valid call of another
-// allele at a callable position) are the OR of the rows' second plane; a candidate's counts are
-// two ballots; the count bound and the exact integer bound are those of k_tile_pileup<0>, the exact
-// sums read the candidate's column from the byte pile.  The next tile's planes are in flight while
-// the current tile's candidates are examined.
+// the bytes.  Wave per tile; lane = (word w, row group g), W words x G groups = 64 lanes: the lane
+// holds word w of rows g, g+G, ... (W rows of a 64-row chunk) and counts them bit-sliced (bit j of
+// count word k = bit k of position 32w+j's count), then a butterfly over the G groups adds the
+// groups' counts, so every lane has the chunk's valid / other-allele counts of its word's 32
+// positions.  Candidates (other-allele calls at a callable position) are split over the G lanes of
+// their word, the count bound (table cb_nr) runs lane-parallel, the rare survivors take the exact
+// integer bound of k_tile_pileup<0> over their column of the byte pile.  The next tile's planes and
+// reference bytes are in flight while a tile is examined.
 // ------------------------------------------------------------------------------------------
+// bit-sliced adders: out = a + b (k-bit numbers, k+1-bit result)
+template <int K>
+__device__ __forceinline__ void bs_add(const uint32_t* a, const uint32_t* b, uint32_t* out) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+        const uint32_t x = a[i] ^ b[i];
+        out[i] = x ^ c;
+        c = (a[i] & b[i]) | (c & x);
+    }
+    out[K] = c;
+}
+// out[0..log2(N)] = number of set bits among x[0..N) per bit position
+template <int N>
+struct BsCount {
+    static constexpr int B = BsCount<N / 2>::B + 1;
+    __device__ static __forceinline__ void run(const uint32_t* x, uint32_t* out) {
+        uint32_t lo[B - 1], hi[B - 1];
+        BsCount<N / 2>::run(x, lo);
+        BsCount<N / 2>::run(x + N / 2, hi);
+        bs_add<B - 1>(lo, hi, out);
+    }
+};
+template <>
+struct BsCount<1> {
+    static constexpr int B = 1;
+    __device__ static __forceinline__ void run(const uint32_t* x, uint32_t* out) { out[0] = x[0]; }
+};
+
 template <int W>
-__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(W >= 16 ? 2 : NGSEP_KT_WAVES_PER_EU)))
+__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(W >= 16 ? 3 : NGSEP_KT_WAVES_PER_EU)))
 void k_tile_planes(const uint32_t* __restrict__ planes, const uint8_t* __restrict__ pile, const TileInfo* __restrict__ tinfo,
                    const uint8_t* __restrict__ ref, int64_t n_tiles, const LikTables* __restrict__ tabs, GenotypeParams gp,
                    QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap,
                    int32_t* __restrict__ bcount, int64_t nb) {
     constexpr int T = W * 32;
-    constexpr int RB = W * 8;                       // plane bytes per row
+    constexpr int G = 64 / W;                       // row groups
+    constexpr int KB0 = BsCount<W>::B;              // bits of a lane's count (<= W rows)
+    constexpr int KC = 7;                           // bits of a 64-row chunk's count
     __shared__ ScanShared sh;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lw = lane & (W - 1), lg = lane / W;   // this lane's word and row group
     for (int64_t i = (int64_t)blockIdx.x * kScanThreads + threadIdx.x; i < nb; i += (int64_t)gridDim.x * kScanThreads) bcount[i] = 0;
     if (threadIdx.x < 64) sh.w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
+    sh.cb[threadIdx.x] = tabs->cb_nr[threadIdx.x];
     __syncthreads();
     const long long th = tabs->t_het, to = tabs->t_homo;
-    const long long cr1 = tabs->c_r1, cr2 = tabs->c_r2, cx1 = tabs->c_x1, cx2 = tabs->c_x2;
     const int32_t maxq = gp.max_q;
+    // this lane's share of its word's candidates: bits j with j % G == lg
+    const uint32_t share = (G == 4 ? 0x11111111u : G == 8 ? 0x01010101u : 0x00010001u) << lg;
     int32_t qn = 0;
-    unsigned long long ncand = 0;
-    uint32_t nexact = 0;
+    uint32_t my_cand = 0, nexact = 0;
     const int64_t nwaves = (int64_t)gridDim.x * kScanWaves;
     const int64_t t0 = (int64_t)blockIdx.x * kScanWaves + wv;
-    auto load_rows = [&](int64_t off, int32_t rows, int g, uint32_t (&V)[W], uint32_t (&N)[W]) {
+    auto load_chunk = [&](int64_t off, int32_t rows, int c, uint32_t (&V)[W], uint32_t (&N)[W]) {
         const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(planes + (off >> 4)), 0, rows * RB, 0x00020000);
-        const int r = g * 64 + lane;
+            __builtin_amdgcn_make_buffer_rsrc((void*)(planes + (off >> 4)), 0, rows * 8 * W, 0x00020000);
 #pragma unroll
-        for (int k = 0; k < W / 4; k++) {
-            const u32x4 a = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, r * RB + 16 * k, 0, 0));
-            const u32x4 b = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, r * RB + 4 * W + 16 * k, 0, 0));
-            V[4 * k] = a.x; V[4 * k + 1] = a.y; V[4 * k + 2] = a.z; V[4 * k + 3] = a.w;
-            N[4 * k] = b.x; N[4 * k + 1] = b.y; N[4 * k + 2] = b.z; N[4 * k + 3] = b.w;
+        for (int i = 0; i < W; i++) {
+            const int r = 64 * c + lg + G * i;
+            V[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, (r * 2 * W + lw) * 4, 0, 0);
+            N[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, (r * 2 * W + W + lw) * 4, 0, 0);
         }
     };
     auto uni64 = [](int64_t v) -> int64_t {
         return ((int64_t)__builtin_amdgcn_readfirstlane((int32_t)(v >> 32)) << 32) |
                (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)v);
     };
+    // chunk counts: lane-local bit-sliced count, then the butterfly over the row groups
+    auto chunk_count = [&](const uint32_t (&X)[W], uint32_t (&out)[KC]) {
+        uint32_t c[KC];
+#pragma unroll
+        for (int k = 0; k < KC; k++) c[k] = 0;
+        BsCount<W>::run(X, c);
+        int kb = KB0;
+#pragma unroll
+        for (int d = W; d < 64; d <<= 1) {
+            uint32_t o[KC], r[KC];
+#pragma unroll
+            for (int k = 0; k < KC; k++) o[k] = k < kb ? (uint32_t)__shfl_xor((int)c[k], d, 64) : 0u;
+            // kb-bit + kb-bit (unused high words are zero): a KC-bit ripple is exact
+            uint32_t cy = 0;
+#pragma unroll
+            for (int k = 0; k < KC; k++) {
+                const uint32_t x = c[k] ^ o[k];
+                r[k] = x ^ cy;
+                cy = (c[k] & o[k]) | (cy & x);
+            }
+#pragma unroll
+            for (int k = 0; k < KC; k++) c[k] = r[k];
+            kb++;
+        }
+#pragma unroll
+        for (int k = 0; k < KC; k++) out[k] = c[k];
+    };
     TileInfo cur = t0 < n_tiles ? tinfo[t0] : TileInfo{0, 0, 0};
     TileInfo nxt = t0 + nwaves < n_tiles ? tinfo[t0 + nwaves] : TileInfo{0, 0, 0};
-    uint32_t Vn[W], Nn[W];
+    uint32_t Vn[W], Nn[W], refn[T / 64];
 #pragma unroll
-    for (int w = 0; w < W; w++) { Vn[w] = 0; Nn[w] = 0; }
-    if (t0 < n_tiles && !(gp.ablate & 4)) load_rows(uni64(cur.off), __builtin_amdgcn_readfirstlane(cur.rows), 0, Vn, Nn);
+    for (int i = 0; i < W; i++) { Vn[i] = 0; Nn[i] = 0; }
+#pragma unroll
+    for (int k = 0; k < T / 64; k++) refn[k] = 0;
+    if (t0 < n_tiles && !(gp.ablate & 4)) {
+        load_chunk(uni64(cur.off), __builtin_amdgcn_readfirstlane(cur.rows), 0, Vn, Nn);
+#pragma unroll
+        for (int k = 0; k < T / 64; k++) refn[k] = ref[t0 * T + 64 * k + lane];
+    }
     for (int64_t t = t0; t < n_tiles; t += nwaves) {
         if (gp.ablate & 4) break;
         const int32_t rows = __builtin_amdgcn_readfirstlane(cur.rows);
         const int64_t off = uni64(cur.off);
-        uint32_t V[W], N[W];
+        uint32_t V[W], N[W], refb[T / 64];
 #pragma unroll
-        for (int w = 0; w < W; w++) { V[w] = Vn[w]; N[w] = Nn[w]; }
+        for (int i = 0; i < W; i++) { V[i] = Vn[i]; N[i] = Nn[i]; }
+#pragma unroll
+        for (int k = 0; k < T / 64; k++) refb[k] = refn[k];
         const int32_t tstart = (int32_t)(t * T);
-        uint32_t refb[T / 64];
-#pragma unroll
-        for (int k = 0; k < T / 64; k++) refb[k] = ref[tstart + 64 * k + lane];
-        // the next tile's descriptor is here: its planes are loaded while this tile is examined
+        // the next tile's descriptor is here: its planes and reference bytes load meanwhile
         const TileInfo nt = nxt;
         if (t + 2 * nwaves < n_tiles) nxt = tinfo[t + 2 * nwaves];
-        if (t + nwaves < n_tiles) load_rows(uni64(nt.off), __builtin_amdgcn_readfirstlane(nt.rows), 0, Vn, Nn);
+        if (t + nwaves < n_tiles) {
+            load_chunk(uni64(nt.off), __builtin_amdgcn_readfirstlane(nt.rows), 0, Vn, Nn);
+#pragma unroll
+            for (int k = 0; k < T / 64; k++) refn[k] = ref[(t + nwaves) * T + 64 * k + lane];
+        }
         cur = nt;
         if (rows == 0) continue;
         const int ng = (rows + 63) >> 6;
-        uint32_t hv[W];
+        const bool bound = gp.use_bound && rows <= 255;   // 32-bit halves of the exact sums cannot overflow
+        // counts (bit-sliced, 8 bits: rows <= 255) or, without the bound, the OR of the other-allele plane
+        uint32_t cv[8], ca[8], hits = 0;
 #pragma unroll
-        for (int w = 0; w < W; w++) hv[w] = N[w];
-        for (int g = 1; g < ng; g++) {                 // deep tiles: further row groups
-            uint32_t V2[W], N2[W];
-            load_rows(off, rows, g, V2, N2);
+        for (int k = 0; k < 8; k++) { cv[k] = 0; ca[k] = 0; }
+        for (int c = 0; c < ng; c++) {
+            if (c > 0) load_chunk(off, rows, c, V, N);
+            if (bound) {
+                uint32_t xv[KC], xa[KC];
+                chunk_count(V, xv);
+                chunk_count(N, xa);
+                if (c == 0) {
 #pragma unroll
-            for (int w = 0; w < W; w++) hv[w] |= N2[w];
+                    for (int k = 0; k < KC; k++) { cv[k] = xv[k]; ca[k] = xa[k]; }
+                } else {
+                    uint32_t sv[8], sa[8], zv[8], za[8];
+#pragma unroll
+                    for (int k = 0; k < 8; k++) { zv[k] = k < KC ? xv[k] : 0u; za[k] = k < KC ? xa[k] : 0u; }
+                    uint32_t tv[9], ta[9];
+                    bs_add<8>(cv, zv, tv);
+                    bs_add<8>(ca, za, ta);
+#pragma unroll
+                    for (int k = 0; k < 8; k++) { sv[k] = tv[k]; sa[k] = ta[k]; }
+#pragma unroll
+                    for (int k = 0; k < 8; k++) { cv[k] = sv[k]; ca[k] = sa[k]; }
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < W; i++) hits |= N[i];
+            }
         }
+        if (bound) {
 #pragma unroll
-        for (int w = 0; w < W; w++)
-            for (int sft = 1; sft < 64; sft <<= 1) hv[w] |= __shfl_xor(hv[w], sft, 64);
-        uint32_t cm[W];
+            for (int k = 0; k < 8; k++) hits |= ca[k];
+        } else {
+#pragma unroll
+            for (int d = W; d < 64; d <<= 1) hits |= (uint32_t)__shfl_xor((int)hits, d, 64);
+        }
+        // callable reference positions of this lane's word
+        uint32_t okw = 0;
 #pragma unroll
         for (int k = 0; k < T / 64; k++) {
-            const unsigned long long okm = __ballot((refb[k] & 0x80u) != 0);    // callable reference
-            cm[2 * k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(hv[2 * k] & (uint32_t)okm));
-            cm[2 * k + 1] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(hv[2 * k + 1] & (uint32_t)(okm >> 32)));
+            const unsigned long long okm = __ballot((refb[k] & 0x80u) != 0);
+            okw = lw == 2 * k ? (uint32_t)okm : okw;
+            okw = lw == 2 * k + 1 ? (uint32_t)(okm >> 32) : okw;
         }
-#pragma unroll
-        for (int w = 0; w < W; w++) ncand += (unsigned long long)__popc(cm[w]);
+        uint32_t mine = hits & okw & share;
+        my_cand += (uint32_t)__popc(mine);
         if (gp.ablate & 1) continue;                   // diagnostics: scan only
-        const bool bound = gp.use_bound && rows <= 255;   // 32-bit halves of the exact sums cannot overflow
-        const bool multi = ng > 1;
+        auto ref_code = [&](int p) -> uint32_t {       // p wave-uniform
+            uint32_t v = 0;
 #pragma unroll
-        for (int w = 0; w < W; w++) {
-            uint32_t c = cm[w];
-            while (c) {
-                const int j = __builtin_ctz(c);
-                c &= c - 1u;
-                const int p = 32 * w + j;
+            for (int k = 0; k < T / 64; k++) v = (p >> 6) == k ? (uint32_t)__builtin_amdgcn_readlane((int)refb[k], p & 63) : v;
+            return v;
+        };
+        auto emit_one = [&](int p) {                   // p wave-uniform
+            if (qn + 1 > kWaveQ) { wave_flush(sh, wv, lane, qn, queue, counters, qcap); qn = 0; }
+            const uint32_t rcode = ref_code(p);
+            if (lane == 0) sh.q[wv][qn] = QueueSite{tstart + p, (int32_t)rcode};
+            qn++;
+        };
+        while (__ballot(mine != 0)) {                  // wave-uniform loop over each lane's candidates
+            const bool has = mine != 0;
+            const int j = has ? __builtin_ctz(mine) : 0;
+            mine &= mine - 1u;
+            const int pp = 32 * lw + j;
+            bool need = has;
+            if (bound && has) {
+                uint32_t nv = 0, na = 0;
+#pragma unroll
+                for (int k = 0; k < 8; k++) { nv |= ((cv[k] >> j) & 1u) << k; na |= ((ca[k] >> j) & 1u) << k; }
+                need = (int32_t)(nv - na) < (int32_t)sh.cb[na];   // the count bound does not drop it
+            }
+            unsigned long long ex = __ballot(need);
+            if (gp.ablate & 128) ex = 0;                   // diagnostics: count bound only
+            while (ex) {
+                const int k = __builtin_ctzll(ex);
+                ex &= ex - 1ull;
+                const int p = __builtin_amdgcn_readlane(pp, k);
                 bool keep = true;
                 if (bound) {
-                    // count bound (as k_tile_pileup<0>): nr reference and na other valid calls
-                    long long cv = 0, ca = 0;
-                    if (!multi) {
-                        cv = __popcll(__ballot((V[w] >> j) & 1u));
-                        ca = __popcll(__ballot((N[w] >> j) & 1u));
-                    } else {
-                        const uint32_t* pl = planes + (off >> 4);
-                        for (int g = 0; g < ng; g++) {
-                            const int r = g * 64 + lane;
-                            const uint32_t v = r < rows ? pl[(int64_t)r * 2 * W + w] : 0u;
-                            const uint32_t x = r < rows ? pl[(int64_t)r * 2 * W + W + w] : 0u;
-                            cv += __popcll(__ballot((v >> j) & 1u));
-                            ca += __popcll(__ballot((x >> j) & 1u));
+                    nexact++;
+                    unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+                    for (int g = 0; g < ng; g++) {
+                        const int r = g * 64 + lane;
+                        const uint32_t cd = r < rows ? (uint32_t)pile[off + (int64_t)r * T + p] : 0u;
+                        if (cd & 0x80u) {
+                            const uint32_t a = (cd >> 5) & 3u;
+                            int q = (int)(cd & 31u);
+                            q = q > maxq ? maxq : q;
+                            const unsigned long long wt = sh.w[a == 0 ? 0 : 1][q];
+                            a0 += a == 0 ? wt : 0ull;
+                            a1 += a == 1 ? wt : 0ull;
+                            a2 += a == 2 ? wt : 0ull;
+                            a3 += a == 3 ? wt : 0ull;
                         }
                     }
-                    const long long nr = cv - ca, na = ca;
-                    if (nr * cr1 - na * cx1 > th && nr * cr2 - na * cx2 > to && nr * cr2 - na * cx1 > th) {
-                        keep = false;
-                    } else {
-                        // exact integer bound over the candidate's column of the byte pile
-                        nexact++;
-                        unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-                        for (int g = 0; g < ng; g++) {
-                            const int r = g * 64 + lane;
-                            const uint32_t cd = r < rows ? (uint32_t)pile[off + (int64_t)r * T + p] : 0u;
-                            if (cd & 0x80u) {
-                                const uint32_t a = (cd >> 5) & 3u;
-                                int q = (int)(cd & 31u);
-                                q = q > maxq ? maxq : q;
-                                const unsigned long long wt = sh.w[a == 0 ? 0 : 1][q];
-                                a0 += a == 0 ? wt : 0ull;
-                                a1 += a == 1 ? wt : 0ull;
-                                a2 += a == 2 ? wt : 0ull;
-                                a3 += a == 3 ? wt : 0ull;
-                            }
-                        }
-                        for (int sft = 1; sft < 64; sft <<= 1) {
-                            a0 += __shfl_xor(a0, sft, 64);
-                            a1 += __shfl_xor(a1, sft, 64);
-                            a2 += __shfl_xor(a2, sft, 64);
-                            a3 += __shfl_xor(a3, sft, 64);
-                        }
-                        const long long R1 = (long long)(a0 & 0xFFFFFFFFull), R2 = (long long)(a0 >> 32);
-                        const long long x1 = (long long)(a1 & 0xFFFFFFFFull), y1 = (long long)(a2 & 0xFFFFFFFFull);
-                        const long long z1 = (long long)(a3 & 0xFFFFFFFFull);
-                        const long long x2 = (long long)(a1 >> 32), y2 = (long long)(a2 >> 32), z2 = (long long)(a3 >> 32);
-                        const bool drop = (R1 - x1 > th) && (R1 - y1 > th) && (R1 - z1 > th) &&
-                                          (R2 - x2 > to) && (R2 - y2 > to) && (R2 - z2 > to) &&
-                                          (R2 - x1 - y1 > th) && (R2 - x1 - z1 > th) && (R2 - y1 - z1 > th);
-                        keep = !drop;
+                    for (int sft = 1; sft < 64; sft <<= 1) {
+                        a0 += __shfl_xor(a0, sft, 64);
+                        a1 += __shfl_xor(a1, sft, 64);
+                        a2 += __shfl_xor(a2, sft, 64);
+                        a3 += __shfl_xor(a3, sft, 64);
                     }
+                    const long long R1 = (long long)(a0 & 0xFFFFFFFFull), R2 = (long long)(a0 >> 32);
+                    const long long x1 = (long long)(a1 & 0xFFFFFFFFull), y1 = (long long)(a2 & 0xFFFFFFFFull);
+                    const long long z1 = (long long)(a3 & 0xFFFFFFFFull);
+                    const long long x2 = (long long)(a1 >> 32), y2 = (long long)(a2 >> 32), z2 = (long long)(a3 >> 32);
+                    keep = !((R1 - x1 > th) && (R1 - y1 > th) && (R1 - z1 > th) &&
+                             (R2 - x2 > to) && (R2 - y2 > to) && (R2 - z2 > to) &&
+                             (R2 - x1 - y1 > th) && (R2 - x1 - z1 > th) && (R2 - y1 - z1 > th));
                 }
-                if (keep) {
-                    if (qn + 1 > kWaveQ) { wave_flush(sh, wv, lane, qn, queue, counters, qcap); qn = 0; }
-                    const uint32_t rcode = (uint32_t)__builtin_amdgcn_readlane((int)refb[w >> 1], p & 63);
-                    if (lane == 0) sh.q[wv][qn] = QueueSite{tstart + p, (int32_t)rcode};
-                    qn++;
-                }
+                if (keep) emit_one(p);
             }
         }
     }
     // one global reservation per workgroup for what its waves staged; one statistics atomic
+    unsigned long long ncand = my_cand;
+    for (int sft = 1; sft < 64; sft <<= 1) ncand += __shfl_xor(ncand, sft, 64);
     if (lane == 0) { sh.qn[wv] = qn; sh.ncand[wv] = ncand; sh.nexact[wv] = nexact; }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1490,7 +1587,7 @@ __global__ __launch_bounds__(256) void kl_read_index(const int4* __restrict__ re
 constexpr int kKofBuckets = 16;
 __global__ __launch_bounds__(256) void ko_fused(const ngsep_site_out* __restrict__ brec, const int32_t* __restrict__ bcount,
                                                 int64_t nb, int32_t bcap, ngsep_site_out* __restrict__ sorted, int64_t cap,
-                                                unsigned long long* counters) {
+                                                unsigned long long* counters, const int4* __restrict__ wins, int32_t n_wins) {
     __shared__ int32_t s_red[4], s_mx[4];
     __shared__ int32_t s_cnt[kKofBuckets], s_off[kKofBuckets];
     __shared__ unsigned long long s_keys[4][1024];
@@ -1530,11 +1627,23 @@ __global__ __launch_bounds__(256) void ko_fused(const ngsep_site_out* __restrict
         if (c == 0) continue;
         const ngsep_site_out* src = brec + b * bcap;
         const int64_t off = base + s_off[j];
+        // the record lands with its (sequence, 1-based position): the window holding its global
+        // position (windows ascend; records only arise in window bodies, where the reference is non-zero)
         auto copy = [&](int32_t from, int64_t to) {
             if (to >= cap) return;
             const uint32_t* sw = reinterpret_cast<const uint32_t*>(src + from);
             uint32_t* dw = reinterpret_cast<uint32_t*>(sorted + to);
-            for (int w = 0; w < W; w++) dw[w] = sw[w];
+            const int32_t gpos = (int32_t)sw[1];
+            int32_t lo = 0, hi = n_wins - 1;
+            while (lo < hi) {
+                const int32_t mid = (lo + hi + 1) >> 1;
+                if (wins[mid].x <= gpos) lo = mid;
+                else hi = mid - 1;
+            }
+            const int4 wd = wins[lo];                 // {global start of w0, w0, seq_id, wlen}
+            dw[0] = (uint32_t)wd.z;
+            dw[1] = (uint32_t)(wd.y + (gpos - wd.x));
+            for (int w = 2; w < W; w++) dw[w] = sw[w];
         };
         if (c <= 64) {
             const unsigned long long mine = lane < c ? ((unsigned long long)(uint32_t)src[lane].pos << 32) | (uint32_t)lane : ~0ull;
@@ -1640,6 +1749,8 @@ void device_release(Device* d) {
     (void)hipFree(d->d_slots); d->d_slots = nullptr;
     (void)hipFree(d->d_pile); d->d_pile = nullptr;
     (void)hipFree(d->d_planes); d->d_planes = nullptr;
+    (void)hipFree(d->d_wins); d->d_wins = nullptr;
+    d->n_wins = 0;
     d->planes_W = 0;
     (void)hipFree(d->d_reads); d->d_reads = nullptr;
     (void)hipFree(d->d_ref); d->d_ref = nullptr;
@@ -1732,6 +1843,14 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
         hipLaunchKernelGGL(kl_read_index, grid, dim3(256), 0, d->stream, d->d_reads, d->n_reads, d->d_lb, d->n_lb, pad);
         HIP_TRY(hipGetLastError());
     }
+    {
+        std::vector<int4> wins;
+        for (const Window& w : s.windows) wins.push_back(int4{(int)(w.gbase + w.pad), w.w0, w.seq_id, w.wlen});
+        if (wins.empty()) wins.push_back(int4{0, 0, -1, 0});
+        HIP_TRY(hipMalloc(&d->d_wins, wins.size() * sizeof(int4)));
+        HIP_TRY(hipMemcpy(d->d_wins, wins.data(), wins.size() * sizeof(int4), hipMemcpyHostToDevice));
+        d->n_wins = (int32_t)wins.size();
+    }
     // single-sample tiles of 128..512 positions: KT scans bit planes (NGSEP_NO_PLANES=1: the byte pile)
     if (s.h_rows.empty() && s.n_tiles > 0 && (s.tile == 128 || s.tile == 256 || s.tile == 512) &&
         std::getenv("NGSEP_NO_PLANES") == nullptr) {
@@ -1809,7 +1928,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         HIP_TRY(hipMemcpyAsync(sl.d_tables, &sl.h_tables, sizeof(LikTables), hipMemcpyHostToDevice, sl.stream));
         sl.tables_valid = true;
     }
-    HIP_TRY(hipEventRecord(sl.ev[0], sl.stream));
+    if (d->time_scan) HIP_TRY(hipEventRecord(sl.ev[0], sl.stream));
     if (d->n_tiles > 0 && prune && d->planes_W) {
         // bit-plane scan, persistent waves as below
         const int wi = d->planes_W == 4 ? 0 : d->planes_W == 8 ? 1 : 2;
@@ -1849,7 +1968,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     } else {
         HIP_TRY(hipMemsetAsync(sl.d_bcount, 0, (size_t)nb * sizeof(int32_t), sl.stream));
     }
-    HIP_TRY(hipEventRecord(sl.ev[1], sl.stream));
+    if (d->time_scan || d->time_posterior) HIP_TRY(hipEventRecord(sl.ev[1], sl.stream));
 #ifdef NGSEP_KP_STAMPS
     if (!d->d_stamps) HIP_TRY(hipMalloc(&d->d_stamps, 16 * sizeof(unsigned long long)));
     {
@@ -1866,7 +1985,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     if (d->time_posterior) HIP_TRY(hipEventRecord(sl.ev[2], sl.stream));
     // order the records by position on the device (one kernel; counters[0] = records | max bucket << 40)
     hipLaunchKernelGGL(ko_fused, dim3((unsigned)((nb + kKofBuckets - 1) / kKofBuckets)), dim3(256), 0, sl.stream, sl.d_brec,
-                       sl.d_bcount, nb, bcap, sl.d_sorted, sl.cap, ctr);
+                       sl.d_bcount, nb, bcap, sl.d_sorted, sl.cap, ctr, d->d_wins, d->n_wins);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(sl.ev[3], sl.stream));
     // copies: counters and a prefix of the ordered records (sized from the previous run) straight into
@@ -1903,7 +2022,15 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
     HIP_TRY(hipSetDevice(d->ordinal));
     if (d->n_collected == d->n_submitted) { err = "no run to collect"; return -1; }
     RunSlot& sl = d->slot[d->n_collected % 2];
+    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    const auto h0 = std::chrono::steady_clock::now();
     HIP_TRY(hipEventSynchronize(sl.ev[4]));
+    if (host_timing) {
+        static double acc = 0;
+        static int cnt = 0;
+        acc += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();
+        if (++cnt == 20) { std::fprintf(stderr, "[ngsep host] event wait %.1f us\n", acc / 20); acc = 0; cnt = 0; }
+    }
     constexpr unsigned long long kNMask = (1ull << 40) - 1;
     int64_t n = (int64_t)(sl.h_ctr[0] & kNMask);
     int64_t mx = (int64_t)(sl.h_ctr[0] >> 40);          // fullest position bucket
@@ -1958,7 +2085,7 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
     sl.host.n = 0;
     *n_out = n;
     float a = 0, a2 = 0;
-    (void)hipEventElapsedTime(&a, sl.ev[0], sl.ev[1]);
+    if (d->time_scan) (void)hipEventElapsedTime(&a, sl.ev[0], sl.ev[1]);
     if (d->time_posterior) (void)hipEventElapsedTime(&a2, sl.ev[1], sl.ev[2]);
     *scan_ms = a;
     *geno_ms = a2;
