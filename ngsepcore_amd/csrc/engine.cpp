@@ -79,6 +79,7 @@ void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g) {
     t->t_het = (long long)std::floor(K * t_het) + kBoundMargin;
     t->t_homo = kBoundMargin;
     g->use_bound = ok && !g->dump_all && std::isfinite(t_het) ? 1 : 0;
+    g->exact_bound = std::getenv("NGSEP_KT_EXACT") != nullptr ? 1 : 0;
     // count bound: a valid call carries q in [4, 30] (engine.hpp code), capped at max_q in the kernel
     t->c_r1 = t->c_r2 = INT64_MAX;
     t->c_x1 = t->c_x2 = 0;

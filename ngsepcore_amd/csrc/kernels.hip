@@ -941,7 +941,7 @@ void k_tile_planes(const uint32_t* __restrict__ planes, const uint8_t* __restric
                 ex &= ex - 1ull;
                 const int p = __builtin_amdgcn_readlane(pp, k);
                 bool keep = true;
-                if (bound) {
+                if (bound && gp.exact_bound) {
                     nexact++;
                     unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
                     for (int g = 0; g < ng; g++) {
