@@ -19,6 +19,7 @@
 //
 // HBM-bound integer/byte work: no MFMA.  Layout and roofline: DESIGN.md.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <chrono>
@@ -59,7 +60,7 @@ struct RunSlot {                     // one in-flight single-sample run (see dev
     unsigned long long* d_ctr = nullptr;     // its counter set (4)
     unsigned long long* h_ctr = nullptr;     // pinned copy
     SiteStore host;                          // pinned D2H destination of the ordered records
-    hipEvent_t ev[5] = {};                   // before KT, after KT, after KP, after KO, copies done
+    hipEvent_t ev[6] = {};                   // KT start, KT end, KP end, after KO, copies done, KP start
     int64_t guess = 0;
     bool busy = false;
     int prune = 0;
@@ -807,19 +808,31 @@ void k_tile_planes(const uint32_t* __restrict__ planes, const uint8_t* __restric
 #pragma unroll
         for (int k = 0; k < KC; k++) c[k] = 0;
         BsCount<W>::run(X, c);
+        // all-reduce over the row groups (lanes w, w+W, ...) without LDS: DPP row rotations inside a
+        // 16-lane row (W = 4, 8), the gfx950 lane swaps across rows (16, 32); x + partner is the same
+        // bit-sliced sum on both sides
         int kb = KB0;
 #pragma unroll
         for (int d = W; d < 64; d <<= 1) {
-            uint32_t o[KC], r[KC];
+            uint32_t a[KC], o[KC], r[KC];
 #pragma unroll
-            for (int k = 0; k < KC; k++) o[k] = k < kb ? (uint32_t)__shfl_xor((int)c[k], d, 64) : 0u;
+            for (int k = 0; k < KC; k++) {
+                a[k] = c[k];
+                o[k] = 0;
+                if (k < kb) {
+                    if (d == 4) o[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)c[k], 0x124, 0xF, 0xF, false);        // row_ror:4
+                    else if (d == 8) o[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)c[k], 0x128, 0xF, 0xF, false);   // row_ror:8
+                    else if (d == 16) { const auto pr = __builtin_amdgcn_permlane16_swap(c[k], c[k], false, false); a[k] = pr[0]; o[k] = pr[1]; }
+                    else { const auto pr = __builtin_amdgcn_permlane32_swap(c[k], c[k], false, false); a[k] = pr[0]; o[k] = pr[1]; }
+                }
+            }
             // kb-bit + kb-bit (unused high words are zero): a KC-bit ripple is exact
             uint32_t cy = 0;
 #pragma unroll
             for (int k = 0; k < KC; k++) {
-                const uint32_t x = c[k] ^ o[k];
+                const uint32_t x = a[k] ^ o[k];
                 r[k] = x ^ cy;
-                cy = (c[k] & o[k]) | (cy & x);
+                cy = (a[k] & o[k]) | (cy & x);
             }
 #pragma unroll
             for (int k = 0; k < KC; k++) c[k] = r[k];
@@ -1584,20 +1597,21 @@ __global__ __launch_bounds__(256) void kl_read_index(const int4* __restrict__ re
 //     buckets sums the counts of the earlier buckets (its output offset), each wave ranks a
 //     bucket's keys and copies the records in order.  One kernel, no atomics, no global scan.
 // ------------------------------------------------------------------------------------------
-constexpr int kKofBuckets = 16;
-__global__ __launch_bounds__(256) void ko_fused(const ngsep_site_out* __restrict__ brec, const int32_t* __restrict__ bcount,
-                                                int64_t nb, int32_t bcap, ngsep_site_out* __restrict__ sorted, int64_t cap,
-                                                unsigned long long* counters, const int4* __restrict__ wins, int32_t n_wins) {
-    __shared__ int32_t s_red[4], s_mx[4];
+constexpr int kKofBuckets = 16;                // one wave per bucket, 16 waves per workgroup
+__global__ __launch_bounds__(1024) void ko_fused(const ngsep_site_out* __restrict__ brec, const int32_t* __restrict__ bcount,
+                                                 int64_t nb, int32_t bcap, ngsep_site_out* __restrict__ sorted, int64_t cap,
+                                                 unsigned long long* counters, const int4* __restrict__ wins, int32_t n_wins,
+                                                 int32_t bucket_span) {
+    __shared__ int32_t s_red[kKofBuckets], s_mx[kKofBuckets];
     __shared__ int32_t s_cnt[kKofBuckets], s_off[kKofBuckets];
-    __shared__ unsigned long long s_keys[4][1024];
+    __shared__ uint32_t s_pos[kKofBuckets][1024];   // crowded buckets only (> 64 records)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int64_t b0 = (int64_t)blockIdx.x * kKofBuckets;
     // offset of this block's records: the records of every earlier bucket (block 0: all, for the total)
     const bool all = blockIdx.x == 0;
     const int64_t lim = all ? nb : b0;
     int32_t part = 0, mx = 0;
-    for (int64_t b = tid; b < lim; b += 256) {
+    for (int64_t b = tid; b < lim; b += 1024) {
         const int32_t c = bcount[b];
         part += all || c < bcap ? c : bcap;
         mx = c > mx ? c : mx;
@@ -1606,64 +1620,86 @@ __global__ __launch_bounds__(256) void ko_fused(const ngsep_site_out* __restrict
     if (lane == 0) { s_red[wv] = part; s_mx[wv] = mx; }
     if (tid < kKofBuckets) s_cnt[tid] = b0 + tid < nb ? (bcount[b0 + tid] < bcap ? bcount[b0 + tid] : bcap) : 0;
     __syncthreads();
-    const int64_t total_before = (int64_t)s_red[0] + s_red[1] + s_red[2] + s_red[3];
+    int64_t total_before = 0;
+#pragma unroll
+    for (int k = 0; k < kKofBuckets; k++) total_before += s_red[k];
     if (tid == 0) {
         int32_t acc = 0;
         for (int j = 0; j < kKofBuckets; j++) { s_off[j] = acc; acc += s_cnt[j]; }
         if (all) {
             // every record KP emitted (block 0 summed all buckets) and the fullest bucket: above bcap the
             // host grows the buckets and runs again
-            const int32_t m = max(max(s_mx[0], s_mx[1]), max(s_mx[2], s_mx[3]));
+            int32_t m = 0;
+            for (int k = 0; k < kKofBuckets; k++) m = max(m, s_mx[k]);
             counters[0] = (unsigned long long)total_before | ((unsigned long long)m << 40);
         }
     }
     __syncthreads();
-    const int64_t base = all ? 0 : total_before;
-    constexpr int W = sizeof(ngsep_site_out) / 4;
-    for (int j = wv; j < kKofBuckets; j += 4) {
-        const int64_t b = b0 + j;
-        if (b >= nb) break;
-        const int32_t c = s_cnt[j];
-        if (c == 0) continue;
-        const ngsep_site_out* src = brec + b * bcap;
-        const int64_t off = base + s_off[j];
-        // the record lands with its (sequence, 1-based position): the window holding its global
-        // position (windows ascend; records only arise in window bodies, where the reference is non-zero)
-        auto copy = [&](int32_t from, int64_t to) {
-            if (to >= cap) return;
-            const uint32_t* sw = reinterpret_cast<const uint32_t*>(src + from);
-            uint32_t* dw = reinterpret_cast<uint32_t*>(sorted + to);
-            const int32_t gpos = (int32_t)sw[1];
-            int32_t lo = 0, hi = n_wins - 1;
-            while (lo < hi) {
-                const int32_t mid = (lo + hi + 1) >> 1;
-                if (wins[mid].x <= gpos) lo = mid;
-                else hi = mid - 1;
-            }
-            const int4 wd = wins[lo];                 // {global start of w0, w0, seq_id, wlen}
-            dw[0] = (uint32_t)wd.z;
-            dw[1] = (uint32_t)(wd.y + (gpos - wd.x));
-            for (int w = 2; w < W; w++) dw[w] = sw[w];
-        };
+    const int64_t b = b0 + wv;
+    if (b >= nb) return;
+    const int32_t c = s_cnt[wv];
+    if (c == 0) return;
+    const ngsep_site_out* src = brec + b * bcap;
+    const int64_t off = (all ? 0 : total_before) + s_off[wv];
+    // the last window starting at or before the bucket (wave-uniform); a record's window is that one or
+    // (rarely) a later one.  Records only arise in window bodies, where the reference is non-zero.
+    int32_t wb = 0;
+    {
+        const int32_t b0pos = (int32_t)(b * bucket_span);
+        int32_t hi = n_wins - 1;
+        while (wb < hi) {
+            const int32_t mid = (wb + hi + 1) >> 1;
+            if (wins[mid].x <= b0pos) wb = mid;
+            else hi = mid - 1;
+        }
+    }
+    constexpr int W = sizeof(ngsep_site_out) / 4;   // 38 dwords
+    // rank (position, then arrival) and the mapped (sequence, 1-based position) of record k, on lane k
+    // (c <= 64) or in rounds (crowded buckets)
+    for (int k0 = 0; k0 < c; k0 += 64) {
+        const int k = k0 + lane;
+        int32_t rank = 0, seq = 0, pos1 = 0;
+        uint32_t mine = 0;
+        if (k < c) {
+            mine = (uint32_t)src[k].pos;
+            int32_t wi = wb;
+            while (wi + 1 < n_wins && wins[wi + 1].x <= (int32_t)mine) wi++;
+            const int4 wd = wins[wi];                 // {global start of w0, w0, seq_id, wlen}
+            seq = wd.z;
+            pos1 = wd.y + ((int32_t)mine - wd.x);
+        }
         if (c <= 64) {
-            const unsigned long long mine = lane < c ? ((unsigned long long)(uint32_t)src[lane].pos << 32) | (uint32_t)lane : ~0ull;
-            int32_t rank = 0;
-            for (int k = 0; k < c; k++) rank += __shfl(mine, k, 64) < mine;
-            if (lane < c) copy(lane, off + rank);
-        } else {                                      // a crowded bucket (dump mode, -minQuality 0): keys via LDS
-            for (int k = lane; k < c; k += 64) s_keys[wv][k] = ((unsigned long long)(uint32_t)src[k].pos << 32) | (uint32_t)k;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (int k = lane; k < c; k += 64) {
-                const unsigned long long mine = s_keys[wv][k];
-                int32_t rank = 0;
-                for (int m = 0; m < c; m++) rank += s_keys[wv][m] < mine;
-                copy(k, off + rank);
+            for (int m = 0; m < c; m++) {
+                const uint32_t o = (uint32_t)__shfl((int)mine, m, 64);
+                rank += (o < mine || (o == mine && m < k)) ? 1 : 0;
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else {
+            if (k0 == 0) {                            // stage every key once
+                for (int m = lane; m < c; m += 64) s_pos[wv][m] = (uint32_t)src[m].pos;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            if (k < c)
+                for (int m = 0; m < c; m++) {
+                    const uint32_t o = s_pos[wv][m];
+                    rank += (o < mine || (o == mine && m < k)) ? 1 : 0;
+                }
+        }
+        // cooperative copy of this round's records: 38 consecutive lanes per record, coalesced
+        const int nr = min(64, c - k0);
+        for (int i0 = 0; i0 < nr * W; i0 += 64) {     // wave-uniform trip count: the shuffles see every lane
+            const int idx = i0 + lane;
+            const int r = min(idx / W, 63), w = idx - (idx / W) * W;
+            const int32_t rk = __shfl(rank, r, 64);
+            const int32_t sq = __shfl(seq, r, 64);
+            const int32_t p1 = __shfl(pos1, r, 64);
+            if (idx < nr * W) {
+                const int64_t to = off + rk;
+                const uint32_t v = w == 0 ? (uint32_t)sq : w == 1 ? (uint32_t)p1
+                                                                  : reinterpret_cast<const uint32_t*>(src + k0 + r)[w];
+                if (to < cap) reinterpret_cast<uint32_t*>(sorted + to)[w] = v;
+            }
         }
     }
 }
@@ -1715,8 +1751,8 @@ Device* device_create(int ordinal, std::string& err) {
         if (one_stream) sl.stream = d->stream;
         else if (hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess) { err = "stream"; return nullptr; }
         if (hipMalloc(&sl.d_tables, sizeof(LikTables)) != hipSuccess) { err = "device allocation failed"; return nullptr; }
-        for (int k = 0; k < 5; k++)     // 0-2 time the kernels; 3-4 only order the streams
-            (void)hipEventCreateWithFlags(&sl.ev[k], k < 3 ? hipEventDefault : hipEventDisableTiming);
+        for (int k = 0; k < 6; k++)     // 0-2 and 5 time the kernels; 3-4 only order the streams
+            (void)hipEventCreateWithFlags(&sl.ev[k], (k < 3 || k == 5) ? hipEventDefault : hipEventDisableTiming);
     }
     if (hipMalloc(&d->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(d->d_counters, 0, 16 * sizeof(unsigned long long)) != hipSuccess ||
@@ -1928,7 +1964,8 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         HIP_TRY(hipMemcpyAsync(sl.d_tables, &sl.h_tables, sizeof(LikTables), hipMemcpyHostToDevice, sl.stream));
         sl.tables_valid = true;
     }
-    if (d->time_scan) HIP_TRY(hipEventRecord(sl.ev[0], sl.stream));
+    // KT is timed by events bound to its dispatch (hipExtLaunchKernelGGL): the kernel's own start and end
+    hipEvent_t k0 = d->time_scan ? sl.ev[0] : nullptr, k1 = d->time_scan ? sl.ev[1] : nullptr;
     if (d->n_tiles > 0 && prune && d->planes_W) {
         // bit-plane scan, persistent waves as below
         const int wi = d->planes_W == 4 ? 0 : d->planes_W == 8 ? 1 : 2;
@@ -1940,9 +1977,9 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((d->n_tiles + kScanWaves - 1) / kScanWaves, (int64_t)d->n_cu * bpc));
         dim3 grid((unsigned)nblk);
 #define NGSEP_KTP_ARGS d->d_planes, d->d_pile, d->d_tinfo, d->d_ref, d->n_tiles, sl.d_tables, g, sl.d_hard, ctr, sl.cap_hard, sl.d_bcount, nb
-        if (wi == 0) hipLaunchKernelGGL(k_tile_planes<4>, grid, dim3(kScanThreads), 0, sl.stream, NGSEP_KTP_ARGS);
-        else if (wi == 1) hipLaunchKernelGGL(k_tile_planes<8>, grid, dim3(kScanThreads), 0, sl.stream, NGSEP_KTP_ARGS);
-        else hipLaunchKernelGGL(k_tile_planes<16>, grid, dim3(kScanThreads), 0, sl.stream, NGSEP_KTP_ARGS);
+        if (wi == 0) hipExtLaunchKernelGGL(k_tile_planes<4>, grid, dim3(kScanThreads), 0, sl.stream, k0, k1, 0, NGSEP_KTP_ARGS);
+        else if (wi == 1) hipExtLaunchKernelGGL(k_tile_planes<8>, grid, dim3(kScanThreads), 0, sl.stream, k0, k1, 0, NGSEP_KTP_ARGS);
+        else hipExtLaunchKernelGGL(k_tile_planes<16>, grid, dim3(kScanThreads), 0, sl.stream, k0, k1, 0, NGSEP_KTP_ARGS);
 #undef NGSEP_KTP_ARGS
         HIP_TRY(hipGetLastError());
     } else if (d->n_tiles > 0) {
@@ -1957,18 +1994,19 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((d->n_tiles + kScanWaves - 1) / kScanWaves, (int64_t)d->n_cu * bpc));
         dim3 grid((unsigned)nblk);
         if (prune)
-            hipLaunchKernelGGL(k_tile_pileup<0>, grid, dim3(kScanThreads), 0, sl.stream, (const u32x4*)d->d_pile,
-                               d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, sl.d_tables, g, sl.d_hard, ctr, sl.cap_hard,
-                               sl.d_bcount, nb);
+            hipExtLaunchKernelGGL(k_tile_pileup<0>, grid, dim3(kScanThreads), 0, sl.stream, k0, k1, 0, (const u32x4*)d->d_pile,
+                                  d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, sl.d_tables, g, sl.d_hard, ctr, sl.cap_hard,
+                                  sl.d_bcount, nb);
         else
-            hipLaunchKernelGGL(k_tile_pileup<1>, grid, dim3(kScanThreads), 0, sl.stream, (const u32x4*)d->d_pile,
-                               d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, sl.d_tables, g, sl.d_hard, ctr, sl.cap_hard,
-                               sl.d_bcount, nb);
+            hipExtLaunchKernelGGL(k_tile_pileup<1>, grid, dim3(kScanThreads), 0, sl.stream, k0, k1, 0, (const u32x4*)d->d_pile,
+                                  d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, sl.d_tables, g, sl.d_hard, ctr, sl.cap_hard,
+                                  sl.d_bcount, nb);
         HIP_TRY(hipGetLastError());
     } else {
+        if (k0) HIP_TRY(hipEventRecord(k0, sl.stream));
         HIP_TRY(hipMemsetAsync(sl.d_bcount, 0, (size_t)nb * sizeof(int32_t), sl.stream));
+        if (k1) HIP_TRY(hipEventRecord(k1, sl.stream));
     }
-    if (d->time_scan || d->time_posterior) HIP_TRY(hipEventRecord(sl.ev[1], sl.stream));
 #ifdef NGSEP_KP_STAMPS
     if (!d->d_stamps) HIP_TRY(hipMalloc(&d->d_stamps, 16 * sizeof(unsigned long long)));
     {
@@ -1978,14 +2016,15 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     }
 #endif
     static const int kp_grid = std::getenv("NGSEP_KP_GRID") ? std::max(1, std::atoi(std::getenv("NGSEP_KP_GRID"))) : 2048;   // tuning
-    hipLaunchKernelGGL(k_posterior, dim3(kp_grid), dim3(kPostWaves * 64), 0, sl.stream, sl.d_hard, ctr + 2, sl.cap_hard,
-                       d->d_reads, d->n_reads, d->d_lb, d->d_slots, d->slot_size, sl.d_tables, g, sl.d_brec,
-                       sl.d_bcount, shift, bcap, d->d_stamps);
+    hipExtLaunchKernelGGL(k_posterior, dim3(kp_grid), dim3(kPostWaves * 64), 0, sl.stream,
+                          d->time_posterior ? sl.ev[5] : nullptr, d->time_posterior ? sl.ev[2] : nullptr, 0,
+                          (const QueueSite*)sl.d_hard, (const unsigned long long*)(ctr + 2), sl.cap_hard,
+                          (const int4*)d->d_reads, d->n_reads, (const int32_t*)d->d_lb, (const uint8_t*)d->d_slots,
+                          d->slot_size, (const LikTables*)sl.d_tables, g, sl.d_brec, sl.d_bcount, shift, bcap, d->d_stamps);
     HIP_TRY(hipGetLastError());
-    if (d->time_posterior) HIP_TRY(hipEventRecord(sl.ev[2], sl.stream));
     // order the records by position on the device (one kernel; counters[0] = records | max bucket << 40)
-    hipLaunchKernelGGL(ko_fused, dim3((unsigned)((nb + kKofBuckets - 1) / kKofBuckets)), dim3(256), 0, sl.stream, sl.d_brec,
-                       sl.d_bcount, nb, bcap, sl.d_sorted, sl.cap, ctr, d->d_wins, d->n_wins);
+    hipLaunchKernelGGL(ko_fused, dim3((unsigned)((nb + kKofBuckets - 1) / kKofBuckets)), dim3(64 * kKofBuckets), 0, sl.stream, sl.d_brec,
+                       sl.d_bcount, nb, bcap, sl.d_sorted, sl.cap, ctr, d->d_wins, d->n_wins, 1 << shift);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(sl.ev[3], sl.stream));
     // copies: counters and a prefix of the ordered records (sized from the previous run) straight into
@@ -2086,7 +2125,7 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
     *n_out = n;
     float a = 0, a2 = 0;
     if (d->time_scan) (void)hipEventElapsedTime(&a, sl.ev[0], sl.ev[1]);
-    if (d->time_posterior) (void)hipEventElapsedTime(&a2, sl.ev[1], sl.ev[2]);
+    if (d->time_posterior) (void)hipEventElapsedTime(&a2, sl.ev[5], sl.ev[2]);
     *scan_ms = a;
     *geno_ms = a2;
     *total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - sl.t0).count();
@@ -2148,22 +2187,26 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     }
     unsigned long long* ctr = d->d_counters;
     HIP_TRY(hipMemsetAsync(ctr, 0, 4 * sizeof(unsigned long long), d->stream));
-    HIP_TRY(hipEventRecord(d->ev[0], d->stream));
+    // KTM and KPM are timed by events bound to their dispatches (ev 0-1 and 3-2)
     if (d->n_tiles > 0) {
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_tile_pileup_multi, kScanThreads, 0) != hipSuccess || per_cu < 1) per_cu = 2;
         const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>(d->n_tiles, (int64_t)d->n_cu * per_cu));
-        hipLaunchKernelGGL(k_tile_pileup_multi, dim3((unsigned)nblk), dim3(kScanThreads), 0, d->stream, (const u32x4*)d->d_pile,
-                           d->d_toff, d->d_rows, S, d->d_ref, d->log2_tile, d->n_tiles, d->d_tables, g, d->d_hard, ctr,
-                           d->cap_hard);
+        hipExtLaunchKernelGGL(k_tile_pileup_multi, dim3((unsigned)nblk), dim3(kScanThreads), 0, d->stream, d->ev[0], d->ev[1], 0,
+                              (const u32x4*)d->d_pile, (const int64_t*)d->d_toff, (const uint16_t*)d->d_rows, S,
+                              (const uint8_t*)d->d_ref, d->log2_tile, d->n_tiles, (const LikTables*)d->d_tables, g, d->d_hard,
+                              ctr, d->cap_hard);
         HIP_TRY(hipGetLastError());
+    } else {
+        HIP_TRY(hipEventRecord(d->ev[0], d->stream));
+        HIP_TRY(hipEventRecord(d->ev[1], d->stream));
     }
-    HIP_TRY(hipEventRecord(d->ev[1], d->stream));
-    hipLaunchKernelGGL(k_posterior_multi, dim3(2048), dim3(kPopThreads), 0, d->stream, d->d_hard, ctr + 2, d->cap_hard,
-                       d->d_reads, d->d_perm, d->d_bseg, d->d_blb, d->nblk_b, d->d_bbase, d->d_slots, d->slot_size,
-                       d->d_tables, g, S, min_adf, ploidy, d->d_psites, d->d_pcalls, ctr, d->cap_psites, d->d_stamps);
+    hipExtLaunchKernelGGL(k_posterior_multi, dim3(2048), dim3(kPopThreads), 0, d->stream, d->ev[3], d->ev[2], 0,
+                          (const QueueSite*)d->d_hard, (const unsigned long long*)(ctr + 2), d->cap_hard, (const int4*)d->d_reads,
+                          (const int32_t*)d->d_perm, (const int32_t*)d->d_bseg, (const int32_t*)d->d_blb, d->nblk_b,
+                          (const int32_t*)d->d_bbase, (const uint8_t*)d->d_slots, d->slot_size, (const LikTables*)d->d_tables, g,
+                          S, min_adf, ploidy, d->d_psites, d->d_pcalls, ctr, d->cap_psites, d->d_stamps);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(d->ev[2], d->stream));
     HIP_TRY(hipMemcpyAsync(d->h_counters, ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, d->stream));
     HIP_TRY(hipStreamSynchronize(d->stream));
     const unsigned long long c3 = d->h_counters[3];
@@ -2199,7 +2242,7 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     }
     float a = 0, a2 = 0;
     (void)hipEventElapsedTime(&a, d->ev[0], d->ev[1]);
-    (void)hipEventElapsedTime(&a2, d->ev[1], d->ev[2]);
+    (void)hipEventElapsedTime(&a2, d->ev[3], d->ev[2]);
     *scan_ms = a;
     *geno_ms = a2;
     *total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -8,10 +8,10 @@ if [ -z "$SKIP_TESTS" ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1
 timeout -k 10 300 python -u __graft_entry__.py smoke > gpurun_out/smoke_$TAG.log 2>&1
 fi
-timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf_$TAG -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/pmcf_$TAG.out 2>&1
-timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw_$TAG -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/pmcw_$TAG.out 2>&1
-python tools/pmc_traffic.py gpurun_out/pmcf_$TAG gpurun_out/pmcw_$TAG k_tile_pileup yeast:30x:seed2 gpurun_out/pmc_traffic_$TAG.json
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf_$TAG -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cold > gpurun_out/pmcf_$TAG.out 2>&1
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw_$TAG -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cold > gpurun_out/pmcw_$TAG.out 2>&1
+python tools/pmc_traffic.py gpurun_out/pmcf_$TAG gpurun_out/pmcw_$TAG k_tile_p yeast:30x:seed2 gpurun_out/pmc_traffic_$TAG.json
 cp gpurun_out/pmc_traffic_$TAG.json profiles/pmc_traffic.json
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof_$TAG.out 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-cold > gpurun_out/prof_$TAG.out 2>&1
 echo done
