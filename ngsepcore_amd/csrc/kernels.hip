@@ -197,6 +197,7 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
 #endif
     __shared__ double s_t[3][32];
     __shared__ uint8_t s_code[kPostWaves][64];      // a chunk's valid codes in read order
+    __shared__ uint32_t s_rec[kPostWaves][sizeof(ngsep_site_out) / 4];   // the record awaiting its bucket slot
     if (threadIdx.x < 96)
         s_t[threadIdx.x >> 5][threadIdx.x & 31] =
             (threadIdx.x < 32 ? tabs->A : threadIdx.x < 64 ? tabs->H : tabs->E)[threadIdx.x & 31];
@@ -210,6 +211,22 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
     // a read of allele a adds table tm[q] when bit a of am is set, else E[q] (CountsHelper.java:231-248)
     const uint32_t am = lane < 4 ? 1u << lane : lane < 10 ? (0xCA6953u >> (4 * (lane - 4))) & 15u : 0u;
     const int tm = lane < 4 ? 0 : 1;
+    // the wave's staged record (s_rec[wv]) and its bucket slot request; lanes 0..37 store it
+    bool pending = false;
+    int32_t pend_k = 0, pend_bk = 0;
+    auto flush_pending = [&]() {
+        if (!pending) return;
+        const int32_t k = __builtin_amdgcn_readfirstlane(pend_k);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        constexpr int RW = sizeof(ngsep_site_out) / 4;
+        if (k < bcap && lane < RW) reinterpret_cast<uint32_t*>(brec + (int64_t)pend_bk * bcap + k)[lane] = s_rec[wv][lane];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        pending = false;
+    };
     auto load_h = [&](int64_t r0) -> int4 {
         const int64_t r = r0 + lane;
         return r < n_reads ? reads[r] : int4{INT32_MAX, 0, 0, 0};
@@ -368,35 +385,46 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
         st_b += t2 - t1;
 #endif
         if (!keep && !gp.dump_all) continue;
-        // the record goes to its position bucket (KO orders each bucket; no global reservation): lane 0
-        // writes the header, sum lane m its log-likelihood (logc order 00 01 02 03 11 12 13 22 23 33)
+        // the record goes to its position bucket (KO orders each bucket; no global reservation).  The
+        // slot's atomic is issued now and the record is staged in LDS; it is stored at the wave's next
+        // record (or at the end), so the atomic's round trip overlaps the next site
         {
             const int32_t bk = gpos >> shift;
             int32_t k = 0;
             if (lane == 0) k = atomicAdd(&bcount[bk], 1);
-            k = __builtin_amdgcn_readfirstlane(k);
-            if (k < bcap) {
-                ngsep_site_out* dst = brec + (int64_t)bk * bcap + k;
-                if (lane == 0) {
-                    const uint32_t ref = callable ? (uint32_t)(uint8_t)"ACGT"[(rc >> 5) & 3] : (uint32_t)'N';
-                    uint2* h8 = reinterpret_cast<uint2*>(dst);
-                    h8[0] = uint2{0xFFFFFFFFu, (uint32_t)gpos};
-                    h8[1] = uint2{ref | (uint32_t)(uint8_t)nal << 8 | (uint32_t)(uint8_t)alt << 16 | (uint32_t)(uint8_t)third << 24,
-                                  (uint32_t)(uint8_t)genotype | 0xFF00u | (uint32_t)(uint16_t)gq << 16};
-                    h8[2] = uint2{(uint32_t)(uint16_t)qual | (uint32_t)(keep ? 1 : 0) << 16, (uint32_t)total};
-                    h8[3] = uint2{(uint32_t)cnt[0], (uint32_t)cnt[1]};
-                    h8[4] = uint2{(uint32_t)cnt[2], (uint32_t)cnt[3]};
+            flush_pending();
+            if (lane == 0) {
+                const uint32_t ref = callable ? (uint32_t)(uint8_t)"ACGT"[(rc >> 5) & 3] : (uint32_t)'N';
+                uint32_t* h = s_rec[wv];
+                h[0] = 0xFFFFFFFFu;
+                h[1] = (uint32_t)gpos;
+                h[2] = ref | (uint32_t)(uint8_t)nal << 8 | (uint32_t)(uint8_t)alt << 16 | (uint32_t)(uint8_t)third << 24;
+                h[3] = (uint32_t)(uint8_t)genotype | 0xFF00u | (uint32_t)(uint16_t)gq << 16;
+                h[4] = (uint32_t)(uint16_t)qual | (uint32_t)(keep ? 1 : 0) << 16;
+                h[5] = (uint32_t)total;
 #pragma unroll
-                    for (int t = 0; t < 4; t++) h8[5 + t] = uint2{(uint32_t)sc[t][0], (uint32_t)sc[t][1]};
+                for (int t = 0; t < 4; t++) {
+                    h[6 + t] = (uint32_t)cnt[t];
+                    h[10 + 2 * t] = (uint32_t)sc[t][0];
+                    h[11 + 2 * t] = (uint32_t)sc[t][1];
                 }
-                if (lane < 10) dst->logc[(0x8653219740ull >> (4 * lane)) & 15u] = acc;
             }
+            if (lane < 10) {
+                const int li = (int)((0x8653219740ull >> (4 * lane)) & 15u);
+                const unsigned long long bits = __builtin_bit_cast(unsigned long long, acc);
+                s_rec[wv][18 + 2 * li] = (uint32_t)bits;
+                s_rec[wv][19 + 2 * li] = (uint32_t)(bits >> 32);
+            }
+            pend_k = k;
+            pend_bk = bk;
+            pending = true;
         }
 #ifdef NGSEP_KP_STAMPS
         KP_STAMP(t3);
         st_c += t3 - t2;
 #endif
     }
+    flush_pending();
 #ifdef NGSEP_KP_STAMPS
     if (lane == 0 && stamps) {
         const unsigned long long w1 = __builtin_amdgcn_s_memtime();
@@ -2026,16 +2054,19 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     hipLaunchKernelGGL(ko_fused, dim3((unsigned)((nb + kKofBuckets - 1) / kKofBuckets)), dim3(64 * kKofBuckets), 0, sl.stream, sl.d_brec,
                        sl.d_bcount, nb, bcap, sl.d_sorted, sl.cap, ctr, d->d_wins, d->n_wins, 1 << shift);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(sl.ev[3], sl.stream));
     // copies: counters and a prefix of the ordered records (sized from the previous run) straight into
-    // the slot's pinned store, then the counter set is cleared for the slot's next run
+    // the slot's pinned store, then the counter set is cleared for the slot's next run.  On the copy
+    // stream (ordered after KO by ev[3]) or, with NGSEP_COPY_ON_COMPUTE=1, on the compute stream
+    static const bool on_compute = std::getenv("NGSEP_COPY_ON_COMPUTE") != nullptr;   // diagnostics
+    hipStream_t cs = on_compute ? sl.stream : d->copy_stream;
+    if (!on_compute) HIP_TRY(hipEventRecord(sl.ev[3], sl.stream));
     sl.guess = std::min<int64_t>(d->cap_sites, d->last_n_sites + d->last_n_sites / 64 + 64);
     sl.host.reserve((size_t)sl.guess);
-    HIP_TRY(hipStreamWaitEvent(d->copy_stream, sl.ev[3], 0));
-    HIP_TRY(hipMemcpyAsync(sl.h_ctr, ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, d->copy_stream));
-    HIP_TRY(hipMemcpyAsync(sl.host.buf, sl.d_sorted, (size_t)sl.guess * sizeof(ngsep_site_out), hipMemcpyDeviceToHost, d->copy_stream));
-    HIP_TRY(hipMemsetAsync(ctr, 0, 4 * sizeof(unsigned long long), d->copy_stream));
-    HIP_TRY(hipEventRecord(sl.ev[4], d->copy_stream));
+    if (!on_compute) HIP_TRY(hipStreamWaitEvent(cs, sl.ev[3], 0));
+    HIP_TRY(hipMemcpyAsync(sl.h_ctr, ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemcpyAsync(sl.host.buf, sl.d_sorted, (size_t)sl.guess * sizeof(ngsep_site_out), hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemsetAsync(ctr, 0, 4 * sizeof(unsigned long long), cs));
+    HIP_TRY(hipEventRecord(sl.ev[4], cs));
     sl.g = g;
     sl.prune = prune;
     sl.tabs = t;
