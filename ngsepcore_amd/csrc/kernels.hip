@@ -1,21 +1,21 @@
 // kernels.hip -- gfx950 kernels of the NGSEP SNV pileup path.
 //
-//   KT  k_tile_pileup : one workgroup per tile of T reference positions (global coordinates).
-//        phase 1  stage the tile's read slots HBM -> LDS (global_load_lds, 16 B per lane; the slots
-//                 of the reads overlapping a tile are one contiguous range) and compare every
-//                 projected read byte with the reference code of its position: a position whose
-//                 pileup holds a valid non-reference call becomes a candidate (LDS bitmap).  This is
-//                 AlignmentsPileupGenerator.processCurrentPosition (discovery/AlignmentsPileupGenerator.java:475-498)
-//                 reduced to the fact that decides whether SNVQ can call a variant there
-//                 ("why pruning is exact").
-//        phase 2  integer hom-ref bound of every candidate (order-independent LDS atomics).
-//        phase 3  drop the candidates the bound proves hom-ref, queue the rest.
-//        Tiles whose reads do not fit the LDS budget scan from global memory and queue every candidate.
+//   KT  k_tile_planes<W> : single-sample scan of the pile's bit planes (valid call / valid call of
+//        another allele, 2 bits per position-row), one wavefront per tile: bit-sliced counts of every
+//        position (LDS-free butterfly over row groups), the candidates (a valid non-reference call at a
+//        callable position) and the count bound as a table; survivors queued.  This is
+//        AlignmentsPileupGenerator.processCurrentPosition (discovery/AlignmentsPileupGenerator.java:475-498)
+//        reduced to the fact that decides whether SNVQ can call a variant there ("why
+//        pruning is exact").
+//   KT  k_tile_pileup<MODE> : the same over the byte pile (other tile widths; MODE 1 = dump mode).
+//   KB  kb_planes : the bit planes from the byte pile, once per staged batch.
 //   KP  k_posterior : exact CountsHelper tally (pending-list order, bit-exact fp64), posterior and
-//                 SNVQ call of the queued candidates (discovery/CountsHelper.java:83-95,209-251,410-495,
-//                 VariantDiscoverySNVQAlgorithm.java:100-243, SingleSampleVariantPileupListener.java:213-232).
+//        SNVQ call of the queued candidates (discovery/CountsHelper.java:83-95,209-251,410-495,
+//        VariantDiscoverySNVQAlgorithm.java:100-243, SingleSampleVariantPileupListener.java:213-232);
+//        records go to position buckets.
+//   KO  ko_fused : position order of the records (rank per bucket) and their (sequence, position).
+//   KTM / KPM k_tile_pileup_multi / k_posterior_multi : MultisampleVariantsDetector.
 //   KL  kl_read_index : per 64-position block, first read that can cover it (binary search).
-//   KO  ko_* : position order of the emitted records.
 //
 // HBM-bound integer/byte work: no MFMA.  Layout and roofline: DESIGN.md.
 #include <hip/hip_runtime.h>
