@@ -14,4 +14,8 @@ python tools/pmc_traffic.py gpurun_out/pmcf_$TAG gpurun_out/pmcw_$TAG k_tile_p y
 cp gpurun_out/pmc_traffic_$TAG.json profiles/pmc_traffic.json
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-cold > gpurun_out/prof_$TAG.out 2>&1
+if [ -n "$WITH_MS" ]; then
+timeout -k 10 600 python bench.py --config multisample --steps 5 --warmup 2 > gpurun_out/bench_ms_$TAG.json 2> gpurun_out/bench_ms_$TAG.err
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ms_$TAG -o run --output-format csv -- python bench.py --config multisample --steps 3 --warmup 1 --no-cpu-baseline --no-cold > gpurun_out/prof_ms_$TAG.out 2>&1
+fi
 echo done
