@@ -106,15 +106,17 @@ def cold_passes(sess, n: int = 5):
 
 
 def load_traffic(workload_key: str):
-    """Per-launch HBM bytes of k_tile_pileup from the committed PMC pass (profiles/), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        d = json.load(open(path))
-    except (OSError, ValueError):
-        return None
-    if d.get("workload_key") != workload_key:
-        return None
-    return d.get("bytes_per_launch")
+    """Per-launch HBM bytes of the scan kernel from the committed PMC passes (profiles/pmc_traffic*.json,
+    one file per workload), or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json"))):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload_key") == workload_key:
+            return d.get("bytes_per_launch")
+    return None
 
 
 def main():
