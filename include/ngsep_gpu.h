@@ -68,6 +68,10 @@ typedef struct ngsep_params {
     /* MultisampleVariantsDetector (discovery/MultisampleVariantsDetector.java:54-95) */
     int32_t multisample;          /* 1: population calling over the samples of ngsep_set_samples */
     double  min_allele_depth_freq;/* -minAlleleDepthFrequency 0 (setMinAlleleDepthFrequency, :398-403) */
+    /* CoverageStatisticsCalculator (discovery/CoverageStatisticsCalculator.java:37-51,108-122): the caller
+     * also sets process_secondary = 1 and max_alns_per_start = 100 as its processFile does */
+    int32_t coverage_stats;       /* 1: the alignments feed the coverage histograms instead of the variant caller */
+    int32_t max_coverage;         /* maxCoverage 300 (setMaxCoverage): bins [0, max_coverage) + "More"; <= 2048 */
 } ngsep_params;
 
 /* Alignments as AlignmentsPileupGenerator.processAlignment receives them
@@ -205,6 +209,20 @@ int ngsep_call_population_bams(ngsep_ctx* ctx, const char* const* bam_paths, int
 
 /* ---- path B: the whole SingleSampleVariantsDetector.findSNVS on a BAM file (:896-931) ---- */
 int ngsep_call_bam(ngsep_ctx* ctx, const char* bam_path, const char* out_vcf_path);
+
+/* ---- CoverageStatisticsCalculator (discovery/CoverageStatisticsCalculator.java:108-216) ----
+ * path A: params.coverage_stats = 1, alignments through ngsep_process_alignments, ngsep_notify_end runs
+ * the device histogram (the PileupListener.onPileup -> processPileup loop, :124-131,177-190) over every
+ * sequence received; the staged entry points (ngsep_stage_*, ngsep_run_staged) run it on resident reads.
+ * ngsep_fetch_coverage returns getCoverageCounts() and the unique-alignment counts for i in [1, max_coverage)
+ * (entry 0 is set to 0: the reference's bin 0 counts empty pileups, which are never printed) and the two
+ * "More" counts; ngsep_write_coverage prints printCoverageStats (:209-215).  Counts accumulate over runs
+ * until ngsep_clear_coverage. */
+int ngsep_fetch_coverage(ngsep_ctx* ctx, int64_t* counts, int64_t* counts_unique, int64_t* high, int64_t* high_unique);
+int ngsep_write_coverage(ngsep_ctx* ctx, const char* path);   /* "-" = stdout */
+int ngsep_clear_coverage(ngsep_ctx* ctx);
+/* path B: `CoverageStats -i BAM -o OUT [-minMQ N]` (CoverageStatisticsCalculator.processFile, :99-122) */
+int ngsep_coverage_bam(ngsep_ctx* ctx, const char* bam_path, const char* out_path);
 
 /* ---- BAM reading (ReadAlignmentFileReader semantics, alignments/io/ReadAlignmentFileReader.java:219-354) ---- */
 typedef struct ngsep_bam ngsep_bam;

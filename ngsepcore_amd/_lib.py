@@ -45,6 +45,8 @@ class NgsepParams(ctypes.Structure):
         ("window_positions", ctypes.c_int32),
         ("multisample", ctypes.c_int32),
         ("min_allele_depth_freq", ctypes.c_double),
+        ("coverage_stats", ctypes.c_int32),
+        ("max_coverage", ctypes.c_int32),
     ]
 
 
@@ -173,6 +175,11 @@ SIGNATURES = {
     "ngsep_stage_finish": (ctypes.c_int, [_CTX]),
     "ngsep_run_staged": (ctypes.c_int, [_CTX, P(ctypes.c_double)]),
     "ngsep_release_staged": (ctypes.c_int, [_CTX]),
+    "ngsep_fetch_coverage": (ctypes.c_int, [_CTX, P(ctypes.c_int64), P(ctypes.c_int64), P(ctypes.c_int64),
+                                            P(ctypes.c_int64)]),
+    "ngsep_write_coverage": (ctypes.c_int, [_CTX, ctypes.c_char_p]),
+    "ngsep_clear_coverage": (ctypes.c_int, [_CTX]),
+    "ngsep_coverage_bam": (ctypes.c_int, [_CTX, ctypes.c_char_p, ctypes.c_char_p]),
 }
 
 _lib = None

@@ -114,6 +114,8 @@ extern "C" int ngsep_bam_open(ngsep_ctx* c, const char* path, ngsep_bam** out) {
     b->pos += 4;
     std::unordered_map<std::string, int32_t> seq_index;
     for (size_t i = 0; i < c->seq_names.size(); i++) seq_index[c->seq_names[i]] = (int32_t)i;
+    // CoverageStatisticsCalculator runs without a genome (-r is optional there): the header's sequences
+    const bool header_seqs = c->params.coverage_stats && c->seq_names.empty();
     for (int32_t i = 0; i < n_ref; i++) {
         if (!need(b, 4, err)) break;
         int32_t ln = rd<int32_t>(&b->buf[b->pos]);
@@ -121,6 +123,13 @@ extern "C" int ngsep_bam_open(ngsep_ctx* c, const char* path, ngsep_bam** out) {
         std::string name(&b->buf[b->pos + 4], (size_t)(ln > 0 ? ln - 1 : 0));
         int32_t lref = rd<int32_t>(&b->buf[b->pos + 4 + ln]);
         b->pos += 8 + (size_t)ln;
+        if (header_seqs && !seq_index.count(name)) {
+            seq_index[name] = (int32_t)c->seq_names.size();
+            c->seq_names.push_back(name);
+            c->seq_bases.emplace_back();
+            b->ref_to_seq.push_back(seq_index[name]);
+            continue;
+        }
         auto it = seq_index.find(name);
         // ReadAlignmentFileReader.loadHeader validation (:198-214)
         if (it == seq_index.end()) {
@@ -330,6 +339,28 @@ int call_bam(ngsep_ctx* c, const char* bam_path, const char* out_vcf) {
     return ngsep_append_vcf_records(c, out_vcf);
 }
 }  // namespace ngsep
+
+// CoverageStatisticsCalculator.processFile (discovery/CoverageStatisticsCalculator.java:99-122): the reader
+// keeps secondary and non-unique alignments (processSecondaryAlignments = true), the same-start cap is 100
+extern "C" int ngsep_coverage_bam(ngsep_ctx* c, const char* bam_path, const char* out_path) {
+    if (!c || !bam_path) return NGSEP_E_INVALID;
+    if (!c->params.coverage_stats) return set_error(c, NGSEP_E_INVALID, "ngsep_coverage_bam needs params.coverage_stats = 1");
+    ngsep_bam* b = nullptr;
+    int rc = ngsep_bam_open(c, bam_path, &b);
+    if (rc != NGSEP_OK) return rc;
+    ngsep_read_batch batch;
+    while (true) {
+        rc = ngsep_bam_next_batch(b, 1 << 20, &batch);
+        if (rc != NGSEP_OK || batch.n_reads == 0) break;
+        rc = ngsep_process_alignments(c, &batch);
+        if (rc != NGSEP_OK) break;
+    }
+    ngsep_bam_close(b);
+    if (rc != NGSEP_OK) return rc;
+    rc = ngsep_notify_end(c);
+    if (rc != NGSEP_OK || !out_path) return rc;
+    return ngsep_write_coverage(c, out_path);
+}
 
 extern "C" int ngsep_call_bam(ngsep_ctx* c, const char* bam_path, const char* out_vcf_path) {
     if (!c || !bam_path || !out_vcf_path) return NGSEP_E_INVALID;

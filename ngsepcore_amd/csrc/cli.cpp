@@ -72,6 +72,42 @@ static int main_mvd(int argc, char** argv, int i) {
     return 0;
 }
 
+// `ngsep-amd CoverageStats -i BAM [-o OUT] [-r REF] [-minMQ N]`
+// (CoverageStatisticsCalculator.main/run, discovery/CoverageStatisticsCalculator.java:93-122,
+// main/CommandsDescriptor.xml:458-477): writes to standard output unless -o is given
+static int main_coverage(int argc, char** argv, int i) {
+    ngsep_params p;
+    ngsep_params_default(&p);
+    p.coverage_stats = 1;
+    p.process_secondary = 1;
+    p.max_alns_per_start = 100;
+    const char *in = nullptr, *ref = nullptr, *outp = "-";
+    int device = 0;
+    for (; i < argc; i++) {
+        const char* a = argv[i];
+        const char* v = i + 1 < argc ? argv[i + 1] : nullptr;
+        auto takes = [&](const char* name) { if (std::strcmp(a, name) == 0 && v) { i++; return true; } return false; };
+        if (takes("-i")) in = v;
+        else if (takes("-o")) outp = v;
+        else if (takes("-r")) ref = v;
+        else if (takes("-minMQ")) p.min_mq = std::atoi(v);
+        else if (takes("-device")) device = std::atoi(v);
+        else { std::fprintf(stderr, "unknown or unsupported option %s\n", a); return 2; }
+    }
+    if (!in) {
+        std::fprintf(stderr, "The alignments input file is a required parameter\n"
+                             "usage: ngsep-amd CoverageStats -i <alignments.bam> [-o <out.txt>] [-r <reference.fa>] [-minMQ N]\n");
+        return 2;
+    }
+    ngsep_ctx* c = nullptr;
+    int rc = ngsep_open(device, &p, &c);
+    if (rc == NGSEP_OK && ref) rc = ngsep_load_fasta(c, ref);
+    if (rc == NGSEP_OK) rc = ngsep_coverage_bam(c, in, outp);
+    if (rc != NGSEP_OK) { std::fprintf(stderr, "error %d: %s\n", rc, c ? ngsep_last_error(c) : "open failed"); if (c) ngsep_close(c); return 1; }
+    ngsep_close(c);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     ngsep_params p;
     ngsep_params_default(&p);
@@ -79,6 +115,7 @@ int main(int argc, char** argv) {
     int device = 0;
     int i = 1;
     if (i < argc && std::strcmp(argv[i], "MultisampleVariantsDetector") == 0) return main_mvd(argc, argv, i + 1);
+    if (i < argc && std::strcmp(argv[i], "CoverageStats") == 0) return main_coverage(argc, argv, i + 1);
     if (i < argc && std::strcmp(argv[i], "SingleSampleVariantsDetector") == 0) i++;
     else if (i < argc && argv[i][0] != '-') { std::fprintf(stderr, "unsupported command %s\n", argv[i]); return usage(argv[0]); }
     for (; i < argc; i++) {

@@ -1,0 +1,226 @@
+// coverage.hip -- CoverageStatisticsCalculator on gfx950 (discovery/CoverageStatisticsCalculator.java:108-216).
+//
+// The reference listener bins, for every pileup the generator emits, PileupRecord.getNumAlignments() and
+// getNumUniqueAlns() (PileupRecord.java:154-177) into coverageCounts[0, maxCoverage) + "More".  Both counts
+// are interval depths over the admitted alignments [first, last], so no allele call is touched: the device
+// sees 12 bytes per admitted read (global first position, span and the unique bit) and the positions are
+// implicit.
+//
+// Layout: admitted reads of all sequences in one global coordinate (sequence regions back to back),
+// ascending first position (pending order).  Positions are cut into tiles of kCovTile positions.
+//   KCI kc_tile_index : tstart[t] = first read whose tile(first) >= t           (one thread per read)
+//   KCH kc_tile_hist  : one workgroup per tile: the reads that can overlap the tile (tiles back to
+//                       lo_tile = tile(t0 - max_span + 1)) add +/-(1 | unique << 32) to an LDS
+//                       difference array, a workgroup prefix sum turns it into packed (depth, unique
+//                       depth) per position (modular u64 arithmetic: the packed sums are exact because
+//                       every final depth is >= 0 and < 2^32), and run-length-compressed LDS histogram
+//                       updates bin both depths; the tile's nonzero bins are flushed with global atomics.
+// HBM traffic: 12 B per read (+ the lookback of one tile of reads) and the histogram; the kernel is bound
+// by its LDS work (atomics + scan over 4096 positions per tile), not by HBM.
+#include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
+#include <cstdint>
+#include <string>
+#include <vector>
+#include "engine.hpp"
+
+namespace ngsep {
+
+constexpr int kCovLog2Tile = 12;
+constexpr int kCovTile = 1 << kCovLog2Tile;          // positions per tile
+constexpr int kCovThreads = 256;                     // 4 wavefronts
+constexpr int kCovPerThread = kCovTile / kCovThreads; // 16 consecutive positions per thread
+constexpr int kCovMaxBins = 2048;                    // largest maxCoverage served by the LDS histogram (LDS <= 48 KB)
+
+#define COV_TRY(expr)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess) {                                                        \
+            err = std::string(#expr) + ": " + hipGetErrorString(e_);                   \
+            return -1;                                                                 \
+        }                                                                              \
+    } while (0)
+
+struct CovDevice {
+    int ordinal = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[2] = {};
+    int64_t* d_gfirst = nullptr;      // global first position per read (ascending)
+    uint32_t* d_spanu = nullptr;      // span << 1 | unique
+    int64_t* d_tstart = nullptr;      // n_tiles + 1
+    unsigned long long* d_hist = nullptr;   // 2 x (max_cov + 1): depth bins, unique-depth bins (index max_cov = More)
+    int64_t n_reads = 0, g_len = 0, n_tiles = 0;
+    int32_t max_span = 1;
+    int32_t hist_cap = 0;
+};
+
+// KCI: tile start index of the read list (tiles with no read starting in them point at the next read)
+__global__ void kc_tile_index(const int64_t* __restrict__ gfirst, int64_t n, int64_t n_tiles, int64_t* __restrict__ tstart) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    const int64_t tp = i == 0 ? -1 : (gfirst[i - 1] >> kCovLog2Tile);
+    const int64_t tc = i == n ? n_tiles : (gfirst[i] >> kCovLog2Tile);
+    for (int64_t t = tp + 1; t <= tc; t++) tstart[t] = i;
+}
+
+// KCH: one workgroup per tile
+__global__ void __launch_bounds__(kCovThreads)
+kc_tile_hist(const int64_t* __restrict__ gfirst, const uint32_t* __restrict__ spanu, const int64_t* __restrict__ tstart,
+             int64_t g_len, int32_t max_span, int32_t max_cov, unsigned long long* __restrict__ hist) {
+    __shared__ unsigned long long diff[kCovTile + 1];
+    __shared__ unsigned long long wave_tot[kCovThreads / 64];
+    extern __shared__ uint32_t bins[];                 // 2 x (max_cov + 1)
+    const int tid = threadIdx.x;
+    const int64_t t = blockIdx.x;
+    const int64_t t0 = t << kCovLog2Tile;
+    const int nb = 2 * (max_cov + 1);
+    for (int k = tid; k <= kCovTile; k += kCovThreads) diff[k] = 0ull;
+    for (int k = tid; k < nb; k += kCovThreads) bins[k] = 0u;
+    __syncthreads();
+    // reads that can overlap [t0, t0 + T): first in [t0 - max_span + 1, t0 + T)
+    int64_t lo_pos = t0 - (int64_t)max_span + 1;
+    const int64_t lo_tile = lo_pos <= 0 ? 0 : (lo_pos >> kCovLog2Tile);
+    const int64_t r0 = tstart[lo_tile], r1 = tstart[t + 1];
+    for (int64_t r = r0 + tid; r < r1; r += kCovThreads) {
+        const int64_t f = gfirst[r];
+        const uint32_t su = spanu[r];
+        const int64_t l = f + (int64_t)(su >> 1) - 1;
+        if (l < t0) continue;
+        const unsigned long long inc = 1ull | ((unsigned long long)(su & 1u) << 32);
+        const int64_t a = (f > t0 ? f : t0) - t0;
+        const int64_t b = l + 1 - t0;
+        atomicAdd(&diff[a], inc);
+        if (b < kCovTile) atomicAdd(&diff[b], 0ull - inc);
+    }
+    __syncthreads();
+    // workgroup prefix sum: 16 consecutive positions per thread, wavefront scan of the thread sums
+    const int base = tid * kCovPerThread;
+    unsigned long long v[kCovPerThread];
+    unsigned long long s = 0;
+#pragma unroll
+    for (int k = 0; k < kCovPerThread; k++) { s += diff[base + k]; v[k] = s; }
+    const int lane = tid & 63, wave = tid >> 6;
+    unsigned long long inc_scan = s;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long o = __shfl_up(inc_scan, d, 64);
+        if (lane >= d) inc_scan += o;
+    }
+    if (lane == 63) wave_tot[wave] = inc_scan;
+    __syncthreads();
+    unsigned long long carry = inc_scan - s;
+    for (int w = 0; w < wave; w++) carry += wave_tot[w];
+    // histogram with run-length compression (depth changes only at read ends)
+    const int64_t p_end = g_len - t0;                  // positions of this tile inside the coordinate space
+    uint32_t run_d = 0xffffffffu, run_u = 0xffffffffu, cnt_d = 0, cnt_u = 0;
+#pragma unroll
+    for (int k = 0; k < kCovPerThread; k++) {
+        if (base + k >= p_end) continue;           // (no break: the loop stays unrolled, v[] in registers)
+        const unsigned long long pk = v[k] + carry;
+        uint32_t dd = (uint32_t)pk, du = (uint32_t)(pk >> 32);
+        dd = dd < (uint32_t)max_cov ? dd : (uint32_t)max_cov;
+        du = du < (uint32_t)max_cov ? du : (uint32_t)max_cov;
+        if (dd != run_d) { if (cnt_d) atomicAdd(&bins[run_d], cnt_d); run_d = dd; cnt_d = 0; }
+        if (du != run_u) { if (cnt_u) atomicAdd(&bins[max_cov + 1 + run_u], cnt_u); run_u = du; cnt_u = 0; }
+        cnt_d++;
+        cnt_u++;
+    }
+    if (cnt_d) atomicAdd(&bins[run_d], cnt_d);
+    if (cnt_u) atomicAdd(&bins[max_cov + 1 + run_u], cnt_u);
+    __syncthreads();
+    for (int k = tid; k < nb; k += kCovThreads) {
+        const uint32_t c = bins[k];
+        if (c) atomicAdd(&hist[k], (unsigned long long)c);
+    }
+}
+
+CovDevice* cov_create(int ordinal, std::string& err) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        err = "no HIP device available (libngsep_amd requires an MI355X / gfx950 GPU)";
+        return nullptr;
+    }
+    if (ordinal < 0 || ordinal >= n) { err = "device ordinal out of range"; return nullptr; }
+    if (hipSetDevice(ordinal) != hipSuccess) { err = "hipSetDevice failed"; return nullptr; }
+    CovDevice* d = new CovDevice();
+    d->ordinal = ordinal;
+    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) { err = "stream"; delete d; return nullptr; }
+    for (auto& e : d->ev) (void)hipEventCreate(&e);
+    return d;
+}
+
+void cov_release(CovDevice* d) {
+    if (!d) return;
+    (void)hipSetDevice(d->ordinal);
+    (void)hipStreamSynchronize(d->stream);
+    (void)hipFree(d->d_gfirst); d->d_gfirst = nullptr;
+    (void)hipFree(d->d_spanu); d->d_spanu = nullptr;
+    (void)hipFree(d->d_tstart); d->d_tstart = nullptr;
+    d->n_reads = d->g_len = d->n_tiles = 0;
+}
+
+void cov_destroy(CovDevice* d) {
+    if (!d) return;
+    cov_release(d);
+    (void)hipFree(d->d_hist);
+    for (auto& e : d->ev) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(d->stream);
+    delete d;
+}
+
+int cov_upload(CovDevice* d, const std::vector<int64_t>& gfirst, const std::vector<uint32_t>& spanu, int64_t g_len,
+               int32_t max_span, std::string& err) {
+    cov_release(d);
+    COV_TRY(hipSetDevice(d->ordinal));
+    const int64_t n = (int64_t)gfirst.size();
+    if ((int64_t)spanu.size() != n) { err = "coverage read arrays differ in length"; return -1; }
+    for (int64_t i = 1; i < n; i++)
+        if (gfirst[i] < gfirst[i - 1]) { err = "coverage reads not in ascending global order"; return -1; }
+    if (n && (gfirst[0] < 0 || gfirst[n - 1] >= g_len)) { err = "coverage read outside the coordinate space"; return -1; }
+    d->n_reads = n;
+    d->g_len = g_len;
+    d->n_tiles = (g_len + kCovTile - 1) >> kCovLog2Tile;
+    d->max_span = max_span > 0 ? max_span : 1;
+    COV_TRY(hipMalloc(&d->d_gfirst, sizeof(int64_t) * (size_t)(n > 0 ? n : 1)));
+    COV_TRY(hipMalloc(&d->d_spanu, sizeof(uint32_t) * (size_t)(n > 0 ? n : 1)));
+    COV_TRY(hipMalloc(&d->d_tstart, sizeof(int64_t) * (size_t)(d->n_tiles + 1)));
+    if (n) {
+        COV_TRY(hipMemcpyAsync(d->d_gfirst, gfirst.data(), sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, d->stream));
+        COV_TRY(hipMemcpyAsync(d->d_spanu, spanu.data(), sizeof(uint32_t) * (size_t)n, hipMemcpyHostToDevice, d->stream));
+    }
+    const int64_t blocks = (n + 1 + 255) / 256;
+    kc_tile_index<<<dim3((unsigned)blocks), dim3(256), 0, d->stream>>>(d->d_gfirst, n, d->n_tiles, d->d_tstart);
+    COV_TRY(hipGetLastError());
+    COV_TRY(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+// one pass over the uploaded reads: hist_out[0 .. max_cov] = depth bins (max_cov = More),
+// hist_out[max_cov + 1 .. 2 max_cov + 1] = unique-depth bins
+int cov_run(CovDevice* d, int32_t max_cov, uint64_t* hist_out, double* kernel_ms, std::string& err) {
+    if (max_cov < 1 || max_cov > kCovMaxBins) { err = "maxCoverage outside [1, 2048]"; return -1; }
+    COV_TRY(hipSetDevice(d->ordinal));
+    const int nb = 2 * (max_cov + 1);
+    if (nb > d->hist_cap) {
+        (void)hipFree(d->d_hist);
+        d->d_hist = nullptr;
+        COV_TRY(hipMalloc(&d->d_hist, sizeof(unsigned long long) * (size_t)nb));
+        d->hist_cap = nb;
+    }
+    COV_TRY(hipMemsetAsync(d->d_hist, 0, sizeof(unsigned long long) * (size_t)nb, d->stream));
+    float ms = 0.f;
+    if (d->n_tiles > 0) {
+        if (d->n_tiles > 0x7fffffff) { err = "coordinate space too large for one launch"; return -1; }
+        hipExtLaunchKernelGGL(kc_tile_hist, dim3((unsigned)d->n_tiles), dim3(kCovThreads), sizeof(uint32_t) * (size_t)nb,
+                              d->stream, d->ev[0], d->ev[1], 0, d->d_gfirst, d->d_spanu, d->d_tstart, d->g_len,
+                              d->max_span, max_cov, d->d_hist);
+        COV_TRY(hipGetLastError());
+    }
+    COV_TRY(hipMemcpyAsync(hist_out, d->d_hist, sizeof(unsigned long long) * (size_t)nb, hipMemcpyDeviceToHost, d->stream));
+    COV_TRY(hipStreamSynchronize(d->stream));
+    if (d->n_tiles > 0) COV_TRY(hipEventElapsedTime(&ms, d->ev[0], d->ev[1]));
+    if (kernel_ms) *kernel_ms = ms;
+    return 0;
+}
+
+}  // namespace ngsep

@@ -200,6 +200,22 @@ static int32_t alignment_last(const RawRead& r) {
 static void admit(ngsep_ctx* c, const RawRead& r) {
     ContigReads& cr = c->contig;
     int32_t last = alignment_last(r);
+    if (c->params.coverage_stats) {
+        // CoverageStatisticsCalculator: only [first, last] and isUnique reach the listener
+        // (PileupRecord.addAlignment, :154-167); positions past the sequence end still get pileups
+        cr.first.push_back(r.first);
+        cr.last.push_back(last);
+        cr.uniq.push_back((r.flags & 0x1000) ? 0 : 1);
+        const int32_t span = last - r.first + 1;
+        if (span > cr.max_span) cr.max_span = span;
+        if (last >= r.first) {
+            if (r.first > cr.cov_last) cr.covered += last - r.first + 1;
+            else if (last > cr.cov_last) cr.covered += last - cr.cov_last;
+            if (last > cr.cov_last) cr.cov_last = last;
+        }
+        c->stats.alignments_admitted++;
+        return;
+    }
     std::vector<uint8_t> bytes;
     project_read(c, r, last, bytes);
     cr.first.push_back(r.first);
@@ -264,7 +280,7 @@ static int flush_sequence(ngsep_ctx* c) {
 int stage_contig_reads(ngsep_ctx* c, ContigReads& cr, bool run_now) {
     if (cr.seq_id < 0) return NGSEP_OK;
     c->stats.positions_genotyped += cr.covered;
-    if (!run_now) {
+    if (!run_now || c->params.coverage_stats) {     // coverage: one device run over all sequences at the end
         c->staged_contigs.emplace_back(std::move(cr));
         cr = ContigReads();
         return NGSEP_OK;
@@ -296,7 +312,7 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b) {
         r.cigar.assign(b->cigar + b->cigar_off[i], b->cigar + b->cigar_off[i] + b->cigar_n[i]);
         for (int32_t v : r.cigar) {
             int op = v & 7;
-            if (op == 1 || op == 2)
+            if ((op == 1 || op == 2) && !c->params.coverage_stats)
                 return set_error(c, NGSEP_E_UNSUPPORTED,
                                  "alignment with an indel (CIGAR I/D): the indel realigner path "
                                  "(IndelRealignerPileupListener) is not implemented on the GPU yet");
@@ -947,6 +963,58 @@ static int finish_run(ngsep_ctx* c, size_t from, int64_t n, double scan_ms, doub
 }
 
 // ---- reference loading: FastaFileReader with keepLowerCase (sequences/io/FastaFileReader.java:170-205) ----
+// ---- CoverageStatisticsCalculator (discovery/CoverageStatisticsCalculator.java:108-216) ----
+// The admitted reads of every sequence in one global coordinate: sequence k's region starts at gbase_k
+// (position p -> gbase_k + p) and spans max(sequence length, largest last) + 2 positions, so a read's
+// end never leaks into the next region.
+int coverage_stage(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
+    std::vector<int64_t> gfirst;
+    std::vector<uint32_t> spanu;
+    int64_t n = 0;
+    for (const auto& cr : contigs) n += (int64_t)cr.first.size();
+    gfirst.reserve((size_t)n);
+    spanu.reserve((size_t)n);
+    int64_t gbase = 0;
+    int32_t max_span = 1;
+    for (const auto& cr : contigs) {
+        int64_t region = cr.seq_id >= 0 ? (int64_t)c->seq_bases[(size_t)cr.seq_id].size() : 0;
+        for (size_t i = 0; i < cr.first.size(); i++) {
+            if (cr.first[i] < 0) return set_error(c, NGSEP_E_INVALID, "alignment with a negative first position");
+            const int32_t span = std::max<int32_t>(0, cr.last[i] - cr.first[i] + 1);
+            gfirst.push_back(gbase + cr.first[i]);
+            spanu.push_back(((uint32_t)span << 1) | (cr.uniq[i] ? 1u : 0u));
+            region = std::max<int64_t>(region, cr.last[i]);
+            max_span = std::max(max_span, span);
+        }
+        gbase += region + 2;
+    }
+    if (!c->cov_dev) {
+        std::string err;
+        c->cov_dev = cov_create(c->device, err);
+        if (!c->cov_dev) return set_error(c, NGSEP_E_DEVICE, err);
+    }
+    std::string err;
+    if (cov_upload(c->cov_dev, gfirst, spanu, gbase, max_span, err) != 0) return set_error(c, NGSEP_E_DEVICE, err);
+    c->cov_staged = true;
+    return NGSEP_OK;
+}
+
+int coverage_run(ngsep_ctx* c, double* kernel_ms) {
+    if (!c->cov_dev || !c->cov_staged) return set_error(c, NGSEP_E_INVALID, "no coverage reads staged");
+    const int32_t mc = c->params.max_coverage;
+    std::vector<uint64_t> h((size_t)(2 * (mc + 1)), 0);
+    std::string err;
+    double ms = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (cov_run(c->cov_dev, mc, h.data(), &ms, err) != 0) return set_error(c, NGSEP_E_DEVICE, err);
+    c->stats.kernel_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->stats.scan_ms = ms;
+    if (c->cov_hist.size() != h.size()) c->cov_hist.assign(h.size(), 0);
+    for (size_t k = 0; k < h.size(); k++) c->cov_hist[k] += h[k];
+    if (kernel_ms) *kernel_ms = ms;
+    return NGSEP_OK;
+}
+
 static inline char mask_base(char ch) {
     switch (ch) {
         case 'A': case 'a': case 'C': case 'c': case 'N': case 'n':
@@ -1008,6 +1076,7 @@ extern "C" void ngsep_params_default(ngsep_params* p) {
     std::snprintf(p->sample_id, sizeof p->sample_id, "Sample");
     p->prune_candidates = 1;
     p->window_positions = 1 << 26;
+    p->max_coverage = 300;
 }
 
 extern "C" int ngsep_open(int device, const ngsep_params* params, ngsep_ctx** out) {
@@ -1016,6 +1085,13 @@ extern "C" int ngsep_open(int device, const ngsep_params* params, ngsep_ctx** ou
     if (params) c->params = *params;
     else ngsep_params_default(&c->params);
     c->device = device;
+    if (c->params.coverage_stats) {
+        *out = c;
+        if (c->params.max_coverage < 1 || c->params.max_coverage > 2048)
+            return set_error(c, NGSEP_E_UNSUPPORTED, "maxCoverage outside [1, 2048] (LDS histogram of the coverage kernel)");
+        if (c->params.multisample || c->params.query_seq[0])
+            return set_error(c, NGSEP_E_INVALID, "coverage statistics take no samples and no query region");
+    }
     if (c->params.ploidy >= 3) {
         *out = c;
         return set_error(c, NGSEP_E_UNSUPPORTED, "ploidy >= 3 uses the pool algorithm (SingleSampleVariantPileupListener.genotypeVariantPool), not implemented");
@@ -1030,6 +1106,7 @@ extern "C" int ngsep_open(int device, const ngsep_params* params, ngsep_ctx** ou
 extern "C" int ngsep_close(ngsep_ctx* c) {
     if (!c) return NGSEP_E_INVALID;
     if (c->dev) device_destroy(c->dev);
+    if (c->cov_dev) cov_destroy(c->cov_dev);
     delete c;
     return NGSEP_OK;
 }
@@ -1072,7 +1149,58 @@ extern "C" int ngsep_process_alignments(ngsep_ctx* c, const ngsep_read_batch* b)
 
 extern "C" int ngsep_notify_end(ngsep_ctx* c) {
     if (!c) return NGSEP_E_INVALID;
-    return flush_sequence(c);
+    int rc = flush_sequence(c);
+    if (rc != NGSEP_OK || !c->params.coverage_stats || c->staging_mode) return rc;
+    rc = coverage_stage(c, c->staged_contigs);
+    c->staged_contigs.clear();
+    if (rc == NGSEP_OK) rc = coverage_run(c, nullptr);
+    cov_release(c->cov_dev);
+    c->cov_staged = false;
+    return rc;
+}
+
+extern "C" int ngsep_fetch_coverage(ngsep_ctx* c, int64_t* counts, int64_t* counts_unique, int64_t* high, int64_t* high_unique) {
+    if (!c) return NGSEP_E_INVALID;
+    if (!c->params.coverage_stats) return set_error(c, NGSEP_E_INVALID, "context not in coverage mode");
+    const int32_t mc = c->params.max_coverage;
+    if (c->cov_hist.size() != (size_t)(2 * (mc + 1))) c->cov_hist.assign((size_t)(2 * (mc + 1)), 0);
+    for (int32_t i = 0; i < mc; i++) {
+        if (counts) counts[i] = i == 0 ? 0 : (int64_t)c->cov_hist[(size_t)i];
+        if (counts_unique) counts_unique[i] = i == 0 ? 0 : (int64_t)c->cov_hist[(size_t)(mc + 1 + i)];
+    }
+    if (high) *high = (int64_t)c->cov_hist[(size_t)mc];
+    if (high_unique) *high_unique = (int64_t)c->cov_hist[(size_t)(2 * mc + 1)];
+    return NGSEP_OK;
+}
+
+extern "C" int ngsep_clear_coverage(ngsep_ctx* c) {
+    if (!c) return NGSEP_E_INVALID;
+    c->cov_hist.clear();
+    return NGSEP_OK;
+}
+
+// CoverageStatisticsCalculator.printCoverageStats (:209-215)
+extern "C" int ngsep_write_coverage(ngsep_ctx* c, const char* path) {
+    if (!c || !path) return NGSEP_E_INVALID;
+    const int32_t mc = c->params.max_coverage;
+    std::vector<int64_t> a((size_t)mc), u((size_t)mc);
+    int64_t hi = 0, hu = 0;
+    int rc = ngsep_fetch_coverage(c, a.data(), u.data(), &hi, &hu);
+    if (rc != NGSEP_OK) return rc;
+    std::string out;
+    char line[96];
+    for (int32_t i = 1; i < mc; i++) {
+        std::snprintf(line, sizeof line, "%d\t%lld\t%lld\n", i, (long long)a[(size_t)i], (long long)u[(size_t)i]);
+        out += line;
+    }
+    std::snprintf(line, sizeof line, "More\t%lld\t%lld\n", (long long)hi, (long long)hu);
+    out += line;
+    const bool to_stdout = std::strcmp(path, "-") == 0;
+    FILE* f = to_stdout ? stdout : std::fopen(path, "w");
+    if (!f) return set_error(c, NGSEP_E_IO, std::string("cannot write ") + path);
+    const bool ok = std::fwrite(out.data(), 1, out.size(), f) == out.size();
+    if (to_stdout) std::fflush(f); else std::fclose(f);
+    return ok ? NGSEP_OK : set_error(c, NGSEP_E_IO, std::string("cannot write ") + path);
 }
 
 extern "C" int ngsep_fetch_sites(ngsep_ctx* c, ngsep_site_out* out, int64_t cap, int64_t* n_out) {
@@ -1100,12 +1228,17 @@ extern "C" int ngsep_stage_finish(ngsep_ctx* c) {
     c->staging_mode = true;
     int rc = flush_sequence(c);
     if (rc != NGSEP_OK) return rc;
-    rc = build_and_upload(c, c->staged_contigs);
+    rc = c->params.coverage_stats ? coverage_stage(c, c->staged_contigs) : build_and_upload(c, c->staged_contigs);
     c->staged_contigs.clear();
     return rc;
 }
 
 extern "C" int ngsep_run_staged(ngsep_ctx* c, double* elapsed_ms) {
+    if (c && c->params.coverage_stats) {
+        const int rc = coverage_run(c, nullptr);
+        if (rc == NGSEP_OK && elapsed_ms) *elapsed_ms = c->stats.kernel_ms;
+        return rc;
+    }
     if (!c || !c->dev) return set_error(c, NGSEP_E_INVALID, "nothing staged");
     c->sites.clear();
     c->pop_sites.clear();
@@ -1118,6 +1251,7 @@ extern "C" int ngsep_run_staged(ngsep_ctx* c, double* elapsed_ms) {
 // the oldest submitted pass and makes its calls the context's result.  At most two passes in flight,
 // so the D2H and host work of one pass overlap the next pass's kernels.
 extern "C" int ngsep_submit_staged(ngsep_ctx* c) {
+    if (c && c->params.coverage_stats) return set_error(c, NGSEP_E_INVALID, "coverage runs are synchronous: ngsep_run_staged");
     if (!c || !c->dev) return set_error(c, NGSEP_E_INVALID, "nothing staged");
     if (c->params.multisample) {            // population runs are synchronous: the result waits for collect
         c->pop_sites.clear();
@@ -1180,6 +1314,8 @@ extern "C" int ngsep_collect_staged(ngsep_ctx* c, double* elapsed_ms) {
 extern "C" int ngsep_release_staged(ngsep_ctx* c) {
     if (!c) return NGSEP_E_INVALID;
     if (c->dev) device_release(c->dev);
+    if (c->cov_dev) cov_release(c->cov_dev);
+    c->cov_staged = false;
     c->staged = Staged();
     return NGSEP_OK;
 }

@@ -109,6 +109,7 @@ struct ContigReads {
     int32_t seq_id = -1;
     std::vector<int32_t> first, last;
     std::vector<uint8_t> neg;          // 1 = negative strand
+    std::vector<uint8_t> uniq;         // coverage mode: 1 = ReadAlignment.isUnique (no FLAG_MULTIPLE_ALN)
     std::vector<int16_t> sample;       // multisample: sample of the read's group (-1 none)
     std::vector<uint8_t> rank;         // multisample: rank of the read group in its sample's set
     std::vector<int64_t> boff;         // offset of the read's projected bytes
@@ -117,7 +118,7 @@ struct ContigReads {
     int64_t covered = 0;               // union of [first,last] (positions with a pileup)
     int32_t cov_last = 0;              // running max of last (for `covered`)
     void clear() {
-        first.clear(); last.clear(); neg.clear(); sample.clear(); rank.clear(); boff.clear(); bytes.clear();
+        first.clear(); last.clear(); neg.clear(); uniq.clear(); sample.clear(); rank.clear(); boff.clear(); bytes.clear();
         max_span = 0; covered = 0; cov_last = 0; seq_id = -1;
     }
 };
@@ -131,6 +132,7 @@ struct RawRead {
 };
 
 struct Device;   // kernels.hip
+struct CovDevice;   // coverage.hip
 
 // pinned host memory (kernels.hip): the device copies results straight into it
 void* pinned_alloc(size_t bytes);
@@ -222,6 +224,10 @@ struct ngsep_ctx {
     std::vector<ngsep::ContigReads> staged_contigs;
     ngsep::Staged staged;
     ngsep::Device* dev = nullptr;
+    // CoverageStatisticsCalculator mode (params.coverage_stats)
+    ngsep::CovDevice* cov_dev = nullptr;
+    bool cov_staged = false;
+    std::vector<uint64_t> cov_hist;          // 2 x (max_coverage + 1), accumulated over runs
     // multisample (ngsep_set_samples)
     std::vector<std::string> sample_ids;
     std::vector<int32_t> rg_sample, rg_rank;
@@ -266,6 +272,16 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
 int64_t device_last_hard(const Device* d);
 int64_t device_last_exact(const Device* d);
 int device_count();
+// coverage.hip
+CovDevice* cov_create(int ordinal, std::string& err);
+void cov_release(CovDevice* d);
+void cov_destroy(CovDevice* d);
+int cov_upload(CovDevice* d, const std::vector<int64_t>& gfirst, const std::vector<uint32_t>& spanu, int64_t g_len,
+               int32_t max_span, std::string& err);
+int cov_run(CovDevice* d, int32_t max_cov, uint64_t* hist_out, double* kernel_ms, std::string& err);
+// engine.cpp
+int coverage_stage(ngsep_ctx* c, std::vector<ContigReads>& contigs);
+int coverage_run(ngsep_ctx* c, double* kernel_ms);
 // vcf.cpp
 std::string format_header(const ngsep_ctx* c);
 int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& out);

@@ -406,3 +406,89 @@ class MultisampleVariantsDetector:
         s.notifyEndOfAlignments()
         s.write_population_vcf(self.outFilename)
         return s
+
+
+class CoverageStatisticsCalculator:
+    """Drop-in for ngsep.discovery.CoverageStatisticsCalculator (discovery/CoverageStatisticsCalculator.java:
+    31-216; command CoverageStats, main/CommandsDescriptor.xml:458-477): per-position numAlignments and
+    numUniqueAlns histograms, the per-position loop on the GPU (coverage.hip)."""
+
+    DEF_MIN_MQ_UNIQUE_ALIGNMENT = 20
+
+    def __init__(self):
+        self.params = default_params()
+        self.params.coverage_stats = 1
+        self.params.process_secondary = 1      # processFile (:108-114)
+        self.params.max_alns_per_start = 100
+        self.params.max_coverage = 300
+        self.inputFile: Optional[str] = None
+        self.outputFile: Optional[str] = None
+        self.genomeFile: Optional[str] = None
+        self.device = 0
+        self.coverageCounts: List[int] = []
+        self.coverageCountUniqueAlignments: List[int] = []
+        self.highCoverageCount = 0
+        self.highCoverageCountUniqueAlignments = 0
+
+    def setInputFile(self, v: str): self.inputFile = v
+    def setOutputFile(self, v: str): self.outputFile = v
+    def setGenome(self, v: str): self.genomeFile = v
+    def setMinMQ(self, v: int): self.params.min_mq = int(v)
+    def getMinMQ(self) -> int: return self.params.min_mq
+    def setMaxCoverage(self, v: int): self.params.max_coverage = int(v)
+    def getMaxCoverage(self) -> int: return self.params.max_coverage
+    def getCoverageCounts(self) -> List[int]: return self.coverageCounts
+    def getHighCoverageCount(self) -> int: return self.highCoverageCount
+
+    def getCoverageMaxCount(self) -> int:
+        """Most frequent depth >= 1 (:200-208)."""
+        m = 1
+        for i in range(1, len(self.coverageCounts)):
+            if self.coverageCounts[m] < self.coverageCounts[i]:
+                m = i
+        return m
+
+    def _session(self) -> GpuPileupSession:
+        s = GpuPileupSession(self.params, self.device)
+        if self.genomeFile is not None:
+            s.load_fasta(self.genomeFile)
+        return s
+
+    def _collect(self, s: GpuPileupSession):
+        n = self.params.max_coverage
+        a, u = (ctypes.c_int64 * n)(), (ctypes.c_int64 * n)()
+        hi, hu = ctypes.c_int64(), ctypes.c_int64()
+        s._check(s._lib.ngsep_fetch_coverage(s._ctx, a, u, ctypes.byref(hi), ctypes.byref(hu)))
+        self.coverageCounts, self.coverageCountUniqueAlignments = list(a), list(u)
+        self.highCoverageCount, self.highCoverageCountUniqueAlignments = hi.value, hu.value
+
+    def run(self):
+        if self.inputFile is None:
+            raise NgsepError(_lib.NGSEP_E_IO, "The alignments input file is a required parameter")
+        self.processFile(self.inputFile, self.outputFile)
+
+    def processFile(self, inputFile: str, outputFile: Optional[str] = None):
+        """processFile (:99-122): BAM -> histograms -> printCoverageStats (stdout when outputFile is None)."""
+        with self._session() as s:
+            s._check(s._lib.ngsep_coverage_bam(s._ctx, inputFile.encode(), (outputFile or "-").encode()))
+            self._collect(s)
+
+    def processBatches(self, batches, contigs=None):
+        """Path A: reader-filtered alignment batches (the generator's input) -> histograms."""
+        with self._session() as s:
+            if contigs is not None:
+                for name, seq in contigs:
+                    s.set_reference(name, seq)
+            for b in batches:
+                s.processAlignments(b)
+            s.notifyEndOfAlignments()
+            self._collect(s)
+
+    def printCoverageStats(self, out=None) -> str:
+        lines = [f"{i}\t{self.coverageCounts[i]}\t{self.coverageCountUniqueAlignments[i]}"
+                 for i in range(1, len(self.coverageCounts))]
+        lines.append(f"More\t{self.highCoverageCount}\t{self.highCoverageCountUniqueAlignments}")
+        txt = "\n".join(lines) + "\n"
+        if out is not None:
+            out.write(txt)
+        return txt

@@ -26,6 +26,7 @@
 #define NGO_ERR_IO 1
 #define NGO_ERR_FORMAT 2
 #define NGO_UNSUPPORTED 3
+#define NGO_ERR_ARG 4
 
 /* ------------------------------------------------------------------ */
 /* Java numerics                                                        */
@@ -629,6 +630,7 @@ typedef struct {
     ngo_calls calls;
     ngo_stats* st;
     int unsupported;
+    ngo_coverage* cov;         /* CoverageStatisticsCalculator listener instead of the variant listeners */
 } ngo_gen;
 
 static void on_sequence_end(ngo_gen* G) {
@@ -985,6 +987,24 @@ static int process_current_position(ngo_gen* G) {
     const ngo_params* p = G->p;
     if (p->query_seq && (G->cur_pos < p->query_first || G->cur_pos > p->query_last)) { G->cur_pos++; return 0; }
     int pos = G->cur_pos;
+    if (G->cov) {
+        /* CoverageStatisticsCalculator.onPileup -> processPileup (CoverageStatisticsCalculator.java:124-131,
+         * 177-190): PileupRecord.getNumAlignments / getNumUniqueAlns (PileupRecord.java:154-177; unique =
+         * !FLAG_MULTIPLE_ALN, ReadAlignment.isUnique) binned at [0, maxCoverage), the rest in "More" */
+        ngo_coverage* cv = G->cov;
+        int numAlignments = 0, numUnique = 0;
+        for (int k = 0; k < G->pending.n; k++) {
+            const ngo_aln* a = G->pending.a[k];
+            if (a->first > pos || a->last < pos) continue;
+            numAlignments++;
+            if (!(a->flags & FLAG_MULTIPLE)) numUnique++;
+        }
+        if (numAlignments < cv->max_coverage) cv->counts[numAlignments]++; else cv->high++;
+        if (numUnique < cv->max_coverage) cv->counts_unique[numUnique]++; else cv->high_unique++;
+        if (numAlignments > 0) G->st->positions_genotyped++;
+        G->cur_pos++;
+        return numAlignments > 0;
+    }
     if (G->mvd) {
         int numAlignments = 0;
         for (int k = 0; k < G->pending.n; k++)
@@ -1131,7 +1151,8 @@ static char* split_tab(char** s) {
 }
 
 static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
-                        const char* dump_path, const ngo_params* p, ngo_stats* stats, double min_adf, int multisample) {
+                        const char* dump_path, const ngo_params* p, ngo_stats* stats, double min_adf, int multisample,
+                        ngo_coverage* cov) {
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     ngo_stats st_local; ngo_stats* st = stats ? stats : &st_local;
@@ -1150,7 +1171,8 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
     /* SingleSampleVariantsDetector.run, :591-593 (MultisampleVariantsDetector keeps -h as given) */
     G.het_rate = p->het_rate;
     if (!multisample && !p->het_rate_set && p->ploidy == 1) G.het_rate = 1e-6;
-    if (!multisample) print_header(out, p);
+    G.cov = cov;
+    if (!multisample && !cov) print_header(out, p);
     ngo_mvd M; memset(&M, 0, sizeof(M));
     ngo_strlist rg_sm = {0};       /* SM of each @RG (parallel to rgs) */
     int header_done = !multisample;
@@ -1293,11 +1315,17 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
             } else if (query_found) { aln_free(a); break; }
             else { aln_free(a); continue; }
         }
-        if (a->has_indel) { G.unsupported = 1; aln_free(a); rc = NGO_UNSUPPORTED; break; }
+        if (a->has_indel && !cov) { G.unsupported = 1; aln_free(a); rc = NGO_UNSUPPORTED; break; }
         process_alignment(&G, a);
     }
     if (multisample && !header_done) { header_done = 1; print_header_samples(out, p, NULL, 0); }
     if (rc == NGO_OK) notify_end(&G);
+    if (rc == NGO_OK && cov) {
+        /* CoverageStatisticsCalculator.printCoverageStats (:209-215) */
+        for (int i = 1; i < cov->max_coverage; i++)
+            fprintf(out, "%d\t%lld\t%lld\n", i, (long long)cov->counts[i], (long long)cov->counts_unique[i]);
+        fprintf(out, "More\t%lld\t%lld\n", (long long)cov->high, (long long)cov->high_unique);
+    }
     free(line); free(last_qname); fclose(in);
     if (out != stdout) fclose(out); else fflush(out);
     if (dump) fclose(dump);
@@ -1322,7 +1350,7 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
 
 int ngo_run_ssvd(const char* fasta, const char* sam, const char* out_vcf,
                  const char* dump_path, const ngo_params* p, ngo_stats* stats) {
-    return run_detector(fasta, sam, out_vcf, dump_path, p, stats, 0.0, 0);
+    return run_detector(fasta, sam, out_vcf, dump_path, p, stats, 0.0, 0, NULL);
 }
 
 /* MultisampleVariantsDetector.run (discovery/MultisampleVariantsDetector.java:421-459) on one SAM
@@ -1330,5 +1358,31 @@ int ngo_run_ssvd(const char* fasta, const char* sam, const char* out_vcf,
 int ngo_run_mvd(const char* fasta, const char* sam, const char* out_vcf, const ngo_params* p,
                 double min_allele_depth_freq, ngo_stats* stats) {
     if (p->ploidy >= 3) return NGO_UNSUPPORTED;
-    return run_detector(fasta, sam, out_vcf, NULL, p, stats, min_allele_depth_freq, 1);
+    return run_detector(fasta, sam, out_vcf, NULL, p, stats, min_allele_depth_freq, 1, NULL);
+}
+
+/* CoverageStatisticsCalculator.processFile (discovery/CoverageStatisticsCalculator.java:108-122): the
+ * generator with processSecondaryAlignments=true (reader filters only unmapped records), maxAlnsPerStartPos
+ * 100 and -minMQ (which decides isUnique); reads with indels are admitted (the coverage listener reads no
+ * allele calls).  counts/counts_unique: max_coverage entries, caller-owned. */
+int ngo_run_coverage(const char* fasta, const char* sam, const char* out_txt, int min_mq, int max_coverage,
+                     int64_t* counts, int64_t* counts_unique, int64_t* high, int64_t* high_unique, ngo_stats* stats) {
+    if (max_coverage < 1) return NGO_ERR_ARG;
+    ngo_params p;
+    ngo_params_default(&p);
+    p.min_mq = min_mq;
+    p.process_secondary = 1;
+    p.max_alns_per_start = 100;
+    ngo_coverage cv;
+    memset(&cv, 0, sizeof(cv));
+    cv.max_coverage = max_coverage;
+    cv.counts = calloc(max_coverage, sizeof(int64_t));
+    cv.counts_unique = calloc(max_coverage, sizeof(int64_t));
+    int rc = run_detector(fasta, sam, out_txt, NULL, &p, stats, 0.0, 0, &cv);
+    if (counts) memcpy(counts, cv.counts, sizeof(int64_t) * max_coverage);
+    if (counts_unique) memcpy(counts_unique, cv.counts_unique, sizeof(int64_t) * max_coverage);
+    if (high) *high = cv.high;
+    if (high_unique) *high_unique = cv.high_unique;
+    free(cv.counts); free(cv.counts_unique);
+    return rc;
 }

@@ -100,6 +100,17 @@ int ngo_run_ssvd(const char* fasta, const char* sam, const char* out_vcf,
 int ngo_run_mvd(const char* fasta, const char* sam, const char* out_vcf, const ngo_params* p,
                 double min_allele_depth_freq, ngo_stats* stats);
 
+/* CoverageStatisticsCalculator (discovery/CoverageStatisticsCalculator.java:108-216): per-position
+ * numAlignments / numUniqueAlns histograms; out_txt gets printCoverageStats' text ("-" = stdout). */
+typedef struct ngo_coverage {
+    int max_coverage;              /* maxCoverage (300) */
+    int64_t* counts;               /* coverageCounts[max_coverage] */
+    int64_t* counts_unique;        /* coverageCountUniqueAlignments[max_coverage] */
+    int64_t high, high_unique;     /* highCoverageCount, highCoverageCountUniqueAlignments */
+} ngo_coverage;
+int ngo_run_coverage(const char* fasta, const char* sam, const char* out_txt, int min_mq, int max_coverage,
+                     int64_t* counts, int64_t* counts_unique, int64_t* high, int64_t* high_unique, ngo_stats* stats);
+
 /* DecimalFormat("##0.0#") with HALF_EVEN (main/io/ParseUtils.java:29) */
 int ngo_java_fmt2(double x, char* buf, int cap);
 /* INFO of a population record: NS, AN, AFS, OH, MAF (biallelic) from the calls' (n_called, called[2], acn[4]) */

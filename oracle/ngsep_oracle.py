@@ -68,6 +68,10 @@ def lib():
                                           ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         l.ngo_run_mvd.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(OracleParams),
                                   ctypes.c_double, ctypes.POINTER(OracleStats)]
+        l.ngo_run_coverage.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                       ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                       ctypes.POINTER(OracleStats)]
         _lib = l
     return _lib
 
@@ -139,3 +143,18 @@ class Counts:
         out = (ctypes.c_double * (n * n))()
         lib().ngo_counts_posteriors(ctypes.byref(self.c), het_rate, out)
         return [[out[i * n + j] for j in range(n)] for i in range(n)]
+
+
+def run_coverage(fasta: str, sam: str, out_txt: str, min_mq: int = 20, max_coverage: int = 300):
+    """CoverageStatisticsCalculator restatement (discovery/CoverageStatisticsCalculator.java:108-216).
+    Returns (counts, counts_unique, high, high_unique, stats); counts[i] = positions whose pileup holds i
+    alignments, i < max_coverage."""
+    c = (ctypes.c_int64 * max_coverage)()
+    u = (ctypes.c_int64 * max_coverage)()
+    hi, hu = ctypes.c_int64(), ctypes.c_int64()
+    st = OracleStats()
+    rc = lib().ngo_run_coverage(fasta.encode(), sam.encode(), out_txt.encode(), min_mq, max_coverage, c, u,
+                                ctypes.byref(hi), ctypes.byref(hu), ctypes.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"oracle failed rc={rc}")
+    return list(c), list(u), hi.value, hu.value, st
