@@ -71,7 +71,7 @@ typedef struct ngsep_params {
     /* CoverageStatisticsCalculator (discovery/CoverageStatisticsCalculator.java:37-51,108-122): the caller
      * also sets process_secondary = 1 and max_alns_per_start = 100 as its processFile does */
     int32_t coverage_stats;       /* 1: the alignments feed the coverage histograms instead of the variant caller */
-    int32_t max_coverage;         /* maxCoverage 300 (setMaxCoverage): bins [0, max_coverage) + "More"; <= 2048 */
+    int32_t max_coverage;         /* maxCoverage 300 (setMaxCoverage): bins [0, max_coverage) + "More"; <= 1024 */
 } ngsep_params;
 
 /* Alignments as AlignmentsPileupGenerator.processAlignment receives them

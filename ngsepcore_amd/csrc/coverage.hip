@@ -7,30 +7,31 @@
 // implicit.
 //
 // Layout: admitted reads of all sequences in one global coordinate (sequence regions back to back),
-// ascending first position (pending order).  Positions are cut into tiles of kCovTile positions.
+// ascending first position (pending order).  Positions are cut into tiles (index: 4096 positions).
 //   KCI kc_tile_index : tstart[t] = first read whose tile(first) >= t           (one thread per read)
-//   KCH kc_tile_hist  : one workgroup per tile: the reads that can overlap the tile (tiles back to
+//   KCH kc_tile_hist  : persistent workgroups over tiles of 4096 positions: the reads that can overlap the tile (tiles back to
 //                       lo_tile = tile(t0 - max_span + 1)) add +/-(1 | unique << 32) to an LDS
 //                       difference array, a workgroup prefix sum turns it into packed (depth, unique
 //                       depth) per position (modular u64 arithmetic: the packed sums are exact because
 //                       every final depth is >= 0 and < 2^32), and run-length-compressed LDS histogram
-//                       updates bin both depths; the tile's nonzero bins are flushed with global atomics.
+//                       updates bin both depths in LDS; each workgroup flushes its bins with global atomics once.
 // HBM traffic: 12 B per read (+ the lookback of one tile of reads) and the histogram; the kernel is bound
-// by its LDS work (atomics + scan over 4096 positions per tile), not by HBM.
+// by its LDS work (atomics + scan over the tile's positions) and load latency, not by HBM.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <cstdint>
+#include <climits>
+#include <algorithm>
+#include <cstdlib>
 #include <string>
 #include <vector>
 #include "engine.hpp"
 
 namespace ngsep {
 
-constexpr int kCovLog2Tile = 12;
-constexpr int kCovTile = 1 << kCovLog2Tile;          // positions per tile
+constexpr int kCovLog2Tile = 12;                     // tile index granularity (KCI) = the largest tile
 constexpr int kCovThreads = 256;                     // 4 wavefronts
-constexpr int kCovPerThread = kCovTile / kCovThreads; // 16 consecutive positions per thread
-constexpr int kCovMaxBins = 2048;                    // largest maxCoverage served by the LDS histogram (LDS <= 48 KB)
+constexpr int kCovMaxBins = 1024;                    // largest maxCoverage: 4 private bin sets + 16 KB <= 64 KB LDS
 
 #define COV_TRY(expr)                                                                  \
     do {                                                                               \
@@ -52,6 +53,7 @@ struct CovDevice {
     int64_t n_reads = 0, g_len = 0, n_tiles = 0;
     int32_t max_span = 1;
     int32_t hist_cap = 0;
+    int32_t n_cu = 256;
 };
 
 // KCI: tile start index of the read list (tiles with no read starting in them point at the next read)
@@ -63,74 +65,115 @@ __global__ void kc_tile_index(const int64_t* __restrict__ gfirst, int64_t n, int
     for (int64_t t = tp + 1; t <= tc; t++) tstart[t] = i;
 }
 
-// KCH: one workgroup per tile
+// KCH: persistent workgroups, each walks tiles of 2^LOG2T positions with a grid stride (LOG2T <=
+// kCovLog2Tile; the read range comes from the 4096-position index).  Histogram bins live in LDS for the
+// workgroup's whole life, private per wavefront (4 copies: the run-length updates of different waves never
+// hit the same LDS word), and are summed and flushed to the global histogram once at the end -- measured:
+// zeroing and flushing the bins per tile cost more than the tile's own work (71-125 us vs 4096/2048-position
+// workgroup-per-tile launches on the yeast 30x genome).
+template <int LOG2T>
 __global__ void __launch_bounds__(kCovThreads)
 kc_tile_hist(const int64_t* __restrict__ gfirst, const uint32_t* __restrict__ spanu, const int64_t* __restrict__ tstart,
-             int64_t g_len, int32_t max_span, int32_t max_cov, unsigned long long* __restrict__ hist) {
-    __shared__ unsigned long long diff[kCovTile + 1];
+             int64_t g_len, int64_t n_tl, int32_t max_span, int32_t max_cov, unsigned long long* __restrict__ hist) {
+    constexpr int T = 1 << LOG2T;
+    constexpr int PER = T / kCovThreads;               // consecutive positions per thread
+    __shared__ unsigned long long diff[T + 1];
     __shared__ unsigned long long wave_tot[kCovThreads / 64];
-    extern __shared__ uint32_t bins[];                 // 2 x (max_cov + 1)
+    extern __shared__ uint32_t bins[];                 // 4 waves x 2 x (max_cov + 1)
     const int tid = threadIdx.x;
-    const int64_t t = blockIdx.x;
-    const int64_t t0 = t << kCovLog2Tile;
-    const int nb = 2 * (max_cov + 1);
-    for (int k = tid; k <= kCovTile; k += kCovThreads) diff[k] = 0ull;
-    for (int k = tid; k < nb; k += kCovThreads) bins[k] = 0u;
-    __syncthreads();
-    // reads that can overlap [t0, t0 + T): first in [t0 - max_span + 1, t0 + T)
-    int64_t lo_pos = t0 - (int64_t)max_span + 1;
-    const int64_t lo_tile = lo_pos <= 0 ? 0 : (lo_pos >> kCovLog2Tile);
-    const int64_t r0 = tstart[lo_tile], r1 = tstart[t + 1];
-    for (int64_t r = r0 + tid; r < r1; r += kCovThreads) {
-        const int64_t f = gfirst[r];
-        const uint32_t su = spanu[r];
-        const int64_t l = f + (int64_t)(su >> 1) - 1;
-        if (l < t0) continue;
-        const unsigned long long inc = 1ull | ((unsigned long long)(su & 1u) << 32);
-        const int64_t a = (f > t0 ? f : t0) - t0;
-        const int64_t b = l + 1 - t0;
-        atomicAdd(&diff[a], inc);
-        if (b < kCovTile) atomicAdd(&diff[b], 0ull - inc);
-    }
-    __syncthreads();
-    // workgroup prefix sum: 16 consecutive positions per thread, wavefront scan of the thread sums
-    const int base = tid * kCovPerThread;
-    unsigned long long v[kCovPerThread];
-    unsigned long long s = 0;
-#pragma unroll
-    for (int k = 0; k < kCovPerThread; k++) { s += diff[base + k]; v[k] = s; }
     const int lane = tid & 63, wave = tid >> 6;
-    unsigned long long inc_scan = s;
+    const int nb = 2 * (max_cov + 1);
+    uint32_t* wb = bins + wave * nb;
+    for (int k = tid; k < 4 * nb; k += kCovThreads) bins[k] = 0u;
+    // read range of a tile: reads whose first lies in [t0 - max_span + 1, t0 + T)
+    auto range = [&](int64_t t, int64_t& r0, int64_t& r1) {
+        const int64_t t0 = t << LOG2T;
+        const int64_t lo_pos = t0 - (int64_t)max_span + 1;
+        const int64_t lo_tile = lo_pos <= 0 ? 0 : (lo_pos >> kCovLog2Tile);
+        r0 = tstart[lo_tile];
+        r1 = tstart[((t0 + T - 1) >> kCovLog2Tile) + 1];
+    };
+    int64_t r0 = 0, r1 = 0;
+    if ((int64_t)blockIdx.x < n_tl) range(blockIdx.x, r0, r1);
+    for (int64_t t = blockIdx.x; t < n_tl; t += gridDim.x) {
+        const int64_t t0 = t << LOG2T;
+        // this tile's reads in flight in batches of kCovBatch per thread (independent loads), and the next
+        // tile's range, before the LDS work
+        constexpr int kCovBatch = 4;
+        int64_t f[kCovBatch];
+        uint32_t su[kCovBatch];
+        int64_t r = r0 + tid;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const unsigned long long o = __shfl_up(inc_scan, d, 64);
-        if (lane >= d) inc_scan += o;
-    }
-    if (lane == 63) wave_tot[wave] = inc_scan;
-    __syncthreads();
-    unsigned long long carry = inc_scan - s;
-    for (int w = 0; w < wave; w++) carry += wave_tot[w];
-    // histogram with run-length compression (depth changes only at read ends)
-    const int64_t p_end = g_len - t0;                  // positions of this tile inside the coordinate space
-    uint32_t run_d = 0xffffffffu, run_u = 0xffffffffu, cnt_d = 0, cnt_u = 0;
+        for (int j = 0; j < kCovBatch; j++) {
+            const int64_t rj = r + (int64_t)j * kCovThreads;
+            f[j] = rj < r1 ? gfirst[rj] : INT64_MAX;
+            su[j] = rj < r1 ? spanu[rj] : 0u;
+        }
+        const int64_t cur1 = r1;
+        if (t + gridDim.x < n_tl) range(t + gridDim.x, r0, r1);
+        for (int k = tid; k <= T; k += kCovThreads) diff[k] = 0ull;
+        __syncthreads();
+        while (true) {
 #pragma unroll
-    for (int k = 0; k < kCovPerThread; k++) {
-        if (base + k >= p_end) continue;           // (no break: the loop stays unrolled, v[] in registers)
-        const unsigned long long pk = v[k] + carry;
-        uint32_t dd = (uint32_t)pk, du = (uint32_t)(pk >> 32);
-        dd = dd < (uint32_t)max_cov ? dd : (uint32_t)max_cov;
-        du = du < (uint32_t)max_cov ? du : (uint32_t)max_cov;
-        if (dd != run_d) { if (cnt_d) atomicAdd(&bins[run_d], cnt_d); run_d = dd; cnt_d = 0; }
-        if (du != run_u) { if (cnt_u) atomicAdd(&bins[max_cov + 1 + run_u], cnt_u); run_u = du; cnt_u = 0; }
-        cnt_d++;
-        cnt_u++;
+            for (int j = 0; j < kCovBatch; j++) {
+                if (f[j] >= t0 + T) continue;          // past the tile (the index is coarser) or no read
+                const int64_t l = f[j] + (int64_t)(su[j] >> 1) - 1;
+                if (l < t0) continue;
+                const unsigned long long inc = 1ull | ((unsigned long long)(su[j] & 1u) << 32);
+                const int64_t a = (f[j] > t0 ? f[j] : t0) - t0;
+                const int64_t b = l + 1 - t0;
+                atomicAdd(&diff[a], inc);
+                if (b < T) atomicAdd(&diff[b], 0ull - inc);
+            }
+            r += (int64_t)kCovBatch * kCovThreads;
+            if (r >= cur1) break;                      // deep tiles: the next batch
+#pragma unroll
+            for (int j = 0; j < kCovBatch; j++) {
+                const int64_t rj = r + (int64_t)j * kCovThreads;
+                f[j] = rj < cur1 ? gfirst[rj] : INT64_MAX;
+                su[j] = rj < cur1 ? spanu[rj] : 0u;
+            }
+        }
+        __syncthreads();
+        // workgroup prefix sum: PER consecutive positions per thread, wavefront scan of the thread sums
+        const int base = tid * PER;
+        unsigned long long v[PER];
+        unsigned long long s = 0;
+#pragma unroll
+        for (int k = 0; k < PER; k++) { s += diff[base + k]; v[k] = s; }
+        unsigned long long inc_scan = s;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned long long o = __shfl_up(inc_scan, d, 64);
+            if (lane >= d) inc_scan += o;
+        }
+        if (lane == 63) wave_tot[wave] = inc_scan;
+        __syncthreads();
+        unsigned long long carry = inc_scan - s;
+        for (int w = 0; w < wave; w++) carry += wave_tot[w];
+        // histogram with run-length compression (depth changes only at read ends)
+        const int64_t p_end = g_len - t0;              // positions of this tile inside the coordinate space
+        uint32_t run_d = 0xffffffffu, run_u = 0xffffffffu, cnt_d = 0, cnt_u = 0;
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            if (base + k >= p_end) continue;           // (no break: the loop stays unrolled, v[] in registers)
+            const unsigned long long pk = v[k] + carry;
+            uint32_t dd = (uint32_t)pk, du = (uint32_t)(pk >> 32);
+            dd = dd < (uint32_t)max_cov ? dd : (uint32_t)max_cov;
+            du = du < (uint32_t)max_cov ? du : (uint32_t)max_cov;
+            if (dd != run_d) { if (cnt_d) atomicAdd(&wb[run_d], cnt_d); run_d = dd; cnt_d = 0; }
+            if (du != run_u) { if (cnt_u) atomicAdd(&wb[max_cov + 1 + run_u], cnt_u); run_u = du; cnt_u = 0; }
+            cnt_d++;
+            cnt_u++;
+        }
+        if (cnt_d) atomicAdd(&wb[run_d], cnt_d);
+        if (cnt_u) atomicAdd(&wb[max_cov + 1 + run_u], cnt_u);
+        __syncthreads();                               // diff and wave_tot are reused by the next tile
     }
-    if (cnt_d) atomicAdd(&bins[run_d], cnt_d);
-    if (cnt_u) atomicAdd(&bins[max_cov + 1 + run_u], cnt_u);
-    __syncthreads();
+    __syncthreads();                                   // (a workgroup without tiles: the zeroed bins)
     for (int k = tid; k < nb; k += kCovThreads) {
-        const uint32_t c = bins[k];
-        if (c) atomicAdd(&hist[k], (unsigned long long)c);
+        const unsigned long long c = (unsigned long long)bins[k] + bins[nb + k] + bins[2 * nb + k] + bins[3 * nb + k];
+        if (c) atomicAdd(&hist[k], c);
     }
 }
 
@@ -144,6 +187,10 @@ CovDevice* cov_create(int ordinal, std::string& err) {
     if (hipSetDevice(ordinal) != hipSuccess) { err = "hipSetDevice failed"; return nullptr; }
     CovDevice* d = new CovDevice();
     d->ordinal = ordinal;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, ordinal) == hipSuccess && prop.multiProcessorCount > 0) d->n_cu = prop.multiProcessorCount;
+    }
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) { err = "stream"; delete d; return nullptr; }
     for (auto& e : d->ev) (void)hipEventCreate(&e);
     return d;
@@ -179,7 +226,7 @@ int cov_upload(CovDevice* d, const std::vector<int64_t>& gfirst, const std::vect
     if (n && (gfirst[0] < 0 || gfirst[n - 1] >= g_len)) { err = "coverage read outside the coordinate space"; return -1; }
     d->n_reads = n;
     d->g_len = g_len;
-    d->n_tiles = (g_len + kCovTile - 1) >> kCovLog2Tile;
+    d->n_tiles = (g_len + (1 << kCovLog2Tile) - 1) >> kCovLog2Tile;
     d->max_span = max_span > 0 ? max_span : 1;
     COV_TRY(hipMalloc(&d->d_gfirst, sizeof(int64_t) * (size_t)(n > 0 ? n : 1)));
     COV_TRY(hipMalloc(&d->d_spanu, sizeof(uint32_t) * (size_t)(n > 0 ? n : 1)));
@@ -198,7 +245,7 @@ int cov_upload(CovDevice* d, const std::vector<int64_t>& gfirst, const std::vect
 // one pass over the uploaded reads: hist_out[0 .. max_cov] = depth bins (max_cov = More),
 // hist_out[max_cov + 1 .. 2 max_cov + 1] = unique-depth bins
 int cov_run(CovDevice* d, int32_t max_cov, uint64_t* hist_out, double* kernel_ms, std::string& err) {
-    if (max_cov < 1 || max_cov > kCovMaxBins) { err = "maxCoverage outside [1, 2048]"; return -1; }
+    if (max_cov < 1 || max_cov > kCovMaxBins) { err = "maxCoverage outside [1, 1024]"; return -1; }
     COV_TRY(hipSetDevice(d->ordinal));
     const int nb = 2 * (max_cov + 1);
     if (nb > d->hist_cap) {
@@ -211,9 +258,22 @@ int cov_run(CovDevice* d, int32_t max_cov, uint64_t* hist_out, double* kernel_ms
     float ms = 0.f;
     if (d->n_tiles > 0) {
         if (d->n_tiles > 0x7fffffff) { err = "coordinate space too large for one launch"; return -1; }
-        hipExtLaunchKernelGGL(kc_tile_hist, dim3((unsigned)d->n_tiles), dim3(kCovThreads), sizeof(uint32_t) * (size_t)nb,
-                              d->stream, d->ev[0], d->ev[1], 0, d->d_gfirst, d->d_spanu, d->d_tstart, d->g_len,
-                              d->max_span, max_cov, d->d_hist);
+        // tile width 4096 (NGSEP_COV_TILE=2048 selects the narrow tile, diagnostics); as many workgroups as are
+        // co-resident, each walking tiles with a grid stride
+        const size_t lds = sizeof(uint32_t) * 4 * (size_t)nb;
+        static const bool narrow_env = std::getenv("NGSEP_COV_TILE") && std::atoi(std::getenv("NGSEP_COV_TILE")) == 2048;
+        const bool narrow = narrow_env || lds > 32768;
+        const int64_t ntl = narrow ? (d->g_len + 2047) >> 11 : d->n_tiles;
+        int per_cu = 0;
+        if (narrow) COV_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kc_tile_hist<11>, kCovThreads, lds));
+        else COV_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kc_tile_hist<12>, kCovThreads, lds));
+        const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(ntl, (int64_t)d->n_cu * std::max(1, per_cu)));
+        if (narrow)
+            hipExtLaunchKernelGGL(kc_tile_hist<11>, dim3((unsigned)grid), dim3(kCovThreads), lds, d->stream, d->ev[0], d->ev[1],
+                                  0, d->d_gfirst, d->d_spanu, d->d_tstart, d->g_len, ntl, d->max_span, max_cov, d->d_hist);
+        else
+            hipExtLaunchKernelGGL(kc_tile_hist<12>, dim3((unsigned)grid), dim3(kCovThreads), lds, d->stream, d->ev[0], d->ev[1],
+                                  0, d->d_gfirst, d->d_spanu, d->d_tstart, d->g_len, ntl, d->max_span, max_cov, d->d_hist);
         COV_TRY(hipGetLastError());
     }
     COV_TRY(hipMemcpyAsync(hist_out, d->d_hist, sizeof(unsigned long long) * (size_t)nb, hipMemcpyDeviceToHost, d->stream));

@@ -1087,8 +1087,8 @@ extern "C" int ngsep_open(int device, const ngsep_params* params, ngsep_ctx** ou
     c->device = device;
     if (c->params.coverage_stats) {
         *out = c;
-        if (c->params.max_coverage < 1 || c->params.max_coverage > 2048)
-            return set_error(c, NGSEP_E_UNSUPPORTED, "maxCoverage outside [1, 2048] (LDS histogram of the coverage kernel)");
+        if (c->params.max_coverage < 1 || c->params.max_coverage > 1024)
+            return set_error(c, NGSEP_E_UNSUPPORTED, "maxCoverage outside [1, 1024] (LDS histograms of the coverage kernel)");
         if (c->params.multisample || c->params.query_seq[0])
             return set_error(c, NGSEP_E_INVALID, "coverage statistics take no samples and no query region");
     }

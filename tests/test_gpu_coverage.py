@@ -25,7 +25,7 @@ def gpu_text(bam, out, fa=None, **setters):
     return open(out).read(), calc
 
 
-@pytest.mark.parametrize("max_cov", [300, 3, 1])
+@pytest.mark.parametrize("max_cov", [1024, 300, 3, 1])
 def test_kat_identical(tmp_path, max_cov):
     """Indels, N skips longer than a tile, soft clips, secondary / low-MAPQ / unmapped records."""
     fa, sam = coverage_kat.write(tmp_path)
