@@ -37,6 +37,8 @@ CASES = {
                                            lower_frac=0.01, quality_model=2, snv_rate=3e-3),
                                       {"calc_strand_bias": 1, "ploidy": 1, "min_quality": 20}),
 }
+# CoverageStats (CoverageStatisticsCalculator) fixtures: synth case -> (min_mq, max_coverage)
+COVERAGE_CASES = {"edge_2contigs_25x": (20, 300), "c1_chrI_10x": (20, 12)}
 DUMP_CASE = ("dump_custom8k_30x", dict(genome=2, custom_len=8000, depth=30, seed=5, noqual_rate=0.01,
                                        softclip_rate=0.05, quality_model=2))
 
@@ -124,6 +126,14 @@ def oracle_fixtures():
             g.write(f.read())
         open(os.path.join(HERE, name + ".sam.md5"), "w").write(md5(sam) + "\n")
         print(name, "ok")
+        for name, (min_mq, max_cov) in COVERAGE_CASES.items():
+            skw, _ = CASES[name]
+            syn = pysynth.Synth(**skw)
+            fa, sam, _ = syn.write(os.path.join(d, name))
+            syn.close()
+            ngsep_oracle.run_coverage(fa, sam, os.path.join(HERE, name + ".coverage.txt"), min_mq=min_mq,
+                                      max_coverage=max_cov)
+            print(name, "coverage ok")
 
 
 if __name__ == "__main__":

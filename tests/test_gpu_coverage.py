@@ -110,3 +110,22 @@ def test_cli(tmp_path):
     assert open(out).read() == coverage_kat.text(*coverage_kat.expected(300))
     r = subprocess.run([exe, "CoverageStats", "-i", bam], check=True, timeout=60, capture_output=True, text=True)
     assert r.stdout == coverage_kat.text(*coverage_kat.expected(300))
+
+
+@pytest.mark.parametrize("name", ["c1_chrI_10x", "edge_2contigs_25x"])
+def test_golden_coverage(tmp_path, name):
+    """HIP path vs the committed oracle fixtures (tests/golden/*.coverage.txt), no oracle run needed."""
+    import hashlib
+    import importlib.util
+    golden = os.path.join(ROOT, "tests", "golden")
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(golden, "make_golden.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    skw, _ = m.CASES[name]
+    min_mq, max_cov = m.COVERAGE_CASES[name]
+    syn = pysynth.Synth(**skw)
+    fa, sam, bam = syn.write(os.path.join(str(tmp_path), name))
+    syn.close()
+    assert hashlib.md5(open(sam, "rb").read()).hexdigest() == open(os.path.join(golden, name + ".sam.md5")).read().strip()
+    g, _ = gpu_text(bam, os.path.join(str(tmp_path), "g.txt"), fa, setMinMQ=min_mq, setMaxCoverage=max_cov)
+    assert g == open(os.path.join(golden, name + ".coverage.txt")).read()
