@@ -404,6 +404,7 @@ static int choose_tile(const std::vector<int32_t>& cov_max16, int64_t g_len, std
     double best_cost = -1;
     std::vector<int32_t> best_rows;
     const int64_t budget = kScanRegUnits;   // 16-byte units held in registers
+    static const bool no_planes = std::getenv("NGSEP_NO_PLANES") != nullptr;
     for (int T = kTileMinPos; T <= kTileMaxPos; T *= 2) {
         if (T > kTileMinPos) {
             std::vector<int32_t> nxt((cur.size() + 1) / 2);
@@ -418,8 +419,13 @@ static int choose_tile(const std::vector<int32_t>& cov_max16, int64_t g_len, std
             bytes += (double)cur[t] * T;
             if ((int64_t)cur[t] * (T / 16) > budget) over++;
         }
-        if (over * 1000 > ntiles) continue;
-        const double cost = bytes + 2048.0 * (double)ntiles;
+        // tiles of 128..512 positions are scanned as bit planes (2 bits per row-position: a quarter of the
+        // byte pile, streamed in 64-row chunks, so the byte kernel's register budget does not apply); the
+        // per-tile term prices the tile's fixed instruction stream.  Measured on the 30x yeast / chr20
+        // genomes: T = 512 scans in 0.041 / 0.144 ms vs 0.048 / 0.188 ms at T = 256.
+        const bool planes = (T == 128 || T == 256 || T == 512) && !no_planes;
+        if (!planes && over * 1000 > ntiles) continue;
+        const double cost = (planes ? bytes / 4 : bytes) + 2048.0 * (double)ntiles;
         if (best_cost < 0 || cost < best_cost) { best_cost = cost; bestT = T; best_rows.assign(cur.begin(), cur.begin() + ntiles); }
     }
     if (const char* e = std::getenv("NGSEP_TILE_T")) {   // tests and tuning: a fixed tile width
