@@ -520,6 +520,9 @@ template <int MODE>
 #ifndef NGSEP_KT_WAVES_PER_EU
 #define NGSEP_KT_WAVES_PER_EU 4      // build-time tuning: resident waves per SIMD the register budget targets
 #endif
+#ifndef NGSEP_KT16_WAVES_PER_EU
+#define NGSEP_KT16_WAVES_PER_EU 3    // the same for the 512-position plane tiles (118 VGPRs at 3: 4 waves resident)
+#endif
 __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(NGSEP_KT_WAVES_PER_EU)))
 void k_tile_pileup(
     const u32x4* __restrict__ pile, const TileInfo* __restrict__ tinfo, const uint8_t* __restrict__ ref,
@@ -791,7 +794,7 @@ struct BsCount<1> {
 };
 
 template <int W>
-__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(W >= 16 ? 3 : NGSEP_KT_WAVES_PER_EU)))
+__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(W >= 16 ? NGSEP_KT16_WAVES_PER_EU : NGSEP_KT_WAVES_PER_EU)))
 void k_tile_planes(const uint32_t* __restrict__ planes, const uint8_t* __restrict__ pile, const TileInfo* __restrict__ tinfo,
                    const uint8_t* __restrict__ ref, int64_t n_tiles, const LikTables* __restrict__ tabs, GenotypeParams gp,
                    QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap,
