@@ -1,0 +1,117 @@
+"""Contig sharding across the GPUs of one node: one process per GPU, no collective on
+the hot path.
+
+Sequences are independent units of SingleSampleVariantsDetector: the reference writes each sequence's
+calls sorted on onSequenceEnd (SingleSampleVariantsDetector.java:933-968, 1026-1032), so the VCF of a
+whole run is the header followed by the per-sequence record blocks in reference order.  Each rank calls
+the sequences assigned to it (largest first onto the least-loaded rank), the record blocks are gathered
+to rank 0 once at the end (a host-side object gather over torch.distributed: nccl/RCCL on the GPU
+node, gloo in the CPU tests) and rank 0 writes header + blocks in reference order -- byte-identical to
+the single-process output.
+"""
+from __future__ import annotations
+
+import os
+import tempfile
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+
+def assign_contigs(contigs: Sequence[Tuple[str, int]], world: int) -> List[List[str]]:
+    """Longest-processing-time assignment of (name, length) sequences to `world` ranks; ties go to the
+    lowest rank, so every rank computes the same assignment."""
+    if world < 1:
+        raise ValueError("world size must be >= 1")
+    load = [0] * world
+    out: List[List[str]] = [[] for _ in range(world)]
+    order = sorted(range(len(contigs)), key=lambda i: (-int(contigs[i][1]), i))
+    for i in order:
+        r = min(range(world), key=lambda k: (load[k], k))
+        out[r].append(contigs[i][0])
+        load[r] += int(contigs[i][1])
+    return out
+
+
+def split_vcf(text: str) -> Tuple[str, Dict[str, str]]:
+    """VCF text -> (header, {sequence: its record lines})."""
+    header, blocks = [], {}
+    for line in text.splitlines(keepends=True):
+        if line.startswith("#"):
+            header.append(line)
+        else:
+            seq = line.split("\t", 1)[0]
+            blocks[seq] = blocks.get(seq, "") + line
+    return "".join(header), blocks
+
+
+def merge_vcf(header: str, blocks: Dict[str, str], order: Sequence[str]) -> str:
+    """Header + record blocks in reference order (sequences without calls contribute nothing)."""
+    extra = set(blocks) - set(order)
+    if extra:
+        raise ValueError(f"records on sequences outside the reference: {sorted(extra)}")
+    return header + "".join(blocks.get(s, "") for s in order)
+
+
+def gather_blocks(local: Dict[str, str], dist=None) -> Optional[Dict[str, str]]:
+    """Rank 0 receives every rank's {sequence: records}; other ranks get None.  Without a process group
+    (single process) the local blocks are returned."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return dict(local)
+    rank = dist.get_rank()
+    got = [None] * dist.get_world_size() if rank == 0 else None
+    dist.gather_object(local, got, dst=0)
+    if rank != 0:
+        return None
+    merged: Dict[str, str] = {}
+    for part in got:
+        for seq, rec in part.items():
+            if seq in merged:
+                raise ValueError(f"sequence {seq} called on two ranks")
+            merged[seq] = rec
+    return merged
+
+
+def call_sharded(contigs: Sequence[Tuple[str, int]], call_contig: Callable[[str], str], out_vcf: str,
+                 dist=None) -> Optional[str]:
+    """Runs `call_contig(name) -> VCF text of that sequence` for this rank's sequences and writes the
+    merged VCF on rank 0 (returns its text there, None elsewhere)."""
+    world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
+    rank = dist.get_rank() if dist is not None and dist.is_initialized() else 0
+    mine = assign_contigs(contigs, world)[rank]
+    header = ""
+    local: Dict[str, str] = {}
+    for name in mine:
+        h, blocks = split_vcf(call_contig(name))
+        header = header or h
+        local.update(blocks)
+    # every rank may hold no calls; the header is the same on all ranks (options + reference)
+    if world > 1:
+        hs = [None] * world if rank == 0 else None
+        dist.gather_object(header, hs, dst=0)
+        if rank == 0:
+            header = next((x for x in hs if x), "")
+    merged = gather_blocks(local, dist)
+    if merged is None:
+        return None
+    text = merge_vcf(header, merged, [c[0] for c in contigs])
+    with open(out_vcf, "w") as f:
+        f.write(text)
+    return text
+
+
+def gpu_contig_caller(fasta: str, bam: str, params=None, device: int = 0) -> Callable[[str], str]:
+    """The production per-sequence caller: SingleSampleVariantsDetector.findSNVS restricted to one
+    sequence (-querySeq) on this rank's GPU (libngsep_amd.so path B)."""
+    from .discovery import GpuPileupSession, default_params
+
+    def call(name: str) -> str:
+        p = params if params is not None else default_params()
+        import ctypes
+        q = type(p)()
+        ctypes.pointer(q)[0] = p
+        q.query_seq = name.encode()
+        with tempfile.TemporaryDirectory() as d, GpuPileupSession(q, device) as s:
+            s.load_fasta(fasta)
+            out = os.path.join(d, "c.vcf")
+            s.processFile(bam, out)
+            return open(out).read()
+    return call
