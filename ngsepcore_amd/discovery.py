@@ -136,6 +136,22 @@ class GpuPileupSession:
         """SingleSampleVariantsDetector.findSNVS on a BAM file, VCF written to out_vcf."""
         self._check(self._lib.ngsep_call_bam(self._ctx, bam_path.encode(), out_vcf.encode()))
 
+    def processFileBatches(self, bam_path: str, batch_reads: int = 1 << 20):
+        """Path A fed by the C++ reader: the BAM's reader-filtered alignments in batches through
+        processAlignments, then notifyEndOfAlignments (what a JNI host with its own reader does)."""
+        b = ctypes.c_void_p()
+        self._check(self._lib.ngsep_bam_open(self._ctx, bam_path.encode(), ctypes.byref(b)))
+        try:
+            batch = NgsepReadBatch()
+            while True:
+                self._check(self._lib.ngsep_bam_next_batch(b, batch_reads, ctypes.byref(batch)))
+                if batch.n_reads == 0:
+                    break
+                self.processAlignments(batch)
+        finally:
+            self._lib.ngsep_bam_close(b)
+        self.notifyEndOfAlignments()
+
     # -- staged runs (measurement)
     def stage(self, batch: NgsepReadBatch):
         self._check(self._lib.ngsep_stage_alignments(self._ctx, ctypes.byref(batch)))

@@ -3,7 +3,7 @@
 1. reference_demo_pl.csv.gz -- data extracted from the reference's own output file
    training/yeastDemo_ann_q40_s_fi_I2_noREP_noCNV.vcf.gz (an NGSEP VCF, 2 samples): every
    biallelic-SNV genotype field whose BSDP holds only REF/ALT base counts, as
-   (n_ref, n_alt, ref_idx, alt_idx, PL0, PL1, PL2, DP).  Needs /root/reference (read only).
+   (n_ref, n_alt, ref_idx, alt_idx, PL0, PL1, PL2, DP, GQ, GT).  Needs /root/reference (read only).
 2. <case>.vcf / <case>.dump.gz -- outputs of the oracle (CPU restatement) on seeded synthetic
    inputs (tools/synth), plus <case>.sam.md5 pinning the generator's output.  The GPU tests
    compare the HIP path with these files without running the oracle.
@@ -57,15 +57,15 @@ def reference_fixture(out_path: str) -> int:
             ri, ai = "ACGT".index(ref), "ACGT".index(alt)
             for s in fs[9:]:
                 d = dict(zip(fmt, s.split(":")))
-                if "BSDP" not in d or "PL" not in d or "DP" not in d:
+                if "BSDP" not in d or "PL" not in d or "DP" not in d or "GQ" not in d:
                     continue
                 b = [int(x) for x in d["BSDP"].split(",")]
                 if sum(b) != b[ri] + b[ai]:
                     continue
                 pl = d["PL"].split(",")
-                rows.append(f"{b[ri]},{b[ai]},{ri},{ai},{pl[0]},{pl[1]},{pl[2]},{d['DP']}\n")
+                rows.append(f"{b[ri]},{b[ai]},{ri},{ai},{pl[0]},{pl[1]},{pl[2]},{d['DP']},{d['GQ']},{d['GT']}\n")
     with gzip.GzipFile(out_path, "wb", mtime=0) as g:
-        g.write(b"n_ref,n_alt,ref_idx,alt_idx,pl_rr,pl_ra,pl_aa,dp\n")
+        g.write(b"n_ref,n_alt,ref_idx,alt_idx,pl_rr,pl_ra,pl_aa,dp,gq,gt\n")
         g.write("".join(rows).encode())
     return len(rows)
 

@@ -71,6 +71,9 @@ def diff_vcf(a_path, b_path, limit=10):
             out.append("only gpu:    " + l)
             if len(out) > 2 * limit:
                 break
+    if not out and a != b:   # same lines, different order or multiplicity
+        i = next(k for k in range(min(len(a), len(b))) if a[k] != b[k])
+        out.append(f"record order differs at line {i + 1}: {a[i]!r} vs {b[i]!r}")
     return out
 
 

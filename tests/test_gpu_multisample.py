@@ -103,3 +103,22 @@ def test_population_bams_path_b(tmp_path):
     subprocess.run([cli, "MultisampleVariantsDetector", "-r", fa, "-o", out_cli] + bams, check=True)
     diff = diff_vcf(o, out_cli)
     assert not diff, "\n".join(diff[:20])
+
+
+def test_reference_fields_replayed_on_gpu(tmp_path):
+    """The reference's own genotype fields (training/yeastDemo_*.vcf.gz, the 10,508 all-Q30-consistent
+    ones, tests/demo_replay.py) replayed as Q30 pileups through the HIP population path (KTM + KPM, BAM
+    decoded in C++): GT, PL, GQ, DP and BSDP equal the reference's own output."""
+    import demo_replay as R
+    from ngsepcore_amd import MultisampleVariantsDetector
+    rs = R.rows()
+    fa, sam, site = R.write(tmp_path, R.keys(rs))
+    bam = pysynth.sam_to_bam(sam, os.path.join(str(tmp_path), "demo.bam"))
+    d = MultisampleVariantsDetector()
+    d.setGenome(fa)
+    d.setMaxAlnsPerStartPos(0)
+    d.setOutFilename(os.path.join(str(tmp_path), "replay_gpu.vcf"))
+    d.run([bam]).close()
+    checked, bad = R.check(rs, site, R.parse_vcf(d.outFilename))
+    assert not bad, bad[:10]
+    assert checked == 10508

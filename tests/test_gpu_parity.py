@@ -227,3 +227,37 @@ def test_tile_width_vcf_identical(tmp_path, monkeypatch, tile):
     d = diff_vcf(o, g)
     assert not d, "\n".join(d)
     assert gst.tile_positions == tile
+
+
+def test_reference_fields_single_sample_dump(tmp_path):
+    """The reference's genotype fields replayed as Q30 pileups (tests/demo_replay.py, sample S0 only)
+    through the single-sample HIP path in dump mode (KT + KP, every covered position): DP, BSDP and the
+    PL triple from the fp64 log-conditionals (float cast, Math.round) equal the reference's own output
+    for all 10,508 all-Q30-consistent fields."""
+    import math
+    import numpy as np
+    import demo_replay as R
+    rs = R.rows()
+    fa, sam, site = R.write(tmp_path, R.keys(rs))
+    lines = [l for l in open(sam) if l.startswith("@") or not l.rstrip("\n").endswith("RG:Z:S1")]
+    open(sam, "w").writelines(lines)
+    bam = pysynth.sam_to_bam(sam, os.path.join(str(tmp_path), "demo_s0.bam"))
+    with GpuPileupSession(gpu_params(dump_all_positions=1, max_alns_per_start=0)) as s:
+        s.load_fasta(fa)
+        s.processFileBatches(bam)
+        got = {x.pos: x for x in s.getCalledVariants()}
+    pl = lambda v: int(math.floor(-10.0 * float(np.float32(v)) + 0.5))
+    checked = 0
+    by_key = {k: got.get(p) for p, k in site.items()}
+    for r in rs:
+        nr, na, ri, ai, dp = (int(r["n_ref"]), int(r["n_alt"]), int(r["ref_idx"]), int(r["alt_idx"]), int(r["dp"]))
+        x = by_key[(nr, na, ri, ai, dp)]
+        assert x is not None and x.dp == dp
+        bsdp = [0, 0, 0, 0]
+        bsdp[ri] += nr
+        bsdp[ai] += na
+        assert x.counts == bsdp
+        got_pl = (pl(x.log_conditional(ri, ri)), pl(x.log_conditional(ri, ai)), pl(x.log_conditional(ai, ai)))
+        if got_pl == (int(r["pl_rr"]), int(r["pl_ra"]), int(r["pl_aa"])):
+            checked += 1
+    assert checked == 10508
