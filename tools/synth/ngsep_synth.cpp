@@ -1,16 +1,25 @@
-// ngsep_synth.cpp -- seeded synthetic FASTA / SAM / BAM / truth for tests and bench.py.
+// ngsep_synth.cpp -- seeded synthetic FASTA / SAM / BAM (+BAI) / truth for tests and bench.py.
 // Test/bench data infrastructure; the product never links it.
+//
+// Records are kept as a structure of arrays (one entry per BAM record, the bases and qualities in two
+// shared byte arrays; PCR-duplicate and secondary copies share their original's bytes), so a human
+// chromosome at 30x fits in a few GB.  The BAM writer deflates its BGZF blocks on all cores and writes
+// a BAI index (SAM spec section 5) next to the file.
 #include "ngsep_synth.h"
 
+#include <dlfcn.h>
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cctype>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -50,16 +59,44 @@ const ContigDef kHuman[] = {
     {"chr21", 46709983}, {"chr22", 50818468}, {"chrX", 156040895}, {"chrY", 57227415}};
 
 const char kBases[] = "ACGT";
+const char kOps[] = "HDIMPNSX";           // NGSEP op codes (ReadAlignment.java:60-67) -> SAM letters
 
-struct Read {
-    int32_t contig, pos, flags, mapq;
-    int32_t sample = 0;             // index into the sample list (RG/SM S%03d of sample_idx + sample)
-    std::string name, cigar_s;      // SAM CIGAR text
-    std::vector<int32_t> cigar;     // NGSEP codes
-    std::string seq, qual;          // qual empty -> '*'
-};
+// error probability of a phred score, 10^(-q/10), tabulated once (the same doubles std::pow returns)
+const double* err_table() {
+    static double t[94];
+    static bool init = [] { for (int q = 0; q < 94; q++) t[q] = std::pow(10.0, -q / 10.0); return true; }();
+    (void)init;
+    return t;
+}
 
 struct Snv { int32_t contig, pos; char ref, alt; int gt; };  // gt 1 het, 2 hom
+
+// every record in BAM order (incl. those the reader filters)
+struct Records {
+    std::vector<int32_t> contig, pos, flags, mapq, sample, cig_n, seq_len;
+    std::vector<int64_t> readno, cig_off, seq_off;
+    std::vector<uint8_t> suffix, hasq;     // name suffix 0 / 'd' (PCR duplicate) / 's' (secondary)
+    std::vector<int32_t> cigar;            // NGSEP codes len*8+op
+    std::string bases, quals;              // quals are '!' for a record without qualities
+    size_t size() const { return pos.size(); }
+    void push(int32_t c, int32_t p, int32_t fl, int32_t mq, int32_t sm, int64_t no, uint8_t sfx, int64_t coff, int32_t cn,
+              int64_t soff, int32_t sl, uint8_t hq) {
+        contig.push_back(c); pos.push_back(p); flags.push_back(fl); mapq.push_back(mq); sample.push_back(sm);
+        readno.push_back(no); suffix.push_back(sfx); cig_off.push_back(coff); cig_n.push_back(cn);
+        seq_off.push_back(soff); seq_len.push_back(sl); hasq.push_back(hq);
+    }
+    // records [from, size()) reordered by idx (relative to from)
+    void permute(size_t from, const std::vector<size_t>& idx) {
+        auto perm = [&](auto& v) {
+            using V = typename std::decay<decltype(v)>::type;
+            V tmp(idx.size());
+            for (size_t i = 0; i < idx.size(); i++) tmp[i] = v[from + idx[i]];
+            std::copy(tmp.begin(), tmp.end(), v.begin() + (ptrdiff_t)from);
+        };
+        perm(contig); perm(pos); perm(flags); perm(mapq); perm(sample); perm(cig_n); perm(seq_len);
+        perm(readno); perm(cig_off); perm(seq_off); perm(suffix); perm(hasq);
+    }
+};
 
 }  // namespace
 
@@ -67,13 +104,12 @@ struct ngs_synth {
     ngs_synth_params p;
     std::vector<std::string> names;
     std::vector<std::string> seqs;
-    std::vector<Read> reads;   // all records in BAM order (incl. filtered ones)
+    Records rec;
     std::vector<Snv> truth;
-    // batch storage
-    std::vector<int32_t> b_seq, b_first, b_flags, b_rg, b_cig_n, b_cigar, b_seqlen;
+    // batch view (reader-filtered records; bases/quals/cigar point into rec's arrays)
+    std::vector<int32_t> b_seq, b_first, b_flags, b_rg, b_cig_n, b_seqlen;
     std::vector<int64_t> b_cig_off, b_seq_off;
     std::vector<uint8_t> b_hasq;
-    std::string b_bases, b_quals;
 };
 
 extern "C" void ngs_synth_default(ngs_synth_params* p) {
@@ -102,6 +138,84 @@ static int sample_quality(Rng& r, int model) {
 static void make_population(ngs_synth* s);
 static void make_batch(ngs_synth* s);
 
+// the kept contigs of the genome table, optionally truncated (trunc_len)
+static std::vector<ContigDef> kept_contigs(const ngs_synth_params& p, int* first_out, double* pa) {
+    std::vector<ContigDef> defs;
+    *pa = 0.31;  // P(A)=P(T)
+    if (p.genome == NGS_GENOME_YEAST) defs.assign(std::begin(kYeast), std::end(kYeast));
+    else if (p.genome == NGS_GENOME_HUMAN) { defs.assign(std::begin(kHuman), std::end(kHuman)); *pa = 0.295; }
+    else defs.push_back({"chrS", p.custom_len});
+    int first = std::max(0, p.contig_first);
+    first = std::min<int>(first, (int)defs.size());
+    int n = p.n_contigs > 0 ? std::min<int>(p.n_contigs, (int)defs.size() - first) : (int)defs.size() - first;
+    std::vector<ContigDef> keep(defs.begin() + first, defs.begin() + first + n);
+    if (p.trunc_len > 0)
+        for (auto& d : keep) d.len = std::min<int64_t>(d.len, p.trunc_len);
+    *first_out = first;
+    return keep;
+}
+
+// reference, seed 0x4E475345 + contig index
+static std::string make_reference(const ngs_synth_params& p, int contig_index, int64_t len, double pa) {
+    Rng r(0x4E475345ull + (uint64_t)contig_index + (p.seed << 32));
+    std::string seq((size_t)len, 'A');
+    for (int64_t i = 0; i < len; i++) {
+        double u = r.uniform();
+        char b = u < pa ? 'A' : u < 0.5 ? 'C' : u < 1.0 - pa ? 'G' : 'T';
+        if (p.lower_frac > 0 && r.uniform() < p.lower_frac) b = (char)(b - 'A' + 'a');
+        seq[(size_t)i] = b;
+    }
+    return seq;
+}
+
+// one simulated read (and whether it gets a PCR-duplicate / secondary copy): haplotype, strand, MAPQ,
+// bases with substitution errors at their phred probability and N at Q2, optional soft clip, missing
+// qualities.  The order of draws from r is the generator's data contract (golden fixtures pin it).
+struct GenOut { int32_t pos, flags, mapq, cn; uint8_t hq; bool dup, sec; };
+static GenOut gen_read(Rng& r, const ngs_synth_params& p, const std::string& h0, const std::string& h1, int64_t L,
+                       int32_t pos, const double* et, char* bases, char* quals, int32_t* cig) {
+    GenOut o{};
+    const int rl = p.read_len;
+    const std::string& hap = r.below(2) ? h1 : h0;
+    o.flags = r.below(2) ? 16 : 0;
+    o.mapq = (p.lowmq_rate > 0 && r.uniform() < p.lowmq_rate) ? 5 : 60;
+    for (int i = 0; i < rl; i++) {
+        char b = hap[pos - 1 + i];
+        int q = sample_quality(r, p.quality_model);
+        if (r.uniform() < et[q]) {
+            int bi = (int)(std::strchr(kBases, b) - kBases);
+            b = kBases[(bi + 1 + (int)r.below(3)) % 4];
+        }
+        if (p.n_frac > 0 && r.uniform() < p.n_frac) { b = 'N'; q = 2; }
+        bases[i] = b;
+        quals[i] = (char)(33 + q);
+    }
+    int clip = 0, clip_end = 0;
+    if (p.softclip_rate > 0 && r.uniform() < p.softclip_rate) { clip = 5 + (int)r.below(16); clip_end = (int)r.below(2); }
+    if (clip && clip_end) {          // soft clip keeps the read characters
+        cig[0] = (rl - clip) * 8 + 3;
+        cig[1] = clip * 8 + 6;
+        o.cn = 2;
+    } else if (clip && pos + clip + (rl - clip) - 1 <= L) {   // a leading clip shifts the aligned start
+        cig[0] = clip * 8 + 6;
+        cig[1] = (rl - clip) * 8 + 3;
+        o.cn = 2;
+        pos += clip;
+    } else {
+        cig[0] = rl * 8 + 3;
+        o.cn = 1;
+    }
+    o.hq = 1;
+    if (p.noqual_rate > 0 && r.uniform() < p.noqual_rate) {
+        o.hq = 0;
+        std::memset(quals, '!', (size_t)rl);
+    }
+    o.dup = p.dup_rate > 0 && r.uniform() < p.dup_rate;
+    o.sec = p.secondary_rate > 0 && r.uniform() < p.secondary_rate;
+    o.pos = pos;
+    return o;
+}
+
 extern "C" ngs_synth* ngs_synth_create(const ngs_synth_params* pp) {
     ngs_synth* s = new ngs_synth();
     s->p = *pp;
@@ -111,32 +225,23 @@ extern "C" ngs_synth* ngs_synth_create(const ngs_synth_params* pp) {
         make_batch(s);
         return s;
     }
-    std::vector<ContigDef> defs;
-    double pa = 0.31;  // P(A)=P(T)
-    if (p.genome == NGS_GENOME_YEAST) defs.assign(std::begin(kYeast), std::end(kYeast));
-    else if (p.genome == NGS_GENOME_HUMAN) { defs.assign(std::begin(kHuman), std::end(kHuman)); pa = 0.295; }
-    else defs.push_back({"chrS", p.custom_len});
-    int first = std::max(0, p.contig_first);
-    int n = p.n_contigs > 0 ? std::min<int>(p.n_contigs, (int)defs.size() - first) : (int)defs.size() - first;
-    std::vector<ContigDef> keep(defs.begin() + first, defs.begin() + first + n);
-    // reference, seed 0x4E475345 + contig index
+    double pa;
+    int first;
+    const std::vector<ContigDef> keep = kept_contigs(p, &first, &pa);
     for (size_t c = 0; c < keep.size(); c++) {
-        Rng r(0x4E475345ull + (uint64_t)(first + c) + (p.seed << 32));
-        std::string seq(keep[c].len, 'A');
-        for (int64_t i = 0; i < keep[c].len; i++) {
-            double u = r.uniform();
-            char b = u < pa ? 'A' : u < 0.5 ? 'C' : u < 1.0 - pa ? 'G' : 'T';
-            if (p.lower_frac > 0 && r.uniform() < p.lower_frac) b = (char)(b - 'A' + 'a');
-            seq[i] = b;
-        }
         s->names.push_back(keep[c].name);
-        s->seqs.push_back(std::move(seq));
+        s->seqs.push_back(make_reference(p, first + (int)c, keep[c].len, pa));
     }
-    Rng r(p.seed * 0x9E3779B97F4A7C15ull + 17 + (uint64_t)p.sample_idx * 7919);
-    char rg[16];
-    std::snprintf(rg, sizeof rg, "S%03d", p.sample_idx);
+    const uint64_t base_seed = p.seed * 0x9E3779B97F4A7C15ull + 17 + (uint64_t)p.sample_idx * 7919;
+    Rng r(base_seed);
+    const double* et = err_table();
+    Records& R = s->rec;
     int64_t readno = 0;
     for (size_t c = 0; c < s->seqs.size(); c++) {
+        // rng_per_contig: every contig's donor and reads come from their own streams (reads in chunks,
+        // generated in parallel), so one contig generated alone (a rank's shard of the genome) equals that
+        // contig of the whole-genome run
+        if (p.rng_per_contig) r = Rng(base_seed + 0x632BE59BD9B4E019ull * (uint64_t)(first + (int)c + 1));
         const std::string& ref = s->seqs[c];
         int64_t L = (int64_t)ref.size();
         // donor haplotypes
@@ -156,75 +261,57 @@ extern "C" ngs_synth* ngs_synth_create(const ngs_synth_params* pp) {
             }
         }
         int rl = p.read_len;
-        size_t cstart = s->reads.size();
+        size_t cstart = R.size();
         if (L < rl) continue;
         int64_t nreads = (int64_t)std::llround(p.depth * (double)L / rl);
         struct Gen { int32_t pos; int64_t order; };
         std::vector<Gen> starts(nreads);
         for (int64_t k = 0; k < nreads; k++) starts[k] = {(int32_t)(1 + r.below((uint64_t)(L - rl + 1))), k};
         std::sort(starts.begin(), starts.end(), [](const Gen& a, const Gen& b) { return a.pos != b.pos ? a.pos < b.pos : a.order < b.order; });
+        // read k: bases/qualities at b0 + k*rl, CIGAR at c0 + 2k (<= 2 items)
+        const int64_t b0 = (int64_t)R.bases.size(), c0 = (int64_t)R.cigar.size();
+        R.bases.resize((size_t)(b0 + nreads * rl));
+        R.quals.resize((size_t)(b0 + nreads * rl));
+        R.cigar.resize((size_t)(c0 + 2 * nreads));
+        std::vector<GenOut> outs((size_t)nreads);
+        auto gen = [&](Rng& rr, int64_t k) {
+            outs[(size_t)k] = gen_read(rr, p, h0, h1, L, starts[(size_t)k].pos, et, &R.bases[(size_t)(b0 + k * rl)],
+                                       &R.quals[(size_t)(b0 + k * rl)], &R.cigar[(size_t)(c0 + 2 * k)]);
+        };
+        if (p.rng_per_contig) {
+            // independent streams per chunk of 65536 reads: generated on all cores
+            constexpr int64_t kChunk = 65536;
+            const int64_t nchunk = (nreads + kChunk - 1) / kChunk;
+            const uint64_t cseed = base_seed + 0x632BE59BD9B4E019ull * (uint64_t)(first + (int)c + 1);
+            std::atomic<int64_t> next{0};
+            auto work = [&]() {
+                for (int64_t j; (j = next.fetch_add(1)) < nchunk;) {
+                    Rng rr(cseed ^ (0xD1B54A32D192ED03ull * (uint64_t)(j + 1)));
+                    for (int64_t k = j * kChunk; k < std::min(nreads, (j + 1) * kChunk); k++) gen(rr, k);
+                }
+            };
+            std::vector<std::thread> th;
+            const unsigned nt = std::max(1u, std::min<unsigned>(std::thread::hardware_concurrency(), 16u));
+            for (unsigned t = 1; t < nt; t++) th.emplace_back(work);
+            work();
+            for (auto& t : th) t.join();
+        } else {
+            for (int64_t k = 0; k < nreads; k++) gen(r, k);
+        }
         for (int64_t k = 0; k < nreads; k++) {
-            Read rd;
-            rd.contig = (int32_t)c;
-            rd.pos = starts[k].pos;
-            const std::string& hap = r.below(2) ? h1 : h0;
-            rd.flags = r.below(2) ? 16 : 0;
-            rd.mapq = (p.lowmq_rate > 0 && r.uniform() < p.lowmq_rate) ? 5 : 60;
-            char nm[32];
-            std::snprintf(nm, sizeof nm, "r%09lld", (long long)readno++);
-            rd.name = nm;
-            rd.seq.resize(rl);
-            rd.qual.resize(rl);
-            for (int i = 0; i < rl; i++) {
-                char b = hap[rd.pos - 1 + i];
-                int q = sample_quality(r, p.quality_model);
-                double e = std::pow(10.0, -q / 10.0);
-                if (r.uniform() < e) {
-                    int bi = (int)(std::strchr(kBases, b) - kBases);
-                    b = kBases[(bi + 1 + (int)r.below(3)) % 4];
-                }
-                if (p.n_frac > 0 && r.uniform() < p.n_frac) { b = 'N'; q = 2; }
-                rd.seq[i] = b;
-                rd.qual[i] = (char)(33 + q);
-            }
-            int clip = 0, clip_end = 0;
-            if (p.softclip_rate > 0 && r.uniform() < p.softclip_rate) { clip = 5 + (int)r.below(16); clip_end = (int)r.below(2); }
-            if (clip) {
-                // soft clip keeps the read characters, shifts the aligned start to the first M base
-                char buf[64];
-                if (clip_end) {
-                    std::snprintf(buf, sizeof buf, "%dM%dS", rl - clip, clip);
-                    rd.cigar = {(rl - clip) * 8 + 3, clip * 8 + 6};
-                } else {
-                    std::snprintf(buf, sizeof buf, "%dS%dM", clip, rl - clip);
-                    rd.cigar = {clip * 8 + 6, (rl - clip) * 8 + 3};
-                    rd.pos += clip;
-                    if (rd.pos + (rl - clip) - 1 > L) { rd.pos -= clip; rd.cigar = {rl * 8 + 3}; std::snprintf(buf, sizeof buf, "%dM", rl); }
-                }
-                rd.cigar_s = buf;
-            } else {
-                rd.cigar_s = std::to_string(rl) + "M";
-                rd.cigar = {rl * 8 + 3};
-            }
-            if (p.noqual_rate > 0 && r.uniform() < p.noqual_rate) rd.qual.clear();
-            bool dup = p.dup_rate > 0 && r.uniform() < p.dup_rate;
-            bool sec = p.secondary_rate > 0 && r.uniform() < p.secondary_rate;
-            s->reads.push_back(rd);
-            if (dup) {
-                Read d = rd;
-                d.name += "d";
-                s->reads.push_back(d);
-            }
-            if (sec) {
-                Read d = rd;
-                d.name += "s";
-                d.flags |= 0x100;
-                s->reads.push_back(d);
-            }
+            const GenOut& o = outs[(size_t)k];
+            const int64_t no = readno++, soff = b0 + k * rl, coff = c0 + 2 * k;
+            R.push((int32_t)c, o.pos, o.flags, o.mapq, 0, no, 0, coff, o.cn, soff, rl, o.hq);
+            if (o.dup) R.push((int32_t)c, o.pos, o.flags, o.mapq, 0, no, 'd', coff, o.cn, soff, rl, o.hq);
+            if (o.sec) R.push((int32_t)c, o.pos, o.flags | 0x100, o.mapq, 0, no, 's', coff, o.cn, soff, rl, o.hq);
         }
         // keep BAM coordinate order: records were generated sorted except soft-clipped starts
-        std::stable_sort(s->reads.begin() + (ptrdiff_t)cstart, s->reads.end(),
-                         [](const Read& a, const Read& b) { return a.pos < b.pos; });
+        std::vector<size_t> idx(R.size() - cstart);
+        std::iota(idx.begin(), idx.end(), (size_t)0);
+        std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return R.pos[cstart + a] < R.pos[cstart + b]; });
+        bool sorted = true;
+        for (size_t i = 0; i < idx.size() && sorted; i++) sorted = idx[i] == i;
+        if (!sorted) R.permute(cstart, idx);
     }
     make_batch(s);
     return s;
@@ -238,30 +325,21 @@ extern "C" ngs_synth* ngs_synth_create(const ngs_synth_params* pp) {
 // BAM per sample with equal read lengths.
 static void make_population(ngs_synth* s) {
     const ngs_synth_params& p = s->p;
-    std::vector<ContigDef> defs;
-    double pa = 0.31;
-    if (p.genome == NGS_GENOME_YEAST) defs.assign(std::begin(kYeast), std::end(kYeast));
-    else if (p.genome == NGS_GENOME_HUMAN) { defs.assign(std::begin(kHuman), std::end(kHuman)); pa = 0.295; }
-    else defs.push_back({"chrS", p.custom_len});
-    int first = std::max(0, p.contig_first);
-    int n = p.n_contigs > 0 ? std::min<int>(p.n_contigs, (int)defs.size() - first) : (int)defs.size() - first;
+    double pa;
+    int first;
+    const std::vector<ContigDef> keep = kept_contigs(p, &first, &pa);
     const int ns = p.n_samples;
-    for (int c = 0; c < n; c++) {
-        const ContigDef& d = defs[first + c];
-        Rng r(0x4E475345ull + (uint64_t)(first + c) + (p.seed << 32));
-        std::string seq(d.len, 'A');
-        for (int64_t i = 0; i < d.len; i++) {
-            double u = r.uniform();
-            char b = u < pa ? 'A' : u < 0.5 ? 'C' : u < 1.0 - pa ? 'G' : 'T';
-            if (p.lower_frac > 0 && r.uniform() < p.lower_frac) b = (char)(b - 'A' + 'a');
-            seq[i] = b;
-        }
-        s->names.push_back(d.name);
-        s->seqs.push_back(std::move(seq));
+    for (size_t c = 0; c < keep.size(); c++) {
+        s->names.push_back(keep[c].name);
+        s->seqs.push_back(make_reference(p, first + (int)c, keep[c].len, pa));
     }
-    Rng r(p.seed * 0x9E3779B97F4A7C15ull + 31);
+    const uint64_t base_seed = p.seed * 0x9E3779B97F4A7C15ull + 31;
+    Rng r(base_seed);
+    const double* et = err_table();
+    Records& R = s->rec;
     int64_t readno = 0;
     for (size_t c = 0; c < s->seqs.size(); c++) {
+        if (p.rng_per_contig) r = Rng(base_seed + 0x632BE59BD9B4E019ull * (uint64_t)(first + (int)c + 1));
         const std::string& ref = s->seqs[c];
         const int64_t L = (int64_t)ref.size();
         // population variants: position, alt base, per-sample allele bits (bit0 hap0, bit1 hap1)
@@ -298,19 +376,12 @@ static void make_population(ngs_synth* s) {
             if (a.sample != b.sample) return a.sample < b.sample;
             return a.order < b.order;
         });
+        R.bases.reserve(R.bases.size() + starts.size() * (size_t)rl);
+        R.quals.reserve(R.quals.size() + starts.size() * (size_t)rl);
         for (const Gen& g : starts) {
-            Read rd;
-            rd.contig = (int32_t)c;
-            rd.pos = g.pos;
-            rd.sample = g.sample;
             const int hap = (int)r.below(2);
-            rd.flags = r.below(2) ? 16 : 0;
-            rd.mapq = 60;
-            char nm[32];
-            std::snprintf(nm, sizeof nm, "r%09lld", (long long)readno++);
-            rd.name = nm;
-            rd.seq.resize(rl);
-            rd.qual.resize(rl);
+            const int32_t flags = r.below(2) ? 16 : 0;
+            const int64_t soff = (int64_t)R.bases.size();
             size_t vi = (size_t)(std::lower_bound(vpos.begin(), vpos.end(), g.pos) - vpos.begin());
             for (int i = 0; i < rl; i++) {
                 const int32_t pos = g.pos + i;
@@ -318,46 +389,40 @@ static void make_population(ngs_synth* s) {
                 while (vi < vpos.size() && vpos[vi] < pos) vi++;
                 if (vi < vpos.size() && vpos[vi] == pos && ((vgt[vi * ns + g.sample] >> hap) & 1)) b = valt[vi];
                 int q = sample_quality(r, p.quality_model);
-                double e = std::pow(10.0, -q / 10.0);
-                if (r.uniform() < e) {
+                if (r.uniform() < et[q]) {
                     const char* pb = std::strchr(kBases, b);
                     int bi = pb ? (int)(pb - kBases) : 0;
                     b = kBases[(bi + 1 + (int)r.below(3)) % 4];
                 }
                 if (p.n_frac > 0 && r.uniform() < p.n_frac) { b = 'N'; q = 2; }
-                rd.seq[i] = b;
-                rd.qual[i] = (char)(33 + q);
+                R.bases.push_back(b);
+                R.quals.push_back((char)(33 + q));
             }
-            rd.cigar_s = std::to_string(rl) + "M";
-            rd.cigar = {rl * 8 + 3};
+            const int64_t coff = (int64_t)R.cigar.size();
+            R.cigar.push_back(rl * 8 + 3);
             const bool dup = p.dup_rate > 0 && r.uniform() < p.dup_rate;
-            s->reads.push_back(rd);
-            if (dup) {
-                Read d = rd;
-                d.name += "d";
-                s->reads.push_back(d);
-            }
+            const int64_t no = readno++;
+            R.push((int32_t)c, g.pos, flags, 60, g.sample, no, 0, coff, 1, soff, rl, 1);
+            if (dup) R.push((int32_t)c, g.pos, flags, 60, g.sample, no, 'd', coff, 1, soff, rl, 1);
         }
     }
 }
 
 static void make_batch(ngs_synth* s) {
     // batch view: reader filters with default options (drop secondary and MAPQ<20 without NH)
-    for (const Read& rd : s->reads) {
-        if (rd.flags & 0x100) continue;
-        if (rd.mapq < 20) continue;
-        s->b_seq.push_back(rd.contig);
-        s->b_first.push_back(rd.pos);
-        s->b_flags.push_back(rd.flags);
-        s->b_rg.push_back(rd.sample);
-        s->b_cig_off.push_back((int64_t)s->b_cigar.size());
-        s->b_cig_n.push_back((int32_t)rd.cigar.size());
-        for (int32_t v : rd.cigar) s->b_cigar.push_back(v);
-        s->b_seq_off.push_back((int64_t)s->b_bases.size());
-        s->b_seqlen.push_back((int32_t)rd.seq.size());
-        s->b_bases += rd.seq;
-        if (rd.qual.empty()) { s->b_quals += std::string(rd.seq.size(), '!'); s->b_hasq.push_back(0); }
-        else { s->b_quals += rd.qual; s->b_hasq.push_back(1); }
+    const Records& R = s->rec;
+    for (size_t i = 0; i < R.size(); i++) {
+        if (R.flags[i] & 0x100) continue;
+        if (R.mapq[i] < 20) continue;
+        s->b_seq.push_back(R.contig[i]);
+        s->b_first.push_back(R.pos[i]);
+        s->b_flags.push_back(R.flags[i]);
+        s->b_rg.push_back(R.sample[i]);
+        s->b_cig_off.push_back(R.cig_off[i]);
+        s->b_cig_n.push_back(R.cig_n[i]);
+        s->b_seq_off.push_back(R.seq_off[i]);
+        s->b_seqlen.push_back(R.seq_len[i]);
+        s->b_hasq.push_back(R.hasq[i]);
     }
 }
 
@@ -367,7 +432,11 @@ extern "C" const char* ngs_synth_contig_name(const ngs_synth* s, int i) { return
 extern "C" int64_t ngs_synth_contig_len(const ngs_synth* s, int i) { return (int64_t)s->seqs[i].size(); }
 extern "C" const char* ngs_synth_contig_seq(const ngs_synth* s, int i) { return s->seqs[i].data(); }
 extern "C" int64_t ngs_synth_n_reads(const ngs_synth* s) { return (int64_t)s->b_first.size(); }
-extern "C" int64_t ngs_synth_n_bases(const ngs_synth* s) { return (int64_t)s->b_bases.size(); }
+extern "C" int64_t ngs_synth_n_bases(const ngs_synth* s) {
+    int64_t n = 0;
+    for (int32_t l : s->b_seqlen) n += l;
+    return n;
+}
 
 extern "C" int ngs_synth_batch(ngs_synth* s, ngsep_read_batch* b) {
     b->n_reads = (int64_t)s->b_first.size();
@@ -377,11 +446,11 @@ extern "C" int ngs_synth_batch(ngs_synth* s, ngsep_read_batch* b) {
     b->read_group = s->b_rg.data();
     b->cigar_off = s->b_cig_off.data();
     b->cigar_n = s->b_cig_n.data();
-    b->cigar = s->b_cigar.data();
+    b->cigar = s->rec.cigar.data();
     b->seq_off = s->b_seq_off.data();
     b->seq_len = s->b_seqlen.data();
-    b->bases = s->b_bases.data();
-    b->quals = s->b_quals.data();
+    b->bases = s->rec.bases.data();
+    b->quals = s->rec.quals.data();
     b->has_quals = s->b_hasq.data();
     return 0;
 }
@@ -413,35 +482,94 @@ static std::string header_text(const ngs_synth* s) {
     return h;
 }
 
+static std::string read_name(const Records& R, size_t i) {
+    char nm[40];
+    int n = std::snprintf(nm, sizeof nm, "r%09lld", (long long)R.readno[i]);
+    if (R.suffix[i]) nm[n++] = (char)R.suffix[i];
+    return std::string(nm, (size_t)n);
+}
+
 extern "C" int ngs_synth_write_sam(const ngs_synth* s, const char* path) {
     FILE* f = std::fopen(path, "w");
     if (!f) return -1;
     std::string h = header_text(s);
     std::fwrite(h.data(), 1, h.size(), f);
-    for (const Read& rd : s->reads) {
-        std::fprintf(f, "%s\t%d\t%s\t%d\t%d\t%s\t*\t0\t0\t%s\t%s\tRG:Z:S%03d\n", rd.name.c_str(), rd.flags,
-                     s->names[rd.contig].c_str(), rd.pos, rd.mapq, rd.cigar_s.c_str(), rd.seq.c_str(),
-                     rd.qual.empty() ? "*" : rd.qual.c_str(), s->p.sample_idx + rd.sample);
+    const Records& R = s->rec;
+    std::string line;
+    for (size_t i = 0; i < R.size(); i++) {
+        std::string cig;
+        for (int32_t k = 0; k < R.cig_n[i]; k++) {
+            const int32_t v = R.cigar[(size_t)(R.cig_off[i] + k)];
+            cig += std::to_string(v / 8);
+            cig.push_back(kOps[v & 7]);
+        }
+        line = read_name(R, i);
+        char mid[160];
+        std::snprintf(mid, sizeof mid, "\t%d\t%s\t%d\t%d\t", R.flags[i], s->names[(size_t)R.contig[i]].c_str(), R.pos[i], R.mapq[i]);
+        line += mid;
+        line += cig;
+        line += "\t*\t0\t0\t";
+        line.append(R.bases, (size_t)R.seq_off[i], (size_t)R.seq_len[i]);
+        line.push_back('\t');
+        if (R.hasq[i]) line.append(R.quals, (size_t)R.seq_off[i], (size_t)R.seq_len[i]);
+        else line.push_back('*');
+        char rg[32];
+        std::snprintf(rg, sizeof rg, "\tRG:Z:S%03d\n", s->p.sample_idx + R.sample[i]);
+        line += rg;
+        std::fwrite(line.data(), 1, line.size(), f);
     }
     std::fclose(f);
     return 0;
 }
 
-// ---- BGZF / BAM writer (SAM spec section 4) ----
+// ---- BGZF / BAM writer (SAM spec section 4) and BAI index (section 5) ----
 namespace {
+constexpr size_t kBlockData = 65280;     // uncompressed bytes per BGZF block
+
+// Deflates 64 KB blocks of a stream on all cores, in order.  Records' uncompressed offsets map to
+// virtual offsets (compressed block offset << 16 | offset in block) once their block is written.
 struct Bgzf {
     FILE* f;
-    std::string buf;
+    std::string buf;                      // uncompressed bytes not yet written
+    uint64_t written_u = 0;               // uncompressed bytes already handed to blocks
+    uint64_t coff = 0;                    // compressed bytes written
+    std::vector<uint64_t> block_coff;     // compressed offset of every block written
     explicit Bgzf(FILE* ff) : f(ff) {}
-    void block(const char* data, size_t n) {
-        std::vector<unsigned char> out(n + 1024);
-        z_stream z{};
-        deflateInit2(&z, 6, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY);
-        z.next_in = (Bytef*)data; z.avail_in = (uInt)n;
-        z.next_out = out.data() + 18; z.avail_out = (uInt)(out.size() - 26);
-        deflate(&z, Z_FINISH);
-        size_t clen = z.total_out;
-        deflateEnd(&z);
+    uint64_t upos() const { return written_u + buf.size(); }
+    // raw deflate of one block at level 6 (htslib's default): libdeflate when the image has it (dlopen,
+    // ~3x zlib's speed), zlib otherwise
+    struct Libdeflate {
+        void* (*alloc)(int) = nullptr;
+        size_t (*compress)(void*, const void*, size_t, void*, size_t) = nullptr;
+        void (*release)(void*) = nullptr;
+        Libdeflate() {
+            void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+            if (!h) return;
+            alloc = (void* (*)(int))dlsym(h, "libdeflate_alloc_compressor");
+            compress = (size_t (*)(void*, const void*, size_t, void*, size_t))dlsym(h, "libdeflate_deflate_compress");
+            release = (void (*)(void*))dlsym(h, "libdeflate_free_compressor");
+            if (!alloc || !compress || !release) alloc = nullptr;
+        }
+    };
+    static const Libdeflate& libdeflate() { static Libdeflate l; return l; }
+    static void deflate_block(const char* data, size_t n, std::vector<unsigned char>& out) {
+        out.assign(n + 1024, 0);
+        size_t clen = 0;
+        const Libdeflate& ld = libdeflate();
+        if (ld.alloc && !std::getenv("NGS_SYNTH_ZLIB")) {
+            thread_local struct Cmp { void* c = nullptr; ~Cmp() { if (c) libdeflate().release(c); } } cmp;
+            if (!cmp.c) cmp.c = ld.alloc(6);
+            clen = ld.compress(cmp.c, data, n, out.data() + 18, out.size() - 26);
+        }
+        if (clen == 0) {
+            z_stream z{};
+            deflateInit2(&z, 6, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY);
+            z.next_in = (Bytef*)data; z.avail_in = (uInt)n;
+            z.next_out = out.data() + 18; z.avail_out = (uInt)(out.size() - 26);
+            deflate(&z, Z_FINISH);
+            clen = z.total_out;
+            deflateEnd(&z);
+        }
         unsigned char* h = out.data();
         const unsigned char hdr[18] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 'B', 'C', 2, 0, 0, 0};
         std::memcpy(h, hdr, 18);
@@ -451,16 +579,50 @@ struct Bgzf {
         unsigned char* t = out.data() + 18 + clen;
         for (int i = 0; i < 4; i++) t[i] = (crc >> (8 * i)) & 0xff;
         for (int i = 0; i < 4; i++) t[4 + i] = ((uint32_t)n >> (8 * i)) & 0xff;
-        std::fwrite(out.data(), 1, 18 + clen + 8, f);
+        out.resize(18 + clen + 8);
+    }
+    // compresses and writes every complete block (all blocks when final)
+    void flush(bool final) {
+        size_t nb = buf.size() / kBlockData;
+        if (final && buf.size() % kBlockData) nb++;
+        if (nb == 0) return;
+        std::vector<std::vector<unsigned char>> out(nb);
+        std::atomic<size_t> next{0};
+        const unsigned nt = std::max(1u, std::min<unsigned>(std::thread::hardware_concurrency(), 16u));
+        auto work = [&]() {
+            for (size_t b; (b = next.fetch_add(1)) < nb;) {
+                const size_t o = b * kBlockData;
+                deflate_block(buf.data() + o, std::min(kBlockData, buf.size() - o), out[b]);
+            }
+        };
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < nt && t < nb; t++) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+        size_t used = 0;
+        for (size_t b = 0; b < nb; b++) {
+            block_coff.push_back(coff);
+            std::fwrite(out[b].data(), 1, out[b].size(), f);
+            coff += out[b].size();
+            used += std::min(kBlockData, buf.size() - b * kBlockData);
+        }
+        written_u += used;
+        buf.erase(0, used);
     }
     void write(const void* d, size_t n) {
         buf.append((const char*)d, n);
-        while (buf.size() >= 65280) { block(buf.data(), 65280); buf.erase(0, 65280); }
+        if (buf.size() >= 256 * kBlockData) flush(false);
     }
     void close() {
-        if (!buf.empty()) block(buf.data(), buf.size());
+        flush(true);
+        block_coff.push_back(coff);       // the EOF block: end offset of the last record
         static const unsigned char eof[28] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0, 27, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         std::fwrite(eof, 1, 28, f);
+    }
+    // virtual offset of uncompressed position u (u <= total)
+    uint64_t voff(uint64_t u) const {
+        const size_t b = (size_t)(u / kBlockData);
+        return (block_coff[b] << 16) | (u % kBlockData);
     }
 };
 int reg2bin(int beg, int end) {
@@ -473,6 +635,52 @@ int reg2bin(int beg, int end) {
     return 0;
 }
 template <class T> void put(std::string& b, T v) { b.append((const char*)&v, sizeof(T)); }
+
+// one indexed record: reference, [beg, end) 0-based, bin and its uncompressed [start, stop) in the stream
+struct IdxRec { int32_t ref, beg, end, bin; uint64_t u0, u1; };
+
+// BAI (SAM spec 5.2): per reference the bins' chunks (merged when contiguous in the file) and the
+// 16 kb linear index (smallest virtual offset of a record overlapping each window)
+void write_bai(const std::string& path, const Bgzf& z, const std::vector<IdxRec>& recs, int32_t n_ref) {
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) return;
+    std::string out = "BAI\1";
+    put<int32_t>(out, n_ref);
+    size_t i = 0;
+    for (int32_t ref = 0; ref < n_ref; ref++) {
+        size_t j = i;
+        while (j < recs.size() && recs[j].ref == ref) j++;
+        std::vector<std::pair<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>>> bins;
+        std::vector<int> bin_slot(37450, -1);
+        std::vector<uint64_t> lin;
+        for (size_t k = i; k < j; k++) {
+            const IdxRec& r = recs[k];
+            const uint64_t v0 = z.voff(r.u0), v1 = z.voff(r.u1);
+            int& sl = bin_slot[(size_t)r.bin];
+            if (sl < 0) { sl = (int)bins.size(); bins.push_back({(uint32_t)r.bin, {}}); }
+            auto& ch = bins[(size_t)sl].second;
+            if (!ch.empty() && ch.back().second == v0) ch.back().second = v1;
+            else ch.push_back({v0, v1});
+            const int w0 = r.beg >> 14, w1 = (r.end - 1) >> 14;
+            if ((int)lin.size() <= w1) lin.resize((size_t)w1 + 1, 0);
+            for (int w = w0; w <= w1; w++)
+                if (lin[(size_t)w] == 0 || v0 < lin[(size_t)w]) lin[(size_t)w] = v0;
+        }
+        for (size_t w = 1; w < lin.size(); w++)          // empty windows: the previous window's offset
+            if (lin[w] == 0) lin[w] = lin[w - 1];
+        put<int32_t>(out, (int32_t)bins.size());
+        for (auto& b : bins) {
+            put<uint32_t>(out, b.first);
+            put<int32_t>(out, (int32_t)b.second.size());
+            for (auto& c : b.second) { put<uint64_t>(out, c.first); put<uint64_t>(out, c.second); }
+        }
+        put<int32_t>(out, (int32_t)lin.size());
+        for (uint64_t v : lin) put<uint64_t>(out, v);
+        i = j;
+    }
+    std::fwrite(out.data(), 1, out.size(), f);
+    std::fclose(f);
+}
 }  // namespace
 
 static int write_bam_impl(const ngs_synth* s, const char* path, int only_sample);
@@ -510,41 +718,96 @@ static int write_bam_impl(const ngs_synth* s, const char* path, int only_sample)
     z.write(b.data(), b.size());
     static const int bam_op[8] = {5, 2, 1, 0, 6, 3, 4, 8};  // NGSEP op -> BAM op (H D I M P N S X)
     const char* nt16 = "=ACMGRSVTWYHKDBN";
-    for (const Read& rd : s->reads) {
-        if (only_sample >= 0 && rd.sample != only_sample) continue;
-        char rg[16];
-        std::snprintf(rg, sizeof rg, "S%03d", s->p.sample_idx + rd.sample);
-        std::string r;
-        int l_seq = (int)rd.seq.size();
-        int reflen = 0;
-        for (int32_t v : rd.cigar) if ((v & 7) & 1) reflen += v / 8;
-        put<int32_t>(r, rd.contig);
-        put<int32_t>(r, rd.pos - 1);
-        put<uint8_t>(r, (uint8_t)(rd.name.size() + 1));
-        put<uint8_t>(r, (uint8_t)rd.mapq);
-        put<uint16_t>(r, (uint16_t)reg2bin(rd.pos - 1, rd.pos - 1 + reflen));
-        put<uint16_t>(r, (uint16_t)rd.cigar.size());
-        put<uint16_t>(r, (uint16_t)rd.flags);
-        put<int32_t>(r, l_seq);
-        put<int32_t>(r, -1);
-        put<int32_t>(r, -1);
-        put<int32_t>(r, 0);
-        r += rd.name; r.push_back(0);
-        for (int32_t v : rd.cigar) put<uint32_t>(r, (uint32_t)((v / 8) << 4 | bam_op[v & 7]));
-        for (int i = 0; i < l_seq; i += 2) {
-            int hi = (int)(std::strchr(nt16, rd.seq[i]) - nt16);
-            int lo = i + 1 < l_seq ? (int)(std::strchr(nt16, rd.seq[i + 1]) - nt16) : 0;
-            put<uint8_t>(r, (uint8_t)(hi << 4 | lo));
+    int8_t code[256];
+    std::memset(code, 15, sizeof code);
+    for (int k = 0; k < 16; k++) code[(unsigned char)nt16[k]] = (int8_t)k;
+    const Records& R = s->rec;
+    std::vector<size_t> sel;                 // records written, in order
+    sel.reserve(R.size());
+    for (size_t i = 0; i < R.size(); i++)
+        if (only_sample < 0 || R.sample[i] == only_sample) sel.push_back(i);
+    auto name_len = [&](size_t i) -> size_t {
+        size_t n = 10;                       // "r%09lld"
+        for (long long v = R.readno[i]; v >= 1000000000LL; v /= 10) n++;
+        return n + (R.suffix[i] ? 1 : 0);
+    };
+    // records are serialized in chunks, each chunk's records on all cores into one buffer
+    std::vector<IdxRec> idx(sel.size());
+    std::vector<uint64_t> roff;
+    std::string chunk;
+    const unsigned nt = std::max(1u, std::min<unsigned>(std::thread::hardware_concurrency(), 16u));
+    constexpr size_t kRecChunk = 1 << 18;
+    for (size_t c0 = 0; c0 < sel.size(); c0 += kRecChunk) {
+        const size_t c1 = std::min(sel.size(), c0 + kRecChunk);
+        roff.assign(c1 - c0 + 1, 0);
+        for (size_t k = c0; k < c1; k++) {
+            const size_t i = sel[k];
+            roff[k - c0 + 1] = roff[k - c0] + 4 + 32 + name_len(i) + 1 + 4 * (size_t)R.cig_n[i] +
+                               (size_t)(R.seq_len[i] + 1) / 2 + (size_t)R.seq_len[i] + 3 + 4 + 1;
         }
-        for (int i = 0; i < l_seq; i++) put<uint8_t>(r, rd.qual.empty() ? 0xff : (uint8_t)(rd.qual[i] - 33));
-        r += "RGZ"; r += rg; r.push_back(0);
-        std::string rec;
-        put<int32_t>(rec, (int32_t)r.size());
-        rec += r;
-        z.write(rec.data(), rec.size());
+        chunk.resize(roff.back());
+        const uint64_t u_base = z.upos();
+        std::atomic<size_t> next{c0};
+        auto work = [&]() {
+            for (size_t k0; (k0 = next.fetch_add(4096)) < c1;) {
+                for (size_t k = k0; k < std::min(c1, k0 + 4096); k++) {
+                    const size_t i = sel[k];
+                    char* o = &chunk[roff[k - c0]];
+                    const int l_seq = R.seq_len[i];
+                    const int32_t* cig = &R.cigar[(size_t)R.cig_off[i]];
+                    int reflen = 0;
+                    for (int32_t j = 0; j < R.cig_n[i]; j++) if ((cig[j] & 7) & 1) reflen += cig[j] / 8;
+                    const int bin = reg2bin(R.pos[i] - 1, R.pos[i] - 1 + reflen);
+                    const size_t nl = name_len(i);
+                    auto w32 = [&](int32_t v) { std::memcpy(o, &v, 4); o += 4; };
+                    auto w16 = [&](uint16_t v) { std::memcpy(o, &v, 2); o += 2; };
+                    w32((int32_t)(roff[k - c0 + 1] - roff[k - c0] - 4));
+                    w32(R.contig[i]);
+                    w32(R.pos[i] - 1);
+                    *o++ = (char)(uint8_t)(nl + 1);
+                    *o++ = (char)(uint8_t)R.mapq[i];
+                    w16((uint16_t)bin);
+                    w16((uint16_t)R.cig_n[i]);
+                    w16((uint16_t)R.flags[i]);
+                    w32(l_seq);
+                    w32(-1);
+                    w32(-1);
+                    w32(0);
+                    char nm[40];
+                    std::snprintf(nm, sizeof nm, "r%09lld", (long long)R.readno[i]);
+                    std::memcpy(o, nm, nl - (R.suffix[i] ? 1 : 0));
+                    o += nl - (R.suffix[i] ? 1 : 0);
+                    if (R.suffix[i]) *o++ = (char)R.suffix[i];
+                    *o++ = 0;
+                    for (int32_t j = 0; j < R.cig_n[i]; j++) w32((int32_t)((uint32_t)(cig[j] / 8) << 4 | (uint32_t)bam_op[cig[j] & 7]));
+                    const char* sq = R.bases.data() + R.seq_off[i];
+                    const char* ql = R.quals.data() + R.seq_off[i];
+                    for (int j = 0; j < l_seq; j += 2) {
+                        const int hi = code[(unsigned char)sq[j]];
+                        const int lo = j + 1 < l_seq ? code[(unsigned char)sq[j + 1]] : 0;
+                        *o++ = (char)(uint8_t)(hi << 4 | lo);
+                    }
+                    if (R.hasq[i]) for (int j = 0; j < l_seq; j++) *o++ = (char)(uint8_t)(ql[j] - 33);
+                    else { std::memset(o, 0xff, (size_t)l_seq); o += l_seq; }
+                    char rg[16];
+                    std::snprintf(rg, sizeof rg, "RGZS%03d", s->p.sample_idx + R.sample[i]);
+                    std::memcpy(o, rg, 7);
+                    o += 7;
+                    *o++ = 0;
+                    idx[k] = {R.contig[i], R.pos[i] - 1, R.pos[i] - 1 + std::max(reflen, 1), bin, u_base + roff[k - c0],
+                              u_base + roff[k - c0 + 1]};
+                }
+            }
+        };
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < nt; t++) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+        z.write(chunk.data(), chunk.size());
     }
     z.close();
     std::fclose(f);
+    write_bai(std::string(path) + ".bai", z, idx, (int32_t)s->seqs.size());
     return 0;
 }
 
@@ -557,7 +820,6 @@ extern "C" int ngs_synth_write_truth(const ngs_synth* s, const char* path) {
     std::fclose(f);
     return 0;
 }
-
 // ---- SAM text -> BAM (for hand-written fixtures under tests/golden) ----
 // Keeps the header text verbatim, all records in file order, and the aux tags of types
 // A/i/f/Z (integers written as 'i').  Test infrastructure only.

@@ -36,6 +36,9 @@ typedef struct ngs_synth_params {
     double  softclip_rate;   /* fraction of reads with a 5-20 bp soft clip at one end */
     int32_t n_samples;       /* >1: a population of diploid samples S%03d (sample_idx..), depth per sample,
                                 population SNVs at snv_rate with AF U(0.02,0.98) in HWE (multisample config C5) */
+    int64_t trunc_len;       /* >0: every contig truncated to this length (bounded CPU-baseline samples) */
+    int32_t rng_per_contig;  /* 1: each contig's donor/reads from its own seeded stream, so a contig generated
+                                alone (one rank's shard, contig_first=k, n_contigs=1) equals it in the whole genome */
 } ngs_synth_params;
 
 typedef struct ngs_synth ngs_synth;
@@ -54,7 +57,7 @@ int64_t ngs_synth_n_bases(const ngs_synth* s);
 int ngs_synth_batch(ngs_synth* s, ngsep_read_batch* out);
 int ngs_synth_write_fasta(const ngs_synth* s, const char* path);
 int ngs_synth_write_sam(const ngs_synth* s, const char* path);
-int ngs_synth_write_bam(const ngs_synth* s, const char* path);
+int ngs_synth_write_bam(const ngs_synth* s, const char* path);   /* also writes path + ".bai" */
 int ngs_synth_write_bam_sample(const ngs_synth* s, const char* path, int sample);
 int ngs_synth_write_truth(const ngs_synth* s, const char* path);
 /* SAM text -> BAM (header verbatim, records in file order, aux tags A/i/f/Z) */
