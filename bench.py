@@ -1,26 +1,39 @@
 """bench.py -- genotyped reference positions/s of the MI355X SNV pileup path.
 
-Workload (BASELINE.json configs[1]): yeast whole genome (sacCer3 contig names/lengths,
-12,157,105 bp, synthetic bases) at 30x, 150 bp single-end synthetic reads, one sample.
-A step = one pass of the hot path over the whole genome with the pileup resident in HBM:
-k_tile_pileup (tile scan + hom-ref bounds) + k_posterior (exact tally, posterior and call of the
-undecided candidates) + ko_* (position order) + D2H of the called sites + host mapping to
-(sequence, position) (libngsep_amd.so, ngsep_submit_staged / ngsep_collect_staged, two passes in
-flight so one pass's copies overlap the next pass's kernels).  N>1: one process per GPU, each rank owns its own
-synthetic genome (seed 2+rank) -- windows shard with no data-path collective ("weak").
+Workload (BASELINE.json configs[2], the largest single-GPU configuration and the one the roofline is
+quoted on): human chr20 (64,444,167 bp, synthetic bases) at 30x, 150 bp single-end synthetic reads, one
+sample.  The host packer's layout (bit planes, position-major byte pile, per-tile read segments,
+reference codes -- DESIGN.md section 2) is resident in HBM before the timed region; a step = one pass of
+the hot path over it: KT (bit-plane scan + hom-ref bounds) + KP (exact tally, posterior and call of the
+survivors) + KO (position order, (sequence, position) mapping) + D2H of the called sites + the host
+collect (libngsep_amd.so ngsep_submit_staged / ngsep_collect_staged, two passes in flight).
 
---config multisample (BASELINE.json configs[4], MultisampleVariantsDetector): 200 samples at 10x
-(population SNVs in HWE), one rank = one contig shard of the 8-GPU split (default chrIV, the largest
-yeast contig, ~1/8 of the genome); a step = KTM (per-sample tile scan) + KPM (population
-genotyping) + D2H of the sites and every sample's call.
+Beside the resident rate the line carries:
+  * roofline   -- KT's bytes moved per launch (planes + reference + tile descriptors) / KT's average
+                  launch time from HIP events bound to its dispatch; `traffic` = HBM bytes per launch
+                  from the committed rocprofv3 PMC passes (profiles/pmc_traffic*.json);
+                  `alg_equiv_GBs` = SURVEY.md 8(d)'s algorithmic bytes / KT time (not a roofline);
+  * end_to_end -- BAM on disk -> VCF on disk through ngsep_call_bam (path B: BGZF decode, admission,
+                  projection, layout, H2D, kernels, VCF), wall time and positions/s;
+  * cpu_baseline -- the oracle (C restatement of the reference, SAM -> VCF) on a bounded sample of the
+                  same workload, single-thread and one process per core.
 
-Prints one JSON line (rank 0).  --gpus N under torch.distributed.run for N>1.
+--gpus N: one process per GPU (spawned here under torch.distributed.run when WORLD_SIZE is unset); each
+rank owns its own synthetic chr20-sized genome (seed 3 + rank) -- windows shard with no data-path
+collective ("weak").  --config wgs: configs[3], the GRCh38 sequences split over the ranks by
+sharding.assign_contigs, each rank generating and calling only its own sequences.
+--config yeast: configs[1].  --config multisample: configs[4] (one GPU's contig shard of the 200-sample
+population).  --config coverage: CoverageStats on yeast 30x.
+
+Prints one JSON line (rank 0).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import shutil
+import socket
 import subprocess
 import sys
 import tempfile
@@ -33,31 +46,68 @@ for p in (ROOT, os.path.join(ROOT, "tools", "synth"), os.path.join(ROOT, "oracle
 
 METRIC = "genotyped ref positions/sec on 30x synthetic BAM; 1/2/4/8 GPU scaling"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+HUMAN_CHR20 = 19               # index of chr20 in the synthetic GRCh38 table
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(depth: float, seed: int, n_contigs: int):
-    """The oracle (single-thread C restatement of the reference) on a bounded sample of the same
-    workload: the first n_contigs yeast contigs at the same depth, SAM text -> VCF."""
-    import ngsep_oracle
+def cpu_cores() -> int:
+    """The CPU share this job may use: OMP_NUM_THREADS on the GPU box (16), else the affinity mask."""
+    v = os.environ.get("OMP_NUM_THREADS")
+    if v and v.isdigit() and int(v) > 0:
+        return int(v)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+# ------------------------------------------------------------------------------------------------
+# CPU baseline: the oracle on a bounded sample of the same workload (before any GPU call)
+# ------------------------------------------------------------------------------------------------
+def _write_piece(d, k, genome, contig_first, trunc, depth, seed):
     import pysynth
-    syn = pysynth.Synth(genome=pysynth.YEAST, depth=depth, seed=seed, n_contigs=n_contigs)
-    names = [n for n, _ in syn.contigs()]
-    with tempfile.TemporaryDirectory() as d:
-        fa, sam, _ = syn.write(os.path.join(d, "cpu"))
-        st = ngsep_oracle.run_ssvd(fa, sam, os.path.join(d, "cpu.vcf"))
+    syn = pysynth.Synth(genome=genome, contig_first=contig_first, n_contigs=1, trunc_len=trunc, depth=depth,
+                        seed=seed, rng_per_contig=1)
+    fa, sam, _ = syn.write(os.path.join(d, f"piece{k}"))
     syn.close()
-    return {
-        "value": st.positions_genotyped / st.seconds,
-        "unit": "positions/s",
-        "cores": 1,
-        "kind": "port",
-        "sample": f"oracle (C restatement, SAM->VCF incl. parsing) on yeast {names[0]}..{names[-1]} "
-                  f"({st.positions_genotyped} positions) at {depth:g}x, {st.seconds:.2f} s",
-    }
+    return fa, sam
+
+
+def cpu_baseline(genome: int, contig_first: int, depth: float, trunc: int, seed: int):
+    """Single thread: the oracle (SAM text -> VCF, like the Java path incl. reading its input) on the first
+    `trunc` bp of the workload's sequence.  All cores: one oracle process per core, each on its own
+    `trunc`-bp piece (independent synthetic sequences), wall time over the pool."""
+    import ngsep_oracle
+    cli = os.path.join(ROOT, "oracle", "build", "ngsep_oracle")
+    cores = cpu_cores()
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        fa, sam = _write_piece(d, 0, genome, contig_first, trunc, depth, seed)
+        st = ngsep_oracle.run_ssvd(fa, sam, os.path.join(d, "one.vcf"))
+        one = {"value": st.positions_genotyped / st.seconds, "cores": 1,
+               "sample": f"{st.positions_genotyped} positions ({trunc / 1e6:g} Mb of the workload's sequence) at "
+                         f"{depth:g}x, {st.seconds:.2f} s"}
+        pieces = [(fa, sam)] + [_write_piece(d, k, genome, contig_first, trunc, depth, seed + 1000 * k)
+                                for k in range(1, cores)]
+        t0 = time.perf_counter()
+        procs = [subprocess.Popen([cli, "-r", f, "-i", s, "-o", os.path.join(d, f"all{k}")],
+                                  stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+                 for k, (f, s) in enumerate(pieces)]
+        positions = 0
+        for p in procs:
+            _, err = p.communicate()
+            if p.returncode != 0:
+                raise RuntimeError(f"oracle failed: {err}")
+            positions += int(err.split("positions=")[1].split()[0])
+        wall = time.perf_counter() - t0
+    out = {"value": positions / wall, "unit": "positions/s", "cores": cores, "kind": "port",
+           "sample": f"oracle (C restatement of the reference, SAM -> VCF incl. parsing), {cores} processes x "
+                     f"{trunc / 1e6:g} Mb synthetic pieces at {depth:g}x ({positions} positions) in {wall:.2f} s wall",
+           "single_thread": one}
+    return out
 
 
 def cpu_baseline_mvd(samples: int, depth: float, length: int = 20000):
@@ -80,10 +130,12 @@ def cpu_baseline_mvd(samples: int, depth: float, length: int = 20000):
     }
 
 
+# ------------------------------------------------------------------------------------------------
+# measurement helpers
+# ------------------------------------------------------------------------------------------------
 def cold_passes(sess, n: int = 5):
     """Passes with the Infinity Cache (256 MiB) flushed first: a 1 GiB device fill before each (HIP
-    runtime through ctypes), so the scan reads its layout from HBM (steady-state passes re-read a
-    bit-plane pile that fits on-die)."""
+    runtime through ctypes), so the scan reads its layout from HBM."""
     import ctypes
     hip = ctypes.CDLL("libamdhip64.so")
     size = ctypes.c_size_t(1 << 30)
@@ -119,9 +171,29 @@ def load_traffic(workload_key: str):
     return None
 
 
+def end_to_end(fa: str, bam: str, device: int):
+    """BAM on disk -> VCF on disk: SingleSampleVariantsDetector.findSNVS through ngsep_call_bam in a fresh
+    context (decode, admission, projection, layout, H2D, kernels, VCF writing), wall time."""
+    from ngsepcore_amd import GpuPileupSession
+    out = os.path.join(os.path.dirname(bam), "e2e.vcf")
+    with GpuPileupSession(device=device) as s:
+        t0 = time.perf_counter()
+        s.load_fasta(fa)
+        t1 = time.perf_counter()
+        s.processFile(bam, out)
+        t2 = time.perf_counter()
+        st = s.stats()
+    n_rec = sum(1 for l in open(out) if not l.startswith("#"))
+    return {"wall_s": t2 - t0, "fasta_s": t1 - t0, "call_bam_s": t2 - t1,
+            "positions": int(st.positions_genotyped), "value": st.positions_genotyped / (t2 - t0),
+            "unit": "positions/s", "vcf_records": n_rec, "bam_bytes": os.path.getsize(bam),
+            "note": "ngsep_call_bam: BAM on disk -> VCF on disk incl. FASTA load; host threads "
+                    f"{os.environ.get('NGSEP_THREADS') or cpu_cores()}"}
+
+
 def bench_coverage(args):
-    """--config coverage: CoverageStats (CoverageStatisticsCalculator) on the same
-    yeast 30x reads, resident in HBM; a step = one kc_tile_hist pass + D2H of the histograms (1 GPU)."""
+    """--config coverage: CoverageStats (CoverageStatisticsCalculator) on yeast 30x
+    reads, resident in HBM; a step = one kc_tile_hist pass + D2H of the histograms (1 GPU)."""
     import pysynth
     from ngsepcore_amd import GpuPileupSession, default_params
     syn = pysynth.Synth(genome=pysynth.YEAST, depth=args.depth, seed=2)
@@ -145,7 +217,7 @@ def bench_coverage(args):
     sess.release_staged()
     sess.close()
     k_ms = sum(ks) / len(ks)
-    # algorithmic bytes per launch: 12 B per admitted read (global first + span|unique) + the histograms
+    # bytes per launch: 12 B per admitted read (global first + span|unique) + the histograms
     alg = 12 * st.alignments_admitted + 16 * (p.max_coverage + 1)
     ach = alg / (k_ms * 1e-3) / 1e9
     print(json.dumps({
@@ -156,22 +228,35 @@ def bench_coverage(args):
         "config": {"workload": "CoverageStats on yeast whole genome 30x synthetic 150 bp SE", "positions_per_gpu": st.positions_genotyped,
                    "reads_per_gpu": int(st.alignments_admitted), "max_coverage": p.max_coverage},
         "roofline": {"bound": "hbm", "kernel": "kc_tile_hist", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": ach / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": alg, "kernel_avg_ms": k_ms,
+                     "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel_avg_ms": k_ms,
                      "note": "LDS-bound (difference array + workgroup scan over 4096 positions per tile), not HBM-bound"},
     }), flush=True)
 
 
+def spawn_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: run this script under torch.distributed.run as a child (nothing
+    here has touched the GPU) and return its exit code."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
+# ------------------------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--depth", type=float, default=30.0)
+    ap.add_argument("--config", default="chr20", choices=["chr20", "yeast", "wgs", "multisample", "coverage"])
     ap.add_argument("--no-cold", action="store_true", help="skip the cache-flushed passes")
-    ap.add_argument("--genome", default="yeast", choices=["yeast", "human_chr20"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-contigs", type=int, default=4)
-    ap.add_argument("--config", default="single", choices=["single", "multisample", "coverage"])
+    ap.add_argument("--no-e2e", action="store_true", help="skip the BAM -> VCF end-to-end run")
+    ap.add_argument("--cpu-trunc", type=int, default=2_000_000, help="bp per CPU-baseline piece")
     ap.add_argument("--samples", type=int, default=200)
     ap.add_argument("--contig-first", type=int, default=3, help="multisample: first yeast contig of the shard")
     ap.add_argument("--n-contigs", type=int, default=1, help="multisample: contigs in the shard")
@@ -179,11 +264,33 @@ def main():
     if args.config == "multisample" and args.depth == 30.0:
         args.depth = 10.0
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
+    if world != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one process per GPU")
+        sys.exit(2)
     if args.config == "coverage":
         return bench_coverage(args)
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    multi = args.config == "multisample"
+
+    # the CPU baseline runs first, before this process touches the GPU (its oracle pool is child processes)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            t = time.time()
+            if multi:
+                cpu = cpu_baseline_mvd(args.samples, args.depth)
+            elif args.config == "yeast":
+                cpu = cpu_baseline(0, 3, args.depth, args.cpu_trunc, 2)
+            else:
+                cpu = cpu_baseline(1, HUMAN_CHR20, args.depth, args.cpu_trunc, 3)
+            log(f"[rank 0] cpu baseline in {time.time() - t:.1f}s: {cpu['value']:.4g} positions/s on {cpu['cores']} cores")
+        except Exception as e:  # the baseline is reported, never required
+            cpu = {"value": None, "error": str(e)}
+
     dist = None
     if world > 1:
         import torch
@@ -194,43 +301,104 @@ def main():
 
     import pysynth
     from ngsepcore_amd import GpuPileupSession, default_params
+    from ngsepcore_amd.sharding import assign_contigs
 
-    seed = 2 + rank
     t0 = time.time()
-    multi = args.config == "multisample"
+    params = default_params()
     if multi:
-        seed = 5
-        syn = pysynth.Synth(genome=pysynth.YEAST, depth=args.depth, seed=seed, n_samples=args.samples,
+        params.multisample = 1
+    sessions = []          # (session, synthetic sequences) -- wgs: several device runs of < 2^31 positions
+    e2e_src = None
+    if multi:
+        syn = pysynth.Synth(genome=pysynth.YEAST, depth=args.depth, seed=5, n_samples=args.samples,
                             contig_first=args.contig_first + rank, n_contigs=args.n_contigs)
         names = [n for n, _ in syn.contigs()]
         workload = (f"MultisampleVariantsDetector: {args.samples} synthetic yeast samples at {args.depth:g}x, "
                     f"shard {'+'.join(names)} (one GPU's contig shard of the 8-GPU split)")
-    elif args.genome == "yeast":
-        syn = pysynth.Synth(genome=pysynth.YEAST, depth=args.depth, seed=seed)
-        workload = "yeast whole genome (sacCer3 names/lengths, 12,157,105 bp) 30x synthetic 150 bp SE"
+        workload_key = f"multisample{args.samples}:{args.depth:g}x:contig{args.contig_first}"
+        sources = [syn]
+    elif args.config == "yeast":
+        sources = [pysynth.Synth(genome=pysynth.YEAST, depth=args.depth, seed=2 + rank)]
+        workload = "configs[1]: yeast whole genome (sacCer3 names/lengths, 12,157,105 bp) 30x synthetic 150 bp SE"
+        workload_key = f"yeast:{args.depth:g}x:seed{2 + rank}"
+    elif args.config == "chr20":
+        sources = [pysynth.Synth(genome=pysynth.HUMAN, depth=args.depth, seed=3 + rank, contig_first=HUMAN_CHR20,
+                                 n_contigs=1, rng_per_contig=1)]
+        workload = "configs[2]: human chr20 (64,444,167 bp) 30x synthetic 150 bp SE"
+        workload_key = f"human_chr20:{args.depth:g}x:seed{3 + rank}:v2"
     else:
-        syn = pysynth.Synth(genome=pysynth.HUMAN, depth=args.depth, seed=3 + rank, contig_first=19, n_contigs=1)
-        workload = "human chr20 (64,444,167 bp) 30x synthetic 150 bp SE"
-    t_gen = time.time() - t0
-    params = default_params()
-    if multi:
-        params.multisample = 1
-    sess = GpuPileupSession(params, device=local_rank)
-    if multi:
-        n = max(1, syn.params.n_samples)
-        sess.set_samples([(f"S{k:03d}", f"S{k:03d}") for k in range(n)])
-    for name, seq in syn.contigs():
-        sess.set_reference(name, seq)
-    t1 = time.time()
-    sess.stage(syn.batch())
-    sess.stage_finish()
-    t_stage = time.time() - t1
-    n_reads_in = syn.n_reads
-    syn.close()
-    st = sess.stats()
-    positions = st.positions_genotyped
-    log(f"[rank {rank}] generated in {t_gen:.1f}s, staged {st.alignments_admitted} reads "
-        f"({st.read_bases} read bases, {st.slot_bytes} slot bytes) over {positions} positions in {t_stage:.1f}s")
+        # configs[3]: GRCh38 lengths, sequences assigned largest-first to the least-loaded rank; each rank
+        # generates and calls only its own (the synthetic sequences are independent: rng_per_contig)
+        import ctypes
+        lib = pysynth.lib()
+        p = pysynth.SynthParams()
+        lib.ngs_synth_default(ctypes.byref(p))
+        human = [("chr1", 248956422), ("chr2", 242193529), ("chr3", 198295559), ("chr4", 190214555), ("chr5", 181538259),
+                 ("chr6", 170805979), ("chr7", 159345973), ("chr8", 145138636), ("chr9", 138394717), ("chr10", 133797422),
+                 ("chr11", 135086622), ("chr12", 133275309), ("chr13", 114364328), ("chr14", 107043718), ("chr15", 101991189),
+                 ("chr16", 90338345), ("chr17", 83257441), ("chr18", 80373285), ("chr19", 58617616), ("chr20", 64444167),
+                 ("chr21", 46709983), ("chr22", 50818468), ("chrX", 156040895), ("chrY", 57227415)]
+        mine = assign_contigs(human, world)[rank]
+        idx = [k for k, (n, _) in enumerate(human) if n in mine]
+        sources = [("lazy", k) for k in idx]
+        workload = (f"configs[3]: human WGS (GRCh38 lengths, 3.10e9 bp) 30x synthetic 150 bp SE, contig-sharded: "
+                    f"rank {rank} of {world} calls {'+'.join(mine)}")
+        workload_key = f"wgs:{args.depth:g}x:rank{rank}of{world}"
+
+    # stage: one session per device run (< 2^31 positions each)
+    positions = 0
+    t_gen = t_stage = 0.0
+    reads = read_bases = sites_called = 0
+    group, group_len = [], 0
+    groups = []
+    if sources and isinstance(sources[0], tuple):
+        lens = {k: human[k][1] for _, k in sources}
+        for _, k in sources:
+            if group and group_len + lens[k] > 1_800_000_000:
+                groups.append(group)
+                group, group_len = [], 0
+            group.append(k)
+            group_len += lens[k]
+        groups.append(group)
+    else:
+        groups = [[None]]
+    for gi, grp in enumerate(groups):
+        sess = GpuPileupSession(params, device=local_rank)
+        if multi:
+            n = max(1, sources[0].params.n_samples)
+            sess.set_samples([(f"S{k:03d}", f"S{k:03d}") for k in range(n)])
+        for item in grp:
+            tg = time.time()
+            syn = sources[0] if item is None else pysynth.Synth(genome=pysynth.HUMAN, depth=args.depth, seed=4,
+                                                               contig_first=item, n_contigs=1, rng_per_contig=1)
+            t_gen += time.time() - tg
+            for name, seq in syn.contigs():
+                sess.set_reference(name, seq)
+            ts = time.time()
+            sess.stage(syn.batch())
+            t_stage += time.time() - ts
+            if args.config == "chr20" and rank == 0 and world == 1 and not args.no_e2e:
+                # the same reads as a BAM on local disk for the end-to-end run
+                tmp = tempfile.mkdtemp(prefix="ngsep_e2e_")
+                tw = time.time()
+                fa = os.path.join(tmp, "chr20.fa")
+                bam = os.path.join(tmp, "chr20.bam")
+                pysynth.lib().ngs_synth_write_fasta(syn.h, fa.encode())
+                pysynth.lib().ngs_synth_write_bam(syn.h, bam.encode())
+                e2e_src = (tmp, fa, bam)
+                log(f"[rank 0] wrote the end-to-end BAM ({os.path.getsize(bam) / 1e9:.2f} GB) in {time.time() - tw:.1f}s")
+            if item is not None or len(grp) == 1:
+                syn.close()
+        ts = time.time()
+        sess.stage_finish()
+        t_stage += time.time() - ts
+        st = sess.stats()
+        positions += st.positions_genotyped
+        reads += st.alignments_admitted
+        read_bases += st.read_bases
+        sessions.append(sess)
+    log(f"[rank {rank}] generated in {t_gen:.1f}s, staged {reads} reads ({read_bases} read bases) over {positions} "
+        f"positions in {t_stage:.1f}s ({len(sessions)} device run(s))")
 
     def barrier():
         if dist is not None:
@@ -240,54 +408,64 @@ def main():
             torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        sess.run_staged()
+        for s in sessions:
+            s.run_staged()
     barrier()
-    scan_ms, geno_ms, dev_ms = [], [], []
+    scan_ms, geno_ms = [], []
     t_start = time.perf_counter()
-    # a stream of passes, two in flight: pass k+1's kernels run while pass k's records are copied
-    # back and mapped (ngsep_submit_staged / ngsep_collect_staged); every pass is collected
-    sess.submit_staged()
-    t_sub = t_col = 0.0
-    for k in range(args.steps):
-        t1 = time.perf_counter()
-        if k + 1 < args.steps:
-            sess.submit_staged()
-        t2 = time.perf_counter()
-        sess.collect_staged()
-        t3 = time.perf_counter()
-        t_sub += t2 - t1
-        t_col += t3 - t2
-        s = sess.stats()
-        scan_ms.append(s.scan_ms)
-        geno_ms.append(s.genotype_ms)
-        dev_ms.append(s.kernel_ms)
+    if len(sessions) == 1 and not multi:
+        # a stream of passes, two in flight: pass k+1's kernels run while pass k's records are copied back
+        # and collected (ngsep_submit_staged / ngsep_collect_staged); every pass is collected
+        sess = sessions[0]
+        sess.submit_staged()
+        for k in range(args.steps):
+            if k + 1 < args.steps:
+                sess.submit_staged()
+            sess.collect_staged()
+            s = sess.stats()
+            scan_ms.append(s.scan_ms)
+            geno_ms.append(s.genotype_ms)
+            sites_called = s.sites_called
+    else:
+        for k in range(args.steps):
+            sites_called = 0
+            for sess in sessions:
+                sess.run_staged()
+                s = sess.stats()
+                scan_ms.append(s.scan_ms)
+                geno_ms.append(s.genotype_ms)
+                sites_called += s.sites_called
     barrier()
     elapsed = time.perf_counter() - t_start
-    st = sess.stats()
-    if os.environ.get("NGSEP_PROBE_HOST"):     # diagnostics: host cost of a collect whose pass is done
-        tc = ts = tt = 0.0
-        for _ in range(20):
-            t1 = time.perf_counter()
-            sess.submit_staged()
-            t2 = time.perf_counter()
-            time.sleep(0.003)
-            t3 = time.perf_counter()
-            sess.collect_staged()
-            t4 = time.perf_counter()
-            sess.stats()
-            t5 = time.perf_counter()
-            ts += t2 - t1
-            tc += t4 - t3
-            tt += t5 - t4
-        log(f"[rank {rank}] idle-GPU host cost: submit {ts / 20 * 1e3:.4f} ms, collect {tc / 20 * 1e3:.4f} ms, stats {tt / 20 * 1e3:.4f} ms")
-    n_sites = st.sites_called
-    log(f"[rank {rank}] host per pass: submit {1e3 * t_sub / args.steps:.4f} ms, collect (incl. wait) {1e3 * t_col / args.steps:.4f} ms")
+    st = sessions[0].stats()
     log(f"[rank {rank}] tile {st.tile_positions} positions (max {st.tile_rows_max} rows), pile {st.pile_bytes} B, "
-        f"slot {st.slot_size} B, {st.candidates} candidates, {st.exact_bound_passes} exact-bound passes, "
-        f"{st.hard_sites} needed the exact tally + posterior")
-    cold = cold_passes(sess) if world == 1 and not args.no_cold else None
-    sess.release_staged()
-    sess.close()
+        f"{st.candidates} candidates, {st.hard_sites} needed the exact tally + posterior, {sites_called} calls")
+    cold = cold_passes(sessions[0]) if world == 1 and not args.no_cold and len(sessions) == 1 else None
+    stats_all = [s.stats() for s in sessions]
+    pile_bytes = sum(x.pile_bytes for x in stats_all)
+    tile = st.tile_positions
+    # bytes KT moves per launch: the bit planes (rows_t * T / 4 per tile), the reference codes (1 B per
+    # global position, halos included) and the 16-B tile descriptors; the multisample KTM streams its
+    # per-sample byte blocks and the reference codes
+    if multi:
+        kt_bytes = sum(x.pile_bytes + x.global_positions + 16 * x.n_tiles for x in stats_all)
+    else:
+        kt_bytes = sum(x.pile_bytes // 4 + x.global_positions + 16 * x.n_tiles for x in stats_all)
+    layout_ms = sum(x.layout_ms for x in stats_all)
+    upload_ms = sum(x.upload_ms for x in stats_all)
+    for s in sessions:
+        s.release_staged()
+        s.close()
+
+    e2e = None
+    if e2e_src is not None:
+        try:
+            e2e = end_to_end(e2e_src[1], e2e_src[2], local_rank)
+            log(f"[rank 0] end-to-end BAM -> VCF: {e2e['wall_s']:.2f}s, {e2e['value']:.4g} positions/s")
+        except Exception as e:
+            e2e = {"value": None, "error": str(e)}
+        finally:
+            shutil.rmtree(e2e_src[0], ignore_errors=True)
 
     if dist is not None:
         import torch
@@ -303,18 +481,14 @@ def main():
     if rank == 0:
         steps = args.steps
         value = total_positions * steps / elapsed
-        k_avg_ms = sum(scan_ms) / len(scan_ms)
+        k_avg_ms = sum(scan_ms) / len(scan_ms) * (len(sessions) if len(sessions) > 1 else 1)
         post_avg_ms = (sum(geno_ms) / len(geno_ms)) if max(geno_ms, default=0) > 0 else None
-        # algorithmic bytes per k_tile_pileup launch: 1 B per projected read base,
-        # 1 B reference per genotyped position, 16 B read header per admitted read
-        alg_bytes = st.read_bases + positions + 16 * st.alignments_admitted
-        achieved = alg_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else None
-        workload_key = (f"multisample{args.samples}:{args.depth:g}x:contig{args.contig_first}" if multi
-                        else f"{args.genome}:{args.depth:g}x:seed{seed}")
+        # SURVEY.md 8(d)'s algorithmic bytes (1 B per read base + 1 B reference + 16 B per read) as an
+        # equivalent rate beside the bytes KT moves
+        alg_bytes = read_bases + positions + 16 * reads
+        achieved = kt_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else None
         traffic = load_traffic(workload_key)
-        planes = not multi and st.tile_positions in (128, 256, 512) and not os.environ.get("NGSEP_NO_PLANES")
-        scan_kernel = ("k_tile_pileup_multi" if multi else
-                       f"k_tile_planes<{st.tile_positions // 32}>" if planes else "k_tile_pileup<0>")
+        scan_kernel = "k_tile_pileup_multi" if multi else f"k_tile_planes<{tile // 32}>"
         line = {
             "metric": METRIC,
             "value": value,
@@ -327,17 +501,20 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8,f64",
-            "data": "synthetic (seeded generator, SURVEY.md 8(d)); read SoA resident in HBM",
+            "data": "synthetic (seeded generator, SURVEY.md 8(d)); host-packed layout resident in HBM",
             "config": {
                 "workload": workload,
                 "positions_per_gpu": positions,
-                "reads_per_gpu": int(st.alignments_admitted),
-                "read_bases_per_gpu": int(st.read_bases),
-                "sites_called_per_gpu": int(n_sites),
+                "reads_per_gpu": int(reads),
+                "read_bases_per_gpu": int(read_bases),
+                "sites_called_per_gpu": int(sites_called),
                 "candidates_per_gpu": int(st.candidates),
                 "exact_sites_per_gpu": int(st.hard_sites),
-                "pile_bytes_per_gpu": int(st.pile_bytes),
-                "tile_positions": int(st.tile_positions),
+                "pile_bytes_per_gpu": int(pile_bytes),
+                "tile_positions": int(tile),
+                "device_runs_per_gpu": len(sessions),
+                "host_layout_ms": layout_ms,
+                "h2d_upload_ms": upload_ms,
                 "parallelism": f"dp{world} (independent genomic windows per GPU, no collective)",
             },
             "roofline": {
@@ -348,26 +525,23 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS if achieved else None,
                 "traffic": traffic,
-                "alg_bytes_per_launch": alg_bytes,
+                "bytes_per_launch": kt_bytes,
                 "kernel_avg_ms": k_avg_ms,
-                # achieved counts the algorithmic bytes; the bit-plane scan moves a quarter
-                # of them, so its HBM rate is traffic / time
                 "traffic_rate_GBs": (traffic / (k_avg_ms * 1e-3) / 1e9) if traffic and k_avg_ms > 0 else None,
+                "alg_bytes_per_launch": alg_bytes,
+                "alg_equiv_GBs": alg_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else None,
                 "cold": cold,
-                # KP is timed only with NGSEP_TIME_POSTERIOR=1 (its event costs ~7 us of pipeline gap)
+                # KP is timed only with NGSEP_TIME_POSTERIOR=1 (its event costs a few us of pipeline gap)
                 "posterior_kernel_avg_ms": post_avg_ms,
             },
-            "kernel_positions_per_s": (total_positions / ((k_avg_ms + post_avg_ms) * 1e-3)) if post_avg_ms else None,
         }
         if multi:
             line["config"]["samples"] = args.samples
-            line["config"]["sample_calls_per_step"] = int(n_sites) * args.samples
-        if not args.no_cpu_baseline:
-            try:
-                line["cpu_baseline"] = (cpu_baseline_mvd(args.samples, args.depth) if multi
-                                        else cpu_baseline(args.depth, 2, args.cpu_contigs))
-            except Exception as e:  # the baseline is reported, never required
-                line["cpu_baseline"] = {"value": None, "error": str(e)}
+            line["config"]["sample_calls_per_step"] = int(sites_called) * args.samples
+        if e2e is not None:
+            line["end_to_end"] = e2e
+        if cpu is not None:
+            line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

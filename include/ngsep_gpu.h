@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define NGSEP_ABI_VERSION 1
+#define NGSEP_ABI_VERSION 2
 
 #define NGSEP_OK 0
 #define NGSEP_E_INVALID (-1)      /* bad argument / state */
@@ -157,6 +157,10 @@ typedef struct ngsep_stats {
     int32_t hard_sites;             /* candidates that needed the exact tally + posterior */
     int64_t pile_bytes;             /* bytes of the tile-blocked pileup matrix streamed by the scan */
     int64_t exact_bound_passes;     /* wavefront passes of the scan's exact integer hom-ref bound */
+    int64_t global_positions;       /* positions of the device coordinate (windows + halos, whole tiles) */
+    int64_t n_tiles;                /* pileup tiles */
+    double  layout_ms;              /* host time to build the device layout of the last staged run */
+    double  upload_ms;              /* host time of its H2D upload */
 } ngsep_stats;
 
 /* ---- context ---- */

@@ -135,6 +135,10 @@ class NgsepStats(ctypes.Structure):
         ("hard_sites", ctypes.c_int32),
         ("pile_bytes", ctypes.c_int64),
         ("exact_bound_passes", ctypes.c_int64),
+        ("global_positions", ctypes.c_int64),
+        ("n_tiles", ctypes.c_int64),
+        ("layout_ms", ctypes.c_double),
+        ("upload_ms", ctypes.c_double),
     ]
 
 

@@ -107,12 +107,12 @@ void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g) {
 }
 
 // ReadAlignment.updateAlleleCallsInfo (ReadAlignment.java:747-834): allele-call length per read position.
-static void allele_call_lengths(const RawRead& r, int read_length, int ignore_start, int ignore_end, std::vector<int16_t>& acl) {
-    acl.assign(read_length > 0 ? read_length : 1, 0);
+static void allele_call_lengths(const ReadView& r, int read_length, int ignore_start, int ignore_end, int16_t* acl) {
+    std::memset(acl, 0, sizeof(int16_t) * (size_t)(read_length > 0 ? read_length : 1));
     int readPos = 0;
     bool prevIndel = false;
     const int closeIndel = 2;   // basesToIgnoreCloseToIndel (:115)
-    const int n = (int)r.cigar.size();
+    const int n = r.n_cigar;
     for (int i = 0; i < n; i++) {
         int len = r.cigar[i] / 8, op = r.cigar[i] & 7;
         bool cRef = op & 1, cRead = (op & 2) != 0;
@@ -149,24 +149,27 @@ static void allele_call_lengths(const RawRead& r, int read_length, int ignore_st
     }
 }
 
-// Projects one admitted read to one code byte per reference position in [first, last].
-// Equivalent to evaluating, for every covered position p, PileupRecord.getAlleleCalls(1)'s
-// per-read step (PileupRecord.java:132-148) and CountsHelper.calculateCountsGTSNV's
-// quality clamp (CountsHelper.java:91).
-void project_read(const ngsep_ctx* c, const RawRead& r, int32_t last, std::vector<uint8_t>& out) {
-    const int64_t span = (int64_t)last - r.first + 1;
-    out.assign(span > 0 ? span : 0, 0);
-    if (span <= 0 || r.chars.empty()) return;   // getAlleleCall returns null without characters
+// Projects one admitted read to one code byte per reference position in [first, last] (out holds
+// last - first + 1 bytes, zero-filled here).  Equivalent to evaluating, for every covered position p,
+// PileupRecord.getAlleleCalls(1)'s per-read step (PileupRecord.java:132-148) and
+// CountsHelper.calculateCountsGTSNV's quality clamp (CountsHelper.java:91).
+void project_read(const ngsep_ctx* c, const ReadView& r, uint8_t* out) {
+    const int64_t span = (int64_t)r.last - r.first + 1;
+    if (span <= 0) return;
+    std::memset(out, 0, (size_t)span);
+    if (!r.chars) return;   // getAlleleCall returns null without characters
     int read_length = 0;
-    for (int32_t v : r.cigar) if (v & 2) read_length += v / 8;
+    for (int32_t k = 0; k < r.n_cigar; k++) if (r.cigar[k] & 2) read_length += r.cigar[k] / 8;
     // setBasesToIgnore5P/3P (ReadAlignment.java:613-644)
     const bool neg = (r.flags & 0x10) != 0;
     int ignore_start = neg ? c->params.ignore3 : c->params.ignore5;
     int ignore_end = neg ? c->params.ignore5 : c->params.ignore3;
-    std::vector<int16_t> acl;
-    allele_call_lengths(r, read_length, ignore_start, ignore_end, acl);
+    thread_local std::vector<int16_t> acl;
+    if ((int)acl.size() < read_length + 1) acl.resize((size_t)read_length + 1);
+    allele_call_lengths(r, read_length, ignore_start, ignore_end, acl.data());
     int64_t refPos = r.first, readPos = 0;
-    for (int32_t v : r.cigar) {
+    for (int32_t k = 0; k < r.n_cigar; k++) {
+        const int32_t v = r.cigar[k];
         int len = v / 8, op = v & 7;
         bool cRef = op & 1, cRead = (op & 2) != 0;
         if (cRef && cRead) {
@@ -174,9 +177,9 @@ void project_read(const ngsep_ctx* c, const RawRead& r, int32_t last, std::vecto
                 int64_t rp = readPos + j;
                 int64_t o = refPos + j - r.first;
                 if (rp >= read_length || o < 0 || o >= span) continue;
-                if (acl[rp] != 1) continue;   // 0: masked (getAlleleCall null); >1: skipped for span 1
-                int qc = r.quals.empty() ? '+' : (unsigned char)r.quals[rp];   // getBaseQualityScore
-                if (qc > 127) qc = 127;                                          // setQualityScores cap
+                if (acl[(size_t)rp] != 1) continue;   // 0: masked (getAlleleCall null); >1: skipped for span 1
+                int qc = r.quals ? (unsigned char)r.quals[rp] : '+';                   // getBaseQualityScore
+                if (qc > 127) qc = 127;                                                 // setQualityScores cap
                 int q = (int8_t)std::min(30, qc - 33);
                 int a = dna_index(r.chars[rp]);
                 uint8_t code;
@@ -191,15 +194,11 @@ void project_read(const ngsep_ctx* c, const RawRead& r, int32_t last, std::vecto
     }
 }
 
-static int32_t alignment_last(const RawRead& r) {
-    int32_t e = r.first;
-    for (int32_t v : r.cigar) if (v & 1) e += v / 8;
-    return e - 1;
-}
-
-static void admit(ngsep_ctx* c, const RawRead& r) {
+// admission of one read into the current sequence's pending list (AlignmentsPileupGenerator
+// .processSameStartAlns :428-430); its projection is deferred to project_pending (batched, parallel)
+static void admit(ngsep_ctx* c, const ReadView& r) {
     ContigReads& cr = c->contig;
-    int32_t last = alignment_last(r);
+    const int32_t last = r.last;
     if (c->params.coverage_stats) {
         // CoverageStatisticsCalculator: only [first, last] and isUnique reach the listener
         // (PileupRecord.addAlignment, :154-167); positions past the sequence end still get pileups
@@ -216,8 +215,6 @@ static void admit(ngsep_ctx* c, const RawRead& r) {
         c->stats.alignments_admitted++;
         return;
     }
-    std::vector<uint8_t> bytes;
-    project_read(c, r, last, bytes);
     cr.first.push_back(r.first);
     cr.last.push_back(last);
     cr.neg.push_back((r.flags & 0x10) ? 1 : 0);
@@ -226,8 +223,7 @@ static void admit(ngsep_ctx* c, const RawRead& r) {
         cr.sample.push_back((int16_t)(in ? c->rg_sample[r.rg] : -1));
         cr.rank.push_back((uint8_t)(in && c->rg_sample[r.rg] >= 0 ? c->rg_rank[r.rg] : 0));
     }
-    cr.boff.push_back((int64_t)cr.bytes.size());
-    cr.bytes.insert(cr.bytes.end(), bytes.begin(), bytes.end());
+    c->to_project.push_back(r);
     int32_t span = last - r.first + 1;
     if (span > cr.max_span) cr.max_span = span;
     // union of covered positions inside the sequence (and the query range)
@@ -247,22 +243,53 @@ static void admit(ngsep_ctx* c, const RawRead& r) {
     c->stats.alignments_admitted++;
 }
 
+// projects the admitted reads whose bytes are still pending into the sequence's byte store, on all
+// host threads (every read's bytes go to its own preallocated range)
+static void project_pending(ngsep_ctx* c) {
+    std::vector<ReadView>& v = c->to_project;
+    if (v.empty()) return;
+    ContigReads& cr = c->contig;
+    const size_t n = v.size();
+    size_t off = cr.bytes.size();
+    const size_t b0 = cr.boff.size();
+    cr.boff.resize(b0 + n);
+    for (size_t i = 0; i < n; i++) {
+        cr.boff[b0 + i] = (int64_t)off;
+        const int64_t span = (int64_t)v[i].last - v[i].first + 1;
+        off += span > 0 ? (size_t)span : 0;
+    }
+    if (cr.bytes.capacity() < off) cr.bytes.reserve(std::max(off, cr.bytes.capacity() * 3 / 2));
+    cr.bytes.resize(off);
+    uint8_t* base = cr.bytes.data();
+    const int64_t* boff = cr.boff.data() + b0;
+    parallel_for((int64_t)n, 2048, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; i++) project_read(c, v[(size_t)i], base + boff[i]);
+    });
+    v.clear();
+}
+
 // AlignmentsPileupGenerator.processSameStartAlns (:407-433)
 static void process_same_start(ngsep_ctx* c) {
     if (c->ss_primary.empty() && c->ss_secondary.empty()) return;
-    std::vector<std::pair<int32_t, int32_t>> per_rg;   // (rg, count): few read groups per start
-    auto handle = [&](const RawRead& r) {
-        for (auto& pr : per_rg) {
-            if (pr.first == r.rg) {
-                if (c->params.max_alns_per_start <= 0 || pr.second < c->params.max_alns_per_start) { pr.second++; admit(c, r); }
+    std::pair<int32_t, int32_t> per_rg_small[8];   // (rg, count): few read groups per start
+    std::vector<std::pair<int32_t, int32_t>> per_rg_big;
+    int n_rg = 0;
+    auto handle = [&](const ReadView& r) {
+        std::pair<int32_t, int32_t>* tab = per_rg_big.empty() ? per_rg_small : per_rg_big.data();
+        for (int k = 0; k < n_rg; k++) {
+            if (tab[k].first == r.rg) {
+                if (c->params.max_alns_per_start <= 0 || tab[k].second < c->params.max_alns_per_start) { tab[k].second++; admit(c, r); }
                 return;
             }
         }
-        per_rg.push_back({r.rg, 1});
+        if (n_rg == 8 && per_rg_big.empty()) per_rg_big.assign(per_rg_small, per_rg_small + 8);
+        if (per_rg_big.empty()) per_rg_small[n_rg] = {r.rg, 1};
+        else per_rg_big.push_back({r.rg, 1});
+        n_rg++;
         admit(c, r);
     };
-    for (const RawRead& r : c->ss_primary) handle(r);
-    for (const RawRead& r : c->ss_secondary) handle(r);
+    for (const ReadView& r : c->ss_primary) handle(r);
+    for (const ReadView& r : c->ss_secondary) handle(r);
     c->ss_primary.clear();
     c->ss_secondary.clear();
 }
@@ -271,6 +298,7 @@ static void process_same_start(ngsep_ctx* c) {
 static int flush_sequence(ngsep_ctx* c) {
     if (c->cur_seq < 0) return NGSEP_OK;
     process_same_start(c);
+    project_pending(c);
     int rc = stage_contig_reads(c, c->contig, !c->staging_mode);
     c->contig.clear();
     c->cur_seq = -1;
@@ -296,37 +324,72 @@ int stage_contig_reads(ngsep_ctx* c, ContigReads& cr, bool run_now) {
     return rc;
 }
 
+// the open same-start group outlives the caller's batch: its reads' bytes move to the carry store
+static void carry_open_group(ngsep_ctx* c) {
+    if (c->ss_primary.empty() && c->ss_secondary.empty()) return;
+    CarryStore& cs = c->carry[c->carry_cur ^ 1];
+    size_t nc = 0, nb = 0;
+    for (auto* g : {&c->ss_primary, &c->ss_secondary})
+        for (const ReadView& r : *g) { nc += (size_t)r.n_cigar; nb += (size_t)r.len; }
+    cs.cigar.clear(); cs.chars.clear(); cs.quals.clear();
+    cs.cigar.reserve(nc); cs.chars.reserve(nb); cs.quals.reserve(nb);
+    for (auto* g : {&c->ss_primary, &c->ss_secondary})
+        for (ReadView& r : *g) {
+            const size_t co = cs.cigar.size(), so = cs.chars.size();
+            cs.cigar.insert(cs.cigar.end(), r.cigar, r.cigar + r.n_cigar);
+            if (r.chars) cs.chars.append(r.chars, (size_t)r.len);
+            if (r.quals) cs.quals.append(r.quals, (size_t)r.len);
+            else cs.quals.append((size_t)r.len, '\0');
+            r.cigar = cs.cigar.data() + co;
+            if (r.chars) r.chars = cs.chars.data() + so;
+            if (r.quals) r.quals = cs.quals.data() + so;
+        }
+    c->carry_cur ^= 1;
+}
+
 static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b) {
     if (!b || b->n_reads < 0) return set_error(c, NGSEP_E_INVALID, "null batch");
     const int nseq = (int)c->seq_names.size();
+    int rc = NGSEP_OK;
     for (int64_t i = 0; i < b->n_reads; i++) {
         if (c->query_done) break;
         c->stats.alignments_in++;
-        RawRead r;
+        ReadView r;
         r.seq_id = b->seq_id[i];
         r.first = b->first[i];
         r.flags = b->flags[i];
         r.rg = b->read_group ? b->read_group[i] : -1;
-        if (r.seq_id < 0 || r.seq_id >= nseq)
-            return set_error(c, NGSEP_E_INVALID, "alignment on unknown sequence id " + std::to_string(r.seq_id));
-        r.cigar.assign(b->cigar + b->cigar_off[i], b->cigar + b->cigar_off[i] + b->cigar_n[i]);
-        for (int32_t v : r.cigar) {
-            int op = v & 7;
-            if ((op == 1 || op == 2) && !c->params.coverage_stats)
-                return set_error(c, NGSEP_E_UNSUPPORTED,
-                                 "alignment with an indel (CIGAR I/D): the indel realigner path "
-                                 "(IndelRealignerPileupListener) is not implemented on the GPU yet");
+        if (r.seq_id < 0 || r.seq_id >= nseq) {
+            rc = set_error(c, NGSEP_E_INVALID, "alignment on unknown sequence id " + std::to_string(r.seq_id));
+            break;
         }
-        int32_t sl = b->seq_len[i];
+        r.cigar = b->cigar + b->cigar_off[i];
+        r.n_cigar = b->cigar_n[i];
+        bool indel = false;
+        int32_t last = r.first - 1, read_length = 0;
+        for (int32_t k = 0; k < r.n_cigar; k++) {
+            const int32_t v = r.cigar[k], op = v & 7;
+            indel |= op == 1 || op == 2;
+            if (v & 1) last += v / 8;
+            if (v & 2) read_length += v / 8;
+        }
+        if (indel && !c->params.coverage_stats) {
+            rc = set_error(c, NGSEP_E_UNSUPPORTED,
+                           "alignment with an indel (CIGAR I/D): the indel realigner path "
+                           "(IndelRealignerPileupListener) is not implemented on the GPU yet");
+            break;
+        }
+        r.last = last;
+        const int32_t sl = b->seq_len[i];
+        r.len = sl > 0 ? sl : 0;
+        r.chars = nullptr;
+        r.quals = nullptr;
         if (sl > 0) {
-            r.chars.assign(b->bases + b->seq_off[i], sl);
-            bool hq = b->quals && (!b->has_quals || b->has_quals[i]);
-            if (hq) r.quals.assign(b->quals + b->seq_off[i], sl);
-            int read_length = 0;
-            for (int32_t v : r.cigar) if (v & 2) read_length += v / 8;
+            r.chars = b->bases + b->seq_off[i];
+            const bool hq = b->quals && (!b->has_quals || b->has_quals[i]);
+            if (hq) r.quals = b->quals + b->seq_off[i];
             if (read_length != sl) continue;   // ReadAlignment.setReadCharacters throws -> record skipped
         }
-        int32_t last = alignment_last(r);
         // querySeq handling (AlignmentsPileupGenerator.java:342-354)
         if (c->params.query_seq[0]) {
             if (c->seq_names[r.seq_id] == c->params.query_seq) {
@@ -343,13 +406,15 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b) {
         // processAlignment (:377-403)
         if (c->cur_seq >= 0) {
             bool same = c->cur_seq == r.seq_id;
-            if (same && r.first < c->last_start)
-                return set_error(c, NGSEP_E_INVALID, "alignments are not coordinate-sorted");
+            if (same && r.first < c->last_start) {
+                rc = set_error(c, NGSEP_E_INVALID, "alignments are not coordinate-sorted");
+                break;
+            }
             if (!same || c->last_start != r.first) {
                 process_same_start(c);
                 if (!same) {
-                    int rc = flush_sequence(c);
-                    if (rc != NGSEP_OK) return rc;
+                    rc = flush_sequence(c);
+                    if (rc != NGSEP_OK) break;
                 }
             }
         }
@@ -360,11 +425,14 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b) {
             c->cur_last = last;
         }
         if (last > c->cur_last) c->cur_last = last;
-        if (r.flags & 0x100) c->ss_secondary.push_back(std::move(r));
-        else c->ss_primary.push_back(std::move(r));
-        c->last_start = b->first[i];
+        if (r.flags & 0x100) c->ss_secondary.push_back(r);
+        else c->ss_primary.push_back(r);
+        c->last_start = r.first;
     }
-    return NGSEP_OK;
+    // the admitted reads' bytes are projected while the batch is alive; the open group is carried
+    project_pending(c);
+    carry_open_group(c);
+    return rc;
 }
 
 // ---- staging: fixed-stride slot layout of every window's reads ----
@@ -394,85 +462,74 @@ static inline uint8_t ref_code(const ngsep_ctx* c, char ch) {
     return (uint8_t)(kRefCallable | (a << 5));
 }
 
-// ---- tile-blocked pileup matrix (engine.hpp TileInfo) ----
-// Tile size: every T in [kTileMinPos, kTileMaxPos] is costed as the bytes of its matrix
-// (sum over tiles of rows_t * T, rows_t = the tile's maximum depth) plus a fixed per-tile cost;
-// T must keep >= 99.9 % of tiles within the registers of one wavefront (the rest reload).
-static int choose_tile(const std::vector<int32_t>& cov_max16, int64_t g_len, std::vector<int32_t>& rows_out) {
-    std::vector<int32_t> cur = cov_max16;   // maxima over blocks of T positions, T = 16, 32, ...
-    int bestT = kTileMinPos;
-    double best_cost = -1;
-    std::vector<int32_t> best_rows;
-    const int64_t budget = kScanRegUnits;   // 16-byte units held in registers
-    static const bool no_planes = std::getenv("NGSEP_NO_PLANES") != nullptr;
-    for (int T = kTileMinPos; T <= kTileMaxPos; T *= 2) {
-        if (T > kTileMinPos) {
-            std::vector<int32_t> nxt((cur.size() + 1) / 2);
-            for (size_t i = 0; i < nxt.size(); i++)
-                nxt[i] = std::max(cur[2 * i], 2 * i + 1 < cur.size() ? cur[2 * i + 1] : 0);
-            cur.swap(nxt);
-        }
-        const int64_t ntiles = g_len / T;
-        int64_t over = 0;
-        double bytes = 0;
-        for (int64_t t = 0; t < ntiles; t++) {
-            bytes += (double)cur[t] * T;
-            if ((int64_t)cur[t] * (T / 16) > budget) over++;
-        }
-        // tiles of 128..512 positions are scanned as bit planes (2 bits per row-position: a quarter of the
-        // byte pile, streamed in 64-row chunks, so the byte kernel's register budget does not apply); the
-        // per-tile term prices the tile's fixed instruction stream.  Measured on the 30x yeast / chr20
-        // genomes: T = 512 scans in 0.041 / 0.144 ms vs 0.048 / 0.188 ms at T = 256.
-        const bool planes = (T == 128 || T == 256 || T == 512) && !no_planes;
-        if (!planes && over * 1000 > ntiles) continue;
-        const double cost = (planes ? bytes / 4 : bytes) + 2048.0 * (double)ntiles;
-        if (best_cost < 0 || cost < best_cost) { best_cost = cost; bestT = T; best_rows.assign(cur.begin(), cur.begin() + ntiles); }
-    }
-    if (const char* e = std::getenv("NGSEP_TILE_T")) {   // tests and tuning: a fixed tile width
-        const int T = std::atoi(e);
-        if (T >= kTileMinPos && T <= kTileMaxPos && (T & (T - 1)) == 0) {
-            std::vector<int32_t> c = cov_max16;
-            for (int t = kTileMinPos; t < T; t *= 2) {
-                std::vector<int32_t> nxt((c.size() + 1) / 2);
-                for (size_t i = 0; i < nxt.size(); i++) nxt[i] = std::max(c[2 * i], 2 * i + 1 < c.size() ? c[2 * i + 1] : 0);
-                c.swap(nxt);
-            }
-            rows_out.assign(c.begin(), c.begin() + g_len / T);
-            return T;
-        }
-    }
-    if (best_cost < 0) {   // every T overflows the registers somewhere: smallest tiles, reload path
-        bestT = kTileMinPos;
-        best_rows.assign(cov_max16.begin(), cov_max16.begin() + g_len / kTileMinPos);
-    }
-    rows_out.swap(best_rows);
-    return bestT;
-}
-
-// Each tile's reads (clipped to the tile) are packed into rows by greedy interval colouring in
-// pending-list order: a read takes a row whose previous read ended before it starts, so rows_t
-// equals the maximum depth inside the tile.  Codes are stored allele-XOR-reference.
-static void build_pile(Staged& s) {
-    const int64_t g_len = s.g_len, nreads = s.n_reads;
-    const int32_t* R = s.h_reads.data();
-    // depth per position (difference array), then maxima over 16-position blocks
+// ---- tile-blocked pileup (engine.hpp TileInfo) ----
+// maxima of the per-position depth over blocks of 16 positions (difference array over the read table)
+static std::vector<int32_t> depth_max16(const int32_t* R, int64_t nreads, int stride, int64_t g_len) {
     std::vector<int32_t> cov((size_t)g_len + 1, 0);
     for (int64_t i = 0; i < nreads; i++) {
-        const int32_t a = R[i * 4], b = R[i * 4 + 1];
+        const int32_t a = R[i * stride], b = R[i * stride + 1];
         if (b < a) continue;
-        cov[a]++;
+        cov[(size_t)a]++;
         cov[(size_t)b + 1]--;
     }
     std::vector<int32_t> m16((size_t)(g_len / kTileMinPos), 0);
     int32_t run = 0;
-    for (int64_t p = 0; p < g_len; p++) {
-        run += cov[p];
-        int32_t& m = m16[p / kTileMinPos];
+    for (int64_t p = 0; p < (int64_t)m16.size() * kTileMinPos; p++) {
+        run += cov[(size_t)p];
+        int32_t& m = m16[(size_t)(p / kTileMinPos)];
         if (run > m) m = run;
     }
-    std::vector<int32_t>().swap(cov);
+    return m16;
+}
+static std::vector<int32_t> widen_max(const std::vector<int32_t>& m16, int T, int64_t ntiles) {
+    std::vector<int32_t> c = m16;
+    for (int t = kTileMinPos; t < T; t *= 2) {
+        std::vector<int32_t> nxt((c.size() + 1) / 2);
+        for (size_t i = 0; i < nxt.size(); i++) nxt[i] = std::max(c[2 * i], 2 * i + 1 < c.size() ? c[2 * i + 1] : 0);
+        c.swap(nxt);
+    }
+    c.resize((size_t)ntiles, 0);
+    return c;
+}
+// Tile width of the single-sample layout: KT scans bit planes of 128, 256 or 512 positions (one wavefront
+// per tile, W = T/32 words per plane row).  Each width is costed as the planes' bytes (a quarter of
+// sum rows_t * T) plus a fixed per-tile cost for the tile's instruction stream.  Measured on the 30x
+// yeast / chr20 genomes (round 1): T = 512 scans in 0.041 / 0.144 ms vs 0.048 / 0.188 ms at T = 256.
+static int choose_tile(const std::vector<int32_t>& m16, int64_t g_len, std::vector<int32_t>& rows_out) {
+    int bestT = 512;
+    double best_cost = -1;
+    for (int T : {128, 256, 512}) {
+        const int64_t ntiles = g_len / T;
+        const std::vector<int32_t> r = widen_max(m16, T, ntiles);
+        double bytes = 0;
+        for (int64_t t = 0; t < ntiles; t++) bytes += (double)r[(size_t)t] * T;
+        const double cost = bytes / 4 + 2048.0 * (double)ntiles;
+        if (best_cost < 0 || cost < best_cost) { best_cost = cost; bestT = T; }
+    }
+    if (const char* e = std::getenv("NGSEP_TILE_T")) {   // tests and tuning: a fixed tile width
+        const int T = std::atoi(e);
+        if (T == 128 || T == 256 || T == 512) bestT = T;
+    }
+    rows_out = widen_max(m16, bestT, g_len / bestT);
+    return bestT;
+}
+
+// Single-sample layout.  Each tile's reads (clipped to the tile) are packed into
+// rows by greedy interval colouring in pending-list order: a read takes a row whose previous read ended
+// before it starts, so rows_t equals the maximum depth inside the tile.  Three products per tile:
+//   * the bit planes (KT): row r holds W = T/32 words of "valid call" bits, then W words of "valid call
+//     of another allele" bits; the tile's planes start at word off_t / 16;
+//   * the position-major byte pile (KP): position p's rows_t codes at off_t + p * rows_t;
+//   * the tile's read segments in pending-list order (KP's summation order): row << 18 | a << 9 | b,
+//     the read covers tile positions a..b in that row.
+// Tiles are independent: built on all host threads.
+static int build_single_layout(Staged& s, const std::vector<SRead>& reads) {
+    const int64_t g_len = s.g_len, nreads = (int64_t)reads.size();
+    std::vector<int32_t> R2((size_t)nreads * 2);
+    for (int64_t i = 0; i < nreads; i++) { R2[(size_t)(2 * i)] = reads[(size_t)i].gfirst; R2[(size_t)(2 * i + 1)] = reads[(size_t)i].glast; }
     std::vector<int32_t> rows;
-    const int T = choose_tile(m16, g_len, rows);
+    const int T = choose_tile(depth_max16(R2.data(), nreads, 2, g_len), g_len, rows);
+    std::vector<int32_t>().swap(R2);
     const int64_t ntiles = g_len / T;
     s.tile = T;
     s.n_tiles = ntiles;
@@ -480,63 +537,99 @@ static void build_pile(Staged& s) {
     int64_t off = 0;
     int32_t rmax = 0;
     for (int64_t t = 0; t < ntiles; t++) {
-        s.h_tinfo[t].off = off;
-        s.h_tinfo[t].rows = rows[t];
-        s.h_tinfo[t].pad = 0;
-        off += (int64_t)rows[t] * T;
-        rmax = std::max(rmax, rows[t]);
+        s.h_tinfo[(size_t)t].off = off;
+        s.h_tinfo[(size_t)t].rows = rows[(size_t)t];
+        s.h_tinfo[(size_t)t].pad = 0;
+        off += (int64_t)rows[(size_t)t] * T;
+        rmax = std::max(rmax, rows[(size_t)t]);
     }
+    if (rmax >= (1 << 14)) return -1;      // segment rows are 14-bit
     s.pile_bytes = off;
     s.tile_rows_max = rmax;
-    s.h_pile.assign((size_t)off, 0);
-    const int S = s.slot_size;
-    const uint8_t* slots = s.h_slots.data();
+    // first read that can reach tile t (reads are sorted by global first position)
+    auto first_read = [&](int64_t t) -> int64_t {
+        const int64_t lo_pos = t * T - s.max_span;
+        return std::lower_bound(reads.begin(), reads.end(), lo_pos, [](const SRead& r, int64_t v) { return (int64_t)r.gfirst <= v; }) - reads.begin();
+    };
+    // segments per tile (reads overlapping it), then their offsets
+    s.h_tseg.assign((size_t)ntiles + 1, 0);
+    parallel_for(ntiles, 512, [&](int64_t t0, int64_t t1) {
+        int64_t r = first_read(t0);
+        for (int64_t t = t0; t < t1; t++) {
+            const int32_t tstart = (int32_t)(t * T), tend = tstart + T;
+            while (r < nreads && (int64_t)reads[(size_t)r].gfirst <= (int64_t)tstart - s.max_span) r++;
+            int32_t n = 0;
+            for (int64_t k = r; k < nreads && reads[(size_t)k].gfirst < tend; k++)
+                if (reads[(size_t)k].glast >= tstart && reads[(size_t)k].glast >= reads[(size_t)k].gfirst) n++;
+            s.h_tseg[(size_t)t + 1] = rows[(size_t)t] ? n : 0;
+        }
+    });
+    for (int64_t t = 0; t < ntiles; t++) s.h_tseg[(size_t)t + 1] += s.h_tseg[(size_t)t];
+    s.h_seg.alloc((size_t)s.h_tseg[(size_t)ntiles]);
+    s.h_segneg.alloc((size_t)s.h_tseg[(size_t)ntiles]);
+    s.h_cpile.alloc((size_t)off);
+    s.h_planes.alloc((size_t)(off / 16));
+    const int W = T / 32;
     const uint8_t* ref = s.h_ref.data();
-    std::vector<std::pair<int32_t, int32_t>> heap;   // (last clipped position, row): min-heap
-    std::vector<int32_t> free_rows;
-    int64_t r_lo = 0;
-    for (int64_t t = 0; t < ntiles; t++) {
-        if (!rows[t]) continue;
-        const int32_t tstart = (int32_t)(t * T), tend = tstart + T;
-        while (r_lo < nreads && R[r_lo * 4] <= tstart - s.max_span) r_lo++;   // cannot reach this tile
-        heap.clear();
-        free_rows.clear();
-        int32_t next_row = 0;
-        uint8_t* blk = &s.h_pile[(size_t)s.h_tinfo[t].off];
-        for (int64_t r = r_lo; r < nreads && R[r * 4] < tend; r++) {
-            const int32_t gfirst = R[r * 4], glast = R[r * 4 + 1];
-            if (glast < tstart || glast < gfirst) continue;
-            const int32_t a = std::max(gfirst, tstart) - tstart, b = std::min(glast, tend - 1) - tstart;
-            while (!heap.empty() && heap.front().first < a) {
-                free_rows.push_back(heap.front().second);
-                std::pop_heap(heap.begin(), heap.end(), std::greater<>());
-                heap.pop_back();
-            }
-            int32_t row;
-            if (!free_rows.empty()) { row = free_rows.back(); free_rows.pop_back(); }
-            else row = next_row++;
-            heap.push_back({b, row});
-            std::push_heap(heap.begin(), heap.end(), std::greater<>());
-            const uint8_t* src = slots + (size_t)R[r * 4 + 2] * S + (tstart + a - gfirst);
-            uint8_t* dst = blk + (size_t)row * T;
-            for (int32_t p = a; p <= b; p++) {
-                uint8_t cd = src[p - a];
-                if (cd & kCodeValid) {
-                    const uint8_t rc = ref[tstart + p];
-                    const uint8_t ra = (rc & kRefCallable) ? (uint8_t)((rc >> 5) & 3) : 0;
-                    cd = (uint8_t)((cd & 0x9F) | ((((cd >> 5) & 3) ^ ra) << 5));
+    parallel_for(ntiles, 256, [&](int64_t t0, int64_t t1) {
+        std::vector<std::pair<int32_t, int32_t>> heap;   // (last clipped position, row): min-heap
+        std::vector<int32_t> free_rows;
+        int64_t r_lo = first_read(t0);
+        for (int64_t t = t0; t < t1; t++) {
+            const int32_t nrow = rows[(size_t)t];
+            const int32_t tstart = (int32_t)(t * T), tend = tstart + T;
+            while (r_lo < nreads && (int64_t)reads[(size_t)r_lo].gfirst <= (int64_t)tstart - s.max_span) r_lo++;
+            if (!nrow) continue;
+            const int64_t toff = s.h_tinfo[(size_t)t].off;
+            uint8_t* col = s.h_cpile.p + toff;
+            uint32_t* pl = s.h_planes.p + toff / 16;
+            std::memset(col, 0, (size_t)nrow * T);
+            std::memset(pl, 0, (size_t)nrow * T / 4);
+            uint32_t* seg = s.h_seg.p + s.h_tseg[(size_t)t];
+            uint8_t* segneg = s.h_segneg.p + s.h_tseg[(size_t)t];
+            heap.clear();
+            free_rows.clear();
+            int32_t next_row = 0;
+            for (int64_t r = r_lo; r < nreads && reads[(size_t)r].gfirst < tend; r++) {
+                const SRead& rd = reads[(size_t)r];
+                if (rd.glast < tstart || rd.glast < rd.gfirst) continue;
+                const int32_t a = std::max(rd.gfirst, tstart) - tstart, b = std::min(rd.glast, tend - 1) - tstart;
+                while (!heap.empty() && heap.front().first < a) {
+                    free_rows.push_back(heap.front().second);
+                    std::pop_heap(heap.begin(), heap.end(), std::greater<>());
+                    heap.pop_back();
                 }
-                dst[p] = cd;
+                int32_t row;
+                if (!free_rows.empty()) { row = free_rows.back(); free_rows.pop_back(); }
+                else row = next_row++;
+                heap.push_back({b, row});
+                std::push_heap(heap.begin(), heap.end(), std::greater<>());
+                *seg++ = (uint32_t)row << 18 | (uint32_t)a << 9 | (uint32_t)b;
+                *segneg++ = rd.neg;
+                const uint8_t* src = rd.bytes + (tstart + a - rd.gfirst);
+                uint32_t* pv = pl + (size_t)row * 2 * W;
+                uint32_t* pn = pv + W;
+                for (int32_t p = a; p <= b; p++) {
+                    const uint8_t cd = src[p - a];
+                    if (cd & kCodeValid) {
+                        const uint8_t rc = ref[tstart + p];
+                        const uint8_t ra = (rc & kRefCallable) ? (uint8_t)((rc >> 5) & 3) : 0;
+                        pv[p >> 5] |= 1u << (p & 31);
+                        if (((cd >> 5) & 3) != ra) pn[p >> 5] |= 1u << (p & 31);
+                    }
+                    col[(size_t)p * nrow + row] = cd;
+                }
             }
         }
-    }
+    });
+    return 0;
 }
 
 // Multisample layout: the same tiles of T positions, one block per (tile, sample) holding that
 // sample's reads coloured into rows (MultisampleVariantsDetector genotypes every sample from its own
 // read groups, PileupRecord.getAlleleCalls(span, readGroups), :104-111).  Reads of no sample only
 // enter the pooled counts, which the population kernel takes from the read table.
-static void build_pile_multi(Staged& s) {
+static int build_pile_multi(Staged& s) {
     const int64_t g_len = s.g_len, nreads = s.n_reads;
     const int S = s.n_samples;
     const int32_t* R = s.h_reads.data();
@@ -546,8 +639,9 @@ static void build_pile_multi(Staged& s) {
         const int sm = (R[i * 4 + 3] >> 8) - 1;
         if (sm >= 0 && sm < S) by_sample[(size_t)sm].push_back(i);
     }
-    // per-sample maxima of the depth over 16-position blocks (saturating at 65535)
+    // per-sample maxima of the depth over 16-position blocks (rows per (tile, sample) are 16-bit)
     std::vector<uint16_t> m16((size_t)S * (size_t)nb16, 0);
+    bool overflow = false;
     {
         std::vector<int32_t> cov((size_t)g_len + 1);
         for (int sm = 0; sm < S; sm++) {
@@ -562,11 +656,13 @@ static void build_pile_multi(Staged& s) {
             int32_t run = 0;
             for (int64_t p = 0; p < nb16 * kTileMinPos; p++) {
                 run += cov[p];
+                if (run > 65535) overflow = true;
                 const int32_t v = run > 65535 ? 65535 : run;
                 if (v > m[p / kTileMinPos]) m[p / kTileMinPos] = (uint16_t)v;
             }
         }
     }
+    if (overflow) return -1;
     // tile size: bytes of all blocks + a fixed cost per (tile, sample) block (the scan's per-block
     // reduction and bound work, in byte equivalents; NGSEP_MS_BLOCK_COST overrides it for tuning)
     double block_cost = 1024.0;
@@ -663,6 +759,7 @@ static void build_pile_multi(Staged& s) {
             }
         }
     }
+    return 0;
 }
 
 // Population kernel read index: bucket b = (sample, read-group rank) in sample order, then the reads
@@ -704,15 +801,16 @@ static void build_buckets(const ngsep_ctx* c, Staged& s) {
 }
 
 int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
+    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    const auto h0 = std::chrono::steady_clock::now();
     Staged& s = c->staged;
     s = Staged();
     int32_t max_span = 1;
     for (const ContigReads& cr : contigs) max_span = std::max(max_span, cr.max_span);
-    const int S = choose_slot_size(contigs);
     const int32_t pad = ((max_span + 63) / 64) * 64;
-    s.slot_size = S;
     s.max_span = max_span;
-    // windows
+    // windows: the covered span of every sequence (and the query range), cut at window_positions, laid out
+    // in one global coordinate with a halo of pad >= max read span positions between windows
     int64_t g = 0;
     const int64_t W = c->params.window_positions > 0 ? c->params.window_positions : (int64_t)1 << 40;
     struct WR { size_t contig; int64_t lo, hi; };
@@ -723,7 +821,6 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
         int64_t len = (int64_t)c->seq_bases[cr.seq_id].size();
         int64_t lo = 1, hi = len;
         if (c->params.query_seq[0]) { lo = std::max<int64_t>(lo, c->params.query_first); hi = std::min<int64_t>(hi, c->params.query_last); }
-        // only the span of covered positions is needed
         lo = std::max<int64_t>(lo, cr.first.front());
         int64_t maxlast = 0;
         for (int32_t l : cr.last) maxlast = std::max<int64_t>(maxlast, l);
@@ -741,74 +838,104 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     s.g_len = ((g + 64 + kTileMaxPos - 1) / kTileMaxPos) * kTileMaxPos;   // whole tiles, halo for 16-B reads
     if (s.g_len >= ((int64_t)1 << 31))
         return set_error(c, NGSEP_E_UNSUPPORTED, "staged genome exceeds 2^31 positions per device run; use window batching");
-    // reads and slots (read-major SoA: the exact tally of queued candidates walks it in pending order)
-    s.h_reads.clear();
-    s.h_slots.clear();
-    int64_t nslots = 0, nreads = 0, nbases = 0;
+    // reads of every window: those starting in [w0 - max_span + 1, w1]
     std::vector<std::pair<int64_t, int64_t>> ranges(s.windows.size());
+    int64_t nreads = 0, nbases = 0;
     for (size_t wi = 0; wi < s.windows.size(); wi++) {
         const ContigReads& cr = contigs[wr[wi].contig];
-        int64_t w0 = wr[wi].lo, w1 = wr[wi].hi;
+        const int64_t w0 = wr[wi].lo, w1 = wr[wi].hi;
         auto lo_it = std::lower_bound(cr.first.begin(), cr.first.end(), (int32_t)std::max<int64_t>(INT32_MIN, w0 - max_span + 1));
         auto hi_it = std::upper_bound(cr.first.begin(), cr.first.end(), (int32_t)w1);
-        int64_t a = lo_it - cr.first.begin(), b = hi_it - cr.first.begin();
-        ranges[wi] = {a, b};
-        for (int64_t i = a; i < b; i++) {
-            int64_t span = (int64_t)cr.last[i] - cr.first[i] + 1;
-            if (span < 1) span = 1;
-            nslots += (span + S - 1) / S;
-        }
-        nreads += b - a;
+        ranges[wi] = {lo_it - cr.first.begin(), hi_it - cr.first.begin()};
+        nreads += ranges[wi].second - ranges[wi].first;
     }
-    s.h_slots.assign((size_t)nslots * S, 0);
-    s.h_reads.resize((size_t)nreads * 4);
-    int64_t slot = 0, ri = 0;
-    for (size_t wi = 0; wi < s.windows.size(); wi++) {
-        Window& w = s.windows[wi];
-        const ContigReads& cr = contigs[wr[wi].contig];
-        w.read_begin = ri;
-        const int64_t goff = w.gbase + w.pad - w.w0;   // G = pos + goff
-        for (int64_t i = ranges[wi].first; i < ranges[wi].second; i++) {
-            int64_t span = (int64_t)cr.last[i] - cr.first[i] + 1;
-            int64_t ns = span < 1 ? 1 : (span + S - 1) / S;
-            int64_t gfirst = cr.first[i] + goff;
-            s.h_reads[ri * 4 + 0] = (int32_t)gfirst;
-            s.h_reads[ri * 4 + 1] = (int32_t)(cr.last[i] + goff);
-            s.h_reads[ri * 4 + 2] = (int32_t)slot;
-            int32_t fl = cr.neg[i];
-            if (!cr.sample.empty()) fl |= ((int32_t)cr.rank[i] << 1) | (((int32_t)cr.sample[i] + 1) << 8);
-            s.h_reads[ri * 4 + 3] = fl;
-            if (span > 0) std::memcpy(&s.h_slots[(size_t)slot * S], &cr.bytes[cr.boff[i]], (size_t)span);
-            slot += ns;
-            nbases += span > 0 ? span : 0;
-            ri++;
-        }
-        w.read_end = ri;
-    }
-    s.n_reads = nreads;
-    s.n_slots = nslots;
-    s.n_read_bases = nbases;
     for (const ContigReads& cr : contigs) s.covered += cr.covered;
     // reference codes in global coordinates
     s.h_ref.assign((size_t)s.g_len, 0);
     for (const Window& w : s.windows) {
         const std::string& ref = c->seq_bases[w.seq_id];
         uint8_t* dst = &s.h_ref[(size_t)(w.gbase + w.pad)];
-        for (int32_t k = 0; k < w.wlen; k++) dst[k] = ref_code(c, ref[(size_t)w.w0 - 1 + k]);
+        parallel_for(w.wlen, 1 << 20, [&](int64_t lo, int64_t hi) {
+            for (int64_t k = lo; k < hi; k++) dst[k] = ref_code(c, ref[(size_t)(w.w0 - 1 + k)]);
+        });
     }
-    if (c->params.multisample) {
-        s.n_samples = (int32_t)c->sample_ids.size();
-        build_pile_multi(s);
-        build_buckets(c, s);
+    if (!c->params.multisample) {
+        // single sample: the reads' projected bytes go straight into the tile layout
+        s.single = true;
+        std::vector<SRead> reads((size_t)nreads);
+        int64_t ri = 0;
+        for (size_t wi = 0; wi < s.windows.size(); wi++) {
+            Window& w = s.windows[wi];
+            const ContigReads& cr = contigs[wr[wi].contig];
+            w.read_begin = ri;
+            const int64_t goff = w.gbase + w.pad - w.w0;   // G = pos + goff
+            for (int64_t i = ranges[wi].first; i < ranges[wi].second; i++) {
+                reads[(size_t)ri++] = SRead{(int32_t)(cr.first[(size_t)i] + goff), (int32_t)(cr.last[(size_t)i] + goff),
+                                            cr.bytes.data() + cr.boff[(size_t)i], cr.neg[(size_t)i]};
+                const int64_t span = (int64_t)cr.last[(size_t)i] - cr.first[(size_t)i] + 1;
+                nbases += span > 0 ? span : 0;
+            }
+            w.read_end = ri;
+        }
+        s.n_reads = nreads;
+        s.n_read_bases = nbases;
+        if (build_single_layout(s, reads) != 0)
+            return set_error(c, NGSEP_E_UNSUPPORTED, "a pileup tile deeper than 16383 alignments");
+        c->stats.slot_bytes = 0;
+        c->stats.slot_size = 0;
     } else {
-        build_pile(s);
+        const int S = choose_slot_size(contigs);
+        s.slot_size = S;
+        // reads and slots (read-major SoA: the population kernel walks it in pending order)
+        int64_t nslots = 0;
+        for (size_t wi = 0; wi < s.windows.size(); wi++) {
+            const ContigReads& cr = contigs[wr[wi].contig];
+            for (int64_t i = ranges[wi].first; i < ranges[wi].second; i++) {
+                int64_t span = (int64_t)cr.last[i] - cr.first[i] + 1;
+                if (span < 1) span = 1;
+                nslots += (span + S - 1) / S;
+            }
+        }
+        s.h_slots.assign((size_t)nslots * S, 0);
+        s.h_reads.resize((size_t)nreads * 4);
+        int64_t slot = 0, ri = 0;
+        for (size_t wi = 0; wi < s.windows.size(); wi++) {
+            Window& w = s.windows[wi];
+            const ContigReads& cr = contigs[wr[wi].contig];
+            w.read_begin = ri;
+            const int64_t goff = w.gbase + w.pad - w.w0;   // G = pos + goff
+            for (int64_t i = ranges[wi].first; i < ranges[wi].second; i++) {
+                int64_t span = (int64_t)cr.last[i] - cr.first[i] + 1;
+                int64_t ns = span < 1 ? 1 : (span + S - 1) / S;
+                int64_t gfirst = cr.first[i] + goff;
+                s.h_reads[ri * 4 + 0] = (int32_t)gfirst;
+                s.h_reads[ri * 4 + 1] = (int32_t)(cr.last[i] + goff);
+                s.h_reads[ri * 4 + 2] = (int32_t)slot;
+                int32_t fl = cr.neg[i];
+                if (!cr.sample.empty()) fl |= ((int32_t)cr.rank[i] << 1) | (((int32_t)cr.sample[i] + 1) << 8);
+                s.h_reads[ri * 4 + 3] = fl;
+                if (span > 0) std::memcpy(&s.h_slots[(size_t)slot * S], &cr.bytes[cr.boff[i]], (size_t)span);
+                slot += ns;
+                nbases += span > 0 ? span : 0;
+                ri++;
+            }
+            w.read_end = ri;
+        }
+        s.n_reads = nreads;
+        s.n_slots = nslots;
+        s.n_read_bases = nbases;
+        s.n_samples = (int32_t)c->sample_ids.size();
+        if (build_pile_multi(s) != 0)
+            return set_error(c, NGSEP_E_UNSUPPORTED, "a sample's pileup tile is deeper than 65535 alignments");
+        build_buckets(c, s);
+        c->stats.slot_bytes = nslots * S;
+        c->stats.slot_size = S;
     }
     c->stats.read_bases = nbases;
-    c->stats.slot_bytes = nslots * S;
     c->stats.pile_bytes = s.pile_bytes;
     c->stats.tile_positions = s.tile;
     c->stats.tile_rows_max = s.tile_rows_max;
-    c->stats.slot_size = S;
+    const auto h1 = std::chrono::steady_clock::now();
     if (!c->dev) {
         std::string err;
         c->dev = device_create(c->device, err);
@@ -816,6 +943,15 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     }
     std::string err;
     if (device_upload(c->dev, s, err) != 0) return set_error(c, NGSEP_E_DEVICE, err);
+    c->stats.global_positions = s.g_len;
+    c->stats.n_tiles = s.n_tiles;
+    c->stats.layout_ms = std::chrono::duration<double, std::milli>(h1 - h0).count();
+    c->stats.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h1).count();
+    if (host_timing)
+        std::fprintf(stderr, "[ngsep host] layout %.1f ms, device upload %.1f ms (%lld reads, %lld tiles)\n",
+                     std::chrono::duration<double, std::milli>(h1 - h0).count(),
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h1).count(),
+                     (long long)nreads, (long long)s.n_tiles);
     // host mirrors are not needed any more
     std::vector<uint8_t>().swap(s.h_slots);
     std::vector<int32_t>().swap(s.h_reads);
@@ -828,6 +964,11 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     std::vector<int32_t>().swap(s.h_bseg);
     std::vector<int32_t>().swap(s.h_blb);
     std::vector<int32_t>().swap(s.h_bbase);
+    s.h_planes.release();
+    s.h_cpile.release();
+    s.h_seg.release();
+    s.h_segneg.release();
+    std::vector<int32_t>().swap(s.h_tseg);
     return NGSEP_OK;
 }
 

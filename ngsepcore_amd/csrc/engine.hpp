@@ -6,10 +6,14 @@
 // (PileupRecord -> CountsHelper -> VariantDiscoverySNVQAlgorithm) runs in kernels.hip.
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
+#include <atomic>
 #include <mutex>
 #include <utility>
 
@@ -123,13 +127,47 @@ struct ContigReads {
     }
 };
 
-// One raw alignment as received (kept while its same-start group is open)
-struct RawRead {
-    int32_t seq_id, first, flags, rg;
-    std::vector<int32_t> cigar;
-    std::string chars;     // empty = no characters
-    std::string quals;     // empty = no qualities ('*')
+// One alignment as the admission sweep sees it: a view into the caller's batch, or into the context's
+// carry storage when its same-start group is still open at the end of a batch
+struct ReadView {
+    int32_t seq_id, first, last, flags, rg;
+    const int32_t* cigar;
+    int32_t n_cigar;
+    const char* chars;     // nullptr = no characters (getReadCharacters() == null)
+    const char* quals;     // nullptr = no qualities ('*')
+    int32_t len;
 };
+struct CarryStore {        // owned copies of the open same-start group's reads
+    std::vector<int32_t> cigar;
+    std::string chars, quals;
+};
+
+// host worker threads: NGSEP_THREADS, else OMP_NUM_THREADS (the GPU box's CPU share), else the cores
+inline unsigned host_threads() {
+    static const unsigned n = [] {
+        const char* e = std::getenv("NGSEP_THREADS");
+        if (!e) e = std::getenv("OMP_NUM_THREADS");
+        long v = e ? std::atol(e) : (long)std::thread::hardware_concurrency();
+        return (unsigned)std::max(1L, std::min(v, 64L));
+    }();
+    return n;
+}
+// fn(lo, hi) over [0, n) in chunks of >= grain on the host threads (inline below 2 chunks)
+template <class F>
+void parallel_for(int64_t n, int64_t grain, F&& fn) {
+    if (n <= 0) return;
+    const int64_t nt = std::min<int64_t>(host_threads(), (n + grain - 1) / std::max<int64_t>(grain, 1));
+    if (nt <= 1) { fn((int64_t)0, n); return; }
+    const int64_t chunk = std::max<int64_t>(grain, (n + nt * 4 - 1) / (nt * 4));
+    std::atomic<int64_t> next{0};
+    auto work = [&]() {
+        for (int64_t lo; (lo = next.fetch_add(chunk)) < n;) fn(lo, std::min(n, lo + chunk));
+    };
+    std::vector<std::thread> th;
+    for (int64_t t = 1; t < nt; t++) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+}
 
 struct Device;   // kernels.hip
 struct CovDevice;   // coverage.hip
@@ -168,6 +206,28 @@ struct SiteStore {
     void swap(SiteStore& o) { std::swap(buf, o.buf); std::swap(n, o.n); std::swap(cap, o.cap); }
 };
 
+// uninitialised host array, filled in parallel (no serial zero-fill of GB-sized layouts)
+template <class T>
+struct HostArray {
+    T* p = nullptr;
+    size_t n = 0;
+    HostArray() = default;
+    HostArray(const HostArray&) = delete;
+    HostArray& operator=(const HostArray&) = delete;
+    HostArray(HostArray&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+    HostArray& operator=(HostArray&& o) noexcept { if (this != &o) { release(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; } return *this; }
+    ~HostArray() { release(); }
+    void alloc(size_t k) { release(); n = k; p = k ? static_cast<T*>(std::malloc(k * sizeof(T))) : nullptr; }
+    void release() { std::free(p); p = nullptr; n = 0; }
+};
+
+// a read of the single-sample layout: global [gfirst, glast] and its projected bytes
+struct SRead {
+    int32_t gfirst, glast;
+    const uint8_t* bytes;
+    uint8_t neg;                        // negative strand
+};
+
 struct Staged {            // everything resident for one run
     std::vector<Window> windows;
     int64_t g_len = 0;                  // global coordinate length
@@ -193,6 +253,14 @@ struct Staged {            // everything resident for one run
     std::vector<int32_t> h_perm, h_bseg, h_blb, h_bbase;
     int64_t nblk_b = 0;
     std::vector<uint8_t> h_ref;
+    // single-sample layout (engine.cpp build_single_layout): bit planes, position-major byte pile,
+    // per-tile read segments in pending order
+    HostArray<uint32_t> h_planes;
+    HostArray<uint8_t> h_cpile;
+    HostArray<uint32_t> h_seg;
+    HostArray<uint8_t> h_segneg;        // per segment: 1 = the read is on the negative strand
+    std::vector<int32_t> h_tseg;        // tile t's segments: h_seg[h_tseg[t] .. h_tseg[t+1])
+    bool single = false;                // the single-sample layout (else the multisample one)
 };
 
 }  // namespace ngsep
@@ -215,7 +283,10 @@ struct ngsep_ctx {
     int32_t cur_seq = -1;
     int32_t last_start = 0;
     int32_t cur_last = 0;
-    std::vector<ngsep::RawRead> ss_primary, ss_secondary;
+    std::vector<ngsep::ReadView> ss_primary, ss_secondary;   // the open same-start group
+    ngsep::CarryStore carry[2];                               // its reads' bytes across batches
+    int carry_cur = 0;
+    std::vector<ngsep::ReadView> to_project;                 // admitted, projection pending (batch end)
     ngsep::ContigReads contig;
     bool query_found = false;
     bool query_done = false;
@@ -243,7 +314,7 @@ struct ngsep_ctx {
 namespace ngsep {
 // engine.cpp
 int set_error(ngsep_ctx* c, int code, const std::string& msg);
-void project_read(const ngsep_ctx* c, const RawRead& r, int32_t last, std::vector<uint8_t>& out);
+void project_read(const ngsep_ctx* c, const ReadView& r, uint8_t* out);
 int stage_contig_reads(ngsep_ctx* c, ContigReads& cr, bool run_now);
 int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs);
 int run_device(ngsep_ctx* c, double* elapsed_ms);

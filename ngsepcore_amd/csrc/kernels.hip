@@ -7,15 +7,13 @@
 //        AlignmentsPileupGenerator.processCurrentPosition (discovery/AlignmentsPileupGenerator.java:475-498)
 //        reduced to the fact that decides whether SNVQ can call a variant there ("why
 //        pruning is exact").
-//   KT  k_tile_pileup<MODE> : the same over the byte pile (other tile widths; MODE 1 = dump mode).
-//   KB  kb_planes : the bit planes from the byte pile, once per staged batch.
+//   KQ  k_queue_all : every in-window position queued (dump mode, runs without the exact pruning).
 //   KP  k_posterior : exact CountsHelper tally (pending-list order, bit-exact fp64), posterior and
 //        SNVQ call of the queued candidates (discovery/CountsHelper.java:83-95,209-251,410-495,
 //        VariantDiscoverySNVQAlgorithm.java:100-243, SingleSampleVariantPileupListener.java:213-232);
 //        records go to position buckets.
 //   KO  ko_fused : position order of the records (rank per bucket) and their (sequence, position).
 //   KTM / KPM k_tile_pileup_multi / k_posterior_multi : MultisampleVariantsDetector.
-//   KL  kl_read_index : per 64-position block, first read that can cover it (binary search).
 //
 // HBM-bound integer/byte work: no MFMA.  Layout and roofline: DESIGN.md.
 #include <hip/hip_runtime.h>
@@ -81,15 +79,17 @@ struct Device {
     bool time_posterior = std::getenv("NGSEP_TIME_POSTERIOR") != nullptr;
     bool time_scan = std::getenv("NGSEP_NO_SCAN_TIMING") == nullptr;   // diagnostics: without KT's events
     hipEvent_t ev[4] = {};
-    uint8_t* d_slots = nullptr;
-    uint8_t* d_pile = nullptr;
-    uint32_t* d_planes = nullptr;    // bit planes of the pile (KB), 0 when the tile width has none
+    uint8_t* d_slots = nullptr;      // multisample: read-major SoA
+    uint8_t* d_pile = nullptr;       // single sample: position-major byte pile; multisample: per-sample blocks
+    uint32_t* d_planes = nullptr;    // single sample: bit planes of the pile (KT)
+    uint32_t* d_seg = nullptr;       // single sample: per-tile read segments in pending order (KP)
+    uint8_t* d_segneg = nullptr;     // their strands
+    int32_t* d_tseg = nullptr;       // tile t's segments: [tseg[t], tseg[t+1])
     int4* d_wins = nullptr;          // windows {global start of w0, w0, seq_id, wlen}, ascending (KO maps records)
     int32_t n_wins = 0;
     int32_t planes_W = 0;            // words per plane row (T / 32)
     int4* d_reads = nullptr;
     uint8_t* d_ref = nullptr;
-    int32_t* d_lb = nullptr;
     TileInfo* d_tinfo = nullptr;
     uint16_t* d_rows = nullptr;      // multisample: rows per (tile, sample)
     int64_t* d_toff = nullptr;       // multisample: block offset per tile
@@ -111,7 +111,7 @@ struct Device {
     unsigned long long* d_counters = nullptr;
     unsigned long long* h_counters = nullptr;
     int64_t cap_sites = 0;
-    int64_t n_units = 0, n_slots = 0, n_lb = 0, n_reads = 0, g_len = 0, n_tiles = 0;
+    int64_t n_units = 0, n_slots = 0, n_reads = 0, g_len = 0, n_tiles = 0;
     int32_t slot_size = 0, max_span = 0, pad = 0, tile = 512, log2_tile = 9;
     int64_t last_n_sites = 1024;
     int64_t last_hard = 0;
@@ -166,13 +166,16 @@ static_assert(sizeof(QueueSite) == 8, "QueueSite layout");
 // KP: exact tally + posterior + SNVQ call of the queued candidates (one wavefront per site)
 // ------------------------------------------------------------------------------------------
 // CountsHelper.calculateCountsSNV/updateCounts (discovery/CountsHelper.java:83-95,209-251) over the
-// reads covering gpos in pending-list order (the order of the read table), so the fp64 sums are
-// bit-identical to the reference's; then getPosteriorProbabilities (:410-495),
-// VariantDiscoverySNVQAlgorithm.discoverSNV (:100-243) and the listener filters
-// (SingleSampleVariantPileupListener.java:213-232).
-// The 64 lanes fetch 64 consecutive reads' codes at once (the memory round trips are what a site
-// costs); integer counts come from ballots, and the fp64 sums are then added in lane (= read) order,
-// wave-uniformly.  Lane 0 appends each emitted record to the bucket of its position (KO orders them).
+// reads covering gpos in pending-list order, so the fp64 sums are bit-identical to the reference's;
+// then getPosteriorProbabilities (:410-495), VariantDiscoverySNVQAlgorithm.discoverSNV (:100-243) and
+// the listener filters (SingleSampleVariantPileupListener.java:213-232).
+// The reads of gpos's tile are its segments, stored in pending-list order (row << 18 | a << 9 | b, the
+// strand in a parallel bitmap); the site's codes are one contiguous column of the position-major byte
+// pile (rows_t bytes at off_t + p * rows_t).  Lane j takes segment j of a 64-segment chunk: covered
+// (a <= p <= b) -> its row's code.  A site therefore reads its tile's segment list (~0.5 KB at 30x) and
+// one column line, not one cache line per read.  Integer counts come from ballots; the valid codes are
+// compacted in LDS in lane (= pending) order and ten lanes each add one of the ten log-likelihood sums.
+// Lane 0 appends each emitted record to the bucket of its position (KO orders them).
 __device__ __forceinline__ double readlane_d(double v, int l) {
     const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
@@ -182,21 +185,14 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 
 constexpr int kPostWaves = 4;
 __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* __restrict__ queue, const unsigned long long* qn,
-                                                   int64_t qcap, const int4* __restrict__ reads, int64_t n_reads,
-                                                   const int32_t* __restrict__ lb, const uint8_t* __restrict__ slots,
-                                                   int32_t S, const LikTables* __restrict__ tabs, GenotypeParams gp,
+                                                   int64_t qcap, const TileInfo* __restrict__ tinfo,
+                                                   const int32_t* __restrict__ tseg, const uint32_t* __restrict__ seg,
+                                                   const uint8_t* __restrict__ segneg, const uint8_t* __restrict__ cpile,
+                                                   int32_t log2T, const LikTables* __restrict__ tabs, GenotypeParams gp,
                                                    ngsep_site_out* __restrict__ brec, int32_t* __restrict__ bcount,
-                                                   int shift, int32_t bcap, unsigned long long* __restrict__ stamps) {
-#ifdef NGSEP_KP_STAMPS
-    // diagnostics build: cycles per phase summed over sites, walk iterations, valid reads, wave spans
-    unsigned long long st_w0 = __builtin_amdgcn_s_memtime(), st_a = 0, st_b = 0, st_c = 0;
-    int32_t st_it = 0, st_nv = 0, st_sites = 0;
-#define KP_STAMP(v) v = __builtin_amdgcn_s_memtime()
-#else
-#define KP_STAMP(v)
-#endif
+                                                   int shift, int32_t bcap) {
     __shared__ double s_t[3][32];
-    __shared__ uint8_t s_code[kPostWaves][64];      // a chunk's valid codes in read order
+    __shared__ uint8_t s_code[kPostWaves][64];      // a chunk's valid codes in pending order
     __shared__ uint32_t s_rec[kPostWaves][sizeof(ngsep_site_out) / 4];   // the record awaiting its bucket slot
     if (threadIdx.x < 96)
         s_t[threadIdx.x >> 5][threadIdx.x & 31] =
@@ -204,6 +200,7 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int32_t Tm = (1 << log2T) - 1;
     int64_t n = (int64_t)*qn;
     if (n > qcap) n = qcap;
     const int64_t nwaves = (int64_t)gridDim.x * kPostWaves;
@@ -227,53 +224,45 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         pending = false;
     };
-    auto load_h = [&](int64_t r0) -> int4 {
-        const int64_t r = r0 + lane;
-        return r < n_reads ? reads[r] : int4{INT32_MAX, 0, 0, 0};
-    };
-    auto load_code = [&](const int4& h, int32_t g) -> uint32_t {
-        const bool cov = h.x <= g && h.y >= g;
-        const int32_t o = cov ? g - h.x : 0;
-        return cov ? (uint32_t)slots[(int64_t)(h.z + o / S) * S + (o % S)] : 0u;
-    };
-    // software pipeline over this wave's sites: the next site's queue entry and read-index entry are
-    // loaded during the current site's walk, its first 64 reads during the current posterior, the
-    // entry after next meanwhile, so a site waits on one dependent load (its read bytes)
+    // software pipeline over this wave's sites: the next site's queue entry, tile descriptor and segment
+    // range load during the current site's walk, its first segment chunk during the current posterior
     int64_t i = (int64_t)blockIdx.x * kPostWaves + wv;
     QueueSite qs = i < n ? queue[i] : QueueSite{0, 0};
-    int32_t lb_c = i < n ? lb[qs.gpos >> 6] : 0, lb_n = 0;
-    int4 h_c = i < n ? load_h(lb_c) : int4{INT32_MAX, 0, 0, 0};
-    QueueSite qs_n = i + nwaves < n ? queue[i + nwaves] : QueueSite{0, 0}, qs_nn{0, 0};
-    for (; i < n; i += nwaves, qs = qs_n, qs_n = qs_nn, lb_c = lb_n) {
-#ifdef NGSEP_KP_STAMPS
-        unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
-        KP_STAMP(t0);
-        st_sites++;
-#endif
+    int32_t t_c = qs.gpos >> log2T;
+    TileInfo ti_c = i < n ? tinfo[t_c] : TileInfo{0, 0, 0};
+    int32_t s0_c = i < n ? tseg[t_c] : 0, s1_c = i < n ? tseg[t_c + 1] : 0;
+    uint32_t sg_c = s0_c + lane < s1_c ? seg[s0_c + lane] : 0u;
+    QueueSite qs_n = i + nwaves < n ? queue[i + nwaves] : QueueSite{0, 0};
+    for (; i < n; i += nwaves) {
         const int32_t gpos = __builtin_amdgcn_readfirstlane(qs.gpos);
         const uint32_t rc = (uint32_t)__builtin_amdgcn_readfirstlane(qs.rc);
-        const int64_t r_first = __builtin_amdgcn_readfirstlane(lb_c);
+        const int32_t p = gpos & Tm;
+        const int32_t rows = __builtin_amdgcn_readfirstlane(ti_c.rows);
+        const int64_t coff = ((int64_t)__builtin_amdgcn_readfirstlane((int32_t)(ti_c.off >> 32)) << 32 |
+                              (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)ti_c.off)) + (int64_t)p * rows;
+        const int32_t s0 = __builtin_amdgcn_readfirstlane(s0_c), s1 = __builtin_amdgcn_readfirstlane(s1_c);
+        // next site's descriptor
         const bool more = i + nwaves < n;
-        lb_n = more ? lb[qs_n.gpos >> 6] : 0;
-        qs_nn = i + 2 * nwaves < n ? queue[i + 2 * nwaves] : QueueSite{0, 0};
-        int4 h = h_c;
-        uint32_t code = load_code(h, gpos);
-        if (gp.ablate & 16) { h_c = more ? load_h(lb_n) : int4{INT32_MAX, 0, 0, 0}; continue; }   // diagnostics
+        const int32_t t_n = qs_n.gpos >> log2T;
+        const TileInfo ti_n = more ? tinfo[t_n] : TileInfo{0, 0, 0};
+        const int32_t s0_n = more ? tseg[t_n] : 0, s1_n = more ? tseg[t_n + 1] : 0;
+        const QueueSite qs_nn = i + 2 * nwaves < n ? queue[i + 2 * nwaves] : QueueSite{0, 0};
         int32_t total = 0;
         int32_t cnt[4] = {0, 0, 0, 0};
         int32_t sc[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
         double acc = 0;                                   // this lane's log-likelihood sum
-        // reads that can cover gpos start at lb[gpos/64] (every earlier read ends before gpos); the
-        // table is sorted by start, so the first read starting after gpos ends the walk
-        for (int64_t r0 = r_first;;) {
-#ifdef NGSEP_KP_STAMPS
-            st_it++;
-#endif
-            const bool in = h.x <= gpos;
+        uint32_t sg = sg_c;
+        for (int32_t j0 = s0; j0 < s1; j0 += 64) {
+            const int32_t j = j0 + lane;
+            const uint32_t sg_next = j + 64 < s1 ? seg[j + 64] : 0u;
+            const int32_t a = (int32_t)((sg >> 9) & 511u), b = (int32_t)(sg & 511u), row = (int32_t)(sg >> 18);
+            const bool cov = j < s1 && a <= p && p <= b;
+            const uint32_t code = cov ? (uint32_t)cpile[coff + row] : 0u;
+            const bool neg = cov && segneg[j] != 0;
             total += __popcll(__ballot(code != 0));                       // CountsHelper.java:210
             const bool valid = (code & 0x80u) != 0;                       // q<=3 or not A/C/G/T: not counted (:214-221)
             const uint32_t al = (code >> 5) & 3u;
-            const unsigned long long negm = __ballot(h.w & 1);
+            const unsigned long long negm = __ballot(neg);
 #pragma unroll
             for (int t = 0; t < 4; t++) {
                 const unsigned long long m = __ballot(valid && al == (uint32_t)t);
@@ -282,12 +271,9 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
                 sc[t][1] += __popcll(m & ~negm);
             }
             const unsigned long long mv = __ballot(valid);
-#ifdef NGSEP_KP_STAMPS
-            st_nv += __popcll(mv);
-#endif
-            // updateCounts (:231-248) in read order: the valid codes are compacted in LDS, then each
-            // of the ten sum lanes adds its term of every read in turn (the loads do not depend on the
-            // sums, so they pipeline; each sum's order of additions is the reference's)
+            // updateCounts (:231-248) in pending order: the valid codes are compacted in LDS, then each
+            // of the ten sum lanes adds its term of every read in turn (each sum's order of additions is
+            // the reference's)
             const int32_t nv = __popcll(mv);
             const int32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mv >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mv, 0u));
             if (valid) s_code[wv][rank] = (uint8_t)code;
@@ -296,8 +282,8 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             if (lane < 10) {
 #pragma unroll 4
-                for (int32_t j = 0; j < nv; j++) {
-                    const uint32_t cd = s_code[wv][j];
+                for (int32_t k = 0; k < nv; k++) {
+                    const uint32_t cd = s_code[wv][k];
                     int q = (int)(cd & 31u);
                     q = q > gp.max_q ? gp.max_q : q;                      // -maxBaseQS (:217-219)
                     acc += s_t[((am >> ((cd >> 5) & 3u)) & 1u) ? tm : 2][q];
@@ -306,17 +292,15 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (__ballot(!in)) break;
-            r0 += 64;
-            if (r0 >= n_reads) break;
-            h = load_h(r0);
-            code = load_code(h, gpos);
+            sg = sg_next;
         }
-        h_c = more ? load_h(lb_n) : int4{INT32_MAX, 0, 0, 0};
-#ifdef NGSEP_KP_STAMPS
-        KP_STAMP(t1);
-        st_a += t1 - t0;
-#endif
+        // the next site's first segment chunk loads during this site's posterior
+        sg_c = more && s0_n + lane < s1_n ? seg[s0_n + lane] : 0u;
+        qs = qs_n;
+        qs_n = qs_nn;
+        ti_c = ti_n;
+        s0_c = s0_n;
+        s1_c = s1_n;
         if (total == 0 || (gp.ablate & 8)) continue;                      // VariantDiscoverySNVQAlgorithm.java:101-103
         const bool callable = (rc & 0x80u) != 0;
         int8_t genotype = -1, alt = -1, third = -1, nal = 0;
@@ -355,12 +339,12 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
             double probMax = readlane_d(post, 4 * refIdx);
             const double refProb = probMax;
 #pragma unroll
-            for (int p = 0; p < 10; p++) {
-                const double g = readlane_d(gsum, p);
+            for (int q = 0; q < 10; q++) {
+                const double g = readlane_d(gsum, q);
                 if (g > probMax + 0.01) {
                     probMax = g;
-                    I = (int)((0x3221110000ull >> (4 * p)) & 15u);
-                    J = (int)((0x3323213210ull >> (4 * p)) & 15u);
+                    I = (int)((0x3221110000ull >> (4 * q)) & 15u);
+                    J = (int)((0x3323213210ull >> (4 * q)) & 15u);
                 }
             }
             // maxP = post(I,J) [+ post(J,I)] is the pair sum the scan kept (the initial one: post(ref,ref))
@@ -380,10 +364,6 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
             }
             if (keep && gp.min_quality > gq) keep = false;
         }
-#ifdef NGSEP_KP_STAMPS
-        KP_STAMP(t2);
-        st_b += t2 - t1;
-#endif
         if (!keep && !gp.dump_all) continue;
         // the record goes to its position bucket (KO orders each bucket; no global reservation).  The
         // slot's atomic is issued now and the record is staged in LDS; it is stored at the wave's next
@@ -419,27 +399,8 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
             pend_bk = bk;
             pending = true;
         }
-#ifdef NGSEP_KP_STAMPS
-        KP_STAMP(t3);
-        st_c += t3 - t2;
-#endif
     }
     flush_pending();
-#ifdef NGSEP_KP_STAMPS
-    if (lane == 0 && stamps) {
-        const unsigned long long w1 = __builtin_amdgcn_s_memtime();
-        atomicAdd(&stamps[0], st_a);
-        atomicAdd(&stamps[1], st_b);
-        atomicAdd(&stamps[2], st_c);
-        atomicAdd(&stamps[3], (unsigned long long)st_it);
-        atomicAdd(&stamps[4], (unsigned long long)st_nv);
-        atomicAdd(&stamps[5], (unsigned long long)st_sites);
-        atomicAdd(&stamps[6], w1 - st_w0);
-        atomicMin(&stamps[7], st_w0);
-        atomicMax(&stamps[8], w1);
-        atomicAdd(&stamps[9], 1ull);
-    }
-#endif
 }
 
 
@@ -465,10 +426,6 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
 //   phase 3  a candidate the bounds prove hom-ref is dropped; the others are staged in LDS and
 //            queued for k_posterior (one global reservation per workgroup).
 // No LDS traffic on the streamed bytes, no workgroup barriers inside the tile loop.
-#ifndef NGSEP_KT_CHUNK
-#define NGSEP_KT_CHUNK 16
-#endif
-constexpr int kScanChunk = NGSEP_KT_CHUNK;   // wave-loads (16 B per lane) in flight per chunk (build-time tuning)
 constexpr int kScanWaves = kScanThreads / 64;
 constexpr int kWaveQ = 512;             // survivors staged per wave before a global reservation
 
@@ -516,242 +473,13 @@ __device__ __forceinline__ void wave_flush(ScanShared& sh, int wv, int lane, int
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int MODE>
 #ifndef NGSEP_KT_WAVES_PER_EU
 #define NGSEP_KT_WAVES_PER_EU 4      // build-time tuning: resident waves per SIMD the register budget targets
 #endif
 #ifndef NGSEP_KT16_WAVES_PER_EU
 #define NGSEP_KT16_WAVES_PER_EU 3    // the same for the 512-position plane tiles (118 VGPRs at 3: 4 waves resident)
 #endif
-__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(NGSEP_KT_WAVES_PER_EU)))
-void k_tile_pileup(
-    const u32x4* __restrict__ pile, const TileInfo* __restrict__ tinfo, const uint8_t* __restrict__ ref,
-    int32_t log2T, int64_t n_tiles, const LikTables* __restrict__ tabs, GenotypeParams gp,
-    QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap,
-    int32_t* __restrict__ bcount, int64_t nb) {
-    __shared__ ScanShared sh;
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // KP's position buckets start empty (KT precedes KP on the stream)
-    for (int64_t i = (int64_t)blockIdx.x * kScanThreads + threadIdx.x; i < nb; i += (int64_t)gridDim.x * kScanThreads) bcount[i] = 0;
-    if (threadIdx.x < 64) sh.w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
-    __syncthreads();
-    const int log2U = log2T - 4;
-    const uint32_t U = 1u << log2U;
-    const int col = lane & (int)(U - 1);
-    const bool lead = lane < (int)U;               // phase-0 lane of its column: reports the column's candidates
-    const bool bound_on = MODE == 0 && gp.use_bound;
-    const long long th = tabs->t_het, to = tabs->t_homo;
-    const int32_t maxq = gp.max_q;
-    int32_t qn = 0;                                 // wave-uniform count of staged survivors
-    unsigned long long ncand = 0;
-    uint32_t nexact = 0;                            // wave passes of the exact integer bound (statistics)
-    const int64_t nwaves = (int64_t)gridDim.x * kScanWaves;
-    const int64_t t0 = (int64_t)blockIdx.x * kScanWaves + wv;
-    TileInfo nxt = t0 < n_tiles ? tinfo[t0] : TileInfo{0, 0, 0};
-    for (int64_t t = t0; t < n_tiles; t += nwaves) {
-        if (gp.ablate & 4) break;
-        const TileInfo ti = nxt;
-        if (t + nwaves < n_tiles) nxt = tinfo[t + nwaves];    // the next descriptor is in flight meanwhile
-        const int32_t rows = __builtin_amdgcn_readfirstlane(ti.rows);
-        if (rows == 0) continue;
-        const int32_t nunits = rows << log2U;
-        const int64_t off = ((int64_t)__builtin_amdgcn_readfirstlane((int32_t)(ti.off >> 32)) << 32) |
-                            (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)ti.off);
-        const u32x4* blk = pile + (off >> 4);
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)blk, 0, nunits * 16, 0x00020000);
-        const int32_t tstart = (int32_t)(t << log2T);
-        const u32x4 rc = *reinterpret_cast<const u32x4*>(ref + tstart + col * 16);
-        uint32_t ok;
-        {
-            auto okf = [](uint32_t v) -> uint32_t {
-                return nib4(MODE == 0 ? (v & 0x80808080u) : ((((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u));
-            };
-            ok = okf(rc.x) | (okf(rc.y) << 4) | (okf(rc.z) << 8) | (okf(rc.w) << 12);
-        }
-        // MODE 0 counts valid calls (cv) and non-reference valid calls (ca) per position, byte-wise
-        // (SWAR): a column holds <= rows_t <= 255 calls, so no byte carries into its neighbour, and
-        // the candidates are the positions with ca > 0.  Deeper tiles (and MODE 1) OR hit bits.
-        const bool counted = MODE == 0 && rows <= 255;
-        uint32_t hits = 0;
-        uint32_t cv0 = 0, cv1 = 0, cv2 = 0, cv3 = 0, ca0 = 0, ca1 = 0, ca2 = 0, ca3 = 0;
-        auto cnt = [](uint32_t w, uint32_t& cv, uint32_t& ca) {
-            const uint32_t v = w & 0x80808080u;                             // valid calls
-            const uint32_t n = ((w & 0x60606060u) + 0x60606060u) & v;       // ... of an allele other than the reference
-            cv += v >> 7;
-            ca += n >> 7;
-        };
-        // stream the block: chunks of kScanChunk wave-loads (8 KiB per wave) issued back to back;
-        // loads past the block's end return zeros, which hold no calls
-        if (counted) {
-            for (int32_t u0 = 0; u0 < nunits; u0 += kScanChunk * 64) {
-                u32x4 R[kScanChunk];
-#pragma unroll
-                for (int j = 0; j < kScanChunk; j++)
-                    R[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u0 + j * 64 + lane) * 16, 0, 0));
-#pragma unroll
-                for (int j = 0; j < kScanChunk; j++) {
-                    cnt(R[j].x, cv0, ca0); cnt(R[j].y, cv1, ca1); cnt(R[j].z, cv2, ca2); cnt(R[j].w, cv3, ca3);
-                }
-            }
-            for (int s = (int)U; s < 64; s <<= 1) {
-                cv0 += __shfl_xor(cv0, s, 64); cv1 += __shfl_xor(cv1, s, 64);
-                cv2 += __shfl_xor(cv2, s, 64); cv3 += __shfl_xor(cv3, s, 64);
-                ca0 += __shfl_xor(ca0, s, 64); ca1 += __shfl_xor(ca1, s, 64);
-                ca2 += __shfl_xor(ca2, s, 64); ca3 += __shfl_xor(ca3, s, 64);
-            }
-            auto nz = [](uint32_t w) -> uint32_t { return nib4((((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u); };
-            hits = nz(ca0) | (nz(ca1) << 4) | (nz(ca2) << 8) | (nz(ca3) << 12);
-        } else {
-            for (int32_t u0 = 0; u0 < nunits; u0 += kScanChunk * 64) {
-                u32x4 R[kScanChunk];
-#pragma unroll
-                for (int j = 0; j < kScanChunk; j++)
-                    R[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u0 + j * 64 + lane) * 16, 0, 0));
-#pragma unroll
-                for (int j = 0; j < kScanChunk; j++) hits |= unit_hits<MODE>(R[j]);
-            }
-            for (int s = (int)U; s < 64; s <<= 1) hits |= __shfl_xor(hits, s, 64);
-        }
-        uint32_t cm = hits & ok;
-        if (lead) ncand += (unsigned long long)__popc(cm);
-        if (gp.ablate & 1) continue;                                  // diagnostics: scan only
-        const bool bound = bound_on && counted;                       // 32-bit halves of the sums cannot overflow either
-        if (bound && __ballot(cm != 0)) {
-            // count bound: with nr reference and na other valid calls at the position, the exact
-            // integer sums below satisfy R >= nr * (smallest addend) and X <= na * (largest), so a
-            // candidate that passes with those is hom-ref without walking its column.  Most candidates
-            // are one or two sequencing errors in a deep pileup and end here.
-            const u32x4 nref = {cv0 - ca0, cv1 - ca1, cv2 - ca2, cv3 - ca3}, nalt = {ca0, ca1, ca2, ca3};
-            uint32_t c = cm;
-            while (c) {
-                const int k = __builtin_ctz(c);
-                c &= c - 1u;
-                const long long nr = (unit_dword(nref, k >> 2) >> (8 * (k & 3))) & 0xFFu;
-                const long long na = (unit_dword(nalt, k >> 2) >> (8 * (k & 3))) & 0xFFu;
-                if (nr * tabs->c_r1 - na * tabs->c_x1 > th && nr * tabs->c_r2 - na * tabs->c_x2 > to &&
-                    nr * tabs->c_r2 - na * tabs->c_x1 > th)
-                    cm &= ~(1u << k);
-            }
-        }
-        // wave-uniform candidate loop: the lanes of one column hold the same mask, so they visit the
-        // same position in the same iteration and their partial sums meet in the shuffles below
-        while (__ballot(cm != 0)) {
-            const bool has = cm != 0;
-            const int k = has ? __builtin_ctz(cm) : 0;
-            cm &= cm - 1u;
-            const int sel = k >> 2, shb = 8 * (k & 3);
-            bool keep = has;
-            if (bound) {
-                unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;   // indexed by allele XOR reference
-                auto add = [&](const u32x4 d) {
-                    const uint32_t cd = (unit_dword(d, sel) >> shb) & 0xFFu;
-                    if (cd & 0x80u) {
-                        const uint32_t a = (cd >> 5) & 3u;
-                        int q = (int)(cd & 31u);
-                        q = q > maxq ? maxq : q;
-                        const unsigned long long w = sh.w[a == 0 ? 0 : 1][q];
-                        a0 += a == 0 ? w : 0ull;
-                        a1 += a == 1 ? w : 0ull;
-                        a2 += a == 2 ? w : 0ull;
-                        a3 += a == 3 ? w : 0ull;
-                    }
-                };
-                nexact++;
-                for (int32_t u0 = 0; u0 < nunits; u0 += kScanChunk * 64) {   // re-read (L2-warm)
-                    u32x4 R[kScanChunk];
-#pragma unroll
-                    for (int j = 0; j < kScanChunk; j++)
-                        R[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u0 + j * 64 + lane) * 16, 0, 0));
-#pragma unroll
-                    for (int j = 0; j < kScanChunk; j++) add(R[j]);
-                }
-                for (int s = (int)U; s < 64; s <<= 1) {
-                    a0 += __shfl_xor(a0, s, 64);
-                    a1 += __shfl_xor(a1, s, 64);
-                    a2 += __shfl_xor(a2, s, 64);
-                    a3 += __shfl_xor(a3, s, 64);
-                }
-                // hom-ref if, for every other genotype G, the lower bound of L[r][r]-L[G] keeps
-                // P(G) (het: P(x,y)+P(y,x)) <= P(r,r)  (DESIGN.md "hom-ref bound").
-                // het (r,x): R1 - X1[x];  hom (x,x): R2 - X2[x];  het (x,y), x,y != r: R2 - X1[x] - X1[y]
-                const long long R1 = (long long)(a0 & 0xFFFFFFFFull), R2 = (long long)(a0 >> 32);
-                const long long x1 = (long long)(a1 & 0xFFFFFFFFull), y1 = (long long)(a2 & 0xFFFFFFFFull);
-                const long long z1 = (long long)(a3 & 0xFFFFFFFFull);
-                const long long x2 = (long long)(a1 >> 32), y2 = (long long)(a2 >> 32), z2 = (long long)(a3 >> 32);
-                const bool drop = (R1 - x1 > th) && (R1 - y1 > th) && (R1 - z1 > th) &&
-                                  (R2 - x2 > to) && (R2 - y2 > to) && (R2 - z2 > to) &&
-                                  (R2 - x1 - y1 > th) && (R2 - x1 - z1 > th) && (R2 - y1 - z1 > th);
-                keep = has && !drop;
-            }
-            const bool emit = keep && lead;
-            const unsigned long long m = __ballot(emit);
-            if (!m) continue;
-            const int32_t nm = __popcll(m);
-            if (qn + nm > kWaveQ) { wave_flush(sh, wv, lane, qn, queue, counters, qcap); qn = 0; }
-            if (emit) {
-                const int32_t idx = qn + __popcll(m & ((1ull << lane) - 1ull));
-                const uint32_t rcode = (unit_dword(rc, sel) >> shb) & 0xFFu;
-                sh.q[wv][idx] = QueueSite{tstart + col * 16 + k, (int32_t)rcode};
-            }
-            qn += nm;
-        }
-    }
-    // one global reservation per workgroup for what its waves staged; one statistics atomic
-    for (int s = 1; s < 64; s <<= 1) ncand += __shfl_xor(ncand, s, 64);
-    if (lane == 0) { sh.qn[wv] = qn; sh.ncand[wv] = ncand; sh.nexact[wv] = nexact; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int32_t tot = 0;
-        unsigned long long nc = 0, ne = 0;
-        for (int w = 0; w < kScanWaves; w++) { sh.qbase[w] = tot; tot += sh.qn[w]; nc += sh.ncand[w]; ne += sh.nexact[w]; }
-        if (ne) atomicAdd(&counters[3], ne);
-        const unsigned long long base = tot ? atomicAdd(&counters[2], (unsigned long long)tot) : 0ull;
-        for (int w = 0; w < kScanWaves; w++) sh.qbase[w] += (int32_t)base;   // queue indices fit 31 bits (g_len < 2^31)
-        if (nc) atomicAdd(&counters[1], nc);
-    }
-    __syncthreads();
-    {
-        const int64_t base = sh.qbase[wv];
-        for (int i = lane; i < qn; i += 64)
-            if (base + i < qcap) queue[base + i] = sh.q[wv][i];
-    }
-}
 
-
-// ------------------------------------------------------------------------------------------
-// KB: bit planes of the pile (once per staged batch, for KT's scan).  Row r of a tile holds W = T/32
-//     words of "valid call" bits, then W words of "valid call of another allele" bits; bit j of word
-//     w is position 32w + j of the tile.  The planes of a tile start at word (pile offset / 16).
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void kb_planes(const uint8_t* __restrict__ pile, const TileInfo* __restrict__ tinfo,
-                                                 int64_t n_tiles, int32_t T, uint32_t* __restrict__ planes) {
-    const int lane = threadIdx.x & 63;
-    const int W = T >> 5;
-    const int64_t nw = (int64_t)gridDim.x * 4;
-    for (int64_t t = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6; t < n_tiles; t += nw) {
-        const TileInfo ti = tinfo[t];
-        uint32_t* dst = planes + (ti.off >> 4);
-        for (int64_t idx = lane; idx < (int64_t)ti.rows * W; idx += 64) {
-            const int64_t r = idx / W;
-            const int w = (int)(idx % W);
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(pile + ti.off + r * T + 32 * w);
-            uint32_t v = 0, x = 0;
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const uint32_t d = src[k];
-#pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    const uint32_t c = (d >> (8 * b)) & 0xFFu;
-                    v |= ((c >> 7) & 1u) << (4 * k + b);
-                    x |= (((c & 0x80u) && (c & 0x60u)) ? 1u : 0u) << (4 * k + b);
-                }
-            }
-            dst[r * 2 * W + w] = v;
-            dst[r * 2 * W + W + w] = x;
-        }
-    }
-}
 
 // ------------------------------------------------------------------------------------------
 // KT (bit planes): the single-sample scan over the planes instead of the byte pile -- a quarter of
@@ -988,11 +716,13 @@ void k_tile_planes(const uint32_t* __restrict__ planes, const uint8_t* __restric
                 if (bound && gp.exact_bound) {
                     nexact++;
                     unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+                    const uint32_t ra = (ref_code(p) >> 5) & 3u;
                     for (int g = 0; g < ng; g++) {
                         const int r = g * 64 + lane;
-                        const uint32_t cd = r < rows ? (uint32_t)pile[off + (int64_t)r * T + p] : 0u;
+                        // the position-major byte pile: position p's rows are one contiguous column
+                        const uint32_t cd = r < rows ? (uint32_t)pile[off + (int64_t)p * rows + r] : 0u;
                         if (cd & 0x80u) {
-                            const uint32_t a = (cd >> 5) & 3u;
+                            const uint32_t a = ((cd >> 5) & 3u) ^ ra;     // 0: a reference call
                             int q = (int)(cd & 31u);
                             q = q > maxq ? maxq : q;
                             const unsigned long long wt = sh.w[a == 0 ? 0 : 1][q];
@@ -1039,6 +769,31 @@ void k_tile_planes(const uint32_t* __restrict__ planes, const uint8_t* __restric
         const int64_t base = sh.qbase[wv];
         for (int i = lane; i < qn; i += 64)
             if (base + i < qcap) queue[base + i] = sh.q[wv][i];
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// KQ: every in-window position queued (dump mode, and runs without the exact pruning: -h > 0.1 or
+//     prune_candidates = 0); KP skips positions without a pileup (VariantDiscoverySNVQAlgorithm.java:101-103)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_queue_all(const uint8_t* __restrict__ ref, int64_t g_len, QueueSite* __restrict__ queue,
+                                                   unsigned long long* __restrict__ counters, int64_t qcap,
+                                                   int32_t* __restrict__ bcount, int64_t nb) {
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += stride) bcount[i] = 0;
+    const int64_t nwave = (g_len + 63) / 64;
+    for (int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nwave; w += stride >> 6) {
+        const int64_t g = w * 64 + lane;
+        const uint32_t rc = g < g_len ? (uint32_t)ref[g] : 0u;
+        const unsigned long long m = __ballot(rc != 0);
+        if (!m) continue;
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(&counters[2], (unsigned long long)__popcll(m));
+        base = __shfl(base, 0, 64);
+        const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (rc != 0 && (int64_t)(base + rank) < qcap) queue[base + rank] = QueueSite{(int32_t)g, (int32_t)rc};
+        if (lane == 0) atomicAdd(&counters[1], (unsigned long long)__popcll(m));
     }
 }
 
@@ -1606,23 +1361,6 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
 }
 
 // ------------------------------------------------------------------------------------------
-// KL: lb[k] = first read index whose gfirst >= 64k - pad + 1
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void kl_read_index(const int4* __restrict__ reads, int64_t n_reads,
-                                                     int32_t* __restrict__ lb, int64_t n_lb, int32_t pad) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n_lb) return;
-    const int64_t key = k * 64 - pad + 1;
-    int64_t lo = 0, hi = n_reads;
-    while (lo < hi) {
-        int64_t mid = (lo + hi) >> 1;
-        if ((int64_t)reads[mid].x < key) lo = mid + 1;
-        else hi = mid;
-    }
-    lb[k] = (int32_t)lo;
-}
-
-// ------------------------------------------------------------------------------------------
 // KO: order the emitted records by global position.  KP appended every record to the bucket of its
 //     position (2^shift positions per bucket, bcap records each); one workgroup per kKofBuckets
 //     buckets sums the counts of the earlier buckets (its output offset), each wave ranks a
@@ -1816,12 +1554,14 @@ void device_release(Device* d) {
     (void)hipFree(d->d_slots); d->d_slots = nullptr;
     (void)hipFree(d->d_pile); d->d_pile = nullptr;
     (void)hipFree(d->d_planes); d->d_planes = nullptr;
+    (void)hipFree(d->d_seg); d->d_seg = nullptr;
+    (void)hipFree(d->d_segneg); d->d_segneg = nullptr;
+    (void)hipFree(d->d_tseg); d->d_tseg = nullptr;
     (void)hipFree(d->d_wins); d->d_wins = nullptr;
     d->n_wins = 0;
     d->planes_W = 0;
     (void)hipFree(d->d_reads); d->d_reads = nullptr;
     (void)hipFree(d->d_ref); d->d_ref = nullptr;
-    (void)hipFree(d->d_lb); d->d_lb = nullptr;
     (void)hipFree(d->d_tinfo); d->d_tinfo = nullptr;
     (void)hipFree(d->d_rows); d->d_rows = nullptr;
     (void)hipFree(d->d_toff); d->d_toff = nullptr;
@@ -1831,7 +1571,7 @@ void device_release(Device* d) {
     (void)hipFree(d->d_blb); d->d_blb = nullptr;
     (void)hipFree(d->d_bbase); d->d_bbase = nullptr;
     d->n_samples = 0;
-    d->n_units = d->n_slots = d->n_lb = d->n_reads = d->g_len = d->n_tiles = 0;
+    d->n_units = d->n_slots = d->n_reads = d->g_len = d->n_tiles = 0;
 }
 
 void device_destroy(Device* d) {
@@ -1863,23 +1603,42 @@ void device_destroy(Device* d) {
 int device_upload(Device* d, const Staged& s, std::string& err) {
     HIP_TRY(hipSetDevice(d->ordinal));
     device_release(d);
-    const int S = s.slot_size;
-    const int64_t slot_bytes = s.n_slots * (int64_t)S;
     const int32_t pad = s.windows.empty() ? 64 : s.windows[0].pad;
-    HIP_TRY(hipMalloc(&d->d_slots, (size_t)std::max<int64_t>(slot_bytes, 16)));
     HIP_TRY(hipMalloc(&d->d_pile, (size_t)std::max<int64_t>(s.pile_bytes, 16)));
     HIP_TRY(hipMalloc(&d->d_tinfo, (size_t)std::max<int64_t>(s.n_tiles, 1) * sizeof(TileInfo)));
-    HIP_TRY(hipMalloc(&d->d_reads, (size_t)std::max<int64_t>(s.n_reads, 1) * sizeof(int4)));
     HIP_TRY(hipMalloc(&d->d_ref, (size_t)s.g_len + 64));
-    d->n_lb = (s.g_len + pad + 63) / 64 + 2;
-    HIP_TRY(hipMalloc(&d->d_lb, (size_t)d->n_lb * 4));
-    if (slot_bytes) HIP_TRY(hipMemcpyAsync(d->d_slots, s.h_slots.data(), (size_t)slot_bytes, hipMemcpyHostToDevice, d->stream));
-    if (s.pile_bytes) HIP_TRY(hipMemcpyAsync(d->d_pile, s.h_pile.data(), (size_t)s.pile_bytes, hipMemcpyHostToDevice, d->stream));
     if (s.n_tiles && !s.h_tinfo.empty()) HIP_TRY(hipMemcpyAsync(d->d_tinfo, s.h_tinfo.data(), (size_t)s.n_tiles * sizeof(TileInfo), hipMemcpyHostToDevice, d->stream));
-    if (s.n_samples > 0) {
+    HIP_TRY(hipMemsetAsync(d->d_ref, 0, (size_t)s.g_len + 64, d->stream));
+    HIP_TRY(hipMemcpyAsync(d->d_ref, s.h_ref.data(), (size_t)s.g_len, hipMemcpyHostToDevice, d->stream));
+    if (s.single) {
+        // single sample: planes (KT), position-major pile + segments (KP) -- everything KT/KP/KO read
+        const size_t nseg = s.h_seg.n;
+        HIP_TRY(hipMalloc(&d->d_planes, (size_t)std::max<int64_t>(s.pile_bytes / 4, 16)));
+        HIP_TRY(hipMalloc(&d->d_seg, std::max<size_t>(nseg, 1) * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc(&d->d_segneg, std::max<size_t>(nseg, 1)));
+        HIP_TRY(hipMalloc(&d->d_tseg, ((size_t)s.n_tiles + 1) * sizeof(int32_t)));
+        if (s.pile_bytes) {
+            HIP_TRY(hipMemcpyAsync(d->d_pile, s.h_cpile.p, (size_t)s.pile_bytes, hipMemcpyHostToDevice, d->stream));
+            HIP_TRY(hipMemcpyAsync(d->d_planes, s.h_planes.p, (size_t)(s.pile_bytes / 4), hipMemcpyHostToDevice, d->stream));
+        }
+        if (nseg) {
+            HIP_TRY(hipMemcpyAsync(d->d_seg, s.h_seg.p, nseg * sizeof(uint32_t), hipMemcpyHostToDevice, d->stream));
+            HIP_TRY(hipMemcpyAsync(d->d_segneg, s.h_segneg.p, nseg, hipMemcpyHostToDevice, d->stream));
+        }
+        if (!s.h_tseg.empty()) HIP_TRY(hipMemcpyAsync(d->d_tseg, s.h_tseg.data(), s.h_tseg.size() * sizeof(int32_t), hipMemcpyHostToDevice, d->stream));
+        d->planes_W = s.tile / 32;
+    } else {
+        // multisample: per-(tile, sample) blocks (KTM), the read-major SoA and its bucket index (KPM)
+        const int S = s.slot_size;
+        const int64_t slot_bytes = s.n_slots * (int64_t)S;
+        HIP_TRY(hipMalloc(&d->d_slots, (size_t)std::max<int64_t>(slot_bytes, 16)));
+        HIP_TRY(hipMalloc(&d->d_reads, (size_t)std::max<int64_t>(s.n_reads, 1) * sizeof(int4)));
+        if (slot_bytes) HIP_TRY(hipMemcpyAsync(d->d_slots, s.h_slots.data(), (size_t)slot_bytes, hipMemcpyHostToDevice, d->stream));
+        if (s.pile_bytes) HIP_TRY(hipMemcpyAsync(d->d_pile, s.h_pile.data(), (size_t)s.pile_bytes, hipMemcpyHostToDevice, d->stream));
+        if (s.n_reads) HIP_TRY(hipMemcpyAsync(d->d_reads, s.h_reads.data(), (size_t)s.n_reads * 16, hipMemcpyHostToDevice, d->stream));
         HIP_TRY(hipMalloc(&d->d_rows, std::max<size_t>(s.h_rows.size(), 1) * sizeof(uint16_t)));
         HIP_TRY(hipMalloc(&d->d_toff, std::max<size_t>(s.h_toff.size(), 1) * sizeof(int64_t)));
-        HIP_TRY(hipMalloc(&d->d_nrank, (size_t)s.n_samples));
+        HIP_TRY(hipMalloc(&d->d_nrank, (size_t)std::max(s.n_samples, 1)));
         if (!s.h_rows.empty()) HIP_TRY(hipMemcpyAsync(d->d_rows, s.h_rows.data(), s.h_rows.size() * sizeof(uint16_t), hipMemcpyHostToDevice, d->stream));
         if (!s.h_toff.empty()) HIP_TRY(hipMemcpyAsync(d->d_toff, s.h_toff.data(), s.h_toff.size() * sizeof(int64_t), hipMemcpyHostToDevice, d->stream));
         auto up32 = [&](int32_t** dst, const std::vector<int32_t>& v) -> int {
@@ -1890,15 +1649,12 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
         if (up32(&d->d_perm, s.h_perm) || up32(&d->d_bseg, s.h_bseg) || up32(&d->d_blb, s.h_blb) || up32(&d->d_bbase, s.h_bbase)) return -1;
         d->nblk_b = s.nblk_b;
         d->n_samples = s.n_samples;
+        d->n_units = slot_bytes / 16;
+        d->n_slots = s.n_slots;
+        d->slot_size = S;
     }
-    if (s.n_reads) HIP_TRY(hipMemcpyAsync(d->d_reads, s.h_reads.data(), (size_t)s.n_reads * 16, hipMemcpyHostToDevice, d->stream));
-    HIP_TRY(hipMemsetAsync(d->d_ref, 0, (size_t)s.g_len + 64, d->stream));
-    HIP_TRY(hipMemcpyAsync(d->d_ref, s.h_ref.data(), (size_t)s.g_len, hipMemcpyHostToDevice, d->stream));
-    d->n_units = slot_bytes / 16;
-    d->n_slots = s.n_slots;
     d->n_reads = s.n_reads;
     d->g_len = s.g_len;
-    d->slot_size = S;
     d->max_span = s.max_span;
     d->pad = pad;
     d->tile = s.tile;
@@ -1906,25 +1662,12 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
     while ((1 << d->log2_tile) < s.tile) d->log2_tile++;
     d->n_tiles = s.n_tiles;
     {
-        dim3 grid((unsigned)((d->n_lb + 255) / 256));
-        hipLaunchKernelGGL(kl_read_index, grid, dim3(256), 0, d->stream, d->d_reads, d->n_reads, d->d_lb, d->n_lb, pad);
-        HIP_TRY(hipGetLastError());
-    }
-    {
         std::vector<int4> wins;
         for (const Window& w : s.windows) wins.push_back(int4{(int)(w.gbase + w.pad), w.w0, w.seq_id, w.wlen});
         if (wins.empty()) wins.push_back(int4{0, 0, -1, 0});
         HIP_TRY(hipMalloc(&d->d_wins, wins.size() * sizeof(int4)));
         HIP_TRY(hipMemcpy(d->d_wins, wins.data(), wins.size() * sizeof(int4), hipMemcpyHostToDevice));
         d->n_wins = (int32_t)wins.size();
-    }
-    // single-sample tiles of 128..512 positions: KT scans bit planes (NGSEP_NO_PLANES=1: the byte pile)
-    if (s.h_rows.empty() && s.n_tiles > 0 && (s.tile == 128 || s.tile == 256 || s.tile == 512) &&
-        std::getenv("NGSEP_NO_PLANES") == nullptr) {
-        HIP_TRY(hipMalloc(&d->d_planes, (size_t)std::max<int64_t>(s.pile_bytes / 4, 16)));
-        hipLaunchKernelGGL(kb_planes, dim3(1024), dim3(256), 0, d->stream, d->d_pile, d->d_tinfo, d->n_tiles, s.tile, d->d_planes);
-        HIP_TRY(hipGetLastError());
-        d->planes_W = s.tile / 32;
     }
     HIP_TRY(hipStreamSynchronize(d->stream));
     return 0;
@@ -1953,7 +1696,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     // capacities (shared buffers only change while nothing runs): calls are rare; dump mode needs one
     // record per covered position
     const int64_t want = g.dump_all ? std::max<int64_t>(s.covered + 1024, 1024) : std::max<int64_t>(s.g_len / 256 + 4096, 4096);
-    const int64_t qwant = g.dump_all ? std::max<int64_t>(s.covered + 1024, 1024) : std::max<int64_t>(s.g_len / 64 + 65536, 65536);
+    const int64_t qwant = (g.dump_all || !prune) ? s.g_len + 1024 : std::max<int64_t>(s.g_len / 64 + 65536, 65536);
     if (want > d->cap_sites || qwant > sl.cap_hard) {
         if (!idle) HIP_TRY(hipStreamSynchronize(sl.stream));
         if (grow_slot(d, sl, want, qwant, err) != 0) return -1;
@@ -1998,7 +1741,8 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     // KT is timed by events bound to its dispatch (hipExtLaunchKernelGGL): the kernel's own start and end
     hipEvent_t k0 = d->time_scan ? sl.ev[0] : nullptr, k1 = d->time_scan ? sl.ev[1] : nullptr;
     if (d->n_tiles > 0 && prune && d->planes_W) {
-        // bit-plane scan, persistent waves as below
+        // bit-plane scan, persistent waves: as many workgroups as are co-resident, each wave walks the
+        // tiles with a grid stride, so at any moment the waves stream one contiguous stretch of the planes
         const int wi = d->planes_W == 4 ? 0 : d->planes_W == 8 ? 1 : 2;
         auto kt = wi == 0 ? (const void*)k_tile_planes<4> : wi == 1 ? (const void*)k_tile_planes<8> : (const void*)k_tile_planes<16>;
         int& per_cu = d->kt_planes_per_cu[wi];
@@ -2013,45 +1757,20 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         else hipExtLaunchKernelGGL(k_tile_planes<16>, grid, dim3(kScanThreads), 0, sl.stream, k0, k1, 0, NGSEP_KTP_ARGS);
 #undef NGSEP_KTP_ARGS
         HIP_TRY(hipGetLastError());
-    } else if (d->n_tiles > 0) {
-        // persistent waves: as many workgroups as are co-resident (register-limited), each wave
-        // walks the tiles with a grid stride, so at any moment the waves stream one contiguous
-        // stretch of the pile
-        auto kt = prune ? (const void*)k_tile_pileup<0> : (const void*)k_tile_pileup<1>;
-        int& per_cu = d->kt_blocks_per_cu[prune ? 0 : 1];
-        if (per_cu == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kt, kScanThreads, 0) != hipSuccess || per_cu < 1)) per_cu = 2;
-        int bpc = per_cu;
-        if (const char* e = std::getenv("NGSEP_BLOCKS_PER_CU")) bpc = std::max(1, std::atoi(e));   // tuning
-        const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((d->n_tiles + kScanWaves - 1) / kScanWaves, (int64_t)d->n_cu * bpc));
-        dim3 grid((unsigned)nblk);
-        if (prune)
-            hipExtLaunchKernelGGL(k_tile_pileup<0>, grid, dim3(kScanThreads), 0, sl.stream, k0, k1, 0, (const u32x4*)d->d_pile,
-                                  d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, sl.d_tables, g, sl.d_hard, ctr, sl.cap_hard,
-                                  sl.d_bcount, nb);
-        else
-            hipExtLaunchKernelGGL(k_tile_pileup<1>, grid, dim3(kScanThreads), 0, sl.stream, k0, k1, 0, (const u32x4*)d->d_pile,
-                                  d->d_tinfo, d->d_ref, d->log2_tile, d->n_tiles, sl.d_tables, g, sl.d_hard, ctr, sl.cap_hard,
-                                  sl.d_bcount, nb);
-        HIP_TRY(hipGetLastError());
     } else {
-        if (k0) HIP_TRY(hipEventRecord(k0, sl.stream));
-        HIP_TRY(hipMemsetAsync(sl.d_bcount, 0, (size_t)nb * sizeof(int32_t), sl.stream));
-        if (k1) HIP_TRY(hipEventRecord(k1, sl.stream));
+        // dump mode / no pruning: every in-window position goes to KP
+        const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((s.g_len + 255) / 256, (int64_t)d->n_cu * 8));
+        hipExtLaunchKernelGGL(k_queue_all, dim3((unsigned)nblk), dim3(256), 0, sl.stream, k0, k1, 0, (const uint8_t*)d->d_ref,
+                              s.g_len, sl.d_hard, ctr, sl.cap_hard, sl.d_bcount, nb);
+        HIP_TRY(hipGetLastError());
     }
-#ifdef NGSEP_KP_STAMPS
-    if (!d->d_stamps) HIP_TRY(hipMalloc(&d->d_stamps, 16 * sizeof(unsigned long long)));
-    {
-        unsigned long long init[16] = {0, 0, 0, 0, 0, 0, 0, ~0ull, 0, 0, 0, 0, 0, 0, 0, 0};
-        HIP_TRY(hipMemcpyAsync(d->d_stamps, init, sizeof init, hipMemcpyHostToDevice, sl.stream));
-        HIP_TRY(hipStreamSynchronize(sl.stream));
-    }
-#endif
     static const int kp_grid = std::getenv("NGSEP_KP_GRID") ? std::max(1, std::atoi(std::getenv("NGSEP_KP_GRID"))) : 2048;   // tuning
     hipExtLaunchKernelGGL(k_posterior, dim3(kp_grid), dim3(kPostWaves * 64), 0, sl.stream,
                           d->time_posterior ? sl.ev[5] : nullptr, d->time_posterior ? sl.ev[2] : nullptr, 0,
                           (const QueueSite*)sl.d_hard, (const unsigned long long*)(ctr + 2), sl.cap_hard,
-                          (const int4*)d->d_reads, d->n_reads, (const int32_t*)d->d_lb, (const uint8_t*)d->d_slots,
-                          d->slot_size, (const LikTables*)sl.d_tables, g, sl.d_brec, sl.d_bcount, shift, bcap, d->d_stamps);
+                          (const TileInfo*)d->d_tinfo, (const int32_t*)d->d_tseg, (const uint32_t*)d->d_seg,
+                          (const uint8_t*)d->d_segneg, (const uint8_t*)d->d_pile, d->log2_tile, (const LikTables*)sl.d_tables, g,
+                          sl.d_brec, sl.d_bcount, shift, bcap);
     HIP_TRY(hipGetLastError());
     // order the records by position on the device (one kernel; counters[0] = records | max bucket << 40)
     hipLaunchKernelGGL(ko_fused, dim3((unsigned)((nb + kKofBuckets - 1) / kKofBuckets)), dim3(64 * kKofBuckets), 0, sl.stream, sl.d_brec,
@@ -2129,17 +1848,6 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
     }
     sl.busy = false;
     d->n_collected++;
-#ifdef NGSEP_KP_STAMPS
-    {
-        unsigned long long st[16];
-        HIP_TRY(hipMemcpy(st, d->d_stamps, sizeof st, hipMemcpyDeviceToHost));
-        const double ns = st[5] ? (double)st[5] : 1.0;
-        std::fprintf(stderr, "[kp stamps] sites %llu waves %llu | per site cycles: tally %.0f posterior %.0f emit %.0f | "
-                     "walk iters %.2f valid reads %.1f | wave busy avg %.0f, span %llu\n",
-                     st[5], st[9], st[0] / ns, st[1] / ns, st[2] / ns, st[3] / ns, st[4] / ns,
-                     st[9] ? (double)st[6] / st[9] : 0.0, st[8] - st[7]);
-    }
-#endif
     if (n > sl.guess) {
         sl.host.n = (size_t)sl.guess;                 // keep the records already copied when the store grows
         sl.host.reserve((size_t)n);

@@ -142,6 +142,25 @@ def test_pruning_is_exact(tmp_path, depth, snv_rate, het):
     assert st.hard_sites < st.candidates     # the bound dropped candidates
 
 
+def test_exact_bound_path(tmp_path, monkeypatch):
+    """NGSEP_KT_EXACT=1: KT applies the exact integer hom-ref bound to the count-bound survivors over the
+    position-major byte column; the calls equal genotyping every position."""
+    monkeypatch.setenv("NGSEP_KT_EXACT", "1")
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=2, depth=20, seed=13, quality_model=2, snv_rate=3e-3)
+    res = []
+    for prune in (1, 0):
+        with GpuPileupSession(gpu_params(prune_candidates=prune, min_quality=0)) as s:
+            for name, seq in syn.contigs():
+                s.set_reference(name, seq)
+            s.processAlignments(syn.batch())
+            s.notifyEndOfAlignments()
+            res.append([(x.sequence, x.pos, x.gq, x.qual, tuple(x.counts), tuple(x.logc)) for x in s.getCalledVariants()])
+            if prune:
+                st = s.stats()
+    assert res[0] == res[1] and len(res[0]) > 100
+    assert st.exact_bound_passes > 0
+
+
 def test_path_a_equals_path_b(tmp_path):
     """ngsep_process_alignments (JNI-style batches) == ngsep_call_bam (BAM decoded in C++)."""
     syn, fa, sam, bam = make_data(tmp_path, genome=pysynth.YEAST, n_contigs=2, depth=20, seed=9)
@@ -195,11 +214,11 @@ def test_async_passes_identical(tmp_path):
         assert g == ref
 
 
-@pytest.mark.parametrize("tile", [64, 128, 256, 512])
-@pytest.mark.parametrize("depth,het", [(12, 0.05), (40, 0.1), (90, 0.001)])
+@pytest.mark.parametrize("tile", [128, 256, 512])
+@pytest.mark.parametrize("depth,het", [(12, 0.05), (40, 0.1), (90, 0.001), (300, 0.001)])
 def test_tile_width_scan_paths(tmp_path, monkeypatch, tile, depth, het):
-    """Fixed tile widths: 128..512 take the bit-plane scan (one or several 64-row groups; above 255
-    rows no bound), 64 the byte-pile scan.  Pruned calls == genotyping every position."""
+    """Fixed tile widths of the bit-plane scan (one or several 64-row groups; above 255 rows no bound).
+    Pruned calls == genotyping every position (KQ queues all, KP genotypes them)."""
     monkeypatch.setenv("NGSEP_TILE_T", str(tile))
     syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=1, depth=depth, seed=11, quality_model=2, snv_rate=3e-3)
     res = []

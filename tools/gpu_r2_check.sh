@@ -1,0 +1,13 @@
+#!/bin/bash
+# round-2 GPU check: the -m gpu suite, then a short default bench (chr20) with rocprof kernel stats
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+rc=$?
+tail -30 gpurun_out/gpu_tests.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+timeout -k 10 600 python -u bench.py --steps 20 --warmup 3 > gpurun_out/bench.json 2> gpurun_out/bench.err
+rc=$?
+tail -5 gpurun_out/bench.err; cat gpurun_out/bench.json
+exit $rc
