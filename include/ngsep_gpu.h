@@ -211,8 +211,16 @@ int ngsep_write_population_vcf(ngsep_ctx* ctx, const char* path);
  * files merged as AlignmentsPileupGenerator.processFiles does (:201-266, chooseNextAln :268-289) */
 int ngsep_call_population_bams(ngsep_ctx* ctx, const char* const* bam_paths, int32_t n_files, const char* out_vcf_path);
 
-/* ---- path B: the whole SingleSampleVariantsDetector.findSNVS on a BAM file (:896-931) ---- */
+/* ---- path B: the whole SingleSampleVariantsDetector.findSNVS on a BAM file (:896-931) ----
+ * BGZF blocks inflate on the host threads (NGSEP_THREADS / OMP_NUM_THREADS) while records are decoded;
+ * with params.query_seq set the reader seeks through the BAI index (path.bai) when one exists. */
 int ngsep_call_bam(ngsep_ctx* ctx, const char* bam_path, const char* out_vcf_path);
+/* findSNVS restricted to seq:first-last (1-based, inclusive) -- `-querySeq seq -first first -last last`
+ * (SingleSampleVariantsDetector options, AlignmentsPileupGenerator.java:242-254,342-354) -- reading only
+ * the region's BGZF blocks through the BAI index (htsjdk SamReader.query's role in
+ * ReadAlignmentFileReader.java:171-183).  Writes the VCF header and the region's calls to out_vcf_path. */
+int ngsep_call_region_bam(ngsep_ctx* ctx, const char* bam_path, const char* seq, int64_t first, int64_t last,
+                          const char* out_vcf_path);
 
 /* ---- CoverageStatisticsCalculator (discovery/CoverageStatisticsCalculator.java:108-216) ----
  * path A: params.coverage_stats = 1, alignments through ngsep_process_alignments, ngsep_notify_end runs
@@ -233,6 +241,10 @@ typedef struct ngsep_bam ngsep_bam;
 int  ngsep_bam_open(ngsep_ctx* ctx, const char* path, ngsep_bam** out);
 /* reads up to max_reads filtered alignments; the batch arrays stay valid until the next call */
 int  ngsep_bam_next_batch(ngsep_bam* bam, int64_t max_reads, ngsep_read_batch* batch);
+/* positions the reader at the first BGZF chunk that can hold alignments overlapping seq:first-last (BAI
+ * index, SAM spec 5.2); next_batch then returns records in file order and stops after the last record
+ * of seq starting at or before last.  NGSEP_E_IO when the BAM has no index. */
+int  ngsep_bam_set_region(ngsep_bam* bam, const char* seq_name, int64_t first, int64_t last);
 int  ngsep_bam_close(ngsep_bam* bam);
 
 /* ---- measurement entry points (bench.py): split staging (pack + H2D) from the device run ---- */

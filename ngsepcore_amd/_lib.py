@@ -175,6 +175,8 @@ SIGNATURES = {
     "ngsep_bam_open": (ctypes.c_int, [_CTX, ctypes.c_char_p, P(ctypes.c_void_p)]),
     "ngsep_bam_next_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, P(NgsepReadBatch)]),
     "ngsep_bam_close": (ctypes.c_int, [ctypes.c_void_p]),
+    "ngsep_bam_set_region": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64]),
+    "ngsep_call_region_bam": (ctypes.c_int, [_CTX, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p]),
     "ngsep_stage_alignments": (ctypes.c_int, [_CTX, P(NgsepReadBatch)]),
     "ngsep_stage_finish": (ctypes.c_int, [_CTX]),
     "ngsep_run_staged": (ctypes.c_int, [_CTX, P(ctypes.c_double)]),

@@ -5,25 +5,125 @@
 //   ("=ACMGRSVTWYHKDBN" decoding), getBaseQualityString (0xFF -> "*"), RG (header lookup), NH.
 // Reader filters: consecutive duplicates (isSameAlignment :292-306), FLAG_MULTIPLE_ALN (:284-291),
 // unmapped/secondary/multiple filter flags (AlignmentsPileupGenerator.java:363-375).
+//
+// Host pipeline: a decoder thread reads the compressed file in 32 MB chunks,
+// inflates their BGZF blocks on all host threads (libdeflate through dlopen when the image has it, zlib
+// otherwise) and hands the decoded bytes over a bounded queue; ngsep_bam_next_batch cuts the records
+// (one pass over the block_size chain) and decodes them into the batch arrays in parallel.  A BAI index
+// (path.bai, SAM spec 5.2) gives random access: ngsep_bam_set_region seeks to the first chunk of a
+// region (ngsep_call_region_bam, the sharded callers).
+#include <dlfcn.h>
 #include <zlib.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
 #include "engine.hpp"
 
+namespace {
+
+// raw-deflate decompression of one BGZF block: libdeflate when present (dlopen, ~2-3x zlib), zlib otherwise
+struct Inflater {
+    void* (*alloc)() = nullptr;
+    int (*decompress)(void*, const void*, size_t, void*, size_t, size_t*) = nullptr;
+    void (*release)(void*) = nullptr;
+    Inflater() {
+        if (std::getenv("NGSEP_ZLIB")) return;     // diagnostics: force zlib
+        void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        alloc = (void* (*)())dlsym(h, "libdeflate_alloc_decompressor");
+        decompress = (int (*)(void*, const void*, size_t, void*, size_t, size_t*))dlsym(h, "libdeflate_deflate_decompress");
+        release = (void (*)(void*))dlsym(h, "libdeflate_free_decompressor");
+        if (!alloc || !decompress || !release) alloc = nullptr;
+    }
+    static const Inflater& get() { static Inflater i; return i; }
+    // inflates in[0, n) into exactly out_n bytes
+    bool run(const uint8_t* in, size_t n, uint8_t* out, size_t out_n) const {
+        if (alloc) {
+            thread_local struct D { void* d = nullptr; ~D() { if (d) Inflater::get().release(d); } } dd;
+            if (!dd.d) dd.d = alloc();
+            size_t got = 0;
+            return decompress(dd.d, in, n, out, out_n, &got) == 0 && got == out_n;
+        }
+        z_stream z{};
+        if (inflateInit2(&z, -15) != Z_OK) return false;
+        z.next_in = const_cast<Bytef*>(in);
+        z.avail_in = (uInt)n;
+        z.next_out = out;
+        z.avail_out = (uInt)out_n;
+        const int rc = inflate(&z, Z_FINISH);
+        inflateEnd(&z);
+        return rc == Z_STREAM_END && z.total_out == out_n;
+    }
+};
+
+// growable array without value-initialisation (batch and chunk buffers are overwritten in parallel)
+template <class T>
+struct RawBuf {
+    T* p = nullptr;
+    size_t n = 0, cap = 0;
+    RawBuf() = default;
+    RawBuf(const RawBuf&) = delete;
+    RawBuf& operator=(const RawBuf&) = delete;
+    RawBuf(RawBuf&& o) noexcept : p(o.p), n(o.n), cap(o.cap) { o.p = nullptr; o.n = o.cap = 0; }
+    RawBuf& operator=(RawBuf&& o) noexcept { std::swap(p, o.p); std::swap(n, o.n); std::swap(cap, o.cap); return *this; }
+    ~RawBuf() { std::free(p); }
+    void resize(size_t k) {
+        if (k > cap) {
+            const size_t c = std::max(k, cap + cap / 2);
+            T* q = static_cast<T*>(std::malloc(c * sizeof(T)));
+            if (n) std::memcpy(q, p, n * sizeof(T));
+            std::free(p);
+            p = q;
+            cap = c;
+        }
+        n = k;
+    }
+    T* data() { return p; }
+    T& operator[](size_t i) { return p[i]; }
+};
+
+constexpr size_t kChunkHead = (size_t)4 << 20;   // headroom before a chunk's bytes for the previous chunk's tail
+
+struct Chunk {                 // decoded bytes of whole BGZF blocks at mem.p + kChunkHead
+    RawBuf<uint8_t> mem;
+    size_t len = 0;
+    bool eof = false;
+    std::string err;
+};
+
+// BAI (SAM spec 5.2): per reference, the bins' chunks and the 16 kb linear index
+struct BaiRef {
+    std::unordered_map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>> bins;
+    std::vector<uint64_t> lin;
+};
+
+}  // namespace
+
 struct ngsep_bam {
     ngsep_ctx* ctx = nullptr;
     std::FILE* f = nullptr;
-    std::vector<uint8_t> comp;
-    std::string buf;        // inflated bytes not yet consumed
-    size_t pos = 0;
+    std::string path;
+    // decoder thread -> consumer queue
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<Chunk> q;
+    bool stop = false, producer_done = false;
+    // consumer side: the current decoded buffer; bytes [pos, end) not yet consumed
+    RawBuf<uint8_t> mem;
+    uint8_t* buf = nullptr;
+    size_t end = 0, pos = 0;
     bool eof = false;
     std::vector<int32_t> ref_to_seq;   // BAM refID -> ctx sequence id
+    std::vector<std::string> ref_names;
     std::vector<std::string> rg_ids;   // header read groups
     std::vector<std::string> rg_sm;    // their SM tags (the read group id when absent, ReadAlignmentFileReader.java:186-188)
     std::unordered_map<std::string, int32_t> rg_index;
@@ -34,62 +134,219 @@ struct ngsep_bam {
     int32_t last_pos = 0;
     int last_paired = 0, last_fop = 0;
     std::string last_name;
-    // batch storage
-    std::vector<int32_t> b_seq, b_first, b_flags, b_rg, b_cig_n, b_cigar, b_seqlen;
-    std::vector<int64_t> b_cig_off, b_seq_off;
-    std::vector<uint8_t> b_hasq;
-    std::string b_bases, b_quals;
+    // region (ngsep_bam_set_region): stop at the first record past it
+    int32_t region_ref = -1;
+    int64_t region_last = 0;
+    bool region_done = false;
+    // index
+    bool bai_loaded = false;
+    std::vector<BaiRef> bai;
+    // batch storage (filled in parallel, never value-initialised)
+    RawBuf<int32_t> b_seq, b_first, b_flags, b_rg, b_cig_n, b_cigar, b_seqlen;
+    RawBuf<int64_t> b_cig_off, b_seq_off;
+    RawBuf<uint8_t> b_hasq;
+    RawBuf<char> b_bases, b_quals;
 };
 
 namespace {
 
-// inflates the next BGZF block into bam->buf; returns false at end of file
-bool next_block(ngsep_bam* b, std::string& err) {
-    uint8_t h[18];
-    size_t n = std::fread(h, 1, 18, b->f);
-    if (n == 0) return false;
-    if (n < 18 || h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) { err = "not a BGZF file"; return false; }
-    uint16_t xlen = (uint16_t)(h[10] | (h[11] << 8));
-    // standard BGZF: XLEN=6 with the BC subfield
-    std::vector<uint8_t> extra(xlen);
-    std::memcpy(extra.data(), h + 12, std::min<size_t>(6, xlen));
-    if (xlen > 6 && std::fread(extra.data() + 6, 1, xlen - 6, b->f) != (size_t)(xlen - 6)) { err = "truncated BGZF header"; return false; }
-    int bsize = -1;
-    for (size_t i = 0; i + 4 <= extra.size();) {
-        uint16_t sl = (uint16_t)(extra[i + 2] | (extra[i + 3] << 8));
-        if (extra[i] == 'B' && extra[i + 1] == 'C' && sl == 2) bsize = extra[i + 4] | (extra[i + 5] << 8);
-        i += 4 + sl;
+using ngsep::parallel_for;
+
+// decoder thread: 32 MB of compressed blocks at a time, inflated on all host threads
+void decoder_loop(ngsep_bam* b) {
+    const size_t kRead = (size_t)32 << 20;
+    std::vector<uint8_t> comp, carry;
+    bool file_eof = false;
+    while (true) {
+        {
+            std::unique_lock<std::mutex> lk(b->mu);
+            b->cv.wait(lk, [&] { return b->stop || b->q.size() < 3; });
+            if (b->stop) break;
+        }
+        Chunk ch;
+        comp.swap(carry);
+        carry.clear();
+        if (!file_eof) {
+            const size_t o = comp.size();
+            comp.resize(o + kRead);
+            const size_t got = std::fread(comp.data() + o, 1, kRead, b->f);
+            comp.resize(o + got);
+            if (got < kRead) file_eof = true;
+        }
+        // whole blocks in comp: offsets and decoded sizes
+        std::vector<size_t> boff, bclen;
+        std::vector<uint32_t> bisize;
+        size_t p = 0;
+        while (p + 18 <= comp.size()) {
+            const uint8_t* h = comp.data() + p;
+            if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) { ch.err = "not a BGZF file"; break; }
+            const uint16_t xlen = (uint16_t)(h[10] | (h[11] << 8));
+            if (p + 12 + xlen > comp.size()) break;
+            int bsize = -1;
+            for (size_t i = 0; i + 4 <= xlen;) {
+                const uint8_t* x = h + 12 + i;
+                const uint16_t sl = (uint16_t)(x[2] | (x[3] << 8));
+                if (x[0] == 'B' && x[1] == 'C' && sl == 2) bsize = x[4] | (x[5] << 8);
+                i += 4 + sl;
+            }
+            if (bsize < 0) { ch.err = "BGZF block without BC field"; break; }
+            const size_t total = (size_t)bsize + 1;
+            if (p + total > comp.size()) break;
+            const uint8_t* t = h + total - 4;
+            boff.push_back(p + 12 + xlen);
+            bclen.push_back(total - 12 - xlen - 8);
+            bisize.push_back((uint32_t)(t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24)));
+            p += total;
+        }
+        if (ch.err.empty() && p < comp.size()) {
+            if (file_eof && boff.empty()) ch.err = "truncated BGZF block";
+            carry.assign(comp.begin() + (ptrdiff_t)p, comp.end());
+        }
+        std::vector<size_t> dout(boff.size() + 1, 0);
+        for (size_t k = 0; k < boff.size(); k++) dout[k + 1] = dout[k] + bisize[k];
+        ch.mem.resize(kChunkHead + dout.back());
+        ch.len = dout.back();
+        uint8_t* dst = ch.mem.data() + kChunkHead;
+        std::atomic<int> bad{0};
+        const Inflater& inf = Inflater::get();
+        parallel_for((int64_t)boff.size(), 16, [&](int64_t lo, int64_t hi) {
+            for (int64_t k = lo; k < hi; k++)
+                if (bisize[(size_t)k] && !inf.run(comp.data() + boff[(size_t)k], bclen[(size_t)k], dst + dout[(size_t)k], bisize[(size_t)k]))
+                    bad = 1;
+        });
+        if (bad && ch.err.empty()) ch.err = "BGZF inflate failed";
+        ch.eof = file_eof && carry.empty();
+        const bool last = ch.eof || !ch.err.empty();
+        {
+            std::lock_guard<std::mutex> lk(b->mu);
+            b->q.push_back(std::move(ch));
+        }
+        b->cv.notify_all();
+        if (last) break;
     }
-    if (bsize < 0) { err = "BGZF block without BC field"; return false; }
-    size_t rest = (size_t)bsize + 1 - 12 - xlen;
-    b->comp.resize(rest);
-    if (std::fread(b->comp.data(), 1, rest, b->f) != rest) { err = "truncated BGZF block"; return false; }
-    uint32_t isize = (uint32_t)(b->comp[rest - 4] | (b->comp[rest - 3] << 8) | (b->comp[rest - 2] << 16) | ((uint32_t)b->comp[rest - 1] << 24));
-    if (isize == 0) return true;
-    size_t o = b->buf.size();
-    b->buf.resize(o + isize);
-    z_stream z{};
-    inflateInit2(&z, -15);
-    z.next_in = b->comp.data();
-    z.avail_in = (uInt)(rest - 8);
-    z.next_out = (Bytef*)&b->buf[o];
-    z.avail_out = isize;
-    int rc = inflate(&z, Z_FINISH);
-    inflateEnd(&z);
-    if (rc != Z_STREAM_END) { err = "BGZF inflate failed"; return false; }
-    return true;
+    std::lock_guard<std::mutex> lk(b->mu);
+    b->producer_done = true;
+    b->cv.notify_all();
 }
 
-// ensures at least n unconsumed bytes; false at EOF
+void stop_decoder(ngsep_bam* b) {
+    if (b->th.joinable()) {
+        {
+            std::lock_guard<std::mutex> lk(b->mu);
+            b->stop = true;
+        }
+        b->cv.notify_all();
+        b->th.join();
+    }
+    b->q.clear();
+    b->stop = false;
+    b->producer_done = false;
+}
+
+void start_decoder(ngsep_bam* b) {
+    stop_decoder(b);
+    b->eof = false;
+    b->th = std::thread(decoder_loop, b);
+}
+
+// ensures at least n unconsumed bytes; false at EOF (err set on a format error).  The unconsumed tail moves
+// into the next chunk's headroom (no copy of the chunk itself).
 bool need(ngsep_bam* b, size_t n, std::string& err) {
-    while (b->buf.size() - b->pos < n) {
-        if (b->pos > (1u << 20)) { b->buf.erase(0, b->pos); b->pos = 0; }
-        if (!next_block(b, err)) return false;
+    while (b->end - b->pos < n) {
+        if (b->eof) return false;
+        Chunk ch;
+        {
+            std::unique_lock<std::mutex> lk(b->mu);
+            b->cv.wait(lk, [&] { return !b->q.empty() || b->producer_done; });
+            if (b->q.empty()) { b->eof = true; return false; }
+            ch = std::move(b->q.front());
+            b->q.pop_front();
+        }
+        b->cv.notify_all();
+        if (!ch.err.empty()) { err = ch.err; b->eof = true; return false; }
+        const size_t rem = b->end - b->pos;
+        if (rem <= kChunkHead) {
+            uint8_t* start = ch.mem.data() + kChunkHead - rem;
+            if (rem) std::memcpy(start, b->buf + b->pos, rem);
+            b->mem = std::move(ch.mem);
+            b->buf = start;
+            b->pos = 0;
+            b->end = rem + ch.len;
+        } else {                                   // a record longer than the headroom: one copy
+            RawBuf<uint8_t> m;
+            m.resize(rem + ch.len);
+            std::memcpy(m.data(), b->buf + b->pos, rem);
+            std::memcpy(m.data() + rem, ch.mem.data() + kChunkHead, ch.len);
+            b->mem = std::move(m);
+            b->buf = b->mem.data();
+            b->pos = 0;
+            b->end = rem + ch.len;
+        }
+        if (ch.eof) b->eof = true;
     }
     return true;
 }
 
-template <class T> T rd(const char* p) { T v; std::memcpy(&v, p, sizeof(T)); return v; }
+template <class T> T rd(const uint8_t* p) { T v; std::memcpy(&v, p, sizeof(T)); return v; }
+
+// BAI of a BAM: path + ".bai", else the path with ".bam" replaced by ".bai"
+bool load_bai(ngsep_bam* b) {
+    if (b->bai_loaded) return !b->bai.empty();
+    b->bai_loaded = true;
+    std::string p1 = b->path + ".bai", p2;
+    if (b->path.size() > 4 && b->path.compare(b->path.size() - 4, 4, ".bam") == 0) p2 = b->path.substr(0, b->path.size() - 4) + ".bai";
+    std::FILE* f = std::fopen(p1.c_str(), "rb");
+    if (!f && !p2.empty()) f = std::fopen(p2.c_str(), "rb");
+    if (!f) return false;
+    std::vector<uint8_t> d;
+    uint8_t tmp[1 << 16];
+    size_t got;
+    while ((got = std::fread(tmp, 1, sizeof tmp, f)) > 0) d.insert(d.end(), tmp, tmp + got);
+    std::fclose(f);
+    size_t o = 0;
+    auto ok = [&](size_t k) { return o + k <= d.size(); };
+    if (!ok(8) || std::memcmp(d.data(), "BAI\1", 4) != 0) return false;
+    o = 4;
+    const int32_t n_ref = rd<int32_t>(&d[o]);
+    o += 4;
+    std::vector<BaiRef> refs((size_t)std::max(n_ref, 0));
+    for (int32_t r = 0; r < n_ref; r++) {
+        if (!ok(4)) return false;
+        const int32_t n_bin = rd<int32_t>(&d[o]);
+        o += 4;
+        for (int32_t k = 0; k < n_bin; k++) {
+            if (!ok(8)) return false;
+            const uint32_t bin = rd<uint32_t>(&d[o]);
+            const int32_t n_chunk = rd<int32_t>(&d[o + 4]);
+            o += 8;
+            if (!ok((size_t)n_chunk * 16)) return false;
+            auto& v = refs[(size_t)r].bins[bin];
+            for (int32_t c = 0; c < n_chunk; c++) v.push_back({rd<uint64_t>(&d[o + 16 * c]), rd<uint64_t>(&d[o + 16 * c + 8])});
+            o += (size_t)n_chunk * 16;
+        }
+        if (!ok(4)) return false;
+        const int32_t n_intv = rd<int32_t>(&d[o]);
+        o += 4;
+        if (!ok((size_t)n_intv * 8)) return false;
+        refs[(size_t)r].lin.resize((size_t)n_intv);
+        for (int32_t k = 0; k < n_intv; k++) refs[(size_t)r].lin[(size_t)k] = rd<uint64_t>(&d[o + 8 * k]);
+        o += (size_t)n_intv * 8;
+    }
+    b->bai.swap(refs);
+    return true;
+}
+
+// bins overlapping [beg, end) (SAM spec 5.3 reg2bins)
+void reg2bins(int64_t beg, int64_t end, std::vector<uint32_t>& out) {
+    out.clear();
+    --end;
+    out.push_back(0);
+    for (int64_t k = 1 + (beg >> 26); k <= 1 + (end >> 26); k++) out.push_back((uint32_t)k);
+    for (int64_t k = 9 + (beg >> 23); k <= 9 + (end >> 23); k++) out.push_back((uint32_t)k);
+    for (int64_t k = 73 + (beg >> 20); k <= 73 + (end >> 20); k++) out.push_back((uint32_t)k);
+    for (int64_t k = 585 + (beg >> 17); k <= 585 + (end >> 17); k++) out.push_back((uint32_t)k);
+    for (int64_t k = 4681 + (beg >> 14); k <= 4681 + (end >> 14); k++) out.push_back((uint32_t)k);
+}
 
 }  // namespace
 
@@ -99,16 +356,21 @@ extern "C" int ngsep_bam_open(ngsep_ctx* c, const char* path, ngsep_bam** out) {
     if (!c || !path || !out) return NGSEP_E_INVALID;
     ngsep_bam* b = new ngsep_bam();
     b->ctx = c;
+    b->path = path;
     b->f = std::fopen(path, "rb");
     if (!b->f) { delete b; return set_error(c, NGSEP_E_IO, std::string("cannot open ") + path); }
+    start_decoder(b);
+    auto fail = [&](int code, const std::string& m) {
+        stop_decoder(b);
+        std::fclose(b->f);
+        delete b;
+        return set_error(c, code, m);
+    };
     std::string err;
-    if (!need(b, 8, err) || std::memcmp(&b->buf[0], "BAM\1", 4) != 0) {
-        std::fclose(b->f); delete b;
-        return set_error(c, NGSEP_E_FORMAT, err.empty() ? "not a BAM file" : err);
-    }
+    if (!need(b, 8, err) || std::memcmp(&b->buf[0], "BAM\1", 4) != 0) return fail(NGSEP_E_FORMAT, err.empty() ? "not a BAM file" : err);
     int32_t l_text = rd<int32_t>(&b->buf[4]);
-    if (!need(b, 8 + (size_t)l_text + 4, err)) { std::fclose(b->f); delete b; return set_error(c, NGSEP_E_FORMAT, "truncated BAM header"); }
-    std::string text = b->buf.substr(8, (size_t)l_text);
+    if (!need(b, 8 + (size_t)l_text + 4, err)) return fail(NGSEP_E_FORMAT, "truncated BAM header");
+    std::string text((const char*)&b->buf[8], (size_t)l_text);
     b->pos = 8 + (size_t)l_text;
     int32_t n_ref = rd<int32_t>(&b->buf[b->pos]);
     b->pos += 4;
@@ -120,9 +382,10 @@ extern "C" int ngsep_bam_open(ngsep_ctx* c, const char* path, ngsep_bam** out) {
         if (!need(b, 4, err)) break;
         int32_t ln = rd<int32_t>(&b->buf[b->pos]);
         if (!need(b, 4 + (size_t)ln + 4, err)) break;
-        std::string name(&b->buf[b->pos + 4], (size_t)(ln > 0 ? ln - 1 : 0));
+        std::string name((const char*)&b->buf[b->pos + 4], (size_t)(ln > 0 ? ln - 1 : 0));
         int32_t lref = rd<int32_t>(&b->buf[b->pos + 4 + ln]);
         b->pos += 8 + (size_t)ln;
+        b->ref_names.push_back(name);
         if (header_seqs && !seq_index.count(name)) {
             seq_index[name] = (int32_t)c->seq_names.size();
             c->seq_names.push_back(name);
@@ -132,14 +395,8 @@ extern "C" int ngsep_bam_open(ngsep_ctx* c, const char* path, ngsep_bam** out) {
         }
         auto it = seq_index.find(name);
         // ReadAlignmentFileReader.loadHeader validation (:198-214)
-        if (it == seq_index.end()) {
-            std::fclose(b->f); delete b;
-            return set_error(c, NGSEP_E_FORMAT, "Inconsistent file header. Sequence " + name + " not present in the reference sequences");
-        }
-        if ((int64_t)c->seq_bases[it->second].size() != lref) {
-            std::fclose(b->f); delete b;
-            return set_error(c, NGSEP_E_FORMAT, "Inconsistent length in file header. Sequence " + name);
-        }
+        if (it == seq_index.end()) return fail(NGSEP_E_FORMAT, "Inconsistent file header. Sequence " + name + " not present in the reference sequences");
+        if ((int64_t)c->seq_bases[it->second].size() != lref) return fail(NGSEP_E_FORMAT, "Inconsistent length in file header. Sequence " + name);
         b->ref_to_seq.push_back(it->second);
     }
     // @RG lines
@@ -175,124 +432,253 @@ extern "C" int ngsep_bam_open(ngsep_ctx* c, const char* path, ngsep_bam** out) {
     return NGSEP_OK;
 }
 
+// Positions the reader at the first record that can overlap seq:first-last (1-based) through the BAI
+// index; records come in file order from there and next_batch stops after the last record starting at
+// or before `last` on that sequence.  Returns NGSEP_E_IO without an index, NGSEP_E_INVALID for an
+// unknown sequence.
+extern "C" int ngsep_bam_set_region(ngsep_bam* b, const char* seq_name, int64_t first, int64_t last) {
+    if (!b || !seq_name) return NGSEP_E_INVALID;
+    int32_t ref = -1;
+    for (size_t i = 0; i < b->ref_names.size(); i++) if (b->ref_names[i] == seq_name) ref = (int32_t)i;
+    if (ref < 0) return set_error(b->ctx, NGSEP_E_INVALID, std::string("sequence not in the BAM header: ") + seq_name);
+    if (!load_bai(b)) return set_error(b->ctx, NGSEP_E_IO, "no BAI index for " + b->path);
+    if (first < 1) first = 1;
+    if (last < first) last = first;
+    // the smallest record offset of a chunk that can hold records overlapping the region: chunks of the
+    // region's bins ending after the linear-index offset of its first 16 kb window, entered no earlier
+    // than that offset (every record before it ends before the window)
+    uint64_t start = UINT64_MAX;
+    if ((size_t)ref < b->bai.size()) {
+        const BaiRef& br = b->bai[(size_t)ref];
+        const int64_t w = (first - 1) >> 14;
+        const uint64_t min_off = br.lin.empty() ? 0 : br.lin[(size_t)std::min<int64_t>(w, (int64_t)br.lin.size() - 1)];
+        std::vector<uint32_t> bins;
+        reg2bins(first - 1, std::min<int64_t>(last, (int64_t)1 << 29), bins);
+        for (uint32_t bin : bins) {
+            auto it = br.bins.find(bin);
+            if (it == br.bins.end()) continue;
+            for (const auto& ch : it->second)
+                if (ch.second > min_off) start = std::min(start, std::max(ch.first, min_off));
+        }
+    }
+    stop_decoder(b);
+    b->buf = nullptr;
+    b->end = b->pos = 0;
+    b->have_last = false;
+    b->region_ref = ref;
+    b->region_last = last;
+    b->region_done = start == UINT64_MAX;       // no chunk: the region holds no record
+    if (b->region_done) { b->eof = true; return NGSEP_OK; }
+    if (std::fseek(b->f, (long)(start >> 16), SEEK_SET) != 0) return set_error(b->ctx, NGSEP_E_IO, "seek failed in " + b->path);
+    start_decoder(b);
+    std::string err;
+    if (!need(b, (size_t)(start & 0xFFFF), err)) return set_error(b->ctx, NGSEP_E_FORMAT, err.empty() ? "region start past the end of the file" : err);
+    b->pos = (size_t)(start & 0xFFFF);
+    return NGSEP_OK;
+}
+
 extern "C" int ngsep_bam_next_batch(ngsep_bam* b, int64_t max_reads, ngsep_read_batch* out) {
     if (!b || !out) return NGSEP_E_INVALID;
     static const int kOp[9] = {3, 2, 1, 5, 6, 0, 4, 3, 7};   // BAM M I D N S H P = X -> NGSEP H0 D1 I2 M3 P4 N5 S6 X7
     static const char kNt[] = "=ACMGRSVTWYHKDBN";
-    b->b_seq.clear(); b->b_first.clear(); b->b_flags.clear(); b->b_rg.clear(); b->b_cig_n.clear();
-    b->b_cigar.clear(); b->b_seqlen.clear(); b->b_cig_off.clear(); b->b_seq_off.clear(); b->b_hasq.clear();
-    b->b_bases.clear(); b->b_quals.clear();
     std::string err;
-    int64_t n = 0;
-    while (n < max_reads) {
-        if (!need(b, 4, err)) break;
-        int32_t bs = rd<int32_t>(&b->buf[b->pos]);
+    // 1. cut up to max_reads whole records (their offsets in buf), sequentially along the block_size chain
+    std::vector<size_t> roff;
+    // (more decoded bytes are only pulled in while no record is cut: pulling compacts the buffer)
+    while ((int64_t)roff.size() < max_reads && !b->region_done) {
+        if (b->end - b->pos < 4) {
+            if (!roff.empty()) break;
+            if (!need(b, 4, err)) break;
+        }
+        const int32_t bs = rd<int32_t>(&b->buf[b->pos]);
         if (bs < 32) return set_error(b->ctx, NGSEP_E_FORMAT, "malformed BAM record");
-        if (!need(b, 4 + (size_t)bs, err)) return set_error(b->ctx, NGSEP_E_FORMAT, "truncated BAM record");
-        const char* r = &b->buf[b->pos + 4];
+        if (b->end - b->pos < 4 + (size_t)bs) {
+            // the rest of this record is in the next chunk: decode the records cut so far first
+            if (!roff.empty()) break;
+            if (!need(b, 4 + (size_t)bs, err)) return set_error(b->ctx, NGSEP_E_FORMAT, err.empty() ? "truncated BAM record" : err);
+        }
+        const uint8_t* r = &b->buf[b->pos + 4];
+        if (b->region_ref >= 0) {
+            const int32_t refid = rd<int32_t>(r), pos0 = rd<int32_t>(r + 4);
+            if (refid != b->region_ref || (int64_t)pos0 + 1 > b->region_last) { b->region_done = true; break; }
+        }
+        roff.push_back(b->pos + 4);
         b->pos += 4 + (size_t)bs;
-        int32_t refid = rd<int32_t>(r);
-        int32_t pos0 = rd<int32_t>(r + 4);
-        uint8_t l_name = (uint8_t)r[8];
-        uint8_t mapq = (uint8_t)r[9];
-        uint16_t n_cig = rd<uint16_t>(r + 12);
-        uint16_t flag = rd<uint16_t>(r + 14);
-        int32_t l_seq = rd<int32_t>(r + 16);
-        const char* name = r + 32;
-        const char* cig = name + l_name;
-        const char* seq = cig + 4 * n_cig;
-        const char* qual = seq + (l_seq + 1) / 2;
-        const char* aux = qual + l_seq;
-        const char* end = r + bs;
-        int32_t start = pos0 + 1;
-        // isSameAlignment (ReadAlignmentFileReader.java:292-306)
-        int paired = (flag & 1) != 0, fop = (flag & 0x40) != 0;
-        std::string nm(name, l_name ? l_name - 1 : 0);
-        if (b->have_last && b->last_pos == start && b->last_paired == paired && (!paired || b->last_fop == fop) && b->last_name == nm) continue;
-        b->have_last = true; b->last_pos = start; b->last_paired = paired; b->last_fop = fop; b->last_name = nm;
-        if (flag & 0x4) continue;               // FLAG_READ_UNMAPPED (filtered)
-        if (refid < 0 || refid >= (int32_t)b->ref_to_seq.size()) continue;
-        // tags: NH and RG
-        int nh = 0, nh_present = 0, rg = -1;
-        for (const char* t = aux; t + 3 <= end;) {
-            char t0 = t[0], t1 = t[1], ty = t[2];
-            const char* v = t + 3;
-            size_t sz = 0;
-            long long iv = 0;
-            bool isint = true;
-            switch (ty) {
-                case 'A': case 'c': case 'C': sz = 1; iv = ty == 'c' ? (int8_t)v[0] : (uint8_t)v[0]; break;
-                case 's': sz = 2; iv = rd<int16_t>(v); break;
-                case 'S': sz = 2; iv = rd<uint16_t>(v); break;
-                case 'i': sz = 4; iv = rd<int32_t>(v); break;
-                case 'I': sz = 4; iv = rd<uint32_t>(v); break;
-                case 'f': sz = 4; isint = false; break;
-                case 'Z': case 'H': { isint = false; const char* z = v; while (z < end && *z) z++; sz = (size_t)(z - v) + 1; break; }
-                case 'B': {
-                    isint = false;
-                    char sub = v[0];
-                    int32_t cnt = rd<int32_t>(v + 1);
-                    int es = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
-                    sz = 5 + (size_t)cnt * es;
-                    break;
-                }
-                default: t = end; continue;
-            }
-            if (t0 == 'N' && t1 == 'H' && isint && ty != 'A') { nh = (int)iv; nh_present = 1; }
-            if (t0 == 'R' && t1 == 'G' && ty == 'Z') {
-                auto it = b->rg_index.find(std::string(v));
-                rg = it == b->rg_index.end() ? -1 : it->second;   // getReadGroup() is null if not in header
-            }
-            t = v + sz;
-        }
-        int flags = flag;
-        // isMultiple (:284-291)
-        bool multiple;
-        if (flag & 0x100) multiple = true;
-        else if (nh_present && nh > 1) multiple = true;
-        else if (nh_present && nh == 1) multiple = false;
-        else multiple = mapq < b->min_mq;
-        if (multiple) flags += 0x1000;
-        if (n_cig == 0) continue;               // mapped read without CIGAR: setCigarString throws
-        // CIGAR -> NGSEP codes with collapseEqualEvents
-        int64_t coff = (int64_t)b->b_cigar.size();
-        int read_len = 0;
-        bool bad = false;
-        int nc = 0;
-        for (int i = 0; i < n_cig; i++) {
-            uint32_t v = rd<uint32_t>(cig + 4 * i);
-            uint32_t op = v & 15, len = v >> 4;
-            if (op > 8) { bad = true; break; }
-            int nop = kOp[op];
-            if (nc > 0 && (b->b_cigar.back() & 7) == nop) b->b_cigar.back() += (int32_t)len * 8;
-            else { b->b_cigar.push_back((int32_t)len * 8 + nop); nc++; }
-            if (nop & 2) read_len += (int)len;
-        }
-        if (bad) { b->b_cigar.resize((size_t)coff); continue; }
-        if (l_seq > 0 && l_seq != read_len) { b->b_cigar.resize((size_t)coff); continue; }   // setReadCharacters throws
-        if ((flags & b->filter_flags) != 0) { b->b_cigar.resize((size_t)coff); continue; }
-        b->b_seq.push_back(b->ref_to_seq[refid]);
-        b->b_first.push_back(start);
-        b->b_flags.push_back(flags);
-        b->b_rg.push_back(rg);
-        b->b_cig_off.push_back(coff);
-        b->b_cig_n.push_back(nc);
-        b->b_seq_off.push_back((int64_t)b->b_bases.size());
-        b->b_seqlen.push_back(l_seq);
-        size_t so = b->b_bases.size();
-        b->b_bases.resize(so + (size_t)l_seq);
-        b->b_quals.resize(so + (size_t)l_seq);
-        for (int32_t i = 0; i < l_seq; i++) {
-            uint8_t byte = (uint8_t)seq[i >> 1];
-            b->b_bases[so + i] = kNt[(i & 1) ? (byte & 15) : (byte >> 4)];
-        }
-        bool hasq = l_seq > 0 && (uint8_t)qual[0] != 0xFF;
-        for (int32_t i = 0; i < l_seq; i++) b->b_quals[so + i] = hasq ? (char)((uint8_t)qual[i] + 33) : '!';
-        b->b_hasq.push_back(hasq ? 1 : 0);
-        n++;
     }
     if (!err.empty()) return set_error(b->ctx, NGSEP_E_FORMAT, err);
-    out->n_reads = n;
+    const int64_t n = (int64_t)roff.size();
+    // 2. per record: filters (isSameAlignment against the previous raw record, isMultiple, filter flags,
+    //    malformed CIGAR / read length) and output sizes -- in parallel
+    struct Rec { int32_t keep, ncig, lseq, flags, rg, seq, first; };
+    std::vector<Rec> rec((size_t)n);
+    const uint8_t* base = b->buf;
+    auto name_of = [&](size_t o) { return std::make_pair((const char*)base + o + 32, (size_t)(base[o + 8] ? base[o + 8] - 1 : 0)); };
+    parallel_for(n, 4096, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; i++) {
+            const uint8_t* r = base + roff[(size_t)i];
+            const int32_t refid = rd<int32_t>(r), pos0 = rd<int32_t>(r + 4);
+            const uint8_t l_name = r[8], mapq = r[9];
+            const uint16_t n_cig = rd<uint16_t>(r + 12), flag = rd<uint16_t>(r + 14);
+            const int32_t l_seq = rd<int32_t>(r + 16);
+            const int32_t bs = rd<int32_t>(r - 4);
+            Rec& o = rec[(size_t)i];
+            o.keep = 0;
+            o.first = pos0 + 1;
+            // isSameAlignment (ReadAlignmentFileReader.java:292-306) with the previous raw record
+            const int paired = (flag & 1) != 0, fop = (flag & 0x40) != 0;
+            bool same;
+            if (i == 0) {
+                same = b->have_last && b->last_pos == pos0 + 1 && b->last_paired == paired && (!paired || b->last_fop == fop) &&
+                       b->last_name.size() == (size_t)(l_name ? l_name - 1 : 0) &&
+                       std::memcmp(b->last_name.data(), r + 32, b->last_name.size()) == 0;
+            } else {
+                const uint8_t* pr = base + roff[(size_t)i - 1];
+                const uint16_t pflag = rd<uint16_t>(pr + 14);
+                const int pp = (pflag & 1) != 0, pf = (pflag & 0x40) != 0;
+                same = rd<int32_t>(pr + 4) == pos0 && pp == paired && (!paired || pf == fop) && pr[8] == l_name &&
+                       std::memcmp(pr + 32, r + 32, l_name) == 0;
+            }
+            if (same) continue;
+            if (flag & 0x4) continue;               // FLAG_READ_UNMAPPED (filtered)
+            if (refid < 0 || refid >= (int32_t)b->ref_to_seq.size()) continue;
+            const uint8_t* end = r + bs;
+            const uint8_t* cig = r + 32 + l_name;
+            const uint8_t* seq = cig + 4 * n_cig;
+            const uint8_t* qual = seq + (l_seq + 1) / 2;
+            const uint8_t* aux = qual + l_seq;
+            if (aux > end) continue;
+            // tags: NH and RG
+            int nh = 0, nh_present = 0, rg = -1;
+            for (const uint8_t* t = aux; t + 3 <= end;) {
+                const char t0 = (char)t[0], t1 = (char)t[1], ty = (char)t[2];
+                const uint8_t* v = t + 3;
+                size_t sz = 0;
+                long long iv = 0;
+                bool isint = true;
+                switch (ty) {
+                    case 'A': case 'c': case 'C': sz = 1; iv = ty == 'c' ? (int8_t)v[0] : (uint8_t)v[0]; break;
+                    case 's': sz = 2; iv = rd<int16_t>(v); break;
+                    case 'S': sz = 2; iv = rd<uint16_t>(v); break;
+                    case 'i': sz = 4; iv = rd<int32_t>(v); break;
+                    case 'I': sz = 4; iv = rd<uint32_t>(v); break;
+                    case 'f': sz = 4; isint = false; break;
+                    case 'Z': case 'H': { isint = false; const uint8_t* z = v; while (z < end && *z) z++; sz = (size_t)(z - v) + 1; break; }
+                    case 'B': {
+                        isint = false;
+                        const char sub = (char)v[0];
+                        const int32_t cnt = rd<int32_t>(v + 1);
+                        const int es = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
+                        sz = 5 + (size_t)cnt * es;
+                        break;
+                    }
+                    default: t = end; continue;
+                }
+                if (t0 == 'N' && t1 == 'H' && isint && ty != 'A') { nh = (int)iv; nh_present = 1; }
+                if (t0 == 'R' && t1 == 'G' && ty == 'Z') {
+                    auto it = b->rg_index.find(std::string((const char*)v));
+                    rg = it == b->rg_index.end() ? -1 : it->second;   // getReadGroup() is null if not in header
+                }
+                t = v + sz;
+            }
+            int flags = flag;
+            // isMultiple (:284-291)
+            bool multiple;
+            if (flag & 0x100) multiple = true;
+            else if (nh_present && nh > 1) multiple = true;
+            else if (nh_present && nh == 1) multiple = false;
+            else multiple = mapq < b->min_mq;
+            if (multiple) flags += 0x1000;
+            if (n_cig == 0) continue;               // mapped read without CIGAR: setCigarString throws
+            // CIGAR -> NGSEP codes with collapseEqualEvents
+            int read_len = 0, nc = 0, prev = -1;
+            bool bad = false;
+            for (int k = 0; k < n_cig; k++) {
+                const uint32_t v = rd<uint32_t>(cig + 4 * k);
+                const uint32_t op = v & 15;
+                if (op > 8) { bad = true; break; }
+                const int nop = kOp[op];
+                if (nop != prev) { nc++; prev = nop; }
+                if (nop & 2) read_len += (int)(v >> 4);
+            }
+            if (bad) continue;
+            if (l_seq > 0 && l_seq != read_len) continue;   // setReadCharacters throws
+            if ((flags & b->filter_flags) != 0) continue;
+            o.keep = 1;
+            o.ncig = nc;
+            o.lseq = l_seq;
+            o.flags = flags;
+            o.rg = rg;
+            o.seq = b->ref_to_seq[(size_t)refid];
+        }
+    });
+    if (n > 0) {        // the last raw record of this batch is the next batch's "previous"
+        const uint8_t* r = base + roff[(size_t)n - 1];
+        const uint16_t flag = rd<uint16_t>(r + 14);
+        b->have_last = true;
+        b->last_pos = rd<int32_t>(r + 4) + 1;
+        b->last_paired = (flag & 1) != 0;
+        b->last_fop = (flag & 0x40) != 0;
+        auto nm = name_of(roff[(size_t)n - 1]);
+        b->last_name.assign(nm.first, nm.second);
+    }
+    // 3. output offsets of the kept records, then their fields in parallel
+    std::vector<int64_t> oidx((size_t)n + 1, 0), coff((size_t)n + 1, 0), soff((size_t)n + 1, 0);
+    for (int64_t i = 0; i < n; i++) {
+        const Rec& o = rec[(size_t)i];
+        oidx[(size_t)i + 1] = oidx[(size_t)i] + o.keep;
+        coff[(size_t)i + 1] = coff[(size_t)i] + (o.keep ? o.ncig : 0);
+        soff[(size_t)i + 1] = soff[(size_t)i] + (o.keep ? o.lseq : 0);
+    }
+    const int64_t nk = oidx[(size_t)n];
+    b->b_seq.resize((size_t)nk); b->b_first.resize((size_t)nk); b->b_flags.resize((size_t)nk); b->b_rg.resize((size_t)nk);
+    b->b_cig_off.resize((size_t)nk); b->b_cig_n.resize((size_t)nk); b->b_seq_off.resize((size_t)nk); b->b_seqlen.resize((size_t)nk);
+    b->b_hasq.resize((size_t)nk);
+    b->b_cigar.resize((size_t)coff[(size_t)n]);
+    b->b_bases.resize((size_t)soff[(size_t)n]);
+    b->b_quals.resize((size_t)soff[(size_t)n]);
+    parallel_for(n, 4096, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; i++) {
+            const Rec& o = rec[(size_t)i];
+            if (!o.keep) continue;
+            const size_t k = (size_t)oidx[(size_t)i];
+            const uint8_t* r = base + roff[(size_t)i];
+            const uint8_t l_name = r[8];
+            const uint16_t n_cig = rd<uint16_t>(r + 12);
+            const int32_t l_seq = o.lseq;
+            const uint8_t* cig = r + 32 + l_name;
+            const uint8_t* seq = cig + 4 * n_cig;
+            const uint8_t* qual = seq + (l_seq + 1) / 2;
+            b->b_seq[k] = o.seq;
+            b->b_first[k] = o.first;
+            b->b_flags[k] = o.flags;
+            b->b_rg[k] = o.rg;
+            b->b_cig_off[k] = coff[(size_t)i];
+            b->b_cig_n[k] = o.ncig;
+            int32_t* cd = &b->b_cigar[(size_t)coff[(size_t)i]];
+            int nc = 0;
+            for (int c2 = 0; c2 < n_cig; c2++) {
+                const uint32_t v = rd<uint32_t>(cig + 4 * c2);
+                const int nop = kOp[v & 15];
+                if (nc > 0 && (cd[nc - 1] & 7) == nop) cd[nc - 1] += (int32_t)(v >> 4) * 8;
+                else cd[nc++] = (int32_t)(v >> 4) * 8 + nop;
+            }
+            b->b_seq_off[k] = soff[(size_t)i];
+            b->b_seqlen[k] = l_seq;
+            char* bs = &b->b_bases[(size_t)soff[(size_t)i]];
+            char* qs = &b->b_quals[(size_t)soff[(size_t)i]];
+            for (int32_t j = 0; j + 1 < l_seq; j += 2) {
+                const uint8_t byte = seq[j >> 1];
+                bs[j] = kNt[byte >> 4];
+                bs[j + 1] = kNt[byte & 15];
+            }
+            if (l_seq & 1) bs[l_seq - 1] = kNt[seq[(l_seq - 1) >> 1] >> 4];
+            const bool hasq = l_seq > 0 && qual[0] != 0xFF;
+            if (hasq) for (int32_t j = 0; j < l_seq; j++) qs[j] = (char)(qual[j] + 33);
+            else std::memset(qs, '!', (size_t)l_seq);
+            b->b_hasq[k] = hasq ? 1 : 0;
+        }
+    });
+    out->n_reads = nk;
     out->seq_id = b->b_seq.data();
     out->first = b->b_first.data();
     out->flags = b->b_flags.data();
@@ -305,26 +691,36 @@ extern "C" int ngsep_bam_next_batch(ngsep_bam* b, int64_t max_reads, ngsep_read_
     out->bases = b->b_bases.data();
     out->quals = b->b_quals.data();
     out->has_quals = b->b_hasq.data();
+    // a batch with every record filtered is not the end of the file: the caller stops at n_reads == 0
+    if (nk == 0 && n > 0) return ngsep_bam_next_batch(b, max_reads, out);
     return NGSEP_OK;
 }
 
 extern "C" int ngsep_bam_close(ngsep_bam* b) {
     if (!b) return NGSEP_E_INVALID;
+    stop_decoder(b);
     if (b->f) std::fclose(b->f);
     delete b;
     return NGSEP_OK;
 }
 
 namespace ngsep {
-// SingleSampleVariantsDetector.findSNVS (:896-931) + onSequenceEnd/saveSequenceVariants (:933-968, :1026-1032)
+// SingleSampleVariantsDetector.findSNVS (:896-931) + onSequenceEnd/saveSequenceVariants (:933-968, :1026-1032).
+// With -querySeq the reader jumps to the region through the BAI index when there is one (the reference
+// decodes the file from its start, AlignmentsPileupGenerator.java:310-322, 342-354); reading stops once the
+// query region is done either way.
 int call_bam(ngsep_ctx* c, const char* bam_path, const char* out_vcf) {
     ngsep_bam* b = nullptr;
     int rc = ngsep_bam_open(c, bam_path, &b);
     if (rc != NGSEP_OK) return rc;
+    if (c->params.query_seq[0]) {
+        const int r = ngsep_bam_set_region(b, c->params.query_seq, std::max<int64_t>(1, c->params.query_first), c->params.query_last);
+        if (r != NGSEP_OK && r != NGSEP_E_IO) { ngsep_bam_close(b); return r; }   // no index: stream from the start
+    }
     rc = ngsep_write_vcf_header(c, out_vcf);
     if (rc != NGSEP_OK) { ngsep_bam_close(b); return rc; }
     ngsep_read_batch batch;
-    while (true) {
+    while (!c->query_done) {
         rc = ngsep_bam_next_batch(b, 1 << 20, &batch);
         if (rc != NGSEP_OK) break;
         if (batch.n_reads == 0) break;
@@ -365,6 +761,22 @@ extern "C" int ngsep_coverage_bam(ngsep_ctx* c, const char* bam_path, const char
 extern "C" int ngsep_call_bam(ngsep_ctx* c, const char* bam_path, const char* out_vcf_path) {
     if (!c || !bam_path || !out_vcf_path) return NGSEP_E_INVALID;
     return ngsep::call_bam(c, bam_path, out_vcf_path);
+}
+
+// findSNVS restricted to seq:first-last (-querySeq/-first/-last) through the BAI index: the per-region
+// caller of the sharded drivers (every rank reads only its sequences' blocks of the BAM)
+extern "C" int ngsep_call_region_bam(ngsep_ctx* c, const char* bam_path, const char* seq, int64_t first, int64_t last,
+                                     const char* out_vcf_path) {
+    if (!c || !bam_path || !seq || !out_vcf_path || std::strlen(seq) >= sizeof c->params.query_seq) return NGSEP_E_INVALID;
+    if (c->cur_seq >= 0 || c->query_found) return set_error(c, NGSEP_E_INVALID, "ngsep_call_region_bam needs a context without alignments");
+    const ngsep_params saved = c->params;
+    std::snprintf(c->params.query_seq, sizeof c->params.query_seq, "%s", seq);
+    c->params.query_first = (int32_t)std::max<int64_t>(0, std::min<int64_t>(first, INT32_MAX));
+    c->params.query_last = (int32_t)std::max<int64_t>(0, std::min<int64_t>(last, INT32_MAX));
+    const int rc = ngsep::call_bam(c, bam_path, out_vcf_path);
+    c->params = saved;
+    c->query_found = c->query_done = false;
+    return rc;
 }
 
 // ---- MultisampleVariantsDetector.run on BAM files (discovery/MultisampleVariantsDetector.java:421-459) ----

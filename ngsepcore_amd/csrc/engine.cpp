@@ -514,14 +514,14 @@ static int choose_tile(const std::vector<int32_t>& m16, int64_t g_len, std::vect
     return bestT;
 }
 
-// Single-sample layout.  Each tile's reads (clipped to the tile) are packed into
-// rows by greedy interval colouring in pending-list order: a read takes a row whose previous read ended
-// before it starts, so rows_t equals the maximum depth inside the tile.  Three products per tile:
-//   * the bit planes (KT): row r holds W = T/32 words of "valid call" bits, then W words of "valid call
-//     of another allele" bits; the tile's planes start at word off_t / 16;
-//   * the position-major byte pile (KP): position p's rows_t codes at off_t + p * rows_t;
-//   * the tile's read segments in pending-list order (KP's summation order): row << 18 | a << 9 | b,
-//     the read covers tile positions a..b in that row.
+// Single-sample layout: tiles of T positions; tile t has rows_t = its maximum depth
+// and, at every position p, the codes of the reads covering p in pending-list order -- the order in which
+// PileupRecord.getAlleleCalls (PileupRecord.java:126-152) visits them -- in ranks 0, 1, ... (rank r at p is
+// the r-th covering read).  Three products per tile:
+//   * the bit planes (KT): rank row r holds W = T/32 words of "valid call" bits, then W words of "valid
+//     call of another allele than the reference" bits; the tile's planes start at word off_t / 16;
+//   * the position-major byte pile (KP): position p's rows_t codes at off_t + p * rows_t, rank order;
+//   * the strand bits (KP, countsStrand): bit off_t + p * rows_t + r = the rank-r read is reverse.
 // Tiles are independent: built on all host threads.
 static int build_single_layout(Staged& s, const std::vector<SRead>& reads) {
     const int64_t g_len = s.g_len, nreads = (int64_t)reads.size();
@@ -543,7 +543,6 @@ static int build_single_layout(Staged& s, const std::vector<SRead>& reads) {
         off += (int64_t)rows[(size_t)t] * T;
         rmax = std::max(rmax, rows[(size_t)t]);
     }
-    if (rmax >= (1 << 14)) return -1;      // segment rows are 14-bit
     s.pile_bytes = off;
     s.tile_rows_max = rmax;
     // first read that can reach tile t (reads are sorted by global first position)
@@ -551,29 +550,14 @@ static int build_single_layout(Staged& s, const std::vector<SRead>& reads) {
         const int64_t lo_pos = t * T - s.max_span;
         return std::lower_bound(reads.begin(), reads.end(), lo_pos, [](const SRead& r, int64_t v) { return (int64_t)r.gfirst <= v; }) - reads.begin();
     };
-    // segments per tile (reads overlapping it), then their offsets
-    s.h_tseg.assign((size_t)ntiles + 1, 0);
-    parallel_for(ntiles, 512, [&](int64_t t0, int64_t t1) {
-        int64_t r = first_read(t0);
-        for (int64_t t = t0; t < t1; t++) {
-            const int32_t tstart = (int32_t)(t * T), tend = tstart + T;
-            while (r < nreads && (int64_t)reads[(size_t)r].gfirst <= (int64_t)tstart - s.max_span) r++;
-            int32_t n = 0;
-            for (int64_t k = r; k < nreads && reads[(size_t)k].gfirst < tend; k++)
-                if (reads[(size_t)k].glast >= tstart && reads[(size_t)k].glast >= reads[(size_t)k].gfirst) n++;
-            s.h_tseg[(size_t)t + 1] = rows[(size_t)t] ? n : 0;
-        }
-    });
-    for (int64_t t = 0; t < ntiles; t++) s.h_tseg[(size_t)t + 1] += s.h_tseg[(size_t)t];
-    s.h_seg.alloc((size_t)s.h_tseg[(size_t)ntiles]);
-    s.h_segneg.alloc((size_t)s.h_tseg[(size_t)ntiles]);
     s.h_cpile.alloc((size_t)off);
     s.h_planes.alloc((size_t)(off / 16));
+    s.h_cneg.alloc((size_t)(off / 32));
     const int W = T / 32;
     const uint8_t* ref = s.h_ref.data();
+    std::atomic<int> bad{0};
     parallel_for(ntiles, 256, [&](int64_t t0, int64_t t1) {
-        std::vector<std::pair<int32_t, int32_t>> heap;   // (last clipped position, row): min-heap
-        std::vector<int32_t> free_rows;
+        std::vector<int32_t> fill((size_t)T);
         int64_t r_lo = first_read(t0);
         for (int64_t t = t0; t < t1; t++) {
             const int32_t nrow = rows[(size_t)t];
@@ -583,46 +567,35 @@ static int build_single_layout(Staged& s, const std::vector<SRead>& reads) {
             const int64_t toff = s.h_tinfo[(size_t)t].off;
             uint8_t* col = s.h_cpile.p + toff;
             uint32_t* pl = s.h_planes.p + toff / 16;
+            uint32_t* ng = s.h_cneg.p + toff / 32;
             std::memset(col, 0, (size_t)nrow * T);
             std::memset(pl, 0, (size_t)nrow * T / 4);
-            uint32_t* seg = s.h_seg.p + s.h_tseg[(size_t)t];
-            uint8_t* segneg = s.h_segneg.p + s.h_tseg[(size_t)t];
-            heap.clear();
-            free_rows.clear();
-            int32_t next_row = 0;
+            std::memset(ng, 0, (size_t)nrow * T / 8);
+            std::fill(fill.begin(), fill.end(), 0);
             for (int64_t r = r_lo; r < nreads && reads[(size_t)r].gfirst < tend; r++) {
                 const SRead& rd = reads[(size_t)r];
                 if (rd.glast < tstart || rd.glast < rd.gfirst) continue;
                 const int32_t a = std::max(rd.gfirst, tstart) - tstart, b = std::min(rd.glast, tend - 1) - tstart;
-                while (!heap.empty() && heap.front().first < a) {
-                    free_rows.push_back(heap.front().second);
-                    std::pop_heap(heap.begin(), heap.end(), std::greater<>());
-                    heap.pop_back();
-                }
-                int32_t row;
-                if (!free_rows.empty()) { row = free_rows.back(); free_rows.pop_back(); }
-                else row = next_row++;
-                heap.push_back({b, row});
-                std::push_heap(heap.begin(), heap.end(), std::greater<>());
-                *seg++ = (uint32_t)row << 18 | (uint32_t)a << 9 | (uint32_t)b;
-                *segneg++ = rd.neg;
                 const uint8_t* src = rd.bytes + (tstart + a - rd.gfirst);
-                uint32_t* pv = pl + (size_t)row * 2 * W;
-                uint32_t* pn = pv + W;
                 for (int32_t p = a; p <= b; p++) {
+                    const int32_t rank = fill[(size_t)p]++;
+                    if (rank >= nrow) { bad = 1; continue; }
                     const uint8_t cd = src[p - a];
+                    const int64_t cell = (int64_t)p * nrow + rank;
+                    col[cell] = cd;
+                    if (rd.neg) ng[cell >> 5] |= 1u << (cell & 31);
                     if (cd & kCodeValid) {
                         const uint8_t rc = ref[tstart + p];
                         const uint8_t ra = (rc & kRefCallable) ? (uint8_t)((rc >> 5) & 3) : 0;
+                        uint32_t* pv = pl + (size_t)rank * 2 * W;
                         pv[p >> 5] |= 1u << (p & 31);
-                        if (((cd >> 5) & 3) != ra) pn[p >> 5] |= 1u << (p & 31);
+                        if (((cd >> 5) & 3) != ra) pv[W + (p >> 5)] |= 1u << (p & 31);
                     }
-                    col[(size_t)p * nrow + row] = cd;
                 }
             }
         }
     });
-    return 0;
+    return bad ? -1 : 0;
 }
 
 // Multisample layout: the same tiles of T positions, one block per (tile, sample) holding that
@@ -880,7 +853,7 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
         s.n_reads = nreads;
         s.n_read_bases = nbases;
         if (build_single_layout(s, reads) != 0)
-            return set_error(c, NGSEP_E_UNSUPPORTED, "a pileup tile deeper than 16383 alignments");
+            return set_error(c, NGSEP_E_INVALID, "internal error: pileup depth above the tile's row count");
         c->stats.slot_bytes = 0;
         c->stats.slot_size = 0;
     } else {
@@ -966,9 +939,7 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     std::vector<int32_t>().swap(s.h_bbase);
     s.h_planes.release();
     s.h_cpile.release();
-    s.h_seg.release();
-    s.h_segneg.release();
-    std::vector<int32_t>().swap(s.h_tseg);
+    s.h_cneg.release();
     return NGSEP_OK;
 }
 

@@ -253,13 +253,11 @@ struct Staged {            // everything resident for one run
     std::vector<int32_t> h_perm, h_bseg, h_blb, h_bbase;
     int64_t nblk_b = 0;
     std::vector<uint8_t> h_ref;
-    // single-sample layout (engine.cpp build_single_layout): bit planes, position-major byte pile,
-    // per-tile read segments in pending order
+    // single-sample layout (engine.cpp build_single_layout): bit planes, position-major byte pile in
+    // pending-list rank order, strand bits of its cells
     HostArray<uint32_t> h_planes;
     HostArray<uint8_t> h_cpile;
-    HostArray<uint32_t> h_seg;
-    HostArray<uint8_t> h_segneg;        // per segment: 1 = the read is on the negative strand
-    std::vector<int32_t> h_tseg;        // tile t's segments: h_seg[h_tseg[t] .. h_tseg[t+1])
+    HostArray<uint32_t> h_cneg;
     bool single = false;                // the single-sample layout (else the multisample one)
 };
 

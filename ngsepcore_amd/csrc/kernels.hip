@@ -49,6 +49,7 @@ struct RunSlot {                     // one in-flight single-sample run (see dev
     int64_t cap_hard = 0;
     ngsep_site_out* d_brec = nullptr;        // KP's records by position bucket: bucket b = d_brec[b * bcap ..]
     int32_t* d_bcount = nullptr;             // records per bucket (zeroed by KT)
+    int32_t* d_boff = nullptr;               // output offset per bucket (KS)
     int64_t nb_cap = 0, brec_cap = 0;
     LikTables* d_tables = nullptr;
     LikTables h_tables{};                    // last uploaded tables
@@ -82,9 +83,7 @@ struct Device {
     uint8_t* d_slots = nullptr;      // multisample: read-major SoA
     uint8_t* d_pile = nullptr;       // single sample: position-major byte pile; multisample: per-sample blocks
     uint32_t* d_planes = nullptr;    // single sample: bit planes of the pile (KT)
-    uint32_t* d_seg = nullptr;       // single sample: per-tile read segments in pending order (KP)
-    uint8_t* d_segneg = nullptr;     // their strands
-    int32_t* d_tseg = nullptr;       // tile t's segments: [tseg[t], tseg[t+1])
+    uint32_t* d_cneg = nullptr;      // single sample: strand bits of the pile's cells (KP)
     int4* d_wins = nullptr;          // windows {global start of w0, w0, seq_id, wlen}, ascending (KO maps records)
     int32_t n_wins = 0;
     int32_t planes_W = 0;            // words per plane row (T / 32)
@@ -105,7 +104,7 @@ struct Device {
     int64_t cap_psites = 0;
     unsigned long long* d_stamps = nullptr;   // diagnostics (NGSEP_TIMING)
     LikTables* d_tables = nullptr;
-    int32_t ko_shift = 12, ko_bcap = 64;   // 2^ko_shift positions per bucket (grown on overflow)
+    int32_t ko_shift = 14, ko_bcap = 64;   // 2^ko_shift positions per bucket (grown on overflow)
     QueueSite* d_hard = nullptr;
     int64_t cap_hard = 0;
     unsigned long long* d_counters = nullptr;
@@ -163,144 +162,93 @@ static_assert(sizeof(QueueSite) == 8, "QueueSite layout");
 
 
 // ------------------------------------------------------------------------------------------
-// KP: exact tally + posterior + SNVQ call of the queued candidates (one wavefront per site)
+// KP: exact tally + posterior + SNVQ call of the queued candidates -- one lane per site
 // ------------------------------------------------------------------------------------------
-// CountsHelper.calculateCountsSNV/updateCounts (discovery/CountsHelper.java:83-95,209-251) over the
-// reads covering gpos in pending-list order, so the fp64 sums are bit-identical to the reference's;
-// then getPosteriorProbabilities (:410-495), VariantDiscoverySNVQAlgorithm.discoverSNV (:100-243) and
-// the listener filters (SingleSampleVariantPileupListener.java:213-232).
-// The reads of gpos's tile are its segments, stored in pending-list order (row << 18 | a << 9 | b, the
-// strand in a parallel bitmap); the site's codes are one contiguous column of the position-major byte
-// pile (rows_t bytes at off_t + p * rows_t).  Lane j takes segment j of a 64-segment chunk: covered
-// (a <= p <= b) -> its row's code.  A site therefore reads its tile's segment list (~0.5 KB at 30x) and
-// one column line, not one cache line per read.  Integer counts come from ballots; the valid codes are
-// compacted in LDS in lane (= pending) order and ten lanes each add one of the ten log-likelihood sums.
-// Lane 0 appends each emitted record to the bucket of its position (KO orders them).
-__device__ __forceinline__ double readlane_d(double v, int l) {
-    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
-    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
+// The codes of the reads covering gpos are one contiguous column of the position-major byte pile,
+// already in pending-list rank order (engine.cpp build_single_layout), and their strands the matching
+// bits of the strand array.  A lane walks its site's column in rank order and runs
+// CountsHelper.calculateCountsSNV/updateCounts (discovery/CountsHelper.java:83-95,209-251): the ten
+// fp64 log-likelihood sums get their addends in the reference's order, so they are bit-identical; then
+// getPosteriorProbabilities / calculatePosteriorProbabilities (:410-495, events in Java's order, the
+// normaliser summed in that order), VariantDiscoverySNVQAlgorithm.discoverSNV / getIndexesMaxGenotype
+// (:100-243) and the listener filters (SingleSampleVariantPileupListener.java:213-232).  No cross-lane
+// work: every lane of the wave does useful fp64 work on its own site.  An emitted record goes to the
+// bucket of its position (KO orders the buckets).
+__device__ inline double pow10_j(double x) { return pow(10.0, x); }   // Math.pow(10.0, x)
 
-constexpr int kPostWaves = 4;
-__global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* __restrict__ queue, const unsigned long long* qn,
+constexpr int kPostThreads = 256;
+__global__ __launch_bounds__(kPostThreads) void k_posterior(const QueueSite* __restrict__ queue, const unsigned long long* qn,
                                                    int64_t qcap, const TileInfo* __restrict__ tinfo,
-                                                   const int32_t* __restrict__ tseg, const uint32_t* __restrict__ seg,
-                                                   const uint8_t* __restrict__ segneg, const uint8_t* __restrict__ cpile,
+                                                   const uint8_t* __restrict__ cpile, const uint32_t* __restrict__ cneg,
                                                    int32_t log2T, const LikTables* __restrict__ tabs, GenotypeParams gp,
                                                    ngsep_site_out* __restrict__ brec, int32_t* __restrict__ bcount,
                                                    int shift, int32_t bcap) {
-    __shared__ double s_t[3][32];
-    __shared__ uint8_t s_code[kPostWaves][64];      // a chunk's valid codes in pending order
-    __shared__ uint32_t s_rec[kPostWaves][sizeof(ngsep_site_out) / 4];   // the record awaiting its bucket slot
+    __shared__ double s_t[3][32];   // A (log10(1-e)), H (heterozygous), E (error) per capped quality
+    __shared__ double s_ev[16][kPostThreads];   // each lane's 16 genotype events (posterior phase)
     if (threadIdx.x < 96)
         s_t[threadIdx.x >> 5][threadIdx.x & 31] =
             (threadIdx.x < 32 ? tabs->A : threadIdx.x < 64 ? tabs->H : tabs->E)[threadIdx.x & 31];
     __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int32_t Tm = (1 << log2T) - 1;
     int64_t n = (int64_t)*qn;
     if (n > qcap) n = qcap;
-    const int64_t nwaves = (int64_t)gridDim.x * kPostWaves;
-    // lane k < 10 owns one of the ten log-likelihood sums (k: L00 L11 L22 L33 L01 L02 L03 L12 L13 L23):
-    // a read of allele a adds table tm[q] when bit a of am is set, else E[q] (CountsHelper.java:231-248)
-    const uint32_t am = lane < 4 ? 1u << lane : lane < 10 ? (0xCA6953u >> (4 * (lane - 4))) & 15u : 0u;
-    const int tm = lane < 4 ? 0 : 1;
-    // the wave's staged record (s_rec[wv]) and its bucket slot request; lanes 0..37 store it
-    bool pending = false;
-    int32_t pend_k = 0, pend_bk = 0;
-    auto flush_pending = [&]() {
-        if (!pending) return;
-        const int32_t k = __builtin_amdgcn_readfirstlane(pend_k);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        constexpr int RW = sizeof(ngsep_site_out) / 4;
-        if (k < bcap && lane < RW) reinterpret_cast<uint32_t*>(brec + (int64_t)pend_bk * bcap + k)[lane] = s_rec[wv][lane];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        pending = false;
-    };
-    // software pipeline over this wave's sites: the next site's queue entry, tile descriptor and segment
-    // range load during the current site's walk, its first segment chunk during the current posterior
-    int64_t i = (int64_t)blockIdx.x * kPostWaves + wv;
-    QueueSite qs = i < n ? queue[i] : QueueSite{0, 0};
-    int32_t t_c = qs.gpos >> log2T;
-    TileInfo ti_c = i < n ? tinfo[t_c] : TileInfo{0, 0, 0};
-    int32_t s0_c = i < n ? tseg[t_c] : 0, s1_c = i < n ? tseg[t_c + 1] : 0;
-    uint32_t sg_c = s0_c + lane < s1_c ? seg[s0_c + lane] : 0u;
-    QueueSite qs_n = i + nwaves < n ? queue[i + nwaves] : QueueSite{0, 0};
-    for (; i < n; i += nwaves) {
-        const int32_t gpos = __builtin_amdgcn_readfirstlane(qs.gpos);
-        const uint32_t rc = (uint32_t)__builtin_amdgcn_readfirstlane(qs.rc);
-        const int32_t p = gpos & Tm;
-        const int32_t rows = __builtin_amdgcn_readfirstlane(ti_c.rows);
-        const int64_t coff = ((int64_t)__builtin_amdgcn_readfirstlane((int32_t)(ti_c.off >> 32)) << 32 |
-                              (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)ti_c.off)) + (int64_t)p * rows;
-        const int32_t s0 = __builtin_amdgcn_readfirstlane(s0_c), s1 = __builtin_amdgcn_readfirstlane(s1_c);
-        // next site's descriptor
-        const bool more = i + nwaves < n;
-        const int32_t t_n = qs_n.gpos >> log2T;
-        const TileInfo ti_n = more ? tinfo[t_n] : TileInfo{0, 0, 0};
-        const int32_t s0_n = more ? tseg[t_n] : 0, s1_n = more ? tseg[t_n + 1] : 0;
-        const QueueSite qs_nn = i + 2 * nwaves < n ? queue[i + 2 * nwaves] : QueueSite{0, 0};
+    const int64_t stride = (int64_t)gridDim.x * kPostThreads;
+    for (int64_t i = (int64_t)blockIdx.x * kPostThreads + threadIdx.x; i < n; i += stride) {
+        const QueueSite qs = queue[i];
+        const int32_t gpos = qs.gpos;
+        const uint32_t rc = (uint32_t)qs.rc;
+        const TileInfo ti = tinfo[gpos >> log2T];
+        const int32_t rows = ti.rows;
+        const int64_t base = ti.off + (int64_t)(gpos & Tm) * rows;
+        // tally in rank (= pending-list) order
         int32_t total = 0;
         int32_t cnt[4] = {0, 0, 0, 0};
         int32_t sc[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
-        double acc = 0;                                   // this lane's log-likelihood sum
-        uint32_t sg = sg_c;
-        for (int32_t j0 = s0; j0 < s1; j0 += 64) {
-            const int32_t j = j0 + lane;
-            const uint32_t sg_next = j + 64 < s1 ? seg[j + 64] : 0u;
-            const int32_t a = (int32_t)((sg >> 9) & 511u), b = (int32_t)(sg & 511u), row = (int32_t)(sg >> 18);
-            const bool cov = j < s1 && a <= p && p <= b;
-            const uint32_t code = cov ? (uint32_t)cpile[coff + row] : 0u;
-            const bool neg = cov && segneg[j] != 0;
-            total += __popcll(__ballot(code != 0));                       // CountsHelper.java:210
-            const bool valid = (code & 0x80u) != 0;                       // q<=3 or not A/C/G/T: not counted (:214-221)
-            const uint32_t al = (code >> 5) & 3u;
-            const unsigned long long negm = __ballot(neg);
+        // L00 L01 L02 L03 L11 L12 L13 L22 L23 L33 (upper triangle, ngsep_site_out.logc order)
+        double L[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        // the column's dwords in order (rank r = byte sh + r of the dword stream), the strand bits from the
+        // matching words; a small loop, so the kernel's code stays in the instruction cache
+        {
+            const uint32_t* cw = reinterpret_cast<const uint32_t*>(cpile) + (base >> 2);
+            const int sh = (int)(base & 3);
+            const int nd = (rows + sh + 3) >> 2;
+            uint32_t dn = nd > 0 ? cw[0] : 0u;
+            for (int k = 0; k < nd; k++) {
+                const uint32_t d = dn;
+                dn = k + 1 < nd ? cw[k + 1] : 0u;                          // the next dword is in flight
 #pragma unroll
-            for (int t = 0; t < 4; t++) {
-                const unsigned long long m = __ballot(valid && al == (uint32_t)t);
-                cnt[t] += __popcll(m);
-                sc[t][0] += __popcll(m & negm);                           // countsStrand[idx][neg?0:1] (:226-227)
-                sc[t][1] += __popcll(m & ~negm);
-            }
-            const unsigned long long mv = __ballot(valid);
-            // updateCounts (:231-248) in pending order: the valid codes are compacted in LDS, then each
-            // of the ten sum lanes adds its term of every read in turn (each sum's order of additions is
-            // the reference's)
-            const int32_t nv = __popcll(mv);
-            const int32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mv >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mv, 0u));
-            if (valid) s_code[wv][rank] = (uint8_t)code;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (lane < 10) {
-#pragma unroll 4
-                for (int32_t k = 0; k < nv; k++) {
-                    const uint32_t cd = s_code[wv][k];
+                for (int e = 0; e < 4; e++) {
+                    const int r = 4 * k + e - sh;                          // rank of this byte
+                    const uint32_t cd = (r >= 0 && r < rows) ? (d >> (8 * e)) & 0xFFu : 0u;
+                    if (cd == 0) continue;
+                    total++;                                              // CountsHelper.java:210
+                    if (!(cd & 0x80u)) continue;                          // q<=3 or not A/C/G/T (:214-221)
+                    const int a = (int)((cd >> 5) & 3u);
                     int q = (int)(cd & 31u);
                     q = q > gp.max_q ? gp.max_q : q;                      // -maxBaseQS (:217-219)
-                    acc += s_t[((am >> ((cd >> 5) & 3u)) & 1u) ? tm : 2][q];
+                    const int64_t cell = base + r;
+                    const int neg = (int)((cneg[cell >> 5] >> (cell & 31)) & 1u);
+#pragma unroll
+                    for (int t = 0; t < 4; t++) {                         // constant indices: registers, not scratch
+                        cnt[t] += a == t ? 1 : 0;
+                        sc[t][0] += (a == t && neg) ? 1 : 0;              // countsStrand[idx][neg?0:1] (:226-227)
+                        sc[t][1] += (a == t && !neg) ? 1 : 0;
+                    }
+                    const double A = s_t[0][q], H = s_t[1][q], E = s_t[2][q];
+                    // updateCounts (:231-248): [i][i] += i==idx ? A : E; [i][j] += (i==idx || j==idx) ? H : E
+                    L[0] += a == 0 ? A : E;
+                    L[1] += (a == 0 || a == 1) ? H : E;
+                    L[2] += (a == 0 || a == 2) ? H : E;
+                    L[3] += (a == 0 || a == 3) ? H : E;
+                    L[4] += a == 1 ? A : E;
+                    L[5] += (a == 1 || a == 2) ? H : E;
+                    L[6] += (a == 1 || a == 3) ? H : E;
+                    L[7] += a == 2 ? A : E;
+                    L[8] += (a == 2 || a == 3) ? H : E;
+                    L[9] += a == 3 ? A : E;
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            sg = sg_next;
         }
-        // the next site's first segment chunk loads during this site's posterior
-        sg_c = more && s0_n + lane < s1_n ? seg[s0_n + lane] : 0u;
-        qs = qs_n;
-        qs_n = qs_nn;
-        ti_c = ti_n;
-        s0_c = s0_n;
-        s1_c = s1_n;
         if (total == 0 || (gp.ablate & 8)) continue;                      // VariantDiscoverySNVQAlgorithm.java:101-103
         const bool callable = (rc & 0x80u) != 0;
         int8_t genotype = -1, alt = -1, third = -1, nal = 0;
@@ -308,51 +256,63 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
         bool keep = false;
         if (callable) {
             const int refIdx = (int)((rc >> 5) & 3u);
-            // getPosteriorProbabilities (CountsHelper.java:410-443), one event per lane k < 16 in Java's
-            // order: row i holds post(i,i) at 4i and post(i,j) at 4i+1+j (j<i) or 4i+j (j>i); event
-            // k's log-likelihood is the sum on lane kEvSum[k] (nibble k of 0x9863975287416540)
-            const int k16 = lane & 15;
-            const int src = (int)((0x9863975287416540ull >> (4 * k16)) & 15u);
-            const double ev = __shfl(acc, src, 64) + ((k16 & 3) == 0 ? gp.log_prior_homo : gp.log_prior_hetero);
-            // calculatePosteriorProbabilities (:472-495): the maximum (no NaN: order-free), each
-            // lane's power of ten, the normaliser summed in Java's order, one division per lane
-            double logMax = ev;
+            // getPosteriorProbabilities (CountsHelper.java:410-443): events in Java's order -- row i holds
+            // (i,i) then (i,j) for j != i ascending; L is symmetric
+            constexpr int kEv[16] = {0, 1, 2, 3, 4, 1, 5, 6, 7, 2, 5, 8, 9, 3, 6, 8};   // event -> L index
+            double ev[16];
 #pragma unroll
-            for (int o = 1; o < 16; o <<= 1) {
-                const double w = __shfl_xor(logMax, o, 64);
-                logMax = w > logMax ? w : logMax;
+            for (int k = 0; k < 16; k++) ev[k] = L[kEv[k]] + ((k & 3) == 0 ? gp.log_prior_homo : gp.log_prior_hetero);
+            // calculatePosteriorProbabilities (:472-495).  Events more than 20 below the maximum are 0 and add
+            // nothing to the normaliser, so only the others take a pow and a division -- each lane walks its
+            // own active events in Java's order, so the normaliser is summed exactly as the reference does.
+            // The lane's 16 events live in LDS (column tid), so the walk indexes them without scratch memory.
+            double logMax = 1;
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                if (logMax > 0 || logMax < ev[k]) logMax = ev[k];
+            uint32_t act = 0;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const double x = ev[k] - logMax;
+                const bool on = !(x < -20);
+                act |= on ? 1u << k : 0u;
+                s_ev[k][threadIdx.x] = on ? x : 0.0;
             }
-            const double x = ev - logMax;
-            const double pk = x < -20 ? 0.0 : pow(10.0, x);
             double totalProb = 0;
-#pragma unroll
-            for (int k = 0; k < 16; k++) totalProb += readlane_d(pk, k);
-            const double post = pk / totalProb;            // lane k: posterior of event k
-            // getIndexesMaxGenotype (VariantDiscoverySNVQAlgorithm.java:223-243): lane p < 10 sums pair
-            // p = (a,b), a <= b, as post(a,b) + post(b,a); the scan keeps the reference's order and margin
-            const int pa = (int)((0x3221110000ull >> (4 * (lane % 10))) & 15u);
-            const int pb = (int)((0x3323213210ull >> (4 * (lane % 10))) & 15u);
-            const double p_ab = __shfl(post, pa == pb ? 4 * pa : 4 * pa + pb, 64);
-            const double p_ba = __shfl(post, 4 * pb + 1 + pa, 64);
-            const double gsum = pa == pb ? p_ab : p_ab + p_ba;
-            int I = refIdx, J = refIdx;
-            double probMax = readlane_d(post, 4 * refIdx);
-            const double refProb = probMax;
-#pragma unroll
-            for (int q = 0; q < 10; q++) {
-                const double g = readlane_d(gsum, q);
-                if (g > probMax + 0.01) {
-                    probMax = g;
-                    I = (int)((0x3221110000ull >> (4 * q)) & 15u);
-                    J = (int)((0x3323213210ull >> (4 * q)) & 15u);
-                }
+            for (uint32_t rem = act; rem; rem &= rem - 1) {
+                const int k = __builtin_ctz(rem);
+                const double pk = pow10_j(s_ev[k][threadIdx.x]);
+                totalProb += pk;
+                s_ev[k][threadIdx.x] = pk;
             }
-            // maxP = post(I,J) [+ post(J,I)] is the pair sum the scan kept (the initial one: post(ref,ref))
-            const int16_t ph2 = phred_d(lane == 0 ? 1 - probMax : refProb);    // lanes 0, 1 in parallel
-            gq = (int16_t)__builtin_amdgcn_readlane((int)ph2, 0);
-            qual = (int16_t)__builtin_amdgcn_readlane((int)ph2, 1);
+            for (uint32_t rem = act; rem; rem &= rem - 1) {
+                const int k = __builtin_ctz(rem);
+                s_ev[k][threadIdx.x] = s_ev[k][threadIdx.x] / totalProb;
+            }
+#pragma unroll
+            for (int k = 0; k < 16; k++) ev[k] = s_ev[k][threadIdx.x];
+            // post(i, j) is event 4i + (j < i ? j + 1 : j) for j != i, 4i for j == i
+            auto post = [&](int i, int j) -> double {
+                return s_ev[i == j ? 4 * i : 4 * i + (j < i ? j + 1 : j)][threadIdx.x];
+            };
+            // getIndexesMaxGenotype (VariantDiscoverySNVQAlgorithm.java:223-243), default index = reference
+            int I = refIdx, J = refIdx;
+            const double refProb = post(refIdx, refIdx);
+            double probMax = refProb;
+#pragma unroll
+            for (int pi = 0; pi < 4; pi++)
+#pragma unroll
+                for (int pj = pi; pj < 4; pj++) {
+                    const int k1 = pi == pj ? 4 * pi : 4 * pi + pj;          // (pi, pj), pj > pi
+                    const int k2 = 4 * pj + pi + 1;                          // (pj, pi), pi < pj
+                    double g = ev[k1];
+                    if (pi != pj) g += ev[k2];
+                    if (g > probMax + 0.01) { probMax = g; I = pi; J = pj; }
+                }
+            gq = phred_d(1 - probMax);
+            qual = phred_d(refProb);
             if (I != J && I != refIdx && J != refIdx) {           // triallelic (:128-177)
-                if (readlane_d(post, 4 * I) > readlane_d(post, 4 * J) + 0.01) { alt = (int8_t)I; third = (int8_t)J; }
+                if (post(I, I) > post(J, J) + 0.01) { alt = (int8_t)I; third = (int8_t)J; }
                 else { alt = (int8_t)J; third = (int8_t)I; }
                 nal = 3; genotype = 3; keep = true;
             } else if (I != J) {
@@ -365,42 +325,34 @@ __global__ __launch_bounds__(kPostWaves * 64) void k_posterior(const QueueSite* 
             if (keep && gp.min_quality > gq) keep = false;
         }
         if (!keep && !gp.dump_all) continue;
-        // the record goes to its position bucket (KO orders each bucket; no global reservation).  The
-        // slot's atomic is issued now and the record is staged in LDS; it is stored at the wave's next
-        // record (or at the end), so the atomic's round trip overlaps the next site
-        {
-            const int32_t bk = gpos >> shift;
-            int32_t k = 0;
-            if (lane == 0) k = atomicAdd(&bcount[bk], 1);
-            flush_pending();
-            if (lane == 0) {
-                const uint32_t ref = callable ? (uint32_t)(uint8_t)"ACGT"[(rc >> 5) & 3] : (uint32_t)'N';
-                uint32_t* h = s_rec[wv];
-                h[0] = 0xFFFFFFFFu;
-                h[1] = (uint32_t)gpos;
-                h[2] = ref | (uint32_t)(uint8_t)nal << 8 | (uint32_t)(uint8_t)alt << 16 | (uint32_t)(uint8_t)third << 24;
-                h[3] = (uint32_t)(uint8_t)genotype | 0xFF00u | (uint32_t)(uint16_t)gq << 16;
-                h[4] = (uint32_t)(uint16_t)qual | (uint32_t)(keep ? 1 : 0) << 16;
-                h[5] = (uint32_t)total;
+        // the record goes to its position bucket (KO orders each bucket)
+        const int32_t bk = gpos >> shift;
+        const int32_t k = atomicAdd(&bcount[bk], 1);
+        if (k >= bcap) continue;                       // overflow: the host grows the buckets and reruns
+        uint32_t h[18];
+        h[0] = 0xFFFFFFFFu;
+        h[1] = (uint32_t)gpos;
+        const uint32_t ref = callable ? (uint32_t)(uint8_t)"ACGT"[(rc >> 5) & 3] : (uint32_t)'N';
+        h[2] = ref | (uint32_t)(uint8_t)nal << 8 | (uint32_t)(uint8_t)alt << 16 | (uint32_t)(uint8_t)third << 24;
+        h[3] = (uint32_t)(uint8_t)genotype | 0xFF00u | (uint32_t)(uint16_t)gq << 16;
+        h[4] = (uint32_t)(uint16_t)qual | (uint32_t)(keep ? 1 : 0) << 16;
+        h[5] = (uint32_t)total;
 #pragma unroll
-                for (int t = 0; t < 4; t++) {
-                    h[6 + t] = (uint32_t)cnt[t];
-                    h[10 + 2 * t] = (uint32_t)sc[t][0];
-                    h[11 + 2 * t] = (uint32_t)sc[t][1];
-                }
-            }
-            if (lane < 10) {
-                const int li = (int)((0x8653219740ull >> (4 * lane)) & 15u);
-                const unsigned long long bits = __builtin_bit_cast(unsigned long long, acc);
-                s_rec[wv][18 + 2 * li] = (uint32_t)bits;
-                s_rec[wv][19 + 2 * li] = (uint32_t)(bits >> 32);
-            }
-            pend_k = k;
-            pend_bk = bk;
-            pending = true;
+        for (int t = 0; t < 4; t++) {
+            h[6 + t] = (uint32_t)cnt[t];
+            h[10 + 2 * t] = (uint32_t)sc[t][0];
+            h[11 + 2 * t] = (uint32_t)sc[t][1];
+        }
+        uint32_t* o = reinterpret_cast<uint32_t*>(brec + (int64_t)bk * bcap + k);
+#pragma unroll
+        for (int t = 0; t < 18; t++) o[t] = h[t];
+#pragma unroll
+        for (int t = 0; t < 10; t++) {
+            const unsigned long long bits = __builtin_bit_cast(unsigned long long, L[t]);
+            o[18 + 2 * t] = (uint32_t)bits;
+            o[19 + 2 * t] = (uint32_t)(bits >> 32);
         }
     }
-    flush_pending();
 }
 
 
@@ -1362,54 +1314,72 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
 
 // ------------------------------------------------------------------------------------------
 // KO: order the emitted records by global position.  KP appended every record to the bucket of its
-//     position (2^shift positions per bucket, bcap records each); one workgroup per kKofBuckets
-//     buckets sums the counts of the earlier buckets (its output offset), each wave ranks a
-//     bucket's keys and copies the records in order.  One kernel, no atomics, no global scan.
+//     position (2^shift positions per bucket, bcap records each).  KS (one workgroup) turns the bucket
+//     counts into output offsets (exclusive prefix) and writes the record count and the fullest
+//     bucket; KO ranks each bucket's keys (one wave per bucket) and copies the records in order.
 // ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void ko_scan(const int32_t* __restrict__ bcount, int64_t nb, int32_t bcap,
+                                                int32_t* __restrict__ boff, unsigned long long* counters) {
+    __shared__ int32_t s_wsum[16];
+    __shared__ int32_t s_mx[16];
+    __shared__ long long s_raw[16];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t per = (nb + 1023) / 1024;
+    const int64_t b0 = tid * per, b1 = b0 + per < nb ? b0 + per : nb;
+    int32_t sum = 0, mx = 0;
+    long long raw = 0;
+    for (int64_t b = b0; b < b1; b++) {
+        const int32_t c = bcount[b];
+        sum += c < bcap ? c : bcap;
+        raw += c;
+        mx = c > mx ? c : mx;
+    }
+    // inclusive wave scan of the per-thread sums, then the 16 wave totals
+    int32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t v = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += v;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const int32_t m2 = __shfl_xor(mx, o, 64);
+        mx = m2 > mx ? m2 : mx;
+        raw += __shfl_xor(raw, o, 64);
+    }
+    if (lane == 63) s_wsum[wv] = inc;
+    if (lane == 0) { s_mx[wv] = mx; s_raw[wv] = raw; }
+    __syncthreads();
+    int32_t before = 0;
+    for (int k = 0; k < wv; k++) before += s_wsum[k];
+    int32_t run = before + inc - sum;
+    for (int64_t b = b0; b < b1; b++) {
+        boff[b] = run;
+        const int32_t c = bcount[b];
+        run += c < bcap ? c : bcap;
+    }
+    if (tid == 0) {
+        int32_t m = 0;
+        long long total = 0;
+        for (int k = 0; k < 16; k++) { m = s_mx[k] > m ? s_mx[k] : m; total += s_raw[k]; }
+        // every record KP emitted and the fullest bucket: above bcap the host grows the buckets and reruns
+        counters[0] = (unsigned long long)total | ((unsigned long long)m << 40);
+    }
+}
+
 constexpr int kKofBuckets = 16;                // one wave per bucket, 16 waves per workgroup
 __global__ __launch_bounds__(1024) void ko_fused(const ngsep_site_out* __restrict__ brec, const int32_t* __restrict__ bcount,
-                                                 int64_t nb, int32_t bcap, ngsep_site_out* __restrict__ sorted, int64_t cap,
-                                                 unsigned long long* counters, const int4* __restrict__ wins, int32_t n_wins,
-                                                 int32_t bucket_span) {
-    __shared__ int32_t s_red[kKofBuckets], s_mx[kKofBuckets];
-    __shared__ int32_t s_cnt[kKofBuckets], s_off[kKofBuckets];
+                                                 const int32_t* __restrict__ boff, int64_t nb, int32_t bcap,
+                                                 ngsep_site_out* __restrict__ sorted, int64_t cap,
+                                                 const int4* __restrict__ wins, int32_t n_wins, int32_t bucket_span) {
     __shared__ uint32_t s_pos[kKofBuckets][1024];   // crowded buckets only (> 64 records)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int64_t b0 = (int64_t)blockIdx.x * kKofBuckets;
-    // offset of this block's records: the records of every earlier bucket (block 0: all, for the total)
-    const bool all = blockIdx.x == 0;
-    const int64_t lim = all ? nb : b0;
-    int32_t part = 0, mx = 0;
-    for (int64_t b = tid; b < lim; b += 1024) {
-        const int32_t c = bcount[b];
-        part += all || c < bcap ? c : bcap;
-        mx = c > mx ? c : mx;
-    }
-    for (int o = 32; o > 0; o >>= 1) { part += __shfl_xor(part, o, 64); const int32_t m2 = __shfl_xor(mx, o, 64); mx = m2 > mx ? m2 : mx; }
-    if (lane == 0) { s_red[wv] = part; s_mx[wv] = mx; }
-    if (tid < kKofBuckets) s_cnt[tid] = b0 + tid < nb ? (bcount[b0 + tid] < bcap ? bcount[b0 + tid] : bcap) : 0;
-    __syncthreads();
-    int64_t total_before = 0;
-#pragma unroll
-    for (int k = 0; k < kKofBuckets; k++) total_before += s_red[k];
-    if (tid == 0) {
-        int32_t acc = 0;
-        for (int j = 0; j < kKofBuckets; j++) { s_off[j] = acc; acc += s_cnt[j]; }
-        if (all) {
-            // every record KP emitted (block 0 summed all buckets) and the fullest bucket: above bcap the
-            // host grows the buckets and runs again
-            int32_t m = 0;
-            for (int k = 0; k < kKofBuckets; k++) m = max(m, s_mx[k]);
-            counters[0] = (unsigned long long)total_before | ((unsigned long long)m << 40);
-        }
-    }
-    __syncthreads();
     const int64_t b = b0 + wv;
     if (b >= nb) return;
-    const int32_t c = s_cnt[wv];
+    const int32_t c = bcount[b] < bcap ? bcount[b] : bcap;
     if (c == 0) return;
     const ngsep_site_out* src = brec + b * bcap;
-    const int64_t off = (all ? 0 : total_before) + s_off[wv];
+    const int64_t off = boff[b];
     // the last window starting at or before the bucket (wave-uniform); a record's window is that one or
     // (rarely) a later one.  Records only arise in window bodies, where the reference is non-zero.
     int32_t wb = 0;
@@ -1554,9 +1524,7 @@ void device_release(Device* d) {
     (void)hipFree(d->d_slots); d->d_slots = nullptr;
     (void)hipFree(d->d_pile); d->d_pile = nullptr;
     (void)hipFree(d->d_planes); d->d_planes = nullptr;
-    (void)hipFree(d->d_seg); d->d_seg = nullptr;
-    (void)hipFree(d->d_segneg); d->d_segneg = nullptr;
-    (void)hipFree(d->d_tseg); d->d_tseg = nullptr;
+    (void)hipFree(d->d_cneg); d->d_cneg = nullptr;
     (void)hipFree(d->d_wins); d->d_wins = nullptr;
     d->n_wins = 0;
     d->planes_W = 0;
@@ -1581,6 +1549,7 @@ void device_destroy(Device* d) {
     for (auto& sl : d->slot) {
         (void)hipFree(sl.d_brec);
         (void)hipFree(sl.d_bcount);
+        (void)hipFree(sl.d_boff);
         (void)hipFree(sl.d_hard);
         (void)hipFree(sl.d_tables);
         if (sl.stream && sl.stream != d->stream) (void)hipStreamDestroy(sl.stream);
@@ -1604,28 +1573,23 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
     HIP_TRY(hipSetDevice(d->ordinal));
     device_release(d);
     const int32_t pad = s.windows.empty() ? 64 : s.windows[0].pad;
-    HIP_TRY(hipMalloc(&d->d_pile, (size_t)std::max<int64_t>(s.pile_bytes, 16)));
+    HIP_TRY(hipMalloc(&d->d_pile, (size_t)s.pile_bytes + 64));     // + 64: KP loads whole dwords of a column
     HIP_TRY(hipMalloc(&d->d_tinfo, (size_t)std::max<int64_t>(s.n_tiles, 1) * sizeof(TileInfo)));
     HIP_TRY(hipMalloc(&d->d_ref, (size_t)s.g_len + 64));
     if (s.n_tiles && !s.h_tinfo.empty()) HIP_TRY(hipMemcpyAsync(d->d_tinfo, s.h_tinfo.data(), (size_t)s.n_tiles * sizeof(TileInfo), hipMemcpyHostToDevice, d->stream));
     HIP_TRY(hipMemsetAsync(d->d_ref, 0, (size_t)s.g_len + 64, d->stream));
     HIP_TRY(hipMemcpyAsync(d->d_ref, s.h_ref.data(), (size_t)s.g_len, hipMemcpyHostToDevice, d->stream));
     if (s.single) {
-        // single sample: planes (KT), position-major pile + segments (KP) -- everything KT/KP/KO read
-        const size_t nseg = s.h_seg.n;
+        // single sample: planes (KT), the position-major pile and its strand bits (KP)
+        const size_t ncw = (size_t)(s.pile_bytes / 32);
         HIP_TRY(hipMalloc(&d->d_planes, (size_t)std::max<int64_t>(s.pile_bytes / 4, 16)));
-        HIP_TRY(hipMalloc(&d->d_seg, std::max<size_t>(nseg, 1) * sizeof(uint32_t)));
-        HIP_TRY(hipMalloc(&d->d_segneg, std::max<size_t>(nseg, 1)));
-        HIP_TRY(hipMalloc(&d->d_tseg, ((size_t)s.n_tiles + 1) * sizeof(int32_t)));
+        HIP_TRY(hipMalloc(&d->d_cneg, (ncw + 2) * sizeof(uint32_t)));    // + 2: KP reads word pairs
+        HIP_TRY(hipMemsetAsync(d->d_cneg, 0, (ncw + 2) * sizeof(uint32_t), d->stream));
         if (s.pile_bytes) {
             HIP_TRY(hipMemcpyAsync(d->d_pile, s.h_cpile.p, (size_t)s.pile_bytes, hipMemcpyHostToDevice, d->stream));
             HIP_TRY(hipMemcpyAsync(d->d_planes, s.h_planes.p, (size_t)(s.pile_bytes / 4), hipMemcpyHostToDevice, d->stream));
+            HIP_TRY(hipMemcpyAsync(d->d_cneg, s.h_cneg.p, ncw * sizeof(uint32_t), hipMemcpyHostToDevice, d->stream));
         }
-        if (nseg) {
-            HIP_TRY(hipMemcpyAsync(d->d_seg, s.h_seg.p, nseg * sizeof(uint32_t), hipMemcpyHostToDevice, d->stream));
-            HIP_TRY(hipMemcpyAsync(d->d_segneg, s.h_segneg.p, nseg, hipMemcpyHostToDevice, d->stream));
-        }
-        if (!s.h_tseg.empty()) HIP_TRY(hipMemcpyAsync(d->d_tseg, s.h_tseg.data(), s.h_tseg.size() * sizeof(int32_t), hipMemcpyHostToDevice, d->stream));
         d->planes_W = s.tile / 32;
     } else {
         // multisample: per-(tile, sample) blocks (KTM), the read-major SoA and its bucket index (KPM)
@@ -1717,8 +1681,11 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         if (!idle) HIP_TRY(hipStreamSynchronize(sl.stream));
         if (nb > sl.nb_cap) {
             (void)hipFree(sl.d_bcount);
+            (void)hipFree(sl.d_boff);
             sl.d_bcount = nullptr;
+            sl.d_boff = nullptr;
             HIP_TRY(hipMalloc(&sl.d_bcount, (size_t)nb * sizeof(int32_t)));
+            HIP_TRY(hipMalloc(&sl.d_boff, (size_t)nb * sizeof(int32_t)));
             sl.nb_cap = nb;
         }
         if (nb * bcap > sl.brec_cap) {
@@ -1764,17 +1731,20 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
                               s.g_len, sl.d_hard, ctr, sl.cap_hard, sl.d_bcount, nb);
         HIP_TRY(hipGetLastError());
     }
-    static const int kp_grid = std::getenv("NGSEP_KP_GRID") ? std::max(1, std::atoi(std::getenv("NGSEP_KP_GRID"))) : 2048;   // tuning
-    hipExtLaunchKernelGGL(k_posterior, dim3(kp_grid), dim3(kPostWaves * 64), 0, sl.stream,
+    // one lane per queued site: enough workgroups for the queue (the count is on the device; sized from the
+    // previous run's survivors, grid-stride beyond)
+    static const int kp_env = std::getenv("NGSEP_KP_GRID") ? std::max(1, std::atoi(std::getenv("NGSEP_KP_GRID"))) : 0;   // tuning
+    const int kp_grid = kp_env ? kp_env : (int)std::max<int64_t>(d->n_cu, std::min<int64_t>((d->last_hard + kPostThreads - 1) / kPostThreads, 8 * (int64_t)d->n_cu));
+    hipExtLaunchKernelGGL(k_posterior, dim3(kp_grid), dim3(kPostThreads), 0, sl.stream,
                           d->time_posterior ? sl.ev[5] : nullptr, d->time_posterior ? sl.ev[2] : nullptr, 0,
                           (const QueueSite*)sl.d_hard, (const unsigned long long*)(ctr + 2), sl.cap_hard,
-                          (const TileInfo*)d->d_tinfo, (const int32_t*)d->d_tseg, (const uint32_t*)d->d_seg,
-                          (const uint8_t*)d->d_segneg, (const uint8_t*)d->d_pile, d->log2_tile, (const LikTables*)sl.d_tables, g,
-                          sl.d_brec, sl.d_bcount, shift, bcap);
+                          (const TileInfo*)d->d_tinfo, (const uint8_t*)d->d_pile, (const uint32_t*)d->d_cneg, d->log2_tile,
+                          (const LikTables*)sl.d_tables, g, sl.d_brec, sl.d_bcount, shift, bcap);
     HIP_TRY(hipGetLastError());
     // order the records by position on the device (one kernel; counters[0] = records | max bucket << 40)
+    hipLaunchKernelGGL(ko_scan, dim3(1), dim3(1024), 0, sl.stream, (const int32_t*)sl.d_bcount, nb, bcap, sl.d_boff, ctr);
     hipLaunchKernelGGL(ko_fused, dim3((unsigned)((nb + kKofBuckets - 1) / kKofBuckets)), dim3(64 * kKofBuckets), 0, sl.stream, sl.d_brec,
-                       sl.d_bcount, nb, bcap, sl.d_sorted, sl.cap, ctr, d->d_wins, d->n_wins, 1 << shift);
+                       (const int32_t*)sl.d_bcount, (const int32_t*)sl.d_boff, nb, bcap, sl.d_sorted, sl.cap, d->d_wins, d->n_wins, 1 << shift);
     HIP_TRY(hipGetLastError());
     // copies: counters and a prefix of the ordered records (sized from the previous run) straight into
     // the slot's pinned store, then the counter set is cleared for the slot's next run.  On the copy
