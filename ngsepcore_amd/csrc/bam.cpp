@@ -826,6 +826,10 @@ extern "C" int ngsep_call_population_bams(ngsep_ctx* c, const char* const* bam_p
         int rc = ngsep_bam_open(c, bam_paths[f], &cur[(size_t)f].bam);
         if (rc != NGSEP_OK) { close_all(); return rc; }
         ngsep_bam* b = cur[(size_t)f].bam;
+        if (c->params.query_seq[0]) {      // -querySeq: every file read from the region's index chunks
+            rc = ngsep_bam_set_region(b, c->params.query_seq, std::max<int64_t>(1, c->params.query_first), c->params.query_last);
+            if (rc != NGSEP_OK && rc != NGSEP_E_IO) { close_all(); return rc; }
+        }
         for (size_t g = 0; g < b->rg_ids.size(); g++) {
             auto it = rg_global.find(b->rg_ids[g]);
             if (it == rg_global.end()) {
@@ -885,7 +889,7 @@ extern "C" int ngsep_call_population_bams(ngsep_ctx* c, const char* const* bam_p
         m_cig_off.clear(); m_seq_off.clear(); m_hasq.clear(); m_bases.clear(); m_quals.clear();
         return r;
     };
-    while (true) {
+    while (!c->query_done) {
         int best = -1;
         int32_t bs = 0, bf = 0, bl = 0;
         for (int f = 0; f < n_files; f++) {

@@ -11,9 +11,29 @@ the single-process output.
 """
 from __future__ import annotations
 
+import gzip
 import os
+import struct
 import tempfile
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+
+def bam_header_sequences(bam: str) -> List[Tuple[str, int]]:
+    """(name, length) of every @SQ reference of a BAM header, in header order -- the order in which a
+    single-process SingleSampleVariantsDetector run meets (and writes) the sequences of a sorted BAM."""
+    with gzip.open(bam, "rb") as f:
+        if f.read(4) != b"BAM\1":
+            raise ValueError(f"{bam}: not a BAM file")
+        (l_text,) = struct.unpack("<i", f.read(4))
+        f.read(l_text)
+        (n_ref,) = struct.unpack("<i", f.read(4))
+        out = []
+        for _ in range(n_ref):
+            (l_name,) = struct.unpack("<i", f.read(4))
+            name = f.read(l_name)[:-1].decode()
+            (l_ref,) = struct.unpack("<i", f.read(4))
+            out.append((name, l_ref))
+        return out
 
 
 def assign_contigs(contigs: Sequence[Tuple[str, int]], world: int) -> List[List[str]]:
@@ -73,7 +93,8 @@ def gather_blocks(local: Dict[str, str], dist=None) -> Optional[Dict[str, str]]:
 def call_sharded(contigs: Sequence[Tuple[str, int]], call_contig: Callable[[str], str], out_vcf: str,
                  dist=None) -> Optional[str]:
     """Runs `call_contig(name) -> VCF text of that sequence` for this rank's sequences and writes the
-    merged VCF on rank 0 (returns its text there, None elsewhere)."""
+    merged VCF on rank 0 (returns its text there, None elsewhere).  `contigs` must be the alignment file's
+    sequences in its header order (bam_header_sequences): records on any other sequence are an error."""
     world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
     rank = dist.get_rank() if dist is not None and dist.is_initialized() else 0
     mine = assign_contigs(contigs, world)[rank]

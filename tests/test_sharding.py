@@ -81,3 +81,83 @@ def test_gpu_contig_caller_merge_identical(tmp_path):
         s.processFile(bam, full)
     merged = call_sharded(contigs, gpu_contig_caller(fa, bam), os.path.join(str(tmp_path), "m.vcf"))
     assert merged == open(full).read()
+
+
+def test_bam_header_sequences(tmp_path):
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=4, depth=2, seed=3)
+    _, _, bam = syn.write(os.path.join(str(tmp_path), "h"))
+    from ngsepcore_amd.sharding import bam_header_sequences
+    assert bam_header_sequences(bam) == [(n, len(s)) for n, s in syn.contigs()]
+    syn.close()
+
+
+def _reordered_sam(src, dst, order):
+    """the same records with the @SQ lines in another order (sorted by the new reference order)"""
+    head, recs = [], []
+    for l in open(src):
+        (head if l.startswith("@") else recs).append(l)
+    sq = {l.split("\t")[1][3:]: l for l in head if l.startswith("@SQ")}
+    other = [l for l in head if not l.startswith("@SQ")]
+    rank = {n: k for k, n in enumerate(order)}
+    recs.sort(key=lambda l: (rank[l.split("\t")[2]], int(l.split("\t")[3])))
+    with open(dst, "w") as f:
+        f.writelines(other[:1] + [sq[n] for n in order] + other[1:] + recs)
+    return dst
+
+
+def test_two_rank_sharded_bam_order_differs_from_fasta(tmp_path):
+    """BAM header order != FASTA order: the single-process run writes the sequences in BAM order, and so
+    does the merge when its order comes from the BAM header."""
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=3, depth=8, seed=4)
+    fa, sam, _ = syn.write(os.path.join(str(tmp_path), "d"))
+    names = [n for n, _ in syn.contigs()]
+    lens = dict((n, len(s)) for n, s in syn.contigs())
+    syn.close()
+    order = [names[2], names[0], names[1]]
+    sam2 = _reordered_sam(sam, os.path.join(str(tmp_path), "re.sam"), order)
+    bam2 = pysynth.sam_to_bam(sam2, os.path.join(str(tmp_path), "re.bam"))
+    from ngsepcore_amd.sharding import bam_header_sequences
+    contigs = bam_header_sequences(bam2)
+    assert [n for n, _ in contigs] == order and dict(contigs) == lens
+    full = os.path.join(str(tmp_path), "full.vcf")
+    ngsep_oracle.run_ssvd(fa, sam2, full)
+    mp.spawn(_worker, args=(2, _free_port(), fa, sam2, contigs, str(tmp_path)), nprocs=2, join=True)
+    merged = open(os.path.join(str(tmp_path), "merged.vcf")).read()
+    assert merged == open(full).read()
+    assert [l.split("\t")[0] for l in merged.splitlines() if not l.startswith("#")][0] == order[0]
+
+
+@pytest.mark.gpu
+def test_gpu_region_calls_merged_equal_whole_file(tmp_path):
+    """ngsep_call_region_bam over pieces of every sequence (BAI seeks), concatenated in order == the
+    whole-file GPU VCF; and call_bam_sharded on a BAM whose header order differs from the FASTA's."""
+    from ngsepcore_amd import GpuPileupSession
+    from ngsepcore_amd.sharding import bam_header_sequences, call_bam_sharded
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=3, depth=15, seed=8, softclip_rate=0.05)
+    fa, sam, bam = syn.write(os.path.join(str(tmp_path), "d"))
+    syn.close()
+    full = os.path.join(str(tmp_path), "full.vcf")
+    with GpuPileupSession() as s:
+        s.load_fasta(fa)
+        s.processFile(bam, full)
+    header, body = "", []
+    with GpuPileupSession() as s:
+        s.load_fasta(fa)
+        for name, L in bam_header_sequences(bam):
+            cuts = [1, L // 3, L // 3 + 1, 2 * L // 3, 2 * L // 3 + 1, L]
+            for a, b in ((cuts[0], cuts[1]), (cuts[2], cuts[3]), (cuts[4], cuts[5])):
+                out = os.path.join(str(tmp_path), f"{name}_{a}.vcf")
+                s._check(s._lib.ngsep_call_region_bam(s._ctx, bam.encode(), name.encode(), a, b, out.encode()))
+                t = open(out).read()
+                header = header or "".join(l for l in t.splitlines(True) if l.startswith("#"))
+                body += [l for l in t.splitlines(True) if not l.startswith("#")]
+    assert header + "".join(body) == open(full).read()
+    names = [n for n, _ in bam_header_sequences(bam)]
+    sam2 = _reordered_sam(sam, os.path.join(str(tmp_path), "re.sam"), [names[1], names[2], names[0]])
+    bam2 = pysynth.sam_to_bam(sam2, os.path.join(str(tmp_path), "re.bam"))
+    full2 = os.path.join(str(tmp_path), "full2.vcf")
+    with GpuPileupSession() as s:
+        s.load_fasta(fa)
+        s.processFile(bam2, full2)
+    merged = call_bam_sharded(fa, bam2, os.path.join(str(tmp_path), "m2.vcf"))
+    assert merged == open(full2).read()
