@@ -33,7 +33,7 @@ extern "C" {
 #define NGSEP_E_IO (-2)           /* file cannot be read or written */
 #define NGSEP_E_FORMAT (-3)       /* malformed BAM / FASTA */
 #define NGSEP_E_DEVICE (-4)       /* HIP runtime error or no device */
-#define NGSEP_E_UNSUPPORTED (-5)  /* input outside the implemented path (indels, ploidy>=3, ...) */
+#define NGSEP_E_UNSUPPORTED (-5)  /* input outside the implemented path (ploidy>=3, > 255 samples, ...) */
 #define NGSEP_E_NOMEM (-6)
 
 typedef struct ngsep_ctx ngsep_ctx;
@@ -161,6 +161,7 @@ typedef struct ngsep_stats {
     int64_t n_tiles;                /* pileup tiles */
     double  layout_ms;              /* host time to build the device layout of the last staged run */
     double  upload_ms;              /* host time of its H2D upload */
+    int64_t carved_positions;       /* covered positions inside carved indel regions (not called here) */
 } ngsep_stats;
 
 /* ---- context ---- */
@@ -187,6 +188,17 @@ int ngsep_notify_end(ngsep_ctx* ctx);
  * (sequence, position) order.  n_out receives the number available; at most cap are copied. */
 int ngsep_fetch_sites(ngsep_ctx* ctx, ngsep_site_out* out, int64_t cap, int64_t* n_out);
 int ngsep_clear_sites(ngsep_ctx* ctx);
+/* Alignments with insertions/deletions (CIGAR I/D) go through IndelRealignerPileupListener in the
+ * reference (discovery/IndelRealignerPileupListener.java:85-526), which realigns the alignments around
+ * each indel event and calls indels.  The device path does not run the realigner: every admitted
+ * alignment with an I/D item carves [first - R, last + indel bases + R] out of the device plan, R = the
+ * largest alignment span + 100 (the reach of an event's realignment: every alignment overlapping it),
+ * merged per sequence.  No call is made inside a carved region; outside them the calls are the
+ * reference's (the realigner is a pass-through there).  The carved regions are returned here, in
+ * processing order, for the caller's own path (the JNI host runs the Java listener chain on them):
+ * sequence ids, 1-based first and last positions.  n_out receives the number available. */
+int ngsep_fetch_carved_regions(ngsep_ctx* ctx, int32_t* seq_id, int64_t* first, int64_t* last, int64_t cap, int64_t* n_out);
+int ngsep_clear_carved_regions(ngsep_ctx* ctx);
 
 /* ---- VCF text, VCFFileWriter.printHeader / printVCFRecord (vcf/VCFFileWriter.java:44-68,309-311) ---- */
 int ngsep_write_vcf_header(ngsep_ctx* ctx, const char* path);

@@ -139,6 +139,7 @@ class NgsepStats(ctypes.Structure):
         ("n_tiles", ctypes.c_int64),
         ("layout_ms", ctypes.c_double),
         ("upload_ms", ctypes.c_double),
+        ("carved_positions", ctypes.c_int64),
     ]
 
 
@@ -175,6 +176,8 @@ SIGNATURES = {
     "ngsep_bam_open": (ctypes.c_int, [_CTX, ctypes.c_char_p, P(ctypes.c_void_p)]),
     "ngsep_bam_next_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, P(NgsepReadBatch)]),
     "ngsep_bam_close": (ctypes.c_int, [ctypes.c_void_p]),
+    "ngsep_fetch_carved_regions": (ctypes.c_int, [_CTX, P(ctypes.c_int32), P(ctypes.c_int64), P(ctypes.c_int64), ctypes.c_int64, P(ctypes.c_int64)]),
+    "ngsep_clear_carved_regions": (ctypes.c_int, [_CTX]),
     "ngsep_bam_set_region": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64]),
     "ngsep_call_region_bam": (ctypes.c_int, [_CTX, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p]),
     "ngsep_stage_alignments": (ctypes.c_int, [_CTX, P(NgsepReadBatch)]),

@@ -10,6 +10,27 @@
 
 #include "../../include/ngsep_gpu.h"
 
+// regions around indel-bearing alignments that the device path left uncalled (ngsep_fetch_carved_regions):
+// written as BED next to the output for the caller's own indel path, with a warning
+static void report_carved(ngsep_ctx* c, const std::string& prefix) {
+    int64_t n = 0;
+    ngsep_fetch_carved_regions(c, nullptr, nullptr, nullptr, 0, &n);
+    if (n == 0) return;
+    std::vector<int32_t> sid((size_t)n);
+    std::vector<int64_t> a((size_t)n), b((size_t)n);
+    ngsep_fetch_carved_regions(c, sid.data(), a.data(), b.data(), n, &n);
+    const std::string path = prefix + ".carved.bed";
+    FILE* f = std::fopen(path.c_str(), "w");
+    int64_t total = 0;
+    for (int64_t k = 0; k < n; k++) {
+        if (f) std::fprintf(f, "%s\t%lld\t%lld\n", ngsep_sequence_name(c, sid[(size_t)k]), (long long)a[(size_t)k] - 1, (long long)b[(size_t)k]);
+        total += b[(size_t)k] - a[(size_t)k] + 1;
+    }
+    if (f) std::fclose(f);
+    std::fprintf(stderr, "warning: %lld regions (%lld bp) around alignments with indels were not called on the GPU "
+                 "(the indel realigner's reach); listed in %s\n", (long long)n, (long long)total, path.c_str());
+}
+
 static int usage(const char* argv0) {
     std::fprintf(stderr,
                  "usage: %s SingleSampleVariantsDetector -i <alignments.bam> -r <reference.fa> -o <output prefix> [options]\n"
@@ -68,6 +89,7 @@ static int main_mvd(int argc, char** argv, int i) {
     std::fprintf(stderr, "alignments=%lld admitted=%lld positions=%lld candidates=%lld variants=%lld\n",
                  (long long)st.alignments_in, (long long)st.alignments_admitted, (long long)st.positions_genotyped,
                  (long long)st.candidates, (long long)st.sites_called);
+    report_carved(c, outp);
     ngsep_close(c);
     return 0;
 }
@@ -159,6 +181,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "alignments=%lld admitted=%lld positions=%lld candidates=%lld variants=%lld\n",
                  (long long)st.alignments_in, (long long)st.alignments_admitted, (long long)st.positions_genotyped,
                  (long long)st.candidates, (long long)st.sites_called);
+    report_carved(c, outp);
     ngsep_close(c);
     return 0;
 }

@@ -224,6 +224,7 @@ static void admit(ngsep_ctx* c, const ReadView& r) {
         cr.rank.push_back((uint8_t)(in && c->rg_sample[r.rg] >= 0 ? c->rg_rank[r.rg] : 0));
     }
     c->to_project.push_back(r);
+    if (r.indel_len > 0) cr.indel_reads.push_back({r.first, last + r.indel_len});   // the realigner's events
     int32_t span = last - r.first + 1;
     if (span > cr.max_span) cr.max_span = span;
     // union of covered positions inside the sequence (and the query range)
@@ -305,8 +306,47 @@ static int flush_sequence(ngsep_ctx* c) {
     return rc;
 }
 
+// IndelRealignerPileupListener's reach (ngsep_gpu.h ngsep_fetch_carved_regions): every indel-bearing
+// admitted alignment carves [first - R, last + indel bases + R], R = max span + 100 (DEF_REGION_BOUNDARY,
+// IndelRealignerPileupListener.java:43), merged; the covered positions inside leave the genotyped count
+static void carve_indel_regions(ngsep_ctx* c, ContigReads& cr) {
+    if (cr.indel_reads.empty()) return;
+    const int64_t R = (int64_t)cr.max_span + 100;
+    const int64_t len = (int64_t)c->seq_bases[(size_t)cr.seq_id].size();
+    std::vector<std::pair<int64_t, int64_t>> iv;
+    for (const auto& x : cr.indel_reads) iv.push_back({std::max<int64_t>(1, x.first - R), std::min<int64_t>(len, (int64_t)x.second + R)});
+    std::sort(iv.begin(), iv.end());
+    for (const auto& x : iv) {
+        if (x.first > x.second) continue;
+        if (!cr.carved.empty() && x.first <= (int64_t)cr.carved.back().second + 1)
+            cr.carved.back().second = (int32_t)std::max<int64_t>(cr.carved.back().second, x.second);
+        else cr.carved.push_back({(int32_t)x.first, (int32_t)x.second});
+    }
+    // covered positions inside the carved regions (reads sorted by first), also limited to the query range
+    int64_t lo_q = 1, hi_q = len;
+    if (c->params.query_seq[0]) { lo_q = std::max<int64_t>(lo_q, c->params.query_first); hi_q = std::min<int64_t>(hi_q, c->params.query_last); }
+    int64_t inside = 0;
+    size_t r0 = 0;
+    for (const auto& cv : cr.carved) {
+        const int64_t a = std::max<int64_t>(cv.first, lo_q), b = std::min<int64_t>(cv.second, hi_q);
+        c->carved.push_back({cr.seq_id, {cv.first, cv.second}});
+        if (a > b) continue;
+        while (r0 < cr.first.size() && (int64_t)cr.first[r0] + cr.max_span < a) r0++;
+        int64_t run = a - 1;
+        for (size_t i = r0; i < cr.first.size() && cr.first[i] <= b; i++) {
+            const int64_t f = std::max<int64_t>(cr.first[i], a), l = std::min<int64_t>(cr.last[i], b);
+            if (l < f || l <= run) continue;
+            inside += l - std::max(f, run + 1) + 1;
+            run = l;
+        }
+    }
+    cr.covered -= inside;
+    c->stats.carved_positions += inside;
+}
+
 int stage_contig_reads(ngsep_ctx* c, ContigReads& cr, bool run_now) {
     if (cr.seq_id < 0) return NGSEP_OK;
+    if (!c->params.coverage_stats) carve_indel_regions(c, cr);
     c->stats.positions_genotyped += cr.covered;
     if (!run_now || c->params.coverage_stats) {     // coverage: one device run over all sequences at the end
         c->staged_contigs.emplace_back(std::move(cr));
@@ -365,21 +405,15 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b) {
         }
         r.cigar = b->cigar + b->cigar_off[i];
         r.n_cigar = b->cigar_n[i];
-        bool indel = false;
-        int32_t last = r.first - 1, read_length = 0;
+        int32_t last = r.first - 1, read_length = 0, indel_len = 0;
         for (int32_t k = 0; k < r.n_cigar; k++) {
             const int32_t v = r.cigar[k], op = v & 7;
-            indel |= op == 1 || op == 2;
+            if (op == 1 || op == 2) indel_len += v / 8;
             if (v & 1) last += v / 8;
             if (v & 2) read_length += v / 8;
         }
-        if (indel && !c->params.coverage_stats) {
-            rc = set_error(c, NGSEP_E_UNSUPPORTED,
-                           "alignment with an indel (CIGAR I/D): the indel realigner path "
-                           "(IndelRealignerPileupListener) is not implemented on the GPU yet");
-            break;
-        }
         r.last = last;
+        r.indel_len = indel_len;
         const int32_t sl = b->seq_len[i];
         r.len = sl > 0 ? sl : 0;
         r.chars = nullptr;
@@ -823,14 +857,19 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
         nreads += ranges[wi].second - ranges[wi].first;
     }
     for (const ContigReads& cr : contigs) s.covered += cr.covered;
-    // reference codes in global coordinates
+    // reference codes in global coordinates; carved indel regions get no code (no call is made there)
     s.h_ref.assign((size_t)s.g_len, 0);
-    for (const Window& w : s.windows) {
+    for (size_t wi = 0; wi < s.windows.size(); wi++) {
+        const Window& w = s.windows[wi];
         const std::string& ref = c->seq_bases[w.seq_id];
         uint8_t* dst = &s.h_ref[(size_t)(w.gbase + w.pad)];
         parallel_for(w.wlen, 1 << 20, [&](int64_t lo, int64_t hi) {
             for (int64_t k = lo; k < hi; k++) dst[k] = ref_code(c, ref[(size_t)(w.w0 - 1 + k)]);
         });
+        for (const auto& cv : contigs[wr[wi].contig].carved) {
+            const int64_t a = std::max<int64_t>(cv.first, w.w0), b = std::min<int64_t>(cv.second, (int64_t)w.w0 + w.wlen - 1);
+            if (a <= b) std::memset(dst + (a - w.w0), 0, (size_t)(b - a + 1));
+        }
     }
     if (!c->params.multisample) {
         // single sample: the reads' projected bytes go straight into the tile layout
@@ -1332,6 +1371,25 @@ extern "C" int ngsep_fetch_sites(ngsep_ctx* c, ngsep_site_out* out, int64_t cap,
 extern "C" int ngsep_clear_sites(ngsep_ctx* c) {
     if (!c) return NGSEP_E_INVALID;
     c->sites.clear();
+    return NGSEP_OK;
+}
+
+extern "C" int ngsep_fetch_carved_regions(ngsep_ctx* c, int32_t* seq_id, int64_t* first, int64_t* last, int64_t cap,
+                                          int64_t* n_out) {
+    if (!c) return NGSEP_E_INVALID;
+    const int64_t n = (int64_t)c->carved.size();
+    if (n_out) *n_out = n;
+    for (int64_t i = 0; i < std::min(n, cap); i++) {
+        if (seq_id) seq_id[i] = c->carved[(size_t)i].first;
+        if (first) first[i] = c->carved[(size_t)i].second.first;
+        if (last) last[i] = c->carved[(size_t)i].second.second;
+    }
+    return NGSEP_OK;
+}
+
+extern "C" int ngsep_clear_carved_regions(ngsep_ctx* c) {
+    if (!c) return NGSEP_E_INVALID;
+    c->carved.clear();
     return NGSEP_OK;
 }
 

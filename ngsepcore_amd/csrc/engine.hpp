@@ -118,11 +118,16 @@ struct ContigReads {
     std::vector<uint8_t> rank;         // multisample: rank of the read group in its sample's set
     std::vector<int64_t> boff;         // offset of the read's projected bytes
     std::vector<uint8_t> bytes;        // projected codes over [first, last]
+    // indel-bearing admitted reads: [first, last + indel bases]; widened by the realigner's reach and merged
+    // into `carved` when the sequence is staged (engine.cpp carve_indel_regions)
+    std::vector<std::pair<int32_t, int32_t>> indel_reads;
+    std::vector<std::pair<int32_t, int32_t>> carved;
     int32_t max_span = 0;
     int64_t covered = 0;               // union of [first,last] (positions with a pileup)
     int32_t cov_last = 0;              // running max of last (for `covered`)
     void clear() {
         first.clear(); last.clear(); neg.clear(); uniq.clear(); sample.clear(); rank.clear(); boff.clear(); bytes.clear();
+        indel_reads.clear(); carved.clear();
         max_span = 0; covered = 0; cov_last = 0; seq_id = -1;
     }
 };
@@ -136,6 +141,7 @@ struct ReadView {
     const char* chars;     // nullptr = no characters (getReadCharacters() == null)
     const char* quals;     // nullptr = no qualities ('*')
     int32_t len;
+    int32_t indel_len;     // bases in the CIGAR's I/D items (0: SNV-only alignment)
 };
 struct CarryStore {        // owned copies of the open same-start group's reads
     std::vector<int32_t> cigar;
@@ -303,6 +309,9 @@ struct ngsep_ctx {
     std::vector<int8_t> sample_nrank;        // read groups per sample
     // outputs
     ngsep::SiteStore sites;
+    // regions around indel-bearing alignments the device path did not call (the indel realigner's reach,
+    // ngsep_fetch_carved_regions): (sequence, first, last), 1-based inclusive, in processing order
+    std::vector<std::pair<int32_t, std::pair<int64_t, int64_t>>> carved;
     int pending_sync = 0;                         // multisample runs submitted, not yet collected
     std::vector<ngsep_popsite_out> pop_sites;     // (sequence, position) order
     std::vector<ngsep_sample_call> pop_calls;     // pop_sites.size() x n_samples

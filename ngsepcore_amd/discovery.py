@@ -202,6 +202,17 @@ class GpuPileupSession:
     def clear(self):
         self._check(self._lib.ngsep_clear_sites(self._ctx))
 
+    def carved_regions(self):
+        """Regions around indel-bearing alignments the device path did not call (the indel realigner's
+        reach, ngsep_fetch_carved_regions): [(sequence, first, last)], 1-based inclusive."""
+        n = ctypes.c_int64()
+        self._check(self._lib.ngsep_fetch_carved_regions(self._ctx, None, None, None, 0, ctypes.byref(n)))
+        k = max(n.value, 1)
+        sid, a, b = (ctypes.c_int32 * k)(), (ctypes.c_int64 * k)(), (ctypes.c_int64 * k)()
+        self._check(self._lib.ngsep_fetch_carved_regions(self._ctx, sid, a, b, n.value, ctypes.byref(n)))
+        names = self.sequence_names()
+        return [(names[sid[i]], a[i], b[i]) for i in range(n.value)]
+
     def format_site(self, s: NgsepSiteOut) -> str:
         buf = ctypes.create_string_buffer(4096)
         self._lib.ngsep_format_site(self._ctx, ctypes.byref(s), buf, 4096)

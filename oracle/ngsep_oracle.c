@@ -1315,7 +1315,7 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
             } else if (query_found) { aln_free(a); break; }
             else { aln_free(a); continue; }
         }
-        if (a->has_indel && !cov) { G.unsupported = 1; aln_free(a); rc = NGO_UNSUPPORTED; break; }
+        if (a->has_indel && !cov && !p->indel_passthrough) { G.unsupported = 1; aln_free(a); rc = NGO_UNSUPPORTED; break; }
         process_alignment(&G, a);
     }
     if (multisample && !header_done) { header_done = 1; print_header_samples(out, p, NULL, 0); }

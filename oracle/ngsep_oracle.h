@@ -47,6 +47,10 @@ typedef struct ngo_params {
     const char* query_seq;         /* -querySeq (NULL) */
     int32_t query_first;           /* -first (0) */
     int32_t query_last;            /* -last (1e9) */
+    int32_t indel_passthrough;     /* 1: reads with I/D are admitted and the indel realigner is a pass-through
+                                      (IndelRealignerPileupListener.java:85-126 without its events): the SNV
+                                      calls are the reference's only outside the realigner's windows -- what
+                                      the GPU path's carved regions leave (tests/test_gpu_indels.py) */
 } ngo_params;
 
 void ngo_params_default(ngo_params* p);

@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <numeric>
 #include <string>
 #include <thread>
@@ -216,6 +217,77 @@ static GenOut gen_read(Rng& r, const ngs_synth_params& p, const std::string& h0,
     return o;
 }
 
+// a donor indel: `len` bases inserted after the position, or `len` reference bases deleted from it
+struct Indel { bool ins = false; int len = 0; std::string seq; };
+typedef std::map<int32_t, Indel> IndelMap;
+constexpr int kIndelCigar = 16;
+
+// one read on a haplotype with indels: the read walks the donor haplotype from reference position pos and
+// its CIGAR records the alignment (M runs, I for inserted bases, D for deleted reference bases); a read
+// never starts with a deletion nor ends inside an insertion.  Same error/quality model as gen_read.
+static GenOut gen_read_indel(Rng& r, const ngs_synth_params& p, const std::string& h0, const std::string& h1,
+                             const IndelMap* ev, int64_t L, int32_t pos, const double* et, char* bases, char* quals,
+                             int32_t* cig) {
+    GenOut o{};
+    const int rl = p.read_len;
+    const int hp = r.below(2) ? 1 : 0;
+    const std::string& hap = hp ? h1 : h0;
+    const IndelMap& m = ev[hp];
+    o.flags = r.below(2) ? 16 : 0;
+    o.mapq = (p.lowmq_rate > 0 && r.uniform() < p.lowmq_rate) ? 5 : 60;
+    int n = 0, nc = 0, lastop = -1;
+    auto op = [&](int code, int len) {
+        if (len <= 0) return;
+        if (nc > 0 && lastop == code) cig[nc - 1] += len * 8;
+        else if (nc < kIndelCigar) { cig[nc++] = len * 8 + code; lastop = code; }
+    };
+    auto emit = [&](char b) {
+        int q = sample_quality(r, p.quality_model);
+        if (r.uniform() < et[q]) {
+            const char* pb = std::strchr(kBases, b);
+            b = kBases[((pb ? (int)(pb - kBases) : 0) + 1 + (int)r.below(3)) % 4];
+        }
+        if (p.n_frac > 0 && r.uniform() < p.n_frac) { b = 'N'; q = 2; }
+        bases[n] = b;
+        quals[n] = (char)(33 + q);
+        n++;
+    };
+    int64_t i = pos;                                       // 1-based reference position
+    {   // a deletion at the start: the read starts after it
+        auto it = m.find((int32_t)i);
+        if (it != m.end() && !it->second.ins) i += it->second.len;
+    }
+    o.pos = (int32_t)i;
+    while (n < rl && i <= L) {
+        auto it = m.find((int32_t)i);
+        if (it != m.end() && !it->second.ins && n > 0) {   // deleted reference bases
+            op(1, it->second.len);
+            i += it->second.len;
+            continue;
+        }
+        emit(hap[(size_t)(i - 1)]);
+        op(3, 1);
+        if (it != m.end() && it->second.ins && n + it->second.len < rl) {
+            for (char b : it->second.seq) emit(b);
+            op(2, it->second.len);
+        }
+        i++;
+    }
+    while (n < rl) {                                       // past the contig end: pad with reference-less M
+        emit('N');
+        op(3, 1);
+    }
+    o.cn = nc;
+    o.hq = 1;
+    if (p.noqual_rate > 0 && r.uniform() < p.noqual_rate) {
+        o.hq = 0;
+        std::memset(quals, '!', (size_t)rl);
+    }
+    o.dup = p.dup_rate > 0 && r.uniform() < p.dup_rate;
+    o.sec = p.secondary_rate > 0 && r.uniform() < p.secondary_rate;
+    return o;
+}
+
 extern "C" ngs_synth* ngs_synth_create(const ngs_synth_params* pp) {
     ngs_synth* s = new ngs_synth();
     s->p = *pp;
@@ -260,6 +332,25 @@ extern "C" ngs_synth* ngs_synth_create(const ngs_synth_params* pp) {
                 s->truth.push_back({(int32_t)c, (int32_t)(i + 1), rb, kBases[ai], gt});
             }
         }
+        // donor indels (indel_rate > 0, SURVEY.md 8(d) second dataset): 1-10 bp insertions after or
+        // deletions from a reference position, on one haplotype (2/3) or both; from their own stream so the
+        // SNV donor above is the same with and without them
+        IndelMap ev[2];
+        if (p.indel_rate > 0) {
+            Rng ri(base_seed ^ 0x5851F42D4C957F2Dull ^ (uint64_t)(first + (int)c + 1) * 0x9E3779B97F4A7C15ull);
+            for (int64_t i = 10; i + 20 < L; i++) {
+                if (ri.uniform() >= p.indel_rate) continue;
+                Indel d;
+                d.ins = ri.below(2) != 0;
+                d.len = 1 + (int)ri.below(10);
+                for (int k = 0; k < d.len; k++) d.seq.push_back(kBases[ri.below(4)]);
+                const int gt = ri.uniform() < 2.0 / 3.0 ? 1 : 2;
+                const int hap = (int)ri.below(2);
+                if (gt == 2 || hap == 0) ev[0][(int32_t)(i + 1)] = d;
+                if (gt == 2 || hap == 1) ev[1][(int32_t)(i + 1)] = d;
+                i += d.len + 5;                                   // no overlapping events
+            }
+        }
         int rl = p.read_len;
         size_t cstart = R.size();
         if (L < rl) continue;
@@ -272,11 +363,16 @@ extern "C" ngs_synth* ngs_synth_create(const ngs_synth_params* pp) {
         const int64_t b0 = (int64_t)R.bases.size(), c0 = (int64_t)R.cigar.size();
         R.bases.resize((size_t)(b0 + nreads * rl));
         R.quals.resize((size_t)(b0 + nreads * rl));
-        R.cigar.resize((size_t)(c0 + 2 * nreads));
+        const int64_t cs = p.indel_rate > 0 ? kIndelCigar : 2;   // CIGAR items per read slot
+        R.cigar.resize((size_t)(c0 + cs * nreads));
         std::vector<GenOut> outs((size_t)nreads);
         auto gen = [&](Rng& rr, int64_t k) {
-            outs[(size_t)k] = gen_read(rr, p, h0, h1, L, starts[(size_t)k].pos, et, &R.bases[(size_t)(b0 + k * rl)],
-                                       &R.quals[(size_t)(b0 + k * rl)], &R.cigar[(size_t)(c0 + 2 * k)]);
+            if (p.indel_rate > 0)
+                outs[(size_t)k] = gen_read_indel(rr, p, h0, h1, ev, L, starts[(size_t)k].pos, et, &R.bases[(size_t)(b0 + k * rl)],
+                                                 &R.quals[(size_t)(b0 + k * rl)], &R.cigar[(size_t)(c0 + cs * k)]);
+            else
+                outs[(size_t)k] = gen_read(rr, p, h0, h1, L, starts[(size_t)k].pos, et, &R.bases[(size_t)(b0 + k * rl)],
+                                           &R.quals[(size_t)(b0 + k * rl)], &R.cigar[(size_t)(c0 + 2 * k)]);
         };
         if (p.rng_per_contig) {
             // independent streams per chunk of 65536 reads: generated on all cores
@@ -300,7 +396,7 @@ extern "C" ngs_synth* ngs_synth_create(const ngs_synth_params* pp) {
         }
         for (int64_t k = 0; k < nreads; k++) {
             const GenOut& o = outs[(size_t)k];
-            const int64_t no = readno++, soff = b0 + k * rl, coff = c0 + 2 * k;
+            const int64_t no = readno++, soff = b0 + k * rl, coff = c0 + cs * k;
             R.push((int32_t)c, o.pos, o.flags, o.mapq, 0, no, 0, coff, o.cn, soff, rl, o.hq);
             if (o.dup) R.push((int32_t)c, o.pos, o.flags, o.mapq, 0, no, 'd', coff, o.cn, soff, rl, o.hq);
             if (o.sec) R.push((int32_t)c, o.pos, o.flags | 0x100, o.mapq, 0, no, 's', coff, o.cn, soff, rl, o.hq);

@@ -39,6 +39,7 @@ typedef struct ngs_synth_params {
     int64_t trunc_len;       /* >0: every contig truncated to this length (bounded CPU-baseline samples) */
     int32_t rng_per_contig;  /* 1: each contig's donor/reads from its own seeded stream, so a contig generated
                                 alone (one rank's shard, contig_first=k, n_contigs=1) equals it in the whole genome */
+    double  indel_rate;      /* donor indels (1-10 bp insertions/deletions) per bp; reads across them carry I/D */
 } ngs_synth_params;
 
 typedef struct ngs_synth ngs_synth;

@@ -24,7 +24,7 @@ class SynthParams(ctypes.Structure):
         ("lower_frac", ctypes.c_double), ("n_frac", ctypes.c_double), ("sample_idx", ctypes.c_int32),
         ("quality_model", ctypes.c_int32), ("secondary_rate", ctypes.c_double), ("lowmq_rate", ctypes.c_double),
         ("noqual_rate", ctypes.c_double), ("softclip_rate", ctypes.c_double), ("n_samples", ctypes.c_int32),
-        ("trunc_len", ctypes.c_int64), ("rng_per_contig", ctypes.c_int32),
+        ("trunc_len", ctypes.c_int64), ("rng_per_contig", ctypes.c_int32), ("indel_rate", ctypes.c_double),
     ]
 
 
