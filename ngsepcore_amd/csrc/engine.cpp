@@ -153,11 +153,58 @@ static void allele_call_lengths(const ReadView& r, int read_length, int ignore_s
 // last - first + 1 bytes, zero-filled here).  Equivalent to evaluating, for every covered position p,
 // PileupRecord.getAlleleCalls(1)'s per-read step (PileupRecord.java:132-148) and
 // CountsHelper.calculateCountsGTSNV's quality clamp (CountsHelper.java:91).
+// code byte of a valid-or-counted call from its quality character and base (setQualityScores cap at 127,
+// CountsHelper.java:91's min(30, q), q <= 3 or a base other than A/C/G/T counted only), for every pair
+static const uint8_t* code_table() {
+    static uint8_t t[256 * 256];
+    static const bool init = [] {
+        for (int qc0 = 0; qc0 < 256; qc0++)
+            for (int b = 0; b < 256; b++) {
+                const int qc = qc0 > 127 ? 127 : qc0;
+                const int q = (int8_t)std::min(30, qc - 33);
+                const int a = dna_index((char)b);
+                uint8_t code;
+                if (q <= 3) code = (uint8_t)(kCodeCounted | (q < 0 ? 0 : q));
+                else if (a < 0) code = (uint8_t)(kCodeCounted | q);
+                else code = (uint8_t)(kCodeValid | (a << 5) | q);
+                t[qc0 * 256 + b] = code;
+            }
+        return true;
+    }();
+    (void)init;
+    return t;
+}
+
 void project_read(const ngsep_ctx* c, const ReadView& r, uint8_t* out) {
     const int64_t span = (int64_t)r.last - r.first + 1;
     if (span <= 0) return;
+    if (!r.chars) { std::memset(out, 0, (size_t)span); return; }   // getAlleleCall returns null without characters
+    // fast path: no I/D item and nothing ignored at the read ends -- every aligned base is a call
+    // (updateAlleleCallsInfo's masks are all about indels and ignore5/3, ReadAlignment.java:747-834)
+    if (r.indel_len == 0 && c->params.ignore5 == 0 && c->params.ignore3 == 0) {
+        static const uint8_t* tab = code_table();
+        const uint8_t* chars = reinterpret_cast<const uint8_t*>(r.chars);
+        const uint8_t* quals = reinterpret_cast<const uint8_t*>(r.quals);
+        int64_t o = 0, rp = 0;
+        for (int32_t k = 0; k < r.n_cigar; k++) {
+            const int32_t v = r.cigar[k], len = v / 8, op = v & 7;
+            const bool cRef = op & 1, cRead = (op & 2) != 0;
+            if (cRef && cRead) {
+                const int64_t n = std::min<int64_t>(len, std::min<int64_t>(span - o, (int64_t)r.len - rp));
+                if (quals)
+                    for (int64_t j = 0; j < n; j++) out[o + j] = tab[(size_t)quals[rp + j] * 256 + chars[rp + j]];
+                else
+                    for (int64_t j = 0; j < n; j++) out[o + j] = tab[(size_t)'+' * 256 + chars[rp + j]];
+                for (int64_t j = n > 0 ? n : 0; j < len && o + j < span; j++) out[o + j] = 0;
+            } else if (cRef) {
+                std::memset(out + o, 0, (size_t)std::max<int64_t>(0, std::min<int64_t>(len, span - o)));
+            }
+            if (cRef) o += len;
+            if (cRead) rp += len;
+        }
+        return;
+    }
     std::memset(out, 0, (size_t)span);
-    if (!r.chars) return;   // getAlleleCall returns null without characters
     int read_length = 0;
     for (int32_t k = 0; k < r.n_cigar; k++) if (r.cigar[k] & 2) read_length += r.cigar[k] / 8;
     // setBasesToIgnore5P/3P (ReadAlignment.java:613-644)
@@ -251,21 +298,27 @@ static void project_pending(ngsep_ctx* c) {
     if (v.empty()) return;
     ContigReads& cr = c->contig;
     const size_t n = v.size();
-    size_t off = cr.bytes.size();
-    const size_t b0 = cr.boff.size();
-    cr.boff.resize(b0 + n);
+    std::vector<int64_t> off(n + 1, 0);
     for (size_t i = 0; i < n; i++) {
-        cr.boff[b0 + i] = (int64_t)off;
         const int64_t span = (int64_t)v[i].last - v[i].first + 1;
-        off += span > 0 ? (size_t)span : 0;
+        off[i + 1] = off[i] + (span > 0 ? span : 0);
     }
-    if (cr.bytes.capacity() < off) cr.bytes.reserve(std::max(off, cr.bytes.capacity() * 3 / 2));
-    cr.bytes.resize(off);
-    uint8_t* base = cr.bytes.data();
-    const int64_t* boff = cr.boff.data() + b0;
+    // a fresh uninitialised chunk for this batch's codes: every read writes its own range
+    cr.chunks.emplace_back();
+    HostArray<uint8_t>& ch = cr.chunks.back();
+    ch.alloc((size_t)std::max<int64_t>(off[n], 1));
+    uint8_t* base = ch.p;
+    const size_t b0 = cr.bptr.size();
+    cr.bptr.resize(b0 + n);
+    for (size_t i = 0; i < n; i++) cr.bptr[b0 + i] = base + off[i];
+    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    const auto t1 = std::chrono::steady_clock::now();
     parallel_for((int64_t)n, 2048, [&](int64_t lo, int64_t hi) {
-        for (int64_t i = lo; i < hi; i++) project_read(c, v[(size_t)i], base + boff[i]);
+        for (int64_t i = lo; i < hi; i++) project_read(c, v[(size_t)i], base + off[(size_t)i]);
     });
+    if (host_timing)
+        std::fprintf(stderr, "[ngsep host] projection: %.1f ms (%u threads)\n",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count(), host_threads());
     v.clear();
 }
 
@@ -391,6 +444,16 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b) {
     if (!b || b->n_reads < 0) return set_error(c, NGSEP_E_INVALID, "null batch");
     const int nseq = (int)c->seq_names.size();
     int rc = NGSEP_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    {   // the batch's admitted reads land in these: one growth per batch
+        ContigReads& cr = c->contig;
+        const size_t k = (size_t)b->n_reads;
+        c->to_project.reserve(c->to_project.size() + k);
+        cr.first.reserve(cr.first.size() + k);
+        cr.last.reserve(cr.last.size() + k);
+        if (c->params.coverage_stats) cr.uniq.reserve(cr.uniq.size() + k);
+        else cr.neg.reserve(cr.neg.size() + k);
+    }
     for (int64_t i = 0; i < b->n_reads; i++) {
         if (c->query_done) break;
         c->stats.alignments_in++;
@@ -464,8 +527,14 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b) {
         c->last_start = r.first;
     }
     // the admitted reads' bytes are projected while the batch is alive; the open group is carried
+    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    const auto t1 = std::chrono::steady_clock::now();
     project_pending(c);
     carry_open_group(c);
+    if (host_timing)
+        std::fprintf(stderr, "[ngsep host] batch of %lld: admission %.1f ms, projection %.1f ms\n", (long long)b->n_reads,
+                     std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
     return rc;
 }
 
@@ -883,7 +952,7 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
             const int64_t goff = w.gbase + w.pad - w.w0;   // G = pos + goff
             for (int64_t i = ranges[wi].first; i < ranges[wi].second; i++) {
                 reads[(size_t)ri++] = SRead{(int32_t)(cr.first[(size_t)i] + goff), (int32_t)(cr.last[(size_t)i] + goff),
-                                            cr.bytes.data() + cr.boff[(size_t)i], cr.neg[(size_t)i]};
+                                            cr.bptr[(size_t)i], cr.neg[(size_t)i]};
                 const int64_t span = (int64_t)cr.last[(size_t)i] - cr.first[(size_t)i] + 1;
                 nbases += span > 0 ? span : 0;
             }
@@ -926,7 +995,7 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
                 int32_t fl = cr.neg[i];
                 if (!cr.sample.empty()) fl |= ((int32_t)cr.rank[i] << 1) | (((int32_t)cr.sample[i] + 1) << 8);
                 s.h_reads[ri * 4 + 3] = fl;
-                if (span > 0) std::memcpy(&s.h_slots[(size_t)slot * S], &cr.bytes[cr.boff[i]], (size_t)span);
+                if (span > 0) std::memcpy(&s.h_slots[(size_t)slot * S], cr.bptr[i], (size_t)span);
                 slot += ns;
                 nbases += span > 0 ? span : 0;
                 ri++;

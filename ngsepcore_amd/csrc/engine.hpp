@@ -108,6 +108,21 @@ struct Window {            // a contiguous range of one sequence, resident in HB
     int64_t read_begin, read_end;    // index range in the global read table
 };
 
+// uninitialised host array, filled in parallel (no serial zero-fill of GB-sized layouts)
+template <class T>
+struct HostArray {
+    T* p = nullptr;
+    size_t n = 0;
+    HostArray() = default;
+    HostArray(const HostArray&) = delete;
+    HostArray& operator=(const HostArray&) = delete;
+    HostArray(HostArray&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+    HostArray& operator=(HostArray&& o) noexcept { if (this != &o) { release(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; } return *this; }
+    ~HostArray() { release(); }
+    void alloc(size_t k) { release(); n = k; p = k ? static_cast<T*>(std::malloc(k * sizeof(T))) : nullptr; }
+    void release() { std::free(p); p = nullptr; n = 0; }
+};
+
 // Admitted reads of one sequence in pending order (AlignmentsPileupGenerator.pendingAlignments)
 struct ContigReads {
     int32_t seq_id = -1;
@@ -116,8 +131,8 @@ struct ContigReads {
     std::vector<uint8_t> uniq;         // coverage mode: 1 = ReadAlignment.isUnique (no FLAG_MULTIPLE_ALN)
     std::vector<int16_t> sample;       // multisample: sample of the read's group (-1 none)
     std::vector<uint8_t> rank;         // multisample: rank of the read group in its sample's set
-    std::vector<int64_t> boff;         // offset of the read's projected bytes
-    std::vector<uint8_t> bytes;        // projected codes over [first, last]
+    std::vector<const uint8_t*> bptr;  // the read's projected codes over [first, last]
+    std::vector<HostArray<uint8_t>> chunks;   // their storage: one uninitialised chunk per projected batch
     // indel-bearing admitted reads: [first, last + indel bases]; widened by the realigner's reach and merged
     // into `carved` when the sequence is staged (engine.cpp carve_indel_regions)
     std::vector<std::pair<int32_t, int32_t>> indel_reads;
@@ -126,7 +141,7 @@ struct ContigReads {
     int64_t covered = 0;               // union of [first,last] (positions with a pileup)
     int32_t cov_last = 0;              // running max of last (for `covered`)
     void clear() {
-        first.clear(); last.clear(); neg.clear(); uniq.clear(); sample.clear(); rank.clear(); boff.clear(); bytes.clear();
+        first.clear(); last.clear(); neg.clear(); uniq.clear(); sample.clear(); rank.clear(); bptr.clear(); chunks.clear();
         indel_reads.clear(); carved.clear();
         max_span = 0; covered = 0; cov_last = 0; seq_id = -1;
     }
@@ -210,21 +225,6 @@ struct SiteStore {
     }
     void push_back(const ngsep_site_out& o) { reserve(n + 1); buf[n++] = o; }
     void swap(SiteStore& o) { std::swap(buf, o.buf); std::swap(n, o.n); std::swap(cap, o.cap); }
-};
-
-// uninitialised host array, filled in parallel (no serial zero-fill of GB-sized layouts)
-template <class T>
-struct HostArray {
-    T* p = nullptr;
-    size_t n = 0;
-    HostArray() = default;
-    HostArray(const HostArray&) = delete;
-    HostArray& operator=(const HostArray&) = delete;
-    HostArray(HostArray&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
-    HostArray& operator=(HostArray&& o) noexcept { if (this != &o) { release(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; } return *this; }
-    ~HostArray() { release(); }
-    void alloc(size_t k) { release(); n = k; p = k ? static_cast<T*>(std::malloc(k * sizeof(T))) : nullptr; }
-    void release() { std::free(p); p = nullptr; n = 0; }
 };
 
 // a read of the single-sample layout: global [gfirst, glast] and its projected bytes

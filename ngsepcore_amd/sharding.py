@@ -121,18 +121,72 @@ def call_sharded(contigs: Sequence[Tuple[str, int]], call_contig: Callable[[str]
 
 def gpu_contig_caller(fasta: str, bam: str, params=None, device: int = 0) -> Callable[[str], str]:
     """The production per-sequence caller: SingleSampleVariantsDetector.findSNVS restricted to one
-    sequence (-querySeq) on this rank's GPU (libngsep_amd.so path B)."""
-    from .discovery import GpuPileupSession, default_params
+    sequence on this rank's GPU through the BAI index (ngsep_call_region_bam: only that sequence's BGZF
+    blocks are read; without an index the file is streamed up to the sequence).  One device context per
+    rank, the reference loaded once."""
+    from .discovery import GpuPileupSession
+
+    lengths = dict(bam_header_sequences(bam))
+    state = {}
 
     def call(name: str) -> str:
-        p = params if params is not None else default_params()
-        import ctypes
-        q = type(p)()
-        ctypes.pointer(q)[0] = p
-        q.query_seq = name.encode()
-        with tempfile.TemporaryDirectory() as d, GpuPileupSession(q, device) as s:
-            s.load_fasta(fasta)
+        if "s" not in state:
+            state["s"] = GpuPileupSession(params, device)
+            state["s"].load_fasta(fasta)
+        s = state["s"]
+        with tempfile.TemporaryDirectory() as d:
             out = os.path.join(d, "c.vcf")
-            s.processFile(bam, out)
+            s._check(s._lib.ngsep_call_region_bam(s._ctx, bam.encode(), name.encode(), 1, lengths[name], out.encode()))
             return open(out).read()
+
+    def close():
+        if "s" in state:
+            state.pop("s").close()
+    call.close = close
     return call
+
+
+def call_bam_sharded(fasta: str, bam: str, out_vcf: str, params=None, dist=None, device: Optional[int] = None) -> Optional[str]:
+    """SingleSampleVariantsDetector over the GPUs of one node: the BAM header's sequences split over the
+    ranks (assign_contigs), each rank calling its own through the index on its GPU (device = local rank
+    by default), the per-sequence blocks merged on rank 0 in header order."""
+    contigs = bam_header_sequences(bam)
+    if device is None:
+        device = int(os.environ.get("LOCAL_RANK", "0"))
+    caller = gpu_contig_caller(fasta, bam, params, device)
+    try:
+        return call_sharded(contigs, caller, out_vcf, dist)
+    finally:
+        caller.close()
+
+
+def gpu_population_caller(fasta: str, bams: Sequence[str], params=None, device: int = 0) -> Callable[[str], str]:
+    """MultisampleVariantsDetector restricted to one sequence (-querySeq; every BAM read from that
+    sequence's index chunks): the population VCF text of that sequence."""
+    from .discovery import MultisampleVariantsDetector
+
+    def call(name: str) -> str:
+        d = MultisampleVariantsDetector()
+        if params is not None:
+            import ctypes
+            ctypes.pointer(d.params)[0] = params
+            d.params.multisample = 1
+        d.setGenome(fasta)
+        d.setQuerySeq(name)
+        d.device = device
+        with tempfile.TemporaryDirectory() as t:
+            d.setOutFilename(os.path.join(t, "p.vcf"))
+            d.run(list(bams)).close()
+            return open(d.outFilename).read()
+    return call
+
+
+def call_population_sharded(fasta: str, bams: Sequence[str], out_vcf: str, params=None, dist=None,
+                            device: Optional[int] = None) -> Optional[str]:
+    """MultisampleVariantsDetector over the GPUs of one node (configs[4]): sequences split over the ranks,
+    the population VCF blocks merged on rank 0 in the first BAM's header order (the multi-file merge meets
+    the sequences in that order, AlignmentsPileupGenerator.java:268-289)."""
+    contigs = bam_header_sequences(bams[0])
+    if device is None:
+        device = int(os.environ.get("LOCAL_RANK", "0"))
+    return call_sharded(contigs, gpu_population_caller(fasta, bams, params, device), out_vcf, dist)

@@ -37,6 +37,14 @@ CASES = {
                                            lower_frac=0.01, quality_model=2, snv_rate=3e-3),
                                       {"calc_strand_bias": 1, "ploidy": 1, "min_quality": 20}),
 }
+# BASELINE.json configs at full size (the bench workloads): only the md5 and the record count of the oracle's
+# VCF are committed (tests/golden/full_sizes.json); the GPU suite regenerates the data on the box and
+# compares the HIP VCF byte for byte.  configs[1] = yeast 30x (seed 2), configs[2] = human chr20 30x
+# (seed 3, per-contig streams: the bench's chr20 workload)
+FULL_CASES = {
+    "configs1_yeast_30x": dict(genome=0, depth=30, seed=2),
+    "configs2_chr20_30x": dict(genome=1, contig_first=19, n_contigs=1, depth=30, seed=3, rng_per_contig=1),
+}
 # CoverageStats (CoverageStatisticsCalculator) fixtures: synth case -> (min_mq, max_coverage)
 COVERAGE_CASES = {"edge_2contigs_25x": (20, 300), "c1_chrI_10x": (20, 12)}
 DUMP_CASE = ("dump_custom8k_30x", dict(genome=2, custom_len=8000, depth=30, seed=5, noqual_rate=0.01,
@@ -136,7 +144,40 @@ def oracle_fixtures():
             print(name, "coverage ok")
 
 
+def full_size_fixtures(names=None):
+    """oracle VCF md5 + record count (+ SAM md5 pinning the generator) of the full-size configs"""
+    import json
+    import time
+    import ngsep_oracle
+    import pysynth
+    path = os.path.join(HERE, "full_sizes.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
+    with tempfile.TemporaryDirectory(dir=os.environ.get("NGSEP_GOLDEN_TMP")) as d:
+        for name, skw in FULL_CASES.items():
+            if names and name not in names:
+                continue
+            t = time.time()
+            syn = pysynth.Synth(**skw)
+            fa, sam, _ = syn.write(os.path.join(d, name))
+            syn.close()
+            vcf = os.path.join(d, name + ".vcf")
+            st = ngsep_oracle.run_ssvd(fa, sam, vcf)
+            n = sum(1 for l in open(vcf) if not l.startswith("#"))
+            out[name] = {"synth": skw, "sam_md5": md5(sam), "vcf_md5": md5(vcf), "vcf_records": n,
+                         "positions_genotyped": st.positions_genotyped, "oracle_seconds": round(st.seconds, 1)}
+            with gzip.GzipFile(os.path.join(HERE, name + ".vcf.gz"), "wb", mtime=0) as g:
+                g.write(open(vcf, "rb").read())
+            print(name, out[name], f"{time.time() - t:.0f}s", flush=True)
+            for f in (fa, sam, vcf, os.path.join(d, name + ".bam"), os.path.join(d, name + ".bam.bai")):
+                if os.path.exists(f):
+                    os.remove(f)
+    json.dump(out, open(path, "w"), indent=1, sort_keys=True)
+
+
 if __name__ == "__main__":
+    if "--full" in sys.argv:
+        full_size_fixtures([a for a in sys.argv[2:] if not a.startswith("-")] or None)
+        sys.exit(0)
     if "--no-reference" not in sys.argv:
         n = reference_fixture(os.path.join(HERE, "reference_demo_pl.csv.gz"))
         print("reference fixture rows:", n)

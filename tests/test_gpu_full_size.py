@@ -1,0 +1,67 @@
+"""BASELINE.json configs[1] (yeast 30x) and configs[2] (human chr20 30x) at full size: the HIP VCF equals,
+byte for byte, the oracle's VCF committed as tests/golden/<name>.vcf.gz (md5 and record count in
+tests/golden/full_sizes.json, made by make_golden.py --full in the build container).  The data is
+regenerated here from the same seeds; at 30x the scan's count bound drops ~98.6 % of the candidates, so
+these runs put the pruning of whole genomes under the oracle's check."""
+import gzip
+import hashlib
+import json
+import os
+
+import pytest
+
+import pysynth
+from ngsepcore_amd import GpuPileupSession
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CASES = json.load(open(os.path.join(GOLDEN, "full_sizes.json")))
+
+
+def _md5(path):
+    h = hashlib.md5()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def _first_diff(got_path, name):
+    want = gzip.open(os.path.join(GOLDEN, name + ".vcf.gz"), "rt").read().splitlines()
+    got = open(got_path).read().splitlines()
+    for k, (a, b) in enumerate(zip(want, got)):
+        if a != b:
+            return f"line {k + 1}: oracle {a!r} != gpu {b!r}"
+    return f"line counts {len(want)} vs {len(got)}"
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_full_size_vcf_identical(tmp_path, name):
+    case = CASES[name]
+    syn = pysynth.Synth(**case["synth"])
+    d = str(tmp_path)
+    fa, bam = os.path.join(d, "g.fa"), os.path.join(d, "g.bam")
+    pysynth.lib().ngs_synth_write_fasta(syn.h, fa.encode())
+    pysynth.lib().ngs_synth_write_bam(syn.h, bam.encode())
+    # path B: BAM on disk -> VCF (the drop-in for SingleSampleVariantsDetector)
+    out = os.path.join(d, "b.vcf")
+    with GpuPileupSession() as s:
+        s.load_fasta(fa)
+        s.processFile(bam, out)
+        st = s.stats()
+    assert st.positions_genotyped == case["positions_genotyped"]
+    assert _md5(out) == case["vcf_md5"], _first_diff(out, name)
+    # the bench's staged path over the same reads (resident layout, two passes in flight)
+    out2 = os.path.join(d, "a.vcf")
+    with GpuPileupSession() as s:
+        for n, q in syn.contigs():
+            s.set_reference(n, q)
+        s.stage(syn.batch())
+        s.stage_finish()
+        s.submit_staged()
+        s.submit_staged()
+        s.collect_staged()
+        s.collect_staged()
+        s.write_vcf(out2)
+    syn.close()
+    assert _md5(out2) == case["vcf_md5"], _first_diff(out2, name)

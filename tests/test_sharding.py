@@ -161,3 +161,49 @@ def test_gpu_region_calls_merged_equal_whole_file(tmp_path):
         s.processFile(bam2, full2)
     merged = call_bam_sharded(fa, bam2, os.path.join(str(tmp_path), "m2.vcf"))
     assert merged == open(full2).read()
+
+
+def _mvd_worker(rank, world, port, fa, sam, contigs, out_dir):
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        def call(name):
+            out = os.path.join(out_dir, f"m{rank}_{name}.vcf")
+            ngsep_oracle.run_mvd(fa, sam, out, query_seq=name)
+            return open(out).read()
+        call_sharded(contigs, call, os.path.join(out_dir, "merged_mvd.vcf"), dist)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_sharded_population_vcf_identical(tmp_path):
+    """MultisampleVariantsDetector split by sequence over two gloo ranks (the oracle restricted to each
+    sequence as the per-rank caller): merged population VCF == the single-process one."""
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=3, depth=6, seed=9, n_samples=6, snv_rate=2e-3)
+    contigs = [(n, len(s)) for n, s in syn.contigs()]
+    fa, sam, _ = syn.write(os.path.join(str(tmp_path), "p"))
+    syn.close()
+    full = os.path.join(str(tmp_path), "full_mvd.vcf")
+    ngsep_oracle.run_mvd(fa, sam, full)
+    mp.spawn(_mvd_worker, args=(2, _free_port(), fa, sam, contigs, str(tmp_path)), nprocs=2, join=True)
+    merged = open(os.path.join(str(tmp_path), "merged_mvd.vcf")).read()
+    assert merged == open(full).read()
+    assert len(split_vcf(merged)[1]) == 3
+
+
+@pytest.mark.gpu
+def test_gpu_population_sharded_identical(tmp_path):
+    """call_population_sharded (per-sequence population calls over the per-sample BAMs' indexes) == the
+    single-process MultisampleVariantsDetector VCF on the same BAMs."""
+    from ngsepcore_amd import MultisampleVariantsDetector
+    from ngsepcore_amd.sharding import call_population_sharded
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=3, depth=8, seed=10, n_samples=12, snv_rate=2e-3)
+    fa, _, _ = syn.write(os.path.join(str(tmp_path), "p"))
+    bams = syn.write_sample_bams(os.path.join(str(tmp_path), "p"))
+    syn.close()
+    d = MultisampleVariantsDetector()
+    d.setGenome(fa)
+    d.setOutFilename(os.path.join(str(tmp_path), "whole.vcf"))
+    d.run(bams).close()
+    merged = call_population_sharded(fa, bams, os.path.join(str(tmp_path), "sharded.vcf"))
+    assert merged == open(d.outFilename).read()
+    assert sum(1 for l in merged.splitlines() if not l.startswith("#")) > 20
