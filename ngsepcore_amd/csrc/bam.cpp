@@ -16,6 +16,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
@@ -116,6 +117,7 @@ struct ngsep_bam {
     std::mutex mu;
     std::condition_variable cv;
     std::deque<Chunk> q;
+    std::vector<RawBuf<uint8_t>> pool;   // consumed chunk buffers, reused by the decoder (no page faults / unmaps)
     bool stop = false, producer_done = false;
     // consumer side: the current decoded buffer; bytes [pos, end) not yet consumed
     RawBuf<uint8_t> mem;
@@ -141,11 +143,17 @@ struct ngsep_bam {
     // index
     bool bai_loaded = false;
     std::vector<BaiRef> bai;
-    // batch storage (filled in parallel, never value-initialised)
-    RawBuf<int32_t> b_seq, b_first, b_flags, b_rg, b_cig_n, b_cigar, b_seqlen;
-    RawBuf<int64_t> b_cig_off, b_seq_off;
-    RawBuf<uint8_t> b_hasq;
-    RawBuf<char> b_bases, b_quals;
+    // batch storage (filled in parallel, never value-initialised): two sets used in turn, so a batch stays
+    // valid while the next one is decoded (call_bam decodes batch k+1 while batch k is admitted)
+    struct BatchStore {
+        RawBuf<int32_t> b_seq, b_first, b_flags, b_rg, b_cig_n, b_cigar, b_seqlen;
+        RawBuf<int64_t> b_cig_off, b_seq_off;
+        RawBuf<uint8_t> b_hasq;
+        RawBuf<char> b_bases, b_quals;
+    } store[2];
+    int store_cur = 0;
+    // NGSEP_HOST_TIMING diagnostics: seconds in the decoder's inflate, the record cut, parse and emit
+    double t_inflate = 0, t_wait = 0, t_need = 0, t_cut = 0, t_parse = 0, t_emit = 0;
 };
 
 namespace {
@@ -204,16 +212,23 @@ void decoder_loop(ngsep_bam* b) {
         }
         std::vector<size_t> dout(boff.size() + 1, 0);
         for (size_t k = 0; k < boff.size(); k++) dout[k + 1] = dout[k] + bisize[k];
+        {
+            std::lock_guard<std::mutex> lk(b->mu);
+            if (!b->pool.empty()) { ch.mem = std::move(b->pool.back()); b->pool.pop_back(); }
+        }
+        ch.mem.n = 0;                       // nothing to keep when a recycled buffer grows
         ch.mem.resize(kChunkHead + dout.back());
         ch.len = dout.back();
         uint8_t* dst = ch.mem.data() + kChunkHead;
         std::atomic<int> bad{0};
         const Inflater& inf = Inflater::get();
+        const auto ti0 = std::chrono::steady_clock::now();
         parallel_for((int64_t)boff.size(), 16, [&](int64_t lo, int64_t hi) {
             for (int64_t k = lo; k < hi; k++)
                 if (bisize[(size_t)k] && !inf.run(comp.data() + boff[(size_t)k], bclen[(size_t)k], dst + dout[(size_t)k], bisize[(size_t)k]))
                     bad = 1;
         });
+        b->t_inflate += std::chrono::duration<double>(std::chrono::steady_clock::now() - ti0).count();
         if (bad && ch.err.empty()) ch.err = "BGZF inflate failed";
         ch.eof = file_eof && carry.empty();
         const bool last = ch.eof || !ch.err.empty();
@@ -252,9 +267,12 @@ void start_decoder(ngsep_bam* b) {
 // ensures at least n unconsumed bytes; false at EOF (err set on a format error).  The unconsumed tail moves
 // into the next chunk's headroom (no copy of the chunk itself).
 bool need(ngsep_bam* b, size_t n, std::string& err) {
+    struct T { ngsep_bam* b; std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+               ~T() { b->t_need += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); } } tm{b};
     while (b->end - b->pos < n) {
         if (b->eof) return false;
         Chunk ch;
+        const auto tw0 = std::chrono::steady_clock::now();
         {
             std::unique_lock<std::mutex> lk(b->mu);
             b->cv.wait(lk, [&] { return !b->q.empty() || b->producer_done; });
@@ -262,6 +280,7 @@ bool need(ngsep_bam* b, size_t n, std::string& err) {
             ch = std::move(b->q.front());
             b->q.pop_front();
         }
+        b->t_wait += std::chrono::duration<double>(std::chrono::steady_clock::now() - tw0).count();
         b->cv.notify_all();
         if (!ch.err.empty()) { err = ch.err; b->eof = true; return false; }
         const size_t rem = b->end - b->pos;
@@ -281,6 +300,11 @@ bool need(ngsep_bam* b, size_t n, std::string& err) {
             b->buf = b->mem.data();
             b->pos = 0;
             b->end = rem + ch.len;
+            ch.mem = std::move(m);         // the consumed buffer (now in m) goes back to the pool below
+        }
+        {
+            std::lock_guard<std::mutex> lk(b->mu);
+            if (ch.mem.cap && b->pool.size() < 6) b->pool.push_back(std::move(ch.mem));
         }
         if (ch.eof) b->eof = true;
     }
@@ -477,13 +501,18 @@ extern "C" int ngsep_bam_set_region(ngsep_bam* b, const char* seq_name, int64_t 
     return NGSEP_OK;
 }
 
-extern "C" int ngsep_bam_next_batch(ngsep_bam* b, int64_t max_reads, ngsep_read_batch* out) {
-    if (!b || !out) return NGSEP_E_INVALID;
+namespace {
+
+// one batch of up to max_reads kept records into B (ngsep_bam_next_batch)
+int fill_batch(ngsep_bam* b, ngsep_bam::BatchStore& B, int64_t max_reads, ngsep_read_batch* out, bool* retry, bool packed) {
+    *retry = false;
     static const int kOp[9] = {3, 2, 1, 5, 6, 0, 4, 3, 7};   // BAM M I D N S H P = X -> NGSEP H0 D1 I2 M3 P4 N5 S6 X7
     static const char kNt[] = "=ACMGRSVTWYHKDBN";
     std::string err;
     // 1. cut up to max_reads whole records (their offsets in buf), sequentially along the block_size chain
     std::vector<size_t> roff;
+    roff.reserve((size_t)std::min<int64_t>(max_reads, 1 << 20));
+    const auto tc0 = std::chrono::steady_clock::now();
     // (more decoded bytes are only pulled in while no record is cut: pulling compacts the buffer)
     while ((int64_t)roff.size() < max_reads && !b->region_done) {
         if (b->end - b->pos < 4) {
@@ -498,6 +527,9 @@ extern "C" int ngsep_bam_next_batch(ngsep_bam* b, int64_t max_reads, ngsep_read_
             if (!need(b, 4 + (size_t)bs, err)) return set_error(b->ctx, NGSEP_E_FORMAT, err.empty() ? "truncated BAM record" : err);
         }
         const uint8_t* r = &b->buf[b->pos + 4];
+        // the record chain is a dependent walk through freshly inflated memory: pull the lines a few
+        // records ahead (the chain only moves forward)
+        if (b->end - b->pos > 4096) __builtin_prefetch(&b->buf[b->pos + 4096]);
         if (b->region_ref >= 0) {
             const int32_t refid = rd<int32_t>(r), pos0 = rd<int32_t>(r + 4);
             if (refid != b->region_ref || (int64_t)pos0 + 1 > b->region_last) { b->region_done = true; break; }
@@ -507,6 +539,7 @@ extern "C" int ngsep_bam_next_batch(ngsep_bam* b, int64_t max_reads, ngsep_read_
     }
     if (!err.empty()) return set_error(b->ctx, NGSEP_E_FORMAT, err);
     const int64_t n = (int64_t)roff.size();
+    const auto tc1 = std::chrono::steady_clock::now();
     // 2. per record: filters (isSameAlignment against the previous raw record, isMultiple, filter flags,
     //    malformed CIGAR / read length) and output sizes -- in parallel
     struct Rec { int32_t keep, ncig, lseq, flags, rg, seq, first; };
@@ -575,8 +608,15 @@ extern "C" int ngsep_bam_next_batch(ngsep_bam* b, int64_t max_reads, ngsep_read_
                 }
                 if (t0 == 'N' && t1 == 'H' && isint && ty != 'A') { nh = (int)iv; nh_present = 1; }
                 if (t0 == 'R' && t1 == 'G' && ty == 'Z') {
-                    auto it = b->rg_index.find(std::string((const char*)v));
-                    rg = it == b->rg_index.end() ? -1 : it->second;   // getReadGroup() is null if not in header
+                    // getReadGroup() is null if not in the header (a few groups: compared in place)
+                    rg = -1;
+                    if (b->rg_ids.size() <= 16) {
+                        for (size_t g = 0; g < b->rg_ids.size(); g++)
+                            if (std::strcmp(b->rg_ids[g].c_str(), (const char*)v) == 0) { rg = (int32_t)g; break; }
+                    } else {
+                        auto it = b->rg_index.find(std::string((const char*)v));
+                        if (it != b->rg_index.end()) rg = it->second;
+                    }
                 }
                 t = v + sz;
             }
@@ -621,6 +661,7 @@ extern "C" int ngsep_bam_next_batch(ngsep_bam* b, int64_t max_reads, ngsep_read_
         auto nm = name_of(roff[(size_t)n - 1]);
         b->last_name.assign(nm.first, nm.second);
     }
+    const auto tc2 = std::chrono::steady_clock::now();
     // 3. output offsets of the kept records, then their fields in parallel
     std::vector<int64_t> oidx((size_t)n + 1, 0), coff((size_t)n + 1, 0), soff((size_t)n + 1, 0);
     for (int64_t i = 0; i < n; i++) {
@@ -630,12 +671,12 @@ extern "C" int ngsep_bam_next_batch(ngsep_bam* b, int64_t max_reads, ngsep_read_
         soff[(size_t)i + 1] = soff[(size_t)i] + (o.keep ? o.lseq : 0);
     }
     const int64_t nk = oidx[(size_t)n];
-    b->b_seq.resize((size_t)nk); b->b_first.resize((size_t)nk); b->b_flags.resize((size_t)nk); b->b_rg.resize((size_t)nk);
-    b->b_cig_off.resize((size_t)nk); b->b_cig_n.resize((size_t)nk); b->b_seq_off.resize((size_t)nk); b->b_seqlen.resize((size_t)nk);
-    b->b_hasq.resize((size_t)nk);
-    b->b_cigar.resize((size_t)coff[(size_t)n]);
-    b->b_bases.resize((size_t)soff[(size_t)n]);
-    b->b_quals.resize((size_t)soff[(size_t)n]);
+    B.b_seq.resize((size_t)nk); B.b_first.resize((size_t)nk); B.b_flags.resize((size_t)nk); B.b_rg.resize((size_t)nk);
+    B.b_cig_off.resize((size_t)nk); B.b_cig_n.resize((size_t)nk); B.b_seq_off.resize((size_t)nk); B.b_seqlen.resize((size_t)nk);
+    B.b_hasq.resize((size_t)nk);
+    B.b_cigar.resize((size_t)coff[(size_t)n]);
+    B.b_bases.resize((size_t)soff[(size_t)n]);
+    B.b_quals.resize((size_t)soff[(size_t)n]);
     parallel_for(n, 4096, [&](int64_t lo, int64_t hi) {
         for (int64_t i = lo; i < hi; i++) {
             const Rec& o = rec[(size_t)i];
@@ -648,13 +689,13 @@ extern "C" int ngsep_bam_next_batch(ngsep_bam* b, int64_t max_reads, ngsep_read_
             const uint8_t* cig = r + 32 + l_name;
             const uint8_t* seq = cig + 4 * n_cig;
             const uint8_t* qual = seq + (l_seq + 1) / 2;
-            b->b_seq[k] = o.seq;
-            b->b_first[k] = o.first;
-            b->b_flags[k] = o.flags;
-            b->b_rg[k] = o.rg;
-            b->b_cig_off[k] = coff[(size_t)i];
-            b->b_cig_n[k] = o.ncig;
-            int32_t* cd = &b->b_cigar[(size_t)coff[(size_t)i]];
+            B.b_seq[k] = o.seq;
+            B.b_first[k] = o.first;
+            B.b_flags[k] = o.flags;
+            B.b_rg[k] = o.rg;
+            B.b_cig_off[k] = coff[(size_t)i];
+            B.b_cig_n[k] = o.ncig;
+            int32_t* cd = &B.b_cigar[(size_t)coff[(size_t)i]];
             int nc = 0;
             for (int c2 = 0; c2 < n_cig; c2++) {
                 const uint32_t v = rd<uint32_t>(cig + 4 * c2);
@@ -662,49 +703,98 @@ extern "C" int ngsep_bam_next_batch(ngsep_bam* b, int64_t max_reads, ngsep_read_
                 if (nc > 0 && (cd[nc - 1] & 7) == nop) cd[nc - 1] += (int32_t)(v >> 4) * 8;
                 else cd[nc++] = (int32_t)(v >> 4) * 8 + nop;
             }
-            b->b_seq_off[k] = soff[(size_t)i];
-            b->b_seqlen[k] = l_seq;
-            char* bs = &b->b_bases[(size_t)soff[(size_t)i]];
-            char* qs = &b->b_quals[(size_t)soff[(size_t)i]];
-            for (int32_t j = 0; j + 1 < l_seq; j += 2) {
-                const uint8_t byte = seq[j >> 1];
-                bs[j] = kNt[byte >> 4];
-                bs[j + 1] = kNt[byte & 15];
-            }
-            if (l_seq & 1) bs[l_seq - 1] = kNt[seq[(l_seq - 1) >> 1] >> 4];
+            B.b_seq_off[k] = soff[(size_t)i];
+            B.b_seqlen[k] = l_seq;
+            char* bs = &B.b_bases[(size_t)soff[(size_t)i]];
+            char* qs = &B.b_quals[(size_t)soff[(size_t)i]];
             const bool hasq = l_seq > 0 && qual[0] != 0xFF;
-            if (hasq) for (int32_t j = 0; j < l_seq; j++) qs[j] = (char)(qual[j] + 33);
-            else std::memset(qs, '!', (size_t)l_seq);
-            b->b_hasq[k] = hasq ? 1 : 0;
+            if (packed) {
+                // BAM's own encoding (ReadView::packed): the 4-bit bases and the raw qualities as they are
+                std::memcpy(bs, seq, (size_t)(l_seq + 1) / 2);
+                if (hasq) std::memcpy(qs, qual, (size_t)l_seq);
+            } else {
+                static const uint16_t* pair = [] {    // one byte of two bases -> their two characters
+                    static uint16_t t[256];
+                    for (int v = 0; v < 256; v++) t[v] = (uint16_t)((uint8_t)kNt[v >> 4] | ((uint16_t)(uint8_t)kNt[v & 15] << 8));
+                    return t;
+                }();
+                for (int32_t j = 0; j + 1 < l_seq; j += 2) std::memcpy(bs + j, &pair[seq[j >> 1]], 2);
+                if (l_seq & 1) bs[l_seq - 1] = kNt[seq[(l_seq - 1) >> 1] >> 4];
+                if (hasq) for (int32_t j = 0; j < l_seq; j++) qs[j] = (char)(qual[j] + 33);
+                else std::memset(qs, '!', (size_t)l_seq);
+            }
+            B.b_hasq[k] = hasq ? 1 : 0;
         }
     });
+    const auto tc3 = std::chrono::steady_clock::now();
+    b->t_cut += std::chrono::duration<double>(tc1 - tc0).count();
+    b->t_parse += std::chrono::duration<double>(tc2 - tc1).count();
+    b->t_emit += std::chrono::duration<double>(tc3 - tc2).count();
     out->n_reads = nk;
-    out->seq_id = b->b_seq.data();
-    out->first = b->b_first.data();
-    out->flags = b->b_flags.data();
-    out->read_group = b->b_rg.data();
-    out->cigar_off = b->b_cig_off.data();
-    out->cigar_n = b->b_cig_n.data();
-    out->cigar = b->b_cigar.data();
-    out->seq_off = b->b_seq_off.data();
-    out->seq_len = b->b_seqlen.data();
-    out->bases = b->b_bases.data();
-    out->quals = b->b_quals.data();
-    out->has_quals = b->b_hasq.data();
+    out->seq_id = B.b_seq.data();
+    out->first = B.b_first.data();
+    out->flags = B.b_flags.data();
+    out->read_group = B.b_rg.data();
+    out->cigar_off = B.b_cig_off.data();
+    out->cigar_n = B.b_cig_n.data();
+    out->cigar = B.b_cigar.data();
+    out->seq_off = B.b_seq_off.data();
+    out->seq_len = B.b_seqlen.data();
+    out->bases = B.b_bases.data();
+    out->quals = B.b_quals.data();
+    out->has_quals = B.b_hasq.data();
     // a batch with every record filtered is not the end of the file: the caller stops at n_reads == 0
-    if (nk == 0 && n > 0) return ngsep_bam_next_batch(b, max_reads, out);
+    *retry = nk == 0 && n > 0;
     return NGSEP_OK;
+}
+
+}  // namespace
+
+static int next_batch(ngsep_bam* b, int64_t max_reads, ngsep_read_batch* out, bool packed) {
+    if (!b || !out) return NGSEP_E_INVALID;
+    ngsep_bam::BatchStore& B = b->store[b->store_cur];
+    b->store_cur ^= 1;
+    bool retry = true;
+    int rc = NGSEP_OK;
+    while (retry && rc == NGSEP_OK) rc = fill_batch(b, B, max_reads, out, &retry, packed);
+    return rc;
+}
+
+extern "C" int ngsep_bam_next_batch(ngsep_bam* b, int64_t max_reads, ngsep_read_batch* out) {
+    return next_batch(b, max_reads, out, false);
 }
 
 extern "C" int ngsep_bam_close(ngsep_bam* b) {
     if (!b) return NGSEP_E_INVALID;
     stop_decoder(b);
+    if (std::getenv("NGSEP_HOST_TIMING"))
+        std::fprintf(stderr, "[ngsep host] bam: inflate %.3f s (decoder thread), consumer wait %.3f s, need %.3f s, cut %.3f s (incl. wait), parse %.3f s, emit %.3f s\n",
+                     b->t_inflate, b->t_wait, b->t_need, b->t_cut, b->t_parse, b->t_emit);
     if (b->f) std::fclose(b->f);
     delete b;
     return NGSEP_OK;
 }
 
 namespace ngsep {
+// the reader's batches through fn in order, the next batch decoding (its own storage set) while fn runs on
+// the current one; stops at the end of the file, at an error, or once the query region is done
+template <class F>
+static int for_each_batch(ngsep_ctx* c, ngsep_bam* b, F&& fn) {
+    // (BAM-encoded batches: bases and qualities are not re-encoded, ReadView::packed)
+    ngsep_read_batch batch[2];
+    int cur = 0;
+    int rc = next_batch(b, 1 << 20, &batch[0], true);
+    while (rc == NGSEP_OK && batch[cur].n_reads > 0 && !c->query_done) {
+        int rc_next = NGSEP_OK;
+        std::thread th([&] { rc_next = next_batch(b, 1 << 20, &batch[cur ^ 1], true); });
+        rc = fn(batch[cur]);
+        th.join();
+        if (rc == NGSEP_OK) rc = rc_next;
+        cur ^= 1;
+    }
+    return rc;
+}
+
 // SingleSampleVariantsDetector.findSNVS (:896-931) + onSequenceEnd/saveSequenceVariants (:933-968, :1026-1032).
 // With -querySeq the reader jumps to the region through the BAI index when there is one (the reference
 // decodes the file from its start, AlignmentsPileupGenerator.java:310-322, 342-354); reading stops once the
@@ -719,15 +809,11 @@ int call_bam(ngsep_ctx* c, const char* bam_path, const char* out_vcf) {
     }
     rc = ngsep_write_vcf_header(c, out_vcf);
     if (rc != NGSEP_OK) { ngsep_bam_close(b); return rc; }
-    ngsep_read_batch batch;
-    while (!c->query_done) {
-        rc = ngsep_bam_next_batch(b, 1 << 20, &batch);
-        if (rc != NGSEP_OK) break;
-        if (batch.n_reads == 0) break;
-        rc = ngsep_process_alignments(c, &batch);
-        if (rc != NGSEP_OK) break;
-        if (!c->sites.empty()) { rc = ngsep_append_vcf_records(c, out_vcf); if (rc != NGSEP_OK) break; }
-    }
+    rc = for_each_batch(c, b, [&](const ngsep_read_batch& batch) {
+        int r = process_alignments_packed(c, &batch);
+        if (r == NGSEP_OK && !c->sites.empty()) r = ngsep_append_vcf_records(c, out_vcf);
+        return r;
+    });
     ngsep_bam_close(b);
     if (rc != NGSEP_OK) return rc;
     rc = ngsep_notify_end(c);
@@ -744,13 +830,7 @@ extern "C" int ngsep_coverage_bam(ngsep_ctx* c, const char* bam_path, const char
     ngsep_bam* b = nullptr;
     int rc = ngsep_bam_open(c, bam_path, &b);
     if (rc != NGSEP_OK) return rc;
-    ngsep_read_batch batch;
-    while (true) {
-        rc = ngsep_bam_next_batch(b, 1 << 20, &batch);
-        if (rc != NGSEP_OK || batch.n_reads == 0) break;
-        rc = ngsep_process_alignments(c, &batch);
-        if (rc != NGSEP_OK) break;
-    }
+    rc = for_each_batch(c, b, [&](const ngsep_read_batch& batch) { return process_alignments_packed(c, &batch); });
     ngsep_bam_close(b);
     if (rc != NGSEP_OK) return rc;
     rc = ngsep_notify_end(c);

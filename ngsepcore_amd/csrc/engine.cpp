@@ -175,13 +175,72 @@ static const uint8_t* code_table() {
     return t;
 }
 
+// the same codes from BAM's encoding: raw quality (0xFF = none: '+' + ... is handled by the caller) and 4-bit base
+static const uint8_t* code_table_packed() {
+    static uint8_t t[256 * 16];
+    static const bool init = [] {
+        static const char kNt[] = "=ACMGRSVTWYHKDBN";
+        const uint8_t* ascii = code_table();
+        for (int rq = 0; rq < 256; rq++)
+            for (int nb = 0; nb < 16; nb++) t[rq * 16 + nb] = ascii[(size_t)std::min(255, rq + 33) * 256 + (uint8_t)kNt[nb]];
+        return true;
+    }();
+    (void)init;
+    return t;
+}
+static inline char packed_base(const char* seq, int64_t i) {
+    static const char kNt[] = "=ACMGRSVTWYHKDBN";
+    const uint8_t b = (uint8_t)seq[i >> 1];
+    return kNt[(i & 1) ? (b & 15) : (b >> 4)];
+}
+
 void project_read(const ngsep_ctx* c, const ReadView& r, uint8_t* out) {
     const int64_t span = (int64_t)r.last - r.first + 1;
     if (span <= 0) return;
     if (!r.chars) { std::memset(out, 0, (size_t)span); return; }   // getAlleleCall returns null without characters
     // fast path: no I/D item and nothing ignored at the read ends -- every aligned base is a call
     // (updateAlleleCallsInfo's masks are all about indels and ignore5/3, ReadAlignment.java:747-834)
-    if (r.indel_len == 0 && c->params.ignore5 == 0 && c->params.ignore3 == 0) {
+    if (r.packed && r.indel_len == 0 && c->params.ignore5 == 0 && c->params.ignore3 == 0) {
+        static const uint8_t* tab = code_table_packed();
+        const uint8_t* seq = reinterpret_cast<const uint8_t*>(r.chars);
+        const uint8_t* quals = reinterpret_cast<const uint8_t*>(r.quals);
+        int64_t o = 0, rp = 0;
+        for (int32_t k = 0; k < r.n_cigar; k++) {
+            const int32_t v = r.cigar[k], len = v / 8, op = v & 7;
+            const bool cRef = op & 1, cRead = (op & 2) != 0;
+            if (cRef && cRead) {
+                const int64_t n = std::min<int64_t>(len, std::min<int64_t>(span - o, (int64_t)r.len - rp));
+                int64_t j = 0;
+                if (quals) {
+                    if (((rp ^ 1) & 1) == 0 && n > 0) {        // odd start: the low nibble of a byte first
+                        out[o] = tab[(size_t)quals[rp] * 16 + (seq[rp >> 1] & 15)];
+                        j = 1;
+                    }
+                    for (; j + 1 < n; j += 2) {                  // whole bytes: two bases
+                        const uint8_t b = seq[(rp + j) >> 1];
+                        out[o + j] = tab[(size_t)quals[rp + j] * 16 + (b >> 4)];
+                        out[o + j + 1] = tab[(size_t)quals[rp + j + 1] * 16 + (b & 15)];
+                    }
+                    for (; j < n; j++) {
+                        const uint8_t b = seq[(rp + j) >> 1];
+                        out[o + j] = tab[(size_t)quals[rp + j] * 16 + (((rp + j) & 1) ? (b & 15) : (b >> 4))];
+                    }
+                } else {
+                    for (; j < n; j++) {
+                        const uint8_t b = seq[(rp + j) >> 1];
+                        out[o + j] = tab[(size_t)('+' - 33) * 16 + (((rp + j) & 1) ? (b & 15) : (b >> 4))];
+                    }
+                }
+                for (j = n > 0 ? n : 0; j < len && o + j < span; j++) out[o + j] = 0;
+            } else if (cRef) {
+                std::memset(out + o, 0, (size_t)std::max<int64_t>(0, std::min<int64_t>(len, span - o)));
+            }
+            if (cRef) o += len;
+            if (cRead) rp += len;
+        }
+        return;
+    }
+    if (!r.packed && r.indel_len == 0 && c->params.ignore5 == 0 && c->params.ignore3 == 0) {
         static const uint8_t* tab = code_table();
         const uint8_t* chars = reinterpret_cast<const uint8_t*>(r.chars);
         const uint8_t* quals = reinterpret_cast<const uint8_t*>(r.quals);
@@ -225,10 +284,10 @@ void project_read(const ngsep_ctx* c, const ReadView& r, uint8_t* out) {
                 int64_t o = refPos + j - r.first;
                 if (rp >= read_length || o < 0 || o >= span) continue;
                 if (acl[(size_t)rp] != 1) continue;   // 0: masked (getAlleleCall null); >1: skipped for span 1
-                int qc = r.quals ? (unsigned char)r.quals[rp] : '+';                   // getBaseQualityScore
+                int qc = r.quals ? (unsigned char)r.quals[rp] + (r.packed ? 33 : 0) : '+';   // getBaseQualityScore
                 if (qc > 127) qc = 127;                                                 // setQualityScores cap
                 int q = (int8_t)std::min(30, qc - 33);
-                int a = dna_index(r.chars[rp]);
+                int a = dna_index(r.packed ? packed_base(r.chars, rp) : r.chars[rp]);
                 uint8_t code;
                 if (q <= 3) code = (uint8_t)(kCodeCounted | (q < 0 ? 0 : q));
                 else if (a < 0) code = (uint8_t)(kCodeCounted | q);
@@ -243,9 +302,26 @@ void project_read(const ngsep_ctx* c, const ReadView& r, uint8_t* out) {
 
 // admission of one read into the current sequence's pending list (AlignmentsPileupGenerator
 // .processSameStartAlns :428-430); its projection is deferred to project_pending (batched, parallel)
+static void admit_core(ngsep_ctx* c, int32_t first, int32_t last, int32_t flags, int32_t rg, int32_t indel_len);
 static void admit(ngsep_ctx* c, const ReadView& r) {
+    if (!c->params.coverage_stats) {
+        if (r.bidx >= 0) c->to_project.push_back(r.bidx);
+        else {
+            c->to_project.push_back(-1 - (int32_t)c->to_project_carried.size());
+            c->to_project_carried.push_back(r);
+        }
+    }
+    admit_core(c, r.first, r.last, r.flags, r.rg, r.indel_len);
+}
+// the same for the current batch's read i (no view built)
+static inline void admit_index(ngsep_ctx* c, int32_t i) {
+    const ngsep_read_batch* b = c->cur_batch.b;
+    if (!c->params.coverage_stats) c->to_project.push_back(i);
+    admit_core(c, b->first[i], c->cur_batch.last[i], b->flags[i], b->read_group ? b->read_group[i] : -1, c->cur_batch.indel[i]);
+}
+static void admit_core(ngsep_ctx* c, int32_t first, int32_t last, int32_t flags, int32_t rg, int32_t indel_len) {
+    struct { int32_t first, flags, rg, indel_len; } r{first, flags, rg, indel_len};
     ContigReads& cr = c->contig;
-    const int32_t last = r.last;
     if (c->params.coverage_stats) {
         // CoverageStatisticsCalculator: only [first, last] and isUnique reach the listener
         // (PileupRecord.addAlignment, :154-167); positions past the sequence end still get pileups
@@ -270,13 +346,12 @@ static void admit(ngsep_ctx* c, const ReadView& r) {
         cr.sample.push_back((int16_t)(in ? c->rg_sample[r.rg] : -1));
         cr.rank.push_back((uint8_t)(in && c->rg_sample[r.rg] >= 0 ? c->rg_rank[r.rg] : 0));
     }
-    c->to_project.push_back(r);
     if (r.indel_len > 0) cr.indel_reads.push_back({r.first, last + r.indel_len});   // the realigner's events
     int32_t span = last - r.first + 1;
     if (span > cr.max_span) cr.max_span = span;
     // union of covered positions inside the sequence (and the query range)
     int64_t lo = r.first, hi = last;
-    int64_t len = (int64_t)c->seq_bases[r.seq_id].size();
+    const int64_t len = cr.seq_len;
     if (hi > len) hi = len;
     if (lo < 1) lo = 1;
     if (c->params.query_seq[0]) {
@@ -293,38 +368,95 @@ static void admit(ngsep_ctx* c, const ReadView& r) {
 
 // projects the admitted reads whose bytes are still pending into the sequence's byte store, on all
 // host threads (every read's bytes go to its own preallocated range)
+// the view of read i of the batch being admitted
+static inline ReadView batch_view(const BatchRef& br, int32_t i) {
+    const ngsep_read_batch* b = br.b;
+    ReadView r;
+    r.seq_id = b->seq_id[i];
+    r.first = b->first[i];
+    r.last = br.last[i];
+    r.flags = b->flags[i];
+    r.rg = b->read_group ? b->read_group[i] : -1;
+    r.cigar = b->cigar + b->cigar_off[i];
+    r.n_cigar = b->cigar_n[i];
+    const int32_t sl = b->seq_len[i];
+    r.len = sl > 0 ? sl : 0;
+    r.chars = nullptr;
+    r.quals = nullptr;
+    if (sl > 0) {
+        r.chars = b->bases + b->seq_off[i];
+        if (b->quals && (!b->has_quals || b->has_quals[i])) r.quals = b->quals + b->seq_off[i];
+    }
+    r.indel_len = br.indel[i];
+    r.packed = br.packed;
+    r.bidx = i;
+    return r;
+}
+
 static void project_pending(ngsep_ctx* c) {
-    std::vector<ReadView>& v = c->to_project;
+    std::vector<int32_t>& v = c->to_project;
     if (v.empty()) return;
     ContigReads& cr = c->contig;
     const size_t n = v.size();
+    const size_t b0 = cr.bptr.size();          // the admitted reads' [first, last] are cr.first/last[b0 ...]
     std::vector<int64_t> off(n + 1, 0);
+    int32_t maxlast = INT32_MIN;
     for (size_t i = 0; i < n; i++) {
-        const int64_t span = (int64_t)v[i].last - v[i].first + 1;
+        const int64_t span = (int64_t)cr.last[b0 + i] - cr.first[b0 + i] + 1;
         off[i + 1] = off[i] + (span > 0 ? span : 0);
+        maxlast = std::max(maxlast, cr.last[b0 + i]);
     }
-    // a fresh uninitialised chunk for this batch's codes: every read writes its own range
-    cr.chunks.emplace_back();
-    HostArray<uint8_t>& ch = cr.chunks.back();
-    ch.alloc((size_t)std::max<int64_t>(off[n], 1));
+    // an uninitialised chunk for this batch's codes (a released one when it is large enough): every read
+    // writes its own range
+    const size_t need = (size_t)std::max<int64_t>(off[n], 1);
+    HostArray<uint8_t> ch;
+    for (size_t k = 0; k < c->chunk_pool.size(); k++)
+        if (c->chunk_pool[k].n >= need) {
+            ch = std::move(c->chunk_pool[k]);
+            c->chunk_pool.erase(c->chunk_pool.begin() + (ptrdiff_t)k);
+            break;
+        }
+    if (!ch.p) ch.alloc(need + need / 8);
     uint8_t* base = ch.p;
-    const size_t b0 = cr.bptr.size();
+    cr.chunks.emplace_back(std::move(ch));
     cr.bptr.resize(b0 + n);
     for (size_t i = 0; i < n; i++) cr.bptr[b0 + i] = base + off[i];
+    cr.chunk_end.push_back(b0 + n);
+    cr.chunk_maxlast.push_back(maxlast);
     static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     const auto t1 = std::chrono::steady_clock::now();
+    const BatchRef br = c->cur_batch;
+    const int32_t* ent = v.data();
+    const ReadView* carried = c->to_project_carried.data();
     parallel_for((int64_t)n, 2048, [&](int64_t lo, int64_t hi) {
-        for (int64_t i = lo; i < hi; i++) project_read(c, v[(size_t)i], base + off[(size_t)i]);
+        for (int64_t i = lo; i < hi; i++) {
+            const int32_t e = ent[i];
+            if (e >= 0) project_read(c, batch_view(br, e), base + off[(size_t)i]);
+            else project_read(c, carried[-1 - e], base + off[(size_t)i]);
+        }
     });
     if (host_timing)
         std::fprintf(stderr, "[ngsep host] projection: %.1f ms (%u threads)\n",
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count(), host_threads());
     v.clear();
+    c->to_project_carried.clear();
 }
 
 // AlignmentsPileupGenerator.processSameStartAlns (:407-433)
 static void process_same_start(ngsep_ctx* c) {
-    if (c->ss_primary.empty() && c->ss_secondary.empty()) return;
+    if (c->ss_one >= 0) {                         // one primary alignment at this start (the common case): admitted
+        admit_index(c, c->ss_one);
+        c->ss_one = -1;
+        return;
+    }
+    if (c->ss_secondary.empty()) {
+        if (c->ss_primary.empty()) return;
+        if (c->ss_primary.size() == 1) {          // one alignment at this start (the common case): admitted
+            admit(c, c->ss_primary[0]);
+            c->ss_primary.clear();
+            return;
+        }
+    }
     std::pair<int32_t, int32_t> per_rg_small[8];   // (rg, count): few read groups per start
     std::vector<std::pair<int32_t, int32_t>> per_rg_big;
     int n_rg = 0;
@@ -349,11 +481,25 @@ static void process_same_start(ngsep_ctx* c) {
 }
 
 // flushes the current sequence: onSequenceEnd of the listener chain
+static int stream_advance(ngsep_ctx* c, bool final);
+
+static bool streaming(const ngsep_ctx* c) { return !c->staging_mode && !c->params.coverage_stats && !c->params.multisample; }
+
 static int flush_sequence(ngsep_ctx* c) {
     if (c->cur_seq < 0) return NGSEP_OK;
     process_same_start(c);
     project_pending(c);
-    int rc = stage_contig_reads(c, c->contig, !c->staging_mode);
+    int rc;
+    if (streaming(c)) {
+        // the sequence's remaining windows, then its genotyped-position count
+        rc = stream_advance(c, true);
+        c->stats.positions_genotyped += c->contig.covered - c->stream.carved_inside;
+        c->stream.next_w0 = 0;
+        c->stream.indel_lo = c->stream.chunk_lo = 0;
+        c->stream.carved_inside = 0;
+    } else {
+        rc = stage_contig_reads(c, c->contig, !c->staging_mode);
+    }
     c->contig.clear();
     c->cur_seq = -1;
     return rc;
@@ -417,8 +563,161 @@ int stage_contig_reads(ngsep_ctx* c, ContigReads& cr, bool run_now) {
     return rc;
 }
 
+// ---- streamed single-sample windows ----
+// While the alignments are read, every window of WL positions whose reads are all admitted (and whose
+// carved indel regions are known: the stream is 2 R past it) is laid out, uploaded and run on a worker
+// thread, one window at a time, while admission goes on; its records join the context's list in window
+// order.  The window cut changes no call (windows carry a halo of the reads' span).
+static int64_t stream_window_len(const ngsep_ctx* c) {
+    static const int64_t env = std::getenv("NGSEP_STREAM_WINDOW") ? std::atoll(std::getenv("NGSEP_STREAM_WINDOW")) : 0;   // tuning
+    int64_t w = env > 0 ? env : (int64_t)1 << 22;
+    if (c->params.window_positions > 0) w = std::min<int64_t>(w, c->params.window_positions);
+    return std::max<int64_t>(w, 1024);
+}
+
+static void run_window_job(ngsep_ctx* c, WindowJob* j);
+
+// joins the window in flight: its records after those already called, then the projected chunks no later
+// window reads are released
+static int stream_collect(ngsep_ctx* c) {
+    auto& st = c->stream;
+    if (!st.job) return NGSEP_OK;
+    st.job->th.join();
+    std::unique_ptr<WindowJob> j = std::move(st.job);
+    if (j->rc != NGSEP_OK) return set_error(c, j->rc, j->err);
+    if (c->sites.empty()) c->sites.swap(j->sites);
+    else if (!j->sites.empty()) {
+        const size_t from = c->sites.size();
+        c->sites.reserve(from + j->sites.size());
+        std::memcpy(c->sites.buf + from, j->sites.buf, j->sites.size() * sizeof(ngsep_site_out));
+        c->sites.n = from + j->sites.size();
+    }
+    ContigReads& cr = c->contig;
+    // (a later window's reads start at >= its w0 - max span + 1; reads ending 2 spans before it reach no tile of it)
+    const int64_t keep_from = st.next_w0 - 2 * (int64_t)std::max<int32_t>(1, cr.max_span) - 64;
+    while (st.chunk_lo + 1 < cr.chunks.size() && cr.chunk_maxlast[st.chunk_lo] < keep_from) {
+        HostArray<uint8_t>& ch = cr.chunks[st.chunk_lo++];
+        if (c->chunk_pool.size() < 4) c->chunk_pool.push_back(std::move(ch));   // the next batches' projections reuse it
+        else ch.release();
+    }
+    return NGSEP_OK;
+}
+
+// hands [w0, w1] of the current sequence to the worker: its reads (first in [w0 - max span + 1, w1]) in
+// window coordinates, and the carved indel regions inside it (carve_indel_regions' geometry with R = 100 +
+// the longest span admitted so far)
+static void stream_launch(ngsep_ctx* c, int64_t w0, int64_t w1) {
+    auto& st = c->stream;
+    ContigReads& cr = c->contig;
+    const int32_t max_span = std::max<int32_t>(1, cr.max_span);
+    const int64_t lo = std::lower_bound(cr.first.begin(), cr.first.end(), (int32_t)std::max<int64_t>(INT32_MIN, w0 - max_span + 1)) - cr.first.begin();
+    const int64_t hi = std::upper_bound(cr.first.begin(), cr.first.end(), (int32_t)w1) - cr.first.begin();
+    const int64_t len = (int64_t)c->seq_bases[(size_t)cr.seq_id].size();
+    // carved regions: reported whole (clipped to the sequence, merged with what earlier windows reported),
+    // applied clipped to the window
+    std::vector<std::pair<int64_t, int64_t>> cut;
+    if (!cr.indel_reads.empty()) {
+        const int64_t R = (int64_t)cr.max_span + 100;
+        while (st.indel_lo < cr.indel_reads.size() && (int64_t)cr.indel_reads[st.indel_lo].second + R < w0) st.indel_lo++;
+        std::vector<std::pair<int64_t, int64_t>> whole;
+        for (size_t k = st.indel_lo; k < cr.indel_reads.size() && (int64_t)cr.indel_reads[k].first - R <= w1; k++) {
+            const int64_t a = std::max<int64_t>(1, cr.indel_reads[k].first - R), b = std::min<int64_t>(len, (int64_t)cr.indel_reads[k].second + R);
+            if (a > b) continue;
+            whole.push_back({a, b});
+            if (std::max(a, w0) <= std::min(b, w1)) cut.push_back({std::max(a, w0), std::min(b, w1)});
+        }
+        std::sort(whole.begin(), whole.end());
+        for (const auto& x : whole) {
+            auto& v = c->carved;
+            if (!v.empty() && v.back().first == cr.seq_id && x.first <= v.back().second.second + 1) {
+                v.back().second.first = std::min(v.back().second.first, x.first);
+                v.back().second.second = std::max(v.back().second.second, x.second);
+            } else {
+                v.push_back({cr.seq_id, {x.first, x.second}});
+            }
+        }
+        std::sort(cut.begin(), cut.end());
+        std::vector<std::pair<int64_t, int64_t>> merged;
+        for (const auto& x : cut) {
+            if (!merged.empty() && x.first <= merged.back().second + 1) merged.back().second = std::max(merged.back().second, x.second);
+            else merged.push_back(x);
+        }
+        cut.swap(merged);
+        // covered positions inside them
+        int64_t inside = 0;
+        size_t r0 = (size_t)lo;
+        for (const auto& cv : cut) {
+            while (r0 < (size_t)hi && (int64_t)cr.first[r0] + cr.max_span < cv.first) r0++;
+            int64_t run = cv.first - 1;
+            for (size_t i = r0; i < (size_t)hi && cr.first[i] <= cv.second; i++) {
+                const int64_t f = std::max<int64_t>(cr.first[i], cv.first), l = std::min<int64_t>(cr.last[i], cv.second);
+                if (l < f || l <= run) continue;
+                inside += l - std::max(f, run + 1) + 1;
+                run = l;
+            }
+        }
+        st.carved_inside += inside;
+        c->stats.carved_positions += inside;
+    }
+    if (hi <= lo) return;                       // no read reaches the window: nothing to call
+    auto j = std::make_unique<WindowJob>();
+    j->seq_id = cr.seq_id;
+    j->w0 = w0;
+    j->w1 = w1;
+    j->max_span = max_span;
+    j->carved.swap(cut);
+    const int32_t pad = ((max_span + 63) / 64) * 64;
+    const int64_t goff = pad - w0;              // window position p -> global p + goff
+    j->reads.resize((size_t)(hi - lo));
+    SRead* out = j->reads.data();
+    parallel_for(hi - lo, 1 << 16, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; i++) {
+            const size_t k = (size_t)(lo + i);
+            out[i] = SRead{(int32_t)(cr.first[k] + goff), (int32_t)(cr.last[k] + goff), cr.bptr[k], cr.neg[k]};
+        }
+    });
+    WindowJob* jp = j.get();
+    j->th = std::thread(run_window_job, c, jp);
+    st.job = std::move(j);
+    st.windows++;
+}
+
+// mid-stream (after a batch): the windows that are complete, while the worker keeps up; final (end of the
+// sequence): every remaining window, then the last one is joined
+static int stream_advance(ngsep_ctx* c, bool final) {
+    auto& st = c->stream;
+    ContigReads& cr = c->contig;
+    if (cr.seq_id < 0 || cr.first.empty()) return final ? stream_collect(c) : NGSEP_OK;
+    const int64_t len = (int64_t)c->seq_bases[(size_t)cr.seq_id].size();
+    int64_t lo = std::max<int64_t>(1, cr.first.front()), hi = std::min<int64_t>(len, cr.cov_last);
+    if (c->params.query_seq[0]) { lo = std::max<int64_t>(lo, c->params.query_first); hi = std::min<int64_t>(hi, c->params.query_last); }
+    if (st.next_w0 == 0) st.next_w0 = lo;
+    const int64_t WL = stream_window_len(c);
+    const int64_t R = (int64_t)cr.max_span + 100;
+    const int64_t limit = final ? hi : std::min<int64_t>(hi, (int64_t)c->last_start - 1 - 2 * R);
+    while (st.next_w0 <= limit) {
+        const int64_t w1 = std::min<int64_t>(st.next_w0 + WL - 1, limit);
+        if (!final && w1 - st.next_w0 + 1 < WL) break;          // mid-stream: whole windows only
+        if (st.job) {
+            if (!final && !st.job->done.load()) break;           // the worker is busy: after the next batch
+            const int rc = stream_collect(c);
+            if (rc != NGSEP_OK) return rc;
+        }
+        const int64_t w0 = st.next_w0;
+        st.next_w0 = w1 + 1;
+        stream_launch(c, w0, w1);
+    }
+    if (final) return stream_collect(c);
+    if (st.job && st.job->done.load()) return stream_collect(c);
+    return NGSEP_OK;
+}
+
 // the open same-start group outlives the caller's batch: its reads' bytes move to the carry store
 static void carry_open_group(ngsep_ctx* c) {
+    if (c->ss_one >= 0) {
+        c->ss_primary.push_back(batch_view(c->cur_batch, c->ss_one));
+        c->ss_one = -1;
+    }
     if (c->ss_primary.empty() && c->ss_secondary.empty()) return;
     CarryStore& cs = c->carry[c->carry_cur ^ 1];
     size_t nc = 0, nb = 0;
@@ -436,57 +735,65 @@ static void carry_open_group(ngsep_ctx* c) {
             r.cigar = cs.cigar.data() + co;
             if (r.chars) r.chars = cs.chars.data() + so;
             if (r.quals) r.quals = cs.quals.data() + so;
+            r.bidx = -1;
         }
     c->carry_cur ^= 1;
 }
 
-static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b) {
+static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed) {
     if (!b || b->n_reads < 0) return set_error(c, NGSEP_E_INVALID, "null batch");
     const int nseq = (int)c->seq_names.size();
     int rc = NGSEP_OK;
     const auto t0 = std::chrono::steady_clock::now();
-    {   // the batch's admitted reads land in these: one growth per batch
+    {   // the batch's admitted reads land in these: at most one (geometric) growth per batch
         ContigReads& cr = c->contig;
         const size_t k = (size_t)b->n_reads;
-        c->to_project.reserve(c->to_project.size() + k);
-        cr.first.reserve(cr.first.size() + k);
-        cr.last.reserve(cr.last.size() + k);
-        if (c->params.coverage_stats) cr.uniq.reserve(cr.uniq.size() + k);
-        else cr.neg.reserve(cr.neg.size() + k);
+        auto grow = [k](auto& v) { if (v.capacity() < v.size() + k) v.reserve(std::max(v.size() + k, 2 * v.capacity())); };
+        grow(c->to_project);
+        grow(cr.first);
+        grow(cr.last);
+        if (c->params.coverage_stats) grow(cr.uniq);
+        else grow(cr.neg);
+        grow(cr.bptr);
     }
+    // the alignments' reference ends, indel bases and read lengths from their CIGARs (all threads)
+    thread_local std::vector<int32_t> lastv, indelv, rlenv;
+    if (lastv.size() < (size_t)b->n_reads) {
+        lastv.resize((size_t)b->n_reads);
+        indelv.resize((size_t)b->n_reads);
+        rlenv.resize((size_t)b->n_reads);
+    }
+    int32_t* lastp = lastv.data();       // (the workers see their own thread_local instances)
+    int32_t* indelp = indelv.data();
+    int32_t* rlenp = rlenv.data();
+    parallel_for(b->n_reads, 1 << 15, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; i++) {
+            const int32_t* cg = b->cigar + b->cigar_off[i];
+            int32_t last = b->first[i] - 1, read_length = 0, indel_len = 0;
+            for (int32_t k = 0; k < b->cigar_n[i]; k++) {
+                const int32_t v = cg[k], op = v & 7;
+                if (op == 1 || op == 2) indel_len += v / 8;
+                if (v & 1) last += v / 8;
+                if (v & 2) read_length += v / 8;
+            }
+            lastp[i] = last;
+            indelp[i] = indel_len;
+            rlenp[i] = read_length;
+        }
+    });
+    c->cur_batch = BatchRef{b, lastp, indelp, packed};
+    int64_t n_in = 0;
     for (int64_t i = 0; i < b->n_reads; i++) {
         if (c->query_done) break;
-        c->stats.alignments_in++;
-        ReadView r;
-        r.seq_id = b->seq_id[i];
-        r.first = b->first[i];
-        r.flags = b->flags[i];
-        r.rg = b->read_group ? b->read_group[i] : -1;
+        n_in++;
+        struct { int32_t seq_id, first, flags; } r{b->seq_id[i], b->first[i], b->flags[i]};
         if (r.seq_id < 0 || r.seq_id >= nseq) {
             rc = set_error(c, NGSEP_E_INVALID, "alignment on unknown sequence id " + std::to_string(r.seq_id));
             break;
         }
-        r.cigar = b->cigar + b->cigar_off[i];
-        r.n_cigar = b->cigar_n[i];
-        int32_t last = r.first - 1, read_length = 0, indel_len = 0;
-        for (int32_t k = 0; k < r.n_cigar; k++) {
-            const int32_t v = r.cigar[k], op = v & 7;
-            if (op == 1 || op == 2) indel_len += v / 8;
-            if (v & 1) last += v / 8;
-            if (v & 2) read_length += v / 8;
-        }
-        r.last = last;
-        r.indel_len = indel_len;
+        const int32_t last = lastp[i], read_length = rlenp[i];
         const int32_t sl = b->seq_len[i];
-        r.len = sl > 0 ? sl : 0;
-        r.chars = nullptr;
-        r.quals = nullptr;
-        if (sl > 0) {
-            r.chars = b->bases + b->seq_off[i];
-            const bool hq = b->quals && (!b->has_quals || b->has_quals[i]);
-            if (hq) r.quals = b->quals + b->seq_off[i];
-            if (read_length != sl) continue;   // ReadAlignment.setReadCharacters throws -> record skipped
-        }
+        if (sl > 0 && read_length != sl) continue;   // ReadAlignment.setReadCharacters throws -> record skipped
         // querySeq handling (AlignmentsPileupGenerator.java:342-354)
         if (c->params.query_seq[0]) {
             if (c->seq_names[r.seq_id] == c->params.query_seq) {
@@ -519,17 +826,26 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b) {
             c->cur_seq = r.seq_id;
             c->contig.clear();
             c->contig.seq_id = r.seq_id;
+            c->contig.seq_len = (int64_t)c->seq_bases[(size_t)r.seq_id].size();
             c->cur_last = last;
         }
         if (last > c->cur_last) c->cur_last = last;
-        if (r.flags & 0x100) c->ss_secondary.push_back(r);
-        else c->ss_primary.push_back(r);
+        // the open same-start group: a lone primary alignment stays an index (no view is built)
+        if (!(r.flags & 0x100) && c->ss_one < 0 && c->ss_primary.empty() && c->ss_secondary.empty()) {
+            c->ss_one = (int32_t)i;
+        } else {
+            if (c->ss_one >= 0) { c->ss_primary.push_back(batch_view(c->cur_batch, c->ss_one)); c->ss_one = -1; }
+            if (r.flags & 0x100) c->ss_secondary.push_back(batch_view(c->cur_batch, (int32_t)i));
+            else c->ss_primary.push_back(batch_view(c->cur_batch, (int32_t)i));
+        }
         c->last_start = r.first;
     }
+    c->stats.alignments_in += n_in;
     // the admitted reads' bytes are projected while the batch is alive; the open group is carried
     static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     const auto t1 = std::chrono::steady_clock::now();
     project_pending(c);
+    if (rc == NGSEP_OK && streaming(c)) rc = stream_advance(c, false);
     carry_open_group(c);
     if (host_timing)
         std::fprintf(stderr, "[ngsep host] batch of %lld: admission %.1f ms, projection %.1f ms\n", (long long)b->n_reads,
@@ -563,6 +879,19 @@ static inline uint8_t ref_code(const ngsep_ctx* c, char ch) {
     int a = dna_index((char)std::toupper((unsigned char)ch));                                      // :199
     if (a < 0) return kRefInWindow;    // VariantDiscoverySNVQAlgorithm.java:104-107 (N reference)
     return (uint8_t)(kRefCallable | (a << 5));
+}
+
+// reference codes of window w in global coordinates; carved indel regions get no code (no call is made there)
+static void fill_ref_codes(const ngsep_ctx* c, Staged& s, const Window& w, const std::vector<std::pair<int64_t, int64_t>>& carved) {
+    const std::string& ref = c->seq_bases[w.seq_id];
+    uint8_t* dst = &s.h_ref[(size_t)(w.gbase + w.pad)];
+    parallel_for(w.wlen, 1 << 20, [&](int64_t lo, int64_t hi) {
+        for (int64_t k = lo; k < hi; k++) dst[k] = ref_code(c, ref[(size_t)(w.w0 - 1 + k)]);
+    });
+    for (const auto& cv : carved) {
+        const int64_t a = std::max<int64_t>(cv.first, w.w0), b = std::min<int64_t>(cv.second, (int64_t)w.w0 + w.wlen - 1);
+        if (a <= b) std::memset(dst + (a - w.w0), 0, (size_t)(b - a + 1));
+    }
 }
 
 // ---- tile-blocked pileup (engine.hpp TileInfo) ----
@@ -626,13 +955,21 @@ static int choose_tile(const std::vector<int32_t>& m16, int64_t g_len, std::vect
 //   * the position-major byte pile (KP): position p's rows_t codes at off_t + p * rows_t, rank order;
 //   * the strand bits (KP, countsStrand): bit off_t + p * rows_t + r = the rank-r read is reverse.
 // Tiles are independent: built on all host threads.
-static int build_single_layout(Staged& s, const std::vector<SRead>& reads) {
+static int build_single_layout(Staged& s, const std::vector<SRead>& reads, LayoutArena& arena, bool exact) {
+    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    auto lap = [t = std::chrono::steady_clock::now()](const char* what) mutable {
+        if (!host_timing) return;
+        const auto n = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[ngsep host]   layout %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    };
     const int64_t g_len = s.g_len, nreads = (int64_t)reads.size();
     std::vector<int32_t> R2((size_t)nreads * 2);
     for (int64_t i = 0; i < nreads; i++) { R2[(size_t)(2 * i)] = reads[(size_t)i].gfirst; R2[(size_t)(2 * i + 1)] = reads[(size_t)i].glast; }
     std::vector<int32_t> rows;
     const int T = choose_tile(depth_max16(R2.data(), nreads, 2, g_len), g_len, rows);
     std::vector<int32_t>().swap(R2);
+    lap("depth + tile choice");
     const int64_t ntiles = g_len / T;
     s.tile = T;
     s.n_tiles = ntiles;
@@ -653,9 +990,11 @@ static int build_single_layout(Staged& s, const std::vector<SRead>& reads) {
         const int64_t lo_pos = t * T - s.max_span;
         return std::lower_bound(reads.begin(), reads.end(), lo_pos, [](const SRead& r, int64_t v) { return (int64_t)r.gfirst <= v; }) - reads.begin();
     };
-    s.h_cpile.alloc((size_t)off);
-    s.h_planes.alloc((size_t)(off / 16));
-    s.h_cneg.alloc((size_t)(off / 32));
+    if (!arena.ensure(off, exact)) return -2;
+    s.h_cpile = arena.cpile;
+    s.h_planes = arena.planes;
+    s.h_cneg = arena.cneg;
+    lap("tile table + alloc");
     const int W = T / 32;
     const uint8_t* ref = s.h_ref.data();
     std::atomic<int> bad{0};
@@ -668,9 +1007,9 @@ static int build_single_layout(Staged& s, const std::vector<SRead>& reads) {
             while (r_lo < nreads && (int64_t)reads[(size_t)r_lo].gfirst <= (int64_t)tstart - s.max_span) r_lo++;
             if (!nrow) continue;
             const int64_t toff = s.h_tinfo[(size_t)t].off;
-            uint8_t* col = s.h_cpile.p + toff;
-            uint32_t* pl = s.h_planes.p + toff / 16;
-            uint32_t* ng = s.h_cneg.p + toff / 32;
+            uint8_t* col = s.h_cpile + toff;
+            uint32_t* pl = s.h_planes + toff / 16;
+            uint32_t* ng = s.h_cneg + toff / 32;
             std::memset(col, 0, (size_t)nrow * T);
             std::memset(pl, 0, (size_t)nrow * T / 4);
             std::memset(ng, 0, (size_t)nrow * T / 8);
@@ -698,7 +1037,30 @@ static int build_single_layout(Staged& s, const std::vector<SRead>& reads) {
             }
         }
     });
+    lap("tiles");
     return bad ? -1 : 0;
+}
+
+bool LayoutArena::ensure(int64_t pile_bytes, bool exact) {
+    if (cpile && pile_bytes <= cap) return true;
+    release();
+    int64_t want = exact ? pile_bytes : pile_bytes + pile_bytes / 4;
+    want = (std::max<int64_t>(want, 1 << 16) + 4095) / 4096 * 4096;
+    cpile = static_cast<uint8_t*>(pinned_alloc((size_t)want));
+    planes = static_cast<uint32_t*>(pinned_alloc((size_t)want / 4));
+    cneg = static_cast<uint32_t*>(pinned_alloc((size_t)want / 8));
+    if (!cpile || !planes || !cneg) { release(); return false; }
+    cap = want;
+    return true;
+}
+void LayoutArena::release() {
+    pinned_free(cpile);
+    pinned_free(planes);
+    pinned_free(cneg);
+    cpile = nullptr;
+    planes = nullptr;
+    cneg = nullptr;
+    cap = 0;
 }
 
 // Multisample layout: the same tiles of T positions, one block per (tile, sample) holding that
@@ -929,17 +1291,12 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     // reference codes in global coordinates; carved indel regions get no code (no call is made there)
     s.h_ref.assign((size_t)s.g_len, 0);
     for (size_t wi = 0; wi < s.windows.size(); wi++) {
-        const Window& w = s.windows[wi];
-        const std::string& ref = c->seq_bases[w.seq_id];
-        uint8_t* dst = &s.h_ref[(size_t)(w.gbase + w.pad)];
-        parallel_for(w.wlen, 1 << 20, [&](int64_t lo, int64_t hi) {
-            for (int64_t k = lo; k < hi; k++) dst[k] = ref_code(c, ref[(size_t)(w.w0 - 1 + k)]);
-        });
-        for (const auto& cv : contigs[wr[wi].contig].carved) {
-            const int64_t a = std::max<int64_t>(cv.first, w.w0), b = std::min<int64_t>(cv.second, (int64_t)w.w0 + w.wlen - 1);
-            if (a <= b) std::memset(dst + (a - w.w0), 0, (size_t)(b - a + 1));
-        }
+        const auto& cv = contigs[wr[wi].contig].carved;
+        fill_ref_codes(c, s, s.windows[wi], std::vector<std::pair<int64_t, int64_t>>(cv.begin(), cv.end()));
     }
+    if (host_timing)
+        std::fprintf(stderr, "[ngsep host]   layout windows + reference codes %.1f ms\n",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count());
     if (!c->params.multisample) {
         // single sample: the reads' projected bytes go straight into the tile layout
         s.single = true;
@@ -960,8 +1317,9 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
         }
         s.n_reads = nreads;
         s.n_read_bases = nbases;
-        if (build_single_layout(s, reads) != 0)
-            return set_error(c, NGSEP_E_INVALID, "internal error: pileup depth above the tile's row count");
+        const int lr = build_single_layout(s, reads, c->arena, true);
+        if (lr == -2) return set_error(c, NGSEP_E_DEVICE, "pinned host memory for the layout could not be allocated");
+        if (lr != 0) return set_error(c, NGSEP_E_INVALID, "internal error: pileup depth above the tile's row count");
         c->stats.slot_bytes = 0;
         c->stats.slot_size = 0;
     } else {
@@ -1045,10 +1403,74 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     std::vector<int32_t>().swap(s.h_bseg);
     std::vector<int32_t>().swap(s.h_blb);
     std::vector<int32_t>().swap(s.h_bbase);
-    s.h_planes.release();
-    s.h_cpile.release();
-    s.h_cneg.release();
+    // one-shot runs give the pinned layout buffers back (streamed windows keep theirs)
+    s.h_planes = nullptr;
+    s.h_cpile = nullptr;
+    s.h_cneg = nullptr;
+    c->arena.release();
     return NGSEP_OK;
+}
+
+// one streamed window (worker thread; the context's staged run, device and layout buffers are its own
+// until stream_collect joins it): reference codes, layout, upload, kernels, records into j->sites
+static void run_window_job(ngsep_ctx* c, WindowJob* j) {
+    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    const auto h0 = std::chrono::steady_clock::now();
+    Staged& s = c->staged;
+    s = Staged();
+    const int32_t pad = ((j->max_span + 63) / 64) * 64;
+    Window w;
+    w.seq_id = j->seq_id;
+    w.w0 = (int32_t)j->w0;
+    w.wlen = (int32_t)(j->w1 - j->w0 + 1);
+    w.gbase = 0;
+    w.pad = pad;
+    w.read_begin = 0;
+    w.read_end = (int64_t)j->reads.size();
+    s.windows.push_back(w);
+    s.max_span = j->max_span;
+    s.g_len = (((int64_t)w.wlen + 2 * pad + 64 + kTileMaxPos - 1) / kTileMaxPos) * kTileMaxPos;
+    s.covered = w.wlen;                 // (the dump mode's record capacity)
+    s.h_ref.assign((size_t)s.g_len, 0);
+    fill_ref_codes(c, s, w, j->carved);
+    s.single = true;
+    s.n_reads = (int64_t)j->reads.size();
+    int64_t nb = 0;
+    for (const SRead& r : j->reads) nb += r.glast >= r.gfirst ? (int64_t)r.glast - r.gfirst + 1 : 0;
+    s.n_read_bases = nb;
+    const int lr = build_single_layout(s, j->reads, c->arena, false);
+    if (lr != 0) {
+        j->rc = lr == -2 ? NGSEP_E_DEVICE : NGSEP_E_INVALID;
+        j->err = lr == -2 ? "pinned host memory for the layout could not be allocated" : "internal error: pileup depth above the tile's row count";
+        j->done = true;
+        return;
+    }
+    const auto h1 = std::chrono::steady_clock::now();
+    std::string err;
+    if (!c->dev) c->dev = device_create(c->device, err);
+    if (!c->dev || device_upload(c->dev, s, err) != 0) {
+        j->rc = NGSEP_E_DEVICE;
+        j->err = err;
+        j->done = true;
+        return;
+    }
+    const auto h2 = std::chrono::steady_clock::now();
+    c->stats.read_bases += nb;
+    c->stats.pile_bytes = s.pile_bytes;
+    c->stats.tile_positions = s.tile;
+    c->stats.tile_rows_max = std::max(c->stats.tile_rows_max, s.tile_rows_max);
+    c->stats.global_positions += s.g_len;
+    c->stats.n_tiles += s.n_tiles;
+    c->stats.layout_ms += std::chrono::duration<double, std::milli>(h1 - h0).count();
+    c->stats.upload_ms += std::chrono::duration<double, std::milli>(h2 - h1).count();
+    j->rc = run_device_into(c, j->sites, nullptr);
+    if (j->rc != NGSEP_OK) j->err = c->err;
+    if (host_timing)
+        std::fprintf(stderr, "[ngsep host] window %d:%lld-%lld: layout %.1f ms, upload %.1f ms, run %.1f ms (%lld reads)\n", j->seq_id,
+                     (long long)j->w0, (long long)j->w1, std::chrono::duration<double, std::milli>(h1 - h0).count(),
+                     std::chrono::duration<double, std::milli>(h2 - h1).count(),
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h2).count(), (long long)s.n_reads);
+    j->done = true;
 }
 
 // java.lang.Math.round + PhredScoreHelper.calculatePhredScore (math/PhredScoreHelper.java:31-40)
@@ -1155,32 +1577,49 @@ static int finish_run(ngsep_ctx* c, size_t from, int64_t n, double scan_ms, doub
                       int64_t ncand, double* elapsed_ms);
 
 int run_device(ngsep_ctx* c, double* elapsed_ms) {
+    if (c->params.multisample) {
+        LikTables t;
+        GenotypeParams gp;
+        compute_tables(c, &t, &gp);
+        return run_device_multi(c, t, gp, elapsed_ms);
+    }
+    return run_device_into(c, c->sites, elapsed_ms);
+}
+
+static int finish_run_into(ngsep_ctx* c, SiteStore& dest, size_t from, int64_t n, double scan_ms, double geno_ms, double total_ms,
+                           int64_t ncand, double* elapsed_ms);
+
+// single sample: the staged run's records appended to dest
+int run_device_into(ngsep_ctx* c, SiteStore& dest, double* elapsed_ms) {
     LikTables t;
     GenotypeParams gp;
     compute_tables(c, &t, &gp);
-    if (c->params.multisample) return run_device_multi(c, t, gp, elapsed_ms);
     int64_t n = 0;
     double scan_ms = 0, geno_ms = 0, total_ms = 0;
     int64_t ncand = 0;
     std::string err;
     // exact pruning is proven for h <= 0.1 ("why pruning is exact")
     int prune = c->params.prune_candidates && !c->params.dump_all_positions && c->het_rate <= 0.1;
-    const size_t from = c->sites.size();
-    if (device_run(c->dev, c->staged, t, gp, prune, &c->sites, &n, &scan_ms, &geno_ms, &total_ms, &ncand, err) != 0)
+    const size_t from = dest.size();
+    if (device_run(c->dev, c->staged, t, gp, prune, &dest, &n, &scan_ms, &geno_ms, &total_ms, &ncand, err) != 0)
         return set_error(c, NGSEP_E_DEVICE, err);
-    return finish_run(c, from, n, scan_ms, geno_ms, total_ms, ncand, elapsed_ms);
+    return finish_run_into(c, dest, from, n, scan_ms, geno_ms, total_ms, ncand, elapsed_ms);
 }
 
 // records arrive sorted by global position with their (sequence, position) set by KO; windows are
 // laid out in processing order, so this is (sequence order, position).
 static int finish_run(ngsep_ctx* c, size_t from, int64_t n, double scan_ms, double geno_ms, double total_ms,
                       int64_t ncand, double* elapsed_ms) {
-    c->sites.n = from + (size_t)n;
-    if (c->params.calc_strand_bias) apply_strand_bias(c->sites, from);
+    return finish_run_into(c, c->sites, from, n, scan_ms, geno_ms, total_ms, ncand, elapsed_ms);
+}
+static int finish_run_into(ngsep_ctx* c, SiteStore& dest, size_t from, int64_t n, double scan_ms, double geno_ms, double total_ms,
+                           int64_t ncand, double* elapsed_ms) {
+    dest.n = from + (size_t)n;
+    if (c->params.calc_strand_bias) apply_strand_bias(dest, from);
     c->stats.candidates = ncand;
     c->stats.hard_sites = (int32_t)device_last_hard(c->dev);
     c->stats.exact_bound_passes = device_last_exact(c->dev);
-    c->stats.sites_called += (int64_t)(c->sites.size() - from);
+    c->stats.sites_called += (int64_t)(dest.size() - from);
     c->stats.kernel_ms = total_ms;
     c->stats.scan_ms = scan_ms;
     c->stats.genotype_ms = geno_ms;
@@ -1331,6 +1770,9 @@ extern "C" int ngsep_open(int device, const ngsep_params* params, ngsep_ctx** ou
 
 extern "C" int ngsep_close(ngsep_ctx* c) {
     if (!c) return NGSEP_E_INVALID;
+    if (c->stream.job && c->stream.job->th.joinable()) c->stream.job->th.join();
+    c->stream.job.reset();
+    c->arena.release();
     if (c->dev) device_destroy(c->dev);
     if (c->cov_dev) cov_destroy(c->cov_dev);
     delete c;
@@ -1370,8 +1812,16 @@ extern "C" const char* ngsep_sequence_name(ngsep_ctx* c, int i) {
 extern "C" int ngsep_process_alignments(ngsep_ctx* c, const ngsep_read_batch* b) {
     if (!c) return NGSEP_E_INVALID;
     c->staging_mode = false;
-    return process_batch(c, b);
+    return process_batch(c, b, false);
 }
+
+namespace ngsep {
+int process_alignments_packed(ngsep_ctx* c, const ngsep_read_batch* b) {
+    if (!c) return NGSEP_E_INVALID;
+    c->staging_mode = false;
+    return process_batch(c, b, true);
+}
+}  // namespace ngsep
 
 extern "C" int ngsep_notify_end(ngsep_ctx* c) {
     if (!c) return NGSEP_E_INVALID;
@@ -1465,7 +1915,7 @@ extern "C" int ngsep_clear_carved_regions(ngsep_ctx* c) {
 extern "C" int ngsep_stage_alignments(ngsep_ctx* c, const ngsep_read_batch* b) {
     if (!c) return NGSEP_E_INVALID;
     c->staging_mode = true;
-    return process_batch(c, b);
+    return process_batch(c, b, false);
 }
 
 extern "C" int ngsep_stage_finish(ngsep_ctx* c) {

@@ -10,6 +10,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -126,6 +127,7 @@ struct HostArray {
 // Admitted reads of one sequence in pending order (AlignmentsPileupGenerator.pendingAlignments)
 struct ContigReads {
     int32_t seq_id = -1;
+    int64_t seq_len = 0;               // the sequence's length
     std::vector<int32_t> first, last;
     std::vector<uint8_t> neg;          // 1 = negative strand
     std::vector<uint8_t> uniq;         // coverage mode: 1 = ReadAlignment.isUnique (no FLAG_MULTIPLE_ALN)
@@ -137,12 +139,14 @@ struct ContigReads {
     // into `carved` when the sequence is staged (engine.cpp carve_indel_regions)
     std::vector<std::pair<int32_t, int32_t>> indel_reads;
     std::vector<std::pair<int32_t, int32_t>> carved;
+    std::vector<size_t> chunk_end;     // reads [chunk_end[k-1], chunk_end[k]) have their bytes in chunks[k]
+    std::vector<int32_t> chunk_maxlast;   // their largest last position (streamed windows release the chunk after)
     int32_t max_span = 0;
     int64_t covered = 0;               // union of [first,last] (positions with a pileup)
     int32_t cov_last = 0;              // running max of last (for `covered`)
     void clear() {
         first.clear(); last.clear(); neg.clear(); uniq.clear(); sample.clear(); rank.clear(); bptr.clear(); chunks.clear();
-        indel_reads.clear(); carved.clear();
+        indel_reads.clear(); carved.clear(); chunk_end.clear(); chunk_maxlast.clear();
         max_span = 0; covered = 0; cov_last = 0; seq_id = -1;
     }
 };
@@ -157,6 +161,16 @@ struct ReadView {
     const char* quals;     // nullptr = no qualities ('*')
     int32_t len;
     int32_t indel_len;     // bases in the CIGAR's I/D items (0: SNV-only alignment)
+    bool packed;           // BAM encoding (ngsep_call_bam's reader): chars = 4-bit bases, 2 per byte (high nibble
+                           // first, "=ACMGRSVTWYHKDBN"), quals = raw Phred values (no +33)
+    int32_t bidx;          // index in the batch being processed (-1: a carried read, in the carry store)
+};
+// the batch being admitted (engine.cpp process_batch): its reads are referenced by index until projected
+struct BatchRef {
+    const ngsep_read_batch* b = nullptr;
+    const int32_t* last = nullptr;      // per read: reference end, indel bases (from the CIGAR)
+    const int32_t* indel = nullptr;
+    bool packed = false;
 };
 struct CarryStore {        // owned copies of the open same-start group's reads
     std::vector<int32_t> cigar;
@@ -260,11 +274,39 @@ struct Staged {            // everything resident for one run
     int64_t nblk_b = 0;
     std::vector<uint8_t> h_ref;
     // single-sample layout (engine.cpp build_single_layout): bit planes, position-major byte pile in
-    // pending-list rank order, strand bits of its cells
-    HostArray<uint32_t> h_planes;
-    HostArray<uint8_t> h_cpile;
-    HostArray<uint32_t> h_cneg;
+    // pending-list rank order, strand bits of its cells -- in the context's pinned LayoutArena
+    uint32_t* h_planes = nullptr;
+    uint8_t* h_cpile = nullptr;
+    uint32_t* h_cneg = nullptr;
     bool single = false;                // the single-sample layout (else the multisample one)
+};
+
+// Pinned host buffers of the single-sample layout, reused run after run (streamed windows: no page faults,
+// DMA-speed uploads).  Grown geometrically; sized by the pile bytes (planes = pile / 4, strand bits = / 8).
+struct LayoutArena {
+    uint8_t* cpile = nullptr;
+    uint32_t* planes = nullptr;
+    uint32_t* cneg = nullptr;
+    int64_t cap = 0;
+    bool ensure(int64_t pile_bytes, bool exact);
+    void release();
+    ~LayoutArena() { release(); }
+};
+
+// One streamed window of a sequence (single-sample calls while the alignments are still being read,
+// engine.cpp stream_advance): its reads in window coordinates and the carved indel regions inside it,
+// laid out, uploaded and run on the context's worker thread; its records come back in `sites`.
+struct WindowJob {
+    int32_t seq_id = -1;
+    int64_t w0 = 0, w1 = 0;
+    int32_t max_span = 1;
+    std::vector<SRead> reads;                               // global coordinates (window at pad)
+    std::vector<std::pair<int64_t, int64_t>> carved;        // 1-based, inside [w0, w1]
+    SiteStore sites;
+    int rc = 0;
+    std::string err;
+    std::atomic<bool> done{false};
+    std::thread th;
 };
 
 }  // namespace ngsep
@@ -290,7 +332,13 @@ struct ngsep_ctx {
     std::vector<ngsep::ReadView> ss_primary, ss_secondary;   // the open same-start group
     ngsep::CarryStore carry[2];                               // its reads' bytes across batches
     int carry_cur = 0;
-    std::vector<ngsep::ReadView> to_project;                 // admitted, projection pending (batch end)
+    // admitted reads whose projection is pending (batch end): >= 0 an index in the current batch,
+    // < 0 entry -1 - k of to_project_carried
+    std::vector<int32_t> to_project;
+    std::vector<ngsep::ReadView> to_project_carried;
+    ngsep::BatchRef cur_batch;
+    int32_t ss_one = -1;                                     // the open group's only read, by batch index (or -1)
+    std::vector<ngsep::HostArray<uint8_t>> chunk_pool;       // released projection chunks, reused
     ngsep::ContigReads contig;
     bool query_found = false;
     bool query_done = false;
@@ -298,6 +346,16 @@ struct ngsep_ctx {
     // windows collected for a staged run
     std::vector<ngsep::ContigReads> staged_contigs;
     ngsep::Staged staged;
+    ngsep::LayoutArena arena;
+    // streamed single-sample windows of the current sequence (run_now paths)
+    struct {
+        int64_t next_w0 = 0;                      // first position not yet handed to a window (0: not started)
+        size_t indel_lo = 0;                      // indel reads before this index reach no later window
+        size_t chunk_lo = 0;                      // projected chunks before this index are released
+        int64_t carved_inside = 0;                // covered positions inside carved regions (this sequence)
+        std::unique_ptr<ngsep::WindowJob> job;    // in flight on its own thread
+        int64_t windows = 0;                      // windows run (diagnostics)
+    } stream;
     ngsep::Device* dev = nullptr;
     // CoverageStatisticsCalculator mode (params.coverage_stats)
     ngsep::CovDevice* cov_dev = nullptr;
@@ -321,9 +379,12 @@ struct ngsep_ctx {
 namespace ngsep {
 // engine.cpp
 int set_error(ngsep_ctx* c, int code, const std::string& msg);
+// ngsep_process_alignments for a batch in BAM encoding (ReadView::packed; bam.cpp's call_bam)
+int process_alignments_packed(ngsep_ctx* c, const ngsep_read_batch* b);
 void project_read(const ngsep_ctx* c, const ReadView& r, uint8_t* out);
 int stage_contig_reads(ngsep_ctx* c, ContigReads& cr, bool run_now);
 int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs);
+int run_device_into(ngsep_ctx* c, SiteStore& dest, double* elapsed_ms);
 int run_device(ngsep_ctx* c, double* elapsed_ms);
 void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g);
 // kernels.hip

@@ -85,6 +85,8 @@ struct Device {
     uint32_t* d_planes = nullptr;    // single sample: bit planes of the pile (KT)
     uint32_t* d_cneg = nullptr;      // single sample: strand bits of the pile's cells (KP)
     int4* d_wins = nullptr;          // windows {global start of w0, w0, seq_id, wlen}, ascending (KO maps records)
+    // single-sample buffers are kept from run to run (streamed windows) and grown when a run needs more
+    size_t cap_pile = 0, cap_planes = 0, cap_cneg = 0, cap_ref = 0, cap_tinfo = 0, cap_wins = 0;
     int32_t n_wins = 0;
     int32_t planes_W = 0;            // words per plane row (T / 32)
     int4* d_reads = nullptr;
@@ -585,7 +587,7 @@ void k_tile_planes(const uint32_t* __restrict__ planes, const uint8_t* __restric
         cur = nt;
         if (rows == 0) continue;
         const int ng = (rows + 63) >> 6;
-        const bool bound = gp.use_bound && rows <= 255;   // 32-bit halves of the exact sums cannot overflow
+        const bool bound = gp.use_bound && rows <= 255 && !(gp.ablate & 256);   // (diagnostics: 256 = loads only) 32-bit halves of the exact sums cannot overflow
         // counts (bit-sliced, 8 bits: rows <= 255) or, without the bound, the OR of the other-allele plane
         uint32_t cv[8], ca[8], hits = 0;
 #pragma unroll
@@ -1540,6 +1542,20 @@ void device_release(Device* d) {
     (void)hipFree(d->d_bbase); d->d_bbase = nullptr;
     d->n_samples = 0;
     d->n_units = d->n_slots = d->n_reads = d->g_len = d->n_tiles = 0;
+    d->cap_pile = d->cap_planes = d->cap_cneg = d->cap_ref = d->cap_tinfo = d->cap_wins = 0;
+}
+
+// a device buffer of at least `bytes` (kept when it is large enough; grown by a quarter otherwise)
+template <class T>
+static int ensure_dev(T** p, size_t* cap, size_t bytes, bool slack, std::string& err) {
+    if (*p && *cap >= bytes) return 0;
+    (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    const size_t want = slack ? bytes + bytes / 4 : bytes;
+    HIP_TRY(hipMalloc(p, want));
+    *cap = want;
+    return 0;
 }
 
 void device_destroy(Device* d) {
@@ -1571,24 +1587,30 @@ void device_destroy(Device* d) {
 
 int device_upload(Device* d, const Staged& s, std::string& err) {
     HIP_TRY(hipSetDevice(d->ordinal));
-    device_release(d);
     const int32_t pad = s.windows.empty() ? 64 : s.windows[0].pad;
-    HIP_TRY(hipMalloc(&d->d_pile, (size_t)s.pile_bytes + 64));     // + 64: KP loads whole dwords of a column
-    HIP_TRY(hipMalloc(&d->d_tinfo, (size_t)std::max<int64_t>(s.n_tiles, 1) * sizeof(TileInfo)));
-    HIP_TRY(hipMalloc(&d->d_ref, (size_t)s.g_len + 64));
+    // single sample (a streamed window or a whole run): buffers kept across runs while large enough; the
+    // multisample run starts from nothing
+    const bool keep = s.single && d->d_slots == nullptr && d->d_reads == nullptr;
+    if (!keep) device_release(d);
+    else HIP_TRY(hipDeviceSynchronize());          // the previous run is done reading them
+    if (ensure_dev(&d->d_pile, &d->cap_pile, (size_t)s.pile_bytes + 64, keep, err) ||      // + 64: KP loads whole dwords of a column
+        ensure_dev(&d->d_tinfo, &d->cap_tinfo, (size_t)std::max<int64_t>(s.n_tiles, 1) * sizeof(TileInfo), keep, err) ||
+        ensure_dev(&d->d_ref, &d->cap_ref, (size_t)s.g_len + 64, keep, err))
+        return -1;
     if (s.n_tiles && !s.h_tinfo.empty()) HIP_TRY(hipMemcpyAsync(d->d_tinfo, s.h_tinfo.data(), (size_t)s.n_tiles * sizeof(TileInfo), hipMemcpyHostToDevice, d->stream));
-    HIP_TRY(hipMemsetAsync(d->d_ref, 0, (size_t)s.g_len + 64, d->stream));
+    HIP_TRY(hipMemsetAsync(d->d_ref + s.g_len, 0, 64, d->stream));
     HIP_TRY(hipMemcpyAsync(d->d_ref, s.h_ref.data(), (size_t)s.g_len, hipMemcpyHostToDevice, d->stream));
     if (s.single) {
         // single sample: planes (KT), the position-major pile and its strand bits (KP)
         const size_t ncw = (size_t)(s.pile_bytes / 32);
-        HIP_TRY(hipMalloc(&d->d_planes, (size_t)std::max<int64_t>(s.pile_bytes / 4, 16)));
-        HIP_TRY(hipMalloc(&d->d_cneg, (ncw + 2) * sizeof(uint32_t)));    // + 2: KP reads word pairs
-        HIP_TRY(hipMemsetAsync(d->d_cneg, 0, (ncw + 2) * sizeof(uint32_t), d->stream));
+        if (ensure_dev(&d->d_planes, &d->cap_planes, (size_t)std::max<int64_t>(s.pile_bytes / 4, 16), keep, err) ||
+            ensure_dev(&d->d_cneg, &d->cap_cneg, (ncw + 2) * sizeof(uint32_t), keep, err))    // + 2: KP reads word pairs
+            return -1;
+        HIP_TRY(hipMemsetAsync(d->d_cneg + ncw, 0, 2 * sizeof(uint32_t), d->stream));
         if (s.pile_bytes) {
-            HIP_TRY(hipMemcpyAsync(d->d_pile, s.h_cpile.p, (size_t)s.pile_bytes, hipMemcpyHostToDevice, d->stream));
-            HIP_TRY(hipMemcpyAsync(d->d_planes, s.h_planes.p, (size_t)(s.pile_bytes / 4), hipMemcpyHostToDevice, d->stream));
-            HIP_TRY(hipMemcpyAsync(d->d_cneg, s.h_cneg.p, ncw * sizeof(uint32_t), hipMemcpyHostToDevice, d->stream));
+            HIP_TRY(hipMemcpyAsync(d->d_pile, s.h_cpile, (size_t)s.pile_bytes, hipMemcpyHostToDevice, d->stream));
+            HIP_TRY(hipMemcpyAsync(d->d_planes, s.h_planes, (size_t)(s.pile_bytes / 4), hipMemcpyHostToDevice, d->stream));
+            HIP_TRY(hipMemcpyAsync(d->d_cneg, s.h_cneg, ncw * sizeof(uint32_t), hipMemcpyHostToDevice, d->stream));
         }
         d->planes_W = s.tile / 32;
     } else {
@@ -1629,7 +1651,7 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
         std::vector<int4> wins;
         for (const Window& w : s.windows) wins.push_back(int4{(int)(w.gbase + w.pad), w.w0, w.seq_id, w.wlen});
         if (wins.empty()) wins.push_back(int4{0, 0, -1, 0});
-        HIP_TRY(hipMalloc(&d->d_wins, wins.size() * sizeof(int4)));
+        if (ensure_dev(&d->d_wins, &d->cap_wins, wins.size() * sizeof(int4), false, err)) return -1;
         HIP_TRY(hipMemcpy(d->d_wins, wins.data(), wins.size() * sizeof(int4), hipMemcpyHostToDevice));
         d->n_wins = (int32_t)wins.size();
     }

@@ -82,21 +82,33 @@ def _outside(vcf, carved):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kw", [dict(depth=25, seed=32, indel_rate=1e-4),
-                                dict(depth=15, seed=33, indel_rate=3e-4, quality_model=2, snv_rate=3e-3)])
-def test_calls_outside_carved_regions_identical(tmp_path, kw):
+@pytest.mark.parametrize("kw,win", [(dict(depth=25, seed=32, indel_rate=1e-4), 0),
+                                    (dict(depth=15, seed=33, indel_rate=3e-4, quality_model=2, snv_rate=3e-3), 0),
+                                    (dict(depth=25, seed=32, indel_rate=1e-4), 40000)])
+def test_calls_outside_carved_regions_identical(tmp_path, kw, win):
+    """win > 0: ngsep_call_bam streams windows of `win` positions while it reads (engine.cpp stream_advance):
+    the carved regions, the calls and the genotyped-position count do not depend on the cut."""
     syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=2, **kw)
     fa, sam, bam = syn.write(os.path.join(str(tmp_path), "ind"))
     syn.close()
     o = os.path.join(str(tmp_path), "o.vcf")
     ost = ngsep_oracle.run_ssvd(fa, sam, o, indel_passthrough=1)
     g = os.path.join(str(tmp_path), "g.vcf")
-    with GpuPileupSession(gpu_params()) as s:
+    p = gpu_params()
+    if win:
+        p.window_positions = win
+    with GpuPileupSession(p) as s:
         s.load_fasta(fa)
         s.processFile(bam, g)
         carved = s.carved_regions()
         st = s.stats()
     assert len(carved) > 2
+    if win:
+        with GpuPileupSession(gpu_params()) as s:
+            s.load_fasta(fa)
+            s.processFile(bam, g + ".whole")
+            assert s.carved_regions() == carved
+        assert open(g).read() == open(g + ".whole").read()
     ro, rg = _outside(o, carved), _outside(g, carved)
     assert rg == [l for l in open(g) if not l.startswith("#")]      # no call inside a carved region
     assert ro == rg and len(rg) > 50
