@@ -325,7 +325,7 @@ def main():
         sources = [pysynth.Synth(genome=pysynth.HUMAN, depth=args.depth, seed=3 + rank, contig_first=HUMAN_CHR20,
                                  n_contigs=1, rng_per_contig=1)]
         workload = "configs[2]: human chr20 (64,444,167 bp) 30x synthetic 150 bp SE"
-        workload_key = f"human_chr20:{args.depth:g}x:seed{3 + rank}:v2"
+        workload_key = f"human_chr20:{args.depth:g}x:seed{3 + rank}:v3"
     else:
         # configs[3]: GRCh38 lengths, sequences assigned largest-first to the least-loaded rank; each rank
         # generates and calls only its own (the synthetic sequences are independent: rng_per_contig)
@@ -444,13 +444,14 @@ def main():
     stats_all = [s.stats() for s in sessions]
     pile_bytes = sum(x.pile_bytes for x in stats_all)
     tile = st.tile_positions
-    # bytes KT moves per launch: the bit planes (rows_t * T / 4 per tile), the reference codes (1 B per
-    # global position, halos included) and the 16-B tile descriptors; the multisample KTM streams its
-    # per-sample byte blocks and the reference codes
+    # bytes KT moves per launch: the valid-call plane (rows_t * T / 8 per tile), the other-allele lists
+    # (2 B per entry, 4 B of range per tile), the reference codes (1 B per global position, halos
+    # included) and the 16-B tile descriptors; the multisample KTM streams its per-sample byte blocks and
+    # the reference codes
     if multi:
         kt_bytes = sum(x.pile_bytes + x.global_positions + 16 * x.n_tiles for x in stats_all)
     else:
-        kt_bytes = sum(x.pile_bytes // 4 + x.global_positions + 16 * x.n_tiles for x in stats_all)
+        kt_bytes = sum(x.pile_bytes // 8 + 2 * x.other_allele_calls + x.global_positions + 20 * x.n_tiles for x in stats_all)
     layout_ms = sum(x.layout_ms for x in stats_all)
     upload_ms = sum(x.upload_ms for x in stats_all)
     for s in sessions:
@@ -488,7 +489,7 @@ def main():
         alg_bytes = read_bases + positions + 16 * reads
         achieved = kt_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else None
         traffic = load_traffic(workload_key)
-        scan_kernel = "k_tile_pileup_multi" if multi else f"k_tile_planes<{tile // 32}>"
+        scan_kernel = "k_tile_pileup_multi" if multi else f"k_tile_scan<{tile // 32}>"
         line = {
             "metric": METRIC,
             "value": value,

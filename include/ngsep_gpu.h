@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define NGSEP_ABI_VERSION 2
+#define NGSEP_ABI_VERSION 3
 
 #define NGSEP_OK 0
 #define NGSEP_E_INVALID (-1)      /* bad argument / state */
@@ -149,7 +149,7 @@ typedef struct ngsep_stats {
     int64_t read_bases;             /* projected read bytes resident in HBM */
     int64_t slot_bytes;             /* bytes of the slot array (incl. padding) */
     double  kernel_ms;              /* host wall time of the last device run (kernels + D2H) */
-    double  scan_ms;                /* device time of k_tile_pileup (scan + tally) */
+    double  scan_ms;                /* device time of the tile scan (KT) */
     double  genotype_ms;            /* device time of the posterior kernel */
     int32_t tile_positions;         /* positions per pileup tile (T) */
     int32_t tile_rows_max;          /* largest tile depth (rows of the tile-blocked pileup matrix) */
@@ -162,6 +162,7 @@ typedef struct ngsep_stats {
     double  layout_ms;              /* host time to build the device layout of the last staged run */
     double  upload_ms;              /* host time of its H2D upload */
     int64_t carved_positions;       /* covered positions inside carved indel regions (not called here) */
+    int64_t other_allele_calls;     /* entries of the scan's other-allele lists (valid non-reference calls) */
 } ngsep_stats;
 
 /* ---- context ---- */

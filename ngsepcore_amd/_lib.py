@@ -140,6 +140,7 @@ class NgsepStats(ctypes.Structure):
         ("layout_ms", ctypes.c_double),
         ("upload_ms", ctypes.c_double),
         ("carved_positions", ctypes.c_int64),
+        ("other_allele_calls", ctypes.c_int64),
     ]
 
 

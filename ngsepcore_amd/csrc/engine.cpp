@@ -950,8 +950,10 @@ static int choose_tile(const std::vector<int32_t>& m16, int64_t g_len, std::vect
 // and, at every position p, the codes of the reads covering p in pending-list order -- the order in which
 // PileupRecord.getAlleleCalls (PileupRecord.java:126-152) visits them -- in ranks 0, 1, ... (rank r at p is
 // the r-th covering read).  Three products per tile:
-//   * the bit planes (KT): rank row r holds W = T/32 words of "valid call" bits, then W words of "valid
-//     call of another allele than the reference" bits; the tile's planes start at word off_t / 16;
+//   * the valid-call plane (KT): rank row r holds W = T/32 words of "valid call" bits; the tile's plane
+//     starts at word off_t / 32;
+//   * the other-allele list (KT): the tile-relative position of every valid call of another allele than
+//     the reference, ascending (a position appears once per such call), at entry loff_t;
 //   * the position-major byte pile (KP): position p's rows_t codes at off_t + p * rows_t, rank order;
 //   * the strand bits (KP, countsStrand): bit off_t + p * rows_t + r = the rank-r read is reverse.
 // Tiles are independent: built on all host threads.
@@ -998,45 +1000,69 @@ static int build_single_layout(Staged& s, const std::vector<SRead>& reads, Layou
     const int W = T / 32;
     const uint8_t* ref = s.h_ref.data();
     std::atomic<int> bad{0};
-    parallel_for(ntiles, 256, [&](int64_t t0, int64_t t1) {
+    // tiles in chunks of 256 (each chunk's other-allele lists are concatenated after the parallel pass)
+    const int64_t kChunk = 256, nchunk = (ntiles + kChunk - 1) / kChunk;
+    std::vector<std::vector<uint16_t>> chunk_list((size_t)nchunk);
+    std::vector<int32_t> tile_nl((size_t)ntiles + 1, 0);
+    parallel_for(nchunk, 1, [&](int64_t c0, int64_t c1) {
         std::vector<int32_t> fill((size_t)T);
-        int64_t r_lo = first_read(t0);
-        for (int64_t t = t0; t < t1; t++) {
-            const int32_t nrow = rows[(size_t)t];
-            const int32_t tstart = (int32_t)(t * T), tend = tstart + T;
-            while (r_lo < nreads && (int64_t)reads[(size_t)r_lo].gfirst <= (int64_t)tstart - s.max_span) r_lo++;
-            if (!nrow) continue;
-            const int64_t toff = s.h_tinfo[(size_t)t].off;
-            uint8_t* col = s.h_cpile + toff;
-            uint32_t* pl = s.h_planes + toff / 16;
-            uint32_t* ng = s.h_cneg + toff / 32;
-            std::memset(col, 0, (size_t)nrow * T);
-            std::memset(pl, 0, (size_t)nrow * T / 4);
-            std::memset(ng, 0, (size_t)nrow * T / 8);
-            std::fill(fill.begin(), fill.end(), 0);
-            for (int64_t r = r_lo; r < nreads && reads[(size_t)r].gfirst < tend; r++) {
-                const SRead& rd = reads[(size_t)r];
-                if (rd.glast < tstart || rd.glast < rd.gfirst) continue;
-                const int32_t a = std::max(rd.gfirst, tstart) - tstart, b = std::min(rd.glast, tend - 1) - tstart;
-                const uint8_t* src = rd.bytes + (tstart + a - rd.gfirst);
-                for (int32_t p = a; p <= b; p++) {
-                    const int32_t rank = fill[(size_t)p]++;
-                    if (rank >= nrow) { bad = 1; continue; }
-                    const uint8_t cd = src[p - a];
-                    const int64_t cell = (int64_t)p * nrow + rank;
-                    col[cell] = cd;
-                    if (rd.neg) ng[cell >> 5] |= 1u << (cell & 31);
-                    if (cd & kCodeValid) {
-                        const uint8_t rc = ref[tstart + p];
-                        const uint8_t ra = (rc & kRefCallable) ? (uint8_t)((rc >> 5) & 3) : 0;
-                        uint32_t* pv = pl + (size_t)rank * 2 * W;
-                        pv[p >> 5] |= 1u << (p & 31);
-                        if (((cd >> 5) & 3) != ra) pv[W + (p >> 5)] |= 1u << (p & 31);
+        std::vector<uint16_t> na((size_t)T);
+        for (int64_t ch = c0; ch < c1; ch++) {
+            const int64_t t0 = ch * kChunk, t1 = std::min(ntiles, t0 + kChunk);
+            std::vector<uint16_t>& lst = chunk_list[(size_t)ch];
+            int64_t r_lo = first_read(t0);
+            for (int64_t t = t0; t < t1; t++) {
+                const int32_t nrow = rows[(size_t)t];
+                const int32_t tstart = (int32_t)(t * T), tend = tstart + T;
+                while (r_lo < nreads && (int64_t)reads[(size_t)r_lo].gfirst <= (int64_t)tstart - s.max_span) r_lo++;
+                if (!nrow) continue;
+                const int64_t toff = s.h_tinfo[(size_t)t].off;
+                uint8_t* col = s.h_cpile + toff;
+                uint32_t* pl = s.h_planes + toff / 32;
+                uint32_t* ng = s.h_cneg + toff / 32;
+                std::memset(col, 0, (size_t)nrow * T);
+                std::memset(pl, 0, (size_t)nrow * T / 8);
+                std::memset(ng, 0, (size_t)nrow * T / 8);
+                std::fill(fill.begin(), fill.end(), 0);
+                std::fill(na.begin(), na.end(), (uint16_t)0);
+                for (int64_t r = r_lo; r < nreads && reads[(size_t)r].gfirst < tend; r++) {
+                    const SRead& rd = reads[(size_t)r];
+                    if (rd.glast < tstart || rd.glast < rd.gfirst) continue;
+                    const int32_t a = std::max(rd.gfirst, tstart) - tstart, b = std::min(rd.glast, tend - 1) - tstart;
+                    const uint8_t* src = rd.bytes + (tstart + a - rd.gfirst);
+                    for (int32_t p = a; p <= b; p++) {
+                        const int32_t rank = fill[(size_t)p]++;
+                        if (rank >= nrow) { bad = 1; continue; }
+                        const uint8_t cd = src[p - a];
+                        const int64_t cell = (int64_t)p * nrow + rank;
+                        col[cell] = cd;
+                        if (rd.neg) ng[cell >> 5] |= 1u << (cell & 31);
+                        if (cd & kCodeValid) {
+                            const uint8_t rc = ref[tstart + p];
+                            const uint8_t ra = (rc & kRefCallable) ? (uint8_t)((rc >> 5) & 3) : 0;
+                            pl[(size_t)rank * W + (p >> 5)] |= 1u << (p & 31);
+                            if (((cd >> 5) & 3) != ra) na[(size_t)p]++;
+                        }
                     }
                 }
+                // the tile's other-allele calls: their positions, ascending (one entry per call)
+                const size_t before = lst.size();
+                for (int32_t p = 0; p < T; p++) lst.insert(lst.end(), na[(size_t)p], (uint16_t)p);
+                tile_nl[(size_t)t] = (int32_t)(lst.size() - before);
             }
         }
     });
+    s.h_loff.assign((size_t)ntiles + 1, 0);
+    for (int64_t t = 0; t < ntiles; t++) s.h_loff[(size_t)t + 1] = s.h_loff[(size_t)t] + tile_nl[(size_t)t];
+    s.h_olist.resize((size_t)s.h_loff[(size_t)ntiles] + 64);      // + 64: KT reads a whole wave of entries
+    std::vector<int64_t> cbase((size_t)nchunk + 1, 0);
+    for (int64_t ch = 0; ch < nchunk; ch++) cbase[(size_t)ch + 1] = cbase[(size_t)ch] + (int64_t)chunk_list[(size_t)ch].size();
+    parallel_for(nchunk, 16, [&](int64_t c0, int64_t c1) {
+        for (int64_t ch = c0; ch < c1; ch++)
+            if (!chunk_list[(size_t)ch].empty())
+                std::memcpy(&s.h_olist[(size_t)cbase[(size_t)ch]], chunk_list[(size_t)ch].data(), chunk_list[(size_t)ch].size() * 2);
+    });
+    std::fill(s.h_olist.end() - 64, s.h_olist.end(), (uint16_t)0);
     lap("tiles");
     return bad ? -1 : 0;
 }
@@ -1047,7 +1073,7 @@ bool LayoutArena::ensure(int64_t pile_bytes, bool exact) {
     int64_t want = exact ? pile_bytes : pile_bytes + pile_bytes / 4;
     want = (std::max<int64_t>(want, 1 << 16) + 4095) / 4096 * 4096;
     cpile = static_cast<uint8_t*>(pinned_alloc((size_t)want));
-    planes = static_cast<uint32_t*>(pinned_alloc((size_t)want / 4));
+    planes = static_cast<uint32_t*>(pinned_alloc((size_t)want / 8));
     cneg = static_cast<uint32_t*>(pinned_alloc((size_t)want / 8));
     if (!cpile || !planes || !cneg) { release(); return false; }
     cap = want;
@@ -1384,6 +1410,7 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     if (device_upload(c->dev, s, err) != 0) return set_error(c, NGSEP_E_DEVICE, err);
     c->stats.global_positions = s.g_len;
     c->stats.n_tiles = s.n_tiles;
+    c->stats.other_allele_calls = s.h_loff.empty() ? 0 : s.h_loff.back();
     c->stats.layout_ms = std::chrono::duration<double, std::milli>(h1 - h0).count();
     c->stats.upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h1).count();
     if (host_timing)
@@ -1397,6 +1424,8 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     std::vector<uint8_t>().swap(s.h_ref);
     std::vector<uint8_t>().swap(s.h_pile);
     std::vector<TileInfo>().swap(s.h_tinfo);
+    std::vector<uint16_t>().swap(s.h_olist);
+    std::vector<int32_t>().swap(s.h_loff);
     std::vector<uint16_t>().swap(s.h_rows);
     std::vector<int64_t>().swap(s.h_toff);
     std::vector<int32_t>().swap(s.h_perm);
@@ -1461,6 +1490,7 @@ static void run_window_job(ngsep_ctx* c, WindowJob* j) {
     c->stats.tile_rows_max = std::max(c->stats.tile_rows_max, s.tile_rows_max);
     c->stats.global_positions += s.g_len;
     c->stats.n_tiles += s.n_tiles;
+    c->stats.other_allele_calls += s.h_loff.empty() ? 0 : s.h_loff.back();
     c->stats.layout_ms += std::chrono::duration<double, std::milli>(h1 - h0).count();
     c->stats.upload_ms += std::chrono::duration<double, std::milli>(h2 - h1).count();
     j->rc = run_device_into(c, j->sites, nullptr);

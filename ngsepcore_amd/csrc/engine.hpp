@@ -273,8 +273,11 @@ struct Staged {            // everything resident for one run
     std::vector<int32_t> h_perm, h_bseg, h_blb, h_bbase;
     int64_t nblk_b = 0;
     std::vector<uint8_t> h_ref;
-    // single-sample layout (engine.cpp build_single_layout): bit planes, position-major byte pile in
-    // pending-list rank order, strand bits of its cells -- in the context's pinned LayoutArena
+    // single-sample layout (engine.cpp build_single_layout): the valid-call plane, position-major byte
+    // pile in pending-list rank order, strand bits of its cells -- in the context's pinned LayoutArena --
+    // and the per-tile lists of other-allele call positions
+    std::vector<uint16_t> h_olist;
+    std::vector<int32_t> h_loff;        // tile t's entries: h_olist[h_loff[t] .. h_loff[t+1])
     uint32_t* h_planes = nullptr;
     uint8_t* h_cpile = nullptr;
     uint32_t* h_cneg = nullptr;
@@ -282,7 +285,7 @@ struct Staged {            // everything resident for one run
 };
 
 // Pinned host buffers of the single-sample layout, reused run after run (streamed windows: no page faults,
-// DMA-speed uploads).  Grown geometrically; sized by the pile bytes (planes = pile / 4, strand bits = / 8).
+// DMA-speed uploads).  Grown geometrically; sized by the pile bytes (valid-call plane and strand bits = / 8).
 struct LayoutArena {
     uint8_t* cpile = nullptr;
     uint32_t* planes = nullptr;

@@ -1,6 +1,6 @@
 // kernels.hip -- gfx950 kernels of the NGSEP SNV pileup path.
 //
-//   KT  k_tile_planes<W> : single-sample scan of the pile's bit planes (valid call / valid call of
+//   KT  k_tile_scan<W> : single-sample scan of the valid-call plane and the other-allele lists (valid call /
 //        another allele, 2 bits per position-row), one wavefront per tile: bit-sliced counts of every
 //        position (LDS-free butterfly over row groups), the candidates (a valid non-reference call at a
 //        callable position) and the count bound as a table; survivors queued.  This is
@@ -82,7 +82,10 @@ struct Device {
     hipEvent_t ev[4] = {};
     uint8_t* d_slots = nullptr;      // multisample: read-major SoA
     uint8_t* d_pile = nullptr;       // single sample: position-major byte pile; multisample: per-sample blocks
-    uint32_t* d_planes = nullptr;    // single sample: bit planes of the pile (KT)
+    uint32_t* d_planes = nullptr;    // single sample: valid-call plane of the pile (KT)
+    uint16_t* d_olist = nullptr;     // single sample: other-allele call positions per tile (KT)
+    int32_t* d_loff = nullptr;       // their per-tile ranges
+    size_t cap_olist = 0, cap_loff = 0;
     uint32_t* d_cneg = nullptr;      // single sample: strand bits of the pile's cells (KP)
     int4* d_wins = nullptr;          // windows {global start of w0, w0, seq_id, wlen}, ascending (KO maps records)
     // single-sample buffers are kept from run to run (streamed windows) and grown when a run needs more
@@ -208,16 +211,32 @@ __global__ __launch_bounds__(kPostThreads) void k_posterior(const QueueSite* __r
         int32_t sc[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
         // L00 L01 L02 L03 L11 L12 L13 L22 L23 L33 (upper triangle, ngsep_site_out.logc order)
         double L[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        // the column's dwords in order (rank r = byte sh + r of the dword stream), the strand bits from the
-        // matching words; a small loop, so the kernel's code stays in the instruction cache
+        // the column's dwords in order (rank r = byte sh + r of the dword stream) through a window of 8
+        // dwords in flight, the strand bits through a window of 3 words of the strand array (the pile has 64
+        // bytes and the strand array 4 words of slack, so the loads past the column need no guard); a small
+        // loop, so the kernel's code stays in the instruction cache
         {
-            const uint32_t* cw = reinterpret_cast<const uint32_t*>(cpile) + (base >> 2);
-            const int sh = (int)(base & 3);
+            const int64_t c0 = base & ~(int64_t)3;                        // cell of the first dword's byte 0
+            const uint32_t* cw = reinterpret_cast<const uint32_t*>(cpile) + (c0 >> 2);
+            const int sh = (int)(base - c0);
             const int nd = (rows + sh + 3) >> 2;
-            uint32_t dn = nd > 0 ? cw[0] : 0u;
+            uint32_t q0 = cw[0], q1 = cw[1], q2 = cw[2], q3 = cw[3], q4 = cw[4], q5 = cw[5], q6 = cw[6], q7 = cw[7];
+            const uint32_t* nw = cneg + (c0 >> 5);
+            uint64_t nb = (uint64_t)nw[0] | ((uint64_t)nw[1] << 32);
+            uint32_t nb2 = nw[2];
+            int nbo = (int)(c0 & 31);                                      // (a multiple of 4)
             for (int k = 0; k < nd; k++) {
-                const uint32_t d = dn;
-                dn = k + 1 < nd ? cw[k + 1] : 0u;                          // the next dword is in flight
+                const uint32_t d = q0;
+                q0 = q1; q1 = q2; q2 = q3; q3 = q4; q4 = q5; q5 = q6; q6 = q7;
+                q7 = cw[k + 8];
+                const uint32_t n4 = (uint32_t)(nb >> nbo) & 0xFu;             // the 4 cells' strand bits
+                nbo += 4;
+                if (nbo == 32) {
+                    nb = (nb >> 32) | ((uint64_t)nb2 << 32);
+                    nw++;
+                    nb2 = nw[2];
+                    nbo = 0;
+                }
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
                     const int r = 4 * k + e - sh;                          // rank of this byte
@@ -228,8 +247,7 @@ __global__ __launch_bounds__(kPostThreads) void k_posterior(const QueueSite* __r
                     const int a = (int)((cd >> 5) & 3u);
                     int q = (int)(cd & 31u);
                     q = q > gp.max_q ? gp.max_q : q;                      // -maxBaseQS (:217-219)
-                    const int64_t cell = base + r;
-                    const int neg = (int)((cneg[cell >> 5] >> (cell & 31)) & 1u);
+                    const int neg = (int)((n4 >> e) & 1u);
 #pragma unroll
                     for (int t = 0; t < 4; t++) {                         // constant indices: registers, not scratch
                         cnt[t] += a == t ? 1 : 0;
@@ -436,15 +454,18 @@ __device__ __forceinline__ void wave_flush(ScanShared& sh, int wv, int lane, int
 
 
 // ------------------------------------------------------------------------------------------
-// KT (bit planes): the single-sample scan over the planes instead of the byte pile -- a quarter of
-// the bytes.  Wave per tile; lane = (word w, row group g), W words x G groups = 64 lanes: the lane
-// holds word w of rows g, g+G, ... (W rows of a 64-row chunk) and counts them bit-sliced (bit j of
-// count word k = bit k of position 32w+j's count), then a butterfly over the G groups adds the
-// groups' counts, so every lane has the chunk's valid / other-allele counts of its word's 32
-// positions.  Candidates (other-allele calls at a callable position) are split over the G lanes of
-// their word, the count bound (table cb_nr) runs lane-parallel, the rare survivors take the exact
-// integer bound of k_tile_pileup<0> over their column of the byte pile.  The next tile's planes and
-// reference bytes are in flight while a tile is examined.
+// KT: the single-sample tile scan -- one wavefront per tile (persistent waves, grid stride), two inputs:
+//   * the valid-call plane: rows_t rank rows of W = T/32 words.  Lane = (word w, row group g), W words x
+//     G groups = 64 lanes: the lane holds word w of rows g, g+G, ... of a 64-row chunk and counts them
+//     bit-sliced (bit j of count word k = bit k of position 32w+j's count); a butterfly over the G groups
+//     (DPP row rotations, the gfx950 lane swaps) leaves every lane its word's valid-call counts nv;
+//   * the other-allele list: one entry per valid call of another allele than the reference (its tile
+//     position), which the wave adds into per-position LDS counters na.
+// Lane l then owns positions P l .. P l + P-1 (P = T/64): a candidate is a callable position with na > 0
+// (every other position is hom-ref or has no pileup, DESIGN.md "why pruning is exact"); the count bound
+// (table cb_nr) drops those whose counts prove them hom-ref, the rest are queued for KP (with
+// gp.exact_bound, after the exact integer bound over their column of the byte pile).  The next tile's
+// plane words, reference bytes and first 64 list entries are in flight while a tile is examined.
 // ------------------------------------------------------------------------------------------
 // bit-sliced adders: out = a + b (k-bit numbers, k+1-bit result)
 template <int K>
@@ -477,39 +498,51 @@ struct BsCount<1> {
 
 template <int W>
 __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(W >= 16 ? NGSEP_KT16_WAVES_PER_EU : NGSEP_KT_WAVES_PER_EU)))
-void k_tile_planes(const uint32_t* __restrict__ planes, const uint8_t* __restrict__ pile, const TileInfo* __restrict__ tinfo,
-                   const uint8_t* __restrict__ ref, int64_t n_tiles, const LikTables* __restrict__ tabs, GenotypeParams gp,
-                   QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap,
-                   int32_t* __restrict__ bcount, int64_t nb) {
+void k_tile_scan(const uint32_t* __restrict__ vplane, const uint16_t* __restrict__ olist, const int32_t* __restrict__ loff,
+                 const uint8_t* __restrict__ pile, const TileInfo* __restrict__ tinfo,
+                 const uint8_t* __restrict__ ref, int64_t n_tiles, const LikTables* __restrict__ tabs, GenotypeParams gp,
+                 QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap,
+                 int32_t* __restrict__ bcount, int64_t nb) {
     constexpr int T = W * 32;
     constexpr int G = 64 / W;                       // row groups
     constexpr int KB0 = BsCount<W>::B;              // bits of a lane's count (<= W rows)
     constexpr int KC = 7;                           // bits of a 64-row chunk's count
+    constexpr int P = T / 64;                       // positions per lane
     __shared__ ScanShared sh;
+    __shared__ uint32_t s_na[kScanWaves][T];        // per-position other-allele counts of the wave's tile
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lw = lane & (W - 1), lg = lane / W;   // this lane's word and row group
+    const int lw = lane & (W - 1), lg = lane / W;   // this lane's word and row group (plane counting)
     for (int64_t i = (int64_t)blockIdx.x * kScanThreads + threadIdx.x; i < nb; i += (int64_t)gridDim.x * kScanThreads) bcount[i] = 0;
     if (threadIdx.x < 64) sh.w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
     sh.cb[threadIdx.x] = tabs->cb_nr[threadIdx.x];
     __syncthreads();
     const long long th = tabs->t_het, to = tabs->t_homo;
     const int32_t maxq = gp.max_q;
-    // this lane's share of its word's candidates: bits j with j % G == lg
-    const uint32_t share = (G == 4 ? 0x11111111u : G == 8 ? 0x01010101u : 0x00010001u) << lg;
     int32_t qn = 0;
     uint32_t my_cand = 0, nexact = 0;
     const int64_t nwaves = (int64_t)gridDim.x * kScanWaves;
     const int64_t t0 = (int64_t)blockIdx.x * kScanWaves + wv;
-    auto load_chunk = [&](int64_t off, int32_t rows, int c, uint32_t (&V)[W], uint32_t (&N)[W]) {
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    auto load_chunk = [&](int64_t off, int32_t rows, int c, uint32_t (&V)[W]) {
         const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(planes + (off >> 4)), 0, rows * 8 * W, 0x00020000);
+            __builtin_amdgcn_make_buffer_rsrc((void*)(vplane + (off >> 5)), 0, rows * 4 * W, 0x00020000);
 #pragma unroll
         for (int i = 0; i < W; i++) {
             const int r = 64 * c + lg + G * i;
-            V[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, (r * 2 * W + lw) * 4, 0, 0);
-            N[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, (r * 2 * W + W + lw) * 4, 0, 0);
+            V[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, (r * W + lw) * 4, 0, 0);
         }
+    };
+    // the reference codes of this lane's P positions, one byte each
+    auto load_ref = [&](int64_t t) -> uint64_t {
+        const uint8_t* rp = ref + t * T + P * lane;
+        if (P == 8) return *reinterpret_cast<const uint64_t*>(rp);
+        if (P == 4) return *reinterpret_cast<const uint32_t*>(rp);
+        return *reinterpret_cast<const uint16_t*>(rp);
     };
     auto uni64 = [](int64_t v) -> int64_t {
         return ((int64_t)__builtin_amdgcn_readfirstlane((int32_t)(v >> 32)) << 32) |
@@ -554,123 +587,125 @@ void k_tile_planes(const uint32_t* __restrict__ planes, const uint8_t* __restric
 #pragma unroll
         for (int k = 0; k < KC; k++) out[k] = c[k];
     };
+    // prefetch pipeline: the descriptor and list range two tiles ahead, the plane words, reference bytes and
+    // first list entries one tile ahead
     TileInfo cur = t0 < n_tiles ? tinfo[t0] : TileInfo{0, 0, 0};
+    int32_t cur_lo = t0 < n_tiles ? loff[t0] : 0, cur_hi = t0 < n_tiles ? loff[t0 + 1] : 0;
     TileInfo nxt = t0 + nwaves < n_tiles ? tinfo[t0 + nwaves] : TileInfo{0, 0, 0};
-    uint32_t Vn[W], Nn[W], refn[T / 64];
+    int32_t nxt_lo = t0 + nwaves < n_tiles ? loff[t0 + nwaves] : 0, nxt_hi = t0 + nwaves < n_tiles ? loff[t0 + nwaves + 1] : 0;
+    uint32_t Vn[W];
 #pragma unroll
-    for (int i = 0; i < W; i++) { Vn[i] = 0; Nn[i] = 0; }
-#pragma unroll
-    for (int k = 0; k < T / 64; k++) refn[k] = 0;
+    for (int i = 0; i < W; i++) Vn[i] = 0;
+    uint64_t refn = 0;
+    uint32_t en = 0;
     if (t0 < n_tiles && !(gp.ablate & 4)) {
-        load_chunk(uni64(cur.off), __builtin_amdgcn_readfirstlane(cur.rows), 0, Vn, Nn);
-#pragma unroll
-        for (int k = 0; k < T / 64; k++) refn[k] = ref[t0 * T + 64 * k + lane];
+        load_chunk(uni64(cur.off), __builtin_amdgcn_readfirstlane(cur.rows), 0, Vn);
+        refn = load_ref(t0);
+        en = olist[__builtin_amdgcn_readfirstlane(cur_lo) + lane];     // (the list has 64 entries of slack)
     }
     for (int64_t t = t0; t < n_tiles; t += nwaves) {
         if (gp.ablate & 4) break;
         const int32_t rows = __builtin_amdgcn_readfirstlane(cur.rows);
         const int64_t off = uni64(cur.off);
-        uint32_t V[W], N[W], refb[T / 64];
+        const int32_t lo = __builtin_amdgcn_readfirstlane(cur_lo), ne = __builtin_amdgcn_readfirstlane(cur_hi) - lo;
+        uint32_t V[W];
 #pragma unroll
-        for (int i = 0; i < W; i++) { V[i] = Vn[i]; N[i] = Nn[i]; }
-#pragma unroll
-        for (int k = 0; k < T / 64; k++) refb[k] = refn[k];
+        for (int i = 0; i < W; i++) V[i] = Vn[i];
+        const uint64_t refq = refn;
+        const uint32_t e0 = en;
         const int32_t tstart = (int32_t)(t * T);
-        // the next tile's descriptor is here: its planes and reference bytes load meanwhile
+        // the next tile's inputs load meanwhile
         const TileInfo nt = nxt;
-        if (t + 2 * nwaves < n_tiles) nxt = tinfo[t + 2 * nwaves];
+        const int32_t nt_lo = nxt_lo, nt_hi = nxt_hi;
+        if (t + 2 * nwaves < n_tiles) {
+            nxt = tinfo[t + 2 * nwaves];
+            nxt_lo = loff[t + 2 * nwaves];
+            nxt_hi = loff[t + 2 * nwaves + 1];
+        }
         if (t + nwaves < n_tiles) {
-            load_chunk(uni64(nt.off), __builtin_amdgcn_readfirstlane(nt.rows), 0, Vn, Nn);
-#pragma unroll
-            for (int k = 0; k < T / 64; k++) refn[k] = ref[(t + nwaves) * T + 64 * k + lane];
+            load_chunk(uni64(nt.off), __builtin_amdgcn_readfirstlane(nt.rows), 0, Vn);
+            refn = load_ref(t + nwaves);
+            en = olist[__builtin_amdgcn_readfirstlane(nt_lo) + lane];
         }
         cur = nt;
+        cur_lo = nt_lo;
+        cur_hi = nt_hi;
         if (rows == 0) continue;
         const int ng = (rows + 63) >> 6;
-        const bool bound = gp.use_bound && rows <= 255 && !(gp.ablate & 256);   // (diagnostics: 256 = loads only) 32-bit halves of the exact sums cannot overflow
-        // counts (bit-sliced, 8 bits: rows <= 255) or, without the bound, the OR of the other-allele plane
-        uint32_t cv[8], ca[8], hits = 0;
+        const bool bound = gp.use_bound && rows <= 255 && !(gp.ablate & 256);   // (diagnostics: 256 = no counting)
+        // valid-call counts (bit-sliced, 8 bits: rows <= 255)
+        uint32_t cv[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) { cv[k] = 0; ca[k] = 0; }
-        for (int c = 0; c < ng; c++) {
-            if (c > 0) load_chunk(off, rows, c, V, N);
-            if (bound) {
-                uint32_t xv[KC], xa[KC];
+        for (int k = 0; k < 8; k++) cv[k] = 0;
+        if (bound) {
+            for (int c = 0; c < ng; c++) {
+                if (c > 0) load_chunk(off, rows, c, V);
+                uint32_t xv[KC];
                 chunk_count(V, xv);
-                chunk_count(N, xa);
                 if (c == 0) {
 #pragma unroll
-                    for (int k = 0; k < KC; k++) { cv[k] = xv[k]; ca[k] = xa[k]; }
+                    for (int k = 0; k < KC; k++) cv[k] = xv[k];
                 } else {
-                    uint32_t sv[8], sa[8], zv[8], za[8];
+                    uint32_t zv[8], tv[9];
 #pragma unroll
-                    for (int k = 0; k < 8; k++) { zv[k] = k < KC ? xv[k] : 0u; za[k] = k < KC ? xa[k] : 0u; }
-                    uint32_t tv[9], ta[9];
+                    for (int k = 0; k < 8; k++) zv[k] = k < KC ? xv[k] : 0u;
                     bs_add<8>(cv, zv, tv);
-                    bs_add<8>(ca, za, ta);
 #pragma unroll
-                    for (int k = 0; k < 8; k++) { sv[k] = tv[k]; sa[k] = ta[k]; }
-#pragma unroll
-                    for (int k = 0; k < 8; k++) { cv[k] = sv[k]; ca[k] = sa[k]; }
+                    for (int k = 0; k < 8; k++) cv[k] = tv[k];
                 }
-            } else {
-#pragma unroll
-                for (int i = 0; i < W; i++) hits |= N[i];
             }
         }
-        if (bound) {
+        // other-allele counts per position: the list's entries into LDS counters
+        uint32_t* na_w = s_na[wv];
 #pragma unroll
-            for (int k = 0; k < 8; k++) hits |= ca[k];
-        } else {
-#pragma unroll
-            for (int d = W; d < 64; d <<= 1) hits |= (uint32_t)__shfl_xor((int)hits, d, 64);
+        for (int j = 0; j < P; j++) na_w[P * lane + j] = 0;
+        wave_sync();
+        for (int e = 0; e < ne; e += 64) {
+            const uint32_t pe = e == 0 ? e0 : (uint32_t)olist[lo + e + lane];
+            if (e + lane < ne) atomicAdd(&na_w[pe & (T - 1)], 1u);
         }
-        // callable reference positions of this lane's word
-        uint32_t okw = 0;
+        wave_sync();
+        uint32_t mine = 0;
 #pragma unroll
-        for (int k = 0; k < T / 64; k++) {
-            const unsigned long long okm = __ballot((refb[k] & 0x80u) != 0);
-            okw = lw == 2 * k ? (uint32_t)okm : okw;
-            okw = lw == 2 * k + 1 ? (uint32_t)(okm >> 32) : okw;
+        for (int j = 0; j < P; j++) {
+            const bool callable = ((refq >> (8 * j)) & 0x80u) != 0;
+            mine |= (callable && na_w[P * lane + j] != 0) ? 1u << j : 0u;
         }
-        uint32_t mine = hits & okw & share;
         my_cand += (uint32_t)__popc(mine);
         if (gp.ablate & 1) continue;                   // diagnostics: scan only
-        auto ref_code = [&](int p) -> uint32_t {       // p wave-uniform
-            uint32_t v = 0;
+        if (!__ballot(mine != 0)) continue;
+        // this lane's slices of its positions' valid-call counts: bits [P lane, P lane + P) of the counts of
+        // word (P lane) / 32, which lane (P lane) / 32 holds (row group 0)
+        uint32_t vs[8];
+        {
+            const int wsrc = (P * lane) >> 5, bo = (P * lane) & 31;
 #pragma unroll
-            for (int k = 0; k < T / 64; k++) v = (p >> 6) == k ? (uint32_t)__builtin_amdgcn_readlane((int)refb[k], p & 63) : v;
-            return v;
-        };
-        auto emit_one = [&](int p) {                   // p wave-uniform
-            if (qn + 1 > kWaveQ) { wave_flush(sh, wv, lane, qn, queue, counters, qcap); qn = 0; }
-            const uint32_t rcode = ref_code(p);
-            if (lane == 0) sh.q[wv][qn] = QueueSite{tstart + p, (int32_t)rcode};
-            qn++;
-        };
+            for (int k = 0; k < 8; k++) vs[k] = ((uint32_t)__shfl((int)cv[k], wsrc, 64) >> bo) & ((1u << P) - 1u);
+        }
         while (__ballot(mine != 0)) {                  // wave-uniform loop over each lane's candidates
             const bool has = mine != 0;
             const int j = has ? __builtin_ctz(mine) : 0;
             mine &= mine - 1u;
-            const int pp = 32 * lw + j;
+            const int pp = P * lane + j;
+            const uint32_t rcode = (uint32_t)(refq >> (8 * j)) & 0xFFu;
             bool need = has;
             if (bound && has) {
-                uint32_t nv = 0, na = 0;
+                uint32_t nv = 0;
 #pragma unroll
-                for (int k = 0; k < 8; k++) { nv |= ((cv[k] >> j) & 1u) << k; na |= ((ca[k] >> j) & 1u) << k; }
+                for (int k = 0; k < 8; k++) nv |= ((vs[k] >> j) & 1u) << k;
+                const uint32_t na = na_w[pp];
                 need = (int32_t)(nv - na) < (int32_t)sh.cb[na];   // the count bound does not drop it
             }
-            unsigned long long ex = __ballot(need);
-            if (gp.ablate & 128) ex = 0;                   // diagnostics: count bound only
-            while (ex) {
-                const int k = __builtin_ctzll(ex);
-                ex &= ex - 1ull;
-                const int p = __builtin_amdgcn_readlane(pp, k);
-                bool keep = true;
-                if (bound && gp.exact_bound) {
+            if (bound && gp.exact_bound) {
+                // the exact integer bound over the candidate's column of the byte pile, one candidate at a time
+                unsigned long long ex = __ballot(need);
+                while (ex) {
+                    const int k = __builtin_ctzll(ex);
+                    ex &= ex - 1ull;
+                    const int p = __builtin_amdgcn_readlane(pp, k);
+                    const uint32_t ra = ((uint32_t)__builtin_amdgcn_readlane((int)rcode, k) >> 5) & 3u;
                     nexact++;
                     unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-                    const uint32_t ra = (ref_code(p) >> 5) & 3u;
                     for (int g = 0; g < ng; g++) {
                         const int r = g * 64 + lane;
                         // the position-major byte pile: position p's rows are one contiguous column
@@ -696,11 +731,21 @@ void k_tile_planes(const uint32_t* __restrict__ planes, const uint8_t* __restric
                     const long long x1 = (long long)(a1 & 0xFFFFFFFFull), y1 = (long long)(a2 & 0xFFFFFFFFull);
                     const long long z1 = (long long)(a3 & 0xFFFFFFFFull);
                     const long long x2 = (long long)(a1 >> 32), y2 = (long long)(a2 >> 32), z2 = (long long)(a3 >> 32);
-                    keep = !((R1 - x1 > th) && (R1 - y1 > th) && (R1 - z1 > th) &&
-                             (R2 - x2 > to) && (R2 - y2 > to) && (R2 - z2 > to) &&
-                             (R2 - x1 - y1 > th) && (R2 - x1 - z1 > th) && (R2 - y1 - z1 > th));
+                    const bool drop = (R1 - x1 > th) && (R1 - y1 > th) && (R1 - z1 > th) &&
+                                      (R2 - x2 > to) && (R2 - y2 > to) && (R2 - z2 > to) &&
+                                      (R2 - x1 - y1 > th) && (R2 - x1 - z1 > th) && (R2 - y1 - z1 > th);
+                    if (drop && lane == k) need = false;
                 }
-                if (keep) emit_one(p);
+            }
+            if (gp.ablate & 128) need = false;         // diagnostics: count bound only
+            // the survivors into the wave's staging area (rank among this round's survivors)
+            const unsigned long long m = __ballot(need);
+            const int32_t cnt = (int32_t)__popcll(m);
+            if (cnt) {
+                if (qn + cnt > kWaveQ) { wave_flush(sh, wv, lane, qn, queue, counters, qcap); qn = 0; }
+                const int rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                if (need) sh.q[wv][qn + rk] = QueueSite{tstart + pp, (int32_t)rcode};
+                qn += cnt;
             }
         }
     }
@@ -1526,6 +1571,9 @@ void device_release(Device* d) {
     (void)hipFree(d->d_slots); d->d_slots = nullptr;
     (void)hipFree(d->d_pile); d->d_pile = nullptr;
     (void)hipFree(d->d_planes); d->d_planes = nullptr;
+    (void)hipFree(d->d_olist); d->d_olist = nullptr;
+    (void)hipFree(d->d_loff); d->d_loff = nullptr;
+    d->cap_olist = d->cap_loff = 0;
     (void)hipFree(d->d_cneg); d->d_cneg = nullptr;
     (void)hipFree(d->d_wins); d->d_wins = nullptr;
     d->n_wins = 0;
@@ -1603,15 +1651,19 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
     if (s.single) {
         // single sample: planes (KT), the position-major pile and its strand bits (KP)
         const size_t ncw = (size_t)(s.pile_bytes / 32);
-        if (ensure_dev(&d->d_planes, &d->cap_planes, (size_t)std::max<int64_t>(s.pile_bytes / 4, 16), keep, err) ||
-            ensure_dev(&d->d_cneg, &d->cap_cneg, (ncw + 2) * sizeof(uint32_t), keep, err))    // + 2: KP reads word pairs
+        if (ensure_dev(&d->d_planes, &d->cap_planes, (size_t)std::max<int64_t>(s.pile_bytes / 8, 16), keep, err) ||
+            ensure_dev(&d->d_olist, &d->cap_olist, std::max<size_t>(s.h_olist.size(), 64) * sizeof(uint16_t), keep, err) ||
+            ensure_dev(&d->d_loff, &d->cap_loff, std::max<size_t>(s.h_loff.size(), 2) * sizeof(int32_t), keep, err) ||
+            ensure_dev(&d->d_cneg, &d->cap_cneg, (ncw + 4) * sizeof(uint32_t), keep, err))    // + 4: KP's strand-word window
             return -1;
-        HIP_TRY(hipMemsetAsync(d->d_cneg + ncw, 0, 2 * sizeof(uint32_t), d->stream));
+        HIP_TRY(hipMemsetAsync(d->d_cneg + ncw, 0, 4 * sizeof(uint32_t), d->stream));
         if (s.pile_bytes) {
             HIP_TRY(hipMemcpyAsync(d->d_pile, s.h_cpile, (size_t)s.pile_bytes, hipMemcpyHostToDevice, d->stream));
-            HIP_TRY(hipMemcpyAsync(d->d_planes, s.h_planes, (size_t)(s.pile_bytes / 4), hipMemcpyHostToDevice, d->stream));
+            HIP_TRY(hipMemcpyAsync(d->d_planes, s.h_planes, (size_t)(s.pile_bytes / 8), hipMemcpyHostToDevice, d->stream));
             HIP_TRY(hipMemcpyAsync(d->d_cneg, s.h_cneg, ncw * sizeof(uint32_t), hipMemcpyHostToDevice, d->stream));
         }
+        if (!s.h_olist.empty()) HIP_TRY(hipMemcpyAsync(d->d_olist, s.h_olist.data(), s.h_olist.size() * sizeof(uint16_t), hipMemcpyHostToDevice, d->stream));
+        if (!s.h_loff.empty()) HIP_TRY(hipMemcpyAsync(d->d_loff, s.h_loff.data(), s.h_loff.size() * sizeof(int32_t), hipMemcpyHostToDevice, d->stream));
         d->planes_W = s.tile / 32;
     } else {
         // multisample: per-(tile, sample) blocks (KTM), the read-major SoA and its bucket index (KPM)
@@ -1733,17 +1785,17 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         // bit-plane scan, persistent waves: as many workgroups as are co-resident, each wave walks the
         // tiles with a grid stride, so at any moment the waves stream one contiguous stretch of the planes
         const int wi = d->planes_W == 4 ? 0 : d->planes_W == 8 ? 1 : 2;
-        auto kt = wi == 0 ? (const void*)k_tile_planes<4> : wi == 1 ? (const void*)k_tile_planes<8> : (const void*)k_tile_planes<16>;
+        auto kt = wi == 0 ? (const void*)k_tile_scan<4> : wi == 1 ? (const void*)k_tile_scan<8> : (const void*)k_tile_scan<16>;
         int& per_cu = d->kt_planes_per_cu[wi];
         if (per_cu == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kt, kScanThreads, 0) != hipSuccess || per_cu < 1)) per_cu = 2;
         int bpc = per_cu;
         if (const char* e = std::getenv("NGSEP_BLOCKS_PER_CU")) bpc = std::max(1, std::atoi(e));   // tuning
         const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((d->n_tiles + kScanWaves - 1) / kScanWaves, (int64_t)d->n_cu * bpc));
         dim3 grid((unsigned)nblk);
-#define NGSEP_KTP_ARGS d->d_planes, d->d_pile, d->d_tinfo, d->d_ref, d->n_tiles, sl.d_tables, g, sl.d_hard, ctr, sl.cap_hard, sl.d_bcount, nb
-        if (wi == 0) hipExtLaunchKernelGGL(k_tile_planes<4>, grid, dim3(kScanThreads), 0, sl.stream, k0, k1, 0, NGSEP_KTP_ARGS);
-        else if (wi == 1) hipExtLaunchKernelGGL(k_tile_planes<8>, grid, dim3(kScanThreads), 0, sl.stream, k0, k1, 0, NGSEP_KTP_ARGS);
-        else hipExtLaunchKernelGGL(k_tile_planes<16>, grid, dim3(kScanThreads), 0, sl.stream, k0, k1, 0, NGSEP_KTP_ARGS);
+#define NGSEP_KTP_ARGS d->d_planes, d->d_olist, d->d_loff, d->d_pile, d->d_tinfo, d->d_ref, d->n_tiles, sl.d_tables, g, sl.d_hard, ctr, sl.cap_hard, sl.d_bcount, nb
+        if (wi == 0) hipExtLaunchKernelGGL(k_tile_scan<4>, grid, dim3(kScanThreads), 0, sl.stream, k0, k1, 0, NGSEP_KTP_ARGS);
+        else if (wi == 1) hipExtLaunchKernelGGL(k_tile_scan<8>, grid, dim3(kScanThreads), 0, sl.stream, k0, k1, 0, NGSEP_KTP_ARGS);
+        else hipExtLaunchKernelGGL(k_tile_scan<16>, grid, dim3(kScanThreads), 0, sl.stream, k0, k1, 0, NGSEP_KTP_ARGS);
 #undef NGSEP_KTP_ARGS
         HIP_TRY(hipGetLastError());
     } else {
