@@ -72,6 +72,11 @@ typedef struct ngsep_params {
      * also sets process_secondary = 1 and max_alns_per_start = 100 as its processFile does */
     int32_t coverage_stats;       /* 1: the alignments feed the coverage histograms instead of the variant caller */
     int32_t max_coverage;         /* maxCoverage 300 (setMaxCoverage): bins [0, max_coverage) + "More"; <= 1024 */
+    /* RelativeAlleleCountsCalculator (discovery/RelativeAlleleCountsCalculator.java:28-52,183-211): the caller
+     * also sets max_alns_per_start = maxRD (1000) and process_secondary = secondaryAlns as its runProcess does */
+    int32_t relative_allele_counts; /* 1: the pileups feed the allele-proportion distributions */
+    int32_t rac_min_rd;           /* -minRD 10 */
+    int32_t rac_min_bq;           /* -minBQ 20 (4..30 here: the pile's codes keep qualities clamped to 30) */
 } ngsep_params;
 
 /* Alignments as AlignmentsPileupGenerator.processAlignment receives them
@@ -164,6 +169,16 @@ typedef struct ngsep_stats {
     int64_t carved_positions;       /* covered positions inside carved indel regions (not called here) */
     int64_t other_allele_calls;     /* entries of the scan's other-allele lists (valid non-reference calls) */
 } ngsep_stats;
+
+/* ---- RelativeAlleleCountsCalculator (params.relative_allele_counts) ---- */
+/* RelativeAlleleCountsCalculator.runProcess + printResults (:183-244) on a BAM: the report text to out_path */
+int  ngsep_rac_bam(ngsep_ctx* c, const char* bam_path, const char* out_path);
+/* the distributions so far: prop[51] (bins 0, 0.01, .., 0.5), n_alleles[10] (bins 1..10), moments[6] =
+ * proportion count, sum, sum of squares, number-of-alleles count, sum, sum of squares (any may be NULL) */
+int  ngsep_fetch_rac(ngsep_ctx* c, double* prop, double* n_alleles, double* moments);
+/* printResults' text ("-" = stdout) */
+int  ngsep_write_rac(ngsep_ctx* c, const char* out_path);
+int  ngsep_clear_rac(ngsep_ctx* c);
 
 /* ---- context ---- */
 int  ngsep_abi_version(void);

@@ -5,7 +5,7 @@ include/ngsep_gpu.h); this package is the host-side mirror of the reference inte
 """
 from ._lib import LIB_PATH, NgsepError, load  # noqa: F401
 from .discovery import (CalledSite, CoverageStatisticsCalculator, GpuPileupSession, MultisampleVariantsDetector, PopulationSite,  # noqa: F401
-                        SingleSampleVariantsDetector, default_params)
+                        RelativeAlleleCountsCalculator, SingleSampleVariantsDetector, default_params)
 
-__all__ = ["GpuPileupSession", "CoverageStatisticsCalculator", "SingleSampleVariantsDetector", "MultisampleVariantsDetector", "PopulationSite", "CalledSite", "NgsepError", "default_params",
+__all__ = ["GpuPileupSession", "CoverageStatisticsCalculator", "RelativeAlleleCountsCalculator", "SingleSampleVariantsDetector", "MultisampleVariantsDetector", "PopulationSite", "CalledSite", "NgsepError", "default_params",
            "load", "LIB_PATH"]

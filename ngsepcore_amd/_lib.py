@@ -47,6 +47,9 @@ class NgsepParams(ctypes.Structure):
         ("min_allele_depth_freq", ctypes.c_double),
         ("coverage_stats", ctypes.c_int32),
         ("max_coverage", ctypes.c_int32),
+        ("relative_allele_counts", ctypes.c_int32),
+        ("rac_min_rd", ctypes.c_int32),
+        ("rac_min_bq", ctypes.c_int32),
     ]
 
 
@@ -190,6 +193,10 @@ SIGNATURES = {
     "ngsep_write_coverage": (ctypes.c_int, [_CTX, ctypes.c_char_p]),
     "ngsep_clear_coverage": (ctypes.c_int, [_CTX]),
     "ngsep_coverage_bam": (ctypes.c_int, [_CTX, ctypes.c_char_p, ctypes.c_char_p]),
+    "ngsep_rac_bam": (ctypes.c_int, [_CTX, ctypes.c_char_p, ctypes.c_char_p]),
+    "ngsep_fetch_rac": (ctypes.c_int, [_CTX, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_double)]),
+    "ngsep_write_rac": (ctypes.c_int, [_CTX, ctypes.c_char_p]),
+    "ngsep_clear_rac": (ctypes.c_int, [_CTX]),
 }
 
 _lib = None

@@ -400,8 +400,9 @@ extern "C" int ngsep_bam_open(ngsep_ctx* c, const char* path, ngsep_bam** out) {
     b->pos += 4;
     std::unordered_map<std::string, int32_t> seq_index;
     for (size_t i = 0; i < c->seq_names.size(); i++) seq_index[c->seq_names[i]] = (int32_t)i;
-    // CoverageStatisticsCalculator runs without a genome (-r is optional there): the header's sequences
-    const bool header_seqs = c->params.coverage_stats && c->seq_names.empty();
+    // CoverageStatisticsCalculator and RelativeAlleleCountsCalculator run without a genome (-r is optional
+    // there): the header's sequences (for the latter with their lengths, as N bases: it reads no reference)
+    const bool header_seqs = (c->params.coverage_stats || c->params.relative_allele_counts) && c->seq_names.empty();
     for (int32_t i = 0; i < n_ref; i++) {
         if (!need(b, 4, err)) break;
         int32_t ln = rd<int32_t>(&b->buf[b->pos]);
@@ -413,7 +414,8 @@ extern "C" int ngsep_bam_open(ngsep_ctx* c, const char* path, ngsep_bam** out) {
         if (header_seqs && !seq_index.count(name)) {
             seq_index[name] = (int32_t)c->seq_names.size();
             c->seq_names.push_back(name);
-            c->seq_bases.emplace_back();
+            if (c->params.relative_allele_counts) c->seq_bases.emplace_back((size_t)std::max(lref, 0), 'N');
+            else c->seq_bases.emplace_back();
             b->ref_to_seq.push_back(seq_index[name]);
             continue;
         }
@@ -836,6 +838,22 @@ extern "C" int ngsep_coverage_bam(ngsep_ctx* c, const char* bam_path, const char
     rc = ngsep_notify_end(c);
     if (rc != NGSEP_OK || !out_path) return rc;
     return ngsep_write_coverage(c, out_path);
+}
+
+// RelativeAlleleCountsCalculator.run (discovery/RelativeAlleleCountsCalculator.java:183-211): the generator over
+// the BAM (maxAlnsPerStartPos = maxRD and secondaryAlns come with the context's params), printResults' text
+extern "C" int ngsep_rac_bam(ngsep_ctx* c, const char* bam_path, const char* out_path) {
+    if (!c || !bam_path) return NGSEP_E_INVALID;
+    if (!c->params.relative_allele_counts) return set_error(c, NGSEP_E_INVALID, "ngsep_rac_bam needs params.relative_allele_counts = 1");
+    ngsep_bam* b = nullptr;
+    int rc = ngsep_bam_open(c, bam_path, &b);
+    if (rc != NGSEP_OK) return rc;
+    rc = for_each_batch(c, b, [&](const ngsep_read_batch& batch) { return process_alignments_packed(c, &batch); });
+    ngsep_bam_close(b);
+    if (rc != NGSEP_OK) return rc;
+    rc = ngsep_notify_end(c);
+    if (rc != NGSEP_OK || !out_path) return rc;
+    return ngsep_write_rac(c, out_path);
 }
 
 extern "C" int ngsep_call_bam(ngsep_ctx* c, const char* bam_path, const char* out_vcf_path) {

@@ -130,6 +130,44 @@ static int main_coverage(int argc, char** argv, int i) {
     return 0;
 }
 
+// `ngsep-amd RelativeAlleleCounts -i BAM [-o OUT] [-r REF] [-minRD N] [-maxRD N] [-minBQ N] [-s]`
+// (RelativeAlleleCountsCalculator.main/run, discovery/RelativeAlleleCountsCalculator.java:175-211):
+// writes to standard output unless -o is given
+static int main_rac(int argc, char** argv, int i) {
+    ngsep_params p;
+    ngsep_params_default(&p);
+    p.relative_allele_counts = 1;
+    p.max_alns_per_start = 1000;            // DEF_MAX_RD
+    const char *in = nullptr, *ref = nullptr, *outp = "-";
+    int device = 0;
+    for (; i < argc; i++) {
+        const char* a = argv[i];
+        const char* v = i + 1 < argc ? argv[i + 1] : nullptr;
+        auto takes = [&](const char* name) { if (std::strcmp(a, name) == 0 && v) { i++; return true; } return false; };
+        if (takes("-i")) in = v;
+        else if (takes("-o")) outp = v;
+        else if (takes("-r")) ref = v;
+        else if (takes("-minRD")) p.rac_min_rd = std::atoi(v);
+        else if (takes("-maxRD")) p.max_alns_per_start = std::atoi(v);
+        else if (takes("-minBQ")) p.rac_min_bq = std::atoi(v);
+        else if (std::strcmp(a, "-s") == 0) p.process_secondary = 1;
+        else if (takes("-device")) device = std::atoi(v);
+        else { std::fprintf(stderr, "unknown or unsupported option %s\n", a); return 2; }
+    }
+    if (!in) {
+        std::fprintf(stderr, "The alignments input file is a required parameter\n"
+                             "usage: ngsep-amd RelativeAlleleCounts -i <alignments.bam> [-o <out.txt>] [-r <reference.fa>] [-minRD N] [-maxRD N] [-minBQ N] [-s]\n");
+        return 2;
+    }
+    ngsep_ctx* c = nullptr;
+    int rc = ngsep_open(device, &p, &c);
+    if (rc == NGSEP_OK && ref) rc = ngsep_load_fasta(c, ref);
+    if (rc == NGSEP_OK) rc = ngsep_rac_bam(c, in, outp);
+    if (rc != NGSEP_OK) { std::fprintf(stderr, "error %d: %s\n", rc, c ? ngsep_last_error(c) : "open failed"); if (c) ngsep_close(c); return 1; }
+    ngsep_close(c);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     ngsep_params p;
     ngsep_params_default(&p);
@@ -138,6 +176,7 @@ int main(int argc, char** argv) {
     int i = 1;
     if (i < argc && std::strcmp(argv[i], "MultisampleVariantsDetector") == 0) return main_mvd(argc, argv, i + 1);
     if (i < argc && std::strcmp(argv[i], "CoverageStats") == 0) return main_coverage(argc, argv, i + 1);
+    if (i < argc && std::strcmp(argv[i], "RelativeAlleleCounts") == 0) return main_rac(argc, argv, i + 1);
     if (i < argc && std::strcmp(argv[i], "SingleSampleVariantsDetector") == 0) i++;
     else if (i < argc && argv[i][0] != '-') { std::fprintf(stderr, "unsupported command %s\n", argv[i]); return usage(argv[0]); }
     for (; i < argc; i++) {

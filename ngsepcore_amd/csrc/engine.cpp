@@ -585,6 +585,25 @@ static int stream_collect(ngsep_ctx* c) {
     st.job->th.join();
     std::unique_ptr<WindowJob> j = std::move(st.job);
     if (j->rc != NGSEP_OK) return set_error(c, j->rc, j->err);
+    if (c->params.relative_allele_counts) {
+        auto& R = c->rac;
+        double np = 0;
+        for (int b = 0; b < 51; b++) {
+            R.prop[b] += (double)j->rac_hist[b];
+            np += (double)j->rac_hist[b];
+            if (j->rac_seq_slot >= 0) R.seq_prop[(size_t)j->rac_seq_slot][(size_t)b] += (double)j->rac_hist[b];
+        }
+        R.prop_count += np;
+        R.prop_sum += j->rac_sum;
+        R.prop_sum_sq += j->rac_sum_sq;
+        for (int b = 0; b < 10; b++) {
+            const double n = (double)j->rac_hist[51 + b], v = (double)(b + 1);
+            R.nall[b] += n;
+            R.nall_count += n;
+            R.nall_sum += n * v;            // (integers: exact in any order)
+            R.nall_sum_sq += n * v * v;
+        }
+    }
     if (c->sites.empty()) c->sites.swap(j->sites);
     else if (!j->sites.empty()) {
         const size_t from = c->sites.size();
@@ -616,7 +635,7 @@ static void stream_launch(ngsep_ctx* c, int64_t w0, int64_t w1) {
     // carved regions: reported whole (clipped to the sequence, merged with what earlier windows reported),
     // applied clipped to the window
     std::vector<std::pair<int64_t, int64_t>> cut;
-    if (!cr.indel_reads.empty()) {
+    if (!cr.indel_reads.empty() && !c->params.relative_allele_counts) {   // (no realigner in that listener chain)
         const int64_t R = (int64_t)cr.max_span + 100;
         while (st.indel_lo < cr.indel_reads.size() && (int64_t)cr.indel_reads[st.indel_lo].second + R < w0) st.indel_lo++;
         std::vector<std::pair<int64_t, int64_t>> whole;
@@ -666,6 +685,7 @@ static void stream_launch(ngsep_ctx* c, int64_t w0, int64_t w1) {
     j->w1 = w1;
     j->max_span = max_span;
     j->carved.swap(cut);
+    j->rac_seq_slot = c->rac.cur_slot;
     const int32_t pad = ((max_span + 63) / 64) * 64;
     const int64_t goff = pad - w0;              // window position p -> global p + goff
     j->reads.resize((size_t)(hi - lo));
@@ -828,6 +848,15 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed) {
             c->contig.seq_id = r.seq_id;
             c->contig.seq_len = (int64_t)c->seq_bases[(size_t)r.seq_id].size();
             c->cur_last = last;
+            if (c->params.relative_allele_counts) {      // onSequenceStart (RelativeAlleleCountsCalculator.java:312-322)
+                if (c->contig.seq_len > 100000) {
+                    c->rac.seq_names.push_back(c->seq_names[(size_t)r.seq_id]);
+                    c->rac.seq_prop.emplace_back(51, 0.0);
+                    c->rac.cur_slot = (int32_t)c->rac.seq_prop.size() - 1;
+                } else {
+                    c->rac.cur_slot = -1;
+                }
+            }
         }
         if (last > c->cur_last) c->cur_last = last;
         // the open same-start group: a lone primary alignment stays an index (no view is built)
@@ -1493,8 +1522,22 @@ static void run_window_job(ngsep_ctx* c, WindowJob* j) {
     c->stats.other_allele_calls += s.h_loff.empty() ? 0 : s.h_loff.back();
     c->stats.layout_ms += std::chrono::duration<double, std::milli>(h1 - h0).count();
     c->stats.upload_ms += std::chrono::duration<double, std::milli>(h2 - h1).count();
-    j->rc = run_device_into(c, j->sites, nullptr);
-    if (j->rc != NGSEP_OK) j->err = c->err;
+    if (c->params.relative_allele_counts) {
+        double ms = 0;
+        std::string e2;
+        if (device_run_rac(c->dev, s, w.gbase + w.pad, w.gbase + w.pad + w.wlen, c->params.rac_min_rd, c->params.rac_min_bq,
+                           j->rac_hist, &j->rac_sum, &j->rac_sum_sq, &ms, e2) != 0) {
+            j->rc = NGSEP_E_DEVICE;
+            j->err = e2;
+        } else {
+            j->rc = NGSEP_OK;
+            c->rac.kernel_ms += ms;
+            c->stats.scan_ms = ms;
+        }
+    } else {
+        j->rc = run_device_into(c, j->sites, nullptr);
+        if (j->rc != NGSEP_OK) j->err = c->err;
+    }
     if (host_timing)
         std::fprintf(stderr, "[ngsep host] window %d:%lld-%lld: layout %.1f ms, upload %.1f ms, run %.1f ms (%lld reads)\n", j->seq_id,
                      (long long)j->w0, (long long)j->w1, std::chrono::duration<double, std::milli>(h1 - h0).count(),
@@ -1772,6 +1815,9 @@ extern "C" void ngsep_params_default(ngsep_params* p) {
     p->prune_candidates = 1;
     p->window_positions = 1 << 26;
     p->max_coverage = 300;
+    p->relative_allele_counts = 0;
+    p->rac_min_rd = 10;                     // RelativeAlleleCountsCalculator.DEF_MIN_RD
+    p->rac_min_bq = 20;                     // DEF_MIN_BASE_QUALITY_SCORE
 }
 
 extern "C" int ngsep_open(int device, const ngsep_params* params, ngsep_ctx** out) {
@@ -1786,6 +1832,13 @@ extern "C" int ngsep_open(int device, const ngsep_params* params, ngsep_ctx** ou
             return set_error(c, NGSEP_E_UNSUPPORTED, "maxCoverage outside [1, 1024] (LDS histograms of the coverage kernel)");
         if (c->params.multisample || c->params.query_seq[0])
             return set_error(c, NGSEP_E_INVALID, "coverage statistics take no samples and no query region");
+    }
+    if (c->params.relative_allele_counts) {
+        *out = c;
+        if (c->params.multisample || c->params.coverage_stats)
+            return set_error(c, NGSEP_E_INVALID, "relative allele counts run alone (no samples, no coverage statistics)");
+        if (c->params.rac_min_bq < 4 || c->params.rac_min_bq > 30)
+            return set_error(c, NGSEP_E_UNSUPPORTED, "minBQ outside [4, 30] (the pile's codes clamp qualities to 30 and drop the base of q <= 3 calls)");
     }
     if (c->params.ploidy >= 3) {
         *out = c;
@@ -1923,6 +1976,87 @@ extern "C" int ngsep_clear_sites(ngsep_ctx* c) {
     return NGSEP_OK;
 }
 
+extern "C" int ngsep_fetch_rac(ngsep_ctx* c, double* prop, double* n_alleles, double* moments) {
+    if (!c) return NGSEP_E_INVALID;
+    if (!c->params.relative_allele_counts) return set_error(c, NGSEP_E_INVALID, "context not in relative-allele-counts mode");
+    const auto& R = c->rac;
+    if (prop) std::memcpy(prop, R.prop, sizeof R.prop);
+    if (n_alleles) std::memcpy(n_alleles, R.nall, sizeof R.nall);
+    if (moments) {
+        moments[0] = R.prop_count; moments[1] = R.prop_sum; moments[2] = R.prop_sum_sq;
+        moments[3] = R.nall_count; moments[4] = R.nall_sum; moments[5] = R.nall_sum_sq;
+    }
+    return NGSEP_OK;
+}
+
+extern "C" int ngsep_clear_rac(ngsep_ctx* c) {
+    if (!c) return NGSEP_E_INVALID;
+    c->rac = {};
+    return NGSEP_OK;
+}
+
+namespace {
+// DecimalFormat("##0.0#") (main/io/ParseUtils.java:29): HALF_EVEN on the double's exact value
+std::string java_fmt2(double x) {
+    const double p = x * 100.0, err = std::fma(x, 100.0, -p);
+    const double k = std::floor(p), fr = p - k;
+    long long n = (long long)k;
+    if (fr > 0.5 || (fr == 0.5 && (err > 0 || (err == 0 && (n & 1))))) n++;
+    char b[64];
+    if (n % 10 == 0) std::snprintf(b, sizeof b, "%lld.%lld", n / 100, (n % 100) / 10);
+    else std::snprintf(b, sizeof b, "%lld.%02lld", n / 100, n % 100);
+    return b;
+}
+// Distribution.printDistribution (math/Distribution.java:301-345) of a distribution with no outliers
+void print_distribution(std::string& o, const double* dist, int nbins, double min, double bin, double max, bool integer,
+                        double count, double sum, double sum_sq) {
+    const int max_idx = (int)((max - min) / bin);
+    for (int i = 0; i < nbins && i <= max_idx; i++) {
+        if (integer) o += std::to_string((int)(min + i * bin)) + "\t" + std::to_string((long long)java_round(dist[i])) + "\n";
+        else o += java_fmt2(min + i * bin) + "\t" + java_fmt2(dist[i]) + "\n";
+    }
+    o += "Count\t" + std::to_string((long long)java_round(count)) + "\n";
+    if (integer) o += "Sum\t" + std::to_string((long long)java_round(sum)) + "\n";
+    else o += "Sum\t" + java_fmt2(sum) + "\n";
+    if (count > 0) o += "Average\t" + java_fmt2(sum / count) + "\n";
+    if (count > 1) {
+        const double var = (sum_sq - sum * sum / count) / (count - 1);
+        o += "Variance\t" + java_fmt2(var) + "\n";
+        o += "STDev\t" + java_fmt2(std::sqrt(var)) + "\n";
+    }
+}
+}  // namespace
+
+// RelativeAlleleCountsCalculator.printResults (discovery/RelativeAlleleCountsCalculator.java:213-244)
+extern "C" int ngsep_write_rac(ngsep_ctx* c, const char* out_path) {
+    if (!c || !out_path) return NGSEP_E_INVALID;
+    if (!c->params.relative_allele_counts) return set_error(c, NGSEP_E_INVALID, "context not in relative-allele-counts mode");
+    const auto& R = c->rac;
+    std::string o;
+    o += "Distribution of allele proportions\n";
+    print_distribution(o, R.prop, 51, 0.0, 0.01, 0.5, false, R.prop_count, R.prop_sum, R.prop_sum_sq);
+    o += "Distribution of number of alleles\n";
+    print_distribution(o, R.nall, 10, 1.0, 1.0, 10.0, true, R.nall_count, R.nall_sum, R.nall_sum_sq);
+    if (!R.seq_names.empty()) {
+        o += "Distribution of allele proportions per sequence\nProportion";
+        for (const auto& n : R.seq_names) o += "\t" + n;
+        o += "\n";
+        double min = 0;
+        for (int b = 0; b < 51; b++) {
+            o += java_fmt2(min);
+            for (const auto& d : R.seq_prop) o += "\t" + java_fmt2(d[(size_t)b]);
+            o += "\n";
+            min += 0.01;
+        }
+    }
+    std::FILE* f = std::strcmp(out_path, "-") == 0 ? stdout : std::fopen(out_path, "w");
+    if (!f) return set_error(c, NGSEP_E_IO, std::string("cannot write ") + out_path);
+    std::fwrite(o.data(), 1, o.size(), f);
+    if (f != stdout) std::fclose(f);
+    else std::fflush(f);
+    return NGSEP_OK;
+}
+
 extern "C" int ngsep_fetch_carved_regions(ngsep_ctx* c, int32_t* seq_id, int64_t* first, int64_t* last, int64_t cap,
                                           int64_t* n_out) {
     if (!c) return NGSEP_E_INVALID;
@@ -1953,6 +2087,10 @@ extern "C" int ngsep_stage_finish(ngsep_ctx* c) {
     c->staging_mode = true;
     int rc = flush_sequence(c);
     if (rc != NGSEP_OK) return rc;
+    if (c->params.relative_allele_counts) {
+        c->staged_contigs.clear();
+        return set_error(c, NGSEP_E_UNSUPPORTED, "relative allele counts run on the streaming paths (ngsep_process_alignments / ngsep_rac_bam)");
+    }
     rc = c->params.coverage_stats ? coverage_stage(c, c->staged_contigs) : build_and_upload(c, c->staged_contigs);
     c->staged_contigs.clear();
     return rc;

@@ -306,6 +306,11 @@ struct WindowJob {
     std::vector<SRead> reads;                               // global coordinates (window at pad)
     std::vector<std::pair<int64_t, int64_t>> carved;        // 1-based, inside [w0, w1]
     SiteStore sites;
+    // RelativeAlleleCounts mode: the window's histograms and proportion sums; its sequence's slot in the
+    // per-sequence distributions (-1: a sequence of <= 100000 bp)
+    unsigned long long rac_hist[61] = {};
+    double rac_sum = 0, rac_sum_sq = 0;
+    int32_t rac_seq_slot = -1;
     int rc = 0;
     std::string err;
     std::atomic<bool> done{false};
@@ -350,6 +355,15 @@ struct ngsep_ctx {
     std::vector<ngsep::ContigReads> staged_contigs;
     ngsep::Staged staged;
     ngsep::LayoutArena arena;
+    // RelativeAlleleCountsCalculator mode (params.relative_allele_counts): its Distributions
+    struct {
+        double prop[51] = {}, prop_count = 0, prop_sum = 0, prop_sum_sq = 0;
+        double nall[10] = {}, nall_count = 0, nall_sum = 0, nall_sum_sq = 0;
+        std::vector<std::string> seq_names;                  // sequences longer than 100000 bp, in order
+        std::vector<std::vector<double>> seq_prop;           // their proportion bins
+        int32_t cur_slot = -1;                               // the current sequence's slot
+        double kernel_ms = 0;
+    } rac;
     // streamed single-sample windows of the current sequence (run_now paths)
     struct {
         int64_t next_w0 = 0;                      // first position not yet handed to a window (0: not started)
@@ -411,6 +425,10 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
                      const std::vector<int8_t>& sample_nrank, double min_adf, int ploidy,
                      std::vector<ngsep_popsite_out>* sites, std::vector<ngsep_sample_call>* calls,
                      double* scan_ms, double* geno_ms, double* total_ms, int64_t* n_candidates, std::string& err);
+// RelativeAlleleCountsCalculator over positions [g0, g1) of the resident single-sample layout: hist_out[0..51)
+// the proportion bins, [51..61) the number-of-alleles bins; the proportion's sum and sum of squares
+int device_run_rac(Device* d, const Staged& s, int64_t g0, int64_t g1, int32_t min_rd, int32_t min_bq,
+                   unsigned long long* hist_out, double* sum, double* sum_sq, double* kernel_ms, std::string& err);
 int64_t device_last_hard(const Device* d);
 int64_t device_last_exact(const Device* d);
 int device_count();

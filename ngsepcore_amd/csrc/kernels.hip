@@ -108,6 +108,8 @@ struct Device {
     ngsep_sample_call* d_pcalls = nullptr;
     int64_t cap_psites = 0;
     unsigned long long* d_stamps = nullptr;   // diagnostics (NGSEP_TIMING)
+    void* d_rac = nullptr;           // RelativeAlleleCounts: histograms + per-block sums (device, pinned host)
+    void* h_rac = nullptr;
     LikTables* d_tables = nullptr;
     int32_t ko_shift = 14, ko_bcap = 64;   // 2^ko_shift positions per bucket (grown on overflow)
     QueueSite* d_hard = nullptr;
@@ -1610,6 +1612,8 @@ void device_destroy(Device* d) {
     if (!d) return;
     device_release(d);
     (void)hipDeviceSynchronize();
+    (void)hipFree(d->d_rac);
+    if (d->h_rac) (void)hipHostFree(d->h_rac);
     for (auto& sl : d->slot) {
         (void)hipFree(sl.d_brec);
         (void)hipFree(sl.d_bcount);
@@ -1933,6 +1937,120 @@ int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypePar
     }
     if (device_submit(d, s, t, g, prune, err) != 0) return -1;
     return device_collect(d, out, n_out, scan_ms, geno_ms, total_ms, n_candidates, err);
+}
+
+// ------------------------------------------------------------------------------------------
+// KR: RelativeAlleleCountsCalculator.onPileup (discovery/RelativeAlleleCountsCalculator.java:246-294) over
+// every position of the run's window -- one lane per position, its column of the position-major byte pile
+// (the rows of the reads covering it, rank order).  A nonzero code is an allele call of getAlleleCalls(1);
+// a call of quality >= minBaseQualityScore counts for its base (A, C, G, T from a valid code, any other
+// character as 'N' from a counted one: min_bq is in [4, 30], so the code's clamped quality decides it and
+// q <= 3 calls, whose base the code drops, never count).  Positions with >= minRD calls and >= 1 counted
+// allele add their number of alleles and the proportion of the second most frequent allele (TreeMap order
+// A < C < G < N < T, strict maxima) to the histograms of math.Distribution (bins (int)((v - min) / len)).
+// The proportion's sums are kept per block in grid-stride order (the host adds the blocks in order).
+// ------------------------------------------------------------------------------------------
+constexpr int kRacThreads = 256;
+constexpr int kRacBlocks = 1024;
+constexpr int kRacPropBins = 51, kRacNallBins = 10;
+__global__ __launch_bounds__(kRacThreads) void k_rac(const uint8_t* __restrict__ cpile, const TileInfo* __restrict__ tinfo,
+                                                     int32_t log2T, int64_t g0, int64_t g1, int32_t min_rd, int32_t min_bq,
+                                                     unsigned long long* __restrict__ hist, double* __restrict__ part) {
+    __shared__ uint32_t s_h[kRacPropBins + kRacNallBins];
+    __shared__ double s_sum[kRacThreads], s_sq[kRacThreads];
+    for (int i = threadIdx.x; i < kRacPropBins + kRacNallBins; i += kRacThreads) s_h[i] = 0;
+    __syncthreads();
+    const int32_t Tm = (1 << log2T) - 1;
+    double sum = 0, sq = 0;
+    for (int64_t g = g0 + (int64_t)blockIdx.x * kRacThreads + threadIdx.x; g < g1; g += (int64_t)gridDim.x * kRacThreads) {
+        const TileInfo ti = tinfo[g >> log2T];
+        const int32_t rows = ti.rows;
+        if (rows == 0) continue;
+        const int64_t base = ti.off + (int64_t)(g & Tm) * rows;
+        const int64_t c0 = base & ~(int64_t)3;
+        const uint32_t* cw = reinterpret_cast<const uint32_t*>(cpile) + (c0 >> 2);
+        const int sh = (int)(base - c0);
+        const int nd = (rows + sh + 3) >> 2;
+        int32_t calls = 0, cA = 0, cC = 0, cG = 0, cT = 0, cN = 0;
+        for (int k = 0; k < nd; k++) {
+            const uint32_t d = cw[k];
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int r = 4 * k + e - sh;
+                const uint32_t cd = (r >= 0 && r < rows) ? (d >> (8 * e)) & 0xFFu : 0u;
+                if (cd == 0) continue;
+                calls++;
+                if ((int32_t)(cd & 31u) < min_bq) continue;
+                if (cd & 0x80u) {
+                    const uint32_t a = (cd >> 5) & 3u;
+                    cA += a == 0; cC += a == 1; cG += a == 2; cT += a == 3;
+                } else {
+                    cN++;
+                }
+            }
+        }
+        if (calls < min_rd) continue;
+        const int32_t c[5] = {cA, cC, cG, cN, cT};      // TreeMap<String> order
+        int32_t nz = 0, mx = -1, mc = -1;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            nz += c[k] > 0;
+            if (c[k] > 0 && (mx < 0 || mc < c[k])) { mx = k; mc = c[k]; }
+        }
+        if (nz == 0) continue;
+        atomicAdd(&s_h[kRacPropBins + (int)((double)(nz - 1) / 1.0)], 1u);
+        int32_t s2 = -1, sc = 0;
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+            if (k != mx && c[k] > 0 && (s2 < 0 || sc < c[k])) { s2 = k; sc = c[k]; }
+        const double prop = (double)sc / (double)(mc + sc);
+        atomicAdd(&s_h[(int)((prop - 0.0) / 0.01)], 1u);
+        sum += prop;
+        sq += prop * prop;
+    }
+    s_sum[threadIdx.x] = sum;
+    s_sq[threadIdx.x] = sq;
+    __syncthreads();
+    if (threadIdx.x == 0) {                          // the block's partial sums in thread order
+        double a = 0, b = 0;
+        for (int i = 0; i < kRacThreads; i++) { a += s_sum[i]; b += s_sq[i]; }
+        part[2 * blockIdx.x] = a;
+        part[2 * blockIdx.x + 1] = b;
+    }
+    for (int i = threadIdx.x; i < kRacPropBins + kRacNallBins; i += kRacThreads)
+        if (s_h[i]) atomicAdd(&hist[i], (unsigned long long)s_h[i]);
+}
+
+// one RelativeAlleleCounts pass over positions [g0, g1) of the resident single-sample layout: the 51 + 10
+// histogram counts, the proportion's sum and sum of squares (blocks added in order)
+int device_run_rac(Device* d, const Staged& s, int64_t g0, int64_t g1, int32_t min_rd, int32_t min_bq,
+                   unsigned long long* hist_out, double* sum, double* sum_sq, double* kernel_ms, std::string& err) {
+    HIP_TRY(hipSetDevice(d->ordinal));
+    if (!s.single || !d->d_pile || !d->d_tinfo) { err = "no single-sample layout resident"; return -1; }
+    if (g0 < 0 || g1 > s.g_len || g1 < g0 || (g1 > 0 && ((g1 - 1) >> d->log2_tile) >= d->n_tiles)) { err = "position range outside the layout"; return -1; }
+    if (!d->d_rac) {
+        HIP_TRY(hipMalloc(&d->d_rac, 64 * sizeof(unsigned long long) + 2 * kRacBlocks * sizeof(double)));
+        HIP_TRY(hipHostMalloc(&d->h_rac, 64 * sizeof(unsigned long long) + 2 * kRacBlocks * sizeof(double), hipHostMallocDefault));
+    }
+    unsigned long long* hist = reinterpret_cast<unsigned long long*>(d->d_rac);
+    double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(d->d_rac) + 64 * sizeof(unsigned long long));
+    HIP_TRY(hipMemsetAsync(d->d_rac, 0, 64 * sizeof(unsigned long long), d->stream));
+    hipExtLaunchKernelGGL(k_rac, dim3(kRacBlocks), dim3(kRacThreads), 0, d->stream, d->ev[0], d->ev[1], 0,
+                          (const uint8_t*)d->d_pile, (const TileInfo*)d->d_tinfo, d->log2_tile, g0, g1, min_rd, min_bq, hist, part);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(d->h_rac, d->d_rac, 64 * sizeof(unsigned long long) + 2 * kRacBlocks * sizeof(double), hipMemcpyDeviceToHost, d->stream));
+    HIP_TRY(hipStreamSynchronize(d->stream));
+    const unsigned long long* hh = reinterpret_cast<const unsigned long long*>(d->h_rac);
+    const double* pp = reinterpret_cast<const double*>(reinterpret_cast<const char*>(d->h_rac) + 64 * sizeof(unsigned long long));
+    for (int i = 0; i < kRacPropBins + kRacNallBins; i++) hist_out[i] = hh[i];
+    double a = 0, b = 0;
+    for (int i = 0; i < kRacBlocks; i++) { a += pp[2 * i]; b += pp[2 * i + 1]; }
+    *sum = a;
+    *sum_sq = b;
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, d->ev[0], d->ev[1]);
+    *kernel_ms = ms;
+    return 0;
 }
 
 // MultisampleVariantsDetector run: KTM over every resident tile, KPM over the queued positions,

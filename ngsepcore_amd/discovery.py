@@ -519,3 +519,76 @@ class CoverageStatisticsCalculator:
         if out is not None:
             out.write(txt)
         return txt
+
+
+class RelativeAlleleCountsCalculator:
+    """Drop-in for ngsep.discovery.RelativeAlleleCountsCalculator (discovery/RelativeAlleleCountsCalculator.java:
+    26-331; command RelativeAlleleCounts, main/CommandsDescriptor.xml): the distributions of the proportion of
+    the second most frequent allele and of the number of alleles over the pileups, the per-position loop on the
+    GPU (kernels.hip k_rac over the streamed windows' byte pile)."""
+
+    DEF_MIN_RD = 10
+    DEF_MAX_RD = 1000
+    DEF_MIN_BASE_QUALITY_SCORE = 20
+
+    def __init__(self):
+        self.params = default_params()
+        self.params.relative_allele_counts = 1
+        self.params.rac_min_rd = self.DEF_MIN_RD
+        self.params.rac_min_bq = self.DEF_MIN_BASE_QUALITY_SCORE
+        self.params.max_alns_per_start = self.DEF_MAX_RD       # runProcess: generator.setMaxAlnsPerStartPos(maxRD)
+        self.params.process_secondary = 0
+        self.inputFile: Optional[str] = None
+        self.outputFile: Optional[str] = None
+        self.genomeFile: Optional[str] = None
+        self.device = 0
+        self.proportions: List[float] = []
+        self.numAlleles: List[float] = []
+        self.moments: List[float] = []
+
+    def setInputFile(self, v: str): self.inputFile = v
+    def setOutputFile(self, v: str): self.outputFile = v
+    def setGenome(self, v: str): self.genomeFile = v
+    def setMinRD(self, v: int): self.params.rac_min_rd = int(v)
+    def getMinRD(self) -> int: return self.params.rac_min_rd
+    def setMaxRD(self, v: int): self.params.max_alns_per_start = int(v)
+    def getMaxRD(self) -> int: return self.params.max_alns_per_start
+    def setMinBaseQualityScore(self, v: int): self.params.rac_min_bq = int(v)
+    def getMinBaseQualityScore(self) -> int: return self.params.rac_min_bq
+    def setSecondaryAlns(self, v: bool): self.params.process_secondary = 1 if v else 0
+    def isSecondaryAlns(self) -> bool: return bool(self.params.process_secondary)
+
+    def _session(self) -> GpuPileupSession:
+        s = GpuPileupSession(self.params, self.device)
+        if self.genomeFile is not None:
+            s.load_fasta(self.genomeFile)
+        return s
+
+    def _collect(self, s: GpuPileupSession):
+        p, n, m = (ctypes.c_double * 51)(), (ctypes.c_double * 10)(), (ctypes.c_double * 6)()
+        s._check(s._lib.ngsep_fetch_rac(s._ctx, p, n, m))
+        self.proportions, self.numAlleles, self.moments = list(p), list(n), list(m)
+
+    def run(self):
+        if self.inputFile is None:
+            raise NgsepError(_lib.NGSEP_E_IO, "The alignments input file is a required parameter")
+        self.runProcess(self.inputFile, self.outputFile or "-")
+
+    def runProcess(self, filename: str, out_path: Optional[str] = None):
+        """runProcess + printResults (:183-244): BAM -> distributions -> report text (out_path; None = no text)."""
+        with self._session() as s:
+            s._check(s._lib.ngsep_rac_bam(s._ctx, filename.encode(), out_path.encode() if out_path else None))
+            self._collect(s)
+
+    def processBatches(self, batches, contigs=None, out_path: Optional[str] = None):
+        """Path A: reader-filtered alignment batches (the generator's input) -> distributions."""
+        with self._session() as s:
+            if contigs is not None:
+                for name, seq in contigs:
+                    s.set_reference(name, seq)
+            for b in batches:
+                s.processAlignments(b)
+            s.notifyEndOfAlignments()
+            self._collect(s)
+            if out_path:
+                s._check(s._lib.ngsep_write_rac(s._ctx, out_path.encode()))

@@ -631,7 +631,133 @@ typedef struct {
     ngo_stats* st;
     int unsupported;
     ngo_coverage* cov;         /* CoverageStatisticsCalculator listener instead of the variant listeners */
+    struct ngo_rac* rac;       /* RelativeAlleleCountsCalculator listener instead of the variant listeners */
 } ngo_gen;
+
+/* ------------------------------------------------------------------ */
+/* RelativeAlleleCountsCalculator (discovery/RelativeAlleleCountsCalculator.java:246-331) with the     */
+/* math.Distribution it fills (math/Distribution.java:52-93,301-345)                                    */
+/* ------------------------------------------------------------------ */
+#define RAC_PROP_BINS 51           /* Distribution(0, 0.5, 0.01): (int)((0.5 - 0) / 0.01) + 1 */
+#define RAC_NALL_BINS 10           /* Distribution(1, 10, 1) */
+typedef struct {
+    double dist[RAC_PROP_BINS];
+    double sum, sum_sq, count;
+} rac_dist;
+typedef struct ngo_rac {
+    int min_rd, min_bq;
+    rac_dist prop;
+    double nall[RAC_NALL_BINS], nall_sum, nall_sum_sq, nall_count;
+    int n_seq;                     /* sequences longer than 100000 bp (onSequenceStart, :312-322) */
+    char** seq_names;
+    rac_dist* seq_dist;
+    rac_dist* cur;                 /* currentSequencePropDist (NULL for short sequences) */
+    int64_t covered;               /* coveredGenomeSize */
+} ngo_rac;
+
+/* Distribution.processDatapoint(1, value) for the bins that cannot overflow here */
+static void rac_point(rac_dist* d, double v) {
+    d->sum += v;
+    d->sum_sq += v * v;
+    d->count += 1;
+    d->dist[(int)((v - 0.0) / 0.01)] += 1;
+}
+
+/* onPileup (:246-294): calls = getAlleleCalls(1); alleles counted by their character when the call's
+ * quality is >= minBaseQualityScore; the proportion of the second most frequent allele among the two
+ * most frequent ones (TreeMap order, strict maxima: the first of equal counts wins, :296-308) */
+static void rac_on_pileup(ngo_gen* G, int pos) {
+    ngo_rac* R = G->rac;
+    int ncalls = 0;
+    int cnt[256];
+    memset(cnt, 0, sizeof(cnt));
+    for (int k = 0; k < G->pending.n; k++) {
+        ngo_aln* a = G->pending.a[k];
+        if (a->first > pos || a->last < pos) continue;
+        if (!a->chars) continue;
+        int rp = aligned_read_pos(a, pos);
+        if (rp < 0) continue;
+        if (a->acl[rp] != 1) continue;                  /* PileupRecord.getAlleleCalls(1), :126-152 */
+        ncalls++;
+        int qc = a->quals ? a->quals[rp] : '+';          /* getQualityScores: '+' without qualities */
+        int qs = (int)(int8_t)(uint8_t)qc - 33;
+        if (qs >= R->min_bq) cnt[(uint8_t)a->chars[rp]]++;
+    }
+    if (ncalls < R->min_rd) return;
+    int n_all = 0;
+    for (int c = 0; c < 256; c++) n_all += cnt[c] > 0;
+    if (n_all == 0) return;
+    {   /* distNumAlleles.processDatapoint(alleleCounts.size()) */
+        double v = n_all;
+        R->nall_sum += v; R->nall_sum_sq += v * v; R->nall_count += 1;
+        R->nall[(int)((v - 1.0) / 1.0)] += 1;
+    }
+    int mx = -1, mc = -1;                               /* TreeMap iteration: ascending characters */
+    for (int c = 0; c < 256; c++) if (cnt[c] > 0 && (mx < 0 || mc < cnt[c])) { mx = c; mc = cnt[c]; }
+    int sc = 0, s2 = -1;
+    for (int c = 0; c < 256; c++) if (c != mx && cnt[c] > 0 && (s2 < 0 || sc < cnt[c])) { s2 = c; sc = cnt[c]; }
+    if (mc > 0) {
+        double prop = (double)sc / (mc + sc);
+        rac_point(&R->prop, prop);
+        if (R->cur) rac_point(R->cur, prop);
+    }
+    R->covered++;
+}
+
+static void rac_on_sequence_start(ngo_gen* G, int seq) {
+    ngo_rac* R = G->rac;
+    if (G->g->s[seq].len > 100000) {
+        R->seq_names = realloc(R->seq_names, sizeof(char*) * (R->n_seq + 1));
+        R->seq_dist = realloc(R->seq_dist, sizeof(rac_dist) * (R->n_seq + 1));
+        R->seq_names[R->n_seq] = G->g->s[seq].name;
+        memset(&R->seq_dist[R->n_seq], 0, sizeof(rac_dist));
+        R->n_seq++;
+        R->cur = &R->seq_dist[R->n_seq - 1];
+    } else {
+        R->cur = NULL;
+    }
+}
+
+static void rac_fmt(FILE* out, double x) { char b[64]; ngo_java_fmt2(x, b, sizeof b); fputs(b, out); }
+
+/* Distribution.printDistribution (:301-345) of a distribution with no outliers */
+static void rac_print_dist(FILE* out, const double* dist, int nbins, double min, double bin, double max, int integer,
+                           double count, double sum, double sum_sq) {
+    int maxIdx = (int)((max - min) / bin);
+    for (int i = 0; i < nbins && i <= maxIdx; i++) {
+        if (integer) fprintf(out, "%d\t%lld\n", (int)(min + i * bin), (long long)ngo_java_round(dist[i]));
+        else { rac_fmt(out, min + i * bin); fputc('\t', out); rac_fmt(out, dist[i]); fputc('\n', out); }
+    }
+    fprintf(out, "Count\t%lld\n", (long long)ngo_java_round(count));
+    if (integer) fprintf(out, "Sum\t%lld\n", (long long)ngo_java_round(sum));
+    else { fputs("Sum\t", out); rac_fmt(out, sum); fputc('\n', out); }
+    if (count > 0) { fputs("Average\t", out); rac_fmt(out, sum / count); fputc('\n', out); }
+    if (count > 1) {
+        double var = (sum_sq - sum * sum / count) / (count - 1);
+        fputs("Variance\t", out); rac_fmt(out, var); fputc('\n', out);
+        fputs("STDev\t", out); rac_fmt(out, sqrt(var)); fputc('\n', out);
+    }
+}
+
+/* printResults (:213-244) */
+static void rac_print(FILE* out, const ngo_rac* R) {
+    fprintf(out, "Distribution of allele proportions\n");
+    rac_print_dist(out, R->prop.dist, RAC_PROP_BINS, 0.0, 0.01, 0.5, 0, R->prop.count, R->prop.sum, R->prop.sum_sq);
+    fprintf(out, "Distribution of number of alleles\n");
+    rac_print_dist(out, R->nall, RAC_NALL_BINS, 1.0, 1.0, 10.0, 1, R->nall_count, R->nall_sum, R->nall_sum_sq);
+    if (R->n_seq == 0) return;
+    fprintf(out, "Distribution of allele proportions per sequence\n");
+    fprintf(out, "Proportion");
+    for (int i = 0; i < R->n_seq; i++) fprintf(out, "\t%s", R->seq_names[i]);
+    fputc('\n', out);
+    double min = 0;
+    for (int b = 0; b < RAC_PROP_BINS; b++) {
+        rac_fmt(out, min);
+        for (int i = 0; i < R->n_seq; i++) { fputc('\t', out); rac_fmt(out, R->seq_dist[i].dist[b]); }
+        fputc('\n', out);
+        min += 0.01;
+    }
+}
 
 static void on_sequence_end(ngo_gen* G) {
     /* SingleSampleVariantsDetector.saveSequenceVariants, :933-968: calls are already in position order */
@@ -1005,6 +1131,17 @@ static int process_current_position(ngo_gen* G) {
         G->cur_pos++;
         return numAlignments > 0;
     }
+    if (G->rac) {
+        int numAlignments = 0;
+        for (int k = 0; k < G->pending.n; k++)
+            if (G->pending.a[k]->first <= pos && G->pending.a[k]->last >= pos) numAlignments++;
+        if (numAlignments > 0) {
+            G->st->positions_genotyped++;
+            rac_on_pileup(G, pos);
+        }
+        G->cur_pos++;
+        return numAlignments > 0;
+    }
     if (G->mvd) {
         int numAlignments = 0;
         for (int k = 0; k < G->pending.n; k++)
@@ -1124,6 +1261,7 @@ static void process_alignment(ngo_gen* G, ngo_aln* a) {
     }
     if (G->cur_seq < 0) {   /* startSequence, :435-444 */
         G->cur_seq = a->seq; G->cur_pos = a->first; G->cur_last = a->last;
+        if (G->rac) rac_on_sequence_start(G, a->seq);
     }
     if (a->last > G->cur_last) G->cur_last = a->last;
     if (a->flags & FLAG_SECONDARY) alist_push(&G->ss_secondary, a);
@@ -1152,7 +1290,7 @@ static char* split_tab(char** s) {
 
 static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
                         const char* dump_path, const ngo_params* p, ngo_stats* stats, double min_adf, int multisample,
-                        ngo_coverage* cov) {
+                        ngo_coverage* cov, ngo_rac* rac) {
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     ngo_stats st_local; ngo_stats* st = stats ? stats : &st_local;
@@ -1172,7 +1310,8 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
     G.het_rate = p->het_rate;
     if (!multisample && !p->het_rate_set && p->ploidy == 1) G.het_rate = 1e-6;
     G.cov = cov;
-    if (!multisample && !cov) print_header(out, p);
+    G.rac = rac;
+    if (!multisample && !cov && !rac) print_header(out, p);
     ngo_mvd M; memset(&M, 0, sizeof(M));
     ngo_strlist rg_sm = {0};       /* SM of each @RG (parallel to rgs) */
     int header_done = !multisample;
@@ -1315,7 +1454,7 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
             } else if (query_found) { aln_free(a); break; }
             else { aln_free(a); continue; }
         }
-        if (a->has_indel && !cov && !p->indel_passthrough) { G.unsupported = 1; aln_free(a); rc = NGO_UNSUPPORTED; break; }
+        if (a->has_indel && !cov && !rac && !p->indel_passthrough) { G.unsupported = 1; aln_free(a); rc = NGO_UNSUPPORTED; break; }
         process_alignment(&G, a);
     }
     if (multisample && !header_done) { header_done = 1; print_header_samples(out, p, NULL, 0); }
@@ -1326,6 +1465,7 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
             fprintf(out, "%d\t%lld\t%lld\n", i, (long long)cov->counts[i], (long long)cov->counts_unique[i]);
         fprintf(out, "More\t%lld\t%lld\n", (long long)cov->high, (long long)cov->high_unique);
     }
+    if (rc == NGO_OK && rac) rac_print(out, rac);
     free(line); free(last_qname); fclose(in);
     if (out != stdout) fclose(out); else fflush(out);
     if (dump) fclose(dump);
@@ -1350,7 +1490,7 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
 
 int ngo_run_ssvd(const char* fasta, const char* sam, const char* out_vcf,
                  const char* dump_path, const ngo_params* p, ngo_stats* stats) {
-    return run_detector(fasta, sam, out_vcf, dump_path, p, stats, 0.0, 0, NULL);
+    return run_detector(fasta, sam, out_vcf, dump_path, p, stats, 0.0, 0, NULL, NULL);
 }
 
 /* MultisampleVariantsDetector.run (discovery/MultisampleVariantsDetector.java:421-459) on one SAM
@@ -1358,7 +1498,7 @@ int ngo_run_ssvd(const char* fasta, const char* sam, const char* out_vcf,
 int ngo_run_mvd(const char* fasta, const char* sam, const char* out_vcf, const ngo_params* p,
                 double min_allele_depth_freq, ngo_stats* stats) {
     if (p->ploidy >= 3) return NGO_UNSUPPORTED;
-    return run_detector(fasta, sam, out_vcf, NULL, p, stats, min_allele_depth_freq, 1, NULL);
+    return run_detector(fasta, sam, out_vcf, NULL, p, stats, min_allele_depth_freq, 1, NULL, NULL);
 }
 
 /* CoverageStatisticsCalculator.processFile (discovery/CoverageStatisticsCalculator.java:108-122): the
@@ -1378,11 +1518,30 @@ int ngo_run_coverage(const char* fasta, const char* sam, const char* out_txt, in
     cv.max_coverage = max_coverage;
     cv.counts = calloc(max_coverage, sizeof(int64_t));
     cv.counts_unique = calloc(max_coverage, sizeof(int64_t));
-    int rc = run_detector(fasta, sam, out_txt, NULL, &p, stats, 0.0, 0, &cv);
+    int rc = run_detector(fasta, sam, out_txt, NULL, &p, stats, 0.0, 0, &cv, NULL);
     if (counts) memcpy(counts, cv.counts, sizeof(int64_t) * max_coverage);
     if (counts_unique) memcpy(counts_unique, cv.counts_unique, sizeof(int64_t) * max_coverage);
     if (high) *high = cv.high;
     if (high_unique) *high_unique = cv.high_unique;
     free(cv.counts); free(cv.counts_unique);
+    return rc;
+}
+
+/* RelativeAlleleCountsCalculator.runProcess + printResults (discovery/RelativeAlleleCountsCalculator.java:183-244):
+ * the generator with maxAlnsPerStartPos = maxRD and processSecondaryAlignments = secondaryAlns, default
+ * minMQ; reads with indels are admitted (no realigner in this listener chain). */
+int ngo_run_rac(const char* fasta, const char* sam, const char* out_txt, int min_rd, int max_rd, int min_bq,
+                int secondary, ngo_stats* stats) {
+    ngo_params p;
+    ngo_params_default(&p);
+    p.max_alns_per_start = max_rd;
+    p.process_secondary = secondary;
+    ngo_rac R;
+    memset(&R, 0, sizeof(R));
+    R.min_rd = min_rd;
+    R.min_bq = min_bq;
+    int rc = run_detector(fasta, sam, out_txt, NULL, &p, stats, 0.0, 0, NULL, &R);
+    free(R.seq_names);
+    free(R.seq_dist);
     return rc;
 }

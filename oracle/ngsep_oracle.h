@@ -115,6 +115,11 @@ typedef struct ngo_coverage {
 int ngo_run_coverage(const char* fasta, const char* sam, const char* out_txt, int min_mq, int max_coverage,
                      int64_t* counts, int64_t* counts_unique, int64_t* high, int64_t* high_unique, ngo_stats* stats);
 
+/* RelativeAlleleCountsCalculator (discovery/RelativeAlleleCountsCalculator.java:183-331): printResults' text
+ * into out_txt ("-" = stdout).  Defaults: min_rd 10, max_rd 1000 (maxAlnsPerStartPos), min_bq 20. */
+int ngo_run_rac(const char* fasta, const char* sam, const char* out_txt, int min_rd, int max_rd, int min_bq,
+                int secondary, ngo_stats* stats);
+
 /* DecimalFormat("##0.0#") with HALF_EVEN (main/io/ParseUtils.java:29) */
 int ngo_java_fmt2(double x, char* buf, int cap);
 /* INFO of a population record: NS, AN, AFS, OH, MAF (biallelic) from the calls' (n_called, called[2], acn[4]) */

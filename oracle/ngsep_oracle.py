@@ -73,6 +73,8 @@ def lib():
                                        ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                                        ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                                        ctypes.POINTER(OracleStats)]
+        l.ngo_run_rac.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_int, ctypes.POINTER(OracleStats)]
         _lib = l
     return _lib
 
@@ -159,3 +161,15 @@ def run_coverage(fasta: str, sam: str, out_txt: str, min_mq: int = 20, max_cover
     if rc != 0:
         raise RuntimeError(f"oracle failed rc={rc}")
     return list(c), list(u), hi.value, hu.value, st
+
+
+def run_rac(fasta: str, sam: str, out_txt: str, min_rd: int = 10, max_rd: int = 1000, min_bq: int = 20,
+            secondary: int = 0) -> OracleStats:
+    """RelativeAlleleCountsCalculator restatement (discovery/RelativeAlleleCountsCalculator.java:183-331):
+    printResults' text into out_txt."""
+    st = OracleStats()
+    rc = lib().ngo_run_rac(fasta.encode(), sam.encode(), out_txt.encode(), min_rd, max_rd, min_bq, secondary,
+                           ctypes.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"oracle failed rc={rc}")
+    return st
