@@ -170,6 +170,13 @@ typedef struct ngsep_stats {
     int64_t other_allele_calls;     /* entries of the scan's other-allele lists (valid non-reference calls) */
 } ngsep_stats;
 
+/* ---- -knownVariants (SingleSampleVariantsDetector.findSNVS :896-906) ---- */
+/* Genotype the biallelic SNVs of this VCF at their covered positions instead of discovering variants
+ * (SingleSampleVariantPileupListener.onPileup with input variants, :158-176; genotypeSNV): every input
+ * variant with a pileup gets a record (hom-ref, het, hom-alt or undecided, QUAL = its input QUAL, ID kept).
+ * Call after the reference is loaded; NULL or "" returns to discovery.  Other variant types: E_UNSUPPORTED. */
+int  ngsep_set_known_variants(ngsep_ctx* c, const char* vcf_path);
+
 /* ---- RelativeAlleleCountsCalculator (params.relative_allele_counts) ---- */
 /* RelativeAlleleCountsCalculator.runProcess + printResults (:183-244) on a BAM: the report text to out_path */
 int  ngsep_rac_bam(ngsep_ctx* c, const char* bam_path, const char* out_path);

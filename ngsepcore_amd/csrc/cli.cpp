@@ -36,7 +36,7 @@ static int usage(const char* argv0) {
                  "usage: %s SingleSampleVariantsDetector -i <alignments.bam> -r <reference.fa> -o <output prefix> [options]\n"
                  "options: -sampleId S -ploidy N -psp -minMQ N -maxAlnsPerStartPos N -p -s -ignore5 N -ignore3 N\n"
                  "         -h RATE -maxBaseQS N -minQuality N -ignoreLowerCaseRef -embeddedSNVs -csb\n"
-                 "         -querySeq SEQ -first N -last N -device N\n", argv0);
+                 "         -querySeq SEQ -first N -last N -knownVariants VCF -device N\n", argv0);
     return 2;
 }
 
@@ -171,7 +171,7 @@ static int main_rac(int argc, char** argv, int i) {
 int main(int argc, char** argv) {
     ngsep_params p;
     ngsep_params_default(&p);
-    const char *in = nullptr, *ref = nullptr, *outp = nullptr;
+    const char *in = nullptr, *ref = nullptr, *outp = nullptr, *known = nullptr;
     int device = 0;
     int i = 1;
     if (i < argc && std::strcmp(argv[i], "MultisampleVariantsDetector") == 0) return main_mvd(argc, argv, i + 1);
@@ -199,6 +199,7 @@ int main(int argc, char** argv) {
         else if (takes("-first")) p.query_first = std::atoi(v);
         else if (takes("-last")) p.query_last = std::atoi(v);
         else if (takes("-device")) device = std::atoi(v);
+        else if (takes("-knownVariants")) known = v;
         else if (!std::strcmp(a, "-psp")) p.print_sample_ploidy = 1;
         else if (!std::strcmp(a, "-p")) p.process_nonunique = 1;
         else if (!std::strcmp(a, "-s")) p.process_secondary = 1;
@@ -212,6 +213,7 @@ int main(int argc, char** argv) {
     int rc = ngsep_open(device, &p, &c);
     if (rc != NGSEP_OK) { std::fprintf(stderr, "error: %s\n", c ? ngsep_last_error(c) : "open failed"); return 1; }
     rc = ngsep_load_fasta(c, ref);
+    if (rc == NGSEP_OK && known) rc = ngsep_set_known_variants(c, known);
     std::string vcf = std::string(outp) + ".vcf";
     if (rc == NGSEP_OK) rc = ngsep_call_bam(c, in, vcf.c_str());
     if (rc != NGSEP_OK) { std::fprintf(stderr, "error %d: %s\n", rc, ngsep_last_error(c)); ngsep_close(c); return 1; }

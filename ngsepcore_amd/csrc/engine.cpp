@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstring>
 #include <chrono>
+#include <unordered_map>
 #include <cstdlib>
 #include <fstream>
 #include <functional>
@@ -604,6 +605,30 @@ static int stream_collect(ngsep_ctx* c) {
             R.nall_sum_sq += n * v * v;
         }
     }
+    if (!c->known.empty() && !j->sites.empty()) {
+        // the input variant of every record (sequence, position, ALT): its QS, and input order at a shared position
+        const int64_t kb = c->known_seq_begin[(size_t)j->seq_id], ke = c->known_seq_begin[(size_t)j->seq_id + 1];
+        std::vector<int64_t> kidx(j->sites.size());
+        std::vector<int64_t> taken;                    // known entries already matched at the current position
+        for (size_t i = 0; i < j->sites.size(); i++) {
+            ngsep_site_out& o = j->sites[i];
+            if (i == 0 || j->sites[i - 1].pos != o.pos) taken.clear();
+            auto it = std::lower_bound(c->known.begin() + kb, c->known.begin() + ke, (int64_t)o.pos,
+                                       [](const ngsep_ctx::KnownVar& v, int64_t p) { return v.pos < p; });
+            int64_t k = it - c->known.begin();
+            while (k < ke && c->known[(size_t)k].pos == o.pos &&
+                   (c->known[(size_t)k].alt != o.alt || std::find(taken.begin(), taken.end(), k) != taken.end()))
+                k++;
+            taken.push_back(k);
+            kidx[i] = k;
+            if (k < ke) o.qual = c->known[(size_t)k].qs;
+        }
+        for (size_t i = 1; i < j->sites.size(); i++)            // (records at one position: input order)
+            for (size_t k = i; k > 0 && j->sites[k - 1].pos == j->sites[k].pos && kidx[k - 1] > kidx[k]; k--) {
+                std::swap(j->sites[k - 1], j->sites[k]);
+                std::swap(kidx[k - 1], kidx[k]);
+            }
+    }
     if (c->sites.empty()) c->sites.swap(j->sites);
     else if (!j->sites.empty()) {
         const size_t from = c->sites.size();
@@ -680,6 +705,26 @@ static void stream_launch(ngsep_ctx* c, int64_t w0, int64_t w1) {
     }
     if (hi <= lo) return;                       // no read reaches the window: nothing to call
     auto j = std::make_unique<WindowJob>();
+    if (!c->known.empty()) {
+        // -knownVariants: the window's input variants at positions with a pileup (onPileup, :158-176), outside
+        // the carved regions; queue code 0x80 | ref << 5 | alt << 8 | 0x400 (kernels.hip k_posterior)
+        const int32_t pad_k = ((max_span + 63) / 64) * 64;
+        const int64_t goff_k = pad_k - w0;
+        const int64_t kb = c->known_seq_begin[(size_t)cr.seq_id], ke = c->known_seq_begin[(size_t)cr.seq_id + 1];
+        auto it = std::lower_bound(c->known.begin() + kb, c->known.begin() + ke, w0,
+                                   [](const ngsep_ctx::KnownVar& v, int64_t p) { return v.pos < p; });
+        size_t r = (size_t)lo, ci = 0;
+        int64_t maxlast = INT64_MIN;
+        for (; it != c->known.begin() + ke && it->pos <= w1; ++it) {
+            const int64_t p = it->pos;
+            while (r < (size_t)hi && cr.first[r] <= p) { maxlast = std::max<int64_t>(maxlast, cr.last[r]); r++; }
+            if (maxlast < p) continue;                                    // no pileup here
+            while (ci < cut.size() && cut[ci].second < p) ci++;
+            if (ci < cut.size() && cut[ci].first <= p) continue;          // carved: the caller's own path
+            j->forced.push_back((int32_t)(p + goff_k));
+            j->forced.push_back(0x80 | (it->ref << 5) | (it->alt << 8) | 0x400);
+        }
+    }
     j->seq_id = cr.seq_id;
     j->w0 = w0;
     j->w1 = w1;
@@ -1492,6 +1537,11 @@ static void run_window_job(ngsep_ctx* c, WindowJob* j) {
     s.h_ref.assign((size_t)s.g_len, 0);
     fill_ref_codes(c, s, w, j->carved);
     s.single = true;
+    s.known = !c->known.empty();
+    if (s.known) {
+        s.h_forced.swap(j->forced);
+        s.h_forced_ctr[2] = (unsigned long long)(s.h_forced.size() / 2);
+    }
     s.n_reads = (int64_t)j->reads.size();
     int64_t nb = 0;
     for (const SRead& r : j->reads) nb += r.glast >= r.gfirst ? (int64_t)r.glast - r.gfirst + 1 : 0;
@@ -1688,7 +1738,7 @@ static int finish_run(ngsep_ctx* c, size_t from, int64_t n, double scan_ms, doub
 static int finish_run_into(ngsep_ctx* c, SiteStore& dest, size_t from, int64_t n, double scan_ms, double geno_ms, double total_ms,
                            int64_t ncand, double* elapsed_ms) {
     dest.n = from + (size_t)n;
-    if (c->params.calc_strand_bias) apply_strand_bias(dest, from);
+    if (c->params.calc_strand_bias && c->known.empty()) apply_strand_bias(dest, from);   // (genotypeSNV: none)
     c->stats.candidates = ncand;
     c->stats.hard_sites = (int32_t)device_last_hard(c->dev);
     c->stats.exact_bound_passes = device_last_exact(c->dev);
@@ -1976,6 +2026,93 @@ extern "C" int ngsep_clear_sites(ngsep_ctx* c) {
     return NGSEP_OK;
 }
 
+// SingleSampleVariantsDetector.findSNVS with -knownVariants (:896-906): VCFFileReader.loadVariants(file, true,
+// true) (vcf/VCFFileReader.java:196-260,585-600) into a GenomicRegionSortedCollection over the genome.  Biallelic
+// SNVs (one-base REF and ALT in ACGT) are genotyped here; ALT '.' records are skipped, as are records on
+// sequences outside the reference; any other variant is refused (E_UNSUPPORTED: the indel / multi-allelic
+// genotyping of genotypeVariantSample is not in this build).  path NULL or "": back to discovery.
+extern "C" int ngsep_set_known_variants(ngsep_ctx* c, const char* vcf_path) {
+    if (!c) return NGSEP_E_INVALID;
+    c->known.clear();
+    c->known_seq_begin.clear();
+    if (!vcf_path || !vcf_path[0]) return NGSEP_OK;
+    if (c->seq_names.empty()) return set_error(c, NGSEP_E_INVALID, "load the reference before the known variants");
+    if (c->params.multisample || c->params.coverage_stats || c->params.relative_allele_counts)
+        return set_error(c, NGSEP_E_INVALID, "known variants are genotyped by the single-sample detector only");
+    std::FILE* f = std::fopen(vcf_path, "r");
+    if (!f) return set_error(c, NGSEP_E_IO, std::string("cannot read ") + vcf_path);
+    std::unordered_map<std::string, int32_t> idx;
+    for (size_t i = 0; i < c->seq_names.size(); i++) idx[c->seq_names[i]] = (int32_t)i;
+    std::vector<ngsep_ctx::KnownVar> v;
+    char* line = nullptr;
+    size_t cap = 0;
+    ssize_t l;
+    int rc = NGSEP_OK;
+    int64_t lineno = 0;
+    while ((l = getline(&line, &cap, f)) >= 0) {
+        lineno++;
+        while (l > 0 && (line[l - 1] == '\n' || line[l - 1] == '\r')) line[--l] = 0;
+        if (l == 0 || line[0] == '#') continue;
+        const char* fld[6];
+        int k = 0;
+        char* p = line;
+        while (k < 6) { fld[k++] = p; char* t = std::strchr(p, '\t'); if (!t) break; *t = 0; p = t + 1; }
+        if (k < 6) { rc = set_error(c, NGSEP_E_FORMAT, "VCF line " + std::to_string(lineno) + " has fewer than 8 columns"); break; }
+        if (fld[4][0] == '.') continue;                                  // a reference site (filterReferenceSitesGVCF)
+        auto it = idx.find(fld[0]);
+        if (it == idx.end()) continue;
+        const int a = dna_index(fld[3][0]), b = dna_index(fld[4][0]);
+        if (std::strlen(fld[3]) != 1 || std::strlen(fld[4]) != 1 || a < 0 || b < 0) {
+            rc = set_error(c, NGSEP_E_UNSUPPORTED, std::string("known variant ") + fld[0] + ":" + fld[1] +
+                                                   " is not a biallelic SNV (indel / multi-allelic genotyping is not in this build)");
+            break;
+        }
+        int16_t qs = 0;
+        if (fld[5][0] && fld[5][0] != '.') {
+            double q = std::atof(fld[5]);
+            if (q > 32767) q = 255;
+            qs = (int16_t)java_round(q);
+        }
+        ngsep_ctx::KnownVar kv;
+        kv.seq = it->second;
+        kv.pos = std::atoi(fld[1]);
+        kv.ref = (int8_t)a;
+        kv.alt = (int8_t)b;
+        kv.qs = qs;
+        if (std::strcmp(fld[2], ".") != 0) kv.id = fld[2];
+        v.push_back(std::move(kv));
+    }
+    std::free(line);
+    std::fclose(f);
+    if (rc != NGSEP_OK) return rc;
+    std::stable_sort(v.begin(), v.end(), [](const ngsep_ctx::KnownVar& x, const ngsep_ctx::KnownVar& y) {
+        return x.seq != y.seq ? x.seq < y.seq : x.pos < y.pos;
+    });
+    c->known.swap(v);
+    c->known_seq_begin.assign(c->seq_names.size() + 1, 0);
+    for (const auto& kv : c->known) c->known_seq_begin[(size_t)kv.seq + 1]++;
+    for (size_t i = 0; i < c->seq_names.size(); i++) c->known_seq_begin[i + 1] += c->known_seq_begin[i];
+    return NGSEP_OK;
+}
+
+// the input variant of a -knownVariants record: its ID (nullptr for '.').  Records are written in order, and at
+// one position in the input order (stream_collect), so a record is the first input variant of its position and
+// ALT that no earlier record there took.
+const char* ngsep::known_id(const ngsep_ctx* c, const ngsep_site_out& s) {
+    if (c->known.empty() || s.seq_id < 0 || (size_t)s.seq_id + 1 >= c->known_seq_begin.size()) return nullptr;
+    auto& st = c->vcf_known;
+    if (st.seq != s.seq_id || st.pos != s.pos) { st.seq = s.seq_id; st.pos = s.pos; st.taken.clear(); }
+    const int64_t kb = c->known_seq_begin[(size_t)s.seq_id], ke = c->known_seq_begin[(size_t)s.seq_id + 1];
+    auto it = std::lower_bound(c->known.begin() + kb, c->known.begin() + ke, (int64_t)s.pos,
+                               [](const ngsep_ctx::KnownVar& v, int64_t p) { return v.pos < p; });
+    for (int64_t k = it - c->known.begin(); k < ke && c->known[(size_t)k].pos == s.pos; k++)
+        if (c->known[(size_t)k].alt == s.alt && std::find(st.taken.begin(), st.taken.end(), k) == st.taken.end()) {
+            st.taken.push_back(k);
+            return c->known[(size_t)k].id.empty() ? nullptr : c->known[(size_t)k].id.c_str();
+        }
+    return nullptr;
+}
+
 extern "C" int ngsep_fetch_rac(ngsep_ctx* c, double* prop, double* n_alleles, double* moments) {
     if (!c) return NGSEP_E_INVALID;
     if (!c->params.relative_allele_counts) return set_error(c, NGSEP_E_INVALID, "context not in relative-allele-counts mode");
@@ -2087,9 +2224,10 @@ extern "C" int ngsep_stage_finish(ngsep_ctx* c) {
     c->staging_mode = true;
     int rc = flush_sequence(c);
     if (rc != NGSEP_OK) return rc;
-    if (c->params.relative_allele_counts) {
+    if (c->params.relative_allele_counts || !c->known.empty()) {
         c->staged_contigs.clear();
-        return set_error(c, NGSEP_E_UNSUPPORTED, "relative allele counts run on the streaming paths (ngsep_process_alignments / ngsep_rac_bam)");
+        return set_error(c, NGSEP_E_UNSUPPORTED, "relative allele counts and known-variant genotyping run on the streaming paths "
+                                                 "(ngsep_process_alignments / ngsep_call_bam / ngsep_rac_bam)");
     }
     rc = c->params.coverage_stats ? coverage_stage(c, c->staged_contigs) : build_and_upload(c, c->staged_contigs);
     c->staged_contigs.clear();

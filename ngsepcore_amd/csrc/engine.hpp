@@ -282,6 +282,11 @@ struct Staged {            // everything resident for one run
     uint8_t* h_cpile = nullptr;
     uint32_t* h_cneg = nullptr;
     bool single = false;                // the single-sample layout (else the multisample one)
+    // -knownVariants: the run genotypes these sites (KP queue entries {global position, code}: code =
+    // 0x80 | ref << 5 | alt << 8 | 0x400) instead of scanning; counters preset to their number
+    bool known = false;
+    std::vector<int32_t> h_forced;
+    unsigned long long h_forced_ctr[4] = {0, 0, 0, 0};
 };
 
 // Pinned host buffers of the single-sample layout, reused run after run (streamed windows: no page faults,
@@ -305,6 +310,7 @@ struct WindowJob {
     int32_t max_span = 1;
     std::vector<SRead> reads;                               // global coordinates (window at pad)
     std::vector<std::pair<int64_t, int64_t>> carved;        // 1-based, inside [w0, w1]
+    std::vector<int32_t> forced;                            // -knownVariants: KP queue entries (global position, code)
     SiteStore sites;
     // RelativeAlleleCounts mode: the window's histograms and proportion sums; its sequence's slot in the
     // per-sequence distributions (-1: a sequence of <= 100000 bp)
@@ -355,6 +361,12 @@ struct ngsep_ctx {
     std::vector<ngsep::ContigReads> staged_contigs;
     ngsep::Staged staged;
     ngsep::LayoutArena arena;
+    // -knownVariants (ngsep_set_known_variants): biallelic SNVs to genotype instead of discovering, in
+    // GenomicRegionSortedCollection order (sequence, position; input order at equal positions)
+    struct KnownVar { int32_t seq, pos; int8_t ref, alt; int16_t qs; std::string id; };
+    std::vector<KnownVar> known;
+    std::vector<int64_t> known_seq_begin;                    // per sequence: first entry (size n_seq + 1)
+    mutable struct { int32_t seq = -1, pos = -1; std::vector<int64_t> taken; } vcf_known;   // known_id: the position written
     // RelativeAlleleCountsCalculator mode (params.relative_allele_counts): its Distributions
     struct {
         double prop[51] = {}, prop_count = 0, prop_sum = 0, prop_sum_sq = 0;
@@ -442,6 +454,8 @@ int cov_run(CovDevice* d, int32_t max_cov, uint64_t* hist_out, double* kernel_ms
 // engine.cpp
 int coverage_stage(ngsep_ctx* c, std::vector<ContigReads>& contigs);
 int coverage_run(ngsep_ctx* c, double* kernel_ms);
+// engine.cpp: the ID of a -knownVariants record's input variant (nullptr: '.')
+const char* known_id(const ngsep_ctx* c, const ngsep_site_out& s);
 // vcf.cpp
 std::string format_header(const ngsep_ctx* c);
 int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& out);

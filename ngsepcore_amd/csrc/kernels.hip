@@ -271,12 +271,62 @@ __global__ __launch_bounds__(kPostThreads) void k_posterior(const QueueSite* __r
                 }
             }
         }
-        if (total == 0 || (gp.ablate & 8)) continue;                      // VariantDiscoverySNVQAlgorithm.java:101-103
+        const bool known = (rc & 0x400u) != 0;     // -knownVariants site: ref (bits 5-6) and alt (bits 8-9) given
+        if ((total == 0 && !known) || (gp.ablate & 8)) continue;        // VariantDiscoverySNVQAlgorithm.java:101-103
         const bool callable = (rc & 0x80u) != 0;
         int8_t genotype = -1, alt = -1, third = -1, nal = 0;
         int16_t gq = 0, qual = 0;
         bool keep = false;
-        if (callable) {
+        if (known) {
+            // genotypeVariantSample (SingleSampleVariantPileupListener.java:361-391) -> genotypeSNV
+            // (VariantDiscoverySNVQAlgorithm.java:21-62): hom-ref, hom-alt (+0.01), het (+0.01) over the input
+            // alleles; GQ 0 or below -minQuality: undecided.  No calls at all: undecided, no log-conditionals.
+            const int r = (int)((rc >> 5) & 3u), a = (int)((rc >> 8) & 3u);
+            nal = 2;
+            alt = (int8_t)a;
+            keep = true;
+            if (total > 0) {
+                constexpr int kEv[16] = {0, 1, 2, 3, 4, 1, 5, 6, 7, 2, 5, 8, 9, 3, 6, 8};
+                double ev[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) ev[k] = L[kEv[k]] + ((k & 3) == 0 ? gp.log_prior_homo : gp.log_prior_hetero);
+                double logMax = 1;
+#pragma unroll
+                for (int k = 0; k < 16; k++)
+                    if (logMax > 0 || logMax < ev[k]) logMax = ev[k];
+                uint32_t act = 0;
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const double x = ev[k] - logMax;
+                    const bool on = !(x < -20);
+                    act |= on ? 1u << k : 0u;
+                    s_ev[k][threadIdx.x] = on ? x : 0.0;
+                }
+                double totalProb = 0;
+                for (uint32_t rem = act; rem; rem &= rem - 1) {
+                    const int k = __builtin_ctz(rem);
+                    const double pk = pow10_j(s_ev[k][threadIdx.x]);
+                    totalProb += pk;
+                    s_ev[k][threadIdx.x] = pk;
+                }
+                for (uint32_t rem = act; rem; rem &= rem - 1) {
+                    const int k = __builtin_ctz(rem);
+                    s_ev[k][threadIdx.x] = s_ev[k][threadIdx.x] / totalProb;
+                }
+                auto post = [&](int i, int j) -> double {
+                    return s_ev[i == j ? 4 * i : 4 * i + (j < i ? j + 1 : j)][threadIdx.x];
+                };
+                double pMax = post(r, r);
+                int gt = 0;
+                if (post(a, a) > pMax + 0.01) { pMax = post(a, a); gt = 2; }
+                const double pHet = post(r, a) + post(a, r);
+                if (pHet > pMax + 0.01) { pMax = pHet; gt = 1; }
+                gq = phred_d(1 - pMax);
+                if (gq == 0) gt = -1;
+                if (gp.min_quality > gq) { gt = -1; gq = 0; }           // makeUndecided (:388)
+                genotype = (int8_t)gt;
+            }
+        } else if (callable) {
             const int refIdx = (int)((rc >> 5) & 3u);
             // getPosteriorProbabilities (CountsHelper.java:410-443): events in Java's order -- row i holds
             // (i,i) then (i,j) for j != i ascending; L is symmetric
@@ -771,6 +821,10 @@ void k_tile_scan(const uint32_t* __restrict__ vplane, const uint16_t* __restrict
         for (int i = lane; i < qn; i += 64)
             if (base + i < qcap) queue[base + i] = sh.q[wv][i];
     }
+}
+
+__global__ __launch_bounds__(256) void k_zero_i32(int32_t* __restrict__ p, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1737,8 +1791,11 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
                        bool idle, std::string& err) {
     // capacities (shared buffers only change while nothing runs): calls are rare; dump mode needs one
     // record per covered position
-    const int64_t want = g.dump_all ? std::max<int64_t>(s.covered + 1024, 1024) : std::max<int64_t>(s.g_len / 256 + 4096, 4096);
-    const int64_t qwant = (g.dump_all || !prune) ? s.g_len + 1024 : std::max<int64_t>(s.g_len / 64 + 65536, 65536);
+    const int64_t nforced = (int64_t)s.h_forced.size() / 2;     // -knownVariants: the sites to genotype
+    int64_t want = g.dump_all ? std::max<int64_t>(s.covered + 1024, 1024) : std::max<int64_t>(s.g_len / 256 + 4096, 4096);
+    int64_t qwant = (g.dump_all || !prune) ? s.g_len + 1024 : std::max<int64_t>(s.g_len / 64 + 65536, 65536);
+    want = std::max<int64_t>(want, nforced + 1024);
+    qwant = std::max<int64_t>(qwant, nforced + 1024);
     if (want > d->cap_sites || qwant > sl.cap_hard) {
         if (!idle) HIP_TRY(hipStreamSynchronize(sl.stream));
         if (grow_slot(d, sl, want, qwant, err) != 0) return -1;
@@ -1785,7 +1842,14 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     }
     // KT is timed by events bound to its dispatch (hipExtLaunchKernelGGL): the kernel's own start and end
     hipEvent_t k0 = d->time_scan ? sl.ev[0] : nullptr, k1 = d->time_scan ? sl.ev[1] : nullptr;
-    if (d->n_tiles > 0 && prune && d->planes_W) {
+    if (s.known) {
+        // -knownVariants: no scan, the input variants' sites (covered, in window order) are KP's queue
+        if (nforced > 0) HIP_TRY(hipMemcpyAsync(sl.d_hard, s.h_forced.data(), (size_t)nforced * sizeof(QueueSite), hipMemcpyHostToDevice, sl.stream));
+        HIP_TRY(hipMemcpyAsync(ctr, s.h_forced_ctr, 4 * sizeof(unsigned long long), hipMemcpyHostToDevice, sl.stream));
+        hipLaunchKernelGGL(k_zero_i32, dim3((unsigned)std::min<int64_t>((nb + 255) / 256, 4096)), dim3(256), 0, sl.stream, sl.d_bcount, nb);
+        HIP_TRY(hipGetLastError());
+        d->last_hard = nforced;
+    } else if (d->n_tiles > 0 && prune && d->planes_W) {
         // bit-plane scan, persistent waves: as many workgroups as are co-resident, each wave walks the
         // tiles with a grid stride, so at any moment the waves stream one contiguous stretch of the planes
         const int wi = d->planes_W == 4 ? 0 : d->planes_W == 8 ? 1 : 2;

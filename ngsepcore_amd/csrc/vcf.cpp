@@ -70,7 +70,8 @@ int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& o)
     while (ri < 4 && kB[ri] != s.ref) ri++;
     if (ri == 4 || s.n_alleles < 2) return 0;
     const std::string& name = (s.seq_id >= 0 && s.seq_id < (int)c->seq_names.size()) ? c->seq_names[s.seq_id] : std::string("?");
-    o += name; o += '\t'; app(o, s.pos); o += "\t.\t"; o += (char)s.ref; o += '\t';
+    const char* id = known_id(c, s);              // -knownVariants: the input variant's ID
+    o += name; o += '\t'; app(o, s.pos); o += '\t'; o += id ? id : "."; o += '\t'; o += (char)s.ref; o += '\t';
     o += kB[(int)s.alt];
     if (s.n_alleles == 3) { o += ','; o += kB[(int)s.third]; }
     o += '\t'; app(o, s.qual); o += "\t.\t";
@@ -83,6 +84,8 @@ int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& o)
     if (s.n_alleles == 2) {
         const int ai = s.alt;
         if (s.genotype == 2) { o += '1'; if (ploidy > 1) o += "/1"; }
+        else if (s.genotype == 0) { o += '0'; if (ploidy > 1) o += "/0"; }       // (-knownVariants: hom-ref,
+        else if (s.genotype < 0) { o += '.'; if (ploidy > 1) o += "/."; }        //  undecided; VCFFileWriter.java:168-185)
         else o += "0/1";
         o += ':';
         // CalledSNV keeps float log-conditionals (CalledSNV.java:42-45,259-265)
@@ -101,6 +104,7 @@ int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& o)
         // CalledSNV.updateAllelesCopyNumberFromCounts (CalledSNV.java:134-158)
         int total = ploidy, refcn = 0;
         if (s.genotype == 2) refcn = 0;
+        else if (s.genotype <= 0) refcn = total;    // hom-ref; undecided: ACN[0] = total (VCFFileWriter.java:237)
         else if (total <= 2) { total = 2; refcn = 1; }
         else {
             double cr = s.counts[ri], sum = cr + s.counts[ai];

@@ -118,6 +118,10 @@ class GpuPileupSession:
     def load_fasta(self, path: str):
         self._check(self._lib.ngsep_load_fasta(self._ctx, path.encode()))
 
+    def set_known_variants(self, vcf_path: Optional[str]):
+        """-knownVariants (SingleSampleVariantsDetector.findSNVS :896-906): genotype these biallelic SNVs."""
+        self._check(self._lib.ngsep_set_known_variants(self._ctx, vcf_path.encode() if vcf_path else None))
+
     def set_reference(self, name: str, bases: bytes):
         self._check(self._lib.ngsep_set_reference(self._ctx, name.encode(), bases, len(bases)))
 
@@ -291,9 +295,12 @@ class SingleSampleVariantsDetector:
         self.inputFile: Optional[str] = None
         self.genomeFile: Optional[str] = None
         self.outputPrefix: Optional[str] = None
+        self.knownVariantsFile: Optional[str] = None
         self.device = 0
 
     # setters (CommandsDescriptor reflective setters)
+    def setKnownVariantsFile(self, v: str): self.knownVariantsFile = v
+    def getKnownVariantsFile(self) -> Optional[str]: return self.knownVariantsFile
     def setInputFile(self, v: str): self.inputFile = v
     def setGenome(self, v: str): self.genomeFile = v
     def setOutputPrefix(self, v: str): self.outputPrefix = v
@@ -326,6 +333,7 @@ class SingleSampleVariantsDetector:
         "-h": ("setHeterozygosityRate", float), "-maxBaseQS": ("setMaxBaseQS", int),
         "-minQuality": ("setMinQuality", int), "-querySeq": ("setQuerySeq", str),
         "-first": ("setQueryFirst", int), "-last": ("setQueryLast", int),
+        "-knownVariants": ("setKnownVariantsFile", str),
     }
     _FLAGS = {
         "-psp": "setPrintSamplePloidy", "-p": "setProcessNonUniquePrimaryAlignments",
@@ -359,6 +367,8 @@ class SingleSampleVariantsDetector:
             raise NgsepError(_lib.NGSEP_E_IO, "The reference genome file is a required parameter")
         with GpuPileupSession(self.params, self.device) as s:
             s.load_fasta(self.genomeFile)
+            if self.knownVariantsFile:
+                s.set_known_variants(self.knownVariantsFile)
             s.processFile(self.inputFile, (self.outputPrefix or "variants") + ".vcf")
             self.stats = s.stats()
 

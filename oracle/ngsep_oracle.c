@@ -412,6 +412,9 @@ typedef struct ngo_call {
     double logc[4][4];
     int strand_bias;          /* -1 invalid */
     int ploidy;
+    const char* id;           /* -knownVariants: the input variant's ID (NULL: '.') */
+    int known;                /* 1: a genotyped input variant (genotype 0 hom-ref, -1 undecided allowed) */
+    int logc_present;         /* 0: no log-conditionals (an undecided call without allele calls) */
 } ngo_call;
 
 typedef struct { ngo_call* c; int n, cap; } ngo_calls;
@@ -478,7 +481,7 @@ static void print_header_samples(FILE* out, const ngo_params* p, const char* con
 
 /* one VCF line per call: VCFFileWriter.printVCFRecord + printGenotypeInfo */
 static void print_call(FILE* out, const char* seqName, const ngo_call* c) {
-    fprintf(out, "%s\t%d\t.\t%c\t", seqName, c->pos, c->ref);
+    fprintf(out, "%s\t%d\t%s\t%c\t", seqName, c->pos, c->id ? c->id : ".", c->ref);
     if (c->n_alleles == 2) fprintf(out, "%c", BASES[c->idx[1]]);
     else fprintf(out, "%c,%c", BASES[c->idx[1]], BASES[c->idx[2]]);
     fprintf(out, "\t%d\t.\t", c->qual);
@@ -490,8 +493,10 @@ static void print_call(FILE* out, const char* seqName, const ngo_call* c) {
     fprintf(out, "\tGT:PL:GQ:DP:BSDP:ACN\t");
     int ploidy = c->ploidy;
     if (c->n_alleles == 2) {
-        /* CalledSNV: GT */
+        /* CalledSNV: GT (VCFFileWriter.java:168-197) */
         if (c->genotype == 2) { fprintf(out, "1"); if (ploidy > 1) fprintf(out, "/1"); }
+        else if (c->genotype == 0) { fprintf(out, "0"); if (ploidy > 1) fprintf(out, "/0"); }
+        else if (c->genotype == -1) { fprintf(out, "."); if (ploidy > 1) fprintf(out, "/."); }
         else fprintf(out, "0/1");
         fprintf(out, ":");
         /* PL from float log-conds (CalledSNV.java:259-265, :413-435; VCFFileWriter.java:200-212) */
@@ -500,7 +505,7 @@ static void print_call(FILE* out, const char* seqName, const ngo_call* c) {
         float ra = (float)c->logc[c->idx[0]][c->idx[1]];
         float ar = (float)c->logc[c->idx[1]][c->idx[0]];
         double lc[2][2] = {{hr, ra}, {ar, ha}};
-        int present = (hr + ra + ar + ha) != 0;
+        int present = c->logc_present && (hr + ra + ar + ha) != 0;
         for (int j = 0; j < 2; j++)
             for (int i = 0; i <= j; i++) {
                 if (i > 0 || j > 0) fprintf(out, ",");
@@ -511,6 +516,7 @@ static void print_call(FILE* out, const char* seqName, const ngo_call* c) {
         /* ACN: CalledSNV.updateAllelesCopyNumberFromCounts(ploidy), CalledSNV.java:134-168 */
         int total = ploidy, refcn = 0;
         if (c->genotype == 2) refcn = 0;
+        else if (c->genotype == 0 || c->genotype == -1) refcn = total;   /* hom-ref; undecided: ACN[0] = total (:237) */
         else if (total <= 2) { total = 2; refcn = 1; }
         else {
             double cr = c->counts[c->idx[0]], sum = cr + c->counts[c->idx[1]];
@@ -581,6 +587,7 @@ static int discover_snv(const ngo_counts* h, int pos, char refBase, const ngo_pa
     memset(out, 0, sizeof(*out));
     out->pos = pos; out->ref = refBase; out->gq = gq; out->dp = h->total_count;
     out->qual = ngo_phred(refProb);
+    out->logc_present = 1;
     out->strand_bias = -1;
     out->ploidy = p->ploidy;
     memcpy(out->counts, h->counts, sizeof(out->counts));
@@ -608,6 +615,39 @@ static int discover_snv(const ngo_counts* h, int pos, char refBase, const ngo_pa
 }
 
 /* ------------------------------------------------------------------ */
+/* -knownVariants: SingleSampleVariantPileupListener.onPileup with input variants (:158-176) ->      */
+/* genotypeVariantSample (:361-391) -> VariantDiscoverySNVQAlgorithm.genotypeSNV (:21-62), biallelic  */
+/* SNVs as VCFFileReader.loadGenomicVariant makes them (vcf/VCFFileReader.java:196-260)               */
+/* ------------------------------------------------------------------ */
+typedef struct { int seq, pos; char ref, alt; int qs; char* id; } ngo_known;
+static void genotype_known(const ngo_counts* h, const ngo_known* kv, const ngo_params* p, double hetRate, ngo_call* out) {
+    memset(out, 0, sizeof(*out));
+    out->pos = kv->pos; out->ref = kv->ref; out->n_alleles = 2; out->known = 1; out->id = kv->id;
+    out->idx[0] = base_idx(kv->ref); out->idx[1] = base_idx(kv->alt);
+    out->qual = kv->qs;                         /* the input variant's QS: genotypeSNV sets none */
+    out->strand_bias = -1;                      /* genotypeSNV(.., calcStrandBias = false) */
+    out->ploidy = p->ploidy;
+    out->dp = h->total_count;
+    memcpy(out->counts, h->counts, sizeof(out->counts));
+    if (h->total_count == 0) { out->genotype = -1; return; }   /* undecided, no log-conditionals (:23-27) */
+    out->logc_present = 1;
+    for (int i = 0; i < 4; i++) for (int j = 0; j < 4; j++) out->logc[i][j] = h->logc[i][j];
+    double post[16];
+    ngo_counts_posteriors(h, hetRate, post);
+    const int r = out->idx[0], a = out->idx[1];
+    double pMax = post[r * 4 + r];
+    int gt = 0;
+    if (post[a * 4 + a] > pMax + 0.01) { pMax = post[a * 4 + a]; gt = 2; }
+    const double pHet = post[r * 4 + a] + post[a * 4 + r];
+    if (pHet > pMax + 0.01) { pMax = pHet; gt = 1; }
+    int gq = ngo_phred(1 - pMax);
+    if (gq == 0) gt = -1;
+    if ((int16_t)p->min_quality > gq) { gt = -1; gq = 0; }   /* makeUndecided (:388) */
+    out->genotype = gt;
+    out->gq = gq;
+}
+
+/* ------------------------------------------------------------------ */
 /* AlignmentsPileupGenerator sweep (discovery/AlignmentsPileupGenerator.java:377-504) */
 /* ------------------------------------------------------------------ */
 typedef struct { ngo_aln** a; int n, cap; } ngo_alist;
@@ -632,6 +672,8 @@ typedef struct {
     int unsupported;
     ngo_coverage* cov;         /* CoverageStatisticsCalculator listener instead of the variant listeners */
     struct ngo_rac* rac;       /* RelativeAlleleCountsCalculator listener instead of the variant listeners */
+    ngo_known* known;          /* -knownVariants (sequence order, then position, input order kept) */
+    int n_known, known_next;   /* known_next: nextSIVIndex over the whole list */
 } ngo_gen;
 
 /* ------------------------------------------------------------------ */
@@ -1181,7 +1223,17 @@ static int process_current_position(ngo_gen* G) {
             for (int i = 0; i < 4; i++) for (int j = i; j < 4; j++) fprintf(G->dump, "\t%.17g", h.logc[i][j]);
             fprintf(G->dump, "\n");
         }
-        if (!(p->ignore_lowercase_ref && islower((unsigned char)r))) {
+        if (G->known) {
+            /* onPileup with input variants: every input variant at this position, in input order */
+            while (G->known_next < G->n_known && G->known[G->known_next].seq == G->cur_seq && G->known[G->known_next].pos <= pos) {
+                const ngo_known* kv = &G->known[G->known_next++];
+                if (kv->pos != pos) continue;
+                ngo_call c;
+                genotype_known(&h, kv, p, G->het_rate, &c);
+                if (G->calls.n == G->calls.cap) { G->calls.cap = G->calls.cap ? 2 * G->calls.cap : 1024; G->calls.c = realloc(G->calls.c, sizeof(ngo_call) * G->calls.cap); }
+                G->calls.c[G->calls.n++] = c;
+            }
+        } else if (!(p->ignore_lowercase_ref && islower((unsigned char)r))) {
             char R = (char)toupper((unsigned char)r);
             ngo_call c;
             if (discover_snv(&h, pos, R, p, G->het_rate, &c)) {
@@ -1262,6 +1314,10 @@ static void process_alignment(ngo_gen* G, ngo_aln* a) {
     if (G->cur_seq < 0) {   /* startSequence, :435-444 */
         G->cur_seq = a->seq; G->cur_pos = a->first; G->cur_last = a->last;
         if (G->rac) rac_on_sequence_start(G, a->seq);
+        if (G->known) {          /* onSequenceStart: this sequence's input variants, nextSIVIndex = 0 */
+            G->known_next = 0;
+            while (G->known_next < G->n_known && G->known[G->known_next].seq != a->seq) G->known_next++;
+        }
     }
     if (a->last > G->cur_last) G->cur_last = a->last;
     if (a->flags & FLAG_SECONDARY) alist_push(&G->ss_secondary, a);
@@ -1288,6 +1344,55 @@ static char* split_tab(char** s) {
     return b;
 }
 
+/* VCFFileReader.loadVariants(file, true, true) (vcf/VCFFileReader.java:585-600) sorted as a
+ * GenomicRegionSortedCollection over the genome's sequences (stable: input order at equal positions).
+ * Only biallelic SNVs (one-base REF and ALT in ACGT) are supported; ALT '.' records are skipped
+ * (filterReferenceSitesGVCF); records on sequences outside the genome are skipped. */
+static int known_cmp(const void* a, const void* b) {
+    const ngo_known *x = a, *y = b;
+    if (x->seq != y->seq) return x->seq < y->seq ? -1 : 1;
+    if (x->pos != y->pos) return x->pos < y->pos ? -1 : 1;
+    return 0;
+}
+static int load_known(const char* path, const ngo_genome* g, ngo_known** out, int* n_out) {
+    FILE* f = fopen(path, "r");
+    if (!f) return NGO_ERR_IO;
+    char* line = NULL; size_t cap = 0; ssize_t l;
+    ngo_known* v = NULL; int n = 0, vc = 0, rc = NGO_OK;
+    while ((l = getline(&line, &cap, f)) >= 0) {
+        while (l > 0 && (line[l - 1] == '\n' || line[l - 1] == '\r')) line[--l] = 0;
+        if (l == 0 || line[0] == '#') continue;
+        char* fld[6]; int k = 0; char* s2 = line;
+        while (k < 6) { fld[k++] = s2; char* t = strchr(s2, '\t'); if (!t) break; *t = 0; s2 = t + 1; }
+        if (k < 6) { rc = NGO_ERR_ARG; break; }
+        if (fld[4][0] == '.') continue;
+        const int seq = genome_find(g, fld[0]);
+        if (seq < 0) continue;
+        if (strlen(fld[3]) != 1 || strlen(fld[4]) != 1 || !strchr("ACGT", fld[3][0]) || !strchr("ACGT", fld[4][0])) { rc = NGO_UNSUPPORTED; break; }
+        int qs = 0;
+        if (fld[5][0] && fld[5][0] != '.') { double q = atof(fld[5]); if (q > 32767) q = 255; qs = (int)ngo_java_round(q); }
+        if (n == vc) { vc = vc ? 2 * vc : 256; v = realloc(v, sizeof(ngo_known) * vc); }
+        v[n].seq = seq; v[n].pos = atoi(fld[1]); v[n].ref = fld[3][0]; v[n].alt = fld[4][0]; v[n].qs = qs;
+        v[n].id = strcmp(fld[2], ".") == 0 ? NULL : strdup(fld[2]);
+        n++;
+    }
+    free(line); fclose(f);
+    if (rc != NGO_OK) { for (int i = 0; i < n; i++) free(v[i].id); free(v); return rc; }
+    /* stable sort: (seq, pos) then input index */
+    int* ord = malloc(sizeof(int) * (n > 0 ? n : 1));
+    for (int i = 0; i < n; i++) ord[i] = i;
+    for (int i = 1; i < n; i++) {          /* insertion sort keeps equal keys in order; input is nearly sorted */
+        int x = ord[i], j = i - 1;
+        while (j >= 0 && known_cmp(&v[ord[j]], &v[x]) > 0) { ord[j + 1] = ord[j]; j--; }
+        ord[j + 1] = x;
+    }
+    ngo_known* w = malloc(sizeof(ngo_known) * (n > 0 ? n : 1));
+    for (int i = 0; i < n; i++) w[i] = v[ord[i]];
+    free(v); free(ord);
+    *out = w; *n_out = n;
+    return NGO_OK;
+}
+
 static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
                         const char* dump_path, const ngo_params* p, ngo_stats* stats, double min_adf, int multisample,
                         ngo_coverage* cov, ngo_rac* rac) {
@@ -1311,6 +1416,12 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
     if (!multisample && !p->het_rate_set && p->ploidy == 1) G.het_rate = 1e-6;
     G.cov = cov;
     G.rac = rac;
+    if (p->known_vcf && p->known_vcf[0]) {
+        if (load_known(p->known_vcf, &g, &G.known, &G.n_known) != NGO_OK) {
+            fclose(in); if (out != stdout) fclose(out); if (dump) fclose(dump);
+            return NGO_UNSUPPORTED;
+        }
+    }
     if (!multisample && !cov && !rac) print_header(out, p);
     ngo_mvd M; memset(&M, 0, sizeof(M));
     ngo_strlist rg_sm = {0};       /* SM of each @RG (parallel to rgs) */
@@ -1473,6 +1584,8 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
     for (int i = 0; i < G.ss_primary.n; i++) aln_free(G.ss_primary.a[i]);
     for (int i = 0; i < G.ss_secondary.n; i++) aln_free(G.ss_secondary.a[i]);
     free(G.pending.a); free(G.ss_primary.a); free(G.ss_secondary.a); free(G.retired.a); free(G.calls.c);
+    for (int i = 0; i < G.n_known; i++) free(G.known[i].id);
+    free(G.known);
     for (int i = 0; i < g.n; i++) { free(g.s[i].name); free(g.s[i].seq); }
     free(g.s);
     for (int i = 0; i < rgs.n; i++) free(rgs.ids[i]);

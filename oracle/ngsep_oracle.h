@@ -51,6 +51,7 @@ typedef struct ngo_params {
                                       (IndelRealignerPileupListener.java:85-126 without its events): the SNV
                                       calls are the reference's only outside the realigner's windows -- what
                                       the GPU path's carved regions leave (tests/test_gpu_indels.py) */
+    const char* known_vcf;         /* -knownVariants (NULL): genotype these biallelic SNVs instead of discovering */
 } ngo_params;
 
 void ngo_params_default(ngo_params* p);
