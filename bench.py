@@ -315,7 +315,7 @@ def main():
         names = [n for n, _ in syn.contigs()]
         workload = (f"MultisampleVariantsDetector: {args.samples} synthetic yeast samples at {args.depth:g}x, "
                     f"shard {'+'.join(names)} (one GPU's contig shard of the 8-GPU split)")
-        workload_key = f"multisample{args.samples}:{args.depth:g}x:contig{args.contig_first}"
+        workload_key = f"multisample{args.samples}:{args.depth:g}x:contig{args.contig_first}:v2"
         sources = [syn]
     elif args.config == "yeast":
         sources = [pysynth.Synth(genome=pysynth.YEAST, depth=args.depth, seed=2 + rank)]
@@ -446,10 +446,12 @@ def main():
     tile = st.tile_positions
     # bytes KT moves per launch: the valid-call plane (rows_t * T / 8 per tile), the other-allele lists
     # (2 B per entry, 4 B of range per tile), the reference codes (1 B per global position, halos
-    # included) and the 16-B tile descriptors; the multisample KTM streams its per-sample byte blocks and
-    # the reference codes
+    # included) and the 16-B tile descriptors.  The multisample scan (KTM + KQN) reads its candidate
+    # columns (1 B per valid call, 5 B per column, 8 B per 64 columns), the open-position bits (1 bit per
+    # global position) and writes the queue (8 B per open position)
     if multi:
-        kt_bytes = sum(x.pile_bytes + x.global_positions + 16 * x.n_tiles for x in stats_all)
+        kt_bytes = sum(x.pile_bytes + 5 * x.candidates + 8 * x.n_tiles + x.global_positions // 8 + 8 * x.hard_sites
+                       for x in stats_all)
     else:
         kt_bytes = sum(x.pile_bytes // 8 + 2 * x.other_allele_calls + x.global_positions + 20 * x.n_tiles for x in stats_all)
     layout_ms = sum(x.layout_ms for x in stats_all)
@@ -489,7 +491,7 @@ def main():
         alg_bytes = read_bases + positions + 16 * reads
         achieved = kt_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else None
         traffic = load_traffic(workload_key)
-        scan_kernel = "k_tile_pileup_multi" if multi else f"k_tile_scan<{tile // 32}>"
+        scan_kernel = "k_scan_multi+k_queue_need" if multi else f"k_tile_scan<{tile // 32}>"
         line = {
             "metric": METRIC,
             "value": value,

@@ -1163,179 +1163,213 @@ void LayoutArena::release() {
     cap = 0;
 }
 
-// Multisample layout: the same tiles of T positions, one block per (tile, sample) holding that
-// sample's reads coloured into rows (MultisampleVariantsDetector genotypes every sample from its own
-// read groups, PileupRecord.getAlleleCalls(span, readGroups), :104-111).  Reads of no sample only
-// enter the pooled counts, which the population kernel takes from the read table.
-static int build_pile_multi(Staged& s) {
+// Multisample layout.  MultisampleVariantsDetector genotypes every sample from its own read groups
+// (PileupRecord.getAlleleCalls(span, readGroups), :104-111).
+//  * KTM's candidate columns: a sample without a valid call of another allele than the reference at a
+//    position cannot make a decided non-reference call there, so the scan only needs the
+//    (sample, position) columns that hold such a call: its valid calls as bytes ((allele XOR reference
+//    allele) << 5 | quality), in no particular order (the bounds are sums).  Entries are position-major,
+//    then sample, 64 per KTM wave (h_mc_gbase: the byte offset of entry 64k's column).  A column deeper
+//    than kMcMaxCalls keeps its position open without bytes (n = 255).
+//  * KPM's pile: per tile of kPopTile positions and per sample (and one block for the reads of no sample,
+//    which only enter the pooled counts), position-major columns of the sample's nonzero codes in the
+//    order getAlleleCalls visits them: read-group rank, then pending order -- rows = the tile's deepest
+//    column, zero padded (a zero code is no call and counts nothing).
+static int build_multi_layout(Staged& s) {
     const int64_t g_len = s.g_len, nreads = s.n_reads;
-    const int S = s.n_samples;
+    const int S = s.n_samples, S1 = S + 1;
     const int32_t* R = s.h_reads.data();
-    const int64_t nb16 = g_len / kTileMinPos;
-    std::vector<std::vector<int64_t>> by_sample((size_t)S);
-    for (int64_t i = 0; i < nreads; i++) {
-        const int sm = (R[i * 4 + 3] >> 8) - 1;
-        if (sm >= 0 && sm < S) by_sample[(size_t)sm].push_back(i);
-    }
-    // per-sample maxima of the depth over 16-position blocks (rows per (tile, sample) are 16-bit)
-    std::vector<uint16_t> m16((size_t)S * (size_t)nb16, 0);
-    bool overflow = false;
-    {
-        std::vector<int32_t> cov((size_t)g_len + 1);
-        for (int sm = 0; sm < S; sm++) {
-            std::fill(cov.begin(), cov.end(), 0);
-            for (int64_t i : by_sample[(size_t)sm]) {
-                const int32_t a = R[i * 4], b = R[i * 4 + 1];
-                if (b < a) continue;
-                cov[a]++;
-                cov[(size_t)b + 1]--;
-            }
-            uint16_t* m = &m16[(size_t)sm * (size_t)nb16];
-            int32_t run = 0;
-            for (int64_t p = 0; p < nb16 * kTileMinPos; p++) {
-                run += cov[p];
-                if (run > 65535) overflow = true;
-                const int32_t v = run > 65535 ? 65535 : run;
-                if (v > m[p / kTileMinPos]) m[p / kTileMinPos] = (uint16_t)v;
-            }
-        }
-    }
-    if (overflow) return -1;
-    // tile size: bytes of all blocks + a fixed cost per (tile, sample) block (the scan's per-block
-    // reduction and bound work, in byte equivalents; NGSEP_MS_BLOCK_COST overrides it for tuning)
-    double block_cost = 1024.0;
-    if (const char* e = std::getenv("NGSEP_MS_BLOCK_COST")) block_cost = std::atof(e);
-    int bestT = kTileMinPos;
-    double best = -1;
-    for (int T = kTileMinPos; T <= kTileMaxPos; T *= 2) {
-        const int64_t f = T / kTileMinPos, nt = g_len / T;
-        double bytes = 0;
-        for (int sm = 0; sm < S; sm++) {
-            const uint16_t* m = &m16[(size_t)sm * (size_t)nb16];
-            for (int64_t t = 0; t < nt; t++) {
-                uint16_t mx = 0;
-                for (int64_t k = 0; k < f; k++) mx = std::max(mx, m[t * f + k]);
-                bytes += (double)mx * T;
-            }
-        }
-        const double cost = bytes + block_cost * (double)nt * S;
-        if (best < 0 || cost < best) { best = cost; bestT = T; }
-    }
-    const int T = bestT;
-    const int64_t nt = g_len / T, f = T / kTileMinPos;
-    s.tile = T;
-    s.n_tiles = nt;
-    s.h_rows.assign((size_t)nt * S, 0);
-    s.h_toff.assign((size_t)nt + 1, 0);
-    int64_t off = 0;
-    int32_t rmax = 0;
-    for (int64_t t = 0; t < nt; t++) {
-        s.h_toff[(size_t)t] = off;
-        for (int sm = 0; sm < S; sm++) {
-            const uint16_t* m = &m16[(size_t)sm * (size_t)nb16];
-            uint16_t mx = 0;
-            for (int64_t k = 0; k < f; k++) mx = std::max(mx, m[t * f + k]);
-            s.h_rows[(size_t)t * S + sm] = mx;
-            off += (int64_t)mx * T;
-            rmax = std::max<int32_t>(rmax, mx);
-        }
-    }
-    s.h_toff[(size_t)nt] = off;
-    std::vector<uint16_t>().swap(m16);
-    s.pile_bytes = off;
-    s.tile_rows_max = rmax;
-    s.h_pile.assign((size_t)off, 0);
     const int SL = s.slot_size;
     const uint8_t* slots = s.h_slots.data();
     const uint8_t* ref = s.h_ref.data();
-    std::vector<std::vector<int64_t>> tile_reads((size_t)S);
-    std::vector<std::pair<int32_t, int32_t>> heap;
-    std::vector<int32_t> free_rows;
-    int64_t r_lo = 0;
-    for (int64_t t = 0; t < nt; t++) {
-        const int32_t tstart = (int32_t)(t * T), tend = tstart + T;
-        while (r_lo < nreads && R[r_lo * 4] <= tstart - s.max_span) r_lo++;
-        for (auto& v : tile_reads) v.clear();
-        for (int64_t r = r_lo; r < nreads && R[r * 4] < tend; r++) {
-            const int32_t gfirst = R[r * 4], glast = R[r * 4 + 1];
-            if (glast < tstart || glast < gfirst) continue;
-            const int sm = (R[r * 4 + 3] >> 8) - 1;
-            if (sm >= 0 && sm < S) tile_reads[(size_t)sm].push_back(r);
+    const int32_t maxspan = s.max_span;
+    const int64_t PT = kPopTile;
+    int64_t C = ((int64_t)1 << 21) / S1;
+    C = std::max<int64_t>(256, std::min<int64_t>(8192, C));        // a multiple of PT (g_len is one of 1024)
+    const int64_t nchunk = (g_len + C - 1) / C, ntile = g_len / PT;
+    s.tile = (int32_t)PT;
+    s.h_prow.assign((size_t)ntile * S1, 0);
+    auto first_read = [&](int64_t c0) {         // first read that can overlap [c0, ..): gfirst > c0 - maxspan
+        int64_t lo = 0, hi = nreads;
+        while (lo < hi) {
+            const int64_t m = (lo + hi) / 2;
+            if ((int64_t)R[m * 4] <= c0 - maxspan) lo = m + 1; else hi = m;
         }
-        int64_t boff = s.h_toff[(size_t)t];
-        for (int sm = 0; sm < S; sm++) {
-            const int32_t rows = s.h_rows[(size_t)t * S + sm];
-            uint8_t* blk = &s.h_pile[(size_t)boff];
-            boff += (int64_t)rows * T;
-            heap.clear();
-            free_rows.clear();
-            int32_t next_row = 0;
-            for (int64_t r : tile_reads[(size_t)sm]) {
-                const int32_t gfirst = R[r * 4], glast = R[r * 4 + 1];
-                const int32_t a = std::max(gfirst, tstart) - tstart, b = std::min(glast, tend - 1) - tstart;
-                while (!heap.empty() && heap.front().first < a) {
-                    free_rows.push_back(heap.front().second);
-                    std::pop_heap(heap.begin(), heap.end(), std::greater<>());
-                    heap.pop_back();
+        return lo;
+    };
+    auto sample_of = [&](int64_t r) { const int sm = (R[r * 4 + 3] >> 8) - 1; return sm >= 0 && sm < S ? sm : S; };
+    // f(s1, first, last, bytes) for the reads overlapping [c0, c1), in read order
+    auto each_read = [&](int64_t c0, int64_t c1, auto&& f) {
+        for (int64_t r = first_read(c0); r < nreads && R[r * 4] < c1; r++) {
+            const int64_t gfirst = R[r * 4], glast = R[r * 4 + 1];
+            const int64_t a = std::max(gfirst, c0), b = std::min(glast, c1 - 1);
+            if (b < a) continue;
+            f(sample_of(r), a, b, slots + (size_t)R[r * 4 + 2] * SL + (a - gfirst));
+        }
+    };
+    struct Out { std::vector<int32_t> pos; std::vector<uint8_t> n; std::vector<uint8_t> bytes; };
+    std::vector<Out> outs((size_t)nchunk);
+    std::atomic<bool> overflow{false};
+    parallel_for(nchunk, 1, [&](int64_t k0, int64_t k1) {
+        std::vector<uint16_t> nz((size_t)S1 * C), nv((size_t)S * C);
+        std::vector<uint8_t> alt((size_t)S * C);
+        std::vector<uint32_t> cur((size_t)S * C);
+        for (int64_t k = k0; k < k1; k++) {
+            const int64_t c0 = k * C, c1 = std::min(g_len, c0 + C), len = c1 - c0;
+            std::fill(nz.begin(), nz.end(), 0);
+            std::fill(nv.begin(), nv.end(), 0);
+            std::fill(alt.begin(), alt.end(), 0);
+            // calls per (sample, position); flag the positions with a valid call of another allele
+            each_read(c0, c1, [&](int s1, int64_t a, int64_t b, const uint8_t* src) {
+                uint16_t* z = &nz[(size_t)s1 * C];
+                if (s1 == S) {
+                    for (int64_t p = a; p <= b; p++)
+                        if (src[p - a]) {
+                            if (z[p - c0] == 65535) { overflow = true; continue; }
+                            z[p - c0]++;
+                        }
+                    return;
                 }
-                int32_t row;
-                if (!free_rows.empty()) { row = free_rows.back(); free_rows.pop_back(); }
-                else row = next_row++;
-                heap.push_back({b, row});
-                std::push_heap(heap.begin(), heap.end(), std::greater<>());
-                const uint8_t* src = slots + (size_t)R[r * 4 + 2] * SL + (tstart + a - gfirst);
-                uint8_t* dst = blk + (size_t)row * T;
-                for (int32_t p = a; p <= b; p++) {
-                    uint8_t cd = src[p - a];
-                    if (cd & kCodeValid) {
-                        const uint8_t rc = ref[tstart + p];
-                        const uint8_t ra = (rc & kRefCallable) ? (uint8_t)((rc >> 5) & 3) : 0;
-                        cd = (uint8_t)((cd & 0x9F) | ((((cd >> 5) & 3) ^ ra) << 5));
-                    }
-                    dst[p] = cd;
+                uint16_t* v = &nv[(size_t)s1 * C];
+                uint8_t* x = &alt[(size_t)s1 * C];
+                for (int64_t p = a; p <= b; p++) {
+                    const uint8_t cd = src[p - a];
+                    if (!cd) continue;
+                    if (z[p - c0] == 65535) { overflow = true; continue; }
+                    z[p - c0]++;
+                    if (!(cd & kCodeValid)) continue;
+                    v[p - c0]++;
+                    const uint8_t rc = ref[p];
+                    if ((rc & kRefCallable) && ((rc ^ cd) & 0x60)) x[p - c0] = 1;
+                }
+            });
+            // KPM rows per (tile, sample)
+            for (int64_t t = c0 / PT; t < c1 / PT; t++)
+                for (int s1 = 0; s1 < S1; s1++) {
+                    const uint16_t* z = &nz[(size_t)s1 * C + (size_t)(t * PT - c0)];
+                    uint16_t mx = 0;
+                    for (int64_t p = 0; p < PT; p++) mx = std::max(mx, z[p]);
+                    s.h_prow[(size_t)t * S1 + s1] = mx;
+                }
+            // KTM columns
+            Out& o = outs[(size_t)k];
+            uint32_t nb = 0;
+            for (int64_t p = 0; p < len; p++)
+                for (int sm = 0; sm < S; sm++) {
+                    const size_t i = (size_t)sm * C + p;
+                    if (!alt[i]) continue;
+                    o.pos.push_back((int32_t)(c0 + p));
+                    const bool deep = nv[i] > kMcMaxCalls;
+                    o.n.push_back(deep ? 255 : (uint8_t)nv[i]);
+                    cur[i] = nb;
+                    if (deep) alt[i] = 0;       // no bytes
+                    else nb += nv[i];
+                }
+            o.bytes.resize(nb);
+            if (!nb) continue;
+            uint8_t* out = o.bytes.data();
+            each_read(c0, c1, [&](int s1, int64_t a, int64_t b, const uint8_t* src) {
+                if (s1 == S) return;
+                const uint8_t* x = &alt[(size_t)s1 * C];
+                uint32_t* cu = &cur[(size_t)s1 * C];
+                for (int64_t p = a; p <= b; p++) {
+                    if (!x[p - c0]) continue;
+                    const uint8_t cd = src[p - a];
+                    if (!(cd & kCodeValid)) continue;
+                    out[cu[p - c0]++] = (uint8_t)(((cd ^ ref[p]) & 0x60) | (cd & 0x1F));
+                }
+            });
+        }
+    });
+    if (overflow) return -1;
+    // KTM entries and bytes, concatenated in chunk order
+    std::vector<int64_t> eoff((size_t)nchunk + 1, 0), boff((size_t)nchunk + 1, 0);
+    for (int64_t k = 0; k < nchunk; k++) {
+        eoff[(size_t)k + 1] = eoff[(size_t)k] + (int64_t)outs[(size_t)k].pos.size();
+        boff[(size_t)k + 1] = boff[(size_t)k] + (int64_t)outs[(size_t)k].bytes.size();
+    }
+    const int64_t ne = eoff[(size_t)nchunk], nbytes = boff[(size_t)nchunk];
+    s.mc_entries = ne;
+    s.h_mc_pos.resize((size_t)ne);
+    s.h_mc_n.resize((size_t)ne);
+    s.h_pile.resize((size_t)nbytes);
+    parallel_for(nchunk, 4, [&](int64_t k0, int64_t k1) {
+        for (int64_t k = k0; k < k1; k++) {
+            Out& o = outs[(size_t)k];
+            if (!o.pos.empty()) {
+                std::memcpy(&s.h_mc_pos[(size_t)eoff[(size_t)k]], o.pos.data(), o.pos.size() * sizeof(int32_t));
+                std::memcpy(&s.h_mc_n[(size_t)eoff[(size_t)k]], o.n.data(), o.n.size());
+            }
+            if (!o.bytes.empty()) std::memcpy(&s.h_pile[(size_t)boff[(size_t)k]], o.bytes.data(), o.bytes.size());
+            o = Out();
+        }
+    });
+    s.h_mc_gbase.assign((size_t)((ne + 63) / 64) + 1, 0);
+    int64_t off = 0;
+    for (int64_t i = 0; i < ne; i++) {
+        if ((i & 63) == 0) s.h_mc_gbase[(size_t)(i >> 6)] = off;
+        const uint8_t n = s.h_mc_n[(size_t)i];
+        off += n == 255 ? 0 : n;
+    }
+    s.h_mc_gbase.back() = off;
+    s.pile_bytes = nbytes;
+    s.n_tiles = (ne + 63) / 64;         // KTM's groups of 64 columns
+    // KPM pile: block offsets, then the columns filled chunk by chunk in getAlleleCalls order
+    s.h_pboff.assign((size_t)ntile * S1 + 1, 0);
+    int64_t po = 0;
+    int32_t rmax = 0;
+    for (size_t i = 0; i < (size_t)ntile * S1; i++) {
+        s.h_pboff[i] = po;
+        po += (int64_t)s.h_prow[i] * PT;
+        rmax = std::max<int32_t>(rmax, s.h_prow[i]);
+    }
+    s.h_pboff.back() = po;
+    s.ppile_bytes = po;
+    s.tile_rows_max = rmax;
+    s.h_ppile.reset(new (std::nothrow) uint8_t[(size_t)po + 64]);
+    if (!s.h_ppile) return -2;
+    std::memset(s.h_ppile.get() + po, 0, 64);
+    uint8_t* pile = s.h_ppile.get();
+    parallel_for(nchunk, 1, [&](int64_t k0, int64_t k1) {
+        std::vector<uint16_t> cu((size_t)S1 * C);
+        std::vector<int64_t> rl;
+        std::vector<uint32_t> key;
+        std::vector<int32_t> cnt((size_t)S1 * 128 + 1);
+        std::vector<int64_t> sorted;
+        for (int64_t k = k0; k < k1; k++) {
+            const int64_t c0 = k * C, c1 = std::min(g_len, c0 + C);
+            const int64_t t0 = c0 / PT, t1 = c1 / PT;
+            std::memset(pile + s.h_pboff[(size_t)t0 * S1], 0, (size_t)(s.h_pboff[(size_t)t1 * S1] - s.h_pboff[(size_t)t0 * S1]));
+            std::fill(cu.begin(), cu.end(), 0);
+            // the chunk's reads by (sample, read-group rank), pending order inside (a stable counting sort)
+            rl.clear();
+            key.clear();
+            for (int64_t r = first_read(c0); r < nreads && R[r * 4] < c1; r++) {
+                if (std::min<int64_t>(R[r * 4 + 1], c1 - 1) < std::max<int64_t>(R[r * 4], c0)) continue;
+                rl.push_back(r);
+                key.push_back((uint32_t)(sample_of(r) * 128 + ((R[r * 4 + 3] >> 1) & 127)));
+            }
+            std::fill(cnt.begin(), cnt.end(), 0);
+            for (uint32_t kk : key) cnt[kk + 1]++;
+            for (size_t i = 1; i < cnt.size(); i++) cnt[i] += cnt[i - 1];
+            sorted.resize(rl.size());
+            for (size_t i = 0; i < rl.size(); i++) sorted[(size_t)cnt[key[i]]++] = rl[i];
+            for (int64_t r : sorted) {
+                const int s1 = sample_of(r);
+                const int64_t gfirst = R[r * 4], glast = R[r * 4 + 1];
+                const int64_t a = std::max(gfirst, c0), b = std::min(glast, c1 - 1);
+                const uint8_t* src = slots + (size_t)R[r * 4 + 2] * SL + (a - gfirst);
+                uint16_t* cc = &cu[(size_t)s1 * C];
+                for (int64_t p = a; p <= b; p++) {
+                    const uint8_t cd = src[p - a];
+                    if (!cd) continue;
+                    const size_t bi = (size_t)(p / PT) * S1 + s1;
+                    pile[s.h_pboff[bi] + (p % PT) * s.h_prow[bi] + cc[p - c0]++] = cd;
                 }
             }
         }
-    }
+    });
     return 0;
-}
-
-// Population kernel read index: bucket b = (sample, read-group rank) in sample order, then the reads
-// of no sample; a stable counting sort of the read table by bucket keeps the pending order inside a
-// bucket, so walking a sample's buckets in rank order visits its calls exactly as
-// PileupRecord.getAlleleCalls(span, readGroups) does (:104-111).
-static void build_buckets(const ngsep_ctx* c, Staged& s) {
-    const int S = s.n_samples;
-    const int32_t* R = s.h_reads.data();
-    s.h_bbase.assign((size_t)S + 2, 0);
-    for (int sm = 0; sm < S; sm++) s.h_bbase[(size_t)sm + 1] = s.h_bbase[(size_t)sm] + std::max<int>(1, c->sample_nrank[(size_t)sm]);
-    s.h_bbase[(size_t)S + 1] = s.h_bbase[(size_t)S] + 1;
-    const int nb = s.h_bbase[(size_t)S + 1];
-    auto bucket = [&](int64_t r) -> int {
-        const int32_t fl = R[r * 4 + 3];
-        const int sm = (fl >> 8) - 1, rk = (fl >> 1) & 127;
-        return sm >= 0 && sm < S ? s.h_bbase[(size_t)sm] + rk : nb - 1;
-    };
-    s.h_bseg.assign((size_t)nb + 1, 0);
-    for (int64_t r = 0; r < s.n_reads; r++) s.h_bseg[(size_t)bucket(r) + 1]++;
-    for (int b = 0; b < nb; b++) s.h_bseg[(size_t)b + 1] += s.h_bseg[(size_t)b];
-    s.h_perm.assign((size_t)s.n_reads, 0);
-    std::vector<int32_t> fill(s.h_bseg.begin(), s.h_bseg.end() - 1);
-    for (int64_t r = 0; r < s.n_reads; r++) s.h_perm[(size_t)fill[(size_t)bucket(r)]++] = (int32_t)r;
-    // per bucket and 64-position block k: first index whose read starts at >= 64k - pad + 1
-    const int32_t pad = s.windows.empty() ? 64 : s.windows[0].pad;
-    s.nblk_b = (s.g_len + pad + 63) / 64 + 2;
-    s.h_blb.assign((size_t)nb * (size_t)s.nblk_b, 0);
-    for (int b = 0; b < nb; b++) {
-        int32_t j = s.h_bseg[(size_t)b];
-        const int32_t end = s.h_bseg[(size_t)b + 1];
-        int32_t* out = &s.h_blb[(size_t)b * (size_t)s.nblk_b];
-        for (int64_t k = 0; k < s.nblk_b; k++) {
-            const int64_t key = k * 64 - pad + 1;
-            while (j < end && (int64_t)R[(int64_t)s.h_perm[(size_t)j] * 4] < key) j++;
-            out[k] = j;
-        }
-    }
 }
 
 int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
@@ -1464,10 +1498,10 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
         s.n_slots = nslots;
         s.n_read_bases = nbases;
         s.n_samples = (int32_t)c->sample_ids.size();
-        if (build_pile_multi(s) != 0)
-            return set_error(c, NGSEP_E_UNSUPPORTED, "a sample's pileup tile is deeper than 65535 alignments");
-        build_buckets(c, s);
-        c->stats.slot_bytes = nslots * S;
+        const int lr = build_multi_layout(s);
+        if (lr == -2) return set_error(c, NGSEP_E_DEVICE, "host memory for the population pile could not be allocated");
+        if (lr != 0) return set_error(c, NGSEP_E_UNSUPPORTED, "a sample's pileup is deeper than 65535 alignments");
+        c->stats.slot_bytes = s.ppile_bytes;
         c->stats.slot_size = S;
     }
     c->stats.read_bases = nbases;
@@ -1500,12 +1534,12 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     std::vector<TileInfo>().swap(s.h_tinfo);
     std::vector<uint16_t>().swap(s.h_olist);
     std::vector<int32_t>().swap(s.h_loff);
-    std::vector<uint16_t>().swap(s.h_rows);
-    std::vector<int64_t>().swap(s.h_toff);
-    std::vector<int32_t>().swap(s.h_perm);
-    std::vector<int32_t>().swap(s.h_bseg);
-    std::vector<int32_t>().swap(s.h_blb);
-    std::vector<int32_t>().swap(s.h_bbase);
+    std::vector<int32_t>().swap(s.h_mc_pos);
+    std::vector<uint8_t>().swap(s.h_mc_n);
+    std::vector<int64_t>().swap(s.h_mc_gbase);
+    s.h_ppile.reset();
+    std::vector<uint16_t>().swap(s.h_prow);
+    std::vector<int64_t>().swap(s.h_pboff);
     // one-shot runs give the pinned layout buffers back (streamed windows keep theirs)
     s.h_planes = nullptr;
     s.h_cpile = nullptr;
@@ -1658,21 +1692,24 @@ static void apply_strand_bias(SiteStore& sites, size_t from) {
 // MultisampleVariantsDetector run: sites come back unordered with global positions; order them by
 // position and map them to (sequence, position) (the listener writes in pileup order, :534-535)
 static int run_device_multi(ngsep_ctx* c, const LikTables& t, const GenotypeParams& gp, double* elapsed_ms) {
-    std::vector<ngsep_popsite_out> sites;
-    std::vector<ngsep_sample_call> calls;
+    const ngsep_popsite_out* sites = nullptr;
+    const ngsep_sample_call* calls = nullptr;
+    int64_t n = 0;
     double scan_ms = 0, geno_ms = 0, total_ms = 0;
     int64_t ncand = 0;
     std::string err;
-    if (device_run_multi(c->dev, c->staged, t, gp, c->sample_nrank, c->params.min_allele_depth_freq, c->params.ploidy,
-                         &sites, &calls, &scan_ms, &geno_ms, &total_ms, &ncand, err) != 0)
-        return set_error(c, NGSEP_E_DEVICE, err);
     const size_t S = c->sample_ids.size();
-    std::vector<int64_t> order(sites.size());
+    if (device_run_multi(c->dev, c->staged, t, gp, (int32_t)S, c->params.min_allele_depth_freq, c->params.ploidy,
+                         &sites, &calls, &n, &scan_ms, &geno_ms, &total_ms, &ncand, err) != 0)
+        return set_error(c, NGSEP_E_DEVICE, err);
+    std::vector<int64_t> order((size_t)n);
     for (size_t i = 0; i < order.size(); i++) order[i] = (int64_t)i;
     std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return sites[a].pos < sites[b].pos; });
     const std::vector<Window>& ws = c->staged.windows;
     size_t wi = 0;
     const size_t from = c->pop_sites.size();
+    std::vector<int64_t> src;                   // staging index of each kept site, in output order
+    src.reserve((size_t)n);
     for (int64_t i : order) {
         ngsep_popsite_out o = sites[(size_t)i];
         const int64_t gpos = o.pos;
@@ -1683,8 +1720,16 @@ static int run_device_multi(ngsep_ctx* c, const LikTables& t, const GenotypePara
         o.seq_id = w.seq_id;
         o.pos = (int32_t)(w.w0 + off);
         c->pop_sites.push_back(o);
-        c->pop_calls.insert(c->pop_calls.end(), calls.begin() + (ptrdiff_t)((size_t)i * S), calls.begin() + (ptrdiff_t)((size_t)(i + 1) * S));
+        src.push_back(i);
     }
+    // the sites' calls in output order (host threads: a few tens of MB per run)
+    const size_t cfrom = c->pop_calls.size();
+    c->pop_calls.resize(cfrom + src.size() * S);
+    ngsep_sample_call* dst = c->pop_calls.data() + cfrom;
+    parallel_for((int64_t)src.size(), 64, [&](int64_t lo, int64_t hi) {
+        for (int64_t k = lo; k < hi; k++)
+            std::memcpy(dst + (size_t)k * S, calls + (size_t)src[(size_t)k] * S, S * sizeof(ngsep_sample_call));
+    });
     c->stats.candidates = ncand;
     c->stats.hard_sites = (int32_t)device_last_hard(c->dev);
     c->stats.exact_bound_passes = device_last_exact(c->dev);

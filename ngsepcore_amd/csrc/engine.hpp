@@ -54,6 +54,8 @@ constexpr int kScanThreads = 256;          // threads per tile-scan workgroup (o
 constexpr int kScanRegUnits = 64 * 24;     // tile-size budget: 16-byte units per tile (deeper tiles are rare)
 constexpr int kTileMaxPos = 1024;          // largest tile (positions): <= 64 units per row
 constexpr int kTileMinPos = 16;
+constexpr int kPopTile = 128;              // positions per KPM pile tile
+constexpr int kMcMaxCalls = 254;           // multisample candidate column: valid calls the bounds take (sums fit 32 bits)
 
 // K2 output record (device layout == ngsep_site_out, with gpos in .pos)
 static_assert(sizeof(ngsep_site_out) == 152, "site record layout");
@@ -211,35 +213,40 @@ struct CovDevice;   // coverage.hip
 void* pinned_alloc(size_t bytes);
 void pinned_free(void* p);
 
-// Called-site list (SingleSampleVariantPileupListener.calledVariants).  Backed by pinned host
-// memory so the per-run D2H copy lands in place, without a staging copy.
-struct SiteStore {
-    ngsep_site_out* buf = nullptr;
+// Record lists backed by pinned host memory, so a D2H copy lands in place without a staging copy:
+// the called sites (SingleSampleVariantPileupListener.calledVariants) and the population calls.
+template <class T>
+struct PinnedStore {
+    T* buf = nullptr;
     size_t n = 0, cap = 0;
-    SiteStore() = default;
-    SiteStore(const SiteStore&) = delete;
-    SiteStore& operator=(const SiteStore&) = delete;
-    ~SiteStore() { if (buf) pinned_free(buf); }
+    PinnedStore() = default;
+    PinnedStore(const PinnedStore&) = delete;
+    PinnedStore& operator=(const PinnedStore&) = delete;
+    ~PinnedStore() { if (buf) pinned_free(buf); }
     size_t size() const { return n; }
     bool empty() const { return n == 0; }
     void clear() { n = 0; }
-    ngsep_site_out* data() { return buf; }
-    ngsep_site_out& operator[](size_t i) { return buf[i]; }
-    const ngsep_site_out* begin() const { return buf; }
-    const ngsep_site_out* end() const { return buf + n; }
+    T* data() { return buf; }
+    const T* data() const { return buf; }
+    T& operator[](size_t i) { return buf[i]; }
+    const T& operator[](size_t i) const { return buf[i]; }
+    const T* begin() const { return buf; }
+    const T* end() const { return buf + n; }
     void reserve(size_t want) {
         if (want <= cap) return;
         size_t nc = cap ? cap : 4096;
         while (nc < want) nc *= 2;
-        auto* nb = static_cast<ngsep_site_out*>(pinned_alloc(nc * sizeof(ngsep_site_out)));
-        if (n) std::memcpy(nb, buf, n * sizeof(ngsep_site_out));
+        auto* nb = static_cast<T*>(pinned_alloc(nc * sizeof(T)));
+        if (n) std::memcpy(nb, buf, n * sizeof(T));
         if (buf) pinned_free(buf);
         buf = nb;
         cap = nc;
     }
-    void push_back(const ngsep_site_out& o) { reserve(n + 1); buf[n++] = o; }
-    void swap(SiteStore& o) { std::swap(buf, o.buf); std::swap(n, o.n); std::swap(cap, o.cap); }
+    void resize(size_t want) { reserve(want); n = want; }          // new records are not initialised
+    void push_back(const T& o) { reserve(n + 1); buf[n++] = o; }
+    void swap(PinnedStore& o) { std::swap(buf, o.buf); std::swap(n, o.n); std::swap(cap, o.cap); }
 };
+using SiteStore = PinnedStore<ngsep_site_out>;
 
 // a read of the single-sample layout: global [gfirst, glast] and its projected bytes
 struct SRead {
@@ -265,13 +272,20 @@ struct Staged {            // everything resident for one run
     std::vector<int32_t> h_reads;       // 4 ints per read: gfirst, glast, slot, flags
                                         //   flags: bit0 negative strand, bits 1-7 read-group rank,
                                         //   bits 8-23 sample + 1 (0: no sample) -- multisample only
-    // multisample: per-sample tile blocks (tile t, sample s: rows[t*S+s] x T bytes at toff[t] + ...)
+    // multisample (engine.cpp build_columns_multi): the (sample, position) columns holding a valid call of
+    // another allele -- global position, number of valid calls (255: deeper than kMcMaxCalls, no bytes),
+    // their bytes in h_pile, the byte offset of every 64th entry's column
     int32_t n_samples = 0;
-    std::vector<uint16_t> h_rows;
-    std::vector<int64_t> h_toff;
-    // multisample: reads grouped by (sample, read-group rank) bucket for the population kernel
-    std::vector<int32_t> h_perm, h_bseg, h_blb, h_bbase;
-    int64_t nblk_b = 0;
+    int64_t mc_entries = 0;
+    std::vector<int32_t> h_mc_pos;
+    std::vector<uint8_t> h_mc_n;
+    std::vector<int64_t> h_mc_gbase;
+    // multisample: KPM's pile -- per (tile of kPopTile positions, sample + the reads of no sample) block of
+    // rows x kPopTile code bytes, position-major (column p at pboff + p * rows), in getAlleleCalls order
+    std::unique_ptr<uint8_t[]> h_ppile;
+    std::vector<uint16_t> h_prow;       // rows per (tile, sample): h_prow[t * (S + 1) + s]
+    std::vector<int64_t> h_pboff;       // block offsets, same index (+ the total at the end)
+    int64_t ppile_bytes = 0;
     std::vector<uint8_t> h_ref;
     // single-sample layout (engine.cpp build_single_layout): the valid-call plane, position-major byte
     // pile in pending-list rank order, strand bits of its cells -- in the context's pinned LayoutArena --
@@ -401,7 +415,7 @@ struct ngsep_ctx {
     std::vector<std::pair<int32_t, std::pair<int64_t, int64_t>>> carved;
     int pending_sync = 0;                         // multisample runs submitted, not yet collected
     std::vector<ngsep_popsite_out> pop_sites;     // (sequence, position) order
-    std::vector<ngsep_sample_call> pop_calls;     // pop_sites.size() x n_samples
+    ngsep::PinnedStore<ngsep_sample_call> pop_calls;     // pop_sites.size() x n_samples
     ngsep_stats stats{};
 };
 
@@ -431,11 +445,12 @@ int device_submit(Device* d, const Staged& s, const LikTables& t, const Genotype
 int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, double* geno_ms, double* total_ms,
                    int64_t* n_candidates, std::string& err);
 int64_t device_inflight(const Device* d);
-// multisample: tile scan over the per-sample blocks + population genotyping of the queued
-// positions; appends the sites (global positions, unordered) and their calls
+// multisample: scan over the candidate columns + population genotyping of the queued positions; the
+// sites (global positions, unordered) and their calls (n_samples per site) in the device's pinned
+// staging buffers, valid until the next run
 int device_run_multi(Device* d, const Staged& s, const LikTables& t, const GenotypeParams& g,
-                     const std::vector<int8_t>& sample_nrank, double min_adf, int ploidy,
-                     std::vector<ngsep_popsite_out>* sites, std::vector<ngsep_sample_call>* calls,
+                     int32_t n_samples, double min_adf, int ploidy,
+                     const ngsep_popsite_out** sites, const ngsep_sample_call** calls, int64_t* n_sites,
                      double* scan_ms, double* geno_ms, double* total_ms, int64_t* n_candidates, std::string& err);
 // RelativeAlleleCountsCalculator over positions [g0, g1) of the resident single-sample layout: hist_out[0..51)
 // the proportion bins, [51..61) the number-of-alleles bins; the proportion's sum and sum of squares

@@ -80,7 +80,6 @@ struct Device {
     bool time_posterior = std::getenv("NGSEP_TIME_POSTERIOR") != nullptr;
     bool time_scan = std::getenv("NGSEP_NO_SCAN_TIMING") == nullptr;   // diagnostics: without KT's events
     hipEvent_t ev[4] = {};
-    uint8_t* d_slots = nullptr;      // multisample: read-major SoA
     uint8_t* d_pile = nullptr;       // single sample: position-major byte pile; multisample: per-sample blocks
     uint32_t* d_planes = nullptr;    // single sample: valid-call plane of the pile (KT)
     uint16_t* d_olist = nullptr;     // single sample: other-allele call positions per tile (KT)
@@ -92,17 +91,19 @@ struct Device {
     size_t cap_pile = 0, cap_planes = 0, cap_cneg = 0, cap_ref = 0, cap_tinfo = 0, cap_wins = 0;
     int32_t n_wins = 0;
     int32_t planes_W = 0;            // words per plane row (T / 32)
-    int4* d_reads = nullptr;
     uint8_t* d_ref = nullptr;
     TileInfo* d_tinfo = nullptr;
-    uint16_t* d_rows = nullptr;      // multisample: rows per (tile, sample)
-    int64_t* d_toff = nullptr;       // multisample: block offset per tile
-    int8_t* d_nrank = nullptr;       // multisample: read groups per sample
-    int32_t* d_perm = nullptr;       // multisample: read indexes grouped by (sample, read-group rank) bucket
-    int32_t* d_bseg = nullptr;       // bucket b = perm[bseg[b] .. bseg[b+1])
-    int32_t* d_blb = nullptr;        // per bucket and 64-position block: first perm index that can cover it
-    int32_t* d_bbase = nullptr;      // sample s = buckets bbase[s] .. bbase[s+1]; sample n_samples = reads of no sample
-    int64_t nblk_b = 0;
+    int32_t* d_mc_pos = nullptr;     // multisample: candidate columns' global positions (KTM)
+    uint8_t* d_mc_n = nullptr;       //   their valid-call counts
+    int64_t* d_mc_gbase = nullptr;   //   byte offset of every 64th column
+    uint32_t* d_need = nullptr;      //   open positions, a bit per global position
+    int64_t mc_entries = 0;
+    ngsep_popsite_out* h_psites = nullptr;      // multisample: pinned staging of the emitted sites and calls
+    ngsep_sample_call* h_pcalls = nullptr;
+    int64_t cap_h_psites = 0, cap_h_pcalls = 0;
+    uint8_t* d_ppile = nullptr;      // multisample: KPM's position-major per-(tile, sample) pile
+    uint16_t* d_prow = nullptr;      //   rows per block
+    int64_t* d_pboff = nullptr;      //   block offsets
     int32_t n_samples = 0;
     ngsep_popsite_out* d_psites = nullptr;
     ngsep_sample_call* d_pcalls = nullptr;
@@ -117,8 +118,8 @@ struct Device {
     unsigned long long* d_counters = nullptr;
     unsigned long long* h_counters = nullptr;
     int64_t cap_sites = 0;
-    int64_t n_units = 0, n_slots = 0, n_reads = 0, g_len = 0, n_tiles = 0;
-    int32_t slot_size = 0, max_span = 0, pad = 0, tile = 512, log2_tile = 9;
+    int64_t n_reads = 0, g_len = 0, n_tiles = 0;
+    int32_t max_span = 0, pad = 0, tile = 512, log2_tile = 9;
     int64_t last_n_sites = 1024;
     int64_t last_hard = 0;
     int64_t last_exact = 0;     // wave passes of KT's exact integer bound in the last run
@@ -853,208 +854,117 @@ __global__ __launch_bounds__(256) void k_queue_all(const uint8_t* __restrict__ r
 }
 
 // ------------------------------------------------------------------------------------------
-// KTM: multisample tile scan -- one wavefront per tile, the samples in turn
+// KTM: multisample scan over the candidate columns -- one wavefront per 64 columns
 // ------------------------------------------------------------------------------------------
-// Tile t holds one block per sample (rows[t*S+s] x T code bytes, consecutive from toff[t]).  The wave
-// streams each sample's block as KT streams a tile and bounds every candidate with that SAMPLE's
-// calls: a sample the bounds prove hom-ref cannot make a decided non-reference call
-// (SingleSampleVariantPileupListener.genotypeVariantSample, :361-391, evaluates the same posterior),
-// and a position where every sample is proven hom-ref gets variant QS 0, which
-// MultisampleVariantsDetector.onPileup never writes (:534).  The other positions are queued for KPM.
-constexpr int kScanChunkMulti = 8;      // a sample's block at 10x is a few wave-loads: one chunk
-__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(3)))
-void k_tile_pileup_multi(const u32x4* __restrict__ pile, const int64_t* __restrict__ toff,
-                         const uint16_t* __restrict__ rows_ts, int32_t n_samples, const uint8_t* __restrict__ ref,
-                         int32_t log2T, int64_t n_tiles, const LikTables* __restrict__ tabs, GenotypeParams gp,
-                         QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap) {
-    __shared__ ScanShared sh;
+// A column is one sample's valid calls at one position that holds a valid call of another allele than the
+// reference (engine.cpp build_columns_multi); every other (sample, position) is hom-ref by §5.  The lane
+// adds its column's calls into the exact integer bound and keeps the position open unless the bound proves
+// the sample hom-ref: such a sample cannot make a decided non-reference call
+// (SingleSampleVariantPileupListener.genotypeVariantSample, :361-391, evaluates the same posterior), and a
+// position where every sample is proven hom-ref gets variant QS 0, which MultisampleVariantsDetector.onPileup
+// never writes (:534).  Open positions are ORed into a bit per global position; KQN queues them for KPM.
+// The 64 columns of a group are consecutive bytes, so the wave's dword loads are coalesced.
+__global__ __launch_bounds__(256)
+void k_scan_multi(const int32_t* __restrict__ mc_pos, const uint8_t* __restrict__ mc_n, const int64_t* __restrict__ mc_gbase,
+                  const uint8_t* __restrict__ cols, int64_t n_entries, const LikTables* __restrict__ tabs, GenotypeParams gp,
+                  uint32_t* __restrict__ need, unsigned long long* __restrict__ counters) {
+    __shared__ unsigned long long w[2][32];
+    __shared__ unsigned long long s_ne[4];
     const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (threadIdx.x < 64) sh.w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
+    const int wv = threadIdx.x >> 6;
+    if (threadIdx.x < 64) w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
     __syncthreads();
-    const int log2U = log2T - 4;
-    const uint32_t U = 1u << log2U;
-    const int col = lane & (int)(U - 1);
-    const bool lead = lane < (int)U;
     const bool bound_on = gp.use_bound != 0;
     const long long th = tabs->t_het, to = tabs->t_homo;
     const int32_t maxq = gp.max_q;
-    int32_t qn = 0;
-    unsigned long long ncand = 0;
-    uint32_t nexact = 0;
-    // one workgroup per tile: its waves take the samples in turn (s % 4 == wave) and OR their open
-    // positions in LDS, so a tile's samples are scanned in parallel
-    static_assert(kScanWaves == 4, "the open-position OR below combines four waves");
-    __shared__ uint32_t s_need[kScanWaves][64];
-    for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
-        int64_t base = toff[t];
-        base = ((int64_t)__builtin_amdgcn_readfirstlane((int32_t)(base >> 32)) << 32) |
-               (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)base);
-        const int32_t tstart = (int32_t)(t << log2T);
-        const u32x4 rc = *reinterpret_cast<const u32x4*>(ref + tstart + col * 16);
-        const uint32_t ok = nib4(rc.x & 0x80808080u) | (nib4(rc.y & 0x80808080u) << 4) |
-                            (nib4(rc.z & 0x80808080u) << 8) | (nib4(rc.w & 0x80808080u) << 12);
-        uint32_t need = 0;      // positions with a sample the bounds leave open (same in every lane of a column)
-        for (int32_t s0 = 0; s0 < n_samples; s0 += 64) {
-            const int32_t myrows = s0 + lane < n_samples ? (int32_t)rows_ts[t * n_samples + s0 + lane] : 0;
-            const int32_t nsb = n_samples - s0 < 64 ? n_samples - s0 : 64;
-            int32_t incl = myrows;                       // block offsets: prefix of rows over the samples
-            for (int o = 1; o < 64; o <<= 1) {
-                const int32_t v = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += v;
-            }
-            const int32_t excl = incl - myrows;
-            const int32_t btot = __shfl(incl, 63, 64);
-            for (int j = wv; j < nsb; j += kScanWaves) {
-                const int32_t rows = __builtin_amdgcn_readlane(myrows, j);
-                if (rows == 0) continue;
-                const int32_t nunits = rows << log2U;
-                const int64_t off = base + ((int64_t)__builtin_amdgcn_readlane(excl, j) << log2T);
-                const u32x4* blk = pile + (off >> 4);
-                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)blk, 0, nunits * 16, 0x00020000);
-                const bool counted = rows <= 255;
-                uint32_t hits = 0;
-                uint32_t cv0 = 0, cv1 = 0, cv2 = 0, cv3 = 0, ca0 = 0, ca1 = 0, ca2 = 0, ca3 = 0;
-                auto cnt = [](uint32_t w, uint32_t& cv, uint32_t& ca) {
-                    const uint32_t v = w & 0x80808080u;
-                    const uint32_t n = ((w & 0x60606060u) + 0x60606060u) & v;
-                    cv += v >> 7;
-                    ca += n >> 7;
-                };
-                for (int32_t u0 = 0; u0 < nunits; u0 += kScanChunkMulti * 64) {
-                    u32x4 R[kScanChunkMulti];
-#pragma unroll
-                    for (int k = 0; k < kScanChunkMulti; k++)
-                        R[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u0 + k * 64 + lane) * 16, 0, 0));
-                    if (counted) {
-#pragma unroll
-                        for (int k = 0; k < kScanChunkMulti; k++) {
-                            cnt(R[k].x, cv0, ca0); cnt(R[k].y, cv1, ca1); cnt(R[k].z, cv2, ca2); cnt(R[k].w, cv3, ca3);
-                        }
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < kScanChunkMulti; k++) hits |= unit_hits<0>(R[k]);
-                    }
-                }
-                if (counted) {
-                    for (int sft = (int)U; sft < 64; sft <<= 1) {
-                        cv0 += __shfl_xor(cv0, sft, 64); cv1 += __shfl_xor(cv1, sft, 64);
-                        cv2 += __shfl_xor(cv2, sft, 64); cv3 += __shfl_xor(cv3, sft, 64);
-                        ca0 += __shfl_xor(ca0, sft, 64); ca1 += __shfl_xor(ca1, sft, 64);
-                        ca2 += __shfl_xor(ca2, sft, 64); ca3 += __shfl_xor(ca3, sft, 64);
-                    }
-                    auto nz = [](uint32_t w) -> uint32_t { return nib4((((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u); };
-                    hits = nz(ca0) | (nz(ca1) << 4) | (nz(ca2) << 8) | (nz(ca3) << 12);
-                } else {
-                    for (int sft = (int)U; sft < 64; sft <<= 1) hits |= __shfl_xor(hits, sft, 64);
-                }
-                uint32_t cm = hits & ok & ~need;
-                if (lead) ncand += (unsigned long long)__popc(cm);
-                if (gp.ablate & 1) continue;
-                const bool bound = bound_on && counted;
-                if (bound && __ballot(cm != 0)) {
-                    const u32x4 nref = {cv0 - ca0, cv1 - ca1, cv2 - ca2, cv3 - ca3}, nalt = {ca0, ca1, ca2, ca3};
-                    uint32_t c = cm;
-                    while (c) {
-                        const int k = __builtin_ctz(c);
-                        c &= c - 1u;
-                        const long long nr = (unit_dword(nref, k >> 2) >> (8 * (k & 3))) & 0xFFu;
-                        const long long na = (unit_dword(nalt, k >> 2) >> (8 * (k & 3))) & 0xFFu;
-                        if (nr * tabs->c_r1 - na * tabs->c_x1 > th && nr * tabs->c_r2 - na * tabs->c_x2 > to &&
-                            nr * tabs->c_r2 - na * tabs->c_x1 > th)
-                            cm &= ~(1u << k);
-                    }
-                }
-                while (__ballot(cm != 0)) {
-                    const bool has = cm != 0;
-                    const int k = has ? __builtin_ctz(cm) : 0;
-                    cm &= cm - 1u;
-                    const int sel = k >> 2, shb = 8 * (k & 3);
-                    bool keep = has;
-                    if (bound) {
-                        unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-                        auto add = [&](const u32x4 d) {
-                            const uint32_t cd = (unit_dword(d, sel) >> shb) & 0xFFu;
-                            if (cd & 0x80u) {
-                                const uint32_t a = (cd >> 5) & 3u;
-                                int q = (int)(cd & 31u);
-                                q = q > maxq ? maxq : q;
-                                const unsigned long long w = sh.w[a == 0 ? 0 : 1][q];
-                                a0 += a == 0 ? w : 0ull;
-                                a1 += a == 1 ? w : 0ull;
-                                a2 += a == 2 ? w : 0ull;
-                                a3 += a == 3 ? w : 0ull;
-                            }
-                        };
-                        nexact++;
-                        for (int32_t u0 = 0; u0 < nunits; u0 += kScanChunkMulti * 64) {
-                            u32x4 R[kScanChunkMulti];
-#pragma unroll
-                            for (int kk = 0; kk < kScanChunkMulti; kk++)
-                                R[kk] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u0 + kk * 64 + lane) * 16, 0, 0));
-#pragma unroll
-                            for (int kk = 0; kk < kScanChunkMulti; kk++) add(R[kk]);
-                        }
-                        for (int sft = (int)U; sft < 64; sft <<= 1) {
-                            a0 += __shfl_xor(a0, sft, 64);
-                            a1 += __shfl_xor(a1, sft, 64);
-                            a2 += __shfl_xor(a2, sft, 64);
-                            a3 += __shfl_xor(a3, sft, 64);
-                        }
-                        const long long R1 = (long long)(a0 & 0xFFFFFFFFull), R2 = (long long)(a0 >> 32);
-                        const long long x1 = (long long)(a1 & 0xFFFFFFFFull), y1 = (long long)(a2 & 0xFFFFFFFFull);
-                        const long long z1 = (long long)(a3 & 0xFFFFFFFFull);
-                        const long long x2 = (long long)(a1 >> 32), y2 = (long long)(a2 >> 32), z2 = (long long)(a3 >> 32);
-                        const bool drop = (R1 - x1 > th) && (R1 - y1 > th) && (R1 - z1 > th) &&
-                                          (R2 - x2 > to) && (R2 - y2 > to) && (R2 - z2 > to) &&
-                                          (R2 - x1 - y1 > th) && (R2 - x1 - z1 > th) && (R2 - y1 - z1 > th);
-                        keep = has && !drop;
-                    }
-                    if (keep) need |= 1u << k;
-                }
-            }
-            base += (int64_t)btot << log2T;
+    const uint32_t* cw = reinterpret_cast<const uint32_t*>(cols);
+    const int64_t ngroups = (n_entries + 63) >> 6;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    unsigned long long nexact = 0;
+    for (int64_t grp = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv; grp < ngroups; grp += nwaves) {
+        const int64_t i = (grp << 6) + lane;
+        const bool has = i < n_entries;
+        const int32_t pos = has ? mc_pos[i] : 0;
+        const uint32_t n = has ? (uint32_t)mc_n[i] : 0u;
+        const uint32_t nb = n == 255u ? 0u : n;
+        uint32_t incl = nb;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
         }
-        s_need[wv][lane] = need;
-        __syncthreads();
-        need = s_need[0][lane] | s_need[1][lane] | s_need[2][lane] | s_need[3][lane];
-        if (wv != 0) need = 0;                           // wave 0 queues the tile's open positions
-        __syncthreads();
-        // queue the open positions (the lead lane of each column)
-        while (__ballot(need != 0)) {
-            const bool has = need != 0;
-            const int k = has ? __builtin_ctz(need) : 0;
-            need &= need - 1u;
-            const bool emit = has && lead;
-            const unsigned long long m = __ballot(emit);
-            if (!m) continue;
-            const int32_t nm = __popcll(m);
-            if (qn + nm > kWaveQ) { wave_flush(sh, wv, lane, qn, queue, counters, qcap); qn = 0; }
-            if (emit) {
-                const int32_t idx = qn + __popcll(m & ((1ull << lane) - 1ull));
-                const uint32_t rcode = (unit_dword(rc, k >> 2) >> (8 * (k & 3))) & 0xFFu;
-                sh.q[wv][idx] = QueueSite{tstart + col * 16 + k, (int32_t)rcode};
+        int64_t gb = mc_gbase[grp];
+        gb = ((int64_t)__builtin_amdgcn_readfirstlane((int32_t)(gb >> 32)) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)gb);
+        const int64_t start = gb + (int64_t)(incl - nb), end = start + nb;
+        bool keep = has;
+        if (has && bound_on && n != 255u) {
+            unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+            for (int64_t d = start >> 2; d < (end + 3) >> 2; d++) {
+                const uint32_t word = cw[d];
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const int64_t at = d * 4 + b;
+                    if (at < start || at >= end) continue;
+                    const uint32_t cd = (word >> (8 * b)) & 0xFFu;
+                    const uint32_t al = (cd >> 5) & 3u;
+                    int q = (int)(cd & 31u);
+                    q = q > maxq ? maxq : q;
+                    const unsigned long long wt = w[al == 0 ? 0 : 1][q];
+                    a0 += al == 0 ? wt : 0ull;
+                    a1 += al == 1 ? wt : 0ull;
+                    a2 += al == 2 ? wt : 0ull;
+                    a3 += al == 3 ? wt : 0ull;
+                }
             }
-            qn += nm;
+            const long long R1 = (long long)(a0 & 0xFFFFFFFFull), R2 = (long long)(a0 >> 32);
+            const long long x1 = (long long)(a1 & 0xFFFFFFFFull), y1 = (long long)(a2 & 0xFFFFFFFFull);
+            const long long z1 = (long long)(a3 & 0xFFFFFFFFull);
+            const long long x2 = (long long)(a1 >> 32), y2 = (long long)(a2 >> 32), z2 = (long long)(a3 >> 32);
+            const bool drop = (R1 - x1 > th) && (R1 - y1 > th) && (R1 - z1 > th) &&
+                              (R2 - x2 > to) && (R2 - y2 > to) && (R2 - z2 > to) &&
+                              (R2 - x1 - y1 > th) && (R2 - x1 - z1 > th) && (R2 - y1 - z1 > th);
+            keep = !drop;
+            nexact++;
         }
+        if (keep) atomicOr(&need[pos >> 5], 1u << (pos & 31));
     }
-    for (int sft = 1; sft < 64; sft <<= 1) ncand += __shfl_xor(ncand, sft, 64);
-    if (lane == 0) { sh.qn[wv] = qn; sh.ncand[wv] = ncand; sh.nexact[wv] = nexact; }
+    for (int sft = 1; sft < 64; sft <<= 1) nexact += __shfl_xor(nexact, sft, 64);
+    if (lane == 0) s_ne[wv] = nexact;
     __syncthreads();
     if (threadIdx.x == 0) {
-        int32_t tot = 0;
-        unsigned long long nc = 0, ne = 0;
-        for (int w = 0; w < kScanWaves; w++) { sh.qbase[w] = tot; tot += sh.qn[w]; nc += sh.ncand[w]; ne += sh.nexact[w]; }
+        unsigned long long ne = 0;
+        for (int k = 0; k < (int)(blockDim.x >> 6); k++) ne += s_ne[k];
         if (ne) atomicAdd(&counters[3], ne);
-        const unsigned long long base = tot ? atomicAdd(&counters[2], (unsigned long long)tot) : 0ull;
-        for (int w = 0; w < kScanWaves; w++) sh.qbase[w] += (int32_t)base;
-        if (nc) atomicAdd(&counters[1], nc);
     }
-    __syncthreads();
-    {
-        const int64_t base = sh.qbase[wv];
-        for (int i = lane; i < qn; i += 64)
-            if (base + i < qcap) queue[base + i] = sh.q[wv][i];
+}
+
+// KQN: the open positions (a bit per global position) into the KPM queue, {position, reference code}
+__global__ __launch_bounds__(256) void k_queue_need(const uint32_t* __restrict__ need, const uint8_t* __restrict__ ref, int64_t nwords,
+                                                    QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap) {
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < nwords; base += stride) {
+        const int64_t i = base + threadIdx.x;
+        uint32_t m = i < nwords ? need[i] : 0u;
+        const uint32_t c = (uint32_t)__popc(m);
+        uint32_t incl = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        const uint32_t tot = __shfl(incl, 63, 64);
+        if (!tot) continue;
+        unsigned long long q0 = 0;
+        if (lane == 63) q0 = atomicAdd(&counters[2], (unsigned long long)tot);
+        q0 = __shfl(q0, 63, 64);
+        int64_t at = (int64_t)q0 + (incl - c);
+        while (m) {
+            const int b = __builtin_ctz(m);
+            m &= m - 1u;
+            const int64_t g = i * 32 + b;
+            if (at < qcap) queue[at] = QueueSite{(int32_t)g, (int32_t)ref[g]};
+            at++;
+        }
     }
 }
 
@@ -1069,6 +979,8 @@ void k_tile_pileup_multi(const u32x4* __restrict__ pile, const int64_t* __restri
 // VariantDiscoverySNVQAlgorithm.genotypeSNV, :21-97); the multi-allelic loop (discoverPopulationSNV,
 // :585-597, makeNewVariant :642-656) and the variant QS (genotypeVariant, :674-693) are block reductions.
 constexpr int kPopThreads = 256;
+constexpr int kPopTileLog2 = 7;
+static_assert((1 << kPopTileLog2) == kPopTile, "KPM pile tile");
 static_assert(kPopThreads >= kMaxSamplesDevice, "one thread per sample");
 
 struct PopCall {
@@ -1230,9 +1142,8 @@ __device__ PopCall genotype_sample_d(const double* L, const int* cnt, int total,
 
 __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
     const QueueSite* __restrict__ queue, const unsigned long long* qn, int64_t qcap,
-    const int4* __restrict__ reads, const int32_t* __restrict__ perm, const int32_t* __restrict__ bseg,
-    const int32_t* __restrict__ blb, int64_t nblk, const int32_t* __restrict__ bbase,
-    const uint8_t* __restrict__ slots, int32_t S, const LikTables* __restrict__ tabs, GenotypeParams gp,
+    const uint8_t* __restrict__ ppile, const uint16_t* __restrict__ prow, const int64_t* __restrict__ pboff,
+    const LikTables* __restrict__ tabs, GenotypeParams gp,
     int32_t n_samples, double min_adf, int32_t ploidy,
     ngsep_popsite_out* __restrict__ sites, ngsep_sample_call* __restrict__ calls,
     unsigned long long* counters, int64_t cap, unsigned long long* __restrict__ stamps) {
@@ -1256,55 +1167,43 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
         const uint32_t rc = (uint32_t)qs.rc;
         if (tid == 0) { s_pc[0] = s_pc[1] = s_pc[2] = s_pc[3] = 0; s_tot = 0; s_called = 0; s_qs = 0; }
         __syncthreads();
-        // 1-3. thread s walks sample s's reads (bucket = sample, read-group rank: the order of
-        //      PileupRecord.getAlleleCalls(span, readGroups), :104-111, pending order inside a group)
-        //      that can cover gpos, 8 in flight; thread n_samples walks the reads of no sample, which
-        //      only enter the pooled counts (getAlleleCalls(1, null))
+        // 1-3. thread s walks sample s's column of the pile (read-group rank order, pending order inside:
+        //      PileupRecord.getAlleleCalls(span, readGroups), :104-111), 8 codes in flight; thread n_samples
+        //      walks the column of the reads of no sample, which only enter the pooled counts
+        //      (getAlleleCalls(1, null))
         int total = 0;
         int cnt[4] = {0, 0, 0, 0};
         double L[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         if (tid <= n_samples) {
-            const int b0 = bbase[tid], b1 = bbase[tid + 1];
+            const int64_t bi = (int64_t)(gpos >> kPopTileLog2) * (n_samples + 1) + tid;
+            const int32_t rows = prow[bi];
+            const uint8_t* col = ppile + pboff[bi] + (int64_t)(gpos & (kPopTile - 1)) * rows;
             const bool tally = tid < n_samples;
-            for (int b = b0; b < b1; b++) {
-                const int32_t kend = bseg[b + 1];
-                bool more = true;
-                for (int32_t k0 = blb[(int64_t)b * nblk + (gpos >> 6)]; more && k0 < kend; k0 += 8) {
-                    int4 h[8];
+            for (int32_t r0 = 0; r0 < rows; r0 += 8) {
+                uint32_t code[8];
 #pragma unroll
-                    for (int k = 0; k < 8; k++) h[k] = reads[perm[k0 + k < kend ? k0 + k : kend - 1]];
-                    uint32_t code[8];
+                for (int k = 0; k < 8; k++) code[k] = r0 + k < rows ? (uint32_t)col[r0 + k] : 0u;
 #pragma unroll
-                    for (int k = 0; k < 8; k++) {
-                        const bool in = k0 + k < kend && h[k].x <= gpos;
-                        if (!in) more = false;
-                        const bool cov = in && h[k].y >= gpos;
-                        const int32_t o = cov ? gpos - h[k].x : 0;
-                        const uint32_t cd = slots[(int64_t)(h[k].z + o / S) * S + (o % S)];
-                        code[k] = cov ? cd : 0u;
-                    }
-#pragma unroll
-                    for (int k = 0; k < 8; k++) {
-                        const uint32_t cd = code[k];
-                        total += cd != 0;                                  // CountsHelper.java:210
-                        if (!(cd & 0x80u)) continue;                       // q<=3 or not A/C/G/T (:214-221)
-                        const uint32_t a = (cd >> 5) & 3u;
-                        cnt[0] += a == 0; cnt[1] += a == 1; cnt[2] += a == 2; cnt[3] += a == 3;
-                        if (!tally) continue;
-                        int q = (int)(cd & 31u);
-                        q = q > gp.max_q ? gp.max_q : q;                   // -maxBaseQS (:217-219)
-                        const double A = s_t[0][q], H = s_t[1][q], E = s_t[2][q];
-                        L[0] += a == 0 ? A : E;
-                        L[4] += a == 1 ? A : E;
-                        L[7] += a == 2 ? A : E;
-                        L[9] += a == 3 ? A : E;
-                        L[1] += a <= 1 ? H : E;
-                        L[2] += (a & 1) == 0 ? H : E;
-                        L[3] += (a == 0 || a == 3) ? H : E;
-                        L[5] += (a == 1 || a == 2) ? H : E;
-                        L[6] += (a & 1) == 1 ? H : E;
-                        L[8] += a >= 2 ? H : E;
-                    }
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t cd = code[k];
+                    total += cd != 0;                                  // CountsHelper.java:210
+                    if (!(cd & 0x80u)) continue;                       // q<=3 or not A/C/G/T (:214-221)
+                    const uint32_t a = (cd >> 5) & 3u;
+                    cnt[0] += a == 0; cnt[1] += a == 1; cnt[2] += a == 2; cnt[3] += a == 3;
+                    if (!tally) continue;
+                    int q = (int)(cd & 31u);
+                    q = q > gp.max_q ? gp.max_q : q;                   // -maxBaseQS (:217-219)
+                    const double A = s_t[0][q], H = s_t[1][q], E = s_t[2][q];
+                    L[0] += a == 0 ? A : E;
+                    L[4] += a == 1 ? A : E;
+                    L[7] += a == 2 ? A : E;
+                    L[9] += a == 3 ? A : E;
+                    L[1] += a <= 1 ? H : E;
+                    L[2] += (a & 1) == 0 ? H : E;
+                    L[3] += (a == 0 || a == 3) ? H : E;
+                    L[5] += (a == 1 || a == 2) ? H : E;
+                    L[6] += (a & 1) == 1 ? H : E;
+                    L[8] += a >= 2 ? H : E;
                 }
             }
         }
@@ -1624,7 +1523,6 @@ void device_release(Device* d) {
     (void)hipDeviceSynchronize();                    // uncollected runs are dropped
     for (auto& sl : d->slot) sl.busy = false;
     d->n_collected = d->n_submitted;
-    (void)hipFree(d->d_slots); d->d_slots = nullptr;
     (void)hipFree(d->d_pile); d->d_pile = nullptr;
     (void)hipFree(d->d_planes); d->d_planes = nullptr;
     (void)hipFree(d->d_olist); d->d_olist = nullptr;
@@ -1634,18 +1532,17 @@ void device_release(Device* d) {
     (void)hipFree(d->d_wins); d->d_wins = nullptr;
     d->n_wins = 0;
     d->planes_W = 0;
-    (void)hipFree(d->d_reads); d->d_reads = nullptr;
     (void)hipFree(d->d_ref); d->d_ref = nullptr;
     (void)hipFree(d->d_tinfo); d->d_tinfo = nullptr;
-    (void)hipFree(d->d_rows); d->d_rows = nullptr;
-    (void)hipFree(d->d_toff); d->d_toff = nullptr;
-    (void)hipFree(d->d_nrank); d->d_nrank = nullptr;
-    (void)hipFree(d->d_perm); d->d_perm = nullptr;
-    (void)hipFree(d->d_bseg); d->d_bseg = nullptr;
-    (void)hipFree(d->d_blb); d->d_blb = nullptr;
-    (void)hipFree(d->d_bbase); d->d_bbase = nullptr;
+    (void)hipFree(d->d_mc_pos); d->d_mc_pos = nullptr;
+    (void)hipFree(d->d_mc_n); d->d_mc_n = nullptr;
+    (void)hipFree(d->d_mc_gbase); d->d_mc_gbase = nullptr;
+    (void)hipFree(d->d_need); d->d_need = nullptr;
+    (void)hipFree(d->d_ppile); d->d_ppile = nullptr;
+    (void)hipFree(d->d_prow); d->d_prow = nullptr;
+    (void)hipFree(d->d_pboff); d->d_pboff = nullptr;
     d->n_samples = 0;
-    d->n_units = d->n_slots = d->n_reads = d->g_len = d->n_tiles = 0;
+    d->n_reads = d->g_len = d->n_tiles = 0;
     d->cap_pile = d->cap_planes = d->cap_cneg = d->cap_ref = d->cap_tinfo = d->cap_wins = 0;
 }
 
@@ -1681,6 +1578,8 @@ void device_destroy(Device* d) {
     }
     (void)hipFree(d->d_psites);
     (void)hipFree(d->d_pcalls);
+    if (d->h_psites) (void)hipHostFree(d->h_psites);
+    if (d->h_pcalls) (void)hipHostFree(d->h_pcalls);
     (void)hipFree(d->d_hard);
     (void)hipFree(d->d_counters);
     (void)hipFree(d->d_tables);
@@ -1696,7 +1595,7 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
     const int32_t pad = s.windows.empty() ? 64 : s.windows[0].pad;
     // single sample (a streamed window or a whole run): buffers kept across runs while large enough; the
     // multisample run starts from nothing
-    const bool keep = s.single && d->d_slots == nullptr && d->d_reads == nullptr;
+    const bool keep = s.single && d->d_ppile == nullptr;
     if (!keep) device_release(d);
     else HIP_TRY(hipDeviceSynchronize());          // the previous run is done reading them
     if (ensure_dev(&d->d_pile, &d->cap_pile, (size_t)s.pile_bytes + 64, keep, err) ||      // + 64: KP loads whole dwords of a column
@@ -1724,30 +1623,24 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
         if (!s.h_loff.empty()) HIP_TRY(hipMemcpyAsync(d->d_loff, s.h_loff.data(), s.h_loff.size() * sizeof(int32_t), hipMemcpyHostToDevice, d->stream));
         d->planes_W = s.tile / 32;
     } else {
-        // multisample: per-(tile, sample) blocks (KTM), the read-major SoA and its bucket index (KPM)
-        const int S = s.slot_size;
-        const int64_t slot_bytes = s.n_slots * (int64_t)S;
-        HIP_TRY(hipMalloc(&d->d_slots, (size_t)std::max<int64_t>(slot_bytes, 16)));
-        HIP_TRY(hipMalloc(&d->d_reads, (size_t)std::max<int64_t>(s.n_reads, 1) * sizeof(int4)));
-        if (slot_bytes) HIP_TRY(hipMemcpyAsync(d->d_slots, s.h_slots.data(), (size_t)slot_bytes, hipMemcpyHostToDevice, d->stream));
+        // multisample: the candidate columns (KTM), the position-major per-sample pile (KPM)
+        HIP_TRY(hipMalloc(&d->d_mc_pos, std::max<size_t>(s.h_mc_pos.size(), 1) * sizeof(int32_t)));
+        HIP_TRY(hipMalloc(&d->d_mc_n, std::max<size_t>(s.h_mc_n.size(), 1)));
+        HIP_TRY(hipMalloc(&d->d_mc_gbase, std::max<size_t>(s.h_mc_gbase.size(), 1) * sizeof(int64_t)));
+        HIP_TRY(hipMalloc(&d->d_need, (size_t)(s.g_len / 32 + 1) * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc(&d->d_ppile, (size_t)s.ppile_bytes + 64));
+        HIP_TRY(hipMalloc(&d->d_prow, std::max<size_t>(s.h_prow.size(), 1) * sizeof(uint16_t)));
+        HIP_TRY(hipMalloc(&d->d_pboff, std::max<size_t>(s.h_pboff.size(), 1) * sizeof(int64_t)));
         if (s.pile_bytes) HIP_TRY(hipMemcpyAsync(d->d_pile, s.h_pile.data(), (size_t)s.pile_bytes, hipMemcpyHostToDevice, d->stream));
-        if (s.n_reads) HIP_TRY(hipMemcpyAsync(d->d_reads, s.h_reads.data(), (size_t)s.n_reads * 16, hipMemcpyHostToDevice, d->stream));
-        HIP_TRY(hipMalloc(&d->d_rows, std::max<size_t>(s.h_rows.size(), 1) * sizeof(uint16_t)));
-        HIP_TRY(hipMalloc(&d->d_toff, std::max<size_t>(s.h_toff.size(), 1) * sizeof(int64_t)));
-        HIP_TRY(hipMalloc(&d->d_nrank, (size_t)std::max(s.n_samples, 1)));
-        if (!s.h_rows.empty()) HIP_TRY(hipMemcpyAsync(d->d_rows, s.h_rows.data(), s.h_rows.size() * sizeof(uint16_t), hipMemcpyHostToDevice, d->stream));
-        if (!s.h_toff.empty()) HIP_TRY(hipMemcpyAsync(d->d_toff, s.h_toff.data(), s.h_toff.size() * sizeof(int64_t), hipMemcpyHostToDevice, d->stream));
-        auto up32 = [&](int32_t** dst, const std::vector<int32_t>& v) -> int {
-            HIP_TRY(hipMalloc(dst, std::max<size_t>(v.size(), 1) * sizeof(int32_t)));
-            if (!v.empty()) HIP_TRY(hipMemcpyAsync(*dst, v.data(), v.size() * sizeof(int32_t), hipMemcpyHostToDevice, d->stream));
-            return 0;
-        };
-        if (up32(&d->d_perm, s.h_perm) || up32(&d->d_bseg, s.h_bseg) || up32(&d->d_blb, s.h_blb) || up32(&d->d_bbase, s.h_bbase)) return -1;
-        d->nblk_b = s.nblk_b;
+        if (!s.h_mc_pos.empty()) HIP_TRY(hipMemcpyAsync(d->d_mc_pos, s.h_mc_pos.data(), s.h_mc_pos.size() * sizeof(int32_t), hipMemcpyHostToDevice, d->stream));
+        if (!s.h_mc_n.empty()) HIP_TRY(hipMemcpyAsync(d->d_mc_n, s.h_mc_n.data(), s.h_mc_n.size(), hipMemcpyHostToDevice, d->stream));
+        if (!s.h_mc_gbase.empty()) HIP_TRY(hipMemcpyAsync(d->d_mc_gbase, s.h_mc_gbase.data(), s.h_mc_gbase.size() * sizeof(int64_t), hipMemcpyHostToDevice, d->stream));
+        HIP_TRY(hipMemcpyAsync(d->d_ppile, s.h_ppile.get(), (size_t)s.ppile_bytes + 64, hipMemcpyHostToDevice, d->stream));
+        if (!s.h_prow.empty()) HIP_TRY(hipMemcpyAsync(d->d_prow, s.h_prow.data(), s.h_prow.size() * sizeof(uint16_t), hipMemcpyHostToDevice, d->stream));
+        if (!s.h_pboff.empty()) HIP_TRY(hipMemcpyAsync(d->d_pboff, s.h_pboff.data(), s.h_pboff.size() * sizeof(int64_t), hipMemcpyHostToDevice, d->stream));
+        HIP_TRY(hipStreamSynchronize(d->stream));       // the host layout is freed after the upload
+        d->mc_entries = s.mc_entries;
         d->n_samples = s.n_samples;
-        d->n_units = slot_bytes / 16;
-        d->n_slots = s.n_slots;
-        d->slot_size = S;
     }
     d->n_reads = s.n_reads;
     d->g_len = s.g_len;
@@ -2120,15 +2013,14 @@ int device_run_rac(Device* d, const Staged& s, int64_t g0, int64_t g1, int32_t m
 // MultisampleVariantsDetector run: KTM over every resident tile, KPM over the queued positions,
 // D2H of the emitted sites and their per-sample calls (unordered; the host orders them)
 int device_run_multi(Device* d, const Staged& s, const LikTables& t, const GenotypeParams& g,
-                     const std::vector<int8_t>& sample_nrank, double min_adf, int ploidy,
-                     std::vector<ngsep_popsite_out>* sites, std::vector<ngsep_sample_call>* calls,
+                     int32_t n_samples, double min_adf, int ploidy,
+                     const ngsep_popsite_out** sites, const ngsep_sample_call** calls, int64_t* n_sites,
                      double* scan_ms, double* geno_ms, double* total_ms, int64_t* n_candidates, std::string& err) {
     HIP_TRY(hipSetDevice(d->ordinal));
     auto t0 = std::chrono::steady_clock::now();
     const int32_t S = d->n_samples;
-    if (S <= 0 || (int32_t)sample_nrank.size() != S) { err = "multisample run without samples (ngsep_set_samples)"; return -1; }
+    if (S <= 0 || n_samples != S) { err = "multisample run without samples (ngsep_set_samples)"; return -1; }
     if (S > kMaxSamplesDevice) { err = "too many samples for one device run"; return -1; }
-    HIP_TRY(hipMemcpyAsync(d->d_nrank, sample_nrank.data(), (size_t)S, hipMemcpyHostToDevice, d->stream));
     const bool timing = std::getenv("NGSEP_TIMING") != nullptr;
     if (timing && !d->d_stamps) HIP_TRY(hipMalloc(&d->d_stamps, 16 * sizeof(unsigned long long)));
     if (timing) HIP_TRY(hipMemsetAsync(d->d_stamps, 0, 16 * sizeof(unsigned long long), d->stream));
@@ -2156,23 +2048,24 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     unsigned long long* ctr = d->d_counters;
     HIP_TRY(hipMemsetAsync(ctr, 0, 4 * sizeof(unsigned long long), d->stream));
     // KTM and KPM are timed by events bound to their dispatches (ev 0-1 and 3-2)
-    if (d->n_tiles > 0) {
-        int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_tile_pileup_multi, kScanThreads, 0) != hipSuccess || per_cu < 1) per_cu = 2;
-        const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>(d->n_tiles, (int64_t)d->n_cu * per_cu));
-        hipExtLaunchKernelGGL(k_tile_pileup_multi, dim3((unsigned)nblk), dim3(kScanThreads), 0, d->stream, d->ev[0], d->ev[1], 0,
-                              (const u32x4*)d->d_pile, (const int64_t*)d->d_toff, (const uint16_t*)d->d_rows, S,
-                              (const uint8_t*)d->d_ref, d->log2_tile, d->n_tiles, (const LikTables*)d->d_tables, g, d->d_hard,
-                              ctr, d->cap_hard);
+    // KTM + KQN, timed together by events bound to their dispatches (ev 0-1), KPM by ev 3-2
+    const int64_t nwords = d->g_len / 32 + 1;
+    HIP_TRY(hipMemsetAsync(d->d_need, 0, (size_t)nwords * sizeof(uint32_t), d->stream));
+    {
+        const int64_t ngroups = (d->mc_entries + 63) / 64;
+        const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((ngroups + 3) / 4, (int64_t)d->n_cu * 8));
+        hipExtLaunchKernelGGL(k_scan_multi, dim3((unsigned)nblk), dim3(256), 0, d->stream, d->ev[0], nullptr, 0,
+                              (const int32_t*)d->d_mc_pos, (const uint8_t*)d->d_mc_n, (const int64_t*)d->d_mc_gbase,
+                              (const uint8_t*)d->d_pile, d->mc_entries, (const LikTables*)d->d_tables, g, d->d_need, ctr);
         HIP_TRY(hipGetLastError());
-    } else {
-        HIP_TRY(hipEventRecord(d->ev[0], d->stream));
-        HIP_TRY(hipEventRecord(d->ev[1], d->stream));
+        const int64_t qblk = std::max<int64_t>(1, std::min<int64_t>((nwords + 255) / 256, (int64_t)d->n_cu * 4));
+        hipExtLaunchKernelGGL(k_queue_need, dim3((unsigned)qblk), dim3(256), 0, d->stream, nullptr, d->ev[1], 0,
+                              (const uint32_t*)d->d_need, (const uint8_t*)d->d_ref, nwords, d->d_hard, ctr, d->cap_hard);
+        HIP_TRY(hipGetLastError());
     }
     hipExtLaunchKernelGGL(k_posterior_multi, dim3(2048), dim3(kPopThreads), 0, d->stream, d->ev[3], d->ev[2], 0,
-                          (const QueueSite*)d->d_hard, (const unsigned long long*)(ctr + 2), d->cap_hard, (const int4*)d->d_reads,
-                          (const int32_t*)d->d_perm, (const int32_t*)d->d_bseg, (const int32_t*)d->d_blb, d->nblk_b,
-                          (const int32_t*)d->d_bbase, (const uint8_t*)d->d_slots, d->slot_size, (const LikTables*)d->d_tables, g,
+                          (const QueueSite*)d->d_hard, (const unsigned long long*)(ctr + 2), d->cap_hard, (const uint8_t*)d->d_ppile,
+                          (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, (const LikTables*)d->d_tables, g,
                           S, min_adf, ploidy, d->d_psites, d->d_pcalls, ctr, d->cap_psites, d->d_stamps);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(d->h_counters, ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, d->stream));
@@ -2185,20 +2078,31 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
         d->d_hard = nullptr;
         HIP_TRY(hipMalloc(&d->d_hard, (size_t)(d->h_counters[2] + 1024) * sizeof(QueueSite)));
         d->cap_hard = (int64_t)d->h_counters[2] + 1024;
-        return device_run_multi(d, s, t, g, sample_nrank, min_adf, ploidy, sites, calls, scan_ms, geno_ms, total_ms, n_candidates, err);
+        return device_run_multi(d, s, t, g, n_samples, min_adf, ploidy, sites, calls, n_sites, scan_ms, geno_ms, total_ms, n_candidates, err);
     }
     if (n > d->cap_psites) {
         d->last_n_sites = n;
         d->cap_psites = 0;
-        return device_run_multi(d, s, t, g, sample_nrank, min_adf, ploidy, sites, calls, scan_ms, geno_ms, total_ms, n_candidates, err);
+        return device_run_multi(d, s, t, g, n_samples, min_adf, ploidy, sites, calls, n_sites, scan_ms, geno_ms, total_ms, n_candidates, err);
     }
-    sites->resize((size_t)n);
-    calls->resize((size_t)n * S);
+    if (n > d->cap_h_psites || n * S > d->cap_h_pcalls) {          // pinned staging, grown geometrically
+        if (d->h_psites) (void)hipHostFree(d->h_psites);
+        if (d->h_pcalls) (void)hipHostFree(d->h_pcalls);
+        d->h_psites = nullptr;
+        d->h_pcalls = nullptr;
+        d->cap_h_psites = std::max<int64_t>(n + n / 2, 1024);
+        d->cap_h_pcalls = d->cap_h_psites * S;
+        HIP_TRY(hipHostMalloc((void**)&d->h_psites, (size_t)d->cap_h_psites * sizeof(ngsep_popsite_out), hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc((void**)&d->h_pcalls, (size_t)d->cap_h_pcalls * sizeof(ngsep_sample_call), hipHostMallocDefault));
+    }
     if (n) {
-        HIP_TRY(hipMemcpyAsync(sites->data(), d->d_psites, (size_t)n * sizeof(ngsep_popsite_out), hipMemcpyDeviceToHost, d->stream));
-        HIP_TRY(hipMemcpyAsync(calls->data(), d->d_pcalls, (size_t)n * S * sizeof(ngsep_sample_call), hipMemcpyDeviceToHost, d->stream));
+        HIP_TRY(hipMemcpyAsync(d->h_psites, d->d_psites, (size_t)n * sizeof(ngsep_popsite_out), hipMemcpyDeviceToHost, d->stream));
+        HIP_TRY(hipMemcpyAsync(d->h_pcalls, d->d_pcalls, (size_t)n * S * sizeof(ngsep_sample_call), hipMemcpyDeviceToHost, d->stream));
         HIP_TRY(hipStreamSynchronize(d->stream));
     }
+    *sites = d->h_psites;
+    *calls = d->h_pcalls;
+    *n_sites = n;
     d->last_n_sites = n;
     d->last_hard = (int64_t)d->h_counters[2];
     d->last_exact = (int64_t)(c3 & 0x7FFFFFFFFFFFFFFFull);
@@ -2214,7 +2118,7 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     *scan_ms = a;
     *geno_ms = a2;
     *total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    *n_candidates = (int64_t)d->h_counters[1];
+    *n_candidates = d->mc_entries;          // candidate columns (sample, position) the scan bounded
     return 0;
 }
 
