@@ -152,7 +152,7 @@ typedef struct ngsep_stats {
     int64_t candidates;             /* positions sent to K2 */
     int64_t sites_called;
     int64_t read_bases;             /* projected read bytes resident in HBM */
-    int64_t slot_bytes;             /* bytes of the slot array (incl. padding) */
+    int64_t slot_bytes;             /* multisample: bytes of the population kernel's per-sample pile (incl. padding) */
     double  kernel_ms;              /* host wall time of the last device run (kernels + D2H) */
     double  scan_ms;                /* device time of the tile scan (KT) */
     double  genotype_ms;            /* device time of the posterior kernel */
@@ -160,10 +160,10 @@ typedef struct ngsep_stats {
     int32_t tile_rows_max;          /* largest tile depth (rows of the tile-blocked pileup matrix) */
     int32_t slot_size;              /* bytes per read slot of the read-major SoA */
     int32_t hard_sites;             /* candidates that needed the exact tally + posterior */
-    int64_t pile_bytes;             /* bytes of the tile-blocked pileup matrix streamed by the scan */
+    int64_t pile_bytes;             /* bytes of the pileup streamed by the scan (multisample: candidate-column bytes) */
     int64_t exact_bound_passes;     /* wavefront passes of the scan's exact integer hom-ref bound */
     int64_t global_positions;       /* positions of the device coordinate (windows + halos, whole tiles) */
-    int64_t n_tiles;                /* pileup tiles */
+    int64_t n_tiles;                /* pileup tiles (multisample: scan groups of 64 candidate columns) */
     double  layout_ms;              /* host time to build the device layout of the last staged run */
     double  upload_ms;              /* host time of its H2D upload */
     int64_t carved_positions;       /* covered positions inside carved indel regions (not called here) */
