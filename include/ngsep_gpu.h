@@ -26,14 +26,14 @@
 extern "C" {
 #endif
 
-#define NGSEP_ABI_VERSION 3
+#define NGSEP_ABI_VERSION 4
 
 #define NGSEP_OK 0
 #define NGSEP_E_INVALID (-1)      /* bad argument / state */
 #define NGSEP_E_IO (-2)           /* file cannot be read or written */
 #define NGSEP_E_FORMAT (-3)       /* malformed BAM / FASTA */
 #define NGSEP_E_DEVICE (-4)       /* HIP runtime error or no device */
-#define NGSEP_E_UNSUPPORTED (-5)  /* input outside the implemented path (ploidy>=3, > 255 samples, ...) */
+#define NGSEP_E_UNSUPPORTED (-5)  /* input outside the implemented path (ploidy > 128, > 255 samples, ...) */
 #define NGSEP_E_NOMEM (-6)
 
 typedef struct ngsep_ctx ngsep_ctx;
@@ -112,7 +112,15 @@ typedef struct ngsep_site_out {
     int8_t  strand_bias;     /* FS phred score (-csb) or -1 */
     int16_t gq;              /* genotype quality, PhredScoreHelper.calculatePhredScore(1-maxP) */
     int16_t qual;            /* variant QS, phred(P[ref][ref]) */
-    int16_t is_call;         /* 1 = passes the listener filters (always 1 unless dump_all_positions) */
+    int8_t  is_call;         /* 1 = passes the listener filters (always 1 unless dump_all_positions) */
+    uint8_t pool;            /* ploidy >= 3 (SingleSampleVariantPileupListener.genotypeVariantPool, :402-503):
+                              * bits 0-3 = the variant's alleles as DNA-index bits (reference included; the
+                              * alleles are the reference, then the others in A,C,G,T order), bit 4 = the call
+                              * report (PL / ADP) is present; 0 = an SNVQ record.  In a pool record n_alleles =
+                              * the variant's allele count, genotype = number of called alleles (0 undecided,
+                              * 1 homozygous, 2 heterozygous), alt / third = DNA indexes of the called alleles
+                              * (-1 when absent), logc = the report's log-conditionals over the variant's alleles
+                              * (upper triangle, i <= j < n_alleles, row-major), dp = the pool call's read depth */
     int32_t dp;              /* CountsHelper.getTotalCount() */
     int32_t counts[4];       /* A,C,G,T base counts (BSDP) */
     int32_t strand_counts[4][2]; /* [allele][0=negative,1=positive] (CountsHelper.countsStrand) */

@@ -86,7 +86,7 @@ class NgsepSiteOut(ctypes.Structure):
         ("strand_bias", ctypes.c_int8),
         ("gq", ctypes.c_int16),
         ("qual", ctypes.c_int16),
-        ("is_call", ctypes.c_int16),
+        ("is_call", ctypes.c_int8), ("pool", ctypes.c_uint8),
         ("dp", ctypes.c_int32),
         ("counts", ctypes.c_int32 * 4),
         ("strand_counts", (ctypes.c_int32 * 2) * 4),

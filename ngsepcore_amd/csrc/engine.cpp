@@ -79,7 +79,10 @@ void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g) {
     const double t_het = g->log_prior_hetero - g->log_prior_homo + std::log10(2.0);
     t->t_het = (long long)std::floor(K * t_het) + kBoundMargin;
     t->t_homo = kBoundMargin;
-    g->use_bound = ok && !g->dump_all && std::isfinite(t_het) ? 1 : 0;
+    g->ploidy = c->params.ploidy;
+    // the bounds prove SNVQ hom-ref calls; the pool algorithm only needs a valid non-reference call (its
+    // variant needs an alternative allele count >= 1, createSNVVariantPool :313-320), the scan's candidate test
+    g->use_bound = ok && !g->dump_all && std::isfinite(t_het) && g->ploidy < 3 ? 1 : 0;
     g->exact_bound = std::getenv("NGSEP_KT_EXACT") != nullptr ? 1 : 0;
     // count bound: a valid call carries q in [4, 30] (engine.hpp code), capped at max_q in the kernel
     t->c_r1 = t->c_r2 = INT64_MAX;
@@ -105,6 +108,48 @@ void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g) {
         }
         t->cb_nr[na] = (int16_t)lo;
     }
+}
+
+// genotypeVariantPool's hypotheses (SingleSampleVariantPileupListener.java:408-416) and the CountsHelper
+// caches they read (CountsHelper.java:147-185) for ploidy >= 3
+void compute_pool_tables(const ngsep_ctx* c, PoolTables* pt) {
+    std::memset(pt, 0, sizeof(*pt));
+    const int P = c->params.ploidy;
+    pt->ploidy = P;
+    const double step = 1.0 / (double)P;
+    int nf = 0;
+    for (double freq = step; freq < 0.51 && nf < kPoolMaxFreq; freq += step) pt->freq[nf++] = freq;
+    pt->nf = nf;
+    auto gt = [](int f, int q, int j) {      // logProbCacheGT[f][q][j], CountsHelper.java:168-185
+        const double af = (double)f / 500.0;
+        const double errorProb = std::pow(10.0, -0.1 * q), successProb = 1 - errorProb;
+        return j == 0 ? std::log10(successProb) : std::log10(af * successProb + (1 - af) * errorProb / (j - 1));
+    };
+    for (int q = 3; q <= 30; q++) {
+        pt->A[q] = gt(0, q, 0);
+        for (int ni = 0; ni < 3; ni++) pt->E[ni][q] = -0.1 * q - std::log10((double)(ni + 1));   // logProbCacheError[q][n]
+        for (int j = 0; j < nf; j++) {
+            const int f = (int)java_round(pt->freq[j] * 500), g = (int)java_round((1 - pt->freq[j]) * 500);   // :212-213
+            for (int ni = 0; ni < 3; ni++) {
+                pt->F[j][ni][q] = gt(f, q, ni + 2);
+                pt->G[j][ni][q] = gt(g, q, ni + 2);
+            }
+        }
+    }
+    const double h = c->het_rate;
+    pt->log_h = std::log10(h);
+    pt->log_1h = std::log10(1 - h);
+    for (int ni = 0; ni < 3; ni++) pt->log_h_n[ni] = std::log10(h / (ni + 1));
+}
+
+// ploidy >= 3: the pool tables onto the context's device before a run
+int prepare_pool(ngsep_ctx* c) {
+    if (c->params.ploidy < 3 || !c->dev) return NGSEP_OK;
+    PoolTables pt;
+    compute_pool_tables(c, &pt);
+    std::string err;
+    if (device_set_pool(c->dev, &pt, err) != 0) return set_error(c, NGSEP_E_DEVICE, err);
+    return NGSEP_OK;
 }
 
 // ReadAlignment.updateAlleleCallsInfo (ReadAlignment.java:747-834): allele-call length per read position.
@@ -617,7 +662,7 @@ static int stream_collect(ngsep_ctx* c) {
                                        [](const ngsep_ctx::KnownVar& v, int64_t p) { return v.pos < p; });
             int64_t k = it - c->known.begin();
             while (k < ke && c->known[(size_t)k].pos == o.pos &&
-                   (c->known[(size_t)k].alt != o.alt || std::find(taken.begin(), taken.end(), k) != taken.end()))
+                   (c->known[(size_t)k].alt != site_alt(o) || std::find(taken.begin(), taken.end(), k) != taken.end()))
                 k++;
             taken.push_back(k);
             kidx[i] = k;
@@ -1749,6 +1794,7 @@ int run_device(ngsep_ctx* c, double* elapsed_ms) {
         LikTables t;
         GenotypeParams gp;
         compute_tables(c, &t, &gp);
+        if (const int rc = prepare_pool(c)) return rc;
         return run_device_multi(c, t, gp, elapsed_ms);
     }
     return run_device_into(c, c->sites, elapsed_ms);
@@ -1762,12 +1808,14 @@ int run_device_into(ngsep_ctx* c, SiteStore& dest, double* elapsed_ms) {
     LikTables t;
     GenotypeParams gp;
     compute_tables(c, &t, &gp);
+    if (const int rc = prepare_pool(c)) return rc;
     int64_t n = 0;
     double scan_ms = 0, geno_ms = 0, total_ms = 0;
     int64_t ncand = 0;
     std::string err;
-    // exact pruning is proven for h <= 0.1 ("why pruning is exact")
-    int prune = c->params.prune_candidates && !c->params.dump_all_positions && c->het_rate <= 0.1;
+    // exact pruning is proven for h <= 0.1 ("why pruning is exact"); the pool algorithm's
+    // candidate test holds for any h
+    int prune = c->params.prune_candidates && !c->params.dump_all_positions && (c->het_rate <= 0.1 || c->params.ploidy >= 3);
     const size_t from = dest.size();
     if (device_run(c->dev, c->staged, t, gp, prune, &dest, &n, &scan_ms, &geno_ms, &total_ms, &ncand, err) != 0)
         return set_error(c, NGSEP_E_DEVICE, err);
@@ -1935,9 +1983,14 @@ extern "C" int ngsep_open(int device, const ngsep_params* params, ngsep_ctx** ou
         if (c->params.rac_min_bq < 4 || c->params.rac_min_bq > 30)
             return set_error(c, NGSEP_E_UNSUPPORTED, "minBQ outside [4, 30] (the pile's codes clamp qualities to 30 and drop the base of q <= 3 calls)");
     }
-    if (c->params.ploidy >= 3) {
+    if (c->params.ploidy > 2 * kPoolMaxFreq) {
         *out = c;
-        return set_error(c, NGSEP_E_UNSUPPORTED, "ploidy >= 3 uses the pool algorithm (SingleSampleVariantPileupListener.genotypeVariantPool), not implemented");
+        return set_error(c, NGSEP_E_UNSUPPORTED, "ploidy above " + std::to_string(2 * kPoolMaxFreq) +
+                                                     " (the pool algorithm's hypotheses table)");
+    }
+    if (c->params.ploidy >= 3 && c->params.multisample) {
+        *out = c;
+        return set_error(c, NGSEP_E_UNSUPPORTED, "multisample pool genotyping (ploidy >= 3) is not implemented");
     }
     // SingleSampleVariantsDetector.run (:591-593); MultisampleVariantsDetector keeps -h as given
     c->het_rate = c->params.het_rate;
@@ -2151,7 +2204,7 @@ const char* ngsep::known_id(const ngsep_ctx* c, const ngsep_site_out& s) {
     auto it = std::lower_bound(c->known.begin() + kb, c->known.begin() + ke, (int64_t)s.pos,
                                [](const ngsep_ctx::KnownVar& v, int64_t p) { return v.pos < p; });
     for (int64_t k = it - c->known.begin(); k < ke && c->known[(size_t)k].pos == s.pos; k++)
-        if (c->known[(size_t)k].alt == s.alt && std::find(st.taken.begin(), st.taken.end(), k) == st.taken.end()) {
+        if (c->known[(size_t)k].alt == site_alt(s) && std::find(st.taken.begin(), st.taken.end(), k) == st.taken.end()) {
             st.taken.push_back(k);
             return c->known[(size_t)k].id.empty() ? nullptr : c->known[(size_t)k].id.c_str();
         }
@@ -2318,7 +2371,8 @@ extern "C" int ngsep_submit_staged(ngsep_ctx* c) {
     }
     const LikTables& t = c->tables_t;
     const GenotypeParams& gp = c->tables_gp;
-    const int prune = c->params.prune_candidates && !c->params.dump_all_positions && c->het_rate <= 0.1;
+    if (const int rc = prepare_pool(c)) return rc;
+    const int prune = c->params.prune_candidates && !c->params.dump_all_positions && (c->het_rate <= 0.1 || c->params.ploidy >= 3);
     std::string err;
     if (device_submit(c->dev, c->staged, t, gp, prune, err) != 0) return set_error(c, NGSEP_E_DEVICE, err);
     return NGSEP_OK;

@@ -57,6 +57,15 @@ constexpr int kTileMinPos = 16;
 constexpr int kPopTile = 128;              // positions per KPM pile tile
 constexpr int kMcMaxCalls = 254;           // multisample candidate column: valid calls the bounds take (sums fit 32 bits)
 
+// the (first) alternative allele of a record as a DNA index: a pool record keeps its variant's alleles in
+// the mask bits (ngsep_site_out.pool), an SNVQ record in .alt
+inline int site_alt(const ngsep_site_out& s) {
+    if (!s.pool) return s.alt;
+    for (int a = 0; a < 4; a++)
+        if (((s.pool >> a) & 1) && "ACGT"[a] != s.ref) return a;
+    return -1;
+}
+
 // K2 output record (device layout == ngsep_site_out, with gpos in .pos)
 static_assert(sizeof(ngsep_site_out) == 152, "site record layout");
 static_assert(sizeof(ngsep_sample_call) == 76, "sample call layout");
@@ -87,6 +96,21 @@ struct LikTables {
 constexpr double kBoundScale = 1048576.0;   // 2^20: a tile holds <= 512 reads -> sums < 2^31
 constexpr long long kBoundMargin = 64;      // 6e-5 in log10 units, >> fp64 rounding of the sums
 
+// Pool genotyping (ploidy >= 3, SingleSampleVariantPileupListener.genotypeVariantPool :402-503): the
+// hypotheses' frequencies, accumulated as the reference does (freq = step; freq < 0.51; freq += step), and
+// the CountsHelper caches they index (CountsHelper.java:135-187) for variants of n = 2..4 alleles
+constexpr int kPoolMaxFreq = 64;           // ploidy <= 128
+struct PoolTables {
+    int32_t ploidy, nf;                     // haplotypes, number of frequency hypotheses
+    double freq[kPoolMaxFreq];              // hypothesis j's heterozygous proportion
+    double A[32];                           // logProbCacheGT[*][q][0] = log10(1-e)
+    double E[3][32];                        // logProbCacheError[q][n], n = 2, 3, 4
+    double F[kPoolMaxFreq][3][32];          // logProbCacheGT[round(500 freq_j)][q][n]
+    double G[kPoolMaxFreq][3][32];          // logProbCacheGT[round(500 (1-freq_j))][q][n]
+    double log_h, log_1h;                   // log10(h), log10(1-h) (:446-447)
+    double log_h_n[3];                      // log10(h/(n-1)), n = 2, 3, 4 (CountsHelper.java:451-467)
+};
+
 struct GenotypeParams {
     double log_prior_homo;     // log10((1-h)/4), CountsHelper.java:416
     double log_prior_hetero;   // log10(h/12),    CountsHelper.java:415
@@ -97,6 +121,8 @@ struct GenotypeParams {
                                // 4 no tiles, 8 tally without posterior, 16 posterior kernel reads the queue only,
                                // 32 population kernel gathers only, 64 population kernel stops after the tallies
     int32_t use_bound;         // 1: candidates proven hom-ref by the integer bound are dropped in the tile kernel
+    int32_t ploidy;            // >= 3: KP runs the pool algorithm (k_posterior_pool), KT queues every
+                               // position with a valid non-reference call (the pool variant needs one)
     int32_t exact_bound;       // bit-plane KT: 1 applies the exact integer bound to count-bound survivors
                                // (env NGSEP_KT_EXACT=1); 0 queues them for KP (measured: the exact
                                // bound dropped 4% of them on the 30x headline and cost 30% of KT)
@@ -430,6 +456,8 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs);
 int run_device_into(ngsep_ctx* c, SiteStore& dest, double* elapsed_ms);
 int run_device(ngsep_ctx* c, double* elapsed_ms);
 void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g);
+int prepare_pool(ngsep_ctx* c);
+int64_t java_round(double x);
 // kernels.hip
 Device* device_create(int ordinal, std::string& err);
 void device_destroy(Device* d);
@@ -439,6 +467,8 @@ int device_run(Device* d, const Staged& s, const LikTables& t, const GenotypePar
                SiteStore* out, int64_t* n_out, double* scan_ms, double* geno_ms, double* total_ms,
                int64_t* n_candidates, std::string& err);
 void device_release(Device* d);
+// ploidy >= 3: the pool algorithm's tables for the next runs (uploaded when they change; NULL: unchanged)
+int device_set_pool(Device* d, const PoolTables* pt, std::string& err);
 // asynchronous single-sample runs (two result slots): submit enqueues kernels and copies; collect
 // waits for the oldest run (an overflowed run is grown and re-run in place)
 int device_submit(Device* d, const Staged& s, const LikTables& t, const GenotypeParams& g, int prune, std::string& err);

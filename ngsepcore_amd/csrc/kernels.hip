@@ -112,6 +112,9 @@ struct Device {
     void* d_rac = nullptr;           // RelativeAlleleCounts: histograms + per-block sums (device, pinned host)
     void* h_rac = nullptr;
     LikTables* d_tables = nullptr;
+    PoolTables* d_pool = nullptr;    // ploidy >= 3: the pool algorithm's tables (device_set_pool)
+    PoolTables h_pool{};             // their last upload
+    bool pool_valid = false;
     int32_t ko_shift = 14, ko_bcap = 64;   // 2^ko_shift positions per bucket (grown on overflow)
     QueueSite* d_hard = nullptr;
     int64_t cap_hard = 0;
@@ -425,6 +428,261 @@ __global__ __launch_bounds__(kPostThreads) void k_posterior(const QueueSite* __r
             o[18 + 2 * t] = (uint32_t)bits;
             o[19 + 2 * t] = (uint32_t)(bits >> 32);
         }
+    }
+}
+
+
+// ------------------------------------------------------------------------------------------
+// KPP: ploidy >= 3 -- the pool algorithm over the queued candidates, one lane per site
+// ------------------------------------------------------------------------------------------
+// SingleSampleVariantPileupListener.discoverSNV's pool branch (:238-254): createSNVVariantPool (:297-332)
+// picks the variant's alleles from the SNV counts (count >= max(1, 0.5/ploidy * sum)), genotypeVariantPool
+// (:402-503) scores one homozygous and nf heterozygous-frequency hypotheses per alternative allele, a
+// multi-allelic variant called {0, k} or {k} is re-genotyped as the biallelic {ref, k}; -knownVariants sites
+// (genotypeVariantSample, :361-391) genotype the input's two alleles.  Every likelihood sum is the
+// CountsHelper.updateCounts addend sequence (CountsHelper.java:209-251) over the site's column in rank
+// order, so each sum is bit-identical; only the entries the decision reads are formed: the major allele's
+// row for each hypothesis, then the report's upper triangle at the chosen hypothesis.
+struct PoolResult {
+    int n_called, c0, c1;       // called allele indexes into the variant's alleles (ascending)
+    int gq, dp;                 // dp: setTotalReadDepth (0 for the undecided low-count call)
+    bool report;                // VariantCallReport present
+    double L[10];               // report log-conditionals, upper triangle over the variant's alleles
+};
+
+// one pass over a site's column: f(allele index into dna[] or -1, capped q) for every counted call
+// (q <= 3: lowBaseQualityCount only, not passed)
+template <class F>
+__device__ inline void pool_walk(const uint8_t* __restrict__ col, int32_t rows, const int* dna, int n, int32_t max_q, F&& f) {
+    for (int32_t r = 0; r < rows; r++) {
+        const uint32_t cd = col[r];
+        if (!(cd & 0x80u)) continue;                   // no call, or q <= 3 / not A,C,G,T: no likelihood update
+        const int a = (int)((cd >> 5) & 3u);
+        int q = (int)(cd & 31u);
+        q = q > max_q ? max_q : q;
+        int idx = -1;                                  // alleles.indexOf(allele)
+        for (int i = 0; i < n; i++) idx = (idx < 0 && dna[i] == a) ? i : idx;
+        if (idx >= 0) f(idx, q);
+    }
+}
+
+// genotypeVariantPool for the variant dna[0..n) (reference first); cnt4 = the column's A,C,G,T valid counts
+__device__ PoolResult pool_genotype(const uint8_t* __restrict__ col, int32_t rows, int32_t total, const int* cnt4,
+                                    const int* dna, int n, const PoolTables* __restrict__ pt, int32_t max_q) {
+    PoolResult R;
+    R.n_called = 0; R.c0 = -1; R.c1 = -1; R.gq = 0; R.dp = 0; R.report = false;
+    for (int k = 0; k < 10; k++) R.L[k] = 0;
+    const int P = pt->ploidy, nf = pt->nf, ni = n - 2;
+    int major = 0;                                     // NumberArrays.getIndexMaximum: the first maximum
+    for (int i = 1; i < n; i++) major = cnt4[dna[major]] < cnt4[dna[i]] ? i : major;
+    if (cnt4[dna[major]] < P) return R;                // undecided, no report (:436-440)
+    // the major allele's row L_j[major][*] of every hypothesis j
+    double Lr[kPoolMaxFreq][4];
+    for (int j = 0; j < nf; j++) {
+        double l0 = 0, l1 = 0, l2 = 0, l3 = 0;
+        pool_walk(col, rows, dna, n, max_q, [&](int idx, int q) {
+            const double A = pt->A[q], E = pt->E[ni][q], Fv = pt->F[j][ni][q], Gv = pt->G[j][ni][q];
+            // [m][m] += idx == m ? A : E;  [m][k] += k == idx ? F : (m == idx ? G : E)
+            const double v0 = major == 0 ? (idx == 0 ? A : E) : (idx == 0 ? Fv : (major == idx ? Gv : E));
+            const double v1 = major == 1 ? (idx == 1 ? A : E) : (idx == 1 ? Fv : (major == idx ? Gv : E));
+            const double v2 = major == 2 ? (idx == 2 ? A : E) : (idx == 2 ? Fv : (major == idx ? Gv : E));
+            const double v3 = major == 3 ? (idx == 3 ? A : E) : (idx == 3 ? Fv : (major == idx ? Gv : E));
+            l0 += v0; l1 += v1;
+            if (n > 2) l2 += v2;
+            if (n > 3) l3 += v3;
+        });
+        Lr[j][0] = l0; Lr[j][1] = l1; Lr[j][2] = l2; Lr[j][3] = l3;
+    }
+    const double termHomozygous = Lr[0][major] + pt->log_1h;
+    double maxHetPosterior = 0, minHomoPosterior = 1;
+    int maxFreqIdx = 0, maxAlt = -1;
+    for (int i = 0; i < n; i++) {
+        if (i == major) continue;
+        // calculatePosteriorProbabilities over {homozygous, hypothesis 0..nf-1} (CountsHelper.java:472-495)
+        double logMax = 1;
+        for (int j = -1; j < nf; j++) {
+            const double x = j < 0 ? termHomozygous : Lr[j][i] + pt->log_h;
+            if (logMax > 0 || logMax < x) logMax = x;
+        }
+        double totalProb = 0;
+        for (int j = -1; j < nf; j++) {
+            const double x = (j < 0 ? termHomozygous : Lr[j][i] + pt->log_h) - logMax;
+            totalProb += x < -20 ? 0.0 : pow10_j(x);
+        }
+        int idxMax = 0;
+        double best = 0, post0 = 0;
+        for (int j = -1; j < nf; j++) {
+            const double x = (j < 0 ? termHomozygous : Lr[j][i] + pt->log_h) - logMax;
+            const double pj = (x < -20 ? 0.0 : pow10_j(x)) / totalProb;
+            if (j < 0) { post0 = pj; best = pj; }
+            else if (best < pj) { best = pj; idxMax = j + 1; }
+        }
+        if (idxMax == 0) minHomoPosterior = post0 < minHomoPosterior ? post0 : minHomoPosterior;
+        else if (maxAlt == -1 || maxHetPosterior < best) { maxHetPosterior = best; maxFreqIdx = idxMax - 1; maxAlt = i; }
+    }
+    if (maxAlt == -1) { R.n_called = 1; R.c0 = major; }
+    else { R.n_called = 2; R.c0 = major < maxAlt ? major : maxAlt; R.c1 = major < maxAlt ? maxAlt : major; }
+    R.dp = total;
+    const int jr = maxAlt == -1 ? 0 : maxFreqIdx;      // the report's hypothesis
+    if (maxAlt == -1) {
+        R.gq = phred_d(1 - minHomoPosterior);
+    } else {
+        // getPosteriorProbabilities(h, major) (CountsHelper.java:451-467) over the chosen hypothesis' row
+        const double lph = pt->log_h_n[ni];
+        double logMax = 1;
+        for (int k = 0; k < n; k++) {
+            const double x = Lr[jr][k] + (k == major ? pt->log_1h : lph);
+            if (logMax > 0 || logMax < x) logMax = x;
+        }
+        double totalProb = 0, pAlt = 0;
+        for (int k = 0; k < n; k++) {
+            const double x = Lr[jr][k] + (k == major ? pt->log_1h : lph) - logMax;
+            const double pk = x < -20 ? 0.0 : pow10_j(x);
+            totalProb += pk;
+            if (k == maxAlt) pAlt = pk;
+        }
+        R.gq = phred_d(1 - pAlt / totalProb);
+    }
+    // the report: the chosen helper's log-conditionals, upper triangle
+    R.report = true;
+    double L[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    pool_walk(col, rows, dna, n, max_q, [&](int idx, int q) {
+        const double A = pt->A[q], E = pt->E[ni][q], Fv = pt->F[jr][ni][q], Gv = pt->G[jr][ni][q];
+        int k = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = i; j < 4; j++) {
+                if (j < n) {
+                    // [i][i] += i == idx ? A : E;  [i][j] += j == idx ? F : (i == idx ? G : E)
+                    const double v = i == j ? (i == idx ? A : E) : (j == idx ? Fv : (i == idx ? Gv : E));
+                    L[k] += v;
+                }
+                k++;
+            }
+    });
+    // repack the 4x4 upper triangle into the n-allele upper triangle
+    int o = 0, k = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = i; j < 4; j++) {
+            if (j < n) R.L[o++] = L[k];
+            k++;
+        }
+    return R;
+}
+
+__global__ __launch_bounds__(kPostThreads) void k_posterior_pool(const QueueSite* __restrict__ queue, const unsigned long long* qn,
+                                                        int64_t qcap, const TileInfo* __restrict__ tinfo,
+                                                        const uint8_t* __restrict__ cpile, const uint32_t* __restrict__ cneg,
+                                                        int32_t log2T, const PoolTables* __restrict__ pt, GenotypeParams gp,
+                                                        ngsep_site_out* __restrict__ brec, int32_t* __restrict__ bcount,
+                                                        int shift, int32_t bcap) {
+    const int32_t Tm = (1 << log2T) - 1;
+    int64_t nq = (int64_t)*qn;
+    if (nq > qcap) nq = qcap;
+    const int64_t stride = (int64_t)gridDim.x * kPostThreads;
+    for (int64_t i = (int64_t)blockIdx.x * kPostThreads + threadIdx.x; i < nq; i += stride) {
+        const QueueSite qs = queue[i];
+        const int32_t gpos = qs.gpos;
+        const uint32_t rc = (uint32_t)qs.rc;
+        const TileInfo ti = tinfo[gpos >> log2T];
+        const int32_t rows = ti.rows;
+        const int64_t base = ti.off + (int64_t)(gpos & Tm) * rows;
+        const uint8_t* col = cpile + base;
+        // the SNV tally of calculateCountsSNV (CountsHelper.java:83-95): totals, A,C,G,T and strand counts
+        int32_t total = 0;
+        int cnt[4] = {0, 0, 0, 0};
+        int32_t sc[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
+        for (int32_t r = 0; r < rows; r++) {
+            const uint32_t cd = col[r];
+            if (cd == 0) continue;
+            total++;
+            if (!(cd & 0x80u)) continue;
+            const int a = (int)((cd >> 5) & 3u);
+            const int64_t cell = base + r;
+            const int neg = (int)((cneg[cell >> 5] >> (cell & 31)) & 1u);
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                cnt[t] += a == t ? 1 : 0;
+                sc[t][0] += (a == t && neg) ? 1 : 0;
+                sc[t][1] += (a == t && !neg) ? 1 : 0;
+            }
+        }
+        const bool known = (rc & 0x400u) != 0;
+        const bool callable = (rc & 0x80u) != 0;
+        int dna[4] = {0, 0, 0, 0};
+        int n = 0;
+        bool keep = false, multi = false;
+        PoolResult R;
+        R.n_called = 0; R.c0 = -1; R.c1 = -1; R.gq = 0; R.dp = 0; R.report = false;
+        if (known) {
+            dna[0] = (int)((rc >> 5) & 3u);
+            dna[1] = (int)((rc >> 8) & 3u);
+            n = 2;
+            R = pool_genotype(col, rows, total, cnt, dna, n, pt, gp.max_q);
+            if (gp.min_quality > R.gq) { R.n_called = 0; R.c0 = R.c1 = -1; R.gq = 0; }   // makeUndecided (:388)
+            keep = true;
+        } else if (callable && total > 0) {
+            // createSNVVariantPool(pileup, helperSNV, reference, 0.5 / ploidy)
+            const int refIdx = (int)((rc >> 5) & 3u);
+            const int sum = cnt[0] + cnt[1] + cnt[2] + cnt[3];
+            double minCount = (0.5 / (double)pt->ploidy) * sum;
+            minCount = minCount < 1 ? 1 : minCount;
+            dna[n++] = refIdx;
+            for (int t = 0; t < 4; t++)
+                if (cnt[t] >= minCount && t != refIdx) dna[n++] = t;
+            if (n >= 2) {
+                multi = n > 2;
+                R = pool_genotype(col, rows, total, cnt, dna, n, pt, gp.max_q);
+                bool ok = true;
+                if (multi) {
+                    if (R.n_called == 0 || (R.n_called == 1 && R.c0 == 0)) ok = false;
+                    else if (!(R.n_called == 2 && R.c0 != 0)) {
+                        // makeNewVariant(variant, {ref} + called alleles) (:346-359): the biallelic SNV
+                        const int alt = R.n_called == 1 ? dna[R.c0] : dna[R.c1];
+                        dna[1] = alt;
+                        n = 2;
+                        multi = false;
+                        R = pool_genotype(col, rows, total, cnt, dna, n, pt, gp.max_q);
+                    }
+                }
+                // discoverVariant (:221-227): undecided, hom-ref and GQ below -minQuality are dropped
+                keep = ok && R.n_called > 0 && !(R.n_called == 1 && R.c0 == 0) && !(gp.min_quality > R.gq);
+            }
+        }
+        if (!keep) continue;
+        const int32_t bk = gpos >> shift;
+        const int32_t k = atomicAdd(&bcount[bk], 1);
+        if (k >= bcap) continue;                       // overflow: the host grows the buckets and reruns
+        uint32_t mask = 0;
+        for (int t = 0; t < n; t++) mask |= 1u << dna[t];
+        const int a0 = R.c0 >= 0 ? dna[R.c0] : -1, a1 = R.c1 >= 0 ? dna[R.c1] : -1;
+        uint32_t h[18];
+        h[0] = 0xFFFFFFFFu;
+        h[1] = (uint32_t)gpos;
+        const uint32_t ref = (uint32_t)(uint8_t)"ACGT"[dna[0]];
+        h[2] = ref | (uint32_t)(uint8_t)n << 8 | (uint32_t)(uint8_t)(int8_t)a0 << 16 | (uint32_t)(uint8_t)(int8_t)a1 << 24;
+        h[3] = (uint32_t)(uint8_t)R.n_called | 0xFF00u | (uint32_t)(uint16_t)R.gq << 16;
+        h[4] = 1u << 16 | (mask | (R.report ? 0x10u : 0u)) << 24;
+        h[5] = (uint32_t)R.dp;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            h[6 + t] = (uint32_t)cnt[t];
+            h[10 + 2 * t] = (uint32_t)sc[t][0];
+            h[11 + 2 * t] = (uint32_t)sc[t][1];
+        }
+        uint32_t* o = reinterpret_cast<uint32_t*>(brec + (int64_t)bk * bcap + k);
+#pragma unroll
+        for (int t = 0; t < 18; t++) o[t] = h[t];
+#pragma unroll
+        for (int t = 0; t < 10; t++) {
+            const unsigned long long bits = __builtin_bit_cast(unsigned long long, R.L[t]);
+            o[18 + 2 * t] = (uint32_t)bits;
+            o[19 + 2 * t] = (uint32_t)(bits >> 32);
+        }
+        (void)multi;
     }
 }
 
@@ -1583,6 +1841,7 @@ void device_destroy(Device* d) {
     (void)hipFree(d->d_hard);
     (void)hipFree(d->d_counters);
     (void)hipFree(d->d_tables);
+    (void)hipFree(d->d_pool);
     (void)hipHostFree(d->h_counters);
     for (auto& e : d->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(d->stream);
@@ -1770,11 +2029,20 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     // previous run's survivors, grid-stride beyond)
     static const int kp_env = std::getenv("NGSEP_KP_GRID") ? std::max(1, std::atoi(std::getenv("NGSEP_KP_GRID"))) : 0;   // tuning
     const int kp_grid = kp_env ? kp_env : (int)std::max<int64_t>(d->n_cu, std::min<int64_t>((d->last_hard + kPostThreads - 1) / kPostThreads, 8 * (int64_t)d->n_cu));
-    hipExtLaunchKernelGGL(k_posterior, dim3(kp_grid), dim3(kPostThreads), 0, sl.stream,
-                          d->time_posterior ? sl.ev[5] : nullptr, d->time_posterior ? sl.ev[2] : nullptr, 0,
-                          (const QueueSite*)sl.d_hard, (const unsigned long long*)(ctr + 2), sl.cap_hard,
-                          (const TileInfo*)d->d_tinfo, (const uint8_t*)d->d_pile, (const uint32_t*)d->d_cneg, d->log2_tile,
-                          (const LikTables*)sl.d_tables, g, sl.d_brec, sl.d_bcount, shift, bcap);
+    if (g.ploidy >= 3 && !g.dump_all) {
+        if (!d->pool_valid) { err = "ploidy >= 3 without pool tables (device_set_pool)"; return -1; }
+        hipExtLaunchKernelGGL(k_posterior_pool, dim3(kp_grid), dim3(kPostThreads), 0, sl.stream,
+                              d->time_posterior ? sl.ev[5] : nullptr, d->time_posterior ? sl.ev[2] : nullptr, 0,
+                              (const QueueSite*)sl.d_hard, (const unsigned long long*)(ctr + 2), sl.cap_hard,
+                              (const TileInfo*)d->d_tinfo, (const uint8_t*)d->d_pile, (const uint32_t*)d->d_cneg, d->log2_tile,
+                              (const PoolTables*)d->d_pool, g, sl.d_brec, sl.d_bcount, shift, bcap);
+    } else {
+        hipExtLaunchKernelGGL(k_posterior, dim3(kp_grid), dim3(kPostThreads), 0, sl.stream,
+                              d->time_posterior ? sl.ev[5] : nullptr, d->time_posterior ? sl.ev[2] : nullptr, 0,
+                              (const QueueSite*)sl.d_hard, (const unsigned long long*)(ctr + 2), sl.cap_hard,
+                              (const TileInfo*)d->d_tinfo, (const uint8_t*)d->d_pile, (const uint32_t*)d->d_cneg, d->log2_tile,
+                              (const LikTables*)sl.d_tables, g, sl.d_brec, sl.d_bcount, shift, bcap);
+    }
     HIP_TRY(hipGetLastError());
     // order the records by position on the device (one kernel; counters[0] = records | max bucket << 40)
     hipLaunchKernelGGL(ko_scan, dim3(1), dim3(1024), 0, sl.stream, (const int32_t*)sl.d_bcount, nb, bcap, sl.d_boff, ctr);
@@ -1798,6 +2066,19 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     sl.prune = prune;
     sl.tabs = t;
     sl.staged = &s;
+    return 0;
+}
+
+// the pool algorithm's tables (ploidy >= 3): uploaded when they change, after the runs that read the old ones
+int device_set_pool(Device* d, const PoolTables* pt, std::string& err) {
+    if (!pt) return 0;
+    if (d->pool_valid && std::memcmp(&d->h_pool, pt, sizeof(PoolTables)) == 0) return 0;
+    HIP_TRY(hipSetDevice(d->ordinal));
+    HIP_TRY(hipDeviceSynchronize());
+    if (!d->d_pool) HIP_TRY(hipMalloc(&d->d_pool, sizeof(PoolTables)));
+    HIP_TRY(hipMemcpy(d->d_pool, pt, sizeof(PoolTables), hipMemcpyHostToDevice));
+    d->h_pool = *pt;
+    d->pool_valid = true;
     return 0;
 }
 

@@ -71,6 +71,71 @@ int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& o)
     if (ri == 4 || s.n_alleles < 2) return 0;
     const std::string& name = (s.seq_id >= 0 && s.seq_id < (int)c->seq_names.size()) ? c->seq_names[s.seq_id] : std::string("?");
     const char* id = known_id(c, s);              // -knownVariants: the input variant's ID
+    if (s.pool) {
+        // ploidy >= 3: genotypeVariantPool's CalledGenomicVariantImpl.  FORMAT NGSEP_NOSNV for discovery (no
+        // getAllCounts), NGSEP_SNV for -knownVariants (setAllCounts) (SingleSampleVariantsDetector.java:942-946);
+        // QUAL = the variant's QS (never set in discovery, the input's for known variants)
+        int dna[4], n = 0;
+        dna[n++] = ri;
+        for (int a = 0; a < 4; a++) if (((s.pool >> a) & 1) && a != ri) dna[n++] = a;
+        const bool known = !c->known.empty();
+        const bool report = (s.pool & 0x10) != 0;
+        auto index_of = [&](int a) { for (int i = 0; i < n; i++) if (dna[i] == a) return i; return -1; };
+        const int nc = s.genotype;                       // called alleles
+        const int c0 = nc > 0 ? index_of(s.alt) : -1, c1 = nc > 1 ? index_of(s.third) : -1;
+        o += name; o += '\t'; app(o, s.pos); o += '\t'; o += id ? id : "."; o += '\t'; o += (char)s.ref; o += '\t';
+        for (int i = 1; i < n; i++) { if (i > 1) o += ','; o += kB[dna[i]]; }
+        o += '\t'; app(o, s.qual); o += "\t.\t";
+        o += n > 2 ? "TYPE=MULTISNV" : ".";               // VCFFileWriter.java:47-49
+        o += known ? "\tGT:PL:GQ:DP:BSDP:ACN\t" : "\tGT:PL:GQ:DP:ADP:ACN\t";
+        if (nc == 0) o += "./.";
+        else if (nc == 1) { app(o, c0); o += '/'; app(o, c0); }
+        else { app(o, c0); o += '/'; app(o, c1); }
+        o += ':';
+        // PL over the report's log-conditionals (VCFFileWriter.java:200-212), upper triangle i <= j < n
+        auto lt = [&](int i, int j) { return s.logc[i * n - i * (i - 1) / 2 + (j - i)]; };
+        for (int j = 0; j < n; j++)
+            for (int i = 0; i <= j; i++) {
+                if (i > 0 || j > 0) o += ',';
+                app(o, report ? (int)java_round(-10 * lt(i, j)) : 0);
+            }
+        o += ':'; app(o, s.gq); o += ':'; app(o, s.dp); o += ':';
+        if (known) for (int k = 0; k < 4; k++) { if (k) o += ','; app(o, s.counts[k]); }
+        else for (int i = 0; i < n; i++) { if (i) o += ','; app(o, report ? s.counts[dna[i]] : 0); }
+        o += ':';
+        // ACN: updateAllelesCopyNumberFromCounts(ploidy) from the report's counts (discoverVariant :226,
+        // intersectVariantsCNVs :986; CalledGenomicVariantImpl.java:228-282)
+        int acn[4] = {0, 0, 0, 0};
+        const int called[2] = {c0, c1};
+        if (nc == 1 && c0 == 0) acn[0] = ploidy;
+        else if (nc > 0 && ploidy <= nc) { for (int i = 0; i < nc; i++) acn[called[i]] = 1; }
+        else if (nc > 0 && !report) {
+            const int def = ploidy / nc;
+            for (int i = 0; i < nc; i++) acn[called[i]] = def;
+            acn[called[0]] += ploidy - def * nc;
+        } else if (nc > 0) {
+            int rc[2], tr = 0, tc = 0;
+            for (int i = 0; i < nc; i++) { rc[i] = s.counts[dna[called[i]]]; if (rc[i] == 0) rc[i] = 1; tr += rc[i]; }
+            for (int i = 0; i < nc; i++) {
+                const long long r = java_round((double)ploidy * rc[i] / tr);
+                acn[called[i]] = (int)(r > 1 ? r : 1);
+                tc += acn[called[i]];
+            }
+            if (tc < ploidy) acn[called[0]] += ploidy - tc;
+            else {
+                int ex = tc - ploidy;
+                for (int i = nc - 1; ex > 0 && i >= 0; i--) {
+                    const int rm = ex < acn[called[i]] - 1 ? ex : acn[called[i]] - 1;
+                    acn[called[i]] -= rm;
+                    ex -= rm;
+                }
+            }
+        }
+        if (nc == 0) acn[0] = ploidy;                    // undecided: ACN[0] = the copy number (VCFFileWriter.java:237)
+        for (int i = 0; i < n; i++) { if (i) o += ','; app(o, acn[i]); }
+        o += '\n';
+        return (int64_t)(o.size() - start);
+    }
     o += name; o += '\t'; app(o, s.pos); o += '\t'; o += id ? id : "."; o += '\t'; o += (char)s.ref; o += '\t';
     o += kB[(int)s.alt];
     if (s.n_alleles == 3) { o += ','; o += kB[(int)s.third]; }

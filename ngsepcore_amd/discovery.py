@@ -29,7 +29,8 @@ def default_params() -> NgsepParams:
 
 @dataclass
 class CalledSite:
-    """One called variant (CalledSNV or triallelic CalledGenomicVariantImpl)."""
+    """One called variant (CalledSNV, triallelic CalledGenomicVariantImpl, or -- ploidy >= 3 -- the
+    CalledGenomicVariantImpl of genotypeVariantPool: `called` holds its called alleles' indexes)."""
     sequence: str
     pos: int
     ref: str
@@ -43,11 +44,14 @@ class CalledSite:
     logc: List[float]
     strand_bias: int
     is_call: bool
+    called: List[int] = None
 
     def log_conditional(self, i: int, j: int) -> float:
+        """SNVQ records: i, j are DNA indexes; pool records: indexes into `alleles`."""
         if i > j:
             i, j = j, i
-        base = (0, 4, 7, 9)[i]
+        n = len(self.alleles) if self.called is not None else 4
+        base = i * n - i * (i - 1) // 2
         return self.logc[base + j - i]
 
 
@@ -192,15 +196,20 @@ class GpuPileupSession:
         out = []
         for s in self.raw_sites():
             alleles = [chr(s.ref)]
-            if s.n_alleles >= 2:
-                alleles.append(BASES[s.alt])
-            if s.n_alleles == 3:
-                alleles.append(BASES[s.third])
+            called = None
+            if s.pool:
+                alleles += [BASES[k] for k in range(4) if (s.pool >> k) & 1 and BASES[k] != chr(s.ref)]
+                called = [alleles.index(BASES[x]) for x in (s.alt, s.third) if x >= 0]
+            else:
+                if s.n_alleles >= 2:
+                    alleles.append(BASES[s.alt])
+                if s.n_alleles == 3:
+                    alleles.append(BASES[s.third])
             out.append(CalledSite(
                 sequence=names[s.seq_id] if 0 <= s.seq_id < len(names) else "?", pos=s.pos, ref=chr(s.ref),
                 alleles=alleles, genotype=s.genotype, gq=s.gq, qual=s.qual, dp=s.dp, counts=list(s.counts),
                 strand_counts=[list(x) for x in s.strand_counts], logc=list(s.logc),
-                strand_bias=s.strand_bias, is_call=bool(s.is_call)))
+                strand_bias=s.strand_bias, is_call=bool(s.is_call), called=called))
         return out
 
     def clear(self):

@@ -8,7 +8,7 @@
  * (paths relative to src/ngsep/ of acastem15/NGSEPcore).
  *
  * Scope restated: SAM text + FASTA -> VCF for SingleSampleVariantsDetector with
- * ploidy 1/2, SNV-only alignments (no I/D CIGAR operations: the indel realigner
+ * ploidy 1/2 (SNVQ) and >= 3 (the pool algorithm), SNV-only alignments (no I/D CIGAR operations: the indel realigner
  * is then a pass-through, discovery/IndelRealignerPileupListener.java:85-126).
  * Inputs outside that scope make ngo_run_ssvd() return NGO_UNSUPPORTED.
  */
@@ -415,6 +415,15 @@ typedef struct ngo_call {
     const char* id;           /* -knownVariants: the input variant's ID (NULL: '.') */
     int known;                /* 1: a genotyped input variant (genotype 0 hom-ref, -1 undecided allowed) */
     int logc_present;         /* 0: no log-conditionals (an undecided call without allele calls) */
+    /* ploidy >= 3 (genotypeVariantPool): a CalledGenomicVariantImpl over the pool variant's alleles */
+    int pool;                 /* 1: the fields below describe the call, logc[][] is over the variant alleles */
+    int pool_n;               /* variant alleles: DNA indexes pool_dna[0..n) (reference first) */
+    int pool_dna[4];
+    int pool_multi;           /* TYPE_MULTIALLELIC_SNV (INFO TYPE=MULTISNV) */
+    int pool_ncalled, pool_called[2];
+    int pool_report;          /* VariantCallReport present (counts + log-conditionals) */
+    int pool_counts[4];       /* report counts over the variant alleles (ADP) */
+    int pool_acn[4], pool_total_cn;
 } ngo_call;
 
 typedef struct { ngo_call* c; int n, cap; } ngo_calls;
@@ -480,7 +489,39 @@ static void print_header_samples(FILE* out, const ngo_params* p, const char* con
 }
 
 /* one VCF line per call: VCFFileWriter.printVCFRecord + printGenotypeInfo */
+static void print_pool_call(FILE* out, const char* seqName, const ngo_call* c) {
+    /* a CalledGenomicVariantImpl of genotypeVariantPool: FORMAT NGSEP_NOSNV (discovery: no getAllCounts) or
+     * NGSEP_SNV (-knownVariants: setAllCounts), SingleSampleVariantsDetector.java:942-946 */
+    const int n = c->pool_n;
+    fprintf(out, "%s\t%d\t%s\t%c\t", seqName, c->pos, c->id ? c->id : ".", c->ref);
+    for (int i = 1; i < n; i++) fprintf(out, "%s%c", i > 1 ? "," : "", BASES[c->pool_dna[i]]);
+    fprintf(out, "\t%d\t.\t%s", c->qual, c->pool_multi ? "TYPE=MULTISNV" : ".");
+    fprintf(out, c->known ? "\tGT:PL:GQ:DP:BSDP:ACN\t" : "\tGT:PL:GQ:DP:ADP:ACN\t");
+    if (c->pool_ncalled == 0) fprintf(out, "./.");
+    else if (c->pool_ncalled == 1) fprintf(out, "%d/%d", c->pool_called[0], c->pool_called[0]);
+    else fprintf(out, "%d/%d", c->pool_called[0], c->pool_called[1]);
+    fprintf(out, ":");
+    for (int j = 0; j < n; j++)
+        for (int i = 0; i <= j; i++) {
+            if (i > 0 || j > 0) fprintf(out, ",");
+            fprintf(out, "%d", c->pool_report ? (int)ngo_java_round(-10 * c->logc[i][j]) : 0);
+        }
+    fprintf(out, ":%d:%d:", c->gq, c->dp);
+    if (c->known) fprintf(out, "%d,%d,%d,%d", c->counts[0], c->counts[1], c->counts[2], c->counts[3]);
+    else for (int i = 0; i < n; i++) fprintf(out, "%s%d", i ? "," : "", c->pool_report ? c->pool_counts[i] : 0);
+    fprintf(out, ":");
+    if (c->pool_total_cn == 0) fprintf(out, ".");
+    else
+        for (int j = 0; j < n; j++) {
+            int v = c->pool_acn[j];
+            if (c->pool_ncalled == 0 && j == 0) v = c->pool_total_cn;
+            fprintf(out, "%s%d", j ? "," : "", v);
+        }
+    fprintf(out, "\n");
+}
+
 static void print_call(FILE* out, const char* seqName, const ngo_call* c) {
+    if (c->pool) { print_pool_call(out, seqName, c); return; }
     fprintf(out, "%s\t%d\t%s\t%c\t", seqName, c->pos, c->id ? c->id : ".", c->ref);
     if (c->n_alleles == 2) fprintf(out, "%c", BASES[c->idx[1]]);
     else fprintf(out, "%c,%c", BASES[c->idx[1]], BASES[c->idx[2]]);
@@ -656,6 +697,14 @@ static void alist_push(ngo_alist* l, ngo_aln* a) {
     l->a[l->n++] = a;
 }
 
+/* one PileupAlleleCall of span 1 as calculateCountsGTSNV reads it (CountsHelper.java:86-95) */
+typedef struct { int base; int q; int neg; } ngo_acall;   /* base: DNA index or -1; q = min(30, qual-33) */
+typedef struct { ngo_acall* c; int n, cap; } ngo_acalls;
+static void acalls_push(ngo_acalls* l, int base, int q, int neg) {
+    if (l->n == l->cap) { l->cap = l->cap ? 2 * l->cap : 64; l->c = realloc(l->c, sizeof(ngo_acall) * l->cap); }
+    l->c[l->n].base = base; l->c[l->n].q = q; l->c[l->n].neg = neg; l->n++;
+}
+
 struct ngo_mvd;
 typedef struct {
     const ngo_params* p;
@@ -674,6 +723,7 @@ typedef struct {
     struct ngo_rac* rac;       /* RelativeAlleleCountsCalculator listener instead of the variant listeners */
     ngo_known* known;          /* -knownVariants (sequence order, then position, input order kept) */
     int n_known, known_next;   /* known_next: nextSIVIndex over the whole list */
+    ngo_acalls acalls;         /* ploidy >= 3: the position's allele calls in pending order */
 } ngo_gen;
 
 /* ------------------------------------------------------------------ */
@@ -836,6 +886,215 @@ static void java_hashset_order(char** ids, int* idx, int n) {
     free(bucket);
 }
 
+/* ------------------------------------------------------------------ */
+/* Ploidy >= 3: SingleSampleVariantPileupListener.genotypeVariantPool (:402-503), the pool paths of   */
+/* discoverSNV (:234-255), genotypeVariantSample (:361-391) and createSNVVariantPool (:297-332)       */
+/* ------------------------------------------------------------------ */
+
+typedef struct {
+    int n_called, called[2];  /* indexes into the variant alleles, ascending */
+    int gq, dp;               /* dp: setTotalReadDepth (0 for the low-count undecided call) */
+    int report;               /* VariantCallReport present */
+    int counts[4];            /* report counts over the variant alleles */
+    double logc[4][4];        /* report log-conditionals over the variant alleles */
+    int acn[4], total_cn;
+} ngo_pcall;
+
+/* CalledGenomicVariantImpl.updateAllelesCopyNumberFromCounts (variants/CalledGenomicVariantImpl.java:228-282) */
+static void pool_update_cn(ngo_pcall* c, int total) {
+    c->total_cn = total;
+    for (int i = 0; i < 4; i++) c->acn[i] = 0;
+    if (c->n_called == 0) return;
+    if (c->n_called == 1 && c->called[0] == 0) { c->acn[0] = total; return; }
+    int nc = c->n_called;
+    if (total <= nc) { for (int i = 0; i < nc; i++) c->acn[c->called[i]] = 1; return; }
+    if (!c->report) {
+        int def = total / nc;
+        for (int i = 0; i < nc; i++) c->acn[c->called[i]] = def;
+        c->acn[c->called[0]] += total - def * nc;
+        return;
+    }
+    int rc[2], tr = 0;
+    for (int i = 0; i < nc; i++) { rc[i] = c->counts[c->called[i]]; if (rc[i] == 0) rc[i] = 1; tr += rc[i]; }
+    int tc = 0;
+    for (int i = 0; i < nc; i++) {
+        int64_t r = ngo_java_round((double)total * rc[i] / tr);
+        c->acn[c->called[i]] = (int)(r > 1 ? r : 1);
+        tc += c->acn[c->called[i]];
+    }
+    if (tc < total) c->acn[c->called[0]] += total - tc;
+    else {
+        int ex = tc - total;
+        for (int i = nc - 1; ex > 0 && i >= 0; i--) {
+            int j = c->called[i];
+            int rm = ex < c->acn[j] - 1 ? ex : c->acn[j] - 1;
+            c->acn[j] -= rm; ex -= rm;
+        }
+    }
+}
+
+/* CountsHelper.calculateCountsGTSNV(alleles, calls, maxBaseQS, freq) (CountsHelper.java:86-95) */
+static void pool_helper(ngo_counts* h, const int* dna, int n, const ngo_acalls* calls, double freq, int max_base_qs) {
+    ngo_counts_init(h, n, freq, max_base_qs);
+    for (int k = 0; k < calls->n; k++) {
+        int idx = -1;                                    /* alleles.indexOf(allele) */
+        for (int i = 0; i < n; i++) if (calls->c[k].base >= 0 && dna[i] == calls->c[k].base) { idx = i; break; }
+        ngo_counts_update(h, idx, calls->c[k].q, calls->c[k].neg);
+    }
+}
+
+/* genotypeVariantPool (SingleSampleVariantPileupListener.java:402-503) for the variant with alleles dna[0..n) */
+static void genotype_pool(const int* dna, int n, int haplotypes, const ngo_acalls* calls, double h, int max_base_qs,
+                          ngo_pcall* out) {
+    memset(out, 0, sizeof(*out));
+    double step = 1.0 / (double)haplotypes;
+    int nf = 0;
+    for (double freq = step; freq < 0.51; freq += step) nf++;
+    double* freqs = malloc(sizeof(double) * (nf ? nf : 1));
+    ngo_counts* hs = malloc(sizeof(ngo_counts) * (nf ? nf : 1));
+    nf = 0;
+    for (double freq = step; freq < 0.51; freq += step) {
+        freqs[nf] = freq;
+        pool_helper(&hs[nf], dna, n, calls, freq, max_base_qs);
+        nf++;
+    }
+    const ngo_counts* helper = &hs[0];
+    const int* counts = helper->counts;
+    int major = 0;                                       /* NumberArrays.getIndexMaximum: first maximum */
+    for (int i = 1; i < n; i++) if (counts[major] < counts[i]) major = i;
+    if (counts[major] < haplotypes) {                    /* undecided, no report (:436-440) */
+        pool_update_cn(out, haplotypes);
+        free(freqs); free(hs);
+        return;
+    }
+    double logPriorHetero = log10(h), logPriorHomo = log10(1 - h);
+    double* terms = malloc(sizeof(double) * (nf + 1));
+    double termHomozygous = helper->logc[major][major] + logPriorHomo;
+    double maxHetPosterior = 0, minHomoPosterior = 1, maxFreq = 0;
+    int maxFreqIdx = 0, maxAlt = -1;
+    for (int i = 0; i < n; i++) {
+        if (i == major) continue;
+        terms[0] = termHomozygous;
+        for (int j = 0; j < nf; j++) terms[j + 1] = hs[j].logc[major][i] + logPriorHetero;
+        calc_posteriors(terms, nf + 1);
+        int idxMax = 0;
+        for (int j = 1; j <= nf; j++) if (terms[idxMax] < terms[j]) idxMax = j;
+        if (idxMax == 0) {
+            if (terms[0] < minHomoPosterior) minHomoPosterior = terms[0];
+        } else if (maxAlt == -1 || maxHetPosterior < terms[idxMax]) {
+            maxHetPosterior = terms[idxMax];
+            maxFreqIdx = idxMax - 1;
+            maxFreq = freqs[maxFreqIdx];
+            maxAlt = i;
+        }
+    }
+    free(terms);
+    if (maxAlt == -1) { out->n_called = 1; out->called[0] = major; }
+    else {
+        out->n_called = 2;
+        out->called[0] = major < maxAlt ? major : maxAlt;
+        out->called[1] = major < maxAlt ? maxAlt : major;
+    }
+    out->dp = helper->total_count;
+    if (maxAlt == -1) {
+        out->gq = ngo_phred(1 - minHomoPosterior);
+        out->acn[major] = haplotypes;
+    } else {
+        helper = &hs[maxFreqIdx];
+        /* CountsHelper.getPosteriorProbabilities(hetRate, majorAlleleIdx) (CountsHelper.java:451-467) */
+        double ev[4];
+        double lph = log10(h / (n - 1)), lpo = log10(1 - h);
+        for (int j = 0; j < n; j++) ev[j] = helper->logc[major][j] + (j == major ? lpo : lph);
+        calc_posteriors(ev, n);
+        out->gq = ngo_phred(1 - ev[maxAlt]);
+        int altCN = (int)(int16_t)ngo_java_round(maxFreq * haplotypes);
+        if (altCN == 0) altCN++;
+        else if (altCN == haplotypes) altCN--;
+        out->acn[maxAlt] = altCN;
+        out->acn[major] = haplotypes - altCN;
+    }
+    out->total_cn = haplotypes;                          /* setAllelesCopyNumber */
+    out->report = 1;
+    for (int i = 0; i < n; i++) {
+        out->counts[i] = counts[i];
+        for (int j = 0; j < n; j++) out->logc[i][j] = helper->logc[i][j];
+    }
+    free(freqs); free(hs);
+}
+
+static void pool_to_call(const ngo_pcall* pc, const int* dna, int n, ngo_call* out) {
+    out->pool = 1;
+    out->pool_n = n;
+    for (int i = 0; i < 4; i++) out->pool_dna[i] = i < n ? dna[i] : -1;
+    out->pool_ncalled = pc->n_called;
+    out->pool_called[0] = pc->called[0]; out->pool_called[1] = pc->called[1];
+    out->pool_report = pc->report;
+    for (int i = 0; i < 4; i++) { out->pool_counts[i] = pc->counts[i]; out->pool_acn[i] = pc->acn[i]; }
+    out->pool_total_cn = pc->total_cn;
+    out->gq = pc->gq; out->dp = pc->dp;
+    for (int i = 0; i < 4; i++) for (int j = 0; j < 4; j++) out->logc[i][j] = pc->logc[i][j];
+}
+
+/* discoverSNV with ploidy >= 3 (SingleSampleVariantPileupListener.java:238-254) and the discoverVariant
+ * filters (:221-227: undecided / hom-ref / GQ below -minQuality dropped, ACN from the counts); 1 = kept */
+static int pool_discover(const ngo_counts* h4, const ngo_acalls* calls, int pos, char refBase, const ngo_params* p,
+                         double hetRate, ngo_call* out) {
+    /* createSNVVariantPool(pileup, helperSNV, reference, 0.5/ploidy) (:297-332) */
+    if (h4->total_count == 0) return 0;
+    int refIdx = base_idx(refBase);
+    if (refIdx < 0) return 0;
+    int sum = h4->counts[0] + h4->counts[1] + h4->counts[2] + h4->counts[3];
+    double minCount = (0.5 / (double)p->ploidy) * sum;
+    if (minCount < 1) minCount = 1;
+    int dna[4], n = 0;
+    dna[n++] = refIdx;
+    for (int i = 0; i < 4; i++) if (h4->counts[i] >= minCount && i != refIdx) dna[n++] = i;
+    if (n < 2) return 0;
+    int multi = n > 2;
+    ngo_pcall pc;
+    genotype_pool(dna, n, p->ploidy, calls, hetRate, p->max_base_qs, &pc);
+    if (multi) {
+        if (pc.n_called == 0 || (pc.n_called == 1 && pc.called[0] == 0)) return 0;
+        if (!(pc.n_called == 2 && pc.called[0] != 0)) {
+            /* makeNewVariant(variant, {ref} + called alleles) (:346-359): a biallelic SNV */
+            int nd[4], nn = 0;
+            nd[nn++] = refIdx;
+            for (int i = 0; i < pc.n_called; i++) if (dna[pc.called[i]] != refIdx) nd[nn++] = dna[pc.called[i]];
+            for (int i = 0; i < nn; i++) dna[i] = nd[i];
+            n = nn;
+            multi = 0;
+            genotype_pool(dna, n, p->ploidy, calls, hetRate, p->max_base_qs, &pc);
+        }
+    }
+    if (pc.n_called == 0 || (pc.n_called == 1 && pc.called[0] == 0) || (int16_t)p->min_quality > pc.gq) return 0;
+    pool_update_cn(&pc, p->ploidy);                      /* discoverVariant / intersectVariantsCNVs */
+    memset(out, 0, sizeof(*out));
+    out->pos = pos; out->ref = refBase; out->strand_bias = -1; out->ploidy = p->ploidy;
+    out->qual = 0;                                       /* the variant's QS is never set on this path */
+    memcpy(out->counts, h4->counts, sizeof(out->counts));
+    pool_to_call(&pc, dna, n, out);
+    out->pool_multi = multi;
+    out->n_alleles = n;
+    return 1;
+}
+
+/* -knownVariants with ploidy >= 3: genotypeVariantSample (:361-391) -> genotypeVariantPool, setAllCounts,
+ * makeUndecided below -minQuality; intersectVariantsCNVs then recomputes ACN from the counts (:986) */
+static void pool_known(const ngo_counts* h4, const ngo_acalls* calls, const ngo_known* kv, const ngo_params* p,
+                       double hetRate, ngo_call* out) {
+    int dna[2] = {base_idx(kv->ref), base_idx(kv->alt)};
+    ngo_pcall pc;
+    genotype_pool(dna, 2, p->ploidy, calls, hetRate, p->max_base_qs, &pc);
+    if ((int16_t)p->min_quality > pc.gq) { pc.n_called = 0; pc.gq = 0; }   /* makeUndecided */
+    pool_update_cn(&pc, p->ploidy);
+    memset(out, 0, sizeof(*out));
+    out->pos = kv->pos; out->ref = kv->ref; out->known = 1; out->id = kv->id; out->qual = kv->qs;
+    out->strand_bias = -1; out->ploidy = p->ploidy;
+    memcpy(out->counts, h4->counts, sizeof(out->counts));
+    pool_to_call(&pc, dna, 2, out);
+    out->n_alleles = 2;
+}
+
 /* One sample's call: CalledSNV (biallelic SNV) or CalledGenomicVariantImpl (multi-allelic SNV or
  * the no-data undecided call), as far as the VCF line and DiversityStatistics read them. */
 typedef struct {
@@ -906,9 +1165,24 @@ static void cgv_update_cn(ngo_scall* c, int n_alleles, int total, const int* rep
 
 /* SingleSampleVariantPileupListener.genotypeVariantSample (:361-391) with a fresh listener
  * (minQuality = DEF_MIN_QUALITY 40) and VariantDiscoverySNVQAlgorithm.genotypeSNV (:21-97) */
-static void genotype_sample(const ngo_counts* h, const ngo_pvar* v, double het, int ploidy, ngo_scall* c) {
+static void genotype_sample(const ngo_counts* h, const ngo_acalls* calls, const ngo_pvar* v, double het, int ploidy,
+                            ngo_scall* c) {
     memset(c, 0, sizeof(*c));
     memcpy(c->counts, h->counts, sizeof(c->counts));
+    if (ploidy >= 3) {
+        /* genotypeVariantPool + setAllCounts (:368-371), makeUndecided below the fresh listener's minQuality */
+        ngo_pcall pc;
+        genotype_pool(v->idx, v->n, ploidy, calls, het, h->max_base_qs, &pc);
+        c->kind = 1;
+        c->n_called = pc.n_called; c->called[0] = pc.called[0]; c->called[1] = pc.called[1];
+        c->gq = pc.gq; c->dp = pc.dp;
+        c->has_logs = pc.report;
+        for (int i = 0; i < 4; i++) for (int j = 0; j < 4; j++) c->logs[i][j] = pc.logc[i][j];
+        if (40 > pc.gq) { pc.n_called = 0; pc.gq = 0; pool_update_cn(&pc, pc.total_cn); c->n_called = 0; c->gq = 0; }
+        c->total_cn = pc.total_cn;
+        for (int i = 0; i < 4; i++) c->acn[i] = pc.acn[i];
+        return;
+    }
     if (h->total_count == 0) {
         /* undecided CalledGenomicVariantImpl(variant, new byte[0]) with the counts, no report */
         c->kind = 1;
@@ -982,6 +1256,7 @@ typedef struct ngo_mvd {
     double min_adf;
     int ploidy;
     ngo_counts* h;                /* per-sample helpers */
+    ngo_acalls* sc;               /* ploidy >= 3: per-sample allele calls in getAlleleCalls order */
     ngo_scall* calls;
 } ngo_mvd;
 
@@ -1024,7 +1299,7 @@ int ngo_population_info(int n_calls, const int* n_called, const int* called, con
 static void mvd_genotype_all(ngo_mvd* M, const ngo_pvar* v, double het, int* qs) {
     int q = 0;
     for (int s = 0; s < M->n_samples; s++) {
-        genotype_sample(&M->h[s], v, het, M->ploidy, &M->calls[s]);
+        genotype_sample(&M->h[s], &M->sc[s], v, het, M->ploidy, &M->calls[s]);
         const ngo_scall* c = &M->calls[s];
         int homref = c->n_called == 1 && c->called[0] == 0;
         if (c->n_called > 0 && !homref && c->gq > q) q = c->gq;   /* MultisampleVariantsDetector.java:683-685 */
@@ -1094,7 +1369,7 @@ static void mvd_on_pileup(ngo_gen* G, int pos) {
      * order of its read groups (PileupRecord.getAlleleCalls, :104-152) */
     ngo_counts pooled;
     ngo_counts_init(&pooled, 4, 0.5, p->max_base_qs);
-    for (int s = 0; s < M->n_samples; s++) ngo_counts_init(&M->h[s], 4, 0.5, p->max_base_qs);
+    for (int s = 0; s < M->n_samples; s++) { ngo_counts_init(&M->h[s], 4, 0.5, p->max_base_qs); M->sc[s].n = 0; }
     int maxrank = 0;
     for (int s = 0; s < M->n_samples; s++) if (M->n_rank[s] > maxrank) maxrank = M->n_rank[s];
     for (int rank = -1; rank < maxrank; rank++) {
@@ -1112,6 +1387,7 @@ static void mvd_on_pileup(ngo_gen* G, int pos) {
             int q = qc - 33; if (q > 30) q = 30;
             ngo_counts* h = rank < 0 ? &pooled : &M->h[sm];
             ngo_counts_update(h, base_idx(a->chars[rp]), (int8_t)q, (a->flags & FLAG_REVERSE) != 0);
+            if (rank >= 0 && M->ploidy >= 3) acalls_push(&M->sc[sm], base_idx(a->chars[rp]), (int8_t)q, (a->flags & FLAG_REVERSE) != 0);
         }
     }
     /* SingleSampleVariantPileupListener.createSNVVariantPool (:297-332) */
@@ -1198,6 +1474,8 @@ static int process_current_position(ngo_gen* G) {
     int numAlignments = 0;
     ngo_counts h;
     ngo_counts_init(&h, 4, 0.5, p->max_base_qs);     /* CountsHelper.calculateCountsSNV(calls, maxBaseQS, 0.5) */
+    const int pool = p->ploidy >= 3;                 /* SingleSampleVariantPileupListener.DEF_MIN_PLOIDY_POOL_ALGORITHM */
+    G->acalls.n = 0;
     for (int k = 0; k < G->pending.n; k++) {
         ngo_aln* a = G->pending.a[k];
         if (a->first > pos || a->last < pos) continue;   /* PileupRecord.addAlignment, :154-167 */
@@ -1212,6 +1490,7 @@ static int process_current_position(ngo_gen* G) {
         int qc = a->quals ? a->quals[rp] : '+';
         int q = qc - 33; if (q > 30) q = 30;              /* CountsHelper.java:91 */
         ngo_counts_update(&h, base_idx(a->chars[rp]), (int8_t)q, (a->flags & FLAG_REVERSE) != 0);
+        if (pool) acalls_push(&G->acalls, base_idx(a->chars[rp]), (int8_t)q, (a->flags & FLAG_REVERSE) != 0);
     }
     if (numAlignments > 0) G->st->positions_genotyped++;
     /* SingleSampleVariantPileupListener.onPileup -> calculateReferenceAlleleDiscovery (:191-206) */
@@ -1229,14 +1508,16 @@ static int process_current_position(ngo_gen* G) {
                 const ngo_known* kv = &G->known[G->known_next++];
                 if (kv->pos != pos) continue;
                 ngo_call c;
-                genotype_known(&h, kv, p, G->het_rate, &c);
+                if (pool) pool_known(&h, &G->acalls, kv, p, G->het_rate, &c);
+                else genotype_known(&h, kv, p, G->het_rate, &c);
                 if (G->calls.n == G->calls.cap) { G->calls.cap = G->calls.cap ? 2 * G->calls.cap : 1024; G->calls.c = realloc(G->calls.c, sizeof(ngo_call) * G->calls.cap); }
                 G->calls.c[G->calls.n++] = c;
             }
         } else if (!(p->ignore_lowercase_ref && islower((unsigned char)r))) {
             char R = (char)toupper((unsigned char)r);
             ngo_call c;
-            if (discover_snv(&h, pos, R, p, G->het_rate, &c)) {
+            if (pool ? pool_discover(&h, &G->acalls, pos, R, p, G->het_rate, &c)
+                     : discover_snv(&h, pos, R, p, G->het_rate, &c)) {
                 if (G->calls.n == G->calls.cap) { G->calls.cap = G->calls.cap ? 2 * G->calls.cap : 1024; G->calls.c = realloc(G->calls.c, sizeof(ngo_call) * G->calls.cap); }
                 G->calls.c[G->calls.n++] = c;
             }
@@ -1400,7 +1681,6 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
     clock_gettime(CLOCK_MONOTONIC, &t0);
     ngo_stats st_local; ngo_stats* st = stats ? stats : &st_local;
     memset(st, 0, sizeof(*st));
-    if (p->ploidy >= 3) return NGO_UNSUPPORTED;   /* pool algorithm (SingleSampleVariantPileupListener.java:240-254) */
     ngo_genome g;
     if (load_fasta(fasta, &g) != NGO_OK) return NGO_ERR_IO;
     FILE* in = fopen(sam, "r");
@@ -1492,6 +1772,7 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
             M.ploidy = p->ploidy;
             M.h = calloc(M.n_samples ? M.n_samples : 1, sizeof(ngo_counts));
             M.calls = calloc(M.n_samples ? M.n_samples : 1, sizeof(ngo_scall));
+            M.sc = calloc(M.n_samples ? M.n_samples : 1, sizeof(ngo_acalls));
             G.mvd = &M;
             print_header_samples(out, p, (const char* const*)M.ids, M.n_samples);
         }
@@ -1583,7 +1864,7 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
     for (int i = 0; i < G.pending.n; i++) aln_free(G.pending.a[i]);
     for (int i = 0; i < G.ss_primary.n; i++) aln_free(G.ss_primary.a[i]);
     for (int i = 0; i < G.ss_secondary.n; i++) aln_free(G.ss_secondary.a[i]);
-    free(G.pending.a); free(G.ss_primary.a); free(G.ss_secondary.a); free(G.retired.a); free(G.calls.c);
+    free(G.pending.a); free(G.ss_primary.a); free(G.ss_secondary.a); free(G.retired.a); free(G.calls.c); free(G.acalls.c);
     for (int i = 0; i < G.n_known; i++) free(G.known[i].id);
     free(G.known);
     for (int i = 0; i < g.n; i++) { free(g.s[i].name); free(g.s[i].seq); }
@@ -1595,6 +1876,8 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
     if (multisample) {
         for (int i = 0; i < M.n_samples; i++) free(M.ids[i]);
         free(M.ids); free(M.rg_sample); free(M.rg_rank); free(M.n_rank); free(M.h); free(M.calls);
+        for (int i = 0; i < M.n_samples; i++) free(M.sc[i].c);
+        free(M.sc);
     }
     clock_gettime(CLOCK_MONOTONIC, &t1);
     st->seconds = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
@@ -1610,7 +1893,6 @@ int ngo_run_ssvd(const char* fasta, const char* sam, const char* out_vcf,
  * holding every sample's read groups (the generator's merge of per-sample files). */
 int ngo_run_mvd(const char* fasta, const char* sam, const char* out_vcf, const ngo_params* p,
                 double min_allele_depth_freq, ngo_stats* stats) {
-    if (p->ploidy >= 3) return NGO_UNSUPPORTED;
     return run_detector(fasta, sam, out_vcf, NULL, p, stats, min_allele_depth_freq, 1, NULL, NULL);
 }
 

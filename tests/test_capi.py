@@ -28,7 +28,7 @@ def test_every_declared_symbol_is_exported():
 
 def test_abi_version_and_defaults():
     lib = _lib.load()
-    assert lib.ngsep_abi_version() == 3
+    assert lib.ngsep_abi_version() == 4
     p = _lib.NgsepParams()
     lib.ngsep_params_default(ctypes.byref(p))
     # DEF_* constants: SingleSampleVariantsDetector.java:65-78, CountsHelper.java:42-48
@@ -45,7 +45,7 @@ def test_unsupported_inputs_fail_loudly():
     from ngsepcore_amd import GpuPileupSession, NgsepError
     p = _lib.NgsepParams()
     _lib.load().ngsep_params_default(ctypes.byref(p))
-    p.ploidy = 4
+    p.ploidy = 129          # the pool algorithm's hypotheses table holds ploidy <= 128
     with pytest.raises(NgsepError) as e:
         GpuPileupSession(p)
     assert e.value.code == _lib.NGSEP_E_UNSUPPORTED
