@@ -1988,10 +1988,6 @@ extern "C" int ngsep_open(int device, const ngsep_params* params, ngsep_ctx** ou
         return set_error(c, NGSEP_E_UNSUPPORTED, "ploidy above " + std::to_string(2 * kPoolMaxFreq) +
                                                      " (the pool algorithm's hypotheses table)");
     }
-    if (c->params.ploidy >= 3 && c->params.multisample) {
-        *out = c;
-        return set_error(c, NGSEP_E_UNSUPPORTED, "multisample pool genotyping (ploidy >= 3) is not implemented");
-    }
     // SingleSampleVariantsDetector.run (:591-593); MultisampleVariantsDetector keeps -h as given
     c->het_rate = c->params.het_rate;
     if (!c->params.multisample && !c->params.het_rate_set && c->params.ploidy == 1) c->het_rate = 1e-6;

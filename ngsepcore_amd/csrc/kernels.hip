@@ -447,6 +447,7 @@ struct PoolResult {
     int n_called, c0, c1;       // called allele indexes into the variant's alleles (ascending)
     int gq, dp;                 // dp: setTotalReadDepth (0 for the undecided low-count call)
     bool report;                // VariantCallReport present
+    int acn[4];                 // setAllelesCopyNumber of genotypeVariantPool (:480-497) over the variant's alleles
     double L[10];               // report log-conditionals, upper triangle over the variant's alleles
 };
 
@@ -471,6 +472,7 @@ __device__ PoolResult pool_genotype(const uint8_t* __restrict__ col, int32_t row
                                     const int* dna, int n, const PoolTables* __restrict__ pt, int32_t max_q) {
     PoolResult R;
     R.n_called = 0; R.c0 = -1; R.c1 = -1; R.gq = 0; R.dp = 0; R.report = false;
+    R.acn[0] = R.acn[1] = R.acn[2] = R.acn[3] = 0;
     for (int k = 0; k < 10; k++) R.L[k] = 0;
     const int P = pt->ploidy, nf = pt->nf, ni = n - 2;
     int major = 0;                                     // NumberArrays.getIndexMaximum: the first maximum
@@ -524,9 +526,19 @@ __device__ PoolResult pool_genotype(const uint8_t* __restrict__ col, int32_t row
     else { R.n_called = 2; R.c0 = major < maxAlt ? major : maxAlt; R.c1 = major < maxAlt ? maxAlt : major; }
     R.dp = total;
     const int jr = maxAlt == -1 ? 0 : maxFreqIdx;      // the report's hypothesis
+    auto set_acn = [&](int k, int v) {
+#pragma unroll
+        for (int e = 0; e < 4; e++) R.acn[e] = e == k ? v : R.acn[e];
+    };
     if (maxAlt == -1) {
         R.gq = phred_d(1 - minHomoPosterior);
+        set_acn(major, P);
     } else {
+        int altCN = (int)(int16_t)java_round_d(pt->freq[maxFreqIdx] * P);
+        if (altCN == 0) altCN++;
+        else if (altCN == P) altCN--;
+        set_acn(maxAlt, altCN);
+        set_acn(major, P - altCN);
         // getPosteriorProbabilities(h, major) (CountsHelper.java:451-467) over the chosen hypothesis' row
         const double lph = pt->log_h_n[ni];
         double logMax = 1;
@@ -1402,7 +1414,7 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
     const QueueSite* __restrict__ queue, const unsigned long long* qn, int64_t qcap,
     const uint8_t* __restrict__ ppile, const uint16_t* __restrict__ prow, const int64_t* __restrict__ pboff,
     const LikTables* __restrict__ tabs, GenotypeParams gp,
-    int32_t n_samples, double min_adf, int32_t ploidy,
+    int32_t n_samples, double min_adf, int32_t ploidy, const PoolTables* __restrict__ pt,
     ngsep_popsite_out* __restrict__ sites, ngsep_sample_call* __restrict__ calls,
     unsigned long long* counters, int64_t cap, unsigned long long* __restrict__ stamps) {
     // stamps (diagnostics, NGSEP_TIMING): s_memtime at the phase ends of block 0's first site
@@ -1432,11 +1444,14 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
         int total = 0;
         int cnt[4] = {0, 0, 0, 0};
         double L[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        const bool pool = ploidy >= 3;
+        int32_t rows = 0;
+        const uint8_t* col = nullptr;
         if (tid <= n_samples) {
             const int64_t bi = (int64_t)(gpos >> kPopTileLog2) * (n_samples + 1) + tid;
-            const int32_t rows = prow[bi];
-            const uint8_t* col = ppile + pboff[bi] + (int64_t)(gpos & (kPopTile - 1)) * rows;
-            const bool tally = tid < n_samples;
+            rows = prow[bi];
+            col = ppile + pboff[bi] + (int64_t)(gpos & (kPopTile - 1)) * rows;
+            const bool tally = tid < n_samples && !pool;        // (the pool algorithm walks the column itself)
             for (int32_t r0 = 0; r0 < rows; r0 += 8) {
                 uint32_t code[8];
 #pragma unroll
@@ -1499,12 +1514,27 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
         int multisnv = nal > 2;
         // 5. genotype every sample; shrink a multi-allelic variant to the called alleles
         PopCall call;
+        PoolResult pr;
         int qsv = 0;
         for (;;) {
             if (tid == 0) { s_called = 0; s_qs = 0; }
             __syncthreads();
+            if (tid < n_samples && pool) {
+                // genotypeVariantSample's pool branch (SingleSampleVariantPileupListener.java:368-371): genotypeVariantPool
+                // over the sample's calls, setAllCounts, makeUndecided below the fresh listener's minQuality (40)
+                pr = pool_genotype(col, rows, total, cnt, idx, nal, pt, gp.max_q);
+                call.kind = 1; call.n_called = pr.n_called; call.c0 = pr.c0 < 0 ? 0 : pr.c0; call.c1 = pr.c1 < 0 ? 0 : pr.c1;
+                call.gq = pr.gq; call.total_cn = ploidy;
+#pragma unroll
+                for (int k = 0; k < 4; k++) call.acn[k] = pr.acn[k];
+                if (40 > call.gq) {
+                    call.n_called = 0; call.gq = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; k++) call.acn[k] = 0;
+                }
+            }
             if (tid < n_samples) {
-                call = genotype_sample_d(L, cnt, total, nal, idx, gp, ploidy);
+                if (!pool) call = genotype_sample_d(L, cnt, total, nal, idx, gp, ploidy);
                 const bool homref = call.n_called == 1 && call.c0 == 0;
                 if (call.n_called > 0 && !homref) atomicMax(&s_qs, call.gq);
                 int bits = 0;
@@ -1544,11 +1574,22 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
             o.kind = (int8_t)call.kind; o.n_called = (int8_t)call.n_called;
             o.called[0] = (int8_t)call.c0; o.called[1] = (int8_t)call.c1;
             o.gq = (int16_t)call.gq; o.total_cn = (int16_t)call.total_cn;
-            o.dp = total;
+            o.dp = pool ? pr.dp : total;
             for (int k = 0; k < 4; k++) { o.counts[k] = cnt[k]; o.acn[k] = (int16_t)call.acn[k]; o.pl[k] = 0; }
             for (int k = 4; k < 10; k++) o.pl[k] = 0;
             // PL (VCFFileWriter.java:200-212) from the call report
-            if (call.kind == 0) {
+            if (pool) {
+                if (pr.report) {
+                    int k = 0;
+                    for (int j = 0; j < nal; j++)
+                        for (int ii = 0; ii <= j; ii++) {
+                            const int32_t v = (int32_t)java_round_d(-10 * sel10(pr.L, ii * nal - ii * (ii - 1) / 2 + (j - ii)));
+#pragma unroll
+                            for (int e = 0; e < 10; e++) if (e == k) o.pl[e] = v;
+                            k++;
+                        }
+                }
+            } else if (call.kind == 0) {
                 const float hr = (float)sel10(L, tri_d(idx[0], idx[0])), ha = (float)sel10(L, tri_d(idx[1], idx[1]));
                 const float ra = (float)sel10(L, tri_d(idx[0], idx[1])), ar = ra;
                 const bool present = (hr + ra + ar + ha) != 0;     // CalledSNV.java:422 (float sum)
@@ -2344,10 +2385,12 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
                               (const uint32_t*)d->d_need, (const uint8_t*)d->d_ref, nwords, d->d_hard, ctr, d->cap_hard);
         HIP_TRY(hipGetLastError());
     }
+    if (ploidy >= 3 && !d->pool_valid) { err = "ploidy >= 3 without pool tables (device_set_pool)"; return -1; }
     hipExtLaunchKernelGGL(k_posterior_multi, dim3(2048), dim3(kPopThreads), 0, d->stream, d->ev[3], d->ev[2], 0,
                           (const QueueSite*)d->d_hard, (const unsigned long long*)(ctr + 2), d->cap_hard, (const uint8_t*)d->d_ppile,
                           (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, (const LikTables*)d->d_tables, g,
-                          S, min_adf, ploidy, d->d_psites, d->d_pcalls, ctr, d->cap_psites, d->d_stamps);
+                          S, min_adf, ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), d->d_psites, d->d_pcalls,
+                          ctr, d->cap_psites, d->d_stamps);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(d->h_counters, ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, d->stream));
     HIP_TRY(hipStreamSynchronize(d->stream));

@@ -104,3 +104,35 @@ def test_pool_known_variants_vcf_identical(tmp_path, ploidy):
     gts = {l.split("\t")[9].split(":")[0] for l in orec}
     assert {"0/0", "0/1"} <= gts
     assert _records(g) == orec
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ploidy,n_samples,opts", [
+    (4, 6, {}),
+    (3, 12, {"min_allele_depth_freq": 0.05}),
+    (8, 4, {"min_quality": 20}),
+])
+def test_pool_population_vcf_identical(tmp_path, ploidy, n_samples, opts):
+    """MultisampleVariantsDetector with -ploidy >= 3: every sample genotyped by genotypeVariantPool
+    (genotypeVariantSample :368-371, setAllCounts, makeUndecided below 40), the multi-allelic shrink loop,
+    the variant QS and INFO from the pool calls (KTM without the SNVQ bound + KPM's pool branch); one BAM
+    holding every sample's read group, as ngsep_call_population_bams reads it."""
+    from ngsepcore_amd import MultisampleVariantsDetector
+    samples = [f"P{k:02d}" for k in range(n_samples)]
+    fa, sam, bam = pool_data.write_pool(os.path.join(str(tmp_path), "pop"), seed=30 + ploidy, depth=25.0 * n_samples,
+                                        haplotypes=ploidy, rg_samples=samples, length=30000)
+    o = os.path.join(str(tmp_path), "o.vcf")
+    ngsep_oracle.run_mvd(fa, sam, o, opts.get("min_allele_depth_freq", 0.0), ploidy=ploidy,
+                         **{k: v for k, v in opts.items() if k != "min_allele_depth_freq"})
+    d = MultisampleVariantsDetector()
+    d.setGenome(fa)
+    d.setNormalPloidy(ploidy)
+    if "min_allele_depth_freq" in opts:
+        d.setMinAlleleDepthFrequency(opts["min_allele_depth_freq"])
+    if "min_quality" in opts:
+        d.setMinQuality(opts["min_quality"])
+    d.setOutFilename(os.path.join(str(tmp_path), "g.vcf"))
+    d.run([bam])
+    orec = _records(o)
+    assert len(orec) > 30
+    assert _records(d.outFilename) == orec
