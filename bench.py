@@ -260,6 +260,10 @@ def main():
     ap.add_argument("--samples", type=int, default=200)
     ap.add_argument("--contig-first", type=int, default=3, help="multisample: first yeast contig of the shard")
     ap.add_argument("--n-contigs", type=int, default=1, help="multisample: contigs in the shard")
+    ap.add_argument("--wgs-shards", type=int, default=0,
+                    help="wgs: split the genome over this many shards (default: the world size); with one process, "
+                         "--wgs-shard picks the shard this GPU calls (one GPU's part of the 8-GPU split)")
+    ap.add_argument("--wgs-shard", type=int, default=-1, help="wgs: the shard to call (default: the rank)")
     args = ap.parse_args()
     if args.config == "multisample" and args.depth == 30.0:
         args.depth = 10.0
@@ -338,12 +342,17 @@ def main():
                  ("chr11", 135086622), ("chr12", 133275309), ("chr13", 114364328), ("chr14", 107043718), ("chr15", 101991189),
                  ("chr16", 90338345), ("chr17", 83257441), ("chr18", 80373285), ("chr19", 58617616), ("chr20", 64444167),
                  ("chr21", 46709983), ("chr22", 50818468), ("chrX", 156040895), ("chrY", 57227415)]
-        mine = assign_contigs(human, world)[rank]
+        nsh = args.wgs_shards if args.wgs_shards > 0 else world
+        shard = args.wgs_shard if args.wgs_shard >= 0 else rank
+        if world > 1 and nsh != world:
+            log("bench.py: --wgs-shards must equal the world size when several ranks run")
+            sys.exit(2)
+        mine = assign_contigs(human, nsh)[shard]
         idx = [k for k, (n, _) in enumerate(human) if n in mine]
         sources = [("lazy", k) for k in idx]
         workload = (f"configs[3]: human WGS (GRCh38 lengths, 3.10e9 bp) 30x synthetic 150 bp SE, contig-sharded: "
-                    f"rank {rank} of {world} calls {'+'.join(mine)}")
-        workload_key = f"wgs:{args.depth:g}x:rank{rank}of{world}"
+                    f"shard {shard} of {nsh} calls {'+'.join(mine)}")
+        workload_key = f"wgs:{args.depth:g}x:shard{shard}of{nsh}"
 
     # stage: one session per device run (< 2^31 positions each)
     positions = 0
@@ -372,10 +381,19 @@ def main():
             syn = sources[0] if item is None else pysynth.Synth(genome=pysynth.HUMAN, depth=args.depth, seed=4,
                                                                contig_first=item, n_contigs=1, rng_per_contig=1)
             t_gen += time.time() - tg
+            seq_base = len(sess.sequence_names())
             for name, seq in syn.contigs():
                 sess.set_reference(name, seq)
             ts = time.time()
-            sess.stage(syn.batch())
+            batch = syn.batch()
+            if seq_base:
+                # the synthetic contig's reads index its own sequence list: shift to the session's indexes
+                import ctypes
+                import numpy as np
+                sid = np.ctypeslib.as_array(batch.seq_id, shape=(batch.n_reads,)) + seq_base
+                sid = np.ascontiguousarray(sid, dtype=np.int32)
+                batch.seq_id = sid.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+            sess.stage(batch)
             t_stage += time.time() - ts
             if args.config == "chr20" and rank == 0 and world == 1 and not args.no_e2e:
                 # the same reads as a BAM on local disk for the end-to-end run
