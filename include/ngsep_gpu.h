@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define NGSEP_ABI_VERSION 4
+#define NGSEP_ABI_VERSION 5
 
 #define NGSEP_OK 0
 #define NGSEP_E_INVALID (-1)      /* bad argument / state */
@@ -77,6 +77,12 @@ typedef struct ngsep_params {
     int32_t relative_allele_counts; /* 1: the pileups feed the allele-proportion distributions */
     int32_t rac_min_rd;           /* -minRD 10 */
     int32_t rac_min_bq;           /* -minBQ 20 (4..30 here: the pile's codes keep qualities clamped to 30) */
+    /* ABI 5: what a biallelic SNV record carries back from the device.  0 (default): what the reference's
+     * CalledSNV keeps (variants/CalledSNV.java:42-45,259-265) -- logc only at (ref,ref), (ref,alt), (alt,alt)
+     * and strand_counts only for the reference and alternative alleles, the other entries 0; 1: the whole
+     * CountsHelper state (all ten log-conditionals, every strand count).  Multi-allelic, pool and
+     * dump_all_positions records are always whole. */
+    int32_t full_records;
 } ngsep_params;
 
 /* Alignments as AlignmentsPileupGenerator.processAlignment receives them
@@ -123,8 +129,10 @@ typedef struct ngsep_site_out {
                               * (upper triangle, i <= j < n_alleles, row-major), dp = the pool call's read depth */
     int32_t dp;              /* CountsHelper.getTotalCount() */
     int32_t counts[4];       /* A,C,G,T base counts (BSDP) */
-    int32_t strand_counts[4][2]; /* [allele][0=negative,1=positive] (CountsHelper.countsStrand) */
-    double  logc[10];        /* log10 P(data|genotype) upper triangle: 00 01 02 03 11 12 13 22 23 33 */
+    int32_t strand_counts[4][2]; /* [allele][0=negative,1=positive] (CountsHelper.countsStrand); biallelic SNV
+                              * records without full_records: the reference and alternative rows only */
+    double  logc[10];        /* log10 P(data|genotype) upper triangle: 00 01 02 03 11 12 13 22 23 33; biallelic
+                              * SNV records without full_records: (ref,ref), (ref,alt), (alt,alt) only */
 } ngsep_site_out;
 
 /* One population VCF line of MultisampleVariantsDetector (VCFRecord.createDefaultPopulationVCFRecord,

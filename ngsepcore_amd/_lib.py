@@ -50,6 +50,7 @@ class NgsepParams(ctypes.Structure):
         ("relative_allele_counts", ctypes.c_int32),
         ("rac_min_rd", ctypes.c_int32),
         ("rac_min_bq", ctypes.c_int32),
+        ("full_records", ctypes.c_int32),
     ]
 
 

@@ -80,6 +80,7 @@ void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g) {
     t->t_het = (long long)std::floor(K * t_het) + kBoundMargin;
     t->t_homo = kBoundMargin;
     g->ploidy = c->params.ploidy;
+    g->full_records = c->params.full_records || c->params.dump_all_positions ? 1 : 0;
     // the bounds prove SNVQ hom-ref calls; the pool algorithm only needs a valid non-reference call (its
     // variant needs an alternative allele count >= 1, createSNVVariantPool :313-320), the scan's candidate test
     g->use_bound = ok && !g->dump_all && std::isfinite(t_het) && g->ploidy < 3 ? 1 : 0;
@@ -656,8 +657,8 @@ static int stream_collect(ngsep_ctx* c) {
         std::vector<int64_t> kidx(j->sites.size());
         std::vector<int64_t> taken;                    // known entries already matched at the current position
         for (size_t i = 0; i < j->sites.size(); i++) {
-            ngsep_site_out& o = j->sites[i];
-            if (i == 0 || j->sites[i - 1].pos != o.pos) taken.clear();
+            SiteRec& o = j->sites.rec[i];
+            if (i == 0 || j->sites.rec[i - 1].pos != o.pos) taken.clear();
             auto it = std::lower_bound(c->known.begin() + kb, c->known.begin() + ke, (int64_t)o.pos,
                                        [](const ngsep_ctx::KnownVar& v, int64_t p) { return v.pos < p; });
             int64_t k = it - c->known.begin();
@@ -669,18 +670,13 @@ static int stream_collect(ngsep_ctx* c) {
             if (k < ke) o.qual = c->known[(size_t)k].qs;
         }
         for (size_t i = 1; i < j->sites.size(); i++)            // (records at one position: input order)
-            for (size_t k = i; k > 0 && j->sites[k - 1].pos == j->sites[k].pos && kidx[k - 1] > kidx[k]; k--) {
-                std::swap(j->sites[k - 1], j->sites[k]);
+            for (size_t k = i; k > 0 && j->sites.rec[k - 1].pos == j->sites.rec[k].pos && kidx[k - 1] > kidx[k]; k--) {
+                std::swap(j->sites.rec[k - 1], j->sites.rec[k]);
                 std::swap(kidx[k - 1], kidx[k]);
             }
     }
     if (c->sites.empty()) c->sites.swap(j->sites);
-    else if (!j->sites.empty()) {
-        const size_t from = c->sites.size();
-        c->sites.reserve(from + j->sites.size());
-        std::memcpy(c->sites.buf + from, j->sites.buf, j->sites.size() * sizeof(ngsep_site_out));
-        c->sites.n = from + j->sites.size();
-    }
+    else c->sites.append(j->sites);
     ContigReads& cr = c->contig;
     // (a later window's reads start at >= its w0 - max span + 1; reads ending 2 spans before it reach no tile of it)
     const int64_t keep_from = st.next_w0 - 2 * (int64_t)std::max<int32_t>(1, cr.max_span) - 64;
@@ -1726,10 +1722,15 @@ static double fisher_pvalue(std::vector<double>& lf, int a, int b, int c, int d)
 static void apply_strand_bias(SiteStore& sites, size_t from) {
     std::vector<double> lf;
     for (size_t i = from; i < sites.size(); i++) {
-        ngsep_site_out& s = sites[i];
-        if (s.n_alleles != 2 || s.genotype <= 0) continue;   // CalledSNV, not undecided/homRef (:218-220)
+        SiteRec& s = sites.rec[i];
+        if (s.pool || s.n_alleles != 2 || s.genotype <= 0) continue;   // CalledSNV, not undecided/homRef (:218-220)
         int r = dna_index(s.ref), a = s.alt;
-        double pv = fisher_pvalue(lf, s.strand_counts[r][0], s.strand_counts[a][0], s.strand_counts[r][1], s.strand_counts[a][1]);
+        int rn = s.strand[0], rp = s.strand[1], an = s.strand[2], ap = s.strand[3];
+        if (s.is_call & kRecExt) {
+            const ngsep_site_out& w = sites.ext[(size_t)SiteSet::ext_index(s)];
+            rn = w.strand_counts[r][0]; rp = w.strand_counts[r][1]; an = w.strand_counts[a][0]; ap = w.strand_counts[a][1];
+        }
+        double pv = fisher_pvalue(lf, rn, an, rp, ap);
         s.strand_bias = (int8_t)std::min(100, java_phred(pv));   // MAX_STRAND_BIAS_SCORE
     }
 }
@@ -1830,7 +1831,7 @@ static int finish_run(ngsep_ctx* c, size_t from, int64_t n, double scan_ms, doub
 }
 static int finish_run_into(ngsep_ctx* c, SiteStore& dest, size_t from, int64_t n, double scan_ms, double geno_ms, double total_ms,
                            int64_t ncand, double* elapsed_ms) {
-    dest.n = from + (size_t)n;
+    (void)n;
     if (c->params.calc_strand_bias && c->known.empty()) apply_strand_bias(dest, from);   // (genotypeSNV: none)
     c->stats.candidates = ncand;
     c->stats.hard_sites = (int32_t)device_last_hard(c->dev);
@@ -2110,7 +2111,8 @@ extern "C" int ngsep_fetch_sites(ngsep_ctx* c, ngsep_site_out* out, int64_t cap,
     if (!c) return NGSEP_E_INVALID;
     int64_t n = (int64_t)c->sites.size();
     if (n_out) *n_out = n;
-    if (out && cap > 0) std::memcpy(out, c->sites.data(), sizeof(ngsep_site_out) * (size_t)std::min(n, cap));
+    if (out && cap > 0)
+        for (int64_t i = 0; i < std::min(n, cap); i++) out[i] = c->sites.full((size_t)i);
     return NGSEP_OK;
 }
 

@@ -59,7 +59,8 @@ constexpr int kMcMaxCalls = 254;           // multisample candidate column: vali
 
 // the (first) alternative allele of a record as a DNA index: a pool record keeps its variant's alleles in
 // the mask bits (ngsep_site_out.pool), an SNVQ record in .alt
-inline int site_alt(const ngsep_site_out& s) {
+template <class R>
+inline int site_alt(const R& s) {
     if (!s.pool) return s.alt;
     for (int a = 0; a < 4; a++)
         if (((s.pool >> a) & 1) && "ACGT"[a] != s.ref) return a;
@@ -121,6 +122,7 @@ struct GenotypeParams {
                                // 4 no tiles, 8 tally without posterior, 16 posterior kernel reads the queue only,
                                // 32 population kernel gathers only, 64 population kernel stops after the tallies
     int32_t use_bound;         // 1: candidates proven hom-ref by the integer bound are dropped in the tile kernel
+    int32_t full_records;      // 1: every record whole (ngsep_params.full_records); dump mode implies it
     int32_t ploidy;            // >= 3: KP runs the pool algorithm (k_posterior_pool), KT queues every
                                // position with a valid non-reference call (the pool variant needs one)
     int32_t exact_bound;       // bit-plane KT: 1 applies the exact integer bound to count-bound survivors
@@ -272,7 +274,86 @@ struct PinnedStore {
     void push_back(const T& o) { reserve(n + 1); buf[n++] = o; }
     void swap(PinnedStore& o) { std::swap(buf, o.buf); std::swap(n, o.n); std::swap(cap, o.cap); }
 };
-using SiteStore = PinnedStore<ngsep_site_out>;
+// Device -> host record of one site: 64 B, what the reference's CalledSNV keeps
+// (variants/CalledSNV.java:42-45,259-265: genotype, GQ, QUAL, DP, the base counts, log-conditionals of the
+// called pair, the strand-bias inputs).  A record that needs more (multi-allelic / pool calls, dump mode,
+// params.full_records, counts past 65535) is whole in the set's `ext` list: is_call bit 1 set and L[0]'s bits
+// hold its index there; its header fields below are filled as well.
+struct SiteRec {
+    int32_t seq_id;
+    int32_t pos;               // KP: the global position; KO: the 1-based position
+    int8_t ref, n_alleles, alt, third, genotype, strand_bias;
+    int16_t gq;
+    int16_t qual;
+    int8_t is_call;            // bit 0: passes the listener filters; bit 1: whole record in ext
+    uint8_t pool;
+    int32_t dp;
+    uint16_t counts[4];        // A,C,G,T
+    uint16_t strand[4];        // reference negative / positive, alternative negative / positive
+    double L[3];               // logc (ref,ref), (ref,alt), (alt,alt)
+};
+static_assert(sizeof(SiteRec) == 64, "site record layout");
+constexpr int8_t kRecCall = 1, kRecExt = 2;
+
+inline int site_tri(int i, int j) {   // index of L[i][j] in ngsep_site_out.logc
+    if (i > j) std::swap(i, j);
+    static const int base[4] = {0, 4, 7, 9};
+    return base[i] + (j - i);
+}
+
+// the called sites of a run or a whole detector: the records (pinned: the device copies into them) and the
+// whole records they point to
+struct SiteSet {
+    PinnedStore<SiteRec> rec;
+    PinnedStore<ngsep_site_out> ext;
+    size_t size() const { return rec.size(); }
+    bool empty() const { return rec.empty(); }
+    void clear() { rec.clear(); ext.clear(); }
+    void swap(SiteSet& o) { rec.swap(o.rec); ext.swap(o.ext); }
+    static int64_t ext_index(const SiteRec& r) { return __builtin_bit_cast(int64_t, r.L[0]); }
+    // o's records after ours (ext indexes rebased)
+    void append(const SiteSet& o) {
+        if (o.empty()) return;
+        const size_t from = rec.size(), ebase = ext.size();
+        rec.reserve(from + o.rec.size());
+        std::memcpy(rec.buf + from, o.rec.buf, o.rec.size() * sizeof(SiteRec));
+        rec.n = from + o.rec.size();
+        if (!o.ext.empty()) {
+            ext.reserve(ebase + o.ext.size());
+            std::memcpy(ext.buf + ebase, o.ext.buf, o.ext.size() * sizeof(ngsep_site_out));
+            ext.n = ebase + o.ext.size();
+            if (ebase)
+                for (size_t i = from; i < rec.size(); i++)
+                    if (rec[i].is_call & kRecExt) rec[i].L[0] = __builtin_bit_cast(double, ext_index(rec[i]) + (int64_t)ebase);
+        }
+    }
+    // the ABI record of site i (ngsep_site_out)
+    ngsep_site_out full(size_t i) const {
+        const SiteRec& r = rec[i];
+        ngsep_site_out o;
+        if (r.is_call & kRecExt) {
+            o = ext[(size_t)ext_index(r)];
+        } else {
+            std::memset(&o, 0, sizeof o);
+            o.ref = r.ref; o.n_alleles = r.n_alleles; o.alt = r.alt; o.third = r.third; o.genotype = r.genotype;
+            o.gq = r.gq; o.dp = r.dp; o.pool = r.pool;
+            for (int k = 0; k < 4; k++) o.counts[k] = r.counts[k];
+            int ri = 0;
+            while (ri < 4 && "ACGT"[ri] != r.ref) ri++;
+            if (ri < 4 && r.alt >= 0 && r.alt < 4) {
+                o.strand_counts[ri][0] = r.strand[0]; o.strand_counts[ri][1] = r.strand[1];
+                o.strand_counts[(int)r.alt][0] = r.strand[2]; o.strand_counts[(int)r.alt][1] = r.strand[3];
+                o.logc[site_tri(ri, ri)] = r.L[0];
+                o.logc[site_tri(ri, r.alt)] = r.L[1];
+                o.logc[site_tri(r.alt, r.alt)] = r.L[2];
+            }
+        }
+        o.seq_id = r.seq_id; o.pos = r.pos; o.qual = r.qual; o.strand_bias = r.strand_bias;
+        o.is_call = (int8_t)(r.is_call & kRecCall);
+        return o;
+    }
+};
+using SiteStore = SiteSet;
 
 // a read of the single-sample layout: global [gfirst, glast] and its projected bytes
 struct SRead {
@@ -326,7 +407,7 @@ struct Staged {            // everything resident for one run
     // 0x80 | ref << 5 | alt << 8 | 0x400) instead of scanning; counters preset to their number
     bool known = false;
     std::vector<int32_t> h_forced;
-    unsigned long long h_forced_ctr[4] = {0, 0, 0, 0};
+    unsigned long long h_forced_ctr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
 
 // Pinned host buffers of the single-sample layout, reused run after run (streamed windows: no page faults,

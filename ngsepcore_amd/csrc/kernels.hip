@@ -47,18 +47,21 @@ struct RunSlot {                     // one in-flight single-sample run (see dev
     hipStream_t stream = nullptr;            // its compute stream (runs of the two slots overlap)
     QueueSite* d_hard = nullptr;             // KT -> KP queue
     int64_t cap_hard = 0;
-    ngsep_site_out* d_brec = nullptr;        // KP's records by position bucket: bucket b = d_brec[b * bcap ..]
+    SiteRec* d_brec = nullptr;               // KP's records by position bucket: bucket b = d_brec[b * bcap ..]
+    ngsep_site_out* d_ext = nullptr;         // KP's whole records (multi-allelic, pool, dump mode, full_records)
+    int64_t cap_ext = 0, guess_ext = 0;
     int32_t* d_bcount = nullptr;             // records per bucket (zeroed by KT)
     int32_t* d_boff = nullptr;               // output offset per bucket (KS)
     int64_t nb_cap = 0, brec_cap = 0;
     LikTables* d_tables = nullptr;
     LikTables h_tables{};                    // last uploaded tables
     bool tables_valid = false;
-    ngsep_site_out* d_sorted = nullptr;
+    SiteRec* d_sorted = nullptr;
     int64_t cap = 0;
-    unsigned long long* d_ctr = nullptr;     // its counter set (4)
+    unsigned long long* d_ctr = nullptr;     // its counter set (8): records | fullest bucket, candidates, queue,
+                                             // exact-bound passes, whole records
     unsigned long long* h_ctr = nullptr;     // pinned copy
-    SiteStore host;                          // pinned D2H destination of the ordered records
+    SiteSet host;                            // pinned D2H destination of the ordered records and the whole ones
     hipEvent_t ev[6] = {};                   // KT start, KT end, KP end, after KO, copies done, KP start
     int64_t guess = 0;
     bool busy = false;
@@ -124,6 +127,7 @@ struct Device {
     int64_t n_reads = 0, g_len = 0, n_tiles = 0;
     int32_t max_span = 0, pad = 0, tile = 512, log2_tile = 9;
     int64_t last_n_sites = 1024;
+    int64_t last_n_ext = 0;
     int64_t last_hard = 0;
     int64_t last_exact = 0;     // wave passes of KT's exact integer bound in the last run
     int kt_blocks_per_cu[2] = {0, 0};
@@ -187,13 +191,81 @@ static_assert(sizeof(QueueSite) == 8, "QueueSite layout");
 // bucket of its position (KO orders the buckets).
 __device__ inline double pow10_j(double x) { return pow(10.0, x); }   // Math.pow(10.0, x)
 
+// One emitted site into its bucket slot: the 64-B SiteRec (engine.hpp) from the record's header dwords h
+// (ngsep_site_out layout: seq, gpos, ref|n_alleles|alt|third, genotype|strand_bias|gq, qual|is_call|pool, dp,
+// counts[4], strand_counts[4][2]) and its ten log-conditionals L.  A record the 64 B cannot hold (whole =
+// multi-allelic / pool / dump / full_records, or counts past 65535) goes whole to ext, the SiteRec pointing to it.
+__device__ inline void put_site(SiteRec* __restrict__ slot, ngsep_site_out* __restrict__ ext, unsigned long long* ext_n,
+                                int64_t ext_cap, const uint32_t (&h)[18], const double (&L)[10], bool whole, int ri, int ai) {
+    uint32_t big = 0;
+#pragma unroll
+    for (int t = 6; t < 18; t++) big |= h[t];
+    whole = whole || big > 0xFFFFu || ri < 0 || ri > 3 || ai < 0 || ai > 3;
+    auto pick = [&](int k) {                           // L[k] without dynamic register indexing
+        double v = 0;
+#pragma unroll
+        for (int e = 0; e < 10; e++) v = e == k ? L[e] : v;
+        return v;
+    };
+    auto tri = [](int i, int j) {
+        const int a = i < j ? i : j, b = i < j ? j : i;
+        return (a == 0 ? 0 : a == 1 ? 4 : a == 2 ? 7 : 9) + (b - a);
+    };
+    auto sel = [&](int k) {                            // h[k] for k in 10..17
+        uint32_t v = 0;
+#pragma unroll
+        for (int e = 10; e < 18; e++) v = e == k ? h[e] : v;
+        return v;
+    };
+    uint32_t w[16];
+    w[0] = h[0]; w[1] = h[1]; w[2] = h[2]; w[3] = h[3];
+    w[4] = h[4] | (whole ? (uint32_t)kRecExt << 16 : 0u);
+    w[5] = h[5];
+    w[6] = (h[6] & 0xFFFFu) | h[7] << 16;
+    w[7] = (h[8] & 0xFFFFu) | h[9] << 16;
+    double d0 = 0, d1 = 0, d2 = 0;
+    if (whole) {
+        w[8] = w[9] = 0;
+        const unsigned long long e = atomicAdd(ext_n, 1ull);
+        if ((int64_t)e < ext_cap) {
+            uint32_t* o = reinterpret_cast<uint32_t*>(ext + e);
+#pragma unroll
+            for (int t = 0; t < 18; t++) o[t] = h[t];
+#pragma unroll
+            for (int t = 0; t < 10; t++) {
+                const unsigned long long bits = __builtin_bit_cast(unsigned long long, L[t]);
+                o[18 + 2 * t] = (uint32_t)bits;
+                o[19 + 2 * t] = (uint32_t)(bits >> 32);
+            }
+        }
+        d0 = __builtin_bit_cast(double, (long long)e);
+    } else {
+        w[8] = (sel(10 + 2 * ri) & 0xFFFFu) | sel(11 + 2 * ri) << 16;
+        w[9] = (sel(10 + 2 * ai) & 0xFFFFu) | sel(11 + 2 * ai) << 16;
+        d0 = pick(tri(ri, ri));
+        d1 = pick(tri(ri, ai));
+        d2 = pick(tri(ai, ai));
+    }
+    const unsigned long long b0 = __builtin_bit_cast(unsigned long long, d0), b1 = __builtin_bit_cast(unsigned long long, d1),
+                             b2 = __builtin_bit_cast(unsigned long long, d2);
+    w[10] = (uint32_t)b0; w[11] = (uint32_t)(b0 >> 32);
+    w[12] = (uint32_t)b1; w[13] = (uint32_t)(b1 >> 32);
+    w[14] = (uint32_t)b2; w[15] = (uint32_t)(b2 >> 32);
+    uint4* o = reinterpret_cast<uint4*>(slot);
+    o[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    o[2] = make_uint4(w[8], w[9], w[10], w[11]);
+    o[3] = make_uint4(w[12], w[13], w[14], w[15]);
+}
+
 constexpr int kPostThreads = 256;
 __global__ __launch_bounds__(kPostThreads) void k_posterior(const QueueSite* __restrict__ queue, const unsigned long long* qn,
                                                    int64_t qcap, const TileInfo* __restrict__ tinfo,
                                                    const uint8_t* __restrict__ cpile, const uint32_t* __restrict__ cneg,
                                                    int32_t log2T, const LikTables* __restrict__ tabs, GenotypeParams gp,
-                                                   ngsep_site_out* __restrict__ brec, int32_t* __restrict__ bcount,
-                                                   int shift, int32_t bcap) {
+                                                   SiteRec* __restrict__ brec, int32_t* __restrict__ bcount,
+                                                   int shift, int32_t bcap, ngsep_site_out* __restrict__ ext,
+                                                   unsigned long long* ext_n, int64_t ext_cap) {
     __shared__ double s_t[3][32];   // A (log10(1-e)), H (heterozygous), E (error) per capped quality
     __shared__ double s_ev[16][kPostThreads];   // each lane's 16 genotype events (posterior phase)
     if (threadIdx.x < 96)
@@ -419,15 +491,8 @@ __global__ __launch_bounds__(kPostThreads) void k_posterior(const QueueSite* __r
             h[10 + 2 * t] = (uint32_t)sc[t][0];
             h[11 + 2 * t] = (uint32_t)sc[t][1];
         }
-        uint32_t* o = reinterpret_cast<uint32_t*>(brec + (int64_t)bk * bcap + k);
-#pragma unroll
-        for (int t = 0; t < 18; t++) o[t] = h[t];
-#pragma unroll
-        for (int t = 0; t < 10; t++) {
-            const unsigned long long bits = __builtin_bit_cast(unsigned long long, L[t]);
-            o[18 + 2 * t] = (uint32_t)bits;
-            o[19 + 2 * t] = (uint32_t)(bits >> 32);
-        }
+        const int ri = callable ? (int)((rc >> 5) & 3u) : -1;
+        put_site(brec + (int64_t)bk * bcap + k, ext, ext_n, ext_cap, h, L, gp.full_records != 0 || nal != 2, ri, alt);
     }
 }
 
@@ -589,8 +654,9 @@ __global__ __launch_bounds__(kPostThreads) void k_posterior_pool(const QueueSite
                                                         int64_t qcap, const TileInfo* __restrict__ tinfo,
                                                         const uint8_t* __restrict__ cpile, const uint32_t* __restrict__ cneg,
                                                         int32_t log2T, const PoolTables* __restrict__ pt, GenotypeParams gp,
-                                                        ngsep_site_out* __restrict__ brec, int32_t* __restrict__ bcount,
-                                                        int shift, int32_t bcap) {
+                                                        SiteRec* __restrict__ brec, int32_t* __restrict__ bcount,
+                                                        int shift, int32_t bcap, ngsep_site_out* __restrict__ ext,
+                                                        unsigned long long* ext_n, int64_t ext_cap) {
     const int32_t Tm = (1 << log2T) - 1;
     int64_t nq = (int64_t)*qn;
     if (nq > qcap) nq = qcap;
@@ -685,15 +751,7 @@ __global__ __launch_bounds__(kPostThreads) void k_posterior_pool(const QueueSite
             h[10 + 2 * t] = (uint32_t)sc[t][0];
             h[11 + 2 * t] = (uint32_t)sc[t][1];
         }
-        uint32_t* o = reinterpret_cast<uint32_t*>(brec + (int64_t)bk * bcap + k);
-#pragma unroll
-        for (int t = 0; t < 18; t++) o[t] = h[t];
-#pragma unroll
-        for (int t = 0; t < 10; t++) {
-            const unsigned long long bits = __builtin_bit_cast(unsigned long long, R.L[t]);
-            o[18 + 2 * t] = (uint32_t)bits;
-            o[19 + 2 * t] = (uint32_t)(bits >> 32);
-        }
+        put_site(brec + (int64_t)bk * bcap + k, ext, ext_n, ext_cap, h, R.L, true, dna[0], -1);
         (void)multi;
     }
 }
@@ -1668,9 +1726,9 @@ __global__ __launch_bounds__(1024) void ko_scan(const int32_t* __restrict__ bcou
 }
 
 constexpr int kKofBuckets = 16;                // one wave per bucket, 16 waves per workgroup
-__global__ __launch_bounds__(1024) void ko_fused(const ngsep_site_out* __restrict__ brec, const int32_t* __restrict__ bcount,
+__global__ __launch_bounds__(1024) void ko_fused(const SiteRec* __restrict__ brec, const int32_t* __restrict__ bcount,
                                                  const int32_t* __restrict__ boff, int64_t nb, int32_t bcap,
-                                                 ngsep_site_out* __restrict__ sorted, int64_t cap,
+                                                 SiteRec* __restrict__ sorted, int64_t cap,
                                                  const int4* __restrict__ wins, int32_t n_wins, int32_t bucket_span) {
     __shared__ uint32_t s_pos[kKofBuckets][1024];   // crowded buckets only (> 64 records)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1679,7 +1737,7 @@ __global__ __launch_bounds__(1024) void ko_fused(const ngsep_site_out* __restric
     if (b >= nb) return;
     const int32_t c = bcount[b] < bcap ? bcount[b] : bcap;
     if (c == 0) return;
-    const ngsep_site_out* src = brec + b * bcap;
+    const SiteRec* src = brec + b * bcap;
     const int64_t off = boff[b];
     // the last window starting at or before the bucket (wave-uniform); a record's window is that one or
     // (rarely) a later one.  Records only arise in window bodies, where the reference is non-zero.
@@ -1693,7 +1751,7 @@ __global__ __launch_bounds__(1024) void ko_fused(const ngsep_site_out* __restric
             else hi = mid - 1;
         }
     }
-    constexpr int W = sizeof(ngsep_site_out) / 4;   // 38 dwords
+    constexpr int W = sizeof(SiteRec) / 4;          // 16 dwords
     // rank (position, then arrival) and the mapped (sequence, 1-based position) of record k, on lane k
     // (c <= 64) or in rounds (crowded buckets)
     for (int k0 = 0; k0 < c; k0 += 64) {
@@ -1726,7 +1784,7 @@ __global__ __launch_bounds__(1024) void ko_fused(const ngsep_site_out* __restric
                     rank += (o < mine || (o == mine && m < k)) ? 1 : 0;
                 }
         }
-        // cooperative copy of this round's records: 38 consecutive lanes per record, coalesced
+        // cooperative copy of this round's records: 16 consecutive lanes per record, coalesced
         const int nr = min(64, c - k0);
         for (int i0 = 0; i0 < nr * W; i0 += 64) {     // wave-uniform trip count: the shuffles see every lane
             const int idx = i0 + lane;
@@ -1794,8 +1852,8 @@ Device* device_create(int ordinal, std::string& err) {
         for (int k = 0; k < 6; k++)     // 0-2 and 5 time the kernels; 3-4 only order the streams
             (void)hipEventCreateWithFlags(&sl.ev[k], (k < 3 || k == 5) ? hipEventDefault : hipEventDisableTiming);
     }
-    if (hipMalloc(&d->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(d->d_counters, 0, 16 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc(&d->d_counters, 24 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(d->d_counters, 0, 24 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&d->h_counters, 4 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
         hipMalloc(&d->d_tables, sizeof(LikTables)) != hipSuccess) {
         err = "device allocation failed";
@@ -1803,8 +1861,8 @@ Device* device_create(int ordinal, std::string& err) {
         return nullptr;
     }
     for (int k = 0; k < 2; k++) {
-        d->slot[k].d_ctr = d->d_counters + 8 + 4 * k;          // sets 2 and 3 (0-1: the multisample run)
-        if (hipHostMalloc(&d->slot[k].h_ctr, 4 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
+        d->slot[k].d_ctr = d->d_counters + 8 + 8 * k;          // sets 1 and 2 (0: the multisample run)
+        if (hipHostMalloc(&d->slot[k].h_ctr, 8 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
             err = "pinned allocation failed";
             return nullptr;
         }
@@ -1872,6 +1930,7 @@ void device_destroy(Device* d) {
         (void)hipFree(sl.d_tables);
         if (sl.stream && sl.stream != d->stream) (void)hipStreamDestroy(sl.stream);
         (void)hipFree(sl.d_sorted);
+        (void)hipFree(sl.d_ext);
         (void)hipHostFree(sl.h_ctr);
         for (auto& e : sl.ev) (void)hipEventDestroy(e);
     }
@@ -1997,8 +2056,18 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         HIP_TRY(hipEventSynchronize(sl.ev[4]));
         (void)hipFree(sl.d_sorted);
         sl.d_sorted = nullptr;
-        HIP_TRY(hipMalloc(&sl.d_sorted, (size_t)d->cap_sites * sizeof(ngsep_site_out)));
+        HIP_TRY(hipMalloc(&sl.d_sorted, (size_t)d->cap_sites * sizeof(SiteRec)));
         sl.cap = d->cap_sites;
+    }
+    // whole records: every record in dump mode / with full_records, else the rare multi-allelic and pool calls
+    const int64_t ewant = g.full_records ? d->cap_sites : std::max<int64_t>(4096, d->cap_sites / 64);
+    if (ewant > sl.cap_ext) {
+        HIP_TRY(hipEventSynchronize(sl.ev[4]));
+        if (!idle) HIP_TRY(hipStreamSynchronize(sl.stream));
+        (void)hipFree(sl.d_ext);
+        sl.d_ext = nullptr;
+        HIP_TRY(hipMalloc(&sl.d_ext, (size_t)ewant * sizeof(ngsep_site_out)));
+        sl.cap_ext = ewant;
     }
     // position buckets of the ordering pass: a few records each (dump mode: 16 positions, so 16
     // records at most; calls: 4096 positions and room for 64, grown when a run overflows)
@@ -2019,7 +2088,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         if (nb * bcap > sl.brec_cap) {
             (void)hipFree(sl.d_brec);
             sl.d_brec = nullptr;
-            HIP_TRY(hipMalloc(&sl.d_brec, (size_t)(nb * bcap) * sizeof(ngsep_site_out)));
+            HIP_TRY(hipMalloc(&sl.d_brec, (size_t)(nb * bcap) * sizeof(SiteRec)));
             sl.brec_cap = nb * bcap;
         }
     }
@@ -2038,7 +2107,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     if (s.known) {
         // -knownVariants: no scan, the input variants' sites (covered, in window order) are KP's queue
         if (nforced > 0) HIP_TRY(hipMemcpyAsync(sl.d_hard, s.h_forced.data(), (size_t)nforced * sizeof(QueueSite), hipMemcpyHostToDevice, sl.stream));
-        HIP_TRY(hipMemcpyAsync(ctr, s.h_forced_ctr, 4 * sizeof(unsigned long long), hipMemcpyHostToDevice, sl.stream));
+        HIP_TRY(hipMemcpyAsync(ctr, s.h_forced_ctr, 8 * sizeof(unsigned long long), hipMemcpyHostToDevice, sl.stream));
         hipLaunchKernelGGL(k_zero_i32, dim3((unsigned)std::min<int64_t>((nb + 255) / 256, 4096)), dim3(256), 0, sl.stream, sl.d_bcount, nb);
         HIP_TRY(hipGetLastError());
         d->last_hard = nforced;
@@ -2076,13 +2145,13 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
                               d->time_posterior ? sl.ev[5] : nullptr, d->time_posterior ? sl.ev[2] : nullptr, 0,
                               (const QueueSite*)sl.d_hard, (const unsigned long long*)(ctr + 2), sl.cap_hard,
                               (const TileInfo*)d->d_tinfo, (const uint8_t*)d->d_pile, (const uint32_t*)d->d_cneg, d->log2_tile,
-                              (const PoolTables*)d->d_pool, g, sl.d_brec, sl.d_bcount, shift, bcap);
+                              (const PoolTables*)d->d_pool, g, sl.d_brec, sl.d_bcount, shift, bcap, sl.d_ext, ctr + 4, sl.cap_ext);
     } else {
         hipExtLaunchKernelGGL(k_posterior, dim3(kp_grid), dim3(kPostThreads), 0, sl.stream,
                               d->time_posterior ? sl.ev[5] : nullptr, d->time_posterior ? sl.ev[2] : nullptr, 0,
                               (const QueueSite*)sl.d_hard, (const unsigned long long*)(ctr + 2), sl.cap_hard,
                               (const TileInfo*)d->d_tinfo, (const uint8_t*)d->d_pile, (const uint32_t*)d->d_cneg, d->log2_tile,
-                              (const LikTables*)sl.d_tables, g, sl.d_brec, sl.d_bcount, shift, bcap);
+                              (const LikTables*)sl.d_tables, g, sl.d_brec, sl.d_bcount, shift, bcap, sl.d_ext, ctr + 4, sl.cap_ext);
     }
     HIP_TRY(hipGetLastError());
     // order the records by position on the device (one kernel; counters[0] = records | max bucket << 40)
@@ -2097,11 +2166,15 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     hipStream_t cs = on_compute ? sl.stream : d->copy_stream;
     if (!on_compute) HIP_TRY(hipEventRecord(sl.ev[3], sl.stream));
     sl.guess = std::min<int64_t>(d->cap_sites, d->last_n_sites + d->last_n_sites / 64 + 64);
-    sl.host.reserve((size_t)sl.guess);
+    sl.guess_ext = std::min<int64_t>(sl.cap_ext, d->last_n_ext + d->last_n_ext / 64 + 16);
+    sl.host.rec.reserve((size_t)sl.guess);
+    sl.host.ext.reserve((size_t)sl.guess_ext);
     if (!on_compute) HIP_TRY(hipStreamWaitEvent(cs, sl.ev[3], 0));
-    HIP_TRY(hipMemcpyAsync(sl.h_ctr, ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, cs));
-    HIP_TRY(hipMemcpyAsync(sl.host.buf, sl.d_sorted, (size_t)sl.guess * sizeof(ngsep_site_out), hipMemcpyDeviceToHost, cs));
-    HIP_TRY(hipMemsetAsync(ctr, 0, 4 * sizeof(unsigned long long), cs));
+    HIP_TRY(hipMemcpyAsync(sl.h_ctr, ctr, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemcpyAsync(sl.host.rec.buf, sl.d_sorted, (size_t)sl.guess * sizeof(SiteRec), hipMemcpyDeviceToHost, cs));
+    if (sl.guess_ext > 0)
+        HIP_TRY(hipMemcpyAsync(sl.host.ext.buf, sl.d_ext, (size_t)sl.guess_ext * sizeof(ngsep_site_out), hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemsetAsync(ctr, 0, 8 * sizeof(unsigned long long), cs));
     HIP_TRY(hipEventRecord(sl.ev[4], cs));
     sl.g = g;
     sl.prune = prune;
@@ -2154,12 +2227,19 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
     int64_t n = (int64_t)(sl.h_ctr[0] & kNMask);
     int64_t mx = (int64_t)(sl.h_ctr[0] >> 40);          // fullest position bucket
     int64_t q = (int64_t)sl.h_ctr[2];
-    for (int attempt = 0; n > d->cap_sites || q > sl.cap_hard || (!sl.g.dump_all && mx > d->ko_bcap); attempt++) {
+    int64_t ne = (int64_t)sl.h_ctr[4];
+    for (int attempt = 0; n > d->cap_sites || q > sl.cap_hard || ne > sl.cap_ext || (!sl.g.dump_all && mx > d->ko_bcap); attempt++) {
         // more calls or undecided candidates than the buffers hold (e.g. -minQuality 0): drain, grow
         // and run this slot again in place (a later run in the other slot keeps its own results)
         if (attempt == 3) { err = "result buffers kept overflowing"; return -1; }
         HIP_TRY(hipDeviceSynchronize());
         if (grow_slot(d, sl, std::max(d->cap_sites, n + 1024), std::max(sl.cap_hard, q + 1024), err) != 0) return -1;
+        if (ne > sl.cap_ext) {
+            (void)hipFree(sl.d_ext);
+            sl.d_ext = nullptr;
+            HIP_TRY(hipMalloc(&sl.d_ext, (size_t)(ne + 1024) * sizeof(ngsep_site_out)));
+            sl.cap_ext = ne + 1024;
+        }
         if (!sl.g.dump_all && mx > d->ko_bcap) {
             // crowded buckets (e.g. -minQuality 0 calls most positions): room for the fullest one, up to
             // the 1024 keys a KO wave ranks; past that, 16-position buckets that cannot overflow
@@ -2172,25 +2252,29 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
         n = (int64_t)(sl.h_ctr[0] & kNMask);
         mx = (int64_t)(sl.h_ctr[0] >> 40);
         q = (int64_t)sl.h_ctr[2];
+        ne = (int64_t)sl.h_ctr[4];
     }
     sl.busy = false;
     d->n_collected++;
     if (n > sl.guess) {
-        sl.host.n = (size_t)sl.guess;                 // keep the records already copied when the store grows
-        sl.host.reserve((size_t)n);
-        HIP_TRY(hipMemcpy(sl.host.buf + sl.guess, sl.d_sorted + sl.guess, (size_t)(n - sl.guess) * sizeof(ngsep_site_out),
+        sl.host.rec.n = (size_t)sl.guess;             // keep the records already copied when the store grows
+        sl.host.rec.reserve((size_t)n);
+        HIP_TRY(hipMemcpy(sl.host.rec.buf + sl.guess, sl.d_sorted + sl.guess, (size_t)(n - sl.guess) * sizeof(SiteRec),
                           hipMemcpyDeviceToHost));
     }
-    sl.host.n = (size_t)n;
-    d->last_n_sites = n;
-    if (out->size() == 0) out->swap(sl.host);
-    else {
-        const size_t from = out->size();
-        out->reserve(from + (size_t)n);
-        std::memcpy(out->buf + from, sl.host.buf, (size_t)n * sizeof(ngsep_site_out));
-        out->n = from + (size_t)n;
+    if (ne > sl.guess_ext) {
+        sl.host.ext.n = (size_t)sl.guess_ext;
+        sl.host.ext.reserve((size_t)ne);
+        HIP_TRY(hipMemcpy(sl.host.ext.buf + sl.guess_ext, sl.d_ext + sl.guess_ext,
+                          (size_t)(ne - sl.guess_ext) * sizeof(ngsep_site_out), hipMemcpyDeviceToHost));
     }
-    sl.host.n = 0;
+    sl.host.rec.n = (size_t)n;
+    sl.host.ext.n = (size_t)ne;
+    d->last_n_sites = n;
+    d->last_n_ext = ne;
+    if (out->size() == 0) out->swap(sl.host);
+    else out->append(sl.host);
+    sl.host.clear();
     *n_out = n;
     float a = 0, a2 = 0;
     if (d->time_scan) (void)hipEventElapsedTime(&a, sl.ev[0], sl.ev[1]);

@@ -331,8 +331,9 @@ extern "C" int ngsep_append_vcf_records(ngsep_ctx* c, const char* path) {
     if (!f) return set_error(c, NGSEP_E_IO, std::string("cannot write ") + path);
     std::string buf;
     buf.reserve(1 << 20);
-    for (const ngsep_site_out& s : c->sites) {
-        if (!s.is_call) continue;
+    for (size_t i = 0; i < c->sites.size(); i++) {
+        if (!(c->sites.rec[i].is_call & kRecCall)) continue;
+        const ngsep_site_out s = c->sites.full(i);
         format_site(c, s, buf);
         if (buf.size() > (1 << 20)) { std::fwrite(buf.data(), 1, buf.size(), f); buf.clear(); }
     }

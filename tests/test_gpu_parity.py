@@ -280,3 +280,36 @@ def test_reference_fields_single_sample_dump(tmp_path):
         if got_pl == (int(r["pl_rr"]), int(r["pl_ra"]), int(r["pl_aa"])):
             checked += 1
     assert checked == 10508
+
+
+def test_full_records_agree_with_default(tmp_path):
+    """ngsep_params.full_records (ABI 5): the whole CountsHelper state per record.  The default records carry
+    what CalledSNV keeps -- the (ref,ref), (ref,alt), (alt,alt) log-conditionals and the reference / alternative
+    strand counts -- and must equal those entries of the whole records bit for bit; the VCF is the same."""
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=2, depth=20, seed=71, snv_rate=3e-3)
+    fa, sam, bam = syn.write(os.path.join(str(tmp_path), "fr"))
+    syn.close()
+    runs = {}
+    for full in (0, 1):
+        out = os.path.join(str(tmp_path), f"fr{full}.vcf")
+        with GpuPileupSession(gpu_params(full_records=full, calc_strand_bias=1)) as s:
+            s.load_fasta(fa)
+            s.processFileBatches(bam)
+            runs[full] = s.getCalledVariants()
+            s.write_vcf(out)
+    lean, whole = runs[0], runs[1]
+    assert len(lean) == len(whole) > 100
+    n_multi = 0
+    for a, b in zip(lean, whole):
+        assert (a.sequence, a.pos, a.alleles, a.genotype, a.gq, a.qual, a.dp, a.counts, a.strand_bias) == \
+               (b.sequence, b.pos, b.alleles, b.genotype, b.gq, b.qual, b.dp, b.counts, b.strand_bias)
+        if len(a.alleles) == 2:
+            ri, ai = "ACGT".index(a.alleles[0]), "ACGT".index(a.alleles[1])
+            for i, j in ((ri, ri), (ri, ai), (ai, ai)):
+                assert a.log_conditional(i, j) == b.log_conditional(i, j)
+            for k in (ri, ai):
+                assert a.strand_counts[k] == b.strand_counts[k]
+        else:
+            n_multi += 1
+            assert a.logc == b.logc and a.strand_counts == b.strand_counts   # multi-allelic records are whole
+    assert open(os.path.join(str(tmp_path), "fr0.vcf")).read() == open(os.path.join(str(tmp_path), "fr1.vcf")).read()
