@@ -890,7 +890,12 @@ void k_tile_scan(const uint32_t* __restrict__ vplane, const uint16_t* __restrict
     constexpr int KC = 7;                           // bits of a 64-row chunk's count
     constexpr int P = T / 64;                       // positions per lane
     __shared__ ScanShared sh;
-    __shared__ uint32_t s_na[kScanWaves][T];        // per-position other-allele counts of the wave's tile
+    // per-position other-allele counts of the wave's tile; position p at (p % P) * 65 + p / P, so the P reads and
+    // writes of a lane's own positions (p = P lane + j) touch consecutive banks across the wave and consecutive
+    // positions of the list fall in different banks
+    constexpr int NAS = 65;
+    __shared__ uint32_t s_na[kScanWaves][P * NAS];
+    auto na_at = [](int p) { return (p % P) * NAS + p / P; };
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lw = lane & (W - 1), lg = lane / W;   // this lane's word and row group (plane counting)
@@ -1039,18 +1044,18 @@ void k_tile_scan(const uint32_t* __restrict__ vplane, const uint16_t* __restrict
         // other-allele counts per position: the list's entries into LDS counters
         uint32_t* na_w = s_na[wv];
 #pragma unroll
-        for (int j = 0; j < P; j++) na_w[P * lane + j] = 0;
+        for (int j = 0; j < P; j++) na_w[j * NAS + lane] = 0;
         wave_sync();
         for (int e = 0; e < ne; e += 64) {
             const uint32_t pe = e == 0 ? e0 : (uint32_t)olist[lo + e + lane];
-            if (e + lane < ne) atomicAdd(&na_w[pe & (T - 1)], 1u);
+            if (e + lane < ne) atomicAdd(&na_w[na_at((int)(pe & (T - 1)))], 1u);
         }
         wave_sync();
         uint32_t mine = 0;
 #pragma unroll
         for (int j = 0; j < P; j++) {
             const bool callable = ((refq >> (8 * j)) & 0x80u) != 0;
-            mine |= (callable && na_w[P * lane + j] != 0) ? 1u << j : 0u;
+            mine |= (callable && na_w[j * NAS + lane] != 0) ? 1u << j : 0u;
         }
         my_cand += (uint32_t)__popc(mine);
         if (gp.ablate & 1) continue;                   // diagnostics: scan only
@@ -1074,7 +1079,7 @@ void k_tile_scan(const uint32_t* __restrict__ vplane, const uint16_t* __restrict
                 uint32_t nv = 0;
 #pragma unroll
                 for (int k = 0; k < 8; k++) nv |= ((vs[k] >> j) & 1u) << k;
-                const uint32_t na = na_w[pp];
+                const uint32_t na = na_w[j * NAS + lane];
                 need = (int32_t)(nv - na) < (int32_t)sh.cb[na];   // the count bound does not drop it
             }
             if (bound && gp.exact_bound) {
