@@ -51,7 +51,6 @@ struct RunSlot {                     // one in-flight single-sample run (see dev
     ngsep_site_out* d_ext = nullptr;         // KP's whole records (multi-allelic, pool, dump mode, full_records)
     int64_t cap_ext = 0, guess_ext = 0;
     int32_t* d_bcount = nullptr;             // records per bucket (zeroed by KT)
-    int32_t* d_boff = nullptr;               // output offset per bucket (KS)
     int64_t nb_cap = 0, brec_cap = 0;
     LikTables* d_tables = nullptr;
     LikTables h_tables{};                    // last uploaded tables
@@ -1678,72 +1677,63 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
 
 // ------------------------------------------------------------------------------------------
 // KO: order the emitted records by global position.  KP appended every record to the bucket of its
-//     position (2^shift positions per bucket, bcap records each).  KS (one workgroup) turns the bucket
-//     counts into output offsets (exclusive prefix) and writes the record count and the fullest
-//     bucket; KO ranks each bucket's keys (one wave per bucket) and copies the records in order.
+//     position (2^shift positions per bucket, bcap records each).  Each KO workgroup sums the (capped)
+//     counts of the buckets before its 16 for their output offsets (an L2-resident read: no separate
+//     scan launch), block 0 writes the record count and the fullest bucket; one wave per bucket ranks
+//     its keys and copies the records in order.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void ko_scan(const int32_t* __restrict__ bcount, int64_t nb, int32_t bcap,
-                                                int32_t* __restrict__ boff, unsigned long long* counters) {
-    __shared__ int32_t s_wsum[16];
-    __shared__ int32_t s_mx[16];
-    __shared__ long long s_raw[16];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int64_t per = (nb + 1023) / 1024;
-    const int64_t b0 = tid * per, b1 = b0 + per < nb ? b0 + per : nb;
-    int32_t sum = 0, mx = 0;
-    long long raw = 0;
-    for (int64_t b = b0; b < b1; b++) {
-        const int32_t c = bcount[b];
-        sum += c < bcap ? c : bcap;
-        raw += c;
-        mx = c > mx ? c : mx;
-    }
-    // inclusive wave scan of the per-thread sums, then the 16 wave totals
-    int32_t inc = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int32_t v = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += v;
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        const int32_t m2 = __shfl_xor(mx, o, 64);
-        mx = m2 > mx ? m2 : mx;
-        raw += __shfl_xor(raw, o, 64);
-    }
-    if (lane == 63) s_wsum[wv] = inc;
-    if (lane == 0) { s_mx[wv] = mx; s_raw[wv] = raw; }
-    __syncthreads();
-    int32_t before = 0;
-    for (int k = 0; k < wv; k++) before += s_wsum[k];
-    int32_t run = before + inc - sum;
-    for (int64_t b = b0; b < b1; b++) {
-        boff[b] = run;
-        const int32_t c = bcount[b];
-        run += c < bcap ? c : bcap;
-    }
-    if (tid == 0) {
-        int32_t m = 0;
-        long long total = 0;
-        for (int k = 0; k < 16; k++) { m = s_mx[k] > m ? s_mx[k] : m; total += s_raw[k]; }
-        // every record KP emitted and the fullest bucket: above bcap the host grows the buckets and reruns
-        counters[0] = (unsigned long long)total | ((unsigned long long)m << 40);
-    }
-}
 
 constexpr int kKofBuckets = 16;                // one wave per bucket, 16 waves per workgroup
 __global__ __launch_bounds__(1024) void ko_fused(const SiteRec* __restrict__ brec, const int32_t* __restrict__ bcount,
-                                                 const int32_t* __restrict__ boff, int64_t nb, int32_t bcap,
+                                                 int64_t nb, int32_t bcap, unsigned long long* __restrict__ counters,
                                                  SiteRec* __restrict__ sorted, int64_t cap,
                                                  const int4* __restrict__ wins, int32_t n_wins, int32_t bucket_span) {
     __shared__ uint32_t s_pos[kKofBuckets][1024];   // crowded buckets only (> 64 records)
+    __shared__ int32_t s_red[16], s_cnt[kKofBuckets];
+    __shared__ int32_t s_mx[16];
+    __shared__ long long s_raw[16];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int64_t b0 = (int64_t)blockIdx.x * kKofBuckets;
+    // the output offset of this block's buckets: the (capped) records of every bucket before them, then a prefix
+    // over its own 16; block 0 also totals every record KP emitted and the fullest bucket (above bcap the host
+    // grows the buckets and reruns)
+    {
+        int32_t part = 0, mx = 0;
+        long long raw = 0;
+        const int64_t lim = blockIdx.x == 0 ? nb : b0;
+        for (int64_t b = tid; b < lim; b += 1024) {
+            const int32_t c = bcount[b];
+            if (b < b0) part += c < bcap ? c : bcap;
+            raw += c;
+            mx = c > mx ? c : mx;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            part += __shfl_xor(part, o, 64);
+            raw += __shfl_xor(raw, o, 64);
+            const int32_t m2 = __shfl_xor(mx, o, 64);
+            mx = m2 > mx ? m2 : mx;
+        }
+        if (lane == 0) { s_red[wv] = part; s_mx[wv] = mx; s_raw[wv] = raw; }
+        if (tid < kKofBuckets) {
+            const int32_t c = b0 + tid < nb ? bcount[b0 + tid] : 0;
+            s_cnt[tid] = c < bcap ? c : bcap;
+        }
+        __syncthreads();
+        if (blockIdx.x == 0 && tid == 0) {
+            int32_t m = 0;
+            long long total = 0;
+            for (int k = 0; k < 16; k++) { m = s_mx[k] > m ? s_mx[k] : m; total += s_raw[k]; }
+            counters[0] = (unsigned long long)total | ((unsigned long long)m << 40);
+        }
+    }
     const int64_t b = b0 + wv;
     if (b >= nb) return;
-    const int32_t c = bcount[b] < bcap ? bcount[b] : bcap;
+    const int32_t c = s_cnt[wv];
     if (c == 0) return;
     const SiteRec* src = brec + b * bcap;
-    const int64_t off = boff[b];
+    int64_t off = 0;
+    for (int k = 0; k < 16; k++) off += s_red[k];
+    for (int k = 0; k < wv; k++) off += s_cnt[k];
     // the last window starting at or before the bucket (wave-uniform); a record's window is that one or
     // (rarely) a later one.  Records only arise in window bodies, where the reference is non-zero.
     int32_t wb = 0;
@@ -1930,7 +1920,6 @@ void device_destroy(Device* d) {
     for (auto& sl : d->slot) {
         (void)hipFree(sl.d_brec);
         (void)hipFree(sl.d_bcount);
-        (void)hipFree(sl.d_boff);
         (void)hipFree(sl.d_hard);
         (void)hipFree(sl.d_tables);
         if (sl.stream && sl.stream != d->stream) (void)hipStreamDestroy(sl.stream);
@@ -2083,11 +2072,8 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         if (!idle) HIP_TRY(hipStreamSynchronize(sl.stream));
         if (nb > sl.nb_cap) {
             (void)hipFree(sl.d_bcount);
-            (void)hipFree(sl.d_boff);
             sl.d_bcount = nullptr;
-            sl.d_boff = nullptr;
             HIP_TRY(hipMalloc(&sl.d_bcount, (size_t)nb * sizeof(int32_t)));
-            HIP_TRY(hipMalloc(&sl.d_boff, (size_t)nb * sizeof(int32_t)));
             sl.nb_cap = nb;
         }
         if (nb * bcap > sl.brec_cap) {
@@ -2160,9 +2146,8 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     }
     HIP_TRY(hipGetLastError());
     // order the records by position on the device (one kernel; counters[0] = records | max bucket << 40)
-    hipLaunchKernelGGL(ko_scan, dim3(1), dim3(1024), 0, sl.stream, (const int32_t*)sl.d_bcount, nb, bcap, sl.d_boff, ctr);
     hipLaunchKernelGGL(ko_fused, dim3((unsigned)((nb + kKofBuckets - 1) / kKofBuckets)), dim3(64 * kKofBuckets), 0, sl.stream, sl.d_brec,
-                       (const int32_t*)sl.d_bcount, (const int32_t*)sl.d_boff, nb, bcap, sl.d_sorted, sl.cap, d->d_wins, d->n_wins, 1 << shift);
+                       (const int32_t*)sl.d_bcount, nb, bcap, ctr, sl.d_sorted, sl.cap, d->d_wins, d->n_wins, 1 << shift);
     HIP_TRY(hipGetLastError());
     // copies: counters and a prefix of the ordered records (sized from the previous run) straight into
     // the slot's pinned store, then the counter set is cleared for the slot's next run.  On the copy
