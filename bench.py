@@ -161,7 +161,7 @@ def load_traffic(workload_key: str):
     """Per-launch HBM bytes of the scan kernel from the committed PMC passes (profiles/pmc_traffic*.json,
     one file per workload), or None."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json"))):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json")), reverse=True):   # newest tag first
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
