@@ -40,10 +40,12 @@ CASES = {
 # BASELINE.json configs at full size (the bench workloads): only the md5 and the record count of the oracle's
 # VCF are committed (tests/golden/full_sizes.json); the GPU suite regenerates the data on the box and
 # compares the HIP VCF byte for byte.  configs[1] = yeast 30x (seed 2), configs[2] = human chr20 30x
-# (seed 3, per-contig streams: the bench's chr20 workload)
+# (seed 3, per-contig streams: the bench's chr20 workload); configs[3] = human WGS 30x (seed 4): chr21, one of
+# the contigs of the bench's shard 0 of 8 (bench.py --config wgs generates each contig exactly this way)
 FULL_CASES = {
     "configs1_yeast_30x": dict(genome=0, depth=30, seed=2),
     "configs2_chr20_30x": dict(genome=1, contig_first=19, n_contigs=1, depth=30, seed=3, rng_per_contig=1),
+    "configs3_wgs_chr21_30x": dict(genome=1, contig_first=20, n_contigs=1, depth=30, seed=4, rng_per_contig=1),
 }
 # CoverageStats (CoverageStatisticsCalculator) fixtures: synth case -> (min_mq, max_coverage)
 COVERAGE_CASES = {"edge_2contigs_25x": (20, 300), "c1_chrI_10x": (20, 12)}
