@@ -1,4 +1,5 @@
-"""BASELINE.json configs[1] (yeast 30x) and configs[2] (human chr20 30x) at full size: the HIP VCF equals,
+"""BASELINE.json configs[1] (yeast 30x), configs[2] (human chr20 30x) and a configs[3] contig (human WGS 30x, chr21
+of the bench's 8-GPU shard 0) at full size: the HIP VCF equals,
 byte for byte, the oracle's VCF committed as tests/golden/<name>.vcf.gz (md5 and record count in
 tests/golden/full_sizes.json, made by make_golden.py --full in the build container).  The data is
 regenerated here from the same seeds; at 30x the scan's count bound drops ~98.6 % of the candidates, so
