@@ -191,6 +191,29 @@ def end_to_end(fa: str, bam: str, device: int):
                     f"{os.environ.get('NGSEP_THREADS') or cpu_cores()}"}
 
 
+def end_to_end_population(fa: str, bams, device: int):
+    """BAM files on disk -> population VCF on disk: MultisampleVariantsDetector.run through
+    ngsep_call_population_bams in a fresh context (merge of the sample BAMs in the generator's order, decode,
+    admission, population layout, H2D, KTM/KPM, VCF writing), wall time."""
+    from ngsepcore_amd.discovery import MultisampleVariantsDetector
+    out = os.path.join(os.path.dirname(fa), "e2e_pop.vcf")
+    mvd = MultisampleVariantsDetector()
+    mvd.device = device
+    mvd.setGenome(fa)
+    mvd.setOutFilename(out)
+    t0 = time.perf_counter()
+    s = mvd.run(list(bams))
+    t1 = time.perf_counter()
+    st = s.stats()
+    s.close()
+    n_rec = sum(1 for l in open(out) if not l.startswith("#"))
+    return {"wall_s": t1 - t0, "positions": int(st.positions_genotyped), "value": st.positions_genotyped / (t1 - t0),
+            "unit": "positions/s", "vcf_records": n_rec, "bams": len(bams),
+            "bam_bytes": sum(os.path.getsize(b) for b in bams),
+            "note": "ngsep_call_population_bams: sample BAMs on disk -> population VCF on disk incl. FASTA load; "
+                    f"host threads {os.environ.get('NGSEP_THREADS') or cpu_cores()}"}
+
+
 def bench_coverage(args):
     """--config coverage: CoverageStats (CoverageStatisticsCalculator) on yeast 30x
     reads, resident in HBM; a step = one kc_tile_hist pass + D2H of the histograms (1 GPU)."""
@@ -296,11 +319,17 @@ def main():
             cpu = {"value": None, "error": str(e)}
 
     dist = None
+    backend = os.environ.get("NGSEP_DIST_BACKEND", "nccl")   # gloo: rehearsal of N ranks on fewer GPUs
     if world > 1:
         import torch
         import torch.distributed as tdist
+        ndev = torch.cuda.device_count()             # (does not initialise the GPU on this image)
+        if backend == "nccl" and ndev < world:
+            log(f"bench.py: {world} ranks but {ndev} GPU(s); one process per GPU (NGSEP_DIST_BACKEND=gloo to rehearse)")
+            sys.exit(2)
+        local_rank = local_rank % max(1, ndev)
         torch.cuda.set_device(local_rank)
-        tdist.init_process_group(backend="nccl")
+        tdist.init_process_group(backend=backend)
         dist = tdist
 
     import pysynth
@@ -405,6 +434,15 @@ def main():
                 pysynth.lib().ngs_synth_write_bam(syn.h, bam.encode())
                 e2e_src = (tmp, fa, bam)
                 log(f"[rank 0] wrote the end-to-end BAM ({os.path.getsize(bam) / 1e9:.2f} GB) in {time.time() - tw:.1f}s")
+            if multi and rank == 0 and world == 1 and not args.no_e2e:
+                # the same population as one BAM per sample on local disk for the end-to-end run
+                tmp = tempfile.mkdtemp(prefix="ngsep_e2e_")
+                tw = time.time()
+                fa = os.path.join(tmp, "shard.fa")
+                pysynth.lib().ngs_synth_write_fasta(syn.h, fa.encode())
+                bams = syn.write_sample_bams(os.path.join(tmp, "pop"))
+                e2e_src = (tmp, fa, bams)
+                log(f"[rank 0] wrote {len(bams)} sample BAMs for the end-to-end run in {time.time() - tw:.1f}s")
             if item is not None or len(grp) == 1:
                 syn.close()
         ts = time.time()
@@ -481,7 +519,7 @@ def main():
     e2e = None
     if e2e_src is not None:
         try:
-            e2e = end_to_end(e2e_src[1], e2e_src[2], local_rank)
+            e2e = (end_to_end_population if multi else end_to_end)(e2e_src[1], e2e_src[2], local_rank)
             log(f"[rank 0] end-to-end BAM -> VCF: {e2e['wall_s']:.2f}s, {e2e['value']:.4g} positions/s")
         except Exception as e:
             e2e = {"value": None, "error": str(e)}
@@ -490,7 +528,7 @@ def main():
 
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed, float(positions)], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, float(positions)], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         mx = t.clone()
         dist.all_reduce(mx[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
