@@ -901,6 +901,8 @@ std::vector<int> hashset_order(const std::vector<std::string>& ids) {
 struct Cursor {
     ngsep_bam* bam = nullptr;
     ngsep_read_batch batch{};
+    ngsep_read_batch pending{};        // the batch after `batch`, read ahead by the whole-file probe
+    bool has_pending = false;
     int64_t i = 0;
     bool done = false;
     std::vector<int32_t> rg_global;    // file read group -> global read group
@@ -910,24 +912,227 @@ struct Cursor {
         return e - 1;
     }
 };
+
+// AlignmentsPileupGenerator.processFiles over files read whole: the merged order (sequence, first, last, then
+// the lowest file index -- chooseNextAln, :268-289) built in parallel.  Split keys cut every file at the same key
+// (lower_bound), so each key range is an independent k-way merge; the records are then gathered into one merged
+// SoA by all host threads and handed to the sweep in batches of 2^18.
+int merge_whole_files(ngsep_ctx* c, std::vector<Cursor>& cur, int n_files) {
+    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    auto t_0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!host_timing) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[ngsep host] population merge: %s %.3f s\n", what, std::chrono::duration<double>(t - t_0).count());
+        t_0 = t;
+    };
+    struct Key { int32_t seq, first, last; };
+    auto kless = [](const Key& a, const Key& b) {
+        if (a.seq != b.seq) return a.seq < b.seq;
+        if (a.first != b.first) return a.first < b.first;
+        return a.last < b.last;
+    };
+    std::vector<std::vector<Key>> keys((size_t)n_files);
+    int64_t n_total = 0, fmax = 0;
+    for (int f = 0; f < n_files; f++) {
+        const int64_t n = cur[(size_t)f].done ? 0 : cur[(size_t)f].batch.n_reads;
+        keys[(size_t)f].resize((size_t)n);
+        n_total += n;
+        if (n > (cur[(size_t)fmax].done ? 0 : cur[(size_t)fmax].batch.n_reads)) fmax = f;
+    }
+    if (n_total == 0) return NGSEP_OK;
+    ngsep::parallel_for(n_files, 1, [&](int64_t lo, int64_t hi) {
+        for (int64_t f = lo; f < hi; f++) {
+            const Cursor& k = cur[(size_t)f];
+            for (size_t i = 0; i < keys[(size_t)f].size(); i++)
+                keys[(size_t)f][i] = Key{k.batch.seq_id[i], k.batch.first[i], k.last((int64_t)i)};
+        }
+    });
+    // split keys: quantiles of the largest file (a key range holds every file's records of those keys)
+    const std::vector<Key>& kf = keys[(size_t)fmax];
+    const int64_t parts = std::max<int64_t>(1, std::min<int64_t>(1024, n_total / 32768));
+    std::vector<Key> split;
+    for (int64_t q = 1; q < parts; q++) {
+        const Key x = kf[(size_t)((int64_t)kf.size() * q / parts)];
+        if (split.empty() || kless(split.back(), x)) split.push_back(x);
+    }
+    const int64_t np = (int64_t)split.size() + 1;
+    lap("keys");
+    // cut[f][p] = first record of file f in range p (np + 1 entries per file)
+    std::vector<std::vector<int64_t>> cut((size_t)n_files, std::vector<int64_t>((size_t)np + 1));
+    ngsep::parallel_for(n_files, 1, [&](int64_t lo, int64_t hi) {
+        for (int64_t f = lo; f < hi; f++) {
+            const auto& v = keys[(size_t)f];
+            auto& ct = cut[(size_t)f];
+            ct[0] = 0;
+            for (int64_t p = 1; p < np; p++)
+                ct[(size_t)p] = std::lower_bound(v.begin(), v.end(), split[(size_t)p - 1], kless) - v.begin();
+            ct[(size_t)np] = (int64_t)v.size();
+        }
+    });
+    // per range: the merged order (file, record) and its CIGAR / base totals
+    std::vector<std::vector<std::pair<int32_t, int32_t>>> order((size_t)np);
+    std::vector<int64_t> n_rec((size_t)np + 1, 0), n_cig((size_t)np + 1, 0), n_base((size_t)np + 1, 0);
+    ngsep::parallel_for(np, 1, [&](int64_t lo, int64_t hi) {
+        struct Head { Key k; int32_t file; int64_t i; };
+        std::vector<Head> heap;
+        auto before = [&](const Head& a, const Head& b) {
+            if (kless(a.k, b.k)) return true;
+            if (kless(b.k, a.k)) return false;
+            return a.file < b.file;
+        };
+        auto sift_down = [&](size_t i) {
+            const size_t n = heap.size();
+            while (true) {
+                size_t m = i;
+                const size_t l = 2 * i + 1, r = l + 1;
+                if (l < n && before(heap[l], heap[m])) m = l;
+                if (r < n && before(heap[r], heap[m])) m = r;
+                if (m == i) return;
+                std::swap(heap[i], heap[m]);
+                i = m;
+            }
+        };
+        for (int64_t p = lo; p < hi; p++) {
+            heap.clear();
+            int64_t tot = 0;
+            for (int f = 0; f < n_files; f++) {
+                const int64_t a = cut[(size_t)f][(size_t)p], b = cut[(size_t)f][(size_t)p + 1];
+                tot += b - a;
+                if (a < b) heap.push_back(Head{keys[(size_t)f][(size_t)a], f, a});
+            }
+            for (size_t i = heap.size() / 2; i-- > 0;) sift_down(i);
+            auto& ord = order[(size_t)p];
+            ord.reserve((size_t)tot);
+            int64_t nc = 0, nb = 0;
+            while (!heap.empty()) {
+                const int32_t f = heap[0].file;
+                const int64_t i = heap[0].i;
+                ord.emplace_back(f, (int32_t)i);
+                nc += cur[(size_t)f].batch.cigar_n[i];
+                nb += cur[(size_t)f].batch.seq_len[i];
+                if (i + 1 < cut[(size_t)f][(size_t)p + 1]) {
+                    heap[0].i = i + 1;
+                    heap[0].k = keys[(size_t)f][(size_t)i + 1];
+                } else {
+                    heap[0] = heap.back();
+                    heap.pop_back();
+                }
+                if (!heap.empty()) sift_down(0);
+            }
+            n_rec[(size_t)p + 1] = (int64_t)ord.size();
+            n_cig[(size_t)p + 1] = nc;
+            n_base[(size_t)p + 1] = nb;
+        }
+    });
+    lap("ordered ranges");
+    for (int64_t p = 0; p < np; p++) {
+        n_rec[(size_t)p + 1] += n_rec[(size_t)p];
+        n_cig[(size_t)p + 1] += n_cig[(size_t)p];
+        n_base[(size_t)p + 1] += n_base[(size_t)p];
+    }
+    const int64_t N = n_rec[(size_t)np];
+    // (uninitialised storage: the pages are first touched by the parallel gather)
+    RawBuf<int32_t> m_seq, m_first, m_flags, m_rg, m_cig_n, m_seqlen, m_cigar;
+    RawBuf<int64_t> m_cig_off, m_seq_off;
+    RawBuf<uint8_t> m_hasq;
+    RawBuf<char> m_bases, m_quals;
+    for (auto* v : {&m_seq, &m_first, &m_flags, &m_rg, &m_cig_n, &m_seqlen}) v->resize((size_t)N);
+    m_cigar.resize((size_t)std::max<int64_t>(1, n_cig[(size_t)np]));
+    m_cig_off.resize((size_t)N);
+    m_seq_off.resize((size_t)N);
+    m_hasq.resize((size_t)N);
+    m_bases.resize((size_t)std::max<int64_t>(1, n_base[(size_t)np]));
+    m_quals.resize((size_t)std::max<int64_t>(1, n_base[(size_t)np]));
+    ngsep::parallel_for(np, 1, [&](int64_t lo, int64_t hi) {
+        for (int64_t p = lo; p < hi; p++) {
+            int64_t r = n_rec[(size_t)p], co = n_cig[(size_t)p], so = n_base[(size_t)p];
+            for (const auto& fi : order[(size_t)p]) {
+                const Cursor& k = cur[(size_t)fi.first];
+                const int64_t i = fi.second;
+                m_seq[(size_t)r] = k.batch.seq_id[i];
+                m_first[(size_t)r] = k.batch.first[i];
+                m_flags[(size_t)r] = k.batch.flags[i];
+                const int32_t lrg = k.batch.read_group ? k.batch.read_group[i] : -1;
+                m_rg[(size_t)r] = lrg >= 0 && lrg < (int32_t)k.rg_global.size() ? k.rg_global[(size_t)lrg] : -1;
+                const int32_t cn = k.batch.cigar_n[i];
+                m_cig_off[(size_t)r] = co;
+                m_cig_n[(size_t)r] = cn;
+                std::memcpy(&m_cigar[(size_t)co], k.batch.cigar + k.batch.cigar_off[i], (size_t)cn * sizeof(int32_t));
+                co += cn;
+                const int32_t sl = k.batch.seq_len[i];
+                m_seq_off[(size_t)r] = so;
+                m_seqlen[(size_t)r] = sl;
+                std::memcpy(&m_bases[(size_t)so], k.batch.bases + k.batch.seq_off[i], (size_t)sl);
+                std::memcpy(&m_quals[(size_t)so], k.batch.quals + k.batch.seq_off[i], (size_t)sl);
+                so += sl;
+                m_hasq[(size_t)r] = k.batch.has_quals ? k.batch.has_quals[i] : 1;
+                r++;
+            }
+        }
+    });
+    lap("gather");
+    keys.clear();
+    order.clear();
+    const int64_t kBatch = (int64_t)1 << 18;
+    for (int64_t s0 = 0; s0 < N && !c->query_done; s0 += kBatch) {
+        ngsep_read_batch mb{};
+        mb.n_reads = std::min(kBatch, N - s0);
+        mb.seq_id = m_seq.data() + s0; mb.first = m_first.data() + s0; mb.flags = m_flags.data() + s0;
+        mb.read_group = m_rg.data() + s0; mb.cigar_off = m_cig_off.data() + s0; mb.cigar_n = m_cig_n.data() + s0;
+        mb.cigar = m_cigar.data(); mb.seq_off = m_seq_off.data() + s0; mb.seq_len = m_seqlen.data() + s0;
+        mb.bases = m_bases.data(); mb.quals = m_quals.data(); mb.has_quals = m_hasq.data() + s0;
+        const int r = ngsep_process_alignments(c, &mb);
+        if (r != NGSEP_OK) return r;
+    }
+    lap("sweep of the merged batches");
+    return NGSEP_OK;
+}
 }  // namespace
 
 extern "C" int ngsep_call_population_bams(ngsep_ctx* c, const char* const* bam_paths, int32_t n_files, const char* out_vcf_path) {
     if (!c || !bam_paths || n_files <= 0 || !out_vcf_path) return NGSEP_E_INVALID;
     if (!c->params.multisample) return set_error(c, NGSEP_E_INVALID, "ngsep_call_population_bams needs params.multisample = 1");
+    static const bool pop_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    auto tp = std::chrono::steady_clock::now();
+    auto plap = [&](const char* what) {
+        if (!pop_timing) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[ngsep host] population: %s %.3f s\n", what, std::chrono::duration<double>(t - tp).count());
+        tp = t;
+    };
     std::vector<Cursor> cur((size_t)n_files);
     auto close_all = [&]() { for (auto& k : cur) if (k.bam) ngsep_bam_close(k.bam); };
     // loadSamplesFromAlignmentHeaders (:499-523): read group -> sample over all files, samples by id
     std::vector<std::string> rg_ids, rg_sm;
     std::unordered_map<std::string, int32_t> rg_global;
+    // the files are opened (header read, decoder started) on all host threads; errors reported in file order
+    {
+        std::vector<int> orc((size_t)n_files, NGSEP_OK);
+        ngsep::parallel_for(n_files, 1, [&](int64_t lo, int64_t hi) {
+            for (int64_t f = lo; f < hi; f++) {
+                ngsep_bam* b = nullptr;
+                int r = ngsep_bam_open(c, bam_paths[f], &b);
+                if (r == NGSEP_OK && c->params.query_seq[0]) {   // -querySeq: every file read from the region's index chunks
+                    r = ngsep_bam_set_region(b, c->params.query_seq, std::max<int64_t>(1, c->params.query_first), c->params.query_last);
+                    if (r == NGSEP_E_IO) r = NGSEP_OK;
+                }
+                cur[(size_t)f].bam = b;
+                orc[(size_t)f] = r;
+            }
+        });
+        for (int f = 0; f < n_files; f++)
+            if (orc[(size_t)f] != NGSEP_OK) {
+                // the first failing file's message, deterministically: its open repeated alone
+                close_all();
+                ngsep_bam* b = nullptr;
+                const int r = ngsep_bam_open(c, bam_paths[f], &b);
+                if (r == NGSEP_OK) ngsep_bam_close(b);
+                return orc[(size_t)f];
+            }
+    }
     for (int f = 0; f < n_files; f++) {
-        int rc = ngsep_bam_open(c, bam_paths[f], &cur[(size_t)f].bam);
-        if (rc != NGSEP_OK) { close_all(); return rc; }
         ngsep_bam* b = cur[(size_t)f].bam;
-        if (c->params.query_seq[0]) {      // -querySeq: every file read from the region's index chunks
-            rc = ngsep_bam_set_region(b, c->params.query_seq, std::max<int64_t>(1, c->params.query_first), c->params.query_last);
-            if (rc != NGSEP_OK && rc != NGSEP_E_IO) { close_all(); return rc; }
-        }
         for (size_t g = 0; g < b->rg_ids.size(); g++) {
             auto it = rg_global.find(b->rg_ids[g]);
             if (it == rg_global.end()) {
@@ -941,6 +1146,7 @@ extern "C" int ngsep_call_population_bams(ngsep_ctx* c, const char* const* bam_p
             cur[(size_t)f].rg_global.push_back(it->second);
         }
     }
+    plap("open");
     std::vector<std::string> samples(rg_sm);
     std::sort(samples.begin(), samples.end());
     samples.erase(std::unique(samples.begin(), samples.end()), samples.end());
@@ -957,18 +1163,51 @@ extern "C" int ngsep_call_population_bams(ngsep_ctx* c, const char* const* bam_p
     for (const auto& x : samples) sid.push_back(x.c_str());
     int rc = ngsep_set_samples(c, (int32_t)samples.size(), sid.data(), (int32_t)rg_ids.size(), rg_sample.data(), rg_rank.data());
     if (rc != NGSEP_OK) { close_all(); return rc; }
+    plap("samples");
     // AlignmentsPileupGenerator.processFiles: k-way merge by GenomicRegionComparator (sequence order,
     // first, last), ties to the lowest file index (chooseNextAln, :268-289)
     auto refill = [&](Cursor& k) -> int {
         while (!k.done && k.i >= k.batch.n_reads) {
-            int r = ngsep_bam_next_batch(k.bam, 1 << 18, &k.batch);
-            if (r != NGSEP_OK) return r;
+            if (k.has_pending) {
+                k.batch = k.pending;
+                k.has_pending = false;
+            } else {
+                int r = ngsep_bam_next_batch(k.bam, 1 << 18, &k.batch);
+                if (r != NGSEP_OK) return r;
+            }
             k.i = 0;
             if (k.batch.n_reads == 0) k.done = true;
         }
         return NGSEP_OK;
     };
-    for (auto& k : cur) { rc = refill(k); if (rc != NGSEP_OK) { close_all(); return rc; } }
+    // every file read whole when it fits one batch of kWhole records (the reader keeps two batches, so the probe
+    // for a second one leaves the first valid): the merge then runs in parallel over key ranges
+    const int64_t kWhole = (int64_t)1 << 22;
+    bool whole = true;
+    const auto tl0 = std::chrono::steady_clock::now();
+    {
+        std::vector<int> brc((size_t)n_files, NGSEP_OK);
+        ngsep::parallel_for(n_files, 1, [&](int64_t lo, int64_t hi) {
+            for (int64_t f = lo; f < hi; f++) {
+                Cursor& k = cur[(size_t)f];
+                int r = ngsep_bam_next_batch(k.bam, kWhole, &k.batch);
+                if (r == NGSEP_OK && k.batch.n_reads > 0) {
+                    r = ngsep_bam_next_batch(k.bam, kWhole, &k.pending);
+                    k.has_pending = r == NGSEP_OK && k.pending.n_reads > 0;
+                }
+                k.i = 0;
+                if (k.batch.n_reads == 0) k.done = true;
+                brc[(size_t)f] = r;
+            }
+        });
+        for (int f = 0; f < n_files; f++) {
+            if (brc[(size_t)f] != NGSEP_OK) { close_all(); return brc[(size_t)f]; }
+            if (cur[(size_t)f].has_pending) whole = false;
+        }
+    }
+    if (std::getenv("NGSEP_HOST_TIMING"))
+        std::fprintf(stderr, "[ngsep host] population: %d files opened and read in %.3f s\n", n_files,
+                     std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0).count());
     // merged batch storage
     std::vector<int32_t> m_seq, m_first, m_flags, m_rg, m_cig_n, m_cigar, m_seqlen;
     std::vector<int64_t> m_cig_off, m_seq_off;
@@ -987,17 +1226,62 @@ extern "C" int ngsep_call_population_bams(ngsep_ctx* c, const char* const* bam_p
         m_cig_off.clear(); m_seq_off.clear(); m_hasq.clear(); m_bases.clear(); m_quals.clear();
         return r;
     };
-    while (!c->query_done) {
-        int best = -1;
-        int32_t bs = 0, bf = 0, bl = 0;
-        for (int f = 0; f < n_files; f++) {
-            Cursor& k = cur[(size_t)f];
-            if (k.done) continue;
-            const int32_t s2 = k.batch.seq_id[k.i], f2 = k.batch.first[k.i];
-            if (best >= 0 && (s2 > bs || (s2 == bs && (f2 > bf || (f2 == bf && k.last(k.i) >= bl))))) continue;
-            best = f; bs = s2; bf = f2; bl = k.last(k.i);
+    plap("open + whole-file reads");
+    if (whole && !c->query_done) {
+        rc = merge_whole_files(c, cur, n_files);
+        plap("merge + sweep");
+        // nothing references the files' batches any more: they are closed (decoders joined, buffers freed) on
+        // a thread of their own while the population layout and the device run proceed
+        std::thread closer(close_all);
+        if (rc == NGSEP_OK) {
+            rc = ngsep_notify_end(c);
+            plap("end of alignments (layout, device run)");
         }
-        if (best < 0) break;
+        if (rc == NGSEP_OK) {
+            rc = ngsep_write_population_vcf(c, out_vcf_path);
+            plap("VCF");
+        }
+        closer.join();
+        return rc;
+    }
+    // the files' next records in a binary min-heap on (sequence, first, last, file index): log2(files)
+    // comparisons per record instead of a scan over every file
+    struct Head { int32_t seq, first, last, file; };
+    auto before = [](const Head& a, const Head& b) {
+        if (a.seq != b.seq) return a.seq < b.seq;
+        if (a.first != b.first) return a.first < b.first;
+        if (a.last != b.last) return a.last < b.last;
+        return a.file < b.file;
+    };
+    std::vector<Head> heap;
+    heap.reserve((size_t)n_files);
+    auto head_of = [&](int f) {
+        const Cursor& k = cur[(size_t)f];
+        return Head{k.batch.seq_id[k.i], k.batch.first[k.i], k.last(k.i), f};
+    };
+    auto sift_down = [&](size_t i) {
+        const size_t n = heap.size();
+        while (true) {
+            size_t m = i;
+            const size_t l = 2 * i + 1, r = l + 1;
+            if (l < n && before(heap[l], heap[m])) m = l;
+            if (r < n && before(heap[r], heap[m])) m = r;
+            if (m == i) return;
+            std::swap(heap[i], heap[m]);
+            i = m;
+        }
+    };
+    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    double t_refill = 0, t_flush = 0;
+    const auto tm0 = std::chrono::steady_clock::now();
+    auto secs = [](std::chrono::steady_clock::time_point a) {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
+    };
+    for (int f = 0; f < n_files; f++)
+        if (!cur[(size_t)f].done) heap.push_back(head_of(f));
+    for (size_t i = heap.size() / 2; i-- > 0;) sift_down(i);
+    while (!c->query_done && !heap.empty()) {
+        const int best = heap[0].file;
         Cursor& k = cur[(size_t)best];
         const int64_t i = k.i;
         m_seq.push_back(k.batch.seq_id[i]);
@@ -1016,11 +1300,28 @@ extern "C" int ngsep_call_population_bams(ngsep_ctx* c, const char* const* bam_p
         k.i++;
         if (k.i >= k.batch.n_reads) {
             // the merged batch references nothing of this reader's arrays any more (copied above)
+            const auto tr = std::chrono::steady_clock::now();
             rc = refill(k);
+            t_refill += secs(tr);
             if (rc != NGSEP_OK) { close_all(); return rc; }
         }
-        if (m_first.size() >= (1u << 18)) { rc = flush(); if (rc != NGSEP_OK) { close_all(); return rc; } }
+        if (k.done) {
+            heap[0] = heap.back();
+            heap.pop_back();
+        } else {
+            heap[0] = head_of(best);
+        }
+        if (!heap.empty()) sift_down(0);
+        if (m_first.size() >= (1u << 18)) {
+            const auto tf = std::chrono::steady_clock::now();
+            rc = flush();
+            t_flush += secs(tf);
+            if (rc != NGSEP_OK) { close_all(); return rc; }
+        }
     }
+    if (host_timing)
+        std::fprintf(stderr, "[ngsep host] population merge of %d files: %.3f s (refills %.3f s, admission of the merged batches %.3f s)\n",
+                     n_files, secs(tm0), t_refill, t_flush);
     rc = flush();
     close_all();
     if (rc != NGSEP_OK) return rc;

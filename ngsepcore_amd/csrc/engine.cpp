@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstring>
 #include <chrono>
+#include <mutex>
 #include <unordered_map>
 #include <cstdlib>
 #include <fstream>
@@ -24,6 +25,8 @@
 namespace ngsep {
 
 int set_error(ngsep_ctx* c, int code, const std::string& msg) {
+    static std::mutex mu;                        // readers of several files may fail on host threads at once
+    std::lock_guard<std::mutex> lk(mu);
     if (c) c->err = msg;
     return code;
 }
