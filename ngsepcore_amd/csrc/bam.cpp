@@ -802,6 +802,7 @@ static int for_each_batch(ngsep_ctx* c, ngsep_bam* b, F&& fn) {
 // decodes the file from its start, AlignmentsPileupGenerator.java:310-322, 342-354); reading stops once the
 // query region is done either way.
 int call_bam(ngsep_ctx* c, const char* bam_path, const char* out_vcf) {
+    start_device_init(c);
     ngsep_bam* b = nullptr;
     int rc = ngsep_bam_open(c, bam_path, &b);
     if (rc != NGSEP_OK) return rc;
@@ -1093,6 +1094,7 @@ int merge_whole_files(ngsep_ctx* c, std::vector<Cursor>& cur, int n_files) {
 extern "C" int ngsep_call_population_bams(ngsep_ctx* c, const char* const* bam_paths, int32_t n_files, const char* out_vcf_path) {
     if (!c || !bam_paths || n_files <= 0 || !out_vcf_path) return NGSEP_E_INVALID;
     if (!c->params.multisample) return set_error(c, NGSEP_E_INVALID, "ngsep_call_population_bams needs params.multisample = 1");
+    start_device_init(c);
     static const bool pop_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     auto tp = std::chrono::steady_clock::now();
     auto plap = [&](const char* what) {
@@ -1226,6 +1228,7 @@ extern "C" int ngsep_call_population_bams(ngsep_ctx* c, const char* const* bam_p
         m_cig_off.clear(); m_seq_off.clear(); m_hasq.clear(); m_bases.clear(); m_quals.clear();
         return r;
     };
+    if (std::getenv("NGSEP_POP_STREAM")) whole = false;     // diagnostics / tests: the streaming merge
     plap("open + whole-file reads");
     if (whole && !c->query_done) {
         rc = merge_whole_files(c, cur, n_files);

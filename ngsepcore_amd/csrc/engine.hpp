@@ -507,6 +507,12 @@ struct ngsep_ctx {
         int64_t windows = 0;                      // windows run (diagnostics)
     } stream;
     ngsep::Device* dev = nullptr;
+    // path B: the device is created on a thread of its own while the input is read (start_device_init), adopted
+    // by the first device step (ensure_device)
+    std::thread dev_init;
+    ngsep::Device* dev_init_result = nullptr;
+    std::string dev_init_err;
+    std::mutex dev_mu;
     // CoverageStatisticsCalculator mode (params.coverage_stats)
     ngsep::CovDevice* cov_dev = nullptr;
     bool cov_staged = false;
@@ -541,6 +547,8 @@ int prepare_pool(ngsep_ctx* c);
 int64_t java_round(double x);
 // kernels.hip
 Device* device_create(int ordinal, std::string& err);
+void start_device_init(ngsep_ctx* c);            // engine.cpp
+Device* ensure_device(ngsep_ctx* c, std::string& err);
 void device_destroy(Device* d);
 int device_upload(Device* d, const Staged& s, std::string& err);
 // runs the tile + posterior kernels and copies the position-ordered records into out->buf[out->n ...]

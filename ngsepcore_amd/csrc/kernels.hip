@@ -1855,6 +1855,9 @@ Device* device_create(int ordinal, std::string& err) {
         delete d;
         return nullptr;
     }
+    // the code object is loaded now (an empty launch), not inside the first run
+    hipLaunchKernelGGL(k_zero_i32, dim3(1), dim3(256), 0, d->stream, (int32_t*)nullptr, (int64_t)0);
+    (void)hipStreamSynchronize(d->stream);
     for (int k = 0; k < 2; k++) {
         d->slot[k].d_ctr = d->d_counters + 8 + 8 * k;          // sets 1 and 2 (0: the multisample run)
         if (hipHostMalloc(&d->slot[k].h_ctr, 8 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {

@@ -98,6 +98,15 @@ def test_population_bams_path_b(tmp_path):
     d.run(bams[::-1])                       # file order does not change the merge (ties: equal spans)
     diff = diff_vcf(o, d.outFilename)
     assert not diff, "\n".join(diff[:20])
+    # the streaming heap merge (files larger than one whole-file batch) == the parallel whole-file merge
+    os.environ["NGSEP_POP_STREAM"] = "1"
+    try:
+        d.setOutFilename(os.path.join(str(tmp_path), "gpu_b_stream.vcf"))
+        d.run(bams)
+    finally:
+        del os.environ["NGSEP_POP_STREAM"]
+    diff = diff_vcf(o, d.outFilename)
+    assert not diff, "\n".join(diff[:20])
     cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ngsepcore_amd", "lib", "ngsep-amd")
     out_cli = os.path.join(str(tmp_path), "cli.vcf")
     subprocess.run([cli, "MultisampleVariantsDetector", "-r", fa, "-o", out_cli] + bams, check=True)
