@@ -1769,14 +1769,12 @@ static int run_device_multi(ngsep_ctx* c, const LikTables& t, const GenotypePara
         c->pop_sites.push_back(o);
         src.push_back(i);
     }
-    // the sites' calls in output order (host threads: a few tens of MB per run)
+    // the sites' calls in output order: gathered on the device, copied straight into the (pinned) call store
+    (void)calls;
     const size_t cfrom = c->pop_calls.size();
     c->pop_calls.resize(cfrom + src.size() * S);
-    ngsep_sample_call* dst = c->pop_calls.data() + cfrom;
-    parallel_for((int64_t)src.size(), 64, [&](int64_t lo, int64_t hi) {
-        for (int64_t k = lo; k < hi; k++)
-            std::memcpy(dst + (size_t)k * S, calls + (size_t)src[(size_t)k] * S, S * sizeof(ngsep_sample_call));
-    });
+    if (device_fetch_calls_ordered(c->dev, src.data(), (int64_t)src.size(), c->pop_calls.data() + cfrom, err) != 0)
+        return set_error(c, NGSEP_E_DEVICE, err);
     c->stats.candidates = ncand;
     c->stats.hard_sites = (int32_t)device_last_hard(c->dev);
     c->stats.exact_bound_passes = device_last_exact(c->dev);

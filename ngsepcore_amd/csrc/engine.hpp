@@ -567,6 +567,7 @@ int64_t device_inflight(const Device* d);
 // multisample: scan over the candidate columns + population genotyping of the queued positions; the
 // sites (global positions, unordered) and their calls (n_samples per site) in the device's pinned
 // staging buffers, valid until the next run
+int device_fetch_calls_ordered(Device* d, const int64_t* src, int64_t m, ngsep_sample_call* dst, std::string& err);
 int device_run_multi(Device* d, const Staged& s, const LikTables& t, const GenotypeParams& g,
                      int32_t n_samples, double min_adf, int ploidy,
                      const ngsep_popsite_out** sites, const ngsep_sample_call** calls, int64_t* n_sites,

@@ -109,6 +109,11 @@ struct Device {
     int32_t n_samples = 0;
     ngsep_popsite_out* d_psites = nullptr;
     ngsep_sample_call* d_pcalls = nullptr;
+    ngsep_sample_call* d_pcalls_ord = nullptr;   // the kept sites' calls in output order (k_gather_calls)
+    int64_t cap_pcalls_ord = 0;                  // records
+    int64_t* d_csrc = nullptr;                   // staging index of each kept site, in output order
+    int64_t* h_csrc = nullptr;                   // (pinned)
+    int64_t cap_csrc = 0;
     int64_t cap_psites = 0;
     unsigned long long* d_stamps = nullptr;   // diagnostics (NGSEP_TIMING)
     void* d_rac = nullptr;           // RelativeAlleleCounts: histograms + per-block sums (device, pinned host)
@@ -1933,6 +1938,9 @@ void device_destroy(Device* d) {
     }
     (void)hipFree(d->d_psites);
     (void)hipFree(d->d_pcalls);
+    (void)hipFree(d->d_pcalls_ord);
+    (void)hipFree(d->d_csrc);
+    if (d->h_csrc) (void)hipHostFree(d->h_csrc);
     if (d->h_psites) (void)hipHostFree(d->h_psites);
     if (d->h_pcalls) (void)hipHostFree(d->h_pcalls);
     (void)hipFree(d->d_hard);
@@ -2497,12 +2505,12 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
         HIP_TRY(hipHostMalloc((void**)&d->h_pcalls, (size_t)d->cap_h_pcalls * sizeof(ngsep_sample_call), hipHostMallocDefault));
     }
     if (n) {
+        // the sites only: their calls come back in output order through device_fetch_calls_ordered
         HIP_TRY(hipMemcpyAsync(d->h_psites, d->d_psites, (size_t)n * sizeof(ngsep_popsite_out), hipMemcpyDeviceToHost, d->stream));
-        HIP_TRY(hipMemcpyAsync(d->h_pcalls, d->d_pcalls, (size_t)n * S * sizeof(ngsep_sample_call), hipMemcpyDeviceToHost, d->stream));
         HIP_TRY(hipStreamSynchronize(d->stream));
     }
     *sites = d->h_psites;
-    *calls = d->h_pcalls;
+    *calls = nullptr;
     *n_sites = n;
     d->last_n_sites = n;
     d->last_hard = (int64_t)d->h_counters[2];
@@ -2520,6 +2528,50 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     *geno_ms = a2;
     *total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     *n_candidates = d->mc_entries;          // candidate columns (sample, position) the scan bounded
+    return 0;
+}
+
+// the kept sites' per-sample calls gathered into output order (dwords: a record is 76 B)
+__global__ __launch_bounds__(256) void k_gather_calls(const uint32_t* __restrict__ calls, const int64_t* __restrict__ src,
+                                                      int64_t m, int64_t site_dw, uint32_t* __restrict__ out) {
+    const int64_t total = m * site_dw;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = i / site_dw, r = i - k * site_dw;
+        out[i] = calls[src[k] * site_dw + r];
+    }
+}
+
+// after device_run_multi: the calls of the m kept sites (staging indexes src, output order) gathered on the device
+// and copied straight into dst (pinned host memory of the context's call store) -- no host-side reordering copy
+int device_fetch_calls_ordered(Device* d, const int64_t* src, int64_t m, ngsep_sample_call* dst, std::string& err) {
+    if (m <= 0) return 0;
+    HIP_TRY(hipSetDevice(d->ordinal));
+    const int64_t S = d->n_samples;
+    static_assert(sizeof(ngsep_sample_call) % 4 == 0, "ngsep_sample_call is gathered in dwords");
+    if (m > d->cap_csrc) {
+        (void)hipFree(d->d_csrc);
+        if (d->h_csrc) (void)hipHostFree(d->h_csrc);
+        d->d_csrc = nullptr;
+        d->h_csrc = nullptr;
+        d->cap_csrc = std::max<int64_t>(m + m / 2, 4096);
+        HIP_TRY(hipMalloc(&d->d_csrc, (size_t)d->cap_csrc * sizeof(int64_t)));
+        HIP_TRY(hipHostMalloc((void**)&d->h_csrc, (size_t)d->cap_csrc * sizeof(int64_t), hipHostMallocDefault));
+    }
+    if (m * S > d->cap_pcalls_ord) {
+        (void)hipFree(d->d_pcalls_ord);
+        d->d_pcalls_ord = nullptr;
+        d->cap_pcalls_ord = std::max<int64_t>(m * S + m * S / 2, 4096 * S);
+        HIP_TRY(hipMalloc(&d->d_pcalls_ord, (size_t)d->cap_pcalls_ord * sizeof(ngsep_sample_call)));
+    }
+    std::memcpy(d->h_csrc, src, (size_t)m * sizeof(int64_t));
+    HIP_TRY(hipMemcpyAsync(d->d_csrc, d->h_csrc, (size_t)m * sizeof(int64_t), hipMemcpyHostToDevice, d->stream));
+    const int64_t site_dw = S * (int64_t)(sizeof(ngsep_sample_call) / 4);
+    const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((m * site_dw + 255) / 256, (int64_t)d->n_cu * 8));
+    hipLaunchKernelGGL(k_gather_calls, dim3((unsigned)nblk), dim3(256), 0, d->stream, (const uint32_t*)d->d_pcalls,
+                       (const int64_t*)d->d_csrc, m, site_dw, (uint32_t*)d->d_pcalls_ord);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(dst, d->d_pcalls_ord, (size_t)(m * S) * sizeof(ngsep_sample_call), hipMemcpyDeviceToHost, d->stream));
+    HIP_TRY(hipStreamSynchronize(d->stream));
     return 0;
 }
 
