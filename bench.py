@@ -469,9 +469,10 @@ def main():
     barrier()
     scan_ms, geno_ms = [], []
     t_start = time.perf_counter()
-    if len(sessions) == 1 and not multi:
-        # a stream of passes, two in flight: pass k+1's kernels run while pass k's records are copied back
-        # and collected (ngsep_submit_staged / ngsep_collect_staged); every pass is collected
+    if len(sessions) == 1:
+        # a stream of passes, two in flight: pass k+1's kernels run while pass k's records (multisample: its
+        # per-sample calls, gathered into position order) are copied back and collected
+        # (ngsep_submit_staged / ngsep_collect_staged); every pass is collected
         sess = sessions[0]
         sess.submit_staged()
         for k in range(args.steps):

@@ -1738,17 +1738,12 @@ static void apply_strand_bias(SiteStore& sites, size_t from) {
 
 // MultisampleVariantsDetector run: sites come back unordered with global positions; order them by
 // position and map them to (sequence, position) (the listener writes in pileup order, :534-535)
-static int run_device_multi(ngsep_ctx* c, const LikTables& t, const GenotypeParams& gp, double* elapsed_ms) {
-    const ngsep_popsite_out* sites = nullptr;
-    const ngsep_sample_call* calls = nullptr;
-    int64_t n = 0;
-    double scan_ms = 0, geno_ms = 0, total_ms = 0;
-    int64_t ncand = 0;
-    std::string err;
+// the emitted sites (unordered) of one pass into the context's result in position order; `fetch` brings their
+// calls back in that order into the call store
+template <class Fetch>
+static int order_population_sites(ngsep_ctx* c, const ngsep_popsite_out* sites, int64_t n, Fetch&& fetch) {
     const size_t S = c->sample_ids.size();
-    if (device_run_multi(c->dev, c->staged, t, gp, (int32_t)S, c->params.min_allele_depth_freq, c->params.ploidy,
-                         &sites, &calls, &n, &scan_ms, &geno_ms, &total_ms, &ncand, err) != 0)
-        return set_error(c, NGSEP_E_DEVICE, err);
+    std::string err;
     std::vector<int64_t> order((size_t)n);
     for (size_t i = 0; i < order.size(); i++) order[i] = (int64_t)i;
     std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return sites[a].pos < sites[b].pos; });
@@ -1770,15 +1765,32 @@ static int run_device_multi(ngsep_ctx* c, const LikTables& t, const GenotypePara
         src.push_back(i);
     }
     // the sites' calls in output order: gathered on the device, copied straight into the (pinned) call store
-    (void)calls;
     const size_t cfrom = c->pop_calls.size();
     c->pop_calls.resize(cfrom + src.size() * S);
-    if (device_fetch_calls_ordered(c->dev, src.data(), (int64_t)src.size(), c->pop_calls.data() + cfrom, err) != 0)
+    if (fetch(src.data(), (int64_t)src.size(), c->pop_calls.data() + cfrom, err) != 0)
         return set_error(c, NGSEP_E_DEVICE, err);
+    c->stats.sites_called += (int64_t)(c->pop_sites.size() - from);
+    return NGSEP_OK;
+}
+
+static int run_device_multi(ngsep_ctx* c, const LikTables& t, const GenotypeParams& gp, double* elapsed_ms) {
+    const ngsep_popsite_out* sites = nullptr;
+    const ngsep_sample_call* calls = nullptr;
+    int64_t n = 0;
+    double scan_ms = 0, geno_ms = 0, total_ms = 0;
+    int64_t ncand = 0;
+    std::string err;
+    const size_t S = c->sample_ids.size();
+    if (device_run_multi(c->dev, c->staged, t, gp, (int32_t)S, c->params.min_allele_depth_freq, c->params.ploidy,
+                         &sites, &calls, &n, &scan_ms, &geno_ms, &total_ms, &ncand, err) != 0)
+        return set_error(c, NGSEP_E_DEVICE, err);
+    const int rc = order_population_sites(c, sites, n, [&](const int64_t* src, int64_t m, ngsep_sample_call* dst, std::string& e) {
+        return device_fetch_calls_ordered(c->dev, src, m, dst, e);
+    });
+    if (rc != NGSEP_OK) return rc;
     c->stats.candidates = ncand;
     c->stats.hard_sites = (int32_t)device_last_hard(c->dev);
     c->stats.exact_bound_passes = device_last_exact(c->dev);
-    c->stats.sites_called += (int64_t)(c->pop_sites.size() - from);
     c->stats.kernel_ms = total_ms;
     c->stats.scan_ms = scan_ms;
     c->stats.genotype_ms = geno_ms;
@@ -2374,13 +2386,17 @@ extern "C" int ngsep_run_staged(ngsep_ctx* c, double* elapsed_ms) {
 extern "C" int ngsep_submit_staged(ngsep_ctx* c) {
     if (c && c->params.coverage_stats) return set_error(c, NGSEP_E_INVALID, "coverage runs are synchronous: ngsep_run_staged");
     if (!c || !c->dev) return set_error(c, NGSEP_E_INVALID, "nothing staged");
-    if (c->params.multisample) {            // population runs are synchronous: the result waits for collect
-        c->pop_sites.clear();
-        c->pop_calls.clear();
-        c->stats.sites_called = 0;
-        const int rc = run_device(c, nullptr);
-        if (rc == NGSEP_OK) c->pending_sync++;
-        return rc;
+    if (c->params.multisample) {
+        // population runs: kernels of one pass while the previous pass's calls are gathered and copied back
+        LikTables t;
+        GenotypeParams gp;
+        compute_tables(c, &t, &gp);
+        if (const int rc = prepare_pool(c)) return rc;
+        std::string err;
+        if (device_submit_multi(c->dev, t, gp, (int32_t)c->sample_ids.size(), c->params.min_allele_depth_freq,
+                                c->params.ploidy, err) != 0)
+            return set_error(c, NGSEP_E_DEVICE, err);
+        return NGSEP_OK;
     }
     if (device_inflight(c->dev) >= 2) return set_error(c, NGSEP_E_INVALID, "two staged runs already in flight: collect first");
     // the tables depend only on the options: computed once per option set
@@ -2403,8 +2419,29 @@ extern "C" int ngsep_submit_staged(ngsep_ctx* c) {
 extern "C" int ngsep_collect_staged(ngsep_ctx* c, double* elapsed_ms) {
     if (!c || !c->dev) return set_error(c, NGSEP_E_INVALID, "nothing staged");
     if (c->params.multisample) {
-        if (c->pending_sync <= 0) return set_error(c, NGSEP_E_INVALID, "no run to collect");
-        c->pending_sync--;
+        c->pop_sites.clear();
+        c->pop_calls.clear();
+        c->stats.sites_called = 0;
+        const ngsep_popsite_out* sites = nullptr;
+        int64_t n = 0, ncand = 0;
+        int slot = 0;
+        bool rerun = false;
+        double scan_ms = 0, geno_ms = 0;
+        std::string err;
+        const auto t0 = std::chrono::steady_clock::now();
+        if (device_collect_multi(c->dev, &sites, &n, &slot, &rerun, &scan_ms, &geno_ms, &ncand, err) != 0)
+            return set_error(c, NGSEP_E_DEVICE, err);
+        if (rerun) return run_device(c, elapsed_ms);    // a buffer overflowed: the pass again, synchronously (grows them)
+        const int rc = order_population_sites(c, sites, n, [&](const int64_t* src, int64_t m, ngsep_sample_call* dst, std::string& e) {
+            return device_fetch_calls_slot(c->dev, slot, src, m, dst, e);
+        });
+        if (rc != NGSEP_OK) return rc;
+        c->stats.candidates = ncand;
+        c->stats.hard_sites = (int32_t)device_last_hard(c->dev);
+        c->stats.exact_bound_passes = device_last_exact(c->dev);
+        c->stats.scan_ms = scan_ms;
+        c->stats.genotype_ms = geno_ms;
+        c->stats.kernel_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         if (elapsed_ms) *elapsed_ms = c->stats.kernel_ms;
         return NGSEP_OK;
     }

@@ -568,6 +568,12 @@ int64_t device_inflight(const Device* d);
 // sites (global positions, unordered) and their calls (n_samples per site) in the device's pinned
 // staging buffers, valid until the next run
 int device_fetch_calls_ordered(Device* d, const int64_t* src, int64_t m, ngsep_sample_call* dst, std::string& err);
+int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, int32_t n_samples, double min_adf,
+                        int ploidy, std::string& err);
+int device_collect_multi(Device* d, const ngsep_popsite_out** sites, int64_t* n_sites, int* slot, bool* rerun,
+                         double* scan_ms, double* geno_ms, int64_t* n_candidates, std::string& err);
+int device_fetch_calls_slot(Device* d, int slot, const int64_t* src, int64_t m, ngsep_sample_call* dst, std::string& err);
+int device_multi_inflight(const Device* d);
 int device_run_multi(Device* d, const Staged& s, const LikTables& t, const GenotypeParams& g,
                      int32_t n_samples, double min_adf, int ploidy,
                      const ngsep_popsite_out** sites, const ngsep_sample_call** calls, int64_t* n_sites,

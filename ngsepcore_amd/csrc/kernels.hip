@@ -71,8 +71,24 @@ struct RunSlot {                     // one in-flight single-sample run (see dev
     std::chrono::steady_clock::time_point t0;
 };
 
+struct MultiSlot {                   // one in-flight multisample run (device_submit_multi / device_collect_multi)
+    QueueSite* d_hard = nullptr;             // KQN -> KPM queue
+    int64_t cap_hard = 0;
+    uint32_t* d_need = nullptr;              // open positions (a bit per global position)
+    int64_t cap_need = 0;                    // words
+    ngsep_popsite_out* d_psites = nullptr;   // KPM's sites (unordered) and their per-sample calls
+    ngsep_sample_call* d_pcalls = nullptr;
+    int64_t cap_psites = 0;
+    ngsep_popsite_out* h_psites = nullptr;   // pinned D2H destination of the sites
+    int64_t cap_h_psites = 0, guess = 0;
+    hipEvent_t ev[5] = {};                   // KTM start, KQN end, KPM start, KPM end, copies done
+    bool busy = false;
+};
+
 struct Device {
     int ordinal = 0;
+    MultiSlot mslot[2];
+    int mnext = 0, mfirst = 0, minflight = 0;
     hipStream_t stream = nullptr;
     hipStream_t copy_stream = nullptr;
     RunSlot slot[2];
@@ -1939,6 +1955,11 @@ void device_destroy(Device* d) {
     (void)hipFree(d->d_psites);
     (void)hipFree(d->d_pcalls);
     (void)hipFree(d->d_pcalls_ord);
+    for (auto& m : d->mslot) {
+        (void)hipFree(m.d_hard); (void)hipFree(m.d_need); (void)hipFree(m.d_psites); (void)hipFree(m.d_pcalls);
+        if (m.h_psites) (void)hipHostFree(m.h_psites);
+        for (auto& e : m.ev) if (e) (void)hipEventDestroy(e);
+    }
     (void)hipFree(d->d_csrc);
     if (d->h_csrc) (void)hipHostFree(d->h_csrc);
     if (d->h_psites) (void)hipHostFree(d->h_psites);
@@ -2543,7 +2564,14 @@ __global__ __launch_bounds__(256) void k_gather_calls(const uint32_t* __restrict
 
 // after device_run_multi: the calls of the m kept sites (staging indexes src, output order) gathered on the device
 // and copied straight into dst (pinned host memory of the context's call store) -- no host-side reordering copy
+int device_fetch_calls_from(Device* d, const ngsep_sample_call* calls, hipStream_t stream, const int64_t* src, int64_t m,
+                            ngsep_sample_call* dst, std::string& err);
 int device_fetch_calls_ordered(Device* d, const int64_t* src, int64_t m, ngsep_sample_call* dst, std::string& err) {
+    return device_fetch_calls_from(d, d->d_pcalls, d->stream, src, m, dst, err);
+}
+
+int device_fetch_calls_from(Device* d, const ngsep_sample_call* calls, hipStream_t stream, const int64_t* src, int64_t m,
+                            ngsep_sample_call* dst, std::string& err) {
     if (m <= 0) return 0;
     HIP_TRY(hipSetDevice(d->ordinal));
     const int64_t S = d->n_samples;
@@ -2564,15 +2592,137 @@ int device_fetch_calls_ordered(Device* d, const int64_t* src, int64_t m, ngsep_s
         HIP_TRY(hipMalloc(&d->d_pcalls_ord, (size_t)d->cap_pcalls_ord * sizeof(ngsep_sample_call)));
     }
     std::memcpy(d->h_csrc, src, (size_t)m * sizeof(int64_t));
-    HIP_TRY(hipMemcpyAsync(d->d_csrc, d->h_csrc, (size_t)m * sizeof(int64_t), hipMemcpyHostToDevice, d->stream));
+    HIP_TRY(hipMemcpyAsync(d->d_csrc, d->h_csrc, (size_t)m * sizeof(int64_t), hipMemcpyHostToDevice, stream));
     const int64_t site_dw = S * (int64_t)(sizeof(ngsep_sample_call) / 4);
     const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((m * site_dw + 255) / 256, (int64_t)d->n_cu * 8));
-    hipLaunchKernelGGL(k_gather_calls, dim3((unsigned)nblk), dim3(256), 0, d->stream, (const uint32_t*)d->d_pcalls,
+    hipLaunchKernelGGL(k_gather_calls, dim3((unsigned)nblk), dim3(256), 0, stream, (const uint32_t*)calls,
                        (const int64_t*)d->d_csrc, m, site_dw, (uint32_t*)d->d_pcalls_ord);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(dst, d->d_pcalls_ord, (size_t)(m * S) * sizeof(ngsep_sample_call), hipMemcpyDeviceToHost, d->stream));
-    HIP_TRY(hipStreamSynchronize(d->stream));
+    HIP_TRY(hipMemcpyAsync(dst, d->d_pcalls_ord, (size_t)(m * S) * sizeof(ngsep_sample_call), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
     return 0;
 }
+
+// Asynchronous multisample runs: submit enqueues KTM + KQN + KPM of one pass into a slot of its own and the D2H of
+// its counters and (a guess of) its sites; collect waits for the oldest pass, and device_fetch_calls_from gathers
+// its calls on the copy stream, so the gather and the big D2H of one pass overlap the next pass's kernels.
+int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, int32_t n_samples, double min_adf,
+                        int ploidy, std::string& err) {
+    HIP_TRY(hipSetDevice(d->ordinal));
+    const int32_t S = d->n_samples;
+    if (S <= 0 || n_samples != S) { err = "multisample run without samples (ngsep_set_samples)"; return -1; }
+    if (S > kMaxSamplesDevice) { err = "too many samples for one device run"; return -1; }
+    if (ploidy >= 3 && !d->pool_valid) { err = "ploidy >= 3 without pool tables (device_set_pool)"; return -1; }
+    if (d->minflight >= 2) { err = "two staged runs already in flight: collect first"; return -1; }
+    MultiSlot& m = d->mslot[d->mnext];
+    // capacities from the synchronous run's counts (device_run_multi grows them); a pass that still overflows is
+    // rerun synchronously by the collect
+    const int64_t want = std::max<int64_t>(d->last_n_sites + d->last_n_sites / 4 + 1024, 4096);
+    if (want > m.cap_psites) {
+        (void)hipFree(m.d_psites);
+        (void)hipFree(m.d_pcalls);
+        m.d_psites = nullptr;
+        m.d_pcalls = nullptr;
+        HIP_TRY(hipMalloc(&m.d_psites, (size_t)want * sizeof(ngsep_popsite_out)));
+        HIP_TRY(hipMalloc(&m.d_pcalls, (size_t)want * S * sizeof(ngsep_sample_call)));
+        m.cap_psites = want;
+    }
+    if (want > m.cap_h_psites) {
+        if (m.h_psites) (void)hipHostFree(m.h_psites);
+        m.h_psites = nullptr;
+        HIP_TRY(hipHostMalloc((void**)&m.h_psites, (size_t)want * sizeof(ngsep_popsite_out), hipHostMallocDefault));
+        m.cap_h_psites = want;
+    }
+    const int64_t qwant = std::max<int64_t>(std::max<int64_t>(d->g_len / 64 + 65536, d->last_hard + 1024), 65536);
+    if (qwant > m.cap_hard) {
+        (void)hipFree(m.d_hard);
+        m.d_hard = nullptr;
+        HIP_TRY(hipMalloc(&m.d_hard, (size_t)qwant * sizeof(QueueSite)));
+        m.cap_hard = qwant;
+    }
+    const int64_t nwords = d->g_len / 32 + 1;
+    if (nwords > m.cap_need) {
+        (void)hipFree(m.d_need);
+        m.d_need = nullptr;
+        HIP_TRY(hipMalloc(&m.d_need, (size_t)nwords * sizeof(uint32_t)));
+        m.cap_need = nwords;
+    }
+    if (!m.ev[0])
+        for (int k = 0; k < 5; k++) HIP_TRY(hipEventCreateWithFlags(&m.ev[k], k < 4 ? hipEventDefault : hipEventDisableTiming));
+    if (!d->tables_valid || std::memcmp(&d->h_tables, &t, sizeof(LikTables)) != 0) {
+        HIP_TRY(hipStreamSynchronize(d->stream));     // an earlier upload may still read h_tables
+        d->h_tables = t;
+        HIP_TRY(hipMemcpyAsync(d->d_tables, &d->h_tables, sizeof(LikTables), hipMemcpyHostToDevice, d->stream));
+        d->tables_valid = true;
+    }
+    unsigned long long* ctr = d->slot[d->mnext].d_ctr;
+    HIP_TRY(hipMemsetAsync(ctr, 0, 4 * sizeof(unsigned long long), d->stream));
+    HIP_TRY(hipMemsetAsync(m.d_need, 0, (size_t)nwords * sizeof(uint32_t), d->stream));
+    const int64_t ngroups = (d->mc_entries + 63) / 64;
+    const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((ngroups + 3) / 4, (int64_t)d->n_cu * 8));
+    hipExtLaunchKernelGGL(k_scan_multi, dim3((unsigned)nblk), dim3(256), 0, d->stream, m.ev[0], nullptr, 0,
+                          (const int32_t*)d->d_mc_pos, (const uint8_t*)d->d_mc_n, (const int64_t*)d->d_mc_gbase,
+                          (const uint8_t*)d->d_pile, d->mc_entries, (const LikTables*)d->d_tables, g, m.d_need, ctr);
+    HIP_TRY(hipGetLastError());
+    const int64_t qblk = std::max<int64_t>(1, std::min<int64_t>((nwords + 255) / 256, (int64_t)d->n_cu * 4));
+    hipExtLaunchKernelGGL(k_queue_need, dim3((unsigned)qblk), dim3(256), 0, d->stream, nullptr, m.ev[1], 0,
+                          (const uint32_t*)m.d_need, (const uint8_t*)d->d_ref, nwords, m.d_hard, ctr, m.cap_hard);
+    HIP_TRY(hipGetLastError());
+    hipExtLaunchKernelGGL(k_posterior_multi, dim3(2048), dim3(kPopThreads), 0, d->stream, m.ev[2], m.ev[3], 0,
+                          (const QueueSite*)m.d_hard, (const unsigned long long*)(ctr + 2), m.cap_hard, (const uint8_t*)d->d_ppile,
+                          (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, (const LikTables*)d->d_tables, g,
+                          S, min_adf, ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), m.d_psites, m.d_pcalls,
+                          ctr, m.cap_psites, (unsigned long long*)nullptr);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(d->slot[d->mnext].h_ctr, ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, d->stream));
+    m.guess = std::min<int64_t>(m.cap_psites, d->last_n_sites + d->last_n_sites / 16 + 64);
+    HIP_TRY(hipMemcpyAsync(m.h_psites, m.d_psites, (size_t)m.guess * sizeof(ngsep_popsite_out), hipMemcpyDeviceToHost, d->stream));
+    HIP_TRY(hipEventRecord(m.ev[4], d->stream));
+    m.busy = true;
+    d->mnext ^= 1;
+    d->minflight++;
+    return 0;
+}
+
+// the oldest submitted multisample pass: its sites (unordered, pinned) and the slot holding its calls.  *rerun = true
+// when the pass overflowed a buffer (the caller reruns it synchronously through device_run_multi)
+int device_collect_multi(Device* d, const ngsep_popsite_out** sites, int64_t* n_sites, int* slot, bool* rerun,
+                         double* scan_ms, double* geno_ms, int64_t* n_candidates, std::string& err) {
+    if (d->minflight <= 0) { err = "no run to collect"; return -1; }
+    HIP_TRY(hipSetDevice(d->ordinal));
+    const int k = d->mfirst;
+    MultiSlot& m = d->mslot[k];
+    d->mfirst ^= 1;
+    d->minflight--;
+    m.busy = false;
+    HIP_TRY(hipEventSynchronize(m.ev[4]));
+    const unsigned long long* hc = d->slot[k].h_ctr;
+    const unsigned long long c3 = hc[3];
+    if (c3 >> 63) { err = "a position is covered by more reads than the population kernel holds (" + std::to_string(kPopListCap) + ")"; return -1; }
+    const int64_t n = (int64_t)hc[0];
+    *rerun = (int64_t)hc[2] > m.cap_hard || n > m.cap_psites;
+    *slot = k;
+    if (*rerun) return 0;
+    if (n > m.guess)
+        HIP_TRY(hipMemcpy(m.h_psites + m.guess, m.d_psites + m.guess, (size_t)(n - m.guess) * sizeof(ngsep_popsite_out), hipMemcpyDeviceToHost));
+    *sites = m.h_psites;
+    *n_sites = n;
+    d->last_n_sites = n;
+    d->last_hard = (int64_t)hc[2];
+    d->last_exact = (int64_t)(c3 & 0x7FFFFFFFFFFFFFFFull);
+    float a = 0, a2 = 0;
+    (void)hipEventElapsedTime(&a, m.ev[0], m.ev[1]);
+    (void)hipEventElapsedTime(&a2, m.ev[2], m.ev[3]);
+    *scan_ms = a;
+    *geno_ms = a2;
+    *n_candidates = d->mc_entries;
+    return 0;
+}
+
+int device_fetch_calls_slot(Device* d, int slot, const int64_t* src, int64_t m, ngsep_sample_call* dst, std::string& err) {
+    return device_fetch_calls_from(d, d->mslot[slot].d_pcalls, d->copy_stream, src, m, dst, err);
+}
+
+int device_multi_inflight(const Device* d) { return d->minflight; }
 
 }  // namespace ngsep

@@ -38,7 +38,15 @@ def gpu_mvd(tmp_path, syn, rgs, staged=False, **opts):
         s.set_samples(rgs)
         for name, seq in syn.contigs():
             s.set_reference(name, seq)
-        if staged:
+        if staged == "pipelined":
+            # two passes in flight (ngsep_submit_staged x2, then collect x2): the second pass's result is written
+            s.stage(syn.batch())
+            s.stage_finish()
+            s.submit_staged()
+            s.submit_staged()
+            s.collect_staged()
+            s.collect_staged()
+        elif staged:
             s.stage(syn.batch())
             s.stage_finish()
             s.run_staged()
@@ -81,6 +89,9 @@ def test_population_200_samples_staged(tmp_path):
     assert not d, "\n".join(d[:20])
     assert n_records(o) > 10
     assert st.hard_sites < st.positions_genotyped      # the per-sample bounds dropped positions
+    g2, _ = gpu_mvd(tmp_path, syn, rgs, staged="pipelined")
+    d = diff_vcf(o, g2)
+    assert not d, "\n".join(d[:20])
 
 
 def test_population_bams_path_b(tmp_path):
