@@ -1767,7 +1767,7 @@ static int order_population_sites(ngsep_ctx* c, const ngsep_popsite_out* sites, 
     // the sites' calls in output order: gathered on the device, copied straight into the (pinned) call store
     const size_t cfrom = c->pop_calls.size();
     c->pop_calls.resize(cfrom + src.size() * S);
-    if (fetch(src.data(), (int64_t)src.size(), c->pop_calls.data() + cfrom, err) != 0)
+    if (fetch(src.data(), (int64_t)src.size(), c->pop_calls.data() + cfrom, &c->pop_big, err) != 0)
         return set_error(c, NGSEP_E_DEVICE, err);
     c->stats.sites_called += (int64_t)(c->pop_sites.size() - from);
     return NGSEP_OK;
@@ -1784,8 +1784,9 @@ static int run_device_multi(ngsep_ctx* c, const LikTables& t, const GenotypePara
     if (device_run_multi(c->dev, c->staged, t, gp, (int32_t)S, c->params.min_allele_depth_freq, c->params.ploidy,
                          &sites, &calls, &n, &scan_ms, &geno_ms, &total_ms, &ncand, err) != 0)
         return set_error(c, NGSEP_E_DEVICE, err);
-    const int rc = order_population_sites(c, sites, n, [&](const int64_t* src, int64_t m, ngsep_sample_call* dst, std::string& e) {
-        return device_fetch_calls_ordered(c->dev, src, m, dst, e);
+    const int rc = order_population_sites(c, sites, n, [&](const int64_t* src, int64_t m, PopCall32* dst,
+                                                           PinnedStore<ngsep_sample_call>* big, std::string& e) {
+        return device_fetch_calls_ordered(c->dev, src, m, dst, big, e);
     });
     if (rc != NGSEP_OK) return rc;
     c->stats.candidates = ncand;
@@ -2376,6 +2377,7 @@ extern "C" int ngsep_run_staged(ngsep_ctx* c, double* elapsed_ms) {
     c->sites.clear();
     c->pop_sites.clear();
     c->pop_calls.clear();
+    c->pop_big.clear();
     c->stats.sites_called = 0;
     return run_device(c, elapsed_ms);
 }
@@ -2421,6 +2423,7 @@ extern "C" int ngsep_collect_staged(ngsep_ctx* c, double* elapsed_ms) {
     if (c->params.multisample) {
         c->pop_sites.clear();
         c->pop_calls.clear();
+        c->pop_big.clear();
         c->stats.sites_called = 0;
         const ngsep_popsite_out* sites = nullptr;
         int64_t n = 0, ncand = 0;
@@ -2432,8 +2435,9 @@ extern "C" int ngsep_collect_staged(ngsep_ctx* c, double* elapsed_ms) {
         if (device_collect_multi(c->dev, &sites, &n, &slot, &rerun, &scan_ms, &geno_ms, &ncand, err) != 0)
             return set_error(c, NGSEP_E_DEVICE, err);
         if (rerun) return run_device(c, elapsed_ms);    // a buffer overflowed: the pass again, synchronously (grows them)
-        const int rc = order_population_sites(c, sites, n, [&](const int64_t* src, int64_t m, ngsep_sample_call* dst, std::string& e) {
-            return device_fetch_calls_slot(c->dev, slot, src, m, dst, e);
+        const int rc = order_population_sites(c, sites, n, [&](const int64_t* src, int64_t m, PopCall32* dst,
+                                                               PinnedStore<ngsep_sample_call>* big, std::string& e) {
+            return device_fetch_calls_slot(c->dev, slot, src, m, dst, big, e);
         });
         if (rc != NGSEP_OK) return rc;
         c->stats.candidates = ncand;
@@ -2510,6 +2514,7 @@ extern "C" int ngsep_fetch_population_sites(ngsep_ctx* c, ngsep_popsite_out* sit
     const size_t S = c->sample_ids.size();
     const int64_t k = std::min<int64_t>(n, std::max<int64_t>(cap, 0));
     if (sites && k) std::memcpy(sites, c->pop_sites.data(), (size_t)k * sizeof(ngsep_popsite_out));
-    if (calls && k && S) std::memcpy(calls, c->pop_calls.data(), (size_t)k * S * sizeof(ngsep_sample_call));
+    if (calls && k && S)
+        for (size_t i = 0; i < (size_t)k * S; i++) calls[i] = expand_call(c->pop_calls.data()[i], c->pop_big.data());
     return NGSEP_OK;
 }

@@ -303,6 +303,35 @@ inline int site_tri(int i, int j) {   // index of L[i][j] in ngsep_site_out.logc
 
 // the called sites of a run or a whole detector: the records (pinned: the device copies into them) and the
 // whole records they point to
+// One sample's call at a population site as it comes back from the device and is kept (32 B instead of the
+// 76-B ngsep_sample_call): flags = kind | n_called << 1 | whole << 7, called = (c0 + 1) | (c1 + 1) << 4.  A call
+// a field of which does not fit (GQ > 255, DP / counts / PL > 65535, |ACN| > 127, more than six PL values) is
+// kept whole in pop_big, pl[0] | pl[1] << 16 its index.
+struct PopCall32 {
+    uint8_t flags, called, gq, pad0;
+    int16_t total_cn;
+    uint16_t dp;
+    uint16_t counts[4];
+    int8_t acn[4];
+    uint16_t pl[6];
+};
+static_assert(sizeof(PopCall32) == 32, "PopCall32 layout");
+
+inline ngsep_sample_call expand_call(const PopCall32& p, const ngsep_sample_call* big) {
+    if (p.flags & 0x80) return big[(size_t)p.pl[0] | ((size_t)p.pl[1] << 16)];
+    ngsep_sample_call o;
+    o.kind = (int8_t)(p.flags & 1);
+    o.n_called = (int8_t)((p.flags >> 1) & 3);
+    o.called[0] = (int8_t)((int)(p.called & 15) - 1);
+    o.called[1] = (int8_t)((int)(p.called >> 4) - 1);
+    o.gq = (int16_t)p.gq;
+    o.total_cn = p.total_cn;
+    o.dp = (int32_t)p.dp;
+    for (int k = 0; k < 4; k++) { o.counts[k] = (int32_t)p.counts[k]; o.acn[k] = (int16_t)p.acn[k]; }
+    for (int k = 0; k < 10; k++) o.pl[k] = k < 6 ? (int32_t)p.pl[k] : 0;
+    return o;
+}
+
 struct SiteSet {
     PinnedStore<SiteRec> rec;
     PinnedStore<ngsep_site_out> ext;
@@ -528,7 +557,8 @@ struct ngsep_ctx {
     std::vector<std::pair<int32_t, std::pair<int64_t, int64_t>>> carved;
     int pending_sync = 0;                         // multisample runs submitted, not yet collected
     std::vector<ngsep_popsite_out> pop_sites;     // (sequence, position) order
-    ngsep::PinnedStore<ngsep_sample_call> pop_calls;     // pop_sites.size() x n_samples
+    ngsep::PinnedStore<ngsep::PopCall32> pop_calls;     // pop_sites.size() x n_samples (compact; expand_call)
+    ngsep::PinnedStore<ngsep_sample_call> pop_big;      // the calls a PopCall32 cannot hold, whole
     ngsep_stats stats{};
 };
 
@@ -567,12 +597,14 @@ int64_t device_inflight(const Device* d);
 // multisample: scan over the candidate columns + population genotyping of the queued positions; the
 // sites (global positions, unordered) and their calls (n_samples per site) in the device's pinned
 // staging buffers, valid until the next run
-int device_fetch_calls_ordered(Device* d, const int64_t* src, int64_t m, ngsep_sample_call* dst, std::string& err);
+// the kept sites' calls gathered into output order and packed on the device (dst: m x S PopCall32; the calls that
+// do not fit are appended whole to big, the records index it from big->size())
+int device_fetch_calls_ordered(Device* d, const int64_t* src, int64_t m, PopCall32* dst, PinnedStore<ngsep_sample_call>* big, std::string& err);
 int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, int32_t n_samples, double min_adf,
                         int ploidy, std::string& err);
 int device_collect_multi(Device* d, const ngsep_popsite_out** sites, int64_t* n_sites, int* slot, bool* rerun,
                          double* scan_ms, double* geno_ms, int64_t* n_candidates, std::string& err);
-int device_fetch_calls_slot(Device* d, int slot, const int64_t* src, int64_t m, ngsep_sample_call* dst, std::string& err);
+int device_fetch_calls_slot(Device* d, int slot, const int64_t* src, int64_t m, PopCall32* dst, PinnedStore<ngsep_sample_call>* big, std::string& err);
 int device_multi_inflight(const Device* d);
 int device_run_multi(Device* d, const Staged& s, const LikTables& t, const GenotypeParams& g,
                      int32_t n_samples, double min_adf, int ploidy,

@@ -125,7 +125,8 @@ struct Device {
     int32_t n_samples = 0;
     ngsep_popsite_out* d_psites = nullptr;
     ngsep_sample_call* d_pcalls = nullptr;
-    ngsep_sample_call* d_pcalls_ord = nullptr;   // the kept sites' calls in output order (k_gather_calls)
+    PopCall32* d_pcalls_ord = nullptr;           // the kept sites' calls in output order, packed (k_gather_calls)
+    ngsep_sample_call* d_pbig = nullptr;         // the calls a PopCall32 cannot hold (+ their counter)
     int64_t cap_pcalls_ord = 0;                  // records
     int64_t* d_csrc = nullptr;                   // staging index of each kept site, in output order
     int64_t* h_csrc = nullptr;                   // (pinned)
@@ -1955,6 +1956,7 @@ void device_destroy(Device* d) {
     (void)hipFree(d->d_psites);
     (void)hipFree(d->d_pcalls);
     (void)hipFree(d->d_pcalls_ord);
+    (void)hipFree(d->d_pbig);
     for (auto& m : d->mslot) {
         (void)hipFree(m.d_hard); (void)hipFree(m.d_need); (void)hipFree(m.d_psites); (void)hipFree(m.d_pcalls);
         if (m.h_psites) (void)hipHostFree(m.h_psites);
@@ -2552,30 +2554,62 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     return 0;
 }
 
-// the kept sites' per-sample calls gathered into output order (dwords: a record is 76 B)
-__global__ __launch_bounds__(256) void k_gather_calls(const uint32_t* __restrict__ calls, const int64_t* __restrict__ src,
-                                                      int64_t m, int64_t site_dw, uint32_t* __restrict__ out) {
-    const int64_t total = m * site_dw;
+// the kept sites' per-sample calls gathered into output order and packed into PopCall32 (engine.hpp); a call a
+// field of which does not fit goes whole to big[], its record holding big_base + its index there
+__global__ __launch_bounds__(256) void k_gather_calls(const ngsep_sample_call* __restrict__ calls, const int64_t* __restrict__ src,
+                                                      int64_t m, int64_t S, PopCall32* __restrict__ out,
+                                                      ngsep_sample_call* __restrict__ big, unsigned long long* nbig,
+                                                      int64_t big_cap, int64_t big_base, int force_big) {
+    const int64_t total = m * S;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t k = i / site_dw, r = i - k * site_dw;
-        out[i] = calls[src[k] * site_dw + r];
+        const int64_t k = i / S, smp = i - k * S;
+        const ngsep_sample_call c = calls[src[k] * S + smp];
+        bool fit = c.kind >= 0 && c.kind <= 1 && c.n_called >= 0 && c.n_called <= 3 && c.called[0] >= -1 && c.called[0] <= 14 &&
+                   c.called[1] >= -1 && c.called[1] <= 14 && c.gq >= 0 && c.gq <= 255 && c.dp >= 0 && c.dp <= 65535;
+#pragma unroll
+        for (int t = 0; t < 4; t++) fit = fit && c.counts[t] >= 0 && c.counts[t] <= 65535 && c.acn[t] >= -128 && c.acn[t] <= 127;
+#pragma unroll
+        for (int t = 0; t < 10; t++) fit = fit && (t < 6 ? (c.pl[t] >= 0 && c.pl[t] <= 65535) : c.pl[t] == 0);
+        fit = fit && !force_big;
+        PopCall32 o;
+        if (fit) {
+            o.flags = (uint8_t)(c.kind | c.n_called << 1);
+            o.called = (uint8_t)((c.called[0] + 1) | (c.called[1] + 1) << 4);
+            o.gq = (uint8_t)c.gq;
+            o.pad0 = 0;
+            o.total_cn = c.total_cn;
+            o.dp = (uint16_t)c.dp;
+#pragma unroll
+            for (int t = 0; t < 4; t++) { o.counts[t] = (uint16_t)c.counts[t]; o.acn[t] = (int8_t)c.acn[t]; }
+#pragma unroll
+            for (int t = 0; t < 6; t++) o.pl[t] = (uint16_t)c.pl[t];
+        } else {
+            const unsigned long long b = atomicAdd(nbig, 1ull);
+            if ((int64_t)b < big_cap) big[b] = c;
+            const unsigned long long gi = (unsigned long long)big_base + b;
+            o = PopCall32{};
+            o.flags = 0x80;
+            o.pl[0] = (uint16_t)(gi & 0xFFFFu);
+            o.pl[1] = (uint16_t)(gi >> 16);
+        }
+        out[i] = o;
     }
 }
 
-// after device_run_multi: the calls of the m kept sites (staging indexes src, output order) gathered on the device
-// and copied straight into dst (pinned host memory of the context's call store) -- no host-side reordering copy
+// after device_run_multi: the calls of the m kept sites (staging indexes src, output order) gathered and packed on
+// the device and copied straight into dst (pinned host memory of the context's call store); the calls that do not
+// fit a PopCall32 are appended whole to big
 int device_fetch_calls_from(Device* d, const ngsep_sample_call* calls, hipStream_t stream, const int64_t* src, int64_t m,
-                            ngsep_sample_call* dst, std::string& err);
-int device_fetch_calls_ordered(Device* d, const int64_t* src, int64_t m, ngsep_sample_call* dst, std::string& err) {
-    return device_fetch_calls_from(d, d->d_pcalls, d->stream, src, m, dst, err);
+                            PopCall32* dst, PinnedStore<ngsep_sample_call>* big, std::string& err);
+int device_fetch_calls_ordered(Device* d, const int64_t* src, int64_t m, PopCall32* dst, PinnedStore<ngsep_sample_call>* big, std::string& err) {
+    return device_fetch_calls_from(d, d->d_pcalls, d->stream, src, m, dst, big, err);
 }
 
 int device_fetch_calls_from(Device* d, const ngsep_sample_call* calls, hipStream_t stream, const int64_t* src, int64_t m,
-                            ngsep_sample_call* dst, std::string& err) {
+                            PopCall32* dst, PinnedStore<ngsep_sample_call>* big, std::string& err) {
     if (m <= 0) return 0;
     HIP_TRY(hipSetDevice(d->ordinal));
     const int64_t S = d->n_samples;
-    static_assert(sizeof(ngsep_sample_call) % 4 == 0, "ngsep_sample_call is gathered in dwords");
     if (m > d->cap_csrc) {
         (void)hipFree(d->d_csrc);
         if (d->h_csrc) (void)hipHostFree(d->h_csrc);
@@ -2583,23 +2617,37 @@ int device_fetch_calls_from(Device* d, const ngsep_sample_call* calls, hipStream
         d->h_csrc = nullptr;
         d->cap_csrc = std::max<int64_t>(m + m / 2, 4096);
         HIP_TRY(hipMalloc(&d->d_csrc, (size_t)d->cap_csrc * sizeof(int64_t)));
-        HIP_TRY(hipHostMalloc((void**)&d->h_csrc, (size_t)d->cap_csrc * sizeof(int64_t), hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc((void**)&d->h_csrc, (size_t)(d->cap_csrc + 1) * sizeof(int64_t), hipHostMallocDefault));
     }
     if (m * S > d->cap_pcalls_ord) {
         (void)hipFree(d->d_pcalls_ord);
+        (void)hipFree(d->d_pbig);
         d->d_pcalls_ord = nullptr;
+        d->d_pbig = nullptr;
         d->cap_pcalls_ord = std::max<int64_t>(m * S + m * S / 2, 4096 * S);
-        HIP_TRY(hipMalloc(&d->d_pcalls_ord, (size_t)d->cap_pcalls_ord * sizeof(ngsep_sample_call)));
+        HIP_TRY(hipMalloc(&d->d_pcalls_ord, (size_t)d->cap_pcalls_ord * sizeof(PopCall32)));
+        HIP_TRY(hipMalloc(&d->d_pbig, (size_t)d->cap_pcalls_ord * sizeof(ngsep_sample_call) + 8));
     }
+    // the big-record counter sits after the records
+    unsigned long long* d_nbig = reinterpret_cast<unsigned long long*>(d->d_pbig + d->cap_pcalls_ord);
     std::memcpy(d->h_csrc, src, (size_t)m * sizeof(int64_t));
     HIP_TRY(hipMemcpyAsync(d->d_csrc, d->h_csrc, (size_t)m * sizeof(int64_t), hipMemcpyHostToDevice, stream));
-    const int64_t site_dw = S * (int64_t)(sizeof(ngsep_sample_call) / 4);
-    const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((m * site_dw + 255) / 256, (int64_t)d->n_cu * 8));
-    hipLaunchKernelGGL(k_gather_calls, dim3((unsigned)nblk), dim3(256), 0, stream, (const uint32_t*)calls,
-                       (const int64_t*)d->d_csrc, m, site_dw, (uint32_t*)d->d_pcalls_ord);
+    HIP_TRY(hipMemsetAsync(d_nbig, 0, sizeof(unsigned long long), stream));
+    const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((m * S + 255) / 256, (int64_t)d->n_cu * 8));
+    hipLaunchKernelGGL(k_gather_calls, dim3((unsigned)nblk), dim3(256), 0, stream, calls, (const int64_t*)d->d_csrc, m, S,
+                       d->d_pcalls_ord, d->d_pbig, d_nbig, d->cap_pcalls_ord, (int64_t)big->size(),
+                       std::getenv("NGSEP_POP_ALL_BIG") ? 1 : 0);   // (tests: every call through the whole-record list)
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(dst, d->d_pcalls_ord, (size_t)(m * S) * sizeof(ngsep_sample_call), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(dst, d->d_pcalls_ord, (size_t)(m * S) * sizeof(PopCall32), hipMemcpyDeviceToHost, stream));
+    unsigned long long* h_nbig = reinterpret_cast<unsigned long long*>(d->h_csrc + d->cap_csrc);
+    HIP_TRY(hipMemcpyAsync(h_nbig, d_nbig, sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
+    const int64_t nb = (int64_t)*h_nbig;
+    if (nb > 0) {
+        const size_t b0 = big->size();
+        big->resize(b0 + (size_t)nb);
+        HIP_TRY(hipMemcpy(big->data() + b0, d->d_pbig, (size_t)nb * sizeof(ngsep_sample_call), hipMemcpyDeviceToHost));
+    }
     return 0;
 }
 
@@ -2719,8 +2767,9 @@ int device_collect_multi(Device* d, const ngsep_popsite_out** sites, int64_t* n_
     return 0;
 }
 
-int device_fetch_calls_slot(Device* d, int slot, const int64_t* src, int64_t m, ngsep_sample_call* dst, std::string& err) {
-    return device_fetch_calls_from(d, d->mslot[slot].d_pcalls, d->copy_stream, src, m, dst, err);
+int device_fetch_calls_slot(Device* d, int slot, const int64_t* src, int64_t m, PopCall32* dst, PinnedStore<ngsep_sample_call>* big,
+                            std::string& err) {
+    return device_fetch_calls_from(d, d->mslot[slot].d_pcalls, d->copy_stream, src, m, dst, big, err);
 }
 
 int device_multi_inflight(const Device* d) { return d->minflight; }

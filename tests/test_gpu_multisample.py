@@ -92,6 +92,14 @@ def test_population_200_samples_staged(tmp_path):
     g2, _ = gpu_mvd(tmp_path, syn, rgs, staged="pipelined")
     d = diff_vcf(o, g2)
     assert not d, "\n".join(d[:20])
+    # every per-sample call through the whole-record list instead of the packed 32-B record
+    os.environ["NGSEP_POP_ALL_BIG"] = "1"
+    try:
+        g3, _ = gpu_mvd(tmp_path, syn, rgs, staged="pipelined")
+    finally:
+        del os.environ["NGSEP_POP_ALL_BIG"]
+    d = diff_vcf(o, g3)
+    assert not d, "\n".join(d[:20])
 
 
 def test_population_bams_path_b(tmp_path):
