@@ -465,7 +465,12 @@ def main():
 
     for _ in range(args.warmup):
         for s in sessions:
-            s.run_staged()
+            if len(sessions) == 1:
+                # the timed loop's own path (two result slots, pinned stores): its buffers reach their size here
+                s.submit_staged()
+                s.collect_staged()
+            else:
+                s.run_staged()
     barrier()
     scan_ms, geno_ms = [], []
     t_start = time.perf_counter()

@@ -1764,11 +1764,9 @@ static int order_population_sites(ngsep_ctx* c, const ngsep_popsite_out* sites, 
         c->pop_sites.push_back(o);
         src.push_back(i);
     }
-    // the sites' calls in output order: gathered on the device, copied straight into the (pinned) call store
-    const size_t cfrom = c->pop_calls.size();
-    c->pop_calls.resize(cfrom + src.size() * S);
-    if (fetch(src.data(), (int64_t)src.size(), c->pop_calls.data() + cfrom, &c->pop_big, err) != 0)
-        return set_error(c, NGSEP_E_DEVICE, err);
+    // the sites' calls: fetch puts them into the call store and sets the sites' pop_order entries
+    (void)S;
+    if (fetch(src.data(), (int64_t)src.size(), err) != 0) return set_error(c, NGSEP_E_DEVICE, err);
     c->stats.sites_called += (int64_t)(c->pop_sites.size() - from);
     return NGSEP_OK;
 }
@@ -1784,9 +1782,12 @@ static int run_device_multi(ngsep_ctx* c, const LikTables& t, const GenotypePara
     if (device_run_multi(c->dev, c->staged, t, gp, (int32_t)S, c->params.min_allele_depth_freq, c->params.ploidy,
                          &sites, &calls, &n, &scan_ms, &geno_ms, &total_ms, &ncand, err) != 0)
         return set_error(c, NGSEP_E_DEVICE, err);
-    const int rc = order_population_sites(c, sites, n, [&](const int64_t* src, int64_t m, PopCall32* dst,
-                                                           PinnedStore<ngsep_sample_call>* big, std::string& e) {
-        return device_fetch_calls_ordered(c->dev, src, m, dst, big, e);
+    const int rc = order_population_sites(c, sites, n, [&](const int64_t* src, int64_t m, std::string& e) {
+        // gathered into output order on the device, copied straight into the (pinned) call store
+        const size_t cfrom = c->pop_calls.size(), blk0 = cfrom / S;
+        c->pop_calls.resize(cfrom + (size_t)m * S);
+        for (int64_t k = 0; k < m; k++) c->pop_order.push_back((int64_t)blk0 + k);
+        return device_fetch_calls_ordered(c->dev, src, m, c->pop_calls.data() + cfrom, &c->pop_big, e);
     });
     if (rc != NGSEP_OK) return rc;
     c->stats.candidates = ncand;
@@ -2378,6 +2379,7 @@ extern "C" int ngsep_run_staged(ngsep_ctx* c, double* elapsed_ms) {
     c->pop_sites.clear();
     c->pop_calls.clear();
     c->pop_big.clear();
+    c->pop_order.clear();
     c->stats.sites_called = 0;
     return run_device(c, elapsed_ms);
 }
@@ -2389,10 +2391,17 @@ extern "C" int ngsep_submit_staged(ngsep_ctx* c) {
     if (c && c->params.coverage_stats) return set_error(c, NGSEP_E_INVALID, "coverage runs are synchronous: ngsep_run_staged");
     if (!c || !c->dev) return set_error(c, NGSEP_E_INVALID, "nothing staged");
     if (c->params.multisample) {
-        // population runs: kernels of one pass while the previous pass's calls are gathered and copied back
-        LikTables t;
-        GenotypeParams gp;
-        compute_tables(c, &t, &gp);
+        // population runs: kernels of one pass while the previous pass's calls are gathered and copied back; the
+        // tables depend only on the options (computed once per option set)
+        if (!c->tables_cached || std::memcmp(&c->tables_params, &c->params, sizeof(ngsep_params)) != 0 ||
+            c->tables_het != c->het_rate) {
+            compute_tables(c, &c->tables_t, &c->tables_gp);
+            c->tables_params = c->params;
+            c->tables_het = c->het_rate;
+            c->tables_cached = true;
+        }
+        const LikTables& t = c->tables_t;
+        const GenotypeParams& gp = c->tables_gp;
         if (const int rc = prepare_pool(c)) return rc;
         std::string err;
         if (device_submit_multi(c->dev, t, gp, (int32_t)c->sample_ids.size(), c->params.min_allele_depth_freq,
@@ -2424,6 +2433,7 @@ extern "C" int ngsep_collect_staged(ngsep_ctx* c, double* elapsed_ms) {
         c->pop_sites.clear();
         c->pop_calls.clear();
         c->pop_big.clear();
+        c->pop_order.clear();
         c->stats.sites_called = 0;
         const ngsep_popsite_out* sites = nullptr;
         int64_t n = 0, ncand = 0;
@@ -2435,9 +2445,13 @@ extern "C" int ngsep_collect_staged(ngsep_ctx* c, double* elapsed_ms) {
         if (device_collect_multi(c->dev, &sites, &n, &slot, &rerun, &scan_ms, &geno_ms, &ncand, err) != 0)
             return set_error(c, NGSEP_E_DEVICE, err);
         if (rerun) return run_device(c, elapsed_ms);    // a buffer overflowed: the pass again, synchronously (grows them)
-        const int rc = order_population_sites(c, sites, n, [&](const int64_t* src, int64_t m, PopCall32* dst,
-                                                               PinnedStore<ngsep_sample_call>* big, std::string& e) {
-            return device_fetch_calls_slot(c->dev, slot, src, m, dst, big, e);
+        const auto t1 = std::chrono::steady_clock::now();
+        // the slot's calls came back packed in KPM's site order: its buffers become the call store (swapped, not
+        // copied) and pop_order maps the ordered sites to their blocks
+        const int rc = order_population_sites(c, sites, n, [&](const int64_t* src, int64_t m, std::string&) {
+            device_slot_take(c->dev, slot, n, c->pop_calls, c->pop_big);
+            c->pop_order.assign(src, src + m);
+            return 0;
         });
         if (rc != NGSEP_OK) return rc;
         c->stats.candidates = ncand;
@@ -2447,6 +2461,18 @@ extern "C" int ngsep_collect_staged(ngsep_ctx* c, double* elapsed_ms) {
         c->stats.genotype_ms = geno_ms;
         c->stats.kernel_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         if (elapsed_ms) *elapsed_ms = c->stats.kernel_ms;
+        static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+        if (host_timing) {
+            static double acc_w = 0, acc_f = 0;
+            static int cnt = 0;
+            acc_w += std::chrono::duration<double, std::micro>(t1 - t0).count();
+            acc_f += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count();
+            if (++cnt == 8) {
+                std::fprintf(stderr, "[ngsep host] population collect: wait %.1f us, order + gather + D2H %.1f us (avg of 8)\n", acc_w / 8, acc_f / 8);
+                acc_w = acc_f = 0;
+                cnt = 0;
+            }
+        }
         return NGSEP_OK;
     }
     c->sites.clear();
@@ -2515,6 +2541,8 @@ extern "C" int ngsep_fetch_population_sites(ngsep_ctx* c, ngsep_popsite_out* sit
     const int64_t k = std::min<int64_t>(n, std::max<int64_t>(cap, 0));
     if (sites && k) std::memcpy(sites, c->pop_sites.data(), (size_t)k * sizeof(ngsep_popsite_out));
     if (calls && k && S)
-        for (size_t i = 0; i < (size_t)k * S; i++) calls[i] = expand_call(c->pop_calls.data()[i], c->pop_big.data());
+        for (size_t i = 0; i < (size_t)k; i++)
+            for (size_t j = 0; j < S; j++)
+                calls[i * S + j] = expand_call(c->pop_calls.data()[(size_t)c->pop_order[i] * S + j], c->pop_big.data());
     return NGSEP_OK;
 }

@@ -559,6 +559,7 @@ struct ngsep_ctx {
     std::vector<ngsep_popsite_out> pop_sites;     // (sequence, position) order
     ngsep::PinnedStore<ngsep::PopCall32> pop_calls;     // pop_sites.size() x n_samples (compact; expand_call)
     ngsep::PinnedStore<ngsep_sample_call> pop_big;      // the calls a PopCall32 cannot hold, whole
+    std::vector<int64_t> pop_order;                     // site i's calls: pop_calls[pop_order[i] * n_samples ..]
     ngsep_stats stats{};
 };
 
@@ -604,7 +605,9 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
                         int ploidy, std::string& err);
 int device_collect_multi(Device* d, const ngsep_popsite_out** sites, int64_t* n_sites, int* slot, bool* rerun,
                          double* scan_ms, double* geno_ms, int64_t* n_candidates, std::string& err);
-int device_fetch_calls_slot(Device* d, int slot, const int64_t* src, int64_t m, PopCall32* dst, PinnedStore<ngsep_sample_call>* big, std::string& err);
+// the collected slot's packed calls (KPM's site order) and whole records handed over to the context's stores (the
+// buffers are swapped, nothing is copied)
+void device_slot_take(Device* d, int slot, int64_t n_sites, PinnedStore<PopCall32>& calls, PinnedStore<ngsep_sample_call>& big);
 int device_multi_inflight(const Device* d);
 int device_run_multi(Device* d, const Staged& s, const LikTables& t, const GenotypeParams& g,
                      int32_t n_samples, double min_adf, int ploidy,

@@ -81,8 +81,14 @@ struct MultiSlot {                   // one in-flight multisample run (device_su
     int64_t cap_psites = 0;
     ngsep_popsite_out* h_psites = nullptr;   // pinned D2H destination of the sites
     int64_t cap_h_psites = 0, guess = 0;
-    hipEvent_t ev[5] = {};                   // KTM start, KQN end, KPM start, KPM end, copies done
+    hipEvent_t ev[6] = {};                   // KTM start, KQN end, (unused), KPM end, copies done, calls packed
     bool busy = false;
+    PopCall32* d_pack = nullptr;             // KPM's calls packed in KPM's (unordered) site order
+    PinnedStore<PopCall32> h_pack;           // pinned D2H destination (handed to the context at collect)
+    ngsep_sample_call* d_big = nullptr;      // the calls a PopCall32 cannot hold
+    PinnedStore<ngsep_sample_call> h_big;
+    int64_t cap_pack = 0;                    // sites
+    int64_t guess_big = 0, cap_big = 0;
 };
 
 struct Device {
@@ -1960,6 +1966,7 @@ void device_destroy(Device* d) {
     for (auto& m : d->mslot) {
         (void)hipFree(m.d_hard); (void)hipFree(m.d_need); (void)hipFree(m.d_psites); (void)hipFree(m.d_pcalls);
         if (m.h_psites) (void)hipHostFree(m.h_psites);
+        (void)hipFree(m.d_pack); (void)hipFree(m.d_big);
         for (auto& e : m.ev) if (e) (void)hipEventDestroy(e);
     }
     (void)hipFree(d->d_csrc);
@@ -2494,7 +2501,9 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
         HIP_TRY(hipGetLastError());
     }
     if (ploidy >= 3 && !d->pool_valid) { err = "ploidy >= 3 without pool tables (device_set_pool)"; return -1; }
-    hipExtLaunchKernelGGL(k_posterior_multi, dim3(2048), dim3(kPopThreads), 0, d->stream, d->ev[3], d->ev[2], 0,
+    // (no start event on KPM: a start event between KQN and KPM was measured to idle the device; KPM's time is
+    // taken from KQN's end)
+    hipExtLaunchKernelGGL(k_posterior_multi, dim3(2048), dim3(kPopThreads), 0, d->stream, nullptr, d->ev[2], 0,
                           (const QueueSite*)d->d_hard, (const unsigned long long*)(ctr + 2), d->cap_hard, (const uint8_t*)d->d_ppile,
                           (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, (const LikTables*)d->d_tables, g,
                           S, min_adf, ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), d->d_psites, d->d_pcalls,
@@ -2546,7 +2555,7 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     }
     float a = 0, a2 = 0;
     (void)hipEventElapsedTime(&a, d->ev[0], d->ev[1]);
-    (void)hipEventElapsedTime(&a2, d->ev[3], d->ev[2]);
+    (void)hipEventElapsedTime(&a2, d->ev[1], d->ev[2]);
     *scan_ms = a;
     *geno_ms = a2;
     *total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -2651,6 +2660,48 @@ int device_fetch_calls_from(Device* d, const ngsep_sample_call* calls, hipStream
     return 0;
 }
 
+// KPM's calls packed in place of order (no site permutation: the host orders the packed records), the emitted
+// site count read from the device counter; the calls that do not fit go whole to big[] (index = their slot there)
+__global__ __launch_bounds__(256) void k_pack_calls(const ngsep_sample_call* __restrict__ calls, const unsigned long long* nsites,
+                                                    int64_t cap_sites, int64_t S, PopCall32* __restrict__ out,
+                                                    ngsep_sample_call* __restrict__ big, unsigned long long* nbig, int64_t big_cap,
+                                                    int force_big) {
+    int64_t n = (int64_t)*nsites;
+    if (n > cap_sites) n = cap_sites;
+    const int64_t total = n * S;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const ngsep_sample_call c = calls[i];
+        bool fit = c.kind >= 0 && c.kind <= 1 && c.n_called >= 0 && c.n_called <= 3 && c.called[0] >= -1 && c.called[0] <= 14 &&
+                   c.called[1] >= -1 && c.called[1] <= 14 && c.gq >= 0 && c.gq <= 255 && c.dp >= 0 && c.dp <= 65535;
+#pragma unroll
+        for (int t = 0; t < 4; t++) fit = fit && c.counts[t] >= 0 && c.counts[t] <= 65535 && c.acn[t] >= -128 && c.acn[t] <= 127;
+#pragma unroll
+        for (int t = 0; t < 10; t++) fit = fit && (t < 6 ? (c.pl[t] >= 0 && c.pl[t] <= 65535) : c.pl[t] == 0);
+        fit = fit && !force_big;
+        PopCall32 o;
+        if (fit) {
+            o.flags = (uint8_t)(c.kind | c.n_called << 1);
+            o.called = (uint8_t)((c.called[0] + 1) | (c.called[1] + 1) << 4);
+            o.gq = (uint8_t)c.gq;
+            o.pad0 = 0;
+            o.total_cn = c.total_cn;
+            o.dp = (uint16_t)c.dp;
+#pragma unroll
+            for (int t = 0; t < 4; t++) { o.counts[t] = (uint16_t)c.counts[t]; o.acn[t] = (int8_t)c.acn[t]; }
+#pragma unroll
+            for (int t = 0; t < 6; t++) o.pl[t] = (uint16_t)c.pl[t];
+        } else {
+            const unsigned long long b = atomicAdd(nbig, 1ull);
+            if ((int64_t)b < big_cap) big[b] = c;
+            o = PopCall32{};
+            o.flags = 0x80;
+            o.pl[0] = (uint16_t)(b & 0xFFFFu);
+            o.pl[1] = (uint16_t)(b >> 16);
+        }
+        out[i] = o;
+    }
+}
+
 // Asynchronous multisample runs: submit enqueues KTM + KQN + KPM of one pass into a slot of its own and the D2H of
 // its counters and (a guess of) its sites; collect waits for the oldest pass, and device_fetch_calls_from gathers
 // its calls on the copy stream, so the gather and the big D2H of one pass overlap the next pass's kernels.
@@ -2716,16 +2767,47 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
     hipExtLaunchKernelGGL(k_queue_need, dim3((unsigned)qblk), dim3(256), 0, d->stream, nullptr, m.ev[1], 0,
                           (const uint32_t*)m.d_need, (const uint8_t*)d->d_ref, nwords, m.d_hard, ctr, m.cap_hard);
     HIP_TRY(hipGetLastError());
-    hipExtLaunchKernelGGL(k_posterior_multi, dim3(2048), dim3(kPopThreads), 0, d->stream, m.ev[2], m.ev[3], 0,
+    hipExtLaunchKernelGGL(k_posterior_multi, dim3(2048), dim3(kPopThreads), 0, d->stream, nullptr, m.ev[3], 0,
                           (const QueueSite*)m.d_hard, (const unsigned long long*)(ctr + 2), m.cap_hard, (const uint8_t*)d->d_ppile,
                           (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, (const LikTables*)d->d_tables, g,
                           S, min_adf, ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), m.d_psites, m.d_pcalls,
                           ctr, m.cap_psites, (unsigned long long*)nullptr);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(d->slot[d->mnext].h_ctr, ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, d->stream));
+    // the calls packed right behind KPM on the compute stream; the copies (counters, a guess of the sites, their
+    // packed calls and whole records) on the copy stream, so the next pass's kernels do not wait for them
+    if (m.cap_pack < m.cap_psites) {
+        (void)hipFree(m.d_pack);
+        (void)hipFree(m.d_big);
+        m.d_pack = nullptr;
+        m.d_big = nullptr;
+        HIP_TRY(hipMalloc(&m.d_pack, (size_t)m.cap_psites * S * sizeof(PopCall32)));
+        m.cap_big = std::max<int64_t>(4096, m.cap_psites * S / 8);
+        HIP_TRY(hipMalloc(&m.d_big, (size_t)m.cap_big * sizeof(ngsep_sample_call)));
+        m.cap_pack = m.cap_psites;
+    }
+    // (stores handed back by the context keep their capacity: no reallocation once warm)
+    m.h_pack.clear();
+    m.h_pack.reserve((size_t)(m.cap_psites * S));
+    m.h_big.clear();
+    m.h_big.reserve((size_t)m.cap_big);
+    if (!m.ev[5]) HIP_TRY(hipEventCreateWithFlags(&m.ev[5], hipEventDisableTiming));
+    unsigned long long* d_nbig = ctr + 5;
+    HIP_TRY(hipMemsetAsync(d_nbig, 0, sizeof(unsigned long long), d->stream));
+    const int64_t pblk = std::max<int64_t>(1, std::min<int64_t>((m.cap_psites * S + 255) / 256, (int64_t)d->n_cu * 8));
+    hipLaunchKernelGGL(k_pack_calls, dim3((unsigned)pblk), dim3(256), 0, d->stream, (const ngsep_sample_call*)m.d_pcalls,
+                       (const unsigned long long*)ctr, m.cap_psites, (int64_t)S, m.d_pack, m.d_big, d_nbig, m.cap_big,
+                       std::getenv("NGSEP_POP_ALL_BIG") ? 1 : 0);   // (tests: every call through the whole-record list)
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(m.ev[5], d->stream));
+    HIP_TRY(hipStreamWaitEvent(d->copy_stream, m.ev[5], 0));
+    hipStream_t cs = d->copy_stream;
+    HIP_TRY(hipMemcpyAsync(d->slot[d->mnext].h_ctr, ctr, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, cs));
     m.guess = std::min<int64_t>(m.cap_psites, d->last_n_sites + d->last_n_sites / 16 + 64);
-    HIP_TRY(hipMemcpyAsync(m.h_psites, m.d_psites, (size_t)m.guess * sizeof(ngsep_popsite_out), hipMemcpyDeviceToHost, d->stream));
-    HIP_TRY(hipEventRecord(m.ev[4], d->stream));
+    HIP_TRY(hipMemcpyAsync(m.h_psites, m.d_psites, (size_t)m.guess * sizeof(ngsep_popsite_out), hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemcpyAsync(m.h_pack.data(), m.d_pack, (size_t)(m.guess * S) * sizeof(PopCall32), hipMemcpyDeviceToHost, cs));
+    m.guess_big = std::min<int64_t>(m.cap_big, 4096);
+    HIP_TRY(hipMemcpyAsync(m.h_big.data(), m.d_big, (size_t)m.guess_big * sizeof(ngsep_sample_call), hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipEventRecord(m.ev[4], cs));
     m.busy = true;
     d->mnext ^= 1;
     d->minflight++;
@@ -2748,11 +2830,17 @@ int device_collect_multi(Device* d, const ngsep_popsite_out** sites, int64_t* n_
     const unsigned long long c3 = hc[3];
     if (c3 >> 63) { err = "a position is covered by more reads than the population kernel holds (" + std::to_string(kPopListCap) + ")"; return -1; }
     const int64_t n = (int64_t)hc[0];
-    *rerun = (int64_t)hc[2] > m.cap_hard || n > m.cap_psites;
+    *rerun = (int64_t)hc[2] > m.cap_hard || n > m.cap_psites || (int64_t)hc[5] > m.cap_big;
     *slot = k;
     if (*rerun) return 0;
-    if (n > m.guess)
+    const int64_t S = d->n_samples;
+    if (n > m.guess) {
         HIP_TRY(hipMemcpy(m.h_psites + m.guess, m.d_psites + m.guess, (size_t)(n - m.guess) * sizeof(ngsep_popsite_out), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(m.h_pack.data() + m.guess * S, m.d_pack + m.guess * S, (size_t)((n - m.guess) * S) * sizeof(PopCall32), hipMemcpyDeviceToHost));
+    }
+    const int64_t nb = (int64_t)hc[5];
+    if (nb > m.guess_big)
+        HIP_TRY(hipMemcpy(m.h_big.data() + m.guess_big, m.d_big + m.guess_big, (size_t)(nb - m.guess_big) * sizeof(ngsep_sample_call), hipMemcpyDeviceToHost));
     *sites = m.h_psites;
     *n_sites = n;
     d->last_n_sites = n;
@@ -2760,16 +2848,19 @@ int device_collect_multi(Device* d, const ngsep_popsite_out** sites, int64_t* n_
     d->last_exact = (int64_t)(c3 & 0x7FFFFFFFFFFFFFFFull);
     float a = 0, a2 = 0;
     (void)hipEventElapsedTime(&a, m.ev[0], m.ev[1]);
-    (void)hipEventElapsedTime(&a2, m.ev[2], m.ev[3]);
+    (void)hipEventElapsedTime(&a2, m.ev[1], m.ev[3]);
     *scan_ms = a;
     *geno_ms = a2;
     *n_candidates = d->mc_entries;
     return 0;
 }
 
-int device_fetch_calls_slot(Device* d, int slot, const int64_t* src, int64_t m, PopCall32* dst, PinnedStore<ngsep_sample_call>* big,
-                            std::string& err) {
-    return device_fetch_calls_from(d, d->mslot[slot].d_pcalls, d->copy_stream, src, m, dst, big, err);
+void device_slot_take(Device* d, int slot, int64_t n_sites, PinnedStore<PopCall32>& calls, PinnedStore<ngsep_sample_call>& big) {
+    MultiSlot& m = d->mslot[slot];
+    m.h_pack.n = (size_t)(n_sites * d->n_samples);
+    m.h_big.n = (size_t)d->slot[slot].h_ctr[5];
+    calls.swap(m.h_pack);
+    big.swap(m.h_big);
 }
 
 int device_multi_inflight(const Device* d) { return d->minflight; }

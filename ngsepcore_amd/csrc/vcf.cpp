@@ -308,7 +308,7 @@ extern "C" int ngsep_write_population_vcf(ngsep_ctx* c, const char* path) {
     const size_t S = c->sample_ids.size();
     std::vector<ngsep_sample_call> calls(S);
     for (size_t i = 0; i < c->pop_sites.size(); i++) {
-        for (size_t k = 0; k < S; k++) calls[k] = expand_call(c->pop_calls.data()[i * S + k], c->pop_big.data());
+        for (size_t k = 0; k < S; k++) calls[k] = expand_call(c->pop_calls.data()[(size_t)c->pop_order[i] * S + k], c->pop_big.data());
         format_population_site(c, c->pop_sites[i], calls.data(), buf);
         if (buf.size() > (1 << 20)) { std::fwrite(buf.data(), 1, buf.size(), f); buf.clear(); }
     }
