@@ -531,6 +531,34 @@ def main():
             e2e = {"value": None, "error": str(e)}
         finally:
             shutil.rmtree(e2e_src[0], ignore_errors=True)
+    elif args.config == "wgs" and rank == 0 and world == 1 and not args.no_e2e:
+        # configs[3] shard end to end: each of the shard's sequences as a BAM on local disk (written untimed), then
+        # BAM -> VCF through ngsep_call_bam; wall times and positions summed over the shard
+        try:
+            tot_wall = tot_pos = tot_bytes = tot_rec = 0
+            for _, k in sources:
+                tmp = tempfile.mkdtemp(prefix="ngsep_e2e_")
+                try:
+                    syn = pysynth.Synth(genome=pysynth.HUMAN, depth=args.depth, seed=4, contig_first=k, n_contigs=1,
+                                        rng_per_contig=1)
+                    fa, bam = os.path.join(tmp, "c.fa"), os.path.join(tmp, "c.bam")
+                    pysynth.lib().ngs_synth_write_fasta(syn.h, fa.encode())
+                    pysynth.lib().ngs_synth_write_bam(syn.h, bam.encode())
+                    syn.close()
+                    r = end_to_end(fa, bam, local_rank)
+                    log(f"[rank 0] end-to-end {human[k][0]}: {r['wall_s']:.2f}s, {r['value']:.4g} positions/s")
+                    tot_wall += r["wall_s"]
+                    tot_pos += r["positions"]
+                    tot_bytes += r["bam_bytes"]
+                    tot_rec += r["vcf_records"]
+                finally:
+                    shutil.rmtree(tmp, ignore_errors=True)
+            e2e = {"wall_s": tot_wall, "positions": tot_pos, "value": tot_pos / tot_wall, "unit": "positions/s",
+                   "vcf_records": tot_rec, "bam_bytes": tot_bytes,
+                   "note": "ngsep_call_bam per sequence of the shard: BAM on disk -> VCF on disk incl. FASTA load, "
+                           f"summed; host threads {os.environ.get('NGSEP_THREADS') or cpu_cores()}"}
+        except Exception as e:
+            e2e = {"value": None, "error": str(e)}
 
     if dist is not None:
         import torch
