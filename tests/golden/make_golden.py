@@ -47,6 +47,11 @@ FULL_CASES = {
     "configs2_chr20_30x": dict(genome=1, contig_first=19, n_contigs=1, depth=30, seed=3, rng_per_contig=1),
     "configs3_wgs_chr21_30x": dict(genome=1, contig_first=20, n_contigs=1, depth=30, seed=4, rng_per_contig=1),
 }
+# configs[4] at full size for one GPU's shard: MultisampleVariantsDetector on 200 synthetic yeast samples at 10x,
+# chrIV (the bench's --config multisample workload); the oracle's population VCF md5 + record count
+FULL_POP_CASES = {
+    "configs4_chrIV_200x10x": dict(genome=0, depth=10.0, seed=5, n_samples=200, contig_first=3, n_contigs=1),
+}
 # CoverageStats (CoverageStatisticsCalculator) fixtures: synth case -> (min_mq, max_coverage)
 COVERAGE_CASES = {"edge_2contigs_25x": (20, 300), "c1_chrI_10x": (20, 12)}
 DUMP_CASE = ("dump_custom8k_30x", dict(genome=2, custom_len=8000, depth=30, seed=5, noqual_rate=0.01,
@@ -176,7 +181,39 @@ def full_size_fixtures(names=None):
     json.dump(out, open(path, "w"), indent=1, sort_keys=True)
 
 
+def full_size_population_fixtures(names=None):
+    """oracle population VCF md5 + record count of the full-size multisample shard (tests/golden/full_sizes_pop.json)"""
+    import json
+    import time
+    import ngsep_oracle
+    import pysynth
+    path = os.path.join(HERE, "full_sizes_pop.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
+    with tempfile.TemporaryDirectory(dir=os.environ.get("NGSEP_GOLDEN_TMP")) as d:
+        for name, skw in FULL_POP_CASES.items():
+            if names and name not in names:
+                continue
+            t = time.time()
+            syn = pysynth.Synth(**skw)
+            fa, sam, _ = syn.write(os.path.join(d, name))
+            syn.close()
+            vcf = os.path.join(d, name + ".vcf")
+            st = ngsep_oracle.run_mvd(fa, sam, vcf, 0.0)
+            n = sum(1 for l in open(vcf) if not l.startswith("#"))
+            out[name] = {"synth": skw, "sam_md5": md5(sam), "vcf_md5": md5(vcf), "vcf_records": n,
+                         "positions_genotyped": st.positions_genotyped, "oracle_seconds": round(st.seconds, 1)}
+            with gzip.GzipFile(os.path.join(HERE, name + ".vcf.gz"), "wb", mtime=0) as g:
+                g.write(open(vcf, "rb").read())
+            print(name, out[name], f"{time.time() - t:.0f}s", flush=True)
+            for f in os.listdir(d):
+                os.remove(os.path.join(d, f))
+    json.dump(out, open(path, "w"), indent=1, sort_keys=True)
+
+
 if __name__ == "__main__":
+    if "--full-pop" in sys.argv:
+        full_size_population_fixtures([a for a in sys.argv[2:] if not a.startswith("-")] or None)
+        sys.exit(0)
     if "--full" in sys.argv:
         full_size_fixtures([a for a in sys.argv[2:] if not a.startswith("-")] or None)
         sys.exit(0)
