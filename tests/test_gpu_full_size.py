@@ -66,3 +66,55 @@ def test_full_size_vcf_identical(tmp_path, name):
         s.write_vcf(out2)
     syn.close()
     assert _md5(out2) == case["vcf_md5"], _first_diff(out2, name)
+
+
+POP_JSON = os.path.join(GOLDEN, "full_sizes_pop.json")
+POP_CASES = json.load(open(POP_JSON)) if os.path.exists(POP_JSON) else {}
+
+
+def _first_diff_pop(got_path, name):
+    want = gzip.open(os.path.join(GOLDEN, name + ".vcf.gz"), "rt").read().splitlines()
+    got = open(got_path).read().splitlines()
+    for k, (a, b) in enumerate(zip(want, got)):
+        if a != b:
+            return f"line {k + 1}: oracle {a[:300]!r} != gpu {b[:300]!r}"
+    return f"line counts {len(want)} vs {len(got)}"
+
+
+@pytest.mark.parametrize("name", sorted(POP_CASES))
+def test_full_size_population_vcf_identical(tmp_path, name):
+    """configs[4] at one GPU's full shard (200 samples x 10x, chrIV): the population VCF of
+    MultisampleVariantsDetector path B (200 sample BAMs) and of the bench's pipelined staged path equal the
+    oracle's byte for byte."""
+    from ngsepcore_amd import MultisampleVariantsDetector, default_params
+    case = POP_CASES[name]
+    syn = pysynth.Synth(**case["synth"])
+    d = str(tmp_path)
+    fa = os.path.join(d, "g.fa")
+    pysynth.lib().ngs_synth_write_fasta(syn.h, fa.encode())
+    bams = syn.write_sample_bams(os.path.join(d, "pop"))
+    mvd = MultisampleVariantsDetector()
+    mvd.setGenome(fa)
+    mvd.setOutFilename(os.path.join(d, "b.vcf"))
+    mvd.run(bams).close()
+    assert _md5(mvd.outFilename) == case["vcf_md5"], _first_diff_pop(mvd.outFilename, name)
+    for b in bams:
+        os.remove(b)
+    # the bench's path: staged population, two passes in flight
+    p = default_params()
+    p.multisample = 1
+    out2 = os.path.join(d, "a.vcf")
+    n = max(1, syn.params.n_samples)
+    with GpuPileupSession(p) as s:
+        s.set_samples([(f"S{k:03d}", f"S{k:03d}") for k in range(n)])
+        for nm, q in syn.contigs():
+            s.set_reference(nm, q)
+        s.stage(syn.batch())
+        s.stage_finish()
+        s.submit_staged()
+        s.submit_staged()
+        s.collect_staged()
+        s.collect_staged()
+        s.write_population_vcf(out2)
+    syn.close()
+    assert _md5(out2) == case["vcf_md5"], _first_diff_pop(out2, name)
