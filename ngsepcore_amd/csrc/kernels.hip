@@ -2861,6 +2861,12 @@ void device_slot_take(Device* d, int slot, int64_t n_sites, PinnedStore<PopCall3
     m.h_big.n = (size_t)d->slot[slot].h_ctr[5];
     calls.swap(m.h_pack);
     big.swap(m.h_big);
+    // the slot keeps what the context handed back, grown here (on the collect that makes the swap) rather than in
+    // a later submit: from the second collect on, no pinned allocation happens in the pipeline
+    m.h_pack.clear();
+    m.h_pack.reserve((size_t)(m.cap_psites * d->n_samples));
+    m.h_big.clear();
+    m.h_big.reserve((size_t)m.cap_big);
 }
 
 int device_multi_inflight(const Device* d) { return d->minflight; }
