@@ -46,7 +46,7 @@ static int main_mvd(int argc, char** argv, int i) {
     ngsep_params p;
     ngsep_params_default(&p);
     p.multisample = 1;
-    const char *ref = nullptr, *outp = "variants.vcf";
+    const char *ref = nullptr, *outp = "variants.vcf", *known = nullptr;
     int device = 0;
     std::vector<const char*> bams;
     for (; i < argc; i++) {
@@ -68,6 +68,7 @@ static int main_mvd(int argc, char** argv, int i) {
         else if (takes("-first")) p.query_first = std::atoi(v);
         else if (takes("-last")) p.query_last = std::atoi(v);
         else if (takes("-device")) device = std::atoi(v);
+        else if (takes("-knownVariants")) known = v;    // MultisampleVariantsDetector.setKnownVariantsFile (:193-195)
         else if (!std::strcmp(a, "-psp")) p.print_sample_ploidy = 1;
         else if (!std::strcmp(a, "-p")) p.process_nonunique = 1;
         else if (!std::strcmp(a, "-s")) p.process_secondary = 1;
@@ -82,6 +83,7 @@ static int main_mvd(int argc, char** argv, int i) {
     ngsep_ctx* c = nullptr;
     int rc = ngsep_open(device, &p, &c);
     if (rc == NGSEP_OK) rc = ngsep_load_fasta(c, ref);
+    if (rc == NGSEP_OK && known) rc = ngsep_set_known_variants(c, known);
     if (rc == NGSEP_OK) rc = ngsep_call_population_bams(c, bams.data(), (int32_t)bams.size(), outp);
     if (rc != NGSEP_OK) { std::fprintf(stderr, "error %d: %s\n", rc, c ? ngsep_last_error(c) : "open failed"); if (c) ngsep_close(c); return 1; }
     ngsep_stats st;

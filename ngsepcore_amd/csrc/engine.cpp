@@ -1542,6 +1542,29 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
         s.n_slots = nslots;
         s.n_read_bases = nbases;
         s.n_samples = (int32_t)c->sample_ids.size();
+        if (!c->known.empty()) {
+            // -knownVariants (MultisampleVariantsDetector.onPileup :539-551): the input variants at positions with
+            // a pileup (a read with first <= p <= last), in input order; queue code 0x80 | ref << 5 | alt << 8 | 0x400
+            for (size_t wi = 0; wi < s.windows.size(); wi++) {
+                const Window& w = s.windows[wi];
+                const ContigReads& cr = contigs[wr[wi].contig];
+                const int64_t goff = w.gbase + w.pad - w.w0;
+                const int64_t w1 = (int64_t)w.w0 + w.wlen - 1;
+                const int64_t kb = c->known_seq_begin[(size_t)cr.seq_id], ke = c->known_seq_begin[(size_t)cr.seq_id + 1];
+                auto it = std::lower_bound(c->known.begin() + kb, c->known.begin() + ke, (int64_t)w.w0,
+                                           [](const ngsep_ctx::KnownVar& v, int64_t p) { return v.pos < p; });
+                size_t r = 0;
+                int64_t maxlast = INT64_MIN;
+                for (; it != c->known.begin() + ke && it->pos <= w1; ++it) {
+                    const int64_t p = it->pos;
+                    while (r < cr.first.size() && cr.first[r] <= p) { maxlast = std::max<int64_t>(maxlast, cr.last[r]); r++; }
+                    if (maxlast < p) continue;                                    // no pileup here
+                    s.h_forced.push_back((int32_t)(p + goff));
+                    s.h_forced.push_back(0x80 | (it->ref << 5) | (it->alt << 8) | 0x400);
+                }
+            }
+            s.known = true;
+        }
         const int lr = build_multi_layout(s);
         if (lr == -2) return set_error(c, NGSEP_E_DEVICE, "host memory for the population pile could not be allocated");
         if (lr != 0) return set_error(c, NGSEP_E_UNSUPPORTED, "a sample's pileup is deeper than 65535 alignments");
@@ -1746,7 +1769,11 @@ static int order_population_sites(ngsep_ctx* c, const ngsep_popsite_out* sites, 
     std::string err;
     std::vector<int64_t> order((size_t)n);
     for (size_t i = 0; i < order.size(); i++) order[i] = (int64_t)i;
-    std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return sites[a].pos < sites[b].pos; });
+    // position order; KPM leaves each site's queue index in seq_id, so sites of one position (input variants
+    // of -knownVariants) keep the queue's (input) order
+    std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+        return sites[a].pos != sites[b].pos ? sites[a].pos < sites[b].pos : sites[a].seq_id < sites[b].seq_id;
+    });
     const std::vector<Window>& ws = c->staged.windows;
     size_t wi = 0;
     const size_t from = c->pop_sites.size();
@@ -2171,8 +2198,8 @@ extern "C" int ngsep_set_known_variants(ngsep_ctx* c, const char* vcf_path) {
     c->known_seq_begin.clear();
     if (!vcf_path || !vcf_path[0]) return NGSEP_OK;
     if (c->seq_names.empty()) return set_error(c, NGSEP_E_INVALID, "load the reference before the known variants");
-    if (c->params.multisample || c->params.coverage_stats || c->params.relative_allele_counts)
-        return set_error(c, NGSEP_E_INVALID, "known variants are genotyped by the single-sample detector only");
+    if (c->params.coverage_stats || c->params.relative_allele_counts)
+        return set_error(c, NGSEP_E_INVALID, "known variants are genotyped by the variant detectors only");
     std::FILE* f = std::fopen(vcf_path, "r");
     if (!f) return set_error(c, NGSEP_E_IO, std::string("cannot read ") + vcf_path);
     std::unordered_map<std::string, int32_t> idx;
@@ -2232,15 +2259,17 @@ extern "C" int ngsep_set_known_variants(ngsep_ctx* c, const char* vcf_path) {
 // the input variant of a -knownVariants record: its ID (nullptr for '.').  Records are written in order, and at
 // one position in the input order (stream_collect), so a record is the first input variant of its position and
 // ALT that no earlier record there took.
-const char* ngsep::known_id(const ngsep_ctx* c, const ngsep_site_out& s) {
-    if (c->known.empty() || s.seq_id < 0 || (size_t)s.seq_id + 1 >= c->known_seq_begin.size()) return nullptr;
+const char* ngsep::known_id(const ngsep_ctx* c, const ngsep_site_out& s) { return known_id_at(c, s.seq_id, s.pos, site_alt(s)); }
+
+const char* ngsep::known_id_at(const ngsep_ctx* c, int32_t seq_id, int32_t pos, int alt) {
+    if (c->known.empty() || seq_id < 0 || (size_t)seq_id + 1 >= c->known_seq_begin.size()) return nullptr;
     auto& st = c->vcf_known;
-    if (st.seq != s.seq_id || st.pos != s.pos) { st.seq = s.seq_id; st.pos = s.pos; st.taken.clear(); }
-    const int64_t kb = c->known_seq_begin[(size_t)s.seq_id], ke = c->known_seq_begin[(size_t)s.seq_id + 1];
-    auto it = std::lower_bound(c->known.begin() + kb, c->known.begin() + ke, (int64_t)s.pos,
+    if (st.seq != seq_id || st.pos != pos) { st.seq = seq_id; st.pos = pos; st.taken.clear(); }
+    const int64_t kb = c->known_seq_begin[(size_t)seq_id], ke = c->known_seq_begin[(size_t)seq_id + 1];
+    auto it = std::lower_bound(c->known.begin() + kb, c->known.begin() + ke, (int64_t)pos,
                                [](const ngsep_ctx::KnownVar& v, int64_t p) { return v.pos < p; });
-    for (int64_t k = it - c->known.begin(); k < ke && c->known[(size_t)k].pos == s.pos; k++)
-        if (c->known[(size_t)k].alt == site_alt(s) && std::find(st.taken.begin(), st.taken.end(), k) == st.taken.end()) {
+    for (int64_t k = it - c->known.begin(); k < ke && c->known[(size_t)k].pos == pos; k++)
+        if (c->known[(size_t)k].alt == alt && std::find(st.taken.begin(), st.taken.end(), k) == st.taken.end()) {
             st.taken.push_back(k);
             return c->known[(size_t)k].id.empty() ? nullptr : c->known[(size_t)k].id.c_str();
         }

@@ -632,6 +632,7 @@ int coverage_stage(ngsep_ctx* c, std::vector<ContigReads>& contigs);
 int coverage_run(ngsep_ctx* c, double* kernel_ms);
 // engine.cpp: the ID of a -knownVariants record's input variant (nullptr: '.')
 const char* known_id(const ngsep_ctx* c, const ngsep_site_out& s);
+const char* known_id_at(const ngsep_ctx* c, int32_t seq_id, int32_t pos, int alt);
 // vcf.cpp
 std::string format_header(const ngsep_ctx* c);
 int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& out);

@@ -131,6 +131,9 @@ struct Device {
     int32_t n_samples = 0;
     ngsep_popsite_out* d_psites = nullptr;
     ngsep_sample_call* d_pcalls = nullptr;
+    QueueSite* d_mforced = nullptr;              // multisample -knownVariants: the input variants to genotype (KPM's queue)
+    unsigned long long* d_mforced_ctr = nullptr; //   [2] = their count (KPM's queue length)
+    int64_t n_mforced = -1;                      //   -1: discovery (KTM + KQN build the queue)
     PopCall32* d_pcalls_ord = nullptr;           // the kept sites' calls in output order, packed (k_gather_calls)
     ngsep_sample_call* d_pbig = nullptr;         // the calls a PopCall32 cannot hold (+ their counter)
     int64_t cap_pcalls_ord = 0;                  // records
@@ -1587,7 +1590,10 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
         if (tid == n_samples) { total = 0; cnt[0] = cnt[1] = cnt[2] = cnt[3] = 0; }
         __syncthreads();
         if (i == blockIdx.x) stamp(2);
-        if (s_tot == 0) continue;                                 // createSNVVariantPool: totalCount 0
+        // -knownVariants (MultisampleVariantsDetector.onPileup :539-551): the input variant's own alleles, every
+        // sample genotyped (genotypeVariant :674-693) and the record written whatever its QS
+        const bool known = (rc & 0x400u) != 0;
+        if (s_tot == 0 && !known) continue;                       // createSNVVariantPool: totalCount 0
         if (gp.ablate & 64) continue;                             // diagnostics: tallies only
         // 4. candidate alleles from the pooled counts (createSNVVariantPool)
         if (!(rc & 0x80u)) continue;                               // N (or masked) reference: no variant
@@ -1598,8 +1604,13 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
         if (minCount < 1) minCount = 1;
         int idx[4] = {refIdx, 0, 0, 0};
         int nal = 1;
-        for (int a = 0; a < 4; a++)
-            if (a != refIdx && pc[a] >= minCount) { idx[nal < 4 ? nal : 3] = a; nal++; }
+        if (known) {
+            idx[1] = (int)((rc >> 8) & 3u);
+            nal = 2;
+        } else {
+            for (int a = 0; a < 4; a++)
+                if (a != refIdx && pc[a] >= minCount) { idx[nal < 4 ? nal : 3] = a; nal++; }
+        }
         if (nal < 2) continue;
         int multisnv = nal > 2;
         // 5. genotype every sample; shrink a multi-allelic variant to the called alleles
@@ -1645,7 +1656,7 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
         }
         if (i == blockIdx.x) stamp(5);
         if (nal < 2) continue;                                     // only the reference allele is left
-        if (qsv == 0 || qsv < gp.min_quality) continue;            // MultisampleVariantsDetector.java:534
+        if (!known && (qsv == 0 || qsv < gp.min_quality)) continue;   // MultisampleVariantsDetector.java:534
         // 6. emit the site and its calls
         __syncthreads();
         if (tid == 0) s_base = atomicAdd(&counters[0], 1ull);
@@ -1654,7 +1665,7 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
         if ((int64_t)at >= cap) continue;
         if (tid == 0) {
             ngsep_popsite_out o;
-            o.seq_id = -1; o.pos = gpos; o.n_alleles = (int8_t)nal;
+            o.seq_id = (int32_t)i; o.pos = gpos; o.n_alleles = (int8_t)nal;   // (seq_id: the queue index, host order)
             for (int k = 0; k < 4; k++) o.alleles[k] = (int8_t)(k < nal ? idx[k] : -1);
             o.multisnv_type = (int8_t)multisnv; o.qual = (int16_t)qsv; o.pad = 0;
             sites[at] = o;
@@ -1921,6 +1932,9 @@ void device_release(Device* d) {
     (void)hipFree(d->d_mc_n); d->d_mc_n = nullptr;
     (void)hipFree(d->d_mc_gbase); d->d_mc_gbase = nullptr;
     (void)hipFree(d->d_need); d->d_need = nullptr;
+    (void)hipFree(d->d_mforced); d->d_mforced = nullptr;
+    (void)hipFree(d->d_mforced_ctr); d->d_mforced_ctr = nullptr;
+    d->n_mforced = -1;
     (void)hipFree(d->d_ppile); d->d_ppile = nullptr;
     (void)hipFree(d->d_prow); d->d_prow = nullptr;
     (void)hipFree(d->d_pboff); d->d_pboff = nullptr;
@@ -1962,6 +1976,8 @@ void device_destroy(Device* d) {
     (void)hipFree(d->d_psites);
     (void)hipFree(d->d_pcalls);
     (void)hipFree(d->d_pcalls_ord);
+    (void)hipFree(d->d_mforced);
+    (void)hipFree(d->d_mforced_ctr);
     (void)hipFree(d->d_pbig);
     for (auto& m : d->mslot) {
         (void)hipFree(m.d_hard); (void)hipFree(m.d_need); (void)hipFree(m.d_psites); (void)hipFree(m.d_pcalls);
@@ -2025,6 +2041,16 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
         HIP_TRY(hipMalloc(&d->d_ppile, (size_t)s.ppile_bytes + 64));
         HIP_TRY(hipMalloc(&d->d_prow, std::max<size_t>(s.h_prow.size(), 1) * sizeof(uint16_t)));
         HIP_TRY(hipMalloc(&d->d_pboff, std::max<size_t>(s.h_pboff.size(), 1) * sizeof(int64_t)));
+        if (s.known) {
+            // -knownVariants: the input variants at covered positions are KPM's whole queue (no scan)
+            const int64_t nf = (int64_t)s.h_forced.size() / 2;
+            unsigned long long hc[8] = {0, 0, (unsigned long long)nf, 0, 0, 0, 0, 0};
+            HIP_TRY(hipMalloc(&d->d_mforced, (size_t)std::max<int64_t>(nf, 1) * sizeof(QueueSite)));
+            HIP_TRY(hipMalloc(&d->d_mforced_ctr, 8 * sizeof(unsigned long long)));
+            if (nf) HIP_TRY(hipMemcpy(d->d_mforced, s.h_forced.data(), (size_t)nf * sizeof(QueueSite), hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(d->d_mforced_ctr, hc, sizeof hc, hipMemcpyHostToDevice));
+            d->n_mforced = nf;
+        }
         if (s.pile_bytes) HIP_TRY(hipMemcpyAsync(d->d_pile, s.h_pile.data(), (size_t)s.pile_bytes, hipMemcpyHostToDevice, d->stream));
         if (!s.h_mc_pos.empty()) HIP_TRY(hipMemcpyAsync(d->d_mc_pos, s.h_mc_pos.data(), s.h_mc_pos.size() * sizeof(int32_t), hipMemcpyHostToDevice, d->stream));
         if (!s.h_mc_n.empty()) HIP_TRY(hipMemcpyAsync(d->d_mc_n, s.h_mc_n.data(), s.h_mc_n.size(), hipMemcpyHostToDevice, d->stream));
@@ -2487,6 +2513,11 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     // KTM and KPM are timed by events bound to their dispatches (ev 0-1 and 3-2)
     // KTM + KQN, timed together by events bound to their dispatches (ev 0-1), KPM by ev 3-2
     const int64_t nwords = d->g_len / 32 + 1;
+    const bool mknown = d->n_mforced >= 0;             // -knownVariants: the input variants are the queue
+    if (mknown) {
+        HIP_TRY(hipEventRecord(d->ev[0], d->stream));
+        HIP_TRY(hipEventRecord(d->ev[1], d->stream));
+    } else {
     HIP_TRY(hipMemsetAsync(d->d_need, 0, (size_t)nwords * sizeof(uint32_t), d->stream));
     {
         const int64_t ngroups = (d->mc_entries + 63) / 64;
@@ -2500,11 +2531,14 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
                               (const uint32_t*)d->d_need, (const uint8_t*)d->d_ref, nwords, d->d_hard, ctr, d->cap_hard);
         HIP_TRY(hipGetLastError());
     }
+    }
     if (ploidy >= 3 && !d->pool_valid) { err = "ploidy >= 3 without pool tables (device_set_pool)"; return -1; }
     // (no start event on KPM: a start event between KQN and KPM was measured to idle the device; KPM's time is
     // taken from KQN's end)
     hipExtLaunchKernelGGL(k_posterior_multi, dim3(2048), dim3(kPopThreads), 0, d->stream, nullptr, d->ev[2], 0,
-                          (const QueueSite*)d->d_hard, (const unsigned long long*)(ctr + 2), d->cap_hard, (const uint8_t*)d->d_ppile,
+                          (const QueueSite*)(mknown ? d->d_mforced : d->d_hard),
+                          (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : ctr + 2),
+                          mknown ? std::max<int64_t>(d->n_mforced, 1) : d->cap_hard, (const uint8_t*)d->d_ppile,
                           (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, (const LikTables*)d->d_tables, g,
                           S, min_adf, ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), d->d_psites, d->d_pcalls,
                           ctr, d->cap_psites, d->d_stamps);
@@ -2756,6 +2790,11 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
     }
     unsigned long long* ctr = d->slot[d->mnext].d_ctr;
     HIP_TRY(hipMemsetAsync(ctr, 0, 4 * sizeof(unsigned long long), d->stream));
+    const bool mknown = d->n_mforced >= 0;             // -knownVariants: the input variants are the queue
+    if (mknown) {
+        HIP_TRY(hipEventRecord(m.ev[0], d->stream));
+        HIP_TRY(hipEventRecord(m.ev[1], d->stream));
+    } else {
     HIP_TRY(hipMemsetAsync(m.d_need, 0, (size_t)nwords * sizeof(uint32_t), d->stream));
     const int64_t ngroups = (d->mc_entries + 63) / 64;
     const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((ngroups + 3) / 4, (int64_t)d->n_cu * 8));
@@ -2767,8 +2806,11 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
     hipExtLaunchKernelGGL(k_queue_need, dim3((unsigned)qblk), dim3(256), 0, d->stream, nullptr, m.ev[1], 0,
                           (const uint32_t*)m.d_need, (const uint8_t*)d->d_ref, nwords, m.d_hard, ctr, m.cap_hard);
     HIP_TRY(hipGetLastError());
+    }
     hipExtLaunchKernelGGL(k_posterior_multi, dim3(2048), dim3(kPopThreads), 0, d->stream, nullptr, m.ev[3], 0,
-                          (const QueueSite*)m.d_hard, (const unsigned long long*)(ctr + 2), m.cap_hard, (const uint8_t*)d->d_ppile,
+                          (const QueueSite*)(mknown ? d->d_mforced : m.d_hard),
+                          (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : ctr + 2),
+                          mknown ? std::max<int64_t>(d->n_mforced, 1) : m.cap_hard, (const uint8_t*)d->d_ppile,
                           (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, (const LikTables*)d->d_tables, g,
                           S, min_adf, ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), m.d_psites, m.d_pcalls,
                           ctr, m.cap_psites, (unsigned long long*)nullptr);

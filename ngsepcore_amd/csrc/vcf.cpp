@@ -252,7 +252,9 @@ void format_population_site(const ngsep_ctx* c, const ngsep_popsite_out& s, cons
     const int S = (int)c->sample_ids.size();
     const int ploidy = c->params.ploidy;
     const std::string& name = (s.seq_id >= 0 && s.seq_id < (int)c->seq_names.size()) ? c->seq_names[s.seq_id] : std::string("?");
-    o += name; o += '\t'; app(o, s.pos); o += "\t.\t"; o += kB[(int)s.alleles[0]]; o += '\t';
+    // -knownVariants: the input variant's ID (MultisampleVariantsDetector.java:543-545 writes the input variant)
+    const char* id = s.n_alleles == 2 ? known_id_at(c, s.seq_id, s.pos, s.alleles[1]) : nullptr;
+    o += name; o += '\t'; app(o, s.pos); o += '\t'; o += id ? id : "."; o += '\t'; o += kB[(int)s.alleles[0]]; o += '\t';
     for (int i = 1; i < s.n_alleles; i++) { if (i > 1) o += ','; o += kB[(int)s.alleles[i]]; }
     o += '\t'; app(o, s.qual); o += "\t.\t";
     int counts[4] = {0, 0, 0, 0}, sum = 0, ng = 0, nhet = 0;

@@ -401,6 +401,7 @@ class MultisampleVariantsDetector:
         self.device = 0
 
     def setGenome(self, v: str): self.genomeFile = v
+    def setKnownVariantsFile(self, v: str): self.knownVariantsFile = v          # (:193-195)
     def setOutFilename(self, v: str): self.outFilename = v
     def setMinAlleleDepthFrequency(self, v: float): self.params.min_allele_depth_freq = float(v)
     def setHeterozygosityRate(self, v: float):
@@ -428,6 +429,8 @@ class MultisampleVariantsDetector:
             raise NgsepError(_lib.NGSEP_E_IO, "The reference genome file is a required parameter")
         s = GpuPileupSession(self.params, self.device)
         s.load_fasta(self.genomeFile)
+        if getattr(self, "knownVariantsFile", None):
+            s.set_known_variants(self.knownVariantsFile)
         arr = (ctypes.c_char_p * len(input_files))(*[f.encode() for f in input_files])
         s._check(s._lib.ngsep_call_population_bams(s._ctx, arr, len(input_files), self.outFilename.encode()))
         return s

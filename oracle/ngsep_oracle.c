@@ -1307,8 +1307,8 @@ static void mvd_genotype_all(ngo_mvd* M, const ngo_pvar* v, double het, int* qs)
     *qs = q;
 }
 
-static void mvd_print(FILE* out, const char* seqName, int pos, const ngo_pvar* v, int qs, const ngo_mvd* M) {
-    fprintf(out, "%s\t%d\t.\t%c\t", seqName, pos, BASES[v->idx[0]]);
+static void mvd_print(FILE* out, const char* seqName, int pos, const char* id, const ngo_pvar* v, int qs, const ngo_mvd* M) {
+    fprintf(out, "%s\t%d\t%s\t%c\t", seqName, pos, id ? id : ".", BASES[v->idx[0]]);
     for (int i = 1; i < v->n; i++) fprintf(out, "%s%c", i > 1 ? "," : "", BASES[v->idx[i]]);
     fprintf(out, "\t%d\t.\t", qs);
     {
@@ -1362,8 +1362,10 @@ static void mvd_on_pileup(ngo_gen* G, int pos) {
     const ngo_seq* sq = &G->g->s[G->cur_seq];
     if (pos < 1 || pos > sq->len) return;
     char r = sq->seq[pos - 1];
-    /* calculateReferenceAlleleDiscovery (SingleSampleVariantPileupListener.java:191-206) */
-    if (p->ignore_lowercase_ref && islower((unsigned char)r)) return;
+    if (!G->known) {
+        /* calculateReferenceAlleleDiscovery (SingleSampleVariantPileupListener.java:191-206) */
+        if (p->ignore_lowercase_ref && islower((unsigned char)r)) return;
+    }
     char R = (char)toupper((unsigned char)r);
     /* discoverPopulationSNV (:585-597): pooled calls of every alignment, then per sample in the
      * order of its read groups (PileupRecord.getAlleleCalls, :104-152) */
@@ -1389,6 +1391,23 @@ static void mvd_on_pileup(ngo_gen* G, int pos) {
             ngo_counts_update(h, base_idx(a->chars[rp]), (int8_t)q, (a->flags & FLAG_REVERSE) != 0);
             if (rank >= 0 && M->ploidy >= 3) acalls_push(&M->sc[sm], base_idx(a->chars[rp]), (int8_t)q, (a->flags & FLAG_REVERSE) != 0);
         }
+    }
+    if (G->known) {
+        /* onPileup with input variants (MultisampleVariantsDetector.java:539-551): every input variant at this
+         * position (nextSIVIndex), genotypeVariant (:664-693) over its own alleles, the record always written
+         * (QUAL = the variant QS genotypeVariant sets, ID = the input's) */
+        while (G->known_next < G->n_known && G->known[G->known_next].seq == G->cur_seq && G->known[G->known_next].pos <= pos) {
+            const ngo_known* kv = &G->known[G->known_next++];
+            if (kv->pos != pos) continue;
+            ngo_pvar kvv = {0, {0}, 0};
+            kvv.idx[kvv.n++] = base_idx(kv->ref);
+            kvv.idx[kvv.n++] = base_idx(kv->alt);
+            int kqs = 0;
+            mvd_genotype_all(M, &kvv, G->het_rate, &kqs);
+            mvd_print(G->out, sq->name, pos, kv->id, &kvv, kqs, M);
+            G->st->variants_called++;
+        }
+        return;
     }
     /* SingleSampleVariantPileupListener.createSNVVariantPool (:297-332) */
     if (pooled.total_count == 0) return;
@@ -1421,7 +1440,7 @@ static void mvd_on_pileup(ngo_gen* G, int pos) {
     if (v.n < 2) return;   /* only the reference allele is left: not an SNV, no decided non-reference call */
     mvd_genotype_all(M, &v, G->het_rate, &qs);
     if (qs == 0 || qs < p->min_quality) return;           /* MultisampleVariantsDetector.java:534 */
-    mvd_print(G->out, sq->name, pos, &v, qs, M);
+    mvd_print(G->out, sq->name, pos, NULL, &v, qs, M);
     G->st->variants_called++;
 }
 

@@ -150,3 +150,34 @@ def test_reference_fields_replayed_on_gpu(tmp_path):
     checked, bad = R.check(rs, site, R.parse_vcf(d.outFilename))
     assert not bad, bad[:10]
     assert checked == 10508
+
+
+@pytest.mark.parametrize("kw,opts", [
+    (dict(genome=pysynth.CUSTOM, custom_len=30000, seed=9, n_samples=16, depth=10, snv_rate=3e-3), {}),
+    (dict(genome=pysynth.CUSTOM, custom_len=20000, seed=10, n_samples=12, depth=8, snv_rate=3e-3, quality_model=2),
+     {"ploidy": 1, "het_rate": 0.01}),
+])
+def test_population_known_variants(tmp_path, kw, opts):
+    """`MultisampleVariantsDetector -knownVariants` (MultisampleVariantsDetector.onPileup :539-551, genotypeVariant
+    :664-693): every input SNV at a covered position genotyped in every sample and written with the input's ID,
+    whatever its QS; population VCF identical to the oracle's through path B (sample BAMs) and the staged path."""
+    from test_gpu_known import _known_vcf
+    from ngsepcore_amd import MultisampleVariantsDetector
+    syn, fa, sam, rgs = population(tmp_path, **kw)
+    known = os.path.join(str(tmp_path), "known.vcf")
+    _known_vcf(known, syn, os.path.join(str(tmp_path), "pop_truth.vcf"), kw["seed"], n_random=400)
+    o = os.path.join(str(tmp_path), "o.vcf")
+    ngsep_oracle.run_mvd(fa, sam, o, 0.0, known_vcf=known, **oracle_params_from(opts))
+    assert n_records(o) > 100
+    bams = syn.write_sample_bams(os.path.join(str(tmp_path), "pop"))
+    d = MultisampleVariantsDetector()
+    for k, v in opts.items():
+        setattr(d.params, k, v)
+    if "het_rate" in opts:
+        d.params.het_rate_set = 1
+    d.setGenome(fa)
+    d.setKnownVariantsFile(known)
+    d.setOutFilename(os.path.join(str(tmp_path), "gpu_b.vcf"))
+    d.run(bams).close()
+    diff = diff_vcf(o, d.outFilename)
+    assert not diff, "\n".join(diff[:20])
