@@ -156,6 +156,7 @@ def test_reference_fields_replayed_on_gpu(tmp_path):
     (dict(genome=pysynth.CUSTOM, custom_len=30000, seed=9, n_samples=16, depth=10, snv_rate=3e-3), {}),
     (dict(genome=pysynth.CUSTOM, custom_len=20000, seed=10, n_samples=12, depth=8, snv_rate=3e-3, quality_model=2),
      {"ploidy": 1, "het_rate": 0.01}),
+    (dict(genome=pysynth.CUSTOM, custom_len=15000, seed=11, n_samples=8, depth=16, snv_rate=3e-3), {"ploidy": 4}),
 ])
 def test_population_known_variants(tmp_path, kw, opts):
     """`MultisampleVariantsDetector -knownVariants` (MultisampleVariantsDetector.onPileup :539-551, genotypeVariant
