@@ -119,7 +119,8 @@ def call_sharded(contigs: Sequence[Tuple[str, int]], call_contig: Callable[[str]
     return text
 
 
-def gpu_contig_caller(fasta: str, bam: str, params=None, device: int = 0) -> Callable[[str], str]:
+def gpu_contig_caller(fasta: str, bam: str, params=None, device: int = 0,
+                      known_vcf: Optional[str] = None) -> Callable[[str], str]:
     """The production per-sequence caller: SingleSampleVariantsDetector.findSNVS restricted to one
     sequence on this rank's GPU through the BAI index (ngsep_call_region_bam: only that sequence's BGZF
     blocks are read; without an index the file is streamed up to the sequence).  One device context per
@@ -133,6 +134,8 @@ def gpu_contig_caller(fasta: str, bam: str, params=None, device: int = 0) -> Cal
         if "s" not in state:
             state["s"] = GpuPileupSession(params, device)
             state["s"].load_fasta(fasta)
+            if known_vcf:                          # -knownVariants: each rank genotypes its sequences' inputs
+                state["s"].set_known_variants(known_vcf)
         s = state["s"]
         with tempfile.TemporaryDirectory() as d:
             out = os.path.join(d, "c.vcf")
@@ -146,21 +149,23 @@ def gpu_contig_caller(fasta: str, bam: str, params=None, device: int = 0) -> Cal
     return call
 
 
-def call_bam_sharded(fasta: str, bam: str, out_vcf: str, params=None, dist=None, device: Optional[int] = None) -> Optional[str]:
+def call_bam_sharded(fasta: str, bam: str, out_vcf: str, params=None, dist=None, device: Optional[int] = None,
+                     known_vcf: Optional[str] = None) -> Optional[str]:
     """SingleSampleVariantsDetector over the GPUs of one node: the BAM header's sequences split over the
     ranks (assign_contigs), each rank calling its own through the index on its GPU (device = local rank
     by default), the per-sequence blocks merged on rank 0 in header order."""
     contigs = bam_header_sequences(bam)
     if device is None:
         device = int(os.environ.get("LOCAL_RANK", "0"))
-    caller = gpu_contig_caller(fasta, bam, params, device)
+    caller = gpu_contig_caller(fasta, bam, params, device, known_vcf)
     try:
         return call_sharded(contigs, caller, out_vcf, dist)
     finally:
         caller.close()
 
 
-def gpu_population_caller(fasta: str, bams: Sequence[str], params=None, device: int = 0) -> Callable[[str], str]:
+def gpu_population_caller(fasta: str, bams: Sequence[str], params=None, device: int = 0,
+                          known_vcf: Optional[str] = None) -> Callable[[str], str]:
     """MultisampleVariantsDetector restricted to one sequence (-querySeq; every BAM read from that
     sequence's index chunks): the population VCF text of that sequence."""
     from .discovery import MultisampleVariantsDetector
@@ -172,6 +177,8 @@ def gpu_population_caller(fasta: str, bams: Sequence[str], params=None, device: 
             ctypes.pointer(d.params)[0] = params
             d.params.multisample = 1
         d.setGenome(fasta)
+        if known_vcf:
+            d.setKnownVariantsFile(known_vcf)
         d.setQuerySeq(name)
         d.device = device
         with tempfile.TemporaryDirectory() as t:
@@ -182,11 +189,11 @@ def gpu_population_caller(fasta: str, bams: Sequence[str], params=None, device: 
 
 
 def call_population_sharded(fasta: str, bams: Sequence[str], out_vcf: str, params=None, dist=None,
-                            device: Optional[int] = None) -> Optional[str]:
+                            device: Optional[int] = None, known_vcf: Optional[str] = None) -> Optional[str]:
     """MultisampleVariantsDetector over the GPUs of one node (configs[4]): sequences split over the ranks,
     the population VCF blocks merged on rank 0 in the first BAM's header order (the multi-file merge meets
     the sequences in that order, AlignmentsPileupGenerator.java:268-289)."""
     contigs = bam_header_sequences(bams[0])
     if device is None:
         device = int(os.environ.get("LOCAL_RANK", "0"))
-    return call_sharded(contigs, gpu_population_caller(fasta, bams, params, device), out_vcf, dist)
+    return call_sharded(contigs, gpu_population_caller(fasta, bams, params, device, known_vcf), out_vcf, dist)

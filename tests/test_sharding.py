@@ -207,3 +207,38 @@ def test_gpu_population_sharded_identical(tmp_path):
     merged = call_population_sharded(fa, bams, os.path.join(str(tmp_path), "sharded.vcf"))
     assert merged == open(d.outFilename).read()
     assert sum(1 for l in merged.splitlines() if not l.startswith("#")) > 20
+
+
+@pytest.mark.gpu
+def test_gpu_sharded_known_variants_equal_whole_file(tmp_path):
+    """-knownVariants through the sharded drivers (every rank genotypes its sequences' input variants): the
+    merged single-sample and population VCFs equal the whole-file runs."""
+    from test_gpu_known import _known_vcf
+    from ngsepcore_amd import GpuPileupSession, MultisampleVariantsDetector
+    from ngsepcore_amd.sharding import call_bam_sharded, call_population_sharded
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=3, depth=12, seed=12)
+    base = os.path.join(str(tmp_path), "d")
+    fa, sam, bam = syn.write(base)
+    known = os.path.join(str(tmp_path), "known.vcf")
+    _known_vcf(known, syn, base + "_truth.vcf", 12, n_random=600)
+    syn.close()
+    full = os.path.join(str(tmp_path), "full.vcf")
+    with GpuPileupSession() as s:
+        s.load_fasta(fa)
+        s.set_known_variants(known)
+        s.processFile(bam, full)
+    merged = call_bam_sharded(fa, bam, os.path.join(str(tmp_path), "m.vcf"), known_vcf=known)
+    assert merged == open(full).read()
+    pop = pysynth.Synth(genome=pysynth.YEAST, n_contigs=2, depth=8, seed=13, n_samples=6)
+    pfa, psam, _ = pop.write(os.path.join(str(tmp_path), "p"))
+    bams = pop.write_sample_bams(os.path.join(str(tmp_path), "pop"))
+    pknown = os.path.join(str(tmp_path), "pknown.vcf")
+    _known_vcf(pknown, pop, os.path.join(str(tmp_path), "p_truth.vcf"), 13, n_random=300)
+    pop.close()
+    d = MultisampleVariantsDetector()
+    d.setGenome(pfa)
+    d.setKnownVariantsFile(pknown)
+    d.setOutFilename(os.path.join(str(tmp_path), "pfull.vcf"))
+    d.run(bams).close()
+    pmerged = call_population_sharded(pfa, bams, os.path.join(str(tmp_path), "pm.vcf"), known_vcf=pknown)
+    assert pmerged == open(d.outFilename).read()
