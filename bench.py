@@ -2,26 +2,30 @@
 
 Workload (BASELINE.json configs[2], the largest single-GPU configuration and the one the roofline is
 quoted on): human chr20 (64,444,167 bp, synthetic bases) at 30x, 150 bp single-end synthetic reads, one
-sample.  The host packer's layout (bit planes, position-major byte pile, per-tile read segments,
-reference codes -- DESIGN.md section 2) is resident in HBM before the timed region; a step = one pass of
-the hot path over it: KT (bit-plane scan + hom-ref bounds) + KP (exact tally, posterior and call of the
-survivors) + KO (position order, (sequence, position) mapping) + D2H of the called sites + the host
-collect (libngsep_amd.so ngsep_submit_staged / ngsep_collect_staged, two passes in flight).
+sample.  The host packer's output -- the admitted reads' reference-projected code bytes (1 B per read base,
+pending-list order) in 64-read groups, 8-byte headers, reference codes -- is resident
+in HBM before the timed region; a step = one pass of the hot path over it: KL (per-position coverage, the
+other-allele / exception tallies and the count bound straight from the read bytes, the survivors' columns
+gathered) + KP (exact tally, posterior and call of the survivors) + KO (position order, (sequence,
+position) mapping) + D2H of the called sites + the host collect (libngsep_amd.so ngsep_submit_staged /
+ngsep_collect_staged, two passes in flight).
 
 Beside the resident rate the line carries:
-  * roofline   -- KT's bytes moved per launch (planes + reference + tile descriptors) / KT's average
-                  launch time from HIP events bound to its dispatch; `traffic` = HBM bytes per launch
+  * roofline   -- SURVEY.md 8(d)'s algorithmic bytes per launch (1 B per read base + 1 B of reference per
+                  genotyped position + 16 B per read) / KL's average launch time from HIP events bound to
+                  its dispatch; `bytes_moved_per_launch` = what KL actually reads (units incl. padding,
+                  8-B headers, group and block tables, reference codes); `traffic` = HBM bytes per launch
                   from the committed rocprofv3 PMC passes (profiles/pmc_traffic*.json);
-                  `alg_equiv_GBs` = SURVEY.md 8(d)'s algorithmic bytes / KT time (not a roofline);
   * end_to_end -- BAM on disk -> VCF on disk through ngsep_call_bam (path B: BGZF decode, admission,
                   projection, layout, H2D, kernels, VCF), wall time and positions/s;
   * cpu_baseline -- the oracle (C restatement of the reference, SAM -> VCF) on a bounded sample of the
                   same workload, single-thread and one process per core.
 
---gpus N: one process per GPU (spawned here under torch.distributed.run when WORLD_SIZE is unset); each
-rank owns its own synthetic chr20-sized genome (seed 3 + rank) -- windows shard with no data-path
-collective ("weak").  --config wgs: configs[3], the GRCh38 sequences split over the ranks by
-sharding.assign_contigs, each rank generating and calling only its own sequences.
+--gpus N > 1: one process per GPU (spawned here under torch.distributed.run when WORLD_SIZE is unset),
+by default BASELINE.json configs[3]: the GRCh38 sequences (30x) split over the ranks by
+sharding.assign_contigs, each rank generating and calling only its own sequences, no data-path collective
+(the genome is fixed: "strong").  --config chr20 with --gpus N: each rank its own chr20-sized genome (seed
+3 + rank, "weak").  --config wgs with one process: --wgs-shard picks one GPU's shard of the 8-way split.
 --config yeast: configs[1].  --config multisample: configs[4] (one GPU's contig shard of the 200-sample
 population).  --config coverage: CoverageStats on yeast 30x.
 
@@ -298,7 +302,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--depth", type=float, default=30.0)
-    ap.add_argument("--config", default="chr20", choices=["chr20", "yeast", "wgs", "multisample", "coverage"])
+    ap.add_argument("--config", default=None, choices=["chr20", "yeast", "wgs", "multisample", "coverage"],
+                    help="default: chr20 (configs[2]) on one GPU, wgs (configs[3], the contig split) on several")
     ap.add_argument("--no-cold", action="store_true", help="skip the cache-flushed passes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the BAM -> VCF end-to-end run")
@@ -311,6 +316,8 @@ def main():
                          "--wgs-shard picks the shard this GPU calls (one GPU's part of the 8-GPU split)")
     ap.add_argument("--wgs-shard", type=int, default=-1, help="wgs: the shard to call (default: the rank)")
     args = ap.parse_args()
+    if args.config is None:
+        args.config = "wgs" if args.gpus > 1 else "chr20"
     if args.config == "multisample" and args.depth == 30.0:
         args.depth = 10.0
 
@@ -529,16 +536,18 @@ def main():
     stats_all = [s.stats() for s in sessions]
     pile_bytes = sum(x.pile_bytes for x in stats_all)
     tile = st.tile_positions
-    # bytes KT moves per launch: the valid-call plane (rows_t * T / 8 per tile), the other-allele lists
-    # (2 B per entry, 4 B of range per tile), the reference codes (1 B per global position, halos
-    # included) and the 16-B tile descriptors.  The multisample scan (KTM + KQN) reads its candidate
-    # columns (1 B per valid call, 5 B per column, 8 B per 64 columns), the open-position bits (1 bit per
-    # global position) and writes the queue (8 B per open position)
+    # bytes the scan kernel moves per launch.  KL: the read-group units (1 B per read base, zero padded to the
+    # group's longest read in 8-B units; stats.pile_bytes), 8-B entry headers, 16 B per 64-read group, the
+    # reference codes (1 B per global position, halos included) and the two block tables (8 B per 256
+    # positions).  The multisample scan (KTM + KQN) reads its candidate columns (1 B per valid call, 5 B per
+    # column, 8 B per 64 columns), the open-position bits (1 bit per global position) and writes the queue (8 B
+    # per open position)
     if multi:
         kt_bytes = sum(x.pile_bytes + 5 * x.candidates + 8 * x.n_tiles + x.global_positions // 8 + 8 * x.hard_sites
                        for x in stats_all)
     else:
-        kt_bytes = sum(x.pile_bytes // 8 + 2 * x.other_allele_calls + x.global_positions + 20 * x.n_tiles for x in stats_all)
+        kt_bytes = sum(x.pile_bytes + 8 * x.alignments_admitted + 16 * ((x.alignments_admitted + 63) // 64) +
+                       x.global_positions + x.global_positions // 32 for x in stats_all)
     layout_ms = sum(x.layout_ms for x in stats_all)
     upload_ms = sum(x.upload_ms for x in stats_all)
     for s in sessions:
@@ -599,12 +608,15 @@ def main():
         value = total_positions * steps / elapsed
         k_avg_ms = sum(scan_ms) / len(scan_ms) * (len(sessions) if len(sessions) > 1 else 1)
         post_avg_ms = (sum(geno_ms) / len(geno_ms)) if max(geno_ms, default=0) > 0 else None
-        # SURVEY.md 8(d)'s algorithmic bytes (1 B per read base + 1 B reference + 16 B per read) as an
-        # equivalent rate beside the bytes KT moves
+        # SURVEY.md 8(d)'s algorithmic bytes (1 B per read base + 1 B reference per genotyped position + 16 B per
+        # read) per launch: `achieved` for the single-sample scan KL, which reads exactly that input
         alg_bytes = read_bases + positions + 16 * reads
-        achieved = kt_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else None
+        if multi:
+            achieved = kt_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else None
+        else:
+            achieved = alg_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else None
         traffic = load_traffic(workload_key)
-        scan_kernel = "k_scan_multi+k_queue_need" if multi else f"k_tile_scan<{tile // 32}>"
+        scan_kernel = "k_scan_multi+k_queue_need" if multi else f"k_read_scan<{tile}>"
         line = {
             "metric": METRIC,
             "value": value,
@@ -614,10 +626,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if (args.config == "wgs" and world > 1) else "weak",
             "vs_baseline": None,
             "dtype": "u8,f64",
-            "data": "synthetic (seeded generator, SURVEY.md 8(d)); host-packed layout resident in HBM",
+            "data": ("synthetic (seeded generator, SURVEY.md 8(d)); " +
+                     ("population candidate columns + pile resident in HBM" if multi else
+                      "the host packer's read-group layout (1 B per read base) resident in HBM; the step scans it")),
             "config": {
                 "workload": workload,
                 "positions_per_gpu": positions,
@@ -631,7 +645,8 @@ def main():
                 "device_runs_per_gpu": len(sessions),
                 "host_layout_ms": layout_ms,
                 "h2d_upload_ms": upload_ms,
-                "parallelism": f"dp{world} (independent genomic windows per GPU, no collective)",
+                "parallelism": (f"dp{world} (contig split of the genome over the GPUs, no collective)" if args.config == "wgs"
+                                else f"dp{world} (independent genomic windows per GPU, no collective)"),
             },
             "roofline": {
                 "bound": "hbm",
@@ -641,7 +656,8 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS if achieved else None,
                 "traffic": traffic,
-                "bytes_per_launch": kt_bytes,
+                "bytes_per_launch": alg_bytes if not multi else kt_bytes,
+                "bytes_moved_per_launch": kt_bytes,
                 "kernel_avg_ms": k_avg_ms,
                 "traffic_rate_GBs": (traffic / (k_avg_ms * 1e-3) / 1e9) if traffic and k_avg_ms > 0 else None,
                 "alg_bytes_per_launch": alg_bytes,

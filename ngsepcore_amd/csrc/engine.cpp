@@ -765,8 +765,10 @@ static void stream_launch(ngsep_ctx* c, int64_t w0, int64_t w1) {
             if (maxlast < p) continue;                                    // no pileup here
             while (ci < cut.size() && cut[ci].second < p) ci++;
             if (ci < cut.size() && cut[ci].first <= p) continue;          // carved: the caller's own path
-            j->forced.push_back((int32_t)(p + goff_k));
+            j->forced.push_back((int32_t)(p + goff_k));                   // a KP queue entry (SiteQ): no column yet
             j->forced.push_back(0x80 | (it->ref << 5) | (it->alt << 8) | 0x400);
+            j->forced.push_back(0);
+            j->forced.push_back(-1);
         }
     }
     j->seq_id = cr.seq_id;
@@ -1185,6 +1187,109 @@ static int build_single_layout(Staged& s, const std::vector<SRead>& reads, Layou
     return bad ? -1 : 0;
 }
 
+// Read-group layout (engine.hpp RGroup): the variant caller's device input.  The reads'
+// projected bytes are the ones the host packer produced (one code byte per reference position of the read,
+// pending-list order); here they are only regrouped so that the scan's loads coalesce: 64 consecutive reads per
+// group, interleaved in 8-byte units.  Headers: global first / last position and the strand bit.  The two
+// block tables give the scan its tile's entry range and the column gather the entries that can cover a
+// position.  Groups are independent: built on all host threads.
+static int build_rg_layout(Staged& s, const std::vector<SRead>& reads, LayoutArena& arena, bool exact) {
+    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    const auto t0 = std::chrono::steady_clock::now();
+    const int64_t n = (int64_t)reads.size();
+    const int64_t ng = (n + 63) / 64, ne = ng * 64;
+    s.rg = true;
+    s.tile = kKlTile;
+    s.n_tiles = s.g_len / kKlTile;
+    s.n_entries = ne;
+    s.n_groups = ng;
+    s.h_rh.resize((size_t)ne * 2);
+    s.h_grp.resize((size_t)ng);
+    // groups: units per read and unit offsets
+    int64_t base = 0;
+    for (int64_t g = 0; g < ng; g++) {
+        int32_t K = 0;
+        for (int64_t e = g * 64; e < std::min(n, g * 64 + 64); e++) {
+            const int64_t span = (int64_t)reads[(size_t)e].glast - reads[(size_t)e].gfirst + 1;
+            if (span > 0) K = std::max<int32_t>(K, (int32_t)((span + 7) / 8));
+        }
+        s.h_grp[(size_t)g] = RGroup{base, K, 0};
+        base += (int64_t)K * 64;
+    }
+    s.n_units = base;
+    if (!arena.ensure_units(base + 8, exact)) return -2;       // + 8: slack past the last unit
+    s.h_units = arena.units;
+    const int32_t last_first = n ? reads[(size_t)n - 1].gfirst : 1;
+    uint64_t* units = s.h_units;
+    parallel_for(ng, 64, [&](int64_t g0, int64_t g1) {
+        for (int64_t g = g0; g < g1; g++) {
+            const RGroup G = s.h_grp[(size_t)g];
+            for (int l = 0; l < 64; l++) {
+                const int64_t e = g * 64 + l;
+                uint64_t* dst = units + G.base + l;
+                if (e >= n) {                          // padding entry: empty
+                    s.h_rh[(size_t)(2 * e)] = last_first;
+                    s.h_rh[(size_t)(2 * e + 1)] = last_first - 1;
+                    for (int32_t k = 0; k < G.K; k++) dst[(int64_t)k * 64] = 0;
+                    continue;
+                }
+                const SRead& rd = reads[(size_t)e];
+                const int64_t span = std::max<int64_t>(0, (int64_t)rd.glast - rd.gfirst + 1);
+                s.h_rh[(size_t)(2 * e)] = rd.gfirst;
+                s.h_rh[(size_t)(2 * e + 1)] = (int32_t)((uint32_t)(span > 0 ? rd.glast : rd.gfirst - 1) | (rd.neg ? 0x80000000u : 0u));
+                const int64_t whole = span / 8;
+                for (int64_t k = 0; k < whole; k++) {
+                    uint64_t u;
+                    std::memcpy(&u, rd.bytes + 8 * k, 8);
+                    dst[k * 64] = u;
+                }
+                int64_t k = whole;
+                if (span % 8) {
+                    uint64_t u = 0;
+                    std::memcpy(&u, rd.bytes + 8 * k, (size_t)(span % 8));
+                    dst[k * 64] = u;
+                    k++;
+                }
+                for (; k < G.K; k++) dst[k * 64] = 0;
+            }
+        }
+    });
+    // block tables over the global coordinate (reads are sorted by gfirst)
+    const int64_t nb = (s.g_len >> kRgBlockShift) + 2;
+    s.h_blkA.resize((size_t)nb);
+    s.h_blkB.resize((size_t)nb);
+    parallel_for(nb, 1 << 14, [&](int64_t b0, int64_t b1) {
+        auto first_at = [&](int64_t v) {          // first read with gfirst >= v
+            return (int32_t)(std::lower_bound(reads.begin(), reads.end(), v, [](const SRead& r, int64_t x) { return (int64_t)r.gfirst < x; }) - reads.begin());
+        };
+        int64_t ia = first_at((b0 << kRgBlockShift) - s.max_span + 1), ib = first_at(b0 << kRgBlockShift);
+        for (int64_t b = b0; b < b1; b++) {
+            const int64_t va = (b << kRgBlockShift) - s.max_span + 1, vb = b << kRgBlockShift;
+            while (ia < n && (int64_t)reads[(size_t)ia].gfirst < va) ia++;
+            while (ib < n && (int64_t)reads[(size_t)ib].gfirst < vb) ib++;
+            s.h_blkA[(size_t)b] = (int32_t)ia;
+            s.h_blkB[(size_t)b] = (int32_t)ib;
+        }
+    });
+    if (host_timing)
+        std::fprintf(stderr, "[ngsep host]   read-group layout %.1f ms (%lld reads, %lld units)\n",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), (long long)n, (long long)base);
+    return 0;
+}
+
+bool LayoutArena::ensure_units(int64_t n_units, bool exact) {
+    if (units && n_units <= units_cap) return true;
+    pinned_free(units);
+    units = nullptr;
+    units_cap = 0;
+    int64_t want = exact ? n_units : n_units + n_units / 4;
+    want = std::max<int64_t>(want, 4096);
+    units = static_cast<uint64_t*>(pinned_alloc((size_t)want * sizeof(uint64_t)));
+    if (!units) return false;
+    units_cap = want;
+    return true;
+}
+
 bool LayoutArena::ensure(int64_t pile_bytes, bool exact) {
     if (cpile && pile_bytes <= cap) return true;
     release();
@@ -1201,10 +1306,12 @@ void LayoutArena::release() {
     pinned_free(cpile);
     pinned_free(planes);
     pinned_free(cneg);
+    pinned_free(units);
     cpile = nullptr;
     planes = nullptr;
     cneg = nullptr;
-    cap = 0;
+    units = nullptr;
+    cap = units_cap = 0;
 }
 
 // Multisample layout.  MultisampleVariantsDetector genotypes every sample from its own read groups
@@ -1451,7 +1558,7 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
             wr.push_back({ci, w0, w1});
         }
     }
-    s.g_len = ((g + 64 + kTileMaxPos - 1) / kTileMaxPos) * kTileMaxPos;   // whole tiles, halo for 16-B reads
+    s.g_len = ((g + 64 + kRunAlign - 1) / kRunAlign) * kRunAlign;   // whole tiles, halo for 16-B reads
     if (s.g_len >= ((int64_t)1 << 31))
         return set_error(c, NGSEP_E_UNSUPPORTED, "staged genome exceeds 2^31 positions per device run; use window batching");
     // reads of every window: those starting in [w0 - max_span + 1, w1]
@@ -1495,7 +1602,10 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
         }
         s.n_reads = nreads;
         s.n_read_bases = nbases;
-        const int lr = build_single_layout(s, reads, c->arena, true);
+        // the variant caller reads the read-group layout (KL scans it on the device); the relative allele counts
+        // listener the position-major pile
+        const int lr = c->params.relative_allele_counts ? build_single_layout(s, reads, c->arena, true)
+                                                        : build_rg_layout(s, reads, c->arena, true);
         if (lr == -2) return set_error(c, NGSEP_E_DEVICE, "pinned host memory for the layout could not be allocated");
         if (lr != 0) return set_error(c, NGSEP_E_INVALID, "internal error: pileup depth above the tile's row count");
         c->stats.slot_bytes = 0;
@@ -1572,7 +1682,7 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
         c->stats.slot_size = S;
     }
     c->stats.read_bases = nbases;
-    c->stats.pile_bytes = s.pile_bytes;
+    c->stats.pile_bytes = s.rg ? s.n_units * 8 : s.pile_bytes;
     c->stats.tile_positions = s.tile;
     c->stats.tile_rows_max = s.tile_rows_max;
     const auto h1 = std::chrono::steady_clock::now();
@@ -1600,6 +1710,11 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     std::vector<TileInfo>().swap(s.h_tinfo);
     std::vector<uint16_t>().swap(s.h_olist);
     std::vector<int32_t>().swap(s.h_loff);
+    std::vector<int32_t>().swap(s.h_rh);
+    std::vector<RGroup>().swap(s.h_grp);
+    std::vector<int32_t>().swap(s.h_blkA);
+    std::vector<int32_t>().swap(s.h_blkB);
+    s.h_units = nullptr;
     std::vector<int32_t>().swap(s.h_mc_pos);
     std::vector<uint8_t>().swap(s.h_mc_n);
     std::vector<int64_t>().swap(s.h_mc_gbase);
@@ -1632,7 +1747,7 @@ static void run_window_job(ngsep_ctx* c, WindowJob* j) {
     w.read_end = (int64_t)j->reads.size();
     s.windows.push_back(w);
     s.max_span = j->max_span;
-    s.g_len = (((int64_t)w.wlen + 2 * pad + 64 + kTileMaxPos - 1) / kTileMaxPos) * kTileMaxPos;
+    s.g_len = (((int64_t)w.wlen + 2 * pad + 64 + kRunAlign - 1) / kRunAlign) * kRunAlign;
     s.covered = w.wlen;                 // (the dump mode's record capacity)
     s.h_ref.assign((size_t)s.g_len, 0);
     fill_ref_codes(c, s, w, j->carved);
@@ -1640,13 +1755,14 @@ static void run_window_job(ngsep_ctx* c, WindowJob* j) {
     s.known = !c->known.empty();
     if (s.known) {
         s.h_forced.swap(j->forced);
-        s.h_forced_ctr[2] = (unsigned long long)(s.h_forced.size() / 2);
+        s.h_forced_ctr[2] = (unsigned long long)(s.h_forced.size() / 4);
     }
     s.n_reads = (int64_t)j->reads.size();
     int64_t nb = 0;
     for (const SRead& r : j->reads) nb += r.glast >= r.gfirst ? (int64_t)r.glast - r.gfirst + 1 : 0;
     s.n_read_bases = nb;
-    const int lr = build_single_layout(s, j->reads, c->arena, false);
+    const int lr = c->params.relative_allele_counts ? build_single_layout(s, j->reads, c->arena, false)
+                                                    : build_rg_layout(s, j->reads, c->arena, false);
     if (lr != 0) {
         j->rc = lr == -2 ? NGSEP_E_DEVICE : NGSEP_E_INVALID;
         j->err = lr == -2 ? "pinned host memory for the layout could not be allocated" : "internal error: pileup depth above the tile's row count";
@@ -1663,7 +1779,7 @@ static void run_window_job(ngsep_ctx* c, WindowJob* j) {
     }
     const auto h2 = std::chrono::steady_clock::now();
     c->stats.read_bases += nb;
-    c->stats.pile_bytes = s.pile_bytes;
+    c->stats.pile_bytes = s.rg ? s.n_units * 8 : s.pile_bytes;
     c->stats.tile_positions = s.tile;
     c->stats.tile_rows_max = std::max(c->stats.tile_rows_max, s.tile_rows_max);
     c->stats.global_positions += s.g_len;

@@ -55,6 +55,22 @@ constexpr int kScanRegUnits = 64 * 24;     // tile-size budget: 16-byte units pe
 constexpr int kTileMaxPos = 1024;          // largest tile (positions): <= 64 units per row
 constexpr int kTileMinPos = 16;
 constexpr int kPopTile = 128;              // positions per KPM pile tile
+constexpr int kRunAlign = 4096;            // a run's global coordinate is a whole number of these (KL tiles)
+
+// Read-group layout of the single-sample variant caller: the admitted reads of a run
+// in pending-list order are its entries; 64 consecutive entries form a group, and the group's reads'
+// projected code bytes (one per reference position of [gfirst, glast]) are interleaved in 8-byte units:
+// unit k of entry 64 g + l is units[base_g + 64 k + l] (bytes 8k .. 8k+7 of the read, zero past its end).
+// A wavefront that reads unit k of its 64 reads loads 512 contiguous bytes.  Entry header: {gfirst,
+// glast | negative-strand << 31}; padding entries are empty (glast = gfirst - 1, gfirst = the last real one).
+struct RGroup {
+    int64_t base;    // unit offset of the group
+    int32_t K;       // units per read (the group's longest span / 8, rounded up)
+    int32_t pad;
+};
+static_assert(sizeof(RGroup) == 16, "RGroup layout");
+constexpr int kRgBlockShift = 8;           // entry index tables per 256 positions (blkA / blkB)
+constexpr int kKlTile = 2048;              // positions per KL tile (one workgroup each; divides kRunAlign)
 constexpr int kMcMaxCalls = 254;           // multisample candidate column: valid calls the bounds take (sums fit 32 bits)
 
 // the (first) alternative allele of a record as a DNA index: a pool record keeps its variant's alleles in
@@ -432,6 +448,16 @@ struct Staged {            // everything resident for one run
     uint8_t* h_cpile = nullptr;
     uint32_t* h_cneg = nullptr;
     bool single = false;                // the single-sample layout (else the multisample one)
+    // read-group layout (engine.cpp build_rg_layout; the variant caller's device input): units in the
+    // context's pinned arena, entry headers, group table and the entry index of every 256-position block:
+    // blkA[b] = first entry with gfirst >= 256 b - max_span + 1 (the first that can cover the block),
+    // blkB[b] = first entry with gfirst >= 256 b
+    bool rg = false;
+    int64_t n_entries = 0, n_groups = 0, n_units = 0;
+    uint64_t* h_units = nullptr;
+    std::vector<int32_t> h_rh;          // 2 per entry
+    std::vector<RGroup> h_grp;
+    std::vector<int32_t> h_blkA, h_blkB;
     // -knownVariants: the run genotypes these sites (KP queue entries {global position, code}: code =
     // 0x80 | ref << 5 | alt << 8 | 0x400) instead of scanning; counters preset to their number
     bool known = false;
@@ -446,7 +472,10 @@ struct LayoutArena {
     uint32_t* planes = nullptr;
     uint32_t* cneg = nullptr;
     int64_t cap = 0;
+    uint64_t* units = nullptr;          // read-group layout units
+    int64_t units_cap = 0;
     bool ensure(int64_t pile_bytes, bool exact);
+    bool ensure_units(int64_t n_units, bool exact);
     void release();
     ~LayoutArena() { release(); }
 };

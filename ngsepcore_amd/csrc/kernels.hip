@@ -42,11 +42,14 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     } while (0)
 
 struct QueueSite;
+struct SiteQ;
 
 struct RunSlot {                     // one in-flight single-sample run (see device_submit)
     hipStream_t stream = nullptr;            // its compute stream (runs of the two slots overlap)
-    QueueSite* d_hard = nullptr;             // KT -> KP queue
+    SiteQ* d_hard = nullptr;                 // KL (KQ, -knownVariants) -> KG -> KP queue
     int64_t cap_hard = 0;
+    uint16_t* d_cols = nullptr;              // the queued sites' columns (KL / KG -> KP), u16 entries
+    int64_t cap_cols = 0;
     SiteRec* d_brec = nullptr;               // KP's records by position bucket: bucket b = d_brec[b * bcap ..]
     ngsep_site_out* d_ext = nullptr;         // KP's whole records (multi-allelic, pool, dump mode, full_records)
     int64_t cap_ext = 0, guess_ext = 0;
@@ -117,6 +120,15 @@ struct Device {
     int32_t planes_W = 0;            // words per plane row (T / 32)
     uint8_t* d_ref = nullptr;
     TileInfo* d_tinfo = nullptr;
+    // single-sample variant calling: the read-group layout (engine.hpp RGroup) KL scans
+    uint64_t* d_units = nullptr;
+    int2* d_rh = nullptr;
+    RGroup* d_grp = nullptr;
+    int32_t* d_blkA = nullptr;
+    int32_t* d_blkB = nullptr;
+    size_t cap_units = 0, cap_rh = 0, cap_grp = 0, cap_blk = 0, cap_blkB = 0;
+    int64_t n_entries = 0;
+    bool rg = false;
     int32_t* d_mc_pos = nullptr;     // multisample: candidate columns' global positions (KTM)
     uint8_t* d_mc_n = nullptr;       //   their valid-call counts
     int64_t* d_mc_gbase = nullptr;   //   byte offset of every 64th column
@@ -159,6 +171,7 @@ struct Device {
     int64_t last_n_sites = 1024;
     int64_t last_n_ext = 0;
     int64_t last_hard = 0;
+    int64_t last_cols = 0;      // column entries the last run reserved
     int64_t last_exact = 0;     // wave passes of KT's exact integer bound in the last run
     int kt_blocks_per_cu[2] = {0, 0};
     int kt_planes_per_cu[3] = {0, 0, 0};
@@ -204,6 +217,18 @@ struct QueueSite {
     int32_t rc;            // reference code
 };
 static_assert(sizeof(QueueSite) == 8, "QueueSite layout");
+
+// A single-sample site for KP: its position and reference code (-knownVariants: the input alleles, kernels.hip
+// k_posterior) and its column -- the nonzero codes of the reads covering it in pending-list order, u16 entries
+// code | negative strand << 8 at cols[4 coff ..], rows of them (-1: not gathered yet, KG does it; -2: the column
+// buffer overflowed, the host grows it and runs the pass again)
+struct SiteQ {
+    int32_t gpos;
+    int32_t rc;
+    int32_t coff;          // in units of 4 entries
+    int32_t rows;
+};
+static_assert(sizeof(SiteQ) == 16, "SiteQ layout");
 
 
 // ------------------------------------------------------------------------------------------
@@ -289,10 +314,9 @@ __device__ inline void put_site(SiteRec* __restrict__ slot, ngsep_site_out* __re
 }
 
 constexpr int kPostThreads = 256;
-__global__ __launch_bounds__(kPostThreads) void k_posterior(const QueueSite* __restrict__ queue, const unsigned long long* qn,
-                                                   int64_t qcap, const TileInfo* __restrict__ tinfo,
-                                                   const uint8_t* __restrict__ cpile, const uint32_t* __restrict__ cneg,
-                                                   int32_t log2T, const LikTables* __restrict__ tabs, GenotypeParams gp,
+__global__ __launch_bounds__(kPostThreads) void k_posterior(const SiteQ* __restrict__ queue, const unsigned long long* qn,
+                                                   int64_t qcap, const uint16_t* __restrict__ cols,
+                                                   const LikTables* __restrict__ tabs, GenotypeParams gp,
                                                    SiteRec* __restrict__ brec, int32_t* __restrict__ bcount,
                                                    int shift, int32_t bcap, ngsep_site_out* __restrict__ ext,
                                                    unsigned long long* ext_n, int64_t ext_cap) {
@@ -302,60 +326,44 @@ __global__ __launch_bounds__(kPostThreads) void k_posterior(const QueueSite* __r
         s_t[threadIdx.x >> 5][threadIdx.x & 31] =
             (threadIdx.x < 32 ? tabs->A : threadIdx.x < 64 ? tabs->H : tabs->E)[threadIdx.x & 31];
     __syncthreads();
-    const int32_t Tm = (1 << log2T) - 1;
     int64_t n = (int64_t)*qn;
     if (n > qcap) n = qcap;
     const int64_t stride = (int64_t)gridDim.x * kPostThreads;
     for (int64_t i = (int64_t)blockIdx.x * kPostThreads + threadIdx.x; i < n; i += stride) {
-        const QueueSite qs = queue[i];
+        const SiteQ qs = queue[i];
         const int32_t gpos = qs.gpos;
         const uint32_t rc = (uint32_t)qs.rc;
-        const TileInfo ti = tinfo[gpos >> log2T];
-        const int32_t rows = ti.rows;
-        const int64_t base = ti.off + (int64_t)(gpos & Tm) * rows;
+        const int32_t rows = qs.rows;
+        if (rows < 0) continue;                    // no column: an overflowed pass, which the host runs again
         // tally in rank (= pending-list) order
         int32_t total = 0;
         int32_t cnt[4] = {0, 0, 0, 0};
         int32_t sc[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
         // L00 L01 L02 L03 L11 L12 L13 L22 L23 L33 (upper triangle, ngsep_site_out.logc order)
         double L[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        // the column's dwords in order (rank r = byte sh + r of the dword stream) through a window of 8
-        // dwords in flight, the strand bits through a window of 3 words of the strand array (the pile has 64
-        // bytes and the strand array 4 words of slack, so the loads past the column need no guard); a small
-        // loop, so the kernel's code stays in the instruction cache
+        // the column's entries in order (rank r = entry r: two per dword) through a window of 8 dwords in flight
+        // (the column buffer has 64 bytes of slack, so the loads past the column need no guard); a small loop, so
+        // the kernel's code stays in the instruction cache
         {
-            const int64_t c0 = base & ~(int64_t)3;                        // cell of the first dword's byte 0
-            const uint32_t* cw = reinterpret_cast<const uint32_t*>(cpile) + (c0 >> 2);
-            const int sh = (int)(base - c0);
-            const int nd = (rows + sh + 3) >> 2;
+            const uint32_t* cw = reinterpret_cast<const uint32_t*>(cols) + ((int64_t)qs.coff << 1);
+            const int nd = (rows + 1) >> 1;
             uint32_t q0 = cw[0], q1 = cw[1], q2 = cw[2], q3 = cw[3], q4 = cw[4], q5 = cw[5], q6 = cw[6], q7 = cw[7];
-            const uint32_t* nw = cneg + (c0 >> 5);
-            uint64_t nb = (uint64_t)nw[0] | ((uint64_t)nw[1] << 32);
-            uint32_t nb2 = nw[2];
-            int nbo = (int)(c0 & 31);                                      // (a multiple of 4)
             for (int k = 0; k < nd; k++) {
                 const uint32_t d = q0;
                 q0 = q1; q1 = q2; q2 = q3; q3 = q4; q4 = q5; q5 = q6; q6 = q7;
                 q7 = cw[k + 8];
-                const uint32_t n4 = (uint32_t)(nb >> nbo) & 0xFu;             // the 4 cells' strand bits
-                nbo += 4;
-                if (nbo == 32) {
-                    nb = (nb >> 32) | ((uint64_t)nb2 << 32);
-                    nw++;
-                    nb2 = nw[2];
-                    nbo = 0;
-                }
 #pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const int r = 4 * k + e - sh;                          // rank of this byte
-                    const uint32_t cd = (r >= 0 && r < rows) ? (d >> (8 * e)) & 0xFFu : 0u;
+                for (int e = 0; e < 2; e++) {
+                    const int r = 2 * k + e;                               // rank of this entry
+                    const uint32_t ent = r < rows ? (d >> (16 * e)) & 0xFFFFu : 0u;
+                    const uint32_t cd = ent & 0xFFu;
                     if (cd == 0) continue;
                     total++;                                              // CountsHelper.java:210
                     if (!(cd & 0x80u)) continue;                          // q<=3 or not A/C/G/T (:214-221)
                     const int a = (int)((cd >> 5) & 3u);
                     int q = (int)(cd & 31u);
                     q = q > gp.max_q ? gp.max_q : q;                      // -maxBaseQS (:217-219)
-                    const int neg = (int)((n4 >> e) & 1u);
+                    const int neg = (int)((ent >> 8) & 1u);
 #pragma unroll
                     for (int t = 0; t < 4; t++) {                         // constant indices: registers, not scratch
                         cnt[t] += a == t ? 1 : 0;
@@ -547,11 +555,12 @@ struct PoolResult {
 };
 
 // one pass over a site's column: f(allele index into dna[] or -1, capped q) for every counted call
-// (q <= 3: lowBaseQualityCount only, not passed)
-template <class F>
-__device__ inline void pool_walk(const uint8_t* __restrict__ col, int32_t rows, const int* dna, int n, int32_t max_q, F&& f) {
+// (q <= 3: lowBaseQualityCount only, not passed).  A column is code bytes (KPM's pile) or u16 entries whose low
+// byte is the code (KP's columns)
+template <class C, class F>
+__device__ inline void pool_walk(const C* __restrict__ col, int32_t rows, const int* dna, int n, int32_t max_q, F&& f) {
     for (int32_t r = 0; r < rows; r++) {
-        const uint32_t cd = col[r];
+        const uint32_t cd = col[r] & 0xFFu;
         if (!(cd & 0x80u)) continue;                   // no call, or q <= 3 / not A,C,G,T: no likelihood update
         const int a = (int)((cd >> 5) & 3u);
         int q = (int)(cd & 31u);
@@ -563,7 +572,8 @@ __device__ inline void pool_walk(const uint8_t* __restrict__ col, int32_t rows, 
 }
 
 // genotypeVariantPool for the variant dna[0..n) (reference first); cnt4 = the column's A,C,G,T valid counts
-__device__ PoolResult pool_genotype(const uint8_t* __restrict__ col, int32_t rows, int32_t total, const int* cnt4,
+template <class C>
+__device__ PoolResult pool_genotype(const C* __restrict__ col, int32_t rows, int32_t total, const int* cnt4,
                                     const int* dna, int n, const PoolTables* __restrict__ pt, int32_t max_q) {
     PoolResult R;
     R.n_called = 0; R.c0 = -1; R.c1 = -1; R.gq = 0; R.dp = 0; R.report = false;
@@ -680,37 +690,34 @@ __device__ PoolResult pool_genotype(const uint8_t* __restrict__ col, int32_t row
     return R;
 }
 
-__global__ __launch_bounds__(kPostThreads) void k_posterior_pool(const QueueSite* __restrict__ queue, const unsigned long long* qn,
-                                                        int64_t qcap, const TileInfo* __restrict__ tinfo,
-                                                        const uint8_t* __restrict__ cpile, const uint32_t* __restrict__ cneg,
-                                                        int32_t log2T, const PoolTables* __restrict__ pt, GenotypeParams gp,
+__global__ __launch_bounds__(kPostThreads) void k_posterior_pool(const SiteQ* __restrict__ queue, const unsigned long long* qn,
+                                                        int64_t qcap, const uint16_t* __restrict__ cols,
+                                                        const PoolTables* __restrict__ pt, GenotypeParams gp,
                                                         SiteRec* __restrict__ brec, int32_t* __restrict__ bcount,
                                                         int shift, int32_t bcap, ngsep_site_out* __restrict__ ext,
                                                         unsigned long long* ext_n, int64_t ext_cap) {
-    const int32_t Tm = (1 << log2T) - 1;
     int64_t nq = (int64_t)*qn;
     if (nq > qcap) nq = qcap;
     const int64_t stride = (int64_t)gridDim.x * kPostThreads;
     for (int64_t i = (int64_t)blockIdx.x * kPostThreads + threadIdx.x; i < nq; i += stride) {
-        const QueueSite qs = queue[i];
+        const SiteQ qs = queue[i];
         const int32_t gpos = qs.gpos;
         const uint32_t rc = (uint32_t)qs.rc;
-        const TileInfo ti = tinfo[gpos >> log2T];
-        const int32_t rows = ti.rows;
-        const int64_t base = ti.off + (int64_t)(gpos & Tm) * rows;
-        const uint8_t* col = cpile + base;
+        const int32_t rows = qs.rows;
+        if (rows < 0) continue;                    // no column: an overflowed pass, which the host runs again
+        const uint16_t* col = cols + ((int64_t)qs.coff << 2);
         // the SNV tally of calculateCountsSNV (CountsHelper.java:83-95): totals, A,C,G,T and strand counts
         int32_t total = 0;
         int cnt[4] = {0, 0, 0, 0};
         int32_t sc[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
         for (int32_t r = 0; r < rows; r++) {
-            const uint32_t cd = col[r];
+            const uint32_t ent = col[r];
+            const uint32_t cd = ent & 0xFFu;
             if (cd == 0) continue;
             total++;
             if (!(cd & 0x80u)) continue;
             const int a = (int)((cd >> 5) & 3u);
-            const int64_t cell = base + r;
-            const int neg = (int)((cneg[cell >> 5] >> (cell & 31)) & 1u);
+            const int neg = (int)((ent >> 8) & 1u);
 #pragma unroll
             for (int t = 0; t < 4; t++) {
                 cnt[t] += a == t ? 1 : 0;
@@ -788,404 +795,263 @@ __global__ __launch_bounds__(kPostThreads) void k_posterior_pool(const QueueSite
 
 
 // ------------------------------------------------------------------------------------------
-// KT: pileup tile scan over the tile-blocked pileup matrix -- one wavefront per tile
+// KL: the single-sample scan over the read-group layout -- one workgroup per tile of T positions
 // ------------------------------------------------------------------------------------------
-// Tile t is rows_t x T code bytes, row-major, U = T/16 sixteen-byte units per row (T <= 1024, so
-// U <= 64).  Lane l of the wave owns column c = l % U (positions 16c .. 16c+15 of the tile) and
-// rows l/U, l/U + 64/U, ... : wave-load j fetches the contiguous kilobyte of units 64j .. 64j+63
-// (buffer loads, bounds-checked by the descriptor, so a short tile reads zeros past its end --
-// no branches around the loads), and every unit a lane holds belongs to its own column.
-//   phase 1  per-lane OR of the unit hit masks, then OR across the lanes of a column (shuffles):
-//            the positions whose pileup holds a valid non-reference call (MODE 0) or any counted
-//            call (MODE 1), restricted to callable / in-window positions.  Every other position is
-//            hom-ref (DESIGN.md "why pruning is exact") or has no pileup.  This is
-//            AlignmentsPileupGenerator.processCurrentPosition (discovery/AlignmentsPileupGenerator.java:475-498)
-//            reduced to the fact that decides whether SNVQ can call a variant there.  The same pass
-//            counts reference / other valid calls per position (byte-wise SWAR counters).
-//   phase 2  (MODE 0) count bound: a candidate whose counts already prove it hom-ref is dropped.
-//            The rest get the integer hom-ref bound: the lanes of a column re-read (L2-warm) their
-//            rows' byte at the candidate position and sum its fixed-point addends (integers:
-//            order-independent, so exact), then add up across the column's lanes.
-//   phase 3  a candidate the bounds prove hom-ref is dropped; the others are staged in LDS and
-//            queued for k_posterior (one global reservation per workgroup).
-// No LDS traffic on the streamed bytes, no workgroup barriers inside the tile loop.
-constexpr int kScanWaves = kScanThreads / 64;
-constexpr int kWaveQ = 512;             // survivors staged per wave before a global reservation
+// AlignmentsPileupGenerator.processCurrentPosition (discovery/AlignmentsPileupGenerator.java:475-498) reduced to
+// what decides whether SNVQ can call a variant at a position, straight from the packed
+// reads (engine.hpp RGroup: 1 B per read base, 8 B per read header):
+//   * coverage: every read segment inside the tile adds +1 / -1 to an LDS difference array (2 atomics per read);
+//   * exceptions: a wave takes a group of 64 reads, lane = read, and streams its 8-byte units (512 contiguous
+//     bytes per wave load); a byte is an exception when its position is callable and it is not a valid call of
+//     the reference allele (SWAR against the tile's reference codes in LDS).  Exceptions (a few % of the bytes)
+//     add to the position's LDS counter: low word = exceptions, high word = valid calls of another allele (na);
+//   * candidates: callable positions with na > 0; the reference calls are nr = coverage - exceptions, and the
+//     count bound (table cb_nr) drops those whose counts prove them hom-ref;
+//   * survivors: their columns (PileupRecord.getAlleleCalls(1) order) are gathered from the layout by the
+//     workgroup (wave_gather, L2-warm) into the column buffer, and queued for KP.
+// No MFMA: byte SWAR and integer counters.
+constexpr int kKlThreads = 256;
+constexpr int kKlSurv = 128;            // survivors one workgroup gathers (more: queued without a column, KG does them)
 
-// nonzero-allele valid bytes (MODE 0: a valid call that is not the reference allele, codes are
-// allele-XOR-reference) or any counted byte (MODE 1), one bit per byte
-template <int MODE>
-__device__ inline uint32_t unit_hits(const u32x4 d) {
-    auto f = [](uint32_t w) -> uint32_t {
-        uint32_t c;
-        if (MODE == 0) c = w & (((w & 0x60606060u) + 0x60606060u)) & 0x80808080u;
-        else c = (((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u;
-        return nib4(c);
-    };
-    return f(d.x) | (f(d.y) << 4) | (f(d.z) << 8) | (f(d.w) << 12);
-}
-// dword `sel` (0..3) of a unit without dynamic register indexing
-__device__ inline uint32_t unit_dword(const u32x4 d, int sel) {
-    const uint32_t lo = (sel & 1) ? d.y : d.x, hi = (sel & 1) ? d.w : d.z;
-    return (sel & 2) ? hi : lo;
-}
-
-struct ScanShared {
-    unsigned long long w[2][32];            // bound addends: [0] reference call, [1] other allele
-    int16_t cb[256];                        // count bound table (LikTables::cb_nr)
-    QueueSite q[kScanWaves][kWaveQ];        // survivors staged per wave
-    int32_t qn[kScanWaves];
-    int32_t qbase[kScanWaves];
-    unsigned long long ncand[kScanWaves];
-    uint32_t nexact[kScanWaves];
-};
-
-// wave-level reservation of the wave's staged survivors in the global queue
-__device__ __forceinline__ void wave_flush(ScanShared& sh, int wv, int lane, int32_t n, QueueSite* __restrict__ queue,
-                                           unsigned long long* __restrict__ counters, int64_t qcap) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    unsigned long long base = 0;
-    if (lane == 0) base = atomicAdd(&counters[2], (unsigned long long)n);
-    base = __shfl(base, 0, 64);
-    for (int i = lane; i < n; i += 64)
-        if ((int64_t)base + i < qcap) queue[base + i] = sh.q[wv][i];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-#ifndef NGSEP_KT_WAVES_PER_EU
-#define NGSEP_KT_WAVES_PER_EU 4      // build-time tuning: resident waves per SIMD the register budget targets
-#endif
-#ifndef NGSEP_KT16_WAVES_PER_EU
-#define NGSEP_KT16_WAVES_PER_EU 3    // the same for the 512-position plane tiles (118 VGPRs at 3: 4 waves resident)
-#endif
-
-
-// ------------------------------------------------------------------------------------------
-// KT: the single-sample tile scan -- one wavefront per tile (persistent waves, grid stride), two inputs:
-//   * the valid-call plane: rows_t rank rows of W = T/32 words.  Lane = (word w, row group g), W words x
-//     G groups = 64 lanes: the lane holds word w of rows g, g+G, ... of a 64-row chunk and counts them
-//     bit-sliced (bit j of count word k = bit k of position 32w+j's count); a butterfly over the G groups
-//     (DPP row rotations, the gfx950 lane swaps) leaves every lane its word's valid-call counts nv;
-//   * the other-allele list: one entry per valid call of another allele than the reference (its tile
-//     position), which the wave adds into per-position LDS counters na.
-// Lane l then owns positions P l .. P l + P-1 (P = T/64): a candidate is a callable position with na > 0
-// (every other position is hom-ref or has no pileup, DESIGN.md "why pruning is exact"); the count bound
-// (table cb_nr) drops those whose counts prove them hom-ref, the rest are queued for KP (with
-// gp.exact_bound, after the exact integer bound over their column of the byte pile).  The next tile's
-// plane words, reference bytes and first 64 list entries are in flight while a tile is examined.
-// ------------------------------------------------------------------------------------------
-// bit-sliced adders: out = a + b (k-bit numbers, k+1-bit result)
-template <int K>
-__device__ __forceinline__ void bs_add(const uint32_t* a, const uint32_t* b, uint32_t* out) {
-    uint32_t c = 0;
-#pragma unroll
-    for (int i = 0; i < K; i++) {
-        const uint32_t x = a[i] ^ b[i];
-        out[i] = x ^ c;
-        c = (a[i] & b[i]) | (c & x);
-    }
-    out[K] = c;
-}
-// out[0..log2(N)] = number of set bits among x[0..N) per bit position
-template <int N>
-struct BsCount {
-    static constexpr int B = BsCount<N / 2>::B + 1;
-    __device__ static __forceinline__ void run(const uint32_t* x, uint32_t* out) {
-        uint32_t lo[B - 1], hi[B - 1];
-        BsCount<N / 2>::run(x, lo);
-        BsCount<N / 2>::run(x + N / 2, hi);
-        bs_add<B - 1>(lo, hi, out);
-    }
-};
-template <>
-struct BsCount<1> {
-    static constexpr int B = 1;
-    __device__ static __forceinline__ void run(const uint32_t* x, uint32_t* out) { out[0] = x[0]; }
-};
-
-template <int W>
-__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(W >= 16 ? NGSEP_KT16_WAVES_PER_EU : NGSEP_KT_WAVES_PER_EU)))
-void k_tile_scan(const uint32_t* __restrict__ vplane, const uint16_t* __restrict__ olist, const int32_t* __restrict__ loff,
-                 const uint8_t* __restrict__ pile, const TileInfo* __restrict__ tinfo,
-                 const uint8_t* __restrict__ ref, int64_t n_tiles, const LikTables* __restrict__ tabs, GenotypeParams gp,
-                 QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap,
-                 int32_t* __restrict__ bcount, int64_t nb) {
-    constexpr int T = W * 32;
-    constexpr int G = 64 / W;                       // row groups
-    constexpr int KB0 = BsCount<W>::B;              // bits of a lane's count (<= W rows)
-    constexpr int KC = 7;                           // bits of a 64-row chunk's count
-    constexpr int P = T / 64;                       // positions per lane
-    __shared__ ScanShared sh;
-    // per-position other-allele counts of the wave's tile; position p at (p % P) * 65 + p / P, so the P reads and
-    // writes of a lane's own positions (p = P lane + j) touch consecutive banks across the wave and consecutive
-    // positions of the list fall in different banks
-    constexpr int NAS = 65;
-    __shared__ uint32_t s_na[kScanWaves][P * NAS];
-    auto na_at = [](int p) { return (p % P) * NAS + p / P; };
+// PileupRecord.getAlleleCalls(1) at global position p over the read-group layout: the nonzero codes of the reads
+// covering p, in pending-list (entry) order, as u16 entries code | negative strand << 8 (WRITE), one wave.  e0 is
+// at or before the first entry that can cover p (blkA).  Returns the entries written; *cov = the covering reads.
+template <bool WRITE>
+__device__ inline int32_t wave_gather(int32_t p, int64_t e0, int64_t n_entries, const int2* __restrict__ rh,
+                                      const RGroup* __restrict__ grp, const uint64_t* __restrict__ units,
+                                      uint16_t* __restrict__ dst, int32_t* cov_out) {
     const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lw = lane & (W - 1), lg = lane / W;   // this lane's word and row group (plane counting)
-    for (int64_t i = (int64_t)blockIdx.x * kScanThreads + threadIdx.x; i < nb; i += (int64_t)gridDim.x * kScanThreads) bcount[i] = 0;
-    if (threadIdx.x < 64) sh.w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
-    sh.cb[threadIdx.x] = tabs->cb_nr[threadIdx.x];
-    __syncthreads();
-    const long long th = tabs->t_het, to = tabs->t_homo;
-    const int32_t maxq = gp.max_q;
-    int32_t qn = 0;
-    uint32_t my_cand = 0, nexact = 0;
-    const int64_t nwaves = (int64_t)gridDim.x * kScanWaves;
-    const int64_t t0 = (int64_t)blockIdx.x * kScanWaves + wv;
-    auto wave_sync = [] {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    auto load_chunk = [&](int64_t off, int32_t rows, int c, uint32_t (&V)[W]) {
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(vplane + (off >> 5)), 0, rows * 4 * W, 0x00020000);
-#pragma unroll
-        for (int i = 0; i < W; i++) {
-            const int r = 64 * c + lg + G * i;
-            V[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, (r * W + lw) * 4, 0, 0);
-        }
-    };
-    // the reference codes of this lane's P positions, one byte each
-    auto load_ref = [&](int64_t t) -> uint64_t {
-        const uint8_t* rp = ref + t * T + P * lane;
-        if (P == 8) return *reinterpret_cast<const uint64_t*>(rp);
-        if (P == 4) return *reinterpret_cast<const uint32_t*>(rp);
-        return *reinterpret_cast<const uint16_t*>(rp);
-    };
-    auto uni64 = [](int64_t v) -> int64_t {
-        return ((int64_t)__builtin_amdgcn_readfirstlane((int32_t)(v >> 32)) << 32) |
-               (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)v);
-    };
-    // chunk counts: lane-local bit-sliced count, then the butterfly over the row groups
-    auto chunk_count = [&](const uint32_t (&X)[W], uint32_t (&out)[KC]) {
-        uint32_t c[KC];
-#pragma unroll
-        for (int k = 0; k < KC; k++) c[k] = 0;
-        BsCount<W>::run(X, c);
-        // all-reduce over the row groups (lanes w, w+W, ...) without LDS: DPP row rotations inside a
-        // 16-lane row (W = 4, 8), the gfx950 lane swaps across rows (16, 32); x + partner is the same
-        // bit-sliced sum on both sides
-        int kb = KB0;
-#pragma unroll
-        for (int d = W; d < 64; d <<= 1) {
-            uint32_t a[KC], o[KC], r[KC];
-#pragma unroll
-            for (int k = 0; k < KC; k++) {
-                a[k] = c[k];
-                o[k] = 0;
-                if (k < kb) {
-                    if (d == 4) o[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)c[k], 0x124, 0xF, 0xF, false);        // row_ror:4
-                    else if (d == 8) o[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)c[k], 0x128, 0xF, 0xF, false);   // row_ror:8
-                    else if (d == 16) { const auto pr = __builtin_amdgcn_permlane16_swap(c[k], c[k], false, false); a[k] = pr[0]; o[k] = pr[1]; }
-                    else { const auto pr = __builtin_amdgcn_permlane32_swap(c[k], c[k], false, false); a[k] = pr[0]; o[k] = pr[1]; }
-                }
+    int32_t n = 0, cov = 0;
+    for (int64_t e = e0 & ~(int64_t)63; e < n_entries; e += 64) {
+        const int2 h = rh[e + lane];                        // (n_entries is a multiple of 64)
+        const int32_t gf = h.x, gl = h.y & 0x7FFFFFFF;
+        const bool covers = gf <= p && p <= gl;
+        cov += (int32_t)__popcll(__ballot(covers));
+        if (WRITE) {
+            uint32_t code = 0;
+            if (covers) {
+                const RGroup G = grp[e >> 6];
+                const int32_t o = p - gf;
+                const uint64_t u = units[G.base + (int64_t)(o >> 3) * 64 + lane];
+                code = (uint32_t)(u >> (8 * (o & 7))) & 0xFFu;
             }
-            // kb-bit + kb-bit (unused high words are zero): a KC-bit ripple is exact
-            uint32_t cy = 0;
-#pragma unroll
-            for (int k = 0; k < KC; k++) {
-                const uint32_t x = a[k] ^ o[k];
-                r[k] = x ^ cy;
-                cy = (a[k] & o[k]) | (cy & x);
-            }
-#pragma unroll
-            for (int k = 0; k < KC; k++) c[k] = r[k];
-            kb++;
-        }
-#pragma unroll
-        for (int k = 0; k < KC; k++) out[k] = c[k];
-    };
-    // prefetch pipeline: the descriptor and list range two tiles ahead, the plane words, reference bytes and
-    // first list entries one tile ahead
-    TileInfo cur = t0 < n_tiles ? tinfo[t0] : TileInfo{0, 0, 0};
-    int32_t cur_lo = t0 < n_tiles ? loff[t0] : 0, cur_hi = t0 < n_tiles ? loff[t0 + 1] : 0;
-    TileInfo nxt = t0 + nwaves < n_tiles ? tinfo[t0 + nwaves] : TileInfo{0, 0, 0};
-    int32_t nxt_lo = t0 + nwaves < n_tiles ? loff[t0 + nwaves] : 0, nxt_hi = t0 + nwaves < n_tiles ? loff[t0 + nwaves + 1] : 0;
-    uint32_t Vn[W];
-#pragma unroll
-    for (int i = 0; i < W; i++) Vn[i] = 0;
-    uint64_t refn = 0;
-    uint32_t en = 0;
-    if (t0 < n_tiles && !(gp.ablate & 4)) {
-        load_chunk(uni64(cur.off), __builtin_amdgcn_readfirstlane(cur.rows), 0, Vn);
-        refn = load_ref(t0);
-        en = olist[__builtin_amdgcn_readfirstlane(cur_lo) + lane];     // (the list has 64 entries of slack)
-    }
-    for (int64_t t = t0; t < n_tiles; t += nwaves) {
-        if (gp.ablate & 4) break;
-        const int32_t rows = __builtin_amdgcn_readfirstlane(cur.rows);
-        const int64_t off = uni64(cur.off);
-        const int32_t lo = __builtin_amdgcn_readfirstlane(cur_lo), ne = __builtin_amdgcn_readfirstlane(cur_hi) - lo;
-        uint32_t V[W];
-#pragma unroll
-        for (int i = 0; i < W; i++) V[i] = Vn[i];
-        const uint64_t refq = refn;
-        const uint32_t e0 = en;
-        const int32_t tstart = (int32_t)(t * T);
-        // the next tile's inputs load meanwhile
-        const TileInfo nt = nxt;
-        const int32_t nt_lo = nxt_lo, nt_hi = nxt_hi;
-        if (t + 2 * nwaves < n_tiles) {
-            nxt = tinfo[t + 2 * nwaves];
-            nxt_lo = loff[t + 2 * nwaves];
-            nxt_hi = loff[t + 2 * nwaves + 1];
-        }
-        if (t + nwaves < n_tiles) {
-            load_chunk(uni64(nt.off), __builtin_amdgcn_readfirstlane(nt.rows), 0, Vn);
-            refn = load_ref(t + nwaves);
-            en = olist[__builtin_amdgcn_readfirstlane(nt_lo) + lane];
-        }
-        cur = nt;
-        cur_lo = nt_lo;
-        cur_hi = nt_hi;
-        if (rows == 0) continue;
-        const int ng = (rows + 63) >> 6;
-        const bool bound = gp.use_bound && rows <= 255 && !(gp.ablate & 256);   // (diagnostics: 256 = no counting)
-        // valid-call counts (bit-sliced, 8 bits: rows <= 255)
-        uint32_t cv[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) cv[k] = 0;
-        if (bound) {
-            for (int c = 0; c < ng; c++) {
-                if (c > 0) load_chunk(off, rows, c, V);
-                uint32_t xv[KC];
-                chunk_count(V, xv);
-                if (c == 0) {
-#pragma unroll
-                    for (int k = 0; k < KC; k++) cv[k] = xv[k];
-                } else {
-                    uint32_t zv[8], tv[9];
-#pragma unroll
-                    for (int k = 0; k < 8; k++) zv[k] = k < KC ? xv[k] : 0u;
-                    bs_add<8>(cv, zv, tv);
-#pragma unroll
-                    for (int k = 0; k < 8; k++) cv[k] = tv[k];
-                }
-            }
-        }
-        // other-allele counts per position: the list's entries into LDS counters
-        uint32_t* na_w = s_na[wv];
-#pragma unroll
-        for (int j = 0; j < P; j++) na_w[j * NAS + lane] = 0;
-        wave_sync();
-        for (int e = 0; e < ne; e += 64) {
-            const uint32_t pe = e == 0 ? e0 : (uint32_t)olist[lo + e + lane];
-            if (e + lane < ne) atomicAdd(&na_w[na_at((int)(pe & (T - 1)))], 1u);
-        }
-        wave_sync();
-        uint32_t mine = 0;
-#pragma unroll
-        for (int j = 0; j < P; j++) {
-            const bool callable = ((refq >> (8 * j)) & 0x80u) != 0;
-            mine |= (callable && na_w[j * NAS + lane] != 0) ? 1u << j : 0u;
-        }
-        my_cand += (uint32_t)__popc(mine);
-        if (gp.ablate & 1) continue;                   // diagnostics: scan only
-        if (!__ballot(mine != 0)) continue;
-        // this lane's slices of its positions' valid-call counts: bits [P lane, P lane + P) of the counts of
-        // word (P lane) / 32, which lane (P lane) / 32 holds (row group 0)
-        uint32_t vs[8];
-        {
-            const int wsrc = (P * lane) >> 5, bo = (P * lane) & 31;
-#pragma unroll
-            for (int k = 0; k < 8; k++) vs[k] = ((uint32_t)__shfl((int)cv[k], wsrc, 64) >> bo) & ((1u << P) - 1u);
-        }
-        while (__ballot(mine != 0)) {                  // wave-uniform loop over each lane's candidates
-            const bool has = mine != 0;
-            const int j = has ? __builtin_ctz(mine) : 0;
-            mine &= mine - 1u;
-            const int pp = P * lane + j;
-            const uint32_t rcode = (uint32_t)(refq >> (8 * j)) & 0xFFu;
-            bool need = has;
-            if (bound && has) {
-                uint32_t nv = 0;
-#pragma unroll
-                for (int k = 0; k < 8; k++) nv |= ((vs[k] >> j) & 1u) << k;
-                const uint32_t na = na_w[j * NAS + lane];
-                need = (int32_t)(nv - na) < (int32_t)sh.cb[na];   // the count bound does not drop it
-            }
-            if (bound && gp.exact_bound) {
-                // the exact integer bound over the candidate's column of the byte pile, one candidate at a time
-                unsigned long long ex = __ballot(need);
-                while (ex) {
-                    const int k = __builtin_ctzll(ex);
-                    ex &= ex - 1ull;
-                    const int p = __builtin_amdgcn_readlane(pp, k);
-                    const uint32_t ra = ((uint32_t)__builtin_amdgcn_readlane((int)rcode, k) >> 5) & 3u;
-                    nexact++;
-                    unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-                    for (int g = 0; g < ng; g++) {
-                        const int r = g * 64 + lane;
-                        // the position-major byte pile: position p's rows are one contiguous column
-                        const uint32_t cd = r < rows ? (uint32_t)pile[off + (int64_t)p * rows + r] : 0u;
-                        if (cd & 0x80u) {
-                            const uint32_t a = ((cd >> 5) & 3u) ^ ra;     // 0: a reference call
-                            int q = (int)(cd & 31u);
-                            q = q > maxq ? maxq : q;
-                            const unsigned long long wt = sh.w[a == 0 ? 0 : 1][q];
-                            a0 += a == 0 ? wt : 0ull;
-                            a1 += a == 1 ? wt : 0ull;
-                            a2 += a == 2 ? wt : 0ull;
-                            a3 += a == 3 ? wt : 0ull;
-                        }
-                    }
-                    for (int sft = 1; sft < 64; sft <<= 1) {
-                        a0 += __shfl_xor(a0, sft, 64);
-                        a1 += __shfl_xor(a1, sft, 64);
-                        a2 += __shfl_xor(a2, sft, 64);
-                        a3 += __shfl_xor(a3, sft, 64);
-                    }
-                    const long long R1 = (long long)(a0 & 0xFFFFFFFFull), R2 = (long long)(a0 >> 32);
-                    const long long x1 = (long long)(a1 & 0xFFFFFFFFull), y1 = (long long)(a2 & 0xFFFFFFFFull);
-                    const long long z1 = (long long)(a3 & 0xFFFFFFFFull);
-                    const long long x2 = (long long)(a1 >> 32), y2 = (long long)(a2 >> 32), z2 = (long long)(a3 >> 32);
-                    const bool drop = (R1 - x1 > th) && (R1 - y1 > th) && (R1 - z1 > th) &&
-                                      (R2 - x2 > to) && (R2 - y2 > to) && (R2 - z2 > to) &&
-                                      (R2 - x1 - y1 > th) && (R2 - x1 - z1 > th) && (R2 - y1 - z1 > th);
-                    if (drop && lane == k) need = false;
-                }
-            }
-            if (gp.ablate & 128) need = false;         // diagnostics: count bound only
-            // the survivors into the wave's staging area (rank among this round's survivors)
-            const unsigned long long m = __ballot(need);
-            const int32_t cnt = (int32_t)__popcll(m);
-            if (cnt) {
-                if (qn + cnt > kWaveQ) { wave_flush(sh, wv, lane, qn, queue, counters, qcap); qn = 0; }
+            const unsigned long long m = __ballot(code != 0);
+            if (code) {
                 const int rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                if (need) sh.q[wv][qn + rk] = QueueSite{tstart + pp, (int32_t)rcode};
-                qn += cnt;
+                dst[n + rk] = (uint16_t)(code | (((uint32_t)h.y >> 31) << 8));
+            }
+            n += (int32_t)__popcll(m);
+        }
+        if (__ballot(gf > p)) break;                       // entries are sorted by gfirst: none later covers p
+    }
+    if (cov_out) *cov_out = cov;
+    return n;
+}
+
+__device__ __forceinline__ uint32_t kl_exc(uint32_t x, uint32_t r) {
+    // bit 7 of byte k: the position is callable (r has bit 7) and byte k is not a valid call of r's allele
+    const uint32_t t = ((x ^ r) >> 5) & 0x07070707u;
+    return ((t + 0x7F7F7F7Fu) & 0x80808080u) & r;
+}
+__device__ __forceinline__ uint32_t kl_nonref(uint32_t x, uint32_t r) {
+    // bit 7 of byte k: a valid call (x bit 7) of another allele than the callable reference r
+    const uint32_t al = ((x ^ r) >> 5) & 0x03030303u;
+    return ((al + 0x7F7F7F7Fu) & 0x80808080u) & r & x;
+}
+
+template <int T>
+__global__ __launch_bounds__(kKlThreads) void k_read_scan(
+    const uint64_t* __restrict__ units, const int2* __restrict__ rh, const RGroup* __restrict__ grp,
+    const int32_t* __restrict__ blkA, const int32_t* __restrict__ blkB, int64_t n_entries,
+    const uint8_t* __restrict__ ref, const LikTables* __restrict__ tabs, GenotypeParams gp,
+    SiteQ* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap,
+    uint16_t* __restrict__ cols, int64_t col_cap, int32_t* __restrict__ bcount, int64_t nb) {
+    constexpr int PT = T / kKlThreads;                 // positions per thread in the candidate phase
+    __shared__ int32_t s_diff[T + 1];
+    __shared__ unsigned long long s_cnt[T];
+    __shared__ uint32_t s_ref[T / 4 + 4];              // tile position i's reference code at byte 8 + i; 8 zero bytes each side
+    __shared__ int16_t s_cb[256];
+    __shared__ int32_t s_sp[kKlSurv], s_scov[kKlSurv], s_src[kKlSurv], s_coff[kKlSurv];
+    __shared__ int32_t s_nsurv, s_wsum[kKlThreads / 64];
+    __shared__ unsigned long long s_colbase, s_qbase, s_ncand[kKlThreads / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int32_t tstart = (int32_t)((int64_t)blockIdx.x * T);
+    for (int64_t i = (int64_t)blockIdx.x * kKlThreads + tid; i < nb; i += (int64_t)gridDim.x * kKlThreads) bcount[i] = 0;
+    for (int i = tid; i <= T; i += kKlThreads) s_diff[i] = 0;
+    for (int i = tid; i < T; i += kKlThreads) s_cnt[i] = 0;
+    {
+        const uint32_t* r32 = reinterpret_cast<const uint32_t*>(ref + tstart);
+        for (int i = tid; i < T / 4; i += kKlThreads) s_ref[2 + i] = r32[i];
+        if (tid < 4) s_ref[tid < 2 ? tid : T / 4 + tid] = 0;
+    }
+    s_cb[tid] = tabs->cb_nr[tid];
+    if (tid == 0) s_nsurv = 0;
+    const int64_t e_lo = blkA[tstart >> kRgBlockShift], e_hi = blkB[(tstart + T) >> kRgBlockShift];
+    __syncthreads();
+    // ---- coverage and exceptions: wave w takes groups g_lo + w, g_lo + w + 4, ...
+    const int64_t g_lo = e_lo >> 6, g_hi = (e_hi + 63) >> 6;
+    for (int64_t g = g_lo + wv; g < g_hi; g += kKlThreads / 64) {
+        const int64_t e = g * 64 + lane;
+        const int2 h = rh[e];
+        const int32_t gf = h.x, gl = h.y & 0x7FFFFFFF;
+        const int32_t a = max(gf, tstart), b = min(gl, tstart + T - 1);
+        const bool act = e >= e_lo && e < e_hi && a <= b;
+        if (act) {
+            atomicAdd(&s_diff[a - tstart], 1);
+            atomicAdd(&s_diff[b - tstart + 1], -1);
+        }
+        const RGroup G = grp[g];
+        const int32_t k0 = act ? (a - gf) >> 3 : 0x7FFFFFFF, k1 = act ? (b - gf) >> 3 : -1;
+        int32_t kmin = k0, kmax = k1;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            kmin = min(kmin, __shfl_xor(kmin, o, 64));
+            kmax = max(kmax, __shfl_xor(kmax, o, 64));
+        }
+        const uint64_t* ub = units + G.base + lane;
+        const int32_t o0 = gf - tstart, lastb = gl - gf;   // tile position of the read's byte 0, its last byte index
+        auto unit = [&](uint64_t u, int32_t kk) {
+            const int32_t o = o0 + 8 * kk;                  // tile position of the unit's byte 0 (-7 .. T-1)
+            const int32_t ob = o + 8;
+            const int w = ob >> 2, sh = ob & 3;
+            const uint32_t r0 = s_ref[w], r1 = s_ref[w + 1], r2 = s_ref[w + 2];
+            const uint32_t rlo = __builtin_amdgcn_alignbyte(r1, r0, sh), rhi = __builtin_amdgcn_alignbyte(r2, r1, sh);
+            const uint32_t ulo = (uint32_t)u, uhi = (uint32_t)(u >> 32);
+            uint32_t elo = kl_exc(ulo, rlo), ehi = kl_exc(uhi, rhi);
+            const int32_t lb = lastb - 8 * kk;             // the read's last byte in this unit (>= 0)
+            if (lb < 7) {                                   // zero padding past the read's end
+                if (lb < 3) elo &= (1u << (8 * (lb + 1))) - 1u;
+                ehi = lb < 4 ? 0u : ehi & ((1u << (8 * (lb - 3))) - 1u);
+            }
+            if (!(elo | ehi)) return;
+            const uint32_t nlo = kl_nonref(ulo, rlo), nhi = kl_nonref(uhi, rhi);
+            while (elo) {
+                const int bit = __builtin_ctz(elo);
+                elo &= elo - 1u;
+                atomicAdd(&s_cnt[o + (bit >> 3)], 1ull + ((unsigned long long)((nlo >> bit) & 1u) << 32));
+            }
+            while (ehi) {
+                const int bit = __builtin_ctz(ehi);
+                ehi &= ehi - 1u;
+                atomicAdd(&s_cnt[o + 4 + (bit >> 3)], 1ull + ((unsigned long long)((nhi >> bit) & 1u) << 32));
+            }
+        };
+        for (int32_t k = kmin; k <= kmax; k += 4) {
+            uint64_t u[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int32_t kk = k + i;
+                u[i] = (kk >= k0 && kk <= k1) ? ub[(int64_t)kk * 64] : 0ull;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if (k + i >= k0 && k + i <= k1) unit(u[i], k + i);
+        }
+    }
+    __syncthreads();
+    // ---- coverage (prefix of the difference array), candidates, the count bound
+    int32_t loc[PT];
+    int32_t run = 0;
+#pragma unroll
+    for (int j = 0; j < PT; j++) { run += s_diff[PT * tid + j]; loc[j] = run; }
+    int32_t incl = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) s_wsum[wv] = incl;
+    __syncthreads();
+    int32_t off = incl - run;
+    for (int w = 0; w < wv; w++) off += s_wsum[w];
+    const bool bound = gp.use_bound != 0;
+    uint32_t ncand = 0;
+#pragma unroll
+    for (int j = 0; j < PT; j++) {
+        const int p = PT * tid + j;
+        const int32_t cov = off + loc[j];
+        const uint32_t rc = (s_ref[(p + 8) >> 2] >> (8 * ((p + 8) & 3))) & 0xFFu;
+        const unsigned long long cn = s_cnt[p];
+        const uint32_t exc = (uint32_t)cn, na = (uint32_t)(cn >> 32);
+        const bool cand = (rc & 0x80u) && na > 0;
+        ncand += cand ? 1u : 0u;
+        const bool need = cand && !(bound && na <= 255 && cov - (int32_t)exc >= (int32_t)s_cb[na]) && !(gp.ablate & 1);
+        if (need) {
+            const int slot = atomicAdd(&s_nsurv, 1);
+            if (slot < kKlSurv) {
+                s_sp[slot] = p;
+                s_scov[slot] = cov;
+                s_src[slot] = (int32_t)rc;
+            } else {                                        // past the workgroup's list: KG gathers it
+                const unsigned long long qi = atomicAdd(&counters[2], 1ull);
+                if ((int64_t)qi < qcap) queue[qi] = SiteQ{tstart + p, (int32_t)rc, 0, -1};
             }
         }
     }
-    // one global reservation per workgroup for what its waves staged; one statistics atomic
-    unsigned long long ncand = my_cand;
-    for (int sft = 1; sft < 64; sft <<= 1) ncand += __shfl_xor(ncand, sft, 64);
-    if (lane == 0) { sh.qn[wv] = qn; sh.ncand[wv] = ncand; sh.nexact[wv] = nexact; }
+    unsigned long long nc = ncand;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nc += __shfl_xor(nc, o, 64);
+    if (lane == 0) s_ncand[wv] = nc;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int32_t tot = 0;
-        unsigned long long nc = 0, ne = 0;
-        for (int w = 0; w < kScanWaves; w++) { sh.qbase[w] = tot; tot += sh.qn[w]; nc += sh.ncand[w]; ne += sh.nexact[w]; }
-        if (ne) atomicAdd(&counters[3], ne);
-        const unsigned long long base = tot ? atomicAdd(&counters[2], (unsigned long long)tot) : 0ull;
-        for (int w = 0; w < kScanWaves; w++) sh.qbase[w] += (int32_t)base;
-        if (nc) atomicAdd(&counters[1], nc);
+    const int ns = min(s_nsurv, kKlSurv);
+    if (tid == 0) {
+        unsigned long long tnc = 0;
+        for (int w = 0; w < kKlThreads / 64; w++) tnc += s_ncand[w];
+        if (tnc) atomicAdd(&counters[1], tnc);
+        if (ns) {
+            int32_t tot = 0;                                // column offsets, in units of 4 entries
+            for (int i = 0; i < ns; i++) { s_coff[i] = tot; tot += (s_scov[i] + 3) >> 2; }
+            s_colbase = atomicAdd(&counters[5], (unsigned long long)tot);
+            s_qbase = atomicAdd(&counters[2], (unsigned long long)ns);
+        }
     }
+    if (ns == 0) return;
     __syncthreads();
-    {
-        const int64_t base = sh.qbase[wv];
-        for (int i = lane; i < qn; i += 64)
-            if (base + i < qcap) queue[base + i] = sh.q[wv][i];
+    // ---- the survivors' columns (one wave each; the tile's headers and units are in L2)
+    for (int i = wv; i < ns; i += kKlThreads / 64) {
+        const int32_t p = tstart + s_sp[i];
+        const int64_t c4 = (int64_t)s_colbase + s_coff[i];
+        int32_t rows = -2;
+        if ((c4 << 2) + s_scov[i] <= col_cap)
+            rows = wave_gather<true>(p, blkA[p >> kRgBlockShift], n_entries, rh, grp, units, cols + (c4 << 2), nullptr);
+        const int64_t qi = (int64_t)s_qbase + i;
+        if (lane == 0 && qi < qcap) queue[qi] = SiteQ{p, s_src[i], (int32_t)c4, rows};
     }
 }
+
+// KG: the columns of queued sites without one (-knownVariants, dump mode / no pruning, a KL workgroup's overflow):
+// one wave per site, a counting pass, a reservation in the column buffer, the gather
+__global__ __launch_bounds__(256) void k_gather_cols(SiteQ* __restrict__ queue, const unsigned long long* __restrict__ qn,
+                                                     int64_t qcap, const int2* __restrict__ rh, const RGroup* __restrict__ grp,
+                                                     const uint64_t* __restrict__ units, const int32_t* __restrict__ blkA,
+                                                     int64_t n_entries, uint16_t* __restrict__ cols, int64_t col_cap,
+                                                     unsigned long long* __restrict__ counters) {
+    const int lane = threadIdx.x & 63;
+    int64_t n = (int64_t)*qn;
+    if (n > qcap) n = qcap;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; base < n; base += nw * 64) {
+        const int64_t i = base + lane;
+        int32_t gpos = 0, rows = 0;
+        if (i < n) { gpos = queue[i].gpos; rows = queue[i].rows; }
+        unsigned long long m = __ballot(i < n && rows == -1);
+        while (m) {
+            const int k = __builtin_ctzll(m);
+            m &= m - 1ull;
+            const int32_t p = __shfl(gpos, k, 64);
+            const int64_t e0 = blkA[p >> kRgBlockShift];
+            int32_t cov = 0;
+            wave_gather<false>(p, e0, n_entries, rh, grp, units, nullptr, &cov);
+            unsigned long long c4 = 0;
+            if (lane == 0) c4 = atomicAdd(&counters[5], (unsigned long long)((cov + 3) >> 2));
+            c4 = __shfl(c4, 0, 64);
+            int32_t r = -2;
+            if ((int64_t)(c4 << 2) + cov <= col_cap) r = wave_gather<true>(p, e0, n_entries, rh, grp, units, cols + (c4 << 2), nullptr);
+            if (lane == 0) { queue[base + k].coff = (int32_t)c4; queue[base + k].rows = r; }
+        }
+    }
+}
+
 
 __global__ __launch_bounds__(256) void k_zero_i32(int32_t* __restrict__ p, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0;
@@ -1195,7 +1061,7 @@ __global__ __launch_bounds__(256) void k_zero_i32(int32_t* __restrict__ p, int64
 // KQ: every in-window position queued (dump mode, and runs without the exact pruning: -h > 0.1 or
 //     prune_candidates = 0); KP skips positions without a pileup (VariantDiscoverySNVQAlgorithm.java:101-103)
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_queue_all(const uint8_t* __restrict__ ref, int64_t g_len, QueueSite* __restrict__ queue,
+__global__ __launch_bounds__(256) void k_queue_all(const uint8_t* __restrict__ ref, int64_t g_len, SiteQ* __restrict__ queue,
                                                    unsigned long long* __restrict__ counters, int64_t qcap,
                                                    int32_t* __restrict__ bcount, int64_t nb) {
     const int lane = threadIdx.x & 63;
@@ -1211,7 +1077,7 @@ __global__ __launch_bounds__(256) void k_queue_all(const uint8_t* __restrict__ r
         if (lane == 0) base = atomicAdd(&counters[2], (unsigned long long)__popcll(m));
         base = __shfl(base, 0, 64);
         const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (rc != 0 && (int64_t)(base + rank) < qcap) queue[base + rank] = QueueSite{(int32_t)g, (int32_t)rc};
+        if (rc != 0 && (int64_t)(base + rank) < qcap) queue[base + rank] = SiteQ{(int32_t)g, (int32_t)rc, 0, -1};
         if (lane == 0) atomicAdd(&counters[1], (unsigned long long)__popcll(m));
     }
 }
@@ -1928,6 +1794,14 @@ void device_release(Device* d) {
     d->planes_W = 0;
     (void)hipFree(d->d_ref); d->d_ref = nullptr;
     (void)hipFree(d->d_tinfo); d->d_tinfo = nullptr;
+    (void)hipFree(d->d_units); d->d_units = nullptr;
+    (void)hipFree(d->d_rh); d->d_rh = nullptr;
+    (void)hipFree(d->d_grp); d->d_grp = nullptr;
+    (void)hipFree(d->d_blkA); d->d_blkA = nullptr;
+    (void)hipFree(d->d_blkB); d->d_blkB = nullptr;
+    d->cap_units = d->cap_rh = d->cap_grp = d->cap_blk = d->cap_blkB = 0;
+    d->n_entries = 0;
+    d->rg = false;
     (void)hipFree(d->d_mc_pos); d->d_mc_pos = nullptr;
     (void)hipFree(d->d_mc_n); d->d_mc_n = nullptr;
     (void)hipFree(d->d_mc_gbase); d->d_mc_gbase = nullptr;
@@ -1966,6 +1840,7 @@ void device_destroy(Device* d) {
         (void)hipFree(sl.d_brec);
         (void)hipFree(sl.d_bcount);
         (void)hipFree(sl.d_hard);
+        (void)hipFree(sl.d_cols);
         (void)hipFree(sl.d_tables);
         if (sl.stream && sl.stream != d->stream) (void)hipStreamDestroy(sl.stream);
         (void)hipFree(sl.d_sorted);
@@ -2008,14 +1883,36 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
     const bool keep = s.single && d->d_ppile == nullptr;
     if (!keep) device_release(d);
     else HIP_TRY(hipDeviceSynchronize());          // the previous run is done reading them
-    if (ensure_dev(&d->d_pile, &d->cap_pile, (size_t)s.pile_bytes + 64, keep, err) ||      // + 64: KP loads whole dwords of a column
-        ensure_dev(&d->d_tinfo, &d->cap_tinfo, (size_t)std::max<int64_t>(s.n_tiles, 1) * sizeof(TileInfo), keep, err) ||
-        ensure_dev(&d->d_ref, &d->cap_ref, (size_t)s.g_len + 64, keep, err))
-        return -1;
-    if (s.n_tiles && !s.h_tinfo.empty()) HIP_TRY(hipMemcpyAsync(d->d_tinfo, s.h_tinfo.data(), (size_t)s.n_tiles * sizeof(TileInfo), hipMemcpyHostToDevice, d->stream));
+    if (ensure_dev(&d->d_ref, &d->cap_ref, (size_t)s.g_len + 64, keep, err)) return -1;
     HIP_TRY(hipMemsetAsync(d->d_ref + s.g_len, 0, 64, d->stream));
     HIP_TRY(hipMemcpyAsync(d->d_ref, s.h_ref.data(), (size_t)s.g_len, hipMemcpyHostToDevice, d->stream));
-    if (s.single) {
+    d->rg = s.rg;
+    if (s.rg) {
+        // the read-group layout: units, entry headers, group table, block tables (KL, KG)
+        const size_t nblk = (size_t)(s.g_len >> kRgBlockShift) + 2;
+        if (ensure_dev(&d->d_units, &d->cap_units, (size_t)(s.n_units + 8) * sizeof(uint64_t), keep, err) ||
+            ensure_dev(&d->d_rh, &d->cap_rh, (size_t)std::max<int64_t>(s.n_entries, 64) * sizeof(int2), keep, err) ||
+            ensure_dev(&d->d_grp, &d->cap_grp, (size_t)std::max<int64_t>(s.n_groups, 1) * sizeof(RGroup), keep, err) ||
+            ensure_dev(&d->d_blkA, &d->cap_blk, nblk * sizeof(int32_t), keep, err) ||
+            ensure_dev(&d->d_blkB, &d->cap_blkB, nblk * sizeof(int32_t), keep, err))
+            return -1;
+        if (s.n_units) HIP_TRY(hipMemcpyAsync(d->d_units, s.h_units, (size_t)s.n_units * sizeof(uint64_t), hipMemcpyHostToDevice, d->stream));
+        HIP_TRY(hipMemsetAsync(d->d_units + s.n_units, 0, 8 * sizeof(uint64_t), d->stream));
+        if (s.n_entries) HIP_TRY(hipMemcpyAsync(d->d_rh, s.h_rh.data(), (size_t)s.n_entries * sizeof(int2), hipMemcpyHostToDevice, d->stream));
+        else {
+            const int32_t empty[2] = {1, 0};
+            for (int k = 0; k < 64; k++) HIP_TRY(hipMemcpyAsync(d->d_rh + k, empty, sizeof empty, hipMemcpyHostToDevice, d->stream));
+            HIP_TRY(hipStreamSynchronize(d->stream));
+        }
+        if (s.n_groups) HIP_TRY(hipMemcpyAsync(d->d_grp, s.h_grp.data(), (size_t)s.n_groups * sizeof(RGroup), hipMemcpyHostToDevice, d->stream));
+        HIP_TRY(hipMemcpyAsync(d->d_blkA, s.h_blkA.data(), nblk * sizeof(int32_t), hipMemcpyHostToDevice, d->stream));
+        HIP_TRY(hipMemcpyAsync(d->d_blkB, s.h_blkB.data(), nblk * sizeof(int32_t), hipMemcpyHostToDevice, d->stream));
+        d->n_entries = std::max<int64_t>(s.n_entries, 64);
+    } else if (s.single) {
+        if (ensure_dev(&d->d_pile, &d->cap_pile, (size_t)s.pile_bytes + 64, keep, err) ||      // + 64: KP loads whole dwords of a column
+            ensure_dev(&d->d_tinfo, &d->cap_tinfo, (size_t)std::max<int64_t>(s.n_tiles, 1) * sizeof(TileInfo), keep, err))
+            return -1;
+        if (s.n_tiles && !s.h_tinfo.empty()) HIP_TRY(hipMemcpyAsync(d->d_tinfo, s.h_tinfo.data(), (size_t)s.n_tiles * sizeof(TileInfo), hipMemcpyHostToDevice, d->stream));
         // single sample: planes (KT), the position-major pile and its strand bits (KP)
         const size_t ncw = (size_t)(s.pile_bytes / 32);
         if (ensure_dev(&d->d_planes, &d->cap_planes, (size_t)std::max<int64_t>(s.pile_bytes / 8, 16), keep, err) ||
@@ -2033,6 +1930,7 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
         if (!s.h_loff.empty()) HIP_TRY(hipMemcpyAsync(d->d_loff, s.h_loff.data(), s.h_loff.size() * sizeof(int32_t), hipMemcpyHostToDevice, d->stream));
         d->planes_W = s.tile / 32;
     } else {
+        if (ensure_dev(&d->d_pile, &d->cap_pile, (size_t)s.pile_bytes + 64, false, err)) return -1;
         // multisample: the candidate columns (KTM), the position-major per-sample pile (KPM)
         HIP_TRY(hipMalloc(&d->d_mc_pos, std::max<size_t>(s.h_mc_pos.size(), 1) * sizeof(int32_t)));
         HIP_TRY(hipMalloc(&d->d_mc_n, std::max<size_t>(s.h_mc_n.size(), 1)));
@@ -2088,13 +1986,20 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
 // its ordered-record buffer, its counter set and a pinned host store.  Compute stream: [wait slot
 // free] KT KP KO; copy stream: [wait KO] D2H counters + records, clear the counter set.
 // ------------------------------------------------------------------------------------------
-static int grow_slot(Device* d, RunSlot& sl, int64_t sites, int64_t queue, std::string& err) {
+static int grow_slot(Device* d, RunSlot& sl, int64_t sites, int64_t queue, std::string& err, int64_t cols = 0) {
     if (sites > d->cap_sites) d->cap_sites = sites;     // the slots' ordered-record buffers follow
     if (queue > sl.cap_hard) {
         (void)hipFree(sl.d_hard);
         sl.d_hard = nullptr;
-        HIP_TRY(hipMalloc(&sl.d_hard, (size_t)queue * sizeof(QueueSite)));
+        HIP_TRY(hipMalloc(&sl.d_hard, (size_t)queue * sizeof(SiteQ)));
         sl.cap_hard = queue;
+    }
+    if (cols > sl.cap_cols) {                            // + 64 entries: KP's dword window reads past a column
+        (void)hipFree(sl.d_cols);
+        sl.d_cols = nullptr;
+        HIP_TRY(hipMalloc(&sl.d_cols, (size_t)(cols + 64) * sizeof(uint16_t)));
+        HIP_TRY(hipMemset(sl.d_cols, 0, (size_t)(cols + 64) * sizeof(uint16_t)));
+        sl.cap_cols = cols;
     }
     return 0;
 }
@@ -2104,14 +2009,18 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
                        bool idle, std::string& err) {
     // capacities (shared buffers only change while nothing runs): calls are rare; dump mode needs one
     // record per covered position
-    const int64_t nforced = (int64_t)s.h_forced.size() / 2;     // -knownVariants: the sites to genotype
+    const int64_t nforced = (int64_t)s.h_forced.size() / 4;     // -knownVariants: the sites to genotype (SiteQ)
     int64_t want = g.dump_all ? std::max<int64_t>(s.covered + 1024, 1024) : std::max<int64_t>(s.g_len / 256 + 4096, 4096);
     int64_t qwant = (g.dump_all || !prune) ? s.g_len + 1024 : std::max<int64_t>(s.g_len / 64 + 65536, 65536);
     want = std::max<int64_t>(want, nforced + 1024);
     qwant = std::max<int64_t>(qwant, nforced + 1024);
-    if (want > d->cap_sites || qwant > sl.cap_hard) {
+    // the queued sites' columns (u16 entries): the survivors are ~1 in 1000 positions at 30x; every covered
+    // position in dump mode (the read bases bound it); grown when a run overflows
+    int64_t cwant = std::max<int64_t>(std::max<int64_t>(1 << 20, s.g_len / 16), d->last_cols + d->last_cols / 4);
+    if (g.dump_all || !prune) cwant = std::max<int64_t>(cwant, s.n_read_bases + 4 * s.g_len);
+    if (want > d->cap_sites || qwant > sl.cap_hard || cwant > sl.cap_cols) {
         if (!idle) HIP_TRY(hipStreamSynchronize(sl.stream));
-        if (grow_slot(d, sl, want, qwant, err) != 0) return -1;
+        if (grow_slot(d, sl, want, qwant, err, cwant) != 0) return -1;
     }
     if (sl.cap < d->cap_sites) {
         HIP_TRY(hipEventSynchronize(sl.ev[4]));
@@ -2162,35 +2071,37 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     }
     // KT is timed by events bound to its dispatch (hipExtLaunchKernelGGL): the kernel's own start and end
     hipEvent_t k0 = d->time_scan ? sl.ev[0] : nullptr, k1 = d->time_scan ? sl.ev[1] : nullptr;
+    if (!d->rg) { err = "no read-group layout resident"; return -1; }
+    int64_t kg_sites = 0;                                        // sites queued without a column (KG's share)
     if (s.known) {
         // -knownVariants: no scan, the input variants' sites (covered, in window order) are KP's queue
-        if (nforced > 0) HIP_TRY(hipMemcpyAsync(sl.d_hard, s.h_forced.data(), (size_t)nforced * sizeof(QueueSite), hipMemcpyHostToDevice, sl.stream));
+        if (nforced > 0) HIP_TRY(hipMemcpyAsync(sl.d_hard, s.h_forced.data(), (size_t)nforced * sizeof(SiteQ), hipMemcpyHostToDevice, sl.stream));
         HIP_TRY(hipMemcpyAsync(ctr, s.h_forced_ctr, 8 * sizeof(unsigned long long), hipMemcpyHostToDevice, sl.stream));
         hipLaunchKernelGGL(k_zero_i32, dim3((unsigned)std::min<int64_t>((nb + 255) / 256, 4096)), dim3(256), 0, sl.stream, sl.d_bcount, nb);
         HIP_TRY(hipGetLastError());
         d->last_hard = nforced;
-    } else if (d->n_tiles > 0 && prune && d->planes_W) {
-        // bit-plane scan, persistent waves: as many workgroups as are co-resident, each wave walks the
-        // tiles with a grid stride, so at any moment the waves stream one contiguous stretch of the planes
-        const int wi = d->planes_W == 4 ? 0 : d->planes_W == 8 ? 1 : 2;
-        auto kt = wi == 0 ? (const void*)k_tile_scan<4> : wi == 1 ? (const void*)k_tile_scan<8> : (const void*)k_tile_scan<16>;
-        int& per_cu = d->kt_planes_per_cu[wi];
-        if (per_cu == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kt, kScanThreads, 0) != hipSuccess || per_cu < 1)) per_cu = 2;
-        int bpc = per_cu;
-        if (const char* e = std::getenv("NGSEP_BLOCKS_PER_CU")) bpc = std::max(1, std::atoi(e));   // tuning
-        const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((d->n_tiles + kScanWaves - 1) / kScanWaves, (int64_t)d->n_cu * bpc));
-        dim3 grid((unsigned)nblk);
-#define NGSEP_KTP_ARGS d->d_planes, d->d_olist, d->d_loff, d->d_pile, d->d_tinfo, d->d_ref, d->n_tiles, sl.d_tables, g, sl.d_hard, ctr, sl.cap_hard, sl.d_bcount, nb
-        if (wi == 0) hipExtLaunchKernelGGL(k_tile_scan<4>, grid, dim3(kScanThreads), 0, sl.stream, k0, k1, 0, NGSEP_KTP_ARGS);
-        else if (wi == 1) hipExtLaunchKernelGGL(k_tile_scan<8>, grid, dim3(kScanThreads), 0, sl.stream, k0, k1, 0, NGSEP_KTP_ARGS);
-        else hipExtLaunchKernelGGL(k_tile_scan<16>, grid, dim3(kScanThreads), 0, sl.stream, k0, k1, 0, NGSEP_KTP_ARGS);
-#undef NGSEP_KTP_ARGS
+        kg_sites = nforced;
+    } else if (d->n_tiles > 0 && prune) {
+        // KL: one workgroup per tile of kKlTile positions, straight from the read-group layout
+        hipExtLaunchKernelGGL(k_read_scan<kKlTile>, dim3((unsigned)d->n_tiles), dim3(kKlThreads), 0, sl.stream, k0, k1, 0,
+                              (const uint64_t*)d->d_units, (const int2*)d->d_rh, (const RGroup*)d->d_grp, (const int32_t*)d->d_blkA,
+                              (const int32_t*)d->d_blkB, d->n_entries, (const uint8_t*)d->d_ref, (const LikTables*)sl.d_tables, g,
+                              sl.d_hard, ctr, sl.cap_hard, sl.d_cols, sl.cap_cols, sl.d_bcount, nb);
         HIP_TRY(hipGetLastError());
     } else {
         // dump mode / no pruning: every in-window position goes to KP
         const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((s.g_len + 255) / 256, (int64_t)d->n_cu * 8));
         hipExtLaunchKernelGGL(k_queue_all, dim3((unsigned)nblk), dim3(256), 0, sl.stream, k0, k1, 0, (const uint8_t*)d->d_ref,
                               s.g_len, sl.d_hard, ctr, sl.cap_hard, sl.d_bcount, nb);
+        HIP_TRY(hipGetLastError());
+        kg_sites = s.g_len;
+    }
+    {
+        // KG: the columns of the sites queued without one (a KL workgroup's overflow only, in a scan run)
+        const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((kg_sites + 255) / 256, (int64_t)d->n_cu * 8));
+        hipLaunchKernelGGL(k_gather_cols, dim3((unsigned)(kg_sites ? nblk : d->n_cu)), dim3(256), 0, sl.stream, sl.d_hard,
+                           (const unsigned long long*)(ctr + 2), sl.cap_hard, (const int2*)d->d_rh, (const RGroup*)d->d_grp,
+                           (const uint64_t*)d->d_units, (const int32_t*)d->d_blkA, d->n_entries, sl.d_cols, sl.cap_cols, ctr);
         HIP_TRY(hipGetLastError());
     }
     // one lane per queued site: enough workgroups for the queue (the count is on the device; sized from the
@@ -2201,14 +2112,12 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         if (!d->pool_valid) { err = "ploidy >= 3 without pool tables (device_set_pool)"; return -1; }
         hipExtLaunchKernelGGL(k_posterior_pool, dim3(kp_grid), dim3(kPostThreads), 0, sl.stream,
                               d->time_posterior ? sl.ev[5] : nullptr, d->time_posterior ? sl.ev[2] : nullptr, 0,
-                              (const QueueSite*)sl.d_hard, (const unsigned long long*)(ctr + 2), sl.cap_hard,
-                              (const TileInfo*)d->d_tinfo, (const uint8_t*)d->d_pile, (const uint32_t*)d->d_cneg, d->log2_tile,
+                              (const SiteQ*)sl.d_hard, (const unsigned long long*)(ctr + 2), sl.cap_hard, (const uint16_t*)sl.d_cols,
                               (const PoolTables*)d->d_pool, g, sl.d_brec, sl.d_bcount, shift, bcap, sl.d_ext, ctr + 4, sl.cap_ext);
     } else {
         hipExtLaunchKernelGGL(k_posterior, dim3(kp_grid), dim3(kPostThreads), 0, sl.stream,
                               d->time_posterior ? sl.ev[5] : nullptr, d->time_posterior ? sl.ev[2] : nullptr, 0,
-                              (const QueueSite*)sl.d_hard, (const unsigned long long*)(ctr + 2), sl.cap_hard,
-                              (const TileInfo*)d->d_tinfo, (const uint8_t*)d->d_pile, (const uint32_t*)d->d_cneg, d->log2_tile,
+                              (const SiteQ*)sl.d_hard, (const unsigned long long*)(ctr + 2), sl.cap_hard, (const uint16_t*)sl.d_cols,
                               (const LikTables*)sl.d_tables, g, sl.d_brec, sl.d_bcount, shift, bcap, sl.d_ext, ctr + 4, sl.cap_ext);
     }
     HIP_TRY(hipGetLastError());
@@ -2285,12 +2194,15 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
     int64_t mx = (int64_t)(sl.h_ctr[0] >> 40);          // fullest position bucket
     int64_t q = (int64_t)sl.h_ctr[2];
     int64_t ne = (int64_t)sl.h_ctr[4];
-    for (int attempt = 0; n > d->cap_sites || q > sl.cap_hard || ne > sl.cap_ext || (!sl.g.dump_all && mx > d->ko_bcap); attempt++) {
+    int64_t nc = (int64_t)sl.h_ctr[5] * 4;               // column entries reserved
+    for (int attempt = 0; n > d->cap_sites || q > sl.cap_hard || ne > sl.cap_ext || nc > sl.cap_cols ||
+                          (!sl.g.dump_all && mx > d->ko_bcap); attempt++) {
         // more calls or undecided candidates than the buffers hold (e.g. -minQuality 0): drain, grow
         // and run this slot again in place (a later run in the other slot keeps its own results)
         if (attempt == 3) { err = "result buffers kept overflowing"; return -1; }
         HIP_TRY(hipDeviceSynchronize());
-        if (grow_slot(d, sl, std::max(d->cap_sites, n + 1024), std::max(sl.cap_hard, q + 1024), err) != 0) return -1;
+        if (grow_slot(d, sl, std::max(d->cap_sites, n + 1024), std::max(sl.cap_hard, q + 1024), err,
+                      std::max(sl.cap_cols, nc + nc / 4 + 1024)) != 0) return -1;
         if (ne > sl.cap_ext) {
             (void)hipFree(sl.d_ext);
             sl.d_ext = nullptr;
@@ -2310,7 +2222,9 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
         mx = (int64_t)(sl.h_ctr[0] >> 40);
         q = (int64_t)sl.h_ctr[2];
         ne = (int64_t)sl.h_ctr[4];
+        nc = (int64_t)sl.h_ctr[5] * 4;
     }
+    d->last_cols = nc;
     sl.busy = false;
     d->n_collected++;
     if (n > sl.guess) {

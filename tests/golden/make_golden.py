@@ -46,6 +46,10 @@ FULL_CASES = {
     "configs1_yeast_30x": dict(genome=0, depth=30, seed=2),
     "configs2_chr20_30x": dict(genome=1, contig_first=19, n_contigs=1, depth=30, seed=3, rng_per_contig=1),
     "configs3_wgs_chr21_30x": dict(genome=1, contig_first=20, n_contigs=1, depth=30, seed=4, rng_per_contig=1),
+    # the other two sequences of the bench's shard 0 of 8 (chr1 + chr15 + chr21): the staged 3-sequence device run
+    # of bench.py --config wgs is compared with all three (tests/test_gpu_wgs_shard.py)
+    "configs3_wgs_chr15_30x": dict(genome=1, contig_first=14, n_contigs=1, depth=30, seed=4, rng_per_contig=1),
+    "configs3_wgs_chr1_30x": dict(genome=1, contig_first=0, n_contigs=1, depth=30, seed=4, rng_per_contig=1),
 }
 # configs[4] at full size for one GPU's shard: MultisampleVariantsDetector on 200 synthetic yeast samples at 10x,
 # chrIV (the bench's --config multisample workload); the oracle's population VCF md5 + record count

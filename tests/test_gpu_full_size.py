@@ -36,7 +36,8 @@ def _first_diff(got_path, name):
     return f"line counts {len(want)} vs {len(got)}"
 
 
-@pytest.mark.parametrize("name", sorted(CASES))
+# chr1 (249 Mb) is compared in the staged shard-0 run only (tests/test_gpu_wgs_shard.py)
+@pytest.mark.parametrize("name", sorted(n for n in CASES if n != "configs3_wgs_chr1_30x"))
 def test_full_size_vcf_identical(tmp_path, name):
     case = CASES[name]
     syn = pysynth.Synth(**case["synth"])

@@ -142,11 +142,10 @@ def test_pruning_is_exact(tmp_path, depth, snv_rate, het):
     assert st.hard_sites < st.candidates     # the bound dropped candidates
 
 
-def test_exact_bound_path(tmp_path, monkeypatch):
-    """NGSEP_KT_EXACT=1: KT applies the exact integer hom-ref bound to the count-bound survivors over the
-    position-major byte column; the calls equal genotyping every position."""
-    monkeypatch.setenv("NGSEP_KT_EXACT", "1")
-    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=2, depth=20, seed=13, quality_model=2, snv_rate=3e-3)
+def test_scan_overflow_survivors(tmp_path):
+    """Dense variants (1 in 10 positions) and -minQuality 0: more count-bound survivors per 2048-position KL tile
+    than the workgroup gathers itself, so KG gathers the rest; calls equal genotyping every position."""
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=1, depth=20, seed=13, quality_model=2, snv_rate=0.1)
     res = []
     for prune in (1, 0):
         with GpuPileupSession(gpu_params(prune_candidates=prune, min_quality=0)) as s:
@@ -157,8 +156,8 @@ def test_exact_bound_path(tmp_path, monkeypatch):
             res.append([(x.sequence, x.pos, x.gq, x.qual, tuple(x.counts), tuple(x.logc)) for x in s.getCalledVariants()])
             if prune:
                 st = s.stats()
-    assert res[0] == res[1] and len(res[0]) > 100
-    assert st.exact_bound_passes > 0
+    assert res[0] == res[1] and len(res[0]) > 10000
+    assert st.hard_sites > 128 * (st.global_positions // 2048) // 4     # survivors well past the tiles' own lists
 
 
 def test_path_a_equals_path_b(tmp_path):
@@ -214,38 +213,34 @@ def test_async_passes_identical(tmp_path):
         assert g == ref
 
 
-@pytest.mark.parametrize("tile", [128, 256, 512])
+@pytest.mark.parametrize("window", [0, 5000])
 @pytest.mark.parametrize("depth,het", [(12, 0.05), (40, 0.1), (90, 0.001), (300, 0.001)])
-def test_tile_width_scan_paths(tmp_path, monkeypatch, tile, depth, het):
-    """Fixed tile widths of the bit-plane scan (one or several 64-row groups; above 255 rows no bound).
-    Pruned calls == genotyping every position (KQ queues all, KP genotypes them)."""
-    monkeypatch.setenv("NGSEP_TILE_T", str(tile))
+def test_scan_depths(tmp_path, window, depth, het):
+    """KL at several depths (above 255 covering reads the count bound is skipped) and window sizes (a window's
+    halo and tile cuts): pruned calls == genotyping every position (KQ queues all, KG gathers, KP genotypes)."""
     syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=1, depth=depth, seed=11, quality_model=2, snv_rate=3e-3)
     res = []
     for prune in (1, 0):
-        with GpuPileupSession(gpu_params(prune_candidates=prune, het_rate=het, min_quality=0)) as s:
+        with GpuPileupSession(gpu_params(prune_candidates=prune, het_rate=het, min_quality=0, window_positions=window)) as s:
             for name, seq in syn.contigs():
                 s.set_reference(name, seq)
             s.processAlignments(syn.batch())
             s.notifyEndOfAlignments()
             res.append([(x.sequence, x.pos, x.gq, x.qual, tuple(x.counts), tuple(x.logc)) for x in s.getCalledVariants()])
-            if prune:
-                st = s.stats()
-    assert st.tile_positions == tile
     assert res[0] == res[1]
     assert len(res[0]) > 100
 
 
-@pytest.mark.parametrize("tile", [128, 256, 512])
-def test_tile_width_vcf_identical(tmp_path, monkeypatch, tile):
-    """configs[0] data through each bit-plane tile width: VCF identical to the oracle's."""
-    monkeypatch.setenv("NGSEP_TILE_T", str(tile))
+@pytest.mark.parametrize("window", [1024, 7000, 0])
+def test_window_size_vcf_identical(tmp_path, window):
+    """configs[0] data through windows of several sizes (each a separate device run with its halo): VCF
+    identical to the oracle's."""
     _, fa, sam, bam = make_data(tmp_path, genome=pysynth.YEAST, n_contigs=1, depth=10, seed=1)
     o, _, _ = oracle_vcf(tmp_path, fa, sam)
-    g, gst = gpu_vcf_bam(tmp_path, fa, bam)
+    g, gst = gpu_vcf_bam(tmp_path, fa, bam, window_positions=window)
     d = diff_vcf(o, g)
     assert not d, "\n".join(d)
-    assert gst.tile_positions == tile
+    assert gst.tile_positions == 2048
 
 
 def test_reference_fields_single_sample_dump(tmp_path):
