@@ -261,6 +261,11 @@ int ngsep_write_population_vcf(ngsep_ctx* ctx, const char* path);
  * (MultisampleVariantsDetector.main/run, :412-459): samples from the BAM headers' @RG SM tags,
  * files merged as AlignmentsPileupGenerator.processFiles does (:201-266, chooseNextAln :268-289) */
 int ngsep_call_population_bams(ngsep_ctx* ctx, const char* const* bam_paths, int32_t n_files, const char* out_vcf_path);
+/* the same restricted to seq:first-last (1-based, inclusive; -querySeq -first -last), every file read from the region's
+ * BAI chunks; the context (reference, -knownVariants, device) is reused by the next call -- one context per rank in the
+ * sharded population caller (MultisampleVariantsDetector.run per sequence, :421-459) */
+int ngsep_call_population_region_bams(ngsep_ctx* ctx, const char* const* bam_paths, int32_t n_files, const char* seq,
+                                      int64_t first, int64_t last, const char* out_vcf_path);
 
 /* ---- path B: the whole SingleSampleVariantsDetector.findSNVS on a BAM file (:896-931) ----
  * BGZF blocks inflate on the host threads (NGSEP_THREADS / OMP_NUM_THREADS) while records are decoded;

@@ -178,6 +178,8 @@ SIGNATURES = {
     "ngsep_submit_staged": (ctypes.c_int, [_CTX]),
     "ngsep_collect_staged": (ctypes.c_int, [_CTX, P(ctypes.c_double)]),
     "ngsep_call_population_bams": (ctypes.c_int, [_CTX, P(ctypes.c_char_p), ctypes.c_int32, ctypes.c_char_p]),
+    "ngsep_call_population_region_bams": (ctypes.c_int, [_CTX, P(ctypes.c_char_p), ctypes.c_int32, ctypes.c_char_p,
+                                                          ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p]),
     "ngsep_bam_open": (ctypes.c_int, [_CTX, ctypes.c_char_p, P(ctypes.c_void_p)]),
     "ngsep_bam_next_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, P(NgsepReadBatch)]),
     "ngsep_bam_close": (ctypes.c_int, [ctypes.c_void_p]),

@@ -1332,3 +1332,27 @@ extern "C" int ngsep_call_population_bams(ngsep_ctx* c, const char* const* bam_p
     if (rc != NGSEP_OK) return rc;
     return ngsep_write_population_vcf(c, out_vcf_path);
 }
+
+// MultisampleVariantsDetector restricted to seq:first-last (-querySeq/-first/-last), every file read from the region's
+// index chunks: the per-sequence caller of the sharded population driver (sharding.call_population_sharded), one
+// context per rank -- reference, known variants and device kept from sequence to sequence.  Writes the VCF header and
+// the region's population records to out_vcf_path.
+extern "C" int ngsep_call_population_region_bams(ngsep_ctx* c, const char* const* bam_paths, int32_t n_files, const char* seq,
+                                                 int64_t first, int64_t last, const char* out_vcf_path) {
+    if (!c || !bam_paths || n_files <= 0 || !seq || !out_vcf_path || std::strlen(seq) >= sizeof c->params.query_seq) return NGSEP_E_INVALID;
+    if (c->cur_seq >= 0 || c->query_found)
+        return set_error(c, NGSEP_E_INVALID, "ngsep_call_population_region_bams needs a context without alignments");
+    const ngsep_params saved = c->params;
+    std::snprintf(c->params.query_seq, sizeof c->params.query_seq, "%s", seq);
+    c->params.query_first = (int32_t)std::max<int64_t>(0, std::min<int64_t>(first, INT32_MAX));
+    c->params.query_last = (int32_t)std::max<int64_t>(0, std::min<int64_t>(last, INT32_MAX));
+    const int rc = ngsep_call_population_bams(c, bam_paths, n_files, out_vcf_path);
+    c->params = saved;
+    c->query_found = c->query_done = false;
+    // the region's records are in its file; the next region starts from an empty population store
+    c->pop_sites.clear();
+    c->pop_calls.clear();
+    c->pop_big.clear();
+    c->pop_order.clear();
+    return rc;
+}

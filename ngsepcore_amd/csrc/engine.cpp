@@ -1663,12 +1663,16 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
                 const int64_t kb = c->known_seq_begin[(size_t)cr.seq_id], ke = c->known_seq_begin[(size_t)cr.seq_id + 1];
                 auto it = std::lower_bound(c->known.begin() + kb, c->known.begin() + ke, (int64_t)w.w0,
                                            [](const ngsep_ctx::KnownVar& v, int64_t p) { return v.pos < p; });
-                size_t r = 0;
+                // reads that start before the window's range end before w0, so they cannot cover an input variant
+                size_t r = (size_t)ranges[wi].first, ci = 0;
                 int64_t maxlast = INT64_MIN;
+                const auto& cv = cr.carved;
                 for (; it != c->known.begin() + ke && it->pos <= w1; ++it) {
                     const int64_t p = it->pos;
                     while (r < cr.first.size() && cr.first[r] <= p) { maxlast = std::max<int64_t>(maxlast, cr.last[r]); r++; }
                     if (maxlast < p) continue;                                    // no pileup here
+                    while (ci < cv.size() && cv[ci].second < p) ci++;
+                    if (ci < cv.size() && cv[ci].first <= p) continue;            // carved: the caller's own indel path
                     s.h_forced.push_back((int32_t)(p + goff));
                     s.h_forced.push_back(0x80 | (it->ref << 5) | (it->alt << 8) | 0x400);
                 }
@@ -2334,7 +2338,7 @@ extern "C" int ngsep_set_known_variants(ngsep_ctx* c, const char* vcf_path) {
         int k = 0;
         char* p = line;
         while (k < 6) { fld[k++] = p; char* t = std::strchr(p, '\t'); if (!t) break; *t = 0; p = t + 1; }
-        if (k < 6) { rc = set_error(c, NGSEP_E_FORMAT, "VCF line " + std::to_string(lineno) + " has fewer than 8 columns"); break; }
+        if (k < 6) { rc = set_error(c, NGSEP_E_FORMAT, "VCF line " + std::to_string(lineno) + " has fewer than the 6 columns CHROM to QUAL"); break; }
         if (fld[4][0] == '.') continue;                                  // a reference site (filterReferenceSitesGVCF)
         auto it = idx.find(fld[0]);
         if (it == idx.end()) continue;

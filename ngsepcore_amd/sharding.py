@@ -167,24 +167,36 @@ def call_bam_sharded(fasta: str, bam: str, out_vcf: str, params=None, dist=None,
 def gpu_population_caller(fasta: str, bams: Sequence[str], params=None, device: int = 0,
                           known_vcf: Optional[str] = None) -> Callable[[str], str]:
     """MultisampleVariantsDetector restricted to one sequence (-querySeq; every BAM read from that
-    sequence's index chunks): the population VCF text of that sequence."""
-    from .discovery import MultisampleVariantsDetector
+    sequence's index chunks): the population VCF text of that sequence.  One device context per rank, the
+    reference and the known variants loaded once (ngsep_call_population_region_bams reuses it)."""
+    import ctypes
+    from .discovery import GpuPileupSession, default_params
+
+    lengths = dict(bam_header_sequences(bams[0]))
+    arr = (ctypes.c_char_p * len(bams))(*[b.encode() for b in bams])
+    state = {}
 
     def call(name: str) -> str:
-        d = MultisampleVariantsDetector()
-        if params is not None:
-            import ctypes
-            ctypes.pointer(d.params)[0] = params
-            d.params.multisample = 1
-        d.setGenome(fasta)
-        if known_vcf:
-            d.setKnownVariantsFile(known_vcf)
-        d.setQuerySeq(name)
-        d.device = device
+        if "s" not in state:
+            p = default_params()
+            if params is not None:
+                ctypes.pointer(p)[0] = params
+            p.multisample = 1
+            state["s"] = GpuPileupSession(p, device)
+            state["s"].load_fasta(fasta)
+            if known_vcf:                          # -knownVariants: each rank genotypes its sequences' inputs
+                state["s"].set_known_variants(known_vcf)
+        s = state["s"]
         with tempfile.TemporaryDirectory() as t:
-            d.setOutFilename(os.path.join(t, "p.vcf"))
-            d.run(list(bams)).close()
-            return open(d.outFilename).read()
+            out = os.path.join(t, "p.vcf")
+            s._check(s._lib.ngsep_call_population_region_bams(s._ctx, arr, len(bams), name.encode(), 1,
+                                                                lengths.get(name, 1 << 31), out.encode()))
+            return open(out).read()
+
+    def close():
+        if "s" in state:
+            state.pop("s").close()
+    call.close = close
     return call
 
 
@@ -196,4 +208,8 @@ def call_population_sharded(fasta: str, bams: Sequence[str], out_vcf: str, param
     contigs = bam_header_sequences(bams[0])
     if device is None:
         device = int(os.environ.get("LOCAL_RANK", "0"))
-    return call_sharded(contigs, gpu_population_caller(fasta, bams, params, device, known_vcf), out_vcf, dist)
+    caller = gpu_population_caller(fasta, bams, params, device, known_vcf)
+    try:
+        return call_sharded(contigs, caller, out_vcf, dist)
+    finally:
+        caller.close()

@@ -279,6 +279,10 @@ enum { OP_H = 0, OP_D = 1, OP_I = 2, OP_M = 3, OP_P = 4, OP_N = 5, OP_S = 6, OP_
 #define FLAG_SECONDARY 0x100
 #define FLAG_MULTIPLE 0x1000
 
+/* an indel call of an alignment: GenomicVariantImpl(seq, refPos, refLast, TYPE_INDEL) with setLength(opLen),
+ * keyed by refPos = the reference position of the base before the event (ReadAlignment.java:798-815) */
+typedef struct { int first, last, len; } ngo_indel;
+
 typedef struct ngo_aln {
     int seq;                 /* genome index */
     int first, last, read_length, flags, rg;
@@ -288,15 +292,19 @@ typedef struct ngo_aln {
     int ignore_start, ignore_end;
     int16_t* acl;            /* alleleCallLength, :747-834 */
     int has_indel;
+    int n_indel, cap_indel;  /* indelCalls (TreeMap by refPos: ascending), rebuilt with acl */
+    ngo_indel* indel;
 } ngo_aln;
 
-static void aln_free(ngo_aln* a) { free(a->ops); free(a->chars); free(a->quals); free(a->acl); free(a); }
+static void aln_free(ngo_aln* a) { free(a->ops); free(a->chars); free(a->quals); free(a->acl); free(a->indel); free(a); }
 
-/* ReadAlignment.updateAlleleCallsInfo, ReadAlignment.java:747-834 (indel-call map omitted:
- * SNV-only inputs never populate it) */
+/* ReadAlignment.updateAlleleCallsInfo, ReadAlignment.java:747-834: alleleCallLength per read position and the
+ * indel calls (recomputed after every change of the alignment or of the bases to ignore, which is when the
+ * reference's lazy alleleCallsUpdated flag would trigger it) */
 static void update_allele_calls(ngo_aln* a) {
     free(a->acl);
     a->acl = calloc(a->read_length > 0 ? a->read_length : 1, sizeof(int16_t));
+    a->n_indel = 0;
     int refPos = a->first, readPos = 0, prevIndel = 0;
     const int closeIndel = 2;  /* basesToIgnoreCloseToIndel, :115 */
     for (int i = 0; i < a->n_ops; i++) {
@@ -320,8 +328,16 @@ static void update_allele_calls(ngo_aln* a) {
                     int readPosAfterIndel = readPos + nextReadCons + 1;
                     skip = skip || (nextIsIndel && j == len - 1 && (a->read_length - readPosAfterIndel < a->ignore_end));
                     if (!skip && readPos < a->read_length) {
-                        if (j == len - 1 && nextIsIndel) a->acl[readPos] = (nextOp == OP_I) ? (int16_t)(nextLen + 2) : 2;
-                        else a->acl[readPos] = 1;
+                        if (j == len - 1 && nextIsIndel) {
+                            a->acl[readPos] = (nextOp == OP_I) ? (int16_t)(nextLen + 2) : 2;
+                            int refLast = refPos + 1;
+                            if (nextOp != OP_I) refLast += nextLen;
+                            if (a->n_indel == a->cap_indel) { a->cap_indel = a->cap_indel ? 2 * a->cap_indel : 4; a->indel = realloc(a->indel, sizeof(ngo_indel) * a->cap_indel); }
+                            /* TreeMap.put: a later event at the same key replaces the earlier one */
+                            if (a->n_indel > 0 && a->indel[a->n_indel - 1].first == refPos) a->n_indel--;
+                            a->indel[a->n_indel].first = refPos; a->indel[a->n_indel].last = refLast; a->indel[a->n_indel].len = nextLen;
+                            a->n_indel++;
+                        } else a->acl[readPos] = 1;
                     }
                     refPos++; readPos++;
                 }
@@ -415,6 +431,8 @@ typedef struct ngo_call {
     const char* id;           /* -knownVariants: the input variant's ID (NULL: '.') */
     int known;                /* 1: a genotyped input variant (genotype 0 hom-ref, -1 undecided allowed) */
     int logc_present;         /* 0: no log-conditionals (an undecided call without allele calls) */
+    int embedded;             /* TYPE_EMBEDDED_SNV (-embeddedSNVs inside a called indel, :227) */
+    struct ngo_indel_call_s* indel;   /* an indel / STR call instead of an SNV (ngsep_oracle_indel.inc) */
     /* ploidy >= 3 (genotypeVariantPool): a CalledGenomicVariantImpl over the pool variant's alleles */
     int pool;                 /* 1: the fields below describe the call, logc[][] is over the variant alleles */
     int pool_n;               /* variant alleles: DNA indexes pool_dna[0..n) (reference first) */
@@ -520,7 +538,9 @@ static void print_pool_call(FILE* out, const char* seqName, const ngo_call* c) {
     fprintf(out, "\n");
 }
 
+static void print_indel_call_any(FILE* out, const char* seqName, const ngo_call* c);
 static void print_call(FILE* out, const char* seqName, const ngo_call* c) {
+    if (c->indel) { print_indel_call_any(out, seqName, c); return; }
     if (c->pool) { print_pool_call(out, seqName, c); return; }
     fprintf(out, "%s\t%d\t%s\t%c\t", seqName, c->pos, c->id ? c->id : ".", c->ref);
     if (c->n_alleles == 2) fprintf(out, "%c", BASES[c->idx[1]]);
@@ -529,7 +549,8 @@ static void print_call(FILE* out, const char* seqName, const ngo_call* c) {
     /* INFO: FS (SingleSampleVariantsDetector.java:957, CalledSNV only) then TYPE (VCFFileWriter.java:47-49) */
     int printed = 0;
     if (c->n_alleles == 2 && c->strand_bias != -1) { fprintf(out, "FS=%d", c->strand_bias); printed = 1; }
-    if (c->n_alleles == 3) { fprintf(out, "%sTYPE=MULTISNV", printed ? ";" : ""); printed = 1; }
+    if (c->embedded) { fprintf(out, "%sTYPE=EMBEDDED", printed ? ";" : ""); printed = 1; }
+    else if (c->n_alleles == 3) { fprintf(out, "%sTYPE=MULTISNV", printed ? ";" : ""); printed = 1; }
     if (!printed) fprintf(out, ".");
     fprintf(out, "\tGT:PL:GQ:DP:BSDP:ACN\t");
     int ploidy = c->ploidy;
@@ -724,6 +745,9 @@ typedef struct {
     ngo_known* known;          /* -knownVariants (sequence order, then position, input order kept) */
     int n_known, known_next;   /* known_next: nextSIVIndex over the whole list */
     ngo_acalls acalls;         /* ploidy >= 3: the position's allele calls in pending order */
+    int realign;               /* IndelRealignerPileupListener active (single-sample discovery, ploidy < 3) */
+    int last_indel_end;        /* SingleSampleVariantPileupListener.lastIndelEnd, :143 */
+    ngo_alist pileup;          /* the position's alignments (PileupRecord.getAlignments) */
 } ngo_gen;
 
 /* ------------------------------------------------------------------ */
@@ -851,9 +875,13 @@ static void rac_print(FILE* out, const ngo_rac* R) {
     }
 }
 
+static void free_indel_call(struct ngo_indel_call_s* c);
 static void on_sequence_end(ngo_gen* G) {
     /* SingleSampleVariantsDetector.saveSequenceVariants, :933-968: calls are already in position order */
-    for (int i = 0; i < G->calls.n; i++) print_call(G->out, G->g->s[G->cur_seq].name, &G->calls.c[i]);
+    for (int i = 0; i < G->calls.n; i++) {
+        print_call(G->out, G->g->s[G->cur_seq].name, &G->calls.c[i]);
+        if (G->calls.c[i].indel) free_indel_call(G->calls.c[i].indel);
+    }
     G->st->variants_called += G->calls.n;
     G->calls.n = 0;
 }
@@ -1444,6 +1472,68 @@ static void mvd_on_pileup(ngo_gen* G, int pos) {
     G->st->variants_called++;
 }
 
+#include "ngsep_oracle_indel.inc"
+struct ngo_indel_call_s { ngo_indel_call c; int ploidy; };
+static void free_indel_call(struct ngo_indel_call_s* c) { for (int i = 0; i < c->c.n; i++) free(c->c.alleles[i]); free(c); }
+static void print_indel_call_any(FILE* out, const char* seqName, const ngo_call* c) { print_indel_call(out, seqName, &c->indel->c, c->indel->ploidy); }
+
+static void push_call(ngo_gen* G, const ngo_call* c) {
+    if (G->calls.n == G->calls.cap) { G->calls.cap = G->calls.cap ? 2 * G->calls.cap : 1024; G->calls.c = realloc(G->calls.c, sizeof(ngo_call) * G->calls.cap); }
+    G->calls.c[G->calls.n++] = *c;
+}
+
+/* SingleSampleVariantPileupListener.onPileup (no input variants, :146-161) -> calculateReferenceAlleleDiscovery
+ * (:191-206) -> discoverVariant (:213-232) with the pileup's reference span from the indel realigner: span 1 is
+ * discoverSNV over `h`, a longer span discoverVariantWithSpan (:257-273) */
+static void discover_with_span(ngo_gen* G, int pos, int span, int is_str, int is_new_str, const ngo_counts* h) {
+    const ngo_params* p = G->p;
+    const ngo_seq* s = &G->g->s[G->cur_seq];
+    const int is_input_str = is_str && !is_new_str;
+    int embedded = 0;
+    if (is_input_str && pos >= G->last_indel_end) G->last_indel_end = pos + span - 1;
+    else if (pos <= G->last_indel_end) embedded = 1;
+    if (!p->call_embedded && embedded) return;
+    const int last = pos + span - 1;
+    if (pos < 1 || last > s->len) return;                       /* getReference -> null */
+    if (p->ignore_lowercase_ref && islower((unsigned char)s->seq[pos - 1])) return;
+    int eff = embedded ? 1 : span;
+    ngo_call c;
+    if (eff > 1) {
+        int lr = 0;
+        char* ref = ref_upper(s, pos, last, &lr);
+        ngo_icalls calls = {0};
+        pileup_calls(G->pileup.a, G->pileup.n, pos, eff, &calls);
+        ngo_sv alleles = {0};
+        cluster_allele_calls(&calls, ref, p->max_base_qs, &alleles);
+        ngo_icounts ih;
+        icounts_run(&ih, &alleles, &calls, p->max_base_qs, 0.5);
+        struct ngo_indel_call_s* ic = calloc(1, sizeof(*ic));
+        const int ok = call_indel(&ih, &alleles, pos, is_str, is_input_str, G->het_rate, p->min_quality, p->ploidy, &ic->c);
+        free(ih.counts); free(ih.logc);
+        sv_free(&alleles);
+        icalls_free(&calls);
+        free(ref);
+        if (ok) {
+            memset(&c, 0, sizeof(c));
+            c.pos = pos;
+            ic->ploidy = p->ploidy;
+            c.indel = ic;
+            push_call(G, &c);
+            G->last_indel_end = ic->c.last;                     /* a decided non-SNV call, :157-160 */
+            return;
+        }
+        free(ic);
+        if (is_input_str) return;
+    }
+    /* discoverSNV (also the fallback of a span whose indel alleles made no call, :264-271) */
+    char R = (char)toupper((unsigned char)s->seq[pos - 1]);
+    if (discover_snv(h, pos, R, p, G->het_rate, &c)) {
+        c.embedded = embedded;
+        c.indel = NULL;
+        push_call(G, &c);
+    }
+}
+
 /* processCurrentPosition + listeners for one position, AlignmentsPileupGenerator.java:475-498 */
 static int process_current_position(ngo_gen* G) {
     if (G->pending.n == 0) { G->cur_pos++; return 0; }
@@ -1491,6 +1581,16 @@ static int process_current_position(ngo_gen* G) {
         return numAlignments > 0;
     }
     int numAlignments = 0;
+    int span = 1, is_str = 0, is_new_str = 0;
+    if (G->realign) {
+        /* IndelRealignerPileupListener.onPileup runs first and may edit the alignments (:85-126) */
+        G->pileup.n = 0;
+        for (int k = 0; k < G->pending.n; k++) {
+            ngo_aln* a = G->pending.a[k];
+            if (a->first <= pos && a->last >= pos) alist_push(&G->pileup, a);
+        }
+        if (G->pileup.n > 0) span = realigner_on_pileup(&G->g->s[G->cur_seq], G->pileup.a, G->pileup.n, pos, &is_str, &is_new_str);
+    }
     ngo_counts h;
     ngo_counts_init(&h, 4, 0.5, p->max_base_qs);     /* CountsHelper.calculateCountsSNV(calls, maxBaseQS, 0.5) */
     const int pool = p->ploidy >= 3;                 /* SingleSampleVariantPileupListener.DEF_MIN_PLOIDY_POOL_ALGORITHM */
@@ -1532,6 +1632,8 @@ static int process_current_position(ngo_gen* G) {
                 if (G->calls.n == G->calls.cap) { G->calls.cap = G->calls.cap ? 2 * G->calls.cap : 1024; G->calls.c = realloc(G->calls.c, sizeof(ngo_call) * G->calls.cap); }
                 G->calls.c[G->calls.n++] = c;
             }
+        } else if (G->realign) {
+            discover_with_span(G, pos, span, is_str, is_new_str, &h);
         } else if (!(p->ignore_lowercase_ref && islower((unsigned char)r))) {
             char R = (char)toupper((unsigned char)r);
             ngo_call c;
@@ -1614,6 +1716,7 @@ static void process_alignment(ngo_gen* G, ngo_aln* a) {
     if (G->cur_seq < 0) {   /* startSequence, :435-444 */
         G->cur_seq = a->seq; G->cur_pos = a->first; G->cur_last = a->last;
         if (G->rac) rac_on_sequence_start(G, a->seq);
+        G->last_indel_end = 0;                                 /* SingleSampleVariantPileupListener.onSequenceStart, :186 */
         if (G->known) {          /* onSequenceStart: this sequence's input variants, nextSIVIndex = 0 */
             G->known_next = 0;
             while (G->known_next < G->n_known && G->known[G->known_next].seq != a->seq) G->known_next++;
@@ -1715,6 +1818,7 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
     if (!multisample && !p->het_rate_set && p->ploidy == 1) G.het_rate = 1e-6;
     G.cov = cov;
     G.rac = rac;
+    G.realign = !multisample && !cov && !rac && !p->indel_passthrough && p->ploidy < 3 && !(p->known_vcf && p->known_vcf[0]);
     if (p->known_vcf && p->known_vcf[0]) {
         if (load_known(p->known_vcf, &g, &G.known, &G.n_known) != NGO_OK) {
             fclose(in); if (out != stdout) fclose(out); if (dump) fclose(dump);
@@ -1865,7 +1969,9 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
             } else if (query_found) { aln_free(a); break; }
             else { aln_free(a); continue; }
         }
-        if (a->has_indel && !cov && !rac && !p->indel_passthrough) { G.unsupported = 1; aln_free(a); rc = NGO_UNSUPPORTED; break; }
+        /* reads with I/D: the indel realigner + indel discovery run for single-sample discovery at ploidy < 3; the
+         * other listener chains with indels are outside this restatement (or pass-through on request) */
+        if (a->has_indel && !cov && !rac && !p->indel_passthrough && !G.realign) { G.unsupported = 1; aln_free(a); rc = NGO_UNSUPPORTED; break; }
         process_alignment(&G, a);
     }
     if (multisample && !header_done) { header_done = 1; print_header_samples(out, p, NULL, 0); }
@@ -1883,7 +1989,8 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
     for (int i = 0; i < G.pending.n; i++) aln_free(G.pending.a[i]);
     for (int i = 0; i < G.ss_primary.n; i++) aln_free(G.ss_primary.a[i]);
     for (int i = 0; i < G.ss_secondary.n; i++) aln_free(G.ss_secondary.a[i]);
-    free(G.pending.a); free(G.ss_primary.a); free(G.ss_secondary.a); free(G.retired.a); free(G.calls.c); free(G.acalls.c);
+    for (int i = 0; i < G.calls.n; i++) if (G.calls.c[i].indel) free_indel_call(G.calls.c[i].indel);
+    free(G.pending.a); free(G.ss_primary.a); free(G.ss_secondary.a); free(G.retired.a); free(G.calls.c); free(G.acalls.c); free(G.pileup.a);
     for (int i = 0; i < G.n_known; i++) free(G.known[i].id);
     free(G.known);
     for (int i = 0; i < g.n; i++) { free(g.s[i].name); free(g.s[i].seq); }
