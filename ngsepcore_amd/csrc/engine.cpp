@@ -87,7 +87,6 @@ void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g) {
     // the bounds prove SNVQ hom-ref calls; the pool algorithm only needs a valid non-reference call (its
     // variant needs an alternative allele count >= 1, createSNVVariantPool :313-320), the scan's candidate test
     g->use_bound = ok && !g->dump_all && std::isfinite(t_het) && g->ploidy < 3 ? 1 : 0;
-    g->exact_bound = std::getenv("NGSEP_KT_EXACT") != nullptr ? 1 : 0;
     // count bound: a valid call carries q in [4, 30] (engine.hpp code), capped at max_q in the kernel
     t->c_r1 = t->c_r2 = INT64_MAX;
     t->c_x1 = t->c_x2 = 0;
@@ -1189,8 +1188,10 @@ static int build_single_layout(Staged& s, const std::vector<SRead>& reads, Layou
 
 // Read-group layout (engine.hpp RGroup): the variant caller's device input.  The reads'
 // projected bytes are the ones the host packer produced (one code byte per reference position of the read,
-// pending-list order); here they are only regrouped so that the scan's loads coalesce: 64 consecutive reads per
-// group, interleaved in 8-byte units.  Headers: global first / last position and the strand bit.  The two
+// pending-list order), stored relative to the reference (code ^ reference code, as CRAM stores bases against the
+// reference): KL then needs no reference in its stream, and a gather restores the code with one byte per
+// position.  Regrouped so that the scan's loads coalesce: 64 consecutive reads per group, interleaved in 8-byte
+// units.  Headers: global first / last position and the strand bit.  The two
 // block tables give the scan its tile's entry range and the column gather the entries that can cover a
 // position.  Groups are independent: built on all host threads.
 static int build_rg_layout(Staged& s, const std::vector<SRead>& reads, LayoutArena& arena, bool exact) {
@@ -1237,16 +1238,23 @@ static int build_rg_layout(Staged& s, const std::vector<SRead>& reads, LayoutAre
                 const int64_t span = std::max<int64_t>(0, (int64_t)rd.glast - rd.gfirst + 1);
                 s.h_rh[(size_t)(2 * e)] = rd.gfirst;
                 s.h_rh[(size_t)(2 * e + 1)] = (int32_t)((uint32_t)(span > 0 ? rd.glast : rd.gfirst - 1) | (rd.neg ? 0x80000000u : 0u));
+                // reference-relative bytes: code ^ the position's reference code (0: a valid reference call of
+                // quality 0 -- what the padding past the read's end holds, never an exception in KL)
+                const uint8_t* rf = s.h_ref.data() + rd.gfirst;
                 const int64_t whole = span / 8;
                 for (int64_t k = 0; k < whole; k++) {
-                    uint64_t u;
+                    uint64_t u, r;
                     std::memcpy(&u, rd.bytes + 8 * k, 8);
-                    dst[k * 64] = u;
+                    std::memcpy(&r, rf + 8 * k, 8);
+                    dst[k * 64] = u ^ r;
                 }
                 int64_t k = whole;
                 if (span % 8) {
-                    uint64_t u = 0;
-                    std::memcpy(&u, rd.bytes + 8 * k, (size_t)(span % 8));
+                    uint8_t b8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                    const int64_t rem = span % 8;
+                    for (int64_t t = 0; t < rem; t++) b8[t] = (uint8_t)(rd.bytes[8 * k + t] ^ rf[8 * k + t]);
+                    uint64_t u;
+                    std::memcpy(&u, b8, 8);
                     dst[k * 64] = u;
                     k++;
                 }

@@ -59,8 +59,9 @@ constexpr int kRunAlign = 4096;            // a run's global coordinate is a who
 
 // Read-group layout of the single-sample variant caller: the admitted reads of a run
 // in pending-list order are its entries; 64 consecutive entries form a group, and the group's reads'
-// projected code bytes (one per reference position of [gfirst, glast]) are interleaved in 8-byte units:
-// unit k of entry 64 g + l is units[base_g + 64 k + l] (bytes 8k .. 8k+7 of the read, zero past its end).
+// projected code bytes (one per reference position of [gfirst, glast]), each XOR-ed with its position's
+// reference code (reference-relative: 0 is a valid reference call of quality 0), are interleaved in 8-byte
+// units: unit k of entry 64 g + l is units[base_g + 64 k + l] (bytes 8k .. 8k+7 of the read, zero past its end).
 // A wavefront that reads unit k of its 64 reads loads 512 contiguous bytes.  Entry header: {gfirst,
 // glast | negative-strand << 31}; padding entries are empty (glast = gfirst - 1, gfirst = the last real one).
 struct RGroup {
@@ -135,15 +136,13 @@ struct GenotypeParams {
     int32_t min_quality;       // -minQuality
     int32_t dump_all;          // emit a record for every position with DP>0
     int32_t ablate;            // diagnostics only (env NGSEP_ABLATE): 1 scan only (no bound, no queue),
-                               // 4 no tiles, 8 tally without posterior, 16 posterior kernel reads the queue only,
-                               // 32 population kernel gathers only, 64 population kernel stops after the tallies
+                               // 8 tally without posterior, 16 posterior kernel reads the queue only,
+                               // 32 population kernel gathers only, 64 population kernel stops after the tallies,
+                               // 128 KL without the exception counters, 256 KL without the read bases
     int32_t use_bound;         // 1: candidates proven hom-ref by the integer bound are dropped in the tile kernel
     int32_t full_records;      // 1: every record whole (ngsep_params.full_records); dump mode implies it
     int32_t ploidy;            // >= 3: KP runs the pool algorithm (k_posterior_pool), KT queues every
                                // position with a valid non-reference call (the pool variant needs one)
-    int32_t exact_bound;       // bit-plane KT: 1 applies the exact integer bound to count-bound survivors
-                               // (env NGSEP_KT_EXACT=1); 0 queues them for KP (measured: the exact
-                               // bound dropped 4% of them on the 30x headline and cost 30% of KT)
 };
 
 struct Window {            // a contiguous range of one sequence, resident in HBM

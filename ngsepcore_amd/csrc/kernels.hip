@@ -44,9 +44,17 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 struct QueueSite;
 struct SiteQ;
 
+// counter set of a single-sample run: [0] records | fullest bucket << 40, [1] candidates (KQ), [2] KP's queue
+// length, [3] spare, [4] whole records, [5] column space reserved by KG (units of 4 entries), then KL's shards:
+// shard t at kCtrShard0 + kCtrShardStride t = {queue sites, column space, candidates} (one 128-B line each)
+constexpr int kKlShards = 64;
+constexpr int kCtrShard0 = 8, kCtrShardStride = 16;
+constexpr int kCtrWords = kCtrShard0 + kCtrShardStride * kKlShards;
+
 struct RunSlot {                     // one in-flight single-sample run (see device_submit)
     hipStream_t stream = nullptr;            // its compute stream (runs of the two slots overlap)
-    SiteQ* d_hard = nullptr;                 // KL (KQ, -knownVariants) -> KG -> KP queue
+    SiteQ* d_hard = nullptr;                 // KL (KQ, -knownVariants) -> KG queue (KL: kKlShards segments)
+    SiteQ* d_hard2 = nullptr;                // KG -> KP queue (compact)
     int64_t cap_hard = 0;
     uint16_t* d_cols = nullptr;              // the queued sites' columns (KL / KG -> KP), u16 entries
     int64_t cap_cols = 0;
@@ -60,8 +68,7 @@ struct RunSlot {                     // one in-flight single-sample run (see dev
     bool tables_valid = false;
     SiteRec* d_sorted = nullptr;
     int64_t cap = 0;
-    unsigned long long* d_ctr = nullptr;     // its counter set (8): records | fullest bucket, candidates, queue,
-                                             // exact-bound passes, whole records
+    unsigned long long* d_ctr = nullptr;     // its counter set (kCtrWords, see above)
     unsigned long long* h_ctr = nullptr;     // pinned copy
     SiteSet host;                            // pinned D2H destination of the ordered records and the whole ones
     hipEvent_t ev[6] = {};                   // KT start, KT end, KP end, after KO, copies done, KP start
@@ -802,16 +809,18 @@ __global__ __launch_bounds__(kPostThreads) void k_posterior_pool(const SiteQ* __
 // reads (engine.hpp RGroup: 1 B per read base, 8 B per read header):
 //   * coverage: every read segment inside the tile adds +1 / -1 to an LDS difference array (2 atomics per read);
 //   * exceptions: a wave takes a group of 64 reads, lane = read, and streams its 8-byte units (512 contiguous
-//     bytes per wave load); a byte is an exception when its position is callable and it is not a valid call of
-//     the reference allele (SWAR against the tile's reference codes in LDS).  Exceptions (a few % of the bytes)
-//     add to the position's LDS counter: low word = exceptions, high word = valid calls of another allele (na);
+//     bytes per wave load, kKlUnroll loads in flight per lane); a byte is an exception when its position is
+//     callable and it is not a valid call of the reference allele (SWAR against the tile's reference codes in
+//     LDS).  Exceptions (a few % of the bytes) add to the position's LDS counter: low half = exceptions, high
+//     half = valid calls of another allele (na);
 //   * candidates: callable positions with na > 0; the reference calls are nr = coverage - exceptions, and the
-//     count bound (table cb_nr) drops those whose counts prove them hom-ref;
-//   * survivors: their columns (PileupRecord.getAlleleCalls(1) order) are gathered from the layout by the
-//     workgroup (wave_gather, L2-warm) into the column buffer, and queued for KP.
+//     count bound (table cb_nr) drops those whose counts prove them hom-ref.  A position
+//     deeper than 65535 reads (the halves could carry into each other) is queued whenever it is callable;
+//   * survivors: queued for KP with their column space reserved (rows = -3 - coverage); KG gathers the columns.
+//     The workgroup's queue slots and column space come from one atomic each (a block scan orders them).
 // No MFMA: byte SWAR and integer counters.
 constexpr int kKlThreads = 256;
-constexpr int kKlSurv = 128;            // survivors one workgroup gathers (more: queued without a column, KG does them)
+constexpr int kKlUnroll = 8;
 
 // PileupRecord.getAlleleCalls(1) at global position p over the read-group layout: the nonzero codes of the reads
 // covering p, in pending-list (entry) order, as u16 entries code | negative strand << 8 (WRITE), one wave.  e0 is
@@ -819,11 +828,13 @@ constexpr int kKlSurv = 128;            // survivors one workgroup gathers (more
 template <bool WRITE>
 __device__ inline int32_t wave_gather(int32_t p, int64_t e0, int64_t n_entries, const int2* __restrict__ rh,
                                       const RGroup* __restrict__ grp, const uint64_t* __restrict__ units,
-                                      uint16_t* __restrict__ dst, int32_t* cov_out) {
+                                      uint32_t refcode, uint16_t* __restrict__ dst, int32_t* cov_out) {
     const int lane = threadIdx.x & 63;
     int32_t n = 0, cov = 0;
-    for (int64_t e = e0 & ~(int64_t)63; e < n_entries; e += 64) {
-        const int2 h = rh[e + lane];                        // (n_entries is a multiple of 64)
+    int64_t e = e0 & ~(int64_t)63;
+    int2 h = e < n_entries ? rh[e + lane] : make_int2(0x7FFFFFFF, 0);
+    for (; e < n_entries; e += 64) {
+        const int2 hn = e + 64 < n_entries ? rh[e + 64 + lane] : make_int2(0x7FFFFFFF, 0);   // next chunk in flight
         const int32_t gf = h.x, gl = h.y & 0x7FFFFFFF;
         const bool covers = gf <= p && p <= gl;
         cov += (int32_t)__popcll(__ballot(covers));
@@ -833,7 +844,7 @@ __device__ inline int32_t wave_gather(int32_t p, int64_t e0, int64_t n_entries, 
                 const RGroup G = grp[e >> 6];
                 const int32_t o = p - gf;
                 const uint64_t u = units[G.base + (int64_t)(o >> 3) * 64 + lane];
-                code = (uint32_t)(u >> (8 * (o & 7))) & 0xFFu;
+                code = ((uint32_t)(u >> (8 * (o & 7))) & 0xFFu) ^ refcode;   // (the layout is reference-relative)
             }
             const unsigned long long m = __ballot(code != 0);
             if (code) {
@@ -843,113 +854,140 @@ __device__ inline int32_t wave_gather(int32_t p, int64_t e0, int64_t n_entries, 
             n += (int32_t)__popcll(m);
         }
         if (__ballot(gf > p)) break;                       // entries are sorted by gfirst: none later covers p
+        h = hn;
     }
     if (cov_out) *cov_out = cov;
     return n;
 }
 
-__device__ __forceinline__ uint32_t kl_exc(uint32_t x, uint32_t r) {
-    // bit 7 of byte k: the position is callable (r has bit 7) and byte k is not a valid call of r's allele
-    const uint32_t t = ((x ^ r) >> 5) & 0x07070707u;
-    return ((t + 0x7F7F7F7Fu) & 0x80808080u) & r;
+// KL's flags from reference-relative bytes y = code ^ reference code (bit 7 of byte k):
+__device__ __forceinline__ uint32_t kl_exc(uint32_t y) {
+    // not a valid call of the reference's allele (bits 5-7 differ); at a callable position an exception
+    return ((((y >> 5) & 0x07070707u) + 0x7F7F7F7Fu) & 0x80808080u);
 }
-__device__ __forceinline__ uint32_t kl_nonref(uint32_t x, uint32_t r) {
-    // bit 7 of byte k: a valid call (x bit 7) of another allele than the callable reference r
-    const uint32_t al = ((x ^ r) >> 5) & 0x03030303u;
-    return ((al + 0x7F7F7F7Fu) & 0x80808080u) & r & x;
+__device__ __forceinline__ uint32_t kl_nonref(uint32_t y) {
+    // a valid call (code bit 7 = reference bit 7) of another allele (bits 5-6 differ)
+    return ((((y >> 5) & 0x03030303u) + 0x7F7F7F7Fu) & ~y & 0x80808080u);
 }
 
-template <int T>
-__global__ __launch_bounds__(kKlThreads) void k_read_scan(
-    const uint64_t* __restrict__ units, const int2* __restrict__ rh, const RGroup* __restrict__ grp,
-    const int32_t* __restrict__ blkA, const int32_t* __restrict__ blkB, int64_t n_entries,
-    const uint8_t* __restrict__ ref, const LikTables* __restrict__ tabs, GenotypeParams gp,
-    SiteQ* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap,
-    uint16_t* __restrict__ cols, int64_t col_cap, int32_t* __restrict__ bcount, int64_t nb) {
-    constexpr int PT = T / kKlThreads;                 // positions per thread in the candidate phase
-    __shared__ int32_t s_diff[T + 1];
-    __shared__ unsigned long long s_cnt[T];
-    __shared__ uint32_t s_ref[T / 4 + 4];              // tile position i's reference code at byte 8 + i; 8 zero bytes each side
-    __shared__ int16_t s_cb[256];
-    __shared__ int32_t s_sp[kKlSurv], s_scov[kKlSurv], s_src[kKlSurv], s_coff[kKlSurv];
-    __shared__ int32_t s_nsurv, s_wsum[kKlThreads / 64];
-    __shared__ unsigned long long s_colbase, s_qbase, s_ncand[kKlThreads / 64];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int32_t tstart = (int32_t)((int64_t)blockIdx.x * T);
-    for (int64_t i = (int64_t)blockIdx.x * kKlThreads + tid; i < nb; i += (int64_t)gridDim.x * kKlThreads) bcount[i] = 0;
-    for (int i = tid; i <= T; i += kKlThreads) s_diff[i] = 0;
-    for (int i = tid; i < T; i += kKlThreads) s_cnt[i] = 0;
-    {
-        const uint32_t* r32 = reinterpret_cast<const uint32_t*>(ref + tstart);
-        for (int i = tid; i < T / 4; i += kKlThreads) s_ref[2 + i] = r32[i];
-        if (tid < 4) s_ref[tid < 2 ? tid : T / 4 + tid] = 0;
-    }
-    s_cb[tid] = tabs->cb_nr[tid];
-    if (tid == 0) s_nsurv = 0;
-    const int64_t e_lo = blkA[tstart >> kRgBlockShift], e_hi = blkB[(tstart + T) >> kRgBlockShift];
-    __syncthreads();
-    // ---- coverage and exceptions: wave w takes groups g_lo + w, g_lo + w + 4, ...
+// KL's read stream over the tile's groups (wave w: groups g_lo + w, g_lo + w + 4, ...).  A lane takes its read's
+// units from the first one inside the tile, kKlUnroll loads in flight; the bytes are reference-relative
+// (engine.hpp RGroup), so the stream reads no reference and no LDS: its counter adds never hold it up.
+//   !DEEP: per position a 16-bit counter, exceptions in the low byte, other-allele calls in the high byte; a
+//          unit's 8 positions take five 32-bit LDS adds -- exact while no position of the tile is deeper than
+//          255 reads (the kernel checks, and reruns the stream DEEP).  Counter of tile position i: halfword 8 + i;
+//   DEEP:  one 32-bit counter per position (exceptions | other-allele << 16) at word 8 + i, one add per exception.
+// Counts at positions outside the tile (margins) are never read; they are bounded by the tile's own depth (a read
+// that reaches them covers the tile's first or last position), so they cannot carry into the tile's counters.
+template <int T, bool DEEP, int U>
+__device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, const int2* __restrict__ rh,
+                                          const RGroup* __restrict__ grp, int64_t e_lo, int64_t e_hi, int32_t tstart,
+                                          int32_t* s_diff, uint32_t* s_cnt, bool do_diff, int32_t ablate, uint32_t& sink) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t g_lo = e_lo >> 6, g_hi = (e_hi + 63) >> 6;
-    for (int64_t g = g_lo + wv; g < g_hi; g += kKlThreads / 64) {
+    const bool no_counts = (ablate & 128) != 0, no_units = (ablate & 256) != 0;   // diagnostics
+    int64_t g = g_lo + wv;
+    int2 h = g < g_hi ? rh[g * 64 + lane] : make_int2(0, 0);
+    for (; g < g_hi; g += kKlThreads / 64) {
         const int64_t e = g * 64 + lane;
-        const int2 h = rh[e];
+        const int2 hn = g + kKlThreads / 64 < g_hi ? rh[e + kKlThreads] : make_int2(0, 0);   // the next group's headers in flight
         const int32_t gf = h.x, gl = h.y & 0x7FFFFFFF;
         const int32_t a = max(gf, tstart), b = min(gl, tstart + T - 1);
         const bool act = e >= e_lo && e < e_hi && a <= b;
-        if (act) {
+        if (do_diff && act) {
             atomicAdd(&s_diff[a - tstart], 1);
             atomicAdd(&s_diff[b - tstart + 1], -1);
         }
         const RGroup G = grp[g];
-        const int32_t k0 = act ? (a - gf) >> 3 : 0x7FFFFFFF, k1 = act ? (b - gf) >> 3 : -1;
-        int32_t kmin = k0, kmax = k1;
+        const int32_t k0 = act ? (a - gf) >> 3 : 0, kn = act && !no_units ? ((b - gf) >> 3) - k0 : -1;   // units k0 .. k0 + kn
+        const int32_t ob0 = gf - tstart + 8 * k0 + 8;     // counter index of unit k0's byte 0 (>= 1)
+        const int sh = (ob0 & 1) << 1;                    // !DEEP: byte offset of the unit's first halfword
+        const uint64_t* ub = units + G.base + lane + (int64_t)k0 * 64;
+        // a lane's own trip count (the wave runs while any lane has units left); loads are unconditional (a
+        // batch's slots past the read's last unit repeat it) so that each unit waits for its own load only
+        for (int32_t j = 0; j <= kn; j += U) {
+            uint64_t u[U];
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            kmin = min(kmin, __shfl_xor(kmin, o, 64));
-            kmax = max(kmax, __shfl_xor(kmax, o, 64));
+            for (int i = 0; i < U; i++) u[i] = ub[(int64_t)min(j + i, kn) * 64];
+#pragma unroll
+            for (int i = 0; i < U; i++) {
+                if (j + i > kn) continue;
+                const uint32_t ylo = (uint32_t)u[i], yhi = (uint32_t)(u[i] >> 32);
+                const uint32_t elo = kl_exc(ylo), ehi = kl_exc(yhi);
+                if (no_counts) { sink += elo + ehi + kl_nonref(ylo) + kl_nonref(yhi); continue; }
+                if (!(elo | ehi) && !(ablate & 2048)) continue;   // (2048, diagnostics: every lane adds)
+                const uint32_t nlo = kl_nonref(ylo), nhi = kl_nonref(yhi);
+                const int32_t ob = ob0 + 8 * (j + i);     // counter index of the unit's byte 0
+                if (!DEEP) {
+                    // (exception, other-allele) byte pairs of the 8 positions, then shifted to the halfword
+                    const uint32_t fl = elo >> 7, fh = ehi >> 7, ml = nlo >> 7, mh = nhi >> 7;
+                    const uint32_t w0 = __builtin_amdgcn_perm(ml, fl, 0x05010400u), w1 = __builtin_amdgcn_perm(ml, fl, 0x07030602u);
+                    const uint32_t w2 = __builtin_amdgcn_perm(mh, fh, 0x05010400u), w3 = __builtin_amdgcn_perm(mh, fh, 0x07030602u);
+                    uint32_t* c = s_cnt + ((ob + 1) >> 1) - 1;   // sh = 0: the first add is of 0
+                    if (ablate & 512) {                   // diagnostics: stores instead of adds
+                        c[0] = __builtin_amdgcn_alignbyte(w0, 0u, sh);
+                        c[1] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+                        c[2] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+                        c[3] = __builtin_amdgcn_alignbyte(w3, w2, sh);
+                        c[4] = __builtin_amdgcn_alignbyte(0u, w3, sh);
+                        continue;
+                    }
+                    if (ablate & 1024) { atomicAdd(c, w0 + w1 + w2 + w3); continue; }   // diagnostics: one add
+                    if ((ablate & 8192) && i != 0) continue;   // diagnostics: a batch's first unit only
+                    if (ablate & 16384) { sink += atomicAdd(c, w0 + w1 + w2 + w3); continue; }   // diagnostics: returning add
+                    atomicAdd(c, __builtin_amdgcn_alignbyte(w0, 0u, sh));
+                    atomicAdd(c + 1, __builtin_amdgcn_alignbyte(w1, w0, sh));
+                    atomicAdd(c + 2, __builtin_amdgcn_alignbyte(w2, w1, sh));
+                    atomicAdd(c + 3, __builtin_amdgcn_alignbyte(w3, w2, sh));
+                    atomicAdd(c + 4, __builtin_amdgcn_alignbyte(0u, w3, sh));
+                } else {
+                    uint64_t ex = (uint64_t)elo | (uint64_t)ehi << 32;
+                    const uint64_t nr = (uint64_t)nlo | (uint64_t)nhi << 32;
+                    while (ex) {
+                        const int bit = __builtin_ctzll(ex);
+                        ex &= ex - 1ull;
+                        atomicAdd(&s_cnt[ob + (bit >> 3)], 1u + ((uint32_t)(nr >> bit) & 1u) * 0x10000u);
+                    }
+                }
+            }
         }
-        const uint64_t* ub = units + G.base + lane;
-        const int32_t o0 = gf - tstart, lastb = gl - gf;   // tile position of the read's byte 0, its last byte index
-        auto unit = [&](uint64_t u, int32_t kk) {
-            const int32_t o = o0 + 8 * kk;                  // tile position of the unit's byte 0 (-7 .. T-1)
-            const int32_t ob = o + 8;
-            const int w = ob >> 2, sh = ob & 3;
-            const uint32_t r0 = s_ref[w], r1 = s_ref[w + 1], r2 = s_ref[w + 2];
-            const uint32_t rlo = __builtin_amdgcn_alignbyte(r1, r0, sh), rhi = __builtin_amdgcn_alignbyte(r2, r1, sh);
-            const uint32_t ulo = (uint32_t)u, uhi = (uint32_t)(u >> 32);
-            uint32_t elo = kl_exc(ulo, rlo), ehi = kl_exc(uhi, rhi);
-            const int32_t lb = lastb - 8 * kk;             // the read's last byte in this unit (>= 0)
-            if (lb < 7) {                                   // zero padding past the read's end
-                if (lb < 3) elo &= (1u << (8 * (lb + 1))) - 1u;
-                ehi = lb < 4 ? 0u : ehi & ((1u << (8 * (lb - 3))) - 1u);
-            }
-            if (!(elo | ehi)) return;
-            const uint32_t nlo = kl_nonref(ulo, rlo), nhi = kl_nonref(uhi, rhi);
-            while (elo) {
-                const int bit = __builtin_ctz(elo);
-                elo &= elo - 1u;
-                atomicAdd(&s_cnt[o + (bit >> 3)], 1ull + ((unsigned long long)((nlo >> bit) & 1u) << 32));
-            }
-            while (ehi) {
-                const int bit = __builtin_ctz(ehi);
-                ehi &= ehi - 1u;
-                atomicAdd(&s_cnt[o + 4 + (bit >> 3)], 1ull + ((unsigned long long)((nhi >> bit) & 1u) << 32));
-            }
-        };
-        for (int32_t k = kmin; k <= kmax; k += 4) {
-            uint64_t u[4];
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int32_t kk = k + i;
-                u[i] = (kk >= k0 && kk <= k1) ? ub[(int64_t)kk * 64] : 0ull;
-            }
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-                if (k + i >= k0 && k + i <= k1) unit(u[i], k + i);
-        }
+        h = hn;
     }
+}
+
+template <int T, int U>
+__global__ __launch_bounds__(kKlThreads) void k_read_scan(
+    const uint64_t* __restrict__ units, const int2* __restrict__ rh, const RGroup* __restrict__ grp,
+    const int32_t* __restrict__ blkA, const int32_t* __restrict__ blkB, int64_t n_entries,
+    const uint8_t* __restrict__ ref, const LikTables* __restrict__ tabs, GenotypeParams gp,
+    SiteQ* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qseg,
+    int64_t cseg4, int32_t* __restrict__ bcount, int64_t nb) {
+    constexpr int PT = T / kKlThreads;                 // positions per thread in the candidate phase
+    constexpr int NC = T + 24;                         // counter words (DEEP: one per position, margins 8 and 16)
+    static_assert(PT == 8, "candidate phase reads 16 bytes of counters per thread");
+    __shared__ int32_t s_diff[T + 1];
+    __shared__ alignas(16) uint32_t s_ref[T / 4];
+    __shared__ alignas(16) uint32_t s_cnt[NC];
+    __shared__ int16_t s_cb[256];
+    __shared__ int32_t s_wsum[kKlThreads / 64], s_wmax[kKlThreads / 64];
+    __shared__ unsigned long long s_wscan[kKlThreads / 64], s_ncand[kKlThreads / 64], s_colbase, s_qbase;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int32_t tstart = (int32_t)((int64_t)blockIdx.x * T);
+    (void)n_entries;
+    for (int64_t i = (int64_t)blockIdx.x * kKlThreads + tid; i < nb; i += (int64_t)gridDim.x * kKlThreads) bcount[i] = 0;
+    for (int i = tid; i <= T; i += kKlThreads) s_diff[i] = 0;
+    for (int i = tid; i < T / 2 + 16; i += kKlThreads) s_cnt[i] = 0;
+    {
+        const uint32_t* r32 = reinterpret_cast<const uint32_t*>(ref + tstart);
+        for (int i = tid; i < T / 4; i += kKlThreads) s_ref[i] = r32[i];
+    }
+    s_cb[tid] = tabs->cb_nr[tid];
+    const int64_t e_lo = blkA[tstart >> kRgBlockShift], e_hi = blkB[(tstart + T) >> kRgBlockShift];
     __syncthreads();
-    // ---- coverage (prefix of the difference array), candidates, the count bound
+    uint32_t sink = 0;
+    kl_stream<T, false, U>(units, rh, grp, e_lo, e_hi, tstart, s_diff, s_cnt, true, gp.ablate, sink);
+    __syncthreads();
+    // ---- coverage (prefix of the difference array)
     int32_t loc[PT];
     int32_t run = 0;
 #pragma unroll
@@ -964,94 +1002,158 @@ __global__ __launch_bounds__(kKlThreads) void k_read_scan(
     __syncthreads();
     int32_t off = incl - run;
     for (int w = 0; w < wv; w++) off += s_wsum[w];
-    const bool bound = gp.use_bound != 0;
-    uint32_t ncand = 0;
+    int32_t cmax = 0;
+#pragma unroll
+    for (int j = 0; j < PT; j++) { loc[j] += off; cmax = max(cmax, loc[j]); }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cmax = max(cmax, __shfl_xor(cmax, o, 64));
+    if (lane == 0) s_wmax[wv] = cmax;
+    __syncthreads();
+    const bool deep = max(max(s_wmax[0], s_wmax[1]), max(s_wmax[2], s_wmax[3])) > 255;
+    if (deep) {                                          // byte counters could carry: stream again, 32-bit counters
+        for (int i = tid; i < NC; i += kKlThreads) s_cnt[i] = 0;
+        __syncthreads();
+        kl_stream<T, true, U>(units, rh, grp, e_lo, e_hi, tstart, s_diff, s_cnt, false, gp.ablate, sink);
+        __syncthreads();
+    }
+    if (sink == 0xFFFFFFFFu) s_diff[0] = (int32_t)sink;   // keeps the diagnostics' work alive
+    // ---- candidates and the count bound
+    const bool bound = gp.use_bound != 0 && !(gp.ablate & 1);
+    const uint2 rw = *reinterpret_cast<const uint2*>(&s_ref[2 * tid]);
+    uint32_t ncand = 0, need_bits = 0;
+    uint64_t mine = 0;                                   // survivors << 40 | column space (units of 4 entries)
+    uint4 cw = make_uint4(0, 0, 0, 0);
+    if (!deep) cw = *reinterpret_cast<const uint4*>(&s_cnt[4 * tid + 4]);   // halfwords 8 tid + 8 ..
 #pragma unroll
     for (int j = 0; j < PT; j++) {
-        const int p = PT * tid + j;
-        const int32_t cov = off + loc[j];
-        const uint32_t rc = (s_ref[(p + 8) >> 2] >> (8 * ((p + 8) & 3))) & 0xFFu;
-        const unsigned long long cn = s_cnt[p];
-        const uint32_t exc = (uint32_t)cn, na = (uint32_t)(cn >> 32);
-        const bool cand = (rc & 0x80u) && na > 0;
-        ncand += cand ? 1u : 0u;
-        const bool need = cand && !(bound && na <= 255 && cov - (int32_t)exc >= (int32_t)s_cb[na]) && !(gp.ablate & 1);
-        if (need) {
-            const int slot = atomicAdd(&s_nsurv, 1);
-            if (slot < kKlSurv) {
-                s_sp[slot] = p;
-                s_scov[slot] = cov;
-                s_src[slot] = (int32_t)rc;
-            } else {                                        // past the workgroup's list: KG gathers it
-                const unsigned long long qi = atomicAdd(&counters[2], 1ull);
-                if ((int64_t)qi < qcap) queue[qi] = SiteQ{tstart + p, (int32_t)rc, 0, -1};
-            }
+        const int32_t cov = loc[j];
+        const uint32_t rc = ((j < 4 ? rw.x : rw.y) >> (8 * (j & 3))) & 0xFFu;
+        int32_t exc, na;
+        if (!deep) {
+            const uint32_t word = j < 2 ? cw.x : j < 4 ? cw.y : j < 6 ? cw.z : cw.w;
+            const uint32_t hw = word >> (16 * (j & 1));
+            exc = (int32_t)(hw & 0xFFu);
+            na = (int32_t)((hw >> 8) & 0xFFu);
+        } else {
+            const uint32_t cn = s_cnt[PT * tid + j + 8];
+            exc = (int32_t)(cn & 0xFFFFu);
+            na = (int32_t)(cn >> 16);
         }
+        bool need;
+        if (cov > 0xFFFF) {                              // (the 16-bit halves could carry)
+            need = (rc & 0x80u) != 0;
+            ncand += need ? 1u : 0u;
+        } else {
+            const bool cand = (rc & 0x80u) && na > 0;
+            ncand += cand ? 1u : 0u;
+            need = cand && !(bound && na <= 255 && cov - exc >= (int32_t)s_cb[na]);
+        }
+        if (gp.ablate & 1) need = false;
+        if (need) {
+            need_bits |= 1u << j;
+            mine += (1ull << 40) + (uint64_t)((cov + 3) >> 2);
+        }
+    }
+    // block scan of (survivors, column space): queue slots and column offsets in position order
+    uint64_t sc = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t v = __shfl_up(sc, o, 64);
+        if (lane >= o) sc += v;
     }
     unsigned long long nc = ncand;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) nc += __shfl_xor(nc, o, 64);
+    if (lane == 63) s_wscan[wv] = sc;
     if (lane == 0) s_ncand[wv] = nc;
     __syncthreads();
-    const int ns = min(s_nsurv, kKlSurv);
+    // the workgroup's queue slots and column space: one atomic each on its shard's counters (a counter that
+    // every workgroup adds to serializes them: ~88 adds per microsecond on one word)
+    const int shard = blockIdx.x % kKlShards;
+    unsigned long long* sctr = counters + kCtrShard0 + kCtrShardStride * shard;
     if (tid == 0) {
-        unsigned long long tnc = 0;
-        for (int w = 0; w < kKlThreads / 64; w++) tnc += s_ncand[w];
-        if (tnc) atomicAdd(&counters[1], tnc);
-        if (ns) {
-            int32_t tot = 0;                                // column offsets, in units of 4 entries
-            for (int i = 0; i < ns; i++) { s_coff[i] = tot; tot += (s_scov[i] + 3) >> 2; }
-            s_colbase = atomicAdd(&counters[5], (unsigned long long)tot);
-            s_qbase = atomicAdd(&counters[2], (unsigned long long)ns);
-        }
+        unsigned long long tnc = 0, tot = 0;
+        for (int w = 0; w < kKlThreads / 64; w++) { tnc += s_ncand[w]; tot += s_wscan[w]; }
+        if (tnc) atomicAdd(&sctr[2], tnc);
+        const unsigned long long ns = tot >> 40, c4 = tot & ((1ull << 40) - 1ull);
+        s_qbase = ns ? atomicAdd(&sctr[0], ns) : 0ull;
+        s_colbase = ns ? atomicAdd(&sctr[1], c4) : 0ull;
     }
-    if (ns == 0) return;
     __syncthreads();
-    // ---- the survivors' columns (one wave each; the tile's headers and units are in L2)
-    for (int i = wv; i < ns; i += kKlThreads / 64) {
-        const int32_t p = tstart + s_sp[i];
-        const int64_t c4 = (int64_t)s_colbase + s_coff[i];
-        int32_t rows = -2;
-        if ((c4 << 2) + s_scov[i] <= col_cap)
-            rows = wave_gather<true>(p, blkA[p >> kRgBlockShift], n_entries, rh, grp, units, cols + (c4 << 2), nullptr);
-        const int64_t qi = (int64_t)s_qbase + i;
-        if (lane == 0 && qi < qcap) queue[qi] = SiteQ{p, s_src[i], (int32_t)c4, rows};
+    if (!need_bits) return;
+    uint64_t ex = sc - mine;
+    for (int w = 0; w < wv; w++) ex += s_wscan[w];
+    int64_t qi = (int64_t)s_qbase + (int64_t)(ex >> 40);                        // in the shard's segment
+    int64_t c4 = (int64_t)s_colbase + (int64_t)(ex & ((1ull << 40) - 1ull));
+#pragma unroll
+    for (int j = 0; j < PT; j++) {
+        if (!((need_bits >> j) & 1u)) continue;
+        const int32_t cov = loc[j];
+        const uint32_t rc = ((j < 4 ? rw.x : rw.y) >> (8 * (j & 3))) & 0xFFu;
+        const int32_t rows = (c4 << 2) + cov <= (cseg4 << 2) ? -3 - cov : -2;   // -2: the shard's columns are full (rerun)
+        if (qi < qseg) queue[shard * qseg + qi] = SiteQ{tstart + PT * tid + j, (int32_t)rc, (int32_t)(shard * cseg4 + c4), rows};
+        qi++;
+        c4 += (cov + 3) >> 2;
     }
 }
 
-// KG: the columns of queued sites without one (-knownVariants, dump mode / no pruning, a KL workgroup's overflow):
-// one wave per site, a counting pass, a reservation in the column buffer, the gather
-__global__ __launch_bounds__(256) void k_gather_cols(SiteQ* __restrict__ queue, const unsigned long long* __restrict__ qn,
-                                                     int64_t qcap, const int2* __restrict__ rh, const RGroup* __restrict__ grp,
+// KG: the queued sites' columns, and the compact queue KP reads.  The input queue is nshard segments of qseg
+// entries (segment t holds qcnt[t * stride] sites: KL's shards; one segment otherwise); qout gets them in segment
+// order and counters[2] their number.  rows <= -3: space for -3 - rows entries reserved at coff (KL's survivors);
+// rows == -1: none reserved (-knownVariants, dump mode / no pruning): a counting pass and a reservation first.
+// One wave per site.
+__global__ __launch_bounds__(256) void k_gather_cols(const SiteQ* __restrict__ qin, const unsigned long long* __restrict__ qcnt,
+                                                     int stride, int nshard, int64_t qseg, SiteQ* __restrict__ qout,
+                                                     const int2* __restrict__ rh, const RGroup* __restrict__ grp,
                                                      const uint64_t* __restrict__ units, const int32_t* __restrict__ blkA,
+                                                     const uint8_t* __restrict__ ref,
                                                      int64_t n_entries, uint16_t* __restrict__ cols, int64_t col_cap,
                                                      unsigned long long* __restrict__ counters) {
+    __shared__ int64_t s_pre[kKlShards + 1];
     const int lane = threadIdx.x & 63;
-    int64_t n = (int64_t)*qn;
-    if (n > qcap) n = qcap;
+    if (threadIdx.x == 0) {
+        int64_t t = 0;
+        for (int k = 0; k < nshard; k++) {
+            s_pre[k] = t;
+            t += min((int64_t)qcnt[(int64_t)k * stride], qseg);
+        }
+        s_pre[nshard] = t;
+        if (blockIdx.x == 0) counters[2] = (unsigned long long)t;   // (KP runs after this kernel)
+    }
+    __syncthreads();
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-    for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; base < n; base += nw * 64) {
-        const int64_t i = base + lane;
-        int32_t gpos = 0, rows = 0;
-        if (i < n) { gpos = queue[i].gpos; rows = queue[i].rows; }
-        unsigned long long m = __ballot(i < n && rows == -1);
-        while (m) {
-            const int k = __builtin_ctzll(m);
-            m &= m - 1ull;
-            const int32_t p = __shfl(gpos, k, 64);
-            const int64_t e0 = blkA[p >> kRgBlockShift];
-            int32_t cov = 0;
-            wave_gather<false>(p, e0, n_entries, rh, grp, units, nullptr, &cov);
-            unsigned long long c4 = 0;
-            if (lane == 0) c4 = atomicAdd(&counters[5], (unsigned long long)((cov + 3) >> 2));
-            c4 = __shfl(c4, 0, 64);
-            int32_t r = -2;
-            if ((int64_t)(c4 << 2) + cov <= col_cap) r = wave_gather<true>(p, e0, n_entries, rh, grp, units, cols + (c4 << 2), nullptr);
-            if (lane == 0) { queue[base + k].coff = (int32_t)c4; queue[base + k].rows = r; }
+    const int64_t w0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t total = s_pre[nshard];
+    for (int64_t i = w0; i < total; i += nw) {
+        int k = 0;                                       // the segment of compact index i (binary search)
+        for (int step = kKlShards; step > 0; step >>= 1)
+            if (k + step < nshard && s_pre[k + step] <= i) k += step;
+        const int64_t j = i - s_pre[k];
+        {
+            SiteQ q = qin[(int64_t)k * qseg + j];
+            if (q.rows < 0 && q.rows != -2) {
+                const int32_t p = q.gpos;
+                const int64_t e0 = blkA[p >> kRgBlockShift];
+                int64_t c4;
+                int32_t cov;
+                if (q.rows == -1) {
+                    wave_gather<false>(p, e0, n_entries, rh, grp, units, 0u, nullptr, &cov);
+                    unsigned long long r = 0;
+                    if (lane == 0) r = atomicAdd(&counters[5], (unsigned long long)((cov + 3) >> 2));
+                    c4 = (int64_t)__shfl(r, 0, 64);
+                } else {
+                    cov = -3 - q.rows;
+                    c4 = q.coff;
+                }
+                int32_t r = -2;
+                if ((c4 << 2) + cov <= col_cap) r = wave_gather<true>(p, e0, n_entries, rh, grp, units, (uint32_t)ref[p], cols + (c4 << 2), nullptr);
+                q.coff = (int32_t)c4;
+                q.rows = r;
+            }
+            if (lane == 0) qout[i] = q;
         }
     }
 }
-
 
 __global__ __launch_bounds__(256) void k_zero_i32(int32_t* __restrict__ p, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0;
@@ -1764,8 +1866,9 @@ Device* device_create(int ordinal, std::string& err) {
     hipLaunchKernelGGL(k_zero_i32, dim3(1), dim3(256), 0, d->stream, (int32_t*)nullptr, (int64_t)0);
     (void)hipStreamSynchronize(d->stream);
     for (int k = 0; k < 2; k++) {
-        d->slot[k].d_ctr = d->d_counters + 8 + 8 * k;          // sets 1 and 2 (0: the multisample run)
-        if (hipHostMalloc(&d->slot[k].h_ctr, 8 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
+        if (hipMalloc(&d->slot[k].d_ctr, kCtrWords * sizeof(unsigned long long)) != hipSuccess ||
+            hipMemset(d->slot[k].d_ctr, 0, kCtrWords * sizeof(unsigned long long)) != hipSuccess ||
+            hipHostMalloc(&d->slot[k].h_ctr, kCtrWords * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
             err = "pinned allocation failed";
             return nullptr;
         }
@@ -1840,6 +1943,8 @@ void device_destroy(Device* d) {
         (void)hipFree(sl.d_brec);
         (void)hipFree(sl.d_bcount);
         (void)hipFree(sl.d_hard);
+        (void)hipFree(sl.d_hard2);
+        (void)hipFree(sl.d_ctr);
         (void)hipFree(sl.d_cols);
         (void)hipFree(sl.d_tables);
         if (sl.stream && sl.stream != d->stream) (void)hipStreamDestroy(sl.stream);
@@ -1990,8 +2095,10 @@ static int grow_slot(Device* d, RunSlot& sl, int64_t sites, int64_t queue, std::
     if (sites > d->cap_sites) d->cap_sites = sites;     // the slots' ordered-record buffers follow
     if (queue > sl.cap_hard) {
         (void)hipFree(sl.d_hard);
-        sl.d_hard = nullptr;
+        (void)hipFree(sl.d_hard2);
+        sl.d_hard = sl.d_hard2 = nullptr;
         HIP_TRY(hipMalloc(&sl.d_hard, (size_t)queue * sizeof(SiteQ)));
+        HIP_TRY(hipMalloc(&sl.d_hard2, (size_t)queue * sizeof(SiteQ)));
         sl.cap_hard = queue;
     }
     if (cols > sl.cap_cols) {                            // + 64 entries: KP's dword window reads past a column
@@ -2072,7 +2179,8 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     // KT is timed by events bound to its dispatch (hipExtLaunchKernelGGL): the kernel's own start and end
     hipEvent_t k0 = d->time_scan ? sl.ev[0] : nullptr, k1 = d->time_scan ? sl.ev[1] : nullptr;
     if (!d->rg) { err = "no read-group layout resident"; return -1; }
-    int64_t kg_sites = 0;                                        // sites queued without a column (KG's share)
+    int64_t kg_sites = 0;                                        // KG's sites (estimate)
+    bool kl_run = false;                                         // KL's sharded queue (else one segment, count at [2])
     if (s.known) {
         // -knownVariants: no scan, the input variants' sites (covered, in window order) are KP's queue
         if (nforced > 0) HIP_TRY(hipMemcpyAsync(sl.d_hard, s.h_forced.data(), (size_t)nforced * sizeof(SiteQ), hipMemcpyHostToDevice, sl.stream));
@@ -2083,11 +2191,15 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         kg_sites = nforced;
     } else if (d->n_tiles > 0 && prune) {
         // KL: one workgroup per tile of kKlTile positions, straight from the read-group layout
-        hipExtLaunchKernelGGL(k_read_scan<kKlTile>, dim3((unsigned)d->n_tiles), dim3(kKlThreads), 0, sl.stream, k0, k1, 0,
+        static const int kl_unroll = std::getenv("NGSEP_KL_UNROLL") ? std::atoi(std::getenv("NGSEP_KL_UNROLL")) : kKlUnroll;   // tuning
+        auto kl = kl_unroll == 24 ? k_read_scan<kKlTile, 24> : kl_unroll == 16 ? k_read_scan<kKlTile, 16> : k_read_scan<kKlTile, 8>;
+        hipExtLaunchKernelGGL(kl, dim3((unsigned)d->n_tiles), dim3(kKlThreads), 0, sl.stream, k0, k1, 0,
                               (const uint64_t*)d->d_units, (const int2*)d->d_rh, (const RGroup*)d->d_grp, (const int32_t*)d->d_blkA,
                               (const int32_t*)d->d_blkB, d->n_entries, (const uint8_t*)d->d_ref, (const LikTables*)sl.d_tables, g,
-                              sl.d_hard, ctr, sl.cap_hard, sl.d_cols, sl.cap_cols, sl.d_bcount, nb);
+                              sl.d_hard, ctr, sl.cap_hard / kKlShards, (sl.cap_cols >> 2) / kKlShards, sl.d_bcount, nb);
         HIP_TRY(hipGetLastError());
+        kg_sites = d->last_hard + d->last_hard / 8;              // KL's survivors (sized from the previous run)
+        kl_run = true;
     } else {
         // dump mode / no pruning: every in-window position goes to KP
         const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((s.g_len + 255) / 256, (int64_t)d->n_cu * 8));
@@ -2097,11 +2209,14 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         kg_sites = s.g_len;
     }
     {
-        // KG: the columns of the sites queued without one (a KL workgroup's overflow only, in a scan run)
-        const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((kg_sites + 255) / 256, (int64_t)d->n_cu * 8));
-        hipLaunchKernelGGL(k_gather_cols, dim3((unsigned)(kg_sites ? nblk : d->n_cu)), dim3(256), 0, sl.stream, sl.d_hard,
-                           (const unsigned long long*)(ctr + 2), sl.cap_hard, (const int2*)d->d_rh, (const RGroup*)d->d_grp,
-                           (const uint64_t*)d->d_units, (const int32_t*)d->d_blkA, d->n_entries, sl.d_cols, sl.cap_cols, ctr);
+        // KG: the queued sites' columns, one wave per site (grid-stride past the estimate)
+        const int64_t nblk = std::max<int64_t>(d->n_cu, std::min<int64_t>((kg_sites + 3) / 4, (int64_t)d->n_cu * 32));
+        hipLaunchKernelGGL(k_gather_cols, dim3((unsigned)nblk), dim3(256), 0, sl.stream, (const SiteQ*)sl.d_hard,
+                           (const unsigned long long*)(kl_run ? ctr + kCtrShard0 : ctr + 2), kl_run ? kCtrShardStride : 1,
+                           kl_run ? kKlShards : 1, kl_run ? sl.cap_hard / kKlShards : sl.cap_hard, sl.d_hard2,
+                           (const int2*)d->d_rh, (const RGroup*)d->d_grp,
+                           (const uint64_t*)d->d_units, (const int32_t*)d->d_blkA, (const uint8_t*)d->d_ref, d->n_entries, sl.d_cols,
+                           sl.cap_cols, ctr);
         HIP_TRY(hipGetLastError());
     }
     // one lane per queued site: enough workgroups for the queue (the count is on the device; sized from the
@@ -2112,12 +2227,12 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         if (!d->pool_valid) { err = "ploidy >= 3 without pool tables (device_set_pool)"; return -1; }
         hipExtLaunchKernelGGL(k_posterior_pool, dim3(kp_grid), dim3(kPostThreads), 0, sl.stream,
                               d->time_posterior ? sl.ev[5] : nullptr, d->time_posterior ? sl.ev[2] : nullptr, 0,
-                              (const SiteQ*)sl.d_hard, (const unsigned long long*)(ctr + 2), sl.cap_hard, (const uint16_t*)sl.d_cols,
+                              (const SiteQ*)sl.d_hard2, (const unsigned long long*)(ctr + 2), sl.cap_hard, (const uint16_t*)sl.d_cols,
                               (const PoolTables*)d->d_pool, g, sl.d_brec, sl.d_bcount, shift, bcap, sl.d_ext, ctr + 4, sl.cap_ext);
     } else {
         hipExtLaunchKernelGGL(k_posterior, dim3(kp_grid), dim3(kPostThreads), 0, sl.stream,
                               d->time_posterior ? sl.ev[5] : nullptr, d->time_posterior ? sl.ev[2] : nullptr, 0,
-                              (const SiteQ*)sl.d_hard, (const unsigned long long*)(ctr + 2), sl.cap_hard, (const uint16_t*)sl.d_cols,
+                              (const SiteQ*)sl.d_hard2, (const unsigned long long*)(ctr + 2), sl.cap_hard, (const uint16_t*)sl.d_cols,
                               (const LikTables*)sl.d_tables, g, sl.d_brec, sl.d_bcount, shift, bcap, sl.d_ext, ctr + 4, sl.cap_ext);
     }
     HIP_TRY(hipGetLastError());
@@ -2136,11 +2251,11 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     sl.host.rec.reserve((size_t)sl.guess);
     sl.host.ext.reserve((size_t)sl.guess_ext);
     if (!on_compute) HIP_TRY(hipStreamWaitEvent(cs, sl.ev[3], 0));
-    HIP_TRY(hipMemcpyAsync(sl.h_ctr, ctr, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemcpyAsync(sl.h_ctr, ctr, kCtrWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, cs));
     HIP_TRY(hipMemcpyAsync(sl.host.rec.buf, sl.d_sorted, (size_t)sl.guess * sizeof(SiteRec), hipMemcpyDeviceToHost, cs));
     if (sl.guess_ext > 0)
         HIP_TRY(hipMemcpyAsync(sl.host.ext.buf, sl.d_ext, (size_t)sl.guess_ext * sizeof(ngsep_site_out), hipMemcpyDeviceToHost, cs));
-    HIP_TRY(hipMemsetAsync(ctr, 0, 8 * sizeof(unsigned long long), cs));
+    HIP_TRY(hipMemsetAsync(ctr, 0, kCtrWords * sizeof(unsigned long long), cs));
     HIP_TRY(hipEventRecord(sl.ev[4], cs));
     sl.g = g;
     sl.prune = prune;
@@ -2190,19 +2305,42 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
         if (++cnt == 20) { std::fprintf(stderr, "[ngsep host] event wait %.1f us\n", acc / 20); acc = 0; cnt = 0; }
     }
     constexpr unsigned long long kNMask = (1ull << 40) - 1;
-    int64_t n = (int64_t)(sl.h_ctr[0] & kNMask);
-    int64_t mx = (int64_t)(sl.h_ctr[0] >> 40);          // fullest position bucket
-    int64_t q = (int64_t)sl.h_ctr[2];
-    int64_t ne = (int64_t)sl.h_ctr[4];
-    int64_t nc = (int64_t)sl.h_ctr[5] * 4;               // column entries reserved
-    for (int attempt = 0; n > d->cap_sites || q > sl.cap_hard || ne > sl.cap_ext || nc > sl.cap_cols ||
+    int64_t n, mx, q, ne, nc, ncand;
+    bool qfull, cfull;
+    auto read_ctr = [&]() {
+        const unsigned long long* h = sl.h_ctr;
+        n = (int64_t)(h[0] & kNMask);
+        mx = (int64_t)(h[0] >> 40);                      // fullest position bucket
+        ne = (int64_t)h[4];
+        // KL's shards (the queue and column segments of cap / kKlShards each), then KG's reservations
+        int64_t qs = 0, qmax = 0, cs4 = 0, cmax4 = 0;
+        ncand = (int64_t)h[1];
+        for (int t = 0; t < kKlShards; t++) {
+            const unsigned long long* c = h + kCtrShard0 + kCtrShardStride * t;
+            qs += (int64_t)c[0];
+            qmax = std::max<int64_t>(qmax, (int64_t)c[0]);
+            cs4 += (int64_t)c[1];
+            cmax4 = std::max<int64_t>(cmax4, (int64_t)c[1]);
+            ncand += (int64_t)c[2];
+        }
+        q = qs > 0 ? qs : (int64_t)h[2];
+        nc = (cs4 + (int64_t)h[5]) * 4;                  // column entries reserved
+        qfull = q > sl.cap_hard || qmax > sl.cap_hard / kKlShards;
+        cfull = (int64_t)h[5] * 4 > sl.cap_cols || cmax4 > (sl.cap_cols >> 2) / kKlShards;
+        if (qs > 0) {                                    // sized for the fullest shard
+            q = std::max<int64_t>(q, qmax * kKlShards);
+            nc = std::max<int64_t>(nc, cmax4 * 4 * kKlShards);
+        }
+    };
+    read_ctr();
+    for (int attempt = 0; n > d->cap_sites || qfull || ne > sl.cap_ext || cfull ||
                           (!sl.g.dump_all && mx > d->ko_bcap); attempt++) {
         // more calls or undecided candidates than the buffers hold (e.g. -minQuality 0): drain, grow
         // and run this slot again in place (a later run in the other slot keeps its own results)
         if (attempt == 3) { err = "result buffers kept overflowing"; return -1; }
         HIP_TRY(hipDeviceSynchronize());
-        if (grow_slot(d, sl, std::max(d->cap_sites, n + 1024), std::max(sl.cap_hard, q + 1024), err,
-                      std::max(sl.cap_cols, nc + nc / 4 + 1024)) != 0) return -1;
+        if (grow_slot(d, sl, std::max(d->cap_sites, n + 1024), qfull ? std::max(sl.cap_hard, q + q / 4 + 1024) : sl.cap_hard, err,
+                      cfull ? std::max(sl.cap_cols, nc + nc / 4 + 1024) : sl.cap_cols) != 0) return -1;
         if (ne > sl.cap_ext) {
             (void)hipFree(sl.d_ext);
             sl.d_ext = nullptr;
@@ -2218,11 +2356,7 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
         d->last_n_sites = n;
         if (enqueue_run(d, sl, *sl.staged, sl.tabs, sl.g, sl.prune, true, err) != 0) return -1;
         HIP_TRY(hipEventSynchronize(sl.ev[4]));
-        n = (int64_t)(sl.h_ctr[0] & kNMask);
-        mx = (int64_t)(sl.h_ctr[0] >> 40);
-        q = (int64_t)sl.h_ctr[2];
-        ne = (int64_t)sl.h_ctr[4];
-        nc = (int64_t)sl.h_ctr[5] * 4;
+        read_ctr();
     }
     d->last_cols = nc;
     sl.busy = false;
@@ -2253,8 +2387,8 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
     *scan_ms = a;
     *geno_ms = a2;
     *total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - sl.t0).count();
-    *n_candidates = (int64_t)sl.h_ctr[1];
-    d->last_hard = q;
+    *n_candidates = ncand;
+    d->last_hard = (int64_t)sl.h_ctr[2];
     d->last_exact = (int64_t)sl.h_ctr[3];
     return 0;
 }
