@@ -963,9 +963,9 @@ __global__ __launch_bounds__(kKlThreads) void k_read_scan(
     SiteQ* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qseg,
     int64_t cseg4, int32_t* __restrict__ bcount, int64_t nb) {
     constexpr int PT = T / kKlThreads;                 // positions per thread in the candidate phase
-    constexpr int NC = T + 24;                         // counter words (DEEP: one per position, margins 8 and 16)
-    static_assert(PT == 8, "candidate phase reads 16 bytes of counters per thread");
-    __shared__ int32_t s_diff[T + 1];
+    constexpr int NC = T / 2 + 16;                     // counter words (halfword per position, margins 8 and 24)
+    static_assert(PT == 8 || PT == 16, "candidate phase: whole 16-byte counter words per thread");
+    __shared__ alignas(16) int32_t s_diff[T + 32];     // coverage differences; then DEEP's counters (word 8 + i)
     __shared__ alignas(16) uint32_t s_ref[T / 4];
     __shared__ alignas(16) uint32_t s_cnt[NC];
     __shared__ int16_t s_cb[256];
@@ -976,7 +976,7 @@ __global__ __launch_bounds__(kKlThreads) void k_read_scan(
     (void)n_entries;
     for (int64_t i = (int64_t)blockIdx.x * kKlThreads + tid; i < nb; i += (int64_t)gridDim.x * kKlThreads) bcount[i] = 0;
     for (int i = tid; i <= T; i += kKlThreads) s_diff[i] = 0;
-    for (int i = tid; i < T / 2 + 16; i += kKlThreads) s_cnt[i] = 0;
+    for (int i = tid; i < NC; i += kKlThreads) s_cnt[i] = 0;
     {
         const uint32_t* r32 = reinterpret_cast<const uint32_t*>(ref + tstart);
         for (int i = tid; i < T / 4; i += kKlThreads) s_ref[i] = r32[i];
@@ -1010,32 +1010,44 @@ __global__ __launch_bounds__(kKlThreads) void k_read_scan(
     if (lane == 0) s_wmax[wv] = cmax;
     __syncthreads();
     const bool deep = max(max(s_wmax[0], s_wmax[1]), max(s_wmax[2], s_wmax[3])) > 255;
+    uint32_t* s_deep = reinterpret_cast<uint32_t*>(s_diff);   // (the coverage is in registers now)
     if (deep) {                                          // byte counters could carry: stream again, 32-bit counters
-        for (int i = tid; i < NC; i += kKlThreads) s_cnt[i] = 0;
+        for (int i = tid; i < T + 32; i += kKlThreads) s_deep[i] = 0;
         __syncthreads();
-        kl_stream<T, true, U>(units, rh, grp, e_lo, e_hi, tstart, s_diff, s_cnt, false, gp.ablate, sink);
+        kl_stream<T, true, U>(units, rh, grp, e_lo, e_hi, tstart, s_diff, s_deep, false, gp.ablate, sink);
         __syncthreads();
     }
-    if (sink == 0xFFFFFFFFu) s_diff[0] = (int32_t)sink;   // keeps the diagnostics' work alive
+    if (sink == 0xFFFFFFFFu) s_cnt[0] = sink;            // keeps the diagnostics' work alive
     // ---- candidates and the count bound
     const bool bound = gp.use_bound != 0 && !(gp.ablate & 1);
-    const uint2 rw = *reinterpret_cast<const uint2*>(&s_ref[2 * tid]);
+    uint32_t rwv[PT / 4];                                // the thread's positions' reference codes
+#pragma unroll
+    for (int k = 0; k < PT / 4; k += 2) {
+        const uint2 v = *reinterpret_cast<const uint2*>(&s_ref[PT / 4 * tid + k]);
+        rwv[k] = v.x;
+        rwv[k + 1] = v.y;
+    }
     uint32_t ncand = 0, need_bits = 0;
     uint64_t mine = 0;                                   // survivors << 40 | column space (units of 4 entries)
-    uint4 cw = make_uint4(0, 0, 0, 0);
-    if (!deep) cw = *reinterpret_cast<const uint4*>(&s_cnt[4 * tid + 4]);   // halfwords 8 tid + 8 ..
+    uint32_t cwv[PT / 2];                                // !deep: the positions' counters (halfwords PT tid + 8 ..)
+#pragma unroll
+    for (int k = 0; k < PT / 2; k += 4) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (!deep) v = *reinterpret_cast<const uint4*>(&s_cnt[PT / 2 * tid + 4 + k]);
+        cwv[k] = v.x; cwv[k + 1] = v.y; cwv[k + 2] = v.z; cwv[k + 3] = v.w;
+    }
 #pragma unroll
     for (int j = 0; j < PT; j++) {
         const int32_t cov = loc[j];
-        const uint32_t rc = ((j < 4 ? rw.x : rw.y) >> (8 * (j & 3))) & 0xFFu;
+        const uint32_t rc = (rwv[j >> 2] >> (8 * (j & 3))) & 0xFFu;
         int32_t exc, na;
         if (!deep) {
-            const uint32_t word = j < 2 ? cw.x : j < 4 ? cw.y : j < 6 ? cw.z : cw.w;
+            const uint32_t word = cwv[j >> 1];
             const uint32_t hw = word >> (16 * (j & 1));
             exc = (int32_t)(hw & 0xFFu);
             na = (int32_t)((hw >> 8) & 0xFFu);
         } else {
-            const uint32_t cn = s_cnt[PT * tid + j + 8];
+            const uint32_t cn = s_deep[PT * tid + j + 8];
             exc = (int32_t)(cn & 0xFFFFu);
             na = (int32_t)(cn >> 16);
         }
@@ -1089,12 +1101,35 @@ __global__ __launch_bounds__(kKlThreads) void k_read_scan(
     for (int j = 0; j < PT; j++) {
         if (!((need_bits >> j) & 1u)) continue;
         const int32_t cov = loc[j];
-        const uint32_t rc = ((j < 4 ? rw.x : rw.y) >> (8 * (j & 3))) & 0xFFu;
+        const uint32_t rc = (rwv[j >> 2] >> (8 * (j & 3))) & 0xFFu;
         const int32_t rows = (c4 << 2) + cov <= (cseg4 << 2) ? -3 - cov : -2;   // -2: the shard's columns are full (rerun)
         if (qi < qseg) queue[shard * qseg + qi] = SiteQ{tstart + PT * tid + j, (int32_t)rc, (int32_t)(shard * cseg4 + c4), rows};
         qi++;
         c4 += (cov + 3) >> 2;
     }
+}
+
+// KG's segment table: s_pre[k] = sites in segments before k (each segment's count capped at qseg), s_pre[nshard]
+// = all; block 0 stores the total in counters[2].  The first wave loads the counts in parallel (a scan).
+__device__ __forceinline__ void kg_segments(const unsigned long long* __restrict__ qcnt, int stride, int nshard, int64_t qseg,
+                                            int64_t* s_pre, unsigned long long* __restrict__ counters) {
+    static_assert(kKlShards <= 64, "one lane per segment");
+    if (threadIdx.x < 64) {
+        const int k = threadIdx.x;
+        const int64_t c = k < nshard ? min((int64_t)qcnt[(int64_t)k * stride], qseg) : 0;
+        int64_t incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t v = __shfl_up(incl, o, 64);
+            if (k >= o) incl += v;
+        }
+        if (k < nshard) s_pre[k] = incl - c;
+        if (k == nshard - 1) {
+            s_pre[nshard] = incl;
+            if (blockIdx.x == 0) counters[2] = (unsigned long long)incl;   // (KP runs after this kernel)
+        }
+    }
+    __syncthreads();
 }
 
 // KG: the queued sites' columns, and the compact queue KP reads.  The input queue is nshard segments of qseg
@@ -1111,16 +1146,7 @@ __global__ __launch_bounds__(256) void k_gather_cols(const SiteQ* __restrict__ q
                                                      unsigned long long* __restrict__ counters) {
     __shared__ int64_t s_pre[kKlShards + 1];
     const int lane = threadIdx.x & 63;
-    if (threadIdx.x == 0) {
-        int64_t t = 0;
-        for (int k = 0; k < nshard; k++) {
-            s_pre[k] = t;
-            t += min((int64_t)qcnt[(int64_t)k * stride], qseg);
-        }
-        s_pre[nshard] = t;
-        if (blockIdx.x == 0) counters[2] = (unsigned long long)t;   // (KP runs after this kernel)
-    }
-    __syncthreads();
+    kg_segments(qcnt, stride, nshard, qseg, s_pre, counters);
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
     const int64_t w0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t total = s_pre[nshard];
@@ -1152,6 +1178,92 @@ __global__ __launch_bounds__(256) void k_gather_cols(const SiteQ* __restrict__ q
             }
             if (lane == 0) qout[i] = q;
         }
+    }
+}
+
+// KG for KL's queue (every site's column space reserved: rows <= -3, or -2 when the shard's columns were full):
+// a wave gathers kKgSites sites at once, their chunk loads interleaved (one site's gather is a chain of dependent
+// loads -- block table, headers, units -- so a wave per site leaves the chip waiting).  Compacts like k_gather_cols.
+constexpr int kKgSites = 4;
+__global__ __launch_bounds__(256) void k_gather_kl(const SiteQ* __restrict__ qin, const unsigned long long* __restrict__ qcnt,
+                                                   int stride, int nshard, int64_t qseg, SiteQ* __restrict__ qout,
+                                                   const int2* __restrict__ rh, const RGroup* __restrict__ grp,
+                                                   const uint64_t* __restrict__ units, const int32_t* __restrict__ blkA,
+                                                   const uint8_t* __restrict__ ref, int64_t n_entries,
+                                                   uint16_t* __restrict__ cols, unsigned long long* __restrict__ counters) {
+    __shared__ int64_t s_pre[kKlShards + 1];
+    const int lane = threadIdx.x & 63;
+    kg_segments(qcnt, stride, nshard, qseg, s_pre, counters);
+    const int64_t total = s_pre[nshard];
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t w0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (int64_t i0 = w0 * kKgSites; i0 < total; i0 += nw * kKgSites) {
+        SiteQ q[kKgSites];
+        int64_t e[kKgSites];
+        int32_t n[kKgSites];
+        uint32_t rcode[kKgSites];
+        bool live[kKgSites];
+#pragma unroll
+        for (int t = 0; t < kKgSites; t++) {
+            const int64_t i = i0 + t;
+            live[t] = false;
+            n[t] = 0;
+            e[t] = 0;
+            rcode[t] = 0;
+            q[t] = SiteQ{0, 0, 0, -2};
+            if (i >= total) continue;
+            int k = 0;
+            for (int step = kKlShards; step > 0; step >>= 1)
+                if (k + step < nshard && s_pre[k + step] <= i) k += step;
+            q[t] = qin[(int64_t)k * qseg + (i - s_pre[k])];
+            live[t] = q[t].rows <= -3;
+        }
+#pragma unroll
+        for (int t = 0; t < kKgSites; t++)
+            if (live[t]) {
+                e[t] = (int64_t)blkA[q[t].gpos >> kRgBlockShift] & ~(int64_t)63;
+                rcode[t] = ref[q[t].gpos];
+            }
+        // chunk steps: every live site reads its next 64 entries' headers, then the covering ones' units
+        while (live[0] || live[1] || live[2] || live[3]) {
+            int2 h[kKgSites];
+            int64_t gb[kKgSites];
+#pragma unroll
+            for (int t = 0; t < kKgSites; t++) {
+                const bool l = live[t] && e[t] < n_entries;
+                h[t] = l ? rh[e[t] + lane] : make_int2(0x7FFFFFFF, 0);
+                gb[t] = l ? grp[e[t] >> 6].base : 0;
+            }
+            uint64_t u[kKgSites];
+            int32_t o[kKgSites];
+#pragma unroll
+            for (int t = 0; t < kKgSites; t++) {
+                const int32_t p = q[t].gpos, gf = h[t].x, gl = h[t].y & 0x7FFFFFFF;
+                const bool covers = live[t] && gf <= p && p <= gl;
+                o[t] = covers ? p - gf : -1;
+                u[t] = covers ? units[gb[t] + (int64_t)(o[t] >> 3) * 64 + lane] : 0ull;
+            }
+#pragma unroll
+            for (int t = 0; t < kKgSites; t++) {
+                if (!live[t]) continue;
+                const int32_t p = q[t].gpos;
+                const uint32_t code = o[t] >= 0 ? (((uint32_t)(u[t] >> (8 * (o[t] & 7))) & 0xFFu) ^ rcode[t]) : 0u;
+                const unsigned long long m = __ballot(code != 0);
+                if (code) {
+                    const int rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    cols[((int64_t)q[t].coff << 2) + n[t] + rk] = (uint16_t)(code | (((uint32_t)h[t].y >> 31) << 8));
+                }
+                n[t] += (int32_t)__popcll(m);
+                e[t] += 64;
+                if (__ballot(h[t].x > p) || e[t] >= n_entries) {   // entries are sorted by gfirst: none later covers p
+                    live[t] = false;
+                    q[t].rows = n[t];
+                }
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < kKgSites; t++)
+            if (lane == t && i0 + t < total) qout[i0 + t] = q[t];
     }
 }
 
@@ -2191,9 +2303,8 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         kg_sites = nforced;
     } else if (d->n_tiles > 0 && prune) {
         // KL: one workgroup per tile of kKlTile positions, straight from the read-group layout
-        static const int kl_unroll = std::getenv("NGSEP_KL_UNROLL") ? std::atoi(std::getenv("NGSEP_KL_UNROLL")) : kKlUnroll;   // tuning
-        auto kl = kl_unroll == 24 ? k_read_scan<kKlTile, 24> : kl_unroll == 16 ? k_read_scan<kKlTile, 16> : k_read_scan<kKlTile, 8>;
-        hipExtLaunchKernelGGL(kl, dim3((unsigned)d->n_tiles), dim3(kKlThreads), 0, sl.stream, k0, k1, 0,
+        // (measured on chr20 30x: 2048-position tiles and 8 loads in flight per lane beat 4096 / 16 and 24)
+        hipExtLaunchKernelGGL(k_read_scan<kKlTile, kKlUnroll>, dim3((unsigned)(s.g_len / kKlTile)), dim3(kKlThreads), 0, sl.stream, k0, k1, 0,
                               (const uint64_t*)d->d_units, (const int2*)d->d_rh, (const RGroup*)d->d_grp, (const int32_t*)d->d_blkA,
                               (const int32_t*)d->d_blkB, d->n_entries, (const uint8_t*)d->d_ref, (const LikTables*)sl.d_tables, g,
                               sl.d_hard, ctr, sl.cap_hard / kKlShards, (sl.cap_cols >> 2) / kKlShards, sl.d_bcount, nb);
@@ -2211,6 +2322,12 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     {
         // KG: the queued sites' columns, one wave per site (grid-stride past the estimate)
         const int64_t nblk = std::max<int64_t>(d->n_cu, std::min<int64_t>((kg_sites + 3) / 4, (int64_t)d->n_cu * 32));
+        if (kl_run)
+            hipLaunchKernelGGL(k_gather_kl, dim3((unsigned)std::max<int64_t>(d->n_cu, std::min<int64_t>((kg_sites + 4 * kKgSites - 1) / (4 * kKgSites), (int64_t)d->n_cu * 32))),
+                               dim3(256), 0, sl.stream, (const SiteQ*)sl.d_hard, (const unsigned long long*)(ctr + kCtrShard0), kCtrShardStride,
+                               kKlShards, sl.cap_hard / kKlShards, sl.d_hard2, (const int2*)d->d_rh, (const RGroup*)d->d_grp,
+                               (const uint64_t*)d->d_units, (const int32_t*)d->d_blkA, (const uint8_t*)d->d_ref, d->n_entries, sl.d_cols, ctr);
+        else
         hipLaunchKernelGGL(k_gather_cols, dim3((unsigned)nblk), dim3(256), 0, sl.stream, (const SiteQ*)sl.d_hard,
                            (const unsigned long long*)(kl_run ? ctr + kCtrShard0 : ctr + 2), kl_run ? kCtrShardStride : 1,
                            kl_run ? kKlShards : 1, kl_run ? sl.cap_hard / kKlShards : sl.cap_hard, sl.d_hard2,
