@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define NGSEP_ABI_VERSION 5
+#define NGSEP_ABI_VERSION 6
 
 #define NGSEP_OK 0
 #define NGSEP_E_INVALID (-1)      /* bad argument / state */
@@ -83,6 +83,12 @@ typedef struct ngsep_params {
      * CountsHelper state (all ten log-conditionals, every strand count).  Multi-allelic, pool and
      * dump_all_positions records are always whole. */
     int32_t full_records;
+    /* ABI 6: the indel realigner and indel / STR discovery (IndelRealignerPileupListener + VariantDiscovery-
+     * SNVQAlgorithm.callIndel, single-sample discovery at ploidy < 3 without -knownVariants, streamed runs).
+     * 0 (default): regions around alignments with indels are realigned and called here (indel / STR records,
+     * TYPE=EMBEDDED SNVs with call_embedded); 1: pass-through -- no call inside those regions, which are returned
+     * by ngsep_fetch_carved_regions for the caller's own indel path (the ABI 5 behaviour). */
+    int32_t indel_passthrough;
 } ngsep_params;
 
 /* Alignments as AlignmentsPileupGenerator.processAlignment receives them
@@ -118,7 +124,10 @@ typedef struct ngsep_site_out {
     int8_t  strand_bias;     /* FS phred score (-csb) or -1 */
     int16_t gq;              /* genotype quality, PhredScoreHelper.calculatePhredScore(1-maxP) */
     int16_t qual;            /* variant QS, phred(P[ref][ref]) */
-    int8_t  is_call;         /* 1 = passes the listener filters (always 1 unless dump_all_positions) */
+    int8_t  is_call;         /* bit 0: passes the listener filters (always set unless dump_all_positions);
+                              * bit 2: an SNV inside a called indel (INFO TYPE=EMBEDDED, params.call_embedded);
+                              * bit 3: an indel / STR record -- its fields here are 0 except seq_id / pos, its
+                              * VCF line comes from ngsep_site_vcf_line (ABI 6) */
     uint8_t pool;            /* ploidy >= 3 (SingleSampleVariantPileupListener.genotypeVariantPool, :402-503):
                               * bits 0-3 = the variant's alleles as DNA-index bits (reference included; the
                               * alleles are the reference, then the others in A,C,G,T order), bit 4 = the call
@@ -229,13 +238,15 @@ int ngsep_fetch_sites(ngsep_ctx* ctx, ngsep_site_out* out, int64_t cap, int64_t*
 int ngsep_clear_sites(ngsep_ctx* ctx);
 /* Alignments with insertions/deletions (CIGAR I/D) go through IndelRealignerPileupListener in the
  * reference (discovery/IndelRealignerPileupListener.java:85-526), which realigns the alignments around
- * each indel event and calls indels.  The device path does not run the realigner: every admitted
- * alignment with an I/D item carves [first - R, last + indel bases + R] out of the device plan, R = the
- * largest alignment span + 100 (the reach of an event's realignment: every alignment overlapping it),
- * merged per sequence.  No call is made inside a carved region; outside them the calls are the
- * reference's (the realigner is a pass-through there).  The carved regions are returned here, in
- * processing order, for the caller's own path (the JNI host runs the Java listener chain on them):
- * sequence ids, 1-based first and last positions.  n_out receives the number available. */
+ * each indel event and calls indels.  Every admitted alignment with an I/D item opens a region
+ * [first - R, last + indel bases + R], R = the largest alignment span + 100 (the reach of an event's
+ * realignment: every alignment overlapping it), merged per sequence.  With params.indel_passthrough = 0
+ * (ABI 6, the default for single-sample discovery at ploidy < 3 without -knownVariants in streamed runs)
+ * the regions are realigned and called here: indel / STR records (is_call bit 3) and the SNVs of the
+ * realigned alignments join the other calls, and no region is listed below.  Otherwise (pass-through, and
+ * every other mode) no call is made inside a region; outside them the calls are the reference's; the regions
+ * are returned here, in processing order, for the caller's own path (the JNI host runs the Java listener
+ * chain on them): sequence ids, 1-based first and last positions.  n_out receives the number available. */
 int ngsep_fetch_carved_regions(ngsep_ctx* ctx, int32_t* seq_id, int64_t* first, int64_t* last, int64_t cap, int64_t* n_out);
 int ngsep_clear_carved_regions(ngsep_ctx* ctx);
 
@@ -243,6 +254,9 @@ int ngsep_clear_carved_regions(ngsep_ctx* ctx);
 int ngsep_write_vcf_header(ngsep_ctx* ctx, const char* path);
 int ngsep_append_vcf_records(ngsep_ctx* ctx, const char* path);   /* all fetched sites, then clears them */
 int64_t ngsep_format_site(ngsep_ctx* ctx, const ngsep_site_out* site, char* buf, int64_t cap);
+/* ABI 6: the VCF line of fetched site i (any record kind, indel / STR records included); returns its length,
+ * copies at most cap - 1 characters and a terminating 0 (VCFFileWriter.printVCFRecord) */
+int64_t ngsep_site_vcf_line(ngsep_ctx* ctx, int64_t i, char* buf, int64_t cap);
 
 /* ---- MultisampleVariantsDetector (discovery/MultisampleVariantsDetector.java:421-693) ----
  * Samples in VCF column order (loadSamplesFromAlignmentHeaders: TreeMap by id, :499-523).

@@ -442,6 +442,9 @@ static inline ReadView batch_view(const BatchRef& br, int32_t i) {
     return r;
 }
 
+static bool realign_active(const ngsep_ctx* c);
+static void keep_raw(ngsep_ctx* c, size_t b0, size_t n, const int32_t* ent, const ReadView* carried);
+
 static void project_pending(ngsep_ctx* c) {
     std::vector<int32_t>& v = c->to_project;
     if (v.empty()) return;
@@ -487,6 +490,7 @@ static void project_pending(ngsep_ctx* c) {
     if (host_timing)
         std::fprintf(stderr, "[ngsep host] projection: %.1f ms (%u threads)\n",
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count(), host_threads());
+    if (realign_active(c)) keep_raw(c, b0, n, ent, carried);
     v.clear();
     c->to_project_carried.clear();
 }
@@ -534,6 +538,96 @@ static int stream_advance(ngsep_ctx* c, bool final);
 
 static bool streaming(const ngsep_ctx* c) { return !c->staging_mode && !c->params.coverage_stats && !c->params.multisample; }
 
+// the indel realigner runs here (realign.hpp) in streamed single-sample discovery at ploidy < 3 without input
+// variants (the reference's listener chain for findSNVS; SingleSampleVariantsDetector.java:896-931); elsewhere
+// its regions are carved out and returned (params.indel_passthrough)
+static bool realign_active(const ngsep_ctx* c) {
+    return streaming(c) && !c->params.indel_passthrough && !c->params.relative_allele_counts && !c->params.dump_all_positions &&
+           c->params.ploidy < 3 && c->known.empty();
+}
+
+// keeps the raw alignments (RawRead) a realigner region can need: those inside the reach of an indel read
+// admitted so far, and those a later one could still reach (`maybe`: last + R >= the admission frontier).
+// Called after each projection with the newly admitted reads b0 .. b0 + n (ent / carried: their batch views).
+static void keep_raw(ngsep_ctx* c, size_t b0, size_t n, const int32_t* ent, const ReadView* carried) {
+    ContigReads& cr = c->contig;
+    auto& st = c->stream;
+    while (st.indel_pmax.size() < cr.indel_reads.size()) {
+        const size_t k = st.indel_pmax.size();
+        st.indel_pmax.push_back(std::max(k ? st.indel_pmax[k - 1] : INT32_MIN, cr.indel_reads[k].second));
+    }
+    const int64_t R = (int64_t)cr.max_span + 100;
+    auto covered = [&](int64_t f, int64_t l) {             // an indel read Y: Y.first - R <= l and Y.second + R >= f
+        const size_t k = (size_t)(std::upper_bound(cr.indel_reads.begin(), cr.indel_reads.end(), l + R,
+                                                   [](int64_t v, const std::pair<int32_t, int32_t>& y) { return v < (int64_t)y.first; }) -
+                                  cr.indel_reads.begin());
+        return k > 0 && (int64_t)st.indel_pmax[k - 1] + R >= f;
+    };
+    const int64_t frontier = c->last_start;                // later indel reads start here or after
+    for (size_t k = st.kept_maybe_from; k < st.kept.size(); k++) {
+        auto& e = st.kept[k];
+        if (!e.maybe) continue;
+        if (covered(e.first, e.last)) e.maybe = false;
+        else if ((int64_t)e.last + R < frontier) { e.maybe = false; e.dead = true; }
+    }
+    for (size_t i = 0; i < n; i++) {
+        const int32_t f = cr.first[b0 + i], l = cr.last[b0 + i];
+        const bool cov = covered(f, l);
+        const bool maybe = !cov && (int64_t)l + R >= frontier;
+        if (!cov && !maybe) continue;
+        const ReadView r = ent[i] >= 0 ? batch_view(c->cur_batch, ent[i]) : carried[-1 - ent[i]];
+        std::remove_reference_t<decltype(st.kept)>::value_type e;
+        e.first = f;
+        e.last = l;
+        e.maybe = maybe;
+        e.dead = false;
+        RawRead& rr = e.r;
+        rr.first = r.first;
+        rr.last = r.last;
+        rr.flags = r.flags;
+        rr.ops.assign(r.cigar, r.cigar + r.n_cigar);
+        rr.has_chars = r.chars != nullptr && r.len > 0;
+        if (rr.has_chars) {
+            rr.chars.resize((size_t)r.len);
+            for (int32_t k = 0; k < r.len; k++) rr.chars[(size_t)k] = r.packed ? packed_base(r.chars, k) : r.chars[k];
+        }
+        rr.has_quals = rr.has_chars && r.quals != nullptr;
+        if (rr.has_quals) {
+            rr.quals.resize((size_t)r.len);
+            for (int32_t k = 0; k < r.len; k++)
+                rr.quals[(size_t)k] = r.packed ? (char)std::min(255, (unsigned char)r.quals[k] + 33) : r.quals[k];
+        }
+        const bool neg = (r.flags & 0x10) != 0;            // setBasesToIgnore5P/3P (ReadAlignment.java:613-644)
+        rr.ignore_start = neg ? c->params.ignore3 : c->params.ignore5;
+        rr.ignore_end = neg ? c->params.ignore5 : c->params.ignore3;
+        st.kept.push_back(std::move(e));
+    }
+    while (st.kept_maybe_from < st.kept.size() && !st.kept[st.kept_maybe_from].maybe) st.kept_maybe_from++;
+}
+
+// the realigner's regions (carve_indel_regions' geometry with the current R) that reach [lo, hi] -- merged, so a
+// region that reaches them is returned whole (as far as the indel reads admitted so far make it)
+static std::vector<std::pair<int64_t, int64_t>> regions_near(const ngsep_ctx* c, int64_t lo, int64_t hi) {
+    const ContigReads& cr = c->contig;
+    std::vector<std::pair<int64_t, int64_t>> out;
+    if (cr.indel_reads.empty()) return out;
+    const int64_t R = (int64_t)cr.max_span + 100, len = (int64_t)c->seq_bases[(size_t)cr.seq_id].size();
+    std::vector<std::pair<int64_t, int64_t>> iv;
+    for (size_t k = c->stream.indel_lo; k < cr.indel_reads.size(); k++) {
+        const int64_t a = std::max<int64_t>(1, cr.indel_reads[k].first - R), b = std::min<int64_t>(len, (int64_t)cr.indel_reads[k].second + R);
+        if (a > b) continue;
+        iv.push_back({a, b});
+    }
+    std::sort(iv.begin(), iv.end());
+    std::vector<std::pair<int64_t, int64_t>> merged;
+    for (const auto& x : iv) {
+        if (!merged.empty() && x.first <= merged.back().second + 1) merged.back().second = std::max(merged.back().second, x.second);
+        else merged.push_back(x);
+    }
+    for (const auto& m : merged) if (m.second >= lo && m.first <= hi) out.push_back(m);
+    return out;
+}
+
 static int flush_sequence(ngsep_ctx* c) {
     if (c->cur_seq < 0) return NGSEP_OK;
     process_same_start(c);
@@ -546,6 +640,10 @@ static int flush_sequence(ngsep_ctx* c) {
         c->stream.next_w0 = 0;
         c->stream.indel_lo = c->stream.chunk_lo = 0;
         c->stream.carved_inside = 0;
+        c->stream.kept.clear();
+        c->stream.kept_maybe_from = 0;
+        c->stream.indel_pmax.clear();
+        c->stream.last_indel_end = 0;                // SingleSampleVariantPileupListener.onSequenceStart (:186)
     } else {
         rc = stage_contig_reads(c, c->contig, !c->staging_mode);
     }
@@ -634,6 +732,7 @@ static int stream_collect(ngsep_ctx* c) {
     st.job->th.join();
     std::unique_ptr<WindowJob> j = std::move(st.job);
     if (j->rc != NGSEP_OK) return set_error(c, j->rc, j->err);
+    if (j->realign) st.last_indel_end = j->last_indel_end;
     if (c->params.relative_allele_counts) {
         auto& R = c->rac;
         double np = 0;
@@ -715,6 +814,7 @@ static void stream_launch(ngsep_ctx* c, int64_t w0, int64_t w1) {
         }
         std::sort(whole.begin(), whole.end());
         for (const auto& x : whole) {
+            if (realign_active(c)) break;                 // (called here: nothing handed back)
             auto& v = c->carved;
             if (!v.empty() && v.back().first == cr.seq_id && x.first <= v.back().second.second + 1) {
                 v.back().second.first = std::min(v.back().second.first, x.first);
@@ -730,24 +830,54 @@ static void stream_launch(ngsep_ctx* c, int64_t w0, int64_t w1) {
             else merged.push_back(x);
         }
         cut.swap(merged);
-        // covered positions inside them
+        // covered positions inside them (the realigner's regions are called here: they stay in the count)
         int64_t inside = 0;
-        size_t r0 = (size_t)lo;
-        for (const auto& cv : cut) {
-            while (r0 < (size_t)hi && (int64_t)cr.first[r0] + cr.max_span < cv.first) r0++;
-            int64_t run = cv.first - 1;
-            for (size_t i = r0; i < (size_t)hi && cr.first[i] <= cv.second; i++) {
-                const int64_t f = std::max<int64_t>(cr.first[i], cv.first), l = std::min<int64_t>(cr.last[i], cv.second);
-                if (l < f || l <= run) continue;
-                inside += l - std::max(f, run + 1) + 1;
-                run = l;
+        if (!realign_active(c)) {
+            size_t r0 = (size_t)lo;
+            for (const auto& cv : cut) {
+                while (r0 < (size_t)hi && (int64_t)cr.first[r0] + cr.max_span < cv.first) r0++;
+                int64_t run = cv.first - 1;
+                for (size_t i = r0; i < (size_t)hi && cr.first[i] <= cv.second; i++) {
+                    const int64_t f = std::max<int64_t>(cr.first[i], cv.first), l = std::min<int64_t>(cr.last[i], cv.second);
+                    if (l < f || l <= run) continue;
+                    inside += l - std::max(f, run + 1) + 1;
+                    run = l;
+                }
             }
+            st.carved_inside += inside;
+            c->stats.carved_positions += inside;
         }
-        st.carved_inside += inside;
-        c->stats.carved_positions += inside;
+    }
+    std::vector<std::vector<RawRead>> region_reads;
+    std::string region_err;
+    if (realign_active(c)) {
+        // the regions' alignments (whole regions: stream_advance never cuts one), in pending-list order; every
+        // alignment that overlaps a region must have been kept
+        region_reads.resize(cut.size());
+        for (size_t k = 0; k < cut.size(); k++) {
+            const int64_t a = cut[k].first, b = cut[k].second;
+            for (const auto& e : st.kept)
+                if (!e.dead && e.first <= b && e.last >= a) region_reads[k].push_back(e.r);
+            size_t want = 0;
+            for (int64_t i = lo; i < hi && cr.first[(size_t)i] <= b; i++) want += cr.last[(size_t)i] >= a ? 1 : 0;
+            if (want != region_reads[k].size())
+                region_err = "internal error: indel realigner region " + std::to_string(a) + "-" + std::to_string(b) + " lacks " +
+                             std::to_string((int64_t)want - (int64_t)region_reads[k].size()) + " alignments";
+        }
+        // alignments that end in this window reach no later region
+        std::deque<std::remove_reference_t<decltype(st.kept)>::value_type> keep;
+        for (auto& e : st.kept) if (!e.dead && e.last > w1) keep.push_back(std::move(e));
+        st.kept.swap(keep);
+        st.kept_maybe_from = 0;
     }
     if (hi <= lo) return;                       // no read reaches the window: nothing to call
     auto j = std::make_unique<WindowJob>();
+    if (realign_active(c)) {
+        j->realign = true;
+        j->region_reads.swap(region_reads);
+        j->last_indel_end = st.last_indel_end;
+        if (!region_err.empty()) { j->rc = NGSEP_E_INVALID; j->err = region_err; }
+    }
     if (!c->known.empty()) {
         // -knownVariants: the window's input variants at positions with a pileup (onPileup, :158-176), outside
         // the carved regions; queue code 0x80 | ref << 5 | alt << 8 | 0x400 (kernels.hip k_posterior)
@@ -806,8 +936,20 @@ static int stream_advance(ngsep_ctx* c, bool final) {
     const int64_t R = (int64_t)cr.max_span + 100;
     const int64_t limit = final ? hi : std::min<int64_t>(hi, (int64_t)c->last_start - 1 - 2 * R);
     while (st.next_w0 <= limit) {
-        const int64_t w1 = std::min<int64_t>(st.next_w0 + WL - 1, limit);
+        int64_t w1 = std::min<int64_t>(st.next_w0 + WL - 1, limit);
         if (!final && w1 - st.next_w0 + 1 < WL) break;          // mid-stream: whole windows only
+        if (realign_active(c) && w1 < hi) {
+            // a realigner region is never cut: the window ends before it, or after it once no later indel read
+            // can reach it (its end + R before the admission frontier)
+            bool wait = false;
+            for (const auto& r : regions_near(c, w1, w1)) {
+                if (!(r.first <= w1 && r.second > w1)) continue;
+                if (final || r.second + R + 1 < (int64_t)c->last_start) w1 = std::min<int64_t>(r.second, hi);
+                else if (r.first - 1 >= st.next_w0) w1 = r.first - 1;
+                else wait = true;
+            }
+            if (wait) break;
+        }
         if (st.job) {
             if (!final && !st.job->done.load()) break;           // the worker is busy: after the next batch
             const int rc = stream_collect(c);
@@ -1743,8 +1885,11 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
 
 // one streamed window (worker thread; the context's staged run, device and layout buffers are its own
 // until stream_collect joins it): reference codes, layout, upload, kernels, records into j->sites
+static int run_regions(ngsep_ctx* c, WindowJob* j, int64_t goff);
+
 static void run_window_job(ngsep_ctx* c, WindowJob* j) {
     static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    if (j->rc != NGSEP_OK) { j->done = true; return; }   // (stream_launch found a fault)
     const auto h0 = std::chrono::steady_clock::now();
     Staged& s = c->staged;
     s = Staged();
@@ -1813,6 +1958,7 @@ static void run_window_job(ngsep_ctx* c, WindowJob* j) {
         }
     } else {
         j->rc = run_device_into(c, j->sites, nullptr);
+        if (j->rc == NGSEP_OK && j->realign && !j->carved.empty()) j->rc = run_regions(c, j, (int64_t)pad - j->w0);
         if (j->rc != NGSEP_OK) j->err = c->err;
     }
     if (host_timing)
@@ -1821,6 +1967,101 @@ static void run_window_job(ngsep_ctx* c, WindowJob* j) {
                      std::chrono::duration<double, std::milli>(h2 - h1).count(),
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h2).count(), (long long)s.n_reads);
     j->done = true;
+}
+
+// The window's realigner regions (realign.hpp): each replayed on a host thread (alignment edits, span-1 columns,
+// the indel calls of longer spans); the columns genotyped on the device in one more run over the window's
+// layout (KP, queue entries with their columns); the listener's span rules over both; the kept SNV and indel
+// records merged into the window's, by position.  goff: window position p -> global p + goff.
+static int run_regions(ngsep_ctx* c, WindowJob* j, int64_t goff) {
+    const std::string& seq = c->seq_bases[(size_t)j->seq_id];
+    const size_t nr = j->carved.size();
+    std::vector<RegionOut> outs(nr);
+    RealignParams rp;
+    rp.max_base_qs = c->params.max_base_qs;
+    rp.min_quality = c->params.min_quality;
+    rp.ploidy = c->params.ploidy;
+    rp.het_rate = c->het_rate;
+    rp.ignore_lowercase = c->params.ignore_lowercase_ref != 0;
+    parallel_for((int64_t)nr, 1, [&](int64_t a, int64_t b) {
+        for (int64_t k = a; k < b; k++)
+            replay_region(seq, j->carved[(size_t)k].first, j->carved[(size_t)k].second, j->region_reads[(size_t)k], rp, outs[(size_t)k]);
+    });
+    // KP's queue: {global position, reference code, column offset / 4, entries} per callable position
+    Staged& s = c->staged;
+    s.known = true;
+    s.h_forced.clear();
+    s.h_cols.clear();
+    for (size_t k = 0; k < nr; k++) {
+        const RegionOut& o = outs[k];
+        const size_t cbase = s.h_cols.size();
+        s.h_cols.insert(s.h_cols.end(), o.cols.begin(), o.cols.end());
+        for (const RegionPos& p : o.pos) {
+            if (p.blocked || p.col_len == 0) continue;
+            const uint8_t rc = ref_code(c, seq[(size_t)p.pos - 1]);
+            if (!(rc & kRefCallable)) continue;
+            s.h_forced.push_back((int32_t)(p.pos + goff));
+            s.h_forced.push_back((int32_t)rc);
+            s.h_forced.push_back((int32_t)((cbase + (size_t)p.col_off) / 4));
+            s.h_forced.push_back(p.col_len);
+        }
+    }
+    std::memset(s.h_forced_ctr, 0, sizeof s.h_forced_ctr);
+    s.h_forced_ctr[2] = (unsigned long long)(s.h_forced.size() / 4);
+    s.h_forced_ctr[5] = (unsigned long long)(s.h_cols.size() / 4);
+    SiteStore snv;
+    if (!s.h_forced.empty()) {
+        const int rc = run_device_into(c, snv, nullptr);
+        if (rc != NGSEP_OK) return rc;
+    }
+    // the listener's decisions, region by region (records and positions both ascending)
+    SiteStore add;
+    size_t ri = 0;
+    int64_t kept = 0;
+    std::vector<uint8_t> has;
+    std::vector<size_t> rec_at;
+    std::vector<RegionDecision> dec;
+    for (size_t k = 0; k < nr; k++) {
+        const RegionOut& o = outs[k];
+        has.assign(o.pos.size(), 0);
+        rec_at.assign(o.pos.size(), 0);
+        for (size_t i = 0; i < o.pos.size(); i++) {
+            while (ri < snv.size() && snv.rec[ri].pos < o.pos[i].pos) ri++;
+            if (ri < snv.size() && snv.rec[ri].pos == o.pos[i].pos) { has[i] = 1; rec_at[i] = ri; }
+        }
+        resolve_region(o, has, c->params.call_embedded != 0, &j->last_indel_end, dec);
+        size_t pi = 0;
+        for (const RegionDecision& d : dec) {
+            while (o.pos[pi].pos != d.pos) pi++;
+            if (d.kind == 1) {
+                add.push_from(snv, rec_at[pi], d.embedded ? kRecEmbedded : 0);
+            } else {
+                SiteRec r;
+                std::memset(&r, 0, sizeof r);
+                r.seq_id = j->seq_id;
+                r.pos = d.pos;
+                r.is_call = kRecCall | kRecIndel;
+                add.text.push_back(o.indels[(size_t)d.idx].line);
+                r.L[0] = __builtin_bit_cast(double, (int64_t)add.text.size() - 1);
+                add.rec.push_back(r);
+            }
+            kept++;
+        }
+    }
+    c->stats.sites_called += kept - (int64_t)snv.size();
+    // merged with the window's records by position
+    SiteStore merged;
+    merged.rec.reserve(j->sites.size() + add.size());
+    size_t a = 0, b = 0;
+    while (a < j->sites.size() || b < add.size()) {
+        if (b >= add.size() || (a < j->sites.size() && j->sites.rec[a].pos <= add.rec[b].pos)) merged.push_from(j->sites, a++);
+        else merged.push_from(add, b++);
+    }
+    j->sites.swap(merged);
+    s.known = false;
+    s.h_forced.clear();
+    s.h_cols.clear();
+    return NGSEP_OK;
 }
 
 // java.lang.Math.round + PhredScoreHelper.calculatePhredScore (math/PhredScoreHelper.java:31-40)

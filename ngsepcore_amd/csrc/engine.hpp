@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <deque>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -19,6 +20,7 @@
 #include <utility>
 
 #include "../../include/ngsep_gpu.h"
+#include "realign.hpp"
 
 namespace ngsep {
 
@@ -300,7 +302,9 @@ struct SiteRec {
     int8_t ref, n_alleles, alt, third, genotype, strand_bias;
     int16_t gq;
     int16_t qual;
-    int8_t is_call;            // bit 0: passes the listener filters; bit 1: whole record in ext
+    int8_t is_call;            // bit 0: passes the listener filters; bit 1: whole record in ext; bit 2: an SNV inside
+                               // a called indel (TYPE=EMBEDDED); bit 3: an indel / STR call, its VCF text in the
+                               // set's `text` list (L[0]'s bits hold its index)
     uint8_t pool;
     int32_t dp;
     uint16_t counts[4];        // A,C,G,T
@@ -308,7 +312,7 @@ struct SiteRec {
     double L[3];               // logc (ref,ref), (ref,alt), (alt,alt)
 };
 static_assert(sizeof(SiteRec) == 64, "site record layout");
-constexpr int8_t kRecCall = 1, kRecExt = 2;
+constexpr int8_t kRecCall = 1, kRecExt = 2, kRecEmbedded = 4, kRecIndel = 8;
 
 inline int site_tri(int i, int j) {   // index of L[i][j] in ngsep_site_out.logc
     if (i > j) std::swap(i, j);
@@ -350,15 +354,16 @@ inline ngsep_sample_call expand_call(const PopCall32& p, const ngsep_sample_call
 struct SiteSet {
     PinnedStore<SiteRec> rec;
     PinnedStore<ngsep_site_out> ext;
+    std::vector<std::string> text;     // indel / STR records: the VCF line after the sequence name
     size_t size() const { return rec.size(); }
     bool empty() const { return rec.empty(); }
-    void clear() { rec.clear(); ext.clear(); }
-    void swap(SiteSet& o) { rec.swap(o.rec); ext.swap(o.ext); }
+    void clear() { rec.clear(); ext.clear(); text.clear(); }
+    void swap(SiteSet& o) { rec.swap(o.rec); ext.swap(o.ext); text.swap(o.text); }
     static int64_t ext_index(const SiteRec& r) { return __builtin_bit_cast(int64_t, r.L[0]); }
-    // o's records after ours (ext indexes rebased)
+    // o's records after ours (ext / text indexes rebased)
     void append(const SiteSet& o) {
         if (o.empty()) return;
-        const size_t from = rec.size(), ebase = ext.size();
+        const size_t from = rec.size(), ebase = ext.size(), tbase = text.size();
         rec.reserve(from + o.rec.size());
         std::memcpy(rec.buf + from, o.rec.buf, o.rec.size() * sizeof(SiteRec));
         rec.n = from + o.rec.size();
@@ -366,10 +371,26 @@ struct SiteSet {
             ext.reserve(ebase + o.ext.size());
             std::memcpy(ext.buf + ebase, o.ext.buf, o.ext.size() * sizeof(ngsep_site_out));
             ext.n = ebase + o.ext.size();
-            if (ebase)
-                for (size_t i = from; i < rec.size(); i++)
-                    if (rec[i].is_call & kRecExt) rec[i].L[0] = __builtin_bit_cast(double, ext_index(rec[i]) + (int64_t)ebase);
         }
+        text.insert(text.end(), o.text.begin(), o.text.end());
+        if (ebase || tbase)
+            for (size_t i = from; i < rec.size(); i++) {
+                if (rec[i].is_call & kRecExt) rec[i].L[0] = __builtin_bit_cast(double, ext_index(rec[i]) + (int64_t)ebase);
+                else if (rec[i].is_call & kRecIndel) rec[i].L[0] = __builtin_bit_cast(double, ext_index(rec[i]) + (int64_t)tbase);
+            }
+    }
+    // record i of o after ours (its ext / text entry copied)
+    void push_from(const SiteSet& o, size_t i, int8_t extra_flags = 0) {
+        SiteRec r = o.rec[i];
+        if (r.is_call & kRecExt) {
+            ext.push_back(o.ext[(size_t)ext_index(r)]);
+            r.L[0] = __builtin_bit_cast(double, (int64_t)ext.size() - 1);
+        } else if (r.is_call & kRecIndel) {
+            text.push_back(o.text[(size_t)ext_index(r)]);
+            r.L[0] = __builtin_bit_cast(double, (int64_t)text.size() - 1);
+        }
+        r.is_call = (int8_t)(r.is_call | extra_flags);
+        rec.push_back(r);
     }
     // the ABI record of site i (ngsep_site_out)
     ngsep_site_out full(size_t i) const {
@@ -392,8 +413,9 @@ struct SiteSet {
                 o.logc[site_tri(r.alt, r.alt)] = r.L[2];
             }
         }
+        if (r.is_call & kRecIndel) std::memset(&o, 0, sizeof o);   // (the record is its text)
         o.seq_id = r.seq_id; o.pos = r.pos; o.qual = r.qual; o.strand_bias = r.strand_bias;
-        o.is_call = (int8_t)(r.is_call & kRecCall);
+        o.is_call = (int8_t)(r.is_call & (kRecCall | kRecEmbedded | kRecIndel));
         return o;
     }
 };
@@ -462,6 +484,9 @@ struct Staged {            // everything resident for one run
     bool known = false;
     std::vector<int32_t> h_forced;
     unsigned long long h_forced_ctr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // the realigner's regions (realign.hpp): their queue entries carry their columns (rows >= 0), uploaded
+    // here (u16 entries, h_forced_ctr[5] = their size / 4)
+    std::vector<uint16_t> h_cols;
 };
 
 // Pinned host buffers of the single-sample layout, reused run after run (streamed windows: no page faults,
@@ -488,6 +513,11 @@ struct WindowJob {
     int32_t max_span = 1;
     std::vector<SRead> reads;                               // global coordinates (window at pad)
     std::vector<std::pair<int64_t, int64_t>> carved;        // 1-based, inside [w0, w1]
+    // the indel realigner's regions (whole inside the window, = carved) and their alignments; the listener's
+    // lastIndelEnd before and after the window
+    bool realign = false;
+    std::vector<std::vector<RawRead>> region_reads;
+    int32_t last_indel_end = 0;
     std::vector<int32_t> forced;                            // -knownVariants: KP queue entries (global position, code)
     SiteStore sites;
     // RelativeAlleleCounts mode: the window's histograms and proportion sums; its sequence's slot in the
@@ -560,6 +590,13 @@ struct ngsep_ctx {
         size_t indel_lo = 0;                      // indel reads before this index reach no later window
         size_t chunk_lo = 0;                      // projected chunks before this index are released
         int64_t carved_inside = 0;                // covered positions inside carved regions (this sequence)
+        // the indel realigner (params.indel_passthrough = 0): admitted alignments kept for its regions' replays --
+        // those inside a known region's reach and those a later indel read could still reach (`maybe`)
+        struct Kept { int32_t first, last; bool maybe, dead; ngsep::RawRead r; };
+        std::deque<Kept> kept;
+        size_t kept_maybe_from = 0;               // entries before this one are not `maybe`
+        std::vector<int32_t> indel_pmax;          // running max of indel_reads[k].second (the regions' ends)
+        int32_t last_indel_end = 0;               // SingleSampleVariantPileupListener.lastIndelEnd (this sequence)
         std::unique_ptr<ngsep::WindowJob> job;    // in flight on its own thread
         int64_t windows = 0;                      // windows run (diagnostics)
     } stream;

@@ -2237,6 +2237,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     // position in dump mode (the read bases bound it); grown when a run overflows
     int64_t cwant = std::max<int64_t>(std::max<int64_t>(1 << 20, s.g_len / 16), d->last_cols + d->last_cols / 4);
     if (g.dump_all || !prune) cwant = std::max<int64_t>(cwant, s.n_read_bases + 4 * s.g_len);
+    cwant = std::max<int64_t>(cwant, (int64_t)s.h_cols.size() + 1024);         // the realigner regions' columns
     if (want > d->cap_sites || qwant > sl.cap_hard || cwant > sl.cap_cols) {
         if (!idle) HIP_TRY(hipStreamSynchronize(sl.stream));
         if (grow_slot(d, sl, want, qwant, err, cwant) != 0) return -1;
@@ -2296,6 +2297,8 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     if (s.known) {
         // -knownVariants: no scan, the input variants' sites (covered, in window order) are KP's queue
         if (nforced > 0) HIP_TRY(hipMemcpyAsync(sl.d_hard, s.h_forced.data(), (size_t)nforced * sizeof(SiteQ), hipMemcpyHostToDevice, sl.stream));
+        if (!s.h_cols.empty())                                   // entries with their columns (realigner regions)
+            HIP_TRY(hipMemcpyAsync(sl.d_cols, s.h_cols.data(), s.h_cols.size() * sizeof(uint16_t), hipMemcpyHostToDevice, sl.stream));
         HIP_TRY(hipMemcpyAsync(ctr, s.h_forced_ctr, 8 * sizeof(unsigned long long), hipMemcpyHostToDevice, sl.stream));
         hipLaunchKernelGGL(k_zero_i32, dim3((unsigned)std::min<int64_t>((nb + 255) / 256, 4096)), dim3(256), 0, sl.stream, sl.d_bcount, nb);
         HIP_TRY(hipGetLastError());

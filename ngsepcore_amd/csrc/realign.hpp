@@ -1,15 +1,15 @@
-// realign.hpp -- the indel realigner's regions on the host (realign.cpp) and the device's indel genotyping
-// inputs (kernels.hip KI).  Internal to libngsep_amd.so.
+// realign.hpp -- the indel realigner's regions on the host (realign.cpp).  Internal to libngsep_amd.so.
 //
 // A region is the reach of the reference's IndelRealignerPileupListener around alignments with indels
 // (discovery/IndelRealignerPileupListener.java:85-526): inside it the listener edits alignments (moves indel
 // starts, realigns and trims alignment ends) while the pileup sweep goes on, so every pileup of the region is
-// taken from the alignments as edited so far.  realign_region replays that sweep over the region's admitted
+// taken from the alignments as edited so far.  replay_region replays that sweep over the region's admitted
 // alignments and returns, per position with a pileup, its reference span, its span-1 column (PileupRecord
-// .getAlleleCalls(1)) and, where the span is longer, the span's allele calls clustered into the candidate alleles
-// (AlleleCallClustersBuilder.clusterAlleleCalls).  Genotyping (KP for the columns, KI for the indel sites) runs on
-// the device; the listener's sequential rules (lastIndelEnd / embedded, the SNV fallback) are applied afterwards
-// by the host over the device's results (engine.cpp resolve_regions).
+// .getAlleleCalls(1), the device's u16 column entries: genotyped by KP like every other position) and, where the
+// span is longer, the span's indel call (AlleleCallClustersBuilder + CountsHelper indel counts + callIndel: a few
+// sites per kilobase of region, genotyped here).  resolve_region then applies the listener's sequential rules
+// (SingleSampleVariantPileupListener.onPileup :146-161, discoverVariant :213-273: lastIndelEnd, embedded SNVs,
+// the SNV fallback of a span whose alleles made no call) over the device's SNV calls.
 #pragma once
 
 #include <cstdint>
@@ -18,21 +18,28 @@
 
 namespace ngsep {
 
-// an admitted alignment as the realigner needs it (ReadAlignment fields)
+// an admitted alignment as the realigner needs it (ReadAlignment fields), in admission (pending-list) order
 struct RawRead {
     int32_t first = 0, last = 0, flags = 0;
     std::vector<int32_t> ops;          // NGSEP CIGAR codes len * 8 + op
-    std::string chars;                 // upper case (empty: no characters)
-    std::string quals;                 // phred + 33 (empty: no qualities)
+    std::string chars;                 // read characters (has_chars = false: getReadCharacters() == null)
+    std::string quals;                 // phred + 33 (has_quals = false: '*')
     bool has_chars = false, has_quals = false;
-    int16_t ignore_start = 0, ignore_end = 0;   // bases to ignore at the alignment's start / end (ignore5/3 by strand)
+    int32_t ignore_start = 0, ignore_end = 0;   // setBasesToIgnore5P/3P by strand (ReadAlignment.java:613-644)
 };
 
-// one allele call of an indel site (PileupAlleleCall with span > 1)
-struct ICall {
-    int32_t off;                       // chars / quals offset in the site's text
-    int32_t len;
-    int32_t neg;
+struct RealignParams {
+    int32_t max_base_qs = 30;          // -maxBaseQS
+    int32_t min_quality = 40;          // -minQuality
+    int32_t ploidy = 2;
+    double het_rate = 0.001;           // -h
+    bool ignore_lowercase = false;     // -ignoreLowerCaseRef
+};
+
+// a decided indel / STR call (callIndel + the listener's filters), its VCF line already formatted
+struct IndelCall {
+    int32_t pos = 0, last = 0;         // first, first + |REF| - 1
+    std::string line;                  // without the sequence name: "POS\t.\tREF\tALT\t..." + '\n'
 };
 
 // what one position of a region contributes
@@ -40,34 +47,34 @@ struct RegionPos {
     int32_t pos = 0;                   // 1-based
     int32_t span = 1;                  // the realigner's reference span
     bool str = false, new_str = false;
-    int32_t col_off = -1, col_len = 0; // span-1 column (u16 entries) in RegionOut::cols (-1: no non-reference call: hom-ref)
-    int32_t indel = -1;                // index of its indel site (span > 1 and calls present)
-};
-
-// an indel site for KI: the clustered alleles (reference first) and the span's allele calls in pileup order
-struct IndelSite {
-    int32_t pos = 0;
-    std::vector<std::string> alleles;
-    std::string text;                  // the calls' alleles, then their qualities
-    std::vector<ICall> calls;
+    int32_t col_off = 0, col_len = 0;  // span-1 column: u16 entries code | negative strand << 8 in RegionOut::cols
+    int32_t indel = -1;                // span > 1: index into RegionOut::indels of the span's call (-1: none)
+    bool blocked = false;              // no call at all (span past the sequence end, lower-case reference ignored)
 };
 
 struct RegionOut {
-    int32_t seq_id = -1;
     int64_t first = 0, last = 0;       // the region (1-based, inclusive)
     std::vector<RegionPos> pos;        // positions with a pileup, ascending
-    std::vector<uint16_t> cols;        // the columns, each padded to a multiple of 4 entries
-    std::vector<IndelSite> sites;
+    std::vector<uint16_t> cols;
+    std::vector<IndelCall> indels;
 };
 
-struct RealignParams {
-    int32_t max_base_qs = 30;          // -maxBaseQS (byte, as the listener passes it)
-    bool ignore_lowercase = false;     // the column's reference code (non-callable lower case: no column)
-};
+// replays AlignmentsPileupGenerator + IndelRealignerPileupListener over [first, last] of one sequence (`seq`: the
+// reference as loaded, case kept); `reads` are the admitted alignments overlapping it in pending-list order
+// (edited in place)
+void replay_region(const std::string& seq, int64_t first, int64_t last, std::vector<RawRead>& reads, const RealignParams& p,
+                   RegionOut& out);
 
-// replays AlignmentsPileupGenerator + IndelRealignerPileupListener over [first, last] of one sequence; `reads` are
-// the admitted alignments overlapping it in pending-list order (edited in place)
-void realign_region(const std::string& ref, int32_t seq_id, int64_t first, int64_t last, std::vector<RawRead>& reads,
-                    const RealignParams& p, RegionOut& out);
+// the listener's decisions over a replayed region, position by position: kind 0 nothing, 1 the position's SNV
+// call (flag embedded: TYPE=EMBEDDED), 2 the indel call out.indels[idx].  last_indel_end is the listener's
+// lastIndelEnd (per sequence, carried across regions)
+struct RegionDecision {
+    int32_t pos;
+    int8_t kind;
+    bool embedded;
+    int32_t idx;
+};
+void resolve_region(const RegionOut& out, const std::vector<uint8_t>& has_snv_call, bool call_embedded, int32_t* last_indel_end,
+                    std::vector<RegionDecision>& dec);
 
 }  // namespace ngsep

@@ -143,7 +143,8 @@ int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& o)
     // INFO: FS for CalledSNV (SingleSampleVariantsDetector.java:956-958), TYPE for non-SNV types (VCFFileWriter.java:47-49)
     bool printed = false;
     if (s.n_alleles == 2 && s.strand_bias != -1) { o += "FS="; app(o, s.strand_bias); printed = true; }
-    if (s.n_alleles == 3) { if (printed) o += ';'; o += "TYPE=MULTISNV"; printed = true; }
+    if (s.is_call & kRecEmbedded) { if (printed) o += ';'; o += "TYPE=EMBEDDED"; printed = true; }   // -embeddedSNVs (:227)
+    else if (s.n_alleles == 3) { if (printed) o += ';'; o += "TYPE=MULTISNV"; printed = true; }
     if (!printed) o += '.';
     o += "\tGT:PL:GQ:DP:BSDP:ACN\t";
     if (s.n_alleles == 2) {
@@ -213,6 +214,18 @@ int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& o)
     }
     o += '\n';
     return (int64_t)(o.size() - start);
+}
+
+// record i of the context's site list: an SNV record (format_site), or an indel / STR record's text
+void format_record(const ngsep_ctx* c, size_t i, std::string& o) {
+    const SiteRec& r = c->sites.rec[i];
+    if (r.is_call & kRecIndel) {
+        o += (r.seq_id >= 0 && r.seq_id < (int)c->seq_names.size()) ? c->seq_names[(size_t)r.seq_id] : std::string("?");
+        o += '\t';
+        o += c->sites.text[(size_t)SiteSet::ext_index(r)];
+        return;
+    }
+    format_site(c, c->sites.full(i), o);
 }
 
 // ---- MultisampleVariantsDetector output ----
@@ -337,14 +350,25 @@ extern "C" int ngsep_append_vcf_records(ngsep_ctx* c, const char* path) {
     buf.reserve(1 << 20);
     for (size_t i = 0; i < c->sites.size(); i++) {
         if (!(c->sites.rec[i].is_call & kRecCall)) continue;
-        const ngsep_site_out s = c->sites.full(i);
-        format_site(c, s, buf);
+        format_record(c, i, buf);
         if (buf.size() > (1 << 20)) { std::fwrite(buf.data(), 1, buf.size(), f); buf.clear(); }
     }
     std::fwrite(buf.data(), 1, buf.size(), f);
     std::fclose(f);
     c->sites.clear();
     return NGSEP_OK;
+}
+
+extern "C" int64_t ngsep_site_vcf_line(ngsep_ctx* c, int64_t i, char* buf, int64_t cap) {
+    if (!c || i < 0 || i >= (int64_t)c->sites.size()) return NGSEP_E_INVALID;
+    std::string o;
+    format_record(c, (size_t)i, o);
+    if (buf && cap > 0) {
+        const int64_t k = std::min<int64_t>((int64_t)o.size(), cap - 1);
+        std::memcpy(buf, o.data(), (size_t)k);
+        buf[k] = 0;
+    }
+    return (int64_t)o.size();
 }
 
 extern "C" int64_t ngsep_format_site(ngsep_ctx* c, const ngsep_site_out* s, char* buf, int64_t cap) {

@@ -1,4 +1,12 @@
-"""Alignments with indels (first step): the device path carves the indel realigner's
+"""Alignments with indels.
+
+Default (params.indel_passthrough = 0): the indel realigner's regions are replayed on the host (realign.cpp:
+alignment edits, span calls, allele clusters, indel genotypes, the listener's span rules) and their span-1
+columns genotyped on the device; the WHOLE VCF -- indel / STR records, SNVs of realigned alignments,
+TYPE=EMBEDDED with -embeddedSNVs -- must equal the oracle's (oracle/ngsep_oracle_indel.inc).  Parity here is
+against the oracle restatement only: the reference holds no indel fixture (parity unpinned).
+
+Pass-through (indel_passthrough = 1, the ABI 5 behaviour): the device path carves the indel realigner's
 reach out of its plan (ngsep_gpu.h ngsep_fetch_carved_regions) and calls every other position.
 
 The reference runs IndelRealignerPileupListener (discovery/IndelRealignerPileupListener.java:85-526) before
@@ -51,7 +59,9 @@ def test_carved_regions_host_geometry():
     """The carve intervals (host side, before any device work) on path A batches; the device step then
     fails loudly here (no GPU), after the regions are recorded."""
     syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=1, contig_first=1, depth=12, seed=31, indel_rate=2e-4, dup_rate=0)
-    s = GpuPileupSession(default_params())
+    p = default_params()
+    p.indel_passthrough = 1
+    s = GpuPileupSession(p)
     for n, q in syn.contigs():
         s.set_reference(n, q)
     rc = s._lib.ngsep_process_alignments(s._ctx, __import__("ctypes").byref(syn.batch()))
@@ -94,7 +104,7 @@ def test_calls_outside_carved_regions_identical(tmp_path, kw, win):
     o = os.path.join(str(tmp_path), "o.vcf")
     ost = ngsep_oracle.run_ssvd(fa, sam, o, indel_passthrough=1)
     g = os.path.join(str(tmp_path), "g.vcf")
-    p = gpu_params()
+    p = gpu_params(indel_passthrough=1)
     if win:
         p.window_positions = win
     with GpuPileupSession(p) as s:
@@ -104,7 +114,7 @@ def test_calls_outside_carved_regions_identical(tmp_path, kw, win):
         st = s.stats()
     assert len(carved) > 2
     if win:
-        with GpuPileupSession(gpu_params()) as s:
+        with GpuPileupSession(gpu_params(indel_passthrough=1)) as s:
             s.load_fasta(fa)
             s.processFile(bam, g + ".whole")
             assert s.carved_regions() == carved
@@ -114,3 +124,42 @@ def test_calls_outside_carved_regions_identical(tmp_path, kw, win):
     assert ro == rg and len(rg) > 50
     # every covered position is either genotyped on the device or inside a carved region
     assert st.positions_genotyped + st.carved_positions == ost.positions_genotyped
+
+
+def _records(vcf):
+    return [l for l in open(vcf) if not l.startswith("#")]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw,opts", [
+    (dict(depth=25, seed=32, indel_rate=1e-4), {}),
+    (dict(depth=15, seed=33, indel_rate=3e-4, quality_model=2, snv_rate=3e-3), {}),
+    (dict(depth=25, seed=32, indel_rate=1e-4), dict(window_positions=40000)),
+    (dict(depth=30, seed=34, indel_rate=1e-3, snv_rate=2e-2, n_contigs=1), dict(call_embedded=1)),
+    (dict(depth=20, seed=35, indel_rate=2e-4, quality_model=2), dict(min_quality=0, ploidy=1)),
+])
+def test_indel_regions_vcf_identical(tmp_path, kw, opts):
+    """The realigner's regions called here: the WHOLE VCF equals the oracle's (indel / STR records, the
+    realigned alignments' SNVs, embedded SNVs), no region is handed back, every covered position is genotyped;
+    a window cut (window_positions) changes nothing."""
+    syn = pysynth.Synth(genome=pysynth.YEAST, **{"n_contigs": 2, **kw})
+    fa, sam, bam = syn.write(os.path.join(str(tmp_path), "ind"))
+    syn.close()
+    o = os.path.join(str(tmp_path), "o.vcf")
+    oopts = {k: v for k, v in opts.items() if k != "window_positions"}
+    ost = ngsep_oracle.run_ssvd(fa, sam, o, **oopts)
+    g = os.path.join(str(tmp_path), "g.vcf")
+    with GpuPileupSession(gpu_params(**opts)) as s:
+        s.load_fasta(fa)
+        s.processFile(bam, g)
+        assert s.carved_regions() == []
+        st = s.stats()
+    ro, rg = _records(o), _records(g)
+    n_indel = sum(1 for l in ro if "TYPE=INDEL" in l or "TYPE=STR" in l)
+    assert n_indel > 3
+    if opts.get("call_embedded"):
+        assert any("TYPE=EMBEDDED" in l for l in ro)
+    for a, b in zip(ro, rg):
+        assert a == b, (a, b)
+    assert len(ro) == len(rg)
+    assert st.positions_genotyped == ost.positions_genotyped
