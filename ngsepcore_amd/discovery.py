@@ -45,6 +45,8 @@ class CalledSite:
     strand_bias: int
     is_call: bool
     called: List[int] = None
+    vcf_line: str = None        # indel / STR records (ABI 6): the record's VCF line; embedded SNVs: TYPE=EMBEDDED
+    embedded: bool = False
 
     def log_conditional(self, i: int, j: int) -> float:
         """SNVQ records: i, j are DNA indexes; pool records: indexes into `alleles`."""
@@ -194,7 +196,19 @@ class GpuPileupSession:
     def getCalledVariants(self) -> List[CalledSite]:
         names = self.sequence_names()
         out = []
-        for s in self.raw_sites():
+        for i, s in enumerate(self.raw_sites()):
+            if s.is_call & 8:                    # an indel / STR call (IndelRealignerPileupListener + callIndel)
+                buf = ctypes.create_string_buffer(1 << 16)
+                self._lib.ngsep_site_vcf_line(self._ctx, i, buf, 1 << 16)
+                f = buf.value.decode().rstrip("\n").split("\t")
+                gt = f[9].split(":")[0]
+                out.append(CalledSite(
+                    sequence=f[0], pos=int(f[1]), ref=f[3], alleles=[f[3]] + f[4].split(","),
+                    genotype=-1, gq=int(f[9].split(":")[2]), qual=int(f[5]), dp=int(f[9].split(":")[3]),
+                    counts=[int(x) for x in f[9].split(":")[4].split(",")], strand_counts=[], logc=[],
+                    strand_bias=-1, is_call=True, called=[int(x) for x in gt.replace("|", "/").split("/")],
+                    vcf_line=buf.value.decode()))
+                continue
             alleles = [chr(s.ref)]
             called = None
             if s.pool:
@@ -209,7 +223,7 @@ class GpuPileupSession:
                 sequence=names[s.seq_id] if 0 <= s.seq_id < len(names) else "?", pos=s.pos, ref=chr(s.ref),
                 alleles=alleles, genotype=s.genotype, gq=s.gq, qual=s.qual, dp=s.dp, counts=list(s.counts),
                 strand_counts=[list(x) for x in s.strand_counts], logc=list(s.logc),
-                strand_bias=s.strand_bias, is_call=bool(s.is_call), called=called))
+                strand_bias=s.strand_bias, is_call=bool(s.is_call & 1), called=called, embedded=bool(s.is_call & 4)))
         return out
 
     def clear(self):
