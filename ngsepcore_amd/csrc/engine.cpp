@@ -1616,13 +1616,23 @@ static int build_multi_layout(Staged& s) {
     s.pile_bytes = nbytes;
     s.n_tiles = (ne + 63) / 64;         // KTM's groups of 64 columns
     // KPM pile: block offsets, then the columns filled chunk by chunk in getAlleleCalls order
+    // site-major inside a tile: position p's columns of every sample are consecutive (sample order), so KPM's
+    // workgroup at p reads one contiguous run of stride_t bytes; pboff[t * S1 + s] = the tile's base + the earlier
+    // samples' rows, and stride_t = (pboff[(t + 1) * S1] - pboff[t * S1]) / PT
     s.h_pboff.assign((size_t)ntile * S1 + 1, 0);
+    std::vector<int64_t> pstride((size_t)ntile, 0);
     int64_t po = 0;
     int32_t rmax = 0;
-    for (size_t i = 0; i < (size_t)ntile * S1; i++) {
-        s.h_pboff[i] = po;
-        po += (int64_t)s.h_prow[i] * PT;
-        rmax = std::max<int32_t>(rmax, s.h_prow[i]);
+    for (int64_t t = 0; t < ntile; t++) {
+        int64_t so = 0;
+        for (int s1 = 0; s1 < S1; s1++) {
+            const size_t i = (size_t)t * S1 + s1;
+            s.h_pboff[i] = po + so;
+            so += s.h_prow[i];
+            rmax = std::max<int32_t>(rmax, s.h_prow[i]);
+        }
+        pstride[(size_t)t] = so;
+        po += so * PT;
     }
     s.h_pboff.back() = po;
     s.ppile_bytes = po;
@@ -1665,7 +1675,7 @@ static int build_multi_layout(Staged& s) {
                     const uint8_t cd = src[p - a];
                     if (!cd) continue;
                     const size_t bi = (size_t)(p / PT) * S1 + s1;
-                    pile[s.h_pboff[bi] + (p % PT) * s.h_prow[bi] + cc[p - c0]++] = cd;
+                    pile[s.h_pboff[bi] + (p % PT) * pstride[(size_t)(p / PT)] + cc[p - c0]++] = cd;
                 }
             }
         }

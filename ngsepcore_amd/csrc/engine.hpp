@@ -454,7 +454,9 @@ struct Staged {            // everything resident for one run
     std::vector<uint8_t> h_mc_n;
     std::vector<int64_t> h_mc_gbase;
     // multisample: KPM's pile -- per (tile of kPopTile positions, sample + the reads of no sample) block of
-    // rows x kPopTile code bytes, position-major (column p at pboff + p * rows), in getAlleleCalls order
+    // per tile of kPopTile positions, site-major: position p's columns of samples 0 .. S (the reads of no sample
+    // last) back to back, each rows(t, s) code bytes in getAlleleCalls order -- column (p, s) at pboff[t * (S + 1) + s]
+    // + (p % kPopTile) * stride_t, stride_t = the tile's rows summed over its samples
     std::unique_ptr<uint8_t[]> h_ppile;
     std::vector<uint16_t> h_prow;       // rows per (tile, sample): h_prow[t * (S + 1) + s]
     std::vector<int64_t> h_pboff;       // block offsets, same index (+ the total at the end)

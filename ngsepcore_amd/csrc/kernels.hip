@@ -144,7 +144,7 @@ struct Device {
     ngsep_popsite_out* h_psites = nullptr;      // multisample: pinned staging of the emitted sites and calls
     ngsep_sample_call* h_pcalls = nullptr;
     int64_t cap_h_psites = 0, cap_h_pcalls = 0;
-    uint8_t* d_ppile = nullptr;      // multisample: KPM's position-major per-(tile, sample) pile
+    uint8_t* d_ppile = nullptr;      // multisample: KPM's site-major per-tile pile
     uint16_t* d_prow = nullptr;      //   rows per block
     int64_t* d_pboff = nullptr;      //   block offsets
     int32_t n_samples = 0;
@@ -1307,12 +1307,18 @@ __global__ __launch_bounds__(256) void k_queue_all(const uint8_t* __restrict__ r
 // position where every sample is proven hom-ref gets variant QS 0, which MultisampleVariantsDetector.onPileup
 // never writes (:534).  Open positions are ORed into a bit per global position; KQN queues them for KPM.
 // The 64 columns of a group are consecutive bytes, so the wave's dword loads are coalesced.
+constexpr int kKtmWords = 8;                   // KTM: column dwords per lane staged in LDS (a 2 KB group)
+__device__ __forceinline__ int64_t ktm_uniform(int64_t v) {
+    return ((int64_t)__builtin_amdgcn_readfirstlane((int32_t)(v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)v);
+}
 __global__ __launch_bounds__(256)
 void k_scan_multi(const int32_t* __restrict__ mc_pos, const uint8_t* __restrict__ mc_n, const int64_t* __restrict__ mc_gbase,
                   const uint8_t* __restrict__ cols, int64_t n_entries, const LikTables* __restrict__ tabs, GenotypeParams gp,
                   uint32_t* __restrict__ need, unsigned long long* __restrict__ counters) {
     __shared__ unsigned long long w[2][32];
     __shared__ unsigned long long s_ne[4];
+    __shared__ uint32_t s_col[4][64 * kKtmWords];
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     if (threadIdx.x < 64) w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
@@ -1323,27 +1329,60 @@ void k_scan_multi(const int32_t* __restrict__ mc_pos, const uint8_t* __restrict_
     const uint32_t* cw = reinterpret_cast<const uint32_t*>(cols);
     const int64_t ngroups = (n_entries + 63) >> 6;
     const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    uint32_t* buf = s_col[wv];
     unsigned long long nexact = 0;
-    for (int64_t grp = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv; grp < ngroups; grp += nwaves) {
+    // A group's columns are the bytes [gbase[g], gbase[g + 1]): the wave loads them whole (coalesced, one round
+    // trip) into LDS, and the next group's metadata and bytes are in flight while this one is bounded; the group
+    // after that has its byte range (gbase) in flight too.  A group larger than the staging buffer is read from
+    // global memory column by column.
+    int64_t grp = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+    grp = ktm_uniform(grp);
+    auto ld_gb = [&](int64_t g, int64_t& g0, int64_t& g1) {
+        if (g < ngroups) { g0 = ktm_uniform(mc_gbase[g]); g1 = ktm_uniform(mc_gbase[g + 1]); } else { g0 = g1 = 0; }
+    };
+    int32_t c_pos = 0, n_pos = 0;
+    uint32_t c_n = 0, n_n = 0;
+    uint32_t c_w[kKtmWords], n_w[kKtmWords];
+    int64_t c_g0, c_g1, n_g0, n_g1, f_g0, f_g1;
+    auto ld_group = [&](int64_t g, int64_t g0, int64_t g1, int32_t& pos, uint32_t& n, uint32_t* wds) {
+        const int64_t i = (g << 6) + lane;
+        const bool has = g < ngroups && i < n_entries;
+        pos = has ? mc_pos[i] : 0;
+        n = has ? (uint32_t)mc_n[i] : 0u;
+        const int64_t d0 = g0 >> 2, nd = ((g1 + 3) >> 2) - d0;
+        const bool fits = nd <= 64 * kKtmWords;
+#pragma unroll
+        for (int k = 0; k < kKtmWords; k++) wds[k] = fits && lane + 64 * k < nd ? cw[d0 + lane + 64 * k] : 0u;
+    };
+    ld_gb(grp, c_g0, c_g1);
+    ld_group(grp, c_g0, c_g1, c_pos, c_n, c_w);
+    ld_gb(grp + nwaves, n_g0, n_g1);
+    for (; grp < ngroups; grp += nwaves) {
+        // in flight: the next group's columns, the byte range of the one after
+        ld_group(grp + nwaves, n_g0, n_g1, n_pos, n_n, n_w);
+        ld_gb(grp + 2 * nwaves, f_g0, f_g1);
         const int64_t i = (grp << 6) + lane;
         const bool has = i < n_entries;
-        const int32_t pos = has ? mc_pos[i] : 0;
-        const uint32_t n = has ? (uint32_t)mc_n[i] : 0u;
+        const uint32_t n = c_n;
         const uint32_t nb = n == 255u ? 0u : n;
         uint32_t incl = nb;
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t v = __shfl_up(incl, o, 64);
             if (lane >= o) incl += v;
         }
-        int64_t gb = mc_gbase[grp];
-        gb = ((int64_t)__builtin_amdgcn_readfirstlane((int32_t)(gb >> 32)) << 32) |
-             (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)gb);
-        const int64_t start = gb + (int64_t)(incl - nb), end = start + nb;
+        const int64_t d0 = c_g0 >> 2, nd = ((c_g1 + 3) >> 2) - d0;
+        const bool fits = nd <= 64 * kKtmWords;
+        if (fits) {
+#pragma unroll
+            for (int k = 0; k < kKtmWords; k++) buf[lane + 64 * k] = c_w[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int64_t start = c_g0 + (int64_t)(incl - nb), end = start + nb;
         bool keep = has;
         if (has && bound_on && n != 255u) {
             unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
             for (int64_t d = start >> 2; d < (end + 3) >> 2; d++) {
-                const uint32_t word = cw[d];
+                const uint32_t word = fits ? buf[d - d0] : cw[d];
 #pragma unroll
                 for (int b = 0; b < 4; b++) {
                     const int64_t at = d * 4 + b;
@@ -1369,7 +1408,12 @@ void k_scan_multi(const int32_t* __restrict__ mc_pos, const uint8_t* __restrict_
             keep = !drop;
             nexact++;
         }
-        if (keep) atomicOr(&need[pos >> 5], 1u << (pos & 31));
+        if (keep) atomicOr(&need[c_pos >> 5], 1u << (c_pos & 31));
+        __builtin_amdgcn_wave_barrier();
+        c_pos = n_pos; c_n = n_n; c_g0 = n_g0; c_g1 = n_g1;
+        n_g0 = f_g0; n_g1 = f_g1;
+#pragma unroll
+        for (int k = 0; k < kKtmWords; k++) c_w[k] = n_w[k];
     }
     for (int sft = 1; sft < 64; sft <<= 1) nexact += __shfl_xor(nexact, sft, 64);
     if (lane == 0) s_ne[wv] = nexact;
@@ -1583,6 +1627,8 @@ __device__ PopCall genotype_sample_d(const double* L, const int* cnt, int total,
     return c;
 }
 
+// POOL: ploidy >= 3 (the pool branch's report arrays would otherwise cost every run registers and scratch)
+template <bool POOL>
 __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
     const QueueSite* __restrict__ queue, const unsigned long long* qn, int64_t qcap,
     const uint8_t* __restrict__ ppile, const uint16_t* __restrict__ prow, const int64_t* __restrict__ pboff,
@@ -1617,13 +1663,15 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
         int total = 0;
         int cnt[4] = {0, 0, 0, 0};
         double L[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        const bool pool = ploidy >= 3;
+        constexpr bool pool = POOL;
         int32_t rows = 0;
         const uint8_t* col = nullptr;
         if (tid <= n_samples) {
-            const int64_t bi = (int64_t)(gpos >> kPopTileLog2) * (n_samples + 1) + tid;
+            // site-major tile (engine.hpp): the S + 1 columns of gpos are one contiguous run of stride bytes
+            const int64_t b0 = (int64_t)(gpos >> kPopTileLog2) * (n_samples + 1), bi = b0 + tid;
+            const int64_t stride = (pboff[b0 + n_samples + 1] - pboff[b0]) >> kPopTileLog2;
             rows = prow[bi];
-            col = ppile + pboff[bi] + (int64_t)(gpos & (kPopTile - 1)) * rows;
+            col = ppile + pboff[bi] + (int64_t)(gpos & (kPopTile - 1)) * stride;
             const bool tally = tid < n_samples && !pool;        // (the pool algorithm walks the column itself)
             for (int32_t r0 = 0; r0 < rows; r0 += 8) {
                 uint32_t code[8];
@@ -2703,7 +2751,7 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     if (ploidy >= 3 && !d->pool_valid) { err = "ploidy >= 3 without pool tables (device_set_pool)"; return -1; }
     // (no start event on KPM: a start event between KQN and KPM was measured to idle the device; KPM's time is
     // taken from KQN's end)
-    hipExtLaunchKernelGGL(k_posterior_multi, dim3(2048), dim3(kPopThreads), 0, d->stream, nullptr, d->ev[2], 0,
+    hipExtLaunchKernelGGL(ploidy >= 3 ? k_posterior_multi<true> : k_posterior_multi<false>, dim3(2048), dim3(kPopThreads), 0, d->stream, nullptr, d->ev[2], 0,
                           (const QueueSite*)(mknown ? d->d_mforced : d->d_hard),
                           (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : ctr + 2),
                           mknown ? std::max<int64_t>(d->n_mforced, 1) : d->cap_hard, (const uint8_t*)d->d_ppile,
@@ -2975,7 +3023,7 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
                           (const uint32_t*)m.d_need, (const uint8_t*)d->d_ref, nwords, m.d_hard, ctr, m.cap_hard);
     HIP_TRY(hipGetLastError());
     }
-    hipExtLaunchKernelGGL(k_posterior_multi, dim3(2048), dim3(kPopThreads), 0, d->stream, nullptr, m.ev[3], 0,
+    hipExtLaunchKernelGGL(ploidy >= 3 ? k_posterior_multi<true> : k_posterior_multi<false>, dim3(2048), dim3(kPopThreads), 0, d->stream, nullptr, m.ev[3], 0,
                           (const QueueSite*)(mknown ? d->d_mforced : m.d_hard),
                           (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : ctr + 2),
                           mknown ? std::max<int64_t>(d->n_mforced, 1) : m.cap_hard, (const uint8_t*)d->d_ppile,
