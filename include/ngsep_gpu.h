@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define NGSEP_ABI_VERSION 6
+#define NGSEP_ABI_VERSION 7
 
 #define NGSEP_OK 0
 #define NGSEP_E_INVALID (-1)      /* bad argument / state */
@@ -201,6 +201,15 @@ typedef struct ngsep_stats {
  * variant with a pileup gets a record (hom-ref, het, hom-alt or undecided, QUAL = its input QUAL, ID kept).
  * Call after the reference is loaded; NULL or "" returns to discovery.  Other variant types: E_UNSUPPORTED. */
 int  ngsep_set_known_variants(ngsep_ctx* c, const char* vcf_path);
+
+/* ---- -knownSTRs (ABI 7; SingleSampleVariantsDetector.findSNVS :906-912, makeNonRedundantSTRs :843-894) ----
+ * Regions "sequence first last" (1-based, space or tab separated; SimpleGenomicRegionFileHandler.loadRegions) merged
+ * into the indel realigner's input STR variants [first - 1, last + 1]: at an STR's first position the pileup takes the
+ * STR's span and is genotyped as an STR (TYPE=STR whatever its allele lengths), inside it the pileup is embedded.  Every
+ * STR opens a realigner region like an alignment with an indel (ngsep_fetch_carved_regions' geometry).  Single-sample
+ * discovery only; -knownVariants takes precedence, as in the reference.  Call after the reference is loaded; NULL or ""
+ * clears them. */
+int  ngsep_set_known_strs(ngsep_ctx* c, const char* path);
 
 /* ---- RelativeAlleleCountsCalculator (params.relative_allele_counts) ---- */
 /* RelativeAlleleCountsCalculator.runProcess + printResults (:183-244) on a BAM: the report text to out_path */

@@ -200,6 +200,7 @@ SIGNATURES = {
     "ngsep_coverage_bam": (ctypes.c_int, [_CTX, ctypes.c_char_p, ctypes.c_char_p]),
     "ngsep_rac_bam": (ctypes.c_int, [_CTX, ctypes.c_char_p, ctypes.c_char_p]),
     "ngsep_set_known_variants": (ctypes.c_int, [_CTX, ctypes.c_char_p]),
+    "ngsep_set_known_strs": (ctypes.c_int, [_CTX, ctypes.c_char_p]),
     "ngsep_fetch_rac": (ctypes.c_int, [_CTX, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_double)]),
     "ngsep_write_rac": (ctypes.c_int, [_CTX, ctypes.c_char_p]),
     "ngsep_clear_rac": (ctypes.c_int, [_CTX]),

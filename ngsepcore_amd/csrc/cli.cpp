@@ -173,7 +173,7 @@ static int main_rac(int argc, char** argv, int i) {
 int main(int argc, char** argv) {
     ngsep_params p;
     ngsep_params_default(&p);
-    const char *in = nullptr, *ref = nullptr, *outp = nullptr, *known = nullptr;
+    const char *in = nullptr, *ref = nullptr, *outp = nullptr, *known = nullptr, *strs = nullptr;
     int device = 0;
     int i = 1;
     if (i < argc && std::strcmp(argv[i], "MultisampleVariantsDetector") == 0) return main_mvd(argc, argv, i + 1);
@@ -202,6 +202,7 @@ int main(int argc, char** argv) {
         else if (takes("-last")) p.query_last = std::atoi(v);
         else if (takes("-device")) device = std::atoi(v);
         else if (takes("-knownVariants")) known = v;
+        else if (takes("-knownSTRs")) strs = v;
         else if (!std::strcmp(a, "-psp")) p.print_sample_ploidy = 1;
         else if (!std::strcmp(a, "-p")) p.process_nonunique = 1;
         else if (!std::strcmp(a, "-s")) p.process_secondary = 1;
@@ -216,6 +217,7 @@ int main(int argc, char** argv) {
     if (rc != NGSEP_OK) { std::fprintf(stderr, "error: %s\n", c ? ngsep_last_error(c) : "open failed"); return 1; }
     rc = ngsep_load_fasta(c, ref);
     if (rc == NGSEP_OK && known) rc = ngsep_set_known_variants(c, known);
+    else if (rc == NGSEP_OK && strs) rc = ngsep_set_known_strs(c, strs);   // (:897-912: -knownVariants first)
     std::string vcf = std::string(outp) + ".vcf";
     if (rc == NGSEP_OK) rc = ngsep_call_bam(c, in, vcf.c_str());
     if (rc != NGSEP_OK) { std::fprintf(stderr, "error %d: %s\n", rc, ngsep_last_error(c)); ngsep_close(c); return 1; }

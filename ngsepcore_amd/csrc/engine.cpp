@@ -368,6 +368,19 @@ static inline void admit_index(ngsep_ctx* c, int32_t i) {
     if (!c->params.coverage_stats) c->to_project.push_back(i);
     admit_core(c, b->first[i], c->cur_batch.last[i], b->flags[i], b->read_group ? b->read_group[i] : -1, c->cur_batch.indel[i]);
 }
+// -knownSTRs: the input STRs of the current sequence that start at or before `upto` join the realigner's events
+// (IndelRealignerPileupListener realigns around every input variant, :85-126), in start order among the indel reads,
+// so they open regions of the same reach (carve_indel_regions, keep_raw, stream_launch)
+static void inject_strs(ngsep_ctx* c, int64_t upto) {
+    ContigReads& cr = c->contig;
+    if (cr.seq_id < 0 || (size_t)cr.seq_id >= c->strs.size() || !c->known.empty()) return;
+    const std::vector<StrVar>& v = c->strs[(size_t)cr.seq_id];
+    while (c->str_next < v.size() && (int64_t)v[c->str_next].first <= upto) {
+        cr.indel_reads.push_back({v[c->str_next].first, v[c->str_next].last});
+        c->str_next++;
+    }
+}
+
 static void admit_core(ngsep_ctx* c, int32_t first, int32_t last, int32_t flags, int32_t rg, int32_t indel_len) {
     struct { int32_t first, flags, rg, indel_len; } r{first, flags, rg, indel_len};
     ContigReads& cr = c->contig;
@@ -387,6 +400,7 @@ static void admit_core(ngsep_ctx* c, int32_t first, int32_t last, int32_t flags,
         c->stats.alignments_admitted++;
         return;
     }
+    if (!c->strs.empty()) inject_strs(c, r.first);
     cr.first.push_back(r.first);
     cr.last.push_back(last);
     cr.neg.push_back((r.flags & 0x10) ? 1 : 0);
@@ -632,6 +646,7 @@ static int flush_sequence(ngsep_ctx* c) {
     if (c->cur_seq < 0) return NGSEP_OK;
     process_same_start(c);
     project_pending(c);
+    if (!c->strs.empty()) inject_strs(c, INT64_MAX);      // the sequence's remaining input STRs
     int rc;
     if (streaming(c)) {
         // the sequence's remaining windows, then its genotyped-position count
@@ -1080,6 +1095,7 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed) {
             c->contig.seq_id = r.seq_id;
             c->contig.seq_len = (int64_t)c->seq_bases[(size_t)r.seq_id].size();
             c->cur_last = last;
+            c->str_next = 0;                             // IndelRealignerPileupListener.onSequenceStart (:128-133)
             if (c->params.relative_allele_counts) {      // onSequenceStart (RelativeAlleleCountsCalculator.java:312-322)
                 if (c->contig.seq_len > 100000) {
                     c->rac.seq_names.push_back(c->seq_names[(size_t)r.seq_id]);
@@ -1995,7 +2011,8 @@ static int run_regions(ngsep_ctx* c, WindowJob* j, int64_t goff) {
     rp.ignore_lowercase = c->params.ignore_lowercase_ref != 0;
     parallel_for((int64_t)nr, 1, [&](int64_t a, int64_t b) {
         for (int64_t k = a; k < b; k++)
-            replay_region(seq, j->carved[(size_t)k].first, j->carved[(size_t)k].second, j->region_reads[(size_t)k], rp, outs[(size_t)k]);
+            replay_region(seq, j->carved[(size_t)k].first, j->carved[(size_t)k].second, j->region_reads[(size_t)k], rp,
+                          (size_t)j->seq_id < c->strs.size() ? &c->strs[(size_t)j->seq_id] : nullptr, outs[(size_t)k]);
     });
     // KP's queue: {global position, reference code, column offset / 4, entries} per callable position
     Staged& s = c->staged;
@@ -2571,6 +2588,114 @@ extern "C" int ngsep_clear_sites(ngsep_ctx* c) {
 // SNVs (one-base REF and ALT in ACGT) are genotyped here; ALT '.' records are skipped, as are records on
 // sequences outside the reference; any other variant is refused (E_UNSUPPORTED: the indel / multi-allelic
 // genotyping of genotypeVariantSample is not in this build).  path NULL or "": back to discovery.
+// ---- -knownSTRs ----
+// Integer.parseInt: an optional sign and decimal digits, inside the int range
+static bool parse_java_int(const char* t, int32_t* out) {
+    const char* q = t;
+    bool neg = false;
+    if (*q == '-' || *q == '+') { neg = *q == '-'; q++; }
+    if (!*q) return false;
+    int64_t v = 0;
+    for (; *q; q++) {
+        if (*q < '0' || *q > '9') return false;
+        v = v * 10 + (*q - '0');
+        if (v > 2147483648LL) return false;
+    }
+    if (neg) v = -v;
+    if (v > INT32_MAX || v < INT32_MIN) return false;
+    *out = (int32_t)v;
+    return true;
+}
+
+// ReferenceGenome.getReference(first, last) upper-cased (ReferenceGenome.java:217-237: absent outside [1, length])
+static bool ref_upper(const std::string& seq, int64_t first, int64_t last, std::string* out) {
+    if (first < 1 || last > (int64_t)seq.size() || last < first - 1) return false;
+    out->assign(seq, (size_t)first - 1, (size_t)(last - first + 1));
+    for (char& ch : *out) if (ch >= 'a' && ch <= 'z') ch = (char)(ch - 32);
+    return true;
+}
+
+// SingleSampleVariantsDetector.mergeSTRs (:873-881) with AbstractLimitedSequence.getOverlapLength
+// (sequences/AbstractLimitedSequence.java:376-390: the longest suffix of the first that prefixes the second)
+static bool merge_strs(const std::string& seq, int64_t first, int64_t last, int64_t rfirst, int64_t rlast) {
+    if (rfirst - last > 5) return false;
+    if (rfirst - last <= 2) return true;
+    std::string a, b;
+    if (!ref_upper(seq, std::max(first, last - 10), last, &a) || !ref_upper(seq, rfirst, rlast, &b)) return false;
+    for (size_t i = 0; i < a.size(); i++) {
+        const size_t l = a.size() - i;
+        if (l <= b.size() && a.compare(i, l, b, 0, l) == 0) return l > 5;
+    }
+    return false;
+}
+
+extern "C" int ngsep_set_known_strs(ngsep_ctx* c, const char* path) {
+    if (!c) return NGSEP_E_INVALID;
+    c->strs.clear();
+    if (!path || !path[0]) return NGSEP_OK;
+    if (c->seq_names.empty()) return set_error(c, NGSEP_E_INVALID, "load the reference before the known STRs");
+    if (c->params.coverage_stats || c->params.relative_allele_counts || c->params.multisample)
+        return set_error(c, NGSEP_E_INVALID, "known STRs are an option of SingleSampleVariantsDetector only");
+    std::FILE* f = std::fopen(path, "r");
+    if (!f) return set_error(c, NGSEP_E_IO, std::string("cannot read ") + path);
+    std::unordered_map<std::string, int32_t> idx;
+    for (size_t i = 0; i < c->seq_names.size(); i++) idx[c->seq_names[i]] = (int32_t)i;
+    // SimpleGenomicRegionFileHandler.loadRegions (genome/io/SimpleGenomicRegionFileHandler.java:57-80): fields split at
+    // every space or tab; a line whose name, first or last does not parse is skipped (a warning there)
+    std::vector<std::vector<StrVar>> per(c->seq_names.size());
+    char* line = nullptr;
+    size_t cap = 0;
+    ssize_t l;
+    while ((l = getline(&line, &cap, f)) >= 0) {
+        while (l > 0 && (line[l - 1] == '\n' || line[l - 1] == '\r')) line[--l] = 0;
+        const char* fld[3];
+        int k = 0;
+        char* p = line;
+        while (k < 3) {
+            fld[k++] = p;
+            char* t = p;
+            while (*t && *t != ' ' && *t != '\t') t++;
+            if (!*t) break;
+            *t = 0;
+            p = t + 1;
+        }
+        int32_t a, b;
+        if (k < 3 || !parse_java_int(fld[1], &a) || !parse_java_int(fld[2], &b)) continue;
+        auto it = idx.find(fld[0]);
+        if (it == idx.end() || b < a - 1) continue;   // (a sequence the genome lacks is never emitted; subSequence would throw)
+        per[(size_t)it->second].push_back(StrVar{a, b});
+    }
+    std::free(line);
+    std::fclose(f);
+    // makeNonRedundantSTRs / makeSTRVariant (SingleSampleVariantsDetector.java:843-894): per sequence, in
+    // GenomicRegionPositionComparator order (first, then last; stable), runs of mergeable regions become one variant
+    // [first - 1, last + 1] clipped to the sequence (`last` is the run's LAST region's end)
+    c->strs.assign(c->seq_names.size(), {});
+    for (size_t sq = 0; sq < per.size(); sq++) {
+        std::vector<StrVar>& v = per[sq];
+        if (v.empty()) continue;
+        std::stable_sort(v.begin(), v.end(), [](const StrVar& x, const StrVar& y) { return x.first != y.first ? x.first < y.first : x.last < y.last; });
+        const std::string& seq = c->seq_bases[sq];
+        const int64_t len = (int64_t)seq.size();
+        std::vector<StrVar>& out = c->strs[sq];
+        auto emit = [&](int64_t first, int64_t last) {
+            const int64_t vf = std::max<int64_t>(1, first - 1), vl = std::min<int64_t>(last + 1, len);
+            if (vf >= 1 && vl <= len && vl >= vf - 1) out.push_back(StrVar{(int32_t)vf, (int32_t)vl});
+        };
+        int64_t first = 0, last = 0;
+        for (const StrVar& r : v) {
+            if (last == 0 || !merge_strs(seq, first, last, r.first, r.last)) {
+                if (last > 0) emit(first, last);
+                first = r.first;
+            }
+            last = r.last;
+        }
+        if (last > 0) emit(first, last);
+        std::stable_sort(out.begin(), out.end(), [](const StrVar& x, const StrVar& y) { return x.first != y.first ? x.first < y.first : x.last < y.last; });
+    }
+    return NGSEP_OK;
+}
+
 extern "C" int ngsep_set_known_variants(ngsep_ctx* c, const char* vcf_path) {
     if (!c) return NGSEP_E_INVALID;
     c->known.clear();

@@ -140,7 +140,8 @@ struct GenotypeParams {
     int32_t ablate;            // diagnostics only (env NGSEP_ABLATE): 1 scan only (no bound, no queue),
                                // 8 tally without posterior, 16 posterior kernel reads the queue only,
                                // 32 population kernel gathers only, 64 population kernel stops after the tallies,
-                               // 128 KL without the exception counters, 256 KL without the read bases
+                               // 128 KL without the exception counters, 256 KL without the read bases,
+                               // 32768 KTM without the column bounds
     int32_t use_bound;         // 1: candidates proven hom-ref by the integer bound are dropped in the tile kernel
     int32_t full_records;      // 1: every record whole (ngsep_params.full_records); dump mode implies it
     int32_t ploidy;            // >= 3: KP runs the pool algorithm (k_posterior_pool), KT queues every
@@ -576,6 +577,10 @@ struct ngsep_ctx {
     struct KnownVar { int32_t seq, pos; int8_t ref, alt; int16_t qs; std::string id; };
     std::vector<KnownVar> known;
     std::vector<int64_t> known_seq_begin;                    // per sequence: first entry (size n_seq + 1)
+    // -knownSTRs (ngsep_set_known_strs): per sequence, the indel realigner's input STR variants (sorted, disjoint);
+    // str_next: the next one of the current sequence to enter its realigner regions (engine.cpp inject_strs)
+    std::vector<std::vector<ngsep::StrVar>> strs;
+    size_t str_next = 0;
     mutable struct { int32_t seq = -1, pos = -1; std::vector<int64_t> taken; } vcf_known;   // known_id: the position written
     // RelativeAlleleCountsCalculator mode (params.relative_allele_counts): its Distributions
     struct {

@@ -1,19 +1,22 @@
 // kernels.hip -- gfx950 kernels of the NGSEP SNV pileup path.
 //
-//   KT  k_tile_scan<W> : single-sample scan of the valid-call plane and the other-allele lists (valid call /
-//        another allele, 2 bits per position-row), one wavefront per tile: bit-sliced counts of every
-//        position (LDS-free butterfly over row groups), the candidates (a valid non-reference call at a
-//        callable position) and the count bound as a table; survivors queued.  This is
-//        AlignmentsPileupGenerator.processCurrentPosition (discovery/AlignmentsPileupGenerator.java:475-498)
-//        reduced to the fact that decides whether SNVQ can call a variant there ("why
-//        pruning is exact").
+//   KL  k_read_scan<T, U> : single-sample scan straight from the read-group layout (1 B per read base, engine.hpp
+//        RGroup), one workgroup per tile of T positions: coverage from an LDS difference array, per-position
+//        exception / other-allele counters from SWAR over the reads' 8-byte units, the candidates (a valid
+//        non-reference call at a callable position) and the count bound as a table; survivors queued with their
+//        column space.  This is AlignmentsPileupGenerator.processCurrentPosition
+//        (discovery/AlignmentsPileupGenerator.java:475-498) reduced to the fact that decides whether SNVQ can call a
+//        variant there ("why pruning is exact").
+//   KG  k_gather_kl / k_gather_cols : the queued sites' columns (PileupRecord.getAlleleCalls(1) in pending order)
+//        gathered from the read-group layout, the queue compacted.
 //   KQ  k_queue_all : every in-window position queued (dump mode, runs without the exact pruning).
 //   KP  k_posterior : exact CountsHelper tally (pending-list order, bit-exact fp64), posterior and
 //        SNVQ call of the queued candidates (discovery/CountsHelper.java:83-95,209-251,410-495,
 //        VariantDiscoverySNVQAlgorithm.java:100-243, SingleSampleVariantPileupListener.java:213-232);
 //        records go to position buckets.
 //   KO  ko_fused : position order of the records (rank per bucket) and their (sequence, position).
-//   KTM / KPM k_tile_pileup_multi / k_posterior_multi : MultisampleVariantsDetector.
+//   KTM / KQN / KPM k_scan_multi / k_queue_need / k_posterior_multi : MultisampleVariantsDetector.
+//   KR  k_rac : RelativeAlleleCountsCalculator over the tile-blocked byte pile (engine.cpp build_single_layout).
 //
 // HBM-bound integer/byte work: no MFMA.  Layout and roofline: DESIGN.md.
 #include <hip/hip_runtime.h>
@@ -1379,7 +1382,8 @@ void k_scan_multi(const int32_t* __restrict__ mc_pos, const uint8_t* __restrict_
         __builtin_amdgcn_wave_barrier();
         const int64_t start = c_g0 + (int64_t)(incl - nb), end = start + nb;
         bool keep = has;
-        if (has && bound_on && n != 255u) {
+        if (gp.ablate & 32768) keep = false;               // diagnostics: metadata and staging only
+        if (has && bound_on && n != 255u && !(gp.ablate & 32768)) {
             unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
             for (int64_t d = start >> 2; d < (end + 3) >> 2; d++) {
                 const uint32_t word = fits ? buf[d - d0] : cw[d];
@@ -3013,7 +3017,8 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
     } else {
     HIP_TRY(hipMemsetAsync(m.d_need, 0, (size_t)nwords * sizeof(uint32_t), d->stream));
     const int64_t ngroups = (d->mc_entries + 63) / 64;
-    const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((ngroups + 3) / 4, (int64_t)d->n_cu * 8));
+    static const int ktm_env = std::getenv("NGSEP_KTM_BPC") ? std::max(1, std::atoi(std::getenv("NGSEP_KTM_BPC"))) : 8;   // tuning
+    const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((ngroups + 3) / 4, (int64_t)d->n_cu * ktm_env));
     hipExtLaunchKernelGGL(k_scan_multi, dim3((unsigned)nblk), dim3(256), 0, d->stream, m.ev[0], nullptr, 0,
                           (const int32_t*)d->d_mc_pos, (const uint8_t*)d->d_mc_n, (const int64_t*)d->d_mc_gbase,
                           (const uint8_t*)d->d_pile, d->mc_entries, (const LikTables*)d->d_tables, g, m.d_need, ctr);

@@ -305,17 +305,30 @@ public:
     Realigner(const std::string& seq) : seq_(seq) {}
 
     // onPileup without input variants (:85-126): the pileup's reference span
-    int on_pileup(const std::vector<Aln*>& alns, int pos, bool* is_str, bool* is_new_str) {
-        int maxLen = 0, maxSpan = 0;
-        for (const Aln* a : alns)
-            if (const IndelEv* e = a->indel_at(pos)) {
-                maxLen = std::max(maxLen, e->len);
-                maxSpan = std::max(maxSpan, e->last - e->first + 1);
+    // var: the input STR intersectWithVariants found at pos (:137-153), or null.  At its first position the span is
+    // the variant's and the pileup an STR (:90-95); inside it the pileup is embedded (:96-98, *embedded)
+    int on_pileup(const std::vector<Aln*>& alns, int pos, const StrVar* var, bool* is_str, bool* is_new_str, bool* embedded) {
+        int span = 1, predictedEnd = pos;
+        if (var) {
+            if (var->first == pos) {
+                *is_str = true;
+                span = var->last - var->first + 1;
+                predictedEnd = var->last;
+            } else {
+                *embedded = true;
             }
-        if (maxLen <= 0) return 1;
-        const int predictedEnd = pos + std::max(maxLen, maxSpan) + 1;
-        const int c = conciliate(alns, pos, predictedEnd, is_str, is_new_str);
-        return c > 0 ? c : 1;
+        } else {
+            int maxLen = 0, maxSpan = 0;
+            for (const Aln* a : alns)
+                if (const IndelEv* e = a->indel_at(pos)) {
+                    maxLen = std::max(maxLen, e->len);
+                    maxSpan = std::max(maxSpan, e->last - e->first + 1);
+                }
+            if (maxLen > 0) predictedEnd = pos + std::max(maxLen, maxSpan) + 1;
+        }
+        if (predictedEnd <= pos) return span;
+        const int c = conciliate(alns, pos, predictedEnd, var != nullptr, is_str, is_new_str);
+        return c > 0 ? c : span;
     }
 
 private:
@@ -498,9 +511,8 @@ private:
     }
 
     // conciliateIndels (:165-216) with analyzeIndels (:229-265); the reference span if indels are called, else 0
-    int conciliate(const std::vector<Aln*>& alns, int pos, int eventEnd, bool* is_str, bool* is_new_str) {
-        int answer = 0, maxLength = 0;
-        bool fixedEvent = false;
+    int conciliate(const std::vector<Aln*>& alns, int pos, int eventEnd, bool fixedEvent, bool* is_str, bool* is_new_str) {
+        int answer = 0, maxLength = 0;                   // fixedEvent: varG != null (an input STR)
         const int nvotes = eventEnd - pos + 1;
         std::vector<int> votes((size_t)nvotes, 0), lengths;
         std::vector<Aln*> indelAlns;
@@ -516,8 +528,8 @@ private:
                 }
         if (lengths.empty()) return 0;
         int maxI = 0;
-        for (int i = 1; i < nvotes; i++) if (votes[(size_t)maxI] < votes[(size_t)i]) maxI = i;   // getIndexMaximum
-        if (lengths.size() > 1) {
+        if (!fixedEvent) for (int i = 1; i < nvotes; i++) if (votes[(size_t)maxI] < votes[(size_t)i]) maxI = i;   // getIndexMaximum
+        if (!fixedEvent && lengths.size() > 1) {
             const int span = new_str(pos, indelAlns, maxLength);
             if (span > 1) {
                 maxI = 0;
@@ -686,7 +698,7 @@ inline double log_sum(double a, double b) {
 // calculateCountsIndel + updateCountsIndel (CountsHelper.java:96-105,253-304), calculateLogCond (:384-396), then
 // callIndel (VariantDiscoverySNVQAlgorithm.java:265-361) and the listener's filters; the VCF fields of a kept call
 bool genotype_indel(const std::vector<std::string>& alleles, const std::vector<SpanCall>& calls, int pos, bool is_str,
-                    const RealignParams& p, IndelCall* out) {
+                    bool is_input_str, const RealignParams& p, IndelCall* out) {
     const int n = (int)alleles.size();
     const int maxBaseQS = (int8_t)p.max_base_qs > 0 ? (int8_t)p.max_base_qs : 30;
     const int f = (int)java_round(0.5 * kNumFreq);                     // (:256: 501, not 500)
@@ -766,7 +778,7 @@ bool genotype_indel(const std::vector<std::string>& alleles, const std::vector<S
         lengthChange |= alleles[(size_t)im1].size() != lref;
         if (na == 3 && alleles[(size_t)im1].size() != alleles[(size_t)idx[1]].size()) lengthChange = true;
     }
-    if (!lengthChange) return false;                                      // (no input STR in discovery)
+    if (!lengthChange && !is_input_str) return false;                     // (:318: an input STR is called whatever its lengths)
     int ncalled, called[2];
     if (im1 != im0) { ncalled = 2; called[0] = na == 3 ? 1 : 0; called[1] = na == 3 ? 2 : 1; }
     else { ncalled = 1; called[0] = im0 == 0 ? 0 : 1; }
@@ -825,7 +837,7 @@ bool genotype_indel(const std::vector<std::string>& alleles, const std::vector<S
 }  // namespace
 
 void replay_region(const std::string& seq, int64_t first, int64_t last, std::vector<RawRead>& reads, const RealignParams& p,
-                   RegionOut& out) {
+                   const std::vector<StrVar>* strs, RegionOut& out) {
     out.first = first;
     out.last = last;
     out.pos.clear();
@@ -853,6 +865,9 @@ void replay_region(const std::string& seq, int64_t first, int64_t last, std::vec
     std::vector<SpanCall> calls;
     size_t next = 0;
     const int seq_len = (int)seq.size();
+    // idxNextVariant: the input STRs are sorted and disjoint, so the first one ending at or after the region's start
+    size_t vi = 0, vn = strs ? strs->size() : 0;
+    if (vn) vi = (size_t)(std::lower_bound(strs->begin(), strs->end(), first, [](const StrVar& v, int64_t x) { return (int64_t)v.last < x; }) - strs->begin());
     for (int64_t p64 = first; p64 <= last; p64++) {
         const int pos = (int)p64;
         while (next < alns.size() && reads[next].first <= pos) pending.push_back((int32_t)next++);   // (original starts)
@@ -865,7 +880,14 @@ void replay_region(const std::string& seq, int64_t first, int64_t last, std::vec
         if (pileup.empty()) continue;
         RegionPos rp;
         rp.pos = pos;
-        rp.span = rl.on_pileup(pileup, pos, &rp.str, &rp.new_str);
+        const StrVar* var = nullptr;                                       // intersectWithVariants (:137-153)
+        while (vi < vn) {
+            const StrVar& v = (*strs)[vi];
+            if (pos < v.first) break;
+            if (pos <= v.last) { var = &v; break; }
+            vi++;
+        }
+        rp.span = rl.on_pileup(pileup, pos, var, &rp.str, &rp.new_str, &rp.var_embedded);
         // getAlleleCalls(1): the device's column entries (engine.cpp project_read's codes)
         rp.col_off = (int32_t)out.cols.size();
         for (const Aln* a : pileup) {
@@ -894,7 +916,7 @@ void replay_region(const std::string& seq, int64_t first, int64_t last, std::vec
             span_calls(pileup, pos, rp.span, calls);
             const std::vector<std::string> alleles = cluster_alleles(calls, reference, p.max_base_qs);
             IndelCall ic;
-            if (genotype_indel(alleles, calls, pos, rp.str, p, &ic)) {
+            if (genotype_indel(alleles, calls, pos, rp.str, rp.str && !rp.new_str, p, &ic)) {
                 rp.indel = (int32_t)out.indels.size();
                 out.indels.push_back(std::move(ic));
             }
@@ -916,8 +938,11 @@ void resolve_region(const RegionOut& out, const std::vector<uint8_t>& has_snv_ca
     dec.clear();
     for (size_t i = 0; i < out.pos.size(); i++) {
         const RegionPos& rp = out.pos[i];
-        // onPileup (:146-161): discovery has no input STRs, so only a decided indel call moves lastIndelEnd
-        const bool embedded = rp.pos <= *last_indel_end;
+        // onPileup (:146-161): an input STR moves lastIndelEnd to its end, a position up to lastIndelEnd is embedded
+        const bool input_str = rp.str && !rp.new_str;
+        bool embedded = rp.var_embedded;
+        if (input_str && rp.pos >= *last_indel_end) *last_indel_end = rp.pos + rp.span - 1;
+        else if (rp.pos <= *last_indel_end) embedded = true;
         if (!call_embedded && embedded) continue;
         if (rp.blocked) continue;
         const int eff = embedded ? 1 : rp.span;
@@ -926,6 +951,7 @@ void resolve_region(const RegionOut& out, const std::vector<uint8_t>& has_snv_ca
             *last_indel_end = out.indels[(size_t)rp.indel].last;
             continue;
         }
+        if (eff > 1 && input_str) continue;                                 // no SNV fallback for an input STR (:264)
         if (has_snv_call[i]) dec.push_back(RegionDecision{rp.pos, 1, embedded, -1});   // discoverSNV (and the fallback)
     }
 }

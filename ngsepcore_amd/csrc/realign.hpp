@@ -46,7 +46,8 @@ struct IndelCall {
 struct RegionPos {
     int32_t pos = 0;                   // 1-based
     int32_t span = 1;                  // the realigner's reference span
-    bool str = false, new_str = false;
+    bool str = false, new_str = false; // input STR = str && !new_str (PileupRecord.isInputSTR)
+    bool var_embedded = false;         // inside an input STR past its first position (the realigner's setEmbedded)
     int32_t col_off = 0, col_len = 0;  // span-1 column: u16 entries code | negative strand << 8 in RegionOut::cols
     int32_t indel = -1;                // span > 1: index into RegionOut::indels of the span's call (-1: none)
     bool blocked = false;              // no call at all (span past the sequence end, lower-case reference ignored)
@@ -59,11 +60,16 @@ struct RegionOut {
     std::vector<IndelCall> indels;
 };
 
+// an input STR variant of -knownSTRs (SingleSampleVariantsDetector.makeNonRedundantSTRs): 1-based [first, last]
+struct StrVar {
+    int32_t first, last;
+};
+
 // replays AlignmentsPileupGenerator + IndelRealignerPileupListener over [first, last] of one sequence (`seq`: the
 // reference as loaded, case kept); `reads` are the admitted alignments overlapping it in pending-list order
-// (edited in place)
+// (edited in place); `strs`: the sequence's input STR variants (sorted, disjoint; may be null)
 void replay_region(const std::string& seq, int64_t first, int64_t last, std::vector<RawRead>& reads, const RealignParams& p,
-                   RegionOut& out);
+                   const std::vector<StrVar>* strs, RegionOut& out);
 
 // the listener's decisions over a replayed region, position by position: kind 0 nothing, 1 the position's SNV
 // call (flag embedded: TYPE=EMBEDDED), 2 the indel call out.indels[idx].  last_indel_end is the listener's

@@ -128,6 +128,10 @@ class GpuPileupSession:
         """-knownVariants (SingleSampleVariantsDetector.findSNVS :896-906): genotype these biallelic SNVs."""
         self._check(self._lib.ngsep_set_known_variants(self._ctx, vcf_path.encode() if vcf_path else None))
 
+    def set_known_strs(self, path: Optional[str]):
+        """-knownSTRs (SingleSampleVariantsDetector.findSNVS :906-912): input STRs for the indel realigner."""
+        self._check(self._lib.ngsep_set_known_strs(self._ctx, path.encode() if path else None))
+
     def set_reference(self, name: str, bases: bytes):
         self._check(self._lib.ngsep_set_reference(self._ctx, name.encode(), bases, len(bases)))
 
@@ -319,11 +323,14 @@ class SingleSampleVariantsDetector:
         self.genomeFile: Optional[str] = None
         self.outputPrefix: Optional[str] = None
         self.knownVariantsFile: Optional[str] = None
+        self.knownSTRsFile: Optional[str] = None
         self.device = 0
 
     # setters (CommandsDescriptor reflective setters)
     def setKnownVariantsFile(self, v: str): self.knownVariantsFile = v
     def getKnownVariantsFile(self) -> Optional[str]: return self.knownVariantsFile
+    def setKnownSTRsFile(self, v: str): self.knownSTRsFile = v                   # (:400-402)
+    def getKnownSTRsFile(self) -> Optional[str]: return self.knownSTRsFile
     def setInputFile(self, v: str): self.inputFile = v
     def setGenome(self, v: str): self.genomeFile = v
     def setOutputPrefix(self, v: str): self.outputPrefix = v
@@ -357,6 +364,7 @@ class SingleSampleVariantsDetector:
         "-minQuality": ("setMinQuality", int), "-querySeq": ("setQuerySeq", str),
         "-first": ("setQueryFirst", int), "-last": ("setQueryLast", int),
         "-knownVariants": ("setKnownVariantsFile", str),
+        "-knownSTRs": ("setKnownSTRsFile", str),
     }
     _FLAGS = {
         "-psp": "setPrintSamplePloidy", "-p": "setProcessNonUniquePrimaryAlignments",
@@ -392,6 +400,8 @@ class SingleSampleVariantsDetector:
             s.load_fasta(self.genomeFile)
             if self.knownVariantsFile:
                 s.set_known_variants(self.knownVariantsFile)
+            elif self.knownSTRsFile:
+                s.set_known_strs(self.knownSTRsFile)
             s.processFile(self.inputFile, (self.outputPrefix or "variants") + ".vcf")
             self.stats = s.stats()
 

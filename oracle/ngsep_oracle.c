@@ -727,6 +727,7 @@ static void acalls_push(ngo_acalls* l, int base, int q, int neg) {
 }
 
 struct ngo_mvd;
+typedef struct ngo_strv { int seq, first, last; } ngo_strv;   /* an input STR variant (-knownSTRs) */
 typedef struct {
     const ngo_params* p;
     struct ngo_mvd* mvd;       /* MultisampleVariantsDetector listener instead of the single-sample one */
@@ -748,6 +749,8 @@ typedef struct {
     int realign;               /* IndelRealignerPileupListener active (single-sample discovery, ploidy < 3) */
     int last_indel_end;        /* SingleSampleVariantPileupListener.lastIndelEnd, :143 */
     ngo_alist pileup;          /* the position's alignments (PileupRecord.getAlignments) */
+    struct ngo_strv* strs;     /* -knownSTRs: the realigner's input STR variants (sequence order, then first, last) */
+    int n_strs, str_next;      /* str_next: IndelRealignerPileupListener.idxNextVariant over the whole list */
 } ngo_gen;
 
 /* ------------------------------------------------------------------ */
@@ -1485,11 +1488,11 @@ static void push_call(ngo_gen* G, const ngo_call* c) {
 /* SingleSampleVariantPileupListener.onPileup (no input variants, :146-161) -> calculateReferenceAlleleDiscovery
  * (:191-206) -> discoverVariant (:213-232) with the pileup's reference span from the indel realigner: span 1 is
  * discoverSNV over `h`, a longer span discoverVariantWithSpan (:257-273) */
-static void discover_with_span(ngo_gen* G, int pos, int span, int is_str, int is_new_str, const ngo_counts* h) {
+static void discover_with_span(ngo_gen* G, int pos, int span, int is_str, int is_new_str, int r_embedded, const ngo_counts* h) {
     const ngo_params* p = G->p;
     const ngo_seq* s = &G->g->s[G->cur_seq];
     const int is_input_str = is_str && !is_new_str;
-    int embedded = 0;
+    int embedded = r_embedded;                                   /* inside an input STR (the realigner's flag) */
     if (is_input_str && pos >= G->last_indel_end) G->last_indel_end = pos + span - 1;
     else if (pos <= G->last_indel_end) embedded = 1;
     if (!p->call_embedded && embedded) return;
@@ -1581,7 +1584,7 @@ static int process_current_position(ngo_gen* G) {
         return numAlignments > 0;
     }
     int numAlignments = 0;
-    int span = 1, is_str = 0, is_new_str = 0;
+    int span = 1, is_str = 0, is_new_str = 0, r_embedded = 0;
     if (G->realign) {
         /* IndelRealignerPileupListener.onPileup runs first and may edit the alignments (:85-126) */
         G->pileup.n = 0;
@@ -1589,7 +1592,18 @@ static int process_current_position(ngo_gen* G) {
             ngo_aln* a = G->pending.a[k];
             if (a->first <= pos && a->last >= pos) alist_push(&G->pileup, a);
         }
-        if (G->pileup.n > 0) span = realigner_on_pileup(&G->g->s[G->cur_seq], G->pileup.a, G->pileup.n, pos, &is_str, &is_new_str);
+        if (G->pileup.n > 0) {
+            int var_first = 0, var_last = 0;
+            /* intersectWithVariants (IndelRealignerPileupListener.java:137-153) over the input STRs */
+            while (G->str_next < G->n_strs && G->strs[G->str_next].seq == G->cur_seq) {
+                const ngo_strv* v = &G->strs[G->str_next];
+                if (pos < v->first) break;
+                if (pos <= v->last) { var_first = v->first; var_last = v->last; break; }
+                G->str_next++;
+            }
+            span = realigner_on_pileup(&G->g->s[G->cur_seq], G->pileup.a, G->pileup.n, pos, var_first, var_last, &is_str,
+                                       &is_new_str, &r_embedded);
+        }
     }
     ngo_counts h;
     ngo_counts_init(&h, 4, 0.5, p->max_base_qs);     /* CountsHelper.calculateCountsSNV(calls, maxBaseQS, 0.5) */
@@ -1633,7 +1647,7 @@ static int process_current_position(ngo_gen* G) {
                 G->calls.c[G->calls.n++] = c;
             }
         } else if (G->realign) {
-            discover_with_span(G, pos, span, is_str, is_new_str, &h);
+            discover_with_span(G, pos, span, is_str, is_new_str, r_embedded, &h);
         } else if (!(p->ignore_lowercase_ref && islower((unsigned char)r))) {
             char R = (char)toupper((unsigned char)r);
             ngo_call c;
@@ -1717,6 +1731,8 @@ static void process_alignment(ngo_gen* G, ngo_aln* a) {
         G->cur_seq = a->seq; G->cur_pos = a->first; G->cur_last = a->last;
         if (G->rac) rac_on_sequence_start(G, a->seq);
         G->last_indel_end = 0;                                 /* SingleSampleVariantPileupListener.onSequenceStart, :186 */
+        G->str_next = 0;                                       /* IndelRealignerPileupListener.onSequenceStart, :128-133 */
+        while (G->str_next < G->n_strs && G->strs[G->str_next].seq != a->seq) G->str_next++;
         if (G->known) {          /* onSequenceStart: this sequence's input variants, nextSIVIndex = 0 */
             G->known_next = 0;
             while (G->known_next < G->n_known && G->known[G->known_next].seq != a->seq) G->known_next++;
@@ -1796,6 +1812,133 @@ static int load_known(const char* path, const ngo_genome* g, ngo_known** out, in
     return NGO_OK;
 }
 
+/* ---- -knownSTRs ---- */
+
+/* Integer.parseInt: an optional sign and decimal digits, within the int range */
+static int java_parse_int(const char* t, int* out) {
+    const char* c = t;
+    int neg = 0;
+    if (*c == '-' || *c == '+') { neg = *c == '-'; c++; }
+    if (!*c) return 0;
+    long long v = 0;
+    for (; *c; c++) {
+        if (*c < '0' || *c > '9') return 0;
+        v = v * 10 + (*c - '0');
+        if (v > 2147483648LL) return 0;
+    }
+    if (neg) v = -v;
+    if (v > 2147483647LL || v < -2147483648LL) return 0;
+    *out = (int)v;
+    return 1;
+}
+
+/* genome.getReference(seq, first, last) upper-cased (ReferenceGenome.java:217-237: null outside [1, length]) */
+static char* ref_sub_upper(const ngo_seq* s, int first, int last) {
+    if (first < 1 || last > s->len || last < first - 1) return NULL;
+    const int n = last - first + 1;
+    char* r = malloc((size_t)n + 1);
+    for (int i = 0; i < n; i++) r[i] = (char)toupper((unsigned char)s->seq[first - 1 + i]);
+    r[n] = 0;
+    return r;
+}
+
+/* AbstractLimitedSequence.getOverlapLength (sequences/AbstractLimitedSequence.java:376-390): the longest suffix of a
+ * that is a prefix of b (a suffix longer than b never matches) */
+static int overlap_length(const char* a, const char* b) {
+    const int la = (int)strlen(a), lb = (int)strlen(b);
+    for (int i = 0; i < la; i++) {
+        if (la - i > lb) continue;
+        if (memcmp(a + i, b, (size_t)(la - i)) == 0) return la - i;
+    }
+    return 0;
+}
+
+/* SingleSampleVariantsDetector.mergeSTRs (:873-881) */
+static int merge_strs(const ngo_seq* s, int first, int last, int rfirst, int rlast) {
+    if (rfirst - last > 5) return 0;
+    if (rfirst - last <= 2) return 1;
+    char* r1 = ref_sub_upper(s, first > last - 10 ? first : last - 10, last);
+    char* r2 = ref_sub_upper(s, rfirst, rlast);
+    int ans = 0;
+    if (r1 && r2) ans = overlap_length(r1, r2) > 5;
+    free(r1); free(r2);
+    return ans;
+}
+
+static int strv_cmp(const void* a, const void* b) {
+    const ngo_strv* x = a; const ngo_strv* y = b;
+    if (x->seq != y->seq) return x->seq - y->seq;
+    if (x->first != y->first) return x->first < y->first ? -1 : 1;
+    return x->last < y->last ? -1 : x->last > y->last;
+}
+
+/* SimpleGenomicRegionFileHandler.loadRegions (genome/io/SimpleGenomicRegionFileHandler.java:57-80: fields split at
+ * every space or tab, lines whose name / first / last do not parse are skipped) + makeNonRedundantSTRs / mergeSTRs /
+ * makeSTRVariant (SingleSampleVariantsDetector.java:843-894).  Regions on sequences the genome does not hold are
+ * never emitted (makeNonRedundantSTRs walks the genome's sequences); a region with last < first - 1 (Java's
+ * subSequence would throw) is skipped. */
+static int load_known_strs(const char* path, const ngo_genome* g, ngo_strv** out, int* n_out) {
+    FILE* f = fopen(path, "r");
+    if (!f) return NGO_ERR_IO;
+    char* line = NULL; size_t cap = 0; ssize_t l;
+    ngo_strv* v = NULL; int n = 0, vc = 0;
+    while ((l = getline(&line, &cap, f)) >= 0) {
+        while (l > 0 && (line[l - 1] == '\n' || line[l - 1] == '\r')) line[--l] = 0;
+        char* fld[3]; int k = 0; char* s2 = line;
+        while (k < 3) {
+            fld[k++] = s2;
+            char* t = s2;
+            while (*t && *t != ' ' && *t != '\t') t++;
+            if (!*t) break;
+            *t = 0; s2 = t + 1;
+        }
+        if (k < 3) continue;
+        int a, b;
+        if (!java_parse_int(fld[1], &a) || !java_parse_int(fld[2], &b)) continue;
+        const int seq = genome_find(g, fld[0]);
+        if (seq < 0 || b < a - 1) continue;
+        if (n == vc) { vc = vc ? 2 * vc : 256; v = realloc(v, sizeof(ngo_strv) * vc); }
+        v[n].seq = seq; v[n].first = a; v[n].last = b;
+        n++;
+    }
+    free(line); fclose(f);
+    /* GenomicRegionSortedCollection: per sequence, GenomicRegionPositionComparator (first, then last), stable */
+    int* ord = malloc(sizeof(int) * (n > 0 ? n : 1));
+    for (int i = 0; i < n; i++) ord[i] = i;
+    for (int i = 1; i < n; i++) {
+        int x = ord[i], j = i - 1;
+        while (j >= 0 && strv_cmp(&v[ord[j]], &v[x]) > 0) { ord[j + 1] = ord[j]; j--; }
+        ord[j + 1] = x;
+    }
+    ngo_strv* w = malloc(sizeof(ngo_strv) * (n > 0 ? n : 1));
+    int m = 0;
+    for (int i = 0; i < n;) {
+        const int seq = v[ord[i]].seq;
+        const ngo_seq* s = &g->s[seq];
+        int first = 0, last = 0;
+        for (; i < n && v[ord[i]].seq == seq; i++) {
+            const ngo_strv* r = &v[ord[i]];
+            if (last == 0 || !merge_strs(s, first, last, r->first, r->last)) {
+                if (last > 0) {
+                    const int vf = first - 1 > 1 ? first - 1 : 1, vl = last + 1 < s->len ? last + 1 : (int)s->len;
+                    if (vf >= 1 && vl <= s->len && vl >= vf - 1) { w[m].seq = seq; w[m].first = vf; w[m].last = vl; m++; }
+                }
+                first = r->first;
+            }
+            last = r->last;
+        }
+        if (last > 0) {
+            const int vf = first - 1 > 1 ? first - 1 : 1, vl = last + 1 < s->len ? last + 1 : (int)s->len;
+            if (vf >= 1 && vl <= s->len && vl >= vf - 1) { w[m].seq = seq; w[m].first = vf; w[m].last = vl; m++; }
+        }
+    }
+    free(v); free(ord);
+    /* the variants' collection is sorted again (same comparator) */
+    qsort(w, (size_t)m, sizeof(ngo_strv), strv_cmp);
+    *out = w; *n_out = m;
+    return NGO_OK;
+}
+
 static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
                         const char* dump_path, const ngo_params* p, ngo_stats* stats, double min_adf, int multisample,
                         ngo_coverage* cov, ngo_rac* rac) {
@@ -1823,6 +1966,12 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
         if (load_known(p->known_vcf, &g, &G.known, &G.n_known) != NGO_OK) {
             fclose(in); if (out != stdout) fclose(out); if (dump) fclose(dump);
             return NGO_UNSUPPORTED;
+        }
+    }
+    if (G.realign && p->known_strs && p->known_strs[0]) {
+        if (load_known_strs(p->known_strs, &g, &G.strs, &G.n_strs) != NGO_OK) {
+            fclose(in); if (out != stdout) fclose(out); if (dump) fclose(dump);
+            return NGO_ERR_IO;
         }
     }
     if (!multisample && !cov && !rac) print_header(out, p);
@@ -1991,6 +2140,7 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
     for (int i = 0; i < G.ss_secondary.n; i++) aln_free(G.ss_secondary.a[i]);
     for (int i = 0; i < G.calls.n; i++) if (G.calls.c[i].indel) free_indel_call(G.calls.c[i].indel);
     free(G.pending.a); free(G.ss_primary.a); free(G.ss_secondary.a); free(G.retired.a); free(G.calls.c); free(G.acalls.c); free(G.pileup.a);
+    free(G.strs);
     for (int i = 0; i < G.n_known; i++) free(G.known[i].id);
     free(G.known);
     for (int i = 0; i < g.n; i++) { free(g.s[i].name); free(g.s[i].seq); }

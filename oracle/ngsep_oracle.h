@@ -52,6 +52,9 @@ typedef struct ngo_params {
                                       calls are the reference's only outside the realigner's windows -- what
                                       the GPU path's carved regions leave (tests/test_gpu_indels.py) */
     const char* known_vcf;         /* -knownVariants (NULL): genotype these biallelic SNVs instead of discovering */
+    const char* known_strs;        /* -knownSTRs (NULL): regions "seq first last" given to the indel realigner as input
+                                      STR variants (SingleSampleVariantsDetector.findSNVS :906-912); ignored with
+                                      -knownVariants, as there */
 } ngo_params;
 
 void ngo_params_default(ngo_params* p);

@@ -22,7 +22,7 @@ class OracleParams(ctypes.Structure):
         ("calc_strand_bias", ctypes.c_int32), ("print_sample_ploidy", ctypes.c_int32),
         ("het_rate_set", ctypes.c_int32), ("het_rate", ctypes.c_double), ("sample_id", ctypes.c_char_p),
         ("query_seq", ctypes.c_char_p), ("query_first", ctypes.c_int32), ("query_last", ctypes.c_int32),
-        ("indel_passthrough", ctypes.c_int32), ("known_vcf", ctypes.c_char_p),
+        ("indel_passthrough", ctypes.c_int32), ("known_vcf", ctypes.c_char_p), ("known_strs", ctypes.c_char_p),
     ]
 
 

@@ -38,6 +38,8 @@ int main(int argc, char** argv) {
         else if (OPT("-querySeq")) p.query_seq = v;
         else if (OPT("-first")) p.query_first = atoi(v);
         else if (OPT("-last")) p.query_last = atoi(v);
+        else if (OPT("-knownVariants")) p.known_vcf = v;
+        else if (OPT("-knownSTRs")) p.known_strs = v;
         else if (strcmp(a, "-p") == 0) p.process_nonunique = 1;
         else if (strcmp(a, "-s") == 0) p.process_secondary = 1;
         else if (strcmp(a, "-ignoreLowerCaseRef") == 0) p.ignore_lowercase_ref = 1;

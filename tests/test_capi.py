@@ -28,7 +28,7 @@ def test_every_declared_symbol_is_exported():
 
 def test_abi_version_and_defaults():
     lib = _lib.load()
-    assert lib.ngsep_abi_version() == 6
+    assert lib.ngsep_abi_version() == 7
     p = _lib.NgsepParams()
     lib.ngsep_params_default(ctypes.byref(p))
     # DEF_* constants: SingleSampleVariantsDetector.java:65-78, CountsHelper.java:42-48
@@ -64,3 +64,29 @@ def test_no_device_fails_loudly(tmp_path):
             s.processAlignments(syn.batch())
             s.notifyEndOfAlignments()
         assert e.value.code == _lib.NGSEP_E_DEVICE
+
+
+def test_known_strs_argument_checks(tmp_path):
+    """ngsep_set_known_strs (ABI 7): needs the reference first, belongs to SingleSampleVariantsDetector only, reads
+    its file; lines the reference's loader skips (SimpleGenomicRegionFileHandler.java:57-80) are skipped here too."""
+    from ngsepcore_amd import GpuPileupSession, NgsepError, default_params
+    path = os.path.join(str(tmp_path), "strs.txt")
+    with open(path, "w") as f:
+        f.write("c1\t10\t20\nc1 30 40\nnope\t1\t2\nc1\tx\t3\nc1\t5\n\n")
+    with GpuPileupSession() as s:
+        with pytest.raises(NgsepError) as e:
+            s.set_known_strs(path)
+        assert e.value.code == _lib.NGSEP_E_INVALID
+        s.set_reference("c1", b"ACGT" * 100)
+        s.set_known_strs(path)
+        s.set_known_strs(None)
+        with pytest.raises(NgsepError) as e:
+            s.set_known_strs(os.path.join(str(tmp_path), "missing.txt"))
+        assert e.value.code == _lib.NGSEP_E_IO
+    p = default_params()
+    p.multisample = 1
+    with GpuPileupSession(p) as s:
+        s.set_reference("c1", b"ACGT" * 100)
+        with pytest.raises(NgsepError) as e:
+            s.set_known_strs(path)
+        assert e.value.code == _lib.NGSEP_E_INVALID

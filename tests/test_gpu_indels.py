@@ -163,3 +163,67 @@ def test_indel_regions_vcf_identical(tmp_path, kw, opts):
         assert a == b, (a, b)
     assert len(ro) == len(rg)
     assert st.positions_genotyped == ost.positions_genotyped
+
+
+def _str_file(path, syn, seed, around=()):
+    """A -knownSTRs regions file: random regions (some pairs 0-6 bp apart, exercising mergeSTRs' gap and overlap
+    rules), regions around the given positions (indel events), space- and tab-separated lines, and lines the reference
+    skips (unknown sequence, unparsable numbers)."""
+    import random
+    names = [n for n, _ in syn.contigs()]
+    seqs = [q for _, q in syn.contigs()]
+    rnd = random.Random(seed)
+    lines = []
+    for _ in range(250):
+        c = rnd.randrange(len(names))
+        a = rnd.randrange(1, len(seqs[c]) - 60)
+        b = a + rnd.randrange(0, 30)
+        lines.append(f"{names[c]}\t{a}\t{b}")
+        if rnd.random() < 0.4:
+            g = rnd.randrange(0, 7)
+            lines.append(f"{names[c]} {b + g} {b + g + rnd.randrange(1, 12)}")
+        if rnd.random() < 0.1:      # 3-5 bp apart: mergeSTRs compares the reference suffix / prefix
+            lines.append(f"{names[c]}\t{b + 4}\t{b + 4 + rnd.randrange(6, 15)}")
+    for name, p in around:
+        lines.append(f"{name}\t{p - rnd.randrange(0, 4)}\t{p + rnd.randrange(2, 12)}")
+    lines += ["chrNotInGenome\t5\t10", "a line that does not parse", f"{names[0]}\tx\t5", f"{names[0]}\t7"]
+    rnd.shuffle(lines)
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw,opts", [
+    (dict(depth=25, seed=32, indel_rate=1e-4), {}),
+    (dict(depth=25, seed=36, indel_rate=3e-4, snv_rate=3e-3), dict(call_embedded=1)),
+    (dict(depth=20, seed=37, indel_rate=2e-4, quality_model=2), dict(window_positions=40000)),
+])
+def test_known_strs_vcf_identical(tmp_path, kw, opts):
+    """-knownSTRs (SingleSampleVariantsDetector.findSNVS :906-912): the input STRs become the indel realigner's input
+    variants (IndelRealignerPileupListener.java:85-153), so every STR opens a realigned region; TYPE=STR records,
+    embedded positions and lastIndelEnd follow the listener (:146-161, :264).  The WHOLE VCF equals the oracle's."""
+    syn = pysynth.Synth(genome=pysynth.YEAST, **{"n_contigs": 2, **kw})
+    fa, sam, bam = syn.write(os.path.join(str(tmp_path), "ind"))
+    o0 = os.path.join(str(tmp_path), "o0.vcf")
+    ngsep_oracle.run_ssvd(fa, sam, o0)
+    around = [(l.split("\t")[0], int(l.split("\t")[1])) for l in _records(o0) if "TYPE=INDEL" in l][::2]
+    strs = os.path.join(str(tmp_path), "strs.txt")
+    _str_file(strs, syn, kw["seed"], around)
+    syn.close()
+    o = os.path.join(str(tmp_path), "o.vcf")
+    oopts = {k: v for k, v in opts.items() if k != "window_positions"}
+    ost = ngsep_oracle.run_ssvd(fa, sam, o, known_strs=strs.encode(), **oopts)
+    g = os.path.join(str(tmp_path), "g.vcf")
+    with GpuPileupSession(gpu_params(**opts)) as s:
+        s.load_fasta(fa)
+        s.set_known_strs(strs)
+        s.processFile(bam, g)
+        assert s.carved_regions() == []
+        st = s.stats()
+    ro, rg = _records(o), _records(g)
+    assert sum(1 for l in ro if "TYPE=STR" in l) > 5
+    assert ro != _records(o0)
+    for a, b in zip(ro, rg):
+        assert a == b, (a, b)
+    assert len(ro) == len(rg)
+    assert st.positions_genotyped == ost.positions_genotyped

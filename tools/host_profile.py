@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--depth", type=float, default=30.0)
     ap.add_argument("--contig", type=int, default=19)
     ap.add_argument("--e2e-only", action="store_true", help="only the BAM -> VCF run (needs a GPU)")
+    ap.add_argument("--decode-only", action="store_true", help="only the BAM decode (ngsep_bam_next_batch)")
     a = ap.parse_args()
     d = a.dir or tempfile.mkdtemp(prefix="ngsep_hp_")
     os.makedirs(d, exist_ok=True)
@@ -64,6 +65,8 @@ def main():
     lib.ngsep_bam_close(b)
     t_dec = time.time() - t
     print(f"decode: {n} reads in {t_dec:.2f}s", flush=True)
+    if a.decode_only:
+        return
     # (2) decode + staging
     t = time.time()
     assert lib.ngsep_bam_open(s._ctx, bam.encode(), ctypes.byref(b)) == 0
