@@ -14,6 +14,7 @@
 // region (ngsep_call_region_bam, the sharded callers).
 #include <dlfcn.h>
 #include <zlib.h>
+#include <sys/stat.h>
 
 #include <algorithm>
 #include <chrono>
@@ -79,7 +80,7 @@ struct RawBuf {
     void resize(size_t k) {
         if (k > cap) {
             const size_t c = std::max(k, cap + cap / 2);
-            T* q = static_cast<T*>(std::malloc(c * sizeof(T)));
+            T* q = static_cast<T*>(ngsep::huge_alloc(c * sizeof(T)));
             if (n) std::memcpy(q, p, n * sizeof(T));
             std::free(p);
             p = q;
@@ -803,6 +804,10 @@ static int for_each_batch(ngsep_ctx* c, ngsep_bam* b, F&& fn) {
 // query region is done either way.
 int call_bam(ngsep_ctx* c, const char* bam_path, const char* out_vcf) {
     start_device_init(c);
+    {
+        struct stat sb;
+        if (!c->params.query_seq[0] && stat(bam_path, &sb) == 0) c->reads_hint = (int64_t)sb.st_size / 40;
+    }
     ngsep_bam* b = nullptr;
     int rc = ngsep_bam_open(c, bam_path, &b);
     if (rc != NGSEP_OK) return rc;
@@ -812,16 +817,27 @@ int call_bam(ngsep_ctx* c, const char* bam_path, const char* out_vcf) {
     }
     rc = ngsep_write_vcf_header(c, out_vcf);
     if (rc != NGSEP_OK) { ngsep_bam_close(b); return rc; }
+    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    const auto t0 = std::chrono::steady_clock::now();
     rc = for_each_batch(c, b, [&](const ngsep_read_batch& batch) {
         int r = process_alignments_packed(c, &batch);
         if (r == NGSEP_OK && !c->sites.empty()) r = ngsep_append_vcf_records(c, out_vcf);
         return r;
     });
+    const auto t1 = std::chrono::steady_clock::now();
     ngsep_bam_close(b);
     if (rc != NGSEP_OK) return rc;
+    const auto t2 = std::chrono::steady_clock::now();
     rc = ngsep_notify_end(c);
     if (rc != NGSEP_OK) return rc;
-    return ngsep_append_vcf_records(c, out_vcf);
+    const auto t3 = std::chrono::steady_clock::now();
+    rc = ngsep_append_vcf_records(c, out_vcf);
+    if (host_timing)
+        std::fprintf(stderr, "[ngsep host] call_bam: batches %.3f s, close %.3f s, end of alignments %.3f s, last records %.3f s\n",
+                     std::chrono::duration<double>(t1 - t0).count(), std::chrono::duration<double>(t2 - t1).count(),
+                     std::chrono::duration<double>(t3 - t2).count(),
+                     std::chrono::duration<double>(std::chrono::steady_clock::now() - t3).count());
+    return rc;
 }
 }  // namespace ngsep
 

@@ -18,11 +18,24 @@
 #include <chrono>
 #include <mutex>
 #include <unordered_map>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <cstdlib>
 #include <fstream>
 #include <functional>
 
 namespace ngsep {
+
+void* huge_alloc(size_t bytes) {
+    constexpr size_t kHuge = (size_t)2 << 20;
+    if (bytes < ((size_t)4 << 20)) return std::malloc(bytes);
+    const size_t n = (bytes + kHuge - 1) / kHuge * kHuge;
+    void* p = std::aligned_alloc(kHuge, n);
+    if (p) madvise(p, n, MADV_HUGEPAGE);
+    return p;
+}
 
 int set_error(ngsep_ctx* c, int code, const std::string& msg) {
     static std::mutex mu;                        // readers of several files may fail on host threads at once
@@ -1007,6 +1020,127 @@ static void carry_open_group(ngsep_ctx* c) {
     c->carry_cur ^= 1;
 }
 
+// AlignmentsPileupGenerator.processAlignment + processSameStartAlns (:377-433) over whole same-start groups [from, to)
+// of the current batch, all on the current sequence: each thread takes a run of groups and lists its admitted reads
+// (a lone primary alignment; otherwise the primaries, then the secondaries, at most max_alns_per_start per read group
+// -- process_same_start's rule), then the lists are appended in order as admit_core would one by one: the sequence's
+// read arrays, the projection list, the indel events (with the input STRs before them), the covered positions (a
+// running union, the chunks' entry maxima as a prefix) and the longest span.
+static void admit_middle(ngsep_ctx* c, int64_t from, int64_t to) {
+    const ngsep_read_batch* b = c->cur_batch.b;
+    const int32_t* lastp = c->cur_batch.last;
+    const int32_t* indelp = c->cur_batch.indel;
+    ContigReads& cr = c->contig;
+    const int maxa = c->params.max_alns_per_start;
+    const int nchunk = (int)std::max<int64_t>(1, std::min<int64_t>((to - from) >> 14, 4 * (int64_t)host_threads()));
+    std::vector<int64_t> cut((size_t)nchunk + 1);
+    cut[0] = from;
+    cut[(size_t)nchunk] = to;
+    for (int k = 1; k < nchunk; k++) {
+        int64_t x = from + (to - from) * k / nchunk;
+        while (x < to && b->first[x] == b->first[x - 1]) x++;
+        cut[(size_t)k] = std::max(x, cut[(size_t)k - 1]);
+    }
+    struct Part {
+        std::vector<int32_t> adm;
+        std::vector<std::pair<int32_t, int32_t>> indels;
+        int64_t hi_max = INT64_MIN, covered = 0;
+        int32_t span_max = 0, last_max = INT32_MIN;
+    };
+    std::vector<Part> parts((size_t)nchunk);
+    const int64_t len = cr.seq_len;
+    parallel_for(nchunk, 1, [&](int64_t k0, int64_t k1) {
+        for (int64_t k = k0; k < k1; k++) {
+            Part& P = parts[(size_t)k];
+            const int64_t a = cut[(size_t)k], z = cut[(size_t)k + 1];
+            P.adm.reserve((size_t)(z - a));
+            std::pair<int32_t, int32_t> tab[64];
+            for (int64_t g = a; g < z;) {
+                int64_t e = g + 1;
+                while (e < z && b->first[e] == b->first[g]) e++;
+                if (e - g == 1 && !(b->flags[g] & 0x100)) {
+                    P.adm.push_back((int32_t)g);
+                } else {
+                    int n_rg = 0;
+                    std::vector<std::pair<int32_t, int32_t>> big;
+                    auto handle = [&](int64_t i) {
+                        const int32_t rg = b->read_group ? b->read_group[i] : -1;
+                        std::pair<int32_t, int32_t>* t = big.empty() ? tab : big.data();
+                        for (int q = 0; q < n_rg; q++)
+                            if (t[q].first == rg) {
+                                if (maxa <= 0 || t[q].second < maxa) { t[q].second++; P.adm.push_back((int32_t)i); }
+                                return;
+                            }
+                        if (n_rg == 64 && big.empty()) big.assign(tab, tab + 64);
+                        if (big.empty()) tab[n_rg] = {rg, 1};
+                        else big.push_back({rg, 1});
+                        n_rg++;
+                        P.adm.push_back((int32_t)i);
+                    };
+                    for (int64_t i = g; i < e; i++) if (!(b->flags[i] & 0x100)) handle(i);
+                    for (int64_t i = g; i < e; i++) if (b->flags[i] & 0x100) handle(i);
+                }
+                g = e;
+            }
+            for (int64_t i = a; i < z; i++) P.last_max = std::max(P.last_max, lastp[i]);
+            for (int32_t i : P.adm) {
+                const int32_t f = b->first[i], l = lastp[i];
+                if (indelp[i] > 0) P.indels.push_back({f, l + indelp[i]});
+                P.span_max = std::max(P.span_max, l - f + 1);
+                const int64_t lo = std::max<int64_t>(f, 1), hi = std::min<int64_t>(l, len);
+                if (hi >= lo) P.hi_max = std::max(P.hi_max, hi);
+            }
+        }
+    });
+    // offsets, the entry union maximum of every chunk, the arrays filled in parallel
+    std::vector<int64_t> off((size_t)nchunk + 1, 0);
+    std::vector<int64_t> m_in((size_t)nchunk + 1);
+    m_in[0] = cr.cov_last;
+    for (int k = 0; k < nchunk; k++) {
+        off[(size_t)k + 1] = off[(size_t)k] + (int64_t)parts[(size_t)k].adm.size();
+        m_in[(size_t)k + 1] = std::max<int64_t>(m_in[(size_t)k], parts[(size_t)k].hi_max);
+    }
+    const int64_t total = off[(size_t)nchunk];
+    const size_t r0 = cr.first.size(), p0 = c->to_project.size();
+    cr.first.resize(r0 + (size_t)total);
+    cr.last.resize(r0 + (size_t)total);
+    cr.neg.resize(r0 + (size_t)total);
+    c->to_project.resize(p0 + (size_t)total);
+    parallel_for(nchunk, 1, [&](int64_t k0, int64_t k1) {
+        for (int64_t k = k0; k < k1; k++) {
+            Part& P = parts[(size_t)k];
+            const size_t o = (size_t)off[(size_t)k];
+            int64_t m = m_in[(size_t)k];
+            for (size_t j = 0; j < P.adm.size(); j++) {
+                const int32_t i = P.adm[j], f = b->first[i], l = lastp[i];
+                cr.first[r0 + o + j] = f;
+                cr.last[r0 + o + j] = l;
+                cr.neg[r0 + o + j] = (b->flags[i] & 0x10) ? 1 : 0;
+                c->to_project[p0 + o + j] = i;
+                const int64_t lo = std::max<int64_t>(f, 1), hi = std::min<int64_t>(l, len);
+                if (hi >= lo) {
+                    if (lo > m) P.covered += hi - lo + 1;
+                    else if (hi > m) P.covered += hi - m;
+                    if (hi > m) m = hi;
+                }
+            }
+        }
+    });
+    for (int k = 0; k < nchunk; k++) {
+        const Part& P = parts[(size_t)k];
+        for (const auto& ev : P.indels) {
+            if (!c->strs.empty()) inject_strs(c, ev.first);
+            cr.indel_reads.push_back(ev);
+        }
+        cr.covered += P.covered;
+        cr.max_span = std::max(cr.max_span, P.span_max);
+        if (P.last_max > c->cur_last) c->cur_last = P.last_max;
+    }
+    if (!c->strs.empty() && total > 0) inject_strs(c, cr.first.back());
+    cr.cov_last = (int32_t)std::max<int64_t>(cr.cov_last, m_in[(size_t)nchunk]);
+    c->stats.alignments_admitted += total;
+}
+
 static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed) {
     if (!b || b->n_reads < 0) return set_error(c, NGSEP_E_INVALID, "null batch");
     const int nseq = (int)c->seq_names.size();
@@ -1050,13 +1184,15 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed) {
     });
     c->cur_batch = BatchRef{b, lastp, indelp, packed};
     int64_t n_in = 0;
-    for (int64_t i = 0; i < b->n_reads; i++) {
-        if (c->query_done) break;
+    // the admission sweep (processAlignment + processSameStartAlns) over reads [from, to); false: stop the batch
+    auto sweep = [&](int64_t from, int64_t to) -> bool {
+    for (int64_t i = from; i < to; i++) {
+        if (c->query_done) return false;
         n_in++;
         struct { int32_t seq_id, first, flags; } r{b->seq_id[i], b->first[i], b->flags[i]};
         if (r.seq_id < 0 || r.seq_id >= nseq) {
             rc = set_error(c, NGSEP_E_INVALID, "alignment on unknown sequence id " + std::to_string(r.seq_id));
-            break;
+            return false;
         }
         const int32_t last = lastp[i], read_length = rlenp[i];
         const int32_t sl = b->seq_len[i];
@@ -1065,11 +1201,11 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed) {
         if (c->params.query_seq[0]) {
             if (c->seq_names[r.seq_id] == c->params.query_seq) {
                 c->query_found = true;
-                if (r.first > c->params.query_last) { c->query_done = true; break; }
+                if (r.first > c->params.query_last) { c->query_done = true; return false; }
                 if (c->params.query_first > last) continue;
             } else if (c->query_found) {
                 c->query_done = true;
-                break;
+                return false;
             } else {
                 continue;
             }
@@ -1079,13 +1215,13 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed) {
             bool same = c->cur_seq == r.seq_id;
             if (same && r.first < c->last_start) {
                 rc = set_error(c, NGSEP_E_INVALID, "alignments are not coordinate-sorted");
-                break;
+                return false;
             }
             if (!same || c->last_start != r.first) {
                 process_same_start(c);
                 if (!same) {
                     rc = flush_sequence(c);
-                    if (rc != NGSEP_OK) break;
+                    if (rc != NGSEP_OK) return false;
                 }
             }
         }
@@ -1096,6 +1232,18 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed) {
             c->contig.seq_len = (int64_t)c->seq_bases[(size_t)r.seq_id].size();
             c->cur_last = last;
             c->str_next = 0;                             // IndelRealignerPileupListener.onSequenceStart (:128-133)
+            if (c->reads_hint > 0 && !c->params.coverage_stats) {
+                int64_t glen = 0;
+                for (const std::string& q : c->seq_bases) glen += (int64_t)q.size();
+                const int64_t want = (int64_t)((double)c->reads_hint * (double)c->contig.seq_len / (double)std::max<int64_t>(glen, 1) * 1.25) + 4096;
+                ContigReads& cr = c->contig;
+                if ((int64_t)cr.first.capacity() < want) {
+                    cr.first.reserve((size_t)want);
+                    cr.last.reserve((size_t)want);
+                    cr.neg.reserve((size_t)want);
+                    cr.bptr.reserve((size_t)want);
+                }
+            }
             if (c->params.relative_allele_counts) {      // onSequenceStart (RelativeAlleleCountsCalculator.java:312-322)
                 if (c->contig.seq_len > 100000) {
                     c->rac.seq_names.push_back(c->seq_names[(size_t)r.seq_id]);
@@ -1117,17 +1265,55 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed) {
         }
         c->last_start = r.first;
     }
+    return true;
+    };
+    // the batch's middle -- whole same-start groups of the current sequence -- admitted on all threads
+    // (admit_middle); its first group (which may continue the carried one) and its last (left open) go through the
+    // sweep.  Only for a sorted batch of the current sequence whose reads all carry their characters' length.
+    int64_t g1 = 0, gL = 0;
+    if (streaming(c) && !c->params.query_seq[0] && b->n_reads >= (1 << 16) && c->cur_seq >= 0 &&
+        b->seq_id[0] == c->cur_seq && b->first[0] >= c->last_start) {
+        const int64_t n = b->n_reads;
+        std::atomic<bool> bad{false};
+        parallel_for(n, 1 << 15, [&](int64_t lo, int64_t hi) {
+            for (int64_t i = lo; i < hi && !bad.load(std::memory_order_relaxed); i++) {
+                const int32_t sl = b->seq_len[i];
+                if (b->seq_id[i] != c->cur_seq || (i > 0 && b->first[i] < b->first[i - 1]) || (sl > 0 && rlenp[i] != sl)) bad = true;
+            }
+        });
+        if (!bad) {
+            g1 = 1;
+            while (g1 < n && b->first[g1] == b->first[0]) g1++;
+            gL = n - 1;
+            while (gL > 0 && b->first[gL - 1] == b->first[n - 1]) gL--;
+        }
+    }
+    if (g1 < gL) {
+        if (sweep(0, g1)) {
+            process_same_start(c);                       // read g1 starts another group
+            admit_middle(c, g1, gL);
+            n_in += gL - g1;
+            c->last_start = b->first[gL - 1];
+            sweep(gL, b->n_reads);
+        }
+    } else {
+        sweep(0, b->n_reads);
+    }
     c->stats.alignments_in += n_in;
     // the admitted reads' bytes are projected while the batch is alive; the open group is carried
     static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     const auto t1 = std::chrono::steady_clock::now();
     project_pending(c);
+    const auto t2 = std::chrono::steady_clock::now();
     if (rc == NGSEP_OK && streaming(c)) rc = stream_advance(c, false);
+    const auto t3 = std::chrono::steady_clock::now();
     carry_open_group(c);
     if (host_timing)
-        std::fprintf(stderr, "[ngsep host] batch of %lld: admission %.1f ms, projection %.1f ms\n", (long long)b->n_reads,
-                     std::chrono::duration<double, std::milli>(t1 - t0).count(),
-                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
+        std::fprintf(stderr, "[ngsep host] batch of %lld: admission %.1f ms, projection %.1f ms, stream %.1f ms, carry %.1f ms\n",
+                     (long long)b->n_reads, std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                     std::chrono::duration<double, std::milli>(t2 - t1).count(),
+                     std::chrono::duration<double, std::milli>(t3 - t2).count(),
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t3).count());
     return rc;
 }
 
@@ -1234,7 +1420,7 @@ static int choose_tile(const std::vector<int32_t>& m16, int64_t g_len, std::vect
 //   * the position-major byte pile (KP): position p's rows_t codes at off_t + p * rows_t, rank order;
 //   * the strand bits (KP, countsStrand): bit off_t + p * rows_t + r = the rank-r read is reverse.
 // Tiles are independent: built on all host threads.
-static int build_single_layout(Staged& s, const std::vector<SRead>& reads, LayoutArena& arena, bool exact) {
+static int build_single_layout(Staged& s, const HugeVec<SRead>& reads, LayoutArena& arena, bool exact) {
     static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     auto lap = [t = std::chrono::steady_clock::now()](const char* what) mutable {
         if (!host_timing) return;
@@ -1352,7 +1538,7 @@ static int build_single_layout(Staged& s, const std::vector<SRead>& reads, Layou
 // units.  Headers: global first / last position and the strand bit.  The two
 // block tables give the scan its tile's entry range and the column gather the entries that can cover a
 // position.  Groups are independent: built on all host threads.
-static int build_rg_layout(Staged& s, const std::vector<SRead>& reads, LayoutArena& arena, bool exact) {
+static int build_rg_layout(Staged& s, const HugeVec<SRead>& reads, LayoutArena& arena, bool exact) {
     static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     const auto t0 = std::chrono::steady_clock::now();
     const int64_t n = (int64_t)reads.size();
@@ -1761,7 +1947,7 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     if (!c->params.multisample) {
         // single sample: the reads' projected bytes go straight into the tile layout
         s.single = true;
-        std::vector<SRead> reads((size_t)nreads);
+        HugeVec<SRead> reads((size_t)nreads);
         int64_t ri = 0;
         for (size_t wi = 0; wi < s.windows.size(); wi++) {
             Window& w = s.windows[wi];
@@ -2340,37 +2526,60 @@ static inline char mask_base(char ch) {
         default: return 'N';   // DNAMaskedSequence default index
     }
 }
+// ReferenceGenome(filename, keepLowerCase = true) (genome/ReferenceGenome.java:40-62): the file is mapped, its lines
+// cut with memchr on one thread, and the sequence lines translated (mask_base) into the sequences on all threads
 int load_fasta(ngsep_ctx* c, const char* path) {
-    std::FILE* f = std::fopen(path, "rb");
-    if (!f) return set_error(c, NGSEP_E_IO, std::string("cannot open ") + path);
-    std::string name, seq;
-    bool have = false;
-    char* line = nullptr;
-    size_t cap = 0;
-    ssize_t l;
-    auto commit = [&]() {
-        if (!have) return;
-        c->seq_names.push_back(name);
-        c->seq_bases.push_back(std::move(seq));
-        seq.clear();
-    };
-    while ((l = getline(&line, &cap, f)) >= 0) {
-        while (l > 0 && (line[l - 1] == '\n' || line[l - 1] == '\r')) line[--l] = 0;
-        if (l > 0 && line[0] == '>') {
-            commit();
-            size_t e = 1;
-            while (line[e] && line[e] != ' ' && line[e] != '\t') e++;
-            name.assign(line + 1, e - 1);
-            have = true;
-        } else if (have) {
-            size_t o = seq.size();
-            seq.resize(o + (size_t)l);
-            for (ssize_t i = 0; i < l; i++) seq[o + i] = mask_base(line[i]);
-        }
+    const int fd = ::open(path, O_RDONLY);
+    if (fd < 0) return set_error(c, NGSEP_E_IO, std::string("cannot open ") + path);
+    struct stat sb;
+    if (fstat(fd, &sb) != 0) { ::close(fd); return set_error(c, NGSEP_E_IO, std::string("cannot stat ") + path); }
+    const size_t n = (size_t)sb.st_size;
+    const char* buf = nullptr;
+    void* map = nullptr;
+    if (n) {
+        map = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (map == MAP_FAILED) { ::close(fd); return set_error(c, NGSEP_E_IO, std::string("cannot map ") + path); }
+        madvise(map, n, MADV_SEQUENTIAL);
+        buf = static_cast<const char*>(map);
     }
-    commit();
-    std::free(line);
-    std::fclose(f);
+    struct Seg { size_t src; int64_t dst; int64_t len; };
+    struct Rec { std::string name; int64_t len = 0; size_t seg0 = 0; };
+    std::vector<Rec> recs;
+    std::vector<Seg> segs;
+    size_t pos = 0;
+    while (pos < n) {
+        const char* nl = static_cast<const char*>(std::memchr(buf + pos, '\n', n - pos));
+        const size_t end = nl ? (size_t)(nl - buf) : n;
+        size_t l = end - pos;
+        while (l > 0 && (buf[pos + l - 1] == '\r' || buf[pos + l - 1] == '\n')) l--;   // (getline + trailing CR/LF strip)
+        if (l > 0 && buf[pos] == '>') {
+            size_t e = 1;
+            while (e < l && buf[pos + e] != ' ' && buf[pos + e] != '\t' && buf[pos + e] != '\0') e++;
+            recs.push_back(Rec{std::string(buf + pos + 1, e - 1), 0, segs.size()});
+        } else if (!recs.empty() && l > 0) {
+            segs.push_back(Seg{pos, recs.back().len, (int64_t)l});
+            recs.back().len += (int64_t)l;
+        }
+        pos = end + 1;
+    }
+    const size_t first = c->seq_bases.size();
+    for (Rec& r : recs) {
+        c->seq_names.push_back(r.name);
+        c->seq_bases.emplace_back();
+        c->seq_bases.back().resize((size_t)r.len);
+    }
+    std::vector<int32_t> seg_rec(segs.size());
+    for (size_t k = 0; k < recs.size(); k++)
+        for (size_t i = recs[k].seg0, e = k + 1 < recs.size() ? recs[k + 1].seg0 : segs.size(); i < e; i++) seg_rec[i] = (int32_t)k;
+    parallel_for((int64_t)segs.size(), 1 << 12, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; i++) {
+            const Seg& g = segs[(size_t)i];
+            char* dst = &c->seq_bases[first + (size_t)seg_rec[(size_t)i]][(size_t)g.dst];
+            for (int64_t k = 0; k < g.len; k++) dst[k] = mask_base(buf[g.src + (size_t)k]);
+        }
+    });
+    if (map) munmap(map, n);
+    ::close(fd);
     return NGSEP_OK;
 }
 

@@ -158,6 +158,10 @@ struct Window {            // a contiguous range of one sequence, resident in HB
 };
 
 // uninitialised host array, filled in parallel (no serial zero-fill of GB-sized layouts)
+// malloc for host arrays of the streamed path: blocks of 4 MB and more come 2 MB-aligned with transparent huge pages
+// requested (madvise), so filling them takes 512x fewer page faults (engine.cpp)
+void* huge_alloc(size_t bytes);
+
 template <class T>
 struct HostArray {
     T* p = nullptr;
@@ -168,20 +172,37 @@ struct HostArray {
     HostArray(HostArray&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
     HostArray& operator=(HostArray&& o) noexcept { if (this != &o) { release(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; } return *this; }
     ~HostArray() { release(); }
-    void alloc(size_t k) { release(); n = k; p = k ? static_cast<T*>(std::malloc(k * sizeof(T))) : nullptr; }
+    void alloc(size_t k) { release(); n = k; p = k ? static_cast<T*>(huge_alloc(k * sizeof(T))) : nullptr; }
     void release() { std::free(p); p = nullptr; n = 0; }
 };
+
+// std::allocator with huge_alloc's pages: the admitted reads' arrays of a sequence (ContigReads)
+template <class T>
+struct HugeAllocator {
+    using value_type = T;
+    HugeAllocator() = default;
+    template <class U> HugeAllocator(const HugeAllocator<U>&) {}
+    T* allocate(size_t n) {
+        void* p = huge_alloc(n * sizeof(T));
+        if (!p) throw std::bad_alloc();
+        return static_cast<T*>(p);
+    }
+    void deallocate(T* p, size_t) { std::free(p); }
+    template <class U> bool operator==(const HugeAllocator<U>&) const { return true; }
+    template <class U> bool operator!=(const HugeAllocator<U>&) const { return false; }
+};
+template <class T> using HugeVec = std::vector<T, HugeAllocator<T>>;
 
 // Admitted reads of one sequence in pending order (AlignmentsPileupGenerator.pendingAlignments)
 struct ContigReads {
     int32_t seq_id = -1;
     int64_t seq_len = 0;               // the sequence's length
-    std::vector<int32_t> first, last;
-    std::vector<uint8_t> neg;          // 1 = negative strand
+    HugeVec<int32_t> first, last;
+    HugeVec<uint8_t> neg;              // 1 = negative strand
     std::vector<uint8_t> uniq;         // coverage mode: 1 = ReadAlignment.isUnique (no FLAG_MULTIPLE_ALN)
     std::vector<int16_t> sample;       // multisample: sample of the read's group (-1 none)
     std::vector<uint8_t> rank;         // multisample: rank of the read group in its sample's set
-    std::vector<const uint8_t*> bptr;  // the read's projected codes over [first, last]
+    HugeVec<const uint8_t*> bptr;      // the read's projected codes over [first, last]
     std::vector<HostArray<uint8_t>> chunks;   // their storage: one uninitialised chunk per projected batch
     // indel-bearing admitted reads: [first, last + indel bases]; widened by the realigner's reach and merged
     // into `carved` when the sequence is staged (engine.cpp carve_indel_regions)
@@ -514,7 +535,7 @@ struct WindowJob {
     int32_t seq_id = -1;
     int64_t w0 = 0, w1 = 0;
     int32_t max_span = 1;
-    std::vector<SRead> reads;                               // global coordinates (window at pad)
+    HugeVec<SRead> reads;                                   // global coordinates (window at pad)
     std::vector<std::pair<int64_t, int64_t>> carved;        // 1-based, inside [w0, w1]
     // the indel realigner's regions (whole inside the window, = carved) and their alignments; the listener's
     // lastIndelEnd before and after the window
@@ -581,6 +602,9 @@ struct ngsep_ctx {
     // str_next: the next one of the current sequence to enter its realigner regions (engine.cpp inject_strs)
     std::vector<std::vector<ngsep::StrVar>> strs;
     size_t str_next = 0;
+    // path B: the alignments the BAM is expected to hold (its size / 40 B, an upper estimate); a sequence's read
+    // arrays reserve their share up front (virtual memory, touched only as they fill: no regrowth copies)
+    int64_t reads_hint = 0;
     mutable struct { int32_t seq = -1, pos = -1; std::vector<int64_t> taken; } vcf_known;   // known_id: the position written
     // RelativeAlleleCountsCalculator mode (params.relative_allele_counts): its Distributions
     struct {

@@ -255,6 +255,12 @@ static_assert(sizeof(SiteQ) == 16, "SiteQ layout");
 // work: every lane of the wave does useful fp64 work on its own site.  An emitted record goes to the
 // bucket of its position (KO orders the buckets).
 __device__ inline double pow10_j(double x) { return pow(10.0, x); }   // Math.pow(10.0, x)
+// getPosteriorProbabilities' 16 events (row i: (i,i), then (i,j), j != i ascending) take L[min][max]: event (j,i) has
+// the exponent of the earlier event (i,j).  The earlier one's index (0: none): 5->1, 9->2, 10->6, 13->3, 14->7, 15->11
+__device__ __forceinline__ int ev_partner(int k) {
+    constexpr unsigned long long kTab = (1ull << 20) | (2ull << 36) | (6ull << 40) | (3ull << 52) | (7ull << 56) | (11ull << 60);
+    return (int)((kTab >> (4 * k)) & 15ull);
+}
 
 // One emitted site into its bucket slot: the 64-B SiteRec (engine.hpp) from the record's header dwords h
 // (ngsep_site_out layout: seq, gpos, ref|n_alleles|alt|third, genotype|strand_bias|gq, qual|is_call|pool, dp,
@@ -429,7 +435,8 @@ __global__ __launch_bounds__(kPostThreads) void k_posterior(const SiteQ* __restr
                 double totalProb = 0;
                 for (uint32_t rem = act; rem; rem &= rem - 1) {
                     const int k = __builtin_ctz(rem);
-                    const double pk = pow10_j(s_ev[k][threadIdx.x]);
+                    const int src = ev_partner(k);
+                    const double pk = src ? s_ev[src][threadIdx.x] : pow10_j(s_ev[k][threadIdx.x]);
                     totalProb += pk;
                     s_ev[k][threadIdx.x] = pk;
                 }
@@ -477,7 +484,8 @@ __global__ __launch_bounds__(kPostThreads) void k_posterior(const SiteQ* __restr
             double totalProb = 0;
             for (uint32_t rem = act; rem; rem &= rem - 1) {
                 const int k = __builtin_ctz(rem);
-                const double pk = pow10_j(s_ev[k][threadIdx.x]);
+                const int src = ev_partner(k);              // (j, i) repeats (i, j)'s exponent: its pow is reused
+                const double pk = src ? s_ev[src][threadIdx.x] : pow10_j(s_ev[k][threadIdx.x]);
                 totalProb += pk;
                 s_ev[k][threadIdx.x] = pk;
             }
@@ -1187,7 +1195,7 @@ __global__ __launch_bounds__(256) void k_gather_cols(const SiteQ* __restrict__ q
 // KG for KL's queue (every site's column space reserved: rows <= -3, or -2 when the shard's columns were full):
 // a wave gathers kKgSites sites at once, their chunk loads interleaved (one site's gather is a chain of dependent
 // loads -- block table, headers, units -- so a wave per site leaves the chip waiting).  Compacts like k_gather_cols.
-constexpr int kKgSites = 4;
+template <int kKgSites>
 __global__ __launch_bounds__(256) void k_gather_kl(const SiteQ* __restrict__ qin, const unsigned long long* __restrict__ qcnt,
                                                    int stride, int nshard, int64_t qseg, SiteQ* __restrict__ qout,
                                                    const int2* __restrict__ rh, const RGroup* __restrict__ grp,
@@ -1228,7 +1236,11 @@ __global__ __launch_bounds__(256) void k_gather_kl(const SiteQ* __restrict__ qin
                 rcode[t] = ref[q[t].gpos];
             }
         // chunk steps: every live site reads its next 64 entries' headers, then the covering ones' units
-        while (live[0] || live[1] || live[2] || live[3]) {
+        for (;;) {
+            bool any = false;
+#pragma unroll
+            for (int t = 0; t < kKgSites; t++) any |= live[t];
+            if (!any) break;
             int2 h[kKgSites];
             int64_t gb[kKgSites];
 #pragma unroll
@@ -1575,7 +1587,8 @@ __device__ PopCall genotype_sample_d(const double* L, const int* cnt, int total,
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         const double x = ev[k] - logMax;
-        ev[k] = x < -20 ? 0.0 : pow(10.0, x);
+        const int src = ev_partner(k);                        // (j, i) repeats (i, j)'s exponent: its pow is reused
+        ev[k] = src ? ev[src] : (x < -20 ? 0.0 : pow(10.0, x));
         totalProb += ev[k];
     }
 #pragma unroll
@@ -1653,11 +1666,32 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
     if (tid < 96) s_t[tid >> 5][tid & 31] = (tid < 32 ? tabs->A : tid < 64 ? tabs->H : tabs->E)[tid & 31];
     int64_t n = (int64_t)*qn;
     if (n > qcap) n = qcap;
+    // thread s's column of a queued position: its rows and first code (site-major tile, engine.hpp: the S + 1 columns
+    // of gpos are one contiguous run of stride bytes).  The next position's entry and column are fetched while the
+    // current one is genotyped.
+    auto column_of = [&](int32_t gpos, int32_t& rows, const uint8_t*& col) {
+        rows = 0;
+        col = nullptr;
+        if (tid > n_samples) return;
+        const int64_t b0 = (int64_t)(gpos >> kPopTileLog2) * (n_samples + 1), bi = b0 + tid;
+        const int64_t stride = (pboff[b0 + n_samples + 1] - pboff[b0]) >> kPopTileLog2;
+        rows = prow[bi];
+        col = ppile + pboff[bi] + (int64_t)(gpos & (kPopTile - 1)) * stride;
+    };
+    QueueSite qs_next{0, 0};
+    int32_t rows_next = 0;
+    const uint8_t* col_next = nullptr;
+    if ((int64_t)blockIdx.x < n) {
+        qs_next = queue[blockIdx.x];
+        column_of(qs_next.gpos, rows_next, col_next);
+    }
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         __syncthreads();
-        const QueueSite qs = queue[i];
+        const QueueSite qs = qs_next;
         const int32_t gpos = qs.gpos;
         const uint32_t rc = (uint32_t)qs.rc;
+        const int64_t inext = i + gridDim.x;
+        if (inext < n) qs_next = queue[inext];
         if (tid == 0) { s_pc[0] = s_pc[1] = s_pc[2] = s_pc[3] = 0; s_tot = 0; s_called = 0; s_qs = 0; }
         __syncthreads();
         // 1-3. thread s walks sample s's column of the pile (read-group rank order, pending order inside:
@@ -1668,14 +1702,9 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
         int cnt[4] = {0, 0, 0, 0};
         double L[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         constexpr bool pool = POOL;
-        int32_t rows = 0;
-        const uint8_t* col = nullptr;
+        const int32_t rows = rows_next;
+        const uint8_t* col = col_next;
         if (tid <= n_samples) {
-            // site-major tile (engine.hpp): the S + 1 columns of gpos are one contiguous run of stride bytes
-            const int64_t b0 = (int64_t)(gpos >> kPopTileLog2) * (n_samples + 1), bi = b0 + tid;
-            const int64_t stride = (pboff[b0 + n_samples + 1] - pboff[b0]) >> kPopTileLog2;
-            rows = prow[bi];
-            col = ppile + pboff[bi] + (int64_t)(gpos & (kPopTile - 1)) * stride;
             const bool tally = tid < n_samples && !pool;        // (the pool algorithm walks the column itself)
             for (int32_t r0 = 0; r0 < rows; r0 += 8) {
                 uint32_t code[8];
@@ -1706,6 +1735,7 @@ __global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
             }
         }
         if (i == blockIdx.x) stamp(1);
+        if (inext < n) column_of(qs_next.gpos, rows_next, col_next);   // (in flight during the genotyping)
         // pooled counts: the sum over every sample and the reads of no sample
         {
             int c0 = cnt[0], c1 = cnt[1], c2 = cnt[2], c3 = cnt[3], tt = total;
@@ -2377,8 +2407,11 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     {
         // KG: the queued sites' columns, one wave per site (grid-stride past the estimate)
         const int64_t nblk = std::max<int64_t>(d->n_cu, std::min<int64_t>((kg_sites + 3) / 4, (int64_t)d->n_cu * 32));
+        static const int kg_env = std::getenv("NGSEP_KG_SITES") ? std::atoi(std::getenv("NGSEP_KG_SITES")) : 4;   // tuning
+        const int kgs = kg_env == 8 ? 8 : kg_env == 2 ? 2 : 4;
         if (kl_run)
-            hipLaunchKernelGGL(k_gather_kl, dim3((unsigned)std::max<int64_t>(d->n_cu, std::min<int64_t>((kg_sites + 4 * kKgSites - 1) / (4 * kKgSites), (int64_t)d->n_cu * 32))),
+            hipLaunchKernelGGL(kgs == 8 ? k_gather_kl<8> : kgs == 2 ? k_gather_kl<2> : k_gather_kl<4>,
+                               dim3((unsigned)std::max<int64_t>(d->n_cu, std::min<int64_t>((kg_sites + 4 * kgs - 1) / (4 * kgs), (int64_t)d->n_cu * 32))),
                                dim3(256), 0, sl.stream, (const SiteQ*)sl.d_hard, (const unsigned long long*)(ctr + kCtrShard0), kCtrShardStride,
                                kKlShards, sl.cap_hard / kKlShards, sl.d_hard2, (const int2*)d->d_rh, (const RGroup*)d->d_grp,
                                (const uint64_t*)d->d_units, (const int32_t*)d->d_blkA, (const uint8_t*)d->d_ref, d->n_entries, sl.d_cols, ctr);
