@@ -1636,7 +1636,10 @@ bool LayoutArena::ensure_units(int64_t n_units, bool exact) {
     units_cap = 0;
     int64_t want = exact ? n_units : n_units + n_units / 4;
     want = std::max<int64_t>(want, 4096);
-    units = static_cast<uint64_t*>(pinned_alloc((size_t)want * sizeof(uint64_t)));
+    // a whole-run layout beyond 4 GB (a staged multi-contig device run) stays pageable: the upload goes through the
+    // runtime's staging buffers instead of pinning tens of GB at once (pinned_free releases either kind)
+    const size_t bytes = (size_t)want * sizeof(uint64_t);
+    units = static_cast<uint64_t*>(bytes > ((size_t)4 << 30) ? huge_alloc(bytes) : pinned_alloc(bytes));
     if (!units) return false;
     units_cap = want;
     return true;

@@ -145,8 +145,27 @@ def gpu_contig_caller(fasta: str, bam: str, params=None, device: int = 0,
     def close():
         if "s" in state:
             state.pop("s").close()
+
+    def carved():
+        # the indel realigner's regions this rank handed back (pass-through mode, -knownVariants with indel reads)
+        return state["s"].carved_regions() if "s" in state else []
     call.close = close
+    call.carved = carved
     return call
+
+
+def gather_carved(local: List[Tuple[str, int, int]], order: Sequence[str], dist=None) -> Optional[List[Tuple[str, int, int]]]:
+    """Every rank's carved regions on rank 0 (None elsewhere), in the BAM header's sequence order."""
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        got = [None] * dist.get_world_size() if dist.get_rank() == 0 else None
+        dist.gather_object(local, got, dst=0)
+        if dist.get_rank() != 0:
+            return None
+        allr = [r for part in got for r in part]
+    else:
+        allr = list(local)
+    rank_of = {n: k for k, n in enumerate(order)}
+    return sorted(allr, key=lambda r: (rank_of.get(r[0], len(order)), r[1], r[2]))
 
 
 def call_bam_sharded(fasta: str, bam: str, out_vcf: str, params=None, dist=None, device: Optional[int] = None,
@@ -159,7 +178,15 @@ def call_bam_sharded(fasta: str, bam: str, out_vcf: str, params=None, dist=None,
         device = int(os.environ.get("LOCAL_RANK", "0"))
     caller = gpu_contig_caller(fasta, bam, params, device, known_vcf)
     try:
-        return call_sharded(contigs, caller, out_vcf, dist)
+        text = call_sharded(contigs, caller, out_vcf, dist)
+        # the regions left to the caller's own indel path (ngsep_fetch_carved_regions), merged like the records and
+        # written beside the VCF as the CLI does (<out>.carved.bed, 0-based half-open)
+        regions = gather_carved(caller.carved(), [c[0] for c in contigs], dist)
+        if regions:
+            with open(out_vcf + ".carved.bed", "w") as f:
+                for n, a, b in regions:
+                    f.write(f"{n}\t{a - 1}\t{b}\n")
+        return text
     finally:
         caller.close()
 

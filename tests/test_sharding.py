@@ -280,3 +280,50 @@ def test_gpu_contig_caller_indels_merge_identical(tmp_path):
     merged = call_sharded(contigs, gpu_contig_caller(fa, bam), os.path.join(str(tmp_path), "m.vcf"))
     assert merged == open(full).read()
     assert "TYPE=INDEL" in merged
+
+
+def _carved_worker(rank, world, port, out_dir):
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        from ngsepcore_amd.sharding import gather_carved
+        local = [[("chrII", 500, 900), ("chrI", 10, 20)], [("chrIII", 5, 7), ("chrI", 1, 4)]][rank]
+        got = gather_carved(local, ["chrI", "chrII", "chrIII"], dist)
+        if rank == 0:
+            with open(os.path.join(out_dir, "carved.txt"), "w") as f:
+                f.write(repr(got))
+        else:
+            assert got is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_carved_regions_gathered(tmp_path):
+    """Pass-through mode: each rank's carved regions (ngsep_fetch_carved_regions) reach rank 0 in the BAM header's
+    sequence order, then by position (sharding.gather_carved)."""
+    mp.spawn(_carved_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    got = eval(open(os.path.join(str(tmp_path), "carved.txt")).read())
+    assert got == [("chrI", 1, 4), ("chrI", 10, 20), ("chrII", 500, 900), ("chrIII", 5, 7)]
+
+
+@pytest.mark.gpu
+def test_gpu_sharded_passthrough_carved_bed(tmp_path):
+    """call_bam_sharded in pass-through mode (indel_passthrough = 1): the merged VCF equals the whole-file run and
+    <out>.carved.bed lists the same regions as the whole-file session (SingleSampleVariantsDetector.java:919-925 is
+    the reference behaviour those regions stand in for)."""
+    from ngsepcore_amd import GpuPileupSession
+    from ngsepcore_amd.sharding import call_bam_sharded
+    from helpers import gpu_params
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=3, depth=15, seed=39, indel_rate=3e-4)
+    fa, sam, bam = syn.write(os.path.join(str(tmp_path), "d"))
+    syn.close()
+    full = os.path.join(str(tmp_path), "full.vcf")
+    with GpuPileupSession(gpu_params(indel_passthrough=1)) as s:
+        s.load_fasta(fa)
+        s.processFile(bam, full)
+        want = s.carved_regions()
+    assert len(want) > 3
+    out = os.path.join(str(tmp_path), "m.vcf")
+    merged = call_bam_sharded(fa, bam, out, params=gpu_params(indel_passthrough=1))
+    assert merged == open(full).read()
+    bed = [l.split("\t") for l in open(out + ".carved.bed").read().splitlines()]
+    assert [(n, int(a) + 1, int(b)) for n, a, b in bed] == want
