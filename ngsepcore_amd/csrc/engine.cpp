@@ -1318,24 +1318,6 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed) {
 }
 
 // ---- staging: fixed-stride slot layout of every window's reads ----
-static int choose_slot_size(const std::vector<ContigReads>& contigs) {
-    std::vector<int64_t> hist(4097, 0);
-    for (const ContigReads& cr : contigs)
-        for (size_t i = 0; i < cr.first.size(); i++) {
-            int64_t span = (int64_t)cr.last[i] - cr.first[i] + 1;
-            if (span < 1) span = 1;
-            hist[std::min<int64_t>(span, 4096)]++;
-        }
-    int best = 16;
-    double best_cost = -1;
-    for (int S = 16; S <= 512; S += 16) {
-        double cost = 0;
-        for (int s = 1; s <= 4096; s++)
-            if (hist[s]) cost += (double)hist[s] * ((s + S - 1) / S) * (S + 4);
-        if (best_cost < 0 || cost < best_cost) { best_cost = cost; best = S; }
-    }
-    return best;
-}
 
 static inline uint8_t ref_code(const ngsep_ctx* c, char ch) {
     if (c->params.ignore_lowercase_ref && std::islower((unsigned char)ch)) return kRefInWindow;   // :198
@@ -1564,6 +1546,7 @@ static int build_rg_layout(Staged& s, const HugeVec<SRead>& reads, LayoutArena& 
     s.n_units = base;
     if (!arena.ensure_units(base + 8, exact)) return -2;       // + 8: slack past the last unit
     s.h_units = arena.units;
+    s.units_pinned = arena.units_pinned;
     const int32_t last_first = n ? reads[(size_t)n - 1].gfirst : 1;
     uint64_t* units = s.h_units;
     parallel_for(ng, 64, [&](int64_t g0, int64_t g1) {
@@ -1631,7 +1614,8 @@ static int build_rg_layout(Staged& s, const HugeVec<SRead>& reads, LayoutArena& 
 
 bool LayoutArena::ensure_units(int64_t n_units, bool exact) {
     if (units && n_units <= units_cap) return true;
-    pinned_free(units);
+    if (units_pinned) pinned_free(units);
+    else std::free(units);
     units = nullptr;
     units_cap = 0;
     int64_t want = exact ? n_units : n_units + n_units / 4;
@@ -1639,7 +1623,8 @@ bool LayoutArena::ensure_units(int64_t n_units, bool exact) {
     // a whole-run layout beyond 4 GB (a staged multi-contig device run) stays pageable: the upload goes through the
     // runtime's staging buffers instead of pinning tens of GB at once (pinned_free releases either kind)
     const size_t bytes = (size_t)want * sizeof(uint64_t);
-    units = static_cast<uint64_t*>(bytes > ((size_t)4 << 30) ? huge_alloc(bytes) : pinned_alloc(bytes));
+    units_pinned = bytes <= ((size_t)4 << 30);
+    units = static_cast<uint64_t*>(units_pinned ? pinned_alloc(bytes) : huge_alloc(bytes));
     if (!units) return false;
     units_cap = want;
     return true;
@@ -1661,7 +1646,8 @@ void LayoutArena::release() {
     pinned_free(cpile);
     pinned_free(planes);
     pinned_free(cneg);
-    pinned_free(units);
+    if (units_pinned) pinned_free(units);
+    else std::free(units);
     cpile = nullptr;
     planes = nullptr;
     cneg = nullptr;
@@ -1682,16 +1668,25 @@ void LayoutArena::release() {
 //    order getAlleleCalls visits them: read-group rank, then pending order -- rows = the tile's deepest
 //    column, zero padded (a zero code is no call and counts nothing).
 static int build_multi_layout(Staged& s) {
+    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    auto t_last = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!host_timing) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[ngsep host]   population layout: %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+        t_last = t;
+    };
     const int64_t g_len = s.g_len, nreads = s.n_reads;
     const int S = s.n_samples, S1 = S + 1;
     const int32_t* R = s.h_reads.data();
-    const int SL = s.slot_size;
-    const uint8_t* slots = s.h_slots.data();
+    const uint8_t* const* rptr = s.h_rptr.data();      // each read's projected bytes over [gfirst, glast]
     const uint8_t* ref = s.h_ref.data();
     const int32_t maxspan = s.max_span;
     const int64_t PT = kPopTile;
-    int64_t C = ((int64_t)1 << 21) / S1;
-    C = std::max<int64_t>(256, std::min<int64_t>(8192, C));        // a multiple of PT (g_len is one of 1024)
+    // positions per chunk of work: the chunk's per-(sample, position) counters (~8 B each) stay cache-sized
+    static const int64_t c_env = std::getenv("NGSEP_POP_CHUNK") ? std::atoll(std::getenv("NGSEP_POP_CHUNK")) : 0;   // tuning
+    int64_t C = c_env > 0 ? c_env : ((int64_t)1 << 19) / S1;
+    C = std::max<int64_t>(256, std::min<int64_t>(8192, C)) / PT * PT;   // a multiple of PT (g_len is one of 1024)
     const int64_t nchunk = (g_len + C - 1) / C, ntile = g_len / PT;
     s.tile = (int32_t)PT;
     s.h_prow.assign((size_t)ntile * S1, 0);
@@ -1710,7 +1705,7 @@ static int build_multi_layout(Staged& s) {
             const int64_t gfirst = R[r * 4], glast = R[r * 4 + 1];
             const int64_t a = std::max(gfirst, c0), b = std::min(glast, c1 - 1);
             if (b < a) continue;
-            f(sample_of(r), a, b, slots + (size_t)R[r * 4 + 2] * SL + (a - gfirst));
+            f(sample_of(r), a, b, rptr[r] + (a - gfirst));
         }
     };
     struct Out { std::vector<int32_t> pos; std::vector<uint8_t> n; std::vector<uint8_t> bytes; };
@@ -1720,11 +1715,14 @@ static int build_multi_layout(Staged& s) {
         std::vector<uint16_t> nz((size_t)S1 * C), nv((size_t)S * C);
         std::vector<uint8_t> alt((size_t)S * C);
         std::vector<uint32_t> cur((size_t)S * C);
+        std::vector<uint32_t> cand;
+        static_assert(kMaxSamplesDevice < 256, "candidate keys hold the sample in 8 bits");
         for (int64_t k = k0; k < k1; k++) {
             const int64_t c0 = k * C, c1 = std::min(g_len, c0 + C), len = c1 - c0;
             std::fill(nz.begin(), nz.end(), 0);
             std::fill(nv.begin(), nv.end(), 0);
             std::fill(alt.begin(), alt.end(), 0);
+            cand.clear();
             // calls per (sample, position); flag the positions with a valid call of another allele
             each_read(c0, c1, [&](int s1, int64_t a, int64_t b, const uint8_t* src) {
                 uint16_t* z = &nz[(size_t)s1 * C];
@@ -1746,7 +1744,10 @@ static int build_multi_layout(Staged& s) {
                     if (!(cd & kCodeValid)) continue;
                     v[p - c0]++;
                     const uint8_t rc = ref[p];
-                    if ((rc & kRefCallable) && ((rc ^ cd) & 0x60)) x[p - c0] = 1;
+                    if ((rc & kRefCallable) && ((rc ^ cd) & 0x60) && !x[p - c0]) {
+                        x[p - c0] = 1;
+                        cand.push_back((uint32_t)(p - c0) << 8 | (uint32_t)s1);   // a candidate column (sparse)
+                    }
                 }
             });
             // KPM rows per (tile, sample)
@@ -1757,20 +1758,24 @@ static int build_multi_layout(Staged& s) {
                     for (int64_t p = 0; p < PT; p++) mx = std::max(mx, z[p]);
                     s.h_prow[(size_t)t * S1 + s1] = mx;
                 }
-            // KTM columns
+            // KTM columns, position-major then sample (the candidate list sorted; no dense scan of every column)
             Out& o = outs[(size_t)k];
             uint32_t nb = 0;
-            for (int64_t p = 0; p < len; p++)
-                for (int sm = 0; sm < S; sm++) {
-                    const size_t i = (size_t)sm * C + p;
-                    if (!alt[i]) continue;
-                    o.pos.push_back((int32_t)(c0 + p));
-                    const bool deep = nv[i] > kMcMaxCalls;
-                    o.n.push_back(deep ? 255 : (uint8_t)nv[i]);
-                    cur[i] = nb;
-                    if (deep) alt[i] = 0;       // no bytes
-                    else nb += nv[i];
-                }
+            std::sort(cand.begin(), cand.end());
+            o.pos.reserve(cand.size());
+            o.n.reserve(cand.size());
+            for (uint32_t key : cand) {
+                const int64_t p = key >> 8;
+                const int sm = (int)(key & 255u);
+                const size_t i = (size_t)sm * C + (size_t)p;
+                o.pos.push_back((int32_t)(c0 + p));
+                const bool deep = nv[i] > kMcMaxCalls;
+                o.n.push_back(deep ? 255 : (uint8_t)nv[i]);
+                cur[i] = nb;
+                if (deep) alt[i] = 0;       // no bytes
+                else nb += nv[i];
+            }
+            (void)len;
             o.bytes.resize(nb);
             if (!nb) continue;
             uint8_t* out = o.bytes.data();
@@ -1788,6 +1793,7 @@ static int build_multi_layout(Staged& s) {
         }
     });
     if (overflow) return -1;
+    lap("counts + candidate columns");
     // KTM entries and bytes, concatenated in chunk order
     std::vector<int64_t> eoff((size_t)nchunk + 1, 0), boff((size_t)nchunk + 1, 0);
     for (int64_t k = 0; k < nchunk; k++) {
@@ -1820,6 +1826,7 @@ static int build_multi_layout(Staged& s) {
     s.h_mc_gbase.back() = off;
     s.pile_bytes = nbytes;
     s.n_tiles = (ne + 63) / 64;         // KTM's groups of 64 columns
+    lap("column concatenation");
     // KPM pile: block offsets, then the columns filled chunk by chunk in getAlleleCalls order
     // site-major inside a tile: position p's columns of every sample are consecutive (sample order), so KPM's
     // workgroup at p reads one contiguous run of stride_t bytes; pboff[t * S1 + s] = the tile's base + the earlier
@@ -1851,7 +1858,7 @@ static int build_multi_layout(Staged& s) {
         std::vector<int64_t> rl;
         std::vector<uint32_t> key;
         std::vector<int32_t> cnt((size_t)S1 * 128 + 1);
-        std::vector<int64_t> sorted;
+        std::vector<int64_t> sorted, tcnt, tfill, tlist;
         for (int64_t k = k0; k < k1; k++) {
             const int64_t c0 = k * C, c1 = std::min(g_len, c0 + C);
             const int64_t t0 = c0 / PT, t1 = c1 / PT;
@@ -1870,21 +1877,42 @@ static int build_multi_layout(Staged& s) {
             for (size_t i = 1; i < cnt.size(); i++) cnt[i] += cnt[i - 1];
             sorted.resize(rl.size());
             for (size_t i = 0; i < rl.size(); i++) sorted[(size_t)cnt[key[i]]++] = rl[i];
+            // tile by tile (a tile's site-major block is stride_t x PT bytes: cache-resident while it fills), each
+            // tile's reads in the sorted order
+            const int64_t nt = t1 - t0;
+            tcnt.assign((size_t)nt + 1, 0);
             for (int64_t r : sorted) {
-                const int s1 = sample_of(r);
-                const int64_t gfirst = R[r * 4], glast = R[r * 4 + 1];
-                const int64_t a = std::max(gfirst, c0), b = std::min(glast, c1 - 1);
-                const uint8_t* src = slots + (size_t)R[r * 4 + 2] * SL + (a - gfirst);
-                uint16_t* cc = &cu[(size_t)s1 * C];
-                for (int64_t p = a; p <= b; p++) {
-                    const uint8_t cd = src[p - a];
-                    if (!cd) continue;
-                    const size_t bi = (size_t)(p / PT) * S1 + s1;
-                    pile[s.h_pboff[bi] + (p % PT) * pstride[(size_t)(p / PT)] + cc[p - c0]++] = cd;
+                const int64_t a = std::max<int64_t>(R[r * 4], c0), b = std::min<int64_t>(R[r * 4 + 1], c1 - 1);
+                for (int64_t t = a / PT; t <= b / PT; t++) tcnt[(size_t)(t - t0) + 1]++;
+            }
+            for (int64_t t = 0; t < nt; t++) tcnt[(size_t)t + 1] += tcnt[(size_t)t];
+            tlist.resize((size_t)tcnt[(size_t)nt]);
+            tfill.assign(tcnt.begin(), tcnt.end() - 1);
+            for (int64_t r : sorted) {
+                const int64_t a = std::max<int64_t>(R[r * 4], c0), b = std::min<int64_t>(R[r * 4 + 1], c1 - 1);
+                for (int64_t t = a / PT; t <= b / PT; t++) tlist[(size_t)tfill[(size_t)(t - t0)]++] = r;
+            }
+            for (int64_t t = t0; t < t1; t++) {
+                const int64_t p0 = t * PT, p1 = p0 + PT - 1;
+                const int64_t stride = pstride[(size_t)t];
+                for (int64_t j = tcnt[(size_t)(t - t0)]; j < tcnt[(size_t)(t - t0) + 1]; j++) {
+                    const int64_t r = tlist[(size_t)j];
+                    const int s1 = sample_of(r);
+                    const int64_t gfirst = R[r * 4], glast = R[r * 4 + 1];
+                    const int64_t a = std::max(gfirst, p0), b = std::min(glast, p1);
+                    const uint8_t* src = rptr[r] + (a - gfirst);
+                    uint16_t* cc = &cu[(size_t)s1 * C];
+                    uint8_t* blk = pile + s.h_pboff[(size_t)t * S1 + s1];
+                    for (int64_t p = a; p <= b; p++) {
+                        const uint8_t cd = src[p - a];
+                        if (!cd) continue;
+                        blk[(p - p0) * stride + cc[p - c0]++] = cd;
+                    }
                 }
             }
         }
     });
+    lap("population pile");
     return 0;
 }
 
@@ -1976,43 +2004,41 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
         c->stats.slot_bytes = 0;
         c->stats.slot_size = 0;
     } else {
-        const int S = choose_slot_size(contigs);
-        s.slot_size = S;
-        // reads and slots (read-major SoA: the population kernel walks it in pending order)
-        int64_t nslots = 0;
-        for (size_t wi = 0; wi < s.windows.size(); wi++) {
-            const ContigReads& cr = contigs[wr[wi].contig];
-            for (int64_t i = ranges[wi].first; i < ranges[wi].second; i++) {
-                int64_t span = (int64_t)cr.last[i] - cr.first[i] + 1;
-                if (span < 1) span = 1;
-                nslots += (span + S - 1) / S;
-            }
-        }
-        s.h_slots.assign((size_t)nslots * S, 0);
+        // the reads in pending order with their projected bytes in place (no copy): the population layout reads
+        // them through h_rptr
+        s.slot_size = 0;
         s.h_reads.resize((size_t)nreads * 4);
-        int64_t slot = 0, ri = 0;
+        s.h_rptr.resize((size_t)nreads);
+        std::vector<int64_t> wbase(s.windows.size() + 1, 0);
+        for (size_t wi = 0; wi < s.windows.size(); wi++) wbase[wi + 1] = wbase[wi] + (ranges[wi].second - ranges[wi].first);
         for (size_t wi = 0; wi < s.windows.size(); wi++) {
             Window& w = s.windows[wi];
             const ContigReads& cr = contigs[wr[wi].contig];
-            w.read_begin = ri;
+            w.read_begin = wbase[wi];
+            w.read_end = wbase[wi + 1];
             const int64_t goff = w.gbase + w.pad - w.w0;   // G = pos + goff
-            for (int64_t i = ranges[wi].first; i < ranges[wi].second; i++) {
-                int64_t span = (int64_t)cr.last[i] - cr.first[i] + 1;
-                int64_t ns = span < 1 ? 1 : (span + S - 1) / S;
-                int64_t gfirst = cr.first[i] + goff;
-                s.h_reads[ri * 4 + 0] = (int32_t)gfirst;
-                s.h_reads[ri * 4 + 1] = (int32_t)(cr.last[i] + goff);
-                s.h_reads[ri * 4 + 2] = (int32_t)slot;
-                int32_t fl = cr.neg[i];
-                if (!cr.sample.empty()) fl |= ((int32_t)cr.rank[i] << 1) | (((int32_t)cr.sample[i] + 1) << 8);
-                s.h_reads[ri * 4 + 3] = fl;
-                if (span > 0) std::memcpy(&s.h_slots[(size_t)slot * S], cr.bptr[i], (size_t)span);
-                slot += ns;
-                nbases += span > 0 ? span : 0;
-                ri++;
-            }
-            w.read_end = ri;
+            const int64_t i0 = ranges[wi].first;
+            std::atomic<int64_t> nb{0};
+            parallel_for(ranges[wi].second - i0, 1 << 14, [&](int64_t lo, int64_t hi) {
+                int64_t local = 0;
+                for (int64_t k = lo; k < hi; k++) {
+                    const int64_t i = i0 + k, ri = wbase[wi] + k;
+                    const int64_t span = (int64_t)cr.last[i] - cr.first[i] + 1;
+                    s.h_reads[ri * 4 + 0] = (int32_t)(cr.first[i] + goff);
+                    s.h_reads[ri * 4 + 1] = (int32_t)(cr.last[i] + goff);
+                    s.h_reads[ri * 4 + 2] = 0;
+                    int32_t fl = cr.neg[i];
+                    if (!cr.sample.empty()) fl |= ((int32_t)cr.rank[i] << 1) | (((int32_t)cr.sample[i] + 1) << 8);
+                    s.h_reads[ri * 4 + 3] = fl;
+                    s.h_rptr[(size_t)ri] = cr.bptr[i];
+                    local += span > 0 ? span : 0;
+                }
+                nb += local;
+            });
+            nbases += nb.load();
         }
+        const int S = 0;
+        const int64_t nslots = 0;
         s.n_reads = nreads;
         s.n_slots = nslots;
         s.n_read_bases = nbases;
@@ -2045,6 +2071,21 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
             s.known = true;
         }
         const int lr = build_multi_layout(s);
+        if (const char* dump = std::getenv("NGSEP_DUMP_POP_LAYOUT")) {   // diagnostics: a digest of the population layout
+            auto fnv = [](const void* p, size_t n) {
+                uint64_t h = 1469598103934665603ull;
+                for (size_t i = 0; i < n; i++) { h ^= static_cast<const uint8_t*>(p)[i]; h *= 1099511628211ull; }
+                return (unsigned long long)h;
+            };
+            if (std::FILE* f = std::fopen(dump, "w")) {
+                std::fprintf(f, "mc_pos %llu\nmc_n %llu\nmc_gbase %llu\npile %llu\nppile %llu\nprow %llu\npboff %llu\n",
+                             fnv(s.h_mc_pos.data(), s.h_mc_pos.size() * 4), fnv(s.h_mc_n.data(), s.h_mc_n.size()),
+                             fnv(s.h_mc_gbase.data(), s.h_mc_gbase.size() * 8), fnv(s.h_pile.data(), s.h_pile.size()),
+                             fnv(s.h_ppile.get(), (size_t)s.ppile_bytes), fnv(s.h_prow.data(), s.h_prow.size() * 2),
+                             fnv(s.h_pboff.data(), s.h_pboff.size() * 8));
+                std::fclose(f);
+            }
+        }
         if (lr == -2) return set_error(c, NGSEP_E_DEVICE, "host memory for the population pile could not be allocated");
         if (lr != 0) return set_error(c, NGSEP_E_UNSUPPORTED, "a sample's pileup is deeper than 65535 alignments");
         c->stats.slot_bytes = s.ppile_bytes;
@@ -2072,7 +2113,7 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h1).count(),
                      (long long)nreads, (long long)s.n_tiles);
     // host mirrors are not needed any more
-    std::vector<uint8_t>().swap(s.h_slots);
+    std::vector<const uint8_t*>().swap(s.h_rptr);
     std::vector<int32_t>().swap(s.h_reads);
     std::vector<uint8_t>().swap(s.h_ref);
     std::vector<uint8_t>().swap(s.h_pile);

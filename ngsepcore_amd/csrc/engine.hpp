@@ -461,7 +461,7 @@ struct Staged {            // everything resident for one run
     int64_t n_tiles = 0;
     int64_t pile_bytes = 0;
     // host mirrors (freed after upload)
-    std::vector<uint8_t> h_slots;
+    std::vector<const uint8_t*> h_rptr;  // multisample: each read's projected bytes (the sequence's chunks, in place)
     std::vector<uint8_t> h_pile;
     std::vector<TileInfo> h_tinfo;
     std::vector<int32_t> h_reads;       // 4 ints per read: gfirst, glast, slot, flags
@@ -500,6 +500,7 @@ struct Staged {            // everything resident for one run
     bool rg = false;
     int64_t n_entries = 0, n_groups = 0, n_units = 0;
     uint64_t* h_units = nullptr;
+    bool units_pinned = true;           // h_units is the arena's pinned block (false: pageable, copied synchronously)
     std::vector<int32_t> h_rh;          // 2 per entry
     std::vector<RGroup> h_grp;
     std::vector<int32_t> h_blkA, h_blkB;
@@ -522,6 +523,7 @@ struct LayoutArena {
     int64_t cap = 0;
     uint64_t* units = nullptr;          // read-group layout units
     int64_t units_cap = 0;
+    bool units_pinned = false;          // false: a pageable block (a layout beyond 4 GB, engine.cpp ensure_units)
     bool ensure(int64_t pile_bytes, bool exact);
     bool ensure_units(int64_t n_units, bool exact);
     void release();
