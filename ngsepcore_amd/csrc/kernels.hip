@@ -967,16 +967,13 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
     }
 }
 
-// FUSE: the tile's survivors (up to kKlFuse of them) have their columns gathered right here by the workgroup that
-// found them (wave_gather over the tile's reads, just streamed: mostly L2 hits), so KG only compacts the queue
-constexpr int kKlFuse = 128;
-template <int T, int U, bool FUSE>
+template <int T, int U>
 __global__ __launch_bounds__(kKlThreads) void k_read_scan(
     const uint64_t* __restrict__ units, const int2* __restrict__ rh, const RGroup* __restrict__ grp,
     const int32_t* __restrict__ blkA, const int32_t* __restrict__ blkB, int64_t n_entries,
     const uint8_t* __restrict__ ref, const LikTables* __restrict__ tabs, GenotypeParams gp,
     SiteQ* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qseg,
-    int64_t cseg4, int32_t* __restrict__ bcount, int64_t nb, uint16_t* __restrict__ cols) {
+    int64_t cseg4, int32_t* __restrict__ bcount, int64_t nb) {
     constexpr int PT = T / kKlThreads;                 // positions per thread in the candidate phase
     constexpr int NC = T / 2 + 16;                     // counter words (halfword per position, margins 8 and 24)
     static_assert(PT == 8 || PT == 16, "candidate phase: whole 16-byte counter words per thread");
@@ -985,8 +982,7 @@ __global__ __launch_bounds__(kKlThreads) void k_read_scan(
     __shared__ alignas(16) uint32_t s_cnt[NC];
     __shared__ int16_t s_cb[256];
     __shared__ int32_t s_wsum[kKlThreads / 64], s_wmax[kKlThreads / 64];
-    __shared__ unsigned long long s_wscan[kKlThreads / 64], s_ncand[kKlThreads / 64], s_colbase, s_qbase, s_nsurv;
-    __shared__ int4 s_surv[FUSE ? kKlFuse : 1];        // FUSE: {position, queue slot, column offset / 4, coverage}
+    __shared__ unsigned long long s_wscan[kKlThreads / 64], s_ncand[kKlThreads / 64], s_colbase, s_qbase;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int32_t tstart = (int32_t)((int64_t)blockIdx.x * T);
     (void)n_entries;
@@ -1106,14 +1102,12 @@ __global__ __launch_bounds__(kKlThreads) void k_read_scan(
         const unsigned long long ns = tot >> 40, c4 = tot & ((1ull << 40) - 1ull);
         s_qbase = ns ? atomicAdd(&sctr[0], ns) : 0ull;
         s_colbase = ns ? atomicAdd(&sctr[1], c4) : 0ull;
-        s_nsurv = ns;
     }
     __syncthreads();
-    if (!FUSE && !need_bits) return;
+    if (!need_bits) return;
     uint64_t ex = sc - mine;
     for (int w = 0; w < wv; w++) ex += s_wscan[w];
-    int64_t si = (int64_t)(ex >> 40);                                           // the survivor's index in the tile
-    int64_t qi = (int64_t)s_qbase + si;                                         // in the shard's segment
+    int64_t qi = (int64_t)s_qbase + (int64_t)(ex >> 40);                        // in the shard's segment
     int64_t c4 = (int64_t)s_colbase + (int64_t)(ex & ((1ull << 40) - 1ull));
 #pragma unroll
     for (int j = 0; j < PT; j++) {
@@ -1121,26 +1115,9 @@ __global__ __launch_bounds__(kKlThreads) void k_read_scan(
         const int32_t cov = loc[j];
         const uint32_t rc = (rwv[j >> 2] >> (8 * (j & 3))) & 0xFFu;
         const int32_t rows = (c4 << 2) + cov <= (cseg4 << 2) ? -3 - cov : -2;   // -2: the shard's columns are full (rerun)
-        const bool fused = FUSE && si < kKlFuse && qi < qseg && rows != -2;     // (its wave writes the entry)
-        if (qi < qseg && !fused) queue[shard * qseg + qi] = SiteQ{tstart + PT * tid + j, (int32_t)rc, (int32_t)(shard * cseg4 + c4), rows};
-        if (FUSE && si < kKlFuse) s_surv[si] = make_int4(tstart + PT * tid + j, (int32_t)(fused ? qi : -1),
-                                                         (int32_t)(shard * cseg4 + c4), (int32_t)rc);
+        if (qi < qseg) queue[shard * qseg + qi] = SiteQ{tstart + PT * tid + j, (int32_t)rc, (int32_t)(shard * cseg4 + c4), rows};
         qi++;
-        si++;
         c4 += (cov + 3) >> 2;
-    }
-    if (FUSE) {
-        __syncthreads();
-        // one wave per survivor: getAlleleCalls(1) in pending order (KG's gather), the queue entry completed
-        const int64_t nsv = min((int64_t)s_nsurv, (int64_t)kKlFuse);
-        for (int64_t k = wv; k < nsv; k += kKlThreads / 64) {
-            const int4 v = s_surv[k];
-            if (v.y < 0) continue;                                          // (past the queue segment or no column space)
-            const int32_t p = v.x;
-            const int32_t n = wave_gather<true>(p, blkA[p >> kRgBlockShift], n_entries, rh, grp, units, (uint32_t)v.w,
-                                                cols + ((int64_t)v.z << 2), nullptr);
-            if (lane == 0) queue[shard * qseg + v.y] = SiteQ{p, v.w, v.z, n};
-        }
     }
 }
 
@@ -2425,12 +2402,10 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     } else if (d->n_tiles > 0 && prune) {
         // KL: one workgroup per tile of kKlTile positions, straight from the read-group layout
         // (measured on chr20 30x: 2048-position tiles and 8 loads in flight per lane beat 4096 / 16 and 24)
-        static const bool kl_fuse = std::getenv("NGSEP_KL_FUSE") != nullptr;   // tuning: KL gathers its survivors' columns
-        hipExtLaunchKernelGGL(kl_fuse ? k_read_scan<kKlTile, kKlUnroll, true> : k_read_scan<kKlTile, kKlUnroll, false>,
-                              dim3((unsigned)(s.g_len / kKlTile)), dim3(kKlThreads), 0, sl.stream, k0, k1, 0,
+        hipExtLaunchKernelGGL(k_read_scan<kKlTile, kKlUnroll>, dim3((unsigned)(s.g_len / kKlTile)), dim3(kKlThreads), 0, sl.stream, k0, k1, 0,
                               (const uint64_t*)d->d_units, (const int2*)d->d_rh, (const RGroup*)d->d_grp, (const int32_t*)d->d_blkA,
                               (const int32_t*)d->d_blkB, d->n_entries, (const uint8_t*)d->d_ref, (const LikTables*)sl.d_tables, g,
-                              sl.d_hard, ctr, sl.cap_hard / kKlShards, (sl.cap_cols >> 2) / kKlShards, sl.d_bcount, nb, sl.d_cols);
+                              sl.d_hard, ctr, sl.cap_hard / kKlShards, (sl.cap_cols >> 2) / kKlShards, sl.d_bcount, nb);
         HIP_TRY(hipGetLastError());
         kg_sites = d->last_hard + d->last_hard / 8;              // KL's survivors (sized from the previous run)
         kl_run = true;
