@@ -155,6 +155,8 @@ struct ngsep_bam {
     int store_cur = 0;
     // NGSEP_HOST_TIMING diagnostics: seconds in the decoder's inflate, the record cut, parse and emit
     double t_inflate = 0, t_wait = 0, t_need = 0, t_cut = 0, t_parse = 0, t_emit = 0;
+    int64_t n_pcut = 0, n_pcut_serial = 0;      // parallel cuts, and their segments walked sequentially
+    double t_pcut_walk = 0, t_pcut_merge = 0;
 };
 
 namespace {
@@ -506,6 +508,99 @@ extern "C" int ngsep_bam_set_region(ngsep_bam* b, const char* seq_name, int64_t 
 
 namespace {
 
+// A plausible record start at o (block_size, refID, pos, the NUL-terminated printable read name, the fixed fields'
+// sizes within block_size, next refID): where a parallel cut segment starts its own walk
+bool plausible_record(const ngsep_bam* b, const uint8_t* buf, size_t o, size_t hi) {
+    if (o + 40 > hi) return false;
+    const int32_t bs = rd<int32_t>(buf + o);
+    if (bs < 34 || bs > (1 << 22) || o + 4 + (size_t)bs > hi) return false;
+    const int32_t nref = (int32_t)b->ref_to_seq.size();
+    const int32_t refid = rd<int32_t>(buf + o + 4), pos0 = rd<int32_t>(buf + o + 8), nref2 = rd<int32_t>(buf + o + 24);
+    if (refid < -1 || refid >= nref || pos0 < -1 || nref2 < -1 || nref2 >= nref) return false;
+    const int l_name = buf[o + 12];
+    const int n_cig = rd<uint16_t>(buf + o + 16);
+    const int32_t l_seq = rd<int32_t>(buf + o + 20);
+    if (l_name < 2 || l_seq < 0) return false;
+    if (32 + (int64_t)l_name + 4 * (int64_t)n_cig + (l_seq + 1) / 2 + (int64_t)l_seq > bs) return false;
+    const uint8_t* nm = buf + o + 36;
+    for (int k = 0; k + 1 < l_name; k++)
+        if (nm[k] < 33 || nm[k] > 126 || nm[k] == '@') return false;
+    return nm[l_name - 1] == 0;
+}
+
+// The record chain over the whole decoded buffer [b->pos, b->end), cut on all host threads: segment t > 0 walks
+// its own chain from the first position that looks like two consecutive records, and the merge takes a segment's
+// offsets only from the record at which the true chain (walked from b->pos) enters it -- a chain is determined by
+// any one of its records, so the result equals the sequential walk; a segment whose walk never meets the true
+// chain is walked sequentially.  Stops at max_reads, at a record past the buffer's end, or at a malformed record
+// (left for the sequential cut to report).
+void parallel_cut(ngsep_bam* b, int64_t max_reads, size_t span, std::vector<size_t>& roff) {
+    const uint8_t* buf = b->buf;
+    const size_t lo = b->pos, hi = b->pos + span;            // (a record past hi is left to the sequential cut)
+    constexpr int T = 32;
+    size_t bnd[T + 1];
+    for (int t = 0; t <= T; t++) bnd[t] = lo + (hi - lo) / T * (size_t)t;
+    bnd[T] = hi;
+    std::vector<size_t> seg[T];
+    size_t seg_end[T] = {};
+    const auto tw0 = std::chrono::steady_clock::now();
+    // (tests: NGSEP_PCUT_MISS=1 makes every odd segment's own walk start one byte off the chain, so the merge walks it)
+    static const bool miss = std::getenv("NGSEP_PCUT_MISS") != nullptr;
+    parallel_for(T, 1, [&](int64_t t0, int64_t t1) {
+        for (int64_t t = t0; t < t1; t++) {
+            size_t o = bnd[t];
+            if (miss && (t & 1)) {
+                const int32_t bs0 = rd<int32_t>(buf + o);
+                if (bs0 < 32) continue;
+                o += 1;
+            } else if (t > 0) {
+                const size_t lim = std::min(bnd[t + 1], bnd[t] + ((size_t)1 << 20));
+                while (o < lim && !(plausible_record(b, buf, o, hi) && plausible_record(b, buf, o + 4 + (size_t)rd<int32_t>(buf + o), hi))) o++;
+                if (o >= lim) continue;
+            }
+            std::vector<size_t>& v = seg[t];
+            v.reserve((bnd[t + 1] - bnd[t]) / 200 + 16);
+            while (o < bnd[t + 1] && o + 4 <= hi) {
+                const int32_t bs = rd<int32_t>(buf + o);
+                if (bs < 32 || o + 4 + (size_t)bs > hi) break;
+                if (o + 4096 < hi) __builtin_prefetch(buf + o + 4096);
+                v.push_back(o);
+                o += 4 + (size_t)bs;
+            }
+            seg_end[t] = o;                                  // the record after the segment's last one
+        }
+    });
+    const auto tw1 = std::chrono::steady_clock::now();
+    size_t cur = lo;
+    bool stop = false;
+    for (int t = 0; t < T && !stop; t++) {
+        const std::vector<size_t>& v = seg[t];
+        auto it = std::lower_bound(v.begin(), v.end(), cur);
+        if (cur < bnd[t + 1] && it != v.end() && *it == cur) {
+            // the segment's offsets from cur on, in bulk (no record is touched again)
+            const size_t j = (size_t)(it - v.begin());
+            const size_t take = std::min(v.size() - j, (size_t)(max_reads - (int64_t)roff.size()));
+            const size_t at = roff.size();
+            roff.resize(at + take);
+            for (size_t k = 0; k < take; k++) roff[at + k] = v[j + k] + 4;
+            if (j + take < v.size()) { cur = v[j + take]; stop = true; }
+            else cur = seg_end[t];
+        }
+        if (!stop && cur < bnd[t + 1]) b->n_pcut_serial++;
+        while (!stop && cur < bnd[t + 1]) {                 // (the segment's own walk missed the chain, or stopped)
+            if ((int64_t)roff.size() >= max_reads || cur + 4 > hi) { stop = true; break; }
+            const int32_t bs = rd<int32_t>(buf + cur);
+            if (bs < 32 || cur + 4 + (size_t)bs > hi) { stop = true; break; }
+            roff.push_back(cur + 4);
+            cur += 4 + (size_t)bs;
+        }
+    }
+    b->pos = cur;
+    b->n_pcut++;
+    b->t_pcut_walk += std::chrono::duration<double>(tw1 - tw0).count();
+    b->t_pcut_merge += std::chrono::duration<double>(std::chrono::steady_clock::now() - tw1).count();
+}
+
 // one batch of up to max_reads kept records into B (ngsep_bam_next_batch)
 int fill_batch(ngsep_bam* b, ngsep_bam::BatchStore& B, int64_t max_reads, ngsep_read_batch* out, bool* retry, bool packed) {
     *retry = false;
@@ -528,6 +623,13 @@ int fill_batch(ngsep_bam* b, ngsep_bam::BatchStore& B, int64_t max_reads, ngsep_
             // the rest of this record is in the next chunk: decode the records cut so far first
             if (!roff.empty()) break;
             if (!need(b, 4 + (size_t)bs, err)) return set_error(b->ctx, NGSEP_E_FORMAT, err.empty() ? "truncated BAM record" : err);
+        }
+        // a decoded chunk's worth of records (bounded by max_reads at 512 B a record): cut on all threads; the
+        // sequential walk below picks up where it stopped
+        const size_t span = std::min(b->end - b->pos, (size_t)max_reads * 512);
+        if (roff.empty() && b->region_ref < 0 && span >= ((size_t)8 << 20)) {
+            parallel_cut(b, max_reads, span, roff);
+            continue;
         }
         const uint8_t* r = &b->buf[b->pos + 4];
         // the record chain is a dependent walk through freshly inflated memory: pull the lines a few
@@ -771,8 +873,9 @@ extern "C" int ngsep_bam_close(ngsep_bam* b) {
     if (!b) return NGSEP_E_INVALID;
     stop_decoder(b);
     if (std::getenv("NGSEP_HOST_TIMING"))
-        std::fprintf(stderr, "[ngsep host] bam: inflate %.3f s (decoder thread), consumer wait %.3f s, need %.3f s, cut %.3f s (incl. wait), parse %.3f s, emit %.3f s\n",
-                     b->t_inflate, b->t_wait, b->t_need, b->t_cut, b->t_parse, b->t_emit);
+        std::fprintf(stderr, "[ngsep host] bam: inflate %.3f s (decoder thread), consumer wait %.3f s, need %.3f s, cut %.3f s (incl. wait; %lld parallel: walks %.3f s, merge %.3f s, %lld segments walked sequentially), parse %.3f s, emit %.3f s\n",
+                     b->t_inflate, b->t_wait, b->t_need, b->t_cut, (long long)b->n_pcut, b->t_pcut_walk, b->t_pcut_merge,
+                     (long long)b->n_pcut_serial, b->t_parse, b->t_emit);
     if (b->f) std::fclose(b->f);
     delete b;
     return NGSEP_OK;

@@ -1646,8 +1646,8 @@ __device__ PopCall genotype_sample_d(const double* L, const int* cnt, int total,
 }
 
 // POOL: ploidy >= 3 (the pool branch's report arrays would otherwise cost every run registers and scratch)
-template <bool POOL>
-__global__ __launch_bounds__(kPopThreads) void k_posterior_multi(
+template <bool POOL, int WPE>
+__global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE))) void k_posterior_multi(
     const QueueSite* __restrict__ queue, const unsigned long long* qn, int64_t qcap,
     const uint8_t* __restrict__ ppile, const uint16_t* __restrict__ prow, const int64_t* __restrict__ pboff,
     const LikTables* __restrict__ tabs, GenotypeParams gp,
@@ -2002,6 +2002,14 @@ __global__ __launch_bounds__(1024) void ko_fused(const SiteRec* __restrict__ bre
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
+// a launch's error; with NGSEP_SYNC_CHECK (diagnostics) the device is drained after every launch, so a fault
+// is reported at the launch (HIP_TRY's line) that caused it
+static hipError_t launch_check() {
+    static const bool sync = std::getenv("NGSEP_SYNC_CHECK") != nullptr;
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !sync) return e;
+    return hipDeviceSynchronize();
+}
 void* pinned_alloc(size_t bytes) {
     void* p = std::aligned_alloc(4096, (bytes + 4095) / 4096 * 4096);
     if (p && hipHostRegister(p, bytes, hipHostRegisterDefault) != hipSuccess) {
@@ -2188,7 +2196,12 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
     // single sample (a streamed window or a whole run): buffers kept across runs while large enough; the
     // multisample run starts from nothing
     const bool keep = s.single && d->d_ppile == nullptr;
-    if (!keep) device_release(d);
+    if (!keep) {
+        // (a fault of earlier work is reported as such, not against this upload's copies)
+        const hipError_t e = hipDeviceSynchronize();
+        if (e != hipSuccess) { err = std::string("device fault pending before the upload (earlier work): ") + hipGetErrorString(e); return -1; }
+        device_release(d);
+    }
     else HIP_TRY(hipDeviceSynchronize());          // the previous run is done reading them
     if (ensure_dev(&d->d_ref, &d->cap_ref, (size_t)s.g_len + 64, keep, err)) return -1;
     HIP_TRY(hipMemsetAsync(d->d_ref + s.g_len, 0, 64, d->stream));
@@ -2396,7 +2409,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
             HIP_TRY(hipMemcpyAsync(sl.d_cols, s.h_cols.data(), s.h_cols.size() * sizeof(uint16_t), hipMemcpyHostToDevice, sl.stream));
         HIP_TRY(hipMemcpyAsync(ctr, s.h_forced_ctr, 8 * sizeof(unsigned long long), hipMemcpyHostToDevice, sl.stream));
         hipLaunchKernelGGL(k_zero_i32, dim3((unsigned)std::min<int64_t>((nb + 255) / 256, 4096)), dim3(256), 0, sl.stream, sl.d_bcount, nb);
-        HIP_TRY(hipGetLastError());
+        HIP_TRY(launch_check());
         d->last_hard = nforced;
         kg_sites = nforced;
     } else if (d->n_tiles > 0 && prune) {
@@ -2406,7 +2419,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
                               (const uint64_t*)d->d_units, (const int2*)d->d_rh, (const RGroup*)d->d_grp, (const int32_t*)d->d_blkA,
                               (const int32_t*)d->d_blkB, d->n_entries, (const uint8_t*)d->d_ref, (const LikTables*)sl.d_tables, g,
                               sl.d_hard, ctr, sl.cap_hard / kKlShards, (sl.cap_cols >> 2) / kKlShards, sl.d_bcount, nb);
-        HIP_TRY(hipGetLastError());
+        HIP_TRY(launch_check());
         kg_sites = d->last_hard + d->last_hard / 8;              // KL's survivors (sized from the previous run)
         kl_run = true;
     } else {
@@ -2414,7 +2427,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((s.g_len + 255) / 256, (int64_t)d->n_cu * 8));
         hipExtLaunchKernelGGL(k_queue_all, dim3((unsigned)nblk), dim3(256), 0, sl.stream, k0, k1, 0, (const uint8_t*)d->d_ref,
                               s.g_len, sl.d_hard, ctr, sl.cap_hard, sl.d_bcount, nb);
-        HIP_TRY(hipGetLastError());
+        HIP_TRY(launch_check());
         kg_sites = s.g_len;
     }
     {
@@ -2435,7 +2448,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
                            (const int2*)d->d_rh, (const RGroup*)d->d_grp,
                            (const uint64_t*)d->d_units, (const int32_t*)d->d_blkA, (const uint8_t*)d->d_ref, d->n_entries, sl.d_cols,
                            sl.cap_cols, ctr);
-        HIP_TRY(hipGetLastError());
+        HIP_TRY(launch_check());
     }
     // one lane per queued site: enough workgroups for the queue (the count is on the device; sized from the
     // previous run's survivors, grid-stride beyond)
@@ -2453,11 +2466,11 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
                               (const SiteQ*)sl.d_hard2, (const unsigned long long*)(ctr + 2), sl.cap_hard, (const uint16_t*)sl.d_cols,
                               (const LikTables*)sl.d_tables, g, sl.d_brec, sl.d_bcount, shift, bcap, sl.d_ext, ctr + 4, sl.cap_ext);
     }
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(launch_check());
     // order the records by position on the device (one kernel; counters[0] = records | max bucket << 40)
     hipLaunchKernelGGL(ko_fused, dim3((unsigned)((nb + kKofBuckets - 1) / kKofBuckets)), dim3(64 * kKofBuckets), 0, sl.stream, sl.d_brec,
                        (const int32_t*)sl.d_bcount, nb, bcap, ctr, sl.d_sorted, sl.cap, d->d_wins, d->n_wins, 1 << shift);
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(launch_check());
     // copies: counters and a prefix of the ordered records (sized from the previous run) straight into
     // the slot's pinned store, then the counter set is cleared for the slot's next run.  On the copy
     // stream (ordered after KO by ev[3]) or, with NGSEP_COPY_ON_COMPUTE=1, on the compute stream
@@ -2723,7 +2736,7 @@ int device_run_rac(Device* d, const Staged& s, int64_t g0, int64_t g1, int32_t m
     HIP_TRY(hipMemsetAsync(d->d_rac, 0, 64 * sizeof(unsigned long long), d->stream));
     hipExtLaunchKernelGGL(k_rac, dim3(kRacBlocks), dim3(kRacThreads), 0, d->stream, d->ev[0], d->ev[1], 0,
                           (const uint8_t*)d->d_pile, (const TileInfo*)d->d_tinfo, d->log2_tile, g0, g1, min_rd, min_bq, hist, part);
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(launch_check());
     HIP_TRY(hipMemcpyAsync(d->h_rac, d->d_rac, 64 * sizeof(unsigned long long) + 2 * kRacBlocks * sizeof(double), hipMemcpyDeviceToHost, d->stream));
     HIP_TRY(hipStreamSynchronize(d->stream));
     const unsigned long long* hh = reinterpret_cast<const unsigned long long*>(d->h_rac);
@@ -2737,6 +2750,14 @@ int device_run_rac(Device* d, const Staged& s, int64_t g0, int64_t g1, int32_t m
     (void)hipEventElapsedTime(&ms, d->ev[0], d->ev[1]);
     *kernel_ms = ms;
     return 0;
+}
+
+// KPM's variant and grid: registers capped for 4 waves per SIMD (145 -> 128 VGPRs; a few spill) and 16384
+// workgroups looping over the queue (measured on configs[4]: 235 -> 204 us against 3 waves and 2048 workgroups)
+constexpr int kKpmWavesPerEu = 4;
+constexpr unsigned kKpmGrid = 16384;
+static auto kpm_kernel(int ploidy) {
+    return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu> : k_posterior_multi<false, kKpmWavesPerEu>;
 }
 
 // MultisampleVariantsDetector run: KTM over every resident tile, KPM over the queued positions,
@@ -2791,24 +2812,24 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
         hipExtLaunchKernelGGL(k_scan_multi, dim3((unsigned)nblk), dim3(256), 0, d->stream, d->ev[0], nullptr, 0,
                               (const int32_t*)d->d_mc_pos, (const uint8_t*)d->d_mc_n, (const int64_t*)d->d_mc_gbase,
                               (const uint8_t*)d->d_pile, d->mc_entries, (const LikTables*)d->d_tables, g, d->d_need, ctr);
-        HIP_TRY(hipGetLastError());
+        HIP_TRY(launch_check());
         const int64_t qblk = std::max<int64_t>(1, std::min<int64_t>((nwords + 255) / 256, (int64_t)d->n_cu * 4));
         hipExtLaunchKernelGGL(k_queue_need, dim3((unsigned)qblk), dim3(256), 0, d->stream, nullptr, d->ev[1], 0,
                               (const uint32_t*)d->d_need, (const uint8_t*)d->d_ref, nwords, d->d_hard, ctr, d->cap_hard);
-        HIP_TRY(hipGetLastError());
+        HIP_TRY(launch_check());
     }
     }
     if (ploidy >= 3 && !d->pool_valid) { err = "ploidy >= 3 without pool tables (device_set_pool)"; return -1; }
     // (no start event on KPM: a start event between KQN and KPM was measured to idle the device; KPM's time is
     // taken from KQN's end)
-    hipExtLaunchKernelGGL(ploidy >= 3 ? k_posterior_multi<true> : k_posterior_multi<false>, dim3(2048), dim3(kPopThreads), 0, d->stream, nullptr, d->ev[2], 0,
+    hipExtLaunchKernelGGL(kpm_kernel(ploidy), dim3(kKpmGrid), dim3(kPopThreads), 0, d->stream, nullptr, d->ev[2], 0,
                           (const QueueSite*)(mknown ? d->d_mforced : d->d_hard),
                           (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : ctr + 2),
                           mknown ? std::max<int64_t>(d->n_mforced, 1) : d->cap_hard, (const uint8_t*)d->d_ppile,
                           (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, (const LikTables*)d->d_tables, g,
                           S, min_adf, ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), d->d_psites, d->d_pcalls,
                           ctr, d->cap_psites, d->d_stamps);
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(launch_check());
     HIP_TRY(hipMemcpyAsync(d->h_counters, ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, d->stream));
     HIP_TRY(hipStreamSynchronize(d->stream));
     const unsigned long long c3 = d->h_counters[3];
@@ -2946,7 +2967,7 @@ int device_fetch_calls_from(Device* d, const ngsep_sample_call* calls, hipStream
     hipLaunchKernelGGL(k_gather_calls, dim3((unsigned)nblk), dim3(256), 0, stream, calls, (const int64_t*)d->d_csrc, m, S,
                        d->d_pcalls_ord, d->d_pbig, d_nbig, d->cap_pcalls_ord, (int64_t)big->size(),
                        std::getenv("NGSEP_POP_ALL_BIG") ? 1 : 0);   // (tests: every call through the whole-record list)
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(launch_check());
     HIP_TRY(hipMemcpyAsync(dst, d->d_pcalls_ord, (size_t)(m * S) * sizeof(PopCall32), hipMemcpyDeviceToHost, stream));
     unsigned long long* h_nbig = reinterpret_cast<unsigned long long*>(d->h_csrc + d->cap_csrc);
     HIP_TRY(hipMemcpyAsync(h_nbig, d_nbig, sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
@@ -3068,20 +3089,20 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
     hipExtLaunchKernelGGL(k_scan_multi, dim3((unsigned)nblk), dim3(256), 0, d->stream, m.ev[0], nullptr, 0,
                           (const int32_t*)d->d_mc_pos, (const uint8_t*)d->d_mc_n, (const int64_t*)d->d_mc_gbase,
                           (const uint8_t*)d->d_pile, d->mc_entries, (const LikTables*)d->d_tables, g, m.d_need, ctr);
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(launch_check());
     const int64_t qblk = std::max<int64_t>(1, std::min<int64_t>((nwords + 255) / 256, (int64_t)d->n_cu * 4));
     hipExtLaunchKernelGGL(k_queue_need, dim3((unsigned)qblk), dim3(256), 0, d->stream, nullptr, m.ev[1], 0,
                           (const uint32_t*)m.d_need, (const uint8_t*)d->d_ref, nwords, m.d_hard, ctr, m.cap_hard);
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(launch_check());
     }
-    hipExtLaunchKernelGGL(ploidy >= 3 ? k_posterior_multi<true> : k_posterior_multi<false>, dim3(2048), dim3(kPopThreads), 0, d->stream, nullptr, m.ev[3], 0,
+    hipExtLaunchKernelGGL(kpm_kernel(ploidy), dim3(kKpmGrid), dim3(kPopThreads), 0, d->stream, nullptr, m.ev[3], 0,
                           (const QueueSite*)(mknown ? d->d_mforced : m.d_hard),
                           (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : ctr + 2),
                           mknown ? std::max<int64_t>(d->n_mforced, 1) : m.cap_hard, (const uint8_t*)d->d_ppile,
                           (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, (const LikTables*)d->d_tables, g,
                           S, min_adf, ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), m.d_psites, m.d_pcalls,
                           ctr, m.cap_psites, (unsigned long long*)nullptr);
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(launch_check());
     // the calls packed right behind KPM on the compute stream; the copies (counters, a guess of the sites, their
     // packed calls and whole records) on the copy stream, so the next pass's kernels do not wait for them
     if (m.cap_pack < m.cap_psites) {
@@ -3106,7 +3127,7 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
     hipLaunchKernelGGL(k_pack_calls, dim3((unsigned)pblk), dim3(256), 0, d->stream, (const ngsep_sample_call*)m.d_pcalls,
                        (const unsigned long long*)ctr, m.cap_psites, (int64_t)S, m.d_pack, m.d_big, d_nbig, m.cap_big,
                        std::getenv("NGSEP_POP_ALL_BIG") ? 1 : 0);   // (tests: every call through the whole-record list)
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(launch_check());
     HIP_TRY(hipEventRecord(m.ev[5], d->stream));
     HIP_TRY(hipStreamWaitEvent(d->copy_stream, m.ev[5], 0));
     hipStream_t cs = d->copy_stream;

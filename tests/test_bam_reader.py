@@ -55,12 +55,14 @@ def _read_all(lib, ctx, bam, batch_reads=1 << 20, region=None):
 
 @pytest.mark.parametrize("kw,batch_reads", [
     (dict(genome=pysynth.YEAST, n_contigs=3, depth=12, seed=21), 1 << 20),
+    (dict(genome=pysynth.YEAST, n_contigs=3, depth=12, seed=22, softclip_rate=0.05), 20000),   # parallel cuts stopped at max_reads
     (dict(genome=pysynth.YEAST, n_contigs=2, depth=15, seed=7, secondary_rate=0.02, lowmq_rate=0.02, noqual_rate=0.01,
           softclip_rate=0.05, dup_rate=0.03, quality_model=2), 777),
 ])
 def test_reader_matches_generator(tmp_path, kw, batch_reads):
     """Every record the reader keeps (after isSameAlignment, isMultiple and the filter flags) equals the
-    generator's filtered view, in order, whatever the batch size (records cut across decoded chunks)."""
+    generator's filtered view, in order, whatever the batch size (records cut across decoded chunks; a whole
+    decoded chunk cut on all threads, bam.cpp parallel_cut, at 1 << 20 and 20000 reads a batch)."""
     syn = pysynth.Synth(**kw)
     _, _, bam = syn.write(os.path.join(str(tmp_path), "r"))
     lib, ctx = _ctx(syn.contigs())
@@ -70,6 +72,35 @@ def test_reader_matches_generator(tmp_path, kw, batch_reads):
     syn.close()
     assert len(got) == len(want) > 1000
     assert got == want
+
+
+def test_parallel_cut_merge_walks_missed_segments(tmp_path, monkeypatch):
+    """A parallel-cut segment whose own walk never meets the true record chain is walked sequentially by the
+    merge (NGSEP_PCUT_MISS: odd segments start off the chain): the records are the same."""
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=3, depth=12, seed=23)
+    _, _, bam = syn.write(os.path.join(str(tmp_path), "m"))
+    import subprocess
+    import sys
+    code = ("import sys; sys.path[:0] = %r; import test_bam_reader as t, pysynth, hashlib; "
+            "syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=3, depth=12, seed=23); "
+            "lib, ctx = t._ctx(syn.contigs()); print(hashlib.sha1(repr(t._read_all(lib, ctx, %r)).encode()).hexdigest())"
+            % (sys.path[:6], bam))
+    runs = []
+    for miss in ("", "1"):
+        env = dict(os.environ, NGSEP_HOST_TIMING="1")
+        env.pop("NGSEP_PCUT_MISS", None)
+        if miss:
+            env["NGSEP_PCUT_MISS"] = miss
+        out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+        runs.append(out.stdout.strip())
+        if miss:
+            assert "0 segments walked sequentially" not in out.stderr, out.stderr
+    lib, ctx = _ctx(syn.contigs())
+    want = _records(syn.batch())
+    lib.ngsep_close(ctx)
+    syn.close()
+    import hashlib
+    assert runs[0] == runs[1] == hashlib.sha1(repr(want).encode()).hexdigest()
 
 
 def test_reader_zlib_and_libdeflate_agree(tmp_path, monkeypatch):
