@@ -17,6 +17,8 @@
 #include <vector>
 #include <atomic>
 #include <mutex>
+#include <condition_variable>
+#include <functional>
 #include <utility>
 
 #include "../../include/ngsep_gpu.h"
@@ -256,6 +258,63 @@ inline unsigned host_threads() {
     }();
     return n;
 }
+// The host worker pool: host_threads() - 1 persistent workers shared by every parallel_for, whichever thread calls
+// it (the BGZF decoder, the batch reader, the admission sweep and the layouts run concurrently; threads created per
+// call oversubscribed the cores).  A call queues helper tickets and works itself; on finishing it cancels the
+// tickets no worker has taken and waits only for the taken ones, so nested and concurrent calls cannot deadlock.
+class HostPool {
+public:
+    struct Job {
+        std::function<void()> work;
+        std::unique_ptr<std::atomic<int>[]> state;   // per ticket: 0 queued, 1 taken, 2 done, 3 cancelled
+        int n = 0;
+        std::mutex mu;
+        std::condition_variable cv;
+    };
+    static HostPool& get() {
+        static HostPool* p = new HostPool((int)host_threads() - 1);   // (never destroyed: workers outlive statics)
+        return *p;
+    }
+    int workers() const { return (int)th_.size(); }
+    void submit(const std::shared_ptr<Job>& job) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            for (int k = 0; k < job->n; k++) q_.emplace_back(job, k);
+        }
+        if (job->n == 1) cv_.notify_one();
+        else cv_.notify_all();
+    }
+private:
+    explicit HostPool(int n) {
+        for (int k = 0; k < n; k++) th_.emplace_back([this] { loop(); });
+        for (auto& t : th_) t.detach();
+    }
+    void loop() {
+        for (;;) {
+            std::pair<std::shared_ptr<Job>, int> tk;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return !q_.empty(); });
+                tk = std::move(q_.front());
+                q_.pop_front();
+            }
+            Job& j = *tk.first;
+            int expect = 0;
+            if (!j.state[tk.second].compare_exchange_strong(expect, 1)) continue;   // cancelled: the call is done
+            j.work();
+            {
+                std::lock_guard<std::mutex> lk(j.mu);
+                j.state[tk.second].store(2);
+            }
+            j.cv.notify_all();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::pair<std::shared_ptr<Job>, int>> q_;
+    std::vector<std::thread> th_;
+};
+
 // fn(lo, hi) over [0, n) in chunks of >= grain on the host threads (inline below 2 chunks)
 template <class F>
 void parallel_for(int64_t n, int64_t grain, F&& fn) {
@@ -267,10 +326,26 @@ void parallel_for(int64_t n, int64_t grain, F&& fn) {
     auto work = [&]() {
         for (int64_t lo; (lo = next.fetch_add(chunk)) < n;) fn(lo, std::min(n, lo + chunk));
     };
-    std::vector<std::thread> th;
-    for (int64_t t = 1; t < nt; t++) th.emplace_back(work);
+    HostPool& pool = HostPool::get();
+    const int helpers = (int)std::min<int64_t>(nt - 1, pool.workers());
+    if (helpers <= 0) { work(); return; }
+    auto job = std::make_shared<HostPool::Job>();
+    job->work = work;
+    job->n = helpers;
+    job->state.reset(new std::atomic<int>[(size_t)helpers]);
+    for (int k = 0; k < helpers; k++) job->state[k].store(0);
+    pool.submit(job);
     work();
-    for (auto& t : th) t.join();
+    for (int k = 0; k < helpers; k++) {
+        int expect = 0;
+        job->state[k].compare_exchange_strong(expect, 3);
+    }
+    std::unique_lock<std::mutex> lk(job->mu);
+    job->cv.wait(lk, [&] {
+        for (int k = 0; k < helpers; k++)
+            if (job->state[k].load() == 1) return false;
+        return true;
+    });
 }
 
 struct Device;   // kernels.hip

@@ -169,6 +169,12 @@ struct Device {
     void* h_rac = nullptr;
     LikTables* d_tables = nullptr;
     PoolTables* d_pool = nullptr;    // ploidy >= 3: the pool algorithm's tables (device_set_pool)
+    // host -> device copies of pageable host memory go through these pinned buffers (h2d): the DMA engines only
+    // ever read pinned memory
+    uint8_t* stage[2] = {nullptr, nullptr};
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    bool stage_busy[2] = {false, false};
+    int stage_k = 0;
     PoolTables h_pool{};             // their last upload
     bool pool_valid = false;
     int32_t ko_shift = 14, ko_bcap = 64;   // 2^ko_shift positions per bucket (grown on overflow)
@@ -2010,6 +2016,42 @@ static hipError_t launch_check() {
     if (e != hipSuccess || !sync) return e;
     return hipDeviceSynchronize();
 }
+
+// host -> device copy of pageable host memory: chunks memcpy'd (all host threads) into the device's two pinned
+// staging buffers, each DMA'd on `st` while the next is filled.  Returns once the source has been read (it may be
+// freed); the last chunk's DMA may still run, and a staging buffer is reused only after its event.  (DMA straight
+// from pageable memory was seen to fault the device intermittently: the pageable copies of the uploads all go here.)
+constexpr size_t kStageBytes = (size_t)64 << 20;
+static int h2d(Device* d, void* dst, const void* src, size_t bytes, hipStream_t st, std::string& err) {
+    if (!bytes) return 0;
+    for (int k = 0; k < 2; k++)
+        if (!d->stage[k]) {
+            HIP_TRY(hipHostMalloc((void**)&d->stage[k], kStageBytes, hipHostMallocDefault));
+            HIP_TRY(hipEventCreateWithFlags(&d->stage_ev[k], hipEventDisableTiming));
+            d->stage_busy[k] = false;
+        }
+    const uint8_t* in = static_cast<const uint8_t*>(src);
+    uint8_t* out = static_cast<uint8_t*>(dst);
+    for (size_t off = 0; off < bytes;) {
+        const size_t n = std::min(kStageBytes, bytes - off);
+        const int k = d->stage_k;
+        if (d->stage_busy[k]) HIP_TRY(hipEventSynchronize(d->stage_ev[k]));
+        uint8_t* buf = d->stage[k];
+        if (n >= ((size_t)4 << 20))
+            parallel_for((int64_t)((n + (1 << 20) - 1) >> 20), 1, [&](int64_t a, int64_t b) {
+                const size_t lo = (size_t)a << 20, hi = std::min(n, (size_t)b << 20);
+                std::memcpy(buf + lo, in + off + lo, hi - lo);
+            });
+        else std::memcpy(buf, in + off, n);
+        HIP_TRY(hipMemcpyAsync(out + off, buf, n, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipEventRecord(d->stage_ev[k], st));
+        d->stage_busy[k] = true;
+        d->stage_k ^= 1;
+        off += n;
+    }
+    return 0;
+}
+#define H2D(dst, src, bytes, st) do { if (h2d(d, (dst), (src), (bytes), (st), err) != 0) return -1; } while (0)
 void* pinned_alloc(size_t bytes) {
     void* p = std::aligned_alloc(4096, (bytes + 4095) / 4096 * 4096);
     if (p && hipHostRegister(p, bytes, hipHostRegisterDefault) != hipSuccess) {
@@ -2184,6 +2226,10 @@ void device_destroy(Device* d) {
     (void)hipFree(d->d_tables);
     (void)hipFree(d->d_pool);
     (void)hipHostFree(d->h_counters);
+    for (int k = 0; k < 2; k++) {
+        if (d->stage[k]) (void)hipHostFree(d->stage[k]);
+        if (d->stage_ev[k]) (void)hipEventDestroy(d->stage_ev[k]);
+    }
     for (auto& e : d->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(d->stream);
     (void)hipStreamDestroy(d->copy_stream);
@@ -2205,7 +2251,7 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
     else HIP_TRY(hipDeviceSynchronize());          // the previous run is done reading them
     if (ensure_dev(&d->d_ref, &d->cap_ref, (size_t)s.g_len + 64, keep, err)) return -1;
     HIP_TRY(hipMemsetAsync(d->d_ref + s.g_len, 0, 64, d->stream));
-    HIP_TRY(hipMemcpyAsync(d->d_ref, s.h_ref.data(), (size_t)s.g_len, hipMemcpyHostToDevice, d->stream));
+    H2D(d->d_ref, s.h_ref.data(), (size_t)s.g_len, d->stream);
     d->rg = s.rg;
     if (s.rg) {
         // the read-group layout: units, entry headers, group table, block tables (KL, KG)
@@ -2217,27 +2263,26 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
             ensure_dev(&d->d_blkB, &d->cap_blkB, nblk * sizeof(int32_t), keep, err))
             return -1;
         if (s.n_units) {
-            // a pinned arena is copied asynchronously; a pageable one (a layout beyond 4 GB) synchronously, so the
-            // host block is never read by a copy still in flight
-            HIP_TRY(hipMemcpyAsync(d->d_units, s.h_units, (size_t)s.n_units * sizeof(uint64_t), hipMemcpyHostToDevice, d->stream));
-            if (!s.units_pinned) HIP_TRY(hipStreamSynchronize(d->stream));
+            // a pinned arena is copied directly; a pageable one (a layout beyond 4 GB) through the staging buffers
+            if (s.units_pinned) HIP_TRY(hipMemcpyAsync(d->d_units, s.h_units, (size_t)s.n_units * sizeof(uint64_t), hipMemcpyHostToDevice, d->stream));
+            else H2D(d->d_units, s.h_units, (size_t)s.n_units * sizeof(uint64_t), d->stream);
         }
         HIP_TRY(hipMemsetAsync(d->d_units + s.n_units, 0, 8 * sizeof(uint64_t), d->stream));
-        if (s.n_entries) HIP_TRY(hipMemcpyAsync(d->d_rh, s.h_rh.data(), (size_t)s.n_entries * sizeof(int2), hipMemcpyHostToDevice, d->stream));
+        if (s.n_entries) H2D(d->d_rh, s.h_rh.data(), (size_t)s.n_entries * sizeof(int2), d->stream);
         else {
-            const int32_t empty[2] = {1, 0};
-            for (int k = 0; k < 64; k++) HIP_TRY(hipMemcpyAsync(d->d_rh + k, empty, sizeof empty, hipMemcpyHostToDevice, d->stream));
-            HIP_TRY(hipStreamSynchronize(d->stream));
+            int32_t empty[128];
+            for (int k = 0; k < 64; k++) { empty[2 * k] = 1; empty[2 * k + 1] = 0; }
+            H2D(d->d_rh, empty, sizeof empty, d->stream);
         }
-        if (s.n_groups) HIP_TRY(hipMemcpyAsync(d->d_grp, s.h_grp.data(), (size_t)s.n_groups * sizeof(RGroup), hipMemcpyHostToDevice, d->stream));
-        HIP_TRY(hipMemcpyAsync(d->d_blkA, s.h_blkA.data(), nblk * sizeof(int32_t), hipMemcpyHostToDevice, d->stream));
-        HIP_TRY(hipMemcpyAsync(d->d_blkB, s.h_blkB.data(), nblk * sizeof(int32_t), hipMemcpyHostToDevice, d->stream));
+        if (s.n_groups) H2D(d->d_grp, s.h_grp.data(), (size_t)s.n_groups * sizeof(RGroup), d->stream);
+        H2D(d->d_blkA, s.h_blkA.data(), nblk * sizeof(int32_t), d->stream);
+        H2D(d->d_blkB, s.h_blkB.data(), nblk * sizeof(int32_t), d->stream);
         d->n_entries = std::max<int64_t>(s.n_entries, 64);
     } else if (s.single) {
         if (ensure_dev(&d->d_pile, &d->cap_pile, (size_t)s.pile_bytes + 64, keep, err) ||      // + 64: KP loads whole dwords of a column
             ensure_dev(&d->d_tinfo, &d->cap_tinfo, (size_t)std::max<int64_t>(s.n_tiles, 1) * sizeof(TileInfo), keep, err))
             return -1;
-        if (s.n_tiles && !s.h_tinfo.empty()) HIP_TRY(hipMemcpyAsync(d->d_tinfo, s.h_tinfo.data(), (size_t)s.n_tiles * sizeof(TileInfo), hipMemcpyHostToDevice, d->stream));
+        if (s.n_tiles && !s.h_tinfo.empty()) H2D(d->d_tinfo, s.h_tinfo.data(), (size_t)s.n_tiles * sizeof(TileInfo), d->stream);
         // single sample: planes (KT), the position-major pile and its strand bits (KP)
         const size_t ncw = (size_t)(s.pile_bytes / 32);
         if (ensure_dev(&d->d_planes, &d->cap_planes, (size_t)std::max<int64_t>(s.pile_bytes / 8, 16), keep, err) ||
@@ -2251,8 +2296,8 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
             HIP_TRY(hipMemcpyAsync(d->d_planes, s.h_planes, (size_t)(s.pile_bytes / 8), hipMemcpyHostToDevice, d->stream));
             HIP_TRY(hipMemcpyAsync(d->d_cneg, s.h_cneg, ncw * sizeof(uint32_t), hipMemcpyHostToDevice, d->stream));
         }
-        if (!s.h_olist.empty()) HIP_TRY(hipMemcpyAsync(d->d_olist, s.h_olist.data(), s.h_olist.size() * sizeof(uint16_t), hipMemcpyHostToDevice, d->stream));
-        if (!s.h_loff.empty()) HIP_TRY(hipMemcpyAsync(d->d_loff, s.h_loff.data(), s.h_loff.size() * sizeof(int32_t), hipMemcpyHostToDevice, d->stream));
+        if (!s.h_olist.empty()) H2D(d->d_olist, s.h_olist.data(), s.h_olist.size() * sizeof(uint16_t), d->stream);
+        if (!s.h_loff.empty()) H2D(d->d_loff, s.h_loff.data(), s.h_loff.size() * sizeof(int32_t), d->stream);
         d->planes_W = s.tile / 32;
     } else {
         if (ensure_dev(&d->d_pile, &d->cap_pile, (size_t)s.pile_bytes + 64, false, err)) return -1;
@@ -2270,17 +2315,17 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
             unsigned long long hc[8] = {0, 0, (unsigned long long)nf, 0, 0, 0, 0, 0};
             HIP_TRY(hipMalloc(&d->d_mforced, (size_t)std::max<int64_t>(nf, 1) * sizeof(QueueSite)));
             HIP_TRY(hipMalloc(&d->d_mforced_ctr, 8 * sizeof(unsigned long long)));
-            if (nf) HIP_TRY(hipMemcpy(d->d_mforced, s.h_forced.data(), (size_t)nf * sizeof(QueueSite), hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(d->d_mforced_ctr, hc, sizeof hc, hipMemcpyHostToDevice));
+            if (nf) H2D(d->d_mforced, s.h_forced.data(), (size_t)nf * sizeof(QueueSite), d->stream);
+            H2D(d->d_mforced_ctr, hc, sizeof hc, d->stream);
             d->n_mforced = nf;
         }
-        if (s.pile_bytes) HIP_TRY(hipMemcpyAsync(d->d_pile, s.h_pile.data(), (size_t)s.pile_bytes, hipMemcpyHostToDevice, d->stream));
-        if (!s.h_mc_pos.empty()) HIP_TRY(hipMemcpyAsync(d->d_mc_pos, s.h_mc_pos.data(), s.h_mc_pos.size() * sizeof(int32_t), hipMemcpyHostToDevice, d->stream));
-        if (!s.h_mc_n.empty()) HIP_TRY(hipMemcpyAsync(d->d_mc_n, s.h_mc_n.data(), s.h_mc_n.size(), hipMemcpyHostToDevice, d->stream));
-        if (!s.h_mc_gbase.empty()) HIP_TRY(hipMemcpyAsync(d->d_mc_gbase, s.h_mc_gbase.data(), s.h_mc_gbase.size() * sizeof(int64_t), hipMemcpyHostToDevice, d->stream));
-        HIP_TRY(hipMemcpyAsync(d->d_ppile, s.h_ppile.get(), (size_t)s.ppile_bytes + 64, hipMemcpyHostToDevice, d->stream));
-        if (!s.h_prow.empty()) HIP_TRY(hipMemcpyAsync(d->d_prow, s.h_prow.data(), s.h_prow.size() * sizeof(uint16_t), hipMemcpyHostToDevice, d->stream));
-        if (!s.h_pboff.empty()) HIP_TRY(hipMemcpyAsync(d->d_pboff, s.h_pboff.data(), s.h_pboff.size() * sizeof(int64_t), hipMemcpyHostToDevice, d->stream));
+        if (s.pile_bytes) H2D(d->d_pile, s.h_pile.data(), (size_t)s.pile_bytes, d->stream);
+        if (!s.h_mc_pos.empty()) H2D(d->d_mc_pos, s.h_mc_pos.data(), s.h_mc_pos.size() * sizeof(int32_t), d->stream);
+        if (!s.h_mc_n.empty()) H2D(d->d_mc_n, s.h_mc_n.data(), s.h_mc_n.size(), d->stream);
+        if (!s.h_mc_gbase.empty()) H2D(d->d_mc_gbase, s.h_mc_gbase.data(), s.h_mc_gbase.size() * sizeof(int64_t), d->stream);
+        H2D(d->d_ppile, s.h_ppile.get(), (size_t)s.ppile_bytes + 64, d->stream);
+        if (!s.h_prow.empty()) H2D(d->d_prow, s.h_prow.data(), s.h_prow.size() * sizeof(uint16_t), d->stream);
+        if (!s.h_pboff.empty()) H2D(d->d_pboff, s.h_pboff.data(), s.h_pboff.size() * sizeof(int64_t), d->stream);
         HIP_TRY(hipStreamSynchronize(d->stream));       // the host layout is freed after the upload
         d->mc_entries = s.mc_entries;
         d->n_samples = s.n_samples;
@@ -2298,7 +2343,8 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
         for (const Window& w : s.windows) wins.push_back(int4{(int)(w.gbase + w.pad), w.w0, w.seq_id, w.wlen});
         if (wins.empty()) wins.push_back(int4{0, 0, -1, 0});
         if (ensure_dev(&d->d_wins, &d->cap_wins, wins.size() * sizeof(int4), false, err)) return -1;
-        HIP_TRY(hipMemcpy(d->d_wins, wins.data(), wins.size() * sizeof(int4), hipMemcpyHostToDevice));
+        H2D(d->d_wins, wins.data(), wins.size() * sizeof(int4), d->stream);
+        HIP_TRY(hipStreamSynchronize(d->stream));
         d->n_wins = (int32_t)wins.size();
     }
     HIP_TRY(hipStreamSynchronize(d->stream));
@@ -2394,7 +2440,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     if (!sl.tables_valid || std::memcmp(&sl.h_tables, &t, sizeof(LikTables)) != 0) {
         HIP_TRY(hipStreamSynchronize(sl.stream));     // the previous upload may still read h_tables
         sl.h_tables = t;
-        HIP_TRY(hipMemcpyAsync(sl.d_tables, &sl.h_tables, sizeof(LikTables), hipMemcpyHostToDevice, sl.stream));
+        H2D(sl.d_tables, &sl.h_tables, sizeof(LikTables), sl.stream);
         sl.tables_valid = true;
     }
     // KT is timed by events bound to its dispatch (hipExtLaunchKernelGGL): the kernel's own start and end
@@ -2404,10 +2450,10 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     bool kl_run = false;                                         // KL's sharded queue (else one segment, count at [2])
     if (s.known) {
         // -knownVariants: no scan, the input variants' sites (covered, in window order) are KP's queue
-        if (nforced > 0) HIP_TRY(hipMemcpyAsync(sl.d_hard, s.h_forced.data(), (size_t)nforced * sizeof(SiteQ), hipMemcpyHostToDevice, sl.stream));
+        if (nforced > 0) H2D(sl.d_hard, s.h_forced.data(), (size_t)nforced * sizeof(SiteQ), sl.stream);
         if (!s.h_cols.empty())                                   // entries with their columns (realigner regions)
-            HIP_TRY(hipMemcpyAsync(sl.d_cols, s.h_cols.data(), s.h_cols.size() * sizeof(uint16_t), hipMemcpyHostToDevice, sl.stream));
-        HIP_TRY(hipMemcpyAsync(ctr, s.h_forced_ctr, 8 * sizeof(unsigned long long), hipMemcpyHostToDevice, sl.stream));
+            H2D(sl.d_cols, s.h_cols.data(), s.h_cols.size() * sizeof(uint16_t), sl.stream);
+        H2D(ctr, s.h_forced_ctr, 8 * sizeof(unsigned long long), sl.stream);
         hipLaunchKernelGGL(k_zero_i32, dim3((unsigned)std::min<int64_t>((nb + 255) / 256, 4096)), dim3(256), 0, sl.stream, sl.d_bcount, nb);
         HIP_TRY(launch_check());
         d->last_hard = nforced;
@@ -2502,7 +2548,8 @@ int device_set_pool(Device* d, const PoolTables* pt, std::string& err) {
     HIP_TRY(hipSetDevice(d->ordinal));
     HIP_TRY(hipDeviceSynchronize());
     if (!d->d_pool) HIP_TRY(hipMalloc(&d->d_pool, sizeof(PoolTables)));
-    HIP_TRY(hipMemcpy(d->d_pool, pt, sizeof(PoolTables), hipMemcpyHostToDevice));
+    H2D(d->d_pool, pt, sizeof(PoolTables), d->stream);
+    HIP_TRY(hipStreamSynchronize(d->stream));
     d->h_pool = *pt;
     d->pool_valid = true;
     return 0;
@@ -2792,7 +2839,7 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     }
     if (!d->tables_valid || std::memcmp(&d->h_tables, &t, sizeof(LikTables)) != 0) {
         d->h_tables = t;
-        HIP_TRY(hipMemcpyAsync(d->d_tables, &d->h_tables, sizeof(LikTables), hipMemcpyHostToDevice, d->stream));
+        H2D(d->d_tables, &d->h_tables, sizeof(LikTables), d->stream);
         d->tables_valid = true;
     }
     unsigned long long* ctr = d->d_counters;
@@ -3072,7 +3119,7 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
     if (!d->tables_valid || std::memcmp(&d->h_tables, &t, sizeof(LikTables)) != 0) {
         HIP_TRY(hipStreamSynchronize(d->stream));     // an earlier upload may still read h_tables
         d->h_tables = t;
-        HIP_TRY(hipMemcpyAsync(d->d_tables, &d->h_tables, sizeof(LikTables), hipMemcpyHostToDevice, d->stream));
+        H2D(d->d_tables, &d->h_tables, sizeof(LikTables), d->stream);
         d->tables_valid = true;
     }
     unsigned long long* ctr = d->slot[d->mnext].d_ctr;
