@@ -2037,10 +2037,8 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
             });
             nbases += nb.load();
         }
-        const int S = 0;
-        const int64_t nslots = 0;
         s.n_reads = nreads;
-        s.n_slots = nslots;
+        s.n_slots = 0;
         s.n_read_bases = nbases;
         s.n_samples = (int32_t)c->sample_ids.size();
         if (!c->known.empty()) {
@@ -2089,7 +2087,7 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
         if (lr == -2) return set_error(c, NGSEP_E_DEVICE, "host memory for the population pile could not be allocated");
         if (lr != 0) return set_error(c, NGSEP_E_UNSUPPORTED, "a sample's pileup is deeper than 65535 alignments");
         c->stats.slot_bytes = s.ppile_bytes;
-        c->stats.slot_size = S;
+        c->stats.slot_size = 0;                  // (no fixed-size slots: the site-major pile is sized per tile)
     }
     c->stats.read_bases = nbases;
     c->stats.pile_bytes = s.rg ? s.n_units * 8 : s.pile_bytes;
