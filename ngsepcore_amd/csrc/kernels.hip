@@ -1341,6 +1341,7 @@ void k_scan_multi(const int32_t* __restrict__ mc_pos, const uint8_t* __restrict_
     __shared__ unsigned long long w[2][32];
     __shared__ unsigned long long s_ne[4];
     __shared__ uint32_t s_col[4][64 * kKtmWords];
+    __shared__ unsigned long long s_acc[4][64 * 4];   // per lane: its column's {ref, alt 1, alt 2, alt 3} sums
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     if (threadIdx.x < 64) w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
@@ -1403,7 +1404,10 @@ void k_scan_multi(const int32_t* __restrict__ mc_pos, const uint8_t* __restrict_
         bool keep = has;
         if (gp.ablate & 32768) keep = false;               // diagnostics: metadata and staging only
         if (has && bound_on && n != 255u && !(gp.ablate & 32768)) {
-            unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+            // each byte's weight goes to its allele's sum with one LDS add (a lane's own four slots): no per-byte
+            // selects over four 64-bit registers
+            unsigned long long* acc = &s_acc[wv][lane * 4];
+            acc[0] = 0ull; acc[1] = 0ull; acc[2] = 0ull; acc[3] = 0ull;
             for (int64_t d = start >> 2; d < (end + 3) >> 2; d++) {
                 const uint32_t word = fits ? buf[d - d0] : cw[d];
 #pragma unroll
@@ -1414,13 +1418,11 @@ void k_scan_multi(const int32_t* __restrict__ mc_pos, const uint8_t* __restrict_
                     const uint32_t al = (cd >> 5) & 3u;
                     int q = (int)(cd & 31u);
                     q = q > maxq ? maxq : q;
-                    const unsigned long long wt = w[al == 0 ? 0 : 1][q];
-                    a0 += al == 0 ? wt : 0ull;
-                    a1 += al == 1 ? wt : 0ull;
-                    a2 += al == 2 ? wt : 0ull;
-                    a3 += al == 3 ? wt : 0ull;
+                    atomicAdd(&acc[al], w[al == 0 ? 0 : 1][q]);
                 }
             }
+            __builtin_amdgcn_wave_barrier();
+            const unsigned long long a0 = acc[0], a1 = acc[1], a2 = acc[2], a3 = acc[3];
             const long long R1 = (long long)(a0 & 0xFFFFFFFFull), R2 = (long long)(a0 >> 32);
             const long long x1 = (long long)(a1 & 0xFFFFFFFFull), y1 = (long long)(a2 & 0xFFFFFFFFull);
             const long long z1 = (long long)(a3 & 0xFFFFFFFFull);
