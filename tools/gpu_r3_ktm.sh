@@ -1,5 +1,6 @@
 #!/bin/bash
 # round 3: KTM byte-parallel bound -- multisample parity, then the configs[4] step and kernel times.
+# (historical: the NGSEP_KPM_WPE / NGSEP_KPM_GRID knobs and the byte-parallel KTM were removed once measured)
 # Usage: bash tools/gpu_r3_ktm.sh TAG
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"

@@ -1,5 +1,6 @@
 #!/bin/bash
 # round 3: KTM variants (NGSEP_ABLATE 65536: a lane per column; 131072: an atomic per column) and KPM grid.
+# (historical: the NGSEP_ABLATE 65536 / 131072 KTM variants and the NGSEP_KPM_* knobs were removed once measured)
 # Usage: bash tools/gpu_r3_ktm2.sh TAG
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
