@@ -37,7 +37,7 @@ struct Inflater {
     int (*decompress)(void*, const void*, size_t, void*, size_t, size_t*) = nullptr;
     void (*release)(void*) = nullptr;
     Inflater() {
-        if (std::getenv("NGSEP_ZLIB")) return;     // diagnostics: force zlib
+        if (ngsep::env_hook("NGSEP_ZLIB")) return;     // diagnostics: force zlib
         void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
         if (!h) return;
         alloc = (void* (*)())dlsym(h, "libdeflate_alloc_decompressor");
@@ -545,7 +545,7 @@ void parallel_cut(ngsep_bam* b, int64_t max_reads, size_t span, std::vector<size
     size_t seg_end[T] = {};
     const auto tw0 = std::chrono::steady_clock::now();
     // (tests: NGSEP_PCUT_MISS=1 makes every odd segment's own walk start one byte off the chain, so the merge walks it)
-    static const bool miss = std::getenv("NGSEP_PCUT_MISS") != nullptr;
+    static const bool miss = env_hook("NGSEP_PCUT_MISS") != nullptr;
     parallel_for(T, 1, [&](int64_t t0, int64_t t1) {
         for (int64_t t = t0; t < t1; t++) {
             size_t o = bnd[t];
@@ -626,10 +626,12 @@ int fill_batch(ngsep_bam* b, ngsep_bam::BatchStore& B, int64_t max_reads, ngsep_
         }
         // a decoded chunk's worth of records (bounded by max_reads at 512 B a record): cut on all threads; the
         // sequential walk below picks up where it stopped
+        // (only when the span holds the record at b->pos: a single record longer than the span, e.g. an ultra-long
+        // read, would leave the cut empty and b->pos unmoved; the sequential walk takes it)
         const size_t span = std::min(b->end - b->pos, (size_t)max_reads * 512);
-        if (roff.empty() && b->region_ref < 0 && span >= ((size_t)8 << 20)) {
+        if (roff.empty() && b->region_ref < 0 && span >= ((size_t)8 << 20) && 4 + (size_t)bs <= span) {
             parallel_cut(b, max_reads, span, roff);
-            continue;
+            if (!roff.empty()) continue;
         }
         const uint8_t* r = &b->buf[b->pos + 4];
         // the record chain is a dependent walk through freshly inflated memory: pull the lines a few
@@ -872,7 +874,7 @@ extern "C" int ngsep_bam_next_batch(ngsep_bam* b, int64_t max_reads, ngsep_read_
 extern "C" int ngsep_bam_close(ngsep_bam* b) {
     if (!b) return NGSEP_E_INVALID;
     stop_decoder(b);
-    if (std::getenv("NGSEP_HOST_TIMING"))
+    if (env_hook("NGSEP_HOST_TIMING"))
         std::fprintf(stderr, "[ngsep host] bam: inflate %.3f s (decoder thread), consumer wait %.3f s, need %.3f s, cut %.3f s (incl. wait; %lld parallel: walks %.3f s, merge %.3f s, %lld segments walked sequentially), parse %.3f s, emit %.3f s\n",
                      b->t_inflate, b->t_wait, b->t_need, b->t_cut, (long long)b->n_pcut, b->t_pcut_walk, b->t_pcut_merge,
                      (long long)b->n_pcut_serial, b->t_parse, b->t_emit);
@@ -920,7 +922,7 @@ int call_bam(ngsep_ctx* c, const char* bam_path, const char* out_vcf) {
     }
     rc = ngsep_write_vcf_header(c, out_vcf);
     if (rc != NGSEP_OK) { ngsep_bam_close(b); return rc; }
-    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     const auto t0 = std::chrono::steady_clock::now();
     rc = for_each_batch(c, b, [&](const ngsep_read_batch& batch) {
         int r = process_alignments_packed(c, &batch);
@@ -1038,7 +1040,7 @@ struct Cursor {
 // (lower_bound), so each key range is an independent k-way merge; the records are then gathered into one merged
 // SoA by all host threads and handed to the sweep in batches of 2^18.
 int merge_whole_files(ngsep_ctx* c, std::vector<Cursor>& cur, int n_files) {
-    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     auto t_0 = std::chrono::steady_clock::now();
     auto lap = [&](const char* what) {
         if (!host_timing) return;
@@ -1214,7 +1216,7 @@ extern "C" int ngsep_call_population_bams(ngsep_ctx* c, const char* const* bam_p
     if (!c || !bam_paths || n_files <= 0 || !out_vcf_path) return NGSEP_E_INVALID;
     if (!c->params.multisample) return set_error(c, NGSEP_E_INVALID, "ngsep_call_population_bams needs params.multisample = 1");
     start_device_init(c);
-    static const bool pop_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    static const bool pop_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     auto tp = std::chrono::steady_clock::now();
     auto plap = [&](const char* what) {
         if (!pop_timing) return;
@@ -1326,7 +1328,7 @@ extern "C" int ngsep_call_population_bams(ngsep_ctx* c, const char* const* bam_p
             if (cur[(size_t)f].has_pending) whole = false;
         }
     }
-    if (std::getenv("NGSEP_HOST_TIMING"))
+    if (env_hook("NGSEP_HOST_TIMING"))
         std::fprintf(stderr, "[ngsep host] population: %d files opened and read in %.3f s\n", n_files,
                      std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0).count());
     // merged batch storage
@@ -1347,7 +1349,7 @@ extern "C" int ngsep_call_population_bams(ngsep_ctx* c, const char* const* bam_p
         m_cig_off.clear(); m_seq_off.clear(); m_hasq.clear(); m_bases.clear(); m_quals.clear();
         return r;
     };
-    if (std::getenv("NGSEP_POP_STREAM")) whole = false;     // diagnostics / tests: the streaming merge
+    if (env_hook("NGSEP_POP_STREAM")) whole = false;     // diagnostics / tests: the streaming merge
     plap("open + whole-file reads");
     if (whole && !c->query_done) {
         rc = merge_whole_files(c, cur, n_files);
@@ -1393,7 +1395,7 @@ extern "C" int ngsep_call_population_bams(ngsep_ctx* c, const char* const* bam_p
             i = m;
         }
     };
-    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     double t_refill = 0, t_flush = 0;
     const auto tm0 = std::chrono::steady_clock::now();
     auto secs = [](std::chrono::steady_clock::time_point a) {

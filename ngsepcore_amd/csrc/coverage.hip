@@ -232,8 +232,19 @@ int cov_upload(CovDevice* d, const std::vector<int64_t>& gfirst, const std::vect
     COV_TRY(hipMalloc(&d->d_spanu, sizeof(uint32_t) * (size_t)(n > 0 ? n : 1)));
     COV_TRY(hipMalloc(&d->d_tstart, sizeof(int64_t) * (size_t)(d->n_tiles + 1)));
     if (n) {
-        COV_TRY(hipMemcpyAsync(d->d_gfirst, gfirst.data(), sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, d->stream));
-        COV_TRY(hipMemcpyAsync(d->d_spanu, spanu.data(), sizeof(uint32_t) * (size_t)n, hipMemcpyHostToDevice, d->stream));
+        // (no copy's host side is pageable memory, kernels.hip "pinned host memory": the arrays go through a
+        // pinned block)
+        const size_t bg = sizeof(int64_t) * (size_t)n, bs = sizeof(uint32_t) * (size_t)n;
+        uint8_t* h = static_cast<uint8_t*>(pinned_alloc(bg + bs));
+        if (!h) { err = "pinned allocation failed"; return -1; }
+        std::memcpy(h, gfirst.data(), bg);
+        std::memcpy(h + bg, spanu.data(), bs);
+        int rc = dma_copy(d->d_gfirst, h, bg, 0, d->stream, false, err, "coverage.hip", __LINE__);
+        if (rc == 0) rc = dma_copy(d->d_spanu, h + bg, bs, 0, d->stream, false, err, "coverage.hip", __LINE__);
+        const hipError_t e = hipStreamSynchronize(d->stream);
+        pinned_free(h);
+        if (rc != 0) return -1;
+        COV_TRY(e);
     }
     const int64_t blocks = (n + 1 + 255) / 256;
     kc_tile_index<<<dim3((unsigned)blocks), dim3(256), 0, d->stream>>>(d->d_gfirst, n, d->n_tiles, d->d_tstart);
@@ -261,7 +272,7 @@ int cov_run(CovDevice* d, int32_t max_cov, uint64_t* hist_out, double* kernel_ms
         // tile width 4096 (NGSEP_COV_TILE=2048 selects the narrow tile, diagnostics); as many workgroups as are
         // co-resident, each walking tiles with a grid stride
         const size_t lds = sizeof(uint32_t) * 4 * (size_t)nb;
-        static const bool narrow_env = std::getenv("NGSEP_COV_TILE") && std::atoi(std::getenv("NGSEP_COV_TILE")) == 2048;
+        static const bool narrow_env = diag_env("NGSEP_COV_TILE") && std::atoi(diag_env("NGSEP_COV_TILE")) == 2048;
         const bool narrow = narrow_env || lds > 32768;
         const int64_t ntl = narrow ? (d->g_len + 2047) >> 11 : d->n_tiles;
         int per_cu = 0;
@@ -276,8 +287,17 @@ int cov_run(CovDevice* d, int32_t max_cov, uint64_t* hist_out, double* kernel_ms
                                   0, d->d_gfirst, d->d_spanu, d->d_tstart, d->g_len, ntl, d->max_span, max_cov, d->d_hist);
         COV_TRY(hipGetLastError());
     }
-    COV_TRY(hipMemcpyAsync(hist_out, d->d_hist, sizeof(unsigned long long) * (size_t)nb, hipMemcpyDeviceToHost, d->stream));
-    COV_TRY(hipStreamSynchronize(d->stream));
+    {
+        const size_t bytes = sizeof(unsigned long long) * (size_t)nb;
+        void* h = pinned_alloc(bytes);
+        if (!h) { err = "pinned allocation failed"; return -1; }
+        const int rc = dma_copy(h, d->d_hist, bytes, 1, d->stream, false, err, "coverage.hip", __LINE__);
+        const hipError_t e = hipStreamSynchronize(d->stream);
+        if (rc == 0 && e == hipSuccess) std::memcpy(hist_out, h, bytes);
+        pinned_free(h);
+        if (rc != 0) return -1;
+        COV_TRY(e);
+    }
     if (d->n_tiles > 0) COV_TRY(hipEventElapsedTime(&ms, d->ev[0], d->ev[1]));
     if (kernel_ms) *kernel_ms = ms;
     return 0;

@@ -75,7 +75,7 @@ void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g) {
     g->max_q = mq > 0 ? mq : 30;
     g->min_quality = (int16_t)c->params.min_quality;
     g->dump_all = c->params.dump_all_positions;
-    const char* ab = std::getenv("NGSEP_ABLATE");
+    const char* ab = diag_env("NGSEP_ABLATE");
     g->ablate = ab ? std::atoi(ab) : 0;
     // Integer hom-ref bound.  Per valid call of quality q the differences
     // L[r][r]-L[r][x] etc. take one of the four values below; floor/ceil make the integer sums
@@ -502,7 +502,7 @@ static void project_pending(ngsep_ctx* c) {
     for (size_t i = 0; i < n; i++) cr.bptr[b0 + i] = base + off[i];
     cr.chunk_end.push_back(b0 + n);
     cr.chunk_maxlast.push_back(maxlast);
-    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     const auto t1 = std::chrono::steady_clock::now();
     const BatchRef br = c->cur_batch;
     const int32_t* ent = v.data();
@@ -744,7 +744,7 @@ int stage_contig_reads(ngsep_ctx* c, ContigReads& cr, bool run_now) {
 // thread, one window at a time, while admission goes on; its records join the context's list in window
 // order.  The window cut changes no call (windows carry a halo of the reads' span).
 static int64_t stream_window_len(const ngsep_ctx* c) {
-    static const int64_t env = std::getenv("NGSEP_STREAM_WINDOW") ? std::atoll(std::getenv("NGSEP_STREAM_WINDOW")) : 0;   // tuning
+    static const int64_t env = diag_env("NGSEP_STREAM_WINDOW") ? std::atoll(diag_env("NGSEP_STREAM_WINDOW")) : 0;   // tuning
     int64_t w = env > 0 ? env : (int64_t)1 << 22;
     if (c->params.window_positions > 0) w = std::min<int64_t>(w, c->params.window_positions);
     return std::max<int64_t>(w, 1024);
@@ -1301,8 +1301,13 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed) {
     }
     c->stats.alignments_in += n_in;
     // the admitted reads' bytes are projected while the batch is alive; the open group is carried
-    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     const auto t1 = std::chrono::steady_clock::now();
+    // -knownSTRs: the input STRs that start at or before the open group's start join the events now, not when a read
+    // at or after them is admitted: keep_raw's frontier and stream_advance's limit both take last_start as the point
+    // before which nothing more can start (a coverage gap after an STR would otherwise leave it out of the window's
+    // regions).  The order among the events is unchanged: admit_core injects STRs up to a read's start before it.
+    if (!c->strs.empty() && c->contig.seq_id >= 0 && c->last_start > 0) inject_strs(c, c->last_start);
     project_pending(c);
     const auto t2 = std::chrono::steady_clock::now();
     if (rc == NGSEP_OK && streaming(c)) rc = stream_advance(c, false);
@@ -1383,7 +1388,7 @@ static int choose_tile(const std::vector<int32_t>& m16, int64_t g_len, std::vect
         const double cost = bytes / 4 + 2048.0 * (double)ntiles;
         if (best_cost < 0 || cost < best_cost) { best_cost = cost; bestT = T; }
     }
-    if (const char* e = std::getenv("NGSEP_TILE_T")) {   // tests and tuning: a fixed tile width
+    if (const char* e = diag_env("NGSEP_TILE_T")) {   // tests and tuning: a fixed tile width
         const int T = std::atoi(e);
         if (T == 128 || T == 256 || T == 512) bestT = T;
     }
@@ -1403,7 +1408,7 @@ static int choose_tile(const std::vector<int32_t>& m16, int64_t g_len, std::vect
 //   * the strand bits (KP, countsStrand): bit off_t + p * rows_t + r = the rank-r read is reverse.
 // Tiles are independent: built on all host threads.
 static int build_single_layout(Staged& s, const HugeVec<SRead>& reads, LayoutArena& arena, bool exact) {
-    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     auto lap = [t = std::chrono::steady_clock::now()](const char* what) mutable {
         if (!host_timing) return;
         const auto n = std::chrono::steady_clock::now();
@@ -1521,7 +1526,7 @@ static int build_single_layout(Staged& s, const HugeVec<SRead>& reads, LayoutAre
 // block tables give the scan its tile's entry range and the column gather the entries that can cover a
 // position.  Groups are independent: built on all host threads.
 static int build_rg_layout(Staged& s, const HugeVec<SRead>& reads, LayoutArena& arena, bool exact) {
-    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     const auto t0 = std::chrono::steady_clock::now();
     const int64_t n = (int64_t)reads.size();
     const int64_t ng = (n + 63) / 64, ne = ng * 64;
@@ -1668,7 +1673,7 @@ void LayoutArena::release() {
 //    order getAlleleCalls visits them: read-group rank, then pending order -- rows = the tile's deepest
 //    column, zero padded (a zero code is no call and counts nothing).
 static int build_multi_layout(Staged& s) {
-    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     auto t_last = std::chrono::steady_clock::now();
     auto lap = [&](const char* what) {
         if (!host_timing) return;
@@ -1684,7 +1689,7 @@ static int build_multi_layout(Staged& s) {
     const int32_t maxspan = s.max_span;
     const int64_t PT = kPopTile;
     // positions per chunk of work: the chunk's per-(sample, position) counters (~8 B each) stay cache-sized
-    static const int64_t c_env = std::getenv("NGSEP_POP_CHUNK") ? std::atoll(std::getenv("NGSEP_POP_CHUNK")) : 0;   // tuning
+    static const int64_t c_env = diag_env("NGSEP_POP_CHUNK") ? std::atoll(diag_env("NGSEP_POP_CHUNK")) : 0;   // tuning
     int64_t C = c_env > 0 ? c_env : ((int64_t)1 << 19) / S1;
     C = std::max<int64_t>(256, std::min<int64_t>(8192, C)) / PT * PT;   // a multiple of PT (g_len is one of 1024)
     const int64_t nchunk = (g_len + C - 1) / C, ntile = g_len / PT;
@@ -1917,7 +1922,7 @@ static int build_multi_layout(Staged& s) {
 }
 
 int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
-    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     const auto h0 = std::chrono::steady_clock::now();
     Staged& s = c->staged;
     s = Staged();
@@ -2069,7 +2074,7 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
             s.known = true;
         }
         const int lr = build_multi_layout(s);
-        if (const char* dump = std::getenv("NGSEP_DUMP_POP_LAYOUT")) {   // diagnostics: a digest of the population layout
+        if (const char* dump = diag_env("NGSEP_DUMP_POP_LAYOUT")) {   // diagnostics: a digest of the population layout
             auto fnv = [](const void* p, size_t n) {
                 uint64_t h = 1469598103934665603ull;
                 for (size_t i = 0; i < n; i++) { h ^= static_cast<const uint8_t*>(p)[i]; h *= 1099511628211ull; }
@@ -2142,7 +2147,7 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
 static int run_regions(ngsep_ctx* c, WindowJob* j, int64_t goff);
 
 static void run_window_job(ngsep_ctx* c, WindowJob* j) {
-    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     if (j->rc != NGSEP_OK) { j->done = true; return; }   // (stream_launch found a fault)
     const auto h0 = std::chrono::steady_clock::now();
     Staged& s = c->staged;
@@ -3245,7 +3250,7 @@ extern "C" int ngsep_collect_staged(ngsep_ctx* c, double* elapsed_ms) {
         c->stats.genotype_ms = geno_ms;
         c->stats.kernel_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         if (elapsed_ms) *elapsed_ms = c->stats.kernel_ms;
-        static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+        static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
         if (host_timing) {
             static double acc_w = 0, acc_f = 0;
             static int cnt = 0;
@@ -3264,7 +3269,7 @@ extern "C" int ngsep_collect_staged(ngsep_ctx* c, double* elapsed_ms) {
     int64_t n = 0, ncand = 0;
     double scan_ms = 0, geno_ms = 0, total_ms = 0;
     std::string err;
-    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     const auto h0 = std::chrono::steady_clock::now();
     if (device_collect(c->dev, &c->sites, &n, &scan_ms, &geno_ms, &total_ms, &ncand, err) != 0)
         return set_error(c, NGSEP_E_DEVICE, err);

@@ -248,6 +248,18 @@ struct CarryStore {        // owned copies of the open same-start group's reads
     std::string chars, quals;
 };
 
+// Environment.  A release build reads only: the host thread count (NGSEP_THREADS, OMP_NUM_THREADS); timing switches
+// that add stderr lines or kernel events (NGSEP_HOST_TIMING, NGSEP_TIME_POSTERIOR); and test hooks that force an
+// equivalent code path whose output the tests compare with the default one (NGSEP_ZLIB, NGSEP_PCUT_MISS,
+// NGSEP_POP_STREAM, NGSEP_POP_ALL_BIG).  Tuning overrides and ablations (which may change launches or results) exist
+// only in diagnostic builds (make DIAG=1 defines NGSEP_DIAG): elsewhere diag_env is always null.
+inline const char* env_hook(const char* name) { return std::getenv(name); }
+#ifdef NGSEP_DIAG
+inline const char* diag_env(const char* name) { return std::getenv(name); }
+#else
+inline const char* diag_env(const char*) { return nullptr; }
+#endif
+
 // host worker threads: NGSEP_THREADS, else OMP_NUM_THREADS (the GPU box's CPU share), else the cores
 inline unsigned host_threads() {
     static const unsigned n = [] {
@@ -351,9 +363,19 @@ void parallel_for(int64_t n, int64_t grain, F&& fn) {
 struct Device;   // kernels.hip
 struct CovDevice;   // coverage.hip
 
-// pinned host memory (kernels.hip): the device copies results straight into it
+// Pinned host memory (kernels.hip).  Every host address a device copy reads or writes lies in a block recorded in
+// one registry: pinned_alloc's blocks (a page-aligned block registered with hipHostRegister, or hipHostMalloc when
+// the registration is refused) and the runtime-allocated buffers of kernels.hip / coverage.hip.  The copies check
+// their host endpoint against it (dma_copy); pageable sources go through the staging buffers (DESIGN.md section 4,
+// "Uploads": the runtime's pin-in-place path for pageable copies is what faulted in round 3).  With a device present
+// pinned_alloc returns pinned memory or nullptr; without one (host-only code paths) plain memory.
 void* pinned_alloc(size_t bytes);
 void pinned_free(void* p);
+bool pinned_covers(const void* p, size_t bytes);      // [p, p + bytes) inside one registered block
+// a device copy whose host endpoint must be registered (kind 0: host -> device, 1: device -> host); `stream` is a
+// hipStream_t, nullptr with sync = true is the synchronous hipMemcpy.  Returns 0, or -1 with err set (an
+// unregistered host endpoint is an internal error, never copied).
+int dma_copy(void* dst, const void* src, size_t bytes, int kind, void* stream, bool sync, std::string& err, const char* file, int line);
 
 // Record lists backed by pinned host memory, so a D2H copy lands in place without a staging copy:
 // the called sites (SingleSampleVariantPileupListener.calledVariants) and the population calls.
@@ -379,6 +401,7 @@ struct PinnedStore {
         size_t nc = cap ? cap : 4096;
         while (nc < want) nc *= 2;
         auto* nb = static_cast<T*>(pinned_alloc(nc * sizeof(T)));
+        if (!nb) throw std::bad_alloc();
         if (n) std::memcpy(nb, buf, n * sizeof(T));
         if (buf) pinned_free(buf);
         buf = nb;

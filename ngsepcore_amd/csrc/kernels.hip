@@ -26,6 +26,8 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -34,6 +36,14 @@
 namespace ngsep {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// ablation bits (GenotypeParams.ablate, NGSEP_ABLATE) exist only in diagnostic builds (make DIAG=1): a release
+// build compiles every ablated branch out
+#ifdef NGSEP_DIAG
+#define ABLATE(mask, bit) ((((mask) & (bit)) != 0))
+#else
+#define ABLATE(mask, bit) false
+#endif
 
 #define HIP_TRY(expr)                                                                  \
     do {                                                                               \
@@ -115,8 +125,8 @@ struct Device {
     int64_t n_submitted = 0, n_collected = 0;
     // an event between KP and KO costs a few microseconds of idle GPU per pass: recorded only when
     // the posterior kernel's duration is asked for (NGSEP_TIME_POSTERIOR, diagnostics)
-    bool time_posterior = std::getenv("NGSEP_TIME_POSTERIOR") != nullptr;
-    bool time_scan = std::getenv("NGSEP_NO_SCAN_TIMING") == nullptr;   // diagnostics: without KT's events
+    bool time_posterior = env_hook("NGSEP_TIME_POSTERIOR") != nullptr;
+    bool time_scan = diag_env("NGSEP_NO_SCAN_TIMING") == nullptr;   // diagnostics: without KT's events
     hipEvent_t ev[4] = {};
     uint8_t* d_pile = nullptr;       // single sample: position-major byte pile; multisample: per-sample blocks
     uint32_t* d_planes = nullptr;    // single sample: valid-call plane of the pile (KT)
@@ -409,7 +419,7 @@ __global__ __launch_bounds__(kPostThreads) void k_posterior(const SiteQ* __restr
             }
         }
         const bool known = (rc & 0x400u) != 0;     // -knownVariants site: ref (bits 5-6) and alt (bits 8-9) given
-        if ((total == 0 && !known) || (gp.ablate & 8)) continue;        // VariantDiscoverySNVQAlgorithm.java:101-103
+        if ((total == 0 && !known) || ABLATE(gp.ablate, 8)) continue;        // VariantDiscoverySNVQAlgorithm.java:101-103
         const bool callable = (rc & 0x80u) != 0;
         int8_t genotype = -1, alt = -1, third = -1, nal = 0;
         int16_t gq = 0, qual = 0;
@@ -903,7 +913,7 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
                                           int32_t* s_diff, uint32_t* s_cnt, bool do_diff, int32_t ablate, uint32_t& sink) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t g_lo = e_lo >> 6, g_hi = (e_hi + 63) >> 6;
-    const bool no_counts = (ablate & 128) != 0, no_units = (ablate & 256) != 0;   // diagnostics
+    const bool no_counts = ABLATE(ablate, 128), no_units = ABLATE(ablate, 256);   // diagnostics
     int64_t g = g_lo + wv;
     int2 h = g < g_hi ? rh[g * 64 + lane] : make_int2(0, 0);
     for (; g < g_hi; g += kKlThreads / 64) {
@@ -933,7 +943,7 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
                 const uint32_t ylo = (uint32_t)u[i], yhi = (uint32_t)(u[i] >> 32);
                 const uint32_t elo = kl_exc(ylo), ehi = kl_exc(yhi);
                 if (no_counts) { sink += elo + ehi + kl_nonref(ylo) + kl_nonref(yhi); continue; }
-                if (!(elo | ehi) && !(ablate & 2048)) continue;   // (2048, diagnostics: every lane adds)
+                if (!(elo | ehi) && !ABLATE(ablate, 2048)) continue;   // (2048, diagnostics: every lane adds)
                 const uint32_t nlo = kl_nonref(ylo), nhi = kl_nonref(yhi);
                 const int32_t ob = ob0 + 8 * (j + i);     // counter index of the unit's byte 0
                 if (!DEEP) {
@@ -942,7 +952,7 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
                     const uint32_t w0 = __builtin_amdgcn_perm(ml, fl, 0x05010400u), w1 = __builtin_amdgcn_perm(ml, fl, 0x07030602u);
                     const uint32_t w2 = __builtin_amdgcn_perm(mh, fh, 0x05010400u), w3 = __builtin_amdgcn_perm(mh, fh, 0x07030602u);
                     uint32_t* c = s_cnt + ((ob + 1) >> 1) - 1;   // sh = 0: the first add is of 0
-                    if (ablate & 512) {                   // diagnostics: stores instead of adds
+                    if (ABLATE(ablate, 512)) {                   // diagnostics: stores instead of adds
                         c[0] = __builtin_amdgcn_alignbyte(w0, 0u, sh);
                         c[1] = __builtin_amdgcn_alignbyte(w1, w0, sh);
                         c[2] = __builtin_amdgcn_alignbyte(w2, w1, sh);
@@ -950,9 +960,9 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
                         c[4] = __builtin_amdgcn_alignbyte(0u, w3, sh);
                         continue;
                     }
-                    if (ablate & 1024) { atomicAdd(c, w0 + w1 + w2 + w3); continue; }   // diagnostics: one add
-                    if ((ablate & 8192) && i != 0) continue;   // diagnostics: a batch's first unit only
-                    if (ablate & 16384) { sink += atomicAdd(c, w0 + w1 + w2 + w3); continue; }   // diagnostics: returning add
+                    if (ABLATE(ablate, 1024)) { atomicAdd(c, w0 + w1 + w2 + w3); continue; }   // diagnostics: one add
+                    if (ABLATE(ablate, 8192) && i != 0) continue;   // diagnostics: a batch's first unit only
+                    if (ABLATE(ablate, 16384)) { sink += atomicAdd(c, w0 + w1 + w2 + w3); continue; }   // diagnostics: returning add
                     atomicAdd(c, __builtin_amdgcn_alignbyte(w0, 0u, sh));
                     atomicAdd(c + 1, __builtin_amdgcn_alignbyte(w1, w0, sh));
                     atomicAdd(c + 2, __builtin_amdgcn_alignbyte(w2, w1, sh));
@@ -1037,7 +1047,7 @@ __global__ __launch_bounds__(kKlThreads) void k_read_scan(
     }
     if (sink == 0xFFFFFFFFu) s_cnt[0] = sink;            // keeps the diagnostics' work alive
     // ---- candidates and the count bound
-    const bool bound = gp.use_bound != 0 && !(gp.ablate & 1);
+    const bool bound = gp.use_bound != 0 && !ABLATE(gp.ablate, 1);
     uint32_t rwv[PT / 4];                                // the thread's positions' reference codes
 #pragma unroll
     for (int k = 0; k < PT / 4; k += 2) {
@@ -1078,7 +1088,7 @@ __global__ __launch_bounds__(kKlThreads) void k_read_scan(
             ncand += cand ? 1u : 0u;
             need = cand && !(bound && na <= 255 && cov - exc >= (int32_t)s_cb[na]);
         }
-        if (gp.ablate & 1) need = false;
+        if (ABLATE(gp.ablate, 1)) need = false;
         if (need) {
             need_bits |= 1u << j;
             mine += (1ull << 40) + (uint64_t)((cov + 3) >> 2);
@@ -1402,8 +1412,8 @@ void k_scan_multi(const int32_t* __restrict__ mc_pos, const uint8_t* __restrict_
         __builtin_amdgcn_wave_barrier();
         const int64_t start = c_g0 + (int64_t)(incl - nb), end = start + nb;
         bool keep = has;
-        if (gp.ablate & 32768) keep = false;               // diagnostics: metadata and staging only
-        if (has && bound_on && n != 255u && !(gp.ablate & 32768)) {
+        if (ABLATE(gp.ablate, 32768)) keep = false;               // diagnostics: metadata and staging only
+        if (has && bound_on && n != 255u && !ABLATE(gp.ablate, 32768)) {
             // each byte's weight goes to its allele's sum with one LDS add (a lane's own four slots): no per-byte
             // selects over four 64-bit registers
             unsigned long long* acc = &s_acc[wv][lane * 4];
@@ -1765,7 +1775,7 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
         // sample genotyped (genotypeVariant :674-693) and the record written whatever its QS
         const bool known = (rc & 0x400u) != 0;
         if (s_tot == 0 && !known) continue;                       // createSNVVariantPool: totalCount 0
-        if (gp.ablate & 64) continue;                             // diagnostics: tallies only
+        if (ABLATE(gp.ablate, 64)) continue;                             // diagnostics: tallies only
         // 4. candidate alleles from the pooled counts (createSNVVariantPool)
         if (!(rc & 0x80u)) continue;                               // N (or masked) reference: no variant
         const int refIdx = (int)((rc >> 5) & 3u);
@@ -2013,22 +2023,116 @@ __global__ __launch_bounds__(1024) void ko_fused(const SiteRec* __restrict__ bre
 // a launch's error; with NGSEP_SYNC_CHECK (diagnostics) the device is drained after every launch, so a fault
 // is reported at the launch (HIP_TRY's line) that caused it
 static hipError_t launch_check() {
-    static const bool sync = std::getenv("NGSEP_SYNC_CHECK") != nullptr;
+    static const bool sync = diag_env("NGSEP_SYNC_CHECK") != nullptr;
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess || !sync) return e;
     return hipDeviceSynchronize();
 }
 
+// ---- pinned host memory and the DMA endpoint registry (engine.hpp) ----
+// Round 3's intermittent "illegal memory access" faults all surfaced at host <-> device copies whose host side was
+// pageable memory (std::vector / new[] arrays of the uploads, freed right after each upload, engine.cpp
+// release_staged).  For a pageable copy above GPU_PINNED_MIN_XFER_SIZE the HIP runtime pins the host range in place
+// (hsa_amd_memory_lock_to_pool, a KFD userptr mapping) and keeps the pin cached after the copy returns; the freed
+// range comes back from glibc at the same address for the next window / contig / test's same-sized array, so a later
+// copy could go through a pin whose pages had been unmapped.  Hence the invariant: no copy's host endpoint is ever
+// pageable.  Pageable sources are memcpy'd into two hipHostMalloc'd staging buffers (h2d); every other host endpoint
+// must lie in a block recorded below, which dma_copy checks before it enqueues the copy.
+namespace {
+struct PinBlock { size_t bytes; int kind; };       // kind 1: aligned_alloc + hipHostRegister, 2: hipHostMalloc
+std::mutex g_pin_mu;
+std::map<uintptr_t, PinBlock> g_pins;
+int host_device_count() {
+    static const int n = [] { int k = 0; return hipGetDeviceCount(&k) == hipSuccess ? k : 0; }();
+    return n;
+}
+void pin_record(void* p, size_t bytes, int kind) {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    g_pins[(uintptr_t)p] = PinBlock{bytes, kind};
+}
+int pin_forget(void* p) {                          // the block's kind (0: not recorded)
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pins.find((uintptr_t)p);
+    if (it == g_pins.end()) return 0;
+    const int k = it->second.kind;
+    g_pins.erase(it);
+    return k;
+}
+}  // namespace
+
+bool pinned_covers(const void* p, size_t bytes) {
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pins.upper_bound(a);
+    if (it == g_pins.begin()) return false;
+    --it;
+    return a >= it->first && a + bytes <= it->first + it->second.bytes;
+}
+
+// runtime-allocated pinned host buffers (hipHostMalloc), recorded for dma_copy
+static hipError_t host_pinned_malloc(void** p, size_t bytes) {
+    const hipError_t e = hipHostMalloc(p, bytes, hipHostMallocDefault);
+    if (e == hipSuccess) pin_record(*p, bytes, 2);
+    return e;
+}
+static void host_pinned_free(void* p) {
+    if (!p) return;
+    (void)pin_forget(p);
+    (void)hipHostFree(p);                          // (the runtime waits for the device's streams)
+}
+
+void* pinned_alloc(size_t bytes) {
+    const size_t rounded = (std::max<size_t>(bytes, 1) + 4095) / 4096 * 4096;
+    if (host_device_count() <= 0) return std::malloc(rounded);     // host-only code paths: nothing is copied
+    void* p = std::aligned_alloc(4096, rounded);
+    if (p && hipHostRegister(p, rounded, hipHostRegisterDefault) == hipSuccess) {
+        pin_record(p, rounded, 1);
+        return p;
+    }
+    std::free(p);
+    // registration refused (locked-memory limit, an overlapping registration): runtime-allocated pinned memory
+    void* q = nullptr;
+    if (host_pinned_malloc(&q, rounded) == hipSuccess) return q;
+    return nullptr;
+}
+void pinned_free(void* p) {
+    if (!p) return;
+    const int kind = pin_forget(p);
+    if (kind == 0) { std::free(p); return; }       // (host-only code paths)
+    // no copy may still be reading the block when it is unregistered (an upload whose run launched nothing after it
+    // is not waited for by the run's own synchronisation)
+    (void)hipDeviceSynchronize();
+    if (kind == 2) { (void)hipHostFree(p); return; }
+    (void)hipHostUnregister(p);
+    std::free(p);
+}
+
+int dma_copy(void* dst, const void* src, size_t bytes, int kind, void* stream, bool sync, std::string& err, const char* file, int line) {
+    if (!bytes) return 0;
+    const void* host = kind == 0 ? src : static_cast<const void*>(dst);
+    const std::string where = std::string(file) + ":" + std::to_string(line);
+    if (!pinned_covers(host, bytes)) {
+        err = "internal error: the host side of the device copy at " + where + " is not registered pinned memory";
+        return -1;
+    }
+    const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
+    const hipError_t e = sync ? hipMemcpy(dst, src, bytes, k) : hipMemcpyAsync(dst, src, bytes, k, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) { err = "device copy at " + where + ": " + hipGetErrorString(e); return -1; }
+    return 0;
+}
+#define DMA(dst, src, bytes, kind, st) do { if (dma_copy((dst), (src), (bytes), (kind), (st), false, err, "kernels.hip", __LINE__) != 0) return -1; } while (0)
+#define DMA_SYNC(dst, src, bytes, kind) do { if (dma_copy((dst), (src), (bytes), (kind), nullptr, true, err, "kernels.hip", __LINE__) != 0) return -1; } while (0)
+
 // host -> device copy of pageable host memory: chunks memcpy'd (all host threads) into the device's two pinned
 // staging buffers, each DMA'd on `st` while the next is filled.  Returns once the source has been read (it may be
-// freed); the last chunk's DMA may still run, and a staging buffer is reused only after its event.  (DMA straight
-// from pageable memory was seen to fault the device intermittently: the pageable copies of the uploads all go here.)
+// freed); the last chunk's DMA may still run, and a staging buffer is reused only after its event.  One thread at a
+// time drives a device (the window worker, or the caller's thread), so the staging state needs no lock.
 constexpr size_t kStageBytes = (size_t)64 << 20;
 static int h2d(Device* d, void* dst, const void* src, size_t bytes, hipStream_t st, std::string& err) {
     if (!bytes) return 0;
     for (int k = 0; k < 2; k++)
         if (!d->stage[k]) {
-            HIP_TRY(hipHostMalloc((void**)&d->stage[k], kStageBytes, hipHostMallocDefault));
+            HIP_TRY(host_pinned_malloc((void**)&d->stage[k], kStageBytes));
             HIP_TRY(hipEventCreateWithFlags(&d->stage_ev[k], hipEventDisableTiming));
             d->stage_busy[k] = false;
         }
@@ -2054,21 +2158,6 @@ static int h2d(Device* d, void* dst, const void* src, size_t bytes, hipStream_t 
     return 0;
 }
 #define H2D(dst, src, bytes, st) do { if (h2d(d, (dst), (src), (bytes), (st), err) != 0) return -1; } while (0)
-void* pinned_alloc(size_t bytes) {
-    void* p = std::aligned_alloc(4096, (bytes + 4095) / 4096 * 4096);
-    if (p && hipHostRegister(p, bytes, hipHostRegisterDefault) != hipSuccess) {
-        // no device (CPU-only host code paths): plain memory is fine there
-    }
-    return p;
-}
-void pinned_free(void* p) {
-    if (!p) return;
-    // no copy may still be reading the block when it is unmapped (an upload whose run launched nothing after it
-    // is not waited for by the run's own synchronisation)
-    (void)hipDeviceSynchronize();
-    (void)hipHostUnregister(p);
-    std::free(p);
-}
 
 int device_count() {
     int n = 0;
@@ -2096,7 +2185,7 @@ Device* device_create(int ordinal, std::string& err) {
     for (auto& e : d->ev) (void)hipEventCreate(&e);
     // both slots' runs go to the device stream: with a stream per slot (NGSEP_SLOT_STREAMS=1) the next
     // run's KT overlaps this run's KP/KO, measured slower (KT shares the CUs: 70 -> 60 G positions/s)
-    const bool one_stream = std::getenv("NGSEP_SLOT_STREAMS") == nullptr;
+    const bool one_stream = diag_env("NGSEP_SLOT_STREAMS") == nullptr;
     for (auto& sl : d->slot) {
         if (one_stream) sl.stream = d->stream;
         else if (hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess) { err = "stream"; return nullptr; }
@@ -2106,7 +2195,7 @@ Device* device_create(int ordinal, std::string& err) {
     }
     if (hipMalloc(&d->d_counters, 24 * sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(d->d_counters, 0, 24 * sizeof(unsigned long long)) != hipSuccess ||
-        hipHostMalloc(&d->h_counters, 4 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
+        host_pinned_malloc((void**)&d->h_counters, 4 * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&d->d_tables, sizeof(LikTables)) != hipSuccess) {
         err = "device allocation failed";
         delete d;
@@ -2118,7 +2207,7 @@ Device* device_create(int ordinal, std::string& err) {
     for (int k = 0; k < 2; k++) {
         if (hipMalloc(&d->slot[k].d_ctr, kCtrWords * sizeof(unsigned long long)) != hipSuccess ||
             hipMemset(d->slot[k].d_ctr, 0, kCtrWords * sizeof(unsigned long long)) != hipSuccess ||
-            hipHostMalloc(&d->slot[k].h_ctr, kCtrWords * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
+            host_pinned_malloc((void**)&d->slot[k].h_ctr, kCtrWords * sizeof(unsigned long long)) != hipSuccess) {
             err = "pinned allocation failed";
             return nullptr;
         }
@@ -2192,7 +2281,7 @@ void device_destroy(Device* d) {
     device_release(d);
     (void)hipDeviceSynchronize();
     (void)hipFree(d->d_rac);
-    if (d->h_rac) (void)hipHostFree(d->h_rac);
+    if (d->h_rac) host_pinned_free(d->h_rac);
     for (auto& sl : d->slot) {
         (void)hipFree(sl.d_brec);
         (void)hipFree(sl.d_bcount);
@@ -2204,7 +2293,7 @@ void device_destroy(Device* d) {
         if (sl.stream && sl.stream != d->stream) (void)hipStreamDestroy(sl.stream);
         (void)hipFree(sl.d_sorted);
         (void)hipFree(sl.d_ext);
-        (void)hipHostFree(sl.h_ctr);
+        host_pinned_free(sl.h_ctr);
         for (auto& e : sl.ev) (void)hipEventDestroy(e);
     }
     (void)hipFree(d->d_psites);
@@ -2215,21 +2304,21 @@ void device_destroy(Device* d) {
     (void)hipFree(d->d_pbig);
     for (auto& m : d->mslot) {
         (void)hipFree(m.d_hard); (void)hipFree(m.d_need); (void)hipFree(m.d_psites); (void)hipFree(m.d_pcalls);
-        if (m.h_psites) (void)hipHostFree(m.h_psites);
+        if (m.h_psites) host_pinned_free(m.h_psites);
         (void)hipFree(m.d_pack); (void)hipFree(m.d_big);
         for (auto& e : m.ev) if (e) (void)hipEventDestroy(e);
     }
     (void)hipFree(d->d_csrc);
-    if (d->h_csrc) (void)hipHostFree(d->h_csrc);
-    if (d->h_psites) (void)hipHostFree(d->h_psites);
-    if (d->h_pcalls) (void)hipHostFree(d->h_pcalls);
+    if (d->h_csrc) host_pinned_free(d->h_csrc);
+    if (d->h_psites) host_pinned_free(d->h_psites);
+    if (d->h_pcalls) host_pinned_free(d->h_pcalls);
     (void)hipFree(d->d_hard);
     (void)hipFree(d->d_counters);
     (void)hipFree(d->d_tables);
     (void)hipFree(d->d_pool);
-    (void)hipHostFree(d->h_counters);
+    host_pinned_free(d->h_counters);
     for (int k = 0; k < 2; k++) {
-        if (d->stage[k]) (void)hipHostFree(d->stage[k]);
+        if (d->stage[k]) host_pinned_free(d->stage[k]);
         if (d->stage_ev[k]) (void)hipEventDestroy(d->stage_ev[k]);
     }
     for (auto& e : d->ev) (void)hipEventDestroy(e);
@@ -2266,7 +2355,7 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
             return -1;
         if (s.n_units) {
             // a pinned arena is copied directly; a pageable one (a layout beyond 4 GB) through the staging buffers
-            if (s.units_pinned) HIP_TRY(hipMemcpyAsync(d->d_units, s.h_units, (size_t)s.n_units * sizeof(uint64_t), hipMemcpyHostToDevice, d->stream));
+            if (pinned_covers(s.h_units, (size_t)s.n_units * sizeof(uint64_t))) DMA(d->d_units, s.h_units, (size_t)s.n_units * sizeof(uint64_t), 0, d->stream);
             else H2D(d->d_units, s.h_units, (size_t)s.n_units * sizeof(uint64_t), d->stream);
         }
         HIP_TRY(hipMemsetAsync(d->d_units + s.n_units, 0, 8 * sizeof(uint64_t), d->stream));
@@ -2294,9 +2383,13 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
             return -1;
         HIP_TRY(hipMemsetAsync(d->d_cneg + ncw, 0, 4 * sizeof(uint32_t), d->stream));
         if (s.pile_bytes) {
-            HIP_TRY(hipMemcpyAsync(d->d_pile, s.h_cpile, (size_t)s.pile_bytes, hipMemcpyHostToDevice, d->stream));
-            HIP_TRY(hipMemcpyAsync(d->d_planes, s.h_planes, (size_t)(s.pile_bytes / 8), hipMemcpyHostToDevice, d->stream));
-            HIP_TRY(hipMemcpyAsync(d->d_cneg, s.h_cneg, ncw * sizeof(uint32_t), hipMemcpyHostToDevice, d->stream));
+            // (the pinned arena is copied directly; H2D stages it should a registration have been refused)
+            if (pinned_covers(s.h_cpile, (size_t)s.pile_bytes)) DMA(d->d_pile, s.h_cpile, (size_t)s.pile_bytes, 0, d->stream);
+            else H2D(d->d_pile, s.h_cpile, (size_t)s.pile_bytes, d->stream);
+            if (pinned_covers(s.h_planes, (size_t)(s.pile_bytes / 8))) DMA(d->d_planes, s.h_planes, (size_t)(s.pile_bytes / 8), 0, d->stream);
+            else H2D(d->d_planes, s.h_planes, (size_t)(s.pile_bytes / 8), d->stream);
+            if (pinned_covers(s.h_cneg, ncw * sizeof(uint32_t))) DMA(d->d_cneg, s.h_cneg, ncw * sizeof(uint32_t), 0, d->stream);
+            else H2D(d->d_cneg, s.h_cneg, ncw * sizeof(uint32_t), d->stream);
         }
         if (!s.h_olist.empty()) H2D(d->d_olist, s.h_olist.data(), s.h_olist.size() * sizeof(uint16_t), d->stream);
         if (!s.h_loff.empty()) H2D(d->d_loff, s.h_loff.data(), s.h_loff.size() * sizeof(int32_t), d->stream);
@@ -2481,7 +2574,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     {
         // KG: the queued sites' columns, one wave per site (grid-stride past the estimate)
         const int64_t nblk = std::max<int64_t>(d->n_cu, std::min<int64_t>((kg_sites + 3) / 4, (int64_t)d->n_cu * 32));
-        static const int kg_env = std::getenv("NGSEP_KG_SITES") ? std::atoi(std::getenv("NGSEP_KG_SITES")) : 4;   // tuning
+        static const int kg_env = diag_env("NGSEP_KG_SITES") ? std::atoi(diag_env("NGSEP_KG_SITES")) : 4;   // tuning
         const int kgs = kg_env == 8 ? 8 : kg_env == 2 ? 2 : 4;
         if (kl_run)
             hipLaunchKernelGGL(kgs == 8 ? k_gather_kl<8> : kgs == 2 ? k_gather_kl<2> : k_gather_kl<4>,
@@ -2500,7 +2593,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     }
     // one lane per queued site: enough workgroups for the queue (the count is on the device; sized from the
     // previous run's survivors, grid-stride beyond)
-    static const int kp_env = std::getenv("NGSEP_KP_GRID") ? std::max(1, std::atoi(std::getenv("NGSEP_KP_GRID"))) : 0;   // tuning
+    static const int kp_env = diag_env("NGSEP_KP_GRID") ? std::max(1, std::atoi(diag_env("NGSEP_KP_GRID"))) : 0;   // tuning
     const int kp_grid = kp_env ? kp_env : (int)std::max<int64_t>(d->n_cu, std::min<int64_t>((d->last_hard + kPostThreads - 1) / kPostThreads, 8 * (int64_t)d->n_cu));
     if (g.ploidy >= 3 && !g.dump_all) {
         if (!d->pool_valid) { err = "ploidy >= 3 without pool tables (device_set_pool)"; return -1; }
@@ -2522,7 +2615,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     // copies: counters and a prefix of the ordered records (sized from the previous run) straight into
     // the slot's pinned store, then the counter set is cleared for the slot's next run.  On the copy
     // stream (ordered after KO by ev[3]) or, with NGSEP_COPY_ON_COMPUTE=1, on the compute stream
-    static const bool on_compute = std::getenv("NGSEP_COPY_ON_COMPUTE") != nullptr;   // diagnostics
+    static const bool on_compute = diag_env("NGSEP_COPY_ON_COMPUTE") != nullptr;   // diagnostics
     hipStream_t cs = on_compute ? sl.stream : d->copy_stream;
     if (!on_compute) HIP_TRY(hipEventRecord(sl.ev[3], sl.stream));
     sl.guess = std::min<int64_t>(d->cap_sites, d->last_n_sites + d->last_n_sites / 64 + 64);
@@ -2530,10 +2623,10 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     sl.host.rec.reserve((size_t)sl.guess);
     sl.host.ext.reserve((size_t)sl.guess_ext);
     if (!on_compute) HIP_TRY(hipStreamWaitEvent(cs, sl.ev[3], 0));
-    HIP_TRY(hipMemcpyAsync(sl.h_ctr, ctr, kCtrWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, cs));
-    HIP_TRY(hipMemcpyAsync(sl.host.rec.buf, sl.d_sorted, (size_t)sl.guess * sizeof(SiteRec), hipMemcpyDeviceToHost, cs));
+    DMA(sl.h_ctr, ctr, kCtrWords * sizeof(unsigned long long), 1, cs);
+    DMA(sl.host.rec.buf, sl.d_sorted, (size_t)sl.guess * sizeof(SiteRec), 1, cs);
     if (sl.guess_ext > 0)
-        HIP_TRY(hipMemcpyAsync(sl.host.ext.buf, sl.d_ext, (size_t)sl.guess_ext * sizeof(ngsep_site_out), hipMemcpyDeviceToHost, cs));
+        DMA(sl.host.ext.buf, sl.d_ext, (size_t)sl.guess_ext * sizeof(ngsep_site_out), 1, cs);
     HIP_TRY(hipMemsetAsync(ctr, 0, kCtrWords * sizeof(unsigned long long), cs));
     HIP_TRY(hipEventRecord(sl.ev[4], cs));
     sl.g = g;
@@ -2575,7 +2668,7 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
     HIP_TRY(hipSetDevice(d->ordinal));
     if (d->n_collected == d->n_submitted) { err = "no run to collect"; return -1; }
     RunSlot& sl = d->slot[d->n_collected % 2];
-    static const bool host_timing = std::getenv("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     const auto h0 = std::chrono::steady_clock::now();
     HIP_TRY(hipEventSynchronize(sl.ev[4]));
     if (host_timing) {
@@ -2644,14 +2737,12 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
     if (n > sl.guess) {
         sl.host.rec.n = (size_t)sl.guess;             // keep the records already copied when the store grows
         sl.host.rec.reserve((size_t)n);
-        HIP_TRY(hipMemcpy(sl.host.rec.buf + sl.guess, sl.d_sorted + sl.guess, (size_t)(n - sl.guess) * sizeof(SiteRec),
-                          hipMemcpyDeviceToHost));
+        DMA_SYNC(sl.host.rec.buf + sl.guess, sl.d_sorted + sl.guess, (size_t)(n - sl.guess) * sizeof(SiteRec), 1);
     }
     if (ne > sl.guess_ext) {
         sl.host.ext.n = (size_t)sl.guess_ext;
         sl.host.ext.reserve((size_t)ne);
-        HIP_TRY(hipMemcpy(sl.host.ext.buf + sl.guess_ext, sl.d_ext + sl.guess_ext,
-                          (size_t)(ne - sl.guess_ext) * sizeof(ngsep_site_out), hipMemcpyDeviceToHost));
+        DMA_SYNC(sl.host.ext.buf + sl.guess_ext, sl.d_ext + sl.guess_ext, (size_t)(ne - sl.guess_ext) * sizeof(ngsep_site_out), 1);
     }
     sl.host.rec.n = (size_t)n;
     sl.host.ext.n = (size_t)ne;
@@ -2778,7 +2869,7 @@ int device_run_rac(Device* d, const Staged& s, int64_t g0, int64_t g1, int32_t m
     if (g0 < 0 || g1 > s.g_len || g1 < g0 || (g1 > 0 && ((g1 - 1) >> d->log2_tile) >= d->n_tiles)) { err = "position range outside the layout"; return -1; }
     if (!d->d_rac) {
         HIP_TRY(hipMalloc(&d->d_rac, 64 * sizeof(unsigned long long) + 2 * kRacBlocks * sizeof(double)));
-        HIP_TRY(hipHostMalloc(&d->h_rac, 64 * sizeof(unsigned long long) + 2 * kRacBlocks * sizeof(double), hipHostMallocDefault));
+        HIP_TRY(host_pinned_malloc((void**)&d->h_rac, 64 * sizeof(unsigned long long) + 2 * kRacBlocks * sizeof(double)));
     }
     unsigned long long* hist = reinterpret_cast<unsigned long long*>(d->d_rac);
     double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(d->d_rac) + 64 * sizeof(unsigned long long));
@@ -2786,7 +2877,7 @@ int device_run_rac(Device* d, const Staged& s, int64_t g0, int64_t g1, int32_t m
     hipExtLaunchKernelGGL(k_rac, dim3(kRacBlocks), dim3(kRacThreads), 0, d->stream, d->ev[0], d->ev[1], 0,
                           (const uint8_t*)d->d_pile, (const TileInfo*)d->d_tinfo, d->log2_tile, g0, g1, min_rd, min_bq, hist, part);
     HIP_TRY(launch_check());
-    HIP_TRY(hipMemcpyAsync(d->h_rac, d->d_rac, 64 * sizeof(unsigned long long) + 2 * kRacBlocks * sizeof(double), hipMemcpyDeviceToHost, d->stream));
+    DMA(d->h_rac, d->d_rac, 64 * sizeof(unsigned long long) + 2 * kRacBlocks * sizeof(double), 1, d->stream);
     HIP_TRY(hipStreamSynchronize(d->stream));
     const unsigned long long* hh = reinterpret_cast<const unsigned long long*>(d->h_rac);
     const double* pp = reinterpret_cast<const double*>(reinterpret_cast<const char*>(d->h_rac) + 64 * sizeof(unsigned long long));
@@ -2820,7 +2911,7 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     const int32_t S = d->n_samples;
     if (S <= 0 || n_samples != S) { err = "multisample run without samples (ngsep_set_samples)"; return -1; }
     if (S > kMaxSamplesDevice) { err = "too many samples for one device run"; return -1; }
-    const bool timing = std::getenv("NGSEP_TIMING") != nullptr;
+    const bool timing = diag_env("NGSEP_TIMING") != nullptr;
     if (timing && !d->d_stamps) HIP_TRY(hipMalloc(&d->d_stamps, 16 * sizeof(unsigned long long)));
     if (timing) HIP_TRY(hipMemsetAsync(d->d_stamps, 0, 16 * sizeof(unsigned long long), d->stream));
     int64_t want = std::max<int64_t>(d->last_n_sites + d->last_n_sites / 4 + 1024, 4096);
@@ -2879,7 +2970,7 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
                           S, min_adf, ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), d->d_psites, d->d_pcalls,
                           ctr, d->cap_psites, d->d_stamps);
     HIP_TRY(launch_check());
-    HIP_TRY(hipMemcpyAsync(d->h_counters, ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, d->stream));
+    DMA(d->h_counters, ctr, 4 * sizeof(unsigned long long), 1, d->stream);
     HIP_TRY(hipStreamSynchronize(d->stream));
     const unsigned long long c3 = d->h_counters[3];
     if (c3 >> 63) { err = "a position is covered by more reads than the population kernel holds (" + std::to_string(kPopListCap) + ")"; return -1; }
@@ -2897,18 +2988,18 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
         return device_run_multi(d, s, t, g, n_samples, min_adf, ploidy, sites, calls, n_sites, scan_ms, geno_ms, total_ms, n_candidates, err);
     }
     if (n > d->cap_h_psites || n * S > d->cap_h_pcalls) {          // pinned staging, grown geometrically
-        if (d->h_psites) (void)hipHostFree(d->h_psites);
-        if (d->h_pcalls) (void)hipHostFree(d->h_pcalls);
+        if (d->h_psites) host_pinned_free(d->h_psites);
+        if (d->h_pcalls) host_pinned_free(d->h_pcalls);
         d->h_psites = nullptr;
         d->h_pcalls = nullptr;
         d->cap_h_psites = std::max<int64_t>(n + n / 2, 1024);
         d->cap_h_pcalls = d->cap_h_psites * S;
-        HIP_TRY(hipHostMalloc((void**)&d->h_psites, (size_t)d->cap_h_psites * sizeof(ngsep_popsite_out), hipHostMallocDefault));
-        HIP_TRY(hipHostMalloc((void**)&d->h_pcalls, (size_t)d->cap_h_pcalls * sizeof(ngsep_sample_call), hipHostMallocDefault));
+        HIP_TRY(host_pinned_malloc((void**)&d->h_psites, (size_t)d->cap_h_psites * sizeof(ngsep_popsite_out)));
+        HIP_TRY(host_pinned_malloc((void**)&d->h_pcalls, (size_t)d->cap_h_pcalls * sizeof(ngsep_sample_call)));
     }
     if (n) {
         // the sites only: their calls come back in output order through device_fetch_calls_ordered
-        HIP_TRY(hipMemcpyAsync(d->h_psites, d->d_psites, (size_t)n * sizeof(ngsep_popsite_out), hipMemcpyDeviceToHost, d->stream));
+        DMA(d->h_psites, d->d_psites, (size_t)n * sizeof(ngsep_popsite_out), 1, d->stream);
         HIP_TRY(hipStreamSynchronize(d->stream));
     }
     *sites = d->h_psites;
@@ -2918,10 +3009,12 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     d->last_hard = (int64_t)d->h_counters[2];
     d->last_exact = (int64_t)(c3 & 0x7FFFFFFFFFFFFFFFull);
     if (timing) {
-        unsigned long long st[16];
-        HIP_TRY(hipMemcpy(st, d->d_stamps, sizeof st, hipMemcpyDeviceToHost));
+        unsigned long long* st = nullptr;                        // (a pinned endpoint, as every copy's)
+        HIP_TRY(host_pinned_malloc((void**)&st, 16 * sizeof(unsigned long long)));
+        DMA_SYNC(st, d->d_stamps, 16 * sizeof(unsigned long long), 1);
         std::fprintf(stderr, "[ngsep timing] KPM block 0 phases (cycles): tally %lld, pooled %lld, genotype %lld\n",
                      (long long)(st[1] - st[0]), (long long)(st[2] - st[1]), (long long)(st[5] - st[2]));
+        host_pinned_free(st);
     }
     float a = 0, a2 = 0;
     (void)hipEventElapsedTime(&a, d->ev[0], d->ev[1]);
@@ -2991,12 +3084,12 @@ int device_fetch_calls_from(Device* d, const ngsep_sample_call* calls, hipStream
     const int64_t S = d->n_samples;
     if (m > d->cap_csrc) {
         (void)hipFree(d->d_csrc);
-        if (d->h_csrc) (void)hipHostFree(d->h_csrc);
+        if (d->h_csrc) host_pinned_free(d->h_csrc);
         d->d_csrc = nullptr;
         d->h_csrc = nullptr;
         d->cap_csrc = std::max<int64_t>(m + m / 2, 4096);
         HIP_TRY(hipMalloc(&d->d_csrc, (size_t)d->cap_csrc * sizeof(int64_t)));
-        HIP_TRY(hipHostMalloc((void**)&d->h_csrc, (size_t)(d->cap_csrc + 1) * sizeof(int64_t), hipHostMallocDefault));
+        HIP_TRY(host_pinned_malloc((void**)&d->h_csrc, (size_t)(d->cap_csrc + 1) * sizeof(int64_t)));
     }
     if (m * S > d->cap_pcalls_ord) {
         (void)hipFree(d->d_pcalls_ord);
@@ -3010,22 +3103,22 @@ int device_fetch_calls_from(Device* d, const ngsep_sample_call* calls, hipStream
     // the big-record counter sits after the records
     unsigned long long* d_nbig = reinterpret_cast<unsigned long long*>(d->d_pbig + d->cap_pcalls_ord);
     std::memcpy(d->h_csrc, src, (size_t)m * sizeof(int64_t));
-    HIP_TRY(hipMemcpyAsync(d->d_csrc, d->h_csrc, (size_t)m * sizeof(int64_t), hipMemcpyHostToDevice, stream));
+    DMA(d->d_csrc, d->h_csrc, (size_t)m * sizeof(int64_t), 0, stream);
     HIP_TRY(hipMemsetAsync(d_nbig, 0, sizeof(unsigned long long), stream));
     const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((m * S + 255) / 256, (int64_t)d->n_cu * 8));
     hipLaunchKernelGGL(k_gather_calls, dim3((unsigned)nblk), dim3(256), 0, stream, calls, (const int64_t*)d->d_csrc, m, S,
                        d->d_pcalls_ord, d->d_pbig, d_nbig, d->cap_pcalls_ord, (int64_t)big->size(),
-                       std::getenv("NGSEP_POP_ALL_BIG") ? 1 : 0);   // (tests: every call through the whole-record list)
+                       env_hook("NGSEP_POP_ALL_BIG") ? 1 : 0);   // (tests: every call through the whole-record list)
     HIP_TRY(launch_check());
-    HIP_TRY(hipMemcpyAsync(dst, d->d_pcalls_ord, (size_t)(m * S) * sizeof(PopCall32), hipMemcpyDeviceToHost, stream));
+    DMA(dst, d->d_pcalls_ord, (size_t)(m * S) * sizeof(PopCall32), 1, stream);
     unsigned long long* h_nbig = reinterpret_cast<unsigned long long*>(d->h_csrc + d->cap_csrc);
-    HIP_TRY(hipMemcpyAsync(h_nbig, d_nbig, sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+    DMA(h_nbig, d_nbig, sizeof(unsigned long long), 1, stream);
     HIP_TRY(hipStreamSynchronize(stream));
     const int64_t nb = (int64_t)*h_nbig;
     if (nb > 0) {
         const size_t b0 = big->size();
         big->resize(b0 + (size_t)nb);
-        HIP_TRY(hipMemcpy(big->data() + b0, d->d_pbig, (size_t)nb * sizeof(ngsep_sample_call), hipMemcpyDeviceToHost));
+        DMA_SYNC(big->data() + b0, d->d_pbig, (size_t)nb * sizeof(ngsep_sample_call), 1);
     }
     return 0;
 }
@@ -3097,9 +3190,9 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
         m.cap_psites = want;
     }
     if (want > m.cap_h_psites) {
-        if (m.h_psites) (void)hipHostFree(m.h_psites);
+        if (m.h_psites) host_pinned_free(m.h_psites);
         m.h_psites = nullptr;
-        HIP_TRY(hipHostMalloc((void**)&m.h_psites, (size_t)want * sizeof(ngsep_popsite_out), hipHostMallocDefault));
+        HIP_TRY(host_pinned_malloc((void**)&m.h_psites, (size_t)want * sizeof(ngsep_popsite_out)));
         m.cap_h_psites = want;
     }
     const int64_t qwant = std::max<int64_t>(std::max<int64_t>(d->g_len / 64 + 65536, d->last_hard + 1024), 65536);
@@ -3133,7 +3226,7 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
     } else {
     HIP_TRY(hipMemsetAsync(m.d_need, 0, (size_t)nwords * sizeof(uint32_t), d->stream));
     const int64_t ngroups = (d->mc_entries + 63) / 64;
-    static const int ktm_env = std::getenv("NGSEP_KTM_BPC") ? std::max(1, std::atoi(std::getenv("NGSEP_KTM_BPC"))) : 8;   // tuning
+    static const int ktm_env = diag_env("NGSEP_KTM_BPC") ? std::max(1, std::atoi(diag_env("NGSEP_KTM_BPC"))) : 8;   // tuning
     const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((ngroups + 3) / 4, (int64_t)d->n_cu * ktm_env));
     hipExtLaunchKernelGGL(k_scan_multi, dim3((unsigned)nblk), dim3(256), 0, d->stream, m.ev[0], nullptr, 0,
                           (const int32_t*)d->d_mc_pos, (const uint8_t*)d->d_mc_n, (const int64_t*)d->d_mc_gbase,
@@ -3175,17 +3268,17 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
     const int64_t pblk = std::max<int64_t>(1, std::min<int64_t>((m.cap_psites * S + 255) / 256, (int64_t)d->n_cu * 8));
     hipLaunchKernelGGL(k_pack_calls, dim3((unsigned)pblk), dim3(256), 0, d->stream, (const ngsep_sample_call*)m.d_pcalls,
                        (const unsigned long long*)ctr, m.cap_psites, (int64_t)S, m.d_pack, m.d_big, d_nbig, m.cap_big,
-                       std::getenv("NGSEP_POP_ALL_BIG") ? 1 : 0);   // (tests: every call through the whole-record list)
+                       env_hook("NGSEP_POP_ALL_BIG") ? 1 : 0);   // (tests: every call through the whole-record list)
     HIP_TRY(launch_check());
     HIP_TRY(hipEventRecord(m.ev[5], d->stream));
     HIP_TRY(hipStreamWaitEvent(d->copy_stream, m.ev[5], 0));
     hipStream_t cs = d->copy_stream;
-    HIP_TRY(hipMemcpyAsync(d->slot[d->mnext].h_ctr, ctr, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, cs));
+    DMA(d->slot[d->mnext].h_ctr, ctr, 8 * sizeof(unsigned long long), 1, cs);
     m.guess = std::min<int64_t>(m.cap_psites, d->last_n_sites + d->last_n_sites / 16 + 64);
-    HIP_TRY(hipMemcpyAsync(m.h_psites, m.d_psites, (size_t)m.guess * sizeof(ngsep_popsite_out), hipMemcpyDeviceToHost, cs));
-    HIP_TRY(hipMemcpyAsync(m.h_pack.data(), m.d_pack, (size_t)(m.guess * S) * sizeof(PopCall32), hipMemcpyDeviceToHost, cs));
+    DMA(m.h_psites, m.d_psites, (size_t)m.guess * sizeof(ngsep_popsite_out), 1, cs);
+    DMA(m.h_pack.data(), m.d_pack, (size_t)(m.guess * S) * sizeof(PopCall32), 1, cs);
     m.guess_big = std::min<int64_t>(m.cap_big, 4096);
-    HIP_TRY(hipMemcpyAsync(m.h_big.data(), m.d_big, (size_t)m.guess_big * sizeof(ngsep_sample_call), hipMemcpyDeviceToHost, cs));
+    DMA(m.h_big.data(), m.d_big, (size_t)m.guess_big * sizeof(ngsep_sample_call), 1, cs);
     HIP_TRY(hipEventRecord(m.ev[4], cs));
     m.busy = true;
     d->mnext ^= 1;
@@ -3214,12 +3307,12 @@ int device_collect_multi(Device* d, const ngsep_popsite_out** sites, int64_t* n_
     if (*rerun) return 0;
     const int64_t S = d->n_samples;
     if (n > m.guess) {
-        HIP_TRY(hipMemcpy(m.h_psites + m.guess, m.d_psites + m.guess, (size_t)(n - m.guess) * sizeof(ngsep_popsite_out), hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(m.h_pack.data() + m.guess * S, m.d_pack + m.guess * S, (size_t)((n - m.guess) * S) * sizeof(PopCall32), hipMemcpyDeviceToHost));
+        DMA_SYNC(m.h_psites + m.guess, m.d_psites + m.guess, (size_t)(n - m.guess) * sizeof(ngsep_popsite_out), 1);
+        DMA_SYNC(m.h_pack.data() + m.guess * S, m.d_pack + m.guess * S, (size_t)((n - m.guess) * S) * sizeof(PopCall32), 1);
     }
     const int64_t nb = (int64_t)hc[5];
     if (nb > m.guess_big)
-        HIP_TRY(hipMemcpy(m.h_big.data() + m.guess_big, m.d_big + m.guess_big, (size_t)(nb - m.guess_big) * sizeof(ngsep_sample_call), hipMemcpyDeviceToHost));
+        DMA_SYNC(m.h_big.data() + m.guess_big, m.d_big + m.guess_big, (size_t)(nb - m.guess_big) * sizeof(ngsep_sample_call), 1);
     *sites = m.h_psites;
     *n_sites = n;
     d->last_n_sites = n;

@@ -202,8 +202,13 @@ class GpuPileupSession:
         out = []
         for i, s in enumerate(self.raw_sites()):
             if s.is_call & 8:                    # an indel / STR call (IndelRealignerPileupListener + callIndel)
-                buf = ctypes.create_string_buffer(1 << 16)
-                self._lib.ngsep_site_vcf_line(self._ctx, i, buf, 1 << 16)
+                # the record's length first (cap 0), then the whole line: a multi-allelic STR's PL list grows
+                # with the square of its allele count
+                need = self._lib.ngsep_site_vcf_line(self._ctx, i, None, 0)
+                if need < 0:
+                    raise NgsepError(int(need), self._lib.ngsep_last_error(self._ctx).decode())
+                buf = ctypes.create_string_buffer(int(need) + 1)
+                self._lib.ngsep_site_vcf_line(self._ctx, i, buf, int(need) + 1)
                 f = buf.value.decode().rstrip("\n").split("\t")
                 gt = f[9].split(":")[0]
                 out.append(CalledSite(
