@@ -1357,7 +1357,8 @@ static void mvd_print(FILE* out, const char* seqName, int pos, const char* id, c
         fputs(info, out);
         free(nc); free(cl); free(acn);
     }
-    if (v->multisnv_type) fprintf(out, ";TYPE=MULTISNV");   /* VCFFileWriter.java:47-49 */
+    if (v->multisnv_type == 2) fprintf(out, ";TYPE=EMBEDDED");   /* TYPE_EMBEDDED_SNV (MultisampleVariantsDetector.java:581) */
+    else if (v->multisnv_type) fprintf(out, ";TYPE=MULTISNV");   /* VCFFileWriter.java:47-49 */
     fprintf(out, "\tGT:PL:GQ:DP:BSDP:ACN");
     for (int s = 0; s < M->n_samples; s++) {
         const ngo_scall* c = &M->calls[s];
@@ -1386,7 +1387,74 @@ static void mvd_print(FILE* out, const char* seqName, int pos, const char* id, c
     fprintf(out, "\n");
 }
 
-/* MultisampleVariantsDetector.onPileup (:522-558) for a pileup without STRs / known variants */
+/* the position's per-sample span-1 counts (getAlleleCalls(1, sample.getReadGroups()): the sample's read groups in
+ * HashSet order, pending order inside each, PileupRecord.getAlleleCalls :104-152) and the pooled counts of every
+ * alignment (getAlleleCalls(1, null)); `alns` is the pileup (its membership fixed before the realigner's edits:
+ * aligned_read_pos drops an alignment an edit moved off the position) */
+static void mvd_snv_counts(ngo_gen* G, int pos, ngo_aln** alns, int n, ngo_counts* pooled) {
+    ngo_mvd* M = G->mvd;
+    const ngo_params* p = G->p;
+    ngo_counts_init(pooled, 4, 0.5, p->max_base_qs);
+    for (int s = 0; s < M->n_samples; s++) { ngo_counts_init(&M->h[s], 4, 0.5, p->max_base_qs); M->sc[s].n = 0; }
+    int maxrank = 0;
+    for (int s = 0; s < M->n_samples; s++) if (M->n_rank[s] > maxrank) maxrank = M->n_rank[s];
+    for (int rank = -1; rank < maxrank; rank++) {
+        for (int k = 0; k < n; k++) {
+            ngo_aln* a = alns[k];
+            if (a->first > pos || a->last < pos) continue;
+            int sm = a->rg >= 0 ? M->rg_sample[a->rg] : -1;
+            if (rank >= 0 && (sm < 0 || M->rg_rank[a->rg] != rank)) continue;
+            if (!a->chars) continue;
+            int rp = aligned_read_pos(a, pos);
+            if (rp < 0) continue;
+            int len = a->acl[rp];
+            if (len != 1) continue;
+            int qc = a->quals ? a->quals[rp] : '+';
+            int q = qc - 33; if (q > 30) q = 30;
+            ngo_counts* h = rank < 0 ? pooled : &M->h[sm];
+            ngo_counts_update(h, base_idx(a->chars[rp]), (int8_t)q, (a->flags & FLAG_REVERSE) != 0);
+            if (rank >= 0 && M->ploidy >= 3) acalls_push(&M->sc[sm], base_idx(a->chars[rp]), (int8_t)q, (a->flags & FLAG_REVERSE) != 0);
+        }
+    }
+}
+
+/* discoverPopulationSNV (:585-597): createSNVVariantPool (SingleSampleVariantPileupListener.java:297-332) over the
+ * pooled counts, then the multi-allelic loop (makeNewVariant :642-656); 1 with the variant in *v */
+static int mvd_snv_variant(ngo_gen* G, char R, const ngo_counts* pooled, ngo_pvar* out) {
+    ngo_mvd* M = G->mvd;
+    if (pooled->total_count == 0) return 0;
+    int refIdx = base_idx(R);
+    if (refIdx < 0) return 0;
+    int sum = pooled->counts[0] + pooled->counts[1] + pooled->counts[2] + pooled->counts[3];
+    double minCount = M->min_adf * sum;
+    if (minCount < 1) minCount = 1;
+    ngo_pvar v = {0, {0}, 0};
+    v.idx[v.n++] = refIdx;
+    for (int i = 0; i < 4; i++)
+        if (pooled->counts[i] >= minCount && i != refIdx) v.idx[v.n++] = i;
+    if (v.n < 2) return 0;
+    v.multisnv_type = v.n > 2;
+    int qs = 0;
+    while (v.n > 2) {
+        mvd_genotype_all(M, &v, G->het_rate, &qs);
+        /* makeNewVariant (MultisampleVariantsDetector.java:642-656, SingleSampleVariantPileupListener.java:346-359) */
+        int called[4] = {0, 0, 0, 0};
+        called[v.idx[0]] = 1;
+        for (int s = 0; s < M->n_samples; s++)
+            for (int i = 0; i < M->calls[s].n_called; i++) called[v.idx[M->calls[s].called[i]]] = 1;
+        int nset = called[0] + called[1] + called[2] + called[3];
+        if (nset == v.n) break;
+        ngo_pvar nv = {0, {0}, 0};
+        nv.idx[nv.n++] = v.idx[0];
+        for (int i = 0; i < 4; i++) if (called[i] && i != v.idx[0]) nv.idx[nv.n++] = i;
+        v = nv;   /* SNV (BIALLELIC type) or GenomicVariantImpl (UNDETERMINED type): no TYPE annotation */
+    }
+    if (v.n < 2) return 0;   /* only the reference allele is left: not an SNV, no decided non-reference call */
+    *out = v;
+    return 1;
+}
+
+/* MultisampleVariantsDetector.onPileup (:522-558) without the indel realigner (indel pass-through) */
 static void mvd_on_pileup(ngo_gen* G, int pos) {
     ngo_mvd* M = G->mvd;
     const ngo_params* p = G->p;
@@ -1398,31 +1466,8 @@ static void mvd_on_pileup(ngo_gen* G, int pos) {
         if (p->ignore_lowercase_ref && islower((unsigned char)r)) return;
     }
     char R = (char)toupper((unsigned char)r);
-    /* discoverPopulationSNV (:585-597): pooled calls of every alignment, then per sample in the
-     * order of its read groups (PileupRecord.getAlleleCalls, :104-152) */
     ngo_counts pooled;
-    ngo_counts_init(&pooled, 4, 0.5, p->max_base_qs);
-    for (int s = 0; s < M->n_samples; s++) { ngo_counts_init(&M->h[s], 4, 0.5, p->max_base_qs); M->sc[s].n = 0; }
-    int maxrank = 0;
-    for (int s = 0; s < M->n_samples; s++) if (M->n_rank[s] > maxrank) maxrank = M->n_rank[s];
-    for (int rank = -1; rank < maxrank; rank++) {
-        for (int k = 0; k < G->pending.n; k++) {
-            ngo_aln* a = G->pending.a[k];
-            if (a->first > pos || a->last < pos) continue;
-            int sm = a->rg >= 0 ? M->rg_sample[a->rg] : -1;
-            if (rank >= 0 && (sm < 0 || M->rg_rank[a->rg] != rank)) continue;
-            if (!a->chars) continue;
-            int rp = aligned_read_pos(a, pos);
-            if (rp < 0) continue;
-            int len = a->acl[rp];
-            if (len != 1) continue;
-            int qc = a->quals ? a->quals[rp] : '+';
-            int q = qc - 33; if (q > 30) q = 30;
-            ngo_counts* h = rank < 0 ? &pooled : &M->h[sm];
-            ngo_counts_update(h, base_idx(a->chars[rp]), (int8_t)q, (a->flags & FLAG_REVERSE) != 0);
-            if (rank >= 0 && M->ploidy >= 3) acalls_push(&M->sc[sm], base_idx(a->chars[rp]), (int8_t)q, (a->flags & FLAG_REVERSE) != 0);
-        }
-    }
+    mvd_snv_counts(G, pos, G->pending.a, G->pending.n, &pooled);
     if (G->known) {
         /* onPileup with input variants (MultisampleVariantsDetector.java:539-551): every input variant at this
          * position (nextSIVIndex), genotypeVariant (:664-693) over its own alleles, the record always written
@@ -1440,35 +1485,9 @@ static void mvd_on_pileup(ngo_gen* G, int pos) {
         }
         return;
     }
-    /* SingleSampleVariantPileupListener.createSNVVariantPool (:297-332) */
-    if (pooled.total_count == 0) return;
-    int refIdx = base_idx(R);
-    if (refIdx < 0) return;
-    int sum = pooled.counts[0] + pooled.counts[1] + pooled.counts[2] + pooled.counts[3];
-    double minCount = M->min_adf * sum;
-    if (minCount < 1) minCount = 1;
-    ngo_pvar v = {0, {0}, 0};
-    v.idx[v.n++] = refIdx;
-    for (int i = 0; i < 4; i++)
-        if (pooled.counts[i] >= minCount && i != refIdx) v.idx[v.n++] = i;
-    if (v.n < 2) return;
-    v.multisnv_type = v.n > 2;
+    ngo_pvar v;
+    if (!mvd_snv_variant(G, R, &pooled, &v)) return;
     int qs = 0;
-    while (v.n > 2) {
-        mvd_genotype_all(M, &v, G->het_rate, &qs);
-        /* makeNewVariant (MultisampleVariantsDetector.java:642-656, SingleSampleVariantPileupListener.java:346-359) */
-        int called[4] = {0, 0, 0, 0};
-        called[v.idx[0]] = 1;
-        for (int s = 0; s < M->n_samples; s++)
-            for (int i = 0; i < M->calls[s].n_called; i++) called[v.idx[M->calls[s].called[i]]] = 1;
-        int nset = called[0] + called[1] + called[2] + called[3];
-        if (nset == v.n) break;
-        ngo_pvar nv = {0, {0}, 0};
-        nv.idx[nv.n++] = v.idx[0];
-        for (int i = 0; i < 4; i++) if (called[i] && i != v.idx[0]) nv.idx[nv.n++] = i;
-        v = nv;   /* SNV (BIALLELIC type) or GenomicVariantImpl (UNDETERMINED type): no TYPE annotation */
-    }
-    if (v.n < 2) return;   /* only the reference allele is left: not an SNV, no decided non-reference call */
     mvd_genotype_all(M, &v, G->het_rate, &qs);
     if (qs == 0 || qs < p->min_quality) return;           /* MultisampleVariantsDetector.java:534 */
     mvd_print(G->out, sq->name, pos, NULL, &v, qs, M);
@@ -1479,6 +1498,424 @@ static void mvd_on_pileup(ngo_gen* G, int pos) {
 struct ngo_indel_call_s { ngo_indel_call c; int ploidy; };
 static void free_indel_call(struct ngo_indel_call_s* c) { for (int i = 0; i < c->c.n; i++) free(c->c.alleles[i]); free(c); }
 static void print_indel_call_any(FILE* out, const char* seqName, const ngo_call* c) { print_indel_call(out, seqName, &c->indel->c, c->indel->ploidy); }
+
+/* ==== MultisampleVariantsDetector with IndelRealignerPileupListener first in the listener chain
+ * (MultisampleVariantsDetector.java:449-450): onPileup's span rules (:522-538), the span branch
+ * discoverPopulationVariantWithSpan / discoverPopulationIndel (:599-634) and every sample's indel genotype
+ * (SingleSampleVariantPileupListener.genotypeVariantSample :361-391 -> VariantDiscoverySNVQAlgorithm.callIndel
+ * :265-361 with the variant given) ==== */
+
+/* one sample's call of an indel variant of n alleles (a CalledGenomicVariantImpl) */
+typedef struct {
+    int n_called, called[2], gq, dp, has_report, total_cn;
+    int* counts;               /* n: the report's counts (CountsHelper.getCounts) */
+    double* logc;              /* n x n: the report's log-conditionals */
+    int* acn;                  /* n: allelesCopyNumber */
+} ngo_iscall;
+
+static void iscall_free(ngo_iscall* c) { free(c->counts); free(c->logc); free(c->acn); c->counts = NULL; c->logc = NULL; c->acn = NULL; }
+
+/* CalledGenomicVariantImpl.updateAllelesCopyNumberFromCounts (variants/CalledGenomicVariantImpl.java:228-282) */
+static void iscall_update_cn(ngo_iscall* c, int n, int total) {
+    c->total_cn = total;
+    for (int i = 0; i < n; i++) c->acn[i] = 0;
+    if (c->n_called == 0) return;
+    if (c->n_called == 1 && c->called[0] == 0) { c->acn[0] = total; return; }
+    const int nc = c->n_called;
+    if (total <= nc) { for (int i = 0; i < nc; i++) c->acn[c->called[i]] = 1; return; }
+    if (!c->has_report) {
+        const int def = total / nc;
+        for (int i = 0; i < nc; i++) c->acn[c->called[i]] = def;
+        c->acn[c->called[0]] += total - def * nc;
+        return;
+    }
+    int rc[2], tr = 0;
+    for (int i = 0; i < nc; i++) { rc[i] = c->counts[c->called[i]]; if (rc[i] == 0) rc[i] = 1; tr += rc[i]; }
+    int tc = 0;
+    for (int i = 0; i < nc; i++) {
+        const int64_t r = ngo_java_round((double)total * rc[i] / tr);
+        c->acn[c->called[i]] = (int)(r > 1 ? (int16_t)r : 1);
+        tc += c->acn[c->called[i]];
+    }
+    if (tc < total) c->acn[c->called[0]] += total - tc;
+    else {
+        int ex = tc - total;
+        for (int i = nc - 1; ex > 0 && i >= 0; i--) {
+            const int j = c->called[i];
+            const int rm = ex < c->acn[j] - 1 ? ex : c->acn[j] - 1;
+            c->acn[j] -= rm;
+            ex -= rm;
+        }
+    }
+}
+
+/* genotypeVariantSample for an indel variant at ploidy < 3 (SingleSampleVariantPileupListener.java:377-390) with a
+ * fresh listener (minQuality = DEF_MIN_QUALITY 40): calculateCountsIndel over the variant's alleles, callIndel with
+ * the variant (indexes of the maximum genotype taken as they are, :335-345), updateAllelesCopyNumberFromCounts(ploidy),
+ * makeUndecided below 40 (:320-325) */
+static void genotype_indel_sample(const ngo_sv* alleles, const ngo_icalls* calls, double het, int ploidy, int max_base_qs,
+                                  ngo_iscall* c) {
+    const int n = alleles->n;
+    memset(c, 0, sizeof(*c));
+    c->counts = calloc((size_t)n, sizeof(int));
+    c->logc = calloc((size_t)n * n, sizeof(double));
+    c->acn = calloc((size_t)n, sizeof(int));
+    ngo_icounts ih;
+    icounts_run(&ih, alleles, calls, max_base_qs, 0.5);
+    if (ih.total_count == 0) {
+        /* new CalledGenomicVariantImpl(variant, new byte[0]) (:274-277), then the copy number of the ploidy */
+        free(ih.counts); free(ih.logc);
+        iscall_update_cn(c, n, ploidy);
+        return;
+    }
+    const int heteroGenotypes = n * (n - 1);                  /* getPosteriorProbabilities (CountsHelper.java:410-443) */
+    const double logPriorHetero = log10(het / heteroGenotypes), logPriorHomo = log10((1 - het) / n);
+    double* ev = malloc(sizeof(double) * (size_t)n * n);
+    double* post = calloc((size_t)n * n, sizeof(double));
+    int k = 0;
+    for (int i = 0; i < n; i++) {
+        ev[k++] = ih.logc[i * n + i] + logPriorHomo;
+        for (int j = 0; j < n; j++) if (i != j) ev[k++] = ih.logc[i * n + j] + logPriorHetero;
+    }
+    calc_posteriors(ev, n * n);
+    k = 0;
+    for (int i = 0; i < n; i++) {
+        post[i * n + i] = ev[k++];
+        for (int j = 0; j < n; j++) if (i != j) post[i * n + j] = ev[k++];
+    }
+    free(ev);
+    int im0 = 0, im1 = 0;                                     /* getIndexesMaxGenotype(post, 0) (:223-243) */
+    double probMax = post[0];
+    for (int i = 0; i < n; i++)
+        for (int j = i; j < n; j++) {
+            double gp = post[i * n + j];
+            if (i != j) gp += post[j * n + i];
+            if (gp > probMax + 0.01) { probMax = gp; im0 = i; im1 = j; }
+        }
+    if (im0 > 100 || im1 > 100) c->n_called = 0;              /* GenomicVariant.MAX_NUM_ALLELES */
+    else if (im1 != im0) { c->n_called = 2; c->called[0] = im0; c->called[1] = im1; }
+    else { c->n_called = 1; c->called[0] = im0; }
+    double maxP = post[im0 * n + im1];
+    if (im0 != im1) maxP += post[im1 * n + im0];
+    free(post);
+    c->gq = ngo_phred(1 - maxP);
+    c->dp = ih.total_count;
+    c->has_report = 1;                                        /* setCallReport when totalDepth > 0 */
+    memcpy(c->counts, ih.counts, sizeof(int) * (size_t)n);
+    memcpy(c->logc, ih.logc, sizeof(double) * (size_t)n * n);
+    free(ih.counts); free(ih.logc);
+    iscall_update_cn(c, n, ploidy);
+    if (40 > c->gq) { c->n_called = 0; c->gq = 0; iscall_update_cn(c, n, c->total_cn); }
+}
+
+/* the sample's span calls, PileupRecord.getAlleleCalls(span, sample.getReadGroups()) (:104-111): read groups in
+ * HashSet order, the pileup's order inside each */
+static void sample_span_calls(ngo_gen* G, int s, int pos, int span, ngo_alist* tmp, ngo_icalls* out) {
+    ngo_mvd* M = G->mvd;
+    tmp->n = 0;
+    for (int rank = 0; rank < M->n_rank[s]; rank++)
+        for (int k = 0; k < G->pileup.n; k++) {
+            ngo_aln* a = G->pileup.a[k];
+            if (a->rg < 0 || M->rg_sample[a->rg] != s || M->rg_rank[a->rg] != rank) continue;
+            alist_push(tmp, a);
+        }
+    pileup_calls(tmp->a, tmp->n, pos, span, out);
+}
+
+/* MultisampleVariantsDetector.genotypeVariant (:674-693) over an indel variant: every sample's call, the variant QS */
+static int mvd_genotype_indel_all(ngo_gen* G, int pos, const ngo_sv* alleles, ngo_iscall* calls) {
+    ngo_mvd* M = G->mvd;
+    ngo_alist tmp = {0};
+    ngo_icalls ic = {0};
+    int qs = 0;
+    const int span = (int)strlen(alleles->s[0]);
+    for (int s = 0; s < M->n_samples; s++) {
+        sample_span_calls(G, s, pos, span, &tmp, &ic);
+        genotype_indel_sample(alleles, &ic, G->het_rate, M->ploidy, G->p->max_base_qs, &calls[s]);
+        for (int i = 0; i < ic.n; i++) { free(ic.c[i].allele); free(ic.c[i].qual); }
+        ic.n = 0;
+        const ngo_iscall* c = &calls[s];
+        const int homref = c->n_called == 1 && c->called[0] == 0;
+        if (c->n_called > 0 && !homref && c->gq > qs) qs = c->gq;
+    }
+    icalls_free(&ic);
+    free(tmp.a);
+    return qs;
+}
+
+static int same_lengths(const ngo_sv* v) {                 /* SingleSampleVariantPileupListener.allelesSameLength, :339-345 */
+    for (int i = 1; i < v->n; i++) if (strlen(v->s[i]) != strlen(v->s[0])) return 0;
+    return 1;
+}
+
+/* discoverPopulationVariantWithSpan (:599-604) + discoverPopulationIndel (:616-634): 1 with the variant's alleles
+ * in *v (reference first), 0 for null */
+static int mvd_discover_indel(ngo_gen* G, int pos, const char* ref, int input_str, ngo_sv* v) {
+    ngo_mvd* M = G->mvd;
+    const int lref = (int)strlen(ref);
+    ngo_icalls calls = {0};
+    pileup_calls(G->pileup.a, G->pileup.n, pos, lref, &calls);
+    ngo_sv alleles = {0};
+    cluster_allele_calls(&calls, ref, G->p->max_base_qs, &alleles);
+    ngo_icounts ih;
+    icounts_run(&ih, &alleles, &calls, G->p->max_base_qs, 0.5);
+    /* createIndelVariantPool (SingleSampleVariantPileupListener.java:333-338) */
+    const int ok = alleles.n > 1 && ih.total_count > 0;
+    free(ih.counts); free(ih.logc);
+    icalls_free(&calls);
+    if (!ok) { sv_free(&alleles); return 0; }
+    ngo_iscall* sc = calloc((size_t)(M->n_samples ? M->n_samples : 1), sizeof(ngo_iscall));
+    while (alleles.n > 2) {
+        if (!input_str && same_lengths(&alleles)) { sv_free(&alleles); free(sc); return 0; }
+        const int qs = mvd_genotype_indel_all(G, pos, &alleles, sc);
+        int drop = qs < G->p->min_quality;
+        /* makeNewVariant (:642-656): a TreeSet of the reference and every sample's called alleles */
+        ngo_sv set = {0};
+        sv_push(&set, alleles.s[0], (int)strlen(alleles.s[0]));
+        for (int s = 0; s < M->n_samples; s++)
+            for (int i = 0; i < sc[s].n_called; i++) sv_push(&set, alleles.s[sc[s].called[i]], (int)strlen(alleles.s[sc[s].called[i]]));
+        for (int s = 0; s < M->n_samples; s++) iscall_free(&sc[s]);
+        if (drop) { sv_free(&set); sv_free(&alleles); free(sc); return 0; }
+        sv_sort_unique(&set);
+        if (set.n == alleles.n) { sv_free(&set); break; }
+        ngo_sv nv = {0};                                       /* SingleSampleVariantPileupListener.makeNewVariant, :346-359 */
+        sv_push(&nv, alleles.s[0], lref);
+        for (int i = 0; i < set.n; i++) if (strcmp(set.s[i], alleles.s[0]) != 0) sv_push(&nv, set.s[i], (int)strlen(set.s[i]));
+        sv_free(&set);
+        sv_free(&alleles);
+        alleles = nv;
+    }
+    free(sc);
+    *v = alleles;
+    return 1;
+}
+
+/* VCFRecord.createDefaultPopulationVCFRecord (vcf/VCFRecord.java:277-282, FORMAT DEF_FORMAT_ARRAY_NGSEP_NOSNV) +
+ * VCFFileWriter.printVCFRecord / printGenotypeInfo (:44-68,159-256) for an indel / STR variant */
+static void mvd_print_indel(ngo_gen* G, const char* seqName, int pos, const ngo_sv* v, int is_str, int qs, const ngo_iscall* calls) {
+    ngo_mvd* M = G->mvd;
+    FILE* out = G->out;
+    const int n = v->n, S = M->n_samples;
+    fprintf(out, "%s\t%d\t.\t%s\t", seqName, pos, v->s[0]);
+    if (n == 1) fprintf(out, ".");
+    for (int i = 1; i < n; i++) fprintf(out, "%s%s", i > 1 ? "," : "", v->s[i]);
+    fprintf(out, "\t%d\t.\t", qs);
+    /* DiversityStatistics.calculateDiversityStatistics(calls, false) (variants/DiversityStatistics.java:123-218) */
+    int* counts = calloc((size_t)n, sizeof(int));
+    int sum = 0, ng = 0, nhet = 0;
+    for (int s = 0; s < S; s++) {
+        const ngo_iscall* c = &calls[s];
+        if (c->n_called == 0) continue;
+        ng++;
+        if (c->n_called > 1) nhet++;
+        for (int i = 0; i < c->n_called; i++) { counts[c->called[i]] += c->acn[c->called[i]]; sum += c->acn[c->called[i]]; }
+    }
+    int ncalled = 0, minAC = 0;
+    for (int i = 0; i < n; i++) if (counts[i] > 0) { ncalled++; if (minAC == 0 || minAC > counts[i]) minAC = counts[i]; }
+    char buf[64];
+    fprintf(out, "NS=%d;AN=%d;AFS=", ng, ncalled);
+    for (int i = 0; i < n; i++) fprintf(out, "%s%d", i ? "," : "", counts[i]);
+    ngo_java_fmt2(ng > 0 ? (double)nhet / ng : 0.0, buf, sizeof buf);
+    fprintf(out, ";OH=%s", buf);
+    if (n == 2) { ngo_java_fmt2(ncalled < 2 ? 0.0 : (double)minAC / sum, buf, sizeof buf); fprintf(out, ";MAF=%s", buf); }
+    free(counts);
+    fprintf(out, ";TYPE=%s\tGT:PL:GQ:DP:ADP:ACN", is_str ? "STR" : "INDEL");
+    for (int s = 0; s < S; s++) {
+        const ngo_iscall* c = &calls[s];
+        fprintf(out, "\t");
+        if (c->n_called == 0) fprintf(out, M->ploidy > 1 ? "./." : ".");
+        else if (c->n_called == 1) { fprintf(out, "%d", c->called[0]); if (M->ploidy > 1) fprintf(out, "/%d", c->called[0]); }
+        else fprintf(out, "%d/%d", c->called[0], c->called[1]);
+        fprintf(out, ":");
+        for (int j = 0; j < n; j++)
+            for (int i = 0; i <= j; i++)
+                fprintf(out, "%s%d", (i > 0 || j > 0) ? "," : "", c->has_report ? (int)ngo_java_round(-10 * c->logc[i * n + j]) : 0);
+        fprintf(out, ":%d:%d:", c->gq, c->dp);
+        for (int i = 0; i < n; i++) fprintf(out, "%s%d", i ? "," : "", c->has_report ? c->counts[i] : 0);
+        fprintf(out, ":");
+        if (c->total_cn == 0) fprintf(out, ".");
+        else for (int j = 0; j < n; j++) fprintf(out, "%s%d", j ? "," : "", (c->n_called == 0 && j == 0) ? c->total_cn : c->acn[j]);
+    }
+    fprintf(out, "\n");
+}
+
+/* ==== test entry points (tests/test_oracle_indel_kat.py): the indel functions above on given inputs, checked there
+ * against an independent pure-Python restatement of the Java (tests/indel_restatement.py) ==== */
+static void t_calls(int m, const char* const* calls, const char* const* quals, ngo_icalls* out) {
+    out->n = 0;
+    for (int i = 0; i < m; i++) {
+        if (out->n == out->cap) { out->cap = out->cap ? 2 * out->cap : 16; out->c = realloc(out->c, sizeof(ngo_icall) * out->cap); }
+        ngo_icall* c = &out->c[out->n++];
+        c->allele = strdup(calls[i]);
+        c->qual = strdup(quals[i]);
+        c->len = (int)strlen(calls[i]);
+        c->neg = 0;
+    }
+}
+static void t_alleles(int n, const char* const* alleles, ngo_sv* v) { for (int i = 0; i < n; i++) sv_push(v, alleles[i], (int)strlen(alleles[i])); }
+
+/* CountsHelper.calculateCountsIndel: counts[n] and the n x n log-conditionals; returns totalCount */
+int ngo_t_indel_counts(int n, const char* const* alleles, int m, const char* const* calls, const char* const* quals,
+                       int max_base_qs, int* counts, double* logc) {
+    ngo_sv al = {0};
+    ngo_icalls ic = {0};
+    t_alleles(n, alleles, &al);
+    t_calls(m, calls, quals, &ic);
+    ngo_icounts h;
+    icounts_run(&h, &al, &ic, max_base_qs, 0.5);
+    memcpy(counts, h.counts, sizeof(int) * (size_t)n);
+    memcpy(logc, h.logc, sizeof(double) * (size_t)n * n);
+    const int t = h.total_count;
+    free(h.counts); free(h.logc);
+    sv_free(&al); icalls_free(&ic);
+    return t;
+}
+
+/* AlleleCallClustersBuilder.clusterAlleleCalls: the alleles joined by ',' (reference first); returns their number */
+int ngo_t_cluster(const char* ref, int m, const char* const* calls, const char* const* quals, int max_base_qs, char* out, int cap) {
+    ngo_icalls ic = {0};
+    t_calls(m, calls, quals, &ic);
+    ngo_sv al = {0};
+    cluster_allele_calls(&ic, ref, max_base_qs, &al);
+    int k = 0;
+    out[0] = 0;
+    for (int i = 0; i < al.n; i++) k += snprintf(out + k, (size_t)(cap > k ? cap - k : 0), "%s%s", i ? "," : "", al.s[i]);
+    const int n = al.n;
+    sv_free(&al); icalls_free(&ic);
+    return n;
+}
+
+/* callIndel with variant == null + the single-sample listener's filters: the record's fields
+ * "REF\tALT\tQS\tTYPE\tGT:PL:GQ:DP:ADP:ACN" in `out`; returns 1 when a call is kept */
+int ngo_t_call_indel(int n, const char* const* alleles, int m, const char* const* calls, const char* const* quals,
+                     int max_base_qs, double het, int is_str, int is_input_str, int min_quality, int ploidy, char* out, int cap) {
+    ngo_sv al = {0};
+    ngo_icalls ic = {0};
+    t_alleles(n, alleles, &al);
+    t_calls(m, calls, quals, &ic);
+    ngo_icounts h;
+    icounts_run(&h, &al, &ic, max_base_qs, 0.5);
+    ngo_indel_call c;
+    const int ok = call_indel(&h, &al, 1, is_str, is_input_str, het, min_quality, ploidy, &c);
+    out[0] = 0;
+    if (ok) {
+        char* buf = NULL; size_t len = 0;
+        FILE* f = open_memstream(&buf, &len);
+        print_indel_call(f, "s", &c, ploidy);
+        fclose(f);
+        snprintf(out, (size_t)cap, "%s", buf);
+        free(buf);
+        for (int i = 0; i < c.n; i++) free(c.alleles[i]);
+    }
+    free(h.counts); free(h.logc);
+    sv_free(&al); icalls_free(&ic);
+    return ok;
+}
+
+/* genotypeVariantSample over an indel variant (the population path): "GT:PL:GQ:DP:ADP:ACN" of the call */
+void ngo_t_genotype_indel_sample(int n, const char* const* alleles, int m, const char* const* calls, const char* const* quals,
+                                 int max_base_qs, double het, int ploidy, char* out, int cap) {
+    ngo_sv al = {0};
+    ngo_icalls ic = {0};
+    t_alleles(n, alleles, &al);
+    t_calls(m, calls, quals, &ic);
+    ngo_iscall c;
+    genotype_indel_sample(&al, &ic, het, ploidy, max_base_qs, &c);
+    int k = 0;
+    if (c.n_called == 0) k += snprintf(out + k, (size_t)(cap - k), ploidy > 1 ? "./." : ".");
+    else if (c.n_called == 1) k += snprintf(out + k, (size_t)(cap - k), ploidy > 1 ? "%d/%d" : "%d", c.called[0], c.called[0]);
+    else k += snprintf(out + k, (size_t)(cap - k), "%d/%d", c.called[0], c.called[1]);
+    k += snprintf(out + k, (size_t)(cap - k), ":");
+    for (int j = 0; j < n; j++)
+        for (int i = 0; i <= j; i++)
+            k += snprintf(out + k, (size_t)(cap - k), "%s%d", (i > 0 || j > 0) ? "," : "", c.has_report ? (int)ngo_java_round(-10 * c.logc[i * n + j]) : 0);
+    k += snprintf(out + k, (size_t)(cap - k), ":%d:%d:", c.gq, c.dp);
+    for (int i = 0; i < n; i++) k += snprintf(out + k, (size_t)(cap - k), "%s%d", i ? "," : "", c.has_report ? c.counts[i] : 0);
+    k += snprintf(out + k, (size_t)(cap - k), ":");
+    if (c.total_cn == 0) k += snprintf(out + k, (size_t)(cap - k), ".");
+    else for (int j = 0; j < n; j++) k += snprintf(out + k, (size_t)(cap - k), "%s%d", j ? "," : "", (c.n_called == 0 && j == 0) ? c.total_cn : c.acn[j]);
+    iscall_free(&c);
+    sv_free(&al); icalls_free(&ic);
+}
+
+/* ReadAlignment edits on an alignment given by its first position and CIGAR (NGSEP codes via parse_cigar):
+ * op 0 moveIndelStart(a1, a2), 1 realignStart(a1, a2, a3, a4), 2 realignEnd(a1, a2, a3, a4).  The new CIGAR (the
+ * alignment's codes written as SAM text, not collapsed), first and last go to out / *first / *last; returns
+ * moveIndelStart's result (1 for the others) */
+int ngo_t_edit(int op, const char* cigar, int first, int a1, int a2, int a3, int a4, char* out, int cap, int* first_out, int* last_out) {
+    ngo_aln a;
+    memset(&a, 0, sizeof a);
+    if (parse_cigar(cigar, &a.ops, &a.n_ops) != 0) return -1;
+    a.first = first;
+    int span = 0;
+    for (int i = 0; i < a.n_ops; i++) { if (a.ops[i] & 1) span += a.ops[i] / 8; if (a.ops[i] & 2) a.read_length += a.ops[i] / 8; }
+    a.last = first + span - 1;
+    update_allele_calls(&a);
+    int r = 1;
+    if (op == 0) r = aln_move_indel_start(&a, a1, a2);
+    else if (op == 1) aln_realign_start(&a, a1, a2, a3, a4);
+    else aln_realign_end(&a, a1, a2, a3, a4);
+    static const char kOps[] = "HDIMPNSX";
+    int k = 0;
+    out[0] = 0;
+    for (int i = 0; i < a.n_ops; i++) k += snprintf(out + k, (size_t)(cap > k ? cap - k : 0), "%d%c", a.ops[i] / 8, kOps[a.ops[i] & 7]);
+    *first_out = a.first;
+    *last_out = a.last;
+    free(a.ops); free(a.acl); free(a.indel);
+    return r;
+}
+
+/* MultisampleVariantsDetector.onPileup (:522-538) after the realigner set the pileup's span / STR / embedded flags */
+static void mvd_on_pileup_realign(ngo_gen* G, int pos, int span, int is_str, int is_new_str, int r_embedded) {
+    ngo_mvd* M = G->mvd;
+    const ngo_params* p = G->p;
+    const ngo_seq* sq = &G->g->s[G->cur_seq];
+    const int input_str = is_str && !is_new_str;
+    int embedded = r_embedded;
+    if (input_str) G->last_indel_end = pos + span - 1;        /* (no ">= lastIndelEnd" test here, unlike the single-sample listener) */
+    else if (pos <= G->last_indel_end) embedded = 1;
+    /* calculateReferenceAlleleDiscovery (SingleSampleVariantPileupListener.java:191-206) */
+    if (!p->call_embedded && embedded) return;
+    const int last = pos + span - 1;
+    if (pos < 1 || last > sq->len) return;
+    if (p->ignore_lowercase_ref && islower((unsigned char)sq->seq[pos - 1])) return;
+    const int lref = embedded ? 1 : span;
+    if (embedded) { is_str = 0; }
+    const char R = (char)toupper((unsigned char)sq->seq[pos - 1]);
+    ngo_counts pooled;
+    mvd_snv_counts(G, pos, G->pileup.a, G->pileup.n, &pooled);
+    /* discoverPopulationVariant (:573-584) */
+    if (lref > 1) {
+        int lr = 0;
+        char* ref = ref_upper(sq, pos, last, &lr);
+        ngo_sv v = {0};
+        const int got = mvd_discover_indel(G, pos, ref, input_str, &v);
+        free(ref);
+        if (got) {
+            ngo_iscall* sc = calloc((size_t)(M->n_samples ? M->n_samples : 1), sizeof(ngo_iscall));
+            const int qs = mvd_genotype_indel_all(G, pos, &v, sc);
+            if (!(qs == 0 || qs < p->min_quality)) {
+                mvd_print_indel(G, sq->name, pos, &v, is_str, qs, sc);
+                G->st->variants_called++;
+                G->last_indel_end = pos + (int)strlen(v.s[0]) - 1;   /* !variant.isSNV(): lastIndelEnd = variant.getLast() */
+            }
+            for (int s = 0; s < M->n_samples; s++) iscall_free(&sc[s]);
+            free(sc);
+            sv_free(&v);
+            return;
+        }
+        if (input_str) return;                                   /* no SNV fallback for an input STR (:605) */
+        /* (isNewSTR: setSTR(false), setNewSTR(false) -- the SNV fallback does not read them) */
+    }
+    ngo_pvar v;
+    if (!mvd_snv_variant(G, R, &pooled, &v)) return;
+    if (embedded) v.multisnv_type = 2;                         /* TYPE_EMBEDDED_SNV (:581) */
+    int qs = 0;
+    mvd_genotype_all(M, &v, G->het_rate, &qs);
+    if (qs == 0 || qs < p->min_quality) return;
+    mvd_print(G->out, sq->name, pos, NULL, &v, qs, M);
+    G->st->variants_called++;
+}
 
 static void push_call(ngo_gen* G, const ngo_call* c) {
     if (G->calls.n == G->calls.cap) { G->calls.cap = G->calls.cap ? 2 * G->calls.cap : 1024; G->calls.c = realloc(G->calls.c, sizeof(ngo_call) * G->calls.cap); }
@@ -1578,7 +2015,26 @@ static int process_current_position(ngo_gen* G) {
             if (G->pending.a[k]->first <= pos && G->pending.a[k]->last >= pos) numAlignments++;
         if (numAlignments > 0) {
             G->st->positions_genotyped++;
-            mvd_on_pileup(G, pos);
+            if (G->realign) {
+                /* IndelRealignerPileupListener.onPileup first (MultisampleVariantsDetector.java:449-450) */
+                G->pileup.n = 0;
+                for (int k = 0; k < G->pending.n; k++) {
+                    ngo_aln* a = G->pending.a[k];
+                    if (a->first <= pos && a->last >= pos) alist_push(&G->pileup, a);
+                }
+                int var_first = 0, var_last = 0, is_str = 0, is_new_str = 0, r_embedded = 0;
+                while (G->str_next < G->n_strs && G->strs[G->str_next].seq == G->cur_seq) {
+                    const ngo_strv* v = &G->strs[G->str_next];
+                    if (pos < v->first) break;
+                    if (pos <= v->last) { var_first = v->first; var_last = v->last; break; }
+                    G->str_next++;
+                }
+                const int span = realigner_on_pileup(&G->g->s[G->cur_seq], G->pileup.a, G->pileup.n, pos, var_first, var_last,
+                                                     &is_str, &is_new_str, &r_embedded);
+                mvd_on_pileup_realign(G, pos, span, is_str, is_new_str, r_embedded);
+            } else {
+                mvd_on_pileup(G, pos);
+            }
         }
         G->cur_pos++;
         return numAlignments > 0;
@@ -1961,7 +2417,9 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
     if (!multisample && !p->het_rate_set && p->ploidy == 1) G.het_rate = 1e-6;
     G.cov = cov;
     G.rac = rac;
-    G.realign = !multisample && !cov && !rac && !p->indel_passthrough && p->ploidy < 3 && !(p->known_vcf && p->known_vcf[0]);
+    /* the indel realigner: single-sample discovery at ploidy < 3, and MultisampleVariantsDetector at ploidy < 3 (its
+     * chain, :449-450); not with -knownVariants (the realigner's input variants) -- those runs stay pass-through */
+    G.realign = !cov && !rac && !p->indel_passthrough && p->ploidy < 3 && !(p->known_vcf && p->known_vcf[0]);
     if (p->known_vcf && p->known_vcf[0]) {
         if (load_known(p->known_vcf, &g, &G.known, &G.n_known) != NGO_OK) {
             fclose(in); if (out != stdout) fclose(out); if (dump) fclose(dump);

@@ -459,6 +459,26 @@ static void make_population(ngs_synth* s) {
             }
             if (carriers) s->truth.push_back({(int32_t)c, (int32_t)(i + 1), rb, kBases[ai], 1});
         }
+        // population indels (indel_rate > 0): 1-10 bp insertions / deletions from their own stream (the SNV population
+        // above is the same with and without them), allele frequency U(0.05, 0.95), per-sample allele bits
+        std::vector<int32_t> ipos;
+        std::vector<Indel> iev;
+        std::vector<uint8_t> igt;    // ipos.size() x ns
+        if (p.indel_rate > 0) {
+            Rng ri(base_seed ^ 0x5851F42D4C957F2Dull ^ (uint64_t)(first + (int)c + 1) * 0x9E3779B97F4A7C15ull);
+            for (int64_t i = 10; i + 20 < L; i++) {
+                if (ri.uniform() >= p.indel_rate) continue;
+                Indel d;
+                d.ins = ri.below(2) != 0;
+                d.len = 1 + (int)ri.below(10);
+                for (int k = 0; k < d.len; k++) d.seq.push_back(kBases[ri.below(4)]);
+                const double af = 0.05 + 0.9 * ri.uniform();
+                for (int k = 0; k < ns; k++) igt.push_back((uint8_t)((ri.uniform() < af ? 1 : 0) | (ri.uniform() < af ? 2 : 0)));
+                ipos.push_back((int32_t)(i + 1));
+                iev.push_back(d);
+                i += d.len + 5;                                   // no overlapping events
+            }
+        }
         const int rl = p.read_len;
         if (L < rl) continue;
         const int64_t nper = (int64_t)std::llround(p.depth * (double)L / rl);
@@ -474,10 +494,63 @@ static void make_population(ngs_synth* s) {
         });
         R.bases.reserve(R.bases.size() + starts.size() * (size_t)rl);
         R.quals.reserve(R.quals.size() + starts.size() * (size_t)rl);
+        const size_t cstart = R.size();
         for (const Gen& g : starts) {
             const int hap = (int)r.below(2);
             const int32_t flags = r.below(2) ? 16 : 0;
             const int64_t soff = (int64_t)R.bases.size();
+            if (p.indel_rate > 0) {
+                // the read walks sample g.sample's haplotype `hap`: its SNVs and its indel events (gen_read_indel's walk)
+                auto base_at = [&](int64_t pos) {
+                    char b = (char)std::toupper(ref[(size_t)(pos - 1)]);
+                    const size_t v = (size_t)(std::lower_bound(vpos.begin(), vpos.end(), (int32_t)pos) - vpos.begin());
+                    if (v < vpos.size() && vpos[v] == pos && ((vgt[v * ns + g.sample] >> hap) & 1)) b = valt[v];
+                    return b;
+                };
+                auto event_at = [&](int64_t pos) -> const Indel* {
+                    const size_t v = (size_t)(std::lower_bound(ipos.begin(), ipos.end(), (int32_t)pos) - ipos.begin());
+                    if (v < ipos.size() && ipos[v] == pos && ((igt[v * ns + g.sample] >> hap) & 1)) return &iev[v];
+                    return nullptr;
+                };
+                const int64_t coff = (int64_t)R.cigar.size();
+                int n = 0, nc = 0, lastop = -1;
+                auto op = [&](int code, int len) {
+                    if (len <= 0) return;
+                    if (nc > 0 && lastop == code) R.cigar.back() += len * 8;
+                    else if (nc < kIndelCigar) { R.cigar.push_back(len * 8 + code); nc++; lastop = code; }
+                };
+                auto emit = [&](char b) {
+                    int q = sample_quality(r, p.quality_model);
+                    if (r.uniform() < et[q]) {
+                        const char* pb = std::strchr(kBases, b);
+                        b = kBases[((pb ? (int)(pb - kBases) : 0) + 1 + (int)r.below(3)) % 4];
+                    }
+                    if (p.n_frac > 0 && r.uniform() < p.n_frac) { b = 'N'; q = 2; }
+                    R.bases.push_back(b);
+                    R.quals.push_back((char)(33 + q));
+                    n++;
+                };
+                int64_t i = g.pos;
+                if (const Indel* e = event_at(i)) if (!e->ins) i += e->len;     // a deletion at the start: the read starts after it
+                const int32_t start = (int32_t)i;
+                while (n < rl && i <= L) {
+                    const Indel* e = event_at(i);
+                    if (e && !e->ins && n > 0) { op(1, e->len); i += e->len; continue; }
+                    emit(base_at(i));
+                    op(3, 1);
+                    if (e && e->ins && n + e->len < rl) {
+                        for (char b : e->seq) emit(b);
+                        op(2, e->len);
+                    }
+                    i++;
+                }
+                while (n < rl) { emit('N'); op(3, 1); }
+                const bool dup = p.dup_rate > 0 && r.uniform() < p.dup_rate;
+                const int64_t no = readno++;
+                R.push((int32_t)c, start, flags, 60, g.sample, no, 0, coff, nc, soff, rl, 1);
+                if (dup) R.push((int32_t)c, start, flags, 60, g.sample, no, 'd', coff, nc, soff, rl, 1);
+                continue;
+            }
             size_t vi = (size_t)(std::lower_bound(vpos.begin(), vpos.end(), g.pos) - vpos.begin());
             for (int i = 0; i < rl; i++) {
                 const int32_t pos = g.pos + i;
@@ -500,6 +573,29 @@ static void make_population(ngs_synth* s) {
             const int64_t no = readno++;
             R.push((int32_t)c, g.pos, flags, 60, g.sample, no, 0, coff, 1, soff, rl, 1);
             if (dup) R.push((int32_t)c, g.pos, flags, 60, g.sample, no, 'd', coff, 1, soff, rl, 1);
+        }
+        if (p.indel_rate > 0) {
+            // a read that starts after a deletion moved: records in (first, last, sample) order, the order in which
+            // AlignmentsPileupGenerator merges the per-sample files (GenomicRegionComparator, ties to the lowest
+            // file index, :268-289), each sample's file sorted by (first, last)
+            const size_t m = R.size() - cstart;
+            std::vector<int32_t> last(m);
+            for (size_t k = 0; k < m; k++) {
+                int32_t span = 0;
+                for (int32_t j = 0; j < R.cig_n[cstart + k]; j++) {
+                    const int32_t v = R.cigar[(size_t)(R.cig_off[cstart + k] + j)];
+                    if ((v & 7) == 3 || (v & 7) == 1) span += v / 8;
+                }
+                last[k] = R.pos[cstart + k] + span - 1;
+            }
+            std::vector<size_t> idx(m);
+            std::iota(idx.begin(), idx.end(), (size_t)0);
+            std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {
+                if (R.pos[cstart + a] != R.pos[cstart + b]) return R.pos[cstart + a] < R.pos[cstart + b];
+                if (last[a] != last[b]) return last[a] < last[b];
+                return R.sample[cstart + a] < R.sample[cstart + b];
+            });
+            R.permute(cstart, idx);
         }
     }
 }
