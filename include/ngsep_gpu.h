@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define NGSEP_ABI_VERSION 7
+#define NGSEP_ABI_VERSION 8
 
 #define NGSEP_OK 0
 #define NGSEP_E_INVALID (-1)      /* bad argument / state */
@@ -84,7 +84,8 @@ typedef struct ngsep_params {
      * dump_all_positions records are always whole. */
     int32_t full_records;
     /* ABI 6: the indel realigner and indel / STR discovery (IndelRealignerPileupListener + VariantDiscovery-
-     * SNVQAlgorithm.callIndel, single-sample discovery at ploidy < 3 without -knownVariants, streamed runs).
+     * SNVQAlgorithm.callIndel, single-sample discovery at ploidy < 3 without -knownVariants, streamed runs; ABI 8:
+     * also MultisampleVariantsDetector at ploidy < 3 without -knownVariants, discoverPopulationIndel).
      * 0 (default): regions around alignments with indels are realigned and called here (indel / STR records,
      * TYPE=EMBEDDED SNVs with call_embedded); 1: pass-through -- no call inside those regions, which are returned
      * by ngsep_fetch_carved_regions for the caller's own indel path (the ABI 5 behaviour). */
@@ -149,9 +150,13 @@ typedef struct ngsep_site_out {
 typedef struct ngsep_popsite_out {
     int32_t seq_id;
     int32_t pos;             /* 1-based */
-    int8_t  n_alleles;       /* 2..4 */
+    int8_t  n_alleles;       /* 2..4 (0 for an indel / STR record) */
     int8_t  alleles[4];      /* DNA indexes (0=A..3=T): reference first, then alternatives in A,C,G,T order */
-    int8_t  multisnv_type;   /* 1: the pooled multi-allelic SNV kept all its alleles -> INFO TYPE=MULTISNV */
+    int8_t  multisnv_type;   /* 1: the pooled multi-allelic SNV kept all its alleles -> INFO TYPE=MULTISNV;
+                              * 2 (ABI 8): an SNV inside an indel / STR (-embeddedSNVs) -> TYPE=EMBEDDED;
+                              * 3 (ABI 8): an indel / STR record of the realigner's regions (discoverPopulationIndel,
+                              * MultisampleVariantsDetector.java:599-634): its alleles and sample calls are only in its
+                              * VCF line (ngsep_population_site_vcf_line); its calls[] entries are zeroed */
     int16_t qual;            /* variant QS: max GQ over decided non-reference sample calls (:674-693) */
     int16_t pad;
 } ngsep_popsite_out;
@@ -250,9 +255,10 @@ int ngsep_clear_sites(ngsep_ctx* ctx);
  * each indel event and calls indels.  Every admitted alignment with an I/D item opens a region
  * [first - R, last + indel bases + R], R = the largest alignment span + 100 (the reach of an event's
  * realignment: every alignment overlapping it), merged per sequence.  With params.indel_passthrough = 0
- * (ABI 6, the default for single-sample discovery at ploidy < 3 without -knownVariants in streamed runs)
- * the regions are realigned and called here: indel / STR records (is_call bit 3) and the SNVs of the
- * realigned alignments join the other calls, and no region is listed below.  Otherwise (pass-through, and
+ * (ABI 6, the default for single-sample discovery at ploidy < 3 without -knownVariants in streamed runs; ABI 8:
+ * MultisampleVariantsDetector at ploidy < 3 without -knownVariants, outside the staged measurement entry points)
+ * the regions are realigned and called here: indel / STR records (is_call bit 3; population records with
+ * multisnv_type 3) and the SNVs of the realigned alignments join the other calls, and no region is listed below.  Otherwise (pass-through, and
  * every other mode) no call is made inside a region; outside them the calls are the reference's; the regions
  * are returned here, in processing order, for the caller's own path (the JNI host runs the Java listener
  * chain on them): sequence ids, 1-based first and last positions.  n_out receives the number available. */
@@ -280,6 +286,10 @@ int ngsep_fetch_population_sites(ngsep_ctx* ctx, ngsep_popsite_out* sites, ngsep
                                  int64_t cap, int64_t* n_out);
 /* MultisampleVariantsDetector output: VCF header with the samples, then every fetched site */
 int ngsep_write_population_vcf(ngsep_ctx* ctx, const char* path);
+/* ABI 8: the VCF line of population site i (any record kind, indel / STR records included); returns its length,
+ * copies at most cap - 1 characters and a terminating 0 (VCFFileWriter.printVCFRecord of
+ * VCFRecord.createDefaultPopulationVCFRecord, vcf/VCFRecord.java:277-282) */
+int64_t ngsep_population_site_vcf_line(ngsep_ctx* ctx, int64_t i, char* buf, int64_t cap);
 /* path B of the multisample detector: `MultisampleVariantsDetector -r REF -o OUT.vcf BAM...`
  * (MultisampleVariantsDetector.main/run, :412-459): samples from the BAM headers' @RG SM tags,
  * files merged as AlignmentsPileupGenerator.processFiles does (:201-266, chooseNextAln :268-289) */

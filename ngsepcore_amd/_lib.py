@@ -171,6 +171,7 @@ SIGNATURES = {
     "ngsep_append_vcf_records": (ctypes.c_int, [_CTX, ctypes.c_char_p]),
     "ngsep_format_site": (ctypes.c_int64, [_CTX, P(NgsepSiteOut), ctypes.c_char_p, ctypes.c_int64]),
     "ngsep_site_vcf_line": (ctypes.c_int64, [_CTX, ctypes.c_int64, ctypes.c_char_p, ctypes.c_int64]),
+    "ngsep_population_site_vcf_line": (ctypes.c_int64, [_CTX, ctypes.c_int64, ctypes.c_char_p, ctypes.c_int64]),
     "ngsep_call_bam": (ctypes.c_int, [_CTX, ctypes.c_char_p, ctypes.c_char_p]),
     "ngsep_set_samples": (ctypes.c_int, [_CTX, ctypes.c_int32, P(ctypes.c_char_p), ctypes.c_int32, P(ctypes.c_int32),
                                          P(ctypes.c_int32)]),

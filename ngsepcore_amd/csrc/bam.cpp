@@ -1475,5 +1475,6 @@ extern "C" int ngsep_call_population_region_bams(ngsep_ctx* c, const char* const
     c->pop_calls.clear();
     c->pop_big.clear();
     c->pop_order.clear();
+    c->pop_text.clear();
     return rc;
 }

@@ -46,7 +46,7 @@ static int main_mvd(int argc, char** argv, int i) {
     ngsep_params p;
     ngsep_params_default(&p);
     p.multisample = 1;
-    const char *ref = nullptr, *outp = "variants.vcf", *known = nullptr;
+    const char *ref = nullptr, *outp = "variants.vcf", *known = nullptr, *strs = nullptr;
     int device = 0;
     std::vector<const char*> bams;
     for (; i < argc; i++) {
@@ -69,6 +69,8 @@ static int main_mvd(int argc, char** argv, int i) {
         else if (takes("-last")) p.query_last = std::atoi(v);
         else if (takes("-device")) device = std::atoi(v);
         else if (takes("-knownVariants")) known = v;    // MultisampleVariantsDetector.setKnownVariantsFile (:193-195)
+        else if (takes("-knownSTRs")) strs = v;         // the realigner's input STRs without -knownVariants (:439-446)
+        else if (!std::strcmp(a, "-embeddedSNVs")) p.call_embedded = 1;
         else if (!std::strcmp(a, "-psp")) p.print_sample_ploidy = 1;
         else if (!std::strcmp(a, "-p")) p.process_nonunique = 1;
         else if (!std::strcmp(a, "-s")) p.process_secondary = 1;
@@ -84,6 +86,7 @@ static int main_mvd(int argc, char** argv, int i) {
     int rc = ngsep_open(device, &p, &c);
     if (rc == NGSEP_OK) rc = ngsep_load_fasta(c, ref);
     if (rc == NGSEP_OK && known) rc = ngsep_set_known_variants(c, known);
+    else if (rc == NGSEP_OK && strs) rc = ngsep_set_known_strs(c, strs);
     if (rc == NGSEP_OK) rc = ngsep_call_population_bams(c, bams.data(), (int32_t)bams.size(), outp);
     if (rc != NGSEP_OK) { std::fprintf(stderr, "error %d: %s\n", rc, c ? ngsep_last_error(c) : "open failed"); if (c) ngsep_close(c); return 1; }
     ngsep_stats st;

@@ -565,11 +565,13 @@ static int stream_advance(ngsep_ctx* c, bool final);
 
 static bool streaming(const ngsep_ctx* c) { return !c->staging_mode && !c->params.coverage_stats && !c->params.multisample; }
 
-// the indel realigner runs here (realign.hpp) in streamed single-sample discovery at ploidy < 3 without input
-// variants (the reference's listener chain for findSNVS; SingleSampleVariantsDetector.java:896-931); elsewhere
-// its regions are carved out and returned (params.indel_passthrough)
+// the indel realigner runs here (realign.hpp) in streamed single-sample discovery and in MultisampleVariantsDetector
+// (run per sequence), at ploidy < 3 without input variants (the reference's listener chains:
+// SingleSampleVariantsDetector.java:896-931, MultisampleVariantsDetector.java:449-450); elsewhere its regions are
+// carved out and returned (params.indel_passthrough)
 static bool realign_active(const ngsep_ctx* c) {
-    return streaming(c) && !c->params.indel_passthrough && !c->params.relative_allele_counts && !c->params.dump_all_positions &&
+    const bool path = streaming(c) || (c->params.multisample && !c->staging_mode);
+    return path && !c->params.indel_passthrough && !c->params.relative_allele_counts && !c->params.dump_all_positions &&
            c->params.ploidy < 3 && c->known.empty();
 }
 
@@ -627,9 +629,26 @@ static void keep_raw(ngsep_ctx* c, size_t b0, size_t n, const int32_t* ent, cons
         const bool neg = (r.flags & 0x10) != 0;            // setBasesToIgnore5P/3P (ReadAlignment.java:613-644)
         rr.ignore_start = neg ? c->params.ignore3 : c->params.ignore5;
         rr.ignore_end = neg ? c->params.ignore5 : c->params.ignore3;
+        if (c->params.multisample) {                        // the read group's sample and its rank there
+            const bool in = r.rg >= 0 && r.rg < (int32_t)c->rg_sample.size();
+            rr.sample = (int16_t)(in ? c->rg_sample[(size_t)r.rg] : -1);
+            rr.rank = (uint8_t)(in && c->rg_sample[(size_t)r.rg] >= 0 ? c->rg_rank[(size_t)r.rg] : 0);
+        }
         st.kept.push_back(std::move(e));
     }
     while (st.kept_maybe_from < st.kept.size() && !st.kept[st.kept_maybe_from].maybe) st.kept_maybe_from++;
+    if (!streaming(c)) {
+        // a whole sequence is kept until its end (multisample): the reads no region can reach leave as they die
+        size_t dead = 0;
+        for (size_t k = st.kept_maybe_from; k < st.kept.size(); k++) dead += st.kept[k].dead ? 1 : 0;
+        if (dead > (1u << 14) && dead * 2 > st.kept.size() - st.kept_maybe_from) {
+            std::deque<std::remove_reference_t<decltype(st.kept)>::value_type> live;
+            for (auto& e : st.kept) if (!e.dead) live.push_back(std::move(e));
+            st.kept.swap(live);
+            st.kept_maybe_from = 0;
+            while (st.kept_maybe_from < st.kept.size() && !st.kept[st.kept_maybe_from].maybe) st.kept_maybe_from++;
+        }
+    }
 }
 
 // the realigner's regions (carve_indel_regions' geometry with the current R) that reach [lo, hi] -- merged, so a
@@ -674,6 +693,10 @@ static int flush_sequence(ngsep_ctx* c) {
         c->stream.last_indel_end = 0;                // SingleSampleVariantPileupListener.onSequenceStart (:186)
     } else {
         rc = stage_contig_reads(c, c->contig, !c->staging_mode);
+        c->stream.kept.clear();                      // (multisample: the realigner's alignments of the sequence)
+        c->stream.kept_maybe_from = 0;
+        c->stream.indel_pmax.clear();
+        c->stream.last_indel_end = 0;
     }
     c->contig.clear();
     c->cur_seq = -1;
@@ -685,6 +708,7 @@ static int flush_sequence(ngsep_ctx* c) {
 // IndelRealignerPileupListener.java:43), merged; the covered positions inside leave the genotyped count
 static void carve_indel_regions(ngsep_ctx* c, ContigReads& cr) {
     if (cr.indel_reads.empty()) return;
+    const bool replay = realign_active(c);              // multisample: the regions are replayed, not handed back
     const int64_t R = (int64_t)cr.max_span + 100;
     const int64_t len = (int64_t)c->seq_bases[(size_t)cr.seq_id].size();
     std::vector<std::pair<int64_t, int64_t>> iv;
@@ -701,6 +725,7 @@ static void carve_indel_regions(ngsep_ctx* c, ContigReads& cr) {
     if (c->params.query_seq[0]) { lo_q = std::max<int64_t>(lo_q, c->params.query_first); hi_q = std::min<int64_t>(hi_q, c->params.query_last); }
     int64_t inside = 0;
     size_t r0 = 0;
+    if (replay) return;
     for (const auto& cv : cr.carved) {
         const int64_t a = std::max<int64_t>(cv.first, lo_q), b = std::min<int64_t>(cv.second, hi_q);
         c->carved.push_back({cr.seq_id, {cv.first, cv.second}});
@@ -718,6 +743,8 @@ static void carve_indel_regions(ngsep_ctx* c, ContigReads& cr) {
     c->stats.carved_positions += inside;
 }
 
+static int run_population_regions(ngsep_ctx* c, const ContigReads& cr, size_t from);
+
 int stage_contig_reads(ngsep_ctx* c, ContigReads& cr, bool run_now) {
     if (cr.seq_id < 0) return NGSEP_OK;
     if (!c->params.coverage_stats) carve_indel_regions(c, cr);
@@ -733,7 +760,11 @@ int stage_contig_reads(ngsep_ctx* c, ContigReads& cr, bool run_now) {
     int rc = build_and_upload(c, one);
     if (rc != NGSEP_OK) return rc;
     double ms = 0;
+    const size_t from = c->pop_sites.size();
     rc = run_device(c, &ms);
+    // MultisampleVariantsDetector with the indel realigner: the regions (kept out of the run above) replayed here
+    if (rc == NGSEP_OK && c->params.multisample && realign_active(c) && !one[0].carved.empty())
+        rc = run_population_regions(c, one[0], from);
     device_release(c->dev);
     return rc;
 }
@@ -2324,6 +2355,189 @@ static int run_regions(ngsep_ctx* c, WindowJob* j, int64_t goff) {
     return NGSEP_OK;
 }
 
+// MultisampleVariantsDetector with the indel realigner (MultisampleVariantsDetector.java:449-450): the sequence's
+// realigner regions (carve_indel_regions' geometry; kept out of the sequence's run, which has just appended its records
+// to pop_sites from index `from`) are replayed on the host threads (realign.cpp, population mode: alignment edits, every
+// sample's span-1 columns, the span's population indel variant); the regions' positions are then genotyped by KPM from
+// those columns (a queue of every replayed position in a layout of its own), onPileup's span rules resolve each region
+// (resolve_population_region), and the region records join the sequence's records in position order.
+static int run_population_regions(ngsep_ctx* c, const ContigReads& cr, size_t from) {
+    const std::string& seq = c->seq_bases[(size_t)cr.seq_id];
+    const int S = (int)c->sample_ids.size(), S1 = S + 1;
+    auto& st = c->stream;
+    const size_t nr = cr.carved.size();
+    // every region's alignments, in admission (pending-list) order: the kept ones that overlap it, all of them
+    std::vector<std::vector<RawRead>> reads(nr);
+    {
+        std::vector<const std::remove_reference_t<decltype(st.kept)>::value_type*> live;
+        for (const auto& e : st.kept) if (!e.dead) live.push_back(&e);
+        size_t lo = 0;
+        for (size_t k = 0; k < nr; k++) {
+            const int64_t a = cr.carved[k].first, b = cr.carved[k].second;
+            while (lo < live.size() && (int64_t)live[lo]->first + cr.max_span < a) lo++;
+            for (size_t i = lo; i < live.size() && live[i]->first <= b; i++)
+                if (live[i]->last >= a) reads[k].push_back(live[i]->r);
+            const int64_t r0 = std::lower_bound(cr.first.begin(), cr.first.end(), (int32_t)std::max<int64_t>(INT32_MIN, a - cr.max_span)) - cr.first.begin();
+            size_t want = 0;
+            for (int64_t i = r0; i < (int64_t)cr.first.size() && cr.first[(size_t)i] <= b; i++) want += cr.last[(size_t)i] >= a ? 1 : 0;
+            if (want != reads[k].size())
+                return set_error(c, NGSEP_E_INVALID, "internal error: indel realigner region " + std::to_string(a) + "-" + std::to_string(b) +
+                                                     " lacks " + std::to_string((int64_t)want - (int64_t)reads[k].size()) + " alignments");
+        }
+    }
+    std::vector<RegionOut> outs(nr);
+    RealignParams rp;
+    rp.max_base_qs = c->params.max_base_qs;
+    rp.min_quality = c->params.min_quality;
+    rp.ploidy = c->params.ploidy;
+    rp.het_rate = c->het_rate;
+    rp.ignore_lowercase = c->params.ignore_lowercase_ref != 0;
+    rp.n_samples = S;
+    parallel_for((int64_t)nr, 1, [&](int64_t a, int64_t b) {
+        for (int64_t k = a; k < b; k++)
+            replay_region(seq, cr.carved[(size_t)k].first, cr.carved[(size_t)k].second, reads[(size_t)k], rp,
+                          (size_t)cr.seq_id < c->strs.size() ? &c->strs[(size_t)cr.seq_id] : nullptr, outs[(size_t)k]);
+    });
+    // KPM over the regions' positions: position v of the queue is virtual position v of a layout of its own (tiles of
+    // kPopTile positions, site-major columns as build_multi_layout lays them out), discovery mode (no input alleles)
+    std::vector<std::pair<uint32_t, uint32_t>> vpos;          // (region, index in its pos list) of virtual position v
+    for (size_t k = 0; k < nr; k++)
+        for (size_t i = 0; i < outs[k].pos.size(); i++) vpos.push_back({(uint32_t)k, (uint32_t)i});
+    const int64_t V = (int64_t)vpos.size();
+    std::vector<int64_t> at_site((size_t)V, -1);             // v -> index of its KPM site (-1: none written)
+    const ngsep_popsite_out* sites = nullptr;
+    int64_t nsites = 0;
+    if (V > 0) {
+        Staged rs;
+        rs.single = false;
+        rs.known = true;                                       // the queue is given (no KTM / KQN) ...
+        rs.n_samples = S;
+        rs.tile = kPopTile;
+        rs.g_len = ((V + kRunAlign - 1) / kRunAlign) * kRunAlign;
+        rs.max_span = 1;
+        rs.h_ref.assign((size_t)rs.g_len, 0);
+        const int64_t ntile = rs.g_len / kPopTile;
+        rs.h_prow.assign((size_t)ntile * S1, 0);
+        auto col = [&](int64_t v, int s1, const uint8_t** p) -> uint32_t {
+            const RegionOut& o = outs[vpos[(size_t)v].first];
+            const RegionPos& q = o.pos[vpos[(size_t)v].second];
+            const uint32_t b0 = o.poff[(size_t)(q.pcol + s1)], b1 = o.poff[(size_t)(q.pcol + s1 + 1)];
+            *p = o.pcodes.data() + b0;
+            return b1 - b0;
+        };
+        for (int64_t v = 0; v < V; v++)
+            for (int s1 = 0; s1 < S1; s1++) {
+                const uint8_t* p;
+                const uint32_t n = col(v, s1, &p);
+                if (n > 65535) return set_error(c, NGSEP_E_UNSUPPORTED, "more than 65535 calls of one sample at one position");
+                uint16_t& r = rs.h_prow[(size_t)(v / kPopTile) * S1 + s1];
+                r = std::max<uint16_t>(r, (uint16_t)n);
+            }
+        rs.h_pboff.assign((size_t)ntile * S1 + 1, 0);
+        std::vector<int64_t> stride((size_t)ntile, 0);
+        int64_t po = 0;
+        for (int64_t t = 0; t < ntile; t++) {
+            int64_t so = 0;
+            for (int s1 = 0; s1 < S1; s1++) { rs.h_pboff[(size_t)t * S1 + s1] = po + so; so += rs.h_prow[(size_t)t * S1 + s1]; }
+            stride[(size_t)t] = so;
+            po += so * kPopTile;
+        }
+        rs.h_pboff.back() = po;
+        rs.ppile_bytes = po;
+        rs.h_ppile.reset(new (std::nothrow) uint8_t[(size_t)po + 64]);
+        if (!rs.h_ppile) return set_error(c, NGSEP_E_DEVICE, "host memory for the regions' population pile");
+        std::memset(rs.h_ppile.get(), 0, (size_t)po + 64);
+        for (int64_t v = 0; v < V; v++) {
+            const int64_t t = v / kPopTile;
+            for (int s1 = 0; s1 < S1; s1++) {
+                const uint8_t* p;
+                const uint32_t n = col(v, s1, &p);
+                if (n) std::memcpy(rs.h_ppile.get() + rs.h_pboff[(size_t)t * S1 + s1] + (v - t * kPopTile) * stride[(size_t)t], p, n);
+            }
+            const RegionOut& o = outs[vpos[(size_t)v].first];
+            const RegionPos& q = o.pos[vpos[(size_t)v].second];
+            rs.h_forced.push_back((int32_t)v);                 // ... of discovery entries (no 0x400: createSNVVariantPool)
+            rs.h_forced.push_back(q.blocked ? 0 : (int32_t)ref_code(c, seq[(size_t)q.pos - 1]));
+        }
+        std::string err;
+        if (!ensure_device(c, err) || device_upload(c->dev, rs, err) != 0) return set_error(c, NGSEP_E_DEVICE, err);
+        LikTables t;
+        GenotypeParams gp;
+        compute_tables(c, &t, &gp);
+        const ngsep_sample_call* calls = nullptr;
+        double a = 0, b = 0, tot = 0;
+        int64_t ncand = 0;
+        if (device_run_multi(c->dev, rs, t, gp, S, c->params.min_allele_depth_freq, c->params.ploidy, &sites, &calls, &nsites,
+                             &a, &b, &tot, &ncand, err) != 0)
+            return set_error(c, NGSEP_E_DEVICE, err);
+        for (int64_t i = 0; i < nsites; i++) at_site[(size_t)sites[i].seq_id] = i;   // (seq_id: the queue index)
+    }
+    // onPileup's rules, region by region (lastIndelEnd carried along the sequence)
+    std::vector<int64_t> src;                                  // the kept SNV sites (KPM order), in output order
+    std::vector<ngsep_popsite_out> add;
+    std::vector<int64_t> add_text;                             // per added record: pop_text index (-1: an SNV site)
+    std::vector<uint8_t> has;
+    std::vector<RegionDecision> dec;
+    int64_t v0 = 0;
+    int32_t lie = 0;
+    for (size_t k = 0; k < nr; k++) {
+        const RegionOut& o = outs[k];
+        has.assign(o.pos.size(), 0);
+        for (size_t i = 0; i < o.pos.size(); i++) has[i] = at_site[(size_t)(v0 + (int64_t)i)] >= 0;
+        resolve_population_region(o, has, c->params.call_embedded != 0, &lie, dec);
+        size_t pi = 0;
+        for (const RegionDecision& d : dec) {
+            while (o.pos[pi].pos != d.pos) pi++;
+            ngsep_popsite_out r;
+            std::memset(&r, 0, sizeof r);
+            if (d.kind == 1) {
+                const int64_t si = at_site[(size_t)(v0 + (int64_t)pi)];
+                r = sites[si];
+                if (d.embedded) r.multisnv_type = 2;           // TYPE_EMBEDDED_SNV (MultisampleVariantsDetector.java:581)
+                src.push_back(si);
+                add_text.push_back(-1);
+            } else {
+                const PopIndel& pi2 = o.pindels[(size_t)d.idx];
+                r.n_alleles = 0;
+                r.multisnv_type = 3;                           // an indel / STR record: its text in pop_text
+                r.qual = (int16_t)pi2.qs;
+                for (int q = 0; q < 4; q++) r.alleles[q] = -1;
+                add_text.push_back((int64_t)c->pop_text.size());
+                c->pop_text.push_back(pi2.line);
+            }
+            r.seq_id = cr.seq_id;
+            r.pos = d.pos;
+            add.push_back(r);
+        }
+        v0 += (int64_t)o.pos.size();
+    }
+    // the SNV records' calls, gathered on the device into the call store (as run_device_multi's)
+    std::string err;
+    const size_t cfrom = c->pop_calls.size(), blk0 = cfrom / (size_t)std::max(S, 1);
+    if (!src.empty()) {
+        c->pop_calls.resize(cfrom + src.size() * (size_t)S);
+        if (device_fetch_calls_ordered(c->dev, src.data(), (int64_t)src.size(), c->pop_calls.data() + cfrom, &c->pop_big, err) != 0)
+            return set_error(c, NGSEP_E_DEVICE, err);
+    }
+    size_t ks = 0;
+    for (size_t i = 0; i < add.size(); i++) {
+        c->pop_sites.push_back(add[i]);
+        c->pop_order.push_back(add_text[i] >= 0 ? add_text[i] : (int64_t)(blk0 + ks++));
+    }
+    c->stats.sites_called += (int64_t)add.size();
+    // the sequence's records in position order (the region positions were kept out of its run: no position twice)
+    const size_t n = c->pop_sites.size() - from;
+    std::vector<size_t> ord(n);
+    for (size_t i = 0; i < n; i++) ord[i] = i;
+    std::stable_sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return c->pop_sites[from + x].pos < c->pop_sites[from + y].pos; });
+    std::vector<ngsep_popsite_out> ps(n);
+    std::vector<int64_t> po(n);
+    for (size_t i = 0; i < n; i++) { ps[i] = c->pop_sites[from + ord[i]]; po[i] = c->pop_order[from + ord[i]]; }
+    std::copy(ps.begin(), ps.end(), c->pop_sites.begin() + (ptrdiff_t)from);
+    std::copy(po.begin(), po.end(), c->pop_order.begin() + (ptrdiff_t)from);
+    return NGSEP_OK;
+}
+
 // java.lang.Math.round + PhredScoreHelper.calculatePhredScore (math/PhredScoreHelper.java:31-40)
 int64_t java_round(double x) {
     if (std::isnan(x)) return 0;
@@ -2890,8 +3104,10 @@ extern "C" int ngsep_set_known_strs(ngsep_ctx* c, const char* path) {
     c->strs.clear();
     if (!path || !path[0]) return NGSEP_OK;
     if (c->seq_names.empty()) return set_error(c, NGSEP_E_INVALID, "load the reference before the known STRs");
-    if (c->params.coverage_stats || c->params.relative_allele_counts || c->params.multisample)
-        return set_error(c, NGSEP_E_INVALID, "known STRs are an option of SingleSampleVariantsDetector only");
+    // (an option of both variant detectors: SingleSampleVariantsDetector.findSNVS :906-912, MultisampleVariantsDetector.run
+    // :439-446 -- in both the indel realigner's input variants)
+    if (c->params.coverage_stats || c->params.relative_allele_counts)
+        return set_error(c, NGSEP_E_INVALID, "known STRs are an option of the variant detectors only");
     std::FILE* f = std::fopen(path, "r");
     if (!f) return set_error(c, NGSEP_E_IO, std::string("cannot read ") + path);
     std::unordered_map<std::string, int32_t> idx;
@@ -3169,6 +3385,7 @@ extern "C" int ngsep_run_staged(ngsep_ctx* c, double* elapsed_ms) {
     c->pop_calls.clear();
     c->pop_big.clear();
     c->pop_order.clear();
+    c->pop_text.clear();
     c->stats.sites_called = 0;
     return run_device(c, elapsed_ms);
 }
@@ -3223,6 +3440,7 @@ extern "C" int ngsep_collect_staged(ngsep_ctx* c, double* elapsed_ms) {
         c->pop_calls.clear();
         c->pop_big.clear();
         c->pop_order.clear();
+        c->pop_text.clear();
         c->stats.sites_called = 0;
         const ngsep_popsite_out* sites = nullptr;
         int64_t n = 0, ncand = 0;
@@ -3331,7 +3549,12 @@ extern "C" int ngsep_fetch_population_sites(ngsep_ctx* c, ngsep_popsite_out* sit
     if (sites && k) std::memcpy(sites, c->pop_sites.data(), (size_t)k * sizeof(ngsep_popsite_out));
     if (calls && k && S)
         for (size_t i = 0; i < (size_t)k; i++)
-            for (size_t j = 0; j < S; j++)
+            for (size_t j = 0; j < S; j++) {
+                if (c->pop_sites[i].multisnv_type == 3) {     // an indel / STR record: ngsep_population_site_vcf_line
+                    std::memset(&calls[i * S + j], 0, sizeof(ngsep_sample_call));
+                    continue;
+                }
                 calls[i * S + j] = expand_call(c->pop_calls.data()[(size_t)c->pop_order[i] * S + j], c->pop_big.data());
+            }
     return NGSEP_OK;
 }

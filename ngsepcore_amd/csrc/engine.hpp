@@ -756,6 +756,8 @@ struct ngsep_ctx {
     ngsep::PinnedStore<ngsep::PopCall32> pop_calls;     // pop_sites.size() x n_samples (compact; expand_call)
     ngsep::PinnedStore<ngsep_sample_call> pop_big;      // the calls a PopCall32 cannot hold, whole
     std::vector<int64_t> pop_order;                     // site i's calls: pop_calls[pop_order[i] * n_samples ..]
+                                                        // (an indel / STR record, multisnv_type 3: pop_text[pop_order[i]])
+    std::vector<std::string> pop_text;                  // indel / STR population records (realigner regions), no sequence name
     ngsep_stats stats{};
 };
 

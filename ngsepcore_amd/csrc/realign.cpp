@@ -72,6 +72,8 @@ struct Aln {
     int32_t ignore_start, ignore_end;
     std::vector<int16_t> acl;            // alleleCallLength per read position
     std::vector<IndelEv> indels;         // indelCalls (TreeMap by refPos)
+    int16_t sample = -1;                 // multisample: sample and read-group rank (RawRead)
+    uint8_t rank = 0;
 
     // updateAlleleCallsInfo (ReadAlignment.java:747-834)
     void update() {
@@ -695,20 +697,26 @@ inline double log_sum(double a, double b) {
     return a + std::log10(1 + std::pow(10.0, b - a));
 }
 
-// calculateCountsIndel + updateCountsIndel (CountsHelper.java:96-105,253-304), calculateLogCond (:384-396), then
-// callIndel (VariantDiscoverySNVQAlgorithm.java:265-361) and the listener's filters; the VCF fields of a kept call
-bool genotype_indel(const std::vector<std::string>& alleles, const std::vector<SpanCall>& calls, int pos, bool is_str,
-                    bool is_input_str, const RealignParams& p, IndelCall* out) {
+// CountsHelper over indel alleles: calculateCountsIndel + updateCountsIndel (CountsHelper.java:96-105,253-304) with
+// calculateLogCond (:384-396); logc is n x n row-major (not symmetric)
+struct IndelCounts {
+    int n = 0, total = 0;
+    std::vector<int> counts;
+    std::vector<double> logc;
+};
+void indel_counts(const std::vector<std::string>& alleles, const std::vector<SpanCall>& calls, int max_base_qs, IndelCounts& h) {
     const int n = (int)alleles.size();
-    const int maxBaseQS = (int8_t)p.max_base_qs > 0 ? (int8_t)p.max_base_qs : 30;
+    const int maxBaseQS = (int8_t)max_base_qs > 0 ? (int8_t)max_base_qs : 30;
     const int f = (int)java_round(0.5 * kNumFreq);                     // (:256: 501, not 500)
     const double af0 = std::log10((double)f / (kNumFreq - 1)), af1 = std::log10(1 - (double)f / (kNumFreq - 1));
     const double E = std::log10(0.0001);                                  // DEF_LOG_ERROR_PROB_INDEL (:48)
-    std::vector<int> counts((size_t)n, 0);
-    std::vector<double> logc((size_t)n * n, 0.0), lca((size_t)n);
-    int total = 0;
+    h.n = n;
+    h.total = 0;
+    h.counts.assign((size_t)n, 0);
+    h.logc.assign((size_t)n * n, 0.0);
+    std::vector<double> lca((size_t)n);
     for (const SpanCall& c : calls) {
-        total++;
+        h.total++;
         int index = -1;
         for (int i = 0; i < n; i++) if (alleles[(size_t)i] == c.allele) { index = i; break; }
         int bestIndex = -1;
@@ -730,26 +738,30 @@ bool genotype_indel(const std::vector<std::string>& alleles, const std::vector<S
         }
         if (index >= 0 && bestIndex >= 0 && bestIndex != index) index = std::min(index, bestIndex);
         else if (index < 0 && bestIndex >= 0) index = bestIndex;
-        if (index >= 0) counts[(size_t)index]++;
+        if (index >= 0) h.counts[(size_t)index]++;
         for (int i = 0; i < n; i++) {
-            logc[(size_t)(i * n + i)] += lca[(size_t)i];
+            h.logc[(size_t)(i * n + i)] += lca[(size_t)i];
             for (int j = 0; j < n; j++) {
                 if (i == j) continue;
-                double& v = logc[(size_t)(i * n + j)];
+                double& v = h.logc[(size_t)(i * n + j)];
                 if (j == index) v += log_sum(af0 + lca[(size_t)index], af1 + E);
                 else if (i == index) v += log_sum(af1 + lca[(size_t)index], af0 + E);
                 else v += E;
             }
         }
     }
-    if (total == 0) return false;
-    // getPosteriorProbabilities (:410-443)
-    const double lph = std::log10(p.het_rate / (n * (n - 1))), lpo = std::log10((1 - p.het_rate) / n);
-    std::vector<double> ev((size_t)n * n), post((size_t)n * n);
+}
+
+// getPosteriorProbabilities (CountsHelper.java:410-443) + calculatePosteriorProbabilities (:472-495) over n alleles
+void indel_posteriors(const IndelCounts& h, double het, std::vector<double>& post) {
+    const int n = h.n;
+    const double lph = std::log10(het / (n * (n - 1))), lpo = std::log10((1 - het) / n);
+    std::vector<double> ev((size_t)n * n);
+    post.assign((size_t)n * n, 0.0);
     int k = 0;
     for (int i = 0; i < n; i++) {
-        ev[(size_t)k++] = logc[(size_t)(i * n + i)] + lpo;
-        for (int j = 0; j < n; j++) if (i != j) ev[(size_t)k++] = logc[(size_t)(i * n + j)] + lph;
+        ev[(size_t)k++] = h.logc[(size_t)(i * n + i)] + lpo;
+        for (int j = 0; j < n; j++) if (i != j) ev[(size_t)k++] = h.logc[(size_t)(i * n + j)] + lph;
     }
     double logMax = 1, tot = 0;
     for (double v : ev) if (logMax > 0 || logMax < v) logMax = v;
@@ -759,15 +771,35 @@ bool genotype_indel(const std::vector<std::string>& alleles, const std::vector<S
         post[(size_t)(i * n + i)] = ev[(size_t)k++] / tot;
         for (int j = 0; j < n; j++) if (i != j) post[(size_t)(i * n + j)] = ev[(size_t)k++] / tot;
     }
-    // getIndexesMaxGenotype(post, 0) (:223-243)
-    int im0 = 0, im1 = 0;
+}
+
+// getIndexesMaxGenotype(post, 0) (VariantDiscoverySNVQAlgorithm.java:223-243)
+void max_genotype(const std::vector<double>& post, int n, int* im0, int* im1) {
+    *im0 = *im1 = 0;
     double probMax = post[0];
     for (int i = 0; i < n; i++)
         for (int j = i; j < n; j++) {
             double gp = post[(size_t)(i * n + j)];
             if (i != j) gp += post[(size_t)(j * n + i)];
-            if (gp > probMax + 0.01) { probMax = gp; im0 = i; im1 = j; }
+            if (gp > probMax + 0.01) { probMax = gp; *im0 = i; *im1 = j; }
         }
+}
+
+// calculateCountsIndel + callIndel (VariantDiscoverySNVQAlgorithm.java:265-361) with variant == null and the
+// listener's filters; the VCF fields of a kept call
+bool genotype_indel(const std::vector<std::string>& alleles, const std::vector<SpanCall>& calls, int pos, bool is_str,
+                    bool is_input_str, const RealignParams& p, IndelCall* out) {
+    const int n = (int)alleles.size();
+    IndelCounts h;
+    indel_counts(alleles, calls, p.max_base_qs, h);
+    const std::vector<int>& counts = h.counts;
+    const std::vector<double>& logc = h.logc;
+    const int total = h.total;
+    if (total == 0) return false;
+    std::vector<double> post;
+    indel_posteriors(h, p.het_rate, post);
+    int im0 = 0, im1 = 0;
+    max_genotype(post, n, &im0, &im1);
     int idx[3], na = 0;
     bool lengthChange = false;
     const size_t lref = alleles[0].size();
@@ -834,6 +866,205 @@ bool genotype_indel(const std::vector<std::string>& alleles, const std::vector<S
     return true;
 }
 
+// ---- MultisampleVariantsDetector over a region (population mode) ----
+// one sample's call of an indel variant (a CalledGenomicVariantImpl of SingleSampleVariantPileupListener
+// .genotypeVariantSample, :361-391)
+struct SampleIndelCall {
+    int n_called = 0, called[2] = {0, 0}, gq = 0, dp = 0, total_cn = 0;
+    bool report = false;
+    std::vector<int> acn;
+};
+
+// CalledGenomicVariantImpl.updateAllelesCopyNumberFromCounts (variants/CalledGenomicVariantImpl.java:228-282)
+void update_cn(SampleIndelCall& c, const std::vector<int>& counts, int total) {
+    c.total_cn = total;
+    std::fill(c.acn.begin(), c.acn.end(), 0);
+    if (c.n_called == 0) return;
+    if (c.n_called == 1 && c.called[0] == 0) { c.acn[0] = total; return; }
+    const int nc = c.n_called;
+    if (total <= nc) { for (int i = 0; i < nc; i++) c.acn[(size_t)c.called[i]] = 1; return; }
+    if (!c.report) {
+        const int def = total / nc;
+        for (int i = 0; i < nc; i++) c.acn[(size_t)c.called[i]] = def;
+        c.acn[(size_t)c.called[0]] += total - def * nc;
+        return;
+    }
+    int rc[2] = {0, 0}, tr = 0;
+    for (int i = 0; i < nc; i++) { rc[i] = counts[(size_t)c.called[i]]; if (rc[i] == 0) rc[i] = 1; tr += rc[i]; }
+    int tc = 0;
+    for (int i = 0; i < nc; i++) {
+        const int64_t r = java_round((double)total * rc[i] / tr);
+        c.acn[(size_t)c.called[i]] = std::max(1, (int)(int16_t)r);
+        tc += c.acn[(size_t)c.called[i]];
+    }
+    if (tc < total) c.acn[(size_t)c.called[0]] += total - tc;
+    else {
+        int ex = tc - total;
+        for (int i = nc - 1; ex > 0 && i >= 0; i--) {
+            int& v = c.acn[(size_t)c.called[i]];
+            const int rm = std::min(ex, v - 1);
+            v -= rm;
+            ex -= rm;
+        }
+    }
+}
+
+// the sample's span calls: PileupRecord.getAlleleCalls(span, sample.getReadGroups()) (:104-111) -- read groups in
+// their HashSet order (rank), the pileup's order inside each
+void sample_span_calls(const std::vector<Aln*>& pileup, int s, int pos, int span, std::vector<Aln*>& tmp, std::vector<SpanCall>& out) {
+    tmp.clear();
+    int maxrank = -1;
+    for (const Aln* a : pileup) if (a->sample == s) maxrank = std::max<int>(maxrank, a->rank);
+    for (int r = 0; r <= maxrank; r++)
+        for (Aln* a : pileup) if (a->sample == s && a->rank == r) tmp.push_back(a);
+    span_calls(tmp, pos, span, out);
+}
+
+// MultisampleVariantsDetector.genotypeVariant (:674-693) over an indel variant: genotypeVariantSample for every
+// sample with a fresh listener (minQuality DEF_MIN_QUALITY 40): calculateCountsIndel over the variant's alleles,
+// callIndel with the variant given (the maximum genotype's indexes taken as they are, :335-345),
+// updateAllelesCopyNumberFromCounts(ploidy), makeUndecided below 40 (CalledGenomicVariantImpl.java:320-325).
+// Returns the variant QS: the largest GQ of a decided, non-homozygous-reference call.
+int genotype_indel_population(const std::vector<std::string>& alleles, const std::vector<Aln*>& pileup, int pos,
+                              const RealignParams& p, std::vector<SampleIndelCall>& calls, std::vector<IndelCounts>& helpers) {
+    const int n = (int)alleles.size(), S = p.n_samples;
+    const int span = (int)alleles[0].size();
+    calls.assign((size_t)S, SampleIndelCall());
+    helpers.assign((size_t)S, IndelCounts());
+    std::vector<Aln*> tmp;
+    std::vector<SpanCall> sc;
+    std::vector<double> post;
+    int qs = 0;
+    for (int s = 0; s < S; s++) {
+        SampleIndelCall& c = calls[(size_t)s];
+        IndelCounts& h = helpers[(size_t)s];
+        c.acn.assign((size_t)n, 0);
+        sample_span_calls(pileup, s, pos, span, tmp, sc);
+        indel_counts(alleles, sc, p.max_base_qs, h);
+        if (h.total == 0) {                      // new CalledGenomicVariantImpl(variant, new byte[0]) (callIndel :274-277)
+            update_cn(c, h.counts, p.ploidy);
+            continue;
+        }
+        indel_posteriors(h, p.het_rate, post);
+        int im0 = 0, im1 = 0;
+        max_genotype(post, n, &im0, &im1);
+        if (im0 > 100 || im1 > 100) c.n_called = 0;                      // GenomicVariant.MAX_NUM_ALLELES
+        else if (im1 != im0) { c.n_called = 2; c.called[0] = im0; c.called[1] = im1; }
+        else { c.n_called = 1; c.called[0] = im0; }
+        double maxP = post[(size_t)(im0 * n + im1)];
+        if (im0 != im1) maxP += post[(size_t)(im1 * n + im0)];
+        c.gq = java_phred(1 - maxP);
+        c.dp = h.total;
+        c.report = true;                                                  // setCallReport (totalDepth > 0)
+        update_cn(c, h.counts, p.ploidy);
+        if (40 > c.gq) { c.n_called = 0; c.gq = 0; update_cn(c, h.counts, c.total_cn); }
+        const bool homref = c.n_called == 1 && c.called[0] == 0;
+        if (c.n_called > 0 && !homref && c.gq > qs) qs = c.gq;
+    }
+    return qs;
+}
+
+// DecimalFormat("##0.0#") (main/io/ParseUtils.java:29): HALF_EVEN on the exact binary value
+void app_fmt2(std::string& o, double x) {
+    const double q = x * 100.0, err = std::fma(x, 100.0, -q);
+    const double k = std::floor(q), fr = q - k;
+    long long v = (long long)k;
+    if (fr > 0.5 || (fr == 0.5 && (err > 0 || (err == 0 && (v & 1))))) v++;
+    char b[48];
+    if (v % 10 == 0) std::snprintf(b, sizeof b, "%lld.%lld", v / 100, (v % 100) / 10);
+    else std::snprintf(b, sizeof b, "%lld.%02lld", v / 100, v % 100);
+    o += b;
+}
+
+// VCFRecord.createDefaultPopulationVCFRecord (vcf/VCFRecord.java:277-282: FORMAT DEF_FORMAT_ARRAY_NGSEP_NOSNV, INFO
+// from DiversityStatistics.calculateDiversityStatistics(calls, false), variants/DiversityStatistics.java:123-218) as
+// VCFFileWriter.printVCFRecord / printGenotypeInfo write it (:44-68,159-256); without the sequence name
+void format_population_indel(int pos, const std::vector<std::string>& alleles, bool is_str, int qs,
+                             const std::vector<SampleIndelCall>& calls, const std::vector<IndelCounts>& helpers, int ploidy,
+                             std::string& o) {
+    const int n = (int)alleles.size(), S = (int)calls.size();
+    o.clear();
+    o += std::to_string(pos); o += "\t.\t"; o += alleles[0]; o += '\t';
+    if (n == 1) o += '.';
+    for (int i = 1; i < n; i++) { if (i > 1) o += ','; o += alleles[(size_t)i]; }
+    o += '\t'; o += std::to_string(qs); o += "\t.\t";
+    std::vector<int> counts((size_t)n, 0);
+    int sum = 0, ng = 0, nhet = 0;
+    for (const SampleIndelCall& c : calls) {
+        if (c.n_called == 0) continue;
+        ng++;
+        if (c.n_called > 1) nhet++;
+        for (int i = 0; i < c.n_called; i++) { counts[(size_t)c.called[i]] += c.acn[(size_t)c.called[i]]; sum += c.acn[(size_t)c.called[i]]; }
+    }
+    int ncalled = 0, minAC = 0;
+    for (int i = 0; i < n; i++) if (counts[(size_t)i] > 0) { ncalled++; if (minAC == 0 || minAC > counts[(size_t)i]) minAC = counts[(size_t)i]; }
+    o += "NS="; o += std::to_string(ng); o += ";AN="; o += std::to_string(ncalled); o += ";AFS=";
+    for (int i = 0; i < n; i++) { if (i) o += ','; o += std::to_string(counts[(size_t)i]); }
+    o += ";OH="; app_fmt2(o, ng > 0 ? (double)nhet / ng : 0.0);
+    if (n == 2) { o += ";MAF="; app_fmt2(o, ncalled < 2 ? 0.0 : (double)minAC / sum); }
+    o += is_str ? ";TYPE=STR" : ";TYPE=INDEL";
+    o += "\tGT:PL:GQ:DP:ADP:ACN";
+    for (int s = 0; s < S; s++) {
+        const SampleIndelCall& c = calls[(size_t)s];
+        const IndelCounts& h = helpers[(size_t)s];
+        o += '\t';
+        if (c.n_called == 0) o += ploidy > 1 ? "./." : ".";
+        else if (c.n_called == 1) { o += std::to_string(c.called[0]); if (ploidy > 1) { o += '/'; o += std::to_string(c.called[0]); } }
+        else { o += std::to_string(c.called[0]); o += '/'; o += std::to_string(c.called[1]); }
+        o += ':';
+        for (int j = 0; j < n; j++)
+            for (int i = 0; i <= j; i++) {
+                if (i > 0 || j > 0) o += ',';
+                o += std::to_string(c.report ? (int)java_round(-10 * h.logc[(size_t)(i * n + j)]) : 0);
+            }
+        o += ':'; o += std::to_string(c.gq); o += ':'; o += std::to_string(c.dp); o += ':';
+        for (int i = 0; i < n; i++) { if (i) o += ','; o += std::to_string(c.report ? h.counts[(size_t)i] : 0); }
+        o += ':';
+        if (c.total_cn == 0) o += '.';
+        else for (int j = 0; j < n; j++) { if (j) o += ','; o += std::to_string((c.n_called == 0 && j == 0) ? c.total_cn : c.acn[(size_t)j]); }
+    }
+    o += '\n';
+}
+
+// discoverPopulationVariantWithSpan (MultisampleVariantsDetector.java:599-604) + discoverPopulationIndel (:616-634)
+// + onPileup's genotypeVariant and QS test (:532-533): false for a null variant (the caller's SNV fallback), else the
+// variant's record
+bool population_indel(const std::vector<Aln*>& pileup, const std::vector<SpanCall>& calls, const std::string& reference,
+                      int pos, bool is_str, bool input_str, const RealignParams& p, PopIndel* out) {
+    std::vector<std::string> alleles = cluster_alleles(calls, reference, p.max_base_qs);
+    {
+        // createIndelVariantPool (SingleSampleVariantPileupListener.java:333-338): one allele, or no call -> null
+        if (alleles.size() == 1) return false;
+        IndelCounts h;
+        indel_counts(alleles, calls, p.max_base_qs, h);
+        if (h.total == 0) return false;
+    }
+    std::vector<SampleIndelCall> sc;
+    std::vector<IndelCounts> hs;
+    while (alleles.size() > 2) {
+        bool same = true;                                                  // allelesSameLength (:339-345)
+        for (const std::string& a : alleles) same = same && a.size() == alleles[0].size();
+        if (!input_str && same) return false;
+        const int qs = genotype_indel_population(alleles, pileup, pos, p, sc, hs);
+        if (qs < p.min_quality) return false;
+        // makeNewVariant (:642-656): a TreeSet of the reference and every sample's called alleles
+        std::set<std::string> called{alleles[0]};
+        for (const SampleIndelCall& c : sc)
+            for (int i = 0; i < c.n_called; i++) called.insert(alleles[(size_t)c.called[i]]);
+        if (called.size() == alleles.size()) break;
+        std::vector<std::string> nv{alleles[0]};                           // SingleSampleVariantPileupListener.makeNewVariant
+        for (const std::string& a : called) if (a != alleles[0]) nv.push_back(a);
+        alleles.swap(nv);
+    }
+    const int qs = genotype_indel_population(alleles, pileup, pos, p, sc, hs);
+    out->qs = qs;
+    out->last = pos + (int32_t)alleles[0].size() - 1;
+    out->pass = !(qs == 0 || qs < p.min_quality);
+    out->line.clear();
+    if (out->pass) format_population_indel(pos, alleles, is_str, qs, sc, hs, p.ploidy, out->line);
+    return true;
+}
+
 }  // namespace
 
 void replay_region(const std::string& seq, int64_t first, int64_t last, std::vector<RawRead>& reads, const RealignParams& p,
@@ -843,6 +1074,11 @@ void replay_region(const std::string& seq, int64_t first, int64_t last, std::vec
     out.pos.clear();
     out.cols.clear();
     out.indels.clear();
+    out.pcodes.clear();
+    out.poff.clear();
+    out.pindels.clear();
+    const bool pop = p.n_samples > 0;
+    const int S = p.n_samples;
     std::vector<Aln> alns(reads.size());
     for (size_t i = 0; i < reads.size(); i++) {
         const RawRead& r = reads[i];
@@ -857,6 +1093,8 @@ void replay_region(const std::string& seq, int64_t first, int64_t last, std::vec
         a.quals = r.has_quals ? &r.quals : nullptr;
         a.ignore_start = r.ignore_start;
         a.ignore_end = r.ignore_end;
+        a.sample = r.sample;
+        a.rank = r.rank;
         a.update();
     }
     Realigner rl(seq);
@@ -906,6 +1144,33 @@ void replay_region(const std::string& seq, int64_t first, int64_t last, std::vec
         }
         rp.col_len = (int32_t)out.cols.size() - rp.col_off;
         while (out.cols.size() % 4) out.cols.push_back(0);
+        if (pop) {
+            // getAlleleCalls(1, sample.getReadGroups()) per sample (read-group rank, then the pileup's order) and the
+            // calls of the reads of no sample (the pooled counts' getAlleleCalls(1, null) adds them): KPM's columns
+            rp.pcol = (int32_t)out.poff.size();
+            for (int sm = 0; sm <= S; sm++) {
+                out.poff.push_back((uint32_t)out.pcodes.size());
+                int maxrank = sm < S ? -1 : 0;
+                if (sm < S) for (const Aln* a : pileup) if (a->sample == sm) maxrank = std::max<int>(maxrank, a->rank);
+                for (int r = 0; r <= maxrank; r++)
+                    for (const Aln* a : pileup) {
+                        const bool mine = sm < S ? (a->sample == sm && a->rank == r) : (a->sample < 0 || a->sample >= S);
+                        if (!mine || !a->chars) continue;
+                        const int rr = a->read_pos(pos);
+                        if (rr < 0 || a->acl[(size_t)rr] != 1) continue;
+                        int qc = (unsigned char)a->qual(rr);
+                        if (qc > 127) qc = 127;
+                        const int q = (int8_t)std::min(30, qc - 33);
+                        const int b = base_index((*a->chars)[(size_t)rr]);
+                        uint8_t code;
+                        if (q <= 3) code = (uint8_t)(kCodeCounted | (q < 0 ? 0 : q));
+                        else if (b < 0) code = (uint8_t)(kCodeCounted | q);
+                        else code = (uint8_t)(kCodeValid | (b << 5) | q);
+                        out.pcodes.push_back(code);
+                    }
+            }
+            out.poff.push_back((uint32_t)out.pcodes.size());
+        }
         // discoverVariant's early exits (SingleSampleVariantPileupListener.java:191-213): no reference for the span
         // (getReference -> null), a lower-case reference base with -ignoreLowerCaseRef
         const int plast = pos + rp.span - 1;
@@ -914,11 +1179,19 @@ void replay_region(const std::string& seq, int64_t first, int64_t last, std::vec
             std::string reference(seq, (size_t)pos - 1, (size_t)rp.span);
             for (char& ch : reference) ch = upper(ch);
             span_calls(pileup, pos, rp.span, calls);
-            const std::vector<std::string> alleles = cluster_alleles(calls, reference, p.max_base_qs);
-            IndelCall ic;
-            if (genotype_indel(alleles, calls, pos, rp.str, rp.str && !rp.new_str, p, &ic)) {
-                rp.indel = (int32_t)out.indels.size();
-                out.indels.push_back(std::move(ic));
+            if (pop) {
+                PopIndel pi;
+                if (population_indel(pileup, calls, reference, pos, rp.str, rp.str && !rp.new_str, p, &pi)) {
+                    rp.pindel = (int32_t)out.pindels.size();
+                    out.pindels.push_back(std::move(pi));
+                }
+            } else {
+                const std::vector<std::string> alleles = cluster_alleles(calls, reference, p.max_base_qs);
+                IndelCall ic;
+                if (genotype_indel(alleles, calls, pos, rp.str, rp.str && !rp.new_str, p, &ic)) {
+                    rp.indel = (int32_t)out.indels.size();
+                    out.indels.push_back(std::move(ic));
+                }
             }
         }
         out.pos.push_back(rp);
@@ -953,6 +1226,37 @@ void resolve_region(const RegionOut& out, const std::vector<uint8_t>& has_snv_ca
         }
         if (eff > 1 && input_str) continue;                                 // no SNV fallback for an input STR (:264)
         if (has_snv_call[i]) dec.push_back(RegionDecision{rp.pos, 1, embedded, -1});   // discoverSNV (and the fallback)
+    }
+}
+
+// MultisampleVariantsDetector.onPileup (:522-538): an input STR sets lastIndelEnd to its end (no ">= lastIndelEnd"
+// test, unlike the single-sample listener), a position up to lastIndelEnd is embedded; the span's indel variant is
+// written when its QS passes and moves lastIndelEnd to its end; a span without one falls back to the SNV
+// (discoverPopulationSNV, :605-612), except at an input STR
+void resolve_population_region(const RegionOut& out, const std::vector<uint8_t>& has_snv_record, bool call_embedded,
+                               int32_t* last_indel_end, std::vector<RegionDecision>& dec) {
+    dec.clear();
+    for (size_t i = 0; i < out.pos.size(); i++) {
+        const RegionPos& rp = out.pos[i];
+        const bool input_str = rp.str && !rp.new_str;
+        bool embedded = rp.var_embedded;
+        if (input_str) *last_indel_end = rp.pos + rp.span - 1;
+        else if (rp.pos <= *last_indel_end) embedded = true;
+        if (!call_embedded && embedded) continue;
+        if (rp.blocked) continue;
+        const int eff = embedded ? 1 : rp.span;
+        if (eff > 1) {
+            if (rp.pindel >= 0) {
+                const PopIndel& pi = out.pindels[(size_t)rp.pindel];
+                if (pi.pass) {
+                    dec.push_back(RegionDecision{rp.pos, 2, false, rp.pindel});
+                    *last_indel_end = pi.last;
+                }
+                continue;
+            }
+            if (input_str) continue;
+        }
+        if (has_snv_record[i]) dec.push_back(RegionDecision{rp.pos, 1, embedded, -1});
     }
 }
 

@@ -26,6 +26,8 @@ struct RawRead {
     std::string quals;                 // phred + 33 (has_quals = false: '*')
     bool has_chars = false, has_quals = false;
     int32_t ignore_start = 0, ignore_end = 0;   // setBasesToIgnore5P/3P by strand (ReadAlignment.java:613-644)
+    int16_t sample = -1;               // multisample: the sample of the read group (-1: none), and the read group's rank
+    uint8_t rank = 0;                  //   in the sample's HashSet order (PileupRecord.getAlleleCalls(span, readGroups))
 };
 
 struct RealignParams {
@@ -34,6 +36,7 @@ struct RealignParams {
     int32_t ploidy = 2;
     double het_rate = 0.001;           // -h
     bool ignore_lowercase = false;     // -ignoreLowerCaseRef
+    int32_t n_samples = 0;             // > 0: MultisampleVariantsDetector's listener (population mode)
 };
 
 // a decided indel / STR call (callIndel + the listener's filters), its VCF line already formatted
@@ -51,6 +54,18 @@ struct RegionPos {
     int32_t col_off = 0, col_len = 0;  // span-1 column: u16 entries code | negative strand << 8 in RegionOut::cols
     int32_t indel = -1;                // span > 1: index into RegionOut::indels of the span's call (-1: none)
     bool blocked = false;              // no call at all (span past the sequence end, lower-case reference ignored)
+    int32_t pcol = -1;                 // population mode: its span-1 columns, samples 0 .. S - 1 then the reads of no
+                                       // sample: RegionOut::pcodes[poff[pcol + s] .. poff[pcol + s + 1])
+    int32_t pindel = -1;               // population mode, span > 1: index into RegionOut::pindels when
+                                       // discoverPopulationVariantWithSpan found an indel variant (-1: null)
+};
+
+// MultisampleVariantsDetector's indel / STR variant at a span (discoverPopulationIndel non-null): genotyped again by
+// onPileup (genotypeVariant, :532) -- written iff its QS passes, and never followed by the SNV fallback
+struct PopIndel {
+    bool pass = false;                 // QS > 0 and >= minQuality (MultisampleVariantsDetector.java:533)
+    int32_t qs = 0, last = 0;          // the variant QS; first + |REF| - 1 (lastIndelEnd when written)
+    std::string line;                  // the record without the sequence name: "POS\t.\tREF\tALT\t..." + '\n'
 };
 
 struct RegionOut {
@@ -58,6 +73,9 @@ struct RegionOut {
     std::vector<RegionPos> pos;        // positions with a pileup, ascending
     std::vector<uint16_t> cols;
     std::vector<IndelCall> indels;
+    std::vector<uint8_t> pcodes;       // population mode: the positions' per-sample span-1 codes (engine.hpp codes)
+    std::vector<uint32_t> poff;        //   S + 2 offsets per position
+    std::vector<PopIndel> pindels;
 };
 
 // an input STR variant of -knownSTRs (SingleSampleVariantsDetector.makeNonRedundantSTRs): 1-based [first, last]
@@ -82,5 +100,10 @@ struct RegionDecision {
 };
 void resolve_region(const RegionOut& out, const std::vector<uint8_t>& has_snv_call, bool call_embedded, int32_t* last_indel_end,
                     std::vector<RegionDecision>& dec);
+// MultisampleVariantsDetector.onPileup's rules (:522-538) over a replayed region in population mode: kind 1 the
+// position's population SNV record (has_snv_record: the device wrote one; flag embedded: TYPE=EMBEDDED), 2 the
+// indel / STR record out.pindels[idx]
+void resolve_population_region(const RegionOut& out, const std::vector<uint8_t>& has_snv_record, bool call_embedded,
+                               int32_t* last_indel_end, std::vector<RegionDecision>& dec);
 
 }  // namespace ngsep

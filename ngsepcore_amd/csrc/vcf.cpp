@@ -285,7 +285,8 @@ void format_population_site(const ngsep_ctx* c, const ngsep_popsite_out& s, cons
     for (int i = 0; i < s.n_alleles; i++) { if (i) o += ','; app(o, counts[i]); }
     o += ";OH="; app_fmt2(o, ng > 0 ? (double)nhet / ng : 0.0);
     if (s.n_alleles == 2) { o += ";MAF="; app_fmt2(o, ncalled < 2 ? 0.0 : (double)minAC / sum); }
-    if (s.multisnv_type) o += ";TYPE=MULTISNV";
+    if (s.multisnv_type == 2) o += ";TYPE=EMBEDDED";        // an SNV inside an indel / STR (MultisampleVariantsDetector.java:581)
+    else if (s.multisnv_type) o += ";TYPE=MULTISNV";
     o += "\tGT:PL:GQ:DP:BSDP:ACN";
     for (int k = 0; k < S; k++) {
         const ngsep_sample_call& cl = calls[k];
@@ -311,9 +312,37 @@ void format_population_site(const ngsep_ctx* c, const ngsep_popsite_out& s, cons
     o += '\n';
 }
 
+// an indel / STR population record (multisnv_type 3, the realigner regions, engine.cpp run_population_regions): its
+// text appended; false for any other record
+bool append_population_text(const ngsep_ctx* c, size_t i, std::string& o) {
+    const ngsep_popsite_out& s = c->pop_sites[i];
+    if (s.multisnv_type != 3) return false;
+    o += (s.seq_id >= 0 && s.seq_id < (int)c->seq_names.size()) ? c->seq_names[(size_t)s.seq_id] : std::string("?");
+    o += '\t';
+    o += c->pop_text[(size_t)c->pop_order[i]];
+    return true;
+}
+
 }  // namespace ngsep
 
 using namespace ngsep;
+
+extern "C" int64_t ngsep_population_site_vcf_line(ngsep_ctx* c, int64_t i, char* buf, int64_t cap) {
+    if (!c || i < 0 || i >= (int64_t)c->pop_sites.size()) return NGSEP_E_INVALID;
+    std::string o;
+    if (!append_population_text(c, (size_t)i, o)) {
+        const size_t S = c->sample_ids.size();
+        std::vector<ngsep_sample_call> calls(S);
+        for (size_t k = 0; k < S; k++) calls[k] = expand_call(c->pop_calls.data()[(size_t)c->pop_order[(size_t)i] * S + k], c->pop_big.data());
+        format_population_site(c, c->pop_sites[(size_t)i], calls.data(), o);
+    }
+    if (buf && cap > 0) {
+        const int64_t k = std::min<int64_t>((int64_t)o.size(), cap - 1);
+        std::memcpy(buf, o.data(), (size_t)k);
+        buf[k] = 0;
+    }
+    return (int64_t)o.size();
+}
 
 extern "C" int ngsep_write_population_vcf(ngsep_ctx* c, const char* path) {
     if (!c || !path) return NGSEP_E_INVALID;
@@ -323,6 +352,7 @@ extern "C" int ngsep_write_population_vcf(ngsep_ctx* c, const char* path) {
     const size_t S = c->sample_ids.size();
     std::vector<ngsep_sample_call> calls(S);
     for (size_t i = 0; i < c->pop_sites.size(); i++) {
+        if (append_population_text(c, i, buf)) { if (buf.size() > (1 << 20)) { std::fwrite(buf.data(), 1, buf.size(), f); buf.clear(); } continue; }
         for (size_t k = 0; k < S; k++) calls[k] = expand_call(c->pop_calls.data()[(size_t)c->pop_order[i] * S + k], c->pop_big.data());
         format_population_site(c, c->pop_sites[i], calls.data(), buf);
         if (buf.size() > (1 << 20)) { std::fwrite(buf.data(), 1, buf.size(), f); buf.clear(); }

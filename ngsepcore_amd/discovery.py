@@ -86,6 +86,8 @@ class PopulationSite:
     qual: int
     multisnv_type: bool
     calls: List[NgsepSampleCall]
+    embedded: bool = False               # TYPE=EMBEDDED (an SNV inside an indel / STR, -embeddedSNVs)
+    vcf_line: Optional[str] = None       # an indel / STR record: its whole VCF line
 
 
 class GpuPileupSession:
@@ -287,16 +289,34 @@ class GpuPileupSession:
         self._check(self._lib.ngsep_fetch_population_sites(self._ctx, sites, calls, n.value, ctypes.byref(n)))
         return sites[: n.value], calls[: n.value * S]
 
+    def population_vcf_line(self, i: int) -> str:
+        """the VCF line of population site i (ngsep_population_site_vcf_line, ABI 8)"""
+        need = self._lib.ngsep_population_site_vcf_line(self._ctx, i, None, 0)
+        if need < 0:
+            raise NgsepError(int(need), self._lib.ngsep_last_error(self._ctx).decode())
+        buf = ctypes.create_string_buffer(int(need) + 1)
+        self._lib.ngsep_population_site_vcf_line(self._ctx, i, buf, int(need) + 1)
+        return buf.value.decode()
+
     def getPopulationVariants(self) -> List[PopulationSite]:
+        """the population records; an indel / STR record (multisnv_type 3: the realigner's regions, ABI 8) takes its
+        alleles from its VCF line and carries that line in vcf_line (its per-sample calls are only there)"""
         names = self.sequence_names()
         sites, calls = self.raw_population_sites()
         S = len(self.samples)
         out = []
         for i, s in enumerate(sites):
+            seq = names[s.seq_id] if 0 <= s.seq_id < len(names) else "?"
+            if s.multisnv_type == 3:
+                line = self.population_vcf_line(i)
+                f = line.split("\t", 6)
+                out.append(PopulationSite(sequence=seq, pos=s.pos, alleles=[f[3]] + ([] if f[4] == "." else f[4].split(",")),
+                                          qual=s.qual, multisnv_type=False, calls=[], vcf_line=line))
+                continue
             out.append(PopulationSite(
-                sequence=names[s.seq_id] if 0 <= s.seq_id < len(names) else "?", pos=s.pos,
+                sequence=seq, pos=s.pos,
                 alleles=[BASES[s.alleles[k]] for k in range(s.n_alleles)], qual=s.qual,
-                multisnv_type=bool(s.multisnv_type), calls=list(calls[i * S:(i + 1) * S])))
+                multisnv_type=s.multisnv_type == 1, calls=list(calls[i * S:(i + 1) * S]), embedded=s.multisnv_type == 2))
         return out
 
     def write_population_vcf(self, path: str):
@@ -431,6 +451,8 @@ class MultisampleVariantsDetector:
 
     def setGenome(self, v: str): self.genomeFile = v
     def setKnownVariantsFile(self, v: str): self.knownVariantsFile = v          # (:193-195)
+    def setKnownSTRsFile(self, v: str): self.knownSTRsFile = v                  # (:439-446)
+    def setCallEmbeddedSNVs(self, v: bool): self.params.call_embedded = int(bool(v))
     def setOutFilename(self, v: str): self.outFilename = v
     def setMinAlleleDepthFrequency(self, v: float): self.params.min_allele_depth_freq = float(v)
     def setHeterozygosityRate(self, v: float):
@@ -460,6 +482,8 @@ class MultisampleVariantsDetector:
         s.load_fasta(self.genomeFile)
         if getattr(self, "knownVariantsFile", None):
             s.set_known_variants(self.knownVariantsFile)
+        elif getattr(self, "knownSTRsFile", None):          # (the realigner's input STRs when no input variants)
+            s.set_known_strs(self.knownSTRsFile)
         arr = (ctypes.c_char_p * len(input_files))(*[f.encode() for f in input_files])
         s._check(s._lib.ngsep_call_population_bams(s._ctx, arr, len(input_files), self.outFilename.encode()))
         return s

@@ -8,7 +8,12 @@
    inputs (tools/synth), plus <case>.sam.md5 pinning the generator's output.  The GPU tests
    compare the HIP path with these files without running the oracle.
 
-Usage: python tests/golden/make_golden.py [--no-reference]
+3. reference_strs.txt.gz -- data extracted from the reference's own input file training/Saccharomyces_cerevisiae_STRs.txt
+   (TRF output over sacCer3): the first three fields of every line (sequence, first, last), the only fields
+   SimpleGenomicRegionFileHandler.loadRegions reads for -knownSTRs, in file order with the file's separators.
+   Needs /root/reference (read only): python tests/golden/make_golden.py --strs
+
+Usage: python tests/golden/make_golden.py [--no-reference] [--strs]
 """
 from __future__ import annotations
 
@@ -25,6 +30,20 @@ for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tools", "synth
         sys.path.insert(0, p)
 
 REF_VCF = "/root/reference/training/yeastDemo_ann_q40_s_fi_I2_noREP_noCNV.vcf.gz"
+REF_STRS = "/root/reference/training/Saccharomyces_cerevisiae_STRs.txt"
+
+
+def str_fixture(path):
+    """the (sequence, first, last) fields of the reference's STR file, space separated as there"""
+    n = 0
+    with open(REF_STRS) as f, gzip.GzipFile(path, "wb", mtime=0) as g:
+        for line in f:
+            fl = line.split()
+            if len(fl) < 3:
+                continue
+            g.write((" ".join(fl[:3]) + "\n").encode())
+            n += 1
+    return n
 
 # name -> (synth kwargs, oracle option kwargs); kept small so the oracle runs in seconds
 CASES = {
@@ -215,6 +234,9 @@ def full_size_population_fixtures(names=None):
 
 
 if __name__ == "__main__":
+    if "--strs" in sys.argv:
+        print("reference STR rows:", str_fixture(os.path.join(HERE, "reference_strs.txt.gz")))
+        sys.exit(0)
     if "--full-pop" in sys.argv:
         full_size_population_fixtures([a for a in sys.argv[2:] if not a.startswith("-")] or None)
         sys.exit(0)

@@ -15,6 +15,7 @@ OPTION_MAP = {  # GPU ngsep_params field -> oracle params field (same meaning)
     "ignore_lowercase_ref": "ignore_lowercase_ref", "calc_strand_bias": "calc_strand_bias",
     "print_sample_ploidy": "print_sample_ploidy", "het_rate": "het_rate", "query_seq": "query_seq",
     "query_first": "query_first", "query_last": "query_last", "sample_id": "sample_id",
+    "call_embedded": "call_embedded", "indel_passthrough": "indel_passthrough",
 }
 
 

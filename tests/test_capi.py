@@ -28,7 +28,7 @@ def test_every_declared_symbol_is_exported():
 
 def test_abi_version_and_defaults():
     lib = _lib.load()
-    assert lib.ngsep_abi_version() == 7
+    assert lib.ngsep_abi_version() == 8
     p = _lib.NgsepParams()
     lib.ngsep_params_default(ctypes.byref(p))
     # DEF_* constants: SingleSampleVariantsDetector.java:65-78, CountsHelper.java:42-48
@@ -67,7 +67,7 @@ def test_no_device_fails_loudly(tmp_path):
 
 
 def test_known_strs_argument_checks(tmp_path):
-    """ngsep_set_known_strs (ABI 7): needs the reference first, belongs to SingleSampleVariantsDetector only, reads
+    """ngsep_set_known_strs (ABI 7): needs the reference first, belongs to the variant detectors only, reads
     its file; lines the reference's loader skips (SimpleGenomicRegionFileHandler.java:57-80) are skipped here too."""
     from ngsepcore_amd import GpuPileupSession, NgsepError, default_params
     path = os.path.join(str(tmp_path), "strs.txt")
@@ -84,7 +84,12 @@ def test_known_strs_argument_checks(tmp_path):
             s.set_known_strs(os.path.join(str(tmp_path), "missing.txt"))
         assert e.value.code == _lib.NGSEP_E_IO
     p = default_params()
-    p.multisample = 1
+    p.multisample = 1                       # MultisampleVariantsDetector -knownSTRs (:439-446): accepted (ABI 8)
+    with GpuPileupSession(p) as s:
+        s.set_reference("c1", b"ACGT" * 100)
+        s.set_known_strs(path)
+    p = default_params()
+    p.coverage_stats = 1
     with GpuPileupSession(p) as s:
         s.set_reference("c1", b"ACGT" * 100)
         with pytest.raises(NgsepError) as e:

@@ -227,3 +227,69 @@ def test_known_strs_vcf_identical(tmp_path, kw, opts):
         assert a == b, (a, b)
     assert len(ro) == len(rg)
     assert st.positions_genotyped == ost.positions_genotyped
+
+
+def _reference_strs(tmp_path):
+    """the reference's own -knownSTRs input (training/Saccharomyces_cerevisiae_STRs.txt: TRF regions over sacCer3, 14,063
+    lines, overlapping and nested ones included), as committed in tests/golden/reference_strs.txt.gz (its sequence,
+    first and last fields; tests/golden/make_golden.py --strs)"""
+    import gzip
+    src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_strs.txt.gz")
+    path = os.path.join(str(tmp_path), "Saccharomyces_cerevisiae_STRs.txt")
+    with gzip.open(src, "rb") as g, open(path, "wb") as f:
+        f.write(g.read())
+    return path
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opts", [{}, dict(call_embedded=1)])
+def test_reference_strs_vcf_identical(tmp_path, opts):
+    """-knownSTRs with the reference's own STR file on a synthetic genome of sacCer3's names and lengths (chrI, chrII) with
+    donor indels: makeNonRedundantSTRs over its regions, every merged STR a realigner input variant; the WHOLE VCF equals
+    the oracle's through ngsep_call_bam.  (The regions are the reference's; the bases they cover are synthetic, so most
+    are not repeats here -- the realigner and the listener treat them as input STRs all the same.)"""
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=2, depth=15, seed=41, indel_rate=3e-4, snv_rate=2e-3)
+    fa, sam, bam = syn.write(os.path.join(str(tmp_path), "yst"))
+    syn.close()
+    strs = _reference_strs(tmp_path)
+    o = os.path.join(str(tmp_path), "o.vcf")
+    ost = ngsep_oracle.run_ssvd(fa, sam, o, known_strs=strs.encode(), **opts)
+    g = os.path.join(str(tmp_path), "g.vcf")
+    with GpuPileupSession(gpu_params(**opts)) as s:
+        s.load_fasta(fa)
+        s.set_known_strs(strs)
+        s.processFile(bam, g)
+        assert s.carved_regions() == []
+        st = s.stats()
+    ro, rg = _records(o), _records(g)
+    assert sum(1 for l in ro if "TYPE=STR" in l) > 10
+    for a, b in zip(ro, rg):
+        assert a == b, (a, b)
+    assert len(ro) == len(rg)
+    assert st.positions_genotyped == ost.positions_genotyped
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opts", [{}, dict(call_embedded=1)])
+def test_reference_strs_population_vcf_identical(tmp_path, opts):
+    """MultisampleVariantsDetector -knownSTRs (:439-446) with the reference's STR file: 12 samples on sacCer3's chrI
+    with population indels; the WHOLE population VCF equals the oracle's (path B: one BAM per sample)."""
+    from ngsepcore_amd import MultisampleVariantsDetector
+    from helpers import diff_vcf
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=1, depth=8, seed=42, n_samples=12, indel_rate=4e-4, snv_rate=2e-3)
+    fa, sam, _ = syn.write(os.path.join(str(tmp_path), "pop"))
+    bams = syn.write_sample_bams(os.path.join(str(tmp_path), "pop"))
+    syn.close()
+    strs = _reference_strs(tmp_path)
+    o = os.path.join(str(tmp_path), "o.vcf")
+    ngsep_oracle.run_mvd(fa, sam, o, 0.0, known_strs=strs.encode(), **opts)
+    assert sum(1 for l in _records(o) if "TYPE=STR" in l) > 3
+    d = MultisampleVariantsDetector()
+    for k, v in opts.items():
+        setattr(d.params, k, v)
+    d.setGenome(fa)
+    d.setKnownSTRsFile(strs)
+    d.setOutFilename(os.path.join(str(tmp_path), "g.vcf"))
+    d.run(bams).close()
+    diff = diff_vcf(o, d.outFilename)
+    assert not diff, "\n".join(diff[:20])

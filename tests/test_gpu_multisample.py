@@ -182,3 +182,40 @@ def test_population_known_variants(tmp_path, kw, opts):
     d.run(bams).close()
     diff = diff_vcf(o, d.outFilename)
     assert not diff, "\n".join(diff[:20])
+
+
+@pytest.mark.parametrize("kw,opts", [
+    (dict(n_samples=12, depth=10, seed=21, indel_rate=3e-4, snv_rate=2e-3), {}),
+    (dict(n_samples=16, depth=8, seed=22, indel_rate=5e-4, snv_rate=3e-3, quality_model=2), {"call_embedded": 1}),
+    (dict(n_samples=10, depth=12, seed=23, indel_rate=4e-4, snv_rate=2e-3), {"ploidy": 1, "het_rate": 0.01}),
+    (dict(n_samples=20, depth=6, seed=24, indel_rate=6e-4, snv_rate=3e-3), {"min_quality": 20, "min_allele_depth_freq": 0.02}),
+])
+def test_population_indels_vcf_identical(tmp_path, kw, opts):
+    """MultisampleVariantsDetector with the indel realigner first in its chain (MultisampleVariantsDetector.java:449-450):
+    population indel / STR records (discoverPopulationVariantWithSpan / discoverPopulationIndel :599-634, every sample
+    genotyped by callIndel over the variant's alleles), the SNVs of the realigned alignments (KPM over the regions'
+    columns), lastIndelEnd / embedded SNVs (:522-538).  The WHOLE population VCF equals the oracle's through path A
+    (ngsep_process_alignments) and path B (one BAM per sample, files in sample order: the merge's ties go to the lower
+    file index); no region is handed back.  Parity is against the oracle restatement only: the reference holds no
+    population indel fixture (parity unpinned)."""
+    from ngsepcore_amd import MultisampleVariantsDetector
+    syn, fa, sam, rgs = population(tmp_path, genome=pysynth.CUSTOM, custom_len=60000, **kw)
+    min_adf = opts.get("min_allele_depth_freq", 0.0)
+    oopts = {k: v for k, v in opts.items() if k != "min_allele_depth_freq"}
+    o = oracle_mvd(tmp_path, fa, sam, min_adf, **oopts)
+    ro = [l for l in open(o) if not l.startswith("#")]
+    assert sum(1 for l in ro if "TYPE=INDEL" in l or "TYPE=STR" in l) > 3
+    g, st = gpu_mvd(tmp_path, syn, rgs, **opts)
+    d = diff_vcf(o, g)
+    assert not d, "\n".join(d[:20])
+    bams = syn.write_sample_bams(os.path.join(str(tmp_path), "pop"))
+    det = MultisampleVariantsDetector()
+    for k, v in opts.items():
+        setattr(det.params, k, v)
+    if "het_rate" in opts:
+        det.params.het_rate_set = 1
+    det.setGenome(fa)
+    det.setOutFilename(os.path.join(str(tmp_path), "gpu_b.vcf"))
+    det.run(bams).close()
+    d = diff_vcf(o, det.outFilename)
+    assert not d, "\n".join(d[:20])
