@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define NGSEP_ABI_VERSION 8
+#define NGSEP_ABI_VERSION 9
 
 #define NGSEP_OK 0
 #define NGSEP_E_INVALID (-1)      /* bad argument / state */
@@ -84,8 +84,9 @@ typedef struct ngsep_params {
      * dump_all_positions records are always whole. */
     int32_t full_records;
     /* ABI 6: the indel realigner and indel / STR discovery (IndelRealignerPileupListener + VariantDiscovery-
-     * SNVQAlgorithm.callIndel, single-sample discovery at ploidy < 3 without -knownVariants, streamed runs; ABI 8:
-     * also MultisampleVariantsDetector at ploidy < 3 without -knownVariants, discoverPopulationIndel).
+     * SNVQAlgorithm.callIndel, single-sample discovery at ploidy < 3, streamed runs; ABI 8: also
+     * MultisampleVariantsDetector at ploidy < 3, discoverPopulationIndel; ABI 9: also with -knownVariants, whose
+     * records are the realigner's input variants).
      * 0 (default): regions around alignments with indels are realigned and called here (indel / STR records,
      * TYPE=EMBEDDED SNVs with call_embedded); 1: pass-through -- no call inside those regions, which are returned
      * by ngsep_fetch_carved_regions for the caller's own indel path (the ABI 5 behaviour). */
@@ -127,8 +128,9 @@ typedef struct ngsep_site_out {
     int16_t qual;            /* variant QS, phred(P[ref][ref]) */
     int8_t  is_call;         /* bit 0: passes the listener filters (always set unless dump_all_positions);
                               * bit 2: an SNV inside a called indel (INFO TYPE=EMBEDDED, params.call_embedded);
-                              * bit 3: an indel / STR record -- its fields here are 0 except seq_id / pos, its
-                              * VCF line comes from ngsep_site_vcf_line (ABI 6) */
+                              * bit 3: an indel / STR record (ABI 9: or a -knownVariants record that is not an
+                              * SNV) -- its fields here are 0 except seq_id / pos, its VCF line comes from
+                              * ngsep_site_vcf_line (ABI 6) */
     uint8_t pool;            /* ploidy >= 3 (SingleSampleVariantPileupListener.genotypeVariantPool, :402-503):
                               * bits 0-3 = the variant's alleles as DNA-index bits (reference included; the
                               * alleles are the reference, then the others in A,C,G,T order), bit 4 = the call
@@ -155,8 +157,9 @@ typedef struct ngsep_popsite_out {
     int8_t  multisnv_type;   /* 1: the pooled multi-allelic SNV kept all its alleles -> INFO TYPE=MULTISNV;
                               * 2 (ABI 8): an SNV inside an indel / STR (-embeddedSNVs) -> TYPE=EMBEDDED;
                               * 3 (ABI 8): an indel / STR record of the realigner's regions (discoverPopulationIndel,
-                              * MultisampleVariantsDetector.java:599-634): its alleles and sample calls are only in its
-                              * VCF line (ngsep_population_site_vcf_line); its calls[] entries are zeroed */
+                              * MultisampleVariantsDetector.java:599-634; ABI 9: or a -knownVariants record that is
+                              * not an SNV): its alleles and sample calls are only in its VCF line
+                              * (ngsep_population_site_vcf_line); its calls[] entries are zeroed */
     int16_t qual;            /* variant QS: max GQ over decided non-reference sample calls (:674-693) */
     int16_t pad;
 } ngsep_popsite_out;
@@ -200,12 +203,19 @@ typedef struct ngsep_stats {
     int64_t other_allele_calls;     /* entries of the scan's other-allele lists (valid non-reference calls) */
 } ngsep_stats;
 
-/* ---- -knownVariants (SingleSampleVariantsDetector.findSNVS :896-906) ---- */
-/* Genotype the biallelic SNVs of this VCF at their covered positions instead of discovering variants
- * (SingleSampleVariantPileupListener.onPileup with input variants, :158-176; genotypeSNV): every input
- * variant with a pileup gets a record (hom-ref, het, hom-alt or undecided, QUAL = its input QUAL, ID kept).
- * Call after the reference is loaded; NULL or "" returns to discovery.  Other variant types: E_UNSUPPORTED. */
-int  ngsep_set_known_variants(ngsep_ctx* c, const char* vcf_path);
+/* ---- -knownVariants (SingleSampleVariantsDetector.findSNVS :896-906, MultisampleVariantsDetector.run :432-438) ---- */
+/* Genotype the records of this VCF (VCFFileReader.loadVariants(file, true, true): ALT '.' and structural records
+ * skipped) at their covered first positions instead of discovering variants (SingleSampleVariantPileupListener.onPileup
+ * with input variants, :158-176; MultisampleVariantsDetector.onPileup :539-551): every input variant with a pileup gets
+ * a record (hom-ref, het, hom-alt or undecided; ID, alleles and INFO TYPE kept; QUAL the input's, or the population
+ * QS).  Biallelic SNVs are genotyped on the device (genotypeSNV / the pool algorithm); ABI 9: indels, MNPs and other
+ * records that are not SNVs are accepted at ploidy < 3 -- they are the indel realigner's fixed events
+ * (IndelRealignerPileupListener.setInputVariants, findSNVS :904) and are genotyped in their realigner regions by
+ * callIndel with the variant given (genotypeVariantSample :377-386).  Multi-allelic SNVs, records that repeat an
+ * allele and non-SNV records at ploidy >= 3: E_UNSUPPORTED.  Call after the reference is loaded; NULL or "" returns
+ * to discovery; a file with no usable record also discovers (inputVariants.size() == 0, :148).  Once a file is set,
+ * ngsep_set_known_strs is ignored (the reference's else-if, :906). */
+int  ngsep_set_known_variants(ngsep_ctx* c, const char* vcf_path);   /* ngsep_set_known_variants(c, NULL) clears it */
 
 /* ---- -knownSTRs (ABI 7; SingleSampleVariantsDetector.findSNVS :906-912, makeNonRedundantSTRs :843-894) ----
  * Regions "sequence first last" (1-based, space or tab separated; SimpleGenomicRegionFileHandler.loadRegions) merged
@@ -255,8 +265,8 @@ int ngsep_clear_sites(ngsep_ctx* ctx);
  * each indel event and calls indels.  Every admitted alignment with an I/D item opens a region
  * [first - R, last + indel bases + R], R = the largest alignment span + 100 (the reach of an event's
  * realignment: every alignment overlapping it), merged per sequence.  With params.indel_passthrough = 0
- * (ABI 6, the default for single-sample discovery at ploidy < 3 without -knownVariants in streamed runs; ABI 8:
- * MultisampleVariantsDetector at ploidy < 3 without -knownVariants, outside the staged measurement entry points)
+ * (ABI 6, the default for single-sample runs at ploidy < 3 in streamed runs; ABI 8: MultisampleVariantsDetector at
+ * ploidy < 3, outside the staged measurement entry points; ABI 9: with -knownVariants too)
  * the regions are realigned and called here: indel / STR records (is_call bit 3; population records with
  * multisnv_type 3) and the SNVs of the realigned alignments join the other calls, and no region is listed below.  Otherwise (pass-through, and
  * every other mode) no call is made inside a region; outside them the calls are the reference's; the regions

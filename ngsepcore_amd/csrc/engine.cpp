@@ -381,15 +381,16 @@ static inline void admit_index(ngsep_ctx* c, int32_t i) {
     if (!c->params.coverage_stats) c->to_project.push_back(i);
     admit_core(c, b->first[i], c->cur_batch.last[i], b->flags[i], b->read_group ? b->read_group[i] : -1, c->cur_batch.indel[i]);
 }
-// -knownSTRs: the input STRs of the current sequence that start at or before `upto` join the realigner's events
-// (IndelRealignerPileupListener realigns around every input variant, :85-126), in start order among the indel reads,
-// so they open regions of the same reach (carve_indel_regions, keep_raw, stream_launch)
+// the realigner's input variants of the current sequence that start at or before `upto` and open a region (the input
+// STRs; with -knownVariants the records that are not SNVs) join its events (IndelRealignerPileupListener realigns
+// around every input variant, :85-126), in start order among the indel reads, so they open regions of the same reach
+// (carve_indel_regions, keep_raw, stream_launch); an SNV input changes nothing where no indel read reaches it
 static void inject_strs(ngsep_ctx* c, int64_t upto) {
     ContigReads& cr = c->contig;
-    if (cr.seq_id < 0 || (size_t)cr.seq_id >= c->strs.size() || !c->known.empty()) return;
-    const std::vector<StrVar>& v = c->strs[(size_t)cr.seq_id];
+    if (cr.seq_id < 0 || (size_t)cr.seq_id >= c->strs.size()) return;
+    const std::vector<StrVar>& v = c->strs[(size_t)cr.seq_id].v;
     while (c->str_next < v.size() && (int64_t)v[c->str_next].first <= upto) {
-        cr.indel_reads.push_back({v[c->str_next].first, v[c->str_next].last});
+        if (v[c->str_next].event) cr.indel_reads.push_back({v[c->str_next].first, v[c->str_next].last});
         c->str_next++;
     }
 }
@@ -565,14 +566,14 @@ static int stream_advance(ngsep_ctx* c, bool final);
 
 static bool streaming(const ngsep_ctx* c) { return !c->staging_mode && !c->params.coverage_stats && !c->params.multisample; }
 
-// the indel realigner runs here (realign.hpp) in streamed single-sample discovery and in MultisampleVariantsDetector
-// (run per sequence), at ploidy < 3 without input variants (the reference's listener chains:
-// SingleSampleVariantsDetector.java:896-931, MultisampleVariantsDetector.java:449-450); elsewhere its regions are
+// the indel realigner runs here (realign.hpp) in streamed single-sample runs and in MultisampleVariantsDetector (run
+// per sequence), at ploidy < 3, discovering or genotyping -knownVariants (the reference's listener chains:
+// SingleSampleVariantsDetector.java:896-931, MultisampleVariantsDetector.java:432-450); elsewhere its regions are
 // carved out and returned (params.indel_passthrough)
 static bool realign_active(const ngsep_ctx* c) {
     const bool path = streaming(c) || (c->params.multisample && !c->staging_mode);
     return path && !c->params.indel_passthrough && !c->params.relative_allele_counts && !c->params.dump_all_positions &&
-           c->params.ploidy < 3 && c->known.empty();
+           c->params.ploidy < 3;
 }
 
 // keeps the raw alignments (RawRead) a realigner region can need: those inside the reach of an indel read
@@ -819,6 +820,10 @@ static int stream_collect(ngsep_ctx* c) {
         for (size_t i = 0; i < j->sites.size(); i++) {
             SiteRec& o = j->sites.rec[i];
             if (i == 0 || j->sites.rec[i - 1].pos != o.pos) taken.clear();
+            if (o.is_call & kRecIndel) {                   // a non-SNV input variant's record: its index kept in L[1]
+                kidx[i] = __builtin_bit_cast(int64_t, o.L[1]);
+                continue;
+            }
             auto it = std::lower_bound(c->known.begin() + kb, c->known.begin() + ke, (int64_t)o.pos,
                                        [](const ngsep_ctx::KnownVar& v, int64_t p) { return v.pos < p; });
             int64_t k = it - c->known.begin();
@@ -949,10 +954,11 @@ static void stream_launch(ngsep_ctx* c, int64_t w0, int64_t w1) {
         int64_t maxlast = INT64_MIN;
         for (; it != c->known.begin() + ke && it->pos <= w1; ++it) {
             const int64_t p = it->pos;
+            if (it->alt < 0) continue;                                    // not an SNV: genotyped in its region
             while (r < (size_t)hi && cr.first[r] <= p) { maxlast = std::max<int64_t>(maxlast, cr.last[r]); r++; }
             if (maxlast < p) continue;                                    // no pileup here
             while (ci < cut.size() && cut[ci].second < p) ci++;
-            if (ci < cut.size() && cut[ci].first <= p) continue;          // carved: the caller's own path
+            if (ci < cut.size() && cut[ci].first <= p) continue;          // a realigner region: run_regions
             j->forced.push_back((int32_t)(p + goff_k));                   // a KP queue entry (SiteQ): no column yet
             j->forced.push_back(0x80 | (it->ref << 5) | (it->alt << 8) | 0x400);
             j->forced.push_back(0);
@@ -2094,6 +2100,7 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
                 const auto& cv = cr.carved;
                 for (; it != c->known.begin() + ke && it->pos <= w1; ++it) {
                     const int64_t p = it->pos;
+                    if (it->alt < 0) continue;                            // not an SNV: genotyped in its region
                     while (r < cr.first.size() && cr.first[r] <= p) { maxlast = std::max<int64_t>(maxlast, cr.last[r]); r++; }
                     if (maxlast < p) continue;                                    // no pileup here
                     while (ci < cv.size() && cv[ci].second < p) ci++;
@@ -2273,20 +2280,42 @@ static int run_regions(ngsep_ctx* c, WindowJob* j, int64_t goff) {
     rp.ploidy = c->params.ploidy;
     rp.het_rate = c->het_rate;
     rp.ignore_lowercase = c->params.ignore_lowercase_ref != 0;
+    const bool known = !c->known.empty();
+    rp.known = known;
     parallel_for((int64_t)nr, 1, [&](int64_t a, int64_t b) {
         for (int64_t k = a; k < b; k++)
             replay_region(seq, j->carved[(size_t)k].first, j->carved[(size_t)k].second, j->region_reads[(size_t)k], rp,
-                          (size_t)j->seq_id < c->strs.size() ? &c->strs[(size_t)j->seq_id] : nullptr, outs[(size_t)k]);
+                          (size_t)j->seq_id < c->strs.size() ? &c->strs[(size_t)j->seq_id] : nullptr, &c->known_recs,
+                          outs[(size_t)k]);
     });
     // KP's queue: {global position, reference code, column offset / 4, entries} per callable position
     Staged& s = c->staged;
     s.known = true;
     s.h_forced.clear();
     s.h_cols.clear();
+    const int64_t kb = known ? c->known_seq_begin[(size_t)j->seq_id] : 0, ke = known ? c->known_seq_begin[(size_t)j->seq_id + 1] : 0;
     for (size_t k = 0; k < nr; k++) {
         const RegionOut& o = outs[k];
         const size_t cbase = s.h_cols.size();
         s.h_cols.insert(s.h_cols.end(), o.cols.begin(), o.cols.end());
+        if (known) {
+            // -knownVariants: the region's input SNVs at positions with a pileup, in input order, genotyped from the
+            // replayed columns (queue code 0x80 | ref << 5 | alt << 8 | 0x400, as stream_launch's)
+            auto it = std::lower_bound(c->known.begin() + kb, c->known.begin() + ke, o.first,
+                                       [](const ngsep_ctx::KnownVar& v, int64_t p) { return v.pos < p; });
+            size_t pi = 0;
+            for (; it != c->known.begin() + ke && it->pos <= o.last; ++it) {
+                if (it->alt < 0) continue;
+                while (pi < o.pos.size() && o.pos[pi].pos < it->pos) pi++;
+                if (pi == o.pos.size() || o.pos[pi].pos != it->pos) continue;       // no pileup here
+                const RegionPos& p = o.pos[pi];
+                s.h_forced.push_back((int32_t)(p.pos + goff));
+                s.h_forced.push_back(0x80 | (it->ref << 5) | (it->alt << 8) | 0x400);
+                s.h_forced.push_back((int32_t)((cbase + (size_t)p.col_off) / 4));
+                s.h_forced.push_back(p.col_len);
+            }
+            continue;
+        }
         for (const RegionPos& p : o.pos) {
             if (p.blocked || p.col_len == 0) continue;
             const uint8_t rc = ref_code(c, seq[(size_t)p.pos - 1]);
@@ -2312,7 +2341,29 @@ static int run_regions(ngsep_ctx* c, WindowJob* j, int64_t goff) {
     std::vector<uint8_t> has;
     std::vector<size_t> rec_at;
     std::vector<RegionDecision> dec;
-    for (size_t k = 0; k < nr; k++) {
+    for (size_t k = 0; k < nr && known; k++) {
+        // -knownVariants: every input SNV record, and the non-SNV records genotyped by the replay (their order at a
+        // shared position is the input's: stream_collect, by the known index kept in L[1])
+        const RegionOut& o = outs[k];
+        for (const KnownCall& kc : o.kcalls) {
+            while (ri < snv.size() && snv.rec[ri].pos <= kc.pos) add.push_from(snv, ri++);
+            SiteRec r;
+            std::memset(&r, 0, sizeof r);
+            r.seq_id = j->seq_id;
+            r.pos = kc.pos;
+            r.is_call = kRecCall | kRecIndel;
+            add.text.push_back(kc.line);
+            r.L[0] = __builtin_bit_cast(double, (int64_t)add.text.size() - 1);
+            r.L[1] = __builtin_bit_cast(double, kc.known);
+            add.rec.push_back(r);
+            kept++;
+        }
+    }
+    if (known) {
+        while (ri < snv.size()) add.push_from(snv, ri++);
+        kept += (int64_t)snv.size();
+    }
+    for (size_t k = 0; k < nr && !known; k++) {
         const RegionOut& o = outs[k];
         has.assign(o.pos.size(), 0);
         rec_at.assign(o.pos.size(), 0);
@@ -2393,16 +2444,38 @@ static int run_population_regions(ngsep_ctx* c, const ContigReads& cr, size_t fr
     rp.het_rate = c->het_rate;
     rp.ignore_lowercase = c->params.ignore_lowercase_ref != 0;
     rp.n_samples = S;
+    const bool known = !c->known.empty();
+    rp.known = known;
     parallel_for((int64_t)nr, 1, [&](int64_t a, int64_t b) {
         for (int64_t k = a; k < b; k++)
             replay_region(seq, cr.carved[(size_t)k].first, cr.carved[(size_t)k].second, reads[(size_t)k], rp,
-                          (size_t)cr.seq_id < c->strs.size() ? &c->strs[(size_t)cr.seq_id] : nullptr, outs[(size_t)k]);
+                          (size_t)cr.seq_id < c->strs.size() ? &c->strs[(size_t)cr.seq_id] : nullptr, &c->known_recs,
+                          outs[(size_t)k]);
     });
     // KPM over the regions' positions: position v of the queue is virtual position v of a layout of its own (tiles of
-    // kPopTile positions, site-major columns as build_multi_layout lays them out), discovery mode (no input alleles)
+    // kPopTile positions, site-major columns as build_multi_layout lays them out), discovery mode (no input alleles);
+    // with -knownVariants one virtual position per input SNV at a region position with a pileup (its alleles given)
     std::vector<std::pair<uint32_t, uint32_t>> vpos;          // (region, index in its pos list) of virtual position v
-    for (size_t k = 0; k < nr; k++)
-        for (size_t i = 0; i < outs[k].pos.size(); i++) vpos.push_back({(uint32_t)k, (uint32_t)i});
+    std::vector<int64_t> vknown;                              // -knownVariants: the input variant of virtual position v
+    if (known) {
+        const int64_t kb = c->known_seq_begin[(size_t)cr.seq_id], ke = c->known_seq_begin[(size_t)cr.seq_id + 1];
+        for (size_t k = 0; k < nr; k++) {
+            const RegionOut& o = outs[k];
+            auto it = std::lower_bound(c->known.begin() + kb, c->known.begin() + ke, o.first,
+                                       [](const ngsep_ctx::KnownVar& v, int64_t p) { return v.pos < p; });
+            size_t pi = 0;
+            for (; it != c->known.begin() + ke && it->pos <= o.last; ++it) {
+                if (it->alt < 0) continue;
+                while (pi < o.pos.size() && o.pos[pi].pos < it->pos) pi++;
+                if (pi == o.pos.size() || o.pos[pi].pos != it->pos) continue;   // no pileup here
+                vpos.push_back({(uint32_t)k, (uint32_t)pi});
+                vknown.push_back(it - c->known.begin());
+            }
+        }
+    } else {
+        for (size_t k = 0; k < nr; k++)
+            for (size_t i = 0; i < outs[k].pos.size(); i++) vpos.push_back({(uint32_t)k, (uint32_t)i});
+    }
     const int64_t V = (int64_t)vpos.size();
     std::vector<int64_t> at_site((size_t)V, -1);             // v -> index of its KPM site (-1: none written)
     const ngsep_popsite_out* sites = nullptr;
@@ -2457,7 +2530,12 @@ static int run_population_regions(ngsep_ctx* c, const ContigReads& cr, size_t fr
             const RegionOut& o = outs[vpos[(size_t)v].first];
             const RegionPos& q = o.pos[vpos[(size_t)v].second];
             rs.h_forced.push_back((int32_t)v);                 // ... of discovery entries (no 0x400: createSNVVariantPool)
-            rs.h_forced.push_back(q.blocked ? 0 : (int32_t)ref_code(c, seq[(size_t)q.pos - 1]));
+            if (known) {                                       //     or of the input SNVs (0x400: their alleles)
+                const ngsep_ctx::KnownVar& kv = c->known[(size_t)vknown[(size_t)v]];
+                rs.h_forced.push_back(0x80 | (kv.ref << 5) | (kv.alt << 8) | 0x400);
+            } else {
+                rs.h_forced.push_back(q.blocked ? 0 : (int32_t)ref_code(c, seq[(size_t)q.pos - 1]));
+            }
         }
         std::string err;
         if (!ensure_device(c, err) || device_upload(c->dev, rs, err) != 0) return set_error(c, NGSEP_E_DEVICE, err);
@@ -2480,7 +2558,51 @@ static int run_population_regions(ngsep_ctx* c, const ContigReads& cr, size_t fr
     std::vector<RegionDecision> dec;
     int64_t v0 = 0;
     int32_t lie = 0;
-    for (size_t k = 0; k < nr; k++) {
+    if (known) {
+        // -knownVariants: every input SNV's record (KPM) and every non-SNV record of the replay, by position, input
+        // order at a shared position (MultisampleVariantsDetector.onPileup :539-551 writes them all)
+        auto text_rec = [&](const KnownCall& kc) {
+            ngsep_popsite_out r;
+            std::memset(&r, 0, sizeof r);
+            r.multisnv_type = 3;
+            for (int q = 0; q < 4; q++) r.alleles[q] = -1;
+            r.seq_id = cr.seq_id;
+            r.pos = kc.pos;
+            add.push_back(r);
+            add_text.push_back((int64_t)c->pop_text.size());
+            c->pop_text.push_back(kc.line);
+        };
+        int64_t v = 0;
+        for (size_t k = 0; k < nr; k++) {
+            for (const KnownCall& kc : outs[k].kcalls) {
+                while (v < V && vpos[(size_t)v].first == k && (outs[k].pos[vpos[(size_t)v].second].pos < kc.pos ||
+                                                             (outs[k].pos[vpos[(size_t)v].second].pos == kc.pos && vknown[(size_t)v] < kc.known))) {
+                    if (at_site[(size_t)v] >= 0) {
+                        ngsep_popsite_out r = sites[at_site[(size_t)v]];
+                        r.seq_id = cr.seq_id;
+                        r.pos = outs[k].pos[vpos[(size_t)v].second].pos;
+                        src.push_back(at_site[(size_t)v]);
+                        add_text.push_back(-1);
+                        add.push_back(r);
+                    }
+                    v++;
+                }
+                text_rec(kc);
+            }
+            while (v < V && vpos[(size_t)v].first == k) {
+                if (at_site[(size_t)v] >= 0) {
+                    ngsep_popsite_out r = sites[at_site[(size_t)v]];
+                    r.seq_id = cr.seq_id;
+                    r.pos = outs[k].pos[vpos[(size_t)v].second].pos;
+                    src.push_back(at_site[(size_t)v]);
+                    add_text.push_back(-1);
+                    add.push_back(r);
+                }
+                v++;
+            }
+        }
+    }
+    for (size_t k = 0; k < nr && !known; k++) {
         const RegionOut& o = outs[k];
         has.assign(o.pos.size(), 0);
         for (size_t i = 0; i < o.pos.size(); i++) has[i] = at_site[(size_t)(v0 + (int64_t)i)] >= 0;
@@ -3101,6 +3223,7 @@ static bool merge_strs(const std::string& seq, int64_t first, int64_t last, int6
 
 extern "C" int ngsep_set_known_strs(ngsep_ctx* c, const char* path) {
     if (!c) return NGSEP_E_INVALID;
+    if (c->known_given) return NGSEP_OK;   // -knownVariants set: the realigner's inputs are its records (findSNVS :897-906)
     c->strs.clear();
     if (!path || !path[0]) return NGSEP_OK;
     if (c->seq_names.empty()) return set_error(c, NGSEP_E_INVALID, "load the reference before the known STRs");
@@ -3149,7 +3272,7 @@ extern "C" int ngsep_set_known_strs(ngsep_ctx* c, const char* path) {
         std::stable_sort(v.begin(), v.end(), [](const StrVar& x, const StrVar& y) { return x.first != y.first ? x.first < y.first : x.last < y.last; });
         const std::string& seq = c->seq_bases[sq];
         const int64_t len = (int64_t)seq.size();
-        std::vector<StrVar>& out = c->strs[sq];
+        std::vector<StrVar>& out = c->strs[sq].v;
         auto emit = [&](int64_t first, int64_t last) {
             const int64_t vf = std::max<int64_t>(1, first - 1), vl = std::min<int64_t>(last + 1, len);
             if (vf >= 1 && vl <= len && vl >= vf - 1) out.push_back(StrVar{(int32_t)vf, (int32_t)vl});
@@ -3164,6 +3287,7 @@ extern "C" int ngsep_set_known_strs(ngsep_ctx* c, const char* path) {
         }
         if (last > 0) emit(first, last);
         std::stable_sort(out.begin(), out.end(), [](const StrVar& x, const StrVar& y) { return x.first != y.first ? x.first < y.first : x.last < y.last; });
+        c->strs[sq].finish();
     }
     return NGSEP_OK;
 }
@@ -3171,7 +3295,9 @@ extern "C" int ngsep_set_known_strs(ngsep_ctx* c, const char* path) {
 extern "C" int ngsep_set_known_variants(ngsep_ctx* c, const char* vcf_path) {
     if (!c) return NGSEP_E_INVALID;
     c->known.clear();
+    c->known_recs.clear();
     c->known_seq_begin.clear();
+    c->known_given = false;
     if (!vcf_path || !vcf_path[0]) return NGSEP_OK;
     if (c->seq_names.empty()) return set_error(c, NGSEP_E_INVALID, "load the reference before the known variants");
     if (c->params.coverage_stats || c->params.relative_allele_counts)
@@ -3181,29 +3307,58 @@ extern "C" int ngsep_set_known_variants(ngsep_ctx* c, const char* vcf_path) {
     std::unordered_map<std::string, int32_t> idx;
     for (size_t i = 0; i < c->seq_names.size(); i++) idx[c->seq_names[i]] = (int32_t)i;
     std::vector<ngsep_ctx::KnownVar> v;
+    std::vector<KnownRecord> recs;
     char* line = nullptr;
     size_t cap = 0;
     ssize_t l;
     int rc = NGSEP_OK;
     int64_t lineno = 0;
+    // GenomicVariantImpl.getVariantTypeId names (GenomicVariant.java:32-56, GenomicVariantImpl.java:44-60)
+    static const char* kNames[] = {"SNV", "MULTISNV", "EMBEDDED", "INDEL", "STR", "CNV", "REPEAT", "DEL", "INS", "INV", "DUP",
+                                   "Deletion", "Insertion"};
+    static const int kIds[] = {1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 15, 12, 13};
+    auto type_id = [&](const char* name, size_t n) {
+        for (int q = 0; q < 13; q++) if (std::strlen(kNames[q]) == n && std::strncmp(kNames[q], name, n) == 0) return kIds[q];
+        return 0;
+    };
     while ((l = getline(&line, &cap, f)) >= 0) {
         lineno++;
         while (l > 0 && (line[l - 1] == '\n' || line[l - 1] == '\r')) line[--l] = 0;
         if (l == 0 || line[0] == '#') continue;
-        const char* fld[6];
+        const char* fld[8];
         int k = 0;
         char* p = line;
-        while (k < 6) { fld[k++] = p; char* t = std::strchr(p, '\t'); if (!t) break; *t = 0; p = t + 1; }
+        while (k < 8) { fld[k++] = p; char* t = std::strchr(p, '\t'); if (!t) break; *t = 0; p = t + 1; }
         if (k < 6) { rc = set_error(c, NGSEP_E_FORMAT, "VCF line " + std::to_string(lineno) + " has fewer than the 6 columns CHROM to QUAL"); break; }
         if (fld[4][0] == '.') continue;                                  // a reference site (filterReferenceSitesGVCF)
         auto it = idx.find(fld[0]);
         if (it == idx.end()) continue;
-        const int a = dna_index(fld[3][0]), b = dna_index(fld[4][0]);
-        if (std::strlen(fld[3]) != 1 || std::strlen(fld[4]) != 1 || a < 0 || b < 0) {
-            rc = set_error(c, NGSEP_E_UNSUPPORTED, std::string("known variant ") + fld[0] + ":" + fld[1] +
-                                                   " is not a biallelic SNV (indel / multi-allelic genotyping is not in this build)");
-            break;
+        // loadInfoField (VCFFileReader.java:261-305), attribute by attribute: TYPE sets an id in (0, TYPE_INVERSION],
+        // SVTYPE one >= 10, END the last position of a GenomicVariantImpl
+        int type = 0;
+        int32_t end = 0;
+        if (k >= 8 && std::strcmp(fld[7], ".") != 0) {
+            for (const char* t = fld[7]; *t;) {
+                const char* e = std::strchr(t, ';');
+                const size_t n = e ? (size_t)(e - t) : std::strlen(t);
+                if (n > 5 && std::strncmp(t, "TYPE=", 5) == 0) { const int id = type_id(t + 5, n - 5); if (id > 0 && id <= 14) type = id; }
+                if (n > 7 && std::strncmp(t, "SVTYPE=", 7) == 0) { const int id = type_id(t + 7, n - 7); if (id >= 10) type = id; }
+                if (n > 4 && std::strncmp(t, "END=", 4) == 0) end = std::atoi(t + 4);
+                t = e ? e + 1 : t + n;
+            }
         }
+        if (type >= 10) continue;                                        // structural (filterSVs)
+        // loadGenomicVariant (:192-255): an SNV object for one-base A/C/G/T REF and ALT, else a GenomicVariantImpl
+        // over REF and the ALT alleles (upper-cased)
+        std::vector<std::string> alleles{fld[3]};
+        for (const char* t = fld[4];;) {
+            const char* e = std::strchr(t, ',');
+            alleles.emplace_back(t, e ? (size_t)(e - t) : std::strlen(t));
+            if (!e) break;
+            t = e + 1;
+        }
+        const int a = dna_index(fld[3][0]), b = dna_index(fld[4][0]);
+        const bool snv = alleles.size() == 2 && alleles[0].size() == 1 && alleles[1].size() == 1 && a >= 0 && b >= 0;
         int16_t qs = 0;
         if (fld[5][0] && fld[5][0] != '.') {
             double q = std::atof(fld[5]);
@@ -3213,31 +3368,82 @@ extern "C" int ngsep_set_known_variants(ngsep_ctx* c, const char* vcf_path) {
         ngsep_ctx::KnownVar kv;
         kv.seq = it->second;
         kv.pos = std::atoi(fld[1]);
-        kv.ref = (int8_t)a;
-        kv.alt = (int8_t)b;
+        kv.last = kv.pos + (int32_t)alleles[0].size() - 1;
         kv.qs = qs;
+        kv.type = (int8_t)type;
+        kv.rec = -1;
         if (std::strcmp(fld[2], ".") != 0) kv.id = fld[2];
+        if (snv) {
+            kv.ref = (int8_t)a;
+            kv.alt = (int8_t)b;
+        } else {
+            for (std::string& x : alleles) for (char& ch : x) ch = (char)std::toupper((unsigned char)ch);
+            bool all_snv = true, dup = false;                            // GenomicVariantImpl.isSNV (:254-261)
+            for (size_t i = 0; i < alleles.size(); i++) {
+                all_snv = all_snv && alleles[i].size() == 1 && dna_index(alleles[i][0]) >= 0;
+                for (size_t j = 0; j < i; j++) dup = dup || alleles[i] == alleles[j];
+            }
+            if (all_snv || dup || alleles.size() > 100 || alleles[0].empty()) {
+                rc = set_error(c, NGSEP_E_UNSUPPORTED, std::string("known variant ") + fld[0] + ":" + fld[1] +
+                                                       (all_snv ? " is a multi-allelic SNV" : dup ? " repeats an allele" : " has too many alleles") +
+                                                       " (not genotyped by this build)");
+                break;
+            }
+            if (c->params.ploidy >= 3) {
+                rc = set_error(c, NGSEP_E_UNSUPPORTED, std::string("known variant ") + fld[0] + ":" + fld[1] +
+                                                       " is not an SNV: the pool algorithm's indel branch (ploidy >= 3) is not in this build");
+                break;
+            }
+            if (end > 0) kv.last = end;                                  // END of a GenomicVariantImpl (:282-289)
+            kv.ref = dna_index(alleles[0][0]) >= 0 ? (int8_t)dna_index(alleles[0][0]) : 0;
+            kv.alt = -1;
+            kv.rec = (int32_t)recs.size();
+            KnownRecord kr;
+            kr.alleles = std::move(alleles);
+            kr.id = kv.id;
+            kr.qs = qs;
+            kr.type = (int8_t)type;
+            recs.push_back(std::move(kr));
+        }
         v.push_back(std::move(kv));
     }
     std::free(line);
     std::fclose(f);
     if (rc != NGSEP_OK) return rc;
+    c->known_given = true;
+    c->strs.clear();                                   // -knownSTRs are ignored with -knownVariants (findSNVS :897-912)
     std::stable_sort(v.begin(), v.end(), [](const ngsep_ctx::KnownVar& x, const ngsep_ctx::KnownVar& y) {
-        return x.seq != y.seq ? x.seq < y.seq : x.pos < y.pos;
+        if (x.seq != y.seq) return x.seq < y.seq;
+        return x.pos != y.pos ? x.pos < y.pos : x.last < y.last;   // GenomicRegionPositionComparator
     });
     c->known.swap(v);
+    c->known_recs.swap(recs);
     c->known_seq_begin.assign(c->seq_names.size() + 1, 0);
     for (const auto& kv : c->known) c->known_seq_begin[(size_t)kv.seq + 1]++;
     for (size_t i = 0; i < c->seq_names.size(); i++) c->known_seq_begin[i + 1] += c->known_seq_begin[i];
+    // the realigner's input variants (every record: an SNV marks its position, SingleSampleVariantsDetector.java:904)
+    if (!c->known.empty()) {
+        c->strs.assign(c->seq_names.size(), {});
+        for (size_t k = 0; k < c->known.size(); k++) {
+            const ngsep_ctx::KnownVar& kv = c->known[k];
+            StrVar sv{kv.pos, kv.last};
+            sv.str = kv.type == 5;                     // GenomicVariant.TYPE_STR
+            sv.event = kv.alt < 0;
+            sv.known = kv.alt < 0 ? (int64_t)k : -1;
+            sv.rec = kv.rec;
+            c->strs[(size_t)kv.seq].v.push_back(sv);
+        }
+        for (InputVars& iv : c->strs) iv.finish();
+    }
     return NGSEP_OK;
 }
 
-// the input variant of a -knownVariants record: its ID (nullptr for '.').  Records are written in order, and at
-// one position in the input order (stream_collect), so a record is the first input variant of its position and
-// ALT that no earlier record there took.
-const char* ngsep::known_id(const ngsep_ctx* c, const ngsep_site_out& s) { return known_id_at(c, s.seq_id, s.pos, site_alt(s)); }
+// the input variant of a -knownVariants record (nullptr: none).  Records are written in order, and at one position
+// in the input order (stream_collect), so a record is the first input variant of its position and ALT that no
+// earlier record there took.
+const ngsep_ctx::KnownVar* ngsep::known_of(const ngsep_ctx* c, const ngsep_site_out& s) { return known_at(c, s.seq_id, s.pos, site_alt(s)); }
 
-const char* ngsep::known_id_at(const ngsep_ctx* c, int32_t seq_id, int32_t pos, int alt) {
+const ngsep_ctx::KnownVar* ngsep::known_at(const ngsep_ctx* c, int32_t seq_id, int32_t pos, int alt) {
     if (c->known.empty() || seq_id < 0 || (size_t)seq_id + 1 >= c->known_seq_begin.size()) return nullptr;
     auto& st = c->vcf_known;
     if (st.seq != seq_id || st.pos != pos) { st.seq = seq_id; st.pos = pos; st.taken.clear(); }
@@ -3247,7 +3453,7 @@ const char* ngsep::known_id_at(const ngsep_ctx* c, int32_t seq_id, int32_t pos, 
     for (int64_t k = it - c->known.begin(); k < ke && c->known[(size_t)k].pos == pos; k++)
         if (c->known[(size_t)k].alt == alt && std::find(st.taken.begin(), st.taken.end(), k) == st.taken.end()) {
             st.taken.push_back(k);
-            return c->known[(size_t)k].id.empty() ? nullptr : c->known[(size_t)k].id.c_str();
+            return &c->known[(size_t)k];
         }
     return nullptr;
 }

@@ -693,14 +693,19 @@ struct ngsep_ctx {
     std::vector<ngsep::ContigReads> staged_contigs;
     ngsep::Staged staged;
     ngsep::LayoutArena arena;
-    // -knownVariants (ngsep_set_known_variants): biallelic SNVs to genotype instead of discovering, in
-    // GenomicRegionSortedCollection order (sequence, position; input order at equal positions)
-    struct KnownVar { int32_t seq, pos; int8_t ref, alt; int16_t qs; std::string id; };
+    // -knownVariants (ngsep_set_known_variants): the input variants to genotype instead of discovering, in
+    // GenomicRegionSortedCollection order (sequence, first, last; input order at equal keys).  A biallelic SNV has
+    // ref / alt DNA codes; any other record alt = -1 and its alleles in known_recs[rec] (genotyped on the host, in the
+    // realigner's regions); type: its INFO TYPE id
+    struct KnownVar { int32_t seq, pos, last; int8_t ref, alt, type; int16_t qs; int32_t rec; std::string id; };
     std::vector<KnownVar> known;
+    std::vector<ngsep::KnownRecord> known_recs;
     std::vector<int64_t> known_seq_begin;                    // per sequence: first entry (size n_seq + 1)
-    // -knownSTRs (ngsep_set_known_strs): per sequence, the indel realigner's input STR variants (sorted, disjoint);
-    // str_next: the next one of the current sequence to enter its realigner regions (engine.cpp inject_strs)
-    std::vector<std::vector<ngsep::StrVar>> strs;
+    bool known_given = false;                                // a -knownVariants file was set (its -knownSTRs are ignored)
+    // the indel realigner's input variants per sequence (IndelRealignerPileupListener.setInputVariants): the known
+    // variants when given, else the -knownSTRs (ngsep_set_known_strs); str_next: the next event of the current
+    // sequence to enter its realigner regions (engine.cpp inject_strs)
+    std::vector<ngsep::InputVars> strs;
     size_t str_next = 0;
     // path B: the alignments the BAM is expected to hold (its size / 40 B, an upper estimate); a sequence's read
     // arrays reserve their share up front (virtual memory, touched only as they fill: no regrowth copies)
@@ -829,8 +834,8 @@ int cov_run(CovDevice* d, int32_t max_cov, uint64_t* hist_out, double* kernel_ms
 int coverage_stage(ngsep_ctx* c, std::vector<ContigReads>& contigs);
 int coverage_run(ngsep_ctx* c, double* kernel_ms);
 // engine.cpp: the ID of a -knownVariants record's input variant (nullptr: '.')
-const char* known_id(const ngsep_ctx* c, const ngsep_site_out& s);
-const char* known_id_at(const ngsep_ctx* c, int32_t seq_id, int32_t pos, int alt);
+const ngsep_ctx::KnownVar* known_of(const ngsep_ctx* c, const ngsep_site_out& s);
+const ngsep_ctx::KnownVar* known_at(const ngsep_ctx* c, int32_t seq_id, int32_t pos, int alt);
 // vcf.cpp
 std::string format_header(const ngsep_ctx* c);
 int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& out);

@@ -306,14 +306,15 @@ class Realigner {
 public:
     Realigner(const std::string& seq) : seq_(seq) {}
 
-    // onPileup without input variants (:85-126): the pileup's reference span
-    // var: the input STR intersectWithVariants found at pos (:137-153), or null.  At its first position the span is
-    // the variant's and the pileup an STR (:90-95); inside it the pileup is embedded (:96-98, *embedded)
+    // onPileup (:85-126): the pileup's reference span
+    // var: the input variant intersectWithVariants found at pos (:137-153), or null.  At its first position the span
+    // is the variant's and the pileup an STR when the variant is one (:90-95); inside it the pileup is embedded
+    // (:96-98, *embedded)
     int on_pileup(const std::vector<Aln*>& alns, int pos, const StrVar* var, bool* is_str, bool* is_new_str, bool* embedded) {
         int span = 1, predictedEnd = pos;
         if (var) {
             if (var->first == pos) {
-                *is_str = true;
+                if (var->str) *is_str = true;
                 span = var->last - var->first + 1;
                 predictedEnd = var->last;
             } else {
@@ -558,12 +559,21 @@ struct SpanCall {
     std::string allele, qual;
 };
 
-// PileupRecord.getAlleleCalls(span, null) (PileupRecord.java:126-152), span > 1
+// PileupRecord.getAlleleCalls(span, null) (PileupRecord.java:126-152); span 1 keeps the one-base calls only (:143)
 void span_calls(const std::vector<Aln*>& alns, int pos, int span, std::vector<SpanCall>& out) {
     out.clear();
     for (const Aln* a : alns) {
         int l1 = 0;
-        if (a->call1(pos, &l1) < 0) continue;
+        const int o1 = a->call1(pos, &l1);
+        if (o1 < 0) continue;
+        if (span == 1) {
+            if (l1 > 1) continue;
+            SpanCall c;
+            c.allele.assign(1, (*a->chars)[(size_t)o1]);
+            c.qual.assign(1, a->qual(o1));
+            out.push_back(std::move(c));
+            continue;
+        }
         int len = 0;
         const int off = a->call_range(pos, pos + span - 1, &len);
         if (off < 0) continue;
@@ -925,39 +935,49 @@ void sample_span_calls(const std::vector<Aln*>& pileup, int s, int pos, int span
 // callIndel with the variant given (the maximum genotype's indexes taken as they are, :335-345),
 // updateAllelesCopyNumberFromCounts(ploidy), makeUndecided below 40 (CalledGenomicVariantImpl.java:320-325).
 // Returns the variant QS: the largest GQ of a decided, non-homozygous-reference call.
+// genotypeVariantSample (SingleSampleVariantPileupListener.java:361-391) of an indel variant at ploidy < 3:
+// calculateCountsIndel over the variant's alleles, callIndel with the variant given (the maximum genotype's indexes
+// taken as they are, VariantDiscoverySNVQAlgorithm.java:335-345; no calls: an undecided call, :274-277),
+// updateAllelesCopyNumberFromCounts(ploidy), makeUndecided below min_quality (CalledGenomicVariantImpl.java:320-325)
+void genotype_indel_sample(const std::vector<std::string>& alleles, const std::vector<SpanCall>& sc, const RealignParams& p,
+                           int min_quality, SampleIndelCall& c, IndelCounts& h) {
+    const int n = (int)alleles.size();
+    c = SampleIndelCall();
+    c.acn.assign((size_t)n, 0);
+    indel_counts(alleles, sc, p.max_base_qs, h);
+    if (h.total == 0) {
+        update_cn(c, h.counts, p.ploidy);
+        return;
+    }
+    std::vector<double> post;
+    indel_posteriors(h, p.het_rate, post);
+    int im0 = 0, im1 = 0;
+    max_genotype(post, n, &im0, &im1);
+    if (im0 > 100 || im1 > 100) c.n_called = 0;                           // GenomicVariant.MAX_NUM_ALLELES
+    else if (im1 != im0) { c.n_called = 2; c.called[0] = im0; c.called[1] = im1; }
+    else { c.n_called = 1; c.called[0] = im0; }
+    double maxP = post[(size_t)(im0 * n + im1)];
+    if (im0 != im1) maxP += post[(size_t)(im1 * n + im0)];
+    c.gq = java_phred(1 - maxP);
+    c.dp = h.total;
+    c.report = true;                                                      // setCallReport (totalDepth > 0)
+    update_cn(c, h.counts, p.ploidy);
+    if ((int16_t)min_quality > c.gq) { c.n_called = 0; c.gq = 0; update_cn(c, h.counts, c.total_cn); }
+}
+
 int genotype_indel_population(const std::vector<std::string>& alleles, const std::vector<Aln*>& pileup, int pos,
                               const RealignParams& p, std::vector<SampleIndelCall>& calls, std::vector<IndelCounts>& helpers) {
-    const int n = (int)alleles.size(), S = p.n_samples;
+    const int S = p.n_samples;
     const int span = (int)alleles[0].size();
     calls.assign((size_t)S, SampleIndelCall());
     helpers.assign((size_t)S, IndelCounts());
     std::vector<Aln*> tmp;
     std::vector<SpanCall> sc;
-    std::vector<double> post;
     int qs = 0;
     for (int s = 0; s < S; s++) {
         SampleIndelCall& c = calls[(size_t)s];
-        IndelCounts& h = helpers[(size_t)s];
-        c.acn.assign((size_t)n, 0);
         sample_span_calls(pileup, s, pos, span, tmp, sc);
-        indel_counts(alleles, sc, p.max_base_qs, h);
-        if (h.total == 0) {                      // new CalledGenomicVariantImpl(variant, new byte[0]) (callIndel :274-277)
-            update_cn(c, h.counts, p.ploidy);
-            continue;
-        }
-        indel_posteriors(h, p.het_rate, post);
-        int im0 = 0, im1 = 0;
-        max_genotype(post, n, &im0, &im1);
-        if (im0 > 100 || im1 > 100) c.n_called = 0;                      // GenomicVariant.MAX_NUM_ALLELES
-        else if (im1 != im0) { c.n_called = 2; c.called[0] = im0; c.called[1] = im1; }
-        else { c.n_called = 1; c.called[0] = im0; }
-        double maxP = post[(size_t)(im0 * n + im1)];
-        if (im0 != im1) maxP += post[(size_t)(im1 * n + im0)];
-        c.gq = java_phred(1 - maxP);
-        c.dp = h.total;
-        c.report = true;                                                  // setCallReport (totalDepth > 0)
-        update_cn(c, h.counts, p.ploidy);
-        if (40 > c.gq) { c.n_called = 0; c.gq = 0; update_cn(c, h.counts, c.total_cn); }
+        genotype_indel_sample(alleles, sc, p, 40, c, helpers[(size_t)s]);
         const bool homref = c.n_called == 1 && c.called[0] == 0;
         if (c.n_called > 0 && !homref && c.gq > qs) qs = c.gq;
     }
@@ -979,12 +999,12 @@ void app_fmt2(std::string& o, double x) {
 // VCFRecord.createDefaultPopulationVCFRecord (vcf/VCFRecord.java:277-282: FORMAT DEF_FORMAT_ARRAY_NGSEP_NOSNV, INFO
 // from DiversityStatistics.calculateDiversityStatistics(calls, false), variants/DiversityStatistics.java:123-218) as
 // VCFFileWriter.printVCFRecord / printGenotypeInfo write it (:44-68,159-256); without the sequence name
-void format_population_indel(int pos, const std::vector<std::string>& alleles, bool is_str, int qs,
+void format_population_indel(int pos, const std::string& id, const std::vector<std::string>& alleles, const char* type, int qs,
                              const std::vector<SampleIndelCall>& calls, const std::vector<IndelCounts>& helpers, int ploidy,
                              std::string& o) {
     const int n = (int)alleles.size(), S = (int)calls.size();
     o.clear();
-    o += std::to_string(pos); o += "\t.\t"; o += alleles[0]; o += '\t';
+    o += std::to_string(pos); o += '\t'; o += id.empty() ? "." : id; o += '\t'; o += alleles[0]; o += '\t';
     if (n == 1) o += '.';
     for (int i = 1; i < n; i++) { if (i > 1) o += ','; o += alleles[(size_t)i]; }
     o += '\t'; o += std::to_string(qs); o += "\t.\t";
@@ -1002,7 +1022,7 @@ void format_population_indel(int pos, const std::vector<std::string>& alleles, b
     for (int i = 0; i < n; i++) { if (i) o += ','; o += std::to_string(counts[(size_t)i]); }
     o += ";OH="; app_fmt2(o, ng > 0 ? (double)nhet / ng : 0.0);
     if (n == 2) { o += ";MAF="; app_fmt2(o, ncalled < 2 ? 0.0 : (double)minAC / sum); }
-    o += is_str ? ";TYPE=STR" : ";TYPE=INDEL";
+    if (type) { o += ";TYPE="; o += type; }
     o += "\tGT:PL:GQ:DP:ADP:ACN";
     for (int s = 0; s < S; s++) {
         const SampleIndelCall& c = calls[(size_t)s];
@@ -1061,14 +1081,62 @@ bool population_indel(const std::vector<Aln*>& pileup, const std::vector<SpanCal
     out->last = pos + (int32_t)alleles[0].size() - 1;
     out->pass = !(qs == 0 || qs < p.min_quality);
     out->line.clear();
-    if (out->pass) format_population_indel(pos, alleles, is_str, qs, sc, hs, p.ploidy, out->line);
+    if (out->pass) format_population_indel(pos, std::string(), alleles, is_str ? "STR" : "INDEL", qs, sc, hs, p.ploidy, out->line);
     return true;
+}
+
+// GenomicVariantImpl.getVariantTypeName for the INFO TYPE of an input record: written when 2-5 (VCFFileWriter.java:47-49)
+const char* type_name(int t) {
+    static const char* kNames[] = {nullptr, nullptr, "MULTISNV", "EMBEDDED", "INDEL", "STR"};
+    return t >= 2 && t <= 5 ? kNames[t] : nullptr;
+}
+
+// -knownVariants, a non-SNV input variant at its first position: SingleSampleVariantsDetector's listener genotypes it in
+// the one sample (genotypeVariantSample :361-391 with -minQuality) and the record carries the input's ID, alleles, QS
+// and TYPE, FORMAT DEF_FORMAT_ARRAY_NGSEP_NOSNV (SingleSampleVariantsDetector.java:946-953); MultisampleVariantsDetector
+// genotypes it in every sample (genotypeVariant :664-693) and writes the population record with the variant QS it sets
+void known_record(const std::vector<Aln*>& pileup, int pos, const KnownRecord& kr, const RealignParams& p, std::string& o) {
+    const int n = (int)kr.alleles.size();
+    const char* type = type_name(kr.type);
+    if (p.n_samples > 0) {
+        std::vector<SampleIndelCall> sc;
+        std::vector<IndelCounts> hs;
+        const int qs = genotype_indel_population(kr.alleles, pileup, pos, p, sc, hs);
+        format_population_indel(pos, kr.id, kr.alleles, type, qs, sc, hs, p.ploidy, o);
+        return;
+    }
+    std::vector<SpanCall> calls;
+    span_calls(pileup, pos, (int)kr.alleles[0].size(), calls);
+    SampleIndelCall c;
+    IndelCounts h;
+    genotype_indel_sample(kr.alleles, calls, p, p.min_quality, c, h);
+    o.clear();
+    o += std::to_string(pos); o += '\t'; o += kr.id.empty() ? "." : kr.id; o += '\t'; o += kr.alleles[0]; o += '\t';
+    for (int i = 1; i < n; i++) { if (i > 1) o += ','; o += kr.alleles[(size_t)i]; }
+    o += '\t'; o += std::to_string(kr.qs); o += "\t.\t";
+    if (type) { o += "TYPE="; o += type; } else o += '.';
+    o += "\tGT:PL:GQ:DP:ADP:ACN\t";
+    if (c.n_called == 0) o += p.ploidy > 1 ? "./." : ".";
+    else if (c.n_called == 1) { o += std::to_string(c.called[0]); if (p.ploidy > 1) { o += '/'; o += std::to_string(c.called[0]); } }
+    else { o += std::to_string(c.called[0]); o += '/'; o += std::to_string(c.called[1]); }
+    o += ':';
+    for (int j = 0; j < n; j++)
+        for (int i = 0; i <= j; i++) {
+            if (i > 0 || j > 0) o += ',';
+            o += std::to_string(c.report ? (int)java_round(-10 * h.logc[(size_t)(i * n + j)]) : 0);
+        }
+    o += ':'; o += std::to_string(c.gq); o += ':'; o += std::to_string(c.dp); o += ':';
+    for (int i = 0; i < n; i++) { if (i) o += ','; o += std::to_string(c.report ? h.counts[(size_t)i] : 0); }
+    o += ':';
+    if (c.total_cn == 0) o += '.';
+    else for (int j = 0; j < n; j++) { if (j) o += ','; o += std::to_string((c.n_called == 0 && j == 0) ? c.total_cn : c.acn[(size_t)j]); }
+    o += '\n';
 }
 
 }  // namespace
 
 void replay_region(const std::string& seq, int64_t first, int64_t last, std::vector<RawRead>& reads, const RealignParams& p,
-                   const std::vector<StrVar>* strs, RegionOut& out) {
+                   const InputVars* inputs, const std::vector<KnownRecord>* knowns, RegionOut& out) {
     out.first = first;
     out.last = last;
     out.pos.clear();
@@ -1077,6 +1145,7 @@ void replay_region(const std::string& seq, int64_t first, int64_t last, std::vec
     out.pcodes.clear();
     out.poff.clear();
     out.pindels.clear();
+    out.kcalls.clear();
     const bool pop = p.n_samples > 0;
     const int S = p.n_samples;
     std::vector<Aln> alns(reads.size());
@@ -1103,9 +1172,20 @@ void replay_region(const std::string& seq, int64_t first, int64_t last, std::vec
     std::vector<SpanCall> calls;
     size_t next = 0;
     const int seq_len = (int)seq.size();
-    // idxNextVariant: the input STRs are sorted and disjoint, so the first one ending at or after the region's start
+    // idxNextVariant at the region's first position: the first input variant that ends at or after it or starts past it
+    // (every earlier one was passed at some pileup before, whatever the positions with pileups were) -- from the
+    // prefix maximum of `last`; from there the listener's own loop moves it along (it never moves back)
+    const std::vector<StrVar>* strs = inputs ? &inputs->v : nullptr;
     size_t vi = 0, vn = strs ? strs->size() : 0;
-    if (vn) vi = (size_t)(std::lower_bound(strs->begin(), strs->end(), first, [](const StrVar& v, int64_t x) { return (int64_t)v.last < x; }) - strs->begin());
+    if (vn) {
+        const size_t a = (size_t)(std::lower_bound(inputs->pmax.begin(), inputs->pmax.end(), (int32_t)first) - inputs->pmax.begin());
+        const size_t b = (size_t)(std::upper_bound(strs->begin(), strs->end(), first, [](int64_t x, const StrVar& v) { return x < (int64_t)v.first; }) - strs->begin());
+        vi = std::min(a, b);
+    }
+    // -knownVariants: the non-SNV input variants to genotype at their first positions (kj: the first starting at or
+    // after the position swept)
+    size_t kj = 0;
+    if (p.known && vn) kj = (size_t)(std::lower_bound(strs->begin(), strs->end(), first, [](const StrVar& v, int64_t x) { return (int64_t)v.first < x; }) - strs->begin());
     for (int64_t p64 = first; p64 <= last; p64++) {
         const int pos = (int)p64;
         while (next < alns.size() && reads[next].first <= pos) pending.push_back((int32_t)next++);   // (original starts)
@@ -1175,7 +1255,21 @@ void replay_region(const std::string& seq, int64_t first, int64_t last, std::vec
         // (getReference -> null), a lower-case reference base with -ignoreLowerCaseRef
         const int plast = pos + rp.span - 1;
         rp.blocked = pos < 1 || plast > seq_len || (p.ignore_lowercase && pos <= seq_len && seq[(size_t)pos - 1] >= 'a' && seq[(size_t)pos - 1] <= 'z');
-        if (rp.span > 1 && !rp.blocked) {
+        if (p.known) {
+            // onPileup with input variants (SingleSampleVariantPileupListener.java:162-176, MultisampleVariantsDetector
+            // .java:539-551): every input variant starting here, in list order; the SNVs are the device's (KP / KPM
+            // over this position's columns), the others are genotyped here
+            while (kj < vn && (*strs)[kj].first < pos) kj++;
+            for (size_t q = kj; q < vn && (*strs)[q].first == pos; q++) {
+                const StrVar& v = (*strs)[q];
+                if (v.rec < 0 || !knowns) continue;
+                KnownCall kc;
+                kc.pos = pos;
+                kc.known = v.known;
+                known_record(pileup, pos, (*knowns)[(size_t)v.rec], p, kc.line);
+                out.kcalls.push_back(std::move(kc));
+            }
+        } else if (rp.span > 1 && !rp.blocked) {
             std::string reference(seq, (size_t)pos - 1, (size_t)rp.span);
             for (char& ch : reference) ch = upper(ch);
             span_calls(pileup, pos, rp.span, calls);

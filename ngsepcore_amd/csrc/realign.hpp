@@ -37,6 +37,7 @@ struct RealignParams {
     double het_rate = 0.001;           // -h
     bool ignore_lowercase = false;     // -ignoreLowerCaseRef
     int32_t n_samples = 0;             // > 0: MultisampleVariantsDetector's listener (population mode)
+    bool known = false;                // -knownVariants: the listeners genotype the input variants (no discovery)
 };
 
 // a decided indel / STR call (callIndel + the listener's filters), its VCF line already formatted
@@ -68,6 +69,15 @@ struct PopIndel {
     std::string line;                  // the record without the sequence name: "POS\t.\tREF\tALT\t..." + '\n'
 };
 
+// -knownVariants: a genotyped input indel / MNP / other non-SNV record (a GenomicVariantImpl of VCFFileReader
+// .loadGenomicVariant, :249-253) -- its record, written whatever the genotype (the known index orders records that
+// share a position)
+struct KnownCall {
+    int32_t pos = 0;
+    int64_t known = 0;                 // index of the input variant in the context's sorted list
+    std::string line;                  // without the sequence name
+};
+
 struct RegionOut {
     int64_t first = 0, last = 0;       // the region (1-based, inclusive)
     std::vector<RegionPos> pos;        // positions with a pileup, ascending
@@ -76,18 +86,46 @@ struct RegionOut {
     std::vector<uint8_t> pcodes;       // population mode: the positions' per-sample span-1 codes (engine.hpp codes)
     std::vector<uint32_t> poff;        //   S + 2 offsets per position
     std::vector<PopIndel> pindels;
+    std::vector<KnownCall> kcalls;     // -knownVariants: the region's non-SNV input variants, genotyped (position order)
 };
 
-// an input STR variant of -knownSTRs (SingleSampleVariantsDetector.makeNonRedundantSTRs): 1-based [first, last]
+// an input variant of the indel realigner (IndelRealignerPileupListener.setInputVariants): a -knownSTRs region
+// (SingleSampleVariantsDetector.makeNonRedundantSTRs, TYPE_STR) or a -knownVariants record (findSNVS :897-905,
+// MultisampleVariantsDetector.run :432-438); 1-based [first, last]
 struct StrVar {
     int32_t first, last;
+    bool str = true;                   // TYPE_STR: the pileup at `first` gets the STR flag (:92)
+    bool event = true;                 // opens a realigner region (an STR, or a known record that is not an SNV)
+    int64_t known = -1;                // -knownVariants, not an SNV: its index in the context's list (genotyped in the region)
+    int32_t rec = -1;                  //   and its KnownRecord
+};
+
+// the input variants of one sequence in GenomicRegionPositionComparator order (first, then last; stable) and the
+// prefix maximum of `last`, so intersectWithVariants' index can be found at any position (replay_region)
+struct InputVars {
+    std::vector<StrVar> v;
+    std::vector<int32_t> pmax;
+    void finish() {
+        pmax.resize(v.size());
+        int32_t m = INT32_MIN;
+        for (size_t i = 0; i < v.size(); i++) { m = v[i].last > m ? v[i].last : m; pmax[i] = m; }
+    }
+};
+
+// a -knownVariants record that is not an SNV, as replay_region genotypes it
+struct KnownRecord {
+    std::vector<std::string> alleles;  // reference first (upper case)
+    std::string id;                    // "" for '.'
+    int16_t qs = 0;
+    int8_t type = 0;                   // INFO TYPE id (GenomicVariant.TYPE_*): printed when 2-5
 };
 
 // replays AlignmentsPileupGenerator + IndelRealignerPileupListener over [first, last] of one sequence (`seq`: the
 // reference as loaded, case kept); `reads` are the admitted alignments overlapping it in pending-list order
-// (edited in place); `strs`: the sequence's input STR variants (sorted, disjoint; may be null)
+// (edited in place); `inputs`: the sequence's realigner input variants (may be null); `knowns`: the records their
+// `known` indexes name (p.known)
 void replay_region(const std::string& seq, int64_t first, int64_t last, std::vector<RawRead>& reads, const RealignParams& p,
-                   const std::vector<StrVar>* strs, RegionOut& out);
+                   const InputVars* inputs, const std::vector<KnownRecord>* knowns, RegionOut& out);
 
 // the listener's decisions over a replayed region, position by position: kind 0 nothing, 1 the position's SNV
 // call (flag embedded: TYPE=EMBEDDED), 2 the indel call out.indels[idx].  last_indel_end is the listener's

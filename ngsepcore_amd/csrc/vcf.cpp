@@ -62,6 +62,12 @@ static inline int tri(int i, int j) {   // index of L[i][j] in the upper-triangl
 
 static void app(std::string& o, long long v) { o += std::to_string(v); }
 
+// GenomicVariantImpl.getVariantTypeName of a -knownVariants record's INFO TYPE, written when 2-5 (VCFFileWriter.java:47-49)
+static const char* type_name(int t) {
+    static const char* kNames[] = {nullptr, nullptr, "MULTISNV", "EMBEDDED", "INDEL", "STR"};
+    return t >= 2 && t <= 5 ? kNames[t] : nullptr;
+}
+
 int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& o) {
     static const char kB[] = "ACGT";
     const size_t start = o.size();
@@ -70,7 +76,9 @@ int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& o)
     while (ri < 4 && kB[ri] != s.ref) ri++;
     if (ri == 4 || s.n_alleles < 2) return 0;
     const std::string& name = (s.seq_id >= 0 && s.seq_id < (int)c->seq_names.size()) ? c->seq_names[s.seq_id] : std::string("?");
-    const char* id = known_id(c, s);              // -knownVariants: the input variant's ID
+    const ngsep_ctx::KnownVar* kv = known_of(c, s);   // -knownVariants: the input variant (its ID and INFO TYPE)
+    const char* id = kv && !kv->id.empty() ? kv->id.c_str() : nullptr;
+    const char* ktype = kv ? type_name(kv->type) : nullptr;
     if (s.pool) {
         // ploidy >= 3: genotypeVariantPool's CalledGenomicVariantImpl.  FORMAT NGSEP_NOSNV for discovery (no
         // getAllCounts), NGSEP_SNV for -knownVariants (setAllCounts) (SingleSampleVariantsDetector.java:942-946);
@@ -86,7 +94,9 @@ int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& o)
         o += name; o += '\t'; app(o, s.pos); o += '\t'; o += id ? id : "."; o += '\t'; o += (char)s.ref; o += '\t';
         for (int i = 1; i < n; i++) { if (i > 1) o += ','; o += kB[dna[i]]; }
         o += '\t'; app(o, s.qual); o += "\t.\t";
-        o += n > 2 ? "TYPE=MULTISNV" : ".";               // VCFFileWriter.java:47-49
+        if (n > 2) o += "TYPE=MULTISNV";                  // VCFFileWriter.java:47-49
+        else if (ktype) { o += "TYPE="; o += ktype; }
+        else o += '.';
         o += known ? "\tGT:PL:GQ:DP:BSDP:ACN\t" : "\tGT:PL:GQ:DP:ADP:ACN\t";
         if (nc == 0) o += "./.";
         else if (nc == 1) { app(o, c0); o += '/'; app(o, c0); }
@@ -145,6 +155,7 @@ int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& o)
     if (s.n_alleles == 2 && s.strand_bias != -1) { o += "FS="; app(o, s.strand_bias); printed = true; }
     if (s.is_call & kRecEmbedded) { if (printed) o += ';'; o += "TYPE=EMBEDDED"; printed = true; }   // -embeddedSNVs (:227)
     else if (s.n_alleles == 3) { if (printed) o += ';'; o += "TYPE=MULTISNV"; printed = true; }
+    else if (ktype) { if (printed) o += ';'; o += "TYPE="; o += ktype; printed = true; }
     if (!printed) o += '.';
     o += "\tGT:PL:GQ:DP:BSDP:ACN\t";
     if (s.n_alleles == 2) {
@@ -266,7 +277,8 @@ void format_population_site(const ngsep_ctx* c, const ngsep_popsite_out& s, cons
     const int ploidy = c->params.ploidy;
     const std::string& name = (s.seq_id >= 0 && s.seq_id < (int)c->seq_names.size()) ? c->seq_names[s.seq_id] : std::string("?");
     // -knownVariants: the input variant's ID (MultisampleVariantsDetector.java:543-545 writes the input variant)
-    const char* id = s.n_alleles == 2 ? known_id_at(c, s.seq_id, s.pos, s.alleles[1]) : nullptr;
+    const ngsep_ctx::KnownVar* kv = s.n_alleles == 2 ? known_at(c, s.seq_id, s.pos, s.alleles[1]) : nullptr;
+    const char* id = kv && !kv->id.empty() ? kv->id.c_str() : nullptr;
     o += name; o += '\t'; app(o, s.pos); o += '\t'; o += id ? id : "."; o += '\t'; o += kB[(int)s.alleles[0]]; o += '\t';
     for (int i = 1; i < s.n_alleles; i++) { if (i > 1) o += ','; o += kB[(int)s.alleles[i]]; }
     o += '\t'; app(o, s.qual); o += "\t.\t";
@@ -287,6 +299,7 @@ void format_population_site(const ngsep_ctx* c, const ngsep_popsite_out& s, cons
     if (s.n_alleles == 2) { o += ";MAF="; app_fmt2(o, ncalled < 2 ? 0.0 : (double)minAC / sum); }
     if (s.multisnv_type == 2) o += ";TYPE=EMBEDDED";        // an SNV inside an indel / STR (MultisampleVariantsDetector.java:581)
     else if (s.multisnv_type) o += ";TYPE=MULTISNV";
+    else if (kv && type_name(kv->type)) { o += ";TYPE="; o += type_name(kv->type); }   // an input record's TYPE
     o += "\tGT:PL:GQ:DP:BSDP:ACN";
     for (int k = 0; k < S; k++) {
         const ngsep_sample_call& cl = calls[k];

@@ -433,6 +433,8 @@ typedef struct ngo_call {
     int logc_present;         /* 0: no log-conditionals (an undecided call without allele calls) */
     int embedded;             /* TYPE_EMBEDDED_SNV (-embeddedSNVs inside a called indel, :227) */
     struct ngo_indel_call_s* indel;   /* an indel / STR call instead of an SNV (ngsep_oracle_indel.inc) */
+    struct ngo_kindel* kindel;        /* -knownVariants: a genotyped input indel / MNP (GenomicVariantImpl) instead */
+    int known_type;                   /* -knownVariants: the input record's INFO TYPE id (printed when 2-5) */
     /* ploidy >= 3 (genotypeVariantPool): a CalledGenomicVariantImpl over the pool variant's alleles */
     int pool;                 /* 1: the fields below describe the call, logc[][] is over the variant alleles */
     int pool_n;               /* variant alleles: DNA indexes pool_dna[0..n) (reference first) */
@@ -447,6 +449,11 @@ typedef struct ngo_call {
 typedef struct { ngo_call* c; int n, cap; } ngo_calls;
 
 static const char* BASES = "ACGT";
+/* GenomicVariantImpl.getVariantTypeName for the types a -knownVariants record can carry here (2-5) */
+static const char* type_name(int t) {
+    static const char* names[] = {NULL, NULL, "MULTISNV", "EMBEDDED", "INDEL", "STR"};
+    return t >= 2 && t <= 5 ? names[t] : NULL;
+}
 static int base_idx(char c) { const char* p = strchr(BASES, c); return (c && p) ? (int)(p - BASES) : -1; }
 
 static void print_header(FILE* out, const ngo_params* p) {
@@ -513,7 +520,9 @@ static void print_pool_call(FILE* out, const char* seqName, const ngo_call* c) {
     const int n = c->pool_n;
     fprintf(out, "%s\t%d\t%s\t%c\t", seqName, c->pos, c->id ? c->id : ".", c->ref);
     for (int i = 1; i < n; i++) fprintf(out, "%s%c", i > 1 ? "," : "", BASES[c->pool_dna[i]]);
-    fprintf(out, "\t%d\t.\t%s", c->qual, c->pool_multi ? "TYPE=MULTISNV" : ".");
+    if (c->pool_multi) fprintf(out, "\t%d\t.\tTYPE=MULTISNV", c->qual);
+    else if (type_name(c->known_type)) fprintf(out, "\t%d\t.\tTYPE=%s", c->qual, type_name(c->known_type));
+    else fprintf(out, "\t%d\t.\t.", c->qual);
     fprintf(out, c->known ? "\tGT:PL:GQ:DP:BSDP:ACN\t" : "\tGT:PL:GQ:DP:ADP:ACN\t");
     if (c->pool_ncalled == 0) fprintf(out, "./.");
     else if (c->pool_ncalled == 1) fprintf(out, "%d/%d", c->pool_called[0], c->pool_called[0]);
@@ -539,8 +548,11 @@ static void print_pool_call(FILE* out, const char* seqName, const ngo_call* c) {
 }
 
 static void print_indel_call_any(FILE* out, const char* seqName, const ngo_call* c);
+static void print_kindel(FILE* out, const char* seqName, const struct ngo_kindel* k);
+static void free_kindel(struct ngo_kindel* k);
 static void print_call(FILE* out, const char* seqName, const ngo_call* c) {
     if (c->indel) { print_indel_call_any(out, seqName, c); return; }
+    if (c->kindel) { print_kindel(out, seqName, c->kindel); return; }
     if (c->pool) { print_pool_call(out, seqName, c); return; }
     fprintf(out, "%s\t%d\t%s\t%c\t", seqName, c->pos, c->id ? c->id : ".", c->ref);
     if (c->n_alleles == 2) fprintf(out, "%c", BASES[c->idx[1]]);
@@ -551,6 +563,7 @@ static void print_call(FILE* out, const char* seqName, const ngo_call* c) {
     if (c->n_alleles == 2 && c->strand_bias != -1) { fprintf(out, "FS=%d", c->strand_bias); printed = 1; }
     if (c->embedded) { fprintf(out, "%sTYPE=EMBEDDED", printed ? ";" : ""); printed = 1; }
     else if (c->n_alleles == 3) { fprintf(out, "%sTYPE=MULTISNV", printed ? ";" : ""); printed = 1; }
+    else if (type_name(c->known_type)) { fprintf(out, "%sTYPE=%s", printed ? ";" : "", type_name(c->known_type)); printed = 1; }
     if (!printed) fprintf(out, ".");
     fprintf(out, "\tGT:PL:GQ:DP:BSDP:ACN\t");
     int ploidy = c->ploidy;
@@ -681,12 +694,20 @@ static int discover_snv(const ngo_counts* h, int pos, char refBase, const ngo_pa
 /* genotypeVariantSample (:361-391) -> VariantDiscoverySNVQAlgorithm.genotypeSNV (:21-62), biallelic  */
 /* SNVs as VCFFileReader.loadGenomicVariant makes them (vcf/VCFFileReader.java:196-260)               */
 /* ------------------------------------------------------------------ */
-typedef struct { int seq, pos; char ref, alt; int qs; char* id; } ngo_known;
+typedef struct {
+    int seq, pos, last;       /* last = pos + |REF| - 1 (GenomicVariantImpl(seq, first, alleles)) */
+    char ref, alt;            /* a biallelic SNV (snv = 1): its bases */
+    int qs; char* id;
+    int snv;                  /* 1: an SNV object (two alleles of one base each, VCFFileReader.java:243-248) */
+    int n_alleles; char** alleles;   /* a GenomicVariantImpl (snv = 0): its alleles, reference first */
+    int type;                 /* INFO TYPE (VCFFileReader.loadInfoField :274-279): 0 undetermined, 2-5 */
+} ngo_known;
 static void genotype_known(const ngo_counts* h, const ngo_known* kv, const ngo_params* p, double hetRate, ngo_call* out) {
     memset(out, 0, sizeof(*out));
     out->pos = kv->pos; out->ref = kv->ref; out->n_alleles = 2; out->known = 1; out->id = kv->id;
     out->idx[0] = base_idx(kv->ref); out->idx[1] = base_idx(kv->alt);
     out->qual = kv->qs;                         /* the input variant's QS: genotypeSNV sets none */
+    out->known_type = kv->type;
     out->strand_bias = -1;                      /* genotypeSNV(.., calcStrandBias = false) */
     out->ploidy = p->ploidy;
     out->dp = h->total_count;
@@ -751,7 +772,30 @@ typedef struct {
     ngo_alist pileup;          /* the position's alignments (PileupRecord.getAlignments) */
     struct ngo_strv* strs;     /* -knownSTRs: the realigner's input STR variants (sequence order, then first, last) */
     int n_strs, str_next;      /* str_next: IndelRealignerPileupListener.idxNextVariant over the whole list */
+    int rk_next;               /* -knownVariants: the realigner's idxNextVariant over `known` (its own index) */
 } ngo_gen;
+
+/* IndelRealignerPileupListener.intersectWithVariants (:141-157): the input variant at pos (first 0: none) -- the
+ * -knownVariants records when given (SingleSampleVariantsDetector.java:897-905, MultisampleVariantsDetector.java:
+ * 432-438), else the -knownSTRs (always TYPE_STR) */
+static void realigner_input_at(ngo_gen* G, int pos, int* first, int* last, int* is_str) {
+    *first = *last = *is_str = 0;
+    if (G->known) {
+        while (G->rk_next < G->n_known && G->known[G->rk_next].seq == G->cur_seq) {
+            const ngo_known* v = &G->known[G->rk_next];
+            if (pos < v->pos) break;
+            if (pos <= v->last) { *first = v->pos; *last = v->last; *is_str = v->type == 5; return; }
+            G->rk_next++;
+        }
+        return;
+    }
+    while (G->str_next < G->n_strs && G->strs[G->str_next].seq == G->cur_seq) {
+        const ngo_strv* v = &G->strs[G->str_next];
+        if (pos < v->first) break;
+        if (pos <= v->last) { *first = v->first; *last = v->last; *is_str = 1; return; }
+        G->str_next++;
+    }
+}
 
 /* ------------------------------------------------------------------ */
 /* RelativeAlleleCountsCalculator (discovery/RelativeAlleleCountsCalculator.java:246-331) with the     */
@@ -884,6 +928,7 @@ static void on_sequence_end(ngo_gen* G) {
     for (int i = 0; i < G->calls.n; i++) {
         print_call(G->out, G->g->s[G->cur_seq].name, &G->calls.c[i]);
         if (G->calls.c[i].indel) free_indel_call(G->calls.c[i].indel);
+        if (G->calls.c[i].kindel) free_kindel(G->calls.c[i].kindel);
     }
     G->st->variants_called += G->calls.n;
     G->calls.n = 0;
@@ -1119,7 +1164,7 @@ static void pool_known(const ngo_counts* h4, const ngo_acalls* calls, const ngo_
     if ((int16_t)p->min_quality > pc.gq) { pc.n_called = 0; pc.gq = 0; }   /* makeUndecided */
     pool_update_cn(&pc, p->ploidy);
     memset(out, 0, sizeof(*out));
-    out->pos = kv->pos; out->ref = kv->ref; out->known = 1; out->id = kv->id; out->qual = kv->qs;
+    out->pos = kv->pos; out->ref = kv->ref; out->known = 1; out->id = kv->id; out->qual = kv->qs; out->known_type = kv->type;
     out->strand_bias = -1; out->ploidy = p->ploidy;
     memcpy(out->counts, h4->counts, sizeof(out->counts));
     pool_to_call(&pc, dna, 2, out);
@@ -1140,7 +1185,7 @@ typedef struct {
 } ngo_scall;
 
 /* GenomicVariant as the MVD path builds it: reference first, then alternatives in A,C,G,T order */
-typedef struct { int n; int idx[4]; int multisnv_type; } ngo_pvar;
+typedef struct { int n; int idx[4]; int multisnv_type; int known_type; } ngo_pvar;   /* known_type: an input record's TYPE */
 
 /* CalledSNV.updateAllelesCopyNumberFromCounts (variants/CalledSNV.java:134-158); genotype -1..2 */
 static void csnv_update_cn(int genotype, const int* counts, const ngo_pvar* v, int total, int* tot_out, int* ref_out) {
@@ -1359,6 +1404,7 @@ static void mvd_print(FILE* out, const char* seqName, int pos, const char* id, c
     }
     if (v->multisnv_type == 2) fprintf(out, ";TYPE=EMBEDDED");   /* TYPE_EMBEDDED_SNV (MultisampleVariantsDetector.java:581) */
     else if (v->multisnv_type) fprintf(out, ";TYPE=MULTISNV");   /* VCFFileWriter.java:47-49 */
+    else if (type_name(v->known_type)) fprintf(out, ";TYPE=%s", type_name(v->known_type));
     fprintf(out, "\tGT:PL:GQ:DP:BSDP:ACN");
     for (int s = 0; s < M->n_samples; s++) {
         const ngo_scall* c = &M->calls[s];
@@ -1428,7 +1474,7 @@ static int mvd_snv_variant(ngo_gen* G, char R, const ngo_counts* pooled, ngo_pva
     int sum = pooled->counts[0] + pooled->counts[1] + pooled->counts[2] + pooled->counts[3];
     double minCount = M->min_adf * sum;
     if (minCount < 1) minCount = 1;
-    ngo_pvar v = {0, {0}, 0};
+    ngo_pvar v = {0, {0}, 0, 0};
     v.idx[v.n++] = refIdx;
     for (int i = 0; i < 4; i++)
         if (pooled->counts[i] >= minCount && i != refIdx) v.idx[v.n++] = i;
@@ -1444,7 +1490,7 @@ static int mvd_snv_variant(ngo_gen* G, char R, const ngo_counts* pooled, ngo_pva
             for (int i = 0; i < M->calls[s].n_called; i++) called[v.idx[M->calls[s].called[i]]] = 1;
         int nset = called[0] + called[1] + called[2] + called[3];
         if (nset == v.n) break;
-        ngo_pvar nv = {0, {0}, 0};
+        ngo_pvar nv = {0, {0}, 0, 0};
         nv.idx[nv.n++] = v.idx[0];
         for (int i = 0; i < 4; i++) if (called[i] && i != v.idx[0]) nv.idx[nv.n++] = i;
         v = nv;   /* SNV (BIALLELIC type) or GenomicVariantImpl (UNDETERMINED type): no TYPE annotation */
@@ -1454,6 +1500,7 @@ static int mvd_snv_variant(ngo_gen* G, char R, const ngo_counts* pooled, ngo_pva
     return 1;
 }
 
+static void mvd_on_pileup_known(ngo_gen* G, int pos);
 /* MultisampleVariantsDetector.onPileup (:522-558) without the indel realigner (indel pass-through) */
 static void mvd_on_pileup(ngo_gen* G, int pos) {
     ngo_mvd* M = G->mvd;
@@ -1465,26 +1512,10 @@ static void mvd_on_pileup(ngo_gen* G, int pos) {
         /* calculateReferenceAlleleDiscovery (SingleSampleVariantPileupListener.java:191-206) */
         if (p->ignore_lowercase_ref && islower((unsigned char)r)) return;
     }
+    if (G->known) { mvd_on_pileup_known(G, pos); return; }
     char R = (char)toupper((unsigned char)r);
     ngo_counts pooled;
     mvd_snv_counts(G, pos, G->pending.a, G->pending.n, &pooled);
-    if (G->known) {
-        /* onPileup with input variants (MultisampleVariantsDetector.java:539-551): every input variant at this
-         * position (nextSIVIndex), genotypeVariant (:664-693) over its own alleles, the record always written
-         * (QUAL = the variant QS genotypeVariant sets, ID = the input's) */
-        while (G->known_next < G->n_known && G->known[G->known_next].seq == G->cur_seq && G->known[G->known_next].pos <= pos) {
-            const ngo_known* kv = &G->known[G->known_next++];
-            if (kv->pos != pos) continue;
-            ngo_pvar kvv = {0, {0}, 0};
-            kvv.idx[kvv.n++] = base_idx(kv->ref);
-            kvv.idx[kvv.n++] = base_idx(kv->alt);
-            int kqs = 0;
-            mvd_genotype_all(M, &kvv, G->het_rate, &kqs);
-            mvd_print(G->out, sq->name, pos, kv->id, &kvv, kqs, M);
-            G->st->variants_called++;
-        }
-        return;
-    }
     ngo_pvar v;
     if (!mvd_snv_variant(G, R, &pooled, &v)) return;
     int qs = 0;
@@ -1554,7 +1585,7 @@ static void iscall_update_cn(ngo_iscall* c, int n, int total) {
  * the variant (indexes of the maximum genotype taken as they are, :335-345), updateAllelesCopyNumberFromCounts(ploidy),
  * makeUndecided below 40 (:320-325) */
 static void genotype_indel_sample(const ngo_sv* alleles, const ngo_icalls* calls, double het, int ploidy, int max_base_qs,
-                                  ngo_iscall* c) {
+                                  int min_quality, ngo_iscall* c) {
     const int n = alleles->n;
     memset(c, 0, sizeof(*c));
     c->counts = calloc((size_t)n, sizeof(int));
@@ -1605,7 +1636,7 @@ static void genotype_indel_sample(const ngo_sv* alleles, const ngo_icalls* calls
     memcpy(c->logc, ih.logc, sizeof(double) * (size_t)n * n);
     free(ih.counts); free(ih.logc);
     iscall_update_cn(c, n, ploidy);
-    if (40 > c->gq) { c->n_called = 0; c->gq = 0; iscall_update_cn(c, n, c->total_cn); }
+    if ((int16_t)min_quality > c->gq) { c->n_called = 0; c->gq = 0; iscall_update_cn(c, n, c->total_cn); }
 }
 
 /* the sample's span calls, PileupRecord.getAlleleCalls(span, sample.getReadGroups()) (:104-111): read groups in
@@ -1631,7 +1662,7 @@ static int mvd_genotype_indel_all(ngo_gen* G, int pos, const ngo_sv* alleles, ng
     const int span = (int)strlen(alleles->s[0]);
     for (int s = 0; s < M->n_samples; s++) {
         sample_span_calls(G, s, pos, span, &tmp, &ic);
-        genotype_indel_sample(alleles, &ic, G->het_rate, M->ploidy, G->p->max_base_qs, &calls[s]);
+        genotype_indel_sample(alleles, &ic, G->het_rate, M->ploidy, G->p->max_base_qs, 40, &calls[s]);
         for (int i = 0; i < ic.n; i++) { free(ic.c[i].allele); free(ic.c[i].qual); }
         ic.n = 0;
         const ngo_iscall* c = &calls[s];
@@ -1692,11 +1723,12 @@ static int mvd_discover_indel(ngo_gen* G, int pos, const char* ref, int input_st
 
 /* VCFRecord.createDefaultPopulationVCFRecord (vcf/VCFRecord.java:277-282, FORMAT DEF_FORMAT_ARRAY_NGSEP_NOSNV) +
  * VCFFileWriter.printVCFRecord / printGenotypeInfo (:44-68,159-256) for an indel / STR variant */
-static void mvd_print_indel(ngo_gen* G, const char* seqName, int pos, const ngo_sv* v, int is_str, int qs, const ngo_iscall* calls) {
+static void mvd_print_indel(ngo_gen* G, const char* seqName, int pos, const char* id, const ngo_sv* v, const char* type, int qs,
+                            const ngo_iscall* calls) {
     ngo_mvd* M = G->mvd;
     FILE* out = G->out;
     const int n = v->n, S = M->n_samples;
-    fprintf(out, "%s\t%d\t.\t%s\t", seqName, pos, v->s[0]);
+    fprintf(out, "%s\t%d\t%s\t%s\t", seqName, pos, id ? id : ".", v->s[0]);
     if (n == 1) fprintf(out, ".");
     for (int i = 1; i < n; i++) fprintf(out, "%s%s", i > 1 ? "," : "", v->s[i]);
     fprintf(out, "\t%d\t.\t", qs);
@@ -1719,7 +1751,8 @@ static void mvd_print_indel(ngo_gen* G, const char* seqName, int pos, const ngo_
     fprintf(out, ";OH=%s", buf);
     if (n == 2) { ngo_java_fmt2(ncalled < 2 ? 0.0 : (double)minAC / sum, buf, sizeof buf); fprintf(out, ";MAF=%s", buf); }
     free(counts);
-    fprintf(out, ";TYPE=%s\tGT:PL:GQ:DP:ADP:ACN", is_str ? "STR" : "INDEL");
+    if (type) fprintf(out, ";TYPE=%s", type);
+    fprintf(out, "\tGT:PL:GQ:DP:ADP:ACN");
     for (int s = 0; s < S; s++) {
         const ngo_iscall* c = &calls[s];
         fprintf(out, "\t");
@@ -1820,7 +1853,7 @@ void ngo_t_genotype_indel_sample(int n, const char* const* alleles, int m, const
     t_alleles(n, alleles, &al);
     t_calls(m, calls, quals, &ic);
     ngo_iscall c;
-    genotype_indel_sample(&al, &ic, het, ploidy, max_base_qs, &c);
+    genotype_indel_sample(&al, &ic, het, ploidy, max_base_qs, 40, &c);
     int k = 0;
     if (c.n_called == 0) k += snprintf(out + k, (size_t)(cap - k), ploidy > 1 ? "./." : ".");
     else if (c.n_called == 1) k += snprintf(out + k, (size_t)(cap - k), ploidy > 1 ? "%d/%d" : "%d", c.called[0], c.called[0]);
@@ -1895,7 +1928,7 @@ static void mvd_on_pileup_realign(ngo_gen* G, int pos, int span, int is_str, int
             ngo_iscall* sc = calloc((size_t)(M->n_samples ? M->n_samples : 1), sizeof(ngo_iscall));
             const int qs = mvd_genotype_indel_all(G, pos, &v, sc);
             if (!(qs == 0 || qs < p->min_quality)) {
-                mvd_print_indel(G, sq->name, pos, &v, is_str, qs, sc);
+                mvd_print_indel(G, sq->name, pos, NULL, &v, is_str ? "STR" : "INDEL", qs, sc);
                 G->st->variants_called++;
                 G->last_indel_end = pos + (int)strlen(v.s[0]) - 1;   /* !variant.isSNV(): lastIndelEnd = variant.getLast() */
             }
@@ -1916,6 +1949,111 @@ static void mvd_on_pileup_realign(ngo_gen* G, int pos, int span, int is_str, int
     mvd_print(G->out, sq->name, pos, NULL, &v, qs, M);
     G->st->variants_called++;
 }
+
+/* the position's alignments as PileupRecord.getAlignments (built by the realigner's step; here when it is off) */
+static void ensure_pileup(ngo_gen* G, int pos) {
+    if (G->realign) return;
+    G->pileup.n = 0;
+    for (int k = 0; k < G->pending.n; k++) {
+        ngo_aln* a = G->pending.a[k];
+        if (a->first <= pos && a->last >= pos) alist_push(&G->pileup, a);
+    }
+}
+static void known_alleles(const ngo_known* kv, ngo_sv* v) {
+    for (int i = 0; i < kv->n_alleles; i++) sv_push(v, kv->alleles[i], (int)strlen(kv->alleles[i]));
+}
+
+/* MultisampleVariantsDetector.onPileup with input variants (:539-551): every input variant at this position
+ * (nextSIVIndex), genotypeVariant (:664-693) over its own alleles -- an SNV through the per-sample SNV counts, an
+ * indel / MNP through every sample's getAlleleCalls(|REF|, readGroups) and callIndel with the variant (fresh
+ * listener: minQuality 40) -- and the record always written (QUAL = the variant QS genotypeVariant sets, ID and
+ * TYPE the input's) */
+static void mvd_on_pileup_known(ngo_gen* G, int pos) {
+    ngo_mvd* M = G->mvd;
+    const ngo_seq* sq = &G->g->s[G->cur_seq];
+    int counted = 0;
+    ngo_counts pooled;
+    while (G->known_next < G->n_known && G->known[G->known_next].seq == G->cur_seq && G->known[G->known_next].pos <= pos) {
+        const ngo_known* kv = &G->known[G->known_next++];
+        if (kv->pos != pos) continue;
+        if (kv->snv) {
+            if (!counted) {
+                if (G->realign) mvd_snv_counts(G, pos, G->pileup.a, G->pileup.n, &pooled);
+                else mvd_snv_counts(G, pos, G->pending.a, G->pending.n, &pooled);
+                counted = 1;
+            }
+            ngo_pvar kvv = {0, {0}, 0, kv->type};
+            kvv.idx[kvv.n++] = base_idx(kv->ref);
+            kvv.idx[kvv.n++] = base_idx(kv->alt);
+            int kqs = 0;
+            mvd_genotype_all(M, &kvv, G->het_rate, &kqs);
+            mvd_print(G->out, sq->name, pos, kv->id, &kvv, kqs, M);
+        } else {
+            ensure_pileup(G, pos);
+            ngo_sv v = {0};
+            known_alleles(kv, &v);
+            ngo_iscall* sc = calloc((size_t)(M->n_samples ? M->n_samples : 1), sizeof(ngo_iscall));
+            const int qs = mvd_genotype_indel_all(G, pos, &v, sc);
+            mvd_print_indel(G, sq->name, pos, kv->id, &v, type_name(kv->type), qs, sc);
+            for (int s = 0; s < M->n_samples; s++) iscall_free(&sc[s]);
+            free(sc);
+            sv_free(&v);
+        }
+        G->st->variants_called++;
+    }
+}
+
+/* a genotyped -knownVariants indel / MNP of the single-sample listener */
+struct ngo_kindel { ngo_iscall c; const ngo_known* kv; int ploidy; };
+
+/* SingleSampleVariantPileupListener.genotypeVariantSample (:361-391), non-SNV branch at ploidy < 3: getAlleleCalls(
+ * |REF|, null), calculateCountsIndel over the variant's alleles, callIndel with the variant (VariantDiscoverySNVQ
+ * Algorithm.java:265-361), updateAllelesCopyNumberFromCounts(ploidy), makeUndecided below -minQuality */
+static void genotype_known_indel(ngo_gen* G, const ngo_known* kv, int pos, ngo_call* out) {
+    const ngo_params* p = G->p;
+    ensure_pileup(G, pos);
+    ngo_sv v = {0};
+    known_alleles(kv, &v);
+    ngo_icalls calls = {0};
+    pileup_calls(G->pileup.a, G->pileup.n, pos, (int)strlen(kv->alleles[0]), &calls);
+    struct ngo_kindel* k = calloc(1, sizeof(*k));
+    genotype_indel_sample(&v, &calls, G->het_rate, p->ploidy, p->max_base_qs, p->min_quality, &k->c);
+    k->kv = kv;
+    k->ploidy = p->ploidy;
+    icalls_free(&calls);
+    sv_free(&v);
+    memset(out, 0, sizeof(*out));
+    out->pos = pos;
+    out->known = 1;
+    out->kindel = k;
+}
+
+/* VCFFileWriter.printVCFRecord of the call: the input's ID, alleles, QS and TYPE, FORMAT DEF_FORMAT_ARRAY_NGSEP_NOSNV */
+static void print_kindel(FILE* out, const char* seqName, const struct ngo_kindel* k) {
+    const ngo_known* kv = k->kv;
+    const ngo_iscall* c = &k->c;
+    const int n = kv->n_alleles;
+    fprintf(out, "%s\t%d\t%s\t%s\t", seqName, kv->pos, kv->id ? kv->id : ".", kv->alleles[0]);
+    for (int i = 1; i < n; i++) fprintf(out, "%s%s", i > 1 ? "," : "", kv->alleles[i]);
+    fprintf(out, "\t%d\t.\t", kv->qs);
+    if (type_name(kv->type)) fprintf(out, "TYPE=%s", type_name(kv->type));
+    else fprintf(out, ".");
+    fprintf(out, "\tGT:PL:GQ:DP:ADP:ACN\t");
+    if (c->n_called == 0) fprintf(out, k->ploidy > 1 ? "./." : ".");
+    else if (c->n_called == 1) { fprintf(out, "%d", c->called[0]); if (k->ploidy > 1) fprintf(out, "/%d", c->called[0]); }
+    else fprintf(out, "%d/%d", c->called[0], c->called[1]);
+    fprintf(out, ":");
+    for (int j = 0; j < n; j++)
+        for (int i = 0; i <= j; i++)
+            fprintf(out, "%s%d", (i > 0 || j > 0) ? "," : "", c->has_report ? (int)ngo_java_round(-10 * c->logc[i * n + j]) : 0);
+    fprintf(out, ":%d:%d:", c->gq, c->dp);
+    for (int i = 0; i < n; i++) fprintf(out, "%s%d", i ? "," : "", c->has_report ? c->counts[i] : 0);
+    fprintf(out, ":");
+    if (c->total_cn == 0) fprintf(out, ".");
+    else for (int j = 0; j < n; j++) fprintf(out, "%s%d", j ? "," : "", (c->n_called == 0 && j == 0) ? c->total_cn : c->acn[j]);
+    fprintf(out, "\n");
+}
+static void free_kindel(struct ngo_kindel* k) { iscall_free(&k->c); free(k); }
 
 static void push_call(ngo_gen* G, const ngo_call* c) {
     if (G->calls.n == G->calls.cap) { G->calls.cap = G->calls.cap ? 2 * G->calls.cap : 1024; G->calls.c = realloc(G->calls.c, sizeof(ngo_call) * G->calls.cap); }
@@ -2022,16 +2160,12 @@ static int process_current_position(ngo_gen* G) {
                     ngo_aln* a = G->pending.a[k];
                     if (a->first <= pos && a->last >= pos) alist_push(&G->pileup, a);
                 }
-                int var_first = 0, var_last = 0, is_str = 0, is_new_str = 0, r_embedded = 0;
-                while (G->str_next < G->n_strs && G->strs[G->str_next].seq == G->cur_seq) {
-                    const ngo_strv* v = &G->strs[G->str_next];
-                    if (pos < v->first) break;
-                    if (pos <= v->last) { var_first = v->first; var_last = v->last; break; }
-                    G->str_next++;
-                }
+                int var_first, var_last, var_str, is_str = 0, is_new_str = 0, r_embedded = 0;
+                realigner_input_at(G, pos, &var_first, &var_last, &var_str);
                 const int span = realigner_on_pileup(&G->g->s[G->cur_seq], G->pileup.a, G->pileup.n, pos, var_first, var_last,
-                                                     &is_str, &is_new_str, &r_embedded);
-                mvd_on_pileup_realign(G, pos, span, is_str, is_new_str, r_embedded);
+                                                     var_str, &is_str, &is_new_str, &r_embedded);
+                if (G->known) mvd_on_pileup_known(G, pos);
+                else mvd_on_pileup_realign(G, pos, span, is_str, is_new_str, r_embedded);
             } else {
                 mvd_on_pileup(G, pos);
             }
@@ -2049,15 +2183,9 @@ static int process_current_position(ngo_gen* G) {
             if (a->first <= pos && a->last >= pos) alist_push(&G->pileup, a);
         }
         if (G->pileup.n > 0) {
-            int var_first = 0, var_last = 0;
-            /* intersectWithVariants (IndelRealignerPileupListener.java:137-153) over the input STRs */
-            while (G->str_next < G->n_strs && G->strs[G->str_next].seq == G->cur_seq) {
-                const ngo_strv* v = &G->strs[G->str_next];
-                if (pos < v->first) break;
-                if (pos <= v->last) { var_first = v->first; var_last = v->last; break; }
-                G->str_next++;
-            }
-            span = realigner_on_pileup(&G->g->s[G->cur_seq], G->pileup.a, G->pileup.n, pos, var_first, var_last, &is_str,
+            int var_first, var_last, var_str;
+            realigner_input_at(G, pos, &var_first, &var_last, &var_str);
+            span = realigner_on_pileup(&G->g->s[G->cur_seq], G->pileup.a, G->pileup.n, pos, var_first, var_last, var_str, &is_str,
                                        &is_new_str, &r_embedded);
         }
     }
@@ -2097,7 +2225,8 @@ static int process_current_position(ngo_gen* G) {
                 const ngo_known* kv = &G->known[G->known_next++];
                 if (kv->pos != pos) continue;
                 ngo_call c;
-                if (pool) pool_known(&h, &G->acalls, kv, p, G->het_rate, &c);
+                if (!kv->snv) genotype_known_indel(G, kv, pos, &c);
+                else if (pool) pool_known(&h, &G->acalls, kv, p, G->het_rate, &c);
                 else genotype_known(&h, kv, p, G->het_rate, &c);
                 if (G->calls.n == G->calls.cap) { G->calls.cap = G->calls.cap ? 2 * G->calls.cap : 1024; G->calls.c = realloc(G->calls.c, sizeof(ngo_call) * G->calls.cap); }
                 G->calls.c[G->calls.n++] = c;
@@ -2192,6 +2321,7 @@ static void process_alignment(ngo_gen* G, ngo_aln* a) {
         if (G->known) {          /* onSequenceStart: this sequence's input variants, nextSIVIndex = 0 */
             G->known_next = 0;
             while (G->known_next < G->n_known && G->known[G->known_next].seq != a->seq) G->known_next++;
+            G->rk_next = G->known_next;                        /* and the realigner's idxNextVariant */
         }
     }
     if (a->last > G->cur_last) G->cur_last = a->last;
@@ -2220,13 +2350,24 @@ static char* split_tab(char** s) {
 }
 
 /* VCFFileReader.loadVariants(file, true, true) (vcf/VCFFileReader.java:585-600) sorted as a
- * GenomicRegionSortedCollection over the genome's sequences (stable: input order at equal positions).
- * Only biallelic SNVs (one-base REF and ALT in ACGT) are supported; ALT '.' records are skipped
- * (filterReferenceSitesGVCF); records on sequences outside the genome are skipped. */
+ * GenomicRegionSortedCollection over the genome's sequences (GenomicRegionPositionComparator: first, then last;
+ * stable).  loadGenomicVariant (:192-255): a biallelic SNV object for one-base ACGT REF and ALT, else a
+ * GenomicVariantImpl over REF and the ALT alleles (indels, MNPs, alleles with N); a multi-allelic SNV (every allele
+ * one ACGT base) is refused (NGO_UNSUPPORTED).  ALT '.' records are skipped (filterReferenceSitesGVCF), so are
+ * structural types (filterSVs) and records on sequences outside the genome. */
+static void known_free(ngo_known* v, int n) {
+    for (int i = 0; i < n; i++) {
+        free(v[i].id);
+        for (int j = 0; j < v[i].n_alleles; j++) free(v[i].alleles[j]);
+        free(v[i].alleles);
+    }
+    free(v);
+}
 static int known_cmp(const void* a, const void* b) {
     const ngo_known *x = a, *y = b;
     if (x->seq != y->seq) return x->seq < y->seq ? -1 : 1;
     if (x->pos != y->pos) return x->pos < y->pos ? -1 : 1;
+    if (x->last != y->last) return x->last < y->last ? -1 : 1;
     return 0;
 }
 static int load_known(const char* path, const ngo_genome* g, ngo_known** out, int* n_out) {
@@ -2237,23 +2378,86 @@ static int load_known(const char* path, const ngo_genome* g, ngo_known** out, in
     while ((l = getline(&line, &cap, f)) >= 0) {
         while (l > 0 && (line[l - 1] == '\n' || line[l - 1] == '\r')) line[--l] = 0;
         if (l == 0 || line[0] == '#') continue;
-        char* fld[6]; int k = 0; char* s2 = line;
-        while (k < 6) { fld[k++] = s2; char* t = strchr(s2, '\t'); if (!t) break; *t = 0; s2 = t + 1; }
+        char* fld[8]; int k = 0; char* s2 = line;
+        while (k < 8) { fld[k++] = s2; char* t = strchr(s2, '\t'); if (!t) break; *t = 0; s2 = t + 1; }
         if (k < 6) { rc = NGO_ERR_ARG; break; }
-        if (fld[4][0] == '.') continue;
+        if (fld[4][0] == '.') continue;                        /* loadVariants: reference sites (< 2 alleles) */
         const int seq = genome_find(g, fld[0]);
         if (seq < 0) continue;
-        if (strlen(fld[3]) != 1 || strlen(fld[4]) != 1 || !strchr("ACGT", fld[3][0]) || !strchr("ACGT", fld[4][0])) { rc = NGO_UNSUPPORTED; break; }
+        /* loadInfoField (:261-305), attribute by attribute: TYPE sets a type id in (0, TYPE_INVERSION], SVTYPE one >= 10
+         * (GenomicVariantImpl.getVariantTypeId names, GenomicVariant.java:32-56), END the last position of a
+         * GenomicVariantImpl */
+        int type = 0, end = 0;
+        if (k >= 8 && strcmp(fld[7], ".") != 0) {
+            static const char* kNames[] = {"SNV", "MULTISNV", "EMBEDDED", "INDEL", "STR", "CNV", "REPEAT", "DEL", "INS", "INV", "DUP",
+                                           "Deletion", "Insertion"};
+            static const int kIds[] = {1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 15, 12, 13};
+            for (char* t = fld[7]; t && *t;) {
+                char* e = strchr(t, ';');
+                if (e) *e = 0;
+                int is_type = strncmp(t, "TYPE=", 5) == 0, is_sv = strncmp(t, "SVTYPE=", 7) == 0;
+                if (is_type || is_sv) {
+                    const char* name = t + (is_type ? 5 : 7);
+                    int id = 0;
+                    for (int q = 0; q < 13; q++) if (strcmp(name, kNames[q]) == 0) id = kIds[q];
+                    if (is_type && id > 0 && id <= 14) type = id;
+                    if (is_sv && id >= 10) type = id;
+                }
+                if (strncmp(t, "END=", 4) == 0) end = atoi(t + 4);
+                t = e ? e + 1 : NULL;
+            }
+        }
+        if (type >= 10) continue;                              /* loadVariants: filterSVs (isStructural) */
+        /* the alleles: REF, then ALT split at commas */
+        int na = 1;
+        for (const char* t = fld[4]; *t; t++) na += *t == ',';
+        na += 1;
+        int snv = na == 2 && strlen(fld[3]) == 1 && strlen(fld[4]) == 1 && strchr("ACGT", fld[3][0]) && strchr("ACGT", fld[4][0]);
+        int allsnv = 1;                                        /* GenomicVariantImpl.isSNV: every allele one base */
+        if (!snv) {
+            if (strlen(fld[3]) != 1 || !strchr("ACGT", fld[3][0])) allsnv = 0;
+            for (char* t = fld[4]; allsnv && *t;) {
+                char* e = strchr(t, ',');
+                const size_t len = e ? (size_t)(e - t) : strlen(t);
+                if (len != 1 || !strchr("ACGT", t[0])) allsnv = 0;
+                t = e ? e + 1 : t + len;
+            }
+            if (allsnv) { rc = NGO_UNSUPPORTED; break; }       /* multi-allelic SNV inputs: not supported here */
+        }
         int qs = 0;
         if (fld[5][0] && fld[5][0] != '.') { double q = atof(fld[5]); if (q > 32767) q = 255; qs = (int)ngo_java_round(q); }
         if (n == vc) { vc = vc ? 2 * vc : 256; v = realloc(v, sizeof(ngo_known) * vc); }
-        v[n].seq = seq; v[n].pos = atoi(fld[1]); v[n].ref = fld[3][0]; v[n].alt = fld[4][0]; v[n].qs = qs;
-        v[n].id = strcmp(fld[2], ".") == 0 ? NULL : strdup(fld[2]);
+        ngo_known* kv = &v[n];
+        memset(kv, 0, sizeof(*kv));
+        kv->seq = seq; kv->pos = atoi(fld[1]); kv->qs = qs; kv->snv = snv; kv->type = type;
+        kv->id = strcmp(fld[2], ".") == 0 ? NULL : strdup(fld[2]);
+        kv->last = kv->pos + (int)strlen(fld[3]) - 1;
+        if (!snv && end > 0) kv->last = end;                   /* the END attribute of a GenomicVariantImpl (:282-289) */
+        if (snv) { kv->ref = fld[3][0]; kv->alt = fld[4][0]; }
+        else {
+            kv->n_alleles = na;
+            kv->alleles = malloc(sizeof(char*) * (size_t)na);
+            kv->alleles[0] = strdup(fld[3]);
+            int j = 1;
+            for (char* t = fld[4]; *t && j < na;) {
+                char* e = strchr(t, ',');
+                const size_t len = e ? (size_t)(e - t) : strlen(t);
+                kv->alleles[j] = strndup(t, len);
+                for (char* c = kv->alleles[j]; *c; c++) *c = (char)toupper((unsigned char)*c);
+                j++;
+                t = e ? e + 1 : t + len;
+            }
+            for (char* c = kv->alleles[0]; *c; c++) *c = (char)toupper((unsigned char)*c);
+            kv->n_alleles = j;
+            int dup = 0;                                       /* a repeated allele: refused (not restated) */
+            for (int x = 0; x < j; x++) for (int y = 0; y < x; y++) dup |= strcmp(kv->alleles[x], kv->alleles[y]) == 0;
+            if (dup || j > 100) { n++; rc = NGO_UNSUPPORTED; break; }
+        }
         n++;
     }
     free(line); fclose(f);
-    if (rc != NGO_OK) { for (int i = 0; i < n; i++) free(v[i].id); free(v); return rc; }
-    /* stable sort: (seq, pos) then input index */
+    if (rc != NGO_OK) { known_free(v, n); return rc; }
+    /* GenomicRegionSortedCollection: GenomicRegionPositionComparator (first, then last), stable */
     int* ord = malloc(sizeof(int) * (n > 0 ? n : 1));
     for (int i = 0; i < n; i++) ord[i] = i;
     for (int i = 1; i < n; i++) {          /* insertion sort keeps equal keys in order; input is nearly sorted */
@@ -2417,16 +2621,24 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
     if (!multisample && !p->het_rate_set && p->ploidy == 1) G.het_rate = 1e-6;
     G.cov = cov;
     G.rac = rac;
-    /* the indel realigner: single-sample discovery at ploidy < 3, and MultisampleVariantsDetector at ploidy < 3 (its
-     * chain, :449-450); not with -knownVariants (the realigner's input variants) -- those runs stay pass-through */
-    G.realign = !cov && !rac && !p->indel_passthrough && p->ploidy < 3 && !(p->known_vcf && p->known_vcf[0]);
+    /* the indel realigner: first in both detectors' listener chains (SingleSampleVariantsDetector.java:919-925,
+     * MultisampleVariantsDetector.java:449-450), at ploidy < 3 here; with -knownVariants its input variants are the
+     * known records (fixed events), else the -knownSTRs */
+    G.realign = !cov && !rac && !p->indel_passthrough && p->ploidy < 3;
     if (p->known_vcf && p->known_vcf[0]) {
-        if (load_known(p->known_vcf, &g, &G.known, &G.n_known) != NGO_OK) {
+        int lrc = load_known(p->known_vcf, &g, &G.known, &G.n_known);
+        if (lrc == NGO_OK && p->ploidy >= 3)               /* the pool algorithm's indel branch is not restated */
+            for (int i = 0; i < G.n_known; i++) if (!G.known[i].snv) { lrc = NGO_UNSUPPORTED; break; }
+        if (lrc != NGO_OK) {
+            if (G.known) known_free(G.known, G.n_known);
             fclose(in); if (out != stdout) fclose(out); if (dump) fclose(dump);
-            return NGO_UNSUPPORTED;
+            return lrc == NGO_ERR_IO ? NGO_ERR_IO : NGO_UNSUPPORTED;
         }
+        /* inputVariants.size() == 0: the listeners discover (SingleSampleVariantPileupListener.java:148, Multisample
+         * VariantsDetector.java:523); the -knownSTRs stay unread (else-if, :906) */
+        if (G.n_known == 0) { known_free(G.known, 0); G.known = NULL; }
     }
-    if (G.realign && p->known_strs && p->known_strs[0]) {
+    if (G.realign && !(p->known_vcf && p->known_vcf[0]) && p->known_strs && p->known_strs[0]) {
         if (load_known_strs(p->known_strs, &g, &G.strs, &G.n_strs) != NGO_OK) {
             fclose(in); if (out != stdout) fclose(out); if (dump) fclose(dump);
             return NGO_ERR_IO;
@@ -2596,11 +2808,13 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
     for (int i = 0; i < G.pending.n; i++) aln_free(G.pending.a[i]);
     for (int i = 0; i < G.ss_primary.n; i++) aln_free(G.ss_primary.a[i]);
     for (int i = 0; i < G.ss_secondary.n; i++) aln_free(G.ss_secondary.a[i]);
-    for (int i = 0; i < G.calls.n; i++) if (G.calls.c[i].indel) free_indel_call(G.calls.c[i].indel);
+    for (int i = 0; i < G.calls.n; i++) {
+        if (G.calls.c[i].indel) free_indel_call(G.calls.c[i].indel);
+        if (G.calls.c[i].kindel) free_kindel(G.calls.c[i].kindel);
+    }
     free(G.pending.a); free(G.ss_primary.a); free(G.ss_secondary.a); free(G.retired.a); free(G.calls.c); free(G.acalls.c); free(G.pileup.a);
     free(G.strs);
-    for (int i = 0; i < G.n_known; i++) free(G.known[i].id);
-    free(G.known);
+    if (G.known) known_free(G.known, G.n_known);
     for (int i = 0; i < g.n; i++) { free(g.s[i].name); free(g.s[i].seq); }
     free(g.s);
     for (int i = 0; i < rgs.n; i++) free(rgs.ids[i]);

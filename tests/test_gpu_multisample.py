@@ -219,3 +219,49 @@ def test_population_indels_vcf_identical(tmp_path, kw, opts):
     det.run(bams).close()
     d = diff_vcf(o, det.outFilename)
     assert not d, "\n".join(d[:20])
+
+
+@pytest.mark.parametrize("kw,opts", [
+    (dict(n_samples=12, depth=10, seed=31, indel_rate=4e-4, snv_rate=2e-3), {}),
+    (dict(n_samples=10, depth=12, seed=32, indel_rate=5e-4, snv_rate=2e-3), {"ploidy": 1, "het_rate": 0.01}),
+])
+def test_population_known_indels(tmp_path, kw, opts):
+    """`MultisampleVariantsDetector -knownVariants` with indel / MNP inputs on data with indels: the records are the
+    realigner's input variants (MultisampleVariantsDetector.run :432-438), every input SNV is genotyped by KPM from
+    the realigned columns and every other record in every sample by callIndel with the variant given
+    (genotypeVariant :664-693); the WHOLE population VCF equals the oracle's, through path A and path B."""
+    from test_gpu_known import _known_vcf_indels
+    from ngsepcore_amd import MultisampleVariantsDetector
+    syn, fa, sam, rgs = population(tmp_path, genome=pysynth.CUSTOM, custom_len=50000, **kw)
+    disc = oracle_mvd(tmp_path, fa, sam, 0.0, **opts)
+    known = os.path.join(str(tmp_path), "known.vcf")
+    n = _known_vcf_indels(known, syn, disc, kw["seed"], n_random=150)
+    o = os.path.join(str(tmp_path), "o.vcf")
+    ngsep_oracle.run_mvd(fa, sam, o, 0.0, known_vcf=known, **oracle_params_from(opts))
+    ro = [l for l in open(o) if not l.startswith("#")]
+    assert len(ro) > n // 2
+    assert sum(1 for l in ro if len(l.split("\t")[3]) > 1 or len(l.split("\t")[4]) > 1) > 30
+    g = os.path.join(str(tmp_path), "gpu_a.vcf")
+    with GpuPileupSession(gpu_params(multisample=1, **opts)) as s:
+        s.set_samples(rgs)
+        for name, seq in syn.contigs():
+            s.set_reference(name, seq)
+        s.set_known_variants(known)
+        s.processAlignments(syn.batch())
+        s.notifyEndOfAlignments()
+        s.write_population_vcf(g)
+        assert not s.carved_regions()
+    d = diff_vcf(o, g)
+    assert not d, "\n".join(d[:20])
+    bams = syn.write_sample_bams(os.path.join(str(tmp_path), "pop"))
+    det = MultisampleVariantsDetector()
+    for k, v in opts.items():
+        setattr(det.params, k, v)
+    if "het_rate" in opts:
+        det.params.het_rate_set = 1
+    det.setGenome(fa)
+    det.setKnownVariantsFile(known)
+    det.setOutFilename(os.path.join(str(tmp_path), "gpu_b.vcf"))
+    det.run(bams).close()
+    d = diff_vcf(o, det.outFilename)
+    assert not d, "\n".join(d[:20])
