@@ -320,6 +320,16 @@ int ngsep_call_bam(ngsep_ctx* ctx, const char* bam_path, const char* out_vcf_pat
  * ReadAlignmentFileReader.java:171-183).  Writes the VCF header and the region's calls to out_vcf_path. */
 int ngsep_call_region_bam(ngsep_ctx* ctx, const char* bam_path, const char* seq, int64_t first, int64_t last,
                           const char* out_vcf_path);
+/* ABI 9: a window boundary for the sharded drivers: the first position *cut >= pos of seq that no
+ * indel realigner event can reach -- outside [first - M, last + indel bases + M] of every alignment with I/D in the
+ * files (and of every region-opening input variant), M = 2 x the longest alignment span around pos + 100 -- and
+ * *lead = M + that span.  A region run of seq:(cut_k - lead_k)..(cut_k+1 - 1) (ngsep_call_region_bam /
+ * ngsep_call_population_region_bams) calls every position in [cut_k, cut_k+1) as the whole-file run does
+ * (IndelRealignerPileupListener's state and the listeners' lastIndelEnd are fresh there; AlignmentsPileupGenerator's
+ * querySeq admission, :310-322, differs only before cut_k).  *cut = the sequence length + 1 when no such position
+ * exists.  Reads the files' BAI indexes; deterministic in (files, seq, pos). */
+int ngsep_clean_cut(ngsep_ctx* ctx, const char* const* bam_paths, int32_t n_files, const char* seq, int64_t pos,
+                    int64_t* cut, int64_t* lead);
 
 /* ---- CoverageStatisticsCalculator (discovery/CoverageStatisticsCalculator.java:108-216) ----
  * path A: params.coverage_stats = 1, alignments through ngsep_process_alignments, ngsep_notify_end runs

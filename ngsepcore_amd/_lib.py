@@ -190,6 +190,8 @@ SIGNATURES = {
     "ngsep_clear_carved_regions": (ctypes.c_int, [_CTX]),
     "ngsep_bam_set_region": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64]),
     "ngsep_call_region_bam": (ctypes.c_int, [_CTX, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p]),
+    "ngsep_clean_cut": (ctypes.c_int, [_CTX, P(ctypes.c_char_p), ctypes.c_int32, ctypes.c_char_p, ctypes.c_int64, P(ctypes.c_int64),
+                                       P(ctypes.c_int64)]),
     "ngsep_stage_alignments": (ctypes.c_int, [_CTX, P(NgsepReadBatch)]),
     "ngsep_stage_finish": (ctypes.c_int, [_CTX]),
     "ngsep_run_staged": (ctypes.c_int, [_CTX, P(ctypes.c_double)]),

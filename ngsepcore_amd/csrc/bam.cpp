@@ -999,6 +999,74 @@ extern "C" int ngsep_call_region_bam(ngsep_ctx* c, const char* bam_path, const c
     return rc;
 }
 
+// A window boundary for the sharded drivers: the first position p >= pos that no realigner event can
+// reach.  Events are the alignments with I/D (IndelRealignerPileupListener opens one at an indel start, :101-118) and
+// the realigner's input variants that open regions (-knownSTRs, non-SNV -knownVariants); an event edits only the
+// alignments of its pileup (conciliateIndels :165-216), which end within one alignment span of it, and the calls it
+// makes end inside [first, last + indel bases] of its reads, so with M = 2 x the longest span around pos + 100 a position
+// outside every [first - M, last + indel + M] has the same realigner and listener state (lastIndelEnd, idxNextVariant)
+// whatever happened before it.  A run of seq from p - lead (querySeq first: the alignments that start before it and
+// reach p are then admitted as in a whole run, maxAlnsPerStartPos included) therefore calls every position >= p as the
+// whole run does, and a run to p - 1 calls every position < p as it does.  The alignments are those of every file
+// (all reader-filtered records, whatever maxAlnsPerStartPos admits: more events only move the cut right); *cut =
+// sequence length + 1 when no such position exists before the sequence end.  Deterministic in (files, seq, pos), so
+// neighbouring ranks agree on their shared boundary.
+extern "C" int ngsep_clean_cut(ngsep_ctx* c, const char* const* bam_paths, int32_t n_files, const char* seq, int64_t pos,
+                               int64_t* cut, int64_t* lead) {
+    if (!c || !bam_paths || n_files < 1 || !seq || !cut || !lead) return NGSEP_E_INVALID;
+    int32_t sid = -1;
+    for (size_t i = 0; i < c->seq_names.size(); i++) if (c->seq_names[i] == seq) { sid = (int32_t)i; break; }
+    if (sid < 0) return set_error(c, NGSEP_E_INVALID, std::string("sequence not in the reference: ") + seq);
+    const int64_t len = (int64_t)c->seq_bases[(size_t)sid].size();
+    if (pos < 1) pos = 1;
+    if (pos > len) { *cut = len + 1; *lead = 0; return NGSEP_OK; }
+    for (int64_t W = (int64_t)1 << 16;; W *= 4) {
+        const int64_t lo = std::max<int64_t>(1, pos - W), hi = pos + W;
+        std::vector<std::pair<int64_t, int64_t>> ev;      // [first, last + indel bases] of the events
+        int64_t maxspan = 1;
+        for (int32_t fi = 0; fi < n_files; fi++) {
+            ngsep_bam* b = nullptr;
+            int rc = ngsep_bam_open(c, bam_paths[fi], &b);
+            if (rc != NGSEP_OK) return rc;
+            rc = ngsep_bam_set_region(b, seq, lo, hi);
+            ngsep_read_batch batch{};
+            while (rc == NGSEP_OK) {
+                rc = ngsep_bam_next_batch(b, 1 << 16, &batch);
+                if (rc != NGSEP_OK || batch.n_reads == 0) break;
+                for (int64_t i = 0; i < batch.n_reads; i++) {
+                    if (batch.seq_id[i] != sid) continue;
+                    int64_t last = batch.first[i] - 1, indel = 0;
+                    for (int32_t k = 0; k < batch.cigar_n[i]; k++) {
+                        const int32_t v = batch.cigar[batch.cigar_off[i] + k], op = v & 7;
+                        if (v & 1) last += v / 8;
+                        if (op == 1 || op == 2) indel += v / 8;
+                    }
+                    if (last < lo || batch.first[i] > hi) continue;
+                    maxspan = std::max<int64_t>(maxspan, last - batch.first[i] + 1);
+                    if (indel > 0) ev.push_back({batch.first[i], last + indel});
+                }
+            }
+            ngsep_bam_close(b);
+            if (rc != NGSEP_OK) return rc;
+        }
+        if ((size_t)sid < c->strs.size())
+            for (const StrVar& v : c->strs[(size_t)sid].v)
+                if (v.event && v.last >= lo - W && v.first <= hi + W) ev.push_back({v.first, v.last});
+        const int64_t M = 2 * maxspan + 100;
+        std::sort(ev.begin(), ev.end());
+        int64_t p = pos;                                  // the first uncovered position >= pos
+        for (const auto& e : ev) {
+            if (e.first - M > p) break;
+            if (e.second + M >= p) p = e.second + M + 1;
+        }
+        // decided when no alignment outside [lo, hi] can cover p: those past hi start their intervals after hi - M,
+        // those before lo end theirs before lo + M + their indel bases
+        const bool right = p <= hi - M || hi >= len, left = lo == 1 || pos - lo >= 4 * M;
+        if (right && left) { *cut = std::min<int64_t>(p, len + 1); *lead = M + maxspan; return NGSEP_OK; }
+        if (W > ((int64_t)1 << 34)) { *cut = len + 1; *lead = M + maxspan; return NGSEP_OK; }
+    }
+}
+
 // ---- MultisampleVariantsDetector.run on BAM files (discovery/MultisampleVariantsDetector.java:421-459) ----
 namespace {
 int32_t java_hash(const std::string& s) {

@@ -1,4 +1,4 @@
-"""Contig sharding across the GPUs of one node: one process per GPU, no collective on
+"""Contig and window sharding across the GPUs of one node: one process per GPU, no collective on
 the hot path.
 
 Sequences are independent units of SingleSampleVariantsDetector: the reference writes each sequence's
@@ -8,6 +8,13 @@ the sequences assigned to it (largest first onto the least-loaded rank), the rec
 to rank 0 once at the end (a host-side object gather over torch.distributed: nccl/RCCL on the GPU
 node, gloo in the CPU tests) and rank 0 writes header + blocks in reference order -- byte-identical to
 the single-process output.
+
+Window granularity (window > 0): every sequence is cut into windows of about `window` bp at boundaries the library
+proves exact (ngsep_clean_cut: a position no indel-realigner event can reach, so the realigner and the listeners'
+state there do not depend on what came before); the ranks take windows from a shared queue (a counter in the
+process group's store), each window is called as a region (querySeq, AlignmentsPileupGenerator.java:242-254,310-322)
+from its boundary minus the lead the cut reports, and only the records inside the window are kept.  The blocks of
+(sequence, window) are merged on rank 0 in order: a single-contig BAM uses every GPU.
 """
 from __future__ import annotations
 
@@ -90,6 +97,132 @@ def gather_blocks(local: Dict[str, str], dist=None) -> Optional[Dict[str, str]]:
     return merged
 
 
+def window_starts(length: int, window: int) -> List[int]:
+    """Nominal first positions of a sequence's windows (1, 1 + window, ...)."""
+    return list(range(1, max(1, int(length)) + 1, max(1, int(window))))
+
+
+def window_units(contigs: Sequence[Tuple[str, int]], cuts: Dict[Tuple[str, int], Tuple[int, int]]) -> List[Tuple[str, int, int, int, int]]:
+    """(sequence, window index, first, last, lead) of every non-empty window: [first, last] between consecutive
+    cuts (made monotone: a cut never moves before an earlier one), lead = the cut's lead-in."""
+    out = []
+    for name, length in contigs:
+        ks = sorted(k for (n, k) in cuts if n == name)
+        b = [1]
+        leads = [0]
+        for k in ks:
+            if k == 0:
+                continue
+            c, lead = cuts[(name, k)]
+            b.append(max(b[-1], min(int(c), int(length) + 1)))
+            leads.append(int(lead))
+        b.append(int(length) + 1)
+        for i in range(len(b) - 1):
+            if b[i] < b[i + 1]:
+                out.append((name, i, b[i], b[i + 1] - 1, leads[i]))
+    return out
+
+
+def compute_cuts(contigs: Sequence[Tuple[str, int]], window: int, cut_fn: Callable[[str, int], Tuple[int, int]],
+                 dist=None) -> Dict[Tuple[str, int], Tuple[int, int]]:
+    """Every window boundary's (cut, lead) through cut_fn(sequence, nominal position) -- the boundaries split over
+    the ranks and all-gathered, so every rank holds the same table."""
+    todo = [(name, k, p) for name, length in contigs for k, p in enumerate(window_starts(length, window))]
+    world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
+    rank = dist.get_rank() if dist is not None and dist.is_initialized() else 0
+    mine = {}
+    for i, (name, k, p) in enumerate(todo):
+        if i % world != rank:
+            continue
+        mine[(name, k)] = (1, 0) if k == 0 else tuple(cut_fn(name, p))
+    if world == 1:
+        return mine
+    parts = [None] * world
+    dist.all_gather_object(parts, mine)
+    out = {}
+    for part in parts:
+        out.update(part)
+    return out
+
+
+_queue_uses = [0]
+
+
+def shared_queue(n: int, dist=None):
+    """Unit indexes 0 .. n - 1 handed out to the ranks as they ask (a counter in the process group's store); with
+    no store, rank r takes r, r + world, ..."""
+    world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
+    rank = dist.get_rank() if dist is not None and dist.is_initialized() else 0
+    store = None
+    if world > 1:
+        try:
+            store = dist.distributed_c10d._get_default_store()
+        except Exception:
+            store = None
+    if store is None:
+        yield from range(rank, n, world)
+        return
+    _queue_uses[0] += 1
+    key = f"ngsep_queue_{_queue_uses[0]}"
+    while True:
+        i = int(store.add(key, 1)) - 1
+        if i >= n:
+            return
+        yield i
+
+
+def keep_window(text: str, first: int, last: int) -> Tuple[str, str]:
+    """(header, the records of text with first <= POS <= last)."""
+    header, recs = [], []
+    for line in text.splitlines(keepends=True):
+        if line.startswith("#"):
+            header.append(line)
+            continue
+        pos = int(line.split("\t", 2)[1])
+        if first <= pos <= last:
+            recs.append(line)
+    return "".join(header), "".join(recs)
+
+
+def call_windows(contigs: Sequence[Tuple[str, int]], call_region: Callable[[str, int, int], str],
+                 cut_fn: Callable[[str, int], Tuple[int, int]], out_vcf: str, window: int, dist=None) -> Optional[str]:
+    """Window-granular sharding: call_region(sequence, first, last) -> VCF text of that region run; the merged VCF
+    on rank 0 (its text returned there, None elsewhere)."""
+    world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
+    rank = dist.get_rank() if dist is not None and dist.is_initialized() else 0
+    units = window_units(contigs, compute_cuts(contigs, window, cut_fn, dist))
+    header = ""
+    local: Dict[Tuple[str, int], str] = {}
+    for i in shared_queue(len(units), dist):
+        name, k, first, last, lead = units[i]
+        h, recs = keep_window(call_region(name, max(1, first - lead), last), first, last)
+        header = header or h
+        local[(name, k)] = recs
+    if world > 1:
+        hs = [None] * world if rank == 0 else None
+        dist.gather_object(header, hs, dst=0)
+        if rank == 0:
+            header = next((x for x in hs if x), "")
+        got = [None] * world if rank == 0 else None
+        dist.gather_object(local, got, dst=0)
+        if rank != 0:
+            return None
+        merged: Dict[Tuple[str, int], str] = {}
+        for part in got:
+            for key, rec in part.items():
+                if key in merged:
+                    raise ValueError(f"window {key} called on two ranks")
+                merged[key] = rec
+    else:
+        merged = local
+    if not header:                                    # (no window anywhere: the header of an empty region run)
+        header, _ = keep_window(call_region(contigs[0][0], 1, 0) if contigs else "", 1, 0)
+    text = header + "".join(merged.get((u[0], u[1]), "") for u in units)
+    with open(out_vcf, "w") as f:
+        f.write(text)
+    return text
+
+
 def call_sharded(contigs: Sequence[Tuple[str, int]], call_contig: Callable[[str], str], out_vcf: str,
                  dist=None) -> Optional[str]:
     """Runs `call_contig(name) -> VCF text of that sequence` for this rank's sequences and writes the
@@ -147,11 +280,42 @@ def gpu_contig_caller(fasta: str, bam: str, params=None, device: int = 0,
             state.pop("s").close()
 
     def carved():
-        # the indel realigner's regions this rank handed back (pass-through mode, -knownVariants with indel reads)
+        # the indel realigner's regions this rank handed back (pass-through mode)
         return state["s"].carved_regions() if "s" in state else []
+
+    def region(name: str, first: int, last: int) -> str:
+        session()
+        s = state["s"]
+        with tempfile.TemporaryDirectory() as d:
+            out = os.path.join(d, "c.vcf")
+            s._check(s._lib.ngsep_call_region_bam(s._ctx, bam.encode(), name.encode(), first, last, out.encode()))
+            return open(out).read()
+
+    def cut(name: str, pos: int):
+        session()
+        return clean_cut(state["s"], [bam], name, pos)
+
+    def session():
+        if "s" not in state:
+            state["s"] = GpuPileupSession(params, device)
+            state["s"].load_fasta(fasta)
+            if known_vcf:
+                state["s"].set_known_variants(known_vcf)
     call.close = close
     call.carved = carved
+    call.region = region
+    call.cut = cut
     return call
+
+
+def clean_cut(session, bams: Sequence[str], name: str, pos: int) -> Tuple[int, int]:
+    """ngsep_clean_cut through a session (its reference, and its input variants when set): (cut, lead)."""
+    import ctypes
+    arr = (ctypes.c_char_p * len(bams))(*[b.encode() for b in bams])
+    cut, lead = ctypes.c_int64(0), ctypes.c_int64(0)
+    session._check(session._lib.ngsep_clean_cut(session._ctx, arr, len(bams), name.encode(), int(pos), ctypes.byref(cut),
+                                                ctypes.byref(lead)))
+    return int(cut.value), int(lead.value)
 
 
 def gather_carved(local: List[Tuple[str, int, int]], order: Sequence[str], dist=None) -> Optional[List[Tuple[str, int, int]]]:
@@ -169,16 +333,20 @@ def gather_carved(local: List[Tuple[str, int, int]], order: Sequence[str], dist=
 
 
 def call_bam_sharded(fasta: str, bam: str, out_vcf: str, params=None, dist=None, device: Optional[int] = None,
-                     known_vcf: Optional[str] = None) -> Optional[str]:
-    """SingleSampleVariantsDetector over the GPUs of one node: the BAM header's sequences split over the
-    ranks (assign_contigs), each rank calling its own through the index on its GPU (device = local rank
-    by default), the per-sequence blocks merged on rank 0 in header order."""
+                     known_vcf: Optional[str] = None, window: int = 4 << 20) -> Optional[str]:
+    """SingleSampleVariantsDetector over the GPUs of one node (device = local rank by default): with window > 0
+    (default 4 Mb) the sequences' exact windows from a shared queue (call_windows), else the BAM header's sequences
+    split over the ranks (assign_contigs); each region called through the index on the rank's GPU, the blocks merged
+    on rank 0 in header order."""
     contigs = bam_header_sequences(bam)
     if device is None:
         device = int(os.environ.get("LOCAL_RANK", "0"))
     caller = gpu_contig_caller(fasta, bam, params, device, known_vcf)
     try:
-        text = call_sharded(contigs, caller, out_vcf, dist)
+        if window > 0:
+            text = call_windows(contigs, caller.region, caller.cut, out_vcf, window, dist)
+        else:
+            text = call_sharded(contigs, caller, out_vcf, dist)
         # the regions left to the caller's own indel path (ngsep_fetch_carved_regions), merged like the records and
         # written beside the VCF as the CLI does (<out>.carved.bed, 0-based half-open)
         regions = gather_carved(caller.carved(), [c[0] for c in contigs], dist)
@@ -223,20 +391,48 @@ def gpu_population_caller(fasta: str, bams: Sequence[str], params=None, device: 
     def close():
         if "s" in state:
             state.pop("s").close()
+
+    def region(name: str, first: int, last: int) -> str:
+        session()
+        s = state["s"]
+        with tempfile.TemporaryDirectory() as t:
+            out = os.path.join(t, "p.vcf")
+            s._check(s._lib.ngsep_call_population_region_bams(s._ctx, arr, len(bams), name.encode(), first, last, out.encode()))
+            return open(out).read()
+
+    def cut(name: str, pos: int):
+        session()
+        return clean_cut(state["s"], bams, name, pos)
+
+    def session():
+        if "s" not in state:
+            p = default_params()
+            if params is not None:
+                ctypes.pointer(p)[0] = params
+            p.multisample = 1
+            state["s"] = GpuPileupSession(p, device)
+            state["s"].load_fasta(fasta)
+            if known_vcf:
+                state["s"].set_known_variants(known_vcf)
     call.close = close
+    call.region = region
+    call.cut = cut
     return call
 
 
 def call_population_sharded(fasta: str, bams: Sequence[str], out_vcf: str, params=None, dist=None,
-                            device: Optional[int] = None, known_vcf: Optional[str] = None) -> Optional[str]:
-    """MultisampleVariantsDetector over the GPUs of one node (configs[4]): sequences split over the ranks,
-    the population VCF blocks merged on rank 0 in the first BAM's header order (the multi-file merge meets
-    the sequences in that order, AlignmentsPileupGenerator.java:268-289)."""
+                            device: Optional[int] = None, known_vcf: Optional[str] = None, window: int = 4 << 20) -> Optional[str]:
+    """MultisampleVariantsDetector over the GPUs of one node (configs[4]): exact windows from a shared queue
+    (window > 0, default 4 Mb; call_windows) or whole sequences split over the ranks, the population VCF blocks
+    merged on rank 0 in the first BAM's header order (the multi-file merge meets the sequences in that order,
+    AlignmentsPileupGenerator.java:268-289)."""
     contigs = bam_header_sequences(bams[0])
     if device is None:
         device = int(os.environ.get("LOCAL_RANK", "0"))
     caller = gpu_population_caller(fasta, bams, params, device, known_vcf)
     try:
+        if window > 0:
+            return call_windows(contigs, caller.region, caller.cut, out_vcf, window, dist)
         return call_sharded(contigs, caller, out_vcf, dist)
     finally:
         caller.close()

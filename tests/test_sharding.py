@@ -327,3 +327,122 @@ def test_gpu_sharded_passthrough_carved_bed(tmp_path):
     assert merged == open(full).read()
     bed = [l.split("\t") for l in open(out + ".carved.bed").read().splitlines()]
     assert [(n, int(a) + 1, int(b)) for n, a, b in bed] == want
+
+
+def _window_worker(rank, world, port, fa, sam, bam, contigs, out_dir, window, multi):
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        from ngsepcore_amd import GpuPileupSession
+        from ngsepcore_amd.sharding import call_windows, clean_cut
+        s = GpuPileupSession()                     # (the reference for ngsep_clean_cut: no device needed)
+        s.load_fasta(fa)
+        calls = []
+
+        def region(name, first, last):
+            out = os.path.join(out_dir, f"r{rank}_{name}_{first}.vcf")
+            calls.append((name, first, last))
+            if multi:
+                ngsep_oracle.run_mvd(fa, sam, out, 0.0, query_seq=name, query_first=first, query_last=last)
+            else:
+                ngsep_oracle.run_ssvd(fa, sam, out, query_seq=name, query_first=first, query_last=last)
+            return open(out).read()
+
+        call_windows(contigs, region, lambda n, p: clean_cut(s, [bam], n, p), os.path.join(out_dir, "merged.vcf"), window, dist)
+        with open(os.path.join(out_dir, f"calls{rank}.txt"), "w") as f:
+            f.write(repr(calls))
+        s.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("multi", [False, True])
+def test_two_rank_window_sharding_one_contig(tmp_path, multi):
+    """ONE contig split into exact windows (ngsep_clean_cut) taken by two gloo ranks from the shared queue, each window
+    run as a region from its cut minus the lead (the oracle stands in for each rank's GPU caller): the merged VCF ==
+    the whole-file VCF, on data with indels (the realigner's events decide where a cut may fall) -- for
+    SingleSampleVariantsDetector and MultisampleVariantsDetector."""
+    kw = dict(genome=pysynth.CUSTOM, custom_len=160000, seed=71, snv_rate=2e-3, indel_rate=5e-4)
+    kw.update(dict(n_samples=6, depth=6) if multi else dict(depth=20))
+    syn = pysynth.Synth(**kw)
+    contigs = [(n, len(s)) for n, s in syn.contigs()]
+    assert len(contigs) == 1
+    fa, sam, bam = syn.write(os.path.join(str(tmp_path), "d"))
+    syn.close()
+    full = os.path.join(str(tmp_path), "full.vcf")
+    if multi:
+        ngsep_oracle.run_mvd(fa, sam, full, 0.0)
+    else:
+        ngsep_oracle.run_ssvd(fa, sam, full)
+    text = open(full).read()
+    assert sum(1 for l in text.splitlines() if "TYPE=INDEL" in l or "TYPE=STR" in l) > 5
+    mp.spawn(_window_worker, args=(2, _free_port(), fa, sam, bam, contigs, str(tmp_path), 20000, multi), nprocs=2, join=True)
+    merged = open(os.path.join(str(tmp_path), "merged.vcf")).read()
+    assert merged == text
+    import ast
+    c0 = ast.literal_eval(open(os.path.join(str(tmp_path), "calls0.txt")).read())
+    c1 = ast.literal_eval(open(os.path.join(str(tmp_path), "calls1.txt")).read())
+    assert len(c0) >= 2 and len(c1) >= 2                 # both ranks took windows of the one contig
+
+
+def test_clean_cut_properties(tmp_path):
+    """ngsep_clean_cut: deterministic, never before pos, the sequence end + 1 past it, and no cut inside the reach of
+    an alignment with an indel."""
+    from ngsepcore_amd import GpuPileupSession
+    from ngsepcore_amd.sharding import clean_cut
+    syn = pysynth.Synth(genome=pysynth.CUSTOM, custom_len=80000, seed=72, depth=15, indel_rate=2e-3)
+    fa, sam, bam = syn.write(os.path.join(str(tmp_path), "c"))
+    name, seq = syn.contigs()[0]
+    syn.close()
+    ev = []
+    for l in open(sam):
+        if l.startswith("@"):
+            continue
+        f = l.split("\t")
+        import re
+        ops = re.findall(r"(\d+)([MIDNSHP=X])", f[5])
+        span = sum(int(n) for n, o in ops if o in "MDN=X")
+        ind = sum(int(n) for n, o in ops if o in "ID")
+        if ind:
+            ev.append((int(f[3]), int(f[3]) + span - 1 + ind))
+    with GpuPileupSession() as s:
+        s.load_fasta(fa)
+        prev = 0
+        for pos in range(1, len(seq) + 2000, 7000):
+            c, lead = clean_cut(s, [bam], name, pos)
+            assert (c, lead) == clean_cut(s, [bam], name, pos)
+            assert c >= pos and c <= len(seq) + 1 and lead > 0
+            assert c >= prev or pos > prev
+            if c <= len(seq):
+                assert all(not (a - 150 <= c <= b + 150) for a, b in ev)
+            prev = c
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("multi", [False, True])
+def test_gpu_window_caller_merge_identical(tmp_path, multi):
+    """The production window path on the GPU (ngsep_clean_cut + ngsep_call_region_bam / ngsep_call_population_region_bams
+    per window from its lead-in, the records inside the window kept), single process: the merged VCF == the whole-file
+    GPU VCF on indel-bearing data with 25 kb windows."""
+    from ngsepcore_amd import GpuPileupSession, MultisampleVariantsDetector
+    from ngsepcore_amd.sharding import call_bam_sharded, call_population_sharded
+    kw = dict(genome=pysynth.CUSTOM, custom_len=150000, seed=73, snv_rate=2e-3, indel_rate=5e-4)
+    kw.update(dict(n_samples=6, depth=6) if multi else dict(depth=20))
+    syn = pysynth.Synth(**kw)
+    fa, sam, bam = syn.write(os.path.join(str(tmp_path), "w"))
+    full = os.path.join(str(tmp_path), "full.vcf")
+    if multi:
+        bams = syn.write_sample_bams(os.path.join(str(tmp_path), "pop"))
+        d = MultisampleVariantsDetector()
+        d.setGenome(fa)
+        d.setOutFilename(full)
+        d.run(bams).close()
+        merged = call_population_sharded(fa, bams, os.path.join(str(tmp_path), "m.vcf"), window=25000)
+    else:
+        with GpuPileupSession() as s:
+            s.load_fasta(fa)
+            s.processFile(bam, full)
+        merged = call_bam_sharded(fa, bam, os.path.join(str(tmp_path), "m.vcf"), window=25000)
+    syn.close()
+    text = open(full).read()
+    assert sum(1 for l in text.splitlines() if "TYPE=INDEL" in l or "TYPE=STR" in l) > 5
+    assert merged == text
