@@ -85,8 +85,8 @@ typedef struct ngsep_params {
     int32_t full_records;
     /* ABI 6: the indel realigner and indel / STR discovery (IndelRealignerPileupListener + VariantDiscovery-
      * SNVQAlgorithm.callIndel, single-sample discovery at ploidy < 3, streamed runs; ABI 8: also
-     * MultisampleVariantsDetector at ploidy < 3, discoverPopulationIndel; ABI 9: also with -knownVariants, whose
-     * records are the realigner's input variants).
+     * MultisampleVariantsDetector, discoverPopulationIndel; ABI 9: also with -knownVariants, whose records are the
+     * realigner's input variants, and at ploidy >= 3 -- the pool algorithm's indel branch, genotypeVariantPool).
      * 0 (default): regions around alignments with indels are realigned and called here (indel / STR records,
      * TYPE=EMBEDDED SNVs with call_embedded); 1: pass-through -- no call inside those regions, which are returned
      * by ngsep_fetch_carved_regions for the caller's own indel path (the ABI 5 behaviour). */
@@ -138,7 +138,9 @@ typedef struct ngsep_site_out {
                               * the variant's allele count, genotype = number of called alleles (0 undecided,
                               * 1 homozygous, 2 heterozygous), alt / third = DNA indexes of the called alleles
                               * (-1 when absent), logc = the report's log-conditionals over the variant's alleles
-                              * (upper triangle, i <= j < n_alleles, row-major), dp = the pool call's read depth */
+                              * (upper triangle, i <= j < n_alleles, row-major), dp = the pool call's read depth;
+                              * ABI 9, -knownVariants: strand_bias = the copy number genotypeVariantPool gave the
+                              * first called allele of a heterozygous call (-1 otherwise) */
     int32_t dp;              /* CountsHelper.getTotalCount() */
     int32_t counts[4];       /* A,C,G,T base counts (BSDP) */
     int32_t strand_counts[4][2]; /* [allele][0=negative,1=positive] (CountsHelper.countsStrand); biallelic SNV
@@ -209,10 +211,10 @@ typedef struct ngsep_stats {
  * with input variants, :158-176; MultisampleVariantsDetector.onPileup :539-551): every input variant with a pileup gets
  * a record (hom-ref, het, hom-alt or undecided; ID, alleles and INFO TYPE kept; QUAL the input's, or the population
  * QS).  Biallelic SNVs are genotyped on the device (genotypeSNV / the pool algorithm); ABI 9: indels, MNPs and other
- * records that are not SNVs are accepted at ploidy < 3 -- they are the indel realigner's fixed events
- * (IndelRealignerPileupListener.setInputVariants, findSNVS :904) and are genotyped in their realigner regions by
- * callIndel with the variant given (genotypeVariantSample :377-386).  Multi-allelic SNVs, records that repeat an
- * allele and non-SNV records at ploidy >= 3: E_UNSUPPORTED.  Call after the reference is loaded; NULL or "" returns
+ * records that are not SNVs are accepted -- they are the indel realigner's fixed events (IndelRealignerPileupListener
+ * .setInputVariants, findSNVS :904) and are genotyped in their realigner regions by callIndel with the variant given
+ * (genotypeVariantSample :377-386), or by genotypeVariantPool at ploidy >= 3.  Multi-allelic SNVs and records that
+ * repeat an allele: E_UNSUPPORTED.  Call after the reference is loaded; NULL or "" returns
  * to discovery; a file with no usable record also discovers (inputVariants.size() == 0, :148).  Once a file is set,
  * ngsep_set_known_strs is ignored (the reference's else-if, :906). */
 int  ngsep_set_known_variants(ngsep_ctx* c, const char* vcf_path);   /* ngsep_set_known_variants(c, NULL) clears it */

@@ -567,13 +567,12 @@ static int stream_advance(ngsep_ctx* c, bool final);
 static bool streaming(const ngsep_ctx* c) { return !c->staging_mode && !c->params.coverage_stats && !c->params.multisample; }
 
 // the indel realigner runs here (realign.hpp) in streamed single-sample runs and in MultisampleVariantsDetector (run
-// per sequence), at ploidy < 3, discovering or genotyping -knownVariants (the reference's listener chains:
-// SingleSampleVariantsDetector.java:896-931, MultisampleVariantsDetector.java:432-450); elsewhere its regions are
-// carved out and returned (params.indel_passthrough)
+// per sequence), at every ploidy (the pool algorithm's indel branch at >= 3), discovering or genotyping -knownVariants
+// (the reference's listener chains: SingleSampleVariantsDetector.java:896-931, MultisampleVariantsDetector.java:432-450);
+// elsewhere its regions are carved out and returned (params.indel_passthrough)
 static bool realign_active(const ngsep_ctx* c) {
     const bool path = streaming(c) || (c->params.multisample && !c->staging_mode);
-    return path && !c->params.indel_passthrough && !c->params.relative_allele_counts && !c->params.dump_all_positions &&
-           c->params.ploidy < 3;
+    return path && !c->params.indel_passthrough && !c->params.relative_allele_counts && !c->params.dump_all_positions;
 }
 
 // keeps the raw alignments (RawRead) a realigner region can need: those inside the reach of an indel read
@@ -3387,11 +3386,6 @@ extern "C" int ngsep_set_known_variants(ngsep_ctx* c, const char* vcf_path) {
                 rc = set_error(c, NGSEP_E_UNSUPPORTED, std::string("known variant ") + fld[0] + ":" + fld[1] +
                                                        (all_snv ? " is a multi-allelic SNV" : dup ? " repeats an allele" : " has too many alleles") +
                                                        " (not genotyped by this build)");
-                break;
-            }
-            if (c->params.ploidy >= 3) {
-                rc = set_error(c, NGSEP_E_UNSUPPORTED, std::string("known variant ") + fld[0] + ":" + fld[1] +
-                                                       " is not an SNV: the pool algorithm's indel branch (ploidy >= 3) is not in this build");
                 break;
             }
             if (end > 0) kv.last = end;                                  // END of a GenomicVariantImpl (:282-289)

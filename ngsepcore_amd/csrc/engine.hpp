@@ -710,7 +710,9 @@ struct ngsep_ctx {
     // path B: the alignments the BAM is expected to hold (its size / 40 B, an upper estimate); a sequence's read
     // arrays reserve their share up front (virtual memory, touched only as they fill: no regrowth copies)
     int64_t reads_hint = 0;
-    mutable struct { int32_t seq = -1, pos = -1; std::vector<int64_t> taken; } vcf_known;   // known_id: the position written
+    // known_at: the position written; last_seq: the sequence of the last record written (the first record of a sequence
+    // is the one intersectVariantsCNVs updates, SingleSampleVariantsDetector.java:969-991)
+    mutable struct { int32_t seq = -1, pos = -1, last_seq = -1; std::vector<int64_t> taken; } vcf_known;
     // RelativeAlleleCountsCalculator mode (params.relative_allele_counts): its Distributions
     struct {
         double prop[51] = {}, prop_count = 0, prop_sum = 0, prop_sum_sq = 0;
@@ -838,7 +840,7 @@ const ngsep_ctx::KnownVar* known_of(const ngsep_ctx* c, const ngsep_site_out& s)
 const ngsep_ctx::KnownVar* known_at(const ngsep_ctx* c, int32_t seq_id, int32_t pos, int alt);
 // vcf.cpp
 std::string format_header(const ngsep_ctx* c);
-int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& out);
+int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& out, bool first_of_seq);
 std::string format_population_header(const ngsep_ctx* c);
 void format_population_site(const ngsep_ctx* c, const ngsep_popsite_out& s, const ngsep_sample_call* calls, std::string& out);
 // bam.cpp

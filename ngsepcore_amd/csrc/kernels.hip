@@ -814,7 +814,13 @@ __global__ __launch_bounds__(kPostThreads) void k_posterior_pool(const SiteQ* __
         h[1] = (uint32_t)gpos;
         const uint32_t ref = (uint32_t)(uint8_t)"ACGT"[dna[0]];
         h[2] = ref | (uint32_t)(uint8_t)n << 8 | (uint32_t)(uint8_t)(int8_t)a0 << 16 | (uint32_t)(uint8_t)(int8_t)a1 << 24;
-        h[3] = (uint32_t)(uint8_t)R.n_called | 0xFF00u | (uint32_t)(uint16_t)R.gq << 16;
+        // -knownVariants: genotypeVariantPool's copy number of the first called allele of a heterozygous call (the
+        // writer keeps it past the sequence's first record, vcf.cpp format_site) in the strand-bias byte; -1 otherwise
+        int acn0 = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++) acn0 = e == R.c0 ? R.acn[e] : acn0;
+        const uint32_t sb = (known && R.n_called == 2) ? (uint32_t)(uint8_t)acn0 : 0xFFu;
+        h[3] = (uint32_t)(uint8_t)R.n_called | sb << 8 | (uint32_t)(uint16_t)R.gq << 16;
         h[4] = 1u << 16 | (mask | (R.report ? 0x10u : 0u)) << 24;
         h[5] = (uint32_t)R.dp;
 #pragma unroll

@@ -714,10 +714,11 @@ struct IndelCounts {
     std::vector<int> counts;
     std::vector<double> logc;
 };
-void indel_counts(const std::vector<std::string>& alleles, const std::vector<SpanCall>& calls, int max_base_qs, IndelCounts& h) {
+void indel_counts_f(const std::vector<std::string>& alleles, const std::vector<SpanCall>& calls, int max_base_qs, double freq,
+                    IndelCounts& h) {
     const int n = (int)alleles.size();
     const int maxBaseQS = (int8_t)max_base_qs > 0 ? (int8_t)max_base_qs : 30;
-    const int f = (int)java_round(0.5 * kNumFreq);                     // (:256: 501, not 500)
+    const int f = (int)java_round(freq * kNumFreq);                    // (:256: 501, not 500)
     const double af0 = std::log10((double)f / (kNumFreq - 1)), af1 = std::log10(1 - (double)f / (kNumFreq - 1));
     const double E = std::log10(0.0001);                                  // DEF_LOG_ERROR_PROB_INDEL (:48)
     h.n = n;
@@ -760,6 +761,18 @@ void indel_counts(const std::vector<std::string>& alleles, const std::vector<Spa
             }
         }
     }
+}
+
+void indel_counts(const std::vector<std::string>& alleles, const std::vector<SpanCall>& calls, int max_base_qs, IndelCounts& h) {
+    indel_counts_f(alleles, calls, max_base_qs, 0.5, h);
+}
+
+// CountsHelper.calculatePosteriorProbabilities (:472-495) in place
+void posteriors(std::vector<double>& ev) {
+    double logMax = 1, tot = 0;
+    for (double v : ev) if (logMax > 0 || logMax < v) logMax = v;
+    for (double& v : ev) { v -= logMax; v = v < -20 ? 0.0 : std::pow(10.0, v); tot += v; }
+    for (double& v : ev) v /= tot;
 }
 
 // getPosteriorProbabilities (CountsHelper.java:410-443) + calculatePosteriorProbabilities (:472-495) over n alleles
@@ -939,9 +952,84 @@ void sample_span_calls(const std::vector<Aln*>& pileup, int s, int pos, int span
 // calculateCountsIndel over the variant's alleles, callIndel with the variant given (the maximum genotype's indexes
 // taken as they are, VariantDiscoverySNVQAlgorithm.java:335-345; no calls: an undecided call, :274-277),
 // updateAllelesCopyNumberFromCounts(ploidy), makeUndecided below min_quality (CalledGenomicVariantImpl.java:320-325)
+// genotypeVariantPool (SingleSampleVariantPileupListener.java:402-503) over an indel variant: CountsHelper
+// .calculateCountsIndel per heterozygosity hypothesis (freq = k / haplotypes < 0.51, :410-414), the major allele by the
+// first helper's counts (undecided, no report and no depth below `haplotypes` calls, :428-432), every other allele's
+// homozygous-vs-heterozygous posteriors (:447-470), GQ and setAllelesCopyNumber (:482-498), the report from the chosen
+// helper (:499-500; h = its counts and log-conditionals)
+void genotype_pool_indel(const std::vector<std::string>& alleles, const std::vector<SpanCall>& sc, int haplotypes, double het,
+                         int max_base_qs, SampleIndelCall& c, IndelCounts& h) {
+    const int n = (int)alleles.size();
+    c = SampleIndelCall();
+    c.acn.assign((size_t)n, 0);
+    const double step = 1.0 / (double)haplotypes;
+    std::vector<double> freqs;
+    for (double freq = step; freq < 0.51; freq += step) freqs.push_back(freq);
+    const int nf = (int)freqs.size();
+    std::vector<IndelCounts> hs((size_t)nf);
+    for (int j = 0; j < nf; j++) indel_counts_f(alleles, sc, max_base_qs, freqs[(size_t)j], hs[(size_t)j]);
+    const IndelCounts& h0 = hs[0];
+    int major = 0;                                                       // NumberArrays.getIndexMaximum: first maximum
+    for (int i = 1; i < n; i++) if (h0.counts[(size_t)major] < h0.counts[(size_t)i]) major = i;
+    h = h0;
+    if (h0.counts[(size_t)major] < haplotypes) {
+        update_cn(c, h0.counts, haplotypes);                             // undecided.updateAllelesCopyNumberFromCounts
+        return;
+    }
+    const double lph = std::log10(het), lpo = std::log10(1 - het);
+    std::vector<double> terms((size_t)nf + 1);
+    const double termHomozygous = h0.logc[(size_t)(major * n + major)] + lpo;
+    double maxHetPosterior = 0, minHomoPosterior = 1, maxFreq = 0;
+    int maxFreqIdx = 0, maxAlt = -1;
+    for (int i = 0; i < n; i++) {
+        if (i == major) continue;
+        terms[0] = termHomozygous;
+        for (int j = 0; j < nf; j++) terms[(size_t)j + 1] = hs[(size_t)j].logc[(size_t)(major * n + i)] + lph;
+        posteriors(terms);
+        int idxMax = 0;
+        for (int j = 1; j <= nf; j++) if (terms[(size_t)idxMax] < terms[(size_t)j]) idxMax = j;
+        if (idxMax == 0) minHomoPosterior = std::min(minHomoPosterior, terms[0]);
+        else if (maxAlt == -1 || maxHetPosterior < terms[(size_t)idxMax]) {
+            maxHetPosterior = terms[(size_t)idxMax];
+            maxFreqIdx = idxMax - 1;
+            maxFreq = freqs[(size_t)maxFreqIdx];
+            maxAlt = i;
+        }
+    }
+    if (maxAlt == -1) { c.n_called = 1; c.called[0] = major; }
+    else { c.n_called = 2; c.called[0] = std::min(major, maxAlt); c.called[1] = std::max(major, maxAlt); }
+    c.dp = h0.total;
+    if (maxAlt == -1) {
+        c.gq = java_phred(1 - minHomoPosterior);
+        c.acn[(size_t)major] = haplotypes;
+    } else {
+        h = hs[(size_t)maxFreqIdx];
+        // CountsHelper.getPosteriorProbabilities(hetRate, majorAlleleIdx) (CountsHelper.java:451-467)
+        std::vector<double> ev((size_t)n);
+        const double lh = std::log10(het / (n - 1)), lo = std::log10(1 - het);
+        for (int j = 0; j < n; j++) ev[(size_t)j] = h.logc[(size_t)(major * n + j)] + (j == major ? lo : lh);
+        posteriors(ev);
+        c.gq = java_phred(1 - ev[(size_t)maxAlt]);
+        int altCN = (int)(int16_t)java_round(maxFreq * haplotypes);
+        if (altCN == 0) altCN++;
+        else if (altCN == haplotypes) altCN--;
+        c.acn[(size_t)maxAlt] = altCN;
+        c.acn[(size_t)major] = haplotypes - altCN;
+    }
+    c.total_cn = haplotypes;                                             // setAllelesCopyNumber
+    c.report = true;
+    h.counts = h0.counts;
+}
+
 void genotype_indel_sample(const std::vector<std::string>& alleles, const std::vector<SpanCall>& sc, const RealignParams& p,
                            int min_quality, SampleIndelCall& c, IndelCounts& h) {
     const int n = (int)alleles.size();
+    if (p.ploidy >= 3) {
+        // DEF_MIN_PLOIDY_POOL_ALGORITHM: genotypeVariantPool (:378-379), makeUndecided below min_quality (:388)
+        genotype_pool_indel(alleles, sc, p.ploidy, p.het_rate, p.max_base_qs, c, h);
+        if ((int16_t)min_quality > c.gq) { c.n_called = 0; c.gq = 0; update_cn(c, h.counts, c.total_cn); }
+        return;
+    }
     c = SampleIndelCall();
     c.acn.assign((size_t)n, 0);
     indel_counts(alleles, sc, p.max_base_qs, h);
@@ -1091,33 +1179,19 @@ const char* type_name(int t) {
     return t >= 2 && t <= 5 ? kNames[t] : nullptr;
 }
 
-// -knownVariants, a non-SNV input variant at its first position: SingleSampleVariantsDetector's listener genotypes it in
-// the one sample (genotypeVariantSample :361-391 with -minQuality) and the record carries the input's ID, alleles, QS
-// and TYPE, FORMAT DEF_FORMAT_ARRAY_NGSEP_NOSNV (SingleSampleVariantsDetector.java:946-953); MultisampleVariantsDetector
-// genotypes it in every sample (genotypeVariant :664-693) and writes the population record with the variant QS it sets
-void known_record(const std::vector<Aln*>& pileup, int pos, const KnownRecord& kr, const RealignParams& p, std::string& o) {
-    const int n = (int)kr.alleles.size();
-    const char* type = type_name(kr.type);
-    if (p.n_samples > 0) {
-        std::vector<SampleIndelCall> sc;
-        std::vector<IndelCounts> hs;
-        const int qs = genotype_indel_population(kr.alleles, pileup, pos, p, sc, hs);
-        format_population_indel(pos, kr.id, kr.alleles, type, qs, sc, hs, p.ploidy, o);
-        return;
-    }
-    std::vector<SpanCall> calls;
-    span_calls(pileup, pos, (int)kr.alleles[0].size(), calls);
-    SampleIndelCall c;
-    IndelCounts h;
-    genotype_indel_sample(kr.alleles, calls, p, p.min_quality, c, h);
+// VCFFileWriter.printVCFRecord of a CalledGenomicVariantImpl over a GenomicVariantImpl, FORMAT DEF_FORMAT_ARRAY_NGSEP_NOSNV
+// (SingleSampleVariantsDetector.java:946-953), without the sequence name
+void format_indel_record(int pos, const std::string& id, const std::vector<std::string>& alleles, int qs, const char* type,
+                         const SampleIndelCall& c, const IndelCounts& h, int ploidy, std::string& o) {
+    const int n = (int)alleles.size();
     o.clear();
-    o += std::to_string(pos); o += '\t'; o += kr.id.empty() ? "." : kr.id; o += '\t'; o += kr.alleles[0]; o += '\t';
-    for (int i = 1; i < n; i++) { if (i > 1) o += ','; o += kr.alleles[(size_t)i]; }
-    o += '\t'; o += std::to_string(kr.qs); o += "\t.\t";
+    o += std::to_string(pos); o += '\t'; o += id.empty() ? "." : id; o += '\t'; o += alleles[0]; o += '\t';
+    for (int i = 1; i < n; i++) { if (i > 1) o += ','; o += alleles[(size_t)i]; }
+    o += '\t'; o += std::to_string(qs); o += "\t.\t";
     if (type) { o += "TYPE="; o += type; } else o += '.';
     o += "\tGT:PL:GQ:DP:ADP:ACN\t";
-    if (c.n_called == 0) o += p.ploidy > 1 ? "./." : ".";
-    else if (c.n_called == 1) { o += std::to_string(c.called[0]); if (p.ploidy > 1) { o += '/'; o += std::to_string(c.called[0]); } }
+    if (c.n_called == 0) o += ploidy > 1 ? "./." : ".";
+    else if (c.n_called == 1) { o += std::to_string(c.called[0]); if (ploidy > 1) { o += '/'; o += std::to_string(c.called[0]); } }
     else { o += std::to_string(c.called[0]); o += '/'; o += std::to_string(c.called[1]); }
     o += ':';
     for (int j = 0; j < n; j++)
@@ -1131,6 +1205,77 @@ void known_record(const std::vector<Aln*>& pileup, int pos, const KnownRecord& k
     if (c.total_cn == 0) o += '.';
     else for (int j = 0; j < n; j++) { if (j) o += ','; o += std::to_string((c.n_called == 0 && j == 0) ? c.total_cn : c.acn[(size_t)j]); }
     o += '\n';
+}
+
+// -knownVariants, a non-SNV input variant at its first position: SingleSampleVariantsDetector's listener genotypes it in
+// the one sample (genotypeVariantSample :361-391 with -minQuality) and the record carries the input's ID, alleles, QS
+// and TYPE, FORMAT DEF_FORMAT_ARRAY_NGSEP_NOSNV (SingleSampleVariantsDetector.java:946-953); MultisampleVariantsDetector
+// genotypes it in every sample (genotypeVariant :664-693) and writes the population record with the variant QS it sets
+void known_record(const std::vector<Aln*>& pileup, int pos, const KnownRecord& kr, const RealignParams& p, std::string& o) {
+    const char* type = type_name(kr.type);
+    if (p.n_samples > 0) {
+        std::vector<SampleIndelCall> sc;
+        std::vector<IndelCounts> hs;
+        const int qs = genotype_indel_population(kr.alleles, pileup, pos, p, sc, hs);
+        format_population_indel(pos, kr.id, kr.alleles, type, qs, sc, hs, p.ploidy, o);
+        return;
+    }
+    std::vector<SpanCall> calls;
+    span_calls(pileup, pos, (int)kr.alleles[0].size(), calls);
+    SampleIndelCall c;
+    IndelCounts h;
+    genotype_indel_sample(kr.alleles, calls, p, p.min_quality, c, h);
+    format_indel_record(pos, kr.id, kr.alleles, kr.qs, type, c, h, p.ploidy, o);
+    if (p.ploidy >= 3) {
+        // the pool algorithm's copy numbers stay unless the record is its sequence's first (intersectVariantsCNVs,
+        // SingleSampleVariantsDetector.java:969-991, updates that one from the counts): both lines, NUL-separated
+        // (vcf.cpp format_record)
+        update_cn(c, h.counts, p.ploidy);
+        std::string first;
+        format_indel_record(pos, kr.id, kr.alleles, kr.qs, type, c, h, p.ploidy, first);
+        o += '\0';
+        o += first;
+    }
+}
+
+// ploidy >= 3, a span > 1 (discoverVariantWithSpan :257-273 -> discoverIndel :275-296): the clustered alleles' pool
+// variant (createIndelVariantPool :333-338: none for one allele, no calls or alleles of one length), genotypeVariantPool;
+// a multi-allelic variant keeps its alleles when two non-reference alleles are called, else becomes the reference and the
+// called allele (makeNewVariant :346-359) and is genotyped again; an undecided, homozygous-reference or low-GQ call is
+// dropped (:263, :223); a kept call's ACN from its counts (:226).  The variant keeps TYPE_UNDETERMINED and QS 0.
+bool pool_indel(std::vector<std::string> alleles, const std::vector<SpanCall>& calls, int pos, const RealignParams& p, IndelCall* out) {
+    {
+        IndelCounts h;
+        indel_counts(alleles, calls, p.max_base_qs, h);
+        if (alleles.size() <= 1 || h.total == 0) return false;
+    }
+    auto same_len = [](const std::vector<std::string>& a) {
+        for (const std::string& x : a) if (x.size() != a[0].size()) return false;
+        return true;
+    };
+    if (same_len(alleles)) return false;
+    SampleIndelCall c;
+    IndelCounts h;
+    genotype_pool_indel(alleles, calls, p.ploidy, p.het_rate, p.max_base_qs, c, h);
+    if (alleles.size() > 2) {
+        const bool homref = c.n_called == 1 && c.called[0] == 0;
+        if (c.n_called == 0 || homref) return false;
+        if (!(c.n_called == 2 && c.called[0] != 0)) {
+            std::vector<std::string> nv{alleles[0]};                      // {reference} + the called alleles
+            for (int i = 0; i < c.n_called; i++)
+                if (alleles[(size_t)c.called[i]] != alleles[0]) nv.push_back(alleles[(size_t)c.called[i]]);
+            if (same_len(nv)) return false;
+            alleles.swap(nv);
+            genotype_pool_indel(alleles, calls, p.ploidy, p.het_rate, p.max_base_qs, c, h);
+        }
+    }
+    const bool homref = c.n_called == 1 && c.called[0] == 0;
+    if (c.n_called == 0 || homref || (int16_t)p.min_quality > c.gq) return false;
+    update_cn(c, h.counts, p.ploidy);                                    // discoverVariant (:226)
+    format_indel_record(pos, std::string(), alleles, 0, nullptr, c, h, p.ploidy, out->line);
+    out->pos = pos;
+    out->last = pos + (int32_t)alleles[0].size() - 1;
+    return true;
 }
 
 }  // namespace
@@ -1282,7 +1427,8 @@ void replay_region(const std::string& seq, int64_t first, int64_t last, std::vec
             } else {
                 const std::vector<std::string> alleles = cluster_alleles(calls, reference, p.max_base_qs);
                 IndelCall ic;
-                if (genotype_indel(alleles, calls, pos, rp.str, rp.str && !rp.new_str, p, &ic)) {
+                if (p.ploidy >= 3 ? pool_indel(alleles, calls, pos, p, &ic)
+                                  : genotype_indel(alleles, calls, pos, rp.str, rp.str && !rp.new_str, p, &ic)) {
                     rp.indel = (int32_t)out.indels.size();
                     out.indels.push_back(std::move(ic));
                 }

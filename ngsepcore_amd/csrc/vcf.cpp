@@ -41,6 +41,7 @@ static const char* kHeaderLines[][5] = {
 };
 
 std::string format_header(const ngsep_ctx* c) {
+    c->vcf_known.last_seq = -1;                          // (a new file: its first record is the first of its sequence)
     std::string h = "##fileformat=VCFv4.2\n";
     for (const auto& l : kHeaderLines) {
         h += "##"; h += l[0]; h += "=<ID="; h += l[1]; h += ",Number="; h += l[3];
@@ -68,7 +69,7 @@ static const char* type_name(int t) {
     return t >= 2 && t <= 5 ? kNames[t] : nullptr;
 }
 
-int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& o) {
+int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& o, bool first_of_seq) {
     static const char kB[] = "ACGT";
     const size_t start = o.size();
     const int ploidy = c->params.ploidy;
@@ -94,7 +95,8 @@ int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& o)
         o += name; o += '\t'; app(o, s.pos); o += '\t'; o += id ? id : "."; o += '\t'; o += (char)s.ref; o += '\t';
         for (int i = 1; i < n; i++) { if (i > 1) o += ','; o += kB[dna[i]]; }
         o += '\t'; app(o, s.qual); o += "\t.\t";
-        if (n > 2) o += "TYPE=MULTISNV";                  // VCFFileWriter.java:47-49
+        if (s.is_call & kRecEmbedded) o += "TYPE=EMBEDDED";   // an SNV inside an indel / STR (:227)
+        else if (n > 2) o += "TYPE=MULTISNV";             // VCFFileWriter.java:47-49
         else if (ktype) { o += "TYPE="; o += ktype; }
         else o += '.';
         o += known ? "\tGT:PL:GQ:DP:BSDP:ACN\t" : "\tGT:PL:GQ:DP:ADP:ACN\t";
@@ -114,10 +116,16 @@ int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& o)
         else for (int i = 0; i < n; i++) { if (i) o += ','; app(o, report ? s.counts[dna[i]] : 0); }
         o += ':';
         // ACN: updateAllelesCopyNumberFromCounts(ploidy) from the report's counts (discoverVariant :226,
-        // intersectVariantsCNVs :986; CalledGenomicVariantImpl.java:228-282)
+        // intersectVariantsCNVs :975 for the first record of a sequence; CalledGenomicVariantImpl.java:228-282); an input
+        // record past the first keeps the copy numbers genotypeVariantPool set (:480-498): the device keeps the first
+        // called allele's in strand_bias (kernels.hip k_posterior_pool)
         int acn[4] = {0, 0, 0, 0};
         const int called[2] = {c0, c1};
-        if (nc == 1 && c0 == 0) acn[0] = ploidy;
+        if (known && !first_of_seq && nc == 2 && s.strand_bias > 0 && s.strand_bias < ploidy) {
+            acn[c0] = s.strand_bias;
+            acn[c1] = ploidy - s.strand_bias;
+        } else if (known && !first_of_seq && nc == 1) acn[c0] = ploidy;
+        else if (nc == 1 && c0 == 0) acn[0] = ploidy;
         else if (nc > 0 && ploidy <= nc) { for (int i = 0; i < nc; i++) acn[called[i]] = 1; }
         else if (nc > 0 && !report) {
             const int def = ploidy / nc;
@@ -227,16 +235,24 @@ int64_t format_site(const ngsep_ctx* c, const ngsep_site_out& s, std::string& o)
     return (int64_t)(o.size() - start);
 }
 
-// record i of the context's site list: an SNV record (format_site), or an indel / STR record's text
+// record i of the context's site list: an SNV record (format_site), or an indel / STR record's text.  A text with a
+// NUL holds two lines: the second is the one written when the record is the first of its sequence (a pool -knownVariants
+// record: intersectVariantsCNVs recomputes its ACN from the counts, SingleSampleVariantsDetector.java:969-991)
 void format_record(const ngsep_ctx* c, size_t i, std::string& o) {
     const SiteRec& r = c->sites.rec[i];
+    const bool first = c->vcf_known.last_seq != r.seq_id;
+    c->vcf_known.last_seq = r.seq_id;
     if (r.is_call & kRecIndel) {
         o += (r.seq_id >= 0 && r.seq_id < (int)c->seq_names.size()) ? c->seq_names[(size_t)r.seq_id] : std::string("?");
         o += '\t';
-        o += c->sites.text[(size_t)SiteSet::ext_index(r)];
+        const std::string& t = c->sites.text[(size_t)SiteSet::ext_index(r)];
+        const size_t z = t.find('\0');
+        if (z == std::string::npos) o += t;
+        else if (first) o.append(t, z + 1, std::string::npos);
+        else o.append(t, 0, z);
         return;
     }
-    format_site(c, c->sites.full(i), o);
+    format_site(c, c->sites.full(i), o, first);
 }
 
 // ---- MultisampleVariantsDetector output ----
@@ -417,7 +433,7 @@ extern "C" int64_t ngsep_site_vcf_line(ngsep_ctx* c, int64_t i, char* buf, int64
 extern "C" int64_t ngsep_format_site(ngsep_ctx* c, const ngsep_site_out* s, char* buf, int64_t cap) {
     if (!c || !s) return NGSEP_E_INVALID;
     std::string o;
-    int64_t n = format_site(c, *s, o);
+    int64_t n = format_site(c, *s, o, true);
     if (buf && cap > 0) {
         int64_t k = std::min<int64_t>(n, cap - 1);
         std::memcpy(buf, o.data(), (size_t)k);

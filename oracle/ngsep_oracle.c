@@ -520,7 +520,8 @@ static void print_pool_call(FILE* out, const char* seqName, const ngo_call* c) {
     const int n = c->pool_n;
     fprintf(out, "%s\t%d\t%s\t%c\t", seqName, c->pos, c->id ? c->id : ".", c->ref);
     for (int i = 1; i < n; i++) fprintf(out, "%s%c", i > 1 ? "," : "", BASES[c->pool_dna[i]]);
-    if (c->pool_multi) fprintf(out, "\t%d\t.\tTYPE=MULTISNV", c->qual);
+    if (c->embedded) fprintf(out, "\t%d\t.\tTYPE=EMBEDDED", c->qual);        /* an SNV inside an indel (:227) */
+    else if (c->pool_multi) fprintf(out, "\t%d\t.\tTYPE=MULTISNV", c->qual);
     else if (type_name(c->known_type)) fprintf(out, "\t%d\t.\tTYPE=%s", c->qual, type_name(c->known_type));
     else fprintf(out, "\t%d\t.\t.", c->qual);
     fprintf(out, c->known ? "\tGT:PL:GQ:DP:BSDP:ACN\t" : "\tGT:PL:GQ:DP:ADP:ACN\t");
@@ -923,8 +924,13 @@ static void rac_print(FILE* out, const ngo_rac* R) {
 }
 
 static void free_indel_call(struct ngo_indel_call_s* c);
+static void pool_known_first_cn(ngo_call* c, int ploidy);
 static void on_sequence_end(ngo_gen* G) {
-    /* SingleSampleVariantsDetector.saveSequenceVariants, :933-968: calls are already in position order */
+    /* SingleSampleVariantsDetector.saveSequenceVariants, :933-968: calls are already in position order.
+     * intersectVariantsCNVs (:969-1008) calls updateAllelesCopyNumberFromCounts(normalPloidy) on the first call only
+     * (with no CNV the index runs to the end and the loop breaks): it matters for the pool algorithm's input records,
+     * whose ACN genotypeVariantPool set (setAllelesCopyNumber :498) */
+    if (G->calls.n > 0) pool_known_first_cn(&G->calls.c[0], G->p->ploidy);
     for (int i = 0; i < G->calls.n; i++) {
         print_call(G->out, G->g->s[G->cur_seq].name, &G->calls.c[i]);
         if (G->calls.c[i].indel) free_indel_call(G->calls.c[i].indel);
@@ -1155,14 +1161,15 @@ static int pool_discover(const ngo_counts* h4, const ngo_acalls* calls, int pos,
 }
 
 /* -knownVariants with ploidy >= 3: genotypeVariantSample (:361-391) -> genotypeVariantPool, setAllCounts,
- * makeUndecided below -minQuality; intersectVariantsCNVs then recomputes ACN from the counts (:986) */
+ * makeUndecided below -minQuality */
 static void pool_known(const ngo_counts* h4, const ngo_acalls* calls, const ngo_known* kv, const ngo_params* p,
                        double hetRate, ngo_call* out) {
     int dna[2] = {base_idx(kv->ref), base_idx(kv->alt)};
     ngo_pcall pc;
     genotype_pool(dna, 2, p->ploidy, calls, hetRate, p->max_base_qs, &pc);
-    if ((int16_t)p->min_quality > pc.gq) { pc.n_called = 0; pc.gq = 0; }   /* makeUndecided */
-    pool_update_cn(&pc, p->ploidy);
+    /* makeUndecided below -minQuality; otherwise the ACN genotypeVariantPool set stays (intersectVariantsCNVs recomputes
+     * it from the counts for the first record of the sequence only: on_sequence_end) */
+    if ((int16_t)p->min_quality > pc.gq) { pc.n_called = 0; pc.gq = 0; pool_update_cn(&pc, pc.total_cn); }
     memset(out, 0, sizeof(*out));
     out->pos = kv->pos; out->ref = kv->ref; out->known = 1; out->id = kv->id; out->qual = kv->qs; out->known_type = kv->type;
     out->strand_bias = -1; out->ploidy = p->ploidy;
@@ -1580,6 +1587,87 @@ static void iscall_update_cn(ngo_iscall* c, int n, int total) {
     }
 }
 
+/* genotypeVariantPool (SingleSampleVariantPileupListener.java:402-503) over an indel variant: one CountsHelper
+ * .calculateCountsIndel per heterozygosity hypothesis (freq = k / haplotypes < 0.51, :410-414), the major allele by
+ * the first helper's counts (undecided with no report and no depth below `haplotypes` calls, :428-432), every other
+ * allele's homozygous-vs-heterozygous posteriors (:447-470), GQ and setAllelesCopyNumber (:482-498), the report from
+ * the chosen helper (:499-500) */
+static void genotype_pool_indel(const ngo_sv* alleles, const ngo_icalls* calls, int haplotypes, double h, int max_base_qs,
+                                ngo_iscall* out) {
+    const int n = alleles->n;
+    memset(out, 0, sizeof(*out));
+    out->counts = calloc((size_t)n, sizeof(int));
+    out->logc = calloc((size_t)n * n, sizeof(double));
+    out->acn = calloc((size_t)n, sizeof(int));
+    const double step = 1.0 / (double)haplotypes;
+    int nf = 0;
+    for (double freq = step; freq < 0.51; freq += step) nf++;
+    double* freqs = malloc(sizeof(double) * (nf ? nf : 1));
+    ngo_icounts* hs = malloc(sizeof(ngo_icounts) * (nf ? nf : 1));
+    nf = 0;
+    for (double freq = step; freq < 0.51; freq += step) {
+        freqs[nf] = freq;
+        icounts_run(&hs[nf], alleles, calls, max_base_qs, freq);
+        nf++;
+    }
+    const ngo_icounts* helper = &hs[0];
+    int major = 0;                                            /* NumberArrays.getIndexMaximum: first maximum */
+    for (int i = 1; i < n; i++) if (helper->counts[major] < helper->counts[i]) major = i;
+    if (helper->counts[major] < haplotypes) {
+        iscall_update_cn(out, n, haplotypes);                 /* undecided.updateAllelesCopyNumberFromCounts */
+    } else {
+        const double logPriorHetero = log10(h), logPriorHomo = log10(1 - h);
+        double* terms = malloc(sizeof(double) * (size_t)(nf + 1));
+        const double termHomozygous = helper->logc[major * n + major] + logPriorHomo;
+        double maxHetPosterior = 0, minHomoPosterior = 1, maxFreq = 0;
+        int maxFreqIdx = 0, maxAlt = -1;
+        for (int i = 0; i < n; i++) {
+            if (i == major) continue;
+            terms[0] = termHomozygous;
+            for (int j = 0; j < nf; j++) terms[j + 1] = hs[j].logc[major * n + i] + logPriorHetero;
+            calc_posteriors(terms, nf + 1);
+            int idxMax = 0;
+            for (int j = 1; j <= nf; j++) if (terms[idxMax] < terms[j]) idxMax = j;
+            if (idxMax == 0) {
+                if (terms[0] < minHomoPosterior) minHomoPosterior = terms[0];
+            } else if (maxAlt == -1 || maxHetPosterior < terms[idxMax]) {
+                maxHetPosterior = terms[idxMax];
+                maxFreqIdx = idxMax - 1;
+                maxFreq = freqs[maxFreqIdx];
+                maxAlt = i;
+            }
+        }
+        free(terms);
+        if (maxAlt == -1) { out->n_called = 1; out->called[0] = major; }
+        else { out->n_called = 2; out->called[0] = major < maxAlt ? major : maxAlt; out->called[1] = major < maxAlt ? maxAlt : major; }
+        out->dp = helper->total_count;
+        if (maxAlt == -1) {
+            out->gq = ngo_phred(1 - minHomoPosterior);
+            out->acn[major] = haplotypes;
+        } else {
+            helper = &hs[maxFreqIdx];
+            /* CountsHelper.getPosteriorProbabilities(hetRate, majorAlleleIdx) (CountsHelper.java:451-467) */
+            double* ev = malloc(sizeof(double) * (size_t)n);
+            const double lph = log10(h / (n - 1)), lpo = log10(1 - h);
+            for (int j = 0; j < n; j++) ev[j] = helper->logc[major * n + j] + (j == major ? lpo : lph);
+            calc_posteriors(ev, n);
+            out->gq = ngo_phred(1 - ev[maxAlt]);
+            free(ev);
+            int altCN = (int)(int16_t)ngo_java_round(maxFreq * haplotypes);
+            if (altCN == 0) altCN++;
+            else if (altCN == haplotypes) altCN--;
+            out->acn[maxAlt] = altCN;
+            out->acn[major] = haplotypes - altCN;
+        }
+        out->total_cn = haplotypes;                           /* setAllelesCopyNumber */
+        out->has_report = 1;
+        memcpy(out->counts, hs[0].counts, sizeof(int) * (size_t)n);
+        memcpy(out->logc, helper->logc, sizeof(double) * (size_t)n * n);
+    }
+    for (int j = 0; j < nf; j++) { free(hs[j].counts); free(hs[j].logc); }
+    free(freqs); free(hs);
+}
+
 /* genotypeVariantSample for an indel variant at ploidy < 3 (SingleSampleVariantPileupListener.java:377-390) with a
  * fresh listener (minQuality = DEF_MIN_QUALITY 40): calculateCountsIndel over the variant's alleles, callIndel with
  * the variant (indexes of the maximum genotype taken as they are, :335-345), updateAllelesCopyNumberFromCounts(ploidy),
@@ -1587,6 +1675,12 @@ static void iscall_update_cn(ngo_iscall* c, int n, int total) {
 static void genotype_indel_sample(const ngo_sv* alleles, const ngo_icalls* calls, double het, int ploidy, int max_base_qs,
                                   int min_quality, ngo_iscall* c) {
     const int n = alleles->n;
+    if (ploidy >= 3) {
+        /* ploidy >= DEF_MIN_PLOIDY_POOL_ALGORITHM: genotypeVariantPool (:378-379), then makeUndecided below min_quality */
+        genotype_pool_indel(alleles, calls, ploidy, het, max_base_qs, c);
+        if ((int16_t)min_quality > c->gq) { c->n_called = 0; c->gq = 0; iscall_update_cn(c, n, c->total_cn); }
+        return;
+    }
     memset(c, 0, sizeof(*c));
     c->counts = calloc((size_t)n, sizeof(int));
     c->logc = calloc((size_t)n * n, sizeof(double));
@@ -2003,8 +2097,16 @@ static void mvd_on_pileup_known(ngo_gen* G, int pos) {
     }
 }
 
-/* a genotyped -knownVariants indel / MNP of the single-sample listener */
-struct ngo_kindel { ngo_iscall c; const ngo_known* kv; int ploidy; };
+/* a genotyped -knownVariants indel / MNP of the single-sample listener, or an indel of the pool algorithm (ploidy >= 3)
+ * -- a CalledGenomicVariantImpl over a GenomicVariantImpl, FORMAT DEF_FORMAT_ARRAY_NGSEP_NOSNV */
+struct ngo_kindel {
+    ngo_iscall c;
+    int pos, n, qs, type, ploidy;
+    char** alleles;            /* reference first */
+    int own;                   /* alleles owned (a discovered variant) or the input record's */
+    const char* id;
+    int pool_known;            /* ploidy >= 3 input record: ACN from genotypeVariantPool unless first of its sequence */
+};
 
 /* SingleSampleVariantPileupListener.genotypeVariantSample (:361-391), non-SNV branch at ploidy < 3: getAlleleCalls(
  * |REF|, null), calculateCountsIndel over the variant's alleles, callIndel with the variant (VariantDiscoverySNVQ
@@ -2018,8 +2120,10 @@ static void genotype_known_indel(ngo_gen* G, const ngo_known* kv, int pos, ngo_c
     pileup_calls(G->pileup.a, G->pileup.n, pos, (int)strlen(kv->alleles[0]), &calls);
     struct ngo_kindel* k = calloc(1, sizeof(*k));
     genotype_indel_sample(&v, &calls, G->het_rate, p->ploidy, p->max_base_qs, p->min_quality, &k->c);
-    k->kv = kv;
+    k->pos = kv->pos; k->n = kv->n_alleles; k->alleles = kv->alleles; k->own = 0;
+    k->id = kv->id; k->qs = kv->qs; k->type = kv->type;
     k->ploidy = p->ploidy;
+    k->pool_known = p->ploidy >= 3;
     icalls_free(&calls);
     sv_free(&v);
     memset(out, 0, sizeof(*out));
@@ -2030,13 +2134,12 @@ static void genotype_known_indel(ngo_gen* G, const ngo_known* kv, int pos, ngo_c
 
 /* VCFFileWriter.printVCFRecord of the call: the input's ID, alleles, QS and TYPE, FORMAT DEF_FORMAT_ARRAY_NGSEP_NOSNV */
 static void print_kindel(FILE* out, const char* seqName, const struct ngo_kindel* k) {
-    const ngo_known* kv = k->kv;
     const ngo_iscall* c = &k->c;
-    const int n = kv->n_alleles;
-    fprintf(out, "%s\t%d\t%s\t%s\t", seqName, kv->pos, kv->id ? kv->id : ".", kv->alleles[0]);
-    for (int i = 1; i < n; i++) fprintf(out, "%s%s", i > 1 ? "," : "", kv->alleles[i]);
-    fprintf(out, "\t%d\t.\t", kv->qs);
-    if (type_name(kv->type)) fprintf(out, "TYPE=%s", type_name(kv->type));
+    const int n = k->n;
+    fprintf(out, "%s\t%d\t%s\t%s\t", seqName, k->pos, k->id ? k->id : ".", k->alleles[0]);
+    for (int i = 1; i < n; i++) fprintf(out, "%s%s", i > 1 ? "," : "", k->alleles[i]);
+    fprintf(out, "\t%d\t.\t", k->qs);
+    if (type_name(k->type)) fprintf(out, "TYPE=%s", type_name(k->type));
     else fprintf(out, ".");
     fprintf(out, "\tGT:PL:GQ:DP:ADP:ACN\t");
     if (c->n_called == 0) fprintf(out, k->ploidy > 1 ? "./." : ".");
@@ -2053,7 +2156,101 @@ static void print_kindel(FILE* out, const char* seqName, const struct ngo_kindel
     else for (int j = 0; j < n; j++) fprintf(out, "%s%d", j ? "," : "", (c->n_called == 0 && j == 0) ? c->total_cn : c->acn[j]);
     fprintf(out, "\n");
 }
-static void free_kindel(struct ngo_kindel* k) { iscall_free(&k->c); free(k); }
+static void free_kindel(struct ngo_kindel* k) {
+    iscall_free(&k->c);
+    if (k->own) { for (int i = 0; i < k->n; i++) free(k->alleles[i]); free(k->alleles); }
+    free(k);
+}
+
+static void push_call(ngo_gen* G, const ngo_call* c);
+static int same_lengths(const ngo_sv* v);
+static void pool_known_first_cn(ngo_call* c, int ploidy) {
+    if (c->kindel && c->kindel->pool_known) iscall_update_cn(&c->kindel->c, c->kindel->n, ploidy);
+    if (c->pool && c->known) {
+        ngo_pcall pc;
+        memset(&pc, 0, sizeof(pc));
+        pc.n_called = c->pool_ncalled; pc.called[0] = c->pool_called[0]; pc.called[1] = c->pool_called[1];
+        pc.report = c->pool_report;
+        for (int i = 0; i < 4; i++) pc.counts[i] = c->pool_counts[i];
+        pool_update_cn(&pc, ploidy);
+        for (int i = 0; i < 4; i++) c->pool_acn[i] = pc.acn[i];
+        c->pool_total_cn = pc.total_cn;
+    }
+}
+static void ngo_call_kindel(ngo_gen* G, int pos, const ngo_sv* alleles, ngo_iscall* c) {
+    struct ngo_kindel* k = calloc(1, sizeof(*k));
+    k->c = *c;
+    k->pos = pos; k->n = alleles->n; k->own = 1;
+    k->alleles = malloc(sizeof(char*) * (size_t)alleles->n);
+    for (int i = 0; i < alleles->n; i++) k->alleles[i] = strdup(alleles->s[i]);
+    k->ploidy = G->p->ploidy;
+    ngo_call call;
+    memset(&call, 0, sizeof(call));
+    call.pos = pos;
+    call.kindel = k;
+    push_call(G, &call);
+}
+
+/* ploidy >= 3, a span > 1 (discoverVariantWithSpan :257-273 -> discoverIndel :275-296): the clustered alleles' pool
+ * variant (createIndelVariantPool :333-338: none for one allele, no calls or alleles of one length), genotypeVariantPool;
+ * a multi-allelic variant keeps its alleles when two non-reference alleles are called, else becomes the reference and
+ * the called allele (makeNewVariant :346-359) and is genotyped again; an undecided, homozygous-reference or low-GQ
+ * call is dropped (:263, :223); a kept call's ACN from its counts (:226) and lastIndelEnd = its last (:157-160).
+ * The variant's type stays TYPE_UNDETERMINED (no INFO TYPE) and its QS 0.  1 when a call is kept. */
+static int pool_discover_indel(ngo_gen* G, int pos, int last, int is_input_str) {
+    const ngo_params* p = G->p;
+    const ngo_seq* s = &G->g->s[G->cur_seq];
+    int lr = 0;
+    char* ref = ref_upper(s, pos, last, &lr);
+    ngo_icalls calls = {0};
+    pileup_calls(G->pileup.a, G->pileup.n, pos, lr, &calls);
+    ngo_sv alleles = {0};
+    cluster_allele_calls(&calls, ref, p->max_base_qs, &alleles);
+    ngo_icounts ih;
+    icounts_run(&ih, &alleles, &calls, p->max_base_qs, 0.5);
+    const int total = ih.total_count;
+    free(ih.counts); free(ih.logc);
+    int kept = 0;
+    (void)is_input_str;
+    if (alleles.n > 1 && total > 0 && !same_lengths(&alleles)) {
+        ngo_iscall c;
+        genotype_pool_indel(&alleles, &calls, p->ploidy, G->het_rate, p->max_base_qs, &c);
+        int ok = 1;
+        if (alleles.n > 2) {
+            const int homref = c.n_called == 1 && c.called[0] == 0;
+            if (c.n_called == 0 || homref) ok = 0;
+            else if (!(c.n_called == 2 && c.called[0] != 0)) {
+                ngo_sv nv = {0};                               /* {reference} + the called alleles, in that order */
+                sv_push(&nv, alleles.s[0], (int)strlen(alleles.s[0]));
+                for (int i = 0; i < c.n_called; i++)
+                    if (strcmp(alleles.s[c.called[i]], alleles.s[0]) != 0) sv_push(&nv, alleles.s[c.called[i]], (int)strlen(alleles.s[c.called[i]]));
+                iscall_free(&c);
+                if (same_lengths(&nv)) { ok = 0; sv_free(&nv); }
+                else {
+                    sv_free(&alleles);
+                    alleles = nv;
+                    genotype_pool_indel(&alleles, &calls, p->ploidy, G->het_rate, p->max_base_qs, &c);
+                }
+            }
+        }
+        if (ok) {
+            const int homref = c.n_called == 1 && c.called[0] == 0;
+            if (c.n_called == 0 || homref || (int16_t)p->min_quality > c.gq) ok = 0;
+        }
+        if (ok) {
+            iscall_update_cn(&c, alleles.n, p->ploidy);         /* discoverVariant: updateAllelesCopyNumberFromCounts */
+            ngo_call_kindel(G, pos, &alleles, &c);
+            G->last_indel_end = pos + (int)strlen(alleles.s[0]) - 1;
+            kept = 1;
+        } else if (c.counts) {
+            iscall_free(&c);
+        }
+    }
+    sv_free(&alleles);
+    icalls_free(&calls);
+    free(ref);
+    return kept;
+}
 
 static void push_call(ngo_gen* G, const ngo_call* c) {
     if (G->calls.n == G->calls.cap) { G->calls.cap = G->calls.cap ? 2 * G->calls.cap : 1024; G->calls.c = realloc(G->calls.c, sizeof(ngo_call) * G->calls.cap); }
@@ -2076,7 +2273,11 @@ static void discover_with_span(ngo_gen* G, int pos, int span, int is_str, int is
     if (p->ignore_lowercase_ref && islower((unsigned char)s->seq[pos - 1])) return;
     int eff = embedded ? 1 : span;
     ngo_call c;
-    if (eff > 1) {
+    const int pool = p->ploidy >= 3;
+    if (eff > 1 && pool) {
+        if (pool_discover_indel(G, pos, last, is_input_str)) return;
+        if (is_input_str) return;
+    } else if (eff > 1) {
         int lr = 0;
         char* ref = ref_upper(s, pos, last, &lr);
         ngo_icalls calls = {0};
@@ -2105,7 +2306,7 @@ static void discover_with_span(ngo_gen* G, int pos, int span, int is_str, int is
     }
     /* discoverSNV (also the fallback of a span whose indel alleles made no call, :264-271) */
     char R = (char)toupper((unsigned char)s->seq[pos - 1]);
-    if (discover_snv(h, pos, R, p, G->het_rate, &c)) {
+    if (pool ? pool_discover(h, &G->acalls, pos, R, p, G->het_rate, &c) : discover_snv(h, pos, R, p, G->het_rate, &c)) {
         c.embedded = embedded;
         c.indel = NULL;
         push_call(G, &c);
@@ -2622,13 +2823,11 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
     G.cov = cov;
     G.rac = rac;
     /* the indel realigner: first in both detectors' listener chains (SingleSampleVariantsDetector.java:919-925,
-     * MultisampleVariantsDetector.java:449-450), at ploidy < 3 here; with -knownVariants its input variants are the
-     * known records (fixed events), else the -knownSTRs */
-    G.realign = !cov && !rac && !p->indel_passthrough && p->ploidy < 3;
+     * MultisampleVariantsDetector.java:449-450), at every ploidy; with -knownVariants its input variants are the known
+     * records (fixed events), else the -knownSTRs */
+    G.realign = !cov && !rac && !p->indel_passthrough;
     if (p->known_vcf && p->known_vcf[0]) {
         int lrc = load_known(p->known_vcf, &g, &G.known, &G.n_known);
-        if (lrc == NGO_OK && p->ploidy >= 3)               /* the pool algorithm's indel branch is not restated */
-            for (int i = 0; i < G.n_known; i++) if (!G.known[i].snv) { lrc = NGO_UNSUPPORTED; break; }
         if (lrc != NGO_OK) {
             if (G.known) known_free(G.known, G.n_known);
             fclose(in); if (out != stdout) fclose(out); if (dump) fclose(dump);

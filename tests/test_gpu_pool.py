@@ -136,3 +136,68 @@ def test_pool_population_vcf_identical(tmp_path, ploidy, n_samples, opts):
     orec = _records(o)
     assert len(orec) > 30
     assert _records(d.outFilename) == orec
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ploidy,kw,opts", [
+    (4, dict(depth=40, seed=81, indel_rate=6e-4, snv_rate=3e-3), {}),
+    (3, dict(depth=30, seed=82, indel_rate=4e-4, snv_rate=3e-3), {"call_embedded": 1}),
+    (6, dict(depth=50, seed=83, indel_rate=5e-4, snv_rate=2e-3, quality_model=2), {"window_positions": 40000, "min_quality": 20}),
+])
+def test_pool_indel_regions_vcf_identical(tmp_path, ploidy, kw, opts):
+    """The indel realigner at ploidy >= 3 (its listener chain has no ploidy limit, SingleSampleVariantsDetector.java
+    :919-925): the pool algorithm's indel branch over the realigner's spans (discoverIndel :275-296, createIndelVariantPool
+    :333-338, genotypeVariantPool over the indel alleles :402-503), the pool SNV fallback and the realigned alignments'
+    SNVs on the device (k_posterior_pool over the replayed columns).  WHOLE VCF equal to the oracle's."""
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=2, **kw)
+    fa, sam, bam = syn.write(os.path.join(str(tmp_path), "pi"))
+    syn.close()
+    o = os.path.join(str(tmp_path), "o.vcf")
+    ngsep_oracle.run_ssvd(fa, sam, o, ploidy=ploidy, **{k: v for k, v in opts.items() if k != "window_positions"})
+    g = os.path.join(str(tmp_path), "g.vcf")
+    with GpuPileupSession(gpu_params(ploidy=ploidy, **opts)) as s:
+        s.load_fasta(fa)
+        s.processFile(bam, g)
+        assert s.carved_regions() == []
+    orec, grec = _records(o), _records(g)
+    assert sum(1 for l in orec if len(l.split("\t")[3]) > 1 or "," in l.split("\t")[4] or len(l.split("\t")[4]) > 1) > 5
+    assert grec == orec
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ploidy", [4])
+def test_pool_known_indels_vcf_identical(tmp_path, ploidy):
+    """-knownVariants at ploidy >= 3 with indel / MNP inputs: genotypeVariantPool over each record's alleles
+    (genotypeVariantSample :378-379), makeUndecided below -minQuality, the copy numbers genotypeVariantPool set -- except
+    for a sequence's first record, which intersectVariantsCNVs recomputes from the counts (:969-991)."""
+    from test_gpu_known import _known_vcf_indels
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=2, depth=40, seed=84, indel_rate=5e-4, snv_rate=3e-3)
+    fa, sam, bam = syn.write(os.path.join(str(tmp_path), "pk"))
+    disc = os.path.join(str(tmp_path), "disc.vcf")
+    ngsep_oracle.run_ssvd(fa, sam, disc, ploidy=ploidy)
+    known = os.path.join(str(tmp_path), "known.vcf")
+    n = _known_vcf_indels(known, syn, disc, 84, n_random=300)
+    syn.close()
+    o = os.path.join(str(tmp_path), "o.vcf")
+    ngsep_oracle.run_ssvd(fa, sam, o, ploidy=ploidy, known_vcf=known)
+    g = os.path.join(str(tmp_path), "g.vcf")
+    _run_gpu(fa, bam, g, known=known, ploidy=ploidy)
+    orec = _records(o)
+    assert len(orec) > n // 2
+    assert _records(g) == orec
+
+
+@pytest.mark.gpu
+def test_pool_population_indels_vcf_identical(tmp_path):
+    """MultisampleVariantsDetector at ploidy 4 with the realigner: every sample's indel genotype by genotypeVariantPool
+    (genotypeVariantSample :378-379, makeUndecided below 40), discoverPopulationIndel's shrink loop, KPM's pool branch over
+    the regions' columns.  Population VCF equal to the oracle's (path A)."""
+    from test_gpu_multisample import gpu_mvd, oracle_mvd, population
+    from helpers import diff_vcf
+    syn, fa, sam, rgs = population(tmp_path, genome=pysynth.CUSTOM, custom_len=50000, n_samples=8, depth=16, seed=85,
+                                   indel_rate=5e-4, snv_rate=3e-3)
+    o = oracle_mvd(tmp_path, fa, sam, 0.0, ploidy=4)
+    assert sum(1 for l in _records(o) if "TYPE=INDEL" in l or "TYPE=STR" in l) > 3
+    g, _ = gpu_mvd(tmp_path, syn, rgs, ploidy=4)
+    d = diff_vcf(o, g)
+    assert not d, "\n".join(d[:20])
