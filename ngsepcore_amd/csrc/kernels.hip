@@ -88,6 +88,7 @@ struct RunSlot {                     // one in-flight single-sample run (see dev
     hipEvent_t ev[6] = {};                   // KT start, KT end, KP end, after KO, copies done, KP start
     int64_t guess = 0;
     bool busy = false;
+    bool scan_timed = false;                     // this run recorded ev[0] / ev[1] around its scan (KL or KQ)
     int prune = 0;
     GenotypeParams g{};
     LikTables tabs{};
@@ -913,35 +914,11 @@ __device__ __forceinline__ uint32_t kl_nonref(uint32_t y) {
 //   DEEP:  one 32-bit counter per position (exceptions | other-allele << 16) at word 8 + i, one add per exception.
 // Counts at positions outside the tile (margins) are never read; they are bounded by the tile's own depth (a read
 // that reaches them covers the tile's first or last position), so they cannot carry into the tile's counters.
-// !DEEP: the five packed adds of a unit that holds an exception (unit byte 0 at counter index ob; flags F: per byte k,
-// bit 8k exception in the low dword, bit 8k + 1 in the high dword, bits 8k + 2 / 8k + 3 other-allele calls)
-__device__ __forceinline__ void kl_unit_adds(uint32_t* s_cnt, uint32_t ob, uint32_t F) {
-    const uint32_t fl = F & 0x01010101u, fh = (F >> 1) & 0x01010101u, ml = (F >> 2) & 0x01010101u, mh = (F >> 3) & 0x01010101u;
-    const int sh = (ob & 1) << 1;                         // byte offset of the unit's first halfword
-    const uint32_t w0 = __builtin_amdgcn_perm(ml, fl, 0x05010400u), w1 = __builtin_amdgcn_perm(ml, fl, 0x07030602u);
-    const uint32_t w2 = __builtin_amdgcn_perm(mh, fh, 0x05010400u), w3 = __builtin_amdgcn_perm(mh, fh, 0x07030602u);
-    uint32_t* c = s_cnt + ((ob + 1) >> 1) - 1;            // sh = 0: the first add is of 0
-    atomicAdd(c, __builtin_amdgcn_alignbyte(w0, 0u, sh));
-    atomicAdd(c + 1, __builtin_amdgcn_alignbyte(w1, w0, sh));
-    atomicAdd(c + 2, __builtin_amdgcn_alignbyte(w2, w1, sh));
-    atomicAdd(c + 3, __builtin_amdgcn_alignbyte(w3, w2, sh));
-    atomicAdd(c + 4, __builtin_amdgcn_alignbyte(0u, w3, sh));
-}
-
-// !DEEP: the wave's exception units are queued in its LDS slots (ballot-compacted, one 8-B entry each: ob, F) and
-// their adds issued 64 at a time with every lane busy -- a unit with an exception is ~1 lane in 5, so this issues ~5x
-// fewer LDS add instructions than adding in place
-constexpr int kKlQueue = 128;                             // entries per wave (a flush leaves < 64)
-
 template <int T, bool DEEP, int U>
 __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, const int2* __restrict__ rh,
                                           const RGroup* __restrict__ grp, int64_t e_lo, int64_t e_hi, int32_t tstart,
-                                          int32_t* s_diff, uint32_t* s_cnt, bool do_diff, int32_t ablate, uint32_t& sink,
-                                          uint2* s_q) {
+                                          int32_t* s_diff, uint32_t* s_cnt, bool do_diff, int32_t ablate, uint32_t& sink) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint2* q = s_q + wv * kKlQueue;
-    int fill = 0;                                         // (wave-uniform) queued entries
-    const bool compact = !DEEP && !ABLATE(ablate, 128 | 512 | 1024 | 2048 | 8192 | 16384);
     const int64_t g_lo = e_lo >> 6, g_hi = (e_hi + 63) >> 6;
     const bool no_counts = ABLATE(ablate, 128), no_units = ABLATE(ablate, 256);   // diagnostics
     int64_t g = g_lo + wv;
@@ -961,47 +938,14 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
         const int32_t ob0 = gf - tstart + 8 * k0 + 8;     // counter index of unit k0's byte 0 (>= 1)
         const int sh = (ob0 & 1) << 1;                    // !DEEP: byte offset of the unit's first halfword
         const uint64_t* ub = units + G.base + lane + (int64_t)k0 * 64;
-        // the wave's trip count (its longest lane: every lane stays in the loop, so the queue's ballots and flushes see
-        // all 64); loads are unconditional for a lane with units (a batch's slots past the read's last unit repeat it)
-        // so that each unit waits for its own load only
-        int32_t knw = kn;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) knw = max(knw, __shfl_xor(knw, o, 64));
-        for (int32_t j = 0; j <= knw; j += U) {
+        // a lane's own trip count (the wave runs while any lane has units left); loads are unconditional (a
+        // batch's slots past the read's last unit repeat it) so that each unit waits for its own load only
+        for (int32_t j = 0; j <= kn; j += U) {
             uint64_t u[U];
 #pragma unroll
-            for (int i = 0; i < U; i++) u[i] = kn >= 0 ? ub[(int64_t)min(j + i, kn) * 64] : 0ull;
+            for (int i = 0; i < U; i++) u[i] = ub[(int64_t)min(j + i, kn) * 64];
 #pragma unroll
             for (int i = 0; i < U; i++) {
-                if (compact) {
-                    // every lane reaches the ballot (lanes past their read's last unit queue nothing)
-                    const uint32_t ylo = (uint32_t)u[i], yhi = (uint32_t)(u[i] >> 32);
-                    const uint32_t elo = kl_exc(ylo), ehi = kl_exc(yhi);
-                    const bool has = j + i <= kn && (elo | ehi) != 0;
-                    const unsigned long long m = __ballot(has);
-                    if (m == 0) continue;
-                    if (has) {
-                        const uint32_t nlo = kl_nonref(ylo), nhi = kl_nonref(yhi);
-                        const uint32_t F = (elo >> 7) | (ehi >> 6) | (nlo >> 5) | (nhi >> 4);
-                        const int rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                        q[fill + rk] = make_uint2((uint32_t)(ob0 + 8 * (j + i)), F);
-                    }
-                    fill += (int)__popcll(m);
-                    if (fill >= 64) {
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                        const uint2 e = q[lane];
-                        const uint2 t = lane + 64 < fill ? q[lane + 64] : make_uint2(0u, 0u);
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                        if (lane + 64 < fill) q[lane] = t;
-                        fill -= 64;
-                        kl_unit_adds(s_cnt, e.x, e.y);
-                    }
-                    continue;
-                }
                 if (j + i > kn) continue;
                 const uint32_t ylo = (uint32_t)u[i], yhi = (uint32_t)(u[i] >> 32);
                 const uint32_t elo = kl_exc(ylo), ehi = kl_exc(yhi);
@@ -1026,7 +970,11 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
                     if (ABLATE(ablate, 1024)) { atomicAdd(c, w0 + w1 + w2 + w3); continue; }   // diagnostics: one add
                     if (ABLATE(ablate, 8192) && i != 0) continue;   // diagnostics: a batch's first unit only
                     if (ABLATE(ablate, 16384)) { sink += atomicAdd(c, w0 + w1 + w2 + w3); continue; }   // diagnostics: returning add
-                    kl_unit_adds(s_cnt, (uint32_t)ob, fl | fh << 1 | ml << 2 | mh << 3);
+                    atomicAdd(c, __builtin_amdgcn_alignbyte(w0, 0u, sh));
+                    atomicAdd(c + 1, __builtin_amdgcn_alignbyte(w1, w0, sh));
+                    atomicAdd(c + 2, __builtin_amdgcn_alignbyte(w2, w1, sh));
+                    atomicAdd(c + 3, __builtin_amdgcn_alignbyte(w3, w2, sh));
+                    atomicAdd(c + 4, __builtin_amdgcn_alignbyte(0u, w3, sh));
                 } else {
                     uint64_t ex = (uint64_t)elo | (uint64_t)ehi << 32;
                     const uint64_t nr = (uint64_t)nlo | (uint64_t)nhi << 32;
@@ -1039,12 +987,6 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
             }
         }
         h = hn;
-    }
-    if (compact && fill > 0) {                            // the queue's remainder
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (lane < fill) { const uint2 e = q[lane]; kl_unit_adds(s_cnt, e.x, e.y); }
     }
 }
 
@@ -1061,7 +1003,6 @@ __global__ __launch_bounds__(kKlThreads) void k_read_scan(
     __shared__ alignas(16) int32_t s_diff[T + 32];     // coverage differences; then DEEP's counters (word 8 + i)
     __shared__ alignas(16) uint32_t s_ref[T / 4];
     __shared__ alignas(16) uint32_t s_cnt[NC];
-    __shared__ uint2 s_q[(kKlThreads / 64) * kKlQueue];   // the waves' exception-unit queues (kl_stream)
     __shared__ int16_t s_cb[256];
     __shared__ int32_t s_wsum[kKlThreads / 64], s_wmax[kKlThreads / 64];
     __shared__ unsigned long long s_wscan[kKlThreads / 64], s_ncand[kKlThreads / 64], s_colbase, s_qbase;
@@ -1079,7 +1020,7 @@ __global__ __launch_bounds__(kKlThreads) void k_read_scan(
     const int64_t e_lo = blkA[tstart >> kRgBlockShift], e_hi = blkB[(tstart + T) >> kRgBlockShift];
     __syncthreads();
     uint32_t sink = 0;
-    kl_stream<T, false, U>(units, rh, grp, e_lo, e_hi, tstart, s_diff, s_cnt, true, gp.ablate, sink, s_q);
+    kl_stream<T, false, U>(units, rh, grp, e_lo, e_hi, tstart, s_diff, s_cnt, true, gp.ablate, sink);
     __syncthreads();
     // ---- coverage (prefix of the difference array)
     int32_t loc[PT];
@@ -1108,7 +1049,7 @@ __global__ __launch_bounds__(kKlThreads) void k_read_scan(
     if (deep) {                                          // byte counters could carry: stream again, 32-bit counters
         for (int i = tid; i < T + 32; i += kKlThreads) s_deep[i] = 0;
         __syncthreads();
-        kl_stream<T, true, U>(units, rh, grp, e_lo, e_hi, tstart, s_diff, s_deep, false, gp.ablate, sink, s_q);
+        kl_stream<T, true, U>(units, rh, grp, e_lo, e_hi, tstart, s_diff, s_deep, false, gp.ablate, sink);
         __syncthreads();
     }
     if (sink == 0xFFFFFFFFu) s_cnt[0] = sink;            // keeps the diagnostics' work alive
@@ -2609,6 +2550,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
     if (!d->rg) { err = "no read-group layout resident"; return -1; }
     int64_t kg_sites = 0;                                        // KG's sites (estimate)
     bool kl_run = false;                                         // KL's sharded queue (else one segment, count at [2])
+    sl.scan_timed = false;
     if (s.known) {
         // -knownVariants: no scan, the input variants' sites (covered, in window order) are KP's queue
         if (nforced > 0) H2D(sl.d_hard, s.h_forced.data(), (size_t)nforced * sizeof(SiteQ), sl.stream);
@@ -2627,6 +2569,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
                               (const int32_t*)d->d_blkB, d->n_entries, (const uint8_t*)d->d_ref, (const LikTables*)sl.d_tables, g,
                               sl.d_hard, ctr, sl.cap_hard / kKlShards, (sl.cap_cols >> 2) / kKlShards, sl.d_bcount, nb);
         HIP_TRY(launch_check());
+        sl.scan_timed = k0 != nullptr;
         kg_sites = d->last_hard + d->last_hard / 8;              // KL's survivors (sized from the previous run)
         kl_run = true;
     } else {
@@ -2635,6 +2578,7 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         hipExtLaunchKernelGGL(k_queue_all, dim3((unsigned)nblk), dim3(256), 0, sl.stream, k0, k1, 0, (const uint8_t*)d->d_ref,
                               s.g_len, sl.d_hard, ctr, sl.cap_hard, sl.d_bcount, nb);
         HIP_TRY(launch_check());
+        sl.scan_timed = k0 != nullptr;
         kg_sites = s.g_len;
     }
     {
@@ -2819,7 +2763,9 @@ int device_collect(Device* d, SiteStore* out, int64_t* n_out, double* scan_ms, d
     sl.host.clear();
     *n_out = n;
     float a = 0, a2 = 0;
-    if (d->time_scan) (void)hipEventElapsedTime(&a, sl.ev[0], sl.ev[1]);
+    // (only events this run recorded: a -knownVariants run has no scan, and the elapsed time of events never recorded
+    // is an error the next launch check would report)
+    if (d->time_scan && sl.scan_timed) (void)hipEventElapsedTime(&a, sl.ev[0], sl.ev[1]);
     if (d->time_posterior) (void)hipEventElapsedTime(&a2, sl.ev[5], sl.ev[2]);
     *scan_ms = a;
     *geno_ms = a2;

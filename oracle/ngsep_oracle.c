@@ -1965,6 +1965,33 @@ void ngo_t_genotype_indel_sample(int n, const char* const* alleles, int m, const
     sv_free(&al); icalls_free(&ic);
 }
 
+/* genotypeVariantSample over an indel variant at any ploidy (the pool algorithm from 3) with the given minQuality:
+ * "GT:PL:GQ:DP:ADP:ACN" of the call */
+void ngo_t_genotype_indel_sample_q(int n, const char* const* alleles, int m, const char* const* calls, const char* const* quals,
+                                   int max_base_qs, double het, int ploidy, int min_quality, char* out, int cap) {
+    ngo_sv al = {0};
+    ngo_icalls ic = {0};
+    t_alleles(n, alleles, &al);
+    t_calls(m, calls, quals, &ic);
+    ngo_iscall c;
+    genotype_indel_sample(&al, &ic, het, ploidy, max_base_qs, min_quality, &c);
+    int k = 0;
+    if (c.n_called == 0) k += snprintf(out + k, (size_t)(cap - k), ploidy > 1 ? "./." : ".");
+    else if (c.n_called == 1) k += snprintf(out + k, (size_t)(cap - k), ploidy > 1 ? "%d/%d" : "%d", c.called[0], c.called[0]);
+    else k += snprintf(out + k, (size_t)(cap - k), "%d/%d", c.called[0], c.called[1]);
+    k += snprintf(out + k, (size_t)(cap - k), ":");
+    for (int j = 0; j < n; j++)
+        for (int i = 0; i <= j; i++)
+            k += snprintf(out + k, (size_t)(cap - k), "%s%d", (i > 0 || j > 0) ? "," : "", c.has_report ? (int)ngo_java_round(-10 * c.logc[i * n + j]) : 0);
+    k += snprintf(out + k, (size_t)(cap - k), ":%d:%d:", c.gq, c.dp);
+    for (int i = 0; i < n; i++) k += snprintf(out + k, (size_t)(cap - k), "%s%d", i ? "," : "", c.has_report ? c.counts[i] : 0);
+    k += snprintf(out + k, (size_t)(cap - k), ":");
+    if (c.total_cn == 0) k += snprintf(out + k, (size_t)(cap - k), ".");
+    else for (int j = 0; j < n; j++) k += snprintf(out + k, (size_t)(cap - k), "%s%d", j ? "," : "", (c.n_called == 0 && j == 0) ? c.total_cn : c.acn[j]);
+    iscall_free(&c);
+    sv_free(&al); icalls_free(&ic);
+}
+
 /* ReadAlignment edits on an alignment given by its first position and CIGAR (NGSEP codes via parse_cigar):
  * op 0 moveIndelStart(a1, a2), 1 realignStart(a1, a2, a3, a4), 2 realignEnd(a1, a2, a3, a4).  The new CIGAR (the
  * alignment's codes written as SAM text, not collapsed), first and last go to out / *first / *last; returns

@@ -392,6 +392,92 @@ def population_sample_indel(alleles, calls, het_rate, ploidy, max_base_qs=MAX_BA
     return genotype_fields(c, ploidy)
 
 
+def _normalize(ev):
+    """CountsHelper.calculatePosteriorProbabilities (:472-495) on a list"""
+    log_max = 1.0
+    for x in ev:
+        if log_max > 0 or log_max < x:
+            log_max = x
+    out = [0.0 if x - log_max < -20 else math.pow(10.0, x - log_max) for x in ev]
+    tot = sum(out)
+    return [x / tot for x in out]
+
+
+def _first_max(v):
+    """NumberArrays.getIndexMaximum: the first maximum"""
+    k = 0
+    for i in range(1, len(v)):
+        if v[k] < v[i]:
+            k = i
+    return k
+
+
+def pool_genotype_indel(alleles, calls, haplotypes, het_rate, max_base_qs=MAX_BASE_QS):
+    """genotypeVariantPool (SingleSampleVariantPileupListener.java:402-503) over an indel variant: the Called, with the
+    copy numbers setAllelesCopyNumber leaves (:480-498)"""
+    n = len(alleles)
+    step = 1.0 / haplotypes
+    freqs, helpers = [], []
+    freq = step
+    while freq < 0.51:
+        freqs.append(freq)
+        hp = Helper(alleles, max_base_qs, freq)
+        for a, q in calls:
+            hp.update_indel(a, q)
+        helpers.append(hp)
+        freq += step
+    helper = helpers[0]
+    counts = helper.counts
+    major = _first_max(counts)
+    if counts[major] < haplotypes:
+        c = Called(n, [], total_cn=0)            # new CalledGenomicVariantImpl(variant, new byte[0])
+        c.update_cn(haplotypes)
+        return c
+    lph, lpo = math.log10(het_rate), math.log10(1 - het_rate)
+    term_hom = helper.L[major][major] + lpo
+    max_het, min_hom, max_freq_idx, max_freq, max_alt = 0.0, 1.0, 0, 0.0, -1
+    for i in range(n):
+        if i == major:
+            continue
+        terms = _normalize([term_hom] + [helpers[j].L[major][i] + lph for j in range(len(freqs))])
+        k = _first_max(terms)
+        if k == 0:
+            min_hom = min(min_hom, terms[0])
+        elif max_alt == -1 or max_het < terms[k]:
+            max_het, max_freq_idx, max_freq, max_alt = terms[k], k - 1, freqs[k - 1], i
+    called = sorted([major] + ([max_alt] if max_alt != -1 else []))
+    c = Called(n, called, total_cn=0)
+    c.dp = helper.total
+    acn = [0] * n
+    if max_alt == -1:
+        c.gq = phred(1 - min_hom)
+        acn[major] = haplotypes
+    else:
+        helper = helpers[max_freq_idx]
+        # CountsHelper.getPosteriorProbabilities(h, idxMajorAllele) (CountsHelper.java:451-467)
+        ev = _normalize([helper.L[major][j] + (lpo if j == major else math.log10(het_rate / (n - 1))) for j in range(n)])
+        c.gq = phred(1 - ev[max_alt])
+        alt_cn = to_short(jround(max_freq * haplotypes))
+        if alt_cn == 0:
+            alt_cn += 1
+        elif alt_cn == haplotypes:
+            alt_cn -= 1
+        acn[max_alt] = alt_cn
+        acn[major] = haplotypes - alt_cn
+    c.total_cn = sum(acn)                        # setAllelesCopyNumber
+    c.acn = acn
+    c.report = (list(counts), [row[:] for row in helper.L])
+    return c
+
+
+def pool_sample_indel(alleles, calls, het_rate, ploidy, min_quality=40, max_base_qs=MAX_BASE_QS):
+    """genotypeVariantSample at ploidy >= 3 for an indel variant (:378-379, makeUndecided below min_quality :388)"""
+    c = pool_genotype_indel(alleles, calls, ploidy, het_rate, max_base_qs)
+    if min_quality > c.gq:
+        c.make_undecided()
+    return genotype_fields(c, ploidy)
+
+
 # ---- AlleleCallClustersBuilder ----
 def select_best(items, mx):
     """CountsRankHelper.selectBest: counts in TreeMap (key) order, stable sort by count descending"""

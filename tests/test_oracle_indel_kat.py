@@ -33,6 +33,10 @@ def _lib():
         l.ngo_t_genotype_indel_sample.argtypes = [ctypes.c_int, ctypes.POINTER(CP), ctypes.c_int, ctypes.POINTER(CP),
                                                   ctypes.POINTER(CP), ctypes.c_int, ctypes.c_double, ctypes.c_int,
                                                   ctypes.c_char_p, ctypes.c_int]
+        l.ngo_t_genotype_indel_sample_q.restype = None
+        l.ngo_t_genotype_indel_sample_q.argtypes = [ctypes.c_int, ctypes.POINTER(CP), ctypes.c_int, ctypes.POINTER(CP),
+                                                    ctypes.POINTER(CP), ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                                    ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         l.ngo_t_edit.restype = ctypes.c_int
         l.ngo_t_edit.argtypes = [ctypes.c_int, CP, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
@@ -261,3 +265,35 @@ def test_alignment_edit_kats():
     f, l, new = R.realign_start(101, 150, R.parse_cigar("50M"), 103, 5, 110, 12)
     assert (f, R.cigar_text(new)) == (103, "5M5I2M38M")
     assert _edit(1, "50M", 101, 103, 5, 110, 12)[1:3] == ("5M5I2M38M", 103)
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_pool_sample_indel(seed):
+    """genotypeVariantPool over an indel variant (ploidy >= 3: SingleSampleVariantPileupListener.java:378-379, 402-503)
+    and the given-variant callIndel at ploidy < 3 with -minQuality: the oracle's sample call against the restatement's
+    (undecided below `ploidy` calls of the major allele, heterozygous at the best frequency hypothesis, the copy numbers
+    setAllelesCopyNumber leaves, makeUndecided below min_quality)."""
+    rnd = random.Random(9000 + seed)
+    ref = "".join(rnd.choice("ACGT") for _ in range(rnd.randint(3, 9)))
+    calls = _pileup(rnd, ref, rnd.choice([0, 2, 5, 12, 30, 60]), n_haps=rnd.choice([1, 2, 3]))
+    alleles = R.cluster_alleles(calls, ref)
+    if len(alleles) < 2:
+        alleles = [ref, ref + "A"]
+    ploidy = rnd.choice([1, 2, 3, 4, 6, 8])
+    het = rnd.choice([0.001, 0.01, 0.1])
+    minq = rnd.choice([0, 20, 40])
+    out = ctypes.create_string_buffer(8192)
+    _lib().ngo_t_genotype_indel_sample_q(len(alleles), _arr(alleles), len(calls), _arr([c for c, _ in calls]),
+                                        _arr([q for _, q in calls]), 30, het, ploidy, minq, out, 8192)
+    if ploidy >= 3:
+        want = R.pool_sample_indel(alleles, calls, het, ploidy, minq)
+    else:
+        h = R.indel_helper(alleles, calls)
+        c = R.call_indel(alleles, h, het, False, False, variant=alleles)
+        if isinstance(c, tuple):
+            c = c[3]
+        c.update_cn(ploidy)
+        if minq > c.gq:
+            c.make_undecided()
+        want = R.genotype_fields(c, ploidy)
+    assert out.value.decode() == want
