@@ -454,6 +454,8 @@ def main():
                 batch.seq_id = sid.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
             sess.stage(batch)
             t_stage += time.time() - ts
+            if item is not None:
+                log(f"[rank {rank}] staged {human[item][0]} (device run {gi + 1} of {len(groups)})")
             if args.config == "chr20" and rank == 0 and world == 1 and not args.no_e2e:
                 # the same reads as a BAM on local disk for the end-to-end run
                 tmp = tempfile.mkdtemp(prefix="ngsep_e2e_")
