@@ -221,7 +221,7 @@ def end_to_end(fa: str, bam: str, device: int):
 def end_to_end_population(fa: str, bams, device: int):
     """BAM files on disk -> population VCF on disk: MultisampleVariantsDetector.run through
     ngsep_call_population_bams in a fresh context (merge of the sample BAMs in the generator's order, decode,
-    admission, population layout, H2D, KTM/KPM, VCF writing), wall time."""
+    admission, population layout, H2D, KLM/KPM, VCF writing), wall time."""
     from ngsepcore_amd.discovery import MultisampleVariantsDetector
     out = os.path.join(os.path.dirname(fa), "e2e_pop.vcf")
     mvd = MultisampleVariantsDetector()
@@ -541,12 +541,12 @@ def main():
     # bytes the scan kernel moves per launch.  KL: the read-group units (1 B per read base, zero padded to the
     # group's longest read in 8-B units; stats.pile_bytes), 8-B entry headers, 16 B per 64-read group, the
     # reference codes (1 B per global position, halos included) and the two block tables (8 B per 256
-    # positions).  The multisample scan (KTM + KQN) reads its candidate columns (1 B per valid call, 5 B per
-    # column, 8 B per 64 columns), the open-position bits (1 bit per global position) and writes the queue (8 B
-    # per open position)
+    # positions).  The multisample scan (KLM + KQN) reads the population read-group layout the same way (units,
+    # headers, groups) plus its tile's reference codes once per four samples, and sets / scans the open-position
+    # bits (1 bit per global position)
     if multi:
-        kt_bytes = sum(x.pile_bytes + 5 * x.candidates + 8 * x.n_tiles + x.global_positions // 8 + 8 * x.hard_sites
-                       for x in stats_all)
+        kt_bytes = sum(x.pile_bytes + 8 * x.alignments_admitted + 16 * ((x.alignments_admitted + 63) // 64) +
+                       x.global_positions * ((args.samples + 3) // 4) + x.global_positions // 4 for x in stats_all)
     else:
         kt_bytes = sum(x.pile_bytes + 8 * x.alignments_admitted + 16 * ((x.alignments_admitted + 63) // 64) +
                        x.global_positions + x.global_positions // 32 for x in stats_all)
@@ -613,12 +613,10 @@ def main():
         # SURVEY.md 8(d)'s algorithmic bytes (1 B per read base + 1 B reference per genotyped position + 16 B per
         # read) per launch: `achieved` for the single-sample scan KL, which reads exactly that input
         alg_bytes = read_bases + positions + 16 * reads
-        if multi:
-            achieved = kt_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else None
-        else:
-            achieved = alg_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else None
+        # (the multisample scan KLM reads the same input: every sample's read-group units)
+        achieved = alg_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else None
         traffic = load_traffic(workload_key)
-        scan_kernel = "k_scan_multi+k_queue_need" if multi else f"k_read_scan<{tile}>"
+        scan_kernel = "k_scan_pop+k_queue_need" if multi else f"k_read_scan<{tile}>"
         line = {
             "metric": METRIC,
             "value": value,
@@ -632,7 +630,8 @@ def main():
             "vs_baseline": None,
             "dtype": "u8,f64",
             "data": ("synthetic (seeded generator, SURVEY.md 8(d)); " +
-                     ("population candidate columns + pile resident in HBM" if multi else
+                     ("the host packer's population read-group layout (1 B per read base, one stream per sample) "
+                      "resident in HBM; the step scans it" if multi else
                       "the host packer's read-group layout (1 B per read base) resident in HBM; the step scans it")),
             "config": {
                 "workload": workload,
@@ -658,7 +657,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS if achieved else None,
                 "traffic": traffic,
-                "bytes_per_launch": alg_bytes if not multi else kt_bytes,
+                "bytes_per_launch": alg_bytes,
                 "bytes_moved_per_launch": kt_bytes,
                 "kernel_avg_ms": k_avg_ms,
                 "traffic_rate_GBs": (traffic / (k_avg_ms * 1e-3) / 1e9) if traffic and k_avg_ms > 0 else None,

@@ -1696,19 +1696,14 @@ void LayoutArena::release() {
     cap = units_cap = 0;
 }
 
-// Multisample layout.  MultisampleVariantsDetector genotypes every sample from its own read groups
-// (PileupRecord.getAlleleCalls(span, readGroups), :104-111).
-//  * KTM's candidate columns: a sample without a valid call of another allele than the reference at a
-//    position cannot make a decided non-reference call there, so the scan only needs the
-//    (sample, position) columns that hold such a call: its valid calls as bytes ((allele XOR reference
-//    allele) << 5 | quality), in no particular order (the bounds are sums).  Entries are position-major,
-//    then sample, 64 per KTM wave (h_mc_gbase: the byte offset of entry 64k's column).  A column deeper
-//    than kMcMaxCalls keeps its position open without bytes (n = 255).
-//  * KPM's pile: per tile of kPopTile positions and per sample (and one block for the reads of no sample,
-//    which only enter the pooled counts), position-major columns of the sample's nonzero codes in the
-//    order getAlleleCalls visits them: read-group rank, then pending order -- rows = the tile's deepest
-//    column, zero padded (a zero code is no call and counts nothing).
-static int build_multi_layout(Staged& s) {
+// Population read-group layout.  MultisampleVariantsDetector genotypes every sample from its own
+// read groups (PileupRecord.getAlleleCalls(span, readGroups), :104-111), so the admitted reads are split into one
+// stream per (sample, read-group rank) -- the reads of no sample, which only enter the pooled counts, one stream last
+// -- each in pending-list order and laid out as build_rg_layout lays out a single-sample run: 64-entry groups,
+// reference-relative 8-byte units, entry headers, block tables (per stream).  The host only copies the projected
+// bytes into place; KLM scans a sample's streams tile by tile on the device and KPM gathers a queued position's
+// columns from them in getAlleleCalls order (rank, then pending order).
+static int build_pop_rg_layout(Staged& s, LayoutArena& arena) {
     static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     auto t_last = std::chrono::steady_clock::now();
     auto lap = [&](const char* what) {
@@ -1717,243 +1712,198 @@ static int build_multi_layout(Staged& s) {
         std::fprintf(stderr, "[ngsep host]   population layout: %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
         t_last = t;
     };
-    const int64_t g_len = s.g_len, nreads = s.n_reads;
-    const int S = s.n_samples, S1 = S + 1;
+    const int64_t n = s.n_reads;
+    const int S = s.n_samples;
     const int32_t* R = s.h_reads.data();
     const uint8_t* const* rptr = s.h_rptr.data();      // each read's projected bytes over [gfirst, glast]
     const uint8_t* ref = s.h_ref.data();
-    const int32_t maxspan = s.max_span;
-    const int64_t PT = kPopTile;
-    // positions per chunk of work: the chunk's per-(sample, position) counters (~8 B each) stay cache-sized
-    static const int64_t c_env = diag_env("NGSEP_POP_CHUNK") ? std::atoll(diag_env("NGSEP_POP_CHUNK")) : 0;   // tuning
-    int64_t C = c_env > 0 ? c_env : ((int64_t)1 << 19) / S1;
-    C = std::max<int64_t>(256, std::min<int64_t>(8192, C)) / PT * PT;   // a multiple of PT (g_len is one of 1024)
-    const int64_t nchunk = (g_len + C - 1) / C, ntile = g_len / PT;
-    s.tile = (int32_t)PT;
-    s.h_prow.assign((size_t)ntile * S1, 0);
-    auto first_read = [&](int64_t c0) {         // first read that can overlap [c0, ..): gfirst > c0 - maxspan
-        int64_t lo = 0, hi = nreads;
-        while (lo < hi) {
-            const int64_t m = (lo + hi) / 2;
-            if ((int64_t)R[m * 4] <= c0 - maxspan) lo = m + 1; else hi = m;
-        }
-        return lo;
-    };
-    auto sample_of = [&](int64_t r) { const int sm = (R[r * 4 + 3] >> 8) - 1; return sm >= 0 && sm < S ? sm : S; };
-    // f(s1, first, last, bytes) for the reads overlapping [c0, c1), in read order
-    auto each_read = [&](int64_t c0, int64_t c1, auto&& f) {
-        for (int64_t r = first_read(c0); r < nreads && R[r * 4] < c1; r++) {
-            const int64_t gfirst = R[r * 4], glast = R[r * 4 + 1];
-            const int64_t a = std::max(gfirst, c0), b = std::min(glast, c1 - 1);
-            if (b < a) continue;
-            f(sample_of(r), a, b, rptr[r] + (a - gfirst));
-        }
-    };
-    struct Out { std::vector<int32_t> pos; std::vector<uint8_t> n; std::vector<uint8_t> bytes; };
-    std::vector<Out> outs((size_t)nchunk);
-    std::atomic<bool> overflow{false};
-    parallel_for(nchunk, 1, [&](int64_t k0, int64_t k1) {
-        std::vector<uint16_t> nz((size_t)S1 * C), nv((size_t)S * C);
-        std::vector<uint8_t> alt((size_t)S * C);
-        std::vector<uint32_t> cur((size_t)S * C);
-        std::vector<uint32_t> cand;
-        static_assert(kMaxSamplesDevice < 256, "candidate keys hold the sample in 8 bits");
-        for (int64_t k = k0; k < k1; k++) {
-            const int64_t c0 = k * C, c1 = std::min(g_len, c0 + C), len = c1 - c0;
-            std::fill(nz.begin(), nz.end(), 0);
-            std::fill(nv.begin(), nv.end(), 0);
-            std::fill(alt.begin(), alt.end(), 0);
-            cand.clear();
-            // calls per (sample, position); flag the positions with a valid call of another allele
-            each_read(c0, c1, [&](int s1, int64_t a, int64_t b, const uint8_t* src) {
-                uint16_t* z = &nz[(size_t)s1 * C];
-                if (s1 == S) {
-                    for (int64_t p = a; p <= b; p++)
-                        if (src[p - a]) {
-                            if (z[p - c0] == 65535) { overflow = true; continue; }
-                            z[p - c0]++;
-                        }
-                    return;
-                }
-                uint16_t* v = &nv[(size_t)s1 * C];
-                uint8_t* x = &alt[(size_t)s1 * C];
-                for (int64_t p = a; p <= b; p++) {
-                    const uint8_t cd = src[p - a];
-                    if (!cd) continue;
-                    if (z[p - c0] == 65535) { overflow = true; continue; }
-                    z[p - c0]++;
-                    if (!(cd & kCodeValid)) continue;
-                    v[p - c0]++;
-                    const uint8_t rc = ref[p];
-                    if ((rc & kRefCallable) && ((rc ^ cd) & 0x60) && !x[p - c0]) {
-                        x[p - c0] = 1;
-                        cand.push_back((uint32_t)(p - c0) << 8 | (uint32_t)s1);   // a candidate column (sparse)
-                    }
-                }
-            });
-            // KPM rows per (tile, sample)
-            for (int64_t t = c0 / PT; t < c1 / PT; t++)
-                for (int s1 = 0; s1 < S1; s1++) {
-                    const uint16_t* z = &nz[(size_t)s1 * C + (size_t)(t * PT - c0)];
-                    uint16_t mx = 0;
-                    for (int64_t p = 0; p < PT; p++) mx = std::max(mx, z[p]);
-                    s.h_prow[(size_t)t * S1 + s1] = mx;
-                }
-            // KTM columns, position-major then sample (the candidate list sorted; no dense scan of every column)
-            Out& o = outs[(size_t)k];
-            uint32_t nb = 0;
-            std::sort(cand.begin(), cand.end());
-            o.pos.reserve(cand.size());
-            o.n.reserve(cand.size());
-            for (uint32_t key : cand) {
-                const int64_t p = key >> 8;
-                const int sm = (int)(key & 255u);
-                const size_t i = (size_t)sm * C + (size_t)p;
-                o.pos.push_back((int32_t)(c0 + p));
-                const bool deep = nv[i] > kMcMaxCalls;
-                o.n.push_back(deep ? 255 : (uint8_t)nv[i]);
-                cur[i] = nb;
-                if (deep) alt[i] = 0;       // no bytes
-                else nb += nv[i];
-            }
-            (void)len;
-            o.bytes.resize(nb);
-            if (!nb) continue;
-            uint8_t* out = o.bytes.data();
-            each_read(c0, c1, [&](int s1, int64_t a, int64_t b, const uint8_t* src) {
-                if (s1 == S) return;
-                const uint8_t* x = &alt[(size_t)s1 * C];
-                uint32_t* cu = &cur[(size_t)s1 * C];
-                for (int64_t p = a; p <= b; p++) {
-                    if (!x[p - c0]) continue;
-                    const uint8_t cd = src[p - a];
-                    if (!(cd & kCodeValid)) continue;
-                    out[cu[p - c0]++] = (uint8_t)(((cd ^ ref[p]) & 0x60) | (cd & 0x1F));
-                }
-            });
+    // stream keys: sample * 128 + read-group rank; the reads of no sample: S * 128
+    const int64_t nkeys = (int64_t)(S + 1) * 128;
+    std::vector<uint16_t> key((size_t)n);
+    parallel_for(n, 1 << 16, [&](int64_t a, int64_t b) {
+        for (int64_t r = a; r < b; r++) {
+            const int sm = (R[r * 4 + 3] >> 8) - 1;
+            key[(size_t)r] = sm < 0 || sm >= S ? (uint16_t)(S * 128) : (uint16_t)(sm * 128 + ((R[r * 4 + 3] >> 1) & 127));
         }
     });
-    if (overflow) return -1;
-    lap("counts + candidate columns");
-    // KTM entries and bytes, concatenated in chunk order
-    std::vector<int64_t> eoff((size_t)nchunk + 1, 0), boff((size_t)nchunk + 1, 0);
-    for (int64_t k = 0; k < nchunk; k++) {
-        eoff[(size_t)k + 1] = eoff[(size_t)k] + (int64_t)outs[(size_t)k].pos.size();
-        boff[(size_t)k + 1] = boff[(size_t)k] + (int64_t)outs[(size_t)k].bytes.size();
-    }
-    const int64_t ne = eoff[(size_t)nchunk], nbytes = boff[(size_t)nchunk];
-    s.mc_entries = ne;
-    s.h_mc_pos.resize((size_t)ne);
-    s.h_mc_n.resize((size_t)ne);
-    s.h_pile.resize((size_t)nbytes);
-    parallel_for(nchunk, 4, [&](int64_t k0, int64_t k1) {
-        for (int64_t k = k0; k < k1; k++) {
-            Out& o = outs[(size_t)k];
-            if (!o.pos.empty()) {
-                std::memcpy(&s.h_mc_pos[(size_t)eoff[(size_t)k]], o.pos.data(), o.pos.size() * sizeof(int32_t));
-                std::memcpy(&s.h_mc_n[(size_t)eoff[(size_t)k]], o.n.data(), o.n.size());
-            }
-            if (!o.bytes.empty()) std::memcpy(&s.h_pile[(size_t)boff[(size_t)k]], o.bytes.data(), o.bytes.size());
-            o = Out();
+    // a stable counting sort by key: per-chunk histograms, (key, chunk) offsets, scatter
+    const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(64, n / 65536 + 1)), chl = (n + nch - 1) / nch;
+    std::vector<int64_t> hist((size_t)(nch * nkeys), 0);
+    parallel_for(nch, 1, [&](int64_t a, int64_t b) {
+        for (int64_t c = a; c < b; c++) {
+            int64_t* h = &hist[(size_t)(c * nkeys)];
+            for (int64_t r = c * chl; r < std::min(n, (c + 1) * chl); r++) h[key[(size_t)r]]++;
         }
     });
-    s.h_mc_gbase.assign((size_t)((ne + 63) / 64) + 1, 0);
-    int64_t off = 0;
-    for (int64_t i = 0; i < ne; i++) {
-        if ((i & 63) == 0) s.h_mc_gbase[(size_t)(i >> 6)] = off;
-        const uint8_t n = s.h_mc_n[(size_t)i];
-        off += n == 255 ? 0 : n;
+    std::vector<int64_t> kcount((size_t)nkeys, 0);
+    {
+        int64_t run = 0;
+        for (int64_t k = 0; k < nkeys; k++)
+            for (int64_t c = 0; c < nch; c++) {
+                int64_t& h = hist[(size_t)(c * nkeys + k)];
+                const int64_t v = h;
+                h = run;
+                run += v;
+                kcount[(size_t)k] += v;
+            }
     }
-    s.h_mc_gbase.back() = off;
-    s.pile_bytes = nbytes;
-    s.n_tiles = (ne + 63) / 64;         // KTM's groups of 64 columns
-    lap("column concatenation");
-    // KPM pile: block offsets, then the columns filled chunk by chunk in getAlleleCalls order
-    // site-major inside a tile: position p's columns of every sample are consecutive (sample order), so KPM's
-    // workgroup at p reads one contiguous run of stride_t bytes; pboff[t * S1 + s] = the tile's base + the earlier
-    // samples' rows, and stride_t = (pboff[(t + 1) * S1] - pboff[t * S1]) / PT
-    s.h_pboff.assign((size_t)ntile * S1 + 1, 0);
-    std::vector<int64_t> pstride((size_t)ntile, 0);
-    int64_t po = 0;
-    int32_t rmax = 0;
-    for (int64_t t = 0; t < ntile; t++) {
-        int64_t so = 0;
-        for (int s1 = 0; s1 < S1; s1++) {
-            const size_t i = (size_t)t * S1 + s1;
-            s.h_pboff[i] = po + so;
-            so += s.h_prow[i];
-            rmax = std::max<int32_t>(rmax, s.h_prow[i]);
+    std::vector<int32_t> ord((size_t)n);
+    parallel_for(nch, 1, [&](int64_t a, int64_t b) {
+        for (int64_t c = a; c < b; c++) {
+            int64_t* h = &hist[(size_t)(c * nkeys)];
+            for (int64_t r = c * chl; r < std::min(n, (c + 1) * chl); r++) ord[(size_t)h[key[(size_t)r]]++] = (int32_t)r;
         }
-        pstride[(size_t)t] = so;
-        po += so * PT;
+    });
+    std::vector<uint16_t>().swap(key);
+    std::vector<int64_t>().swap(hist);
+    // streams (non-empty keys in key order), their entries padded to whole groups
+    std::vector<int64_t> st_r0, st_n, st_e0;          // first read (in ord), reads, first entry
+    s.h_samp_st.assign((size_t)S + 2, 0);
+    int64_t r0 = 0, e0 = 0;
+    for (int64_t k = 0; k < nkeys; k++) {
+        const int sm = (int)(k / 128);
+        if (k % 128 == 0) s.h_samp_st[(size_t)sm] = (int32_t)st_n.size();
+        if (!kcount[(size_t)k]) continue;
+        st_r0.push_back(r0);
+        st_n.push_back(kcount[(size_t)k]);
+        st_e0.push_back(e0);
+        r0 += kcount[(size_t)k];
+        e0 += (kcount[(size_t)k] + 63) / 64 * 64;
     }
-    s.h_pboff.back() = po;
-    s.ppile_bytes = po;
-    s.tile_rows_max = rmax;
-    s.h_ppile.reset(new (std::nothrow) uint8_t[(size_t)po + 64]);
-    if (!s.h_ppile) return -2;
-    std::memset(s.h_ppile.get() + po, 0, 64);
-    uint8_t* pile = s.h_ppile.get();
-    parallel_for(nchunk, 1, [&](int64_t k0, int64_t k1) {
-        std::vector<uint16_t> cu((size_t)S1 * C);
-        std::vector<int64_t> rl;
-        std::vector<uint32_t> key;
-        std::vector<int32_t> cnt((size_t)S1 * 128 + 1);
-        std::vector<int64_t> sorted, tcnt, tfill, tlist;
-        for (int64_t k = k0; k < k1; k++) {
-            const int64_t c0 = k * C, c1 = std::min(g_len, c0 + C);
-            const int64_t t0 = c0 / PT, t1 = c1 / PT;
-            std::memset(pile + s.h_pboff[(size_t)t0 * S1], 0, (size_t)(s.h_pboff[(size_t)t1 * S1] - s.h_pboff[(size_t)t0 * S1]));
-            std::fill(cu.begin(), cu.end(), 0);
-            // the chunk's reads by (sample, read-group rank), pending order inside (a stable counting sort)
-            rl.clear();
-            key.clear();
-            for (int64_t r = first_read(c0); r < nreads && R[r * 4] < c1; r++) {
-                if (std::min<int64_t>(R[r * 4 + 1], c1 - 1) < std::max<int64_t>(R[r * 4], c0)) continue;
-                rl.push_back(r);
-                key.push_back((uint32_t)(sample_of(r) * 128 + ((R[r * 4 + 3] >> 1) & 127)));
-            }
-            std::fill(cnt.begin(), cnt.end(), 0);
-            for (uint32_t kk : key) cnt[kk + 1]++;
-            for (size_t i = 1; i < cnt.size(); i++) cnt[i] += cnt[i - 1];
-            sorted.resize(rl.size());
-            for (size_t i = 0; i < rl.size(); i++) sorted[(size_t)cnt[key[i]]++] = rl[i];
-            // tile by tile (a tile's site-major block is stride_t x PT bytes: cache-resident while it fills), each
-            // tile's reads in the sorted order
-            const int64_t nt = t1 - t0;
-            tcnt.assign((size_t)nt + 1, 0);
-            for (int64_t r : sorted) {
-                const int64_t a = std::max<int64_t>(R[r * 4], c0), b = std::min<int64_t>(R[r * 4 + 1], c1 - 1);
-                for (int64_t t = a / PT; t <= b / PT; t++) tcnt[(size_t)(t - t0) + 1]++;
-            }
-            for (int64_t t = 0; t < nt; t++) tcnt[(size_t)t + 1] += tcnt[(size_t)t];
-            tlist.resize((size_t)tcnt[(size_t)nt]);
-            tfill.assign(tcnt.begin(), tcnt.end() - 1);
-            for (int64_t r : sorted) {
-                const int64_t a = std::max<int64_t>(R[r * 4], c0), b = std::min<int64_t>(R[r * 4 + 1], c1 - 1);
-                for (int64_t t = a / PT; t <= b / PT; t++) tlist[(size_t)tfill[(size_t)(t - t0)]++] = r;
-            }
-            for (int64_t t = t0; t < t1; t++) {
-                const int64_t p0 = t * PT, p1 = p0 + PT - 1;
-                const int64_t stride = pstride[(size_t)t];
-                for (int64_t j = tcnt[(size_t)(t - t0)]; j < tcnt[(size_t)(t - t0) + 1]; j++) {
-                    const int64_t r = tlist[(size_t)j];
-                    const int s1 = sample_of(r);
-                    const int64_t gfirst = R[r * 4], glast = R[r * 4 + 1];
-                    const int64_t a = std::max(gfirst, p0), b = std::min(glast, p1);
-                    const uint8_t* src = rptr[r] + (a - gfirst);
-                    uint16_t* cc = &cu[(size_t)s1 * C];
-                    uint8_t* blk = pile + s.h_pboff[(size_t)t * S1 + s1];
-                    for (int64_t p = a; p <= b; p++) {
-                        const uint8_t cd = src[p - a];
-                        if (!cd) continue;
-                        blk[(p - p0) * stride + cc[p - c0]++] = cd;
-                    }
+    const int64_t nst = (int64_t)st_n.size();
+    s.h_samp_st[(size_t)S + 1] = (int32_t)nst;
+    s.n_streams = (int32_t)nst;
+    const int64_t ne = e0, ng = ne / 64;
+    s.n_entries = ne;
+    s.n_groups = ng;
+    s.h_st_end.resize((size_t)nst);
+    for (int64_t st = 0; st < nst; st++) s.h_st_end[(size_t)st] = st_e0[(size_t)st] + (st_n[(size_t)st] + 63) / 64 * 64;
+    // entry -> read (-1: padding) and the entry headers
+    std::vector<int32_t> ent((size_t)ne, -1);
+    s.h_rh.resize((size_t)ne * 2);
+    parallel_for(nst, 1, [&](int64_t a, int64_t b) {
+        for (int64_t st = a; st < b; st++) {
+            const int64_t m = st_n[(size_t)st], eb = st_e0[(size_t)st];
+            const int32_t last_first = R[(int64_t)ord[(size_t)(st_r0[(size_t)st] + m - 1)] * 4];
+            for (int64_t i = 0; i < (m + 63) / 64 * 64; i++) {
+                const int64_t e = eb + i;
+                if (i >= m) {
+                    s.h_rh[(size_t)(2 * e)] = last_first;
+                    s.h_rh[(size_t)(2 * e + 1)] = last_first - 1;
+                    continue;
                 }
+                const int64_t r = ord[(size_t)(st_r0[(size_t)st] + i)];
+                ent[(size_t)e] = (int32_t)r;
+                const int32_t gf = R[r * 4], gl = R[r * 4 + 1];
+                const bool empty = gl < gf;
+                s.h_rh[(size_t)(2 * e)] = gf;
+                s.h_rh[(size_t)(2 * e + 1)] = (int32_t)((uint32_t)(empty ? gf - 1 : gl) | ((R[r * 4 + 3] & 1) ? 0x80000000u : 0u));
             }
         }
     });
-    lap("population pile");
+    lap("streams");
+    // groups: units per read, unit offsets
+    s.h_grp.resize((size_t)ng);
+    int64_t base = 0;
+    for (int64_t g = 0; g < ng; g++) {
+        int32_t K = 0;
+        for (int64_t e = g * 64; e < g * 64 + 64; e++) {
+            const int32_t r = ent[(size_t)e];
+            if (r < 0) continue;
+            const int64_t span = (int64_t)R[(int64_t)r * 4 + 1] - R[(int64_t)r * 4] + 1;
+            if (span > 0) K = std::max<int32_t>(K, (int32_t)((span + 7) / 8));
+        }
+        s.h_grp[(size_t)g] = RGroup{base, K, 0};
+        base += (int64_t)K * 64;
+    }
+    s.n_units = base;
+    if (!arena.ensure_units(base + 8, true)) return -2;
+    s.h_units = arena.units;
+    s.units_pinned = arena.units_pinned;
+    uint64_t* units = s.h_units;
+    parallel_for(ng, 64, [&](int64_t g0, int64_t g1) {
+        for (int64_t g = g0; g < g1; g++) {
+            const RGroup G = s.h_grp[(size_t)g];
+            for (int l = 0; l < 64; l++) {
+                const int32_t r = ent[(size_t)(g * 64 + l)];
+                uint64_t* dst = units + G.base + l;
+                const int64_t gf = r < 0 ? 0 : R[(int64_t)r * 4];
+                const int64_t span = r < 0 ? 0 : std::max<int64_t>(0, (int64_t)R[(int64_t)r * 4 + 1] - gf + 1);
+                const uint8_t* src = r < 0 ? nullptr : rptr[r];
+                const uint8_t* rf = ref + gf;
+                const int64_t whole = span / 8;
+                for (int64_t k = 0; k < whole; k++) {
+                    uint64_t u, v;
+                    std::memcpy(&u, src + 8 * k, 8);
+                    std::memcpy(&v, rf + 8 * k, 8);
+                    dst[k * 64] = u ^ v;
+                }
+                int64_t k = whole;
+                if (span % 8) {
+                    uint8_t b8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                    for (int64_t t = 0; t < span % 8; t++) b8[t] = (uint8_t)(src[8 * k + t] ^ rf[8 * k + t]);
+                    uint64_t u;
+                    std::memcpy(&u, b8, 8);
+                    dst[k * 64] = u;
+                    k++;
+                }
+                for (; k < G.K; k++) dst[k * 64] = 0;
+            }
+        }
+    });
+    lap("units");
+    // block tables per stream, blocks of 2^pblk_shift positions (coarser when the tables would outgrow a quarter of
+    // the units)
+    int32_t shift = kRgBlockShift;
+    while (shift < 20 && ((s.g_len >> shift) + 2) * nst * 8 > std::max<int64_t>((int64_t)64 << 20, s.n_units * 2)) shift++;
+    s.pblk_shift = shift;
+    const int64_t nb = (s.g_len >> shift) + 2;
+    s.pnblk = nb;
+    s.h_blkA.assign((size_t)(nb * nst), 0);
+    s.h_blkB.assign((size_t)(nb * nst), 0);
+    const int64_t ms = s.max_span;
+    parallel_for(nst, 1, [&](int64_t a, int64_t b) {
+        for (int64_t st = a; st < b; st++) {
+            const int64_t m = st_n[(size_t)st], eb = st_e0[(size_t)st];
+            const int32_t* o = &ord[(size_t)st_r0[(size_t)st]];
+            int64_t ia = 0, ib = 0;
+            for (int64_t k = 0; k < nb; k++) {
+                const int64_t va = (k << shift) - ms + 1, vb = k << shift;
+                while (ia < m && (int64_t)R[(int64_t)o[ia] * 4] < va) ia++;
+                while (ib < m && (int64_t)R[(int64_t)o[ib] * 4] < vb) ib++;
+                s.h_blkA[(size_t)(st * nb + k)] = (int32_t)(eb + ia);
+                s.h_blkB[(size_t)(st * nb + k)] = (int32_t)(eb + ib);
+            }
+        }
+    });
+    // a bound on the reads of one sample covering one position (KPM gathers each sample's column into a slot of
+    // this many codes): per stream the most reads starting in max_span consecutive positions, summed over the
+    // sample's streams
+    std::vector<int32_t> sbound((size_t)nst, 0);
+    parallel_for(nst, 1, [&](int64_t a, int64_t b) {
+        for (int64_t st = a; st < b; st++) {
+            const int32_t* o = &ord[(size_t)st_r0[(size_t)st]];
+            const int64_t m = st_n[(size_t)st];
+            int32_t mc = 0;
+            for (int64_t i = 0, j = 0; i < m; i++) {
+                while ((int64_t)R[(int64_t)o[j] * 4] <= (int64_t)R[(int64_t)o[i] * 4] - ms) j++;
+                mc = std::max<int32_t>(mc, (int32_t)(i - j + 1));
+            }
+            sbound[(size_t)st] = mc;
+        }
+    });
+    int32_t stride = 0;
+    for (int sm = 0; sm <= S; sm++) {
+        int32_t b = 0;
+        for (int32_t st = s.h_samp_st[(size_t)sm]; st < s.h_samp_st[(size_t)sm + 1]; st++) b += sbound[(size_t)st];
+        stride = std::max(stride, b);
+    }
+    s.max_cov = (stride + 3) / 4 * 4;
+    s.prg = true;
+    s.tile = kKlmTile;
+    s.n_tiles = s.g_len / kKlmTile;
+    s.pile_bytes = s.n_units * 8;
+    lap("block tables");
     return 0;
 }
 
@@ -2110,29 +2060,18 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
             }
             s.known = true;
         }
-        const int lr = build_multi_layout(s);
-        if (const char* dump = diag_env("NGSEP_DUMP_POP_LAYOUT")) {   // diagnostics: a digest of the population layout
-            auto fnv = [](const void* p, size_t n) {
-                uint64_t h = 1469598103934665603ull;
-                for (size_t i = 0; i < n; i++) { h ^= static_cast<const uint8_t*>(p)[i]; h *= 1099511628211ull; }
-                return (unsigned long long)h;
-            };
-            if (std::FILE* f = std::fopen(dump, "w")) {
-                std::fprintf(f, "mc_pos %llu\nmc_n %llu\nmc_gbase %llu\npile %llu\nppile %llu\nprow %llu\npboff %llu\n",
-                             fnv(s.h_mc_pos.data(), s.h_mc_pos.size() * 4), fnv(s.h_mc_n.data(), s.h_mc_n.size()),
-                             fnv(s.h_mc_gbase.data(), s.h_mc_gbase.size() * 8), fnv(s.h_pile.data(), s.h_pile.size()),
-                             fnv(s.h_ppile.get(), (size_t)s.ppile_bytes), fnv(s.h_prow.data(), s.h_prow.size() * 2),
-                             fnv(s.h_pboff.data(), s.h_pboff.size() * 8));
-                std::fclose(f);
-            }
-        }
-        if (lr == -2) return set_error(c, NGSEP_E_DEVICE, "host memory for the population pile could not be allocated");
-        if (lr != 0) return set_error(c, NGSEP_E_UNSUPPORTED, "a sample's pileup is deeper than 65535 alignments");
-        c->stats.slot_bytes = s.ppile_bytes;
+        const int lr = build_pop_rg_layout(s, c->arena);
+        if (lr == -2) return set_error(c, NGSEP_E_DEVICE, "host memory for the population layout could not be allocated");
+        if (lr != 0) return set_error(c, NGSEP_E_INVALID, "internal error: population layout");
+        if ((int64_t)s.max_cov * (s.n_samples + 1) > kPopGatherCap)
+            return set_error(c, NGSEP_E_UNSUPPORTED, "a sample's pileup is deeper than the population kernel's columns hold (" +
+                             std::to_string(kPopGatherCap / (s.n_samples + 1)) + " alignments per sample at " +
+                             std::to_string(s.n_samples) + " samples)");
+        c->stats.slot_bytes = 0;
         c->stats.slot_size = 0;                  // (no fixed-size slots: the site-major pile is sized per tile)
     }
     c->stats.read_bases = nbases;
-    c->stats.pile_bytes = s.rg ? s.n_units * 8 : s.pile_bytes;
+    c->stats.pile_bytes = s.rg || s.prg ? s.n_units * 8 : s.pile_bytes;
     c->stats.tile_positions = s.tile;
     c->stats.tile_rows_max = s.tile_rows_max;
     const auto h1 = std::chrono::steady_clock::now();
@@ -2165,9 +2104,8 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
     std::vector<int32_t>().swap(s.h_blkA);
     std::vector<int32_t>().swap(s.h_blkB);
     s.h_units = nullptr;
-    std::vector<int32_t>().swap(s.h_mc_pos);
-    std::vector<uint8_t>().swap(s.h_mc_n);
-    std::vector<int64_t>().swap(s.h_mc_gbase);
+    std::vector<int32_t>().swap(s.h_samp_st);
+    std::vector<int64_t>().swap(s.h_st_end);
     s.h_ppile.reset();
     std::vector<uint16_t>().swap(s.h_prow);
     std::vector<int64_t>().swap(s.h_pboff);
@@ -2232,7 +2170,7 @@ static void run_window_job(ngsep_ctx* c, WindowJob* j) {
     }
     const auto h2 = std::chrono::steady_clock::now();
     c->stats.read_bases += nb;
-    c->stats.pile_bytes = s.rg ? s.n_units * 8 : s.pile_bytes;
+    c->stats.pile_bytes = s.rg || s.prg ? s.n_units * 8 : s.pile_bytes;
     c->stats.tile_positions = s.tile;
     c->stats.tile_rows_max = std::max(c->stats.tile_rows_max, s.tile_rows_max);
     c->stats.global_positions += s.g_len;

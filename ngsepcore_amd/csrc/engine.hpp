@@ -77,6 +77,15 @@ static_assert(sizeof(RGroup) == 16, "RGroup layout");
 constexpr int kRgBlockShift = 8;           // entry index tables per 256 positions (blkA / blkB)
 constexpr int kKlTile = 2048;              // positions per KL tile (one workgroup each; divides kRunAlign)
 constexpr int kMcMaxCalls = 254;           // multisample candidate column: valid calls the bounds take (sums fit 32 bits)
+#ifndef NGSEP_KLM_TILE                     // (build-time overrides: A/B builds only, tools/gpu_r4_klm.sh)
+#define NGSEP_KLM_TILE 2048
+#endif
+#ifndef NGSEP_KLM_SLOTS
+#define NGSEP_KLM_SLOTS 96
+#endif
+constexpr int kKlmTile = NGSEP_KLM_TILE;   // positions per KLM sample tile (one wavefront each; divides kRunAlign)
+constexpr int kKlmSlots = NGSEP_KLM_SLOTS; // KLM: candidate columns a sample tile bounds in LDS (more: kept open)
+constexpr int kPopGatherCap = 61440;       // KPM (gather): LDS bytes for one position's columns ((S + 1) x the per-sample bound)
 
 // the (first) alternative allele of a record as a DNA index: a pool record keeps its variant's alleles in
 // the mask bits (ngsep_site_out.pool), an SNVQ record in .alt
@@ -565,18 +574,11 @@ struct Staged {            // everything resident for one run
     std::vector<int32_t> h_reads;       // 4 ints per read: gfirst, glast, slot, flags
                                         //   flags: bit0 negative strand, bits 1-7 read-group rank,
                                         //   bits 8-23 sample + 1 (0: no sample) -- multisample only
-    // multisample (engine.cpp build_columns_multi): the (sample, position) columns holding a valid call of
-    // another allele -- global position, number of valid calls (255: deeper than kMcMaxCalls, no bytes),
-    // their bytes in h_pile, the byte offset of every 64th entry's column
     int32_t n_samples = 0;
-    int64_t mc_entries = 0;
-    std::vector<int32_t> h_mc_pos;
-    std::vector<uint8_t> h_mc_n;
-    std::vector<int64_t> h_mc_gbase;
-    // multisample: KPM's pile -- per (tile of kPopTile positions, sample + the reads of no sample) block of
-    // per tile of kPopTile positions, site-major: position p's columns of samples 0 .. S (the reads of no sample
-    // last) back to back, each rows(t, s) code bytes in getAlleleCalls order -- column (p, s) at pboff[t * (S + 1) + s]
-    // + (p % kPopTile) * stride_t, stride_t = the tile's rows summed over its samples
+    // the realigner's region positions (engine.cpp run_population_regions): KPM's site-major pile -- per tile of
+    // kPopTile positions, position p's columns of samples 0 .. S (the reads of no sample last) back to back, each
+    // rows(t, s) code bytes in getAlleleCalls order -- column (p, s) at pboff[t * (S + 1) + s] + (p % kPopTile) *
+    // stride_t, stride_t = the tile's rows summed over its samples
     std::unique_ptr<uint8_t[]> h_ppile;
     std::vector<uint16_t> h_prow;       // rows per (tile, sample): h_prow[t * (S + 1) + s]
     std::vector<int64_t> h_pboff;       // block offsets, same index (+ the total at the end)
@@ -610,6 +612,17 @@ struct Staged {            // everything resident for one run
     // the realigner's regions (realign.hpp): their queue entries carry their columns (rows >= 0), uploaded
     // here (u16 entries, h_forced_ctr[5] = their size / 4)
     std::vector<uint16_t> h_cols;
+    // population read-group layout (engine.cpp build_pop_rg_layout; MultisampleVariantsDetector's device input):
+    // the read-group layout above with one stream of entries per (sample, read-group rank), in (sample, rank)
+    // order, the reads of no sample last; each stream's entries in pending-list order, padded to whole groups.
+    // Block tables per stream: h_blkA / h_blkB[st * pnblk + b] over blocks of 2^pblk_shift positions (global entry
+    // indexes); h_samp_st[s] .. h_samp_st[s + 1] = the streams of sample s (s = S: the reads of no sample);
+    // h_st_end[st] = one past the stream's last entry (its padding included)
+    bool prg = false;
+    int32_t n_streams = 0, pblk_shift = kRgBlockShift, max_cov = 0;
+    int64_t pnblk = 0;
+    std::vector<int32_t> h_samp_st;
+    std::vector<int64_t> h_st_end;
 };
 
 // Pinned host buffers of the single-sample layout, reused run after run (streamed windows: no page faults,

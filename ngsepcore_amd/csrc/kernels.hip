@@ -15,7 +15,7 @@
 //        VariantDiscoverySNVQAlgorithm.java:100-243, SingleSampleVariantPileupListener.java:213-232);
 //        records go to position buckets.
 //   KO  ko_fused : position order of the records (rank per bucket) and their (sequence, position).
-//   KTM / KQN / KPM k_scan_multi / k_queue_need / k_posterior_multi : MultisampleVariantsDetector.
+//   KLM / KQN / KPM k_scan_pop / k_queue_need / k_posterior_multi : MultisampleVariantsDetector.
 //   KR  k_rac : RelativeAlleleCountsCalculator over the tile-blocked byte pile (engine.cpp build_single_layout).
 //
 // HBM-bound integer/byte work: no MFMA.  Layout and roofline: DESIGN.md.
@@ -151,11 +151,13 @@ struct Device {
     size_t cap_units = 0, cap_rh = 0, cap_grp = 0, cap_blk = 0, cap_blkB = 0;
     int64_t n_entries = 0;
     bool rg = false;
-    int32_t* d_mc_pos = nullptr;     // multisample: candidate columns' global positions (KTM)
-    uint8_t* d_mc_n = nullptr;       //   their valid-call counts
-    int64_t* d_mc_gbase = nullptr;   //   byte offset of every 64th column
+    // multisample: the population read-group layout (the units / headers / groups above, engine.hpp Staged::prg)
+    bool prg = false;
+    int32_t* d_samp_st = nullptr;    //   streams of each sample
+    int64_t* d_st_end = nullptr;     //   one past each stream's last entry
+    int32_t n_streams = 0, pblk_shift = kRgBlockShift, pop_stride = 0;
+    int64_t pnblk = 0;
     uint32_t* d_need = nullptr;      //   open positions, a bit per global position
-    int64_t mc_entries = 0;
     ngsep_popsite_out* h_psites = nullptr;      // multisample: pinned staging of the emitted sites and calls
     ngsep_sample_call* h_pcalls = nullptr;
     int64_t cap_h_psites = 0, cap_h_pcalls = 0;
@@ -1335,138 +1337,6 @@ __global__ __launch_bounds__(256) void k_queue_all(const uint8_t* __restrict__ r
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// KTM: multisample scan over the candidate columns -- one wavefront per 64 columns
-// ------------------------------------------------------------------------------------------
-// A column is one sample's valid calls at one position that holds a valid call of another allele than the
-// reference (engine.cpp build_columns_multi); every other (sample, position) is hom-ref by §5.  The lane
-// adds its column's calls into the exact integer bound and keeps the position open unless the bound proves
-// the sample hom-ref: such a sample cannot make a decided non-reference call
-// (SingleSampleVariantPileupListener.genotypeVariantSample, :361-391, evaluates the same posterior), and a
-// position where every sample is proven hom-ref gets variant QS 0, which MultisampleVariantsDetector.onPileup
-// never writes (:534).  Open positions are ORed into a bit per global position; KQN queues them for KPM.
-// The 64 columns of a group are consecutive bytes, so the wave's dword loads are coalesced.
-constexpr int kKtmWords = 8;                   // KTM: column dwords per lane staged in LDS (a 2 KB group)
-__device__ __forceinline__ int64_t ktm_uniform(int64_t v) {
-    return ((int64_t)__builtin_amdgcn_readfirstlane((int32_t)(v >> 32)) << 32) |
-           (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)v);
-}
-__global__ __launch_bounds__(256)
-void k_scan_multi(const int32_t* __restrict__ mc_pos, const uint8_t* __restrict__ mc_n, const int64_t* __restrict__ mc_gbase,
-                  const uint8_t* __restrict__ cols, int64_t n_entries, const LikTables* __restrict__ tabs, GenotypeParams gp,
-                  uint32_t* __restrict__ need, unsigned long long* __restrict__ counters) {
-    __shared__ unsigned long long w[2][32];
-    __shared__ unsigned long long s_ne[4];
-    __shared__ uint32_t s_col[4][64 * kKtmWords];
-    __shared__ unsigned long long s_acc[4][64 * 4];   // per lane: its column's {ref, alt 1, alt 2, alt 3} sums
-    const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
-    if (threadIdx.x < 64) w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
-    __syncthreads();
-    const bool bound_on = gp.use_bound != 0;
-    const long long th = tabs->t_het, to = tabs->t_homo;
-    const int32_t maxq = gp.max_q;
-    const uint32_t* cw = reinterpret_cast<const uint32_t*>(cols);
-    const int64_t ngroups = (n_entries + 63) >> 6;
-    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-    uint32_t* buf = s_col[wv];
-    unsigned long long nexact = 0;
-    // A group's columns are the bytes [gbase[g], gbase[g + 1]): the wave loads them whole (coalesced, one round
-    // trip) into LDS, and the next group's metadata and bytes are in flight while this one is bounded; the group
-    // after that has its byte range (gbase) in flight too.  A group larger than the staging buffer is read from
-    // global memory column by column.
-    int64_t grp = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
-    grp = ktm_uniform(grp);
-    auto ld_gb = [&](int64_t g, int64_t& g0, int64_t& g1) {
-        if (g < ngroups) { g0 = ktm_uniform(mc_gbase[g]); g1 = ktm_uniform(mc_gbase[g + 1]); } else { g0 = g1 = 0; }
-    };
-    int32_t c_pos = 0, n_pos = 0;
-    uint32_t c_n = 0, n_n = 0;
-    uint32_t c_w[kKtmWords], n_w[kKtmWords];
-    int64_t c_g0, c_g1, n_g0, n_g1, f_g0, f_g1;
-    auto ld_group = [&](int64_t g, int64_t g0, int64_t g1, int32_t& pos, uint32_t& n, uint32_t* wds) {
-        const int64_t i = (g << 6) + lane;
-        const bool has = g < ngroups && i < n_entries;
-        pos = has ? mc_pos[i] : 0;
-        n = has ? (uint32_t)mc_n[i] : 0u;
-        const int64_t d0 = g0 >> 2, nd = ((g1 + 3) >> 2) - d0;
-        const bool fits = nd <= 64 * kKtmWords;
-#pragma unroll
-        for (int k = 0; k < kKtmWords; k++) wds[k] = fits && lane + 64 * k < nd ? cw[d0 + lane + 64 * k] : 0u;
-    };
-    ld_gb(grp, c_g0, c_g1);
-    ld_group(grp, c_g0, c_g1, c_pos, c_n, c_w);
-    ld_gb(grp + nwaves, n_g0, n_g1);
-    for (; grp < ngroups; grp += nwaves) {
-        // in flight: the next group's columns, the byte range of the one after
-        ld_group(grp + nwaves, n_g0, n_g1, n_pos, n_n, n_w);
-        ld_gb(grp + 2 * nwaves, f_g0, f_g1);
-        const int64_t i = (grp << 6) + lane;
-        const bool has = i < n_entries;
-        const uint32_t n = c_n;
-        const uint32_t nb = n == 255u ? 0u : n;
-        uint32_t incl = nb;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t v = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += v;
-        }
-        const int64_t d0 = c_g0 >> 2, nd = ((c_g1 + 3) >> 2) - d0;
-        const bool fits = nd <= 64 * kKtmWords;
-        if (fits) {
-#pragma unroll
-            for (int k = 0; k < kKtmWords; k++) buf[lane + 64 * k] = c_w[k];
-        }
-        __builtin_amdgcn_wave_barrier();
-        const int64_t start = c_g0 + (int64_t)(incl - nb), end = start + nb;
-        bool keep = has;
-        if (ABLATE(gp.ablate, 32768)) keep = false;               // diagnostics: metadata and staging only
-        if (has && bound_on && n != 255u && !ABLATE(gp.ablate, 32768)) {
-            // each byte's weight goes to its allele's sum with one LDS add (a lane's own four slots): no per-byte
-            // selects over four 64-bit registers
-            unsigned long long* acc = &s_acc[wv][lane * 4];
-            acc[0] = 0ull; acc[1] = 0ull; acc[2] = 0ull; acc[3] = 0ull;
-            for (int64_t d = start >> 2; d < (end + 3) >> 2; d++) {
-                const uint32_t word = fits ? buf[d - d0] : cw[d];
-#pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    const int64_t at = d * 4 + b;
-                    if (at < start || at >= end) continue;
-                    const uint32_t cd = (word >> (8 * b)) & 0xFFu;
-                    const uint32_t al = (cd >> 5) & 3u;
-                    int q = (int)(cd & 31u);
-                    q = q > maxq ? maxq : q;
-                    atomicAdd(&acc[al], w[al == 0 ? 0 : 1][q]);
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            const unsigned long long a0 = acc[0], a1 = acc[1], a2 = acc[2], a3 = acc[3];
-            const long long R1 = (long long)(a0 & 0xFFFFFFFFull), R2 = (long long)(a0 >> 32);
-            const long long x1 = (long long)(a1 & 0xFFFFFFFFull), y1 = (long long)(a2 & 0xFFFFFFFFull);
-            const long long z1 = (long long)(a3 & 0xFFFFFFFFull);
-            const long long x2 = (long long)(a1 >> 32), y2 = (long long)(a2 >> 32), z2 = (long long)(a3 >> 32);
-            const bool drop = (R1 - x1 > th) && (R1 - y1 > th) && (R1 - z1 > th) &&
-                              (R2 - x2 > to) && (R2 - y2 > to) && (R2 - z2 > to) &&
-                              (R2 - x1 - y1 > th) && (R2 - x1 - z1 > th) && (R2 - y1 - z1 > th);
-            keep = !drop;
-            nexact++;
-        }
-        if (keep) atomicOr(&need[c_pos >> 5], 1u << (c_pos & 31));
-        __builtin_amdgcn_wave_barrier();
-        c_pos = n_pos; c_n = n_n; c_g0 = n_g0; c_g1 = n_g1;
-        n_g0 = f_g0; n_g1 = f_g1;
-#pragma unroll
-        for (int k = 0; k < kKtmWords; k++) c_w[k] = n_w[k];
-    }
-    for (int sft = 1; sft < 64; sft <<= 1) nexact += __shfl_xor(nexact, sft, 64);
-    if (lane == 0) s_ne[wv] = nexact;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long ne = 0;
-        for (int k = 0; k < (int)(blockDim.x >> 6); k++) ne += s_ne[k];
-        if (ne) atomicAdd(&counters[3], ne);
-    }
-}
-
 // KQN: the open positions (a bit per global position) into the KPM queue, {position, reference code}
 __global__ __launch_bounds__(256) void k_queue_need(const uint32_t* __restrict__ need, const uint8_t* __restrict__ ref, int64_t nwords,
                                                     QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap) {
@@ -1494,6 +1364,255 @@ __global__ __launch_bounds__(256) void k_queue_need(const uint32_t* __restrict__
             if (at < qcap) queue[at] = QueueSite{(int32_t)g, (int32_t)ref[g]};
             at++;
         }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// KLM: the multisample scan over the population read-group layout -- one wavefront per (sample, tile of kKlmTile
+//      positions), four samples per workgroup
+// ------------------------------------------------------------------------------------------
+// A sample without a valid call of another allele than the reference at a position cannot make a decided
+// non-reference call there, and one whose valid calls the exact integer bound (§5) proves hom-ref cannot either
+// (SingleSampleVariantPileupListener.genotypeVariantSample, :361-391); a position where every sample is so proven
+// gets variant QS 0, which MultisampleVariantsDetector.onPileup never writes (:534).  Per sample tile:
+//   pass 1: the wave streams the sample's units over the tile (its read-group streams in turn; lane = read, as KL)
+//           and marks the positions holding a valid call of another allele (SWAR, kl_nonref) in an LDS bitmap;
+//   slots:  the marked positions (a few % of the sample's columns) get LDS slots in position order;
+//   pass 2: every lane adds the weights of its read's valid calls at the marked positions it covers (one 8-byte
+//           reload each: the units were just streamed) into its slot's {ref, alt 1, alt 2, alt 3} sums;
+//   pass 3: a slot the bound cannot prove hom-ref -- or holding more than kMcMaxCalls valid calls, or past
+//           kKlmSlots -- keeps its position open: one bit per global position (atomicOr); KQN queues them for KPM.
+// The reads of no sample only enter the pooled counts: not scanned.  No block barrier after the tables: every
+// wave's state is its own.
+constexpr int kKlmThreads = 256;
+constexpr int kKlmWords = kKlmTile / 32 + 2;   // tile bitmap words, a 32-position margin on either side
+constexpr int kKlmUnroll = 8;                   // pass 1: unit loads in flight per lane
+#ifndef NGSEP_KLM_PEND
+#define NGSEP_KLM_PEND 2
+#endif
+constexpr int kKlmPend = NGSEP_KLM_PEND;        // pass 2: marked-position loads issued together per lane
+#ifndef NGSEP_KLM_WPE
+#define NGSEP_KLM_WPE 1
+#endif
+constexpr int kKlmWpl = kKlmTile / 2048;      // bitmap words per lane in the slot scan
+static_assert(kKlmWpl >= 1 && kKlmWpl <= 4 && kKlmTile % 2048 == 0 && kRunAlign % kKlmTile == 0, "KLM tile");
+
+__device__ __forceinline__ uint32_t nib4_byte7(uint32_t w) {   // bit 7 of the four bytes -> 4 bits
+    return ((w >> 7) & 1u) | ((w >> 14) & 2u) | ((w >> 21) & 4u) | ((w >> 28) & 8u);
+}
+
+__global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(NGSEP_KLM_WPE))) void k_scan_pop(
+    const uint64_t* __restrict__ units, const int2* __restrict__ rh, const RGroup* __restrict__ grp,
+    const int32_t* __restrict__ samp_st, const int32_t* __restrict__ blkA, const int32_t* __restrict__ blkB,
+    int64_t nblk, int32_t shift, int32_t n_samples, const uint8_t* __restrict__ ref, const LikTables* __restrict__ tabs,
+    GenotypeParams gp, uint32_t* __restrict__ need, unsigned long long* __restrict__ counters) {
+    __shared__ unsigned long long w[2][32];
+    __shared__ alignas(16) uint8_t s_ref[kKlmTile];         // the tile's reference codes
+    __shared__ uint32_t s_bm[4][kKlmWords];
+    __shared__ uint16_t s_wb[4][kKlmWords];            // slot of each bitmap word's first marked position
+    __shared__ unsigned long long s_acc[4][kKlmSlots * 4];
+    __shared__ uint32_t s_n[4][kKlmSlots];
+    __shared__ uint16_t s_pos[4][kKlmSlots];           // tile index of each slot
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x < 64) w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
+    const int nsg = (n_samples + 3) >> 2;
+    const int64_t tile = (int64_t)blockIdx.x / nsg;
+    for (int i = threadIdx.x; i < kKlmTile / 16; i += kKlmThreads)
+        reinterpret_cast<uint4*>(s_ref)[i] = reinterpret_cast<const uint4*>(ref + tile * kKlmTile)[i];
+    __syncthreads();
+    const int s = (int)(blockIdx.x % nsg) * 4 + wv;
+    if (s >= n_samples) return;
+    const int32_t tstart = (int32_t)(tile * kKlmTile), tlast = tstart + kKlmTile - 1;
+    uint32_t* bm = s_bm[wv];
+    for (int i = lane; i < kKlmWords; i += 64) bm[i] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int st0 = samp_st[s], st1 = samp_st[s + 1];
+    // ---- pass 1: mark the positions with a valid call of another allele
+    for (int st = st0; st < st1; st++) {
+        const int64_t e_lo = blkA[(int64_t)st * nblk + (tstart >> shift)];
+        const int64_t e_hi = blkB[(int64_t)st * nblk + (tlast >> shift) + 1];
+        const int64_t g_hi = (e_hi + 63) >> 6;
+        int64_t g = e_lo >> 6;
+        int2 h = g < g_hi ? rh[g * 64 + lane] : make_int2(0, -1);
+        int64_t gbase = g < g_hi ? grp[g].base : 0;
+        for (; g < g_hi; g++) {
+            const int64_t e = g * 64 + lane;
+            // the next group's header and base in flight
+            const int2 hn = g + 1 < g_hi ? rh[e + 64] : make_int2(0, -1);
+            const int64_t gbn = g + 1 < g_hi ? grp[g + 1].base : 0;
+            const int32_t gf = h.x, gl = h.y & 0x7FFFFFFF;
+            const int32_t a = max(gf, tstart), b = min(gl, tlast);
+            const bool act = e >= e_lo && e < e_hi && a <= b;
+            const int32_t k0 = act ? (a - gf) >> 3 : 0, kn = act ? ((b - gf) >> 3) - k0 : -1;
+            const uint64_t* ub = units + gbase + lane + (int64_t)k0 * 64;
+            const int32_t ti0 = gf + 8 * k0 - tstart + 32;   // bitmap index of unit k0's byte 0 (>= 25)
+            for (int32_t j = 0; j <= kn; j += kKlmUnroll) {
+                uint64_t u[kKlmUnroll];
+#pragma unroll
+                for (int i = 0; i < kKlmUnroll; i++) u[i] = ub[(int64_t)min(j + i, kn) * 64];
+#pragma unroll
+                for (int i = 0; i < kKlmUnroll; i++) {
+                    if (j + i > kn) continue;
+                    const uint32_t nlo = kl_nonref((uint32_t)u[i]), nhi = kl_nonref((uint32_t)(u[i] >> 32));
+                    if (!(nlo | nhi)) continue;
+                    uint32_t m = nib4_byte7(nlo) | nib4_byte7(nhi) << 4;
+                    const int32_t ti = ti0 + 8 * (j + i);
+                    // at callable positions only (a counted code reads as another allele against a non-callable one)
+                    for (uint32_t x = m; x; x &= x - 1u) {
+                        const int k = __builtin_ctz(x);
+                        const int32_t tp = ti - 32 + k;
+                        if (tp >= 0 && tp < kKlmTile && !(s_ref[tp] & 0x80u)) m &= ~(1u << k);
+                    }
+                    if (!m) continue;
+                    const uint64_t v = (uint64_t)m << (ti & 31);
+                    atomicOr(&bm[ti >> 5], (uint32_t)v);
+                    if (v >> 32) atomicOr(&bm[(ti >> 5) + 1], (uint32_t)(v >> 32));
+                }
+            }
+            h = hn;
+            gbase = gbn;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- slots: the tile's marked positions in order (lane: bitmap words 1 + kKlmWpl lane ..)
+    uint16_t* wb = s_wb[wv];
+    uint16_t* spos = s_pos[wv];
+    unsigned long long* acc = s_acc[wv];
+    uint32_t* sn = s_n[wv];
+    uint32_t bw[kKlmWpl], cw[kKlmWpl];
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < kKlmWpl; k++) {
+        bw[k] = bm[1 + kKlmWpl * lane + k];
+        cw[k] = c;
+        c += (uint32_t)__popc(bw[k]);
+    }
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
+    const uint32_t nslot = __shfl(incl, 63, 64);
+    if (nslot == 0) return;
+    const uint32_t ex = incl - c;
+#pragma unroll
+    for (int k = 0; k < kKlmWpl; k++) wb[1 + kKlmWpl * lane + k] = (uint16_t)min(ex + cw[k], 65535u);
+    const uint32_t nkeep = min(nslot, (uint32_t)kKlmSlots);
+    for (uint32_t i = lane; i < nkeep; i += 64) {
+        acc[4 * i] = 0ull; acc[4 * i + 1] = 0ull; acc[4 * i + 2] = 0ull; acc[4 * i + 3] = 0ull;
+        sn[i] = 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kKlmWpl; k++) {
+        uint32_t word = bw[k];
+        uint32_t sl = ex + cw[k];
+        const int32_t ti_base = 32 * (kKlmWpl * lane + k);   // tile index of the word's bit 0
+        while (word) {
+            const int bit = __builtin_ctz(word);
+            word &= word - 1u;
+            const int32_t ti = ti_base + bit;
+            if (sl < (uint32_t)kKlmSlots) spos[sl] = (uint16_t)ti;
+            else {                                        // past the slots: kept open
+                const int32_t gpos = tstart + ti;
+                atomicOr(&need[gpos >> 5], 1u << (gpos & 31));
+            }
+            sl++;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- pass 2: each lane's valid calls at the marked positions its read covers, into the slots' sums (one
+    //      8-byte unit load per marked position, a group's loads issued together)
+    const int32_t maxq = gp.max_q;
+#ifdef NGSEP_KLM_NOPASS2
+    if (st1 < 0)                                       // (A/B builds: pass 1 alone; results not valid)
+#endif
+    for (int st = st0; st < st1; st++) {
+        const int64_t e_lo = blkA[(int64_t)st * nblk + (tstart >> shift)];
+        const int64_t e_hi = blkB[(int64_t)st * nblk + (tlast >> shift) + 1];
+        for (int64_t g = e_lo >> 6; g < (e_hi + 63) >> 6; g++) {
+            const int64_t e = g * 64 + lane;
+            const int2 h = rh[e];
+            const int32_t gf = h.x, gl = h.y & 0x7FFFFFFF;
+            const int32_t a = max(gf, tstart), b = min(gl, tlast);
+            if (!(e >= e_lo && e < e_hi && a <= b)) continue;
+            const uint64_t* ub = units + grp[g].base + lane;
+            const int32_t A = a - tstart + 32, B = b - tstart + 32;
+            int32_t pend_o[kKlmPend];
+            uint32_t pend_s[kKlmPend];
+#pragma unroll
+            for (int i = 0; i < kKlmPend; i++) { pend_o[i] = 0; pend_s[i] = 0; }
+            int np = 0;
+            auto flush = [&]() {
+                uint64_t u[kKlmPend];
+#pragma unroll
+                for (int i = 0; i < kKlmPend; i++) u[i] = i < np ? ub[(int64_t)(pend_o[i] >> 3) * 64] : 0ull;
+#pragma unroll
+                for (int i = 0; i < kKlmPend; i++) {
+                    if (i >= np) continue;
+                    const uint32_t y = (uint32_t)(u[i] >> (8 * (pend_o[i] & 7))) & 0xFFu;
+                    if (y & 0x80u) continue;                  // not a valid call (the position is callable)
+                    const uint32_t al = (y >> 5) & 3u;
+                    int q = (int)(y & 31u);
+                    q = q > maxq ? maxq : q;
+                    atomicAdd(&acc[4 * pend_s[i] + al], w[al == 0 ? 0 : 1][q]);
+                    atomicAdd(&sn[pend_s[i]], 1u);
+                }
+                np = 0;
+            };
+            for (int32_t wi = A >> 5; wi <= (B >> 5); wi++) {
+                uint32_t word = bm[wi];
+                if (wi == (A >> 5)) word &= ~0u << (A & 31);
+                if (wi == (B >> 5) && (B & 31) != 31) word &= (1u << ((B & 31) + 1)) - 1u;
+                if (!word) continue;
+                const uint32_t full = bm[wi];
+                const uint32_t sbase = wb[wi];
+                while (word) {
+                    const int bit = __builtin_ctz(word);
+                    word &= word - 1u;
+                    const uint32_t sl = sbase + (uint32_t)__popc(full & ((1u << bit) - 1u));
+                    if (sl >= (uint32_t)kKlmSlots) continue;
+#pragma unroll
+                    for (int i = 0; i < kKlmPend; i++)          // (static indexes: registers, not scratch)
+                        if (i == np) { pend_o[i] = wi * 32 + bit - 32 + tstart - gf; pend_s[i] = sl; }   // byte offset in the read
+                    np++;
+                    if (np == kKlmPend) flush();
+                }
+            }
+            if (np) flush();
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- pass 3: the bound per slot
+    const bool bound_on = gp.use_bound != 0;
+    const long long th = tabs->t_het, to = tabs->t_homo;
+    for (uint32_t i = lane; i < nkeep; i += 64) {
+        const unsigned long long a0 = acc[4 * i], a1 = acc[4 * i + 1], a2 = acc[4 * i + 2], a3 = acc[4 * i + 3];
+        const long long R1 = (long long)(a0 & 0xFFFFFFFFull), R2 = (long long)(a0 >> 32);
+        const long long x1 = (long long)(a1 & 0xFFFFFFFFull), y1 = (long long)(a2 & 0xFFFFFFFFull);
+        const long long z1 = (long long)(a3 & 0xFFFFFFFFull);
+        const long long x2 = (long long)(a1 >> 32), y2 = (long long)(a2 >> 32), z2 = (long long)(a3 >> 32);
+        const bool drop = (R1 - x1 > th) && (R1 - y1 > th) && (R1 - z1 > th) &&
+                          (R2 - x2 > to) && (R2 - y2 > to) && (R2 - z2 > to) &&
+                          (R2 - x1 - y1 > th) && (R2 - x1 - z1 > th) && (R2 - y1 - z1 > th);
+        if (!bound_on || sn[i] > (uint32_t)kMcMaxCalls || !drop) {
+            const int32_t gpos = tstart + spos[i];
+            atomicOr(&need[gpos >> 5], 1u << (gpos & 31));
+        }
+    }
+    // candidate columns and bounded columns, on the shard counters (one add per wave)
+    if (lane == 0) {
+        unsigned long long* sc = counters + kCtrShard0 + kCtrShardStride * (int)(blockIdx.x % kKlShards);
+        atomicAdd(&sc[0], (unsigned long long)nslot);
+        atomicAdd(&sc[1], (unsigned long long)nkeep);
     }
 }
 
@@ -1670,12 +1789,71 @@ __device__ PopCall genotype_sample_d(const double* L, const int* cnt, int total,
     return c;
 }
 
-// POOL: ploidy >= 3 (the pool branch's report arrays would otherwise cost every run registers and scratch)
-template <bool POOL, int WPE>
+// KPM's gather from the population read-group layout (engine.hpp Staged::prg): PileupRecord.getAlleleCalls(1,
+// readGroups) of sample s at global position p -- the nonzero codes of the reads covering p, stream (read-group rank)
+// after stream, pending order inside -- into dst (at most cap codes; the host sizes cap by the sample's coverage
+// bound).  Entries are walked from the stream's block-table entry eight headers at a time (their two possible
+// groups' bases loaded alongside), the covering ones' unit loads issued together.
+struct PopGather {
+    const uint64_t* units;
+    const int2* rh;
+    const RGroup* grp;
+    const int32_t* samp_st;     // streams of sample s: [samp_st[s], samp_st[s + 1]) (s = S: the reads of no sample)
+    const int64_t* st_end;      // one past each stream's last entry
+    const int32_t* blkA;        // [stream * nblk + (p >> shift)]: the stream's first entry that can cover p
+    const uint8_t* ref;
+    int64_t nblk;
+    int32_t shift, stride;      // stride: codes per sample column in LDS
+};
+__device__ inline int32_t pop_gather(const PopGather& pg, int32_t p, int s, uint8_t* dst, int32_t cap) {
+    int32_t rows = 0;
+    const uint32_t rc = pg.ref[p];
+    const int st1 = pg.samp_st[s + 1];
+    for (int st = pg.samp_st[s]; st < st1; st++) {
+        int64_t e = pg.blkA[(int64_t)st * pg.nblk + (p >> pg.shift)];
+        const int64_t end = pg.st_end[st];
+        bool done = false;
+        while (!done && e < end) {
+            int2 h[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) h[i] = e + i < end ? pg.rh[e + i] : make_int2(0x7FFFFFFF, 0);
+            const int64_t g0 = e >> 6;
+            const int64_t gb0 = pg.grp[g0].base;
+            const int64_t gb1 = ((e + 7) >> 6) != g0 && e + 7 < end ? pg.grp[g0 + 1].base : gb0;
+            uint64_t u[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int32_t gf = h[i].x, gl = h[i].y & 0x7FFFFFFF;
+                u[i] = 0;
+                if (gf <= p && p <= gl) {
+                    const int64_t ei = e + i;
+                    u[i] = pg.units[((ei >> 6) == g0 ? gb0 : gb1) + (int64_t)((p - gf) >> 3) * 64 + (ei & 63)];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int32_t gf = h[i].x, gl = h[i].y & 0x7FFFFFFF;
+                if (gf > p) done = true;                  // entries are sorted by gfirst: none later covers p
+                if (!(gf <= p && p <= gl)) continue;
+                const uint32_t code = ((uint32_t)(u[i] >> (8 * ((p - gf) & 7))) & 0xFFu) ^ rc;   // (reference-relative)
+                if (!code) continue;
+                if (rows < cap) dst[rows] = (uint8_t)code;
+                rows++;
+            }
+            e += 8;
+        }
+    }
+    return rows;
+}
+
+// POOL: ploidy >= 3 (the pool branch's report arrays would otherwise cost every run registers and scratch).
+// GATHER: the columns come from the population read-group layout (pop_gather into dynamic LDS); else from a
+// site-major pile (the realigner's region positions, engine.cpp run_population_regions)
+template <bool POOL, int WPE, bool GATHER>
 __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE))) void k_posterior_multi(
     const QueueSite* __restrict__ queue, const unsigned long long* qn, int64_t qcap,
     const uint8_t* __restrict__ ppile, const uint16_t* __restrict__ prow, const int64_t* __restrict__ pboff,
-    const LikTables* __restrict__ tabs, GenotypeParams gp,
+    const PopGather pg, const LikTables* __restrict__ tabs, GenotypeParams gp,
     int32_t n_samples, double min_adf, int32_t ploidy, const PoolTables* __restrict__ pt,
     ngsep_popsite_out* __restrict__ sites, ngsep_sample_call* __restrict__ calls,
     unsigned long long* counters, int64_t cap, unsigned long long* __restrict__ stamps) {
@@ -1704,12 +1882,13 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
         rows = prow[bi];
         col = ppile + pboff[bi] + (int64_t)(gpos & (kPopTile - 1)) * stride;
     };
+    extern __shared__ uint8_t s_gcol[];                  // GATHER: the position's columns, pg.stride codes per sample
     QueueSite qs_next{0, 0};
     int32_t rows_next = 0;
     const uint8_t* col_next = nullptr;
     if ((int64_t)blockIdx.x < n) {
         qs_next = queue[blockIdx.x];
-        column_of(qs_next.gpos, rows_next, col_next);
+        if (!GATHER) column_of(qs_next.gpos, rows_next, col_next);
     }
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         __syncthreads();
@@ -1728,8 +1907,17 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
         int cnt[4] = {0, 0, 0, 0};
         double L[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         constexpr bool pool = POOL;
-        const int32_t rows = rows_next;
+        int32_t rows = rows_next;
         const uint8_t* col = col_next;
+        if (GATHER && tid <= n_samples) {
+            uint8_t* dst = s_gcol + (int64_t)tid * pg.stride;
+            rows = pop_gather(pg, gpos, tid, dst, pg.stride);
+            if (rows > pg.stride) {                          // (the host's coverage bound makes this unreachable)
+                atomicOr(&counters[3], 1ull << 63);
+                rows = pg.stride;
+            }
+            col = dst;
+        }
         if (tid <= n_samples) {
             const bool tally = tid < n_samples && !pool;        // (the pool algorithm walks the column itself)
             for (int32_t r0 = 0; r0 < rows; r0 += 8) {
@@ -1761,7 +1949,7 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
             }
         }
         if (i == blockIdx.x) stamp(1);
-        if (inext < n) column_of(qs_next.gpos, rows_next, col_next);   // (in flight during the genotyping)
+        if (!GATHER && inext < n) column_of(qs_next.gpos, rows_next, col_next);   // (in flight during the genotyping)
         // pooled counts: the sum over every sample and the reads of no sample
         {
             int c0 = cnt[0], c1 = cnt[1], c2 = cnt[2], c3 = cnt[3], tt = total;
@@ -2200,9 +2388,9 @@ Device* device_create(int ordinal, std::string& err) {
         for (int k = 0; k < 6; k++)     // 0-2 and 5 time the kernels; 3-4 only order the streams
             (void)hipEventCreateWithFlags(&sl.ev[k], (k < 3 || k == 5) ? hipEventDefault : hipEventDisableTiming);
     }
-    if (hipMalloc(&d->d_counters, 24 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(d->d_counters, 0, 24 * sizeof(unsigned long long)) != hipSuccess ||
-        host_pinned_malloc((void**)&d->h_counters, 4 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc(&d->d_counters, kCtrWords * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(d->d_counters, 0, kCtrWords * sizeof(unsigned long long)) != hipSuccess ||
+        host_pinned_malloc((void**)&d->h_counters, kCtrWords * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&d->d_tables, sizeof(LikTables)) != hipSuccess) {
         err = "device allocation failed";
         delete d;
@@ -2251,9 +2439,11 @@ void device_release(Device* d) {
     d->cap_units = d->cap_rh = d->cap_grp = d->cap_blk = d->cap_blkB = 0;
     d->n_entries = 0;
     d->rg = false;
-    (void)hipFree(d->d_mc_pos); d->d_mc_pos = nullptr;
-    (void)hipFree(d->d_mc_n); d->d_mc_n = nullptr;
-    (void)hipFree(d->d_mc_gbase); d->d_mc_gbase = nullptr;
+    (void)hipFree(d->d_samp_st); d->d_samp_st = nullptr;
+    (void)hipFree(d->d_st_end); d->d_st_end = nullptr;
+    d->prg = false;
+    d->n_streams = 0;
+    d->pop_stride = 0;
     (void)hipFree(d->d_need); d->d_need = nullptr;
     (void)hipFree(d->d_mforced); d->d_mforced = nullptr;
     (void)hipFree(d->d_mforced_ctr); d->d_mforced_ctr = nullptr;
@@ -2339,7 +2529,7 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
     const int32_t pad = s.windows.empty() ? 64 : s.windows[0].pad;
     // single sample (a streamed window or a whole run): buffers kept across runs while large enough; the
     // multisample run starts from nothing
-    const bool keep = s.single && d->d_ppile == nullptr;
+    const bool keep = s.single && d->d_ppile == nullptr && !d->prg;
     if (!keep) {
         // (a fault of earlier work is reported as such, not against this upload's copies)
         const hipError_t e = hipDeviceSynchronize();
@@ -2402,15 +2592,45 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
         if (!s.h_loff.empty()) H2D(d->d_loff, s.h_loff.data(), s.h_loff.size() * sizeof(int32_t), d->stream);
         d->planes_W = s.tile / 32;
     } else {
-        if (ensure_dev(&d->d_pile, &d->cap_pile, (size_t)s.pile_bytes + 64, false, err)) return -1;
-        // multisample: the candidate columns (KTM), the position-major per-sample pile (KPM)
-        HIP_TRY(hipMalloc(&d->d_mc_pos, std::max<size_t>(s.h_mc_pos.size(), 1) * sizeof(int32_t)));
-        HIP_TRY(hipMalloc(&d->d_mc_n, std::max<size_t>(s.h_mc_n.size(), 1)));
-        HIP_TRY(hipMalloc(&d->d_mc_gbase, std::max<size_t>(s.h_mc_gbase.size(), 1) * sizeof(int64_t)));
         HIP_TRY(hipMalloc(&d->d_need, (size_t)(s.g_len / 32 + 1) * sizeof(uint32_t)));
-        HIP_TRY(hipMalloc(&d->d_ppile, (size_t)s.ppile_bytes + 64));
-        HIP_TRY(hipMalloc(&d->d_prow, std::max<size_t>(s.h_prow.size(), 1) * sizeof(uint16_t)));
-        HIP_TRY(hipMalloc(&d->d_pboff, std::max<size_t>(s.h_pboff.size(), 1) * sizeof(int64_t)));
+        if (s.prg) {
+            // multisample: the population read-group layout (KLM scans it, KPM gathers its columns)
+            const size_t nblk = (size_t)(s.pnblk * s.n_streams);
+            HIP_TRY(hipMalloc(&d->d_units, (size_t)(s.n_units + 8) * sizeof(uint64_t)));
+            HIP_TRY(hipMalloc(&d->d_rh, (size_t)std::max<int64_t>(s.n_entries, 64) * sizeof(int2)));
+            HIP_TRY(hipMalloc(&d->d_grp, (size_t)std::max<int64_t>(s.n_groups, 1) * sizeof(RGroup)));
+            HIP_TRY(hipMalloc(&d->d_blkA, std::max<size_t>(nblk, 1) * sizeof(int32_t)));
+            HIP_TRY(hipMalloc(&d->d_blkB, std::max<size_t>(nblk, 1) * sizeof(int32_t)));
+            HIP_TRY(hipMalloc(&d->d_samp_st, s.h_samp_st.size() * sizeof(int32_t)));
+            HIP_TRY(hipMalloc(&d->d_st_end, std::max<size_t>(s.h_st_end.size(), 1) * sizeof(int64_t)));
+            if (s.n_units) {
+                if (pinned_covers(s.h_units, (size_t)s.n_units * sizeof(uint64_t))) DMA(d->d_units, s.h_units, (size_t)s.n_units * sizeof(uint64_t), 0, d->stream);
+                else H2D(d->d_units, s.h_units, (size_t)s.n_units * sizeof(uint64_t), d->stream);
+            }
+            HIP_TRY(hipMemsetAsync(d->d_units + s.n_units, 0, 8 * sizeof(uint64_t), d->stream));
+            if (s.n_entries) H2D(d->d_rh, s.h_rh.data(), (size_t)s.n_entries * sizeof(int2), d->stream);
+            if (s.n_groups) H2D(d->d_grp, s.h_grp.data(), (size_t)s.n_groups * sizeof(RGroup), d->stream);
+            if (nblk) {
+                H2D(d->d_blkA, s.h_blkA.data(), nblk * sizeof(int32_t), d->stream);
+                H2D(d->d_blkB, s.h_blkB.data(), nblk * sizeof(int32_t), d->stream);
+            }
+            H2D(d->d_samp_st, s.h_samp_st.data(), s.h_samp_st.size() * sizeof(int32_t), d->stream);
+            if (!s.h_st_end.empty()) H2D(d->d_st_end, s.h_st_end.data(), s.h_st_end.size() * sizeof(int64_t), d->stream);
+            d->n_entries = s.n_entries;
+            d->prg = true;
+            d->n_streams = s.n_streams;
+            d->pblk_shift = s.pblk_shift;
+            d->pnblk = s.pnblk;
+            d->pop_stride = std::max<int32_t>(s.max_cov, 1);
+        } else {
+            // the realigner's region positions: a site-major pile (KPM)
+            HIP_TRY(hipMalloc(&d->d_ppile, (size_t)s.ppile_bytes + 64));
+            HIP_TRY(hipMalloc(&d->d_prow, std::max<size_t>(s.h_prow.size(), 1) * sizeof(uint16_t)));
+            HIP_TRY(hipMalloc(&d->d_pboff, std::max<size_t>(s.h_pboff.size(), 1) * sizeof(int64_t)));
+            H2D(d->d_ppile, s.h_ppile.get(), (size_t)s.ppile_bytes + 64, d->stream);
+            if (!s.h_prow.empty()) H2D(d->d_prow, s.h_prow.data(), s.h_prow.size() * sizeof(uint16_t), d->stream);
+            if (!s.h_pboff.empty()) H2D(d->d_pboff, s.h_pboff.data(), s.h_pboff.size() * sizeof(int64_t), d->stream);
+        }
         if (s.known) {
             // -knownVariants: the input variants at covered positions are KPM's whole queue (no scan)
             const int64_t nf = (int64_t)s.h_forced.size() / 2;
@@ -2421,15 +2641,7 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
             H2D(d->d_mforced_ctr, hc, sizeof hc, d->stream);
             d->n_mforced = nf;
         }
-        if (s.pile_bytes) H2D(d->d_pile, s.h_pile.data(), (size_t)s.pile_bytes, d->stream);
-        if (!s.h_mc_pos.empty()) H2D(d->d_mc_pos, s.h_mc_pos.data(), s.h_mc_pos.size() * sizeof(int32_t), d->stream);
-        if (!s.h_mc_n.empty()) H2D(d->d_mc_n, s.h_mc_n.data(), s.h_mc_n.size(), d->stream);
-        if (!s.h_mc_gbase.empty()) H2D(d->d_mc_gbase, s.h_mc_gbase.data(), s.h_mc_gbase.size() * sizeof(int64_t), d->stream);
-        H2D(d->d_ppile, s.h_ppile.get(), (size_t)s.ppile_bytes + 64, d->stream);
-        if (!s.h_prow.empty()) H2D(d->d_prow, s.h_prow.data(), s.h_prow.size() * sizeof(uint16_t), d->stream);
-        if (!s.h_pboff.empty()) H2D(d->d_pboff, s.h_pboff.data(), s.h_pboff.size() * sizeof(int64_t), d->stream);
         HIP_TRY(hipStreamSynchronize(d->stream));       // the host layout is freed after the upload
-        d->mc_entries = s.mc_entries;
         d->n_samples = s.n_samples;
     }
     d->n_reads = s.n_reads;
@@ -2908,11 +3120,47 @@ int device_run_rac(Device* d, const Staged& s, int64_t g0, int64_t g1, int32_t m
 // workgroups looping over the queue (measured on configs[4]: 235 -> 204 us against 3 waves and 2048 workgroups)
 constexpr int kKpmWavesPerEu = 4;
 constexpr unsigned kKpmGrid = 16384;
-static auto kpm_kernel(int ploidy) {
-    return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu> : k_posterior_multi<false, kKpmWavesPerEu>;
+static auto kpm_kernel(int ploidy, bool gather) {
+    return gather ? (ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, true> : k_posterior_multi<false, kKpmWavesPerEu, true>)
+                  : (ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, false> : k_posterior_multi<false, kKpmWavesPerEu, false>);
 }
 
-// MultisampleVariantsDetector run: KTM over every resident tile, KPM over the queued positions,
+// KLM over every (sample, tile) of the resident population layout, then KQN (shared by the two multisample paths)
+static hipError_t launch_pop_scan(Device* d, const GenotypeParams& g, uint32_t* need, QueueSite* queue, int64_t qcap,
+                                  unsigned long long* ctr, hipEvent_t ev_start, hipEvent_t ev_end) {
+    const int64_t nwords = d->g_len / 32 + 1;
+    hipError_t e = hipMemsetAsync(need, 0, (size_t)nwords * sizeof(uint32_t), d->stream);
+    if (e != hipSuccess) return e;
+    const int64_t ntile = d->g_len / kKlmTile;
+    const int64_t nblk = std::max<int64_t>(1, ntile * ((d->n_samples + 3) / 4));
+    if (nblk >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+    hipExtLaunchKernelGGL(k_scan_pop, dim3((unsigned)nblk), dim3(kKlmThreads), 0, d->stream, ev_start, nullptr, 0,
+                          (const uint64_t*)d->d_units, (const int2*)d->d_rh, (const RGroup*)d->d_grp,
+                          (const int32_t*)d->d_samp_st, (const int32_t*)d->d_blkA, (const int32_t*)d->d_blkB, d->pnblk,
+                          d->pblk_shift, d->n_samples, (const uint8_t*)d->d_ref, (const LikTables*)d->d_tables, g, need, ctr);
+    if ((e = launch_check()) != hipSuccess) return e;
+    const int64_t qblk = std::max<int64_t>(1, std::min<int64_t>((nwords + 255) / 256, (int64_t)d->n_cu * 4));
+    hipExtLaunchKernelGGL(k_queue_need, dim3((unsigned)qblk), dim3(256), 0, d->stream, nullptr, ev_end, 0,
+                          (const uint32_t*)need, (const uint8_t*)d->d_ref, nwords, queue, ctr, qcap);
+    return launch_check();
+}
+static PopGather pop_gather_of(const Device* d) {
+    PopGather pg{};
+    if (!d->prg) return pg;
+    pg.units = d->d_units; pg.rh = d->d_rh; pg.grp = d->d_grp; pg.samp_st = d->d_samp_st; pg.st_end = d->d_st_end;
+    pg.blkA = d->d_blkA; pg.ref = d->d_ref; pg.nblk = d->pnblk; pg.shift = d->pblk_shift; pg.stride = d->pop_stride;
+    return pg;
+}
+static size_t kpm_lds(const Device* d) { return d->prg ? (size_t)(d->n_samples + 1) * (size_t)d->pop_stride : 0; }
+// the shard counters' sums: KLM's candidate columns and bounded columns
+static void pop_scan_counts(const unsigned long long* h, int64_t* cand, int64_t* bounded) {
+    int64_t a = 0, b = 0;
+    for (int t = 0; t < kKlShards; t++) { a += (int64_t)h[kCtrShard0 + kCtrShardStride * t]; b += (int64_t)h[kCtrShard0 + kCtrShardStride * t + 1]; }
+    *cand = a;
+    *bounded = b;
+}
+
+// MultisampleVariantsDetector run: KLM over every (sample, tile), KQN, KPM over the queued positions,
 // D2H of the emitted sites and their per-sample calls (unordered; the host orders them)
 int device_run_multi(Device* d, const Staged& s, const LikTables& t, const GenotypeParams& g,
                      int32_t n_samples, double min_adf, int ploidy,
@@ -2948,44 +3196,33 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
         d->tables_valid = true;
     }
     unsigned long long* ctr = d->d_counters;
-    HIP_TRY(hipMemsetAsync(ctr, 0, 4 * sizeof(unsigned long long), d->stream));
-    // KTM and KPM are timed by events bound to their dispatches (ev 0-1 and 3-2)
-    // KTM + KQN, timed together by events bound to their dispatches (ev 0-1), KPM by ev 3-2
-    const int64_t nwords = d->g_len / 32 + 1;
-    const bool mknown = d->n_mforced >= 0;             // -knownVariants: the input variants are the queue
-    if (mknown) {
+    HIP_TRY(hipMemsetAsync(ctr, 0, kCtrWords * sizeof(unsigned long long), d->stream));
+    // KLM + KQN, timed together by events bound to their dispatches (ev 0-1), KPM by ev 1-2
+    const bool mknown = d->n_mforced >= 0;             // -knownVariants (and the realigner's regions): the queue is given
+    if (mknown || !d->prg) {
         HIP_TRY(hipEventRecord(d->ev[0], d->stream));
         HIP_TRY(hipEventRecord(d->ev[1], d->stream));
     } else {
-    HIP_TRY(hipMemsetAsync(d->d_need, 0, (size_t)nwords * sizeof(uint32_t), d->stream));
-    {
-        const int64_t ngroups = (d->mc_entries + 63) / 64;
-        const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((ngroups + 3) / 4, (int64_t)d->n_cu * 8));
-        hipExtLaunchKernelGGL(k_scan_multi, dim3((unsigned)nblk), dim3(256), 0, d->stream, d->ev[0], nullptr, 0,
-                              (const int32_t*)d->d_mc_pos, (const uint8_t*)d->d_mc_n, (const int64_t*)d->d_mc_gbase,
-                              (const uint8_t*)d->d_pile, d->mc_entries, (const LikTables*)d->d_tables, g, d->d_need, ctr);
-        HIP_TRY(launch_check());
-        const int64_t qblk = std::max<int64_t>(1, std::min<int64_t>((nwords + 255) / 256, (int64_t)d->n_cu * 4));
-        hipExtLaunchKernelGGL(k_queue_need, dim3((unsigned)qblk), dim3(256), 0, d->stream, nullptr, d->ev[1], 0,
-                              (const uint32_t*)d->d_need, (const uint8_t*)d->d_ref, nwords, d->d_hard, ctr, d->cap_hard);
-        HIP_TRY(launch_check());
-    }
+        HIP_TRY(launch_pop_scan(d, g, d->d_need, d->d_hard, d->cap_hard, ctr, d->ev[0], d->ev[1]));
     }
     if (ploidy >= 3 && !d->pool_valid) { err = "ploidy >= 3 without pool tables (device_set_pool)"; return -1; }
     // (no start event on KPM: a start event between KQN and KPM was measured to idle the device; KPM's time is
     // taken from KQN's end)
-    hipExtLaunchKernelGGL(kpm_kernel(ploidy), dim3(kKpmGrid), dim3(kPopThreads), 0, d->stream, nullptr, d->ev[2], 0,
+    if (!mknown && !d->prg) { err = "multisample run without a population layout"; return -1; }
+    hipExtLaunchKernelGGL(kpm_kernel(ploidy, d->prg), dim3(kKpmGrid), dim3(kPopThreads), kpm_lds(d), d->stream, nullptr, d->ev[2], 0,
                           (const QueueSite*)(mknown ? d->d_mforced : d->d_hard),
                           (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : ctr + 2),
                           mknown ? std::max<int64_t>(d->n_mforced, 1) : d->cap_hard, (const uint8_t*)d->d_ppile,
-                          (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, (const LikTables*)d->d_tables, g,
+                          (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, pop_gather_of(d), (const LikTables*)d->d_tables, g,
                           S, min_adf, ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), d->d_psites, d->d_pcalls,
                           ctr, d->cap_psites, d->d_stamps);
     HIP_TRY(launch_check());
-    DMA(d->h_counters, ctr, 4 * sizeof(unsigned long long), 1, d->stream);
+    DMA(d->h_counters, ctr, kCtrWords * sizeof(unsigned long long), 1, d->stream);
     HIP_TRY(hipStreamSynchronize(d->stream));
     const unsigned long long c3 = d->h_counters[3];
-    if (c3 >> 63) { err = "a position is covered by more reads than the population kernel holds (" + std::to_string(kPopListCap) + ")"; return -1; }
+    if (c3 >> 63) { err = "internal error: a gathered population column exceeds its coverage bound"; return -1; }
+    int64_t cand = 0, bounded = 0;
+    pop_scan_counts(d->h_counters, &cand, &bounded);
     const int64_t n = (int64_t)d->h_counters[0];
     if ((int64_t)d->h_counters[2] > d->cap_hard) {
         (void)hipFree(d->d_hard);
@@ -3019,7 +3256,7 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     *n_sites = n;
     d->last_n_sites = n;
     d->last_hard = (int64_t)d->h_counters[2];
-    d->last_exact = (int64_t)(c3 & 0x7FFFFFFFFFFFFFFFull);
+    d->last_exact = bounded;
     if (timing) {
         unsigned long long* st = nullptr;                        // (a pinned endpoint, as every copy's)
         HIP_TRY(host_pinned_malloc((void**)&st, 16 * sizeof(unsigned long long)));
@@ -3034,7 +3271,7 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     *scan_ms = a;
     *geno_ms = a2;
     *total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    *n_candidates = d->mc_entries;          // candidate columns (sample, position) the scan bounded
+    *n_candidates = cand;                   // candidate columns (sample, position) the scan marked
     return 0;
 }
 
@@ -3230,30 +3467,21 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
         d->tables_valid = true;
     }
     unsigned long long* ctr = d->slot[d->mnext].d_ctr;
-    HIP_TRY(hipMemsetAsync(ctr, 0, 4 * sizeof(unsigned long long), d->stream));
+    HIP_TRY(hipMemsetAsync(ctr, 0, kCtrWords * sizeof(unsigned long long), d->stream));
     const bool mknown = d->n_mforced >= 0;             // -knownVariants: the input variants are the queue
+    if (!mknown && !d->prg) { err = "multisample run without a population layout"; return -1; }
     if (mknown) {
         HIP_TRY(hipEventRecord(m.ev[0], d->stream));
         HIP_TRY(hipEventRecord(m.ev[1], d->stream));
     } else {
-    HIP_TRY(hipMemsetAsync(m.d_need, 0, (size_t)nwords * sizeof(uint32_t), d->stream));
-    const int64_t ngroups = (d->mc_entries + 63) / 64;
-    static const int ktm_env = diag_env("NGSEP_KTM_BPC") ? std::max(1, std::atoi(diag_env("NGSEP_KTM_BPC"))) : 8;   // tuning
-    const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>((ngroups + 3) / 4, (int64_t)d->n_cu * ktm_env));
-    hipExtLaunchKernelGGL(k_scan_multi, dim3((unsigned)nblk), dim3(256), 0, d->stream, m.ev[0], nullptr, 0,
-                          (const int32_t*)d->d_mc_pos, (const uint8_t*)d->d_mc_n, (const int64_t*)d->d_mc_gbase,
-                          (const uint8_t*)d->d_pile, d->mc_entries, (const LikTables*)d->d_tables, g, m.d_need, ctr);
-    HIP_TRY(launch_check());
-    const int64_t qblk = std::max<int64_t>(1, std::min<int64_t>((nwords + 255) / 256, (int64_t)d->n_cu * 4));
-    hipExtLaunchKernelGGL(k_queue_need, dim3((unsigned)qblk), dim3(256), 0, d->stream, nullptr, m.ev[1], 0,
-                          (const uint32_t*)m.d_need, (const uint8_t*)d->d_ref, nwords, m.d_hard, ctr, m.cap_hard);
-    HIP_TRY(launch_check());
+        HIP_TRY(launch_pop_scan(d, g, m.d_need, m.d_hard, m.cap_hard, ctr, m.ev[0], m.ev[1]));
     }
-    hipExtLaunchKernelGGL(kpm_kernel(ploidy), dim3(kKpmGrid), dim3(kPopThreads), 0, d->stream, nullptr, m.ev[3], 0,
+    (void)nwords;
+    hipExtLaunchKernelGGL(kpm_kernel(ploidy, d->prg), dim3(kKpmGrid), dim3(kPopThreads), kpm_lds(d), d->stream, nullptr, m.ev[3], 0,
                           (const QueueSite*)(mknown ? d->d_mforced : m.d_hard),
                           (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : ctr + 2),
                           mknown ? std::max<int64_t>(d->n_mforced, 1) : m.cap_hard, (const uint8_t*)d->d_ppile,
-                          (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, (const LikTables*)d->d_tables, g,
+                          (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, pop_gather_of(d), (const LikTables*)d->d_tables, g,
                           S, min_adf, ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), m.d_psites, m.d_pcalls,
                           ctr, m.cap_psites, (unsigned long long*)nullptr);
     HIP_TRY(launch_check());
@@ -3285,7 +3513,7 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
     HIP_TRY(hipEventRecord(m.ev[5], d->stream));
     HIP_TRY(hipStreamWaitEvent(d->copy_stream, m.ev[5], 0));
     hipStream_t cs = d->copy_stream;
-    DMA(d->slot[d->mnext].h_ctr, ctr, 8 * sizeof(unsigned long long), 1, cs);
+    DMA(d->slot[d->mnext].h_ctr, ctr, kCtrWords * sizeof(unsigned long long), 1, cs);
     m.guess = std::min<int64_t>(m.cap_psites, d->last_n_sites + d->last_n_sites / 16 + 64);
     DMA(m.h_psites, m.d_psites, (size_t)m.guess * sizeof(ngsep_popsite_out), 1, cs);
     DMA(m.h_pack.data(), m.d_pack, (size_t)(m.guess * S) * sizeof(PopCall32), 1, cs);
@@ -3312,7 +3540,9 @@ int device_collect_multi(Device* d, const ngsep_popsite_out** sites, int64_t* n_
     HIP_TRY(hipEventSynchronize(m.ev[4]));
     const unsigned long long* hc = d->slot[k].h_ctr;
     const unsigned long long c3 = hc[3];
-    if (c3 >> 63) { err = "a position is covered by more reads than the population kernel holds (" + std::to_string(kPopListCap) + ")"; return -1; }
+    if (c3 >> 63) { err = "internal error: a gathered population column exceeds its coverage bound"; return -1; }
+    int64_t cand = 0, bounded = 0;
+    pop_scan_counts(hc, &cand, &bounded);
     const int64_t n = (int64_t)hc[0];
     *rerun = (int64_t)hc[2] > m.cap_hard || n > m.cap_psites || (int64_t)hc[5] > m.cap_big;
     *slot = k;
@@ -3329,13 +3559,13 @@ int device_collect_multi(Device* d, const ngsep_popsite_out** sites, int64_t* n_
     *n_sites = n;
     d->last_n_sites = n;
     d->last_hard = (int64_t)hc[2];
-    d->last_exact = (int64_t)(c3 & 0x7FFFFFFFFFFFFFFFull);
+    d->last_exact = bounded;
     float a = 0, a2 = 0;
     (void)hipEventElapsedTime(&a, m.ev[0], m.ev[1]);
     (void)hipEventElapsedTime(&a2, m.ev[1], m.ev[3]);
     *scan_ms = a;
     *geno_ms = a2;
-    *n_candidates = d->mc_entries;
+    *n_candidates = cand;
     return 0;
 }
 
