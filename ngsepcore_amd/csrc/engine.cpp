@@ -1853,9 +1853,9 @@ static int build_pop_rg_layout(Staged& s, LayoutArena& arena) {
     });
     lap("units");
     // block tables per stream, blocks of 2^pblk_shift positions (coarser when the tables would outgrow a quarter of
-    // the units)
-    int32_t shift = kRgBlockShift;
-    while (shift < 20 && ((s.g_len >> shift) + 2) * nst * 8 > std::max<int64_t>((int64_t)64 << 20, s.n_units * 2)) shift++;
+    // the units; at most a KLM tile)
+    int32_t shift = 6;                                 // (KPM's gather walks ~ (64 + max span) x depth / span entries)
+    while (shift < 11 && ((s.g_len >> shift) + 2) * nst * 8 > std::max<int64_t>((int64_t)64 << 20, s.n_units * 2)) shift++;
     s.pblk_shift = shift;
     const int64_t nb = (s.g_len >> shift) + 2;
     s.pnblk = nb;

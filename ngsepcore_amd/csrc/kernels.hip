@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "engine.hpp"
+#include <sys/mman.h>
 
 namespace ngsep {
 
@@ -1720,6 +1721,65 @@ __device__ PopCall genotype_sample_d(const double* L, const int* cnt, int total,
     c.acn[0] = c.acn[1] = c.acn[2] = c.acn[3] = 0;
     if (total == 0) return c;                   // undecided CalledGenomicVariantImpl(variant, new byte[0])
     const double ph = gp.log_prior_homo, px = gp.log_prior_hetero;
+    if (nal == 2) {
+        // the biallelic case without the 16-entry posterior array (registers: KPM's 4-wave build spilled here): the
+        // same sums in the same order, keeping only the four posteriors the call reads and the six exponents the
+        // symmetric genotypes reuse
+        constexpr int LI[16] = {0, 1, 2, 3, 4, 1, 5, 6, 7, 2, 5, 8, 9, 3, 6, 8};   // ev[k] = L[LI[k]] + prior
+        const int r = idx[0], a = idx[1];
+        auto kof = [](int x, int y) { return x == y ? 4 * x : (y < x ? 4 * x + 1 + y : 4 * x + y); };
+        const int k_rr = kof(r, r), k_aa = kof(a, a), k_ra = kof(r, a), k_ar = kof(a, r);
+        double logMax = 1;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const double x = L[LI[k]] + ((k & 3) == 0 ? ph : px);
+            if (logMax > 0 || logMax < x) logMax = x;
+        }
+        double totalProb = 0, v_rr = 0, v_aa = 0, v_ra = 0, v_ar = 0;
+        double s1 = 0, s2 = 0, s3 = 0, s6 = 0, s7 = 0, s11 = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int src = ev_partner(k);
+            double val;
+            if (src) val = src == 1 ? s1 : src == 2 ? s2 : src == 3 ? s3 : src == 6 ? s6 : src == 7 ? s7 : s11;
+            else {
+                const double x = (L[LI[k]] + ((k & 3) == 0 ? ph : px)) - logMax;
+                val = x < -20 ? 0.0 : pow(10.0, x);
+            }
+            if (k == 1) s1 = val;
+            if (k == 2) s2 = val;
+            if (k == 3) s3 = val;
+            if (k == 6) s6 = val;
+            if (k == 7) s7 = val;
+            if (k == 11) s11 = val;
+            totalProb += val;
+            v_rr = k == k_rr ? val : v_rr;
+            v_aa = k == k_aa ? val : v_aa;
+            v_ra = k == k_ra ? val : v_ra;
+            v_ar = k == k_ar ? val : v_ar;
+        }
+        double pMax = v_rr / totalProb;
+        int genotype = 0;
+        const double pHomoAlt = v_aa / totalProb;
+        if (pHomoAlt > pMax + 0.01) { pMax = pHomoAlt; genotype = 2; }
+        const double pHetero = v_ra / totalProb + v_ar / totalProb;
+        if (pHetero > pMax + 0.01) { pMax = pHetero; genotype = 1; }
+        int gq = phred_d(1 - pMax);
+        if (gq == 0) genotype = -1;
+        c.kind = 0;
+        int tot = 0, ref = 0;
+        csnv_cn(genotype, sel4i(cnt, r), sel4i(cnt, a), ploidy, &tot, &ref);
+        if (40 > gq) { genotype = -1; gq = 0; ref = 0; }      // makeUndecided (CalledSNV.java:279-285)
+        c.gq = gq;
+        c.total_cn = tot;
+        if (genotype == -1) c.n_called = 0;
+        else if (genotype == 0) { c.n_called = 1; c.c0 = 0; }
+        else if (genotype == 2) { c.n_called = 1; c.c0 = 1; }
+        else { c.n_called = 2; c.c0 = 0; c.c1 = 1; }
+        c.acn[0] = genotype == -1 ? 0 : ref;
+        c.acn[1] = genotype == -1 ? 0 : tot - ref;
+        return c;
+    }
     double ev[16] = {L[0] + ph, L[1] + px, L[2] + px, L[3] + px,
                      L[4] + ph, L[1] + px, L[5] + px, L[6] + px,
                      L[7] + ph, L[2] + px, L[5] + px, L[8] + px,
@@ -1805,6 +1865,7 @@ struct PopGather {
     int64_t nblk;
     int32_t shift, stride;      // stride: codes per sample column in LDS
 };
+template <int kGatherBatch>                      // entry headers a gathering thread loads at once
 __device__ inline int32_t pop_gather(const PopGather& pg, int32_t p, int s, uint8_t* dst, int32_t cap) {
     int32_t rows = 0;
     const uint32_t rc = pg.ref[p];
@@ -1814,42 +1875,47 @@ __device__ inline int32_t pop_gather(const PopGather& pg, int32_t p, int s, uint
         const int64_t end = pg.st_end[st];
         bool done = false;
         while (!done && e < end) {
-            int2 h[8];
+            int2 h[kGatherBatch];
 #pragma unroll
-            for (int i = 0; i < 8; i++) h[i] = e + i < end ? pg.rh[e + i] : make_int2(0x7FFFFFFF, 0);
+            for (int i = 0; i < kGatherBatch; i++) h[i] = e + i < end ? pg.rh[e + i] : make_int2(0x7FFFFFFF, 0);
             const int64_t g0 = e >> 6;
             const int64_t gb0 = pg.grp[g0].base;
-            const int64_t gb1 = ((e + 7) >> 6) != g0 && e + 7 < end ? pg.grp[g0 + 1].base : gb0;
-            uint64_t u[8];
+            const int64_t gb1 = ((e + kGatherBatch - 1) >> 6) != g0 && ((g0 + 1) << 6) < end ? pg.grp[g0 + 1].base : gb0;
+            uint32_t u[kGatherBatch];
 #pragma unroll
-            for (int i = 0; i < 8; i++) {
+            for (int i = 0; i < kGatherBatch; i++) {
                 const int32_t gf = h[i].x, gl = h[i].y & 0x7FFFFFFF;
                 u[i] = 0;
                 if (gf <= p && p <= gl) {
-                    const int64_t ei = e + i;
-                    u[i] = pg.units[((ei >> 6) == g0 ? gb0 : gb1) + (int64_t)((p - gf) >> 3) * 64 + (ei & 63)];
+                    const int64_t ei = e + i, o = p - gf;
+                    // the covering byte's dword of its unit
+                    const uint32_t* uw = reinterpret_cast<const uint32_t*>(pg.units + ((ei >> 6) == g0 ? gb0 : gb1) + (o >> 3) * 64 + (ei & 63));
+                    u[i] = uw[(o >> 2) & 1];
                 }
             }
 #pragma unroll
-            for (int i = 0; i < 8; i++) {
+            for (int i = 0; i < kGatherBatch; i++) {
                 const int32_t gf = h[i].x, gl = h[i].y & 0x7FFFFFFF;
                 if (gf > p) done = true;                  // entries are sorted by gfirst: none later covers p
                 if (!(gf <= p && p <= gl)) continue;
-                const uint32_t code = ((uint32_t)(u[i] >> (8 * ((p - gf) & 7))) & 0xFFu) ^ rc;   // (reference-relative)
+                const uint32_t code = ((u[i] >> (8 * ((p - gf) & 3))) & 0xFFu) ^ rc;   // (reference-relative)
                 if (!code) continue;
                 if (rows < cap) dst[rows] = (uint8_t)code;
                 rows++;
             }
-            e += 8;
+            e += kGatherBatch;
         }
     }
     return rows;
 }
 
 // POOL: ploidy >= 3 (the pool branch's report arrays would otherwise cost every run registers and scratch).
-// GATHER: the columns come from the population read-group layout (pop_gather into dynamic LDS); else from a
-// site-major pile (the realigner's region positions, engine.cpp run_population_regions)
-template <bool POOL, int WPE, bool GATHER>
+// GATHER, where the columns come from: 0 a site-major pile (the realigner's region positions, engine.cpp
+// run_population_regions; ppile / prow / pboff); 1 the population read-group layout, gathered here into dynamic LDS
+// (measured and not kept: a separate gather kernel, one thread per (position, sample) at 8 waves per SIMD, into
+// columns KPM then read with the next position's in flight -- 0.64 against 0.52 ms for gather + KPM on configs[4]:
+// the gather's cost is its scattered lines, ~10 per sample column, not latency KPM fails to hide)
+template <bool POOL, int WPE, int GATHER>
 __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE))) void k_posterior_multi(
     const QueueSite* __restrict__ queue, const unsigned long long* qn, int64_t qcap,
     const uint8_t* __restrict__ ppile, const uint16_t* __restrict__ prow, const int64_t* __restrict__ pboff,
@@ -1873,10 +1939,11 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
     // thread s's column of a queued position: its rows and first code (site-major tile, engine.hpp: the S + 1 columns
     // of gpos are one contiguous run of stride bytes).  The next position's entry and column are fetched while the
     // current one is genotyped.
-    auto column_of = [&](int32_t gpos, int32_t& rows, const uint8_t*& col) {
+    auto column_of = [&](int64_t qi, int32_t gpos, int32_t& rows, const uint8_t*& col) {
         rows = 0;
         col = nullptr;
         if (tid > n_samples) return;
+        (void)qi;
         const int64_t b0 = (int64_t)(gpos >> kPopTileLog2) * (n_samples + 1), bi = b0 + tid;
         const int64_t stride = (pboff[b0 + n_samples + 1] - pboff[b0]) >> kPopTileLog2;
         rows = prow[bi];
@@ -1888,7 +1955,7 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
     const uint8_t* col_next = nullptr;
     if ((int64_t)blockIdx.x < n) {
         qs_next = queue[blockIdx.x];
-        if (!GATHER) column_of(qs_next.gpos, rows_next, col_next);
+        if (GATHER != 1) column_of(blockIdx.x, qs_next.gpos, rows_next, col_next);
     }
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         __syncthreads();
@@ -1909,9 +1976,9 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
         constexpr bool pool = POOL;
         int32_t rows = rows_next;
         const uint8_t* col = col_next;
-        if (GATHER && tid <= n_samples) {
+        if (GATHER == 1 && tid <= n_samples) {
             uint8_t* dst = s_gcol + (int64_t)tid * pg.stride;
-            rows = pop_gather(pg, gpos, tid, dst, pg.stride);
+            rows = pop_gather<16>(pg, gpos, tid, dst, pg.stride);
             if (rows > pg.stride) {                          // (the host's coverage bound makes this unreachable)
                 atomicOr(&counters[3], 1ull << 63);
                 rows = pg.stride;
@@ -1949,7 +2016,7 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
             }
         }
         if (i == blockIdx.x) stamp(1);
-        if (!GATHER && inext < n) column_of(qs_next.gpos, rows_next, col_next);   // (in flight during the genotyping)
+        if (GATHER != 1 && inext < n) column_of(inext, qs_next.gpos, rows_next, col_next);   // (in flight during the genotyping)
         // pooled counts: the sum over every sample and the reads of no sample
         {
             int c0 = cnt[0], c1 = cnt[1], c2 = cnt[2], c3 = cnt[3], tt = total;
@@ -2047,45 +2114,43 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
             sites[at] = o;
         }
         if (tid < n_samples) {
-            ngsep_sample_call o;
-            o.kind = (int8_t)call.kind; o.n_called = (int8_t)call.n_called;
-            o.called[0] = (int8_t)call.c0; o.called[1] = (int8_t)call.c1;
-            o.gq = (int16_t)call.gq; o.total_cn = (int16_t)call.total_cn;
-            o.dp = pool ? pr.dp : total;
-            for (int k = 0; k < 4; k++) { o.counts[k] = cnt[k]; o.acn[k] = (int16_t)call.acn[k]; o.pl[k] = 0; }
-            for (int k = 4; k < 10; k++) o.pl[k] = 0;
+            // the call's 19 dwords stored as they are computed (a whole record held in registers pushed KPM's
+            // 4-wave build into scratch)
+            uint32_t* o = reinterpret_cast<uint32_t*>(calls + (int64_t)at * n_samples + tid);
+            static_assert(sizeof(ngsep_sample_call) == 76, "ngsep_sample_call: 19 dwords");
+            o[0] = (uint32_t)(uint8_t)call.kind | (uint32_t)(uint8_t)call.n_called << 8 | (uint32_t)(uint8_t)call.c0 << 16 |
+                   (uint32_t)(uint8_t)call.c1 << 24;
+            o[1] = (uint32_t)(uint16_t)call.gq | (uint32_t)(uint16_t)call.total_cn << 16;
+            o[2] = (uint32_t)(pool ? pr.dp : total);
+#pragma unroll
+            for (int k = 0; k < 4; k++) o[3 + k] = (uint32_t)cnt[k];
+            o[7] = (uint32_t)(uint16_t)call.acn[0] | (uint32_t)(uint16_t)call.acn[1] << 16;
+            o[8] = (uint32_t)(uint16_t)call.acn[2] | (uint32_t)(uint16_t)call.acn[3] << 16;
+            uint32_t* pl = o + 9;
+            int npl = 0;                                           // PL values written (the rest are 0)
             // PL (VCFFileWriter.java:200-212) from the call report
             if (pool) {
                 if (pr.report) {
-                    int k = 0;
                     for (int j = 0; j < nal; j++)
-                        for (int ii = 0; ii <= j; ii++) {
-                            const int32_t v = (int32_t)java_round_d(-10 * sel10(pr.L, ii * nal - ii * (ii - 1) / 2 + (j - ii)));
-#pragma unroll
-                            for (int e = 0; e < 10; e++) if (e == k) o.pl[e] = v;
-                            k++;
-                        }
+                        for (int ii = 0; ii <= j; ii++)
+                            pl[npl++] = (uint32_t)(int32_t)java_round_d(-10 * sel10(pr.L, ii * nal - ii * (ii - 1) / 2 + (j - ii)));
                 }
             } else if (call.kind == 0) {
                 const float hr = (float)sel10(L, tri_d(idx[0], idx[0])), ha = (float)sel10(L, tri_d(idx[1], idx[1]));
                 const float ra = (float)sel10(L, tri_d(idx[0], idx[1])), ar = ra;
                 const bool present = (hr + ra + ar + ha) != 0;     // CalledSNV.java:422 (float sum)
                 if (present) {
-                    o.pl[0] = (int32_t)java_round_d(-10 * (double)hr);
-                    o.pl[1] = (int32_t)java_round_d(-10 * (double)ra);
-                    o.pl[2] = (int32_t)java_round_d(-10 * (double)ha);
+                    pl[0] = (uint32_t)(int32_t)java_round_d(-10 * (double)hr);
+                    pl[1] = (uint32_t)(int32_t)java_round_d(-10 * (double)ra);
+                    pl[2] = (uint32_t)(int32_t)java_round_d(-10 * (double)ha);
+                    npl = 3;
                 }
             } else if (total > 0) {
-                int k = 0;
                 for (int j = 0; j < nal; j++)
-                    for (int ii = 0; ii <= j; ii++) {
-                        const int32_t v = (int32_t)java_round_d(-10 * sel10(L, tri_d(idx[ii], idx[j])));
-#pragma unroll
-                        for (int e = 0; e < 10; e++) if (e == k) o.pl[e] = v;
-                        k++;
-                    }
+                    for (int ii = 0; ii <= j; ii++)
+                        pl[npl++] = (uint32_t)(int32_t)java_round_d(-10 * sel10(L, tri_d(idx[ii], idx[j])));
             }
-            calls[(int64_t)at * n_samples + tid] = o;
+            for (int k = npl; k < 10; k++) pl[k] = 0u;
         }
     }
 }
@@ -2279,7 +2344,23 @@ static void host_pinned_free(void* p) {
 void* pinned_alloc(size_t bytes) {
     const size_t rounded = (std::max<size_t>(bytes, 1) + 4095) / 4096 * 4096;
     if (host_device_count() <= 0) return std::malloc(rounded);     // host-only code paths: nothing is copied
-    void* p = std::aligned_alloc(4096, rounded);
+    void* p = nullptr;
+    if (rounded >= ((size_t)64 << 20)) {
+        // a large block: transparent huge pages, faulted in on all host threads before the registration pins them
+        // (4 KB pages faulted one by one inside hipHostRegister took ~0.5 s for a 3 GB population layout)
+        constexpr size_t kHuge = (size_t)2 << 20;
+        const size_t n = (rounded + kHuge - 1) / kHuge * kHuge;
+        p = std::aligned_alloc(kHuge, n);
+        if (p) {
+            madvise(p, n, MADV_HUGEPAGE);
+            char* c = static_cast<char*>(p);
+            parallel_for((int64_t)(n / kHuge), 16, [&](int64_t a, int64_t b) {
+                for (int64_t k = a; k < b; k++) c[(size_t)k * kHuge] = 0;
+            });
+        }
+    } else {
+        p = std::aligned_alloc(4096, rounded);
+    }
     if (p && hipHostRegister(p, rounded, hipHostRegisterDefault) == hipSuccess) {
         pin_record(p, rounded, 1);
         return p;
@@ -3120,9 +3201,9 @@ int device_run_rac(Device* d, const Staged& s, int64_t g0, int64_t g1, int32_t m
 // workgroups looping over the queue (measured on configs[4]: 235 -> 204 us against 3 waves and 2048 workgroups)
 constexpr int kKpmWavesPerEu = 4;
 constexpr unsigned kKpmGrid = 16384;
-static auto kpm_kernel(int ploidy, bool gather) {
-    return gather ? (ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, true> : k_posterior_multi<false, kKpmWavesPerEu, true>)
-                  : (ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, false> : k_posterior_multi<false, kKpmWavesPerEu, false>);
+static auto kpm_kernel(int ploidy, int gather) {
+    if (gather == 1) return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, 1> : k_posterior_multi<false, kKpmWavesPerEu, 1>;
+    return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, 0> : k_posterior_multi<false, kKpmWavesPerEu, 0>;
 }
 
 // KLM over every (sample, tile) of the resident population layout, then KQN (shared by the two multisample paths)
@@ -3151,7 +3232,7 @@ static PopGather pop_gather_of(const Device* d) {
     pg.blkA = d->d_blkA; pg.ref = d->d_ref; pg.nblk = d->pnblk; pg.shift = d->pblk_shift; pg.stride = d->pop_stride;
     return pg;
 }
-static size_t kpm_lds(const Device* d) { return d->prg ? (size_t)(d->n_samples + 1) * (size_t)d->pop_stride : 0; }
+static size_t kpm_lds(const Device* d, int mode) { return mode == 1 ? (size_t)(d->n_samples + 1) * (size_t)d->pop_stride : 0; }
 // the shard counters' sums: KLM's candidate columns and bounded columns
 static void pop_scan_counts(const unsigned long long* h, int64_t* cand, int64_t* bounded) {
     int64_t a = 0, b = 0;
@@ -3209,7 +3290,8 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     // (no start event on KPM: a start event between KQN and KPM was measured to idle the device; KPM's time is
     // taken from KQN's end)
     if (!mknown && !d->prg) { err = "multisample run without a population layout"; return -1; }
-    hipExtLaunchKernelGGL(kpm_kernel(ploidy, d->prg), dim3(kKpmGrid), dim3(kPopThreads), kpm_lds(d), d->stream, nullptr, d->ev[2], 0,
+    const int mode = d->prg ? 1 : 0;
+    hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode), dim3(kKpmGrid), dim3(kPopThreads), kpm_lds(d, mode), d->stream, nullptr, d->ev[2], 0,
                           (const QueueSite*)(mknown ? d->d_mforced : d->d_hard),
                           (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : ctr + 2),
                           mknown ? std::max<int64_t>(d->n_mforced, 1) : d->cap_hard, (const uint8_t*)d->d_ppile,
@@ -3477,7 +3559,8 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
         HIP_TRY(launch_pop_scan(d, g, m.d_need, m.d_hard, m.cap_hard, ctr, m.ev[0], m.ev[1]));
     }
     (void)nwords;
-    hipExtLaunchKernelGGL(kpm_kernel(ploidy, d->prg), dim3(kKpmGrid), dim3(kPopThreads), kpm_lds(d), d->stream, nullptr, m.ev[3], 0,
+    const int mode = d->prg ? 1 : 0;
+    hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode), dim3(kKpmGrid), dim3(kPopThreads), kpm_lds(d, mode), d->stream, nullptr, m.ev[3], 0,
                           (const QueueSite*)(mknown ? d->d_mforced : m.d_hard),
                           (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : ctr + 2),
                           mknown ? std::max<int64_t>(d->n_mforced, 1) : m.cap_hard, (const uint8_t*)d->d_ppile,
