@@ -214,6 +214,7 @@ def end_to_end(fa: str, bam: str, device: int):
     return {"wall_s": t2 - t0, "fasta_s": t1 - t0, "call_bam_s": t2 - t1,
             "positions": int(st.positions_genotyped), "value": st.positions_genotyped / (t2 - t0),
             "unit": "positions/s", "vcf_records": n_rec, "bam_bytes": os.path.getsize(bam),
+            "realign_regions": int(st.realign_regions), "realign_replay_ms": float(st.realign_ms),
             "note": "ngsep_call_bam: BAM on disk -> VCF on disk incl. FASTA load; host threads "
                     f"{os.environ.get('NGSEP_THREADS') or cpu_cores()}"}
 
@@ -372,6 +373,7 @@ def main():
         params.multisample = 1
     sessions = []          # (session, synthetic sequences) -- wgs: several device runs of < 2^31 positions
     e2e_src = None
+    e2e_indel_src = None
     if multi:
         syn = pysynth.Synth(genome=pysynth.YEAST, depth=args.depth, seed=5, n_samples=args.samples,
                             contig_first=args.contig_first + rank, n_contigs=args.n_contigs)
@@ -465,6 +467,14 @@ def main():
                 pysynth.lib().ngs_synth_write_fasta(syn.h, fa.encode())
                 pysynth.lib().ngs_synth_write_bam(syn.h, bam.encode())
                 e2e_src = (tmp, fa, bam)
+                # the same sequence with indels (rate 1e-4 per position) for the end-to-end run with the indel
+                # realigner (its own BAM and FASTA; generated and written untimed)
+                isyn = pysynth.Synth(genome=pysynth.HUMAN, depth=args.depth, seed=3 + rank, contig_first=HUMAN_CHR20,
+                                     n_contigs=1, rng_per_contig=1, indel_rate=1e-4)
+                e2e_indel_src = (os.path.join(tmp, "chr20_indels.fa"), os.path.join(tmp, "chr20_indels.bam"))
+                pysynth.lib().ngs_synth_write_fasta(isyn.h, e2e_indel_src[0].encode())
+                pysynth.lib().ngs_synth_write_bam(isyn.h, e2e_indel_src[1].encode())
+                isyn.close()
                 log(f"[rank 0] wrote the end-to-end BAM ({os.path.getsize(bam) / 1e9:.2f} GB) in {time.time() - tw:.1f}s")
             if multi and rank == 0 and world == 1 and not args.no_e2e:
                 # the same population as one BAM per sample on local disk for the end-to-end run
@@ -561,6 +571,12 @@ def main():
         try:
             e2e = (end_to_end_population if multi else end_to_end)(e2e_src[1], e2e_src[2], local_rank)
             log(f"[rank 0] end-to-end BAM -> VCF: {e2e['wall_s']:.2f}s, {e2e['value']:.4g} positions/s")
+            if e2e_indel_src is not None:
+                r = end_to_end(e2e_indel_src[0], e2e_indel_src[1], local_rank)
+                r["note"] += "; synthetic indels at rate 1e-4 per position (the indel realigner's regions replayed)"
+                e2e["indels"] = r
+                log(f"[rank 0] end-to-end with indels: {r['wall_s']:.2f}s, {r['value']:.4g} positions/s, "
+                    f"{r['realign_regions']} realigner regions replayed in {r['realign_replay_ms']:.1f} ms")
         except Exception as e:
             e2e = {"value": None, "error": str(e)}
         finally:

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define NGSEP_ABI_VERSION 9
+#define NGSEP_ABI_VERSION 10
 
 #define NGSEP_OK 0
 #define NGSEP_E_INVALID (-1)      /* bad argument / state */
@@ -203,6 +203,8 @@ typedef struct ngsep_stats {
     double  upload_ms;              /* host time of its H2D upload */
     int64_t carved_positions;       /* covered positions inside carved indel regions (not called here) */
     int64_t other_allele_calls;     /* entries of the scan's other-allele lists (valid non-reference calls) */
+    double  realign_ms;             /* ABI 10: host wall time of the indel realigner's region replays, summed */
+    int64_t realign_regions;        /* ABI 10: realigner regions replayed */
 } ngsep_stats;
 
 /* ---- -knownVariants (SingleSampleVariantsDetector.findSNVS :896-906, MultisampleVariantsDetector.run :432-438) ---- */

@@ -9,6 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+ABI_VERSION = 10                                   # NGSEP_ABI_VERSION (include/ngsep_gpu.h)
 LIB_PATH = os.environ.get("NGSEP_LIB_PATH") or os.path.join(_HERE, "lib", "libngsep_amd.so")   # override: tuning builds only
 
 NGSEP_OK = 0
@@ -146,6 +147,8 @@ class NgsepStats(ctypes.Structure):
         ("upload_ms", ctypes.c_double),
         ("carved_positions", ctypes.c_int64),
         ("other_allele_calls", ctypes.c_int64),
+        ("realign_ms", ctypes.c_double),         # ABI 10
+        ("realign_regions", ctypes.c_int64),
     ]
 
 
@@ -226,6 +229,8 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.ngsep_abi_version() != ABI_VERSION:     # the structures above are this ABI's (include/ngsep_gpu.h)
+        raise RuntimeError(f"{LIB_PATH} implements ABI {lib.ngsep_abi_version()}, this package ABI {ABI_VERSION}: rebuild it")
     _lib = lib
     return lib
 

@@ -599,18 +599,27 @@ static void keep_raw(ngsep_ctx* c, size_t b0, size_t n, const int32_t* ent, cons
         if (covered(e.first, e.last)) e.maybe = false;
         else if ((int64_t)e.last + R < frontier) { e.maybe = false; e.dead = true; }
     }
+    // the reads to keep (serial: cheap decisions), then their raw alignments copied on all host threads
+    const size_t k0 = st.kept.size();
+    std::vector<size_t> src;
     for (size_t i = 0; i < n; i++) {
         const int32_t f = cr.first[b0 + i], l = cr.last[b0 + i];
         const bool cov = covered(f, l);
         const bool maybe = !cov && (int64_t)l + R >= frontier;
         if (!cov && !maybe) continue;
-        const ReadView r = ent[i] >= 0 ? batch_view(c->cur_batch, ent[i]) : carried[-1 - ent[i]];
         std::remove_reference_t<decltype(st.kept)>::value_type e;
         e.first = f;
         e.last = l;
         e.maybe = maybe;
         e.dead = false;
-        RawRead& rr = e.r;
+        st.kept.push_back(std::move(e));
+        src.push_back(i);
+    }
+    parallel_for((int64_t)src.size(), 512, [&](int64_t q0, int64_t q1) {
+      for (int64_t q = q0; q < q1; q++) {
+        const size_t i = src[(size_t)q];
+        const ReadView r = ent[i] >= 0 ? batch_view(c->cur_batch, ent[i]) : carried[-1 - ent[i]];
+        RawRead& rr = st.kept[k0 + (size_t)q].r;
         rr.first = r.first;
         rr.last = r.last;
         rr.flags = r.flags;
@@ -634,8 +643,8 @@ static void keep_raw(ngsep_ctx* c, size_t b0, size_t n, const int32_t* ent, cons
             rr.sample = (int16_t)(in ? c->rg_sample[(size_t)r.rg] : -1);
             rr.rank = (uint8_t)(in && c->rg_sample[(size_t)r.rg] >= 0 ? c->rg_rank[(size_t)r.rg] : 0);
         }
-        st.kept.push_back(std::move(e));
-    }
+      }
+    });
     while (st.kept_maybe_from < st.kept.size() && !st.kept[st.kept_maybe_from].maybe) st.kept_maybe_from++;
     if (!streaming(c)) {
         // a whole sequence is kept until its end (multisample): the reads no region can reach leave as they die
@@ -703,6 +712,23 @@ static int flush_sequence(ngsep_ctx* c) {
     return rc;
 }
 
+// The reach the replay needs for one realigner event [y1, y2] (an indel read's [first, last + indel bases], or an input
+// variant's span): IndelRealignerPileupListener realigns the alignments of the pileups at the event's positions
+// (conciliateIndels, moveIndelStarts) and writes the event's record there, so the calls it can change lie inside the
+// extents of the admitted alignments that overlap [y1, y2], and DEF_REGION_BOUNDARY (:43) around them.  (carved
+// regions handed back keep the coarser [y1 - R, y2 + R].)  Every alignment this reach needs was admitted before
+// the frontier passed y2, and an alignment keep_raw dropped ends before frontier - R at the time, which is before
+// every later event's reach -- a reach drawn with a span admitted after that drop would not be (the streamed
+// chr20-with-indels run lacked two alignments of such a region).
+static std::pair<int64_t, int64_t> event_reach(const ContigReads& cr, int64_t y1, int64_t y2, int64_t len) {
+    int64_t L = y1, M = y2;
+    const int64_t ms = std::max<int32_t>(1, cr.max_span);
+    size_t i = (size_t)(std::lower_bound(cr.first.begin(), cr.first.end(), (int32_t)std::max<int64_t>(INT32_MIN, y1 - ms + 1)) - cr.first.begin());
+    for (; i < cr.first.size() && (int64_t)cr.first[i] <= y2; i++)
+        if ((int64_t)cr.last[i] >= y1) { L = std::min<int64_t>(L, cr.first[i]); M = std::max<int64_t>(M, cr.last[i]); }
+    return {std::max<int64_t>(1, L - 100), std::min<int64_t>(len, M + 100)};
+}
+
 // IndelRealignerPileupListener's reach (ngsep_gpu.h ngsep_fetch_carved_regions): every indel-bearing
 // admitted alignment carves [first - R, last + indel bases + R], R = max span + 100 (DEF_REGION_BOUNDARY,
 // IndelRealignerPileupListener.java:43), merged; the covered positions inside leave the genotyped count
@@ -712,7 +738,9 @@ static void carve_indel_regions(ngsep_ctx* c, ContigReads& cr) {
     const int64_t R = (int64_t)cr.max_span + 100;
     const int64_t len = (int64_t)c->seq_bases[(size_t)cr.seq_id].size();
     std::vector<std::pair<int64_t, int64_t>> iv;
-    for (const auto& x : cr.indel_reads) iv.push_back({std::max<int64_t>(1, x.first - R), std::min<int64_t>(len, (int64_t)x.second + R)});
+    for (const auto& x : cr.indel_reads)
+        iv.push_back(replay ? event_reach(cr, x.first, x.second, len)        // (replayed here: the reach the replay needs)
+                            : std::pair<int64_t, int64_t>{std::max<int64_t>(1, x.first - R), std::min<int64_t>(len, (int64_t)x.second + R)});
     std::sort(iv.begin(), iv.end());
     for (const auto& x : iv) {
         if (x.first > x.second) continue;
@@ -869,8 +897,14 @@ static void stream_launch(ngsep_ctx* c, int64_t w0, int64_t w1) {
         const int64_t R = (int64_t)cr.max_span + 100;
         while (st.indel_lo < cr.indel_reads.size() && (int64_t)cr.indel_reads[st.indel_lo].second + R < w0) st.indel_lo++;
         std::vector<std::pair<int64_t, int64_t>> whole;
+        const bool tight = realign_active(c);             // replayed here: event_reach (carved regions: [y1 - R, y2 + R])
         for (size_t k = st.indel_lo; k < cr.indel_reads.size() && (int64_t)cr.indel_reads[k].first - R <= w1; k++) {
-            const int64_t a = std::max<int64_t>(1, cr.indel_reads[k].first - R), b = std::min<int64_t>(len, (int64_t)cr.indel_reads[k].second + R);
+            int64_t a = std::max<int64_t>(1, cr.indel_reads[k].first - R), b = std::min<int64_t>(len, (int64_t)cr.indel_reads[k].second + R);
+            if (tight) {
+                const auto r = event_reach(cr, cr.indel_reads[k].first, cr.indel_reads[k].second, len);
+                a = r.first;
+                b = r.second;
+            }
             if (a > b) continue;
             whole.push_back({a, b});
             if (std::max(a, w0) <= std::min(b, w1)) cut.push_back({std::max(a, w0), std::min(b, w1)});
@@ -919,10 +953,16 @@ static void stream_launch(ngsep_ctx* c, int64_t w0, int64_t w1) {
         region_reads.resize(cut.size());
         for (size_t k = 0; k < cut.size(); k++) {
             const int64_t a = cut[k].first, b = cut[k].second;
-            for (const auto& e : st.kept)
-                if (!e.dead && e.first <= b && e.last >= a) region_reads[k].push_back(e.r);
+            // (kept entries and admitted reads are in start order: only those starting in [a - max span + 1, b] can
+            // overlap the region)
+            const int64_t from = std::max<int64_t>(INT32_MIN, a - max_span + 1);
+            auto it = std::lower_bound(st.kept.begin(), st.kept.end(), from,
+                                       [](const auto& e, int64_t v) { return (int64_t)e.first < v; });
+            for (; it != st.kept.end() && (int64_t)it->first <= b; ++it)
+                if (!it->dead && it->last >= a) region_reads[k].push_back(it->r);
             size_t want = 0;
-            for (int64_t i = lo; i < hi && cr.first[(size_t)i] <= b; i++) want += cr.last[(size_t)i] >= a ? 1 : 0;
+            const int64_t i0 = std::max<int64_t>(lo, std::lower_bound(cr.first.begin(), cr.first.end(), (int32_t)from) - cr.first.begin());
+            for (int64_t i = i0; i < hi && cr.first[(size_t)i] <= b; i++) want += cr.last[(size_t)i] >= a ? 1 : 0;
             if (want != region_reads[k].size())
                 region_err = "internal error: indel realigner region " + std::to_string(a) + "-" + std::to_string(b) + " lacks " +
                              std::to_string((int64_t)want - (int64_t)region_reads[k].size()) + " alignments";
@@ -2219,12 +2259,15 @@ static int run_regions(ngsep_ctx* c, WindowJob* j, int64_t goff) {
     rp.ignore_lowercase = c->params.ignore_lowercase_ref != 0;
     const bool known = !c->known.empty();
     rp.known = known;
+    const auto t_rp = std::chrono::steady_clock::now();
     parallel_for((int64_t)nr, 1, [&](int64_t a, int64_t b) {
         for (int64_t k = a; k < b; k++)
             replay_region(seq, j->carved[(size_t)k].first, j->carved[(size_t)k].second, j->region_reads[(size_t)k], rp,
                           (size_t)j->seq_id < c->strs.size() ? &c->strs[(size_t)j->seq_id] : nullptr, &c->known_recs,
                           outs[(size_t)k]);
     });
+    c->realign_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_rp).count();
+    c->realign_regions += (int64_t)nr;
     // KP's queue: {global position, reference code, column offset / 4, entries} per callable position
     Staged& s = c->staged;
     s.known = true;
@@ -2383,12 +2426,15 @@ static int run_population_regions(ngsep_ctx* c, const ContigReads& cr, size_t fr
     rp.n_samples = S;
     const bool known = !c->known.empty();
     rp.known = known;
+    const auto t_rp = std::chrono::steady_clock::now();
     parallel_for((int64_t)nr, 1, [&](int64_t a, int64_t b) {
         for (int64_t k = a; k < b; k++)
             replay_region(seq, cr.carved[(size_t)k].first, cr.carved[(size_t)k].second, reads[(size_t)k], rp,
                           (size_t)cr.seq_id < c->strs.size() ? &c->strs[(size_t)cr.seq_id] : nullptr, &c->known_recs,
                           outs[(size_t)k]);
     });
+    c->realign_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_rp).count();
+    c->realign_regions += (int64_t)nr;
     // KPM over the regions' positions: position v of the queue is virtual position v of a layout of its own (tiles of
     // kPopTile positions, site-major columns as build_multi_layout lays them out), discovery mode (no input alleles);
     // with -knownVariants one virtual position per input SNV at a region position with a pileup (its alleles given)
@@ -3002,6 +3048,8 @@ extern "C" const char* ngsep_last_error(ngsep_ctx* c) { return c ? c->err.c_str(
 extern "C" int ngsep_get_stats(ngsep_ctx* c, ngsep_stats* out) {
     if (!c || !out) return NGSEP_E_INVALID;
     *out = c->stats;
+    out->realign_ms = (double)c->realign_ns.load() * 1e-6;
+    out->realign_regions = c->realign_regions.load();
     return NGSEP_OK;
 }
 

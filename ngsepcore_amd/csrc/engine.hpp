@@ -779,6 +779,7 @@ struct ngsep_ctx {
                                                         // (an indel / STR record, multisnv_type 3: pop_text[pop_order[i]])
     std::vector<std::string> pop_text;                  // indel / STR population records (realigner regions), no sequence name
     ngsep_stats stats{};
+    std::atomic<int64_t> realign_ns{0}, realign_regions{0};   // region replays (worker threads): stats.realign_*
 };
 
 namespace ngsep {
