@@ -1634,28 +1634,48 @@ static_assert(kPopThreads >= kMaxSamplesDevice, "one thread per sample");
 
 struct PopCall {
     int kind, n_called, c0, c1, gq, total_cn;
-    int acn[4];
+    // copy numbers of alleles 0-3, four 16-bit fields of one register pair (indexed fields, even as separate
+    // scalars, were folded into an indexed load and kept the struct in scratch); a field never goes below 0
+    uint64_t acnp;
+    __device__ __forceinline__ int acn(int j) const { return (int)(int16_t)(uint16_t)(acnp >> (16 * j)); }
+    __device__ __forceinline__ void add_acn(int j, int v) { acnp += (uint64_t)(int64_t)v << (16 * j); }
+    __device__ __forceinline__ void set_acn(int j, int v) {
+        acnp = (acnp & ~(0xFFFFull << (16 * j))) | ((uint64_t)(uint16_t)v << (16 * j));
+    }
+    __device__ __forceinline__ void clear_acn() { acnp = 0; }
 };
 
 __device__ inline int tri_d(int i, int j) {      // upper-triangle index of L[i][j] (symmetric, f == g)
     const int a = i < j ? i : j, b = i < j ? j : i;
     return (a == 0 ? 0 : a == 1 ? 4 : a == 2 ? 7 : 9) + (b - a);
 }
-__device__ inline double sel10(const double* L, int k) {
+// a thread's ten log-conditionals kept in LDS (column-major, conflict-free) once its tally is done: KPM's genotyping and
+// PL phases read them from there, so the 20 VGPRs they held are free for the fp64 posterior (the 4-wave build spilled)
+struct LdsRow {
+    const double* p;
+    __device__ double operator[](int k) const { return p[k * kPopThreads]; }
+};
+template <class LA>
+__device__ inline double sel10(const LA& L, int k) {
     double v = 0;
 #pragma unroll
     for (int e = 0; e < 10; e++) v = e == k ? L[e] : v;
     return v;
 }
-__device__ inline int sel4i(const int* a, int k) {
-    int v = 0;
-#pragma unroll
-    for (int e = 0; e < 4; e++) v = e == k ? a[e] : v;
-    return v;
+// element k of a 4-entry register array (static indexes only: a dynamic one sends the array to scratch)
+// (written without loops: SROA runs before the unroller, and a loop index there keeps the array in scratch)
+__device__ __forceinline__ void set4i(int* a, int k, int v) {
+    if (k == 0) a[0] = v;
+    else if (k == 1) a[1] = v;
+    else if (k == 2) a[2] = v;
+    else a[3] = v;
+}
+__device__ __forceinline__ int sel4i(const int* a, int k) {
+    return k == 0 ? a[0] : k == 1 ? a[1] : k == 2 ? a[2] : a[3];
 }
 
 // CalledSNV.updateAllelesCopyNumberFromCounts (variants/CalledSNV.java:134-158)
-__device__ inline void csnv_cn(int genotype, int cref, int calt, int total, int* tot_out, int* ref_out) {
+__device__ __forceinline__ void csnv_cn(int genotype, int cref, int calt, int total, int* tot_out, int* ref_out) {
     int ref = 0;
     if (genotype == -1) { *tot_out = total; *ref_out = 0; return; }
     if (genotype == 0) ref = total;
@@ -1673,29 +1693,35 @@ __device__ inline void csnv_cn(int genotype, int cref, int calt, int total, int*
     *ref_out = ref;
 }
 // CalledGenomicVariantImpl.updateAllelesCopyNumberFromCounts (variants/CalledGenomicVariantImpl.java:228-282)
-__device__ inline void cgv_cn(PopCall& c, int total, const int* rcounts, bool report) {
+__device__ __forceinline__ void cgv_cn(PopCall& c, int total, const int* rcounts, bool report) {
     c.total_cn = total;
-    c.acn[0] = c.acn[1] = c.acn[2] = c.acn[3] = 0;
+    c.clear_acn();
     if (c.n_called == 0) return;
     const int called[2] = {c.c0, c.c1};
-    if (c.n_called == 1 && c.c0 == 0) { c.acn[0] = total; return; }
+    if (c.n_called == 1 && c.c0 == 0) { c.set_acn(0, total); return; }
     const int nc = c.n_called;
-    auto addcn = [&](int j, int v) {
+    auto addcn = [&](int j, int v) { c.add_acn(j, v); };
+    auto getcn = [&](int j) -> int { return c.acn(j); };
+    // (loops over the at most two called alleles unrolled: static indexes)
+    if (total <= nc) {
 #pragma unroll
-        for (int e = 0; e < 4; e++) if (e == j) c.acn[e] += v;
-    };
-    auto getcn = [&](int j) -> int { return sel4i(c.acn, j); };
-    if (total <= nc) { for (int i = 0; i < nc; i++) addcn(called[i], 1); return; }
+        for (int i = 0; i < 2; i++) if (i < nc) addcn(called[i], 1);
+        return;
+    }
     if (!report) {
         const int def = total / nc;
-        for (int i = 0; i < nc; i++) addcn(called[i], def);
+#pragma unroll
+        for (int i = 0; i < 2; i++) if (i < nc) addcn(called[i], def);
         addcn(called[0], total - def * nc);
         return;
     }
     int rc[2] = {0, 0}, tr = 0;
-    for (int i = 0; i < nc; i++) { rc[i] = sel4i(rcounts, called[i]); if (rc[i] == 0) rc[i] = 1; tr += rc[i]; }
+#pragma unroll
+    for (int i = 0; i < 2; i++) if (i < nc) { rc[i] = sel4i(rcounts, called[i]); if (rc[i] == 0) rc[i] = 1; tr += rc[i]; }
     int tc = 0;
-    for (int i = 0; i < nc; i++) {
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        if (i >= nc) continue;
         const long long r = java_round_d((double)total * rc[i] / tr);
         const int v = (int)(r > 1 ? r : 1);
         addcn(called[i], v - getcn(called[i]));
@@ -1704,7 +1730,9 @@ __device__ inline void cgv_cn(PopCall& c, int total, const int* rcounts, bool re
     if (tc < total) addcn(called[0], total - tc);
     else {
         int ex = tc - total;
-        for (int i = nc - 1; ex > 0 && i >= 0; i--) {
+#pragma unroll
+        for (int i = 1; i >= 0; i--) {                     // i = nc - 1 .. 0 while ex > 0
+            if (i >= nc || ex <= 0) continue;
             const int cur = getcn(called[i]);
             const int rm = ex < cur - 1 ? ex : cur - 1;
             addcn(called[i], -rm);
@@ -1714,11 +1742,12 @@ __device__ inline void cgv_cn(PopCall& c, int total, const int* rcounts, bool re
 }
 
 // genotypeVariantSample with a fresh listener (minQuality = DEF_MIN_QUALITY 40) + genotypeSNV
-__device__ PopCall genotype_sample_d(const double* L, const int* cnt, int total, int nal, const int* idx,
+template <class LA>
+__device__ __forceinline__ PopCall genotype_sample_d(const LA& L, const int* cnt, int total, int nal, const int* idx,
                                      const GenotypeParams& gp, int ploidy) {
     PopCall c;
     c.kind = 1; c.n_called = 0; c.c0 = 0; c.c1 = 0; c.gq = 0; c.total_cn = ploidy;
-    c.acn[0] = c.acn[1] = c.acn[2] = c.acn[3] = 0;
+    c.clear_acn();
     if (total == 0) return c;                   // undecided CalledGenomicVariantImpl(variant, new byte[0])
     const double ph = gp.log_prior_homo, px = gp.log_prior_hetero;
     if (nal == 2) {
@@ -1776,8 +1805,9 @@ __device__ PopCall genotype_sample_d(const double* L, const int* cnt, int total,
         else if (genotype == 0) { c.n_called = 1; c.c0 = 0; }
         else if (genotype == 2) { c.n_called = 1; c.c0 = 1; }
         else { c.n_called = 2; c.c0 = 0; c.c1 = 1; }
-        c.acn[0] = genotype == -1 ? 0 : ref;
-        c.acn[1] = genotype == -1 ? 0 : tot - ref;
+        c.clear_acn();
+        c.set_acn(0, genotype == -1 ? 0 : ref);
+        c.set_acn(1, genotype == -1 ? 0 : tot - ref);
         return c;
     }
     double ev[16] = {L[0] + ph, L[1] + px, L[2] + px, L[3] + px,
@@ -1825,22 +1855,27 @@ __device__ PopCall genotype_sample_d(const double* L, const int* cnt, int total,
         else if (genotype == 0) { c.n_called = 1; c.c0 = 0; }
         else if (genotype == 2) { c.n_called = 1; c.c0 = 1; }
         else { c.n_called = 2; c.c0 = 0; c.c1 = 1; }
-        c.acn[0] = genotype == -1 ? 0 : ref;
-        c.acn[1] = genotype == -1 ? 0 : tot - ref;
+        c.clear_acn();
+        c.set_acn(0, genotype == -1 ? 0 : ref);
+        c.set_acn(1, genotype == -1 ? 0 : tot - ref);
         return c;
     }
     int rcounts[4] = {0, 0, 0, 0};
-    for (int i = 0; i < nal; i++) rcounts[i] = sel4i(cnt, idx[i]);
+#pragma unroll
+    for (int i = 0; i < 4; i++) rcounts[i] = i < nal ? sel4i(cnt, idx[i]) : 0;
     int bi = 0, bj = 0;                                       // getIndexesMaxGenotype(report, 0)
     double probMax = post(idx[0], idx[0]);
-    for (int i = 0; i < nal; i++)
-        for (int j = i; j < nal; j++) {
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (!(i < nal && j >= i && j < nal)) continue;
             double g = post(idx[i], idx[j]);
             if (i != j) g += post(idx[j], idx[i]);
             if (g > probMax + 0.01) { probMax = g; bi = i; bj = j; }
         }
-    double maxP = post(idx[bi], idx[bj]);
-    if (bi != bj) { maxP += post(idx[bj], idx[bi]); c.n_called = 2; c.c0 = bi; c.c1 = bj; }
+    double maxP = post(sel4i(idx, bi), sel4i(idx, bj));
+    if (bi != bj) { maxP += post(sel4i(idx, bj), sel4i(idx, bi)); c.n_called = 2; c.c0 = bi; c.c1 = bj; }
     else { c.n_called = 1; c.c0 = bi; }
     c.gq = phred_d(1 - maxP);
     c.kind = 1;
@@ -1929,6 +1964,7 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
     };
     stamp(0);
     __shared__ double s_t[3][32];
+    __shared__ double s_L[10][kPopThreads];             // each thread's log-conditionals after its tally (LdsRow)
     __shared__ int32_t s_pc[4], s_tot;
     __shared__ int32_t s_called, s_qs;
     __shared__ unsigned long long s_base;
@@ -1978,7 +2014,7 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
         const uint8_t* col = col_next;
         if (GATHER == 1 && tid <= n_samples) {
             uint8_t* dst = s_gcol + (int64_t)tid * pg.stride;
-            rows = pop_gather<16>(pg, gpos, tid, dst, pg.stride);
+            rows = pop_gather<8>(pg, gpos, tid, dst, pg.stride);
             if (rows > pg.stride) {                          // (the host's coverage bound makes this unreachable)
                 atomicOr(&counters[3], 1ull << 63);
                 rows = pg.stride;
@@ -2016,6 +2052,10 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
             }
         }
         if (i == blockIdx.x) stamp(1);
+#pragma unroll
+        for (int k = 0; k < 10; k++) s_L[k][tid] = L[k];
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);             // (read back from LDS below: the registers are released)
+        const LdsRow Lr{&s_L[0][tid]};
         if (GATHER != 1 && inext < n) column_of(inext, qs_next.gpos, rows_next, col_next);   // (in flight during the genotyping)
         // pooled counts: the sum over every sample and the reads of no sample
         {
@@ -2052,7 +2092,7 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
             nal = 2;
         } else {
             for (int a = 0; a < 4; a++)
-                if (a != refIdx && pc[a] >= minCount) { idx[nal < 4 ? nal : 3] = a; nal++; }
+                if (a != refIdx && pc[a] >= minCount) { set4i(idx, nal < 4 ? nal : 3, a); nal++; }
         }
         if (nal < 2) continue;
         int multisnv = nal > 2;
@@ -2069,21 +2109,20 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
                 pr = pool_genotype(col, rows, total, cnt, idx, nal, pt, gp.max_q);
                 call.kind = 1; call.n_called = pr.n_called; call.c0 = pr.c0 < 0 ? 0 : pr.c0; call.c1 = pr.c1 < 0 ? 0 : pr.c1;
                 call.gq = pr.gq; call.total_cn = ploidy;
-#pragma unroll
-                for (int k = 0; k < 4; k++) call.acn[k] = pr.acn[k];
+                call.clear_acn();
+                call.set_acn(0, pr.acn[0]); call.set_acn(1, pr.acn[1]); call.set_acn(2, pr.acn[2]); call.set_acn(3, pr.acn[3]);
                 if (40 > call.gq) {
                     call.n_called = 0; call.gq = 0;
-#pragma unroll
-                    for (int k = 0; k < 4; k++) call.acn[k] = 0;
+                    call.clear_acn();
                 }
             }
             if (tid < n_samples) {
-                if (!pool) call = genotype_sample_d(L, cnt, total, nal, idx, gp, ploidy);
+                if (!pool) call = genotype_sample_d(Lr, cnt, total, nal, idx, gp, ploidy);
                 const bool homref = call.n_called == 1 && call.c0 == 0;
                 if (call.n_called > 0 && !homref) atomicMax(&s_qs, call.gq);
                 int bits = 0;
-                if (call.n_called >= 1) bits |= 1 << idx[call.c0 & 3];
-                if (call.n_called == 2) bits |= 1 << idx[call.c1 & 3];
+                if (call.n_called >= 1) bits |= 1 << sel4i(idx, call.c0 & 3);
+                if (call.n_called == 2) bits |= 1 << sel4i(idx, call.c1 & 3);
                 if (bits) atomicOr(&s_called, bits);
             }
             __syncthreads();
@@ -2093,7 +2132,7 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
             if (nal <= 2) break;
             if (__popc(set) == nal) break;
             nal = 1;
-            for (int a = 0; a < 4; a++) if (a != refIdx && (set >> a & 1)) idx[nal++] = a;
+            for (int a = 0; a < 4; a++) if (a != refIdx && (set >> a & 1)) { set4i(idx, nal, a); nal++; }
             multisnv = 0;                                          // makeNewVariant: SNV or GenomicVariantImpl (no TYPE)
             if (nal < 2) break;
         }
@@ -2124,8 +2163,8 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
             o[2] = (uint32_t)(pool ? pr.dp : total);
 #pragma unroll
             for (int k = 0; k < 4; k++) o[3 + k] = (uint32_t)cnt[k];
-            o[7] = (uint32_t)(uint16_t)call.acn[0] | (uint32_t)(uint16_t)call.acn[1] << 16;
-            o[8] = (uint32_t)(uint16_t)call.acn[2] | (uint32_t)(uint16_t)call.acn[3] << 16;
+            o[7] = (uint32_t)call.acnp;                              // (int16 acn[0], acn[1])
+            o[8] = (uint32_t)(call.acnp >> 32);                      // (acn[2], acn[3])
             uint32_t* pl = o + 9;
             int npl = 0;                                           // PL values written (the rest are 0)
             // PL (VCFFileWriter.java:200-212) from the call report
@@ -2136,8 +2175,8 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
                             pl[npl++] = (uint32_t)(int32_t)java_round_d(-10 * sel10(pr.L, ii * nal - ii * (ii - 1) / 2 + (j - ii)));
                 }
             } else if (call.kind == 0) {
-                const float hr = (float)sel10(L, tri_d(idx[0], idx[0])), ha = (float)sel10(L, tri_d(idx[1], idx[1]));
-                const float ra = (float)sel10(L, tri_d(idx[0], idx[1])), ar = ra;
+                const float hr = (float)sel10(Lr, tri_d(idx[0], idx[0])), ha = (float)sel10(Lr, tri_d(idx[1], idx[1]));
+                const float ra = (float)sel10(Lr, tri_d(idx[0], idx[1])), ar = ra;
                 const bool present = (hr + ra + ar + ha) != 0;     // CalledSNV.java:422 (float sum)
                 if (present) {
                     pl[0] = (uint32_t)(int32_t)java_round_d(-10 * (double)hr);
@@ -2148,7 +2187,7 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
             } else if (total > 0) {
                 for (int j = 0; j < nal; j++)
                     for (int ii = 0; ii <= j; ii++)
-                        pl[npl++] = (uint32_t)(int32_t)java_round_d(-10 * sel10(L, tri_d(idx[ii], idx[j])));
+                        pl[npl++] = (uint32_t)(int32_t)java_round_d(-10 * sel10(Lr, tri_d(sel4i(idx, ii), sel4i(idx, j))));
             }
             for (int k = npl; k < 10; k++) pl[k] = 0u;
         }
@@ -3197,9 +3236,14 @@ int device_run_rac(Device* d, const Staged& s, int64_t g0, int64_t g1, int32_t m
     return 0;
 }
 
-// KPM's variant and grid: registers capped for 4 waves per SIMD (145 -> 128 VGPRs; a few spill) and 16384
-// workgroups looping over the queue (measured on configs[4]: 235 -> 204 us against 3 waves and 2048 workgroups)
-constexpr int kKpmWavesPerEu = 4;
+// KPM's variant and grid: 3 waves per SIMD -- 139 VGPRs, no scratch at all (round 4: the log-conditionals read back
+// from LDS, the biallelic posterior without its 16-entry array, the copy numbers in one register pair, static indexes
+// only); the 4-wave build spills 10 VGPRs, which wrote 113 MB per configs[4] launch against 45 MB at 3 waves for
+// the same time (`tools/gpu_r4_kpmab.sh`) -- and 16384 workgroups looping over the queue
+#ifndef NGSEP_KPM_WPE                          // (build-time override: A/B builds only)
+#define NGSEP_KPM_WPE 3
+#endif
+constexpr int kKpmWavesPerEu = NGSEP_KPM_WPE;
 constexpr unsigned kKpmGrid = 16384;
 static auto kpm_kernel(int ploidy, int gather) {
     if (gather == 1) return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, 1> : k_posterior_multi<false, kKpmWavesPerEu, 1>;
