@@ -265,3 +265,36 @@ def test_population_known_indels(tmp_path, kw, opts):
     det.run(bams).close()
     d = diff_vcf(o, det.outFilename)
     assert not d, "\n".join(d[:20])
+
+
+def test_population_read_groups_of_samples(tmp_path):
+    """Samples with several read groups and reads of no sample (round 4's population layout: one stream per
+    (sample, read-group rank), the reads of no sample in the last stream, pooled counts only).  The SAM header maps
+    read groups S000-S009 two by two to samples P0-P4 (their calls in HashSet order of the group ids,
+    PileupRecord.getAlleleCalls(span, readGroups) :104-111), S010 to P5, and lists no S011: its reads enter the
+    pooled counts of every position but no sample."""
+    syn, fa, sam, _ = population(tmp_path, genome=pysynth.CUSTOM, custom_len=30000, seed=9, n_samples=12,
+                                 depth=8, snv_rate=3e-3)
+    sm = {f"S{k:03d}": f"P{k // 2}" for k in range(10)}
+    sm["S010"] = "P5"
+    lines = []
+    for l in open(sam):
+        if l.startswith("@RG"):
+            rid = l.split("\t")[1][3:]
+            if rid not in sm:
+                continue
+            l = f"@RG\tID:{rid}\tSM:{sm[rid]}\n"
+        lines.append(l)
+    sam2 = os.path.join(str(tmp_path), "pop_rg.sam")
+    with open(sam2, "w") as f:
+        f.writelines(lines)
+    rgs = [(f"S{k:03d}", sm.get(f"S{k:03d}")) for k in range(12)]
+    o = oracle_mvd(tmp_path, fa, sam2)
+    for staged in (False, True):
+        g, st = gpu_mvd(tmp_path, syn, rgs, staged=staged)
+        d = diff_vcf(o, g)
+        assert not d, "\n".join(d[:20])
+    assert n_records(o) > 10
+    assert sum(1 for l in open(o) if l.startswith("#CHROM"))  # (header present)
+    hdr = [l for l in open(o) if l.startswith("#CHROM")][0].rstrip("\n").split("\t")
+    assert hdr[9:] == [f"P{k}" for k in range(6)]
