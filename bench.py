@@ -380,7 +380,7 @@ def main():
         names = [n for n, _ in syn.contigs()]
         workload = (f"MultisampleVariantsDetector: {args.samples} synthetic yeast samples at {args.depth:g}x, "
                     f"shard {'+'.join(names)} (one GPU's contig shard of the 8-GPU split)")
-        workload_key = f"multisample{args.samples}:{args.depth:g}x:contig{args.contig_first}:v2"
+        workload_key = f"multisample{args.samples}:{args.depth:g}x:contig{args.contig_first}:v3"
         sources = [syn]
     elif args.config == "yeast":
         sources = [pysynth.Synth(genome=pysynth.YEAST, depth=args.depth, seed=2 + rank)]

@@ -298,3 +298,16 @@ def test_population_read_groups_of_samples(tmp_path):
     assert sum(1 for l in open(o) if l.startswith("#CHROM"))  # (header present)
     hdr = [l for l in open(o) if l.startswith("#CHROM")][0].rstrip("\n").split("\t")
     assert hdr[9:] == [f"P{k}" for k in range(6)]
+
+
+@pytest.mark.parametrize("window", [5000, 12345])
+def test_population_window_sizes(tmp_path, window):
+    """Windows cut the population run's coordinate (each window's reads laid out again with a halo of the read span,
+    KLM's sample tiles and KPM's gathers crossing window and halo boundaries): the VCF is the whole run's."""
+    syn, fa, sam, rgs = population(tmp_path, genome=pysynth.CUSTOM, custom_len=40000, seed=11, n_samples=24, depth=8,
+                                   snv_rate=3e-3)
+    o = oracle_mvd(tmp_path, fa, sam)
+    g, st = gpu_mvd(tmp_path, syn, rgs, window_positions=window)
+    d = diff_vcf(o, g)
+    assert not d, "\n".join(d[:20])
+    assert n_records(o) > 20
