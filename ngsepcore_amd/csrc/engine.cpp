@@ -958,8 +958,14 @@ static void stream_launch(ngsep_ctx* c, int64_t w0, int64_t w1) {
             const int64_t from = std::max<int64_t>(INT32_MIN, a - max_span + 1);
             auto it = std::lower_bound(st.kept.begin(), st.kept.end(), from,
                                        [](const auto& e, int64_t v) { return (int64_t)e.first < v; });
-            for (; it != st.kept.end() && (int64_t)it->first <= b; ++it)
-                if (!it->dead && it->last >= a) region_reads[k].push_back(it->r);
+            for (; it != st.kept.end() && (int64_t)it->first <= b; ++it) {
+                if (it->dead || it->last < a) continue;
+                // moved when no later region and no later window reads it (it ends in this window, before the next
+                // region): the kept list drops it below; copied otherwise
+                const bool last_use = it->last <= w1 && (k + 1 == cut.size() || (int64_t)it->last < cut[k + 1].first);
+                if (last_use) region_reads[k].push_back(std::move(it->r));
+                else region_reads[k].push_back(it->r);
+            }
             size_t want = 0;
             const int64_t i0 = std::max<int64_t>(lo, std::lower_bound(cr.first.begin(), cr.first.end(), (int32_t)from) - cr.first.begin());
             for (int64_t i = i0; i < hi && cr.first[(size_t)i] <= b; i++) want += cr.last[(size_t)i] >= a ? 1 : 0;
