@@ -311,3 +311,21 @@ def test_population_window_sizes(tmp_path, window):
     d = diff_vcf(o, g)
     assert not d, "\n".join(d[:20])
     assert n_records(o) > 20
+
+
+def test_population_sample_without_reads(tmp_path):
+    """A sample of the header with no alignment at all (no stream in the population layout): every site genotypes
+    it undecided with empty counts, as the reference does."""
+    syn, fa, sam, rgs = population(tmp_path, genome=pysynth.CUSTOM, custom_len=20000, seed=12, n_samples=8, depth=10,
+                                   snv_rate=3e-3)
+    lines = open(sam).readlines()
+    last_rg = max(i for i, l in enumerate(lines) if l.startswith("@RG"))
+    lines.insert(last_rg + 1, "@RG\tID:SX00\tSM:S004a\n")     # sorts between S004 and S005
+    sam2 = os.path.join(str(tmp_path), "pop_empty.sam")
+    with open(sam2, "w") as f:
+        f.writelines(lines)
+    o = oracle_mvd(tmp_path, fa, sam2)
+    g, st = gpu_mvd(tmp_path, syn, rgs + [("SX00", "S004a")])
+    d = diff_vcf(o, g)
+    assert not d, "\n".join(d[:20])
+    assert n_records(o) > 10
