@@ -85,7 +85,8 @@ constexpr int kMcMaxCalls = 254;           // multisample candidate column: vali
 #endif
 constexpr int kKlmTile = NGSEP_KLM_TILE;   // positions per KLM sample tile (one wavefront each; divides kRunAlign)
 constexpr int kKlmSlots = NGSEP_KLM_SLOTS; // KLM: candidate columns a sample tile bounds in LDS (more: kept open)
-constexpr int kPopGatherCap = 61440;       // KPM (gather): LDS bytes for one position's columns ((S + 1) x the per-sample bound)
+constexpr int kPopGatherCap = 40960;       // KPM (gather): LDS bytes for one position's columns ((S + 1) x the per-sample bound);
+                                           // with KPM's 21 KB of static LDS, within the 64 KB a workgroup is given
 
 // the (first) alternative allele of a record as a DNA index: a pool record keeps its variant's alleles in
 // the mask bits (ngsep_site_out.pool), an SNVQ record in .alt
