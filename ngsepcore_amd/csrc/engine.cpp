@@ -23,6 +23,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 #include <cstdlib>
+#include <emmintrin.h>
 #include <fstream>
 #include <functional>
 
@@ -1599,6 +1600,41 @@ static int build_single_layout(Staged& s, const HugeVec<SRead>& reads, LayoutAre
     return bad ? -1 : 0;
 }
 
+// One 64-read group of a read-group layout: unit k of lane l (the read's bytes 8k .. 8k+7, XOR-ed with the reference,
+// zero past its end) at dst[64 k + l].  Written one 64-byte line (8 lanes) at a time with streaming stores: a line
+// written whole needs no read-for-ownership, so the layout costs its bytes once instead of twice (span 0: an empty
+// lane).  The caller fences (_mm_sfence) before the layout is uploaded.
+static inline void fill_group_units(uint64_t* dst, int32_t K, const uint8_t* const* src, const uint8_t* const* rf,
+                                    const int64_t* span) {
+    for (int32_t k = 0; k < K; k++) {
+        const int64_t o = 8 * (int64_t)k;
+        for (int lb = 0; lb < 64; lb += 8) {
+            alignas(16) uint64_t line[8];
+            for (int l = lb; l < lb + 8; l++) {
+                uint64_t v = 0;
+                const int64_t sp = span[l];
+                if (o + 8 <= sp) {
+                    uint64_t u, w;
+                    std::memcpy(&u, src[l] + o, 8);
+                    std::memcpy(&w, rf[l] + o, 8);
+                    v = u ^ w;
+                } else if (o < sp) {
+                    uint8_t b8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                    for (int64_t t = 0; t < sp - o; t++) b8[t] = (uint8_t)(src[l][o + t] ^ rf[l][o + t]);
+                    std::memcpy(&v, b8, 8);
+                }
+                line[l - lb] = v;
+            }
+            __m128i* d = reinterpret_cast<__m128i*>(dst + o * 8 + lb);
+            const __m128i* q = reinterpret_cast<const __m128i*>(line);
+            _mm_stream_si128(d, _mm_load_si128(q));
+            _mm_stream_si128(d + 1, _mm_load_si128(q + 1));
+            _mm_stream_si128(d + 2, _mm_load_si128(q + 2));
+            _mm_stream_si128(d + 3, _mm_load_si128(q + 3));
+        }
+    }
+}
+
 // Read-group layout (engine.hpp RGroup): the variant caller's device input.  The reads'
 // projected bytes are the ones the host packer produced (one code byte per reference position of the read,
 // pending-list order), stored relative to the reference (code ^ reference code, as CRAM stores bases against the
@@ -1637,15 +1673,18 @@ static int build_rg_layout(Staged& s, const HugeVec<SRead>& reads, LayoutArena& 
     const int32_t last_first = n ? reads[(size_t)n - 1].gfirst : 1;
     uint64_t* units = s.h_units;
     parallel_for(ng, 64, [&](int64_t g0, int64_t g1) {
+        const uint8_t* src[64];
+        const uint8_t* rfs[64];
+        int64_t spans[64];
         for (int64_t g = g0; g < g1; g++) {
             const RGroup G = s.h_grp[(size_t)g];
             for (int l = 0; l < 64; l++) {
                 const int64_t e = g * 64 + l;
-                uint64_t* dst = units + G.base + l;
+                src[l] = rfs[l] = nullptr;
+                spans[l] = 0;
                 if (e >= n) {                          // padding entry: empty
                     s.h_rh[(size_t)(2 * e)] = last_first;
                     s.h_rh[(size_t)(2 * e + 1)] = last_first - 1;
-                    for (int32_t k = 0; k < G.K; k++) dst[(int64_t)k * 64] = 0;
                     continue;
                 }
                 const SRead& rd = reads[(size_t)e];
@@ -1654,27 +1693,13 @@ static int build_rg_layout(Staged& s, const HugeVec<SRead>& reads, LayoutArena& 
                 s.h_rh[(size_t)(2 * e + 1)] = (int32_t)((uint32_t)(span > 0 ? rd.glast : rd.gfirst - 1) | (rd.neg ? 0x80000000u : 0u));
                 // reference-relative bytes: code ^ the position's reference code (0: a valid reference call of
                 // quality 0 -- what the padding past the read's end holds, never an exception in KL)
-                const uint8_t* rf = s.h_ref.data() + rd.gfirst;
-                const int64_t whole = span / 8;
-                for (int64_t k = 0; k < whole; k++) {
-                    uint64_t u, r;
-                    std::memcpy(&u, rd.bytes + 8 * k, 8);
-                    std::memcpy(&r, rf + 8 * k, 8);
-                    dst[k * 64] = u ^ r;
-                }
-                int64_t k = whole;
-                if (span % 8) {
-                    uint8_t b8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                    const int64_t rem = span % 8;
-                    for (int64_t t = 0; t < rem; t++) b8[t] = (uint8_t)(rd.bytes[8 * k + t] ^ rf[8 * k + t]);
-                    uint64_t u;
-                    std::memcpy(&u, b8, 8);
-                    dst[k * 64] = u;
-                    k++;
-                }
-                for (; k < G.K; k++) dst[k * 64] = 0;
+                src[l] = rd.bytes;
+                rfs[l] = s.h_ref.data() + rd.gfirst;
+                spans[l] = span;
             }
+            fill_group_units(units + G.base, G.K, src, rfs, spans);
         }
+        _mm_sfence();
     });
     // block tables over the global coordinate (reads are sorted by gfirst)
     const int64_t nb = (s.g_len >> kRgBlockShift) + 2;
@@ -1868,34 +1893,21 @@ static int build_pop_rg_layout(Staged& s, LayoutArena& arena) {
     s.units_pinned = arena.units_pinned;
     uint64_t* units = s.h_units;
     parallel_for(ng, 64, [&](int64_t g0, int64_t g1) {
+        const uint8_t* src[64];
+        const uint8_t* rfs[64];
+        int64_t spans[64];
         for (int64_t g = g0; g < g1; g++) {
             const RGroup G = s.h_grp[(size_t)g];
             for (int l = 0; l < 64; l++) {
                 const int32_t r = ent[(size_t)(g * 64 + l)];
-                uint64_t* dst = units + G.base + l;
                 const int64_t gf = r < 0 ? 0 : R[(int64_t)r * 4];
-                const int64_t span = r < 0 ? 0 : std::max<int64_t>(0, (int64_t)R[(int64_t)r * 4 + 1] - gf + 1);
-                const uint8_t* src = r < 0 ? nullptr : rptr[r];
-                const uint8_t* rf = ref + gf;
-                const int64_t whole = span / 8;
-                for (int64_t k = 0; k < whole; k++) {
-                    uint64_t u, v;
-                    std::memcpy(&u, src + 8 * k, 8);
-                    std::memcpy(&v, rf + 8 * k, 8);
-                    dst[k * 64] = u ^ v;
-                }
-                int64_t k = whole;
-                if (span % 8) {
-                    uint8_t b8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                    for (int64_t t = 0; t < span % 8; t++) b8[t] = (uint8_t)(src[8 * k + t] ^ rf[8 * k + t]);
-                    uint64_t u;
-                    std::memcpy(&u, b8, 8);
-                    dst[k * 64] = u;
-                    k++;
-                }
-                for (; k < G.K; k++) dst[k * 64] = 0;
+                spans[l] = r < 0 ? 0 : std::max<int64_t>(0, (int64_t)R[(int64_t)r * 4 + 1] - gf + 1);
+                src[l] = r < 0 ? nullptr : rptr[r];
+                rfs[l] = ref + gf;
             }
+            fill_group_units(units + G.base, G.K, src, rfs, spans);
         }
+        _mm_sfence();
     });
     lap("units");
     // block tables per stream, blocks of 2^pblk_shift positions (coarser when the tables would outgrow a quarter of
