@@ -769,26 +769,48 @@ int fill_batch(ngsep_bam* b, ngsep_bam::BatchStore& B, int64_t max_reads, ngsep_
         b->last_name.assign(nm.first, nm.second);
     }
     const auto tc2 = std::chrono::steady_clock::now();
-    // 3. output offsets of the kept records, then their fields in parallel
-    std::vector<int64_t> oidx((size_t)n + 1, 0), coff((size_t)n + 1, 0), soff((size_t)n + 1, 0);
-    for (int64_t i = 0; i < n; i++) {
-        const Rec& o = rec[(size_t)i];
-        oidx[(size_t)i + 1] = oidx[(size_t)i] + o.keep;
-        coff[(size_t)i + 1] = coff[(size_t)i] + (o.keep ? o.ncig : 0);
-        soff[(size_t)i + 1] = soff[(size_t)i] + (o.keep ? o.lseq : 0);
+    // 3. output offsets of the kept records (a chunked scan: per-chunk totals in parallel, the chunks' starts
+    //    serially, each chunk's records walked from its start), then their fields in parallel
+    constexpr int64_t kEmitChunk = 4096;
+    const int64_t nch = (n + kEmitChunk - 1) / kEmitChunk;
+    struct Offs { int64_t k, c, q; };              // kept records, CIGAR elements, sequence bytes before a chunk
+    std::vector<Offs> cst((size_t)nch + 1, Offs{0, 0, 0});
+    parallel_for(nch, 1, [&](int64_t c0, int64_t c1) {
+        for (int64_t c = c0; c < c1; c++) {
+            Offs t{0, 0, 0};
+            for (int64_t i = c * kEmitChunk; i < std::min(n, (c + 1) * kEmitChunk); i++) {
+                const Rec& o = rec[(size_t)i];
+                if (!o.keep) continue;
+                t.k++;
+                t.c += o.ncig;
+                t.q += o.lseq;
+            }
+            cst[(size_t)c + 1] = t;
+        }
+    });
+    for (int64_t c = 0; c < nch; c++) {
+        cst[(size_t)c + 1].k += cst[(size_t)c].k;
+        cst[(size_t)c + 1].c += cst[(size_t)c].c;
+        cst[(size_t)c + 1].q += cst[(size_t)c].q;
     }
-    const int64_t nk = oidx[(size_t)n];
+    const int64_t nk = cst[(size_t)nch].k;
     B.b_seq.resize((size_t)nk); B.b_first.resize((size_t)nk); B.b_flags.resize((size_t)nk); B.b_rg.resize((size_t)nk);
     B.b_cig_off.resize((size_t)nk); B.b_cig_n.resize((size_t)nk); B.b_seq_off.resize((size_t)nk); B.b_seqlen.resize((size_t)nk);
     B.b_hasq.resize((size_t)nk);
-    B.b_cigar.resize((size_t)coff[(size_t)n]);
-    B.b_bases.resize((size_t)soff[(size_t)n]);
-    B.b_quals.resize((size_t)soff[(size_t)n]);
-    parallel_for(n, 4096, [&](int64_t lo, int64_t hi) {
-        for (int64_t i = lo; i < hi; i++) {
+    B.b_cigar.resize((size_t)cst[(size_t)nch].c);
+    B.b_bases.resize((size_t)cst[(size_t)nch].q);
+    B.b_quals.resize((size_t)cst[(size_t)nch].q);
+    parallel_for(nch, 1, [&](int64_t c0, int64_t c1) {
+      for (int64_t c = c0; c < c1; c++) {
+        Offs at = cst[(size_t)c];
+        for (int64_t i = c * kEmitChunk; i < std::min(n, (c + 1) * kEmitChunk); i++) {
             const Rec& o = rec[(size_t)i];
             if (!o.keep) continue;
-            const size_t k = (size_t)oidx[(size_t)i];
+            const size_t k = (size_t)at.k;
+            const int64_t cig_at = at.c, seq_at = at.q;
+            at.k++;
+            at.c += o.ncig;
+            at.q += o.lseq;
             const uint8_t* r = base + roff[(size_t)i];
             const uint8_t l_name = r[8];
             const uint16_t n_cig = rd<uint16_t>(r + 12);
@@ -800,9 +822,9 @@ int fill_batch(ngsep_bam* b, ngsep_bam::BatchStore& B, int64_t max_reads, ngsep_
             B.b_first[k] = o.first;
             B.b_flags[k] = o.flags;
             B.b_rg[k] = o.rg;
-            B.b_cig_off[k] = coff[(size_t)i];
+            B.b_cig_off[k] = cig_at;
             B.b_cig_n[k] = o.ncig;
-            int32_t* cd = &B.b_cigar[(size_t)coff[(size_t)i]];
+            int32_t* cd = &B.b_cigar[(size_t)cig_at];
             int nc = 0;
             for (int c2 = 0; c2 < n_cig; c2++) {
                 const uint32_t v = rd<uint32_t>(cig + 4 * c2);
@@ -810,10 +832,10 @@ int fill_batch(ngsep_bam* b, ngsep_bam::BatchStore& B, int64_t max_reads, ngsep_
                 if (nc > 0 && (cd[nc - 1] & 7) == nop) cd[nc - 1] += (int32_t)(v >> 4) * 8;
                 else cd[nc++] = (int32_t)(v >> 4) * 8 + nop;
             }
-            B.b_seq_off[k] = soff[(size_t)i];
+            B.b_seq_off[k] = seq_at;
             B.b_seqlen[k] = l_seq;
-            char* bs = &B.b_bases[(size_t)soff[(size_t)i]];
-            char* qs = &B.b_quals[(size_t)soff[(size_t)i]];
+            char* bs = &B.b_bases[(size_t)seq_at];
+            char* qs = &B.b_quals[(size_t)seq_at];
             const bool hasq = l_seq > 0 && qual[0] != 0xFF;
             if (packed) {
                 // BAM's own encoding (ReadView::packed): the 4-bit bases and the raw qualities as they are
@@ -832,6 +854,7 @@ int fill_batch(ngsep_bam* b, ngsep_bam::BatchStore& B, int64_t max_reads, ngsep_
             }
             B.b_hasq[k] = hasq ? 1 : 0;
         }
+      }
     });
     const auto tc3 = std::chrono::steady_clock::now();
     b->t_cut += std::chrono::duration<double>(tc1 - tc0).count();
