@@ -858,7 +858,19 @@ __global__ __launch_bounds__(kPostThreads) void k_posterior_pool(const SiteQ* __
 //     The workgroup's queue slots and column space come from one atomic each (a block scan orders them).
 // No MFMA: byte SWAR and integer counters.
 constexpr int kKlThreads = 256;
-constexpr int kKlUnroll = 8;
+#ifndef NGSEP_KL_UNROLL
+#define NGSEP_KL_UNROLL 4
+#endif
+#ifndef NGSEP_KL_PIPE
+#define NGSEP_KL_PIPE 1     // the next batch's loads issued before the current batch's counters (0: A/B builds)
+#endif
+#ifndef NGSEP_KL_GPRE
+#define NGSEP_KL_GPRE 1     // the next group's unit offset fetched with its headers (0: A/B builds)
+#endif
+#ifndef NGSEP_KL_NT
+#define NGSEP_KL_NT 0       // A/B builds: the unit stream through nontemporal loads
+#endif
+constexpr int kKlUnroll = NGSEP_KL_UNROLL;
 
 // PileupRecord.getAlleleCalls(1) at global position p over the read-group layout: the nonzero codes of the reads
 // covering p, in pending-list (entry) order, as u16 entries code | negative strand << 8 (WRITE), one wave.  e0 is
@@ -909,8 +921,10 @@ __device__ __forceinline__ uint32_t kl_nonref(uint32_t y) {
 }
 
 // KL's read stream over the tile's groups (wave w: groups g_lo + w, g_lo + w + 4, ...).  A lane takes its read's
-// units from the first one inside the tile, kKlUnroll loads in flight; the bytes are reference-relative
-// (engine.hpp RGroup), so the stream reads no reference and no LDS: its counter adds never hold it up.
+// units from the first one inside the tile in batches of kKlUnroll, the next batch's loads issued before the
+// current batch's counter adds (software pipelined: 4-8 loads in flight per lane at 64 VGPRs, 8 waves per SIMD), and
+// the next group's headers and unit offset fetched a group ahead; the bytes are reference-relative (engine.hpp
+// RGroup), so the stream reads no reference and no LDS: its counter adds never hold it up.
 //   !DEEP: per position a 16-bit counter, exceptions in the low byte, other-allele calls in the high byte; a
 //          unit's 8 positions take five 32-bit LDS adds -- exact while no position of the tile is deeper than
 //          255 reads (the kernel checks, and reruns the stream DEEP).  Counter of tile position i: halfword 8 + i;
@@ -926,9 +940,16 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
     const bool no_counts = ABLATE(ablate, 128), no_units = ABLATE(ablate, 256);   // diagnostics
     int64_t g = g_lo + wv;
     int2 h = g < g_hi ? rh[g * 64 + lane] : make_int2(0, 0);
+#if NGSEP_KL_GPRE
+    RGroup Gc = g < g_hi ? grp[g] : RGroup{0, 0, 0};
+#endif
     for (; g < g_hi; g += kKlThreads / 64) {
         const int64_t e = g * 64 + lane;
         const int2 hn = g + kKlThreads / 64 < g_hi ? rh[e + kKlThreads] : make_int2(0, 0);   // the next group's headers in flight
+#if NGSEP_KL_GPRE
+        const RGroup G = Gc;                                // and its unit offset
+        Gc = g + kKlThreads / 64 < g_hi ? grp[g + kKlThreads / 64] : RGroup{0, 0, 0};
+#endif
         const int32_t gf = h.x, gl = h.y & 0x7FFFFFFF;
         const int32_t a = max(gf, tstart), b = min(gl, tstart + T - 1);
         const bool act = e >= e_lo && e < e_hi && a <= b;
@@ -936,17 +957,36 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
             atomicAdd(&s_diff[a - tstart], 1);
             atomicAdd(&s_diff[b - tstart + 1], -1);
         }
+#if !NGSEP_KL_GPRE
         const RGroup G = grp[g];
+#endif
         const int32_t k0 = act ? (a - gf) >> 3 : 0, kn = act && !no_units ? ((b - gf) >> 3) - k0 : -1;   // units k0 .. k0 + kn
         const int32_t ob0 = gf - tstart + 8 * k0 + 8;     // counter index of unit k0's byte 0 (>= 1)
         const int sh = (ob0 & 1) << 1;                    // !DEEP: byte offset of the unit's first halfword
         const uint64_t* ub = units + G.base + lane + (int64_t)k0 * 64;
         // a lane's own trip count (the wave runs while any lane has units left); loads are unconditional (a
         // batch's slots past the read's last unit repeat it) so that each unit waits for its own load only
+#if NGSEP_KL_NT
+#define KL_LOAD(q) __builtin_nontemporal_load(&(q))
+#else
+#define KL_LOAD(q) (q)
+#endif
+#if NGSEP_KL_PIPE
+        uint64_t u[U];
+#pragma unroll
+        for (int i = 0; i < U; i++) u[i] = kn >= 0 ? KL_LOAD(ub[(int64_t)min(i, kn) * 64]) : 0ull;
+        for (int32_t j = 0; j <= kn; j += U) {
+            uint64_t v[U];
+            if (j + U <= kn) {
+#pragma unroll
+                for (int i = 0; i < U; i++) v[i] = KL_LOAD(ub[(int64_t)min(j + U + i, kn) * 64]);
+            }
+#else
         for (int32_t j = 0; j <= kn; j += U) {
             uint64_t u[U];
 #pragma unroll
-            for (int i = 0; i < U; i++) u[i] = ub[(int64_t)min(j + i, kn) * 64];
+            for (int i = 0; i < U; i++) u[i] = KL_LOAD(ub[(int64_t)min(j + i, kn) * 64]);
+#endif
 #pragma unroll
             for (int i = 0; i < U; i++) {
                 if (j + i > kn) continue;
@@ -988,13 +1028,26 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
                     }
                 }
             }
+#if NGSEP_KL_PIPE
+#pragma unroll
+            for (int i = 0; i < U; i++) u[i] = v[i];
+#endif
         }
+#undef KL_LOAD
         h = hn;
     }
 }
 
+#ifndef NGSEP_KL_WPE
+#define NGSEP_KL_WPE 8      // 8 waves per SIMD: the pipelined stream's registers capped at 64 (0: the compiler's choice)
+#endif
+#if NGSEP_KL_WPE
+#define KL_WPE_ATTR __attribute__((amdgpu_waves_per_eu(NGSEP_KL_WPE)))
+#else
+#define KL_WPE_ATTR
+#endif
 template <int T, int U>
-__global__ __launch_bounds__(kKlThreads) void k_read_scan(
+__global__ __launch_bounds__(kKlThreads) KL_WPE_ATTR void k_read_scan(
     const uint64_t* __restrict__ units, const int2* __restrict__ rh, const RGroup* __restrict__ grp,
     const int32_t* __restrict__ blkA, const int32_t* __restrict__ blkB, int64_t n_entries,
     const uint8_t* __restrict__ ref, const LikTables* __restrict__ tabs, GenotypeParams gp,
@@ -2895,7 +2948,8 @@ static int enqueue_run(Device* d, RunSlot& sl, const Staged& s, const LikTables&
         kg_sites = nforced;
     } else if (d->n_tiles > 0 && prune) {
         // KL: one workgroup per tile of kKlTile positions, straight from the read-group layout
-        // (measured on chr20 30x: 2048-position tiles and 8 loads in flight per lane beat 4096 / 16 and 24)
+        // (measured on chr20 30x: 2048-position tiles beat 4096; batches of 8 unpipelined beat 16 and 24; batches
+        // of 4 pipelined at 8 waves per SIMD beat 8 unpipelined by 2 %, tools/gpu_r4_abn.sh)
         hipExtLaunchKernelGGL(k_read_scan<kKlTile, kKlUnroll>, dim3((unsigned)(s.g_len / kKlTile)), dim3(kKlThreads), 0, sl.stream, k0, k1, 0,
                               (const uint64_t*)d->d_units, (const int2*)d->d_rh, (const RGroup*)d->d_grp, (const int32_t*)d->d_blkA,
                               (const int32_t*)d->d_blkB, d->n_entries, (const uint8_t*)d->d_ref, (const LikTables*)sl.d_tables, g,
