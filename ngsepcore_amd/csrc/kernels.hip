@@ -1440,7 +1440,14 @@ __global__ __launch_bounds__(256) void k_queue_need(const uint32_t* __restrict__
 // wave's state is its own.
 constexpr int kKlmThreads = 256;
 constexpr int kKlmWords = kKlmTile / 32 + 2;   // tile bitmap words, a 32-position margin on either side
-constexpr int kKlmUnroll = 8;                   // pass 1: unit loads in flight per lane
+#ifndef NGSEP_KLM_PIPE
+#define NGSEP_KLM_PIPE 1     // (configs[4]: pipelined batches of 4 1.368-1.372 ms vs unpipelined 8 1.393-1.395 ms;
+#endif                       // pipelined 6 at 8 waves 1.422, tools/gpu_r4_klmabn.sh)
+#ifndef NGSEP_KLM_UNROLL
+#define NGSEP_KLM_UNROLL 4
+#endif
+constexpr int kKlmUnroll = NGSEP_KLM_UNROLL;    // pass 1: unit loads in flight per lane (NGSEP_KLM_PIPE: batches
+                                                // pipelined, the next batch's loads before the current one's marks)
 #ifndef NGSEP_KLM_PEND
 #define NGSEP_KLM_PEND 2
 #endif
@@ -1502,10 +1509,22 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(NGS
             const int32_t k0 = act ? (a - gf) >> 3 : 0, kn = act ? ((b - gf) >> 3) - k0 : -1;
             const uint64_t* ub = units + gbase + lane + (int64_t)k0 * 64;
             const int32_t ti0 = gf + 8 * k0 - tstart + 32;   // bitmap index of unit k0's byte 0 (>= 25)
+#if NGSEP_KLM_PIPE
+            uint64_t u[kKlmUnroll];
+#pragma unroll
+            for (int i = 0; i < kKlmUnroll; i++) u[i] = kn >= 0 ? ub[(int64_t)min(i, kn) * 64] : 0ull;
+            for (int32_t j = 0; j <= kn; j += kKlmUnroll) {
+                uint64_t v[kKlmUnroll];
+                if (j + kKlmUnroll <= kn) {
+#pragma unroll
+                    for (int i = 0; i < kKlmUnroll; i++) v[i] = ub[(int64_t)min(j + kKlmUnroll + i, kn) * 64];
+                }
+#else
             for (int32_t j = 0; j <= kn; j += kKlmUnroll) {
                 uint64_t u[kKlmUnroll];
 #pragma unroll
                 for (int i = 0; i < kKlmUnroll; i++) u[i] = ub[(int64_t)min(j + i, kn) * 64];
+#endif
 #pragma unroll
                 for (int i = 0; i < kKlmUnroll; i++) {
                     if (j + i > kn) continue;
@@ -1520,10 +1539,14 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(NGS
                         if (tp >= 0 && tp < kKlmTile && !(s_ref[tp] & 0x80u)) m &= ~(1u << k);
                     }
                     if (!m) continue;
-                    const uint64_t v = (uint64_t)m << (ti & 31);
-                    atomicOr(&bm[ti >> 5], (uint32_t)v);
-                    if (v >> 32) atomicOr(&bm[(ti >> 5) + 1], (uint32_t)(v >> 32));
+                    const uint64_t mv = (uint64_t)m << (ti & 31);
+                    atomicOr(&bm[ti >> 5], (uint32_t)mv);
+                    if (mv >> 32) atomicOr(&bm[(ti >> 5) + 1], (uint32_t)(mv >> 32));
                 }
+#if NGSEP_KLM_PIPE
+#pragma unroll
+                for (int i = 0; i < kKlmUnroll; i++) u[i] = v[i];
+#endif
             }
             h = hn;
             gbase = gbn;

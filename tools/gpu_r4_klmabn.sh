@@ -1,0 +1,24 @@
+#!/bin/bash
+# round 4: population-scan variants (ab/<name>/libngsep_amd.so via NGSEP_LIB_PATH) against the release build on one
+# box: parity of each variant on the population tests, then alternating configs[4] bench lines
+# usage: tools/gpu_r4_klmabn.sh name1 name2 ...
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+for v in "$@"; do
+  NGSEP_LIB_PATH=$PWD/ab/$v/libngsep_amd.so timeout -k 10 300 python -u -m pytest tests/test_gpu_multisample.py -m gpu -x -q \
+      --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/klmabn_parity_$v.log 2>&1 || { echo "parity $v failed"; tail -20 gpurun_out/klmabn_parity_$v.log; exit 1; }
+  echo "parity $v: $(tail -1 gpurun_out/klmabn_parity_$v.log)"
+done
+B="python -u bench.py --config multisample --no-cpu-baseline --no-cold --no-e2e --steps 20 --warmup 4"
+for r in 1 2; do
+  for v in release "$@"; do
+    if [ "$v" = release ]; then L=""; else L=$PWD/ab/$v/libngsep_amd.so; fi
+    NGSEP_TIME_POSTERIOR=1 NGSEP_LIB_PATH=$L timeout -k 10 300 $B > gpurun_out/klmabn_${v}_$r.json 2> gpurun_out/klmabn_${v}_$r.err || { tail -5 gpurun_out/klmabn_${v}_$r.err; exit 1; }
+    python -c "
+import json
+d = json.loads(open('gpurun_out/klmabn_${v}_$r.json').read().strip().splitlines()[-1])
+r = d['roofline']
+print('$v', $r, 'step %.3f ms' % d['ms_per_step'], 'scan %.3f ms' % r['kernel_avg_ms'], 'kpm', r['posterior_kernel_avg_ms'], 'frac %.3f' % r['frac'])"
+  done
+done
