@@ -1443,6 +1443,10 @@ constexpr int kKlmWords = kKlmTile / 32 + 2;   // tile bitmap words, a 32-positi
 #ifndef NGSEP_KLM_PIPE
 #define NGSEP_KLM_PIPE 1     // (configs[4]: pipelined batches of 4 1.368-1.372 ms vs unpipelined 8 1.393-1.395 ms;
 #endif                       // pipelined 6 at 8 waves 1.422, tools/gpu_r4_klmabn.sh)
+#ifndef NGSEP_KLM_P2PRE
+#define NGSEP_KLM_P2PRE 1    // pass 2 fetches the next group's header and base a group ahead (configs[4]: scan 1.343-
+                             // 1.350 vs 1.377-1.419 ms; with 3 / 4 pending loads 1.42 / 1.45, tools/gpu_r4_klmabn.sh)
+#endif
 #ifndef NGSEP_KLM_UNROLL
 #define NGSEP_KLM_UNROLL 4
 #endif
@@ -1613,13 +1617,27 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(NGS
     for (int st = st0; st < st1; st++) {
         const int64_t e_lo = blkA[(int64_t)st * nblk + (tstart >> shift)];
         const int64_t e_hi = blkB[(int64_t)st * nblk + (tlast >> shift) + 1];
+#if NGSEP_KLM_P2PRE
+        const int64_t g_hi = (e_hi + 63) >> 6;
+        int64_t g = e_lo >> 6;
+        int2 hc = g < g_hi ? rh[g * 64 + lane] : make_int2(0, -1);
+        int64_t gbc = g < g_hi ? grp[g].base : 0;
+        for (; g < g_hi; g++) {
+            const int64_t e = g * 64 + lane;
+            const int2 h = hc;                                 // the next group's header and base in flight
+            const int64_t gbase = gbc;
+            hc = g + 1 < g_hi ? rh[e + 64] : make_int2(0, -1);
+            gbc = g + 1 < g_hi ? grp[g + 1].base : 0;
+#else
         for (int64_t g = e_lo >> 6; g < (e_hi + 63) >> 6; g++) {
             const int64_t e = g * 64 + lane;
             const int2 h = rh[e];
+            const int64_t gbase = grp[g].base;
+#endif
             const int32_t gf = h.x, gl = h.y & 0x7FFFFFFF;
             const int32_t a = max(gf, tstart), b = min(gl, tlast);
             if (!(e >= e_lo && e < e_hi && a <= b)) continue;
-            const uint64_t* ub = units + grp[g].base + lane;
+            const uint64_t* ub = units + gbase + lane;
             const int32_t A = a - tstart + 32, B = b - tstart + 32;
             int32_t pend_o[kKlmPend];
             uint32_t pend_s[kKlmPend];
