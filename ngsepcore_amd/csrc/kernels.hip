@@ -1447,13 +1447,22 @@ constexpr int kKlmWords = kKlmTile / 32 + 2;   // tile bitmap words, a 32-positi
 #define NGSEP_KLM_P2PRE 1    // pass 2 fetches the next group's header and base a group ahead (configs[4]: scan 1.343-
                              // 1.350 vs 1.377-1.419 ms; with 3 / 4 pending loads 1.42 / 1.45, tools/gpu_r4_klmabn.sh)
 #endif
+#ifndef NGSEP_KLM_P2DEPTH
+#define NGSEP_KLM_P2DEPTH 0  // A/B builds (with NGSEP_KLM_PEND 1): pass 2's loads in a queue of this depth
+#endif
+// pass 2 pipelined: a marked position's load issued before the previous one's adds (configs[4] scan 1.343-1.350 ->
+// 1.225-1.235 ms at 1 pending load; 2 pending 1.303-1.309; queues of depth 2 / 3 / 4: 1.275 / 1.320 / 1.431 ms,
+// tools/gpu_r4_klmabn.sh)
+#ifndef NGSEP_KLM_P2PIPE
+#define NGSEP_KLM_P2PIPE 1
+#endif
 #ifndef NGSEP_KLM_UNROLL
 #define NGSEP_KLM_UNROLL 4
 #endif
 constexpr int kKlmUnroll = NGSEP_KLM_UNROLL;    // pass 1: unit loads in flight per lane (NGSEP_KLM_PIPE: batches
                                                 // pipelined, the next batch's loads before the current one's marks)
 #ifndef NGSEP_KLM_PEND
-#define NGSEP_KLM_PEND 2
+#define NGSEP_KLM_PEND 1
 #endif
 constexpr int kKlmPend = NGSEP_KLM_PEND;        // pass 2: marked-position loads issued together per lane
 #ifndef NGSEP_KLM_WPE
@@ -1644,6 +1653,76 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(NGS
 #pragma unroll
             for (int i = 0; i < kKlmPend; i++) { pend_o[i] = 0; pend_s[i] = 0; }
             int np = 0;
+#if NGSEP_KLM_P2DEPTH
+            // software-pipelined, one load per marked position: up to kD loads in flight, the oldest added when a
+            // new one is issued (static register indexes only)
+            constexpr int kD = NGSEP_KLM_P2DEPTH;
+            uint64_t qu[kD];
+            uint32_t qsh[kD], qs[kD];
+            int nq = 0;
+#pragma unroll
+            for (int i = 0; i < kD; i++) { qu[i] = 0ull; qsh[i] = 0u; qs[i] = 0u; }
+            auto add1 = [&](uint64_t uu, uint32_t sh8, uint32_t slot) {
+                const uint32_t y = (uint32_t)(uu >> sh8) & 0xFFu;
+                if (y & 0x80u) return;                        // not a valid call (the position is callable)
+                const uint32_t al = (y >> 5) & 3u;
+                int q = (int)(y & 31u);
+                q = q > maxq ? maxq : q;
+                atomicAdd(&acc[4 * slot + al], w[al == 0 ? 0 : 1][q]);
+                atomicAdd(&sn[slot], 1u);
+            };
+            auto add_q = [&]() {
+#pragma unroll
+                for (int i = 0; i < kD; i++)
+                    if (i < nq) add1(qu[i], qsh[i], qs[i]);
+                nq = 0;
+            };
+            auto flush = [&]() {
+                const uint64_t u = ub[(int64_t)(pend_o[0] >> 3) * 64];
+                if (nq == kD) {
+                    add1(qu[0], qsh[0], qs[0]);
+#pragma unroll
+                    for (int i = 0; i + 1 < kD; i++) { qu[i] = qu[i + 1]; qsh[i] = qsh[i + 1]; qs[i] = qs[i + 1]; }
+                    nq--;
+                }
+#pragma unroll
+                for (int i = 0; i < kD; i++)
+                    if (i == nq) { qu[i] = u; qsh[i] = 8u * (uint32_t)(pend_o[0] & 7); qs[i] = pend_s[0]; }
+                nq++;
+                np = 0;
+            };
+#elif NGSEP_KLM_P2PIPE
+            // software-pipelined: a full batch's loads are issued, then the previous batch (in flight) is added
+            uint64_t qu[kKlmPend];
+            uint32_t qsh[kKlmPend], qs[kKlmPend];
+            int nq = 0;
+#pragma unroll
+            for (int i = 0; i < kKlmPend; i++) { qu[i] = 0ull; qsh[i] = 0u; qs[i] = 0u; }
+            auto add_q = [&]() {
+#pragma unroll
+                for (int i = 0; i < kKlmPend; i++) {
+                    if (i >= nq) continue;
+                    const uint32_t y = (uint32_t)(qu[i] >> qsh[i]) & 0xFFu;
+                    if (y & 0x80u) continue;                  // not a valid call (the position is callable)
+                    const uint32_t al = (y >> 5) & 3u;
+                    int q = (int)(y & 31u);
+                    q = q > maxq ? maxq : q;
+                    atomicAdd(&acc[4 * qs[i] + al], w[al == 0 ? 0 : 1][q]);
+                    atomicAdd(&sn[qs[i]], 1u);
+                }
+                nq = 0;
+            };
+            auto flush = [&]() {
+                uint64_t u[kKlmPend];
+#pragma unroll
+                for (int i = 0; i < kKlmPend; i++) u[i] = i < np ? ub[(int64_t)(pend_o[i] >> 3) * 64] : 0ull;
+                add_q();
+#pragma unroll
+                for (int i = 0; i < kKlmPend; i++) { qu[i] = u[i]; qsh[i] = 8u * (uint32_t)(pend_o[i] & 7); qs[i] = pend_s[i]; }
+                nq = np;
+                np = 0;
+            };
+#else
             auto flush = [&]() {
                 uint64_t u[kKlmPend];
 #pragma unroll
@@ -1661,6 +1740,7 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(NGS
                 }
                 np = 0;
             };
+#endif
             for (int32_t wi = A >> 5; wi <= (B >> 5); wi++) {
                 uint32_t word = bm[wi];
                 if (wi == (A >> 5)) word &= ~0u << (A & 31);
@@ -1681,6 +1761,9 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(NGS
                 }
             }
             if (np) flush();
+#if NGSEP_KLM_P2PIPE || NGSEP_KLM_P2DEPTH
+            add_q();
+#endif
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
