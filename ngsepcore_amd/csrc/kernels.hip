@@ -2066,6 +2066,10 @@ __device__ __forceinline__ PopCall genotype_sample_d(const LA& L, const int* cnt
 // after stream, pending order inside -- into dst (at most cap codes; the host sizes cap by the sample's coverage
 // bound).  Entries are walked from the stream's block-table entry eight headers at a time (their two possible
 // groups' bases loaded alongside), the covering ones' unit loads issued together.
+#ifndef NGSEP_KPM_GPIPE
+#define NGSEP_KPM_GPIPE 1    // the gather's next header batch loaded while this batch's units are in flight (configs[4]
+                             // KPM 0.484-0.485 -> 0.423-0.425 ms A/B on one box, tools/gpu_r4_klmabn.sh)
+#endif
 struct PopGather {
     const uint64_t* units;
     const int2* rh;
@@ -2086,10 +2090,22 @@ __device__ inline int32_t pop_gather(const PopGather& pg, int32_t p, int s, uint
         int64_t e = pg.blkA[(int64_t)st * pg.nblk + (p >> pg.shift)];
         const int64_t end = pg.st_end[st];
         bool done = false;
+#if NGSEP_KPM_GPIPE
+        // the next batch's headers are loaded while this batch's unit dwords are in flight (when this batch's last
+        // header still starts at or before p, i.e. the next batch can hold covering reads)
+        int2 hn[kGatherBatch];
+#pragma unroll
+        for (int i = 0; i < kGatherBatch; i++) hn[i] = e + i < end ? pg.rh[e + i] : make_int2(0x7FFFFFFF, 0);
+#endif
         while (!done && e < end) {
             int2 h[kGatherBatch];
+#if NGSEP_KPM_GPIPE
+#pragma unroll
+            for (int i = 0; i < kGatherBatch; i++) h[i] = hn[i];
+#else
 #pragma unroll
             for (int i = 0; i < kGatherBatch; i++) h[i] = e + i < end ? pg.rh[e + i] : make_int2(0x7FFFFFFF, 0);
+#endif
             const int64_t g0 = e >> 6;
             const int64_t gb0 = pg.grp[g0].base;
             const int64_t gb1 = ((e + kGatherBatch - 1) >> 6) != g0 && ((g0 + 1) << 6) < end ? pg.grp[g0 + 1].base : gb0;
@@ -2105,6 +2121,13 @@ __device__ inline int32_t pop_gather(const PopGather& pg, int32_t p, int s, uint
                     u[i] = uw[(o >> 2) & 1];
                 }
             }
+#if NGSEP_KPM_GPIPE
+            if (h[kGatherBatch - 1].x <= p) {
+#pragma unroll
+                for (int i = 0; i < kGatherBatch; i++)
+                    hn[i] = e + kGatherBatch + i < end ? pg.rh[e + kGatherBatch + i] : make_int2(0x7FFFFFFF, 0);
+            }
+#endif
 #pragma unroll
             for (int i = 0; i < kGatherBatch; i++) {
                 const int32_t gf = h[i].x, gl = h[i].y & 0x7FFFFFFF;
