@@ -2093,6 +2093,9 @@ __device__ __forceinline__ PopCall genotype_sample_d(const LA& L, const int* cnt
 // after stream, pending order inside -- into dst (at most cap codes; the host sizes cap by the sample's coverage
 // bound).  Entries are walked from the stream's block-table entry eight headers at a time (their two possible
 // groups' bases loaded alongside), the covering ones' unit loads issued together.
+#ifndef NGSEP_KPM_GBATCH
+#define NGSEP_KPM_GBATCH 8   // entry headers a gathering thread loads at once
+#endif
 #ifndef NGSEP_KPM_GPIPE
 #define NGSEP_KPM_GPIPE 1    // the gather's next header batch loaded while this batch's units are in flight (configs[4]
                              // KPM 0.484-0.485 -> 0.423-0.425 ms A/B on one box, tools/gpu_r4_klmabn.sh)
@@ -2241,7 +2244,7 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
         const uint8_t* col = col_next;
         if (GATHER == 1 && tid <= n_samples) {
             uint8_t* dst = s_gcol + (int64_t)tid * pg.stride;
-            rows = pop_gather<8>(pg, gpos, tid, dst, pg.stride);
+            rows = pop_gather<NGSEP_KPM_GBATCH>(pg, gpos, tid, dst, pg.stride);
             if (rows > pg.stride) {                          // (the host's coverage bound makes this unreachable)
                 atomicOr(&counters[3], 1ull << 63);
                 rows = pg.stride;
