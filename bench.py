@@ -684,6 +684,9 @@ def main():
                 "posterior_kernel_avg_ms": post_avg_ms,
             },
         }
+        from ngsepcore_amd import _lib as nlib
+        if nlib.LIB_PATH != nlib.DEFAULT_LIB_PATH:      # an A/B tuning build (NGSEP_LIB_PATH): named in the line
+            line["config"]["lib_path"] = nlib.LIB_PATH
         if multi:
             line["config"]["samples"] = args.samples
             line["config"]["sample_calls_per_step"] = int(sites_called) * args.samples

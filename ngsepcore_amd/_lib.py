@@ -10,7 +10,13 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ABI_VERSION = 10                                   # NGSEP_ABI_VERSION (include/ngsep_gpu.h)
-LIB_PATH = os.environ.get("NGSEP_LIB_PATH") or os.path.join(_HERE, "lib", "libngsep_amd.so")   # override: tuning builds only
+DEFAULT_LIB_PATH = os.path.join(_HERE, "lib", "libngsep_amd.so")
+# NGSEP_LIB_PATH: an A/B tuning build of the same ABI, for measurements only.  It is announced on stderr when taken, and
+# bench.py records it in its line (config.lib_path), so no result can come from a swapped library silently.
+LIB_PATH = os.environ.get("NGSEP_LIB_PATH") or DEFAULT_LIB_PATH
+if LIB_PATH != DEFAULT_LIB_PATH:
+    import sys
+    print(f"ngsepcore_amd: NGSEP_LIB_PATH overrides the library: {LIB_PATH}", file=sys.stderr, flush=True)
 
 NGSEP_OK = 0
 NGSEP_E_INVALID = -1

@@ -1046,7 +1046,7 @@ extern "C" int ngsep_clean_cut(ngsep_ctx* c, const char* const* bam_paths, int32
     for (int64_t W = (int64_t)1 << 16;; W *= 4) {
         const int64_t lo = std::max<int64_t>(1, pos - W), hi = pos + W;
         std::vector<std::pair<int64_t, int64_t>> ev;      // [first, last + indel bases] of the events
-        int64_t maxspan = 1;
+        int64_t maxspan = 1, maxind = 0;
         for (int32_t fi = 0; fi < n_files; fi++) {
             ngsep_bam* b = nullptr;
             int rc = ngsep_bam_open(c, bam_paths[fi], &b);
@@ -1066,6 +1066,7 @@ extern "C" int ngsep_clean_cut(ngsep_ctx* c, const char* const* bam_paths, int32
                     }
                     if (last < lo || batch.first[i] > hi) continue;
                     maxspan = std::max<int64_t>(maxspan, last - batch.first[i] + 1);
+                    maxind = std::max<int64_t>(maxind, indel);
                     if (indel > 0) ev.push_back({batch.first[i], last + indel});
                 }
             }
@@ -1083,8 +1084,10 @@ extern "C" int ngsep_clean_cut(ngsep_ctx* c, const char* const* bam_paths, int32
             if (e.second + M >= p) p = e.second + M + 1;
         }
         // decided when no alignment outside [lo, hi] can cover p: those past hi start their intervals after hi - M,
-        // those before lo end theirs before lo + M + their indel bases
-        const bool right = p <= hi - M || hi >= len, left = lo == 1 || pos - lo >= 4 * M;
+        // those before lo end theirs before lo + M + their indel bases.  The left margin takes the most indel bases
+        // any alignment of the neighbourhood carries on top of 4 M: an alignment before lo with more insertion bases
+        // than 2 M + that (an insertion longer than twice the longest span seen, a long read's) is assumed absent
+        const bool right = p <= hi - M || hi >= len, left = lo == 1 || pos - lo >= 4 * M + maxind;
         if (right && left) { *cut = std::min<int64_t>(p, len + 1); *lead = M + maxspan; return NGSEP_OK; }
         if (W > ((int64_t)1 << 34)) { *cut = len + 1; *lead = M + maxspan; return NGSEP_OK; }
     }

@@ -1934,28 +1934,35 @@ static int build_pop_rg_layout(Staged& s, LayoutArena& arena) {
             }
         }
     });
-    // a bound on the reads of one sample covering one position (KPM gathers each sample's column into a slot of
-    // this many codes): per stream the most reads starting in max_span consecutive positions, summed over the
-    // sample's streams
-    std::vector<int32_t> sbound((size_t)nst, 0);
-    parallel_for(nst, 1, [&](int64_t a, int64_t b) {
-        for (int64_t st = a; st < b; st++) {
-            const int32_t* o = &ord[(size_t)st_r0[(size_t)st]];
-            const int64_t m = st_n[(size_t)st];
-            int32_t mc = 0;
-            for (int64_t i = 0, j = 0; i < m; i++) {
-                while ((int64_t)R[(int64_t)o[j] * 4] <= (int64_t)R[(int64_t)o[i] * 4] - ms) j++;
-                mc = std::max<int32_t>(mc, (int32_t)(i - j + 1));
+    // the most reads of one sample covering one position (KPM gathers each sample's column into a slot of this many
+    // codes): a sweep over the sample's read starts and ends, all its streams together (a bound from the longest span
+    // in the run would let one long alignment inflate every sample's slot)
+    std::vector<int32_t> sbound((size_t)S + 1, 0);
+    parallel_for(S + 1, 1, [&](int64_t a, int64_t b) {
+        std::vector<int32_t> starts, ends;
+        for (int64_t sm = a; sm < b; sm++) {
+            starts.clear();
+            ends.clear();
+            for (int32_t st = s.h_samp_st[(size_t)sm]; st < s.h_samp_st[(size_t)sm + 1]; st++) {
+                const int32_t* o = &ord[(size_t)st_r0[(size_t)st]];
+                for (int64_t i = 0; i < st_n[(size_t)st]; i++) {
+                    starts.push_back(R[(int64_t)o[i] * 4]);
+                    ends.push_back(R[(int64_t)o[i] * 4 + 1]);
+                }
             }
-            sbound[(size_t)st] = mc;
+            std::sort(starts.begin(), starts.end());
+            std::sort(ends.begin(), ends.end());
+            int32_t mc = 0;
+            size_t j = 0;
+            for (size_t i = 0; i < starts.size(); i++) {       // covering reads at starts[i]: started, not yet ended
+                while (j < ends.size() && ends[j] < starts[i]) j++;
+                mc = std::max<int32_t>(mc, (int32_t)(i + 1 - j));
+            }
+            sbound[(size_t)sm] = mc;
         }
     });
     int32_t stride = 0;
-    for (int sm = 0; sm <= S; sm++) {
-        int32_t b = 0;
-        for (int32_t st = s.h_samp_st[(size_t)sm]; st < s.h_samp_st[(size_t)sm + 1]; st++) b += sbound[(size_t)st];
-        stride = std::max(stride, b);
-    }
+    for (int sm = 0; sm <= S; sm++) stride = std::max(stride, sbound[(size_t)sm]);
     s.max_cov = (stride + 3) / 4 * 4;
     s.prg = true;
     s.tile = kKlmTile;
@@ -3297,6 +3304,12 @@ extern "C" int ngsep_set_known_strs(ngsep_ctx* c, const char* path) {
 
 extern "C" int ngsep_set_known_variants(ngsep_ctx* c, const char* vcf_path) {
     if (!c) return NGSEP_E_INVALID;
+    if (c->known_given) {
+        // the realigner's input variants were the previous file's records: a cleared (or refused) file leaves none,
+        // as in a fresh session (-knownSTRs given before -knownVariants were dropped by it and must be set again)
+        c->strs.clear();
+        c->str_next = 0;
+    }
     c->known.clear();
     c->known_recs.clear();
     c->known_seq_begin.clear();

@@ -867,9 +867,6 @@ constexpr int kKlThreads = 256;
 #ifndef NGSEP_KL_GPRE
 #define NGSEP_KL_GPRE 1     // the next group's unit offset fetched with its headers (0: A/B builds)
 #endif
-#ifndef NGSEP_KL_NT
-#define NGSEP_KL_NT 0       // A/B builds: the unit stream through nontemporal loads
-#endif
 constexpr int kKlUnroll = NGSEP_KL_UNROLL;
 
 // PileupRecord.getAlleleCalls(1) at global position p over the read-group layout: the nonzero codes of the reads
@@ -966,11 +963,7 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
         const uint64_t* ub = units + G.base + lane + (int64_t)k0 * 64;
         // a lane's own trip count (the wave runs while any lane has units left); loads are unconditional (a
         // batch's slots past the read's last unit repeat it) so that each unit waits for its own load only
-#if NGSEP_KL_NT
-#define KL_LOAD(q) __builtin_nontemporal_load(&(q))
-#else
-#define KL_LOAD(q) (q)
-#endif
+#define KL_LOAD(q) (q)                                    // (nontemporal loads measured no change)
 #if NGSEP_KL_PIPE
         uint64_t u[U];
 #pragma unroll
@@ -1275,9 +1268,6 @@ __global__ __launch_bounds__(256) void k_gather_cols(const SiteQ* __restrict__ q
 // KG for KL's queue (every site's column space reserved: rows <= -3, or -2 when the shard's columns were full):
 // a wave gathers kKgSites sites at once, their chunk loads interleaved (one site's gather is a chain of dependent
 // loads -- block table, headers, units -- so a wave per site leaves the chip waiting).  Compacts like k_gather_cols.
-#ifndef NGSEP_KG_PIPE
-#define NGSEP_KG_PIPE 0      // A/B builds: the next chunk's headers loaded while this chunk's units are in flight
-#endif
 template <int kKgSites>
 __global__ __launch_bounds__(256) void k_gather_kl(const SiteQ* __restrict__ qin, const unsigned long long* __restrict__ qcnt,
                                                    int stride, int nshard, int64_t qseg, SiteQ* __restrict__ qout,
@@ -1318,18 +1308,8 @@ __global__ __launch_bounds__(256) void k_gather_kl(const SiteQ* __restrict__ qin
                 e[t] = (int64_t)blkA[q[t].gpos >> kRgBlockShift] & ~(int64_t)63;
                 rcode[t] = ref[q[t].gpos];
             }
-        // chunk steps: every live site reads its next 64 entries' headers, then the covering ones' units (the next
-        // chunk's headers are loaded while this chunk's units are in flight, when the chunk can still hold coverers)
-#if NGSEP_KG_PIPE
-        int2 hn[kKgSites];
-        int64_t gbn[kKgSites];
-#pragma unroll
-        for (int t = 0; t < kKgSites; t++) {
-            const bool l = live[t] && e[t] < n_entries;
-            hn[t] = l ? rh[e[t] + lane] : make_int2(0x7FFFFFFF, 0);
-            gbn[t] = l ? grp[e[t] >> 6].base : 0;
-        }
-#endif
+        // chunk steps: every live site reads its next 64 entries' headers, then the covering ones' units (loading the
+        // next chunk's headers while this chunk's units are in flight measured no change, DESIGN.md 3 KG)
         for (;;) {
             bool any = false;
 #pragma unroll
@@ -1339,14 +1319,9 @@ __global__ __launch_bounds__(256) void k_gather_kl(const SiteQ* __restrict__ qin
             int64_t gb[kKgSites];
 #pragma unroll
             for (int t = 0; t < kKgSites; t++) {
-#if NGSEP_KG_PIPE
-                h[t] = hn[t];
-                gb[t] = gbn[t];
-#else
                 const bool l = live[t] && e[t] < n_entries;
                 h[t] = l ? rh[e[t] + lane] : make_int2(0x7FFFFFFF, 0);
                 gb[t] = l ? grp[e[t] >> 6].base : 0;
-#endif
             }
             uint64_t u[kKgSites];
             int32_t o[kKgSites];
@@ -1357,14 +1332,6 @@ __global__ __launch_bounds__(256) void k_gather_kl(const SiteQ* __restrict__ qin
                 o[t] = covers ? p - gf : -1;
                 u[t] = covers ? units[gb[t] + (int64_t)(o[t] >> 3) * 64 + lane] : 0ull;
             }
-#if NGSEP_KG_PIPE
-#pragma unroll
-            for (int t = 0; t < kKgSites; t++) {
-                const bool more = live[t] && !__ballot(h[t].x > q[t].gpos) && e[t] + 64 < n_entries;
-                hn[t] = more ? rh[e[t] + 64 + lane] : make_int2(0x7FFFFFFF, 0);
-                gbn[t] = more ? grp[(e[t] + 64) >> 6].base : 0;
-            }
-#endif
 #pragma unroll
             for (int t = 0; t < kKgSites; t++) {
                 if (!live[t]) continue;

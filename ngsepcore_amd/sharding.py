@@ -22,6 +22,7 @@ import gzip
 import os
 import struct
 import tempfile
+import zlib
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 
@@ -148,9 +149,11 @@ def compute_cuts(contigs: Sequence[Tuple[str, int]], window: int, cut_fn: Callab
 _queue_uses = [0]
 
 
-def shared_queue(n: int, dist=None):
+def shared_queue(n: int, dist=None, tag: str = ""):
     """Unit indexes 0 .. n - 1 handed out to the ranks as they ask (a counter in the process group's store); with
-    no store, rank r takes r, r + world, ..."""
+    no store, rank r takes r, r + world, ...  The store key is the call's ordinal on this rank plus `tag` (the unit
+    list's digest): ranks that disagree on either use different counters, so every unit is then called on several
+    ranks and the merge refuses the duplicate windows, never mixing two queues."""
     world = dist.get_world_size() if dist is not None and dist.is_initialized() else 1
     rank = dist.get_rank() if dist is not None and dist.is_initialized() else 0
     store = None
@@ -163,7 +166,7 @@ def shared_queue(n: int, dist=None):
         yield from range(rank, n, world)
         return
     _queue_uses[0] += 1
-    key = f"ngsep_queue_{_queue_uses[0]}"
+    key = f"ngsep_queue_{_queue_uses[0]}_{tag}"
     while True:
         i = int(store.add(key, 1)) - 1
         if i >= n:
@@ -193,7 +196,8 @@ def call_windows(contigs: Sequence[Tuple[str, int]], call_region: Callable[[str,
     units = window_units(contigs, compute_cuts(contigs, window, cut_fn, dist))
     header = ""
     local: Dict[Tuple[str, int], str] = {}
-    for i in shared_queue(len(units), dist):
+    tag = "%08x" % zlib.crc32(repr(units).encode())
+    for i in shared_queue(len(units), dist, tag):
         name, k, first, last, lead = units[i]
         h, recs = keep_window(call_region(name, max(1, first - lead), last), first, last)
         header = header or h
@@ -215,8 +219,8 @@ def call_windows(contigs: Sequence[Tuple[str, int]], call_region: Callable[[str,
                 merged[key] = rec
     else:
         merged = local
-    if not header:                                    # (no window anywhere: the header of an empty region run)
-        header, _ = keep_window(call_region(contigs[0][0], 1, 0) if contigs else "", 1, 0)
+    if not header:                                    # (no window anywhere: the header of a one-position region run)
+        header, _ = keep_window(call_region(contigs[0][0], 1, 1) if contigs else "", 1, 0)
     text = header + "".join(merged.get((u[0], u[1]), "") for u in units)
     with open(out_vcf, "w") as f:
         f.write(text)
@@ -342,6 +346,11 @@ def call_bam_sharded(fasta: str, bam: str, out_vcf: str, params=None, dist=None,
     if device is None:
         device = int(os.environ.get("LOCAL_RANK", "0"))
     caller = gpu_contig_caller(fasta, bam, params, device, known_vcf)
+    if params is not None and getattr(params, "indel_passthrough", 0):
+        # pass-through mode carves [first - R, last + R] around every indel read with R from the run's own longest
+        # span: a window's run would see a local R and re-carve its lead-in, so the carve-out (and the positions it
+        # leaves uncalled) would depend on the cuts -- whole sequences only
+        window = 0
     try:
         if window > 0:
             text = call_windows(contigs, caller.region, caller.cut, out_vcf, window, dist)

@@ -187,3 +187,40 @@ def test_known_variants_refused_types(tmp_path):
                           f"{name}\t30\t.\tA\tN\t.\t.\t.\n{name}\t40\t.\tA\tC\t.\t.\tSVTYPE=DEL\n")
     s.set_known_variants(good)
     s.close()
+
+
+@pytest.mark.gpu
+def test_cleared_known_variants_equal_fresh_discovery(tmp_path):
+    """ngsep_set_known_variants(c, NULL) returns the session to discovery: the previous file's records stop being the
+    realigner's input variants (no region opened, no event counted by ngsep_clean_cut), so the VCF equals a fresh
+    session's -- after a cleared file and after a refused one."""
+    kw = dict(genome=pysynth.YEAST, n_contigs=1, depth=15, seed=64, snv_rate=2e-3, indel_rate=4e-4)
+    syn = pysynth.Synth(**kw)
+    base = os.path.join(str(tmp_path), "kc")
+    fa, sam, bam = syn.write(base)
+    disc = os.path.join(str(tmp_path), "disc.vcf")
+    ngsep_oracle.run_ssvd(fa, sam, disc)
+    known = os.path.join(str(tmp_path), "known.vcf")
+    _known_vcf_indels(known, syn, disc, kw["seed"])
+    name = syn.contigs()[0][0]
+    syn.close()
+    bad = os.path.join(str(tmp_path), "bad.vcf")
+    with open(bad, "w") as o:
+        o.write("#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\n" + f"{name}\t10\t.\tA\tC,G\t.\t.\t.\n")
+    fresh = os.path.join(str(tmp_path), "fresh.vcf")
+    with GpuPileupSession(gpu_params()) as s:
+        s.load_fasta(fa)
+        s.processFile(bam, fresh)
+    want = open(fresh).read()
+    for second in (None, bad):
+        out = os.path.join(str(tmp_path), "again.vcf")
+        with GpuPileupSession(gpu_params()) as s:
+            s.load_fasta(fa)
+            s.set_known_variants(known)
+            if second is None:
+                s.set_known_variants(None)
+            else:
+                with pytest.raises(Exception):
+                    s.set_known_variants(second)
+            s.processFile(bam, out)
+        assert open(out).read() == want

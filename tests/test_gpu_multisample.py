@@ -329,3 +329,37 @@ def test_population_sample_without_reads(tmp_path):
     d = diff_vcf(o, g)
     assert not d, "\n".join(d[:20])
     assert n_records(o) > 10
+
+
+def test_population_long_span_alignment(tmp_path):
+    """One alignment with a 30 kb reference skip (CIGAR N) in a 100-sample population: the per-sample column bound
+    KPM's gather is sized by is the true per-sample coverage (a sweep over the starts and ends), not the reads
+    starting within the run's longest span -- which this one alignment would inflate past the kernel's columns and
+    refuse.  Path B (one BAM, 100 read groups) == the oracle."""
+    from ngsepcore_amd import MultisampleVariantsDetector
+    syn, fa, sam, rgs = population(tmp_path, genome=pysynth.CUSTOM, custom_len=60000, seed=9, n_samples=100,
+                                   depth=10, snv_rate=3e-3)
+    name, seq = syn.contigs()[0]
+    syn.close()
+    seq = bytes(seq).decode().upper()
+    p, gap = 5001, 30000
+    bases = seq[p - 1:p - 1 + 60] + seq[p - 1 + 60 + gap:p - 1 + 120 + gap]
+    rec = "\t".join(["longskip", "0", name, str(p), "60", f"60M{gap}N60M", "*", "0", "0", bases, "I" * 120,
+                     "RG:Z:S000"]) + "\n"
+    head, body = [], []
+    for l in open(sam):
+        (head if l.startswith("@") else body).append(l)
+    k = next(i for i, l in enumerate(body) if int(l.split("\t")[3]) > p)
+    body.insert(k, rec)
+    sam2 = os.path.join(str(tmp_path), "long.sam")
+    with open(sam2, "w") as f:
+        f.writelines(head + body)
+    bam = pysynth.sam_to_bam(sam2, os.path.join(str(tmp_path), "long.bam"))
+    o = oracle_mvd(tmp_path, fa, sam2)
+    d = MultisampleVariantsDetector()
+    d.setGenome(fa)
+    d.setOutFilename(os.path.join(str(tmp_path), "gpu_long.vcf"))
+    d.run([bam])
+    diff = diff_vcf(o, d.outFilename)
+    assert not diff, "\n".join(diff[:20])
+    assert n_records(o) > 20

@@ -323,10 +323,13 @@ def test_gpu_sharded_passthrough_carved_bed(tmp_path):
         want = s.carved_regions()
     assert len(want) > 3
     out = os.path.join(str(tmp_path), "m.vcf")
-    merged = call_bam_sharded(fa, bam, out, params=gpu_params(indel_passthrough=1))
-    assert merged == open(full).read()
-    bed = [l.split("\t") for l in open(out + ".carved.bed").read().splitlines()]
-    assert [(n, int(a) + 1, int(b)) for n, a, b in bed] == want
+    # (20 kb windows: pass-through mode must not cut a sequence -- its carve-out uses the run's longest span -- so the
+    # driver falls back to whole sequences and neither the VCF nor the BED depends on the window size)
+    for window in (4 << 20, 20000):
+        merged = call_bam_sharded(fa, bam, out, params=gpu_params(indel_passthrough=1), window=window)
+        assert merged == open(full).read()
+        bed = [l.split("\t") for l in open(out + ".carved.bed").read().splitlines()]
+        assert [(n, int(a) + 1, int(b)) for n, a, b in bed] == want
 
 
 def _window_worker(rank, world, port, fa, sam, bam, contigs, out_dir, window, multi):
