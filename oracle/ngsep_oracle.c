@@ -291,6 +291,7 @@ typedef struct ngo_aln {
     uint8_t* quals;          /* NULL if '*' */
     int ignore_start, ignore_end;
     int16_t* acl;            /* alleleCallLength, :747-834 */
+    int id;                  /* the record's ordinal among the SAM's alignment lines (the realigner trace's key) */
     int has_indel;
     int n_indel, cap_indel;  /* indelCalls (TreeMap by refPos: ascending), rebuilt with acl */
     ngo_indel* indel;
@@ -1533,6 +1534,28 @@ static void mvd_on_pileup(ngo_gen* G, int pos) {
 }
 
 #include "ngsep_oracle_indel.inc"
+
+/* ---- realigner trace (test infrastructure: NGO_REALIGN_TRACE=path; tests/test_oracle_realigner_kat.py compares it with
+ * the independent Python restatement tests/realigner_restatement.py).  Per pileup the realigner ran on:
+ * "P pos span str newSTR embedded"; when the span is > 1 the pileup's getAlleleCalls(span, null) as "C allele quals";
+ * per alignment leaving the pending list (or left at the end): "A id first last CIGAR ignoreStart ignoreEnd". */
+static FILE* g_rtrace = NULL;
+static void rtrace_pileup(ngo_aln** alns, int n, int pos, int span, int is_str, int is_new_str, int embedded) {
+    if (!g_rtrace) return;
+    fprintf(g_rtrace, "P\t%d\t%d\t%d\t%d\t%d\n", pos, span, is_str, is_new_str, embedded);
+    if (span <= 1) return;
+    ngo_icalls calls = {0};
+    pileup_calls(alns, n, pos, span, &calls);
+    for (int i = 0; i < calls.n; i++) fprintf(g_rtrace, "C\t%s\t%s\n", calls.c[i].allele, calls.c[i].qual);
+    icalls_free(&calls);
+}
+static void rtrace_aln(const ngo_aln* a) {
+    if (!g_rtrace) return;
+    static const char kOps[] = "HDIMPNSX";
+    fprintf(g_rtrace, "A\t%d\t%d\t%d\t", a->id, a->first, a->last);
+    for (int i = 0; i < a->n_ops; i++) fprintf(g_rtrace, "%d%c", a->ops[i] / 8, kOps[a->ops[i] & 7]);
+    fprintf(g_rtrace, "\t%d\t%d\n", a->ignore_start, a->ignore_end);
+}
 struct ngo_indel_call_s { ngo_indel_call c; int ploidy; };
 static void free_indel_call(struct ngo_indel_call_s* c) { for (int i = 0; i < c->c.n; i++) free(c->c.alleles[i]); free(c); }
 static void print_indel_call_any(FILE* out, const char* seqName, const ngo_call* c) { print_indel_call(out, seqName, &c->indel->c, c->indel->ploidy); }
@@ -2392,6 +2415,7 @@ static int process_current_position(ngo_gen* G) {
                 realigner_input_at(G, pos, &var_first, &var_last, &var_str);
                 const int span = realigner_on_pileup(&G->g->s[G->cur_seq], G->pileup.a, G->pileup.n, pos, var_first, var_last,
                                                      var_str, &is_str, &is_new_str, &r_embedded);
+                rtrace_pileup(G->pileup.a, G->pileup.n, pos, span, is_str, is_new_str, r_embedded);
                 if (G->known) mvd_on_pileup_known(G, pos);
                 else mvd_on_pileup_realign(G, pos, span, is_str, is_new_str, r_embedded);
             } else {
@@ -2415,6 +2439,7 @@ static int process_current_position(ngo_gen* G) {
             realigner_input_at(G, pos, &var_first, &var_last, &var_str);
             span = realigner_on_pileup(&G->g->s[G->cur_seq], G->pileup.a, G->pileup.n, pos, var_first, var_last, var_str, &is_str,
                                        &is_new_str, &r_embedded);
+            rtrace_pileup(G->pileup.a, G->pileup.n, pos, span, is_str, is_new_str, r_embedded);
         }
     }
     ngo_counts h;
@@ -2481,7 +2506,7 @@ static void update_pending(ngo_gen* G) {
     for (int i = 0; i < G->pending.n; i++) {
         ngo_aln* a = G->pending.a[i];
         if (a->last >= G->cur_pos) G->pending.a[k++] = a;
-        else alist_push(&G->retired, a);
+        else { rtrace_aln(a); alist_push(&G->retired, a); }
     }
     G->pending.n = k;
     for (int i = 0; i < G->retired.n; i++) aln_free(G->retired.a[i]);
@@ -2841,6 +2866,10 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
     FILE* out = strcmp(out_vcf, "-") == 0 ? stdout : fopen(out_vcf, "w");
     if (!out) { fclose(in); return NGO_ERR_IO; }
     FILE* dump = dump_path ? fopen(dump_path, "w") : NULL;
+    {
+        const char* tp = getenv("NGO_REALIGN_TRACE");
+        g_rtrace = tp && tp[0] ? fopen(tp, "w") : NULL;
+    }
 
     ngo_gen G; memset(&G, 0, sizeof(G));
     G.p = p; G.g = &g; G.out = out; G.dump = dump; G.cur_seq = -1; G.st = st;
@@ -2979,6 +3008,7 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
         if (seq < 0) continue;   /* sequence not in the reference: loadAlignment throws, record skipped */
         ngo_aln* a = calloc(1, sizeof(ngo_aln));
         a->seq = seq; a->first = start; a->flags = flags; a->rg = rg;
+        a->id = (int)st->alignments_read - 1;
         int seqlen = strcmp(f[9], "*") == 0 ? 0 : (int)strlen(f[9]);
         a->read_length = seqlen;
         if (strcmp(f[5], "*") == 0 || parse_cigar(f[5], &a->ops, &a->n_ops) != 0) { aln_free(a); continue; }
@@ -3031,7 +3061,8 @@ static int run_detector(const char* fasta, const char* sam, const char* out_vcf,
     free(line); free(last_qname); fclose(in);
     if (out != stdout) fclose(out); else fflush(out);
     if (dump) fclose(dump);
-    for (int i = 0; i < G.pending.n; i++) aln_free(G.pending.a[i]);
+    for (int i = 0; i < G.pending.n; i++) { rtrace_aln(G.pending.a[i]); aln_free(G.pending.a[i]); }
+    if (g_rtrace) { fclose(g_rtrace); g_rtrace = NULL; }
     for (int i = 0; i < G.ss_primary.n; i++) aln_free(G.ss_primary.a[i]);
     for (int i = 0; i < G.ss_secondary.n; i++) aln_free(G.ss_secondary.a[i]);
     for (int i = 0; i < G.calls.n; i++) {
