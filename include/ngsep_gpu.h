@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define NGSEP_ABI_VERSION 10
+#define NGSEP_ABI_VERSION 11
 
 #define NGSEP_OK 0
 #define NGSEP_E_INVALID (-1)      /* bad argument / state */
@@ -334,6 +334,27 @@ int ngsep_call_region_bam(ngsep_ctx* ctx, const char* bam_path, const char* seq,
  * exists.  Reads the files' BAI indexes; deterministic in (files, seq, pos). */
 int ngsep_clean_cut(ngsep_ctx* ctx, const char* const* bam_paths, int32_t n_files, const char* seq, int64_t pos,
                     int64_t* cut, int64_t* lead);
+
+/* ABI 11: several devices from ONE process -- the drop-in's multi-GPU run of
+ * SingleSampleVariantsDetector.findSNVS (:896-931) / MultisampleVariantsDetector.run (:421-459).  ctxs[0..n_ctx) are
+ * open contexts, one per device (ngsep_open(device_k, params), the same params); the first holds the reference (and the
+ * -knownVariants / -knownSTRs inputs); a later context without a reference takes the first one's.  Every header
+ * sequence of the (first) BAM is cut into windows of about `window` bp at ngsep_clean_cut boundaries (window <= 0, or
+ * indel pass-through mode: whole sequences); one host thread per context takes windows from an in-process queue and
+ * runs each as a region (ngsep_call_region_bam / ngsep_call_population_region_bams from the cut minus its lead-in:
+ * AlignmentsPileupGenerator.java:242-254,310-322), on its own device, streams and pinned buffers, keeping the records
+ * inside the window; out_vcf_path gets the header and the windows' records in (sequence, window) order -- the
+ * one-context VCF.  Temporary files out_vcf_path.part<k> are removed.  Errors are reported on ctxs[0]; in pass-through
+ * mode every context's carved regions end up on ctxs[0] (ngsep_fetch_carved_regions). */
+int ngsep_call_bam_multi(ngsep_ctx* const* ctxs, int32_t n_ctx, const char* bam_path, const char* out_vcf_path,
+                         int64_t window);
+int ngsep_call_population_bams_multi(ngsep_ctx* const* ctxs, int32_t n_ctx, const char* const* bam_paths, int32_t n_files,
+                                     const char* out_vcf_path, int64_t window);
+/* the windows those drivers (and ngsepcore_amd/sharding.py) run: for i < min(*n_out, cap), sequence seq_id[i] positions
+ * first[i]..last[i], run from first[i] - lead[i]; every header sequence the reference holds is covered once, in order
+ * (host only: reads the BAM header and the BAI neighbourhoods of the nominal cuts) */
+int ngsep_plan_windows(ngsep_ctx* ctx, const char* const* bam_paths, int32_t n_files, int64_t window, int32_t* seq_id,
+                       int64_t* first, int64_t* last, int64_t* lead, int64_t cap, int64_t* n_out);
 
 /* ---- CoverageStatisticsCalculator (discovery/CoverageStatisticsCalculator.java:108-216) ----
  * path A: params.coverage_stats = 1, alignments through ngsep_process_alignments, ngsep_notify_end runs

@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-ABI_VERSION = 10                                   # NGSEP_ABI_VERSION (include/ngsep_gpu.h)
+ABI_VERSION = 11                                   # NGSEP_ABI_VERSION (include/ngsep_gpu.h)
 DEFAULT_LIB_PATH = os.path.join(_HERE, "lib", "libngsep_amd.so")
 # NGSEP_LIB_PATH: an A/B tuning build of the same ABI, for measurements only.  It is announced on stderr when taken, and
 # bench.py records it in its line (config.lib_path), so no result can come from a swapped library silently.
@@ -201,6 +201,12 @@ SIGNATURES = {
     "ngsep_call_region_bam": (ctypes.c_int, [_CTX, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p]),
     "ngsep_clean_cut": (ctypes.c_int, [_CTX, P(ctypes.c_char_p), ctypes.c_int32, ctypes.c_char_p, ctypes.c_int64, P(ctypes.c_int64),
                                        P(ctypes.c_int64)]),
+    "ngsep_call_bam_multi": (ctypes.c_int, [P(_CTX), ctypes.c_int32, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64]),
+    "ngsep_call_population_bams_multi": (ctypes.c_int, [P(_CTX), ctypes.c_int32, P(ctypes.c_char_p), ctypes.c_int32,
+                                                        ctypes.c_char_p, ctypes.c_int64]),
+    "ngsep_plan_windows": (ctypes.c_int, [_CTX, P(ctypes.c_char_p), ctypes.c_int32, ctypes.c_int64, P(ctypes.c_int32),
+                                          P(ctypes.c_int64), P(ctypes.c_int64), P(ctypes.c_int64), ctypes.c_int64,
+                                          P(ctypes.c_int64)]),
     "ngsep_stage_alignments": (ctypes.c_int, [_CTX, P(NgsepReadBatch)]),
     "ngsep_stage_finish": (ctypes.c_int, [_CTX]),
     "ngsep_run_staged": (ctypes.c_int, [_CTX, P(ctypes.c_double)]),

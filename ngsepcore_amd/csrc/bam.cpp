@@ -17,6 +17,7 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -127,6 +128,7 @@ struct ngsep_bam {
     bool eof = false;
     std::vector<int32_t> ref_to_seq;   // BAM refID -> ctx sequence id
     std::vector<std::string> ref_names;
+    std::vector<int64_t> ref_lens;     // (their @SQ lengths)
     std::vector<std::string> rg_ids;   // header read groups
     std::vector<std::string> rg_sm;    // their SM tags (the read group id when absent, ReadAlignmentFileReader.java:186-188)
     std::unordered_map<std::string, int32_t> rg_index;
@@ -414,6 +416,7 @@ extern "C" int ngsep_bam_open(ngsep_ctx* c, const char* path, ngsep_bam** out) {
         int32_t lref = rd<int32_t>(&b->buf[b->pos + 4 + ln]);
         b->pos += 8 + (size_t)ln;
         b->ref_names.push_back(name);
+        b->ref_lens.push_back(lref);
         if (header_seqs && !seq_index.count(name)) {
             seq_index[name] = (int32_t)c->seq_names.size();
             c->seq_names.push_back(name);
@@ -1571,4 +1574,229 @@ extern "C" int ngsep_call_population_region_bams(ngsep_ctx* c, const char* const
     c->pop_order.clear();
     c->pop_text.clear();
     return rc;
+}
+
+// ---- several devices from one process ----
+// The windows of ngsep_clean_cut (AlignmentsPileupGenerator.java:242-254,310-322: each window a querySeq region run from
+// its cut minus the lead-in) handed to one host thread per context from an in-process queue; each thread drives its own
+// context -- its device, HIP streams and pinned buffers -- and keeps the records inside its window; the blocks are
+// written in (sequence, window) order.  The output equals the one-context run (tests/test_gpu_multi.py).
+namespace {
+struct MultiUnit { int32_t seq; int64_t first, last, lead; };
+
+// the windows of every header sequence the reference holds (window <= 0: whole sequences), cut points monotone
+int plan_windows(ngsep_ctx* const* ctxs, int32_t n_ctx, const char* const* bams, int32_t n_files, int64_t window,
+                 std::vector<MultiUnit>& units) {
+    ngsep_ctx* c0 = ctxs[0];
+    ngsep_bam* b = nullptr;
+    int rc = ngsep_bam_open(c0, bams[0], &b);
+    if (rc != NGSEP_OK) return rc;
+    std::vector<std::pair<int32_t, int64_t>> seqs;      // (sequence id, @SQ length) in header order
+    for (size_t i = 0; i < b->ref_names.size(); i++) {
+        int32_t sid = -1;
+        for (size_t k = 0; k < c0->seq_names.size(); k++) if (c0->seq_names[k] == b->ref_names[i]) { sid = (int32_t)k; break; }
+        if (sid >= 0) seqs.push_back({sid, std::min<int64_t>(b->ref_lens[i], (int64_t)c0->seq_bases[(size_t)sid].size())});
+    }
+    ngsep_bam_close(b);
+    struct Cut { size_t seq; int64_t pos, cut = 0, lead = 0; };
+    std::vector<Cut> cuts;
+    for (size_t q = 0; q < seqs.size(); q++)
+        if (window > 0)
+            for (int64_t p = 1 + window; p <= seqs[q].second; p += window) cuts.push_back({q, p});
+    // the cuts on every context's thread (each reads the BAI neighbourhood of its positions)
+    std::atomic<size_t> next{0};
+    std::atomic<int> bad{NGSEP_OK};
+    std::vector<std::string> errs((size_t)n_ctx);
+    auto work = [&](int t) {
+        for (size_t i; (i = next.fetch_add(1)) < cuts.size() && bad.load() == NGSEP_OK;) {
+            Cut& x = cuts[i];
+            const int r = ngsep_clean_cut(ctxs[t], bams, n_files, ctxs[t]->seq_names[(size_t)seqs[x.seq].first].c_str(), x.pos,
+                                          &x.cut, &x.lead);
+            if (r != NGSEP_OK) { errs[(size_t)t] = ctxs[t]->err; bad.store(r); }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < n_ctx; t++) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    if (bad.load() != NGSEP_OK) {
+        for (const std::string& e : errs) if (!e.empty()) return set_error(c0, bad.load(), e);
+        return bad.load();
+    }
+    size_t k = 0;
+    for (size_t q = 0; q < seqs.size(); q++) {
+        const int64_t len = seqs[q].second;
+        std::vector<int64_t> bnd{1}, lead{0};
+        for (; k < cuts.size() && cuts[k].seq == q; k++) {
+            bnd.push_back(std::max(bnd.back(), std::min(cuts[k].cut, len + 1)));
+            lead.push_back(cuts[k].lead);
+        }
+        bnd.push_back(len + 1);
+        for (size_t i = 0; i + 1 < bnd.size(); i++)
+            if (bnd[i] < bnd[i + 1]) units.push_back({seqs[q].first, bnd[i], bnd[i + 1] - 1, lead[i]});
+    }
+    return NGSEP_OK;
+}
+
+// the records of a VCF file with first <= POS <= last (its header into *header when that is empty)
+bool keep_window(const std::string& path, int64_t first, int64_t last, std::string* header, std::string& recs) {
+    std::FILE* f = std::fopen(path.c_str(), "r");
+    if (!f) return false;
+    char* line = nullptr;
+    size_t cap = 0;
+    ssize_t l;
+    const bool want_header = header->empty();
+    while ((l = getline(&line, &cap, f)) >= 0) {
+        if (line[0] == '#') {
+            if (want_header) header->append(line, (size_t)l);
+            continue;
+        }
+        const char* t = std::strchr(line, '\t');
+        if (!t) continue;
+        const long long pos = std::atoll(t + 1);
+        if (pos >= first && pos <= last) recs.append(line, (size_t)l);
+    }
+    std::free(line);
+    std::fclose(f);
+    return true;
+}
+
+int multi_run(ngsep_ctx* const* ctxs, int32_t n_ctx, const char* const* bams, int32_t n_files, const char* out_vcf,
+              int64_t window, bool population) {
+    if (!ctxs || n_ctx < 1 || !bams || n_files < 1 || !out_vcf) return NGSEP_E_INVALID;
+    for (int32_t t = 0; t < n_ctx; t++) if (!ctxs[t]) return NGSEP_E_INVALID;
+    ngsep_ctx* c0 = ctxs[0];
+    if (c0->seq_names.empty()) return set_error(c0, NGSEP_E_INVALID, "load the reference into the first context");
+    for (int32_t t = 1; t < n_ctx; t++) {
+        ngsep_ctx* c = ctxs[t];
+        for (int32_t u = 0; u < t; u++)
+            if (ctxs[u] == c) return set_error(c0, NGSEP_E_INVALID, "a context is listed twice (one host thread drives each)");
+        ngsep_params a = c0->params, b = c->params;
+        if (std::memcmp(&a, &b, sizeof a) != 0) return set_error(c0, NGSEP_E_INVALID, "the contexts' parameters differ");
+        if (c->seq_names.empty()) {                    // the first context's reference and input variants
+            c->seq_names = c0->seq_names;
+            c->seq_bases = c0->seq_bases;
+            c->known = c0->known;
+            c->known_recs = c0->known_recs;
+            c->known_seq_begin = c0->known_seq_begin;
+            c->known_given = c0->known_given;
+            c->strs = c0->strs;
+            c->het_rate = c0->het_rate;
+        } else if (c->seq_names != c0->seq_names) {
+            return set_error(c0, NGSEP_E_INVALID, "the contexts' references differ");
+        }
+    }
+    // pass-through mode carves with the run's own longest span: whole sequences only (sharding.call_bam_sharded)
+    if (c0->params.indel_passthrough) window = 0;
+    std::vector<MultiUnit> units;
+    int rc = plan_windows(ctxs, n_ctx, bams, n_files, window, units);
+    if (rc != NGSEP_OK) return rc;
+    std::vector<std::string> blocks(units.size()), headers((size_t)n_ctx), errs((size_t)n_ctx);
+    std::atomic<size_t> next{0};
+    std::atomic<int> bad{NGSEP_OK};
+    const std::string tmp_base = std::string(out_vcf) + ".part";
+    auto work = [&](int t) {
+        ngsep_ctx* c = ctxs[t];
+        const std::string tmp = tmp_base + std::to_string(t);
+        for (size_t i; (i = next.fetch_add(1)) < units.size() && bad.load() == NGSEP_OK;) {
+            const MultiUnit& u = units[i];
+            const char* seq = c->seq_names[(size_t)u.seq].c_str();
+            const int64_t from = std::max<int64_t>(1, u.first - u.lead);
+            const int r = population ? ngsep_call_population_region_bams(c, bams, n_files, seq, from, u.last, tmp.c_str())
+                                     : ngsep_call_region_bam(c, bams[0], seq, from, u.last, tmp.c_str());
+            if (r != NGSEP_OK) { errs[(size_t)t] = c->err; bad.store(r); break; }
+            if (!keep_window(tmp, u.first, u.last, &headers[(size_t)t], blocks[i])) {
+                errs[(size_t)t] = "cannot read " + tmp;
+                bad.store(NGSEP_E_IO);
+                break;
+            }
+        }
+        std::remove(tmp.c_str());
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < n_ctx; t++) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    if (bad.load() != NGSEP_OK) {
+        for (const std::string& e : errs) if (!e.empty()) return set_error(c0, bad.load(), e);
+        return bad.load();
+    }
+    std::string header;
+    for (const std::string& h : headers) if (!h.empty()) { header = h; break; }
+    if (header.empty()) {                               // no window anywhere: the header of the run's options
+        if (!population) {
+            if ((rc = ngsep_write_vcf_header(c0, out_vcf)) != NGSEP_OK) return rc;
+            std::FILE* f = std::fopen(out_vcf, "r");
+            if (!f) return set_error(c0, NGSEP_E_IO, std::string("cannot read ") + out_vcf);
+            char buf[1 << 16];
+            size_t n;
+            while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) header.append(buf, n);
+            std::fclose(f);
+        } else if (!c0->seq_names.empty()) {
+            const std::string tmp = tmp_base + "h";
+            rc = ngsep_call_population_region_bams(c0, bams, n_files, c0->seq_names[0].c_str(), 1, 1, tmp.c_str());
+            std::string none;
+            if (rc == NGSEP_OK) keep_window(tmp, 1, 0, &header, none);
+            std::remove(tmp.c_str());
+            if (rc != NGSEP_OK) return rc;
+        }
+    }
+    std::FILE* f = std::fopen(out_vcf, "w");
+    if (!f) return set_error(c0, NGSEP_E_IO, std::string("cannot write ") + out_vcf);
+    std::fwrite(header.data(), 1, header.size(), f);
+    for (const std::string& b : blocks) std::fwrite(b.data(), 1, b.size(), f);
+    const bool ok = std::fclose(f) == 0;
+    if (!ok) return set_error(c0, NGSEP_E_IO, std::string("cannot write ") + out_vcf);
+    // pass-through mode: every context's carved regions, in sequence then position order, on the first context
+    if (c0->params.indel_passthrough) {
+        for (int32_t t = 1; t < n_ctx; t++) {
+            c0->carved.insert(c0->carved.end(), ctxs[t]->carved.begin(), ctxs[t]->carved.end());
+            ctxs[t]->carved.clear();
+        }
+        std::vector<int32_t> order(c0->seq_names.size(), 0);
+        {
+            ngsep_bam* b = nullptr;
+            if (ngsep_bam_open(c0, bams[0], &b) == NGSEP_OK) {
+                for (size_t i = 0; i < b->ref_names.size(); i++)
+                    for (size_t k = 0; k < c0->seq_names.size(); k++) if (c0->seq_names[k] == b->ref_names[i]) order[k] = (int32_t)i;
+                ngsep_bam_close(b);
+            }
+        }
+        std::sort(c0->carved.begin(), c0->carved.end(), [&](const auto& x, const auto& y) {
+            if (order[(size_t)x.first] != order[(size_t)y.first]) return order[(size_t)x.first] < order[(size_t)y.first];
+            return x.second < y.second;
+        });
+    }
+    return NGSEP_OK;
+}
+}  // namespace
+
+extern "C" int ngsep_call_bam_multi(ngsep_ctx* const* ctxs, int32_t n_ctx, const char* bam_path, const char* out_vcf_path,
+                                    int64_t window) {
+    const char* bams[1] = {bam_path};
+    if (!bam_path) return NGSEP_E_INVALID;
+    return multi_run(ctxs, n_ctx, bams, 1, out_vcf_path, window, false);
+}
+
+extern "C" int ngsep_call_population_bams_multi(ngsep_ctx* const* ctxs, int32_t n_ctx, const char* const* bam_paths,
+                                                int32_t n_files, const char* out_vcf_path, int64_t window) {
+    return multi_run(ctxs, n_ctx, bam_paths, n_files, out_vcf_path, window, true);
+}
+
+extern "C" int ngsep_plan_windows(ngsep_ctx* c, const char* const* bam_paths, int32_t n_files, int64_t window, int32_t* seq_id,
+                                  int64_t* first, int64_t* last, int64_t* lead, int64_t cap, int64_t* n_out) {
+    if (!c || !bam_paths || n_files < 1 || !n_out) return NGSEP_E_INVALID;
+    if (c->seq_names.empty()) return set_error(c, NGSEP_E_INVALID, "load the reference before planning windows");
+    std::vector<MultiUnit> units;
+    ngsep_ctx* one[1] = {c};
+    const int rc = plan_windows(one, 1, bam_paths, n_files, c->params.indel_passthrough ? 0 : window, units);
+    if (rc != NGSEP_OK) return rc;
+    *n_out = (int64_t)units.size();
+    for (int64_t i = 0; i < (int64_t)units.size() && i < cap; i++) {
+        if (seq_id) seq_id[i] = units[(size_t)i].seq;
+        if (first) first[i] = units[(size_t)i].first;
+        if (last) last[i] = units[(size_t)i].last;
+        if (lead) lead[i] = units[(size_t)i].lead;
+    }
+    return NGSEP_OK;
 }

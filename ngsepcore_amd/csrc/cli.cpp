@@ -31,12 +31,51 @@ static void report_carved(ngsep_ctx* c, const std::string& prefix) {
                  "(the indel realigner's reach); listed in %s\n", (long long)n, (long long)total, path.c_str());
 }
 
+// -devices 0,1,...: one context per device, the windows of ngsep_call_bam_multi / ngsep_call_population_bams_multi
+// (SURVEY.md 8(e)); empty: the single -device
+static std::vector<int> parse_devices(const char* v) {
+    std::vector<int> d;
+    for (const char* t = v; t && *t;) {
+        d.push_back(std::atoi(t));
+        t = std::strchr(t, ',');
+        if (t) t++;
+    }
+    return d;
+}
+
+// opens one context per device (the first loads the reference and the input variants; the others take them from it)
+static int open_contexts(const std::vector<int>& devices, const ngsep_params& p, const char* ref, const char* known,
+                         const char* strs, std::vector<ngsep_ctx*>& ctxs) {
+    int rc = NGSEP_OK;
+    for (int d : devices) {
+        ngsep_ctx* c = nullptr;
+        rc = ngsep_open(d, &p, &c);
+        if (c) ctxs.push_back(c);
+        if (rc != NGSEP_OK) return rc;
+    }
+    rc = ngsep_load_fasta(ctxs[0], ref);
+    if (rc == NGSEP_OK && known) rc = ngsep_set_known_variants(ctxs[0], known);
+    else if (rc == NGSEP_OK && strs) rc = ngsep_set_known_strs(ctxs[0], strs);   // (:897-912: -knownVariants first)
+    return rc;
+}
+
+static void print_stats(const std::vector<ngsep_ctx*>& ctxs) {
+    long long a = 0, b = 0, q = 0, cnd = 0, v = 0;
+    for (ngsep_ctx* c : ctxs) {
+        ngsep_stats st;
+        ngsep_get_stats(c, &st);
+        a += st.alignments_in; b += st.alignments_admitted; q += st.positions_genotyped; cnd += st.candidates; v += st.sites_called;
+    }
+    std::fprintf(stderr, "alignments=%lld admitted=%lld positions=%lld candidates=%lld variants=%lld\n", a, b, q, cnd, v);
+}
+
 static int usage(const char* argv0) {
     std::fprintf(stderr,
                  "usage: %s SingleSampleVariantsDetector -i <alignments.bam> -r <reference.fa> -o <output prefix> [options]\n"
                  "options: -sampleId S -ploidy N -psp -minMQ N -maxAlnsPerStartPos N -p -s -ignore5 N -ignore3 N\n"
                  "         -h RATE -maxBaseQS N -minQuality N -ignoreLowerCaseRef -embeddedSNVs -csb\n"
-                 "         -querySeq SEQ -first N -last N -knownVariants VCF -device N\n", argv0);
+                 "         -querySeq SEQ -first N -last N -knownVariants VCF -knownSTRs FILE -device N\n"
+                 "         -devices N,N,... [-window BP]   (several GPUs of this process: windows from one queue)\n", argv0);
     return 2;
 }
 
@@ -48,6 +87,8 @@ static int main_mvd(int argc, char** argv, int i) {
     p.multisample = 1;
     const char *ref = nullptr, *outp = "variants.vcf", *known = nullptr, *strs = nullptr;
     int device = 0;
+    std::vector<int> devices;
+    long long window = 4 << 20;
     std::vector<const char*> bams;
     for (; i < argc; i++) {
         const char* a = argv[i];
@@ -68,6 +109,8 @@ static int main_mvd(int argc, char** argv, int i) {
         else if (takes("-first")) p.query_first = std::atoi(v);
         else if (takes("-last")) p.query_last = std::atoi(v);
         else if (takes("-device")) device = std::atoi(v);
+        else if (takes("-devices")) devices = parse_devices(v);
+        else if (takes("-window")) window = std::atoll(v);
         else if (takes("-knownVariants")) known = v;    // MultisampleVariantsDetector.setKnownVariantsFile (:193-195)
         else if (takes("-knownSTRs")) strs = v;         // the realigner's input STRs without -knownVariants (:439-446)
         else if (!std::strcmp(a, "-embeddedSNVs")) p.call_embedded = 1;
@@ -82,20 +125,21 @@ static int main_mvd(int argc, char** argv, int i) {
         std::fprintf(stderr, "usage: ngsep-amd MultisampleVariantsDetector -r <reference.fa> -o <out.vcf> [options] <BAM>...\n");
         return 2;
     }
-    ngsep_ctx* c = nullptr;
-    int rc = ngsep_open(device, &p, &c);
-    if (rc == NGSEP_OK) rc = ngsep_load_fasta(c, ref);
-    if (rc == NGSEP_OK && known) rc = ngsep_set_known_variants(c, known);
-    else if (rc == NGSEP_OK && strs) rc = ngsep_set_known_strs(c, strs);
-    if (rc == NGSEP_OK) rc = ngsep_call_population_bams(c, bams.data(), (int32_t)bams.size(), outp);
-    if (rc != NGSEP_OK) { std::fprintf(stderr, "error %d: %s\n", rc, c ? ngsep_last_error(c) : "open failed"); if (c) ngsep_close(c); return 1; }
-    ngsep_stats st;
-    ngsep_get_stats(c, &st);
-    std::fprintf(stderr, "alignments=%lld admitted=%lld positions=%lld candidates=%lld variants=%lld\n",
-                 (long long)st.alignments_in, (long long)st.alignments_admitted, (long long)st.positions_genotyped,
-                 (long long)st.candidates, (long long)st.sites_called);
-    report_carved(c, outp);
-    ngsep_close(c);
+    if (devices.empty()) devices.push_back(device);
+    std::vector<ngsep_ctx*> ctxs;
+    int rc = open_contexts(devices, p, ref, known, strs, ctxs);
+    if (rc == NGSEP_OK)
+        rc = ctxs.size() == 1 ? ngsep_call_population_bams(ctxs[0], bams.data(), (int32_t)bams.size(), outp)
+                              : ngsep_call_population_bams_multi(ctxs.data(), (int32_t)ctxs.size(), bams.data(),
+                                                                 (int32_t)bams.size(), outp, window);
+    if (rc != NGSEP_OK) {
+        std::fprintf(stderr, "error %d: %s\n", rc, ctxs.empty() ? "open failed" : ngsep_last_error(ctxs[0]));
+        for (ngsep_ctx* c : ctxs) ngsep_close(c);
+        return 1;
+    }
+    print_stats(ctxs);
+    report_carved(ctxs[0], outp);
+    for (ngsep_ctx* c : ctxs) ngsep_close(c);
     return 0;
 }
 
@@ -178,6 +222,8 @@ int main(int argc, char** argv) {
     ngsep_params_default(&p);
     const char *in = nullptr, *ref = nullptr, *outp = nullptr, *known = nullptr, *strs = nullptr;
     int device = 0;
+    std::vector<int> devices;
+    long long window = 4 << 20;
     int i = 1;
     if (i < argc && std::strcmp(argv[i], "MultisampleVariantsDetector") == 0) return main_mvd(argc, argv, i + 1);
     if (i < argc && std::strcmp(argv[i], "CoverageStats") == 0) return main_coverage(argc, argv, i + 1);
@@ -204,6 +250,8 @@ int main(int argc, char** argv) {
         else if (takes("-first")) p.query_first = std::atoi(v);
         else if (takes("-last")) p.query_last = std::atoi(v);
         else if (takes("-device")) device = std::atoi(v);
+        else if (takes("-devices")) devices = parse_devices(v);
+        else if (takes("-window")) window = std::atoll(v);
         else if (takes("-knownVariants")) known = v;
         else if (takes("-knownSTRs")) strs = v;
         else if (!std::strcmp(a, "-psp")) p.print_sample_ploidy = 1;
@@ -215,21 +263,24 @@ int main(int argc, char** argv) {
         else { std::fprintf(stderr, "unknown or unsupported option %s\n", a); return usage(argv[0]); }
     }
     if (!in || !ref || !outp) return usage(argv[0]);
-    ngsep_ctx* c = nullptr;
-    int rc = ngsep_open(device, &p, &c);
-    if (rc != NGSEP_OK) { std::fprintf(stderr, "error: %s\n", c ? ngsep_last_error(c) : "open failed"); return 1; }
-    rc = ngsep_load_fasta(c, ref);
-    if (rc == NGSEP_OK && known) rc = ngsep_set_known_variants(c, known);
-    else if (rc == NGSEP_OK && strs) rc = ngsep_set_known_strs(c, strs);   // (:897-912: -knownVariants first)
+    if (devices.empty()) devices.push_back(device);
+    if (devices.size() > 1 && p.query_seq[0]) {
+        std::fprintf(stderr, "-devices runs the whole file (windows over every sequence): without -querySeq\n");
+        return 2;
+    }
+    std::vector<ngsep_ctx*> ctxs;
+    int rc = open_contexts(devices, p, ref, known, strs, ctxs);
     std::string vcf = std::string(outp) + ".vcf";
-    if (rc == NGSEP_OK) rc = ngsep_call_bam(c, in, vcf.c_str());
-    if (rc != NGSEP_OK) { std::fprintf(stderr, "error %d: %s\n", rc, ngsep_last_error(c)); ngsep_close(c); return 1; }
-    ngsep_stats st;
-    ngsep_get_stats(c, &st);
-    std::fprintf(stderr, "alignments=%lld admitted=%lld positions=%lld candidates=%lld variants=%lld\n",
-                 (long long)st.alignments_in, (long long)st.alignments_admitted, (long long)st.positions_genotyped,
-                 (long long)st.candidates, (long long)st.sites_called);
-    report_carved(c, outp);
-    ngsep_close(c);
+    if (rc == NGSEP_OK)
+        rc = ctxs.size() == 1 ? ngsep_call_bam(ctxs[0], in, vcf.c_str())
+                              : ngsep_call_bam_multi(ctxs.data(), (int32_t)ctxs.size(), in, vcf.c_str(), window);
+    if (rc != NGSEP_OK) {
+        std::fprintf(stderr, "error %d: %s\n", rc, ctxs.empty() ? "open failed" : ngsep_last_error(ctxs[0]));
+        for (ngsep_ctx* c : ctxs) ngsep_close(c);
+        return 1;
+    }
+    print_stats(ctxs);
+    report_carved(ctxs[0], outp);
+    for (ngsep_ctx* c : ctxs) ngsep_close(c);
     return 0;
 }

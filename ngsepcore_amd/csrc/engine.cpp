@@ -125,6 +125,20 @@ void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g) {
         }
         t->cb_nr[na] = (int16_t)lo;
     }
+    // KLM's count bound: reference calls counted only when their quality is >= kKlmQs (the rest are exceptions and
+    // add nothing, a lower bound as every reference addend is >= 0), one call of another allele at its worst quality
+    long long h_r1 = INT64_MAX, h_r2 = INT64_MAX;
+    for (int q0 = kKlmQs; q0 <= 30; q0++) {
+        const int q = q0 > g->max_q ? g->max_q : q0;
+        h_r1 = std::min<long long>(h_r1, (long long)(t->wR[q] & 0xFFFFFFFFull));
+        h_r2 = std::min<long long>(h_r2, (long long)(t->wR[q] >> 32));
+    }
+    t->cb_hi1 = 256;
+    for (long long n = 0; n < 256; n++)
+        if (n * h_r1 - t->c_x1 > t->t_het && n * h_r2 - t->c_x2 > t->t_homo && n * h_r2 - t->c_x1 > t->t_het) {
+            t->cb_hi1 = (int32_t)n;
+            break;
+        }
 }
 
 // genotypeVariantPool's hypotheses (SingleSampleVariantPileupListener.java:408-416) and the CountsHelper

@@ -77,14 +77,10 @@ static_assert(sizeof(RGroup) == 16, "RGroup layout");
 constexpr int kRgBlockShift = 8;           // entry index tables per 256 positions (blkA / blkB)
 constexpr int kKlTile = 2048;              // positions per KL tile (one workgroup each; divides kRunAlign)
 constexpr int kMcMaxCalls = 254;           // multisample candidate column: valid calls the bounds take (sums fit 32 bits)
-#ifndef NGSEP_KLM_TILE                     // (build-time overrides: A/B builds only, tools/gpu_r4_klm.sh)
-#define NGSEP_KLM_TILE 2048
-#endif
-#ifndef NGSEP_KLM_SLOTS
-#define NGSEP_KLM_SLOTS 96
-#endif
-constexpr int kKlmTile = NGSEP_KLM_TILE;   // positions per KLM sample tile (one wavefront each; divides kRunAlign)
-constexpr int kKlmSlots = NGSEP_KLM_SLOTS; // KLM: candidate columns a sample tile bounds in LDS (more: kept open)
+constexpr int kKlmTile = 2048;             // positions per KLM sample tile (one wavefront each; divides kRunAlign)
+constexpr int kKlmSlots = 96;              // KLM: candidate columns a sample tile bounds exactly in LDS (more: kept open)
+constexpr int kKlmQs = 10;                 // KLM's count bound counts the reference calls of quality >= kKlmQs
+constexpr int kKlmCountMaxCov = 127;       // ... when no sample is deeper than this (its byte counters cannot carry)
 constexpr int kPopGatherCap = 40960;       // KPM (gather): LDS bytes for one position's columns ((S + 1) x the per-sample bound);
                                            // with KPM's 21 KB of static LDS, within the 64 KB a workgroup is given
 
@@ -124,6 +120,10 @@ struct LikTables {
     // the count bound as a table: with na other-allele calls, nr >= cb_nr[na] reference calls drop
     // the candidate (the three inequalities are non-decreasing in nr); 256: never (nr, na <= 255)
     int16_t cb_nr[256];
+    // KLM's count bound (multisample): a sample column with ONE valid call of another allele and
+    // at least cb_hi1 valid reference calls of quality >= kKlmQs is hom-ref (the reference addends at their minimum
+    // over q in [kKlmQs, 30], the other allele's at its maximum); 256: never
+    int32_t cb_hi1;
 };
 constexpr double kBoundScale = 1048576.0;   // 2^20: a tile holds <= 512 reads -> sums < 2^31
 constexpr long long kBoundMargin = 64;      // 6e-5 in log10 units, >> fp64 rounding of the sums

@@ -1423,84 +1423,117 @@ __global__ __launch_bounds__(256) void k_queue_need(const uint32_t* __restrict__
 // non-reference call there, and one whose valid calls the exact integer bound (§5) proves hom-ref cannot either
 // (SingleSampleVariantPileupListener.genotypeVariantSample, :361-391); a position where every sample is so proven
 // gets variant QS 0, which MultisampleVariantsDetector.onPileup never writes (:534).  Per sample tile:
-//   pass 1: the wave streams the sample's units over the tile (its read-group streams in turn; lane = read, as KL)
-//           and marks the positions holding a valid call of another allele (SWAR, kl_nonref) in an LDS bitmap;
-//   slots:  the marked positions (a few % of the sample's columns) get LDS slots in position order;
-//   pass 2: every lane adds the weights of its read's valid calls at the marked positions it covers (one 8-byte
-//           reload each: the units were just streamed) into its slot's {ref, alt 1, alt 2, alt 3} sums;
+//   pass 1: the wave streams the sample's units over the tile (its read-group streams in turn; lane = read, as KL),
+//           marks the positions holding a valid call of another allele (SWAR, kl_nonref) in an LDS bitmap (a second
+//           bitmap: marked twice) and, COUNT, tallies per position the bytes that are not a valid reference call of
+//           quality >= kKlmQs (packed byte counters, three LDS adds per unit that has one) and the reads' coverage
+//           (signed byte differences, two adds per read);
+//   count:  COUNT, a callable position marked once whose counted reference calls (coverage - exceptions) reach the
+//           count bound cb_hi1 is hom-ref for this sample: unmarked (about 97 % of the marked columns at 10x);
+//   slots:  the positions still marked get LDS slots in position order;
+//   pass 2: every lane adds the weights of its read's valid calls at the slotted positions it covers (one 8-byte
+//           reload each) into its slot's {ref, alt 1, alt 2, alt 3} sums -- the exact integer bound;
 //   pass 3: a slot the bound cannot prove hom-ref -- or holding more than kMcMaxCalls valid calls, or past
 //           kKlmSlots -- keeps its position open: one bit per global position (atomicOr); KQN queues them for KPM.
-// The reads of no sample only enter the pooled counts: not scanned.  No block barrier after the tables: every
-// wave's state is its own.
+// COUNT needs every sample's coverage below 128 (the host's per-sample bound, pop_stride): the byte counters and the
+// byte differences cannot carry.  Deeper populations run !COUNT: every marked position takes the exact bound.
+// The reads of no sample only enter the pooled counts: not scanned.  No block barrier after the tables: every wave's
+// state is its own.
+#ifndef NGSEP_KLM_COMPACT
+#define NGSEP_KLM_COMPACT 1
+#endif
 constexpr int kKlmThreads = 256;
 constexpr int kKlmWords = kKlmTile / 32 + 2;   // tile bitmap words, a 32-position margin on either side
-#ifndef NGSEP_KLM_PIPE
-#define NGSEP_KLM_PIPE 1     // (configs[4]: pipelined batches of 4 1.368-1.372 ms vs unpipelined 8 1.393-1.395 ms;
-#endif                       // pipelined 6 at 8 waves 1.422, tools/gpu_r4_klmabn.sh)
-#ifndef NGSEP_KLM_P2PRE
-#define NGSEP_KLM_P2PRE 1    // pass 2 fetches the next group's header and base a group ahead (configs[4]: scan 1.343-
-                             // 1.350 vs 1.377-1.419 ms; with 3 / 4 pending loads 1.42 / 1.45, tools/gpu_r4_klmabn.sh)
-#endif
-#ifndef NGSEP_KLM_P2DEPTH
-#define NGSEP_KLM_P2DEPTH 0  // A/B builds (with NGSEP_KLM_PEND 1): pass 2's loads in a queue of this depth
-#endif
-// pass 2 pipelined: a marked position's load issued before the previous one's adds (configs[4] scan 1.343-1.350 ->
-// 1.225-1.235 ms at 1 pending load; 2 pending 1.303-1.309; queues of depth 2 / 3 / 4: 1.275 / 1.320 / 1.431 ms,
-// tools/gpu_r4_klmabn.sh)
-#ifndef NGSEP_KLM_P2PIPE
-#define NGSEP_KLM_P2PIPE 1
-#endif
-#ifndef NGSEP_KLM_UNROLL
-#define NGSEP_KLM_UNROLL 4
-#endif
-constexpr int kKlmUnroll = NGSEP_KLM_UNROLL;    // pass 1: unit loads in flight per lane (NGSEP_KLM_PIPE: batches
-                                                // pipelined, the next batch's loads before the current one's marks)
-#ifndef NGSEP_KLM_PEND
-#define NGSEP_KLM_PEND 1
-#endif
-constexpr int kKlmPend = NGSEP_KLM_PEND;        // pass 2: marked-position loads issued together per lane
-#ifndef NGSEP_KLM_WPE
-#define NGSEP_KLM_WPE 1
-#endif
-constexpr int kKlmWpl = kKlmTile / 2048;      // bitmap words per lane in the slot scan
-static_assert(kKlmWpl >= 1 && kKlmWpl <= 4 && kKlmTile % 2048 == 0 && kRunAlign % kKlmTile == 0, "KLM tile");
+constexpr int kKlmUnroll = 4;                  // pass 1: unit loads per batch, the next batch issued before the current
+                                               // batch's marks (pipelined 4: 1.368-1.372 ms vs 8 unpipelined 1.393-1.395)
+constexpr int kKlmCntBytes = kKlmTile + 16;    // COUNT, per wave: exception byte counters (byte i + 8: tile position i)
+constexpr int kKlmDifBytes = kKlmTile + 16;    // COUNT, per wave: coverage differences, signed bytes (byte i: position i)
+constexpr int kKlmWaveLds = kKlmCntBytes + kKlmDifBytes;   // the exact bound's slots reuse it after the count
+static_assert(kKlmTile == 2048 && kRunAlign % kKlmTile == 0, "KLM tile: one bitmap word per lane");
+static_assert(kKlmSlots * (32 + 4 + 2) <= kKlmWaveLds, "KLM slots within the wave's counter space");
 
 __device__ __forceinline__ uint32_t nib4_byte7(uint32_t w) {   // bit 7 of the four bytes -> 4 bits
     return ((w >> 7) & 1u) | ((w >> 14) & 2u) | ((w >> 21) & 4u) | ((w >> 28) & 8u);
 }
+// KLM's exceptions, bit 7 of byte k: not a valid call of the reference's allele (kl_exc), or one of quality < kKlmQs
+__device__ __forceinline__ uint32_t klm_exc(uint32_t y) {
+    const uint32_t ge = ((y & 0x1F1F1F1Fu) | 0x80808080u) - 0x01010101u * (uint32_t)kKlmQs;   // bit 7 kept: q >= Qs
+    return (kl_exc(y) | ~ge) & 0x80808080u;
+}
+// the four signed byte differences packed in w (each |d| < 128: the sum is exact in 32 bits), in order
+__device__ __forceinline__ void unpack_dif(uint32_t w, int32_t d[4]) {
+    int32_t x = (int32_t)w;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        d[k] = (int32_t)(int8_t)(x & 0xFF);
+        x = (x - d[k]) >> 8;
+    }
+}
 
-__global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(NGSEP_KLM_WPE))) void k_scan_pop(
+#ifdef NGSEP_KLM_WPE
+#define KLM_WPE_ATTR __attribute__((amdgpu_waves_per_eu(NGSEP_KLM_WPE)))
+#else
+#define KLM_WPE_ATTR
+#endif
+template <bool COUNT>
+__global__ __launch_bounds__(kKlmThreads) KLM_WPE_ATTR void k_scan_pop(
     const uint64_t* __restrict__ units, const int2* __restrict__ rh, const RGroup* __restrict__ grp,
     const int32_t* __restrict__ samp_st, const int32_t* __restrict__ blkA, const int32_t* __restrict__ blkB,
     int64_t nblk, int32_t shift, int32_t n_samples, const uint8_t* __restrict__ ref, const LikTables* __restrict__ tabs,
     GenotypeParams gp, uint32_t* __restrict__ need, unsigned long long* __restrict__ counters) {
     __shared__ unsigned long long w[2][32];
-    __shared__ alignas(16) uint8_t s_ref[kKlmTile];         // the tile's reference codes
-    __shared__ uint32_t s_bm[4][kKlmWords];
-    __shared__ uint16_t s_wb[4][kKlmWords];            // slot of each bitmap word's first marked position
-    __shared__ unsigned long long s_acc[4][kKlmSlots * 4];
-    __shared__ uint32_t s_n[4][kKlmSlots];
-    __shared__ uint16_t s_pos[4][kKlmSlots];           // tile index of each slot
+    __shared__ uint32_t s_call[kKlmTile / 32];         // callable positions of the tile
+    __shared__ uint32_t s_bm[4][kKlmWords];            // marked positions, then those the exact bound takes
+    __shared__ uint32_t s_bm2[4][kKlmWords];           // (COUNT) marked at least twice
+    __shared__ uint16_t s_wb[4][kKlmWords];            // slot of each bitmap word's first slotted position
+    __shared__ alignas(16) uint32_t s_wave[4][kKlmWaveLds / 4];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (threadIdx.x < 64) w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
     const int nsg = (n_samples + 3) >> 2;
     const int64_t tile = (int64_t)blockIdx.x / nsg;
-    for (int i = threadIdx.x; i < kKlmTile / 16; i += kKlmThreads)
-        reinterpret_cast<uint4*>(s_ref)[i] = reinterpret_cast<const uint4*>(ref + tile * kKlmTile)[i];
-    __syncthreads();
+    {
+        // 8 positions' callable bits per thread (bit 7 of the reference code), four threads per word
+        const uint2 r = reinterpret_cast<const uint2*>(ref + tile * kKlmTile)[threadIdx.x];
+        uint32_t v = (nib4_byte7(r.x) | nib4_byte7(r.y) << 4) << (8 * (threadIdx.x & 3));
+        v |= __shfl_xor(v, 1, 64);
+        v |= __shfl_xor(v, 2, 64);
+        if ((threadIdx.x & 3) == 0) s_call[threadIdx.x >> 2] = v;
+    }
     const int s = (int)(blockIdx.x % nsg) * 4 + wv;
+    uint32_t* bm = s_bm[wv];
+    uint32_t* bm2 = s_bm2[wv];
+    uint32_t* cnt32 = s_wave[wv];
+    uint32_t* dif32 = s_wave[wv] + kKlmCntBytes / 4;
+    if (s < n_samples) {
+        for (int i = lane; i < kKlmWords; i += 64) { bm[i] = 0u; bm2[i] = 0u; }
+        if (COUNT)
+            for (int i = lane; i < kKlmWaveLds / 4; i += 64) s_wave[wv][i] = 0u;
+    }
+    __syncthreads();
     if (s >= n_samples) return;
     const int32_t tstart = (int32_t)(tile * kKlmTile), tlast = tstart + kKlmTile - 1;
-    uint32_t* bm = s_bm[wv];
-    for (int i = lane; i < kKlmWords; i += 64) bm[i] = 0u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int st0 = samp_st[s], st1 = samp_st[s + 1];
-    // ---- pass 1: mark the positions with a valid call of another allele
+    uint32_t sink = 0;                                  // (diagnostics)
+    // ---- pass 1: marks (and, COUNT, the exception counters and the coverage differences)
     for (int st = st0; st < st1; st++) {
         const int64_t e_lo = blkA[(int64_t)st * nblk + (tstart >> shift)];
         const int64_t e_hi = blkB[(int64_t)st * nblk + (tlast >> shift) + 1];
+#if NGSEP_KLM_COMPACT
+        // rounds of 64 consecutive entries (lane = entry e0 + lane, whatever its group): every lane busy but in the
+        // last round; the next round's header and group base in flight
+        int2 h = e_lo + lane < e_hi ? rh[e_lo + lane] : make_int2(0, -1);
+        int64_t gbase = e_lo + lane < e_hi ? grp[(e_lo + lane) >> 6].base : 0;
+        for (int64_t e0 = e_lo; e0 < e_hi; e0 += 64) {
+            const int64_t e = e0 + lane;
+            const bool nx = e + 64 < e_hi;
+            const int2 hn = nx ? rh[e + 64] : make_int2(0, -1);
+            const int64_t gbn = nx ? grp[(e + 64) >> 6].base : 0;
+            const int32_t gf = h.x, gl = h.y & 0x7FFFFFFF;
+            const int32_t a = max(gf, tstart), b = min(gl, tlast);
+            const bool act = e < e_hi && a <= b;
+            const int32_t k0 = act ? (a - gf) >> 3 : 0, kn = act ? ((b - gf) >> 3) - k0 : -1;
+            const uint64_t* ub = units + gbase + (e & 63) + (int64_t)k0 * 64;
+#else
         const int64_t g_hi = (e_hi + 63) >> 6;
         int64_t g = e_lo >> 6;
         int2 h = g < g_hi ? rh[g * 64 + lane] : make_int2(0, -1);
@@ -1515,8 +1548,16 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(NGS
             const bool act = e >= e_lo && e < e_hi && a <= b;
             const int32_t k0 = act ? (a - gf) >> 3 : 0, kn = act ? ((b - gf) >> 3) - k0 : -1;
             const uint64_t* ub = units + gbase + lane + (int64_t)k0 * 64;
-            const int32_t ti0 = gf + 8 * k0 - tstart + 32;   // bitmap index of unit k0's byte 0 (>= 25)
-#if NGSEP_KLM_PIPE
+#endif
+            const int32_t ti0 = gf + 8 * k0 - tstart + 32;   // bitmap index of unit k0's byte 0 (>= 25); COUNT: its
+                                                              // counter byte is ti0 - 24 (>= 1)
+            // COUNT: the read's last unit holds padding past its last position (zero bytes: quality-0 reference calls)
+            const int32_t jlast = ((gl - gf) >> 3) - k0;
+            if (COUNT && act && !ABLATE(gp.ablate, 1048576)) {
+                const int32_t i0 = a - tstart, i1 = b - tstart + 1;
+                atomicAdd(&dif32[i0 >> 2], 1u << (8 * (i0 & 3)));
+                atomicAdd(&dif32[i1 >> 2], 0u - (1u << (8 * (i1 & 3))));
+            }
             uint64_t u[kKlmUnroll];
 #pragma unroll
             for (int i = 0; i < kKlmUnroll; i++) u[i] = kn >= 0 ? ub[(int64_t)min(i, kn) * 64] : 0ull;
@@ -1526,34 +1567,47 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(NGS
 #pragma unroll
                     for (int i = 0; i < kKlmUnroll; i++) v[i] = ub[(int64_t)min(j + kKlmUnroll + i, kn) * 64];
                 }
-#else
-            for (int32_t j = 0; j <= kn; j += kKlmUnroll) {
-                uint64_t u[kKlmUnroll];
-#pragma unroll
-                for (int i = 0; i < kKlmUnroll; i++) u[i] = ub[(int64_t)min(j + i, kn) * 64];
-#endif
 #pragma unroll
                 for (int i = 0; i < kKlmUnroll; i++) {
                     if (j + i > kn) continue;
-                    const uint32_t nlo = kl_nonref((uint32_t)u[i]), nhi = kl_nonref((uint32_t)(u[i] >> 32));
-                    if (!(nlo | nhi)) continue;
-                    uint32_t m = nib4_byte7(nlo) | nib4_byte7(nhi) << 4;
-                    const int32_t ti = ti0 + 8 * (j + i);
-                    // at callable positions only (a counted code reads as another allele against a non-callable one)
-                    for (uint32_t x = m; x; x &= x - 1u) {
-                        const int k = __builtin_ctz(x);
-                        const int32_t tp = ti - 32 + k;
-                        if (tp >= 0 && tp < kKlmTile && !(s_ref[tp] & 0x80u)) m &= ~(1u << k);
+                    const uint32_t ylo = (uint32_t)u[i], yhi = (uint32_t)(u[i] >> 32);
+                    if (ABLATE(gp.ablate, 524288)) { sink += ylo ^ yhi; continue; }   // (diagnostics: loads only)
+                    if (COUNT) {
+                        uint64_t ex = (uint64_t)klm_exc(ylo) | (uint64_t)klm_exc(yhi) << 32;
+                        if (j + i == jlast) {
+                            const int lb = (gl - gf) & 7;      // the read's last byte in this unit
+                            if (lb < 7) ex &= (1ull << (8 * lb + 8)) - 1ull;
+                        }
+                        if (ABLATE(gp.ablate, 65536)) { sink += (uint32_t)ex; ex = 0; }   // (diagnostics: no counters)
+                        if (ex) {
+                            const uint64_t one = ex >> 7;          // a 0 / 1 byte per position
+                            const int32_t ob = ti0 - 24 + 8 * (j + i);
+                            const int sh = 8 * (ob & 3);
+                            const uint64_t lo = one << sh;
+                            uint32_t* c = cnt32 + (ob >> 2);
+                            atomicAdd(c, (uint32_t)lo);
+                            atomicAdd(c + 1, (uint32_t)(lo >> 32));
+                            if (sh) atomicAdd(c + 2, (uint32_t)(one >> (64 - sh)));
+                        }
                     }
-                    if (!m) continue;
+                    const uint32_t nlo = kl_nonref(ylo), nhi = kl_nonref(yhi);
+                    if (!(nlo | nhi)) continue;
+                    if (ABLATE(gp.ablate, 131072)) { sink += nlo; continue; }     // (diagnostics: no marks)
+                    const uint32_t m = nib4_byte7(nlo) | nib4_byte7(nhi) << 4;
+                    const int32_t ti = ti0 + 8 * (j + i);
                     const uint64_t mv = (uint64_t)m << (ti & 31);
-                    atomicOr(&bm[ti >> 5], (uint32_t)mv);
-                    if (mv >> 32) atomicOr(&bm[(ti >> 5) + 1], (uint32_t)(mv >> 32));
+                    const uint32_t m0 = (uint32_t)mv, m1 = (uint32_t)(mv >> 32);
+                    if (m0) {
+                        const uint32_t old = atomicOr(&bm[ti >> 5], m0);
+                        if (COUNT && (old & m0)) atomicOr(&bm2[ti >> 5], old & m0);
+                    }
+                    if (m1) {
+                        const uint32_t old = atomicOr(&bm[(ti >> 5) + 1], m1);
+                        if (COUNT && (old & m1)) atomicOr(&bm2[(ti >> 5) + 1], old & m1);
+                    }
                 }
-#if NGSEP_KLM_PIPE
 #pragma unroll
                 for (int i = 0; i < kKlmUnroll; i++) u[i] = v[i];
-#endif
             }
             h = hn;
             gbase = gbn;
@@ -1562,44 +1616,89 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(NGS
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- slots: the tile's marked positions in order (lane: bitmap words 1 + kKlmWpl lane ..)
-    uint16_t* wb = s_wb[wv];
-    uint16_t* spos = s_pos[wv];
-    unsigned long long* acc = s_acc[wv];
-    uint32_t* sn = s_n[wv];
-    uint32_t bw[kKlmWpl], cw[kKlmWpl];
-    uint32_t c = 0;
+    // ---- candidates: the callable marked positions (lane: bitmap word 1 + lane = positions 32 lane .. 32 lane + 31);
+    //      COUNT drops those the count bound proves hom-ref
+    if (sink == 0xFFFFFFFFu) bm[1 + lane] = sink;      // keeps the diagnostics' work alive
+    uint32_t word = bm[1 + lane] & s_call[lane];
+    if (ABLATE(gp.ablate, 262144)) word = 0u;           // (diagnostics: no exact pass)
+    const uint32_t ncand = (uint32_t)__popc(word);
+    const bool bound_on = gp.use_bound != 0;
+    if (COUNT && bound_on) {
+        int32_t d[4], tot = 0;
 #pragma unroll
-    for (int k = 0; k < kKlmWpl; k++) {
-        bw[k] = bm[1 + kKlmWpl * lane + k];
-        cw[k] = c;
-        c += (uint32_t)__popc(bw[k]);
+        for (int q = 0; q < 8; q++) {
+            unpack_dif(dif32[8 * lane + q], d);
+            tot += d[0] + d[1] + d[2] + d[3];
+        }
+        int32_t incl = tot;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t x = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += x;
+        }
+        if (word) {
+            const uint32_t twice = bm2[1 + lane];
+            const int32_t cb = tabs->cb_hi1;
+            int32_t cov = incl - tot;                    // coverage before the lane's first position
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                unpack_dif(dif32[8 * lane + q], d);
+                const uint32_t cw = cnt32[8 * lane + 2 + q];   // exception bytes of positions 32 lane + 4q ..
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    cov += d[k];
+                    const int bit = 4 * q + k;
+                    if (((word & ~twice) >> bit) & 1u) {
+                        const int32_t hi = cov - (int32_t)((cw >> (8 * k)) & 0xFFu);
+                        if (hi >= cb) word &= ~(1u << bit);
+                    }
+                }
+            }
+        }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    bm[1 + lane] = word;
+    if (lane == 0) { bm[0] = 0u; bm[kKlmWords - 1] = 0u; }
+    // ---- slots: the tile's remaining positions in order
+    uint16_t* wb = s_wb[wv];
+    unsigned long long* acc = reinterpret_cast<unsigned long long*>(s_wave[wv]);
+    uint32_t* sn = s_wave[wv] + 2 * 4 * kKlmSlots;
+    uint16_t* spos = reinterpret_cast<uint16_t*>(sn + kKlmSlots);
+    const uint32_t c = (uint32_t)__popc(word);
     uint32_t incl = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t v = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += v;
+        const uint32_t x = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += x;
     }
     const uint32_t nslot = __shfl(incl, 63, 64);
+    unsigned long long tcand = ncand;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tcand += __shfl_xor(tcand, o, 64);
+    const uint32_t nkeep = min(nslot, (uint32_t)kKlmSlots);
+    if (lane == 0) {                                   // candidate and exactly bounded columns (one add per wave)
+        unsigned long long* sc = counters + kCtrShard0 + kCtrShardStride * (int)(blockIdx.x % kKlShards);
+        if (tcand) atomicAdd(&sc[0], tcand);
+        if (nkeep) atomicAdd(&sc[1], (unsigned long long)nkeep);
+    }
     if (nslot == 0) return;
     const uint32_t ex = incl - c;
-#pragma unroll
-    for (int k = 0; k < kKlmWpl; k++) wb[1 + kKlmWpl * lane + k] = (uint16_t)min(ex + cw[k], 65535u);
-    const uint32_t nkeep = min(nslot, (uint32_t)kKlmSlots);
+    wb[1 + lane] = (uint16_t)min(ex, 65535u);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     for (uint32_t i = lane; i < nkeep; i += 64) {
         acc[4 * i] = 0ull; acc[4 * i + 1] = 0ull; acc[4 * i + 2] = 0ull; acc[4 * i + 3] = 0ull;
         sn[i] = 0u;
     }
-#pragma unroll
-    for (int k = 0; k < kKlmWpl; k++) {
-        uint32_t word = bw[k];
-        uint32_t sl = ex + cw[k];
-        const int32_t ti_base = 32 * (kKlmWpl * lane + k);   // tile index of the word's bit 0
-        while (word) {
-            const int bit = __builtin_ctz(word);
-            word &= word - 1u;
-            const int32_t ti = ti_base + bit;
+    {
+        uint32_t wd = word, sl = ex;
+        while (wd) {
+            const int bit = __builtin_ctz(wd);
+            wd &= wd - 1u;
+            const int32_t ti = 32 * lane + bit;
             if (sl < (uint32_t)kKlmSlots) spos[sl] = (uint16_t)ti;
             else {                                        // past the slots: kept open
                 const int32_t gpos = tstart + ti;
@@ -1611,160 +1710,65 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(NGS
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- pass 2: each lane's valid calls at the marked positions its read covers, into the slots' sums (one
-    //      8-byte unit load per marked position, a group's loads issued together)
+    // ---- pass 2: each lane's valid calls at the slotted positions its read covers, into the slots' sums (one 8-byte
+    //      unit load per position, software-pipelined: a position's load issued before the previous one's sums are
+    //      added; the next group's header and base fetched a group ahead)
     const int32_t maxq = gp.max_q;
-#ifdef NGSEP_KLM_NOPASS2
-    if (st1 < 0)                                       // (A/B builds: pass 1 alone; results not valid)
-#endif
     for (int st = st0; st < st1; st++) {
         const int64_t e_lo = blkA[(int64_t)st * nblk + (tstart >> shift)];
         const int64_t e_hi = blkB[(int64_t)st * nblk + (tlast >> shift) + 1];
-#if NGSEP_KLM_P2PRE
         const int64_t g_hi = (e_hi + 63) >> 6;
         int64_t g = e_lo >> 6;
         int2 hc = g < g_hi ? rh[g * 64 + lane] : make_int2(0, -1);
         int64_t gbc = g < g_hi ? grp[g].base : 0;
         for (; g < g_hi; g++) {
             const int64_t e = g * 64 + lane;
-            const int2 h = hc;                                 // the next group's header and base in flight
+            const int2 h = hc;
             const int64_t gbase = gbc;
             hc = g + 1 < g_hi ? rh[e + 64] : make_int2(0, -1);
             gbc = g + 1 < g_hi ? grp[g + 1].base : 0;
-#else
-        for (int64_t g = e_lo >> 6; g < (e_hi + 63) >> 6; g++) {
-            const int64_t e = g * 64 + lane;
-            const int2 h = rh[e];
-            const int64_t gbase = grp[g].base;
-#endif
             const int32_t gf = h.x, gl = h.y & 0x7FFFFFFF;
             const int32_t a = max(gf, tstart), b = min(gl, tlast);
             if (!(e >= e_lo && e < e_hi && a <= b)) continue;
             const uint64_t* ub = units + gbase + lane;
             const int32_t A = a - tstart + 32, B = b - tstart + 32;
-            int32_t pend_o[kKlmPend];
-            uint32_t pend_s[kKlmPend];
-#pragma unroll
-            for (int i = 0; i < kKlmPend; i++) { pend_o[i] = 0; pend_s[i] = 0; }
-            int np = 0;
-#if NGSEP_KLM_P2DEPTH
-            // software-pipelined, one load per marked position: up to kD loads in flight, the oldest added when a
-            // new one is issued (static register indexes only)
-            constexpr int kD = NGSEP_KLM_P2DEPTH;
-            uint64_t qu[kD];
-            uint32_t qsh[kD], qs[kD];
-            int nq = 0;
-#pragma unroll
-            for (int i = 0; i < kD; i++) { qu[i] = 0ull; qsh[i] = 0u; qs[i] = 0u; }
-            auto add1 = [&](uint64_t uu, uint32_t sh8, uint32_t slot) {
-                const uint32_t y = (uint32_t)(uu >> sh8) & 0xFFu;
-                if (y & 0x80u) return;                        // not a valid call (the position is callable)
+            uint64_t qu = 0ull;                                 // the position in flight: unit, byte shift, slot
+            uint32_t qsh = 0u, qs = 0u;
+            bool pend = false;
+            auto add = [&]() {
+                const uint32_t y = (uint32_t)(qu >> qsh) & 0xFFu;
+                if (y & 0x80u) return;                          // not a valid call (the position is callable)
                 const uint32_t al = (y >> 5) & 3u;
                 int q = (int)(y & 31u);
                 q = q > maxq ? maxq : q;
-                atomicAdd(&acc[4 * slot + al], w[al == 0 ? 0 : 1][q]);
-                atomicAdd(&sn[slot], 1u);
+                atomicAdd(&acc[4 * qs + al], w[al == 0 ? 0 : 1][q]);
+                atomicAdd(&sn[qs], 1u);
             };
-            auto add_q = [&]() {
-#pragma unroll
-                for (int i = 0; i < kD; i++)
-                    if (i < nq) add1(qu[i], qsh[i], qs[i]);
-                nq = 0;
-            };
-            auto flush = [&]() {
-                const uint64_t u = ub[(int64_t)(pend_o[0] >> 3) * 64];
-                if (nq == kD) {
-                    add1(qu[0], qsh[0], qs[0]);
-#pragma unroll
-                    for (int i = 0; i + 1 < kD; i++) { qu[i] = qu[i + 1]; qsh[i] = qsh[i + 1]; qs[i] = qs[i + 1]; }
-                    nq--;
-                }
-#pragma unroll
-                for (int i = 0; i < kD; i++)
-                    if (i == nq) { qu[i] = u; qsh[i] = 8u * (uint32_t)(pend_o[0] & 7); qs[i] = pend_s[0]; }
-                nq++;
-                np = 0;
-            };
-#elif NGSEP_KLM_P2PIPE
-            // software-pipelined: a full batch's loads are issued, then the previous batch (in flight) is added
-            uint64_t qu[kKlmPend];
-            uint32_t qsh[kKlmPend], qs[kKlmPend];
-            int nq = 0;
-#pragma unroll
-            for (int i = 0; i < kKlmPend; i++) { qu[i] = 0ull; qsh[i] = 0u; qs[i] = 0u; }
-            auto add_q = [&]() {
-#pragma unroll
-                for (int i = 0; i < kKlmPend; i++) {
-                    if (i >= nq) continue;
-                    const uint32_t y = (uint32_t)(qu[i] >> qsh[i]) & 0xFFu;
-                    if (y & 0x80u) continue;                  // not a valid call (the position is callable)
-                    const uint32_t al = (y >> 5) & 3u;
-                    int q = (int)(y & 31u);
-                    q = q > maxq ? maxq : q;
-                    atomicAdd(&acc[4 * qs[i] + al], w[al == 0 ? 0 : 1][q]);
-                    atomicAdd(&sn[qs[i]], 1u);
-                }
-                nq = 0;
-            };
-            auto flush = [&]() {
-                uint64_t u[kKlmPend];
-#pragma unroll
-                for (int i = 0; i < kKlmPend; i++) u[i] = i < np ? ub[(int64_t)(pend_o[i] >> 3) * 64] : 0ull;
-                add_q();
-#pragma unroll
-                for (int i = 0; i < kKlmPend; i++) { qu[i] = u[i]; qsh[i] = 8u * (uint32_t)(pend_o[i] & 7); qs[i] = pend_s[i]; }
-                nq = np;
-                np = 0;
-            };
-#else
-            auto flush = [&]() {
-                uint64_t u[kKlmPend];
-#pragma unroll
-                for (int i = 0; i < kKlmPend; i++) u[i] = i < np ? ub[(int64_t)(pend_o[i] >> 3) * 64] : 0ull;
-#pragma unroll
-                for (int i = 0; i < kKlmPend; i++) {
-                    if (i >= np) continue;
-                    const uint32_t y = (uint32_t)(u[i] >> (8 * (pend_o[i] & 7))) & 0xFFu;
-                    if (y & 0x80u) continue;                  // not a valid call (the position is callable)
-                    const uint32_t al = (y >> 5) & 3u;
-                    int q = (int)(y & 31u);
-                    q = q > maxq ? maxq : q;
-                    atomicAdd(&acc[4 * pend_s[i] + al], w[al == 0 ? 0 : 1][q]);
-                    atomicAdd(&sn[pend_s[i]], 1u);
-                }
-                np = 0;
-            };
-#endif
             for (int32_t wi = A >> 5; wi <= (B >> 5); wi++) {
-                uint32_t word = bm[wi];
-                if (wi == (A >> 5)) word &= ~0u << (A & 31);
-                if (wi == (B >> 5) && (B & 31) != 31) word &= (1u << ((B & 31) + 1)) - 1u;
-                if (!word) continue;
+                uint32_t wd = bm[wi];
+                if (wi == (A >> 5)) wd &= ~0u << (A & 31);
+                if (wi == (B >> 5) && (B & 31) != 31) wd &= (1u << ((B & 31) + 1)) - 1u;
+                if (!wd) continue;
                 const uint32_t full = bm[wi];
                 const uint32_t sbase = wb[wi];
-                while (word) {
-                    const int bit = __builtin_ctz(word);
-                    word &= word - 1u;
+                while (wd) {
+                    const int bit = __builtin_ctz(wd);
+                    wd &= wd - 1u;
                     const uint32_t sl = sbase + (uint32_t)__popc(full & ((1u << bit) - 1u));
                     if (sl >= (uint32_t)kKlmSlots) continue;
-#pragma unroll
-                    for (int i = 0; i < kKlmPend; i++)          // (static indexes: registers, not scratch)
-                        if (i == np) { pend_o[i] = wi * 32 + bit - 32 + tstart - gf; pend_s[i] = sl; }   // byte offset in the read
-                    np++;
-                    if (np == kKlmPend) flush();
+                    const int32_t o = wi * 32 + bit - 32 + tstart - gf;   // byte offset in the read
+                    const uint64_t nu = ub[(int64_t)(o >> 3) * 64];
+                    if (pend) add();
+                    qu = nu; qsh = 8u * (uint32_t)(o & 7); qs = sl; pend = true;
                 }
             }
-            if (np) flush();
-#if NGSEP_KLM_P2PIPE || NGSEP_KLM_P2DEPTH
-            add_q();
-#endif
+            if (pend) add();
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- pass 3: the bound per slot
-    const bool bound_on = gp.use_bound != 0;
+    // ---- pass 3: the exact bound per slot
     const long long th = tabs->t_het, to = tabs->t_homo;
     for (uint32_t i = lane; i < nkeep; i += 64) {
         const unsigned long long a0 = acc[4 * i], a1 = acc[4 * i + 1], a2 = acc[4 * i + 2], a3 = acc[4 * i + 3];
@@ -1779,12 +1783,6 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(NGS
             const int32_t gpos = tstart + spos[i];
             atomicOr(&need[gpos >> 5], 1u << (gpos & 31));
         }
-    }
-    // candidate columns and bounded columns, on the shard counters (one add per wave)
-    if (lane == 0) {
-        unsigned long long* sc = counters + kCtrShard0 + kCtrShardStride * (int)(blockIdx.x % kKlShards);
-        atomicAdd(&sc[0], (unsigned long long)nslot);
-        atomicAdd(&sc[1], (unsigned long long)nkeep);
     }
 }
 
@@ -3457,7 +3455,10 @@ static hipError_t launch_pop_scan(Device* d, const GenotypeParams& g, uint32_t* 
     const int64_t ntile = d->g_len / kKlmTile;
     const int64_t nblk = std::max<int64_t>(1, ntile * ((d->n_samples + 3) / 4));
     if (nblk >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
-    hipExtLaunchKernelGGL(k_scan_pop, dim3((unsigned)nblk), dim3(kKlmThreads), 0, d->stream, ev_start, nullptr, 0,
+    // the count bound needs every sample's coverage below 128 (byte counters); deeper populations take the exact bound
+    // at every marked position
+    auto klm = d->pop_stride <= kKlmCountMaxCov ? k_scan_pop<true> : k_scan_pop<false>;
+    hipExtLaunchKernelGGL(klm, dim3((unsigned)nblk), dim3(kKlmThreads), 0, d->stream, ev_start, nullptr, 0,
                           (const uint64_t*)d->d_units, (const int2*)d->d_rh, (const RGroup*)d->d_grp,
                           (const int32_t*)d->d_samp_st, (const int32_t*)d->d_blkA, (const int32_t*)d->d_blkB, d->pnblk,
                           d->pblk_shift, d->n_samples, (const uint8_t*)d->d_ref, (const LikTables*)d->d_tables, g, need, ctr);

@@ -293,6 +293,8 @@ def gpu_contig_caller(fasta: str, bam: str, params=None, device: int = 0,
         with tempfile.TemporaryDirectory() as d:
             out = os.path.join(d, "c.vcf")
             s._check(s._lib.ngsep_call_region_bam(s._ctx, bam.encode(), name.encode(), first, last, out.encode()))
+            state["windows"] = state.get("windows", 0) + 1
+            state["positions"] = state.get("positions", 0) + int(s.stats().positions_genotyped)
             return open(out).read()
 
     def cut(name: str, pos: int):
@@ -309,6 +311,7 @@ def gpu_contig_caller(fasta: str, bam: str, params=None, device: int = 0,
     call.carved = carved
     call.region = region
     call.cut = cut
+    call.state = state
     return call
 
 
@@ -337,7 +340,7 @@ def gather_carved(local: List[Tuple[str, int, int]], order: Sequence[str], dist=
 
 
 def call_bam_sharded(fasta: str, bam: str, out_vcf: str, params=None, dist=None, device: Optional[int] = None,
-                     known_vcf: Optional[str] = None, window: int = 4 << 20) -> Optional[str]:
+                     known_vcf: Optional[str] = None, window: int = 4 << 20, work: Optional[dict] = None) -> Optional[str]:
     """SingleSampleVariantsDetector over the GPUs of one node (device = local rank by default): with window > 0
     (default 4 Mb) the sequences' exact windows from a shared queue (call_windows), else the BAM header's sequences
     split over the ranks (assign_contigs); each region called through the index on the rank's GPU, the blocks merged
@@ -358,6 +361,9 @@ def call_bam_sharded(fasta: str, bam: str, out_vcf: str, params=None, dist=None,
             text = call_sharded(contigs, caller, out_vcf, dist)
         # the regions left to the caller's own indel path (ngsep_fetch_carved_regions), merged like the records and
         # written beside the VCF as the CLI does (<out>.carved.bed, 0-based half-open)
+        if work is not None:                       # (this rank's share: region runs and their genotyped positions)
+            work["windows"] = caller.state.get("windows", 0)
+            work["positions"] = caller.state.get("positions", 0)
         regions = gather_carved(caller.carved(), [c[0] for c in contigs], dist)
         if regions:
             with open(out_vcf + ".carved.bed", "w") as f:
@@ -445,3 +451,73 @@ def call_population_sharded(fasta: str, bams: Sequence[str], out_vcf: str, param
         return call_sharded(contigs, caller, out_vcf, dist)
     finally:
         caller.close()
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# several devices from ONE process through the C ABI (ngsep_call_bam_multi / ngsep_call_population_bams_multi, ABI 11):
+# one context per device, one host thread each, windows from an in-process queue -- what a Java/JNI caller gets
+# ------------------------------------------------------------------------------------------------------------------
+def plan_windows(session, bams: Sequence[str], window: int) -> List[Tuple[str, int, int, int]]:
+    """ngsep_plan_windows: the (sequence, first, last, lead) windows the multi-device drivers run (host only)."""
+    import ctypes
+    arr = (ctypes.c_char_p * len(bams))(*[b.encode() for b in bams])
+    n = ctypes.c_int64(0)
+    session._check(session._lib.ngsep_plan_windows(session._ctx, arr, len(bams), int(window), None, None, None, None, 0,
+                                                    ctypes.byref(n)))
+    k = n.value
+    sid = (ctypes.c_int32 * max(1, k))()
+    first, last, lead = ((ctypes.c_int64 * max(1, k))() for _ in range(3))
+    session._check(session._lib.ngsep_plan_windows(session._ctx, arr, len(bams), int(window), sid, first, last, lead, k,
+                                                    ctypes.byref(n)))
+    names = session.sequence_names()
+    return [(names[sid[i]], int(first[i]), int(last[i]), int(lead[i])) for i in range(k)]
+
+
+def _multi_sessions(fasta, devices, params, known_vcf, known_strs, multisample):
+    import ctypes
+    from .discovery import GpuPileupSession, default_params
+    p = default_params()
+    if params is not None:
+        ctypes.pointer(p)[0] = params
+    if multisample:
+        p.multisample = 1
+    sessions = [GpuPileupSession(p, int(d)) for d in devices]
+    sessions[0].load_fasta(fasta)                     # (the other contexts take the first one's reference)
+    if known_vcf:
+        sessions[0].set_known_variants(known_vcf)
+    if known_strs:
+        sessions[0].set_known_strs(known_strs)
+    return sessions
+
+
+def call_bam_multi(fasta: str, bam: str, out_vcf: str, devices: Sequence[int], params=None, window: int = 4 << 20,
+                   known_vcf: Optional[str] = None, known_strs: Optional[str] = None, sessions_out=None) -> str:
+    """SingleSampleVariantsDetector over several devices of this process (ngsep_call_bam_multi): the VCF text."""
+    import ctypes
+    sessions = _multi_sessions(fasta, devices, params, known_vcf, known_strs, False)
+    try:
+        ctxs = (ctypes.c_void_p * len(sessions))(*[s._ctx.value for s in sessions])
+        sessions[0]._check(sessions[0]._lib.ngsep_call_bam_multi(ctxs, len(sessions), bam.encode(), out_vcf.encode(), int(window)))
+        if sessions_out is not None:
+            sessions_out.append([s.stats() for s in sessions])
+            sessions_out.append(sessions[0].carved_regions())
+        return open(out_vcf).read()
+    finally:
+        for s in sessions:
+            s.close()
+
+
+def call_population_multi(fasta: str, bams: Sequence[str], out_vcf: str, devices: Sequence[int], params=None,
+                          window: int = 4 << 20, known_vcf: Optional[str] = None, known_strs: Optional[str] = None) -> str:
+    """MultisampleVariantsDetector over several devices of this process (ngsep_call_population_bams_multi)."""
+    import ctypes
+    sessions = _multi_sessions(fasta, devices, params, known_vcf, known_strs, True)
+    try:
+        ctxs = (ctypes.c_void_p * len(sessions))(*[s._ctx.value for s in sessions])
+        arr = (ctypes.c_char_p * len(bams))(*[b.encode() for b in bams])
+        sessions[0]._check(sessions[0]._lib.ngsep_call_population_bams_multi(ctxs, len(sessions), arr, len(bams),
+                                                                           out_vcf.encode(), int(window)))
+        return open(out_vcf).read()
+    finally:
+        for s in sessions:
+            s.close()

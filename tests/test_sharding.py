@@ -449,3 +449,50 @@ def test_gpu_window_caller_merge_identical(tmp_path, multi):
     text = open(full).read()
     assert sum(1 for l in text.splitlines() if "TYPE=INDEL" in l or "TYPE=STR" in l) > 5
     assert merged == text
+
+
+def test_plan_windows_matches_python_plan(tmp_path):
+    """ngsep_plan_windows (the windows ngsep_call_bam_multi's threads take from their in-process queue): every header
+    sequence covered once, in order, contiguous, cut where ngsep_clean_cut cuts -- the same windows sharding.py's
+    window_units(compute_cuts(...)) gives the multi-process driver; whole sequences at window 0 and in pass-through
+    mode."""
+    from ngsepcore_amd import GpuPileupSession
+    from ngsepcore_amd.sharding import bam_header_sequences, clean_cut, compute_cuts, plan_windows, window_units
+    from helpers import gpu_params
+    syn = pysynth.Synth(genome=pysynth.CUSTOM, custom_len=150000, seed=74, depth=12, indel_rate=5e-4)
+    fa, sam, bam = syn.write(os.path.join(str(tmp_path), "p"))
+    syn.close()
+    contigs = bam_header_sequences(bam)
+    with GpuPileupSession() as s:
+        s.load_fasta(fa)
+        for window in (20000, 55555, 1 << 30):
+            got = plan_windows(s, [bam], window)
+            want = window_units(contigs, compute_cuts(contigs, window, lambda n, p: clean_cut(s, [bam], n, p)))
+            assert got == [(n, a, b, lead) for n, _, a, b, lead in want]
+            for (n, a, b, _), nxt in zip(got, got[1:] + [None]):
+                if nxt is not None and nxt[0] == n:
+                    assert nxt[1] == b + 1
+            assert got[0][1] == 1 and got[-1][2] == contigs[-1][1]
+        assert len(plan_windows(s, [bam], 20000)) >= 5
+        assert plan_windows(s, [bam], 0) == [(n, 1, l, 0) for n, l in contigs]
+    with GpuPileupSession(gpu_params(indel_passthrough=1)) as s:
+        s.load_fasta(fa)
+        assert plan_windows(s, [bam], 20000) == [(n, 1, l, 0) for n, l in contigs]
+
+
+def test_multi_driver_fails_loudly_without_device(tmp_path):
+    """ngsep_call_bam_multi on contexts without a HIP device: an error, no output and no CPU fallback."""
+    import ctypes
+    if __import__("torch").cuda.is_available():
+        pytest.skip("a GPU is present")
+    from ngsepcore_amd import GpuPileupSession, NgsepError
+    from ngsepcore_amd.sharding import call_bam_multi
+    syn = pysynth.Synth(genome=pysynth.CUSTOM, custom_len=20000, seed=75, depth=5)
+    fa, sam, bam = syn.write(os.path.join(str(tmp_path), "n"))
+    syn.close()
+    out = os.path.join(str(tmp_path), "m.vcf")
+    with pytest.raises(NgsepError):
+        call_bam_multi(fa, bam, out, [0, 0], window=5000)
+    with GpuPileupSession() as s:              # the same context twice is refused before any device work
+        ctxs = (ctypes.c_void_p * 2)(s._ctx.value, s._ctx.value)
+        assert s._lib.ngsep_call_bam_multi(ctxs, 2, bam.encode(), out.encode(), 5000) == -1
