@@ -97,6 +97,25 @@ struct RunSlot {                     // one in-flight single-sample run (see dev
     std::chrono::steady_clock::time_point t0;
 };
 
+// KPM's two stages (k_posterior_multi STAGEA): KLM's (position, sample) pairs of the columns it could not prove hom-ref,
+// in kKlShards segments of pseg; KQN's queue index of every need word's first bit; per queued position a 256-bit sample
+// mask (zeroed once: the first stage clears what it read); the second stage's queue
+struct PopStage {
+    uint2* pairs = nullptr;
+    int64_t pseg = 0;
+    int32_t* qword = nullptr;
+    int64_t cap_qword = 0;
+    uint32_t* pmask = nullptr;
+    QueueSite* qB = nullptr;
+    int64_t cap = 0;                         // queue entries of pmask and qB
+    void release() {
+        (void)hipFree(pairs); (void)hipFree(qword); (void)hipFree(pmask); (void)hipFree(qB);
+        pairs = nullptr; qword = nullptr; pmask = nullptr; qB = nullptr;
+        pseg = cap_qword = cap = 0;
+    }
+    hipError_t ensure(int64_t qcap, int64_t nwords, hipStream_t st);   // for a queue of qcap positions over nwords words
+};
+
 struct MultiSlot {                   // one in-flight multisample run (device_submit_multi / device_collect_multi)
     QueueSite* d_hard = nullptr;             // KQN -> KPM queue
     int64_t cap_hard = 0;
@@ -115,6 +134,7 @@ struct MultiSlot {                   // one in-flight multisample run (device_su
     PinnedStore<ngsep_sample_call> h_big;
     int64_t cap_pack = 0;                    // sites
     int64_t guess_big = 0, cap_big = 0;
+    PopStage stage;
 };
 
 struct Device {
@@ -159,6 +179,7 @@ struct Device {
     int32_t n_streams = 0, pblk_shift = kRgBlockShift, pop_stride = 0;
     int64_t pnblk = 0;
     uint32_t* d_need = nullptr;      //   open positions, a bit per global position
+    PopStage pstage;                 //   KPM's two stages (device_run_multi)
     ngsep_popsite_out* h_psites = nullptr;      // multisample: pinned staging of the emitted sites and calls
     ngsep_sample_call* h_pcalls = nullptr;
     int64_t cap_h_psites = 0, cap_h_pcalls = 0;
@@ -1387,7 +1408,8 @@ __global__ __launch_bounds__(256) void k_queue_all(const uint8_t* __restrict__ r
 
 // KQN: the open positions (a bit per global position) into the KPM queue, {position, reference code}
 __global__ __launch_bounds__(256) void k_queue_need(const uint32_t* __restrict__ need, const uint8_t* __restrict__ ref, int64_t nwords,
-                                                    QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap) {
+                                                    QueueSite* __restrict__ queue, unsigned long long* __restrict__ counters, int64_t qcap,
+                                                    int32_t* __restrict__ qword) {
     const int lane = threadIdx.x & 63;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < nwords; base += stride) {
@@ -1405,6 +1427,7 @@ __global__ __launch_bounds__(256) void k_queue_need(const uint32_t* __restrict__
         if (lane == 63) q0 = atomicAdd(&counters[2], (unsigned long long)tot);
         q0 = __shfl(q0, 63, 64);
         int64_t at = (int64_t)q0 + (incl - c);
+        if (qword && m) qword[i] = (int32_t)at;           // (KPM's first stage: the queue index of the word's first bit)
         while (m) {
             const int b = __builtin_ctz(m);
             m &= m - 1u;
@@ -1480,7 +1503,8 @@ __global__ __launch_bounds__(kKlmThreads) KLM_WPE_ATTR void k_scan_pop(
     const uint64_t* __restrict__ units, const int2* __restrict__ rh, const RGroup* __restrict__ grp,
     const int32_t* __restrict__ samp_st, const int32_t* __restrict__ blkA, const int32_t* __restrict__ blkB,
     int64_t nblk, int32_t shift, int32_t n_samples, const uint8_t* __restrict__ ref, const LikTables* __restrict__ tabs,
-    GenotypeParams gp, uint32_t* __restrict__ need, unsigned long long* __restrict__ counters) {
+    GenotypeParams gp, uint32_t* __restrict__ need, unsigned long long* __restrict__ counters, uint2* __restrict__ pairs,
+    int64_t pseg) {
     __shared__ unsigned long long w[2][32];
     __shared__ uint32_t s_call[kKlmTile / 32];         // callable positions of the tile
     __shared__ uint32_t s_bm[4][kKlmWords];            // marked positions, then those the exact bound takes
@@ -1703,6 +1727,11 @@ __global__ __launch_bounds__(kKlmThreads) KLM_WPE_ATTR void k_scan_pop(
             else {                                        // past the slots: kept open
                 const int32_t gpos = tstart + ti;
                 atomicOr(&need[gpos >> 5], 1u << (gpos & 31));
+                if (pairs) {                              // (and not proven hom-ref: a pair for KPM's first stage)
+                    const int sh = (int)(blockIdx.x % kKlShards);
+                    const unsigned long long k = atomicAdd(&counters[kCtrShard0 + kCtrShardStride * sh + 2], 1ull);
+                    if ((int64_t)k < pseg) pairs[(int64_t)sh * pseg + (int64_t)k] = make_uint2((uint32_t)gpos, (uint32_t)s);
+                }
             }
             sl++;
         }
@@ -1768,21 +1797,58 @@ __global__ __launch_bounds__(kKlmThreads) KLM_WPE_ATTR void k_scan_pop(
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- pass 3: the exact bound per slot
+    // ---- pass 3: the exact bound per slot.  A column it cannot prove hom-ref opens its position and, with pairs,
+    //      is listed (position, sample) for KPM's first stage: the columns a decided non-reference call can come from
     const long long th = tabs->t_het, to = tabs->t_homo;
-    for (uint32_t i = lane; i < nkeep; i += 64) {
-        const unsigned long long a0 = acc[4 * i], a1 = acc[4 * i + 1], a2 = acc[4 * i + 2], a3 = acc[4 * i + 3];
-        const long long R1 = (long long)(a0 & 0xFFFFFFFFull), R2 = (long long)(a0 >> 32);
-        const long long x1 = (long long)(a1 & 0xFFFFFFFFull), y1 = (long long)(a2 & 0xFFFFFFFFull);
-        const long long z1 = (long long)(a3 & 0xFFFFFFFFull);
-        const long long x2 = (long long)(a1 >> 32), y2 = (long long)(a2 >> 32), z2 = (long long)(a3 >> 32);
-        const bool drop = (R1 - x1 > th) && (R1 - y1 > th) && (R1 - z1 > th) &&
-                          (R2 - x2 > to) && (R2 - y2 > to) && (R2 - z2 > to) &&
-                          (R2 - x1 - y1 > th) && (R2 - x1 - z1 > th) && (R2 - y1 - z1 > th);
-        if (!bound_on || sn[i] > (uint32_t)kMcMaxCalls || !drop) {
-            const int32_t gpos = tstart + spos[i];
-            atomicOr(&need[gpos >> 5], 1u << (gpos & 31));
+    for (uint32_t i0 = 0; i0 < nkeep; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        bool open = false;
+        if (i < nkeep) {
+            const unsigned long long a0 = acc[4 * i], a1 = acc[4 * i + 1], a2 = acc[4 * i + 2], a3 = acc[4 * i + 3];
+            const long long R1 = (long long)(a0 & 0xFFFFFFFFull), R2 = (long long)(a0 >> 32);
+            const long long x1 = (long long)(a1 & 0xFFFFFFFFull), y1 = (long long)(a2 & 0xFFFFFFFFull);
+            const long long z1 = (long long)(a3 & 0xFFFFFFFFull);
+            const long long x2 = (long long)(a1 >> 32), y2 = (long long)(a2 >> 32), z2 = (long long)(a3 >> 32);
+            const bool drop = (R1 - x1 > th) && (R1 - y1 > th) && (R1 - z1 > th) &&
+                              (R2 - x2 > to) && (R2 - y2 > to) && (R2 - z2 > to) &&
+                              (R2 - x1 - y1 > th) && (R2 - x1 - z1 > th) && (R2 - y1 - z1 > th);
+            open = !bound_on || sn[i] > (uint32_t)kMcMaxCalls || !drop;
         }
+        const int32_t gpos = i < nkeep ? tstart + spos[i] : 0;
+        if (open) atomicOr(&need[gpos >> 5], 1u << (gpos & 31));
+        if (pairs) {
+            const unsigned long long m = __ballot(open);
+            if (m) {
+                const int sh = (int)(blockIdx.x % kKlShards);
+                unsigned long long base = 0;
+                if (lane == 0) base = atomicAdd(&counters[kCtrShard0 + kCtrShardStride * sh + 2], (unsigned long long)__popcll(m));
+                base = __shfl(base, 0, 64);
+                if (open) {
+                    const int64_t k = (int64_t)base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    if (k < pseg) pairs[(int64_t)sh * pseg + k] = make_uint2((uint32_t)gpos, (uint32_t)s);
+                }
+            }
+        }
+    }
+}
+
+// KPM's first stage, its per-position sample masks: pair (position, sample) -> bit sample of the position's queue entry
+// (KQN's word bases: qword[w] = the queue index of word w's first open position).  A segment past its capacity sets
+// counters[3] bit 62: the first stage then passes every position to the second.
+__global__ __launch_bounds__(256) void k_pair_mask(const uint2* __restrict__ pairs, int64_t pseg, const uint32_t* __restrict__ need,
+                                                   const int32_t* __restrict__ qword, uint32_t* __restrict__ pmask, int64_t qcap,
+                                                   unsigned long long* __restrict__ counters) {
+    const int sh = (int)blockIdx.y;
+    const unsigned long long n = counters[kCtrShard0 + kCtrShardStride * sh + 2];
+    if ((int64_t)n > pseg) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&counters[3], 1ull << 62);
+        return;
+    }
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < (int64_t)n; k += (int64_t)gridDim.x * blockDim.x) {
+        const uint2 pr = pairs[(int64_t)sh * pseg + k];
+        const uint32_t gpos = pr.x, w = gpos >> 5;
+        const int64_t q = (int64_t)qword[w] + __popc(need[w] & ((1u << (gpos & 31)) - 1u));
+        if (q < qcap) atomicOr(&pmask[q * 8 + (pr.y >> 5)], 1u << (pr.y & 31));
     }
 }
 
@@ -2145,14 +2211,21 @@ __device__ inline int32_t pop_gather(const PopGather& pg, int32_t p, int s, uint
 // (measured and not kept: a separate gather kernel, one thread per (position, sample) at 8 waves per SIMD, into
 // columns KPM then read with the next position's in flight -- 0.64 against 0.52 ms for gather + KPM on configs[4]:
 // the gather's cost is its scattered lines, ~10 per sample column, not latency KPM fails to hide)
-template <bool POOL, int WPE, int GATHER>
+// STAGEA (KPM's first stage; GATHER 1, ploidy < 3, discovery with minAlleleDepthFrequency 0 and the bounds on): only
+// the columns of the samples KLM could not prove hom-ref at the position (pmask: one bit per sample, from KLM's pairs)
+// are gathered and genotyped -- every other sample is hom-ref for any allele set, so it adds no
+// called allele and nothing to the variant QS; its other-allele calls only add alleles that no sample calls, which the
+// multi-allelic loop (discoverPopulationSNV :590-595, makeNewVariant) removes before the QS is final.  A position whose
+// QS passes (onPileup :533) goes to qB for the full genotyping (the second stage, every column); the others are done.
+template <bool POOL, int WPE, int GATHER, bool STAGEA>
 __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE))) void k_posterior_multi(
     const QueueSite* __restrict__ queue, const unsigned long long* qn, int64_t qcap,
     const uint8_t* __restrict__ ppile, const uint16_t* __restrict__ prow, const int64_t* __restrict__ pboff,
     const PopGather pg, const LikTables* __restrict__ tabs, GenotypeParams gp,
     int32_t n_samples, double min_adf, int32_t ploidy, const PoolTables* __restrict__ pt,
     ngsep_popsite_out* __restrict__ sites, ngsep_sample_call* __restrict__ calls,
-    unsigned long long* counters, int64_t cap, unsigned long long* __restrict__ stamps) {
+    unsigned long long* counters, int64_t cap, unsigned long long* __restrict__ stamps,
+    uint32_t* __restrict__ pmask, QueueSite* __restrict__ qB, unsigned long long* __restrict__ qB_n, int64_t qB_cap) {
     // stamps (diagnostics, NGSEP_TIMING): s_memtime at the phase ends of block 0's first site
     auto stamp = [&](int k) {
         if (stamps && blockIdx.x == 0 && threadIdx.x == 0) stamps[k] = __builtin_amdgcn_s_memtime();
@@ -2188,6 +2261,8 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
         qs_next = queue[blockIdx.x];
         if (GATHER != 1) column_of(blockIdx.x, qs_next.gpos, rows_next, col_next);
     }
+    // (a pair segment past its capacity: the first stage hands every position to the second)
+    const bool passall = STAGEA && ((counters[3] >> 62) & 1ull);
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         __syncthreads();
         const QueueSite qs = qs_next;
@@ -2195,6 +2270,14 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
         const uint32_t rc = (uint32_t)qs.rc;
         const int64_t inext = i + gridDim.x;
         if (inext < n) qs_next = queue[inext];
+        if (STAGEA && passall) {
+            if (threadIdx.x == 0) {
+                const unsigned long long k = atomicAdd(qB_n, 1ull);
+                if ((int64_t)k < qB_cap) qB[k] = qs;
+            }
+            if (threadIdx.x < 8) pmask[i * 8 + threadIdx.x] = 0u;
+            continue;
+        }
         if (tid == 0) { s_pc[0] = s_pc[1] = s_pc[2] = s_pc[3] = 0; s_tot = 0; s_called = 0; s_qs = 0; }
         __syncthreads();
         // 1-3. thread s walks sample s's column of the pile (read-group rank order, pending order inside:
@@ -2209,7 +2292,8 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
         const uint8_t* col = col_next;
         if (GATHER == 1 && tid <= n_samples) {
             uint8_t* dst = s_gcol + (int64_t)tid * pg.stride;
-            rows = pop_gather<NGSEP_KPM_GBATCH>(pg, gpos, tid, dst, pg.stride);
+            const bool mine = !STAGEA || (tid < n_samples && ((pmask[i * 8 + (tid >> 5)] >> (tid & 31)) & 1u));
+            rows = mine ? pop_gather<NGSEP_KPM_GBATCH>(pg, gpos, tid, dst, pg.stride) : 0;
             if (rows > pg.stride) {                          // (the host's coverage bound makes this unreachable)
                 atomicOr(&counters[3], 1ull << 63);
                 rows = pg.stride;
@@ -2267,6 +2351,7 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
         }
         if (tid == n_samples) { total = 0; cnt[0] = cnt[1] = cnt[2] = cnt[3] = 0; }
         __syncthreads();
+        if (STAGEA && tid < 8) pmask[i * 8 + tid] = 0u;         // (read: cleared for the next pass)
         if (i == blockIdx.x) stamp(2);
         // -knownVariants (MultisampleVariantsDetector.onPileup :539-551): the input variant's own alleles, every
         // sample genotyped (genotypeVariant :674-693) and the record written whatever its QS
@@ -2334,6 +2419,13 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
         if (i == blockIdx.x) stamp(5);
         if (nal < 2) continue;                                     // only the reference allele is left
         if (!known && (qsv == 0 || qsv < gp.min_quality)) continue;   // MultisampleVariantsDetector.java:534
+        if (STAGEA) {                                              // a record: the second stage genotypes every column
+            if (tid == 0) {
+                const unsigned long long k = atomicAdd(qB_n, 1ull);
+                if ((int64_t)k < qB_cap) qB[k] = qs;
+            }
+            continue;
+        }
         // 6. emit the site and its calls
         __syncthreads();
         if (tid == 0) s_base = atomicAdd(&counters[0], 1ull);
@@ -2760,6 +2852,8 @@ void device_release(Device* d) {
     d->n_streams = 0;
     d->pop_stride = 0;
     (void)hipFree(d->d_need); d->d_need = nullptr;
+    d->pstage.release();
+    for (auto& m : d->mslot) m.stage.release();
     (void)hipFree(d->d_mforced); d->d_mforced = nullptr;
     (void)hipFree(d->d_mforced_ctr); d->d_mforced_ctr = nullptr;
     d->n_mforced = -1;
@@ -2818,6 +2912,7 @@ void device_destroy(Device* d) {
         (void)hipFree(m.d_hard); (void)hipFree(m.d_need); (void)hipFree(m.d_psites); (void)hipFree(m.d_pcalls);
         if (m.h_psites) host_pinned_free(m.h_psites);
         (void)hipFree(m.d_pack); (void)hipFree(m.d_big);
+        m.stage.release();
         for (auto& e : m.ev) if (e) (void)hipEventDestroy(e);
     }
     (void)hipFree(d->d_csrc);
@@ -3441,14 +3536,16 @@ int device_run_rac(Device* d, const Staged& s, int64_t g0, int64_t g1, int32_t m
 #endif
 constexpr int kKpmWavesPerEu = NGSEP_KPM_WPE;
 constexpr unsigned kKpmGrid = 16384;
-static auto kpm_kernel(int ploidy, int gather) {
-    if (gather == 1) return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, 1> : k_posterior_multi<false, kKpmWavesPerEu, 1>;
-    return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, 0> : k_posterior_multi<false, kKpmWavesPerEu, 0>;
+static auto kpm_kernel(int ploidy, int gather, bool stage_a = false) {
+    if (stage_a) return k_posterior_multi<false, kKpmWavesPerEu, 1, true>;
+    if (gather == 1)
+        return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, 1, false> : k_posterior_multi<false, kKpmWavesPerEu, 1, false>;
+    return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, 0, false> : k_posterior_multi<false, kKpmWavesPerEu, 0, false>;
 }
 
 // KLM over every (sample, tile) of the resident population layout, then KQN (shared by the two multisample paths)
 static hipError_t launch_pop_scan(Device* d, const GenotypeParams& g, uint32_t* need, QueueSite* queue, int64_t qcap,
-                                  unsigned long long* ctr, hipEvent_t ev_start, hipEvent_t ev_end) {
+                                  unsigned long long* ctr, hipEvent_t ev_start, hipEvent_t ev_end, PopStage* stage) {
     const int64_t nwords = d->g_len / 32 + 1;
     hipError_t e = hipMemsetAsync(need, 0, (size_t)nwords * sizeof(uint32_t), d->stream);
     if (e != hipSuccess) return e;
@@ -3461,12 +3558,47 @@ static hipError_t launch_pop_scan(Device* d, const GenotypeParams& g, uint32_t* 
     hipExtLaunchKernelGGL(klm, dim3((unsigned)nblk), dim3(kKlmThreads), 0, d->stream, ev_start, nullptr, 0,
                           (const uint64_t*)d->d_units, (const int2*)d->d_rh, (const RGroup*)d->d_grp,
                           (const int32_t*)d->d_samp_st, (const int32_t*)d->d_blkA, (const int32_t*)d->d_blkB, d->pnblk,
-                          d->pblk_shift, d->n_samples, (const uint8_t*)d->d_ref, (const LikTables*)d->d_tables, g, need, ctr);
+                          d->pblk_shift, d->n_samples, (const uint8_t*)d->d_ref, (const LikTables*)d->d_tables, g, need, ctr,
+                          stage ? stage->pairs : nullptr, stage ? stage->pseg : (int64_t)0);
     if ((e = launch_check()) != hipSuccess) return e;
     const int64_t qblk = std::max<int64_t>(1, std::min<int64_t>((nwords + 255) / 256, (int64_t)d->n_cu * 4));
     hipExtLaunchKernelGGL(k_queue_need, dim3((unsigned)qblk), dim3(256), 0, d->stream, nullptr, ev_end, 0,
-                          (const uint32_t*)need, (const uint8_t*)d->d_ref, nwords, queue, ctr, qcap);
-    return launch_check();
+                          (const uint32_t*)need, (const uint8_t*)d->d_ref, nwords, queue, ctr, qcap, stage ? stage->qword : nullptr);
+    if ((e = launch_check()) != hipSuccess) return e;
+    if (stage) {                                       // KPM's first stage's sample masks
+        hipLaunchKernelGGL(k_pair_mask, dim3(16, kKlShards), dim3(256), 0, d->stream, (const uint2*)stage->pairs, stage->pseg,
+                           (const uint32_t*)need, (const int32_t*)stage->qword, stage->pmask, qcap, ctr);
+        e = launch_check();
+    }
+    return e;
+}
+
+hipError_t PopStage::ensure(int64_t qcap, int64_t nwords, hipStream_t st) {
+    hipError_t e = hipSuccess;
+    if (qcap > cap) {
+        (void)hipFree(pmask); (void)hipFree(qB); (void)hipFree(pairs);
+        pmask = nullptr; qB = nullptr; pairs = nullptr;
+        if ((e = hipMalloc(&pmask, (size_t)qcap * 8 * sizeof(uint32_t))) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(pmask, 0, (size_t)qcap * 8 * sizeof(uint32_t), st)) != hipSuccess) return e;
+        if ((e = hipMalloc(&qB, (size_t)qcap * sizeof(QueueSite))) != hipSuccess) return e;
+        pseg = std::max<int64_t>(4096, qcap / 8);           // (segments past this: the first stage passes everything on)
+        if ((e = hipMalloc(&pairs, (size_t)pseg * kKlShards * sizeof(uint2))) != hipSuccess) return e;
+        cap = qcap;
+    }
+    if (nwords > cap_qword) {
+        (void)hipFree(qword);
+        qword = nullptr;
+        if ((e = hipMalloc(&qword, (size_t)nwords * sizeof(int32_t))) != hipSuccess) return e;
+        cap_qword = nwords;
+    }
+    return e;
+}
+
+// KPM's two stages apply to discovery without minAlleleDepthFrequency (the first stage's allele set is the called
+// alleles'), ploidy < 3 and the hom-ref bounds on (the samples they prove hom-ref are hom-ref for any allele set)
+static bool pop_two_stage(const Device* d, const GenotypeParams& g, double min_adf, int ploidy, bool mknown) {
+    static const bool off = env_hook("NGSEP_KPM_ONE_STAGE") != nullptr;   // (test hook: the one-stage path)
+    return !off && !mknown && d->prg && ploidy < 3 && min_adf == 0.0 && g.use_bound != 0;
 }
 static PopGather pop_gather_of(const Device* d) {
     PopGather pg{};
@@ -3523,24 +3655,37 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     HIP_TRY(hipMemsetAsync(ctr, 0, kCtrWords * sizeof(unsigned long long), d->stream));
     // KLM + KQN, timed together by events bound to their dispatches (ev 0-1), KPM by ev 1-2
     const bool mknown = d->n_mforced >= 0;             // -knownVariants (and the realigner's regions): the queue is given
+    const bool two = pop_two_stage(d, g, min_adf, ploidy, mknown);
+    if (two) HIP_TRY(d->pstage.ensure(d->cap_hard, d->g_len / 32 + 1, d->stream));
     if (mknown || !d->prg) {
         HIP_TRY(hipEventRecord(d->ev[0], d->stream));
         HIP_TRY(hipEventRecord(d->ev[1], d->stream));
     } else {
-        HIP_TRY(launch_pop_scan(d, g, d->d_need, d->d_hard, d->cap_hard, ctr, d->ev[0], d->ev[1]));
+        HIP_TRY(launch_pop_scan(d, g, d->d_need, d->d_hard, d->cap_hard, ctr, d->ev[0], d->ev[1], two ? &d->pstage : nullptr));
     }
     if (ploidy >= 3 && !d->pool_valid) { err = "ploidy >= 3 without pool tables (device_set_pool)"; return -1; }
     // (no start event on KPM: a start event between KQN and KPM was measured to idle the device; KPM's time is
     // taken from KQN's end)
     if (!mknown && !d->prg) { err = "multisample run without a population layout"; return -1; }
     const int mode = d->prg ? 1 : 0;
+    if (two) {
+        // the first stage over KQN's queue: the positions whose QS can pass -> the stage's queue (counter 7)
+        hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode, true), dim3(kKpmGrid), dim3(kPopThreads), kpm_lds(d, mode), d->stream,
+                              nullptr, nullptr, 0, (const QueueSite*)d->d_hard, (const unsigned long long*)(ctr + 2), d->cap_hard,
+                              (const uint8_t*)nullptr, (const uint16_t*)nullptr, (const int64_t*)nullptr, pop_gather_of(d),
+                              (const LikTables*)d->d_tables, g, S, min_adf, ploidy, (const PoolTables*)nullptr, d->d_psites,
+                              d->d_pcalls, ctr, d->cap_psites, (unsigned long long*)nullptr, d->pstage.pmask, d->pstage.qB, ctr + 7,
+                              d->pstage.cap);
+        HIP_TRY(launch_check());
+    }
     hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode), dim3(kKpmGrid), dim3(kPopThreads), kpm_lds(d, mode), d->stream, nullptr, d->ev[2], 0,
-                          (const QueueSite*)(mknown ? d->d_mforced : d->d_hard),
-                          (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : ctr + 2),
-                          mknown ? std::max<int64_t>(d->n_mforced, 1) : d->cap_hard, (const uint8_t*)d->d_ppile,
+                          (const QueueSite*)(mknown ? d->d_mforced : two ? d->pstage.qB : d->d_hard),
+                          (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : two ? ctr + 7 : ctr + 2),
+                          mknown ? std::max<int64_t>(d->n_mforced, 1) : two ? d->pstage.cap : d->cap_hard, (const uint8_t*)d->d_ppile,
                           (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, pop_gather_of(d), (const LikTables*)d->d_tables, g,
                           S, min_adf, ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), d->d_psites, d->d_pcalls,
-                          ctr, d->cap_psites, d->d_stamps);
+                          ctr, d->cap_psites, d->d_stamps, (uint32_t*)nullptr, (QueueSite*)nullptr, (unsigned long long*)nullptr,
+                          (int64_t)0);
     HIP_TRY(launch_check());
     DMA(d->h_counters, ctr, kCtrWords * sizeof(unsigned long long), 1, d->stream);
     HIP_TRY(hipStreamSynchronize(d->stream));
@@ -3795,21 +3940,32 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
     HIP_TRY(hipMemsetAsync(ctr, 0, kCtrWords * sizeof(unsigned long long), d->stream));
     const bool mknown = d->n_mforced >= 0;             // -knownVariants: the input variants are the queue
     if (!mknown && !d->prg) { err = "multisample run without a population layout"; return -1; }
+    const bool two = pop_two_stage(d, g, min_adf, ploidy, mknown);
+    if (two) HIP_TRY(m.stage.ensure(m.cap_hard, nwords, d->stream));
     if (mknown) {
         HIP_TRY(hipEventRecord(m.ev[0], d->stream));
         HIP_TRY(hipEventRecord(m.ev[1], d->stream));
     } else {
-        HIP_TRY(launch_pop_scan(d, g, m.d_need, m.d_hard, m.cap_hard, ctr, m.ev[0], m.ev[1]));
+        HIP_TRY(launch_pop_scan(d, g, m.d_need, m.d_hard, m.cap_hard, ctr, m.ev[0], m.ev[1], two ? &m.stage : nullptr));
     }
-    (void)nwords;
     const int mode = d->prg ? 1 : 0;
+    if (two) {
+        hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode, true), dim3(kKpmGrid), dim3(kPopThreads), kpm_lds(d, mode), d->stream,
+                              nullptr, nullptr, 0, (const QueueSite*)m.d_hard, (const unsigned long long*)(ctr + 2), m.cap_hard,
+                              (const uint8_t*)nullptr, (const uint16_t*)nullptr, (const int64_t*)nullptr, pop_gather_of(d),
+                              (const LikTables*)d->d_tables, g, S, min_adf, ploidy, (const PoolTables*)nullptr, m.d_psites,
+                              m.d_pcalls, ctr, m.cap_psites, (unsigned long long*)nullptr, m.stage.pmask, m.stage.qB, ctr + 7,
+                              m.stage.cap);
+        HIP_TRY(launch_check());
+    }
     hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode), dim3(kKpmGrid), dim3(kPopThreads), kpm_lds(d, mode), d->stream, nullptr, m.ev[3], 0,
-                          (const QueueSite*)(mknown ? d->d_mforced : m.d_hard),
-                          (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : ctr + 2),
-                          mknown ? std::max<int64_t>(d->n_mforced, 1) : m.cap_hard, (const uint8_t*)d->d_ppile,
+                          (const QueueSite*)(mknown ? d->d_mforced : two ? m.stage.qB : m.d_hard),
+                          (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : two ? ctr + 7 : ctr + 2),
+                          mknown ? std::max<int64_t>(d->n_mforced, 1) : two ? m.stage.cap : m.cap_hard, (const uint8_t*)d->d_ppile,
                           (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, pop_gather_of(d), (const LikTables*)d->d_tables, g,
                           S, min_adf, ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), m.d_psites, m.d_pcalls,
-                          ctr, m.cap_psites, (unsigned long long*)nullptr);
+                          ctr, m.cap_psites, (unsigned long long*)nullptr, (uint32_t*)nullptr, (QueueSite*)nullptr,
+                          (unsigned long long*)nullptr, (int64_t)0);
     HIP_TRY(launch_check());
     // the calls packed right behind KPM on the compute stream; the copies (counters, a guess of the sites, their
     // packed calls and whole records) on the copy stream, so the next pass's kernels do not wait for them
