@@ -215,6 +215,13 @@ def end_to_end(fa: str, bam: str, device: int):
             "positions": int(st.positions_genotyped), "value": st.positions_genotyped / (t2 - t0),
             "unit": "positions/s", "vcf_records": n_rec, "bam_bytes": os.path.getsize(bam),
             "realign_regions": int(st.realign_regions), "realign_replay_ms": float(st.realign_ms),
+            "phases_ms": {"realign_replay": float(st.realign_ms), "keep_raw": float(st.keep_raw_ms),
+                          "region_setup": float(st.region_setup_ms), "region_device": float(st.region_device_ms),
+                          "region_merge": float(st.region_merge_ms), "window_wait": float(st.window_wait_ms),
+                          "layout": float(st.layout_ms), "upload": float(st.upload_ms),
+                          "note": "host wall times summed over the windows (the replays, the regions' device run and "
+                                  "merge run on the window worker, beside the reader); window_wait: the reader joining "
+                                  "the worker"},
             "note": "ngsep_call_bam: BAM on disk -> VCF on disk incl. FASTA load; host threads "
                     f"{os.environ.get('NGSEP_THREADS') or cpu_cores()}"}
 

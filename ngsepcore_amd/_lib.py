@@ -155,6 +155,11 @@ class NgsepStats(ctypes.Structure):
         ("other_allele_calls", ctypes.c_int64),
         ("realign_ms", ctypes.c_double),         # ABI 10
         ("realign_regions", ctypes.c_int64),
+        ("keep_raw_ms", ctypes.c_double),
+        ("region_setup_ms", ctypes.c_double),
+        ("region_device_ms", ctypes.c_double),
+        ("region_merge_ms", ctypes.c_double),
+        ("window_wait_ms", ctypes.c_double),
     ]
 
 

@@ -533,7 +533,11 @@ static void project_pending(ngsep_ctx* c) {
     if (host_timing)
         std::fprintf(stderr, "[ngsep host] projection: %.1f ms (%u threads)\n",
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count(), host_threads());
-    if (realign_active(c)) keep_raw(c, b0, n, ent, carried);
+    if (realign_active(c)) {
+        const auto t_k = std::chrono::steady_clock::now();
+        keep_raw(c, b0, n, ent, carried);
+        c->keep_raw_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_k).count();
+    }
     v.clear();
     c->to_project_carried.clear();
 }
@@ -800,7 +804,7 @@ int stage_contig_reads(ngsep_ctx* c, ContigReads& cr, bool run_now) {
     std::vector<ContigReads> one;
     one.emplace_back(std::move(cr));
     cr = ContigReads();
-    int rc = build_and_upload(c, one);
+    int rc = build_and_upload(c, one, false);
     if (rc != NGSEP_OK) return rc;
     double ms = 0;
     const size_t from = c->pop_sites.size();
@@ -831,7 +835,9 @@ static void run_window_job(ngsep_ctx* c, WindowJob* j);
 static int stream_collect(ngsep_ctx* c) {
     auto& st = c->stream;
     if (!st.job) return NGSEP_OK;
+    const auto t_w = std::chrono::steady_clock::now();
     st.job->th.join();
+    c->window_wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_w).count();
     std::unique_ptr<WindowJob> j = std::move(st.job);
     if (j->rc != NGSEP_OK) return set_error(c, j->rc, j->err);
     if (j->realign) st.last_indel_end = j->last_indel_end;
@@ -962,6 +968,7 @@ static void stream_launch(ngsep_ctx* c, int64_t w0, int64_t w1) {
     }
     std::vector<std::vector<RawRead>> region_reads;
     std::string region_err;
+    const auto t_rr = std::chrono::steady_clock::now();
     if (realign_active(c)) {
         // the regions' alignments (whole regions: stream_advance never cuts one), in pending-list order; every
         // alignment that overlaps a region must have been kept
@@ -993,6 +1000,7 @@ static void stream_launch(ngsep_ctx* c, int64_t w0, int64_t w1) {
         for (auto& e : st.kept) if (!e.dead && e.last > w1) keep.push_back(std::move(e));
         st.kept.swap(keep);
         st.kept_maybe_from = 0;
+        c->region_setup_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_rr).count();
     }
     if (hi <= lo) return;                       // no read reaches the window: nothing to call
     auto j = std::make_unique<WindowJob>();
@@ -1657,7 +1665,10 @@ static inline void fill_group_units(uint64_t* dst, int32_t K, const uint8_t* con
 // units.  Headers: global first / last position and the strand bit.  The two
 // block tables give the scan its tile's entry range and the column gather the entries that can cover a
 // position.  Groups are independent: built on all host threads.
-static int build_rg_layout(Staged& s, const HugeVec<SRead>& reads, LayoutArena& arena, bool exact) {
+// consumed (a staged whole-genome run): called after every slice of groups with the reads whose bytes are in place, so
+// the caller can return their projected chunks while the rest is filled (peak host memory ~ one copy, not two)
+static int build_rg_layout(Staged& s, const HugeVec<SRead>& reads, LayoutArena& arena, bool exact,
+                           const std::function<void(int64_t)>& consumed = nullptr) {
     static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     const auto t0 = std::chrono::steady_clock::now();
     const int64_t n = (int64_t)reads.size();
@@ -1686,7 +1697,11 @@ static int build_rg_layout(Staged& s, const HugeVec<SRead>& reads, LayoutArena& 
     s.units_pinned = arena.units_pinned;
     const int32_t last_first = n ? reads[(size_t)n - 1].gfirst : 1;
     uint64_t* units = s.h_units;
-    parallel_for(ng, 64, [&](int64_t g0, int64_t g1) {
+    const int64_t slice = consumed ? (int64_t)1 << 15 : std::max<int64_t>(ng, 1);   // groups filled between two releases
+    for (int64_t sa = 0; sa < ng; sa += slice) {
+    const int64_t sb = std::min(ng, sa + slice);
+    parallel_for(sb - sa, 64, [&](int64_t q0, int64_t q1) {
+        const int64_t g0 = sa + q0, g1 = sa + q1;
         const uint8_t* src[64];
         const uint8_t* rfs[64];
         int64_t spans[64];
@@ -1715,6 +1730,8 @@ static int build_rg_layout(Staged& s, const HugeVec<SRead>& reads, LayoutArena& 
         }
         _mm_sfence();
     });
+    if (consumed) consumed(std::min(n, sb * 64));
+    }
     // block tables over the global coordinate (reads are sorted by gfirst)
     const int64_t nb = (s.g_len >> kRgBlockShift) + 2;
     s.h_blkA.resize((size_t)nb);
@@ -1986,7 +2003,7 @@ static int build_pop_rg_layout(Staged& s, LayoutArena& arena) {
     return 0;
 }
 
-int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
+int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs, bool release_chunks) {
     static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     const auto h0 = std::chrono::steady_clock::now();
     Staged& s = c->staged;
@@ -2067,8 +2084,22 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs) {
         s.n_read_bases = nbases;
         // the variant caller reads the read-group layout (KL scans it on the device); the relative allele counts
         // listener the position-major pile
+        // release_chunks (ngsep_stage_finish): a sequence's projected chunks go back once every read of its windows
+        // is in the layout -- the staged genome's bytes are then held about once, not twice (round 4: 114 GiB peak RSS
+        // staging configs[3] on one device)
+        std::vector<int64_t> contig_end(contigs.size(), 0);       // one past the sequence's last read in `reads`
+        for (size_t wi = 0; wi < s.windows.size(); wi++)
+            contig_end[wr[wi].contig] = std::max<int64_t>(contig_end[wr[wi].contig], s.windows[wi].read_end);
+        size_t next_rel = 0;
+        auto consumed = [&](int64_t done) {
+            while (next_rel < contigs.size() && contig_end[next_rel] <= done) {
+                std::vector<HostArray<uint8_t>>().swap(contigs[next_rel].chunks);
+                next_rel++;
+            }
+        };
         const int lr = c->params.relative_allele_counts ? build_single_layout(s, reads, c->arena, true)
-                                                        : build_rg_layout(s, reads, c->arena, true);
+                                                        : build_rg_layout(s, reads, c->arena, true,
+                                                                          release_chunks ? std::function<void(int64_t)>(consumed) : nullptr);
         if (lr == -2) return set_error(c, NGSEP_E_DEVICE, "pinned host memory for the layout could not be allocated");
         if (lr != 0) return set_error(c, NGSEP_E_INVALID, "internal error: pileup depth above the tile's row count");
         c->stats.slot_bytes = 0;
@@ -2287,6 +2318,8 @@ static void run_window_job(ngsep_ctx* c, WindowJob* j) {
 // layout (KP, queue entries with their columns); the listener's span rules over both; the kept SNV and indel
 // records merged into the window's, by position.  goff: window position p -> global p + goff.
 static int run_regions(ngsep_ctx* c, WindowJob* j, int64_t goff) {
+    using clk = std::chrono::steady_clock;
+    auto ns = [](clk::time_point a, clk::time_point b) { return std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count(); };
     const std::string& seq = c->seq_bases[(size_t)j->seq_id];
     const size_t nr = j->carved.size();
     std::vector<RegionOut> outs(nr);
@@ -2305,7 +2338,8 @@ static int run_regions(ngsep_ctx* c, WindowJob* j, int64_t goff) {
                           (size_t)j->seq_id < c->strs.size() ? &c->strs[(size_t)j->seq_id] : nullptr, &c->known_recs,
                           outs[(size_t)k]);
     });
-    c->realign_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_rp).count();
+    const auto t_q = clk::now();
+    c->realign_ns += ns(t_rp, t_q);
     c->realign_regions += (int64_t)nr;
     // KP's queue: {global position, reference code, column offset / 4, entries} per callable position
     Staged& s = c->staged;
@@ -2349,10 +2383,14 @@ static int run_regions(ngsep_ctx* c, WindowJob* j, int64_t goff) {
     s.h_forced_ctr[2] = (unsigned long long)(s.h_forced.size() / 4);
     s.h_forced_ctr[5] = (unsigned long long)(s.h_cols.size() / 4);
     SiteStore snv;
+    const auto t_d = clk::now();
+    c->region_setup_ns += ns(t_q, t_d);
     if (!s.h_forced.empty()) {
         const int rc = run_device_into(c, snv, nullptr);
         if (rc != NGSEP_OK) return rc;
     }
+    const auto t_m = clk::now();
+    c->region_device_ns += ns(t_d, t_m);
     // the listener's decisions, region by region (records and positions both ascending)
     SiteStore add;
     size_t ri = 0;
@@ -2422,6 +2460,7 @@ static int run_regions(ngsep_ctx* c, WindowJob* j, int64_t goff) {
     s.known = false;
     s.h_forced.clear();
     s.h_cols.clear();
+    c->region_merge_ns += ns(t_m, clk::now());
     return NGSEP_OK;
 }
 
@@ -3089,6 +3128,11 @@ extern "C" int ngsep_get_stats(ngsep_ctx* c, ngsep_stats* out) {
     *out = c->stats;
     out->realign_ms = (double)c->realign_ns.load() * 1e-6;
     out->realign_regions = c->realign_regions.load();
+    out->keep_raw_ms = (double)c->keep_raw_ns.load() * 1e-6;
+    out->region_setup_ms = (double)c->region_setup_ns.load() * 1e-6;
+    out->region_device_ms = (double)c->region_device_ns.load() * 1e-6;
+    out->region_merge_ms = (double)c->region_merge_ns.load() * 1e-6;
+    out->window_wait_ms = (double)c->window_wait_ns.load() * 1e-6;
     return NGSEP_OK;
 }
 
@@ -3599,7 +3643,7 @@ extern "C" int ngsep_stage_finish(ngsep_ctx* c) {
         return set_error(c, NGSEP_E_UNSUPPORTED, "relative allele counts and known-variant genotyping run on the streaming paths "
                                                  "(ngsep_process_alignments / ngsep_call_bam / ngsep_rac_bam)");
     }
-    rc = c->params.coverage_stats ? coverage_stage(c, c->staged_contigs) : build_and_upload(c, c->staged_contigs);
+    rc = c->params.coverage_stats ? coverage_stage(c, c->staged_contigs) : build_and_upload(c, c->staged_contigs, true);
     c->staged_contigs.clear();
     return rc;
 }

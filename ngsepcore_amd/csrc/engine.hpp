@@ -781,6 +781,7 @@ struct ngsep_ctx {
     std::vector<std::string> pop_text;                  // indel / STR population records (realigner regions), no sequence name
     ngsep_stats stats{};
     std::atomic<int64_t> realign_ns{0}, realign_regions{0};   // region replays (worker threads): stats.realign_*
+    std::atomic<int64_t> keep_raw_ns{0}, region_setup_ns{0}, region_device_ns{0}, region_merge_ns{0}, window_wait_ns{0};   // stats
 };
 
 namespace ngsep {
@@ -790,7 +791,7 @@ int set_error(ngsep_ctx* c, int code, const std::string& msg);
 int process_alignments_packed(ngsep_ctx* c, const ngsep_read_batch* b);
 void project_read(const ngsep_ctx* c, const ReadView& r, uint8_t* out);
 int stage_contig_reads(ngsep_ctx* c, ContigReads& cr, bool run_now);
-int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs);
+int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs, bool release_chunks);
 int run_device_into(ngsep_ctx* c, SiteStore& dest, double* elapsed_ms);
 int run_device(ngsep_ctx* c, double* elapsed_ms);
 void compute_tables(const ngsep_ctx* c, LikTables* t, GenotypeParams* g);

@@ -97,7 +97,7 @@ struct RunSlot {                     // one in-flight single-sample run (see dev
     std::chrono::steady_clock::time_point t0;
 };
 
-// KPM's two stages (k_posterior_multi STAGEA): KLM's (position, sample) pairs of the columns it could not prove hom-ref,
+// KPM's two stages (k_stage_a, then k_posterior_multi over its queue): KLM's (position, sample) pairs of the columns it could not prove hom-ref,
 // in kKlShards segments of pseg; KQN's queue index of every need word's first bit; per queued position a 256-bit sample
 // mask (zeroed once: the first stage clears what it read); the second stage's queue
 struct PopStage {
@@ -1462,9 +1462,6 @@ __global__ __launch_bounds__(256) void k_queue_need(const uint32_t* __restrict__
 // byte differences cannot carry.  Deeper populations run !COUNT: every marked position takes the exact bound.
 // The reads of no sample only enter the pooled counts: not scanned.  No block barrier after the tables: every wave's
 // state is its own.
-#ifndef NGSEP_KLM_COMPACT
-#define NGSEP_KLM_COMPACT 1
-#endif
 constexpr int kKlmThreads = 256;
 constexpr int kKlmWords = kKlmTile / 32 + 2;   // tile bitmap words, a 32-position margin on either side
 constexpr int kKlmUnroll = 4;                  // pass 1: unit loads per batch, the next batch issued before the current
@@ -1493,13 +1490,8 @@ __device__ __forceinline__ void unpack_dif(uint32_t w, int32_t d[4]) {
     }
 }
 
-#ifdef NGSEP_KLM_WPE
-#define KLM_WPE_ATTR __attribute__((amdgpu_waves_per_eu(NGSEP_KLM_WPE)))
-#else
-#define KLM_WPE_ATTR
-#endif
 template <bool COUNT>
-__global__ __launch_bounds__(kKlmThreads) KLM_WPE_ATTR void k_scan_pop(
+__global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_scan_pop(
     const uint64_t* __restrict__ units, const int2* __restrict__ rh, const RGroup* __restrict__ grp,
     const int32_t* __restrict__ samp_st, const int32_t* __restrict__ blkA, const int32_t* __restrict__ blkB,
     int64_t nblk, int32_t shift, int32_t n_samples, const uint8_t* __restrict__ ref, const LikTables* __restrict__ tabs,
@@ -1542,7 +1534,6 @@ __global__ __launch_bounds__(kKlmThreads) KLM_WPE_ATTR void k_scan_pop(
     for (int st = st0; st < st1; st++) {
         const int64_t e_lo = blkA[(int64_t)st * nblk + (tstart >> shift)];
         const int64_t e_hi = blkB[(int64_t)st * nblk + (tlast >> shift) + 1];
-#if NGSEP_KLM_COMPACT
         // rounds of 64 consecutive entries (lane = entry e0 + lane, whatever its group): every lane busy but in the
         // last round; the next round's header and group base in flight
         int2 h = e_lo + lane < e_hi ? rh[e_lo + lane] : make_int2(0, -1);
@@ -1557,22 +1548,6 @@ __global__ __launch_bounds__(kKlmThreads) KLM_WPE_ATTR void k_scan_pop(
             const bool act = e < e_hi && a <= b;
             const int32_t k0 = act ? (a - gf) >> 3 : 0, kn = act ? ((b - gf) >> 3) - k0 : -1;
             const uint64_t* ub = units + gbase + (e & 63) + (int64_t)k0 * 64;
-#else
-        const int64_t g_hi = (e_hi + 63) >> 6;
-        int64_t g = e_lo >> 6;
-        int2 h = g < g_hi ? rh[g * 64 + lane] : make_int2(0, -1);
-        int64_t gbase = g < g_hi ? grp[g].base : 0;
-        for (; g < g_hi; g++) {
-            const int64_t e = g * 64 + lane;
-            // the next group's header and base in flight
-            const int2 hn = g + 1 < g_hi ? rh[e + 64] : make_int2(0, -1);
-            const int64_t gbn = g + 1 < g_hi ? grp[g + 1].base : 0;
-            const int32_t gf = h.x, gl = h.y & 0x7FFFFFFF;
-            const int32_t a = max(gf, tstart), b = min(gl, tlast);
-            const bool act = e >= e_lo && e < e_hi && a <= b;
-            const int32_t k0 = act ? (a - gf) >> 3 : 0, kn = act ? ((b - gf) >> 3) - k0 : -1;
-            const uint64_t* ub = units + gbase + lane + (int64_t)k0 * 64;
-#endif
             const int32_t ti0 = gf + 8 * k0 - tstart + 32;   // bitmap index of unit k0's byte 0 (>= 25); COUNT: its
                                                               // counter byte is ti0 - 24 (>= 1)
             // COUNT: the read's last unit holds padding past its last position (zero bytes: quality-0 reference calls)
@@ -2205,27 +2180,160 @@ __device__ inline int32_t pop_gather(const PopGather& pg, int32_t p, int s, uint
     return rows;
 }
 
+// KPM's first stage (two-stage discovery: ploidy < 3, no -knownVariants, minAlleleDepthFrequency 0, the bounds on) -- one
+// wavefront per queued position, lane j = the j-th sample KLM could not prove hom-ref there (pmask, from KLM's pairs):
+// only those columns are gathered and genotyped.  Every other sample is hom-ref for any allele set,
+// so it adds no called allele and nothing to the variant QS; its other-allele calls only add alleles that no sample
+// calls, which the multi-allelic loop (discoverPopulationSNV :590-595, makeNewVariant) removes before the QS is final.
+// A position whose QS passes (onPileup :534) -- or with more than 64 such samples, or after a pair segment overflowed --
+// goes to qB, the second stage's queue (k_posterior_multi over every column); the others are done.  (The first version,
+// k_posterior_multi over the masked columns with one workgroup per position, measured 0.45 against one stage's 0.42 ms on
+// configs[4]: a position's chain of dependent gathers, not its columns, sets a workgroup's time.)
+struct LdsRow64 {
+    const double* p;
+    __device__ double operator[](int k) const { return p[k * 64]; }
+};
+__device__ __forceinline__ int nth_set_bit(uint32_t w, int r) {   // the r-th (0-based) set bit of w
+    for (int k = 0; k < r; k++) w &= w - 1u;
+    return __builtin_ctz(w);
+}
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_stage_a(
+    const QueueSite* __restrict__ queue, const unsigned long long* qn, int64_t qcap, const PopGather pg,
+    const LikTables* __restrict__ tabs, GenotypeParams gp, int32_t ploidy, uint32_t* __restrict__ pmask,
+    QueueSite* __restrict__ qB, unsigned long long* __restrict__ qB_n, int64_t qB_cap, unsigned long long* counters) {
+    __shared__ double s_t[3][32];
+    __shared__ double s_L[10][64];
+    extern __shared__ uint8_t s_gcol[];                  // the lanes' columns, pg.stride codes each
+    const int lane = threadIdx.x;
+    for (int k = lane; k < 96; k += 64) s_t[k >> 5][k & 31] = (k < 32 ? tabs->A : k < 64 ? tabs->H : tabs->E)[k & 31];
+    __syncthreads();
+    int64_t n = (int64_t)*qn;
+    if (n > qcap) n = qcap;
+    const bool passall = ((counters[3] >> 62) & 1ull) != 0;   // (a pair segment past its capacity)
+    auto pass_on = [&](const QueueSite& q) {
+        if (lane == 0) {
+            const unsigned long long k = atomicAdd(qB_n, 1ull);
+            if ((int64_t)k < qB_cap) qB[k] = q;
+        }
+    };
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const QueueSite qs = queue[i];
+        const uint32_t mw = lane < 8 ? pmask[i * 8 + lane] : 0u;
+        if (lane < 8) pmask[i * 8 + lane] = 0u;          // (cleared for the next pass)
+        if (passall) { pass_on(qs); continue; }
+        uint32_t incl = (uint32_t)__popc(mw);
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            const uint32_t x = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += x;
+        }
+        const uint32_t nmask = (uint32_t)__shfl((int)incl, 7, 64);
+        if (nmask > 64u) { pass_on(qs); continue; }
+        int s = -1;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t wk = (uint32_t)__shfl((int)mw, k, 64), ik = (uint32_t)__shfl((int)incl, k, 64);
+            const uint32_t ek = ik - (uint32_t)__popc(wk);
+            if ((uint32_t)lane >= ek && (uint32_t)lane < ik) s = 32 * k + nth_set_bit(wk, lane - (int)ek);
+        }
+        const int32_t gpos = qs.gpos;
+        const uint32_t rc = (uint32_t)qs.rc;
+        uint8_t* col = s_gcol + (int64_t)lane * pg.stride;
+        int32_t rows = 0;
+        if (s >= 0) {
+            rows = pop_gather<NGSEP_KPM_GBATCH>(pg, gpos, s, col, pg.stride);
+            if (rows > pg.stride) {                      // (the host's coverage bound makes this unreachable)
+                atomicOr(&counters[3], 1ull << 63);
+                rows = pg.stride;
+            }
+        }
+        // the sample's counts and log-conditionals (CountsHelper, as k_posterior_multi)
+        int total = 0;
+        int cnt[4] = {0, 0, 0, 0};
+        double L[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int32_t r = 0; r < rows; r++) {
+            const uint32_t cd = col[r];
+            total += cd != 0;
+            if (!(cd & 0x80u)) continue;
+            const uint32_t a = (cd >> 5) & 3u;
+            cnt[0] += a == 0; cnt[1] += a == 1; cnt[2] += a == 2; cnt[3] += a == 3;
+            int q = (int)(cd & 31u);
+            q = q > gp.max_q ? gp.max_q : q;
+            const double A = s_t[0][q], H = s_t[1][q], E = s_t[2][q];
+            L[0] += a == 0 ? A : E;
+            L[4] += a == 1 ? A : E;
+            L[7] += a == 2 ? A : E;
+            L[9] += a == 3 ? A : E;
+            L[1] += a <= 1 ? H : E;
+            L[2] += (a & 1) == 0 ? H : E;
+            L[3] += (a == 0 || a == 3) ? H : E;
+            L[5] += (a == 1 || a == 2) ? H : E;
+            L[6] += (a & 1) == 1 ? H : E;
+            L[8] += a >= 2 ? H : E;
+        }
+#pragma unroll
+        for (int k = 0; k < 10; k++) s_L[k][lane] = L[k];
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        const LdsRow64 Lr{&s_L[0][lane]};
+        int pc[4] = {cnt[0], cnt[1], cnt[2], cnt[3]};
+        int tt = total;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            pc[0] += __shfl_xor(pc[0], o, 64); pc[1] += __shfl_xor(pc[1], o, 64);
+            pc[2] += __shfl_xor(pc[2], o, 64); pc[3] += __shfl_xor(pc[3], o, 64);
+            tt += __shfl_xor(tt, o, 64);
+        }
+        if (tt == 0) continue;                                   // createSNVVariantPool: totalCount 0
+        if (!(rc & 0x80u)) continue;                             // N (or masked) reference: no variant
+        const int refIdx = (int)((rc >> 5) & 3u);
+        int idx[4] = {refIdx, 0, 0, 0};
+        int nal = 1;
+#pragma unroll
+        for (int a = 0; a < 4; a++)                              // minAlleleDepthFrequency 0: a count of 1
+            if (a != refIdx && sel4i(pc, a) >= 1) { set4i(idx, nal < 4 ? nal : 3, a); nal++; }
+        if (nal < 2) continue;
+        int qsv = 0;
+        for (;;) {
+            const PopCall call = genotype_sample_d(Lr, cnt, total, nal, idx, gp, ploidy);
+            const bool homref = call.n_called == 1 && call.c0 == 0;
+            int q = call.n_called > 0 && !homref ? call.gq : 0;
+            int bits = 0;
+            if (call.n_called >= 1) bits |= 1 << sel4i(idx, call.c0 & 3);
+            if (call.n_called == 2) bits |= 1 << sel4i(idx, call.c1 & 3);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                q = max(q, __shfl_xor(q, o, 64));
+                bits |= __shfl_xor(bits, o, 64);
+            }
+            qsv = q;
+            const int set = bits | (1 << refIdx);
+            if (nal <= 2) break;
+            if (__popc(set) == nal) break;
+            nal = 1;
+#pragma unroll
+            for (int a = 0; a < 4; a++) if (a != refIdx && (set >> a & 1)) { set4i(idx, nal, a); nal++; }
+            if (nal < 2) break;
+        }
+        if (nal < 2) continue;                                   // only the reference allele is left
+        if (qsv == 0 || qsv < gp.min_quality) continue;          // MultisampleVariantsDetector.java:534
+        pass_on(qs);
+    }
+}
+
 // POOL: ploidy >= 3 (the pool branch's report arrays would otherwise cost every run registers and scratch).
 // GATHER, where the columns come from: 0 a site-major pile (the realigner's region positions, engine.cpp
 // run_population_regions; ppile / prow / pboff); 1 the population read-group layout, gathered here into dynamic LDS
 // (measured and not kept: a separate gather kernel, one thread per (position, sample) at 8 waves per SIMD, into
 // columns KPM then read with the next position's in flight -- 0.64 against 0.52 ms for gather + KPM on configs[4]:
 // the gather's cost is its scattered lines, ~10 per sample column, not latency KPM fails to hide)
-// STAGEA (KPM's first stage; GATHER 1, ploidy < 3, discovery with minAlleleDepthFrequency 0 and the bounds on): only
-// the columns of the samples KLM could not prove hom-ref at the position (pmask: one bit per sample, from KLM's pairs)
-// are gathered and genotyped -- every other sample is hom-ref for any allele set, so it adds no
-// called allele and nothing to the variant QS; its other-allele calls only add alleles that no sample calls, which the
-// multi-allelic loop (discoverPopulationSNV :590-595, makeNewVariant) removes before the QS is final.  A position whose
-// QS passes (onPileup :533) goes to qB for the full genotyping (the second stage, every column); the others are done.
-template <bool POOL, int WPE, int GATHER, bool STAGEA>
+template <bool POOL, int WPE, int GATHER>
 __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE))) void k_posterior_multi(
     const QueueSite* __restrict__ queue, const unsigned long long* qn, int64_t qcap,
     const uint8_t* __restrict__ ppile, const uint16_t* __restrict__ prow, const int64_t* __restrict__ pboff,
     const PopGather pg, const LikTables* __restrict__ tabs, GenotypeParams gp,
     int32_t n_samples, double min_adf, int32_t ploidy, const PoolTables* __restrict__ pt,
     ngsep_popsite_out* __restrict__ sites, ngsep_sample_call* __restrict__ calls,
-    unsigned long long* counters, int64_t cap, unsigned long long* __restrict__ stamps,
-    uint32_t* __restrict__ pmask, QueueSite* __restrict__ qB, unsigned long long* __restrict__ qB_n, int64_t qB_cap) {
+    unsigned long long* counters, int64_t cap, unsigned long long* __restrict__ stamps) {
     // stamps (diagnostics, NGSEP_TIMING): s_memtime at the phase ends of block 0's first site
     auto stamp = [&](int k) {
         if (stamps && blockIdx.x == 0 && threadIdx.x == 0) stamps[k] = __builtin_amdgcn_s_memtime();
@@ -2261,8 +2369,6 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
         qs_next = queue[blockIdx.x];
         if (GATHER != 1) column_of(blockIdx.x, qs_next.gpos, rows_next, col_next);
     }
-    // (a pair segment past its capacity: the first stage hands every position to the second)
-    const bool passall = STAGEA && ((counters[3] >> 62) & 1ull);
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         __syncthreads();
         const QueueSite qs = qs_next;
@@ -2270,14 +2376,6 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
         const uint32_t rc = (uint32_t)qs.rc;
         const int64_t inext = i + gridDim.x;
         if (inext < n) qs_next = queue[inext];
-        if (STAGEA && passall) {
-            if (threadIdx.x == 0) {
-                const unsigned long long k = atomicAdd(qB_n, 1ull);
-                if ((int64_t)k < qB_cap) qB[k] = qs;
-            }
-            if (threadIdx.x < 8) pmask[i * 8 + threadIdx.x] = 0u;
-            continue;
-        }
         if (tid == 0) { s_pc[0] = s_pc[1] = s_pc[2] = s_pc[3] = 0; s_tot = 0; s_called = 0; s_qs = 0; }
         __syncthreads();
         // 1-3. thread s walks sample s's column of the pile (read-group rank order, pending order inside:
@@ -2292,8 +2390,7 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
         const uint8_t* col = col_next;
         if (GATHER == 1 && tid <= n_samples) {
             uint8_t* dst = s_gcol + (int64_t)tid * pg.stride;
-            const bool mine = !STAGEA || (tid < n_samples && ((pmask[i * 8 + (tid >> 5)] >> (tid & 31)) & 1u));
-            rows = mine ? pop_gather<NGSEP_KPM_GBATCH>(pg, gpos, tid, dst, pg.stride) : 0;
+            rows = pop_gather<NGSEP_KPM_GBATCH>(pg, gpos, tid, dst, pg.stride);
             if (rows > pg.stride) {                          // (the host's coverage bound makes this unreachable)
                 atomicOr(&counters[3], 1ull << 63);
                 rows = pg.stride;
@@ -2351,7 +2448,6 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
         }
         if (tid == n_samples) { total = 0; cnt[0] = cnt[1] = cnt[2] = cnt[3] = 0; }
         __syncthreads();
-        if (STAGEA && tid < 8) pmask[i * 8 + tid] = 0u;         // (read: cleared for the next pass)
         if (i == blockIdx.x) stamp(2);
         // -knownVariants (MultisampleVariantsDetector.onPileup :539-551): the input variant's own alleles, every
         // sample genotyped (genotypeVariant :674-693) and the record written whatever its QS
@@ -2419,13 +2515,6 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
         if (i == blockIdx.x) stamp(5);
         if (nal < 2) continue;                                     // only the reference allele is left
         if (!known && (qsv == 0 || qsv < gp.min_quality)) continue;   // MultisampleVariantsDetector.java:534
-        if (STAGEA) {                                              // a record: the second stage genotypes every column
-            if (tid == 0) {
-                const unsigned long long k = atomicAdd(qB_n, 1ull);
-                if ((int64_t)k < qB_cap) qB[k] = qs;
-            }
-            continue;
-        }
         // 6. emit the site and its calls
         __syncthreads();
         if (tid == 0) s_base = atomicAdd(&counters[0], 1ull);
@@ -3536,11 +3625,19 @@ int device_run_rac(Device* d, const Staged& s, int64_t g0, int64_t g1, int32_t m
 #endif
 constexpr int kKpmWavesPerEu = NGSEP_KPM_WPE;
 constexpr unsigned kKpmGrid = 16384;
-static auto kpm_kernel(int ploidy, int gather, bool stage_a = false) {
-    if (stage_a) return k_posterior_multi<false, kKpmWavesPerEu, 1, true>;
+// (diagnostics, DIAG builds: the KPM and first-stage grids, NGSEP_KPM_GRID / NGSEP_STA_GRID)
+static unsigned kpm_grid() {
+    static const unsigned g = diag_env("NGSEP_KPM_GRID") ? std::max(1u, (unsigned)std::atoi(diag_env("NGSEP_KPM_GRID"))) : kKpmGrid;
+    return g;
+}
+static unsigned sta_grid() {
+    static const unsigned g = diag_env("NGSEP_STA_GRID") ? std::max(1u, (unsigned)std::atoi(diag_env("NGSEP_STA_GRID"))) : kKpmGrid;
+    return g;
+}
+static auto kpm_kernel(int ploidy, int gather) {
     if (gather == 1)
-        return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, 1, false> : k_posterior_multi<false, kKpmWavesPerEu, 1, false>;
-    return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, 0, false> : k_posterior_multi<false, kKpmWavesPerEu, 0, false>;
+        return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, 1> : k_posterior_multi<false, kKpmWavesPerEu, 1>;
+    return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, 0> : k_posterior_multi<false, kKpmWavesPerEu, 0>;
 }
 
 // KLM over every (sample, tile) of the resident population layout, then KQN (shared by the two multisample paths)
@@ -3581,7 +3678,7 @@ hipError_t PopStage::ensure(int64_t qcap, int64_t nwords, hipStream_t st) {
         if ((e = hipMalloc(&pmask, (size_t)qcap * 8 * sizeof(uint32_t))) != hipSuccess) return e;
         if ((e = hipMemsetAsync(pmask, 0, (size_t)qcap * 8 * sizeof(uint32_t), st)) != hipSuccess) return e;
         if ((e = hipMalloc(&qB, (size_t)qcap * sizeof(QueueSite))) != hipSuccess) return e;
-        pseg = std::max<int64_t>(4096, qcap / 8);           // (segments past this: the first stage passes everything on)
+        pseg = std::max<int64_t>(4096, qcap / 4);           // (segments past this: the first stage passes everything on)
         if ((e = hipMalloc(&pairs, (size_t)pseg * kKlShards * sizeof(uint2))) != hipSuccess) return e;
         cap = qcap;
     }
@@ -3606,6 +3703,14 @@ static PopGather pop_gather_of(const Device* d) {
     pg.units = d->d_units; pg.rh = d->d_rh; pg.grp = d->d_grp; pg.samp_st = d->d_samp_st; pg.st_end = d->d_st_end;
     pg.blkA = d->d_blkA; pg.ref = d->d_ref; pg.nblk = d->pnblk; pg.shift = d->pblk_shift; pg.stride = d->pop_stride;
     return pg;
+}
+// KPM's first stage over KQN's queue (k_stage_a, one wavefront per position): the positions whose QS can pass -> the
+// stage's queue (counter 7), which the second stage (k_posterior_multi) genotypes in full
+static hipError_t launch_stage_a(Device* d, const GenotypeParams& g, int ploidy, const QueueSite* queue,
+                                 const unsigned long long* qn, int64_t qcap, PopStage& st, unsigned long long* ctr) {
+    hipLaunchKernelGGL(k_stage_a, dim3(sta_grid()), dim3(64), (size_t)64 * (size_t)d->pop_stride, d->stream, queue, qn, qcap,
+                       pop_gather_of(d), (const LikTables*)d->d_tables, g, (int32_t)ploidy, st.pmask, st.qB, ctr + 7, st.cap, ctr);
+    return launch_check();
 }
 static size_t kpm_lds(const Device* d, int mode) { return mode == 1 ? (size_t)(d->n_samples + 1) * (size_t)d->pop_stride : 0; }
 // the shard counters' sums: KLM's candidate columns and bounded columns
@@ -3669,23 +3774,15 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     if (!mknown && !d->prg) { err = "multisample run without a population layout"; return -1; }
     const int mode = d->prg ? 1 : 0;
     if (two) {
-        // the first stage over KQN's queue: the positions whose QS can pass -> the stage's queue (counter 7)
-        hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode, true), dim3(kKpmGrid), dim3(kPopThreads), kpm_lds(d, mode), d->stream,
-                              nullptr, nullptr, 0, (const QueueSite*)d->d_hard, (const unsigned long long*)(ctr + 2), d->cap_hard,
-                              (const uint8_t*)nullptr, (const uint16_t*)nullptr, (const int64_t*)nullptr, pop_gather_of(d),
-                              (const LikTables*)d->d_tables, g, S, min_adf, ploidy, (const PoolTables*)nullptr, d->d_psites,
-                              d->d_pcalls, ctr, d->cap_psites, (unsigned long long*)nullptr, d->pstage.pmask, d->pstage.qB, ctr + 7,
-                              d->pstage.cap);
-        HIP_TRY(launch_check());
+        HIP_TRY(launch_stage_a(d, g, ploidy, d->d_hard, ctr + 2, d->cap_hard, d->pstage, ctr));
     }
-    hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode), dim3(kKpmGrid), dim3(kPopThreads), kpm_lds(d, mode), d->stream, nullptr, d->ev[2], 0,
+    hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode), dim3(kpm_grid()), dim3(kPopThreads), kpm_lds(d, mode), d->stream, nullptr, d->ev[2], 0,
                           (const QueueSite*)(mknown ? d->d_mforced : two ? d->pstage.qB : d->d_hard),
                           (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : two ? ctr + 7 : ctr + 2),
                           mknown ? std::max<int64_t>(d->n_mforced, 1) : two ? d->pstage.cap : d->cap_hard, (const uint8_t*)d->d_ppile,
                           (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, pop_gather_of(d), (const LikTables*)d->d_tables, g,
                           S, min_adf, ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), d->d_psites, d->d_pcalls,
-                          ctr, d->cap_psites, d->d_stamps, (uint32_t*)nullptr, (QueueSite*)nullptr, (unsigned long long*)nullptr,
-                          (int64_t)0);
+                          ctr, d->cap_psites, d->d_stamps);
     HIP_TRY(launch_check());
     DMA(d->h_counters, ctr, kCtrWords * sizeof(unsigned long long), 1, d->stream);
     HIP_TRY(hipStreamSynchronize(d->stream));
@@ -3950,22 +4047,15 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
     }
     const int mode = d->prg ? 1 : 0;
     if (two) {
-        hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode, true), dim3(kKpmGrid), dim3(kPopThreads), kpm_lds(d, mode), d->stream,
-                              nullptr, nullptr, 0, (const QueueSite*)m.d_hard, (const unsigned long long*)(ctr + 2), m.cap_hard,
-                              (const uint8_t*)nullptr, (const uint16_t*)nullptr, (const int64_t*)nullptr, pop_gather_of(d),
-                              (const LikTables*)d->d_tables, g, S, min_adf, ploidy, (const PoolTables*)nullptr, m.d_psites,
-                              m.d_pcalls, ctr, m.cap_psites, (unsigned long long*)nullptr, m.stage.pmask, m.stage.qB, ctr + 7,
-                              m.stage.cap);
-        HIP_TRY(launch_check());
+        HIP_TRY(launch_stage_a(d, g, ploidy, m.d_hard, ctr + 2, m.cap_hard, m.stage, ctr));
     }
-    hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode), dim3(kKpmGrid), dim3(kPopThreads), kpm_lds(d, mode), d->stream, nullptr, m.ev[3], 0,
+    hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode), dim3(kpm_grid()), dim3(kPopThreads), kpm_lds(d, mode), d->stream, nullptr, m.ev[3], 0,
                           (const QueueSite*)(mknown ? d->d_mforced : two ? m.stage.qB : m.d_hard),
                           (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : two ? ctr + 7 : ctr + 2),
                           mknown ? std::max<int64_t>(d->n_mforced, 1) : two ? m.stage.cap : m.cap_hard, (const uint8_t*)d->d_ppile,
                           (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, pop_gather_of(d), (const LikTables*)d->d_tables, g,
                           S, min_adf, ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), m.d_psites, m.d_pcalls,
-                          ctr, m.cap_psites, (unsigned long long*)nullptr, (uint32_t*)nullptr, (QueueSite*)nullptr,
-                          (unsigned long long*)nullptr, (int64_t)0);
+                          ctr, m.cap_psites, (unsigned long long*)nullptr);
     HIP_TRY(launch_check());
     // the calls packed right behind KPM on the compute stream; the copies (counters, a guess of the sites, their
     // packed calls and whole records) on the copy stream, so the next pass's kernels do not wait for them
