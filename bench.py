@@ -218,6 +218,7 @@ def end_to_end(fa: str, bam: str, device: int):
             "phases_ms": {"realign_replay": float(st.realign_ms), "keep_raw": float(st.keep_raw_ms),
                           "region_setup": float(st.region_setup_ms), "region_device": float(st.region_device_ms),
                           "region_merge": float(st.region_merge_ms), "window_wait": float(st.window_wait_ms),
+                          "region_gather": float(st.region_gather_ms),
                           "layout": float(st.layout_ms), "upload": float(st.upload_ms),
                           "note": "host wall times summed over the windows (the replays, the regions' device run and "
                                   "merge run on the window worker, beside the reader); window_wait: the reader joining "

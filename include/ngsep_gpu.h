@@ -207,10 +207,11 @@ typedef struct ngsep_stats {
     int64_t realign_regions;        /* ABI 10: realigner regions replayed */
     /* ABI 11: where the indel path's host time goes (path B, single sample; wall times, summed over windows) */
     double  keep_raw_ms;            /* the reader thread keeping the raw alignments a region can need (keep_raw) */
-    double  region_setup_ms;        /* the regions' reads gathered and their queue built (before / after the replays) */
+    double  region_setup_ms;        /* the regions' device queue built from the replays (window worker) */
     double  region_device_ms;       /* the regions' span-1 columns genotyped on the device (one more KP run per window) */
     double  region_merge_ms;        /* the listener's span rules and the merge of the region records into the window's */
     double  window_wait_ms;         /* the reader thread waiting for a free window worker (device + regions behind) */
+    double  region_gather_ms;       /* the regions' kept alignments gathered for the worker (reader thread) */
 } ngsep_stats;
 
 /* ---- -knownVariants (SingleSampleVariantsDetector.findSNVS :896-906, MultisampleVariantsDetector.run :432-438) ---- */

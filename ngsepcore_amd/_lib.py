@@ -160,6 +160,7 @@ class NgsepStats(ctypes.Structure):
         ("region_device_ms", ctypes.c_double),
         ("region_merge_ms", ctypes.c_double),
         ("window_wait_ms", ctypes.c_double),
+        ("region_gather_ms", ctypes.c_double),
     ]
 
 

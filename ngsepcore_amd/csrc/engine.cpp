@@ -270,6 +270,19 @@ static inline char packed_base(const char* seq, int64_t i) {
     const uint8_t b = (uint8_t)seq[i >> 1];
     return kNt[(i & 1) ? (b & 15) : (b >> 4)];
 }
+// a BAM-packed read's n characters (4 bits each, high nibble first) into out: one table load per byte
+static void unpack_bases(const char* seq, int32_t n, char* out) {
+    static const uint16_t* tab = [] {
+        static uint16_t t[256];
+        static const char kNt[] = "=ACMGRSVTWYHKDBN";
+        for (int b = 0; b < 256; b++) t[b] = (uint16_t)((uint8_t)kNt[b >> 4] | (uint16_t)(uint8_t)kNt[b & 15] << 8);
+        return t;
+    }();
+    const uint8_t* s = reinterpret_cast<const uint8_t*>(seq);
+    const int32_t pairs = n >> 1;
+    for (int32_t k = 0; k < pairs; k++) std::memcpy(out + 2 * k, &tab[s[k]], 2);
+    if (n & 1) out[n - 1] = packed_base(seq, n - 1);
+}
 
 void project_read(const ngsep_ctx* c, const ReadView& r, uint8_t* out) {
     const int64_t span = (int64_t)r.last - r.first + 1;
@@ -618,51 +631,95 @@ static void keep_raw(ngsep_ctx* c, size_t b0, size_t n, const int32_t* ent, cons
         if (covered(e.first, e.last)) e.maybe = false;
         else if ((int64_t)e.last + R < frontier) { e.maybe = false; e.dead = true; }
     }
-    // the reads to keep (serial: cheap decisions), then their raw alignments copied on all host threads
+    // the reads to keep (decided on all host threads: 0 no, 1 covered, 2 maybe), listed in order, their entries then
+    // filled on all host threads
     const size_t k0 = st.kept.size();
+    std::vector<uint8_t> how(n);
+    const auto& Y = cr.indel_reads;
+    const size_t ny = Y.size();
+    parallel_for((int64_t)n, 1 << 14, [&](int64_t lo, int64_t hi) {
+        // covered(f, l) with a cursor instead of a search per read: the reads come in start order (a search again
+        // where one does not), so the indel reads with first <= f + R only grow; those up to l + R are a few more
+        size_t k = 0;
+        int64_t fprev = INT64_MAX;
+        for (int64_t i = lo; i < hi; i++) {
+            const int32_t f = cr.first[b0 + (size_t)i], l = cr.last[b0 + (size_t)i];
+            if ((int64_t)f < fprev)
+                k = (size_t)(std::upper_bound(Y.begin(), Y.end(), (int64_t)f + R,
+                                              [](int64_t v, const std::pair<int32_t, int32_t>& y) { return v < (int64_t)y.first; }) - Y.begin());
+            fprev = f;
+            while (k < ny && (int64_t)Y[k].first <= (int64_t)f + R) k++;
+            size_t kk = k;
+            while (kk < ny && (int64_t)Y[kk].first <= (int64_t)l + R) kk++;
+            const bool cov = kk > 0 && (int64_t)st.indel_pmax[kk - 1] + R >= f;
+            how[(size_t)i] = cov ? 1 : (int64_t)l + R >= frontier ? 2 : 0;
+        }
+    });
     std::vector<size_t> src;
-    for (size_t i = 0; i < n; i++) {
-        const int32_t f = cr.first[b0 + i], l = cr.last[b0 + i];
-        const bool cov = covered(f, l);
-        const bool maybe = !cov && (int64_t)l + R >= frontier;
-        if (!cov && !maybe) continue;
-        std::remove_reference_t<decltype(st.kept)>::value_type e;
-        e.first = f;
-        e.last = l;
-        e.maybe = maybe;
-        e.dead = false;
-        st.kept.push_back(std::move(e));
-        src.push_back(i);
-    }
+    for (size_t i = 0; i < n; i++) if (how[i]) src.push_back(i);
+    st.kept.resize(k0 + src.size());
+    // one block of bytes per slice of kept reads (CIGAR items, then characters and qualities), shared by their RawReads:
+    // a copy for a second region is a view, and no read costs an allocation of its own
     parallel_for((int64_t)src.size(), 512, [&](int64_t q0, int64_t q1) {
-      for (int64_t q = q0; q < q1; q++) {
-        const size_t i = src[(size_t)q];
-        const ReadView r = ent[i] >= 0 ? batch_view(c->cur_batch, ent[i]) : carried[-1 - ent[i]];
-        RawRead& rr = st.kept[k0 + (size_t)q].r;
-        rr.first = r.first;
-        rr.last = r.last;
-        rr.flags = r.flags;
-        rr.ops.assign(r.cigar, r.cigar + r.n_cigar);
-        rr.has_chars = r.chars != nullptr && r.len > 0;
-        if (rr.has_chars) {
-            rr.chars.resize((size_t)r.len);
-            for (int32_t k = 0; k < r.len; k++) rr.chars[(size_t)k] = r.packed ? packed_base(r.chars, k) : r.chars[k];
+        auto view = [&](int64_t q) {
+            const size_t i = src[(size_t)q];
+            return ent[i] >= 0 ? batch_view(c->cur_batch, ent[i]) : carried[-1 - ent[i]];
+        };
+        size_t bytes = 0;
+        for (int64_t q = q0; q < q1; q++) {
+            const ReadView r = view(q);
+            bytes += (size_t)r.n_cigar * sizeof(int32_t) + (r.chars != nullptr && r.len > 0 ? 2 * (size_t)r.len : 0);
         }
-        rr.has_quals = rr.has_chars && r.quals != nullptr;
-        if (rr.has_quals) {
-            rr.quals.resize((size_t)r.len);
-            for (int32_t k = 0; k < r.len; k++)
-                rr.quals[(size_t)k] = r.packed ? (char)std::min(255, (unsigned char)r.quals[k] + 33) : r.quals[k];
+        auto blk = std::make_shared<RawBlock>();
+        blk->bytes.reset(new char[std::max<size_t>(bytes, 1)]);
+        char* at = blk->bytes.get();
+        std::shared_ptr<const RawBlock> hold = blk;
+        // (the CIGAR items of the whole slice first: int32 alignment)
+        char* tail = at;
+        for (int64_t q = q0; q < q1; q++) tail += (size_t)view(q).n_cigar * sizeof(int32_t);
+        for (int64_t q = q0; q < q1; q++) {
+            const ReadView r = view(q);
+            auto& e = st.kept[k0 + (size_t)q];
+            e.first = cr.first[b0 + src[(size_t)q]];
+            e.last = cr.last[b0 + src[(size_t)q]];
+            e.maybe = how[src[(size_t)q]] == 2;
+            e.dead = false;
+            RawRead& rr = e.r;
+            rr.first = r.first;
+            rr.last = r.last;
+            rr.flags = r.flags;
+            rr.n_ops = r.n_cigar;
+            std::memcpy(at, r.cigar, (size_t)r.n_cigar * sizeof(int32_t));
+            rr.ops = reinterpret_cast<const int32_t*>(at);
+            at += (size_t)r.n_cigar * sizeof(int32_t);
+            rr.len = 0;
+            rr.chars = rr.quals = nullptr;
+            if (r.chars != nullptr && r.len > 0) {
+                rr.len = r.len;
+                char* ch = tail;
+                char* qu = tail + r.len;
+                tail += 2 * (size_t)r.len;
+                if (r.packed) unpack_bases(r.chars, r.len, ch);
+                else std::memcpy(ch, r.chars, (size_t)r.len);
+                rr.chars = ch;
+                if (r.quals != nullptr) {
+                    if (r.packed) {
+                        const uint8_t* rq = reinterpret_cast<const uint8_t*>(r.quals);
+                        for (int32_t k = 0; k < r.len; k++) qu[k] = (char)(rq[k] > 222 ? 255 : rq[k] + 33);
+                    } else std::memcpy(qu, r.quals, (size_t)r.len);
+                    rr.quals = qu;
+                }
+            }
+            rr.hold = hold;
+            const bool neg = (r.flags & 0x10) != 0;            // setBasesToIgnore5P/3P (ReadAlignment.java:613-644)
+            rr.ignore_start = neg ? c->params.ignore3 : c->params.ignore5;
+            rr.ignore_end = neg ? c->params.ignore5 : c->params.ignore3;
+            if (c->params.multisample) {                        // the read group's sample and its rank there
+                const bool in = r.rg >= 0 && r.rg < (int32_t)c->rg_sample.size();
+                rr.sample = (int16_t)(in ? c->rg_sample[(size_t)r.rg] : -1);
+                rr.rank = (uint8_t)(in && c->rg_sample[(size_t)r.rg] >= 0 ? c->rg_rank[(size_t)r.rg] : 0);
+            }
         }
-        const bool neg = (r.flags & 0x10) != 0;            // setBasesToIgnore5P/3P (ReadAlignment.java:613-644)
-        rr.ignore_start = neg ? c->params.ignore3 : c->params.ignore5;
-        rr.ignore_end = neg ? c->params.ignore5 : c->params.ignore3;
-        if (c->params.multisample) {                        // the read group's sample and its rank there
-            const bool in = r.rg >= 0 && r.rg < (int32_t)c->rg_sample.size();
-            rr.sample = (int16_t)(in ? c->rg_sample[(size_t)r.rg] : -1);
-            rr.rank = (uint8_t)(in && c->rg_sample[(size_t)r.rg] >= 0 ? c->rg_rank[(size_t)r.rg] : 0);
-        }
-      }
     });
     while (st.kept_maybe_from < st.kept.size() && !st.kept[st.kept_maybe_from].maybe) st.kept_maybe_from++;
     if (!streaming(c)) {
@@ -670,7 +727,7 @@ static void keep_raw(ngsep_ctx* c, size_t b0, size_t n, const int32_t* ent, cons
         size_t dead = 0;
         for (size_t k = st.kept_maybe_from; k < st.kept.size(); k++) dead += st.kept[k].dead ? 1 : 0;
         if (dead > (1u << 14) && dead * 2 > st.kept.size() - st.kept_maybe_from) {
-            std::deque<std::remove_reference_t<decltype(st.kept)>::value_type> live;
+            std::remove_reference_t<decltype(st.kept)> live;
             for (auto& e : st.kept) if (!e.dead) live.push_back(std::move(e));
             st.kept.swap(live);
             st.kept_maybe_from = 0;
@@ -996,11 +1053,11 @@ static void stream_launch(ngsep_ctx* c, int64_t w0, int64_t w1) {
                              std::to_string((int64_t)want - (int64_t)region_reads[k].size()) + " alignments";
         }
         // alignments that end in this window reach no later region
-        std::deque<std::remove_reference_t<decltype(st.kept)>::value_type> keep;
+        std::remove_reference_t<decltype(st.kept)> keep;
         for (auto& e : st.kept) if (!e.dead && e.last > w1) keep.push_back(std::move(e));
         st.kept.swap(keep);
         st.kept_maybe_from = 0;
-        c->region_setup_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_rr).count();
+        c->region_gather_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_rr).count();
     }
     if (hi <= lo) return;                       // no read reaches the window: nothing to call
     auto j = std::make_unique<WindowJob>();
@@ -2347,11 +2404,29 @@ static int run_regions(ngsep_ctx* c, WindowJob* j, int64_t goff) {
     s.h_forced.clear();
     s.h_cols.clear();
     const int64_t kb = known ? c->known_seq_begin[(size_t)j->seq_id] : 0, ke = known ? c->known_seq_begin[(size_t)j->seq_id + 1] : 0;
+    // discovery: only the positions with a valid call of another allele than the reference are genotyped (DESIGN.md
+    // section 5 -- any other column is hom-ref, which no listener writes), under the conditions the window's own run
+    // prunes with; their columns alone are copied
+    const bool prune = c->params.prune_candidates && !c->params.dump_all_positions && (c->het_rate <= 0.1 || c->params.ploidy >= 3);
     for (size_t k = 0; k < nr; k++) {
         const RegionOut& o = outs[k];
+        if (!known) {
+            for (const RegionPos& p : o.pos) {
+                if (p.blocked || p.col_len == 0 || (prune && !p.nonref)) continue;
+                const uint8_t rc = ref_code(c, seq[(size_t)p.pos - 1]);
+                if (!(rc & kRefCallable)) continue;
+                const size_t cb = s.h_cols.size();
+                s.h_cols.insert(s.h_cols.end(), o.cols.begin() + p.col_off, o.cols.begin() + p.col_off + ((p.col_len + 3) & ~3));
+                s.h_forced.push_back((int32_t)(p.pos + goff));
+                s.h_forced.push_back((int32_t)rc);
+                s.h_forced.push_back((int32_t)(cb / 4));
+                s.h_forced.push_back(p.col_len);
+            }
+            continue;
+        }
         const size_t cbase = s.h_cols.size();
         s.h_cols.insert(s.h_cols.end(), o.cols.begin(), o.cols.end());
-        if (known) {
+        {
             // -knownVariants: the region's input SNVs at positions with a pileup, in input order, genotyped from the
             // replayed columns (queue code 0x80 | ref << 5 | alt << 8 | 0x400, as stream_launch's)
             auto it = std::lower_bound(c->known.begin() + kb, c->known.begin() + ke, o.first,
@@ -2367,16 +2442,6 @@ static int run_regions(ngsep_ctx* c, WindowJob* j, int64_t goff) {
                 s.h_forced.push_back((int32_t)((cbase + (size_t)p.col_off) / 4));
                 s.h_forced.push_back(p.col_len);
             }
-            continue;
-        }
-        for (const RegionPos& p : o.pos) {
-            if (p.blocked || p.col_len == 0) continue;
-            const uint8_t rc = ref_code(c, seq[(size_t)p.pos - 1]);
-            if (!(rc & kRefCallable)) continue;
-            s.h_forced.push_back((int32_t)(p.pos + goff));
-            s.h_forced.push_back((int32_t)rc);
-            s.h_forced.push_back((int32_t)((cbase + (size_t)p.col_off) / 4));
-            s.h_forced.push_back(p.col_len);
         }
     }
     std::memset(s.h_forced_ctr, 0, sizeof s.h_forced_ctr);
@@ -3130,6 +3195,7 @@ extern "C" int ngsep_get_stats(ngsep_ctx* c, ngsep_stats* out) {
     out->realign_regions = c->realign_regions.load();
     out->keep_raw_ms = (double)c->keep_raw_ns.load() * 1e-6;
     out->region_setup_ms = (double)c->region_setup_ns.load() * 1e-6;
+    out->region_gather_ms = (double)c->region_gather_ns.load() * 1e-6;
     out->region_device_ms = (double)c->region_device_ns.load() * 1e-6;
     out->region_merge_ms = (double)c->region_merge_ns.load() * 1e-6;
     out->window_wait_ms = (double)c->window_wait_ns.load() * 1e-6;

@@ -745,7 +745,7 @@ struct ngsep_ctx {
         // the indel realigner (params.indel_passthrough = 0): admitted alignments kept for its regions' replays --
         // those inside a known region's reach and those a later indel read could still reach (`maybe`)
         struct Kept { int32_t first, last; bool maybe, dead; ngsep::RawRead r; };
-        std::deque<Kept> kept;
+        std::vector<Kept> kept;
         size_t kept_maybe_from = 0;               // entries before this one are not `maybe`
         std::vector<int32_t> indel_pmax;          // running max of indel_reads[k].second (the regions' ends)
         int32_t last_indel_end = 0;               // SingleSampleVariantPileupListener.lastIndelEnd (this sequence)
@@ -781,7 +781,7 @@ struct ngsep_ctx {
     std::vector<std::string> pop_text;                  // indel / STR population records (realigner regions), no sequence name
     ngsep_stats stats{};
     std::atomic<int64_t> realign_ns{0}, realign_regions{0};   // region replays (worker threads): stats.realign_*
-    std::atomic<int64_t> keep_raw_ns{0}, region_setup_ns{0}, region_device_ns{0}, region_merge_ns{0}, window_wait_ns{0};   // stats
+    std::atomic<int64_t> keep_raw_ns{0}, region_setup_ns{0}, region_device_ns{0}, region_merge_ns{0}, window_wait_ns{0}, region_gather_ns{0};   // stats
 };
 
 namespace ngsep {

@@ -3625,10 +3625,13 @@ int device_run_rac(Device* d, const Staged& s, int64_t g0, int64_t g1, int32_t m
 #endif
 constexpr int kKpmWavesPerEu = NGSEP_KPM_WPE;
 constexpr unsigned kKpmGrid = 16384;
-// (diagnostics, DIAG builds: the KPM and first-stage grids, NGSEP_KPM_GRID / NGSEP_STA_GRID)
-static unsigned kpm_grid() {
-    static const unsigned g = diag_env("NGSEP_KPM_GRID") ? std::max(1u, (unsigned)std::atoi(diag_env("NGSEP_KPM_GRID"))) : kKpmGrid;
-    return g;
+// KPM's grid: one workgroup per slot the occupancy leaves (3 waves per SIMD, 4-wave workgroups: 3 per CU), each looping
+// over the queue -- configs[4] KPM 0.302 -> 0.256 ms against 16384 workgroups (the empty ones' dispatch was the
+// difference; 512 / 1024 / 1536 per 256 CUs: 0.283 / 0.259 / 0.283 ms, tools/gpu_r5_indel.sh).  (DIAG builds:
+// NGSEP_KPM_GRID / NGSEP_STA_GRID override the two grids.)
+static unsigned kpm_grid(const Device* d) {
+    static const char* e = diag_env("NGSEP_KPM_GRID");
+    return e ? std::max(1u, (unsigned)std::atoi(e)) : (unsigned)std::max(1, d->n_cu * 3);
 }
 static unsigned sta_grid() {
     static const unsigned g = diag_env("NGSEP_STA_GRID") ? std::max(1u, (unsigned)std::atoi(diag_env("NGSEP_STA_GRID"))) : kKpmGrid;
@@ -3776,7 +3779,7 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     if (two) {
         HIP_TRY(launch_stage_a(d, g, ploidy, d->d_hard, ctr + 2, d->cap_hard, d->pstage, ctr));
     }
-    hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode), dim3(kpm_grid()), dim3(kPopThreads), kpm_lds(d, mode), d->stream, nullptr, d->ev[2], 0,
+    hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode), dim3(kpm_grid(d)), dim3(kPopThreads), kpm_lds(d, mode), d->stream, nullptr, d->ev[2], 0,
                           (const QueueSite*)(mknown ? d->d_mforced : two ? d->pstage.qB : d->d_hard),
                           (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : two ? ctr + 7 : ctr + 2),
                           mknown ? std::max<int64_t>(d->n_mforced, 1) : two ? d->pstage.cap : d->cap_hard, (const uint8_t*)d->d_ppile,
@@ -4049,7 +4052,7 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
     if (two) {
         HIP_TRY(launch_stage_a(d, g, ploidy, m.d_hard, ctr + 2, m.cap_hard, m.stage, ctr));
     }
-    hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode), dim3(kpm_grid()), dim3(kPopThreads), kpm_lds(d, mode), d->stream, nullptr, m.ev[3], 0,
+    hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode), dim3(kpm_grid(d)), dim3(kPopThreads), kpm_lds(d, mode), d->stream, nullptr, m.ev[3], 0,
                           (const QueueSite*)(mknown ? d->d_mforced : two ? m.stage.qB : m.d_hard),
                           (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : two ? ctr + 7 : ctr + 2),
                           mknown ? std::max<int64_t>(d->n_mforced, 1) : two ? m.stage.cap : m.cap_hard, (const uint8_t*)d->d_ppile,

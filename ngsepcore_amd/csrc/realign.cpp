@@ -67,16 +67,29 @@ struct IndelEv {
 struct Aln {
     int32_t first, last, flags, read_length;
     std::vector<int32_t> ops;
-    const std::string* chars;            // nullptr: no characters
-    const std::string* quals;            // nullptr: no qualities
+    const char* chars;                   // nullptr: no characters (read_length of them otherwise)
+    const char* quals;                   // nullptr: no qualities
     int32_t ignore_start, ignore_end;
     std::vector<int16_t> acl;            // alleleCallLength per read position
     std::vector<IndelEv> indels;         // indelCalls (TreeMap by refPos)
     int16_t sample = -1;                 // multisample: sample and read-group rank (RawRead)
     uint8_t rank = 0;
+    int* edits = nullptr;                // replay_region's count of updates (its indel-position marks are then redrawn)
+    std::vector<uint16_t> codes;         // per read position: the span-1 column entry (update())
+    bool simple = false;                 // one M item over the whole read: read position = pos - first
 
     // updateAlleleCallsInfo (ReadAlignment.java:747-834)
     void update() {
+        if (edits) ++*edits;
+        simple = ops.size() == 1 && (ops[0] & 7) == OP_M && ops[0] / 8 == read_length;
+        if (simple) {
+            // one M item over the whole read: no indel, so only the ignored ends make no call (the loop below, reduced)
+            acl.assign((size_t)std::max(read_length, 1), 0);
+            indels.clear();
+            for (int r = std::max(0, ignore_start); r < read_length && read_length - r > ignore_end; r++) acl[(size_t)r] = 1;
+            fill_codes();
+            return;
+        }
         acl.assign((size_t)std::max(read_length, 1), 0);
         indels.clear();
         int refPos = first, readPos = 0;
@@ -124,6 +137,48 @@ struct Aln {
             }
             prevIndel = op == OP_D || op == OP_I;
         }
+        fill_codes();
+    }
+    // every read position's span-1 column entry (replay_region's getAlleleCalls(1)): engine.hpp's code | negative
+    // strand << 8, 0xFFFF where the read makes no span-1 call there
+    void fill_codes() {
+        codes.assign(acl.size(), 0xFFFF);
+        if (!chars) return;
+        // (code_table: the code of every (quality character, read character) pair, as the branches in its comment)
+        const uint8_t(*T)[256] = code_table();
+        const uint16_t strand = (flags & 0x10) ? 0x100 : 0;
+        const unsigned char* qs = reinterpret_cast<const unsigned char*>(quals);
+        const unsigned char* cs = reinterpret_cast<const unsigned char*>(chars);
+        const int16_t* ac = acl.data();
+        uint16_t* out = codes.data();
+        for (int r = 0; r < read_length; r++)
+            if (ac[r] == 1) out[r] = (uint16_t)(T[qs ? qs[r] : '+'][cs[r]] | strand);
+    }
+    // code_table()[qc][ch]: q = (byte) min(30, min(qc, 127) - 33) (setQualityScores cap); q <= 3: counted | max(q, 0);
+    // a character that is not A/C/G/T: counted | q; else valid | base << 5 | q (engine.hpp codes)
+    static const uint8_t (*code_table())[256] {
+        static const auto* t = [] {
+            static uint8_t tab[256][256];
+            for (int qc0 = 0; qc0 < 256; qc0++) {
+                const int qc = qc0 > 127 ? 127 : qc0;
+                const int q = (int8_t)std::min(30, qc - 33);
+                for (int ch = 0; ch < 256; ch++) {
+                    const int b = base_index((char)ch);
+                    uint8_t code;
+                    if (q <= 3) code = (uint8_t)(kCodeCounted | (q < 0 ? 0 : q));
+                    else if (b < 0) code = (uint8_t)(kCodeCounted | q);
+                    else code = (uint8_t)(kCodeValid | (b << 5) | q);
+                    tab[qc0][ch] = code;
+                }
+            }
+            return &tab;
+        }();
+        return *t;
+    }
+    // the span-1 entry at reference position pos of an alignment of the pileup (first <= pos <= last), 0xFFFF for none
+    uint16_t code_at(int pos) const {
+        const int r = simple ? pos - first : read_pos(pos);
+        return r < 0 ? (uint16_t)0xFFFF : codes[(size_t)r];
     }
     // getAlignedReadPosition (:842-871)
     int read_pos(int refPos) const {
@@ -157,7 +212,7 @@ struct Aln {
     }
     int soft_clip_start() const { return !ops.empty() && (ops.front() & 7) == OP_S ? ops.front() / 8 : 0; }   // :1351-1356
     int soft_clip_end() const { return !ops.empty() && (ops.back() & 7) == OP_S ? ops.back() / 8 : 0; }       // :1358-1363
-    char qual(int rp) const { return quals ? (*quals)[(size_t)rp] : '+'; }
+    char qual(int rp) const { return quals ? quals[rp] : '+'; }
     // getAlleleCall(pos) (:989-1000): read offset, length in *len; -1 for none
     int call1(int pos, int* len) const {
         if (!chars) return -1;
@@ -374,7 +429,7 @@ private:
             int lengthTR = 0;                       // checkTandemRepeat(aln, pos) (:351-357)
             const int rf = a->read_pos(pos);
             if (rf >= 0 && a->chars) {
-                std::string sub = a->chars->substr((size_t)rf + 1, (size_t)(a->read_length - rf - 1));
+                std::string sub(a->chars + rf + 1, (size_t)(a->read_length - rf - 1));
                 for (char& ch : sub) ch = upper(ch);
                 lengthTR = tandem_repeat(sub.data(), (int)sub.size());
             }
@@ -397,7 +452,7 @@ private:
             auto it = std::find(keys.begin(), keys.end(), il);
             size_t g = (size_t)(it - keys.begin());
             if (it == keys.end()) { keys.push_back(il); groups.emplace_back(); }
-            groups[g].push_back(a->chars->substr((size_t)off + 1, (size_t)il));
+            groups[g].push_back(std::string(a->chars + off + 1, (size_t)il));
         }
         if (keys.empty()) return false;
         const std::vector<int> ord = hashmap_order(keys);
@@ -460,8 +515,8 @@ private:
             const int readPosAfter = a->read_pos(eventLast);
             if (!indelBefore && hasBefore && readPosAfter >= bpGood && readPosAfter - offset <= kMaxBpRealignmentEnd &&
                 readPosAfter < lRefB && readPosAfter < lAltB && !a->indel_at(eventFirst) && a->chars) {
-                const int refDist = hamming(refBefore.data() + lRefB - readPosAfter, a->chars->data(), readPosAfter);
-                const int altDist = hamming(altBefore.data() + lAltB - readPosAfter, a->chars->data(), readPosAfter);
+                const int refDist = hamming(refBefore.data() + lRefB - readPosAfter, a->chars, readPosAfter);
+                const int altDist = hamming(altBefore.data() + lAltB - readPosAfter, a->chars, readPosAfter);
                 const int newAlnFirst = eventLast - readPosAfter + 1 + offset;
                 const int firstMatchLength = eventFirst - newAlnFirst + 1;
                 if (altDist < refDist && altDist < 3 && firstMatchLength >= kMinBpGoodRefAln) {
@@ -479,7 +534,7 @@ private:
             const int readSuffixLength = readPosBefore >= 0 ? a->read_length - readPosBefore - 1 : 0;
             if (!indelAfter && hasAfter && readSuffixLength >= bpGood && readSuffixLength - offset <= kMaxBpRealignmentEnd &&
                 readSuffixLength < lRefA && readSuffixLength < lAltA && (!a->indel_at(eventFirst) || readPosAfter < 0) && a->chars) {
-                const char* suffix = a->chars->data() + readPosBefore + 1;
+                const char* suffix = a->chars + readPosBefore + 1;
                 const int refDist = hamming(refAfter.data(), suffix, readSuffixLength);
                 const int altDist = hamming(altAfter.data(), suffix, readSuffixLength);
                 const int finalMatchLength = readSuffixLength - (offset > 0 ? offset : 0);
@@ -569,7 +624,7 @@ void span_calls(const std::vector<Aln*>& alns, int pos, int span, std::vector<Sp
         if (span == 1) {
             if (l1 > 1) continue;
             SpanCall c;
-            c.allele.assign(1, (*a->chars)[(size_t)o1]);
+            c.allele.assign(1, a->chars[o1]);
             c.qual.assign(1, a->qual(o1));
             out.push_back(std::move(c));
             continue;
@@ -578,7 +633,7 @@ void span_calls(const std::vector<Aln*>& alns, int pos, int span, std::vector<Sp
         const int off = a->call_range(pos, pos + span - 1, &len);
         if (off < 0) continue;
         SpanCall c;
-        c.allele = a->chars->substr((size_t)off, (size_t)len);
+        c.allele.assign(a->chars + off, (size_t)len);
         c.qual.resize((size_t)len);
         for (int i = 0; i < len; i++) c.qual[(size_t)i] = a->qual(off + i);
         out.push_back(std::move(c));
@@ -1300,16 +1355,37 @@ void replay_region(const std::string& seq, int64_t first, int64_t last, std::vec
         a.first = r.first;
         a.last = r.last;
         a.flags = r.flags;
-        a.ops = r.ops;
+        a.ops.assign(r.ops, r.ops + r.n_ops);
         a.read_length = 0;
         for (int32_t v : a.ops) if (v & 2) a.read_length += v / 8;
-        a.chars = r.has_chars ? &r.chars : nullptr;
-        a.quals = r.has_quals ? &r.quals : nullptr;
+        // (the characters are the read's; a CIGAR consuming more of the read than it has would index past them)
+        a.chars = r.chars && r.len >= a.read_length ? r.chars : nullptr;
+        a.quals = a.chars ? r.quals : nullptr;
         a.ignore_start = r.ignore_start;
         a.ignore_end = r.ignore_end;
         a.sample = r.sample;
         a.rank = r.rank;
         a.update();
+    }
+    // the positions where some alignment has an indel call (getIndelCall != null): elsewhere, with no input variant
+    // there, the realigner's onPileup returns span 1 without looking further (its loop over the pileup finds no indel);
+    // redrawn after any alignment is edited (a superset of the pileup's is all the shortcut needs)
+    int edits = 0, edits_marked = -1;
+    const int64_t mark_lo = first;
+    std::vector<uint8_t> indel_mark((size_t)std::max<int64_t>(last - first + 1, 1), 0);
+    auto remark = [&]() {
+        std::fill(indel_mark.begin(), indel_mark.end(), 0);
+        for (const Aln& a : alns)
+            for (const IndelEv& e : a.indels)
+                if (e.first >= mark_lo && e.first <= last) indel_mark[(size_t)(e.first - mark_lo)] = 1;
+        edits_marked = edits;
+    };
+    for (Aln& a : alns) a.edits = &edits;
+    {
+        size_t want = 0;                                   // (the columns' entries: at most one per read and position)
+        for (const Aln& a : alns) want += (size_t)std::max<int64_t>(0, std::min<int64_t>(a.last, last) - std::max<int64_t>(a.first, first) + 1);
+        out.cols.reserve(want + 4 * (size_t)(last - first + 1));
+        out.pos.reserve((size_t)(last - first + 1));
     }
     Realigner rl(seq);
     std::vector<int32_t> pending;          // indices into alns, admission order
@@ -1334,15 +1410,6 @@ void replay_region(const std::string& seq, int64_t first, int64_t last, std::vec
     for (int64_t p64 = first; p64 <= last; p64++) {
         const int pos = (int)p64;
         while (next < alns.size() && reads[next].first <= pos) pending.push_back((int32_t)next++);   // (original starts)
-        // updatePendingAlns (AlignmentsPileupGenerator.java:464-471): alignments ending before pos retire
-        size_t k = 0;
-        for (int32_t i : pending) if (alns[(size_t)i].last >= pos) pending[k++] = i;
-        pending.resize(k);
-        pileup.clear();
-        for (int32_t i : pending) if (alns[(size_t)i].first <= pos) pileup.push_back(&alns[(size_t)i]);
-        if (pileup.empty()) continue;
-        RegionPos rp;
-        rp.pos = pos;
         const StrVar* var = nullptr;                                       // intersectWithVariants (:137-153)
         while (vi < vn) {
             const StrVar& v = (*strs)[vi];
@@ -1350,25 +1417,68 @@ void replay_region(const std::string& seq, int64_t first, int64_t last, std::vec
             if (pos <= v.last) { var = &v; break; }
             vi++;
         }
-        rp.span = rl.on_pileup(pileup, pos, var, &rp.str, &rp.new_str, &rp.var_embedded);
-        // getAlleleCalls(1): the device's column entries (engine.cpp project_read's codes)
-        rp.col_off = (int32_t)out.cols.size();
-        for (const Aln* a : pileup) {
-            if (!a->chars) continue;
-            const int r = a->read_pos(pos);
-            if (r < 0 || a->acl[(size_t)r] != 1) continue;
-            int qc = (unsigned char)a->qual(r);
-            if (qc > 127) qc = 127;                                        // setQualityScores cap
-            const int q = (int8_t)std::min(30, qc - 33);
-            const int b = base_index((*a->chars)[(size_t)r]);
-            uint8_t code;
-            if (q <= 3) code = (uint8_t)(kCodeCounted | (q < 0 ? 0 : q));
-            else if (b < 0) code = (uint8_t)(kCodeCounted | q);
-            else code = (uint8_t)(kCodeValid | (b << 5) | q);
-            out.cols.push_back((uint16_t)(code | (((a->flags & 0x10) ? 1u : 0u) << 8)));
+        if (edits != edits_marked) remark();
+        // the realigner's onPileup does something here only with an input variant or an indel call at pos; the pileup
+        // list itself is needed by it, by the population columns and by -knownVariants
+        const bool onp = var || indel_mark[(size_t)(p64 - mark_lo)];
+        RegionPos rp;
+        rp.pos = pos;
+        if (!onp && !pop && !p.known) {
+            // updatePendingAlns (AlignmentsPileupGenerator.java:464-471) and getAlleleCalls(1) in one pass: the pending
+            // alignments that end before pos retire, those that start at or before it give the column's entries
+            const size_t c0 = out.cols.size();
+            out.cols.resize(c0 + pending.size() + 3);
+            uint16_t* dst = out.cols.data() + c0;
+            size_t k = 0, npile = 0;
+            const uint32_t refa = (uint32_t)base_index(upper(seq[(size_t)p64 - 1]));   // (~0u: not A/C/G/T)
+            uint32_t nonref = 0;
+            for (int32_t i : pending) {
+                const Aln* a = &alns[(size_t)i];
+                if (a->last < pos) continue;
+                pending[k++] = i;
+                if (a->first > pos) continue;
+                npile++;
+                const uint16_t cd = a->code_at(pos);                       // (Aln::update's codes)
+                if (cd == 0xFFFF) continue;
+                *dst++ = cd;
+                nonref |= (uint32_t)((cd & kCodeValid) != 0) & (uint32_t)(((cd >> 5) & 3u) != refa);
+            }
+            pending.resize(k);
+            const size_t n = (size_t)(dst - (out.cols.data() + c0));
+            if (npile == 0) { out.cols.resize(c0); continue; }
+            rp.nonref = nonref != 0;
+            rp.span = 1;
+            rp.col_off = (int32_t)c0;
+            rp.col_len = (int32_t)n;
+            out.cols.resize(c0 + ((n + 3) & ~(size_t)3));
+            for (size_t z = c0 + n; z < out.cols.size(); z++) out.cols[z] = 0;
+        } else {
+            // updatePendingAlns (AlignmentsPileupGenerator.java:464-471): alignments ending before pos retire; the
+            // pileup is the pending ones that start at or before pos
+            size_t k = 0;
+            pileup.clear();
+            for (int32_t i : pending) {
+                Aln* a = &alns[(size_t)i];
+                if (a->last < pos) continue;
+                pending[k++] = i;
+                if (a->first <= pos) pileup.push_back(a);
+            }
+            pending.resize(k);
+            if (pileup.empty()) continue;
+            if (onp) rp.span = rl.on_pileup(pileup, pos, var, &rp.str, &rp.new_str, &rp.var_embedded);
+            else rp.span = 1;
+            // getAlleleCalls(1): the device's column entries (engine.cpp project_read's codes)
+            rp.col_off = (int32_t)out.cols.size();
+            const uint32_t refa = (uint32_t)base_index(upper(seq[(size_t)p64 - 1]));
+            for (const Aln* a : pileup) {
+                const uint16_t cd = a->code_at(pos);                       // (Aln::update's codes)
+                if (cd == 0xFFFF) continue;
+                out.cols.push_back(cd);
+                if ((cd & kCodeValid) && ((cd >> 5) & 3u) != refa) rp.nonref = true;
+            }
+            rp.col_len = (int32_t)out.cols.size() - rp.col_off;
+            while (out.cols.size() % 4) out.cols.push_back(0);
         }
-        rp.col_len = (int32_t)out.cols.size() - rp.col_off;
-        while (out.cols.size() % 4) out.cols.push_back(0);
         if (pop) {
             // getAlleleCalls(1, sample.getReadGroups()) per sample (read-group rank, then the pileup's order) and the
             // calls of the reads of no sample (the pooled counts' getAlleleCalls(1, null) adds them): KPM's columns
@@ -1380,18 +1490,9 @@ void replay_region(const std::string& seq, int64_t first, int64_t last, std::vec
                 for (int r = 0; r <= maxrank; r++)
                     for (const Aln* a : pileup) {
                         const bool mine = sm < S ? (a->sample == sm && a->rank == r) : (a->sample < 0 || a->sample >= S);
-                        if (!mine || !a->chars) continue;
-                        const int rr = a->read_pos(pos);
-                        if (rr < 0 || a->acl[(size_t)rr] != 1) continue;
-                        int qc = (unsigned char)a->qual(rr);
-                        if (qc > 127) qc = 127;
-                        const int q = (int8_t)std::min(30, qc - 33);
-                        const int b = base_index((*a->chars)[(size_t)rr]);
-                        uint8_t code;
-                        if (q <= 3) code = (uint8_t)(kCodeCounted | (q < 0 ? 0 : q));
-                        else if (b < 0) code = (uint8_t)(kCodeCounted | q);
-                        else code = (uint8_t)(kCodeValid | (b << 5) | q);
-                        out.pcodes.push_back(code);
+                        if (!mine) continue;
+                        const uint16_t cd = a->code_at(pos);
+                        if (cd != 0xFFFF) out.pcodes.push_back((uint8_t)cd);
                     }
             }
             out.poff.push_back((uint32_t)out.pcodes.size());
@@ -1435,14 +1536,6 @@ void replay_region(const std::string& seq, int64_t first, int64_t last, std::vec
             }
         }
         out.pos.push_back(rp);
-    }
-    // the edited alignments back to the caller
-    for (size_t i = 0; i < reads.size(); i++) {
-        reads[i].first = alns[i].first;
-        reads[i].last = alns[i].last;
-        reads[i].ops = alns[i].ops;
-        reads[i].ignore_start = alns[i].ignore_start;
-        reads[i].ignore_end = alns[i].ignore_end;
     }
 }
 

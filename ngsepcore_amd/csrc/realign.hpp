@@ -13,21 +13,27 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
 namespace ngsep {
 
 // an admitted alignment as the realigner needs it (ReadAlignment fields), in admission (pending-list) order
+// the bytes of a run of kept alignments (engine.cpp keep_raw: one block per slice of reads, shared by their RawReads)
+struct RawBlock {
+    std::unique_ptr<char[]> bytes;
+};
 struct RawRead {
     int32_t first = 0, last = 0, flags = 0;
-    std::vector<int32_t> ops;          // NGSEP CIGAR codes len * 8 + op
-    std::string chars;                 // read characters (has_chars = false: getReadCharacters() == null)
-    std::string quals;                 // phred + 33 (has_quals = false: '*')
-    bool has_chars = false, has_quals = false;
+    int32_t n_ops = 0, len = 0;        // CIGAR items; read characters (and qualities) held
+    const int32_t* ops = nullptr;      // NGSEP CIGAR codes len * 8 + op
+    const char* chars = nullptr;       // read characters (nullptr: getReadCharacters() == null)
+    const char* quals = nullptr;       // phred + 33 (nullptr: '*')
     int32_t ignore_start = 0, ignore_end = 0;   // setBasesToIgnore5P/3P by strand (ReadAlignment.java:613-644)
     int16_t sample = -1;               // multisample: the sample of the read group (-1: none), and the read group's rank
     uint8_t rank = 0;                  //   in the sample's HashSet order (PileupRecord.getAlleleCalls(span, readGroups))
+    std::shared_ptr<const RawBlock> hold;   // keeps ops / chars / quals alive (a copy is a view, not a deep copy)
 };
 
 struct RealignParams {
@@ -55,6 +61,7 @@ struct RegionPos {
     int32_t col_off = 0, col_len = 0;  // span-1 column: u16 entries code | negative strand << 8 in RegionOut::cols
     int32_t indel = -1;                // span > 1: index into RegionOut::indels of the span's call (-1: none)
     bool blocked = false;              // no call at all (span past the sequence end, lower-case reference ignored)
+    bool nonref = false;               // the span-1 column holds a valid call of another allele than the reference base
     int32_t pcol = -1;                 // population mode: its span-1 columns, samples 0 .. S - 1 then the reads of no
                                        // sample: RegionOut::pcodes[poff[pcol + s] .. poff[pcol + s + 1])
     int32_t pindel = -1;               // population mode, span > 1: index into RegionOut::pindels when
@@ -122,7 +129,7 @@ struct KnownRecord {
 
 // replays AlignmentsPileupGenerator + IndelRealignerPileupListener over [first, last] of one sequence (`seq`: the
 // reference as loaded, case kept); `reads` are the admitted alignments overlapping it in pending-list order
-// (edited in place); `inputs`: the sequence's realigner input variants (may be null); `knowns`: the records their
+// (read only); `inputs`: the sequence's realigner input variants (may be null); `knowns`: the records their
 // `known` indexes name (p.known)
 void replay_region(const std::string& seq, int64_t first, int64_t last, std::vector<RawRead>& reads, const RealignParams& p,
                    const InputVars* inputs, const std::vector<KnownRecord>* knowns, RegionOut& out);

@@ -1,6 +1,7 @@
 #!/bin/bash
-# round 5: kept alignments as views into shared blocks (keep_raw) -- the indel / realigner GPU tests, KPM's two stages
-# against one stage, the default bench line (chr20 end-to-end legs with the indel phases), then KPM grid sizes (DIAG)
+# round 5: the indel path's host work (kept alignments as views into shared blocks, the replay's fused sweep) -- the
+# indel / realigner / population GPU tests, the default bench line (chr20 end-to-end legs with the indel phases), the
+# configs[4] line and its rocprof kernel summary
 set -o pipefail
 export NGSEP_SKIP_BUILD=1
 cd "$GRAFT_REPO_ROOT"
@@ -19,16 +20,7 @@ e = d["end_to_end"]
 print("snv e2e %.3f s" % e["wall_s"], json.dumps(e["phases_ms"]))
 print("indel e2e %.3f s" % e["indels"]["wall_s"], json.dumps(e["indels"]["phases_ms"]))
 PY
-B="python -u bench.py --config multisample --no-cpu-baseline --no-cold --no-e2e --steps 20 --warmup 4"
-D=$PWD/ngsepcore_amd/lib_diag/libngsep_amd.so
-run() {   # name [extra env]
-  env $2 NGSEP_TIME_POSTERIOR=1 NGSEP_LIB_PATH=$D timeout -k 10 300 $B > gpurun_out/${TAG}_$1.json 2> gpurun_out/${TAG}_$1.err || { tail -5 gpurun_out/${TAG}_$1.err; return 1; }
-  python - <<PY
-import json
-d = json.loads(open("gpurun_out/${TAG}_$1.json").read().strip().splitlines()[-1])
-r = d["roofline"]
-print("$1", "step %.3f ms" % d["ms_per_step"], "klm %.3f ms" % r["kernel_avg_ms"], "kpm", r["posterior_kernel_avg_ms"])
-PY
-}
-run kg256 NGSEP_KPM_GRID=256 && run kg512 NGSEP_KPM_GRID=512 && run kg768 NGSEP_KPM_GRID=768 && run kg1024 NGSEP_KPM_GRID=1024 && \
-run kg768s1024 "NGSEP_KPM_GRID=768 NGSEP_STA_GRID=1024" && run kg768s2048 "NGSEP_KPM_GRID=768 NGSEP_STA_GRID=2048" && run kg5122 NGSEP_KPM_GRID=512 && run kg7682 NGSEP_KPM_GRID=768
+timeout -k 10 300 python -u bench.py --config multisample --no-cpu-baseline --no-cold --no-e2e --steps 20 --warmup 4 > gpurun_out/${TAG}_ms.json 2> gpurun_out/${TAG}_ms.err || { tail -20 gpurun_out/${TAG}_ms.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_ms -o run --output-format csv -- python -u bench.py --config multisample --no-cpu-baseline --no-cold --no-e2e --steps 20 --warmup 4 \
+    > gpurun_out/prof_${TAG}_ms.out 2>&1 || { tail -5 gpurun_out/prof_${TAG}_ms.out; exit 1; }
+python tools/kstats.py gpurun_out/prof_${TAG}_ms gpurun_out/${TAG}_ms_kernel_stats.csv > gpurun_out/${TAG}_ms_kstats.txt && head -8 gpurun_out/${TAG}_ms_kstats.txt
