@@ -1497,8 +1497,10 @@ static inline uint8_t ref_code(const ngsep_ctx* c, char ch) {
 static void fill_ref_codes(const ngsep_ctx* c, Staged& s, const Window& w, const std::vector<std::pair<int64_t, int64_t>>& carved) {
     const std::string& ref = c->seq_bases[w.seq_id];
     uint8_t* dst = &s.h_ref[(size_t)(w.gbase + w.pad)];
-    parallel_for(w.wlen, 1 << 20, [&](int64_t lo, int64_t hi) {
-        for (int64_t k = lo; k < hi; k++) dst[k] = ref_code(c, ref[(size_t)(w.w0 - 1 + k)]);
+    uint8_t tab[256];
+    for (int ch = 0; ch < 256; ch++) tab[ch] = ref_code(c, (char)ch);
+    parallel_for(w.wlen, 1 << 18, [&](int64_t lo, int64_t hi) {
+        for (int64_t k = lo; k < hi; k++) dst[k] = tab[(uint8_t)ref[(size_t)(w.w0 - 1 + k)]];
     });
     for (const auto& cv : carved) {
         const int64_t a = std::max<int64_t>(cv.first, w.w0), b = std::min<int64_t>(cv.second, (int64_t)w.w0 + w.wlen - 1);
@@ -1724,8 +1726,11 @@ static inline void fill_group_units(uint64_t* dst, int32_t K, const uint8_t* con
 // position.  Groups are independent: built on all host threads.
 // consumed (a staged whole-genome run): called after every slice of groups with the reads whose bytes are in place, so
 // the caller can return their projected chunks while the rest is filled (peak host memory ~ one copy, not two)
+// device_units (streamed windows): the units are built on the device (kernels.hip k_build_units) from the reads'
+// projected bytes, copied here back to back into the arena (runs of reads adjacent in their projection chunk: one copy)
+// -- a copy instead of the 64-lane transposition with its reference XOR, which cost the window worker ~10 ms a window
 static int build_rg_layout(Staged& s, const HugeVec<SRead>& reads, LayoutArena& arena, bool exact,
-                           const std::function<void(int64_t)>& consumed = nullptr) {
+                           const std::function<void(int64_t)>& consumed = nullptr, bool device_units = false) {
     static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     const auto t0 = std::chrono::steady_clock::now();
     const int64_t n = (int64_t)reads.size();
@@ -1749,10 +1754,48 @@ static int build_rg_layout(Staged& s, const HugeVec<SRead>& reads, LayoutArena& 
         base += (int64_t)K * 64;
     }
     s.n_units = base;
+    const int32_t last_first = n ? reads[(size_t)n - 1].gfirst : 1;
+    if (device_units) {
+        auto span_of = [&](int64_t e) { return std::max<int64_t>(0, (int64_t)reads[(size_t)e].glast - reads[(size_t)e].gfirst + 1); };
+        s.units_on_device = true;
+        s.h_roff.resize((size_t)ne + 1);
+        int64_t tot = 0;
+        for (int64_t e = 0; e < ne; e++) {
+            s.h_roff[(size_t)e] = tot;
+            if (e < n) tot += span_of(e);
+        }
+        s.h_roff[(size_t)ne] = tot;
+        s.n_rbytes = tot;
+        if (!arena.ensure_units(tot / 8 + 2, exact)) return -2;
+        s.h_units = arena.units;
+        s.units_pinned = arena.units_pinned;
+        uint8_t* dst = reinterpret_cast<uint8_t*>(arena.units);
+        parallel_for(ne, 4096, [&](int64_t lo, int64_t hi) {
+            for (int64_t e = lo; e < hi; e++) {
+                if (e >= n) {                              // padding entry: empty
+                    s.h_rh[(size_t)(2 * e)] = last_first;
+                    s.h_rh[(size_t)(2 * e + 1)] = last_first - 1;
+                    continue;
+                }
+                const SRead& rd = reads[(size_t)e];
+                const int64_t span = span_of(e);
+                s.h_rh[(size_t)(2 * e)] = rd.gfirst;
+                s.h_rh[(size_t)(2 * e + 1)] = (int32_t)((uint32_t)(span > 0 ? rd.glast : rd.gfirst - 1) | (rd.neg ? 0x80000000u : 0u));
+            }
+            const int64_t top = std::min(hi, n);
+            for (int64_t e = lo; e < top;) {
+                const uint8_t* p = reads[(size_t)e].bytes;
+                int64_t len = span_of(e), f = e + 1;
+                while (f < top && (span_of(f) == 0 || reads[(size_t)f].bytes == p + len)) len += span_of(f++);
+                if (len) std::memcpy(dst + s.h_roff[(size_t)e], p, (size_t)len);
+                e = f;
+            }
+        });
+        if (consumed) consumed(n);
+    } else {
     if (!arena.ensure_units(base + 8, exact)) return -2;       // + 8: slack past the last unit
     s.h_units = arena.units;
     s.units_pinned = arena.units_pinned;
-    const int32_t last_first = n ? reads[(size_t)n - 1].gfirst : 1;
     uint64_t* units = s.h_units;
     const int64_t slice = consumed ? (int64_t)1 << 15 : std::max<int64_t>(ng, 1);   // groups filled between two releases
     for (int64_t sa = 0; sa < ng; sa += slice) {
@@ -1788,6 +1831,7 @@ static int build_rg_layout(Staged& s, const HugeVec<SRead>& reads, LayoutArena& 
         _mm_sfence();
     });
     if (consumed) consumed(std::min(n, sb * 64));
+    }
     }
     // block tables over the global coordinate (reads are sorted by gfirst)
     const int64_t nb = (s.g_len >> kRgBlockShift) + 2;
@@ -1874,11 +1918,11 @@ static int build_pop_rg_layout(Staged& s, LayoutArena& arena) {
     const int64_t n = s.n_reads;
     const int S = s.n_samples;
     const int32_t* R = s.h_reads.data();
-    const uint8_t* const* rptr = s.h_rptr.data();      // each read's projected bytes over [gfirst, glast]
+    const int64_t* rptr = s.h_rdev.data();            // each read's projected bytes: their offset in the uploaded chunks
     const uint8_t* ref = s.h_ref.data();
     // stream keys: sample * 128 + read-group rank; the reads of no sample: S * 128
     const int64_t nkeys = (int64_t)(S + 1) * 128;
-    std::vector<uint16_t> key((size_t)n);
+    RawVec<uint16_t> key((size_t)n);
     parallel_for(n, 1 << 16, [&](int64_t a, int64_t b) {
         for (int64_t r = a; r < b; r++) {
             const int sm = (R[r * 4 + 3] >> 8) - 1;
@@ -1906,14 +1950,14 @@ static int build_pop_rg_layout(Staged& s, LayoutArena& arena) {
                 kcount[(size_t)k] += v;
             }
     }
-    std::vector<int32_t> ord((size_t)n);
+    RawVec<int32_t> ord((size_t)n);
     parallel_for(nch, 1, [&](int64_t a, int64_t b) {
         for (int64_t c = a; c < b; c++) {
             int64_t* h = &hist[(size_t)(c * nkeys)];
             for (int64_t r = c * chl; r < std::min(n, (c + 1) * chl); r++) ord[(size_t)h[key[(size_t)r]]++] = (int32_t)r;
         }
     });
-    std::vector<uint16_t>().swap(key);
+    decltype(key)().swap(key);
     std::vector<int64_t>().swap(hist);
     // streams (non-empty keys in key order), their entries padded to whole groups
     std::vector<int64_t> st_r0, st_n, st_e0;          // first read (in ord), reads, first entry
@@ -1938,7 +1982,7 @@ static int build_pop_rg_layout(Staged& s, LayoutArena& arena) {
     s.h_st_end.resize((size_t)nst);
     for (int64_t st = 0; st < nst; st++) s.h_st_end[(size_t)st] = st_e0[(size_t)st] + (st_n[(size_t)st] + 63) / 64 * 64;
     // entry -> read (-1: padding) and the entry headers
-    std::vector<int32_t> ent((size_t)ne, -1);
+    RawVec<int32_t> ent((size_t)ne);                    // (every entry written below: -1 for padding)
     s.h_rh.resize((size_t)ne * 2);
     parallel_for(nst, 1, [&](int64_t a, int64_t b) {
         for (int64_t st = a; st < b; st++) {
@@ -1947,6 +1991,7 @@ static int build_pop_rg_layout(Staged& s, LayoutArena& arena) {
             for (int64_t i = 0; i < (m + 63) / 64 * 64; i++) {
                 const int64_t e = eb + i;
                 if (i >= m) {
+                    ent[(size_t)e] = -1;
                     s.h_rh[(size_t)(2 * e)] = last_first;
                     s.h_rh[(size_t)(2 * e + 1)] = last_first - 1;
                     continue;
@@ -1961,43 +2006,48 @@ static int build_pop_rg_layout(Staged& s, LayoutArena& arena) {
         }
     });
     lap("streams");
-    // groups: units per read, unit offsets
+    // groups: units per read (on all threads: the entries' reads are scattered over R), then the unit offsets
     s.h_grp.resize((size_t)ng);
+    parallel_for(ng, 1 << 12, [&](int64_t g0, int64_t g1) {
+        for (int64_t g = g0; g < g1; g++) {
+            int32_t K = 0;
+            for (int64_t e = g * 64; e < g * 64 + 64; e++) {
+                const int32_t r = ent[(size_t)e];
+                if (r < 0) continue;
+                const int64_t span = (int64_t)R[(int64_t)r * 4 + 1] - R[(int64_t)r * 4] + 1;
+                if (span > 0) K = std::max<int32_t>(K, (int32_t)((span + 7) / 8));
+            }
+            s.h_grp[(size_t)g] = RGroup{0, K, 0};
+        }
+    });
     int64_t base = 0;
     for (int64_t g = 0; g < ng; g++) {
-        int32_t K = 0;
-        for (int64_t e = g * 64; e < g * 64 + 64; e++) {
-            const int32_t r = ent[(size_t)e];
-            if (r < 0) continue;
-            const int64_t span = (int64_t)R[(int64_t)r * 4 + 1] - R[(int64_t)r * 4] + 1;
-            if (span > 0) K = std::max<int32_t>(K, (int32_t)((span + 7) / 8));
-        }
-        s.h_grp[(size_t)g] = RGroup{base, K, 0};
-        base += (int64_t)K * 64;
+        s.h_grp[(size_t)g].base = base;
+        base += (int64_t)s.h_grp[(size_t)g].K * 64;
     }
     s.n_units = base;
-    if (!arena.ensure_units(base + 8, true)) return -2;
-    s.h_units = arena.units;
-    s.units_pinned = arena.units_pinned;
-    uint64_t* units = s.h_units;
-    parallel_for(ng, 64, [&](int64_t g0, int64_t g1) {
-        const uint8_t* src[64];
-        const uint8_t* rfs[64];
-        int64_t spans[64];
-        for (int64_t g = g0; g < g1; g++) {
-            const RGroup G = s.h_grp[(size_t)g];
-            for (int l = 0; l < 64; l++) {
-                const int32_t r = ent[(size_t)(g * 64 + l)];
-                const int64_t gf = r < 0 ? 0 : R[(int64_t)r * 4];
-                spans[l] = r < 0 ? 0 : std::max<int64_t>(0, (int64_t)R[(int64_t)r * 4 + 1] - gf + 1);
-                src[l] = r < 0 ? nullptr : rptr[r];
-                rfs[l] = ref + gf;
+    // the units are built on the device (kernels.hip k_build_units) from the projection chunks themselves, uploaded as
+    // they are (s.h_chunks, one after the other in d_rbytes): every entry gets its read's offset there (h_rdev) -- no
+    // host copy (round 4's host transposition of the same bytes: 0.7-0.95 s of the chrIV 200-sample end-to-end run)
+    {
+        int64_t tot = 0;
+        for (const auto& ch : s.h_chunks) tot += ch.second;
+        s.units_on_device = true;
+        s.n_rbytes = tot;
+        s.h_units = nullptr;
+        s.h_roff.resize((size_t)ne + 1);
+        parallel_for(ne, 1 << 16, [&](int64_t a, int64_t b) {
+            for (int64_t e = a; e < b; e++) {
+                const int32_t r = ent[(size_t)e];
+                s.h_roff[(size_t)e] = r < 0 ? 0 : s.h_rdev[(size_t)r];
             }
-            fill_group_units(units + G.base, G.K, src, rfs, spans);
-        }
-        _mm_sfence();
-    });
-    lap("units");
+        });
+        s.h_roff[(size_t)ne] = 0;
+        (void)ref;
+        (void)arena;
+        (void)rptr;
+    }
+    lap("read bytes");
     // block tables per stream, blocks of 2^pblk_shift positions (coarser when the tables would outgrow a quarter of
     // the units; at most a KLM tile)
     int32_t shift = 6;                                 // (KPM's gather walks ~ (64 + max span) x depth / span entries)
@@ -2163,10 +2213,23 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs, bool relea
         c->stats.slot_size = 0;
     } else {
         // the reads in pending order with their projected bytes in place (no copy): the population layout reads
-        // them through h_rptr
+        // them through h_rdev, their offsets in the projection chunks as uploaded
         s.slot_size = 0;
         s.h_reads.resize((size_t)nreads * 4);
-        s.h_rptr.resize((size_t)nreads);
+        s.h_rdev.resize((size_t)nreads);
+        // the projection chunks the reads' bytes lie in, uploaded one after the other (kernels.hip device_upload): a
+        // read's bytes are at h_rdev = its chunk's offset there + its offset in the chunk (ContigReads::chunk_end)
+        s.h_chunks.clear();
+        std::vector<std::vector<int64_t>> cdev(contigs.size());
+        {
+            int64_t at = 0;
+            for (size_t ci = 0; ci < contigs.size(); ci++)
+                for (const HostArray<uint8_t>& ch : contigs[ci].chunks) {
+                    cdev[ci].push_back(at);
+                    s.h_chunks.push_back({ch.p, (int64_t)ch.n});
+                    at += (int64_t)ch.n;
+                }
+        }
         std::vector<int64_t> wbase(s.windows.size() + 1, 0);
         for (size_t wi = 0; wi < s.windows.size(); wi++) wbase[wi + 1] = wbase[wi] + (ranges[wi].second - ranges[wi].first);
         for (size_t wi = 0; wi < s.windows.size(); wi++) {
@@ -2177,10 +2240,13 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs, bool relea
             const int64_t goff = w.gbase + w.pad - w.w0;   // G = pos + goff
             const int64_t i0 = ranges[wi].first;
             std::atomic<int64_t> nb{0};
+            const std::vector<int64_t>& cd = cdev[wr[wi].contig];
             parallel_for(ranges[wi].second - i0, 1 << 14, [&](int64_t lo, int64_t hi) {
                 int64_t local = 0;
+                size_t ck = (size_t)(std::upper_bound(cr.chunk_end.begin(), cr.chunk_end.end(), (size_t)(i0 + lo)) - cr.chunk_end.begin());
                 for (int64_t k = lo; k < hi; k++) {
                     const int64_t i = i0 + k, ri = wbase[wi] + k;
+                    while (ck < cr.chunk_end.size() && cr.chunk_end[ck] <= (size_t)i) ck++;
                     const int64_t span = (int64_t)cr.last[i] - cr.first[i] + 1;
                     s.h_reads[ri * 4 + 0] = (int32_t)(cr.first[i] + goff);
                     s.h_reads[ri * 4 + 1] = (int32_t)(cr.last[i] + goff);
@@ -2188,7 +2254,7 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs, bool relea
                     int32_t fl = cr.neg[i];
                     if (!cr.sample.empty()) fl |= ((int32_t)cr.rank[i] << 1) | (((int32_t)cr.sample[i] + 1) << 8);
                     s.h_reads[ri * 4 + 3] = fl;
-                    s.h_rptr[(size_t)ri] = cr.bptr[i];
+                    s.h_rdev[(size_t)ri] = ck < cd.size() && span > 0 ? cd[ck] + (cr.bptr[i] - cr.chunks[ck].p) : 0;
                     local += span > 0 ? span : 0;
                 }
                 nb += local;
@@ -2259,14 +2325,14 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs, bool relea
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h1).count(),
                      (long long)nreads, (long long)s.n_tiles);
     // host mirrors are not needed any more
-    std::vector<const uint8_t*>().swap(s.h_rptr);
-    std::vector<int32_t>().swap(s.h_reads);
+    decltype(s.h_rdev)().swap(s.h_rdev);
+    decltype(s.h_reads)().swap(s.h_reads);
     std::vector<uint8_t>().swap(s.h_ref);
     std::vector<uint8_t>().swap(s.h_pile);
     std::vector<TileInfo>().swap(s.h_tinfo);
     std::vector<uint16_t>().swap(s.h_olist);
     std::vector<int32_t>().swap(s.h_loff);
-    std::vector<int32_t>().swap(s.h_rh);
+    decltype(s.h_rh)().swap(s.h_rh);
     std::vector<RGroup>().swap(s.h_grp);
     std::vector<int32_t>().swap(s.h_blkA);
     std::vector<int32_t>().swap(s.h_blkB);
@@ -2307,8 +2373,23 @@ static void run_window_job(ngsep_ctx* c, WindowJob* j) {
     s.max_span = j->max_span;
     s.g_len = (((int64_t)w.wlen + 2 * pad + 64 + kRunAlign - 1) / kRunAlign) * kRunAlign;
     s.covered = w.wlen;                 // (the dump mode's record capacity)
-    s.h_ref.assign((size_t)s.g_len, 0);
-    fill_ref_codes(c, s, w, j->carved);
+    if (c->params.relative_allele_counts) {
+        s.h_ref.assign((size_t)s.g_len, 0);
+        fill_ref_codes(c, s, w, j->carved);
+    } else {
+        // the reference codes are made on the device from the window's characters (kernels.hip k_ref_codes): the host
+        // layout no longer reads them (its units are built there too)
+        s.ref_on_device = true;
+        s.h_refchars = c->seq_bases[(size_t)w.seq_id].data() + (w.w0 - 1);
+        s.ref_lo = w.gbase + w.pad;
+        s.ref_len = w.wlen;
+        for (int ch = 0; ch < 256; ch++) s.ref_table[ch] = ref_code(c, (char)ch);
+        s.h_zero.clear();
+        for (const auto& cv : j->carved) {            // carved indel regions get no code (no call is made there)
+            const int64_t a = std::max<int64_t>(cv.first, w.w0), b = std::min<int64_t>(cv.second, (int64_t)w.w0 + w.wlen - 1);
+            if (a <= b) { s.h_zero.push_back(s.ref_lo + (a - w.w0)); s.h_zero.push_back(b - a + 1); }
+        }
+    }
     s.single = true;
     s.known = !c->known.empty();
     if (s.known) {
@@ -2320,7 +2401,7 @@ static void run_window_job(ngsep_ctx* c, WindowJob* j) {
     for (const SRead& r : j->reads) nb += r.glast >= r.gfirst ? (int64_t)r.glast - r.gfirst + 1 : 0;
     s.n_read_bases = nb;
     const int lr = c->params.relative_allele_counts ? build_single_layout(s, j->reads, c->arena, false)
-                                                    : build_rg_layout(s, j->reads, c->arena, false);
+                                                    : build_rg_layout(s, j->reads, c->arena, false, nullptr, true);
     if (lr != 0) {
         j->rc = lr == -2 ? NGSEP_E_DEVICE : NGSEP_E_INVALID;
         j->err = lr == -2 ? "pinned host memory for the layout could not be allocated" : "internal error: pileup depth above the tile's row count";

@@ -204,6 +204,26 @@ struct HugeAllocator {
     template <class U> bool operator!=(const HugeAllocator<U>&) const { return false; }
 };
 template <class T> using HugeVec = std::vector<T, HugeAllocator<T>>;
+// huge_alloc's pages with the elements a resize adds left uninitialised: for arrays whose every element the caller
+// writes itself, on all threads (the serial zero fill of a value-initialising resize was ~0.3 s of the 200-sample
+// population layout's 1.2 GB of index arrays)
+template <class T>
+struct RawAllocator {
+    using value_type = T;
+    RawAllocator() = default;
+    template <class U> RawAllocator(const RawAllocator<U>&) {}
+    T* allocate(size_t n) {
+        void* p = huge_alloc(n * sizeof(T));
+        if (!p) throw std::bad_alloc();
+        return static_cast<T*>(p);
+    }
+    void deallocate(T* p, size_t) { std::free(p); }
+    template <class U> void construct(U* p) noexcept { ::new ((void*)p) U; }
+    template <class U, class... A> void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+    template <class U> bool operator==(const RawAllocator<U>&) const { return true; }
+    template <class U> bool operator!=(const RawAllocator<U>&) const { return false; }
+};
+template <class T> using RawVec = std::vector<T, RawAllocator<T>>;
 
 // Admitted reads of one sequence in pending order (AlignmentsPileupGenerator.pendingAlignments)
 struct ContigReads {
@@ -569,10 +589,10 @@ struct Staged {            // everything resident for one run
     int64_t n_tiles = 0;
     int64_t pile_bytes = 0;
     // host mirrors (freed after upload)
-    std::vector<const uint8_t*> h_rptr;  // multisample: each read's projected bytes (the sequence's chunks, in place)
+    RawVec<int64_t> h_rdev;             // multisample: each read's bytes in the uploaded projection chunks (h_chunks): each read's projected bytes (the sequence's chunks, in place)
     std::vector<uint8_t> h_pile;
     std::vector<TileInfo> h_tinfo;
-    std::vector<int32_t> h_reads;       // 4 ints per read: gfirst, glast, slot, flags
+    RawVec<int32_t> h_reads;            // 4 ints per read: gfirst, glast, slot, flags
                                         //   flags: bit0 negative strand, bits 1-7 read-group rank,
                                         //   bits 8-23 sample + 1 (0: no sample) -- multisample only
     int32_t n_samples = 0;
@@ -602,7 +622,21 @@ struct Staged {            // everything resident for one run
     int64_t n_entries = 0, n_groups = 0, n_units = 0;
     uint64_t* h_units = nullptr;
     bool units_pinned = true;           // h_units is the arena's pinned block (false: pageable, copied synchronously)
-    std::vector<int32_t> h_rh;          // 2 per entry
+    // units built on the device (kernels.hip k_build_units): h_units then holds the reads' projected bytes back to
+    // back (n_rbytes), entry e's from h_roff[e] (padding entries: the total)
+    bool units_on_device = false;
+    int64_t n_rbytes = 0;
+    RawVec<int64_t> h_roff;
+    // reference codes made on the device (streamed windows, kernels.hip k_ref_codes): global [ref_lo, ref_lo + ref_len)
+    // from the characters at h_refchars through ref_table (engine.cpp ref_code), 0 elsewhere and on the h_zero ranges
+    // (global start, length pairs)
+    std::vector<std::pair<const uint8_t*, int64_t>> h_chunks;   // population: the projection chunks d_rbytes is made of
+    bool ref_on_device = false;
+    const char* h_refchars = nullptr;
+    int64_t ref_lo = 0, ref_len = 0;
+    uint8_t ref_table[256] = {};
+    std::vector<int64_t> h_zero;
+    RawVec<int32_t> h_rh;               // 2 per entry (every one written by the layout builders)
     std::vector<RGroup> h_grp;
     std::vector<int32_t> h_blkA, h_blkB;
     // -knownVariants: the run genotypes these sites (KP queue entries {global position, code}: code =

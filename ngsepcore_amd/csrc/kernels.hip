@@ -170,6 +170,12 @@ struct Device {
     int32_t* d_blkA = nullptr;
     int32_t* d_blkB = nullptr;
     size_t cap_units = 0, cap_rh = 0, cap_grp = 0, cap_blk = 0, cap_blkB = 0;
+    uint8_t* d_rbytes = nullptr;     // k_build_units' input: the reads' projected bytes back to back, and entry offsets
+    int64_t* d_roff = nullptr;
+    size_t cap_rbytes = 0, cap_roff = 0;
+    char* d_refchars = nullptr;      // k_ref_codes' input: a window's reference characters, and the carved ranges
+    int64_t* d_zero = nullptr;
+    size_t cap_refchars = 0, cap_zero = 0;
     int64_t n_entries = 0;
     bool rg = false;
     // multisample: the population read-group layout (the units / headers / groups above, engine.hpp Staged::prg)
@@ -889,6 +895,10 @@ constexpr int kKlThreads = 256;
 #define NGSEP_KL_GPRE 1     // the next group's unit offset fetched with its headers (0: A/B builds)
 #endif
 constexpr int kKlUnroll = NGSEP_KL_UNROLL;
+// units allocated past a layout's last group: KL's and KLM's next-batch loads are unconditional and may read up to
+// 2 x 4 - 1 rows past a read's last unit, the last group's included (never used, only loaded)
+constexpr int64_t kUnitSlack = 8 + 64 * 8;
+static_assert(NGSEP_KL_UNROLL <= 4, "kUnitSlack covers batches of at most 4 units");
 
 // PileupRecord.getAlleleCalls(1) at global position p over the read-group layout: the nonzero codes of the reads
 // covering p, in pending-list (entry) order, as u16 entries code | negative strand << 8 (WRITE), one wave.  e0 is
@@ -986,15 +996,17 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
         // batch's slots past the read's last unit repeat it) so that each unit waits for its own load only
 #define KL_LOAD(q) (q)                                    // (nontemporal loads measured no change)
 #if NGSEP_KL_PIPE
+        // (the next batch's loads unconditional, past the read's end too -- other reads' rows or the buffer's slack,
+        // never used: a load under a lane condition made the compiler wait for every outstanding load, the next
+        // batch's included, before the current batch)
         uint64_t u[U];
 #pragma unroll
-        for (int i = 0; i < U; i++) u[i] = kn >= 0 ? KL_LOAD(ub[(int64_t)min(i, kn) * 64]) : 0ull;
+        for (int i = 0; i < U; i++) u[i] = KL_LOAD(ub[(int64_t)i * 64]);
         for (int32_t j = 0; j <= kn; j += U) {
             uint64_t v[U];
-            if (j + U <= kn) {
+            const uint64_t* nb = ub + (int64_t)(j + U) * 64;
 #pragma unroll
-                for (int i = 0; i < U; i++) v[i] = KL_LOAD(ub[(int64_t)min(j + U + i, kn) * 64]);
-            }
+            for (int i = 0; i < U; i++) v[i] = KL_LOAD(nb[(int64_t)i * 64]);
 #else
         for (int32_t j = 0; j <= kn; j += U) {
             uint64_t u[U];
@@ -1557,15 +1569,17 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
                 atomicAdd(&dif32[i0 >> 2], 1u << (8 * (i0 & 3)));
                 atomicAdd(&dif32[i1 >> 2], 0u - (1u << (8 * (i1 & 3))));
             }
+            // (every batch's loads are issued unconditionally -- the units past a read's end are other reads' rows, or
+            // the buffer's slack past the last group, and are never used: a load under a lane condition made the
+            // compiler wait for every outstanding load, the next batch's included, before the current batch)
             uint64_t u[kKlmUnroll];
 #pragma unroll
-            for (int i = 0; i < kKlmUnroll; i++) u[i] = kn >= 0 ? ub[(int64_t)min(i, kn) * 64] : 0ull;
+            for (int i = 0; i < kKlmUnroll; i++) u[i] = ub[(int64_t)i * 64];
             for (int32_t j = 0; j <= kn; j += kKlmUnroll) {
                 uint64_t v[kKlmUnroll];
-                if (j + kKlmUnroll <= kn) {
+                const uint64_t* nb = ub + (int64_t)(j + kKlmUnroll) * 64;
 #pragma unroll
-                    for (int i = 0; i < kKlmUnroll; i++) v[i] = ub[(int64_t)min(j + kKlmUnroll + i, kn) * 64];
-                }
+                for (int i = 0; i < kKlmUnroll; i++) v[i] = nb[(int64_t)i * 64];
 #pragma unroll
                 for (int i = 0; i < kKlmUnroll; i++) {
                     if (j + i > kn) continue;
@@ -2928,6 +2942,12 @@ void device_release(Device* d) {
     (void)hipFree(d->d_ref); d->d_ref = nullptr;
     (void)hipFree(d->d_tinfo); d->d_tinfo = nullptr;
     (void)hipFree(d->d_units); d->d_units = nullptr;
+    (void)hipFree(d->d_rbytes); d->d_rbytes = nullptr;
+    (void)hipFree(d->d_roff); d->d_roff = nullptr;
+    d->cap_rbytes = d->cap_roff = 0;
+    (void)hipFree(d->d_refchars); d->d_refchars = nullptr;
+    (void)hipFree(d->d_zero); d->d_zero = nullptr;
+    d->cap_refchars = d->cap_zero = 0;
     (void)hipFree(d->d_rh); d->d_rh = nullptr;
     (void)hipFree(d->d_grp); d->d_grp = nullptr;
     (void)hipFree(d->d_blkA); d->d_blkA = nullptr;
@@ -3023,6 +3043,69 @@ void device_destroy(Device* d) {
     delete d;
 }
 
+// A streamed window's reference codes on the device (engine.cpp run_window_job): global position i in [lo, lo + len)
+// gets t[the window's character i - lo] (engine.cpp ref_code as a 256-entry table), every other position 0 -- the
+// host's fill_ref_codes; k_zero_ranges then clears the carved indel regions (one workgroup per {start, length} pair)
+struct RefTable {
+    uint8_t t[256];
+};
+__global__ __launch_bounds__(256) void k_ref_codes(const uint8_t* __restrict__ chars, int64_t lo, int64_t len, int64_t g_len,
+                                                   const RefTable t, uint8_t* __restrict__ ref) {
+    __shared__ uint8_t s_t[256];
+    s_t[threadIdx.x] = t.t[threadIdx.x];
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < g_len; i += (int64_t)gridDim.x * blockDim.x)
+        ref[i] = (i >= lo && i < lo + len) ? s_t[chars[i - lo]] : (uint8_t)0;
+}
+__global__ __launch_bounds__(256) void k_zero_ranges(const int64_t* __restrict__ ranges, uint8_t* __restrict__ ref) {
+    const int64_t a = ranges[2 * blockIdx.x], n = ranges[2 * blockIdx.x + 1];
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) ref[a + i] = 0;
+}
+
+// The read-group layout's units built on the device (streamed windows: engine.cpp build_rg_layout device_units) --
+// one wavefront per 64-read group, lane = entry: unit k of the lane's read = its projected bytes 8k .. 8k+7 XOR-ed
+// with the reference codes of the same positions, zero past the read's end (the host's fill_group_units, byte for
+// byte).  Each lane walks its read and the reference with aligned 8-byte loads, the unaligned unit funnel-shifted
+// from two of them (every load lies inside the read's bytes + 15 and the reference + 15: both buffers carry 64 bytes
+// of slack); the stores of one k are one 512-byte line run per wave.
+__global__ __launch_bounds__(256) void k_build_units(const uint8_t* __restrict__ rb, const int64_t* __restrict__ roff,
+                                                     const int2* __restrict__ rh, const RGroup* __restrict__ grp,
+                                                     const uint8_t* __restrict__ ref, int64_t n_groups,
+                                                     uint64_t* __restrict__ units) {
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= n_groups) return;
+    const RGroup G = grp[g];
+    const int64_t e = g * 64 + lane;
+    const int2 h = rh[e];
+    const int32_t gf = h.x, gl = h.y & 0x7FFFFFFF;
+    const int64_t span = gl >= gf ? (int64_t)gl - gf + 1 : 0;
+    uint64_t* out = units + G.base + lane;
+    if (span == 0) {
+        for (int32_t k = 0; k < G.K; k++) out[(int64_t)k * 64] = 0ull;
+        return;
+    }
+    const uintptr_t sa = (uintptr_t)(rb + roff[e]), ra = (uintptr_t)(ref + gf);
+    const uint64_t* sp = reinterpret_cast<const uint64_t*>(sa & ~(uintptr_t)7);
+    const uint64_t* rp = reinterpret_cast<const uint64_t*>(ra & ~(uintptr_t)7);
+    const uint32_t ss = 8u * (uint32_t)(sa & 7), rs = 8u * (uint32_t)(ra & 7);
+    uint64_t s0 = sp[0], r0 = rp[0];
+    for (int32_t k = 0; k < G.K; k++) {
+        const int64_t o = 8 * (int64_t)k;
+        uint64_t v = 0ull;
+        if (o < span) {
+            const uint64_t s1 = sp[k + 1], r1 = rp[k + 1];
+            const uint64_t su = ss ? (s0 >> ss) | (s1 << (64u - ss)) : s0;
+            const uint64_t ru = rs ? (r0 >> rs) | (r1 << (64u - rs)) : r0;
+            v = su ^ ru;
+            if (span - o < 8) v &= (1ull << (8 * (span - o))) - 1ull;
+            s0 = s1;
+            r0 = r1;
+        }
+        out[(int64_t)k * 64] = v;
+    }
+}
+
 int device_upload(Device* d, const Staged& s, std::string& err) {
     HIP_TRY(hipSetDevice(d->ordinal));
     const int32_t pad = s.windows.empty() ? 64 : s.windows[0].pad;
@@ -3038,23 +3121,51 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
     else HIP_TRY(hipDeviceSynchronize());          // the previous run is done reading them
     if (ensure_dev(&d->d_ref, &d->cap_ref, (size_t)s.g_len + 64, keep, err)) return -1;
     HIP_TRY(hipMemsetAsync(d->d_ref + s.g_len, 0, 64, d->stream));
-    H2D(d->d_ref, s.h_ref.data(), (size_t)s.g_len, d->stream);
+    if (s.ref_on_device) {
+        if (ensure_dev(&d->d_refchars, &d->cap_refchars, (size_t)std::max<int64_t>(s.ref_len, 1), keep, err)) return -1;
+        if (s.ref_len) H2D(d->d_refchars, s.h_refchars, (size_t)s.ref_len, d->stream);
+        RefTable t;
+        std::memcpy(t.t, s.ref_table, 256);
+        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((s.g_len + 255) / 256, (int64_t)d->n_cu * 16));
+        hipLaunchKernelGGL(k_ref_codes, dim3((unsigned)blocks), dim3(256), 0, d->stream, (const uint8_t*)d->d_refchars,
+                           s.ref_lo, s.ref_len, s.g_len, t, d->d_ref);
+        HIP_TRY(launch_check());
+        const int64_t nz = (int64_t)s.h_zero.size() / 2;
+        if (nz) {
+            if (ensure_dev(&d->d_zero, &d->cap_zero, s.h_zero.size() * sizeof(int64_t), keep, err)) return -1;
+            H2D(d->d_zero, s.h_zero.data(), s.h_zero.size() * sizeof(int64_t), d->stream);
+            hipLaunchKernelGGL(k_zero_ranges, dim3((unsigned)nz), dim3(256), 0, d->stream, (const int64_t*)d->d_zero, d->d_ref);
+            HIP_TRY(launch_check());
+        }
+    } else {
+        H2D(d->d_ref, s.h_ref.data(), (size_t)s.g_len, d->stream);
+    }
     d->rg = s.rg;
     if (s.rg) {
         // the read-group layout: units, entry headers, group table, block tables (KL, KG)
         const size_t nblk = (size_t)(s.g_len >> kRgBlockShift) + 2;
-        if (ensure_dev(&d->d_units, &d->cap_units, (size_t)(s.n_units + 8) * sizeof(uint64_t), keep, err) ||
+        if (ensure_dev(&d->d_units, &d->cap_units, (size_t)(s.n_units + kUnitSlack) * sizeof(uint64_t), keep, err) ||
             ensure_dev(&d->d_rh, &d->cap_rh, (size_t)std::max<int64_t>(s.n_entries, 64) * sizeof(int2), keep, err) ||
             ensure_dev(&d->d_grp, &d->cap_grp, (size_t)std::max<int64_t>(s.n_groups, 1) * sizeof(RGroup), keep, err) ||
             ensure_dev(&d->d_blkA, &d->cap_blk, nblk * sizeof(int32_t), keep, err) ||
             ensure_dev(&d->d_blkB, &d->cap_blkB, nblk * sizeof(int32_t), keep, err))
             return -1;
-        if (s.n_units) {
+        if (s.units_on_device) {
+            // the reads' bytes back to back and their entry offsets; k_build_units lays the units out below
+            if (ensure_dev(&d->d_rbytes, &d->cap_rbytes, (size_t)s.n_rbytes + 64, keep, err) ||
+                ensure_dev(&d->d_roff, &d->cap_roff, (size_t)(s.n_entries + 1) * sizeof(int64_t), keep, err))
+                return -1;
+            if (s.n_rbytes) {
+                if (pinned_covers(s.h_units, (size_t)s.n_rbytes)) DMA(d->d_rbytes, s.h_units, (size_t)s.n_rbytes, 0, d->stream);
+                else H2D(d->d_rbytes, s.h_units, (size_t)s.n_rbytes, d->stream);
+            }
+            H2D(d->d_roff, s.h_roff.data(), (size_t)(s.n_entries + 1) * sizeof(int64_t), d->stream);
+        } else if (s.n_units) {
             // a pinned arena is copied directly; a pageable one (a layout beyond 4 GB) through the staging buffers
             if (pinned_covers(s.h_units, (size_t)s.n_units * sizeof(uint64_t))) DMA(d->d_units, s.h_units, (size_t)s.n_units * sizeof(uint64_t), 0, d->stream);
             else H2D(d->d_units, s.h_units, (size_t)s.n_units * sizeof(uint64_t), d->stream);
         }
-        HIP_TRY(hipMemsetAsync(d->d_units + s.n_units, 0, 8 * sizeof(uint64_t), d->stream));
+        HIP_TRY(hipMemsetAsync(d->d_units + s.n_units, 0, kUnitSlack * sizeof(uint64_t), d->stream));
         if (s.n_entries) H2D(d->d_rh, s.h_rh.data(), (size_t)s.n_entries * sizeof(int2), d->stream);
         else {
             int32_t empty[128];
@@ -3062,6 +3173,16 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
             H2D(d->d_rh, empty, sizeof empty, d->stream);
         }
         if (s.n_groups) H2D(d->d_grp, s.h_grp.data(), (size_t)s.n_groups * sizeof(RGroup), d->stream);
+        if (s.units_on_device && s.n_groups) {
+            if (s.h_roff.size() != (size_t)s.n_entries + 1 || s.n_entries != s.n_groups * 64) {
+                err = "internal error: device unit build without its entry offsets";
+                return -1;
+            }
+            hipLaunchKernelGGL(k_build_units, dim3((unsigned)((s.n_groups + 3) / 4)), dim3(256), 0, d->stream,
+                               (const uint8_t*)d->d_rbytes, (const int64_t*)d->d_roff, (const int2*)d->d_rh,
+                               (const RGroup*)d->d_grp, (const uint8_t*)d->d_ref, s.n_groups, d->d_units);
+            HIP_TRY(launch_check());
+        }
         H2D(d->d_blkA, s.h_blkA.data(), nblk * sizeof(int32_t), d->stream);
         H2D(d->d_blkB, s.h_blkB.data(), nblk * sizeof(int32_t), d->stream);
         d->n_entries = std::max<int64_t>(s.n_entries, 64);
@@ -3095,20 +3216,48 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
         if (s.prg) {
             // multisample: the population read-group layout (KLM scans it, KPM gathers its columns)
             const size_t nblk = (size_t)(s.pnblk * s.n_streams);
-            HIP_TRY(hipMalloc(&d->d_units, (size_t)(s.n_units + 8) * sizeof(uint64_t)));
+            // (+ kUnitSlack: KLM's unconditional next-batch loads may run past the last group)
+            HIP_TRY(hipMalloc(&d->d_units, (size_t)(s.n_units + kUnitSlack) * sizeof(uint64_t)));
             HIP_TRY(hipMalloc(&d->d_rh, (size_t)std::max<int64_t>(s.n_entries, 64) * sizeof(int2)));
             HIP_TRY(hipMalloc(&d->d_grp, (size_t)std::max<int64_t>(s.n_groups, 1) * sizeof(RGroup)));
             HIP_TRY(hipMalloc(&d->d_blkA, std::max<size_t>(nblk, 1) * sizeof(int32_t)));
             HIP_TRY(hipMalloc(&d->d_blkB, std::max<size_t>(nblk, 1) * sizeof(int32_t)));
             HIP_TRY(hipMalloc(&d->d_samp_st, s.h_samp_st.size() * sizeof(int32_t)));
             HIP_TRY(hipMalloc(&d->d_st_end, std::max<size_t>(s.h_st_end.size(), 1) * sizeof(int64_t)));
-            if (s.n_units) {
+            if (s.units_on_device) {
+                // the reads' bytes and entry offsets; k_build_units lays the units out once the headers are there
+                if (s.h_roff.size() != (size_t)s.n_entries + 1 || s.n_entries != s.n_groups * 64) {
+                    err = "internal error: device unit build without its entry offsets";
+                    return -1;
+                }
+                HIP_TRY(hipMalloc(&d->d_rbytes, (size_t)s.n_rbytes + 64));
+                d->cap_rbytes = (size_t)s.n_rbytes + 64;
+                HIP_TRY(hipMalloc(&d->d_roff, (size_t)(s.n_entries + 1) * sizeof(int64_t)));
+                d->cap_roff = (size_t)(s.n_entries + 1) * sizeof(int64_t);
+                int64_t at = 0;                            // the projection chunks, one after the other
+                for (const auto& ch : s.h_chunks) {
+                    H2D(d->d_rbytes + at, ch.first, (size_t)ch.second, d->stream);
+                    at += ch.second;
+                }
+                H2D(d->d_roff, s.h_roff.data(), (size_t)(s.n_entries + 1) * sizeof(int64_t), d->stream);
+            } else if (s.n_units) {
                 if (pinned_covers(s.h_units, (size_t)s.n_units * sizeof(uint64_t))) DMA(d->d_units, s.h_units, (size_t)s.n_units * sizeof(uint64_t), 0, d->stream);
                 else H2D(d->d_units, s.h_units, (size_t)s.n_units * sizeof(uint64_t), d->stream);
             }
-            HIP_TRY(hipMemsetAsync(d->d_units + s.n_units, 0, 8 * sizeof(uint64_t), d->stream));
+            HIP_TRY(hipMemsetAsync(d->d_units + s.n_units, 0, kUnitSlack * sizeof(uint64_t), d->stream));
             if (s.n_entries) H2D(d->d_rh, s.h_rh.data(), (size_t)s.n_entries * sizeof(int2), d->stream);
             if (s.n_groups) H2D(d->d_grp, s.h_grp.data(), (size_t)s.n_groups * sizeof(RGroup), d->stream);
+            if (s.units_on_device && s.n_groups) {
+                hipLaunchKernelGGL(k_build_units, dim3((unsigned)((s.n_groups + 3) / 4)), dim3(256), 0, d->stream,
+                                   (const uint8_t*)d->d_rbytes, (const int64_t*)d->d_roff, (const int2*)d->d_rh,
+                                   (const RGroup*)d->d_grp, (const uint8_t*)d->d_ref, s.n_groups, d->d_units);
+                HIP_TRY(launch_check());
+                // (the bytes are not needed past the build: released once it is done)
+                HIP_TRY(hipStreamSynchronize(d->stream));
+                (void)hipFree(d->d_rbytes); d->d_rbytes = nullptr;
+                (void)hipFree(d->d_roff); d->d_roff = nullptr;
+                d->cap_rbytes = d->cap_roff = 0;
+            }
             if (nblk) {
                 H2D(d->d_blkA, s.h_blkA.data(), nblk * sizeof(int32_t), d->stream);
                 H2D(d->d_blkB, s.h_blkB.data(), nblk * sizeof(int32_t), d->stream);
