@@ -1475,6 +1475,9 @@ __global__ __launch_bounds__(256) void k_queue_need(const uint32_t* __restrict__
 // The reads of no sample only enter the pooled counts: not scanned.  No block barrier after the tables: every wave's
 // state is its own.
 constexpr int kKlmThreads = 256;
+// the population layout's padding past a read's last position (k_build_units): stored 0x1F = a reference call of quality
+// 31 relative to any reference code, which KLM's counters and marks ignore (no per-unit mask of the read's end)
+constexpr uint64_t kPopPadUnit = 0x1F1F1F1F1F1F1F1Full;
 constexpr int kKlmWords = kKlmTile / 32 + 2;   // tile bitmap words, a 32-position margin on either side
 constexpr int kKlmUnroll = 4;                  // pass 1: unit loads per batch, the next batch issued before the current
                                                // batch's marks (pipelined 4: 1.368-1.372 ms vs 8 unpipelined 1.393-1.395)
@@ -1486,6 +1489,12 @@ static_assert(kKlmSlots * (32 + 4 + 2) <= kKlmWaveLds, "KLM slots within the wav
 
 __device__ __forceinline__ uint32_t nib4_byte7(uint32_t w) {   // bit 7 of the four bytes -> 4 bits
     return ((w >> 7) & 1u) | ((w >> 14) & 2u) | ((w >> 21) & 4u) | ((w >> 28) & 8u);
+}
+// the same for a word holding nothing but those four bits (w & 0x80808080 == w), in five full-rate operations: bytes 0-2
+// gathered by one 24-bit multiply (bit 8k of w >> 7 times 2^(14 - 7k) lands on bit 14 + k, the cross terms on distinct
+// bits below 14 or above 16, so nothing carries into 14-16), byte 3 shifted down (KLM A/B: 1.005 -> 0.994 ms)
+__device__ __forceinline__ uint32_t nib4_of_b7(uint32_t w) {
+    return ((__umul24((w >> 7) & 0x010101u, 0x4081u) >> 14) & 7u) | ((w >> 28) & 8u);
 }
 // KLM's exceptions, bit 7 of byte k: not a valid call of the reference's allele (kl_exc), or one of quality < kKlmQs
 __device__ __forceinline__ uint32_t klm_exc(uint32_t y) {
@@ -1562,8 +1571,8 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
             const uint64_t* ub = units + gbase + (e & 63) + (int64_t)k0 * 64;
             const int32_t ti0 = gf + 8 * k0 - tstart + 32;   // bitmap index of unit k0's byte 0 (>= 25); COUNT: its
                                                               // counter byte is ti0 - 24 (>= 1)
-            // COUNT: the read's last unit holds padding past its last position (zero bytes: quality-0 reference calls)
-            const int32_t jlast = ((gl - gf) >> 3) - k0;
+            // (the read's last unit holds padding past its last position: 0x1F bytes in the population layout -- reference
+            // calls of quality 31, no exception, no mark -- so nothing is masked here; k_build_units)
             if (COUNT && act && !ABLATE(gp.ablate, 1048576)) {
                 const int32_t i0 = a - tstart, i1 = b - tstart + 1;
                 atomicAdd(&dif32[i0 >> 2], 1u << (8 * (i0 & 3)));
@@ -1587,10 +1596,6 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
                     if (ABLATE(gp.ablate, 524288)) { sink += ylo ^ yhi; continue; }   // (diagnostics: loads only)
                     if (COUNT) {
                         uint64_t ex = (uint64_t)klm_exc(ylo) | (uint64_t)klm_exc(yhi) << 32;
-                        if (j + i == jlast) {
-                            const int lb = (gl - gf) & 7;      // the read's last byte in this unit
-                            if (lb < 7) ex &= (1ull << (8 * lb + 8)) - 1ull;
-                        }
                         if (ABLATE(gp.ablate, 65536)) { sink += (uint32_t)ex; ex = 0; }   // (diagnostics: no counters)
                         if (ex) {
                             const uint64_t one = ex >> 7;          // a 0 / 1 byte per position
@@ -1606,7 +1611,7 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
                     const uint32_t nlo = kl_nonref(ylo), nhi = kl_nonref(yhi);
                     if (!(nlo | nhi)) continue;
                     if (ABLATE(gp.ablate, 131072)) { sink += nlo; continue; }     // (diagnostics: no marks)
-                    const uint32_t m = nib4_byte7(nlo) | nib4_byte7(nhi) << 4;
+                    const uint32_t m = nib4_of_b7(nlo) | nib4_of_b7(nhi) << 4;
                     const int32_t ti = ti0 + 8 * (j + i);
                     const uint64_t mv = (uint64_t)m << (ti & 31);
                     const uint32_t m0 = (uint32_t)mv, m1 = (uint32_t)(mv >> 32);
@@ -3071,7 +3076,7 @@ __global__ __launch_bounds__(256) void k_zero_ranges(const int64_t* __restrict__
 __global__ __launch_bounds__(256) void k_build_units(const uint8_t* __restrict__ rb, const int64_t* __restrict__ roff,
                                                      const int2* __restrict__ rh, const RGroup* __restrict__ grp,
                                                      const uint8_t* __restrict__ ref, int64_t n_groups,
-                                                     uint64_t* __restrict__ units) {
+                                                     uint64_t* __restrict__ units, uint64_t pad) {
     const int lane = threadIdx.x & 63;
     const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (g >= n_groups) return;
@@ -3098,7 +3103,10 @@ __global__ __launch_bounds__(256) void k_build_units(const uint8_t* __restrict__
             const uint64_t su = ss ? (s0 >> ss) | (s1 << (64u - ss)) : s0;
             const uint64_t ru = rs ? (r0 >> rs) | (r1 << (64u - rs)) : r0;
             v = su ^ ru;
-            if (span - o < 8) v &= (1ull << (8 * (span - o))) - 1ull;
+            if (span - o < 8) {                          // past the read's last position: the layout's padding bytes
+                const uint64_t m = (1ull << (8 * (span - o))) - 1ull;
+                v = (v & m) | (pad & ~m);
+            }
             s0 = s1;
             r0 = r1;
         }
@@ -3180,7 +3188,7 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
             }
             hipLaunchKernelGGL(k_build_units, dim3((unsigned)((s.n_groups + 3) / 4)), dim3(256), 0, d->stream,
                                (const uint8_t*)d->d_rbytes, (const int64_t*)d->d_roff, (const int2*)d->d_rh,
-                               (const RGroup*)d->d_grp, (const uint8_t*)d->d_ref, s.n_groups, d->d_units);
+                               (const RGroup*)d->d_grp, (const uint8_t*)d->d_ref, s.n_groups, d->d_units, 0ull);
             HIP_TRY(launch_check());
         }
         H2D(d->d_blkA, s.h_blkA.data(), nblk * sizeof(int32_t), d->stream);
@@ -3250,7 +3258,8 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
             if (s.units_on_device && s.n_groups) {
                 hipLaunchKernelGGL(k_build_units, dim3((unsigned)((s.n_groups + 3) / 4)), dim3(256), 0, d->stream,
                                    (const uint8_t*)d->d_rbytes, (const int64_t*)d->d_roff, (const int2*)d->d_rh,
-                                   (const RGroup*)d->d_grp, (const uint8_t*)d->d_ref, s.n_groups, d->d_units);
+                                   (const RGroup*)d->d_grp, (const uint8_t*)d->d_ref, s.n_groups, d->d_units,
+                                   kPopPadUnit);
                 HIP_TRY(launch_check());
                 // (the bytes are not needed past the build: released once it is done)
                 HIP_TRY(hipStreamSynchronize(d->stream));
