@@ -1517,7 +1517,7 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
     const int32_t* __restrict__ samp_st, const int32_t* __restrict__ blkA, const int32_t* __restrict__ blkB,
     int64_t nblk, int32_t shift, int32_t n_samples, const uint8_t* __restrict__ ref, const LikTables* __restrict__ tabs,
     GenotypeParams gp, uint32_t* __restrict__ need, unsigned long long* __restrict__ counters, uint2* __restrict__ pairs,
-    int64_t pseg) {
+    int64_t pseg, const int64_t* __restrict__ st_end) {
     __shared__ unsigned long long w[2][32];
     __shared__ uint32_t s_call[kKlmTile / 32];         // callable positions of the tile
     __shared__ uint32_t s_bm[4][kKlmWords];            // marked positions, then those the exact bound takes
@@ -1673,6 +1673,110 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
                 }
             }
         }
+    }
+    if (COUNT) {
+        // ---- the exact bound for the count bound's survivors, eight lanes per column: each lane takes every eighth
+        //      entry of the sample's streams from the column's block-table entry on, the covering reads' units loaded as
+        //      their headers arrive, the valid calls summed into {reference, alt 1-3} weights and reduced across the
+        //      eight; a column the bound cannot prove hom-ref (or with more than kMcMaxCalls valid calls) opens its
+        //      position and, with pairs, is listed for KPM's first stage.  The gathers' latency hides behind the other
+        //      waves' streams (a separate kernel over the same columns: 0.109-0.166 ms after KLM, r05w2 / r05x).
+        const uint32_t c = (uint32_t)__popc(word);
+        uint32_t incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t x = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += x;
+        }
+        const uint32_t tot = (uint32_t)__shfl((int)incl, 63, 64);
+        unsigned long long tcand = ncand;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tcand += __shfl_xor(tcand, o, 64);
+        const int sh = (int)(blockIdx.x % kKlShards);
+        unsigned long long* sc = counters + kCtrShard0 + kCtrShardStride * sh;
+        if (lane == 0) {
+            if (tcand) atomicAdd(&sc[0], tcand);
+            if (tot) atomicAdd(&sc[1], (unsigned long long)tot);
+        }
+        if (tot == 0) return;
+        // the wave's columns in position order (tile offsets; its counters' LDS is free by now)
+        uint16_t* cpos = reinterpret_cast<uint16_t*>(s_wave[wv]);
+        {
+            uint32_t k = incl - c;
+            for (uint32_t wd = word; wd; wd &= wd - 1u) cpos[k++] = (uint16_t)(32 * lane + __builtin_ctz(wd));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int j = lane & 7;
+        const int32_t maxq = gp.max_q;
+        const long long th = tabs->t_het, to = tabs->t_homo;
+        for (uint32_t c0 = 0; c0 < tot; c0 += 8) {
+            const uint32_t ci = c0 + (uint32_t)(lane >> 3);
+            const bool have = ci < tot;
+            const int32_t p = have ? tstart + cpos[ci] : 0;
+            unsigned long long a0 = 0ull, a1 = 0ull, a2 = 0ull, a3 = 0ull;
+            uint32_t sn = 0;
+            if (have) {
+                for (int st = st0; st < st1; st++) {
+                    const int64_t end = st_end[st];
+                    for (int64_t e = blkA[(int64_t)st * nblk + (p >> shift)] + j;; e += 8) {
+                        const int2 h = e < end ? rh[e] : make_int2(0x7FFFFFFF, 0);
+                        const int32_t gf = h.x, gl = h.y & 0x7FFFFFFF;
+                        if (gf <= p && p <= gl) {
+                            const int64_t o = p - gf;
+                            const uint64_t u = units[grp[e >> 6].base + (o >> 3) * 64 + (e & 63)];
+                            const uint32_t y = (uint32_t)(u >> (8 * (o & 7))) & 0xFFu;   // (reference-relative)
+                            if (!(y & 0x80u)) {                                          // a valid call
+                                const uint32_t al = (y >> 5) & 3u;
+                                int q = (int)(y & 31u);
+                                q = q > maxq ? maxq : q;
+                                const unsigned long long wq = w[al == 0 ? 0 : 1][q];
+                                a0 += al == 0 ? wq : 0ull;
+                                a1 += al == 1 ? wq : 0ull;
+                                a2 += al == 2 ? wq : 0ull;
+                                a3 += al == 3 ? wq : 0ull;
+                                sn++;
+                            }
+                        }
+                        // entries are sorted by gfirst: the eight stop once every one's entry starts past p
+                        const unsigned long long mb = __ballot(gf <= p);
+                        if (!((mb >> (lane & ~7)) & 0xFFull)) break;
+                    }
+                }
+            }
+#pragma unroll
+            for (int o = 4; o > 0; o >>= 1) {
+                a0 += __shfl_xor(a0, o, 64); a1 += __shfl_xor(a1, o, 64);
+                a2 += __shfl_xor(a2, o, 64); a3 += __shfl_xor(a3, o, 64);
+                sn += __shfl_xor(sn, o, 64);
+            }
+            bool open = false;
+            if (have && j == 0) {
+                const long long R1 = (long long)(a0 & 0xFFFFFFFFull), R2 = (long long)(a0 >> 32);
+                const long long x1 = (long long)(a1 & 0xFFFFFFFFull), y1 = (long long)(a2 & 0xFFFFFFFFull);
+                const long long z1 = (long long)(a3 & 0xFFFFFFFFull);
+                const long long x2 = (long long)(a1 >> 32), y2 = (long long)(a2 >> 32), z2 = (long long)(a3 >> 32);
+                const bool drop = (R1 - x1 > th) && (R1 - y1 > th) && (R1 - z1 > th) &&
+                                  (R2 - x2 > to) && (R2 - y2 > to) && (R2 - z2 > to) &&
+                                  (R2 - x1 - y1 > th) && (R2 - x1 - z1 > th) && (R2 - y1 - z1 > th);
+                open = !bound_on || sn > (uint32_t)kMcMaxCalls || !drop;
+                if (open) atomicOr(&need[p >> 5], 1u << (p & 31));
+            }
+            if (pairs) {
+                const unsigned long long m = __ballot(open);
+                if (m) {
+                    unsigned long long base = 0;
+                    if (lane == 0) base = atomicAdd(&sc[2], (unsigned long long)__popcll(m));
+                    base = __shfl(base, 0, 64);
+                    if (open) {
+                        const int64_t kp = (int64_t)base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        if (kp < pseg) pairs[(int64_t)sh * pseg + kp] = make_uint2((uint32_t)p, (uint32_t)s);
+                    }
+                }
+            }
+        }
+        return;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -3817,7 +3921,7 @@ static hipError_t launch_pop_scan(Device* d, const GenotypeParams& g, uint32_t* 
                           (const uint64_t*)d->d_units, (const int2*)d->d_rh, (const RGroup*)d->d_grp,
                           (const int32_t*)d->d_samp_st, (const int32_t*)d->d_blkA, (const int32_t*)d->d_blkB, d->pnblk,
                           d->pblk_shift, d->n_samples, (const uint8_t*)d->d_ref, (const LikTables*)d->d_tables, g, need, ctr,
-                          stage ? stage->pairs : nullptr, stage ? stage->pseg : (int64_t)0);
+                          stage ? stage->pairs : nullptr, stage ? stage->pseg : (int64_t)0, (const int64_t*)d->d_st_end);
     if ((e = launch_check()) != hipSuccess) return e;
     const int64_t qblk = std::max<int64_t>(1, std::min<int64_t>((nwords + 255) / 256, (int64_t)d->n_cu * 4));
     hipExtLaunchKernelGGL(k_queue_need, dim3((unsigned)qblk), dim3(256), 0, d->stream, nullptr, ev_end, 0,

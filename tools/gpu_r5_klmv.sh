@@ -1,7 +1,6 @@
 #!/bin/bash
-# round 5: KLM's VALU work per unit cut (no end-of-read mask: the population layout pads with 0x1F; a five-operation
-# bit gather) -- population parity tests, then configs[4] lines against the previous build (ab/prev) on one box, and
-# KL's PMC passes (tools/gpu_r5_pmckl.sh)
+# round 5: KLM changes against the previous build (ab/prev) on one box -- population parity tests, configs[4] lines
+# (last: the count bound's survivors to KX, k_exact_cols, instead of KLM's own exact pass)
 set -o pipefail
 export NGSEP_SKIP_BUILD=1
 cd "$GRAFT_REPO_ROOT"
@@ -26,5 +25,4 @@ M=$PWD/ngsepcore_amd/lib/libngsep_amd.so
 P=$PWD/ab/prev/libngsep_amd.so
 run new $M && run prev $P && run new2 $M && run prev2 $P && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_ms -o run --output-format csv -- $B \
-    > gpurun_out/prof_${TAG}_ms.out 2>&1 && python tools/kstats.py gpurun_out/prof_${TAG}_ms gpurun_out/${TAG}_ms_kernel_stats.csv > gpurun_out/${TAG}_ms_kstats.txt && head -6 gpurun_out/${TAG}_ms_kstats.txt && \
-bash tools/gpu_r5_pmckl.sh ${TAG}kl
+    > gpurun_out/prof_${TAG}_ms.out 2>&1 && python tools/kstats.py gpurun_out/prof_${TAG}_ms gpurun_out/${TAG}_ms_kernel_stats.csv > gpurun_out/${TAG}_ms_kstats.txt && head -6 gpurun_out/${TAG}_ms_kstats.txt
