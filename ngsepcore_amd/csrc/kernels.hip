@@ -999,14 +999,16 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
         // (the next batch's loads unconditional, past the read's end too -- other reads' rows or the buffer's slack,
         // never used: a load under a lane condition made the compiler wait for every outstanding load, the next
         // batch's included, before the current batch)
+        // (clamped to the read's last unit: a slot past it reloads that unit's line, a cache hit -- FETCH_SIZE 2.51 ->
+        // 2.25 GB per configs[2] launch, 1.02x the algorithmic bytes, at the same time, r05c2)
+        const int32_t lim = kn < 0 ? 0 : kn;
         uint64_t u[U];
 #pragma unroll
-        for (int i = 0; i < U; i++) u[i] = KL_LOAD(ub[(int64_t)i * 64]);
+        for (int i = 0; i < U; i++) u[i] = KL_LOAD(ub[(int64_t)min(i, lim) * 64]);
         for (int32_t j = 0; j <= kn; j += U) {
             uint64_t v[U];
-            const uint64_t* nb = ub + (int64_t)(j + U) * 64;
 #pragma unroll
-            for (int i = 0; i < U; i++) v[i] = KL_LOAD(nb[(int64_t)i * 64]);
+            for (int i = 0; i < U; i++) v[i] = KL_LOAD(ub[(int64_t)min(j + U + i, lim) * 64]);
 #else
         for (int32_t j = 0; j <= kn; j += U) {
             uint64_t u[U];
@@ -1581,6 +1583,8 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
             // (every batch's loads are issued unconditionally -- the units past a read's end are other reads' rows, or
             // the buffer's slack past the last group, and are never used: a load under a lane condition made the
             // compiler wait for every outstanding load, the next batch's included, before the current batch)
+            // (not clamped to the read's last unit as KL's are: the clamp's address arithmetic cost this VALU-bound
+            // kernel 1.5 % -- 0.853-0.863 against 0.840-0.845 ms -- for 10 % less FETCH_SIZE, r05c2)
             uint64_t u[kKlmUnroll];
 #pragma unroll
             for (int i = 0; i < kKlmUnroll; i++) u[i] = ub[(int64_t)i * 64];
