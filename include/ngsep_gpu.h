@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define NGSEP_ABI_VERSION 11
+#define NGSEP_ABI_VERSION 12
 
 #define NGSEP_OK 0
 #define NGSEP_E_INVALID (-1)      /* bad argument / state */
@@ -387,6 +387,12 @@ int  ngsep_bam_next_batch(ngsep_bam* bam, int64_t max_reads, ngsep_read_batch* b
  * of seq starting at or before last.  NGSEP_E_IO when the BAM has no index. */
 int  ngsep_bam_set_region(ngsep_bam* bam, const char* seq_name, int64_t first, int64_t last);
 int  ngsep_bam_close(ngsep_bam* bam);
+/* ABI 12: BGZF decompression on the context's device -- htsjdk BlockCompressedInputStream's role for the BAM readers
+ * (ReadAlignmentFileReader.java:171-183).  Every BGZF block of in[0, n) (which ends on a block boundary) is inflated
+ * (RFC 1951) into out; *out_n = the decoded bytes (the sum of the blocks' ISIZE).  NGSEP_E_INVALID with *out_n set
+ * when cap is too small, NGSEP_E_FORMAT for a malformed block or one that does not inflate to its ISIZE.  The
+ * single-sample BAM readers (ngsep_bam_open with no samples set) inflate this way when NGSEP_GPU_INFLATE is set. */
+int  ngsep_bgzf_inflate(ngsep_ctx* ctx, const uint8_t* in, int64_t n, uint8_t* out, int64_t cap, int64_t* out_n);
 
 /* ---- measurement entry points (bench.py): split staging (pack + H2D) from the device run ---- */
 int ngsep_stage_alignments(ngsep_ctx* ctx, const ngsep_read_batch* batch);  /* pack + upload, keep resident */

@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-ABI_VERSION = 11                                   # NGSEP_ABI_VERSION (include/ngsep_gpu.h)
+ABI_VERSION = 12                                   # NGSEP_ABI_VERSION (include/ngsep_gpu.h)
 DEFAULT_LIB_PATH = os.path.join(_HERE, "lib", "libngsep_amd.so")
 # NGSEP_LIB_PATH: an A/B tuning build of the same ABI, for measurements only.  It is announced on stderr when taken, and
 # bench.py records it in its line (config.lib_path), so no result can come from a swapped library silently.
@@ -201,6 +201,8 @@ SIGNATURES = {
     "ngsep_bam_open": (ctypes.c_int, [_CTX, ctypes.c_char_p, P(ctypes.c_void_p)]),
     "ngsep_bam_next_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, P(NgsepReadBatch)]),
     "ngsep_bam_close": (ctypes.c_int, [ctypes.c_void_p]),
+    "ngsep_bgzf_inflate": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.POINTER(ctypes.c_int64)]),
     "ngsep_fetch_carved_regions": (ctypes.c_int, [_CTX, P(ctypes.c_int32), P(ctypes.c_int64), P(ctypes.c_int64), ctypes.c_int64, P(ctypes.c_int64)]),
     "ngsep_clear_carved_regions": (ctypes.c_int, [_CTX]),
     "ngsep_bam_set_region": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64]),

@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <new>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -67,23 +68,38 @@ struct Inflater {
     }
 };
 
-// growable array without value-initialisation (batch and chunk buffers are overwritten in parallel)
+// growable array without value-initialisation (batch and chunk buffers are overwritten in parallel); pinned: page-locked
+// host memory (gz_host_alloc) the device inflate copies into and out of at the link's rate
 template <class T>
 struct RawBuf {
     T* p = nullptr;
     size_t n = 0, cap = 0;
+    bool pinned = false;
     RawBuf() = default;
     RawBuf(const RawBuf&) = delete;
     RawBuf& operator=(const RawBuf&) = delete;
-    RawBuf(RawBuf&& o) noexcept : p(o.p), n(o.n), cap(o.cap) { o.p = nullptr; o.n = o.cap = 0; }
-    RawBuf& operator=(RawBuf&& o) noexcept { std::swap(p, o.p); std::swap(n, o.n); std::swap(cap, o.cap); return *this; }
-    ~RawBuf() { std::free(p); }
+    RawBuf(RawBuf&& o) noexcept : p(o.p), n(o.n), cap(o.cap), pinned(o.pinned) { o.p = nullptr; o.n = o.cap = 0; }
+    RawBuf& operator=(RawBuf&& o) noexcept {
+        std::swap(p, o.p); std::swap(n, o.n); std::swap(cap, o.cap); std::swap(pinned, o.pinned);
+        return *this;
+    }
+    ~RawBuf() { release(); }
+    void release() {
+        if (pinned) ngsep::gz_host_free(p);
+        else std::free(p);
+        p = nullptr;
+        n = cap = 0;
+    }
+    // takes over a pinned allocation (p, cap)
+    void adopt_pinned(void* q, size_t c) { release(); p = static_cast<T*>(q); cap = c / sizeof(T); pinned = true; }
     void resize(size_t k) {
         if (k > cap) {
             const size_t c = std::max(k, cap + cap / 2);
-            T* q = static_cast<T*>(ngsep::huge_alloc(c * sizeof(T)));
+            T* q = static_cast<T*>(pinned ? ngsep::gz_host_alloc(c * sizeof(T)) : ngsep::huge_alloc(c * sizeof(T)));
+            if (!q) throw std::bad_alloc();
             if (n) std::memcpy(q, p, n * sizeof(T));
-            std::free(p);
+            if (pinned) ngsep::gz_host_free(p);
+            else std::free(p);
             p = q;
             cap = c;
         }
@@ -155,8 +171,11 @@ struct ngsep_bam {
         RawBuf<char> b_bases, b_quals;
     } store[2];
     int store_cur = 0;
+    // inflate on the device (the context's GzDevice, borrowed while the reader is open), else on the host threads
+    bool gpu_inflate = false;
     // NGSEP_HOST_TIMING diagnostics: seconds in the decoder's inflate, the record cut, parse and emit
     double t_inflate = 0, t_wait = 0, t_need = 0, t_cut = 0, t_parse = 0, t_emit = 0;
+    double t_read = 0, t_pin = 0;               // device inflate: the decoder's file reads, its pinned allocations
     int64_t n_pcut = 0, n_pcut_serial = 0;      // parallel cuts, and their segments walked sequentially
     double t_pcut_walk = 0, t_pcut_merge = 0;
 };
@@ -165,8 +184,157 @@ namespace {
 
 using ngsep::parallel_for;
 
+// the whole BGZF blocks at the start of comp[0, n) (SAM spec 4.1.1): their raw deflate data (offset, length) and
+// decoded sizes; returns the bytes they span (a block cut off by n stays for the next read)
+size_t scan_bgzf(const uint8_t* comp, size_t n, std::vector<size_t>& boff, std::vector<size_t>& bclen,
+                 std::vector<uint32_t>& bisize, std::string& err) {
+    boff.clear();
+    bclen.clear();
+    bisize.clear();
+    size_t p = 0;
+    while (p + 18 <= n) {
+        const uint8_t* h = comp + p;
+        if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) { err = "not a BGZF file"; break; }
+        const uint16_t xlen = (uint16_t)(h[10] | (h[11] << 8));
+        if (p + 12 + xlen > n) break;
+        int bsize = -1;
+        for (size_t i = 0; i + 4 <= xlen;) {
+            const uint8_t* x = h + 12 + i;
+            const uint16_t sl = (uint16_t)(x[2] | (x[3] << 8));
+            if (x[0] == 'B' && x[1] == 'C' && sl == 2) bsize = x[4] | (x[5] << 8);
+            i += 4 + sl;
+        }
+        if (bsize < 0) { err = "BGZF block without BC field"; break; }
+        const size_t total = (size_t)bsize + 1;
+        if (total < 12 + (size_t)xlen + 8) { err = "malformed BGZF block"; break; }
+        if (p + total > n) break;
+        const uint8_t* t = h + total - 4;
+        boff.push_back(p + 12 + xlen);
+        bclen.push_back(total - 12 - xlen - 8);
+        bisize.push_back((uint32_t)(t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24)));
+        p += total;
+    }
+    return p;
+}
+
+// decoder thread, device inflate (inflate.hip): 32 MB of the file at a time into a pinned buffer, its whole blocks
+// inflated by KZ into a pinned chunk; two reads in flight (the file read of one overlaps the copies and kernel of the
+// previous), the chunk handed over when its batch is done
+void decoder_loop_gpu(ngsep_bam* b) {
+    // (NGSEP_BGZF_READ: a smaller read, test hook -- many batches and blocks cut across reads on small files)
+    const char* rh = ngsep::env_hook("NGSEP_BGZF_READ");
+    const size_t kRead = rh ? std::max<size_t>((size_t)std::atoll(rh), 4096) : (size_t)32 << 20;
+    ngsep_ctx* c = b->ctx;
+    RawBuf<uint8_t> comp[2];
+    for (int i = 0; i < 2; i++) {
+        if (!c->gz_in_pool.empty()) { comp[i].adopt_pinned(c->gz_in_pool.back().first, c->gz_in_pool.back().second); c->gz_in_pool.pop_back(); }
+        else comp[i].pinned = true;
+    }
+    std::vector<size_t> boff, bclen, dout;
+    std::vector<uint32_t> bisize;
+    const uint8_t* tail = nullptr;
+    size_t tail_n = 0;
+    bool file_eof = false;
+    int sl = 0;
+    Chunk pend;
+    bool have_pend = false;
+    int pend_slot = -1;
+    std::string gerr;
+    if (!c->gz) c->gz = ngsep::gz_create(c->device, gerr);
+    auto hand_over = [&](Chunk&& ch) {
+        {
+            std::lock_guard<std::mutex> lk(b->mu);
+            b->q.push_back(std::move(ch));
+        }
+        b->cv.notify_all();
+    };
+    auto finish_pending = [&]() {
+        if (pend_slot < 0) return;
+        const auto tw = std::chrono::steady_clock::now();
+        std::string e;
+        if (ngsep::gz_wait(c->gz, pend_slot, e) != 0 && pend.err.empty()) pend.err = e.empty() ? "BGZF inflate failed" : e;
+        b->t_inflate += std::chrono::duration<double>(std::chrono::steady_clock::now() - tw).count();
+        pend_slot = -1;
+    };
+    while (true) {
+        {
+            std::unique_lock<std::mutex> lk(b->mu);
+            b->cv.wait(lk, [&] { return b->stop || b->q.size() < 3; });
+            if (b->stop) break;
+        }
+        Chunk ch;
+        RawBuf<uint8_t>& cb = comp[sl];
+        size_t total = 0;
+        if (!c->gz) ch.err = "BGZF inflate device: " + gerr;
+        else {
+            cb.n = 0;
+            cb.resize(tail_n + kRead + 256);
+            if (tail_n) std::memmove(cb.data(), tail, tail_n);
+            total = tail_n;
+            if (!file_eof) {
+                const auto tr = std::chrono::steady_clock::now();
+                const size_t got = std::fread(cb.data() + tail_n, 1, kRead, b->f);
+                b->t_read += std::chrono::duration<double>(std::chrono::steady_clock::now() - tr).count();
+                total += got;
+                if (got < kRead) file_eof = true;
+            }
+        }
+        const size_t p = ch.err.empty() ? scan_bgzf(cb.data(), total, boff, bclen, bisize, ch.err) : 0;
+        if (ch.err.empty() && p < total && file_eof && boff.empty()) ch.err = "truncated BGZF block";
+        tail = cb.data() + p;
+        tail_n = ch.err.empty() ? total - p : 0;
+        dout.assign(boff.size() + 1, 0);
+        for (size_t k = 0; k < boff.size(); k++) dout[k + 1] = dout[k] + bisize[k];
+        {
+            std::lock_guard<std::mutex> lk(b->mu);
+            if (!b->pool.empty()) { ch.mem = std::move(b->pool.back()); b->pool.pop_back(); }
+        }
+        if (!ch.mem.pinned) {
+            ch.mem.release();
+            if (!c->gz_chunk_pool.empty()) { ch.mem.adopt_pinned(c->gz_chunk_pool.back().first, c->gz_chunk_pool.back().second); c->gz_chunk_pool.pop_back(); }
+            else ch.mem.pinned = true;
+        }
+        ch.mem.n = 0;
+        const auto tp = std::chrono::steady_clock::now();
+        ch.mem.resize(kChunkHead + dout.back());
+        b->t_pin += std::chrono::duration<double>(std::chrono::steady_clock::now() - tp).count();
+        ch.len = dout.back();
+        if (ch.err.empty() && !boff.empty() &&
+            ngsep::gz_submit(c->gz, sl, cb.data(), total, boff.data(), bclen.data(), bisize.data(), dout.data(), boff.size(),
+                             ch.mem.data() + kChunkHead, ch.len, ch.err) == 0) {
+            // (submitted: finished by the next round's finish_pending)
+        }
+        ch.eof = file_eof && tail_n == 0;
+        const bool last = ch.eof || !ch.err.empty();
+        finish_pending();                                  // the previous read's chunk
+        if (have_pend) hand_over(std::move(pend));
+        pend = std::move(ch);
+        have_pend = true;
+        pend_slot = boff.empty() || !pend.err.empty() ? -1 : sl;
+        if (last) {
+            finish_pending();
+            hand_over(std::move(pend));
+            pend = Chunk();
+            break;
+        }
+        sl ^= 1;
+    }
+    finish_pending();                                      // (stopped: the in-flight batch drains before its buffers go)
+    pend = Chunk();
+    for (int i = 0; i < 2; i++)
+        if (comp[i].p && comp[i].pinned) {
+            c->gz_in_pool.emplace_back(comp[i].p, comp[i].cap);
+            comp[i].p = nullptr;
+            comp[i].cap = comp[i].n = 0;
+        }
+    std::lock_guard<std::mutex> lk(b->mu);
+    b->producer_done = true;
+    b->cv.notify_all();
+}
+
 // decoder thread: 32 MB of compressed blocks at a time, inflated on all host threads
 void decoder_loop(ngsep_bam* b) {
+    if (b->gpu_inflate) return decoder_loop_gpu(b);
     const size_t kRead = (size_t)32 << 20;
     std::vector<uint8_t> comp, carry;
     bool file_eof = false;
@@ -189,28 +357,7 @@ void decoder_loop(ngsep_bam* b) {
         // whole blocks in comp: offsets and decoded sizes
         std::vector<size_t> boff, bclen;
         std::vector<uint32_t> bisize;
-        size_t p = 0;
-        while (p + 18 <= comp.size()) {
-            const uint8_t* h = comp.data() + p;
-            if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) { ch.err = "not a BGZF file"; break; }
-            const uint16_t xlen = (uint16_t)(h[10] | (h[11] << 8));
-            if (p + 12 + xlen > comp.size()) break;
-            int bsize = -1;
-            for (size_t i = 0; i + 4 <= xlen;) {
-                const uint8_t* x = h + 12 + i;
-                const uint16_t sl = (uint16_t)(x[2] | (x[3] << 8));
-                if (x[0] == 'B' && x[1] == 'C' && sl == 2) bsize = x[4] | (x[5] << 8);
-                i += 4 + sl;
-            }
-            if (bsize < 0) { ch.err = "BGZF block without BC field"; break; }
-            const size_t total = (size_t)bsize + 1;
-            if (p + total > comp.size()) break;
-            const uint8_t* t = h + total - 4;
-            boff.push_back(p + 12 + xlen);
-            bclen.push_back(total - 12 - xlen - 8);
-            bisize.push_back((uint32_t)(t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24)));
-            p += total;
-        }
+        const size_t p = scan_bgzf(comp.data(), comp.size(), boff, bclen, bisize, ch.err);
         if (ch.err.empty() && p < comp.size()) {
             if (file_eof && boff.empty()) ch.err = "truncated BGZF block";
             carry.assign(comp.begin() + (ptrdiff_t)p, comp.end());
@@ -381,6 +528,30 @@ void reg2bins(int64_t beg, int64_t end, std::vector<uint32_t>& out) {
 
 using namespace ngsep;
 
+namespace {
+bool gpu_inflate_wanted(const ngsep_ctx* c) {
+    return c->sample_ids.empty() && ngsep::env_hook("NGSEP_GPU_INFLATE") != nullptr;
+}
+// a closing reader's pinned chunk buffers go back to its context, and the context's inflate device is free again
+void give_back_inflate(ngsep_bam* b) {
+    if (!b->gpu_inflate) return;
+    ngsep_ctx* c = b->ctx;
+    auto keep = [&](RawBuf<uint8_t>& m) {
+        if (m.p && m.pinned && c->gz_chunk_pool.size() < 6) {
+            c->gz_chunk_pool.emplace_back(m.p, m.cap);
+            m.p = nullptr;
+            m.n = m.cap = 0;
+        }
+    };
+    for (auto& m : b->pool) keep(m);
+    b->pool.clear();
+    keep(b->mem);
+    b->buf = nullptr;
+    b->gpu_inflate = false;
+    c->gz_busy = false;
+}
+}  // namespace
+
 extern "C" int ngsep_bam_open(ngsep_ctx* c, const char* path, ngsep_bam** out) {
     if (!c || !path || !out) return NGSEP_E_INVALID;
     ngsep_bam* b = new ngsep_bam();
@@ -388,9 +559,13 @@ extern "C" int ngsep_bam_open(ngsep_ctx* c, const char* path, ngsep_bam** out) {
     b->path = path;
     b->f = std::fopen(path, "rb");
     if (!b->f) { delete b; return set_error(c, NGSEP_E_IO, std::string("cannot open ") + path); }
+    // single-sample readers inflate on the device, one reader of the context at a time (a population's hundreds of
+    // open readers stay on the host threads)
+    b->gpu_inflate = gpu_inflate_wanted(c) && !c->gz_busy.exchange(true);
     start_decoder(b);
     auto fail = [&](int code, const std::string& m) {
         stop_decoder(b);
+        give_back_inflate(b);
         std::fclose(b->f);
         delete b;
         return set_error(c, code, m);
@@ -901,11 +1076,47 @@ extern "C" int ngsep_bam_close(ngsep_bam* b) {
     if (!b) return NGSEP_E_INVALID;
     stop_decoder(b);
     if (env_hook("NGSEP_HOST_TIMING"))
-        std::fprintf(stderr, "[ngsep host] bam: inflate %.3f s (decoder thread), consumer wait %.3f s, need %.3f s, cut %.3f s (incl. wait; %lld parallel: walks %.3f s, merge %.3f s, %lld segments walked sequentially), parse %.3f s, emit %.3f s\n",
-                     b->t_inflate, b->t_wait, b->t_need, b->t_cut, (long long)b->n_pcut, b->t_pcut_walk, b->t_pcut_merge,
+        std::fprintf(stderr, "[ngsep host] bam: inflate %.3f s (decoder thread%s), consumer wait %.3f s, need %.3f s, cut %.3f s (incl. wait; %lld parallel: walks %.3f s, merge %.3f s, %lld segments walked sequentially), parse %.3f s, emit %.3f s\n",
+                     b->t_inflate, b->gpu_inflate ? ", waiting on the device" : "", b->t_wait, b->t_need, b->t_cut, (long long)b->n_pcut, b->t_pcut_walk, b->t_pcut_merge,
                      (long long)b->n_pcut_serial, b->t_parse, b->t_emit);
+    if (env_hook("NGSEP_HOST_TIMING") && b->gpu_inflate)
+        std::fprintf(stderr, "[ngsep host] bam (device inflate): file reads %.3f s, pinned allocations %.3f s\n", b->t_read, b->t_pin);
+    give_back_inflate(b);
     if (b->f) std::fclose(b->f);
     delete b;
+    return NGSEP_OK;
+}
+
+// BGZF decompression on the context's device (inflate.hip), the decoder's device path as one call: every block of
+// in[0, n) (which must end on a block boundary) -> out[0, *out_n).  NGSEP_E_INVALID (with *out_n the size needed) when
+// cap is too small.
+extern "C" int ngsep_bgzf_inflate(ngsep_ctx* c, const uint8_t* in, int64_t n, uint8_t* out, int64_t cap, int64_t* out_n) {
+    if (!c || (!in && n) || n < 0 || cap < 0 || !out_n) return NGSEP_E_INVALID;
+    std::vector<size_t> boff, bclen, dout;
+    std::vector<uint32_t> bisize;
+    std::string err;
+    const size_t p = scan_bgzf(in, (size_t)n, boff, bclen, bisize, err);
+    if (!err.empty()) return set_error(c, NGSEP_E_FORMAT, err);
+    if (p != (size_t)n) return set_error(c, NGSEP_E_FORMAT, "truncated BGZF block");
+    dout.assign(boff.size() + 1, 0);
+    for (size_t k = 0; k < boff.size(); k++) dout[k + 1] = dout[k] + bisize[k];
+    *out_n = (int64_t)dout.back();
+    if ((int64_t)dout.back() > cap) return set_error(c, NGSEP_E_INVALID, "output buffer too small");
+    if (boff.empty()) return NGSEP_OK;
+    if (c->gz_busy.exchange(true)) return set_error(c, NGSEP_E_INVALID, "the context's inflate device is in use by an open reader");
+    struct Release { ngsep_ctx* c; ~Release() { c->gz_busy = false; } } rel{c};
+    if (!c->gz) c->gz = ngsep::gz_create(c->device, err);
+    if (!c->gz) return set_error(c, NGSEP_E_DEVICE, err);
+    RawBuf<uint8_t> pin_in, pin_out;
+    pin_in.pinned = pin_out.pinned = true;
+    pin_in.resize((size_t)n);
+    pin_out.resize(std::max<size_t>(dout.back(), 1));
+    std::memcpy(pin_in.data(), in, (size_t)n);
+    if (ngsep::gz_submit(c->gz, 0, pin_in.data(), (size_t)n, boff.data(), bclen.data(), bisize.data(), dout.data(), boff.size(),
+                         pin_out.data(), dout.back(), err) != 0 ||
+        ngsep::gz_wait(c->gz, 0, err) != 0)
+        return set_error(c, NGSEP_E_FORMAT, err);
+    std::memcpy(out, pin_out.data(), dout.back());
     return NGSEP_OK;
 }
 

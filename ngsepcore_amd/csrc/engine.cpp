@@ -3263,6 +3263,9 @@ extern "C" int ngsep_close(ngsep_ctx* c) {
     c->arena.release();
     if (c->dev) device_destroy(c->dev);
     if (c->cov_dev) cov_destroy(c->cov_dev);
+    for (auto& m : c->gz_in_pool) ngsep::gz_host_free(m.first);
+    for (auto& m : c->gz_chunk_pool) ngsep::gz_host_free(m.first);
+    if (c->gz) ngsep::gz_destroy(c->gz);
     delete c;
     return NGSEP_OK;
 }

@@ -392,6 +392,7 @@ void parallel_for(int64_t n, int64_t grain, F&& fn) {
 
 struct Device;   // kernels.hip
 struct CovDevice;   // coverage.hip
+struct GzDevice;    // inflate.hip
 
 // Pinned host memory (kernels.hip).  Every host address a device copy reads or writes lies in a block recorded in
 // one registry: pinned_alloc's blocks (a page-aligned block registered with hipHostRegister, or hipHostMalloc when
@@ -787,6 +788,11 @@ struct ngsep_ctx {
         int64_t windows = 0;                      // windows run (diagnostics)
     } stream;
     ngsep::Device* dev = nullptr;
+    // path B: BGZF blocks inflated on the device (inflate.hip) by the single-sample readers of this context, one
+    // reader at a time (gz_busy); pinned input / decoded-chunk buffers (pointer, capacity) kept across readers
+    ngsep::GzDevice* gz = nullptr;
+    std::atomic<bool> gz_busy{false};
+    std::vector<std::pair<void*, size_t>> gz_in_pool, gz_chunk_pool;
     // path B: the device is created on a thread of its own while the input is read (start_device_init), adopted
     // by the first device step (ensure_device)
     std::thread dev_init;
@@ -882,6 +888,15 @@ void cov_destroy(CovDevice* d);
 int cov_upload(CovDevice* d, const std::vector<int64_t>& gfirst, const std::vector<uint32_t>& spanu, int64_t g_len,
                int32_t max_span, std::string& err);
 int cov_run(CovDevice* d, int32_t max_cov, uint64_t* hist_out, double* kernel_ms, std::string& err);
+// inflate.hip: BGZF blocks inflated on the device (bam.cpp's decoder; two slots in flight)
+struct GzDevice;
+GzDevice* gz_create(int ordinal, std::string& err);
+void gz_destroy(GzDevice* d);
+void* gz_host_alloc(size_t n);                   // pinned host memory
+void gz_host_free(void* p);
+int gz_submit(GzDevice* d, int slot, const uint8_t* in, size_t in_n, const size_t* boff, const size_t* bclen,
+              const uint32_t* bisize, const size_t* dout, size_t nb, uint8_t* out, size_t out_n, std::string& err);
+int gz_wait(GzDevice* d, int slot, std::string& err);
 // engine.cpp
 int coverage_stage(ngsep_ctx* c, std::vector<ContigReads>& contigs);
 int coverage_run(ngsep_ctx* c, double* kernel_ms);

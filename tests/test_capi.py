@@ -28,7 +28,7 @@ def test_every_declared_symbol_is_exported():
 
 def test_abi_version_and_defaults():
     lib = _lib.load()
-    assert lib.ngsep_abi_version() == 11
+    assert lib.ngsep_abi_version() == 12
     p = _lib.NgsepParams()
     lib.ngsep_params_default(ctypes.byref(p))
     # DEF_* constants: SingleSampleVariantsDetector.java:65-78, CountsHelper.java:42-48

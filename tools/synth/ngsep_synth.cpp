@@ -748,14 +748,17 @@ struct Bgzf {
         out.assign(n + 1024, 0);
         size_t clen = 0;
         const Libdeflate& ld = libdeflate();
+        // NGS_SYNTH_LEVEL: another compression level (0 = stored blocks: an inflate-free floor for the
+        // end-to-end measurement)
+        static const int level = std::getenv("NGS_SYNTH_LEVEL") ? std::atoi(std::getenv("NGS_SYNTH_LEVEL")) : 6;
         if (ld.alloc && !std::getenv("NGS_SYNTH_ZLIB")) {
             thread_local struct Cmp { void* c = nullptr; ~Cmp() { if (c) libdeflate().release(c); } } cmp;
-            if (!cmp.c) cmp.c = ld.alloc(6);
+            if (!cmp.c) cmp.c = ld.alloc(level);
             clen = ld.compress(cmp.c, data, n, out.data() + 18, out.size() - 26);
         }
         if (clen == 0) {
             z_stream z{};
-            deflateInit2(&z, 6, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY);
+            deflateInit2(&z, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY);
             z.next_in = (Bytef*)data; z.avail_in = (uInt)n;
             z.next_out = out.data() + 18; z.avail_out = (uInt)(out.size() - 26);
             deflate(&z, Z_FINISH);
