@@ -121,6 +121,7 @@ struct MultiSlot {                   // one in-flight multisample run (device_su
     int64_t cap_hard = 0;
     uint32_t* d_need = nullptr;              // open positions (a bit per global position)
     int64_t cap_need = 0;                    // words
+    bool need_clean = false;                 // d_need is all zero (cleared by the last pass's k_stage_a)
     ngsep_popsite_out* d_psites = nullptr;   // KPM's sites (unordered) and their per-sample calls
     ngsep_sample_call* d_pcalls = nullptr;
     int64_t cap_psites = 0;
@@ -185,6 +186,7 @@ struct Device {
     int32_t n_streams = 0, pblk_shift = kRgBlockShift, pop_stride = 0;
     int64_t pnblk = 0;
     uint32_t* d_need = nullptr;      //   open positions, a bit per global position
+    bool need_clean = false;         //   d_need is all zero (cleared by the last run's k_stage_a)
     PopStage pstage;                 //   KPM's two stages (device_run_multi)
     ngsep_popsite_out* h_psites = nullptr;      // multisample: pinned staging of the emitted sites and calls
     ngsep_sample_call* h_pcalls = nullptr;
@@ -938,6 +940,9 @@ __device__ inline int32_t wave_gather(int32_t p, int64_t e0, int64_t n_entries, 
     return n;
 }
 
+#ifndef NGSEP_KL_EXLOOP
+#define NGSEP_KL_EXLOOP 1   // KL's !DEEP counter adds: 1 one add per exception, 0 the 8-position byte-pair adds
+#endif
 // KL's flags from reference-relative bytes y = code ^ reference code (bit 7 of byte k):
 __device__ __forceinline__ uint32_t kl_exc(uint32_t y) {
     // not a valid call of the reference's allele (bits 5-7 differ); at a callable position an exception
@@ -1024,7 +1029,19 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
                 if (!(elo | ehi) && !ABLATE(ablate, 2048)) continue;   // (2048, diagnostics: every lane adds)
                 const uint32_t nlo = kl_nonref(ylo), nhi = kl_nonref(yhi);
                 const int32_t ob = ob0 + 8 * (j + i);     // counter index of the unit's byte 0
-                if (!DEEP) {
+                if (!DEEP && NGSEP_KL_EXLOOP && !ABLATE(ablate, 512 | 1024 | 8192 | 16384)) {
+                    // one halfword add per exception (exceptions | other-allele << 8 at halfword ob + k): a lane's unit
+                    // rarely holds more than one, and the wave runs the loop as often as its busiest lane -- against
+                    // the 8-position byte-pair adds below, fewer instructions and LDS adds
+                    uint64_t ex = (uint64_t)elo | (uint64_t)ehi << 32;
+                    const uint64_t nr = (uint64_t)nlo | (uint64_t)nhi << 32;
+                    while (ex) {
+                        const int bit = __builtin_ctzll(ex);
+                        ex &= ex - 1ull;
+                        const int32_t hw = ob + (bit >> 3);
+                        atomicAdd(&s_cnt[hw >> 1], (1u + (((uint32_t)(nr >> bit) & 1u) << 8)) << ((hw & 1) << 4));
+                    }
+                } else if (!DEEP) {
                     // (exception, other-allele) byte pairs of the 8 positions, then shifted to the halfword
                     const uint32_t fl = elo >> 7, fh = ehi >> 7, ml = nlo >> 7, mh = nhi >> 7;
                     const uint32_t w0 = __builtin_amdgcn_perm(ml, fl, 0x05010400u), w1 = __builtin_amdgcn_perm(ml, fl, 0x07030602u);
@@ -2327,9 +2344,13 @@ __device__ __forceinline__ int nth_set_bit(uint32_t w, int r) {   // the r-th (0
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_stage_a(
     const QueueSite* __restrict__ queue, const unsigned long long* qn, int64_t qcap, const PopGather pg,
     const LikTables* __restrict__ tabs, GenotypeParams gp, int32_t ploidy, uint32_t* __restrict__ pmask,
-    QueueSite* __restrict__ qB, unsigned long long* __restrict__ qB_n, int64_t qB_cap, unsigned long long* counters) {
+    QueueSite* __restrict__ qB, unsigned long long* __restrict__ qB_n, int64_t qB_cap, unsigned long long* counters,
+    uint32_t* __restrict__ need_clear, int64_t need_words) {
     __shared__ double s_t[3][32];
     __shared__ double s_L[10][64];
+    // the pass's open-position bits are read for the last time by k_pair_mask, before this kernel: cleared here for the
+    // slot's next pass (no memset dispatch of their own)
+    for (int64_t w = (int64_t)blockIdx.x * 64 + threadIdx.x; w < need_words; w += (int64_t)gridDim.x * 64) need_clear[w] = 0u;
     extern __shared__ uint8_t s_gcol[];                  // the lanes' columns, pg.stride codes each
     const int lane = threadIdx.x;
     for (int k = lane; k < 96; k += 64) s_t[k >> 5][k & 31] = (k < 32 ? tabs->A : k < 64 ? tabs->H : tabs->E)[k & 31];
@@ -3329,6 +3350,7 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
         d->planes_W = s.tile / 32;
     } else {
         HIP_TRY(hipMalloc(&d->d_need, (size_t)(s.g_len / 32 + 1) * sizeof(uint32_t)));
+        d->need_clean = false;
         if (s.prg) {
             // multisample: the population read-group layout (KLM scans it, KPM gathers its columns)
             const size_t nblk = (size_t)(s.pnblk * s.n_streams);
@@ -3910,10 +3932,12 @@ static auto kpm_kernel(int ploidy, int gather) {
 }
 
 // KLM over every (sample, tile) of the resident population layout, then KQN (shared by the two multisample paths)
+// (need_clean: the open-position bits are already zero -- the previous pass's k_stage_a cleared them)
 static hipError_t launch_pop_scan(Device* d, const GenotypeParams& g, uint32_t* need, QueueSite* queue, int64_t qcap,
-                                  unsigned long long* ctr, hipEvent_t ev_start, hipEvent_t ev_end, PopStage* stage) {
+                                  unsigned long long* ctr, hipEvent_t ev_start, hipEvent_t ev_end, PopStage* stage,
+                                  bool need_clean) {
     const int64_t nwords = d->g_len / 32 + 1;
-    hipError_t e = hipMemsetAsync(need, 0, (size_t)nwords * sizeof(uint32_t), d->stream);
+    hipError_t e = need_clean ? hipSuccess : hipMemsetAsync(need, 0, (size_t)nwords * sizeof(uint32_t), d->stream);
     if (e != hipSuccess) return e;
     const int64_t ntile = d->g_len / kKlmTile;
     const int64_t nblk = std::max<int64_t>(1, ntile * ((d->n_samples + 3) / 4));
@@ -3976,9 +4000,11 @@ static PopGather pop_gather_of(const Device* d) {
 // KPM's first stage over KQN's queue (k_stage_a, one wavefront per position): the positions whose QS can pass -> the
 // stage's queue (counter 7), which the second stage (k_posterior_multi) genotypes in full
 static hipError_t launch_stage_a(Device* d, const GenotypeParams& g, int ploidy, const QueueSite* queue,
-                                 const unsigned long long* qn, int64_t qcap, PopStage& st, unsigned long long* ctr) {
+                                 const unsigned long long* qn, int64_t qcap, PopStage& st, unsigned long long* ctr,
+                                 uint32_t* need_clear, int64_t need_words) {
     hipLaunchKernelGGL(k_stage_a, dim3(sta_grid()), dim3(64), (size_t)64 * (size_t)d->pop_stride, d->stream, queue, qn, qcap,
-                       pop_gather_of(d), (const LikTables*)d->d_tables, g, (int32_t)ploidy, st.pmask, st.qB, ctr + 7, st.cap, ctr);
+                       pop_gather_of(d), (const LikTables*)d->d_tables, g, (int32_t)ploidy, st.pmask, st.qB, ctr + 7, st.cap, ctr,
+                       need_clear, need_words);
     return launch_check();
 }
 static size_t kpm_lds(const Device* d, int mode) { return mode == 1 ? (size_t)(d->n_samples + 1) * (size_t)d->pop_stride : 0; }
@@ -4035,7 +4061,9 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
         HIP_TRY(hipEventRecord(d->ev[0], d->stream));
         HIP_TRY(hipEventRecord(d->ev[1], d->stream));
     } else {
-        HIP_TRY(launch_pop_scan(d, g, d->d_need, d->d_hard, d->cap_hard, ctr, d->ev[0], d->ev[1], two ? &d->pstage : nullptr));
+        const bool clean = d->need_clean;
+        d->need_clean = false;
+        HIP_TRY(launch_pop_scan(d, g, d->d_need, d->d_hard, d->cap_hard, ctr, d->ev[0], d->ev[1], two ? &d->pstage : nullptr, clean));
     }
     if (ploidy >= 3 && !d->pool_valid) { err = "ploidy >= 3 without pool tables (device_set_pool)"; return -1; }
     // (no start event on KPM: a start event between KQN and KPM was measured to idle the device; KPM's time is
@@ -4043,7 +4071,10 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     if (!mknown && !d->prg) { err = "multisample run without a population layout"; return -1; }
     const int mode = d->prg ? 1 : 0;
     if (two) {
-        HIP_TRY(launch_stage_a(d, g, ploidy, d->d_hard, ctr + 2, d->cap_hard, d->pstage, ctr));
+        const bool scanned = !mknown && d->prg;
+        HIP_TRY(launch_stage_a(d, g, ploidy, d->d_hard, ctr + 2, d->cap_hard, d->pstage, ctr, scanned ? d->d_need : nullptr,
+                               scanned ? d->g_len / 32 + 1 : 0));
+        d->need_clean = scanned;
     }
     hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode), dim3(kpm_grid(d)), dim3(kPopThreads), kpm_lds(d, mode), d->stream, nullptr, d->ev[2], 0,
                           (const QueueSite*)(mknown ? d->d_mforced : two ? d->pstage.qB : d->d_hard),
@@ -4293,6 +4324,7 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
         m.d_need = nullptr;
         HIP_TRY(hipMalloc(&m.d_need, (size_t)nwords * sizeof(uint32_t)));
         m.cap_need = nwords;
+        m.need_clean = false;
     }
     if (!m.ev[0])
         for (int k = 0; k < 5; k++) HIP_TRY(hipEventCreateWithFlags(&m.ev[k], k < 4 ? hipEventDefault : hipEventDisableTiming));
@@ -4312,11 +4344,15 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
         HIP_TRY(hipEventRecord(m.ev[0], d->stream));
         HIP_TRY(hipEventRecord(m.ev[1], d->stream));
     } else {
-        HIP_TRY(launch_pop_scan(d, g, m.d_need, m.d_hard, m.cap_hard, ctr, m.ev[0], m.ev[1], two ? &m.stage : nullptr));
+        const bool clean = m.need_clean;
+        m.need_clean = false;
+        HIP_TRY(launch_pop_scan(d, g, m.d_need, m.d_hard, m.cap_hard, ctr, m.ev[0], m.ev[1], two ? &m.stage : nullptr, clean));
     }
     const int mode = d->prg ? 1 : 0;
     if (two) {
-        HIP_TRY(launch_stage_a(d, g, ploidy, m.d_hard, ctr + 2, m.cap_hard, m.stage, ctr));
+        HIP_TRY(launch_stage_a(d, g, ploidy, m.d_hard, ctr + 2, m.cap_hard, m.stage, ctr, mknown ? nullptr : m.d_need,
+                               mknown ? 0 : nwords));
+        m.need_clean = !mknown;
     }
     hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode), dim3(kpm_grid(d)), dim3(kPopThreads), kpm_lds(d, mode), d->stream, nullptr, m.ev[3], 0,
                           (const QueueSite*)(mknown ? d->d_mforced : two ? m.stage.qB : m.d_hard),
@@ -4344,8 +4380,7 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
     m.h_big.clear();
     m.h_big.reserve((size_t)m.cap_big);
     if (!m.ev[5]) HIP_TRY(hipEventCreateWithFlags(&m.ev[5], hipEventDisableTiming));
-    unsigned long long* d_nbig = ctr + 5;
-    HIP_TRY(hipMemsetAsync(d_nbig, 0, sizeof(unsigned long long), d->stream));
+    unsigned long long* d_nbig = ctr + 5;             // (zero: the pass's kernels before k_pack_calls leave counter 5 alone)
     const int64_t pblk = std::max<int64_t>(1, std::min<int64_t>((m.cap_psites * S + 255) / 256, (int64_t)d->n_cu * 8));
     hipLaunchKernelGGL(k_pack_calls, dim3((unsigned)pblk), dim3(256), 0, d->stream, (const ngsep_sample_call*)m.d_pcalls,
                        (const unsigned long long*)ctr, m.cap_psites, (int64_t)S, m.d_pack, m.d_big, d_nbig, m.cap_big,
