@@ -940,8 +940,11 @@ __device__ inline int32_t wave_gather(int32_t p, int64_t e0, int64_t n_entries, 
     return n;
 }
 
+#ifndef NGSEP_KLM_EXLOOP
+#define NGSEP_KLM_EXLOOP 0  // KLM's exception byte counters: 1 one add per exception, 0 the unit's 8 bytes in 2-3 adds
+#endif
 #ifndef NGSEP_KL_EXLOOP
-#define NGSEP_KL_EXLOOP 1   // KL's !DEEP counter adds: 1 one add per exception, 0 the 8-position byte-pair adds
+#define NGSEP_KL_EXLOOP 0   // KL's !DEEP counter adds: 1 one add per exception, 0 the 8-position byte-pair adds
 #endif
 // KL's flags from reference-relative bytes y = code ^ reference code (bit 7 of byte k):
 __device__ __forceinline__ uint32_t kl_exc(uint32_t y) {
@@ -1618,6 +1621,16 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
                     if (COUNT) {
                         uint64_t ex = (uint64_t)klm_exc(ylo) | (uint64_t)klm_exc(yhi) << 32;
                         if (ABLATE(gp.ablate, 65536)) { sink += (uint32_t)ex; ex = 0; }   // (diagnostics: no counters)
+#if NGSEP_KLM_EXLOOP
+                        // one byte add per exception (a lane's unit rarely holds more than one)
+                        const int32_t ob = ti0 - 24 + 8 * (j + i);
+                        while (ex) {
+                            const int bit = __builtin_ctzll(ex);
+                            ex &= ex - 1ull;
+                            const int32_t bi = ob + (bit >> 3);
+                            atomicAdd(cnt32 + (bi >> 2), 1u << ((bi & 3) << 3));
+                        }
+#endif
                         if (ex) {
                             const uint64_t one = ex >> 7;          // a 0 / 1 byte per position
                             const int32_t ob = ti0 - 24 + 8 * (j + i);
