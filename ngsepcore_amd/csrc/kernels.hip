@@ -940,12 +940,6 @@ __device__ inline int32_t wave_gather(int32_t p, int64_t e0, int64_t n_entries, 
     return n;
 }
 
-#ifndef NGSEP_KLM_EXLOOP
-#define NGSEP_KLM_EXLOOP 0  // KLM's exception byte counters: 1 one add per exception, 0 the unit's 8 bytes in 2-3 adds
-#endif
-#ifndef NGSEP_KL_EXLOOP
-#define NGSEP_KL_EXLOOP 0   // KL's !DEEP counter adds: 1 one add per exception, 0 the 8-position byte-pair adds
-#endif
 // KL's flags from reference-relative bytes y = code ^ reference code (bit 7 of byte k):
 __device__ __forceinline__ uint32_t kl_exc(uint32_t y) {
     // not a valid call of the reference's allele (bits 5-7 differ); at a callable position an exception
@@ -1032,20 +1026,10 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
                 if (!(elo | ehi) && !ABLATE(ablate, 2048)) continue;   // (2048, diagnostics: every lane adds)
                 const uint32_t nlo = kl_nonref(ylo), nhi = kl_nonref(yhi);
                 const int32_t ob = ob0 + 8 * (j + i);     // counter index of the unit's byte 0
-                if (!DEEP && NGSEP_KL_EXLOOP && !ABLATE(ablate, 512 | 1024 | 8192 | 16384)) {
-                    // one halfword add per exception (exceptions | other-allele << 8 at halfword ob + k): a lane's unit
-                    // rarely holds more than one, and the wave runs the loop as often as its busiest lane -- against
-                    // the 8-position byte-pair adds below, fewer instructions and LDS adds
-                    uint64_t ex = (uint64_t)elo | (uint64_t)ehi << 32;
-                    const uint64_t nr = (uint64_t)nlo | (uint64_t)nhi << 32;
-                    while (ex) {
-                        const int bit = __builtin_ctzll(ex);
-                        ex &= ex - 1ull;
-                        const int32_t hw = ob + (bit >> 3);
-                        atomicAdd(&s_cnt[hw >> 1], (1u + (((uint32_t)(nr >> bit) & 1u) << 8)) << ((hw & 1) << 4));
-                    }
-                } else if (!DEEP) {
+                if (!DEEP) {
                     // (exception, other-allele) byte pairs of the 8 positions, then shifted to the halfword
+                    // (measured and not kept: one halfword add per exception, the wave looping as often as its busiest
+                    // lane -- KL 0.460 against 0.399 ms on configs[2], r05ex)
                     const uint32_t fl = elo >> 7, fh = ehi >> 7, ml = nlo >> 7, mh = nhi >> 7;
                     const uint32_t w0 = __builtin_amdgcn_perm(ml, fl, 0x05010400u), w1 = __builtin_amdgcn_perm(ml, fl, 0x07030602u);
                     const uint32_t w2 = __builtin_amdgcn_perm(mh, fh, 0x05010400u), w3 = __builtin_amdgcn_perm(mh, fh, 0x07030602u);
@@ -1621,17 +1605,8 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
                     if (COUNT) {
                         uint64_t ex = (uint64_t)klm_exc(ylo) | (uint64_t)klm_exc(yhi) << 32;
                         if (ABLATE(gp.ablate, 65536)) { sink += (uint32_t)ex; ex = 0; }   // (diagnostics: no counters)
-#if NGSEP_KLM_EXLOOP
-                        // one byte add per exception (a lane's unit rarely holds more than one)
-                        const int32_t ob = ti0 - 24 + 8 * (j + i);
-                        while (ex) {
-                            const int bit = __builtin_ctzll(ex);
-                            ex &= ex - 1ull;
-                            const int32_t bi = ob + (bit >> 3);
-                            atomicAdd(cnt32 + (bi >> 2), 1u << ((bi & 3) << 3));
-                        }
-#endif
-                        if (ex) {
+                        if (ex) {                                  // (one byte add per exception instead: KLM 0.937
+                                                                   // against 0.825 ms on configs[4], r05kx)
                             const uint64_t one = ex >> 7;          // a 0 / 1 byte per position
                             const int32_t ob = ti0 - 24 + 8 * (j + i);
                             const int sh = 8 * (ob & 3);
