@@ -335,8 +335,13 @@ void decoder_loop_gpu(ngsep_bam* b) {
 // decoder thread: 32 MB of compressed blocks at a time, inflated on all host threads
 void decoder_loop(ngsep_bam* b) {
     if (b->gpu_inflate) return decoder_loop_gpu(b);
-    const size_t kRead = (size_t)32 << 20;
-    std::vector<uint8_t> comp, carry;
+    // (NGSEP_BGZF_READ: a smaller read, test hook -- blocks cut across reads on small files)
+    const char* rh = ngsep::env_hook("NGSEP_BGZF_READ");
+    const size_t kRead = rh ? std::max<size_t>((size_t)std::atoll(rh), 4096) : (size_t)32 << 20;
+    // the compressed bytes: one buffer reused read after read (never value-initialised -- a vector's resize zeroed 32 MB
+    // a read, 200 x 32 MB for a population's files), a block cut off by the read moved to its front
+    RawBuf<uint8_t> comp;
+    size_t have = 0;                                   // bytes of a cut block at comp's front
     bool file_eof = false;
     while (true) {
         {
@@ -345,22 +350,22 @@ void decoder_loop(ngsep_bam* b) {
             if (b->stop) break;
         }
         Chunk ch;
-        comp.swap(carry);
-        carry.clear();
+        size_t total = have;
         if (!file_eof) {
-            const size_t o = comp.size();
-            comp.resize(o + kRead);
-            const size_t got = std::fread(comp.data() + o, 1, kRead, b->f);
-            comp.resize(o + got);
+            comp.n = have;                             // (a growth keeps the cut block)
+            comp.resize(have + kRead);
+            const size_t got = std::fread(comp.data() + have, 1, kRead, b->f);
+            total += got;
             if (got < kRead) file_eof = true;
         }
         // whole blocks in comp: offsets and decoded sizes
         std::vector<size_t> boff, bclen;
         std::vector<uint32_t> bisize;
-        const size_t p = scan_bgzf(comp.data(), comp.size(), boff, bclen, bisize, ch.err);
-        if (ch.err.empty() && p < comp.size()) {
+        const size_t p = scan_bgzf(comp.data(), total, boff, bclen, bisize, ch.err);
+        size_t carry_n = 0;
+        if (ch.err.empty() && p < total) {
             if (file_eof && boff.empty()) ch.err = "truncated BGZF block";
-            carry.assign(comp.begin() + (ptrdiff_t)p, comp.end());
+            carry_n = total - p;
         }
         std::vector<size_t> dout(boff.size() + 1, 0);
         for (size_t k = 0; k < boff.size(); k++) dout[k + 1] = dout[k] + bisize[k];
@@ -382,7 +387,9 @@ void decoder_loop(ngsep_bam* b) {
         });
         b->t_inflate += std::chrono::duration<double>(std::chrono::steady_clock::now() - ti0).count();
         if (bad && ch.err.empty()) ch.err = "BGZF inflate failed";
-        ch.eof = file_eof && carry.empty();
+        if (carry_n) std::memmove(comp.data(), comp.data() + p, carry_n);   // (the inflate is done with comp)
+        have = carry_n;
+        ch.eof = file_eof && carry_n == 0;
         const bool last = ch.eof || !ch.err.empty();
         {
             std::lock_guard<std::mutex> lk(b->mu);

@@ -74,6 +74,22 @@ def test_reader_matches_generator(tmp_path, kw, batch_reads):
     assert got == want
 
 
+@pytest.mark.parametrize("read_bytes", ["4096", "100000", "1000003"])
+def test_reader_small_file_reads(tmp_path, monkeypatch, read_bytes):
+    """The decoder's file reads cut BGZF blocks (the cut block carried to the front of the reused buffer): every record
+    equal to the generator's whatever the read size (NGSEP_BGZF_READ, test hook; 32 MB otherwise)."""
+    monkeypatch.setenv("NGSEP_BGZF_READ", read_bytes)
+    syn = pysynth.Synth(genome=pysynth.YEAST, n_contigs=2, depth=10, seed=31, softclip_rate=0.05)
+    _, _, bam = syn.write(os.path.join(str(tmp_path), "r"))
+    lib, ctx = _ctx(syn.contigs())
+    got = _read_all(lib, ctx, bam, 50000)
+    want = _records(syn.batch())
+    lib.ngsep_close(ctx)
+    syn.close()
+    assert len(got) == len(want) > 1000
+    assert got == want
+
+
 def test_parallel_cut_merge_walks_missed_segments(tmp_path, monkeypatch):
     """A parallel-cut segment whose own walk never meets the true record chain is walked sequentially by the
     merge (NGSEP_PCUT_MISS: odd segments start off the chain): the records are the same."""
