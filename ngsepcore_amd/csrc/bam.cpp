@@ -173,6 +173,9 @@ struct ngsep_bam {
     int store_cur = 0;
     // inflate on the device (the context's GzDevice, borrowed while the reader is open), else on the host threads
     bool gpu_inflate = false;
+    // fill_batch's per record state (reused batch after batch)
+    struct Rec { int32_t keep, ncig, lseq, flags, rg, seq, first; };
+    RawBuf<Rec> rec_buf;
     // NGSEP_HOST_TIMING diagnostics: seconds in the decoder's inflate, the record cut, parse and emit
     double t_inflate = 0, t_wait = 0, t_need = 0, t_cut = 0, t_parse = 0, t_emit = 0;
     double t_read = 0, t_pin = 0;               // device inflate: the decoder's file reads, its pinned allocations
@@ -834,8 +837,12 @@ int fill_batch(ngsep_bam* b, ngsep_bam::BatchStore& B, int64_t max_reads, ngsep_
     const auto tc1 = std::chrono::steady_clock::now();
     // 2. per record: filters (isSameAlignment against the previous raw record, isMultiple, filter flags,
     //    malformed CIGAR / read length) and output sizes -- in parallel
-    struct Rec { int32_t keep, ncig, lseq, flags, rg, seq, first; };
-    std::vector<Rec> rec((size_t)n);
+    // (per record state in a buffer the reader keeps: no 14 MB zero fill a batch; every record's keep is written)
+    using Rec = ngsep_bam::Rec;
+    RawBuf<Rec>& recb = b->rec_buf;
+    recb.n = 0;
+    recb.resize((size_t)n);
+    Rec* rec = recb.data();
     const uint8_t* base = b->buf;
     auto name_of = [&](size_t o) { return std::make_pair((const char*)base + o + 32, (size_t)(base[o + 8] ? base[o + 8] - 1 : 0)); };
     parallel_for(n, 4096, [&](int64_t lo, int64_t hi) {

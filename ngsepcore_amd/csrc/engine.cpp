@@ -1571,7 +1571,7 @@ static int choose_tile(const std::vector<int32_t>& m16, int64_t g_len, std::vect
 //   * the position-major byte pile (KP): position p's rows_t codes at off_t + p * rows_t, rank order;
 //   * the strand bits (KP, countsStrand): bit off_t + p * rows_t + r = the rank-r read is reverse.
 // Tiles are independent: built on all host threads.
-static int build_single_layout(Staged& s, const HugeVec<SRead>& reads, LayoutArena& arena, bool exact) {
+static int build_single_layout(Staged& s, const RawVec<SRead>& reads, LayoutArena& arena, bool exact) {
     static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     auto lap = [t = std::chrono::steady_clock::now()](const char* what) mutable {
         if (!host_timing) return;
@@ -1729,7 +1729,7 @@ static inline void fill_group_units(uint64_t* dst, int32_t K, const uint8_t* con
 // device_units (streamed windows): the units are built on the device (kernels.hip k_build_units) from the reads'
 // projected bytes, copied here back to back into the arena (runs of reads adjacent in their projection chunk: one copy)
 // -- a copy instead of the 64-lane transposition with its reference XOR, which cost the window worker ~10 ms a window
-static int build_rg_layout(Staged& s, const HugeVec<SRead>& reads, LayoutArena& arena, bool exact,
+static int build_rg_layout(Staged& s, const RawVec<SRead>& reads, LayoutArena& arena, bool exact,
                            const std::function<void(int64_t)>& consumed = nullptr, bool device_units = false) {
     static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     const auto t0 = std::chrono::steady_clock::now();
@@ -2172,7 +2172,7 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs, bool relea
     if (!c->params.multisample) {
         // single sample: the reads' projected bytes go straight into the tile layout
         s.single = true;
-        HugeVec<SRead> reads((size_t)nreads);
+        RawVec<SRead> reads((size_t)nreads);
         int64_t ri = 0;
         for (size_t wi = 0; wi < s.windows.size(); wi++) {
             Window& w = s.windows[wi];

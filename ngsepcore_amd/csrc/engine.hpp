@@ -188,22 +188,6 @@ struct HostArray {
     void release() { std::free(p); p = nullptr; n = 0; }
 };
 
-// std::allocator with huge_alloc's pages: the admitted reads' arrays of a sequence (ContigReads)
-template <class T>
-struct HugeAllocator {
-    using value_type = T;
-    HugeAllocator() = default;
-    template <class U> HugeAllocator(const HugeAllocator<U>&) {}
-    T* allocate(size_t n) {
-        void* p = huge_alloc(n * sizeof(T));
-        if (!p) throw std::bad_alloc();
-        return static_cast<T*>(p);
-    }
-    void deallocate(T* p, size_t) { std::free(p); }
-    template <class U> bool operator==(const HugeAllocator<U>&) const { return true; }
-    template <class U> bool operator!=(const HugeAllocator<U>&) const { return false; }
-};
-template <class T> using HugeVec = std::vector<T, HugeAllocator<T>>;
 // huge_alloc's pages with the elements a resize adds left uninitialised: for arrays whose every element the caller
 // writes itself, on all threads (the serial zero fill of a value-initialising resize was ~0.3 s of the 200-sample
 // population layout's 1.2 GB of index arrays)
@@ -229,12 +213,12 @@ template <class T> using RawVec = std::vector<T, RawAllocator<T>>;
 struct ContigReads {
     int32_t seq_id = -1;
     int64_t seq_len = 0;               // the sequence's length
-    HugeVec<int32_t> first, last;
-    HugeVec<uint8_t> neg;              // 1 = negative strand
+    RawVec<int32_t> first, last;       // (resized, then written in full on all threads: no zero fill)
+    RawVec<uint8_t> neg;               // 1 = negative strand
     std::vector<uint8_t> uniq;         // coverage mode: 1 = ReadAlignment.isUnique (no FLAG_MULTIPLE_ALN)
     std::vector<int16_t> sample;       // multisample: sample of the read's group (-1 none)
     std::vector<uint8_t> rank;         // multisample: rank of the read group in its sample's set
-    HugeVec<const uint8_t*> bptr;      // the read's projected codes over [first, last]
+    RawVec<const uint8_t*> bptr;       // the read's projected codes over [first, last]
     std::vector<HostArray<uint8_t>> chunks;   // their storage: one uninitialised chunk per projected batch
     // indel-bearing admitted reads: [first, last + indel bases]; widened by the realigner's reach and merged
     // into `carved` when the sequence is staged (engine.cpp carve_indel_regions)
@@ -684,7 +668,7 @@ struct WindowJob {
     int32_t seq_id = -1;
     int64_t w0 = 0, w1 = 0;
     int32_t max_span = 1;
-    HugeVec<SRead> reads;                                   // global coordinates (window at pad)
+    RawVec<SRead> reads;                                    // global coordinates (window at pad)
     std::vector<std::pair<int64_t, int64_t>> carved;        // 1-based, inside [w0, w1]
     // the indel realigner's regions (whole inside the window, = carved) and their alignments; the listener's
     // lastIndelEnd before and after the window
