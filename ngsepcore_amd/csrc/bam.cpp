@@ -274,15 +274,25 @@ void decoder_loop_gpu(ngsep_bam* b) {
             cb.resize(tail_n + kRead + 256);
             if (tail_n) std::memmove(cb.data(), tail, tail_n);
             total = tail_n;
-            if (!file_eof) {
+            if (!file_eof && tail_n < kRead) {             // (the buffer holds kRead bytes at most: carries cannot pile up)
                 const auto tr = std::chrono::steady_clock::now();
-                const size_t got = std::fread(cb.data() + tail_n, 1, kRead, b->f);
+                const size_t want = kRead - tail_n;
+                const size_t got = std::fread(cb.data() + tail_n, 1, want, b->f);
                 b->t_read += std::chrono::duration<double>(std::chrono::steady_clock::now() - tr).count();
                 total += got;
-                if (got < kRead) file_eof = true;
+                if (got < want) file_eof = true;
             }
         }
-        const size_t p = ch.err.empty() ? scan_bgzf(cb.data(), total, boff, bclen, bisize, ch.err) : 0;
+        size_t p = ch.err.empty() ? scan_bgzf(cb.data(), total, boff, bclen, bisize, ch.err) : 0;
+        // at most one wave of KZ workgroups a batch (a batch a few blocks past it would take a second block latency):
+        // the blocks past it are carried to the next read
+        const size_t cap = (size_t)ngsep::gz_wave_blocks(c->gz);
+        if (ch.err.empty() && boff.size() > cap) {
+            p = boff[cap - 1] + bclen[cap - 1] + 8;
+            boff.resize(cap);
+            bclen.resize(cap);
+            bisize.resize(cap);
+        }
         if (ch.err.empty() && p < total && file_eof && boff.empty()) ch.err = "truncated BGZF block";
         tail = cb.data() + p;
         tail_n = ch.err.empty() ? total - p : 0;

@@ -876,6 +876,7 @@ int cov_run(CovDevice* d, int32_t max_cov, uint64_t* hist_out, double* kernel_ms
 struct GzDevice;
 GzDevice* gz_create(int ordinal, std::string& err);
 void gz_destroy(GzDevice* d);
+int gz_wave_blocks(const GzDevice* d);          // blocks a batch should hold at most (one wave of workgroups)
 void* gz_host_alloc(size_t n);                   // pinned host memory
 void gz_host_free(void* p);
 int gz_submit(GzDevice* d, int slot, const uint8_t* in, size_t in_n, const size_t* boff, const size_t* bclen,

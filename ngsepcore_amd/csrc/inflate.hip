@@ -4,16 +4,16 @@
 // htsjdk's BlockCompressedInputStream plays this role in the reference (ReadAlignmentFileReader.java:171-183 opens
 // the BAM through it); the reference inflates one 64 KB block at a time with java.util.zip.Inflater.  Here every
 // BGZF block of a 32 MB read of the file is one workgroup of one wavefront (KZ, k_inflate):
-//   - the block's output window lives in an LDS ring of 32 KB (DEFLATE's distance bound), so LZ77 copies never wait on
-//     memory, and leaves for HBM 16 KB at a time; ~40 KB of LDS a wavefront -> 4 wavefronts a CU, 1024 blocks in
-//     flight on the chip;
+//   - the block's last 16 KB of output live in an LDS ring, so most LZ77 copies never wait on memory (one from further
+//     back, DEFLATE's distances reach 32 KB, reads the flushed bytes from HBM), and leave for HBM 8 KB at a time; ~20 KB
+//     of LDS a wavefront -> 8 wavefronts a CU, 2048 blocks in flight on the chip;
 //   - the bit stream is decoded as scalar code (the bit buffer, table entries and lengths in SGPRs: the decode is serial
 //     by nature, and a vector decode costs 4 cycles an instruction for nothing), and the wavefront's 64 lanes split the
 //     parallel parts: a Huffman table build (ballot ranks), an LZ77 copy (up to 64 bytes per instruction), a stored
 //     block's copy and the 16-B flush of the finished block to HBM;
 //   - the input arrives 16 B at a time, one group ahead (the decode never waits on a load it could have issued
-//     earlier); Huffman codes of <= 10 bits (lit/len) / 8 bits (distance) take one LDS lookup, longer ones the
-//     canonical count walk.
+//     earlier); Huffman codes of <= 9 bits (lit/len) / 7 bits (distance) take one LDS lookup, longer ones the
+//     canonical walk from the 10th / 8th bit.
 // The kernel is latency-bound (a dependent LDS lookup per symbol), not HBM-bound: its algorithmic traffic is the
 // compressed bytes in plus the decoded bytes out, ~5.4 B per compressed byte on BAM data.
 #include <hip/hip_runtime.h>
@@ -26,8 +26,8 @@
 namespace ngsep {
 
 constexpr int kZThreads = 64;
-constexpr int kZLitBits = 10;                    // fast lit/len lookup bits
-constexpr int kZDistBits = 8;                    // fast distance lookup bits
+constexpr int kZLitBits = 9;                     // fast lit/len lookup bits
+constexpr int kZDistBits = 7;                    // fast distance lookup bits (the code-length code's 7 bits too)
 constexpr int kZOutMax = 65536;                  // BGZF ISIZE bound
 constexpr size_t kZInSlack = 256;                // readable bytes past a batch's input (the one-group-ahead loads)
 
@@ -61,23 +61,29 @@ __device__ __forceinline__ uint32_t z_dist_entry(uint32_t s, uint32_t len) {
     return len | (kZBad << 5);
 }
 
-// one Huffman code's decode state in LDS: the fast table and the canonical (count, symbols) of the slow walk
+// one Huffman code's canonical description in LDS (RFC 1951 3.2.2): per length its count, first code and first index
+// into the symbols sorted by (length, symbol) -- the walk for codes longer than the fast table
+template <int NSYM>
 struct ZHuff {
-    uint16_t count[16];
-    uint16_t sym[320];
+    uint16_t count[16], first[16], offs[16];
+    uint16_t sym[NSYM];
 };
 
-constexpr uint32_t kZRing = 32768;               // the output window in LDS (DEFLATE's 32 KB distance bound)
-constexpr uint32_t kZFlush = 16384;              // output bytes flushed to HBM at a time (half the ring)
+// the output window: the last 16 KB in an LDS ring, flushed to HBM 8 KB at a time; a copy from further back (DEFLATE
+// allows 32 KB) reads the flushed bytes from HBM.  ~20 KB of LDS a wavefront: 8 resident a CU.
+constexpr uint32_t kZRing = 16384;
+constexpr uint32_t kZFlush = 8192;
+static_assert(kZRing >= kZFlush + 2 * 258, "a copy never overwrites unflushed ring bytes");
 
 struct ZLds {
     uint8_t ring[kZRing];                        // output byte x of the block at ring[(x + (out_off & 15)) % kZRing]
     uint32_t lit[1 << kZLitBits];
-    uint32_t dist[1 << kZDistBits];
-    uint32_t clen[128];                          // the code-length code (<= 7 bits: no slow path)
-    ZHuff hl, hd;
+    uint32_t dist[1 << kZDistBits];              // (while a block's code lengths are read: the code-length code's table)
+    ZHuff<288> hl;
+    ZHuff<32> hd;                                // (the code-length code's 19 symbols first, then the distances')
     uint8_t lens[320];                           // code lengths being built (HLIT + HDIST <= 320)
 };
+static_assert(sizeof(ZLds) <= 20480, "8 wavefronts a CU");
 
 // wavefront-uniform values live in scalar registers: every LDS / memory value the decode branches on is read into
 // one (the decode is then scalar code; only the copies and the table builds use the lanes)
@@ -150,8 +156,8 @@ __device__ __forceinline__ uint64_t z_byte_pos(const ZBits& b) { return (uint64_
 // kZModeDist distance entries, kZModeRaw the symbol itself (bits 16-31; the code-length code).  Returns false for an
 // over-subscribed code.  Whole wavefront; the tables are read after its closing barrier.
 enum { kZModeRaw = 0, kZModeLit = 1, kZModeDist = 2 };
-template <int MODE>
-__device__ __attribute__((noinline)) bool z_build(const uint8_t* lens, int n, ZHuff& h, uint32_t* tab, int fb) {
+template <int MODE, class H>
+__device__ __attribute__((noinline)) bool z_build(const uint8_t* lens, int n, H& h, uint32_t* tab, int fb) {
     const int lane = (int)threadIdx.x;
     for (int i0 = 0; i0 < (1 << fb); i0 += kZThreads)
         if (i0 + lane < (1 << fb)) tab[i0 + lane] = 0;
@@ -182,6 +188,7 @@ __device__ __attribute__((noinline)) bool z_build(const uint8_t* lens, int n, ZH
         code = (code + c) << 1;
         off += c;
     }
+    if (lane > 0 && lane < 16) { h.first[lane] = (uint16_t)firstv; h.offs[lane] = (uint16_t)offv; }
     // ranks within a length (symbol order), codes, sorted symbols and fast entries
     uint32_t runv = 0;                                   // lane l: length-l symbols in earlier chunks
     const uint64_t lt = (((uint64_t)1) << lane) - 1;
@@ -212,25 +219,21 @@ __device__ __attribute__((noinline)) bool z_build(const uint8_t* lens, int n, ZH
     return ok;
 }
 
-// canonical walk for a code longer than the fast table (RFC 1951 3.2.2; the count / first-code decode): the symbol,
-// or -1 for a bit string that is no code; consumes its bits
-__device__ __forceinline__ int z_slow(ZBits& b, const ZHuff& h) {
-    int code = 0, first = 0, index = 0;
-    uint64_t bb = b.buf;
+// canonical walk for a code longer than the fast table's fb bits (no fast entry: its length is > fb): the code's bits
+// MSB first, length by length from fb + 1 against (first, count); the symbol, or -1 for a bit string that is no code;
+// consumes its bits
+template <class H>
+__device__ __forceinline__ int z_slow(ZBits& b, const H& h, int fb) {
+    uint32_t code = __brev((uint32_t)b.buf & ((1u << fb) - 1u)) >> (32 - fb);
 #pragma unroll 1
-    for (int l = 1; l < 16; l++) {
-        code |= (int)(bb & 1);
-        bb >>= 1;
-        const int c = (int)z_u(h.count[l]);
-        if (code - c < first) {
+    for (int l = fb + 1; l < 16; l++) {
+        code = (code << 1) | (uint32_t)((b.buf >> (l - 1)) & 1u);
+        const uint32_t c = z_u(h.count[l]), f = z_u(h.first[l]);
+        if (code - f < c) {
             b.buf >>= l;
             b.cnt -= l;
-            return (int)z_u(h.sym[index + (code - first)]);
+            return (int)z_u(h.sym[z_u(h.offs[l]) + code - f]);
         }
-        index += c;
-        first += c;
-        first <<= 1;
-        code <<= 1;
     }
     return -1;
 }
@@ -302,6 +305,7 @@ k_inflate(const uint8_t* __restrict__ in, uint64_t in_n, const ZBlock* __restric
                         z_flush(L, out, out_off, ab, flushed, flushed + kZFlush);
                         flushed += kZFlush;
                     }
+                    __threadfence_block();
                 }
                 pos += ln;
                 z_init(b, in, src + ln, lim);
@@ -331,13 +335,13 @@ k_inflate(const uint8_t* __restrict__ in, uint64_t in_n, const ZBlock* __restric
                 }
                 if (lane < hclen) L.lens[kZClenOrder[lane]] = (uint8_t)cl;
                 __syncthreads();
-                if (!z_u((uint32_t)z_build<kZModeRaw>(L.lens, 19, L.hd, L.clen, 7))) { bad = true; break; }
+                if (!z_u((uint32_t)z_build<kZModeRaw>(L.lens, 19, L.hd, L.dist, 7))) { bad = true; break; }
                 // the lit/len and distance lengths (run-length coded by the code-length code)
                 const int total = hlit + hdist;
                 int i = 0, prev = 0;
                 while (i < total) {
                     z_refill(b);
-                    const uint32_t e = z_u(L.clen[(uint32_t)b.buf & 127u]);
+                    const uint32_t e = z_u(L.dist[(uint32_t)b.buf & 127u]);
                     const int ln = (int)(e & 31);
                     if (ln == 0) { bad = true; break; }
                     b.buf >>= ln;
@@ -366,7 +370,7 @@ k_inflate(const uint8_t* __restrict__ in, uint64_t in_n, const ZBlock* __restric
                 z_refill(b);
                 uint32_t e = z_u(L.lit[(uint32_t)b.buf & ((1u << kZLitBits) - 1)]);
                 if ((e & 31) == 0) {
-                    const int s = z_slow(b, L.hl);
+                    const int s = z_slow(b, L.hl, kZLitBits);
                     if (s < 0) { bad = true; break; }
                     e = z_u(z_lit_entry((uint32_t)s, 0));
                 } else {
@@ -385,7 +389,7 @@ k_inflate(const uint8_t* __restrict__ in, uint64_t in_n, const ZBlock* __restric
                     z_refill(b);
                     uint32_t d = z_u(L.dist[(uint32_t)b.buf & ((1u << kZDistBits) - 1)]);
                     if ((d & 31) == 0) {
-                        const int s = z_slow(b, L.hd);
+                        const int s = z_slow(b, L.hd, kZDistBits);
                         if (s < 0) { bad = true; break; }
                         d = z_u(z_dist_entry((uint32_t)s, 0));
                     } else {
@@ -397,7 +401,13 @@ k_inflate(const uint8_t* __restrict__ in, uint64_t in_n, const ZBlock* __restric
                     if (dist > pos || pos + len > isize) { bad = true; break; }
                     // (uniform trip counts, the lanes past len idle: a lane-bounded loop would make the decode state
                     // look divergent to the compiler)
-                    if (dist >= len) {
+                    if (dist > kZRing) {                 // further back than the ring: the flushed bytes in HBM
+                        const uint8_t* src = out + out_off + pos - dist;
+                        for (uint32_t j0 = 0; j0 < len; j0 += kZThreads) {
+                            const uint32_t j = j0 + (uint32_t)lane;
+                            if (j < len) L.ring[(pos + j + ab) & M] = src[j];
+                        }
+                    } else if (dist >= len) {
                         for (uint32_t j0 = 0; j0 < len; j0 += kZThreads) {
                             const uint32_t j = j0 + (uint32_t)lane;
                             if (j < len) L.ring[(pos + j + ab) & M] = L.ring[(pos - dist + j + ab) & M];
@@ -414,6 +424,7 @@ k_inflate(const uint8_t* __restrict__ in, uint64_t in_n, const ZBlock* __restric
                     __syncthreads();
                     z_flush(L, out, out_off, ab, flushed, flushed + kZFlush);
                     flushed += kZFlush;
+                    __threadfence_block();               // (the flushed bytes visible to this wavefront's far copies)
                 }
             }
             __syncthreads();
@@ -449,6 +460,7 @@ struct GzSlot {
 };
 struct GzDevice {
     int ordinal = 0;
+    int wave_blocks = 2048;                      // KZ workgroups resident at once (CUs x workgroups a CU)
     GzSlot slot[2];
 };
 
@@ -481,6 +493,11 @@ GzDevice* gz_create(int ordinal, std::string& err) {
         }
     // (> 64 KB of dynamic LDS: a launch the runtime refuses is reported by gz_wait)
     (void)hipFuncSetAttribute((const void*)k_inflate, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ZLds));
+    hipDeviceProp_t prop;
+    int per_cu = 0;
+    if (hipGetDeviceProperties(&prop, ordinal) == hipSuccess && prop.multiProcessorCount > 0 &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_inflate, kZThreads, sizeof(ZLds)) == hipSuccess && per_cu > 0)
+        d->wave_blocks = prop.multiProcessorCount * per_cu;
     return d;
 }
 
@@ -498,6 +515,10 @@ void gz_destroy(GzDevice* d) {
     }
     delete d;
 }
+
+// BGZF blocks one KZ launch runs at once: a batch of at most this many takes one block's latency (a few more would
+// take two)
+int gz_wave_blocks(const GzDevice* d) { return d ? d->wave_blocks : 2048; }
 
 void* gz_host_alloc(size_t n) {
     void* p = nullptr;
