@@ -169,8 +169,14 @@ struct ngsep_bam {
         RawBuf<int64_t> b_cig_off, b_seq_off;
         RawBuf<uint8_t> b_hasq;
         RawBuf<char> b_bases, b_quals;
+        RawBuf<int64_t> b_qual_off;                // packed batches: the qualities' offsets in the chunk
     } store[2];
     int store_cur = 0;
+    // packed batches reference the decoded chunk in place: a chunk the reader leaves while filling batch j can still be
+    // read by batch j - 1 (admitted meanwhile), so it is recycled only when batch j + 1 starts (for_each_batch admits
+    // batch k while batch k + 1 is read, and k is done before k + 2 is read)
+    int64_t batch_seq = 0;
+    std::vector<std::pair<int64_t, RawBuf<uint8_t>>> retired;
     // inflate on the device (the context's GzDevice, borrowed while the reader is open), else on the host threads
     bool gpu_inflate = false;
     // fill_batch's per record state (reused batch after batch)
@@ -474,10 +480,7 @@ bool need(ngsep_bam* b, size_t n, std::string& err) {
             b->end = rem + ch.len;
             ch.mem = std::move(m);         // the consumed buffer (now in m) goes back to the pool below
         }
-        {
-            std::lock_guard<std::mutex> lk(b->mu);
-            if (ch.mem.cap && b->pool.size() < 6) b->pool.push_back(std::move(ch.mem));
-        }
+        if (ch.mem.cap) b->retired.emplace_back(b->batch_seq, std::move(ch.mem));   // (recycled by fill_batch)
         if (ch.eof) b->eof = true;
     }
     return true;
@@ -800,9 +803,12 @@ void parallel_cut(ngsep_bam* b, int64_t max_reads, size_t span, std::vector<size
 }
 
 // one batch of up to max_reads kept records into B (ngsep_bam_next_batch)
-int fill_batch(ngsep_bam* b, ngsep_bam::BatchStore& B, int64_t max_reads, ngsep_read_batch* out, bool* retry, bool packed) {
+// packed: BAM encoding read in place (bases = quals = the chunk, *qual_off = the qualities' offsets; PackedBatch)
+int fill_batch(ngsep_bam* b, ngsep_bam::BatchStore& B, int64_t max_reads, ngsep_read_batch* out, bool* retry, bool packed,
+               const int64_t** qual_off) {
     *retry = false;
     static const int kOp[9] = {3, 2, 1, 5, 6, 0, 4, 3, 7};   // BAM M I D N S H P = X -> NGSEP H0 D1 I2 M3 P4 N5 S6 X7
+
     static const char kNt[] = "=ACMGRSVTWYHKDBN";
     std::string err;
     // 1. cut up to max_reads whole records (their offsets in buf), sequentially along the block_size chain
@@ -1000,8 +1006,12 @@ int fill_batch(ngsep_bam* b, ngsep_bam::BatchStore& B, int64_t max_reads, ngsep_
     B.b_cig_off.resize((size_t)nk); B.b_cig_n.resize((size_t)nk); B.b_seq_off.resize((size_t)nk); B.b_seqlen.resize((size_t)nk);
     B.b_hasq.resize((size_t)nk);
     B.b_cigar.resize((size_t)cst[(size_t)nch].c);
-    B.b_bases.resize((size_t)cst[(size_t)nch].q);
-    B.b_quals.resize((size_t)cst[(size_t)nch].q);
+    if (packed) {
+        B.b_qual_off.resize((size_t)nk);
+    } else {
+        B.b_bases.resize((size_t)cst[(size_t)nch].q);
+        B.b_quals.resize((size_t)cst[(size_t)nch].q);
+    }
     parallel_for(nch, 1, [&](int64_t c0, int64_t c1) {
       for (int64_t c = c0; c < c1; c++) {
         Offs at = cst[(size_t)c];
@@ -1034,16 +1044,16 @@ int fill_batch(ngsep_bam* b, ngsep_bam::BatchStore& B, int64_t max_reads, ngsep_
                 if (nc > 0 && (cd[nc - 1] & 7) == nop) cd[nc - 1] += (int32_t)(v >> 4) * 8;
                 else cd[nc++] = (int32_t)(v >> 4) * 8 + nop;
             }
-            B.b_seq_off[k] = seq_at;
             B.b_seqlen[k] = l_seq;
-            char* bs = &B.b_bases[(size_t)seq_at];
-            char* qs = &B.b_quals[(size_t)seq_at];
             const bool hasq = l_seq > 0 && qual[0] != 0xFF;
             if (packed) {
-                // BAM's own encoding (ReadView::packed): the 4-bit bases and the raw qualities as they are
-                std::memcpy(bs, seq, (size_t)(l_seq + 1) / 2);
-                if (hasq) std::memcpy(qs, qual, (size_t)l_seq);
+                // BAM's own encoding (ReadView::packed): the 4-bit bases and the raw qualities where they are
+                B.b_seq_off[k] = (int64_t)(seq - base);
+                B.b_qual_off[k] = (int64_t)(qual - base);
             } else {
+                B.b_seq_off[k] = seq_at;
+                char* bs = &B.b_bases[(size_t)seq_at];
+                char* qs = &B.b_quals[(size_t)seq_at];
                 static const uint16_t* pair = [] {    // one byte of two bases -> their two characters
                     static uint16_t t[256];
                     for (int v = 0; v < 256; v++) t[v] = (uint16_t)((uint8_t)kNt[v >> 4] | ((uint16_t)(uint8_t)kNt[v & 15] << 8));
@@ -1072,8 +1082,9 @@ int fill_batch(ngsep_bam* b, ngsep_bam::BatchStore& B, int64_t max_reads, ngsep_
     out->cigar = B.b_cigar.data();
     out->seq_off = B.b_seq_off.data();
     out->seq_len = B.b_seqlen.data();
-    out->bases = B.b_bases.data();
-    out->quals = B.b_quals.data();
+    out->bases = packed ? reinterpret_cast<const char*>(base) : B.b_bases.data();
+    out->quals = packed ? reinterpret_cast<const char*>(base) : B.b_quals.data();
+    if (qual_off) *qual_off = packed ? B.b_qual_off.data() : nullptr;
     out->has_quals = B.b_hasq.data();
     // a batch with every record filtered is not the end of the file: the caller stops at n_reads == 0
     *retry = nk == 0 && n > 0;
@@ -1082,13 +1093,28 @@ int fill_batch(ngsep_bam* b, ngsep_bam::BatchStore& B, int64_t max_reads, ngsep_
 
 }  // namespace
 
-static int next_batch(ngsep_bam* b, int64_t max_reads, ngsep_read_batch* out, bool packed) {
+static int next_batch(ngsep_bam* b, int64_t max_reads, ngsep_read_batch* out, bool packed, const int64_t** qual_off = nullptr) {
     if (!b || !out) return NGSEP_E_INVALID;
     ngsep_bam::BatchStore& B = b->store[b->store_cur];
     b->store_cur ^= 1;
+    {   // this batch's number; the chunks left while reading an earlier batch go back to the decoder (the batch before
+        // this one is done: see ngsep_bam::retired)
+        const int64_t j = ++b->batch_seq;
+        std::lock_guard<std::mutex> lk(b->mu);
+        size_t w = 0;
+        for (size_t k = 0; k < b->retired.size(); k++) {
+            if (b->retired[k].first < j) {
+                if (b->pool.size() < 6) b->pool.push_back(std::move(b->retired[k].second));
+            } else {
+                if (w != k) b->retired[w] = std::move(b->retired[k]);
+                w++;
+            }
+        }
+        b->retired.resize(w);
+    }
     bool retry = true;
     int rc = NGSEP_OK;
-    while (retry && rc == NGSEP_OK) rc = fill_batch(b, B, max_reads, out, &retry, packed);
+    while (retry && rc == NGSEP_OK) rc = fill_batch(b, B, max_reads, out, &retry, packed, qual_off);
     return rc;
 }
 
@@ -1150,12 +1176,12 @@ namespace ngsep {
 template <class F>
 static int for_each_batch(ngsep_ctx* c, ngsep_bam* b, F&& fn) {
     // (BAM-encoded batches: bases and qualities are not re-encoded, ReadView::packed)
-    ngsep_read_batch batch[2];
+    ngsep::PackedBatch batch[2];
     int cur = 0;
-    int rc = next_batch(b, 1 << 20, &batch[0], true);
-    while (rc == NGSEP_OK && batch[cur].n_reads > 0 && !c->query_done) {
+    int rc = next_batch(b, 1 << 20, &batch[0].b, true, &batch[0].qual_off);
+    while (rc == NGSEP_OK && batch[cur].b.n_reads > 0 && !c->query_done) {
         int rc_next = NGSEP_OK;
-        std::thread th([&] { rc_next = next_batch(b, 1 << 20, &batch[cur ^ 1], true); });
+        std::thread th([&] { rc_next = next_batch(b, 1 << 20, &batch[cur ^ 1].b, true, &batch[cur ^ 1].qual_off); });
         rc = fn(batch[cur]);
         th.join();
         if (rc == NGSEP_OK) rc = rc_next;
@@ -1185,7 +1211,7 @@ int call_bam(ngsep_ctx* c, const char* bam_path, const char* out_vcf) {
     if (rc != NGSEP_OK) { ngsep_bam_close(b); return rc; }
     static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     const auto t0 = std::chrono::steady_clock::now();
-    rc = for_each_batch(c, b, [&](const ngsep_read_batch& batch) {
+    rc = for_each_batch(c, b, [&](const ngsep::PackedBatch& batch) {
         int r = process_alignments_packed(c, &batch);
         if (r == NGSEP_OK && !c->sites.empty()) r = ngsep_append_vcf_records(c, out_vcf);
         return r;
@@ -1215,7 +1241,7 @@ extern "C" int ngsep_coverage_bam(ngsep_ctx* c, const char* bam_path, const char
     ngsep_bam* b = nullptr;
     int rc = ngsep_bam_open(c, bam_path, &b);
     if (rc != NGSEP_OK) return rc;
-    rc = for_each_batch(c, b, [&](const ngsep_read_batch& batch) { return process_alignments_packed(c, &batch); });
+    rc = for_each_batch(c, b, [&](const ngsep::PackedBatch& batch) { return process_alignments_packed(c, &batch); });
     ngsep_bam_close(b);
     if (rc != NGSEP_OK) return rc;
     rc = ngsep_notify_end(c);
@@ -1231,7 +1257,7 @@ extern "C" int ngsep_rac_bam(ngsep_ctx* c, const char* bam_path, const char* out
     ngsep_bam* b = nullptr;
     int rc = ngsep_bam_open(c, bam_path, &b);
     if (rc != NGSEP_OK) return rc;
-    rc = for_each_batch(c, b, [&](const ngsep_read_batch& batch) { return process_alignments_packed(c, &batch); });
+    rc = for_each_batch(c, b, [&](const ngsep::PackedBatch& batch) { return process_alignments_packed(c, &batch); });
     ngsep_bam_close(b);
     if (rc != NGSEP_OK) return rc;
     rc = ngsep_notify_end(c);

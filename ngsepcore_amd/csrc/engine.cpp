@@ -490,7 +490,7 @@ static inline ReadView batch_view(const BatchRef& br, int32_t i) {
     r.quals = nullptr;
     if (sl > 0) {
         r.chars = b->bases + b->seq_off[i];
-        if (b->quals && (!b->has_quals || b->has_quals[i])) r.quals = b->quals + b->seq_off[i];
+        if (b->quals && (!b->has_quals || b->has_quals[i])) r.quals = b->quals + (br.qual_off ? br.qual_off[i] : b->seq_off[i]);
     }
     r.indel_len = br.indel[i];
     r.packed = br.packed;
@@ -1303,7 +1303,7 @@ static void admit_middle(ngsep_ctx* c, int64_t from, int64_t to) {
     c->stats.alignments_admitted += total;
 }
 
-static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed) {
+static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed, const int64_t* qual_off = nullptr) {
     if (!b || b->n_reads < 0) return set_error(c, NGSEP_E_INVALID, "null batch");
     const int nseq = (int)c->seq_names.size();
     int rc = NGSEP_OK;
@@ -1344,7 +1344,7 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed) {
             rlenp[i] = read_length;
         }
     });
-    c->cur_batch = BatchRef{b, lastp, indelp, packed};
+    c->cur_batch = BatchRef{b, lastp, indelp, packed, qual_off};
     int64_t n_in = 0;
     // the admission sweep (processAlignment + processSameStartAlns) over reads [from, to); false: stop the batch
     auto sweep = [&](int64_t from, int64_t to) -> bool {
@@ -3315,10 +3315,10 @@ extern "C" int ngsep_process_alignments(ngsep_ctx* c, const ngsep_read_batch* b)
 }
 
 namespace ngsep {
-int process_alignments_packed(ngsep_ctx* c, const ngsep_read_batch* b) {
-    if (!c) return NGSEP_E_INVALID;
+int process_alignments_packed(ngsep_ctx* c, const PackedBatch* b) {
+    if (!c || !b) return NGSEP_E_INVALID;
     c->staging_mode = false;
-    return process_batch(c, b, true);
+    return process_batch(c, &b->b, true, b->qual_off);
 }
 }  // namespace ngsep
 

@@ -256,6 +256,14 @@ struct BatchRef {
     const int32_t* last = nullptr;      // per read: reference end, indel bases (from the CIGAR)
     const int32_t* indel = nullptr;
     bool packed = false;
+    const int64_t* qual_off = nullptr;  // packed batches: the qualities' offsets (else seq_off)
+};
+// bam.cpp's BAM-encoded batches (ReadView::packed): bases and qualities read in place in the reader's decoded chunk
+// (bases = quals = its start, a record's 4-bit bases at seq_off[i], its qualities at qual_off[i]), valid until the
+// batch after next is read
+struct PackedBatch {
+    ngsep_read_batch b{};
+    const int64_t* qual_off = nullptr;
 };
 struct CarryStore {        // owned copies of the open same-start group's reads
     std::vector<int32_t> cigar;
@@ -812,7 +820,7 @@ namespace ngsep {
 // engine.cpp
 int set_error(ngsep_ctx* c, int code, const std::string& msg);
 // ngsep_process_alignments for a batch in BAM encoding (ReadView::packed; bam.cpp's call_bam)
-int process_alignments_packed(ngsep_ctx* c, const ngsep_read_batch* b);
+int process_alignments_packed(ngsep_ctx* c, const PackedBatch* b);
 void project_read(const ngsep_ctx* c, const ReadView& r, uint8_t* out);
 int stage_contig_reads(ngsep_ctx* c, ContigReads& cr, bool run_now);
 int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs, bool release_chunks);

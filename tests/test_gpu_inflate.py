@@ -4,7 +4,7 @@ The reference reads BAMs through htsjdk's BlockCompressedInputStream (ReadAlignm
 inflates with java.util.zip.Inflater; zlib is the same DEFLATE (RFC 1951), so the decoded bytes must be identical.
 The blocks below cover every DEFLATE block type and code path: stored blocks (level 0, incompressible data, the
 empty blocks of a sync flush), fixed Huffman codes (Z_FIXED), dynamic codes with literals only (Z_HUFFMAN_ONLY), run
-copies (Z_RLE, distance 1 overlapping copies), codes longer than the 10-bit fast table (skewed byte frequencies),
+copies (Z_RLE, distance 1 overlapping copies), codes longer than the 9-bit fast table (skewed byte frequencies),
 several deflate blocks in one BGZF block, the 65536-byte ISIZE bound and the empty EOF block.
 """
 import ctypes
@@ -150,6 +150,19 @@ def test_bam_reader_device_inflate_vcf_identical(tmp_path, monkeypatch, read_byt
         monkeypatch.setenv("NGSEP_BGZF_READ", read_bytes)
     dev, _ = gpu_vcf_bam(tmp_path, fa, bam, name="dev")
     assert open(host).read() == open(dev).read()
+
+
+@pytest.mark.parametrize("read_bytes", ["65536", "300000"])
+def test_bam_reader_small_reads_vcf_identical(tmp_path, monkeypatch, read_bytes):
+    """ngsep_call_bam (host inflate) with small file reads: many decoded chunks, the packed batches read in place from
+    them and the chunks recycled only once no batch can still read them -- the VCF of whole 32 MB reads."""
+    _, fa, _, bam = make_data(tmp_path, genome=pysynth.YEAST, n_contigs=2, contig_first=0, depth=25, seed=11,
+                              softclip_rate=0.05, dup_rate=0.02, noqual_rate=0.005)
+    monkeypatch.delenv("NGSEP_GPU_INFLATE", raising=False)
+    whole, _ = gpu_vcf_bam(tmp_path, fa, bam, name="whole")
+    monkeypatch.setenv("NGSEP_BGZF_READ", read_bytes)
+    small, _ = gpu_vcf_bam(tmp_path, fa, bam, name="small")
+    assert open(whole).read() == open(small).read()
 
 
 def test_bam_reader_device_inflate_region(tmp_path, monkeypatch):
