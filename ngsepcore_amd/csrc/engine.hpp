@@ -273,7 +273,8 @@ struct CarryStore {        // owned copies of the open same-start group's reads
 // Environment.  A release build reads only: the host thread count (NGSEP_THREADS, OMP_NUM_THREADS); timing switches
 // that add stderr lines or kernel events (NGSEP_HOST_TIMING, NGSEP_TIME_POSTERIOR); and test hooks that force an
 // equivalent code path whose output the tests compare with the default one (NGSEP_ZLIB, NGSEP_PCUT_MISS,
-// NGSEP_POP_STREAM, NGSEP_POP_ALL_BIG).  Tuning overrides and ablations (which may change launches or results) exist
+// NGSEP_POP_STREAM, NGSEP_POP_ALL_BIG, NGSEP_BGZF_READ, NGSEP_KPM_ONE_STAGE); NGSEP_GPU_INFLATE selects the device inflate
+// for the single-sample BAM readers (same bytes).  Tuning overrides and ablations (which may change launches or results) exist
 // only in diagnostic builds (make DIAG=1 defines NGSEP_DIAG): elsewhere diag_env is always null.
 inline const char* env_hook(const char* name) { return std::getenv(name); }
 #ifdef NGSEP_DIAG
