@@ -1268,6 +1268,11 @@ static void admit_middle(ngsep_ctx* c, int64_t from, int64_t to) {
     cr.last.resize(r0 + (size_t)total);
     cr.neg.resize(r0 + (size_t)total);
     c->to_project.resize(p0 + (size_t)total);
+    const bool ms = c->params.multisample != 0;          // (the read group's sample and rank, as admit_core)
+    if (ms) {
+        cr.sample.resize(r0 + (size_t)total);
+        cr.rank.resize(r0 + (size_t)total);
+    }
     parallel_for(nchunk, 1, [&](int64_t k0, int64_t k1) {
         for (int64_t k = k0; k < k1; k++) {
             Part& P = parts[(size_t)k];
@@ -1279,6 +1284,12 @@ static void admit_middle(ngsep_ctx* c, int64_t from, int64_t to) {
                 cr.last[r0 + o + j] = l;
                 cr.neg[r0 + o + j] = (b->flags[i] & 0x10) ? 1 : 0;
                 c->to_project[p0 + o + j] = i;
+                if (ms) {
+                    const int32_t rg = b->read_group ? b->read_group[i] : -1;
+                    const bool in = rg >= 0 && rg < (int32_t)c->rg_sample.size();
+                    cr.sample[r0 + o + j] = (int16_t)(in ? c->rg_sample[(size_t)rg] : -1);
+                    cr.rank[r0 + o + j] = (uint8_t)(in && c->rg_sample[(size_t)rg] >= 0 ? c->rg_rank[(size_t)rg] : 0);
+                }
                 const int64_t lo = std::max<int64_t>(f, 1), hi = std::min<int64_t>(l, len);
                 if (hi >= lo) {
                     if (lo > m) P.covered += hi - lo + 1;
@@ -1433,7 +1444,9 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed, c
     // (admit_middle); its first group (which may continue the carried one) and its last (left open) go through the
     // sweep.  Only for a sorted batch of the current sequence whose reads all carry their characters' length.
     int64_t g1 = 0, gL = 0;
-    if (streaming(c) && !c->params.query_seq[0] && b->n_reads >= (1 << 16) && c->cur_seq >= 0 &&
+    // (single-sample streamed runs and MultisampleVariantsDetector's merged batches)
+    const bool middle_ok = streaming(c) || (c->params.multisample && !c->staging_mode && !c->params.coverage_stats);
+    if (middle_ok && !c->params.query_seq[0] && b->n_reads >= (1 << 16) && c->cur_seq >= 0 &&
         b->seq_id[0] == c->cur_seq && b->first[0] >= c->last_start) {
         const int64_t n = b->n_reads;
         std::atomic<bool> bad{false};
