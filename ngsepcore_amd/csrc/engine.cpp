@@ -2068,8 +2068,8 @@ static int build_pop_rg_layout(Staged& s, LayoutArena& arena) {
     s.pblk_shift = shift;
     const int64_t nb = (s.g_len >> shift) + 2;
     s.pnblk = nb;
-    s.h_blkA.assign((size_t)(nb * nst), 0);
-    s.h_blkB.assign((size_t)(nb * nst), 0);
+    s.h_blkA.resize((size_t)(nb * nst));               // (every entry written below)
+    s.h_blkB.resize((size_t)(nb * nst));
     const int64_t ms = s.max_span;
     parallel_for(nst, 1, [&](int64_t a, int64_t b) {
         for (int64_t st = a; st < b; st++) {
@@ -2347,8 +2347,8 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs, bool relea
     std::vector<int32_t>().swap(s.h_loff);
     decltype(s.h_rh)().swap(s.h_rh);
     std::vector<RGroup>().swap(s.h_grp);
-    std::vector<int32_t>().swap(s.h_blkA);
-    std::vector<int32_t>().swap(s.h_blkB);
+    RawVec<int32_t>().swap(s.h_blkA);
+    RawVec<int32_t>().swap(s.h_blkB);
     s.h_units = nullptr;
     std::vector<int32_t>().swap(s.h_samp_st);
     std::vector<int64_t>().swap(s.h_st_end);

@@ -632,7 +632,7 @@ struct Staged {            // everything resident for one run
     std::vector<int64_t> h_zero;
     RawVec<int32_t> h_rh;               // 2 per entry (every one written by the layout builders)
     std::vector<RGroup> h_grp;
-    std::vector<int32_t> h_blkA, h_blkB;
+    RawVec<int32_t> h_blkA, h_blkB;     // (written in full by the layout builders)
     // -knownVariants: the run genotypes these sites (KP queue entries {global position, code}: code =
     // 0x80 | ref << 5 | alt << 8 | 0x400) instead of scanning; counters preset to their number
     bool known = false;
