@@ -19,3 +19,13 @@ print("$mode population e2e %.3f s" % d["end_to_end"]["wall_s"])
 PY
   grep -E "population: open |merge \+ sweep|end of alignments" gpurun_out/${TAG}_$mode.err | tail -3
 done
+for mode in thp nothp; do
+  if [ $mode = nothp ]; then export NGSEP_NO_THP=1; else unset NGSEP_NO_THP; fi
+  NGSEP_LIB_PATH=$D timeout -k 10 400 python -u bench.py --no-cold --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/${TAG}_c$mode.json 2> gpurun_out/${TAG}_c$mode.err || { tail -20 gpurun_out/${TAG}_c$mode.err; exit 1; }
+  python - <<PY
+import json
+d = json.loads(open("gpurun_out/${TAG}_c$mode.json").read().strip().splitlines()[-1])
+e = d["end_to_end"]
+print("$mode chr20 e2e %.3f s" % e["wall_s"], "indel %.3f s" % e["indels"]["wall_s"])
+PY
+done
