@@ -21,11 +21,14 @@ Beside the resident rate the line carries:
   * cpu_baseline -- the oracle (C restatement of the reference, SAM -> VCF) on a bounded sample of the
                   same workload, single-thread and one process per core.
 
---gpus N > 1: one process per GPU (spawned here under torch.distributed.run when WORLD_SIZE is unset),
-by default BASELINE.json configs[3]: the GRCh38 sequences (30x) split over the ranks by
-sharding.assign_contigs, each rank generating and calling only its own sequences, no data-path collective
-(the genome is fixed: "strong").  --config chr20 with --gpus N: each rank its own chr20-sized genome (seed
-3 + rank, "weak").  --config wgs with one process: --wgs-shard picks one GPU's shard of the 8-way split.
+--gpus N > 1: one process per GPU (spawned here under torch.distributed.run when WORLD_SIZE is unset), the same
+workload per GPU as at N = 1 (the default chr20: each rank its own chr20-sized genome, seed 3 + rank -- independent
+genomic windows, no data-path collective, "weak"), so the 1/2/4/8 values divide: value = every rank's positions x
+steps / the slowest rank's time.  At N > 1 the line also carries the CPU baseline (rank 0, before any GPU call), the
+end-to-end leg on every rank (its own BAM -> VCF, slowest rank, positions summed) and a strong-scaling leg
+(sharded_end_to_end: ONE chr20 BAM cut into exact windows over the ranks).  --config wgs: BASELINE.json configs[3],
+the GRCh38 sequences (30x) split over the ranks by sharding.assign_contigs (the genome is fixed: "strong"; at N = 1
+the whole genome on one GPU, --wgs-shard picks one GPU's shard of an 8-way split).
 --config yeast: configs[1].  --config multisample: configs[4] (one GPU's contig shard of the 200-sample
 population).  --config coverage: CoverageStats on yeast 30x.
 
@@ -58,14 +61,21 @@ def log(*a):
 
 
 def cpu_cores() -> int:
-    """The CPU share this job may use: OMP_NUM_THREADS on the GPU box (16), else the affinity mask."""
-    v = os.environ.get("OMP_NUM_THREADS")
+    """The CPU share of this process (the same rule as the library's host_threads(), engine.hpp): NGSEP_THREADS; else
+    the affinity mask divided among the node's ranks (LOCAL_WORLD_SIZE), at most OMP_NUM_THREADS when that is above 1
+    (the GPU box's share, 16; torch.distributed.run's default of 1 is not a share)."""
+    v = os.environ.get("NGSEP_THREADS")
     if v and v.isdigit() and int(v) > 0:
-        return int(v)
+        return min(int(v), 64)
     try:
-        return len(os.sched_getaffinity(0))
+        cores = len(os.sched_getaffinity(0))
     except AttributeError:
-        return os.cpu_count() or 1
+        cores = os.cpu_count() or 1
+    share = max(1, cores // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1)))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 1:
+        share = min(share, int(omp))
+    return min(share, 64)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -287,11 +297,12 @@ def sharded_end_to_end(args, dist, rank, local_rank, backend):
     if rank == 0:
         n_rec = sum(1 for l in open(os.path.join(tmp, "sharded.vcf")) if not l.startswith("#"))
         w = float(mx[0])
-        out = {"wall_s": w, "value": seq_len / w, "unit": "bp/s", "sequence_bp": seq_len, "vcf_records": n_rec,
+        out = {"wall_s": w, "value": seq_len / w, "unit": "positions/s", "sequence_bp": seq_len, "vcf_records": n_rec,
                "windows": int(sm[0]), "region_positions": int(sm[1]), "bam_bytes": os.path.getsize(bam),
                "note": f"sharding.call_bam_sharded over {dist.get_world_size()} ranks: chr20 30x BAM on local disk -> "
                        "merged VCF, 4 Mb windows cut by ngsep_clean_cut from the process group's shared queue, BAI region "
-                       "reads; region_positions counts the windows' lead-ins too; host threads per rank "
+                       "reads (strong scaling: one sequence over the ranks); value = the sequence's positions (every one "
+                       "covered at 30x) / wall; region_positions counts the windows' lead-ins too; host threads per rank "
                        f"{os.environ.get('NGSEP_THREADS') or cpu_cores()}"}
         shutil.rmtree(tmp, ignore_errors=True)
     return out
@@ -348,6 +359,12 @@ def spawn_ranks(args) -> int:
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    if "OMP_NUM_THREADS" not in env:                   # (torch.distributed.run would set 1 for every rank)
+        try:
+            cores = len(os.sched_getaffinity(0))
+        except AttributeError:
+            cores = os.cpu_count() or 1
+        env["OMP_NUM_THREADS"] = str(max(1, cores // args.gpus))
     return subprocess.call(cmd, env=env)
 
 
@@ -358,8 +375,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--depth", type=float, default=30.0)
-    ap.add_argument("--config", default=None, choices=["chr20", "yeast", "wgs", "multisample", "coverage"],
-                    help="default: chr20 (configs[2]) on one GPU, wgs (configs[3], the contig split) on several")
+    ap.add_argument("--config", default="chr20", choices=["chr20", "yeast", "wgs", "multisample", "coverage"],
+                    help="default: chr20 (configs[2]) per GPU at every --gpus N (weak scaling); wgs: configs[3] split "
+                         "over the GPUs (strong)")
     ap.add_argument("--no-cold", action="store_true", help="skip the cache-flushed passes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the BAM -> VCF end-to-end run")
@@ -372,8 +390,6 @@ def main():
                          "--wgs-shard picks the shard this GPU calls (one GPU's part of the 8-GPU split)")
     ap.add_argument("--wgs-shard", type=int, default=-1, help="wgs: the shard to call (default: the rank)")
     args = ap.parse_args()
-    if args.config is None:
-        args.config = "wgs" if args.gpus > 1 else "chr20"
     if args.config == "multisample" and args.depth == 30.0:
         args.depth = 10.0
 
@@ -389,9 +405,10 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     multi = args.config == "multisample"
 
-    # the CPU baseline runs first, before this process touches the GPU (its oracle pool is child processes)
+    # the CPU baseline runs first, before this process touches the GPU (its oracle pool is child processes); at N > 1
+    # on rank 0 only, while the other ranks wait in the process group's rendezvous below
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         try:
             t = time.time()
             if multi:
@@ -513,7 +530,7 @@ def main():
             t_stage += time.time() - ts
             if item is not None:
                 log(f"[rank {rank}] staged {human[item][0]} (device run {gi + 1} of {len(groups)})")
-            if args.config == "chr20" and rank == 0 and world == 1 and not args.no_e2e:
+            if args.config == "chr20" and not args.no_e2e:
                 # the same reads as a BAM on local disk for the end-to-end run
                 tmp = tempfile.mkdtemp(prefix="ngsep_e2e_")
                 tw = time.time()
@@ -523,14 +540,15 @@ def main():
                 pysynth.lib().ngs_synth_write_bam(syn.h, bam.encode())
                 e2e_src = (tmp, fa, bam)
                 # the same sequence with indels (rate 1e-4 per position) for the end-to-end run with the indel
-                # realigner (its own BAM and FASTA; generated and written untimed)
-                isyn = pysynth.Synth(genome=pysynth.HUMAN, depth=args.depth, seed=3 + rank, contig_first=HUMAN_CHR20,
+                # realigner (its own BAM and FASTA; generated and written untimed; one process only)
+                isyn = None if world > 1 else pysynth.Synth(genome=pysynth.HUMAN, depth=args.depth, seed=3 + rank, contig_first=HUMAN_CHR20,
                                      n_contigs=1, rng_per_contig=1, indel_rate=1e-4)
-                e2e_indel_src = (os.path.join(tmp, "chr20_indels.fa"), os.path.join(tmp, "chr20_indels.bam"))
-                pysynth.lib().ngs_synth_write_fasta(isyn.h, e2e_indel_src[0].encode())
-                pysynth.lib().ngs_synth_write_bam(isyn.h, e2e_indel_src[1].encode())
-                isyn.close()
-                log(f"[rank 0] wrote the end-to-end BAM ({os.path.getsize(bam) / 1e9:.2f} GB) in {time.time() - tw:.1f}s")
+                if isyn is not None:
+                    e2e_indel_src = (os.path.join(tmp, "chr20_indels.fa"), os.path.join(tmp, "chr20_indels.bam"))
+                    pysynth.lib().ngs_synth_write_fasta(isyn.h, e2e_indel_src[0].encode())
+                    pysynth.lib().ngs_synth_write_bam(isyn.h, e2e_indel_src[1].encode())
+                    isyn.close()
+                log(f"[rank {rank}] wrote the end-to-end BAM ({os.path.getsize(bam) / 1e9:.2f} GB) in {time.time() - tw:.1f}s")
             if multi and rank == 0 and world == 1 and not args.no_e2e:
                 # the same population as one BAM per sample on local disk for the end-to-end run
                 tmp = tempfile.mkdtemp(prefix="ngsep_e2e_")
@@ -665,13 +683,34 @@ def main():
         except Exception as e:
             e2e = {"value": None, "error": str(e)}
 
+    sharded = None
+    if dist is not None and e2e is not None and args.config == "chr20":
+        # every rank its own BAM -> VCF (the N = 1 leg per GPU): the slowest rank's wall, positions summed
+        import torch
+        ok = e2e.get("value") is not None
+        t = torch.tensor([e2e.get("wall_s", 0.0) if ok else 0.0, float(e2e.get("positions", 0) if ok else 0), 0.0 if ok else 1.0],
+                         dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        mx = t[:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = t[1:].clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        if rank == 0:
+            if float(sm[1]) > 0:
+                e2e = {"value": None, "error": f"{int(sm[1])} rank(s) failed the end-to-end leg", "rank0": e2e}
+            else:
+                e2e = dict(e2e, wall_s=float(mx[0]), positions=int(sm[0]), value=float(sm[0]) / float(mx[0]),
+                           rank0_wall_s=e2e["wall_s"],
+                           note=e2e["note"] + f"; every rank its own chr20 BAM (seed 3 + rank): the slowest rank's wall, "
+                                              f"positions summed over {world} ranks")
     if dist is not None and not args.no_e2e and args.config in ("wgs", "chr20"):
         try:
-            e2e = sharded_end_to_end(args, dist, rank, local_rank, backend)
+            sharded = sharded_end_to_end(args, dist, rank, local_rank, backend)
             if rank == 0:
-                log(f"[rank 0] sharded end-to-end over {world} ranks: {e2e['wall_s']:.2f}s, {e2e['windows']} windows")
+                log(f"[rank 0] sharded end-to-end over {world} ranks: {sharded['wall_s']:.2f}s, {sharded['windows']} windows")
         except Exception as ex:
-            e2e = {"value": None, "error": str(ex)}
+            sharded = {"value": None, "error": str(ex)}
+        if args.config == "wgs":
+            e2e, sharded = sharded, None
     if dist is not None:
         import torch
         t = torch.tensor([elapsed, float(positions)], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
@@ -704,7 +743,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / steps,
             "higher_is_better": True,
-            "scaling": "strong" if (args.config == "wgs" and world > 1) else "weak",
+            "scaling": "strong" if args.config == "wgs" else "weak",
             "vs_baseline": None,
             "dtype": "u8,f64",
             "data": ("synthetic (seeded generator, SURVEY.md 8(d)); " +
@@ -754,6 +793,8 @@ def main():
             line["config"]["sample_calls_per_step"] = int(sites_called) * args.samples
         if e2e is not None:
             line["end_to_end"] = e2e
+        if sharded is not None:
+            line["sharded_end_to_end"] = sharded
         if cpu is not None:
             line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)

@@ -230,9 +230,10 @@ size_t scan_bgzf(const uint8_t* comp, size_t n, std::vector<size_t>& boff, std::
 // inflated by KZ into a pinned chunk; two reads in flight (the file read of one overlaps the copies and kernel of the
 // previous), the chunk handed over when its batch is done
 void decoder_loop_gpu(ngsep_bam* b) {
-    // (NGSEP_BGZF_READ: a smaller read, test hook -- many batches and blocks cut across reads on small files)
+    // (NGSEP_BGZF_READ: a smaller read, test hook -- many batches and blocks cut across reads on small files; never
+    // below one whole BGZF block, 64 KB + its header: this buffer holds at most kRead bytes and must fit a block)
     const char* rh = ngsep::env_hook("NGSEP_BGZF_READ");
-    const size_t kRead = rh ? std::max<size_t>((size_t)std::atoll(rh), 4096) : (size_t)32 << 20;
+    const size_t kRead = rh ? std::max<size_t>((size_t)std::atoll(rh), (size_t)65536 + 256) : (size_t)32 << 20;
     ngsep_ctx* c = b->ctx;
     RawBuf<uint8_t> comp[2];
     for (int i = 0; i < 2; i++) {

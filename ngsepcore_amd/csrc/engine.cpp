@@ -531,6 +531,7 @@ static void project_pending(ngsep_ctx* c) {
     cr.bptr.resize(b0 + n);
     for (size_t i = 0; i < n; i++) cr.bptr[b0 + i] = base + off[i];
     cr.chunk_end.push_back(b0 + n);
+    cr.chunk_used.push_back(off[n]);
     cr.chunk_maxlast.push_back(maxlast);
     static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
     const auto t1 = std::chrono::steady_clock::now();
@@ -2089,7 +2090,10 @@ static int build_pop_rg_layout(Staged& s, LayoutArena& arena) {
     // the most reads of one sample covering one position (KPM gathers each sample's column into a slot of this many
     // codes): a sweep over the sample's read starts and ends, all its streams together (a bound from the longest span
     // in the run would let one long alignment inflate every sample's slot)
+    // A sample deeper than kKlmCountMaxCov somewhere also lists the KLM tiles where it is (the maximum over a tile is the
+    // coverage at its first position or at one of the starts inside it): those tiles take KLM's exact-bound scan
     std::vector<int32_t> sbound((size_t)S + 1, 0);
+    std::vector<std::vector<int32_t>> sdeep((size_t)S);
     parallel_for(S + 1, 1, [&](int64_t a, int64_t b) {
         std::vector<int32_t> starts, ends;
         for (int64_t sm = a; sm < b; sm++) {
@@ -2111,11 +2115,30 @@ static int build_pop_rg_layout(Staged& s, LayoutArena& arena) {
                 mc = std::max<int32_t>(mc, (int32_t)(i + 1 - j));
             }
             sbound[(size_t)sm] = mc;
+            if (mc <= kKlmCountMaxCov || sm == S) continue;       // (the reads of no sample are not scanned by KLM)
+            const size_t n = starts.size();
+            size_t ia = 0, ja = 0, ib = 0, jb = 0;
+            for (int64_t t = starts[0] / kKlmTile, t1 = ends[n - 1] / kKlmTile; t <= t1; t++) {
+                const int64_t T = t * kKlmTile, Tn = T + kKlmTile;
+                while (ia < n && starts[ia] <= T) ia++;
+                while (ja < n && ends[ja] < T) ja++;
+                int64_t m = (int64_t)ia - (int64_t)ja;                 // coverage at the tile's first position
+                for (; ib < n && starts[ib] < Tn; ib++) {
+                    if (starts[ib] < T) continue;
+                    while (jb < n && ends[jb] < starts[ib]) jb++;
+                    m = std::max<int64_t>(m, (int64_t)(ib + 1) - (int64_t)jb);
+                }
+                if (m > kKlmCountMaxCov) sdeep[(size_t)sm].push_back((int32_t)t);
+            }
         }
     });
     int32_t stride = 0;
     for (int sm = 0; sm <= S; sm++) stride = std::max(stride, sbound[(size_t)sm]);
     s.max_cov = (stride + 3) / 4 * 4;
+    s.h_deep_tiles.clear();
+    for (const auto& v : sdeep) s.h_deep_tiles.insert(s.h_deep_tiles.end(), v.begin(), v.end());
+    std::sort(s.h_deep_tiles.begin(), s.h_deep_tiles.end());
+    s.h_deep_tiles.erase(std::unique(s.h_deep_tiles.begin(), s.h_deep_tiles.end()), s.h_deep_tiles.end());
     s.prg = true;
     s.tile = kKlmTile;
     s.n_tiles = s.g_len / kKlmTile;
@@ -2238,10 +2261,13 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs, bool relea
         {
             int64_t at = 0;
             for (size_t ci = 0; ci < contigs.size(); ci++)
-                for (const HostArray<uint8_t>& ch : contigs[ci].chunks) {
+                for (size_t k = 0; k < contigs[ci].chunks.size(); k++) {
+                    // only the bytes the chunk holds (a pooled chunk can be much larger than its batch)
+                    const HostArray<uint8_t>& ch = contigs[ci].chunks[k];
+                    const int64_t used = k < contigs[ci].chunk_used.size() ? contigs[ci].chunk_used[k] : (int64_t)ch.n;
                     cdev[ci].push_back(at);
-                    s.h_chunks.push_back({ch.p, (int64_t)ch.n});
-                    at += (int64_t)ch.n;
+                    s.h_chunks.push_back({ch.p, used});
+                    at += used;
                 }
         }
         std::vector<int64_t> wbase(s.windows.size() + 1, 0);
@@ -2310,10 +2336,6 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs, bool relea
         const int lr = build_pop_rg_layout(s, c->arena);
         if (lr == -2) return set_error(c, NGSEP_E_DEVICE, "host memory for the population layout could not be allocated");
         if (lr != 0) return set_error(c, NGSEP_E_INVALID, "internal error: population layout");
-        if ((int64_t)s.max_cov * (s.n_samples + 1) > kPopGatherCap)
-            return set_error(c, NGSEP_E_UNSUPPORTED, "a sample's pileup is deeper than the population kernel's columns hold (" +
-                             std::to_string(kPopGatherCap / (s.n_samples + 1)) + " alignments per sample at " +
-                             std::to_string(s.n_samples) + " samples)");
         c->stats.slot_bytes = 0;
         c->stats.slot_size = 0;                  // (no fixed-size slots: the site-major pile is sized per tile)
     }
@@ -2354,7 +2376,8 @@ int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs, bool relea
     std::vector<int32_t>().swap(s.h_samp_st);
     std::vector<int64_t>().swap(s.h_st_end);
     s.h_ppile.reset();
-    std::vector<uint16_t>().swap(s.h_prow);
+    std::vector<int32_t>().swap(s.h_prow);
+    std::vector<int32_t>().swap(s.h_deep_tiles);
     std::vector<int64_t>().swap(s.h_pboff);
     // one-shot runs give the pinned layout buffers back (streamed windows keep theirs)
     s.h_planes = nullptr;
@@ -2432,7 +2455,7 @@ static void run_window_job(ngsep_ctx* c, WindowJob* j) {
     }
     const auto h2 = std::chrono::steady_clock::now();
     c->stats.read_bases += nb;
-    c->stats.pile_bytes = s.rg || s.prg ? s.n_units * 8 : s.pile_bytes;
+    c->stats.pile_bytes += s.rg || s.prg ? s.n_units * 8 : s.pile_bytes;   // (summed over the streamed windows)
     c->stats.tile_positions = s.tile;
     c->stats.tile_rows_max = std::max(c->stats.tile_rows_max, s.tile_rows_max);
     c->stats.global_positions += s.g_len;
@@ -2723,9 +2746,8 @@ static int run_population_regions(ngsep_ctx* c, const ContigReads& cr, size_t fr
             for (int s1 = 0; s1 < S1; s1++) {
                 const uint8_t* p;
                 const uint32_t n = col(v, s1, &p);
-                if (n > 65535) return set_error(c, NGSEP_E_UNSUPPORTED, "more than 65535 calls of one sample at one position");
-                uint16_t& r = rs.h_prow[(size_t)(v / kPopTile) * S1 + s1];
-                r = std::max<uint16_t>(r, (uint16_t)n);
+                int32_t& r = rs.h_prow[(size_t)(v / kPopTile) * S1 + s1];
+                r = std::max<int32_t>(r, (int32_t)n);
             }
         rs.h_pboff.assign((size_t)ntile * S1 + 1, 0);
         std::vector<int64_t> stride((size_t)ntile, 0);

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <sched.h>
 #include <thread>
 #include <vector>
 #include <atomic>
@@ -82,7 +83,9 @@ constexpr int kKlmSlots = 96;              // KLM: candidate columns a sample ti
 constexpr int kKlmQs = 10;                 // KLM's count bound counts the reference calls of quality >= kKlmQs
 constexpr int kKlmCountMaxCov = 127;       // ... when no sample is deeper than this (its byte counters cannot carry)
 constexpr int kPopGatherCap = 40960;       // KPM (gather): LDS bytes for one position's columns ((S + 1) x the per-sample bound);
-                                           // with KPM's 21 KB of static LDS, within the 64 KB a workgroup is given
+                                           // with KPM's 21 KB of static LDS, within the 64 KB a workgroup is given.  Deeper
+                                           // populations gather into a device scratch buffer instead (kernels.hip, GCOL)
+constexpr int64_t kPopGcolBudget = (int64_t)1 << 30;   // ... of at most this many bytes (fewer KPM workgroups past it)
 
 // the (first) alternative allele of a record as a DNA index: a pool record keeps its variant's alleles in
 // the mask bits (ngsep_site_out.pool), an SNVQ record in .alt
@@ -99,7 +102,6 @@ static_assert(sizeof(ngsep_site_out) == 152, "site record layout");
 static_assert(sizeof(ngsep_sample_call) == 76, "sample call layout");
 static_assert(sizeof(ngsep_popsite_out) == 20, "population site layout");
 constexpr int kMaxSamplesDevice = 255;     // samples genotyped by one workgroup (one thread each, one for reads of no sample)
-constexpr int kPopListCap = 8192;          // reads covering one position in the population kernel (LDS, twice)
 
 // Likelihood addends for the SNV model with n=4 alleles and f=g=250
 // (CountsHelper.java:147-185 with heterozygousProportion 0.5, SingleSampleVariantPileupListener.java:236)
@@ -225,13 +227,14 @@ struct ContigReads {
     std::vector<std::pair<int32_t, int32_t>> indel_reads;
     std::vector<std::pair<int32_t, int32_t>> carved;
     std::vector<size_t> chunk_end;     // reads [chunk_end[k-1], chunk_end[k]) have their bytes in chunks[k]
+    std::vector<int64_t> chunk_used;   // the bytes chunks[k] holds (a pooled chunk may be larger)
     std::vector<int32_t> chunk_maxlast;   // their largest last position (streamed windows release the chunk after)
     int32_t max_span = 0;
     int64_t covered = 0;               // union of [first,last] (positions with a pileup)
     int32_t cov_last = 0;              // running max of last (for `covered`)
     void clear() {
         first.clear(); last.clear(); neg.clear(); uniq.clear(); sample.clear(); rank.clear(); bptr.clear(); chunks.clear();
-        indel_reads.clear(); carved.clear(); chunk_end.clear(); chunk_maxlast.clear();
+        indel_reads.clear(); carved.clear(); chunk_end.clear(); chunk_used.clear(); chunk_maxlast.clear();
         max_span = 0; covered = 0; cov_last = 0; seq_id = -1;
     }
 };
@@ -283,12 +286,20 @@ inline const char* diag_env(const char* name) { return std::getenv(name); }
 inline const char* diag_env(const char*) { return nullptr; }
 #endif
 
-// host worker threads: NGSEP_THREADS, else OMP_NUM_THREADS (the GPU box's CPU share), else the cores
+// host worker threads: NGSEP_THREADS; else this process's share of the cores it may run on -- the affinity mask
+// divided among the node's ranks (LOCAL_WORLD_SIZE, one process per GPU), at most OMP_NUM_THREADS when that is above 1
+// (the GPU box's CPU share; torch.distributed.run sets 1 for its children by default, which is not a share)
 inline unsigned host_threads() {
     static const unsigned n = [] {
-        const char* e = std::getenv("NGSEP_THREADS");
-        if (!e) e = std::getenv("OMP_NUM_THREADS");
-        long v = e ? std::atol(e) : (long)std::thread::hardware_concurrency();
+        if (const char* e = std::getenv("NGSEP_THREADS")) return (unsigned)std::max(1L, std::min(std::atol(e), 64L));
+        long cores = (long)std::thread::hardware_concurrency();
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof set, &set) == 0 && CPU_COUNT(&set) > 0) cores = CPU_COUNT(&set);
+        const char* lw = std::getenv("LOCAL_WORLD_SIZE");
+        const long ranks = lw ? std::max(1L, std::atol(lw)) : 1L;
+        long v = std::max(1L, cores / ranks);
+        const char* omp = std::getenv("OMP_NUM_THREADS");
+        if (omp && std::atol(omp) > 1) v = std::min(v, std::atol(omp));
         return (unsigned)std::max(1L, std::min(v, 64L));
     }();
     return n;
@@ -595,7 +606,7 @@ struct Staged {            // everything resident for one run
     // rows(t, s) code bytes in getAlleleCalls order -- column (p, s) at pboff[t * (S + 1) + s] + (p % kPopTile) *
     // stride_t, stride_t = the tile's rows summed over its samples
     std::unique_ptr<uint8_t[]> h_ppile;
-    std::vector<uint16_t> h_prow;       // rows per (tile, sample): h_prow[t * (S + 1) + s]
+    std::vector<int32_t> h_prow;        // rows per (tile, sample): h_prow[t * (S + 1) + s]
     std::vector<int64_t> h_pboff;       // block offsets, same index (+ the total at the end)
     int64_t ppile_bytes = 0;
     std::vector<uint8_t> h_ref;
@@ -652,6 +663,9 @@ struct Staged {            // everything resident for one run
     int64_t pnblk = 0;
     std::vector<int32_t> h_samp_st;
     std::vector<int64_t> h_st_end;
+    // KLM tiles (kKlmTile positions) where some sample's coverage exceeds kKlmCountMaxCov: KLM's byte counters cannot
+    // carry there, so those tiles take the exact-bound scan (k_scan_pop<false>) and every other tile the counting one
+    std::vector<int32_t> h_deep_tiles;
 };
 
 // Pinned host buffers of the single-sample layout, reused run after run (streamed windows: no page faults,

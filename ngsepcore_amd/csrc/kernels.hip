@@ -185,6 +185,11 @@ struct Device {
     int64_t* d_st_end = nullptr;     //   one past each stream's last entry
     int32_t n_streams = 0, pblk_shift = kRgBlockShift, pop_stride = 0;
     int64_t pnblk = 0;
+    int32_t* d_deep_tiles = nullptr; //   KLM tiles some sample covers deeper than kKlmCountMaxCov (k_scan_pop<false>)
+    int64_t n_deep_tiles = 0;
+    uint8_t* d_deep_flag = nullptr;  //   ... as a byte per tile (k_scan_pop<true> skips them)
+    uint8_t* d_gcol = nullptr;       //   KPM / k_stage_a columns when they do not fit LDS (kPopGatherCap)
+    size_t cap_gcol = 0;
     uint32_t* d_need = nullptr;      //   open positions, a bit per global position
     bool need_clean = false;         //   d_need is all zero (cleared by the last run's k_stage_a)
     PopStage pstage;                 //   KPM's two stages (device_run_multi)
@@ -192,7 +197,7 @@ struct Device {
     ngsep_sample_call* h_pcalls = nullptr;
     int64_t cap_h_psites = 0, cap_h_pcalls = 0;
     uint8_t* d_ppile = nullptr;      // multisample: KPM's site-major per-tile pile
-    uint16_t* d_prow = nullptr;      //   rows per block
+    int32_t* d_prow = nullptr;       //   rows per block
     int64_t* d_pboff = nullptr;      //   block offsets
     int32_t n_samples = 0;
     ngsep_popsite_out* d_psites = nullptr;
@@ -1476,8 +1481,9 @@ __global__ __launch_bounds__(256) void k_queue_need(const uint32_t* __restrict__
 //           reload each) into its slot's {ref, alt 1, alt 2, alt 3} sums -- the exact integer bound;
 //   pass 3: a slot the bound cannot prove hom-ref -- or holding more than kMcMaxCalls valid calls, or past
 //           kKlmSlots -- keeps its position open: one bit per global position (atomicOr); KQN queues them for KPM.
-// COUNT needs every sample's coverage below 128 (the host's per-sample bound, pop_stride): the byte counters and the
-// byte differences cannot carry.  Deeper populations run !COUNT: every marked position takes the exact bound.
+// COUNT needs every sample's coverage over the tile below 128 (the host's per-tile bound, engine.cpp build_pop_rg_layout):
+// the byte counters and the byte differences cannot carry.  The tiles where some sample is deeper (collapsed repeats,
+// rDNA, deep populations) run !COUNT, launched over those tiles only: every marked position takes the exact bound.
 // The reads of no sample only enter the pooled counts: not scanned.  No block barrier after the tables: every wave's
 // state is its own.
 constexpr int kKlmThreads = 256;
@@ -1523,7 +1529,13 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
     const int32_t* __restrict__ samp_st, const int32_t* __restrict__ blkA, const int32_t* __restrict__ blkB,
     int64_t nblk, int32_t shift, int32_t n_samples, const uint8_t* __restrict__ ref, const LikTables* __restrict__ tabs,
     GenotypeParams gp, uint32_t* __restrict__ need, unsigned long long* __restrict__ counters, uint2* __restrict__ pairs,
-    int64_t pseg, const int64_t* __restrict__ st_end) {
+    int64_t pseg, const int64_t* __restrict__ st_end, const uint8_t* __restrict__ deep_flag,
+    const int32_t* __restrict__ deep_tiles) {
+    // deep_flag (COUNT): tiles some sample covers deeper than kKlmCountMaxCov are skipped here -- the !COUNT launch over
+    // deep_tiles (its grid: those tiles only) scans them
+    const int nsg = (n_samples + 3) >> 2;
+    const int64_t tile = COUNT || !deep_tiles ? (int64_t)blockIdx.x / nsg : (int64_t)deep_tiles[blockIdx.x / nsg];
+    if (COUNT && deep_flag && deep_flag[tile]) return;      // (the whole workgroup: no barrier has been reached)
     __shared__ unsigned long long w[2][32];
     __shared__ uint32_t s_call[kKlmTile / 32];         // callable positions of the tile
     __shared__ uint32_t s_bm[4][kKlmWords];            // marked positions, then those the exact bound takes
@@ -1532,8 +1544,6 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
     __shared__ alignas(16) uint32_t s_wave[4][kKlmWaveLds / 4];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (threadIdx.x < 64) w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
-    const int nsg = (n_samples + 3) >> 2;
-    const int64_t tile = (int64_t)blockIdx.x / nsg;
     {
         // 8 positions' callable bits per thread (bit 7 of the reference code), four threads per word
         const uint2 r = reinterpret_cast<const uint2*>(ref + tile * kKlmTile)[threadIdx.x];
@@ -2247,7 +2257,8 @@ struct PopGather {
     const int32_t* blkA;        // [stream * nblk + (p >> shift)]: the stream's first entry that can cover p
     const uint8_t* ref;
     int64_t nblk;
-    int32_t shift, stride;      // stride: codes per sample column in LDS
+    int32_t shift, stride;      // stride: codes per sample column
+    uint8_t* gcol;              // GCOL kernels: the columns in this device scratch (a workgroup's own part), not in LDS
 };
 template <int kGatherBatch>                      // entry headers a gathering thread loads at once
 __device__ inline int32_t pop_gather(const PopGather& pg, int32_t p, int s, uint8_t* dst, int32_t cap) {
@@ -2329,6 +2340,8 @@ __device__ __forceinline__ int nth_set_bit(uint32_t w, int r) {   // the r-th (0
     for (int k = 0; k < r; k++) w &= w - 1u;
     return __builtin_ctz(w);
 }
+// GCOL: the lanes' columns in pg.gcol (blockIdx.x's 64 x stride bytes) -- a population too deep for them in LDS
+template <bool GCOL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_stage_a(
     const QueueSite* __restrict__ queue, const unsigned long long* qn, int64_t qcap, const PopGather pg,
     const LikTables* __restrict__ tabs, GenotypeParams gp, int32_t ploidy, uint32_t* __restrict__ pmask,
@@ -2374,7 +2387,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         }
         const int32_t gpos = qs.gpos;
         const uint32_t rc = (uint32_t)qs.rc;
-        uint8_t* col = s_gcol + (int64_t)lane * pg.stride;
+        uint8_t* col = GCOL ? pg.gcol + ((int64_t)blockIdx.x * 64 + lane) * pg.stride : s_gcol + (int64_t)lane * pg.stride;
         int32_t rows = 0;
         if (s >= 0) {
             rows = pop_gather<NGSEP_KPM_GBATCH>(pg, gpos, s, col, pg.stride);
@@ -2462,10 +2475,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
 // (measured and not kept: a separate gather kernel, one thread per (position, sample) at 8 waves per SIMD, into
 // columns KPM then read with the next position's in flight -- 0.64 against 0.52 ms for gather + KPM on configs[4]:
 // the gather's cost is its scattered lines, ~10 per sample column, not latency KPM fails to hide)
-template <bool POOL, int WPE, int GATHER>
+// GCOL (GATHER 1): the columns in pg.gcol (blockIdx.x's (S + 1) x stride bytes), not LDS -- a population whose per-sample
+// coverage bound times S + 1 exceeds kPopGatherCap (MultisampleVariantsDetector genotypes at any depth, :522-558)
+template <bool POOL, int WPE, int GATHER, bool GCOL>
 __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE))) void k_posterior_multi(
     const QueueSite* __restrict__ queue, const unsigned long long* qn, int64_t qcap,
-    const uint8_t* __restrict__ ppile, const uint16_t* __restrict__ prow, const int64_t* __restrict__ pboff,
+    const uint8_t* __restrict__ ppile, const int32_t* __restrict__ prow, const int64_t* __restrict__ pboff,
     const PopGather pg, const LikTables* __restrict__ tabs, GenotypeParams gp,
     int32_t n_samples, double min_adf, int32_t ploidy, const PoolTables* __restrict__ pt,
     ngsep_popsite_out* __restrict__ sites, ngsep_sample_call* __restrict__ calls,
@@ -2525,7 +2540,8 @@ __global__ __launch_bounds__(kPopThreads) __attribute__((amdgpu_waves_per_eu(WPE
         int32_t rows = rows_next;
         const uint8_t* col = col_next;
         if (GATHER == 1 && tid <= n_samples) {
-            uint8_t* dst = s_gcol + (int64_t)tid * pg.stride;
+            uint8_t* dst = GCOL ? pg.gcol + ((int64_t)blockIdx.x * (n_samples + 1) + tid) * pg.stride
+                                : s_gcol + (int64_t)tid * pg.stride;
             rows = pop_gather<NGSEP_KPM_GBATCH>(pg, gpos, tid, dst, pg.stride);
             if (rows > pg.stride) {                          // (the host's coverage bound makes this unreachable)
                 atomicOr(&counters[3], 1ull << 63);
@@ -3082,6 +3098,9 @@ void device_release(Device* d) {
     d->prg = false;
     d->n_streams = 0;
     d->pop_stride = 0;
+    (void)hipFree(d->d_deep_tiles); d->d_deep_tiles = nullptr;
+    (void)hipFree(d->d_deep_flag); d->d_deep_flag = nullptr;
+    d->n_deep_tiles = 0;
     (void)hipFree(d->d_need); d->d_need = nullptr;
     d->pstage.release();
     for (auto& m : d->mslot) m.stage.release();
@@ -3135,6 +3154,7 @@ void device_destroy(Device* d) {
     }
     (void)hipFree(d->d_psites);
     (void)hipFree(d->d_pcalls);
+    (void)hipFree(d->d_gcol);
     (void)hipFree(d->d_pcalls_ord);
     (void)hipFree(d->d_mforced);
     (void)hipFree(d->d_mforced_ctr);
@@ -3397,13 +3417,23 @@ int device_upload(Device* d, const Staged& s, std::string& err) {
             d->pblk_shift = s.pblk_shift;
             d->pnblk = s.pnblk;
             d->pop_stride = std::max<int32_t>(s.max_cov, 1);
+            d->n_deep_tiles = (int64_t)s.h_deep_tiles.size();
+            if (d->n_deep_tiles) {
+                const int64_t ntile = s.g_len / kKlmTile;
+                std::vector<uint8_t> flag((size_t)ntile, 0);
+                for (int32_t t : s.h_deep_tiles) flag[(size_t)t] = 1;
+                HIP_TRY(hipMalloc(&d->d_deep_tiles, (size_t)d->n_deep_tiles * sizeof(int32_t)));
+                HIP_TRY(hipMalloc(&d->d_deep_flag, (size_t)ntile));
+                H2D(d->d_deep_tiles, s.h_deep_tiles.data(), (size_t)d->n_deep_tiles * sizeof(int32_t), d->stream);
+                H2D(d->d_deep_flag, flag.data(), (size_t)ntile, d->stream);
+            }
         } else {
             // the realigner's region positions: a site-major pile (KPM)
             HIP_TRY(hipMalloc(&d->d_ppile, (size_t)s.ppile_bytes + 64));
-            HIP_TRY(hipMalloc(&d->d_prow, std::max<size_t>(s.h_prow.size(), 1) * sizeof(uint16_t)));
+            HIP_TRY(hipMalloc(&d->d_prow, std::max<size_t>(s.h_prow.size(), 1) * sizeof(int32_t)));
             HIP_TRY(hipMalloc(&d->d_pboff, std::max<size_t>(s.h_pboff.size(), 1) * sizeof(int64_t)));
             H2D(d->d_ppile, s.h_ppile.get(), (size_t)s.ppile_bytes + 64, d->stream);
-            if (!s.h_prow.empty()) H2D(d->d_prow, s.h_prow.data(), s.h_prow.size() * sizeof(uint16_t), d->stream);
+            if (!s.h_prow.empty()) H2D(d->d_prow, s.h_prow.data(), s.h_prow.size() * sizeof(int32_t), d->stream);
             if (!s.h_pboff.empty()) H2D(d->d_pboff, s.h_pboff.data(), s.h_pboff.size() * sizeof(int64_t), d->stream);
         }
         if (s.known) {
@@ -3913,10 +3943,39 @@ static unsigned sta_grid() {
     static const unsigned g = diag_env("NGSEP_STA_GRID") ? std::max(1u, (unsigned)std::atoi(diag_env("NGSEP_STA_GRID"))) : kKpmGrid;
     return g;
 }
-static auto kpm_kernel(int ploidy, int gather) {
+static auto kpm_kernel(int ploidy, int gather, bool gcol) {
+    if (gather == 1 && gcol)
+        return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, 1, true> : k_posterior_multi<false, kKpmWavesPerEu, 1, true>;
     if (gather == 1)
-        return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, 1> : k_posterior_multi<false, kKpmWavesPerEu, 1>;
-    return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, 0> : k_posterior_multi<false, kKpmWavesPerEu, 0>;
+        return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, 1, false> : k_posterior_multi<false, kKpmWavesPerEu, 1, false>;
+    return ploidy >= 3 ? k_posterior_multi<true, kKpmWavesPerEu, 0, false> : k_posterior_multi<false, kKpmWavesPerEu, 0, false>;
+}
+
+// Where KPM's and k_stage_a's gathered columns live: LDS while the bytes of one workgroup's columns ((S + 1) x the
+// per-sample coverage bound for KPM, 64 x it for the first stage) stay within kPopGatherCap, else the device scratch
+// d_gcol, a part per workgroup -- the grid then shrinks so that the scratch stays within kPopGatherCap's budget
+// (kPopGcolBudget).  No depth is refused (MultisampleVariantsDetector genotypes a position at whatever depth it has,
+// :522-558, :674-693).  NGSEP_POP_GCOL=1 (test hook) takes the scratch at any depth.
+struct PopCols {
+    bool kpm_gcol = false, sta_gcol = false;
+    unsigned kpm_grid = 1, sta_grid = 1;
+};
+static PopCols pop_cols(Device* d, std::string& err, bool* fail) {
+    const bool force = env_hook("NGSEP_POP_GCOL") != nullptr;     // (read every run)
+    PopCols c;
+    *fail = false;
+    const int64_t stride = std::max<int32_t>(d->pop_stride, 1);
+    const int64_t kpm_wg = (int64_t)(d->n_samples + 1) * stride, sta_wg = 64 * stride;
+    c.kpm_gcol = d->prg && (force || kpm_wg > kPopGatherCap);
+    c.sta_gcol = d->prg && (force || sta_wg > kPopGatherCap);
+    c.kpm_grid = kpm_grid(d);
+    c.sta_grid = sta_grid();
+    if (c.kpm_gcol) c.kpm_grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(c.kpm_grid, kPopGcolBudget / kpm_wg));
+    if (c.sta_gcol) c.sta_grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(c.sta_grid, kPopGcolBudget / sta_wg));
+    const size_t need = std::max<size_t>(c.kpm_gcol ? (size_t)c.kpm_grid * (size_t)kpm_wg : 0,
+                                         c.sta_gcol ? (size_t)c.sta_grid * (size_t)sta_wg : 0);
+    if (need && ensure_dev(&d->d_gcol, &d->cap_gcol, need, false, err)) *fail = true;
+    return c;
 }
 
 // KLM over every (sample, tile) of the resident population layout, then KQN (shared by the two multisample paths)
@@ -3930,15 +3989,30 @@ static hipError_t launch_pop_scan(Device* d, const GenotypeParams& g, uint32_t* 
     const int64_t ntile = d->g_len / kKlmTile;
     const int64_t nblk = std::max<int64_t>(1, ntile * ((d->n_samples + 3) / 4));
     if (nblk >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
-    // the count bound needs every sample's coverage below 128 (byte counters); deeper populations take the exact bound
-    // at every marked position
-    auto klm = d->pop_stride <= kKlmCountMaxCov ? k_scan_pop<true> : k_scan_pop<false>;
-    hipExtLaunchKernelGGL(klm, dim3((unsigned)nblk), dim3(kKlmThreads), 0, d->stream, ev_start, nullptr, 0,
-                          (const uint64_t*)d->d_units, (const int2*)d->d_rh, (const RGroup*)d->d_grp,
-                          (const int32_t*)d->d_samp_st, (const int32_t*)d->d_blkA, (const int32_t*)d->d_blkB, d->pnblk,
-                          d->pblk_shift, d->n_samples, (const uint8_t*)d->d_ref, (const LikTables*)d->d_tables, g, need, ctr,
-                          stage ? stage->pairs : nullptr, stage ? stage->pseg : (int64_t)0, (const int64_t*)d->d_st_end);
-    if ((e = launch_check()) != hipSuccess) return e;
+    // the count bound needs every sample's coverage over a tile below 128 (byte counters): the tiles where some sample
+    // is deeper take the exact bound at every marked position (k_scan_pop<false>, a launch over those tiles only)
+    const int64_t ndeep = d->n_deep_tiles;
+    const int64_t nsg = (d->n_samples + 3) / 4;
+    const bool counting = ndeep == 0 || ndeep < ntile;
+    if (counting) {
+        hipExtLaunchKernelGGL(k_scan_pop<true>, dim3((unsigned)nblk), dim3(kKlmThreads), 0, d->stream, ev_start, nullptr, 0,
+                              (const uint64_t*)d->d_units, (const int2*)d->d_rh, (const RGroup*)d->d_grp,
+                              (const int32_t*)d->d_samp_st, (const int32_t*)d->d_blkA, (const int32_t*)d->d_blkB, d->pnblk,
+                              d->pblk_shift, d->n_samples, (const uint8_t*)d->d_ref, (const LikTables*)d->d_tables, g, need, ctr,
+                              stage ? stage->pairs : nullptr, stage ? stage->pseg : (int64_t)0, (const int64_t*)d->d_st_end,
+                              (const uint8_t*)(ndeep ? d->d_deep_flag : nullptr), (const int32_t*)nullptr);
+        if ((e = launch_check()) != hipSuccess) return e;
+    }
+    if (ndeep) {
+        hipExtLaunchKernelGGL(k_scan_pop<false>, dim3((unsigned)(ndeep * nsg)), dim3(kKlmThreads), 0, d->stream,
+                              counting ? nullptr : ev_start, nullptr, 0,
+                              (const uint64_t*)d->d_units, (const int2*)d->d_rh, (const RGroup*)d->d_grp,
+                              (const int32_t*)d->d_samp_st, (const int32_t*)d->d_blkA, (const int32_t*)d->d_blkB, d->pnblk,
+                              d->pblk_shift, d->n_samples, (const uint8_t*)d->d_ref, (const LikTables*)d->d_tables, g, need, ctr,
+                              stage ? stage->pairs : nullptr, stage ? stage->pseg : (int64_t)0, (const int64_t*)d->d_st_end,
+                              (const uint8_t*)nullptr, (const int32_t*)d->d_deep_tiles);
+        if ((e = launch_check()) != hipSuccess) return e;
+    }
     const int64_t qblk = std::max<int64_t>(1, std::min<int64_t>((nwords + 255) / 256, (int64_t)d->n_cu * 4));
     hipExtLaunchKernelGGL(k_queue_need, dim3((unsigned)qblk), dim3(256), 0, d->stream, nullptr, ev_end, 0,
                           (const uint32_t*)need, (const uint8_t*)d->d_ref, nwords, queue, ctr, qcap, stage ? stage->qword : nullptr);
@@ -3975,27 +4049,42 @@ hipError_t PopStage::ensure(int64_t qcap, int64_t nwords, hipStream_t st) {
 // KPM's two stages apply to discovery without minAlleleDepthFrequency (the first stage's allele set is the called
 // alleles'), ploidy < 3 and the hom-ref bounds on (the samples they prove hom-ref are hom-ref for any allele set)
 static bool pop_two_stage(const Device* d, const GenotypeParams& g, double min_adf, int ploidy, bool mknown) {
-    static const bool off = env_hook("NGSEP_KPM_ONE_STAGE") != nullptr;   // (test hook: the one-stage path)
+    const bool off = env_hook("NGSEP_KPM_ONE_STAGE") != nullptr;   // (test hook: the one-stage path; read every run)
     return !off && !mknown && d->prg && ploidy < 3 && min_adf == 0.0 && g.use_bound != 0;
 }
-static PopGather pop_gather_of(const Device* d) {
+static PopGather pop_gather_of(const Device* d, bool gcol) {
     PopGather pg{};
     if (!d->prg) return pg;
     pg.units = d->d_units; pg.rh = d->d_rh; pg.grp = d->d_grp; pg.samp_st = d->d_samp_st; pg.st_end = d->d_st_end;
     pg.blkA = d->d_blkA; pg.ref = d->d_ref; pg.nblk = d->pnblk; pg.shift = d->pblk_shift; pg.stride = d->pop_stride;
+    pg.gcol = gcol ? d->d_gcol : nullptr;
     return pg;
 }
 // KPM's first stage over KQN's queue (k_stage_a, one wavefront per position): the positions whose QS can pass -> the
 // stage's queue (counter 7), which the second stage (k_posterior_multi) genotypes in full
-static hipError_t launch_stage_a(Device* d, const GenotypeParams& g, int ploidy, const QueueSite* queue,
+static hipError_t launch_stage_a(Device* d, const PopCols& pc, const GenotypeParams& g, int ploidy, const QueueSite* queue,
                                  const unsigned long long* qn, int64_t qcap, PopStage& st, unsigned long long* ctr,
                                  uint32_t* need_clear, int64_t need_words) {
-    hipLaunchKernelGGL(k_stage_a, dim3(sta_grid()), dim3(64), (size_t)64 * (size_t)d->pop_stride, d->stream, queue, qn, qcap,
-                       pop_gather_of(d), (const LikTables*)d->d_tables, g, (int32_t)ploidy, st.pmask, st.qB, ctr + 7, st.cap, ctr,
-                       need_clear, need_words);
+    hipLaunchKernelGGL(pc.sta_gcol ? k_stage_a<true> : k_stage_a<false>, dim3(pc.sta_grid), dim3(64),
+                       pc.sta_gcol ? (size_t)0 : (size_t)64 * (size_t)d->pop_stride, d->stream, queue, qn, qcap,
+                       pop_gather_of(d, pc.sta_gcol), (const LikTables*)d->d_tables, g, (int32_t)ploidy, st.pmask, st.qB, ctr + 7,
+                       st.cap, ctr, need_clear, need_words);
     return launch_check();
 }
-static size_t kpm_lds(const Device* d, int mode) { return mode == 1 ? (size_t)(d->n_samples + 1) * (size_t)d->pop_stride : 0; }
+// KPM over a queue (mode 1: columns gathered from the population layout; 0: the realigner regions' site-major pile)
+static hipError_t launch_kpm(Device* d, const PopCols& pc, int mode, const GenotypeParams& g, int ploidy, double min_adf,
+                             const QueueSite* queue, const unsigned long long* qn, int64_t qcap, ngsep_popsite_out* sites,
+                             ngsep_sample_call* calls, unsigned long long* ctr, int64_t cap, unsigned long long* stamps,
+                             hipEvent_t ev_end) {
+    const bool gcol = mode == 1 && pc.kpm_gcol;
+    const size_t lds = mode == 1 && !gcol ? (size_t)(d->n_samples + 1) * (size_t)d->pop_stride : 0;
+    hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode, gcol), dim3(mode == 1 ? pc.kpm_grid : kpm_grid(d)), dim3(kPopThreads), lds,
+                          d->stream, nullptr, ev_end, 0, queue, qn, qcap, (const uint8_t*)d->d_ppile, (const int32_t*)d->d_prow,
+                          (const int64_t*)d->d_pboff, pop_gather_of(d, gcol), (const LikTables*)d->d_tables, g, d->n_samples,
+                          min_adf, (int32_t)ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), sites, calls, ctr,
+                          cap, stamps);
+    return launch_check();
+}
 // the shard counters' sums: KLM's candidate columns and bounded columns
 static void pop_scan_counts(const unsigned long long* h, int64_t* cand, int64_t* bounded) {
     int64_t a = 0, b = 0;
@@ -4058,20 +4147,19 @@ int device_run_multi(Device* d, const Staged& s, const LikTables& t, const Genot
     // taken from KQN's end)
     if (!mknown && !d->prg) { err = "multisample run without a population layout"; return -1; }
     const int mode = d->prg ? 1 : 0;
+    bool cfail = false;
+    const PopCols pc = pop_cols(d, err, &cfail);
+    if (cfail) return -1;
     if (two) {
         const bool scanned = !mknown && d->prg;
-        HIP_TRY(launch_stage_a(d, g, ploidy, d->d_hard, ctr + 2, d->cap_hard, d->pstage, ctr, scanned ? d->d_need : nullptr,
+        HIP_TRY(launch_stage_a(d, pc, g, ploidy, d->d_hard, ctr + 2, d->cap_hard, d->pstage, ctr, scanned ? d->d_need : nullptr,
                                scanned ? d->g_len / 32 + 1 : 0));
         d->need_clean = scanned;
     }
-    hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode), dim3(kpm_grid(d)), dim3(kPopThreads), kpm_lds(d, mode), d->stream, nullptr, d->ev[2], 0,
-                          (const QueueSite*)(mknown ? d->d_mforced : two ? d->pstage.qB : d->d_hard),
-                          (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : two ? ctr + 7 : ctr + 2),
-                          mknown ? std::max<int64_t>(d->n_mforced, 1) : two ? d->pstage.cap : d->cap_hard, (const uint8_t*)d->d_ppile,
-                          (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, pop_gather_of(d), (const LikTables*)d->d_tables, g,
-                          S, min_adf, ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), d->d_psites, d->d_pcalls,
-                          ctr, d->cap_psites, d->d_stamps);
-    HIP_TRY(launch_check());
+    HIP_TRY(launch_kpm(d, pc, mode, g, ploidy, min_adf, (const QueueSite*)(mknown ? d->d_mforced : two ? d->pstage.qB : d->d_hard),
+                       (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : two ? ctr + 7 : ctr + 2),
+                       mknown ? std::max<int64_t>(d->n_mforced, 1) : two ? d->pstage.cap : d->cap_hard, d->d_psites, d->d_pcalls,
+                       ctr, d->cap_psites, d->d_stamps, d->ev[2]));
     DMA(d->h_counters, ctr, kCtrWords * sizeof(unsigned long long), 1, d->stream);
     HIP_TRY(hipStreamSynchronize(d->stream));
     const unsigned long long c3 = d->h_counters[3];
@@ -4337,19 +4425,18 @@ int device_submit_multi(Device* d, const LikTables& t, const GenotypeParams& g, 
         HIP_TRY(launch_pop_scan(d, g, m.d_need, m.d_hard, m.cap_hard, ctr, m.ev[0], m.ev[1], two ? &m.stage : nullptr, clean));
     }
     const int mode = d->prg ? 1 : 0;
+    bool cfail = false;
+    const PopCols pc = pop_cols(d, err, &cfail);
+    if (cfail) return -1;
     if (two) {
-        HIP_TRY(launch_stage_a(d, g, ploidy, m.d_hard, ctr + 2, m.cap_hard, m.stage, ctr, mknown ? nullptr : m.d_need,
+        HIP_TRY(launch_stage_a(d, pc, g, ploidy, m.d_hard, ctr + 2, m.cap_hard, m.stage, ctr, mknown ? nullptr : m.d_need,
                                mknown ? 0 : nwords));
         m.need_clean = !mknown;
     }
-    hipExtLaunchKernelGGL(kpm_kernel(ploidy, mode), dim3(kpm_grid(d)), dim3(kPopThreads), kpm_lds(d, mode), d->stream, nullptr, m.ev[3], 0,
-                          (const QueueSite*)(mknown ? d->d_mforced : two ? m.stage.qB : m.d_hard),
-                          (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : two ? ctr + 7 : ctr + 2),
-                          mknown ? std::max<int64_t>(d->n_mforced, 1) : two ? m.stage.cap : m.cap_hard, (const uint8_t*)d->d_ppile,
-                          (const uint16_t*)d->d_prow, (const int64_t*)d->d_pboff, pop_gather_of(d), (const LikTables*)d->d_tables, g,
-                          S, min_adf, ploidy, (const PoolTables*)(ploidy >= 3 ? d->d_pool : nullptr), m.d_psites, m.d_pcalls,
-                          ctr, m.cap_psites, (unsigned long long*)nullptr);
-    HIP_TRY(launch_check());
+    HIP_TRY(launch_kpm(d, pc, mode, g, ploidy, min_adf, (const QueueSite*)(mknown ? d->d_mforced : two ? m.stage.qB : m.d_hard),
+                       (const unsigned long long*)(mknown ? d->d_mforced_ctr + 2 : two ? ctr + 7 : ctr + 2),
+                       mknown ? std::max<int64_t>(d->n_mforced, 1) : two ? m.stage.cap : m.cap_hard, m.d_psites, m.d_pcalls,
+                       ctr, m.cap_psites, (unsigned long long*)nullptr, m.ev[3]));
     // the calls packed right behind KPM on the compute stream; the copies (counters, a guess of the sites, their
     // packed calls and whole records) on the copy stream, so the next pass's kernels do not wait for them
     if (m.cap_pack < m.cap_psites) {

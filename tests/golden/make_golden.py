@@ -74,6 +74,9 @@ FULL_CASES = {
 # chrIV (the bench's --config multisample workload); the oracle's population VCF md5 + record count
 FULL_POP_CASES = {
     "configs4_chrIV_200x10x": dict(genome=0, depth=10.0, seed=5, n_samples=200, contig_first=3, n_contigs=1),
+    # configs[4]'s shape with a 2 kb collapsed repeat where every sample is ~300x deep (tests/test_gpu_deep_population.py)
+    "deep_repeat_200x10x": dict(genome=2, custom_len=16000, depth=10.0, seed=42, n_samples=200, snv_rate=3e-3,
+                                hot_first=7001, hot_len=2000, hot_depth=290.0),
 }
 # CoverageStats (CoverageStatisticsCalculator) fixtures: synth case -> (min_mq, max_coverage)
 COVERAGE_CASES = {"edge_2contigs_25x": (20, 300), "c1_chrI_10x": (20, 12)}

@@ -137,10 +137,11 @@ def test_errors(session):
     assert rc == _lib.NGSEP_OK and got == b""
 
 
-@pytest.mark.parametrize("read_bytes", [None, "100000"])
+@pytest.mark.parametrize("read_bytes", [None, "100000", "4096"])
 def test_bam_reader_device_inflate_vcf_identical(tmp_path, monkeypatch, read_bytes):
     """ngsep_call_bam with the device inflate (NGSEP_GPU_INFLATE) == the host inflate, whole reads and 100 kB reads
-    (blocks cut across reads, many batches in flight)."""
+    (blocks cut across reads, many batches in flight); a 4 KB read request is raised to one whole BGZF block (a
+    smaller buffer could never hold a 64 KB block: the reader looped on empty chunks)."""
     _, fa, _, bam = make_data(tmp_path, genome=pysynth.YEAST, n_contigs=2, contig_first=0, depth=25, seed=7,
                               secondary_rate=0.01, lowmq_rate=0.01, noqual_rate=0.005, softclip_rate=0.05, dup_rate=0.02)
     monkeypatch.delenv("NGSEP_GPU_INFLATE", raising=False)

@@ -138,6 +138,11 @@ static int sample_quality(Rng& r, int model) {
 
 static void make_population(ngs_synth* s);
 static void make_batch(ngs_synth* s);
+// extra reads of a collapsed repeat (hot_depth > 0) on a contig of length L, per sample
+static int64_t hot_reads(const ngs_synth_params& p, int64_t L) {
+    if (p.hot_depth <= 0 || p.hot_len < p.read_len || p.hot_first < 1 || p.hot_first + p.hot_len - 1 > L) return 0;
+    return (int64_t)std::llround(p.hot_depth * (double)p.hot_len / p.read_len);
+}
 
 // the kept contigs of the genome table, optionally truncated (trunc_len)
 static std::vector<ContigDef> kept_contigs(const ngs_synth_params& p, int* first_out, double* pa) {
@@ -358,6 +363,11 @@ extern "C" ngs_synth* ngs_synth_create(const ngs_synth_params* pp) {
         struct Gen { int32_t pos; int64_t order; };
         std::vector<Gen> starts(nreads);
         for (int64_t k = 0; k < nreads; k++) starts[k] = {(int32_t)(1 + r.below((uint64_t)(L - rl + 1))), k};
+        // a collapsed repeat (hot_depth > 0): extra reads inside [hot_first, hot_first + hot_len)
+        const int64_t hot_n = hot_reads(p, L);
+        for (int64_t k = 0; k < hot_n; k++)
+            starts.push_back({(int32_t)(p.hot_first + (int64_t)r.below((uint64_t)(p.hot_len - rl + 1))), nreads + k});
+        nreads += hot_n;
         std::sort(starts.begin(), starts.end(), [](const Gen& a, const Gen& b) { return a.pos != b.pos ? a.pos < b.pos : a.order < b.order; });
         // read k: bases/qualities at b0 + k*rl, CIGAR at c0 + 2k (<= 2 items)
         const int64_t b0 = (int64_t)R.bases.size(), c0 = (int64_t)R.cigar.size();
@@ -487,6 +497,10 @@ static void make_population(ngs_synth* s) {
         starts.reserve((size_t)(nper * ns));
         for (int k = 0; k < ns; k++)
             for (int64_t j = 0; j < nper; j++) starts.push_back({(int32_t)(1 + r.below((uint64_t)(L - rl + 1))), k, j});
+        const int64_t hot_n = hot_reads(p, L);               // a collapsed repeat: every sample hot_depth deeper there
+        for (int k = 0; k < ns; k++)
+            for (int64_t j = 0; j < hot_n; j++)
+                starts.push_back({(int32_t)(p.hot_first + (int64_t)r.below((uint64_t)(p.hot_len - rl + 1))), k, nper + j});
         std::sort(starts.begin(), starts.end(), [](const Gen& a, const Gen& b) {
             if (a.pos != b.pos) return a.pos < b.pos;
             if (a.sample != b.sample) return a.sample < b.sample;

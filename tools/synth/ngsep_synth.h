@@ -40,6 +40,9 @@ typedef struct ngs_synth_params {
     int32_t rng_per_contig;  /* 1: each contig's donor/reads from its own seeded stream, so a contig generated
                                 alone (one rank's shard, contig_first=k, n_contigs=1) equals it in the whole genome */
     double  indel_rate;      /* donor indels (1-10 bp insertions/deletions) per bp; reads across them carry I/D */
+    int64_t hot_first;       /* hot_depth > 0: extra reads starting in [hot_first, hot_first + hot_len - read_len] */
+    int64_t hot_len;         /*   (1-based; a collapsed repeat: every sample hot_depth deeper there) */
+    double  hot_depth;
 } ngs_synth_params;
 
 typedef struct ngs_synth ngs_synth;

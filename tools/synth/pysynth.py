@@ -25,6 +25,7 @@ class SynthParams(ctypes.Structure):
         ("quality_model", ctypes.c_int32), ("secondary_rate", ctypes.c_double), ("lowmq_rate", ctypes.c_double),
         ("noqual_rate", ctypes.c_double), ("softclip_rate", ctypes.c_double), ("n_samples", ctypes.c_int32),
         ("trunc_len", ctypes.c_int64), ("rng_per_contig", ctypes.c_int32), ("indel_rate", ctypes.c_double),
+        ("hot_first", ctypes.c_int64), ("hot_len", ctypes.c_int64), ("hot_depth", ctypes.c_double),
     ]
 
 
