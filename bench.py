@@ -643,7 +643,7 @@ def main():
     if e2e_src is not None:
         try:
             e2e = (end_to_end_population if multi else end_to_end)(e2e_src[1], e2e_src[2], local_rank)
-            log(f"[rank 0] end-to-end BAM -> VCF: {e2e['wall_s']:.2f}s, {e2e['value']:.4g} positions/s")
+            log(f"[rank {rank}] end-to-end BAM -> VCF: {e2e['wall_s']:.2f}s, {e2e['value']:.4g} positions/s")
             if e2e_indel_src is not None:
                 r = end_to_end(e2e_indel_src[0], e2e_indel_src[1], local_rank)
                 r["note"] += "; synthetic indels at rate 1e-4 per position (the indel realigner's regions replayed)"

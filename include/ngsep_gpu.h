@@ -352,7 +352,9 @@ int ngsep_clean_cut(ngsep_ctx* ctx, const char* const* bam_paths, int32_t n_file
  * AlignmentsPileupGenerator.java:242-254,310-322), on its own device, streams and pinned buffers, keeping the records
  * inside the window; out_vcf_path gets the header and the windows' records in (sequence, window) order -- the
  * one-context VCF.  Temporary files out_vcf_path.part<k> are removed.  Errors are reported on ctxs[0]; in pass-through
- * mode every context's carved regions end up on ctxs[0] (ngsep_fetch_carved_regions). */
+ * mode every context's carved regions end up on ctxs[0] (ngsep_fetch_carved_regions).  Host memory: a context without
+ * a reference receives a copy of the first one's (sequences and input variants), so N contexts hold N copies of the
+ * reference (a 3.1 Gb genome: ~3 GB each) on top of the per-context read buffers. */
 int ngsep_call_bam_multi(ngsep_ctx* const* ctxs, int32_t n_ctx, const char* bam_path, const char* out_vcf_path,
                          int64_t window);
 int ngsep_call_population_bams_multi(ngsep_ctx* const* ctxs, int32_t n_ctx, const char* const* bam_paths, int32_t n_files,

@@ -1,8 +1,8 @@
 /*
  * ngsep_gpu_jni.c -- the JNI binding a NGSEPcore maintainer adds for ngsep.discovery.gpu.GpuPileupEngine
  * (INTEGRATION.md section 2 holds the Java class).  Every native forwards to one entry point of include/ngsep_gpu.h;
- * strings are UTF-8 copies, arrays are pinned with Get/ReleasePrimitiveArrayCritical around the call (the library
- * copies what it keeps), errors come back as the int status the Java side turns into an IOException with
+ * strings are UTF-8 copies, arrays are taken with Get<Type>ArrayElements around the call (released with JNI_ABORT;
+ * critical sections only around short copies), errors come back as the int status the Java side turns into an IOException with
  * ngsep_last_error.  Build (with a JDK):
  *   gcc -O2 -shared -fPIC -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -Iinclude jni/ngsep_gpu_jni.c \
  *       -Lngsepcore_amd/lib -lngsep_amd -Wl,-rpath,'$ORIGIN' -o libngsep_amd_jni.so
@@ -174,39 +174,49 @@ JNIEXPORT jint FN(callPopulationBamsMulti)(JNIEnv* env, jclass k, jlongArray con
     return rc;
 }
 
-/* path A: one batch of filtered, coordinate-sorted alignments (AlignmentsPileupGenerator.processAlignment) */
+/* path A: one batch of filtered, coordinate-sorted alignments (AlignmentsPileupGenerator.processAlignment).  The call
+ * projects the batch on every host thread and can wait on the device, far too long to hold critical sections (a JVM's
+ * GC would stall behind them): the arrays are taken with Get<Type>ArrayElements (a copy or a pin the GC can live with)
+ * and released with JNI_ABORT (nothing is written back).  A null element pointer (the JVM out of memory) throws
+ * OutOfMemoryError and returns NGSEP_E_INVALID. */
 JNIEXPORT jint FN(processAlignments)(JNIEnv* env, jclass k, jlong ctx, jintArray seqId, jintArray first, jintArray flags,
                                      jintArray rg, jlongArray cigOff, jintArray cigN, jintArray cig, jlongArray seqOff,
                                      jintArray seqLen, jbyteArray bases, jbyteArray quals, jbyteArray hasQ) {
     (void)k;
-    ngsep_read_batch b;
-    b.n_reads = (*env)->GetArrayLength(env, first);
-    /* critical sections: no other JNI call until every array is released */
-    b.seq_id = (const int32_t*)(*env)->GetPrimitiveArrayCritical(env, seqId, NULL);
-    b.first = (const int32_t*)(*env)->GetPrimitiveArrayCritical(env, first, NULL);
-    b.flags = (const int32_t*)(*env)->GetPrimitiveArrayCritical(env, flags, NULL);
-    b.read_group = (const int32_t*)(*env)->GetPrimitiveArrayCritical(env, rg, NULL);
-    b.cigar_off = (const int64_t*)(*env)->GetPrimitiveArrayCritical(env, cigOff, NULL);
-    b.cigar_n = (const int32_t*)(*env)->GetPrimitiveArrayCritical(env, cigN, NULL);
-    b.cigar = (const int32_t*)(*env)->GetPrimitiveArrayCritical(env, cig, NULL);
-    b.seq_off = (const int64_t*)(*env)->GetPrimitiveArrayCritical(env, seqOff, NULL);
-    b.seq_len = (const int32_t*)(*env)->GetPrimitiveArrayCritical(env, seqLen, NULL);
-    b.bases = (const char*)(*env)->GetPrimitiveArrayCritical(env, bases, NULL);
-    b.quals = quals ? (const char*)(*env)->GetPrimitiveArrayCritical(env, quals, NULL) : NULL;
-    b.has_quals = hasQ ? (const uint8_t*)(*env)->GetPrimitiveArrayCritical(env, hasQ, NULL) : NULL;
-    const int rc = ngsep_process_alignments(CTX(ctx), &b);
-    if (hasQ) (*env)->ReleasePrimitiveArrayCritical(env, hasQ, (void*)b.has_quals, JNI_ABORT);
-    if (quals) (*env)->ReleasePrimitiveArrayCritical(env, quals, (void*)b.quals, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, bases, (void*)b.bases, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, seqLen, (void*)b.seq_len, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, seqOff, (void*)b.seq_off, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, cig, (void*)b.cigar, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, cigN, (void*)b.cigar_n, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, cigOff, (void*)b.cigar_off, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, rg, (void*)b.read_group, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, flags, (void*)b.flags, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, first, (void*)b.first, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, seqId, (void*)b.seq_id, JNI_ABORT);
+    jintArray ia[] = {seqId, first, flags, rg, cigN, cig, seqLen};
+    jint* ie[7] = {NULL};
+    jlongArray la[] = {cigOff, seqOff};
+    jlong* le[2] = {NULL};
+    jbyteArray ba[] = {bases, quals, hasQ};
+    jbyte* be[3] = {NULL};
+    int ok = 1;
+    for (int i = 0; i < 7 && ok; i++) ok = (ie[i] = (*env)->GetIntArrayElements(env, ia[i], NULL)) != NULL;
+    for (int i = 0; i < 2 && ok; i++) ok = (le[i] = (*env)->GetLongArrayElements(env, la[i], NULL)) != NULL;
+    for (int i = 0; i < 3 && ok; i++) ok = !ba[i] || (be[i] = (*env)->GetByteArrayElements(env, ba[i], NULL)) != NULL;
+    int rc = NGSEP_E_INVALID;
+    if (ok) {
+        ngsep_read_batch b;
+        b.n_reads = (*env)->GetArrayLength(env, first);
+        b.seq_id = (const int32_t*)ie[0];
+        b.first = (const int32_t*)ie[1];
+        b.flags = (const int32_t*)ie[2];
+        b.read_group = (const int32_t*)ie[3];
+        b.cigar_off = (const int64_t*)le[0];
+        b.cigar_n = (const int32_t*)ie[4];
+        b.cigar = (const int32_t*)ie[5];
+        b.seq_off = (const int64_t*)le[1];
+        b.seq_len = (const int32_t*)ie[6];
+        b.bases = (const char*)be[0];
+        b.quals = (const char*)be[1];
+        b.has_quals = (const uint8_t*)be[2];
+        rc = ngsep_process_alignments(CTX(ctx), &b);
+    } else {
+        jclass oom = (*env)->FindClass(env, "java/lang/OutOfMemoryError");
+        if (oom) (*env)->ThrowNew(env, oom, "processAlignments: array elements could not be obtained");
+    }
+    for (int i = 0; i < 3; i++) if (be[i]) (*env)->ReleaseByteArrayElements(env, ba[i], be[i], JNI_ABORT);
+    for (int i = 0; i < 2; i++) if (le[i]) (*env)->ReleaseLongArrayElements(env, la[i], le[i], JNI_ABORT);
+    for (int i = 0; i < 7; i++) if (ie[i]) (*env)->ReleaseIntArrayElements(env, ia[i], ie[i], JNI_ABORT);
     return rc;
 }
 
@@ -216,23 +226,41 @@ JNIEXPORT jint FN(notifyEnd)(JNIEnv* env, jclass k, jlong ctx) {
     return ngsep_notify_end(CTX(ctx));
 }
 
-/* the called sites as packed ngsep_site_out records (152 B each, little endian) in a heap ByteBuffer */
+/* the called sites as packed ngsep_site_out records (152 B each) in a heap ByteBuffer whose order is set to
+ * ByteOrder.LITTLE_ENDIAN (the records' own; a wrapped buffer defaults to BIG_ENDIAN, which would byte-swap every
+ * getInt / getLong).  A failing fetch throws IOException (the method's declared exception) and returns null. */
 JNIEXPORT jobject FN(fetchSites)(JNIEnv* env, jclass k, jlong ctx) {
     (void)k;
     int64_t n = 0;
-    if (ngsep_fetch_sites(CTX(ctx), NULL, 0, &n) != NGSEP_OK) return NULL;
+    if (ngsep_fetch_sites(CTX(ctx), NULL, 0, &n) != NGSEP_OK) {
+        throw_io(env, ngsep_last_error(CTX(ctx)));
+        return NULL;
+    }
     ngsep_site_out* buf = (ngsep_site_out*)malloc((size_t)(n > 0 ? n : 1) * sizeof(ngsep_site_out));
-    if (!buf) return NULL;
-    ngsep_fetch_sites(CTX(ctx), buf, n, &n);
+    if (!buf) {
+        throw_io(env, "fetchSites: out of host memory");
+        return NULL;
+    }
+    if (ngsep_fetch_sites(CTX(ctx), buf, n, &n) != NGSEP_OK) {
+        free(buf);
+        throw_io(env, ngsep_last_error(CTX(ctx)));
+        return NULL;
+    }
     ngsep_clear_sites(CTX(ctx));
     const jsize bytes = (jsize)(n * (int64_t)sizeof(ngsep_site_out));
     jbyteArray arr = (*env)->NewByteArray(env, bytes);
     if (arr) (*env)->SetByteArrayRegion(env, arr, 0, bytes, (const jbyte*)buf);
     free(buf);
-    if (!arr) return NULL;
+    if (!arr) return NULL;                             /* (NewByteArray has thrown OutOfMemoryError) */
     jclass bb = (*env)->FindClass(env, "java/nio/ByteBuffer");
     jmethodID wrap = (*env)->GetStaticMethodID(env, bb, "wrap", "([B)Ljava/nio/ByteBuffer;");
-    return (*env)->CallStaticObjectMethod(env, bb, wrap, arr);
+    jobject buffer = (*env)->CallStaticObjectMethod(env, bb, wrap, arr);
+    if (!buffer) return NULL;
+    jclass bo = (*env)->FindClass(env, "java/nio/ByteOrder");
+    jfieldID lef = (*env)->GetStaticFieldID(env, bo, "LITTLE_ENDIAN", "Ljava/nio/ByteOrder;");
+    jobject le = (*env)->GetStaticObjectField(env, bo, lef);
+    jmethodID order = (*env)->GetMethodID(env, bb, "order", "(Ljava/nio/ByteOrder;)Ljava/nio/ByteBuffer;");
+    return (*env)->CallObjectMethod(env, buffer, order, le);
 }
 
 /* the VCF text of fetched record i (indel / STR records, ABI 6) */
@@ -304,10 +332,12 @@ JNIEXPORT jint FN(fetchCoverage)(JNIEnv* env, jclass k, jlong ctx, jlongArray co
     jlong* c = (jlong*)(*env)->GetPrimitiveArrayCritical(env, counts, NULL);
     jlong* u = (jlong*)(*env)->GetPrimitiveArrayCritical(env, unique, NULL);
     jlong* m = (jlong*)(*env)->GetPrimitiveArrayCritical(env, more, NULL);
-    const int rc = ngsep_fetch_coverage(CTX(ctx), (int64_t*)c, (int64_t*)u, (int64_t*)&m[0], (int64_t*)&m[1]);
-    (*env)->ReleasePrimitiveArrayCritical(env, more, m, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, unique, u, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, counts, c, 0);
+    /* (a short copy of the histograms: critical sections are fine here) */
+    const int rc = c && u && m ? ngsep_fetch_coverage(CTX(ctx), (int64_t*)c, (int64_t*)u, (int64_t*)&m[0], (int64_t*)&m[1])
+                               : NGSEP_E_INVALID;
+    if (m) (*env)->ReleasePrimitiveArrayCritical(env, more, m, 0);
+    if (u) (*env)->ReleasePrimitiveArrayCritical(env, unique, u, 0);
+    if (c) (*env)->ReleasePrimitiveArrayCritical(env, counts, c, 0);
     return rc;
 }
 
@@ -325,9 +355,9 @@ JNIEXPORT jint FN(fetchRac)(JNIEnv* env, jclass k, jlong ctx, jdoubleArray prop,
     double* p = (double*)(*env)->GetPrimitiveArrayCritical(env, prop, NULL);
     double* a = (double*)(*env)->GetPrimitiveArrayCritical(env, nAlleles, NULL);
     double* m = (double*)(*env)->GetPrimitiveArrayCritical(env, moments, NULL);
-    const int rc = ngsep_fetch_rac(CTX(ctx), p, a, m);
-    (*env)->ReleasePrimitiveArrayCritical(env, moments, m, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, nAlleles, a, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, prop, p, 0);
+    const int rc = p && a && m ? ngsep_fetch_rac(CTX(ctx), p, a, m) : NGSEP_E_INVALID;
+    if (m) (*env)->ReleasePrimitiveArrayCritical(env, moments, m, 0);
+    if (a) (*env)->ReleasePrimitiveArrayCritical(env, nAlleles, a, 0);
+    if (p) (*env)->ReleasePrimitiveArrayCritical(env, prop, p, 0);
     return rc;
 }

@@ -1744,6 +1744,30 @@ static inline void fill_group_units(uint64_t* dst, int32_t K, const uint8_t* con
 // device_units (streamed windows): the units are built on the device (kernels.hip k_build_units) from the reads'
 // projected bytes, copied here back to back into the arena (runs of reads adjacent in their projection chunk: one copy)
 // -- a copy instead of the 64-lane transposition with its reference XOR, which cost the window worker ~10 ms a window
+// out[e] = max(glast of entries 0 .. e) (non-decreasing: the first entry reaching a position is a lower_bound), on all
+// threads (per-chunk maxima, then the chunks' carried maxima)
+template <class F>
+static void prefix_max_glast(int64_t n, F&& glast, int32_t* out) {
+    if (n <= 0) return;
+    const int64_t kChunk = 1 << 16, nch = (n + kChunk - 1) / kChunk;
+    std::vector<int32_t> cmax((size_t)nch, INT32_MIN);
+    parallel_for(nch, 1, [&](int64_t c0, int64_t c1) {
+        for (int64_t c = c0; c < c1; c++) {
+            int32_t m = INT32_MIN;
+            for (int64_t e = c * kChunk; e < std::min(n, (c + 1) * kChunk); e++) m = std::max<int32_t>(m, glast(e));
+            cmax[(size_t)c] = m;
+        }
+    });
+    std::vector<int32_t> carry((size_t)nch, INT32_MIN);
+    for (int64_t c = 1; c < nch; c++) carry[(size_t)c] = std::max(carry[(size_t)c - 1], cmax[(size_t)c - 1]);
+    parallel_for(nch, 1, [&](int64_t c0, int64_t c1) {
+        for (int64_t c = c0; c < c1; c++) {
+            int32_t m = carry[(size_t)c];
+            for (int64_t e = c * kChunk; e < std::min(n, (c + 1) * kChunk); e++) out[e] = m = std::max<int32_t>(m, glast(e));
+        }
+    });
+}
+
 static int build_rg_layout(Staged& s, const RawVec<SRead>& reads, LayoutArena& arena, bool exact,
                            const std::function<void(int64_t)>& consumed = nullptr, bool device_units = false) {
     static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
@@ -1848,20 +1872,26 @@ static int build_rg_layout(Staged& s, const RawVec<SRead>& reads, LayoutArena& a
     if (consumed) consumed(std::min(n, sb * 64));
     }
     }
-    // block tables over the global coordinate (reads are sorted by gfirst)
+    // block tables over the global coordinate (reads are sorted by gfirst).  blkA[b]: the first entry whose glast
+    // reaches block b (every earlier entry ends before it), capped by blkB[b] -- the first entry with a prefix maximum of
+    // glast at or past the block's start, so one long (or spliced) alignment widens only the blocks it spans, not every
+    // block by the run's longest span
     const int64_t nb = (s.g_len >> kRgBlockShift) + 2;
     s.h_blkA.resize((size_t)nb);
     s.h_blkB.resize((size_t)nb);
+    std::vector<int32_t> pmax((size_t)n);
+    prefix_max_glast(n, [&](int64_t e) { return reads[(size_t)e].glast; }, pmax.data());
     parallel_for(nb, 1 << 14, [&](int64_t b0, int64_t b1) {
         auto first_at = [&](int64_t v) {          // first read with gfirst >= v
             return (int32_t)(std::lower_bound(reads.begin(), reads.end(), v, [](const SRead& r, int64_t x) { return (int64_t)r.gfirst < x; }) - reads.begin());
         };
-        int64_t ia = first_at((b0 << kRgBlockShift) - s.max_span + 1), ib = first_at(b0 << kRgBlockShift);
+        int64_t ia = std::lower_bound(pmax.begin(), pmax.end(), (int32_t)(b0 << kRgBlockShift)) - pmax.begin();
+        int64_t ib = first_at(b0 << kRgBlockShift);
         for (int64_t b = b0; b < b1; b++) {
-            const int64_t va = (b << kRgBlockShift) - s.max_span + 1, vb = b << kRgBlockShift;
-            while (ia < n && (int64_t)reads[(size_t)ia].gfirst < va) ia++;
+            const int64_t vb = b << kRgBlockShift;
+            while (ia < n && (int64_t)pmax[(size_t)ia] < vb) ia++;
             while (ib < n && (int64_t)reads[(size_t)ib].gfirst < vb) ib++;
-            s.h_blkA[(size_t)b] = (int32_t)ia;
+            s.h_blkA[(size_t)b] = (int32_t)std::min(ia, ib);
             s.h_blkB[(size_t)b] = (int32_t)ib;
         }
     });
@@ -2072,17 +2102,22 @@ static int build_pop_rg_layout(Staged& s, LayoutArena& arena) {
     s.pnblk = nb;
     s.h_blkA.resize((size_t)(nb * nst));               // (every entry written below)
     s.h_blkB.resize((size_t)(nb * nst));
-    const int64_t ms = s.max_span;
+    // blkA: the stream's first entry whose glast reaches the block (a running maximum of glast, as the single-sample
+    // tables: one long alignment widens only the blocks it spans), capped by blkB
     parallel_for(nst, 1, [&](int64_t a, int64_t b) {
         for (int64_t st = a; st < b; st++) {
             const int64_t m = st_n[(size_t)st], eb = st_e0[(size_t)st];
             const int32_t* o = &ord[(size_t)st_r0[(size_t)st]];
             int64_t ia = 0, ib = 0;
+            int64_t pm = INT64_MIN;                            // max glast of the stream's entries [0, ia)
             for (int64_t k = 0; k < nb; k++) {
-                const int64_t va = (k << shift) - ms + 1, vb = k << shift;
-                while (ia < m && (int64_t)R[(int64_t)o[ia] * 4] < va) ia++;
+                const int64_t vb = k << shift;
+                while (ia < m && std::max<int64_t>(pm, (int64_t)R[(int64_t)o[ia] * 4 + 1]) < vb) {
+                    pm = std::max<int64_t>(pm, (int64_t)R[(int64_t)o[ia] * 4 + 1]);
+                    ia++;
+                }
                 while (ib < m && (int64_t)R[(int64_t)o[ib] * 4] < vb) ib++;
-                s.h_blkA[(size_t)(st * nb + k)] = (int32_t)(eb + ia);
+                s.h_blkA[(size_t)(st * nb + k)] = (int32_t)(eb + std::min(ia, ib));
                 s.h_blkB[(size_t)(st * nb + k)] = (int32_t)(eb + ib);
             }
         }

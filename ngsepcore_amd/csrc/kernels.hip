@@ -895,12 +895,6 @@ constexpr int kKlThreads = 256;
 #ifndef NGSEP_KL_UNROLL
 #define NGSEP_KL_UNROLL 4
 #endif
-#ifndef NGSEP_KL_PIPE
-#define NGSEP_KL_PIPE 1     // the next batch's loads issued before the current batch's counters (0: A/B builds)
-#endif
-#ifndef NGSEP_KL_GPRE
-#define NGSEP_KL_GPRE 1     // the next group's unit offset fetched with its headers (0: A/B builds)
-#endif
 constexpr int kKlUnroll = NGSEP_KL_UNROLL;
 // units allocated past a layout's last group: KL's and KLM's next-batch loads are unconditional and may read up to
 // 2 x 4 - 1 rows past a read's last unit, the last group's included (never used, only loaded)
@@ -975,16 +969,12 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
     const bool no_counts = ABLATE(ablate, 128), no_units = ABLATE(ablate, 256);   // diagnostics
     int64_t g = g_lo + wv;
     int2 h = g < g_hi ? rh[g * 64 + lane] : make_int2(0, 0);
-#if NGSEP_KL_GPRE
     RGroup Gc = g < g_hi ? grp[g] : RGroup{0, 0, 0};
-#endif
     for (; g < g_hi; g += kKlThreads / 64) {
         const int64_t e = g * 64 + lane;
         const int2 hn = g + kKlThreads / 64 < g_hi ? rh[e + kKlThreads] : make_int2(0, 0);   // the next group's headers in flight
-#if NGSEP_KL_GPRE
         const RGroup G = Gc;                                // and its unit offset
         Gc = g + kKlThreads / 64 < g_hi ? grp[g + kKlThreads / 64] : RGroup{0, 0, 0};
-#endif
         const int32_t gf = h.x, gl = h.y & 0x7FFFFFFF;
         const int32_t a = max(gf, tstart), b = min(gl, tstart + T - 1);
         const bool act = e >= e_lo && e < e_hi && a <= b;
@@ -992,9 +982,6 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
             atomicAdd(&s_diff[a - tstart], 1);
             atomicAdd(&s_diff[b - tstart + 1], -1);
         }
-#if !NGSEP_KL_GPRE
-        const RGroup G = grp[g];
-#endif
         const int32_t k0 = act ? (a - gf) >> 3 : 0, kn = act && !no_units ? ((b - gf) >> 3) - k0 : -1;   // units k0 .. k0 + kn
         const int32_t ob0 = gf - tstart + 8 * k0 + 8;     // counter index of unit k0's byte 0 (>= 1)
         const int sh = (ob0 & 1) << 1;                    // !DEEP: byte offset of the unit's first halfword
@@ -1002,7 +989,6 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
         // a lane's own trip count (the wave runs while any lane has units left); loads are unconditional (a
         // batch's slots past the read's last unit repeat it) so that each unit waits for its own load only
 #define KL_LOAD(q) (q)                                    // (nontemporal loads measured no change)
-#if NGSEP_KL_PIPE
         // (the next batch's loads unconditional, past the read's end too -- other reads' rows or the buffer's slack,
         // never used: a load under a lane condition made the compiler wait for every outstanding load, the next
         // batch's included, before the current batch)
@@ -1016,12 +1002,6 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
             uint64_t v[U];
 #pragma unroll
             for (int i = 0; i < U; i++) v[i] = KL_LOAD(ub[(int64_t)min(j + U + i, lim) * 64]);
-#else
-        for (int32_t j = 0; j <= kn; j += U) {
-            uint64_t u[U];
-#pragma unroll
-            for (int i = 0; i < U; i++) u[i] = KL_LOAD(ub[(int64_t)min(j + i, kn) * 64]);
-#endif
 #pragma unroll
             for (int i = 0; i < U; i++) {
                 if (j + i > kn) continue;
@@ -1065,24 +1045,16 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
                     }
                 }
             }
-#if NGSEP_KL_PIPE
 #pragma unroll
             for (int i = 0; i < U; i++) u[i] = v[i];
-#endif
         }
 #undef KL_LOAD
         h = hn;
     }
 }
 
-#ifndef NGSEP_KL_WPE
-#define NGSEP_KL_WPE 8      // 8 waves per SIMD: the pipelined stream's registers capped at 64 (0: the compiler's choice)
-#endif
-#if NGSEP_KL_WPE
-#define KL_WPE_ATTR __attribute__((amdgpu_waves_per_eu(NGSEP_KL_WPE)))
-#else
-#define KL_WPE_ATTR
-#endif
+// 8 waves per SIMD: the pipelined stream's registers capped at 64
+#define KL_WPE_ATTR __attribute__((amdgpu_waves_per_eu(8)))
 template <int T, int U>
 __global__ __launch_bounds__(kKlThreads) KL_WPE_ATTR void k_read_scan(
     const uint64_t* __restrict__ units, const int2* __restrict__ rh, const RGroup* __restrict__ grp,
@@ -2241,12 +2213,10 @@ __device__ __forceinline__ PopCall genotype_sample_d(const LA& L, const int* cnt
 // after stream, pending order inside -- into dst (at most cap codes; the host sizes cap by the sample's coverage
 // bound).  Entries are walked from the stream's block-table entry eight headers at a time (their two possible
 // groups' bases loaded alongside), the covering ones' unit loads issued together.
+// The next header batch is loaded while this batch's unit dwords are in flight (configs[4] KPM 0.484-0.485 ->
+// 0.423-0.425 ms A/B on one box, tools/history/gpu_r4_klmabn.sh).
 #ifndef NGSEP_KPM_GBATCH
 #define NGSEP_KPM_GBATCH 8   // entry headers a gathering thread loads at once
-#endif
-#ifndef NGSEP_KPM_GPIPE
-#define NGSEP_KPM_GPIPE 1    // the gather's next header batch loaded while this batch's units are in flight (configs[4]
-                             // KPM 0.484-0.485 -> 0.423-0.425 ms A/B on one box, tools/gpu_r4_klmabn.sh)
 #endif
 struct PopGather {
     const uint64_t* units;
@@ -2269,22 +2239,15 @@ __device__ inline int32_t pop_gather(const PopGather& pg, int32_t p, int s, uint
         int64_t e = pg.blkA[(int64_t)st * pg.nblk + (p >> pg.shift)];
         const int64_t end = pg.st_end[st];
         bool done = false;
-#if NGSEP_KPM_GPIPE
         // the next batch's headers are loaded while this batch's unit dwords are in flight (when this batch's last
         // header still starts at or before p, i.e. the next batch can hold covering reads)
         int2 hn[kGatherBatch];
 #pragma unroll
         for (int i = 0; i < kGatherBatch; i++) hn[i] = e + i < end ? pg.rh[e + i] : make_int2(0x7FFFFFFF, 0);
-#endif
         while (!done && e < end) {
             int2 h[kGatherBatch];
-#if NGSEP_KPM_GPIPE
 #pragma unroll
             for (int i = 0; i < kGatherBatch; i++) h[i] = hn[i];
-#else
-#pragma unroll
-            for (int i = 0; i < kGatherBatch; i++) h[i] = e + i < end ? pg.rh[e + i] : make_int2(0x7FFFFFFF, 0);
-#endif
             const int64_t g0 = e >> 6;
             const int64_t gb0 = pg.grp[g0].base;
             const int64_t gb1 = ((e + kGatherBatch - 1) >> 6) != g0 && ((g0 + 1) << 6) < end ? pg.grp[g0 + 1].base : gb0;
@@ -2300,13 +2263,11 @@ __device__ inline int32_t pop_gather(const PopGather& pg, int32_t p, int s, uint
                     u[i] = uw[(o >> 2) & 1];
                 }
             }
-#if NGSEP_KPM_GPIPE
             if (h[kGatherBatch - 1].x <= p) {
 #pragma unroll
                 for (int i = 0; i < kGatherBatch; i++)
                     hn[i] = e + kGatherBatch + i < end ? pg.rh[e + kGatherBatch + i] : make_int2(0x7FFFFFFF, 0);
             }
-#endif
 #pragma unroll
             for (int i = 0; i < kGatherBatch; i++) {
                 const int32_t gf = h[i].x, gl = h[i].y & 0x7FFFFFFF;

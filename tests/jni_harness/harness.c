@@ -3,6 +3,7 @@
  * jni/ngsep_gpu_jni.c, so tests/test_jni_shim.py can drive the shim the way the JVM would (Java strings, int[] /
  * long[] / String[] arrays, exceptions) from ctypes.  Objects are tagged heap blocks; nothing here is product code.
  */
+#include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -114,12 +115,40 @@ static jobject e_CallStaticObjectMethod(JNIEnv* env, jclass k, jmethodID m, ...)
     return arr;
 }
 
+static jbyte* e_GetByteArrayElements(JNIEnv* env, jbyteArray a, jboolean* copy) { (void)env; if (copy) *copy = 1; return (jbyte*)get_copy(a); }
+static void e_ReleaseByteArrayElements(JNIEnv* env, jbyteArray a, jbyte* c, jint mode) { (void)env; release_copy(a, c, mode); }
+/* ByteOrder.LITTLE_ENDIAN (a static field) and ByteBuffer.order(ByteOrder): the order set is recorded */
+static int g_order_le;
+static jfieldID e_GetStaticFieldID(JNIEnv* env, jclass k, const char* n, const char* sig) {
+    (void)env; (void)k; (void)sig;
+    return (jfieldID)(intptr_t)(strcmp(n, "LITTLE_ENDIAN") == 0 ? 2 : 3);
+}
+static jobject e_GetStaticObjectField(JNIEnv* env, jclass k, jfieldID f) {
+    (void)env; (void)k;
+    static struct _jobject le = {K_CLASS, 0, NULL, "LITTLE_ENDIAN"}, be = {K_CLASS, 0, NULL, "BIG_ENDIAN"};
+    return (intptr_t)f == 2 ? &le : &be;
+}
+static jmethodID e_GetMethodID(JNIEnv* env, jclass k, const char* n, const char* sig) {
+    (void)env; (void)k; (void)n; (void)sig;
+    return (jmethodID)(intptr_t)4;
+}
+static jobject e_CallObjectMethod(JNIEnv* env, jobject o, jmethodID m, ...) {
+    (void)env; (void)m;
+    va_list ap;
+    va_start(ap, m);
+    jobject arg = va_arg(ap, jobject);
+    va_end(ap);
+    g_order_le = arg && strcmp(arg->name, "LITTLE_ENDIAN") == 0;
+    return o;
+}
+
 static const struct JNINativeInterface_ g_table = {
     e_FindClass, e_ThrowNew, e_NewStringUTF, e_GetStringUTFChars, e_ReleaseStringUTFChars, e_GetArrayLength,
     e_NewObjectArray, e_GetObjectArrayElement, e_SetObjectArrayElement, e_NewByteArray, e_NewLongArray,
     e_GetIntArrayElements, e_ReleaseIntArrayElements, e_GetLongArrayElements, e_ReleaseLongArrayElements,
     e_SetByteArrayRegion, e_SetLongArrayRegion, e_GetPrimitiveArrayCritical, e_ReleasePrimitiveArrayCritical,
-    e_GetStaticMethodID, e_CallStaticObjectMethod};
+    e_GetStaticMethodID, e_CallStaticObjectMethod, e_GetByteArrayElements, e_ReleaseByteArrayElements,
+    e_GetStaticFieldID, e_GetStaticObjectField, e_GetMethodID, e_CallObjectMethod};
 static JNIEnv g_env = &g_table;
 
 /* ---- the natives (jni/ngsep_gpu_jni.c) ---- */
@@ -136,6 +165,10 @@ jint NAT(callPopulationBamsMulti)(JNIEnv*, jclass, jlongArray, jobjectArray, jst
 jint NAT(setKnownVariants)(JNIEnv*, jclass, jlong, jstring);
 jint NAT(setKnownSTRs)(JNIEnv*, jclass, jlong, jstring);
 jobjectArray NAT(carvedRegions)(JNIEnv*, jclass, jlong);
+jint NAT(processAlignments)(JNIEnv*, jclass, jlong, jintArray, jintArray, jintArray, jintArray, jlongArray, jintArray,
+                            jintArray, jlongArray, jintArray, jbyteArray, jbyteArray, jbyteArray);
+jint NAT(notifyEnd)(JNIEnv*, jclass, jlong);
+jobject NAT(fetchSites)(JNIEnv*, jclass, jlong);
 
 /* ---- a plain C API for ctypes ---- */
 static jstring js(const char* s) { return s ? e_NewStringUTF(&g_env, s) : NULL; }
@@ -228,5 +261,44 @@ int64_t h_carved_regions(int64_t ctx, int64_t* out, int64_t cap) {
     const jsize n = a->len;
     for (jsize i = 0; i < n && i < cap; i++) memcpy(out + 3 * i, ((jobject*)a->data)[i]->data, 3 * sizeof(int64_t));
     drop(a);
+    return n;
+}
+
+/* processAlignments over a batch given as plain arrays (every array copied into a Java array first) */
+static jintArray jints(const int32_t* v, int n) {
+    jintArray a = make(K_INTS, n, 4);
+    if (v) memcpy(a->data, v, (size_t)n * 4);
+    return a;
+}
+static jbyteArray jbytes(const void* v, int64_t n) {
+    jbyteArray a = make(K_BYTES, (jsize)n, 1);
+    if (v) memcpy(a->data, v, (size_t)n);
+    return a;
+}
+int h_process_alignments(int64_t ctx, int n, const int32_t* seq_id, const int32_t* first, const int32_t* flags,
+                         const int32_t* rg, const int64_t* cig_off, const int32_t* cig_n, const int32_t* cig, int n_cig,
+                         const int64_t* seq_off, const int32_t* seq_len, const char* bases, const char* quals, int64_t n_bases,
+                         const uint8_t* has_q) {
+    jintArray a0 = jints(seq_id, n), a1 = jints(first, n), a2 = jints(flags, n), a3 = jints(rg, n);
+    jlongArray a4 = jlongs(cig_off, n);
+    jintArray a5 = jints(cig_n, n), a6 = jints(cig, n_cig);
+    jlongArray a7 = jlongs(seq_off, n);
+    jintArray a8 = jints(seq_len, n);
+    jbyteArray a9 = jbytes(bases, n_bases), a10 = jbytes(quals, n_bases), a11 = jbytes(has_q, n);
+    const int rc = NAT(processAlignments)(&g_env, NULL, ctx, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11);
+    drop(a0); drop(a1); drop(a2); drop(a3); drop(a4); drop(a5); drop(a6); drop(a7); drop(a8); drop(a9); drop(a10); drop(a11);
+    return rc;
+}
+int h_notify_end(int64_t ctx) { return NAT(notifyEnd)(&g_env, NULL, ctx); }
+/* fetchSites: the records' bytes into out (cap bytes); their byte count (-1: null returned); *le = the buffer's order
+   was set to LITTLE_ENDIAN */
+int64_t h_fetch_sites(int64_t ctx, void* out, int64_t cap, int* le) {
+    g_order_le = 0;
+    jobject b = NAT(fetchSites)(&g_env, NULL, ctx);
+    *le = g_order_le;
+    if (!b) return -1;
+    const int64_t n = b->len;
+    memcpy(out, b->data, (size_t)(n < cap ? n : cap));
+    drop(b);
     return n;
 }

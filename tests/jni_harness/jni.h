@@ -23,6 +23,7 @@ typedef struct _jobject* jobject;
 typedef jobject jclass, jstring, jarray, jthrowable;
 typedef jarray jintArray, jlongArray, jbyteArray, jdoubleArray, jobjectArray;
 typedef struct _jmethodID* jmethodID;
+typedef struct _jfieldID* jfieldID;
 
 struct JNINativeInterface_;
 typedef const struct JNINativeInterface_* JNIEnv;
@@ -48,5 +49,11 @@ struct JNINativeInterface_ {
     void (*ReleasePrimitiveArrayCritical)(JNIEnv*, jarray, void*, jint);
     jmethodID (*GetStaticMethodID)(JNIEnv*, jclass, const char*, const char*);
     jobject (*CallStaticObjectMethod)(JNIEnv*, jclass, jmethodID, ...);
+    jbyte* (*GetByteArrayElements)(JNIEnv*, jbyteArray, jboolean*);
+    void (*ReleaseByteArrayElements)(JNIEnv*, jbyteArray, jbyte*, jint);
+    jfieldID (*GetStaticFieldID)(JNIEnv*, jclass, const char*, const char*);
+    jobject (*GetStaticObjectField)(JNIEnv*, jclass, jfieldID);
+    jmethodID (*GetMethodID)(JNIEnv*, jclass, const char*, const char*);
+    jobject (*CallObjectMethod)(JNIEnv*, jobject, jmethodID, ...);
 };
 #endif

@@ -32,7 +32,55 @@ def harness():
     l.h_call_population_bams_multi.argtypes = [ctypes.POINTER(I64), ctypes.c_int, ctypes.POINTER(CP), ctypes.c_int, CP, I64]
     l.h_carved_regions.restype = I64
     l.h_carved_regions.argtypes = [I64, ctypes.POINTER(I64), I64]
+    P = ctypes.POINTER
+    l.h_process_alignments.argtypes = [I64, ctypes.c_int, P(I32), P(I32), P(I32), P(I32), P(I64), P(I32), P(I32),
+                                       ctypes.c_int, P(I64), P(I32), ctypes.c_void_p, ctypes.c_void_p, I64,
+                                       P(ctypes.c_uint8)]
+    l.h_notify_end.argtypes = [I64]
+    l.h_fetch_sites.restype = I64
+    l.h_fetch_sites.argtypes = [I64, ctypes.c_void_p, I64, P(ctypes.c_int)]
     return l
+
+
+def shim_path_a(l, ctx, batch):
+    """processAlignments (the batch copied into Java arrays) + notifyEnd + fetchSites through the natives: the sites'
+    bytes and whether the buffer's order was set to LITTLE_ENDIAN"""
+    import numpy as np
+    n = batch.n_reads
+    def arr(ptr, k, t):
+        return np.ctypeslib.as_array(ptr, shape=(k,)).astype(t)
+    cig_off = arr(batch.cigar_off, n, np.int64)
+    cig_n = arr(batch.cigar_n, n, np.int32)
+    n_cig = int((cig_off + cig_n).max()) if n else 0
+    seq_off = arr(batch.seq_off, n, np.int64)
+    seq_len = arr(batch.seq_len, n, np.int32)
+    n_bases = int((seq_off + seq_len).max()) if n else 0
+    keep = []
+    def p(a, t):
+        a = np.ascontiguousarray(a, dtype=t)
+        keep.append(a)
+        return a.ctypes.data_as(ctypes.POINTER(t if t is not np.int64 else I64))
+    P32 = lambda a: p(a, np.int32)
+    bases_p = ctypes.c_void_p.from_buffer(batch, type(batch).bases.offset).value
+    quals_p = ctypes.c_void_p.from_buffer(batch, type(batch).quals.offset).value
+    hq = np.ascontiguousarray(arr(batch.has_quals, n, np.uint8))
+    rc = l.h_process_alignments(ctx, n, P32(arr(batch.seq_id, n, np.int32)), P32(arr(batch.first, n, np.int32)),
+                                P32(arr(batch.flags, n, np.int32)), P32(arr(batch.read_group, n, np.int32)),
+                                cig_off.ctypes.data_as(ctypes.POINTER(I64)), P32(cig_n),
+                                P32(np.ctypeslib.as_array(batch.cigar, shape=(n_cig,))), n_cig,
+                                seq_off.ctypes.data_as(ctypes.POINTER(I64)), P32(seq_len), bases_p, quals_p, n_bases,
+                                hq.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+    if rc != 0:
+        return rc, None, 0
+    rc = l.h_notify_end(ctx)
+    if rc != 0:
+        return rc, None, 0
+    le = ctypes.c_int(0)
+    m = l.h_fetch_sites(ctx, None, 0, ctypes.byref(le))
+    buf = ctypes.create_string_buffer(max(1, m))
+    le = ctypes.c_int(0)
+    m2 = l.h_fetch_sites(ctx, buf, m, ctypes.byref(le)) if m > 0 else m
+    return 0, buf.raw[:max(0, m2)] if m > 0 else b"", le.value
 
 
 def options(**kw):
@@ -70,6 +118,9 @@ def test_shim_cpu_paths(tmp_path):
         assert err(l, ctx)
     cr = (I64 * 3)()
     assert l.h_carved_regions(ctx, cr, 1) == 0
+    # fetchSites on a context without calls: an empty buffer, its order set to LITTLE_ENDIAN, no exception
+    le = ctypes.c_int(0)
+    assert l.h_fetch_sites(ctx, None, 0, ctypes.byref(le)) == 0 and le.value == 1 and l.h_exception() == b""
     l.h_close(ctx)
     # an option the library refuses: ngsep_open throws IOException through the shim and returns 0
     o, n = options(ploidy=500)
@@ -102,6 +153,25 @@ def test_shim_gpu_runs_equal_library(tmp_path):
     assert open(multi).read() == open(want).read()
     l.h_close(ctx)
     l.h_close(ctx2)
+    # path A through the natives (processAlignments with Get<Type>ArrayElements, notifyEnd, fetchSites): the records,
+    # read little endian from the returned buffer, are the library's own calls (the VCF's positions)
+    import struct
+    syn = pysynth.Synth(genome=pysynth.CUSTOM, custom_len=60000, seed=94, depth=15, snv_rate=2e-3)
+    fa2, sam2, bam2 = syn.write(os.path.join(str(tmp_path), "a"))
+    want2 = os.path.join(str(tmp_path), "a_lib.vcf")
+    with GpuPileupSession() as s:
+        s.load_fasta(fa2)
+        s.processFile(bam2, want2)
+    ctx = l.h_open(0, o, n, 0.001, None, None)
+    assert l.h_load_fasta(ctx, fa2.encode()) == 0
+    rc, raw, le = shim_path_a(l, ctx, syn.batch())
+    assert rc == 0, err(l, ctx)
+    assert le == 1
+    recs = [struct.unpack_from("<ii", raw, k) for k in range(0, len(raw), 152)]
+    vcf_pos = [int(x.split("\t")[1]) for x in open(want2) if not x.startswith("#")]
+    assert [p for _, p in recs] == vcf_pos and len(vcf_pos) > 50
+    l.h_close(ctx)
+    syn.close()
     # MultisampleVariantsDetector through callPopulationBams
     syn = pysynth.Synth(genome=pysynth.CUSTOM, custom_len=40000, seed=93, depth=8, snv_rate=3e-3, n_samples=6)
     fa, sam, _ = syn.write(os.path.join(str(tmp_path), "p"))
