@@ -56,11 +56,11 @@ def shim_path_a(l, ctx, batch):
     seq_len = arr(batch.seq_len, n, np.int32)
     n_bases = int((seq_off + seq_len).max()) if n else 0
     keep = []
-    def p(a, t):
-        a = np.ascontiguousarray(a, dtype=t)
+
+    def P32(a):
+        a = np.ascontiguousarray(a, dtype=np.int32)
         keep.append(a)
-        return a.ctypes.data_as(ctypes.POINTER(t if t is not np.int64 else I64))
-    P32 = lambda a: p(a, np.int32)
+        return a.ctypes.data_as(ctypes.POINTER(I32))
     bases_p = ctypes.c_void_p.from_buffer(batch, type(batch).bases.offset).value
     quals_p = ctypes.c_void_p.from_buffer(batch, type(batch).quals.offset).value
     hq = np.ascontiguousarray(arr(batch.has_quals, n, np.uint8))
@@ -75,12 +75,13 @@ def shim_path_a(l, ctx, batch):
     rc = l.h_notify_end(ctx)
     if rc != 0:
         return rc, None, 0
+    # (fetchSites hands the records over once and clears them: one call with room for them all)
+    cap = 152 * (1 << 16)
+    buf = ctypes.create_string_buffer(cap)
     le = ctypes.c_int(0)
-    m = l.h_fetch_sites(ctx, None, 0, ctypes.byref(le))
-    buf = ctypes.create_string_buffer(max(1, m))
-    le = ctypes.c_int(0)
-    m2 = l.h_fetch_sites(ctx, buf, m, ctypes.byref(le)) if m > 0 else m
-    return 0, buf.raw[:max(0, m2)] if m > 0 else b"", le.value
+    m = l.h_fetch_sites(ctx, buf, cap, ctypes.byref(le))
+    assert m <= cap
+    return 0, buf.raw[:max(0, m)], le.value
 
 
 def options(**kw):
@@ -121,6 +122,16 @@ def test_shim_cpu_paths(tmp_path):
     # fetchSites on a context without calls: an empty buffer, its order set to LITTLE_ENDIAN, no exception
     le = ctypes.c_int(0)
     assert l.h_fetch_sites(ctx, None, 0, ctypes.byref(le)) == 0 and le.value == 1 and l.h_exception() == b""
+    l.h_close(ctx)
+    # processAlignments' marshalling (the twelve arrays through Get<Type>ArrayElements): without a device the batch is
+    # refused with NGSEP_E_DEVICE or buffered, never an OutOfMemoryError
+    syn = pysynth.Synth(genome=pysynth.CUSTOM, custom_len=20000, seed=91, depth=6)
+    o, n = options()
+    ctx = l.h_open(0, o, n, 0.001, None, None)
+    assert l.h_load_fasta(ctx, fa.encode()) == 0
+    rc, _, _ = shim_path_a(l, ctx, syn.batch())
+    syn.close()
+    assert rc in (0, -4) and b"OutOfMemoryError" not in l.h_exception()
     l.h_close(ctx)
     # an option the library refuses: ngsep_open throws IOException through the shim and returns 0
     o, n = options(ploidy=500)
