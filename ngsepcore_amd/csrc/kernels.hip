@@ -1441,32 +1441,34 @@ __global__ __launch_bounds__(256) void k_queue_need(const uint32_t* __restrict__
 // non-reference call there, and one whose valid calls the exact integer bound (§5) proves hom-ref cannot either
 // (SingleSampleVariantPileupListener.genotypeVariantSample, :361-391); a position where every sample is so proven
 // gets variant QS 0, which MultisampleVariantsDetector.onPileup never writes (:534).  Per sample tile:
-//   pass 1: the wave streams the sample's units over the tile (its read-group streams in turn; lane = read, as KL),
-//           marks the positions holding a valid call of another allele (SWAR, kl_nonref) in an LDS bitmap (a second
-//           bitmap: marked twice) and, COUNT, tallies per position the bytes that are not a valid reference call of
-//           quality >= kKlmQs (packed byte counters, three LDS adds per unit that has one) and the reads' coverage
-//           (signed byte differences, two adds per read);
-//   count:  COUNT, a callable position marked once whose counted reference calls (coverage - exceptions) reach the
-//           count bound cb_hi1 is hom-ref for this sample: unmarked (about 97 % of the marked columns at 10x);
+//   pass 1: the wave streams the sample's units over the tile (its read-group streams in turn; lane = read, as KL).
+//           COUNT: per position two byte counters, the valid reference calls of quality >= kKlmQs and the valid calls of
+//           another allele (SWAR flags, klm_flags; three LDS adds per unit each, no branch: at 64 lanes nearly every
+//           unit holds one).  !COUNT: the positions holding a valid call of another allele marked in an LDS bitmap;
+//   count:  COUNT, a callable position with one call of another allele is a candidate the count bound may drop: its
+//           counted reference calls reaching cb_hi1 make it hom-ref for this sample (about 97 % of the candidate
+//           columns at 10x); positions with two or more stay;
 //   slots:  the positions still marked get LDS slots in position order;
 //   pass 2: every lane adds the weights of its read's valid calls at the slotted positions it covers (one 8-byte
 //           reload each) into its slot's {ref, alt 1, alt 2, alt 3} sums -- the exact integer bound;
 //   pass 3: a slot the bound cannot prove hom-ref -- or holding more than kMcMaxCalls valid calls, or past
 //           kKlmSlots -- keeps its position open: one bit per global position (atomicOr); KQN queues them for KPM.
 // COUNT needs every sample's coverage over the tile below 128 (the host's per-tile bound, engine.cpp build_pop_rg_layout):
-// the byte counters and the byte differences cannot carry.  The tiles where some sample is deeper (collapsed repeats,
+// the byte counters cannot carry.  The tiles where some sample is deeper (collapsed repeats,
 // rDNA, deep populations) run !COUNT, launched over those tiles only: every marked position takes the exact bound.
 // The reads of no sample only enter the pooled counts: not scanned.  No block barrier after the tables: every wave's
 // state is its own.
 constexpr int kKlmThreads = 256;
-// the population layout's padding past a read's last position (k_build_units): stored 0x1F = a reference call of quality
-// 31 relative to any reference code, which KLM's counters and marks ignore (no per-unit mask of the read's end)
-constexpr uint64_t kPopPadUnit = 0x1F1F1F1F1F1F1F1Full;
+// the population layout's padding past a read's last position (k_build_units): zero bytes = a reference call of quality
+// 0 relative to any reference code, which KLM's counters (quality >= kKlmQs) and marks ignore (no per-unit mask of the
+// read's end)
+constexpr uint64_t kPopPadUnit = 0ull;
 constexpr int kKlmWords = kKlmTile / 32 + 2;   // tile bitmap words, a 32-position margin on either side
 constexpr int kKlmUnroll = 4;                  // pass 1: unit loads per batch, the next batch issued before the current
                                                // batch's marks (pipelined 4: 1.368-1.372 ms vs 8 unpipelined 1.393-1.395)
-constexpr int kKlmCntBytes = kKlmTile + 16;    // COUNT, per wave: exception byte counters (byte i + 8: tile position i)
-constexpr int kKlmDifBytes = kKlmTile + 16;    // COUNT, per wave: coverage differences, signed bytes (byte i: position i)
+constexpr int kKlmCntBytes = kKlmTile + 16;    // COUNT, per wave: counted reference calls, byte counters (byte i + 8:
+                                               // tile position i)
+constexpr int kKlmDifBytes = kKlmTile + 16;    // COUNT, per wave: valid calls of another allele, byte counters (the same)
 constexpr int kKlmWaveLds = kKlmCntBytes + kKlmDifBytes;   // the exact bound's slots reuse it after the count
 static_assert(kKlmTile == 2048 && kRunAlign % kKlmTile == 0, "KLM tile: one bitmap word per lane");
 static_assert(kKlmSlots * (32 + 4 + 2) <= kKlmWaveLds, "KLM slots within the wave's counter space");
@@ -1480,19 +1482,23 @@ __device__ __forceinline__ uint32_t nib4_byte7(uint32_t w) {   // bit 7 of the f
 __device__ __forceinline__ uint32_t nib4_of_b7(uint32_t w) {
     return ((__umul24((w >> 7) & 0x010101u, 0x4081u) >> 14) & 7u) | ((w >> 28) & 8u);
 }
-// KLM's exceptions, bit 7 of byte k: not a valid call of the reference's allele (kl_exc), or one of quality < kKlmQs
-__device__ __forceinline__ uint32_t klm_exc(uint32_t y) {
-    const uint32_t ge = ((y & 0x1F1F1F1Fu) | 0x80808080u) - 0x01010101u * (uint32_t)kKlmQs;   // bit 7 kept: q >= Qs
-    return (kl_exc(y) | ~ge) & 0x80808080u;
+// KLM's two flags of a reference-relative dword y, bit 7 of byte k: r, a valid call of the reference's allele of quality
+// >= kKlmQs (y in [kKlmQs, 31]); n, a valid call of another allele (y in [32, 127], kl_nonref).  Six operations: with
+// x = y & 0x7F per byte, x + (128 - Qs) and x + 96 reach bit 7 iff x >= Qs / x >= 32 and never carry out of the byte.
+__device__ __forceinline__ void klm_flags(uint32_t y, uint32_t& r, uint32_t& n) {
+    const uint32_t x = y & 0x7F7F7F7Fu;
+    const uint32_t b = x + 0x60606060u;
+    r = (x + 0x01010101u * (uint32_t)(128 - kKlmQs)) & ~(b | y) & 0x80808080u;
+    n = b & ~y & 0x80808080u;
 }
-// the four signed byte differences packed in w (each |d| < 128: the sum is exact in 32 bits), in order
-__device__ __forceinline__ void unpack_dif(uint32_t w, int32_t d[4]) {
-    int32_t x = (int32_t)w;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        d[k] = (int32_t)(int8_t)(x & 0xFF);
-        x = (x - d[k]) >> 8;
-    }
+// adds a unit's eight flag bytes (bit 7 each, lo = bytes 0-3) as 0 / 1 to the byte counters c from byte o1 + 1 on:
+// three funnel shifts take the >> 7 and the byte alignment at once (the first add is of zero when o1 + 1 is aligned)
+__device__ __forceinline__ void klm_add8(uint32_t* c, int32_t o1, uint32_t lo, uint32_t hi) {
+    uint32_t* p = c + (o1 >> 2);
+    const uint32_t fs = 31u - 8u * (uint32_t)(o1 & 3);
+    atomicAdd(p, __builtin_amdgcn_alignbit(lo, 0u, fs));
+    atomicAdd(p + 1, __builtin_amdgcn_alignbit(hi, lo, fs));
+    atomicAdd(p + 2, __builtin_amdgcn_alignbit(0u, hi, fs));
 }
 
 template <bool COUNT>
@@ -1510,9 +1516,9 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
     if (COUNT && deep_flag && deep_flag[tile]) return;      // (the whole workgroup: no barrier has been reached)
     __shared__ unsigned long long w[2][32];
     __shared__ uint32_t s_call[kKlmTile / 32];         // callable positions of the tile
-    __shared__ uint32_t s_bm[4][kKlmWords];            // marked positions, then those the exact bound takes
-    __shared__ uint32_t s_bm2[4][kKlmWords];           // (COUNT) marked at least twice
-    __shared__ uint16_t s_wb[4][kKlmWords];            // slot of each bitmap word's first slotted position
+    constexpr int kBmWords = COUNT ? 1 : kKlmWords;   // (COUNT keeps its columns in registers)
+    __shared__ uint32_t s_bm[4][kBmWords];             // !COUNT: marked positions, then those the exact bound takes
+    __shared__ uint16_t s_wb[4][kBmWords];             // !COUNT: slot of each bitmap word's first slotted position
     __shared__ alignas(16) uint32_t s_wave[4][kKlmWaveLds / 4];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (threadIdx.x < 64) w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
@@ -1526,93 +1532,96 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
     }
     const int s = (int)(blockIdx.x % nsg) * 4 + wv;
     uint32_t* bm = s_bm[wv];
-    uint32_t* bm2 = s_bm2[wv];
-    uint32_t* cnt32 = s_wave[wv];
-    uint32_t* dif32 = s_wave[wv] + kKlmCntBytes / 4;
+    uint32_t* rc32 = s_wave[wv];                        // COUNT: reference calls of quality >= kKlmQs
+    uint32_t* nc32 = s_wave[wv] + kKlmCntBytes / 4;     // COUNT: valid calls of another allele
     if (s < n_samples) {
-        for (int i = lane; i < kKlmWords; i += 64) { bm[i] = 0u; bm2[i] = 0u; }
         if (COUNT)
             for (int i = lane; i < kKlmWaveLds / 4; i += 64) s_wave[wv][i] = 0u;
+        else
+            for (int i = lane; i < kKlmWords; i += 64) bm[i] = 0u;
     }
     __syncthreads();
     if (s >= n_samples) return;
     const int32_t tstart = (int32_t)(tile * kKlmTile), tlast = tstart + kKlmTile - 1;
     const int st0 = samp_st[s], st1 = samp_st[s + 1];
     uint32_t sink = 0;                                  // (diagnostics)
-    // ---- pass 1: marks (and, COUNT, the exception counters and the coverage differences)
+    // ---- pass 1: COUNT the two counters, !COUNT the marks
     for (int st = st0; st < st1; st++) {
         const int64_t e_lo = blkA[(int64_t)st * nblk + (tstart >> shift)];
         const int64_t e_hi = blkB[(int64_t)st * nblk + (tlast >> shift) + 1];
         // rounds of 64 consecutive entries (lane = entry e0 + lane, whatever its group): every lane busy but in the
-        // last round; the next round's header and group base in flight
+        // last round, where a read's units are split over f = 64 / m lanes (m entries left, m <= 32); the next round's
+        // header and group base in flight
         int2 h = e_lo + lane < e_hi ? rh[e_lo + lane] : make_int2(0, -1);
         int64_t gbase = e_lo + lane < e_hi ? grp[(e_lo + lane) >> 6].base : 0;
         for (int64_t e0 = e_lo; e0 < e_hi; e0 += 64) {
-            const int64_t e = e0 + lane;
+            int64_t e = e0 + lane;
             const bool nx = e + 64 < e_hi;
             const int2 hn = nx ? rh[e + 64] : make_int2(0, -1);
             const int64_t gbn = nx ? grp[(e + 64) >> 6].base : 0;
+            const int32_t m = (int32_t)min(e_hi - e0, (int64_t)64);   // (wave-uniform)
+            int32_t f = 1, part = 0;
+            if (m <= 32) {
+                const int32_t src = lane % m;
+                f = 64 / m;
+                part = lane / m;                                // (>= f: no part, the lane idles)
+                h.x = __shfl(h.x, src, 64);
+                h.y = __shfl(h.y, src, 64);
+                gbase = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uint64_t)gbase >> 32), src, 64) << 32) |
+                                  (uint32_t)__shfl((int)(uint32_t)gbase, src, 64));
+                e = e0 + src;
+            }
             const int32_t gf = h.x, gl = h.y & 0x7FFFFFFF;
             const int32_t a = max(gf, tstart), b = min(gl, tlast);
-            const bool act = e < e_hi && a <= b;
-            const int32_t k0 = act ? (a - gf) >> 3 : 0, kn = act ? ((b - gf) >> 3) - k0 : -1;
+            const bool act = e < e_hi && a <= b && part < f;
+            int32_t k0 = act ? (a - gf) >> 3 : 0, kn = act ? ((b - gf) >> 3) - k0 : -1;
+            if (f > 1 && act) {                                 // part `part` of the read's kn + 1 units
+                const int32_t chunk = (kn + f) / f, ks = part * chunk;
+                if (ks > kn) kn = -1;                           // nothing left for this part (its loads: unit k0)
+                else { k0 += ks; kn = min(kn - ks, chunk - 1); }
+            }
             const uint64_t* ub = units + gbase + (e & 63) + (int64_t)k0 * 64;
             const int32_t ti0 = gf + 8 * k0 - tstart + 32;   // bitmap index of unit k0's byte 0 (>= 25); COUNT: its
                                                               // counter byte is ti0 - 24 (>= 1)
-            // (the read's last unit holds padding past its last position: 0x1F bytes in the population layout -- reference
-            // calls of quality 31, no exception, no mark -- so nothing is masked here; k_build_units)
-            if (COUNT && act && !ABLATE(gp.ablate, 1048576)) {
-                const int32_t i0 = a - tstart, i1 = b - tstart + 1;
-                atomicAdd(&dif32[i0 >> 2], 1u << (8 * (i0 & 3)));
-                atomicAdd(&dif32[i1 >> 2], 0u - (1u << (8 * (i1 & 3))));
-            }
-            // (every batch's loads are issued unconditionally -- the units past a read's end are other reads' rows, or
-            // the buffer's slack past the last group, and are never used: a load under a lane condition made the
-            // compiler wait for every outstanding load, the next batch's included, before the current batch)
-            // (not clamped to the read's last unit as KL's are: the clamp's address arithmetic cost this VALU-bound
-            // kernel 1.5 % -- 0.853-0.863 against 0.840-0.845 ms -- for 10 % less FETCH_SIZE, r05c2)
+            // (the read's last unit holds padding past its last position: zero bytes in the population layout -- reference
+            // calls of quality 0, neither counted nor marked -- so nothing is masked here; k_build_units)
+            // (every batch's loads are issued unconditionally: a load under a lane condition made the compiler wait for
+            // every outstanding load, the next batch's included, before the current batch)
+            // (clamped to the read's last unit, as KL's are: a slot past it reloads that unit's line, a cache hit.  Round
+            // 5's VALU-bound kernel lost 1.5 % to the clamp's address arithmetic; once the counters above cut its VALU
+            // by half, the unclamped loads' lines -- 1.53x the algorithmic bytes -- were what it waited on)
+            const int32_t lim = kn < 0 ? 0 : kn;
             uint64_t u[kKlmUnroll];
 #pragma unroll
-            for (int i = 0; i < kKlmUnroll; i++) u[i] = ub[(int64_t)i * 64];
+            for (int i = 0; i < kKlmUnroll; i++) u[i] = ub[(int64_t)min(i, lim) * 64];
             for (int32_t j = 0; j <= kn; j += kKlmUnroll) {
                 uint64_t v[kKlmUnroll];
-                const uint64_t* nb = ub + (int64_t)(j + kKlmUnroll) * 64;
 #pragma unroll
-                for (int i = 0; i < kKlmUnroll; i++) v[i] = nb[(int64_t)i * 64];
+                for (int i = 0; i < kKlmUnroll; i++) v[i] = ub[(int64_t)min(j + kKlmUnroll + i, lim) * 64];
 #pragma unroll
                 for (int i = 0; i < kKlmUnroll; i++) {
                     if (j + i > kn) continue;
                     const uint32_t ylo = (uint32_t)u[i], yhi = (uint32_t)(u[i] >> 32);
                     if (ABLATE(gp.ablate, 524288)) { sink += ylo ^ yhi; continue; }   // (diagnostics: loads only)
-                    if (COUNT) {
-                        uint64_t ex = (uint64_t)klm_exc(ylo) | (uint64_t)klm_exc(yhi) << 32;
-                        if (ABLATE(gp.ablate, 65536)) { sink += (uint32_t)ex; ex = 0; }   // (diagnostics: no counters)
-                        if (ex) {                                  // (one byte add per exception instead: KLM 0.937
-                                                                   // against 0.825 ms on configs[4], r05kx)
-                            const uint64_t one = ex >> 7;          // a 0 / 1 byte per position
-                            const int32_t ob = ti0 - 24 + 8 * (j + i);
-                            const int sh = 8 * (ob & 3);
-                            const uint64_t lo = one << sh;
-                            uint32_t* c = cnt32 + (ob >> 2);
-                            atomicAdd(c, (uint32_t)lo);
-                            atomicAdd(c + 1, (uint32_t)(lo >> 32));
-                            if (sh) atomicAdd(c + 2, (uint32_t)(one >> (64 - sh)));
-                        }
-                    }
-                    const uint32_t nlo = kl_nonref(ylo), nhi = kl_nonref(yhi);
-                    if (!(nlo | nhi)) continue;
-                    if (ABLATE(gp.ablate, 131072)) { sink += nlo; continue; }     // (diagnostics: no marks)
-                    const uint32_t m = nib4_of_b7(nlo) | nib4_of_b7(nhi) << 4;
-                    const int32_t ti = ti0 + 8 * (j + i);
-                    const uint64_t mv = (uint64_t)m << (ti & 31);
-                    const uint32_t m0 = (uint32_t)mv, m1 = (uint32_t)(mv >> 32);
-                    if (m0) {
-                        const uint32_t old = atomicOr(&bm[ti >> 5], m0);
-                        if (COUNT && (old & m0)) atomicOr(&bm2[ti >> 5], old & m0);
-                    }
-                    if (m1) {
-                        const uint32_t old = atomicOr(&bm[(ti >> 5) + 1], m1);
-                        if (COUNT && (old & m1)) atomicOr(&bm2[(ti >> 5) + 1], old & m1);
+                    if constexpr (COUNT) {
+                        // (round 5 counted exceptions (three adds when a unit had one), the reads' coverage as byte
+                        // differences (two adds per read) and marked the other allele's calls with returning ORs into
+                        // a marked / marked-twice bitmap pair: KLM 0.826-0.847 ms on configs[4])
+                        uint32_t r0, n0, r1, n1;
+                        klm_flags(ylo, r0, n0);
+                        klm_flags(yhi, r1, n1);
+                        const int32_t o1 = ti0 - 25 + 8 * (j + i);   // counter byte of the unit's byte 0, minus 1
+                        klm_add8(rc32, o1, r0, r1);
+                        if (n0 | n1) klm_add8(nc32, o1, n0, n1);
+                    } else {
+                        const uint32_t nlo = kl_nonref(ylo), nhi = kl_nonref(yhi);
+                        if (!(nlo | nhi)) continue;
+                        const uint32_t m = nib4_of_b7(nlo) | nib4_of_b7(nhi) << 4;
+                        const int32_t ti = ti0 + 8 * (j + i);
+                        const uint64_t mv = (uint64_t)m << (ti & 31);
+                        const uint32_t m0 = (uint32_t)mv, m1 = (uint32_t)(mv >> 32);
+                        if (m0) atomicOr(&bm[ti >> 5], m0);
+                        if (m1) atomicOr(&bm[(ti >> 5) + 1], m1);
                     }
                 }
 #pragma unroll
@@ -1625,46 +1634,33 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- candidates: the callable marked positions (lane: bitmap word 1 + lane = positions 32 lane .. 32 lane + 31);
-    //      COUNT drops those the count bound proves hom-ref
-    if (sink == 0xFFFFFFFFu) bm[1 + lane] = sink;      // keeps the diagnostics' work alive
-    uint32_t word = bm[1 + lane] & s_call[lane];
-    if (ABLATE(gp.ablate, 262144)) word = 0u;           // (diagnostics: no exact pass)
-    const uint32_t ncand = (uint32_t)__popc(word);
+    // ---- candidates: the callable positions holding a valid call of another allele (lane: positions 32 lane ..
+    //      32 lane + 31); COUNT drops those the count bound proves hom-ref
     const bool bound_on = gp.use_bound != 0;
-    if (COUNT && bound_on) {
-        int32_t d[4], tot = 0;
+    uint32_t word, ncand;
+    if constexpr (COUNT) {
+        // per dword of four positions, bit 7 of byte k: n >= 1, n >= 2, r >= cb_hi1 (every counter is below 128 and
+        // adding at most 128 to one never carries out of its byte)
+        const int32_t cb = max(tabs->cb_hi1, 0);
+        const uint32_t kc = 0x01010101u * (uint32_t)(cb < 128 ? 128 - cb : 0);   // (cb >= 128: nothing reaches it)
+        uint32_t cand = 0u, drop = 0u;
 #pragma unroll
         for (int q = 0; q < 8; q++) {
-            unpack_dif(dif32[8 * lane + q], d);
-            tot += d[0] + d[1] + d[2] + d[3];
+            const uint32_t rw = rc32[8 * lane + 2 + q], nw = nc32[8 * lane + 2 + q];   // positions 32 lane + 4q ..
+            const uint32_t ge1 = (nw + 0x7F7F7F7Fu) & 0x80808080u;
+            const uint32_t dr = (rw + kc) & ~(nw + 0x7E7E7E7Eu) & ge1;               // one such call, r >= cb
+            cand |= nib4_of_b7(ge1) << (4 * q);
+            drop |= nib4_of_b7(dr) << (4 * q);
         }
-        int32_t incl = tot;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t x = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += x;
-        }
-        if (word) {
-            const uint32_t twice = bm2[1 + lane];
-            const int32_t cb = tabs->cb_hi1;
-            int32_t cov = incl - tot;                    // coverage before the lane's first position
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                unpack_dif(dif32[8 * lane + q], d);
-                const uint32_t cw = cnt32[8 * lane + 2 + q];   // exception bytes of positions 32 lane + 4q ..
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    cov += d[k];
-                    const int bit = 4 * q + k;
-                    if (((word & ~twice) >> bit) & 1u) {
-                        const int32_t hi = cov - (int32_t)((cw >> (8 * k)) & 0xFFu);
-                        if (hi >= cb) word &= ~(1u << bit);
-                    }
-                }
-            }
-        }
+        word = cand & s_call[lane];
+        ncand = (uint32_t)__popc(word);
+        if (bound_on) word &= ~drop;
+    } else {
+        word = bm[1 + lane] & s_call[lane];
+        ncand = (uint32_t)__popc(word);
     }
+    if (sink == 0xFFFFFFFFu) word |= 1u;                // keeps the diagnostics' work alive
+    if (ABLATE(gp.ablate, 262144)) word = 0u;           // (diagnostics: no exact pass)
     if (COUNT) {
         // ---- the exact bound for the count bound's survivors, eight lanes per column: each lane takes every eighth
         //      entry of the sample's streams from the column's block-table entry on, the covering reads' units loaded as
