@@ -1466,9 +1466,9 @@ constexpr uint64_t kPopPadUnit = 0ull;
 constexpr int kKlmWords = kKlmTile / 32 + 2;   // tile bitmap words, a 32-position margin on either side
 constexpr int kKlmUnroll = 4;                  // pass 1: unit loads per batch, the next batch issued before the current
                                                // batch's marks (pipelined 4: 1.368-1.372 ms vs 8 unpipelined 1.393-1.395)
-constexpr int kKlmCntBytes = kKlmTile + 16;    // COUNT, per wave: counted reference calls, byte counters (byte i + 8:
-                                               // tile position i)
-constexpr int kKlmDifBytes = kKlmTile + 16;    // COUNT, per wave: valid calls of another allele, byte counters (the same)
+constexpr int kKlmCntBytes = kKlmTile + 48;    // COUNT, per wave: counted reference calls, byte counters (byte i + 8:
+                                               // tile position i; a batch's adds reach 31 positions past the tile)
+constexpr int kKlmDifBytes = kKlmCntBytes;    // COUNT, per wave: valid calls of another allele, byte counters (the same)
 constexpr int kKlmWaveLds = kKlmCntBytes + kKlmDifBytes;   // the exact bound's slots reuse it after the count
 static_assert(kKlmTile == 2048 && kRunAlign % kKlmTile == 0, "KLM tile: one bitmap word per lane");
 static_assert(kKlmSlots * (32 + 4 + 2) <= kKlmWaveLds, "KLM slots within the wave's counter space");
@@ -1491,11 +1491,10 @@ __device__ __forceinline__ void klm_flags(uint32_t y, uint32_t& r, uint32_t& n) 
     r = (x + 0x01010101u * (uint32_t)(128 - kKlmQs)) & ~(b | y) & 0x80808080u;
     n = b & ~y & 0x80808080u;
 }
-// adds a unit's eight flag bytes (bit 7 each, lo = bytes 0-3) as 0 / 1 to the byte counters c from byte o1 + 1 on:
-// three funnel shifts take the >> 7 and the byte alignment at once (the first add is of zero when o1 + 1 is aligned)
-__device__ __forceinline__ void klm_add8(uint32_t* c, int32_t o1, uint32_t lo, uint32_t hi) {
-    uint32_t* p = c + (o1 >> 2);
-    const uint32_t fs = 31u - 8u * (uint32_t)(o1 & 3);
+// adds a unit's eight flag bytes (bit 7 each, lo = bytes 0-3) as 0 / 1 to the byte counters from byte o1 + 1 on, p =
+// the counters' dword o1 >> 2, fs = 31 - 8 (o1 & 3): three funnel shifts take the >> 7 and the byte alignment at once
+// (the first add is of zero when o1 + 1 is aligned)
+__device__ __forceinline__ void klm_add8(uint32_t* p, uint32_t fs, uint32_t lo, uint32_t hi) {
     atomicAdd(p, __builtin_amdgcn_alignbit(lo, 0u, fs));
     atomicAdd(p + 1, __builtin_amdgcn_alignbit(hi, lo, fs));
     atomicAdd(p + 2, __builtin_amdgcn_alignbit(0u, hi, fs));
@@ -1585,35 +1584,59 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
                                                               // counter byte is ti0 - 24 (>= 1)
             // (the read's last unit holds padding past its last position: zero bytes in the population layout -- reference
             // calls of quality 0, neither counted nor marked -- so nothing is masked here; k_build_units)
+            const int32_t o1 = ti0 - 25;                        // COUNT: counter byte of unit k0's byte 0, minus 1 (>= 0);
+            uint32_t* const rcp = rc32 + (o1 >> 2);             // unit k0 + k's adds start 2 k dwords further
+            uint32_t* const ncp = nc32 + (o1 >> 2);
+            const uint32_t fs = 31u - 8u * (uint32_t)(o1 & 3);
             // (every batch's loads are issued unconditionally: a load under a lane condition made the compiler wait for
             // every outstanding load, the next batch's included, before the current batch)
             // (clamped to the read's last unit, as KL's are: a slot past it reloads that unit's line, a cache hit.  Round
             // 5's VALU-bound kernel lost 1.5 % to the clamp's address arithmetic; once the counters above cut its VALU
             // by half, the unclamped loads' lines -- 1.53x the algorithmic bytes -- were what it waited on)
-            const int32_t lim = kn < 0 ? 0 : kn;
+            // (the clamp on byte offsets, 512 per unit: one min and one add per load)
+            const int32_t limb = (kn < 0 ? 0 : kn) << 9;
+            const char* const ubb = reinterpret_cast<const char*>(ub);
+            auto load = [&](int32_t k) { return *reinterpret_cast<const uint64_t*>(ubb + (uint32_t)min(k << 9, limb)); };
             uint64_t u[kKlmUnroll];
 #pragma unroll
-            for (int i = 0; i < kKlmUnroll; i++) u[i] = ub[(int64_t)min(i, lim) * 64];
+            for (int i = 0; i < kKlmUnroll; i++) u[i] = load(i);
             for (int32_t j = 0; j <= kn; j += kKlmUnroll) {
                 uint64_t v[kKlmUnroll];
 #pragma unroll
-                for (int i = 0; i < kKlmUnroll; i++) v[i] = ub[(int64_t)min(j + kKlmUnroll + i, lim) * 64];
+                for (int i = 0; i < kKlmUnroll; i++) v[i] = load(j + kKlmUnroll + i);
+                if constexpr (COUNT) {
+                    // the batch's reference calls in 2 U + 1 adds (one funnel shift each) instead of 3 per unit: a
+                    // wave's LDS add costs its transfer and its bank conflicts whatever its lanes hold (KLM 0.746 ->
+                    // 0.738 ms); the units past the read's last one (their loads repeat it) add zeros; the other
+                    // allele's calls per unit.  (Round 5 marked those calls with returning ORs into a marked /
+                    // marked-twice bitmap pair and counted exceptions and coverage differences: KLM 0.826-0.847 ms;
+                    // exceptions, other-allele calls and coverage differences in three planes, every add on the lanes
+                    // whose unit has one: bank conflicts 122 -> 51 M cycles, but 6 waves per SIMD and VALU +25 %,
+                    // 0.830 ms, r06o)
+                    uint32_t rf[2 * kKlmUnroll];
 #pragma unroll
-                for (int i = 0; i < kKlmUnroll; i++) {
-                    if (j + i > kn) continue;
-                    const uint32_t ylo = (uint32_t)u[i], yhi = (uint32_t)(u[i] >> 32);
-                    if (ABLATE(gp.ablate, 524288)) { sink += ylo ^ yhi; continue; }   // (diagnostics: loads only)
-                    if constexpr (COUNT) {
-                        // (round 5 counted exceptions (three adds when a unit had one), the reads' coverage as byte
-                        // differences (two adds per read) and marked the other allele's calls with returning ORs into
-                        // a marked / marked-twice bitmap pair: KLM 0.826-0.847 ms on configs[4])
+                    for (int i = 0; i < kKlmUnroll; i++) {
+                        const bool in = j + i <= kn;
+                        const uint32_t ylo = (uint32_t)u[i], yhi = (uint32_t)(u[i] >> 32);
                         uint32_t r0, n0, r1, n1;
                         klm_flags(ylo, r0, n0);
                         klm_flags(yhi, r1, n1);
-                        const int32_t o1 = ti0 - 25 + 8 * (j + i);   // counter byte of the unit's byte 0, minus 1
-                        klm_add8(rc32, o1, r0, r1);
-                        if (n0 | n1) klm_add8(nc32, o1, n0, n1);
-                    } else {
+                        rf[2 * i] = in ? r0 : 0u;
+                        rf[2 * i + 1] = in ? r1 : 0u;
+                        if (in && (n0 | n1)) klm_add8(ncp + 2 * (j + i), fs, n0, n1);
+                    }
+                    uint32_t* const p = rcp + 2 * j;
+                    atomicAdd(p, __builtin_amdgcn_alignbit(rf[0], 0u, fs));
+#pragma unroll
+                    for (int t = 1; t < 2 * kKlmUnroll; t++) atomicAdd(p + t, __builtin_amdgcn_alignbit(rf[t], rf[t - 1], fs));
+                    atomicAdd(p + 2 * kKlmUnroll, __builtin_amdgcn_alignbit(0u, rf[2 * kKlmUnroll - 1], fs));
+                }
+#pragma unroll
+                for (int i = 0; i < kKlmUnroll; i++) {
+                    if (COUNT || j + i > kn) continue;
+                    const uint32_t ylo = (uint32_t)u[i], yhi = (uint32_t)(u[i] >> 32);
+                    if (ABLATE(gp.ablate, 524288)) { sink += ylo ^ yhi; continue; }   // (diagnostics: loads only)
+                    {
                         const uint32_t nlo = kl_nonref(ylo), nhi = kl_nonref(yhi);
                         if (!(nlo | nhi)) continue;
                         const uint32_t m = nib4_of_b7(nlo) | nib4_of_b7(nhi) << 4;
