@@ -1511,7 +1511,21 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
     // deep_flag (COUNT): tiles some sample covers deeper than kKlmCountMaxCov are skipped here -- the !COUNT launch over
     // deep_tiles (its grid: those tiles only) scans them
     const int nsg = (n_samples + 3) >> 2;
-    const int64_t tile = COUNT || !deep_tiles ? (int64_t)blockIdx.x / nsg : (int64_t)deep_tiles[blockIdx.x / nsg];
+    // COUNT: one sample group's consecutive tiles on one XCD at about the same time (the blocks b, b + 8, ... share an
+    // XCD: the bijective remap of cdna_hip_programming.md T1, then sample-group-major order), even tiles streaming their
+    // rounds forward and odd tiles backward -- so the 128-B lines that hold units of both tiles at a tile edge are read
+    // by the two workgroups close together, the second read an L2 hit
+    int64_t tile, sgi;
+    if (COUNT) {
+        const uint32_t N = gridDim.x, bid = blockIdx.x, q = N >> 3, r = N & 7, x = bid & 7;
+        const uint32_t lid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+        const uint32_t ntile = N / (uint32_t)nsg;
+        sgi = lid / ntile;
+        tile = lid - (uint32_t)sgi * ntile;
+    } else {
+        sgi = (int64_t)blockIdx.x % nsg;
+        tile = deep_tiles ? (int64_t)deep_tiles[blockIdx.x / nsg] : (int64_t)blockIdx.x / nsg;
+    }
     if (COUNT && deep_flag && deep_flag[tile]) return;      // (the whole workgroup: no barrier has been reached)
     __shared__ unsigned long long w[2][32];
     __shared__ uint32_t s_call[kKlmTile / 32];         // callable positions of the tile
@@ -1519,7 +1533,7 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
     __shared__ uint32_t s_bm[4][kBmWords];             // !COUNT: marked positions, then those the exact bound takes
     __shared__ uint16_t s_wb[4][kBmWords];             // !COUNT: slot of each bitmap word's first slotted position
     __shared__ alignas(16) uint32_t s_wave[4][kKlmWaveLds / 4];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (wave-uniform: in SGPRs)
     if (threadIdx.x < 64) w[threadIdx.x >> 5][threadIdx.x & 31] = (threadIdx.x < 32 ? tabs->wR : tabs->wX)[threadIdx.x & 31];
     {
         // 8 positions' callable bits per thread (bit 7 of the reference code), four threads per word
@@ -1529,7 +1543,7 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
         v |= __shfl_xor(v, 2, 64);
         if ((threadIdx.x & 3) == 0) s_call[threadIdx.x >> 2] = v;
     }
-    const int s = (int)(blockIdx.x % nsg) * 4 + wv;
+    const int s = (int)sgi * 4 + wv;
     uint32_t* bm = s_bm[wv];
     uint32_t* rc32 = s_wave[wv];                        // COUNT: reference calls of quality >= kKlmQs
     uint32_t* nc32 = s_wave[wv] + kKlmCntBytes / 4;     // COUNT: valid calls of another allele
@@ -1551,13 +1565,19 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
         // rounds of 64 consecutive entries (lane = entry e0 + lane, whatever its group): every lane busy but in the
         // last round, where a read's units are split over f = 64 / m lanes (m entries left, m <= 32); the next round's
         // header and group base in flight
-        int2 h = e_lo + lane < e_hi ? rh[e_lo + lane] : make_int2(0, -1);
-        int64_t gbase = e_lo + lane < e_hi ? grp[(e_lo + lane) >> 6].base : 0;
-        for (int64_t e0 = e_lo; e0 < e_hi; e0 += 64) {
+        // (COUNT, odd tiles: the rounds in reverse, the last one first -- round v0 streams entries phys(v0) ..)
+        const int64_t last0 = e_lo + (((e_hi - e_lo - 1) >> 6) << 6);
+        const bool rev = COUNT && (tile & 1);
+        auto phys = [&](int64_t v) { return rev ? e_lo + last0 - v : v; };
+        int2 h = phys(e_lo) + lane < e_hi && e_lo < e_hi ? rh[phys(e_lo) + lane] : make_int2(0, -1);
+        int64_t gbase = phys(e_lo) + lane < e_hi && e_lo < e_hi ? grp[(phys(e_lo) + lane) >> 6].base : 0;
+        for (int64_t v0 = e_lo; v0 < e_hi; v0 += 64) {
+            const int64_t e0 = phys(v0);
             int64_t e = e0 + lane;
-            const bool nx = e + 64 < e_hi;
-            const int2 hn = nx ? rh[e + 64] : make_int2(0, -1);
-            const int64_t gbn = nx ? grp[(e + 64) >> 6].base : 0;
+            const int64_t en = phys(v0 + 64) + lane;           // the next round's entry
+            const bool nx = v0 + 64 < e_hi && en < e_hi;
+            const int2 hn = nx ? rh[en] : make_int2(0, -1);
+            const int64_t gbn = nx ? grp[en >> 6].base : 0;
             const int32_t m = (int32_t)min(e_hi - e0, (int64_t)64);   // (wave-uniform)
             int32_t f = 1, part = 0;
             if (m <= 32) {

@@ -8,7 +8,8 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 TAG=${1:-r06k}
 SUITE=${2:-all}
-LIBS=${3:-"base new"}   # builds to alternate: base = ngsepcore_amd/lib_base, new = ngsepcore_amd/lib, X = ngsepcore_amd/lib_X
+LIBS=${3:-"base new"}
+PMCLIB=${4:-new}       # the build whose counters are collected   # builds to alternate: base = ngsepcore_amd/lib_base, new = ngsepcore_amd/lib, X = ngsepcore_amd/lib_X
 if [ "$SUITE" = none ]; then
   true
 elif [ "$SUITE" = all ]; then
@@ -37,6 +38,7 @@ PY
   done
 done
 P="python -u bench.py --config multisample --no-cpu-baseline --no-cold --no-e2e --steps 3 --warmup 1"
+if [ $PMCLIB != new ]; then export NGSEP_LIB_PATH=$PWD/ngsepcore_amd/lib_$PMCLIB/libngsep_amd.so; fi
 pass() {   # name counters...
   local name=$1; shift
   timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-trace --kernel-include-regex "k_scan_pop" \
