@@ -964,7 +964,7 @@ template <int T, bool DEEP, int U>
 __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, const int2* __restrict__ rh,
                                           const RGroup* __restrict__ grp, int64_t e_lo, int64_t e_hi, int32_t tstart,
                                           int32_t* s_diff, uint32_t* s_cnt, bool do_diff, int32_t ablate, uint32_t& sink) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (wave-uniform: in SGPRs)
     const int64_t g_lo = e_lo >> 6, g_hi = (e_hi + 63) >> 6;
     const bool no_counts = ABLATE(ablate, 128), no_units = ABLATE(ablate, 256);   // diagnostics
     int64_t g = g_lo + wv;

@@ -9,7 +9,9 @@ mkdir -p gpurun_out
 TAG=${1:-r06k}
 SUITE=${2:-all}
 LIBS=${3:-"base new"}
-PMCLIB=${4:-new}       # the build whose counters are collected   # builds to alternate: base = ngsepcore_amd/lib_base, new = ngsepcore_amd/lib, X = ngsepcore_amd/lib_X
+PMCLIB=${4:-new}       # the build whose counters are collected
+CFG=${5:-multisample}  # the bench configuration (chr20: the default, KL)
+KREGEX=k_scan_pop; [ $CFG = chr20 ] && KREGEX=k_read_scan   # builds to alternate: base = ngsepcore_amd/lib_base, new = ngsepcore_amd/lib, X = ngsepcore_amd/lib_X
 if [ "$SUITE" = none ]; then
   true
 elif [ "$SUITE" = all ]; then
@@ -23,7 +25,7 @@ rc=$?
 [ "$SUITE" = none ] || tail -1 gpurun_out/${TAG}_suite.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then tail -40 gpurun_out/${TAG}_suite.log; exit 1; fi
 grep -E "^FAILED|^ERROR" gpurun_out/${TAG}_suite.log | head
-B="python -u bench.py --config multisample --no-cpu-baseline --no-cold --no-e2e --steps 40 --warmup 3"
+B="python -u bench.py --config $CFG --no-cpu-baseline --no-cold --no-e2e --steps 40 --warmup 3"
 for it in 1 2; do
   for v in $LIBS; do
     if [ $v = new ]; then L=ngsepcore_amd/lib/libngsep_amd.so; else L=ngsepcore_amd/lib_$v/libngsep_amd.so; fi
@@ -37,11 +39,11 @@ print("$v $it", "step %.4f ms" % d["ms_per_step"], "KLM %.4f ms frac %.3f" % (r[
 PY
   done
 done
-P="python -u bench.py --config multisample --no-cpu-baseline --no-cold --no-e2e --steps 3 --warmup 1"
+P="python -u bench.py --config $CFG --no-cpu-baseline --no-cold --no-e2e --steps 3 --warmup 1"
 if [ $PMCLIB != new ]; then export NGSEP_LIB_PATH=$PWD/ngsepcore_amd/lib_$PMCLIB/libngsep_amd.so; fi
 pass() {   # name counters...
   local name=$1; shift
-  timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-trace --kernel-include-regex "k_scan_pop" \
+  timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-trace --kernel-include-regex "$KREGEX" \
       -d gpurun_out/pmc_${TAG}_$name -o run --output-format csv -- $P > gpurun_out/pmc_${TAG}_$name.out 2>&1 || { tail -5 gpurun_out/pmc_${TAG}_$name.out; return 1; }
   python - <<PY
 import csv, glob, collections
