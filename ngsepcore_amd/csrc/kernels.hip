@@ -984,7 +984,10 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
         }
         const int32_t k0 = act ? (a - gf) >> 3 : 0, kn = act && !no_units ? ((b - gf) >> 3) - k0 : -1;   // units k0 .. k0 + kn
         const int32_t ob0 = gf - tstart + 8 * k0 + 8;     // counter index of unit k0's byte 0 (>= 1)
-        const int sh = (ob0 & 1) << 1;                    // !DEEP: byte offset of the unit's first halfword
+        // !DEEP: the unit's first halfword at byte (ob0 & 1) << 1 of its dword; fs: the funnel shift that takes the flags'
+        // >> 7 and that alignment at once; cb: unit k0's first counter dword (unit k0 + k's: 4 k dwords further)
+        const uint32_t fs = 7u + 16u * (uint32_t)(ob0 & 1);
+        uint32_t* const cb = s_cnt + ((ob0 + 1) >> 1) - 1;
         const uint64_t* ub = units + G.base + lane + (int64_t)k0 * 64;
         // a lane's own trip count (the wave runs while any lane has units left); loads are unconditional (a
         // batch's slots past the read's last unit repeat it) so that each unit waits for its own load only
@@ -994,14 +997,17 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
         // batch's included, before the current batch)
         // (clamped to the read's last unit: a slot past it reloads that unit's line, a cache hit -- FETCH_SIZE 2.51 ->
         // 2.25 GB per configs[2] launch, 1.02x the algorithmic bytes, at the same time, r05c2)
-        const int32_t lim = kn < 0 ? 0 : kn;
+        // (the clamp on byte offsets, 512 per unit: one min and one add per load)
+        const int32_t limb = (kn < 0 ? 0 : kn) << 9;
+        const char* const ubb = reinterpret_cast<const char*>(ub);
+        auto load = [&](int32_t k) { return *reinterpret_cast<const uint64_t*>(ubb + (uint32_t)min(k << 9, limb)); };
         uint64_t u[U];
 #pragma unroll
-        for (int i = 0; i < U; i++) u[i] = KL_LOAD(ub[(int64_t)min(i, lim) * 64]);
+        for (int i = 0; i < U; i++) u[i] = KL_LOAD(load(i));
         for (int32_t j = 0; j <= kn; j += U) {
             uint64_t v[U];
 #pragma unroll
-            for (int i = 0; i < U; i++) v[i] = KL_LOAD(ub[(int64_t)min(j + U + i, lim) * 64]);
+            for (int i = 0; i < U; i++) v[i] = KL_LOAD(load(j + U + i));
 #pragma unroll
             for (int i = 0; i < U; i++) {
                 if (j + i > kn) continue;
@@ -1015,26 +1021,26 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
                     // (exception, other-allele) byte pairs of the 8 positions, then shifted to the halfword
                     // (measured and not kept: one halfword add per exception, the wave looping as often as its busiest
                     // lane -- KL 0.460 against 0.399 ms on configs[2], r05ex)
-                    const uint32_t fl = elo >> 7, fh = ehi >> 7, ml = nlo >> 7, mh = nhi >> 7;
-                    const uint32_t w0 = __builtin_amdgcn_perm(ml, fl, 0x05010400u), w1 = __builtin_amdgcn_perm(ml, fl, 0x07030602u);
-                    const uint32_t w2 = __builtin_amdgcn_perm(mh, fh, 0x05010400u), w3 = __builtin_amdgcn_perm(mh, fh, 0x07030602u);
-                    uint32_t* c = s_cnt + ((ob + 1) >> 1) - 1;   // sh = 0: the first add is of 0
+                    // (the flag bytes, bit 7 each, interleaved; the >> 7 rides on the funnel shifts below)
+                    const uint32_t w0 = __builtin_amdgcn_perm(nlo, elo, 0x05010400u), w1 = __builtin_amdgcn_perm(nlo, elo, 0x07030602u);
+                    const uint32_t w2 = __builtin_amdgcn_perm(nhi, ehi, 0x05010400u), w3 = __builtin_amdgcn_perm(nhi, ehi, 0x07030602u);
+                    uint32_t* c = cb + 4 * (j + i);              // (ob even: the first add is of 0)
                     if (ABLATE(ablate, 512)) {                   // diagnostics: stores instead of adds
-                        c[0] = __builtin_amdgcn_alignbyte(w0, 0u, sh);
-                        c[1] = __builtin_amdgcn_alignbyte(w1, w0, sh);
-                        c[2] = __builtin_amdgcn_alignbyte(w2, w1, sh);
-                        c[3] = __builtin_amdgcn_alignbyte(w3, w2, sh);
-                        c[4] = __builtin_amdgcn_alignbyte(0u, w3, sh);
+                        c[0] = __builtin_amdgcn_alignbit(w0, 0u, fs);
+                        c[1] = __builtin_amdgcn_alignbit(w1, w0, fs);
+                        c[2] = __builtin_amdgcn_alignbit(w2, w1, fs);
+                        c[3] = __builtin_amdgcn_alignbit(w3, w2, fs);
+                        c[4] = __builtin_amdgcn_alignbit(0u, w3, fs);
                         continue;
                     }
                     if (ABLATE(ablate, 1024)) { atomicAdd(c, w0 + w1 + w2 + w3); continue; }   // diagnostics: one add
                     if (ABLATE(ablate, 8192) && i != 0) continue;   // diagnostics: a batch's first unit only
                     if (ABLATE(ablate, 16384)) { sink += atomicAdd(c, w0 + w1 + w2 + w3); continue; }   // diagnostics: returning add
-                    atomicAdd(c, __builtin_amdgcn_alignbyte(w0, 0u, sh));
-                    atomicAdd(c + 1, __builtin_amdgcn_alignbyte(w1, w0, sh));
-                    atomicAdd(c + 2, __builtin_amdgcn_alignbyte(w2, w1, sh));
-                    atomicAdd(c + 3, __builtin_amdgcn_alignbyte(w3, w2, sh));
-                    atomicAdd(c + 4, __builtin_amdgcn_alignbyte(0u, w3, sh));
+                    atomicAdd(c, __builtin_amdgcn_alignbit(w0, 0u, fs));
+                    atomicAdd(c + 1, __builtin_amdgcn_alignbit(w1, w0, fs));
+                    atomicAdd(c + 2, __builtin_amdgcn_alignbit(w2, w1, fs));
+                    atomicAdd(c + 3, __builtin_amdgcn_alignbit(w3, w2, fs));
+                    atomicAdd(c + 4, __builtin_amdgcn_alignbit(0u, w3, fs));
                 } else {
                     uint64_t ex = (uint64_t)elo | (uint64_t)ehi << 32;
                     const uint64_t nr = (uint64_t)nlo | (uint64_t)nhi << 32;
