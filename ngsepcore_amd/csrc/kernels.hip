@@ -1012,10 +1012,14 @@ __device__ __forceinline__ void kl_stream(const uint64_t* __restrict__ units, co
             for (int i = 0; i < U; i++) {
                 if (j + i > kn) continue;
                 const uint32_t ylo = (uint32_t)u[i], yhi = (uint32_t)(u[i] >> 32);
-                const uint32_t elo = kl_exc(ylo), ehi = kl_exc(yhi);
+                // the flags from x = y & 0x7F per byte and b = x + 0x60 (bit 7: x >= 32, allele bits 5-6 set): an
+                // exception is y >= 32 (y's bit 7 or b's), another allele's valid call b's bit 7 without y's -- three
+                // operations per dword for the test, one more for the other allele (kl_exc / kl_nonref take seven)
+                const uint32_t blo = (ylo & 0x7F7F7F7Fu) + 0x60606060u, bhi = (yhi & 0x7F7F7F7Fu) + 0x60606060u;
+                const uint32_t elo = (ylo | blo) & 0x80808080u, ehi = (yhi | bhi) & 0x80808080u;
                 if (no_counts) { sink += elo + ehi + kl_nonref(ylo) + kl_nonref(yhi); continue; }
                 if (!(elo | ehi) && !ABLATE(ablate, 2048)) continue;   // (2048, diagnostics: every lane adds)
-                const uint32_t nlo = kl_nonref(ylo), nhi = kl_nonref(yhi);
+                const uint32_t nlo = blo & ~ylo & 0x80808080u, nhi = bhi & ~yhi & 0x80808080u;   // (kl_nonref)
                 const int32_t ob = ob0 + 8 * (j + i);     // counter index of the unit's byte 0
                 if (!DEEP) {
                     // (exception, other-allele) byte pairs of the 8 positions, then shifted to the halfword
