@@ -758,6 +758,7 @@ def main():
                 "sites_called_per_gpu": int(sites_called),
                 "candidates_per_gpu": int(st.candidates),
                 "exact_sites_per_gpu": int(st.hard_sites),
+                "exact_bound_columns_per_gpu": int(st.exact_bound_passes),
                 "pile_bytes_per_gpu": int(pile_bytes),
                 "tile_positions": int(tile),
                 "device_runs_per_gpu": len(sessions),
