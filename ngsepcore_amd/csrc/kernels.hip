@@ -1474,6 +1474,7 @@ constexpr int kKlmThreads = 256;
 // read's end)
 constexpr uint64_t kPopPadUnit = 0ull;
 constexpr int kKlmWords = kKlmTile / 32 + 2;   // tile bitmap words, a 32-position margin on either side
+constexpr uint32_t kKlmDirectN = 4;            // COUNT: columns with this many calls of another allele open unwalked
 constexpr int kKlmUnroll = 4;                  // pass 1: unit loads per batch, the next batch issued before the current
                                                // batch's marks (pipelined 4: 1.368-1.372 ms vs 8 unpipelined 1.393-1.395)
 constexpr int kKlmCntBytes = kKlmTile + 48;    // COUNT, per wave: counted reference calls, byte counters (byte i + 8:
@@ -1690,7 +1691,7 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
     // ---- candidates: the callable positions holding a valid call of another allele (lane: positions 32 lane ..
     //      32 lane + 31); COUNT drops those the count bound proves hom-ref
     const bool bound_on = gp.use_bound != 0;
-    uint32_t word, ncand;
+    uint32_t word, ncand, many = 0u;                    // many (COUNT): kKlmDirectN or more calls of another allele
     if constexpr (COUNT) {
         // per dword of four positions, bit 7 of byte k: n >= 1, n >= 2, r >= cb_hi1 (every counter is below 128 and
         // adding at most 128 to one never carries out of its byte)
@@ -1704,6 +1705,7 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
             const uint32_t dr = (rw + kc) & ~(nw + 0x7E7E7E7Eu) & ge1;               // one such call, r >= cb
             cand |= nib4_of_b7(ge1) << (4 * q);
             drop |= nib4_of_b7(dr) << (4 * q);
+            many |= nib4_of_b7((nw + (0x80u - kKlmDirectN) * 0x01010101u) & 0x80808080u) << (4 * q);
         }
         word = cand & s_call[lane];
         ncand = (uint32_t)__popc(word);
@@ -1721,6 +1723,37 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
         //      eight; a column the bound cannot prove hom-ref (or with more than kMcMaxCalls valid calls) opens its
         //      position and, with pairs, is listed for KPM's first stage.  The gathers' latency hides behind the other
         //      waves' streams (a separate kernel over the same columns: 0.109-0.166 ms after KLM, r05w2 / r05x).
+        const int sh = (int)(blockIdx.x % kKlShards);
+        unsigned long long* sc = counters + kCtrShard0 + kCtrShardStride * sh;
+        // a column with kKlmDirectN or more calls of another allele opens without the walk (at 10x nearly every one is
+        // a carrier the exact bound cannot prove hom-ref: 61 % of the walked columns opened, r06cnt); opening a column
+        // only hands one more (position, sample) pair to KPM's first stage, which genotypes it exactly.  configs[4]:
+        // walked columns 329 K -> 158 K at 4 (queued positions 4860 -> 4864), KLM -0.5 %; at 3: 141 K, but 5918 queued
+        // positions cost KPM's first stage +10 us (r06ae / r06af)
+        const uint32_t direct = bound_on ? word & many : 0u;
+        if (__ballot(direct != 0u)) {
+            word &= ~direct;
+            const uint32_t dc = (uint32_t)__popc(direct);
+            for (uint32_t wd = direct; wd; wd &= wd - 1u) {
+                const int32_t p = tstart + 32 * lane + __builtin_ctz(wd);
+                atomicOr(&need[p >> 5], 1u << (p & 31));
+            }
+            if (pairs) {
+                uint32_t dincl = dc;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t x = __shfl_up(dincl, o, 64);
+                    if (lane >= o) dincl += x;
+                }
+                const uint32_t dtot = (uint32_t)__shfl((int)dincl, 63, 64);
+                unsigned long long base = 0;
+                if (lane == 0) base = atomicAdd(&sc[2], (unsigned long long)dtot);
+                base = __shfl(base, 0, 64);
+                int64_t kp = (int64_t)base + (dincl - dc);
+                for (uint32_t wd = direct; wd; wd &= wd - 1u, kp++)
+                    if (kp < pseg) pairs[(int64_t)sh * pseg + kp] = make_uint2((uint32_t)(tstart + 32 * lane + __builtin_ctz(wd)), (uint32_t)s);
+            }
+        }
         const uint32_t c = (uint32_t)__popc(word);
         uint32_t incl = c;
 #pragma unroll
@@ -1732,8 +1765,6 @@ __global__ __launch_bounds__(kKlmThreads) __attribute__((amdgpu_waves_per_eu(8))
         unsigned long long tcand = ncand;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) tcand += __shfl_xor(tcand, o, 64);
-        const int sh = (int)(blockIdx.x % kKlShards);
-        unsigned long long* sc = counters + kCtrShard0 + kCtrShardStride * sh;
         if (lane == 0) {
             if (tcand) atomicAdd(&sc[0], tcand);
             if (tot) atomicAdd(&sc[1], (unsigned long long)tot);
@@ -4504,6 +4535,15 @@ int device_collect_multi(Device* d, const ngsep_popsite_out** sites, int64_t* n_
     if (c3 >> 63) { err = "internal error: a gathered population column exceeds its coverage bound"; return -1; }
     int64_t cand = 0, bounded = 0;
     pop_scan_counts(hc, &cand, &bounded);
+    static const bool host_timing = env_hook("NGSEP_HOST_TIMING") != nullptr;   // diagnostics
+    static std::atomic<int> told{0};
+    if (host_timing && told.fetch_add(1) < 2) {
+        int64_t pairs = 0;
+        for (int t = 0; t < kKlShards; t++) pairs += (int64_t)hc[kCtrShard0 + kCtrShardStride * t + 2];
+        std::fprintf(stderr, "[ngsep host] population pass: candidate columns %lld, exact-bound columns %lld, opened (pairs) %lld, "
+                     "queued positions %lld, second-stage positions %lld, sites %lld\n", (long long)cand, (long long)bounded,
+                     (long long)pairs, (long long)hc[2], (long long)hc[7], (long long)hc[0]);
+    }
     const int64_t n = (int64_t)hc[0];
     *rerun = (int64_t)hc[2] > m.cap_hard || n > m.cap_psites || (int64_t)hc[5] > m.cap_big;
     *slot = k;

@@ -35,7 +35,7 @@ import json
 d = json.loads(open("gpurun_out/${TAG}_ab_${v}_$it.json").read().strip().splitlines()[-1])
 r = d["roofline"]
 print("$v $it", "step %.4f ms" % d["ms_per_step"], "KLM %.4f ms frac %.3f" % (r["kernel_avg_ms"], r["frac"]), "KPM", r.get("posterior_kernel_avg_ms"),
-      "cand", d["config"].get("candidates_per_gpu"), "exact", d["config"].get("exact_sites_per_gpu"))
+      "cand", d["config"].get("candidates_per_gpu"), "exact", d["config"].get("exact_sites_per_gpu"), "walked", d["config"].get("exact_bound_columns_per_gpu"), "sites", d["config"].get("sites_called_per_gpu"))
 PY
   done
 done
