@@ -1452,12 +1452,14 @@ __global__ __launch_bounds__(256) void k_queue_need(const uint32_t* __restrict__
 // (SingleSampleVariantPileupListener.genotypeVariantSample, :361-391); a position where every sample is so proven
 // gets variant QS 0, which MultisampleVariantsDetector.onPileup never writes (:534).  Per sample tile:
 //   pass 1: the wave streams the sample's units over the tile (its read-group streams in turn; lane = read, as KL).
-//           COUNT: per position two byte counters, the valid reference calls of quality >= kKlmQs and the valid calls of
-//           another allele (SWAR flags, klm_flags; three LDS adds per unit each, no branch: at 64 lanes nearly every
-//           unit holds one).  !COUNT: the positions holding a valid call of another allele marked in an LDS bitmap;
+//           COUNT: per position two byte counters, the valid reference calls of quality >= kKlmQs (a batch of units in
+//           2 U + 1 LDS adds, every lane) and the valid calls of another allele (three adds per unit on the lanes whose
+//           unit has one; SWAR flags, klm_flags).  !COUNT: the positions holding a valid call of another allele marked
+//           in an LDS bitmap;
 //   count:  COUNT, a callable position with one call of another allele is a candidate the count bound may drop: its
 //           counted reference calls reaching cb_hi1 make it hom-ref for this sample (about 97 % of the candidate
-//           columns at 10x); positions with two or more stay;
+//           columns at 10x); positions with two or three stay for the exact bound, with four or more open as they are;
+//           COUNT's exact bound is an in-wave walk (below); !COUNT:
 //   slots:  the positions still marked get LDS slots in position order;
 //   pass 2: every lane adds the weights of its read's valid calls at the slotted positions it covers (one 8-byte
 //           reload each) into its slot's {ref, alt 1, alt 2, alt 3} sums -- the exact integer bound;
