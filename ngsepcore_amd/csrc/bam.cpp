@@ -1935,7 +1935,8 @@ int multi_run(ngsep_ctx* const* ctxs, int32_t n_ctx, const char* const* bams, in
             if (ctxs[u] == c) return set_error(c0, NGSEP_E_INVALID, "a context is listed twice (one host thread drives each)");
         ngsep_params a = c0->params, b = c->params;
         if (std::memcmp(&a, &b, sizeof a) != 0) return set_error(c0, NGSEP_E_INVALID, "the contexts' parameters differ");
-        if (c->seq_names.empty()) {                    // the first context's reference and input variants
+        if (c->seq_names.empty()) {                    // the first context's reference and input variants (a copy per
+                                                       // context: N devices hold N references on the host)
             c->seq_names = c0->seq_names;
             c->seq_bases = c0->seq_bases;
             c->known = c0->known;
