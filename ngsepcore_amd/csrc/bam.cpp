@@ -1453,7 +1453,7 @@ int merge_whole_files(ngsep_ctx* c, std::vector<Cursor>& cur, int n_files) {
     });
     // per range: the merged order (file, record) and its CIGAR / base totals
     std::vector<std::vector<std::pair<int32_t, int32_t>>> order((size_t)np);
-    std::vector<int64_t> n_rec((size_t)np + 1, 0), n_cig((size_t)np + 1, 0), n_base((size_t)np + 1, 0);
+    std::vector<int64_t> n_rec((size_t)np + 1, 0), n_cig((size_t)np + 1, 0);
     ngsep::parallel_for(np, 1, [&](int64_t lo, int64_t hi) {
         struct Head { Key k; int32_t file; int64_t i; };
         std::vector<Head> heap;
@@ -1485,13 +1485,12 @@ int merge_whole_files(ngsep_ctx* c, std::vector<Cursor>& cur, int n_files) {
             for (size_t i = heap.size() / 2; i-- > 0;) sift_down(i);
             auto& ord = order[(size_t)p];
             ord.reserve((size_t)tot);
-            int64_t nc = 0, nb = 0;
+            int64_t nc = 0;
             while (!heap.empty()) {
                 const int32_t f = heap[0].file;
                 const int64_t i = heap[0].i;
                 ord.emplace_back(f, (int32_t)i);
                 nc += cur[(size_t)f].batch.cigar_n[i];
-                nb += cur[(size_t)f].batch.seq_len[i];
                 if (i + 1 < cut[(size_t)f][(size_t)p + 1]) {
                     heap[0].i = i + 1;
                     heap[0].k = keys[(size_t)f][(size_t)i + 1];
@@ -1503,31 +1502,28 @@ int merge_whole_files(ngsep_ctx* c, std::vector<Cursor>& cur, int n_files) {
             }
             n_rec[(size_t)p + 1] = (int64_t)ord.size();
             n_cig[(size_t)p + 1] = nc;
-            n_base[(size_t)p + 1] = nb;
         }
     });
     lap("ordered ranges");
     for (int64_t p = 0; p < np; p++) {
         n_rec[(size_t)p + 1] += n_rec[(size_t)p];
         n_cig[(size_t)p + 1] += n_cig[(size_t)p];
-        n_base[(size_t)p + 1] += n_base[(size_t)p];
     }
     const int64_t N = n_rec[(size_t)np];
-    // (uninitialised storage: the pages are first touched by the parallel gather)
+    // (uninitialised storage: the pages are first touched by the parallel gather).  The reads' bases and qualities
+    // stay in their files' batches (two bytes per read base: copying them here, ~6 GB for configs[4], and releasing
+    // the copy cost ~0.4 s); the merged batches point at them.
     RawBuf<int32_t> m_seq, m_first, m_flags, m_rg, m_cig_n, m_seqlen, m_cigar;
-    RawBuf<int64_t> m_cig_off, m_seq_off;
-    RawBuf<uint8_t> m_hasq;
-    RawBuf<char> m_bases, m_quals;
+    RawBuf<int64_t> m_cig_off;
+    RawBuf<const char*> m_chars, m_qp;
     for (auto* v : {&m_seq, &m_first, &m_flags, &m_rg, &m_cig_n, &m_seqlen}) v->resize((size_t)N);
     m_cigar.resize((size_t)std::max<int64_t>(1, n_cig[(size_t)np]));
     m_cig_off.resize((size_t)N);
-    m_seq_off.resize((size_t)N);
-    m_hasq.resize((size_t)N);
-    m_bases.resize((size_t)std::max<int64_t>(1, n_base[(size_t)np]));
-    m_quals.resize((size_t)std::max<int64_t>(1, n_base[(size_t)np]));
+    m_chars.resize((size_t)N);
+    m_qp.resize((size_t)N);
     ngsep::parallel_for(np, 1, [&](int64_t lo, int64_t hi) {
         for (int64_t p = lo; p < hi; p++) {
-            int64_t r = n_rec[(size_t)p], co = n_cig[(size_t)p], so = n_base[(size_t)p];
+            int64_t r = n_rec[(size_t)p], co = n_cig[(size_t)p];
             for (const auto& fi : order[(size_t)p]) {
                 const Cursor& k = cur[(size_t)fi.first];
                 const int64_t i = fi.second;
@@ -1541,13 +1537,10 @@ int merge_whole_files(ngsep_ctx* c, std::vector<Cursor>& cur, int n_files) {
                 m_cig_n[(size_t)r] = cn;
                 std::memcpy(&m_cigar[(size_t)co], k.batch.cigar + k.batch.cigar_off[i], (size_t)cn * sizeof(int32_t));
                 co += cn;
-                const int32_t sl = k.batch.seq_len[i];
-                m_seq_off[(size_t)r] = so;
-                m_seqlen[(size_t)r] = sl;
-                std::memcpy(&m_bases[(size_t)so], k.batch.bases + k.batch.seq_off[i], (size_t)sl);
-                std::memcpy(&m_quals[(size_t)so], k.batch.quals + k.batch.seq_off[i], (size_t)sl);
-                so += sl;
-                m_hasq[(size_t)r] = k.batch.has_quals ? k.batch.has_quals[i] : 1;
+                m_seqlen[(size_t)r] = k.batch.seq_len[i];
+                m_chars[(size_t)r] = k.batch.bases + k.batch.seq_off[i];
+                const bool hq = k.batch.quals && (!k.batch.has_quals || k.batch.has_quals[i]);
+                m_qp[(size_t)r] = hq ? k.batch.quals + k.batch.seq_off[i] : nullptr;
                 r++;
             }
         }
@@ -1561,9 +1554,8 @@ int merge_whole_files(ngsep_ctx* c, std::vector<Cursor>& cur, int n_files) {
         mb.n_reads = std::min(kBatch, N - s0);
         mb.seq_id = m_seq.data() + s0; mb.first = m_first.data() + s0; mb.flags = m_flags.data() + s0;
         mb.read_group = m_rg.data() + s0; mb.cigar_off = m_cig_off.data() + s0; mb.cigar_n = m_cig_n.data() + s0;
-        mb.cigar = m_cigar.data(); mb.seq_off = m_seq_off.data() + s0; mb.seq_len = m_seqlen.data() + s0;
-        mb.bases = m_bases.data(); mb.quals = m_quals.data(); mb.has_quals = m_hasq.data() + s0;
-        const int r = ngsep_process_alignments(c, &mb);
+        mb.cigar = m_cigar.data(); mb.seq_len = m_seqlen.data() + s0;
+        const int r = ngsep::process_alignments_gathered(c, &mb, m_chars.data() + s0, m_qp.data() + s0);
         if (r != NGSEP_OK) return r;
     }
     lap("sweep of the merged batches");

@@ -489,7 +489,10 @@ static inline ReadView batch_view(const BatchRef& br, int32_t i) {
     r.len = sl > 0 ? sl : 0;
     r.chars = nullptr;
     r.quals = nullptr;
-    if (sl > 0) {
+    if (sl > 0 && br.chars_at) {
+        r.chars = br.chars_at[i];
+        r.quals = br.quals_at[i];
+    } else if (sl > 0) {
         r.chars = b->bases + b->seq_off[i];
         if (b->quals && (!b->has_quals || b->has_quals[i])) r.quals = b->quals + (br.qual_off ? br.qual_off[i] : b->seq_off[i]);
     }
@@ -1316,7 +1319,8 @@ static void admit_middle(ngsep_ctx* c, int64_t from, int64_t to) {
     c->stats.alignments_admitted += total;
 }
 
-static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed, const int64_t* qual_off = nullptr) {
+static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed, const int64_t* qual_off = nullptr,
+                         const char* const* chars_at = nullptr, const char* const* quals_at = nullptr) {
     if (!b || b->n_reads < 0) return set_error(c, NGSEP_E_INVALID, "null batch");
     const int nseq = (int)c->seq_names.size();
     int rc = NGSEP_OK;
@@ -1357,7 +1361,7 @@ static int process_batch(ngsep_ctx* c, const ngsep_read_batch* b, bool packed, c
             rlenp[i] = read_length;
         }
     });
-    c->cur_batch = BatchRef{b, lastp, indelp, packed, qual_off};
+    c->cur_batch = BatchRef{b, lastp, indelp, packed, qual_off, chars_at, quals_at};
     int64_t n_in = 0;
     // the admission sweep (processAlignment + processSameStartAlns) over reads [from, to); false: stop the batch
     auto sweep = [&](int64_t from, int64_t to) -> bool {
@@ -3390,6 +3394,11 @@ int process_alignments_packed(ngsep_ctx* c, const PackedBatch* b) {
     if (!c || !b) return NGSEP_E_INVALID;
     c->staging_mode = false;
     return process_batch(c, &b->b, true, b->qual_off);
+}
+int process_alignments_gathered(ngsep_ctx* c, const ngsep_read_batch* b, const char* const* chars_at, const char* const* quals_at) {
+    if (!c || !b || !chars_at || !quals_at) return NGSEP_E_INVALID;
+    c->staging_mode = false;
+    return process_batch(c, b, false, nullptr, chars_at, quals_at);
 }
 }  // namespace ngsep
 

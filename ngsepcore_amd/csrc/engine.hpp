@@ -260,6 +260,8 @@ struct BatchRef {
     const int32_t* indel = nullptr;
     bool packed = false;
     const int64_t* qual_off = nullptr;  // packed batches: the qualities' offsets (else seq_off)
+    const char* const* chars_at = nullptr;   // merged batches: each read's bases and qualities where they lie (else
+    const char* const* quals_at = nullptr;   // bases / quals + seq_off); a null quals_at[i]: no qualities
 };
 // bam.cpp's BAM-encoded batches (ReadView::packed): bases and qualities read in place in the reader's decoded chunk
 // (bases = quals = its start, a record's 4-bit bases at seq_off[i], its qualities at qual_off[i]), valid until the
@@ -836,6 +838,9 @@ namespace ngsep {
 int set_error(ngsep_ctx* c, int code, const std::string& msg);
 // ngsep_process_alignments for a batch in BAM encoding (ReadView::packed; bam.cpp's call_bam)
 int process_alignments_packed(ngsep_ctx* c, const PackedBatch* b);
+// ngsep_process_alignments for a batch whose reads' bytes stay in their own files' batches (bam.cpp's population
+// merge): read i's bases at chars_at[i], its qualities at quals_at[i] (b->bases / quals / seq_off unused)
+int process_alignments_gathered(ngsep_ctx* c, const ngsep_read_batch* b, const char* const* chars_at, const char* const* quals_at);
 void project_read(const ngsep_ctx* c, const ReadView& r, uint8_t* out);
 int stage_contig_reads(ngsep_ctx* c, ContigReads& cr, bool run_now);
 int build_and_upload(ngsep_ctx* c, std::vector<ContigReads>& contigs, bool release_chunks);
